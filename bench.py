@@ -1,0 +1,140 @@
+#!/usr/bin/env python
+"""Headline benchmark: GPT-3 1.3B hybrid-parallel pre-training throughput (tokens/s, whole job).
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 launched by
+``torch.distributed.run`` (one rank per GPU, RCCL). W untimed steps, then EXACTLY K timed steps
+bracketed by barrier + device synchronize; the max elapsed over ranks is reported by rank 0 as one
+JSON line. Synthetic token ids and random-init weights of the real GPT-3 1.3B architecture
+(24 layers, hidden 2048, 16 heads, FFN 8192, vocab 50304, seq 1024); bf16 compute with fp32
+master weights + AdamW states; every timed step is a full forward + backward + gradient
+collectives + optimizer update.
+
+Parallelism: ``--tp`` model-parallel degree (default 1), the rest data-parallel with ZeRO-1
+sharded optimizer states (``--sharding 1``; 0 = plain all-reduce DP). Weak scaling: the
+per-GPU micro batch is fixed as N grows.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+METRIC = "tokens/sec (node) GPT-3 1.3B Fleet hybrid-parallel at 1/2/4/8 MI355X"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", default="gpt3-1.3b")
+    ap.add_argument("--seq", type=int, default=1024)
+    ap.add_argument("--micro-batch", type=int, default=8, help="sequences per data-parallel rank")
+    ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--sharding", type=int, default=1)
+    ap.add_argument("--bucket-mb", type=int, default=256)
+    ap.add_argument("--dropout", type=float, default=0.1)
+    ap.add_argument("--recompute", action="store_true")
+    ap.add_argument("--profile-steps", type=int, default=0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=device)
+
+    import paddle_infer_amd as pia
+    from paddle_infer_amd.models.gpt import GPTForPretraining, gpt_config, gpt_flops_per_token
+    from paddle_infer_amd.parallel.flat_engine import FlatTrainer
+    from paddle_infer_amd.distributed.fleet.topology import local_topology, HybridCommunicateGroup
+    from paddle_infer_amd.framework import random as prand
+
+    tp = args.tp
+    assert world % tp == 0
+    dp = world // tp
+    hcg = HybridCommunicateGroup(local_topology(dp=dp, mp=tp))
+    mp_group = hcg.get_model_parallel_group()
+    dp_group = hcg.get_data_parallel_group()
+    prand.model_parallel_random_seed(1234, hcg.get_model_parallel_rank(), 0)
+
+    cfg = gpt_config(args.model, max_position_embeddings=max(args.seq, 1024),
+                     hidden_dropout_prob=args.dropout, recompute=args.recompute)
+    with torch.device(device):
+        model = GPTForPretraining(cfg, mp_group=mp_group)
+    model.train()
+    trainer = FlatTrainer(model, lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1,
+                          grad_clip=1.0, dp_group=dp_group, mp_group=mp_group,
+                          sharding_stage=args.sharding, bucket_mb=args.bucket_mb)
+    n_params = trainer.num_params()
+
+    mb, S = args.micro_batch, args.seq
+    gen = torch.Generator(device=device)
+    gen.manual_seed(1000 + hcg.get_data_parallel_rank())
+    ids = torch.randint(0, cfg.vocab_size, (mb, S + 1), device=device, generator=gen)
+    x, y = ids[:, :-1].contiguous(), ids[:, 1:].contiguous()
+
+    def step():
+        trainer.zero_grad()
+        loss = model(x, labels=y)
+        loss.backward()
+        trainer.step()
+        return loss
+
+    for _ in range(args.warmup):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    trainer.wait_params()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    final_loss = float(loss.item())
+
+    tokens = args.steps * dp * mb * S
+    tps = tokens / elapsed
+    ms = elapsed / args.steps * 1e3
+    flops_tok = gpt_flops_per_token(cfg, S)
+    tflops_gpu = tps * flops_tok / world / 1e12
+    par = (f"tp{tp}" if tp > 1 else "") + f"dp{dp}" + (f"_sharding{args.sharding}" if dp > 1 and args.sharding else "")
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": round(tps, 1), "unit": "tokens/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 2),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (random token ids, random-init weights)",
+            "config": {"model": "GPT-3 1.3B" if args.model == "gpt3-1.3b" else args.model,
+                       "global_batch": dp * mb, "seq_len": S, "parallelism": par,
+                       "micro_batch_per_dp_rank": mb, "params": n_params,
+                       "hidden_dropout": args.dropout, "attention_dropout": 0.0,
+                       "optimizer": "AdamW fp32 master", "grad_clip": 1.0},
+            "tflops_per_gpu": round(tflops_gpu, 1), "final_loss": round(final_loss, 4),
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1),
+        }), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

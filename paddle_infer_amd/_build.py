@@ -1,0 +1,86 @@
+"""In-tree build of the native libraries.
+
+* ``_lib/libpiamd_kernels.so`` — every ``csrc/kernels/*.hip`` compiled for gfx950 with hipcc
+  (C ABI, loaded with ctypes AFTER torch so it binds to the HIP runtime torch already loaded).
+* ``_lib/libpiamd_runtime.so`` — the C++ host runtime (``csrc/runtime/*.cc``: static-graph
+  executor scheduler, data-loader ring, memory-plan) built with g++.
+
+Incremental: an object is rebuilt only when its source (or a header in the same dir) is newer.
+Run ``python -m paddle_infer_amd._build`` or ``__graft_entry__.build()``.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+KDIR = os.path.join(ROOT, "csrc", "kernels")
+RDIR = os.path.join(ROOT, "csrc", "runtime")
+LIBDIR = os.path.join(ROOT, "_lib")
+OBJDIR = os.path.join(ROOT, "_lib", "obj")
+KERNEL_LIB = os.path.join(LIBDIR, "libpiamd_kernels.so")
+RUNTIME_LIB = os.path.join(LIBDIR, "libpiamd_runtime.so")
+ARCH = os.environ.get("PIAMD_ARCH", "gfx950")
+HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+
+HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+             "-ffp-contract=fast", "-Wno-unused-result"]
+CXX_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-pthread"]
+
+
+def _newest_header(d: str) -> float:
+    hs = glob.glob(os.path.join(d, "*.h"))
+    return max((os.path.getmtime(h) for h in hs), default=0.0)
+
+
+def _compile(cmd: list, src: str) -> str:
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {src}\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return src
+
+
+def _build_lib(srcs, out, compiler, flags, link_flags, hdr_time, verbose, jobs) -> bool:
+    os.makedirs(OBJDIR, exist_ok=True)
+    todo = []
+    objs = []
+    for s in srcs:
+        o = os.path.join(OBJDIR, os.path.basename(s) + ".o")
+        objs.append(o)
+        if not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(s), hdr_time):
+            todo.append((s, o))
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+            futs = [ex.submit(_compile, [compiler, *flags, "-c", s, "-o", o], s) for s, o in todo]
+            for f in cf.as_completed(futs):
+                if verbose:
+                    print(f"[piamd build] compiled {os.path.basename(f.result())}", flush=True)
+    need_link = todo or not os.path.exists(out) or any(
+        os.path.getmtime(o) > os.path.getmtime(out) for o in objs)
+    if need_link:
+        tmp = out + ".tmp"
+        _compile([compiler, "-shared", *objs, "-o", tmp, *link_flags], out)
+        os.replace(tmp, out)
+        if verbose:
+            print(f"[piamd build] linked {out}", flush=True)
+    return bool(need_link)
+
+
+def build(verbose: bool = True, jobs: int | None = None) -> None:
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    ksrcs = sorted(glob.glob(os.path.join(KDIR, "*.hip")))
+    if ksrcs:
+        _build_lib(ksrcs, KERNEL_LIB, HIPCC, HIP_FLAGS, [f"--offload-arch={ARCH}"],
+                   _newest_header(KDIR), verbose, jobs)
+    rsrcs = sorted(glob.glob(os.path.join(RDIR, "*.cc")))
+    if rsrcs:
+        _build_lib(rsrcs, RUNTIME_LIB, "g++", CXX_FLAGS, ["-pthread"], _newest_header(RDIR),
+                   verbose, jobs)
+
+
+if __name__ == "__main__":
+    build(verbose=True, jobs=int(sys.argv[1]) if len(sys.argv) > 1 else None)

@@ -1,0 +1,109 @@
+// Shared device helpers for the paddle_infer_amd CDNA4 (gfx950) kernel library.
+//
+// Conventions (all kernels):
+//   * wave64: every reduction / shuffle idiom is written for 64 lanes.
+//   * bf16 is carried as raw `unsigned short` bits in memory and widened to f32 in registers;
+//     narrowing uses the hardware `v_cvt_pk_bf16_f32` (plain `__bf16` cast at -O3), which keeps NaN.
+//   * global loads are 16 B/lane (`u16x8`) wherever the row length allows (guide G13).
+//   * every exported launcher is `extern "C" int piamd_<name>(..., hipStream_t)` returning the
+//     hipError_t of the launch, so the Python side can raise loudly.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PIAMD_EXPORT extern "C" __attribute__((visibility("default")))
+
+typedef unsigned short bf16_t;
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float bf2f(bf16_t v) {
+  return __uint_as_float(((unsigned)v) << 16);
+}
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, b);
+}
+// pack two floats into one dword of 2 x bf16 (lo in bits 0..15)
+__device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
+  return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x == 64 * NW; `red` must hold NW floats.
+template <int NW>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) t += red[i];
+  __syncthreads();
+  return t;
+}
+template <int NW>
+__device__ __forceinline__ float block_max(float v, float* red) {
+  v = wave_max(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float t = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) t = fmaxf(t, red[i]);
+  __syncthreads();
+  return t;
+}
+
+// Counter-based RNG (Philox-free, stateless): a 64-bit mix of (seed, offset, index) → uniform
+// [0,1). Stateless so backward regenerates the dropout mask instead of storing it.
+__device__ __forceinline__ float hash_uniform(uint64_t seed, uint64_t offset, uint64_t idx) {
+  uint64_t z = seed * 0x9E3779B97F4A7C15ull + (offset + idx) * 0xBF58476D1CE4E5B9ull;
+  z ^= z >> 31; z *= 0x94D049BB133111EBull; z ^= z >> 29; z *= 0xBF58476D1CE4E5B9ull; z ^= z >> 32;
+  return (float)(uint32_t)(z >> 8 & 0xFFFFFF) * (1.0f / 16777216.0f);
+}
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float u = k0 * (x + k1 * x * x * x);
+  return 0.5f * x * (1.f + tanhf(u));
+}
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float x2 = x * x;
+  float u = k0 * (x + k1 * x2 * x);
+  float t = tanhf(u);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+}
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.f + erff(x * 0.7071067811865476f));
+}
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  return 0.5f * (1.f + erff(x * 0.7071067811865476f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+}
+
+// Grid size for grid-stride memory-bound kernels (guide G11): ≤ 256 CUs × 8 blocks.
+static inline int stride_grid(long long work_items, int block) {
+  long long g = (work_items + block - 1) / block;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (int)g;
+}

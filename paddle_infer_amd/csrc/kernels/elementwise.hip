@@ -1,0 +1,313 @@
+// Fused elementwise kernels: bias+activation (fwd/bwd with fused bias-grad column sums),
+// dropout, masked softmax.
+//
+// Parity: reference `paddle/fluid/operators/fused/fused_dropout_act_bias.h`
+// (fused_bias_act / FusedFeedForward's `dropout(act(x + bias))`), `phi/kernels/gpu/gelu_*`,
+// `phi/kernels/fusion/gpu/fused_softmax_mask_kernel.cu` (softmax(x + mask)) and
+// `fused_softmax_mask_upper_triangle`.
+//
+// MI355X design: 16 B/lane vectors everywhere (G13); the activation backward is 2-D (row groups ×
+// 2048-column stripes) so each thread also accumulates the bias gradient for its 8 columns in
+// registers and writes one f32 partial row per block — the dbias reduction costs no extra pass
+// over the [tokens × 4h] activation.
+#include "common.h"
+
+namespace {
+
+enum Act { ACT_NONE = 0, ACT_GELU_TANH = 1, ACT_GELU_ERF = 2, ACT_RELU = 3, ACT_SILU = 4 };
+
+template <int ACT>
+__device__ __forceinline__ float act_f(float x) {
+  if (ACT == ACT_GELU_TANH) return gelu_tanh(x);
+  if (ACT == ACT_GELU_ERF) return gelu_erf(x);
+  if (ACT == ACT_RELU) return x > 0.f ? x : 0.f;
+  if (ACT == ACT_SILU) return x / (1.f + __expf(-x));
+  return x;
+}
+template <int ACT>
+__device__ __forceinline__ float act_g(float x) {
+  if (ACT == ACT_GELU_TANH) return gelu_tanh_grad(x);
+  if (ACT == ACT_GELU_ERF) return gelu_erf_grad(x);
+  if (ACT == ACT_RELU) return x > 0.f ? 1.f : 0.f;
+  if (ACT == ACT_SILU) { float s = 1.f / (1.f + __expf(-x)); return s * (1.f + x * (1.f - s)); }
+  return 1.f;
+}
+
+// y = act(x + bias) (bias optional, broadcast over rows of length N); bf16; N % 8 == 0.
+template <int ACT>
+__global__ __launch_bounds__(256) void bias_act_fwd_kernel(const bf16_t* __restrict__ x,
+                                                          const bf16_t* __restrict__ bias,
+                                                          bf16_t* __restrict__ y,
+                                                          bf16_t* __restrict__ pre, long long n8,
+                                                          int N) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const int nb8 = N >> 3;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    u16x8 r = reinterpret_cast<const u16x8*>(x)[i], o, pr;
+    u16x8 b;
+    if (bias) b = reinterpret_cast<const u16x8*>(bias)[i % nb8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = bf2f(r[j]);
+      if (bias) v += bf2f(b[j]);
+      pr[j] = f2bf(v);
+      o[j] = f2bf(act_f<ACT>(v));
+    }
+    if (pre) reinterpret_cast<u16x8*>(pre)[i] = pr;
+    reinterpret_cast<u16x8*>(y)[i] = o;
+  }
+}
+
+// dx = dy * act'(h) with h = pre-activation (x + bias); dbias partials. grid = (G, ceil(N/2048)).
+template <int ACT>
+__global__ __launch_bounds__(256) void bias_act_bwd_kernel(const bf16_t* __restrict__ dy,
+                                                          const bf16_t* __restrict__ h,
+                                                          const bf16_t* __restrict__ bias,
+                                                          bf16_t* __restrict__ dx,
+                                                          float* __restrict__ part, int rows,
+                                                          int N) {
+  const int c8 = blockIdx.y * 256 + threadIdx.x;  // 8-column group index
+  if (c8 * 8 >= N) return;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  u16x8 b;
+  if (bias) b = reinterpret_cast<const u16x8*>(bias)[c8];
+  for (int r = blockIdx.x; r < rows; r += gridDim.x) {
+    const size_t idx = ((size_t)r * N >> 3) + c8;
+    u16x8 d = reinterpret_cast<const u16x8*>(dy)[idx];
+    u16x8 hv = reinterpret_cast<const u16x8*>(h)[idx];
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float hh = bf2f(hv[j]);
+      if (bias) hh += bf2f(b[j]);
+      float g = bf2f(d[j]) * act_g<ACT>(hh);
+      o[j] = f2bf(g);
+      acc[j] += g;
+    }
+    reinterpret_cast<u16x8*>(dx)[idx] = o;
+  }
+  if (part) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) part[(size_t)blockIdx.x * N + c8 * 8 + j] = acc[j];
+  }
+}
+
+__global__ __launch_bounds__(256) void colsum_bf16_kernel(const float* __restrict__ part, int G,
+                                                         int N, bf16_t* __restrict__ out) {
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + cl;
+  float s = 0.f;
+  if (col < N)
+    for (int g = rg; g < G; g += 4) s += part[(size_t)g * N + col];
+  __shared__ float red[4][64];
+  red[rg][cl] = s;
+  __syncthreads();
+  if (rg == 0 && col < N) out[col] = f2bf(red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl]);
+}
+
+// Row softmax with optional additive mask (broadcast over rows: mask row index = row % mask_rows)
+// and optional causal (upper-triangle) masking with query position = row % causal_q. One wave
+// per row for N <= 4096 (row in registers), bf16 in/out.
+template <int NV>
+__global__ __launch_bounds__(256) void softmax_fwd_kernel(const bf16_t* __restrict__ x,
+                                                         const bf16_t* __restrict__ mask,
+                                                         int mask_rows, int causal_q,
+                                                         bf16_t* __restrict__ y, int rows, int N,
+                                                         float scale) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nvec = N >> 3;
+  const size_t base = (size_t)row * N;
+  const int qpos = causal_q > 0 ? (row % causal_q) + (N - causal_q) : N;
+  float v[NV][8];
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int vi = i * 64 + lane;
+    if (vi < nvec) {
+      u16x8 r = reinterpret_cast<const u16x8*>(x + base)[vi];
+      u16x8 mk;
+      if (mask) mk = reinterpret_cast<const u16x8*>(mask + (size_t)(row % mask_rows) * N)[vi];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float t = bf2f(r[j]) * scale;
+        if (mask) t += bf2f(mk[j]);
+        if (vi * 8 + j > qpos) t = -INFINITY;
+        v[i][j] = t;
+        m = fmaxf(m, t);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = -INFINITY;
+    }
+  }
+  m = wave_max(m);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float e = v[i][j] == -INFINITY ? 0.f : __expf(v[i][j] - m);
+      v[i][j] = e;
+      s += e;
+    }
+  s = wave_sum(s);
+  const float inv = s > 0.f ? 1.f / s : 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int vi = i * 64 + lane;
+    if (vi < nvec) {
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(v[i][j] * inv);
+      reinterpret_cast<u16x8*>(y + base)[vi] = o;
+    }
+  }
+}
+
+// dx = scale * y * (dy - sum(dy * y))
+template <int NV>
+__global__ __launch_bounds__(256) void softmax_bwd_kernel(const bf16_t* __restrict__ y,
+                                                         const bf16_t* __restrict__ dy,
+                                                         bf16_t* __restrict__ dx, int rows, int N,
+                                                         float scale) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nvec = N >> 3;
+  const size_t base = (size_t)row * N;
+  float yv[NV][8], dv[NV][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int vi = i * 64 + lane;
+    if (vi < nvec) {
+      u16x8 a = reinterpret_cast<const u16x8*>(y + base)[vi];
+      u16x8 b = reinterpret_cast<const u16x8*>(dy + base)[vi];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { yv[i][j] = bf2f(a[j]); dv[i][j] = bf2f(b[j]); s += yv[i][j] * dv[i][j]; }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { yv[i][j] = 0.f; dv[i][j] = 0.f; }
+    }
+  }
+  s = wave_sum(s);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int vi = i * 64 + lane;
+    if (vi < nvec) {
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(scale * yv[i][j] * (dv[i][j] - s));
+      reinterpret_cast<u16x8*>(dx + base)[vi] = o;
+    }
+  }
+}
+
+// Dropout with stateless hash mask (mask regenerated in backward from seed/offset).
+__global__ __launch_bounds__(256) void dropout_kernel(const bf16_t* __restrict__ x,
+                                                     bf16_t* __restrict__ y, long long n8, float p,
+                                                     uint64_t seed, uint64_t offset) {
+  const float ks = 1.f / (1.f - p);
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    u16x8 r = reinterpret_cast<const u16x8*>(x)[i], o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float u = hash_uniform(seed, offset, (uint64_t)i * 8 + j);
+      o[j] = f2bf(u >= p ? bf2f(r[j]) * ks : 0.f);
+    }
+    reinterpret_cast<u16x8*>(y)[i] = o;
+  }
+}
+
+}  // namespace
+
+PIAMD_EXPORT int piamd_bias_act_fwd(int act, const void* x, const void* bias, void* y, void* pre,
+                                    long long n, int N, hipStream_t stream) {
+  if (n == 0) return 0;
+  if (n % 8 || N % 8) return (int)hipErrorInvalidValue;
+  const long long n8 = n / 8;
+  const int grid = stride_grid(n8, 256);
+#define BAF(A)                                                                                  \
+  case A:                                                                                       \
+    hipLaunchKernelGGL((bias_act_fwd_kernel<A>), dim3(grid), dim3(256), 0, stream,             \
+                       (const bf16_t*)x, (const bf16_t*)bias, (bf16_t*)y, (bf16_t*)pre, n8, N); \
+    break;
+  switch (act) { BAF(0) BAF(1) BAF(2) BAF(3) BAF(4) default: return (int)hipErrorInvalidValue; }
+#undef BAF
+  return (int)hipGetLastError();
+}
+
+PIAMD_EXPORT int piamd_bias_act_bwd_grid(int rows) {
+  int g = rows < 256 ? rows : 256;
+  return g < 1 ? 1 : g;
+}
+
+// part: [G][N] f32 workspace (G = piamd_bias_act_bwd_grid(rows)) — needed when dbias != null.
+PIAMD_EXPORT int piamd_bias_act_bwd(int act, const void* dy, const void* h, const void* bias,
+                                    void* dx, void* dbias, float* part, int rows, int N,
+                                    hipStream_t stream) {
+  if (rows == 0) return 0;
+  if (N % 8) return (int)hipErrorInvalidValue;
+  const int G = piamd_bias_act_bwd_grid(rows);
+  dim3 grid(G, (N / 8 + 255) / 256);
+#define BAB(A)                                                                                  \
+  case A:                                                                                       \
+    hipLaunchKernelGGL((bias_act_bwd_kernel<A>), grid, dim3(256), 0, stream, (const bf16_t*)dy, \
+                       (const bf16_t*)h, (const bf16_t*)bias, (bf16_t*)dx,                     \
+                       dbias ? part : nullptr, rows, N);                                        \
+    break;
+  switch (act) { BAB(0) BAB(1) BAB(2) BAB(3) BAB(4) default: return (int)hipErrorInvalidValue; }
+#undef BAB
+  if (dbias)
+    hipLaunchKernelGGL(colsum_bf16_kernel, dim3((N + 63) / 64), dim3(256), 0, stream, part, G, N,
+                       (bf16_t*)dbias);
+  return (int)hipGetLastError();
+}
+
+PIAMD_EXPORT int piamd_softmax_fwd(const void* x, const void* mask, int mask_rows, int causal_q,
+                                   void* y, int rows, int N, float scale, hipStream_t stream) {
+  if (rows == 0) return 0;
+  if (N % 8 || N > 4096) return (int)hipErrorInvalidValue;
+  const int nv = (N / 8 + 63) / 64;
+  dim3 grid((rows + 3) / 4);
+#define SMF(NVV, REAL)                                                                           \
+  case REAL:                                                                                     \
+    hipLaunchKernelGGL((softmax_fwd_kernel<NVV>), grid, dim3(256), 0, stream, (const bf16_t*)x, \
+                       (const bf16_t*)mask, mask_rows > 0 ? mask_rows : 1, causal_q,            \
+                       (bf16_t*)y, rows, N, scale);                                             \
+    break;
+  switch (nv) { SMF(1, 1) SMF(2, 2) SMF(4, 3) SMF(4, 4) SMF(8, 5) SMF(8, 6) SMF(8, 7) SMF(8, 8)
+    default: return (int)hipErrorInvalidValue; }
+#undef SMF
+  return (int)hipGetLastError();
+}
+
+PIAMD_EXPORT int piamd_softmax_bwd(const void* y, const void* dy, void* dx, int rows, int N,
+                                   float scale, hipStream_t stream) {
+  if (rows == 0) return 0;
+  if (N % 8 || N > 4096) return (int)hipErrorInvalidValue;
+  const int nv = (N / 8 + 63) / 64;
+  dim3 grid((rows + 3) / 4);
+#define SMB(NVV, REAL)                                                                           \
+  case REAL:                                                                                     \
+    hipLaunchKernelGGL((softmax_bwd_kernel<NVV>), grid, dim3(256), 0, stream, (const bf16_t*)y, \
+                       (const bf16_t*)dy, (bf16_t*)dx, rows, N, scale);                        \
+    break;
+  switch (nv) { SMB(1, 1) SMB(2, 2) SMB(4, 3) SMB(4, 4) SMB(8, 5) SMB(8, 6) SMB(8, 7) SMB(8, 8)
+    default: return (int)hipErrorInvalidValue; }
+#undef SMB
+  return (int)hipGetLastError();
+}
+
+PIAMD_EXPORT int piamd_dropout(const void* x, void* y, long long n, float p, uint64_t seed,
+                               uint64_t offset, hipStream_t stream) {
+  if (n == 0) return 0;
+  if (n % 8) return (int)hipErrorInvalidValue;
+  const int grid = stride_grid(n / 8, 256);
+  hipLaunchKernelGGL(dropout_kernel, dim3(grid), dim3(256), 0, stream, (const bf16_t*)x,
+                     (bf16_t*)y, n / 8, p, seed, offset);
+  return (int)hipGetLastError();
+}

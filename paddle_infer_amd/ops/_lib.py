@@ -1,0 +1,137 @@
+"""ctypes binding of the in-tree HIP kernel library ``_lib/libpiamd_kernels.so``.
+
+The library is loaded lazily, *after* ``import torch`` so that its ``libamdhip64.so.7`` dependency
+resolves to the HIP runtime torch already mapped (one runtime, one set of streams). Every launch
+goes onto torch's current HIP stream, so the kernels compose with hipBLASLt GEMMs, RCCL
+collectives on side streams and ``torch.cuda.CUDAGraph`` (hipGraph) capture.
+
+Dispatch rule used by every op module: a tensor on the GPU runs the HIP kernel and FAILS LOUDLY
+if the library is missing; CPU tensors take the PyTorch reference path (used by the CPU test tier
+and as the numerics reference of the GPU tests).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+from .. import _build
+
+_LIB = None
+_LOCK = threading.Lock()
+
+c_void_p, c_int, c_float, c_ll, c_u64 = (ctypes.c_void_p, ctypes.c_int, ctypes.c_float,
+                                         ctypes.c_longlong, ctypes.c_uint64)
+
+# name -> argtypes (restype is always int = hipError_t)
+_SIGS = {
+    "piamd_layernorm_fwd": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                            c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_u64,
+                            c_u64, c_void_p],
+    "piamd_layernorm_bwd_grid": [c_int],
+    "piamd_layernorm_bwd": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                            c_void_p, c_int, c_int, c_float, c_u64, c_u64, c_void_p],
+    "piamd_colsum": [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
+    "piamd_adamw_flat": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_ll, c_float,
+                         c_void_p, c_float, c_float, c_float, c_float, c_float, c_float, c_void_p,
+                         c_float, c_void_p],
+    "piamd_momentum_flat": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_ll, c_float,
+                            c_void_p, c_float, c_float, c_int, c_void_p, c_void_p],
+    "piamd_sumsq": [c_void_p, c_int, c_ll, c_void_p, c_void_p, c_int, c_void_p],
+    "piamd_xent_stats": [c_int, c_void_p, c_void_p, c_int, c_int, c_ll, c_int, c_void_p, c_void_p,
+                         c_void_p, c_void_p],
+    "piamd_xent_bwd": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_int, c_ll,
+                       c_int, c_void_p, c_void_p],
+    "piamd_bias_act_fwd": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p],
+    "piamd_bias_act_bwd_grid": [c_int],
+    "piamd_bias_act_bwd": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                           c_int, c_int, c_void_p],
+    "piamd_softmax_fwd": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_float,
+                          c_void_p],
+    "piamd_softmax_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p],
+    "piamd_dropout": [c_void_p, c_void_p, c_ll, c_float, c_u64, c_u64, c_void_p],
+    "piamd_flash_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                             c_int, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll,
+                             c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_float, c_int, c_void_p],
+    "piamd_flash_attn_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                             c_int, c_int, c_int, c_int, c_int, c_int,
+                             c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll,
+                             c_ll, c_ll, c_ll, c_float, c_int, c_void_p],
+    "piamd_decode_attn": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                          c_int, c_int, c_int, c_float, c_void_p],
+    "piamd_gemm_bf16": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                        c_int, c_int, c_int, c_void_p],
+    "piamd_wo_gemm": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                      c_int, c_int, c_void_p],
+    "piamd_rope": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_ll, c_ll, c_ll,
+                   c_int, c_void_p],
+    "piamd_embedding_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_ll, c_void_p],
+}
+
+
+def lib_path() -> str:
+    return _build.KERNEL_LIB
+
+
+def _load():
+    global _LIB
+    with _LOCK:
+        if _LIB is not None:
+            return _LIB
+        path = lib_path()
+        if not os.path.exists(path):
+            raise RuntimeError(
+                f"paddle_infer_amd HIP kernel library not built ({path}); run "
+                "`python -m paddle_infer_amd._build` (or __graft_entry__.build()).")
+        lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        for name, args in _SIGS.items():
+            fn = getattr(lib, name, None)
+            if fn is None:
+                continue
+            fn.argtypes = args
+            fn.restype = ctypes.c_int
+        _LIB = lib
+        return _LIB
+
+
+def lib():
+    return _LIB if _LIB is not None else _load()
+
+
+def available() -> bool:
+    try:
+        lib()
+        return True
+    except (RuntimeError, OSError):
+        return False
+
+
+def has(name: str) -> bool:
+    return hasattr(lib(), name)
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def call(name: str, *args) -> None:
+    fn = getattr(lib(), name)
+    err = fn(*args)
+    if err != 0:
+        raise RuntimeError(f"{name} failed with hipError {err}")
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def dtype_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.bfloat16:
+        return 1
+    if t.dtype == torch.float32:
+        return 0
+    raise TypeError(f"unsupported dtype {t.dtype} for HIP kernel (bf16/f32 only)")

@@ -1,0 +1,332 @@
+"""Flat-buffer training engine: bucketed, backward-overlapped gradient collectives + fused optimizer.
+
+This is the MI355X-native replacement for the reference's dygraph DataParallel reducer
+(`paddle/fluid/imperative/reducer.cc`: grad buckets + fused all-reduce on a comm stream),
+``HybridParallelOptimizer`` (`fleet/meta_optimizers/dygraph_optimizer/hybrid_parallel_optimizer.py`:
+global-norm clip across dp/mp/pp) and ``DygraphShardingOptimizer`` / group-sharded stage 1–2
+(`fleet/meta_parallel/sharding/`: reduce-scatter grads, update the local shard, all-gather params).
+
+Design:
+* Every trainable parameter of a group (decay / no-decay × mp-distributed / replicated) is a VIEW
+  into one flat bf16 buffer; its gradient is a view into a flat grad buffer. Linear weights get
+  ``main_grad`` (the GEMM backward accumulates into it directly); all other params get ``.grad``
+  pre-set to their view, which autograd's AccumulateGrad updates in place.
+* Flat order = reverse registration order ≈ backward order, so buckets complete front to back.
+  A bucket's collective is launched (async, RCCL stream) from the grad-ready hook of its last
+  parameter, overlapping the rest of the backward pass.
+* Stage 0 (plain DP): all-reduce each bucket. Stage 1/2 (sharding): reduce-scatter each bucket into
+  a CONTIGUOUS local grad shard, so the optimizer is ONE fused AdamW launch over the shard, then
+  all-gather the updated bf16 shard back into the flat param buffer.
+* Bucket size is chosen for xGMI rings: large (default 256 MB) because a ring all-reduce /
+  reduce-scatter over 7 point-to-point links is per-link bandwidth bound and pays a fixed latency
+  per call; 288 GB of HBM makes the extra staging free.
+* Clip coefficient and the AdamW update stay on device (no host sync in ``step``).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+from ..ops.optim import adamw_flat, momentum_flat, sumsq
+
+ALIGN = 64  # elements (128 B of bf16)
+
+
+def _ceil(a, b):
+    return (a + b - 1) // b * b
+
+
+@dataclass
+class _Bucket:
+    start: int
+    end: int
+    params: list
+    pending: int = 0
+    handle: object = None
+    launched: bool = False
+
+
+class _FlatGroup:
+    def __init__(self, params, dtype, device, world, bucket_numel, weight_decay, distributed, name):
+        self.params = params
+        self.weight_decay = weight_decay
+        self.distributed = distributed
+        self.name = name
+        self.world = world
+        # layout: reverse registration order, each param aligned, buckets padded to world*ALIGN
+        offs = []
+        buckets = []
+        cur = 0
+        bstart = 0
+        bparams = []
+        for p in reversed(params):
+            n = p.numel()
+            offs.append((p, cur, n))
+            bparams.append(p)
+            cur = _ceil(cur + n, ALIGN)
+            if cur - bstart >= bucket_numel:
+                end = bstart + _ceil(cur - bstart, world * ALIGN)
+                buckets.append(_Bucket(bstart, end, bparams))
+                cur = bstart = end
+                bparams = []
+        if bparams:
+            end = bstart + _ceil(cur - bstart, world * ALIGN)
+            buckets.append(_Bucket(bstart, end, bparams))
+            cur = end
+        self.numel = cur
+        self.buckets = buckets
+        self.flat = torch.zeros(self.numel, dtype=dtype, device=device)
+        self.gflat = torch.zeros(self.numel, dtype=dtype, device=device)
+        self.offsets = {}
+        with torch.no_grad():
+            for p, o, n in offs:
+                self.flat[o:o + n].copy_(p.data.reshape(-1))
+                p.data = self.flat[o:o + n].view(p.shape)
+                self.offsets[id(p)] = (o, n)
+        self.bucket_of = {}
+        for bi, b in enumerate(buckets):
+            for p in b.params:
+                self.bucket_of[id(p)] = bi
+        # shard layout: bucket b contributes [b.len / world] elements, contiguous per rank
+        self.shard_numel = sum((b.end - b.start) // world for b in buckets)
+
+    def grad_view(self, p):
+        o, n = self.offsets[id(p)]
+        return self.gflat[o:o + n].view(p.shape)
+
+
+class FlatTrainer:
+    """Hybrid-parallel optimizer engine over flat buffers.
+
+    Args:
+        model: the (already mp-split) model.
+        lr, betas, eps, weight_decay: AdamW hyper-parameters (Paddle semantics).
+        grad_clip: global-norm clip (None to disable).
+        dp_group: data-parallel process group (None = single rank).
+        mp_group / pp_group: for the global norm (distributed params summed over mp, all over pp).
+        sharding_stage: 0 = all-reduce DP, 1/2 = sharded optimizer states (+ grads) over dp_group.
+        no_decay_fn: name -> True to exclude from weight decay (default: biases and norms).
+        optimizer: "adamw" | "momentum".
+    """
+
+    def __init__(self, model, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
+                 grad_clip=1.0, dp_group=None, mp_group=None, pp_group=None, sharding_stage=0,
+                 bucket_mb=256, no_decay_fn=None, optimizer="adamw", momentum=0.9,
+                 overlap=True):
+        self.model = model
+        self.lr = lr
+        self.beta1, self.beta2 = betas
+        self.eps = eps
+        self.grad_clip = grad_clip
+        self.dp_group = dp_group
+        self.mp_group = mp_group
+        self.pp_group = pp_group
+        self.world = dist.get_world_size(dp_group) if dp_group is not None else 1
+        self.rank = dist.get_rank(dp_group) if dp_group is not None else 0
+        self.sharding = sharding_stage if self.world > 1 else 0
+        self.optimizer = optimizer
+        self.momentum = momentum
+        self.overlap = overlap
+        self.step_count = 0
+        no_decay_fn = no_decay_fn or (lambda n, p: p.dim() == 1)
+        named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+        if not named:
+            raise ValueError("model has no trainable parameters")
+        device = named[0][1].device
+        dtype = named[0][1].dtype
+        keyed = {}
+        for n, p in named:
+            k = (not no_decay_fn(n, p), bool(getattr(p, "is_distributed", False)))
+            keyed.setdefault(k, []).append(p)
+        bucket_numel = max(ALIGN * self.world, int(bucket_mb * 2 ** 20 // p.element_size()))
+        self.groups = []
+        for (decay, distd), ps in sorted(keyed.items(), key=lambda kv: (not kv[0][0], kv[0][1])):
+            g = _FlatGroup(ps, dtype, device, self.world, bucket_numel,
+                           weight_decay if decay else 0.0, distd, f"decay{int(decay)}_dist{int(distd)}")
+            self.groups.append(g)
+        # master weights + states: full (stage 0) or local shard (stage >= 1)
+        for g in self.groups:
+            if self.sharding:
+                g.gshard = torch.zeros(g.shard_numel, dtype=dtype, device=device)
+                g.pshard = torch.zeros(g.shard_numel, dtype=dtype, device=device)
+                master = torch.empty(g.shard_numel, dtype=torch.float32, device=device)
+                self._gather_shard(g, g.flat, master)
+            else:
+                master = g.flat.float()
+            g.master = master
+            g.m = torch.zeros_like(master)
+            g.v = torch.zeros_like(master) if optimizer == "adamw" else None
+        self._install_grads()
+        self._norm_buf = torch.zeros(2, device=device, dtype=torch.float32)
+        self._clip_coef = torch.ones((), device=device, dtype=torch.float32)
+        self._ag_handles = []
+
+    # ---------------------------------------------------------------------------------
+    def _gather_shard(self, g, src_flat, out):
+        """Copy this rank's shard of every bucket of ``src_flat`` into contiguous ``out``."""
+        o = 0
+        for b in g.buckets:
+            L = (b.end - b.start) // self.world
+            out[o:o + L].copy_(src_flat[b.start + self.rank * L: b.start + (self.rank + 1) * L])
+            o += L
+
+    def _install_grads(self):
+        linear_weights = set()
+        for m in self.model.modules():
+            # weights used through ops.linear / the LM head get main_grad accumulation
+            for name in ("weight",):
+                w = getattr(m, name, None)
+                if isinstance(w, torch.nn.Parameter) and w.dim() == 2:
+                    linear_weights.add(id(w))
+        for g in self.groups:
+            for p in g.params:
+                view = g.grad_view(p)
+                if id(p) in linear_weights:
+                    p.main_grad = view
+                    p.grad = view  # embedding lookups still accumulate here through autograd
+                else:
+                    p.grad = view
+                p._grad_ready = self._make_ready(g)
+                if not hasattr(p, "_piamd_hooked"):
+                    p.register_post_accumulate_grad_hook(lambda t: t._grad_ready(t))
+                    p._piamd_hooked = True
+
+    def _make_ready(self, g):
+        def ready(p):
+            if not self.overlap or self.world == 1:
+                return
+            b = g.buckets[g.bucket_of[id(p)]]
+            b.pending -= 1
+            if b.pending == 0 and not b.launched:
+                self._launch(g, b)
+        return ready
+
+    def _launch(self, g, b):
+        b.launched = True
+        grads = g.gflat[b.start:b.end]
+        if self.sharding:
+            L = (b.end - b.start) // self.world
+            o = sum((bb.end - bb.start) // self.world for bb in g.buckets[:g.buckets.index(b)])
+            b.handle = dist.reduce_scatter_tensor(g.gshard[o:o + L], grads, group=self.dp_group,
+                                                  async_op=True)
+        else:
+            b.handle = dist.all_reduce(grads, group=self.dp_group, async_op=True)
+
+    # ---------------------------------------------------------------------------------
+    def zero_grad(self):
+        for h in self._ag_handles:
+            h.wait()
+        self._ag_handles = []
+        for g in self.groups:
+            g.gflat.zero_()
+            for b in g.buckets:
+                b.pending = len(b.params)
+                b.launched = False
+                b.handle = None
+        # every grad must still alias the flat buffer
+        for g in self.groups:
+            for p in g.params:
+                if p.grad is None or p.grad.data_ptr() != g.grad_view(p).data_ptr():
+                    p.grad = g.grad_view(p)
+
+    clear_grad = zero_grad
+
+    def _finish_reduction(self):
+        if self.world == 1:
+            return
+        for g in self.groups:
+            for b in g.buckets:
+                if not b.launched:
+                    self._launch(g, b)
+        for g in self.groups:
+            for b in g.buckets:
+                if b.handle is not None:
+                    b.handle.wait()
+                    b.handle = None
+
+    def _grads_for_update(self, g):
+        return g.gshard if self.sharding else g.gflat
+
+    def _compute_clip(self):
+        nb = self._norm_buf
+        nb.zero_()
+        for g in self.groups:
+            sumsq(self._grads_for_update(g), out=nb[1 if g.distributed else 0], accumulate=True)
+        scale = 1.0 / self.world
+        if self.world > 1 and self.sharding:
+            dist.all_reduce(nb, group=self.dp_group)
+        if self.mp_group is not None and dist.get_world_size(self.mp_group) > 1:
+            d = nb[1:2].clone()
+            dist.all_reduce(d, group=self.mp_group)
+            nb[1:2].copy_(d)
+        total = nb.sum()
+        if self.pp_group is not None and dist.get_world_size(self.pp_group) > 1:
+            dist.all_reduce(total, group=self.pp_group)
+        # grads are sums over dp ranks; the update uses grad * scale (mean)
+        norm = torch.sqrt(total) * scale
+        self.last_grad_norm = norm
+        torch.clamp(self.grad_clip / (norm + 1e-6), max=1.0, out=self._clip_coef)
+
+    def step(self, lr=None):
+        lr = self.lr if lr is None else lr
+        self._finish_reduction()
+        self.step_count += 1
+        gscale = None
+        if self.grad_clip:
+            self._compute_clip()
+            gscale = self._clip_coef
+        static = 1.0 / self.world
+        for g in self.groups:
+            grads = self._grads_for_update(g)
+            model_out = g.pshard if self.sharding else g.flat
+            if self.optimizer == "adamw":
+                adamw_flat(g.master, g.m, g.v, grads, lr, self.beta1, self.beta2, self.eps,
+                           g.weight_decay, self.step_count, model=model_out, grad_scale=gscale,
+                           static_grad_scale=static)
+            else:
+                if static != 1.0:
+                    grads = grads * static
+                momentum_flat(g.master, g.m, grads, lr, self.momentum, g.weight_decay,
+                              model=model_out, grad_scale=gscale)
+        if self.sharding:
+            for g in self.groups:
+                o = 0
+                for b in g.buckets:
+                    L = (b.end - b.start) // self.world
+                    h = dist.all_gather_into_tensor(g.flat[b.start:b.end], g.pshard[o:o + L],
+                                                    group=self.dp_group, async_op=True)
+                    self._ag_handles.append(h)
+                    o += L
+
+    def wait_params(self):
+        for h in self._ag_handles:
+            h.wait()
+        self._ag_handles = []
+
+    # ---------------------------------------------------------------------------------
+    def state_dict(self):
+        out = {"step": self.step_count}
+        for g in self.groups:
+            out[g.name] = {"master": g.master, "m": g.m, "v": g.v}
+        return out
+
+    def set_state_dict(self, sd):
+        self.step_count = int(sd.get("step", 0))
+        for g in self.groups:
+            if g.name in sd:
+                for k in ("master", "m", "v"):
+                    if sd[g.name].get(k) is not None and getattr(g, k) is not None:
+                        getattr(g, k).copy_(sd[g.name][k])
+
+    def num_params(self):
+        return sum(p.numel() for g in self.groups for p in g.params)
+
+
+def cosine_lr(step, max_lr, min_lr, warmup, total):
+    if step < warmup:
+        return max_lr * (step + 1) / warmup
+    t = min(1.0, (step - warmup) / max(1, total - warmup))
+    return min_lr + 0.5 * (max_lr - min_lr) * (1 + math.cos(math.pi * t))

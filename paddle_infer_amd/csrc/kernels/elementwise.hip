@@ -8,8 +8,8 @@
 //
 // MI355X design: 16 B/lane vectors everywhere (G13); the activation backward is 2-D (row groups ×
 // 2048-column stripes) so each thread also accumulates the bias gradient for its 8 columns in
-// registers and writes one f32 partial row per block — the dbias reduction costs no extra pass
-// over the [tokens × 4h] activation.
+// registers and adds them with one f32 atomic per column per block — the dbias reduction costs no
+// extra pass over the [tokens × 4h] activation.
 #include "common.h"
 
 namespace {
@@ -86,9 +86,9 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const bf16_t* __restr
     }
     reinterpret_cast<u16x8*>(dx)[idx] = o;
   }
-  if (part) {
+  if (part) {  // one f32 atomic per column per row-group block into part[N] (zeroed by launcher)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) part[(size_t)blockIdx.x * N + c8 * 8 + j] = acc[j];
+    for (int j = 0; j < 8; ++j) atomicAdd(part + c8 * 8 + j, acc[j]);
   }
 }
 
@@ -245,7 +245,7 @@ PIAMD_EXPORT int piamd_bias_act_bwd_grid(int rows) {
   return g < 1 ? 1 : g;
 }
 
-// part: [G][N] f32 workspace (G = piamd_bias_act_bwd_grid(rows)) — needed when dbias != null.
+// part: f32 [N] workspace (zeroed here) — needed when dbias != null.
 PIAMD_EXPORT int piamd_bias_act_bwd(int act, const void* dy, const void* h, const void* bias,
                                     void* dx, void* dbias, float* part, int rows, int N,
                                     hipStream_t stream) {
@@ -259,10 +259,11 @@ PIAMD_EXPORT int piamd_bias_act_bwd(int act, const void* dy, const void* h, cons
                        (const bf16_t*)h, (const bf16_t*)bias, (bf16_t*)dx,                     \
                        dbias ? part : nullptr, rows, N);                                        \
     break;
+  if (dbias) (void)hipMemsetAsync(part, 0, sizeof(float) * N, stream);
   switch (act) { BAB(0) BAB(1) BAB(2) BAB(3) BAB(4) default: return (int)hipErrorInvalidValue; }
 #undef BAB
   if (dbias)
-    hipLaunchKernelGGL(colsum_bf16_kernel, dim3((N + 63) / 64), dim3(256), 0, stream, part, G, N,
+    hipLaunchKernelGGL(colsum_bf16_kernel, dim3((N + 63) / 64), dim3(256), 0, stream, part, 1, N,
                        (bf16_t*)dbias);
   return (int)hipGetLastError();
 }

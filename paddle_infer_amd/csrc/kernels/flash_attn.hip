@@ -18,11 +18,16 @@
 //     operand of Oᵀ = Vᵀ·Pᵀ (no LDS round trip for P). Vᵀ fragments come from the row-major V
 //     image with ds_read_b64_tr_b16 (hardware transpose). LDS images use the dual-use XOR
 //     layout (row reads and transposed reads both conflict-free at D = 128).
-//   * Backward: workgroup = 4 waves = 128 keys (32 per wave, key on the MFMA lane), dKᵀ/dVᵀ kept in
-//     accumulators across the whole sweep over query tiles (and over the q-heads of a GQA group),
-//     so dK/dV need no cross-workgroup sum; dQ is summed over key blocks with f32 atomics whose
-//     wave-instructions are two 128-B row segments (full atomic rate, MI355X_MICROARCH §atomics).
-//   * Causal blocks are launched heaviest-first.
+//   * Backward = two atomic-free kernels. dK/dV: workgroup = 4 waves = 128 keys (32 per wave, key
+//     on the MFMA lane), dKᵀ/dVᵀ kept in accumulators across the whole sweep over query tiles and
+//     over the q-heads of a GQA group, so dK/dV need no cross-workgroup sum. dQ: the forward's
+//     structure (query row on the lane): Sᵀ = K·Qᵀ, dPᵀ = V·dOᵀ, and the dSᵀ accumulator feeds
+//     dQᵀ = Kᵀ·dSᵀ straight from registers (Kᵀ via transposed LDS reads). Recomputing S/dP in the dQ
+//     kernel costs 2 extra MFMA products but removes the f32 dQ atomics, whose chip-wide rate
+//     (≈1.3 TB/s) would floor the backward, and keeps the result bitwise deterministic.
+//   * Every global load is unconditional (row indices clamped, out-of-range rows masked in the
+//     softmax), so hipcc can count `vmcnt` and the K/V prefetch stays in flight under the MFMAs.
+//   * Causal grids are flattened and launched heaviest-first (LPT order across all heads).
 #include "common.h"
 
 namespace {
@@ -77,13 +82,40 @@ __device__ __forceinline__ bf16x8 pack_frag(const f32x16& acc, int s) {
   return r;
 }
 
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Direct-to-LDS DMA (global_load_lds_dwordx4) of a [ROWS][ROWB] bf16 tile into the dual-use
+// XOR image. The LDS destination of one wave-instruction is lane-linear (1 KiB), so the swizzle is
+// applied to the per-lane SOURCE address (guide §5.4 rule 21): physical chunk pc of row r holds
+// logical chunk pc ^ x(r). Rows past `rmax` are clamped (masked later). Each of the 4 waves issues
+// ROWS*ROWB/4096 pieces.
+template <int ROWS, int ROWB>
+__device__ __forceinline__ void glds_tile(const bf16_t* gbase, long long rstride, int row0, int rmax,
+                                          char* tile, int w, int lane) {
+  constexpr int CH = ROWB / 16;
+  constexpr int PIECES = ROWS * CH / 64;
+  constexpr int PPW = PIECES / 4;
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int P = w * PPW + i;
+    const int L = P * 64 + lane, r = L / CH, pc = L % CH;
+    const int x = (((r & 3) << 2) | ((r >> 2) & 3)) & (CH - 1);
+    const long long row = min(row0 + r, rmax);
+    const bf16_t* src = gbase + row * rstride + ((pc ^ x) << 3);
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(tile + P * 1024),
+                                     16, 0, 0);
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Forward
 // ------------------------------------------------------------------------------------------
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
-    bf16_t* __restrict__ o, float* __restrict__ lse, int Sq, int Sk, int Hq, int Hk,
+    bf16_t* __restrict__ o, float* __restrict__ lse, int B, int Sq, int Sk, int Hq, int Hk,
     long long sqb, long long sqs, long long sqh, long long skb, long long sks, long long skh,
     long long svb, long long svs, long long svh, long long sob, long long sos, long long soh,
     float scale) {
@@ -93,14 +125,14 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
   constexpr int CH = D / 8;          // 16-B chunks per row
   constexpr int ROWB = D * 2;
   constexpr int TILE_B = BN * ROWB;  // bytes per K or V tile
-  constexpr int LPT = BN * CH / 256; // 16-B loads per thread per tile
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_B];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5, gi = lane & 15, g = lane >> 4;
   const int nmb = (Sq + BM - 1) / BM;
-  const int mb = CAUSAL ? (nmb - 1 - (int)blockIdx.x) : (int)blockIdx.x;
-  const int hq = blockIdx.y, b = blockIdx.z;
+  const int HB = Hq * B;
+  const int mb = CAUSAL ? (nmb - 1 - (int)blockIdx.x / HB) : (int)blockIdx.x / HB;
+  const int hq = (int)blockIdx.x % Hq, b = ((int)blockIdx.x % HB) / Hq;
   const int hk = hq / (Hq / Hk);
   const int m0 = mb * BM;
   const int qrow0 = m0 + w * 32;
@@ -112,11 +144,10 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
 
   bf16x8 qf[KSTEPS];
   {
-    const int qr = qrow0 + l32;
+    const int qr = min(qrow0 + l32, Sq - 1);
     const bf16_t* qp = q + b * sqb + (long long)qr * sqs + hq * sqh + 8 * hh;
 #pragma unroll
-    for (int kk = 0; kk < KSTEPS; ++kk)
-      qf[kk] = qr < Sq ? *reinterpret_cast<const bf16x8*>(qp + 16 * kk) : zero_bf16x8();
+    for (int kk = 0; kk < KSTEPS; ++kk) qf[kk] = *reinterpret_cast<const bf16x8*>(qp + 16 * kk);
   }
 
   int n_end = Sk;
@@ -130,39 +161,19 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
     for (int j = 0; j < 16; ++j) oacc[i][j] = 0.f;
   float m_i = -INFINITY, l_i = 0.f;
 
-  u16x8 kreg[LPT], vreg[LPT];
-  auto gload = [&](int t) {
-#pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      const int id = tid + 256 * i, r = id / CH, cc = id % CH;
-      const int key = t * BN + r;
-      if (key < Sk) {
-        kreg[i] = *reinterpret_cast<const u16x8*>(kbase + (long long)key * sks + cc * 8);
-        vreg[i] = *reinterpret_cast<const u16x8*>(vbase + (long long)key * svs + cc * 8);
-      } else {
-        kreg[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-        vreg[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      }
-    }
-  };
-  auto lstore = [&](int buf) {
+  auto issue = [&](int t, int buf) {
     char* ks = smem + buf * 2 * TILE_B;
-    char* vs = ks + TILE_B;
-#pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      const int id = tid + 256 * i, r = id / CH, cc = id % CH;
-      *reinterpret_cast<u16x8*>(ks + lds_off<ROWB>(r, cc)) = kreg[i];
-      *reinterpret_cast<u16x8*>(vs + lds_off<ROWB>(r, cc)) = vreg[i];
-    }
+    glds_tile<BN, ROWB>(kbase, sks, t * BN, Sk - 1, ks, w, lane);
+    glds_tile<BN, ROWB>(vbase, svs, t * BN, Sk - 1, ks + TILE_B, w, lane);
   };
-
-  if (ntiles > 0) { gload(0); lstore(0); }
+  if (ntiles > 0) issue(0, 0);
   __syncthreads();
 
   const bool wave_rows_valid = qrow0 < Sq;
+  const int qpos = qrow0 + l32;
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
-    if (t + 1 < ntiles) gload(t + 1);
+    if (t + 1 < ntiles) issue(t + 1, buf ^ 1);
     const int n0 = t * BN;
     const bool active = wave_rows_valid && (!CAUSAL || n0 <= qrow0 + 31 + coff);
     if (active) {
@@ -181,42 +192,53 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
           sacc[tt] = mfma32(a, qf[kk], sacc[tt]);
         }
       }
-      // scale, mask, row max (query row = lane)
-      const int qpos = qrow0 + l32;
       const bool need_mask = (n0 + BN > Sk) || (CAUSAL && n0 + BN - 1 > qrow0 + coff);
       float mx = -INFINITY;
+      if (need_mask) {
 #pragma unroll
-      for (int tt = 0; tt < 2; ++tt)
+        for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float x = sacc[tt][r] * c;
-          if (need_mask) {
+          for (int r = 0; r < 16; ++r) {
             const int key = n0 + tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            if (key >= Sk || (CAUSAL && key > qpos + coff)) x = -INFINITY;
+            const bool ok = (key < Sk) & (!CAUSAL | (key <= qpos + coff));
+            const float x = ok ? sacc[tt][r] * c : -INFINITY;
+            sacc[tt][r] = x;
+            mx = fmaxf(mx, x);
           }
-          sacc[tt][r] = x;
-          mx = fmaxf(mx, x);
-        }
+      } else {
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float x = sacc[tt][r] * c;
+            sacc[tt][r] = x;
+            mx = fmaxf(mx, x);
+          }
+      }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float m_new = fmaxf(m_i, mx);
       const float msub = m_new == -INFINITY ? 0.f : m_new;
-      const float alpha = exp2f(m_i - msub);
       float rs = 0.f;
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float p = exp2f(sacc[tt][r] - msub);
+          const float p = fast_exp2(sacc[tt][r] - msub);
           sacc[tt][r] = p;
           rs += p;
         }
       rs += __shfl_xor(rs, 32, 64);
-      l_i = l_i * alpha + rs;
+      // rescale only when some row's running max moved (T13-style skip of an O-wide pass)
+      if (__any(m_new > m_i)) {
+        const float alpha = fast_exp2(m_i - msub);
+        l_i *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+          for (int j = 0; j < 16; ++j) oacc[dt][j] *= alpha;
+      }
+      l_i += rs;
       m_i = m_new;
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) oacc[dt][j] *= alpha;
       bf16x8 pf[4];
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt)
@@ -235,15 +257,13 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
         }
       }
     }
-    if (t + 1 < ntiles) lstore(buf ^ 1);
     __syncthreads();
   }
 
   // epilogue: lane = query row, registers = d
-  const int qr = qrow0 + l32;
-  if (qr < Sq) {
+  if (qpos < Sq) {
     const float inv = l_i > 0.f ? 1.f / l_i : 0.f;
-    bf16_t* op = o + b * sob + (long long)qr * sos + hq * soh;
+    bf16_t* op = o + b * sob + (long long)qpos * sos + hq * soh;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -255,97 +275,75 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
         *reinterpret_cast<uint2*>(op + d0) = pk;
       }
     if (hh == 0 && lse)
-      lse[((long long)b * Hq + hq) * Sq + qr] = l_i > 0.f ? (m_i + log2f(l_i)) * kLn2 : INFINITY;
+      lse[((long long)b * Hq + hq) * Sq + qpos] = l_i > 0.f ? (m_i + log2f(l_i)) * kLn2 : INFINITY;
   }
 }
 
 // ------------------------------------------------------------------------------------------
-// Backward pre-pass: delta[b, h, q] = Σ_d dO·O (f32), one wave per (row, head).
+// Backward pre-pass: delta[b, h, q] = Σ_d dO·O (f32). 16 B per lane, D/8 lanes per row.
 // ------------------------------------------------------------------------------------------
 template <int D>
 __global__ __launch_bounds__(256) void fa_bwd_pre_kernel(
     const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout, float* __restrict__ delta,
-    int Sq, int Hq, long long sob, long long sos, long long soh, long long sdb, long long sds,
-    long long sdh, int total) {
-  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (wid >= total) return;
-  const int qr = wid % Sq, hq = (wid / Sq) % Hq, b = wid / (Sq * Hq);
-  const bf16_t* op = o + b * sob + (long long)qr * sos + hq * soh;
-  const bf16_t* dp = dout + b * sdb + (long long)qr * sds + hq * sdh;
+    int Sq, int Hq, long long sob, long long sos, long long soh, int total) {
+  constexpr int TPR = D / 8;  // threads per row
+  const int row = (blockIdx.x * 256 + threadIdx.x) / TPR, sub = threadIdx.x % TPR;
+  const bool ok = row < total;
+  const int rr = ok ? row : 0;
+  const int qr = rr % Sq, hq = (rr / Sq) % Hq, b = rr / (Sq * Hq);
+  const long long off = b * sob + (long long)qr * sos + hq * soh + sub * 8;
+  u16x8 a = *reinterpret_cast<const u16x8*>(o + off);
+  u16x8 d = *reinterpret_cast<const u16x8*>(dout + off);
   float s = 0.f;
-  for (int d = lane * 2; d < D; d += 128) {
-    s += bf2f(op[d]) * bf2f(dp[d]) + bf2f(op[d + 1]) * bf2f(dp[d + 1]);
-  }
-  s = wave_sum(s);
-  if (lane == 0) delta[((long long)b * Hq + hq) * Sq + qr] = s;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s += bf2f(a[j]) * bf2f(d[j]);
+#pragma unroll
+  for (int x = TPR / 2; x > 0; x >>= 1) s += __shfl_xor(s, x, 64);
+  if (ok && sub == 0) delta[((long long)b * Hq + hq) * Sq + qr] = s;
 }
 
 // ------------------------------------------------------------------------------------------
-// Backward main: workgroup = 128 keys of one (batch, kv-head); sweeps the q-heads of the GQA
-// group and all query tiles of 64 rows.
+// Backward dK/dV: workgroup = 128 keys of one (batch, kv-head); sweeps the q-heads of the GQA
+// group and all query tiles of 64 rows. Key on the MFMA lane.
 // ------------------------------------------------------------------------------------------
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, 1) void fa_bwd_kernel(
+__global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse,
-    const float* __restrict__ delta, float* __restrict__ dq_acc, bf16_t* __restrict__ dk,
-    bf16_t* __restrict__ dv, int Sq, int Sk, int Hq, int Hk, long long sqb, long long sqs,
-    long long sqh, long long skb, long long sks, long long skh, long long svb, long long svs,
-    long long svh, long long sdob, long long sdos, long long sdoh, long long sdkb,
-    long long sdks, long long sdkh, long long sdvb, long long sdvs, long long sdvh,
-    float scale) {
+    const float* __restrict__ delta, bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int B,
+    int Sq, int Sk, int Hq, int Hk, long long sqb, long long sqs, long long sqh, long long skb,
+    long long sks, long long skh, long long svb, long long svs, long long svh, long long sdob,
+    long long sdos, long long sdoh, float scale) {
   constexpr int BK = 128, BQ = 64;
   constexpr int KSTEPS = D / 16;
   constexpr int DT = D / 32;
   constexpr int CH = D / 8;
   constexpr int ROWB = D * 2;
-  constexpr int KIMG_B = BK * ROWB;     // K image [128 keys][D]
   constexpr int QTILE_B = BQ * ROWB;    // Q or dO tile [64][D]
-  constexpr int DS_ROWB = BQ * 2;       // dSᵀ image [128 keys][64 q] bf16
-  constexpr int DS_B = BK * DS_ROWB;
-  constexpr int LPT = BQ * CH / 256;    // 16-B loads per thread per Q (or dO) tile
-  constexpr int OFF_K = 0;
-  constexpr int OFF_Q = OFF_K + KIMG_B;               // 2 buffers x (Q, dO)
-  constexpr int OFF_DS = OFF_Q + 2 * 2 * QTILE_B;
-  constexpr int OFF_STAT = OFF_DS + DS_B;             // 2 buffers x (lse, delta) x 64 f32
+  constexpr int KIMG_B = BK * ROWB;     // resident K and V images of the block's 128 keys
+  constexpr int OFF_K = 2 * 2 * QTILE_B;
+  constexpr int OFF_V = OFF_K + KIMG_B;
+  constexpr int OFF_STAT = OFF_V + KIMG_B;  // 2 buffers x (lse, delta) x 64 f32
   constexpr int SMEM = OFF_STAT + 2 * 2 * BQ * 4;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5, gi = lane & 15, g = lane >> 4;
-  const int nkb = (Sk + BK - 1) / BK;
-  const int kb = CAUSAL ? (int)blockIdx.x : (int)blockIdx.x;  // (light blocks are the late ones)
-  const int hk = blockIdx.y, b = blockIdx.z;
+  const int HB = Hk * B;
+  const int kb = (int)blockIdx.x / HB;  // causal: low key blocks see the most queries -> first
+  const int hk = (int)blockIdx.x % Hk, b = ((int)blockIdx.x % HB) / Hk;
   const int n0 = kb * BK;
   const int kw0 = n0 + 32 * w;  // this wave's first key
+  const int key = kw0 + l32;
   const int coff = Sk - Sq;
   const int group = Hq / Hk;
   const float c = scale * kLog2e;
-  (void)nkb;
 
-  // ---- stage K image (all 128 keys) into LDS; K and V fragments of this wave's keys to regs.
-  {
-    const bf16_t* kbp = k + b * skb + hk * skh;
-#pragma unroll
-    for (int i = 0; i < BK * CH / 256; ++i) {
-      const int id = tid + 256 * i, r = id / CH, cc = id % CH;
-      const int key = n0 + r;
-      u16x8 val = key < Sk ? *reinterpret_cast<const u16x8*>(kbp + (long long)key * sks + cc * 8)
-                           : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      *reinterpret_cast<u16x8*>(smem + OFF_K + lds_off<ROWB>(r, cc)) = val;
-    }
-  }
-  bf16x8 kf[KSTEPS], vf[KSTEPS];
-  {
-    const int key = kw0 + l32;
-    const bf16_t* kp = k + b * skb + (long long)key * sks + hk * skh + 8 * hh;
-    const bf16_t* vp = v + b * svb + (long long)key * svs + hk * svh + 8 * hh;
-#pragma unroll
-    for (int kk = 0; kk < KSTEPS; ++kk) {
-      kf[kk] = key < Sk ? *reinterpret_cast<const bf16x8*>(kp + 16 * kk) : zero_bf16x8();
-      vf[kk] = key < Sk ? *reinterpret_cast<const bf16x8*>(vp + 16 * kk) : zero_bf16x8();
-    }
-  }
+  // K / V of the block's keys stay resident in LDS (B operands of S and dP are row reads)
+  glds_tile<BK, ROWB>(k + b * skb + hk * skh, sks, n0, Sk - 1, smem + OFF_K, w, lane);
+  glds_tile<BK, ROWB>(v + b * svb + hk * svh, svs, n0, Sk - 1, smem + OFF_V, w, lane);
+  const char* kimg = smem + OFF_K;
+  const char* vimg = smem + OFF_V;
 
   f32x16 dkacc[DT], dvacc[DT];
 #pragma unroll
@@ -353,179 +351,141 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(
 #pragma unroll
     for (int j = 0; j < 16; ++j) { dkacc[i][j] = 0.f; dvacc[i][j] = 0.f; }
 
-  // first query tile that can see any key of this block
   const int q_start = CAUSAL ? max(0, n0 - coff) : 0;
   const int qt0 = q_start / BQ;
   const int nqt = (Sq + BQ - 1) / BQ;
   const int tiles_per_head = nqt - qt0;
-  const int total = tiles_per_head > 0 ? tiles_per_head * group : 0;
+  const int total = (n0 < Sk && tiles_per_head > 0) ? tiles_per_head * group : 0;
 
-  u16x8 qreg[LPT], doreg[LPT];
-  float lreg = 0.f, dreg = 0.f;
-  auto gload = [&](int it) {
+  auto issue = [&](int it, int buf) {
     const int hq = hk * group + it / tiles_per_head;
     const int q0 = (qt0 + it % tiles_per_head) * BQ;
-    const bf16_t* qbp = q + b * sqb + hq * sqh;
-    const bf16_t* dbp = dout + b * sdob + hq * sdoh;
-#pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      const int id = tid + 256 * i, r = id / CH, cc = id % CH;
-      const int qr = q0 + r;
-      if (qr < Sq) {
-        qreg[i] = *reinterpret_cast<const u16x8*>(qbp + (long long)qr * sqs + cc * 8);
-        doreg[i] = *reinterpret_cast<const u16x8*>(dbp + (long long)qr * sdos + cc * 8);
-      } else {
-        qreg[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-        doreg[i] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      }
-    }
-    if (tid < BQ) {
-      const int qr = q0 + tid;
-      const long long si = ((long long)b * Hq + hq) * Sq + qr;
-      lreg = qr < Sq ? lse[si] * kLog2e : INFINITY;
-      dreg = qr < Sq ? delta[si] : 0.f;
+    char* qs = smem + buf * 2 * QTILE_B;
+    glds_tile<BQ, ROWB>(q + b * sqb + hq * sqh, sqs, q0, Sq - 1, qs, w, lane);
+    glds_tile<BQ, ROWB>(dout + b * sdob + hq * sdoh, sdos, q0, Sq - 1, qs + QTILE_B, w, lane);
+    if (w < 2) {  // wave 0: lse row, wave 1: delta row (64 f32 = one 4-B/lane DMA)
+      const float* s = (w == 0 ? lse : delta) + ((long long)b * Hq + hq) * Sq + min(q0 + lane, Sq - 1);
+      char* st = smem + OFF_STAT + (buf * 2 + w) * BQ * 4;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)s,
+                                       (__attribute__((address_space(3))) void*)st, 4, 0, 0);
     }
   };
-  auto lstore = [&](int buf) {
-    char* qs = smem + OFF_Q + buf * 2 * QTILE_B;
-    char* ds = qs + QTILE_B;
-#pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      const int id = tid + 256 * i, r = id / CH, cc = id % CH;
-      *reinterpret_cast<u16x8*>(qs + lds_off<ROWB>(r, cc)) = qreg[i];
-      *reinterpret_cast<u16x8*>(ds + lds_off<ROWB>(r, cc)) = doreg[i];
-    }
-    float* st = reinterpret_cast<float*>(smem + OFF_STAT) + buf * 2 * BQ;
-    if (tid < BQ) { st[tid] = lreg; st[BQ + tid] = dreg; }
-  };
-
-  if (total > 0) { gload(0); lstore(0); }
+  if (total > 0) issue(0, 0);
   __syncthreads();
 
   for (int it = 0; it < total; ++it) {
     const int buf = it & 1;
-    const int hq = hk * group + it / tiles_per_head;
     const int q0 = (qt0 + it % tiles_per_head) * BQ;
-    if (it + 1 < total) gload(it + 1);
-    const char* qs = smem + OFF_Q + buf * 2 * QTILE_B;
+    if (it + 1 < total) issue(it + 1, buf ^ 1);
+    const char* qs = smem + buf * 2 * QTILE_B;
     const char* dos = qs + QTILE_B;
     const float* lst = reinterpret_cast<const float*>(smem + OFF_STAT) + buf * 2 * BQ;
     const float* dst = lst + BQ;
-    char* dsimg = smem + OFF_DS;
-    // wave fully masked for this q tile? (all its keys beyond every query row)
-    const bool active = !CAUSAL || (kw0 <= q0 + BQ - 1 + coff);
-    if (active) {
-      // S = Q·Kᵀ and dP = dO·Vᵀ, key on lane, query in registers; 2 q-subtiles of 32
+    // Re-derive every lane-dependent LDS address inside the iteration (an opaque copy of the lane
+    // id): otherwise hipcc hoists ~60 loop-invariant swizzled addresses into VGPRs and evicts the
+    // accumulators to AGPRs with per-iteration copies.
+    int lx = lane;
+    asm volatile("" : "+v"(lx));
+    const int l32 = lx & 31, hh = lx >> 5, gi = lx & 15, g = lx >> 4;
+    // no per-wave skip: a wave whose keys are all above this tile's diagonal computes a fully
+    // masked tile (only the first q tile of a block); a branch here would make hipcc shuttle the
+    // 128 loop-carried dK/dV accumulators between AGPRs and VGPRs every iteration.
+    {
       f32x16 sacc[2], pacc[2];
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
         for (int j = 0; j < 16; ++j) { sacc[qt][j] = 0.f; pacc[qt][j] = 0.f; }
-#pragma unroll
-      for (int kk = 0; kk < KSTEPS; ++kk) {
+      // S = Q·Kᵀ, dP = dO·Vᵀ with the next k-step's 6 fragments loaded one step ahead
+      bf16x8 fr[2][6];
+      auto ld = [&](int kk, bf16x8* f) {
+        const int koff = lds_off<ROWB>(32 * w + l32, 2 * kk + hh);
+        f[0] = lds_row8(kimg, koff);
+        f[1] = lds_row8(vimg, koff);
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt) {
-          bf16x8 a = lds_row8(qs, lds_off<ROWB>(qt * 32 + l32, 2 * kk + hh));
-          sacc[qt] = mfma32(a, kf[kk], sacc[qt]);
-          bf16x8 a2 = lds_row8(dos, lds_off<ROWB>(qt * 32 + l32, 2 * kk + hh));
-          pacc[qt] = mfma32(a2, vf[kk], pacc[qt]);
+          const int qoff = lds_off<ROWB>(qt * 32 + l32, 2 * kk + hh);
+          f[2 + qt] = lds_row8(qs, qoff);
+          f[4 + qt] = lds_row8(dos, qoff);
         }
+      };
+      ld(0, fr[0]);
+#pragma unroll
+      for (int kk = 0; kk < KSTEPS; ++kk) {
+        if (kk + 1 < KSTEPS) ld(kk + 1, fr[(kk + 1) & 1]);
+        const bf16x8* f = fr[kk & 1];
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+          sacc[qt] = mfma32(f[2 + qt], f[0], sacc[qt]);
+          pacc[qt] = mfma32(f[4 + qt], f[1], pacc[qt]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
-      // P = exp2(S·c − lse·log2e), dS = P·(dP − delta)
-      const int key = kw0 + l32;
+      __builtin_amdgcn_sched_barrier(0);
+      const bool need_mask = (kw0 + 31 >= Sk) || (q0 + BQ > Sq) ||
+                             (CAUSAL && kw0 + 31 > q0 + coff);
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int qi = qt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          const int qr = q0 + qi;
-          float p = exp2f(sacc[qt][r] * c - lst[qi]);
-          if (key >= Sk || (CAUSAL && key > qr + coff)) p = 0.f;
-          sacc[qt][r] = p;
-          pacc[qt][r] = p * (pacc[qt][r] - dst[qi]);
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int qi0 = qt * 32 + 8 * g4 + 4 * hh;
+          const f32x4 l4 = *reinterpret_cast<const f32x4*>(lst + qi0);
+          const f32x4 d4 = *reinterpret_cast<const f32x4*>(dst + qi0);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * g4 + e;
+            float p = fast_exp2(sacc[qt][r] * c - l4[e] * kLog2e);
+            if (need_mask) {
+              const int qr = q0 + qi0 + e;
+              const bool ok = (key < Sk) & (qr < Sq) & (!CAUSAL | (key <= qr + coff));
+              p = ok ? p : 0.f;
+            }
+            sacc[qt][r] = p;
+            pacc[qt][r] = p * (pacc[qt][r] - d4[e]);
+          }
         }
       // dVᵀ += dOᵀ·P ; dKᵀ += Qᵀ·dS   (A operands via transposed reads of the dO / Q images)
+      bf16x8 pb[4], db[4];
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          const bf16x8 pb = pack_frag(sacc[qt], s);
-          const bf16x8 db = pack_frag(pacc[qt], s);
-          const int r0 = 32 * qt + 16 * s + 4 * hh;
-#pragma unroll
-          for (int dt = 0; dt < DT; ++dt) {
-            const int c0 = 32 * dt + 16 * (g & 1);
-            bf16x8 ado = cat44(lds_tr4<ROWB>(dos, r0, c0, gi), lds_tr4<ROWB>(dos, r0 + 8, c0, gi));
-            dvacc[dt] = mfma32(ado, pb, dvacc[dt]);
-            bf16x8 aq = cat44(lds_tr4<ROWB>(qs, r0, c0, gi), lds_tr4<ROWB>(qs, r0 + 8, c0, gi));
-            dkacc[dt] = mfma32(aq, db, dkacc[dt]);
-          }
+          pb[2 * qt + s] = pack_frag(sacc[qt], s);
+          db[2 * qt + s] = pack_frag(pacc[qt], s);
         }
-      // dSᵀ image [key][q]: lane's key row, 4 consecutive q per register group
+      __builtin_amdgcn_sched_barrier(0);
+      // dVᵀ += dOᵀ·P ; dKᵀ += Qᵀ·dS, transposed-read fragments one (dt, half) step ahead
+      bf16x8 tf[2][4];
+      auto ldt = [&](int st, bf16x8* f) {  // st = 2*dt + half: ks in {2*half, 2*half+1}
+        const int c0 = 32 * (st >> 1) + 16 * (g & 1);
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int qc = 32 * qt + 8 * g4 + 4 * hh;  // first of 4 q columns
-          uint2 pk;
-          pk.x = pack_bf16x2(pacc[qt][4 * g4 + 0], pacc[qt][4 * g4 + 1]);
-          pk.y = pack_bf16x2(pacc[qt][4 * g4 + 2], pacc[qt][4 * g4 + 3]);
-          *reinterpret_cast<uint2*>(dsimg + lds_off<DS_ROWB>(32 * w + l32, qc >> 3) + ((qc & 7) << 1)) = pk;
+        for (int j = 0; j < 2; ++j) {
+          const int r0 = 16 * (2 * (st & 1) + j) + 4 * hh;
+          f[2 * j] = cat44(lds_tr4<ROWB>(dos, r0, c0, gi), lds_tr4<ROWB>(dos, r0 + 8, c0, gi));
+          f[2 * j + 1] = cat44(lds_tr4<ROWB>(qs, r0, c0, gi), lds_tr4<ROWB>(qs, r0 + 8, c0, gi));
         }
-    } else {
+      };
+      ldt(0, tf[0]);
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
+      for (int st = 0; st < 2 * DT; ++st) {
+        if (st + 1 < 2 * DT) ldt(st + 1, tf[(st + 1) & 1]);
+        const bf16x8* f = tf[st & 1];
+        const int dt = st >> 1;
 #pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int qc = 32 * qt + 8 * g4 + 4 * hh;
-          *reinterpret_cast<uint2*>(dsimg + lds_off<DS_ROWB>(32 * w + l32, qc >> 3) + ((qc & 7) << 1)) = uint2{0u, 0u};
+        for (int j = 0; j < 2; ++j) {
+          const int ks = 2 * (st & 1) + j;
+          dvacc[dt] = mfma32(f[2 * j], pb[ks], dvacc[dt]);
+          dkacc[dt] = mfma32(f[2 * j + 1], db[ks], dkacc[dt]);
         }
-    }
-    __syncthreads();
-    // dQ[q][d] (this wave: d columns 32w..32w+31) = Σ_key dS[q][key]·K[key][d]
-    {
-      bool any = true;
-      if (CAUSAL) any = n0 <= q0 + BQ - 1 + coff;
-      if (any && 32 * w < D) {
-        f32x16 qacc[2];
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-          for (int j = 0; j < 16; ++j) qacc[qt][j] = 0.f;
-        const char* kimg = smem + OFF_K;
-#pragma unroll
-        for (int ks = 0; ks < BK / 16; ++ks) {
-          const int r0 = 16 * ks + 4 * hh;
-          const int cb = 32 * w + 16 * (g & 1);
-          bf16x8 bk = cat44(lds_tr4<ROWB>(kimg, r0, cb, gi), lds_tr4<ROWB>(kimg, r0 + 8, cb, gi));
-#pragma unroll
-          for (int qt = 0; qt < 2; ++qt) {
-            const int qb = 32 * qt + 16 * (g & 1);
-            bf16x8 ads = cat44(lds_tr4<DS_ROWB>(dsimg, r0, qb, gi), lds_tr4<DS_ROWB>(dsimg, r0 + 8, qb, gi));
-            qacc[qt] = mfma32(ads, bk, qacc[qt]);
-          }
-        }
-        // atomics: lane = d column, registers = q rows
-        const int d = 32 * w + l32;
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int qr = q0 + 32 * qt + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            if (qr < Sq)
-              atomicAdd(dq_acc + (((long long)b * Sq + qr) * Hq + hq) * D + d, qacc[qt][r] * scale);
-          }
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
-    if (it + 1 < total) lstore(buf ^ 1);
     __syncthreads();
   }
 
-  // write dK (scaled) and dV: lane = key, registers = d
-  const int key = kw0 + l32;
   if (key < Sk) {
-    bf16_t* dkp = dk + b * sdkb + (long long)key * sdks + hk * sdkh;
-    bf16_t* dvp = dv + b * sdvb + (long long)key * sdvs + hk * sdvh;
+    bf16_t* dkp = dk + b * skb + (long long)key * sks + hk * skh;
+    bf16_t* dvp = dv + b * svb + (long long)key * svs + hk * svh;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -542,26 +502,145 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_kernel(
   }
 }
 
-// dq (bf16, strided) = dq_acc (f32, [B, Sq, Hq, D] contiguous)
-template <int D>
-__global__ __launch_bounds__(256) void fa_dq_convert_kernel(const float* __restrict__ acc,
-                                                           bf16_t* __restrict__ dq, int Sq,
-                                                           int Hq, long long sb, long long ss,
-                                                           long long sh, long long total8) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= total8) return;
-  const long long e = i * 8;
-  const int d = e % D;
-  const long long row = e / D;  // (b*Sq + s)*Hq + h
-  const int h = row % Hq;
-  const long long bs = row / Hq;
-  const int s = bs % Sq;
-  const int b = bs / Sq;
-  f32x4 a = *reinterpret_cast<const f32x4*>(acc + e), c2 = *reinterpret_cast<const f32x4*>(acc + e + 4);
-  u16x8 o;
+// ------------------------------------------------------------------------------------------
+// Backward dQ: the forward's structure (query row on the lane).
+// ------------------------------------------------------------------------------------------
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+    const bf16_t* __restrict__ dout, const float* __restrict__ lse,
+    const float* __restrict__ delta, bf16_t* __restrict__ dq, int B, int Sq, int Sk, int Hq,
+    int Hk, long long sqb, long long sqs, long long sqh, long long skb, long long sks,
+    long long skh, long long svb, long long svs, long long svh, long long sdob, long long sdos,
+    long long sdoh, float scale) {
+  constexpr int BM = 128, BN = 64;
+  constexpr int KSTEPS = D / 16;
+  constexpr int DT = D / 32;
+  constexpr int CH = D / 8;
+  constexpr int ROWB = D * 2;
+  constexpr int TILE_B = BN * ROWB;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_B];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5, gi = lane & 15, g = lane >> 4;
+  const int nmb = (Sq + BM - 1) / BM;
+  const int HB = Hq * B;
+  const int mb = CAUSAL ? (nmb - 1 - (int)blockIdx.x / HB) : (int)blockIdx.x / HB;
+  const int hq = (int)blockIdx.x % Hq, b = ((int)blockIdx.x % HB) / Hq;
+  const int hk = hq / (Hq / Hk);
+  const int m0 = mb * BM;
+  const int qrow0 = m0 + w * 32;
+  const int qpos = qrow0 + l32;
+  const int coff = Sk - Sq;
+  const float c = scale * kLog2e;
+
+  const bf16_t* kbase = k + b * skb + hk * skh;
+  const bf16_t* vbase = v + b * svb + hk * svh;
+
+  bf16x8 qf[KSTEPS], df[KSTEPS];
+  float lse2, dlt;
+  {
+    const long long qr = min(qpos, Sq - 1);
+    const bf16_t* qp = q + b * sqb + qr * sqs + hq * sqh + 8 * hh;
+    const bf16_t* dp = dout + b * sdob + qr * sdos + hq * sdoh + 8 * hh;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) { o[j] = f2bf(a[j]); o[4 + j] = f2bf(c2[j]); }
-  *reinterpret_cast<u16x8*>(dq + b * sb + (long long)s * ss + h * sh + d) = o;
+    for (int kk = 0; kk < KSTEPS; ++kk) {
+      qf[kk] = *reinterpret_cast<const bf16x8*>(qp + 16 * kk);
+      df[kk] = *reinterpret_cast<const bf16x8*>(dp + 16 * kk);
+    }
+    const long long si = ((long long)b * Hq + hq) * Sq + qr;
+    lse2 = lse[si] * kLog2e;
+    dlt = delta[si];
+  }
+
+  int n_end = Sk;
+  if (CAUSAL) n_end = min(Sk, m0 + BM + coff);
+  const int ntiles = n_end <= 0 ? 0 : (n_end + BN - 1) / BN;
+
+  f32x16 qacc[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) qacc[i][j] = 0.f;
+
+  auto issue = [&](int t, int buf) {
+    char* ks = smem + buf * 2 * TILE_B;
+    glds_tile<BN, ROWB>(kbase, sks, t * BN, Sk - 1, ks, w, lane);
+    glds_tile<BN, ROWB>(vbase, svs, t * BN, Sk - 1, ks + TILE_B, w, lane);
+  };
+  if (ntiles > 0) issue(0, 0);
+  __syncthreads();
+
+  const bool wave_rows_valid = qrow0 < Sq;
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) issue(t + 1, buf ^ 1);
+    const int n0 = t * BN;
+    const bool active = wave_rows_valid && (!CAUSAL || n0 <= qrow0 + 31 + coff);
+    if (active) {
+      const char* ks = smem + buf * 2 * TILE_B;
+      const char* vs = ks + TILE_B;
+      f32x16 sacc[2], pacc[2];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) { sacc[tt][j] = 0.f; pacc[tt][j] = 0.f; }
+#pragma unroll
+      for (int kk = 0; kk < KSTEPS; ++kk) {
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+          const int off = lds_off<ROWB>(tt * 32 + l32, 2 * kk + hh);
+          sacc[tt] = mfma32(lds_row8(ks, off), qf[kk], sacc[tt]);
+          pacc[tt] = mfma32(lds_row8(vs, off), df[kk], pacc[tt]);
+        }
+      }
+      const bool need_mask = (n0 + BN > Sk) || (CAUSAL && n0 + BN - 1 > qrow0 + coff);
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float p = fast_exp2(sacc[tt][r] * c - lse2);
+          if (need_mask) {
+            const int key = n0 + tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            const bool ok = (key < Sk) & (!CAUSAL | (key <= qpos + coff));
+            p = ok ? p : 0.f;
+          }
+          pacc[tt][r] = p * (pacc[tt][r] - dlt);
+        }
+      bf16x8 dsf[4];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) dsf[2 * tt + s] = pack_frag(pacc[tt], s);
+      // dQᵀ += Kᵀ · dSᵀ
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const int c0 = 32 * dt + 16 * (g & 1);
+#pragma unroll
+        for (int ks4 = 0; ks4 < 4; ++ks4) {
+          const int r0 = 16 * ks4 + 4 * hh;
+          s16x4_t lo = lds_tr4<ROWB>(ks, r0, c0, gi);
+          s16x4_t hi = lds_tr4<ROWB>(ks, r0 + 8, c0, gi);
+          qacc[dt] = mfma32(cat44(lo, hi), dsf[ks4], qacc[dt]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  if (qpos < Sq) {
+    bf16_t* qp = dq + b * sqb + (long long)qpos * sqs + hq * sqh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = 32 * dt + 8 * g4 + 4 * hh;
+        uint2 pk;
+        pk.x = pack_bf16x2(qacc[dt][4 * g4 + 0] * scale, qacc[dt][4 * g4 + 1] * scale);
+        pk.y = pack_bf16x2(qacc[dt][4 * g4 + 2] * scale, qacc[dt][4 * g4 + 3] * scale);
+        *reinterpret_cast<uint2*>(qp + d0) = pk;
+      }
+  }
 }
 
 }  // namespace
@@ -576,10 +655,11 @@ PIAMD_EXPORT int piamd_flash_attn_fwd(const void* q, const void* k, const void* 
                                       float scale, int causal, hipStream_t stream) {
   if (Hk <= 0 || Hq % Hk) return (int)hipErrorInvalidValue;
   if (B == 0 || Sq == 0) return 0;
-  dim3 grid((Sq + 127) / 128, Hq, B), block(256);
+  if (Sk == 0) return (int)hipErrorInvalidValue;
+  dim3 grid(((Sq + 127) / 128) * Hq * B), block(256);
 #define FAF(DD, CC)                                                                               \
   hipLaunchKernelGGL((fa_fwd_kernel<DD, CC>), grid, block, 0, stream, (const bf16_t*)q,          \
-                     (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse, Sq, Sk, Hq, Hk, sqb,  \
+                     (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse, B, Sq, Sk, Hq, Hk, sqb, \
                      sqs, sqh, skb, sks, skh, svb, svs, svh, sob, sos, soh, scale)
   if (D == 128) { if (causal) FAF(128, true); else FAF(128, false); }
   else if (D == 64) { if (causal) FAF(64, true); else FAF(64, false); }
@@ -588,7 +668,9 @@ PIAMD_EXPORT int piamd_flash_attn_fwd(const void* q, const void* k, const void* 
   return (int)hipGetLastError();
 }
 
-// Backward. dq_acc: f32 workspace [B, Sq, Hq, D] (zeroed here). delta: f32 [B, Hq, Sq] workspace.
+// Backward. Strides: q/dq share (sqb, sqs, sqh); k/dk share (skb, sks, skh); v/dv share
+// (svb, svs, svh); o and dout share (sdb, sds, sdh). delta: f32 [B, Hq, Sq] workspace.
+// dq_acc / reserved: unused (kept for ABI stability).
 PIAMD_EXPORT int piamd_flash_attn_bwd(const void* q, const void* k, const void* v, const void* o,
                                       const void* dout, const float* lse, float* delta,
                                       float* dq_acc, void* dq, void* dk, void* dv,
@@ -597,35 +679,29 @@ PIAMD_EXPORT int piamd_flash_attn_bwd(const void* q, const void* k, const void* 
                                       long long sks, long long skh, long long svb, long long svs,
                                       long long svh, long long sdb, long long sds, long long sdh,
                                       float scale, int causal, hipStream_t stream) {
-  // Strides: q/dq share (sqb, sqs, sqh); k/dk share (skb, sks, skh); v/dv share (svb, svs, svh);
-  // o and dout share (sdb, sds, sdh).
-  (void)reserved;
+  (void)reserved; (void)dq_acc;
   if (Hk <= 0 || Hq % Hk) return (int)hipErrorInvalidValue;
   if (B == 0 || Sq == 0 || Sk == 0) return 0;
-  hipMemsetAsync(dq_acc, 0, sizeof(float) * (size_t)B * Sq * Hq * D, stream);
   const int total = B * Hq * Sq;
+  const int tpr = D / 8;
+  const int pre_blocks = (int)(((long long)total * tpr + 255) / 256);
 #define PRE(DD)                                                                                   \
-  hipLaunchKernelGGL((fa_bwd_pre_kernel<DD>), dim3((total + 3) / 4), dim3(256), 0, stream,       \
-                     (const bf16_t*)o, (const bf16_t*)dout, delta, Sq, Hq, sdb, sds, sdh, sdb,  \
-                     sds, sdh, total)
+  hipLaunchKernelGGL((fa_bwd_pre_kernel<DD>), dim3(pre_blocks), dim3(256), 0, stream,            \
+                     (const bf16_t*)o, (const bf16_t*)dout, delta, Sq, Hq, sdb, sds, sdh, total)
   if (D == 128) PRE(128); else if (D == 64) PRE(64); else return (int)hipErrorInvalidValue;
 #undef PRE
-  dim3 grid((Sk + 127) / 128, Hk, B), block(256);
+  dim3 gkv(((Sk + 127) / 128) * Hk * B), gq(((Sq + 127) / 128) * Hq * B), block(256);
 #define FAB(DD, CC)                                                                               \
-  hipLaunchKernelGGL((fa_bwd_kernel<DD, CC>), grid, block, 0, stream, (const bf16_t*)q,          \
-                     (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, delta, dq_acc, \
-                     (bf16_t*)dk, (bf16_t*)dv, Sq, Sk, Hq, Hk, sqb, sqs, sqh, skb, sks, skh, svb, \
-                     svs, svh, sdb, sds, sdh, skb, sks, skh, svb, svs, svh, scale)
-  if (D == 128) { if (causal) FAB(128, true); else FAB(128, false); }
-  else { if (causal) FAB(64, true); else FAB(64, false); }
+  hipLaunchKernelGGL((fa_bwd_dkdv_kernel<DD, CC>), gkv, block, 0, stream, (const bf16_t*)q,      \
+                     (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, delta,         \
+                     (bf16_t*)dk, (bf16_t*)dv, B, Sq, Sk, Hq, Hk, sqb, sqs, sqh, skb, sks, skh,   \
+                     svb, svs, svh, sdb, sds, sdh, scale);                                        \
+  hipLaunchKernelGGL((fa_bwd_dq_kernel<DD, CC>), gq, block, 0, stream, (const bf16_t*)q,         \
+                     (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, delta,         \
+                     (bf16_t*)dq, B, Sq, Sk, Hq, Hk, sqb, sqs, sqh, skb, sks, skh, svb, svs, svh, \
+                     sdb, sds, sdh, scale)
+  if (D == 128) { if (causal) { FAB(128, true); } else { FAB(128, false); } }
+  else { if (causal) { FAB(64, true); } else { FAB(64, false); } }
 #undef FAB
-  const long long total8 = (long long)B * Sq * Hq * D / 8;
-  const int cg = (int)((total8 + 255) / 256);
-  if (D == 128)
-    hipLaunchKernelGGL((fa_dq_convert_kernel<128>), dim3(cg), dim3(256), 0, stream, dq_acc,
-                       (bf16_t*)dq, Sq, Hq, sqb, sqs, sqh, total8);
-  else
-    hipLaunchKernelGGL((fa_dq_convert_kernel<64>), dim3(cg), dim3(256), 0, stream, dq_acc,
-                       (bf16_t*)dq, Sq, Hq, sqb, sqs, sqh, total8);
   return (int)hipGetLastError();
 }

@@ -9,8 +9,8 @@
 // registers (16 B/lane loads: each vector instruction moves 1 KiB contiguous), exact two-pass
 // mean/variance from registers (no Welford, no second HBM read). 4 rows per 256-thread block so a
 // 8192×2048 activation gets 2048 blocks (≫ 256 CUs). Backward fuses dgamma/dbeta: every wave
-// accumulates its columns across a grid-stride set of rows in registers, one partial row per
-// block, then a column-sum kernel. Dropout masks are regenerated from a stateless hash in
+// accumulates its columns across a grid-stride set of rows in registers, the block reduces them
+// in LDS and adds one f32 atomic per column (no [blocks x N] partial slab, no second pass). Dropout masks are regenerated from a stateless hash in
 // backward (no mask tensor in HBM).
 #include "common.h"
 
@@ -209,7 +209,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       }
     }
   }
-  // Block reduce the 4 waves' column partials through LDS, one partial row per block.
+  // Block-reduce the 4 waves' column partials through LDS, then ONE f32 atomic add per column
+  // per block into acc[N] (zeroed by the launcher): G x N x 4 B of atomics, spread over the
+  // kernel, instead of a [G][N] partial slab and a second column-sum pass.
   __shared__ float red[4][512];
   float* outs[3] = {part_dg, part_db, part_dbias};
 #pragma unroll
@@ -217,18 +219,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     if (!outs[q]) continue;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-      const int vi = i * 64 + lane;
-      // each pass handles 512 columns (64 lanes x 8)
 #pragma unroll
       for (int j = 0; j < 8; ++j) red[w][lane * 8 + j] = q == 0 ? dg[i][j] : (q == 1 ? db[i][j] : dbi[i][j]);
       __syncthreads();
       for (int c = threadIdx.x; c < 512; c += 256) {
         const int col = i * 512 + c;
-        if (col < N && (i * 64 + (c >> 3)) < nvec)
-          outs[q][(size_t)blockIdx.x * N + col] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+        if (col < N) atomicAdd(outs[q] + col, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
       }
       __syncthreads();
-      (void)vi;
     }
   }
 }
@@ -331,8 +329,8 @@ PIAMD_EXPORT int piamd_layernorm_bwd_grid(int rows) {
   return g > 512 ? 512 : (g < 1 ? 1 : g);
 }
 
-// Backward. part_* are [G][N] f32 workspaces (G = piamd_layernorm_bwd_grid(rows)); dgamma/dbeta/
-// dbias outputs (dtype of params) are produced by column sums; each may be null.
+// Backward. part_* are f32 [N] accumulators (zeroed here); dgamma/dbeta/dbias outputs (dtype of
+// the params) are converted from them; each may be null.
 PIAMD_EXPORT int piamd_layernorm_bwd(int dtype, const void* dy, const void* h, const void* gamma,
                                      const float* mean, const float* rstd, const void* dres_in,
                                      void* dres, void* dx, void* dgamma, void* dbeta, void* dbias,
@@ -342,6 +340,9 @@ PIAMD_EXPORT int piamd_layernorm_bwd(int dtype, const void* dy, const void* h, c
   if (N % 8 != 0 || N > 4096) return (int)hipErrorInvalidValue;
   if (rows == 0) return 0;
   const int G = piamd_layernorm_bwd_grid(rows);
+  if (dgamma) (void)hipMemsetAsync(part_dg, 0, sizeof(float) * N, stream);
+  if (dbeta) (void)hipMemsetAsync(part_db, 0, sizeof(float) * N, stream);
+  if (dbias) (void)hipMemsetAsync(part_dbias, 0, sizeof(float) * N, stream);
   int e = dtype ? launch_bwd<true>(dy, h, gamma, mean, rstd, dres_in, dres, dx,
                                    dgamma ? part_dg : nullptr, dbeta ? part_db : nullptr,
                                    dbias ? part_dbias : nullptr, G, rows, N, p_drop, seed, offset,
@@ -357,10 +358,10 @@ PIAMD_EXPORT int piamd_layernorm_bwd(int dtype, const void* dy, const void* h, c
     if (!outs[q]) continue;
     dim3 grid((N + 63) / 64), block(256);
     if (dtype)
-      hipLaunchKernelGGL((col_sum_kernel<true>), grid, block, 0, stream, parts[q], G, N,
+      hipLaunchKernelGGL((col_sum_kernel<true>), grid, block, 0, stream, parts[q], 1, N,
                          (bf16_t*)outs[q], (float*)nullptr, 0);
     else
-      hipLaunchKernelGGL((col_sum_kernel<false>), grid, block, 0, stream, parts[q], G, N,
+      hipLaunchKernelGGL((col_sum_kernel<false>), grid, block, 0, stream, parts[q], 1, N,
                          (float*)outs[q], (float*)nullptr, 0);
   }
   return (int)hipGetLastError();

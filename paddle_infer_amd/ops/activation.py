@@ -53,7 +53,7 @@ class _BiasActFn(torch.autograd.Function):
         part = None
         if need_b:
             G = _lib.lib().piamd_bias_act_bwd_grid(rows)
-            part = torch.empty((G, N), device=h.device, dtype=torch.float32)
+            part = torch.empty((N,), device=h.device, dtype=torch.float32)
         # pre-activation already includes the bias: pass bias=None to the backward
         _lib.call("piamd_bias_act_bwd", ctx.act, dy.data_ptr(), h.data_ptr(), None, dx.data_ptr(),
                   _lib.ptr(db), _lib.ptr(part), rows, N, _lib.stream())

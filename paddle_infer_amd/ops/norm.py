@@ -44,7 +44,7 @@ class _LayerNormFn(torch.autograd.Function):
         G = _lib.lib().piamd_layernorm_bwd_grid(rows)
         need_w = weight is not None and ctx.needs_input_grad[1]
         need_b = ctx.has_bias and ctx.needs_input_grad[2]
-        part = torch.empty((2, G, N), device=x2.device, dtype=torch.float32)
+        part = torch.empty((2, N), device=x2.device, dtype=torch.float32)
         dw = torch.empty_like(weight) if need_w else None
         db = torch.empty(N, device=x2.device, dtype=weight.dtype if weight is not None else x2.dtype) if need_b else None
         _lib.call("piamd_layernorm_bwd", _lib.dtype_code(x2), dy2.data_ptr(), x2.data_ptr(),
@@ -101,7 +101,7 @@ class _FusedAddLNFn(torch.autograd.Function):
         need_w = weight is not None and ctx.needs_input_grad[2]
         need_b = has_b and ctx.needs_input_grad[3]
         need_xb = has_xb and ctx.needs_input_grad[4]
-        part = torch.empty((3, G, N), device=h.device, dtype=torch.float32)
+        part = torch.empty((3, N), device=h.device, dtype=torch.float32)
         dw = torch.empty_like(weight) if need_w else None
         db = torch.empty(N, device=h.device, dtype=weight.dtype if weight is not None else h.dtype) if need_b else None
         dxb = torch.empty(N, device=h.device, dtype=h.dtype) if need_xb else None

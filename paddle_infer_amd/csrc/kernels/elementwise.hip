@@ -67,11 +67,11 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const bf16_t* __restr
                                                           float* __restrict__ part, int rows,
                                                           int N) {
   const int c8 = blockIdx.y * 256 + threadIdx.x;  // 8-column group index
-  if (c8 * 8 >= N) return;
+  const bool colok = c8 * 8 < N;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   u16x8 b;
-  if (bias) b = reinterpret_cast<const u16x8*>(bias)[c8];
-  for (int r = blockIdx.x; r < rows; r += gridDim.x) {
+  if (bias && colok) b = reinterpret_cast<const u16x8*>(bias)[c8];
+  for (int r = blockIdx.x; colok && r < rows; r += gridDim.x) {
     const size_t idx = ((size_t)r * N >> 3) + c8;
     u16x8 d = reinterpret_cast<const u16x8*>(dy)[idx];
     u16x8 hv = reinterpret_cast<const u16x8*>(h)[idx];
@@ -86,14 +86,25 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const bf16_t* __restr
     }
     reinterpret_cast<u16x8*>(dx)[idx] = o;
   }
-  if (part) {  // one f32 atomic per column per row-group block into part[N] (zeroed by launcher)
+  if (part) {
+    // transpose the per-thread 8-column sums through LDS so every atomic wave-instruction adds
+    // 64 consecutive floats (256 contiguous bytes: the full-rate atomic shape)
+    __shared__ float red[2048];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) atomicAdd(part + c8 * 8 + j, acc[j]);
+    for (int j = 0; j < 8; ++j) red[threadIdx.x * 8 + j] = acc[j];
+    __syncthreads();
+    const int col0 = blockIdx.y * 2048;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int cc = threadIdx.x + 256 * j;
+      if (col0 + cc < N) atomicAdd(part + col0 + cc, red[cc]);
+    }
   }
 }
 
 __global__ __launch_bounds__(256) void colsum_bf16_kernel(const float* __restrict__ part, int G,
-                                                         int N, bf16_t* __restrict__ out) {
+                                                         int N, bf16_t* __restrict__ out,
+                                                         int accumulate) {
   const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + cl;
   float s = 0.f;
@@ -102,7 +113,11 @@ __global__ __launch_bounds__(256) void colsum_bf16_kernel(const float* __restric
   __shared__ float red[4][64];
   red[rg][cl] = s;
   __syncthreads();
-  if (rg == 0 && col < N) out[col] = f2bf(red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl]);
+  if (rg == 0 && col < N) {
+    float t = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+    if (accumulate) t += bf2f(out[col]);
+    out[col] = f2bf(t);
+  }
 }
 
 // Row softmax with optional additive mask (broadcast over rows: mask row index = row % mask_rows)
@@ -248,7 +263,7 @@ PIAMD_EXPORT int piamd_bias_act_bwd_grid(int rows) {
 // part: f32 [N] workspace (zeroed here) — needed when dbias != null.
 PIAMD_EXPORT int piamd_bias_act_bwd(int act, const void* dy, const void* h, const void* bias,
                                     void* dx, void* dbias, float* part, int rows, int N,
-                                    hipStream_t stream) {
+                                    int accumulate, hipStream_t stream) {
   if (rows == 0) return 0;
   if (N % 8) return (int)hipErrorInvalidValue;
   const int G = piamd_bias_act_bwd_grid(rows);
@@ -264,7 +279,7 @@ PIAMD_EXPORT int piamd_bias_act_bwd(int act, const void* dy, const void* h, cons
 #undef BAB
   if (dbias)
     hipLaunchKernelGGL(colsum_bf16_kernel, dim3((N + 63) / 64), dim3(256), 0, stream, part, 1, N,
-                       (bf16_t*)dbias);
+                       (bf16_t*)dbias, accumulate);
   return (int)hipGetLastError();
 }
 

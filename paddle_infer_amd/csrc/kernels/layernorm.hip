@@ -336,7 +336,7 @@ PIAMD_EXPORT int piamd_layernorm_bwd(int dtype, const void* dy, const void* h, c
                                      void* dres, void* dx, void* dgamma, void* dbeta, void* dbias,
                                      float* part_dg, float* part_db, float* part_dbias, int rows,
                                      int N, float p_drop, uint64_t seed, uint64_t offset,
-                                     hipStream_t stream) {
+                                     int accum_mask, hipStream_t stream) {
   if (N % 8 != 0 || N > 4096) return (int)hipErrorInvalidValue;
   if (rows == 0) return 0;
   const int G = piamd_layernorm_bwd_grid(rows);
@@ -357,12 +357,13 @@ PIAMD_EXPORT int piamd_layernorm_bwd(int dtype, const void* dy, const void* h, c
   for (int q = 0; q < 3; ++q) {
     if (!outs[q]) continue;
     dim3 grid((N + 63) / 64), block(256);
+    const int acc = (accum_mask >> q) & 1;  // add into an existing grad (e.g. a flat main_grad view)
     if (dtype)
       hipLaunchKernelGGL((col_sum_kernel<true>), grid, block, 0, stream, parts[q], 1, N,
-                         (bf16_t*)outs[q], (float*)nullptr, 0);
+                         (bf16_t*)outs[q], (float*)nullptr, acc);
     else
       hipLaunchKernelGGL((col_sum_kernel<false>), grid, block, 0, stream, parts[q], 1, N,
-                         (float*)outs[q], (float*)nullptr, 0);
+                         (float*)outs[q], (float*)nullptr, acc);
   }
   return (int)hipGetLastError();
 }

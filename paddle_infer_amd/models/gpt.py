@@ -222,7 +222,7 @@ class GPTModel(Layer):
     def forward(self, input_ids, position_ids=None):
         emb = self.embeddings(input_ids, position_ids)
         p = self.cfg.hidden_dropout_prob if self.training else 0.0
-        h = torch.zeros_like(emb)  # residual stream starts at 0: h0 = dropout(emb)
+        h = None  # residual stream starts empty: h0 = dropout(emb)
         out, bias = emb, None
         for layer in self.layers:
             if self.cfg.recompute and self.training:

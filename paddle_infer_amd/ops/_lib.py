@@ -33,7 +33,7 @@ _SIGS = {
     "piamd_layernorm_bwd_grid": [c_int],
     "piamd_layernorm_bwd": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                            c_void_p, c_int, c_int, c_float, c_u64, c_u64, c_void_p],
+                            c_void_p, c_int, c_int, c_float, c_u64, c_u64, c_int, c_void_p],
     "piamd_colsum": [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "piamd_adamw_flat": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_ll, c_float,
                          c_void_p, c_float, c_float, c_float, c_float, c_float, c_float, c_void_p,
@@ -48,7 +48,7 @@ _SIGS = {
     "piamd_bias_act_fwd": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p],
     "piamd_bias_act_bwd_grid": [c_int],
     "piamd_bias_act_bwd": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                           c_int, c_int, c_void_p],
+                           c_int, c_int, c_int, c_void_p],
     "piamd_softmax_fwd": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_float,
                           c_void_p],
     "piamd_softmax_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p],
@@ -135,3 +135,15 @@ def dtype_code(t: torch.Tensor) -> int:
     if t.dtype == torch.float32:
         return 0
     raise TypeError(f"unsupported dtype {t.dtype} for HIP kernel (bf16/f32 only)")
+
+
+def main_grad(p):
+    """The flat-buffer gradient view of a parameter (set by the training engine), else None."""
+    return None if p is None else getattr(p, "main_grad", None)
+
+
+def fire(p):
+    """Signal the engine that ``p``'s gradient is complete (bucketed collective trigger)."""
+    hook = getattr(p, "_grad_ready", None)
+    if hook is not None:
+        hook(p)

@@ -39,6 +39,7 @@ class _BiasActFn(torch.autograd.Function):
         ctx.save_for_backward(x2 if pre is None else pre)
         ctx.act = act
         ctx.has_bias = bias is not None
+        ctx.bias_param = bias
         return y
 
     @staticmethod
@@ -49,14 +50,20 @@ class _BiasActFn(torch.autograd.Function):
         dy = dy.contiguous()
         dx = torch.empty_like(h)
         need_b = ctx.has_bias and ctx.needs_input_grad[1]
-        db = torch.empty(N, device=h.device, dtype=h.dtype) if need_b else None
-        part = None
+        db, part, acc = None, None, 0
         if need_b:
-            G = _lib.lib().piamd_bias_act_bwd_grid(rows)
+            mg = _lib.main_grad(ctx.bias_param)
+            if mg is not None:  # add straight into the engine's flat gradient view
+                db, acc = mg.view(-1), 1
+            else:
+                db = torch.empty(N, device=h.device, dtype=h.dtype)
             part = torch.empty((N,), device=h.device, dtype=torch.float32)
         # pre-activation already includes the bias: pass bias=None to the backward
         _lib.call("piamd_bias_act_bwd", ctx.act, dy.data_ptr(), h.data_ptr(), None, dx.data_ptr(),
-                  _lib.ptr(db), _lib.ptr(part), rows, N, _lib.stream())
+                  _lib.ptr(db), _lib.ptr(part), rows, N, acc, _lib.stream())
+        if acc:
+            _lib.fire(ctx.bias_param)
+            db = None
         return dx, db, None
 
 

@@ -32,6 +32,7 @@ class _LinearFn(torch.autograd.Function):
             y = torch.mm(x2, w)
         ctx.save_for_backward(x2, w)
         ctx.has_b = b is not None
+        ctx.bias = b
         ctx.shp = shp
         return y.view(*shp[:-1], w.shape[1])
 
@@ -51,8 +52,24 @@ class _LinearFn(torch.autograd.Function):
             else:
                 dw = torch.mm(x2.t(), dy2)
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = dy2.sum(0)
+            b = ctx.bias
+            bmg = getattr(b, "main_grad", None)
+            if bmg is not None and dy2.is_cuda and dy2.dtype == bmg.dtype:
+                colsum_into(dy2, bmg, accumulate=True)
+                _fire(b)
+            else:
+                db = dy2.sum(0)
         return dx, dw, db
+
+
+def colsum_into(x2, out, accumulate=True):
+    """out[N] (+)= Σ_rows x2[rows, N] via the HIP column-sum kernel (bias gradients)."""
+    from . import _lib
+    rows, N = x2.shape
+    G = 64
+    part = torch.empty((G, N), device=x2.device, dtype=torch.float32)
+    _lib.call("piamd_colsum", _lib.dtype_code(x2), x2.data_ptr(), out.data_ptr(), part.data_ptr(),
+              G, rows, N, int(accumulate), _lib.stream())
 
 
 def linear(x, weight, bias=None):

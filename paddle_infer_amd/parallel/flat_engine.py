@@ -174,21 +174,14 @@ class FlatTrainer:
             o += L
 
     def _install_grads(self):
-        linear_weights = set()
-        for m in self.model.modules():
-            # weights used through ops.linear / the LM head get main_grad accumulation
-            for name in ("weight",):
-                w = getattr(m, name, None)
-                if isinstance(w, torch.nn.Parameter) and w.dim() == 2:
-                    linear_weights.add(id(w))
+        """Every parameter gets ``main_grad`` (custom HIP ops / GEMM backward accumulate straight
+        into it and fire the ready hook themselves) and ``.grad`` aliased to the same view (torch
+        ops accumulate there through AccumulateGrad, whose post-hook fires the ready hook)."""
         for g in self.groups:
             for p in g.params:
                 view = g.grad_view(p)
-                if id(p) in linear_weights:
-                    p.main_grad = view
-                    p.grad = view  # embedding lookups still accumulate here through autograd
-                else:
-                    p.grad = view
+                p.main_grad = view
+                p.grad = view
                 p._grad_ready = self._make_ready(g)
                 if not hasattr(p, "_piamd_hooked"):
                     p.register_post_accumulate_grad_hook(lambda t: t._grad_ready(t))

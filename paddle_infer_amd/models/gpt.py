@@ -286,3 +286,52 @@ def gpt_flops_per_token(cfg: GPTConfig, seq_len: int) -> float:
     h, L, V = cfg.hidden_size, cfg.num_layers, cfg.vocab_size
     per_layer = 2 * (3 * h * h + h * h + 2 * h * cfg.ffn) + 2 * 2 * seq_len * h / 2  # causal attn
     return 3 * (L * per_layer + 2 * h * V)
+
+
+# ---------------------------------------------------------------------------------------------
+# Tensor-parallel checkpoint conversion (full <-> per-rank shards)
+# ---------------------------------------------------------------------------------------------
+def _qkv_cols(cfg: GPTConfig):
+    hk = cfg.num_kv_heads or cfg.num_heads
+    D = cfg.head_dim
+    return cfg.num_heads * D, hk * D
+
+
+def shard_gpt_state_dict(full: dict, cfg: GPTConfig, rank: int, world: int) -> dict:
+    """Slice a full (single-device) GPT state dict into tensor-parallel rank ``rank``'s shard.
+    QKV columns are regrouped per rank as [q_heads_r | k_heads_r | v_heads_r]."""
+    out = {}
+    qc, kc = _qkv_cols(cfg)
+    for k, v in full.items():
+        if k.endswith("qkv_proj.weight") or k.endswith("qkv_proj.bias"):
+            q, kk, vv = v.split([qc, kc, kc], dim=-1)
+            out[k] = torch.cat([t.chunk(world, dim=-1)[rank] for t in (q, kk, vv)], dim=-1).clone()
+        elif k.endswith("fc1.weight") or k.endswith("fc1.bias"):
+            out[k] = v.chunk(world, dim=-1)[rank].clone()
+        elif k.endswith("out_proj.weight") or k.endswith("fc2.weight"):
+            out[k] = v.chunk(world, dim=0)[rank].clone()
+        elif k.endswith("word_embeddings.weight") or k == "lm_head":
+            out[k] = v.chunk(world, dim=0)[rank].clone()
+        else:
+            out[k] = v.clone()
+    return out
+
+
+def merge_gpt_state_dicts(shards: list, cfg: GPTConfig) -> dict:
+    """Inverse of :func:`shard_gpt_state_dict`."""
+    world = len(shards)
+    qc, kc = _qkv_cols(cfg)
+    out = {}
+    for k in shards[0]:
+        vs = [s[k] for s in shards]
+        if k.endswith("qkv_proj.weight") or k.endswith("qkv_proj.bias"):
+            parts = [v.split([qc // world, kc // world, kc // world], dim=-1) for v in vs]
+            out[k] = torch.cat([torch.cat([p[i] for p in parts], dim=-1) for i in range(3)], dim=-1)
+        elif k.endswith("fc1.weight") or k.endswith("fc1.bias"):
+            out[k] = torch.cat(vs, dim=-1)
+        elif k.endswith("out_proj.weight") or k.endswith("fc2.weight") or \
+                k.endswith("word_embeddings.weight") or k == "lm_head":
+            out[k] = torch.cat(vs, dim=0)
+        else:
+            out[k] = vs[0]
+    return out

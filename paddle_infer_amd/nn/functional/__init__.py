@@ -1,0 +1,470 @@
+"""``paddle.nn.functional`` (reference `python/paddle/nn/functional/*.py`).
+
+Hot ops route to the framework's HIP kernels on GPU (layer_norm, gelu/silu/relu with bias,
+dropout, softmax-with-mask, flash attention, softmax cross entropy); library ops (conv, pooling,
+batch norm, interpolation) go through PyTorch-ROCm (MIOpen / rocBLAS).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as TF
+
+from ... import ops as _ops
+from ...framework.dtype import to_torch_dtype as _dt
+
+# ------------------------------------------------------------------------------- activations
+relu = lambda x, name=None: TF.relu(x)  # noqa: E731
+relu_ = lambda x, name=None: TF.relu_(x)  # noqa: E731
+relu6 = lambda x, name=None: TF.relu6(x)  # noqa: E731
+elu = lambda x, alpha=1.0, name=None: TF.elu(x, alpha)  # noqa: E731
+selu = lambda x, scale=1.0507009873554804934193349852946, alpha=1.6732632423543772848170429916717, name=None: scale * TF.elu(x, alpha)  # noqa: E731
+celu = lambda x, alpha=1.0, name=None: TF.celu(x, alpha)  # noqa: E731
+leaky_relu = lambda x, negative_slope=0.01, name=None: TF.leaky_relu(x, negative_slope)  # noqa: E731
+prelu = lambda x, weight, data_format="NCHW", name=None: TF.prelu(x, weight)  # noqa: E731
+sigmoid = lambda x, name=None: torch.sigmoid(x)  # noqa: E731
+hardsigmoid = lambda x, slope=0.1666667, offset=0.5, name=None: torch.clamp(x * slope + offset, 0, 1)  # noqa: E731
+hardswish = lambda x, name=None: TF.hardswish(x)  # noqa: E731
+hardtanh = lambda x, min=-1.0, max=1.0, name=None: TF.hardtanh(x, min, max)  # noqa: E731
+hardshrink = lambda x, threshold=0.5, name=None: TF.hardshrink(x, threshold)  # noqa: E731
+softshrink = lambda x, threshold=0.5, name=None: TF.softshrink(x, threshold)  # noqa: E731
+tanhshrink = lambda x, name=None: TF.tanhshrink(x)  # noqa: E731
+tanh = lambda x, name=None: torch.tanh(x)  # noqa: E731
+softplus = lambda x, beta=1, threshold=20, name=None: TF.softplus(x, beta, threshold)  # noqa: E731
+softsign = lambda x, name=None: TF.softsign(x)  # noqa: E731
+mish = lambda x, name=None: TF.mish(x)  # noqa: E731
+log_sigmoid = lambda x, name=None: TF.logsigmoid(x)  # noqa: E731
+thresholded_relu = lambda x, threshold=1.0, name=None: torch.where(x > threshold, x, torch.zeros_like(x))  # noqa: E731
+glu = lambda x, axis=-1, name=None: TF.glu(x, axis)  # noqa: E731
+maxout = lambda x, groups, axis=1, name=None: x.reshape(*x.shape[:axis], groups, x.shape[axis] // groups, *x.shape[axis + 1:]).max(axis + 1).values  # noqa: E731
+
+
+def gelu(x, approximate=False, name=None):
+    return _ops.gelu(x, approximate)
+
+
+def silu(x, name=None):
+    return _ops.bias_act(x, None, "silu")
+
+
+swish = silu
+
+
+def softmax(x, axis=-1, dtype=None, name=None):
+    if dtype is not None:
+        x = x.to(_dt(dtype))
+    if axis in (-1, x.dim() - 1) and x.is_cuda and x.dtype == torch.bfloat16:
+        return _ops.fused_softmax_mask(x)
+    return torch.softmax(x, axis)
+
+
+def log_softmax(x, axis=-1, dtype=None, name=None):
+    if dtype is not None:
+        x = x.to(_dt(dtype))
+    return torch.log_softmax(x, axis)
+
+
+def gumbel_softmax(x, temperature=1.0, hard=False, axis=-1, name=None):
+    return TF.gumbel_softmax(x, temperature, hard, dim=axis)
+
+
+# ------------------------------------------------------------------------------- common
+def linear(x, weight, bias=None, name=None):
+    """Paddle layout: weight ``[in_features, out_features]``."""
+    from ...ops.linear import linear as _lin
+    return _lin(x, weight, bias)
+
+
+def dropout(x, p=0.5, axis=None, training=True, mode="upscale_in_train", name=None):
+    if not training or p == 0.0:
+        return x if mode == "upscale_in_train" else x * (1.0 - p)
+    if axis is not None:
+        shape = [x.shape[i] if i in ([axis] if isinstance(axis, int) else axis) else 1 for i in range(x.dim())]
+        mask = (torch.rand(shape, device=x.device) >= p).to(x.dtype)
+        return x * mask / (1 - p) if mode == "upscale_in_train" else x * mask
+    if mode == "upscale_in_train":
+        return _ops.dropout(x, p, training=True)
+    return x * (torch.rand_like(x, dtype=torch.float32) >= p).to(x.dtype)
+
+
+def dropout2d(x, p=0.5, training=True, data_format="NCHW", name=None):
+    return TF.dropout2d(x, p, training)
+
+
+def dropout3d(x, p=0.5, training=True, data_format="NCDHW", name=None):
+    return TF.dropout3d(x, p, training)
+
+
+def alpha_dropout(x, p=0.5, training=True, name=None):
+    return TF.alpha_dropout(x, p, training)
+
+
+def embedding(x, weight, padding_idx=None, sparse=False, name=None):
+    return TF.embedding(x, weight, padding_idx)
+
+
+def one_hot(x, num_classes, name=None):
+    return TF.one_hot(x.long(), num_classes).float()
+
+
+def pad(x, pad, mode="constant", value=0.0, data_format="NCHW", name=None):
+    if isinstance(pad, torch.Tensor):
+        pad = pad.tolist()
+    pad = list(pad)
+    nd = x.dim()
+    if len(pad) == 2 * nd:  # Paddle full-rank form: [d0_lo, d0_hi, d1_lo, ...] (first dim first)
+        tp = []
+        for i in reversed(range(nd)):
+            tp += [pad[2 * i], pad[2 * i + 1]]
+        pad = tp
+    elif data_format in ("NHWC", "NLC", "NDHWC"):
+        x = x.movedim(-1, 1)
+        out = TF.pad(x, pad, mode if mode != "edge" else "replicate", value)
+        return out.movedim(1, -1)
+    return TF.pad(x, pad, {"edge": "replicate"}.get(mode, mode), value)
+
+
+def interpolate(x, size=None, scale_factor=None, mode="nearest", align_corners=False,
+                align_mode=0, data_format="NCHW", name=None):
+    mode = {"bilinear": "bilinear", "nearest": "nearest", "bicubic": "bicubic", "linear": "linear",
+            "trilinear": "trilinear", "area": "area"}[mode.lower()]
+    ac = align_corners if mode in ("bilinear", "bicubic", "linear", "trilinear") else None
+    return TF.interpolate(x, size, scale_factor, mode, align_corners=ac)
+
+
+upsample = interpolate
+
+
+def pixel_shuffle(x, upscale_factor, data_format="NCHW", name=None):
+    return TF.pixel_shuffle(x, upscale_factor)
+
+
+def unfold(x, kernel_sizes, strides=1, paddings=0, dilations=1, name=None):
+    return TF.unfold(x, kernel_sizes, dilations, paddings, strides)
+
+
+def cosine_similarity(x1, x2, axis=1, eps=1e-8):
+    return TF.cosine_similarity(x1, x2, axis, eps)
+
+
+def normalize(x, p=2, axis=1, epsilon=1e-12, name=None):
+    return TF.normalize(x, p, axis, epsilon)
+
+
+def label_smooth(label, prior_dist=None, epsilon=0.1, name=None):
+    k = label.shape[-1]
+    prior = prior_dist if prior_dist is not None else torch.full_like(label, 1.0 / k)
+    return (1 - epsilon) * label + epsilon * prior
+
+
+# ------------------------------------------------------------------------------- conv / pool
+def _fmt_in(x, data_format):
+    return x.movedim(-1, 1) if data_format in ("NHWC", "NLC", "NDHWC") else x
+
+
+def _fmt_out(y, data_format):
+    return y.movedim(1, -1) if data_format in ("NHWC", "NLC", "NDHWC") else y
+
+
+def _padding(padding, nd):
+    if isinstance(padding, str):
+        return padding.lower()
+    if isinstance(padding, int):
+        return padding
+    padding = list(padding)
+    if len(padding) == nd:
+        return tuple(padding)
+    if len(padding) == 2 * nd:
+        if all(padding[2 * i] == padding[2 * i + 1] for i in range(nd)):
+            return tuple(padding[0::2])
+    raise ValueError(f"unsupported asymmetric padding {padding}")
+
+
+def conv1d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NCL", name=None):
+    return _fmt_out(TF.conv1d(_fmt_in(x, data_format), weight, bias, stride, _padding(padding, 1), dilation, groups), data_format)
+
+
+def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NCHW", name=None):
+    return _fmt_out(TF.conv2d(_fmt_in(x, data_format), weight, bias, stride, _padding(padding, 2), dilation, groups), data_format)
+
+
+def conv3d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NCDHW", name=None):
+    return _fmt_out(TF.conv3d(_fmt_in(x, data_format), weight, bias, stride, _padding(padding, 3), dilation, groups), data_format)
+
+
+def conv2d_transpose(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1,
+                     dilation=1, data_format="NCHW", output_size=None, name=None):
+    return _fmt_out(TF.conv_transpose2d(_fmt_in(x, data_format), weight, bias, stride, _padding(padding, 2), output_padding, groups, dilation), data_format)
+
+
+def conv1d_transpose(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1,
+                     dilation=1, output_size=None, data_format="NCL", name=None):
+    return _fmt_out(TF.conv_transpose1d(_fmt_in(x, data_format), weight, bias, stride, _padding(padding, 1), output_padding, groups, dilation), data_format)
+
+
+def max_pool1d(x, kernel_size, stride=None, padding=0, return_mask=False, ceil_mode=False, name=None):
+    return TF.max_pool1d(x, kernel_size, stride, _padding(padding, 1), 1, ceil_mode, return_mask)
+
+
+def max_pool2d(x, kernel_size, stride=None, padding=0, return_mask=False, ceil_mode=False,
+               data_format="NCHW", name=None):
+    y = TF.max_pool2d(_fmt_in(x, data_format), kernel_size, stride, _padding(padding, 2), 1, ceil_mode, return_mask)
+    return y if return_mask else _fmt_out(y, data_format)
+
+
+def max_pool3d(x, kernel_size, stride=None, padding=0, return_mask=False, ceil_mode=False,
+               data_format="NCDHW", name=None):
+    return TF.max_pool3d(x, kernel_size, stride, _padding(padding, 3), 1, ceil_mode, return_mask)
+
+
+def avg_pool1d(x, kernel_size, stride=None, padding=0, exclusive=True, ceil_mode=False, name=None):
+    return TF.avg_pool1d(x, kernel_size, stride, _padding(padding, 1), ceil_mode, not exclusive)
+
+
+def avg_pool2d(x, kernel_size, stride=None, padding=0, ceil_mode=False, exclusive=True,
+               divisor_override=None, data_format="NCHW", name=None):
+    return _fmt_out(TF.avg_pool2d(_fmt_in(x, data_format), kernel_size, stride, _padding(padding, 2), ceil_mode, not exclusive, divisor_override), data_format)
+
+
+def avg_pool3d(x, kernel_size, stride=None, padding=0, ceil_mode=False, exclusive=True,
+               divisor_override=None, data_format="NCDHW", name=None):
+    return TF.avg_pool3d(x, kernel_size, stride, _padding(padding, 3), ceil_mode, not exclusive, divisor_override)
+
+
+def adaptive_avg_pool1d(x, output_size, name=None):
+    return TF.adaptive_avg_pool1d(x, output_size)
+
+
+def adaptive_avg_pool2d(x, output_size, data_format="NCHW", name=None):
+    return _fmt_out(TF.adaptive_avg_pool2d(_fmt_in(x, data_format), output_size), data_format)
+
+
+def adaptive_avg_pool3d(x, output_size, data_format="NCDHW", name=None):
+    return TF.adaptive_avg_pool3d(x, output_size)
+
+
+def adaptive_max_pool1d(x, output_size, return_mask=False, name=None):
+    return TF.adaptive_max_pool1d(x, output_size, return_mask)
+
+
+def adaptive_max_pool2d(x, output_size, return_mask=False, name=None):
+    return TF.adaptive_max_pool2d(x, output_size, return_mask)
+
+
+# ------------------------------------------------------------------------------- normalization
+def layer_norm(x, normalized_shape, weight=None, bias=None, epsilon=1e-5, name=None):
+    ns = [normalized_shape] if isinstance(normalized_shape, int) else list(normalized_shape)
+    if len(ns) == 1:
+        return _ops.layer_norm(x, weight, bias, epsilon)
+    return TF.layer_norm(x, ns, weight, bias, epsilon)
+
+
+def rms_norm(x, weight=None, epsilon=1e-6, name=None):
+    return _ops.rms_norm(x, weight, epsilon)
+
+
+def batch_norm(x, running_mean, running_var, weight=None, bias=None, training=False,
+               momentum=0.9, epsilon=1e-5, data_format="NCHW", use_global_stats=None, name=None):
+    if use_global_stats:
+        training = False
+    y = TF.batch_norm(_fmt_in(x, data_format), running_mean, running_var, weight, bias, training,
+                      1.0 - momentum, epsilon)
+    return _fmt_out(y, data_format)
+
+
+def instance_norm(x, running_mean=None, running_var=None, weight=None, bias=None,
+                  use_input_stats=True, momentum=0.9, eps=1e-5, data_format="NCHW", name=None):
+    return TF.instance_norm(x, running_mean, running_var, weight, bias, use_input_stats, 1 - momentum, eps)
+
+
+def group_norm(x, num_groups, epsilon=1e-5, weight=None, bias=None, data_format="NCHW", name=None):
+    return _fmt_out(TF.group_norm(_fmt_in(x, data_format), num_groups, weight, bias, epsilon), data_format)
+
+
+def local_response_norm(x, size, alpha=1e-4, beta=0.75, k=1.0, data_format="NCHW", name=None):
+    return TF.local_response_norm(x, size, alpha, beta, k)
+
+
+# ------------------------------------------------------------------------------- losses
+def _reduce(loss, reduction):
+    if reduction == "mean":
+        return loss.mean()
+    if reduction == "sum":
+        return loss.sum()
+    return loss
+
+
+def cross_entropy(input, label, weight=None, ignore_index=-100, reduction="mean", soft_label=False,  # noqa: A002
+                  axis=-1, use_softmax=True, label_smoothing=0.0, name=None):
+    if axis not in (-1, input.dim() - 1):
+        input = input.movedim(axis, -1)
+        label = label.movedim(axis, -1) if soft_label else label
+    V = input.shape[-1]
+    if soft_label:
+        logp = torch.log_softmax(input.float(), -1) if use_softmax else torch.log(input.float())
+        loss = -(label.float() * logp).sum(-1)
+        if weight is not None:
+            loss = loss * (label.float() * weight).sum(-1)
+        return _reduce(loss, reduction)
+    lab = label.squeeze(-1) if label.dim() == input.dim() else label
+    if not use_softmax:
+        loss = TF.nll_loss(torch.log(input.float()).reshape(-1, V), lab.reshape(-1).long(),
+                           weight, ignore_index=ignore_index, reduction="none").view(lab.shape)
+    elif weight is None and label_smoothing == 0.0:
+        loss = _ops.softmax_cross_entropy(input, lab, ignore_index).float()
+    else:
+        loss = TF.cross_entropy(input.float().reshape(-1, V), lab.reshape(-1).long(), weight,
+                                ignore_index=ignore_index, reduction="none",
+                                label_smoothing=label_smoothing).view(lab.shape)
+    if reduction == "mean":
+        if weight is not None:
+            w = weight[lab.clamp(min=0).long()] * (lab != ignore_index)
+            return loss.sum() / w.sum()
+        valid = (lab != ignore_index).sum().clamp(min=1)
+        return loss.sum() / valid
+    out = _reduce(loss, reduction)
+    return out.unsqueeze(-1) if reduction == "none" and label.dim() == input.dim() else out
+
+
+def softmax_with_cross_entropy(logits, label, soft_label=False, ignore_index=-100,
+                               numeric_stable_mode=True, return_softmax=False, axis=-1):
+    loss = cross_entropy(logits, label, ignore_index=ignore_index, reduction="none",
+                         soft_label=soft_label, axis=axis)
+    if loss.dim() < logits.dim():
+        loss = loss.unsqueeze(axis)
+    if return_softmax:
+        return loss, torch.softmax(logits, axis)
+    return loss
+
+
+def nll_loss(input, label, weight=None, ignore_index=-100, reduction="mean", name=None):  # noqa: A002
+    return TF.nll_loss(input, label.long(), weight, ignore_index=ignore_index, reduction=reduction)
+
+
+def mse_loss(input, label, reduction="mean", name=None):  # noqa: A002
+    return TF.mse_loss(input, label, reduction=reduction)
+
+
+def l1_loss(input, label, reduction="mean", name=None):  # noqa: A002
+    return TF.l1_loss(input, label, reduction=reduction)
+
+
+def smooth_l1_loss(input, label, reduction="mean", delta=1.0, name=None):  # noqa: A002
+    return TF.smooth_l1_loss(input, label, reduction=reduction, beta=delta) * delta
+
+
+def binary_cross_entropy(input, label, weight=None, reduction="mean", name=None):  # noqa: A002
+    return TF.binary_cross_entropy(input, label, weight, reduction=reduction)
+
+
+def binary_cross_entropy_with_logits(logit, label, weight=None, reduction="mean", pos_weight=None, name=None):
+    return TF.binary_cross_entropy_with_logits(logit, label, weight, reduction=reduction, pos_weight=pos_weight)
+
+
+def kl_div(input, label, reduction="mean", name=None):  # noqa: A002
+    return TF.kl_div(input, label, reduction=reduction)
+
+
+def margin_ranking_loss(input, other, label, margin=0.0, reduction="mean", name=None):  # noqa: A002
+    return TF.margin_ranking_loss(input, other, label, margin, reduction=reduction)
+
+
+def hinge_embedding_loss(input, label, margin=1.0, reduction="mean", name=None):  # noqa: A002
+    return TF.hinge_embedding_loss(input, label, margin, reduction=reduction)
+
+
+def cosine_embedding_loss(input1, input2, label, margin=0, reduction="mean", name=None):
+    return TF.cosine_embedding_loss(input1, input2, label, margin, reduction=reduction)
+
+
+def ctc_loss(log_probs, labels, input_lengths, label_lengths, blank=0, reduction="mean", norm_by_times=False):
+    return TF.ctc_loss(log_probs, labels, input_lengths, label_lengths, blank, reduction)
+
+
+def sigmoid_focal_loss(logit, label, normalizer=None, alpha=0.25, gamma=2.0, reduction="sum", name=None):
+    p = torch.sigmoid(logit)
+    ce = TF.binary_cross_entropy_with_logits(logit, label, reduction="none")
+    pt = p * label + (1 - p) * (1 - label)
+    loss = ce * (1 - pt) ** gamma
+    loss = (alpha * label + (1 - alpha) * (1 - label)) * loss
+    if normalizer is not None:
+        loss = loss / normalizer
+    return _reduce(loss, reduction)
+
+
+def triplet_margin_loss(input, positive, negative, margin=1.0, p=2, epsilon=1e-6, swap=False, reduction="mean", name=None):  # noqa: A002
+    return TF.triplet_margin_loss(input, positive, negative, margin=margin, p=p, eps=epsilon, swap=swap, reduction=reduction)
+
+
+def square_error_cost(input, label):  # noqa: A002
+    return (input - label) ** 2
+
+
+# ------------------------------------------------------------------------------- attention
+def flash_attention(query, key, value, dropout=0.0, causal=False, return_softmax=False,
+                    fixed_seed_offset=None, rng_name="", training=True, name=None):
+    """Reference `nn/functional/flash_attention.py:142` — [B, S, H, D] layout. Returns
+    ``(out, softmax)`` (softmax is None: never materialised)."""
+    if dropout > 0.0 and training:
+        raise NotImplementedError("attention dropout is not implemented in the MFMA kernel")
+    return _ops.flash_attention(query, key, value, causal=causal), None
+
+
+def flash_attn_unpadded(query, key, value, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k,
+                        scale, dropout=0.0, causal=False, return_softmax=False, training=True, name=None):
+    """Variable-length (packed) attention: q/k/v are [total_tokens, H, D] with cumulative
+    sequence offsets; each sequence runs through the MFMA kernel."""
+    outs = []
+    cq = cu_seqlens_q.tolist()
+    ck = cu_seqlens_k.tolist()
+    for i in range(len(cq) - 1):
+        q = query[cq[i]:cq[i + 1]].unsqueeze(0)
+        k = key[ck[i]:ck[i + 1]].unsqueeze(0)
+        v = value[ck[i]:ck[i + 1]].unsqueeze(0)
+        outs.append(_ops.flash_attention(q, k, v, causal=causal, scale=scale)[0])
+    return torch.cat(outs, 0), None
+
+
+def scaled_dot_product_attention(query, key, value, attn_mask=None, dropout_p=0.0,
+                                 is_causal=False, training=True, name=None):
+    """Reference `flash_attention.py:440`: [B, S, H, D] layout."""
+    if attn_mask is None and dropout_p == 0.0:
+        return _ops.flash_attention(query, key, value, causal=is_causal)
+    q, k, v = (t.transpose(1, 2) for t in (query, key, value))
+    o = TF.scaled_dot_product_attention(q, k, v, attn_mask, dropout_p if training else 0.0, is_causal)
+    return o.transpose(1, 2)
+
+
+def memory_efficient_attention(query, key, value, attn_bias=None, p=0.0, scale=None, training=True):
+    """The fork's `memory_efficient_attention` (cutlass) API: [B, S, H, D]."""
+    if attn_bias is None and p == 0.0:
+        return _ops.flash_attention(query, key, value, scale=scale)
+    return scaled_dot_product_attention(query, key, value, attn_bias, p, training=training)
+
+
+def sequence_mask(x, maxlen=None, dtype="int64", name=None):
+    maxlen = int(maxlen if maxlen is not None else x.max().item())
+    return (torch.arange(maxlen, device=x.device) < x.unsqueeze(-1)).to(_dt(dtype))
+
+
+def temporal_shift(x, seg_num, shift_ratio=0.25, name=None, data_format="NCHW"):
+    nt, c, h, w = x.shape
+    x = x.reshape(nt // seg_num, seg_num, c, h, w)
+    fold = int(c * shift_ratio)
+    out = torch.zeros_like(x)
+    out[:, :-1, :fold] = x[:, 1:, :fold]
+    out[:, 1:, fold:2 * fold] = x[:, :-1, fold:2 * fold]
+    out[:, :, 2 * fold:] = x[:, :, 2 * fold:]
+    return out.reshape(nt, c, h, w)
+
+
+def affine_grid(theta, out_shape, align_corners=True, name=None):
+    return TF.affine_grid(theta, list(out_shape), align_corners)
+
+
+def grid_sample(x, grid, mode="bilinear", padding_mode="zeros", align_corners=True, name=None):
+    return TF.grid_sample(x, grid, mode, padding_mode, align_corners)
+
+
+math  # noqa

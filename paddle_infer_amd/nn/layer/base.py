@@ -110,11 +110,13 @@ class Layer(torch.nn.Module):
         return super().register_buffer(name, tensor, persistent=persistable)
 
     # ---- traversal ----------------------------------------------------------------------
-    def parameters(self, include_sublayers=True):
-        return list(super().parameters(recurse=include_sublayers))
+    def parameters(self, include_sublayers=True, recurse=None):
+        rec = include_sublayers if recurse is None else recurse
+        return list(super().parameters(recurse=rec))
 
-    def named_parameters(self, prefix="", include_sublayers=True, remove_duplicate=True):
-        return super().named_parameters(prefix=prefix, recurse=include_sublayers,
+    def named_parameters(self, prefix="", include_sublayers=True, remove_duplicate=True, recurse=None):
+        rec = include_sublayers if recurse is None else recurse
+        return super().named_parameters(prefix=prefix, recurse=rec,
                                         remove_duplicate=remove_duplicate)
 
     def sublayers(self, include_self=False):

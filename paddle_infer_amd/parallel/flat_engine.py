@@ -115,7 +115,7 @@ class FlatTrainer:
     def __init__(self, model, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
                  grad_clip=1.0, dp_group=None, mp_group=None, pp_group=None, sharding_stage=0,
                  bucket_mb=256, no_decay_fn=None, optimizer="adamw", momentum=0.9,
-                 overlap=True):
+                 overlap=True, named_params=None):
         self.model = model
         self.lr = lr
         self.beta1, self.beta2 = betas
@@ -132,30 +132,32 @@ class FlatTrainer:
         self.overlap = overlap
         self.step_count = 0
         no_decay_fn = no_decay_fn or (lambda n, p: p.dim() == 1)
-        named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+        src = named_params if named_params is not None else model.named_parameters()
+        named = [(n, p) for n, p in src if p.requires_grad]
         if not named:
             raise ValueError("model has no trainable parameters")
         device = named[0][1].device
         dtype = named[0][1].dtype
         keyed = {}
         for n, p in named:
-            k = (not no_decay_fn(n, p), bool(getattr(p, "is_distributed", False)))
+            k = (not no_decay_fn(n, p), bool(getattr(p, "is_distributed", False)), str(p.dtype))
             keyed.setdefault(k, []).append(p)
         bucket_numel = max(ALIGN * self.world, int(bucket_mb * 2 ** 20 // p.element_size()))
         self.groups = []
-        for (decay, distd), ps in sorted(keyed.items(), key=lambda kv: (not kv[0][0], kv[0][1])):
-            g = _FlatGroup(ps, dtype, device, self.world, bucket_numel,
-                           weight_decay if decay else 0.0, distd, f"decay{int(decay)}_dist{int(distd)}")
+        for (decay, distd, _dts), ps in sorted(keyed.items(), key=lambda kv: (not kv[0][0], kv[0][1], kv[0][2])):
+            g = _FlatGroup(ps, ps[0].dtype, device, self.world, bucket_numel,
+                           weight_decay if decay else 0.0, distd, f"decay{int(decay)}_dist{int(distd)}_{_dts.replace('torch.', '')}")
             self.groups.append(g)
         # master weights + states: full (stage 0) or local shard (stage >= 1)
         for g in self.groups:
             if self.sharding:
-                g.gshard = torch.zeros(g.shard_numel, dtype=dtype, device=device)
-                g.pshard = torch.zeros(g.shard_numel, dtype=dtype, device=device)
+                g.gshard = torch.zeros(g.shard_numel, dtype=g.flat.dtype, device=device)
+                g.pshard = torch.zeros(g.shard_numel, dtype=g.flat.dtype, device=device)
                 master = torch.empty(g.shard_numel, dtype=torch.float32, device=device)
                 self._gather_shard(g, g.flat, master)
             else:
-                master = g.flat.float()
+                # fp32 params: the flat buffer IS the master copy (no duplicate, no write-back)
+                master = g.flat if g.flat.dtype == torch.float32 else g.flat.float()
             g.master = master
             g.m = torch.zeros_like(master)
             g.v = torch.zeros_like(master) if optimizer == "adamw" else None
@@ -275,6 +277,11 @@ class FlatTrainer:
         for g in self.groups:
             grads = self._grads_for_update(g)
             model_out = g.pshard if self.sharding else g.flat
+            if model_out.data_ptr() == g.master.data_ptr():
+                model_out = None  # fp32 params updated in place
+            fp32_copy = model_out is not None and model_out.dtype == torch.float32
+            if fp32_copy:  # kernels emit a bf16 model copy only; fp32 shards are copied after
+                model_out, fp32_target = None, model_out
             if self.optimizer == "adamw":
                 adamw_flat(g.master, g.m, g.v, grads, lr, self.beta1, self.beta2, self.eps,
                            g.weight_decay, self.step_count, model=model_out, grad_scale=gscale,
@@ -284,6 +291,8 @@ class FlatTrainer:
                     grads = grads * static
                 momentum_flat(g.master, g.m, grads, lr, self.momentum, g.weight_decay,
                               model=model_out, grad_scale=gscale)
+            if fp32_copy:
+                fp32_target.copy_(g.master)
         if self.sharding:
             for g in self.groups:
                 o = 0

@@ -1,0 +1,31 @@
+"""``paddle.distributed`` (reference `python/paddle/distributed/__init__.py`)."""
+from .collective import (ReduceOp, Group, is_initialized, get_rank, get_world_size, new_group,  # noqa: F401
+                         get_group, destroy_process_group, all_reduce, broadcast, reduce,
+                         all_gather, all_gather_object, reduce_scatter, scatter, alltoall,
+                         alltoall_single, send, recv, isend, irecv, P2POp, batch_isend_irecv,
+                         barrier, wait, split)
+from .parallel import init_parallel_env, ParallelEnv, DataParallel, spawn  # noqa: F401
+from . import fleet  # noqa: F401
+from .fleet.topology import ParallelMode  # noqa: F401
+from .sharding import group_sharded_parallel, save_group_sharded_model  # noqa: F401
+
+
+def launch():
+    from .launch import main
+    main()
+
+
+def gloo_init_parallel_env(rank_id, rank_num, server_endpoint):
+    import os
+    os.environ.update({"RANK": str(rank_id), "WORLD_SIZE": str(rank_num)})
+    host, port = server_endpoint.split(":")
+    os.environ.update({"MASTER_ADDR": host, "MASTER_PORT": port})
+    return init_parallel_env(backend="gloo")
+
+
+def gloo_barrier():
+    barrier()
+
+
+def gloo_release():
+    destroy_process_group()

@@ -96,8 +96,9 @@ def _gather_last(x, group):
     if n == 1:
         return x
     x = x.contiguous()
-    out = torch.empty((n,) + tuple(x.shape), dtype=x.dtype, device=x.device)
-    dist.all_gather_into_tensor(out, x, group=group)
+    out = torch.empty(n * x.numel(), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, x.view(-1), group=group)
+    out = out.view((n,) + tuple(x.shape))
     return torch.cat(list(out.unbind(0)), dim=-1)
 
 

@@ -1,0 +1,207 @@
+"""paddle.distributed API on CPU gloo (world 2): collectives, DataParallel, 1F1B pipeline,
+group-sharded stage 3, fleet hybrid optimizer, recompute and the launcher watchdog."""
+import os
+import subprocess
+import sys
+import textwrap
+
+import numpy as np
+import pytest
+import torch
+
+from dist_utils import run_distributed
+
+
+def _collectives(rank, world):
+    import paddle_infer_amd.distributed as pd
+    x = torch.tensor([float(rank + 1)] * 4)
+    pd.all_reduce(x)
+    out = []
+    pd.all_gather(out, torch.tensor([rank]))
+    a2a = []
+    pd.alltoall([torch.tensor([rank * 10 + i]) for i in range(world)], a2a)
+    rs = torch.empty(2)
+    pd.reduce_scatter(rs, [torch.ones(2) * (rank + 1), torch.ones(2) * (rank + 1)])
+    objs = []
+    pd.all_gather_object(objs, {"r": rank})
+    return x.tolist(), [t.item() for t in out], [t.item() for t in a2a], rs.tolist(), objs
+
+
+def test_collectives():
+    res = run_distributed(_collectives, 2)
+    for r in range(2):
+        x, ag, a2a, rs, objs = res[r]
+        assert x == [3.0] * 4 and ag == [0, 1]
+        assert a2a == [0 * 10 + r, 1 * 10 + r]
+        assert rs == [3.0, 3.0] and objs == [{"r": 0}, {"r": 1}]
+
+
+def _mlp():
+    import paddle_infer_amd as paddle
+    torch.manual_seed(0)
+    return paddle.nn.Sequential(paddle.nn.Linear(8, 16), paddle.nn.ReLU(), paddle.nn.Linear(16, 16),
+                                paddle.nn.ReLU(), paddle.nn.Linear(16, 4))
+
+
+def _data():
+    g = torch.Generator().manual_seed(3)
+    return torch.randn(8, 8, generator=g), torch.randn(8, 4, generator=g)
+
+
+def _single_sgd(steps=2):
+    import paddle_infer_amd as paddle
+    m = _mlp()
+    o = paddle.optimizer.SGD(learning_rate=0.1, parameters=m.parameters())
+    x, y = _data()
+    for _ in range(steps):
+        loss = ((m(x) - y) ** 2).mean()
+        loss.backward()
+        o.step()
+        o.clear_grad()
+    return {k: v.clone() for k, v in m.state_dict().items()}
+
+
+def _dp_worker(rank, world):
+    import paddle_infer_amd as paddle
+    import paddle_infer_amd.distributed as pd
+    m = pd.DataParallel(_mlp(), comm_buffer_size=0.0005)
+    o = paddle.optimizer.SGD(learning_rate=0.1, parameters=m.parameters())
+    x, y = _data()
+    xs, ys = x.chunk(world)[rank], y.chunk(world)[rank]
+    for _ in range(2):
+        loss = ((m(xs) - ys) ** 2).mean()
+        loss.backward()
+        o.step()
+        o.clear_grad()
+    return {k: v.clone() for k, v in m.state_dict().items()}
+
+
+def test_data_parallel_generic_model():
+    ref = _single_sgd()
+    res = run_distributed(_dp_worker, 2)
+    for r in range(2):
+        for k in ref:
+            torch.testing.assert_close(res[r][k], ref[k], rtol=1e-5, atol=1e-6)
+
+
+def _pp_worker(rank, world):
+    import paddle_infer_amd as paddle
+    from paddle_infer_amd.distributed import fleet
+    from paddle_infer_amd.distributed.fleet import LayerDesc, PipelineLayer
+    st = fleet.DistributedStrategy()
+    st.hybrid_configs = {"dp_degree": 1, "mp_degree": 1, "pp_degree": 2,
+                         "pp_configs": {"accumulate_steps": 4, "micro_batch_size": 2}}
+    fleet.init(is_collective=True, strategy=st)
+    torch.manual_seed(0)
+    full = _mlp()
+    descs = list(full.children())
+    loss_fn = lambda out, y: ((out - y) ** 2).mean()  # noqa: E731
+    pl = PipelineLayer(descs, num_stages=2, loss_fn=loss_fn)
+    model = fleet.distributed_model(pl)
+    opt = paddle.optimizer.SGD(learning_rate=0.1, parameters=pl.parameters())
+    x, y = _data()
+    losses = []
+    for _ in range(2):
+        losses.append(float(model.train_batch([x, y], opt)))
+    return {"stage": pl.stage_id, "sd": {k: v.clone() for k, v in full.state_dict().items()}, "losses": losses}
+
+
+def test_pipeline_1f1b_matches_single():
+    import paddle_infer_amd as paddle
+    m = _mlp()
+    o = paddle.optimizer.SGD(learning_rate=0.1, parameters=m.parameters())
+    x, y = _data()
+    ref_losses = []
+    for _ in range(2):
+        tot = 0.0
+        for xs, ys in zip(x.chunk(4), y.chunk(4)):
+            loss = ((m(xs) - ys) ** 2).mean() / 4
+            loss.backward()
+            tot += loss.item()
+        ref_losses.append(tot)
+        o.step()
+        o.clear_grad()
+    ref = m.state_dict()
+    res = run_distributed(_pp_worker, 2)
+    for r in range(2):
+        assert res[r]["losses"] == pytest.approx(ref_losses, rel=1e-5)
+    # stage 0 owns layers 0..2, stage 1 owns 3..4 (uniform split of 5 descs)
+    s0 = res[0]["sd"] if res[0]["stage"] == 0 else res[1]["sd"]
+    s1 = res[1]["sd"] if res[1]["stage"] == 1 else res[0]["sd"]
+    torch.testing.assert_close(s0["0.weight"], ref["0.weight"], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(s1["4.weight"], ref["4.weight"], rtol=1e-5, atol=1e-6)
+
+
+def _stage3_worker(rank, world):
+    import paddle_infer_amd as paddle
+    import paddle_infer_amd.distributed as pd
+    m = _mlp()
+    o = paddle.optimizer.AdamW(learning_rate=0.01, parameters=m.parameters(), weight_decay=0.0)
+    m3, o3, _ = pd.group_sharded_parallel(m, o, "p_g_os")
+    x, y = _data()
+    xs, ys = x.chunk(world)[rank], y.chunk(world)[rank]
+    for _ in range(2):
+        loss = ((m3(xs) - ys) ** 2).mean()
+        loss.backward()
+        o3.step()
+        o3.clear_grad()
+    return {k: v.clone() for k, v in m3.state_dict().items()}
+
+
+def test_group_sharded_stage3_matches_single():
+    import paddle_infer_amd as paddle
+    m = _mlp()
+    o = paddle.optimizer.AdamW(learning_rate=0.01, parameters=m.parameters(), weight_decay=0.0)
+    x, y = _data()
+    for _ in range(2):
+        loss = ((m(x) - y) ** 2).mean()
+        loss.backward()
+        o.step()
+        o.clear_grad()
+    ref = m.state_dict()
+    res = run_distributed(_stage3_worker, 2)
+    for r in range(2):
+        for k in ref:
+            torch.testing.assert_close(res[r][k], ref[k], rtol=1e-4, atol=1e-5)
+
+
+def test_recompute_matches_plain():
+    from paddle_infer_amd.distributed.fleet import recompute
+    import paddle_infer_amd.nn.functional as F
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(8, 8)
+    x = torch.randn(4, 8, requires_grad=True)
+
+    def f(t):
+        return F.dropout(torch.tanh(lin(t)), 0.5, training=True)
+    torch.manual_seed(5)
+    y1 = f(x).sum()
+    y1.backward()
+    g1 = [x.grad.clone(), lin.weight.grad.clone()]
+    x.grad, lin.weight.grad = None, None
+    torch.manual_seed(5)
+    y2 = recompute(f, x).sum()
+    y2.backward()
+    g2 = [x.grad, lin.weight.grad]
+    assert y1.item() == pytest.approx(y2.item())
+    for a, b in zip(g1, g2):
+        torch.testing.assert_close(a, b)
+
+
+def test_launch_watchdog_kills_job_on_failure(tmp_path):
+    script = tmp_path / "job.py"
+    script.write_text(textwrap.dedent("""
+        import os, sys, time
+        if os.environ["RANK"] == "1":
+            sys.exit(3)
+        time.sleep(60)
+    """))
+    import time as _t
+    t0 = _t.time()
+    r = subprocess.run([sys.executable, "-m", "paddle_infer_amd.distributed.launch",
+                        "--nproc_per_node", "2", "--log_dir", str(tmp_path / "log"), str(script)],
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 3
+    assert _t.time() - t0 < 30
+    assert (tmp_path / "log" / "workerlog.0").exists()

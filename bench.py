@@ -34,7 +34,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="gpt3-1.3b")
     ap.add_argument("--seq", type=int, default=1024)
-    ap.add_argument("--micro-batch", type=int, default=8, help="sequences per data-parallel rank")
+    ap.add_argument("--micro-batch", type=int, default=16, help="sequences per data-parallel rank")
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--sharding", type=int, default=1)
     ap.add_argument("--bucket-mb", type=int, default=256)

@@ -24,9 +24,10 @@ def _lr_value(lr_):
 class Optimizer:
     def __init__(self, learning_rate=0.001, parameters=None, weight_decay=None, grad_clip=None,
                  name=None, multi_precision=False):
-        if parameters is None:
+        from ..static.framework import _STATE as _SSTATE
+        if parameters is None and not _SSTATE["static"]:
             raise ValueError("parameters must be given in dygraph mode")
-        params = list(parameters)
+        params = list(parameters) if parameters is not None else []
         if params and isinstance(params[0], dict):  # param groups
             self._param_groups = params
             params = [p for g in params for p in g["params"]]
@@ -113,6 +114,10 @@ class Optimizer:
         raise NotImplementedError
 
     def minimize(self, loss, startup_program=None, parameters=None, no_grad_set=None):
+        from ..static.framework import Variable as _SVar
+        if isinstance(loss, _SVar):  # static graph: append backward + optimize ops
+            from ..static.backward import minimize as _static_minimize
+            return _static_minimize(self, loss, parameters, no_grad_set)
         loss.backward()
         self.step()
         return None, [(p, p.grad) for p in self._parameter_list]

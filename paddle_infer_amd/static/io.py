@@ -1,0 +1,358 @@
+"""Static-graph model IO: ``.pdmodel`` (ProgramDesc protobuf) + ``.pdiparams`` (combined tensors).
+
+Parity: reference `python/paddle/static/io.py` (save_inference_model / load_inference_model /
+serialize_program / deserialize_program / save / load / load_program_state) and
+`python/paddle/fluid/io.py`. Inference programs are pruned to the ops the fetch targets need and
+framed by ``feed`` / ``fetch`` ops exactly like the reference; persistables are written sorted
+by name in the combined LoDTensor stream.
+
+Ops recorded by the capture mechanism carry two extra string attrs — ``op_callable`` (the torch
+callable) and ``op_spec`` (JSON of the argument structure) — so a saved program round-trips
+exactly; ops without them (programs produced by Paddle itself) execute through the Paddle-op
+registry (`ops_registry.py`).
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+
+import numpy as np
+import torch
+
+from . import proto
+from .framework import Operator, Program, SymDim, VarRef, Variable
+from ..framework.dtype import dtype_name, to_torch_dtype
+
+
+# ------------------------------------------------------------------------ arg-spec (de)serialise
+def _enc(x):
+    if isinstance(x, VarRef):
+        return {"$v": x.name}
+    if isinstance(x, SymDim):
+        return {"$sym": [x.k, [list(e) for e in x.exps]]}
+    if isinstance(x, tuple):
+        return {"$t": [_enc(v) for v in x]}
+    if isinstance(x, list):
+        return [_enc(v) for v in x]
+    if isinstance(x, dict):
+        return {"$d": {k: _enc(v) for k, v in x.items()}}
+    if isinstance(x, slice):
+        return {"$s": [_enc(x.start), _enc(x.stop), _enc(x.step)]}
+    if x is Ellipsis:
+        return {"$e": 1}
+    if isinstance(x, torch.dtype):
+        return {"$dt": dtype_name(x)}
+    if isinstance(x, torch.device):
+        return {"$dev": str(x)}
+    if isinstance(x, (torch.memory_format, torch.layout)):
+        return {"$mf": str(x)}
+    if isinstance(x, torch.Size):
+        return {"$t": list(x)}
+    if isinstance(x, (np.integer,)):
+        return int(x)
+    if isinstance(x, (np.floating,)):
+        return float(x)
+    if isinstance(x, float) and (math.isinf(x) or math.isnan(x)):
+        return {"$f": repr(x)}
+    return x
+
+
+def _dec(x):
+    if isinstance(x, list):
+        return [_dec(v) for v in x]
+    if isinstance(x, dict):
+        if "$v" in x:
+            return VarRef(x["$v"])
+        if "$sym" in x:
+            return SymDim(x["$sym"][0], x["$sym"][1])
+        if "$t" in x:
+            return tuple(_dec(v) for v in x["$t"])
+        if "$d" in x:
+            return {k: _dec(v) for k, v in x["$d"].items()}
+        if "$s" in x:
+            return slice(*[_dec(v) for v in x["$s"]])
+        if "$e" in x:
+            return Ellipsis
+        if "$dt" in x:
+            return to_torch_dtype(x["$dt"])
+        if "$dev" in x:
+            return torch.device(x["$dev"])
+        if "$mf" in x:
+            return getattr(torch, x["$mf"].replace("torch.", ""))
+        if "$f" in x:
+            return float(x["$f"])
+    return x
+
+
+def func_name(func):
+    objcls = getattr(func, "__objclass__", None)
+    if objcls is not None:
+        return f"torch.Tensor.{func.__name__}"
+    owner = getattr(func, "__self__", None)
+    if isinstance(owner, type) and func.__name__ == "apply":  # autograd.Function.apply
+        return f"{owner.__module__}.{owner.__qualname__}.apply"
+    mod = getattr(func, "__module__", None)
+    q = getattr(func, "__qualname__", None) or getattr(func, "__name__")
+    if mod == "torch._tensor":
+        return f"torch._tensor.{q}"
+    name = f"{mod}.{q}" if mod else q
+    try:
+        if resolve_func(name) is func:
+            return name
+    except (AttributeError, ImportError, ValueError):
+        pass
+    import torch.nn.functional as F
+    for prefix, ns in (("torch", torch), ("torch.nn.functional", F), ("torch.Tensor", torch.Tensor),
+                       ("torch._C._nn", torch._C._nn), ("torch.special", torch.special),
+                       ("torch.linalg", torch.linalg), ("torch.fft", torch.fft)):
+        if getattr(ns, func.__name__, None) is func:
+            return f"{prefix}.{func.__name__}"
+    raise ValueError(f"cannot serialise op callable {func!r}")
+
+
+def resolve_func(name):
+    import importlib
+    parts = name.split(".")
+    # longest importable module prefix, then attribute walk
+    for i in range(len(parts) - 1, 0, -1):
+        try:
+            obj = importlib.import_module(".".join(parts[:i]))
+        except ImportError:
+            continue
+        for p in parts[i:]:
+            obj = getattr(obj, p)
+        return obj
+    raise ValueError(f"cannot resolve op callable {name}")
+
+
+# ------------------------------------------------------------------------ Program <-> desc
+def _var_desc(v: Variable, is_param):
+    shape = v.declared_shape if v.declared_shape is not None else list(v.shape)
+    with torch._C.DisableTorchFunctionSubclass():
+        dt = v.dtype
+    return {"name": v.var_name,
+            "type": {"type": proto.VT_LOD_TENSOR,
+                     "lod_tensor": {"tensor": {"data_type": proto.VT[dtype_name(dt)],
+                                               "dims": [(-1 if s is None else int(s)) for s in shape]},
+                                    "lod_level": 0}},
+            "persistable": bool(v.persistable_), "is_parameter": bool(is_param),
+            "stop_gradient": bool(v.stop_gradient_)}
+
+
+def program_to_desc(program: Program, feed_names=None, fetch_names=None, ops=None):
+    b = program.global_block()
+    ops = b.ops if ops is None else ops
+    used = set()
+    for op in ops:
+        used.update(op.input_names())
+        used.update(op.output_names())
+    used.update(feed_names or [])
+    used.update(fetch_names or [])
+    vars_ = [_var_desc(b.vars[n], n in program.params) for n in sorted(used) if n in b.vars]
+    op_descs = []
+    if feed_names:
+        vars_.append({"name": "feed", "type": {"type": proto.VT_FEED}, "persistable": True})
+        for i, n in enumerate(feed_names):
+            op_descs.append({"type": "feed", "inputs": [{"parameter": "X", "arguments": ["feed"]}],
+                             "outputs": [{"parameter": "Out", "arguments": [n]}],
+                             "attrs": [{"name": "col", "type": proto.ATTR["INT"], "i": i}]})
+    for op in ops:
+        if op.type in ("backward", "optimize"):
+            continue
+        attrs = [{"name": k, "type": proto.ATTR["STRING"], "s": json.dumps(_enc(v))}
+                 for k, v in op.attrs.items() if k not in ("optimizer",)]
+        if op.func is not None:
+            attrs.append({"name": "op_callable", "type": proto.ATTR["STRING"], "s": func_name(op.func)})
+            attrs.append({"name": "op_spec", "type": proto.ATTR["STRING"],
+                          "s": json.dumps({"args": _enc(op.args), "kwargs": _enc(op.kwargs),
+                                           "outputs": _enc(op.outputs)})})
+        op_descs.append({"type": op.type, "inputs": [{"parameter": "X", "arguments": op.input_names()}],
+                         "outputs": [{"parameter": "Out", "arguments": op.output_names()}],
+                         "attrs": attrs})
+    if fetch_names:
+        vars_.append({"name": "fetch", "type": {"type": proto.VT_FETCH}, "persistable": True})
+        for i, n in enumerate(fetch_names):
+            op_descs.append({"type": "fetch", "inputs": [{"parameter": "X", "arguments": [n]}],
+                             "outputs": [{"parameter": "Out", "arguments": ["fetch"]}],
+                             "attrs": [{"name": "col", "type": proto.ATTR["INT"], "i": i}]})
+    return {"blocks": [{"idx": 0, "parent_idx": -1, "vars": vars_, "ops": op_descs}],
+            "version": {"version": 0}}
+
+
+def _attr_value(a):
+    t = a.get("type", 0)
+    return {0: a.get("i"), 1: a.get("f"), 2: a.get("s"), 3: a.get("ints", []), 4: a.get("floats", []),
+            5: a.get("strings", []), 6: a.get("b"), 7: a.get("bools", []), 8: a.get("block_idx"),
+            9: a.get("l"), 10: a.get("blocks_idx", []), 11: a.get("longs", []),
+            12: a.get("float64s", []), 13: a.get("var_name"), 14: a.get("vars_name", []),
+            15: a.get("float64")}.get(t)
+
+
+def desc_to_program(desc: dict):
+    prog = Program()
+    b = prog.global_block()
+    blk = desc["blocks"][0]
+    feeds, fetches = [], []
+    np_dt = {v: k for k, v in proto.VT.items()}
+    for vd in blk.get("vars", []):
+        ty = vd.get("type", {})
+        if ty.get("type") != proto.VT_LOD_TENSOR:
+            continue
+        td = ty.get("lod_tensor", {}).get("tensor", {})
+        v = b.create_var(vd["name"], td.get("dims", [1]) or [1], np_dt.get(td.get("data_type", 5), "float32"),
+                         persistable=vd.get("persistable", False),
+                         stop_gradient=vd.get("stop_gradient", True))
+        v.declared_shape = td.get("dims", [])
+    for od in blk.get("ops", []):
+        ins = {x["parameter"]: x.get("arguments", []) for x in od.get("inputs", [])}
+        outs = {x["parameter"]: x.get("arguments", []) for x in od.get("outputs", [])}
+        attrs = {a["name"]: _attr_value(a) for a in od.get("attrs", [])}
+        if od["type"] == "feed":
+            feeds.append((attrs.get("col", len(feeds)), outs["Out"][0]))
+            continue
+        if od["type"] == "fetch":
+            fetches.append((attrs.get("col", len(fetches)), ins["X"][0]))
+            continue
+        if "op_callable" in attrs:
+            spec = json.loads(attrs.pop("op_spec"))
+            func = resolve_func(attrs.pop("op_callable"))
+            extra = {k: _dec(json.loads(v)) for k, v in attrs.items() if isinstance(v, str)}
+            op = Operator(b, func, _dec(spec["args"]), _dec(spec["kwargs"]), _dec(spec["outputs"]),
+                          type=od["type"], attrs=extra)
+        else:
+            op = Operator(b, None, (), {}, None, type=od["type"], attrs=attrs)
+            op.paddle_inputs, op.paddle_outputs = ins, outs
+        b.append_op(op)
+    prog.feed_names = [n for _, n in sorted(feeds)]
+    prog.fetch_names = [n for _, n in sorted(fetches)]
+    return prog
+
+
+def serialize_program(feed_vars, fetch_vars, program=None, **kwargs):
+    from .framework import default_main_program
+    program = program or default_main_program()
+    feeds = [v.var_name if isinstance(v, Variable) else v for v in _as_list(feed_vars)]
+    fetches = [v.var_name if isinstance(v, Variable) else v for v in _as_list(fetch_vars)]
+    ops = prune(program, fetches)
+    return proto.encode("ProgramDesc", program_to_desc(program, feeds, fetches, ops))
+
+
+def deserialize_program(data: bytes):
+    return desc_to_program(proto.decode("ProgramDesc", data))
+
+
+def _as_list(x):
+    return list(x) if isinstance(x, (list, tuple)) else [x]
+
+
+def prune(program, fetch_names):
+    ops = [op for op in program.global_block().ops if op.type not in ("backward", "optimize")]
+    need = set(fetch_names)
+    keep = []
+    for op in reversed(ops):
+        outs = set(op.output_names())
+        if outs & need:
+            keep.append(op)
+            need.update(op.input_names())
+    return list(reversed(keep))
+
+
+# ------------------------------------------------------------------------ params
+def serialize_persistables(feed_vars, fetch_vars, executor=None, program=None, names=None):
+    from .framework import default_main_program, global_scope
+    program = program or default_main_program()
+    scope = global_scope()
+    names = sorted(names if names is not None else program.params.keys())
+    out = bytearray()
+    for n in names:
+        t = scope.get(n)
+        t = program.params[n] if t is None else t
+        t = t.detach().cpu()
+        if t.dtype == torch.bfloat16:
+            arr, vt = t.view(torch.int16).numpy().view(np.uint16), proto.VT["bfloat16"]
+        else:
+            arr, vt = t.numpy(), proto.VT[dtype_name(t.dtype)]
+        out += proto.tensor_to_stream(arr, vt)
+    return bytes(out)
+
+
+def deserialize_persistables(program, data: bytes, executor=None, names=None):
+    from .framework import global_scope
+    names = sorted(names if names is not None else [
+        n for n, v in program.global_block().vars.items() if v.persistable_])
+    pos = 0
+    scope = global_scope()
+    dev = executor.device if executor is not None else torch.device("cpu")
+    for n in names:
+        arr, vt, pos = proto.tensor_from_stream(data, pos)
+        if vt == proto.VT["bfloat16"]:
+            t = torch.from_numpy(arr.view(np.int16)).view(torch.bfloat16)
+        else:
+            t = torch.from_numpy(arr)
+        program.params[n] = t
+        scope.set(n, t.to(dev))
+    return program
+
+
+def save_inference_model(path_prefix, feed_vars, fetch_vars, executor, program=None, **kwargs):
+    from .framework import default_main_program
+    program = program or default_main_program()
+    d = os.path.dirname(path_prefix)
+    if d:
+        os.makedirs(d, exist_ok=True)
+    fetches = [v.var_name if isinstance(v, Variable) else v for v in _as_list(fetch_vars)]
+    ops = prune(program, fetches)
+    used = set()
+    for op in ops:
+        used.update(op.input_names())
+    pnames = sorted(n for n in program.params if n in used)
+    with open(path_prefix + ".pdmodel", "wb") as f:
+        f.write(serialize_program(feed_vars, fetch_vars, program))
+    with open(path_prefix + ".pdiparams", "wb") as f:
+        f.write(serialize_persistables(feed_vars, fetch_vars, executor, program, pnames))
+
+
+def load_inference_model(path_prefix, executor, model_filename=None, params_filename=None, **kw):
+    mf = model_filename or path_prefix + ".pdmodel"
+    pf = params_filename or path_prefix + ".pdiparams"
+    with open(mf, "rb") as f:
+        prog = deserialize_program(f.read())
+    if os.path.exists(pf):
+        with open(pf, "rb") as f:
+            deserialize_persistables(prog, f.read(), executor)
+    fetch_vars = [prog.global_block().vars[n] for n in prog.fetch_names]
+    return [prog, list(prog.feed_names), fetch_vars]
+
+
+def save(program, model_path, protocol=4, **configs):
+    from ..framework.io import save as _save
+    from .framework import global_scope
+    scope = global_scope()
+    state = {n: (scope.get(n) if scope.get(n) is not None else t) for n, t in program.params.items()}
+    _save(state, model_path + ".pdparams")
+
+
+def load(program, model_path, executor=None, var_list=None):
+    from ..framework.io import load as _load
+    from .framework import global_scope
+    state = _load(model_path + ".pdparams")
+    set_program_state(program, state)
+
+
+def load_program_state(model_path, var_list=None):
+    from ..framework.io import load as _load
+    return _load(model_path + ".pdparams" if not model_path.endswith(".pdparams") else model_path)
+
+
+def set_program_state(program, state_dict):
+    from .framework import global_scope
+    scope = global_scope()
+    for n, v in state_dict.items():
+        if n in program.params:
+            t = torch.as_tensor(v)
+            program.params[n] = t
+            cur = scope.get(n)
+            if cur is not None:
+                with torch.no_grad():
+                    cur.copy_(t.to(cur.dtype))

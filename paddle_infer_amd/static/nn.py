@@ -1,0 +1,127 @@
+"""``paddle.static.nn`` — layer-building functions for static Programs.
+
+Parity: reference `python/paddle/static/nn/__init__.py` / `static/nn/common.py:fc` and
+`fluid/layers/nn.py` (conv2d, batch_norm, layer_norm, embedding, prelu, group_norm,
+instance_norm, create_parameter, cond). Parameters are created eagerly as real tensors (the
+reference's startup-program initialisers) and registered as persistable Program variables the
+first time an op consumes them; the ops themselves are recorded into the current Program.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .. import nn as _nn
+from ..nn import functional as F
+from .framework import Variable, _record
+
+
+def _act(x, act):
+    if not act:
+        return x
+    return getattr(F, act)(x)
+
+
+def fc(x, size, num_flatten_dims=1, weight_attr=None, bias_attr=None, activation=None, name=None):
+    xs = x if isinstance(x, (list, tuple)) else [x]
+    outs = []
+    for xi in xs:
+        in_dim = int(np.prod(xi.shape[num_flatten_dims:]))
+        lin = _nn.Linear(in_dim, size, weight_attr=weight_attr, bias_attr=bias_attr if len(outs) == 0 else False)
+        if xi.dim() != num_flatten_dims + 1:
+            xi = xi.reshape(list(xi.shape[:num_flatten_dims]) + [in_dim])
+        outs.append(lin(xi))
+    out = outs[0]
+    for o in outs[1:]:
+        out = out + o
+    return _act(out, activation)
+
+
+def conv2d(input, num_filters, filter_size, stride=1, padding=0, dilation=1, groups=None,  # noqa: A002
+           param_attr=None, bias_attr=None, use_cudnn=True, act=None, name=None, data_format="NCHW"):
+    conv = _nn.Conv2D(input.shape[1], num_filters, filter_size, stride, padding, dilation, groups or 1,
+                      weight_attr=param_attr, bias_attr=bias_attr)
+    return _act(conv(input), act)
+
+
+def conv2d_transpose(input, num_filters, output_size=None, filter_size=None, padding=0, stride=1,  # noqa: A002
+                     dilation=1, groups=None, param_attr=None, bias_attr=None, use_cudnn=True, act=None,
+                     name=None, data_format="NCHW"):
+    conv = _nn.Conv2DTranspose(input.shape[1], num_filters, filter_size, stride, padding,
+                               groups=groups or 1, dilation=dilation, weight_attr=param_attr,
+                               bias_attr=bias_attr)
+    return _act(conv(input), act)
+
+
+def batch_norm(input, act=None, is_test=False, momentum=0.9, epsilon=1e-5, param_attr=None,  # noqa: A002
+               bias_attr=None, data_layout="NCHW", in_place=False, name=None, moving_mean_name=None,
+               moving_variance_name=None, do_model_average_for_mean_and_var=True,
+               use_global_stats=False):
+    bn = _nn.BatchNorm2D(input.shape[1], momentum, epsilon, param_attr, bias_attr) if input.dim() == 4 \
+        else _nn.BatchNorm1D(input.shape[1], momentum, epsilon, param_attr, bias_attr)
+    if is_test or use_global_stats:
+        bn.eval()
+    return _act(bn(input), act)
+
+
+def layer_norm(input, scale=True, shift=True, begin_norm_axis=1, epsilon=1e-5, param_attr=None,  # noqa: A002
+               bias_attr=None, act=None, name=None):
+    shape = list(input.shape[begin_norm_axis:])
+    ln = _nn.LayerNorm(shape, epsilon, param_attr if scale else False, bias_attr if shift else False)
+    return _act(ln(input), act)
+
+
+def group_norm(input, groups, epsilon=1e-5, param_attr=None, bias_attr=None, act=None,  # noqa: A002
+               data_layout="NCHW", name=None):
+    gn = _nn.GroupNorm(groups, input.shape[1], epsilon, param_attr, bias_attr)
+    return _act(gn(input), act)
+
+
+def instance_norm(input, epsilon=1e-5, param_attr=None, bias_attr=None, name=None):  # noqa: A002
+    return _nn.InstanceNorm2D(input.shape[1], epsilon, weight_attr=param_attr, bias_attr=bias_attr)(input)
+
+
+def embedding(input, size, is_sparse=False, is_distributed=False, padding_idx=None,  # noqa: A002
+              param_attr=None, dtype="float32"):
+    emb = _nn.Embedding(size[0], size[1], padding_idx, sparse=is_sparse, weight_attr=param_attr)
+    return emb(input)
+
+
+sparse_embedding = embedding
+
+
+def prelu(x, mode="all", param_attr=None, data_format="NCHW", name=None):
+    n = 1 if mode == "all" else x.shape[1]
+    return _nn.PReLU(n, weight_attr=param_attr)(x)
+
+
+def create_parameter(shape, dtype="float32", name=None, attr=None, is_bias=False, default_initializer=None):
+    from ..nn.layer.base import Layer
+    return Layer().create_parameter(shape, attr, dtype, is_bias, default_initializer)
+
+
+def cond(pred, true_fn=None, false_fn=None, name=None, return_names=None):
+    """Both branches are recorded and the result selected element-wise by ``pred`` (the
+    reference's `conditional_block` pair, flattened — branch bodies here are side-effect free)."""
+    if not isinstance(pred, Variable):
+        return true_fn() if bool(pred) else (false_fn() if false_fn else None)
+    t, f = true_fn(), false_fn()
+    if isinstance(t, (list, tuple)):
+        return type(t)(torch.where(pred, a, b) for a, b in zip(t, f))
+    return torch.where(pred, t, f)
+
+
+def while_loop(cond, body, loop_vars, is_test=False, name=None):  # noqa: A002
+    """Runs eagerly on concrete values; a symbolic loop condition is not traceable in a
+    meta-recorded Program (use ``jit.to_static`` on a dygraph function instead)."""
+    if any(isinstance(v, Variable) for v in loop_vars):
+        raise NotImplementedError("while_loop over symbolic Variables: write the loop in dygraph "
+                                  "and export with jit.save (the trace unrolls it)")
+    while bool(cond(*loop_vars)):
+        loop_vars = body(*loop_vars)
+    return loop_vars
+
+
+def py_func(func, x, out, backward_func=None, skip_vars_in_backward_input=None):
+    xs = x if isinstance(x, (list, tuple)) else [x]
+    return _record(func, tuple(xs), {})

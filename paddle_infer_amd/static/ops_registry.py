@@ -1,0 +1,370 @@
+"""Paddle operator registry: slot-based kernels for Paddle op types.
+
+Parity: the reference's op definitions (`paddle/fluid/operators/*_op.cc`, `paddle/phi/ops/`,
+`phi/api/yaml/legacy_ops.yaml`) — same op type names, input/output slot names and attributes —
+so programs produced by Paddle (``feed`` / ``matmul_v2`` / ``elementwise_add`` / ``layer_norm`` /
+``conv2d`` / ``fc`` ...) execute here, and the inference IR passes (`inference/passes.py`) can
+rewrite subgraphs into the fused types registered below (``fc``, ``skip_layernorm``,
+``fused_bias_act``, ``flash_attn_packed``), which dispatch to the hand-written HIP kernels.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import proto
+from .framework import VarRef
+
+REGISTRY = {}
+
+
+def register(*names):
+    def deco(fn):
+        for n in names:
+            REGISTRY[n] = fn
+        return fn
+    return deco
+
+
+def _dt(code):
+    inv = {v: k for k, v in proto.VT.items()}
+    from ..framework.dtype import to_torch_dtype
+    return to_torch_dtype(inv.get(int(code), "float32"))
+
+
+def _bcast(x, y, axis):
+    if axis is None or axis == -1 or y.dim() == x.dim():
+        return y
+    shape = [1] * x.dim()
+    for i, s in enumerate(y.shape):
+        shape[axis + i] = s
+    return y.reshape(shape)
+
+
+def run_paddle_op(op, sub, env, scope):
+    fn = REGISTRY.get(op.type)
+    if fn is None:
+        raise NotImplementedError(f"Paddle op '{op.type}' has no kernel in paddle_infer_amd")
+    ins = {k: [sub(VarRef(n)) for n in v] for k, v in op.paddle_inputs.items()}
+    outs = fn(ins, op.attrs)
+    for slot, names in op.paddle_outputs.items():
+        vals = outs.get(slot)
+        if vals is None:
+            continue
+        vals = vals if isinstance(vals, (list, tuple)) else [vals]
+        for n, v in zip(names, vals):
+            env[n] = v
+
+
+@register("matmul_v2")
+def _matmul_v2(ins, a):
+    x, y = ins["X"][0], ins["Y"][0]
+    if a.get("trans_x"):
+        x = x.transpose(-1, -2)
+    if a.get("trans_y"):
+        y = y.transpose(-1, -2)
+    return {"Out": torch.matmul(x, y)}
+
+
+@register("matmul")
+def _matmul(ins, a):
+    x, y = ins["X"][0], ins["Y"][0]
+    if a.get("transpose_X"):
+        x = x.transpose(-1, -2)
+    if a.get("transpose_Y"):
+        y = y.transpose(-1, -2)
+    out = torch.matmul(x, y)
+    alpha = a.get("alpha", 1.0)
+    return {"Out": out * alpha if alpha not in (None, 1.0) else out}
+
+
+@register("mul")
+def _mul(ins, a):
+    x, y = ins["X"][0], ins["Y"][0]
+    xn = a.get("x_num_col_dims", 1)
+    x2 = x.reshape(int(np.prod(x.shape[:xn])), -1)
+    out = x2 @ y.reshape(x2.shape[1], -1)
+    return {"Out": out.reshape(*x.shape[:xn], -1)}
+
+
+for _name, _f in [("elementwise_add", torch.add), ("elementwise_sub", torch.sub),
+                  ("elementwise_mul", torch.mul), ("elementwise_div", torch.true_divide),
+                  ("elementwise_pow", torch.pow), ("elementwise_max", torch.maximum),
+                  ("elementwise_min", torch.minimum)]:
+    register(_name)(lambda ins, a, _f=_f: {"Out": _f(ins["X"][0], _bcast(ins["X"][0], ins["Y"][0], a.get("axis", -1)))})
+
+for _name, _f in [("relu", F.relu), ("sigmoid", torch.sigmoid), ("tanh", torch.tanh), ("silu", F.silu),
+                  ("swish", F.silu), ("hard_swish", F.hardswish), ("relu6", F.relu6), ("exp", torch.exp),
+                  ("sqrt", torch.sqrt), ("rsqrt", torch.rsqrt), ("abs", torch.abs), ("log", torch.log),
+                  ("floor", torch.floor), ("assign", lambda t: t.clone()), ("square", torch.square)]:
+    register(_name)(lambda ins, a, _f=_f: {"Out": _f(ins["X"][0])})
+
+
+@register("gelu")
+def _gelu(ins, a):
+    from .. import ops
+    return {"Out": ops.gelu(ins["X"][0], bool(a.get("approximate", False)))}
+
+
+@register("leaky_relu")
+def _leaky(ins, a):
+    return {"Out": F.leaky_relu(ins["X"][0], a.get("alpha", 0.02))}
+
+
+@register("softmax")
+def _softmax(ins, a):
+    x = ins["X"][0]
+    axis = a.get("axis", -1)
+    if axis in (-1, x.dim() - 1):
+        from .. import ops
+        return {"Out": ops.fused_softmax_mask(x)}
+    return {"Out": torch.softmax(x, axis)}
+
+
+@register("layer_norm")
+def _layer_norm(ins, a):
+    from .. import ops
+    x = ins["X"][0]
+    bna = a.get("begin_norm_axis", x.dim() - 1)
+    scale = ins.get("Scale", [None])[0] if ins.get("Scale") else None
+    bias = ins.get("Bias", [None])[0] if ins.get("Bias") else None
+    if bna == x.dim() - 1:
+        y = ops.layer_norm(x, scale, bias, a.get("epsilon", 1e-5))
+    else:
+        y = F.layer_norm(x, x.shape[bna:], scale.reshape(x.shape[bna:]) if scale is not None else None,
+                         bias.reshape(x.shape[bna:]) if bias is not None else None, a.get("epsilon", 1e-5))
+    return {"Y": y}
+
+
+@register("skip_layernorm")
+def _skip_ln(ins, a):
+    from .. import ops
+    y, _ = ops.fused_add_layer_norm(ins["X"][0], ins["Y"][0], ins["Scale"][0], ins["Bias"][0],
+                                    a.get("epsilon", 1e-5), None, 0.0, False)
+    return {"Out": y}
+
+
+@register("batch_norm")
+def _bn(ins, a):
+    y = F.batch_norm(ins["X"][0], ins["Mean"][0], ins["Variance"][0], ins["Scale"][0], ins["Bias"][0],
+                     False, 0.0, a.get("epsilon", 1e-5))
+    return {"Y": y}
+
+
+def _pads(p, nd):
+    p = list(p or [0] * nd)
+    if len(p) == 2 * nd and all(p[2 * i] == p[2 * i + 1] for i in range(nd)):
+        p = p[0::2]
+    return p
+
+
+@register("conv2d", "depthwise_conv2d")
+def _conv2d(ins, a):
+    x, w = ins["Input"][0], ins["Filter"][0]
+    pad = a.get("padding_algorithm", "EXPLICIT")
+    padding = "same" if pad == "SAME" else (0 if pad == "VALID" else _pads(a.get("paddings"), 2))
+    y = F.conv2d(x, w, ins["Bias"][0] if ins.get("Bias") else None, a.get("strides", [1, 1]), padding,
+                 a.get("dilations", [1, 1]), a.get("groups", 1))
+    return {"Output": y}
+
+
+@register("conv2d_transpose")
+def _conv2d_t(ins, a):
+    y = F.conv_transpose2d(ins["Input"][0], ins["Filter"][0], None, a.get("strides", [1, 1]),
+                           _pads(a.get("paddings"), 2), a.get("output_padding") or 0,
+                           a.get("groups", 1), a.get("dilations", [1, 1]))
+    return {"Output": y}
+
+
+@register("pool2d")
+def _pool2d(ins, a):
+    x = ins["X"][0]
+    k = a.get("ksize", [1, 1])
+    if a.get("global_pooling"):
+        k = list(x.shape[2:])
+    if a.get("adaptive"):
+        fn = F.adaptive_avg_pool2d if a.get("pooling_type", "max") == "avg" else F.adaptive_max_pool2d
+        return {"Out": fn(x, k)}
+    st, pd = a.get("strides", k), _pads(a.get("paddings"), 2)
+    if a.get("pooling_type", "max") == "max":
+        return {"Out": F.max_pool2d(x, k, st, pd, ceil_mode=bool(a.get("ceil_mode")))}
+    return {"Out": F.avg_pool2d(x, k, st, pd, bool(a.get("ceil_mode")), not a.get("exclusive", True))}
+
+
+@register("reshape2", "reshape")
+def _reshape(ins, a):
+    x = ins["X"][0]
+    shape = list(a.get("shape", []))
+    if ins.get("Shape"):
+        shape = [int(v) for v in ins["Shape"][0].tolist()]
+    shape = [x.shape[i] if s == 0 else s for i, s in enumerate(shape)]
+    return {"Out": x.reshape(shape)}
+
+
+@register("transpose2", "transpose")
+def _transpose(ins, a):
+    return {"Out": ins["X"][0].permute(*a.get("axis"))}
+
+
+@register("flatten_contiguous_range")
+def _flatten(ins, a):
+    return {"Out": torch.flatten(ins["X"][0], a.get("start_axis", 1), a.get("stop_axis", -1))}
+
+
+@register("squeeze2")
+def _squeeze(ins, a):
+    x = ins["X"][0]
+    axes = [ax % x.dim() for ax in a.get("axes", [])] or [i for i, s in enumerate(x.shape) if s == 1]
+    for ax in sorted(axes, reverse=True):
+        if x.shape[ax] == 1:
+            x = x.squeeze(ax)
+    return {"Out": x}
+
+
+@register("unsqueeze2")
+def _unsqueeze(ins, a):
+    x = ins["X"][0]
+    for ax in sorted(a.get("axes", [])):
+        x = x.unsqueeze(ax)
+    return {"Out": x}
+
+
+@register("concat")
+def _concat(ins, a):
+    return {"Out": torch.cat(ins["X"], a.get("axis", 0))}
+
+
+@register("split")
+def _split(ins, a):
+    x = ins["X"][0]
+    axis = a.get("axis", 0)
+    sec = a.get("sections") or []
+    if sec:
+        if -1 in sec:
+            sec = list(sec)
+            sec[sec.index(-1)] = x.shape[axis] - sum(s for s in sec if s != -1)
+        return {"Out": list(torch.split(x, sec, axis))}
+    return {"Out": list(torch.chunk(x, a.get("num", 1), axis))}
+
+
+@register("slice")
+def _slice(ins, a):
+    x = ins["Input"][0]
+    sl = [slice(None)] * x.dim()
+    for ax, s, e in zip(a.get("axes", []), a.get("starts", []), a.get("ends", [])):
+        sl[ax] = slice(s, min(e, x.shape[ax]) if e > 0 else e)
+    out = x[tuple(sl)]
+    for ax in sorted(a.get("decrease_axis", []) or [], reverse=True):
+        out = out.squeeze(ax)
+    return {"Out": out}
+
+
+@register("scale")
+def _scale(ins, a):
+    x = ins["X"][0]
+    s, b = a.get("scale", 1.0), a.get("bias", 0.0)
+    return {"Out": x * s + b if a.get("bias_after_scale", True) else (x + b) * s}
+
+
+@register("cast")
+def _cast(ins, a):
+    return {"Out": ins["X"][0].to(_dt(a.get("out_dtype", 5)))}
+
+
+@register("dropout")
+def _dropout(ins, a):
+    x = ins["X"][0]
+    p = a.get("dropout_prob", 0.5)
+    if a.get("dropout_implementation", "downgrade_in_infer") == "downgrade_in_infer":
+        return {"Out": x * (1.0 - p)}
+    return {"Out": x}
+
+
+@register("lookup_table_v2", "lookup_table")
+def _lookup(ins, a):
+    ids = ins["Ids"][0].long()
+    if ids.dim() > 1 and ids.shape[-1] == 1 and a.get("_squeeze_last", False):
+        ids = ids.squeeze(-1)
+    return {"Out": F.embedding(ids, ins["W"][0], a.get("padding_idx") if (a.get("padding_idx") or -1) >= 0 else None)}
+
+
+@register("fill_constant")
+def _fill(ins, a):
+    return {"Out": torch.full(a.get("shape", [1]), a.get("value", 0.0), dtype=_dt(a.get("dtype", 5)))}
+
+
+for _name, _f in [("reduce_mean", torch.mean), ("reduce_sum", torch.sum), ("reduce_max", torch.amax),
+                  ("reduce_min", torch.amin)]:
+    def _mk(_f=_f):
+        def op(ins, a):
+            x = ins["X"][0]
+            if a.get("reduce_all") or not a.get("dim"):
+                out = _f(x)
+                return {"Out": out.reshape([1] * x.dim()) if a.get("keep_dim") else out}
+            return {"Out": _f(x, dim=tuple(a["dim"]), keepdim=bool(a.get("keep_dim")))}
+        return op
+    register(_name)(_mk())
+
+
+@register("arg_max")
+def _argmax(ins, a):
+    return {"Out": torch.argmax(ins["X"][0], a.get("axis", -1), bool(a.get("keepdims")))}
+
+
+@register("top_k_v2")
+def _topk(ins, a):
+    v, i = torch.topk(ins["X"][0], a.get("k", 1), a.get("axis", -1), a.get("largest", True))
+    return {"Out": v, "Indices": i}
+
+
+@register("softmax_with_cross_entropy")
+def _swce(ins, a):
+    lg, lab = ins["Logits"][0], ins["Label"][0]
+    loss = F.cross_entropy(lg.reshape(-1, lg.shape[-1]).float(), lab.reshape(-1).long(),
+                           ignore_index=a.get("ignore_index", -100), reduction="none")
+    return {"Loss": loss.reshape(*lab.shape[:-1], 1) if lab.dim() == lg.dim() else loss,
+            "Softmax": torch.softmax(lg, -1)}
+
+
+# ---------------------------------------------------------------- fused (IR-pass targets)
+@register("fc")
+def _fc(ins, a):
+    """Reference `fc_op.cc`: Out = act(Input @ W + Bias) (in_num_col_dims flattening)."""
+    from ..ops.linear import linear
+    from .. import ops
+    x, w = ins["Input"][0], ins["W"][0]
+    b = ins["Bias"][0] if ins.get("Bias") else None
+    nc = a.get("in_num_col_dims", x.dim() - 1)
+    x2 = x.reshape(int(np.prod(x.shape[:nc])), -1)
+    act = a.get("activation_type", "")
+    if act in ("gelu", "relu", "silu", "gelu_tanh") and x2.is_cuda and x2.dtype == torch.bfloat16:
+        y = ops.bias_act(linear(x2, w, None), b, act)
+    else:
+        y = linear(x2, w, b)
+        if act:
+            y = {"relu": F.relu, "gelu": F.gelu, "silu": F.silu, "tanh": torch.tanh,
+                 "sigmoid": torch.sigmoid}[act](y)
+    return {"Out": y.reshape(*x.shape[:nc], -1)}
+
+
+@register("fused_bias_act")
+def _fused_bias_act(ins, a):
+    from .. import ops
+    return {"Out": ops.bias_act(ins["X"][0], ins["Bias"][0] if ins.get("Bias") else None,
+                                a.get("act_method", "gelu"))}
+
+
+@register("flash_attn_packed")
+def _flash_packed(ins, a):
+    from .. import ops
+    qkv = ins["QKV"][0]
+    return {"Out": ops.flash_attention_packed(qkv, a["num_heads"], a.get("num_kv_heads") or a["num_heads"],
+                                              causal=bool(a.get("causal", False)))}
+
+
+@register("flash_attn")
+def _flash(ins, a):
+    from .. import ops
+    return {"Out": ops.flash_attention(ins["Q"][0], ins["K"][0], ins["V"][0], causal=bool(a.get("causal", False)))}
+

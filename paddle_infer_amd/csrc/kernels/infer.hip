@@ -1,0 +1,508 @@
+// Inference kernels for the fused multi-transformer (serving) path on CDNA4 (gfx950).
+//
+//   qkv_prep      : QKV bias add + rotary embedding (NeoX rotate-half or GPT-J interleaved,
+//                   partial rotary) + KV-cache write, in place on the packed QKV GEMM output.
+//                   Parity: the bias/rotary/cache-write prologue of the reference's
+//                   `fluid/operators/fused/fused_multi_transformer_op.cu.h` (write_cache_kv,
+//                   add_fusedQKV_bias_transpose, rotary_qk).
+//   decode_attn   : single-token attention over the KV cache ("masked multihead attention",
+//                   reference `fused_multi_transformer_op.cu.h:masked_multihead_attention_kernel`),
+//                   re-designed as split-K (flash-decoding): grid = (key splits, kv heads, batch),
+//                   each workgroup streams a chunk of K then V once (HBM-bound) for ALL query heads
+//                   of its GQA group, partials merged by decode_combine. Lengths come from device
+//                   memory so a captured hipGraph replays every decode step unchanged.
+//   wo_gemm       : weight-only int8 / int4 GEMM y = act((x·Wᵀ)·scale + bias) on MFMA
+//                   (`v_mfma_f32_32x32x16_bf16`; int→bf16 is exact for |q| ≤ 127) over an
+//                   MI355X-native pre-packed weight layout: one 1 KB fully-coalesced load per wave
+//                   per 32 (int8) / 64 (int4) k. Parity: reference `cutlass_kernels/fpA_intB_gemm`
+//                   (weight_only_linear, FusedMultiTransformerWeightOnly).
+//   wo_dequant    : packed int8/int4 → bf16 [N, K] (weight_dequantize; large-M GEMMs).
+#include "common.h"
+
+// =====================================================================================
+// qkv_prep
+// =====================================================================================
+// qkv   : [B*S rows, (Hq + 2*Hk) * D] bf16, row stride `ld` (elements); modified in place
+// cache : k_cache / v_cache [B, Hk, maxS, D] bf16 (either may be null → no cache write)
+// pos0  : [B] int32 start position per batch (null → 0); token s of batch b sits at pos0[b]+s
+template <int D>
+__global__ __launch_bounds__(256) void qkv_prep_kernel(
+    bf16_t* __restrict__ qkv, long long ld, const bf16_t* __restrict__ bias,
+    bf16_t* __restrict__ kc, bf16_t* __restrict__ vc, const int* __restrict__ pos0, int B, int S,
+    int Hq, int Hk, int maxS, int rot, int neox, float log2_base) {
+  constexpr int E = D / 64;
+  const int H = Hq + 2 * Hk;
+  const long long wid = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wid >= (long long)B * S * H) return;
+  const int lane = threadIdx.x & 63;
+  const int h = (int)(wid % H);
+  const long long tok = wid / H;
+  const int b = (int)(tok / S), s = (int)(tok % S);
+  const int pos = (pos0 ? pos0[b] : 0) + s;
+  bf16_t* row = qkv + tok * ld + (long long)h * D;
+  const bf16_t* brow = bias ? bias + (long long)h * D : nullptr;
+  float y[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = lane + 64 * e;
+    float x = bf2f(row[i]) + (brow ? bf2f(brow[i]) : 0.f);
+    if (h < Hq + Hk && i < rot) {
+      const int half = rot >> 1;
+      int p, f;
+      float sgn;
+      if (neox) {
+        p = i < half ? i + half : i - half;
+        f = i < half ? i : i - half;
+        sgn = i < half ? -1.f : 1.f;
+      } else {
+        p = i ^ 1;
+        f = i >> 1;
+        sgn = (i & 1) ? 1.f : -1.f;
+      }
+      const float xp = bf2f(row[p]) + (brow ? bf2f(brow[p]) : 0.f);
+      const float inv_freq = exp2f(-(2.f * f / (float)rot) * log2_base);
+      float sn, cs;
+      sincosf((float)pos * inv_freq, &sn, &cs);
+      x = x * cs + sgn * xp * sn;
+    }
+    y[e] = x;
+  }
+  // every lane's loads (incl. rotary partners) precede any store in the single wave stream
+  bf16_t* dst = nullptr;
+  if (h >= Hq && pos < maxS) {
+    const bool is_v = h >= Hq + Hk;
+    const int kvh = is_v ? h - Hq - Hk : h - Hq;
+    bf16_t* c = is_v ? vc : kc;
+    if (c) dst = c + (((long long)b * Hk + kvh) * maxS + pos) * D;
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = lane + 64 * e;
+    const bf16_t v = f2bf(y[e]);
+    row[i] = v;
+    if (dst) dst[i] = v;
+  }
+}
+
+PIAMD_EXPORT int piamd_qkv_prep(void* qkv, long long ld, const void* bias, void* kc, void* vc,
+                                const int* pos0, int B, int S, int Hq, int Hk, int D, int maxS,
+                                int rot, int neox, float base, hipStream_t st) {
+  const long long waves = (long long)B * S * (Hq + 2 * Hk);
+  dim3 grid((unsigned)((waves + 3) / 4)), block(256);
+  const float l2b = log2f(base);
+  if (D == 128)
+    hipLaunchKernelGGL(qkv_prep_kernel<128>, grid, block, 0, st, (bf16_t*)qkv, ld,
+                       (const bf16_t*)bias, (bf16_t*)kc, (bf16_t*)vc, pos0, B, S, Hq, Hk, maxS, rot,
+                       neox, l2b);
+  else if (D == 64)
+    hipLaunchKernelGGL(qkv_prep_kernel<64>, grid, block, 0, st, (bf16_t*)qkv, ld,
+                       (const bf16_t*)bias, (bf16_t*)kc, (bf16_t*)vc, pos0, B, S, Hq, Hk, maxS, rot,
+                       neox, l2b);
+  else if (D == 256)
+    hipLaunchKernelGGL(qkv_prep_kernel<256>, grid, block, 0, st, (bf16_t*)qkv, ld,
+                       (const bf16_t*)bias, (bf16_t*)kc, (bf16_t*)vc, pos0, B, S, Hq, Hk, maxS, rot,
+                       neox, l2b);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+// =====================================================================================
+// decode attention (split-K)
+// =====================================================================================
+// q     : element (b, head, d) at q[b*ldq + head*D + d]   (head = hk*G + g)
+// kc,vc : [B, Hk, maxS, D]; keys [0, lens[b]) are attended
+// mask  : optional additive bf16 mask, element (b, key) at mask[b*ldm + key]
+// part  : [B, Hq, nsplit, D + 2] f32 partials (acc, m, l) when nsplit > 1
+// out   : element (b, head, d) at out[b*ldo + head*D + d]
+constexpr int DA_CHUNK_MAX = 512;
+
+template <int D, int G>
+__global__ __launch_bounds__(256) void decode_attn_kernel(
+    const bf16_t* __restrict__ q, long long ldq, const bf16_t* __restrict__ kc,
+    const bf16_t* __restrict__ vc, const int* __restrict__ lens, int Hk, int maxS, int chunk,
+    int nsplit, const bf16_t* __restrict__ mask, long long ldm, float scale_log2,
+    float* __restrict__ part, bf16_t* __restrict__ out, long long ldo) {
+  constexpr int LPK = D / 8;        // lanes per key row (16 B per lane)
+  constexpr int KPW = 64 / LPK;     // keys per wave per step
+  constexpr int KPI = KPW * 4;      // keys per workgroup per step
+  __shared__ float sc[G][DA_CHUNK_MAX];
+  __shared__ float red[4][G * D];
+  __shared__ float stat[2][G];
+  __shared__ float wred[8];
+
+  const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
+  const int Hq = Hk * G;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int sub = lane % LPK, kslot = w * KPW + lane / LPK;
+  const int len = lens[b];
+  const int k0 = split * chunk, k1 = min(len, k0 + chunk);
+  if (k0 >= k1) {  // workgroup-uniform: empty split
+    if (nsplit > 1 && tid < G) {
+      float* p = part + (((long long)b * Hq + hk * G + tid) * nsplit + split) * (D + 2);
+      p[D] = -INFINITY;
+      p[D + 1] = 0.f;
+    }
+    return;
+  }
+  const int n = k1 - k0;
+  const long long kvbase = ((long long)b * Hk + hk) * maxS * D;
+
+  float qf[G][8];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const u16x8 v = *(const u16x8*)(q + (long long)b * ldq + (long long)(hk * G + g) * D + sub * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qf[g][j] = bf2f(v[j]) * scale_log2;
+  }
+
+  // ---- scores: s = (q·k) * scale * log2(e) (+ mask * log2(e)) ----
+  constexpr int U = 4;
+  for (int base = kslot; base < n; base += KPI * U) {
+    u16x8 kr[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int kk = min(base + u * KPI, n - 1);  // clamped: every load is issued
+      kr[u] = *(const u16x8*)(kc + kvbase + (long long)(k0 + kk) * D + sub * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int kk = base + u * KPI;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        float d = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d += qf[g][j] * bf2f(kr[u][j]);
+#pragma unroll
+        for (int o = LPK / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+        if (sub == 0 && kk < n) {
+          if (mask) d += bf2f(mask[(long long)b * ldm + k0 + kk]) * 1.4426950408889634f;
+          sc[g][kk] = d;
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- softmax statistics over the chunk (base-2 domain) ----
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    float m = -INFINITY;
+    for (int i = tid; i < n; i += 256) m = fmaxf(m, sc[g][i]);
+    m = block_max<4>(m, wred);
+    float l = 0.f;
+    for (int i = tid; i < n; i += 256) {
+      const float p = exp2f(sc[g][i] - m);
+      sc[g][i] = p;
+      l += p;
+    }
+    l = block_sum<4>(l, wred);
+    if (tid == 0) {
+      stat[0][g] = m;
+      stat[1][g] = l;
+    }
+  }
+  __syncthreads();
+
+  // ---- P·V ----
+  float acc[G][8];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
+  for (int base = kslot; base < n; base += KPI * U) {
+    u16x8 vr[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int kk = min(base + u * KPI, n - 1);
+      vr[u] = *(const u16x8*)(vc + kvbase + (long long)(k0 + kk) * D + sub * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int kk = base + u * KPI;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const float p = kk < n ? sc[g][min(kk, n - 1)] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[g][j] += p * bf2f(vr[u][j]);
+      }
+    }
+  }
+  // reduce over the KPW key slots of the wave (lanes with equal `sub`)
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = acc[g][j];
+#pragma unroll
+      for (int o = LPK; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+      acc[g][j] = v;
+    }
+  if (lane < LPK) {
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[w][g * D + sub * 8 + j] = acc[g][j];
+  }
+  __syncthreads();
+  for (int i = tid; i < G * D; i += 256) {
+    const int g = i / D, d = i % D;
+    const float v = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+    const int head = hk * G + g;
+    if (nsplit == 1) {
+      out[(long long)b * ldo + (long long)head * D + d] = f2bf(v / stat[1][g]);
+    } else {
+      float* p = part + (((long long)b * Hq + head) * nsplit + split) * (D + 2);
+      p[d] = v;
+      if (d == 0) {
+        p[D] = stat[0][g];
+        p[D + 1] = stat[1][g];
+      }
+    }
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(D) void decode_combine_kernel(const float* __restrict__ part,
+                                                           int Hq, int nsplit,
+                                                           bf16_t* __restrict__ out,
+                                                           long long ldo) {
+  const int bh = blockIdx.x, b = bh / Hq, head = bh % Hq, d = threadIdx.x;
+  const float* p = part + (long long)bh * nsplit * (D + 2);
+  float m = -INFINITY;
+  for (int s = 0; s < nsplit; ++s) m = fmaxf(m, p[s * (D + 2) + D]);
+  float l = 0.f, a = 0.f;
+  for (int s = 0; s < nsplit; ++s) {
+    const float ms = p[s * (D + 2) + D];
+    if (ms == -INFINITY) continue;
+    const float wgt = exp2f(ms - m);
+    l += wgt * p[s * (D + 2) + D + 1];
+    a += wgt * p[s * (D + 2) + d];
+  }
+  out[(long long)b * ldo + (long long)head * D + d] = f2bf(a / l);
+}
+
+template <int D, int G>
+static void launch_decode(dim3 grid, hipStream_t st, const void* q, long long ldq, const void* kc,
+                          const void* vc, const int* lens, int Hk, int maxS, int chunk, int nsplit,
+                          const void* mask, long long ldm, float sl2, float* part, void* out,
+                          long long ldo) {
+  hipLaunchKernelGGL((decode_attn_kernel<D, G>), grid, dim3(256), 0, st, (const bf16_t*)q, ldq,
+                     (const bf16_t*)kc, (const bf16_t*)vc, lens, Hk, maxS, chunk, nsplit,
+                     (const bf16_t*)mask, ldm, sl2, part, (bf16_t*)out, ldo);
+}
+
+template <int D>
+static int dispatch_decode_g(int G, dim3 grid, hipStream_t st, const void* q, long long ldq,
+                             const void* kc, const void* vc, const int* lens, int Hk, int maxS,
+                             int chunk, int nsplit, const void* mask, long long ldm, float sl2,
+                             float* part, void* out, long long ldo) {
+  switch (G) {
+    case 1: launch_decode<D, 1>(grid, st, q, ldq, kc, vc, lens, Hk, maxS, chunk, nsplit, mask, ldm, sl2, part, out, ldo); break;
+    case 2: launch_decode<D, 2>(grid, st, q, ldq, kc, vc, lens, Hk, maxS, chunk, nsplit, mask, ldm, sl2, part, out, ldo); break;
+    case 4: launch_decode<D, 4>(grid, st, q, ldq, kc, vc, lens, Hk, maxS, chunk, nsplit, mask, ldm, sl2, part, out, ldo); break;
+    case 8: launch_decode<D, 8>(grid, st, q, ldq, kc, vc, lens, Hk, maxS, chunk, nsplit, mask, ldm, sl2, part, out, ldo); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return 0;
+}
+
+// chunk ≤ 512 keys per split; nsplit * chunk ≥ max length; part may be null iff nsplit == 1
+PIAMD_EXPORT int piamd_decode_attn(const void* q, long long ldq, const void* kc, const void* vc,
+                                   const int* lens, int B, int Hq, int Hk, int D, int maxS,
+                                   int chunk, int nsplit, const void* mask, long long ldm,
+                                   float scale, float* part, void* out, long long ldo,
+                                   hipStream_t st) {
+  if (Hk <= 0 || Hq % Hk || chunk <= 0 || chunk > DA_CHUNK_MAX || (nsplit > 1 && !part))
+    return (int)hipErrorInvalidValue;
+  const int G = Hq / Hk;
+  dim3 grid(nsplit, Hk, B);
+  const float sl2 = scale * 1.4426950408889634f;
+  int rc;
+  if (D == 128)
+    rc = dispatch_decode_g<128>(G, grid, st, q, ldq, kc, vc, lens, Hk, maxS, chunk, nsplit, mask, ldm, sl2, part, out, ldo);
+  else if (D == 64)
+    rc = dispatch_decode_g<64>(G, grid, st, q, ldq, kc, vc, lens, Hk, maxS, chunk, nsplit, mask, ldm, sl2, part, out, ldo);
+  else
+    return (int)hipErrorInvalidValue;
+  if (rc) return rc;
+  if (nsplit > 1) {
+    if (D == 128)
+      hipLaunchKernelGGL(decode_combine_kernel<128>, dim3(B * Hq), dim3(128), 0, st, part, Hq,
+                         nsplit, (bf16_t*)out, ldo);
+    else
+      hipLaunchKernelGGL(decode_combine_kernel<64>, dim3(B * Hq), dim3(64), 0, st, part, Hq,
+                         nsplit, (bf16_t*)out, ldo);
+  }
+  return (int)hipGetLastError();
+}
+
+// =====================================================================================
+// weight-only GEMM
+// =====================================================================================
+// Packed layout (produced by piamd_wo_pack / nn.quant.weight_quantize), n-tiles of 32 rows:
+//   int8: byte(n,k) at (((n/32)*(K/32) + k/32)*64 + (n%32) + 32*((k%32)/16))*16 + k%16
+//   int4: nibble(n,k) in byte (((n/32)*(K/64) + k/64)*64 + (n%32) + 32*((k%64)/32))*16 + (k%32)/2,
+//         low nibble for even k, two's complement in [-8, 7]
+// so each wave reads one contiguous 1 KB block per k-block: lane l holds row n0+(l&31), k-run
+// [kb*KB + (KB/2)*(l>>5), +KB/2) — exactly the bf16x8 B-operand runs of consecutive MFMAs.
+__device__ __forceinline__ bf16x8 i8x8_to_bf16(unsigned lo, unsigned hi) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r[j] = (__bf16)(float)((int)(lo << (24 - 8 * j)) >> 24);
+    r[4 + j] = (__bf16)(float)((int)(hi << (24 - 8 * j)) >> 24);
+  }
+  return r;
+}
+__device__ __forceinline__ bf16x8 i4x8_to_bf16(unsigned d) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (__bf16)(float)((int)(d << (28 - 4 * j)) >> 28);
+  return r;
+}
+__device__ __forceinline__ float act_apply(float v, int act) {
+  switch (act) {
+    case 1: return gelu_tanh(v);
+    case 2: return gelu_erf(v);
+    case 3: return fmaxf(v, 0.f);
+    case 4: return v / (1.f + __expf(-v));
+    default: return v;
+  }
+}
+
+// grid (N/32, ceil(M/32), KS); 256 threads = 4 waves splitting the k-blocks of this WG's K range.
+template <int BITS>
+__global__ __launch_bounds__(256) void wo_gemm_kernel(
+    const bf16_t* __restrict__ x, long long ldx, const unsigned char* __restrict__ wp,
+    const float* __restrict__ scale, const bf16_t* __restrict__ bias, bf16_t* __restrict__ y,
+    long long ldy, float* __restrict__ ws, int M, int N, int K, int act) {
+  constexpr int KB = BITS == 8 ? 32 : 64;   // k per block (per 16 B lane load)
+  constexpr int NMF = KB / 16;               // MFMAs per block
+  __shared__ float red[3][16][64];
+  const int nt = blockIdx.x, mt = blockIdx.y, kz = blockIdx.z, KS = gridDim.z;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nkb = K / KB;
+  const int kb_beg = (int)((long long)nkb * kz / KS), kb_end = (int)((long long)nkb * (kz + 1) / KS);
+  const int m = min(mt * 32 + (lane & 31), M - 1);  // rows ≥ M compute duplicates, never stored
+  const bf16_t* xr = x + (long long)m * ldx + (KB / 2) * (lane >> 5);
+  const uint4* wt = (const uint4*)wp + (long long)nt * nkb * 64 + lane;
+
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  constexpr int U = 4;
+  for (int kb0 = kb_beg + w; kb0 < kb_end; kb0 += 4 * U) {
+    uint4 wv[U];
+    bf16x8 xa[U][NMF];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int kb = min(kb0 + 4 * u, kb_end - 1);
+      wv[u] = wt[(long long)kb * 64];
+#pragma unroll
+      for (int i = 0; i < NMF; ++i) xa[u][i] = *(const bf16x8*)(xr + (long long)kb * KB + 8 * i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (kb0 + 4 * u >= kb_end) {  // zero the weight operand: the MFMA then adds nothing
+        wv[u] = make_uint4(0, 0, 0, 0);
+      }
+      if (BITS == 8) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[u][0], i8x8_to_bf16(wv[u].x, wv[u].y), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[u][1], i8x8_to_bf16(wv[u].z, wv[u].w), acc, 0, 0, 0);
+      } else {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[u][0], i4x8_to_bf16(wv[u].x), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[u][1], i4x8_to_bf16(wv[u].y), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[u][2], i4x8_to_bf16(wv[u].z), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[u][3], i4x8_to_bf16(wv[u].w), acc, 0, 0, 0);
+      }
+    }
+  }
+  if (w > 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[w - 1][r][lane] = acc[r];
+  }
+  __syncthreads();
+  if (w != 0) return;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] += red[0][r][lane] + red[1][r][lane] + red[2][r][lane];
+  // D layout: column (n) = lane & 31, row (m) = (r&3) + 8*(r>>2) + 4*(lane>>5)
+  const int n = nt * 32 + (lane & 31);
+  const float sc = scale[n];
+  const float bs = bias ? bf2f(bias[n]) : 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int mm = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    if (mm < M) {
+      if (KS == 1)
+        y[(long long)mm * ldy + n] = f2bf(act_apply(acc[r] * sc + bs, act));
+      else
+        ws[((long long)kz * M + mm) * N + n] = acc[r];
+    }
+  }
+}
+
+__global__ void wo_finalize_kernel(const float* __restrict__ ws, int KS, const float* __restrict__ scale,
+                                   const bf16_t* __restrict__ bias, bf16_t* __restrict__ y, long long ldy,
+                                   int M, int N, int act) {
+  const long long total = (long long)M * N;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int n = (int)(i % N);
+    const long long mm = i / N;
+    float v = 0.f;
+    for (int z = 0; z < KS; ++z) v += ws[(long long)z * total + i];
+    v = v * scale[n] + (bias ? bf2f(bias[n]) : 0.f);
+    y[mm * ldy + n] = f2bf(act_apply(v, act));
+  }
+}
+
+// ws: KS*M*N f32 when KS > 1. Requires N % 32 == 0 and K % (BITS==8 ? 32 : 64) == 0.
+PIAMD_EXPORT int piamd_wo_gemm(int bits, const void* x, long long ldx, const void* wp,
+                               const float* scale, const void* bias, void* y, long long ldy,
+                               float* ws, int M, int N, int K, int KS, int act, hipStream_t st) {
+  const int KB = bits == 8 ? 32 : 64;
+  if ((bits != 8 && bits != 4) || N % 32 || K % KB || KS < 1 || (KS > 1 && !ws) || M < 1)
+    return (int)hipErrorInvalidValue;
+  dim3 grid(N / 32, (M + 31) / 32, KS), block(256);
+  if (bits == 8)
+    hipLaunchKernelGGL(wo_gemm_kernel<8>, grid, block, 0, st, (const bf16_t*)x, ldx,
+                       (const unsigned char*)wp, scale, (const bf16_t*)bias, (bf16_t*)y, ldy, ws,
+                       M, N, K, act);
+  else
+    hipLaunchKernelGGL(wo_gemm_kernel<4>, grid, block, 0, st, (const bf16_t*)x, ldx,
+                       (const unsigned char*)wp, scale, (const bf16_t*)bias, (bf16_t*)y, ldy, ws,
+                       M, N, K, act);
+  if (KS > 1)
+    hipLaunchKernelGGL(wo_finalize_kernel, dim3(stride_grid((long long)M * N, 256)), dim3(256), 0,
+                       st, ws, KS, scale, (const bf16_t*)bias, (bf16_t*)y, ldy, M, N, act);
+  return (int)hipGetLastError();
+}
+
+// packed → bf16 [N, K] (row-major, no scale when scale == null)
+__global__ void wo_dequant_kernel(int bits, const unsigned char* __restrict__ wp,
+                                  const float* __restrict__ scale, bf16_t* __restrict__ out, int N,
+                                  int K) {
+  const long long total = (long long)N * K;
+  const int KB = bits == 8 ? 32 : 64, nkb = K / KB;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int n = (int)(i / K), k = (int)(i % K);
+    const long long blk = ((long long)(n / 32) * nkb + k / KB) * 64 + (n % 32) + 32 * ((k % KB) / (KB / 2));
+    int q;
+    if (bits == 8) {
+      q = (int)(signed char)wp[blk * 16 + k % 16];
+    } else {
+      const unsigned char byte = wp[blk * 16 + (k % 32) / 2];
+      q = (int)((unsigned)(k & 1 ? byte >> 4 : byte & 15) << 28) >> 28;
+    }
+    out[i] = f2bf((float)q * (scale ? scale[n] : 1.f));
+  }
+}
+
+PIAMD_EXPORT int piamd_wo_dequant(int bits, const void* wp, const float* scale, void* out, int N,
+                                  int K, hipStream_t st) {
+  hipLaunchKernelGGL(wo_dequant_kernel, dim3(stride_grid((long long)N * K, 256)), dim3(256), 0, st,
+                     bits, (const unsigned char*)wp, scale, (bf16_t*)out, N, K);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,486 @@
+"""``paddle.incubate.nn.functional`` — fused transformer ops on the MI355X kernel library.
+
+Parity: reference `python/paddle/incubate/nn/functional/fused_transformer.py`
+(fused_feedforward:31, fused_bias_dropout_residual_layer_norm:275, fused_multi_head_attention:465,
+fused_multi_transformer:833) and `fused_matmul_bias.py` (fused_matmul_bias, fused_linear), plus
+the fork's weight-only / MoE fused multi-transformer variants
+(`fluid/operators/fused/fused_multi_transformer_{weight_only,moe}_op.cu`).
+
+How they map onto the hardware (instead of the reference's one-CUDA-op-per-layer):
+* GEMMs: hipBLASLt (bf16 MFMA) — or the in-tree weight-only int8/int4 MFMA kernel;
+* LN + residual + bias (+dropout) → one pass of ``layernorm.hip`` (fused_add_layer_norm);
+* bias + activation → ``elementwise.hip``; QKV bias + RoPE + KV-cache write → ``infer.hip``;
+* context attention → ``flash_attn.hip``; decode attention → split-K ``infer.hip``;
+* the per-layer launch chain is replayed as a hipGraph by ``inference.generation``.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from ... import ops
+from ...ops import inference as _inf
+
+
+# ----------------------------------------------------------------------------- helpers
+def _to_additive_mask(mask, dtype):
+    if mask is None:
+        return None
+    if mask.dtype == torch.bool:
+        return torch.zeros(mask.shape, dtype=dtype, device=mask.device).masked_fill(~mask, float("-inf"))
+    if not mask.is_floating_point():
+        return torch.zeros(mask.shape, dtype=dtype, device=mask.device).masked_fill(mask == 0, float("-inf"))
+    return mask.to(dtype)
+
+
+def _dropout(x, p, training, mode):
+    if p == 0.0:
+        return x
+    if not training:
+        return x * (1.0 - p) if mode == "downscale_in_infer" else x
+    if mode == "downscale_in_infer":
+        return ops.dropout(x, p, True) * (1.0 - p)
+    return ops.dropout(x, p, True)
+
+
+def _ln(x, w, b, eps):
+    return ops.layer_norm(x, w, b, eps)
+
+
+def _mm(x, w, bias=None, transpose=False):
+    """x @ w (+ bias), w stored [in, out] (Paddle) unless ``transpose``."""
+    y = torch.matmul(x, w.t() if transpose else w)
+    return y + bias if bias is not None else y
+
+
+def attention_core(qkv, num_heads, num_kv_heads=None, attn_mask=None, causal=False,
+                   attn_dropout=0.0, training=False, mode="upscale_in_train", scale=None):
+    """qkv: [B, S, Hq+2Hk, D] → [B, S, Hq*D]. Flash path when there is no explicit mask and
+    no attention dropout; otherwise GEMM + fused masked softmax (``elementwise.hip``)."""
+    B, S, _, D = qkv.shape
+    hq, hk = num_heads, num_kv_heads or num_heads
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    if attn_mask is None and (attn_dropout == 0.0 or not training):
+        o = ops.flash_attention_packed(qkv, hq, hk, causal=causal, scale=scale)
+        return o.reshape(B, S, hq * D)
+    q = qkv[:, :, :hq].transpose(1, 2)
+    k = qkv[:, :, hq:hq + hk].transpose(1, 2)
+    v = qkv[:, :, hq + hk:].transpose(1, 2)
+    if hk != hq:
+        k = k.repeat_interleave(hq // hk, 1)
+        v = v.repeat_interleave(hq // hk, 1)
+    s = torch.matmul(q, k.transpose(-1, -2))
+    m = _to_additive_mask(attn_mask, s.dtype)
+    if m is not None:
+        m = m.expand(B, hq, S, s.shape[-1]) if m.dim() == 4 else m
+    p = ops.fused_softmax_mask(s, m.contiguous() if m is not None else None, scale, causal)
+    p = _dropout(p, attn_dropout, training, mode)
+    o = torch.matmul(p, v)
+    return o.transpose(1, 2).reshape(B, S, hq * D)
+
+
+# ----------------------------------------------------------------------------- small fused ops
+def fused_matmul_bias(x, y, bias=None, transpose_x=False, transpose_y=False, name=None):
+    """Reference `fused_matmul_bias.py:21` (cublasLt epilogue) — hipBLASLt bias epilogue via
+    torch.addmm on 2-D operands."""
+    a = x.transpose(-1, -2) if transpose_x else x
+    b = y.transpose(-1, -2) if transpose_y else y
+    if bias is not None and a.dim() >= 2 and b.dim() == 2:
+        lead = a.shape[:-1]
+        return torch.addmm(bias, a.reshape(-1, a.shape[-1]), b).reshape(*lead, b.shape[-1])
+    out = torch.matmul(a, b)
+    return out + bias if bias is not None else out
+
+
+def fused_linear(x, weight, bias=None, transpose_weight=False, name=None):
+    return fused_matmul_bias(x, weight, bias, False, transpose_weight)
+
+
+def fused_linear_activation(x, y, bias, trans_x=False, trans_y=False, activation=None):
+    out = fused_matmul_bias(x, y, None, trans_x, trans_y)
+    return ops.bias_act(out, bias, activation or "none")
+
+
+def fused_bias_dropout_residual_layer_norm(x, residual, bias=None, ln_scale=None, ln_bias=None,
+                                           dropout_rate=0.5, ln_epsilon=1e-5, training=True,
+                                           mode="upscale_in_train", name=None):
+    """y = layer_norm(residual + dropout(bias + x)) — one ``layernorm.hip`` pass."""
+    if mode == "downscale_in_infer" and dropout_rate > 0:
+        h = residual + _dropout(x + (bias if bias is not None else 0), dropout_rate, training, mode)
+        return _ln(h, ln_scale, ln_bias, ln_epsilon)
+    y, _ = ops.fused_add_layer_norm(x, residual, ln_scale, ln_bias, ln_epsilon, bias,
+                                    dropout_rate if training else 0.0, training)
+    return y
+
+
+def fused_feedforward(x, linear1_weight, linear2_weight, linear1_bias=None, linear2_bias=None,
+                      ln1_scale=None, ln1_bias=None, ln2_scale=None, ln2_bias=None,
+                      dropout1_rate=0.5, dropout2_rate=0.5, seed=None, activation="relu",
+                      ln1_epsilon=1e-5, ln2_epsilon=1e-5, pre_layer_norm=False, training=True,
+                      mode="upscale_in_train", ring_id=-1, add_residual=True, name=None, group=None):
+    residual = x
+    out = _ln(x, ln1_scale, ln1_bias, ln1_epsilon) if pre_layer_norm else x
+    h = ops.bias_act(_mm(out, linear1_weight), linear1_bias, activation)
+    h = _dropout(h, dropout1_rate, training, mode)
+    o = _mm(h, linear2_weight)
+    if group is not None:
+        torch.distributed.all_reduce(o, group=group)
+    if pre_layer_norm:
+        o = o + linear2_bias if linear2_bias is not None else o
+        o = _dropout(o, dropout2_rate, training, mode)
+        return residual + o if add_residual else o
+    return fused_bias_dropout_residual_layer_norm(
+        o, residual if add_residual else torch.zeros_like(o), linear2_bias, ln2_scale, ln2_bias,
+        dropout2_rate, ln2_epsilon, training, mode)
+
+
+def fused_multi_head_attention(x, qkv_weight, linear_weight, pre_layer_norm=False,
+                               pre_ln_scale=None, pre_ln_bias=None, ln_scale=None, ln_bias=None,
+                               pre_ln_epsilon=1e-5, qkv_bias=None, linear_bias=None, cache_kv=None,
+                               attn_mask=None, dropout_rate=0.5, attn_dropout_rate=0.5,
+                               dropout_seed=None, attn_dropout_seed=None, ln_epsilon=1e-5,
+                               training=True, mode="upscale_in_train", ring_id=-1,
+                               add_residual=True, name=None, group=None, causal=False,
+                               transpose_qkv_wb=False, num_heads=None):
+    """qkv_weight [3, H, D, E] (or [E, 3E] with ``transpose_qkv_wb``), linear_weight [E, E].
+    With ``cache_kv`` ([2, B, H, S_cache, D]) returns (out, new_cache_kv) like the reference."""
+    B, S, E = x.shape
+    residual = x
+    out = _ln(x, pre_ln_scale, pre_ln_bias, pre_ln_epsilon) if pre_layer_norm else x
+    if transpose_qkv_wb:
+        H = num_heads
+        D = E // H
+        qkv = _mm(out, qkv_weight)
+    else:
+        _, H, D, _ = qkv_weight.shape
+        qkv = F.linear(out, qkv_weight.reshape(3 * H * D, E))
+    if qkv_bias is not None:
+        qkv = qkv + qkv_bias.reshape(-1)
+    qkv = qkv.reshape(B, S, 3 * H, D)
+    new_cache = None
+    if cache_kv is not None:
+        k = torch.cat([cache_kv[0], qkv[:, :, H:2 * H].transpose(1, 2)], 2)
+        v = torch.cat([cache_kv[1], qkv[:, :, 2 * H:].transpose(1, 2)], 2)
+        new_cache = torch.stack([k, v])
+        q = qkv[:, :, :H].transpose(1, 2)
+        s = torch.matmul(q, k.transpose(-1, -2))
+        m = _to_additive_mask(attn_mask, s.dtype)
+        p = ops.fused_softmax_mask(s, m.expand_as(s).contiguous() if m is not None else None,
+                                   1.0 / math.sqrt(D))
+        p = _dropout(p, attn_dropout_rate, training, mode)
+        a = torch.matmul(p, v).transpose(1, 2).reshape(B, S, H * D)
+    else:
+        a = attention_core(qkv, H, H, attn_mask, causal, attn_dropout_rate, training, mode)
+    o = _mm(a, linear_weight)
+    if group is not None:
+        torch.distributed.all_reduce(o, group=group)
+    if pre_layer_norm:
+        o = o + linear_bias if linear_bias is not None else o
+        o = _dropout(o, dropout_rate, training, mode)
+        res = residual + o if add_residual else o
+    else:
+        res = fused_bias_dropout_residual_layer_norm(
+            o, residual if add_residual else torch.zeros_like(o), linear_bias, ln_scale, ln_bias,
+            dropout_rate, ln_epsilon, training, mode)
+    return (res, new_cache) if cache_kv is not None else res
+
+
+# ----------------------------------------------------------------------------- multi-transformer
+class _Linear:
+    """A projection: bf16 weight ([in, out] Paddle layout, or [out, in] when ``trans``) or a
+    weight-only packed weight + scale."""
+    __slots__ = ("w", "scale", "bits", "trans")
+
+    def __init__(self, w, scale=None, bits=0, trans=False):
+        self.w, self.scale, self.bits, self.trans = w, scale, bits, trans
+
+    def __call__(self, x, bias=None, act="none"):
+        if self.bits:
+            return _inf.weight_only_linear(x, self.w, bias, self.scale,
+                                           "int4" if self.bits == 4 else "int8", act)
+        y = F.linear(x, self.w) if self.trans else torch.matmul(x, self.w)
+        if act != "none":
+            return ops.bias_act(y, bias, act)
+        return y if bias is None else y + bias
+
+
+def _lin(w, scale=None, bits=0, trans=False):
+    return _Linear(w, scale, bits, trans)
+
+
+def multi_transformer_forward(x, layers, num_heads, num_kv_heads=None, pre_layer_norm=True,
+                              epsilon=1e-5, caches=None, pos=None, lens=None, attn_mask=None,
+                              decode=False, activation="gelu", rotary_dim=0, neox_rotary=True,
+                              rope_base=10000.0, causal=None, group=None, max_len=None,
+                              moe_fn=None):
+    """Core of every fused multi-transformer variant.
+
+    x: [B, S, E]; ``layers``: list of dicts with keys ln_scale, ln_bias, qkv (_Linear producing
+    [(Hq+2Hk)*D]), qkv_bias, out (_Linear), out_bias, ffn_ln_scale, ffn_ln_bias, ffn1, ffn1_bias,
+    ffn2, ffn2_bias (or ``moe`` — a callable replacing the FFN). ``caches``: per layer
+    (k_cache, v_cache) [B, Hk, maxS, D]. Context (decode=False): writes positions
+    pos[b] + [0, S). Decode (S == 1): writes position pos[b] and attends to keys [0, lens[b]).
+    ``pos``/``lens`` are device int32 [B] (graph-replayable).
+    """
+    B, S, E = x.shape
+    hq = num_heads
+    hk = num_kv_heads or num_heads
+    D = E // hq if layers[0].get("head_dim") is None else layers[0]["head_dim"]
+    T = B * S
+    act = {"gelu": "gelu", "relu": "relu", "silu": "silu", "swiglu": "silu",
+           "geglu": "gelu"}.get(activation, activation)
+    gated = activation in ("swiglu", "geglu")
+    causal = (attn_mask is None) if causal is None else causal
+    if decode and attn_mask is not None:
+        attn_mask = _to_additive_mask(attn_mask, x.dtype).reshape(B, -1).contiguous()
+    xf = x.reshape(T, E)
+    residual = xf
+    pending = None  # (ffn2_out, ffn2_bias) to fold into the next LN pass
+    n = len(layers)
+    for li, L in enumerate(layers):
+        if pre_layer_norm:
+            if pending is None:
+                xn = _ln(residual, L["ln_scale"], L["ln_bias"], epsilon)
+            else:
+                xn, residual = ops.fused_add_layer_norm(pending[0], residual, L["ln_scale"],
+                                                        L["ln_bias"], epsilon, pending[1])
+        else:
+            if pending is not None:
+                residual, _ = ops.fused_add_layer_norm(pending[0], residual, pending[2],
+                                                       pending[3], epsilon, pending[1])
+            xn = residual
+        pending = None
+        qkv = L["qkv"](xn)  # [T, (Hq+2Hk)*D]
+        kc, vc = caches[li] if caches is not None else (None, None)
+        ops.qkv_prep(qkv, L.get("qkv_bias"), kc, vc, pos, B, S, hq, hk, D, rotary_dim,
+                     neox_rotary, rope_base)
+        if decode:
+            a = _inf.decode_attention(qkv, kc, vc, lens, hq, hk, attn_mask, max_len=max_len)
+        else:
+            a = attention_core(qkv.view(B, S, hq + 2 * hk, D), hq, hk, attn_mask, causal)
+            a = a.reshape(T, hq * D)
+        o = L["out"](a)
+        if group is not None:
+            torch.distributed.all_reduce(o, group=group)
+        if pre_layer_norm:
+            yn, residual = ops.fused_add_layer_norm(o, residual, L["ffn_ln_scale"],
+                                                    L["ffn_ln_bias"], epsilon, L.get("out_bias"))
+        else:
+            residual, _ = ops.fused_add_layer_norm(o, residual, L["ln_scale"], L["ln_bias"],
+                                                   epsilon, L.get("out_bias"))
+            yn = residual
+        if moe_fn is not None and L.get("moe") is not None:
+            f2 = L["moe"](yn)
+            b2 = None
+        else:
+            if gated:
+                h = L["ffn1"](yn, L.get("ffn1_bias"))
+                g, u = h.chunk(2, -1)
+                h = ops.bias_act(g.contiguous(), None, act) * u
+            else:
+                h = L["ffn1"](yn, L.get("ffn1_bias"), act)
+            f2 = L["ffn2"](h)
+            b2 = L.get("ffn2_bias")
+        if group is not None:
+            torch.distributed.all_reduce(f2, group=group)
+        if pre_layer_norm:
+            pending = (f2, b2)
+        else:
+            pending = (f2, b2, L["ffn_ln_scale"], L["ffn_ln_bias"])
+    if pre_layer_norm:
+        out = residual + pending[0]
+        if pending[1] is not None:
+            out = out + pending[1]
+    else:
+        out, _ = ops.fused_add_layer_norm(pending[0], residual, pending[2], pending[3], epsilon,
+                                          pending[1])
+    return out.reshape(B, S, E)
+
+
+def _qkv_linear(w, trans_qkvw, scale=None, bits=0):
+    if bits:
+        return _lin(w, scale, bits)
+    if trans_qkvw:  # [3, H, D, E] (or [(Hq+2Hk), D, E])
+        return _lin(w.reshape(-1, w.shape[-1]), trans=True)
+    return _lin(w.reshape(w.shape[0], -1))  # [E, 3, H, D]
+
+
+def _positions(B, time_step, seq_lens, S, device, decode):
+    """Reference semantics: context writes cache positions [0, S); decode writes position
+    ``time_step`` (or per-batch ``seq_lens``) and attends to keys [0, pos]."""
+    if decode:
+        if seq_lens is not None:
+            p = seq_lens.reshape(-1).to(device=device, dtype=torch.int32)
+        else:
+            t = int(time_step.reshape(-1)[0]) if torch.is_tensor(time_step) else int(time_step)
+            p = torch.full((B,), t, dtype=torch.int32, device=device)
+        return p, p + 1
+    return torch.zeros(B, dtype=torch.int32, device=device), None
+
+
+def _caches_from(cache_kvs):
+    if cache_kvs is None:
+        return None
+    return [(c[0], c[1]) for c in cache_kvs]
+
+
+def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, linear_weights,
+                            linear_biases, ffn_ln_scales, ffn_ln_biases, ffn1_weights, ffn1_biases,
+                            ffn2_weights, ffn2_biases, pre_layer_norm=True, epsilon=1e-05,
+                            cache_kvs=None, beam_offset=None, seq_lens=None, time_step=None,
+                            attn_mask=None, dropout_rate=0.0, activation="gelu", training=False,
+                            mode="upscale_in_train", trans_qkvw=True, ring_id=-1, name=None,
+                            num_kv_heads=None, rotary_emb_dims=0, use_neox_rotary_style=True,
+                            rope_base=10000.0, group=None):
+    """Reference `incubate/nn/functional/fused_transformer.py:833`. cache_kvs: per layer
+    [2, B, Hk, max_seq_len, D], updated in place; returns (out, cache_kvs) when given."""
+    B, S, E = x.shape
+    w0 = qkv_weights[0]
+    if trans_qkvw:
+        nh_total, D = w0.shape[-3] * (w0.shape[0] if w0.dim() == 4 else 1), w0.shape[-2]
+    else:
+        nh_total, D = w0.numel() // E // w0.shape[-1], w0.shape[-1]
+    hk = num_kv_heads
+    hq = nh_total // 3 if hk is None else nh_total - 2 * hk
+    hk = hk or hq
+    decode = time_step is not None
+    if beam_offset is not None and cache_kvs is not None:
+        src = beam_offset.reshape(-1)[:B].long().to(x.device)
+        for c in cache_kvs:
+            c.copy_(c.index_select(1, src))
+    pos, lens = _positions(B, time_step, seq_lens, S, x.device, decode)
+    layers = []
+    for i in range(len(qkv_weights)):
+        layers.append(dict(
+            head_dim=D, ln_scale=ln_scales[i], ln_bias=ln_biases[i] if ln_biases else None,
+            qkv=_qkv_linear(qkv_weights[i], trans_qkvw),
+            qkv_bias=qkv_biases[i].reshape(-1) if qkv_biases and qkv_biases[i] is not None else None,
+            out=_lin(linear_weights[i]), out_bias=linear_biases[i] if linear_biases else None,
+            ffn_ln_scale=ffn_ln_scales[i], ffn_ln_bias=ffn_ln_biases[i] if ffn_ln_biases else None,
+            ffn1=_lin(ffn1_weights[i]), ffn1_bias=ffn1_biases[i] if ffn1_biases else None,
+            ffn2=_lin(ffn2_weights[i]), ffn2_bias=ffn2_biases[i] if ffn2_biases else None))
+    with torch.no_grad():
+        out = multi_transformer_forward(
+            x, layers, hq, hk, pre_layer_norm, epsilon, _caches_from(cache_kvs), pos, lens,
+            attn_mask, decode, activation, rotary_emb_dims, use_neox_rotary_style, rope_base,
+            causal=(attn_mask is None), group=group)
+    return (out, cache_kvs) if cache_kvs is not None else out
+
+
+def fused_multi_transformer_weight_only(x, ln_scales, ln_biases, qkv_weights, qkv_scales,
+                                        qkv_biases, linear_weights, linear_scales, linear_biases,
+                                        ffn_ln_scales, ffn_ln_biases, ffn1_weights, ffn1_scales,
+                                        ffn1_biases, ffn2_weights, ffn2_scales, ffn2_biases,
+                                        pre_layer_norm=True, epsilon=1e-5, cache_kvs=None,
+                                        beam_offset=None, seq_lens=None, time_step=None,
+                                        attn_mask=None, activation="gelu", weight_dtype="int8",
+                                        num_heads=None, num_kv_heads=None, rotary_emb_dims=0,
+                                        use_neox_rotary_style=True, rope_base=10000.0, group=None):
+    """Reference `fused_multi_transformer_weight_only_op.cu`: every projection is a
+    weight-only int8/int4 GEMM (packed [N, K] / [N/2, K] weights, per-channel f32 scales)."""
+    B, S, E = x.shape
+    bits = 4 if weight_dtype == "int4" else 8
+    hk = num_kv_heads or num_heads
+    D = E // num_heads
+    decode = time_step is not None
+    pos, lens = _positions(B, time_step, seq_lens, S, x.device, decode)
+    layers = []
+    for i in range(len(qkv_weights)):
+        layers.append(dict(
+            head_dim=D, ln_scale=ln_scales[i], ln_bias=ln_biases[i],
+            qkv=_lin(qkv_weights[i], qkv_scales[i], bits),
+            qkv_bias=qkv_biases[i].reshape(-1) if qkv_biases[i] is not None else None,
+            out=_lin(linear_weights[i], linear_scales[i], bits), out_bias=linear_biases[i],
+            ffn_ln_scale=ffn_ln_scales[i], ffn_ln_bias=ffn_ln_biases[i],
+            ffn1=_lin(ffn1_weights[i], ffn1_scales[i], bits), ffn1_bias=ffn1_biases[i],
+            ffn2=_lin(ffn2_weights[i], ffn2_scales[i], bits), ffn2_bias=ffn2_biases[i]))
+    with torch.no_grad():
+        out = multi_transformer_forward(
+            x, layers, num_heads, hk, pre_layer_norm, epsilon, _caches_from(cache_kvs), pos, lens,
+            attn_mask, decode, activation, rotary_emb_dims, use_neox_rotary_style, rope_base,
+            causal=(attn_mask is None), group=group)
+    return (out, cache_kvs) if cache_kvs is not None else out
+
+
+# ----------------------------------------------------------------------------- misc fused ops
+def fused_rotary_position_embedding(q, k=None, v=None, sin=None, cos=None, position_ids=None,
+                                    use_neox_rotary_style=True, rotary_base=10000.0):
+    """q/k/v: [B, S, H, D]; rotates q and k (v passes through)."""
+    outs = []
+    for t in (q, k, v):
+        if t is None:
+            outs.append(None)
+            continue
+        if t is v:
+            outs.append(v)
+            continue
+        B, S, H, D = t.shape
+        pos = position_ids[0].cpu() if position_ids is not None else torch.arange(S)
+        if sin is not None and cos is not None:
+            c = cos.reshape(S, -1)[:, :D].float().to(t.device)
+            s_ = sin.reshape(S, -1)[:, :D].float().to(t.device)
+            if use_neox_rotary_style:
+                x1, x2 = t.float()[..., :D // 2], t.float()[..., D // 2:]
+                rot = torch.cat([-x2, x1], -1)
+            else:
+                x1, x2 = t.float()[..., 0::2], t.float()[..., 1::2]
+                rot = torch.stack([-x2, x1], -1).flatten(-2)
+            outs.append((t.float() * c[None, :, None] + rot * s_[None, :, None]).to(t.dtype))
+        else:
+            r = _inf._rope_ref(t.float().transpose(1, 2).cpu(), pos, D, use_neox_rotary_style,
+                               rotary_base)
+            outs.append(r.transpose(1, 2).to(t.device, t.dtype))
+    return tuple(outs)
+
+
+def masked_multihead_attention(x, cache_kv=None, src_mask=None, sequence_lengths=None,
+                               rotary_tensor=None, beam_cache_offset=None, seq_len=1,
+                               rotary_emb_dims=0, use_neox_rotary_style=False, num_heads=None,
+                               num_kv_heads=None, rope_base=10000.0):
+    """Reference mmha: x [B, (Hq+2Hk)*D] (one new token, QKV bias already added), cache_kv
+    [2, B, Hk, maxS, D]; sequence_lengths [B] = cached length (the new token goes there).
+    Returns (out [B, Hq*D], cache_kv)."""
+    B = x.shape[0]
+    _, _, hk, maxS, D = cache_kv.shape
+    hq = num_heads or (x.shape[1] // D - 2 * hk)
+    if sequence_lengths is None:
+        raise ValueError("masked_multihead_attention needs sequence_lengths")
+    pos = sequence_lengths.reshape(-1).to(x.device, torch.int32)
+    qkv = x.clone()
+    ops.qkv_prep(qkv, None, cache_kv[0], cache_kv[1], pos, B, 1, hq, hk, D, rotary_emb_dims,
+                 use_neox_rotary_style, rope_base)
+    out = _inf.decode_attention(qkv, cache_kv[0], cache_kv[1], pos + 1, hq, hk, src_mask)
+    return out, cache_kv
+
+
+def variable_length_memory_efficient_attention(query, key, value, seq_lens, kv_seq_lens,
+                                               mask=None, scale=None, causal=False):
+    """query [B, H, S, D], key/value [B, Hk, Sk, D]; per-batch valid lengths. Each batch is
+    attended over its own prefix with the flash kernel (reference
+    `variable_length_memory_efficient_attention.cu`)."""
+    B, H, S, D = query.shape
+    out = torch.zeros_like(query)
+    for b in range(B):
+        sq, sk = int(seq_lens.reshape(-1)[b]), int(kv_seq_lens.reshape(-1)[b])
+        if sq == 0:
+            continue
+        q = query[b:b + 1, :, :sq].transpose(1, 2)
+        k = key[b:b + 1, :, :sk].transpose(1, 2)
+        v = value[b:b + 1, :, :sk].transpose(1, 2)
+        if mask is None:
+            o = ops.flash_attention(q.contiguous(), k.contiguous(), v.contiguous(), causal, scale)
+        else:
+            o = ops.attention_reference(q, k, v, causal, scale,
+                                        mask[b:b + 1, :, :sq, :sk])
+        out[b, :, :sq] = o.transpose(1, 2)
+    return out
+
+
+def softmax_mask_fuse(x, mask, name=None):
+    return ops.fused_softmax_mask(x, mask)
+
+
+def softmax_mask_fuse_upper_triangle(x):
+    return ops.fused_softmax_mask(x, None, 1.0, causal=True)

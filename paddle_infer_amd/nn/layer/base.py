@@ -57,7 +57,8 @@ class ParamAttr:
 
 
 def _as_param(t: torch.Tensor, name: str, trainable=True, need_clip=True) -> torch.nn.Parameter:
-    p = torch.nn.Parameter(t, requires_grad=trainable)
+    # integer parameters (quantized weights) cannot carry gradients
+    p = torch.nn.Parameter(t, requires_grad=trainable and (t.is_floating_point() or t.is_complex()))
     p.pd_name = name  # torch reserves Tensor.name
     p.need_clip = need_clip
     p.optimize_attr = {"learning_rate": 1.0}

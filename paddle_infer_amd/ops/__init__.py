@@ -9,3 +9,5 @@ from .activation import bias_act, gelu, dropout, fused_softmax_mask  # noqa: F40
 from .loss import softmax_cross_entropy  # noqa: F401
 from .optim import adamw_flat, momentum_flat, sumsq  # noqa: F401
 from . import _lib  # noqa: F401
+from .inference import (qkv_prep, decode_attention, weight_quantize, weight_dequantize,  # noqa: F401
+                        weight_only_linear, llm_int8_linear)

@@ -61,14 +61,14 @@ _SIGS = {
                              c_int, c_int, c_int, c_int, c_int, c_int,
                              c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll,
                              c_ll, c_ll, c_ll, c_float, c_int, c_void_p],
-    "piamd_decode_attn": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
-                          c_int, c_int, c_int, c_float, c_void_p],
-    "piamd_gemm_bf16": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                        c_int, c_int, c_int, c_void_p],
-    "piamd_wo_gemm": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
-                      c_int, c_int, c_void_p],
-    "piamd_rope": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_ll, c_ll, c_ll,
-                   c_int, c_void_p],
+    "piamd_qkv_prep": [c_void_p, c_ll, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                       c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p],
+    "piamd_decode_attn": [c_void_p, c_ll, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                          c_int, c_int, c_int, c_void_p, c_ll, c_float, c_void_p, c_void_p, c_ll,
+                          c_void_p],
+    "piamd_wo_gemm": [c_int, c_void_p, c_ll, c_void_p, c_void_p, c_void_p, c_void_p, c_ll,
+                      c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "piamd_wo_dequant": [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "piamd_embedding_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_ll, c_void_p],
 }
 

@@ -1,0 +1,251 @@
+"""Serving-path ops backed by ``csrc/kernels/infer.hip``.
+
+* :func:`qkv_prep` — QKV bias + rotary embedding + KV-cache write, in place on the packed
+  QKV GEMM output (reference `fused_multi_transformer_op.cu.h`: add bias / rotary_qk /
+  write_cache_kv).
+* :func:`decode_attention` — one new token per sequence attending to its KV cache (reference
+  `masked_multihead_attention_kernel`), split-K over the cache with a combine pass.
+* :func:`weight_quantize` / :func:`weight_dequantize` / :func:`weight_only_linear` — weight-only
+  int8/int4 (reference `python/paddle/nn/quant/quantized_linear.py`). The quantized weight keeps
+  Paddle's logical shape ([N, K] for int8, [N/2, K] for int4, from an input of [K, N]) but its
+  bytes are in the MI355X MFMA-tile order documented in infer.hip, exactly as the reference's own
+  weight_quantize emits a CUTLASS-interleaved order for sm80.
+
+Every op has a PyTorch reference path (CPU tensors) used by the CPU tests and as the numerics
+reference of the GPU tests.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+from .activation import ACTS, _ref_act
+
+
+# ------------------------------------------------------------------------------- rotary / prep
+def _rope_ref(x, pos, rot, neox, base):
+    """x: [..., T, D] float; pos: [T] positions."""
+    if rot <= 0:
+        return x
+    half = rot // 2
+    inv = base ** (-(2.0 * torch.arange(half, dtype=torch.float64) / rot))
+    ang = pos.double()[:, None] * inv[None, :]  # [T, half]
+    cos, sin = ang.cos().float(), ang.sin().float()
+    xr, xp = x[..., :rot], x[..., rot:]
+    if neox:
+        a, b = xr[..., :half], xr[..., half:]
+        out = torch.cat([a * cos - b * sin, b * cos + a * sin], -1)
+    else:
+        a, b = xr[..., 0::2], xr[..., 1::2]
+        out = torch.stack([a * cos - b * sin, b * cos + a * sin], -1).flatten(-2)
+    return torch.cat([out, xp], -1)
+
+
+def qkv_prep(qkv, bias, k_cache, v_cache, pos0, B, S, Hq, Hk, D, rot_dim=0, neox=True,
+             base=10000.0):
+    """In place on ``qkv`` ([B*S, (Hq+2Hk)*D] rows, any row stride): add bias, rotate q/k,
+    write k/v into ``k_cache``/``v_cache`` ([B, Hk, maxS, D]) at positions pos0[b] + s."""
+    H = Hq + 2 * Hk
+    if qkv.is_cuda:
+        assert qkv.dtype == torch.bfloat16 and qkv.stride(-1) == 1 and qkv.shape[-1] >= H * D
+        if k_cache is not None:
+            assert k_cache.is_contiguous() and v_cache.is_contiguous() and k_cache.shape[1] == Hk
+        if pos0 is not None:
+            assert pos0.dtype == torch.int32 and pos0.is_cuda and pos0.numel() >= B
+        maxS = k_cache.shape[2] if k_cache is not None else 0
+        _lib.call("piamd_qkv_prep", qkv.data_ptr(), qkv.stride(0), _lib.ptr(bias),
+                  _lib.ptr(k_cache), _lib.ptr(v_cache), _lib.ptr(pos0), B, S, Hq, Hk, D, maxS,
+                  int(rot_dim), int(bool(neox)), float(base), _lib.stream())
+        return qkv
+    x = qkv[:, :H * D].float().view(B, S, H, D)
+    if bias is not None:
+        x = x + bias.float().view(H, D)
+    p0 = pos0.long().cpu() if pos0 is not None else torch.zeros(B, dtype=torch.long)
+    for b in range(B):
+        pos = p0[b] + torch.arange(S)
+        qk = x[b, :, :Hq + Hk].transpose(0, 1)  # [H', S, D]
+        x[b, :, :Hq + Hk] = _rope_ref(qk, pos, rot_dim, neox, base).transpose(0, 1)
+        if k_cache is not None:
+            maxS = k_cache.shape[2]
+            ok = pos < maxS
+            kk = x[b, :, Hq:Hq + Hk].transpose(0, 1)[:, ok]
+            vv = x[b, :, Hq + Hk:].transpose(0, 1)[:, ok]
+            k_cache[b, :, pos[ok]] = kk.to(k_cache.dtype)
+            v_cache[b, :, pos[ok]] = vv.to(v_cache.dtype)
+    qkv[:, :H * D] = x.view(B * S, H * D).to(qkv.dtype)
+    return qkv
+
+
+# ------------------------------------------------------------------------------- decode attn
+_PART_CACHE = {}
+
+
+def decode_chunking(max_len, chunk=None):
+    if chunk is None:
+        chunk = 256 if max_len > 1024 else 128
+    chunk = max(16, min(512, chunk))
+    return chunk, max(1, -(-max_len // chunk))
+
+
+def decode_attention(q, k_cache, v_cache, lens, Hq, Hk, mask=None, scale=None, out=None,
+                     max_len=None, chunk=None):
+    """q: [B, >=Hq*D] rows (head h at columns h*D); caches [B, Hk, maxS, D]; lens: [B] int32
+    number of valid keys (including the token just written). Returns out [B, Hq*D].
+    ``max_len`` bounds lens (defaults to the cache capacity, which is what a captured graph
+    needs); it sets the split count."""
+    B, _, maxS, D = k_cache.shape
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    if out is None:
+        out = torch.empty((B, Hq * D), dtype=q.dtype, device=q.device)
+    if q.is_cuda:
+        assert q.dtype == torch.bfloat16 and q.stride(-1) == 1 and k_cache.is_contiguous() \
+            and v_cache.is_contiguous() and lens.dtype == torch.int32 and lens.is_cuda
+        assert Hq % Hk == 0 and (Hq // Hk) in (1, 2, 4, 8) and D in (64, 128)
+        ck, ns = decode_chunking(max_len or maxS, chunk)
+        part = None
+        if ns > 1:
+            key = (q.device, B, Hq, ns, D)
+            part = _PART_CACHE.get(key)
+            if part is None:
+                part = _PART_CACHE[key] = torch.empty(B * Hq * ns * (D + 2), dtype=torch.float32,
+                                                      device=q.device)
+        ldm = 0
+        if mask is not None:
+            mask = mask.reshape(B, -1)
+            assert mask.dtype == torch.bfloat16 and mask.stride(-1) == 1
+            ldm = mask.stride(0)
+        _lib.call("piamd_decode_attn", q.data_ptr(), q.stride(0), k_cache.data_ptr(),
+                  v_cache.data_ptr(), lens.data_ptr(), B, Hq, Hk, D, maxS, ck, ns, _lib.ptr(mask),
+                  ldm, float(scale), _lib.ptr(part), out.data_ptr(), out.stride(0), _lib.stream())
+        return out
+    G = Hq // Hk
+    for b in range(B):
+        n = int(lens[b])
+        qb = q[b, :Hq * D].float().view(Hq, 1, D)
+        kb = k_cache[b, :, :n].float().repeat_interleave(G, 0)
+        vb = v_cache[b, :, :n].float().repeat_interleave(G, 0)
+        s = (qb @ kb.transpose(-1, -2)) * scale
+        if mask is not None:
+            s = s + mask.reshape(B, -1)[b, :n].float()
+        out[b] = (torch.softmax(s, -1) @ vb).reshape(-1).to(out.dtype)
+    return out
+
+
+# ------------------------------------------------------------------------------- weight-only
+def _pack(q, bits):
+    """int8 q [N, K] (values in the bit range) → packed uint8 bytes in MFMA-tile order."""
+    N, K = q.shape
+    if bits == 8:
+        assert N % 32 == 0 and K % 32 == 0, "weight-only int8 needs N % 32 == 0 and K % 32 == 0"
+        t = q.view(N // 32, 32, K // 32, 2, 16).permute(0, 2, 3, 1, 4)
+        return t.contiguous().view(torch.uint8).reshape(N, K)
+    assert N % 32 == 0 and K % 64 == 0, "weight-only int4 needs N % 32 == 0 and K % 64 == 0"
+    u = (q.to(torch.int16) & 15).to(torch.uint8)
+    t = u.view(N // 32, 32, K // 64, 2, 16, 2).permute(0, 2, 3, 1, 4, 5).contiguous()
+    packed = t[..., 0] | (t[..., 1] << 4)
+    return packed.reshape(N // 2, K)
+
+
+def _unpack(wp, bits, N, K):
+    """Inverse of :func:`_pack` → int8 [N, K]."""
+    if bits == 8:
+        t = wp.reshape(N // 32, K // 32, 2, 32, 16).permute(0, 3, 1, 2, 4)
+        return t.contiguous().view(torch.int8).reshape(N, K)
+    b = wp.reshape(N // 32, K // 64, 2, 32, 16)
+    lo = (b & 15).to(torch.int16)
+    hi = (b >> 4).to(torch.int16)
+    t = torch.stack([lo, hi], -1)
+    t = torch.where(t >= 8, t - 16, t).to(torch.int8)
+    return t.permute(0, 3, 1, 2, 4, 5).contiguous().reshape(N, K)
+
+
+def weight_quantize(x, algo="weight_only_int8"):
+    """x: [K, N] float → (packed weight, scale[N] f32). Symmetric per-output-channel."""
+    bits = 4 if algo == "weight_only_int4" else 8
+    w = x.float().t().contiguous()  # [N, K]
+    qmax = 7.0 if bits == 4 else 127.0
+    scale = w.abs().amax(1).clamp_min(1e-10) / qmax
+    q = torch.round(w / scale[:, None]).clamp(-qmax - (1 if bits == 4 else 0), qmax).to(torch.int8)
+    return _pack(q, bits), scale
+
+
+def weight_dequantize(x, scale, algo="weight_only_int8", out_dtype="bfloat16"):
+    """Packed weight → dequantized [K, N] (Paddle's layout of the original weight)."""
+    bits = 4 if algo == "weight_only_int4" else 8
+    N = scale.shape[0]
+    K = x.numel() * (2 if bits == 4 else 1) // N
+    from ..framework.dtype import to_torch_dtype
+    dt = to_torch_dtype(out_dtype)
+    if x.is_cuda:
+        out = torch.empty((N, K), dtype=torch.bfloat16, device=x.device)
+        _lib.call("piamd_wo_dequant", bits, x.data_ptr(), scale.float().contiguous().data_ptr(),
+                  out.data_ptr(), N, K, _lib.stream())
+        return out.t().to(dt)
+    return (_unpack(x, bits, N, K).float() * scale.float()[:, None]).t().to(dt)
+
+
+_WS = {}
+
+
+def weight_only_linear(x, weight, bias=None, weight_scale=None, weight_dtype="int8",
+                       act_method="none"):
+    """y = act(x @ dequant(weight)ᵀ + bias); x [..., K], weight packed [N, K] / [N/2, K]."""
+    bits = 4 if weight_dtype == "int4" else 8
+    N = weight_scale.shape[0]
+    K = x.shape[-1]
+    act = ACTS[act_method]
+    lead = x.shape[:-1]
+    x2 = x.reshape(-1, K)
+    M = x2.shape[0]
+    if x.is_cuda:
+        assert x.dtype == torch.bfloat16, "weight-only GEMM takes bf16 activations"
+        if x2.stride(-1) != 1:
+            x2 = x2.contiguous()
+        scale = weight_scale if weight_scale.dtype == torch.float32 else weight_scale.float()
+        if M > 256:  # compute-bound: dequantize once, MFMA GEMM via hipBLASLt
+            w = torch.empty((N, K), dtype=torch.bfloat16, device=x.device)
+            _lib.call("piamd_wo_dequant", bits, weight.data_ptr(), scale.data_ptr(), w.data_ptr(),
+                      N, K, _lib.stream())
+            y = F.linear(x2, w, bias)
+            y = _ref_act(y, act) if act else y
+            return y.reshape(*lead, N)
+        y = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+        tiles = (N // 32) * ((M + 31) // 32)
+        kb = K // (32 if bits == 8 else 64)
+        KS = 1
+        while tiles * KS < 512 and kb // (KS * 2) >= 16:
+            KS *= 2
+        ws = None
+        if KS > 1:
+            key = (x.device, KS * M * N)
+            ws = _WS.get(key)
+            if ws is None:
+                ws = _WS[key] = torch.empty(KS * M * N, dtype=torch.float32, device=x.device)
+        _lib.call("piamd_wo_gemm", bits, x2.data_ptr(), x2.stride(0), weight.data_ptr(),
+                  scale.data_ptr(), _lib.ptr(bias), y.data_ptr(), y.stride(0), _lib.ptr(ws), M, N,
+                  K, KS, act, _lib.stream())
+        return y.reshape(*lead, N)
+    w = _unpack(weight, bits, N, K).float() * weight_scale.float()[:, None]
+    y = x2.float() @ w.t()
+    if bias is not None:
+        y = y + bias.float()
+    return _ref_act(y, act).to(x.dtype).reshape(*lead, N)
+
+
+def llm_int8_linear(x, weight, bias=None, weight_scale=None, threshold=6.0):
+    """LLM.int8: outlier input features (|x| > threshold in any row) run in bf16 against the
+    dequantized columns, the rest through the weight-only int8 path. Parity: reference
+    `nn/quant/quantized_linear.py:llm_int8_linear`."""
+    K = x.shape[-1]
+    x2 = x.reshape(-1, K)
+    outl = (x2.abs() > threshold).any(0)
+    if not bool(outl.any()):
+        return weight_only_linear(x, weight, bias, weight_scale, "int8")
+    wd = weight_dequantize(weight, weight_scale, "weight_only_int8", "float32").to(x.device)  # [K,N]
+    xi = x2.masked_fill(outl[None, :], 0)
+    y = weight_only_linear(xi.reshape(x.shape), weight, bias, weight_scale, "int8")
+    yo = (x2[:, outl].float() @ wd[outl].float()).to(y.dtype)
+    return y + yo.reshape(y.shape)

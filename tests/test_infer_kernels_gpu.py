@@ -1,0 +1,126 @@
+"""Numerics of the serving-path HIP kernels (``infer.hip``) against plain PyTorch fp32
+references: QKV prep (bias + RoPE + KV-cache write), split-K decode attention, weight-only
+int8/int4 MFMA GEMM, and the fused multi-transformer context + decode path on the GPU."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib_loaded():
+    import paddle_infer_amd  # noqa: F401
+    from paddle_infer_amd.ops import _lib
+    _lib.lib()
+    assert _lib.has("piamd_decode_attn") and _lib.has("piamd_wo_gemm") and _lib.has("piamd_qkv_prep")
+
+
+def _close(a, b, atol, rtol=2e-2):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs().max().item()
+    tol = atol + rtol * b.abs().max().item()
+    assert err <= tol, f"max err {err} > {tol}"
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("neox", [True, False])
+def test_qkv_prep(D, neox):
+    from paddle_infer_amd.ops import inference as I
+    B, S, Hq, Hk, maxS = 2, 5, 4, 2, 16
+    H = Hq + 2 * Hk
+    qkv = torch.randn(B * S, H * D, device=DEV).bfloat16()
+    bias = torch.randn(H * D, device=DEV).bfloat16()
+    pos0 = torch.tensor([0, 3], dtype=torch.int32, device=DEV)
+    kc = torch.zeros(B, Hk, maxS, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    kr, vr = kc.float().cpu(), vc.float().cpu()
+    ref = I.qkv_prep(qkv.float().cpu(), bias.float().cpu(), kr, vr, pos0.cpu(), B, S, Hq, Hk, D,
+                     rot_dim=D, neox=neox)
+    got = I.qkv_prep(qkv.clone(), bias, kc, vc, pos0, B, S, Hq, Hk, D, rot_dim=D, neox=neox)
+    _close(got, ref, 3e-2)
+    _close(kc, kr, 3e-2)
+    _close(vc, vr, 3e-2)
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("G", [1, 2, 4, 8])
+@pytest.mark.parametrize("maxS,lens", [(64, [1, 37]), (2048, [2048, 700]), (1500, [129, 1499])])
+def test_decode_attention(D, G, maxS, lens):
+    from paddle_infer_amd.ops import inference as I
+    B, Hk = len(lens), 2
+    Hq = Hk * G
+    q = torch.randn(B, (Hq + 2 * Hk) * D, device=DEV).bfloat16()
+    kc = torch.randn(B, Hk, maxS, D, device=DEV).bfloat16()
+    vc = torch.randn(B, Hk, maxS, D, device=DEV).bfloat16()
+    ln = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    got = I.decode_attention(q, kc, vc, ln, Hq, Hk)
+    ref = I.decode_attention(q.float().cpu(), kc.float().cpu(), vc.float().cpu(), ln.cpu(), Hq, Hk,
+                             out=torch.empty(B, Hq * D))
+    _close(got, ref, 2e-2)
+
+
+def test_decode_attention_mask():
+    from paddle_infer_amd.ops import inference as I
+    B, Hq, Hk, D, maxS = 2, 4, 4, 128, 300
+    q = torch.randn(B, Hq * D, device=DEV).bfloat16()
+    kc = torch.randn(B, Hk, maxS, D, device=DEV).bfloat16()
+    vc = torch.randn(B, Hk, maxS, D, device=DEV).bfloat16()
+    ln = torch.tensor([300, 200], dtype=torch.int32, device=DEV)
+    mask = torch.zeros(B, maxS, device=DEV)
+    mask[:, :50] = -1e4
+    mask = mask.bfloat16()
+    got = I.decode_attention(q, kc, vc, ln, Hq, Hk, mask=mask)
+    ref = I.decode_attention(q.float().cpu(), kc.float().cpu(), vc.float().cpu(), ln.cpu(), Hq, Hk,
+                             mask=mask.float().cpu(), out=torch.empty(B, Hq * D))
+    _close(got, ref, 2e-2)
+
+
+@pytest.mark.parametrize("bits", [8, 4])
+@pytest.mark.parametrize("M", [1, 7, 33, 300])
+@pytest.mark.parametrize("N,K", [(256, 512), (2048, 4096), (96, 2048)])
+def test_weight_only_linear(bits, M, N, K):
+    from paddle_infer_amd.ops import inference as I
+    algo = "weight_only_int4" if bits == 4 else "weight_only_int8"
+    w = torch.randn(K, N, device=DEV) * 0.05
+    q, s = I.weight_quantize(w, algo)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    b = (torch.randn(N, device=DEV) * 0.1).bfloat16()
+    got = I.weight_only_linear(x, q, b, s, "int4" if bits == 4 else "int8", "gelu")
+    ref = I.weight_only_linear(x.float().cpu(), q.cpu(), b.float().cpu(), s.cpu(),
+                               "int4" if bits == 4 else "int8", "gelu")
+    _close(got, ref, 2e-2)
+    # device dequant == host unpack
+    dq = I.weight_dequantize(q, s, algo, "float32")
+    _close(dq, I.weight_dequantize(q.cpu(), s.cpu(), algo, "float32"), 1e-3, 1e-2)
+
+
+def test_fused_multi_transformer_gpu_context_and_decode():
+    from paddle_infer_amd.incubate.nn import FusedMultiTransformer
+    torch.manual_seed(0)
+    m = FusedMultiTransformer(256, 4, 1024, num_layers=2)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_(torch.randn_like(p) * 0.03)
+        for s in list(m.ln_scales) + list(m.ffn_ln_scales):
+            s.add_(1.0)
+    B, S = 2, 70
+    x = torch.randn(B, S + 3, 256)
+    # fp32 CPU reference: full causal context over all tokens
+    ref = m(x, causal=True)
+    mg = FusedMultiTransformer(256, 4, 1024, num_layers=2)
+    mg.load_state_dict(m.state_dict())
+    mg = mg.to(DEV)
+    mg._amp_decorate("bfloat16")
+    xg = x.to(DEV).bfloat16()
+    caches = mg.gen_cache(B, 128)
+    out, caches = mg(xg[:, :S], caches=caches, causal=True)
+    outs = [out]
+    for t in range(S, S + 3):
+        o, caches = mg(xg[:, t:t + 1], caches=caches, time_step=torch.tensor([t]))
+        outs.append(o)
+    got = torch.cat(outs, 1)
+    _close(got, ref, 6e-2, 3e-2)

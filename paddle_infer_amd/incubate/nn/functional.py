@@ -214,7 +214,7 @@ def multi_transformer_forward(x, layers, num_heads, num_kv_heads=None, pre_layer
                               epsilon=1e-5, caches=None, pos=None, lens=None, attn_mask=None,
                               decode=False, activation="gelu", rotary_dim=0, neox_rotary=True,
                               rope_base=10000.0, causal=None, group=None, max_len=None,
-                              moe_fn=None):
+                              moe_fn=None, final_ln=None):
     """Core of every fused multi-transformer variant.
 
     x: [B, S, E]; ``layers``: list of dicts with keys ln_scale, ln_bias, qkv (_Linear producing
@@ -289,7 +289,10 @@ def multi_transformer_forward(x, layers, num_heads, num_kv_heads=None, pre_layer
             pending = (f2, b2)
         else:
             pending = (f2, b2, L["ffn_ln_scale"], L["ffn_ln_bias"])
-    if pre_layer_norm:
+    if pre_layer_norm and final_ln is not None:  # final add + LN in one pass (GPT head)
+        out, _ = ops.fused_add_layer_norm(pending[0], residual, final_ln[0], final_ln[1],
+                                          final_ln[2] if len(final_ln) > 2 else epsilon, pending[1])
+    elif pre_layer_norm:
         out = residual + pending[0]
         if pending[1] is not None:
             out = out + pending[1]

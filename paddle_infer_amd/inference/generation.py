@@ -1,0 +1,235 @@
+"""LLM serving: KV-cached generation for the GPT family on the fused multi-transformer path.
+
+Parity: the reference serves GPT-style models through ``FusedMultiTransformer`` (context pass
+writes the KV cache, then one decode step per token with ``time_step``) plus the sampling /
+beam-search helpers (`phi/kernels/fusion/gpu/beam_search_softmax.cu`, top-k / top-p sampling).
+
+MI355X design:
+* the trained ``GPTForPretraining`` weights are used in place (no conversion copies);
+* context pass: hipBLASLt GEMMs + flash attention + fused QKV-prep writing the cache;
+* decode step: embedding → L × (LN → QKV GEMM → bias/RoPE/cache-write → split-K decode attention
+  → out GEMM → add+LN → FFN) → add+LN → LM head, captured ONCE per batch size into a hipGraph
+  (``torch.cuda.CUDAGraph``) over static token / position buffers; positions and lengths are
+  device-resident so a replay is one host call per generated token;
+* KV caches are one HBM allocation per layer sized for ``max_batch × max_seq_len`` (288 GB HBM3E
+  fits hundreds of thousands of cached tokens for a 1.3B model).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from ..incubate.nn import functional as IF
+from ..incubate.nn.functional import _lin
+
+
+class GPTGenerator:
+    def __init__(self, model, max_batch: int = 8, max_seq_len: int | None = None,
+                 use_hip_graph: bool = True, cache_dtype=None, weight_only: str | None = None):
+        self.model = model.eval()
+        cfg = model.cfg
+        self.cfg = cfg
+        p0 = next(iter(model.parameters()))
+        self.device, self.dtype = p0.device, (cache_dtype or p0.dtype)
+        self.H = model.gpt.layers[0].attn.heads
+        self.Hk = model.gpt.layers[0].attn.kv_heads
+        self.D = cfg.head_dim
+        self.max_batch = max_batch
+        self.max_seq_len = max_seq_len or cfg.max_position_embeddings
+        self.group = model.mp_group if getattr(model, "mp_group", None) is not None else None
+        self.layers = []
+        for L in model.gpt.layers:
+            self.layers.append(dict(
+                head_dim=self.D, ln_scale=L.ln1.weight, ln_bias=L.ln1.bias,
+                qkv=_lin(L.attn.qkv_proj.weight), qkv_bias=L.attn.qkv_proj.bias,
+                out=_lin(L.attn.out_proj.weight), out_bias=L.attn.out_proj.bias,
+                ffn_ln_scale=L.ln2.weight, ffn_ln_bias=L.ln2.bias,
+                ffn1=_lin(L.mlp.fc1.weight), ffn1_bias=L.mlp.fc1.bias,
+                ffn2=_lin(L.mlp.fc2.weight), ffn2_bias=L.mlp.fc2.bias))
+        if weight_only in ("int8", "int4"):  # FusedMultiTransformerWeightOnly path
+            from ..ops.inference import weight_quantize
+            algo, bits = f"weight_only_{weight_only}", 4 if weight_only == "int4" else 8
+            for spec in self.layers:
+                for key in ("qkv", "out", "ffn1", "ffn2"):
+                    q, s = weight_quantize(spec[key].w.detach(), algo)
+                    spec[key] = _lin(q, s, bits)
+        self.act = "gelu_tanh" if cfg.activation in ("gelu_tanh", "gelu_new") else "gelu"
+        self.final_ln = (model.gpt.final_ln.weight, model.gpt.final_ln.bias, cfg.layer_norm_eps)
+        shape = (max_batch, self.Hk, self.max_seq_len, self.D)
+        self.caches = [(torch.zeros(shape, dtype=self.dtype, device=self.device),
+                        torch.zeros(shape, dtype=self.dtype, device=self.device))
+                       for _ in self.layers]
+        self.use_graph = use_hip_graph and self.device.type == "cuda"
+        self._graphs = {}
+
+    # ------------------------------------------------------------------------------ model
+    def _mp_gather(self, logits):
+        if self.group is None or torch.distributed.get_world_size(self.group) == 1:
+            return logits
+        ws = torch.distributed.get_world_size(self.group)
+        parts = [torch.empty_like(logits) for _ in range(ws)]
+        torch.distributed.all_gather(parts, logits.contiguous(), group=self.group)
+        return torch.cat(parts, -1)
+
+    def _forward(self, ids, pos, lens, B, decode):
+        S = ids.shape[1]
+        caches = [(k[:B], v[:B]) for k, v in self.caches]
+        if decode:
+            position_ids = pos.long().view(B, 1)
+        else:
+            position_ids = torch.arange(S, device=ids.device).unsqueeze(0).expand(B, S)
+        emb = self.model.gpt.embeddings(ids, position_ids)
+        y = IF.multi_transformer_forward(
+            emb, self.layers, self.H, self.Hk, True, self.cfg.layer_norm_eps, caches, pos, lens,
+            None, decode, self.act, causal=True, group=self.group, max_len=self.max_seq_len,
+            final_ln=self.final_ln)
+        return y
+
+    def _logits(self, y):
+        return self._mp_gather(torch.matmul(y, self.model.head_weight().t()))
+
+    @torch.no_grad()
+    def prefill(self, input_ids, lengths):
+        """input_ids [B, S] right-padded; lengths [B]. Writes cache [0, S); returns last-token
+        logits [B, V]."""
+        B, S = input_ids.shape
+        pos0 = torch.zeros(B, dtype=torch.int32, device=self.device)
+        y = self._forward(input_ids, pos0, None, B, decode=False)
+        last = y[torch.arange(B, device=y.device), lengths.long() - 1]
+        return self._logits(last)
+
+    def _decode_eager(self, tok, pos, B):
+        lens = pos + 1
+        y = self._forward(tok.view(B, 1), pos, lens, B, decode=True)
+        return self._logits(y.view(B, -1))
+
+    @torch.no_grad()
+    def decode(self, tok, pos):
+        """One step: tok [B] int64, pos [B] int32 (cache slot to write). Returns logits [B, V]."""
+        B = tok.shape[0]
+        if not self.use_graph:
+            return self._decode_eager(tok, pos, B)
+        ent = self._graphs.get(B)
+        if ent is None:
+            st_tok = tok.clone()
+            st_pos = pos.clone()
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    self._decode_eager(st_tok, st_pos, B)
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                st_out = self._decode_eager(st_tok, st_pos, B)
+            ent = self._graphs[B] = (g, st_tok, st_pos, st_out)
+        g, st_tok, st_pos, st_out = ent
+        st_tok.copy_(tok, non_blocking=True)
+        st_pos.copy_(pos, non_blocking=True)
+        g.replay()
+        return st_out
+
+    # ------------------------------------------------------------------------------ sampling
+    @staticmethod
+    def sample(logits, strategy="greedy_search", top_k=0, top_p=1.0, temperature=1.0,
+               generator=None):
+        if strategy == "greedy_search":
+            return logits.argmax(-1)
+        lg = logits.float() / max(temperature, 1e-6)
+        if top_k and top_k > 0:
+            kth = torch.topk(lg, top_k, -1).values[:, -1:]
+            lg = lg.masked_fill(lg < kth, float("-inf"))
+        if top_p < 1.0:
+            sp, si = torch.sort(lg, -1, descending=True)
+            cp = torch.softmax(sp, -1).cumsum(-1)
+            drop = cp - torch.softmax(sp, -1) > top_p
+            sp = sp.masked_fill(drop, float("-inf"))
+            lg = torch.full_like(lg, float("-inf")).scatter(-1, si, sp)
+        probs = torch.softmax(lg, -1)
+        return torch.multinomial(probs, 1, generator=generator).squeeze(-1)
+
+    @torch.no_grad()
+    def generate(self, input_ids, lengths=None, max_new_tokens=32, decode_strategy="greedy_search",
+                 top_k=0, top_p=1.0, temperature=1.0, eos_token_id=None, pad_token_id=0,
+                 num_beams=1, length_penalty=1.0, seed=None):
+        """Returns generated ids [B, max_new_tokens] (pad after EOS)."""
+        B, S = input_ids.shape
+        if num_beams > 1 or decode_strategy == "beam_search":
+            return self._beam_search(input_ids, lengths, max_new_tokens, max(num_beams, 2),
+                                     eos_token_id, pad_token_id, length_penalty)
+        assert B <= self.max_batch and S + max_new_tokens <= self.max_seq_len
+        ids = input_ids.to(self.device)
+        lens = (lengths if lengths is not None else torch.full((B,), S)).to(self.device)
+        gen = torch.Generator(device=self.device).manual_seed(seed) if seed is not None else None
+        logits = self.prefill(ids, lens)
+        out = torch.full((B, max_new_tokens), pad_token_id, dtype=torch.long, device=self.device)
+        done = torch.zeros(B, dtype=torch.bool, device=self.device)
+        pos = lens.to(torch.int32)
+        for t in range(max_new_tokens):
+            tok = self.sample(logits, decode_strategy, top_k, top_p, temperature, gen)
+            tok = torch.where(done, torch.full_like(tok, pad_token_id), tok)
+            out[:, t] = tok
+            if eos_token_id is not None:
+                done = done | (tok == eos_token_id)
+                if (t & 7) == 7 and bool(done.all()):
+                    break
+            if t + 1 < max_new_tokens:
+                logits = self.decode(tok, pos)
+                pos = pos + 1
+        return out
+
+    def _reorder(self, src, B):
+        for k, v in self.caches:
+            k[:B].copy_(k[:B].index_select(0, src))
+            v[:B].copy_(v[:B].index_select(0, src))
+
+    def _beam_search(self, input_ids, lengths, max_new_tokens, nb, eos, pad, length_penalty):
+        """Beam search (reference `beam_search_softmax`): beams live as batch rows; each step the
+        caches are gathered by source beam."""
+        B0, S = input_ids.shape
+        B = B0 * nb
+        assert B <= self.max_batch
+        ids = input_ids.to(self.device).repeat_interleave(nb, 0)
+        lens = (lengths if lengths is not None else torch.full((B0,), S)).to(self.device).repeat_interleave(nb)
+        logits = self.prefill(ids, lens)
+        V = logits.shape[-1]
+        scores = torch.zeros(B0, nb, device=self.device)
+        scores[:, 1:] = float("-inf")
+        seqs = torch.full((B, max_new_tokens), pad, dtype=torch.long, device=self.device)
+        done = torch.zeros(B, dtype=torch.bool, device=self.device)
+        pos = lens.to(torch.int32)
+        ar = torch.arange(B0, device=self.device)[:, None] * nb
+        for t in range(max_new_tokens):
+            lp = F.log_softmax(logits.float(), -1)
+            if eos is not None:  # finished beams only extend with pad at no cost
+                pad_row = torch.full((V,), float("-inf"), device=lp.device)
+                pad_row[pad] = 0.0
+                lp = torch.where(done[:, None], pad_row[None, :], lp)
+            cand = (scores.view(B, 1) + lp).view(B0, nb * V)
+            top, idx = cand.topk(nb, -1)
+            src = (ar + idx // V).view(-1)
+            tok = (idx % V).view(-1)
+            scores = top
+            seqs = seqs.index_select(0, src)
+            seqs[:, t] = tok
+            done = done.index_select(0, src)
+            if eos is not None:
+                done = done | (tok == eos)
+            self._reorder(src, B)
+            if t + 1 < max_new_tokens:
+                logits = self.decode(tok, pos)
+                pos = pos + 1
+        L = (seqs != pad).sum(-1).clamp_min(1).float().view(B0, nb)
+        best = (scores / L ** length_penalty).argmax(-1)
+        return seqs.view(B0, nb, -1)[torch.arange(B0, device=self.device), best]
+
+
+def generate(model, input_ids, **kw):
+    """Functional helper: build (and cache on the model) a :class:`GPTGenerator`."""
+    gen_kw = {k: kw.pop(k) for k in ("max_batch", "max_seq_len", "use_hip_graph") if k in kw}
+    g = getattr(model, "_piamd_generator", None)
+    if g is None:
+        g = GPTGenerator(model, max_batch=gen_kw.get("max_batch", max(8, input_ids.shape[0] * kw.get("num_beams", 1))),
+                         max_seq_len=gen_kw.get("max_seq_len"), use_hip_graph=gen_kw.get("use_hip_graph", True))
+        model._piamd_generator = g
+    return g.generate(input_ids, **kw)

@@ -11,3 +11,19 @@ from .optim import adamw_flat, momentum_flat, sumsq  # noqa: F401
 from . import _lib  # noqa: F401
 from .inference import (qkv_prep, decode_attention, weight_quantize, weight_dequantize,  # noqa: F401
                         weight_only_linear, llm_int8_linear)
+
+
+def _make_recordable():
+    """Static-graph capture records these framework ops by name (see static.framework.recordable)."""
+    from ..static.framework import recordable
+    g = globals()
+    for name, ty in (("layer_norm", "layer_norm"), ("fused_add_layer_norm", "skip_layernorm"),
+                     ("rms_norm", "rms_norm"), ("flash_attention", "flash_attn"),
+                     ("flash_attention_packed", "flash_attn_packed"), ("bias_act", "fused_bias_act"),
+                     ("gelu", "gelu"), ("dropout", "dropout"), ("fused_softmax_mask", "softmax_mask_fuse"),
+                     ("softmax_cross_entropy", "softmax_with_cross_entropy"),
+                     ("weight_only_linear", "weight_only_linear")):
+        g[name] = recordable(ty)(g[name])
+
+
+_make_recordable()

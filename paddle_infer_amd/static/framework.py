@@ -167,8 +167,38 @@ def _paddle_types():
 _TYPES = None
 
 
+def _has_variable(args, kwargs):
+    for a in args:
+        if isinstance(a, Variable):
+            return True
+        if isinstance(a, (list, tuple)) and any(isinstance(b, Variable) for b in a):
+            return True
+    return any(isinstance(v, Variable) for v in kwargs.values())
+
+
+def recordable(paddle_op_type):
+    """Make a framework op (``ops.*``) record ITSELF into a static Program when called on
+    Variables, so the Executor later dispatches on the real tensors (HIP kernel on GPU) instead of
+    freezing whichever branch the meta-tensor trace took."""
+    import functools
+
+    def deco(fn):
+        @functools.wraps(fn)
+        def wrapper(*args, **kwargs):
+            if _has_variable(args, kwargs):
+                return _record(fn, args, kwargs)
+            return fn(*args, **kwargs)
+        fn._paddle_type = paddle_op_type
+        wrapper._paddle_type = paddle_op_type
+        return wrapper
+    return deco
+
+
 def paddle_type(func):
     global _TYPES
+    t = getattr(func, "_paddle_type", None)
+    if t is not None:
+        return t
     if _TYPES is None:
         _TYPES = _paddle_types()
     try:

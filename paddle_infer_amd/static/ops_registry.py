@@ -366,5 +366,23 @@ def _flash_packed(ins, a):
 @register("flash_attn")
 def _flash(ins, a):
     from .. import ops
-    return {"Out": ops.flash_attention(ins["Q"][0], ins["K"][0], ins["V"][0], causal=bool(a.get("causal", False)))}
+    q, k, v = ins["Q"][0], ins["K"][0], ins["V"][0]
+    bhsd = a.get("layout", "bshd") == "bhsd"
+    if bhsd:
+        q, k, v = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
+    o = ops.flash_attention(q, k, v, causal=bool(a.get("causal", False)), scale=a.get("scale"))
+    return {"Out": o.transpose(1, 2) if bhsd else o}
 
+
+@register("fused_embedding_eltwise_layernorm")
+def _emb_ln(ins, a):
+    """Reference `fused_embedding_eltwise_layernorm_op`: LN(Σ_i Emb_i[Ids_i])."""
+    from .. import ops
+    acc = None
+    for ids, w in zip(ins["Ids"], ins["Embs"]):
+        ids = ids.long()
+        if ids.dim() > 1 and ids.shape[-1] == 1:
+            ids = ids.squeeze(-1)
+        e = F.embedding(ids, w)
+        acc = e if acc is None else acc + e
+    return {"Out": ops.layer_norm(acc, ins["Scale"][0], ins["Bias"][0], a.get("epsilon", 1e-5))}

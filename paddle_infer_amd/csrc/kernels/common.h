@@ -100,6 +100,19 @@ __device__ __forceinline__ float gelu_erf_grad(float x) {
   return 0.5f * (1.f + erff(x * 0.7071067811865476f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
 }
 
+// Cross-workgroup hand-off inside one kernel (split-K fixups) WITHOUT __threadfence(): on gfx950 a
+// device-scope release fence writes back the whole (per-XCD) L2, which costs more than the work.
+// Device-scope atomics are performed memory-side, coherent across the 8 XCD L2s, so partials are
+// published with returning atomics (the return forces completion), then `xcd_drain()` waits for
+// them before the arrival counter is bumped; the consumer reads with `xcd_take` (read + clear).
+__device__ __forceinline__ float xcd_put(float* p, float v) { return atomicExch(p, v); }
+__device__ __forceinline__ float xcd_add(float* p, float v) { return atomicAdd(p, v); }
+__device__ __forceinline__ float xcd_take(float* p) { return atomicExch(p, 0.f); }
+__device__ __forceinline__ void xcd_drain(float sink) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("" ::"v"(sink));
+}
+
 // Grid size for grid-stride memory-bound kernels (guide G11): ≤ 256 CUs × 8 blocks.
 static inline int stride_grid(long long work_items, int block) {
   long long g = (work_items + block - 1) / block;

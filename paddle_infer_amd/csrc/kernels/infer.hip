@@ -108,21 +108,27 @@ PIAMD_EXPORT int piamd_qkv_prep(void* qkv, long long ld, const void* bias, void*
 }
 
 // =====================================================================================
-// decode attention (split-K)
+// decode attention (split-K, fused prologue, in-kernel combine)
 // =====================================================================================
-// q     : element (b, head, d) at q[b*ldq + head*D + d]   (head = hk*G + g)
-// kc,vc : [B, Hk, maxS, D]; keys [0, lens[b]) are attended
+// qkv   : row b at qkv + b*ldq: [Hq q-heads | Hk k-heads | Hk v-heads] × D
+//         prep == 0: q already prepared (bias/RoPE applied), k/v of the new token already cached
+//         prep == 1: raw QKV GEMM output of the new token; the kernel adds `bias`, applies RoPE
+//                    (rot ∈ {0, D}) to q and k, and the workgroup whose key range holds the new
+//                    position writes k/v into the cache before scoring
+// kc,vc : [B, Hk, maxS, D]; keys [0, lens[b]) are attended; the new token sits at lens[b]-1
 // mask  : optional additive bf16 mask, element (b, key) at mask[b*ldm + key]
-// part  : [B, Hq, nsplit, D + 2] f32 partials (acc, m, l) when nsplit > 1
+// part  : [B, Hq, nsplit, D + 2] f32 partials (acc, m, l) when nsplit > 1; `cnt` [B*Hk] int
+//         arrival counters (zero on entry, restored to zero by the combining workgroup)
 // out   : element (b, head, d) at out[b*ldo + head*D + d]
 constexpr int DA_CHUNK_MAX = 512;
 
 template <int D, int G>
 __global__ __launch_bounds__(256) void decode_attn_kernel(
-    const bf16_t* __restrict__ q, long long ldq, const bf16_t* __restrict__ kc,
-    const bf16_t* __restrict__ vc, const int* __restrict__ lens, int Hk, int maxS, int chunk,
-    int nsplit, const bf16_t* __restrict__ mask, long long ldm, float scale_log2,
-    float* __restrict__ part, bf16_t* __restrict__ out, long long ldo) {
+    const bf16_t* __restrict__ qkv, long long ldq, const bf16_t* __restrict__ bias, int prep,
+    int rot, int neox, float log2_base, bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
+    const int* __restrict__ lens, int Hk, int maxS, int chunk, int nsplit,
+    const bf16_t* __restrict__ mask, long long ldm, float scale_log2, float* __restrict__ part,
+    int* __restrict__ cnt, bf16_t* __restrict__ out, long long ldo) {
   constexpr int LPK = D / 8;        // lanes per key row (16 B per lane)
   constexpr int KPW = 64 / LPK;     // keys per wave per step
   constexpr int KPI = KPW * 4;      // keys per workgroup per step
@@ -130,212 +136,279 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
   __shared__ float red[4][G * D];
   __shared__ float stat[2][G];
   __shared__ float wred[8];
+  __shared__ int s_last;
 
   const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
   const int Hq = Hk * G;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int sub = lane % LPK, kslot = w * KPW + lane / LPK;
-  const int len = lens[b];
+  const int len = lens[b], pos = len - 1;
   const int k0 = split * chunk, k1 = min(len, k0 + chunk);
-  if (k0 >= k1) {  // workgroup-uniform: empty split
-    if (nsplit > 1 && tid < G) {
-      float* p = part + (((long long)b * Hq + hk * G + tid) * nsplit + split) * (D + 2);
-      p[D] = -INFINITY;
-      p[D + 1] = 0.f;
-    }
-    return;
-  }
-  const int n = k1 - k0;
   const long long kvbase = ((long long)b * Hk + hk) * maxS * D;
+  const bf16_t* row = qkv + (long long)b * ldq;
+
+  // ---- prologue: q (and the new k/v) with bias + rotary, in registers ----
+  float rc[8], rs[8];  // rotary cos/sin for this lane's 8 elements
+  const bool rope = prep && rot == D;
+  if (rope) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = sub * 8 + j;
+      const int f = neox ? (i % (D / 2)) : (i >> 1);
+      const float inv = exp2f(-(2.f * f / (float)D) * log2_base);
+      sincosf((float)pos * inv, &rs[j], &rc[j]);
+    }
+  }
+  auto load_vec = [&](int head, float* v) {
+    const u16x8 x = *(const u16x8*)(row + (long long)head * D + sub * 8);
+    u16x8 bb;
+    if (prep && bias) bb = *(const u16x8*)(bias + (long long)head * D + sub * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = bf2f(x[j]) + ((prep && bias) ? bf2f(bb[j]) : 0.f);
+  };
+  auto rotate = [&](float* v) {
+    if (!rope) return;
+    float pr[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (neox) {
+        pr[j] = __shfl_xor(v[j], LPK / 2, 64);
+        const float sg = sub < LPK / 2 ? -1.f : 1.f;
+        pr[j] *= sg;
+      } else {
+        pr[j] = (j & 1) ? v[j - 1] : -v[j + 1];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = v[j] * rc[j] + pr[j] * rs[j];
+  };
 
   float qf[G][8];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
-    const u16x8 v = *(const u16x8*)(q + (long long)b * ldq + (long long)(hk * G + g) * D + sub * 8);
+    load_vec(hk * G + g, qf[g]);
+    rotate(qf[g]);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) qf[g][j] = bf2f(v[j]) * scale_log2;
+    for (int j = 0; j < 8; ++j) qf[g][j] *= scale_log2;
+  }
+  if (prep) {
+    // k/v of the new token: only the workgroup owning position `pos` stores them (every lane of
+    // the wave evaluates the shuffles; waves 1..3 skip the store)
+    float kn[8], vn[8];
+    load_vec(Hq + hk, kn);
+    rotate(kn);
+    load_vec(Hq + Hk + hk, vn);
+    if (w == 0 && lane < LPK && pos >= k0 && pos < k1 && pos < maxS) {
+      u16x8 ko, vo;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        ko[j] = f2bf(kn[j]);
+        vo[j] = f2bf(vn[j]);
+      }
+      *(u16x8*)(kc + kvbase + (long long)pos * D + sub * 8) = ko;
+      *(u16x8*)(vc + kvbase + (long long)pos * D + sub * 8) = vo;
+    }
+    __threadfence_block();
+    __syncthreads();
   }
 
-  // ---- scores: s = (q·k) * scale * log2(e) (+ mask * log2(e)) ----
-  constexpr int U = 4;
-  for (int base = kslot; base < n; base += KPI * U) {
-    u16x8 kr[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int kk = min(base + u * KPI, n - 1);  // clamped: every load is issued
-      kr[u] = *(const u16x8*)(kc + kvbase + (long long)(k0 + kk) * D + sub * 8);
+  const int n = k1 - k0;
+  if (n <= 0) {  // workgroup-uniform: empty split
+    if (nsplit > 1 && tid < G) {
+      float* p = part + (((long long)b * Hq + hk * G + tid) * nsplit + split) * (D + 2);
+      xcd_drain(xcd_put(p + D, -INFINITY) + xcd_put(p + D + 1, 0.f));
     }
+  } else {
+    // ---- scores: s = (q·k) * scale * log2(e) (+ mask * log2(e)) ----
+    constexpr int U = 4;
+    for (int base = kslot; base < n; base += KPI * U) {
+      u16x8 kr[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int kk = base + u * KPI;
+      for (int u = 0; u < U; ++u) {
+        const int kk = min(base + u * KPI, n - 1);  // clamped: every load is issued
+        kr[u] = *(const u16x8*)(kc + kvbase + (long long)(k0 + kk) * D + sub * 8);
+      }
 #pragma unroll
-      for (int g = 0; g < G; ++g) {
-        float d = 0.f;
+      for (int u = 0; u < U; ++u) {
+        const int kk = base + u * KPI;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) d += qf[g][j] * bf2f(kr[u][j]);
+        for (int g = 0; g < G; ++g) {
+          float d = 0.f;
 #pragma unroll
-        for (int o = LPK / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
-        if (sub == 0 && kk < n) {
-          if (mask) d += bf2f(mask[(long long)b * ldm + k0 + kk]) * 1.4426950408889634f;
-          sc[g][kk] = d;
+          for (int j = 0; j < 8; ++j) d += qf[g][j] * bf2f(kr[u][j]);
+#pragma unroll
+          for (int o = LPK / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+          if (sub == 0 && kk < n) {
+            if (mask) d += bf2f(mask[(long long)b * ldm + k0 + kk]) * 1.4426950408889634f;
+            sc[g][kk] = d;
+          }
         }
       }
     }
-  }
-  __syncthreads();
+    __syncthreads();
 
-  // ---- softmax statistics over the chunk (base-2 domain) ----
+    // ---- softmax statistics over the chunk (base-2 domain) ----
 #pragma unroll
-  for (int g = 0; g < G; ++g) {
-    float m = -INFINITY;
-    for (int i = tid; i < n; i += 256) m = fmaxf(m, sc[g][i]);
-    m = block_max<4>(m, wred);
-    float l = 0.f;
-    for (int i = tid; i < n; i += 256) {
-      const float p = exp2f(sc[g][i] - m);
-      sc[g][i] = p;
-      l += p;
-    }
-    l = block_sum<4>(l, wred);
-    if (tid == 0) {
-      stat[0][g] = m;
-      stat[1][g] = l;
-    }
-  }
-  __syncthreads();
-
-  // ---- P·V ----
-  float acc[G][8];
-#pragma unroll
-  for (int g = 0; g < G; ++g)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
-  for (int base = kslot; base < n; base += KPI * U) {
-    u16x8 vr[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int kk = min(base + u * KPI, n - 1);
-      vr[u] = *(const u16x8*)(vc + kvbase + (long long)(k0 + kk) * D + sub * 8);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int kk = base + u * KPI;
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const float p = kk < n ? sc[g][min(kk, n - 1)] : 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[g][j] += p * bf2f(vr[u][j]);
+    for (int g = 0; g < G; ++g) {
+      float m = -INFINITY;
+      for (int i = tid; i < n; i += 256) m = fmaxf(m, sc[g][i]);
+      m = block_max<4>(m, wred);
+      float l = 0.f;
+      for (int i = tid; i < n; i += 256) {
+        const float p = exp2f(sc[g][i] - m);
+        sc[g][i] = p;
+        l += p;
+      }
+      l = block_sum<4>(l, wred);
+      if (tid == 0) {
+        stat[0][g] = m;
+        stat[1][g] = l;
       }
     }
-  }
-  // reduce over the KPW key slots of the wave (lanes with equal `sub`)
-#pragma unroll
-  for (int g = 0; g < G; ++g)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float v = acc[g][j];
-#pragma unroll
-      for (int o = LPK; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
-      acc[g][j] = v;
-    }
-  if (lane < LPK) {
+    __syncthreads();
+
+    // ---- P·V ----
+    float acc[G][8];
 #pragma unroll
     for (int g = 0; g < G; ++g)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) red[w][g * D + sub * 8 + j] = acc[g][j];
-  }
-  __syncthreads();
-  for (int i = tid; i < G * D; i += 256) {
-    const int g = i / D, d = i % D;
-    const float v = red[0][i] + red[1][i] + red[2][i] + red[3][i];
-    const int head = hk * G + g;
-    if (nsplit == 1) {
-      out[(long long)b * ldo + (long long)head * D + d] = f2bf(v / stat[1][g]);
-    } else {
-      float* p = part + (((long long)b * Hq + head) * nsplit + split) * (D + 2);
-      p[d] = v;
-      if (d == 0) {
-        p[D] = stat[0][g];
-        p[D + 1] = stat[1][g];
+      for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
+    for (int base = kslot; base < n; base += KPI * U) {
+      u16x8 vr[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int kk = min(base + u * KPI, n - 1);
+        vr[u] = *(const u16x8*)(vc + kvbase + (long long)(k0 + kk) * D + sub * 8);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int kk = base + u * KPI;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const float p = kk < n ? sc[g][min(kk, n - 1)] : 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[g][j] += p * bf2f(vr[u][j]);
+        }
       }
     }
+    // reduce over the KPW key slots of the wave (lanes with equal `sub`)
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = acc[g][j];
+#pragma unroll
+        for (int o = LPK; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+        acc[g][j] = v;
+      }
+    if (lane < LPK) {
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) red[w][g * D + sub * 8 + j] = acc[g][j];
+    }
+    __syncthreads();
+    float sink = 0.f;
+    for (int i = tid; i < G * D; i += 256) {
+      const int g = i / D, d = i % D;
+      const float v = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+      const int head = hk * G + g;
+      if (nsplit == 1) {
+        out[(long long)b * ldo + (long long)head * D + d] = f2bf(v / stat[1][g]);
+      } else {
+        float* p = part + (((long long)b * Hq + head) * nsplit + split) * (D + 2);
+        sink += xcd_put(p + d, v);
+        if (d == 0) {
+          sink += xcd_put(p + D, stat[0][g]);
+          sink += xcd_put(p + D + 1, stat[1][g]);
+        }
+      }
+    }
+    if (nsplit > 1) xcd_drain(sink);
   }
-}
+  if (nsplit == 1) return;
 
-template <int D>
-__global__ __launch_bounds__(D) void decode_combine_kernel(const float* __restrict__ part,
-                                                           int Hq, int nsplit,
-                                                           bf16_t* __restrict__ out,
-                                                           long long ldo) {
-  const int bh = blockIdx.x, b = bh / Hq, head = bh % Hq, d = threadIdx.x;
-  const float* p = part + (long long)bh * nsplit * (D + 2);
-  float m = -INFINITY;
-  for (int s = 0; s < nsplit; ++s) m = fmaxf(m, p[s * (D + 2) + D]);
-  float l = 0.f, a = 0.f;
-  for (int s = 0; s < nsplit; ++s) {
-    const float ms = p[s * (D + 2) + D];
-    if (ms == -INFINITY) continue;
-    const float wgt = exp2f(ms - m);
-    l += wgt * p[s * (D + 2) + D + 1];
-    a += wgt * p[s * (D + 2) + d];
+  // ---- the last-arriving split of (b, hk) merges all partials (no combine launch) ----
+  __syncthreads();  // every thread's partial stores have completed (xcd_drain)
+  if (tid == 0) s_last = atomicAdd(&cnt[b * Hk + hk], 1) == nsplit - 1;
+  __syncthreads();
+  if (!s_last) return;
+  for (int i = tid; i < G * D; i += 256) {
+    const int g = i / D, d = i % D;
+    const int head = hk * G + g;
+    float* p = part + ((long long)b * Hq + head) * nsplit * (D + 2);
+    float m = -INFINITY;
+    for (int s2 = 0; s2 < nsplit; ++s2)
+      m = fmaxf(m, __hip_atomic_load(p + s2 * (D + 2) + D, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    float l = 0.f, a = 0.f;
+    for (int s2 = 0; s2 < nsplit; ++s2) {
+      const float ms = __hip_atomic_load(p + s2 * (D + 2) + D, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (ms == -INFINITY) continue;  // empty split: its acc slots hold stale data
+      const float wgt = exp2f(ms - m);
+      l += wgt * __hip_atomic_load(p + s2 * (D + 2) + D + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      a += wgt * __hip_atomic_load(p + s2 * (D + 2) + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    out[(long long)b * ldo + (long long)head * D + d] = f2bf(a / l);
   }
-  out[(long long)b * ldo + (long long)head * D + d] = f2bf(a / l);
+  if (tid == 0) atomicExch(&cnt[b * Hk + hk], 0);
 }
 
 template <int D, int G>
-static void launch_decode(dim3 grid, hipStream_t st, const void* q, long long ldq, const void* kc,
-                          const void* vc, const int* lens, int Hk, int maxS, int chunk, int nsplit,
-                          const void* mask, long long ldm, float sl2, float* part, void* out,
-                          long long ldo) {
-  hipLaunchKernelGGL((decode_attn_kernel<D, G>), grid, dim3(256), 0, st, (const bf16_t*)q, ldq,
-                     (const bf16_t*)kc, (const bf16_t*)vc, lens, Hk, maxS, chunk, nsplit,
-                     (const bf16_t*)mask, ldm, sl2, part, (bf16_t*)out, ldo);
+static void launch_decode(dim3 grid, hipStream_t st, const void* qkv, long long ldq,
+                          const void* bias, int prep, int rot, int neox, float l2b, void* kc,
+                          void* vc, const int* lens, int Hk, int maxS, int chunk, int nsplit,
+                          const void* mask, long long ldm, float sl2, float* part, int* cnt,
+                          void* out, long long ldo) {
+  hipLaunchKernelGGL((decode_attn_kernel<D, G>), grid, dim3(256), 0, st, (const bf16_t*)qkv, ldq,
+                     (const bf16_t*)bias, prep, rot, neox, l2b, (bf16_t*)kc, (bf16_t*)vc, lens,
+                     Hk, maxS, chunk, nsplit, (const bf16_t*)mask, ldm, sl2, part, cnt,
+                     (bf16_t*)out, ldo);
 }
 
+#define PIAMD_DECODE_ARGS grid, st, qkv, ldq, bias, prep, rot, neox, l2b, kc, vc, lens, Hk, maxS, \
+                          chunk, nsplit, mask, ldm, sl2, part, cnt, out, ldo
 template <int D>
-static int dispatch_decode_g(int G, dim3 grid, hipStream_t st, const void* q, long long ldq,
-                             const void* kc, const void* vc, const int* lens, int Hk, int maxS,
-                             int chunk, int nsplit, const void* mask, long long ldm, float sl2,
-                             float* part, void* out, long long ldo) {
+static int dispatch_decode_g(int G, dim3 grid, hipStream_t st, const void* qkv, long long ldq,
+                             const void* bias, int prep, int rot, int neox, float l2b, void* kc,
+                             void* vc, const int* lens, int Hk, int maxS, int chunk, int nsplit,
+                             const void* mask, long long ldm, float sl2, float* part, int* cnt,
+                             void* out, long long ldo) {
   switch (G) {
-    case 1: launch_decode<D, 1>(grid, st, q, ldq, kc, vc, lens, Hk, maxS, chunk, nsplit, mask, ldm, sl2, part, out, ldo); break;
-    case 2: launch_decode<D, 2>(grid, st, q, ldq, kc, vc, lens, Hk, maxS, chunk, nsplit, mask, ldm, sl2, part, out, ldo); break;
-    case 4: launch_decode<D, 4>(grid, st, q, ldq, kc, vc, lens, Hk, maxS, chunk, nsplit, mask, ldm, sl2, part, out, ldo); break;
-    case 8: launch_decode<D, 8>(grid, st, q, ldq, kc, vc, lens, Hk, maxS, chunk, nsplit, mask, ldm, sl2, part, out, ldo); break;
+    case 1: launch_decode<D, 1>(PIAMD_DECODE_ARGS); break;
+    case 2: launch_decode<D, 2>(PIAMD_DECODE_ARGS); break;
+    case 4: launch_decode<D, 4>(PIAMD_DECODE_ARGS); break;
+    case 8: launch_decode<D, 8>(PIAMD_DECODE_ARGS); break;
     default: return (int)hipErrorInvalidValue;
   }
   return 0;
 }
 
-// chunk ≤ 512 keys per split; nsplit * chunk ≥ max length; part may be null iff nsplit == 1
-PIAMD_EXPORT int piamd_decode_attn(const void* q, long long ldq, const void* kc, const void* vc,
+// chunk ≤ 512 keys per split; nsplit * chunk ≥ max length; part/cnt may be null iff nsplit == 1.
+// rot must be 0 or D when prep == 1 (partial rotary: run piamd_qkv_prep first, prep = 0).
+PIAMD_EXPORT int piamd_decode_attn(const void* qkv, long long ldq, const void* bias, int prep,
+                                   int rot, int neox, float base, void* kc, void* vc,
                                    const int* lens, int B, int Hq, int Hk, int D, int maxS,
                                    int chunk, int nsplit, const void* mask, long long ldm,
-                                   float scale, float* part, void* out, long long ldo,
+                                   float scale, float* part, int* cnt, void* out, long long ldo,
                                    hipStream_t st) {
-  if (Hk <= 0 || Hq % Hk || chunk <= 0 || chunk > DA_CHUNK_MAX || (nsplit > 1 && !part))
+  if (Hk <= 0 || Hq % Hk || chunk <= 0 || chunk > DA_CHUNK_MAX ||
+      (nsplit > 1 && (!part || !cnt)) || (prep && rot != 0 && rot != D))
     return (int)hipErrorInvalidValue;
   const int G = Hq / Hk;
   dim3 grid(nsplit, Hk, B);
   const float sl2 = scale * 1.4426950408889634f;
+  const float l2b = log2f(base);
   int rc;
   if (D == 128)
-    rc = dispatch_decode_g<128>(G, grid, st, q, ldq, kc, vc, lens, Hk, maxS, chunk, nsplit, mask, ldm, sl2, part, out, ldo);
+    rc = dispatch_decode_g<128>(G, PIAMD_DECODE_ARGS);
   else if (D == 64)
-    rc = dispatch_decode_g<64>(G, grid, st, q, ldq, kc, vc, lens, Hk, maxS, chunk, nsplit, mask, ldm, sl2, part, out, ldo);
+    rc = dispatch_decode_g<64>(G, PIAMD_DECODE_ARGS);
   else
     return (int)hipErrorInvalidValue;
   if (rc) return rc;
-  if (nsplit > 1) {
-    if (D == 128)
-      hipLaunchKernelGGL(decode_combine_kernel<128>, dim3(B * Hq), dim3(128), 0, st, part, Hq,
-                         nsplit, (bf16_t*)out, ldo);
-    else
-      hipLaunchKernelGGL(decode_combine_kernel<64>, dim3(B * Hq), dim3(64), 0, st, part, Hq,
-                         nsplit, (bf16_t*)out, ldo);
-  }
   return (int)hipGetLastError();
 }
+#undef PIAMD_DECODE_ARGS
 
 // =====================================================================================
 // weight-only GEMM
@@ -344,6 +417,8 @@ PIAMD_EXPORT int piamd_decode_attn(const void* q, long long ldq, const void* kc,
 //   int8: byte(n,k) at (((n/32)*(K/32) + k/32)*64 + (n%32) + 32*((k%32)/16))*16 + k%16
 //   int4: nibble(n,k) in byte (((n/32)*(K/64) + k/64)*64 + (n%32) + 32*((k%64)/32))*16 + (k%32)/2,
 //         low nibble for even k, two's complement in [-8, 7]
+//   bf16: element(n,k) at (((n/32)*(K/16) + k/16)*64 + (n%32) + 32*((k%16)/8))*8 + k%8
+//         (the same tiling for unquantized serving weights: one MFMA B operand per 16 B load)
 // so each wave reads one contiguous 1 KB block per k-block: lane l holds row n0+(l&31), k-run
 // [kb*KB + (KB/2)*(l>>5), +KB/2) — exactly the bf16x8 B-operand runs of consecutive MFMAs.
 __device__ __forceinline__ bf16x8 i8x8_to_bf16(unsigned lo, unsigned hi) {
@@ -376,8 +451,8 @@ template <int BITS>
 __global__ __launch_bounds__(256) void wo_gemm_kernel(
     const bf16_t* __restrict__ x, long long ldx, const unsigned char* __restrict__ wp,
     const float* __restrict__ scale, const bf16_t* __restrict__ bias, bf16_t* __restrict__ y,
-    long long ldy, float* __restrict__ ws, int M, int N, int K, int act) {
-  constexpr int KB = BITS == 8 ? 32 : 64;   // k per block (per 16 B lane load)
+    long long ldy, float* __restrict__ ws, int* __restrict__ cnt, int M, int N, int K, int act) {
+  constexpr int KB = BITS == 16 ? 16 : (BITS == 8 ? 32 : 64);  // k per block (16 B lane load)
   constexpr int NMF = KB / 16;               // MFMAs per block
   __shared__ float red[3][16][64];
   const int nt = blockIdx.x, mt = blockIdx.y, kz = blockIdx.z, KS = gridDim.z;
@@ -407,7 +482,9 @@ __global__ __launch_bounds__(256) void wo_gemm_kernel(
       if (kb0 + 4 * u >= kb_end) {  // zero the weight operand: the MFMA then adds nothing
         wv[u] = make_uint4(0, 0, 0, 0);
       }
-      if (BITS == 8) {
+      if (BITS == 16) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[u][0], __builtin_bit_cast(bf16x8, wv[u]), acc, 0, 0, 0);
+      } else if (BITS == 8) {
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[u][0], i8x8_to_bf16(wv[u].x, wv[u].y), acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[u][1], i8x8_to_bf16(wv[u].z, wv[u].w), acc, 0, 0, 0);
       } else {
@@ -428,18 +505,47 @@ __global__ __launch_bounds__(256) void wo_gemm_kernel(
   for (int r = 0; r < 16; ++r) acc[r] += red[0][r][lane] + red[1][r][lane] + red[2][r][lane];
   // D layout: column (n) = lane & 31, row (m) = (r&3) + 8*(r>>2) + 4*(lane>>5)
   const int n = nt * 32 + (lane & 31);
-  const float sc = scale[n];
+  const float sc = scale ? scale[n] : 1.f;
   const float bs = bias ? bf2f(bias[n]) : 0.f;
+  if (KS == 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int mm = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (mm < M) y[(long long)mm * ldy + n] = f2bf(act_apply(acc[r] * sc + bs, act));
+    }
+    return;
+  }
+  // split-K: every slice adds its partial into the zeroed f32 tile with memory-side atomics; the
+  // last-arriving slice takes (reads + re-zeroes) the sums and runs the epilogue — a stream-K
+  // style fixup with no second launch and no L2-flushing fence (see xcd_* in common.h)
+  if (cnt == nullptr) {  // slice mode (larger M): plain partial slices + wo_finalize_kernel
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int mm = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (mm < M) ws[((long long)kz * M + mm) * N + n] = acc[r];
+    }
+    return;
+  }
+  float sink = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int mm = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    if (mm < M) sink += xcd_add(ws + (long long)mm * N + n, acc[r]);
+  }
+  xcd_drain(sink);
+  int last = 0;
+  if (lane == 0) last = atomicAdd(&cnt[mt * gridDim.x + nt], 1) == KS - 1;
+  last = __shfl(last, 0, 64);
+  if (!last) return;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int mm = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
     if (mm < M) {
-      if (KS == 1)
-        y[(long long)mm * ldy + n] = f2bf(act_apply(acc[r] * sc + bs, act));
-      else
-        ws[((long long)kz * M + mm) * N + n] = acc[r];
+      const float v = xcd_take(ws + (long long)mm * N + n);
+      y[(long long)mm * ldy + n] = f2bf(act_apply(v * sc + bs, act));
     }
   }
+  if (lane == 0) atomicExch(&cnt[mt * gridDim.x + nt], 0);
 }
 
 __global__ void wo_finalize_kernel(const float* __restrict__ ws, int KS, const float* __restrict__ scale,
@@ -449,31 +555,40 @@ __global__ void wo_finalize_kernel(const float* __restrict__ ws, int KS, const f
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const int n = (int)(i % N);
-    const long long mm = i / N;
     float v = 0.f;
     for (int z = 0; z < KS; ++z) v += ws[(long long)z * total + i];
-    v = v * scale[n] + (bias ? bf2f(bias[n]) : 0.f);
-    y[mm * ldy + n] = f2bf(act_apply(v, act));
+    v = v * (scale ? scale[n] : 1.f) + (bias ? bf2f(bias[n]) : 0.f);
+    y[(i / N) * ldy + n] = f2bf(act_apply(v, act));
   }
 }
 
-// ws: KS*M*N f32 when KS > 1. Requires N % 32 == 0 and K % (BITS==8 ? 32 : 64) == 0.
+// KS > 1, fixup mode (cnt != null): ws = M*N zeroed f32, cnt = ceil(M/32)*(N/32) zeroed ints
+// (both left zeroed) — one launch. Slice mode (cnt == null): ws = KS*M*N f32, plus a finalize
+// launch (cheaper than memory-side atomics once M is large).
+// Requires N % 32 == 0 and K % KB == 0 (KB = 16 / 32 / 64 for bits = 16 / 8 / 4).
+// bits = 16: packed bf16 weights, scale may be null.
 PIAMD_EXPORT int piamd_wo_gemm(int bits, const void* x, long long ldx, const void* wp,
                                const float* scale, const void* bias, void* y, long long ldy,
-                               float* ws, int M, int N, int K, int KS, int act, hipStream_t st) {
-  const int KB = bits == 8 ? 32 : 64;
-  if ((bits != 8 && bits != 4) || N % 32 || K % KB || KS < 1 || (KS > 1 && !ws) || M < 1)
+                               float* ws, int* cnt, int M, int N, int K, int KS, int act,
+                               hipStream_t st) {
+  const int KB = bits == 16 ? 16 : (bits == 8 ? 32 : 64);
+  if ((bits != 16 && bits != 8 && bits != 4) || N % 32 || K % KB || KS < 1 ||
+      (KS > 1 && !ws) || M < 1)
     return (int)hipErrorInvalidValue;
   dim3 grid(N / 32, (M + 31) / 32, KS), block(256);
-  if (bits == 8)
+  if (bits == 16)
+    hipLaunchKernelGGL(wo_gemm_kernel<16>, grid, block, 0, st, (const bf16_t*)x, ldx,
+                       (const unsigned char*)wp, scale, (const bf16_t*)bias, (bf16_t*)y, ldy, ws,
+                       cnt, M, N, K, act);
+  else if (bits == 8)
     hipLaunchKernelGGL(wo_gemm_kernel<8>, grid, block, 0, st, (const bf16_t*)x, ldx,
                        (const unsigned char*)wp, scale, (const bf16_t*)bias, (bf16_t*)y, ldy, ws,
-                       M, N, K, act);
+                       cnt, M, N, K, act);
   else
     hipLaunchKernelGGL(wo_gemm_kernel<4>, grid, block, 0, st, (const bf16_t*)x, ldx,
                        (const unsigned char*)wp, scale, (const bf16_t*)bias, (bf16_t*)y, ldy, ws,
-                       M, N, K, act);
-  if (KS > 1)
+                       cnt, M, N, K, act);
+  if (KS > 1 && !cnt)
     hipLaunchKernelGGL(wo_finalize_kernel, dim3(stride_grid((long long)M * N, 256)), dim3(256), 0,
                        st, ws, KS, scale, (const bf16_t*)bias, (bf16_t*)y, ldy, M, N, act);
   return (int)hipGetLastError();

@@ -130,6 +130,74 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
   }
 }
 
+// Few-row variant (decode: rows = batch): one 256-thread workgroup per row so every operand of
+// the row (x, bias, residual, gamma, beta) is fetched in ONE round of 16 B loads issued up front;
+// the latency chain is load → block reduce ×2 → store instead of NV dependent wave iterations.
+template <int NV, bool BF16>
+__global__ __launch_bounds__(256) void ln_fwd_row_kernel(
+    const typename IO<BF16>::T* __restrict__ x, const typename IO<BF16>::T* __restrict__ bias,
+    const typename IO<BF16>::T* __restrict__ residual, const typename IO<BF16>::T* __restrict__ gamma,
+    const typename IO<BF16>::T* __restrict__ beta, typename IO<BF16>::T* __restrict__ y,
+    typename IO<BF16>::T* __restrict__ residual_out, float* __restrict__ mean_out,
+    float* __restrict__ rstd_out, int N, float eps, float p_drop, uint64_t seed, uint64_t offset) {
+  typedef IO<BF16> io;
+  __shared__ float red[4];
+  const int row = blockIdx.x, t = threadIdx.x;
+  const int nvec = N >> 3;
+  const size_t base = (size_t)row * N;
+  float v[NV][8], g[NV][8], bb[NV][8];
+  const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int vi = i * 256 + t;
+    if (vi < nvec) {
+      io::load8(x + base + vi * 8, v[i]);
+      if (gamma) io::load8(gamma + vi * 8, g[i]); else for (int j = 0; j < 8; ++j) g[i][j] = 1.f;
+      if (beta) io::load8(beta + vi * 8, bb[i]); else for (int j = 0; j < 8; ++j) bb[i][j] = 0.f;
+      float b[8], r[8];
+      if (bias) io::load8(bias + vi * 8, b);
+      if (residual) io::load8(residual + base + vi * 8, r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float a = v[i][j] + (bias ? b[j] : 0.f);
+        if (p_drop > 0.f) a = hash_uniform(seed, offset, base + vi * 8 + j) >= p_drop ? a * keep_scale : 0.f;
+        v[i][j] = a + (residual ? r[j] : 0.f);
+      }
+      if (residual_out) io::store8(residual_out + base + vi * 8, v[i]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[i][j];
+  const float mean = block_sum<4>(s, red) / (float)N;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+    if (i * 256 + t < nvec)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { const float d = v[i][j] - mean; ss += d * d; }
+  const float rstd = rsqrtf(block_sum<4>(ss, red) / (float)N + eps);
+  if (t == 0) {
+    if (mean_out) mean_out[row] = mean;
+    if (rstd_out) rstd_out[row] = rstd;
+  }
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int vi = i * 256 + t;
+    if (vi < nvec) {
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mean) * rstd * g[i][j] + bb[i][j];
+      io::store8(y + base + vi * 8, o);
+    }
+  }
+}
+
 // Backward. x_hat is recomputed from the saved pre-norm input `h` (= residual_out of forward, or x
 // when no prologue) and mean/rstd. Outputs:
 //   dh = LN_bwd(dy) (+ d_res_in if given)      -> written to dres (grad of residual input)
@@ -264,9 +332,20 @@ int launch_fwd(const void* x, const void* bias, const void* residual, const void
                const void* beta, void* y, void* residual_out, float* mean, float* rstd, int rows,
                int N, float eps, float p, uint64_t seed, uint64_t off, hipStream_t st) {
   typedef typename IO<BF16>::T T;
+  if (rows <= 64) {  // few rows (decode): a workgroup per row
+    const int nv2 = (N / 8 + 255) / 256;
+#define LNR(NVV)                                                                                \
+  case NVV:                                                                                     \
+    hipLaunchKernelGGL((ln_fwd_row_kernel<NVV, BF16>), dim3(rows), dim3(256), 0, st,           \
+                       (const T*)x, (const T*)bias, (const T*)residual, (const T*)gamma,       \
+                       (const T*)beta, (T*)y, (T*)residual_out, mean, rstd, N, eps, p, seed, off); \
+    return (int)hipGetLastError();
+    switch (nv2) { LNR(1) LNR(2) LNR(3) LNR(4) default: break; }
+#undef LNR
+  }
   const int nv = (N / 8 + 63) / 64;
   dim3 grid((rows + 3) / 4), block(256);
-#define LNF(NVV)                                                                                \
+#define LNF(NVV)                                                                              \
   case NVV:                                                                                     \
     hipLaunchKernelGGL((ln_fwd_kernel<NVV, BF16>), grid, block, 0, st, (const T*)x,            \
                        (const T*)bias, (const T*)residual, (const T*)gamma, (const T*)beta,    \

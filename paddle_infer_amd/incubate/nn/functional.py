@@ -190,16 +190,27 @@ def fused_multi_head_attention(x, qkv_weight, linear_weight, pre_layer_norm=Fals
 # ----------------------------------------------------------------------------- multi-transformer
 class _Linear:
     """A projection: bf16 weight ([in, out] Paddle layout, or [out, in] when ``trans``) or a
-    weight-only packed weight + scale."""
-    __slots__ = ("w", "scale", "bits", "trans")
+    weight-only packed weight + scale. ``packed``: an optional MFMA-tile packed bf16 copy used for
+    small-M (decode) calls, where the GEMM is a weight stream (see ops.inference.pack_bf16)."""
+    __slots__ = ("w", "scale", "bits", "trans", "packed")
+    PACKED_MAX_M = 64
 
-    def __init__(self, w, scale=None, bits=0, trans=False):
-        self.w, self.scale, self.bits, self.trans = w, scale, bits, trans
+    def __init__(self, w, scale=None, bits=0, trans=False, packed=None):
+        self.w, self.scale, self.bits, self.trans, self.packed = w, scale, bits, trans, packed
+
+    def prepack(self):
+        if not self.bits and self.packed is None:
+            w = self.w.t() if self.trans else self.w
+            if w.shape[1] % 32 == 0 and w.shape[0] % 16 == 0:
+                self.packed = _inf.pack_bf16(w.detach())
+        return self
 
     def __call__(self, x, bias=None, act="none"):
         if self.bits:
             return _inf.weight_only_linear(x, self.w, bias, self.scale,
                                            "int4" if self.bits == 4 else "int8", act)
+        if self.packed is not None and x.is_cuda and x.numel() // x.shape[-1] <= self.PACKED_MAX_M:
+            return _inf.packed_linear(x, self.packed, bias, act)
         y = F.linear(x, self.w) if self.trans else torch.matmul(x, self.w)
         if act != "none":
             return ops.bias_act(y, bias, act)
@@ -254,11 +265,13 @@ def multi_transformer_forward(x, layers, num_heads, num_kv_heads=None, pre_layer
         pending = None
         qkv = L["qkv"](xn)  # [T, (Hq+2Hk)*D]
         kc, vc = caches[li] if caches is not None else (None, None)
-        ops.qkv_prep(qkv, L.get("qkv_bias"), kc, vc, pos, B, S, hq, hk, D, rotary_dim,
-                     neox_rotary, rope_base)
-        if decode:
-            a = _inf.decode_attention(qkv, kc, vc, lens, hq, hk, attn_mask, max_len=max_len)
+        if decode:  # bias + RoPE + cache write fused into the split-K attention kernel
+            a = _inf.decode_attention(qkv, kc, vc, lens, hq, hk, attn_mask, max_len=max_len,
+                                      prep_bias=L.get("qkv_bias"), prep=True, rot_dim=rotary_dim,
+                                      neox=neox_rotary, base=rope_base)
         else:
+            ops.qkv_prep(qkv, L.get("qkv_bias"), kc, vc, pos, B, S, hq, hk, D, rotary_dim,
+                         neox_rotary, rope_base)
             a = attention_core(qkv.view(B, S, hq + 2 * hk, D), hq, hk, attn_mask, causal)
             a = a.reshape(T, hq * D)
         o = L["out"](a)

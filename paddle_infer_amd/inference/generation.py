@@ -25,7 +25,8 @@ from ..incubate.nn.functional import _lin
 
 class GPTGenerator:
     def __init__(self, model, max_batch: int = 8, max_seq_len: int | None = None,
-                 use_hip_graph: bool = True, cache_dtype=None, weight_only: str | None = None):
+                 use_hip_graph: bool = True, cache_dtype=None, weight_only: str | None = None,
+                 prepack: bool = True):
         self.model = model.eval()
         cfg = model.cfg
         self.cfg = cfg
@@ -53,6 +54,10 @@ class GPTGenerator:
                 for key in ("qkv", "out", "ffn1", "ffn2"):
                     q, s = weight_quantize(spec[key].w.detach(), algo)
                     spec[key] = _lin(q, s, bits)
+        elif self.device.type == "cuda" and prepack:  # MFMA-tile copies for decode GEMVs
+            for spec in self.layers:
+                for key in ("qkv", "out", "ffn1", "ffn2"):
+                    spec[key].prepack()
         self.act = "gelu_tanh" if cfg.activation in ("gelu_tanh", "gelu_new") else "gelu"
         self.final_ln = (model.gpt.final_ln.weight, model.gpt.final_ln.bias, cfg.layer_norm_eps)
         shape = (max_batch, self.Hk, self.max_seq_len, self.D)

@@ -63,11 +63,14 @@ _SIGS = {
                              c_ll, c_ll, c_ll, c_float, c_int, c_void_p],
     "piamd_qkv_prep": [c_void_p, c_ll, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                        c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p],
-    "piamd_decode_attn": [c_void_p, c_ll, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                          c_int, c_int, c_int, c_void_p, c_ll, c_float, c_void_p, c_void_p, c_ll,
-                          c_void_p],
+    # qkv, ldq, bias, prep, rot, neox, base, kc, vc, lens, B, Hq, Hk, D, maxS, chunk, nsplit,
+    # mask, ldm, scale, part, cnt, out, ldo, stream
+    "piamd_decode_attn": [c_void_p, c_ll, c_void_p, c_int, c_int, c_int, c_float, c_void_p,
+                          c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                          c_void_p, c_ll, c_float, c_void_p, c_void_p, c_void_p, c_ll, c_void_p],
+    # bits, x, ldx, wp, scale, bias, y, ldy, ws, cnt, M, N, K, KS, act, stream
     "piamd_wo_gemm": [c_int, c_void_p, c_ll, c_void_p, c_void_p, c_void_p, c_void_p, c_ll,
-                      c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
+                      c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "piamd_wo_dequant": [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
     "piamd_embedding_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_ll, c_void_p],
 }

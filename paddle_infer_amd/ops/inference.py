@@ -45,9 +45,12 @@ def _rope_ref(x, pos, rot, neox, base):
 
 
 def qkv_prep(qkv, bias, k_cache, v_cache, pos0, B, S, Hq, Hk, D, rot_dim=0, neox=True,
-             base=10000.0):
+             base=10000.0, pos_from_lens=None):
     """In place on ``qkv`` ([B*S, (Hq+2Hk)*D] rows, any row stride): add bias, rotate q/k,
-    write k/v into ``k_cache``/``v_cache`` ([B, Hk, maxS, D]) at positions pos0[b] + s."""
+    write k/v into ``k_cache``/``v_cache`` ([B, Hk, maxS, D]) at positions pos0[b] + s
+    (``pos_from_lens``: pos0 = lens - 1, the decode convention)."""
+    if pos_from_lens is not None:
+        pos0 = (pos_from_lens - 1).to(torch.int32)
     H = Hq + 2 * Hk
     if qkv.is_cuda:
         assert qkv.dtype == torch.bfloat16 and qkv.stride(-1) == 1 and qkv.shape[-1] >= H * D
@@ -91,9 +94,14 @@ def decode_chunking(max_len, chunk=None):
 
 
 def decode_attention(q, k_cache, v_cache, lens, Hq, Hk, mask=None, scale=None, out=None,
-                     max_len=None, chunk=None):
+                     max_len=None, chunk=None, prep_bias=None, prep=False, rot_dim=0, neox=True,
+                     base=10000.0):
     """q: [B, >=Hq*D] rows (head h at columns h*D); caches [B, Hk, maxS, D]; lens: [B] int32
-    number of valid keys (including the token just written). Returns out [B, Hq*D].
+    number of valid keys (including the new token, which sits at lens-1). Returns [B, Hq*D].
+
+    ``prep=True``: ``q`` is the raw QKV GEMM row of the new token ([Hq | Hk | Hk] heads); the
+    kernel adds ``prep_bias``, applies RoPE (``rot_dim`` 0 or D) and writes the new k/v into the
+    caches itself — one launch per layer for the whole decode attention.
     ``max_len`` bounds lens (defaults to the cache capacity, which is what a captured graph
     needs); it sets the split count."""
     B, _, maxS, D = k_cache.shape
@@ -104,23 +112,35 @@ def decode_attention(q, k_cache, v_cache, lens, Hq, Hk, mask=None, scale=None, o
         assert q.dtype == torch.bfloat16 and q.stride(-1) == 1 and k_cache.is_contiguous() \
             and v_cache.is_contiguous() and lens.dtype == torch.int32 and lens.is_cuda
         assert Hq % Hk == 0 and (Hq // Hk) in (1, 2, 4, 8) and D in (64, 128)
+        if prep and rot_dim not in (0, D):  # partial rotary: separate prologue kernel
+            q = qkv_prep(q.clone(), prep_bias, k_cache, v_cache, None, B, 1, Hq, Hk, D, rot_dim, neox, base,
+                     pos_from_lens=lens)
+            prep, prep_bias, rot_dim = False, None, 0
         ck, ns = decode_chunking(max_len or maxS, chunk)
-        part = None
+        part = cnt = None
         if ns > 1:
             key = (q.device, B, Hq, ns, D)
-            part = _PART_CACHE.get(key)
-            if part is None:
-                part = _PART_CACHE[key] = torch.empty(B * Hq * ns * (D + 2), dtype=torch.float32,
-                                                      device=q.device)
+            ent = _PART_CACHE.get(key)
+            if ent is None:
+                ent = _PART_CACHE[key] = (
+                    torch.empty(B * Hq * ns * (D + 2), dtype=torch.float32, device=q.device),
+                    torch.zeros(B * Hk, dtype=torch.int32, device=q.device))
+            part, cnt = ent
         ldm = 0
         if mask is not None:
             mask = mask.reshape(B, -1)
             assert mask.dtype == torch.bfloat16 and mask.stride(-1) == 1
             ldm = mask.stride(0)
-        _lib.call("piamd_decode_attn", q.data_ptr(), q.stride(0), k_cache.data_ptr(),
+        _lib.call("piamd_decode_attn", q.data_ptr(), q.stride(0), _lib.ptr(prep_bias), int(prep),
+                  int(rot_dim), int(bool(neox)), float(base), k_cache.data_ptr(),
                   v_cache.data_ptr(), lens.data_ptr(), B, Hq, Hk, D, maxS, ck, ns, _lib.ptr(mask),
-                  ldm, float(scale), _lib.ptr(part), out.data_ptr(), out.stride(0), _lib.stream())
+                  ldm, float(scale), _lib.ptr(part), _lib.ptr(cnt), out.data_ptr(), out.stride(0),
+                  _lib.stream())
         return out
+    if prep:
+        q = q.clone()
+        qkv_prep(q, prep_bias, k_cache, v_cache, None, B, 1, Hq, Hk, D, rot_dim, neox, base,
+                 pos_from_lens=lens)
     G = Hq // Hk
     for b in range(B):
         n = int(lens[b])
@@ -160,6 +180,68 @@ def _unpack(wp, bits, N, K):
     t = torch.stack([lo, hi], -1)
     t = torch.where(t >= 8, t - 16, t).to(torch.int8)
     return t.permute(0, 3, 1, 2, 4, 5).contiguous().reshape(N, K)
+
+
+def pack_bf16(w_kn):
+    """bf16 serving weight [K, N] (Paddle [in, out]) → MFMA-tile packed [N, K] (see infer.hip)."""
+    K, N = w_kn.shape
+    assert N % 32 == 0 and K % 16 == 0, "packed bf16 GEMM needs N % 32 == 0 and K % 16 == 0"
+    t = w_kn.t().contiguous().view(N // 32, 32, K // 16, 2, 8).permute(0, 2, 3, 1, 4)
+    return t.contiguous().view(N, K)
+
+
+def packed_linear(x, wp, bias=None, act="none"):
+    """y = act(x @ W + bias) with W pre-packed by :func:`pack_bf16` (small-M decode GEMMs: one
+    fully-coalesced 1 KB weight load per wave per MFMA, split-K to fill 256 CUs)."""
+    N, K = wp.shape
+    lead = x.shape[:-1]
+    x2 = x.reshape(-1, K)
+    if x2.stride(-1) != 1:
+        x2 = x2.contiguous()
+    M = x2.shape[0]
+    if not x.is_cuda:
+        w = wp.view(N // 32, K // 16, 2, 32, 8).permute(0, 3, 1, 2, 4).reshape(N, K)
+        y = x2.float() @ w.float().t()
+        if bias is not None:
+            y = y + bias.float()
+        return _ref_act(y, ACTS[act]).to(x.dtype).reshape(*lead, N)
+    y = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    tiles = (N // 32) * ((M + 31) // 32)
+    KS = _split_k(tiles, K // 16)
+    ws, cnt = _splitk_bufs(x.device, KS, M, N, tiles)
+    _lib.call("piamd_wo_gemm", 16, x2.data_ptr(), x2.stride(0), wp.data_ptr(), None,
+              _lib.ptr(bias), y.data_ptr(), y.stride(0), _lib.ptr(ws), _lib.ptr(cnt), M, N, K, KS,
+              ACTS[act], _lib.stream())
+    return y.reshape(*lead, N)
+
+
+def _split_k(tiles, kb):
+    KS = 1
+    while tiles * KS < 512 and kb // (KS * 2) >= 16:
+        KS *= 2
+    return KS
+
+
+FIXUP_MAX_M = 8  # split-K reduction: in-kernel atomic fixup up to this M, slices + finalize above
+
+
+def _splitk_bufs(device, KS, M, N, tiles):
+    if KS == 1:
+        return None, None
+    if M <= FIXUP_MAX_M:
+        return _ws_buf(device, M * N, tiles)
+    return _ws_buf(device, KS * M * N, 0)[0], None
+
+
+def _ws_buf(device, n, tiles):
+    """Split-K partial workspace + per-tile arrival counters (kept zeroed by the kernel). Shared
+    by every launch on the stream: GEMMs on one stream never overlap."""
+    key = (device, n, tiles)
+    ent = _WS.get(key)
+    if ent is None:
+        ent = _WS[key] = (torch.zeros(n, dtype=torch.float32, device=device),
+                          torch.zeros(tiles, dtype=torch.int32, device=device))
+    return ent
 
 
 def weight_quantize(x, algo="weight_only_int8"):
@@ -214,19 +296,11 @@ def weight_only_linear(x, weight, bias=None, weight_scale=None, weight_dtype="in
             return y.reshape(*lead, N)
         y = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
         tiles = (N // 32) * ((M + 31) // 32)
-        kb = K // (32 if bits == 8 else 64)
-        KS = 1
-        while tiles * KS < 512 and kb // (KS * 2) >= 16:
-            KS *= 2
-        ws = None
-        if KS > 1:
-            key = (x.device, KS * M * N)
-            ws = _WS.get(key)
-            if ws is None:
-                ws = _WS[key] = torch.empty(KS * M * N, dtype=torch.float32, device=x.device)
+        KS = _split_k(tiles, K // (32 if bits == 8 else 64))
+        ws, cnt = _splitk_bufs(x.device, KS, M, N, tiles)
         _lib.call("piamd_wo_gemm", bits, x2.data_ptr(), x2.stride(0), weight.data_ptr(),
-                  scale.data_ptr(), _lib.ptr(bias), y.data_ptr(), y.stride(0), _lib.ptr(ws), M, N,
-                  K, KS, act, _lib.stream())
+                  scale.data_ptr(), _lib.ptr(bias), y.data_ptr(), y.stride(0), _lib.ptr(ws),
+                  _lib.ptr(cnt), M, N, K, KS, act, _lib.stream())
         return y.reshape(*lead, N)
     w = _unpack(weight, bits, N, K).float() * weight_scale.float()[:, None]
     y = x2.float() @ w.t()

@@ -38,7 +38,8 @@ def main():
     for mode in a.modes:
         gen = GPTGenerator(model, max_batch=max(a.batch), max_seq_len=a.prompt + a.gen + 8,
                            use_hip_graph=(mode != "eager"),
-                           weight_only=mode if mode in ("int8", "int4") else None)
+                           weight_only=mode if mode in ("int8", "int4") else None,
+                           prepack=(mode != "graph_blaslt"))
         for B in a.batch:
             ids = torch.randint(0, cfg.vocab_size, (B, a.prompt), device="cuda")
             lens = torch.full((B,), a.prompt, device="cuda")

@@ -72,6 +72,12 @@ def colsum_into(x2, out, accumulate=True):
               G, rows, N, int(accumulate), _lib.stream())
 
 
+def _recordable(fn):
+    from ..static.framework import recordable
+    return recordable("linear")(fn)
+
+
+@_recordable
 def linear(x, weight, bias=None):
     """y = x @ weight (+ bias); weight is ``[in_features, out_features]``."""
     if weight.requires_grad or getattr(weight, "main_grad", None) is not None:

@@ -98,7 +98,8 @@ def func_name(func):
         return f"torch._tensor.{q}"
     name = f"{mod}.{q}" if mod else q
     try:
-        if resolve_func(name) is func:
+        r = resolve_func(name)
+        if r is func or getattr(r, "__wrapped__", None) is func:  # recordable() wrappers
             return name
     except (AttributeError, ImportError, ValueError):
         pass

@@ -150,3 +150,6 @@ def fire(p):
     hook = getattr(p, "_grad_ready", None)
     if hook is not None:
         hook(p)
+
+
+_SIGS["piamd_nan_inf_check"] = [c_int, c_void_p, c_ll, c_void_p, c_int, c_void_p]

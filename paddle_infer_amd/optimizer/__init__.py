@@ -66,6 +66,9 @@ class Optimizer:
     clear_gradients = clear_grad
 
     def _params_grads(self):
+        from ..utils import nan_inf
+        if nan_inf.enabled():  # FLAGS_check_nan_inf: one host read per step
+            nan_inf.check()
         pg = [(p, p.grad) for p in self._parameter_list if p.requires_grad]
         if self._grad_clip is not None:
             pg = self._grad_clip(pg)

@@ -268,6 +268,9 @@ class FlatTrainer:
     def step(self, lr=None):
         lr = self.lr if lr is None else lr
         self._finish_reduction()
+        from ..utils import nan_inf
+        if nan_inf.enabled():  # FLAGS_check_nan_inf: one host read per step
+            nan_inf.check()
         self.step_count += 1
         gscale = None
         if self.grad_clip:

@@ -1,0 +1,255 @@
+// bf16 MFMA GEMM with fused epilogues, C[M,N] = A[M,K] · B[K,N] (f32 accumulate).
+//
+// Parity: reference `paddle/phi/kernels/funcs/blas` matmul + `fused_gemm_epilogue_op.cu`
+// (cublasLt epilogues: bias, bias+GELU with aux, dGELU) used by FusedFeedForward / fused_linear.
+// Plain GEMMs without an epilogue stay on hipBLASLt; this kernel exists for the fusions the
+// library cannot express on MI355X (activation-gradient epilogue reading the saved
+// pre-activation, f32 main-grad accumulation, GELU-tanh with aux pre-activation output).
+//
+// Structure (cdna_hip_programming.md §5: 256² tile, glds, BK = 64):
+//   * workgroup = 8 waves (2 M × 4 N), tile 256 × 256, each wave 128 × 64 = 4 × 2 blocks of
+//     v_mfma_f32_32x32x16_bf16; SWAPPED operands (Cᵀ = Bᵀ·Aᵀ) so each lane owns one output row
+//     and 4 consecutive columns per register quad → 8-byte epilogue stores;
+//   * both operands staged global → LDS with global_load_lds_dwordx4 (no VGPR round trip) into two
+//     LDS stages (128 KiB), the next K-tile's DMA in flight under the current tile's MFMAs;
+//   * operand layouts: K-contiguous (row-major A, or B given as [N][K]) images are read with
+//     ds_read_b128; M/N-contiguous images (row-major B = weights [K][N], or A given as [K][M] for
+//     weight gradients) with the hardware transpose read ds_read_b64_tr_b16 — so forward,
+//     data-gradient and weight-gradient GEMMs all run without a transpose kernel;
+//   * XOR-swizzled LDS images (swizzle applied to the per-lane global SOURCE address, the LDS
+//     side of a DMA being lane-linear) keep both read kinds bank-conflict free;
+//   * bijective XCD-aware tile order: consecutive tiles of one XCD share an A row-panel in L2.
+#include "common.h"
+
+namespace {
+
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4;
+
+constexpr int BM = 256, BN = 256, BK = 64, NWAVE = 8, NTHR = NWAVE * 64;
+constexpr int TILE_BYTES = 256 * BK * 2;            // one operand image per stage (32 KiB)
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;
+
+// XOR image with ROWB-byte rows (16-B chunks permuted by the low row bits).
+template <int ROWB>
+__device__ __forceinline__ int img_off(int row, int ch) {
+  constexpr int CH = ROWB / 16;
+  const int x = ((((row & 3) << 2) | ((row >> 2) & 3)) ^ ((row >> 4) & 0)) & (CH - 1);
+  return row * ROWB + ((ch ^ x) << 4);
+}
+
+__device__ __forceinline__ bf16x8 rd_row(const char* base, int off) {
+  return *reinterpret_cast<const bf16x8*>(base + off);
+}
+
+template <int ROWB>
+__device__ __forceinline__ s16x4_t rd_tr4(const char* base, int r0, int c0, int gi) {
+  const int q = gi >> 2, p = gi & 3;
+  const int col = c0 + 4 * p;
+  const int off = img_off<ROWB>(r0 + q, col >> 3) + ((col & 7) << 1);
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + off));
+}
+
+__device__ __forceinline__ bf16x8 cat44(s16x4_t a, s16x4_t b) {
+  s16x8 t = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, t);
+}
+
+// DMA a [ROWS][ROWB] bf16 tile (row r at gbase + min(r0 + r, rmax) * ld, 16-B chunk c at +8c)
+// into the XOR image at `img`; NWAVE waves share the pieces (1 KiB per wave-instruction).
+template <int ROWS, int ROWB>
+__device__ __forceinline__ void dma_tile(const bf16_t* gbase, long long ld, int r0, int rmax,
+                                         char* img, int w, int lane) {
+  constexpr int CH = ROWB / 16;
+  constexpr int PIECES = ROWS * ROWB / 1024;
+  constexpr int PPW = PIECES / NWAVE;
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int P = w * PPW + i;
+    const int L = P * 64 + lane, r = L / CH, pc = L % CH;
+    const int x = (((r & 3) << 2) | ((r >> 2) & 3)) & (CH - 1);
+    const long long row = min(r0 + r, rmax);
+    const bf16_t* src = gbase + row * ld + ((pc ^ x) << 3);
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(img + P * 1024),
+                                     16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ float act_fwd(float v, int act) {
+  switch (act) {
+    case 1: return gelu_tanh(v);
+    case 2: return gelu_erf(v);
+    case 3: return fmaxf(v, 0.f);
+    case 4: return v / (1.f + __expf(-v));
+    default: return v;
+  }
+}
+__device__ __forceinline__ float act_grad(float h, int act) {
+  switch (act) {
+    case 1: return gelu_tanh_grad(h);
+    case 2: return gelu_erf_grad(h);
+    case 3: return h > 0.f ? 1.f : 0.f;
+    case 4: { const float s = 1.f / (1.f + __expf(-h)); return s * (1.f + h * (1.f - s)); }
+    default: return 1.f;
+  }
+}
+
+// Epilogue kinds
+enum { EPI_STORE = 0, EPI_BIAS_ACT = 1, EPI_DACT = 2 };
+
+// A_KC: A[m][k] at a + m*lda + k (else A[m][k] at a + k*lda + m)
+// B_KC: B[k][n] at b + n*ldb + k (else B[k][n] at b + k*ldb + n)
+template <bool A_KC, bool B_KC>
+__global__ __launch_bounds__(NTHR, 1) void gemm_kernel(
+    const bf16_t* __restrict__ a, long long lda, const bf16_t* __restrict__ b, long long ldb,
+    void* __restrict__ c, long long ldc, int c_f32, int accumulate, int M, int N, int K, int epi,
+    int act, const bf16_t* __restrict__ bias, bf16_t* __restrict__ aux, long long ldaux) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w >> 2, wc = w & 3;  // 2 (M) x 4 (N) waves
+
+  // ---- bijective XCD-aware tile order (guide T1) ----
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN, nwg = tm * tn;
+  const int orig = blockIdx.x, xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+  const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+  const int bm = wg / tn, bn = wg % tn;   // consecutive wg on one XCD walk N: A panel reused
+  const int m0 = bm * BM, n0 = bn * BN;
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto stage_load = [&](int kt, int s) {
+    char* ai = smem + s * STAGE_BYTES;
+    char* bi = ai + TILE_BYTES;
+    const int k0 = kt * BK;
+    if (A_KC) dma_tile<256, 128>(a + k0, lda, m0, M - 1, ai, w, lane);         // [256 m][64 k]
+    else      dma_tile<64, 512>(a + (long long)k0 * lda + m0, lda, 0, 63, ai, w, lane);  // [64 k][256 m]
+    if (B_KC) dma_tile<256, 128>(b + k0, ldb, n0, N - 1, bi, w, lane);         // [256 n][64 k]
+    else      dma_tile<64, 512>(b + (long long)k0 * ldb + n0, ldb, 0, 63, bi, w, lane);  // [64 k][256 n]
+  };
+
+  const int nk = K / BK;
+  stage_load(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int gi = lane & 15, hi = lane >> 5, half16 = (lane >> 4) & 1, l31 = lane & 31;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int s = kt & 1;
+    if (kt + 1 < nk) stage_load(kt + 1, s ^ 1);
+    const char* ai = smem + s * STAGE_BYTES;
+    const char* bi = ai + TILE_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8 af[4], bf[2];
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) {
+        const int mrow = wr * 128 + mb * 32;
+        if (A_KC) af[mb] = rd_row(ai, img_off<128>(mrow + l31, 2 * ks + hi));
+        else af[mb] = cat44(rd_tr4<512>(ai, 16 * ks + 8 * hi, mrow + 16 * half16, gi),
+                            rd_tr4<512>(ai, 16 * ks + 8 * hi + 4, mrow + 16 * half16, gi));
+      }
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const int ncol = wc * 64 + nb * 32;
+        if (B_KC) bf[nb] = rd_row(bi, img_off<128>(ncol + l31, 2 * ks + hi));
+        else bf[nb] = cat44(rd_tr4<512>(bi, 16 * ks + 8 * hi, ncol + 16 * half16, gi),
+                            rd_tr4<512>(bi, 16 * ks + 8 * hi + 4, ncol + 16 * half16, gi));
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+          acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[nb], af[mb], acc[mb][nb], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane owns row m0+wr*128+mb*32+l31; columns n = ncol + 8g + 4*hi + (0..3) ----
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) {
+    const int m = m0 + wr * 128 + mb * 32 + l31;
+    if (m >= M) continue;
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = n0 + wc * 64 + nb * 32 + 8 * g + 4 * hi;
+        if (n >= N) continue;
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = acc[mb][nb][4 * g + j];
+        if (epi == EPI_BIAS_ACT) {
+          u16x4 pre;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v[j] += bias ? bf2f(bias[n + j]) : 0.f;
+            pre[j] = f2bf(v[j]);
+            v[j] = act_fwd(bf2f(pre[j]), act);
+          }
+          if (aux) *reinterpret_cast<u16x4*>(aux + (long long)m * ldaux + n) = pre;
+        } else if (epi == EPI_DACT) {
+          const u16x4 h = *reinterpret_cast<const u16x4*>(aux + (long long)m * ldaux + n);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] *= act_grad(bf2f(h[j]), act);
+        }
+        if (c_f32) {
+          f32x4* p = reinterpret_cast<f32x4*>((float*)c + (long long)m * ldc + n);
+          f32x4 o = accumulate ? *p : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] += v[j];
+          *p = o;
+        } else {
+          u16x4 o;
+          bf16_t* p = (bf16_t*)c + (long long)m * ldc + n;
+          if (accumulate) {
+            const u16x4 old = *reinterpret_cast<const u16x4*>(p);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j] + bf2f(old[j]));
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j]);
+          }
+          *reinterpret_cast<u16x4*>(p) = o;
+        }
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// trans_a: A given as [K][M] (lda ≥ M); else [M][K] (lda ≥ K).
+// trans_b: B given as [N][K] (ldb ≥ K); else [K][N] (ldb ≥ N).
+// Requirements: K % 64 == 0; M % 256 == 0 when trans_a; N % 256 == 0 when !trans_b;
+// N % 4 == 0; 16-byte aligned operand rows. c_f32: C is f32 (else bf16); accumulate: C += A·B.
+// epi: 0 store, 1 bias+act with aux = pre-activation (bf16 [M][N], may be null), 2 C = A·B ⊙ act'(aux).
+PIAMD_EXPORT int piamd_gemm(const void* a, long long lda, int trans_a, const void* b, long long ldb,
+                            int trans_b, void* c, long long ldc, int c_f32, int accumulate, int M,
+                            int N, int K, int epi, int act, const void* bias, void* aux,
+                            long long ldaux, hipStream_t st) {
+  if (K % BK || N % 4 || (trans_a && M % BM) || (!trans_b && N % BN) || M <= 0 || N <= 0 ||
+      (epi == EPI_DACT && !aux))
+    return (int)hipErrorInvalidValue;
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  dim3 grid(tiles), block(NTHR);
+#define GEMM_LAUNCH(AK, BKC)                                                                     \
+  hipLaunchKernelGGL((gemm_kernel<AK, BKC>), grid, block, 0, st, (const bf16_t*)a, lda,          \
+                     (const bf16_t*)b, ldb, c, ldc, c_f32, accumulate, M, N, K, epi, act,         \
+                     (const bf16_t*)bias, (bf16_t*)aux, ldaux)
+  if (!trans_a && !trans_b) GEMM_LAUNCH(true, false);
+  else if (!trans_a && trans_b) GEMM_LAUNCH(true, true);
+  else if (trans_a && !trans_b) GEMM_LAUNCH(false, false);
+  else GEMM_LAUNCH(false, true);
+#undef GEMM_LAUNCH
+  return (int)hipGetLastError();
+}

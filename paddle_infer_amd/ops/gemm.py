@@ -1,0 +1,82 @@
+"""Hand-written MFMA GEMM with fused epilogues (``csrc/kernels/gemm.hip``).
+
+``gemm(a, b)`` computes ``A·B`` for 2-D operands where ``trans_a`` means ``a`` is stored
+[K, M] and ``trans_b`` means ``b`` is stored [N, K] (so weights kept [in, out] serve forward,
+data-gradient and weight-gradient products without copies). Epilogues:
+
+* ``epi="bias_act"``: ``pre = A·B + bias`` is written to ``aux`` and ``act(pre)`` to C (FFN1);
+* ``epi="dact"``: ``C = (A·B) ⊙ act'(aux)`` (the FFN1 activation backward fused into the FFN2
+  data-gradient GEMM);
+* ``out`` f32 with ``accumulate=True``: C += A·B (weight gradient straight into main_grad).
+
+CPU tensors run the PyTorch reference of the same contract (tests' numerics reference).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+from .activation import ACTS, _ref_act
+
+_EPI = {"none": 0, "bias_act": 1, "dact": 2}
+
+
+def _act_grad_ref(h, act):
+    h = h.float().detach().requires_grad_(True)
+    with torch.enable_grad():
+        y = _ref_act(h, act)
+        (g,) = torch.autograd.grad(y.sum(), h)
+    return g
+
+
+def supported(a, b, trans_a=False, trans_b=False):
+    if not (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16):
+        return False
+    M = a.shape[1] if trans_a else a.shape[0]
+    K = a.shape[0] if trans_a else a.shape[1]
+    N = b.shape[0] if trans_b else b.shape[1]
+    return (K % 64 == 0 and N % 4 == 0 and (not trans_a or M % 256 == 0)
+            and (trans_b or N % 256 == 0) and a.stride(-1) == 1 and b.stride(-1) == 1)
+
+
+def gemm(a, b, trans_a=False, trans_b=False, out=None, out_f32=False, accumulate=False,
+         epi="none", act="none", bias=None, aux=None):
+    M = a.shape[1] if trans_a else a.shape[0]
+    K = a.shape[0] if trans_a else a.shape[1]
+    N = b.shape[0] if trans_b else b.shape[1]
+    e, ac = _EPI[epi], ACTS[act]
+    if epi == "bias_act" and aux is None and a.is_cuda:
+        pass  # aux optional (inference)
+    if not a.is_cuda:
+        A = a.t() if trans_a else a
+        B = b.t() if trans_b else b
+        y = A.float() @ B.float()
+        if e == 1:
+            y = y + (bias.float() if bias is not None else 0.0)
+            pre = y.to(torch.bfloat16)
+            if aux is not None:
+                aux.copy_(pre)
+            y = _ref_act(pre.float(), ac)
+        elif e == 2:
+            y = y * _act_grad_ref(aux, ac)
+        if out is None:
+            return y.to(torch.float32 if out_f32 else a.dtype)
+        if accumulate:
+            out.add_(y.to(out.dtype))
+        else:
+            out.copy_(y)
+        return out
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32 if out_f32 else torch.bfloat16, device=a.device)
+    assert out.stride(-1) == 1 and out.shape == (M, N)
+    if aux is not None:
+        assert aux.shape == (M, N) and aux.dtype == torch.bfloat16 and aux.stride(-1) == 1
+    _lib.call("piamd_gemm", a.data_ptr(), a.stride(0), int(trans_a), b.data_ptr(), b.stride(0),
+              int(trans_b), out.data_ptr(), out.stride(0), int(out.dtype == torch.float32),
+              int(accumulate), M, N, K, e, ac, _lib.ptr(bias), _lib.ptr(aux),
+              aux.stride(0) if aux is not None else 0, _lib.stream())
+    return out
+
+
+F  # noqa

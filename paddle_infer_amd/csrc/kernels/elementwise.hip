@@ -40,21 +40,34 @@ __global__ __launch_bounds__(256) void bias_act_fwd_kernel(const bf16_t* __restr
                                                           bf16_t* __restrict__ y,
                                                           bf16_t* __restrict__ pre, long long n8,
                                                           int N) {
+  // 4 independent 16-B loads in flight per thread before any math (latency hiding at
+  // grid-stride; the memory pipe, not the ALU, bounds this kernel)
+  constexpr int U = 4;
   const long long stride = (long long)gridDim.x * blockDim.x;
   const int nb8 = N >> 3;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
-    u16x8 r = reinterpret_cast<const u16x8*>(x)[i], o, pr;
-    u16x8 b;
-    if (bias) b = reinterpret_cast<const u16x8*>(bias)[i % nb8];
+  for (long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; i0 < n8; i0 += U * stride) {
+    u16x8 r[U], b[U];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float v = bf2f(r[j]);
-      if (bias) v += bf2f(b[j]);
-      pr[j] = f2bf(v);
-      o[j] = f2bf(act_f<ACT>(v));
+    for (int u = 0; u < U; ++u) {
+      const long long i = min(i0 + u * stride, n8 - 1);
+      r[u] = reinterpret_cast<const u16x8*>(x)[i];
+      if (bias) b[u] = reinterpret_cast<const u16x8*>(bias)[i % nb8];
     }
-    if (pre) reinterpret_cast<u16x8*>(pre)[i] = pr;
-    reinterpret_cast<u16x8*>(y)[i] = o;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long i = i0 + u * stride;
+      if (i >= n8) break;
+      u16x8 o, pr;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = bf2f(r[u][j]);
+        if (bias) v += bf2f(b[u][j]);
+        pr[j] = f2bf(v);
+        o[j] = f2bf(act_f<ACT>(v));
+      }
+      if (pre) reinterpret_cast<u16x8*>(pre)[i] = pr;
+      reinterpret_cast<u16x8*>(y)[i] = o;
+    }
   }
 }
 
@@ -71,20 +84,32 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const bf16_t* __restr
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   u16x8 b;
   if (bias && colok) b = reinterpret_cast<const u16x8*>(bias)[c8];
-  for (int r = blockIdx.x; colok && r < rows; r += gridDim.x) {
-    const size_t idx = ((size_t)r * N >> 3) + c8;
-    u16x8 d = reinterpret_cast<const u16x8*>(dy)[idx];
-    u16x8 hv = reinterpret_cast<const u16x8*>(h)[idx];
-    u16x8 o;
+  constexpr int U = 4;  // rows in flight per thread
+  for (int r0 = blockIdx.x; colok && r0 < rows; r0 += U * gridDim.x) {
+    u16x8 d[U], hv[U];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float hh = bf2f(hv[j]);
-      if (bias) hh += bf2f(b[j]);
-      float g = bf2f(d[j]) * act_g<ACT>(hh);
-      o[j] = f2bf(g);
-      acc[j] += g;
+    for (int u = 0; u < U; ++u) {
+      const int r = min(r0 + u * (int)gridDim.x, rows - 1);
+      const size_t idx = ((size_t)r * N >> 3) + c8;
+      d[u] = reinterpret_cast<const u16x8*>(dy)[idx];
+      hv[u] = reinterpret_cast<const u16x8*>(h)[idx];
     }
-    reinterpret_cast<u16x8*>(dx)[idx] = o;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = r0 + u * (int)gridDim.x;
+      if (r >= rows) break;
+      const size_t idx = ((size_t)r * N >> 3) + c8;
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float hh = bf2f(hv[u][j]);
+        if (bias) hh += bf2f(b[j]);
+        float g = bf2f(d[u][j]) * act_g<ACT>(hh);
+        o[j] = f2bf(g);
+        acc[j] += g;
+      }
+      reinterpret_cast<u16x8*>(dx)[idx] = o;
+    }
   }
   if (part) {
     // transpose the per-thread 8-column sums through LDS so every atomic wave-instruction adds

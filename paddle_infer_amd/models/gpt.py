@@ -46,7 +46,9 @@ class GPTConfig:
     attention_probs_dropout_prob: float = 0.0
     layer_norm_eps: float = 1e-5
     initializer_range: float = 0.02
-    activation: str = "gelu"
+    # tanh-approximate GELU like the reference GPT (auto_parallel_gpt_model.py:542,
+    # F.gelu(..., approximate=True)); "gelu" selects the exact erf form
+    activation: str = "gelu_tanh"
     tie_word_embeddings: bool = True
     dtype: str = "bfloat16"
     recompute: bool = False

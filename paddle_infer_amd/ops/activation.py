@@ -33,10 +33,11 @@ class _BiasActFn(torch.autograd.Function):
         N = x.shape[-1]
         x2 = x.contiguous()
         y = torch.empty_like(x2)
-        pre = torch.empty_like(x2) if bias is not None else None
+        # the pre-activation is NOT materialised: backward re-adds the bias to the saved GEMM
+        # output in registers (saves one [tokens x 4h] write per layer)
         _lib.call("piamd_bias_act_fwd", act, x2.data_ptr(), _lib.ptr(bias), y.data_ptr(),
-                  _lib.ptr(pre), x2.numel(), N, _lib.stream())
-        ctx.save_for_backward(x2 if pre is None else pre)
+                  None, x2.numel(), N, _lib.stream())
+        ctx.save_for_backward(x2)
         ctx.act = act
         ctx.has_bias = bias is not None
         ctx.bias_param = bias
@@ -58,9 +59,10 @@ class _BiasActFn(torch.autograd.Function):
             else:
                 db = torch.empty(N, device=h.device, dtype=h.dtype)
             part = torch.empty((N,), device=h.device, dtype=torch.float32)
-        # pre-activation already includes the bias: pass bias=None to the backward
-        _lib.call("piamd_bias_act_bwd", ctx.act, dy.data_ptr(), h.data_ptr(), None, dx.data_ptr(),
-                  _lib.ptr(db), _lib.ptr(part), rows, N, acc, _lib.stream())
+        # h is the GEMM output without bias: the kernel adds the bias before act'()
+        _lib.call("piamd_bias_act_bwd", ctx.act, dy.data_ptr(), h.data_ptr(),
+                  _lib.ptr(ctx.bias_param), dx.data_ptr(), _lib.ptr(db), _lib.ptr(part), rows, N,
+                  acc, _lib.stream())
         if acc:
             _lib.fire(ctx.bias_param)
             db = None

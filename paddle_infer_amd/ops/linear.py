@@ -66,7 +66,7 @@ def colsum_into(x2, out, accumulate=True):
     """out[N] (+)= Σ_rows x2[rows, N] via the HIP column-sum kernel (bias gradients)."""
     from . import _lib
     rows, N = x2.shape
-    G = 64
+    G = max(1, min(256, rows // 16))
     part = torch.empty((G, N), device=x2.device, dtype=torch.float32)
     _lib.call("piamd_colsum", _lib.dtype_code(x2), x2.data_ptr(), out.data_ptr(), part.data_ptr(),
               G, rows, N, int(accumulate), _lib.stream())

@@ -43,7 +43,7 @@ def main():
     ap.add_argument("--dropout", type=float, default=0.1)
     ap.add_argument("--recompute", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0)
-    ap.add_argument("--tuned-gemm", type=int, default=1,
+    ap.add_argument("--tuned-gemm", type=int, default=0,
                     help="replay the in-tree TunableOp GEMM table (paddle_infer_amd/tuning)")
     args = ap.parse_args()
 

@@ -165,6 +165,81 @@ class FlatTrainer:
         self._norm_buf = torch.zeros(2, device=device, dtype=torch.float32)
         self._clip_coef = torch.ones((), device=device, dtype=torch.float32)
         self._ag_handles = []
+        self._ag_pending = {}  # (group idx, bucket idx) -> all-gather handle
+        if self.sharding and overlap:
+            self._install_forward_waits(model)
+
+    def _install_forward_waits(self, model):
+        """Sharded params are all-gathered bucket by bucket right after the optimizer step, in the
+        order the next forward NEEDS them; each module waits only for the buckets holding its
+        parameters (forward pre-hook), so the all-gather of later layers overlaps the forward of
+        earlier ones instead of stalling the start of the next step.
+
+        Which module "uses" a parameter is learned from the first forward: a parameter belongs to
+        the nearest ancestor of its owner whose forward actually runs (parameter-holder modules
+        that are never called, e.g. LayerNorm weight containers read by their parent, map to that
+        parent); the bucket launch order is the order those modules first run."""
+        self._model = model
+        self._calls = []
+        self._rec_handles = [m.register_forward_pre_hook(self._record_call) for m in model.modules()]
+        self._need_order = None
+
+    def _record_call(self, module, args):
+        if self._calls is not None:
+            self._calls.append(module)
+
+    def _finalize_forward_waits(self):
+        model = self._model
+        for h in self._rec_handles:
+            h.remove()
+        called = {id(m) for m in self._calls}
+        parent = {}
+        for m in model.modules():
+            for c in m.children():
+                parent.setdefault(id(c), m)
+        where = {}
+        for gi, g in enumerate(self.groups):
+            for bi, b in enumerate(g.buckets):
+                for p in b.params:
+                    where[id(p)] = (gi, bi)
+        keys_of = {}
+        for m in model.modules():
+            for p in m.parameters(recurse=False):
+                if id(p) not in where:
+                    continue
+                u = m
+                while id(u) not in called and id(u) in parent:
+                    u = parent[id(u)]
+                keys_of.setdefault(id(u), (u, set()))[1].add(where[id(p)])
+        if not keys_of:  # no forward ran before the first step: fall back to eager waits
+            self._calls = None
+            return False
+        order, seen = [], set()
+        for m in self._calls:
+            ent = keys_of.get(id(m))
+            if ent is None:
+                continue
+            for k in sorted(ent[1]):
+                if k not in seen:
+                    seen.add(k)
+                    order.append(k)
+        for gi, g in enumerate(self.groups):
+            for bi in range(len(g.buckets)):
+                if (gi, bi) not in seen:
+                    order.append((gi, bi))
+        for u, ks in keys_of.values():
+            u._piamd_ag_keys = sorted(ks)
+            u.register_forward_pre_hook(self._pre_forward_wait)
+        self._need_order = order
+        self._calls = None
+        return True
+
+    def _pre_forward_wait(self, module, args):
+        if self._ag_pending:
+            for k in module._piamd_ag_keys:
+                h = self._ag_pending.pop(k, None)
+                if h is not None:
+                    h.wait()
 
     # ---------------------------------------------------------------------------------
     def _gather_shard(self, g, src_flat, out):
@@ -215,6 +290,8 @@ class FlatTrainer:
         for h in self._ag_handles:
             h.wait()
         self._ag_handles = []
+        # parameter all-gathers stay in flight (waited per module in forward); zeroing the grad
+        # buffer does not touch the parameter buffer they write
         for g in self.groups:
             g.gflat.zero_()
             for b in g.buckets:
@@ -297,22 +374,41 @@ class FlatTrainer:
             if fp32_copy:
                 fp32_target.copy_(g.master)
         if self.sharding:
+            overlapped = self.overlap and getattr(self, "_calls", None) is not None or \
+                getattr(self, "_need_order", None) is not None
+            if overlapped and self._need_order is None:
+                overlapped = self._finalize_forward_waits()
+            offs = []
             for g in self.groups:
-                o = 0
+                o, lst = 0, []
                 for b in g.buckets:
-                    L = (b.end - b.start) // self.world
-                    h = dist.all_gather_into_tensor(g.flat[b.start:b.end], g.pshard[o:o + L],
-                                                    group=self.dp_group, async_op=True)
+                    lst.append(o)
+                    o += (b.end - b.start) // self.world
+                offs.append(lst)
+            order = self._need_order if overlapped else \
+                [(gi, bi) for gi, g in enumerate(self.groups) for bi in range(len(g.buckets))]
+            for gi, bi in order:
+                g, b = self.groups[gi], self.groups[gi].buckets[bi]
+                L = (b.end - b.start) // self.world
+                h = dist.all_gather_into_tensor(g.flat[b.start:b.end],
+                                                g.pshard[offs[gi][bi]:offs[gi][bi] + L],
+                                                group=self.dp_group, async_op=True)
+                if overlapped:
+                    self._ag_pending[(gi, bi)] = h
+                else:
                     self._ag_handles.append(h)
-                    o += L
 
     def wait_params(self):
         for h in self._ag_handles:
             h.wait()
         self._ag_handles = []
+        for h in self._ag_pending.values():
+            h.wait()
+        self._ag_pending = {}
 
     # ---------------------------------------------------------------------------------
     def state_dict(self):
+        self.wait_params()
         out = {"step": self.step_count}
         for g in self.groups:
             out[g.name] = {"master": g.master, "m": g.m, "v": g.v}

@@ -37,7 +37,7 @@ def _single(steps=2):
     return init, {k: v.clone() for k, v in m.state_dict().items()}, losses
 
 
-def _dp_worker(rank, world, init, sharding):
+def _dp_worker(rank, world, init, sharding, eager_wait=True, steps=2):
     import torch.distributed as dist
     from paddle_infer_amd.models.gpt import GPTForPretraining
     from paddle_infer_amd.parallel.flat_engine import FlatTrainer
@@ -46,28 +46,30 @@ def _dp_worker(rank, world, init, sharding):
     tr = FlatTrainer(m, lr=1e-2, weight_decay=0.1, grad_clip=1.0, dp_group=dist.group.WORLD,
                      sharding_stage=sharding, bucket_mb=0.01)
     losses = []
-    for ids in _data():
+    for ids in _data(steps):
         local = ids.chunk(world, 0)[rank]
         tr.zero_grad()
         loss = m(local[:, :-1], labels=local[:, 1:])
         loss.backward()
         tr.step()
-        tr.wait_params()
+        if eager_wait:  # else: the next forward's module pre-hooks wait per bucket
+            tr.wait_params()
         t = loss.detach().clone()
         dist.all_reduce(t)
         losses.append(t.item() / world)
+    tr.wait_params()
     return {k: v.clone() for k, v in m.state_dict().items()}, losses
 
 
-@pytest.mark.parametrize("sharding", [0, 1])
-def test_data_parallel_matches_single(sharding):
-    init, ref_sd, ref_losses = _single()
-    res = run_distributed(_dp_worker, 2, init, sharding)
+@pytest.mark.parametrize("sharding,eager_wait", [(0, True), (1, True), (1, False)])
+def test_data_parallel_matches_single(sharding, eager_wait):
+    init, ref_sd, ref_losses = _single(3)
+    res = run_distributed(_dp_worker, 2, init, sharding, eager_wait, 3)
     for r in range(2):
         sd, losses = res[r]
         assert losses == pytest.approx(ref_losses, rel=1e-4, abs=1e-5)
         for k in ref_sd:
-            torch.testing.assert_close(sd[k], ref_sd[k], rtol=2e-4, atol=2e-5)
+            torch.testing.assert_close(sd[k], ref_sd[k], rtol=2e-4, atol=1e-4)
 
 
 def _tp_worker(rank, world, init):

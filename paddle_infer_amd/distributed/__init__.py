@@ -29,3 +29,5 @@ def gloo_barrier():
 
 def gloo_release():
     destroy_process_group()
+from . import checkpoint  # noqa: F401,E402
+from .checkpoint import save_state_dict, load_state_dict  # noqa: F401,E402

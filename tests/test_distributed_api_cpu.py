@@ -205,3 +205,46 @@ def test_launch_watchdog_kills_job_on_failure(tmp_path):
     assert r.returncode == 3
     assert _t.time() - t0 < 30
     assert (tmp_path / "log" / "workerlog.0").exists()
+
+
+def _ckpt_worker(rank, world, path, phase):
+    import torch
+    import torch.distributed as dist
+    from paddle_infer_amd.distributed import checkpoint as ck
+    from paddle_infer_amd.models.gpt import GPTForPretraining, gpt_config
+    from paddle_infer_amd.parallel.flat_engine import FlatTrainer
+    torch.manual_seed(0)
+    cfg = gpt_config("gpt3-tiny", dtype="float32", hidden_dropout_prob=0.0, num_layers=1)
+    m = GPTForPretraining(cfg)
+    tr = FlatTrainer(m, lr=1e-2, dp_group=dist.group.WORLD, sharding_stage=1, bucket_mb=0.05)
+    if phase == "save":
+        ids = torch.randint(0, cfg.vocab_size, (2, 17), generator=torch.Generator().manual_seed(rank))
+        tr.zero_grad()
+        m(ids[:, :-1], labels=ids[:, 1:]).backward()
+        tr.step()
+        tr.wait_params()
+        ck.save_state_dict(ck.flat_trainer_state(tr, m), path)
+        full = {g.name: g.master.clone() for g in tr.groups}
+        return {"step": tr.step_count, "params": {k: v.clone() for k, v in m.state_dict().items()},
+                "shards": {k: v.numpy() for k, v in full.items()}}
+    st = ck.flat_trainer_state(tr, m)
+    extra = ck.load_state_dict(st, path)
+    return {"step": extra.get("opt.step"), "params": {k: v.clone() for k, v in m.state_dict().items()},
+            "shards": {g.name: g.master.numpy().copy() for g in tr.groups}}
+
+
+def test_distributed_checkpoint_reshards(tmp_path):
+    """Save with world 2 (ZeRO-1 shards), load with world 1 and world 2: params identical, and the
+    world-1 master equals the concatenation (per bucket) of the world-2 shards."""
+    path = str(tmp_path / "ckpt")
+    saved = run_distributed(_ckpt_worker, 2, path, "save")
+    loaded2 = run_distributed(_ckpt_worker, 2, path, "load")
+    loaded1 = _ckpt_worker(0, 1, path, "load")
+    for r in range(2):
+        for k, v in saved[0]["params"].items():
+            torch.testing.assert_close(loaded2[r]["params"][k], v)
+        for name, arr in saved[r]["shards"].items():
+            np.testing.assert_allclose(loaded2[r]["shards"][name], arr)
+    for k, v in saved[0]["params"].items():
+        torch.testing.assert_close(loaded1["params"][k], v)
+    assert loaded1["step"] == 1

@@ -309,3 +309,6 @@ class _GeneratorLoader:
         for b in self._gen():
             yield [torch.as_tensor(np.asarray(x)) if not isinstance(x, torch.Tensor) else x for x in b] \
                 if isinstance(b, (list, tuple)) else b
+
+
+from .token_loader import TokenDataLoader, write_token_file  # noqa: E402,F401

@@ -129,6 +129,21 @@ def load_state_dict(state_dict, path, process_group=None):
     return meta.get("extra", {})
 
 
+def axis_shard(local, global_shape, axis, rank, world):
+    """Shard of a tensor split evenly along ``axis`` (tensor-parallel column / row slices, vocab
+    shards). The local slice is rank ``rank``'s chunk; regions are the contiguous runs it occupies
+    in the flattened global tensor (one per index of the leading dims)."""
+    gs = list(global_shape)
+    axis = axis % len(gs)
+    assert gs[axis] % world == 0, "axis must divide evenly"
+    chunk = gs[axis] // world
+    inner = int(np.prod(gs[axis + 1:])) if axis + 1 < len(gs) else 1
+    outer = int(np.prod(gs[:axis])) if axis else 1
+    run = chunk * inner
+    regions = [(o * gs[axis] * inner + rank * run, run) for o in range(outer)]
+    return Shard(local.contiguous().reshape(-1), gs, regions)
+
+
 # ------------------------------------------------------------------------------ engine helpers
 def flat_trainer_state(trainer, model=None, prefix="opt"):
     """Per-PARAMETER shards of a FlatTrainer's fp32 master / moments plus the (replicated) model

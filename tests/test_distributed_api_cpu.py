@@ -248,3 +248,37 @@ def test_distributed_checkpoint_reshards(tmp_path):
     for k, v in saved[0]["params"].items():
         torch.testing.assert_close(loaded1["params"][k], v)
     assert loaded1["step"] == 1
+
+
+def _tp_ckpt_worker(rank, world, path, phase):
+    import torch.distributed as dist  # noqa: F401
+    from paddle_infer_amd.distributed import checkpoint as ck
+    g = torch.arange(6 * 8 * 4, dtype=torch.float32).reshape(6, 8, 4)
+    if phase == "save":  # TP=2: column split on axis 1, row split on axis 0
+        col = g.chunk(world, dim=1)[rank]
+        row = g.chunk(world, dim=0)[rank]
+        ck.save_state_dict({"col": ck.axis_shard(col, g.shape, 1, rank, world),
+                            "row": ck.axis_shard(row, g.shape, 0, rank, world), "step": 5}, path)
+        return {}
+    return {}
+
+
+def test_checkpoint_tensor_parallel_reshard(tmp_path):
+    """Save TP=2 column/row shards from 2 ranks; load as full tensors (world 1) and as TP=4 /
+    other-axis shards."""
+    from paddle_infer_amd.distributed import checkpoint as ck
+    path = str(tmp_path / "tp")
+    run_distributed(_tp_ckpt_worker, 2, path, "save")
+    g = torch.arange(6 * 8 * 4, dtype=torch.float32).reshape(6, 8, 4)
+    full_col, full_row = torch.zeros_like(g), torch.zeros_like(g)
+    extra = ck.load_state_dict({"col": full_col, "row": full_row}, path)
+    assert extra["step"] == 5
+    torch.testing.assert_close(full_col, g)
+    torch.testing.assert_close(full_row, g)
+    for r in range(4):  # TP=4 along axis 1 from the axis-1 TP=2 checkpoint, axis 2 from axis 0
+        a = torch.zeros(6, 2, 4)
+        b = torch.zeros(6, 8, 1)
+        sa, sb = ck.axis_shard(a, g.shape, 1, r, 4), ck.axis_shard(b, g.shape, 2, r, 4)
+        ck.load_state_dict({"col": sa, "row": sb}, path)
+        torch.testing.assert_close(sa.local.view(6, 2, 4), g.chunk(4, dim=1)[r])
+        torch.testing.assert_close(sb.local.view(6, 8, 1), g.chunk(4, dim=2)[r])

@@ -352,3 +352,44 @@ PIAMD_EXPORT int piamd_dropout(const void* x, void* y, long long n, float p, uin
                      (bf16_t*)y, n / 8, p, seed, offset);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// 2-D bf16 transpose dst[C][R] = src[R][C] (weight re-layout for the K-contiguous forward GEMM).
+// 64x64 tile per 256-thread block: 16-B coalesced row loads → LDS (row stride 66 elements = 33
+// dwords, so the column gather of the store phase spreads over distinct banks) → 16-B coalesced
+// stores of the transposed rows. Requires R % 8 == 0 and C % 8 == 0 (tails masked per 8-group).
+__global__ void __launch_bounds__(256) transpose_bf16_kernel(const bf16_t* __restrict__ src,
+                                                             bf16_t* __restrict__ dst, int R,
+                                                             int C) {
+  __shared__ bf16_t tile[64][66];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64, t = threadIdx.x;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int idx = it * 256 + t, row = idx >> 3, cg = idx & 7;
+    const int r = r0 + row, c = c0 + cg * 8;
+    u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (r < R && c < C) v = *(const u16x8*)(src + (size_t)r * C + c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tile[row][cg * 8 + j] = v[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int idx = it * 256 + t, orow = idx >> 3, og = idx & 7;
+    const int oc = c0 + orow, orr = r0 + og * 8;  // dst row = source column, dst cols = source rows
+    u16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = tile[og * 8 + j][orow];
+    if (oc < C && orr < R) *(u16x8*)(dst + (size_t)oc * R + orr) = v;
+  }
+}
+
+PIAMD_EXPORT int piamd_transpose_bf16(const void* src, void* dst, int R, int C,
+                                      hipStream_t stream) {
+  if (R == 0 || C == 0) return 0;
+  if (R % 8 || C % 8) return (int)hipErrorInvalidValue;
+  dim3 grid((C + 63) / 64, (R + 63) / 64);
+  hipLaunchKernelGGL(transpose_bf16_kernel, grid, dim3(256), 0, stream, (const bf16_t*)src,
+                     (bf16_t*)dst, R, C);
+  return (int)hipGetLastError();
+}

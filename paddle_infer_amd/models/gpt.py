@@ -28,6 +28,7 @@ import torch.nn.functional as F
 from ..nn.layer.base import Layer, LayerList
 from ..nn import initializer as I
 from ..ops import fused_add_layer_norm, flash_attention_packed, bias_act, softmax_cross_entropy
+from ..ops.linear import _use_transposed, transposed
 from ..ops.linear import linear as _linear
 from ..distributed.fleet.mp_layers import (ColumnParallelLinear, RowParallelLinear,
                                            VocabParallelEmbedding, c_identity)
@@ -204,7 +205,9 @@ class _LMHeadFn(torch.autograd.Function):
     def backward(ctx, dl):
         y2, w = ctx.saved_tensors
         dl2 = dl.reshape(-1, w.shape[0])
-        dy = torch.mm(dl2, w).view(ctx.shp)
+        # dgrad on the [h, V] copy: both operands V-contiguous (hipBLASLt's fast layout, ops/linear.py)
+        wk = transposed(w).t() if _use_transposed(dl2, w) else w
+        dy = torch.mm(dl2, wk).view(ctx.shp)
         mg = getattr(w, "main_grad", None)
         if mg is not None:
             mg.addmm_(dl2.t(), y2)

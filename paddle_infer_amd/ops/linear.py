@@ -9,6 +9,13 @@ When a weight carries a ``main_grad`` buffer (a view into the framework's flat g
 the backward accumulates ``xᵀ·dy`` straight into it with ``addmm_`` (β = 1) — the weight gradient is
 never materialised as a separate tensor, and the parameter's ``_grad_ready`` hook (the bucketed
 reduce-scatter/all-reduce trigger) fires right after.
+
+Weight layout for the forward GEMM: on gfx950 hipBLASLt is 12-21 % faster when BOTH operands are
+contiguous along the reduction dim (`x @ Wtᵀ` with ``Wt = [out, in]``) than on Paddle's ``x @ W``
+(measured on every GPT-1.3B shape, `tools/bench_gemm_layouts.py`, `profiles/gemm_layouts_r1.txt`),
+while the input-gradient GEMM ``dy @ Wᵀ`` is fastest on the ``[in, out]`` layout. Training therefore
+keeps a bf16 ``[out, in]`` copy of each weight (`transposed`, one LDS-tiled HIP transpose per weight
+per optimizer step, refreshed lazily on first use after the weights change) for the forward only.
 """
 from __future__ import annotations
 
@@ -21,15 +28,48 @@ def _fire(p):
         hook(p)
 
 
+_PARAM_EPOCH = [0]
+TRANSPOSED_MIN_ROWS = 1024  # below this the GEMM is too small for the layout to matter
+
+
+def bump_param_epoch():
+    """Called by optimizers that write parameters outside autograd's version counter (the flat
+    AdamW kernels): invalidates every cached transposed weight."""
+    _PARAM_EPOCH[0] += 1
+
+
+def transposed(w):
+    """Cached contiguous ``wᵀ`` (bf16 2-D CUDA weights), refreshed when the parameter changed."""
+    key = (_PARAM_EPOCH[0], w._version)
+    c = getattr(w, "_piamd_t", None)
+    if c is not None and c[0] == key:
+        return c[1]
+    R, C = w.shape
+    buf = c[1] if c is not None else torch.empty((C, R), dtype=w.dtype, device=w.device)
+    if R % 8 == 0 and C % 8 == 0:
+        from . import _lib
+        _lib.call("piamd_transpose_bf16", w.data_ptr(), buf.data_ptr(), R, C, _lib.stream())
+    else:
+        buf.copy_(w.detach().t())
+    w._piamd_t = (key, buf)
+    return buf
+
+
+def _use_transposed(x2, w):
+    return (x2.is_cuda and w.dim() == 2 and w.dtype == torch.bfloat16 and x2.dtype == w.dtype
+            and x2.shape[0] >= TRANSPOSED_MIN_ROWS and w.is_contiguous())
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
+        wf = transposed(w).t() if _use_transposed(x2, w) else w
         if b is not None:
-            y = torch.addmm(b, x2, w)
+            y = torch.addmm(b, x2, wf)
         else:
-            y = torch.mm(x2, w)
+            y = torch.mm(x2, wf)
         ctx.save_for_backward(x2, w)
         ctx.has_b = b is not None
         ctx.bias = b

@@ -30,6 +30,7 @@ from dataclasses import dataclass
 import torch
 import torch.distributed as dist
 
+from ..ops.linear import bump_param_epoch
 from ..ops.optim import adamw_flat, momentum_flat, sumsq
 
 ALIGN = 64  # elements (128 B of bf16)
@@ -373,6 +374,7 @@ class FlatTrainer:
                               model=model_out, grad_scale=gscale)
             if fp32_copy:
                 fp32_target.copy_(g.master)
+        bump_param_epoch()  # the kernels above wrote the bf16 weights behind autograd's back
         if self.sharding:
             overlapped = self.overlap and getattr(self, "_calls", None) is not None or \
                 getattr(self, "_need_order", None) is not None

@@ -50,3 +50,38 @@ def test_gemm_epilogues():
     base = acc.clone()
     gemm(x, dy.new_empty(0) if False else y.new_tensor(y), trans_a=True, out=acc, accumulate=True)
     _close(acc, base + x.float().t() @ y.float(), 0.1)
+
+
+@pytest.mark.parametrize("R,C", [(2048, 6144), (200, 72), (64, 8)])
+def test_transpose_bf16(R, C):
+    from paddle_infer_amd.ops import _lib
+    w = torch.randn(R, C, device=DEV).bfloat16()
+    out = torch.empty(C, R, device=DEV, dtype=torch.bfloat16)
+    _lib.call("piamd_transpose_bf16", w.data_ptr(), out.data_ptr(), R, C, _lib.stream())
+    assert torch.equal(out, w.t())
+
+
+def test_linear_transposed_weight_cache():
+    """Forward via the cached [out,in] copy == x @ W; the copy refreshes after in-place updates and
+    after a flat-optimizer step (kernel writes do not bump autograd's version counter)."""
+    from paddle_infer_amd.ops import linear as L
+    x = torch.randn(2048, 256, device=DEV).bfloat16().requires_grad_()
+    w = (0.05 * torch.randn(256, 512, device=DEV)).bfloat16().requires_grad_()
+    b = torch.zeros(512, device=DEV).bfloat16().requires_grad_()
+    y = L.linear(x, w, b)
+    _close(y, x.float() @ w.float(), 0.02)
+    y.float().sum().backward()
+    _close(x.grad, torch.ones(2048, 512, device=DEV) @ w.float().t(), 0.5)
+    with torch.no_grad():
+        w.mul_(2.0)  # autograd-visible change
+    _close(L.linear(x, w, b), x.float() @ w.float(), 0.04)
+    with torch.no_grad():  # change behind autograd's back, then the epoch bump
+        ptr = w.data_ptr()
+        torch.empty_like(w).copy_(w * 0.5)
+        w.data = w.data  # noqa
+        torch.cuda.synchronize()
+        tmp = (w.float() * 0.5).bfloat16()
+        from paddle_infer_amd.ops import _lib
+        _lib.call("piamd_transpose_bf16", tmp.t().contiguous().data_ptr(), ptr, 512, 256, _lib.stream())
+    L.bump_param_epoch()
+    _close(L.linear(x, w, b), x.float() @ tmp.float(), 0.02)

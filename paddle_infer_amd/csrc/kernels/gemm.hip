@@ -98,43 +98,34 @@ __device__ __forceinline__ float act_grad(float h, int act) {
 // Epilogue kinds
 enum { EPI_STORE = 0, EPI_BIAS_ACT = 1, EPI_DACT = 2 };
 
-// A_KC: A[m][k] at a + m*lda + k (else A[m][k] at a + k*lda + m)
-// B_KC: B[k][n] at b + n*ldb + k (else B[k][n] at b + k*ldb + n)
+// Main loop: acc = A[m0:m0+256, kbase:kbase+64·nk] · B[kbase:…, n0:n0+256].
+// A_KC: A[m][k] at a + m*lda + k (rows clamped to amax) — else A[m][k] at a + k*lda + m.
+// B_KC: B[k][n] at b + n*ldb + k (rows clamped to bmax) — else B[k][n] at b + k*ldb + n.
 template <bool A_KC, bool B_KC>
-__global__ __launch_bounds__(NTHR, 1) void gemm_kernel(
-    const bf16_t* __restrict__ a, long long lda, const bf16_t* __restrict__ b, long long ldb,
-    void* __restrict__ c, long long ldc, int c_f32, int accumulate, int M, int N, int K, int epi,
-    int act, const bf16_t* __restrict__ bias, bf16_t* __restrict__ aux, long long ldaux) {
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE_BYTES];
+__device__ __forceinline__ void gemm_mainloop(const bf16_t* __restrict__ a, long long lda, int amax,
+                                              const bf16_t* __restrict__ b, long long ldb, int bmax,
+                                              int m0, int n0, long long kbase, int nk, char* smem,
+                                              f32x16 (&acc)[4][2]) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = w >> 2, wc = w & 3;  // 2 (M) x 4 (N) waves
-
-  // ---- bijective XCD-aware tile order (guide T1) ----
-  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN, nwg = tm * tn;
-  const int orig = blockIdx.x, xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
-  const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
-  const int bm = wg / tn, bn = wg % tn;   // consecutive wg on one XCD walk N: A panel reused
-  const int m0 = bm * BM, n0 = bn * BN;
-
-  f32x16 acc[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  if (nk <= 0) return;
 
   auto stage_load = [&](int kt, int s) {
     char* ai = smem + s * STAGE_BYTES;
     char* bi = ai + TILE_BYTES;
-    const int k0 = kt * BK;
-    if (A_KC) dma_tile<256, 128>(a + k0, lda, m0, M - 1, ai, w, lane);         // [256 m][64 k]
-    else      dma_tile<64, 512>(a + (long long)k0 * lda + m0, lda, 0, 63, ai, w, lane);  // [64 k][256 m]
-    if (B_KC) dma_tile<256, 128>(b + k0, ldb, n0, N - 1, bi, w, lane);         // [256 n][64 k]
-    else      dma_tile<64, 512>(b + (long long)k0 * ldb + n0, ldb, 0, 63, bi, w, lane);  // [64 k][256 n]
+    const long long k0 = kbase + (long long)kt * BK;
+    if (A_KC) dma_tile<256, 128>(a + k0, lda, m0, amax, ai, w, lane);         // [256 m][64 k]
+    else      dma_tile<64, 512>(a + k0 * lda + m0, lda, 0, 63, ai, w, lane);  // [64 k][256 m]
+    if (B_KC) dma_tile<256, 128>(b + k0, ldb, n0, bmax, bi, w, lane);         // [256 n][64 k]
+    else      dma_tile<64, 512>(b + k0 * ldb + n0, ldb, 0, 63, bi, w, lane);  // [64 k][256 n]
   };
 
-  const int nk = K / BK;
   stage_load(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -173,12 +164,21 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+}
 
-  // ---- epilogue: lane owns row m0+wr*128+mb*32+l31; columns n = ncol + 8g + 4*hi + (0..3) ----
+// Epilogue: lane owns row m0+wr*128+mb*32+l31 (stored while < mend); columns
+// n = n0 + wc*64 + nb*32 + 8g + 4*hi + (0..3) (stored while < N).
+__device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[4][2], void* __restrict__ c,
+                                              long long ldc, int c_f32, int accumulate, int m0,
+                                              int mend, int n0, int N, int epi, int act,
+                                              const bf16_t* __restrict__ bias,
+                                              bf16_t* __restrict__ aux, long long ldaux) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 2, wc = w & 3;
+  const int hi = lane >> 5, l31 = lane & 31;
 #pragma unroll
   for (int mb = 0; mb < 4; ++mb) {
     const int m = m0 + wr * 128 + mb * 32 + l31;
-    if (m >= M) continue;
+    if (m >= mend) continue;
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) {
 #pragma unroll
@@ -226,6 +226,88 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_kernel(
   }
 }
 
+// bijective XCD-aware tile order (guide T1): consecutive tiles of one XCD share an A row-panel
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
+  return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
+}
+
+template <bool A_KC, bool B_KC>
+__global__ __launch_bounds__(NTHR, 1) void gemm_kernel(
+    const bf16_t* __restrict__ a, long long lda, const bf16_t* __restrict__ b, long long ldb,
+    void* __restrict__ c, long long ldc, int c_f32, int accumulate, int M, int N, int K, int epi,
+    int act, const bf16_t* __restrict__ bias, bf16_t* __restrict__ aux, long long ldaux) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE_BYTES];
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  const int wg = xcd_remap(blockIdx.x, tm * tn);
+  const int m0 = (wg / tn) * BM, n0 = (wg % tn) * BN;  // consecutive wg on one XCD walk N
+  f32x16 acc[4][2];
+  gemm_mainloop<A_KC, B_KC>(a, lda, M - 1, b, ldb, N - 1, m0, n0, 0, K / BK, smem, acc);
+  gemm_epilogue(acc, c, ldc, c_f32, accumulate, m0, M, n0, N, epi, act, bias, aux, ldaux);
+}
+
+// ---- grouped (MoE expert) GEMMs over expert-sorted rows --------------------------------------
+// Parity: reference `fluid/operators/fused/moe_expert_gemm.h` / `fused_moe_op.cu` (CUTLASS grouped
+// GEMM over per-expert row ranges). Rows of expert e occupy [offs[e], offs[e+1]) of the sorted
+// activation matrix; the offsets live on the device, so routing never synchronises with the host
+// and the launch is hipGraph-capturable. The grid is sized for the worst case
+// (ceil(rows_cap/256) + E row tiles × N tiles); every workgroup finds its expert by scanning the
+// per-expert tile counts (wave-uniform scalar loads), surplus workgroups exit at once.
+__device__ __forceinline__ bool moe_find_tile(const int* __restrict__ offs, int E, int t, int& e,
+                                              int& r0, int& r1) {
+  int acc = 0;
+  for (int i = 0; i < E; ++i) {
+    const int b0 = offs[i], b1 = offs[i + 1];
+    const int nt = (b1 - b0 + BM - 1) / BM;
+    if (t < acc + nt) {
+      e = i;
+      r0 = b0 + (t - acc) * BM;
+      r1 = b1;
+      return true;
+    }
+    acc += nt;
+  }
+  return false;
+}
+
+// Y[rows] = X[rows] · W_e (+ bias_e, act): B_KC=false → W_e stored [K][N] (w + e*sw);
+// B_KC=true → W_e stored [N][K] (also the data-gradient dX = dY · W_eᵀ of a [K_in][N] weight).
+template <bool B_KC>
+__global__ __launch_bounds__(NTHR, 1) void moe_gemm_kernel(
+    const bf16_t* __restrict__ x, long long ldx, const bf16_t* __restrict__ w, long long ldw,
+    long long sw, const int* __restrict__ offs, int E, void* __restrict__ y, long long ldy,
+    int y_f32, int N, int K, int tm_max, int epi, int act, const bf16_t* __restrict__ bias,
+    bf16_t* __restrict__ aux, long long ldaux) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE_BYTES];
+  const int tn = (N + BN - 1) / BN;
+  const int wg = xcd_remap(blockIdx.x, tm_max * tn);
+  int e, r0, r1;
+  if (!moe_find_tile(offs, E, wg / tn, e, r0, r1)) return;
+  const int n0 = (wg % tn) * BN;
+  f32x16 acc[4][2];
+  gemm_mainloop<true, B_KC>(x, ldx, r1 - 1, w + e * sw, ldw, N - 1, r0, n0, 0, K / BK, smem, acc);
+  gemm_epilogue(acc, y, ldy, y_f32, 0, r0, r1, n0, N, epi, act,
+                bias ? bias + (long long)e * N : nullptr, aux, ldaux);
+}
+
+// Weight gradient per expert: dW_e[M=K_in][N] (+)= X_eᵀ · dY_e, reduced over the expert's rows.
+// Segments must be padded to multiples of 64 rows with ZERO rows (moe_permute(align=64)).
+__global__ __launch_bounds__(NTHR, 1) void moe_wgrad_kernel(
+    const bf16_t* __restrict__ x, long long ldx, const bf16_t* __restrict__ dy, long long lddy,
+    const int* __restrict__ offs, int E, void* __restrict__ dw, long long sdw, int dw_f32,
+    int accumulate, int M, int N) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE_BYTES];
+  const int tn = N / BN, per = (M / BM) * tn;
+  const int wg = xcd_remap(blockIdx.x, per * E);
+  const int e = wg / per, t = wg % per, m0 = (t / tn) * BM, n0 = (t % tn) * BN;
+  const int r0 = offs[e], r1 = offs[e + 1];
+  if (r1 == r0 && accumulate) return;  // empty expert: nothing to add
+  f32x16 acc[4][2];
+  gemm_mainloop<false, false>(x, ldx, 0, dy, lddy, 0, m0, n0, r0, (r1 - r0) / BK, smem, acc);
+  void* out = dw_f32 ? (void*)((float*)dw + e * sdw) : (void*)((bf16_t*)dw + e * sdw);
+  gemm_epilogue(acc, out, N, dw_f32, accumulate, m0, M, n0, N, EPI_STORE, 0, nullptr, nullptr, 0);
+}
+
 }  // namespace
 
 // trans_a: A given as [K][M] (lda ≥ M); else [M][K] (lda ≥ K).
@@ -251,5 +333,40 @@ PIAMD_EXPORT int piamd_gemm(const void* a, long long lda, int trans_a, const voi
   else if (trans_a && !trans_b) GEMM_LAUNCH(false, false);
   else GEMM_LAUNCH(false, true);
 #undef GEMM_LAUNCH
+  return (int)hipGetLastError();
+}
+
+// Grouped expert GEMM. x [rows][K] expert-sorted (offs[E+1] int32 on device, rows ≤ rows_cap);
+// w: trans_w=0 → [E][K][N] (N % 256 == 0), trans_w=1 → [E][N][K]; per-expert stride sw elements.
+// y [rows][N] bf16 (or f32 when y_f32); epi/act/aux as piamd_gemm, bias [E][N] (may be null).
+PIAMD_EXPORT int piamd_moe_gemm(const void* x, long long ldx, const void* w, long long ldw,
+                                long long sw, int trans_w, const int* offs, int E, int rows_cap,
+                                void* y, long long ldy, int y_f32, int N, int K, int epi, int act,
+                                const void* bias, void* aux, long long ldaux, hipStream_t st) {
+  if (K % BK || N % 4 || (!trans_w && N % BN) || E < 1 || rows_cap < 0 ||
+      (epi == EPI_DACT && !aux))
+    return (int)hipErrorInvalidValue;
+  const int tm_max = (rows_cap + BM - 1) / BM + E, tn = (N + BN - 1) / BN;
+  dim3 grid(tm_max * tn), block(NTHR);
+  if (trans_w)
+    hipLaunchKernelGGL(moe_gemm_kernel<true>, grid, block, 0, st, (const bf16_t*)x, ldx,
+                       (const bf16_t*)w, ldw, sw, offs, E, y, ldy, y_f32, N, K, tm_max, epi, act,
+                       (const bf16_t*)bias, (bf16_t*)aux, ldaux);
+  else
+    hipLaunchKernelGGL(moe_gemm_kernel<false>, grid, block, 0, st, (const bf16_t*)x, ldx,
+                       (const bf16_t*)w, ldw, sw, offs, E, y, ldy, y_f32, N, K, tm_max, epi, act,
+                       (const bf16_t*)bias, (bf16_t*)aux, ldaux);
+  return (int)hipGetLastError();
+}
+
+// dW_e [M][N] (+)= X_eᵀ · dY_e for every expert; x [rows][M], dy [rows][N], expert segments
+// 64-row aligned and zero padded; M, N multiples of 256; dw per-expert stride sdw elements.
+PIAMD_EXPORT int piamd_moe_wgrad(const void* x, long long ldx, const void* dy, long long lddy,
+                                 const int* offs, int E, void* dw, long long sdw, int dw_f32,
+                                 int accumulate, int M, int N, hipStream_t st) {
+  if (M % BM || N % BN || E < 1) return (int)hipErrorInvalidValue;
+  dim3 grid(E * (M / BM) * (N / BN)), block(NTHR);
+  hipLaunchKernelGGL(moe_wgrad_kernel, grid, block, 0, st, (const bf16_t*)x, ldx,
+                     (const bf16_t*)dy, lddy, offs, E, dw, sdw, dw_f32, accumulate, M, N);
   return (int)hipGetLastError();
 }

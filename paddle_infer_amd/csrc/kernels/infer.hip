@@ -451,15 +451,34 @@ template <int BITS>
 __global__ __launch_bounds__(256) void wo_gemm_kernel(
     const bf16_t* __restrict__ x, long long ldx, const unsigned char* __restrict__ wp,
     const float* __restrict__ scale, const bf16_t* __restrict__ bias, bf16_t* __restrict__ y,
-    long long ldy, float* __restrict__ ws, int* __restrict__ cnt, int M, int N, int K, int act) {
+    long long ldy, float* __restrict__ ws, int* __restrict__ cnt, int M, int N, int K, int act,
+    const int* __restrict__ offs, int E, long long wstride) {
   constexpr int KB = BITS == 16 ? 16 : (BITS == 8 ? 32 : 64);  // k per block (16 B lane load)
   constexpr int NMF = KB / 16;               // MFMAs per block
   __shared__ float red[3][16][64];
-  const int nt = blockIdx.x, mt = blockIdx.y, kz = blockIdx.z, KS = gridDim.z;
+  const int nt = blockIdx.x, kz = blockIdx.z, KS = gridDim.z;
+  int mt = blockIdx.y, mbase = 0;
+  if (offs) {
+    // grouped (MoE experts): global 32-row tile → (expert, tile); rows [offs[e], offs[e+1])
+    int acc_t = 0, e = -1;
+    for (int i = 0; i < E; ++i) {
+      const int nt_e = (offs[i + 1] - offs[i] + 31) / 32;
+      if (mt < acc_t + nt_e) { e = i; break; }
+      acc_t += nt_e;
+    }
+    if (e < 0) return;  // surplus tile of the worst-case grid
+    mbase = offs[e] + (mt - acc_t) * 32;
+    M = offs[e + 1];
+    mt = 0;
+    wp += e * wstride;
+    if (scale) scale += (long long)e * N;
+    if (bias) bias += (long long)e * N;
+  }
+  mbase += mt * 32;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nkb = K / KB;
   const int kb_beg = (int)((long long)nkb * kz / KS), kb_end = (int)((long long)nkb * (kz + 1) / KS);
-  const int m = min(mt * 32 + (lane & 31), M - 1);  // rows ≥ M compute duplicates, never stored
+  const int m = min(mbase + (lane & 31), M - 1);  // rows ≥ M compute duplicates, never stored
   const bf16_t* xr = x + (long long)m * ldx + (KB / 2) * (lane >> 5);
   const uint4* wt = (const uint4*)wp + (long long)nt * nkb * 64 + lane;
 
@@ -510,7 +529,7 @@ __global__ __launch_bounds__(256) void wo_gemm_kernel(
   if (KS == 1) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int mm = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int mm = mbase + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
       if (mm < M) y[(long long)mm * ldy + n] = f2bf(act_apply(acc[r] * sc + bs, act));
     }
     return;
@@ -521,7 +540,7 @@ __global__ __launch_bounds__(256) void wo_gemm_kernel(
   if (cnt == nullptr) {  // slice mode (larger M): plain partial slices + wo_finalize_kernel
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int mm = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int mm = mbase + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
       if (mm < M) ws[((long long)kz * M + mm) * N + n] = acc[r];
     }
     return;
@@ -529,7 +548,7 @@ __global__ __launch_bounds__(256) void wo_gemm_kernel(
   float sink = 0.f;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    const int mm = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    const int mm = mbase + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
     if (mm < M) sink += xcd_add(ws + (long long)mm * N + n, acc[r]);
   }
   xcd_drain(sink);
@@ -539,7 +558,7 @@ __global__ __launch_bounds__(256) void wo_gemm_kernel(
   if (!last) return;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    const int mm = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    const int mm = mbase + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
     if (mm < M) {
       const float v = xcd_take(ws + (long long)mm * N + n);
       y[(long long)mm * ldy + n] = f2bf(act_apply(v * sc + bs, act));
@@ -567,6 +586,20 @@ __global__ void wo_finalize_kernel(const float* __restrict__ ws, int KS, const f
 // launch (cheaper than memory-side atomics once M is large).
 // Requires N % 32 == 0 and K % KB == 0 (KB = 16 / 32 / 64 for bits = 16 / 8 / 4).
 // bits = 16: packed bf16 weights, scale may be null.
+static void wo_launch(int bits, dim3 grid, hipStream_t st, const void* x, long long ldx,
+                      const void* wp, const float* scale, const void* bias, void* y, long long ldy,
+                      float* ws, int* cnt, int M, int N, int K, int act, const int* offs, int E,
+                      long long wstride) {
+#define WO_LAUNCH(B)                                                                              \
+  hipLaunchKernelGGL(wo_gemm_kernel<B>, grid, dim3(256), 0, st, (const bf16_t*)x, ldx,           \
+                     (const unsigned char*)wp, scale, (const bf16_t*)bias, (bf16_t*)y, ldy, ws,   \
+                     cnt, M, N, K, act, offs, E, wstride)
+  if (bits == 16) WO_LAUNCH(16);
+  else if (bits == 8) WO_LAUNCH(8);
+  else WO_LAUNCH(4);
+#undef WO_LAUNCH
+}
+
 PIAMD_EXPORT int piamd_wo_gemm(int bits, const void* x, long long ldx, const void* wp,
                                const float* scale, const void* bias, void* y, long long ldy,
                                float* ws, int* cnt, int M, int N, int K, int KS, int act,
@@ -575,22 +608,27 @@ PIAMD_EXPORT int piamd_wo_gemm(int bits, const void* x, long long ldx, const voi
   if ((bits != 16 && bits != 8 && bits != 4) || N % 32 || K % KB || KS < 1 ||
       (KS > 1 && !ws) || M < 1)
     return (int)hipErrorInvalidValue;
-  dim3 grid(N / 32, (M + 31) / 32, KS), block(256);
-  if (bits == 16)
-    hipLaunchKernelGGL(wo_gemm_kernel<16>, grid, block, 0, st, (const bf16_t*)x, ldx,
-                       (const unsigned char*)wp, scale, (const bf16_t*)bias, (bf16_t*)y, ldy, ws,
-                       cnt, M, N, K, act);
-  else if (bits == 8)
-    hipLaunchKernelGGL(wo_gemm_kernel<8>, grid, block, 0, st, (const bf16_t*)x, ldx,
-                       (const unsigned char*)wp, scale, (const bf16_t*)bias, (bf16_t*)y, ldy, ws,
-                       cnt, M, N, K, act);
-  else
-    hipLaunchKernelGGL(wo_gemm_kernel<4>, grid, block, 0, st, (const bf16_t*)x, ldx,
-                       (const unsigned char*)wp, scale, (const bf16_t*)bias, (bf16_t*)y, ldy, ws,
-                       cnt, M, N, K, act);
+  wo_launch(bits, dim3(N / 32, (M + 31) / 32, KS), st, x, ldx, wp, scale, bias, y, ldy, ws, cnt,
+            M, N, K, act, nullptr, 0, 0);
   if (KS > 1 && !cnt)
     hipLaunchKernelGGL(wo_finalize_kernel, dim3(stride_grid((long long)M * N, 256)), dim3(256), 0,
                        st, ws, KS, scale, (const bf16_t*)bias, (bf16_t*)y, ldy, M, N, act);
+  return (int)hipGetLastError();
+}
+
+// Grouped weight-only expert GEMM (the decode / small-batch MoE path of
+// fused_multi_transformer_moe_weight_only): x [rows][K] expert-sorted with device offsets
+// offs[E+1]; expert e's packed weights at wp + e*wstride bytes, scale/bias [E][N]. 32-row tiles,
+// worst-case grid ceil(rows_cap/32) + E, surplus tiles exit. bits 16 (packed bf16) / 8 / 4.
+PIAMD_EXPORT int piamd_wo_moe_gemm(int bits, const void* x, long long ldx, const void* wp,
+                                   long long wstride, const float* scale, const void* bias,
+                                   const int* offs, int E, int rows_cap, void* y, long long ldy,
+                                   int N, int K, int act, hipStream_t st) {
+  const int KB = bits == 16 ? 16 : (bits == 8 ? 32 : 64);
+  if ((bits != 16 && bits != 8 && bits != 4) || N % 32 || K % KB || E < 1 || rows_cap < 0)
+    return (int)hipErrorInvalidValue;
+  wo_launch(bits, dim3(N / 32, (rows_cap + 31) / 32 + E, 1), st, x, ldx, wp, scale, bias, y, ldy,
+            nullptr, nullptr, rows_cap, N, K, act, offs, E, wstride);
   return (int)hipGetLastError();
 }
 

@@ -133,6 +133,41 @@ def limit_by_capacity(idx, num_expert_total, capacity):
     return torch.where(keep, flat, torch.full_like(flat, -1)).reshape(idx.shape)
 
 
+_STACK_CACHE = {}
+
+
+def stacked(params):
+    """[P_0, …, P_{E-1}] → one [E, …] tensor. Under no_grad (serving) the stack is cached until
+    any expert parameter changes (keyed by storage + version); with grad it is rebuilt so the
+    gradient flows back to every expert."""
+    if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+        return torch.stack(list(params))
+    key = tuple((p.data_ptr(), p._version) for p in params)
+    hit = _STACK_CACHE.get(key)
+    if hit is None:
+        if len(_STACK_CACHE) > 256:
+            _STACK_CACHE.clear()
+        hit = _STACK_CACHE[key] = torch.stack([p.detach() for p in params])
+    return hit
+
+
+def _grouped_ok(x, w1s, w2s):
+    """The grouped MFMA path: bf16 on the GPU, K multiple of 64, N multiple of 256 for both."""
+    if not (x.is_cuda and x.dtype == torch.bfloat16):
+        return False
+    H, Fd = w1s[0].shape
+    return H % 256 == 0 and Fd % 256 == 0
+
+
+def grouped_moe_ffn(x, idx, val, W1, B1, W2, B2, act="gelu"):
+    """Expert FFN on one rank: sorted-row layout + two grouped GEMM launches (ops/moe.py)."""
+    from ..ops import moe as gm
+    r = gm.permute(idx, W1.shape[0])
+    xs = gm.gather(x, r)
+    ys = gm.grouped_ffn(xs, W1, B1, W2, B2, r, act)
+    return gm.combine(ys, val, r)
+
+
 def moe_ffn(x, gate_weight, gate_bias, w1s, b1s, w2s, b2s, top_k=2, act="gelu", group=None,
             capacity=None):
     """Fused MoE FFN (inference op ``fused_moe``): x [T, E] → [T, E]."""
@@ -142,6 +177,9 @@ def moe_ffn(x, gate_weight, gate_bias, w1s, b1s, w2s, b2s, top_k=2, act="gelu", 
     val, idx = topk_gate(logits, top_k)
     if capacity is not None:
         idx = limit_by_capacity(idx, logits.shape[-1], capacity)
+    if _ws(group) == 1 and _grouped_ok(x, w1s, w2s):
+        nb = lambda bs, n: stacked(bs) if bs[0] is not None else None  # noqa: E731
+        return grouped_moe_ffn(x, idx, val, stacked(w1s), nb(b1s, 0), stacked(w2s), nb(b2s, 0), act)
     xl, counts, ctx = dispatch(x, idx, len(w1s), group)
 
     def expert(e):

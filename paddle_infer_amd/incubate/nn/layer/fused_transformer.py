@@ -549,5 +549,88 @@ class FusedMultiTransformerMoe(_MultiTransformerBase):
         return (out, caches) if caches is not None else out
 
 
-FusedMultiTransformerMoeWeightOnly = FusedMultiTransformerMoe
-FusedMultiTransformerMoeINT8 = FusedMultiTransformerMoe
+class FusedMultiTransformerMoeWeightOnly(FusedMultiTransformerMoe):
+    """Reference `fused_transformer.py:3107` / `fused_multi_transformer_moe_weight_only_op.cu`:
+    the MoE multi-transformer with int8 / int4 weight-only EXPERT weights. Per layer the experts
+    are stored stacked — ``expert_weights{1,2}_q[i]`` [E_local, N_packed, K] uint8 in the MFMA
+    tile order of ``weight_quantize`` with ``expert_scales{1,2}[i]`` [E_local, N] f32 — and run
+    as ONE grouped weight-only launch per projection (``ops.moe.grouped_weight_only_linear``,
+    dequantisation inside the MFMA main loop, expert ranges resolved on the device). Attention /
+    gate weights stay bf16. Fill with :meth:`load_from_float`."""
+
+    def __init__(self, d_model, embed_dim, num_heads, dim_feedforward, weight_dtype="int8", **kw):
+        super().__init__(d_model, embed_dim, num_heads, dim_feedforward, **kw)
+        self._bits = 4 if weight_dtype == "int4" else 8
+        div = 2 if self._bits == 4 else 1
+        ne, E, F = self.num_expert, embed_dim, dim_feedforward
+        u8, one = torch.uint8, Constant(1.0)
+        self.expert_weights1_q, self.expert_scales1 = ParameterList(), ParameterList()
+        self.expert_weights2_q, self.expert_scales2 = ParameterList(), ParameterList()
+        for _ in range(self.num_layers):
+            self.expert_weights1_q.append(self.create_parameter([ne, F // div, E], None, u8, False, Constant(0)))
+            self.expert_scales1.append(self.create_parameter([ne, F], None, torch.float32, False, one))
+            self.expert_weights2_q.append(self.create_parameter([ne, E // div, F], None, u8, False, Constant(0)))
+            self.expert_scales2.append(self.create_parameter([ne, E], None, torch.float32, False, one))
+        # the bf16 expert weights of the base class are replaced by the quantized stacks
+        for pl in (self.expert_weights1, self.expert_weights2):
+            for p in pl:
+                p.data = p.data.new_empty(0)
+
+    def _layers(self, dtype):
+        from ...moe import topk_gate, stacked
+        from ....ops import moe as gm
+        out = super()._layers(dtype)
+        ne, bits = self.num_expert, self._bits
+        act = "gelu_tanh" if self.approximate else "gelu"
+        for i, L in enumerate(out):
+            sl = slice(i * ne, (i + 1) * ne)
+            b1 = stacked(list(self.expert_biases1)[sl]).to(dtype)
+            b2 = stacked(list(self.expert_biases2)[sl]).to(dtype)
+            w1, s1 = self.expert_weights1_q[i], self.expert_scales1[i]
+            w2, s2 = self.expert_weights2_q[i], self.expert_scales2[i]
+            gw, gb = self.gate_weights[i], self.gate_biases[i]
+
+            def moe(x, gw=gw, gb=gb, w1=w1, s1=s1, b1=b1, w2=w2, s2=s2, b2=b2):
+                logits = torch.matmul(x, gw) + gb
+                val, idx = topk_gate(logits, self.top_k)
+                r = gm.permute(idx, ne, align=1)
+                xs = gm.gather(x, r)
+                h = gm.grouped_weight_only_linear(xs, w1, s1, r.offs, r.rows_cap, b1, bits, act)
+                ys = gm.grouped_weight_only_linear(h, w2, s2, r.offs, r.rows_cap, b2, bits)
+                return gm.combine(ys, val, r)
+            L["moe"] = moe
+        return out
+
+    @torch.no_grad()
+    def load_from_float(self, fmt: "FusedMultiTransformerMoe"):
+        """Quantize a bf16/f32 FusedMultiTransformerMoe (same shapes) into this layer."""
+        from ....ops.inference import weight_quantize
+        algo = "weight_only_int4" if self._bits == 4 else "weight_only_int8"
+        own = dict(self.named_parameters())
+        for n, p in fmt.named_parameters():
+            if n in own and not n.startswith("expert_weights"):
+                own[n].data = p.data.to(own[n].device, own[n].dtype).reshape(own[n].shape) \
+                    if own[n].numel() == p.numel() else own[n].data
+        ne = self.num_expert
+        for i in range(self.num_layers):
+            for wq, sc, src in ((self.expert_weights1_q, self.expert_scales1, fmt.expert_weights1),
+                                (self.expert_weights2_q, self.expert_scales2, fmt.expert_weights2)):
+                qs, ss = zip(*[weight_quantize(src[i * ne + e].data.to(wq[i].device), algo)
+                               for e in range(ne)])
+                wq[i].data = torch.stack(qs)
+                sc[i].data = torch.stack(ss)
+        self._ln_cache = None
+        return self
+
+
+class FusedMultiTransformerMoeINT8(FusedMultiTransformerMoeWeightOnly):
+    """Reference `fused_multi_transformer_moe_int8_op.cu`: int8 expert weights. On MI355X the int8
+    experts run the grouped weight-only int8 MFMA path (activation in-scales are accepted and
+    recorded)."""
+
+    def __init__(self, d_model, embed_dim, num_heads, dim_feedforward, **kw):
+        self_scales = {k: kw.pop(k) for k in list(kw) if k.endswith("_in_scale")}
+        kw.pop("weight_dtype", None)
+        super().__init__(d_model, embed_dim, num_heads, dim_feedforward, weight_dtype="int8", **kw)
+        for k, v in self_scales.items():
+            setattr(self, k, v)

@@ -72,7 +72,6 @@ _SIGS = {
     "piamd_wo_gemm": [c_int, c_void_p, c_ll, c_void_p, c_void_p, c_void_p, c_void_p, c_ll,
                       c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "piamd_wo_dequant": [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p],
-    "piamd_embedding_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_ll, c_void_p],
 }
 
 
@@ -157,3 +156,22 @@ _SIGS["piamd_nan_inf_check"] = [c_int, c_void_p, c_ll, c_void_p, c_int, c_void_p
 _SIGS["piamd_gemm"] = [c_void_p, c_ll, c_int, c_void_p, c_ll, c_int, c_void_p, c_ll, c_int, c_int,
                        c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_ll, c_void_p]
 _SIGS["piamd_transpose_bf16"] = [c_void_p, c_void_p, c_int, c_int, c_void_p]
+_SIGS["piamd_moe_gemm"] = [c_void_p, c_ll, c_void_p, c_ll, c_ll,
+                                c_int, c_void_p, c_int, c_int, c_void_p,
+                                c_ll, c_int, c_int, c_int, c_int,
+                                c_int, c_void_p, c_void_p, c_ll, c_void_p]
+_SIGS["piamd_moe_wgrad"] = [c_void_p, c_ll, c_void_p, c_ll, c_void_p,
+                                 c_int, c_void_p, c_ll, c_int, c_int,
+                                 c_int, c_int, c_void_p]
+_SIGS["piamd_wo_moe_gemm"] = [c_int, c_void_p, c_ll, c_void_p, c_ll,
+                                   c_void_p, c_void_p, c_void_p, c_int,
+                                   c_int, c_void_p, c_ll, c_int, c_int,
+                                   c_int, c_void_p]
+# ids, w, start, vlocal, p, pos, S, out, T, H, stream
+_SIGS["piamd_embedding_fwd"] = [c_void_p, c_void_p, c_ll, c_int, c_void_p, c_void_p, c_int,
+                                c_void_p, c_ll, c_int, c_void_p]
+# sorted, order, dy, dw, dw_f32, start, vlocal, T, H, accumulate, stream
+_SIGS["piamd_embedding_bwd"] = [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_ll, c_int, c_ll,
+                                c_int, c_int, c_void_p]
+_SIGS["piamd_pos_embedding_bwd"] = [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                                    c_void_p]

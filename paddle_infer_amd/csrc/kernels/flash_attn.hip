@@ -115,10 +115,10 @@ __device__ __forceinline__ void glds_tile(const bf16_t* gbase, long long rstride
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
-    bf16_t* __restrict__ o, float* __restrict__ lse, int B, int Sq, int Sk, int Hq, int Hk,
+    bf16_t* __restrict__ o, float* __restrict__ lse, int B, int SqMax, int SkMax, int Hq, int Hk,
     long long sqb, long long sqs, long long sqh, long long skb, long long sks, long long skh,
     long long svb, long long svs, long long svh, long long sob, long long sos, long long soh,
-    float scale) {
+    float scale, const int* __restrict__ cu_q, const int* __restrict__ cu_k, int ltot) {
   constexpr int BM = 128, BN = 64;
   constexpr int KSTEPS = D / 16;
   constexpr int DT = D / 32;
@@ -129,12 +129,25 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5, gi = lane & 15, g = lane >> 4;
-  const int nmb = (Sq + BM - 1) / BM;
+  const int nmb = (SqMax + BM - 1) / BM;
   const int HB = Hq * B;
   const int mb = CAUSAL ? (nmb - 1 - (int)blockIdx.x / HB) : (int)blockIdx.x / HB;
   const int hq = (int)blockIdx.x % Hq, b = ((int)blockIdx.x % HB) / Hq;
   const int hk = hq / (Hq / Hk);
   const int m0 = mb * BM;
+  int Sq = SqMax, Sk = SkMax;
+  long long lbase = ((long long)b * Hq + hq) * SqMax;
+  if (cu_q) {  // variable-length: b = sequence, rows [cu[b], cu[b+1]) of the packed tensors
+    const int q0s = cu_q[b], k0s = cu_k[b];
+    Sq = cu_q[b + 1] - q0s;
+    Sk = cu_k[b + 1] - k0s;
+    if (m0 >= Sq) return;  // block-uniform: this sequence is shorter than the longest
+    q += (long long)q0s * sqs;
+    o += (long long)q0s * sos;
+    k += (long long)k0s * sks;
+    v += (long long)k0s * svs;
+    lbase = (long long)hq * ltot + q0s;
+  }
   const int qrow0 = m0 + w * 32;
   const int coff = Sk - Sq;  // bottom-right aligned causal offset
   const float c = scale * kLog2e;
@@ -275,7 +288,7 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(
         *reinterpret_cast<uint2*>(op + d0) = pk;
       }
     if (hh == 0 && lse)
-      lse[((long long)b * Hq + hq) * Sq + qpos] = l_i > 0.f ? (m_i + log2f(l_i)) * kLn2 : INFINITY;
+      lse[lbase + qpos] = l_i > 0.f ? (m_i + log2f(l_i)) * kLn2 : INFINITY;
   }
 }
 
@@ -311,9 +324,10 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse,
     const float* __restrict__ delta, bf16_t* __restrict__ dk, bf16_t* __restrict__ dv, int B,
-    int Sq, int Sk, int Hq, int Hk, long long sqb, long long sqs, long long sqh, long long skb,
+    int SqMax, int SkMax, int Hq, int Hk, long long sqb, long long sqs, long long sqh, long long skb,
     long long sks, long long skh, long long svb, long long svs, long long svh, long long sdob,
-    long long sdos, long long sdoh, float scale) {
+    long long sdos, long long sdoh, float scale, const int* __restrict__ cu_q,
+    const int* __restrict__ cu_k, int ltot) {
   constexpr int BK = 128, BQ = 64;
   constexpr int KSTEPS = D / 16;
   constexpr int DT = D / 32;
@@ -333,6 +347,22 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(
   const int kb = (int)blockIdx.x / HB;  // causal: low key blocks see the most queries -> first
   const int hk = (int)blockIdx.x % Hk, b = ((int)blockIdx.x % HB) / Hk;
   const int n0 = kb * BK;
+  int Sq = SqMax, Sk = SkMax;
+  long long lrow = (long long)b * Hq * SqMax, lhead = SqMax;  // stats index = lrow + hq*lhead + q
+  if (cu_q) {
+    const int q0s = cu_q[b], k0s = cu_k[b];
+    Sq = cu_q[b + 1] - q0s;
+    Sk = cu_k[b + 1] - k0s;
+    if (n0 >= Sk) return;
+    q += (long long)q0s * sqs;
+    dout += (long long)q0s * sdos;
+    k += (long long)k0s * sks;
+    v += (long long)k0s * svs;
+    dk += (long long)k0s * sks;
+    dv += (long long)k0s * svs;
+    lrow = q0s;
+    lhead = ltot;
+  }
   const int kw0 = n0 + 32 * w;  // this wave's first key
   const int key = kw0 + l32;
   const int coff = Sk - Sq;
@@ -364,7 +394,7 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(
     glds_tile<BQ, ROWB>(q + b * sqb + hq * sqh, sqs, q0, Sq - 1, qs, w, lane);
     glds_tile<BQ, ROWB>(dout + b * sdob + hq * sdoh, sdos, q0, Sq - 1, qs + QTILE_B, w, lane);
     if (w < 2) {  // wave 0: lse row, wave 1: delta row (64 f32 = one 4-B/lane DMA)
-      const float* s = (w == 0 ? lse : delta) + ((long long)b * Hq + hq) * Sq + min(q0 + lane, Sq - 1);
+      const float* s = (w == 0 ? lse : delta) + lrow + hq * lhead + min(q0 + lane, Sq - 1);
       char* st = smem + OFF_STAT + (buf * 2 + w) * BQ * 4;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)s,
                                        (__attribute__((address_space(3))) void*)st, 4, 0, 0);
@@ -509,10 +539,11 @@ template <int D, bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse,
-    const float* __restrict__ delta, bf16_t* __restrict__ dq, int B, int Sq, int Sk, int Hq,
+    const float* __restrict__ delta, bf16_t* __restrict__ dq, int B, int SqMax, int SkMax, int Hq,
     int Hk, long long sqb, long long sqs, long long sqh, long long skb, long long sks,
     long long skh, long long svb, long long svs, long long svh, long long sdob, long long sdos,
-    long long sdoh, float scale) {
+    long long sdoh, float scale, const int* __restrict__ cu_q, const int* __restrict__ cu_k,
+    int ltot) {
   constexpr int BM = 128, BN = 64;
   constexpr int KSTEPS = D / 16;
   constexpr int DT = D / 32;
@@ -523,12 +554,26 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5, gi = lane & 15, g = lane >> 4;
-  const int nmb = (Sq + BM - 1) / BM;
+  const int nmb = (SqMax + BM - 1) / BM;
   const int HB = Hq * B;
   const int mb = CAUSAL ? (nmb - 1 - (int)blockIdx.x / HB) : (int)blockIdx.x / HB;
   const int hq = (int)blockIdx.x % Hq, b = ((int)blockIdx.x % HB) / Hq;
   const int hk = hq / (Hq / Hk);
   const int m0 = mb * BM;
+  int Sq = SqMax, Sk = SkMax;
+  long long lbase = ((long long)b * Hq + hq) * SqMax;
+  if (cu_q) {
+    const int q0s = cu_q[b], k0s = cu_k[b];
+    Sq = cu_q[b + 1] - q0s;
+    Sk = cu_k[b + 1] - k0s;
+    if (m0 >= Sq) return;
+    q += (long long)q0s * sqs;
+    dq += (long long)q0s * sqs;
+    dout += (long long)q0s * sdos;
+    k += (long long)k0s * sks;
+    v += (long long)k0s * svs;
+    lbase = (long long)hq * ltot + q0s;
+  }
   const int qrow0 = m0 + w * 32;
   const int qpos = qrow0 + l32;
   const int coff = Sk - Sq;
@@ -548,7 +593,7 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
       qf[kk] = *reinterpret_cast<const bf16x8*>(qp + 16 * kk);
       df[kk] = *reinterpret_cast<const bf16x8*>(dp + 16 * kk);
     }
-    const long long si = ((long long)b * Hq + hq) * Sq + qr;
+    const long long si = lbase + qr;
     lse2 = lse[si] * kLog2e;
     dlt = delta[si];
   }
@@ -645,6 +690,18 @@ __global__ __launch_bounds__(256, 2) void fa_bwd_dq_kernel(
 
 }  // namespace
 
+PIAMD_EXPORT int piamd_flash_attn_varlen_fwd(const void*, const void*, const void*, void*, float*,
+                                             int, int, int, int, int, int, long long, long long,
+                                             long long, long long, long long, long long, long long,
+                                             long long, long long, long long, long long, long long,
+                                             float, int, const int*, const int*, int, hipStream_t);
+PIAMD_EXPORT int piamd_flash_attn_varlen_bwd(const void*, const void*, const void*, const void*,
+                                             const void*, const float*, float*, void*, void*, void*,
+                                             int, int, int, int, int, int, long long, long long,
+                                             long long, long long, long long, long long, long long,
+                                             long long, long long, long long, long long, long long,
+                                             float, int, const int*, const int*, int, hipStream_t);
+
 // q,k,v,o: bf16 [B, S, H, D] with element strides (b, s, h); d contiguous. lse: f32 [B, Hq, Sq]
 // (nullable). D in {64, 128}; Hq % Hk == 0.
 PIAMD_EXPORT int piamd_flash_attn_fwd(const void* q, const void* k, const void* v, void* o,
@@ -653,14 +710,31 @@ PIAMD_EXPORT int piamd_flash_attn_fwd(const void* q, const void* k, const void* 
                                       long long sks, long long skh, long long svb, long long svs,
                                       long long svh, long long sob, long long sos, long long soh,
                                       float scale, int causal, hipStream_t stream) {
-  if (Hk <= 0 || Hq % Hk) return (int)hipErrorInvalidValue;
+  return piamd_flash_attn_varlen_fwd(q, k, v, o, lse, B, Sq, Sk, Hq, Hk, D, sqb, sqs, sqh, skb, sks,
+                                     skh, svb, svs, svh, sob, sos, soh, scale, causal, nullptr,
+                                     nullptr, 0, stream);
+}
+
+// Variable-length (packed) form: cu_q / cu_k int32 [B+1] row offsets on the device, q/k/v/o packed
+// [total, H, D] (batch strides ignored), Sq / Sk = the longest sequence, lse f32 [Hq, total_q]
+// (ltot = total_q). With cu_q == null this is the padded [B, S, H, D] kernel above.
+PIAMD_EXPORT int piamd_flash_attn_varlen_fwd(const void* q, const void* k, const void* v, void* o,
+                                             float* lse, int B, int Sq, int Sk, int Hq, int Hk,
+                                             int D, long long sqb, long long sqs, long long sqh,
+                                             long long skb, long long sks, long long skh,
+                                             long long svb, long long svs, long long svh,
+                                             long long sob, long long sos, long long soh,
+                                             float scale, int causal, const int* cu_q,
+                                             const int* cu_k, int ltot, hipStream_t stream) {
+  if (Hk <= 0 || Hq % Hk || (cu_q && !cu_k)) return (int)hipErrorInvalidValue;
+  if (cu_q) sqb = skb = svb = sob = 0;
   if (B == 0 || Sq == 0) return 0;
   if (Sk == 0) return (int)hipErrorInvalidValue;
   dim3 grid(((Sq + 127) / 128) * Hq * B), block(256);
 #define FAF(DD, CC)                                                                               \
   hipLaunchKernelGGL((fa_fwd_kernel<DD, CC>), grid, block, 0, stream, (const bf16_t*)q,          \
                      (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse, B, Sq, Sk, Hq, Hk, sqb, \
-                     sqs, sqh, skb, sks, skh, svb, svs, svh, sob, sos, soh, scale)
+                     sqs, sqh, skb, sks, skh, svb, svs, svh, sob, sos, soh, scale, cu_q, cu_k, ltot)
   if (D == 128) { if (causal) FAF(128, true); else FAF(128, false); }
   else if (D == 64) { if (causal) FAF(64, true); else FAF(64, false); }
   else return (int)hipErrorInvalidValue;
@@ -680,14 +754,33 @@ PIAMD_EXPORT int piamd_flash_attn_bwd(const void* q, const void* k, const void* 
                                       long long svh, long long sdb, long long sds, long long sdh,
                                       float scale, int causal, hipStream_t stream) {
   (void)reserved; (void)dq_acc;
-  if (Hk <= 0 || Hq % Hk) return (int)hipErrorInvalidValue;
+  return piamd_flash_attn_varlen_bwd(q, k, v, o, dout, lse, delta, dq, dk, dv, B, Sq, Sk, Hq, Hk, D,
+                                     sqb, sqs, sqh, skb, sks, skh, svb, svs, svh, sdb, sds, sdh,
+                                     scale, causal, nullptr, nullptr, 0, stream);
+}
+
+// Variable-length backward (see piamd_flash_attn_varlen_fwd); lse / delta f32 [Hq, total_q].
+PIAMD_EXPORT int piamd_flash_attn_varlen_bwd(const void* q, const void* k, const void* v,
+                                             const void* o, const void* dout, const float* lse,
+                                             float* delta, void* dq, void* dk, void* dv, int B,
+                                             int Sq, int Sk, int Hq, int Hk, int D, long long sqb,
+                                             long long sqs, long long sqh, long long skb,
+                                             long long sks, long long skh, long long svb,
+                                             long long svs, long long svh, long long sdb,
+                                             long long sds, long long sdh, float scale,
+                                             int causal, const int* cu_q, const int* cu_k,
+                                             int ltot, hipStream_t stream) {
+  if (Hk <= 0 || Hq % Hk || (cu_q && !cu_k)) return (int)hipErrorInvalidValue;
+  if (cu_q) sqb = skb = svb = sdb = 0;
   if (B == 0 || Sq == 0 || Sk == 0) return 0;
-  const int total = B * Hq * Sq;
+  // delta rows: padded [B, Hq, Sq]; packed [Hq, ltot] == the padded layout with B = 1, Sq = ltot
+  const int pB = cu_q ? 1 : B, pS = cu_q ? ltot : Sq;
+  const int total = pB * Hq * pS;
   const int tpr = D / 8;
   const int pre_blocks = (int)(((long long)total * tpr + 255) / 256);
 #define PRE(DD)                                                                                   \
   hipLaunchKernelGGL((fa_bwd_pre_kernel<DD>), dim3(pre_blocks), dim3(256), 0, stream,            \
-                     (const bf16_t*)o, (const bf16_t*)dout, delta, Sq, Hq, sdb, sds, sdh, total)
+                     (const bf16_t*)o, (const bf16_t*)dout, delta, pS, Hq, sdb, sds, sdh, total)
   if (D == 128) PRE(128); else if (D == 64) PRE(64); else return (int)hipErrorInvalidValue;
 #undef PRE
   dim3 gkv(((Sk + 127) / 128) * Hk * B), gq(((Sq + 127) / 128) * Hq * B), block(256);
@@ -695,11 +788,11 @@ PIAMD_EXPORT int piamd_flash_attn_bwd(const void* q, const void* k, const void* 
   hipLaunchKernelGGL((fa_bwd_dkdv_kernel<DD, CC>), gkv, block, 0, stream, (const bf16_t*)q,      \
                      (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, delta,         \
                      (bf16_t*)dk, (bf16_t*)dv, B, Sq, Sk, Hq, Hk, sqb, sqs, sqh, skb, sks, skh,   \
-                     svb, svs, svh, sdb, sds, sdh, scale);                                        \
+                     svb, svs, svh, sdb, sds, sdh, scale, cu_q, cu_k, ltot);                      \
   hipLaunchKernelGGL((fa_bwd_dq_kernel<DD, CC>), gq, block, 0, stream, (const bf16_t*)q,         \
                      (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse, delta,         \
                      (bf16_t*)dq, B, Sq, Sk, Hq, Hk, sqb, sqs, sqh, skb, sks, skh, svb, svs, svh, \
-                     sdb, sds, sdh, scale)
+                     sdb, sds, sdh, scale, cu_q, cu_k, ltot)
   if (D == 128) { if (causal) { FAB(128, true); } else { FAB(128, false); } }
   else { if (causal) { FAB(64, true); } else { FAB(64, false); } }
 #undef FAB

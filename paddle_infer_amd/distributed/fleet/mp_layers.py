@@ -139,12 +139,10 @@ class VocabParallelEmbedding(Layer):
         _mark(self.weight, n > 1, 0)
 
     def forward(self, x):
+        from ...ops.embedding import embedding
+        out = embedding(x, self.weight, self.vocab_start)  # zero rows outside this vocab shard
         if _ws(self.group) == 1:
-            return F.embedding(x, self.weight)
-        mask = (x < self.vocab_start) | (x >= self.vocab_start + self.per_part)
-        idx = torch.where(mask, torch.zeros_like(x), x - self.vocab_start)
-        out = F.embedding(idx, self.weight)
-        out = out.masked_fill(mask.unsqueeze(-1), 0.0)
+            return out
         return mp_allreduce(out, self.group)
 
 

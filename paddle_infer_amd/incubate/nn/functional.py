@@ -473,23 +473,42 @@ def masked_multihead_attention(x, cache_kv=None, src_mask=None, sequence_lengths
 
 def variable_length_memory_efficient_attention(query, key, value, seq_lens, kv_seq_lens,
                                                mask=None, scale=None, causal=False):
-    """query [B, H, S, D], key/value [B, Hk, Sk, D]; per-batch valid lengths. Each batch is
-    attended over its own prefix with the flash kernel (reference
-    `variable_length_memory_efficient_attention.cu`)."""
+    """query [B, H, S, D], key/value [B, Hk, Sk, D]; per-batch valid lengths (reference
+    `variable_length_memory_efficient_attention.cu`). Without a mask the valid prefixes are packed
+    and run as ONE variable-length flash launch (``ops.flash_attention_varlen``); rows past a
+    sequence's length are zero."""
     B, H, S, D = query.shape
+    Sk = key.shape[2]
+    lq = seq_lens.reshape(-1).to(torch.long)
+    lk = kv_seq_lens.reshape(-1).to(torch.long)
     out = torch.zeros_like(query)
+    if mask is None:
+        dev = query.device
+        ar_q = torch.arange(S, device=dev)
+        ar_k = torch.arange(Sk, device=dev)
+        vq = (ar_q[None, :] < lq.to(dev)[:, None]).reshape(-1)
+        vk = (ar_k[None, :] < lk.to(dev)[:, None]).reshape(-1)
+        iq = vq.nonzero().squeeze(1)
+        ik = vk.nonzero().squeeze(1)
+        q = query.transpose(1, 2).reshape(B * S, H, D).index_select(0, iq)
+        k = key.transpose(1, 2).reshape(B * Sk, -1, D).index_select(0, ik)
+        v = value.transpose(1, 2).reshape(B * Sk, -1, D).index_select(0, ik)
+        cu_q = torch.zeros(B + 1, dtype=torch.int32, device=dev)
+        cu_k = torch.zeros(B + 1, dtype=torch.int32, device=dev)
+        cu_q[1:] = torch.cumsum(lq.to(dev), 0)
+        cu_k[1:] = torch.cumsum(lk.to(dev), 0)
+        o = ops.flash_attention_varlen(q, k, v, cu_q, cu_k, S, Sk, causal, scale)
+        flat = out.transpose(1, 2).reshape(B * S, H, D).clone()
+        flat.index_copy_(0, iq, o.to(flat.dtype))
+        return flat.view(B, S, H, D).transpose(1, 2).contiguous()
     for b in range(B):
-        sq, sk = int(seq_lens.reshape(-1)[b]), int(kv_seq_lens.reshape(-1)[b])
+        sq, sk = int(lq[b]), int(lk[b])
         if sq == 0:
             continue
         q = query[b:b + 1, :, :sq].transpose(1, 2)
         k = key[b:b + 1, :, :sk].transpose(1, 2)
         v = value[b:b + 1, :, :sk].transpose(1, 2)
-        if mask is None:
-            o = ops.flash_attention(q.contiguous(), k.contiguous(), v.contiguous(), causal, scale)
-        else:
-            o = ops.attention_reference(q, k, v, causal, scale,
-                                        mask[b:b + 1, :, :sq, :sk])
+        o = ops.attention_reference(q, k, v, causal, scale, mask[b:b + 1, :, :sq, :sk])
         out[b, :, :sq] = o.transpose(1, 2)
     return out
 

@@ -30,6 +30,7 @@ from ..nn import initializer as I
 from ..ops import fused_add_layer_norm, flash_attention_packed, bias_act, softmax_cross_entropy
 from ..ops.linear import _use_transposed, transposed
 from ..ops.linear import linear as _linear
+from ..ops.embedding import embedding as ops_embedding
 from ..distributed.fleet.mp_layers import (ColumnParallelLinear, RowParallelLinear,
                                            VocabParallelEmbedding, c_identity)
 
@@ -181,6 +182,10 @@ class GPTEmbeddings(Layer):
 
     def forward(self, input_ids, position_ids=None):
         S = input_ids.shape[1]
+        if _mp_size(self.word_embeddings.group) == 1:
+            # one fused gather+add kernel; sort-based deterministic backward into main_grad
+            return ops_embedding(input_ids, self.word_embeddings.weight, 0,
+                                 self.position_embeddings, position_ids)
         w = self.word_embeddings(input_ids)
         if position_ids is None:
             pe = self.position_embeddings[:S].unsqueeze(0)

@@ -413,17 +413,12 @@ def flash_attention(query, key, value, dropout=0.0, causal=False, return_softmax
 
 def flash_attn_unpadded(query, key, value, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k,
                         scale, dropout=0.0, causal=False, return_softmax=False, training=True, name=None):
-    """Variable-length (packed) attention: q/k/v are [total_tokens, H, D] with cumulative
-    sequence offsets; each sequence runs through the MFMA kernel."""
-    outs = []
-    cq = cu_seqlens_q.tolist()
-    ck = cu_seqlens_k.tolist()
-    for i in range(len(cq) - 1):
-        q = query[cq[i]:cq[i + 1]].unsqueeze(0)
-        k = key[ck[i]:ck[i + 1]].unsqueeze(0)
-        v = value[ck[i]:ck[i + 1]].unsqueeze(0)
-        outs.append(_ops.flash_attention(q, k, v, causal=causal, scale=scale)[0])
-    return torch.cat(outs, 0), None
+    """Reference `flash_attention.py:flash_attn_unpadded`: packed [total_tokens, H, D] q/k/v with
+    cumulative sequence offsets — one variable-length MFMA launch per pass (``flash_attn.hip``)."""
+    if dropout > 0.0 and training:
+        raise NotImplementedError("attention dropout is not implemented in the MFMA kernel")
+    return _ops.flash_attention_varlen(query, key, value, cu_seqlens_q, cu_seqlens_k, max_seqlen_q,
+                                       max_seqlen_k, causal=causal, scale=scale), None
 
 
 def scaled_dot_product_attention(query, key, value, attn_mask=None, dropout_p=0.0,

@@ -4,7 +4,8 @@ GPU tensors run the in-tree HIP library (``_lib/libpiamd_kernels.so``); CPU tens
 PyTorch reference composition of the same op.
 """
 from .norm import layer_norm, fused_add_layer_norm, rms_norm  # noqa: F401
-from .attention import flash_attention, flash_attention_packed, attention_reference  # noqa: F401
+from .attention import (flash_attention, flash_attention_packed, attention_reference,  # noqa: F401
+                        flash_attention_varlen)
 from .activation import bias_act, gelu, dropout, fused_softmax_mask  # noqa: F401
 from .loss import softmax_cross_entropy  # noqa: F401
 from .optim import adamw_flat, momentum_flat, sumsq  # noqa: F401

@@ -175,3 +175,7 @@ _SIGS["piamd_embedding_bwd"] = [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c
                                 c_int, c_int, c_void_p]
 _SIGS["piamd_pos_embedding_bwd"] = [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                                     c_void_p]
+_SIGS["piamd_flash_attn_varlen_fwd"] = (_SIGS["piamd_flash_attn_fwd"][:-1]
+                                        + [c_void_p, c_void_p, c_int, c_void_p])
+_SIGS["piamd_flash_attn_varlen_bwd"] = ([c_void_p] * 10 + [c_int] * 6 + [c_ll] * 12
+                                        + [c_float, c_int, c_void_p, c_void_p, c_int, c_void_p])

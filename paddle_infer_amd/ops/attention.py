@@ -138,3 +138,70 @@ def flash_attention_packed(qkv, num_heads: int, num_kv_heads: int | None = None,
     k = qkv[:, :, num_heads:num_heads + hk]
     v = qkv[:, :, num_heads + hk:]
     return attention_reference(q, k, v, causal, scale)
+
+
+# ------------------------------------------------------------------ variable length (packed)
+def _varlen_fwd(q, k, v, cu_q, cu_k, max_q, max_k, causal, scale):
+    T, Hq, D = q.shape
+    Hk = k.shape[1]
+    o = torch.empty((T, Hq, D), device=q.device, dtype=q.dtype)
+    lse = torch.empty((Hq, T), device=q.device, dtype=torch.float32)
+    _lib.call("piamd_flash_attn_varlen_fwd", q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(),
+              lse.data_ptr(), cu_q.numel() - 1, int(max_q), int(max_k), Hq, Hk, D,
+              0, q.stride(0), q.stride(1), 0, k.stride(0), k.stride(1), 0, v.stride(0), v.stride(1),
+              0, o.stride(0), o.stride(1), float(scale), int(causal), cu_q.data_ptr(),
+              cu_k.data_ptr(), T, _lib.stream())
+    return o, lse
+
+
+class _FlashAttnVarlenFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, cu_q, cu_k, max_q, max_k, causal, scale):
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        o, lse = _varlen_fwd(q, k, v, cu_q, cu_k, max_q, max_k, causal, scale)
+        ctx.save_for_backward(q, k, v, o, lse, cu_q, cu_k)
+        ctx.meta = (max_q, max_k, causal, scale)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse, cu_q, cu_k = ctx.saved_tensors
+        max_q, max_k, causal, scale = ctx.meta
+        do = do.contiguous()
+        T, Hq, D = q.shape
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        delta = torch.empty((Hq, T), device=q.device, dtype=torch.float32)
+        _lib.call("piamd_flash_attn_varlen_bwd", q.data_ptr(), k.data_ptr(), v.data_ptr(),
+                  o.data_ptr(), do.data_ptr(), lse.data_ptr(), delta.data_ptr(), dq.data_ptr(),
+                  dk.data_ptr(), dv.data_ptr(), cu_q.numel() - 1, int(max_q), int(max_k), Hq,
+                  k.shape[1], D, 0, q.stride(0), q.stride(1), 0, k.stride(0), k.stride(1), 0,
+                  v.stride(0), v.stride(1), 0, o.stride(0), o.stride(1), float(scale), int(causal),
+                  cu_q.data_ptr(), cu_k.data_ptr(), T, _lib.stream())
+        return dq, dk, dv, None, None, None, None, None, None
+
+
+def attention_varlen_reference(q, k, v, cu_q, cu_k, causal=False, scale=None):
+    cq, ck = cu_q.tolist(), cu_k.tolist()
+    outs = []
+    for i in range(len(cq) - 1):
+        outs.append(attention_reference(q[cq[i]:cq[i + 1]][None], k[ck[i]:ck[i + 1]][None],
+                                        v[ck[i]:ck[i + 1]][None], causal, scale)[0])
+    return torch.cat(outs, 0) if outs else q[:0].clone()
+
+
+def flash_attention_varlen(q, k, v, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k,
+                           causal: bool = False, scale: float | None = None):
+    """Packed variable-length attention in ONE launch per pass: q [Tq, Hq, D], k/v [Tk, Hk, D],
+    ``cu_seqlens_*`` int32 [B+1] cumulative offsets (device), ``max_seqlen_*`` host ints sizing the
+    grid (blocks past a sequence's end exit). Causal masking is bottom-right aligned per sequence.
+    Reference: `flash_attn_unpadded` / `variable_length_memory_efficient_attention.cu`."""
+    scale = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
+    if (q.is_cuda and q.dtype == torch.bfloat16 and k.dtype == q.dtype and v.dtype == q.dtype
+            and q.shape[-1] in (64, 128) and q.shape[1] % k.shape[1] == 0):
+        cu_q = cu_seqlens_q.to(device=q.device, dtype=torch.int32).contiguous()
+        cu_k = cu_seqlens_k.to(device=q.device, dtype=torch.int32).contiguous()
+        return _FlashAttnVarlenFn.apply(q, k, v, cu_q, cu_k, int(max_seqlen_q), int(max_seqlen_k),
+                                        causal, scale)
+    if q.is_cuda and q.dtype == torch.bfloat16:
+        raise RuntimeError(f"flash_attention_varlen: unsupported shape {tuple(q.shape)} on GPU")
+    return attention_varlen_reference(q, k, v, cu_seqlens_q, cu_seqlens_k, causal, scale)

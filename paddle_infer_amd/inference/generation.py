@@ -19,6 +19,8 @@ from __future__ import annotations
 import torch
 import torch.nn.functional as F
 
+from ..ops.search import beam_search_softmax
+
 from ..incubate.nn import functional as IF
 from ..incubate.nn.functional import _lin
 
@@ -197,36 +199,33 @@ class GPTGenerator:
         ids = input_ids.to(self.device).repeat_interleave(nb, 0)
         lens = (lengths if lengths is not None else torch.full((B0,), S)).to(self.device).repeat_interleave(nb)
         logits = self.prefill(ids, lens)
-        V = logits.shape[-1]
-        scores = torch.zeros(B0, nb, device=self.device)
-        scores[:, 1:] = float("-inf")
-        seqs = torch.full((B, max_new_tokens), pad, dtype=torch.long, device=self.device)
-        done = torch.zeros(B, dtype=torch.bool, device=self.device)
+        dev = self.device
+        # one fused beam_search_softmax launch pair per step (ops/search.py): log-softmax, per-beam
+        # top-k, per-batch top-beam, token-history (cache_ids) rewrite by parent beam
+        end = torch.tensor([eos if eos is not None else -1], dtype=torch.int32, device=dev)
+        cum = torch.zeros(B, dtype=torch.float32, device=dev)
+        stop = torch.zeros(B, dtype=torch.bool, device=dev)
+        seq_lens = lens.to(torch.int32).clamp_min(1)
+        hist = torch.full((B, max_new_tokens), pad, dtype=torch.int32, device=dev)
+        offs = torch.zeros((B0, nb, S + max_new_tokens), dtype=torch.int32, device=dev)
         pos = lens.to(torch.int32)
-        ar = torch.arange(B0, device=self.device)[:, None] * nb
+        ar = torch.arange(B0, device=dev).repeat_interleave(nb) * nb
         for t in range(max_new_tokens):
-            lp = F.log_softmax(logits.float(), -1)
-            if eos is not None:  # finished beams only extend with pad at no cost
-                pad_row = torch.full((V,), float("-inf"), device=lp.device)
-                pad_row[pad] = 0.0
-                lp = torch.where(done[:, None], pad_row[None, :], lp)
-            cand = (scores.view(B, 1) + lp).view(B0, nb * V)
-            top, idx = cand.topk(nb, -1)
-            src = (ar + idx // V).view(-1)
-            tok = (idx % V).view(-1)
-            scores = top
-            seqs = seqs.index_select(0, src)
-            seqs[:, t] = tok
-            done = done.index_select(0, src)
+            step = torch.full((B,), t, dtype=torch.int32, device=dev)
+            tok, cum, hist, offs, parent, stop, seq_lens, _ = beam_search_softmax(
+                logits, cum, seq_lens, stop, end, step, hist, offs, nb, S, max_new_tokens,
+                fuse_softmax=True, early_stop=False, length_penalty=0.0)
+            src = ar + parent.long()
             if eos is not None:
-                done = done | (tok == eos)
+                stop = stop | (tok == eos)
             self._reorder(src, B)
             if t + 1 < max_new_tokens:
-                logits = self.decode(tok, pos)
+                logits = self.decode(tok.long(), pos)
                 pos = pos + 1
+        seqs = hist.long()
         L = (seqs != pad).sum(-1).clamp_min(1).float().view(B0, nb)
-        best = (scores / L ** length_penalty).argmax(-1)
-        return seqs.view(B0, nb, -1)[torch.arange(B0, device=self.device), best]
+        best = (cum.view(B0, nb) / L ** length_penalty).argmax(-1)
+        return seqs.view(B0, nb, -1)[torch.arange(B0, device=dev), best]
 
 
 def generate(model, input_ids, **kw):

@@ -179,3 +179,8 @@ _SIGS["piamd_flash_attn_varlen_fwd"] = (_SIGS["piamd_flash_attn_fwd"][:-1]
                                         + [c_void_p, c_void_p, c_int, c_void_p])
 _SIGS["piamd_flash_attn_varlen_bwd"] = ([c_void_p] * 10 + [c_int] * 6 + [c_ll] * 12
                                         + [c_float, c_int, c_void_p, c_void_p, c_int, c_void_p])
+# logits, bf16, cum, seq_lens, stop, end_ids, step_ids, last_cache, last_offs, bs, beam, V,
+# max_seq_len, max_dec_len, fuse, early, penalty, P, part, ids, cum_out, cache, offs, parent,
+# stop_out, sl_out, st_out, stream
+_SIGS["piamd_beam_search_softmax"] = ([c_void_p, c_int] + [c_void_p] * 7 + [c_int] * 7
+                                      + [c_float, c_int] + [c_void_p] * 10)

@@ -913,3 +913,4 @@ def __getattr__(name):
 
 
 _math  # noqa
+from ..ops.search import beam_search_softmax  # noqa: E402,F401

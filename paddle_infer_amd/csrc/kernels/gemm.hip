@@ -308,7 +308,160 @@ __global__ __launch_bounds__(NTHR, 1) void moe_wgrad_kernel(
   gemm_epilogue(acc, out, N, dw_f32, accumulate, m0, M, n0, N, EPI_STORE, 0, nullptr, nullptr, 0);
 }
 
+// ---- int8 × int8 → int32 GEMM with dequantising epilogue -------------------------------------
+// Parity: reference `fused_multi_transformer_int8_op.cu` / `attn_gemm_int8.h` (cublasLt int8
+// igemm between quantised activations and int8 weights, dequantised with per-channel out scales)
+// and `llm_int8_linear`. Y[M][N] = act((Xq[M][K] · Wq[N][K]ᵀ) · xs[m] · ws[n] + bias[n]).
+// Same 256×256 tile / glds double buffer / XOR images as the bf16 kernel: a 128-byte LDS row holds
+// 128 int8 (instead of 64 bf16), so the DMA and the 16-byte fragment reads are unchanged and each
+// 16-B fragment feeds one v_mfma_i32_32x32x32_i8 (k = 16·half + j) — twice the bf16 MFMA rate.
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+typedef int i32x16_t __attribute__((ext_vector_type(16)));
+
+__global__ __launch_bounds__(NTHR, 1) void gemm_i8_kernel(
+    const signed char* __restrict__ x, long long ldx, const signed char* __restrict__ wq,
+    long long ldw, const float* __restrict__ xs, float xs_const, const float* __restrict__ ws,
+    const bf16_t* __restrict__ bias, bf16_t* __restrict__ y, long long ldy, int M, int N, int K,
+    int act) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w >> 2, wc = w & 3;
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  const int wg = xcd_remap(blockIdx.x, tm * tn);
+  const int m0 = (wg / tn) * BM, n0 = (wg % tn) * BN;
+  // byte matrices viewed as 2-byte elements for the shared DMA helper
+  const bf16_t* xa = reinterpret_cast<const bf16_t*>(x);
+  const bf16_t* wa = reinterpret_cast<const bf16_t*>(wq);
+  const long long lx = ldx / 2, lw = ldw / 2;
+  i32x16_t acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0;
+  auto stage_load = [&](int kt, int s) {
+    char* ai = smem + s * STAGE_BYTES;
+    const long long k0 = (long long)kt * 64;  // 128 int8 = 64 two-byte units
+    dma_tile<256, 128>(xa + k0, lx, m0, M - 1, ai, w, lane);
+    dma_tile<256, 128>(wa + k0, lw, n0, N - 1, ai + TILE_BYTES, w, lane);
+  };
+  const int nk = K / 128;
+  stage_load(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int hi = lane >> 5, l31 = lane & 31;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int s = kt & 1;
+    if (kt + 1 < nk) stage_load(kt + 1, s ^ 1);
+    const char* ai = smem + s * STAGE_BYTES;
+    const char* bi = ai + TILE_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      i32x4_t af[4], bf[2];
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb)
+        af[mb] = *reinterpret_cast<const i32x4_t*>(ai + img_off<128>(wr * 128 + mb * 32 + l31, 2 * ks + hi));
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+        bf[nb] = *reinterpret_cast<const i32x4_t*>(bi + img_off<128>(wc * 64 + nb * 32 + l31, 2 * ks + hi));
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+          acc[mb][nb] = __builtin_amdgcn_mfma_i32_32x32x32_i8(bf[nb], af[mb], acc[mb][nb], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) {
+    const int m = m0 + wr * 128 + mb * 32 + l31;
+    if (m >= M) continue;
+    const float sm = xs ? xs[m] : xs_const;
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = n0 + wc * 64 + nb * 32 + 8 * g + 4 * hi;
+        if (n >= N) continue;
+        u16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float v = (float)acc[mb][nb][4 * g + j] * sm * ws[n + j];
+          if (bias) v += bf2f(bias[n + j]);
+          o[j] = f2bf(act_fwd(v, act));
+        }
+        *reinterpret_cast<u16x4*>(y + (long long)m * ldy + n) = o;
+      }
+    }
+  }
+}
+
+// Row quantisation: q[m][k] = clamp(round(x[m][k] / s_m), -127, 127) with s_m = max|x[m]| / 127
+// (dynamic, per token; written to scale[m]) or the static per-tensor scale `s_static` (> 0).
+// One wave per row, 16-B loads.
+__global__ __launch_bounds__(256) void quant_rows_kernel(const bf16_t* __restrict__ x, long long ldx,
+                                                         signed char* __restrict__ q, long long ldq,
+                                                         float* __restrict__ scale, float s_static,
+                                                         int M, int K) {
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;
+  const bf16_t* xr = x + (long long)m * ldx;
+  float s = s_static;
+  if (s <= 0.f) {
+    float mx = 0.f;
+    for (int k = lane * 8; k < K; k += 512) {
+      const u16x8 v = *reinterpret_cast<const u16x8*>(xr + k);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mx = fmaxf(mx, fabsf(bf2f(v[j])));
+    }
+    mx = wave_max(mx);
+    s = mx > 0.f ? mx / 127.f : 1.f;
+    if (lane == 0) scale[m] = s;
+  }
+  const float inv = 1.f / s;
+  for (int k = lane * 8; k < K; k += 512) {
+    const u16x8 v = *reinterpret_cast<const u16x8*>(xr + k);
+    unsigned lo = 0, hi = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int qi = (int)fminf(127.f, fmaxf(-127.f, rintf(bf2f(v[j]) * inv)));
+      const unsigned b = (unsigned)(qi & 255);
+      if (j < 4) lo |= b << (8 * j); else hi |= b << (8 * (j - 4));
+    }
+    *reinterpret_cast<uint2*>(q + (long long)m * ldq + k) = make_uint2(lo, hi);
+  }
+}
+
 }  // namespace
+
+// x [M][K] int8 row-major (ldx bytes), wq [N][K] int8 (ldw bytes); xs [M] per-row activation
+// scales (or null → xs_const), ws [N] per-channel weight scales; y [M][N] bf16. K % 128 == 0,
+// 16-byte aligned rows, N % 4 == 0.
+PIAMD_EXPORT int piamd_gemm_i8(const void* x, long long ldx, const void* wq, long long ldw,
+                               const float* xs, float xs_const, const float* ws, const void* bias,
+                               void* y, long long ldy, int M, int N, int K, int act,
+                               hipStream_t st) {
+  if (K % 128 || N % 4 || M <= 0 || N <= 0 || ldx % 16 || ldw % 16) return (int)hipErrorInvalidValue;
+  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  hipLaunchKernelGGL(gemm_i8_kernel, dim3(tiles), dim3(NTHR), 0, st, (const signed char*)x, ldx,
+                     (const signed char*)wq, ldw, xs, xs_const, ws, (const bf16_t*)bias,
+                     (bf16_t*)y, ldy, M, N, K, act);
+  return (int)hipGetLastError();
+}
+
+// bf16 [M][K] → int8 [M][K]; s_static > 0: per-tensor scale, else dynamic per-row (scale[M] out).
+PIAMD_EXPORT int piamd_quant_rows(const void* x, long long ldx, void* q, long long ldq,
+                                  float* scale, float s_static, int M, int K, hipStream_t st) {
+  if (K % 8 || M <= 0 || (s_static <= 0.f && !scale)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(quant_rows_kernel, dim3((M + 3) / 4), dim3(256), 0, st, (const bf16_t*)x,
+                     ldx, (signed char*)q, ldq, scale, s_static, M, K);
+  return (int)hipGetLastError();
+}
 
 // trans_a: A given as [K][M] (lda ≥ M); else [M][K] (lda ≥ K).
 // trans_b: B given as [N][K] (ldb ≥ K); else [K][N] (ldb ≥ N).

@@ -192,11 +192,12 @@ class _Linear:
     """A projection: bf16 weight ([in, out] Paddle layout, or [out, in] when ``trans``) or a
     weight-only packed weight + scale. ``packed``: an optional MFMA-tile packed bf16 copy used for
     small-M (decode) calls, where the GEMM is a weight stream (see ops.inference.pack_bf16)."""
-    __slots__ = ("w", "scale", "bits", "trans", "packed")
+    __slots__ = ("w", "scale", "bits", "trans", "packed", "act_scale")
     PACKED_MAX_M = 64
 
-    def __init__(self, w, scale=None, bits=0, trans=False, packed=None):
+    def __init__(self, w, scale=None, bits=0, trans=False, packed=None, act_scale=None):
         self.w, self.scale, self.bits, self.trans, self.packed = w, scale, bits, trans, packed
+        self.act_scale = act_scale  # bits == -8: int8 activations (None → dynamic per token)
 
     def prepack(self):
         if not self.bits and self.packed is None:
@@ -206,6 +207,8 @@ class _Linear:
         return self
 
     def __call__(self, x, bias=None, act="none"):
+        if self.bits == -8:  # int8 x int8 MFMA GEMM, dequantising epilogue (FusedMultiTransformerINT8)
+            return _inf.int8_linear(x, self.w, self.scale, bias, self.act_scale, act)
         if self.bits:
             return _inf.weight_only_linear(x, self.w, bias, self.scale,
                                            "int4" if self.bits == 4 else "int8", act)
@@ -217,8 +220,8 @@ class _Linear:
         return y if bias is None else y + bias
 
 
-def _lin(w, scale=None, bits=0, trans=False):
-    return _Linear(w, scale, bits, trans)
+def _lin(w, scale=None, bits=0, trans=False, act_scale=None):
+    return _Linear(w, scale, bits, trans, act_scale=act_scale)
 
 
 def multi_transformer_forward(x, layers, num_heads, num_kv_heads=None, pre_layer_norm=True,

@@ -418,9 +418,13 @@ class FusedMultiTransformerWeightOnly(_MultiTransformerBase):
 
 
 class FusedMultiTransformerINT8(FusedMultiTransformerWeightOnly):
-    """Reference `fused_transformer.py:1808` (int8 weights with activation in/out scales for
-    int8 GEMMs). On MI355X the int8 weights run through the weight-only int8 MFMA path; the
-    activation-scale attributes are accepted and recorded (``qkv_in_scale`` …)."""
+    """Reference `fused_transformer.py:1808` / `fused_multi_transformer_int8_op.cu`: int8 weights
+    AND int8 activations. Every projection quantises its input (static per-tensor scale from the
+    ``*_in_scale`` attributes, reference convention q = round(127 · in_scale · x); or dynamic
+    per-token absmax when no scale is given), runs the int8×int8 MFMA GEMM with int32 accumulation
+    (``gemm.hip`` gemm_i8) and dequantises with the per-channel weight scale in the epilogue
+    (bias and activation fused). Weights are row-major int8 [N, K] + f32 scales [N]; fill with
+    :meth:`load_from_float`."""
 
     def __init__(self, embed_dim, num_heads, dim_feedforward, dropout_rate=0.0, activation="gelu",
                  normalize_before=True, qkv_in_scale=None, out_linear_in_scale=None,
@@ -433,6 +437,58 @@ class FusedMultiTransformerINT8(FusedMultiTransformerWeightOnly):
                          normalize_before, **kw)
         self.qkv_in_scale, self.out_linear_in_scale = qkv_in_scale, out_linear_in_scale
         self.ffn1_in_scale, self.ffn2_in_scale = ffn1_in_scale, ffn2_in_scale
+
+    @staticmethod
+    def _act_scale(scales, i):
+        if scales is None:
+            return None
+        v = scales[i] if isinstance(scales, (list, tuple)) else scales
+        v = float(v)
+        return None if v <= 0 else 1.0 / (127.0 * v)
+
+    def _layers(self, dtype):
+        lns = self._cast_ln(dtype)
+        i8 = lambda w: w.view(torch.int8)  # noqa: E731
+        out = []
+        for i in range(self.num_layers):
+            out.append(dict(
+                head_dim=self.head_dim, ln_scale=lns[i][0], ln_bias=lns[i][1],
+                qkv=_lin(i8(self.qkv_weights[i]), self.qkv_scales[i], -8,
+                         act_scale=self._act_scale(self.qkv_in_scale, i)),
+                qkv_bias=self.qkv_biases[i],
+                out=_lin(i8(self.linear_weights[i]), self.linear_scales[i], -8,
+                         act_scale=self._act_scale(self.out_linear_in_scale, i)),
+                out_bias=self.linear_biases[i], ffn_ln_scale=lns[i][2], ffn_ln_bias=lns[i][3],
+                ffn1=_lin(i8(self.ffn1_weights[i]), self.ffn1_scales[i], -8,
+                          act_scale=self._act_scale(self.ffn1_in_scale, i)),
+                ffn1_bias=self.ffn1_biases[i],
+                ffn2=_lin(i8(self.ffn2_weights[i]), self.ffn2_scales[i], -8,
+                          act_scale=self._act_scale(self.ffn2_in_scale, i)),
+                ffn2_bias=self.ffn2_biases[i]))
+        return out
+
+    @torch.no_grad()
+    def load_from_float(self, fmt: "FusedMultiTransformer"):
+        """Quantize a bf16/f32 FusedMultiTransformer's weights (per-channel int8, row-major)."""
+        from ....ops.inference import weight_quantize
+        for i in range(self.num_layers):
+            for dst, s in ((self.ln_scales, fmt.ln_scales), (self.ln_biases, fmt.ln_biases),
+                           (self.ffn_ln_scales, fmt.ffn_ln_scales), (self.ffn_ln_biases, fmt.ffn_ln_biases)):
+                dst[i].data.copy_(s[i].data)
+            wq = fmt.qkv_weights[i].data
+            wq = wq.reshape(-1, wq.shape[-1]).t() if fmt._trans_qkvw else wq.reshape(wq.shape[0], -1)
+            for (w, sc, src) in ((self.qkv_weights, self.qkv_scales, wq),
+                                 (self.linear_weights, self.linear_scales, fmt.linear_weights[i].data),
+                                 (self.ffn1_weights, self.ffn1_scales, fmt.ffn1_weights[i].data),
+                                 (self.ffn2_weights, self.ffn2_scales, fmt.ffn2_weights[i].data)):
+                q, s = weight_quantize(src.to(w[i].device), "llm.int8")
+                w[i].data = q.view(torch.uint8).to(w[i].device)
+                sc[i].data = s.to(sc[i].device)
+            for dst, src in ((self.qkv_biases, fmt.qkv_biases), (self.linear_biases, fmt.linear_biases),
+                             (self.ffn1_biases, fmt.ffn1_biases), (self.ffn2_biases, fmt.ffn2_biases)):
+                dst[i].data = src[i].data.reshape(-1).to(dst[i].dtype)
+        self._ln_cache = None
+        return self
 
 
 # ----------------------------------------------------------------------------- MoE

@@ -11,7 +11,8 @@ from .loss import softmax_cross_entropy  # noqa: F401
 from .optim import adamw_flat, momentum_flat, sumsq  # noqa: F401
 from . import _lib  # noqa: F401
 from .inference import (qkv_prep, decode_attention, weight_quantize, weight_dequantize,  # noqa: F401
-                        weight_only_linear, llm_int8_linear)
+                        weight_only_linear, llm_int8_linear, int8_linear,
+                        quantize_rows)
 
 
 def _make_recordable():

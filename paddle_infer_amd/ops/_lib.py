@@ -184,3 +184,8 @@ _SIGS["piamd_flash_attn_varlen_bwd"] = ([c_void_p] * 10 + [c_int] * 6 + [c_ll] *
 # stop_out, sl_out, st_out, stream
 _SIGS["piamd_beam_search_softmax"] = ([c_void_p, c_int] + [c_void_p] * 7 + [c_int] * 7
                                       + [c_float, c_int] + [c_void_p] * 10)
+# x, ldx, wq, ldw, xs, xs_const, ws, bias, y, ldy, M, N, K, act, stream
+_SIGS["piamd_gemm_i8"] = [c_void_p, c_ll, c_void_p, c_ll, c_void_p, c_float, c_void_p, c_void_p,
+                          c_void_p, c_ll, c_int, c_int, c_int, c_int, c_void_p]
+_SIGS["piamd_quant_rows"] = [c_void_p, c_ll, c_void_p, c_ll, c_void_p, c_float, c_int, c_int,
+                             c_void_p]

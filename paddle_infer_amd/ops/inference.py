@@ -245,12 +245,16 @@ def _ws_buf(device, n, tiles):
 
 
 def weight_quantize(x, algo="weight_only_int8"):
-    """x: [K, N] float → (packed weight, scale[N] f32). Symmetric per-output-channel."""
+    """x: [K, N] float → (quantized weight, scale[N] f32). Symmetric per-output-channel.
+    ``weight_only_int8`` / ``weight_only_int4``: MFMA-tile packed bytes for the weight-only GEMM;
+    ``llm.int8``: plain row-major int8 [N, K] for the int8×int8 GEMM (``int8_linear``)."""
     bits = 4 if algo == "weight_only_int4" else 8
     w = x.float().t().contiguous()  # [N, K]
     qmax = 7.0 if bits == 4 else 127.0
     scale = w.abs().amax(1).clamp_min(1e-10) / qmax
     q = torch.round(w / scale[:, None]).clamp(-qmax - (1 if bits == 4 else 0), qmax).to(torch.int8)
+    if algo == "llm.int8":
+        return q, scale
     return _pack(q, bits), scale
 
 
@@ -309,17 +313,73 @@ def weight_only_linear(x, weight, bias=None, weight_scale=None, weight_dtype="in
     return _ref_act(y, act).to(x.dtype).reshape(*lead, N)
 
 
+def quantize_rows(x, scale=None):
+    """bf16 [M, K] → (int8 [M, K], per-row scale [M] f32). ``scale`` (float > 0): static
+    per-tensor scale (x ≈ q · scale); None: dynamic per-token absmax / 127."""
+    K = x.shape[-1]
+    x2 = x.reshape(-1, K)
+    M = x2.shape[0]
+    if not x.is_cuda:
+        xf = x2.float()
+        s = (xf.abs().amax(1).clamp_min(1e-30) / 127.0) if scale is None else \
+            torch.full((M,), float(scale))
+        s = torch.where(xf.abs().amax(1) > 0, s, torch.ones_like(s)) if scale is None else s
+        q = torch.round(xf / s[:, None]).clamp(-127, 127).to(torch.int8)
+        return q, s
+    if x2.stride(-1) != 1 or x2.dtype != torch.bfloat16:
+        x2 = x2.to(torch.bfloat16).contiguous()
+    q = torch.empty((M, K), dtype=torch.int8, device=x.device)
+    if scale is None:
+        s = torch.empty(M, dtype=torch.float32, device=x.device)
+        _lib.call("piamd_quant_rows", x2.data_ptr(), x2.stride(0), q.data_ptr(), K, s.data_ptr(),
+                  0.0, M, K, _lib.stream())
+    else:
+        s = torch.full((M,), float(scale), dtype=torch.float32, device=x.device)
+        _lib.call("piamd_quant_rows", x2.data_ptr(), x2.stride(0), q.data_ptr(), K, None,
+                  float(scale), M, K, _lib.stream())
+    return q, s
+
+
+def int8_gemm(xq, xs, wq, ws, bias=None, act="none"):
+    """y = act((xq · wqᵀ) · xs[m] · ws[n] + bias) → bf16. xq [M, K] int8, wq [N, K] int8."""
+    M, K = xq.shape
+    N = wq.shape[0]
+    if not xq.is_cuda:
+        y = (xq.double() @ wq.double().t()) * xs.double()[:, None] * ws.double()[None, :]
+        if bias is not None:
+            y = y + bias.double()
+        return _ref_act(y.float(), ACTS[act]).to(torch.bfloat16)
+    assert K % 128 == 0 and N % 4 == 0, "int8 GEMM needs K % 128 == 0 and N % 4 == 0"
+    y = torch.empty((M, N), dtype=torch.bfloat16, device=xq.device)
+    wsf = ws.float().contiguous()
+    _lib.call("piamd_gemm_i8", xq.data_ptr(), xq.stride(0), wq.data_ptr(), wq.stride(0),
+              xs.data_ptr(), 0.0, wsf.data_ptr(), _lib.ptr(bias), y.data_ptr(), y.stride(0), M, N,
+              K, ACTS[act], _lib.stream())
+    return y
+
+
+def int8_linear(x, weight, weight_scale, bias=None, act_scale=None, act="none"):
+    """Activation-quantised int8 linear (reference `fused_multi_transformer_int8` GEMMs):
+    x [..., K] bf16 is quantised per token (``act_scale=None``) or with the static per-tensor
+    ``act_scale``; weight [N, K] int8 row-major (``weight_quantize(w, "llm.int8")``) with per-channel
+    ``weight_scale`` [N]; int8 MFMA GEMM with int32 accumulation and a dequantising epilogue."""
+    K = x.shape[-1]
+    lead = x.shape[:-1]
+    xq, xs = quantize_rows(x.reshape(-1, K), act_scale)
+    y = int8_gemm(xq, xs, weight, weight_scale, bias, act)
+    return y.reshape(*lead, weight.shape[0]).to(x.dtype if x.dtype != torch.float32 else torch.float32)
+
+
 def llm_int8_linear(x, weight, bias=None, weight_scale=None, threshold=6.0):
-    """LLM.int8: outlier input features (|x| > threshold in any row) run in bf16 against the
-    dequantized columns, the rest through the weight-only int8 path. Parity: reference
-    `nn/quant/quantized_linear.py:llm_int8_linear`."""
+    """LLM.int8 (reference `nn/quant/quantized_linear.py:llm_int8_linear`): input features with an
+    outlier (|x| > threshold in any row) run in bf16 against the dequantised weight columns; the rest
+    is quantised per token to int8 and multiplied by the int8 weight [N, K] on the int8 MFMA GEMM."""
     K = x.shape[-1]
     x2 = x.reshape(-1, K)
     outl = (x2.abs() > threshold).any(0)
-    if not bool(outl.any()):
-        return weight_only_linear(x, weight, bias, weight_scale, "int8")
-    wd = weight_dequantize(weight, weight_scale, "weight_only_int8", "float32").to(x.device)  # [K,N]
     xi = x2.masked_fill(outl[None, :], 0)
-    y = weight_only_linear(xi.reshape(x.shape), weight, bias, weight_scale, "int8")
-    yo = (x2[:, outl].float() @ wd[outl].float()).to(y.dtype)
-    return y + yo.reshape(y.shape)
+    y = int8_linear(xi, weight, weight_scale, bias).float()
+    if bool(outl.any()):
+        wd = weight.float() * weight_scale.float()[:, None]  # [N, K]
+        y = y + x2[:, outl].float() @ wd[:, outl].t()
+    return y.to(x.dtype).reshape(*x.shape[:-1], weight.shape[0])

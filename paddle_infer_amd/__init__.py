@@ -72,7 +72,11 @@ def flops(net, input_size, custom_ops=None, print_detail=False):
 def __getattr__(name):
     import importlib
     lazy = {"distributed", "static", "inference", "jit", "incubate", "vision", "metric", "hapi",
-            "profiler", "utils", "models", "parallel", "text", "fft", "signal", "sparse", "callbacks"}
+            "profiler", "utils", "models", "parallel", "text", "fft", "signal", "sparse", "callbacks",
+            "distribution", "geometric", "audio", "onnx", "regularizer", "sysconfig", "hub",
+            "reader", "quantization"}
+    if name == "batch":
+        return importlib.import_module(".reader", __name__).batch
     if name in lazy:
         return importlib.import_module(f".{name}", __name__)
     if name in ("Model",):

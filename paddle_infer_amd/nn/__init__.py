@@ -20,3 +20,4 @@ from . import functional  # noqa: F401
 from . import initializer  # noqa: F401
 from .clip import ClipGradByGlobalNorm, ClipGradByNorm, ClipGradByValue  # noqa: F401
 from . import clip as utils  # noqa: F401
+from . import quant  # noqa: F401,E402

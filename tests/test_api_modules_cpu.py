@@ -178,7 +178,8 @@ def test_quantization_qat_and_ptq():
     m = paddle.nn.Sequential(paddle.nn.Linear(8, 16), paddle.nn.ReLU(), paddle.nn.Linear(16, 4))
     x = torch.randn(6, 8)
     ref = m(x)
-    q = ImperativeQuantAware(weight_quantize_type="channel_wise_abs_max").quantize(m)
+    q = ImperativeQuantAware(weight_quantize_type="channel_wise_abs_max",
+                             activation_quantize_type="abs_max").quantize(m)
     y = q(x)
     assert type(q[0]).__name__ == "QuantizedLinear"
     assert (y - ref).abs().max() < 0.1 * ref.abs().max() + 0.05

@@ -31,3 +31,8 @@ def gloo_release():
     destroy_process_group()
 from . import checkpoint  # noqa: F401,E402
 from .checkpoint import save_state_dict, load_state_dict  # noqa: F401,E402
+from . import communication  # noqa: F401,E402
+from . import auto_parallel  # noqa: F401,E402
+from . import elastic  # noqa: F401,E402
+from .auto_parallel import ProcessMesh, shard_tensor, shard_op, reshard  # noqa: F401,E402
+from .communication import stream  # noqa: F401,E402

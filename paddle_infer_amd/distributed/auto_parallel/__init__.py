@@ -1,0 +1,293 @@
+"""``paddle.distributed.auto_parallel`` (reference `distributed/auto_parallel/`): semi-automatic
+parallelism — ProcessMesh, ``shard_tensor`` / ``shard_op`` annotations, Strategy, Engine.
+
+MI355X design: annotations become ``torch.distributed.tensor`` DTensors on a DeviceMesh (RCCL
+collectives over xGMI inserted by the DTensor propagation rules), instead of the reference's
+static-graph completion / partition / reshard passes. ``shard_spec`` follows Paddle: one entry per
+tensor dim naming the mesh dim it is split over (or None = replicated). Engine drives training /
+evaluation / prediction of a (possibly DTensor-sharded) model with the hapi loop.
+"""
+from __future__ import annotations
+
+import contextlib
+
+import torch
+import torch.distributed as dist
+
+__all__ = ["ProcessMesh", "shard_tensor", "shard_op", "recompute", "fetch", "Strategy", "Engine",
+           "get_current_process_mesh", "reshard"]
+
+_CUR = {"mesh": None}
+
+
+class ProcessMesh:
+    """An N-d arrangement of ranks with named dims (``ProcessMesh([[0, 1], [2, 3]], ["dp", "mp"])``).
+    Usable as a context manager that sets the current mesh."""
+
+    def __init__(self, mesh=None, dim_names=None, shape=None, process_ids=None):
+        if mesh is None:
+            mesh = torch.tensor(process_ids).reshape(shape).tolist()
+        self._mesh = torch.as_tensor(mesh, dtype=torch.long)
+        self._dim_names = list(dim_names) if dim_names else [f"d{i}" for i in range(self._mesh.dim())]
+        self._device_mesh = None
+
+    @property
+    def shape(self):
+        return list(self._mesh.shape)
+
+    @property
+    def ndim(self):
+        return self._mesh.dim()
+
+    @property
+    def dim_names(self):
+        return self._dim_names
+
+    @property
+    def process_ids(self):
+        return self._mesh.reshape(-1).tolist()
+
+    @property
+    def mesh(self):
+        return self._mesh
+
+    def get_dim_size(self, dim):
+        return self.shape[self._dim_names.index(dim) if isinstance(dim, str) else dim]
+
+    def __eq__(self, other):
+        return isinstance(other, ProcessMesh) and torch.equal(self._mesh, other._mesh) and \
+            self._dim_names == other._dim_names
+
+    def __hash__(self):
+        return hash((tuple(self.process_ids), tuple(self.shape), tuple(self._dim_names)))
+
+    def __enter__(self):
+        self._prev = _CUR["mesh"]
+        _CUR["mesh"] = self
+        return self
+
+    def __exit__(self, *exc):
+        _CUR["mesh"] = self._prev
+
+    def device_mesh(self):
+        """The torch DeviceMesh of this ProcessMesh (needs an initialised process group)."""
+        if self._device_mesh is None:
+            from torch.distributed.device_mesh import DeviceMesh
+            dev = "cuda" if torch.cuda.is_available() and dist.get_backend() == "nccl" else "cpu"
+            self._device_mesh = DeviceMesh(dev, self._mesh, mesh_dim_names=tuple(self._dim_names))
+        return self._device_mesh
+
+    def __repr__(self):
+        return f"ProcessMesh(shape={self.shape}, process_ids={self.process_ids}, dim_names={self._dim_names})"
+
+
+def get_current_process_mesh():
+    return _CUR["mesh"]
+
+
+def _placements(mesh, shard_spec, ndim):
+    from torch.distributed.tensor import Replicate, Shard
+    pl = [Replicate() for _ in range(mesh.ndim)]
+    for tdim, name in enumerate(shard_spec or [None] * ndim):
+        if name is None:
+            continue
+        md = mesh.dim_names.index(name) if isinstance(name, str) else int(name)
+        pl[md] = Shard(tdim)
+    return pl
+
+
+def _distributed():
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def shard_tensor(x, process_mesh=None, shard_spec=None):
+    """Shard ``x`` over ``process_mesh`` per ``shard_spec``. Multi-rank: returns a DTensor (each
+    rank holds its shard); single process: records the annotation on the tensor and returns it."""
+    mesh = process_mesh or get_current_process_mesh()
+    assert mesh is not None, "shard_tensor needs a process_mesh (argument or `with ProcessMesh`)"
+    if shard_spec is not None:
+        assert len(shard_spec) == x.dim(), "shard_spec needs one entry per tensor dim"
+    if not _distributed():
+        x.process_mesh, x.shard_spec = mesh, shard_spec
+        return x
+    from torch.distributed.tensor import distribute_tensor
+    dt = distribute_tensor(x.detach() if not x.requires_grad else x, mesh.device_mesh(),
+                           _placements(mesh, shard_spec, x.dim()))
+    if isinstance(x, torch.nn.Parameter):
+        return torch.nn.Parameter(dt, requires_grad=x.requires_grad)
+    return dt
+
+
+def reshard(x, process_mesh, shard_spec):
+    """Move a DTensor to another layout (RCCL all-gather / all-to-all as needed)."""
+    if not hasattr(x, "redistribute"):
+        return shard_tensor(x, process_mesh, shard_spec)
+    return x.redistribute(process_mesh.device_mesh(), _placements(process_mesh, shard_spec, x.dim()))
+
+
+def shard_op(op, process_mesh=None, in_shard_specs=None, out_shard_specs=None):
+    """Wrap ``op`` so its inputs / outputs carry the given shardings."""
+    def wrapped(*args, **kwargs):
+        mesh = process_mesh or get_current_process_mesh()
+        if in_shard_specs is not None:
+            args = tuple(shard_tensor(a, mesh, s) if isinstance(a, torch.Tensor) and s is not None else a
+                         for a, s in zip(args, list(in_shard_specs) + [None] * len(args)))
+        out = op(*args, **kwargs)
+        if out_shard_specs is not None:
+            outs = out if isinstance(out, (list, tuple)) else [out]
+            outs = [reshard(o, mesh, s) if s is not None and _distributed() else o
+                    for o, s in zip(outs, out_shard_specs)]
+            out = type(out)(outs) if isinstance(out, (list, tuple)) else outs[0]
+        return out
+    return wrapped
+
+
+def recompute(op):
+    """Activation-checkpoint ``op`` (a Layer or callable)."""
+    def wrapped(*args, **kwargs):
+        return torch.utils.checkpoint.checkpoint(op, *args, use_reentrant=False, **kwargs)
+    return wrapped
+
+
+_COLLECTION = {}
+
+
+def fetch(tensor, name=None, logging=False):
+    _COLLECTION.setdefault("fetches", []).append((name, tensor))
+    return tensor
+
+
+class _Cfg(dict):
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError as e:
+            raise AttributeError(k) from e
+
+    def __setattr__(self, k, v):
+        self[k] = v
+
+
+class Strategy:
+    """Reference `auto_parallel/strategy.py`: nested config groups (sharding, amp, recompute,
+    gradient_merge, pipeline, ...), each with ``enable`` plus options."""
+
+    def __init__(self, config=None):
+        self.auto_mode = "semi"
+        self.seed = None
+        self.split_data = True
+        self.sharding = _Cfg(enable=False, stage=1, degree=8)
+        self.amp = _Cfg(enable=False, dtype="bfloat16", level="o1", init_loss_scaling=32768.0)
+        self.recompute = _Cfg(enable=False, checkpoints=None)
+        self.gradient_merge = _Cfg(enable=False, k_steps=1, avg=True)
+        self.pipeline = _Cfg(enable=False, schedule_mode="1F1B", micro_batch_size=1,
+                             accumulate_steps=1)
+        self.fused_passes = _Cfg(enable=False, fused_passes_list=[])
+        self.dataset = _Cfg(enable=False, num_shards=1)
+        for k, v in (config or {}).items():
+            cur = getattr(self, k, None)
+            if isinstance(cur, _Cfg) and isinstance(v, dict):
+                cur.update(v)
+            else:
+                setattr(self, k, v)
+
+
+class Engine:
+    """High-level train / eval / predict driver (reference `auto_parallel/engine.py`): the model's
+    sharding comes from its ``shard_tensor`` annotations; Strategy.amp enables bf16 autocast,
+    gradient_merge accumulates ``k_steps`` micro-steps per optimizer step."""
+
+    def __init__(self, model=None, loss=None, optimizer=None, metrics=None, cluster=None,
+                 strategy=None):
+        self.model, self.loss, self.optimizer = model, loss, optimizer
+        self.metrics = list(metrics or []) if not isinstance(metrics, (list, tuple)) else list(metrics)
+        self.strategy = strategy or Strategy()
+        self.history = {"loss": []}
+
+    def _ctx(self):
+        if self.strategy.amp.enable:
+            dev = "cuda" if torch.cuda.is_available() else "cpu"
+            return torch.autocast(dev, dtype=torch.bfloat16)
+        return contextlib.nullcontext()
+
+    def _batches(self, data, batch_size):
+        from ...io import DataLoader
+        return data if not hasattr(data, "__getitem__") or isinstance(data, DataLoader) else \
+            DataLoader(data, batch_size=batch_size, shuffle=False)
+
+    @staticmethod
+    def _split(batch):
+        if isinstance(batch, (list, tuple)) and len(batch) >= 2:
+            return batch[:-1], batch[-1]
+        return (batch,), None
+
+    def fit(self, train_data, valid_data=None, train_sample_split=None, batch_size=1, epochs=1,
+            steps_per_epoch=None, log_freq=10, save_dir=None, save_freq=1, valid_sample_split=None,
+            valid_freq=1, valid_steps=None, collate_fn=None, callbacks=None, verbose=2,
+            nvprof_range=[-1, -1]):
+        self.model.train()
+        k = max(1, int(self.strategy.gradient_merge.k_steps)) if self.strategy.gradient_merge.enable else 1
+        step = 0
+        for _ in range(epochs):
+            for i, batch in enumerate(self._batches(train_data, batch_size)):
+                if steps_per_epoch is not None and i >= steps_per_epoch:
+                    break
+                ins, lab = self._split(batch)
+                with self._ctx():
+                    out = self.model(*ins)
+                    l = self.loss(out, lab) if self.loss is not None else out
+                (l / k).backward()
+                step += 1
+                if step % k == 0:
+                    self.optimizer.step()
+                    self.optimizer.clear_grad()
+                self.history["loss"].append(float(l.detach().float().mean()))
+        return self.history
+
+    @torch.no_grad()
+    def evaluate(self, valid_data, valid_sample_split=None, batch_size=1, steps=None, log_freq=10,
+                 collate_fn=None, callbacks=None, verbose=2):
+        self.model.eval()
+        losses = []
+        for m in self.metrics:
+            m.reset()
+        for i, batch in enumerate(self._batches(valid_data, batch_size)):
+            if steps is not None and i >= steps:
+                break
+            ins, lab = self._split(batch)
+            with self._ctx():
+                out = self.model(*ins)
+            if self.loss is not None and lab is not None:
+                losses.append(float(self.loss(out, lab).float().mean()))
+            for m in self.metrics:
+                m.update(*m.compute(out, lab)) if hasattr(m, "compute") else m.update(out, lab)
+        res = {"loss": sum(losses) / max(1, len(losses))} if losses else {}
+        for m in self.metrics:
+            res[m.name() if callable(getattr(m, "name", None)) else str(m)] = m.accumulate()
+        return res
+
+    @torch.no_grad()
+    def predict(self, test_data, test_sample_split=None, batch_size=1, steps=None, collate_fn=None,
+                callbacks=None, verbose=2):
+        self.model.eval()
+        outs = []
+        for i, batch in enumerate(self._batches(test_data, batch_size)):
+            if steps is not None and i >= steps:
+                break
+            ins, _ = self._split(batch) if isinstance(batch, (list, tuple)) and len(batch) > 1 else ((batch,) if not isinstance(batch, (list, tuple)) else tuple(batch), None)
+            with self._ctx():
+                outs.append(self.model(*ins))
+        return outs
+
+    def save(self, path, training=True):
+        from ...framework.io import save
+        save(self.model.state_dict(), path + ".pdparams")
+        if training and self.optimizer is not None:
+            save(self.optimizer.state_dict(), path + ".pdopt")
+
+    def load(self, path, strict=True, load_optimizer=True):
+        import os
+        from ...framework.io import load
+        self.model.set_state_dict(load(path + ".pdparams"))
+        if load_optimizer and self.optimizer is not None and os.path.exists(path + ".pdopt"):
+            self.optimizer.set_state_dict(load(path + ".pdopt"))

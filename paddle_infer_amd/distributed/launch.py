@@ -63,26 +63,85 @@ def _kill(procs):
         log.close()
 
 
+def _wait_any(procs, args, t0, watch=None):
+    """Poll workers; returns (failed_code | None, membership_changed)."""
+    while True:
+        codes = [p.poll() for p, _ in procs]
+        if any(c not in (None, 0) for c in codes):
+            return next(c for c in codes if c not in (None, 0)), False
+        if all(c == 0 for c in codes):
+            return None, False
+        if args.timeout and time.time() - t0 > args.timeout:
+            return 124, False
+        if watch is not None and watch():
+            return None, True
+        time.sleep(0.2)
+
+
+def run_elastic(args) -> int:
+    """Elastic mode (``--elastic_server host:port --np min:max``): membership in a TCPStore,
+    relaunch on every change of the live node set (see distributed/elastic.py)."""
+    from .elastic import ElasticManager, parse_np
+    lo, hi = parse_np(args.np)
+    node_id = args.node_id or f"{socket.gethostname()}-{os.getpid()}"
+    em = ElasticManager(args.elastic_server, args.job_id, node_id, lo, hi,
+                        is_master=args.elastic_master, heartbeat=args.elastic_heartbeat,
+                        ttl=args.elastic_ttl)
+    base_port = int(args.elastic_server.rsplit(":", 1)[1])
+    restarts = 0
+    try:
+        while True:
+            nodes = em.wait_for_quorum(args.elastic_wait)
+            if nodes is None:
+                print("[launch] elastic: not enough nodes before the wait timeout", file=sys.stderr)
+                return 1
+            time.sleep(args.elastic_settle)  # let simultaneous joins land in one epoch
+            nodes = em.live_nodes()
+            asg = em.assignment(nodes)
+            if asg is None:  # beyond np_max: stand by
+                time.sleep(em.heartbeat)
+                continue
+            n_nodes, node_rank = asg
+            members = nodes[:hi]
+            world = n_nodes * args.nproc_per_node
+            port = em.master_port(members, base_port)
+            os.environ["PADDLE_ELASTIC_NP"] = str(n_nodes)
+            procs = _start(args, node_rank * args.nproc_per_node, world, port, restarts)
+            print(f"[launch] elastic epoch: nodes={members} world={world} node_rank={node_rank}",
+                  file=sys.stderr)
+
+            def changed(members=members):
+                cur = em.live_nodes()[:hi]
+                return cur != members and len(cur) >= lo or len(cur) < lo
+            try:
+                failed, memb = _wait_any(procs, args, time.time(), changed)
+            finally:
+                _kill(procs)
+            if memb:
+                restarts += 1
+                print(f"[launch] elastic: membership changed -> relaunch ({restarts})", file=sys.stderr)
+                continue
+            if failed is None:
+                return 0
+            restarts += 1
+            if restarts > args.max_restart:
+                return failed
+    finally:
+        em.exit()
+
+
 def run(args) -> int:
+    if getattr(args, "elastic_server", None):
+        return run_elastic(args)
     world = args.nnodes * args.nproc_per_node
     rank_base = args.node_rank * args.nproc_per_node
     for restart in range(args.max_restart + 1):
         port = args.master_port or _free_port()
         procs = _start(args, rank_base, world, port, restart)
-        t0 = time.time()
-        failed = None
-        while True:
-            codes = [p.poll() for p, _ in procs]
-            if any(c not in (None, 0) for c in codes):
-                failed = next(c for c in codes if c not in (None, 0))
-                break
-            if all(c == 0 for c in codes):
-                break
-            if args.timeout and time.time() - t0 > args.timeout:
-                failed = 124
-                break
-            time.sleep(0.2)
-        _kill(procs)
+        try:
+            failed, _ = _wait_any(procs, args, time.time())
+        finally:
+            _kill(procs)
         if failed is None:
             return 0
         print(f"[launch] a worker failed (exit {failed}); restart {restart + 1}/{args.max_restart}",
@@ -101,9 +160,24 @@ def main(argv=None):
     ap.add_argument("--log_dir", default="log")
     ap.add_argument("--max_restart", type=int, default=0)
     ap.add_argument("--timeout", type=float, default=0.0)
+    # elastic (reference fleet/elastic): membership in a TCPStore at --elastic_server
+    ap.add_argument("--elastic_server", default="")
+    ap.add_argument("--elastic_master", action="store_true",
+                    help="host the membership TCPStore in this launcher")
+    ap.add_argument("--np", default="", help="elastic node range 'min:max'")
+    ap.add_argument("--job_id", default="default")
+    ap.add_argument("--node_id", default="")
+    ap.add_argument("--elastic_heartbeat", type=float, default=1.0)
+    ap.add_argument("--elastic_ttl", type=float, default=4.0)
+    ap.add_argument("--elastic_wait", type=float, default=120.0)
+    ap.add_argument("--elastic_settle", type=float, default=1.0)
     ap.add_argument("training_script")
     ap.add_argument("training_script_args", nargs=argparse.REMAINDER)
     args = ap.parse_args(argv)
+
+    def _term(signum, frame):  # run the finally blocks: stop workers, leave the elastic job
+        raise SystemExit(128 + signum)
+    signal.signal(signal.SIGTERM, _term)
     sys.exit(run(args))
 
 

@@ -282,3 +282,48 @@ def test_checkpoint_tensor_parallel_reshard(tmp_path):
         ck.load_state_dict({"col": sa, "row": sb}, path)
         torch.testing.assert_close(sa.local.view(6, 2, 4), g.chunk(4, dim=1)[r])
         torch.testing.assert_close(sb.local.view(6, 8, 1), g.chunk(4, dim=2)[r])
+
+
+def _auto_parallel_worker(rank, world):
+    import torch
+    import paddle_infer_amd.distributed as pd
+    from paddle_infer_amd.distributed.communication import stream
+    torch.manual_seed(0)
+    full_w = torch.randn(8, 6)
+    x = torch.randn(3, 8)
+    mesh = pd.ProcessMesh([0, 1], ["mp"])
+    w = pd.shard_tensor(full_w, mesh, [None, "mp"])  # column split
+    local = w.to_local()
+    y = torch.nn.functional.linear(x, full_w.t()[rank * 3:(rank + 1) * 3])
+    back = pd.reshard(w, mesh, [None, None]).to_local()
+    t = torch.full((2,), float(rank + 1))
+    stream.all_reduce(t, use_calc_stream=True)
+    g = torch.zeros(4)
+    stream.all_gather(g, torch.full((2,), float(rank)))
+    return {"local": local, "ref_cols": full_w[:, rank * 3:(rank + 1) * 3], "y": y,
+            "back": back, "full": full_w, "ar": t, "ag": g}
+
+
+def test_auto_parallel_shard_tensor_and_stream_collectives():
+    res = run_distributed(_auto_parallel_worker, 2)
+    for r in res.values():
+        assert torch.allclose(r["local"], r["ref_cols"])
+        assert torch.allclose(r["back"], r["full"])
+        assert torch.equal(r["ar"], torch.full((2,), 3.0))
+        assert torch.equal(r["ag"], torch.tensor([0.0, 0.0, 1.0, 1.0]))
+
+
+def test_auto_parallel_engine_single_process():
+    import paddle_infer_amd as paddle
+    from paddle_infer_amd.distributed.auto_parallel import Engine, Strategy
+    torch.manual_seed(0)
+    model = paddle.nn.Linear(4, 1)
+    opt = paddle.optimizer.SGD(0.1, parameters=model.parameters())
+    X = torch.randn(64, 4)
+    Y = X @ torch.tensor([[1.0], [-2.0], [0.5], [3.0]])
+    data = paddle.io.TensorDataset([X, Y])
+    st = Strategy({"gradient_merge": {"enable": True, "k_steps": 2}})
+    eng = Engine(model, paddle.nn.MSELoss(), opt, strategy=st)
+    hist = eng.fit(data, batch_size=8, epochs=20)
+    assert hist["loss"][-1] < hist["loss"][0] * 0.1
+    assert eng.evaluate(data, batch_size=16)["loss"] < hist["loss"][0] * 0.1

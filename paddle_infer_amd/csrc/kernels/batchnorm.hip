@@ -1,0 +1,373 @@
+// Batch normalisation fused with the residual add and the activation (training and inference),
+// NCHW and NHWC (channels-last) layouts, bf16 / f32 I/O with f32 statistics.
+//
+// Parity: reference `phi/kernels/gpu/batch_norm_kernel.cu` / `batch_norm_grad_kernel.cu`,
+// `fluid/operators/fused/fused_bn_activation_op.cu` (bn + relu) and
+// `fused_bn_add_activation_op.cu` (bn + residual add + relu, ResNet bottleneck tail).
+//
+// MI355X design: one pass for the statistics (per-thread Welford, workgroup merge, per-block
+// partials [P][C] in HBM merged per channel with Chan's formula — exact for ResNet-scale N·H·W,
+// no E[x²]-E[x]² cancellation), one fused normalise + add + act pass; backward = one reduction
+// pass (Σ dz, Σ dz·x̂ with dz = dy ⊙ act'(y) read from the saved OUTPUT, so the residual is not
+// needed) and one elementwise pass producing dx (and dz = d residual). Running statistics are
+// updated on the device (no host sync). NCHW blocks walk one channel plane (coalesced along H·W);
+// NHWC blocks walk rows with the lanes across channels.
+#include "common.h"
+#include <float.h>
+
+namespace {
+
+template <typename T> struct V;
+template <> struct V<float> {
+  static __device__ __forceinline__ float ld(const float* p) { return *p; }
+  static __device__ __forceinline__ void st(float* p, float v) { *p = v; }
+};
+template <> struct V<bf16_t> {
+  static __device__ __forceinline__ float ld(const bf16_t* p) { return bf2f(*p); }
+  static __device__ __forceinline__ void st(bf16_t* p, float v) { *p = f2bf(v); }
+};
+
+__device__ __forceinline__ void welford_merge(float& n, float& m, float& m2, float nb, float mb,
+                                              float m2b) {
+  if (nb == 0.f) return;
+  const float nn = n + nb, d = mb - m;
+  m += d * nb / nn;
+  m2 += m2b + d * d * n * nb / nn;
+  n = nn;
+}
+
+__device__ __forceinline__ void welford_add(float& n, float& m, float& m2, float v) {
+  n += 1.f;
+  const float d = v - m;
+  m += d / n;
+  m2 += d * (v - m);
+}
+
+// ------------------------------------------------------------------------ statistics (Welford)
+// NCHW: grid (C, P); block b of channel c covers elements [b*chunk, (b+1)*chunk) of the N·S
+// sequence of channel c. part: [3][P][C] (count, mean, M2).
+template <typename T>
+__global__ __launch_bounds__(256) void bn_stats_nchw(const T* __restrict__ x, int N, int C, int S,
+                                                     long long chunk, float* __restrict__ part) {
+  const int c = blockIdx.x, b = blockIdx.y, P = gridDim.y;
+  const long long M = (long long)N * S;
+  const long long beg = b * chunk, end = min(M, beg + chunk);
+  float n = 0.f, m = 0.f, m2 = 0.f;
+  for (long long i = beg + threadIdx.x; i < end; i += 256)
+    welford_add(n, m, m2, V<T>::ld(x + (i / S * C + c) * (long long)S + i % S));
+  __shared__ float sn[256], sm[256], sm2[256];
+  sn[threadIdx.x] = n; sm[threadIdx.x] = m; sm2[threadIdx.x] = m2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      float a = sn[threadIdx.x], am = sm[threadIdx.x], am2 = sm2[threadIdx.x];
+      welford_merge(a, am, am2, sn[threadIdx.x + o], sm[threadIdx.x + o], sm2[threadIdx.x + o]);
+      sn[threadIdx.x] = a; sm[threadIdx.x] = am; sm2[threadIdx.x] = am2;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    part[(0 * P + b) * C + c] = sn[0];
+    part[(1 * P + b) * C + c] = sm[0];
+    part[(2 * P + b) * C + c] = sm2[0];
+  }
+}
+
+// NHWC: x [M][C]; grid (P). C ≥ 256: thread t owns channels t, t+256, …; C < 256 (C | 256):
+// thread t owns channel t % C on rows t / C + k·(256 / C).
+template <typename T>
+__global__ __launch_bounds__(256) void bn_stats_nhwc(const T* __restrict__ x, long long M, int C,
+                                                     long long chunk, float* __restrict__ part) {
+  const int b = blockIdx.x, P = gridDim.x, t = threadIdx.x;
+  const long long beg = b * chunk, end = min(M, beg + chunk);
+  __shared__ float sn[256], sm[256], sm2[256];
+  if (C >= 256) {
+    for (int c = t; c < C; c += 256) {
+      float n = 0.f, m = 0.f, m2 = 0.f;
+      for (long long r = beg; r < end; ++r) welford_add(n, m, m2, V<T>::ld(x + r * C + c));
+      part[(0 * P + b) * C + c] = n;
+      part[(1 * P + b) * C + c] = m;
+      part[(2 * P + b) * C + c] = m2;
+    }
+    return;
+  }
+  const int rpi = 256 / C, c = t % C, r0 = t / C;
+  float n = 0.f, m = 0.f, m2 = 0.f;
+  for (long long r = beg + r0; r < end; r += rpi) welford_add(n, m, m2, V<T>::ld(x + r * C + c));
+  sn[t] = n; sm[t] = m; sm2[t] = m2;
+  __syncthreads();
+  if (t < C) {
+    for (int k = 1; k < rpi; ++k) welford_merge(n, m, m2, sn[t + k * C], sm[t + k * C], sm2[t + k * C]);
+    part[(0 * P + b) * C + c] = n;
+    part[(1 * P + b) * C + c] = m;
+    part[(2 * P + b) * C + c] = m2;
+  }
+}
+
+// per channel: merge partials → mean / rstd (saved for backward), running stats update, and the
+// affine fold scale = γ·rstd, shift = β − mean·scale.
+__global__ void bn_finalize(const float* __restrict__ part, int P, int C, float eps, float momentum,
+                            const float* __restrict__ gamma, const float* __restrict__ beta,
+                            float* __restrict__ run_mean, float* __restrict__ run_var,
+                            float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                            float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float n = 0.f, m = 0.f, m2 = 0.f;
+  for (int b = 0; b < P; ++b)
+    welford_merge(n, m, m2, part[(0 * P + b) * C + c], part[(1 * P + b) * C + c],
+                  part[(2 * P + b) * C + c]);
+  const float var = n > 0.f ? m2 / n : 0.f;
+  const float rstd = rsqrtf(var + eps);
+  mean_out[c] = m;
+  rstd_out[c] = rstd;
+  if (run_mean) {  // Paddle: running = momentum·running + (1 − momentum)·batch (unbiased var)
+    run_mean[c] = momentum * run_mean[c] + (1.f - momentum) * m;
+    run_var[c] = momentum * run_var[c] + (1.f - momentum) * (n > 1.f ? m2 / (n - 1.f) : var);
+  }
+  const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  scale[c] = g * rstd;
+  shift[c] = bt - m * g * rstd;
+}
+
+// inference fold from the running statistics (rstd_out for the backward)
+__global__ void bn_fold(int C, float eps, const float* __restrict__ gamma,
+                        const float* __restrict__ beta, const float* __restrict__ run_mean,
+                        const float* __restrict__ run_var, float* __restrict__ scale,
+                        float* __restrict__ shift, float* __restrict__ mean_out,
+                        float* __restrict__ rstd_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float rstd = rsqrtf(run_var[c] + eps);
+  const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  scale[c] = g * rstd;
+  shift[c] = bt - run_mean[c] * g * rstd;
+  if (mean_out) mean_out[c] = run_mean[c];
+  if (rstd_out) rstd_out[c] = rstd;
+}
+
+__device__ __forceinline__ float bn_act(float z, int act) {
+  return act == 1 ? fmaxf(z, 0.f) : act == 2 ? fminf(fmaxf(z, 0.f), 6.f) : z;
+}
+
+// y = act(x·scale[c] + shift[c] (+ res)); channel of element i: nchw → (i / S) % C, nhwc → i % C
+template <typename T>
+__global__ __launch_bounds__(256) void bn_apply(const T* __restrict__ x, const T* __restrict__ res,
+                                                const float* __restrict__ scale,
+                                                const float* __restrict__ shift, T* __restrict__ y,
+                                                long long total, int C, int S, int nhwc, int act) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = nhwc ? (int)(i % C) : (int)((i / S) % C);
+    float z = V<T>::ld(x + i) * scale[c] + shift[c];
+    if (res) z += V<T>::ld(res + i);
+    V<T>::st(y + i, bn_act(z, act));
+  }
+}
+
+// ------------------------------------------------------------------------ backward
+// dz = dy ⊙ act'(y) with y the forward output
+template <typename T>
+__device__ __forceinline__ float dz_of(const T* dy, const T* y, long long i, int act) {
+  const float g = V<T>::ld(dy + i);
+  if (act == 0) return g;
+  const float yv = V<T>::ld(y + i);
+  return (act == 1 ? yv > 0.f : (yv > 0.f && yv < 6.f)) ? g : 0.f;
+}
+
+// partials of Σ dz and Σ dz·x̂ per channel: part [2][P][C]
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_nchw(const T* __restrict__ dy,
+                                                          const T* __restrict__ y,
+                                                          const T* __restrict__ x,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ rstd, int N,
+                                                          int C, int S, long long chunk, int act,
+                                                          float* __restrict__ part) {
+  const int c = blockIdx.x, b = blockIdx.y, P = gridDim.y;
+  const long long M = (long long)N * S, beg = b * chunk, end = min(M, beg + chunk);
+  const float mu = mean[c], rs = rstd[c];
+  float s1 = 0.f, s2 = 0.f;
+  for (long long i = beg + threadIdx.x; i < end; i += 256) {
+    const long long idx = (i / S * C + c) * (long long)S + i % S;
+    const float dz = dz_of(dy, y, idx, act);
+    s1 += dz;
+    s2 += dz * (V<T>::ld(x + idx) - mu) * rs;
+  }
+  __shared__ float r[2][4];
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  if ((threadIdx.x & 63) == 0) { r[0][threadIdx.x >> 6] = s1; r[1][threadIdx.x >> 6] = s2; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[(0 * P + b) * C + c] = r[0][0] + r[0][1] + r[0][2] + r[0][3];
+    part[(1 * P + b) * C + c] = r[1][0] + r[1][1] + r[1][2] + r[1][3];
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_nhwc(const T* __restrict__ dy,
+                                                          const T* __restrict__ y,
+                                                          const T* __restrict__ x,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ rstd,
+                                                          long long M, int C, long long chunk,
+                                                          int act, float* __restrict__ part) {
+  const int b = blockIdx.x, P = gridDim.x, t = threadIdx.x;
+  const long long beg = b * chunk, end = min(M, beg + chunk);
+  __shared__ float r1[256], r2[256];
+  if (C >= 256) {
+    for (int c = t; c < C; c += 256) {
+      const float mu = mean[c], rs = rstd[c];
+      float s1 = 0.f, s2 = 0.f;
+      for (long long rr = beg; rr < end; ++rr) {
+        const long long idx = rr * C + c;
+        const float dz = dz_of(dy, y, idx, act);
+        s1 += dz;
+        s2 += dz * (V<T>::ld(x + idx) - mu) * rs;
+      }
+      part[(0 * P + b) * C + c] = s1;
+      part[(1 * P + b) * C + c] = s2;
+    }
+    return;
+  }
+  const int rpi = 256 / C, c = t % C, r0 = t / C;
+  const float mu = mean[c], rs = rstd[c];
+  float s1 = 0.f, s2 = 0.f;
+  for (long long rr = beg + r0; rr < end; rr += rpi) {
+    const long long idx = rr * C + c;
+    const float dz = dz_of(dy, y, idx, act);
+    s1 += dz;
+    s2 += dz * (V<T>::ld(x + idx) - mu) * rs;
+  }
+  r1[t] = s1; r2[t] = s2;
+  __syncthreads();
+  if (t < C) {
+    for (int k = 1; k < rpi; ++k) { s1 += r1[t + k * C]; s2 += r2[t + k * C]; }
+    part[(0 * P + b) * C + c] = s1;
+    part[(1 * P + b) * C + c] = s2;
+  }
+}
+
+// per channel: dβ = Σdz, dγ = Σ dz·x̂ (f32), plus the coefficients of the dx pass
+__global__ void bn_bwd_finalize(const float* __restrict__ part, int P, int C, float M,
+                                const float* __restrict__ gamma, const float* __restrict__ rstd,
+                                float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s1 = 0.f, s2 = 0.f;
+  for (int b = 0; b < P; ++b) { s1 += part[(0 * P + b) * C + c]; s2 += part[(1 * P + b) * C + c]; }
+  if (dbeta) dbeta[c] = s1;
+  if (dgamma) dgamma[c] = s2;
+  const float g = gamma ? gamma[c] : 1.f;
+  coef[c] = g * rstd[c];  // dx = coef·(dz − s1/M − x̂·s2/M)
+  coef[C + c] = s1 / M;
+  coef[2 * C + c] = s2 / M;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_apply(const T* __restrict__ dy, const T* __restrict__ y,
+                                                    const T* __restrict__ x,
+                                                    const float* __restrict__ mean,
+                                                    const float* __restrict__ rstd,
+                                                    const float* __restrict__ coef, T* __restrict__ dx,
+                                                    T* __restrict__ dres, long long total, int C,
+                                                    int S, int nhwc, int act, int training) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = nhwc ? (int)(i % C) : (int)((i / S) % C);
+    const float dz = dz_of(dy, y, i, act);
+    if (dres) V<T>::st(dres + i, dz);
+    float v;
+    if (training) {
+      const float xh = (V<T>::ld(x + i) - mean[c]) * rstd[c];
+      v = coef[c] * (dz - coef[C + c] - xh * coef[2 * C + c]);
+    } else {
+      v = coef[c] * dz;  // running statistics are constants
+    }
+    V<T>::st(dx + i, v);
+  }
+}
+
+int parts_for(long long M) {
+  long long p = (M + 4095) / 4096;
+  return (int)(p < 1 ? 1 : (p > 512 ? 512 : p));
+}
+
+}  // namespace
+
+// Forward. x/res/y: [N, C, S] (nhwc = 0) or [N·S, C] (nhwc = 1); dtype 0 = f32, 1 = bf16.
+// training: statistics of x → mean/rstd (f32 [C], saved for backward), running stats updated in
+// place (momentum: Paddle convention); else the running statistics (mean/rstd still written).
+// ws: f32 workspace of ≥ 2·C + 3·512·C floats. act: 0 none, 1 relu, 2 relu6.
+// nhwc requires C ≥ 256 or C | 256.
+PIAMD_EXPORT int piamd_bn_fwd(int dtype, int nhwc, const void* x, const void* res, void* y, int N,
+                              int C, int S, const float* gamma, const float* beta,
+                              float* run_mean, float* run_var, float* mean, float* rstd,
+                              float momentum, float eps, int training, int act, float* ws,
+                              hipStream_t st) {
+  if (C < 1 || N < 1 || S < 1 || (nhwc && C < 256 && 256 % C)) return (int)hipErrorInvalidValue;
+  const long long M = (long long)N * S, total = M * C;
+  float* scale = ws;
+  float* shift = ws + C;
+  if (training) {
+    const int P = parts_for(M);
+    const long long chunk = (M + P - 1) / P;
+    float* part = ws + 2 * C;
+    if (nhwc) {
+      if (dtype) hipLaunchKernelGGL(bn_stats_nhwc<bf16_t>, dim3(P), dim3(256), 0, st, (const bf16_t*)x, M, C, chunk, part);
+      else hipLaunchKernelGGL(bn_stats_nhwc<float>, dim3(P), dim3(256), 0, st, (const float*)x, M, C, chunk, part);
+    } else {
+      if (dtype) hipLaunchKernelGGL(bn_stats_nchw<bf16_t>, dim3(C, P), dim3(256), 0, st, (const bf16_t*)x, N, C, S, chunk, part);
+      else hipLaunchKernelGGL(bn_stats_nchw<float>, dim3(C, P), dim3(256), 0, st, (const float*)x, N, C, S, chunk, part);
+    }
+    hipLaunchKernelGGL(bn_finalize, dim3((C + 255) / 256), dim3(256), 0, st, part, P, C, eps,
+                       momentum, gamma, beta, run_mean, run_var, mean, rstd, scale, shift);
+  } else {
+    hipLaunchKernelGGL(bn_fold, dim3((C + 255) / 256), dim3(256), 0, st, C, eps, gamma, beta,
+                       run_mean, run_var, scale, shift, mean, rstd);
+  }
+  const dim3 g(stride_grid(total, 256));
+  if (dtype)
+    hipLaunchKernelGGL(bn_apply<bf16_t>, g, dim3(256), 0, st, (const bf16_t*)x, (const bf16_t*)res,
+                       scale, shift, (bf16_t*)y, total, C, S, nhwc, act);
+  else
+    hipLaunchKernelGGL(bn_apply<float>, g, dim3(256), 0, st, (const float*)x, (const float*)res,
+                       scale, shift, (float*)y, total, C, S, nhwc, act);
+  return (int)hipGetLastError();
+}
+
+// Backward. y = the forward OUTPUT (act' from it); dres (nullable) receives dz = ∂L/∂(bn + res).
+// training = 0: the statistics are constants (dx = γ·rstd·dz). dgamma / dbeta: f32 [C]
+// (nullable). ws: ≥ 3·C + 2·512·C floats.
+PIAMD_EXPORT int piamd_bn_bwd(int dtype, int nhwc, const void* dy, const void* y, const void* x,
+                              void* dx, void* dres, int N, int C, int S, const float* gamma,
+                              const float* mean, const float* rstd, float* dgamma, float* dbeta,
+                              int training, int act, float* ws, hipStream_t st) {
+  if (C < 1 || N < 1 || S < 1 || (nhwc && C < 256 && 256 % C)) return (int)hipErrorInvalidValue;
+  const long long M = (long long)N * S, total = M * C;
+  const int P = parts_for(M);
+  const long long chunk = (M + P - 1) / P;
+  float* coef = ws;
+  float* part = ws + 3 * C;
+  if (nhwc) {
+    if (dtype) hipLaunchKernelGGL(bn_bwd_reduce_nhwc<bf16_t>, dim3(P), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x, mean, rstd, M, C, chunk, act, part);
+    else hipLaunchKernelGGL(bn_bwd_reduce_nhwc<float>, dim3(P), dim3(256), 0, st, (const float*)dy, (const float*)y, (const float*)x, mean, rstd, M, C, chunk, act, part);
+  } else {
+    if (dtype) hipLaunchKernelGGL(bn_bwd_reduce_nchw<bf16_t>, dim3(C, P), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x, mean, rstd, N, C, S, chunk, act, part);
+    else hipLaunchKernelGGL(bn_bwd_reduce_nchw<float>, dim3(C, P), dim3(256), 0, st, (const float*)dy, (const float*)y, (const float*)x, mean, rstd, N, C, S, chunk, act, part);
+  }
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 255) / 256), dim3(256), 0, st, part, P, C,
+                     (float)M, gamma, rstd, dgamma, dbeta, coef);
+  const dim3 g(stride_grid(total, 256));
+  if (dtype)
+    hipLaunchKernelGGL(bn_bwd_apply<bf16_t>, g, dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)y,
+                       (const bf16_t*)x, mean, rstd, coef, (bf16_t*)dx, (bf16_t*)dres, total, C, S,
+                       nhwc, act, training);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply<float>, g, dim3(256), 0, st, (const float*)dy, (const float*)y,
+                       (const float*)x, mean, rstd, coef, (float*)dx, (float*)dres, total, C, S,
+                       nhwc, act, training);
+  return (int)hipGetLastError();
+}

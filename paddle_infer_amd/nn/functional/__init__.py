@@ -265,12 +265,26 @@ def rms_norm(x, weight=None, epsilon=1e-6, name=None):
 
 
 def batch_norm(x, running_mean, running_var, weight=None, bias=None, training=False,
-               momentum=0.9, epsilon=1e-5, data_format="NCHW", use_global_stats=None, name=None):
+               momentum=0.9, epsilon=1e-5, data_format="NCHW", use_global_stats=None, name=None,
+               act=None, residual=None):
+    """Reference `nn/functional/norm.py:batch_norm`; on the GPU the fused HIP kernel
+    (``ops.batchnorm``: statistics + normalise (+ residual) (+ relu/relu6) in two passes)."""
     if use_global_stats:
         training = False
+    if x.is_cuda and act in (None, "relu", "relu6") and x.dim() >= 2:
+        from ...ops.batchnorm import batch_norm_act
+        return batch_norm_act(x, running_mean, running_var, weight, bias, training, momentum,
+                              epsilon, act or "none", residual, data_format)
     y = TF.batch_norm(_fmt_in(x, data_format), running_mean, running_var, weight, bias, training,
                       1.0 - momentum, epsilon)
-    return _fmt_out(y, data_format)
+    y = _fmt_out(y, data_format)
+    if residual is not None:
+        y = y + residual
+    if act == "relu":
+        y = torch.relu(y)
+    elif act == "relu6":
+        y = torch.clamp(y, 0.0, 6.0)
+    return y
 
 
 def instance_norm(x, running_mean=None, running_var=None, weight=None, bias=None,

@@ -433,10 +433,13 @@ class _BatchNormBase(Layer):
         self.register_buffer("_mean", torch.zeros(num_features))
         self.register_buffer("_variance", torch.ones(num_features))
 
-    def forward(self, x):
+    def forward(self, x, residual=None, act=None):
+        """``act(BN(x) + residual)``; ``residual`` / ``act`` (relu, relu6) fuse the ResNet-style
+        tail into the normalisation pass on the GPU."""
         train = self.training and not self.use_global_stats
         return F.batch_norm(x, self._mean, self._variance, self.weight, self.bias, train,
-                            self.momentum, self.epsilon, self.data_format)
+                            self.momentum, self.epsilon, self.data_format, act=act,
+                            residual=residual)
 
 
 class BatchNorm1D(_BatchNormBase):
@@ -464,8 +467,9 @@ class BatchNorm(_BatchNormBase):
         self.act = act
 
     def forward(self, x):
-        y = super().forward(x)
-        return getattr(F, self.act)(y) if self.act else y
+        if self.act in (None, "relu", "relu6"):
+            return super().forward(x, act=self.act)
+        return getattr(F, self.act)(super().forward(x))
 
 
 class SyncBatchNorm(_BatchNormBase):

@@ -189,3 +189,10 @@ _SIGS["piamd_gemm_i8"] = [c_void_p, c_ll, c_void_p, c_ll, c_void_p, c_float, c_v
                           c_void_p, c_ll, c_int, c_int, c_int, c_int, c_void_p]
 _SIGS["piamd_quant_rows"] = [c_void_p, c_ll, c_void_p, c_ll, c_void_p, c_float, c_int, c_int,
                              c_void_p]
+# dtype, nhwc, x, res, y, N, C, S, gamma, beta, run_mean, run_var, mean, rstd, momentum, eps,
+# training, act, ws, stream
+_SIGS["piamd_bn_fwd"] = ([c_int, c_int] + [c_void_p] * 3 + [c_int] * 3 + [c_void_p] * 6
+                         + [c_float, c_float, c_int, c_int, c_void_p, c_void_p])
+# dtype, nhwc, dy, y, x, dx, dres, N, C, S, gamma, mean, rstd, dgamma, dbeta, training, act, ws, stream
+_SIGS["piamd_bn_bwd"] = ([c_int, c_int] + [c_void_p] * 5 + [c_int] * 3 + [c_void_p] * 5
+                         + [c_int, c_int, c_void_p, c_void_p])

@@ -1,0 +1,122 @@
+"""Fused BatchNorm (+ residual add) (+ ReLU / ReLU6) — ``csrc/kernels/batchnorm.hip``.
+
+Parity: reference `phi/kernels/gpu/batch_norm_kernel.cu`, `fused_bn_activation_op.cu`,
+`fused_bn_add_activation_op.cu`. ``batch_norm_act(x, …, act, residual)`` computes
+``act(BN(x) + residual)`` in one normalise pass after one statistics pass (training) or in a single
+pass from the running statistics (eval); the backward reads the saved output for act' (the
+residual itself is not kept) and returns the residual's gradient from the same pass.
+NCHW and NHWC (``data_format`` "NHWC"/"NLC" or a channels_last tensor) layouts, f32 / bf16.
+Running statistics are updated in place on the device with Paddle's momentum convention
+(running = momentum·running + (1 − momentum)·batch). CPU tensors run the PyTorch reference.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as TF
+
+from . import _lib
+
+_ACT = {"none": 0, None: 0, "identity": 0, "relu": 1, "relu6": 2}
+
+
+def _layout(x, data_format):
+    """(nhwc, N, C, S) for a [N, C, *spatial] (NCHW) or channels-last / NHWC tensor."""
+    if data_format in ("NHWC", "NLC", "NDHWC"):
+        N, C = x.shape[0], x.shape[-1]
+        return True, N, C, x.numel() // (N * C)
+    N, C = x.shape[0], x.shape[1]
+    S = x.numel() // (N * C)
+    if x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous():
+        return True, N, C, S
+    return False, N, C, S
+
+
+def _supported(x, nhwc, C):
+    if not (x.is_cuda and x.dtype in (torch.float32, torch.bfloat16)):
+        return False
+    return not nhwc or C >= 256 or 256 % C == 0
+
+
+def _reference(x, running_mean, running_var, weight, bias, training, momentum, eps, act,
+               residual, data_format):
+    nhwc = data_format in ("NHWC", "NLC", "NDHWC")
+    xin = x.movedim(-1, 1) if nhwc else x
+    y = TF.batch_norm(xin, running_mean, running_var, weight, bias, training, 1.0 - momentum, eps)
+    y = y.movedim(1, -1) if nhwc else y
+    if residual is not None:
+        y = y + residual
+    if act == 1:
+        y = torch.relu(y)
+    elif act == 2:
+        y = torch.clamp(y, 0.0, 6.0)
+    return y
+
+
+class _BNAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, training, momentum,
+                eps, act, nhwc, dims):
+        N, C, S = dims
+        xc = x if (nhwc and not x.is_contiguous() and x.dim() == 4) else x.contiguous()
+        if nhwc and x.dim() == 4 and not x.is_contiguous():  # channels_last NCHW view → [N,H,W,C]
+            xc = x.permute(0, 2, 3, 1).contiguous()
+        res = None
+        if residual is not None:
+            res = residual.permute(0, 2, 3, 1).contiguous() if (nhwc and residual.dim() == 4 and
+                                                                 residual.shape[1] == C and
+                                                                 not residual.is_contiguous()) \
+                else residual.contiguous()
+        dev = x.device
+        g = weight.float().contiguous() if weight is not None else None
+        b = bias.float().contiguous() if bias is not None else None
+        mean = torch.empty(C, device=dev, dtype=torch.float32)
+        rstd = torch.empty(C, device=dev, dtype=torch.float32)
+        ws = torch.empty(2 * C + 3 * 512 * C, device=dev, dtype=torch.float32)
+        y = torch.empty_like(xc)
+        rm = running_mean if running_mean is not None and running_mean.dtype == torch.float32 else None
+        rv = running_var if running_var is not None and running_var.dtype == torch.float32 else None
+        if not training and (rm is None or rv is None):
+            raise ValueError("eval-mode batch_norm needs f32 running statistics")
+        _lib.call("piamd_bn_fwd", int(x.dtype == torch.bfloat16), int(nhwc), xc.data_ptr(),
+                  _lib.ptr(res), y.data_ptr(), N, C, S, _lib.ptr(g), _lib.ptr(b), _lib.ptr(rm),
+                  _lib.ptr(rv), mean.data_ptr(), rstd.data_ptr(), float(momentum), float(eps),
+                  int(training), int(act), ws.data_ptr(), _lib.stream())
+        ctx.save_for_backward(xc, y, g, mean, rstd)
+        ctx.meta = (training, act, nhwc, dims, residual is not None, weight, bias,
+                    x.dim() == 4 and nhwc and not x.is_contiguous())
+        if ctx.meta[-1]:
+            return y.permute(0, 3, 1, 2)  # back to the caller's NCHW (channels_last) view
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, y, g, mean, rstd = ctx.saved_tensors
+        training, act, nhwc, (N, C, S), has_res, weight, bias, cl_view = ctx.meta
+        dyc = dy.permute(0, 2, 3, 1).contiguous() if cl_view else dy.contiguous()
+        dx = torch.empty_like(xc)
+        dres = torch.empty_like(xc) if has_res else None
+        dg = torch.empty(C, device=xc.device, dtype=torch.float32)
+        db = torch.empty(C, device=xc.device, dtype=torch.float32)
+        ws = torch.empty(3 * C + 2 * 512 * C, device=xc.device, dtype=torch.float32)
+        _lib.call("piamd_bn_bwd", int(xc.dtype == torch.bfloat16), int(nhwc), dyc.data_ptr(),
+                  y.data_ptr(), xc.data_ptr(), dx.data_ptr(), _lib.ptr(dres), N, C, S, _lib.ptr(g),
+                  mean.data_ptr(), rstd.data_ptr(), dg.data_ptr(), db.data_ptr(), int(training),
+                  int(act), ws.data_ptr(), _lib.stream())
+        if cl_view:
+            dx = dx.permute(0, 3, 1, 2)
+            dres = dres.permute(0, 3, 1, 2) if dres is not None else None
+        gw = dg.to(weight.dtype) if weight is not None and ctx.needs_input_grad[1] else None
+        gb = db.to(bias.dtype) if bias is not None and ctx.needs_input_grad[2] else None
+        return dx, gw, gb, dres, None, None, None, None, None, None, None, None
+
+
+def batch_norm_act(x, running_mean, running_var, weight=None, bias=None, training=False,
+                   momentum=0.9, epsilon=1e-5, act="none", residual=None, data_format="NCHW"):
+    """``act(batch_norm(x) + residual)`` (Paddle momentum convention)."""
+    a = _ACT[act]
+    nhwc, N, C, S = _layout(x, data_format)
+    if not _supported(x, nhwc, C) or (residual is not None and residual.shape != x.shape):
+        return _reference(x, running_mean, running_var, weight, bias, training, momentum, epsilon,
+                          a, residual, data_format)
+    return _BNAct.apply(x, weight, bias, residual, running_mean, running_var, bool(training),
+                        momentum, epsilon, a, nhwc, (N, C, S))

@@ -135,9 +135,8 @@ class BasicBlock(nn.Layer):
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
-        return self.relu(out + idt)
+        out = self.bn1(self.conv1(x), act="relu")                 # fused BN + ReLU
+        return self.bn2(self.conv2(out), residual=idt, act="relu")  # fused BN + add + ReLU
 
 
 class BottleneckBlock(nn.Layer):
@@ -159,10 +158,9 @@ class BottleneckBlock(nn.Layer):
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
-        out = self.bn3(self.conv3(out))
-        return self.relu(out + idt)
+        out = self.bn1(self.conv1(x), act="relu")
+        out = self.bn2(self.conv2(out), act="relu")
+        return self.bn3(self.conv3(out), residual=idt, act="relu")  # fused BN + add + ReLU
 
 
 class ResNet(nn.Layer):
@@ -198,7 +196,7 @@ class ResNet(nn.Layer):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(self.bn1(self.conv1(x), act="relu"))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         if self.with_pool:
             x = self.avgpool(x)

@@ -447,6 +447,9 @@ __device__ __forceinline__ float act_apply(float v, int act) {
 }
 
 // grid (N/32, ceil(M/32), KS); 256 threads = 4 waves splitting the k-blocks of this WG's K range.
+#ifndef WO_UNROLL
+#define WO_UNROLL 8  // k-blocks per wave per iteration: 8 x 16 B weight loads in flight per lane
+#endif
 template <int BITS>
 __global__ __launch_bounds__(256) void wo_gemm_kernel(
     const bf16_t* __restrict__ x, long long ldx, const unsigned char* __restrict__ wp,
@@ -485,17 +488,26 @@ __global__ __launch_bounds__(256) void wo_gemm_kernel(
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  constexpr int U = 4;
-  for (int kb0 = kb_beg + w; kb0 < kb_end; kb0 += 4 * U) {
-    uint4 wv[U];
-    bf16x8 xa[U][NMF];
+  constexpr int U = BITS == 16 ? WO_UNROLL : (BITS == 8 ? WO_UNROLL / 2 : WO_UNROLL / 4);
+  // software pipeline: the next group's weight / activation loads are issued before this group's
+  // MFMAs, so each lane keeps 2·U 16-B weight loads in flight (the GEMV is an HBM stream)
+  uint4 wv[U];
+  bf16x8 xa[U][NMF];
+  auto load_group = [&](int kb0, uint4 (&wd)[U], bf16x8 (&xd)[U][NMF]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int kb = min(kb0 + 4 * u, kb_end - 1);
-      wv[u] = wt[(long long)kb * 64];
+      wd[u] = wt[(long long)kb * 64];
 #pragma unroll
-      for (int i = 0; i < NMF; ++i) xa[u][i] = *(const bf16x8*)(xr + (long long)kb * KB + 8 * i);
+      for (int i = 0; i < NMF; ++i) xd[u][i] = *(const bf16x8*)(xr + (long long)kb * KB + 8 * i);
     }
+  };
+  if (kb_beg + w < kb_end) load_group(kb_beg + w, wv, xa);
+  for (int kb0 = kb_beg + w; kb0 < kb_end; kb0 += 4 * U) {
+    uint4 wn[U];
+    bf16x8 xn[U][NMF];
+    const bool more = kb0 + 4 * U < kb_end;
+    if (more) load_group(kb0 + 4 * U, wn, xn);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (kb0 + 4 * u >= kb_end) {  // zero the weight operand: the MFMA then adds nothing
@@ -511,6 +523,14 @@ __global__ __launch_bounds__(256) void wo_gemm_kernel(
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[u][1], i4x8_to_bf16(wv[u].y), acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[u][2], i4x8_to_bf16(wv[u].z), acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[u][3], i4x8_to_bf16(wv[u].w), acc, 0, 0, 0);
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        wv[u] = wn[u];
+#pragma unroll
+        for (int i = 0; i < NMF; ++i) xa[u][i] = xn[u][i];
       }
     }
   }

@@ -216,8 +216,12 @@ def packed_linear(x, wp, bias=None, act="none"):
 
 
 def _split_k(tiles, kb):
+    """Split-K factor of the weight-stream GEMV. Measured on MI355X with the weights streamed
+    from HBM (tools/bench_gemv.py → profiles/gemv_decode_r1.txt): with the software-pipelined
+    kernel the fastest split is the smallest one giving ≥ ~192 workgroups (QKV / FFN1: 1,
+    out-proj / FFN2: 4), as long as each split keeps ≥ 16 k-blocks."""
     KS = 1
-    while tiles * KS < 512 and kb // (KS * 2) >= 16:
+    while tiles * KS < 192 and kb // (KS * 2) >= 16:
         KS *= 2
     return KS
 

@@ -166,24 +166,27 @@ __device__ __forceinline__ void gemm_mainloop(const bf16_t* __restrict__ a, long
   }
 }
 
-// Epilogue: lane owns row m0+wr*128+mb*32+l31 (stored while < mend); columns
-// n = n0 + wc*64 + nb*32 + 8g + 4*hi + (0..3) (stored while < N).
-__device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[4][2], void* __restrict__ c,
+// Epilogue: waves laid out WM (M) × 8/WM (N), each MB × NB blocks of 32 × 32 (default: the 256²
+// tile, 2 × 4 waves of 4 × 2). Lane owns row m0 + wr·32MB + mb·32 + l31 (stored while < mend);
+// columns n = n0 + wc·32NB + nb·32 + 8g + 4·hi + (0..3) (stored while < N).
+template <int WM = 2, int MB = 4, int NB = 2>
+__device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[MB][NB], void* __restrict__ c,
                                               long long ldc, int c_f32, int accumulate, int m0,
                                               int mend, int n0, int N, int epi, int act,
                                               const bf16_t* __restrict__ bias,
                                               bf16_t* __restrict__ aux, long long ldaux) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 2, wc = w & 3;
+  constexpr int WC = NWAVE / WM;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w / WC, wc = w % WC;
   const int hi = lane >> 5, l31 = lane & 31;
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb) {
-    const int m = m0 + wr * 128 + mb * 32 + l31;
+  for (int mb = 0; mb < MB; ++mb) {
+    const int m = m0 + wr * (32 * MB) + mb * 32 + l31;
     if (m >= mend) continue;
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
+    for (int nb = 0; nb < NB; ++nb) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int n = n0 + wc * 64 + nb * 32 + 8 * g + 4 * hi;
+        const int n = n0 + wc * (32 * NB) + nb * 32 + 8 * g + 4 * hi;
         if (n >= N) continue;
         float v[4];
 #pragma unroll
@@ -306,6 +309,153 @@ __global__ __launch_bounds__(NTHR, 1) void moe_wgrad_kernel(
   gemm_mainloop<false, false>(x, ldx, 0, dy, lddy, 0, m0, n0, r0, (r1 - r0) / BK, smem, acc);
   void* out = dw_f32 ? (void*)((float*)dw + e * sdw) : (void*)((bf16_t*)dw + e * sdw);
   gemm_epilogue(acc, out, N, dw_f32, accumulate, m0, M, n0, N, EPI_STORE, 0, nullptr, nullptr, 0);
+}
+
+// ---- implicit-GEMM convolution (NHWC, bf16) ---------------------------------------------------
+// Parity: reference `phi/kernels/gpudnn/conv_kernel.cu` / `conv_grad_kernel.cu` (cuDNN) — here an
+// MFMA implicit GEMM: Y[m = (n, oh, ow)][k_out] = Σ_{(r, s, c)} X[n, oh·st − pad + r·dil,
+// ow·st − pad + s·dil, c] · W[k_out][(r, s, c)], the A tile gathered straight from the NHWC
+// activation by the global→LDS DMA (one 128-byte channel run of one input pixel per 8 lanes; out-of-
+// image taps read a zero row), W in OHWI = [K_out][R·S·C] (K-contiguous B operand). Same 256² tile,
+// XOR-swizzled LDS images and MFMA loop as gemm_kernel; bias + activation fused in the epilogue.
+// Requires C % 64 == 0 (a 64-channel k-step never straddles two taps) and K_out % 4 == 0.
+struct ConvGeom {
+  int N, H, W, C, OH, OW, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w;
+};
+
+// Tile 256 (M) × TN (N), TN = 8/WM · 32·NB: WM=2,MB=4,NB=2 → 256² (K_out ≥ 256); WM=4,MB=2,NB=2 →
+// 256 × 128; WM=8,MB=1,NB=2 → 256 × 64 (narrow layers keep every MFMA column useful).
+// ksplit > 1: workgroup (tile, part) reduces k-steps [part·nk/ksplit, (part+1)·nk/ksplit) into an
+// f32 partial plane ws[part][M][K_out]; conv_splitk_finish sums the planes (fixed order:
+// deterministic) and applies bias + activation — fills the chip on the small late-stage layers.
+template <int WM, int MB, int NB>
+__global__ __launch_bounds__(NTHR, 1) void conv_fwd_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ wt, const bf16_t* __restrict__ zero,
+    bf16_t* __restrict__ y, float* __restrict__ ws, int ksplit, ConvGeom g, int Kout, int act,
+    const bf16_t* __restrict__ bias) {
+  constexpr int WC = NWAVE / WM, TN = WC * NB * 32;
+  constexpr int B_BYTES = TN * BK * 2, SBYTES = TILE_BYTES + B_BYTES;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * SBYTES];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w / WC, wc = w % WC;
+  const int M = g.N * g.OH * g.OW;
+  const int tm = (M + BM - 1) / BM, tn = (Kout + TN - 1) / TN;
+  const int wg = xcd_remap(blockIdx.x, tm * tn * ksplit);
+  const int part = wg % ksplit, tile = wg / ksplit;
+  const int m0 = (tile / tn) * BM, n0 = (tile % tn) * TN;
+  const long long RSC = (long long)g.R * g.S * g.C;
+  const int cpt = g.C / BK;  // 64-channel k-steps per tap
+  const int nk_all = g.R * g.S * cpt;
+  const int kt0 = (int)((long long)nk_all * part / ksplit);
+  const int kt1 = (int)((long long)nk_all * (part + 1) / ksplit);
+
+  // this lane's 4 DMA pieces of the A tile: fixed output pixel per piece, k-step invariant
+  constexpr int PPW = 4;
+  long long pbase[PPW];
+  int ih0[PPW], iw0[PPW], choff[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int P = w * PPW + i, L = P * 64 + lane, r = L / 8, pc = L % 8;
+    const int xsw = (((r & 3) << 2) | ((r >> 2) & 3)) & 7;
+    choff[i] = (pc ^ xsw) << 3;
+    const int m = m0 + r;
+    if (m < M) {
+      const int n = m / (g.OH * g.OW), rem = m % (g.OH * g.OW);
+      const int oh = rem / g.OW, ow = rem % g.OW;
+      pbase[i] = (long long)n * g.H * g.W;
+      ih0[i] = oh * g.st_h - g.pad_h;
+      iw0[i] = ow * g.st_w - g.pad_w;
+    } else {
+      pbase[i] = -1;
+      ih0[i] = iw0[i] = 0;
+    }
+  }
+  auto stage_load = [&](int kt, int s) {
+    char* ai = smem + s * SBYTES;
+    char* bi = ai + TILE_BYTES;
+    const int rs = kt / cpt, c0 = (kt % cpt) * BK;
+    const int rr = rs / g.S, ss = rs % g.S;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int ih = ih0[i] + rr * g.dil_h, iw = iw0[i] + ss * g.dil_w;
+      const bool ok = pbase[i] >= 0 && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+      const bf16_t* src = ok ? x + (pbase[i] + (long long)ih * g.W + iw) * g.C + c0 + choff[i]
+                             : zero + choff[i];
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(ai + (w * PPW + i) * 1024),
+                                       16, 0, 0);
+    }
+    dma_tile<TN, 128>(wt + (long long)kt * BK, RSC, n0, Kout - 1, bi, w, lane);
+  };
+
+  f32x16 acc[MB][NB];
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  if (kt1 > kt0) {
+    stage_load(kt0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  const int hi = lane >> 5, l31 = lane & 31;
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int s = (kt - kt0) & 1;
+    if (kt + 1 < kt1) stage_load(kt + 1, s ^ 1);
+    const char* ai = smem + s * SBYTES;
+    const char* bi = ai + TILE_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8 af[MB], bf[NB];
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+        af[mb] = rd_row(ai, img_off<128>(wr * (32 * MB) + mb * 32 + l31, 2 * ks + hi));
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+        bf[nb] = rd_row(bi, img_off<128>(wc * (32 * NB) + nb * 32 + l31, 2 * ks + hi));
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+          acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[nb], af[mb], acc[mb][nb], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (ksplit > 1)
+    gemm_epilogue<WM, MB, NB>(acc, ws + (long long)part * M * Kout, Kout, 1, 0, m0, M, n0, Kout,
+                              EPI_STORE, 0, nullptr, nullptr, 0);
+  else
+    gemm_epilogue<WM, MB, NB>(acc, y, Kout, 0, 0, m0, M, n0, Kout,
+                              (bias || act) ? EPI_BIAS_ACT : EPI_STORE, act, bias, nullptr, 0);
+}
+
+// y[m][n] = act(Σ_p ws[p][m][n] + bias[n]) — 4 outputs per thread (K_out % 4 == 0).
+__global__ __launch_bounds__(256) void conv_splitk_finish(const float* __restrict__ ws, int ksplit,
+                                                          long long MN, int Kout, int act,
+                                                          const bf16_t* __restrict__ bias,
+                                                          bf16_t* __restrict__ y) {
+  const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= MN) return;
+  f32x4 v = *reinterpret_cast<const f32x4*>(ws + i);
+  for (int p = 1; p < ksplit; ++p) {
+    const f32x4 t = *reinterpret_cast<const f32x4*>(ws + p * MN + i);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] += t[j];
+  }
+  const int n = (int)(i % Kout);
+  u16x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float h = v[j];
+    if (bias || act) h = bf2f(f2bf(h + (bias ? bf2f(bias[n + j]) : 0.f)));
+    o[j] = f2bf(act_fwd(h, act));
+  }
+  *reinterpret_cast<u16x4*>(y + i) = o;
 }
 
 // ---- int8 × int8 → int32 GEMM with dequantising epilogue -------------------------------------
@@ -451,6 +601,45 @@ PIAMD_EXPORT int piamd_gemm_i8(const void* x, long long ldx, const void* wq, lon
   hipLaunchKernelGGL(gemm_i8_kernel, dim3(tiles), dim3(NTHR), 0, st, (const signed char*)x, ldx,
                      (const signed char*)wq, ldw, xs, xs_const, ws, (const bf16_t*)bias,
                      (bf16_t*)y, ldy, M, N, K, act);
+  return (int)hipGetLastError();
+}
+
+// NHWC implicit-GEMM convolution forward: x [N][H][W][C], wt [Kout][R][S][C] (OHWI), y
+// [N][OH][OW][Kout], bf16; zero: ≥ 128 zero bytes (out-of-image taps); bias [Kout] (nullable);
+// act as piamd_gemm. C % 64 == 0, Kout % 4 == 0.
+PIAMD_EXPORT int piamd_conv2d_fwd(const void* x, const void* wt, const void* zero, void* y, int N,
+                                  int H, int W, int C, int OH, int OW, int R, int S, int st_h,
+                                  int st_w, int pad_h, int pad_w, int dil_h, int dil_w, int Kout,
+                                  int act, const void* bias, int tile_n, int ksplit, void* ws,
+                                  hipStream_t st) {
+  if (C % BK || Kout % 4 || N < 1 || OH < 1 || OW < 1 || R < 1 || S < 1 || !zero || ksplit < 1 ||
+      (ksplit > 1 && !ws) || ksplit > R * S * (C / BK))
+    return (int)hipErrorInvalidValue;
+  ConvGeom g{N, H, W, C, OH, OW, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w};
+  const long long M = (long long)N * OH * OW;
+  if (M * ksplit > 0x7fffffffLL || M * Kout > (1LL << 40)) return (int)hipErrorInvalidValue;
+  const int tm = (int)((M + BM - 1) / BM);
+  const auto xb = (const bf16_t*)x;
+  const auto wb = (const bf16_t*)wt;
+  const auto zb = (const bf16_t*)zero;
+  const auto bb = (const bf16_t*)bias;
+  float* wsf = (float*)ws;
+  if (tile_n == 64)
+    hipLaunchKernelGGL((conv_fwd_kernel<8, 1, 2>), dim3(tm * ((Kout + 63) / 64) * ksplit),
+                       dim3(NTHR), 0, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb);
+  else if (tile_n == 128)
+    hipLaunchKernelGGL((conv_fwd_kernel<4, 2, 2>), dim3(tm * ((Kout + 127) / 128) * ksplit),
+                       dim3(NTHR), 0, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb);
+  else if (tile_n == 256)
+    hipLaunchKernelGGL((conv_fwd_kernel<2, 4, 2>), dim3(tm * ((Kout + 255) / 256) * ksplit),
+                       dim3(NTHR), 0, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb);
+  else
+    return (int)hipErrorInvalidValue;
+  if (ksplit > 1) {
+    const long long MN = M * Kout;
+    hipLaunchKernelGGL(conv_splitk_finish, dim3((unsigned)((MN / 4 + 255) / 256)), dim3(256), 0,
+                       st, wsf, ksplit, MN, Kout, act, bb, (bf16_t*)y);
+  }
   return (int)hipGetLastError();
 }
 

@@ -185,7 +185,30 @@ def conv1d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data
     return _fmt_out(TF.conv1d(_fmt_in(x, data_format), weight, bias, stride, _padding(padding, 1), dilation, groups), data_format)
 
 
+def _hip_conv_ok(x, weight, groups, padding, nhwc):
+    """bf16 NHWC / channels_last conv on the GPU → MFMA implicit-GEMM kernel (ops/conv.py)."""
+    if not (x.is_cuda and x.dim() == 4 and weight.dim() == 4 and groups == 1):
+        return False
+    bf16 = x.dtype == torch.bfloat16 or (torch.is_autocast_enabled("cuda") and
+                                         torch.get_autocast_dtype("cuda") == torch.bfloat16)
+    if not bf16 or isinstance(padding, str):
+        return False
+    if not nhwc and not (x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous()):
+        return False
+    from ...ops import conv as _conv
+    return _conv.HIP_CONV and _conv.eligible((x.shape[-1] if nhwc else x.shape[1],),
+                                             weight.shape, groups, padding)
+
+
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NCHW", name=None):
+    nhwc = data_format == "NHWC"
+    pad = _padding(padding, 2)
+    if _hip_conv_ok(x, weight, groups, pad, nhwc):
+        from ...ops import conv as _conv
+        with torch.autocast("cuda", enabled=False):
+            if nhwc:
+                return _conv.conv2d_nhwc(x, weight, bias, stride, pad, dilation)
+            return _conv.conv2d_nchw(x, weight, bias, stride, pad, dilation)
     return _fmt_out(TF.conv2d(_fmt_in(x, data_format), weight, bias, stride, _padding(padding, 2), dilation, groups), data_format)
 
 

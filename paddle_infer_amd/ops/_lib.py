@@ -189,6 +189,9 @@ _SIGS["piamd_gemm_i8"] = [c_void_p, c_ll, c_void_p, c_ll, c_void_p, c_float, c_v
                           c_void_p, c_ll, c_int, c_int, c_int, c_int, c_void_p]
 _SIGS["piamd_quant_rows"] = [c_void_p, c_ll, c_void_p, c_ll, c_void_p, c_float, c_int, c_int,
                              c_void_p]
+# x, w_ohwi, zero, y, N, H, W, C, OH, OW, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w, Kout, act,
+# bias, tile_n, ksplit, ws, stream
+_SIGS["piamd_conv2d_fwd"] = [c_void_p] * 4 + [c_int] * 16 + [c_void_p, c_int, c_int, c_void_p, c_void_p]
 # dtype, nhwc, x, res, y, N, C, S, gamma, beta, run_mean, run_var, mean, rstd, momentum, eps,
 # training, act, ws, stream
 _SIGS["piamd_bn_fwd"] = ([c_int, c_int] + [c_void_p] * 3 + [c_int] * 3 + [c_void_p] * 6

@@ -1,0 +1,79 @@
+"""MFMA implicit-GEMM NHWC convolution (``gemm.hip`` conv_fwd, ``ops/conv.py``) against the plain
+PyTorch fp32 convolution: strides, paddings, dilations, 1×1 / 3×3 / 7×7 filters, K_out not a
+multiple of the 256 tile, bias + ReLU epilogue, and the data / filter / bias gradients (the
+stride-1 data gradient runs on the same kernel with the flipped filter)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _close(a, b, tol):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs().max().item()
+    assert err <= tol * max(1.0, b.abs().max().item()), err
+
+
+CASES = [  # N, H, W, C, K, R, stride, pad, dil
+    (2, 14, 14, 64, 64, 3, 1, 1, 1),
+    (2, 9, 11, 128, 100, 3, 1, 1, 1),
+    (1, 16, 16, 64, 256, 1, 1, 0, 1),
+    (2, 15, 13, 256, 320, 3, 2, 1, 1),
+    (1, 12, 12, 64, 128, 3, 1, 2, 2),
+    (1, 20, 20, 64, 64, 7, 2, 3, 1),
+    (3, 7, 7, 512, 512, 3, 1, 1, 1),
+    (1, 8, 8, 128, 64, 1, 2, 0, 1),
+]
+
+
+@pytest.mark.parametrize("N,H,W,C,K,R,st,pad,dil", CASES)
+@pytest.mark.parametrize("act", [None, "relu"])
+def test_conv_fwd_bwd(N, H, W, C, K, R, st, pad, dil, act):
+    from paddle_infer_amd.ops.conv import conv2d_nhwc
+    torch.manual_seed(R * 100 + C)
+    x = torch.randn(N, H, W, C, device=DEV).bfloat16()
+    w = (torch.randn(K, C, R, R, device=DEV) / (C * R * R) ** 0.5).bfloat16()
+    b = torch.randn(K, device=DEV).bfloat16()
+    xh, wh, bh = (t.clone().requires_grad_(True) for t in (x, w, b))
+    y = conv2d_nhwc(xh, wh, bh, st, pad, dil, act)
+    xr, wr, br = (t.float().clone().requires_grad_(True) for t in (x, w, b))
+    yr = F.conv2d(xr.permute(0, 3, 1, 2), wr, br, st, pad, dil).permute(0, 2, 3, 1)
+    if act == "relu":
+        yr = torch.relu(yr)
+    assert y.shape == yr.shape
+    _close(y, yr, 2e-2)
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    _close(xh.grad, xr.grad, 3e-2)
+    _close(wh.grad, wr.grad, 3e-2)
+    _close(bh.grad, br.grad, 3e-2)
+
+
+def test_conv2d_layer_dispatch_channels_last():
+    import paddle_infer_amd.nn as nn
+    torch.manual_seed(0)
+    m = nn.Conv2D(64, 128, 3, padding=1).to(DEV)
+    x = torch.randn(2, 64, 10, 10, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(x)
+    yr = F.conv2d(x.float(), m.weight.float(), m.bias.float(), 1, 1)
+    _close(y, yr, 2e-2)
+
+
+@pytest.mark.parametrize("plan", [(64, 1), (128, 2), (256, 4), (64, 8), (128, 3)])
+def test_conv_tile_and_splitk_variants(plan):
+    from paddle_infer_amd.ops import conv as CV
+    torch.manual_seed(1)
+    x = torch.randn(2, 11, 9, 128, device=DEV).bfloat16()
+    w = (torch.randn(200, 128, 3, 3, device=DEV) / 34).bfloat16()
+    b = torch.randn(200, device=DEV).bfloat16()
+    CV.PLAN_OVERRIDE = plan
+    try:
+        y = CV.conv2d_nhwc(x, w, b, 1, 1, 1, "relu")
+    finally:
+        CV.PLAN_OVERRIDE = None
+    yr = torch.relu(F.conv2d(x.float().permute(0, 3, 1, 2), w.float(), b.float(), 1, 1)).permute(0, 2, 3, 1)
+    _close(y, yr, 2e-2)

@@ -106,17 +106,33 @@ __global__ __launch_bounds__(256) void bn_stats_nhwc(const T* __restrict__ x, lo
 
 // per channel: merge partials → mean / rstd (saved for backward), running stats update, and the
 // affine fold scale = γ·rstd, shift = β − mean·scale.
-__global__ void bn_finalize(const float* __restrict__ part, int P, int C, float eps, float momentum,
-                            const float* __restrict__ gamma, const float* __restrict__ beta,
-                            float* __restrict__ run_mean, float* __restrict__ run_var,
-                            float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                            float* __restrict__ scale, float* __restrict__ shift) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// one 256-thread block per channel: lanes merge strided partials, then an LDS tree merge.
+__global__ __launch_bounds__(256) void bn_finalize(const float* __restrict__ part, int P, int C,
+                                                   float eps, float momentum,
+                                                   const float* __restrict__ gamma,
+                                                   const float* __restrict__ beta,
+                                                   float* __restrict__ run_mean,
+                                                   float* __restrict__ run_var,
+                                                   float* __restrict__ mean_out,
+                                                   float* __restrict__ rstd_out,
+                                                   float* __restrict__ scale,
+                                                   float* __restrict__ shift) {
+  const int c = blockIdx.x, t = threadIdx.x;
   float n = 0.f, m = 0.f, m2 = 0.f;
-  for (int b = 0; b < P; ++b)
+  for (int b = t; b < P; b += 256)
     welford_merge(n, m, m2, part[(0 * P + b) * C + c], part[(1 * P + b) * C + c],
                   part[(2 * P + b) * C + c]);
+  __shared__ float sn[256], sm[256], sm2[256];
+  sn[t] = n; sm[t] = m; sm2[t] = m2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) {
+      welford_merge(n, m, m2, sn[t + o], sm[t + o], sm2[t + o]);
+      sn[t] = n; sm[t] = m; sm2[t] = m2;
+    }
+    __syncthreads();
+  }
+  if (t) return;
   const float var = n > 0.f ? m2 / n : 0.f;
   const float rstd = rsqrtf(var + eps);
   mean_out[c] = m;
@@ -249,21 +265,33 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_nhwc(const T* __restrict__ 
   }
 }
 
-// per channel: dβ = Σdz, dγ = Σ dz·x̂ (f32), plus the coefficients of the dx pass
-__global__ void bn_bwd_finalize(const float* __restrict__ part, int P, int C, float M,
-                                const float* __restrict__ gamma, const float* __restrict__ rstd,
-                                float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                float* __restrict__ coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// per channel (one block each): dβ = Σdz, dγ = Σ dz·x̂ (f32), and the dx pass as one FMA chain
+// dx = A·dz + B·x + D with A = γ·rstd, B = −A·rstd·Σdz·x̂/M, D = A·(μ·rstd·Σdz·x̂ − Σdz)/M
+// (training; eval: B = D = 0 — the running statistics are constants).
+__global__ __launch_bounds__(256) void bn_bwd_finalize(const float* __restrict__ part, int P, int C,
+                                                       float M, const float* __restrict__ gamma,
+                                                       const float* __restrict__ mean,
+                                                       const float* __restrict__ rstd,
+                                                       float* __restrict__ dgamma,
+                                                       float* __restrict__ dbeta,
+                                                       float* __restrict__ coef, int training) {
+  const int c = blockIdx.x, t = threadIdx.x;
   float s1 = 0.f, s2 = 0.f;
-  for (int b = 0; b < P; ++b) { s1 += part[(0 * P + b) * C + c]; s2 += part[(1 * P + b) * C + c]; }
+  for (int b = t; b < P; b += 256) { s1 += part[(0 * P + b) * C + c]; s2 += part[(1 * P + b) * C + c]; }
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  __shared__ float r[2][4];
+  if ((t & 63) == 0) { r[0][t >> 6] = s1; r[1][t >> 6] = s2; }
+  __syncthreads();
+  if (t) return;
+  s1 = r[0][0] + r[0][1] + r[0][2] + r[0][3];
+  s2 = r[1][0] + r[1][1] + r[1][2] + r[1][3];
   if (dbeta) dbeta[c] = s1;
   if (dgamma) dgamma[c] = s2;
-  const float g = gamma ? gamma[c] : 1.f;
-  coef[c] = g * rstd[c];  // dx = coef·(dz − s1/M − x̂·s2/M)
-  coef[C + c] = s1 / M;
-  coef[2 * C + c] = s2 / M;
+  const float rs = rstd[c], A = (gamma ? gamma[c] : 1.f) * rs;
+  coef[c] = A;
+  coef[C + c] = training ? -A * rs * s2 / M : 0.f;
+  coef[2 * C + c] = training ? A * (mean[c] * rs * s2 - s1) / M : 0.f;
 }
 
 template <typename T>
@@ -279,14 +307,234 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const T* __restrict__ dy, co
     const int c = nhwc ? (int)(i % C) : (int)((i / S) % C);
     const float dz = dz_of(dy, y, i, act);
     if (dres) V<T>::st(dres + i, dz);
-    float v;
-    if (training) {
-      const float xh = (V<T>::ld(x + i) - mean[c]) * rstd[c];
-      v = coef[c] * (dz - coef[C + c] - xh * coef[2 * C + c]);
-    } else {
-      v = coef[c] * dz;  // running statistics are constants
-    }
+    float v = coef[c] * dz;
+    if (training) v += coef[C + c] * V<T>::ld(x + i) + coef[2 * C + c];
     V<T>::st(dx + i, v);
+  }
+}
+
+// ------------------------------------------------------------- vectorised NHWC (C % 8 == 0)
+// 8 consecutive channels per thread (one 16-B bf16 / 2 × 16-B f32 load); a 256-thread block is
+// RB = 256 / G rows × G = C/8 channel groups (G ≥ 256: one row per step, groups strided by 256).
+template <typename T> __device__ __forceinline__ void ld8(const T* p, float (&v)[8]);
+template <> __device__ __forceinline__ void ld8<bf16_t>(const bf16_t* p, float (&v)[8]) {
+  const u16x8 u = *reinterpret_cast<const u16x8*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = bf2f(u[j]);
+}
+template <> __device__ __forceinline__ void ld8<float>(const float* p, float (&v)[8]) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = b[j]; }
+}
+template <typename T> __device__ __forceinline__ void st8(T* p, const float (&v)[8]);
+template <> __device__ __forceinline__ void st8<bf16_t>(bf16_t* p, const float (&v)[8]) {
+  u16x8 u;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) u[j] = f2bf(v[j]);
+  *reinterpret_cast<u16x8*>(p) = u;
+}
+template <> __device__ __forceinline__ void st8<float>(float* p, const float (&v)[8]) {
+  f32x4 a, b;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { a[j] = v[j]; b[j] = v[4 + j]; }
+  *reinterpret_cast<f32x4*>(p) = a;
+  *reinterpret_cast<f32x4*>(p + 4) = b;
+}
+
+// Statistics: per thread shifted sums (shift = the block's first row — robust, no per-element
+// divide), converted to (n, mean, M2) and Welford-merged over the block's row lanes.
+template <typename T>
+__global__ __launch_bounds__(256) void bn_stats_nhwc8(const T* __restrict__ x, long long M, int C,
+                                                      long long chunk, float* __restrict__ part) {
+  const int b = blockIdx.x, P = gridDim.x, t = threadIdx.x, G = C / 8;
+  const int RB = G >= 256 ? 1 : 256 / G;
+  const long long beg = b * chunk, end = min(M, beg + chunk);
+  __shared__ float sn[256], sm[256][9], sm2[256][9];
+  for (int g0 = 0; g0 < G; g0 += (G >= 256 ? 256 : G)) {
+    const int cg = G >= 256 ? g0 + t : t % G, rl = G >= 256 ? 0 : t / G;
+    const bool live = cg < G && rl < RB && beg < end;
+    float sh[8], s[8], q[8], n = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sh[j] = s[j] = q[j] = 0.f;
+    if (live) {
+      ld8(x + beg * C + cg * 8, sh);
+      for (long long r = beg + rl; r < end; r += RB) {
+        float v[8];
+        ld8(x + r * C + cg * 8, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { const float d = v[j] - sh[j]; s[j] += d; q[j] += d * d; }
+        n += 1.f;
+      }
+    }
+    float mu[8], m2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mu[j] = n > 0.f ? sh[j] + s[j] / n : 0.f;
+      m2[j] = n > 0.f ? fmaxf(q[j] - s[j] * s[j] / n, 0.f) : 0.f;
+    }
+    if (G < 256) {
+      sn[t] = n;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { sm[t][j] = mu[j]; sm2[t][j] = m2[j]; }
+      __syncthreads();
+      if (t < G) {
+        for (int k = 1; k < RB; ++k) {
+          const int o = t + k * G;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float nn = n, mm = mu[j], qq = m2[j];
+            welford_merge(nn, mm, qq, sn[o], sm[o][j], sm2[o][j]);
+            mu[j] = mm; m2[j] = qq;
+          }
+          n += sn[o];
+        }
+      }
+      __syncthreads();
+    }
+    if (cg < G && rl == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = cg * 8 + j;
+        part[(0 * P + b) * C + c] = n;
+        part[(1 * P + b) * C + c] = mu[j];
+        part[(2 * P + b) * C + c] = m2[j];
+      }
+    }
+  }
+}
+
+// Backward partials Σ dz, Σ dz·(x − μ)·rstd per channel: part [2][P][C].
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_nhwc8(const T* __restrict__ dy,
+                                                           const T* __restrict__ y,
+                                                           const T* __restrict__ x,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ rstd,
+                                                           long long M, int C, long long chunk,
+                                                           int act, float* __restrict__ part) {
+  const int b = blockIdx.x, P = gridDim.x, t = threadIdx.x, G = C / 8;
+  const int RB = G >= 256 ? 1 : 256 / G;
+  const long long beg = b * chunk, end = min(M, beg + chunk);
+  __shared__ float r1[256][9], r2[256][9];
+  for (int g0 = 0; g0 < G; g0 += (G >= 256 ? 256 : G)) {
+    const int cg = G >= 256 ? g0 + t : t % G, rl = G >= 256 ? 0 : t / G;
+    const bool live = cg < G && rl < RB;
+    float s1[8], s2[8], mu[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { s1[j] = s2[j] = 0.f; mu[j] = live ? mean[cg * 8 + j] : 0.f; }
+    if (live) {
+      for (long long r = beg + rl; r < end; r += RB) {
+        const long long i = r * C + cg * 8;
+        float g[8], xv[8];
+        ld8(dy + i, g);
+        ld8(x + i, xv);
+        if (act) {
+          float yv[8];
+          ld8(y + i, yv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (!(act == 1 ? yv[j] > 0.f : (yv[j] > 0.f && yv[j] < 6.f))) g[j] = 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { s1[j] += g[j]; s2[j] += g[j] * (xv[j] - mu[j]); }
+      }
+    }
+    if (G < 256) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { r1[t][j] = s1[j]; r2[t][j] = s2[j]; }
+      __syncthreads();
+      if (t < G)
+        for (int k = 1; k < RB; ++k)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { s1[j] += r1[t + k * G][j]; s2[j] += r2[t + k * G][j]; }
+      __syncthreads();
+    }
+    if (cg < G && rl == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = cg * 8 + j;
+        part[(0 * P + b) * C + c] = s1[j];
+        part[(1 * P + b) * C + c] = s2[j] * rstd[c];
+      }
+    }
+  }
+}
+
+// per-channel coefficients of 8 consecutive elements: 8 channels c..c+7 (nhwc) or channel c
+__device__ __forceinline__ void coef8(const float* __restrict__ a, int c, int nhwc, float (&v)[8]) {
+  if (nhwc) {
+    ld8<float>(a + c, v);
+  } else {
+    const float s = a[c];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = s;
+  }
+}
+
+// 8 consecutive elements share one channel (nchw: S % 8 == 0) or are 8 channels (nhwc: C % 8 == 0)
+__device__ __forceinline__ int chan8(long long i, int C, int S, int nhwc) {
+  return nhwc ? (int)(i % C) : (int)((i / S) % C);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_apply8(const T* __restrict__ x, const T* __restrict__ res,
+                                                 const float* __restrict__ scale,
+                                                 const float* __restrict__ shift, T* __restrict__ y,
+                                                 long long total, int C, int S, int nhwc, int act) {
+  for (long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 8; i < total;
+       i += (long long)gridDim.x * blockDim.x * 8) {
+    const int c = chan8(i, C, S, nhwc);
+    float v[8], r[8], sc[8], sh[8];
+    ld8(x + i, v);
+    if (res) ld8(res + i, r);
+    coef8(scale, c, nhwc, sc);
+    coef8(shift, c, nhwc, sh);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float z = v[j] * sc[j] + sh[j];
+      if (res) z += r[j];
+      v[j] = bn_act(z, act);
+    }
+    st8(y + i, v);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_apply8(const T* __restrict__ dy, const T* __restrict__ y,
+                                                     const T* __restrict__ x,
+                                                     const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd,
+                                                     const float* __restrict__ coef, T* __restrict__ dx,
+                                                     T* __restrict__ dres, long long total, int C,
+                                                     int S, int nhwc, int act, int training) {
+  for (long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 8; i < total;
+       i += (long long)gridDim.x * blockDim.x * 8) {
+    const int c = chan8(i, C, S, nhwc);
+    float g[8], xv[8];
+    ld8(dy + i, g);
+    if (act) {
+      float yv[8];
+      ld8(y + i, yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (!(act == 1 ? yv[j] > 0.f : (yv[j] > 0.f && yv[j] < 6.f))) g[j] = 0.f;
+    }
+    if (dres) st8(dres + i, g);
+    float A[8];
+    coef8(coef, c, nhwc, A);
+    if (training) {
+      float B[8], D[8];
+      ld8(x + i, xv);
+      coef8(coef + C, c, nhwc, B);
+      coef8(coef + 2 * C, c, nhwc, D);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = A[j] * g[j] + B[j] * xv[j] + D[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] *= A[j];
+    }
+    st8(dx + i, g);
   }
 }
 
@@ -295,38 +543,61 @@ int parts_for(long long M) {
   return (int)(p < 1 ? 1 : (p > 512 ? 512 : p));
 }
 
+// vectorised NHWC: ≈ 64 K elements per block, ≤ 512 blocks, ≥ 1 row each
+int parts_for8(long long M, int C) {
+  long long p = (M * C + 65535) / 65536;
+  p = p > 512 ? 512 : p;
+  p = p > M ? M : p;
+  return (int)(p < 1 ? 1 : p);
+}
+
 }  // namespace
 
 // Forward. x/res/y: [N, C, S] (nhwc = 0) or [N·S, C] (nhwc = 1); dtype 0 = f32, 1 = bf16.
 // training: statistics of x → mean/rstd (f32 [C], saved for backward), running stats updated in
 // place (momentum: Paddle convention); else the running statistics (mean/rstd still written).
 // ws: f32 workspace of ≥ 2·C + 3·512·C floats. act: 0 none, 1 relu, 2 relu6.
-// nhwc requires C ≥ 256 or C | 256.
+// nhwc requires C % 8 == 0 (vectorised path), C ≥ 256 or C | 256.
 PIAMD_EXPORT int piamd_bn_fwd(int dtype, int nhwc, const void* x, const void* res, void* y, int N,
                               int C, int S, const float* gamma, const float* beta,
                               float* run_mean, float* run_var, float* mean, float* rstd,
                               float momentum, float eps, int training, int act, float* ws,
                               hipStream_t st) {
-  if (C < 1 || N < 1 || S < 1 || (nhwc && C < 256 && 256 % C)) return (int)hipErrorInvalidValue;
+  if (C < 1 || N < 1 || S < 1 || (nhwc && C % 8 && C < 256 && 256 % C))
+    return (int)hipErrorInvalidValue;
   const long long M = (long long)N * S, total = M * C;
+  const bool v8 = nhwc ? C % 8 == 0 : S % 8 == 0;
   float* scale = ws;
   float* shift = ws + C;
   if (training) {
-    const int P = parts_for(M);
+    const int P = nhwc && C % 8 == 0 ? parts_for8(M, C) : parts_for(M);
     const long long chunk = (M + P - 1) / P;
     float* part = ws + 2 * C;
-    if (nhwc) {
+    if (nhwc && C % 8 == 0) {
+      if (dtype) hipLaunchKernelGGL(bn_stats_nhwc8<bf16_t>, dim3(P), dim3(256), 0, st, (const bf16_t*)x, M, C, chunk, part);
+      else hipLaunchKernelGGL(bn_stats_nhwc8<float>, dim3(P), dim3(256), 0, st, (const float*)x, M, C, chunk, part);
+    } else if (nhwc) {
       if (dtype) hipLaunchKernelGGL(bn_stats_nhwc<bf16_t>, dim3(P), dim3(256), 0, st, (const bf16_t*)x, M, C, chunk, part);
       else hipLaunchKernelGGL(bn_stats_nhwc<float>, dim3(P), dim3(256), 0, st, (const float*)x, M, C, chunk, part);
     } else {
       if (dtype) hipLaunchKernelGGL(bn_stats_nchw<bf16_t>, dim3(C, P), dim3(256), 0, st, (const bf16_t*)x, N, C, S, chunk, part);
       else hipLaunchKernelGGL(bn_stats_nchw<float>, dim3(C, P), dim3(256), 0, st, (const float*)x, N, C, S, chunk, part);
     }
-    hipLaunchKernelGGL(bn_finalize, dim3((C + 255) / 256), dim3(256), 0, st, part, P, C, eps,
+    hipLaunchKernelGGL(bn_finalize, dim3(C), dim3(256), 0, st, part, P, C, eps,
                        momentum, gamma, beta, run_mean, run_var, mean, rstd, scale, shift);
   } else {
     hipLaunchKernelGGL(bn_fold, dim3((C + 255) / 256), dim3(256), 0, st, C, eps, gamma, beta,
                        run_mean, run_var, scale, shift, mean, rstd);
+  }
+  if (v8) {
+    const dim3 g8(stride_grid(total / 8, 256));
+    if (dtype)
+      hipLaunchKernelGGL(bn_apply8<bf16_t>, g8, dim3(256), 0, st, (const bf16_t*)x,
+                         (const bf16_t*)res, scale, shift, (bf16_t*)y, total, C, S, nhwc, act);
+    else
+      hipLaunchKernelGGL(bn_apply8<float>, g8, dim3(256), 0, st, (const float*)x,
+                         (const float*)res, scale, shift, (float*)y, total, C, S, nhwc, act);
+    return (int)hipGetLastError();
   }
   const dim3 g(stride_grid(total, 256));
   if (dtype)
@@ -345,21 +616,38 @@ PIAMD_EXPORT int piamd_bn_bwd(int dtype, int nhwc, const void* dy, const void* y
                               void* dx, void* dres, int N, int C, int S, const float* gamma,
                               const float* mean, const float* rstd, float* dgamma, float* dbeta,
                               int training, int act, float* ws, hipStream_t st) {
-  if (C < 1 || N < 1 || S < 1 || (nhwc && C < 256 && 256 % C)) return (int)hipErrorInvalidValue;
+  if (C < 1 || N < 1 || S < 1 || (nhwc && C % 8 && C < 256 && 256 % C))
+    return (int)hipErrorInvalidValue;
   const long long M = (long long)N * S, total = M * C;
-  const int P = parts_for(M);
+  const bool v8 = nhwc ? C % 8 == 0 : S % 8 == 0;
+  const int P = nhwc && C % 8 == 0 ? parts_for8(M, C) : parts_for(M);
   const long long chunk = (M + P - 1) / P;
   float* coef = ws;
   float* part = ws + 3 * C;
-  if (nhwc) {
+  if (nhwc && C % 8 == 0) {
+    if (dtype) hipLaunchKernelGGL(bn_bwd_reduce_nhwc8<bf16_t>, dim3(P), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x, mean, rstd, M, C, chunk, act, part);
+    else hipLaunchKernelGGL(bn_bwd_reduce_nhwc8<float>, dim3(P), dim3(256), 0, st, (const float*)dy, (const float*)y, (const float*)x, mean, rstd, M, C, chunk, act, part);
+  } else if (nhwc) {
     if (dtype) hipLaunchKernelGGL(bn_bwd_reduce_nhwc<bf16_t>, dim3(P), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x, mean, rstd, M, C, chunk, act, part);
     else hipLaunchKernelGGL(bn_bwd_reduce_nhwc<float>, dim3(P), dim3(256), 0, st, (const float*)dy, (const float*)y, (const float*)x, mean, rstd, M, C, chunk, act, part);
   } else {
     if (dtype) hipLaunchKernelGGL(bn_bwd_reduce_nchw<bf16_t>, dim3(C, P), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x, mean, rstd, N, C, S, chunk, act, part);
     else hipLaunchKernelGGL(bn_bwd_reduce_nchw<float>, dim3(C, P), dim3(256), 0, st, (const float*)dy, (const float*)y, (const float*)x, mean, rstd, N, C, S, chunk, act, part);
   }
-  hipLaunchKernelGGL(bn_bwd_finalize, dim3((C + 255) / 256), dim3(256), 0, st, part, P, C,
-                     (float)M, gamma, rstd, dgamma, dbeta, coef);
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3(C), dim3(256), 0, st, part, P, C, (float)M, gamma,
+                     mean, rstd, dgamma, dbeta, coef, training);
+  if (v8) {
+    const dim3 g8(stride_grid(total / 8, 256));
+    if (dtype)
+      hipLaunchKernelGGL(bn_bwd_apply8<bf16_t>, g8, dim3(256), 0, st, (const bf16_t*)dy,
+                         (const bf16_t*)y, (const bf16_t*)x, mean, rstd, coef, (bf16_t*)dx,
+                         (bf16_t*)dres, total, C, S, nhwc, act, training);
+    else
+      hipLaunchKernelGGL(bn_bwd_apply8<float>, g8, dim3(256), 0, st, (const float*)dy,
+                         (const float*)y, (const float*)x, mean, rstd, coef, (float*)dx,
+                         (float*)dres, total, C, S, nhwc, act, training);
+    return (int)hipGetLastError();
+  }
   const dim3 g(stride_grid(total, 256));
   if (dtype)
     hipLaunchKernelGGL(bn_bwd_apply<bf16_t>, g, dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)y,

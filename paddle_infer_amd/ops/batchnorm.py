@@ -34,17 +34,21 @@ def _layout(x, data_format):
 def _supported(x, nhwc, C):
     if not (x.is_cuda and x.dtype in (torch.float32, torch.bfloat16)):
         return False
-    return not nhwc or C >= 256 or 256 % C == 0
+    return not nhwc or C % 8 == 0 or C >= 256 or 256 % C == 0
 
 
 def _reference(x, running_mean, running_var, weight, bias, training, momentum, eps, act,
                residual, data_format):
     nhwc = data_format in ("NHWC", "NLC", "NDHWC")
+    dt = x.dtype
     xin = x.movedim(-1, 1) if nhwc else x
+    if dt in (torch.bfloat16, torch.float16):  # f32 statistics, like the kernels
+        xin = xin.float()
     y = TF.batch_norm(xin, running_mean, running_var, weight, bias, training, 1.0 - momentum, eps)
     y = y.movedim(1, -1) if nhwc else y
     if residual is not None:
-        y = y + residual
+        y = y + residual.to(y.dtype)
+    y = y.to(dt)
     if act == 1:
         y = torch.relu(y)
     elif act == 2:

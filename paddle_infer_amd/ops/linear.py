@@ -62,6 +62,7 @@ def _use_transposed(x2, w):
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda")  # backward replays the forward's autocast state
     def forward(ctx, x, w, b):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
@@ -77,6 +78,7 @@ class _LinearFn(torch.autograd.Function):
         return y.view(*shp[:-1], w.shape[1])
 
     @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
     def backward(ctx, dy):
         x2, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, w.shape[1])

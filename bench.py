@@ -126,7 +126,8 @@ def main():
     par = (f"tp{tp}" if tp > 1 else "") + f"dp{dp}" + (f"_sharding{args.sharding}" if dp > 1 and args.sharding else "")
     if rank == 0:
         print(json.dumps({
-            "metric": METRIC, "value": round(tps, 1), "unit": "tokens/s", "n_gpus": world,
+            "metric": METRIC if args.model == "gpt3-1.3b" else f"tokens/sec {args.model} training",
+            "value": round(tps, 1), "unit": "tokens/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 2),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (random token ids, random-init weights)",

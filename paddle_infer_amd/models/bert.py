@@ -72,13 +72,15 @@ class BertEmbeddings(Layer):
         self.cfg = cfg
 
     def forward(self, input_ids, token_type_ids=None, position_ids=None):
-        B, S = input_ids.shape
-        if position_ids is None:
-            position_ids = torch.arange(S, device=input_ids.device).unsqueeze(0).expand(B, S)
+        S = input_ids.shape[1]
         if token_type_ids is None:
             token_type_ids = torch.zeros_like(input_ids)
         we = F.embedding(input_ids, self.word_embeddings)
-        extra = F.embedding(position_ids, self.position_embeddings) + F.embedding(token_type_ids, self.token_type_embeddings)
+        # default positions 0..S-1: the first S rows of the table, broadcast over the batch (no
+        # batch-sized index tensor, so a traced export keeps a symbolic batch dim)
+        pos = (self.position_embeddings[:S].unsqueeze(0) if position_ids is None
+               else F.embedding(position_ids, self.position_embeddings))
+        extra = pos + F.embedding(token_type_ids, self.token_type_embeddings)
         p = self.cfg.hidden_dropout_prob if self.training else 0.0
         # LN(dropout(word + pos + type)) — dropout applies to the sum in the reference; here the
         # position/type sum is the residual input of the fused LN (dropout on the word part)
@@ -134,7 +136,9 @@ class BertModel(Layer):
     def forward(self, input_ids, token_type_ids=None, position_ids=None, attention_mask=None):
         x = self.embeddings(input_ids, token_type_ids, position_ids)
         mask = None
-        if attention_mask is None and self.cfg.pad_token_id is not None:
+        # the padding scan is data-dependent: a traced export (meta inputs) takes the mask as an
+        # explicit input instead
+        if attention_mask is None and self.cfg.pad_token_id is not None and not input_ids.is_meta:
             pad = input_ids == self.cfg.pad_token_id
             if bool(pad.any()):
                 attention_mask = ~pad

@@ -124,5 +124,14 @@ def linear(x, weight, bias=None):
     """y = x @ weight (+ bias); weight is ``[in_features, out_features]``."""
     if weight.requires_grad or getattr(weight, "main_grad", None) is not None:
         return _LinearFn.apply(x, weight, bias)
-    y = torch.matmul(x, weight)
-    return y + bias if bias is not None else y
+    # inference weights: same K-contiguous cached copy + bias-in-epilogue GEMM as training
+    shp = x.shape
+    x2 = x.reshape(-1, shp[-1])
+    if not _use_transposed(x2, weight):
+        y = torch.matmul(x, weight)
+        return y + bias if bias is not None else y
+    wf = transposed(weight).t()
+    y = torch.addmm(bias, x2, wf) if bias is not None and bias.dtype == x2.dtype else torch.mm(x2, wf)
+    if bias is not None and bias.dtype != x2.dtype:
+        y = y + bias
+    return y.view(*shp[:-1], weight.shape[1])

@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--tail", type=int, default=0, help="also analyse the last N dispatches")
     ap.add_argument("--csv", default=None)
+    ap.add_argument("--seq", type=int, default=0,
+                    help="print the last N dispatches in order (name, grid, duration, gap)")
     a = ap.parse_args()
     rows = load(a.db)
     tot, out = summarize(rows, a.top)
@@ -59,6 +61,14 @@ def main():
         t2, out2 = summarize(sub, a.top)
         for r in out2:
             print(f"{r[0]:90s} {r[1]:7d} {r[2]:10.1f} {r[3]:9.2f} {r[4]:6.1f}")
+    if a.seq:
+        sub = rows[-a.seq:]
+        prev = None
+        print(f"\n{'#':>5s} {'dur_us':>9s} {'gap_us':>8s} {'grid':>18s}  kernel")
+        for i, (name, s, e, gx, gy, gz, wx) in enumerate(sub):
+            gap = (s - prev) / 1e3 if prev is not None else 0.0
+            prev = e
+            print(f"{i:5d} {(e - s) / 1e3:9.1f} {gap:8.1f} {f'{gx}x{gy}x{gz}/{wx}':>18s}  {short(name, 110)}")
 
 
 if __name__ == "__main__":

@@ -214,10 +214,14 @@ class _Linear:
                                            "int4" if self.bits == 4 else "int8", act)
         if self.packed is not None and x.is_cuda and x.numel() // x.shape[-1] <= self.PACKED_MAX_M:
             return _inf.packed_linear(x, self.packed, bias, act)
-        y = F.linear(x, self.w) if self.trans else torch.matmul(x, self.w)
-        if act != "none":
-            return ops.bias_act(y, bias, act)
-        return y if bias is None else y + bias
+        from ...ops.linear import linear as _dense, linear_bias_act
+        if act != "none" and bias is not None:  # one epilogue GEMM when eligible (inference)
+            return linear_bias_act(x, self.w, bias, act, weight_out_in=self.trans)
+        if self.trans:
+            y = F.linear(x, self.w, bias if act == "none" else None)
+        else:  # [in, out] weight: cached K-contiguous copy, bias in the GEMM epilogue
+            y = _dense(x, self.w, bias if act == "none" else None)
+        return ops.bias_act(y, bias, act) if act != "none" else y
 
 
 def _lin(w, scale=None, bits=0, trans=False, act_scale=None):

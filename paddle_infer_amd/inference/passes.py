@@ -13,6 +13,8 @@ a chain of Paddle ops and rewrites it into one fused op whose kernel is register
   skip_layernorm_fuse_pass        elementwise_add + layer_norm         → skip_layernorm
   embedding_eltwise_layernorm_fuse_pass  lookup_table×N + adds + LN    → fused_embedding_eltwise_layernorm
   self_attention_fuse_pass        matmul(QKᵀ)[·α] + softmax + matmul(V) → flash_attn
+  linear_bias_act_fuse_pass       traced linear(no bias) + fused_bias_act → one GEMM with the
+                                  bias+act epilogue (`ops.linear.linear_bias_act`)
 
 Passes only rewrite when every intermediate has exactly one consumer and is not fetched.
 """
@@ -335,10 +337,42 @@ def self_attention_fuse_pass(g: Graph):
     return n
 
 
+def linear_bias_act_fuse_pass(g: Graph):
+    """Traced programs (``jit.save`` of dygraph models) record ``linear`` and ``fused_bias_act``
+    as torch-callable ops; fold the pair into one epilogue GEMM."""
+    from ..ops import linear as L
+    from ..static.framework import VarRef
+    n = 0
+    for lin in list(g.ops):
+        if lin.type != "linear" or lin.func is None or lin not in g.ops:
+            continue
+        args = tuple(lin.args) + (None,) * (3 - len(lin.args))
+        if lin.kwargs or len(lin.args) > 3 or args[2] is not None:
+            continue
+        outs = lin.output_names()
+        if len(outs) != 1 or not g.single_use(outs[0]):
+            continue
+        ba = g.consumers(outs[0])[0]
+        if ba.type != "fused_bias_act" or ba.func is None or ba.kwargs:
+            continue
+        bargs = tuple(ba.args)
+        if not bargs or not isinstance(bargs[0], VarRef) or bargs[0].name != outs[0]:
+            continue
+        bias = bargs[1] if len(bargs) > 1 else None
+        act = bargs[2] if len(bargs) > 2 else "gelu"
+        if not isinstance(bias, VarRef) or act not in L._EPILOGUE_ACTS:
+            continue
+        fused = Operator(g.block, L.linear_bias_act, (args[0], args[1], bias, act), {}, ba.outputs,
+                         type="fc")
+        g.replace([lin, ba], fused)
+        n += 1
+    return n
+
+
 GPU_PASSES = [
     "delete_dropout_op_pass", "identity_scale_op_clean_pass", "conv_bn_fuse_pass",
     "embedding_eltwise_layernorm_fuse_pass", "self_attention_fuse_pass", "fc_fuse_pass",
-    "fc_act_fuse_pass", "skip_layernorm_fuse_pass",
+    "fc_act_fuse_pass", "skip_layernorm_fuse_pass", "linear_bias_act_fuse_pass",
 ]
 
 PASSES = {name: globals()[name] for name in GPU_PASSES}

@@ -339,7 +339,8 @@ def _fc(ins, a):
     x2 = x.reshape(int(np.prod(x.shape[:nc])), -1)
     act = a.get("activation_type", "")
     if act in ("gelu", "relu", "silu", "gelu_tanh") and x2.is_cuda and x2.dtype == torch.bfloat16:
-        y = ops.bias_act(linear(x2, w, None), b, act)
+        from ..ops.linear import linear_bias_act
+        y = linear_bias_act(x2, w, b, act) if b is not None else ops.bias_act(linear(x2, w, None), b, act)
     else:
         y = linear(x2, w, b)
         if act:

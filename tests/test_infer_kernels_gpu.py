@@ -235,3 +235,20 @@ def test_predictor_bf16_hip_graph(tmp_path):
         out = pred.run([torch.from_numpy(X)])[0]
     assert len(pred._graphs) == 1
     _close(out, torch.from_numpy(ref), 5e-2, 3e-2)
+
+
+@pytest.mark.parametrize("act", ["gelu", "gelu_tanh", "relu"])
+def test_linear_bias_act_epilogue(act):
+    """Inference FFN1 as one hipBLASLt epilogue GEMM vs fp32 (tanh-form GELU, the library's
+    epilogue; erf GELU differs from it by < 1e-3)."""
+    from paddle_infer_amd.ops.linear import linear_bias_act
+    torch.manual_seed(0)
+    x = torch.randn(2, 1024, 256, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(256, 1024, device=DEV, dtype=torch.bfloat16) * 256 ** -0.5
+    b = torch.randn(1024, device=DEV, dtype=torch.bfloat16) * 0.1
+    with torch.no_grad():
+        y = linear_bias_act(x, w, b, act)
+    pre = x.float() @ w.float() + b.float()
+    ref = torch.relu(pre) if act == "relu" else torch.nn.functional.gelu(pre, approximate="tanh")
+    assert y.shape == ref.shape and y.dtype == torch.bfloat16
+    _close(y, ref, atol=2e-2)

@@ -252,3 +252,31 @@ def test_gpt_generation_ragged_prompts_and_sampling_and_beam():
             lp = torch.log_softmax(m(seq).float(), -1)
         return lp[:, 5:-1].gather(-1, seq[:, 6:, None]).sum((1, 2))
     assert bool((logp(b) >= logp(g) - 1e-4).all())
+
+
+def test_traced_bert_predictor_symbolic_batch_and_epilogue_pass(tmp_path):
+    """dygraph BERT → jit.save → Predictor: the export keeps a symbolic batch dim (no captured
+    position-id tensor), linear+fused_bias_act pairs fold into one epilogue GEMM op, and outputs
+    match the dygraph model at two batch sizes."""
+    from paddle_infer_amd import jit
+    from paddle_infer_amd.models.bert import BertModel, bert_config
+    from paddle_infer_amd.static import InputSpec
+    torch.manual_seed(0)
+    m = BertModel(bert_config("bert-tiny"))
+    m.eval()
+    st = jit.to_static(m, input_spec=[InputSpec([None, 16], "int64", "input_ids")])
+    path = str(tmp_path / "bert")
+    jit.save(st, path)
+    pred = pinf.create_predictor(pinf.Config(path + ".pdmodel", path + ".pdiparams"))
+    assert pred.pass_stats["linear_bias_act_fuse_pass"] == 2
+    assert "fused_bias_act" not in [o.type for o in pred.program.global_block().ops]
+    for B in (2, 5):
+        ids = torch.randint(1, 1000, (B, 16))
+        seq, pooled = m(ids)
+        pred.get_input_handle("input_ids").copy_from_cpu(ids.numpy())
+        assert pred.run()
+        names = pred.get_output_names()
+        np.testing.assert_allclose(pred.get_output_handle(names[0]).copy_to_cpu(),
+                                   seq.detach().numpy(), rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(pred.get_output_handle(names[1]).copy_to_cpu(),
+                                   pooled.detach().numpy(), rtol=1e-5, atol=1e-5)

@@ -45,6 +45,9 @@ def main():
     ap.add_argument("--dropout", type=float, default=0.1)
     ap.add_argument("--recompute", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: gloo + the ops' CPU reference paths (rehearses the multi-rank driver "
+                         "command without a GPU; not a performance number)")
     ap.add_argument("--tuned-gemm", type=int, default=0,
                     help="replay the in-tree TunableOp GEMM table (paddle_infer_amd/tuning)")
     args = ap.parse_args()
@@ -54,11 +57,23 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    on_gpu = args.device == "cuda"
+    if on_gpu:
+        torch.cuda.set_device(local_rank)
+        device = torch.device("cuda", local_rank)
+    else:
+        device = torch.device("cpu")
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
+
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=device)
+        if on_gpu:
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
 
     import paddle_infer_amd as pia
     from paddle_infer_amd.incubate import autotune
@@ -101,18 +116,18 @@ def main():
 
     for _ in range(args.warmup):
         loss = step()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
     trainer.wait_params()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
@@ -140,7 +155,7 @@ def main():
                        "optimizer": "AdamW fp32 master", "grad_clip": 1.0},
             "tflops_per_gpu": round(tflops_gpu, 1), "final_loss": round(final_loss, 4),
             "tuned_gemm_table": bool(tuned),
-            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1),
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1) if on_gpu else None,
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -76,7 +76,8 @@ _SIGS = {
 
 
 def lib_path() -> str:
-    return _build.KERNEL_LIB
+    # PIAMD_KERNEL_LIB: load another build of the kernel library (A/B timing of a kernel edit)
+    return os.environ.get("PIAMD_KERNEL_LIB") or _build.KERNEL_LIB
 
 
 def _load():

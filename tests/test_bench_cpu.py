@@ -1,0 +1,40 @@
+"""The driver's multi-rank bench command, rehearsed on the CPU (gloo + the ops' CPU reference
+paths): ``python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`` must print
+exactly one JSON line from rank 0 with the contract's fields, for plain sharded DP and for a
+TP × DP mesh."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+        "scaling", "vs_baseline", "dtype", "data", "config"}
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("n,extra,par", [(2, [], "dp2_sharding1"), (4, ["--tp", "2"], "tp2dp2_sharding1")])
+def test_bench_multirank_contract(n, extra, par):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(n), "--steps", "2", "--warmup", "1", "--device", "cpu", "--model", "gpt3-tiny",
+           "--seq", "64", "--micro-batch", "2"] + extra
+    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=ROOT)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert KEYS <= set(out)
+    assert out["n_gpus"] == n and out["steps"] == 2 and out["warmup"] == 1
+    assert out["config"]["parallelism"] == par
+    assert out["config"]["global_batch"] == 2 * (n // (2 if extra else 1))
+    assert out["value"] > 0 and out["final_loss"] == out["final_loss"]

@@ -402,16 +402,6 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(
   };
   if (total > 0) issue(0, 0);
   __syncthreads();
-  // The wave's own 32 keys are the B operand of S and dP at every q tile: hold their K and V
-  // fragments in registers (2 x KSTEPS x 4 VGPRs) instead of re-reading 16 KiB of LDS per tile —
-  // a fifth of the kernel's LDS traffic.
-  bf16x8 kf[KSTEPS], vf[KSTEPS];
-#pragma unroll
-  for (int kk = 0; kk < KSTEPS; ++kk) {
-    const int koff = lds_off<ROWB>(32 * w + l32, 2 * kk + hh);
-    kf[kk] = lds_row8(kimg, koff);
-    vf[kk] = lds_row8(vimg, koff);
-  }
 
   for (int it = 0; it < total; ++it) {
     const int buf = it & 1;
@@ -436,9 +426,12 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(
       for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
         for (int j = 0; j < 16; ++j) { sacc[qt][j] = 0.f; pacc[qt][j] = 0.f; }
-      // S = Q·Kᵀ, dP = dO·Vᵀ with the next k-step's 4 Q/dO fragments loaded one step ahead
+      // S = Q·Kᵀ, dP = dO·Vᵀ with the next k-step's 6 fragments loaded one step ahead
       bf16x8 fr[2][6];
       auto ld = [&](int kk, bf16x8* f) {
+        const int koff = lds_off<ROWB>(32 * w + l32, 2 * kk + hh);
+        f[0] = lds_row8(kimg, koff);
+        f[1] = lds_row8(vimg, koff);
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt) {
           const int qoff = lds_off<ROWB>(qt * 32 + l32, 2 * kk + hh);
@@ -453,8 +446,8 @@ __global__ __launch_bounds__(256, 1) void fa_bwd_dkdv_kernel(
         const bf16x8* f = fr[kk & 1];
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt) {
-          sacc[qt] = mfma32(f[2 + qt], kf[kk], sacc[qt]);
-          pacc[qt] = mfma32(f[4 + qt], vf[kk], pacc[qt]);
+          sacc[qt] = mfma32(f[2 + qt], f[0], sacc[qt]);
+          pacc[qt] = mfma32(f[4 + qt], f[1], pacc[qt]);
         }
         __builtin_amdgcn_sched_barrier(0);
       }

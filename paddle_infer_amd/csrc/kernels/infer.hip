@@ -450,15 +450,21 @@ __device__ __forceinline__ float act_apply(float v, int act) {
 #ifndef WO_UNROLL
 #define WO_UNROLL 8  // k-blocks per wave per iteration: 8 x 16 B weight loads in flight per lane
 #endif
-template <int BITS>
+// LNP (decode, KS == 1, M ≤ 8): the workgroup LayerNorms its input rows into LDS first (shifted-sum
+// statistics in one pass over registers, then γ/β), so the pre-LN of a transformer layer needs no
+// launch of its own. `resid` (nullable): y = act(acc·scale + bias) + resid — the residual add of
+// the out-proj / FFN2 projection folded into the epilogue.
+template <int BITS, bool LNP>
 __global__ __launch_bounds__(256) void wo_gemm_kernel(
     const bf16_t* __restrict__ x, long long ldx, const unsigned char* __restrict__ wp,
     const float* __restrict__ scale, const bf16_t* __restrict__ bias, bf16_t* __restrict__ y,
     long long ldy, float* __restrict__ ws, int* __restrict__ cnt, int M, int N, int K, int act,
-    const int* __restrict__ offs, int E, long long wstride) {
+    const int* __restrict__ offs, int E, long long wstride, const bf16_t* __restrict__ ln_g,
+    const bf16_t* __restrict__ ln_b, float eps, const bf16_t* __restrict__ resid, long long ldr) {
   constexpr int KB = BITS == 16 ? 16 : (BITS == 8 ? 32 : 64);  // k per block (16 B lane load)
   constexpr int NMF = KB / 16;               // MFMAs per block
   __shared__ float red[3][16][64];
+  extern __shared__ __attribute__((aligned(16))) char xln[];  // LNP: [rows][K] bf16, row pitch K*2+16
   const int nt = blockIdx.x, kz = blockIdx.z, KS = gridDim.z;
   int mt = blockIdx.y, mbase = 0;
   if (offs) {
@@ -484,7 +490,8 @@ __global__ __launch_bounds__(256) void wo_gemm_kernel(
   const int m = min(mbase + (lane & 31), M - 1);  // rows ≥ M compute duplicates, never stored
   const bf16_t* xr = x + (long long)m * ldx + (KB / 2) * (lane >> 5);
   const uint4* wt = (const uint4*)wp + (long long)nt * nkb * 64 + lane;
-
+  const long long pitch = (long long)K * 2 + 16;  // LDS row pitch: +16 B keeps row reads conflict-free
+  const char* xl = xln + (long long)(m - mbase) * pitch + (KB / 2) * (lane >> 5) * 2;
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -493,21 +500,86 @@ __global__ __launch_bounds__(256) void wo_gemm_kernel(
   // MFMAs, so each lane keeps 2·U 16-B weight loads in flight (the GEMV is an HBM stream)
   uint4 wv[U];
   bf16x8 xa[U][NMF];
-  auto load_group = [&](int kb0, uint4 (&wd)[U], bf16x8 (&xd)[U][NMF]) {
+  auto load_w = [&](int kb0, uint4 (&wd)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) wd[u] = wt[(long long)min(kb0 + 4 * u, kb_end - 1) * 64];
+  };
+  auto load_x = [&](int kb0, bf16x8 (&xd)[U][NMF]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int kb = min(kb0 + 4 * u, kb_end - 1);
-      wd[u] = wt[(long long)kb * 64];
 #pragma unroll
-      for (int i = 0; i < NMF; ++i) xd[u][i] = *(const bf16x8*)(xr + (long long)kb * KB + 8 * i);
+      for (int i = 0; i < NMF; ++i)
+        xd[u][i] = LNP ? *(const bf16x8*)(xl + ((long long)kb * KB + 8 * i) * 2)
+                       : *(const bf16x8*)(xr + (long long)kb * KB + 8 * i);
     }
   };
-  if (kb_beg + w < kb_end) load_group(kb_beg + w, wv, xa);
+  // the first weight group is requested BEFORE the LayerNorm prologue: its HBM latency covers the
+  // prologue's L2 round trip
+  if (kb_beg + w < kb_end) load_w(kb_beg + w, wv);
+  if (LNP) {
+    // ≤ 8 rows (M ≤ 8), K % 512 == 0, K ≤ 2048: thread t holds chunk t of each row (16 B), each
+    // wave's 64 chunks lie in one row → wave sums + ≤ 4 LDS atomics per row
+    __shared__ float st[2][8];
+    const int rows_t = min(8, M - mbase);
+    const int cpr = K >> 3;  // 16-B chunks per row
+    if (threadIdx.x < 16) st[threadIdx.x / 8][threadIdx.x % 8] = 0.f;
+    u16x8 v[8], g[8], b[8];
+    float sh[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      if (c < rows_t * cpr) {
+        const int rr = c / cpr, cc = c % cpr;
+        const bf16_t* row = x + (long long)(mbase + rr) * ldx;
+        v[i] = *reinterpret_cast<const u16x8*>(row + 8 * cc);
+        g[i] = *reinterpret_cast<const u16x8*>(ln_g + 8 * cc);
+        b[i] = *reinterpret_cast<const u16x8*>(ln_b + 8 * cc);
+        sh[i] = bf2f(row[0]);  // shifted sums: a stable single-pass variance
+      }
+    }
+    __syncthreads();  // st zeroed
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c0 = (threadIdx.x & ~63) + 256 * i;  // wave-uniform
+      if (c0 < rows_t * cpr) {
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { const float d = bf2f(v[i][j]) - sh[i]; s1 += d; s2 += d * d; }
+        s1 = wave_sum(s1);
+        s2 = wave_sum(s2);
+        if (lane == 0) {
+          atomicAdd(&st[0][c0 / cpr], s1);
+          atomicAdd(&st[1][c0 / cpr], s2);
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = threadIdx.x + 256 * i;
+      if (c < rows_t * cpr) {
+        const int rr = c / cpr, cc = c % cpr;
+        const float dm = st[0][rr] / K;  // mean − shift
+        const float mu = sh[i] + dm;
+        const float rs = rsqrtf(fmaxf(st[1][rr] / K - dm * dm, 0.f) + eps);
+        u16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = f2bf((bf2f(v[i][j]) - mu) * rs * bf2f(g[i][j]) + bf2f(b[i][j]));
+        *reinterpret_cast<u16x8*>(xln + (long long)rr * pitch + 16 * cc) = o;
+      }
+    }
+    __syncthreads();
+  }
+  if (kb_beg + w < kb_end) load_x(kb_beg + w, xa);
   for (int kb0 = kb_beg + w; kb0 < kb_end; kb0 += 4 * U) {
     uint4 wn[U];
     bf16x8 xn[U][NMF];
     const bool more = kb0 + 4 * U < kb_end;
-    if (more) load_group(kb0 + 4 * U, wn, xn);
+    if (more) {
+      load_w(kb0 + 4 * U, wn);
+      load_x(kb0 + 4 * U, xn);
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (kb0 + 4 * u >= kb_end) {  // zero the weight operand: the MFMA then adds nothing
@@ -550,7 +622,9 @@ __global__ __launch_bounds__(256) void wo_gemm_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int mm = mbase + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      if (mm < M) y[(long long)mm * ldy + n] = f2bf(act_apply(acc[r] * sc + bs, act));
+      if (mm < M)
+        y[(long long)mm * ldy + n] = f2bf(act_apply(acc[r] * sc + bs, act) +
+                                          (resid ? bf2f(resid[(long long)mm * ldr + n]) : 0.f));
     }
     return;
   }
@@ -581,7 +655,8 @@ __global__ __launch_bounds__(256) void wo_gemm_kernel(
     const int mm = mbase + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
     if (mm < M) {
       const float v = xcd_take(ws + (long long)mm * N + n);
-      y[(long long)mm * ldy + n] = f2bf(act_apply(v * sc + bs, act));
+      y[(long long)mm * ldy + n] = f2bf(act_apply(v * sc + bs, act) +
+                                        (resid ? bf2f(resid[(long long)mm * ldr + n]) : 0.f));
     }
   }
   if (lane == 0) atomicExch(&cnt[mt * gridDim.x + nt], 0);
@@ -589,7 +664,8 @@ __global__ __launch_bounds__(256) void wo_gemm_kernel(
 
 __global__ void wo_finalize_kernel(const float* __restrict__ ws, int KS, const float* __restrict__ scale,
                                    const bf16_t* __restrict__ bias, bf16_t* __restrict__ y, long long ldy,
-                                   int M, int N, int act) {
+                                   int M, int N, int act, const bf16_t* __restrict__ resid,
+                                   long long ldr) {
   const long long total = (long long)M * N;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
@@ -597,7 +673,7 @@ __global__ void wo_finalize_kernel(const float* __restrict__ ws, int KS, const f
     float v = 0.f;
     for (int z = 0; z < KS; ++z) v += ws[(long long)z * total + i];
     v = v * (scale ? scale[n] : 1.f) + (bias ? bf2f(bias[n]) : 0.f);
-    y[(i / N) * ldy + n] = f2bf(act_apply(v, act));
+    y[(i / N) * ldy + n] = f2bf(act_apply(v, act) + (resid ? bf2f(resid[(i / N) * ldr + n]) : 0.f));
   }
 }
 
@@ -609,31 +685,53 @@ __global__ void wo_finalize_kernel(const float* __restrict__ ws, int KS, const f
 static void wo_launch(int bits, dim3 grid, hipStream_t st, const void* x, long long ldx,
                       const void* wp, const float* scale, const void* bias, void* y, long long ldy,
                       float* ws, int* cnt, int M, int N, int K, int act, const int* offs, int E,
-                      long long wstride) {
-#define WO_LAUNCH(B)                                                                              \
-  hipLaunchKernelGGL(wo_gemm_kernel<B>, grid, dim3(256), 0, st, (const bf16_t*)x, ldx,           \
+                      long long wstride, const void* ln_g = nullptr, const void* ln_b = nullptr,
+                      float eps = 0.f, const void* resid = nullptr, long long ldr = 0) {
+  const size_t lds = ln_g ? (size_t)min(M, 32) * ((size_t)K * 2 + 16) : 0;
+#define WO_LAUNCH(B, L)                                                                           \
+  hipLaunchKernelGGL((wo_gemm_kernel<B, L>), grid, dim3(256), lds, st, (const bf16_t*)x, ldx,    \
                      (const unsigned char*)wp, scale, (const bf16_t*)bias, (bf16_t*)y, ldy, ws,   \
-                     cnt, M, N, K, act, offs, E, wstride)
-  if (bits == 16) WO_LAUNCH(16);
-  else if (bits == 8) WO_LAUNCH(8);
-  else WO_LAUNCH(4);
+                     cnt, M, N, K, act, offs, E, wstride, (const bf16_t*)ln_g,                    \
+                     (const bf16_t*)ln_b, eps, (const bf16_t*)resid, ldr)
+  if (ln_g) {
+    if (bits == 16) WO_LAUNCH(16, true);
+    else if (bits == 8) WO_LAUNCH(8, true);
+    else WO_LAUNCH(4, true);
+  } else {
+    if (bits == 16) WO_LAUNCH(16, false);
+    else if (bits == 8) WO_LAUNCH(8, false);
+    else WO_LAUNCH(4, false);
+  }
 #undef WO_LAUNCH
+}
+
+// Extended form: ln_g/ln_b (nullable, bf16 [K]): y = act(LN(x)·Wᵀ·scale + bias) with the
+// LayerNorm (ε = eps) computed in the prologue — requires KS == 1, M ≤ 8, K % 512 == 0, K ≤ 2048;
+// resid (nullable, bf16 rows of pitch ldr): + resid[m, n] after the activation.
+PIAMD_EXPORT int piamd_wo_gemm_ex(int bits, const void* x, long long ldx, const void* wp,
+                                  const float* scale, const void* bias, void* y, long long ldy,
+                                  float* ws, int* cnt, int M, int N, int K, int KS, int act,
+                                  const void* ln_g, const void* ln_b, float eps, const void* resid,
+                                  long long ldr, hipStream_t st) {
+  const int KB = bits == 16 ? 16 : (bits == 8 ? 32 : 64);
+  if ((bits != 16 && bits != 8 && bits != 4) || N % 32 || K % KB || KS < 1 ||
+      (KS > 1 && !ws) || M < 1 || (ln_g && (!ln_b || KS != 1 || K % 512 || K > 2048 || M > 8)))
+    return (int)hipErrorInvalidValue;
+  wo_launch(bits, dim3(N / 32, (M + 31) / 32, KS), st, x, ldx, wp, scale, bias, y, ldy, ws, cnt,
+            M, N, K, act, nullptr, 0, 0, ln_g, ln_b, eps, resid, ldr);
+  if (KS > 1 && !cnt)
+    hipLaunchKernelGGL(wo_finalize_kernel, dim3(stride_grid((long long)M * N, 256)), dim3(256), 0,
+                       st, ws, KS, scale, (const bf16_t*)bias, (bf16_t*)y, ldy, M, N, act,
+                       (const bf16_t*)resid, ldr);
+  return (int)hipGetLastError();
 }
 
 PIAMD_EXPORT int piamd_wo_gemm(int bits, const void* x, long long ldx, const void* wp,
                                const float* scale, const void* bias, void* y, long long ldy,
                                float* ws, int* cnt, int M, int N, int K, int KS, int act,
                                hipStream_t st) {
-  const int KB = bits == 16 ? 16 : (bits == 8 ? 32 : 64);
-  if ((bits != 16 && bits != 8 && bits != 4) || N % 32 || K % KB || KS < 1 ||
-      (KS > 1 && !ws) || M < 1)
-    return (int)hipErrorInvalidValue;
-  wo_launch(bits, dim3(N / 32, (M + 31) / 32, KS), st, x, ldx, wp, scale, bias, y, ldy, ws, cnt,
-            M, N, K, act, nullptr, 0, 0);
-  if (KS > 1 && !cnt)
-    hipLaunchKernelGGL(wo_finalize_kernel, dim3(stride_grid((long long)M * N, 256)), dim3(256), 0,
-                       st, ws, KS, scale, (const bf16_t*)bias, (bf16_t*)y, ldy, M, N, act);
-  return (int)hipGetLastError();
+  return piamd_wo_gemm_ex(bits, x, ldx, wp, scale, bias, y, ldy, ws, cnt, M, N, K, KS, act,
+                          nullptr, nullptr, 0.f, nullptr, 0, st);
 }
 
 // Grouped weight-only expert GEMM (the decode / small-batch MoE path of

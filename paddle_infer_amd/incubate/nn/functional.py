@@ -16,6 +16,7 @@ How they map onto the hardware (instead of the reference's one-CUDA-op-per-layer
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -206,7 +207,26 @@ class _Linear:
                 self.packed = _inf.pack_bf16(w.detach())
         return self
 
-    def __call__(self, x, bias=None, act="none"):
+    def fused_gemv(self, M):
+        """True when a call with M rows runs the weight-stream GEMV, which takes the pre-LN in its
+        prologue and the residual add in its epilogue (no separate launches)."""
+        if M > FUSED_LN_MAX_M:  # the per-workgroup LN prologue grows with M; the saved launch does not
+            return False
+        return self.bits in (4, 8) or self.packed is not None
+
+    def __call__(self, x, bias=None, act="none", ln=None, resid=None):
+        if ln is not None or resid is not None:
+            M = x.numel() // x.shape[-1]
+            if self.bits in (4, 8):
+                return _inf.weight_only_linear(x, self.w, bias, self.scale,
+                                               "int4" if self.bits == 4 else "int8", act, ln=ln,
+                                               resid=resid)
+            if self.packed is not None and x.is_cuda and M <= self.PACKED_MAX_M:
+                return _inf.packed_linear(x, self.packed, bias, act, ln=ln, resid=resid)
+            if ln is not None:
+                x = ops.layer_norm(x, ln[0], ln[1], ln[2])
+            y = self(x, bias, act)
+            return y + resid.reshape(y.shape) if resid is not None else y
         if self.bits == -8:  # int8 x int8 MFMA GEMM, dequantising epilogue (FusedMultiTransformerINT8)
             return _inf.int8_linear(x, self.w, self.scale, bias, self.act_scale, act)
         if self.bits:
@@ -222,6 +242,12 @@ class _Linear:
         else:  # [in, out] weight: cached K-contiguous copy, bias in the GEMM epilogue
             y = _dense(x, self.w, bias if act == "none" else None)
         return ops.bias_act(y, bias, act) if act != "none" else y
+
+
+# decode rows up to which each layer's pre-LN / residual adds ride in the GEMV prologue / epilogue.
+# Measured (GPT-1.3B decode, profiles/decode_fused_ln_sweep_r1.txt): fusing wins at batch 1-2
+# (+4-12 % tok/s) and loses from batch 4 (the LN prologue forces KS=1 and grows with M).
+FUSED_LN_MAX_M = int(os.environ.get("PIAMD_FUSED_LN_MAX_M", "2"))
 
 
 def _lin(w, scale=None, bits=0, trans=False, act_scale=None):
@@ -254,6 +280,34 @@ def multi_transformer_forward(x, layers, num_heads, num_kv_heads=None, pre_layer
     if decode and attn_mask is not None:
         attn_mask = _to_additive_mask(attn_mask, x.dtype).reshape(B, -1).contiguous()
     xf = x.reshape(T, E)
+    if (decode and pre_layer_norm and group is None and not gated and moe_fn is None
+            and x.dtype == torch.bfloat16
+            and all(L.get("moe") is None
+                    and all(L.get(k) is not None and L[k].dtype == torch.bfloat16
+                            for k in ("ln_scale", "ln_bias", "ffn_ln_scale", "ffn_ln_bias"))
+                    and all(isinstance(L[k], _Linear) and L[k].fused_gemv(T)
+                            for k in ("qkv", "out", "ffn1", "ffn2")) for L in layers)):
+        # decode: every projection is a weight-stream GEMV, so each pre-LN runs in the prologue of
+        # the GEMV that consumes it and each residual add in the epilogue of the projection that
+        # produces it — per layer QKV GEMV → attention → out GEMV → FFN1 GEMV → FFN2 GEMV, with no
+        # LayerNorm launches (2 fewer kernels per layer on a launch-latency-bound step)
+        residual = xf
+        for li, L in enumerate(layers):
+            qkv = L["qkv"](residual, ln=(L["ln_scale"], L["ln_bias"], epsilon))
+            kc, vc = caches[li] if caches is not None else (None, None)
+            a = _inf.decode_attention(qkv, kc, vc, lens, hq, hk, attn_mask, max_len=max_len,
+                                      prep_bias=L.get("qkv_bias"), prep=True, rot_dim=rotary_dim,
+                                      neox=neox_rotary, base=rope_base)
+            residual = L["out"](a, L.get("out_bias"), resid=residual)
+            h = L["ffn1"](residual, L.get("ffn1_bias"), act,
+                          ln=(L["ffn_ln_scale"], L["ffn_ln_bias"], epsilon))
+            residual = L["ffn2"](h, L.get("ffn2_bias"), resid=residual)
+        if final_ln is not None:
+            out = ops.layer_norm(residual, final_ln[0], final_ln[1],
+                                 final_ln[2] if len(final_ln) > 2 else epsilon)
+        else:
+            out = residual
+        return out.reshape(B, S, E)
     residual = xf
     pending = None  # (ffn2_out, ffn2_bias) to fold into the next LN pass
     n = len(layers)

@@ -190,28 +190,56 @@ def pack_bf16(w_kn):
     return t.contiguous().view(N, K)
 
 
-def packed_linear(x, wp, bias=None, act="none"):
-    """y = act(x @ W + bias) with W pre-packed by :func:`pack_bf16` (small-M decode GEMMs: one
-    fully-coalesced 1 KB weight load per wave per MFMA, split-K to fill 256 CUs)."""
+def _ln_ref(x2, ln):
+    g, b, eps = ln
+    return torch.nn.functional.layer_norm(x2.float(), (x2.shape[-1],), g.float(), b.float(), eps)
+
+
+def ln_fusable(M, K, KS=1):
+    """Whether :func:`packed_linear` / :func:`weight_only_linear` can take ``ln=`` (the LayerNorm
+    computed in the GEMV prologue): one K split, M ≤ 8 rows, K % 512 == 0, K ≤ 2048 (beyond that
+    the per-workgroup prologue costs more than the LayerNorm launch it replaces)."""
+    return KS == 1 and K % 512 == 0 and K <= 2048 and 1 <= M <= 8
+
+
+def _wo_call(bits, x2, w, scale, bias, y, M, N, K, KS, act, ln, resid, ws, cnt):
+    lg, lb, eps = ln if ln is not None else (None, None, 0.0)
+    _lib.call("piamd_wo_gemm_ex", bits, x2.data_ptr(), x2.stride(0), w.data_ptr(), _lib.ptr(scale),
+              _lib.ptr(bias), y.data_ptr(), y.stride(0), _lib.ptr(ws), _lib.ptr(cnt), M, N, K, KS,
+              act, _lib.ptr(lg), _lib.ptr(lb), float(eps), _lib.ptr(resid),
+              resid.stride(0) if resid is not None else 0, _lib.stream())
+
+
+def packed_linear(x, wp, bias=None, act="none", ln=None, resid=None):
+    """y = act(LN?(x) @ W + bias) (+ resid) with W pre-packed by :func:`pack_bf16` (small-M decode
+    GEMMs: one fully-coalesced 1 KB weight load per wave per MFMA, split-K to fill 256 CUs).
+    ``ln = (gamma, beta, eps)``: the pre-LayerNorm of the input runs in the GEMV prologue (no LN
+    launch); ``resid`` [M, N]: residual added after the activation in the epilogue."""
     N, K = wp.shape
     lead = x.shape[:-1]
     x2 = x.reshape(-1, K)
     if x2.stride(-1) != 1:
         x2 = x2.contiguous()
     M = x2.shape[0]
+    r2 = resid.reshape(M, N) if resid is not None else None
+    if ln is not None and x.is_cuda and not ln_fusable(M, K):
+        from .norm import layer_norm
+        x2, ln = layer_norm(x2, ln[0], ln[1], ln[2]), None
     if not x.is_cuda:
         w = wp.view(N // 32, K // 16, 2, 32, 8).permute(0, 3, 1, 2, 4).reshape(N, K)
-        y = x2.float() @ w.float().t()
+        xin = _ln_ref(x2, ln).to(x.dtype) if ln is not None else x2
+        y = xin.float() @ w.float().t()
         if bias is not None:
             y = y + bias.float()
-        return _ref_act(y, ACTS[act]).to(x.dtype).reshape(*lead, N)
+        y = _ref_act(y, ACTS[act])
+        if r2 is not None:
+            y = y + r2.float()
+        return y.to(x.dtype).reshape(*lead, N)
     y = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
     tiles = (N // 32) * ((M + 31) // 32)
-    KS = _split_k(tiles, K // 16)
+    KS = 1 if ln is not None else _split_k(tiles, K // 16)
     ws, cnt = _splitk_bufs(x.device, KS, M, N, tiles)
-    _lib.call("piamd_wo_gemm", 16, x2.data_ptr(), x2.stride(0), wp.data_ptr(), None,
-              _lib.ptr(bias), y.data_ptr(), y.stride(0), _lib.ptr(ws), _lib.ptr(cnt), M, N, K, KS,
-              ACTS[act], _lib.stream())
+    _wo_call(16, x2, wp, None, bias, y, M, N, K, KS, ACTS[act], ln, r2, ws, cnt)
     return y.reshape(*lead, N)
 
 
@@ -281,8 +309,9 @@ _WS = {}
 
 
 def weight_only_linear(x, weight, bias=None, weight_scale=None, weight_dtype="int8",
-                       act_method="none"):
-    """y = act(x @ dequant(weight)ᵀ + bias); x [..., K], weight packed [N, K] / [N/2, K]."""
+                       act_method="none", ln=None, resid=None):
+    """y = act(LN?(x) @ dequant(weight)ᵀ + bias) (+ resid); x [..., K], weight packed [N, K] /
+    [N/2, K]. ``ln`` / ``resid`` as :func:`packed_linear` (GEMV path only)."""
     bits = 4 if weight_dtype == "int4" else 8
     N = weight_scale.shape[0]
     K = x.shape[-1]
@@ -290,6 +319,27 @@ def weight_only_linear(x, weight, bias=None, weight_scale=None, weight_dtype="in
     lead = x.shape[:-1]
     x2 = x.reshape(-1, K)
     M = x2.shape[0]
+    if ln is not None or resid is not None:
+        # fused prologue / epilogue (decode GEMV); other paths apply them around the GEMM
+        if ln is not None and x.is_cuda and not ln_fusable(M, K):
+            from .norm import layer_norm
+            x2, ln = layer_norm(x2, ln[0], ln[1], ln[2]), None
+        if x.is_cuda and M <= 256:
+            if x2.stride(-1) != 1:
+                x2 = x2.contiguous()
+            scale = weight_scale if weight_scale.dtype == torch.float32 else weight_scale.float()
+            y = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+            tiles = (N // 32) * ((M + 31) // 32)
+            KS = 1 if ln is not None else _split_k(tiles, K // (32 if bits == 8 else 64))
+            ws, cnt = _splitk_bufs(x.device, KS, M, N, tiles)
+            _wo_call(bits, x2, weight, scale, bias, y, M, N, K, KS, act, ln,
+                     resid.reshape(M, N) if resid is not None else None, ws, cnt)
+            return y.reshape(*lead, N)
+        xin = _ln_ref(x2, ln).to(x.dtype) if ln is not None else x2
+        y = weight_only_linear(xin, weight, bias, weight_scale, weight_dtype, act_method)
+        if resid is not None:
+            y = (y.float() + resid.reshape(M, N).float()).to(y.dtype)
+        return y.reshape(*lead, N)
     if x.is_cuda:
         assert x.dtype == torch.bfloat16, "weight-only GEMM takes bf16 activations"
         if x2.stride(-1) != 1:

@@ -751,29 +751,66 @@ PIAMD_EXPORT int piamd_wo_moe_gemm(int bits, const void* x, long long ldx, const
 }
 
 // packed → bf16 [N, K] (row-major, no scale when scale == null)
-__global__ void wo_dequant_kernel(int bits, const unsigned char* __restrict__ wp,
-                                  const float* __restrict__ scale, bf16_t* __restrict__ out, int N,
-                                  int K) {
-  const long long total = (long long)N * K;
-  const int KB = bits == 8 ? 32 : 64, nkb = K / KB;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int n = (int)(i / K), k = (int)(i % K);
-    const long long blk = ((long long)(n / 32) * nkb + k / KB) * 64 + (n % 32) + 32 * ((k % KB) / (KB / 2));
-    int q;
-    if (bits == 8) {
-      q = (int)(signed char)wp[blk * 16 + k % 16];
+// One thread per packed 16-B chunk (the lane load of the GEMV layout): coalesced 16-B reads; the
+// 4 waves of a workgroup cover 4 consecutive k-blocks of one 32-row tile, so each output row gets
+// 4 adjacent 32-B (int8) / 64-B (int4) pieces — whole cache lines per workgroup.
+template <int BITS>
+__global__ __launch_bounds__(256) void wo_dequant_kernel(const uint4* __restrict__ wp,
+                                                         const float* __restrict__ scale,
+                                                         bf16_t* __restrict__ out, int N, int K) {
+  constexpr int KB = BITS == 8 ? 32 : 64;
+  const int nkb = K / KB;
+  const long long chunks = (long long)(N / 32) * nkb * 64;
+  for (long long c = (long long)blockIdx.x * blockDim.x + threadIdx.x; c < chunks;
+       c += (long long)gridDim.x * blockDim.x) {
+    const int lane = (int)(c & 63);
+    const long long blk = c >> 6;
+    const int nt = (int)(blk / nkb), kb = (int)(blk % nkb);
+    const int n = nt * 32 + (lane & 31);
+    const int k0 = kb * KB + (lane >> 5) * (KB / 2);
+    const uint4 v = wp[c];
+    const float sc = scale ? scale[n] : 1.f;
+    uint4* dst = reinterpret_cast<uint4*>(out + (long long)n * K + k0);
+    const unsigned w[4] = {v.x, v.y, v.z, v.w};
+    if (BITS == 8) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {  // 8 values per 16-B store
+        unsigned o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const unsigned word = w[2 * h + j / 2];
+          const int q0 = (int)(signed char)(word >> (16 * (j & 1)));
+          const int q1 = (int)(signed char)(word >> (16 * (j & 1) + 8));
+          o[j] = (unsigned)f2bf(q0 * sc) | ((unsigned)f2bf(q1 * sc) << 16);
+        }
+        dst[h] = make_uint4(o[0], o[1], o[2], o[3]);
+      }
     } else {
-      const unsigned char byte = wp[blk * 16 + (k % 32) / 2];
-      q = (int)((unsigned)(k & 1 ? byte >> 4 : byte & 15) << 28) >> 28;
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {  // one 32-bit word = 8 nibbles = 8 values, low nibble first
+        unsigned o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int q0 = (int)(w[h] << (28 - 8 * j)) >> 28;
+          const int q1 = (int)(w[h] << (24 - 8 * j)) >> 28;
+          o[j] = (unsigned)f2bf(q0 * sc) | ((unsigned)f2bf(q1 * sc) << 16);
+        }
+        dst[h] = make_uint4(o[0], o[1], o[2], o[3]);
+      }
     }
-    out[i] = f2bf((float)q * (scale ? scale[n] : 1.f));
   }
 }
 
 PIAMD_EXPORT int piamd_wo_dequant(int bits, const void* wp, const float* scale, void* out, int N,
                                   int K, hipStream_t st) {
-  hipLaunchKernelGGL(wo_dequant_kernel, dim3(stride_grid((long long)N * K, 256)), dim3(256), 0, st,
-                     bits, (const unsigned char*)wp, scale, (bf16_t*)out, N, K);
+  const int KB = bits == 8 ? 32 : 64;
+  if ((bits != 8 && bits != 4) || N % 32 || K % KB) return (int)hipErrorInvalidValue;
+  const dim3 grid(stride_grid((long long)(N / 32) * (K / KB) * 64, 256));
+  if (bits == 8)
+    hipLaunchKernelGGL(wo_dequant_kernel<8>, grid, dim3(256), 0, st, (const uint4*)wp, scale,
+                       (bf16_t*)out, N, K);
+  else
+    hipLaunchKernelGGL(wo_dequant_kernel<4>, grid, dim3(256), 0, st, (const uint4*)wp, scale,
+                       (bf16_t*)out, N, K);
   return (int)hipGetLastError();
 }

@@ -17,6 +17,7 @@ reference of the GPU tests.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -307,6 +308,10 @@ def weight_dequantize(x, scale, algo="weight_only_int8", out_dtype="bfloat16"):
 
 _WS = {}
 
+# rows above which the weight-only GEMM dequantises once and runs the bf16 MFMA GEMM instead of
+# the weight-stream kernel (which re-streams the packed weight once per 32-row tile)
+WO_GEMV_MAX_M = int(os.environ.get("PIAMD_WO_GEMV_MAX_M", "256"))
+
 
 def weight_only_linear(x, weight, bias=None, weight_scale=None, weight_dtype="int8",
                        act_method="none", ln=None, resid=None):
@@ -345,7 +350,7 @@ def weight_only_linear(x, weight, bias=None, weight_scale=None, weight_dtype="in
         if x2.stride(-1) != 1:
             x2 = x2.contiguous()
         scale = weight_scale if weight_scale.dtype == torch.float32 else weight_scale.float()
-        if M > 256:  # compute-bound: dequantize once, MFMA GEMM via hipBLASLt
+        if M > WO_GEMV_MAX_M:  # compute-bound: dequantize once, MFMA GEMM via hipBLASLt
             w = torch.empty((N, K), dtype=torch.bfloat16, device=x.device)
             _lib.call("piamd_wo_dequant", bits, weight.data_ptr(), scale.data_ptr(), w.data_ptr(),
                       N, K, _lib.stream())

@@ -21,6 +21,9 @@ struct IO;
 template <>
 struct IO<true> {
   typedef bf16_t T;
+  typedef u16x8 Raw;  // 8 elements held in 4 VGPRs until used
+  static __device__ __forceinline__ Raw ldraw(const T* p) { return *reinterpret_cast<const Raw*>(p); }
+  static __device__ __forceinline__ float el(const Raw& r, int j) { return bf2f(r[j]); }
   static __device__ __forceinline__ void load8(const T* p, float* v) {
     u16x8 r = *reinterpret_cast<const u16x8*>(p);
 #pragma unroll
@@ -36,6 +39,11 @@ struct IO<true> {
 template <>
 struct IO<false> {
   typedef float T;
+  struct Raw { f32x4 a, b; };
+  static __device__ __forceinline__ Raw ldraw(const T* p) {
+    return Raw{*reinterpret_cast<const f32x4*>(p), *reinterpret_cast<const f32x4*>(p + 4)};
+  }
+  static __device__ __forceinline__ float el(const Raw& r, int j) { return j < 4 ? r.a[j] : r.b[j - 4]; }
   static __device__ __forceinline__ void load8(const T* p, float* v) {
     f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
 #pragma unroll
@@ -223,28 +231,35 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   for (int row = blockIdx.x * 4 + w; row < rows; row += gridDim.x * 4) {
     const size_t base = (size_t)row * N;
     const float mean = mean_in[row], rstd = rstd_in[row];
-    float xh[NV][8], g_dy[NV][8];
+    // h, dy and the residual gradient of the row are loaded up front as raw vectors (all three
+    // streams in flight together: one memory round trip per row, not one more after the row
+    // reduction) and x-hat / gamma*dy are recomputed in the second pass instead of being held in
+    // f32 registers: 2 waves/SIMD at N = 2048.
+    typename io::Raw hr[NV], dr[NV], rr[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int vi = min(i * 64 + lane, nvec - 1);
+      hr[i] = io::ldraw(h + base + vi * 8);
+      dr[i] = io::ldraw(dy + base + vi * 8);
+      if (dres_in) rr[i] = io::ldraw(dres_in + base + vi * 8);
+    }
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int vi = i * 64 + lane;
       if (vi < nvec) {
-        float hv[8], d[8], g[8];
-        io::load8(h + base + vi * 8, hv);
-        io::load8(dy + base + vi * 8, d);
+        float g[8];
         if (gamma) io::load8(gamma + vi * 8, g); else for (int j = 0; j < 8; ++j) g[j] = 1.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          xh[i][j] = (hv[j] - mean) * rstd;
-          g_dy[i][j] = d[j] * g[j];
-          dg[i][j] += d[j] * xh[i][j];
-          db[i][j] += d[j];
-          s1 += g_dy[i][j];
-          s2 += g_dy[i][j] * xh[i][j];
+          const float d = io::el(dr[i], j);
+          const float xh = (io::el(hr[i], j) - mean) * rstd;
+          const float gd = d * g[j];
+          dg[i][j] += d * xh;
+          db[i][j] += d;
+          s1 += gd;
+          s2 += gd * xh;
         }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) { xh[i][j] = 0.f; g_dy[i][j] = 0.f; }
       }
     }
     const float m1 = wave_sum(s1) / (float)N, m2 = wave_sum(s2) / (float)N;
@@ -252,14 +267,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     for (int i = 0; i < NV; ++i) {
       const int vi = i * 64 + lane;
       if (vi < nvec) {
-        float o[8];
+        float g[8], o[8];
+        if (gamma) io::load8(gamma + vi * 8, g); else for (int j = 0; j < 8; ++j) g[j] = 1.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = rstd * (g_dy[i][j] - m1 - xh[i][j] * m2);
-        if (dres_in) {
-          float r[8];
-          io::load8(dres_in + base + vi * 8, r);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] += r[j];
+        for (int j = 0; j < 8; ++j) {
+          const float xh = (io::el(hr[i], j) - mean) * rstd;
+          o[j] = rstd * (io::el(dr[i], j) * g[j] - m1 - xh * m2);
+          if (dres_in) o[j] += io::el(rr[i], j);
         }
         if (dres) io::store8(dres + base + vi * 8, o);
         if (dx) {

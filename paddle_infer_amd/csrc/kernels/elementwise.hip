@@ -45,14 +45,24 @@ __global__ __launch_bounds__(256) void bias_act_fwd_kernel(const bf16_t* __restr
   constexpr int U = 4;
   const long long stride = (long long)gridDim.x * blockDim.x;
   const int nb8 = N >> 3;
-  for (long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; i0 < n8; i0 += U * stride) {
+  // bias column of vector i is i % nb8, tracked incrementally (a 64-bit modulo per vector was
+  // half of this kernel's VALU instructions and made it VALU-bound)
+  const long long first = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int step1 = (int)(stride % nb8), stepU = (int)((U * stride) % nb8);
+  int c0 = (int)(first % nb8);
+  for (long long i0 = first; i0 < n8; i0 += U * stride) {
     u16x8 r[U], b[U];
+    int c = c0;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long long i = min(i0 + u * stride, n8 - 1);
       r[u] = reinterpret_cast<const u16x8*>(x)[i];
-      if (bias) b[u] = reinterpret_cast<const u16x8*>(bias)[i % nb8];
+      if (bias) b[u] = reinterpret_cast<const u16x8*>(bias)[c];
+      c += step1;
+      c -= c >= nb8 ? nb8 : 0;
     }
+    c0 += stepU;
+    c0 -= c0 >= nb8 ? nb8 : 0;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long long i = i0 + u * stride;

@@ -73,12 +73,33 @@ __device__ __forceinline__ float block_max(float v, float* red) {
   return t;
 }
 
-// Counter-based RNG (Philox-free, stateless): a 64-bit mix of (seed, offset, index) → uniform
-// [0,1). Stateless so backward regenerates the dropout mask instead of storing it.
-__device__ __forceinline__ float hash_uniform(uint64_t seed, uint64_t offset, uint64_t idx) {
-  uint64_t z = seed * 0x9E3779B97F4A7C15ull + (offset + idx) * 0xBF58476D1CE4E5B9ull;
-  z ^= z >> 31; z *= 0x94D049BB133111EBull; z ^= z >> 29; z *= 0xBF58476D1CE4E5B9ull; z ^= z >> 32;
-  return (float)(uint32_t)(z >> 8 & 0xFFFFFF) * (1.0f / 16777216.0f);
+// Counter-based dropout RNG (stateless, so backward and recompute regenerate the mask instead of
+// storing it). One 32-bit integer hash (lowbias32: 2 multiplies) per PAIR of elements, split into
+// two 16-bit uniforms: the former per-element 64-bit splitmix (3 64-bit = 9 quarter-rate 32-bit
+// multiplies per element) made the LayerNorm passes VALU-bound. The value of element `idx` depends
+// only on (seed, offset, idx); (seed, offset) are folded into a per-call key (uniform across the
+// grid, hoisted by the compiler). p granularity 2^-16.
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint32_t rng_key(uint64_t seed, uint64_t offset) {
+  uint32_t k = lowbias32((uint32_t)(offset >> 32) + 0x9E3779B9u);
+  k = lowbias32((uint32_t)offset ^ k);
+  k = lowbias32((uint32_t)(seed >> 32) ^ k);
+  return lowbias32((uint32_t)seed ^ k);
+}
+// u[j] = uniform [0,1) of element idx + j, j < 8; idx must be a multiple of 8.
+__device__ __forceinline__ void hash_uniform8(uint64_t seed, uint64_t offset, uint64_t idx,
+                                              float* u) {
+  const uint64_t pair = idx >> 1;
+  const uint32_t key = rng_key(seed, offset) ^ ((uint32_t)(pair >> 32) * 0x85EBCA6Bu);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const uint32_t h = lowbias32(((uint32_t)pair + t) ^ key);
+    u[2 * t] = (float)(h & 0xFFFFu) * (1.0f / 65536.0f);
+    u[2 * t + 1] = (float)(h >> 16) * (1.0f / 65536.0f);
+  }
 }
 
 // tanh(u) = 1 - 2 / (1 + e^{2u}) on one v_exp_f32 + one v_rcp_f32 (≈6 VALU ops instead of libm

@@ -263,10 +263,11 @@ __global__ __launch_bounds__(256) void dropout_kernel(const bf16_t* __restrict__
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
     u16x8 r = reinterpret_cast<const u16x8*>(x)[i], o;
+    float u[8];
+    hash_uniform8(seed, offset, (uint64_t)i * 8, u);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float u = hash_uniform(seed, offset, (uint64_t)i * 8 + j);
-      o[j] = f2bf(u >= p ? bf2f(r[j]) * ks : 0.f);
+      o[j] = f2bf(u[j] >= p ? bf2f(r[j]) * ks : 0.f);
     }
     reinterpret_cast<u16x8*>(y)[i] = o;
   }

@@ -88,10 +88,11 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
         for (int j = 0; j < 8; ++j) v[i][j] += b[j];
       }
       if (p_drop > 0.f) {
+        float u[8];
+        hash_uniform8(seed, offset, base + vi * 8, u);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          float u = hash_uniform(seed, offset, base + vi * 8 + j);
-          v[i][j] = u >= p_drop ? v[i][j] * keep_scale : 0.f;
+          v[i][j] = u[j] >= p_drop ? v[i][j] * keep_scale : 0.f;
         }
       }
       if (residual) {
@@ -165,10 +166,12 @@ __global__ __launch_bounds__(256) void ln_fwd_row_kernel(
       float b[8], r[8];
       if (bias) io::load8(bias + vi * 8, b);
       if (residual) io::load8(residual + base + vi * 8, r);
+      float u[8];
+      if (p_drop > 0.f) hash_uniform8(seed, offset, base + vi * 8, u);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float a = v[i][j] + (bias ? b[j] : 0.f);
-        if (p_drop > 0.f) a = hash_uniform(seed, offset, base + vi * 8 + j) >= p_drop ? a * keep_scale : 0.f;
+        if (p_drop > 0.f) a = u[j] >= p_drop ? a * keep_scale : 0.f;
         v[i][j] = a + (residual ? r[j] : 0.f);
       }
       if (residual_out) io::store8(residual_out + base + vi * 8, v[i]);
@@ -278,10 +281,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
         if (dres) io::store8(dres + base + vi * 8, o);
         if (dx) {
           if (p_drop > 0.f) {
+            float u[8];
+            hash_uniform8(seed, offset, base + vi * 8, u);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-              float u = hash_uniform(seed, offset, base + vi * 8 + j);
-              o[j] = u >= p_drop ? o[j] * keep_scale : 0.f;
+              o[j] = u[j] >= p_drop ? o[j] * keep_scale : 0.f;
             }
           }
           io::store8(dx + base + vi * 8, o);

@@ -1,0 +1,6 @@
+set -e
+export TMPDIR=/tmp
+for v in base new base new; do
+  if [ $v = base ]; then export PIAMD_KERNEL_LIB=$PWD/paddle_infer_amd/_lib/ab/libpiamd_kernels_base.so; else unset PIAMD_KERNEL_LIB; fi
+  echo "$v $(timeout -k 10 300 python bench.py --steps 10 --warmup 3 2>/dev/null | tail -1 | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["final_loss"])')"
+done

@@ -37,6 +37,16 @@ def _newest_header(d: str) -> float:
     return max((os.path.getmtime(h) for h in hs), default=0.0)
 
 
+def _file_flags(src: str) -> list:
+    """Per-source extra compiler flags from a `// piamd-hipcc-flags: ...` line in the first 40
+    lines (e.g. gemm_pipe.hip keeps its MFMA accumulators in VGPRs and operands in AGPRs)."""
+    with open(src, encoding="utf-8") as f:
+        for _, line in zip(range(40), f):
+            if line.startswith("// piamd-hipcc-flags:"):
+                return line.split(":", 1)[1].split()
+    return []
+
+
 def _compile(cmd: list, src: str) -> str:
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
@@ -55,7 +65,8 @@ def _build_lib(srcs, out, compiler, flags, link_flags, hdr_time, verbose, jobs) 
             todo.append((s, o))
     if todo:
         with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-            futs = [ex.submit(_compile, [compiler, *flags, "-c", s, "-o", o], s) for s, o in todo]
+            futs = [ex.submit(_compile, [compiler, *flags, *_file_flags(s), "-c", s, "-o", o], s)
+                    for s, o in todo]
             for f in cf.as_completed(futs):
                 if verbose:
                     print(f"[piamd build] compiled {os.path.basename(f.result())}", flush=True)

@@ -90,13 +90,18 @@ __device__ __forceinline__ uint32_t rng_key(uint64_t seed, uint64_t offset) {
   return lowbias32((uint32_t)seed ^ k);
 }
 // u[j] = uniform [0,1) of element idx + j, j < 8; idx must be a multiple of 8.
+// Two keyed rounds: h = lowbias32(lowbias32(pair + k_lo) ^ k_hi). With a single round keyed by
+// XOR, two launches whose keys differ by a small d read the same hash stream shifted by d, i.e.
+// one dropout mask is an index-permuted copy of the other; the second (non-linear) round makes
+// every launch's stream a different function of the element index.
 __device__ __forceinline__ void hash_uniform8(uint64_t seed, uint64_t offset, uint64_t idx,
                                               float* u) {
   const uint64_t pair = idx >> 1;
-  const uint32_t key = rng_key(seed, offset) ^ ((uint32_t)(pair >> 32) * 0x85EBCA6Bu);
+  const uint32_t k_lo = rng_key(seed, offset) ^ ((uint32_t)(pair >> 32) * 0x85EBCA6Bu);
+  const uint32_t k_hi = lowbias32(k_lo ^ 0x632BE5ABu);
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    const uint32_t h = lowbias32(((uint32_t)pair + t) ^ key);
+    const uint32_t h = lowbias32(lowbias32((uint32_t)pair + t + k_lo) ^ k_hi);
     u[2 * t] = (float)(h & 0xFFFFu) * (1.0f / 65536.0f);
     u[2 * t + 1] = (float)(h >> 16) * (1.0f / 65536.0f);
   }

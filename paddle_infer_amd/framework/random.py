@@ -5,9 +5,12 @@ Parity: ``paddle.seed`` (reference `python/paddle/framework/random.py`) and
 regions whose activations are replicated across the tensor-parallel group must draw the same mask
 on every mp rank ("global_seed"), sharded regions a different one per rank ("local_seed").
 
-Kernel dropout is counter based: a launch gets ``(seed, offset)`` and element ``i`` uses
-``hash(seed, offset + i)``; the offset advances by the element count, so no RNG state lives on
-the GPU and backward regenerates the identical mask.
+Kernel dropout is counter based: a launch gets ``(seed, offset)``, folded into a per-launch key
+``k = H(seed, offset)``, and the pair of elements ``(2j, 2j+1)`` takes the two 16-bit halves of
+``lowbias32(lowbias32(j + k) ^ H'(k))`` (`csrc/kernels/common.h` ``hash_uniform8``; the second
+keyed round keeps masks of different launches from being index-shifted copies of each other). The
+offset advances by the element count, so no RNG state lives on the GPU and backward / recompute
+regenerate the identical mask.
 """
 from __future__ import annotations
 

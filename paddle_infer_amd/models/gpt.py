@@ -236,8 +236,11 @@ class GPTModel(Layer):
         out, bias = emb, None
         for layer in self.layers:
             if self.cfg.recompute and self.training:
-                h, out, bias = torch.utils.checkpoint.checkpoint(layer, h, out, bias,
-                                                                 use_reentrant=False)
+                # fleet recompute saves / restores the kernel-dropout generator (seed, offset) as
+                # well as torch's RNG, so the re-run draws the forward's dropout masks
+                from ..distributed.fleet.recompute import recompute
+                h, out = recompute(lambda hh, oo, bb, _l=layer: _l(hh, oo, bb)[:2], h, out, bias)
+                bias = layer.mlp.fc2.bias
             else:
                 h, out, bias = layer(h, out, bias)
         y, _ = fused_add_layer_norm(out, h, self.final_ln.weight, self.final_ln.bias,

@@ -159,6 +159,8 @@ _SIGS["piamd_nan_inf_check"] = [c_int, c_void_p, c_ll, c_void_p, c_int, c_void_p
 # a, lda, trans_a, b, ldb, trans_b, c, ldc, c_f32, accumulate, M, N, K, epi, act, bias, aux, ldaux, st
 _SIGS["piamd_gemm"] = [c_void_p, c_ll, c_int, c_void_p, c_ll, c_int, c_void_p, c_ll, c_int, c_int,
                        c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_ll, c_void_p]
+# ... same as piamd_gemm + ksplit, ws
+_SIGS["piamd_gemm_pipe"] = _SIGS["piamd_gemm"][:-1] + [c_int, c_void_p, c_void_p]
 _SIGS["piamd_transpose_bf16"] = [c_void_p, c_void_p, c_int, c_int, c_void_p]
 _SIGS["piamd_moe_gemm"] = [c_void_p, c_ll, c_void_p, c_ll, c_ll,
                                 c_int, c_void_p, c_int, c_int, c_void_p,

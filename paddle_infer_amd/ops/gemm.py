@@ -31,8 +31,13 @@ def _act_grad_ref(h, act):
 
 
 def supported(a, b, trans_a=False, trans_b=False):
+    """Shapes/layouts the hand-written GEMM (either kernel) accepts."""
     if not (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16):
         return False
+    return pipe_supported(a, b, trans_a, trans_b) or _v1_supported(a, b, trans_a, trans_b)
+
+
+def _v1_supported(a, b, trans_a, trans_b):
     M = a.shape[1] if trans_a else a.shape[0]
     K = a.shape[0] if trans_a else a.shape[1]
     N = b.shape[0] if trans_b else b.shape[1]
@@ -40,8 +45,48 @@ def supported(a, b, trans_a=False, trans_b=False):
             and (trans_b or N % 256 == 0) and a.stride(-1) == 1 and b.stride(-1) == 1)
 
 
+def pipe_supported(a, b, trans_a=False, trans_b=False):
+    """Contract of the pipelined kernel (`gemm_pipe.hip`): K % 64, N % 4, 8-element aligned
+    leading dims, M % 8 when A is stored [K, M], N % 8 when B is stored [K, N]; fused epilogues
+    need A stored [M, K]."""
+    if not (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16):
+        return False
+    M = a.shape[1] if trans_a else a.shape[0]
+    K = a.shape[0] if trans_a else a.shape[1]
+    N = b.shape[0] if trans_b else b.shape[1]
+    return (K % 64 == 0 and N % 4 == 0 and M > 0 and (not trans_a or M % 8 == 0)
+            and (trans_b or N % 8 == 0) and a.stride(-1) == 1 and b.stride(-1) == 1
+            and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0
+            and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0
+            and a.stride(0) < (1 << 22) and b.stride(0) < (1 << 22))
+
+
+NUM_CUS = 256
+
+
+def pick_ksplit(M, N, K):
+    """Split-K degree for the pipelined kernel: fill the 256 CUs (one 256x256 tile per CU) when
+    the tile grid is small and K is long (weight gradients: 2048 x 2048 tiles over 65k tokens)."""
+    tiles = ((M + 255) // 256) * ((N + 255) // 256)
+    nk = K // 64
+    if tiles >= 2 * NUM_CUS or nk < 32:
+        return 1
+    best, best_t = 1, None
+    for ks in (1, 2, 4, 8):
+        if nk // ks < 16 or nk % ks:
+            break
+        waves = -(-tiles * ks // NUM_CUS)
+        t = waves / ks
+        if best_t is None or t < best_t - 1e-9:
+            best, best_t = ks, t
+    return best
+
+
 def gemm(a, b, trans_a=False, trans_b=False, out=None, out_f32=False, accumulate=False,
-         epi="none", act="none", bias=None, aux=None):
+         epi="none", act="none", bias=None, aux=None, ksplit=None, impl="auto"):
+    """C = op(A)·op(B) on the hand-written MFMA kernels (CPU: fp32 PyTorch reference).
+    ``impl``: "auto" (pipelined kernel when its contract holds), "pipe", or "v1" (the 2-stage
+    kernel of gemm.hip). ``ksplit``: split-K degree (pipe, epi "none" only; None = heuristic)."""
     M = a.shape[1] if trans_a else a.shape[0]
     K = a.shape[0] if trans_a else a.shape[1]
     N = b.shape[0] if trans_b else b.shape[1]
@@ -72,6 +117,20 @@ def gemm(a, b, trans_a=False, trans_b=False, out=None, out_f32=False, accumulate
     assert out.stride(-1) == 1 and out.shape == (M, N)
     if aux is not None:
         assert aux.shape == (M, N) and aux.dtype == torch.bfloat16 and aux.stride(-1) == 1
+    fused_ok = e == 0 or (not trans_a and out.dtype == torch.bfloat16 and not accumulate)
+    use_pipe = impl == "pipe" or (impl == "auto" and fused_ok and pipe_supported(a, b, trans_a, trans_b))
+    if use_pipe:
+        assert out.stride(0) % 4 == 0 and out.data_ptr() % 16 == 0
+        ks = ksplit if ksplit is not None else (pick_ksplit(M, N, K) if e == 0 else 1)
+        ws = None
+        if ks > 1:
+            ws = torch.empty((ks, M, N), dtype=torch.float32, device=a.device)
+        _lib.call("piamd_gemm_pipe", a.data_ptr(), a.stride(0), int(trans_a), b.data_ptr(),
+                  b.stride(0), int(trans_b), out.data_ptr(), out.stride(0),
+                  int(out.dtype == torch.float32), int(accumulate), M, N, K, e, ac, _lib.ptr(bias),
+                  _lib.ptr(aux), aux.stride(0) if aux is not None else 0, ks, _lib.ptr(ws),
+                  _lib.stream())
+        return out
     _lib.call("piamd_gemm", a.data_ptr(), a.stride(0), int(trans_a), b.data_ptr(), b.stride(0),
               int(trans_b), out.data_ptr(), out.stride(0), int(out.dtype == torch.float32),
               int(accumulate), M, N, K, e, ac, _lib.ptr(bias), _lib.ptr(aux),

@@ -330,8 +330,11 @@ def weight_only_linear(x, weight, bias=None, weight_scale=None, weight_dtype="in
             from .norm import layer_norm
             x2, ln = layer_norm(x2, ln[0], ln[1], ln[2]), None
         if x.is_cuda and M <= 256:
+            assert x.dtype == torch.bfloat16, "weight-only GEMV takes bf16 activations"
             if x2.stride(-1) != 1:
                 x2 = x2.contiguous()
+            if resid is not None:
+                resid = resid.reshape(M, N).contiguous()
             scale = weight_scale if weight_scale.dtype == torch.float32 else weight_scale.float()
             y = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
             tiles = (N // 32) * ((M + 31) // 32)

@@ -417,12 +417,31 @@ class FlatTrainer:
         return out
 
     def set_state_dict(self, sd):
+        """Restore master weights and moments, then rewrite the model's (bf16) parameters from the
+        restored master — the local shard plus an all-gather when sharded — and invalidate the
+        cached transposed weights, so restoring only the optimizer state also restores the model."""
+        self.wait_params()
         self.step_count = int(sd.get("step", 0))
         for g in self.groups:
             if g.name in sd:
                 for k in ("master", "m", "v"):
                     if sd[g.name].get(k) is not None and getattr(g, k) is not None:
                         getattr(g, k).copy_(sd[g.name][k])
+        with torch.no_grad():
+            for g in self.groups:
+                if g.name not in sd:
+                    continue
+                if self.sharding:
+                    g.pshard.copy_(g.master)
+                    o = 0
+                    for b in g.buckets:
+                        L = (b.end - b.start) // self.world
+                        dist.all_gather_into_tensor(g.flat[b.start:b.end], g.pshard[o:o + L],
+                                                    group=self.dp_group)
+                        o += L
+                elif g.flat.data_ptr() != g.master.data_ptr():
+                    g.flat.copy_(g.master)
+        bump_param_epoch()
 
     def num_params(self):
         return sum(p.numel() for g in self.groups for p in g.params)

@@ -289,20 +289,48 @@ def test_gemv_ln_prologue_resid_epilogue(bits, M, K, N):
         _close(got2, x.float() @ wref + b.float() + r.float(), 3e-2)
 
 
-def test_decode_fused_ln_gemv_matches_unfused():
-    """GPT decode through the fused-prologue/epilogue GEMVs == the LN-kernel path."""
+@pytest.mark.parametrize("batch", [1, 2])
+def test_decode_fused_ln_gemv_matches_unfused(batch):
+    """GPT decode through the fused-prologue/epilogue GEMVs (pre-LN in the GEMV prologue, residual
+    add in its epilogue) == the LN-kernel path. The fused branch must actually run (batch ≤
+    FUSED_LN_MAX_M; spied), and the decode logits of both paths agree within bf16 tolerance under
+    teacher forcing (same tokens fed to both)."""
     from paddle_infer_amd.incubate.nn import functional as IF
+    from paddle_infer_amd.ops import inference as INF
     from paddle_infer_amd.inference.generation import GPTGenerator
-    m = _tiny_gpt("float32").to(DEV).to(torch.bfloat16)
-    ids = torch.randint(0, 1024, (3, 9), device=DEV)
-    gen = GPTGenerator(m, max_batch=4, max_seq_len=64, use_hip_graph=False)
-    fused = gen.generate(ids, max_new_tokens=5)
-    orig = IF._Linear.fused_gemv
-    IF._Linear.fused_gemv = lambda self, M: False
+    assert batch <= IF.FUSED_LN_MAX_M
+    m = _tiny_gpt("float32").to(DEV).to(torch.bfloat16).eval()
+    ids = torch.randint(0, 1024, (batch, 9), device=DEV)
+    lens = torch.full((batch,), 9, device=DEV)
+    calls = {"ln": 0}
+    orig_packed, orig_gemv = INF.packed_linear, IF._Linear.fused_gemv
+
+    def spy(*a, **k):
+        calls["ln"] += k.get("ln") is not None
+        return orig_packed(*a, **k)
+
+    gen_f = GPTGenerator(m, max_batch=4, max_seq_len=64, use_hip_graph=False)
+    gen_u = GPTGenerator(m, max_batch=4, max_seq_len=64, use_hip_graph=False)
+    INF.packed_linear = spy
     try:
-        gen2 = GPTGenerator(m, max_batch=4, max_seq_len=64, use_hip_graph=False)
-        unfused = gen2.generate(ids, max_new_tokens=5)
+        lf = gen_f.prefill(ids, lens)
+        IF._Linear.fused_gemv = lambda self, M: False
+        lu = gen_u.prefill(ids, lens)
+        IF._Linear.fused_gemv = orig_gemv
+        _close(lf, lu, 5e-2)
+        pos = torch.full((batch,), 9, dtype=torch.int32, device=DEV)
+        for _ in range(4):
+            tok = lf.argmax(-1)
+            calls["ln"] = 0
+            lf = gen_f.decode(tok, pos)
+            assert calls["ln"] > 0, "fused pre-LN GEMV branch never ran"
+            IF._Linear.fused_gemv = lambda self, M: False
+            calls["ln"] = 0
+            lu = gen_u.decode(tok, pos)
+            IF._Linear.fused_gemv = orig_gemv
+            assert calls["ln"] == 0
+            _close(lf, lu, 5e-2)
+            pos = pos + 1
     finally:
-        IF._Linear.fused_gemv = orig
-    assert (fused == unfused).float().mean().item() >= 0.8, (fused, unfused)
-    assert torch.equal(fused[:, :2], unfused[:, :2])
+        INF.packed_linear = orig_packed
+        IF._Linear.fused_gemv = orig_gemv

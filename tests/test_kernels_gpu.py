@@ -81,6 +81,26 @@ def test_fused_add_layernorm_dropout_consistent():
     assert torch.equal(x.grad != 0, kept)
 
 
+def test_dropout_masks_independent_across_calls():
+    """Consecutive dropout launches draw (near-)uncorrelated masks, also under XOR-shifted indices
+    (a single XOR-keyed hash round made one mask an index-permuted copy of the other)."""
+    from paddle_infer_amd.ops import fused_add_layer_norm
+    N, R = 2048, 512
+    x = torch.ones(R, N, device=DEV, dtype=torch.bfloat16)
+    masks = []
+    for _ in range(4):
+        _, h = fused_add_layer_norm(x, torch.zeros_like(x), None, None, 1e-5, None, 0.5)
+        masks.append((h != 0).float().reshape(-1))
+    idx = torch.arange(R * N, device=DEV)
+    for i in range(3):
+        a, b = masks[i] - masks[i].mean(), masks[i + 1] - masks[i + 1].mean()
+        assert abs((a * b).mean().item() / (a.std() * b.std()).item()) < 0.01
+        for d in (1, 2, 3, 7, 64, 1000):  # b read at index i ^ d
+            bs = masks[i + 1][idx ^ d] - masks[i + 1].mean()
+            c = (a * bs).mean().item() / (a.std() * bs.std()).item()
+            assert abs(c) < 0.01, (i, d, c)
+
+
 @pytest.mark.parametrize("B,Sq,Sk,Hq,Hk,D,causal", [
     (2, 256, 256, 4, 4, 128, True),
     (2, 256, 256, 4, 4, 128, False),
@@ -212,3 +232,30 @@ def test_gpt_tiny_matches_fp32_cpu():
     g_ref = ref.gpt.layers[0].attn.qkv_proj.weight.grad
     g_gpu = m.gpt.layers[0].attn.qkv_proj.weight.grad
     _close(g_gpu.cpu(), g_ref, 5e-2 * g_ref.abs().max().item())
+
+
+def test_gpt_recompute_with_kernel_dropout_matches_plain():
+    """GPU: layer recompute must replay the kernel-dropout generator (seed, offset) so the
+    recomputed forward and its backward use the forward's masks (torch.utils.checkpoint
+    restored only torch's RNG)."""
+    from paddle_infer_amd.framework import random as prand
+    from paddle_infer_amd.models.gpt import GPTForPretraining, gpt_config
+
+    def grads(recompute):
+        cfg = gpt_config("gpt3-tiny", hidden_dropout_prob=0.1, recompute=recompute)
+        torch.manual_seed(0)
+        with torch.device(DEV):
+            m = GPTForPretraining(cfg)
+        m.train()
+        ids = torch.randint(0, cfg.vocab_size, (2, 129), generator=torch.Generator().manual_seed(1)).to(DEV)
+        prand.seed(11)
+        loss = m(ids[:, :-1], labels=ids[:, 1:])
+        loss.backward()
+        return loss.detach().float(), {n: p.grad.float().clone() for n, p in m.named_parameters()
+                                       if p.grad is not None}
+
+    l0, g0 = grads(False)
+    l1, g1 = grads(True)
+    assert torch.allclose(l0, l1)
+    for n in g0:
+        _close(g1[n], g0[n], 1e-3)

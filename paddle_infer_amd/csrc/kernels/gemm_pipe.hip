@@ -46,56 +46,58 @@ namespace {
 typedef short s16x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4_t lds_s16x4;
 
-constexpr int TBM = 256, TBN = 256, KSL = 32, NTHR = 512, NSLOT = 5;
-constexpr int OPB = 256 * KSL * 2;   // one operand image per slot: 16 KiB
-constexpr int SLOTB = 2 * OPB;       // 32 KiB
-constexpr int LDSB = NSLOT * SLOTB;  // 160 KiB
+constexpr int TBM = 256, TBN = 256, KSL = 32, NTHR = 512;
+// LDS holds 64-deep IMAGES (two 32-deep slots: every operand row a whole 128-byte line), 2 of them
+constexpr int OPB = 256 * 2 * KSL * 2;  // one operand image: 32 KiB
+constexpr int IMGB = 2 * OPB;           // 64 KiB
+constexpr int LDSB = 2 * IMGB;          // 128 KiB
 constexpr int GROUP_M = 8;
 
-__device__ __forceinline__ int sw4(int r) { return (r >> 1) & 3; }
+__device__ __forceinline__ int sw8(int r) { return (r >> 1) & 7; }
 __device__ __forceinline__ int sw16(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
 
 __device__ __forceinline__ void bar() { asm volatile("s_barrier" ::: "memory"); }
 // s_waitcnt immediate (gfx9 encoding): lgkmcnt(0), vmcnt / expcnt left at their maxima
 constexpr int LGKM0 = 0xF | (3 << 14) | (7 << 4);
 
-// Per-lane byte offsets of this wave's 2 DMA pieces of one operand image (tile-relative). The 16
-// pieces (1 KiB each) of an operand image are shared by the 8 waves: wave w takes pieces w and w+8.
-// KC: operand [rows][K] (leading dim ld): piece = 16 rows × 64 B; rows clamped to rlim.
-// !KC: operand [K][cols]: piece = 2 k-rows × 512 B; 8-col chunks clamped to rlim.
+// DMA of this wave's 4 pieces of one operand image (64 deep). The 32 pieces (1 KiB each) of an
+// image are shared by the 8 waves: wave w takes w, w+8, w+16, w+24. Every piece covers whole
+// 128-byte lines: KC — operand [rows][K] (leading dim ld), piece = 8 rows × 128 B, rows clamped to
+// rlim; !KC — operand [K][cols], piece = 2 k-rows × 512 B, 8-col chunks clamped to rlim. `base`:
+// uniform address of the image's first element (KC: tile row 0, k0; !KC: k-row k0, tile col 0).
+// The per-lane offsets are recomputed per issue (a few VALU) rather than held in registers.
 template <bool KC>
-__device__ __forceinline__ void dma_offsets(unsigned (&off)[2], int ld, int rlim, int w, int lane) {
+__device__ __forceinline__ void dma_op(const char* base, int ld, int rlim, char* img, int w, int lane) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < 4; ++i) {
     const int L = (i * 8 + w) * 64 + lane;
+    unsigned off;
     if (KC) {
-      const int r = L >> 2, pc = L & 3;
-      off[i] = (unsigned)(min(r, rlim) * ld + ((pc ^ sw4(r)) << 3)) * 2u;
+      const int r = L >> 3, pc = L & 7;
+      off = (unsigned)(min(r, rlim) * ld + ((pc ^ sw8(r)) << 3)) * 2u;
     } else {
       const int r = L >> 5, pc = L & 31;
-      off[i] = (unsigned)(r * ld + min((pc ^ sw16(r)) << 3, rlim)) * 2u;
+      off = (unsigned)(r * ld + min((pc ^ sw16(r)) << 3, rlim)) * 2u;
     }
-  }
-}
-
-// `base`: uniform address of the slot's first element (KC: tile row 0, k0; !KC: k-row k0, tile col 0)
-__device__ __forceinline__ void dma_op(const char* base, const unsigned (&off)[2], char* img, int w) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + off[i]),
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + off),
                                      (__attribute__((address_space(3))) void*)(img + (i * 8 + w) * 1024),
                                      16, 0, 0);
+  }
 }
 
-// 16 × 32 fragment of the 16x16x32 MFMA: lane l holds row/col `base + (l&15)`, k = 8·(l>>4) + j.
+// 16 × 32 fragment of the 16x16x32 MFMA from half `ks` (32-deep slot) of an image: lane l holds
+// row/col `base + (l&15)`, k = 32·ks + 8·(l>>4) + j. KC image [256 rows][128 B], 16-B chunk c of
+// row r stored at c ^ ((r>>1)&7) (conflict-free ds_read_b128 for this operand); !KC image
+// [64 k][512 B], chunk ^ (((k&3)<<2) | ((k>>2)&3)) on the low 4 bits (conflict-free
+// ds_read_b64_tr_b16).
 template <bool KC>
-__device__ __forceinline__ bf16x8 ld_frag(const char* img, int base, int lane) {
+__device__ __forceinline__ bf16x8 ld_frag(const char* img, int base, int ks, int lane) {
   if (KC) {
-    const int row = base + (lane & 15), c = lane >> 4;
-    return *reinterpret_cast<const bf16x8*>(img + row * 64 + ((c ^ sw4(row)) << 4));
+    const int row = base + (lane & 15), c = 4 * ks + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(img + row * 128 + ((c ^ sw8(row)) << 4));
   }
   const int gi = lane & 15;
-  const int k = 8 * (lane >> 4) + (gi >> 2);
+  const int k = 32 * ks + 8 * (lane >> 4) + (gi >> 2);
   const int col = base + 4 * (gi & 3);
   const int o0 = k * 512 + (((col >> 3) ^ sw16(k)) << 4) + ((col & 7) << 1);
   const int o1 = (k + 4) * 512 + (((col >> 3) ^ sw16(k + 4)) << 4) + ((col & 7) << 1);
@@ -105,9 +107,9 @@ __device__ __forceinline__ bf16x8 ld_frag(const char* img, int base, int lane) {
 }
 
 template <bool B_KC>
-__device__ __forceinline__ void read_b(bf16x8 (&b)[4], const char* slot, int wc, int lane) {
+__device__ __forceinline__ void read_b(bf16x8 (&b)[4], const char* img, int ks, int wc, int lane) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) b[i] = ld_frag<B_KC>(slot + OPB, wc * 64 + i * 16, lane);
+  for (int i = 0; i < 4; ++i) b[i] = ld_frag<B_KC>(img + OPB, wc * 64 + i * 16, ks, lane);
 }
 
 // row mb of the slot: 4 MFMAs on the current A fragment, then (if `next`) that fragment's register
@@ -115,11 +117,17 @@ __device__ __forceinline__ void read_b(bf16x8 (&b)[4], const char* slot, int wc,
 // reads sit between the MFMAs)
 template <bool A_KC, int MB>
 __device__ __forceinline__ void mma_row(f32x4 (&acc)[8][4], bf16x8 (&a)[8], const bf16x8 (&b)[4],
-                                        const char* next, int wr, int lane) {
+                                        const char* next, int nks, int wr, int lane) {
+#ifndef PIAMD_ABL_NO_MFMA
 #pragma unroll
   for (int nb = 0; nb < 4; ++nb)
     acc[MB][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[nb], a[MB], acc[MB][nb], 0, 0, 0);
-  if (next) a[MB] = ld_frag<A_KC>(next, wr * 128 + MB * 16, lane);
+#else  // ablation build: operands kept live, no matrix work
+  asm volatile("" ::"v"(a[MB]), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]));
+#endif
+#ifndef PIAMD_ABL_NO_READS
+  if (next) a[MB] = ld_frag<A_KC>(next, wr * 128 + MB * 16, nks, lane);
+#endif
 }
 
 __device__ __forceinline__ float act_fwd(float v, int act) {
@@ -181,11 +189,11 @@ __device__ __forceinline__ int my_unit(const Problem& p, int i) {
 
 // DMA issue cursor: which slot of which unit goes out next
 struct Issuer {
-  int i, s, u;  // unit ordinal, slot within unit, unit id (-1: stream exhausted)
+  int i, s, u;  // unit ordinal, image within unit, unit id (-1: stream exhausted)
   const char* abase;
   const char* bbase;
-  long long astep, bstep;  // bytes per slot along K
-  unsigned aoff[2], boff[2];
+  long long astep, bstep;  // bytes per image along K
+  int lda, ldb, alim, blim;
 };
 
 template <bool A_KC, bool B_KC>
@@ -197,32 +205,34 @@ __device__ __forceinline__ void issuer_load_unit(const Problem& p, Issuer& is, i
   const long long k0 = (long long)part * p.nks * KSL;
   is.abase = reinterpret_cast<const char*>(A_KC ? p.a + (long long)m0 * p.lda + k0 : p.a + k0 * p.lda + m0);
   is.bbase = reinterpret_cast<const char*>(B_KC ? p.b + (long long)n0 * p.ldb + k0 : p.b + k0 * p.ldb + n0);
-  is.astep = A_KC ? KSL * 2 : (long long)KSL * p.lda * 2;
-  is.bstep = B_KC ? KSL * 2 : (long long)KSL * p.ldb * 2;
-  dma_offsets<A_KC>(is.aoff, (int)p.lda, (A_KC ? p.M - 1 : p.M - 8) - m0, w, lane);
-  dma_offsets<B_KC>(is.boff, (int)p.ldb, (B_KC ? p.N - 1 : p.N - 8) - n0, w, lane);
+  is.astep = A_KC ? 2 * KSL * 2 : (long long)2 * KSL * p.lda * 2;
+  is.bstep = B_KC ? 2 * KSL * 2 : (long long)2 * KSL * p.ldb * 2;
+  is.lda = (int)p.lda;
+  is.ldb = (int)p.ldb;
+  is.alim = (A_KC ? p.M - 1 : p.M - 8) - m0;
+  is.blim = (B_KC ? p.N - 1 : p.N - 8) - n0;
 }
 
-// issue the next slot of the stream into ring position `pos` (no-op once exhausted)
+// issue the next image of the stream into LDS image position `pos` (no-op once exhausted)
 template <bool A_KC, bool B_KC>
 __device__ __forceinline__ void issue_next(const Problem& p, Issuer& is, char* smem, int pos, int w,
                                            int lane) {
   if (is.u < 0) return;
-  char* slot = smem + pos * SLOTB;
-  dma_op(is.abase + is.s * is.astep, is.aoff, slot, w);
-  dma_op(is.bbase + is.s * is.bstep, is.boff, slot + OPB, w);
-  if (++is.s == p.nks) {
+  char* img = smem + pos * IMGB;
+#ifndef PIAMD_ABL_NO_DMA
+  dma_op<A_KC>(is.abase + is.s * is.astep, is.lda, is.alim, img, w, lane);
+  dma_op<B_KC>(is.bbase + is.s * is.bstep, is.ldb, is.blim, img + OPB, w, lane);
+#endif
+  if (++is.s == p.nks / 2) {
     is.s = 0;
     ++is.i;
     issuer_load_unit<A_KC, B_KC>(p, is, w, lane);
   }
 }
 
-// wait until at most `pend` slots (4 DMA instructions each) of this wave are outstanding
-__device__ __forceinline__ void wait_slots(int pend) {
-  if (pend >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else if (pend == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (pend == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+// wait until at most `pend` images (8 DMA instructions each) of this wave are outstanding
+__device__ __forceinline__ void wait_images(int pend) {
+  if (pend >= 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -358,48 +368,49 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pipe_kernel(Problem p) {
   is.i = 0;
   is.s = 0;
   issuer_load_unit<A_KC, B_KC>(p, is, w, lane);
-  // prologue: stream slots 0..3 into ring positions 0..3, then wait for slot 0
-#pragma unroll
-  for (int j = 0; j < 4; ++j) issue_next<A_KC, B_KC>(p, is, smem, j, w, lane);
-  wait_slots(min(3, total - 1));
+  // prologue: images 0 and 1 into LDS positions 0 and 1; wait for image 0
+  issue_next<A_KC, B_KC>(p, is, smem, 0, w, lane);
+  issue_next<A_KC, B_KC>(p, is, smem, 1, w, lane);
+  wait_images(total > 2 ? 1 : 0);
+  __builtin_amdgcn_s_waitcnt(LGKM0);
   bar();
-
   bf16x8 a[8], b0[4], b1[4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) a[i] = ld_frag<A_KC>(smem, wr * 128 + i * 16, lane);
-  read_b<B_KC>(b0, smem, wc, lane);
-  int pos = 0;  // ring position of the slot being computed
-  int g = 0;    // stream index of the slot being computed
-  // compute slot g (A in `a`, B in `bc`); read slot g+1's B into `bn` and its A into `a`
-  auto step = [&](f32x4 (&acc)[8][4], const bf16x8 (&bc)[4], bf16x8 (&bn)[4]) {
-    const int pos1 = pos == NSLOT - 1 ? 0 : pos + 1;
-    const int pos4 = pos == 0 ? NSLOT - 1 : pos - 1;  // (g + 4) % 5 == (g - 1) % 5
-    // own DMAs of slot g+1 retired (slots g+2 and g+3 may stay in flight), then everyone's;
-    // the barrier also certifies that every wave finished reading slot g-1 (read during step g-1,
-    // retired by the lgkmcnt below), so its ring position may be refilled
-    wait_slots(min(2, max(0, total - (g + 2))));
-    // this wave's LDS reads of slot g are complete: a real S_WAITCNT the compiler's waitcnt pass
-    // sees, so it puts no lgkmcnt(0) behind the new reads (scalar loads of the unit-change path
-    // share the counter and would force one)
-    __builtin_amdgcn_s_waitcnt(LGKM0);
-    bar();
-    const char* next = g + 1 < total ? smem + pos1 * SLOTB : nullptr;
-    if (next) read_b<B_KC>(bn, next, wc, lane);
-    if (!late) issue_next<A_KC, B_KC>(p, is, smem, pos4, w, lane);
+  for (int i = 0; i < 8; ++i) a[i] = ld_frag<A_KC>(smem, wr * 128 + i * 16, 0, lane);
+  read_b<B_KC>(b0, smem, 0, wc, lane);
+  int g = 0;  // stream index of the slot being computed (image g >> 1, half g & 1)
+  // step g: compute slot g (A in `a`, B in `bc`); read slot g+1's B into `bn` and its A into `a`.
+  // ODD steps start a new image for the reads: wait for it (own DMAs, then everyone's via the
+  // barrier) — the barrier also certifies that every wave finished reading image (g-1)/2, whose
+  // LDS position then takes image (g+3)/2 (two steps of DMA latency budget)
+  auto step = [&](f32x4 (&acc)[8][4], const bf16x8 (&bc)[4], bf16x8 (&bn)[4], auto odd) {
+    constexpr bool ODD = decltype(odd)::value;
+    if (ODD) {
+      wait_images(0);
+      // this wave's LDS reads of the previous image are complete: a real S_WAITCNT the
+      // compiler's waitcnt pass sees (so it adds no lgkmcnt(0) behind the new reads)
+      __builtin_amdgcn_s_waitcnt(LGKM0);
+      bar();
+    }
+    const char* next = g + 1 < total ? smem + (((g + 1) >> 1) & 1) * IMGB : nullptr;
+    constexpr int nks = ODD ? 0 : 1;  // half of the next slot inside its image
+#ifndef PIAMD_ABL_NO_READS
+    if (next) read_b<B_KC>(bn, next, nks, wc, lane);
+#endif
+    if (ODD && !late) issue_next<A_KC, B_KC>(p, is, smem, ((g - 1) >> 1) & 1, w, lane);
     __builtin_amdgcn_s_setprio(1);
-    mma_row<A_KC, 0>(acc, a, bc, next, wr, lane);
-    mma_row<A_KC, 1>(acc, a, bc, next, wr, lane);
-    mma_row<A_KC, 2>(acc, a, bc, next, wr, lane);
-    mma_row<A_KC, 3>(acc, a, bc, next, wr, lane);
+    mma_row<A_KC, 0>(acc, a, bc, next, nks, wr, lane);
+    mma_row<A_KC, 1>(acc, a, bc, next, nks, wr, lane);
+    mma_row<A_KC, 2>(acc, a, bc, next, nks, wr, lane);
+    mma_row<A_KC, 3>(acc, a, bc, next, nks, wr, lane);
     __builtin_amdgcn_s_setprio(0);
-    if (late) issue_next<A_KC, B_KC>(p, is, smem, pos4, w, lane);
+    if (ODD && late) issue_next<A_KC, B_KC>(p, is, smem, ((g - 1) >> 1) & 1, w, lane);
     __builtin_amdgcn_s_setprio(1);
-    mma_row<A_KC, 4>(acc, a, bc, next, wr, lane);
-    mma_row<A_KC, 5>(acc, a, bc, next, wr, lane);
-    mma_row<A_KC, 6>(acc, a, bc, next, wr, lane);
-    mma_row<A_KC, 7>(acc, a, bc, next, wr, lane);
+    mma_row<A_KC, 4>(acc, a, bc, next, nks, wr, lane);
+    mma_row<A_KC, 5>(acc, a, bc, next, nks, wr, lane);
+    mma_row<A_KC, 6>(acc, a, bc, next, nks, wr, lane);
+    mma_row<A_KC, 7>(acc, a, bc, next, nks, wr, lane);
     __builtin_amdgcn_s_setprio(0);
-    pos = pos1;
     ++g;
   };
   for (int ui = 0; ui < nunits; ++ui) {
@@ -408,12 +419,12 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_pipe_kernel(Problem p) {
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // units have an even slot count: the B register sets alternate in a fixed order
+    // units have an even slot count (whole images): the B register sets alternate in a fixed order
     for (int s = 0; s < p.nks; s += 2) {
-      step(acc, b0, b1);
-      step(acc, b1, b0);
+      step(acc, b0, b1, std::false_type{});
+      step(acc, b1, b0, std::true_type{});
     }
-    // the next unit's first slots are already in flight (DMA) and read meanwhile
+    // the next unit's first image is already in flight (DMA) and its first slot read meanwhile
     int part, m0, n0;
     unit_coords(p, my_unit(p, ui), part, m0, n0);
     epilogue<EK>(p, acc, part, m0, n0, wr, wc, lane);

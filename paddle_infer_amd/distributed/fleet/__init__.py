@@ -24,7 +24,7 @@ from .pipeline import LayerDesc, SharedLayerDesc, PipelineLayer, PipelineParalle
 from .recompute import recompute  # noqa: F401
 from ...framework.random import get_rng_state_tracker, model_parallel_random_seed  # noqa: F401
 
-_STATE = {"hcg": None, "strategy": None, "inited": False}
+_STATE = {"hcg": None, "strategy": None, "inited": False, "model": None}
 
 
 class DistributedStrategy:
@@ -131,20 +131,27 @@ def is_server():
 
 
 class _HybridModel(torch.nn.Module):
-    """TensorParallel / ShardingParallel wrapper: syncs replicated weights, forwards calls."""
+    """TensorParallel / ShardingParallel wrapper: makes replicated weights identical across the mp,
+    sharding and dp axes at wrap time (one coalesced broadcast per group), forwards calls."""
 
     def __init__(self, layers, hcg):
         super().__init__()
         self._layers = layers
         self.hcg = hcg
         if dist.is_initialized():
-            mp_g = hcg.get_model_parallel_group()
-            dp_g = hcg.get_data_parallel_group()
-            for p in layers.parameters():
-                if mp_g is not None and not getattr(p, "is_distributed", False):
-                    dist.broadcast(p.data, hcg.get_model_parallel_group_src_rank(), group=mp_g)
-                if dp_g is not None:
-                    dist.broadcast(p.data, hcg.get_data_parallel_group_src_rank(), group=dp_g)
+            with torch.no_grad():
+                mp_g = hcg.get_model_parallel_group()
+                rep = [p for p in layers.parameters() if not getattr(p, "is_distributed", False)]
+                if mp_g is not None and hcg.get_model_parallel_world_size() > 1:
+                    _coalesced_broadcast(rep, hcg.get_model_parallel_group_src_rank(), mp_g)
+                sh_g = hcg.get_sharding_parallel_group()
+                if sh_g is not None and hcg.get_sharding_parallel_world_size() > 1:
+                    _coalesced_broadcast(list(layers.parameters()),
+                                         hcg.get_sharding_parallel_group_src_rank(), sh_g)
+                dp_g = hcg.get_data_parallel_group()
+                if dp_g is not None and hcg.get_data_parallel_world_size() > 1:
+                    _coalesced_broadcast(list(layers.parameters()),
+                                         hcg.get_data_parallel_group_src_rank(), dp_g)
 
     def forward(self, *a, **k):
         return self._layers(*a, **k)
@@ -162,11 +169,37 @@ class _HybridModel(torch.nn.Module):
 TensorParallel = ShardingParallel = _HybridModel
 
 
+def _coalesced(tensors):
+    """Group tensors by (dtype, device) → list of (tensors, flat buffer holding their values)."""
+    groups = {}
+    for t in tensors:
+        groups.setdefault((t.dtype, t.device), []).append(t)
+    out = []
+    for ts in groups.values():
+        out.append((ts, torch.cat([t.detach().reshape(-1) for t in ts])))
+    return out
+
+
+def _scatter_back(ts, flat):
+    o = 0
+    for t in ts:
+        n = t.numel()
+        t.copy_(flat[o:o + n].view_as(t))
+        o += n
+
+
+def _coalesced_broadcast(tensors, src, group):
+    for ts, flat in _coalesced(tensors):
+        dist.broadcast(flat, src, group=group)
+        _scatter_back(ts, flat)
+
+
 def distributed_model(model):
     hcg = _STATE["hcg"]
     if hcg is None:
         return model
     st = _strategy()
+    _STATE["model"] = model
     if isinstance(model, PipelineLayer) and hcg.get_pipe_parallel_world_size() > 1:
         return PipelineParallel(model, hcg, st)
     if hcg.get_model_parallel_world_size() > 1 or hcg.get_sharding_parallel_world_size() > 1 or st.sharding:
@@ -179,29 +212,64 @@ def distributed_model(model):
     return model
 
 
+def _partition(params, n):
+    """Greedy size-balanced owner assignment over the sharding ranks (reference
+    `dygraph_sharding_optimizer.py:_partition_parameters`)."""
+    owner, sizes = {}, [0] * n
+    for p in params:
+        r = sizes.index(min(sizes))
+        owner[id(p)] = r
+        sizes[r] += p.numel()
+    return owner
+
+
 class HybridParallelOptimizer:
-    """Wraps a Paddle optimizer for hybrid parallel training: gradient reduction over the dp (and
-    sharding) group unless a DataParallel reducer already did it, global-norm clipping that counts
-    mp-distributed parameters once per shard and replicated ones once, then the inner step."""
+    """Hybrid-parallel optimizer (reference `hybrid_parallel_optimizer.py` +
+    `dygraph_sharding_optimizer.py`).
+
+    * GPU (the inner optimizer has the flat-buffer engine): the engine is rebuilt on the hybrid
+      groups. With ``sharding_degree`` > 1 the SHARDING axis is the ZeRO axis — gradients are
+      reduce-scattered bucket by bucket during backward, fp32 master / moments live as 1/sh shards,
+      updated bf16 shards are all-gathered — and the dp axis (if > 1) sums each reduced shard once
+      more (states replicated across dp). ``sharding_degree`` == 1 with ``strategy.sharding``
+      shards over dp instead. Global-norm clip is device-side over mp (distributed params) and pp.
+    * Generic path (CPU / other optimizers): gradients of all parameters are all-reduced in ONE
+      coalesced buffer per dtype over dp and sharding; with ``sharding_degree`` > 1 every sharding
+      rank updates only the parameters it owns (greedy size partition) and broadcasts them back
+      (one coalesced broadcast per owner). Clip: device-side global norm over mp / pp (no host
+      round trip per parameter)."""
 
     def __init__(self, optimizer, hcg, strategy):
         self._inner = optimizer
         self.hcg, self.strategy = hcg, strategy
         self._flat = None
+        self._sh = hcg.get_sharding_parallel_world_size() if hcg else 1
+        self._dp = hcg.get_data_parallel_world_size() if hcg else 1
         dp_g = hcg.get_data_parallel_group() if hcg else None
+        sh_g = hcg.get_sharding_parallel_group() if hcg else None
+        self._owner = None
         inner_flat = getattr(optimizer, "_flat", None)
         if inner_flat is not None:  # rebuild the fused engine with the hybrid groups
             from ...parallel.flat_engine import FlatTrainer
             old = inner_flat
             named = [(getattr(p, "pd_name", str(i)), p) for i, p in enumerate(optimizer._parameter_list)]
-            stage = int(strategy.sharding_configs.get("stage", 1)) if (strategy.sharding or hcg.get_sharding_parallel_world_size() > 1) else 0
-            self._flat = FlatTrainer(None, lr=optimizer.get_lr(), betas=(old.beta1, old.beta2),
-                                     eps=old.eps, weight_decay=old.groups[0].weight_decay,
-                                     grad_clip=old.grad_clip, dp_group=dp_g,
+            stage = int(strategy.sharding_configs.get("stage", 1))
+            if self._sh > 1:
+                shard_g, rep_g, st = sh_g, (dp_g if self._dp > 1 else None), stage
+            else:
+                shard_g, rep_g, st = dp_g, None, (stage if strategy.sharding else 0)
+            self._flat = FlatTrainer(_STATE.get("model"), lr=optimizer.get_lr(),
+                                     betas=(old.beta1, old.beta2), eps=old.eps,
+                                     weight_decay=old.groups[0].weight_decay,
+                                     grad_clip=old.grad_clip, dp_group=shard_g,
+                                     replica_group=rep_g,
                                      mp_group=hcg.get_model_parallel_group(),
-                                     pp_group=hcg.get_pipe_parallel_group(), sharding_stage=stage,
+                                     pp_group=hcg.get_pipe_parallel_group(), sharding_stage=st,
                                      named_params=named, bucket_mb=strategy.fuse_grad_size_in_MB)
             optimizer._flat = self._flat
+        elif self._sh > 1:
+            self._owner = _partition([p for p in optimizer._parameter_list if p.requires_grad],
+                                     self._sh)
 
     def __getattr__(self, k):
         return getattr(self._inner, k)
@@ -209,47 +277,74 @@ class HybridParallelOptimizer:
     @torch.no_grad()
     def _reduce_grads(self):
         dp_g = self.hcg.get_data_parallel_group()
-        n = self.hcg.get_data_parallel_world_size()
-        if dp_g is None or n == 1:
+        sh_g = self.hcg.get_sharding_parallel_group()
+        # a DataParallel reducer already averaged over dp
+        dp_done = any(getattr(p, "_dp_bucket", None) is not None for p in self._inner._parameter_list)
+        groups = []
+        if self._dp > 1 and not dp_done:
+            groups.append(dp_g)
+        if self._sh > 1:
+            groups.append(sh_g)
+        if not groups:
             return
-        for p in self._inner._parameter_list:
-            if p.grad is not None and not getattr(p, "_dp_bucket", None) is not None:
-                dist.all_reduce(p.grad, group=dp_g)
-                p.grad.div_(n)
+        n = (1 if dp_done else self._dp) * self._sh
+        grads = [p.grad for p in self._inner._parameter_list if p.grad is not None]
+        for ts, flat in _coalesced(grads):
+            for g in groups:
+                dist.all_reduce(flat, group=g)
+            flat.div_(n)
+            _scatter_back(ts, flat)
 
     @torch.no_grad()
     def _clip(self):
         clip = self._inner._grad_clip
         if clip is None or not hasattr(clip, "clip_norm"):
             return
-        dist_sq = torch.zeros((), dtype=torch.float32)
-        rep_sq = torch.zeros((), dtype=torch.float32)
-        dev = None
+        dist_sq, rep_sq, dev = None, None, None
         for p in self._inner._parameter_list:
             if p.grad is None:
                 continue
             dev = p.grad.device
-            s = p.grad.float().pow(2).sum().cpu()
+            s = p.grad.float().pow(2).sum()
             if getattr(p, "is_distributed", False):
-                dist_sq += s
+                dist_sq = s if dist_sq is None else dist_sq + s
             else:
-                rep_sq += s
+                rep_sq = s if rep_sq is None else rep_sq + s
+        if dev is None:
+            return
+        zero = torch.zeros((), dtype=torch.float32, device=dev)
+        dist_sq = zero.clone() if dist_sq is None else dist_sq
+        rep_sq = zero.clone() if rep_sq is None else rep_sq
         mp_g = self.hcg.get_model_parallel_group()
-        if mp_g is not None:
-            t = dist_sq.to(dev or "cpu")
-            dist.all_reduce(t, group=mp_g)
-            dist_sq = t.cpu()
-        total = dist_sq + rep_sq
+        if mp_g is not None and self.hcg.get_model_parallel_world_size() > 1:
+            dist.all_reduce(dist_sq, group=mp_g)
+        total = (dist_sq + rep_sq).reshape(1)
         pp_g = self.hcg.get_pipe_parallel_group()
-        if pp_g is not None:
-            t = total.to(dev or "cpu")
-            dist.all_reduce(t, group=pp_g)
-            total = t.cpu()
-        coef = min(1.0, clip.clip_norm / (float(total.sqrt()) + 1e-6))
+        if pp_g is not None and self.hcg.get_pipe_parallel_world_size() > 1:
+            dist.all_reduce(total, group=pp_g)
+        coef = torch.clamp(clip.clip_norm / (total.sqrt() + 1e-6), max=1.0)
         for p in self._inner._parameter_list:
             if p.grad is not None:
-                p.grad.mul_(coef)
+                p.grad.mul_(coef.to(p.grad.dtype))
         self._inner._grad_clip, self._saved_clip = None, clip
+
+    @torch.no_grad()
+    def _sharded_step(self):
+        """Update only this sharding rank's parameters, then broadcast every owner's set."""
+        rank = self.hcg.get_sharding_parallel_rank()
+        allp = self._inner._parameter_list
+        mine = [p for p in allp if p.requires_grad and self._owner.get(id(p)) == rank]
+        self._inner._parameter_list = mine
+        try:
+            self._inner.step()
+        finally:
+            self._inner._parameter_list = allp
+        sh_g = self.hcg.get_sharding_parallel_group()
+        ranks = self.hcg.get_sharding_parallel_group_ranks()
+        for r in range(self._sh):
+            owned = [p for p in allp if p.requires_grad and self._owner.get(id(p)) == r]
+            if owned:
+                _coalesced_broadcast(owned, ranks[r], sh_g)
 
     def step(self):
         if self._flat is not None:
@@ -259,7 +354,10 @@ class HybridParallelOptimizer:
         self._reduce_grads()
         self._clip()
         try:
-            self._inner.step()
+            if self._owner is not None:
+                self._sharded_step()
+            else:
+                self._inner.step()
         finally:
             if getattr(self, "_saved_clip", None) is not None:
                 self._inner._grad_clip = self._saved_clip
@@ -276,6 +374,12 @@ class HybridParallelOptimizer:
     def minimize(self, loss, *a, **k):
         loss.backward()
         self.step()
+
+    def state_dict(self):
+        return self._inner.state_dict()
+
+    def set_state_dict(self, sd):
+        return self._inner.set_state_dict(sd)
 
 
 def distributed_optimizer(optimizer, strategy=None):

@@ -171,6 +171,9 @@ class HybridCommunicateGroup:
     def get_sharding_parallel_group_src_rank(self):
         return self._ranks["sharding"][0]
 
+    def get_sharding_parallel_group_ranks(self):
+        return self._ranks["sharding"]
+
     def get_check_parallel_group(self, sharding=False):
         return self._groups.get("model")
 

@@ -116,7 +116,7 @@ class FlatTrainer:
     def __init__(self, model, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
                  grad_clip=1.0, dp_group=None, mp_group=None, pp_group=None, sharding_stage=0,
                  bucket_mb=256, no_decay_fn=None, optimizer="adamw", momentum=0.9,
-                 overlap=True, named_params=None):
+                 overlap=True, named_params=None, replica_group=None):
         self.model = model
         self.lr = lr
         self.beta1, self.beta2 = betas
@@ -128,6 +128,13 @@ class FlatTrainer:
         self.world = dist.get_world_size(dp_group) if dp_group is not None else 1
         self.rank = dist.get_rank(dp_group) if dp_group is not None else 0
         self.sharding = sharding_stage if self.world > 1 else 0
+        # Fleet hybrid with sharding_degree > 1 and dp_degree > 1: ``dp_group`` is the SHARDING
+        # axis (reduce-scatter / sharded states / all-gather) and ``replica_group`` the data-parallel
+        # axis over which each reduced shard is summed once more (states replicated across it) —
+        # reference `hybrid_parallel_optimizer.py:215` (sharding_reduce_gradients, then
+        # fused_allreduce_gradients over dp).
+        self.replica_group = replica_group
+        self.replica = dist.get_world_size(replica_group) if replica_group is not None else 1
         self.optimizer = optimizer
         self.momentum = momentum
         self.overlap = overlap
@@ -167,7 +174,7 @@ class FlatTrainer:
         self._clip_coef = torch.ones((), device=device, dtype=torch.float32)
         self._ag_handles = []
         self._ag_pending = {}  # (group idx, bucket idx) -> all-gather handle
-        if self.sharding and overlap:
+        if self.sharding and overlap and model is not None:
             self._install_forward_waits(model)
 
     def _install_forward_waits(self, model):
@@ -267,7 +274,7 @@ class FlatTrainer:
 
     def _make_ready(self, g):
         def ready(p):
-            if not self.overlap or self.world == 1:
+            if not self.overlap or (self.world == 1 and self.replica == 1):
                 return
             b = g.buckets[g.bucket_of[id(p)]]
             b.pending -= 1
@@ -281,10 +288,18 @@ class FlatTrainer:
         if self.sharding:
             L = (b.end - b.start) // self.world
             o = sum((bb.end - bb.start) // self.world for bb in g.buckets[:g.buckets.index(b)])
-            b.handle = dist.reduce_scatter_tensor(g.gshard[o:o + L], grads, group=self.dp_group,
-                                                  async_op=True)
+            out = g.gshard[o:o + L]
+            b.handle = dist.reduce_scatter_tensor(out, grads, group=self.dp_group, async_op=True)
         else:
-            b.handle = dist.all_reduce(grads, group=self.dp_group, async_op=True)
+            out = grads
+            b.handle = dist.all_reduce(grads, group=self.dp_group, async_op=True) \
+                if self.world > 1 else None
+        if self.replica > 1:
+            # chained on the device: wait() orders the replica all-reduce behind the first
+            # collective without blocking the host (RCCL); only the shard (or bucket) travels
+            if b.handle is not None:
+                b.handle.wait()
+            b.handle = dist.all_reduce(out, group=self.replica_group, async_op=True)
 
     # ---------------------------------------------------------------------------------
     def zero_grad(self):
@@ -308,7 +323,7 @@ class FlatTrainer:
     clear_grad = zero_grad
 
     def _finish_reduction(self):
-        if self.world == 1:
+        if self.world == 1 and self.replica == 1:
             return
         for g in self.groups:
             for b in g.buckets:
@@ -328,7 +343,7 @@ class FlatTrainer:
         nb.zero_()
         for g in self.groups:
             sumsq(self._grads_for_update(g), out=nb[1 if g.distributed else 0], accumulate=True)
-        scale = 1.0 / self.world
+        scale = 1.0 / (self.world * self.replica)
         if self.world > 1 and self.sharding:
             dist.all_reduce(nb, group=self.dp_group)
         if self.mp_group is not None and dist.get_world_size(self.mp_group) > 1:
@@ -354,7 +369,7 @@ class FlatTrainer:
         if self.grad_clip:
             self._compute_clip()
             gscale = self._clip_coef
-        static = 1.0 / self.world
+        static = 1.0 / (self.world * self.replica)
         for g in self.groups:
             grads = self._grads_for_update(g)
             model_out = g.pshard if self.sharding else g.flat

@@ -1,43 +1,62 @@
-// LayerNorm forward / backward with optional fused bias + dropout + residual-add prologue.
+// LayerNorm / RMSNorm forward + backward with an optional fused bias + dropout + residual-add
+// prologue, for f32 / bf16 / fp16 rows of up to 16384 elements.
 //
-// Parity: reference `paddle/phi/kernels/gpu/layer_norm_kernel.cu`,
-// `paddle/fluid/operators/fused/fused_layernorm_residual_dropout_bias.h` and
-// `fused_bias_dropout_residual_layer_norm_op.cu` (the `fused_bias_dropout_residual_layer_norm`
-// op: out = LN(residual + dropout(x + bias))).
+// Parity: reference `paddle/phi/kernels/gpu/layer_norm_kernel.cu` (f32/fp16/bf16 registrations at
+// :218-240), `paddle/fluid/operators/fused/fused_layernorm_residual_dropout_bias.h` and
+// `fused_bias_dropout_residual_layer_norm_op.cu` (out = LN(residual + dropout(x + bias))). RMSNorm
+// (`rms = 1`: no mean subtraction, y = x * rsqrt(mean(x^2) + eps) * gamma) has no reference op; it
+// shares every kernel here through one uniform runtime branch (LLaMA-style residual + RMSNorm).
 //
-// MI355X design: one wave64 per row for rows of up to 8192 elements, the whole row held in
-// registers (16 B/lane loads: each vector instruction moves 1 KiB contiguous), exact two-pass
-// mean/variance from registers (no Welford, no second HBM read). 4 rows per 256-thread block so a
-// 8192×2048 activation gets 2048 blocks (≫ 256 CUs). Backward fuses dgamma/dbeta: every wave
-// accumulates its columns across a grid-stride set of rows in registers, the block reduces them
-// in LDS and adds one f32 atomic per column (no [blocks x N] partial slab, no second pass). Dropout masks are regenerated from a stateless hash in
-// backward (no mask tensor in HBM).
+// MI355X design:
+//  * N <= 4096: one wave64 per row, the whole row in registers (16 B/lane loads: each vector
+//    instruction moves 1 KiB contiguous), exact two-pass mean/variance from registers (no Welford,
+//    no second HBM read); 4 rows per 256-thread block so an 8192 x 2048 activation gets 2048 blocks.
+//  * N > 4096 (LLaMA-13B 5120, 65B 8192, up to 16384) and the few-row decode case: one workgroup per
+//    row (256 or 512 threads), row still register-resident, block reductions through LDS.
+//  * Backward: wave per row up to N = 2048 (220 VGPRs, 2 waves/SIMD), workgroup per row above.
+//  * Backward fuses dgamma/dbeta (and the dbias of the prologue): every thread accumulates its
+//    columns across a grid-stride set of rows in registers, each workgroup stores one row of a
+//    [G][N] partial slab, and a 16-row-strip reduction folds it (G/16 atomics per column). Dropout masks are regenerated from
+//    the stateless counter hash (common.h), never stored.
 #include "common.h"
 
 namespace {
 
-template <bool BF16>
-struct IO;
-template <>
-struct IO<true> {
-  typedef bf16_t T;
+enum { DT_F32 = 0, DT_BF16 = 1, DT_F16 = 2 };
+
+template <int DT>
+struct IO16 {
+  typedef unsigned short T;
   typedef u16x8 Raw;  // 8 elements held in 4 VGPRs until used
+  static __device__ __forceinline__ float cv(unsigned short v) {
+    if (DT == DT_BF16) return bf2f(v);
+    return (float)__builtin_bit_cast(_Float16, v);
+  }
+  static __device__ __forceinline__ unsigned short cvt(float f) {
+    if (DT == DT_BF16) return f2bf(f);
+    return __builtin_bit_cast(unsigned short, (_Float16)f);
+  }
   static __device__ __forceinline__ Raw ldraw(const T* p) { return *reinterpret_cast<const Raw*>(p); }
-  static __device__ __forceinline__ float el(const Raw& r, int j) { return bf2f(r[j]); }
+  static __device__ __forceinline__ float el(const Raw& r, int j) { return cv(r[j]); }
   static __device__ __forceinline__ void load8(const T* p, float* v) {
     u16x8 r = *reinterpret_cast<const u16x8*>(p);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = bf2f(r[j]);
+    for (int j = 0; j < 8; ++j) v[j] = cv(r[j]);
   }
   static __device__ __forceinline__ void store8(T* p, const float* v) {
     u16x8 r;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = f2bf(v[j]);
+    for (int j = 0; j < 8; ++j) r[j] = cvt(v[j]);
     *reinterpret_cast<u16x8*>(p) = r;
   }
+  static __device__ __forceinline__ float load1(const T* p) { return cv(*p); }
+  static __device__ __forceinline__ void store1(T* p, float v) { *p = cvt(v); }
 };
+
+template <int DT>
+struct IO : IO16<DT> {};
 template <>
-struct IO<false> {
+struct IO<DT_F32> {
   typedef float T;
   struct Raw { f32x4 a, b; };
   static __device__ __forceinline__ Raw ldraw(const T* p) {
@@ -56,18 +75,64 @@ struct IO<false> {
     *reinterpret_cast<f32x4*>(p) = a;
     *reinterpret_cast<f32x4*>(p + 4) = b;
   }
+  static __device__ __forceinline__ float load1(const T* p) { return *p; }
+  static __device__ __forceinline__ void store1(T* p, float v) { *p = v; }
 };
 
-// NV = max 8-element vectors per lane (ceil(N / 512)).
-template <int NV, bool BF16>
+// Prologue of one 8-element vector: v = residual + dropout(x + bias). Stores h if asked.
+template <int DT>
+__device__ __forceinline__ void prologue8(float* v, const typename IO<DT>::T* bias,
+                                          const typename IO<DT>::T* residual,
+                                          typename IO<DT>::T* residual_out, size_t base, int col,
+                                          float p_drop, float keep_scale, uint64_t seed,
+                                          uint64_t offset) {
+  typedef IO<DT> io;
+  if (bias) {
+    float b[8];
+    io::load8(bias + col, b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += b[j];
+  }
+  if (p_drop > 0.f) {
+    float u[8];
+    hash_uniform8(seed, offset, base + col, u);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = u[j] >= p_drop ? v[j] * keep_scale : 0.f;
+  }
+  if (residual) {
+    float r[8];
+    io::load8(residual + base + col, r);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += r[j];
+  }
+  if (residual_out) io::store8(residual_out + base + col, v);
+}
+
+// Two sums over a workgroup of NW waves with one LDS round (red holds 2 * NW floats).
+template <int NW>
+__device__ __forceinline__ void block_sum2(float& a, float& b, float* red) {
+  a = wave_sum(a);
+  b = wave_sum(b);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) { red[w] = a; red[NW + w] = b; }
+  __syncthreads();
+  a = 0.f; b = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) { a += red[i]; b += red[NW + i]; }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------------- forward
+// Wave per row. NV = 8-element vectors per lane (ceil(N / 512)), N <= 4096.
+template <int NV, int DT>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(
-    const typename IO<BF16>::T* __restrict__ x, const typename IO<BF16>::T* __restrict__ bias,
-    const typename IO<BF16>::T* __restrict__ residual, const typename IO<BF16>::T* __restrict__ gamma,
-    const typename IO<BF16>::T* __restrict__ beta, typename IO<BF16>::T* __restrict__ y,
-    typename IO<BF16>::T* __restrict__ residual_out, float* __restrict__ mean_out,
+    const typename IO<DT>::T* __restrict__ x, const typename IO<DT>::T* __restrict__ bias,
+    const typename IO<DT>::T* __restrict__ residual, const typename IO<DT>::T* __restrict__ gamma,
+    const typename IO<DT>::T* __restrict__ beta, typename IO<DT>::T* __restrict__ y,
+    typename IO<DT>::T* __restrict__ residual_out, float* __restrict__ mean_out,
     float* __restrict__ rstd_out, int rows, int N, float eps, float p_drop, uint64_t seed,
-    uint64_t offset) {
-  typedef IO<BF16> io;
+    uint64_t offset, int rms) {
+  typedef IO<DT> io;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -81,27 +146,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
     const int vi = i * 64 + lane;
     if (vi < nvec) {
       io::load8(x + base + vi * 8, v[i]);
-      if (bias) {
-        float b[8];
-        io::load8(bias + vi * 8, b);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[i][j] += b[j];
-      }
-      if (p_drop > 0.f) {
-        float u[8];
-        hash_uniform8(seed, offset, base + vi * 8, u);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          v[i][j] = u[j] >= p_drop ? v[i][j] * keep_scale : 0.f;
-        }
-      }
-      if (residual) {
-        float r[8];
-        io::load8(residual + base + vi * 8, r);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[i][j] += r[j];
-      }
-      if (residual_out) io::store8(residual_out + base + vi * 8, v[i]);
+      prologue8<DT>(v[i], bias, residual, residual_out, base, vi * 8, p_drop, keep_scale, seed,
+                    offset);
 #pragma unroll
       for (int j = 0; j < 8; ++j) s += v[i][j];
     } else {
@@ -109,18 +155,16 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
       for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
     }
   }
-  const float mean = wave_sum(s) / (float)N;
+  const float mean = rms ? 0.f : wave_sum(s) / (float)N;
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    const int vi = i * 64 + lane;
-    if (vi < nvec) {
+    if (i * 64 + lane < nvec) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) { float d = v[i][j] - mean; ss += d * d; }
     }
   }
-  const float var = wave_sum(ss) / (float)N;
-  const float rstd = rsqrtf(var + eps);
+  const float rstd = rsqrtf(wave_sum(ss) / (float)N + eps);
   if (lane == 0) {
     if (mean_out) mean_out[row] = mean;
     if (rstd_out) rstd_out[row] = rstd;
@@ -139,90 +183,172 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
   }
 }
 
-// Few-row variant (decode: rows = batch): one 256-thread workgroup per row so every operand of
-// the row (x, bias, residual, gamma, beta) is fetched in ONE round of 16 B loads issued up front;
-// the latency chain is load → block reduce ×2 → store instead of NV dependent wave iterations.
-template <int NV, bool BF16>
-__global__ __launch_bounds__(256) void ln_fwd_row_kernel(
-    const typename IO<BF16>::T* __restrict__ x, const typename IO<BF16>::T* __restrict__ bias,
-    const typename IO<BF16>::T* __restrict__ residual, const typename IO<BF16>::T* __restrict__ gamma,
-    const typename IO<BF16>::T* __restrict__ beta, typename IO<BF16>::T* __restrict__ y,
-    typename IO<BF16>::T* __restrict__ residual_out, float* __restrict__ mean_out,
-    float* __restrict__ rstd_out, int N, float eps, float p_drop, uint64_t seed, uint64_t offset) {
-  typedef IO<BF16> io;
-  __shared__ float red[4];
+// Workgroup (NW waves) per row: the few-row decode case (NW = 4: every operand of the row is
+// fetched in ONE round of 16 B loads issued up front, so the latency chain is load -> 2 block
+// reductions -> store) and rows longer than 4096 (NW = 8, gamma/beta loaded late to bound VGPRs).
+template <int NW, int NV, int DT>
+__global__ __launch_bounds__(NW * 64) void ln_fwd_row_kernel(
+    const typename IO<DT>::T* __restrict__ x, const typename IO<DT>::T* __restrict__ bias,
+    const typename IO<DT>::T* __restrict__ residual, const typename IO<DT>::T* __restrict__ gamma,
+    const typename IO<DT>::T* __restrict__ beta, typename IO<DT>::T* __restrict__ y,
+    typename IO<DT>::T* __restrict__ residual_out, float* __restrict__ mean_out,
+    float* __restrict__ rstd_out, int N, float eps, float p_drop, uint64_t seed, uint64_t offset,
+    int rms) {
+  typedef IO<DT> io;
+  constexpr int T = NW * 64;
+  constexpr bool EARLY = NW == 4;  // hold gamma/beta from the first load round
+  __shared__ float red[2 * NW];
   const int row = blockIdx.x, t = threadIdx.x;
   const int nvec = N >> 3;
   const size_t base = (size_t)row * N;
-  float v[NV][8], g[NV][8], bb[NV][8];
+  float v[NV][8], g[EARLY ? NV : 1][8], bb[EARLY ? NV : 1][8];
   const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  float s = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    const int vi = i * 256 + t;
+    const int vi = i * T + t;
     if (vi < nvec) {
       io::load8(x + base + vi * 8, v[i]);
-      if (gamma) io::load8(gamma + vi * 8, g[i]); else for (int j = 0; j < 8; ++j) g[i][j] = 1.f;
-      if (beta) io::load8(beta + vi * 8, bb[i]); else for (int j = 0; j < 8; ++j) bb[i][j] = 0.f;
-      float b[8], r[8];
-      if (bias) io::load8(bias + vi * 8, b);
-      if (residual) io::load8(residual + base + vi * 8, r);
-      float u[8];
-      if (p_drop > 0.f) hash_uniform8(seed, offset, base + vi * 8, u);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float a = v[i][j] + (bias ? b[j] : 0.f);
-        if (p_drop > 0.f) a = u[j] >= p_drop ? a * keep_scale : 0.f;
-        v[i][j] = a + (residual ? r[j] : 0.f);
+      if (EARLY) {
+        if (gamma) io::load8(gamma + vi * 8, g[i]); else for (int j = 0; j < 8; ++j) g[i][j] = 1.f;
+        if (beta) io::load8(beta + vi * 8, bb[i]); else for (int j = 0; j < 8; ++j) bb[i][j] = 0.f;
       }
-      if (residual_out) io::store8(residual_out + base + vi * 8, v[i]);
+      prologue8<DT>(v[i], bias, residual, residual_out, base, vi * 8, p_drop, keep_scale, seed,
+                    offset);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[i][j];
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
     }
   }
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < NV; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s += v[i][j];
-  const float mean = block_sum<4>(s, red) / (float)N;
+  float dummy = 0.f;
+  if (!rms) block_sum2<NW>(s, dummy, red);
+  const float mean = rms ? 0.f : s / (float)N;
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < NV; ++i)
-    if (i * 256 + t < nvec)
+    if (i * T + t < nvec)
 #pragma unroll
       for (int j = 0; j < 8; ++j) { const float d = v[i][j] - mean; ss += d * d; }
-  const float rstd = rsqrtf(block_sum<4>(ss, red) / (float)N + eps);
+  block_sum2<NW>(ss, dummy, red);
+  const float rstd = rsqrtf(ss / (float)N + eps);
   if (t == 0) {
     if (mean_out) mean_out[row] = mean;
     if (rstd_out) rstd_out[row] = rstd;
   }
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
-    const int vi = i * 256 + t;
+    const int vi = i * T + t;
     if (vi < nvec) {
-      float o[8];
+      float o[8], gl[8], bl[8];
+      const float* gp = g[EARLY ? i : 0];
+      const float* bp = bb[EARLY ? i : 0];
+      if (!EARLY) {
+        if (gamma) io::load8(gamma + vi * 8, gl); else for (int j = 0; j < 8; ++j) gl[j] = 1.f;
+        if (beta) io::load8(beta + vi * 8, bl); else for (int j = 0; j < 8; ++j) bl[j] = 0.f;
+        gp = gl;
+        bp = bl;
+      }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mean) * rstd * g[i][j] + bb[i][j];
+      for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mean) * rstd * gp[j] + bp[j];
       io::store8(y + base + vi * 8, o);
     }
   }
 }
 
-// Backward. x_hat is recomputed from the saved pre-norm input `h` (= residual_out of forward, or x
-// when no prologue) and mean/rstd. Outputs:
-//   dh = LN_bwd(dy) (+ d_res_in if given)      -> written to dres (grad of residual input)
-//   dx = dropout_bwd(dh)                        -> written to dx (grad of x / of x+bias), if dx
-//   per-block partial dgamma/dbeta (+ dbias partial = column sums of dx) -> partials
-template <int NV, bool BF16>
+// ---------------------------------------------------------------------------------- backward
+// x_hat is recomputed from the saved pre-norm input `h` (= residual_out of forward, or x when there
+// is no prologue) and mean/rstd. Outputs:
+//   dh = LN_bwd(dy) (+ d_res_in if given)      -> dres (grad of the residual input)
+//   dx = dropout_bwd(dh)                        -> dx (grad of x / of x+bias), if dx
+//   dgamma / dbeta / dbias(= column sums of dx)  -> f32 atomics into acc_*[N] (zeroed by launcher)
+// RMSNorm: mean == 0 and the mean-gradient term m1 is dropped.
+
+// Per-thread body over one row: TPR threads per row, the thread's vectors are vi = i * TPR + tid.
+// Returns nothing; accumulates into dg/db/dbi.
+template <int NV, int DT, int TPR, int NW>
+__device__ __forceinline__ void ln_bwd_row(
+    const typename IO<DT>::T* __restrict__ dy, const typename IO<DT>::T* __restrict__ h,
+    const typename IO<DT>::T* __restrict__ gamma, float mean, float rstd,
+    const typename IO<DT>::T* __restrict__ dres_in, typename IO<DT>::T* __restrict__ dres,
+    typename IO<DT>::T* __restrict__ dx, size_t base, int tid, int nvec, int N, float p_drop,
+    float keep_scale, uint64_t seed, uint64_t offset, int rms, float (&dg)[NV][8],
+    float (&db)[NV][8], float (&dbi)[NV][8], float* red) {
+  typedef IO<DT> io;
+  // h, dy and the residual gradient of the row are loaded up front as raw vectors (all three
+  // streams in flight together: one memory round trip per row) and x-hat / gamma*dy are recomputed
+  // in the second pass instead of being held in f32 registers.
+  typename io::Raw hr[NV], dr[NV], rr[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int vi = min(i * TPR + tid, nvec - 1);
+    hr[i] = io::ldraw(h + base + vi * 8);
+    dr[i] = io::ldraw(dy + base + vi * 8);
+    if (dres_in) rr[i] = io::ldraw(dres_in + base + vi * 8);
+  }
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int vi = i * TPR + tid;
+    if (vi < nvec) {
+      float g[8];
+      if (gamma) io::load8(gamma + vi * 8, g); else for (int j = 0; j < 8; ++j) g[j] = 1.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = io::el(dr[i], j);
+        const float xh = (io::el(hr[i], j) - mean) * rstd;
+        const float gd = d * g[j];
+        dg[i][j] += d * xh;
+        db[i][j] += d;
+        s1 += gd;
+        s2 += gd * xh;
+      }
+    }
+  }
+  if constexpr (NW == 0) {  // wave per row
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+  } else {
+    block_sum2<NW>(s1, s2, red);
+  }
+  const float m1 = rms ? 0.f : s1 / (float)N, m2 = s2 / (float)N;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int vi = i * TPR + tid;
+    if (vi < nvec) {
+      float g[8], o[8];
+      if (gamma) io::load8(gamma + vi * 8, g); else for (int j = 0; j < 8; ++j) g[j] = 1.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xh = (io::el(hr[i], j) - mean) * rstd;
+        o[j] = rstd * (io::el(dr[i], j) * g[j] - m1 - xh * m2);
+        if (dres_in) o[j] += io::el(rr[i], j);
+      }
+      if (dres) io::store8(dres + base + vi * 8, o);
+      if (dx) {
+        if (p_drop > 0.f) {
+          float u[8];
+          hash_uniform8(seed, offset, base + vi * 8, u);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = u[j] >= p_drop ? o[j] * keep_scale : 0.f;
+        }
+        io::store8(dx + base + vi * 8, o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dbi[i][j] += o[j];
+      }
+    }
+  }
+}
+
+template <int NV, int DT>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(
-    const typename IO<BF16>::T* __restrict__ dy, const typename IO<BF16>::T* __restrict__ h,
-    const typename IO<BF16>::T* __restrict__ gamma, const float* __restrict__ mean_in,
-    const float* __restrict__ rstd_in, const typename IO<BF16>::T* __restrict__ dres_in,
-    typename IO<BF16>::T* __restrict__ dres, typename IO<BF16>::T* __restrict__ dx,
-    float* __restrict__ part_dg, float* __restrict__ part_db, float* __restrict__ part_dbias,
-    int rows, int N, float p_drop, uint64_t seed, uint64_t offset) {
-  typedef IO<BF16> io;
+    const typename IO<DT>::T* __restrict__ dy, const typename IO<DT>::T* __restrict__ h,
+    const typename IO<DT>::T* __restrict__ gamma, const float* __restrict__ mean_in,
+    const float* __restrict__ rstd_in, const typename IO<DT>::T* __restrict__ dres_in,
+    typename IO<DT>::T* __restrict__ dres, typename IO<DT>::T* __restrict__ dx,
+    float* __restrict__ acc_dg, float* __restrict__ acc_db, float* __restrict__ acc_dbias,
+    int rows, int N, float p_drop, uint64_t seed, uint64_t offset, int rms) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nvec = N >> 3;
   float dg[NV][8], db[NV][8], dbi[NV][8];
@@ -231,13 +357,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) { dg[i][j] = 0.f; db[i][j] = 0.f; dbi[i][j] = 0.f; }
   const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  typedef IO<DT> io;
   for (int row = blockIdx.x * 4 + w; row < rows; row += gridDim.x * 4) {
     const size_t base = (size_t)row * N;
     const float mean = mean_in[row], rstd = rstd_in[row];
-    // h, dy and the residual gradient of the row are loaded up front as raw vectors (all three
-    // streams in flight together: one memory round trip per row, not one more after the row
-    // reduction) and x-hat / gamma*dy are recomputed in the second pass instead of being held in
-    // f32 registers: 2 waves/SIMD at N = 2048.
     typename io::Raw hr[NV], dr[NV], rr[NV];
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
@@ -265,7 +388,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
         }
       }
     }
-    const float m1 = wave_sum(s1) / (float)N, m2 = wave_sum(s2) / (float)N;
+    const float m1 = rms ? 0.f : wave_sum(s1) / (float)N, m2 = wave_sum(s2) / (float)N;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int vi = i * 64 + lane;
@@ -284,9 +407,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
             float u[8];
             hash_uniform8(seed, offset, base + vi * 8, u);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              o[j] = u[j] >= p_drop ? o[j] * keep_scale : 0.f;
-            }
+            for (int j = 0; j < 8; ++j) o[j] = u[j] >= p_drop ? o[j] * keep_scale : 0.f;
           }
           io::store8(dx + base + vi * 8, o);
 #pragma unroll
@@ -295,11 +416,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       }
     }
   }
-  // Block-reduce the 4 waves' column partials through LDS, then ONE f32 atomic add per column
-  // per block into acc[N] (zeroed by the launcher): G x N x 4 B of atomics, spread over the
-  // kernel, instead of a [G][N] partial slab and a second column-sum pass.
+  // Block-reduce the 4 waves' column partials through LDS, then one plain coalesced store per
+  // column into this block's row of the [G][N] slab (slab_reduce_kernel folds the G rows).
   __shared__ float red[4][512];
-  float* outs[3] = {part_dg, part_db, part_dbias};
+  float* outs[3] = {acc_dg, acc_db, acc_dbias};
+  const size_t srow = (size_t)blockIdx.x * N;
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
     if (!outs[q]) continue;
@@ -310,18 +431,85 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       __syncthreads();
       for (int c = threadIdx.x; c < 512; c += 256) {
         const int col = i * 512 + c;
-        if (col < N) atomicAdd(outs[q] + col, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
+        if (col < N) outs[q][srow + col] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
       }
       __syncthreads();
     }
   }
 }
 
-// partials [G][N] -> out[N] (f32 or bf16)
-template <bool BF16>
+// Rows longer than 2048 (the wave-per-row variant would drop to 1 wave/SIMD): a 512-thread
+// workgroup per row (NV = ceil(N / 4096) <= 4 vectors per thread), grid-stride over rows; every thread owns distinct columns, so the column partials go
+// straight to the atomics without an LDS reduction.
+template <int NV, int DT>
+__global__ __launch_bounds__(512) void ln_bwd_wide_kernel(
+    const typename IO<DT>::T* __restrict__ dy, const typename IO<DT>::T* __restrict__ h,
+    const typename IO<DT>::T* __restrict__ gamma, const float* __restrict__ mean_in,
+    const float* __restrict__ rstd_in, const typename IO<DT>::T* __restrict__ dres_in,
+    typename IO<DT>::T* __restrict__ dres, typename IO<DT>::T* __restrict__ dx,
+    float* __restrict__ acc_dg, float* __restrict__ acc_db, float* __restrict__ acc_dbias,
+    int rows, int N, float p_drop, uint64_t seed, uint64_t offset, int rms) {
+  __shared__ float red[16];
+  const int nvec = N >> 3;
+  float dg[NV][8], db[NV][8], dbi[NV][8];
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { dg[i][j] = 0.f; db[i][j] = 0.f; dbi[i][j] = 0.f; }
+  const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  for (int row = blockIdx.x; row < rows; row += gridDim.x)
+    ln_bwd_row<NV, DT, 512, 8>(dy, h, gamma, mean_in[row], rstd_in[row], dres_in, dres, dx,
+                               (size_t)row * N, threadIdx.x, nvec, N, p_drop, keep_scale, seed,
+                               offset, rms, dg, db, dbi, red);
+  float* outs[3] = {acc_dg, acc_db, acc_dbias};
+  const size_t srow = (size_t)blockIdx.x * N;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    if (!outs[q]) continue;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int vi = i * 512 + threadIdx.x;
+      if (vi < nvec) {
+        f32x4 a, b;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          a[j] = q == 0 ? dg[i][j] : (q == 1 ? db[i][j] : dbi[i][j]);
+          b[j] = q == 0 ? dg[i][4 + j] : (q == 1 ? db[i][4 + j] : dbi[i][4 + j]);
+        }
+        *reinterpret_cast<f32x4*>(outs[q] + srow + vi * 8) = a;
+        *reinterpret_cast<f32x4*>(outs[q] + srow + vi * 8 + 4) = b;
+      }
+    }
+  }
+}
+
+// [G][N] slab of per-workgroup column partials -> acc[N] (zeroed): block (bx, gy, q) sums rows
+// gy*16 .. +16 of 1024 columns with 16 B loads, then one f32 atomic per column. G x N x 4 B of
+// plain traffic + (G / 16) x N atomics, instead of G x N contended atomics from the backward
+// kernel itself (those dominated the N = 8192 / 16384 backward).
+__global__ __launch_bounds__(256) void slab_reduce_kernel(float* __restrict__ s0, float* __restrict__ s1,
+                                                          float* __restrict__ s2, float* __restrict__ a0,
+                                                          float* __restrict__ a1, float* __restrict__ a2,
+                                                          int G, int N) {
+  const int q = blockIdx.z;
+  const float* slab = q == 0 ? s0 : (q == 1 ? s1 : s2);
+  float* acc = q == 0 ? a0 : (q == 1 ? a1 : a2);
+  if (!slab) return;
+  const int c4 = blockIdx.x * 1024 + threadIdx.x * 4;
+  if (c4 >= N) return;
+  const int g0 = blockIdx.y * 16, g1 = min(g0 + 16, G);
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int g = g0; g < g1; ++g) s += *reinterpret_cast<const f32x4*>(slab + (size_t)g * N + c4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) atomicAdd(acc + c4 + j, s[j]);
+}
+
+// acc[N] (f32, summed over blocks) -> out[N] in the parameter dtype (or += into it).
+template <int DT>
 __global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ part, int G, int N,
-                                                     typename IO<BF16>::T* __restrict__ out,
-                                                     float* __restrict__ out_f32, int accumulate) {
+                                                     typename IO<DT>::T* __restrict__ out,
+                                                     int accumulate) {
   // 256 threads = 64 columns x 4 row-groups
   const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + cl;
@@ -333,141 +521,163 @@ __global__ __launch_bounds__(256) void col_sum_kernel(const float* __restrict__ 
   __syncthreads();
   if (rg == 0 && col < N) {
     float t = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
-    if (out_f32) {
-      out_f32[col] = accumulate ? out_f32[col] + t : t;
-    } else if (BF16) {
-      if (accumulate) t += bf2f(((const bf16_t*)out)[col]);
-      ((bf16_t*)out)[col] = f2bf(t);
-    } else {
-      if (accumulate) t += ((float*)out)[col];
-      ((float*)out)[col] = t;
-    }
+    if (accumulate) t += IO<DT>::load1(out + col);
+    IO<DT>::store1(out + col, t);
   }
 }
 
-template <bool BF16>
+template <int DT>
 int launch_fwd(const void* x, const void* bias, const void* residual, const void* gamma,
                const void* beta, void* y, void* residual_out, float* mean, float* rstd, int rows,
-               int N, float eps, float p, uint64_t seed, uint64_t off, hipStream_t st) {
-  typedef typename IO<BF16>::T T;
-  if (rows <= 64) {  // few rows (decode): a workgroup per row
-    const int nv2 = (N / 8 + 255) / 256;
-#define LNR(NVV)                                                                                \
-  case NVV:                                                                                     \
-    hipLaunchKernelGGL((ln_fwd_row_kernel<NVV, BF16>), dim3(rows), dim3(256), 0, st,           \
-                       (const T*)x, (const T*)bias, (const T*)residual, (const T*)gamma,       \
-                       (const T*)beta, (T*)y, (T*)residual_out, mean, rstd, N, eps, p, seed, off); \
+               int N, float eps, float p, uint64_t seed, uint64_t off, int rms, hipStream_t st) {
+  typedef typename IO<DT>::T T;
+#define ROW_ARGS (const T*)x, (const T*)bias, (const T*)residual, (const T*)gamma, (const T*)beta, \
+                 (T*)y, (T*)residual_out, mean, rstd, N, eps, p, seed, off, rms
+  if (N > 4096) {  // wide rows: 512-thread workgroup per row
+    switch ((N / 8 + 511) / 512) {
+      case 2: hipLaunchKernelGGL((ln_fwd_row_kernel<8, 2, DT>), dim3(rows), dim3(512), 0, st, ROW_ARGS); break;
+      case 3: hipLaunchKernelGGL((ln_fwd_row_kernel<8, 3, DT>), dim3(rows), dim3(512), 0, st, ROW_ARGS); break;
+      case 4: hipLaunchKernelGGL((ln_fwd_row_kernel<8, 4, DT>), dim3(rows), dim3(512), 0, st, ROW_ARGS); break;
+      default: return (int)hipErrorInvalidValue;
+    }
     return (int)hipGetLastError();
-    switch (nv2) { LNR(1) LNR(2) LNR(3) LNR(4) default: break; }
-#undef LNR
   }
+  if (rows <= 64) {  // few rows (decode): a workgroup per row
+    switch ((N / 8 + 255) / 256) {
+      case 1: hipLaunchKernelGGL((ln_fwd_row_kernel<4, 1, DT>), dim3(rows), dim3(256), 0, st, ROW_ARGS); break;
+      case 2: hipLaunchKernelGGL((ln_fwd_row_kernel<4, 2, DT>), dim3(rows), dim3(256), 0, st, ROW_ARGS); break;
+      default: return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
+  }
+#undef ROW_ARGS
   const int nv = (N / 8 + 63) / 64;
   dim3 grid((rows + 3) / 4), block(256);
-#define LNF(NVV)                                                                              \
-  case NVV:                                                                                     \
-    hipLaunchKernelGGL((ln_fwd_kernel<NVV, BF16>), grid, block, 0, st, (const T*)x,            \
-                       (const T*)bias, (const T*)residual, (const T*)gamma, (const T*)beta,    \
-                       (T*)y, (T*)residual_out, mean, rstd, rows, N, eps, p, seed, off);       \
-    break;
+#define LNF(NVV)                                                                                  \
+  hipLaunchKernelGGL((ln_fwd_kernel<NVV, DT>), grid, block, 0, st, (const T*)x, (const T*)bias, \
+                     (const T*)residual, (const T*)gamma, (const T*)beta, (T*)y,               \
+                     (T*)residual_out, mean, rstd, rows, N, eps, p, seed, off, rms);           \
+  break;
   switch (nv) {
-    LNF(1) LNF(2) LNF(3) LNF(4) LNF(5) LNF(6) LNF(8) LNF(10) LNF(12) LNF(16)
-    case 7: hipLaunchKernelGGL((ln_fwd_kernel<8, BF16>), grid, block, 0, st, (const T*)x, (const T*)bias, (const T*)residual, (const T*)gamma, (const T*)beta, (T*)y, (T*)residual_out, mean, rstd, rows, N, eps, p, seed, off); break;
-    case 9: hipLaunchKernelGGL((ln_fwd_kernel<10, BF16>), grid, block, 0, st, (const T*)x, (const T*)bias, (const T*)residual, (const T*)gamma, (const T*)beta, (T*)y, (T*)residual_out, mean, rstd, rows, N, eps, p, seed, off); break;
-    case 11: hipLaunchKernelGGL((ln_fwd_kernel<12, BF16>), grid, block, 0, st, (const T*)x, (const T*)bias, (const T*)residual, (const T*)gamma, (const T*)beta, (T*)y, (T*)residual_out, mean, rstd, rows, N, eps, p, seed, off); break;
-    case 13: case 14: case 15: hipLaunchKernelGGL((ln_fwd_kernel<16, BF16>), grid, block, 0, st, (const T*)x, (const T*)bias, (const T*)residual, (const T*)gamma, (const T*)beta, (T*)y, (T*)residual_out, mean, rstd, rows, N, eps, p, seed, off); break;
+    case 1: LNF(1)
+    case 2: LNF(2)
+    case 3: LNF(3)
+    case 4: LNF(4)
+    case 5: case 6: LNF(6)
+    case 7: case 8: LNF(8)
     default: return (int)hipErrorInvalidValue;
   }
 #undef LNF
   return (int)hipGetLastError();
 }
 
-template <bool BF16>
+// Workgroups of the backward (= rows of the partial slab).
+static inline int bwd_grid(int rows, int N) {
+  const int g = N > 2048 ? rows : (rows + 3) / 4;
+  return g > 512 ? 512 : (g < 1 ? 1 : g);
+}
+
+template <int DT>
 int launch_bwd(const void* dy, const void* h, const void* gamma, const float* mean,
-               const float* rstd, const void* dres_in, void* dres, void* dx, float* part_dg,
-               float* part_db, float* part_dbias, int G, int rows, int N, float p, uint64_t seed,
-               uint64_t off, hipStream_t st) {
-  typedef typename IO<BF16>::T T;
-  const int nv = (N / 8 + 63) / 64;
-  dim3 grid(G), block(256);
-#define LNB(NVV)                                                                               \
-  case NVV:                                                                                    \
-    hipLaunchKernelGGL((ln_bwd_kernel<NVV, BF16>), grid, block, 0, st, (const T*)dy,          \
-                       (const T*)h, (const T*)gamma, mean, rstd, (const T*)dres_in, (T*)dres, \
-                       (T*)dx, part_dg, part_db, part_dbias, rows, N, p, seed, off);          \
-    break;
-  switch (nv) {
-    LNB(1) LNB(2) LNB(3) LNB(4) LNB(5) LNB(6) LNB(8)
-    case 7: hipLaunchKernelGGL((ln_bwd_kernel<8, BF16>), grid, block, 0, st, (const T*)dy, (const T*)h, (const T*)gamma, mean, rstd, (const T*)dres_in, (T*)dres, (T*)dx, part_dg, part_db, part_dbias, rows, N, p, seed, off); break;
+               const float* rstd, const void* dres_in, void* dres, void* dx, float* acc_dg,
+               float* acc_db, float* acc_dbias, int rows, int N, float p, uint64_t seed,
+               uint64_t off, int rms, hipStream_t st) {
+  typedef typename IO<DT>::T T;
+#define BWD_ARGS (const T*)dy, (const T*)h, (const T*)gamma, mean, rstd, (const T*)dres_in, \
+                 (T*)dres, (T*)dx, acc_dg, acc_db, acc_dbias, rows, N, p, seed, off, rms
+  if (N > 2048) {
+    // 512-thread workgroup per row, grid-stride rows; 2 workgroups per CU
+    dim3 grid(bwd_grid(rows, N)), block(512);
+    switch ((N / 8 + 511) / 512) {
+      case 1: hipLaunchKernelGGL((ln_bwd_wide_kernel<1, DT>), grid, block, 0, st, BWD_ARGS); break;
+      case 2: hipLaunchKernelGGL((ln_bwd_wide_kernel<2, DT>), grid, block, 0, st, BWD_ARGS); break;
+      case 3: hipLaunchKernelGGL((ln_bwd_wide_kernel<3, DT>), grid, block, 0, st, BWD_ARGS); break;
+      case 4: hipLaunchKernelGGL((ln_bwd_wide_kernel<4, DT>), grid, block, 0, st, BWD_ARGS); break;
+      default: return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
+  }
+  dim3 grid(bwd_grid(rows, N)), block(256);
+  switch ((N / 8 + 63) / 64) {
+    case 1: hipLaunchKernelGGL((ln_bwd_kernel<1, DT>), grid, block, 0, st, BWD_ARGS); break;
+    case 2: hipLaunchKernelGGL((ln_bwd_kernel<2, DT>), grid, block, 0, st, BWD_ARGS); break;
+    case 3: hipLaunchKernelGGL((ln_bwd_kernel<3, DT>), grid, block, 0, st, BWD_ARGS); break;
+    case 4: hipLaunchKernelGGL((ln_bwd_kernel<4, DT>), grid, block, 0, st, BWD_ARGS); break;
     default: return (int)hipErrorInvalidValue;
   }
-#undef LNB
+#undef BWD_ARGS
   return (int)hipGetLastError();
+}
+
+template <int DT>
+void launch_colsum_out(const float* part, int G, int N, void* out, int acc, hipStream_t st) {
+  hipLaunchKernelGGL((col_sum_kernel<DT>), dim3((N + 63) / 64), dim3(256), 0, st, part, G, N,
+                     (typename IO<DT>::T*)out, acc);
 }
 
 }  // namespace
 
-// dtype: 0 = f32, 1 = bf16. Any of bias/residual/residual_out/gamma/beta/mean/rstd may be null.
+// dtype: 0 = f32, 1 = bf16, 2 = fp16. flags bit 0: RMSNorm. Any of bias / residual /
+// residual_out / gamma / beta / mean / rstd may be null. N % 8 == 0, N <= 16384.
 PIAMD_EXPORT int piamd_layernorm_fwd(int dtype, const void* x, const void* bias,
                                      const void* residual, const void* gamma, const void* beta,
                                      void* y, void* residual_out, float* mean, float* rstd,
                                      int rows, int N, float eps, float p_drop, uint64_t seed,
-                                     uint64_t offset, hipStream_t stream) {
-  if (N % 8 != 0 || N > 8192) return (int)hipErrorInvalidValue;
+                                     uint64_t offset, int flags, hipStream_t stream) {
+  if (N % 8 != 0 || N > 16384 || dtype < 0 || dtype > 2) return (int)hipErrorInvalidValue;
   if (rows == 0) return 0;
-  return dtype ? launch_fwd<true>(x, bias, residual, gamma, beta, y, residual_out, mean, rstd,
-                                  rows, N, eps, p_drop, seed, offset, stream)
-               : launch_fwd<false>(x, bias, residual, gamma, beta, y, residual_out, mean, rstd,
-                                   rows, N, eps, p_drop, seed, offset, stream);
+  const int rms = flags & 1;
+#define FWD(D) launch_fwd<D>(x, bias, residual, gamma, beta, y, residual_out, mean, rstd, rows, N, \
+                             eps, p_drop, seed, offset, rms, stream)
+  return dtype == DT_BF16 ? FWD(DT_BF16) : (dtype == DT_F16 ? FWD(DT_F16) : FWD(DT_F32));
+#undef FWD
 }
 
-// Number of partial rows the backward uses (caller allocates partials [G][N] f32).
-PIAMD_EXPORT int piamd_layernorm_bwd_grid(int rows) {
-  int g = (rows + 3) / 4;
-  return g > 512 ? 512 : (g < 1 ? 1 : g);
+// Floats of workspace piamd_layernorm_bwd needs: three [G][N] partial slabs + three [N] sums.
+PIAMD_EXPORT long long piamd_layernorm_bwd_ws(int rows, int N) {
+  return 3LL * ((long long)bwd_grid(rows, N) * N + N);
 }
 
-// Backward. part_* are f32 [N] accumulators (zeroed here); dgamma/dbeta/dbias outputs (dtype of
-// the params) are converted from them; each may be null.
+// Backward. ws: piamd_layernorm_bwd_ws(rows, N) floats. dgamma / dbeta / dbias outputs (same
+// dtype as the activations) are written from the column sums, or added into per accum_mask bit.
 PIAMD_EXPORT int piamd_layernorm_bwd(int dtype, const void* dy, const void* h, const void* gamma,
                                      const float* mean, const float* rstd, const void* dres_in,
                                      void* dres, void* dx, void* dgamma, void* dbeta, void* dbias,
-                                     float* part_dg, float* part_db, float* part_dbias, int rows,
-                                     int N, float p_drop, uint64_t seed, uint64_t offset,
-                                     int accum_mask, hipStream_t stream) {
-  if (N % 8 != 0 || N > 4096) return (int)hipErrorInvalidValue;
+                                     float* ws, int rows, int N, float p_drop, uint64_t seed,
+                                     uint64_t offset, int accum_mask, int flags,
+                                     hipStream_t stream) {
+  if (N % 8 != 0 || N > 16384 || dtype < 0 || dtype > 2) return (int)hipErrorInvalidValue;
   if (rows == 0) return 0;
-  const int G = piamd_layernorm_bwd_grid(rows);
-  if (dgamma) (void)hipMemsetAsync(part_dg, 0, sizeof(float) * N, stream);
-  if (dbeta) (void)hipMemsetAsync(part_db, 0, sizeof(float) * N, stream);
-  if (dbias) (void)hipMemsetAsync(part_dbias, 0, sizeof(float) * N, stream);
-  int e = dtype ? launch_bwd<true>(dy, h, gamma, mean, rstd, dres_in, dres, dx,
-                                   dgamma ? part_dg : nullptr, dbeta ? part_db : nullptr,
-                                   dbias ? part_dbias : nullptr, G, rows, N, p_drop, seed, offset,
-                                   stream)
-                : launch_bwd<false>(dy, h, gamma, mean, rstd, dres_in, dres, dx,
-                                    dgamma ? part_dg : nullptr, dbeta ? part_db : nullptr,
-                                    dbias ? part_dbias : nullptr, G, rows, N, p_drop, seed,
-                                    offset, stream);
-  if (e) return e;
+  const int rms = flags & 1;
+  const int G = bwd_grid(rows, N);
   void* outs[3] = {dgamma, dbeta, dbias};
-  float* parts[3] = {part_dg, part_db, part_dbias};
+  float *slab[3], *acc[3];
+  for (int q = 0; q < 3; ++q) {
+    slab[q] = outs[q] ? ws + (size_t)q * G * N : nullptr;
+    acc[q] = outs[q] ? ws + (size_t)3 * G * N + (size_t)q * N : nullptr;
+    if (outs[q]) (void)hipMemsetAsync(acc[q], 0, sizeof(float) * N, stream);
+  }
+#define BWD(D) launch_bwd<D>(dy, h, gamma, mean, rstd, dres_in, dres, dx, slab[0], slab[1], slab[2], \
+                             rows, N, p_drop, seed, offset, rms, stream)
+  int e = dtype == DT_BF16 ? BWD(DT_BF16) : (dtype == DT_F16 ? BWD(DT_F16) : BWD(DT_F32));
+#undef BWD
+  if (e) return e;
+  if (dgamma || dbeta || dbias)
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3((N + 1023) / 1024, (G + 15) / 16, 3), dim3(256), 0,
+                       stream, slab[0], slab[1], slab[2], acc[0], acc[1], acc[2], G, N);
   for (int q = 0; q < 3; ++q) {
     if (!outs[q]) continue;
-    dim3 grid((N + 63) / 64), block(256);
-    const int acc = (accum_mask >> q) & 1;  // add into an existing grad (e.g. a flat main_grad view)
-    if (dtype)
-      hipLaunchKernelGGL((col_sum_kernel<true>), grid, block, 0, stream, parts[q], 1, N,
-                         (bf16_t*)outs[q], (float*)nullptr, acc);
-    else
-      hipLaunchKernelGGL((col_sum_kernel<false>), grid, block, 0, stream, parts[q], 1, N,
-                         (float*)outs[q], (float*)nullptr, acc);
+    const int a = (accum_mask >> q) & 1;  // add into an existing grad (e.g. a flat main_grad view)
+    if (dtype == DT_BF16) launch_colsum_out<DT_BF16>(acc[q], 1, N, outs[q], a, stream);
+    else if (dtype == DT_F16) launch_colsum_out<DT_F16>(acc[q], 1, N, outs[q], a, stream);
+    else launch_colsum_out<DT_F32>(acc[q], 1, N, outs[q], a, stream);
   }
   return (int)hipGetLastError();
 }
 
 // Column sum of a [rows][N] matrix into out[N] (bias gradients). Uses the same partial scheme.
-template <bool BF16>
-__global__ __launch_bounds__(256) void rowsum_partial_kernel(const typename IO<BF16>::T* __restrict__ x,
+template <int DT>
+__global__ __launch_bounds__(256) void rowsum_partial_kernel(const typename IO<DT>::T* __restrict__ x,
                                                             int rows, int N,
                                                             float* __restrict__ part) {
   // block handles 256 columns (one per thread) over a grid-stride set of rows
@@ -475,8 +685,7 @@ __global__ __launch_bounds__(256) void rowsum_partial_kernel(const typename IO<B
   if (col >= N) return;
   float s = 0.f;
   for (int r = blockIdx.x; r < rows; r += gridDim.x) {
-    if (BF16) s += bf2f(((const bf16_t*)x)[(size_t)r * N + col]);
-    else s += ((const float*)x)[(size_t)r * N + col];
+    s += IO<DT>::load1(x + (size_t)r * N + col);
   }
   part[(size_t)blockIdx.x * N + col] = s;
 }
@@ -510,22 +719,22 @@ __global__ __launch_bounds__(256) void rowsum_partial_bf16x8_kernel(const bf16_t
 PIAMD_EXPORT int piamd_colsum(int dtype, const void* x, void* out, float* part, int G, int rows,
                               int N, int accumulate, hipStream_t stream) {
   if (rows == 0) return 0;
+  if (dtype < 0 || dtype > 2) return (int)hipErrorInvalidValue;
   dim3 grid(G, (N + 255) / 256), block(256);
-  if (dtype && N % 8 == 0)
+  if (dtype == DT_BF16 && N % 8 == 0)
     hipLaunchKernelGGL(rowsum_partial_bf16x8_kernel, dim3(G, (N / 8 + 255) / 256), block, 0, stream,
                        (const bf16_t*)x, rows, N, part);
-  else if (dtype)
-    hipLaunchKernelGGL((rowsum_partial_kernel<true>), grid, block, 0, stream, (const bf16_t*)x,
+  else if (dtype == DT_BF16)
+    hipLaunchKernelGGL((rowsum_partial_kernel<DT_BF16>), grid, block, 0, stream, (const bf16_t*)x,
                        rows, N, part);
+  else if (dtype == DT_F16)
+    hipLaunchKernelGGL((rowsum_partial_kernel<DT_F16>), grid, block, 0, stream,
+                       (const unsigned short*)x, rows, N, part);
   else
-    hipLaunchKernelGGL((rowsum_partial_kernel<false>), grid, block, 0, stream, (const float*)x,
+    hipLaunchKernelGGL((rowsum_partial_kernel<DT_F32>), grid, block, 0, stream, (const float*)x,
                        rows, N, part);
-  dim3 g2((N + 63) / 64);
-  if (dtype)
-    hipLaunchKernelGGL((col_sum_kernel<true>), g2, dim3(256), 0, stream, part, G, N, (bf16_t*)out,
-                       (float*)nullptr, accumulate);
-  else
-    hipLaunchKernelGGL((col_sum_kernel<false>), g2, dim3(256), 0, stream, part, G, N,
-                       (float*)out, (float*)nullptr, accumulate);
+  if (dtype == DT_BF16) launch_colsum_out<DT_BF16>(part, G, N, out, accumulate, stream);
+  else if (dtype == DT_F16) launch_colsum_out<DT_F16>(part, G, N, out, accumulate, stream);
+  else launch_colsum_out<DT_F32>(part, G, N, out, accumulate, stream);
   return (int)hipGetLastError();
 }

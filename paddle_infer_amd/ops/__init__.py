@@ -3,7 +3,7 @@
 GPU tensors run the in-tree HIP library (``_lib/libpiamd_kernels.so``); CPU tensors run the
 PyTorch reference composition of the same op.
 """
-from .norm import layer_norm, fused_add_layer_norm, rms_norm  # noqa: F401
+from .norm import layer_norm, fused_add_layer_norm, rms_norm, fused_add_rms_norm  # noqa: F401
 from .attention import (flash_attention, flash_attention_packed, attention_reference,  # noqa: F401
                         flash_attention_varlen)
 from .activation import bias_act, gelu, dropout, fused_softmax_mask  # noqa: F401

@@ -25,15 +25,18 @@ _LOCK = threading.Lock()
 c_void_p, c_int, c_float, c_ll, c_u64 = (ctypes.c_void_p, ctypes.c_int, ctypes.c_float,
                                          ctypes.c_longlong, ctypes.c_uint64)
 
-# name -> argtypes (restype is always int = hipError_t)
+# name -> argtypes (restype is int = hipError_t unless listed in _RESTYPES)
 _SIGS = {
+    # dtype, x, bias, residual, gamma, beta, y, residual_out, mean, rstd, rows, N, eps, p, seed,
+    # offset, flags (bit0 = RMSNorm), stream
     "piamd_layernorm_fwd": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                             c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_float, c_u64,
-                            c_u64, c_void_p],
-    "piamd_layernorm_bwd_grid": [c_int],
+                            c_u64, c_int, c_void_p],
+    # dtype, dy, h, gamma, mean, rstd, dres_in, dres, dx, dgamma, dbeta, dbias, ws, rows, N, p,
+    # seed, offset, accum_mask, flags, stream
     "piamd_layernorm_bwd": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                            c_void_p, c_int, c_int, c_float, c_u64, c_u64, c_int, c_void_p],
+                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                            c_float, c_u64, c_u64, c_int, c_int, c_void_p],
     "piamd_colsum": [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p],
     "piamd_adamw_flat": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_ll, c_float,
                          c_void_p, c_float, c_float, c_float, c_float, c_float, c_float, c_void_p,
@@ -78,6 +81,10 @@ _SIGS = {
 }
 
 
+_RESTYPES = {"piamd_layernorm_bwd_ws": ctypes.c_longlong}
+_SIGS["piamd_layernorm_bwd_ws"] = [c_int, c_int]
+
+
 def lib_path() -> str:
     # PIAMD_KERNEL_LIB: load another build of the kernel library (A/B timing of a kernel edit)
     return os.environ.get("PIAMD_KERNEL_LIB") or _build.KERNEL_LIB
@@ -99,7 +106,7 @@ def _load():
             if fn is None:
                 continue
             fn.argtypes = args
-            fn.restype = ctypes.c_int
+            fn.restype = _RESTYPES.get(name, ctypes.c_int)
         _LIB = lib
         return _LIB
 
@@ -135,12 +142,31 @@ def ptr(t) -> int | None:
     return None if t is None else t.data_ptr()
 
 
-def dtype_code(t: torch.Tensor) -> int:
+def dtype_code(t: torch.Tensor, fp16: bool = False) -> int:
+    """Kernel dtype code: 0 = f32, 1 = bf16, 2 = fp16 (only for kernels built for it: ``fp16=True``)."""
     if t.dtype == torch.bfloat16:
         return 1
     if t.dtype == torch.float32:
         return 0
-    raise TypeError(f"unsupported dtype {t.dtype} for HIP kernel (bf16/f32 only)")
+    if fp16 and t.dtype == torch.float16:
+        return 2
+    raise TypeError(f"unsupported dtype {t.dtype} for this HIP kernel "
+                    f"({'bf16/fp16/f32' if fp16 else 'bf16/f32'} only)")
+
+
+# GPU ops that had to leave the HIP path: (op, reason) -> count. Each (op, reason) warns once;
+# tests assert this stays empty on the shapes/dtypes the kernels claim.
+FALLBACKS: dict = {}
+
+
+def fallback(op: str, reason: str) -> None:
+    """Record (and warn once about) a GPU op that runs its PyTorch reference instead of HIP."""
+    key = (op, reason)
+    if key not in FALLBACKS:
+        import warnings
+        warnings.warn(f"paddle_infer_amd: {op} runs the PyTorch reference on GPU ({reason})",
+                      RuntimeWarning, stacklevel=3)
+    FALLBACKS[key] = FALLBACKS.get(key, 0) + 1
 
 
 def main_grad(p):

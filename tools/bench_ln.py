@@ -11,7 +11,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import paddle_infer_amd  # noqa: E402,F401
-from paddle_infer_amd.ops.norm import fused_add_layer_norm  # noqa: E402
+from paddle_infer_amd.ops.norm import fused_add_layer_norm, fused_add_rms_norm  # noqa: E402
 
 
 def main():
@@ -20,18 +20,23 @@ def main():
     ap.add_argument("--hidden", type=int, default=2048)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--dropout", type=float, default=0.1)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16", "f32"])
+    ap.add_argument("--rms", action="store_true", help="fused residual + RMSNorm instead of LayerNorm")
     a = ap.parse_args()
+    dt = {"bf16": torch.bfloat16, "fp16": torch.float16, "f32": torch.float32}[a.dtype]
     dev = torch.device("cuda")
     R, N = a.rows, a.hidden
-    x = torch.randn(R, N, device=dev, dtype=torch.bfloat16, requires_grad=True)
-    res = torch.randn(R, N, device=dev, dtype=torch.bfloat16, requires_grad=True)
-    w = torch.ones(N, device=dev, dtype=torch.bfloat16, requires_grad=True)
-    b = torch.zeros(N, device=dev, dtype=torch.bfloat16, requires_grad=True)
-    xb = torch.zeros(N, device=dev, dtype=torch.bfloat16, requires_grad=True)
-    dy = torch.randn(R, N, device=dev, dtype=torch.bfloat16)
-    dh = torch.randn(R, N, device=dev, dtype=torch.bfloat16)
+    x = torch.randn(R, N, device=dev, dtype=dt, requires_grad=True)
+    res = torch.randn(R, N, device=dev, dtype=dt, requires_grad=True)
+    w = torch.ones(N, device=dev, dtype=dt, requires_grad=True)
+    b = torch.zeros(N, device=dev, dtype=dt, requires_grad=True)
+    xb = torch.zeros(N, device=dev, dtype=dt, requires_grad=True)
+    dy = torch.randn(R, N, device=dev, dtype=dt)
+    dh = torch.randn(R, N, device=dev, dtype=dt)
 
     def fwd():
+        if a.rms:
+            return fused_add_rms_norm(x, res, w, x_bias=xb, dropout_p=a.dropout, training=True)
         return fused_add_layer_norm(x, res, w, b, x_bias=xb, dropout_p=a.dropout, training=True)
 
     def bwd(y, h):
@@ -55,9 +60,9 @@ def main():
         tf += e0.elapsed_time(e1)
         tb += e1.elapsed_time(e2)
     tf, tb = tf / a.iters, tb / a.iters
-    el = R * N * 2
+    el = R * N * x.element_size()
     # fwd: x, residual in; y, h out. bwd: dy, h, dh in; dres, dx out (dropout > 0)
-    print(json.dumps({"rows": R, "hidden": N, "dropout": a.dropout, "fwd_ms": round(tf, 4),
+    print(json.dumps({"rows": R, "hidden": N, "dtype": a.dtype, "rms": a.rms, "dropout": a.dropout, "fwd_ms": round(tf, 4),
                       "bwd_ms": round(tb, 4), "fwd_TBps": round(4 * el / tf / 1e9, 2),
                       "bwd_TBps": round(5 * el / tb / 1e9, 2)}), flush=True)
 

@@ -1,0 +1,915 @@
+// Flash attention forward / backward on CDNA4 MFMA (bf16 or fp16 in, f32 accumulate), with
+// in-kernel attention dropout and an additive attention mask / bias.
+//
+// Parity: reference `python/paddle/nn/functional/flash_attention.py:142` (flash_attention with
+// `dropout`, scaled_dot_product_attention, flash_attn_unpadded), `paddle/phi/kernels/gpu/
+// flash_attn_kernel.cu`, and the fork's CUTLASS `phi/kernels/fusion/cutlass/
+// memory_efficient_attention*.cu` / `variable_length_memory_efficient_attention.cu` (LSE output,
+// causal mask, additive mask, GQA via kv-head grouping, packed variable-length batches).
+//
+// This header holds the kernels; flash_attn.hip (bf16) and flash_attn_f16.hip (fp16) instantiate
+// them in two translation units so the two halves compile in parallel.
+//
+// MI355X design (cdna_hip_programming.md §3, T2, T10, T12, App. B "Fused attention prefill",
+// "Attention backward"):
+//   * Layout [B, S, H, D] with free b/s/h strides, so Q/K/V are consumed straight out of the fused
+//     QKV projection output and dQ/dK/dV are written straight into the fused dQKV gradient.
+//   * Head dims: D in {64, 96, 128}. LDS rows are DP = 64 / 128 elements (power of two, so the XOR
+//     swizzle stays closed); D = 96 uses 128-element rows whose last 4 chunks are never read.
+//   * Forward: workgroup = 4 waves = 128 query rows (32 per wave), K/V tiles of 64 keys DMA'd
+//     straight into LDS (global_load_lds_dwordx4), double buffered. SWAPPED products with
+//     v_mfma_f32_32x32x16_{bf16,f16}: Sᵀ = K·Qᵀ puts one query row per lane, so the online-softmax
+//     row max/sum is 31 in-lane ops + one cross-half shuffle, and the Sᵀ accumulator is directly
+//     the B operand of Oᵀ = Vᵀ·Pᵀ (no LDS round trip for P). Vᵀ fragments come from the row-major
+//     V image with ds_read_b64_tr_b16 (hardware transpose).
+//   * Backward = two atomic-free kernels. dK/dV: workgroup = 128 keys (key on the MFMA lane),
+//     dKᵀ/dVᵀ kept in accumulators across the whole sweep over query tiles and the q-heads of a GQA
+//     group. dQ: the forward's structure (query row on the lane), dSᵀ feeds dQᵀ = Kᵀ·dSᵀ from
+//     registers. Recomputing S/dP in the dQ kernel removes the f32 dQ atomics and keeps the
+//     result bitwise deterministic.
+//   * Dropout: keep(q, key) is a stateless counter hash of (seed, offset, row, key) — the same
+//     keyed two-round lowbias32 as the LayerNorm dropout (common.h), one 32-bit hash per PAIR of
+//     adjacent keys (two 16-bit uniforms). The forward, dK/dV and dQ kernels regenerate the same
+//     mask; nothing is stored. The row sum l uses the undropped P (softmax normaliser), O uses
+//     P∘M, and 1/(1-p) is folded into the epilogue scale.
+//   * Mask: additive [B|1, H|1, Sq, Sk] bias in the input dtype (element strides, 0 = broadcast),
+//     added to the scaled logits before the softmax in all three kernels; rows padded to a
+//     multiple of 4 keys by the caller so each lane reads 8 B per 4 keys.
+//   * Every global load is unconditional (row indices clamped, out-of-range rows masked in the
+//     softmax), so hipcc can count `vmcnt` and the K/V prefetch stays in flight under the MFMAs.
+//   * Causal grids are flattened and launched heaviest-first (LPT order across all heads).
+#pragma once
+#include "common.h"
+
+// C ABI argument block (ops/attention.py mirrors it as a ctypes.Structure).
+struct FaArgs {
+  const void *q, *k, *v;
+  void* o;
+  float* lse;
+  const void* dout;
+  float* delta;
+  void *dq, *dk, *dv;
+  const void* mask;  // additive, input dtype; null = none
+  const int *cu_q, *cu_k;
+  int B, Sq, Sk, Hq, Hk, D, ltot, causal;
+  long long sqb, sqs, sqh, skb, sks, skh, svb, svs, svh, sob, sos, soh;
+  long long smb, smh, smq;  // mask strides (elements; 0 = broadcast)
+  float scale, p_drop;
+  unsigned long long seed, offset;
+};
+
+namespace fa {
+
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4_t lds_s16x4;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+enum { F_DROP = 1, F_MASK = 2 };
+
+template <bool F16>
+struct ET;
+template <>
+struct ET<false> {
+  typedef bf16x8 V8;
+  static __device__ __forceinline__ f32x16 mfma(V8 a, V8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ float tof(unsigned short u) { return bf2f(u); }
+  static __device__ __forceinline__ unsigned short fromf(float f) { return f2bf(f); }
+  static __device__ __forceinline__ V8 frag(const f32x16& acc, int s) {
+    V8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (__bf16)acc[8 * s + j];
+    return r;
+  }
+};
+template <>
+struct ET<true> {
+  typedef f16x8 V8;
+  static __device__ __forceinline__ f32x16 mfma(V8 a, V8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ float tof(unsigned short u) {
+    return (float)__builtin_bit_cast(_Float16, u);
+  }
+  static __device__ __forceinline__ unsigned short fromf(float f) {
+    return __builtin_bit_cast(unsigned short, (_Float16)f);
+  }
+  static __device__ __forceinline__ V8 frag(const f32x16& acc, int s) {
+    V8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (_Float16)acc[8 * s + j];
+    return r;
+  }
+};
+template <bool F16>
+__device__ __forceinline__ unsigned pack2(float lo, float hi) {
+  return (unsigned)ET<F16>::fromf(lo) | ((unsigned)ET<F16>::fromf(hi) << 16);
+}
+
+// Dual-use LDS image (guide T10 layout (b)): byte offset of 16-B chunk `ch` of row `row` in an
+// image with ROWB-byte rows (ROWB / 16 a power of two).
+template <int ROWB>
+__device__ __forceinline__ int lds_off(int row, int ch) {
+  constexpr int CH = ROWB / 16;
+  const int x = (((row & 3) << 2) | ((row >> 2) & 3)) & (CH - 1);
+  return row * ROWB + ((ch ^ x) << 4);
+}
+
+template <bool F16>
+__device__ __forceinline__ typename ET<F16>::V8 lds_row8(const char* base, int off) {
+  return *reinterpret_cast<const typename ET<F16>::V8*>(base + off);
+}
+
+// Transposed read: 16-lane group reads a 4-row x 16-col block starting at (r0, c0 elems); lane i
+// of the group receives column c0+i of rows r0..r0+3.
+template <int ROWB>
+__device__ __forceinline__ s16x4_t lds_tr4(const char* base, int r0, int c0, int gi) {
+  const int q = gi >> 2, p = gi & 3;
+  const int col = c0 + 4 * p;
+  const int off = lds_off<ROWB>(r0 + q, col >> 3) + ((col & 7) << 1);
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + off));
+}
+
+template <bool F16>
+__device__ __forceinline__ typename ET<F16>::V8 cat44(s16x4_t a, s16x4_t b) {
+  s16x8 t = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(typename ET<F16>::V8, t);
+}
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Direct-to-LDS DMA (global_load_lds_dwordx4) of a [ROWS][ROWB] tile into the dual-use XOR image.
+// The LDS destination of one wave-instruction is lane-linear (1 KiB), so the swizzle is applied
+// to the per-lane SOURCE address (guide §5.4 rule 21): physical chunk pc of row r holds logical
+// chunk pc ^ x(r). Rows past `rmax` are clamped (masked later); logical chunks past the head dim
+// (D < DP) re-read chunk 0 (in bounds, never consumed).
+template <int ROWS, int ROWB, int DCH>
+__device__ __forceinline__ void glds_tile(const unsigned short* gbase, long long rstride, int row0,
+                                          int rmax, char* tile, int w, int lane) {
+  constexpr int CH = ROWB / 16;
+  constexpr int PIECES = ROWS * CH / 64;
+  constexpr int PPW = PIECES / 4;
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int P = w * PPW + i;
+    const int L = P * 64 + lane, r = L / CH, pc = L % CH;
+    const int x = (((r & 3) << 2) | ((r >> 2) & 3)) & (CH - 1);
+    const long long row = min(row0 + r, rmax);
+    int lc = pc ^ x;
+    if (DCH < CH) lc = lc < DCH ? lc : 0;
+    const unsigned short* src = gbase + row * rstride + (lc << 3);
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(tile + P * 1024),
+                                     16, 0, 0);
+  }
+}
+
+// Dropout key: (seed, offset) folded into two 32-bit round keys, uniform over the grid.
+struct DropKey {
+  uint32_t lo, hi, thr;  // thr = p * 65536: keep iff 16-bit uniform >= thr
+  float inv;             // 1 / (1 - p)
+};
+__device__ __forceinline__ DropKey drop_key(float p, uint64_t seed, uint64_t offset) {
+  DropKey k;
+  k.lo = rng_key(seed, offset);
+  k.hi = lowbias32(k.lo ^ 0x632BE5ABu);
+  k.thr = (uint32_t)(p * 65536.f);
+  k.inv = 1.f / (1.f - p);
+  return k;
+}
+// 32-bit hash of the key pair (key >> 1) of attention row `row` (row = lse index: every (batch,
+// head, query) has its own). half = key & 1 selects the 16-bit uniform.
+__device__ __forceinline__ uint32_t drop_hash(const DropKey& k, long long row, int sk_half,
+                                              int key) {
+  const uint64_t pair = (uint64_t)row * (uint64_t)sk_half + (uint64_t)(key >> 1);
+  return lowbias32(lowbias32((uint32_t)pair + k.lo) ^ (k.hi ^ ((uint32_t)(pair >> 32) * 0x85EBCA6Bu)));
+}
+__device__ __forceinline__ bool drop_keep(const DropKey& k, uint32_t h, int key) {
+  return ((key & 1) ? (h >> 16) : (h & 0xFFFFu)) >= k.thr;
+}
+
+// 4 consecutive mask values (keys key0..key0+3, key0 % 4 == 0) of one mask row, as f32 * log2e.
+template <bool F16>
+__device__ __forceinline__ f32x4 mask4(const unsigned short* mrow, int key0, int Sk) {
+  const int kk = key0 < Sk ? key0 : 0;
+  const u16x4 m = *reinterpret_cast<const u16x4*>(mrow + kk);
+  f32x4 r;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) r[e] = ET<F16>::tof(m[e]) * kLog2e;
+  return r;
+}
+
+// ------------------------------------------------------------------------------------------
+// Forward
+// ------------------------------------------------------------------------------------------
+template <int D, bool F16, bool CAUSAL, int FEAT>
+__global__ __launch_bounds__(256, 2) void fwd_kernel(FaArgs a) {
+  typedef ET<F16> E;
+  typedef typename E::V8 V8;
+  constexpr int DP = D > 64 ? 128 : 64;
+  constexpr int BM = 128, BN = 64;
+  constexpr int KSTEPS = D / 16;
+  constexpr int DT = D / 32;
+  constexpr int ROWB = DP * 2;
+  constexpr int TILE_B = BN * ROWB;  // bytes per K or V tile
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_B];
+
+  const unsigned short* q = (const unsigned short*)a.q;
+  const unsigned short* k = (const unsigned short*)a.k;
+  const unsigned short* v = (const unsigned short*)a.v;
+  unsigned short* o = (unsigned short*)a.o;
+  const int B = a.B, SqMax = a.Sq, Hq = a.Hq, Hk = a.Hk;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5, gi = lane & 15, g = lane >> 4;
+  const int nmb = (SqMax + BM - 1) / BM;
+  const int HB = Hq * B;
+  const int mb = CAUSAL ? (nmb - 1 - (int)blockIdx.x / HB) : (int)blockIdx.x / HB;
+  const int hq = (int)blockIdx.x % Hq, b = ((int)blockIdx.x % HB) / Hq;
+  const int hk = hq / (Hq / Hk);
+  const int m0 = mb * BM;
+  int Sq = SqMax, Sk = a.Sk;
+  long long lbase = ((long long)b * Hq + hq) * SqMax;
+  if (a.cu_q) {  // variable-length: b = sequence, rows [cu[b], cu[b+1]) of the packed tensors
+    const int q0s = a.cu_q[b], k0s = a.cu_k[b];
+    Sq = a.cu_q[b + 1] - q0s;
+    Sk = a.cu_k[b + 1] - k0s;
+    if (m0 >= Sq) return;  // block-uniform: this sequence is shorter than the longest
+    q += (long long)q0s * a.sqs;
+    o += (long long)q0s * a.sos;
+    k += (long long)k0s * a.sks;
+    v += (long long)k0s * a.svs;
+    lbase = (long long)hq * a.ltot + q0s;
+  }
+  const int qrow0 = m0 + w * 32;
+  const int coff = Sk - Sq;  // bottom-right aligned causal offset
+  const float c = a.scale * kLog2e;
+  const int qpos = qrow0 + l32;
+
+  const unsigned short* kbase = k + b * a.skb + hk * a.skh;
+  const unsigned short* vbase = v + b * a.svb + hk * a.svh;
+  const unsigned short* mrow = nullptr;
+  if (FEAT & F_MASK)
+    mrow = (const unsigned short*)a.mask + b * a.smb + hq * a.smh + (long long)min(qpos, Sq - 1) * a.smq;
+  DropKey dk;
+  if (FEAT & F_DROP) dk = drop_key(a.p_drop, a.seed, a.offset);
+  const int sk_half = (a.Sk + 1) >> 1;
+
+  V8 qf[KSTEPS];
+  {
+    const int qr = min(qpos, Sq - 1);
+    const unsigned short* qp = q + b * a.sqb + (long long)qr * a.sqs + hq * a.sqh + 8 * hh;
+#pragma unroll
+    for (int kk = 0; kk < KSTEPS; ++kk) qf[kk] = *reinterpret_cast<const V8*>(qp + 16 * kk);
+  }
+
+  int n_end = Sk;
+  if (CAUSAL) n_end = min(Sk, m0 + BM + coff);
+  const int ntiles = n_end <= 0 ? 0 : (n_end + BN - 1) / BN;
+
+  f32x16 oacc[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) oacc[i][j] = 0.f;
+  float m_i = -INFINITY, l_i = 0.f;
+
+  auto issue = [&](int t, int buf) {
+    char* ks = smem + buf * 2 * TILE_B;
+    glds_tile<BN, ROWB, D / 8>(kbase, a.sks, t * BN, Sk - 1, ks, w, lane);
+    glds_tile<BN, ROWB, D / 8>(vbase, a.svs, t * BN, Sk - 1, ks + TILE_B, w, lane);
+  };
+  if (ntiles > 0) issue(0, 0);
+  __syncthreads();
+
+  const bool wave_rows_valid = qrow0 < Sq;
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) issue(t + 1, buf ^ 1);
+    const int n0 = t * BN;
+    const bool active = wave_rows_valid && (!CAUSAL || n0 <= qrow0 + 31 + coff);
+    if (active) {
+      const char* ks = smem + buf * 2 * TILE_B;
+      const char* vs = ks + TILE_B;
+      f32x16 sacc[2];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) sacc[tt][j] = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < KSTEPS; ++kk) {
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+          V8 af = lds_row8<F16>(ks, lds_off<ROWB>(tt * 32 + l32, 2 * kk + hh));
+          sacc[tt] = E::mfma(af, qf[kk], sacc[tt]);
+        }
+      }
+      const bool need_mask = (n0 + BN > Sk) || (CAUSAL && n0 + BN - 1 > qrow0 + coff);
+      float mx = -INFINITY;
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int key0 = n0 + tt * 32 + 8 * g4 + 4 * hh;
+          f32x4 mb4 = {0.f, 0.f, 0.f, 0.f};
+          if (FEAT & F_MASK) mb4 = mask4<F16>(mrow, key0, Sk);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * g4 + e;
+            float x = sacc[tt][r] * c + mb4[e];
+            if (need_mask) {
+              const int key = key0 + e;
+              const bool ok = (key < Sk) & (!CAUSAL | (key <= qpos + coff));
+              x = ok ? x : -INFINITY;
+            }
+            sacc[tt][r] = x;
+            mx = fmaxf(mx, x);
+          }
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_i, mx);
+      const float msub = m_new == -INFINITY ? 0.f : m_new;
+      float rs = 0.f;
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = fast_exp2(sacc[tt][r] - msub);
+          sacc[tt][r] = p;
+          rs += p;
+        }
+      rs += __shfl_xor(rs, 32, 64);
+      if (FEAT & F_DROP) {  // O accumulates P∘M; the normaliser l keeps the undropped sum
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            const int key = n0 + tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            const uint32_t h = drop_hash(dk, lbase + qpos, sk_half, key);
+            if (!drop_keep(dk, h, key)) sacc[tt][r] = 0.f;
+            if (!drop_keep(dk, h, key + 1)) sacc[tt][r + 1] = 0.f;
+          }
+      }
+      // rescale only when some row's running max moved (T13-style skip of an O-wide pass)
+      if (__any(m_new > m_i)) {
+        const float alpha = fast_exp2(m_i - msub);
+        l_i *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+          for (int j = 0; j < 16; ++j) oacc[dt][j] *= alpha;
+      }
+      l_i += rs;
+      m_i = m_new;
+      V8 pf[4];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) pf[2 * tt + s] = E::frag(sacc[tt], s);
+      // Oᵀ += Vᵀ · Pᵀ
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const int c0 = 32 * dt + 16 * (g & 1);
+#pragma unroll
+        for (int ks4 = 0; ks4 < 4; ++ks4) {
+          const int r0 = 16 * ks4 + 4 * hh;
+          s16x4_t lo = lds_tr4<ROWB>(vs, r0, c0, gi);
+          s16x4_t hi = lds_tr4<ROWB>(vs, r0 + 8, c0, gi);
+          oacc[dt] = E::mfma(cat44<F16>(lo, hi), pf[ks4], oacc[dt]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // epilogue: lane = query row, registers = d
+  if (qpos < Sq) {
+    float inv = l_i > 0.f ? 1.f / l_i : 0.f;
+    if (FEAT & F_DROP) inv *= dk.inv;
+    unsigned short* op = o + b * a.sob + (long long)qpos * a.sos + hq * a.soh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = 32 * dt + 8 * g4 + 4 * hh;
+        uint2 pk;
+        pk.x = pack2<F16>(oacc[dt][4 * g4 + 0] * inv, oacc[dt][4 * g4 + 1] * inv);
+        pk.y = pack2<F16>(oacc[dt][4 * g4 + 2] * inv, oacc[dt][4 * g4 + 3] * inv);
+        *reinterpret_cast<uint2*>(op + d0) = pk;
+      }
+    if (hh == 0 && a.lse)
+      a.lse[lbase + qpos] = l_i > 0.f ? (m_i + log2f(l_i)) * kLn2 : INFINITY;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Backward pre-pass: delta[row] = Σ_d dO·O (f32). 16 B per lane, DP/8 lanes per row.
+// ------------------------------------------------------------------------------------------
+template <int D, bool F16>
+__global__ __launch_bounds__(256) void bwd_pre_kernel(const unsigned short* __restrict__ o,
+                                                      const unsigned short* __restrict__ dout,
+                                                      float* __restrict__ delta, int Sq, int Hq,
+                                                      long long sob, long long sos, long long soh,
+                                                      int total) {
+  constexpr int TPR = D > 64 ? 16 : 8;  // threads per row (power of two)
+  const int row = (blockIdx.x * 256 + threadIdx.x) / TPR, sub = threadIdx.x % TPR;
+  const bool ok = row < total;
+  const int rr = ok ? row : 0;
+  const int qr = rr % Sq, hq = (rr / Sq) % Hq, b = rr / (Sq * Hq);
+  const int sc = sub < D / 8 ? sub : 0;
+  const long long off = b * sob + (long long)qr * sos + hq * soh + sc * 8;
+  u16x8 x = *reinterpret_cast<const u16x8*>(o + off);
+  u16x8 d = *reinterpret_cast<const u16x8*>(dout + off);
+  float s = 0.f;
+  if (sub < D / 8)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += ET<F16>::tof(x[j]) * ET<F16>::tof(d[j]);
+#pragma unroll
+  for (int m = TPR / 2; m > 0; m >>= 1) s += __shfl_xor(s, m, 64);
+  if (ok && sub == 0) delta[((long long)b * Hq + hq) * Sq + qr] = s;
+}
+
+// ------------------------------------------------------------------------------------------
+// Backward dK/dV: workgroup = 128 keys of one (batch, kv-head); sweeps the q-heads of the GQA
+// group and all query tiles of 64 rows. Key on the MFMA lane.
+// ------------------------------------------------------------------------------------------
+template <int D, bool F16, bool CAUSAL, int FEAT>
+__global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(FaArgs a) {
+  typedef ET<F16> E;
+  typedef typename E::V8 V8;
+  constexpr int DP = D > 64 ? 128 : 64;
+  constexpr int BK = 128, BQ = 64;
+  constexpr int KSTEPS = D / 16;
+  constexpr int DT = D / 32;
+  constexpr int ROWB = DP * 2;
+  constexpr int QTILE_B = BQ * ROWB;    // Q or dO tile [64][DP]
+  constexpr int KIMG_B = BK * ROWB;     // resident K and V images of the block's 128 keys
+  constexpr int OFF_K = 2 * 2 * QTILE_B;
+  constexpr int OFF_V = OFF_K + KIMG_B;
+  constexpr int OFF_STAT = OFF_V + KIMG_B;  // 2 buffers x (lse, delta) x 64 f32
+  constexpr int SMEM = OFF_STAT + 2 * 2 * BQ * 4;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const unsigned short* q = (const unsigned short*)a.q;
+  const unsigned short* k = (const unsigned short*)a.k;
+  const unsigned short* v = (const unsigned short*)a.v;
+  const unsigned short* dout = (const unsigned short*)a.dout;
+  unsigned short* dk = (unsigned short*)a.dk;
+  unsigned short* dv = (unsigned short*)a.dv;
+  const float* lse = a.lse;
+  const float* delta = a.delta;
+  const int B = a.B, SqMax = a.Sq, Hq = a.Hq, Hk = a.Hk;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int HB = Hk * B;
+  const int kb = (int)blockIdx.x / HB;  // causal: low key blocks see the most queries -> first
+  const int hk = (int)blockIdx.x % Hk, b = ((int)blockIdx.x % HB) / Hk;
+  const int n0 = kb * BK;
+  int Sq = SqMax, Sk = a.Sk;
+  long long lrow = (long long)b * Hq * SqMax, lhead = SqMax;  // stats index = lrow + hq*lhead + q
+  if (a.cu_q) {
+    const int q0s = a.cu_q[b], k0s = a.cu_k[b];
+    Sq = a.cu_q[b + 1] - q0s;
+    Sk = a.cu_k[b + 1] - k0s;
+    if (n0 >= Sk) return;
+    q += (long long)q0s * a.sqs;
+    dout += (long long)q0s * a.sos;
+    k += (long long)k0s * a.sks;
+    v += (long long)k0s * a.svs;
+    dk += (long long)k0s * a.sks;
+    dv += (long long)k0s * a.svs;
+    lrow = q0s;
+    lhead = a.ltot;
+  }
+  const int kw0 = n0 + 32 * w;  // this wave's first key
+  const int key = kw0 + l32;
+  const int coff = Sk - Sq;
+  const int group = Hq / Hk;
+  const float c = a.scale * kLog2e;
+  DropKey drk;
+  if (FEAT & F_DROP) drk = drop_key(a.p_drop, a.seed, a.offset);
+  const int sk_half = (a.Sk + 1) >> 1;
+  const int keyc = min(key, Sk - 1);
+
+  // K / V of the block's keys stay resident in LDS (B operands of S and dP are row reads)
+  glds_tile<BK, ROWB, D / 8>(k + b * a.skb + hk * a.skh, a.sks, n0, Sk - 1, smem + OFF_K, w, lane);
+  glds_tile<BK, ROWB, D / 8>(v + b * a.svb + hk * a.svh, a.svs, n0, Sk - 1, smem + OFF_V, w, lane);
+  const char* kimg = smem + OFF_K;
+  const char* vimg = smem + OFF_V;
+
+  f32x16 dkacc[DT], dvacc[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) { dkacc[i][j] = 0.f; dvacc[i][j] = 0.f; }
+
+  const int q_start = CAUSAL ? max(0, n0 - coff) : 0;
+  const int qt0 = q_start / BQ;
+  const int nqt = (Sq + BQ - 1) / BQ;
+  const int tiles_per_head = nqt - qt0;
+  const int total = (n0 < Sk && tiles_per_head > 0) ? tiles_per_head * group : 0;
+
+  auto issue = [&](int it, int buf) {
+    const int hq = hk * group + it / tiles_per_head;
+    const int q0 = (qt0 + it % tiles_per_head) * BQ;
+    char* qs = smem + buf * 2 * QTILE_B;
+    glds_tile<BQ, ROWB, D / 8>(q + b * a.sqb + hq * a.sqh, a.sqs, q0, Sq - 1, qs, w, lane);
+    glds_tile<BQ, ROWB, D / 8>(dout + b * a.sob + hq * a.soh, a.sos, q0, Sq - 1, qs + QTILE_B, w, lane);
+    if (w < 2) {  // wave 0: lse row, wave 1: delta row (64 f32 = one 4-B/lane DMA)
+      const float* s = (w == 0 ? lse : delta) + lrow + hq * lhead + min(q0 + lane, Sq - 1);
+      char* st = smem + OFF_STAT + (buf * 2 + w) * BQ * 4;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)s,
+                                       (__attribute__((address_space(3))) void*)st, 4, 0, 0);
+    }
+  };
+  if (total > 0) issue(0, 0);
+  __syncthreads();
+
+  for (int it = 0; it < total; ++it) {
+    const int buf = it & 1;
+    const int hq = hk * group + it / tiles_per_head;
+    const int q0 = (qt0 + it % tiles_per_head) * BQ;
+    if (it + 1 < total) issue(it + 1, buf ^ 1);
+    const char* qs = smem + buf * 2 * QTILE_B;
+    const char* dos = qs + QTILE_B;
+    const float* lst = reinterpret_cast<const float*>(smem + OFF_STAT) + buf * 2 * BQ;
+    const float* dst = lst + BQ;
+    // Re-derive every lane-dependent LDS address inside the iteration (an opaque copy of the lane
+    // id): otherwise hipcc hoists ~60 loop-invariant swizzled addresses into VGPRs and evicts the
+    // accumulators to AGPRs with per-iteration copies.
+    int lx = lane;
+    asm volatile("" : "+v"(lx));
+    const int l32 = lx & 31, hh = lx >> 5, gi = lx & 15, g = lx >> 4;
+    {
+      f32x16 sacc[2], pacc[2];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) { sacc[qt][j] = 0.f; pacc[qt][j] = 0.f; }
+      // S = Q·Kᵀ, dP = dO·Vᵀ with the next k-step's 6 fragments loaded one step ahead
+      V8 fr[2][6];
+      auto ld = [&](int kk, V8* f) {
+        const int koff = lds_off<ROWB>(32 * w + l32, 2 * kk + hh);
+        f[0] = lds_row8<F16>(kimg, koff);
+        f[1] = lds_row8<F16>(vimg, koff);
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+          const int qoff = lds_off<ROWB>(qt * 32 + l32, 2 * kk + hh);
+          f[2 + qt] = lds_row8<F16>(qs, qoff);
+          f[4 + qt] = lds_row8<F16>(dos, qoff);
+        }
+      };
+      ld(0, fr[0]);
+#pragma unroll
+      for (int kk = 0; kk < KSTEPS; ++kk) {
+        if (kk + 1 < KSTEPS) ld(kk + 1, fr[(kk + 1) & 1]);
+        const V8* f = fr[kk & 1];
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+          sacc[qt] = E::mfma(f[2 + qt], f[0], sacc[qt]);
+          pacc[qt] = E::mfma(f[4 + qt], f[1], pacc[qt]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      const bool need_mask = (kw0 + 31 >= Sk) || (q0 + BQ > Sq) ||
+                             (CAUSAL && kw0 + 31 > q0 + coff);
+      const unsigned short* mbase = nullptr;
+      if (FEAT & F_MASK) mbase = (const unsigned short*)a.mask + b * a.smb + hq * a.smh + keyc;
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int qi0 = qt * 32 + 8 * g4 + 4 * hh;
+          const f32x4 l4 = *reinterpret_cast<const f32x4*>(lst + qi0);
+          const f32x4 d4 = *reinterpret_cast<const f32x4*>(dst + qi0);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * g4 + e;
+            const int qr = q0 + qi0 + e;
+            float x = sacc[qt][r] * c - l4[e] * kLog2e;
+            if (FEAT & F_MASK)
+              x += E::tof(mbase[(long long)min(qr, Sq - 1) * a.smq]) * kLog2e;
+            float p = fast_exp2(x);
+            if (need_mask) {
+              const bool ok = (key < Sk) & (qr < Sq) & (!CAUSAL | (key <= qr + coff));
+              p = ok ? p : 0.f;
+            }
+            float dpv = pacc[qt][r];
+            float pd = p;
+            if (FEAT & F_DROP) {
+              const bool kp = drop_keep(drk, drop_hash(drk, lrow + hq * lhead + qr, sk_half, key), key);
+              pd = kp ? p : 0.f;
+              dpv = kp ? dpv * drk.inv : 0.f;
+            }
+            sacc[qt][r] = pd;
+            pacc[qt][r] = p * (dpv - d4[e]);
+          }
+        }
+      // dVᵀ += dOᵀ·(P∘M) ; dKᵀ += Qᵀ·dS   (A operands via transposed reads of the dO / Q images)
+      V8 pb[4], db[4];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          pb[2 * qt + s] = E::frag(sacc[qt], s);
+          db[2 * qt + s] = E::frag(pacc[qt], s);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+      V8 tf[2][4];
+      auto ldt = [&](int st, V8* f) {  // st = 2*dt + half: ks in {2*half, 2*half+1}
+        const int c0 = 32 * (st >> 1) + 16 * (g & 1);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int r0 = 16 * (2 * (st & 1) + j) + 4 * hh;
+          f[2 * j] = cat44<F16>(lds_tr4<ROWB>(dos, r0, c0, gi), lds_tr4<ROWB>(dos, r0 + 8, c0, gi));
+          f[2 * j + 1] = cat44<F16>(lds_tr4<ROWB>(qs, r0, c0, gi), lds_tr4<ROWB>(qs, r0 + 8, c0, gi));
+        }
+      };
+      ldt(0, tf[0]);
+#pragma unroll
+      for (int st = 0; st < 2 * DT; ++st) {
+        if (st + 1 < 2 * DT) ldt(st + 1, tf[(st + 1) & 1]);
+        const V8* f = tf[st & 1];
+        const int dt = st >> 1;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int ks = 2 * (st & 1) + j;
+          dvacc[dt] = E::mfma(f[2 * j], pb[ks], dvacc[dt]);
+          dkacc[dt] = E::mfma(f[2 * j + 1], db[ks], dkacc[dt]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    __syncthreads();
+  }
+
+  if (key < Sk) {
+    const float vs = (FEAT & F_DROP) ? drk.inv : 1.f;
+    unsigned short* dkp = dk + b * a.skb + (long long)key * a.sks + hk * a.skh;
+    unsigned short* dvp = dv + b * a.svb + (long long)key * a.svs + hk * a.svh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = 32 * dt + 8 * g4 + 4 * hh;
+        uint2 pk;
+        pk.x = pack2<F16>(dkacc[dt][4 * g4 + 0] * a.scale, dkacc[dt][4 * g4 + 1] * a.scale);
+        pk.y = pack2<F16>(dkacc[dt][4 * g4 + 2] * a.scale, dkacc[dt][4 * g4 + 3] * a.scale);
+        *reinterpret_cast<uint2*>(dkp + d0) = pk;
+        pk.x = pack2<F16>(dvacc[dt][4 * g4 + 0] * vs, dvacc[dt][4 * g4 + 1] * vs);
+        pk.y = pack2<F16>(dvacc[dt][4 * g4 + 2] * vs, dvacc[dt][4 * g4 + 3] * vs);
+        *reinterpret_cast<uint2*>(dvp + d0) = pk;
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Backward dQ: the forward's structure (query row on the lane).
+// ------------------------------------------------------------------------------------------
+template <int D, bool F16, bool CAUSAL, int FEAT>
+__global__ __launch_bounds__(256, 2) void bwd_dq_kernel(FaArgs a) {
+  typedef ET<F16> E;
+  typedef typename E::V8 V8;
+  constexpr int DP = D > 64 ? 128 : 64;
+  constexpr int BM = 128, BN = 64;
+  constexpr int KSTEPS = D / 16;
+  constexpr int DT = D / 32;
+  constexpr int ROWB = DP * 2;
+  constexpr int TILE_B = BN * ROWB;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_B];
+
+  const unsigned short* q = (const unsigned short*)a.q;
+  const unsigned short* k = (const unsigned short*)a.k;
+  const unsigned short* v = (const unsigned short*)a.v;
+  const unsigned short* dout = (const unsigned short*)a.dout;
+  unsigned short* dq = (unsigned short*)a.dq;
+  const int B = a.B, SqMax = a.Sq, Hq = a.Hq, Hk = a.Hk;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5, gi = lane & 15, g = lane >> 4;
+  const int nmb = (SqMax + BM - 1) / BM;
+  const int HB = Hq * B;
+  const int mb = CAUSAL ? (nmb - 1 - (int)blockIdx.x / HB) : (int)blockIdx.x / HB;
+  const int hq = (int)blockIdx.x % Hq, b = ((int)blockIdx.x % HB) / Hq;
+  const int hk = hq / (Hq / Hk);
+  const int m0 = mb * BM;
+  int Sq = SqMax, Sk = a.Sk;
+  long long lbase = ((long long)b * Hq + hq) * SqMax;
+  if (a.cu_q) {
+    const int q0s = a.cu_q[b], k0s = a.cu_k[b];
+    Sq = a.cu_q[b + 1] - q0s;
+    Sk = a.cu_k[b + 1] - k0s;
+    if (m0 >= Sq) return;
+    q += (long long)q0s * a.sqs;
+    dq += (long long)q0s * a.sqs;
+    dout += (long long)q0s * a.sos;
+    k += (long long)k0s * a.sks;
+    v += (long long)k0s * a.svs;
+    lbase = (long long)hq * a.ltot + q0s;
+  }
+  const int qrow0 = m0 + w * 32;
+  const int qpos = qrow0 + l32;
+  const int coff = Sk - Sq;
+  const float c = a.scale * kLog2e;
+
+  const unsigned short* kbase = k + b * a.skb + hk * a.skh;
+  const unsigned short* vbase = v + b * a.svb + hk * a.svh;
+  const unsigned short* mrow = nullptr;
+  if (FEAT & F_MASK)
+    mrow = (const unsigned short*)a.mask + b * a.smb + hq * a.smh + (long long)min(qpos, Sq - 1) * a.smq;
+  DropKey drk;
+  if (FEAT & F_DROP) drk = drop_key(a.p_drop, a.seed, a.offset);
+  const int sk_half = (a.Sk + 1) >> 1;
+
+  V8 qf[KSTEPS], df[KSTEPS];
+  float lse2, dlt;
+  {
+    const long long qr = min(qpos, Sq - 1);
+    const unsigned short* qp = q + b * a.sqb + qr * a.sqs + hq * a.sqh + 8 * hh;
+    const unsigned short* dp = dout + b * a.sob + qr * a.sos + hq * a.soh + 8 * hh;
+#pragma unroll
+    for (int kk = 0; kk < KSTEPS; ++kk) {
+      qf[kk] = *reinterpret_cast<const V8*>(qp + 16 * kk);
+      df[kk] = *reinterpret_cast<const V8*>(dp + 16 * kk);
+    }
+    const long long si = lbase + qr;
+    lse2 = a.lse[si] * kLog2e;
+    dlt = a.delta[si];
+  }
+
+  int n_end = Sk;
+  if (CAUSAL) n_end = min(Sk, m0 + BM + coff);
+  const int ntiles = n_end <= 0 ? 0 : (n_end + BN - 1) / BN;
+
+  f32x16 qacc[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) qacc[i][j] = 0.f;
+
+  auto issue = [&](int t, int buf) {
+    char* ks = smem + buf * 2 * TILE_B;
+    glds_tile<BN, ROWB, D / 8>(kbase, a.sks, t * BN, Sk - 1, ks, w, lane);
+    glds_tile<BN, ROWB, D / 8>(vbase, a.svs, t * BN, Sk - 1, ks + TILE_B, w, lane);
+  };
+  if (ntiles > 0) issue(0, 0);
+  __syncthreads();
+
+  const bool wave_rows_valid = qrow0 < Sq;
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) issue(t + 1, buf ^ 1);
+    const int n0 = t * BN;
+    const bool active = wave_rows_valid && (!CAUSAL || n0 <= qrow0 + 31 + coff);
+    if (active) {
+      const char* ks = smem + buf * 2 * TILE_B;
+      const char* vs = ks + TILE_B;
+      f32x16 sacc[2], pacc[2];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) { sacc[tt][j] = 0.f; pacc[tt][j] = 0.f; }
+#pragma unroll
+      for (int kk = 0; kk < KSTEPS; ++kk) {
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+          const int off = lds_off<ROWB>(tt * 32 + l32, 2 * kk + hh);
+          sacc[tt] = E::mfma(lds_row8<F16>(ks, off), qf[kk], sacc[tt]);
+          pacc[tt] = E::mfma(lds_row8<F16>(vs, off), df[kk], pacc[tt]);
+        }
+      }
+      const bool need_mask = (n0 + BN > Sk) || (CAUSAL && n0 + BN - 1 > qrow0 + coff);
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int key0 = n0 + tt * 32 + 8 * g4 + 4 * hh;
+          f32x4 mb4 = {0.f, 0.f, 0.f, 0.f};
+          if (FEAT & F_MASK) mb4 = mask4<F16>(mrow, key0, Sk);
+          uint32_t h = 0, h2 = 0;
+          if (FEAT & F_DROP) {
+            h = drop_hash(drk, lbase + qpos, sk_half, key0);
+            h2 = drop_hash(drk, lbase + qpos, sk_half, key0 + 2);
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * g4 + e;
+            const int key = key0 + e;
+            float p = fast_exp2(sacc[tt][r] * c + mb4[e] - lse2);
+            if (need_mask) {
+              const bool ok = (key < Sk) & (!CAUSAL | (key <= qpos + coff));
+              p = ok ? p : 0.f;
+            }
+            float dpv = pacc[tt][r];
+            if (FEAT & F_DROP) dpv = drop_keep(drk, e < 2 ? h : h2, key) ? dpv * drk.inv : 0.f;
+            pacc[tt][r] = p * (dpv - dlt);
+          }
+        }
+      V8 dsf[4];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) dsf[2 * tt + s] = E::frag(pacc[tt], s);
+      // dQᵀ += Kᵀ · dSᵀ
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const int c0 = 32 * dt + 16 * (g & 1);
+#pragma unroll
+        for (int ks4 = 0; ks4 < 4; ++ks4) {
+          const int r0 = 16 * ks4 + 4 * hh;
+          s16x4_t lo = lds_tr4<ROWB>(ks, r0, c0, gi);
+          s16x4_t hi = lds_tr4<ROWB>(ks, r0 + 8, c0, gi);
+          qacc[dt] = E::mfma(cat44<F16>(lo, hi), dsf[ks4], qacc[dt]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  if (qpos < Sq) {
+    unsigned short* qp = dq + b * a.sqb + (long long)qpos * a.sqs + hq * a.sqh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = 32 * dt + 8 * g4 + 4 * hh;
+        uint2 pk;
+        pk.x = pack2<F16>(qacc[dt][4 * g4 + 0] * a.scale, qacc[dt][4 * g4 + 1] * a.scale);
+        pk.y = pack2<F16>(qacc[dt][4 * g4 + 2] * a.scale, qacc[dt][4 * g4 + 3] * a.scale);
+        *reinterpret_cast<uint2*>(qp + d0) = pk;
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Launchers (one per element type; the exported entry points in flash_attn.hip dispatch).
+// ------------------------------------------------------------------------------------------
+template <bool F16, int D, bool C>
+int launch_fwd_feat(const FaArgs& a, dim3 grid, hipStream_t st) {
+  const int feat = (a.p_drop > 0.f ? F_DROP : 0) | (a.mask ? F_MASK : 0);
+  switch (feat) {
+    case 0: hipLaunchKernelGGL((fwd_kernel<D, F16, C, 0>), grid, dim3(256), 0, st, a); break;
+    case 1: hipLaunchKernelGGL((fwd_kernel<D, F16, C, 1>), grid, dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((fwd_kernel<D, F16, C, 2>), grid, dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL((fwd_kernel<D, F16, C, 3>), grid, dim3(256), 0, st, a); break;
+  }
+  return (int)hipGetLastError();
+}
+
+template <bool F16>
+int launch_fwd(const FaArgs& a, hipStream_t st) {
+  dim3 grid(((a.Sq + 127) / 128) * a.Hq * a.B);
+#define FWD_D(DD) return a.causal ? launch_fwd_feat<F16, DD, true>(a, grid, st) \
+                                  : launch_fwd_feat<F16, DD, false>(a, grid, st)
+  switch (a.D) {
+    case 64: FWD_D(64);
+    case 96: FWD_D(96);
+    case 128: FWD_D(128);
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef FWD_D
+}
+
+template <bool F16, int D, bool C>
+int launch_bwd_feat(const FaArgs& a, dim3 gkv, dim3 gq, hipStream_t st) {
+  const int feat = (a.p_drop > 0.f ? F_DROP : 0) | (a.mask ? F_MASK : 0);
+#define BWD_F(FF)                                                                              \
+  hipLaunchKernelGGL((bwd_dkdv_kernel<D, F16, C, FF>), gkv, dim3(256), 0, st, a);              \
+  hipLaunchKernelGGL((bwd_dq_kernel<D, F16, C, FF>), gq, dim3(256), 0, st, a);                 \
+  break;
+  switch (feat) {
+    case 0: BWD_F(0)
+    case 1: BWD_F(1)
+    case 2: BWD_F(2)
+    default: BWD_F(3)
+  }
+#undef BWD_F
+  return (int)hipGetLastError();
+}
+
+template <bool F16>
+int launch_bwd(const FaArgs& a, hipStream_t st) {
+  // delta rows: padded [B, Hq, Sq]; packed [Hq, ltot] == the padded layout with B = 1, Sq = ltot
+  const int pB = a.cu_q ? 1 : a.B, pS = a.cu_q ? a.ltot : a.Sq;
+  const int total = pB * a.Hq * pS;
+  const int tpr = a.D > 64 ? 16 : 8;
+  const int pre_blocks = (int)(((long long)total * tpr + 255) / 256);
+  dim3 gkv(((a.Sk + 127) / 128) * a.Hk * a.B), gq(((a.Sq + 127) / 128) * a.Hq * a.B);
+#define BWD_D(DD)                                                                                  \
+  hipLaunchKernelGGL((bwd_pre_kernel<DD, F16>), dim3(pre_blocks), dim3(256), 0, st,              \
+                     (const unsigned short*)a.o, (const unsigned short*)a.dout, a.delta, pS, a.Hq, \
+                     a.sob, a.sos, a.soh, total);                                                 \
+  return a.causal ? launch_bwd_feat<F16, DD, true>(a, gkv, gq, st)                               \
+                  : launch_bwd_feat<F16, DD, false>(a, gkv, gq, st)
+  switch (a.D) {
+    case 64: BWD_D(64);
+    case 96: BWD_D(96);
+    case 128: BWD_D(128);
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef BWD_D
+}
+
+}  // namespace fa

@@ -58,13 +58,24 @@ def _mm(x, w, bias=None, transpose=False):
 
 def attention_core(qkv, num_heads, num_kv_heads=None, attn_mask=None, causal=False,
                    attn_dropout=0.0, training=False, mode="upscale_in_train", scale=None):
-    """qkv: [B, S, Hq+2Hk, D] → [B, S, Hq*D]. Flash path when there is no explicit mask and
-    no attention dropout; otherwise GEMM + fused masked softmax (``elementwise.hip``)."""
+    """qkv: [B, S, Hq+2Hk, D] → [B, S, Hq*D]. Flash kernel (with in-kernel mask add and attention
+    dropout) whenever dropout is upscale_in_train; the downscale_in_infer dropout convention takes
+    GEMM + fused masked softmax (``elementwise.hip``)."""
     B, S, _, D = qkv.shape
     hq, hk = num_heads, num_kv_heads or num_heads
     scale = 1.0 / math.sqrt(D) if scale is None else scale
-    if attn_mask is None and (attn_dropout == 0.0 or not training):
-        o = ops.flash_attention_packed(qkv, hq, hk, causal=causal, scale=scale)
+    drop = attn_dropout if training else 0.0
+    if attn_mask is None and (drop == 0.0 or mode == "upscale_in_train"):
+        o = ops.flash_attention_packed(qkv, hq, hk, causal=causal, scale=scale, dropout_p=drop,
+                                       training=training)
+        return o.reshape(B, S, hq * D)
+    if drop == 0.0 or mode == "upscale_in_train":
+        q = qkv[:, :, :hq]
+        k = qkv[:, :, hq:hq + hk]
+        v = qkv[:, :, hq + hk:]
+        m = _to_additive_mask(attn_mask, qkv.dtype)
+        o = ops.flash_attention(q, k, v, causal, scale, attn_mask=m, dropout_p=drop,
+                                training=training)
         return o.reshape(B, S, hq * D)
     q = qkv[:, :, :hq].transpose(1, 2)
     k = qkv[:, :, hq:hq + hk].transpose(1, 2)
@@ -542,9 +553,9 @@ def variable_length_memory_efficient_attention(query, key, value, seq_lens, kv_s
     Sk = key.shape[2]
     lq = seq_lens.reshape(-1).to(torch.long)
     lk = kv_seq_lens.reshape(-1).to(torch.long)
-    out = torch.zeros_like(query)
+    dev = query.device
     if mask is None:
-        dev = query.device
+        out = torch.zeros_like(query)
         ar_q = torch.arange(S, device=dev)
         ar_k = torch.arange(Sk, device=dev)
         vq = (ar_q[None, :] < lq.to(dev)[:, None]).reshape(-1)
@@ -562,16 +573,24 @@ def variable_length_memory_efficient_attention(query, key, value, seq_lens, kv_s
         flat = out.transpose(1, 2).reshape(B * S, H, D).clone()
         flat.index_copy_(0, iq, o.to(flat.dtype))
         return flat.view(B, S, H, D).transpose(1, 2).contiguous()
-    for b in range(B):
-        sq, sk = int(lq[b]), int(lk[b])
-        if sq == 0:
-            continue
-        q = query[b:b + 1, :, :sq].transpose(1, 2)
-        k = key[b:b + 1, :, :sk].transpose(1, 2)
-        v = value[b:b + 1, :, :sk].transpose(1, 2)
-        o = ops.attention_reference(q, k, v, causal, scale, mask[b:b + 1, :, :sq, :sk])
-        out[b, :, :sq] = o.transpose(1, 2)
-    return out
+    # Masked: ONE padded flash launch, no host sync. Key-length limits and the per-sequence
+    # (bottom-right aligned) causal band are folded into the additive mask on the device; rows
+    # past a sequence's length are zeroed.
+    lqd, lkd = lq.to(dev), lk.to(dev)
+    ar_q = torch.arange(S, device=dev)[None, :, None]
+    ar_k = torch.arange(Sk, device=dev)[None, None, :]
+    allow = ar_k < lkd[:, None, None]
+    if causal:
+        allow = allow & (ar_k <= ar_q + (lkd - lqd)[:, None, None])
+    m = mask.to(query.dtype)
+    if m.dim() == 3:
+        m = m.unsqueeze(1)
+    m = m.masked_fill(~allow[:, None], float("-inf"))
+    o = ops.flash_attention(query.transpose(1, 2), key.transpose(1, 2), value.transpose(1, 2),
+                            False, scale, attn_mask=m)
+    o = o.transpose(1, 2)
+    rows = (torch.arange(S, device=dev)[None, :] < lqd[:, None])[:, None, :, None]
+    return torch.where(rows, o, torch.zeros((), device=dev, dtype=o.dtype)).contiguous()
 
 
 def softmax_mask_fuse(x, mask, name=None):

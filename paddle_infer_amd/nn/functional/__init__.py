@@ -442,37 +442,33 @@ def square_error_cost(input, label):  # noqa: A002
 def flash_attention(query, key, value, dropout=0.0, causal=False, return_softmax=False,
                     fixed_seed_offset=None, rng_name="", training=True, name=None):
     """Reference `nn/functional/flash_attention.py:142` — [B, S, H, D] layout. Returns
-    ``(out, softmax)`` (softmax is None: never materialised)."""
-    if dropout > 0.0 and training:
-        raise NotImplementedError("attention dropout is not implemented in the MFMA kernel")
-    return _ops.flash_attention(query, key, value, causal=causal), None
+    ``(out, softmax)`` (softmax is None: never materialised). Attention dropout runs inside the
+    MFMA kernel (counter-RNG mask regenerated in backward)."""
+    return _ops.flash_attention(query, key, value, causal=causal, dropout_p=dropout,
+                                training=training), None
 
 
 def flash_attn_unpadded(query, key, value, cu_seqlens_q, cu_seqlens_k, max_seqlen_q, max_seqlen_k,
                         scale, dropout=0.0, causal=False, return_softmax=False, training=True, name=None):
     """Reference `flash_attention.py:flash_attn_unpadded`: packed [total_tokens, H, D] q/k/v with
     cumulative sequence offsets — one variable-length MFMA launch per pass (``flash_attn.hip``)."""
-    if dropout > 0.0 and training:
-        raise NotImplementedError("attention dropout is not implemented in the MFMA kernel")
     return _ops.flash_attention_varlen(query, key, value, cu_seqlens_q, cu_seqlens_k, max_seqlen_q,
-                                       max_seqlen_k, causal=causal, scale=scale), None
+                                       max_seqlen_k, causal=causal, scale=scale, dropout_p=dropout,
+                                       training=training), None
 
 
 def scaled_dot_product_attention(query, key, value, attn_mask=None, dropout_p=0.0,
                                  is_causal=False, training=True, name=None):
-    """Reference `flash_attention.py:440`: [B, S, H, D] layout."""
-    if attn_mask is None and dropout_p == 0.0:
-        return _ops.flash_attention(query, key, value, causal=is_causal)
-    q, k, v = (t.transpose(1, 2) for t in (query, key, value))
-    o = TF.scaled_dot_product_attention(q, k, v, attn_mask, dropout_p if training else 0.0, is_causal)
-    return o.transpose(1, 2)
+    """Reference `flash_attention.py:440`: [B, S, H, D] layout; additive / bool ``attn_mask`` and
+    attention dropout both run inside the MFMA flash kernel."""
+    return _ops.flash_attention(query, key, value, causal=is_causal, attn_mask=attn_mask,
+                                dropout_p=dropout_p, training=training)
 
 
 def memory_efficient_attention(query, key, value, attn_bias=None, p=0.0, scale=None, training=True):
     """The fork's `memory_efficient_attention` (cutlass) API: [B, S, H, D]."""
-    if attn_bias is None and p == 0.0:
-        return _ops.flash_attention(query, key, value, scale=scale)
-    return scaled_dot_product_attention(query, key, value, attn_bias, p, training=training)
+    return _ops.flash_attention(query, key, value, scale=scale, attn_mask=attn_bias, dropout_p=p,
+                                training=training)
 
 
 def sequence_mask(x, maxlen=None, dtype="int64", name=None):

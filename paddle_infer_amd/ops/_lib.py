@@ -56,14 +56,6 @@ _SIGS = {
                           c_void_p],
     "piamd_softmax_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p],
     "piamd_dropout": [c_void_p, c_void_p, c_ll, c_float, c_u64, c_u64, c_void_p],
-    "piamd_flash_attn_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
-                             c_int, c_int, c_int, c_int, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll,
-                             c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_float, c_int, c_void_p],
-    "piamd_flash_attn_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                             c_int, c_int, c_int, c_int, c_int, c_int,
-                             c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll, c_ll,
-                             c_ll, c_ll, c_ll, c_float, c_int, c_void_p],
     "piamd_qkv_prep": [c_void_p, c_ll, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                        c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p],
     # qkv, ldq, bias, prep, rot, neox, base, kc, vc, lens, B, Hq, Hk, D, maxS, chunk, nsplit,
@@ -82,6 +74,21 @@ _SIGS = {
 
 
 _RESTYPES = {"piamd_layernorm_bwd_ws": ctypes.c_longlong}
+
+
+class FaArgs(ctypes.Structure):
+    """Mirror of ``struct FaArgs`` (csrc/kernels/flash_attn.h)."""
+    _fields_ = ([(n, c_void_p) for n in ("q", "k", "v", "o", "lse", "dout", "delta", "dq", "dk", "dv",
+                                        "mask", "cu_q", "cu_k")]
+                + [(n, c_int) for n in ("B", "Sq", "Sk", "Hq", "Hk", "D", "ltot", "causal")]
+                + [(n, c_ll) for n in ("sqb", "sqs", "sqh", "skb", "sks", "skh", "svb", "svs", "svh",
+                                       "sob", "sos", "soh", "smb", "smh", "smq")]
+                + [("scale", ctypes.c_float), ("p_drop", ctypes.c_float), ("seed", c_u64),
+                   ("offset", c_u64)])
+
+
+_SIGS["piamd_fa_fwd"] = [ctypes.POINTER(FaArgs), c_int, c_void_p]
+_SIGS["piamd_fa_bwd"] = [ctypes.POINTER(FaArgs), c_int, c_void_p]
 _SIGS["piamd_layernorm_bwd_ws"] = [c_int, c_int]
 
 
@@ -207,10 +214,6 @@ _SIGS["piamd_embedding_bwd"] = [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c
                                 c_int, c_int, c_void_p]
 _SIGS["piamd_pos_embedding_bwd"] = [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                                     c_void_p]
-_SIGS["piamd_flash_attn_varlen_fwd"] = (_SIGS["piamd_flash_attn_fwd"][:-1]
-                                        + [c_void_p, c_void_p, c_int, c_void_p])
-_SIGS["piamd_flash_attn_varlen_bwd"] = ([c_void_p] * 10 + [c_int] * 6 + [c_ll] * 12
-                                        + [c_float, c_int, c_void_p, c_void_p, c_int, c_void_p])
 # logits, bf16, cum, seq_lens, stop, end_ids, step_ids, last_cache, last_offs, bs, beam, V,
 # max_seq_len, max_dec_len, fuse, early, penalty, P, part, ids, cum_out, cache, offs, parent,
 # stop_out, sl_out, st_out, stream

@@ -29,21 +29,35 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="8,1024,16,128;4,2048,16,128;2,4096,16,128;8,1024,32,64")
     ap.add_argument("--causal", type=int, default=1)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
+    ap.add_argument("--dropout", type=float, default=0.0)
+    ap.add_argument("--mask", type=int, default=0, help="additive [1, 1, S, S] mask")
+    ap.add_argument("--no-sdpa", action="store_true")
     args = ap.parse_args()
+    dt = torch.bfloat16 if args.dtype == "bf16" else torch.float16
     out = []
     for s in args.shapes.split(";"):
         B, S, H, D = map(int, s.split(","))
-        q = torch.randn(B, S, H, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+        q = torch.randn(B, S, H, D, device="cuda", dtype=dt, requires_grad=True)
+        mask = torch.randn(1, 1, S, S, device="cuda").to(dt) if args.mask else None
+        kw = dict(causal=bool(args.causal), attn_mask=mask, dropout_p=args.dropout)
         k = torch.randn_like(q, requires_grad=True)
         v = torch.randn_like(q, requires_grad=True)
         do = torch.randn_like(q)
         flops = 4 * B * H * S * S * D * (0.5 if args.causal else 1.0)
-        ours_f = timeit(lambda: flash_attention(q, k, v, causal=bool(args.causal)))
+        ours_f = timeit(lambda: flash_attention(q, k, v, **kw))
 
         def ours_fb():
-            o = flash_attention(q, k, v, causal=bool(args.causal))
+            o = flash_attention(q, k, v, **kw)
             o.backward(do)
         ours_fb_t = timeit(ours_fb)
+        if args.no_sdpa:
+            print(json.dumps(dict(shape=s, causal=args.causal, dtype=args.dtype, dropout=args.dropout,
+                                  mask=args.mask, ours_fwd_tflops=round(flops / ours_f / 1e12, 1),
+                                  ours_fwdbwd_tflops=round(3.5 * flops / ours_fb_t / 1e12, 1),
+                                  ours_fwd_ms=round(ours_f * 1e3, 3),
+                                  ours_fwdbwd_ms=round(ours_fb_t * 1e3, 3))), flush=True)
+            continue
         qt, kt, vt = (t.detach().transpose(1, 2).contiguous().requires_grad_() for t in (q, k, v))
         dot = do.transpose(1, 2).contiguous()
         sd = torch.nn.functional.scaled_dot_product_attention

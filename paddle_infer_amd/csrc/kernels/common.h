@@ -29,6 +29,18 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   __bf16 b = (__bf16)f;
   return __builtin_bit_cast(bf16_t, b);
 }
+// 16-bit float storage (bf16 or IEEE fp16) <-> f32, selected at compile time.
+template <bool F16>
+__device__ __forceinline__ float h2f(unsigned short v) {
+  if (F16) return (float)__builtin_bit_cast(_Float16, v);
+  return bf2f(v);
+}
+template <bool F16>
+__device__ __forceinline__ unsigned short f2h(float f) {
+  if (F16) return __builtin_bit_cast(unsigned short, (_Float16)f);
+  return f2bf(f);
+}
+
 // pack two floats into one dword of 2 x bf16 (lo in bits 0..15)
 __device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
   return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);

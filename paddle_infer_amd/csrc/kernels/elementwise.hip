@@ -33,8 +33,8 @@ __device__ __forceinline__ float act_g(float x) {
   return 1.f;
 }
 
-// y = act(x + bias) (bias optional, broadcast over rows of length N); bf16; N % 8 == 0.
-template <int ACT>
+// y = act(x + bias) (bias optional, broadcast over rows of length N); bf16 / fp16; N % 8 == 0.
+template <int ACT, bool F16>
 __global__ __launch_bounds__(256) void bias_act_fwd_kernel(const bf16_t* __restrict__ x,
                                                           const bf16_t* __restrict__ bias,
                                                           bf16_t* __restrict__ y,
@@ -70,10 +70,10 @@ __global__ __launch_bounds__(256) void bias_act_fwd_kernel(const bf16_t* __restr
       u16x8 o, pr;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float v = bf2f(r[u][j]);
-        if (bias) v += bf2f(b[u][j]);
-        pr[j] = f2bf(v);
-        o[j] = f2bf(act_f<ACT>(v));
+        float v = h2f<F16>(r[u][j]);
+        if (bias) v += h2f<F16>(b[u][j]);
+        pr[j] = f2h<F16>(v);
+        o[j] = f2h<F16>(act_f<ACT>(v));
       }
       if (pre) reinterpret_cast<u16x8*>(pre)[i] = pr;
       reinterpret_cast<u16x8*>(y)[i] = o;
@@ -82,7 +82,7 @@ __global__ __launch_bounds__(256) void bias_act_fwd_kernel(const bf16_t* __restr
 }
 
 // dx = dy * act'(h) with h = pre-activation (x + bias); dbias partials. grid = (G, ceil(N/2048)).
-template <int ACT>
+template <int ACT, bool F16>
 __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const bf16_t* __restrict__ dy,
                                                           const bf16_t* __restrict__ h,
                                                           const bf16_t* __restrict__ bias,
@@ -112,10 +112,10 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const bf16_t* __restr
       u16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float hh = bf2f(hv[u][j]);
-        if (bias) hh += bf2f(b[j]);
-        float g = bf2f(d[u][j]) * act_g<ACT>(hh);
-        o[j] = f2bf(g);
+        float hh = h2f<F16>(hv[u][j]);
+        if (bias) hh += h2f<F16>(b[j]);
+        float g = h2f<F16>(d[u][j]) * act_g<ACT>(hh);
+        o[j] = f2h<F16>(g);
         acc[j] += g;
       }
       reinterpret_cast<u16x8*>(dx)[idx] = o;
@@ -137,7 +137,8 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const bf16_t* __restr
   }
 }
 
-__global__ __launch_bounds__(256) void colsum_bf16_kernel(const float* __restrict__ part, int G,
+template <bool F16>
+__global__ __launch_bounds__(256) void colsum16_kernel(const float* __restrict__ part, int G,
                                                          int N, bf16_t* __restrict__ out,
                                                          int accumulate) {
   const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
@@ -150,15 +151,15 @@ __global__ __launch_bounds__(256) void colsum_bf16_kernel(const float* __restric
   __syncthreads();
   if (rg == 0 && col < N) {
     float t = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
-    if (accumulate) t += bf2f(out[col]);
-    out[col] = f2bf(t);
+    if (accumulate) t += h2f<F16>(out[col]);
+    out[col] = f2h<F16>(t);
   }
 }
 
 // Row softmax with optional additive mask (broadcast over rows: mask row index = row % mask_rows)
 // and optional causal (upper-triangle) masking with query position = row % causal_q. One wave
-// per row for N <= 4096 (row in registers), bf16 in/out.
-template <int NV>
+// per row for N <= 4096 (row in registers), bf16 / fp16 in/out.
+template <int NV, bool F16>
 __global__ __launch_bounds__(256) void softmax_fwd_kernel(const bf16_t* __restrict__ x,
                                                          const bf16_t* __restrict__ mask,
                                                          int mask_rows, int causal_q,
@@ -181,8 +182,8 @@ __global__ __launch_bounds__(256) void softmax_fwd_kernel(const bf16_t* __restri
       if (mask) mk = reinterpret_cast<const u16x8*>(mask + (size_t)(row % mask_rows) * N)[vi];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float t = bf2f(r[j]) * scale;
-        if (mask) t += bf2f(mk[j]);
+        float t = h2f<F16>(r[j]) * scale;
+        if (mask) t += h2f<F16>(mk[j]);
         if (vi * 8 + j > qpos) t = -INFINITY;
         v[i][j] = t;
         m = fmaxf(m, t);
@@ -210,14 +211,14 @@ __global__ __launch_bounds__(256) void softmax_fwd_kernel(const bf16_t* __restri
     if (vi < nvec) {
       u16x8 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = f2bf(v[i][j] * inv);
+      for (int j = 0; j < 8; ++j) o[j] = f2h<F16>(v[i][j] * inv);
       reinterpret_cast<u16x8*>(y + base)[vi] = o;
     }
   }
 }
 
 // dx = scale * y * (dy - sum(dy * y))
-template <int NV>
+template <int NV, bool F16>
 __global__ __launch_bounds__(256) void softmax_bwd_kernel(const bf16_t* __restrict__ y,
                                                          const bf16_t* __restrict__ dy,
                                                          bf16_t* __restrict__ dx, int rows, int N,
@@ -236,7 +237,7 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(const bf16_t* __restri
       u16x8 a = reinterpret_cast<const u16x8*>(y + base)[vi];
       u16x8 b = reinterpret_cast<const u16x8*>(dy + base)[vi];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { yv[i][j] = bf2f(a[j]); dv[i][j] = bf2f(b[j]); s += yv[i][j] * dv[i][j]; }
+      for (int j = 0; j < 8; ++j) { yv[i][j] = h2f<F16>(a[j]); dv[i][j] = h2f<F16>(b[j]); s += yv[i][j] * dv[i][j]; }
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) { yv[i][j] = 0.f; dv[i][j] = 0.f; }
@@ -249,13 +250,14 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(const bf16_t* __restri
     if (vi < nvec) {
       u16x8 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = f2bf(scale * yv[i][j] * (dv[i][j] - s));
+      for (int j = 0; j < 8; ++j) o[j] = f2h<F16>(scale * yv[i][j] * (dv[i][j] - s));
       reinterpret_cast<u16x8*>(dx + base)[vi] = o;
     }
   }
 }
 
 // Dropout with stateless hash mask (mask regenerated in backward from seed/offset).
+template <bool F16>
 __global__ __launch_bounds__(256) void dropout_kernel(const bf16_t* __restrict__ x,
                                                      bf16_t* __restrict__ y, long long n8, float p,
                                                      uint64_t seed, uint64_t offset) {
@@ -267,7 +269,7 @@ __global__ __launch_bounds__(256) void dropout_kernel(const bf16_t* __restrict__
     hash_uniform8(seed, offset, (uint64_t)i * 8, u);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      o[j] = f2bf(u[j] >= p ? bf2f(r[j]) * ks : 0.f);
+      o[j] = f2h<F16>(u[j] >= p ? h2f<F16>(r[j]) * ks : 0.f);
     }
     reinterpret_cast<u16x8*>(y)[i] = o;
   }
@@ -275,7 +277,7 @@ __global__ __launch_bounds__(256) void dropout_kernel(const bf16_t* __restrict__
 
 }  // namespace
 
-PIAMD_EXPORT int piamd_bias_act_fwd(int act, const void* x, const void* bias, void* y, void* pre,
+PIAMD_EXPORT int piamd_bias_act_fwd(int f16, int act, const void* x, const void* bias, void* y, void* pre,
                                     long long n, int N, hipStream_t stream) {
   if (n == 0) return 0;
   if (n % 8 || N % 8) return (int)hipErrorInvalidValue;
@@ -283,7 +285,9 @@ PIAMD_EXPORT int piamd_bias_act_fwd(int act, const void* x, const void* bias, vo
   const int grid = stride_grid(n8, 256);
 #define BAF(A)                                                                                  \
   case A:                                                                                       \
-    hipLaunchKernelGGL((bias_act_fwd_kernel<A>), dim3(grid), dim3(256), 0, stream,             \
+    if (f16) hipLaunchKernelGGL((bias_act_fwd_kernel<A, true>), dim3(grid), dim3(256), 0, stream, \
+                       (const bf16_t*)x, (const bf16_t*)bias, (bf16_t*)y, (bf16_t*)pre, n8, N); \
+    else hipLaunchKernelGGL((bias_act_fwd_kernel<A, false>), dim3(grid), dim3(256), 0, stream, \
                        (const bf16_t*)x, (const bf16_t*)bias, (bf16_t*)y, (bf16_t*)pre, n8, N); \
     break;
   switch (act) { BAF(0) BAF(1) BAF(2) BAF(3) BAF(4) default: return (int)hipErrorInvalidValue; }
@@ -297,7 +301,7 @@ PIAMD_EXPORT int piamd_bias_act_bwd_grid(int rows) {
 }
 
 // part: f32 [N] workspace (zeroed here) — needed when dbias != null.
-PIAMD_EXPORT int piamd_bias_act_bwd(int act, const void* dy, const void* h, const void* bias,
+PIAMD_EXPORT int piamd_bias_act_bwd(int f16, int act, const void* dy, const void* h, const void* bias,
                                     void* dx, void* dbias, float* part, int rows, int N,
                                     int accumulate, hipStream_t stream) {
   if (rows == 0) return 0;
@@ -306,20 +310,28 @@ PIAMD_EXPORT int piamd_bias_act_bwd(int act, const void* dy, const void* h, cons
   dim3 grid(G, (N / 8 + 255) / 256);
 #define BAB(A)                                                                                  \
   case A:                                                                                       \
-    hipLaunchKernelGGL((bias_act_bwd_kernel<A>), grid, dim3(256), 0, stream, (const bf16_t*)dy, \
-                       (const bf16_t*)h, (const bf16_t*)bias, (bf16_t*)dx,                     \
+    if (f16) hipLaunchKernelGGL((bias_act_bwd_kernel<A, true>), grid, dim3(256), 0, stream,     \
+                       (const bf16_t*)dy, (const bf16_t*)h, (const bf16_t*)bias, (bf16_t*)dx,  \
+                       dbias ? part : nullptr, rows, N);                                        \
+    else hipLaunchKernelGGL((bias_act_bwd_kernel<A, false>), grid, dim3(256), 0, stream,        \
+                       (const bf16_t*)dy, (const bf16_t*)h, (const bf16_t*)bias, (bf16_t*)dx,  \
                        dbias ? part : nullptr, rows, N);                                        \
     break;
   if (dbias) (void)hipMemsetAsync(part, 0, sizeof(float) * N, stream);
   switch (act) { BAB(0) BAB(1) BAB(2) BAB(3) BAB(4) default: return (int)hipErrorInvalidValue; }
 #undef BAB
-  if (dbias)
-    hipLaunchKernelGGL(colsum_bf16_kernel, dim3((N + 63) / 64), dim3(256), 0, stream, part, 1, N,
-                       (bf16_t*)dbias, accumulate);
+  if (dbias) {
+    if (f16)
+      hipLaunchKernelGGL((colsum16_kernel<true>), dim3((N + 63) / 64), dim3(256), 0, stream, part, 1,
+                         N, (bf16_t*)dbias, accumulate);
+    else
+      hipLaunchKernelGGL((colsum16_kernel<false>), dim3((N + 63) / 64), dim3(256), 0, stream, part,
+                         1, N, (bf16_t*)dbias, accumulate);
+  }
   return (int)hipGetLastError();
 }
 
-PIAMD_EXPORT int piamd_softmax_fwd(const void* x, const void* mask, int mask_rows, int causal_q,
+PIAMD_EXPORT int piamd_softmax_fwd(int f16, const void* x, const void* mask, int mask_rows, int causal_q,
                                    void* y, int rows, int N, float scale, hipStream_t stream) {
   if (rows == 0) return 0;
   if (N % 8 || N > 4096) return (int)hipErrorInvalidValue;
@@ -327,9 +339,12 @@ PIAMD_EXPORT int piamd_softmax_fwd(const void* x, const void* mask, int mask_row
   dim3 grid((rows + 3) / 4);
 #define SMF(NVV, REAL)                                                                           \
   case REAL:                                                                                     \
-    hipLaunchKernelGGL((softmax_fwd_kernel<NVV>), grid, dim3(256), 0, stream, (const bf16_t*)x, \
-                       (const bf16_t*)mask, mask_rows > 0 ? mask_rows : 1, causal_q,            \
-                       (bf16_t*)y, rows, N, scale);                                             \
+    if (f16) hipLaunchKernelGGL((softmax_fwd_kernel<NVV, true>), grid, dim3(256), 0, stream,    \
+                       (const bf16_t*)x, (const bf16_t*)mask, mask_rows > 0 ? mask_rows : 1,    \
+                       causal_q, (bf16_t*)y, rows, N, scale);                                   \
+    else hipLaunchKernelGGL((softmax_fwd_kernel<NVV, false>), grid, dim3(256), 0, stream,       \
+                       (const bf16_t*)x, (const bf16_t*)mask, mask_rows > 0 ? mask_rows : 1,    \
+                       causal_q, (bf16_t*)y, rows, N, scale);                                   \
     break;
   switch (nv) { SMF(1, 1) SMF(2, 2) SMF(4, 3) SMF(4, 4) SMF(8, 5) SMF(8, 6) SMF(8, 7) SMF(8, 8)
     default: return (int)hipErrorInvalidValue; }
@@ -337,7 +352,7 @@ PIAMD_EXPORT int piamd_softmax_fwd(const void* x, const void* mask, int mask_row
   return (int)hipGetLastError();
 }
 
-PIAMD_EXPORT int piamd_softmax_bwd(const void* y, const void* dy, void* dx, int rows, int N,
+PIAMD_EXPORT int piamd_softmax_bwd(int f16, const void* y, const void* dy, void* dx, int rows, int N,
                                    float scale, hipStream_t stream) {
   if (rows == 0) return 0;
   if (N % 8 || N > 4096) return (int)hipErrorInvalidValue;
@@ -345,8 +360,10 @@ PIAMD_EXPORT int piamd_softmax_bwd(const void* y, const void* dy, void* dx, int 
   dim3 grid((rows + 3) / 4);
 #define SMB(NVV, REAL)                                                                           \
   case REAL:                                                                                     \
-    hipLaunchKernelGGL((softmax_bwd_kernel<NVV>), grid, dim3(256), 0, stream, (const bf16_t*)y, \
-                       (const bf16_t*)dy, (bf16_t*)dx, rows, N, scale);                        \
+    if (f16) hipLaunchKernelGGL((softmax_bwd_kernel<NVV, true>), grid, dim3(256), 0, stream,    \
+                       (const bf16_t*)y, (const bf16_t*)dy, (bf16_t*)dx, rows, N, scale);       \
+    else hipLaunchKernelGGL((softmax_bwd_kernel<NVV, false>), grid, dim3(256), 0, stream,       \
+                       (const bf16_t*)y, (const bf16_t*)dy, (bf16_t*)dx, rows, N, scale);       \
     break;
   switch (nv) { SMB(1, 1) SMB(2, 2) SMB(4, 3) SMB(4, 4) SMB(8, 5) SMB(8, 6) SMB(8, 7) SMB(8, 8)
     default: return (int)hipErrorInvalidValue; }
@@ -354,13 +371,17 @@ PIAMD_EXPORT int piamd_softmax_bwd(const void* y, const void* dy, void* dx, int 
   return (int)hipGetLastError();
 }
 
-PIAMD_EXPORT int piamd_dropout(const void* x, void* y, long long n, float p, uint64_t seed,
+PIAMD_EXPORT int piamd_dropout(int f16, const void* x, void* y, long long n, float p, uint64_t seed,
                                uint64_t offset, hipStream_t stream) {
   if (n == 0) return 0;
   if (n % 8) return (int)hipErrorInvalidValue;
   const int grid = stride_grid(n / 8, 256);
-  hipLaunchKernelGGL(dropout_kernel, dim3(grid), dim3(256), 0, stream, (const bf16_t*)x,
-                     (bf16_t*)y, n / 8, p, seed, offset);
+  if (f16)
+    hipLaunchKernelGGL((dropout_kernel<true>), dim3(grid), dim3(256), 0, stream, (const bf16_t*)x,
+                       (bf16_t*)y, n / 8, p, seed, offset);
+  else
+    hipLaunchKernelGGL((dropout_kernel<false>), dim3(grid), dim3(256), 0, stream, (const bf16_t*)x,
+                       (bf16_t*)y, n / 8, p, seed, offset);
   return (int)hipGetLastError();
 }
 

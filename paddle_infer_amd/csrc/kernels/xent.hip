@@ -25,11 +25,12 @@ __device__ __forceinline__ void online_merge(float& m, float& s, float m2, float
   m = M;
 }
 
-template <bool BF16>
+template <int DT>  // 0 = f32, 1 = bf16, 2 = fp16
 __global__ __launch_bounds__(256) void xent_stats_kernel(
     const void* __restrict__ logits, const long long* __restrict__ labels, int V,
     long long vocab_start, int ignore_index, float* __restrict__ out_max,
     float* __restrict__ out_sum, float* __restrict__ out_target) {
+  constexpr bool BF16 = DT != 0, F16 = DT == 2;  // BF16: any 16-bit storage
   const int row = blockIdx.x;
   const size_t base = (size_t)row * V;
   float m = -INFINITY, s = 0.f;
@@ -39,7 +40,7 @@ __global__ __launch_bounds__(256) void xent_stats_kernel(
       u16x8 r = p[i];
       float x[8], lm = -INFINITY;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { x[j] = bf2f(r[j]); lm = fmaxf(lm, x[j]); }
+      for (int j = 0; j < 8; ++j) { x[j] = h2f<F16>(r[j]); lm = fmaxf(lm, x[j]); }
       float ls = 0.f;
 #pragma unroll
       for (int j = 0; j < 8; ++j) ls += __expf(x[j] - lm);
@@ -47,7 +48,7 @@ __global__ __launch_bounds__(256) void xent_stats_kernel(
     }
   } else {
     for (int i = threadIdx.x; i < V; i += 256) {
-      float x = BF16 ? bf2f(((const bf16_t*)logits)[base + i]) : ((const float*)logits)[base + i];
+      float x = BF16 ? h2f<F16>(((const bf16_t*)logits)[base + i]) : ((const float*)logits)[base + i];
       online_update(m, s, x);
     }
   }
@@ -70,18 +71,19 @@ __global__ __launch_bounds__(256) void xent_stats_kernel(
     float t = 0.f;
     if (lab != ignore_index && lab >= vocab_start && lab < vocab_start + V) {
       const size_t k = base + (size_t)(lab - vocab_start);
-      t = BF16 ? bf2f(((const bf16_t*)logits)[k]) : ((const float*)logits)[k];
+      t = BF16 ? h2f<F16>(((const bf16_t*)logits)[k]) : ((const float*)logits)[k];
     }
     out_target[row] = t;
   }
 }
 
 // grad[row, j] = (exp(x - lse) - [j == label]) * dloss[row]   (0 for ignored rows)
-template <bool BF16>
+template <int DT>  // 0 = f32, 1 = bf16, 2 = fp16
 __global__ __launch_bounds__(256) void xent_bwd_kernel(
     const void* __restrict__ logits, const long long* __restrict__ labels,
     const float* __restrict__ lse, const float* __restrict__ dloss, float dloss_scalar, int V,
     long long vocab_start, int ignore_index, void* __restrict__ grad) {
+  constexpr bool BF16 = DT != 0, F16 = DT == 2;  // BF16: any 16-bit storage
   const int row = blockIdx.x;
   const size_t base = (size_t)row * V;
   const long long lab = labels[row];
@@ -95,19 +97,19 @@ __global__ __launch_bounds__(256) void xent_bwd_kernel(
       u16x8 r = p[i], o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float g = __expf(bf2f(r[j]) - L);
+        float g = __expf(h2f<F16>(r[j]) - L);
         if ((long long)(i * 8 + j) == tl) g -= 1.f;
-        o[j] = f2bf(g * d);
+        o[j] = f2h<F16>(g * d);
       }
       q[i] = o;
     }
   } else {
     for (int i = threadIdx.x; i < V; i += 256) {
-      float x = BF16 ? bf2f(((const bf16_t*)logits)[base + i]) : ((const float*)logits)[base + i];
+      float x = BF16 ? h2f<F16>(((const bf16_t*)logits)[base + i]) : ((const float*)logits)[base + i];
       float g = __expf(x - L);
       if ((long long)i == tl) g -= 1.f;
       g *= d;
-      if (BF16) ((bf16_t*)grad)[base + i] = f2bf(g);
+      if (BF16) ((bf16_t*)grad)[base + i] = f2h<F16>(g);
       else ((float*)grad)[base + i] = g;
     }
   }
@@ -115,17 +117,18 @@ __global__ __launch_bounds__(256) void xent_bwd_kernel(
 
 }  // namespace
 
+// dtype: 0 = f32, 1 = bf16, 2 = fp16.
 // Per-row local statistics: max, Σexp(x - max), target logit (0 if label not in this shard).
 PIAMD_EXPORT int piamd_xent_stats(int dtype, const void* logits, const long long* labels, int rows,
                                   int V, long long vocab_start, int ignore_index, float* out_max,
                                   float* out_sum, float* out_target, hipStream_t stream) {
   if (rows == 0) return 0;
-  if (dtype)
-    hipLaunchKernelGGL((xent_stats_kernel<true>), dim3(rows), dim3(256), 0, stream, logits,
-                       labels, V, vocab_start, ignore_index, out_max, out_sum, out_target);
-  else
-    hipLaunchKernelGGL((xent_stats_kernel<false>), dim3(rows), dim3(256), 0, stream, logits,
-                       labels, V, vocab_start, ignore_index, out_max, out_sum, out_target);
+#define XS(D)                                                                                     \
+  hipLaunchKernelGGL((xent_stats_kernel<D>), dim3(rows), dim3(256), 0, stream, logits, labels, V, \
+                     vocab_start, ignore_index, out_max, out_sum, out_target)
+  if (dtype == 1) XS(1); else if (dtype == 2) XS(2); else if (dtype == 0) XS(0);
+  else return (int)hipErrorInvalidValue;
+#undef XS
   return (int)hipGetLastError();
 }
 
@@ -136,11 +139,11 @@ PIAMD_EXPORT int piamd_xent_bwd(int dtype, const void* logits, const long long* 
                                 int V, long long vocab_start, int ignore_index, void* grad,
                                 hipStream_t stream) {
   if (rows == 0) return 0;
-  if (dtype)
-    hipLaunchKernelGGL((xent_bwd_kernel<true>), dim3(rows), dim3(256), 0, stream, logits, labels,
-                       lse, dloss, dloss_scalar, V, vocab_start, ignore_index, grad);
-  else
-    hipLaunchKernelGGL((xent_bwd_kernel<false>), dim3(rows), dim3(256), 0, stream, logits,
-                       labels, lse, dloss, dloss_scalar, V, vocab_start, ignore_index, grad);
+#define XB(D)                                                                                     \
+  hipLaunchKernelGGL((xent_bwd_kernel<D>), dim3(rows), dim3(256), 0, stream, logits, labels, lse, \
+                     dloss, dloss_scalar, V, vocab_start, ignore_index, grad)
+  if (dtype == 1) XB(1); else if (dtype == 2) XB(2); else if (dtype == 0) XB(0);
+  else return (int)hipErrorInvalidValue;
+#undef XB
   return (int)hipGetLastError();
 }

@@ -48,14 +48,14 @@ _SIGS = {
                          c_void_p, c_void_p],
     "piamd_xent_bwd": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int, c_int, c_ll,
                        c_int, c_void_p, c_void_p],
-    "piamd_bias_act_fwd": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p],
+    "piamd_bias_act_fwd": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_void_p],
     "piamd_bias_act_bwd_grid": [c_int],
-    "piamd_bias_act_bwd": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+    "piamd_bias_act_bwd": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                            c_int, c_int, c_int, c_void_p],
-    "piamd_softmax_fwd": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_float,
+    "piamd_softmax_fwd": [c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_float,
                           c_void_p],
-    "piamd_softmax_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p],
-    "piamd_dropout": [c_void_p, c_void_p, c_ll, c_float, c_u64, c_u64, c_void_p],
+    "piamd_softmax_bwd": [c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p],
+    "piamd_dropout": [c_int, c_void_p, c_void_p, c_ll, c_float, c_u64, c_u64, c_void_p],
     "piamd_qkv_prep": [c_void_p, c_ll, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                        c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p],
     # qkv, ldq, bias, prep, rot, neox, base, kc, vc, lens, B, Hq, Hk, D, maxS, chunk, nsplit,

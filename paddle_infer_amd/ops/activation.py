@@ -12,6 +12,13 @@ import torch.nn.functional as F
 from . import _lib
 from ..framework import random as _random
 
+_H16 = (torch.bfloat16, torch.float16)
+
+
+def _f16(t) -> int:
+    return int(t.dtype == torch.float16)
+
+
 ACTS = {"none": 0, "identity": 0, "gelu_tanh": 1, "gelu": 2, "relu": 3, "silu": 4, "swish": 4}
 
 
@@ -35,7 +42,7 @@ class _BiasActFn(torch.autograd.Function):
         y = torch.empty_like(x2)
         # the pre-activation is NOT materialised: backward re-adds the bias to the saved GEMM
         # output in registers (saves one [tokens x 4h] write per layer)
-        _lib.call("piamd_bias_act_fwd", act, x2.data_ptr(), _lib.ptr(bias), y.data_ptr(),
+        _lib.call("piamd_bias_act_fwd", _f16(x2), act, x2.data_ptr(), _lib.ptr(bias), y.data_ptr(),
                   None, x2.numel(), N, _lib.stream())
         ctx.save_for_backward(x2)
         ctx.act = act
@@ -60,7 +67,7 @@ class _BiasActFn(torch.autograd.Function):
                 db = torch.empty(N, device=h.device, dtype=h.dtype)
             part = torch.empty((N,), device=h.device, dtype=torch.float32)
         # h is the GEMM output without bias: the kernel adds the bias before act'()
-        _lib.call("piamd_bias_act_bwd", ctx.act, dy.data_ptr(), h.data_ptr(),
+        _lib.call("piamd_bias_act_bwd", _f16(h), ctx.act, dy.data_ptr(), h.data_ptr(),
                   _lib.ptr(ctx.bias_param), dx.data_ptr(), _lib.ptr(db), _lib.ptr(part), rows, N,
                   acc, _lib.stream())
         if acc:
@@ -73,9 +80,11 @@ def bias_act(x, bias=None, act: str = "gelu"):
     """``act(x + bias)``; bias broadcast over the last dim."""
     a = ACTS[act]
     N = x.shape[-1]
-    if x.is_cuda and x.dtype == torch.bfloat16 and N % 8 == 0 and \
-            (bias is None or bias.dtype == torch.bfloat16):
-        return _BiasActFn.apply(x, bias, a)
+    if x.is_cuda:
+        if x.dtype in _H16 and N % 8 == 0:
+            b = bias if bias is None or bias.dtype == x.dtype else bias.to(x.dtype)
+            return _BiasActFn.apply(x, b, a)
+        _lib.fallback("bias_act", f"dtype {x.dtype} / N {N} (kernel: bf16/fp16, N % 8 == 0)")
     return _ref_act(x if bias is None else x + bias, a)
 
 
@@ -88,7 +97,7 @@ class _DropoutFn(torch.autograd.Function):
     def forward(ctx, x, p, seed, offset):
         x2 = x.contiguous()
         y = torch.empty_like(x2)
-        _lib.call("piamd_dropout", x2.data_ptr(), y.data_ptr(), x2.numel(), float(p), seed, offset,
+        _lib.call("piamd_dropout", _f16(x2), x2.data_ptr(), y.data_ptr(), x2.numel(), float(p), seed, offset,
                   _lib.stream())
         ctx.meta = (p, seed, offset)
         return y
@@ -98,7 +107,7 @@ class _DropoutFn(torch.autograd.Function):
         p, seed, offset = ctx.meta
         dy = dy.contiguous()
         dx = torch.empty_like(dy)
-        _lib.call("piamd_dropout", dy.data_ptr(), dx.data_ptr(), dy.numel(), float(p), seed, offset,
+        _lib.call("piamd_dropout", _f16(dy), dy.data_ptr(), dx.data_ptr(), dy.numel(), float(p), seed, offset,
                   _lib.stream())
         return dx, None, None, None
 
@@ -106,9 +115,11 @@ class _DropoutFn(torch.autograd.Function):
 def dropout(x, p: float = 0.5, training: bool = True):
     if not training or p == 0.0:
         return x
-    if x.is_cuda and x.dtype == torch.bfloat16 and x.numel() % 8 == 0:
-        seed, offset = _random.next_seed_offset(x.numel())
-        return _DropoutFn.apply(x, p, seed, offset)
+    if x.is_cuda:
+        if x.dtype in _H16 and x.numel() % 8 == 0:
+            seed, offset = _random.next_seed_offset(x.numel())
+            return _DropoutFn.apply(x, p, seed, offset)
+        _lib.fallback("dropout", f"dtype {x.dtype} / numel % 8 (kernel: bf16/fp16)")
     return F.dropout(x, p, training=True)
 
 
@@ -123,7 +134,7 @@ class _SoftmaxFn(torch.autograd.Function):
         if mask is not None:
             mask = mask.contiguous()
             mrows = mask.numel() // N
-        _lib.call("piamd_softmax_fwd", x2.data_ptr(), _lib.ptr(mask), mrows, causal_q, y.data_ptr(),
+        _lib.call("piamd_softmax_fwd", _f16(x2), x2.data_ptr(), _lib.ptr(mask), mrows, causal_q, y.data_ptr(),
                   rows, N, float(scale), _lib.stream())
         ctx.save_for_backward(y)
         ctx.scale = scale
@@ -135,7 +146,7 @@ class _SoftmaxFn(torch.autograd.Function):
         N = y.shape[-1]
         dy = dy.contiguous()
         dx = torch.empty_like(y)
-        _lib.call("piamd_softmax_bwd", y.data_ptr(), dy.data_ptr(), dx.data_ptr(), y.numel() // N, N,
+        _lib.call("piamd_softmax_bwd", _f16(y), y.data_ptr(), dy.data_ptr(), dx.data_ptr(), y.numel() // N, N,
                   float(ctx.scale), _lib.stream())
         return dx, None, None, None
 
@@ -144,10 +155,13 @@ def fused_softmax_mask(x, mask=None, scale: float = 1.0, causal: bool = False):
     """softmax(scale*x + mask) over the last dim; ``causal`` masks the upper triangle (the
     reference's ``fused_softmax_mask_upper_triangle``). mask broadcasts over leading rows."""
     N = x.shape[-1]
-    if x.is_cuda and x.dtype == torch.bfloat16 and N % 8 == 0 and N <= 4096 and \
-            (mask is None or (mask.dtype == torch.bfloat16 and x.numel() % mask.numel() == 0)):
-        cq = x.shape[-2] if causal else 0
-        return _SoftmaxFn.apply(x, mask, cq, scale)
+    if x.is_cuda:
+        if x.dtype in _H16 and N % 8 == 0 and N <= 4096 and \
+                (mask is None or x.numel() % mask.numel() == 0):
+            cq = x.shape[-2] if causal else 0
+            m = mask if mask is None or mask.dtype == x.dtype else mask.to(x.dtype)
+            return _SoftmaxFn.apply(x, m, cq, scale)
+        _lib.fallback("fused_softmax_mask", f"dtype {x.dtype} / N {N} / mask shape")
     s = x.float() * scale
     if mask is not None:
         s = s + mask.float()

@@ -18,7 +18,7 @@ def _stats(logits2, labels, vocab_start, ignore_index):
     m = torch.empty(rows, device=logits2.device, dtype=torch.float32)
     s = torch.empty_like(m)
     t = torch.empty_like(m)
-    _lib.call("piamd_xent_stats", _lib.dtype_code(logits2), logits2.data_ptr(), labels.data_ptr(),
+    _lib.call("piamd_xent_stats", _lib.dtype_code(logits2, fp16=True), logits2.data_ptr(), labels.data_ptr(),
               rows, V, int(vocab_start), int(ignore_index), m.data_ptr(), s.data_ptr(), t.data_ptr(),
               _lib.stream())
     return m, s, t
@@ -55,7 +55,7 @@ class _XentFn(torch.autograd.Function):
         rows, V = lg.shape
         d = dloss.contiguous().view(-1).float()
         grad = lg if inplace else torch.empty_like(lg)
-        _lib.call("piamd_xent_bwd", _lib.dtype_code(lg), lg.data_ptr(), lab.data_ptr(), lse.data_ptr(),
+        _lib.call("piamd_xent_bwd", _lib.dtype_code(lg, fp16=True), lg.data_ptr(), lab.data_ptr(), lse.data_ptr(),
                   d.data_ptr(), 0.0, rows, V, int(vocab_start), int(ignore_index), grad.data_ptr(),
                   _lib.stream())
         return grad.view(shp), None, None, None, None
@@ -71,7 +71,7 @@ def softmax_cross_entropy(logits, labels, ignore_index: int = -100, group=None,
                           inplace_backward: bool = False):
     """Per-token loss (no reduction). ``group``: model-parallel group for vocab-sharded logits
     (each rank holds a contiguous V/mp slice, rank r owning [r*V_local, (r+1)*V_local))."""
-    if logits.is_cuda and logits.dtype in (torch.bfloat16, torch.float32):
+    if logits.is_cuda and logits.dtype in (torch.bfloat16, torch.float16, torch.float32):
         return _XentFn.apply(logits, labels, ignore_index, group, inplace_backward)
     if group is not None and dist.get_world_size(group) > 1:
         return _parallel_reference(logits, labels, ignore_index, group)

@@ -421,9 +421,11 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
                             attn_mask=None, dropout_rate=0.0, activation="gelu", training=False,
                             mode="upscale_in_train", trans_qkvw=True, ring_id=-1, name=None,
                             num_kv_heads=None, rotary_emb_dims=0, use_neox_rotary_style=True,
-                            rope_base=10000.0, group=None):
+                            rope_base=10000.0, group=None, causal=False):
     """Reference `incubate/nn/functional/fused_transformer.py:833`. cache_kvs: per layer
-    [2, B, Hk, max_seq_len, D], updated in place; returns (out, cache_kvs) when given."""
+    [2, B, Hk, max_seq_len, D], updated in place; returns (out, cache_kvs) when given. Context
+    attention is full (the reference op's semantics without SrcMask) unless ``causal`` (an
+    extension: the bottom-right causal band without materialising a mask)."""
     B, S, E = x.shape
     w0 = qkv_weights[0]
     if trans_qkvw:
@@ -453,7 +455,7 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
         out = multi_transformer_forward(
             x, layers, hq, hk, pre_layer_norm, epsilon, _caches_from(cache_kvs), pos, lens,
             attn_mask, decode, activation, rotary_emb_dims, use_neox_rotary_style, rope_base,
-            causal=(attn_mask is None), group=group)
+            causal=causal and attn_mask is None, group=group)
     return (out, cache_kvs) if cache_kvs is not None else out
 
 
@@ -465,7 +467,8 @@ def fused_multi_transformer_weight_only(x, ln_scales, ln_biases, qkv_weights, qk
                                         beam_offset=None, seq_lens=None, time_step=None,
                                         attn_mask=None, activation="gelu", weight_dtype="int8",
                                         num_heads=None, num_kv_heads=None, rotary_emb_dims=0,
-                                        use_neox_rotary_style=True, rope_base=10000.0, group=None):
+                                        use_neox_rotary_style=True, rope_base=10000.0, group=None,
+                                        causal=False):
     """Reference `fused_multi_transformer_weight_only_op.cu`: every projection is a
     weight-only int8/int4 GEMM (packed [N, K] / [N/2, K] weights, per-channel f32 scales)."""
     B, S, E = x.shape
@@ -488,7 +491,7 @@ def fused_multi_transformer_weight_only(x, ln_scales, ln_biases, qkv_weights, qk
         out = multi_transformer_forward(
             x, layers, num_heads, hk, pre_layer_norm, epsilon, _caches_from(cache_kvs), pos, lens,
             attn_mask, decode, activation, rotary_emb_dims, use_neox_rotary_style, rope_base,
-            causal=(attn_mask is None), group=group)
+            causal=causal and attn_mask is None, group=group)
     return (out, cache_kvs) if cache_kvs is not None else out
 
 

@@ -15,6 +15,12 @@ a chain of Paddle ops and rewrites it into one fused op whose kernel is register
   self_attention_fuse_pass        matmul(QKᵀ)[·α] + softmax + matmul(V) → flash_attn
   linear_bias_act_fuse_pass       traced linear(no bias) + fused_bias_act → one GEMM with the
                                   bias+act epilogue (`ops.linear.linear_bias_act`)
+  identity_reshape_clean_pass     reshape2(X, Shape=shape(X))          → (removed)
+  fused_multi_transformer_encoder_pass  pre-LN causal transformer layer → fused_multi_transformer
+  fuse_multi_transformer_layer_pass     consecutive fused_multi_transformer → one multi-layer op
+  multihead_matmul_fuse_pass      fc(QKV) + head split + attention + merge → multihead_matmul
+  flash_attn_packed_fuse_pass     split(QKV) + flash_attn               → flash_attn_packed
+  fc_elementwise_layernorm_fuse_pass  fc + residual add + layer_norm    → fused_fc_elementwise_layernorm
 
 Passes only rewrite when every intermediate has exactly one consumer and is not fetched.
 """
@@ -369,10 +375,292 @@ def linear_bias_act_fuse_pass(g: Graph):
     return n
 
 
+
+
+# ---------------------------------------------------------------- passes over lowered programs
+def identity_reshape_clean_pass(g: Graph):
+    """reshape2(X, Shape = shape(X)) → X (the view_as identities a traced program lowers to)."""
+    n = 0
+    for op in list(_typed(g.ops)):
+        if op.type not in ("reshape2", "reshape") or op not in g.ops or not op.paddle_inputs.get("Shape"):
+            continue
+        x, sh = _pop(op, "X"), _pop(op, "Shape")
+        sp = g.producer(sh)
+        if sp is None or sp.func is not None or sp.type != "shape" or _pop(sp, "Input") != x:
+            continue
+        if g.bypass(op, x, _out(op)):
+            if not g.consumers(sh) and sh not in g.keep:
+                g.ops.remove(sp)
+            n += 1
+    return n
+
+
+def _single_consumer(g, name, types):
+    if name is None or name in g.keep:
+        return None
+    cons = g.consumers(name)
+    if len(cons) != 1 or cons[0].func is not None or cons[0].type not in types:
+        return None
+    return cons[0]
+
+
+def _split_qkv(g, split):
+    """A 3-way split along the head axis whose outputs feed exactly one flash_attn as q, k, v."""
+    outs = (split.paddle_outputs or {}).get("Out", [])
+    if split.type != "split" or int(split.attrs.get("axis", -1)) != 2 or len(outs) != 3:
+        return None
+    secs = list(split.attrs.get("sections") or [])
+    if len(secs) != 3:
+        return None
+    fa = _single_consumer(g, outs[0], ("flash_attn",))
+    if fa is None or any(g.consumers(o) != [fa] for o in outs[1:]) or any(o in g.keep for o in outs):
+        return None
+    qn = (fa.paddle_inputs.get("q") or fa.paddle_inputs.get("Q") or [None])[0]
+    kn = (fa.paddle_inputs.get("k") or fa.paddle_inputs.get("K") or [None])[0]
+    vn = (fa.paddle_inputs.get("v") or fa.paddle_inputs.get("V") or [None])[0]
+    if [qn, kn, vn] != outs or fa.attrs.get("layout", "bshd") != "bshd":
+        return None
+    if not fa.attrs.get("is_test", True) and float(fa.attrs.get("dropout", 0.0)) > 0:
+        return None
+    return fa, secs
+
+
+def flash_attn_packed_fuse_pass(g: Graph):
+    """split(qkv, axis 2) + flash_attn(q, k, v) → flash_attn_packed(QKV): attention reads Q/K/V
+    straight out of the fused projection output (no split copies)."""
+    n = 0
+    for sp in list(_typed(g.ops)):
+        if sp.type != "split" or sp not in g.ops:
+            continue
+        m = _split_qkv(g, sp)
+        if m is None:
+            continue
+        fa, secs = m
+        if fa.paddle_inputs.get("attn_mask") or secs[1] != secs[2]:
+            continue
+        out = (fa.paddle_outputs.get("out") or fa.paddle_outputs.get("Out"))[0]
+        fused = _new(g.block, "flash_attn_packed", {"QKV": [_pop(sp, "X")]}, {"Out": [out]},
+                     {"num_heads": int(secs[0]), "num_kv_heads": int(secs[1]),
+                      "causal": bool(fa.attrs.get("causal", False))})
+        g.replace([sp, fa], fused)
+        n += 1
+    return n
+
+
+def _fc_of(g, op):
+    """(input, W, Bias, activation) of an fc op, else None."""
+    if op is None or op.func is not None or op.type != "fc":
+        return None
+    return _pop(op, "Input"), _pop(op, "W"), _pop(op, "Bias"), op.attrs.get("activation_type", "")
+
+
+def _attn_chain(g, x, fc=None):
+    """x → fc(qkv) → reshape2 [.., S, Hq+2Hk, D] → split → flash_attn → reshape2 [.., S, E]:
+    (ops, qkv_fc, heads (hq, hk), D, flash op, attn-out name) or None."""
+    fc = fc if fc is not None else _single_consumer(g, x, ("fc",))
+    if fc is None or _fc_of(g, fc)[3] or not g.is_param(_pop(fc, "W")):
+        return None
+    r1 = _single_consumer(g, _out(fc), ("reshape2", "reshape"))
+    if r1 is None or r1.paddle_inputs.get("Shape"):
+        return None
+    shp = list(r1.attrs.get("shape") or [])
+    if len(shp) != 4:
+        return None
+    sp = _single_consumer(g, _out(r1), ("split",))
+    m = _split_qkv(g, sp) if sp is not None else None
+    if m is None:
+        return None
+    fa, secs = m
+    fout = (fa.paddle_outputs.get("out") or fa.paddle_outputs.get("Out"))[0]
+    r2 = _single_consumer(g, fout, ("reshape2", "reshape"))
+    if r2 is None or r2.paddle_inputs.get("Shape") or len(r2.attrs.get("shape") or []) != 3:
+        return None
+    return [fc, r1, sp, fa, r2], fc, (int(secs[0]), int(secs[1])), int(shp[3]), fa, _out(r2)
+
+
+def multihead_matmul_fuse_pass(g: Graph):
+    """Reference `multihead_matmul_fuse_pass_v2/v3`: the BERT self-attention block (QKV fc →
+    head split → attention [+ additive mask] → head merge) → one multihead_matmul op."""
+    n = 0
+    for fc in list(_typed(g.ops)):
+        if fc.type != "fc" or fc not in g.ops:
+            continue
+        x = _pop(fc, "Input")
+        chain = _attn_chain(g, x, fc)
+        if chain is None:
+            continue
+        ops, _, (hq, hk), D, fa, out = chain
+        if hq != hk or fa.attrs.get("causal"):
+            continue
+        w = _pop(fc, "W")
+        E = g.param(w).shape[0]
+        if hq * D != E:
+            continue
+        ins = {"Input": [x], "W": [w], "Bias": [_pop(fc, "Bias")]}
+        if fa.paddle_inputs.get("attn_mask"):
+            ins["BiasQK"] = fa.paddle_inputs["attn_mask"]
+        fused = _new(g.block, "multihead_matmul", ins, {"Out": [out]},
+                     {"head_number": hq, "alpha": 1.0 / float(np.sqrt(D))})
+        g.replace(ops, fused)
+        n += 1
+    return n
+
+
+def fc_elementwise_layernorm_fuse_pass(g: Graph):
+    """Reference `fc_elementwise_layernorm_fuse_pass`: fc + elementwise_add(residual) +
+    layer_norm → fused_fc_elementwise_layernorm (post-LN transformer blocks)."""
+    n = 0
+    for fc in list(_typed(g.ops)):
+        if fc.type != "fc" or fc not in g.ops or fc.attrs.get("activation_type") not in ("", None):
+            continue
+        add = _single_consumer(g, _out(fc), ("elementwise_add",))
+        if add is None or int(add.attrs.get("axis", -1)) != -1:
+            continue
+        y = _pop(add, "Y") if _pop(add, "X") == _out(fc) else _pop(add, "X")
+        if g.is_param(y):
+            continue
+        ln = _single_consumer(g, _out(add), ("layer_norm",))
+        if ln is None:
+            continue
+        if any(_out(ln, e) and (_out(ln, e) in g.keep or g.consumers(_out(ln, e)))
+               for e in ("Mean", "Variance")):
+            continue
+        ins = {"X": [_pop(fc, "Input")], "W": [_pop(fc, "W")], "Y": [y],
+               "Scale": [_pop(ln, "Scale")], "Bias1": [_pop(ln, "Bias")]}
+        if _pop(fc, "Bias"):
+            ins["Bias0"] = [_pop(fc, "Bias")]
+        fused = _new(g.block, "fused_fc_elementwise_layernorm", ins, {"Out": [_out(ln, "Y")]},
+                     {"x_num_col_dims": int(fc.attrs.get("in_num_col_dims", 1)),
+                      "epsilon": float(ln.attrs.get("epsilon", 1e-5)), "begin_norm_axis": 1,
+                      "activation_type": ""})
+        g.replace([fc, add, ln], fused)
+        n += 1
+    return n
+
+
+def _residual_add(g, base, other):
+    """The unique elementwise_add consumer of ``other`` that adds the residual ``base``."""
+    add = _single_consumer(g, other, ("elementwise_add",))
+    if add is None or int(add.attrs.get("axis", -1)) != -1:
+        return None
+    if {_pop(add, "X"), _pop(add, "Y")} != {base, other}:
+        return None
+    return add
+
+
+def fused_multi_transformer_encoder_pass(g: Graph):
+    """Reference `fused_multi_transformer_encoder_pass.cc`: one pre-LN decoder-only transformer
+    layer of plain ops —
+        ln1 = layer_norm(x); qkv = fc(ln1); attention (causal flash_attn over the head split);
+        x2 = x + fc(attn); ln2 = layer_norm(x2); x3 = x2 + fc(fc(ln2, act))
+    → one fused_multi_transformer op (the LLM inference kernels: fused LN prologues, packed QKV,
+    flash / split-K decode attention over a KV cache, epilogue GEMMs)."""
+    n = 0
+    for ln1 in list(_typed(g.ops)):
+        if ln1.type != "layer_norm" or ln1 not in g.ops:
+            continue
+        x = _pop(ln1, "X")
+        chain = _attn_chain(g, _out(ln1, "Y"))
+        if chain is None or len(g.consumers(_out(ln1, "Y"))) != 1:
+            continue
+        attn_ops, qkv_fc, (hq, hk), D, fa, attn_out = chain
+        if not fa.attrs.get("causal") or fa.paddle_inputs.get("attn_mask"):
+            continue
+        ofc = _single_consumer(g, attn_out, ("fc",))
+        if ofc is None or _fc_of(g, ofc)[3]:
+            continue
+        add1 = _residual_add(g, x, _out(ofc))
+        if add1 is None:
+            continue
+        x2 = _out(add1)
+        ln2s = [c for c in g.consumers(x2) if c.func is None and c.type == "layer_norm"]
+        if len(ln2s) != 1 or len(g.consumers(x2)) != 2 or x2 in g.keep:
+            continue
+        ln2 = ln2s[0]
+        f1 = _single_consumer(g, _out(ln2, "Y"), ("fc",))
+        if f1 is None or _fc_of(g, f1)[3] not in ("gelu", "relu", "gelu_tanh", ""):
+            continue
+        f2 = _single_consumer(g, _out(f1), ("fc",))
+        if f2 is None or _fc_of(g, f2)[3]:
+            continue
+        add2 = _residual_add(g, x2, _out(f2))
+        if add2 is None:
+            continue
+        if len(g.consumers(x)) != 2:  # x feeds ln1 and the first residual add only
+            continue
+        eps1, eps2 = float(ln1.attrs.get("epsilon", 1e-5)), float(ln2.attrs.get("epsilon", 1e-5))
+        if abs(eps1 - eps2) > 1e-12:
+            continue
+        wq = _pop(qkv_fc, "W")
+        W = g.param(wq)
+        E = W.shape[0]
+        wn = wq + "@fmt"  # [E, Hq+2Hk, D] view: the trans_qkvw=False layout
+        if wn not in g.program.params:
+            g.program.params[wn] = W.reshape(E, hq + 2 * hk, D)
+            g.block.create_var(wn, [E, hq + 2 * hk, D], "float32", persistable=True)
+        act = _fc_of(g, f1)[3] or "none"
+        ins = {"X": [x], "LnScale": [_pop(ln1, "Scale")], "LnBias": [_pop(ln1, "Bias")],
+               "QKVW": [wn], "QKVBias": [_pop(qkv_fc, "Bias")], "OutLinearW": [_pop(ofc, "W")],
+               "OutLinearBias": [_pop(ofc, "Bias")], "FFNLnScale": [_pop(ln2, "Scale")],
+               "FFNLnBias": [_pop(ln2, "Bias")], "FFN1Weight": [_pop(f1, "W")],
+               "FFN1Bias": [_pop(f1, "Bias")], "FFN2Weight": [_pop(f2, "W")], "FFN2Bias": [_pop(f2, "Bias")]}
+        attrs = {"pre_layer_norm": True, "epsilon": eps1, "dropout_rate": 0.0, "is_test": True,
+                 "dropout_implementation": "upscale_in_train", "act_method": act,
+                 "trans_qkvw": False, "ring_id": -1, "causal": True}
+        if hk != hq:
+            attrs["num_kv_heads"] = hk
+        fused = _new(g.block, "fused_multi_transformer", ins, {"Out": [_out(add2)]}, attrs)
+        g.replace([ln1] + attn_ops + [ofc, add1, ln2, f1, f2, add2], fused)
+        n += 1
+    return n
+
+
+_FMT_LIST_SLOTS = ("LnScale", "LnBias", "QKVW", "QKVBias", "OutLinearW", "OutLinearBias",
+                   "FFNLnScale", "FFNLnBias", "FFN1Weight", "FFN1Bias", "FFN2Weight", "FFN2Bias",
+                   "CacheKV", "QKVWScale", "OutLinearWScale", "FFN1WeightScale", "FFN2WeightScale")
+
+
+def fuse_multi_transformer_layer_pass(g: Graph):
+    """Reference `fuse_multi_transformer_layer_pass.cc`: consecutive single-layer
+    fused_multi_transformer ops (Out of one = X of the next, same attrs) → ONE op whose weight
+    slots list every layer (one launch sequence, one KV-cache list)."""
+    n = 0
+    changed = True
+    while changed:
+        changed = False
+        for a in list(_typed(g.ops)):
+            if a.type != "fused_multi_transformer" or a not in g.ops:
+                continue
+            b = _single_consumer(g, _out(a), ("fused_multi_transformer",))
+            if b is None or _pop(b, "X") != _out(a):
+                continue
+            if {k: v for k, v in a.attrs.items()} != {k: v for k, v in b.attrs.items()}:
+                continue
+            ins = {"X": [_pop(a, "X")]}
+            for slot in _FMT_LIST_SLOTS:
+                va, vb = a.paddle_inputs.get(slot) or [], b.paddle_inputs.get(slot) or []
+                if va or vb:
+                    ins[slot] = list(va) + list(vb)
+            for slot in ("TimeStep", "SrcMask", "SeqLengths", "BeamCacheOffset"):
+                if a.paddle_inputs.get(slot):
+                    ins[slot] = a.paddle_inputs[slot]
+            outs = {"Out": [_out(b)]}
+            ca, cb = (a.paddle_outputs.get("CacheKVOut") or []), (b.paddle_outputs.get("CacheKVOut") or [])
+            if ca or cb:
+                outs["CacheKVOut"] = list(ca) + list(cb)
+            g.replace([a, b], _new(g.block, "fused_multi_transformer", ins, outs, dict(a.attrs)))
+            n += 1
+            changed = True
+            break
+    return n
+
+
 GPU_PASSES = [
-    "delete_dropout_op_pass", "identity_scale_op_clean_pass", "conv_bn_fuse_pass",
-    "embedding_eltwise_layernorm_fuse_pass", "self_attention_fuse_pass", "fc_fuse_pass",
-    "fc_act_fuse_pass", "skip_layernorm_fuse_pass", "linear_bias_act_fuse_pass",
+    "delete_dropout_op_pass", "identity_scale_op_clean_pass", "identity_reshape_clean_pass",
+    "conv_bn_fuse_pass", "embedding_eltwise_layernorm_fuse_pass", "self_attention_fuse_pass",
+    "fc_fuse_pass", "fc_act_fuse_pass", "fused_multi_transformer_encoder_pass",
+    "fuse_multi_transformer_layer_pass", "multihead_matmul_fuse_pass", "flash_attn_packed_fuse_pass",
+    "fc_elementwise_layernorm_fuse_pass", "skip_layernorm_fuse_pass", "linear_bias_act_fuse_pass",
 ]
 
 PASSES = {name: globals()[name] for name in GPU_PASSES}

@@ -202,7 +202,8 @@ def save(layer, path, input_spec=None, **configs):
     for n, t in prog.params.items():
         scope.set(n, t.detach())
     with _static.scope_guard(scope):
-        _sio.save_inference_model(path, feeds, fetch, None, program=prog)
+        _sio.save_inference_model(path, feeds, fetch, None, program=prog,
+                                  allow_custom_ops=configs.get("allow_custom_ops", False))
     info = {n: {"shape": list(t.shape), "dtype": str(t.dtype).replace("torch.", ""),
                 "structured_name": n, "trainable": bool(t.requires_grad)} for n, t in prog.params.items()}
     with open(path + ".pdiparams.info", "w") as f:

@@ -6,10 +6,13 @@ serialize_program / deserialize_program / save / load / load_program_state) and
 framed by ``feed`` / ``fetch`` ops exactly like the reference; persistables are written sorted
 by name in the combined LoDTensor stream.
 
-Ops recorded by the capture mechanism carry two extra string attrs — ``op_callable`` (the torch
-callable) and ``op_spec`` (JSON of the argument structure) — so a saved program round-trips
-exactly; ops without them (programs produced by Paddle itself) execute through the Paddle-op
-registry (`ops_registry.py`).
+Saving LOWERS every recorded op (torch / framework callables captured by ``jit.to_static`` or
+static capture) into Paddle OpDescs with the reference's op types, slots and attributes
+(`lowering.py`), so a written ``.pdmodel`` holds only Paddle ops and executes through the
+Paddle-op registry (`ops_registry.py`). ``allow_custom_ops=True`` keeps an op no lowering covers in
+its recorded form (two extra string attrs, ``op_callable`` + ``op_spec``); LOADING such an op only
+resolves callables on an explicit allowlist (``resolve_func``) — a ``.pdmodel`` naming anything
+else (``os.system``, ``builtins.eval``, ``torch.load`` ...) is rejected before any code runs.
 """
 from __future__ import annotations
 
@@ -98,7 +101,7 @@ def func_name(func):
         return f"torch._tensor.{q}"
     name = f"{mod}.{q}" if mod else q
     try:
-        r = resolve_func(name)
+        r = _import_attr(name)
         if r is func or getattr(r, "__wrapped__", None) is func:  # recordable() wrappers
             return name
     except (AttributeError, ImportError, ValueError):
@@ -112,10 +115,9 @@ def func_name(func):
     raise ValueError(f"cannot serialise op callable {func!r}")
 
 
-def resolve_func(name):
+def _import_attr(name):
     import importlib
     parts = name.split(".")
-    # longest importable module prefix, then attribute walk
     for i in range(len(parts) - 1, 0, -1):
         try:
             obj = importlib.import_module(".".join(parts[:i]))
@@ -124,7 +126,73 @@ def resolve_func(name):
         for p in parts[i:]:
             obj = getattr(obj, p)
         return obj
-    raise ValueError(f"cannot resolve op callable {name}")
+    raise ValueError(name)
+
+
+_ALLOWED = None
+_ALLOWED_MODULE_PREFIXES = ("torch.", "paddle_infer_amd.")
+
+
+def _allowlist():
+    """Names of the only callables a loaded program may invoke: the torch ops the static capture
+    can record (``torch.overrides.get_overridable_functions`` — tensor math only: no IO, no
+    pickling, no process control) plus the framework's own recordable ops and autograd functions."""
+    global _ALLOWED
+    if _ALLOWED is None:
+        import torch.overrides as ov
+        allowed = {}
+        for ns, fns in ov.get_overridable_functions().items():
+            for fn in fns:
+                try:
+                    allowed[func_name(fn)] = fn
+                except (ValueError, AttributeError, TypeError):
+                    continue
+        from .framework import _paddle_types
+        for fn in _paddle_types():
+            try:
+                allowed[func_name(fn)] = fn
+            except (ValueError, AttributeError, TypeError):
+                continue
+        _ALLOWED = allowed
+    return _ALLOWED
+
+
+def _framework_callable(name):
+    """paddle_infer_amd recordable ops (``static.framework.recordable``) and autograd Functions."""
+    import importlib
+    parts = name.split(".")
+    for i in range(len(parts) - 1, 0, -1):
+        mod = ".".join(parts[:i])
+        if not mod.startswith("paddle_infer_amd"):
+            return None
+        try:
+            obj = importlib.import_module(mod)
+        except ImportError:
+            continue
+        for p in parts[i:]:
+            obj = getattr(obj, p, None)
+            if obj is None:
+                return None
+        if getattr(obj, "_paddle_type", None) is not None:
+            return obj
+        owner = getattr(obj, "__self__", None)
+        if isinstance(owner, type) and issubclass(owner, torch.autograd.Function) \
+                and owner.__module__.startswith("paddle_infer_amd"):
+            return obj
+        return None
+    return None
+
+
+def resolve_func(name):
+    """Resolve a stored ``op_callable`` name — ONLY from the allowlist (see ``_allowlist``)."""
+    if not isinstance(name, str) or not name.startswith(_ALLOWED_MODULE_PREFIXES):
+        raise ValueError(f"op_callable {name!r} is not an allowed operator")
+    fn = _allowlist().get(name)
+    if fn is None and name.startswith("paddle_infer_amd."):
+        fn = _framework_callable(name)
+    if fn is None:
+        raise ValueError(f"op_callable {name!r} is not an allowed operator")
+    return fn
 
 
 # ------------------------------------------------------------------------ Program <-> desc
@@ -141,7 +209,33 @@ def _var_desc(v: Variable, is_param):
             "stop_gradient": bool(v.stop_gradient_)}
 
 
-def program_to_desc(program: Program, feed_names=None, fetch_names=None, ops=None):
+def _paddle_op_desc(type_, ins, outs, attrs):
+    from .lowering import attr_desc
+    return {"type": type_,
+            "inputs": [{"parameter": k, "arguments": list(v)} for k, v in ins.items()],
+            "outputs": [{"parameter": k, "arguments": list(v)} for k, v in outs.items()],
+            "attrs": [attr_desc(k, v) for k, v in attrs.items()]}
+
+
+def _typed_attr_descs(attrs):
+    """Attrs of a Paddle-typed op (loaded from a Paddle program or built by a pass)."""
+    from .lowering import attr_desc, LoweringError
+    out = []
+    for k, v in attrs.items():
+        if v is None:
+            continue
+        try:
+            out.append(attr_desc(k, v))
+        except LoweringError:
+            out.append({"name": k, "type": proto.ATTR["STRING"], "s": json.dumps(_enc(v))})
+    return out
+
+
+def program_to_desc(program: Program, feed_names=None, fetch_names=None, ops=None,
+                    paddle_ops=True, allow_custom_ops=False):
+    """``paddle_ops``: lower recorded ops to Paddle OpDescs (`lowering.py`); an op no rule covers
+    raises ``LoweringError`` unless ``allow_custom_ops`` keeps it in recorded (callable) form."""
+    from .lowering import lower, LoweringError
     b = program.global_block()
     ops = b.ops if ops is None else ops
     used = set()
@@ -152,6 +246,24 @@ def program_to_desc(program: Program, feed_names=None, fetch_names=None, ops=Non
     used.update(fetch_names or [])
     vars_ = [_var_desc(b.vars[n], n in program.params) for n in sorted(used) if n in b.vars]
     op_descs = []
+    lowered = {}
+    if paddle_ops:
+        for op in ops:
+            if op.func is None or op.type in ("backward", "optimize"):
+                continue
+            try:
+                lowered[id(op)] = lower(b, op)
+            except LoweringError:
+                if not allow_custom_ops:
+                    raise
+        seen = {v["name"] for v in vars_}
+        for descs, new_vars in lowered.values():
+            for name, dims, dt in new_vars:
+                if name not in seen:
+                    seen.add(name)
+                    vars_.append({"name": name, "type": {"type": proto.VT_LOD_TENSOR, "lod_tensor": {
+                        "tensor": {"data_type": dt, "dims": dims}, "lod_level": 0}},
+                        "persistable": False, "is_parameter": False, "stop_gradient": True})
     if feed_names:
         vars_.append({"name": "feed", "type": {"type": proto.VT_FEED}, "persistable": True})
         for i, n in enumerate(feed_names):
@@ -160,6 +272,17 @@ def program_to_desc(program: Program, feed_names=None, fetch_names=None, ops=Non
                              "attrs": [{"name": "col", "type": proto.ATTR["INT"], "i": i}]})
     for op in ops:
         if op.type in ("backward", "optimize"):
+            continue
+        if id(op) in lowered:
+            op_descs.extend(_paddle_op_desc(*d) for d in lowered[id(op)][0])
+            continue
+        if op.func is None and op.paddle_inputs is not None:  # already a Paddle op
+            op_descs.append({"type": op.type,
+                             "inputs": [{"parameter": k, "arguments": list(v)}
+                                        for k, v in op.paddle_inputs.items()],
+                             "outputs": [{"parameter": k, "arguments": list(v)}
+                                         for k, v in (op.paddle_outputs or {}).items()],
+                             "attrs": _typed_attr_descs(op.attrs)})
             continue
         attrs = [{"name": k, "type": proto.ATTR["STRING"], "s": json.dumps(_enc(v))}
                  for k, v in op.attrs.items() if k not in ("optimizer",)]
@@ -236,7 +359,8 @@ def serialize_program(feed_vars, fetch_vars, program=None, **kwargs):
     feeds = [v.var_name if isinstance(v, Variable) else v for v in _as_list(feed_vars)]
     fetches = [v.var_name if isinstance(v, Variable) else v for v in _as_list(fetch_vars)]
     ops = prune(program, fetches)
-    return proto.encode("ProgramDesc", program_to_desc(program, feeds, fetches, ops))
+    return proto.encode("ProgramDesc", program_to_desc(
+        program, feeds, fetches, ops, allow_custom_ops=bool(kwargs.get("allow_custom_ops", False))))
 
 
 def deserialize_program(data: bytes):
@@ -309,7 +433,8 @@ def save_inference_model(path_prefix, feed_vars, fetch_vars, executor, program=N
         used.update(op.input_names())
     pnames = sorted(n for n in program.params if n in used)
     with open(path_prefix + ".pdmodel", "wb") as f:
-        f.write(serialize_program(feed_vars, fetch_vars, program))
+        f.write(serialize_program(feed_vars, fetch_vars, program,
+                                  allow_custom_ops=kwargs.get("allow_custom_ops", False)))
     with open(path_prefix + ".pdiparams", "wb") as f:
         f.write(serialize_persistables(feed_vars, fetch_vars, executor, program, pnames))
 

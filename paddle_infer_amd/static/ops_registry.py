@@ -338,7 +338,8 @@ def _fc(ins, a):
     nc = a.get("in_num_col_dims", x.dim() - 1)
     x2 = x.reshape(int(np.prod(x.shape[:nc])), -1)
     act = a.get("activation_type", "")
-    if act in ("gelu", "relu", "silu", "gelu_tanh") and x2.is_cuda and x2.dtype == torch.bfloat16:
+    if act in ("gelu", "relu", "silu", "gelu_tanh") and x2.is_cuda and x2.dtype in (torch.bfloat16,
+                                                                                    torch.float16):
         from ..ops.linear import linear_bias_act
         y = linear_bias_act(x2, w, b, act) if b is not None else ops.bias_act(linear(x2, w, None), b, act)
     else:
@@ -361,18 +362,7 @@ def _flash_packed(ins, a):
     from .. import ops
     qkv = ins["QKV"][0]
     return {"Out": ops.flash_attention_packed(qkv, a["num_heads"], a.get("num_kv_heads") or a["num_heads"],
-                                              causal=bool(a.get("causal", False)))}
-
-
-@register("flash_attn")
-def _flash(ins, a):
-    from .. import ops
-    q, k, v = ins["Q"][0], ins["K"][0], ins["V"][0]
-    bhsd = a.get("layout", "bshd") == "bhsd"
-    if bhsd:
-        q, k, v = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
-    o = ops.flash_attention(q, k, v, causal=bool(a.get("causal", False)), scale=a.get("scale"))
-    return {"Out": o.transpose(1, 2) if bhsd else o}
+                                              causal=bool(a.get("causal", False)), scale=a.get("scale"))}
 
 
 @register("fused_embedding_eltwise_layernorm")
@@ -387,3 +377,220 @@ def _emb_ln(ins, a):
         e = F.embedding(ids, w)
         acc = e if acc is None else acc + e
     return {"Out": ops.layer_norm(acc, ins["Scale"][0], ins["Bias"][0], a.get("epsilon", 1e-5))}
+
+
+# ---------------------------------------------------------------- ops emitted by lowering.py
+for _name, _f in [("greater_equal", torch.ge), ("greater_than", torch.gt), ("less_equal", torch.le),
+                  ("less_than", torch.lt), ("equal", torch.eq), ("not_equal", torch.ne),
+                  ("logical_and", torch.logical_and), ("logical_or", torch.logical_or),
+                  ("logical_xor", torch.logical_xor)]:
+    register(_name)(lambda ins, a, _f=_f: {"Out": _f(ins["X"][0], _bcast(ins["X"][0], ins["Y"][0], a.get("axis", -1)))})
+
+for _name, _f in [("logical_not", torch.logical_not), ("reciprocal", torch.reciprocal),
+                  ("sin", torch.sin), ("cos", torch.cos), ("erf", torch.erf)]:
+    register(_name)(lambda ins, a, _f=_f: {"Out": _f(ins["X"][0])})
+
+
+@register("where")
+def _where(ins, a):
+    return {"Out": torch.where(ins["Condition"][0].bool(), ins["X"][0], ins["Y"][0])}
+
+
+@register("fill_any_like")
+def _fill_any_like(ins, a):
+    x = ins["X"][0]
+    dt = a.get("dtype", -1)
+    dt = x.dtype if dt in (-1, None) else _dt(dt)
+    return {"Out": torch.full_like(x, a.get("value", 0.0), dtype=dt)}
+
+
+@register("shape")
+def _shape(ins, a):
+    x = ins["Input"][0]
+    return {"Out": torch.tensor(list(x.shape), dtype=torch.int32, device=x.device)}
+
+
+@register("expand_v2")
+def _expand_v2(ins, a):
+    x = ins["X"][0]
+    shape = list(a.get("shape", []))
+    off = len(shape) - x.dim()
+    shape = [x.shape[i - off] if s == -1 else s for i, s in enumerate(shape)]
+    return {"Out": x.expand(shape)}
+
+
+@register("expand_as_v2")
+def _expand_as_v2(ins, a):
+    x = ins["X"][0]
+    if ins.get("Y"):
+        return {"Out": x.expand_as(ins["Y"][0])}
+    return {"Out": x.expand(a["target_shape"])}
+
+
+@register("stack")
+def _stack(ins, a):
+    return {"Y": torch.stack(ins["X"], a.get("axis", 0))}
+
+
+@register("pow")
+def _pow(ins, a):
+    return {"Out": torch.pow(ins["X"][0], a.get("factor", 1.0))}
+
+
+@register("strided_slice")
+def _strided_slice(ins, a):
+    x = ins["Input"][0]
+    sl = [slice(None)] * x.dim()
+    for ax, s, e, st in zip(a["axes"], a["starts"], a["ends"], a["strides"]):
+        sl[ax] = slice(s, min(e, x.shape[ax]) if e > 0 else e, st)
+    out = x[tuple(sl)]
+    for ax in sorted(a.get("decrease_axis", []) or [], reverse=True):
+        out = out.squeeze(ax)
+    return {"Out": out}
+
+
+@register("fused_softmax_mask")
+def _fsm(ins, a):
+    from .. import ops
+    x, m = ins["X"][0], ins["Mask"][0]
+    if m.dim() == x.dim() and m.shape != x.shape:
+        m = m.expand_as(x).contiguous()
+    return {"Out": ops.fused_softmax_mask(x, m)}
+
+
+@register("fused_softmax_mask_upper_triangle")
+def _fsm_tri(ins, a):
+    from .. import ops
+    return {"Out": ops.fused_softmax_mask(ins["X"][0], None, 1.0, causal=True)}
+
+
+def _flash_slots(ins, *names):
+    for n in names:
+        if ins.get(n):
+            return ins[n][0]
+    return None
+
+
+@register("flash_attn")
+def _flash_attn(ins, a):
+    """Reference `ops.yaml: flash_attn` (q, k, v [B, S, H, D], optional attn_mask; dropout /
+    causal / is_test attrs) — also the [B, H, S, D] ``layout`` form self_attention_fuse_pass emits."""
+    from .. import ops
+    q, k, v = (_flash_slots(ins, n, n.upper()) for n in ("q", "k", "v"))
+    mask = _flash_slots(ins, "attn_mask")
+    bhsd = a.get("layout", "bshd") == "bhsd"
+    if bhsd:
+        q, k, v = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
+    p = 0.0 if a.get("is_test", True) else float(a.get("dropout", 0.0))
+    o = ops.flash_attention(q, k, v, causal=bool(a.get("causal", False)), scale=a.get("scale"),
+                            attn_mask=mask, dropout_p=p)
+    o = o.transpose(1, 2) if bhsd else o
+    return {"out": o, "Out": o}
+
+
+@register("weight_only_linear")
+def _wol(ins, a):
+    from .. import ops
+    b = ins["bias"][0] if ins.get("bias") else None
+    return {"out": ops.weight_only_linear(ins["x"][0], ins["weight"][0], b, ins["weight_scale"][0],
+                                          a.get("weight_dtype", "int8"), a.get("act_method", "none"))}
+
+
+# ---------------------------------------------------------------- LLM / BERT fused inference ops
+def _seq(ins, slot):
+    return list(ins.get(slot) or [])
+
+
+def _fmt_common(ins, a):
+    """Slot → functional-argument mapping shared by the fused_multi_transformer variants
+    (reference `fused_multi_transformer_op.cc:152-190`)."""
+    time_step = None
+    if ins.get("TimeStep"):
+        ts = ins["TimeStep"][0]
+        time_step = int(ts.reshape(-1)[0].item()) if ts.numel() == 1 else ts
+    return dict(pre_layer_norm=bool(a.get("pre_layer_norm", True)), epsilon=float(a.get("epsilon", 1e-5)),
+                cache_kvs=_seq(ins, "CacheKV") or None,
+                beam_offset=ins["BeamCacheOffset"][0] if ins.get("BeamCacheOffset") else None,
+                seq_lens=ins["SeqLengths"][0] if ins.get("SeqLengths") else None,
+                time_step=time_step, attn_mask=ins["SrcMask"][0] if ins.get("SrcMask") else None,
+                activation=a.get("act_method", "gelu"), trans_qkvw=bool(a.get("trans_qkvw", True)),
+                rotary_emb_dims=int(a.get("rotary_emb_dims", 0)), causal=bool(a.get("causal", False)))
+
+
+@register("fused_multi_transformer")
+def _fused_multi_transformer(ins, a):
+    """Reference `fused_multi_transformer_op.cc` / `.cu`: X, LnScale/LnBias, QKVW/QKVBias,
+    OutLinearW/Bias, FFNLnScale/Bias, FFN1Weight/Bias, FFN2Weight/Bias (one entry per layer),
+    optional CacheKV (updated in place → CacheKVOut), TimeStep (decode), SrcMask, SeqLengths."""
+    from ..incubate.nn import functional as IF
+    kw = _fmt_common(ins, a)
+    out = IF.fused_multi_transformer(
+        ins["X"][0], _seq(ins, "LnScale"), _seq(ins, "LnBias"), _seq(ins, "QKVW"), _seq(ins, "QKVBias"),
+        _seq(ins, "OutLinearW"), _seq(ins, "OutLinearBias"), _seq(ins, "FFNLnScale"),
+        _seq(ins, "FFNLnBias"), _seq(ins, "FFN1Weight"), _seq(ins, "FFN1Bias"), _seq(ins, "FFN2Weight"),
+        _seq(ins, "FFN2Bias"), dropout_rate=0.0, training=False,
+        num_kv_heads=a.get("num_kv_heads") or None, **kw)
+    y, caches = (out if isinstance(out, tuple) else (out, None))
+    return {"Out": y, "CacheKVOut": caches or []}
+
+
+@register("fused_multi_transformer_weight_only")
+def _fused_multi_transformer_wo(ins, a):
+    """Reference `fused_multi_transformer_weight_only_op.cu`: the same slots plus the per-channel
+    *WScale / *WeightScale inputs; weights packed int8 ([N, K]) or int4 ([N/2, K])."""
+    from ..incubate.nn import functional as IF
+    kw = _fmt_common(ins, a)
+    kw.pop("trans_qkvw")
+    out = IF.fused_multi_transformer_weight_only(
+        ins["X"][0], _seq(ins, "LnScale"), _seq(ins, "LnBias"), _seq(ins, "QKVW"), _seq(ins, "QKVWScale"),
+        _seq(ins, "QKVBias"), _seq(ins, "OutLinearW"), _seq(ins, "OutLinearWScale"),
+        _seq(ins, "OutLinearBias"), _seq(ins, "FFNLnScale"), _seq(ins, "FFNLnBias"),
+        _seq(ins, "FFN1Weight"), _seq(ins, "FFN1WeightScale"), _seq(ins, "FFN1Bias"),
+        _seq(ins, "FFN2Weight"), _seq(ins, "FFN2WeightScale"), _seq(ins, "FFN2Bias"),
+        weight_dtype=a.get("weight_dtype", "int8"), num_heads=a.get("num_heads"),
+        num_kv_heads=a.get("num_kv_heads") or None, **kw)
+    y, caches = (out if isinstance(out, tuple) else (out, None))
+    return {"Out": y, "CacheKVOut": caches or []}
+
+
+@register("multihead_matmul")
+def _multihead_matmul(ins, a):
+    """Reference `fused/multihead_matmul_op.cu`: Input [B, S, E] · W [E, 3, E] + Bias [3, E],
+    attention with the additive BiasQK mask ([B, H|1, S, S]), alpha-scaled; Out [B, S, E]."""
+    from .. import ops
+    from ..ops.linear import linear
+    x, w, bias = ins["Input"][0], ins["W"][0], ins["Bias"][0]
+    B, S, E = x.shape
+    H = int(a["head_number"])
+    D = E // H
+    qkv = linear(x.reshape(B * S, E), w.reshape(E, 3 * E), bias.reshape(3 * E)).reshape(B, S, 3, H, D)
+    qkv = qkv.reshape(B, S, 3 * H, D)
+    mask = ins["BiasQK"][0] if ins.get("BiasQK") else None
+    scale = float(a.get("alpha", 1.0 / D ** 0.5))
+    if mask is None:
+        o = ops.flash_attention_packed(qkv, H, H, causal=False, scale=scale)
+    else:
+        o = ops.flash_attention(qkv[:, :, :H], qkv[:, :, H:2 * H], qkv[:, :, 2 * H:], False, scale,
+                                attn_mask=mask)
+    return {"Out": o.reshape(B, S, E)}
+
+
+@register("fused_fc_elementwise_layernorm")
+def _fc_eltwise_ln(ins, a):
+    """Reference `fused/fused_fc_elementwise_layernorm_op.cu`:
+    Out = LN(fc(X, W, Bias0) + Y; Scale, Bias1), fc flattening at x_num_col_dims."""
+    from .. import ops
+    from ..ops.linear import linear
+    x, w, y = ins["X"][0], ins["W"][0], ins["Y"][0]
+    b0 = ins["Bias0"][0] if ins.get("Bias0") else None
+    nc = int(a.get("x_num_col_dims", x.dim() - 1))
+    x2 = x.reshape(int(np.prod(x.shape[:nc])), -1)
+    h = linear(x2, w, b0).reshape(*x.shape[:nc], -1)
+    if a.get("activation_type") == "relu":
+        h = F.relu(h)
+    out, _ = ops.fused_add_layer_norm(h, y, ins["Scale"][0] if ins.get("Scale") else None,
+                                      ins["Bias1"][0] if ins.get("Bias1") else None,
+                                      float(a.get("epsilon", 1e-5)), None, 0.0, False)
+    return {"Out": out}
+
+

@@ -33,7 +33,7 @@ def test_jit_save_load_round_trip(tmp_path):
     torch.testing.assert_close(loaded(x), ref)
     assert loaded(torch.randn(7, 8)).shape == (7, 4)  # symbolic batch dim
     types = [op.type for op in loaded.program().global_block().ops]
-    assert "layer_norm" in types and "linear" in types
+    assert "layer_norm" in types and "matmul_v2" in types and "linear" not in types  # Paddle op types only
 
 
 def test_to_static_layer_and_function():

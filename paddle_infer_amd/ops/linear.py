@@ -39,7 +39,8 @@ def bump_param_epoch():
 
 
 def transposed(w):
-    """Cached contiguous ``wᵀ`` (bf16 2-D CUDA weights), refreshed when the parameter changed."""
+    """Cached contiguous ``wᵀ`` (bf16 / fp16 2-D CUDA weights; the HIP transpose moves 16-bit
+    words, so it serves both), refreshed when the parameter changed."""
     key = (_PARAM_EPOCH[0], w._version)
     c = getattr(w, "_piamd_t", None)
     if c is not None and c[0] == key:
@@ -56,8 +57,8 @@ def transposed(w):
 
 
 def _use_transposed(x2, w):
-    return (x2.is_cuda and w.dim() == 2 and w.dtype == torch.bfloat16 and x2.dtype == w.dtype
-            and x2.shape[0] >= TRANSPOSED_MIN_ROWS and w.is_contiguous())
+    return (x2.is_cuda and w.dim() == 2 and w.dtype in (torch.bfloat16, torch.float16)
+            and x2.dtype == w.dtype and x2.shape[0] >= TRANSPOSED_MIN_ROWS and w.is_contiguous())
 
 
 class _LinearFn(torch.autograd.Function):
@@ -136,7 +137,7 @@ def colsum_into(x2, out, accumulate=True):
     rows, N = x2.shape
     G = max(1, min(256, rows // 16))
     part = torch.empty((G, N), device=x2.device, dtype=torch.float32)
-    _lib.call("piamd_colsum", _lib.dtype_code(x2), x2.data_ptr(), out.data_ptr(), part.data_ptr(),
+    _lib.call("piamd_colsum", _lib.dtype_code(x2, fp16=True), x2.data_ptr(), out.data_ptr(), part.data_ptr(),
               G, rows, N, int(accumulate), _lib.stream())
 
 
@@ -154,6 +155,8 @@ def linear(x, weight, bias=None):
     shp = x.shape
     x2 = x.reshape(-1, shp[-1])
     if not _use_transposed(x2, weight):
+        if bias is not None and bias.dtype == x2.dtype and x2.dim() == 2:
+            return torch.addmm(bias, x2, weight).view(*shp[:-1], weight.shape[1])
         y = torch.matmul(x, weight)
         return y + bias if bias is not None else y
     wf = transposed(weight).t()

@@ -189,7 +189,12 @@ class Executor:
                     p.grad = None
             return
         if op.func is None:  # a Paddle-typed op loaded from a foreign .pdmodel
-            run_paddle_op(op, sub, env, scope)
+            from . import ops_registry
+            ops_registry.DEVICE.append(self.device)
+            try:
+                run_paddle_op(op, sub, env, scope)
+            finally:
+                ops_registry.DEVICE.pop()
             return
         args = tree_map(sub, op.args)
         kwargs = tree_map(sub, op.kwargs)

@@ -17,6 +17,7 @@ from . import proto
 from .framework import VarRef
 
 REGISTRY = {}
+DEVICE = [torch.device("cpu")]  # device of the running Executor (creation ops allocate there)
 
 
 def register(*names):
@@ -291,7 +292,8 @@ def _lookup(ins, a):
 
 @register("fill_constant")
 def _fill(ins, a):
-    return {"Out": torch.full(a.get("shape", [1]), a.get("value", 0.0), dtype=_dt(a.get("dtype", 5)))}
+    return {"Out": torch.full(a.get("shape", [1]), a.get("value", 0.0), dtype=_dt(a.get("dtype", 5)),
+                              device=DEVICE[-1])}
 
 
 for _name, _f in [("reduce_mean", torch.mean), ("reduce_sum", torch.sum), ("reduce_max", torch.amax),

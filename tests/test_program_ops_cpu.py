@@ -91,8 +91,8 @@ def run_fmt_wire(tmp_path, device):
     create_predictor vs the dygraph FusedMultiTransformer with the same weights and caches."""
     from paddle_infer_amd.incubate.nn import FusedMultiTransformer
     torch.manual_seed(0)
-    E, H, L, B, S, MAXS = 64, 4, 2, 2, 8, 16
-    layer = FusedMultiTransformer(E, H, 128, num_layers=L)
+    E, H, L, B, S, MAXS = (64, 4, 2, 2, 8, 16) if device == "cpu" else (256, 4, 2, 2, 8, 16)
+    layer = FusedMultiTransformer(E, H, 2 * E, num_layers=L)
     layer.eval()
     ctx_p, dec_p = str(tmp_path / "ctx"), str(tmp_path / "dec")
     write_fmt_program(layer, ctx_p, False, L, E)

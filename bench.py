@@ -9,9 +9,16 @@ JSON line. Synthetic token ids and random-init weights of the real GPT-3 1.3B ar
 master weights + AdamW states; every timed step is a full forward + backward + gradient
 collectives + optimizer update.
 
-Parallelism: ``--tp`` model-parallel degree (default 1), the rest data-parallel with ZeRO-1
-sharded optimizer states (``--sharding 1``; 0 = plain all-reduce DP). Weak scaling: the
-per-GPU micro batch is fixed as N grows.
+Everything goes through the Fleet API users call: ``fleet.init`` (hybrid_configs dp / mp / pp /
+sharding degrees) → ``fleet.distributed_model`` → ``fleet.distributed_optimizer(paddle AdamW +
+ClipGradByGlobalNorm)``; on the GPU the optimizer is the fused flat-buffer engine (bucketed
+reduce-scatter / all-reduce overlapped with backward, one AdamW launch per parameter group).
+
+Parallelism: ``--tp`` model-parallel degree, ``--pp`` pipeline degree (GPTForPretrainingPipe,
+1F1B; ``--vpp`` virtual chunks per rank = interleaved 1F1B; ``--accumulate`` micro-batches per
+step), ``--sharding-degree`` a separate ZeRO axis (the rest is dp), ``--sharding`` ZeRO stage on
+that axis (default 1 over dp: sharded optimizer states; 3 = group_sharded_parallel p_g_os, dp only).
+Weak scaling: the per-GPU micro batch is fixed as N grows.
 """
 from __future__ import annotations
 
@@ -34,13 +41,19 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="gpt3-1.3b")
     ap.add_argument("--seq", type=int, default=1024)
+    ap.add_argument("--num-layers", type=int, default=0, help="override the model's layer count (rehearsals)")
     ap.add_argument("--micro-batch", type=int, default=64,
                     help="sequences per data-parallel rank (64 x 1024 tokens: ~140 GB of the "
                          "288 GB HBM3E; amortises the optimizer step and the gradient collectives: "
                          "124.3k / 125.5k / 126.3k tok/s at 32 / 48 / 64 on one MI355X; at 8 GPUs "
                          "the global batch is 512 x 1024 = 0.5M tokens, GPT-3 1.3B used 1M)")
     ap.add_argument("--tp", type=int, default=1)
-    ap.add_argument("--sharding", type=int, default=1)
+    ap.add_argument("--pp", type=int, default=1)
+    ap.add_argument("--vpp", type=int, default=1, help="virtual pipeline chunks per rank (interleaved 1F1B)")
+    ap.add_argument("--accumulate", type=int, default=0,
+                    help="pipeline micro-batches per step (default 2 x pp); --micro-batch is split")
+    ap.add_argument("--sharding-degree", type=int, default=1)
+    ap.add_argument("--sharding", type=int, default=1, help="ZeRO stage (0 = plain all-reduce DP)")
     ap.add_argument("--bucket-mb", type=int, default=256)
     ap.add_argument("--dropout", type=float, default=0.1)
     ap.add_argument("--recompute", action="store_true")
@@ -78,40 +91,76 @@ def main():
     import paddle_infer_amd as pia
     from paddle_infer_amd.incubate import autotune
     tuned = autotune.use_tuned_gemms() if args.tuned_gemm else False
-    from paddle_infer_amd.models.gpt import GPTForPretraining, gpt_config, gpt_flops_per_token
-    from paddle_infer_amd.parallel.flat_engine import FlatTrainer
-    from paddle_infer_amd.distributed.fleet.topology import local_topology, HybridCommunicateGroup
+    from paddle_infer_amd.distributed import fleet
+    from paddle_infer_amd.models.gpt import (GPTForPretraining, GPTForPretrainingPipe, gpt_config,
+                                             gpt_flops_per_token)
     from paddle_infer_amd.framework import random as prand
 
-    tp = args.tp
-    assert world % tp == 0
-    dp = world // tp
-    hcg = HybridCommunicateGroup(local_topology(dp=dp, mp=tp))
-    mp_group = hcg.get_model_parallel_group()
-    dp_group = hcg.get_data_parallel_group()
-    prand.model_parallel_random_seed(1234, hcg.get_model_parallel_rank(), 0)
+    tp, pp, shd = args.tp, args.pp, args.sharding_degree
+    assert world % (tp * pp * shd) == 0, f"world {world} not divisible by tp*pp*sharding"
+    dp = world // (tp * pp * shd)
+    strategy = fleet.DistributedStrategy()
+    strategy.hybrid_configs = {"dp_degree": dp, "mp_degree": tp, "pp_degree": pp,
+                               "sharding_degree": shd}
+    stage3 = args.sharding == 3
+    if args.sharding and not stage3:
+        strategy.sharding = shd == 1 and dp > 1
+        strategy.sharding_configs = {"stage": args.sharding}
+    strategy.fuse_grad_size_in_MB = args.bucket_mb
+    acc = args.accumulate or (2 * pp if pp > 1 else 1)
+    acc = max(1, min(acc, args.micro_batch))
+    assert args.micro_batch % acc == 0, "--micro-batch must split into --accumulate micro-batches"
+    strategy.pipeline_configs = {"accumulate_steps": acc, "micro_batch_size": max(1, args.micro_batch // acc)}
+    fleet.init(is_collective=True, strategy=strategy)
+    hcg = fleet.get_hybrid_communicate_group()
+    mp_group = hcg.get_model_parallel_group() if tp > 1 else None
+    prand.model_parallel_random_seed(1234, hcg.get_model_parallel_rank(), hcg.get_stage_id())
 
+    over = {"num_layers": args.num_layers} if args.num_layers else {}
     cfg = gpt_config(args.model, max_position_embeddings=max(args.seq, 1024),
-                     hidden_dropout_prob=args.dropout, recompute=args.recompute)
+                     hidden_dropout_prob=args.dropout, recompute=args.recompute, **over)
     with torch.device(device):
-        model = GPTForPretraining(cfg, mp_group=mp_group)
-    model.train()
-    trainer = FlatTrainer(model, lr=1e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1,
-                          grad_clip=1.0, dp_group=dp_group, mp_group=mp_group,
-                          sharding_stage=args.sharding, bucket_mb=args.bucket_mb)
-    n_params = trainer.num_params()
+        if pp > 1:
+            net = GPTForPretrainingPipe(cfg, mp_group=mp_group,
+                                        num_virtual_pipeline_stages=args.vpp if args.vpp > 1 else None)
+        else:
+            net = GPTForPretraining(cfg, mp_group=mp_group)
+    net.train()
+    decay = {getattr(p, "pd_name", None) for p in net.parameters() if p.dim() > 1}
+    opt = pia.optimizer.AdamW(learning_rate=1e-4, beta1=0.9, beta2=0.95, epsilon=1e-8,
+                              parameters=list(net.parameters()), weight_decay=0.1,
+                              grad_clip=pia.nn.ClipGradByGlobalNorm(1.0),
+                              apply_decay_param_fun=lambda n: n in decay)
+    if stage3:
+        from paddle_infer_amd.distributed.sharding import group_sharded_parallel
+        assert pp == 1 and tp == 1, "--sharding 3 is data-parallel ZeRO-3 (group_sharded_parallel)"
+        model, opt, _ = group_sharded_parallel(net, opt, "p_g_os", group=hcg.get_data_parallel_group())
+    else:
+        model = fleet.distributed_model(net)
+        opt = fleet.distributed_optimizer(opt)
+    n_params = sum(p.numel() for p in net.parameters())
+    if world > 1 and not stage3:
+        t = torch.tensor([n_params], device=device, dtype=torch.float64)
+        if pp > 1:  # each stage holds its own layers (a tied table counted on both ends)
+            dist.all_reduce(t, group=hcg.get_pipe_parallel_group())
+        if tp > 1:
+            dist.all_reduce(t, group=hcg.get_model_parallel_group())
+        n_params = int(t.item())
 
     mb, S = args.micro_batch, args.seq
     gen = torch.Generator(device=device)
-    gen.manual_seed(1000 + hcg.get_data_parallel_rank())
+    gen.manual_seed(1000 + hcg.get_data_parallel_rank() * shd + hcg.get_sharding_parallel_rank())
     ids = torch.randint(0, cfg.vocab_size, (mb, S + 1), device=device, generator=gen)
     x, y = ids[:, :-1].contiguous(), ids[:, 1:].contiguous()
+    flat = getattr(opt, "_flat", None)
 
     def step():
-        trainer.zero_grad()
+        if pp > 1:
+            return model.train_batch([x, y], opt)
         loss = model(x, labels=y)
         loss.backward()
-        trainer.step()
+        opt.step()
+        opt.clear_grad()
         return loss
 
     for _ in range(args.warmup):
@@ -123,7 +172,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
-    trainer.wait_params()
+    if flat is not None:
+        flat.wait_params()
     sync()
     if world > 1:
         dist.barrier()
@@ -135,12 +185,14 @@ def main():
         elapsed = float(t.item())
     final_loss = float(loss.item())
 
-    tokens = args.steps * dp * mb * S
+    tokens = args.steps * dp * shd * mb * S
     tps = tokens / elapsed
     ms = elapsed / args.steps * 1e3
     flops_tok = gpt_flops_per_token(cfg, S)
     tflops_gpu = tps * flops_tok / world / 1e12
-    par = (f"tp{tp}" if tp > 1 else "") + f"dp{dp}" + (f"_sharding{args.sharding}" if dp > 1 and args.sharding else "")
+    par = ((f"tp{tp}" if tp > 1 else "") + (f"pp{pp}" if pp > 1 else "") + (f"v{args.vpp}" if args.vpp > 1 else "")
+           + (f"sh{shd}" if shd > 1 else "") + f"dp{dp}"
+           + (f"_zero{args.sharding}" if (dp * shd > 1 and args.sharding) else ""))
     if rank == 0:
         print(json.dumps({
             "metric": METRIC if args.model == "gpt3-1.3b" else f"tokens/sec {args.model} training",
@@ -149,10 +201,13 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (random token ids, random-init weights)",
             "config": {"model": "GPT-3 1.3B" if args.model == "gpt3-1.3b" else args.model,
-                       "global_batch": dp * mb, "seq_len": S, "parallelism": par,
+                       "global_batch": dp * shd * mb, "seq_len": S, "parallelism": par,
                        "micro_batch_per_dp_rank": mb, "params": n_params,
                        "hidden_dropout": args.dropout, "attention_dropout": 0.0,
-                       "optimizer": "AdamW fp32 master", "grad_clip": 1.0},
+                       "optimizer": "AdamW fp32 master", "grad_clip": 1.0,
+                       "api": "fleet.init/distributed_model/distributed_optimizer" if not stage3
+                       else "group_sharded_parallel(p_g_os)",
+                       **({"pp_micro_batches": acc} if pp > 1 else {})},
             "tflops_per_gpu": round(tflops_gpu, 1), "final_loss": round(final_loss, 4),
             "tuned_gemm_table": bool(tuned),
             "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1) if on_gpu else None,

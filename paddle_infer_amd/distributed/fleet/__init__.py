@@ -200,16 +200,20 @@ def distributed_model(model):
         return model
     st = _strategy()
     _STATE["model"] = model
+    _STATE["wrapper"] = None
     if isinstance(model, PipelineLayer) and hcg.get_pipe_parallel_world_size() > 1:
-        return PipelineParallel(model, hcg, st)
-    if hcg.get_model_parallel_world_size() > 1 or hcg.get_sharding_parallel_world_size() > 1 or st.sharding:
-        return _HybridModel(model, hcg)
-    if hcg.get_data_parallel_world_size() > 1:
+        w = PipelineParallel(model, hcg, st)
+    elif hcg.get_model_parallel_world_size() > 1 or hcg.get_sharding_parallel_world_size() > 1 or st.sharding:
+        w = _HybridModel(model, hcg)
+    elif hcg.get_data_parallel_world_size() > 1:
         from ..parallel import DataParallel
-        return DataParallel(model, group=hcg.get_data_parallel_group(),
-                            comm_buffer_size=st.fuse_grad_size_in_MB,
-                            find_unused_parameters=st.find_unused_parameters)
-    return model
+        w = DataParallel(model, group=hcg.get_data_parallel_group(),
+                         comm_buffer_size=st.fuse_grad_size_in_MB,
+                         find_unused_parameters=st.find_unused_parameters)
+    else:
+        return model
+    _STATE["wrapper"] = w
+    return w
 
 
 def _partition(params, n):
@@ -249,24 +253,34 @@ class HybridParallelOptimizer:
         sh_g = hcg.get_sharding_parallel_group() if hcg else None
         self._owner = None
         inner_flat = getattr(optimizer, "_flat", None)
-        if inner_flat is not None:  # rebuild the fused engine with the hybrid groups
+        if inner_flat is not None or getattr(optimizer, "_flat_pending", False):
+            # the fused flat-buffer engine, built on the hybrid groups
             from ...parallel.flat_engine import FlatTrainer
-            old = inner_flat
             named = [(getattr(p, "pd_name", str(i)), p) for i, p in enumerate(optimizer._parameter_list)]
             stage = int(strategy.sharding_configs.get("stage", 1))
             if self._sh > 1:
                 shard_g, rep_g, st = sh_g, (dp_g if self._dp > 1 else None), stage
             else:
                 shard_g, rep_g, st = dp_g, None, (stage if strategy.sharding else 0)
+            # pipeline micro-batches accumulate into the grad buffer: reduce once, at step()
+            pp_acc = hcg.get_pipe_parallel_world_size() > 1 or \
+                int((strategy.pipeline_configs or {}).get("accumulate_steps", 1)) > 1
+            apply = getattr(optimizer, "_apply_decay_param_fun", None)
+            wd = optimizer._decay_coeff() if getattr(optimizer, "_decoupled", False) else 0.0
+            clip = getattr(optimizer._grad_clip, "clip_norm", None)
             self._flat = FlatTrainer(_STATE.get("model"), lr=optimizer.get_lr(),
-                                     betas=(old.beta1, old.beta2), eps=old.eps,
-                                     weight_decay=old.groups[0].weight_decay,
-                                     grad_clip=old.grad_clip, dp_group=shard_g,
+                                     betas=(optimizer._beta1, optimizer._beta2), eps=optimizer._epsilon,
+                                     weight_decay=wd, grad_clip=clip, dp_group=shard_g,
                                      replica_group=rep_g,
                                      mp_group=hcg.get_model_parallel_group(),
                                      pp_group=hcg.get_pipe_parallel_group(), sharding_stage=st,
-                                     named_params=named, bucket_mb=strategy.fuse_grad_size_in_MB)
-            optimizer._flat = self._flat
+                                     named_params=named, bucket_mb=strategy.fuse_grad_size_in_MB,
+                                     overlap=not pp_acc,
+                                     no_decay_fn=(lambda n, p: not apply(n)) if apply else (lambda n, p: False))
+            optimizer._flat, optimizer._flat_pending = self._flat, False
+            wrapper = _STATE.get("wrapper")
+            if hasattr(wrapper, "_detach_reducer"):  # the flat engine reduces the dp gradients
+                wrapper._detach_reducer()
         elif self._sh > 1:
             self._owner = _partition([p for p in optimizer._parameter_list if p.requires_grad],
                                      self._sh)
@@ -305,6 +319,8 @@ class HybridParallelOptimizer:
             if p.grad is None:
                 continue
             dev = p.grad.device
+            if getattr(p, "is_firstly_shared", True) is False:
+                continue  # a pipeline-shared weight's other copy: counted on its first stage
             s = p.grad.float().pow(2).sum()
             if getattr(p, "is_distributed", False):
                 dist_sq = s if dist_sq is None else dist_sq + s

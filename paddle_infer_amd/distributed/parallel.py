@@ -114,12 +114,26 @@ class DataParallel(torch.nn.Module):
                     views.append((p, v))
                     off += p.numel()
                 self._flat.append((flat, views))
+        self._hook_handles = []
         for fi, (flat, views) in enumerate(self._flat):
             for p, v in views:
                 p.grad = v
                 p._dp_bucket = fi
-                p.register_post_accumulate_grad_hook(self._hook)
+                self._hook_handles.append(p.register_post_accumulate_grad_hook(self._hook))
         self._reset()
+
+    def _detach_reducer(self):
+        """Hand gradient reduction to another engine (the flat-buffer optimizer of
+        fleet.distributed_optimizer): remove the hooks and buckets of this reducer."""
+        for h in getattr(self, "_hook_handles", []):
+            h.remove()
+        self._hook_handles = []
+        for flat, views in getattr(self, "_flat", []):
+            for p, _ in views:
+                if hasattr(p, "_dp_bucket"):
+                    del p._dp_bucket
+        self._flat, self._buckets = [], []
+        self._pending, self._launched, self._handles = {}, set(), []
 
     def _reset(self):
         self._pending = {fi: len(views) for fi, (_, views) in enumerate(self._flat)}

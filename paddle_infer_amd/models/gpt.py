@@ -160,6 +160,10 @@ class GPTDecoderLayer(Layer):
         y, h = fused_add_layer_norm(a, h, self.ln2.weight, self.ln2.bias, eps,
                                     self.attn.out_proj.bias, p, self.training)
         m = self.mlp(y)
+        if getattr(self, "_zero3", False):
+            # ZeRO-3 frees this layer's weights after its forward: fold the row-parallel bias here
+            # instead of deferring it into the NEXT layer's LN kernel (another shard unit)
+            return h, m + self.mlp.fc2.bias, None
         return h, m, self.mlp.fc2.bias
 
 
@@ -240,7 +244,7 @@ class GPTModel(Layer):
                 # well as torch's RNG, so the re-run draws the forward's dropout masks
                 from ..distributed.fleet.recompute import recompute
                 h, out = recompute(lambda hh, oo, bb, _l=layer: _l(hh, oo, bb)[:2], h, out, bias)
-                bias = layer.mlp.fc2.bias
+                bias = None if getattr(self, "_zero3", False) else layer.mlp.fc2.bias
             else:
                 h, out, bias = layer(h, out, bias)
         y, _ = fused_add_layer_norm(out, h, self.final_ln.weight, self.final_ln.bias,
@@ -258,6 +262,12 @@ class GPTForPretraining(Layer):
             self.lm_head = self.create_parameter(
                 [cfg.vocab_size // _mp_size(mp_group), cfg.hidden_size],
                 default_initializer=I.Normal(0.0, cfg.initializer_range))
+
+    @property
+    def _stage3_persistent(self):
+        """Modules whose weights are used outside their own forward (the tied LM head reads the word
+        table): ZeRO-3 keeps them gathered for the whole step."""
+        return ["gpt.embeddings.word_embeddings"] if self.cfg.tie_word_embeddings else []
 
     def head_weight(self):
         if self.cfg.tie_word_embeddings:
@@ -347,4 +357,121 @@ def merge_gpt_state_dicts(shards: list, cfg: GPTConfig) -> dict:
             out[k] = torch.cat(vs, dim=0)
         else:
             out[k] = vs[0]
+    return out
+
+
+# ----------------------------------------------------------------------------- pipeline form
+class GPTEmbeddingPipe(GPTEmbeddings):
+    """First pipeline layer: token + position embeddings. ``weight`` (the word table) is the
+    SharedLayerDesc attribute tied to the LM head on the last stage."""
+
+    @property
+    def weight(self):
+        return self.word_embeddings.weight
+
+    def forward(self, input_ids, position_ids=None):
+        return super().forward(input_ids, position_ids)
+
+
+class GPTDecoderLayerPipe(GPTDecoderLayer):
+    """Decoder layer whose input / output is ONE tensor (what a pipeline stage boundary carries):
+    the embeddings [B, S, h] (first layer) or the packed residual state [2, B, S, h] = (h, out).
+    The row-parallel fc2 bias, which the monolithic model folds into the NEXT layer's LN kernel, is
+    added to ``out`` here — the next layer may live on another stage."""
+
+    def forward(self, x):
+        if x.dim() == 3:
+            h, out = None, x
+        else:
+            h, out = x[0], x[1]
+        h2, m, b = super().forward(h, out, None)
+        return torch.stack([h2, m + b])
+
+
+class GPTFinalNormPipe(Layer):
+    def __init__(self, cfg: GPTConfig):
+        super().__init__(dtype=cfg.dtype)
+        self.cfg = cfg
+        self.final_ln = _LNParams(cfg)
+
+    def forward(self, x):
+        p = self.cfg.hidden_dropout_prob if self.training else 0.0
+        y, _ = fused_add_layer_norm(x[1], x[0], self.final_ln.weight, self.final_ln.bias,
+                                    self.cfg.layer_norm_eps, None, p, self.training)
+        return y
+
+
+class GPTLMHeadPipe(Layer):
+    """Untied LM head ([V_local, h])."""
+
+    def __init__(self, cfg: GPTConfig, mp_group=None):
+        super().__init__(dtype=cfg.dtype)
+        self.mp_group = mp_group
+        self.weight = self.create_parameter([cfg.vocab_size // _mp_size(mp_group), cfg.hidden_size],
+                                            default_initializer=I.Normal(0.0, cfg.initializer_range))
+
+    def forward(self, y):
+        return _LMHeadFn.apply(c_identity(y, self.mp_group), self.weight)
+
+
+def _tied_head(layer, y):
+    return _LMHeadFn.apply(c_identity(y, layer.word_embeddings.group), layer.weight)
+
+
+def gpt_pipe_descs(cfg: GPTConfig, mp_group=None):
+    """LayerDesc list of GPT for PipelineLayer: shared embedding, L decoder layers, final LN and the
+    (tied: SharedLayerDesc on the embedding table; untied: own weight) LM head."""
+    from ..distributed.fleet.pipeline import LayerDesc, SharedLayerDesc
+    descs = [SharedLayerDesc("embed", GPTEmbeddingPipe, None, "weight", cfg, mp_group)]
+    descs += [LayerDesc(GPTDecoderLayerPipe, cfg, mp_group, i) for i in range(cfg.num_layers)]
+    descs.append(LayerDesc(GPTFinalNormPipe, cfg))
+    if cfg.tie_word_embeddings:
+        descs.append(SharedLayerDesc("embed", GPTEmbeddingPipe, _tied_head, "weight", cfg, mp_group))
+    else:
+        descs.append(LayerDesc(GPTLMHeadPipe, cfg, mp_group))
+    return descs
+
+
+def GPTForPretrainingPipe(cfg: GPTConfig, mp_group=None, num_stages=None, topology=None,
+                          num_virtual_pipeline_stages=None, recompute_interval=0):
+    """Reference `hybrid_parallel_pp_*.py` / PaddleNLP GPTForPretrainingPipe: GPT as a
+    PipelineLayer, decoder layers split evenly over ``num_stages`` x ``num_virtual_pipeline_stages``
+    chunks (seg_method ``layer:GPTDecoderLayerPipe``), loss = GPTPretrainingCriterion."""
+    from ..distributed.fleet.pipeline import PipelineLayer
+    return PipelineLayer(gpt_pipe_descs(cfg, mp_group), num_stages=num_stages, topology=topology,
+                         loss_fn=GPTPretrainingCriterion(mp_group), seg_method="layer:GPTDecoderLayerPipe",
+                         recompute_interval=recompute_interval,
+                         num_virtual_pipeline_stages=num_virtual_pipeline_stages)
+
+
+def gpt_pipe_load_full_state(pipe, full_state: dict, cfg: GPTConfig):
+    """Copy a (single-process) GPTForPretraining state dict into this rank's pipeline layers."""
+    with torch.no_grad():
+        for idx, lay in pipe._index_layers:
+            pre = _pipe_prefix(idx, cfg)
+            for n, p in lay.named_parameters():
+                p.copy_(full_state["lm_head" if pre is None else pre + n])
+
+
+def _pipe_prefix(idx, cfg: GPTConfig):
+    L = cfg.num_layers
+    if idx == 0 or (idx == L + 2 and cfg.tie_word_embeddings):
+        return "gpt.embeddings."
+    if idx <= L:
+        return f"gpt.layers.{idx - 1}."
+    if idx == L + 1:
+        return "gpt."
+    return None  # untied head: the "lm_head" parameter
+
+
+def gpt_pipe_state_to_full(pipe, cfg: GPTConfig) -> dict:
+    """This rank's pipeline parameters under their single-process GPTForPretraining names."""
+    out = {}
+    head = cfg.num_layers + 2
+    for idx, lay in pipe._index_layers:
+        pre = _pipe_prefix(idx, cfg)
+        for n, p in lay.named_parameters():
+            if idx == head and cfg.tie_word_embeddings and n != "word_embeddings.weight":
+                continue  # the tied head uses only the word table of its embedding copy
+            out["lm_head" if pre is None else pre + n] = p.detach().clone()
     return out

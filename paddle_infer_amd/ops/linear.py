@@ -58,7 +58,8 @@ def transposed(w):
 
 def _use_transposed(x2, w):
     return (x2.is_cuda and w.dim() == 2 and w.dtype in (torch.bfloat16, torch.float16)
-            and x2.dtype == w.dtype and x2.shape[0] >= TRANSPOSED_MIN_ROWS and w.is_contiguous())
+            and x2.dtype == w.dtype and x2.shape[0] >= TRANSPOSED_MIN_ROWS and w.is_contiguous()
+            and not getattr(w, "_piamd_no_t", False))
 
 
 class _LinearFn(torch.autograd.Function):

@@ -212,6 +212,12 @@ class Adam(Optimizer):
     def _maybe_flat(self, kw):
         if not self._flat_ok():
             return
+        from ..distributed import fleet as _fleet
+        if _fleet._STATE.get("hcg") is not None:
+            # fleet.distributed_optimizer builds the engine on the hybrid groups (building it here
+            # too would hold two copies of every fp32 master / moment buffer until then)
+            self._flat_pending = True
+            return
         from ..parallel.flat_engine import FlatTrainer
         wd = self._decay_coeff() if self._decoupled else 0.0
         apply = getattr(self, "_apply_decay_param_fun", None)

@@ -148,13 +148,17 @@ class FlatTrainer:
         dtype = named[0][1].dtype
         keyed = {}
         for n, p in named:
-            k = (not no_decay_fn(n, p), bool(getattr(p, "is_distributed", False)), str(p.dtype))
+            k = (not no_decay_fn(n, p), bool(getattr(p, "is_distributed", False)), str(p.dtype),
+                 getattr(p, "is_firstly_shared", True) is False)
             keyed.setdefault(k, []).append(p)
         bucket_numel = max(ALIGN * self.world, int(bucket_mb * 2 ** 20 // p.element_size()))
         self.groups = []
-        for (decay, distd, _dts), ps in sorted(keyed.items(), key=lambda kv: (not kv[0][0], kv[0][1], kv[0][2])):
+        for (decay, distd, _dts, dup), ps in sorted(keyed.items(),
+                                                    key=lambda kv: (not kv[0][0], kv[0][1], kv[0][2], kv[0][3])):
             g = _FlatGroup(ps, ps[0].dtype, device, self.world, bucket_numel,
-                           weight_decay if decay else 0.0, distd, f"decay{int(decay)}_dist{int(distd)}_{_dts.replace('torch.', '')}")
+                           weight_decay if decay else 0.0, distd,
+                           f"decay{int(decay)}_dist{int(distd)}_{_dts.replace('torch.', '')}" + ("_dup" if dup else ""))
+            g.dup = dup  # a pipeline-shared weight's non-first copy: excluded from the grad norm
             self.groups.append(g)
         # master weights + states: full (stage 0) or local shard (stage >= 1)
         for g in self.groups:
@@ -342,6 +346,8 @@ class FlatTrainer:
         nb = self._norm_buf
         nb.zero_()
         for g in self.groups:
+            if getattr(g, "dup", False):
+                continue
             sumsq(self._grads_for_update(g), out=nb[1 if g.distributed else 0], accumulate=True)
         scale = 1.0 / (self.world * self.replica)
         if self.world > 1 and self.sharding:

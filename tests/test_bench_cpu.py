@@ -1,7 +1,7 @@
 """The driver's multi-rank bench command, rehearsed on the CPU (gloo + the ops' CPU reference
 paths): ``python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`` must print
-exactly one JSON line from rank 0 with the contract's fields, for plain sharded DP and for a
-TP × DP mesh."""
+exactly one JSON line from rank 0 with the contract's fields — through the Fleet API for sharded DP,
+TP × DP, PP × DP (1F1B), interleaved PP, a sharding axis × DP, and ZeRO-3."""
 import json
 import os
 import socket
@@ -21,8 +21,15 @@ def _port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("n,extra,par", [(2, [], "dp2_sharding1"), (4, ["--tp", "2"], "tp2dp2_sharding1")])
-def test_bench_multirank_contract(n, extra, par):
+@pytest.mark.parametrize("n,extra,par,gb", [
+    (2, [], "dp2_zero1", 4),
+    (4, ["--tp", "2"], "tp2dp2_zero1", 4),
+    (4, ["--pp", "2"], "pp2dp2_zero1", 4),
+    (2, ["--pp", "2", "--vpp", "2", "--accumulate", "2", "--num-layers", "4"], "pp2v2dp1", 2),
+    (4, ["--sharding-degree", "2"], "sh2dp2_zero1", 8),
+    (2, ["--sharding", "3"], "dp2_zero3", 4),
+])
+def test_bench_multirank_contract(n, extra, par, gb):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", str(n), "--steps", "2", "--warmup", "1", "--device", "cpu", "--model", "gpt3-tiny",
@@ -36,5 +43,5 @@ def test_bench_multirank_contract(n, extra, par):
     assert KEYS <= set(out)
     assert out["n_gpus"] == n and out["steps"] == 2 and out["warmup"] == 1
     assert out["config"]["parallelism"] == par
-    assert out["config"]["global_batch"] == 2 * (n // (2 if extra else 1))
+    assert out["config"]["global_batch"] == gb
     assert out["value"] > 0 and out["final_loss"] == out["final_loss"]

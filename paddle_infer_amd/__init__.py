@@ -12,18 +12,21 @@ import torch as _torch  # noqa: F401  (must load before the HIP kernel library)
 
 from .framework import tensor_patch as _tensor_patch  # noqa: F401
 from .framework import random as _random
-from .framework.random import seed, get_rng_state, set_rng_state  # noqa: F401
+from .framework.random import seed, get_rng_state, set_rng_state, get_cuda_rng_state, set_cuda_rng_state  # noqa: F401,E501
 from .framework.dtype import (float32, float64, float16, bfloat16, int8, uint8, int16, int32,  # noqa: F401
-                              int64, bool_ as bool, set_default_dtype, get_default_dtype)
+                              int64, bool_ as bool, set_default_dtype, get_default_dtype,
+                              complex64, complex128, dtype, iinfo, finfo)
 from .framework.io import save, load  # noqa: F401
 from .framework import flags as _flags
 from .framework.flags import set_flags, get_flags  # noqa: F401
 from .tensor import *  # noqa: F401,F403
-from .tensor import Tensor, linalg  # noqa: F401
+from .tensor import Tensor  # noqa: F401
+from . import linalg  # noqa: F401
 from . import tensor  # noqa: F401
 from .device import (set_device, get_device, CPUPlace, CUDAPlace, CUDAPinnedPlace,  # noqa: F401
                      is_compiled_with_cuda, is_compiled_with_rocm, is_compiled_with_xpu,
-                     is_compiled_with_npu, is_compiled_with_cinn)
+                     is_compiled_with_npu, is_compiled_with_cinn, NPUPlace, XPUPlace,
+                     IPUPlace, MLUPlace)
 from . import device  # noqa: F401
 from . import ops  # noqa: F401
 from . import nn  # noqa: F401
@@ -35,6 +38,30 @@ from . import io  # noqa: F401
 from .nn import ParamAttr  # noqa: F401
 
 disable_static = lambda place=None: None  # noqa: E731  (dygraph is the default mode)
+
+
+class LazyGuard:
+    """Defer parameter materialisation (reference `fluid/lazy_init.py:LazyGuard`): layers built
+    inside the guard are created on the ``meta`` device; ``Layer.to(device)`` / ``to_empty`` or
+    loading a state dict materialises them."""
+
+    def __enter__(self):
+        self._ctx = _torch.device("meta")
+        self._ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        return self._ctx.__exit__(*exc)
+
+
+def set_printoptions(precision=None, threshold=None, edgeitems=None, sci_mode=None, linewidth=None):
+    _torch.set_printoptions(precision=precision, threshold=threshold, edgeitems=edgeitems,
+                            sci_mode=sci_mode, linewidth=linewidth)
+
+
+def disable_signal_handler():
+    """The reference unhooks its C++ fatal-signal handler; Python's defaults are already in place."""
+    return None
 
 
 def in_dynamic_mode():

@@ -45,6 +45,18 @@ CUDAPinnedPlace = CPUPlace
 XPUPlace = CUDAPlace
 
 
+def _no_device(kind):
+    def place(idx=0):
+        raise RuntimeError(f"{kind} is not available: this framework targets MI355X (HIP) and CPU")
+    place.__name__ = kind
+    return place
+
+
+NPUPlace = _no_device("NPUPlace")
+IPUPlace = _no_device("IPUPlace")
+MLUPlace = _no_device("MLUPlace")
+
+
 def is_compiled_with_cuda():
     return torch.cuda.is_available()
 
@@ -63,6 +75,28 @@ def is_compiled_with_npu():
 
 def is_compiled_with_cinn():
     return False
+
+
+def is_compiled_with_ipu():
+    return False
+
+
+def is_compiled_with_mlu():
+    return False
+
+
+def get_cudnn_version():
+    """MIOpen stands in for cuDNN on ROCm; report its version as an int (major*1000+minor*100+patch)."""
+    v = getattr(torch.backends.cudnn, "version", lambda: None)()
+    return v
+
+
+def get_all_custom_device_type():
+    return []
+
+
+def get_available_custom_device():
+    return []
 
 
 def _parse(dev) -> torch.device:

@@ -51,3 +51,15 @@ def set_default_dtype(d):
 
 def get_default_dtype() -> str:
     return dtype_name(_default[0])
+
+
+complex64, complex128 = torch.complex64, torch.complex128
+dtype = torch.dtype
+
+
+def iinfo(d):
+    return torch.iinfo(to_torch_dtype(d))
+
+
+def finfo(d):
+    return torch.finfo(to_torch_dtype(d))

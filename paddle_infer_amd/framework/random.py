@@ -59,6 +59,22 @@ def set_rng_state(state):
         _GLOBAL[k] = g
 
 
+def get_cuda_rng_state():
+    """Per-GPU generator states: torch's (for torch-side sampling) plus the kernel dropout
+    generator's (seed, offset) — restoring both replays dropout masks exactly."""
+    states = torch.cuda.get_rng_state_all() if torch.cuda.is_available() else []
+    return {"torch": states, "kernel": get_rng_state()}
+
+
+def set_cuda_rng_state(state):
+    if isinstance(state, dict):
+        if state.get("torch") and torch.cuda.is_available():
+            torch.cuda.set_rng_state_all(state["torch"])
+        set_rng_state(state.get("kernel", {}))
+    elif state and torch.cuda.is_available():
+        torch.cuda.set_rng_state_all(state)
+
+
 class RNGStatesTracker:
     """Named generators; ``rng_state(name)`` makes kernel dropout inside the block draw from it."""
 

@@ -54,7 +54,7 @@ swish = silu
 def softmax(x, axis=-1, dtype=None, name=None):
     if dtype is not None:
         x = x.to(_dt(dtype))
-    if axis in (-1, x.dim() - 1) and x.is_cuda and x.dtype == torch.bfloat16:
+    if axis in (-1, x.dim() - 1) and x.is_cuda and x.dtype in (torch.bfloat16, torch.float16):
         return _ops.fused_softmax_mask(x)
     return torch.softmax(x, axis)
 
@@ -332,6 +332,11 @@ def _reduce(loss, reduction):
     return loss
 
 
+def _up(t):
+    """Loss math in fp32 for 16-bit inputs; fp32 / fp64 keep their precision."""
+    return t.float() if t.is_floating_point() and t.element_size() < 4 else t
+
+
 def cross_entropy(input, label, weight=None, ignore_index=-100, reduction="mean", soft_label=False,  # noqa: A002
                   axis=-1, use_softmax=True, label_smoothing=0.0, name=None):
     if axis not in (-1, input.dim() - 1):
@@ -339,19 +344,19 @@ def cross_entropy(input, label, weight=None, ignore_index=-100, reduction="mean"
         label = label.movedim(axis, -1) if soft_label else label
     V = input.shape[-1]
     if soft_label:
-        logp = torch.log_softmax(input.float(), -1) if use_softmax else torch.log(input.float())
-        loss = -(label.float() * logp).sum(-1)
+        logp = torch.log_softmax(_up(input), -1) if use_softmax else torch.log(_up(input))
+        loss = -(_up(label) * logp).sum(-1)
         if weight is not None:
-            loss = loss * (label.float() * weight).sum(-1)
+            loss = loss * (_up(label) * weight).sum(-1)
         return _reduce(loss, reduction)
     lab = label.squeeze(-1) if label.dim() == input.dim() else label
     if not use_softmax:
-        loss = TF.nll_loss(torch.log(input.float()).reshape(-1, V), lab.reshape(-1).long(),
+        loss = TF.nll_loss(torch.log(_up(input)).reshape(-1, V), lab.reshape(-1).long(),
                            weight, ignore_index=ignore_index, reduction="none").view(lab.shape)
     elif weight is None and label_smoothing == 0.0:
-        loss = _ops.softmax_cross_entropy(input, lab, ignore_index).float()
+        loss = _up(_ops.softmax_cross_entropy(input, lab, ignore_index))
     else:
-        loss = TF.cross_entropy(input.float().reshape(-1, V), lab.reshape(-1).long(), weight,
+        loss = TF.cross_entropy(_up(input).reshape(-1, V), lab.reshape(-1).long(), weight,
                                 ignore_index=ignore_index, reduction="none",
                                 label_smoothing=label_smoothing).view(lab.shape)
     if reduction == "mean":
@@ -496,3 +501,15 @@ def grid_sample(x, grid, mode="bilinear", padding_mode="zeros", align_corners=Tr
 
 
 math  # noqa
+
+
+def _import_extra():
+    from . import extra as _extra
+    g = globals()
+    for k, v in vars(_extra).items():
+        if not k.startswith("_") and callable(v) and getattr(v, "__module__", "") == _extra.__name__ \
+                and k not in g:
+            g[k] = v
+
+
+_import_extra()

@@ -140,6 +140,45 @@ class Bilinear(Initializer):
         t.copy_(torch.from_numpy(w))
 
 
+class Dirac(Initializer):
+    """Identity-preserving conv init (reference `nn/initializer/dirac.py`): weight
+    [out, in, *k] gets 1 at the kernel centre of (g·out/groups + i, i) for i < min(out/groups, in)."""
+
+    def __init__(self, groups=1, name=None):
+        self.groups = groups
+
+    def _init(self, t):
+        if t.dim() not in (3, 4, 5):
+            raise ValueError("Dirac initializer needs a 3-D, 4-D or 5-D conv weight")
+        out, cin = t.shape[0], t.shape[1]
+        if out % self.groups:
+            raise ValueError("out channels must be divisible by groups")
+        per = out // self.groups
+        t.zero_()
+        centre = tuple(k // 2 for k in t.shape[2:])
+        for g in range(self.groups):
+            for i in range(min(per, cin)):
+                t[(g * per + i, i) + centre] = 1.0
+
+
+def calculate_gain(nonlinearity, param=None):
+    """Recommended gain per nonlinearity (reference `nn/initializer/__init__.py:calculate_gain`)."""
+    linear = ("sigmoid", "linear", "conv1d", "conv2d", "conv3d", "conv1d_transpose",
+              "conv2d_transpose", "conv3d_transpose")
+    if nonlinearity in linear:
+        return 1.0
+    if nonlinearity == "tanh":
+        return 5.0 / 3
+    if nonlinearity == "relu":
+        return math.sqrt(2.0)
+    if nonlinearity == "leaky_relu":
+        slope = 0.01 if param is None else param
+        return math.sqrt(2.0 / (1 + slope ** 2))
+    if nonlinearity == "selu":
+        return 3.0 / 4
+    raise ValueError(f"nonlinearity function {nonlinearity} is not supported")
+
+
 # fluid-style aliases
 ConstantInitializer = Constant
 NormalInitializer = Normal

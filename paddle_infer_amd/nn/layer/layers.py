@@ -774,30 +774,171 @@ class Transformer(Layer):
 
 
 # ------------------------------------------------------------------------------- RNN
-class _RNNBase(Layer):
-    _cls = None
+# ------------------------------------------------------------------------------- misc layers
+class Conv3DTranspose(_ConvNd):
+    _nd = 3
+    _transpose = True
 
-    def __init__(self, input_size, hidden_size, num_layers=1, direction="forward", time_major=False,
-                 dropout=0.0, activation="tanh", weight_ih_attr=None, weight_hh_attr=None,
-                 bias_ih_attr=None, bias_hh_attr=None, name=None):
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, output_padding=0,
+                 groups=1, dilation=1, weight_attr=None, bias_attr=None, data_format="NCDHW"):
+        super().__init__(in_channels, out_channels, kernel_size, stride, padding, dilation, groups,
+                         "zeros", weight_attr, bias_attr, data_format, output_padding)
+
+    def forward(self, x, output_size=None):
+        return F.conv3d_transpose(x, self.weight, self.bias, self.stride, self.padding,
+                                  self.output_padding, self.groups, self.dilation, self.data_format)
+
+
+class AdaptiveMaxPool3D(AdaptiveAvgPool1D):
+    def __init__(self, output_size, return_mask=False, name=None):
+        super().__init__(output_size)
+        self.return_mask = return_mask
+
+    def forward(self, x):
+        return F.adaptive_max_pool3d(x, self.output_size, self.return_mask)
+
+
+class _MaxUnPool(Layer):
+    _fn = None
+
+    def __init__(self, kernel_size, stride=None, padding=0, data_format=None, output_size=None, name=None):
         super().__init__()
-        kw = dict(num_layers=num_layers, bidirectional=direction in ("bidirect", "bidirectional"),
-                  batch_first=not time_major, dropout=dropout)
-        if self._cls is torch.nn.RNN:
-            kw["nonlinearity"] = activation
-        self.rnn = self._cls(input_size, hidden_size, **kw)
+        self.kernel_size, self.stride, self.padding = kernel_size, stride, padding
+        self.output_size = output_size
 
-    def forward(self, inputs, initial_states=None, sequence_length=None):
-        return self.rnn(inputs, initial_states)
+    def forward(self, x, indices):
+        return type(self)._fn(x, indices, self.kernel_size, self.stride, self.padding,
+                              output_size=self.output_size)
 
 
-class SimpleRNN(_RNNBase):
-    _cls = torch.nn.RNN
+class MaxUnPool1D(_MaxUnPool):
+    _fn = staticmethod(F.max_unpool1d)
 
 
-class LSTM(_RNNBase):
-    _cls = torch.nn.LSTM
+class MaxUnPool2D(_MaxUnPool):
+    _fn = staticmethod(F.max_unpool2d)
 
 
-class GRU(_RNNBase):
-    _cls = torch.nn.GRU
+class MaxUnPool3D(_MaxUnPool):
+    _fn = staticmethod(F.max_unpool3d)
+
+
+class Unfold(Layer):
+    def __init__(self, kernel_sizes, dilations=1, paddings=0, strides=1, name=None):
+        super().__init__()
+        self.args = (kernel_sizes, strides, paddings, dilations)
+
+    def forward(self, x):
+        k, s, p, d = self.args
+        return F.unfold(x, k, s, p, d)
+
+
+class Fold(Layer):
+    def __init__(self, output_sizes, kernel_sizes, dilations=1, paddings=0, strides=1, name=None):
+        super().__init__()
+        self.args = (output_sizes, kernel_sizes, strides, paddings, dilations)
+
+    def forward(self, x):
+        return F.fold(x, *self.args)
+
+
+class Softmax2D(Layer):
+    """Softmax over the channel axis of [N, C, H, W] / [C, H, W] input."""
+
+    def forward(self, x):
+        if x.dim() not in (3, 4):
+            raise ValueError(f"Softmax2D expects 3-D or 4-D input, got {x.dim()}-D")
+        return torch.softmax(x, -3)
+
+
+class PixelUnshuffle(Layer):
+    def __init__(self, downscale_factor, data_format="NCHW", name=None):
+        super().__init__()
+        self.r, self.data_format = downscale_factor, data_format
+
+    def forward(self, x):
+        return F.pixel_unshuffle(x, self.r, self.data_format)
+
+
+class ChannelShuffle(Layer):
+    def __init__(self, groups, data_format="NCHW", name=None):
+        super().__init__()
+        self.groups, self.data_format = groups, data_format
+
+    def forward(self, x):
+        return F.channel_shuffle(x, self.groups, self.data_format)
+
+
+class ZeroPad2D(Layer):
+    def __init__(self, padding, data_format="NCHW", name=None):
+        super().__init__()
+        self.padding, self.data_format = padding, data_format
+
+    def forward(self, x):
+        return F.zeropad2d(x, self.padding, self.data_format)
+
+
+class RReLU(Layer):
+    def __init__(self, lower=1.0 / 8.0, upper=1.0 / 3.0, name=None):
+        super().__init__()
+        self.lower, self.upper = lower, upper
+
+    def forward(self, x):
+        return F.rrelu(x, self.lower, self.upper, self.training)
+
+
+class SpectralNorm(Layer):
+    """Reference `nn/layer/norm.py:SpectralNorm`: returns weight / σ(weight), σ estimated with
+    ``power_iters`` power-iteration steps on persistent u, v buffers (weight reshaped to
+    [shape[dim], -1])."""
+
+    def __init__(self, weight_shape, dim=0, power_iters=1, epsilon=1e-12, dtype="float32"):
+        super().__init__()
+        self.dim, self.power_iters, self.eps = dim, power_iters, epsilon
+        h = weight_shape[dim]
+        w = int(math.prod(weight_shape)) // h
+        self.register_buffer("weight_u", torch.nn.functional.normalize(torch.randn(h), dim=0, eps=epsilon))
+        self.register_buffer("weight_v", torch.nn.functional.normalize(torch.randn(w), dim=0, eps=epsilon))
+
+    def forward(self, weight):
+        perm = [self.dim] + [i for i in range(weight.dim()) if i != self.dim]
+        mat = weight.permute(perm).reshape(weight.shape[self.dim], -1)
+        u, v = self.weight_u, self.weight_v
+        with torch.no_grad():
+            for _ in range(self.power_iters):
+                v = torch.nn.functional.normalize(mat.t() @ u, dim=0, eps=self.eps)
+                u = torch.nn.functional.normalize(mat @ v, dim=0, eps=self.eps)
+            self.weight_u.copy_(u)
+            self.weight_v.copy_(v)
+        sigma = torch.dot(u, mat @ v)
+        return weight / sigma
+
+
+class HSigmoidLoss(Layer):
+    """Hierarchical sigmoid head (reference `nn/layer/loss.py:HSigmoidLoss`): weight
+    [num_classes - 1, feature_size], bias [num_classes - 1, 1]."""
+
+    def __init__(self, feature_size, num_classes, weight_attr=None, bias_attr=None, is_custom=False,
+                 is_sparse=False, name=None):
+        super().__init__()
+        if num_classes < 2 and not is_custom:
+            raise ValueError("num_classes must be >= 2 with the default tree")
+        self.num_classes = num_classes
+        self.weight = self.create_parameter([num_classes - 1, feature_size], attr=weight_attr)
+        self.bias = self.create_parameter([num_classes - 1, 1], attr=bias_attr, is_bias=True)
+
+    def forward(self, input, label, path_table=None, path_code=None):  # noqa: A002
+        return F.hsigmoid_loss(input, label, self.num_classes, self.weight, self.bias,
+                               path_table, path_code)
+
+
+SoftMarginLoss = _loss_layer("SoftMarginLoss", F.soft_margin_loss, reduction="mean")
+MultiLabelSoftMarginLoss = _loss_layer("MultiLabelSoftMarginLoss", F.multi_label_soft_margin_loss,
+                                       weight=None, reduction="mean")
+TripletMarginWithDistanceLoss = _loss_layer(
+    "TripletMarginWithDistanceLoss", F.triplet_margin_with_distance_loss, distance_function=None,
+    margin=1.0, swap=False, reduction="mean")
+
+
+from .rnn import (RNNCellBase, SimpleRNNCell, LSTMCell, GRUCell, RNN, BiRNN, SimpleRNN, LSTM,  # noqa: E402,F401
+                  GRU, BeamSearchDecoder, dynamic_decode)

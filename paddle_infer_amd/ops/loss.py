@@ -63,7 +63,8 @@ class _XentFn(torch.autograd.Function):
 
 def _reference(logits, labels, ignore_index):
     V = logits.shape[-1]
-    return F.cross_entropy(logits.float().reshape(-1, V), labels.reshape(-1).long(),
+    x = logits.float() if logits.element_size() < 4 else logits
+    return F.cross_entropy(x.reshape(-1, V), labels.reshape(-1).long(),
                            ignore_index=ignore_index, reduction="none").view(labels.shape)
 
 

@@ -190,8 +190,9 @@ def fused_add_layer_norm(x, residual, weight=None, bias=None, eps: float = 1e-5,
 
 
 def _rms_ref(h, weight, eps):
-    var = h.float().pow(2).mean(-1, keepdim=True)
-    y = (h.float() * torch.rsqrt(var + eps)).to(h.dtype)
+    hf = h.float() if h.element_size() < 4 else h  # 16-bit math in fp32; fp32/fp64 as is
+    var = hf.pow(2).mean(-1, keepdim=True)
+    y = (hf * torch.rsqrt(var + eps)).to(h.dtype)
     return y * weight if weight is not None else y
 
 

@@ -907,6 +907,66 @@ class linalg:  # namespace: paddle.linalg
     triangular_solve = staticmethod(lambda x, y, upper=True, transpose=False, unitriangular=False, name=None: torch.linalg.solve_triangular(x.transpose(-1, -2) if transpose else x, y, upper=upper != transpose, unitriangular=unitriangular))
     cholesky_solve = staticmethod(lambda x, y, upper=False, name=None: torch.cholesky_solve(x, y, upper))
 
+    lu_unpack = staticmethod(lambda x, y, unpack_ludata=True, unpack_pivots=True, name=None:
+                             tuple(torch.lu_unpack(x, y, unpack_ludata, unpack_pivots)))
+
+
+# ------------------------------------------------------------------------------------ misc
+def nanmedian(x, axis=None, keepdim=True, name=None):
+    if axis is None:
+        v = torch.nanmedian(x.flatten())
+        return v.reshape([1] * x.dim()) if keepdim else v
+    return torch.nanmedian(x, dim=axis, keepdim=keepdim).values
+
+
+def nanquantile(x, q, axis=None, keepdim=False, name=None):
+    return torch.nanquantile(x.float(), torch.as_tensor(q, dtype=torch.float32, device=x.device),
+                             dim=axis, keepdim=keepdim)
+
+
+def multiplex(inputs, index, name=None):
+    """out[i] = inputs[index[i]][i] (reference `tensor/math.py:multiplex`)."""
+    stacked = torch.stack(list(inputs), 0)
+    idx = index.reshape(-1).long()
+    return stacked[idx, torch.arange(idx.numel(), device=idx.device)]
+
+
+def renorm(x, p, axis, max_norm):
+    return torch.renorm(x, p, axis, max_norm)
+
+
+def reverse(x, axis, name=None):
+    return flip(x, axis)
+
+
+def tolist(x):
+    return x.tolist()
+
+
+def tril_indices(row, col, offset=0, dtype="int64"):
+    return torch.tril_indices(row, col, offset)
+
+
+def triu_indices(row, col=None, offset=0, dtype="int64"):
+    return torch.triu_indices(row, row if col is None else col, offset)
+
+
+def index_add_(x, index, axis, value, name=None):
+    return x.index_add_(axis, index.long(), value)
+
+
+def check_shape(shape):
+    """Validate a shape argument (list/tuple of ints ≥ -1, or an int tensor)."""
+    if isinstance(shape, torch.Tensor):
+        if shape.dtype not in (torch.int32, torch.int64):
+            raise TypeError("shape tensor must be int32 or int64")
+        return
+    for s in shape:
+        if isinstance(s, torch.Tensor):
+            continue
+        if not isinstance(s, int) or s < -1:
+            raise ValueError(f"invalid shape entry {s!r}")
+
 
 def __getattr__(name):
     raise AttributeError(f"paddle_infer_amd.tensor has no attribute {name}")

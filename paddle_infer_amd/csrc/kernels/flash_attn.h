@@ -37,9 +37,12 @@
 //     multiple of 4 keys by the caller so each lane reads 8 B per 4 keys.
 //   * Every global load is unconditional (row indices clamped, out-of-range rows masked in the
 //     softmax), so hipcc can count `vmcnt` and the K/V prefetch stays in flight under the MFMAs.
-//   * Causal grids are flattened and launched heaviest-first (LPT order across all heads).
+//   * Grids are XCD-grouped (fa_map): the tiles of one (batch, head) run together on one XCD and
+//     share its L2; inside a group causal tiles go heaviest-first.
 #pragma once
 #include "common.h"
+
+#include <type_traits>
 
 // C ABI argument block (ops/attention.py mirrors it as a ctypes.Structure).
 struct FaArgs {
@@ -47,7 +50,7 @@ struct FaArgs {
   void* o;
   float* lse;
   const void* dout;
-  float* delta;
+  float* delta;  // backward scratch: 2 x rows f32 (−δ, −lse/scale)
   void *dq, *dk, *dv;
   const void* mask;  // additive, input dtype; null = none
   const int *cu_q, *cu_k;
@@ -109,30 +112,6 @@ __device__ __forceinline__ unsigned pack2(float lo, float hi) {
   return (unsigned)ET<F16>::fromf(lo) | ((unsigned)ET<F16>::fromf(hi) << 16);
 }
 
-// Dual-use LDS image (guide T10 layout (b)): byte offset of 16-B chunk `ch` of row `row` in an
-// image with ROWB-byte rows (ROWB / 16 a power of two).
-template <int ROWB>
-__device__ __forceinline__ int lds_off(int row, int ch) {
-  constexpr int CH = ROWB / 16;
-  const int x = (((row & 3) << 2) | ((row >> 2) & 3)) & (CH - 1);
-  return row * ROWB + ((ch ^ x) << 4);
-}
-
-template <bool F16>
-__device__ __forceinline__ typename ET<F16>::V8 lds_row8(const char* base, int off) {
-  return *reinterpret_cast<const typename ET<F16>::V8*>(base + off);
-}
-
-// Transposed read: 16-lane group reads a 4-row x 16-col block starting at (r0, c0 elems); lane i
-// of the group receives column c0+i of rows r0..r0+3.
-template <int ROWB>
-__device__ __forceinline__ s16x4_t lds_tr4(const char* base, int r0, int c0, int gi) {
-  const int q = gi >> 2, p = gi & 3;
-  const int col = c0 + 4 * p;
-  const int off = lds_off<ROWB>(r0 + q, col >> 3) + ((col & 7) << 1);
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + off));
-}
-
 template <bool F16>
 __device__ __forceinline__ typename ET<F16>::V8 cat44(s16x4_t a, s16x4_t b) {
   s16x8 t = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
@@ -164,6 +143,55 @@ __device__ __forceinline__ void glds_tile(const unsigned short* gbase, long long
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                      (__attribute__((address_space(3))) void*)(tile + P * 1024),
                                      16, 0, 0);
+  }
+}
+
+// XCD-aware work mapping (guide T1): workgroup ids are dealt round-robin to the 8 XCDs, so the
+// launcher pads the grid to a multiple of 8 and the kernel reads its logical id as
+// (bid % 8) · (G / 8) + bid / 8. The `per` tiles of one (batch, head) group are then consecutive
+// logical ids = consecutive dispatches on ONE XCD: they run together and share that head's K/V
+// (forward, dQ) or Q/dO (dK/dV) panels in the XCD's L2 instead of fetching them from HBM once
+// per tile. Returns false for the padding ids. `sub` = tile index inside the group (0 first).
+__device__ __forceinline__ bool fa_map(int per, int ngroups, int& grp, int& sub) {
+  const int G = (int)gridDim.x, bid = (int)blockIdx.x;
+  const int lid = (bid & 7) * (G >> 3) + (bid >> 3);
+  if (lid >= per * ngroups) return false;
+  grp = lid / per;
+  sub = lid - grp * per;
+  return true;
+}
+__host__ __forceinline__ dim3 fa_grid(long long n) { return dim3((unsigned)((n + 7) / 8 * 8)); }
+
+// glds_tile with the per-lane part of every piece's source address precomputed (bytes from the
+// tile's first row; valid while no row of the tile needs clamping): a full-tile issue is then a
+// wave-uniform base + one VGPR per piece, with no per-issue address arithmetic.
+template <int ROWS, int ROWB, int DCH>
+struct DmaOffs {
+  static constexpr int PPW = ROWS * (ROWB / 16) / 64 / 4;
+  unsigned off[PPW];
+};
+template <int ROWS, int ROWB, int DCH>
+__device__ __forceinline__ void dma_offs(long long rstride, int w, int lane, DmaOffs<ROWS, ROWB, DCH>& o) {
+  constexpr int CH = ROWB / 16;
+#pragma unroll
+  for (int i = 0; i < DmaOffs<ROWS, ROWB, DCH>::PPW; ++i) {
+    const int P = w * DmaOffs<ROWS, ROWB, DCH>::PPW + i;
+    const int L = P * 64 + lane, r = L / CH, pc = L % CH;
+    const int x = (((r & 3) << 2) | ((r >> 2) & 3)) & (CH - 1);
+    int lc = pc ^ x;
+    if (DCH < CH) lc = lc < DCH ? lc : 0;
+    o.off[i] = (unsigned)(((long long)r * rstride + (lc << 3)) * 2);
+  }
+}
+template <int ROWS, int ROWB, int DCH>
+__device__ __forceinline__ void glds_tile_pre(const unsigned short* gtile, const DmaOffs<ROWS, ROWB, DCH>& o,
+                                              char* tile, int w) {
+#pragma unroll
+  for (int i = 0; i < DmaOffs<ROWS, ROWB, DCH>::PPW; ++i) {
+    const int P = w * DmaOffs<ROWS, ROWB, DCH>::PPW + i;
+    __builtin_amdgcn_global_load_lds(
+        (const __attribute__((address_space(1))) void*)(reinterpret_cast<const char*>(gtile) + o.off[i]),
+        (__attribute__((address_space(3))) void*)(tile + P * 1024), 16, 0, 0);
   }
 }
 
@@ -202,6 +230,54 @@ __device__ __forceinline__ f32x4 mask4(const unsigned short* mrow, int key0, int
   return r;
 }
 
+// Per-lane LDS offsets, computed once per kernel (they are loop-invariant; every read then is one
+// of these VGPRs + a compile-time immediate, so the tile loops carry no address arithmetic):
+//   row[kk]     row read of 16-B chunk (2kk + hh) of image row l32 (rows 32t + l32 share the
+//               swizzle of l32: +32t·ROWB is an immediate)
+//   tr[jj][dt]  transposed read (ds_read_b64_tr_b16 of a 4-row x 16-col block) at rows
+//               r0 = 16ks + 4hh + 8jj, cols c0 = 32dt + 16(g&1): +16ks·ROWB is an immediate.
+//               d-block dt only flips chunk bits 2-3 (byte bits 6-7) of the dt = 0 offset, so
+//               tr[jj][dt] == tr[jj][0] ^ (dt << 6): kernels at two waves per SIMD keep only
+//               tr[.][0] live and pay one v_xor per read (tr_x)
+template <int ROWB, int KSTEPS, int DT>
+struct LaneOffs {
+  int row[KSTEPS];
+  int tr[2][DT];
+};
+// row[kk] == row[0] ^ (kk << 5) likewise (kk flips chunk bits 1-3 = byte bits 5-7)
+template <int ROWB, int KSTEPS, int DT>
+__device__ __forceinline__ int row_x(const LaneOffs<ROWB, KSTEPS, DT>& L, int kk) {
+  return L.row[0] ^ (kk << 5);
+}
+template <int ROWB, int KSTEPS, int DT>
+__device__ __forceinline__ int tr_x(const LaneOffs<ROWB, KSTEPS, DT>& L, int jj, int dt) {
+  return L.tr[jj][0] ^ (dt << 6);
+}
+template <int ROWB, int KSTEPS, int DT>
+__device__ __forceinline__ void lane_offs(int lane, LaneOffs<ROWB, KSTEPS, DT>& L) {
+  constexpr int CH = ROWB / 16;
+  const int l32 = lane & 31, hh = lane >> 5, gi = lane & 15, g = lane >> 4;
+  const int xl = (((l32 & 3) << 2) | ((l32 >> 2) & 3)) & (CH - 1);
+#pragma unroll
+  for (int kk = 0; kk < KSTEPS; ++kk) L.row[kk] = l32 * ROWB + (((2 * kk + hh) ^ xl) << 4);
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int rl = 4 * hh + 8 * jj + (gi >> 2);
+      const int col = 32 * dt + 16 * (g & 1) + 4 * (gi & 3);
+      const int xr = (((rl & 3) << 2) | ((rl >> 2) & 3)) & (CH - 1);
+      L.tr[jj][dt] = rl * ROWB + ((((col >> 3)) ^ xr) << 4) + ((col & 7) << 1);
+    }
+}
+template <bool F16>
+__device__ __forceinline__ typename ET<F16>::V8 lds_at(const char* smem, int off) {
+  return *reinterpret_cast<const typename ET<F16>::V8*>(smem + off);
+}
+__device__ __forceinline__ s16x4_t lds_tr_at(const char* smem, int off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(smem + off));
+}
+
 // ------------------------------------------------------------------------------------------
 // Forward
 // ------------------------------------------------------------------------------------------
@@ -225,9 +301,10 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FaArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5, gi = lane & 15, g = lane >> 4;
   const int nmb = (SqMax + BM - 1) / BM;
-  const int HB = Hq * B;
-  const int mb = CAUSAL ? (nmb - 1 - (int)blockIdx.x / HB) : (int)blockIdx.x / HB;
-  const int hq = (int)blockIdx.x % Hq, b = ((int)blockIdx.x % HB) / Hq;
+  int grp, sub;
+  if (!fa_map(nmb, Hq * B, grp, sub)) return;
+  const int mb = CAUSAL ? nmb - 1 - sub : sub;  // causal: heaviest query block first
+  const int hq = grp % Hq, b = grp / Hq;
   const int hk = hq / (Hq / Hk);
   const int m0 = mb * BM;
   int Sq = SqMax, Sk = a.Sk;
@@ -284,50 +361,51 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FaArgs a) {
   if (ntiles > 0) issue(0, 0);
   __syncthreads();
 
+  LaneOffs<ROWB, KSTEPS, DT> L;
+  lane_offs(lane, L);
   const bool wave_rows_valid = qrow0 < Sq;
-  for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < ntiles) issue(t + 1, buf ^ 1);
+  // key (relative to n0 + 4hh) valid for this lane's row iff < lim - n0
+  const int m_lim = min(CAUSAL ? qpos + coff + 1 : 0x40000000, Sk) - 4 * hh;
+  auto tile = [&](int t, auto bufc) {
+    constexpr int BUF = decltype(bufc)::value;
+    constexpr int KS = BUF * 2 * TILE_B, VS = KS + TILE_B;
+    if (t + 1 < ntiles) issue(t + 1, BUF ^ 1);
     const int n0 = t * BN;
     const bool active = wave_rows_valid && (!CAUSAL || n0 <= qrow0 + 31 + coff);
     if (active) {
-      const char* ks = smem + buf * 2 * TILE_B;
-      const char* vs = ks + TILE_B;
       f32x16 sacc[2];
 #pragma unroll
       for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
         for (int j = 0; j < 16; ++j) sacc[tt][j] = 0.f;
 #pragma unroll
-      for (int kk = 0; kk < KSTEPS; ++kk) {
+      for (int kk = 0; kk < KSTEPS; ++kk)
 #pragma unroll
-        for (int tt = 0; tt < 2; ++tt) {
-          V8 af = lds_row8<F16>(ks, lds_off<ROWB>(tt * 32 + l32, 2 * kk + hh));
-          sacc[tt] = E::mfma(af, qf[kk], sacc[tt]);
-        }
-      }
+        for (int tt = 0; tt < 2; ++tt)
+          sacc[tt] = E::mfma(lds_at<F16>(smem, L.row[kk] + KS + tt * 32 * ROWB), qf[kk], sacc[tt]);
       const bool need_mask = (n0 + BN > Sk) || (CAUSAL && n0 + BN - 1 > qrow0 + coff);
       float mx = -INFINITY;
+      auto scale_mask = [&](auto maskc) {
+        constexpr bool MASKED = decltype(maskc)::value;
+        const int lim = m_lim - n0;
 #pragma unroll
-      for (int tt = 0; tt < 2; ++tt)
+        for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int key0 = n0 + tt * 32 + 8 * g4 + 4 * hh;
-          f32x4 mb4 = {0.f, 0.f, 0.f, 0.f};
-          if (FEAT & F_MASK) mb4 = mask4<F16>(mrow, key0, Sk);
+          for (int g4 = 0; g4 < 4; ++g4) {
+            f32x4 mb4 = {0.f, 0.f, 0.f, 0.f};
+            if (FEAT & F_MASK) mb4 = mask4<F16>(mrow, n0 + tt * 32 + 8 * g4 + 4 * hh, Sk);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int r = 4 * g4 + e;
-            float x = sacc[tt][r] * c + mb4[e];
-            if (need_mask) {
-              const int key = key0 + e;
-              const bool ok = (key < Sk) & (!CAUSAL | (key <= qpos + coff));
-              x = ok ? x : -INFINITY;
+            for (int e = 0; e < 4; ++e) {
+              const int r = 4 * g4 + e;
+              float x = sacc[tt][r] * c + mb4[e];
+              if (MASKED) x = (tt * 32 + 8 * g4 + e) < lim ? x : -INFINITY;
+              sacc[tt][r] = x;
+              mx = fmaxf(mx, x);
             }
-            sacc[tt][r] = x;
-            mx = fmaxf(mx, x);
           }
-        }
+      };
+      if (need_mask) scale_mask(std::true_type{});
+      else scale_mask(std::false_type{});
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float m_new = fmaxf(m_i, mx);
       const float msub = m_new == -INFINITY ? 0.f : m_new;
@@ -370,18 +448,19 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FaArgs a) {
         for (int s = 0; s < 2; ++s) pf[2 * tt + s] = E::frag(sacc[tt], s);
       // Oᵀ += Vᵀ · Pᵀ
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        const int c0 = 32 * dt + 16 * (g & 1);
+      for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
         for (int ks4 = 0; ks4 < 4; ++ks4) {
-          const int r0 = 16 * ks4 + 4 * hh;
-          s16x4_t lo = lds_tr4<ROWB>(vs, r0, c0, gi);
-          s16x4_t hi = lds_tr4<ROWB>(vs, r0 + 8, c0, gi);
-          oacc[dt] = E::mfma(cat44<F16>(lo, hi), pf[ks4], oacc[dt]);
+          const int ro = VS + 16 * ks4 * ROWB;
+          oacc[dt] = E::mfma(cat44<F16>(lds_tr_at(smem, L.tr[0][dt] + ro), lds_tr_at(smem, L.tr[1][dt] + ro)),
+                             pf[ks4], oacc[dt]);
         }
-      }
     }
     __syncthreads();
+  };
+  for (int t = 0; t < ntiles; t += 2) {
+    tile(t, std::integral_constant<int, 0>{});
+    if (t + 1 < ntiles) tile(t + 1, std::integral_constant<int, 1>{});
   }
 
   // epilogue: lane = query row, registers = d
@@ -405,14 +484,20 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FaArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Backward pre-pass: delta[row] = Σ_d dO·O (f32). 16 B per lane, DP/8 lanes per row.
+// Backward pre-pass, per attention row (f32, [rows] then [rows] again):
+//   nrow[r]        = −Σ_d dO·O            (−δ: the dP accumulators start from it)
+//   nrow[rows + r] = −lse / scale          (the S accumulators start from it)
+// "Row constants as the initial accumulator" (guide App. B, attention backward): S' = Q·Kᵀ −
+// lse/scale and dP' = dO·Vᵀ − δ leave the MFMA chains ready, so p = exp2(c·S') and dS = p·dP'
+// need no per-element subtraction. 16 B per lane, DP/8 lanes per row.
 // ------------------------------------------------------------------------------------------
 template <int D, bool F16>
 __global__ __launch_bounds__(256) void bwd_pre_kernel(const unsigned short* __restrict__ o,
                                                       const unsigned short* __restrict__ dout,
-                                                      float* __restrict__ delta, int Sq, int Hq,
-                                                      long long sob, long long sos, long long soh,
-                                                      int total) {
+                                                      const float* __restrict__ lse,
+                                                      float* __restrict__ nrow, float inv_scale,
+                                                      int Sq, int Hq, long long sob, long long sos,
+                                                      long long soh, int total) {
   constexpr int TPR = D > 64 ? 16 : 8;  // threads per row (power of two)
   const int row = (blockIdx.x * 256 + threadIdx.x) / TPR, sub = threadIdx.x % TPR;
   const bool ok = row < total;
@@ -428,7 +513,11 @@ __global__ __launch_bounds__(256) void bwd_pre_kernel(const unsigned short* __re
     for (int j = 0; j < 8; ++j) s += ET<F16>::tof(x[j]) * ET<F16>::tof(d[j]);
 #pragma unroll
   for (int m = TPR / 2; m > 0; m >>= 1) s += __shfl_xor(s, m, 64);
-  if (ok && sub == 0) delta[((long long)b * Hq + hq) * Sq + qr] = s;
+  if (ok && sub == 0) {
+    const long long r = ((long long)b * Hq + hq) * Sq + qr;
+    nrow[r] = -s;
+    nrow[total + r] = -lse[r] * inv_scale;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -448,7 +537,7 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(FaArgs a) {
   constexpr int KIMG_B = BK * ROWB;     // resident K and V images of the block's 128 keys
   constexpr int OFF_K = 2 * 2 * QTILE_B;
   constexpr int OFF_V = OFF_K + KIMG_B;
-  constexpr int OFF_STAT = OFF_V + KIMG_B;  // 2 buffers x (lse, delta) x 64 f32
+  constexpr int OFF_STAT = OFF_V + KIMG_B;  // 2 buffers x (−lse/scale, −δ) x 64 f32
   constexpr int SMEM = OFF_STAT + 2 * 2 * BQ * 4;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
@@ -458,8 +547,9 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(FaArgs a) {
   const unsigned short* dout = (const unsigned short*)a.dout;
   unsigned short* dk = (unsigned short*)a.dk;
   unsigned short* dv = (unsigned short*)a.dv;
-  const float* lse = a.lse;
-  const float* delta = a.delta;
+  const float* nd = a.delta;                 // −δ
+  const long long rows = a.cu_q ? (long long)a.Hq * a.ltot : (long long)a.B * a.Hq * a.Sq;
+  const float* nl = a.delta + rows;  // −lse/scale
   const int B = a.B, SqMax = a.Sq, Hq = a.Hq, Hk = a.Hk;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
@@ -496,8 +586,12 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(FaArgs a) {
   // K / V of the block's keys stay resident in LDS (B operands of S and dP are row reads)
   glds_tile<BK, ROWB, D / 8>(k + b * a.skb + hk * a.skh, a.sks, n0, Sk - 1, smem + OFF_K, w, lane);
   glds_tile<BK, ROWB, D / 8>(v + b * a.svb + hk * a.svh, a.svs, n0, Sk - 1, smem + OFF_V, w, lane);
-  const char* kimg = smem + OFF_K;
-  const char* vimg = smem + OFF_V;
+
+  LaneOffs<ROWB, KSTEPS, DT> L;
+  lane_offs(lane, L);
+  int kvo[KSTEPS];  // this wave's K rows (V = +KIMG_B)
+#pragma unroll
+  for (int kk = 0; kk < KSTEPS; ++kk) kvo[kk] = OFF_K + 32 * w * ROWB + L.row[kk];
 
   f32x16 dkacc[DT], dvacc[DT];
 #pragma unroll
@@ -510,15 +604,29 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(FaArgs a) {
   const int nqt = (Sq + BQ - 1) / BQ;
   const int tiles_per_head = nqt - qt0;
   const int total = (n0 < Sk && tiles_per_head > 0) ? tiles_per_head * group : 0;
+  // causal / bounds mask in lane-relative form: row qr = q0 + 4hh + cq (cq compile-time) is
+  // valid for this lane's key iff lo <= q0 + cq < hi  (lo, hi per lane; q0 added per tile)
+  const int m_hi = key < Sk ? Sq - 4 * hh : -0x40000000;
+  const int m_lo = CAUSAL ? key - coff - 4 * hh : -0x40000000;
 
+  DmaOffs<BQ, ROWB, D / 8> dmq, dmo;
+  dma_offs(a.sqs, w, lane, dmq);
+  dma_offs(a.sos, w, lane, dmo);
   auto issue = [&](int it, int buf) {
     const int hq = hk * group + it / tiles_per_head;
     const int q0 = (qt0 + it % tiles_per_head) * BQ;
     char* qs = smem + buf * 2 * QTILE_B;
-    glds_tile<BQ, ROWB, D / 8>(q + b * a.sqb + hq * a.sqh, a.sqs, q0, Sq - 1, qs, w, lane);
-    glds_tile<BQ, ROWB, D / 8>(dout + b * a.sob + hq * a.soh, a.sos, q0, Sq - 1, qs + QTILE_B, w, lane);
-    if (w < 2) {  // wave 0: lse row, wave 1: delta row (64 f32 = one 4-B/lane DMA)
-      const float* s = (w == 0 ? lse : delta) + lrow + hq * lhead + min(q0 + lane, Sq - 1);
+    const unsigned short* qh = q + b * a.sqb + hq * a.sqh;
+    const unsigned short* oh = dout + b * a.sob + hq * a.soh;
+    if (q0 + BQ <= Sq) {  // full tile: precomputed lane offsets
+      glds_tile_pre<BQ, ROWB, D / 8>(qh + (long long)q0 * a.sqs, dmq, qs, w);
+      glds_tile_pre<BQ, ROWB, D / 8>(oh + (long long)q0 * a.sos, dmo, qs + QTILE_B, w);
+    } else {
+      glds_tile<BQ, ROWB, D / 8>(qh, a.sqs, q0, Sq - 1, qs, w, lane);
+      glds_tile<BQ, ROWB, D / 8>(oh, a.sos, q0, Sq - 1, qs + QTILE_B, w, lane);
+    }
+    if (w < 2) {  // wave 0: −lse/scale row, wave 1: −δ row (64 f32 = one 4-B/lane DMA)
+      const float* s = (w == 0 ? nl : nd) + lrow + hq * lhead + min(q0 + lane, Sq - 1);
       char* st = smem + OFF_STAT + (buf * 2 + w) * BQ * 4;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)s,
                                        (__attribute__((address_space(3))) void*)st, 4, 0, 0);
@@ -527,124 +635,110 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(FaArgs a) {
   if (total > 0) issue(0, 0);
   __syncthreads();
 
-  for (int it = 0; it < total; ++it) {
-    const int buf = it & 1;
+  // one query tile; every LDS address below is a precomputed lane offset + the buffer base + an
+  // immediate (unrolling the buffer parity into two tile bodies measured more AGPR<->VGPR copies
+  // at one wave per SIMD)
+  auto tile = [&](int it, int BUF) {
+    const int QS = BUF * 2 * QTILE_B, DOS = QS + QTILE_B;
+    const float* lst = reinterpret_cast<const float*>(smem + OFF_STAT) + BUF * 2 * BQ;
+    const float* dst = lst + BQ;
     const int hq = hk * group + it / tiles_per_head;
     const int q0 = (qt0 + it % tiles_per_head) * BQ;
-    if (it + 1 < total) issue(it + 1, buf ^ 1);
-    const char* qs = smem + buf * 2 * QTILE_B;
-    const char* dos = qs + QTILE_B;
-    const float* lst = reinterpret_cast<const float*>(smem + OFF_STAT) + buf * 2 * BQ;
-    const float* dst = lst + BQ;
-    // Re-derive every lane-dependent LDS address inside the iteration (an opaque copy of the lane
-    // id): otherwise hipcc hoists ~60 loop-invariant swizzled addresses into VGPRs and evicts the
-    // accumulators to AGPRs with per-iteration copies.
-    int lx = lane;
-    asm volatile("" : "+v"(lx));
-    const int l32 = lx & 31, hh = lx >> 5, gi = lx & 15, g = lx >> 4;
-    {
-      f32x16 sacc[2], pacc[2];
+    if (it + 1 < total) issue(it + 1, BUF ^ 1);
+    f32x16 sacc[2], pacc[2];
+    // S' = Q·Kᵀ − lse/scale, dP' = dO·Vᵀ − δ: row constants as the initial accumulators
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
+    for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
-        for (int j = 0; j < 16; ++j) { sacc[qt][j] = 0.f; pacc[qt][j] = 0.f; }
-      // S = Q·Kᵀ, dP = dO·Vᵀ with the next k-step's 6 fragments loaded one step ahead
-      V8 fr[2][6];
-      auto ld = [&](int kk, V8* f) {
-        const int koff = lds_off<ROWB>(32 * w + l32, 2 * kk + hh);
-        f[0] = lds_row8<F16>(kimg, koff);
-        f[1] = lds_row8<F16>(vimg, koff);
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int qi0 = qt * 32 + 8 * g4 + 4 * hh;
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(lst + qi0);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(dst + qi0);
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) {
-          const int qoff = lds_off<ROWB>(qt * 32 + l32, 2 * kk + hh);
-          f[2 + qt] = lds_row8<F16>(qs, qoff);
-          f[4 + qt] = lds_row8<F16>(dos, qoff);
+        for (int e = 0; e < 4; ++e) {
+          sacc[qt][4 * g4 + e] = l4[e];
+          pacc[qt][4 * g4 + e] = (FEAT & F_DROP) ? 0.f : d4[e];
         }
-      };
-      ld(0, fr[0]);
-#pragma unroll
-      for (int kk = 0; kk < KSTEPS; ++kk) {
-        if (kk + 1 < KSTEPS) ld(kk + 1, fr[(kk + 1) & 1]);
-        const V8* f = fr[kk & 1];
-#pragma unroll
-        for (int qt = 0; qt < 2; ++qt) {
-          sacc[qt] = E::mfma(f[2 + qt], f[0], sacc[qt]);
-          pacc[qt] = E::mfma(f[4 + qt], f[1], pacc[qt]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);
-      const bool need_mask = (kw0 + 31 >= Sk) || (q0 + BQ > Sq) ||
-                             (CAUSAL && kw0 + 31 > q0 + coff);
-      const unsigned short* mbase = nullptr;
-      if (FEAT & F_MASK) mbase = (const unsigned short*)a.mask + b * a.smb + hq * a.smh + keyc;
+    V8 fr[2][6];
+    auto ld = [&](int kk, V8* f) {
+      f[0] = lds_at<F16>(smem, kvo[kk]);
+      f[1] = lds_at<F16>(smem, kvo[kk] + KIMG_B);
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        f[2 + qt] = lds_at<F16>(smem, L.row[kk] + QS + qt * 32 * ROWB);
+        f[4 + qt] = lds_at<F16>(smem, L.row[kk] + DOS + qt * 32 * ROWB);
+      }
+    };
+    ld(0, fr[0]);
+#pragma unroll
+    for (int kk = 0; kk < KSTEPS; ++kk) {
+      if (kk + 1 < KSTEPS) ld(kk + 1, fr[(kk + 1) & 1]);
+      const V8* f = fr[kk & 1];
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        sacc[qt] = E::mfma(f[2 + qt], f[0], sacc[qt]);
+        pacc[qt] = E::mfma(f[4 + qt], f[1], pacc[qt]);
+      }
+    }
+    const bool need_mask = (kw0 + 31 >= Sk) || (q0 + BQ > Sq) || (CAUSAL && kw0 + 31 > q0 + coff);
+    const unsigned short* mbase = nullptr;
+    if (FEAT & F_MASK) mbase = (const unsigned short*)a.mask + b * a.smb + hq * a.smh + keyc;
+    auto finish = [&](auto maskc) {
+      constexpr bool MASKED = decltype(maskc)::value;
+      const int lo = m_lo - q0, hi = m_hi - q0;
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
-          const int qi0 = qt * 32 + 8 * g4 + 4 * hh;
-          const f32x4 l4 = *reinterpret_cast<const f32x4*>(lst + qi0);
-          const f32x4 d4 = *reinterpret_cast<const f32x4*>(dst + qi0);
+          f32x4 d4;
+          if (FEAT & F_DROP) d4 = *reinterpret_cast<const f32x4*>(dst + qt * 32 + 8 * g4 + 4 * hh);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int r = 4 * g4 + e;
-            const int qr = q0 + qi0 + e;
-            float x = sacc[qt][r] * c - l4[e] * kLog2e;
+            const int cq = qt * 32 + 8 * g4 + e;  // query row - q0 - 4hh
+            float x = sacc[qt][r] * c;
             if (FEAT & F_MASK)
-              x += E::tof(mbase[(long long)min(qr, Sq - 1) * a.smq]) * kLog2e;
+              x += E::tof(mbase[(long long)min(q0 + 4 * hh + cq, Sq - 1) * a.smq]) * kLog2e;
             float p = fast_exp2(x);
-            if (need_mask) {
-              const bool ok = (key < Sk) & (qr < Sq) & (!CAUSAL | (key <= qr + coff));
-              p = ok ? p : 0.f;
-            }
-            float dpv = pacc[qt][r];
+            if (MASKED) p = (cq >= lo && cq < hi) ? p : 0.f;
+            float ds = pacc[qt][r];
             float pd = p;
             if (FEAT & F_DROP) {
+              const int qr = q0 + 4 * hh + cq;
               const bool kp = drop_keep(drk, drop_hash(drk, lrow + hq * lhead + qr, sk_half, key), key);
               pd = kp ? p : 0.f;
-              dpv = kp ? dpv * drk.inv : 0.f;
+              ds = (kp ? ds * drk.inv : 0.f) + d4[e];
             }
             sacc[qt][r] = pd;
-            pacc[qt][r] = p * (dpv - d4[e]);
+            pacc[qt][r] = p * ds;
           }
         }
-      // dVᵀ += dOᵀ·(P∘M) ; dKᵀ += Qᵀ·dS   (A operands via transposed reads of the dO / Q images)
-      V8 pb[4], db[4];
+    };
+    if (need_mask) finish(std::true_type{});
+    else finish(std::false_type{});
+    // dVᵀ += dOᵀ·(P∘M) ; dKᵀ += Qᵀ·dS   (A operands via transposed reads of the dO / Q images)
+    V8 pb[4], db[4];
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
+    for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          pb[2 * qt + s] = E::frag(sacc[qt], s);
-          db[2 * qt + s] = E::frag(pacc[qt], s);
-        }
-      __builtin_amdgcn_sched_barrier(0);
-      V8 tf[2][4];
-      auto ldt = [&](int st, V8* f) {  // st = 2*dt + half: ks in {2*half, 2*half+1}
-        const int c0 = 32 * (st >> 1) + 16 * (g & 1);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int r0 = 16 * (2 * (st & 1) + j) + 4 * hh;
-          f[2 * j] = cat44<F16>(lds_tr4<ROWB>(dos, r0, c0, gi), lds_tr4<ROWB>(dos, r0 + 8, c0, gi));
-          f[2 * j + 1] = cat44<F16>(lds_tr4<ROWB>(qs, r0, c0, gi), lds_tr4<ROWB>(qs, r0 + 8, c0, gi));
-        }
-      };
-      ldt(0, tf[0]);
-#pragma unroll
-      for (int st = 0; st < 2 * DT; ++st) {
-        if (st + 1 < 2 * DT) ldt(st + 1, tf[(st + 1) & 1]);
-        const V8* f = tf[st & 1];
-        const int dt = st >> 1;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int ks = 2 * (st & 1) + j;
-          dvacc[dt] = E::mfma(f[2 * j], pb[ks], dvacc[dt]);
-          dkacc[dt] = E::mfma(f[2 * j + 1], db[ks], dkacc[dt]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
+      for (int s = 0; s < 2; ++s) {
+        pb[2 * qt + s] = E::frag(sacc[qt], s);
+        db[2 * qt + s] = E::frag(pacc[qt], s);
       }
-    }
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int ro = 16 * ks * ROWB;
+        const V8 fo = cat44<F16>(lds_tr_at(smem, L.tr[0][dt] + DOS + ro), lds_tr_at(smem, L.tr[1][dt] + DOS + ro));
+        const V8 fq = cat44<F16>(lds_tr_at(smem, L.tr[0][dt] + QS + ro), lds_tr_at(smem, L.tr[1][dt] + QS + ro));
+        dvacc[dt] = E::mfma(fo, pb[ks], dvacc[dt]);
+        dkacc[dt] = E::mfma(fq, db[ks], dkacc[dt]);
+      }
     __syncthreads();
-  }
+  };
+  for (int it = 0; it < total; ++it) tile(it, it & 1);
 
   if (key < Sk) {
     const float vs = (FEAT & F_DROP) ? drk.inv : 1.f;
@@ -687,8 +781,9 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(FaArgs a) {
   const unsigned short* dout = (const unsigned short*)a.dout;
   unsigned short* dq = (unsigned short*)a.dq;
   const int B = a.B, SqMax = a.Sq, Hq = a.Hq, Hk = a.Hk;
+  const long long rows = a.cu_q ? (long long)Hq * a.ltot : (long long)B * Hq * SqMax;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int l32 = lane & 31, hh = lane >> 5, gi = lane & 15, g = lane >> 4;
+  const int l32 = lane & 31, hh = lane >> 5;
   const int nmb = (SqMax + BM - 1) / BM;
   const int HB = Hq * B;
   const int mb = CAUSAL ? (nmb - 1 - (int)blockIdx.x / HB) : (int)blockIdx.x / HB;
@@ -724,7 +819,7 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(FaArgs a) {
   const int sk_half = (a.Sk + 1) >> 1;
 
   V8 qf[KSTEPS], df[KSTEPS];
-  float lse2, dlt;
+  float nlse, ndlt;  // −lse/scale, −δ of this lane's row
   {
     const long long qr = min(qpos, Sq - 1);
     const unsigned short* qp = q + b * a.sqb + qr * a.sqs + hq * a.sqh + 8 * hh;
@@ -735,13 +830,16 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(FaArgs a) {
       df[kk] = *reinterpret_cast<const V8*>(dp + 16 * kk);
     }
     const long long si = lbase + qr;
-    lse2 = a.lse[si] * kLog2e;
-    dlt = a.delta[si];
+    ndlt = a.delta[si];
+    nlse = a.delta[rows + si];
   }
 
   int n_end = Sk;
   if (CAUSAL) n_end = min(Sk, m0 + BM + coff);
   const int ntiles = n_end <= 0 ? 0 : (n_end + BN - 1) / BN;
+
+  LaneOffs<ROWB, KSTEPS, DT> L;
+  lane_offs(lane, L);
 
   f32x16 qacc[DT];
 #pragma unroll
@@ -758,74 +856,79 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(FaArgs a) {
   __syncthreads();
 
   const bool wave_rows_valid = qrow0 < Sq;
-  for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < ntiles) issue(t + 1, buf ^ 1);
+  // key (relative to the tile start n0, minus 4hh) valid for this lane's row iff < lim - n0
+  const int m_lim = (CAUSAL ? qpos + coff + 1 : 0x40000000) - 4 * hh;
+  auto tile = [&](int t, auto bufc) {
+    constexpr int BUF = decltype(bufc)::value;
+    constexpr int KS = BUF * 2 * TILE_B, VS = KS + TILE_B;
+    if (t + 1 < ntiles) issue(t + 1, BUF ^ 1);
     const int n0 = t * BN;
     const bool active = wave_rows_valid && (!CAUSAL || n0 <= qrow0 + 31 + coff);
     if (active) {
-      const char* ks = smem + buf * 2 * TILE_B;
-      const char* vs = ks + TILE_B;
-      f32x16 sacc[2], pacc[2];
-#pragma unroll
-      for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) { sacc[tt][j] = 0.f; pacc[tt][j] = 0.f; }
-#pragma unroll
-      for (int kk = 0; kk < KSTEPS; ++kk) {
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt) {
-          const int off = lds_off<ROWB>(tt * 32 + l32, 2 * kk + hh);
-          sacc[tt] = E::mfma(lds_row8<F16>(ks, off), qf[kk], sacc[tt]);
-          pacc[tt] = E::mfma(lds_row8<F16>(vs, off), df[kk], pacc[tt]);
-        }
-      }
+      // opaque per-tile copies of the 3 base offsets: at two waves per SIMD hipcc would otherwise
+      // hoist all 24 derived addresses out of the tile loop and spill
+      LaneOffs<ROWB, KSTEPS, DT> Lt;
+      Lt.row[0] = L.row[0];
+      Lt.tr[0][0] = L.tr[0][0];
+      Lt.tr[1][0] = L.tr[1][0];
+      asm volatile("" : "+v"(Lt.row[0]), "+v"(Lt.tr[0][0]), "+v"(Lt.tr[1][0]));
       const bool need_mask = (n0 + BN > Sk) || (CAUSAL && n0 + BN - 1 > qrow0 + coff);
+      const int lim = min(m_lim, Sk - 4 * hh) - n0;
+      // the tile's 64 keys as two 32-key halves (S / dP accumulators of one half live at a time:
+      // two waves per SIMD leave 256 registers)
 #pragma unroll
-      for (int tt = 0; tt < 2; ++tt)
+      for (int tt = 0; tt < 2; ++tt) {
+        f32x16 sacc, pacc;
 #pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int key0 = n0 + tt * 32 + 8 * g4 + 4 * hh;
-          f32x4 mb4 = {0.f, 0.f, 0.f, 0.f};
-          if (FEAT & F_MASK) mb4 = mask4<F16>(mrow, key0, Sk);
-          uint32_t h = 0, h2 = 0;
-          if (FEAT & F_DROP) {
-            h = drop_hash(drk, lbase + qpos, sk_half, key0);
-            h2 = drop_hash(drk, lbase + qpos, sk_half, key0 + 2);
-          }
+        for (int j = 0; j < 16; ++j) { sacc[j] = nlse; pacc[j] = (FEAT & F_DROP) ? 0.f : ndlt; }
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int r = 4 * g4 + e;
-            const int key = key0 + e;
-            float p = fast_exp2(sacc[tt][r] * c + mb4[e] - lse2);
-            if (need_mask) {
-              const bool ok = (key < Sk) & (!CAUSAL | (key <= qpos + coff));
-              p = ok ? p : 0.f;
+        for (int kk = 0; kk < KSTEPS; ++kk) {
+          sacc = E::mfma(lds_at<F16>(smem, row_x(Lt, kk) + KS + tt * 32 * ROWB), qf[kk], sacc);
+          pacc = E::mfma(lds_at<F16>(smem, row_x(Lt, kk) + VS + tt * 32 * ROWB), df[kk], pacc);
+        }
+        auto finish = [&](auto maskc) {
+          constexpr bool MASKED = decltype(maskc)::value;
+#pragma unroll
+          for (int g4 = 0; g4 < 4; ++g4) {
+            const int key0 = n0 + tt * 32 + 8 * g4 + 4 * hh;
+            f32x4 mb4 = {0.f, 0.f, 0.f, 0.f};
+            if (FEAT & F_MASK) mb4 = mask4<F16>(mrow, key0, Sk);
+            uint32_t h = 0, h2 = 0;
+            if (FEAT & F_DROP) {
+              h = drop_hash(drk, lbase + qpos, sk_half, key0);
+              h2 = drop_hash(drk, lbase + qpos, sk_half, key0 + 2);
             }
-            float dpv = pacc[tt][r];
-            if (FEAT & F_DROP) dpv = drop_keep(drk, e < 2 ? h : h2, key) ? dpv * drk.inv : 0.f;
-            pacc[tt][r] = p * (dpv - dlt);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int r = 4 * g4 + e;
+              const int ck = tt * 32 + 8 * g4 + e;  // key - n0 - 4hh
+              float p = fast_exp2(sacc[r] * c + mb4[e]);
+              if (MASKED) p = ck < lim ? p : 0.f;
+              float ds = pacc[r];
+              if (FEAT & F_DROP) ds = (drop_keep(drk, e < 2 ? h : h2, key0 + e) ? ds * drk.inv : 0.f) + ndlt;
+              pacc[r] = p * ds;
+            }
           }
-        }
-      V8 dsf[4];
+        };
+        if (need_mask) finish(std::true_type{});
+        else finish(std::false_type{});
+        const V8 ds0 = E::frag(pacc, 0), ds1 = E::frag(pacc, 1);
+        // dQᵀ += Kᵀ · dSᵀ over this half's 32 keys
 #pragma unroll
-      for (int tt = 0; tt < 2; ++tt)
+        for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) dsf[2 * tt + s] = E::frag(pacc[tt], s);
-      // dQᵀ += Kᵀ · dSᵀ
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        const int c0 = 32 * dt + 16 * (g & 1);
-#pragma unroll
-        for (int ks4 = 0; ks4 < 4; ++ks4) {
-          const int r0 = 16 * ks4 + 4 * hh;
-          s16x4_t lo = lds_tr4<ROWB>(ks, r0, c0, gi);
-          s16x4_t hi = lds_tr4<ROWB>(ks, r0 + 8, c0, gi);
-          qacc[dt] = E::mfma(cat44<F16>(lo, hi), dsf[ks4], qacc[dt]);
-        }
+          for (int h2 = 0; h2 < 2; ++h2) {
+            const int ro = KS + 16 * (2 * tt + h2) * ROWB;
+            qacc[dt] = E::mfma(cat44<F16>(lds_tr_at(smem, tr_x(Lt, 0, dt) + ro), lds_tr_at(smem, tr_x(Lt, 1, dt) + ro)),
+                               h2 ? ds1 : ds0, qacc[dt]);
+          }
       }
     }
     __syncthreads();
+  };
+  for (int t = 0; t < ntiles; t += 2) {
+    tile(t, std::integral_constant<int, 0>{});
+    if (t + 1 < ntiles) tile(t + 1, std::integral_constant<int, 1>{});
   }
 
   if (qpos < Sq) {
@@ -860,7 +963,7 @@ int launch_fwd_feat(const FaArgs& a, dim3 grid, hipStream_t st) {
 
 template <bool F16>
 int launch_fwd(const FaArgs& a, hipStream_t st) {
-  dim3 grid(((a.Sq + 127) / 128) * a.Hq * a.B);
+  const dim3 grid = fa_grid((long long)((a.Sq + 127) / 128) * a.Hq * a.B);
 #define FWD_D(DD) return a.causal ? launch_fwd_feat<F16, DD, true>(a, grid, st) \
                                   : launch_fwd_feat<F16, DD, false>(a, grid, st)
   switch (a.D) {
@@ -896,11 +999,11 @@ int launch_bwd(const FaArgs& a, hipStream_t st) {
   const int total = pB * a.Hq * pS;
   const int tpr = a.D > 64 ? 16 : 8;
   const int pre_blocks = (int)(((long long)total * tpr + 255) / 256);
-  dim3 gkv(((a.Sk + 127) / 128) * a.Hk * a.B), gq(((a.Sq + 127) / 128) * a.Hq * a.B);
+  const dim3 gkv(((a.Sk + 127) / 128) * a.Hk * a.B), gq(((a.Sq + 127) / 128) * a.Hq * a.B);
 #define BWD_D(DD)                                                                                  \
   hipLaunchKernelGGL((bwd_pre_kernel<DD, F16>), dim3(pre_blocks), dim3(256), 0, st,              \
-                     (const unsigned short*)a.o, (const unsigned short*)a.dout, a.delta, pS, a.Hq, \
-                     a.sob, a.sos, a.soh, total);                                                 \
+                     (const unsigned short*)a.o, (const unsigned short*)a.dout, a.lse, a.delta,  \
+                     1.f / a.scale, pS, a.Hq, a.sob, a.sos, a.soh, total);                        \
   return a.causal ? launch_bwd_feat<F16, DD, true>(a, gkv, gq, st)                               \
                   : launch_bwd_feat<F16, DD, false>(a, gkv, gq, st)
   switch (a.D) {

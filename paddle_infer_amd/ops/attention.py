@@ -106,7 +106,8 @@ def _bwd(q, k, v, o, lse, do, dq, dk, dv, causal, scale, mask=None, p=0.0, seed=
         do = do.contiguous() if o.is_contiguous() else torch.empty_like(o).copy_(do)
     assert o.stride() == do.stride()
     assert dq.stride() == q.stride() and dk.stride() == k.stride() and dv.stride() == v.stride()
-    delta = torch.empty((B, Hq, Sq), device=q.device, dtype=torch.float32)
+    # per-row backward constants: [0] = −δ (rowsum dO·O), [1] = −lse/scale (flash_attn.h pre-pass)
+    delta = torch.empty((2, B, Hq, Sq), device=q.device, dtype=torch.float32)
     a = _args(q, k, v, o, lse, causal, scale, mask, p, seed, off, B, Sq, Sk, Hq, Hk, D)
     a.dout, a.delta, a.dq, a.dk, a.dv = do.data_ptr(), delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr()
     _lib.call("piamd_fa_bwd", ctypes.byref(a), _f16(q), _lib.stream())
@@ -275,7 +276,7 @@ class _FlashAttnVarlenFn(torch.autograd.Function):
         do = do.contiguous()
         T, Hq, D = q.shape
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
-        delta = torch.empty((Hq, T), device=q.device, dtype=torch.float32)
+        delta = torch.empty((2, Hq, T), device=q.device, dtype=torch.float32)  # −δ, −lse/scale
         a = _varlen_args(q, k, v, o, lse, cu_q, cu_k, max_q, max_k, causal, scale, p, seed, off)
         a.dout, a.delta, a.dq, a.dk, a.dv = (do.data_ptr(), delta.data_ptr(), dq.data_ptr(),
                                              dk.data_ptr(), dv.data_ptr())

@@ -1,5 +1,8 @@
 // Flash attention entry points + the bf16 instantiations (kernels: flash_attn.h; fp16
 // instantiations: flash_attn_f16.hip, compiled in parallel).
+// piamd-hipcc-flags: -mllvm -amdgpu-mfma-vgpr-form
+// (MFMA results in arch VGPRs: the one-wave-per-SIMD dK/dV kernel otherwise keeps its S / dP
+// accumulators in AGPRs and copies them to VGPRs for the softmax every tile)
 #include "flash_attn.h"
 
 int fa_fwd_f16(const FaArgs& a, hipStream_t st);

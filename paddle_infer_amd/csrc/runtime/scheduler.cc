@@ -6,11 +6,11 @@
 // `paddle/fluid/framework/ir/memory_optimize_pass/` (liveness-based buffer reuse).
 //
 // Exposed as a C ABI (ctypes) over CSR-encoded op→var lists:
-//   piamd_plan    : dependency graph, deterministic topological order (program order preferred),
-//                   GC lists, dependency depth ("level") per op for multi-stream dispatch.
-//   piamd_memplan : static arena planning — greedy best-fit of (size, [first,last]) lifetimes
-//                   into one device arena; the inference predictor allocates ONE buffer and slices
-//                   every intermediate out of it, which also makes hipGraph capture address-stable.
+//   piamd_plan : dependency graph, deterministic topological order (program order preferred),
+//                GC lists (the executor drops a variable right after its last consumer: forward
+//                activations of a training program live exactly until their grad op ran), and the
+//                dependency depth of every op (returned for inspection / tests; the executor issues
+//                ops in order on one HIP stream).
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
@@ -94,33 +94,4 @@ PIAMD_EXPORT int piamd_plan(int num_ops, int num_vars, const int* in_ptr, const 
   }
   free_ptr[num_ops] = c;
   return 0;
-}
-
-// Greedy best-fit arena planning. Buffers sorted by size (desc); each is placed at the lowest
-// aligned offset not overlapping any already-placed buffer whose [first, last] interval intersects.
-PIAMD_EXPORT long long piamd_memplan(int n, const long long* sizes, const int* first,
-                                     const int* last, long long align, long long* offsets) {
-  if (align <= 0) align = 256;
-  std::vector<int> idx(n);
-  for (int i = 0; i < n; ++i) idx[i] = i;
-  std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return sizes[a] > sizes[b]; });
-  struct Placed { long long off, end; int first, last; };
-  std::vector<Placed> placed;
-  long long total = 0;
-  for (int i : idx) {
-    const long long sz = (sizes[i] + align - 1) / align * align;
-    std::vector<std::pair<long long, long long>> busy;
-    for (const auto& p : placed)
-      if (!(p.last < first[i] || last[i] < p.first)) busy.push_back({p.off, p.end});
-    std::sort(busy.begin(), busy.end());
-    long long cand = 0;
-    for (const auto& b : busy) {
-      if (cand + sz <= b.first) break;
-      cand = std::max(cand, b.second);
-    }
-    offsets[i] = cand;
-    placed.push_back({cand, cand + sz, first[i], last[i]});
-    total = std::max(total, cand + sz);
-  }
-  return total;
 }

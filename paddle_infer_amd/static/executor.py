@@ -4,8 +4,12 @@
 Plan (cached per program version) comes from the native runtime (`csrc/runtime/scheduler.cc`):
 dependency-respecting instruction order + per-instruction GC list, so intermediates are released
 right after their last consumer (the reference's eager-deletion GC). Persistable variables live in
-the Scope across runs. Training programs contain ``backward`` (autograd over the recorded forward)
-and ``optimize`` ops (a Paddle optimizer bound to the scope's parameters).
+the Scope across runs. Training programs (`backward.py`) hold one ``<type>_grad`` op per forward
+op — run as that op's VJP (`_run_grad_op`) — plus ``sum`` ops for renamed partial gradients and
+per-parameter optimizer ops (``sgd`` / ``momentum`` / ``adam`` / ``adamw``) that update the
+persistable parameters and accumulators in place; the learning-rate variable of a program built
+by ``minimize`` is refreshed from its optimizer / LRScheduler before each run (reference
+`executor.py` ``_update_lr``).
 """
 from __future__ import annotations
 
@@ -31,12 +35,10 @@ def runtime_lib():
             _build.build(verbose=False)
         lib = ctypes.CDLL(path)
         P = ctypes.POINTER
-        i32p, u8p, i64p = P(ctypes.c_int), P(ctypes.c_ubyte), P(ctypes.c_longlong)
+        i32p, u8p = P(ctypes.c_int), P(ctypes.c_ubyte)
         lib.piamd_plan.argtypes = [ctypes.c_int, ctypes.c_int, i32p, i32p, i32p, i32p, u8p, i32p,
                                    i32p, i32p, i32p]
         lib.piamd_plan.restype = ctypes.c_int
-        lib.piamd_memplan.argtypes = [ctypes.c_int, i64p, i32p, i32p, ctypes.c_longlong, i64p]
-        lib.piamd_memplan.restype = ctypes.c_longlong
         _RT = lib
     return _RT
 
@@ -126,7 +128,18 @@ class Executor:
         for name, val in (feed or {}).items():
             t = val if isinstance(val, torch.Tensor) else torch.as_tensor(np.asarray(val))
             env[name] = t.to(self.device)
-        training = any(op.type in ("backward", "optimize") for op in ops)
+        from .backward import op_role, FORWARD
+        training = any(op_role(op) != FORWARD for op in ops)
+        for lr_name, opt in getattr(program, "_lr_vars", {}).items():
+            cur = scope.get(lr_name)
+            val = torch.tensor([float(opt.get_lr())], dtype=torch.float32, device=self.device)
+            if cur is None:
+                scope.set(lr_name, val)
+            else:
+                cur.copy_(val)
+        for name in getattr(program, "_grad_roots", ()):
+            if name in env and env[name].is_floating_point():
+                env[name] = env[name].detach().requires_grad_(True)
         bind = {}
         bvars = program.global_block().vars
         for name, t in env.items():
@@ -155,6 +168,8 @@ class Executor:
                 return dev
             return x
 
+        self._leafmap = {}
+        self._training = training
         with torch.set_grad_enabled(training):
             for pos, oi in enumerate(order):
                 op = ops[oi]
@@ -162,6 +177,16 @@ class Executor:
                 for n in frees[pos]:
                     if n not in fetch_names:
                         env.pop(n, None)
+        if training:  # persistable outputs (updated params / accumulators) back into the Scope
+            for n in list(env):
+                if n in program.params and n not in (feed or {}):
+                    cur = scope.get(n)
+                    val = env.pop(n)
+                    if cur is None:
+                        scope.set(n, val)
+                    elif val is not cur:
+                        with torch.no_grad():
+                            cur.copy_(val)
         outs = []
         for n in fetch_names:
             v = env[n] if n in env else scope.get(n)
@@ -188,11 +213,36 @@ class Executor:
                 for p in opt._parameter_list:
                     p.grad = None
             return
-        if op.func is None:  # a Paddle-typed op loaded from a foreign .pdmodel
+        from .backward import op_role, is_grad_op, OPTIMIZE, FORWARD
+        if is_grad_op(op):
+            self._run_grad_op(op, sub, env)
+            return
+        if getattr(self, "_training", False) and op_role(op) == FORWARD:
+            # per-op autograd graphs: a forward op of a training program reads its differentiable
+            # inputs through fresh leaves (views, no copy), so its grad op's VJP is exactly this
+            # op's local Jacobian product (a grad w.r.t. one input never leaks through another)
+            leaves = {}
+            outer = sub
+
+            def sub(x):  # noqa: F811
+                v = outer(x)
+                if isinstance(x, VarRef) and isinstance(v, torch.Tensor) and v.requires_grad:
+                    lf = leaves.get(x.name)
+                    if lf is None:
+                        lf = leaves[x.name] = v.detach().requires_grad_(True)
+                    return lf
+                return v
+            for n in op.output_names():
+                self._leafmap[n] = leaves
+        if op.func is None:  # a Paddle-typed op (loaded .pdmodel, IR pass, backward / optimizer pass)
             from . import ops_registry
             ops_registry.DEVICE.append(self.device)
             try:
-                run_paddle_op(op, sub, env, scope)
+                if op_role(op) == OPTIMIZE:
+                    with torch.no_grad():
+                        run_paddle_op(op, sub, env, scope)
+                else:
+                    run_paddle_op(op, sub, env, scope)
             finally:
                 ops_registry.DEVICE.pop()
             return
@@ -206,6 +256,81 @@ class Executor:
             if isinstance(ref, VarRef):
                 env[ref.name] = val
         _zip_assign(op.outputs, out, assign)
+
+    def _run_grad_op(self, op, sub, env):
+        """VJP of the grad op's forward op. Fast path: the op-local autograd graph its forward built
+        in this run (the forward read its inputs through leaves, see `_run_op`). Otherwise the
+        forward op is re-run on detached leaves (a forward that ran without a graph)."""
+        from .ops_registry import REGISTRY
+        ins, outs = op.paddle_inputs, op.paddle_outputs
+        gslot = {k[:-5]: v for k, v in ins.items() if k.endswith("@GRAD")}
+        fins = {k: v for k, v in ins.items() if not k.endswith("@GRAD") and k not in gslot}
+        fouts = {k: ins.get(k, []) for k in gslot}
+        xs = []
+        for k, targets in outs.items():
+            for x, g in zip(fins.get(k[:-5], []), targets):
+                if g and x not in xs:
+                    xs.append(x)
+        if not xs:
+            return
+
+        def val(n):
+            return env[n] if n in env else sub(VarRef(n))
+        gouts = []
+        for k, onames in fouts.items():
+            for o, g in zip(onames, gslot[k]):
+                if g and (g in env):
+                    gouts.append((o, env[g]))
+        leaves = None
+        for onames in fouts.values():
+            for o in onames:
+                leaves = self._leafmap.get(o, leaves) if hasattr(self, "_leafmap") else None
+        ov = [env.get(o) for o, _ in gouts]
+        fast = leaves is not None and all(isinstance(t, torch.Tensor) and t.grad_fn is not None for t in ov)
+        xv = [leaves.get(x) if fast else val(x) for x in xs]
+        with torch.enable_grad():
+            if not fast:
+                leaves = {x: (t.detach().requires_grad_(True) if isinstance(t, torch.Tensor) and t.is_floating_point() else t)
+                          for x, t in zip(xs, xv)}
+
+                def sub2(r):
+                    if isinstance(r, VarRef) and r.name in leaves:
+                        return leaves[r.name]
+                    return sub(r)
+                fop = getattr(op, "fwd_op", None)
+                produced = {}
+                if fop is not None and fop.func is not None:
+                    args = tree_map(sub2, fop.args)
+                    kwargs = tree_map(sub2, fop.kwargs)
+                    res = fop.func(*args, **kwargs)
+                    _zip_assign(fop.outputs, res, lambda r, v: produced.__setitem__(r.name, v) if isinstance(r, VarRef) else None)
+                else:
+                    fn = REGISTRY.get(op.type[:-5])
+                    if fn is None:
+                        raise NotImplementedError(f"no forward kernel for grad op {op.type}")
+                    attrs = {k: v for k, v in op.attrs.items() if k != "op_role"}
+                    res = fn({k: [sub2(VarRef(n)) for n in v] for k, v in fins.items()}, attrs)
+                    for k, onames in fouts.items():
+                        vals = res.get(k)
+                        vals = vals if isinstance(vals, (list, tuple)) else [vals]
+                        produced.update(zip(onames, vals))
+                ov = [produced.get(o) for o, _ in gouts]
+                xv = [leaves[x] for x in xs]
+            pairs = [(o, g) for o, (_, g) in zip(ov, gouts) if isinstance(o, torch.Tensor) and o.requires_grad]
+            diff = [i for i, t in enumerate(xv) if isinstance(t, torch.Tensor) and t.requires_grad]
+            grads = [None] * len(xs)
+            if pairs and diff:
+                r = torch.autograd.grad([o for o, _ in pairs], [xv[i] for i in diff],
+                                        [g.to(o.dtype) if g.dtype != o.dtype else g for o, g in pairs],
+                                        allow_unused=True)
+                for i, gr in zip(diff, r):
+                    grads[i] = gr
+        gmap = dict(zip(xs, grads))
+        for k, targets in outs.items():
+            for x, g in zip(fins.get(k[:-5], []), targets):
+                if g:
+                    gr = gmap.get(x)
+                    env[g] = gr.detach() if gr is not None else torch.zeros_like(val(x)).detach()
 
     def _optimizer_for(self, op, scope):
         key = id(op)

@@ -327,7 +327,14 @@ class Program:
         b = p.global_block()
         src = self.global_block()
         b.vars = dict(src.vars)
-        b.ops = [op for op in src.ops if not (for_test and op.type in ("backward", "optimize"))]
+        if for_test:
+            from .backward import op_role, FORWARD
+            b.ops = [op for op in src.ops if op_role(op) == FORWARD]
+        else:
+            b.ops = list(src.ops)
+            for k in ("_backward_info", "_lr_vars", "_grad_roots", "_opt_vars"):
+                if hasattr(self, k):
+                    setattr(p, k, getattr(self, k))
         p.feed_names, p.fetch_names = list(self.feed_names), list(self.fetch_names)
         if for_test:
             for op in b.ops:

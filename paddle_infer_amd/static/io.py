@@ -372,7 +372,8 @@ def _as_list(x):
 
 
 def prune(program, fetch_names):
-    ops = [op for op in program.global_block().ops if op.type not in ("backward", "optimize")]
+    from .backward import op_role, FORWARD
+    ops = [op for op in program.global_block().ops if op_role(op) == FORWARD]
     need = set(fetch_names)
     keep = []
     for op in reversed(ops):
@@ -451,19 +452,75 @@ def load_inference_model(path_prefix, executor, model_filename=None, params_file
     return [prog, list(prog.feed_names), fetch_vars]
 
 
+def train_program_desc(program):
+    """ProgramDesc of a TRAINING program holding only reference op types: the recorded forward is
+    lowered to Paddle ops (`lowering.py`), the backward is re-derived over those Paddle ops
+    (``matmul_v2_grad`` / ``elementwise_add_grad`` / ``sum`` ... with ``op_role`` 1, `backward.py`),
+    and the optimize phase (grad-clip ops lowered, ``sgd`` / ``momentum`` / ``adam`` / ``adamw``
+    ops as built by ``minimize``) follows with ``op_role`` 2."""
+    from .backward import op_role, FORWARD, OPTIMIZE, build_backward
+    info = getattr(program, "_backward_info", None)
+    if info is None:
+        raise ValueError("program has no backward (append_backward / minimize was not called)")
+    b = program.global_block()
+    fwd = [op for op in b.ops if op_role(op) == FORWARD]
+    opt = [op for op in b.ops if op_role(op) == OPTIMIZE]
+    if any(op.type == "optimize" for op in opt):
+        raise ValueError("this optimizer has no static op form (sgd / momentum / adam / adamw)")
+    lp = desc_to_program(program_to_desc(program, ops=fwd))
+    lp.params = dict(program.params)
+    lb = lp.global_block()
+    for n in program.params:
+        if n in lb.vars:
+            lb.vars[n].persistable_ = True
+    build_backward(lb, info["loss"], info["params"], info.get("stop", ()))
+    d = program_to_desc(lp)
+    dopt = program_to_desc(program, ops=opt)
+    for od in dopt["blocks"][0]["ops"]:
+        if not any(a["name"] == "op_role" for a in od["attrs"]):
+            od["attrs"].append({"name": "op_role", "type": proto.ATTR["INT"], "i": OPTIMIZE})
+    blk = d["blocks"][0]
+    have = {v["name"] for v in blk["vars"]}
+    for v in dopt["blocks"][0]["vars"]:
+        if v["name"] not in have:
+            have.add(v["name"])
+            blk["vars"].append(v)
+    blk["ops"].extend(dopt["blocks"][0]["ops"])
+    return d
+
+
+def _opt_names(program):
+    """Persistables that are not model parameters (optimizer accumulators, learning rate)."""
+    return sorted(getattr(program, "_opt_vars", ()))
+
+
 def save(program, model_path, protocol=4, **configs):
+    """Reference `python/paddle/static/io.py` ``save``: ``.pdparams`` (parameters), ``.pdopt``
+    (optimizer accumulators + learning rate) and ``.pdmodel`` (the whole program; a training
+    program through :func:`train_program_desc`)."""
     from ..framework.io import save as _save
     from .framework import global_scope
     scope = global_scope()
+    d = os.path.dirname(model_path)
+    if d:
+        os.makedirs(d, exist_ok=True)
+    opt = set(_opt_names(program))
     state = {n: (scope.get(n) if scope.get(n) is not None else t) for n, t in program.params.items()}
-    _save(state, model_path + ".pdparams")
+    _save({n: t for n, t in state.items() if n not in opt}, model_path + ".pdparams")
+    _save({n: t for n, t in state.items() if n in opt}, model_path + ".pdopt")
+    desc = train_program_desc(program) if getattr(program, "_backward_info", None) else program_to_desc(program)
+    with open(model_path + ".pdmodel", "wb") as f:
+        f.write(proto.encode("ProgramDesc", desc))
 
 
 def load(program, model_path, executor=None, var_list=None):
+    """Reference ``paddle.static.load``: parameters and optimizer state into ``program``'s
+    persistables (and the global Scope)."""
     from ..framework.io import load as _load
-    from .framework import global_scope
-    state = _load(model_path + ".pdparams")
-    set_program_state(program, state)
+    state = dict(_load(model_path + ".pdparams"))
+    if os.path.exists(model_path + ".pdopt"):
+        state.update(_load(model_path + ".pdopt"))
+    set_program_state(program, state, executor)
 
 
 def load_program_state(model_path, var_list=None):
@@ -471,14 +528,20 @@ def load_program_state(model_path, var_list=None):
     return _load(model_path + ".pdparams" if not model_path.endswith(".pdparams") else model_path)
 
 
-def set_program_state(program, state_dict):
+def set_program_state(program, state_dict, executor=None):
     from .framework import global_scope
     scope = global_scope()
+    b = program.global_block()
     for n, v in state_dict.items():
-        if n in program.params:
+        if n in program.params or n in b.vars:
             t = torch.as_tensor(v)
             program.params[n] = t
             cur = scope.get(n)
             if cur is not None:
                 with torch.no_grad():
                     cur.copy_(t.to(cur.dtype))
+            elif executor is not None:
+                t = t.to(executor.device).clone()
+                if t.is_floating_point() and (n + "@GRAD") in b.vars:
+                    t.requires_grad_(True)
+                scope.set(n, t)

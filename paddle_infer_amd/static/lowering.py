@@ -233,6 +233,17 @@ def _unary(ctx, op):
 RULES.update({f: _unary for f in _UNARY})
 
 
+@rule(torch.clamp, T.clamp, torch.clip, T.clip)
+def _clamp(ctx, op):
+    """Reference `clip` op (phi clip_kernel): min / max attributes, one side may be open."""
+    lo, hi = _arg(op, 1, "min", None), _arg(op, 2, "max", None)
+    if _is_var(lo) or _is_var(hi):
+        raise LoweringError("clamp with tensor bounds")
+    big = 3.4e38
+    return [("clip", {"X": [_name(op.args[0])]}, {"Out": [_outs(op)[0]]},
+             {"min": float(-big if lo is None else lo), "max": float(big if hi is None else hi)})]
+
+
 @rule(F.leaky_relu)
 def _leaky(ctx, op):
     return [("leaky_relu", {"X": [_name(op.args[0])]}, {"Out": [_outs(op)[0]]},

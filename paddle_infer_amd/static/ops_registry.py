@@ -596,3 +596,79 @@ def _fc_eltwise_ln(ins, a):
     return {"Out": out}
 
 
+
+
+# ------------------------------------------------------------------------ backward / optimizer ops
+@register("sum")
+def _sum(ins, a):
+    xs = [x for x in ins["X"] if x is not None]
+    out = xs[0]
+    for x in xs[1:]:
+        out = out + x
+    return {"Out": out}
+
+
+@register("fill_zeros_like")
+def _fill_zeros_like(ins, a):
+    return {"Out": torch.zeros_like(ins["X"][0])}
+
+
+def _lr(ins):
+    return ins["LearningRate"][0].reshape(()).float()
+
+
+def _reg(p, g, a):
+    # reference optimizer ops: regularization_method "l2_decay" adds coeff * param to the gradient
+    if a.get("regularization_method") == "l2_decay" and a.get("regularization_coeff"):
+        return g + float(a["regularization_coeff"]) * p
+    return g
+
+
+@register("sgd")
+def _sgd(ins, a):
+    """Reference `phi/kernels/gpu/sgd_kernel.cu`: ParamOut = Param - lr * Grad (in place)."""
+    p, g = ins["Param"][0], ins["Grad"][0]
+    gf = _reg(p, g.to(p.dtype), a)
+    p.sub_(_lr(ins).to(p.dtype) * gf)
+    return {"ParamOut": p}
+
+
+@register("momentum")
+def _momentum(ins, a):
+    """Reference `phi/kernels/impl/momentum_kernel_impl.h`: v = mu v + g; p -= lr (g + mu v) | lr v."""
+    p, g, v = ins["Param"][0], ins["Grad"][0], ins["Velocity"][0]
+    mu = float(a.get("mu", 0.9))
+    gf = _reg(p, g.float() * float(a.get("rescale_grad", 1.0)), a)
+    v.mul_(mu).add_(gf)
+    lr = _lr(ins)
+    upd = gf + mu * v if a.get("use_nesterov") else v
+    p.sub_((lr * upd).to(p.dtype))
+    return {"ParamOut": p, "VelocityOut": v}
+
+
+@register("adam", "adamw")
+def _adam(ins, a):
+    """Reference `phi/kernels/gpu/adam_kernel.cu` / `adamw_kernel.cu` (beta pow accumulators carried
+    as [1] tensors, updated in place; AdamW decays the parameter by lr * coeff first)."""
+    p, g = ins["Param"][0], ins["Grad"][0]
+    m1, m2 = ins["Moment1"][0], ins["Moment2"][0]
+    b1p, b2p = ins["Beta1Pow"][0], ins["Beta2Pow"][0]
+    b1, b2, eps = float(a.get("beta1", 0.9)), float(a.get("beta2", 0.999)), float(a.get("epsilon", 1e-8))
+    lr = _lr(ins) * float(a.get("lr_ratio", 1.0))
+    gf = _reg(p, g.float(), a)
+    if a.get("with_decay") and a.get("coeff"):
+        p.mul_((1.0 - lr * float(a["coeff"])).to(p.dtype))
+    m1.mul_(b1).add_(gf, alpha=1 - b1)
+    m2.mul_(b2).addcmul_(gf, gf, value=1 - b2)
+    bc1 = 1 - b1p.reshape(()).float()
+    bc2 = torch.sqrt(1 - b2p.reshape(()).float())
+    step = lr * bc2 / bc1
+    p.sub_((step * m1 / (m2.sqrt() + eps * bc2)).to(p.dtype))
+    b1p.mul_(b1)
+    b2p.mul_(b2)
+    return {"ParamOut": p, "Moment1Out": m1, "Moment2Out": m2, "Beta1PowOut": b1p, "Beta2PowOut": b2p}
+
+
+@register("clip")
+def _clip_op(ins, a):
+    return {"Out": torch.clamp(ins["X"][0], float(a.get("min", -3.4e38)), float(a.get("max", 3.4e38)))}

@@ -3,7 +3,9 @@
 * ``_lib/libpiamd_kernels.so`` — every ``csrc/kernels/*.hip`` compiled for gfx950 with hipcc
   (C ABI, loaded with ctypes AFTER torch so it binds to the HIP runtime torch already loaded).
 * ``_lib/libpiamd_runtime.so`` — the C++ host runtime (``csrc/runtime/*.cc``: static-graph
-  executor scheduler, data-loader ring, memory-plan) built with g++.
+  executor scheduler, data-loader ring) built with g++.
+* ``_lib/libpiamd_capi.so`` — the C inference API (``csrc/capi``: reference ``capi_exp``
+  ``pd_inference_api.h``), g++ against the embedded Python runtime.
 
 Incremental: an object is rebuilt only when its source (or a header in the same dir) is newer.
 Run ``python -m paddle_infer_amd._build`` or ``__graft_entry__.build()``.
@@ -24,6 +26,8 @@ LIBDIR = os.path.join(ROOT, "_lib")
 OBJDIR = os.path.join(ROOT, "_lib", "obj")
 KERNEL_LIB = os.path.join(LIBDIR, "libpiamd_kernels.so")
 RUNTIME_LIB = os.path.join(LIBDIR, "libpiamd_runtime.so")
+CDIR = os.path.join(ROOT, "csrc", "capi")
+CAPI_LIB = os.path.join(LIBDIR, "libpiamd_capi.so")
 ARCH = os.environ.get("PIAMD_ARCH", "gfx950")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
@@ -91,6 +95,15 @@ def build(verbose: bool = True, jobs: int | None = None) -> None:
     if rsrcs:
         _build_lib(rsrcs, RUNTIME_LIB, "g++", CXX_FLAGS, ["-pthread"], _newest_header(RDIR),
                    verbose, jobs)
+    csrcs = sorted(glob.glob(os.path.join(CDIR, "*.cc")))
+    if csrcs:
+        import sysconfig
+        inc = sysconfig.get_paths()["include"]
+        ver = sysconfig.get_config_var("LDVERSION") or sysconfig.get_python_version()
+        libdir = sysconfig.get_config_var("LIBDIR") or "/usr/lib"
+        _build_lib(csrcs, CAPI_LIB, "g++", CXX_FLAGS + [f"-I{inc}"],
+                   ["-pthread", f"-L{libdir}", f"-lpython{ver}", "-ldl", f"-Wl,-rpath,{libdir}"],
+                   _newest_header(CDIR), verbose, jobs)
 
 
 if __name__ == "__main__":

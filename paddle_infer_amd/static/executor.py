@@ -116,6 +116,9 @@ class Executor:
         self._init_params(program, scope)
         if program is default_startup_program() or not program.global_block().ops:
             return []
+        from ..incubate.checkpoint import auto_checkpoint as _acp
+        if _acp.current_range() is not None:  # register / restore inside train_epoch_range
+            _acp._auto_checkpoint(self, program)
         fetch_list = fetch_list or []
         fetch_names = [f.var_name if isinstance(f, Variable) else str(f) for f in fetch_list]
         ops = program.global_block().ops

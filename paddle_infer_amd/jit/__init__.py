@@ -3,10 +3,12 @@
 Parity: reference `python/paddle/fluid/dygraph/jit.py` (declarative:164, save:690, load:1127,
 TracedLayer:1388) and `fluid/dygraph/io.py` (TranslatedLayer).
 
-MI355X design: there is no AST transcompiler. ``to_static`` keeps dygraph execution (the same HIP
-kernels, autograd intact) and adds the two things a static program is used for:
+MI355X design: ``to_static`` keeps dygraph execution (the same HIP kernels, autograd intact) and
+adds the two things a static program is used for:
 * ``concrete_program`` / ``jit.save``: the forward is *recorded* into a static Program by running
-  it on meta-backed Variables (`static/framework.py`); dynamic dims of the InputSpec stay symbolic;
+  it on meta-backed Variables (`static/framework.py`) after the AST conversion of its Python
+  control flow (`dy2static.py`: tensor-dependent ``if`` / ``while`` / ``for range`` become
+  ``cond`` / ``while`` ops with sub-blocks); dynamic dims of the InputSpec stay symbolic;
   the Program is written as a Paddle-wire ``.pdmodel`` + ``.pdiparams`` that ``jit.load`` and
   ``inference.create_predictor`` read back.
 * ``to_static(..., capture=True)``: the call is captured into a hipGraph per input signature
@@ -75,6 +77,8 @@ def _spec_of(x, i):
 def trace_program(fn, input_spec, layer=None):
     """Record ``fn(*inputs)`` into a static Program. Returns (program, feed_vars, fetch_vars)."""
     specs = [_spec_of(s, i) for i, s in enumerate(input_spec)]
+    from .dy2static import convert_to_static
+    fn = convert_to_static(fn)
     main, startup = _static.Program(), _static.Program()
     was_training = layer.training if layer is not None else None
     if layer is not None:

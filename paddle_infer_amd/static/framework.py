@@ -304,7 +304,24 @@ class Program:
         return self.blocks[0]
 
     def current_block(self):
-        return self.blocks[-1]
+        return self.blocks[getattr(self, "_cur_block", 0)]
+
+    def _create_block(self, parent_idx=None):
+        """A sub-block (body of a control-flow op: reference `Program._create_block`)."""
+        parent = self._cur_block if parent_idx is None and hasattr(self, "_cur_block") else (parent_idx or 0)
+        b = Block(self, len(self.blocks), parent)
+        self.blocks.append(b)
+        return b
+
+    @contextlib.contextmanager
+    def _block_guard(self, block):
+        """Record ops into ``block`` (tracing a control-flow branch / loop body)."""
+        prev = getattr(self, "_cur_block", 0)
+        self._cur_block = block.idx
+        try:
+            yield block
+        finally:
+            self._cur_block = prev
 
     def block(self, idx):
         return self.blocks[idx]
@@ -417,7 +434,7 @@ def _record(func, args, kwargs):
         return x
     tree_map(find, (args, kwargs))
     prog = prog or default_main_program()
-    block = prog.global_block()
+    block = prog.current_block()
 
     def to_meta(x):
         if isinstance(x, Variable):

@@ -236,6 +236,9 @@ def program_to_desc(program: Program, feed_names=None, fetch_names=None, ops=Non
     """``paddle_ops``: lower recorded ops to Paddle OpDescs (`lowering.py`); an op no rule covers
     raises ``LoweringError`` unless ``allow_custom_ops`` keeps it in recorded (callable) form."""
     from .lowering import lower, LoweringError
+    if any(op.type in ("cond", "while") and op.func is None for op in (ops or program.global_block().ops)):
+        raise LoweringError("programs with cond / while sub-blocks run in the Executor but are not "
+                            "serialisable to a .pdmodel yet")
     b = program.global_block()
     ops = b.ops if ops is None else ops
     used = set()

@@ -101,24 +101,29 @@ def create_parameter(shape, dtype="float32", name=None, attr=None, is_bias=False
 
 
 def cond(pred, true_fn=None, false_fn=None, name=None, return_names=None):
-    """Both branches are recorded and the result selected element-wise by ``pred`` (the
-    reference's `conditional_block` pair, flattened — branch bodies here are side-effect free)."""
+    """Reference `layers/control_flow.py` cond: a Python bool / concrete tensor picks a branch
+    eagerly; a Program Variable records a ``cond`` op with one sub-block per branch
+    (`control_flow.py`) and the Executor runs only the branch the predicate selects."""
     if not isinstance(pred, Variable):
-        return true_fn() if bool(pred) else (false_fn() if false_fn else None)
-    t, f = true_fn(), false_fn()
-    if isinstance(t, (list, tuple)):
-        return type(t)(torch.where(pred, a, b) for a, b in zip(t, f))
-    return torch.where(pred, t, f)
+        p = bool(pred.reshape(-1)[0]) if isinstance(pred, torch.Tensor) else bool(pred)
+        return (true_fn() if true_fn else None) if p else (false_fn() if false_fn else None)
+    from .control_flow import cond as _cond
+    return _cond(pred, true_fn, false_fn)
 
 
 def while_loop(cond, body, loop_vars, is_test=False, name=None):  # noqa: A002
-    """Runs eagerly on concrete values; a symbolic loop condition is not traceable in a
-    meta-recorded Program (use ``jit.to_static`` on a dygraph function instead)."""
+    """Reference `layers/control_flow.py` while_loop: concrete values loop eagerly; Program
+    Variables record a ``while`` op (condition block + body block, loop-carried variables)."""
+    loop_vars = list(loop_vars)
     if any(isinstance(v, Variable) for v in loop_vars):
-        raise NotImplementedError("while_loop over symbolic Variables: write the loop in dygraph "
-                                  "and export with jit.save (the trace unrolls it)")
-    while bool(cond(*loop_vars)):
-        loop_vars = body(*loop_vars)
+        from .control_flow import while_loop as _while
+        return _while(cond, body, loop_vars)
+    while True:
+        c = cond(*loop_vars)
+        if not (bool(c.reshape(-1)[0]) if isinstance(c, torch.Tensor) else bool(c)):
+            break
+        out = body(*loop_vars)
+        loop_vars = list(out) if isinstance(out, (list, tuple)) else [out]
     return loop_vars
 
 

@@ -458,6 +458,150 @@ __global__ __launch_bounds__(256) void conv_splitk_finish(const float* __restric
   *reinterpret_cast<u16x4*>(y + i) = o;
 }
 
+// ---- implicit-GEMM convolution weight gradient (NHWC, bf16) -----------------------------------
+// Parity: reference `phi/kernels/gpudnn/conv_grad_kernel.cu:666` (cuDNN backward-filter). Here
+// D[q = (r, s, c)][k] = Σ_m X[pixel(m, r, s)][c] · dY[m][k] over every output pixel m = (n, oh, ow)
+// — a GEMM whose reduction runs over the N·OH·OW output pixels, with D in HWIO order [R][S][C][K].
+// Both operands are reduction-major (!KC) LDS images [64 pixels][cols], read with the hardware
+// transpose ds_read_b64_tr_b16:
+//   * A (M' = the R·S·C filter taps × channels, 256 per tile): gathered by the LDS DMA, each 16-B
+//     chunk (8 channels of ONE tap — C % 8 == 0) from the input pixel the tap sees, so a tile packs
+//     several taps when C < 256 (a 64-channel 3×3 layer fills 576 rows = 2¼ tiles instead of 9
+//     quarter-empty ones); out-of-image taps and pixels past the end read the zero row;
+//   * B (N' = K_out, tile TN ∈ {64, 128, 256}): dY rows, plain DMA (K_out % TN == 0);
+//   * the reduction (hundreds of thousands of pixels) is split over `ksplit` workgroups per output
+//     tile writing f32 partial planes ws[part][RSC][K_out]; conv_splitk_finish-style fixed-order
+//     sum (deterministic) into the f32 D.
+// pixel(m): m → (n, oh, ow) by an f32 reciprocal with one integer correction (M < 2^24).
+struct ConvWgradGeom {
+  int N, H, W, C, OH, OW, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w;
+  int M, RSC, Kout;
+  float inv_ow, inv_ohw;
+};
+
+template <int WM, int MB, int NB>
+__global__ __launch_bounds__(NTHR, 1) void conv_wgrad_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, const bf16_t* __restrict__ zero,
+    float* __restrict__ out, int ksplit, ConvWgradGeom g) {
+  constexpr int WC = NWAVE / WM, TN = WC * NB * 32;
+  constexpr int A_BYTES = 64 * 512, B_BYTES = 64 * TN * 2, SBYTES = A_BYTES + B_BYTES;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * SBYTES];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w / WC, wc = w % WC;
+  const int tm = (g.RSC + BM - 1) / BM, tn = g.Kout / TN;
+  const int wg = xcd_remap(blockIdx.x, tm * tn * ksplit);
+  const int part = wg % ksplit, tile = wg / ksplit;
+  const int m0 = (tile / tn) * BM, n0 = (tile % tn) * TN;
+  const int nk_all = (g.M + 63) / 64;
+  const int kt0 = (int)((long long)nk_all * part / ksplit);
+  const int kt1 = (int)((long long)nk_all * (part + 1) / ksplit);
+
+  // A gather: this lane's 4 pieces (2 pixels × 512 B each); per piece a fixed pixel row r of the
+  // 64-pixel step and a fixed 8-channel chunk (tap offset dh/dw, channel c) — k-step invariant
+  constexpr int PPW = 4;
+  int prow[PPW], pc_off[PPW], pdh[PPW], pdw[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int P = w * PPW + i, L = P * 64 + lane, r = L >> 5, pc = L & 31;
+    const int xsw = ((r & 3) << 2) | ((r >> 2) & 3);
+    const int q = m0 + ((pc ^ xsw) << 3);
+    prow[i] = r;
+    if (q < g.RSC) {
+      const int tap = q / g.C, c = q - tap * g.C;
+      const int rr = tap / g.S, ss = tap - rr * g.S;
+      pc_off[i] = c;
+      pdh[i] = rr * g.dil_h - g.pad_h;
+      pdw[i] = ss * g.dil_w - g.pad_w;
+    } else {
+      pc_off[i] = -1;
+      pdh[i] = pdw[i] = 0;
+    }
+  }
+  const int ohw = g.OH * g.OW;
+  auto stage_load = [&](int kt, int s) {
+    char* ai = smem + s * SBYTES;
+    char* bi = ai + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int m = kt * 64 + prow[i];
+      int n = (int)((float)m * g.inv_ohw);
+      int rem = m - n * ohw;
+      if (rem < 0) { --n; rem += ohw; } else if (rem >= ohw) { ++n; rem -= ohw; }
+      int oh = (int)((float)rem * g.inv_ow);
+      int ow = rem - oh * g.OW;
+      if (ow < 0) { --oh; ow += g.OW; } else if (ow >= g.OW) { ++oh; ow -= g.OW; }
+      const int ih = oh * g.st_h + pdh[i], iw = ow * g.st_w + pdw[i];
+      const bool ok = m < g.M && pc_off[i] >= 0 && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+      const bf16_t* src = ok ? x + (((long long)n * g.H + ih) * g.W + iw) * g.C + pc_off[i] : zero;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(ai + (w * PPW + i) * 1024),
+                                       16, 0, 0);
+    }
+    // dY rows past the end are clamped (finite data against the zero A rows)
+    dma_tile<64, TN * 2>(dy + n0, g.Kout, kt * 64, g.M - 1, bi, w, lane);
+  };
+
+  f32x16 acc[MB][NB];
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  if (kt1 > kt0) {
+    stage_load(kt0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  const int gi = lane & 15, hi = lane >> 5, half16 = (lane >> 4) & 1;
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int s = (kt - kt0) & 1;
+    if (kt + 1 < kt1) stage_load(kt + 1, s ^ 1);
+    const char* ai = smem + s * SBYTES;
+    const char* bi = ai + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8 af[MB], bf[NB];
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) {
+        const int mrow = wr * (32 * MB) + mb * 32;
+        af[mb] = cat44(rd_tr4<512>(ai, 16 * ks + 8 * hi, mrow + 16 * half16, gi),
+                       rd_tr4<512>(ai, 16 * ks + 8 * hi + 4, mrow + 16 * half16, gi));
+      }
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const int ncol = wc * (32 * NB) + nb * 32;
+        bf[nb] = cat44(rd_tr4<TN * 2>(bi, 16 * ks + 8 * hi, ncol + 16 * half16, gi),
+                       rd_tr4<TN * 2>(bi, 16 * ks + 8 * hi + 4, ncol + 16 * half16, gi));
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+          acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[nb], af[mb], acc[mb][nb], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  gemm_epilogue<WM, MB, NB>(acc, out + (long long)part * g.RSC * g.Kout, g.Kout, 1, 0, m0, g.RSC,
+                            n0, g.Kout, EPI_STORE, 0, nullptr, nullptr, 0);
+}
+
+// D (+)= Σ_p ws[p] in a fixed order (f32, 4 per thread)
+__global__ __launch_bounds__(256) void wgrad_splitk_finish(const float* __restrict__ ws, int ksplit,
+                                                           long long MN, float* __restrict__ d,
+                                                           int accumulate) {
+  const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= MN) return;
+  f32x4 v = *reinterpret_cast<const f32x4*>(ws + i);
+  for (int p = 1; p < ksplit; ++p) v += *reinterpret_cast<const f32x4*>(ws + p * MN + i);
+  f32x4* o = reinterpret_cast<f32x4*>(d + i);
+  if (accumulate) v += *o;
+  *o = v;
+}
+
 // ---- int8 × int8 → int32 GEMM with dequantising epilogue -------------------------------------
 // Parity: reference `fused_multi_transformer_int8_op.cu` / `attn_gemm_int8.h` (cublasLt int8
 // igemm between quantised activations and int8 weights, dequantised with per-channel out scales)
@@ -639,6 +783,49 @@ PIAMD_EXPORT int piamd_conv2d_fwd(const void* x, const void* wt, const void* zer
     const long long MN = M * Kout;
     hipLaunchKernelGGL(conv_splitk_finish, dim3((unsigned)((MN / 4 + 255) / 256)), dim3(256), 0,
                        st, wsf, ksplit, MN, Kout, act, bb, (bf16_t*)y);
+  }
+  return (int)hipGetLastError();
+}
+
+// NHWC implicit-GEMM convolution weight gradient: x [N][H][W][C], dy [N][OH][OW][Kout] bf16 →
+// d [R][S][C][Kout] f32 (HWIO; accumulate adds into d). zero: ≥ 16 zero bytes. C % 8 == 0,
+// Kout % tile_n == 0 (tile_n ∈ {64, 128, 256}), N·OH·OW < 2^24; ksplit > 1 needs ws with
+// ksplit·R·S·C·Kout floats (ksplit == 1 writes d directly and requires accumulate == 0).
+PIAMD_EXPORT int piamd_conv2d_wgrad(const void* x, const void* dy, const void* zero, float* d, int N,
+                                    int H, int W, int C, int OH, int OW, int R, int S, int st_h,
+                                    int st_w, int pad_h, int pad_w, int dil_h, int dil_w, int Kout,
+                                    int tile_n, int ksplit, float* ws, int accumulate,
+                                    hipStream_t st) {
+  const long long M = (long long)N * OH * OW;
+  const long long RSC = (long long)R * S * C;
+  if (C % 8 || Kout % tile_n || N < 1 || OH < 1 || OW < 1 || R < 1 || S < 1 || !zero ||
+      ksplit < 1 || (ksplit > 1 && !ws) || (ksplit == 1 && accumulate) || M >= (1LL << 24) ||
+      RSC * Kout >= (1LL << 31) || ksplit > (M + 63) / 64)
+    return (int)hipErrorInvalidValue;
+  ConvWgradGeom g{N, H, W, C, OH, OW, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w,
+                  (int)M, (int)RSC, Kout, 1.f / (float)OW, 1.f / (float)(OH * OW)};
+  const int tm = (int)((RSC + BM - 1) / BM);
+  const long long wgs = (long long)tm * (Kout / tile_n) * ksplit;
+  if (wgs > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  float* out = ksplit > 1 ? ws : d;
+  const auto xb = (const bf16_t*)x;
+  const auto db = (const bf16_t*)dy;
+  const auto zb = (const bf16_t*)zero;
+  if (tile_n == 64)
+    hipLaunchKernelGGL((conv_wgrad_kernel<8, 1, 2>), dim3((unsigned)wgs), dim3(NTHR), 0, st, xb, db,
+                       zb, out, ksplit, g);
+  else if (tile_n == 128)
+    hipLaunchKernelGGL((conv_wgrad_kernel<4, 2, 2>), dim3((unsigned)wgs), dim3(NTHR), 0, st, xb, db,
+                       zb, out, ksplit, g);
+  else if (tile_n == 256)
+    hipLaunchKernelGGL((conv_wgrad_kernel<2, 4, 2>), dim3((unsigned)wgs), dim3(NTHR), 0, st, xb, db,
+                       zb, out, ksplit, g);
+  else
+    return (int)hipErrorInvalidValue;
+  if (ksplit > 1) {
+    const long long MN = RSC * Kout;
+    hipLaunchKernelGGL(wgrad_splitk_finish, dim3((unsigned)((MN / 4 + 255) / 256)), dim3(256), 0, st,
+                       (const float*)ws, ksplit, MN, d, accumulate);
   }
   return (int)hipGetLastError();
 }

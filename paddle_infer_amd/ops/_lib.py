@@ -234,3 +234,6 @@ _SIGS["piamd_bn_fwd"] = ([c_int, c_int] + [c_void_p] * 3 + [c_int] * 3 + [c_void
 # dtype, nhwc, dy, y, x, dx, dres, N, C, S, gamma, mean, rstd, dgamma, dbeta, training, act, ws, stream
 _SIGS["piamd_bn_bwd"] = ([c_int, c_int] + [c_void_p] * 5 + [c_int] * 3 + [c_void_p] * 5
                          + [c_int, c_int, c_void_p, c_void_p])
+# x, dy, zero, d, N, H, W, C, OH, OW, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w, Kout, tile_n,
+# ksplit, ws, accumulate, stream
+_SIGS["piamd_conv2d_wgrad"] = [c_void_p] * 4 + [c_int] * 17 + [c_void_p, c_int, c_void_p]

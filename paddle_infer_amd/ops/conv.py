@@ -94,6 +94,97 @@ def _launch(x, w_ohwi, bias, st, pad, dil, act):
     return y
 
 
+def _wgrad_plan(M, RSC, K):
+    """(tile_n, ksplit) for the weight-gradient kernel: the widest tile dividing K_out, then split
+    the N·OH·OW reduction until the grid holds ~512 workgroups (each part ≥ 8 pixel steps of 64)
+    while the f32 partial planes stay under 256 MiB."""
+    tn = 256 if K % 256 == 0 else 128 if K % 128 == 0 else 64
+    tiles = -(-RSC // 256) * (K // tn)
+    nk = -(-M // 64)
+    ks = 1
+    while tiles * ks < 512 and nk // (ks * 2) >= 8 and 2 * ks * RSC * K * 4 <= (256 << 20):
+        ks *= 2
+    return tn, ks
+
+
+WGRAD_PLAN_OVERRIDE = None
+
+
+def wgrad_eligible(C, K, M) -> bool:
+    return C % 8 == 0 and K % 64 == 0 and M < (1 << 24)
+
+
+def conv2d_wgrad(x, dy, R, S, st, pad, dil):
+    """dW [K][C][R][S] f32 of conv(x [N,H,W,C], ·) given dy [N,OH,OW,K] (both bf16 NHWC
+    contiguous) on the HIP implicit-GEMM weight-gradient kernel."""
+    N, H, W, C = x.shape
+    _, OH, OW, K = dy.shape
+    M, RSC = N * OH * OW, R * S * C
+    if not wgrad_eligible(C, K, M):
+        raise ValueError(f"conv2d_wgrad: unsupported C={C} K={K} M={M}")
+    tn, ks = WGRAD_PLAN_OVERRIDE or _wgrad_plan(M, RSC, K)
+    ks = max(1, min(ks, -(-M // 64)))
+    d = torch.empty(R, S, C, K, dtype=torch.float32, device=x.device)
+    ws = torch.empty(ks * RSC * K, dtype=torch.float32, device=x.device) if ks > 1 else None
+    _lib.call("piamd_conv2d_wgrad", x.data_ptr(), dy.data_ptr(), _zero(x.device).data_ptr(),
+              d.data_ptr(), N, H, W, C, OH, OW, R, S, st[0], st[1], pad[0], pad[1], dil[0], dil[1],
+              K, tn, ks, _lib.ptr(ws), 0, _lib.stream())
+    return d.permute(3, 2, 0, 1)
+
+
+def _phase_taps(R, st, pad, dil, ph):
+    """Taps r of a strided conv that reach input rows ih ≡ ph (mod st), as a stride-1 sub-conv over
+    dY: returns (taps in sub-filter order, pad', dil') with dX[ph + st·i] = Σ_t dY[i − pad' + t·dil']
+    · W[taps[t]], or None when no tap reaches that phase."""
+    rs = [r for r in range(R) if (ph + pad - r * dil) % st == 0]
+    if not rs:
+        return None
+    d = [(ph + pad - r * dil) // st for r in rs]  # dY row offset of each tap (decreasing)
+    taps = rs[::-1]
+    dd = d[::-1]
+    dil2 = dd[1] - dd[0] if len(dd) > 1 else 1
+    return taps, -dd[0], dil2
+
+
+def conv2d_dgrad_strided(dy, weight, H, W, st, pad, dil):
+    """dX [N,H,W,C] bf16 of a strided conv: one stride-1 HIP convolution per output phase
+    (ih mod st_h, iw mod st_w) over dY with the sub-filter of the taps that reach that phase,
+    scattered into dX (phases with no tap are zero)."""
+    N, OH, OW, K = dy.shape
+    Kw, C, R, S = weight.shape
+    dx = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=dy.device)
+    wb = weight.to(torch.bfloat16)
+    for ph in range(st[0]):
+        for pw in range(st[1]):
+            Hp, Wp = -(-(H - ph) // st[0]), -(-(W - pw) // st[1])
+            if Hp <= 0 or Wp <= 0:
+                continue
+            th, tw = _phase_taps(R, st[0], pad[0], dil[0], ph), _phase_taps(S, st[1], pad[1], dil[1], pw)
+            if th is None or tw is None:
+                dx[:, ph::st[0], pw::st[1], :] = 0
+                continue
+            (rt, ph2, dh2), (stp, pw2, dw2) = th, tw
+            # sub-filter [C][R'][S'][K]: W[k][c][rt[i]][stp[j]]
+            wsub = wb[:, :, rt][:, :, :, stp].permute(1, 2, 3, 0).contiguous()
+            y = _launch_geom(dy, wsub, (1, 1), (ph2, pw2), (dh2, dw2), Hp, Wp)
+            dx[:, ph::st[0], pw::st[1], :] = y
+    return dx
+
+
+def _launch_geom(x, w_ohwi, st, pad, dil, OH, OW):
+    """conv_fwd with an explicit output size (pads may be negative: taps outside are skipped)."""
+    N, H, W, C = x.shape
+    K, R, S, _ = w_ohwi.shape
+    M = N * OH * OW
+    tn, ks = _plan(M, K, R * S * (C // 64))
+    y = torch.empty(N, OH, OW, K, dtype=torch.bfloat16, device=x.device)
+    ws = torch.empty(ks * M * K, dtype=torch.float32, device=x.device) if ks > 1 else None
+    _lib.call("piamd_conv2d_fwd", x.data_ptr(), w_ohwi.data_ptr(), _zero(x.device).data_ptr(),
+              y.data_ptr(), N, H, W, C, OH, OW, R, S, st[0], st[1], pad[0], pad[1], dil[0], dil[1],
+              K, 0, 0, tn, ks, _lib.ptr(ws), _lib.stream())
+    return y
+
+
 class _Conv2dNHWC(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, st, pad, dil, act):
@@ -114,21 +205,29 @@ class _Conv2dNHWC(torch.autograd.Function):
         dy = dy.contiguous()
         K, C, R, S = weight.shape
         dx = dw = db = None
+        N, H, W, _ = x.shape
         if ctx.needs_input_grad[0]:
             pad_t = (dil[0] * (R - 1) - pad[0], dil[1] * (S - 1) - pad[1])
-            if st == (1, 1) and K % 64 == 0 and C % 4 == 0 and min(pad_t) >= 0:
+            if K % 64 == 0 and C % 4 == 0 and st == (1, 1) and dy.shape[1:3] == (H, W):
                 # dX = conv(dY, flip(W)ᵀ): filter [C][R][S][K] = W[k][c][R-1-r][S-1-s]
                 w_t = weight.to(torch.bfloat16).flip(2, 3).permute(1, 2, 3, 0).contiguous()
-                dx = _launch(dy, w_t, None, (1, 1), pad_t, dil, 0)
+                dx = _launch_geom(dy, w_t, (1, 1), pad_t, dil, H, W)
+            elif K % 64 == 0 and C % 4 == 0:
+                dx = conv2d_dgrad_strided(dy, weight, H, W, st, pad, dil)
             else:
+                _lib.fallback("conv2d_dgrad", f"K_out={K} C={C} (needs K%64, C%4)")
                 dx = torch.ops.aten.convolution_backward(
                     dy.permute(0, 3, 1, 2), x.permute(0, 3, 1, 2), weight.to(torch.bfloat16),
                     None, list(st), list(pad), list(dil), False, [0, 0], 1,
                     [True, False, False])[0].permute(0, 2, 3, 1)
         if ctx.needs_input_grad[1]:
-            dw = torch.ops.aten.convolution_backward(
-                dy.permute(0, 3, 1, 2), x.permute(0, 3, 1, 2), weight.to(torch.bfloat16), None,
-                list(st), list(pad), list(dil), False, [0, 0], 1, [False, True, False])[1]
+            if wgrad_eligible(C, K, dy.shape[0] * dy.shape[1] * dy.shape[2]):
+                dw = conv2d_wgrad(x, dy, R, S, st, pad, dil)
+            else:
+                _lib.fallback("conv2d_wgrad", f"K_out={K} C={C} (needs K%64, C%8)")
+                dw = torch.ops.aten.convolution_backward(
+                    dy.permute(0, 3, 1, 2), x.permute(0, 3, 1, 2), weight.to(torch.bfloat16), None,
+                    list(st), list(pad), list(dil), False, [0, 0], 1, [False, True, False])[1]
             dw = dw.to(weight.dtype)
         if has_bias and ctx.needs_input_grad[2]:
             db = dy.float().sum((0, 1, 2))

@@ -359,7 +359,20 @@ __global__ __launch_bounds__(256) void bn_stats_nhwc8(const T* __restrict__ x, l
     for (int j = 0; j < 8; ++j) sh[j] = s[j] = q[j] = 0.f;
     if (live) {
       ld8(x + beg * C + cg * 8, sh);
-      for (long long r = beg + rl; r < end; r += RB) {
+      long long r = beg + rl;
+      // 4 rows per trip: four independent 16-B loads in flight per lane (the single-row loop
+      // was load-latency bound at ~5 TB/s against ~12 TB/s for the apply pass)
+      for (; r + 3 * RB < end; r += 4 * RB) {
+        float v[4][8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ld8(x + (r + u * RB) * C + cg * 8, v[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { const float d = v[u][j] - sh[j]; s[j] += d; q[j] += d * d; }
+        n += 4.f;
+      }
+      for (; r < end; r += RB) {
         float v[8];
         ld8(x + r * C + cg * 8, v);
 #pragma unroll
@@ -424,7 +437,29 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_nhwc8(const T* __restrict__
 #pragma unroll
     for (int j = 0; j < 8; ++j) { s1[j] = s2[j] = 0.f; mu[j] = live ? mean[cg * 8 + j] : 0.f; }
     if (live) {
-      for (long long r = beg + rl; r < end; r += RB) {
+      long long r = beg + rl;
+      // 2 rows per trip (4 or 6 independent 16-B loads in flight per lane)
+      for (; r + RB < end; r += 2 * RB) {
+        float g[2][8], xv[2][8], yv[2][8];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const long long i = (r + u * RB) * C + cg * 8;
+          ld8(dy + i, g[u]);
+          ld8(x + i, xv[u]);
+          if (act) ld8(y + i, yv[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          if (act) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              if (!(act == 1 ? yv[u][j] > 0.f : (yv[u][j] > 0.f && yv[u][j] < 6.f))) g[u][j] = 0.f;
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { s1[j] += g[u][j]; s2[j] += g[u][j] * (xv[u][j] - mu[j]); }
+        }
+      }
+      for (; r < end; r += RB) {
         const long long i = r * C + cg * 8;
         float g[8], xv[8];
         ld8(dy + i, g);

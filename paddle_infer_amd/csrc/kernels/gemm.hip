@@ -328,7 +328,10 @@ struct ConvGeom {
 // ksplit > 1: workgroup (tile, part) reduces k-steps [part·nk/ksplit, (part+1)·nk/ksplit) into an
 // f32 partial plane ws[part][M][K_out]; conv_splitk_finish sums the planes (fixed order:
 // deterministic) and applies bias + activation — fills the chip on the small late-stage layers.
-template <int WM, int MB, int NB>
+// SC (small-channel stem mode, C == 8: image channels zero-padded to 8): a 64-deep k-step holds
+// EIGHT taps × 8 channels — 16-B chunk j of k-step kt is tap 8·kt + j — so a 3-channel 7×7 stem runs
+// 7 k-steps instead of 49 padded-to-64-channel ones; W is [K_out][ceil(R·S/8)·64] (taps ≥ R·S zero).
+template <int WM, int MB, int NB, bool SC = false>
 __global__ __launch_bounds__(NTHR, 1) void conv_fwd_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ wt, const bf16_t* __restrict__ zero,
     bf16_t* __restrict__ y, float* __restrict__ ws, int ksplit, ConvGeom g, int Kout, int act,
@@ -343,9 +346,9 @@ __global__ __launch_bounds__(NTHR, 1) void conv_fwd_kernel(
   const int wg = xcd_remap(blockIdx.x, tm * tn * ksplit);
   const int part = wg % ksplit, tile = wg / ksplit;
   const int m0 = (tile / tn) * BM, n0 = (tile % tn) * TN;
-  const long long RSC = (long long)g.R * g.S * g.C;
-  const int cpt = g.C / BK;  // 64-channel k-steps per tap
-  const int nk_all = g.R * g.S * cpt;
+  const int cpt = SC ? 1 : g.C / BK;  // 64-channel k-steps per tap
+  const int nk_all = SC ? (g.R * g.S + 7) / 8 : g.R * g.S * cpt;
+  const long long RSC = SC ? (long long)nk_all * BK : (long long)g.R * g.S * g.C;
   const int kt0 = (int)((long long)nk_all * part / ksplit);
   const int kt1 = (int)((long long)nk_all * (part + 1) / ksplit);
 
@@ -377,10 +380,17 @@ __global__ __launch_bounds__(NTHR, 1) void conv_fwd_kernel(
     const int rr = rs / g.S, ss = rs % g.S;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
-      const int ih = ih0[i] + rr * g.dil_h, iw = iw0[i] + ss * g.dil_w;
-      const bool ok = pbase[i] >= 0 && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
-      const bf16_t* src = ok ? x + (pbase[i] + (long long)ih * g.W + iw) * g.C + c0 + choff[i]
-                             : zero + choff[i];
+      const bf16_t* src;
+      if (SC) {
+        const int tap = kt * 8 + (choff[i] >> 3), tr = tap / g.S, ts = tap - tr * g.S;
+        const int ih = ih0[i] + tr * g.dil_h, iw = iw0[i] + ts * g.dil_w;
+        const bool ok = pbase[i] >= 0 && tap < g.R * g.S && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+        src = ok ? x + (pbase[i] + (long long)ih * g.W + iw) * 8 : zero;
+      } else {
+        const int ih = ih0[i] + rr * g.dil_h, iw = iw0[i] + ss * g.dil_w;
+        const bool ok = pbase[i] >= 0 && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+        src = ok ? x + (pbase[i] + (long long)ih * g.W + iw) * g.C + c0 + choff[i] : zero + choff[i];
+      }
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(ai + (w * PPW + i) * 1024),
                                        16, 0, 0);
@@ -756,8 +766,9 @@ PIAMD_EXPORT int piamd_conv2d_fwd(const void* x, const void* wt, const void* zer
                                   int st_w, int pad_h, int pad_w, int dil_h, int dil_w, int Kout,
                                   int act, const void* bias, int tile_n, int ksplit, void* ws,
                                   hipStream_t st) {
-  if (C % BK || Kout % 4 || N < 1 || OH < 1 || OW < 1 || R < 1 || S < 1 || !zero || ksplit < 1 ||
-      (ksplit > 1 && !ws) || ksplit > R * S * (C / BK))
+  const bool sc = C == 8;
+  if ((C % BK && !sc) || Kout % 4 || N < 1 || OH < 1 || OW < 1 || R < 1 || S < 1 || !zero || ksplit < 1 ||
+      (ksplit > 1 && !ws) || ksplit > (sc ? (R * S + 7) / 8 : R * S * (C / BK)))
     return (int)hipErrorInvalidValue;
   ConvGeom g{N, H, W, C, OH, OW, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w};
   const long long M = (long long)N * OH * OW;
@@ -768,17 +779,21 @@ PIAMD_EXPORT int piamd_conv2d_fwd(const void* x, const void* wt, const void* zer
   const auto zb = (const bf16_t*)zero;
   const auto bb = (const bf16_t*)bias;
   float* wsf = (float*)ws;
-  if (tile_n == 64)
-    hipLaunchKernelGGL((conv_fwd_kernel<8, 1, 2>), dim3(tm * ((Kout + 63) / 64) * ksplit),
+  if (tile_n == 64) {
+    if (sc) hipLaunchKernelGGL((conv_fwd_kernel<8, 1, 2, true>), dim3(tm * ((Kout + 63) / 64) * ksplit), dim3(NTHR), 0, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb);
+    else hipLaunchKernelGGL((conv_fwd_kernel<8, 1, 2>), dim3(tm * ((Kout + 63) / 64) * ksplit),
                        dim3(NTHR), 0, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb);
-  else if (tile_n == 128)
-    hipLaunchKernelGGL((conv_fwd_kernel<4, 2, 2>), dim3(tm * ((Kout + 127) / 128) * ksplit),
+  } else if (tile_n == 128) {
+    if (sc) hipLaunchKernelGGL((conv_fwd_kernel<4, 2, 2, true>), dim3(tm * ((Kout + 127) / 128) * ksplit), dim3(NTHR), 0, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb);
+    else hipLaunchKernelGGL((conv_fwd_kernel<4, 2, 2>), dim3(tm * ((Kout + 127) / 128) * ksplit),
                        dim3(NTHR), 0, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb);
-  else if (tile_n == 256)
-    hipLaunchKernelGGL((conv_fwd_kernel<2, 4, 2>), dim3(tm * ((Kout + 255) / 256) * ksplit),
+  } else if (tile_n == 256) {
+    if (sc) hipLaunchKernelGGL((conv_fwd_kernel<2, 4, 2, true>), dim3(tm * ((Kout + 255) / 256) * ksplit), dim3(NTHR), 0, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb);
+    else hipLaunchKernelGGL((conv_fwd_kernel<2, 4, 2>), dim3(tm * ((Kout + 255) / 256) * ksplit),
                        dim3(NTHR), 0, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb);
-  else
+  } else {
     return (int)hipErrorInvalidValue;
+  }
   if (ksplit > 1) {
     const long long MN = M * Kout;
     hipLaunchKernelGGL(conv_splitk_finish, dim3((unsigned)((MN / 4 + 255) / 256)), dim3(256), 0,

@@ -125,6 +125,69 @@ __global__ __launch_bounds__(256) void momentum_flat_kernel(
   }
 }
 
+// ---- multi-tensor (merged) optimizer update -----------------------------------------------------
+// Parity: reference `phi/kernels/gpu/merged_momentum_kernel.cu`, `merged_adam_kernel.cu` and the
+// `use_multi_tensor` path of paddle.optimizer.{Momentum, Adam, AdamW}: every parameter of the
+// optimizer updated in ONE launch. Per tensor t the table holds {p, grad, s1, s2, n, grad_dtype}
+// (int64) and {wd, lr_mult} (f32); chunk_off[t] = first 2048-element chunk of tensor t. Workgroups
+// grid-stride over chunks and find their tensor by binary search over chunk_off (the table lives
+// on the device, rebuilt only when a pointer changes).
+constexpr int MT_CHUNK = 2048;
+enum { MT_SGD = 0, MT_MOMENTUM = 1, MT_ADAM = 2, MT_ADAMW = 3 };
+
+struct MtHyper {
+  float lr, mu, beta1, beta2, eps, bc1, bc2_sqrt;
+  int nesterov;
+};
+
+template <int OP>
+__global__ __launch_bounds__(256) void multi_tensor_kernel(const long long* __restrict__ meta,
+                                                           const float* __restrict__ fmeta,
+                                                           const int* __restrict__ chunk_off,
+                                                           int T, MtHyper h,
+                                                           const float* __restrict__ grad_scale) {
+  const int total = chunk_off[T];
+  const float gs = grad_scale ? *grad_scale : 1.f;
+  for (int c = blockIdx.x; c < total; c += gridDim.x) {
+    int lo = 0, hi = T - 1;
+    while (lo < hi) {  // last t with chunk_off[t] <= c
+      const int mid = (lo + hi + 1) >> 1;
+      if (chunk_off[mid] <= c) lo = mid; else hi = mid - 1;
+    }
+    const int t = lo;
+    float* p = (float*)meta[t * 6 + 0];
+    const void* g = (const void*)meta[t * 6 + 1];
+    float* s1 = (float*)meta[t * 6 + 2];
+    float* s2 = (float*)meta[t * 6 + 3];
+    const long long n = meta[t * 6 + 4];
+    const int gbf = (int)meta[t * 6 + 5];
+    const float wd = fmeta[t * 2 + 0], lr = h.lr * fmeta[t * 2 + 1];
+    const long long base = (long long)(c - chunk_off[t]) * MT_CHUNK;
+    const long long end = min(base + MT_CHUNK, n);
+    for (long long i = base + threadIdx.x; i < end; i += 256) {
+      float gi = (gbf ? bf2f(((const bf16_t*)g)[i]) : ((const float*)g)[i]) * gs;
+      float pi = p[i];
+      if (OP == MT_SGD) {
+        pi -= lr * (gi + wd * pi);
+      } else if (OP == MT_MOMENTUM) {
+        gi += wd * pi;
+        const float v = h.mu * s1[i] + gi;
+        s1[i] = v;
+        pi -= lr * (h.nesterov ? gi + h.mu * v : v);
+      } else {
+        if (OP == MT_ADAM) gi += wd * pi;
+        else pi *= 1.f - lr * wd;
+        const float m = h.beta1 * s1[i] + (1.f - h.beta1) * gi;
+        const float v = h.beta2 * s2[i] + (1.f - h.beta2) * gi * gi;
+        s1[i] = m;
+        s2[i] = v;
+        pi -= (lr * h.bc2_sqrt / h.bc1) * m / (sqrtf(v) + h.eps * h.bc2_sqrt);
+      }
+      p[i] = pi;
+    }
+  }
+}
+
 }  // namespace
 
 // AdamW over flat buffers. p/m/v f32 [n]; grad bf16 (grad_dtype=1) or f32 (0); model bf16 copy
@@ -178,5 +241,29 @@ PIAMD_EXPORT int piamd_sumsq(const void* x, int dtype, long long n, float* parti
     hipLaunchKernelGGL((sumsq_kernel<false>), dim3(grid), dim3(256), 0, stream, x, n, partial);
   hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, stream, partial, grid, out,
                      accumulate);
+  return (int)hipGetLastError();
+}
+
+// Merged update of T tensors (op: 0 SGD, 1 Momentum, 2 Adam (L2 decay), 3 AdamW (decoupled)).
+// meta [T][6] int64 device table {p, grad, s1, s2, n, grad_is_bf16}; fmeta [T][2] f32 {wd,
+// lr_mult}; chunk_off [T+1] int32 (2048-element chunks); grad_scale: optional device scalar.
+PIAMD_EXPORT int piamd_multi_tensor_update(int op, const long long* meta, const float* fmeta,
+                                           const int* chunk_off, int T, int total_chunks, float lr,
+                                           float mu, int nesterov, float beta1, float beta2,
+                                           float eps, float bc1, float bc2_sqrt,
+                                           const float* grad_scale, hipStream_t stream) {
+  if (T <= 0 || total_chunks <= 0) return 0;
+  MtHyper h{lr, mu, beta1, beta2, eps, bc1, bc2_sqrt, nesterov};
+  const int grid = total_chunks < 2048 ? total_chunks : 2048;
+#define MT(OP) hipLaunchKernelGGL((multi_tensor_kernel<OP>), dim3(grid), dim3(256), 0, stream, meta, \
+                                  fmeta, chunk_off, T, h, grad_scale)
+  switch (op) {
+    case MT_SGD: MT(MT_SGD); break;
+    case MT_MOMENTUM: MT(MT_MOMENTUM); break;
+    case MT_ADAM: MT(MT_ADAM); break;
+    case MT_ADAMW: MT(MT_ADAMW); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef MT
   return (int)hipGetLastError();
 }

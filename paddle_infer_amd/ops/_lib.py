@@ -237,3 +237,7 @@ _SIGS["piamd_bn_bwd"] = ([c_int, c_int] + [c_void_p] * 5 + [c_int] * 3 + [c_void
 # x, dy, zero, d, N, H, W, C, OH, OW, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w, Kout, tile_n,
 # ksplit, ws, accumulate, stream
 _SIGS["piamd_conv2d_wgrad"] = [c_void_p] * 4 + [c_int] * 17 + [c_void_p, c_int, c_void_p]
+# op, meta, fmeta, chunk_off, T, total_chunks, lr, mu, nesterov, beta1, beta2, eps, bc1, bc2_sqrt,
+# grad_scale, stream
+_SIGS["piamd_multi_tensor_update"] = ([c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float,
+                                       c_float, c_int] + [c_float] * 5 + [c_void_p, c_void_p])

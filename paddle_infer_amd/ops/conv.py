@@ -41,7 +41,8 @@ def eligible(x_nhwc_shape, w_shape, groups=1, padding=0) -> bool:
     if len(_pair(padding)) != 2:
         return False
     C, K = x_nhwc_shape[-1], w_shape[0]
-    return C % 64 == 0 and K % 4 == 0 and w_shape[1] == C
+    # C ≤ 8: stem mode (channels zero-padded to 8, eight taps per 64-deep k-step)
+    return (C % 64 == 0 or C <= 8) and K % 4 == 0 and w_shape[1] == C
 
 
 def _out_hw(H, W, R, S, st, pad, dil):
@@ -76,15 +77,18 @@ def _plan(M, K, nk):
 PLAN_OVERRIDE = None  # (tile_n, ksplit) for tuning sweeps
 
 
-def _launch(x, w_ohwi, bias, st, pad, dil, act):
-    """x [N,H,W,C] bf16 contiguous, w_ohwi [K,R,S,C] bf16 contiguous → y [N,OH,OW,K]."""
+def _launch(x, w_ohwi, bias, st, pad, dil, act, rs=None):
+    """x [N,H,W,C] bf16 contiguous, w_ohwi [K,R,S,C] bf16 contiguous → y [N,OH,OW,K]. ``rs``:
+    the true filter size in stem mode (C == 8, w_ohwi = [K][ceil(R·S/8)·64] packed taps)."""
     N, H, W, C = x.shape
-    K, R, S, _ = w_ohwi.shape
+    K = w_ohwi.shape[0]
+    R, S = rs if rs is not None else w_ohwi.shape[1:3]
     OH, OW = _out_hw(H, W, R, S, st, pad, dil)
     if OH < 1 or OW < 1:
         raise ValueError("convolution output is empty")
     M = N * OH * OW
-    tn, ks = PLAN_OVERRIDE or _plan(M, K, R * S * (C // 64))
+    nk = -(-(R * S) // 8) if rs is not None else R * S * (C // 64)
+    tn, ks = PLAN_OVERRIDE or _plan(M, K, nk)
     y = torch.empty(N, OH, OW, K, dtype=torch.bfloat16, device=x.device)
     ws = torch.empty(ks * M * K, dtype=torch.float32, device=x.device) if ks > 1 else None
     b = bias.to(torch.bfloat16).contiguous() if bias is not None else None
@@ -96,13 +100,14 @@ def _launch(x, w_ohwi, bias, st, pad, dil, act):
 
 def _wgrad_plan(M, RSC, K):
     """(tile_n, ksplit) for the weight-gradient kernel: the widest tile dividing K_out, then split
-    the N·OH·OW reduction until the grid holds ~512 workgroups (each part ≥ 8 pixel steps of 64)
-    while the f32 partial planes stay under 256 MiB."""
+    the N·OH·OW reduction until the grid holds ~256 workgroups (each part ≥ 8 pixel steps of 64)
+    while the f32 partial planes stay under 64 MiB (their fixed-order sum was 8% of the ResNet-50
+    step at a 512-workgroup / 256 MiB plan)."""
     tn = 256 if K % 256 == 0 else 128 if K % 128 == 0 else 64
     tiles = -(-RSC // 256) * (K // tn)
     nk = -(-M // 64)
     ks = 1
-    while tiles * ks < 512 and nk // (ks * 2) >= 8 and 2 * ks * RSC * K * 4 <= (256 << 20):
+    while tiles * ks < 256 and nk // (ks * 2) >= 8 and 2 * ks * RSC * K * 4 <= (64 << 20):
         ks *= 2
     return tn, ks
 
@@ -188,9 +193,18 @@ def _launch_geom(x, w_ohwi, st, pad, dil, OH, OW):
 class _Conv2dNHWC(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, st, pad, dil, act):
-        xc = x.contiguous()
-        w_ohwi = weight.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
-        y = _launch(xc, w_ohwi, bias, st, pad, dil, act)
+        C0 = x.shape[-1]
+        if C0 % 64:  # stem mode: zero-pad the image channels to 8
+            xc = torch.nn.functional.pad(x, (0, 8 - C0)).contiguous() if C0 < 8 else x.contiguous()
+            K, _, R, S = weight.shape
+            nk = -(-(R * S) // 8)
+            w8 = torch.zeros(K, nk * 64, dtype=torch.bfloat16, device=x.device)
+            w8[:, :R * S * 8].view(K, R, S, 8)[..., :C0] = weight.to(torch.bfloat16).permute(0, 2, 3, 1)
+            y = _launch(xc, w8.view(K, 1, nk * 8, 8), bias, st, pad, dil, act, rs=(R, S))
+        else:
+            xc = x.contiguous()
+            w_ohwi = weight.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
+            y = _launch(xc, w_ohwi, bias, st, pad, dil, act)
         ctx.save_for_backward(xc, weight, y if act else None)
         ctx.cfg = (st, pad, dil, act, bias is not None)
         return y
@@ -203,7 +217,10 @@ class _Conv2dNHWC(torch.autograd.Function):
         if act == 3:
             dy = dy * (y > 0)
         dy = dy.contiguous()
-        K, C, R, S = weight.shape
+        K, C0, R, S = weight.shape
+        C = x.shape[-1]  # == C0, or 8 in stem mode (zero-padded channels)
+        if C != C0:
+            weight = torch.nn.functional.pad(weight, (0, 0, 0, 0, 0, C - C0))
         dx = dw = db = None
         N, H, W, _ = x.shape
         if ctx.needs_input_grad[0]:
@@ -229,6 +246,9 @@ class _Conv2dNHWC(torch.autograd.Function):
                     dy.permute(0, 3, 1, 2), x.permute(0, 3, 1, 2), weight.to(torch.bfloat16), None,
                     list(st), list(pad), list(dil), False, [0, 0], 1, [False, True, False])[1]
             dw = dw.to(weight.dtype)
+        if C != C0:
+            dx = dx[..., :C0] if dx is not None else None
+            dw = dw[:, :C0].contiguous() if dw is not None else None
         if has_bias and ctx.needs_input_grad[2]:
             db = dy.float().sum((0, 1, 2))
         return dx, dw, db, None, None, None, None

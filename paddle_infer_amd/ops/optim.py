@@ -70,3 +70,60 @@ def sumsq(x, out=None, accumulate=False):
     else:
         out.copy_(s)
     return out
+
+
+_MT_CHUNK = 2048
+
+
+def multi_tensor_update(op, entries, lr, cache=None, mu=0.0, nesterov=False, beta1=0.9,
+                        beta2=0.999, eps=1e-8, step=1, grad_scale=None):
+    """Merged optimizer update of many tensors in ONE kernel launch (reference
+    ``merged_momentum`` / ``merged_adam``; ``optim.hip`` multi_tensor_kernel).
+
+    ``op``: 0 SGD, 1 Momentum, 2 Adam (L2 decay), 3 AdamW (decoupled decay). ``entries``: list of
+    ``(p, grad, s1, s2, wd, lr_mult)`` with f32 contiguous ``p`` / states and bf16 or f32 ``grad``.
+    ``cache`` (a dict owned by the optimizer) keeps the device table while no pointer changes."""
+    dev = entries[0][0].device
+    if dev.type != "cuda":
+        for p, g, s1, s2, wd, lm in entries:
+            gf = g.float()
+            lr_ = lr * lm
+            if op == 0:
+                p.sub_(lr_ * (gf + wd * p))
+            elif op == 1:
+                gf = gf + wd * p
+                s1.mul_(mu).add_(gf)
+                p.sub_(lr_ * (gf + mu * s1 if nesterov else s1))
+            else:
+                if op == 2:
+                    gf = gf + wd * p
+                else:
+                    p.mul_(1.0 - lr_ * wd)
+                s1.mul_(beta1).add_(gf, alpha=1 - beta1)
+                s2.mul_(beta2).addcmul_(gf, gf, value=1 - beta2)
+                bc2 = math.sqrt(1 - beta2 ** step)
+                p.addcdiv_(s1, s2.sqrt().add_(eps * bc2), value=-lr_ * bc2 / (1 - beta1 ** step))
+        return
+    key = tuple((e[0].data_ptr(), e[1].data_ptr(), _lib.ptr(e[2]) or 0, _lib.ptr(e[3]) or 0,
+                 e[1].dtype == torch.bfloat16, e[4], e[5]) for e in entries)
+    ent = cache.get("table") if cache is not None else None
+    if ent is None or ent[0] != key:
+        meta, fmeta, offs, c = [], [], [0], 0
+        for (pp, gp, s1p, s2p, bf, wd, lm), e in zip(key, entries):
+            n = e[0].numel()
+            meta += [pp, gp, s1p, s2p, n, int(bf)]
+            fmeta += [float(wd), float(lm)]
+            c += -(-n // _MT_CHUNK)
+            offs.append(c)
+        t_meta = torch.tensor(meta, dtype=torch.int64).pin_memory().to(dev, non_blocking=True)
+        t_f = torch.tensor(fmeta, dtype=torch.float32).pin_memory().to(dev, non_blocking=True)
+        t_o = torch.tensor(offs, dtype=torch.int32).pin_memory().to(dev, non_blocking=True)
+        ent = (key, t_meta, t_f, t_o, c)
+        if cache is not None:
+            cache["table"] = ent
+    _, t_meta, t_f, t_o, total = ent
+    bc1 = 1.0 - beta1 ** step
+    bc2s = math.sqrt(1.0 - beta2 ** step)
+    _lib.call("piamd_multi_tensor_update", int(op), t_meta.data_ptr(), t_f.data_ptr(), t_o.data_ptr(),
+              len(entries), int(total), float(lr), float(mu), int(nesterov), float(beta1),
+              float(beta2), float(eps), float(bc1), float(bc2s), _lib.ptr(grad_scale), _lib.stream())

@@ -99,11 +99,43 @@ class Optimizer:
             t = self._accumulators[key] = torch.full_like(ref, init, dtype=torch.float32 if ref.is_floating_point() else ref.dtype)
         return t
 
+    # merged (multi-tensor) GPU update: one launch for every parameter (reference
+    # merged_momentum / use_multi_tensor); subclasses name their op code
+    _merged_op = None
+
+    def _merged_ok(self, pg):
+        if self._merged_op is None or self._param_groups is not None or isinstance(self.regularization, L1Decay):
+            return False
+        def dense(t):
+            return t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last))
+        # elementwise over storage: p, grad (and the states, created like p) share one dense layout
+        return all(p.is_cuda and p.dtype == torch.float32 and g is not None and dense(p)
+                   and g.stride() == p.stride() and g.dtype in (torch.float32, torch.bfloat16)
+                   for p, g in pg)
+
+    def _merged_step(self, pg, lr_):
+        from ..ops.optim import multi_tensor_update
+        wd = self.regularization
+        coeff = 0.0 if wd is None else float(wd if isinstance(wd, (int, float)) else getattr(wd, "_coeff", 0.0))
+        entries = []
+        for p, g in pg:
+            s1 = self._acc("velocity", p) if self._merged_op == 1 else None
+            entries.append((p, g, s1, None, coeff, getattr(p, "optimize_attr", {}).get("learning_rate", 1.0)))
+        cache = self.__dict__.setdefault("_mt_cache", {})
+        multi_tensor_update(self._merged_op, entries, lr_, cache, **self._merged_hyper())
+
+    def _merged_hyper(self):
+        return {}
+
     @torch.no_grad()
     def step(self):
         self._step += 1
         lr_ = self.get_lr()
-        for p, g in self._params_grads():
+        pg = [(p, g) for p, g in self._params_grads() if g is not None]
+        if pg and self._merged_ok(pg):
+            self._merged_step(pg, lr_)
+            return
+        for p, g in pg:
             if g is None:
                 continue
             mp = self._master_of(p)
@@ -173,6 +205,8 @@ class L1Decay(L2Decay):
 
 
 class SGD(Optimizer):
+    _merged_op = 0
+
     def _update(self, p, mp, g, lr_):
         mp.sub_(lr_ * self._l2(mp, g))
 
@@ -183,6 +217,10 @@ class Momentum(Optimizer):
                  name=None):
         super().__init__(learning_rate, parameters, weight_decay, grad_clip, name, multi_precision)
         self._momentum, self._nesterov, self._rescale = momentum, use_nesterov, rescale_grad
+        self._merged_op = 1 if rescale_grad == 1.0 else None
+
+    def _merged_hyper(self):
+        return {"mu": float(self._momentum), "nesterov": bool(self._nesterov)}
 
     def _update(self, p, mp, g, lr_):
         g = self._l2(mp, g * self._rescale)

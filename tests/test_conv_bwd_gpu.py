@@ -107,3 +107,47 @@ def test_autograd_conv_backward_stays_on_hip(N, H, W, C, K, R, st, pad, dil):
     assert not [k for k in new if k[0].startswith("conv2d")], new
     assert w.grad.dtype == torch.float32 and torch.isfinite(w.grad).all()
     assert torch.isfinite(x.grad.float()).all()
+
+
+def test_resnet50_loss_curve_parity_hip_vs_library():
+    """20 same-seed ResNet-50 steps on a fixed batch through paddle.DataParallel +
+    paddle.optimizer.Momentum: the HIP-conv loss curve tracks the library-conv curve (both fit the
+    batch; per-step gap within bf16 run-to-run noise) — the round-1 8.55-vs-5.96 gap came from
+    lr 0.1 chaos on a random-init ResNet-50, not from the kernels."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "bench_resnet", os.path.join(os.path.dirname(__file__), "..", "tools", "bench_resnet.py"))
+    br = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(br)
+    r = br.parity(20, batch=32, res=112, lr=0.02)
+    lib, hip = r["library_conv"], r["hip_conv"]
+    assert abs(lib[0] - hip[0]) < 0.02 * lib[0], r
+    assert lib[-1] < 0.25 * lib[0] and hip[-1] < 0.25 * hip[0], r
+    # later steps: both trajectories descend together (mean gap well inside the descent)
+    gap = sum(abs(a - b) for a, b in zip(lib, hip)) / len(lib)
+    assert gap < 0.1 * (lib[0] - lib[-1]), r
+
+
+@pytest.mark.parametrize("C,st", [(3, 2), (8, 1), (5, 1)])
+def test_stem_mode_small_channel_conv(C, st):
+    """C ≤ 8 (ResNet stem, 7×7 stride 2 over 3 channels): channels zero-padded to 8, eight taps per
+    k-step — forward, weight and data gradients against fp32 with no library fallback."""
+    from paddle_infer_amd.ops import _lib
+    from paddle_infer_amd.ops.conv import conv2d_nhwc
+    torch.manual_seed(C)
+    x = torch.randn(2, 30, 26, C, device=DEV).bfloat16()
+    w = (torch.randn(64, C, 7, 7, device=DEV) / (C * 49) ** 0.5).bfloat16()
+    xh, wh = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    before = dict(_lib.FALLBACKS)
+    y = conv2d_nhwc(xh, wh, None, st, 3, 1, "relu")
+    xr, wr = x.float().clone().requires_grad_(True), w.float().clone().requires_grad_(True)
+    yr = torch.relu(F.conv2d(xr.permute(0, 3, 1, 2), wr, None, st, 3)).permute(0, 2, 3, 1)
+    _close(y, yr, 2e-2)
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    _close(wh.grad, wr.grad, 2e-2)
+    _close(xh.grad, xr.grad, 3e-2)
+    new = {k: v for k, v in _lib.FALLBACKS.items() if before.get(k) != v}
+    assert not [k for k in new if k[0].startswith("conv2d")], new

@@ -80,11 +80,11 @@ def test_conv_tile_and_splitk_variants(plan):
 
 
 def test_resnet18_grads_match_library_conv_and_trains():
-    """ResNet-18 step (channels_last, bf16 autocast): loss and every parameter gradient with the
-    convolutions on the HIP kernel agree with the library-convolution run (bf16 run-to-run noise
-    floor of the library path alone is cos ≈ 0.99; ResNet-50 at random init is chaotic — cos ≈ 0.5
-    between two identical library runs — so it is not used here), then 8 SGD steps on the HIP path
-    fit the fixed batch."""
+    """ResNet-18 step (channels_last, bf16 autocast): with the convolutions on the HIP kernels
+    (stem in small-channel mode included) every parameter gradient is as close to an fp32 library
+    run as the bf16 library-conv run is (cosine within 0.05 of the library's; at random init the
+    bf16-vs-fp32 cosine of either path is only ≈0.9-0.95 — tools/diag_resnet18_grads.py), then 8
+    SGD steps on the HIP path fit the fixed batch."""
     from paddle_infer_amd.ops import conv as CV
     from paddle_infer_amd.vision.models import resnet18
     torch.manual_seed(0)
@@ -93,18 +93,20 @@ def test_resnet18_grads_match_library_conv_and_trains():
     y = torch.randint(0, 10, (16,), device=DEV)
     res = {}
     try:
-        for hc in (False, True):
+        for tag, hc in (("lib", False), ("hip", True), ("fp32", False)):
             CV.HIP_CONV = hc
             m.zero_grad(set_to_none=True)
-            with torch.autocast("cuda", dtype=torch.bfloat16):
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=tag != "fp32"):
                 loss = F.cross_entropy(m(x), y)
             loss.backward()
-            res[hc] = (loss.item(), [p.grad.float().flatten().clone() for p in m.parameters()])
+            res[tag] = (loss.item(), [p.grad.float().flatten().clone() for p in m.parameters()])
     finally:
         CV.HIP_CONV = True
-    assert abs(res[True][0] - res[False][0]) < 1e-2 * abs(res[False][0])
-    for a, b in zip(res[True][1], res[False][1]):
-        assert F.cosine_similarity(a, b, dim=0).item() > 0.9
+    assert abs(res["hip"][0] - res["fp32"][0]) < 1e-2 * abs(res["fp32"][0])
+    for a, b, f in zip(res["hip"][1], res["lib"][1], res["fp32"][1]):
+        ch = F.cosine_similarity(a, f, dim=0).item()
+        cl = F.cosine_similarity(b, f, dim=0).item()
+        assert ch > cl - 0.05, (ch, cl)
     opt = torch.optim.SGD(m.parameters(), lr=0.02, momentum=0.9)
     losses = []
     for _ in range(8):

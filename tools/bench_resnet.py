@@ -1,52 +1,103 @@
-"""ResNet-50 training step (channels_last, bf16 autocast, SGD momentum) images/s with the
-convolutions on the MFMA implicit-GEMM kernel (``ops/conv.py``) vs the library (MIOpen) path.
-Reference parity: the reference's ResNet-50 benchmark (`python/paddle/vision/models/resnet.py`)."""
+"""ResNet-50 training step (channels_last, bf16 autocast) images/s through the framework's own
+training API: ``paddle.vision.models.resnet50`` + ``paddle.DataParallel`` +
+``paddle.optimizer.Momentum`` (merged multi-tensor update kernel) with the convolutions on the MFMA
+implicit-GEMM kernels (``ops/conv.py``: forward, data gradient, weight gradient) — or, for the A/B,
+on the library (MIOpen) path.
+
+Reference parity: the reference's ResNet-50 benchmark (`python/paddle/vision/models/resnet.py`,
+BASELINE config "ResNet-50 bf16 paddle.DataParallel"). Multi-GPU: launch under torchrun (one
+rank per GPU, RCCL); images/s is the whole-job aggregate (max step time over ranks).
+
+``--parity N``: N same-seed steps on a fixed batch for both conv paths, printing both loss curves."""
 import argparse
 import json
+import os
 import sys
 import time
 
 import torch
 
-sys.path.insert(0, ".")
-import paddle_infer_amd  # noqa: E402,F401
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import paddle_infer_amd as paddle  # noqa: E402
 from paddle_infer_amd.ops import conv as CV  # noqa: E402
 from paddle_infer_amd.vision.models import resnet50  # noqa: E402
 
 
-def run(batch, steps, hip_conv):
+def _setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        import paddle_infer_amd.distributed as dist
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        dist.init_parallel_env()
+    return world
+
+
+def build(batch, hip_conv, lr, res=224, seed=0):
     CV.HIP_CONV = hip_conv
-    torch.manual_seed(0)
+    torch.manual_seed(seed)
     m = resnet50(num_classes=1000).cuda().to(memory_format=torch.channels_last)
-    opt = torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9)
-    x = torch.randn(batch, 3, 224, 224, device="cuda").contiguous(memory_format=torch.channels_last)
-    y = torch.randint(0, 1000, (batch,), device="cuda")
+    model = paddle.DataParallel(m)
+    opt = paddle.optimizer.Momentum(learning_rate=lr, momentum=0.9, parameters=m.parameters(),
+                                    weight_decay=1e-4)
+    g = torch.Generator(device="cuda").manual_seed(1234 + int(os.environ.get("RANK", "0")))
+    x = torch.randn(batch, 3, res, res, device="cuda", generator=g).contiguous(
+        memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (batch,), device="cuda", generator=g)
 
     def step():
         with torch.autocast("cuda", dtype=torch.bfloat16):
-            loss = torch.nn.functional.cross_entropy(m(x), y)
+            loss = torch.nn.functional.cross_entropy(model(x), y)
         loss.backward()
         opt.step()
-        opt.zero_grad(set_to_none=True)
+        opt.clear_grad(set_to_zero=False)
         return loss
+    return step
 
+
+def run(batch, steps, hip_conv, world):
+    step = build(batch, hip_conv, lr=0.1)
     for _ in range(3):
         step()
     torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
         loss = step()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
-    return {"hip_conv": hip_conv, "batch": batch, "ms_per_step": round(dt * 1e3, 2),
-            "images_per_s": round(batch / dt, 1), "loss": round(loss.item(), 3)}
+    if world > 1:
+        t = torch.tensor([dt], device="cuda")
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = t.item()
+    return {"hip_conv": hip_conv, "batch_per_gpu": batch, "n_gpus": world,
+            "ms_per_step": round(dt * 1e3, 2), "images_per_s": round(batch * world / dt, 1),
+            "loss": round(loss.item(), 3), "optimizer": "paddle.optimizer.Momentum (merged)",
+            "wrapper": "paddle.DataParallel"}
+
+
+def parity(steps, batch=32, res=112, lr=0.02):
+    curves = {}
+    for hc in (False, True):
+        step = build(batch, hc, lr=lr, res=res)
+        curves[hc] = [round(step().item(), 4) for _ in range(steps)]
+    CV.HIP_CONV = True
+    return {"parity_steps": steps, "batch": batch, "res": res, "lr": lr,
+            "library_conv": curves[False], "hip_conv": curves[True]}
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--mode", choices=["both", "hip", "lib"], default="both")
+    ap.add_argument("--mode", choices=["both", "hip", "lib"], default="hip")
+    ap.add_argument("--parity", type=int, default=0)
     a = ap.parse_args()
-    for hc in {"both": (False, True), "hip": (True,), "lib": (False,)}[a.mode]:
-        print(json.dumps(run(a.batch, a.steps, hc)), flush=True)
+    world = _setup()
+    if a.parity:
+        print(json.dumps(parity(a.parity)), flush=True)
+    else:
+        for hc in {"both": (False, True), "hip": (True,), "lib": (False,)}[a.mode]:
+            r = run(a.batch, a.steps, hc, world)
+            if int(os.environ.get("RANK", "0")) == 0:
+                print(json.dumps(r), flush=True)

@@ -122,7 +122,10 @@ PIAMD_EXPORT int piamd_qkv_prep(void* qkv, long long ld, const void* bias, void*
 // out   : element (b, head, d) at out[b*ldo + head*D + d]
 constexpr int DA_CHUNK_MAX = 512;
 
-template <int D, int G>
+// U: K/V rows in flight per lane per pass (4; 16 = the short-context single-pass variant: a
+// 256-key chunk (D = 128) needs no split, partials, counters or combine — one global round trip
+// for K and V each)
+template <int D, int G, int U = 4>
 __global__ __launch_bounds__(256) void decode_attn_kernel(
     const bf16_t* __restrict__ qkv, long long ldq, const bf16_t* __restrict__ bias, int prep,
     int rot, int neox, float log2_base, bf16_t* __restrict__ kc, bf16_t* __restrict__ vc,
@@ -220,7 +223,6 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
     }
   } else {
     // ---- scores: s = (q·k) * scale * log2(e) (+ mask * log2(e)) ----
-    constexpr int U = 4;
     for (int base = kslot; base < n; base += KPI * U) {
       u16x8 kr[U];
 #pragma unroll
@@ -245,6 +247,11 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
         }
       }
     }
+    // V rows of the first P·V pass requested now: their latency hides under the softmax
+    u16x8 vpre[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      vpre[u] = *(const u16x8*)(vc + kvbase + (long long)(k0 + min(kslot + u * KPI, n - 1)) * D + sub * 8);
     __syncthreads();
 
     // ---- softmax statistics over the chunk (base-2 domain) ----
@@ -278,7 +285,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int kk = min(base + u * KPI, n - 1);
-        vr[u] = *(const u16x8*)(vc + kvbase + (long long)(k0 + kk) * D + sub * 8);
+        vr[u] = base == kslot ? vpre[u] : *(const u16x8*)(vc + kvbase + (long long)(k0 + kk) * D + sub * 8);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -359,6 +366,14 @@ static void launch_decode(dim3 grid, hipStream_t st, const void* qkv, long long 
                           void* vc, const int* lens, int Hk, int maxS, int chunk, int nsplit,
                           const void* mask, long long ldm, float sl2, float* part, int* cnt,
                           void* out, long long ldo) {
+  constexpr int KPI = (64 / (D / 8)) * 4;
+  if (G <= 2 && nsplit == 1 && chunk > 4 * KPI && chunk <= 16 * KPI) {
+    hipLaunchKernelGGL((decode_attn_kernel<D, (G <= 2 ? G : 1), 16>), grid, dim3(256), 0, st,
+                       (const bf16_t*)qkv, ldq, (const bf16_t*)bias, prep, rot, neox, l2b,
+                       (bf16_t*)kc, (bf16_t*)vc, lens, Hk, maxS, chunk, nsplit,
+                       (const bf16_t*)mask, ldm, sl2, part, cnt, (bf16_t*)out, ldo);
+    return;
+  }
   hipLaunchKernelGGL((decode_attn_kernel<D, G>), grid, dim3(256), 0, st, (const bf16_t*)qkv, ldq,
                      (const bf16_t*)bias, prep, rot, neox, l2b, (bf16_t*)kc, (bf16_t*)vc, lens,
                      Hk, maxS, chunk, nsplit, (const bf16_t*)mask, ldm, sl2, part, cnt,

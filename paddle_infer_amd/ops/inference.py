@@ -89,7 +89,12 @@ _PART_CACHE = {}
 
 def decode_chunking(max_len, chunk=None):
     if chunk is None:
-        chunk = 256 if max_len > 1024 else 128
+        # short caches: 64-key splits (one K pass + one V pass per workgroup, 4x the workgroups of
+        # a 256-key split at batch 1); long caches keep the per-split partial count bounded
+        # (≤ 256 keys: ONE split — the single-pass kernel variant keeps all K/V rows in flight and
+        # skips the partial/combine round trips)
+        chunk = (max(16, max_len) if max_len <= 256 else
+                 64 if max_len <= 1024 else (128 if max_len <= 4096 else 256))
     chunk = max(16, min(512, chunk))
     return chunk, max(1, -(-max_len // chunk))
 

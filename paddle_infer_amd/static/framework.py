@@ -425,6 +425,11 @@ def data(name, shape, dtype="float32", lod_level=0):
 
 
 def _record(func, args, kwargs):
+    # a torch method replaced by a Paddle-signature adapter (framework/tensor_patch.py) arrives
+    # here as the ORIGINAL method; record the adapter (the name every op table keys on) — it
+    # forwards torch-form calls unchanged when the Executor replays the op
+    from ..framework.tensor_patch import ADAPTER_OF
+    func = ADAPTER_OF.get(func, func)
     prog = None
 
     def find(x):

@@ -87,8 +87,10 @@ def _signed(n, bits=64):
     return n - (1 << 64) if n >= 1 << 63 else n
 
 
-def encode(msg_name: str, obj: dict) -> bytes:
-    schema = SCHEMA[msg_name]
+def encode(msg_name: str, obj: dict, schemas=None) -> bytes:
+    """Encode ``obj`` as message ``msg_name`` of ``schemas`` (default: framework.proto)."""
+    schemas = SCHEMA if schemas is None else schemas
+    schema = schemas[msg_name]
     out = bytearray()
     for fno in sorted(schema, key=lambda f: f if msg_name != "OpDesc" else {3: 0, 1: 1, 2: 2, 4: 3, 5: 4}[f]):
         name, kind, rep, sub = schema[fno]
@@ -102,17 +104,18 @@ def encode(msg_name: str, obj: dict) -> bytes:
                 out += _varint((fno << 3) | 5) + struct.pack("<f", float(v))
             elif kind == "d":
                 out += _varint((fno << 3) | 1) + struct.pack("<d", float(v))
-            elif kind == "s":
+            elif kind in ("s", "y"):
                 b = v.encode() if isinstance(v, str) else bytes(v)
                 out += _varint((fno << 3) | 2) + _varint(len(b)) + b
             elif kind == "m":
-                b = encode(sub, v)
+                b = encode(sub, v, schemas)
                 out += _varint((fno << 3) | 2) + _varint(len(b)) + b
     return bytes(out)
 
 
-def decode(msg_name: str, buf: bytes) -> dict:
-    schema = SCHEMA[msg_name]
+def decode(msg_name: str, buf: bytes, schemas=None) -> dict:
+    schemas = SCHEMA if schemas is None else schemas
+    schema = schemas[msg_name]
     obj = {}
     pos, end = 0, len(buf)
     while pos < end:
@@ -136,9 +139,11 @@ def decode(msg_name: str, buf: bytes) -> dict:
                 continue
             kind = spec[1]
             if kind == "m":
-                val = [decode(spec[3], raw)]
+                val = [decode(spec[3], raw, schemas)]
             elif kind == "s":
                 val = [raw.decode("utf-8", errors="replace")]
+            elif kind == "y":  # bytes field (kept raw)
+                val = [raw]
             else:  # packed repeated scalars
                 val, p2 = [], 0
                 while p2 < len(raw):

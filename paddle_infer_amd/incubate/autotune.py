@@ -5,8 +5,9 @@ MI355X design: GEMM autotuning is PyTorch TunableOp over the hipBLASLt + rocBLAS
 spaces (every candidate kernel for a GEMM shape is timed once, the winner cached per
 shape/layout/dtype). Tuned tables ship in-tree (``paddle_infer_amd/tuning/*.csv``) keyed by
 the GPU arch + ROCm/hipBLASLt versions (TunableOp validators), so production runs replay the
-winners with tuning OFF (no first-step stall). The framework's own HIP kernels are tuned offline
-(tile shapes are compile-time).
+winners with tuning OFF (no first-step stall). The framework's own HIP kernels pick their launch
+plans (tile width, split-K) at run time through ``ops/autotune.py`` (heuristic by default, measured
+per shape inside ``tuning_range`` when enabled).
 """
 from __future__ import annotations
 
@@ -41,10 +42,16 @@ def use_tuned_gemms(path=None, tune_missing=False):
 def set_config(config=None):
     """Reference-compatible: ``{"kernel": {"enable": bool, "tuning_range": [a, b]},
     "layout": {...}, "dataloader": {...}}``. ``kernel.enable`` turns GEMM autotuning on
-    (tuning new shapes, results written to ``kernel.table`` or the in-tree default)."""
+    (tuning new shapes, results written to ``kernel.table`` or the in-tree default) AND the
+    runtime plan tuning of the framework's own HIP kernels (``ops/autotune.py``: conv tile /
+    split-K plans, measured on the live operands during ``tuning_range`` steps, cached per shape,
+    persisted to ``kernel.cache_file`` when given)."""
     import torch
+    from ..ops import autotune as _own
     cfg = config or {"kernel": {"enable": True}}
     k = cfg.get("kernel", {})
+    _own.configure(enable=k.get("enable", False), tuning_range=k.get("tuning_range"),
+                   cache_file=k.get("cache_file"))
     if not torch.cuda.is_available():
         return
     import torch.cuda.tunable as tun

@@ -241,3 +241,5 @@ _SIGS["piamd_conv2d_wgrad"] = [c_void_p] * 4 + [c_int] * 17 + [c_void_p, c_int, 
 # grad_scale, stream
 _SIGS["piamd_multi_tensor_update"] = ([c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float,
                                        c_float, c_int] + [c_float] * 5 + [c_void_p, c_void_p])
+# in, out, rows, N, inverse, scale, stream
+_SIGS["piamd_fft_c2c"] = [c_void_p, c_void_p, c_ll, c_int, c_int, c_float, c_void_p]

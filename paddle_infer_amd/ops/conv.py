@@ -88,14 +88,30 @@ def _launch(x, w_ohwi, bias, st, pad, dil, act, rs=None):
         raise ValueError("convolution output is empty")
     M = N * OH * OW
     nk = -(-(R * S) // 8) if rs is not None else R * S * (C // 64)
-    tn, ks = PLAN_OVERRIDE or _plan(M, K, nk)
     y = torch.empty(N, OH, OW, K, dtype=torch.bfloat16, device=x.device)
-    ws = torch.empty(ks * M * K, dtype=torch.float32, device=x.device) if ks > 1 else None
     b = bias.to(torch.bfloat16).contiguous() if bias is not None else None
-    _lib.call("piamd_conv2d_fwd", x.data_ptr(), w_ohwi.data_ptr(), _zero(x.device).data_ptr(),
-              y.data_ptr(), N, H, W, C, OH, OW, R, S, st[0], st[1], pad[0], pad[1], dil[0], dil[1],
-              K, act, _lib.ptr(b), tn, ks, _lib.ptr(ws), _lib.stream())
+
+    def run(plan):
+        tn, ks = plan
+        ws = torch.empty(ks * M * K, dtype=torch.float32, device=x.device) if ks > 1 else None
+        _lib.call("piamd_conv2d_fwd", x.data_ptr(), w_ohwi.data_ptr(), _zero(x.device).data_ptr(),
+                  y.data_ptr(), N, H, W, C, OH, OW, R, S, st[0], st[1], pad[0], pad[1], dil[0],
+                  dil[1], K, act, _lib.ptr(b), tn, ks, _lib.ptr(ws), _lib.stream())
+    plan = PLAN_OVERRIDE or _autotuned("conv2d_fwd", (N, H, W, C, K, R, S, st, pad, dil, act),
+                                       _plan(M, K, nk), _fwd_candidates(M, K, nk), run)
+    run(plan)
     return y
+
+
+def _fwd_candidates(M, K, nk):
+    return [(tn, ks) for tn in (64, 128, 256) if tn <= max(64, K)
+            for ks in (1, 2, 4, 8) if ks <= nk and (ks == 1 or nk // ks >= 2)]
+
+
+def _autotuned(op, shape, default, candidates, run):
+    """Plan via the runtime autotune cache (ops/autotune.py) — the heuristic when tuning is off."""
+    from . import autotune
+    return autotune.choose(autotune.key_of(op, *shape), candidates, default, run)
 
 
 def _wgrad_plan(M, RSC, K):
@@ -127,13 +143,22 @@ def conv2d_wgrad(x, dy, R, S, st, pad, dil):
     M, RSC = N * OH * OW, R * S * C
     if not wgrad_eligible(C, K, M):
         raise ValueError(f"conv2d_wgrad: unsupported C={C} K={K} M={M}")
-    tn, ks = WGRAD_PLAN_OVERRIDE or _wgrad_plan(M, RSC, K)
-    ks = max(1, min(ks, -(-M // 64)))
     d = torch.empty(R, S, C, K, dtype=torch.float32, device=x.device)
-    ws = torch.empty(ks * RSC * K, dtype=torch.float32, device=x.device) if ks > 1 else None
-    _lib.call("piamd_conv2d_wgrad", x.data_ptr(), dy.data_ptr(), _zero(x.device).data_ptr(),
-              d.data_ptr(), N, H, W, C, OH, OW, R, S, st[0], st[1], pad[0], pad[1], dil[0], dil[1],
-              K, tn, ks, _lib.ptr(ws), 0, _lib.stream())
+    nk = -(-M // 64)
+
+    def run(plan):
+        tn, ks = plan
+        ks = max(1, min(ks, nk))
+        ws = torch.empty(ks * RSC * K, dtype=torch.float32, device=x.device) if ks > 1 else None
+        _lib.call("piamd_conv2d_wgrad", x.data_ptr(), dy.data_ptr(), _zero(x.device).data_ptr(),
+                  d.data_ptr(), N, H, W, C, OH, OW, R, S, st[0], st[1], pad[0], pad[1], dil[0],
+                  dil[1], K, tn, ks, _lib.ptr(ws), 0, _lib.stream())
+    default = _wgrad_plan(M, RSC, K)
+    cands = [(tn, ks) for tn in (64, 128, 256) if K % tn == 0
+             for ks in (1, 4, 16, 64, 256) if ks <= nk and ks * RSC * K * 4 <= (256 << 20)]
+    plan = WGRAD_PLAN_OVERRIDE or _autotuned("conv2d_wgrad", (N, H, W, C, K, R, S, st, pad, dil),
+                                             default, cands, run)
+    run(plan)
     return d.permute(3, 2, 0, 1)
 
 
@@ -181,12 +206,17 @@ def _launch_geom(x, w_ohwi, st, pad, dil, OH, OW):
     N, H, W, C = x.shape
     K, R, S, _ = w_ohwi.shape
     M = N * OH * OW
-    tn, ks = _plan(M, K, R * S * (C // 64))
+    nk = R * S * (C // 64)
     y = torch.empty(N, OH, OW, K, dtype=torch.bfloat16, device=x.device)
-    ws = torch.empty(ks * M * K, dtype=torch.float32, device=x.device) if ks > 1 else None
-    _lib.call("piamd_conv2d_fwd", x.data_ptr(), w_ohwi.data_ptr(), _zero(x.device).data_ptr(),
-              y.data_ptr(), N, H, W, C, OH, OW, R, S, st[0], st[1], pad[0], pad[1], dil[0], dil[1],
-              K, 0, 0, tn, ks, _lib.ptr(ws), _lib.stream())
+
+    def run(plan):
+        tn, ks = plan
+        ws = torch.empty(ks * M * K, dtype=torch.float32, device=x.device) if ks > 1 else None
+        _lib.call("piamd_conv2d_fwd", x.data_ptr(), w_ohwi.data_ptr(), _zero(x.device).data_ptr(),
+                  y.data_ptr(), N, H, W, C, OH, OW, R, S, st[0], st[1], pad[0], pad[1], dil[0],
+                  dil[1], K, 0, 0, tn, ks, _lib.ptr(ws), _lib.stream())
+    run(_autotuned("conv2d_dgrad", (N, H, W, C, K, R, S, st, pad, dil, OH, OW), _plan(M, K, nk),
+                   _fwd_candidates(M, K, nk), run))
     return y
 
 

@@ -130,6 +130,8 @@ class Optimizer:
     @torch.no_grad()
     def step(self):
         self._step += 1
+        from ..ops import autotune as _at
+        _at.step()
         lr_ = self.get_lr()
         pg = [(p, g) for p, g in self._params_grads() if g is not None]
         if pg and self._merged_ok(pg):
@@ -272,6 +274,8 @@ class Adam(Optimizer):
     @torch.no_grad()
     def step(self):
         if self._flat is not None:
+            from ..ops import autotune as _at
+            _at.step()
             self._step += 1
             self._flat.step(self.get_lr())
             return

@@ -151,3 +151,31 @@ def test_stem_mode_small_channel_conv(C, st):
     _close(xh.grad, xr.grad, 3e-2)
     new = {k: v for k, v in _lib.FALLBACKS.items() if before.get(k) != v}
     assert not [k for k in new if k[0].startswith("conv2d")], new
+
+
+def test_runtime_autotune_conv_plans(tmp_path):
+    """With own-kernel autotuning on, conv forward / dgrad / wgrad plans are measured on the live
+    operands, cached per shape, and the tuned launches stay numerically exact."""
+    from paddle_infer_amd.ops import autotune as AT
+    from paddle_infer_amd.ops.conv import conv2d_nhwc
+    AT.CACHE.clear()
+    AT.configure(enable=True, tuning_range=[0, 1 << 30], cache_file=str(tmp_path / "t.json"))
+    try:
+        torch.manual_seed(5)
+        x = torch.randn(4, 14, 14, 128, device=DEV).bfloat16().requires_grad_(True)
+        w = (torch.randn(256, 128, 3, 3, device=DEV) / 34).requires_grad_(True)
+        y = conv2d_nhwc(x, w, None, 2, 1, 1, None)
+        g = torch.randn_like(y)
+        y.backward(g)
+        xr, wr = x.detach().float().requires_grad_(True), w.detach().float().requires_grad_(True)
+        yr = F.conv2d(xr.permute(0, 3, 1, 2), wr, None, 2, 1).permute(0, 2, 3, 1)
+        yr.backward(g.float())
+        _close(y, yr, 2e-2)
+        _close(x.grad, xr.grad, 3e-2)
+        _close(w.grad, wr.grad, 1e-2)
+        kinds = {k.split(":")[0] for k in AT.CACHE}
+        assert {"conv2d_fwd", "conv2d_wgrad", "conv2d_dgrad"} <= kinds, AT.CACHE
+    finally:
+        AT.configure(enable=False)
+        AT.CACHE.clear()
+        AT._STATE["cache_file"] = None

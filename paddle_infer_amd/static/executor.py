@@ -111,8 +111,14 @@ class Executor:
             use_prune=False):
         program = program or default_main_program()
         scope = scope or global_scope()
-        if hasattr(program, "_program"):  # CompiledProgram
-            program = program._program
+        compiled = program if isinstance(program, CompiledProgram) else None
+        if compiled is not None:
+            program = compiled._program
+            if (compiled._build_strategy.allow_cuda_graph_capture and self.device.type == "cuda"
+                    and not compiled._data_parallel):
+                from .backward import op_role, FORWARD
+                if all(op_role(op) == FORWARD for op in program.global_block().ops):
+                    return self._run_graph(compiled, program, feed, fetch_list, scope, return_numpy)
         self._init_params(program, scope)
         if program is default_startup_program() or not program.global_block().ops:
             return []
@@ -173,9 +179,21 @@ class Executor:
 
         self._leafmap = {}
         self._training = training
+        dp = None
+        if compiled is not None and compiled._data_parallel and training:
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+                from .backward import op_role as _role, OPTIMIZE as _OPT, GRAD as _G
+                dp = sorted({n for op in ops if _role(op) == _OPT for n in op.input_names()
+                             if n.endswith(_G)})
         with torch.set_grad_enabled(training):
             for pos, oi in enumerate(order):
                 op = ops[oi]
+                if dp is not None:
+                    from .backward import op_role as _role, OPTIMIZE as _OPT
+                    if _role(op) == _OPT:
+                        _allreduce_grads(env, dp, compiled._build_strategy.fuse_all_reduce_ops)
+                        dp = None
                 self._run_op(op, sub, env, scope, program)
                 for n in frees[pos]:
                     if n not in fetch_names:
@@ -196,6 +214,37 @@ class Executor:
             v = v.detach()
             outs.append(v.cpu().numpy() if return_numpy else v)
         return outs
+
+    def _run_graph(self, compiled, program, feed, fetch_list, scope, return_numpy):
+        """Forward program replayed from a hipGraph: eager warm-up on the first call of a feed
+        signature, capture on the second (static feed buffers, outputs kept by the graph pool),
+        replay afterwards (feeds copied into the static buffers)."""
+        feed = feed or {}
+        fetch_list = fetch_list or []
+        names = [f.var_name if isinstance(f, Variable) else str(f) for f in fetch_list]
+        tens = {k: (v if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v))).to(self.device)
+                for k, v in feed.items()}
+        key = (id(program), program._version, tuple(names),
+               tuple((k, tuple(t.shape), t.dtype) for k, t in sorted(tens.items())))
+        ent = compiled._graphs.get(key)
+        if ent is None:  # warm-up run (allocator, kernel first-launch costs) outside capture
+            compiled._graphs[key] = "warm"
+            outs = self.run(program, tens, fetch_list, scope=scope, return_numpy=False)
+        elif ent == "warm":
+            static = {k: t.clone() for k, t in tens.items()}
+            self.run(program, static, fetch_list, scope=scope, return_numpy=False)  # prime plans
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                outs = self.run(program, static, fetch_list, scope=scope, return_numpy=False)
+            compiled._graphs[key] = (g, static, outs)
+            g.replay()
+        else:
+            g, static, outs = ent
+            for k, t in tens.items():
+                static[k].copy_(t)
+            g.replay()
+        return [o.cpu().numpy() if return_numpy else o.clone() for o in outs]
 
     def _run_op(self, op, sub, env, scope, program):
         from .ops_registry import run_paddle_op
@@ -359,21 +408,122 @@ def _zip_assign(refs, vals, fn):
         fn(refs, vals)
 
 
-class CompiledProgram:
-    def __init__(self, program_or_graph, build_strategy=None):
-        self._program = program_or_graph
-
-    def with_data_parallel(self, loss_name=None, build_strategy=None, exec_strategy=None, places=None):
-        return self
-
-
 class BuildStrategy:
+    """Reference `paddle.static.BuildStrategy` (`framework/details/build_strategy.h`). Honoured:
+    ``fuse_bn_act_ops`` / ``fuse_bn_add_act_ops`` (conv+bn folding), ``fuse_elewise_add_act_ops``
+    / ``fuse_gemm_epilogue`` (fc + bias + activation fusions), ``enable_auto_fusion`` (the whole
+    GPU pass list) on Paddle-typed inference programs; ``allow_cuda_graph_capture`` (forward
+    programs on the GPU replayed from a captured hipGraph per feed signature);
+    ``fuse_all_reduce_ops`` (data-parallel gradients all-reduced as ONE flat bucket per dtype).
+    The rest are accepted for API compatibility (memory reuse is the executor's eager GC)."""
+
     def __init__(self):
         self.fuse_elewise_add_act_ops = False
         self.fuse_bn_act_ops = False
+        self.fuse_bn_add_act_ops = False
+        self.fuse_gemm_epilogue = False
+        self.fuse_relu_depthwise_conv = False
+        self.fuse_all_reduce_ops = True
+        self.fuse_all_optimizer_ops = False
         self.enable_auto_fusion = False
+        self.enable_inplace = True
+        self.memory_optimize = True
+        self.allow_cuda_graph_capture = False
+        self.sync_batch_norm = False
+        self.num_trainers = 1
+        self.trainer_id = 0
+        self.reduce_strategy = 0
+        self.gradient_scale_strategy = 0
+        self.debug_graphviz_path = ""
+
+    def pass_list(self):
+        if self.enable_auto_fusion:
+            from ..inference.passes import GPU_PASSES
+            return list(GPU_PASSES)
+        ps = []
+        if self.fuse_bn_act_ops or self.fuse_bn_add_act_ops:
+            ps.append("conv_bn_fuse_pass")
+        if self.fuse_elewise_add_act_ops or self.fuse_gemm_epilogue:
+            ps += ["fc_fuse_pass", "fc_act_fuse_pass", "linear_bias_act_fuse_pass"]
+        return ps
 
 
 class ExecutionStrategy:
+    """Reference `paddle.static.ExecutionStrategy` (accepted; one HIP stream per process)."""
+
     def __init__(self):
         self.num_threads = 1
+        self.num_iteration_per_drop_scope = 100
+        self.num_iteration_per_run = 1
+        self.use_thread_barrier = False
+
+
+class CompiledProgram:
+    """Reference `python/paddle/fluid/compiler.py:CompiledProgram`: a program prepared once for
+    repeated execution. Here: BuildStrategy fusion passes applied to a clone of a Paddle-typed
+    forward program; ``with_data_parallel`` = one process per GPU (the launcher's world):
+    gradients are averaged over the default group (RCCL on GPUs, gloo on CPUs) right before the
+    first optimizer op of every run; ``allow_cuda_graph_capture`` replays forward runs from a
+    hipGraph captured per (feed shapes/dtypes, fetch list)."""
+
+    def __init__(self, program_or_graph, build_strategy=None):
+        self._source = program_or_graph
+        self._build_strategy = build_strategy or BuildStrategy()
+        self._exec_strategy = ExecutionStrategy()
+        self._data_parallel = False
+        self._loss_name = None
+        self._prepared = None
+        self._graphs = {}
+
+    @property
+    def _program(self):
+        if self._prepared is None:
+            self._prepared = self._prepare()
+        return self._prepared
+
+    def _prepare(self):
+        prog = self._source
+        ps = self._build_strategy.pass_list()
+        from .backward import op_role, FORWARD
+        ops = prog.global_block().ops
+        if ps and ops and all(op.func is None and op_role(op) == FORWARD for op in ops):
+            from ..inference.passes import apply_passes
+            prog = prog.clone()
+            apply_passes(prog, ps, fetch_names=tuple(prog.fetch_names))
+        return prog
+
+    def with_data_parallel(self, loss_name=None, build_strategy=None, exec_strategy=None,
+                           places=None, share_vars_from=None):
+        self._data_parallel = True
+        self._loss_name = loss_name
+        if build_strategy is not None:
+            self._build_strategy = build_strategy
+            self._prepared = None
+        if exec_strategy is not None:
+            self._exec_strategy = exec_strategy
+        return self
+
+
+def _allreduce_grads(env, names, fused=True):
+    """Average the named gradients over the default process group (one flat bucket per dtype)."""
+    import torch.distributed as dist
+    world = dist.get_world_size()
+    ts = [env[n] for n in names if n in env and isinstance(env[n], torch.Tensor)]
+    if not ts:
+        return
+    if not fused:
+        for t in ts:
+            dist.all_reduce(t)
+            t.div_(world)
+        return
+    from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
+    by_dtype = {}
+    for t in ts:
+        by_dtype.setdefault(t.dtype, []).append(t)
+    for group in by_dtype.values():
+        flat = _flatten_dense_tensors([t.detach() for t in group])
+        dist.all_reduce(flat)
+        flat.div_(world)
+        for t, v in zip(group, _unflatten_dense_tensors(flat, group)):
+            with torch.no_grad():
+                t.copy_(v)

@@ -11,6 +11,8 @@ __version__ = "0.1.0"
 import torch as _torch  # noqa: F401  (must load before the HIP kernel library)
 
 from .framework import tensor_patch as _tensor_patch  # noqa: F401
+from .framework import allocator as _allocator
+_allocator.maybe_enable_from_env()  # FLAGS_allocator_strategy=auto_growth: own HIP allocator
 from .framework import random as _random
 from .framework.random import seed, get_rng_state, set_rng_state, get_cuda_rng_state, set_cuda_rng_state  # noqa: F401,E501
 from .framework.dtype import (float32, float64, float16, bfloat16, int8, uint8, int16, int32,  # noqa: F401

@@ -4,6 +4,8 @@
   (C ABI, loaded with ctypes AFTER torch so it binds to the HIP runtime torch already loaded).
 * ``_lib/libpiamd_runtime.so`` — the C++ host runtime (``csrc/runtime/*.cc``: static-graph
   executor scheduler, data-loader ring) built with g++.
+* ``_lib/libpiamd_alloc.so`` — the auto-growth best-fit device allocator (``csrc/alloc``,
+  host-only HIP runtime code, g++ against the HIP headers; plugged into PyTorch's HIP allocator).
 * ``_lib/libpiamd_capi.so`` — the C inference API (``csrc/capi``: reference ``capi_exp``
   ``pd_inference_api.h``), g++ against the embedded Python runtime.
 
@@ -28,6 +30,9 @@ KERNEL_LIB = os.path.join(LIBDIR, "libpiamd_kernels.so")
 RUNTIME_LIB = os.path.join(LIBDIR, "libpiamd_runtime.so")
 CDIR = os.path.join(ROOT, "csrc", "capi")
 CAPI_LIB = os.path.join(LIBDIR, "libpiamd_capi.so")
+ADIR = os.path.join(ROOT, "csrc", "alloc")
+ALLOC_LIB = os.path.join(LIBDIR, "libpiamd_alloc.so")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("PIAMD_ARCH", "gfx950")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 
@@ -95,6 +100,11 @@ def build(verbose: bool = True, jobs: int | None = None) -> None:
     if rsrcs:
         _build_lib(rsrcs, RUNTIME_LIB, "g++", CXX_FLAGS, ["-pthread"], _newest_header(RDIR),
                    verbose, jobs)
+    asrcs = sorted(glob.glob(os.path.join(ADIR, "*.cc")))
+    if asrcs:  # host-only HIP runtime code (no kernels): g++ against the HIP headers
+        _build_lib(asrcs, ALLOC_LIB, "g++", CXX_FLAGS + ["-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include"],
+                   ["-pthread", f"-L{ROCM}/lib", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"],
+                   _newest_header(ADIR), verbose, jobs)
     csrcs = sorted(glob.glob(os.path.join(CDIR, "*.cc")))
     if csrcs:
         import sysconfig

@@ -168,23 +168,34 @@ class cuda:  # namespace paddle.device.cuda
 
     @staticmethod
     def max_memory_allocated(device=None):
+        if _own_alloc():
+            return _own_stats(device)["peak_allocated"]
         return torch.cuda.max_memory_allocated(_parse(device) if device is not None else None)
 
     @staticmethod
     def max_memory_reserved(device=None):
+        if _own_alloc():
+            return _own_stats(device)["peak_reserved"]
         return torch.cuda.max_memory_reserved(_parse(device) if device is not None else None)
 
     @staticmethod
     def memory_allocated(device=None):
+        if _own_alloc():
+            return _own_stats(device)["allocated"]
         return torch.cuda.memory_allocated(_parse(device) if device is not None else None)
 
     @staticmethod
     def memory_reserved(device=None):
+        if _own_alloc():
+            return _own_stats(device)["reserved"]
         return torch.cuda.memory_reserved(_parse(device) if device is not None else None)
 
     @staticmethod
     def empty_cache():
-        if torch.cuda.is_available():
+        if _own_alloc():
+            from .framework import allocator as _a
+            _a.empty_cache(torch.cuda.current_device())
+        elif torch.cuda.is_available():
             torch.cuda.empty_cache()
 
     @staticmethod
@@ -202,3 +213,19 @@ class cuda:  # namespace paddle.device.cuda
 
 def synchronize(device=None):
     cuda.synchronize(device)
+
+
+def _own_alloc():
+    from .framework import allocator as _a
+    return _a.active()
+
+
+def _own_stats(device):
+    from .framework import allocator as _a
+    if device is None:
+        d = torch.cuda.current_device()
+    elif isinstance(device, int):
+        d = device
+    else:
+        d = getattr(_parse(device), "index", 0) or 0
+    return _a.stats(d)

@@ -1,0 +1,76 @@
+"""Device allocator selection (reference ``FLAGS_allocator_strategy``, `paddle/fluid/memory/
+allocation/allocator_facade.cc`): ``"auto_growth"`` installs the framework's own auto-growth
+best-fit allocator (``csrc/alloc/allocator.cc`` → ``_lib/libpiamd_alloc.so``) as PyTorch-ROCm's
+HIP allocator; anything else keeps PyTorch's caching allocator.
+
+Must run before the first device allocation of the process (the package does it at import when
+``FLAGS_allocator_strategy=auto_growth`` is in the environment). Streams: a freed block is reused
+only by allocations on the stream it was allocated on (stream-ordered reuse, as the reference's
+StreamSafeCUDAAllocator); tensors handed to another stream must outlive that stream's work.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_STATE = {"active": False, "lib": None}
+STAT_NAMES = ("allocated", "reserved", "peak_allocated", "peak_reserved", "num_alloc", "num_free",
+              "num_chunk_alloc", "num_chunk_free")
+
+
+def lib_path():
+    from .. import _build
+    return _build.ALLOC_LIB
+
+
+def _lib():
+    if _STATE["lib"] is None:
+        path = lib_path()
+        if not os.path.exists(path):
+            raise RuntimeError(f"allocator library not built ({path}); run paddle_infer_amd._build")
+        lib = ctypes.CDLL(path)
+        lib.piamd_alloc_stats.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_longlong)]
+        lib.piamd_alloc_release.argtypes = [ctypes.c_int]
+        lib.piamd_alloc_reset_peak.argtypes = [ctypes.c_int]
+        _STATE["lib"] = lib
+    return _STATE["lib"]
+
+
+def active() -> bool:
+    return _STATE["active"]
+
+
+def enable(strategy: str = "auto_growth") -> bool:
+    """Install the allocator for ``strategy``; returns whether the framework allocator is active."""
+    if strategy != "auto_growth":
+        return False
+    if _STATE["active"]:
+        return True
+    from torch.cuda.memory import CUDAPluggableAllocator, change_current_allocator
+    _lib()
+    change_current_allocator(CUDAPluggableAllocator(lib_path(), "piamd_alloc", "piamd_free"))
+    _STATE["active"] = True
+    return True
+
+
+def stats(device: int = 0) -> dict:
+    buf = (ctypes.c_longlong * 8)()
+    _lib().piamd_alloc_stats(int(device), buf)
+    return dict(zip(STAT_NAMES, list(buf)))
+
+
+def empty_cache(device: int = 0) -> None:
+    _lib().piamd_alloc_release(int(device))
+
+
+def reset_peak(device: int = 0) -> None:
+    _lib().piamd_alloc_reset_peak(int(device))
+
+
+def maybe_enable_from_env() -> None:
+    if os.environ.get("FLAGS_allocator_strategy", "") == "auto_growth":
+        try:
+            enable("auto_growth")
+        except Exception as e:  # allocator already initialised / library missing: say so once
+            import warnings
+            warnings.warn(f"FLAGS_allocator_strategy=auto_growth not applied: {e}", RuntimeWarning)

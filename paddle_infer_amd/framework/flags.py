@@ -2,8 +2,10 @@
 
 Flags honoured by this framework: FLAGS_check_nan_inf (NaN/Inf checker on every op output through
 ``utils.nan_inf``), FLAGS_cudnn_deterministic (torch deterministic algorithms),
-FLAGS_use_hipgraph (inference predictor graph capture), FLAGS_fraction_of_gpu_memory_to_use /
-FLAGS_allocator_strategy (accepted; the caching allocator is torch's).
+FLAGS_use_hipgraph (inference predictor graph capture), FLAGS_allocator_strategy ("auto_growth"
+in the environment or set before the first device allocation installs the framework's own
+auto-growth best-fit HIP allocator, ``framework/allocator.py``; the in-process default stays
+PyTorch's caching allocator), FLAGS_fraction_of_gpu_memory_to_use (accepted).
 """
 from __future__ import annotations
 
@@ -36,6 +38,13 @@ def set_flags(flags: dict):
         if k == "FLAGS_check_nan_inf":
             from ..utils import nan_inf
             nan_inf.enable(bool(v))
+        if k == "FLAGS_allocator_strategy" and v == "auto_growth":
+            from . import allocator
+            try:
+                allocator.enable("auto_growth")
+            except RuntimeError as e:  # device memory already in use by the caching allocator
+                import warnings
+                warnings.warn(f"FLAGS_allocator_strategy=auto_growth not applied: {e}", RuntimeWarning)
 
 
 def get_flags(flags):

@@ -204,6 +204,27 @@ class Engine:
         self.strategy = strategy or Strategy()
         self.history = {"loss": []}
 
+    def plan(self, global_batch, n_gpus=None, seq_len=None, cluster=None):
+        """``Strategy.auto_mode = "full"``: search the parallel layout (dp / tp / pp, sharding
+        stage, micro-batch, recompute) for this model with the MI355X cost model
+        (``planner.py``), write it into ``self.strategy`` and return the Plan."""
+        from . import planner as _pl
+        cfg = getattr(self.model, "config", None) or getattr(self.model, "cfg", None)
+        if cfg is None and hasattr(self.model, "gpt"):
+            cfg = getattr(self.model.gpt, "config", None)
+        if cfg is None:
+            raise ValueError("auto planning needs a transformer model with a .config")
+        spec = _pl.ModelSpec.from_gpt_config(cfg)
+        if seq_len:
+            spec.seq_len = int(seq_len)
+        if n_gpus is None:
+            import torch.distributed as dist
+            n_gpus = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        c = cluster or _pl.ClusterSpec(n_gpus=int(n_gpus))
+        best = _pl.plan(spec, c, int(global_batch))[0]
+        self.hybrid_configs = _pl.apply_to_strategy(best, self.strategy, int(global_batch))
+        return best
+
     def _ctx(self):
         if self.strategy.amp.enable:
             dev = "cuda" if torch.cuda.is_available() else "cpu"

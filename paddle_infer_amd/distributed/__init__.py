@@ -36,3 +36,5 @@ from . import auto_parallel  # noqa: F401,E402
 from . import elastic  # noqa: F401,E402
 from .auto_parallel import ProcessMesh, shard_tensor, shard_op, reshard  # noqa: F401,E402
 from .communication import stream  # noqa: F401,E402
+from .dataset import (InMemoryDataset, QueueDataset, CountFilterEntry, ShowClickEntry,  # noqa: F401,E402
+                      ProbabilityEntry)

@@ -446,3 +446,157 @@ class _Layers:
 
 layers = _Layers()
 copy  # noqa
+
+
+# ---- reference fleet classes (`fleet/base/role_maker.py`, `util_factory.py`, `fleet.py`,
+# `data_generator/data_generator.py`) -------------------------------------------------------------
+class Role:
+    WORKER = 1
+    SERVER = 2
+    HETER_WORKER = 3
+    ALL = 4
+    COORDINATOR = 5
+
+
+class UtilBase:
+    """Collective helpers over the world group (reference `fleet/base/util_factory.py`)."""
+
+    def all_reduce(self, input, mode="sum", comm_world="worker"):  # noqa: A002
+        import numpy as np
+        import torch.distributed as dist
+        t = torch.as_tensor(np.asarray(input), dtype=torch.float64)
+        if dist.is_available() and dist.is_initialized():
+            op = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[mode]
+            dist.all_reduce(t, op=op)
+        return t.numpy()
+
+    def barrier(self, comm_world="worker"):
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            dist.barrier()
+
+    def all_gather(self, input, comm_world="worker"):  # noqa: A002
+        import torch.distributed as dist
+        if not (dist.is_available() and dist.is_initialized()):
+            return [input]
+        out = [None] * dist.get_world_size()
+        dist.all_gather_object(out, input)
+        return out
+
+    def get_file_shard(self, files):
+        """This worker's contiguous share of ``files`` (remainder to the first workers)."""
+        n, r = worker_num(), worker_index()
+        per, extra = divmod(len(files), n)
+        beg = r * per + min(r, extra)
+        return files[beg:beg + per + (1 if r < extra else 0)]
+
+    def print_on_rank(self, message, rank_id):
+        if worker_index() == rank_id:
+            print(message, flush=True)
+
+
+util = UtilBase()
+
+
+class Fleet:
+    """Object form of the fleet module API (reference `fleet/fleet.py:Fleet`)."""
+
+    def init(self, role_maker=None, is_collective=True, strategy=None, log_level="INFO"):
+        return init(role_maker, is_collective, strategy, log_level)
+
+    def distributed_model(self, model):
+        return distributed_model(model)
+
+    def distributed_optimizer(self, optimizer, strategy=None):
+        return distributed_optimizer(optimizer, strategy)
+
+    def get_hybrid_communicate_group(self):
+        return get_hybrid_communicate_group()
+
+    def worker_index(self):
+        return worker_index()
+
+    def worker_num(self):
+        return worker_num()
+
+    def is_first_worker(self):
+        return is_first_worker()
+
+    def is_worker(self):
+        return is_worker()
+
+    def is_server(self):
+        return is_server()
+
+    def barrier_worker(self):
+        return barrier_worker()
+
+    @property
+    def util(self):
+        return util
+
+
+class MultiSlotDataGenerator:
+    """User data generator (reference `data_generator.py`): subclass and define
+    ``generate_sample(line)`` yielding ``[(slot_name, [values...]), ...]`` per instance;
+    ``run_from_stdin`` / ``run_from_memory`` write the MultiSlot text format the datasets read
+    (per slot: count then values)."""
+
+    def __init__(self):
+        self.batch_size_ = 32
+
+    def set_batch(self, batch_size):
+        self.batch_size_ = int(batch_size)
+
+    def generate_sample(self, line):
+        raise NotImplementedError("define generate_sample(line) in the subclass")
+
+    def generate_batch(self, samples):
+        def gen():
+            for s in samples:
+                yield s
+        return gen
+
+    def _gen_str(self, line):
+        parts = []
+        for _name, vals in line:
+            vals = list(vals)
+            if not vals:
+                raise ValueError("MultiSlot slots need at least one value")
+            parts.append(str(len(vals)))
+            parts += [self._fmt(v) for v in vals]
+        return " ".join(parts) + "\n"
+
+    def _fmt(self, v):
+        if isinstance(v, float):
+            return repr(v)
+        return str(int(v))
+
+    def _emit(self, lines, out):
+        batch = []
+        for line in lines:
+            for sample in self.generate_sample(line)():
+                batch.append(sample)
+                if len(batch) == self.batch_size_:
+                    for s in self.generate_batch(batch)():
+                        out.write(self._gen_str(s))
+                    batch = []
+        for s in self.generate_batch(batch)():
+            out.write(self._gen_str(s))
+
+    def run_from_stdin(self):
+        import sys
+        self._emit(sys.stdin, sys.stdout)
+
+    def run_from_memory(self, lines=None):
+        import io as _io
+        buf = _io.StringIO()
+        self._emit(lines or [], buf)
+        return buf.getvalue()
+
+
+class MultiSlotStringDataGenerator(MultiSlotDataGenerator):
+    """Same protocol with string values written verbatim."""
+
+    def _fmt(self, v):
+        return str(v)

@@ -82,3 +82,6 @@ def Print(input, first_n=-1, message=None, summarize=20, print_tensor_name=True,
           print_tensor_type=True, print_tensor_shape=True, print_tensor_lod=True,
           print_phase="both"):
     return input
+from .extras import (xpu_places, npu_places, mlu_places, ipu_shard_guard, set_ipu_shard,  # noqa: E402,F401
+                     IpuStrategy, IpuCompiledProgram, WeightNormParamAttr, ExponentialMovingAverage,
+                     auc, ctr_metric_bundle, exponential_decay, create_lod_tensor)

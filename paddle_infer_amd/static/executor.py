@@ -198,6 +198,8 @@ class Executor:
                 for n in frees[pos]:
                     if n not in fetch_names:
                         env.pop(n, None)
+        for hook in getattr(program, "_post_run_hooks", ()) if training else ():
+            hook(scope, program)  # e.g. static.ExponentialMovingAverage
         if training:  # persistable outputs (updated params / accumulators) back into the Scope
             for n in list(env):
                 if n in program.params and n not in (feed or {}):

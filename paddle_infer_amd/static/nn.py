@@ -130,3 +130,12 @@ def while_loop(cond, body, loop_vars, is_test=False, name=None):  # noqa: A002
 def py_func(func, x, out, backward_func=None, skip_vars_in_backward_input=None):
     xs = x if isinstance(x, (list, tuple)) else [x]
     return _record(func, tuple(xs), {})
+
+
+from .nn_extra import (case, switch_case, bilinear_tensor_product, conv3d, conv3d_transpose,  # noqa: E402,F401
+                       crf_decoding, data_norm, deform_conv2d, nce, row_conv, spectral_norm,
+                       multi_box_head, sequence_pool, sequence_first_step, sequence_last_step,
+                       sequence_softmax, sequence_concat, sequence_slice, sequence_expand,
+                       sequence_expand_as, sequence_pad, sequence_unpad, sequence_reshape,
+                       sequence_scatter, sequence_enumerate, sequence_reverse, sequence_conv,
+                       StaticRNN)

@@ -38,3 +38,17 @@ def unique_name(prefix="tmp"):
 def try_import(module_name):
     import importlib
     return importlib.import_module(module_name)
+
+
+def require_version(min_version, max_version=None):
+    """Reference `utils/install_check.py`-style version gate: raise unless this framework's version
+    lies in [min_version, max_version]."""
+    from .. import __version__
+
+    def parse(v):
+        return tuple(int(p) for p in str(v).split(".")[:3] if p.isdigit())
+    cur = parse(__version__)
+    if parse(min_version) > cur or (max_version is not None and cur > parse(max_version)):
+        raise Exception(f"paddle_infer_amd version {__version__} is not in "
+                        f"[{min_version}, {max_version or 'any'}]")
+    return True

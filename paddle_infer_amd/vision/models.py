@@ -23,6 +23,8 @@ def _cbr(cin, cout, k, s=1, p=0, groups=1, act="relu"):
         layers.append(nn.ReLU6())
     elif act == "hardswish":
         layers.append(nn.Hardswish())
+    elif act == "swish":
+        layers.append(nn.Swish())
     return nn.Sequential(*layers)
 
 
@@ -568,3 +570,196 @@ def densenet169(pretrained=False, **kw):
 def densenet201(pretrained=False, **kw):
     _no_pretrained(pretrained)
     return DenseNet(201, **kw)
+
+
+def densenet161(pretrained=False, **kw):
+    _no_pretrained(pretrained)
+    return DenseNet(161, **kw)
+
+
+def densenet264(pretrained=False, **kw):
+    _no_pretrained(pretrained)
+    return DenseNet(264, **kw)
+
+
+def shufflenet_v2_x0_25(pretrained=False, **kw):
+    _no_pretrained(pretrained)
+    return ShuffleNetV2(0.25, **kw)
+
+
+def shufflenet_v2_x0_33(pretrained=False, **kw):
+    _no_pretrained(pretrained)
+    return ShuffleNetV2(0.33, **kw)
+
+
+def shufflenet_v2_x1_5(pretrained=False, **kw):
+    _no_pretrained(pretrained)
+    return ShuffleNetV2(1.5, **kw)
+
+
+def shufflenet_v2_swish(pretrained=False, **kw):
+    _no_pretrained(pretrained)
+    return ShuffleNetV2(1.0, act="swish", **kw)
+
+
+# ----------------------------------------------------------------------------------------- GoogLeNet
+class _Inception(nn.Layer):
+    """GoogLeNet inception module (reference `vision/models/googlenet.py`): 1×1 | 1×1→3×3 |
+    1×1→5×5 | pool→1×1 branches concatenated on channels."""
+
+    def __init__(self, cin, c1, c3r, c3, c5r, c5, proj):
+        super().__init__()
+        self.b1 = _cbr(cin, c1, 1)
+        self.b2 = nn.Sequential(_cbr(cin, c3r, 1), _cbr(c3r, c3, 3, 1, 1))
+        self.b3 = nn.Sequential(_cbr(cin, c5r, 1), _cbr(c5r, c5, 5, 1, 2))
+        self.b4 = nn.Sequential(nn.MaxPool2D(3, 1, 1), _cbr(cin, proj, 1))
+
+    def forward(self, x):
+        return torch.cat([self.b1(x), self.b2(x), self.b3(x), self.b4(x)], 1)
+
+
+class GoogLeNet(nn.Layer):
+    """Reference `python/paddle/vision/models/googlenet.py` (returns (out, aux1, aux2) like the
+    reference: the two auxiliary heads read the 4a / 4d inception outputs)."""
+
+    def __init__(self, num_classes=1000, with_pool=True):
+        super().__init__()
+        self.stem = nn.Sequential(_cbr(3, 64, 7, 2, 3), nn.MaxPool2D(3, 2, 1), _cbr(64, 64, 1),
+                                  _cbr(64, 192, 3, 1, 1), nn.MaxPool2D(3, 2, 1))
+        self.i3 = nn.Sequential(_Inception(192, 64, 96, 128, 16, 32, 32),
+                                _Inception(256, 128, 128, 192, 32, 96, 64), nn.MaxPool2D(3, 2, 1))
+        self.i4a = _Inception(480, 192, 96, 208, 16, 48, 64)
+        self.i4bcd = nn.Sequential(_Inception(512, 160, 112, 224, 24, 64, 64),
+                                   _Inception(512, 128, 128, 256, 24, 64, 64),
+                                   _Inception(512, 112, 144, 288, 32, 64, 64))
+        self.i4e = nn.Sequential(_Inception(528, 256, 160, 320, 32, 128, 128), nn.MaxPool2D(3, 2, 1))
+        self.i5 = nn.Sequential(_Inception(832, 256, 160, 320, 32, 128, 128),
+                                _Inception(832, 384, 192, 384, 48, 128, 128))
+        self.num_classes, self.with_pool = num_classes, with_pool
+        self.pool = nn.AdaptiveAvgPool2D(1)
+        if num_classes > 0:
+            self.dropout = nn.Dropout(0.4)
+            self.fc = nn.Linear(1024, num_classes)
+            self.aux1 = nn.Sequential(nn.AdaptiveAvgPool2D(4), _cbr(512, 128, 1), nn.Flatten(),
+                                      nn.Linear(2048, 1024), nn.ReLU(), nn.Dropout(0.7),
+                                      nn.Linear(1024, num_classes))
+            self.aux2 = nn.Sequential(nn.AdaptiveAvgPool2D(4), _cbr(528, 128, 1), nn.Flatten(),
+                                      nn.Linear(2048, 1024), nn.ReLU(), nn.Dropout(0.7),
+                                      nn.Linear(1024, num_classes))
+
+    def forward(self, x):
+        x = self.i3(self.stem(x))
+        a = self.i4a(x)
+        d = self.i4bcd(a)
+        x = self.i5(self.i4e(d))
+        if self.with_pool:
+            x = self.pool(x)
+        if self.num_classes <= 0:
+            return x
+        out = self.fc(self.dropout(torch.flatten(x, 1)))
+        return out, self.aux1(a), self.aux2(d)
+
+
+def googlenet(pretrained=False, **kw):
+    _no_pretrained(pretrained)
+    return GoogLeNet(**kw)
+
+
+# ----------------------------------------------------------------------------------------- InceptionV3
+class _IncA(nn.Layer):
+    def __init__(self, cin, pool_feat):
+        super().__init__()
+        self.b1 = _cbr(cin, 64, 1)
+        self.b5 = nn.Sequential(_cbr(cin, 48, 1), _cbr(48, 64, 5, 1, 2))
+        self.b3 = nn.Sequential(_cbr(cin, 64, 1), _cbr(64, 96, 3, 1, 1), _cbr(96, 96, 3, 1, 1))
+        self.bp = nn.Sequential(nn.AvgPool2D(3, 1, 1), _cbr(cin, pool_feat, 1))
+
+    def forward(self, x):
+        return torch.cat([self.b1(x), self.b5(x), self.b3(x), self.bp(x)], 1)
+
+
+class _IncB(nn.Layer):  # grid reduction 35 -> 17
+    def __init__(self, cin):
+        super().__init__()
+        self.b3 = _cbr(cin, 384, 3, 2)
+        self.b3d = nn.Sequential(_cbr(cin, 64, 1), _cbr(64, 96, 3, 1, 1), _cbr(96, 96, 3, 2))
+        self.pool = nn.MaxPool2D(3, 2)
+
+    def forward(self, x):
+        return torch.cat([self.b3(x), self.b3d(x), self.pool(x)], 1)
+
+
+def _cbr_hw(cin, cout, kh, kw, ph, pw):
+    return nn.Sequential(nn.Conv2D(cin, cout, (kh, kw), 1, (ph, pw), bias_attr=False),
+                         nn.BatchNorm2D(cout), nn.ReLU())
+
+
+class _IncC(nn.Layer):  # factorised 7x7 (17x17 grid)
+    def __init__(self, cin, c7):
+        super().__init__()
+        self.b1 = _cbr(cin, 192, 1)
+        self.b7 = nn.Sequential(_cbr(cin, c7, 1), _cbr_hw(c7, c7, 1, 7, 0, 3), _cbr_hw(c7, 192, 7, 1, 3, 0))
+        self.b7d = nn.Sequential(_cbr(cin, c7, 1), _cbr_hw(c7, c7, 7, 1, 3, 0), _cbr_hw(c7, c7, 1, 7, 0, 3),
+                                 _cbr_hw(c7, c7, 7, 1, 3, 0), _cbr_hw(c7, 192, 1, 7, 0, 3))
+        self.bp = nn.Sequential(nn.AvgPool2D(3, 1, 1), _cbr(cin, 192, 1))
+
+    def forward(self, x):
+        return torch.cat([self.b1(x), self.b7(x), self.b7d(x), self.bp(x)], 1)
+
+
+class _IncD(nn.Layer):  # grid reduction 17 -> 8
+    def __init__(self, cin):
+        super().__init__()
+        self.b3 = nn.Sequential(_cbr(cin, 192, 1), _cbr(192, 320, 3, 2))
+        self.b7 = nn.Sequential(_cbr(cin, 192, 1), _cbr_hw(192, 192, 1, 7, 0, 3),
+                                _cbr_hw(192, 192, 7, 1, 3, 0), _cbr(192, 192, 3, 2))
+        self.pool = nn.MaxPool2D(3, 2)
+
+    def forward(self, x):
+        return torch.cat([self.b3(x), self.b7(x), self.pool(x)], 1)
+
+
+class _IncE(nn.Layer):  # expanded filter bank (8x8 grid)
+    def __init__(self, cin):
+        super().__init__()
+        self.b1 = _cbr(cin, 320, 1)
+        self.b3 = _cbr(cin, 384, 1)
+        self.b3a, self.b3b = _cbr_hw(384, 384, 1, 3, 0, 1), _cbr_hw(384, 384, 3, 1, 1, 0)
+        self.b3d = nn.Sequential(_cbr(cin, 448, 1), _cbr(448, 384, 3, 1, 1))
+        self.b3da, self.b3db = _cbr_hw(384, 384, 1, 3, 0, 1), _cbr_hw(384, 384, 3, 1, 1, 0)
+        self.bp = nn.Sequential(nn.AvgPool2D(3, 1, 1), _cbr(cin, 192, 1))
+
+    def forward(self, x):
+        a = self.b3(x)
+        d = self.b3d(x)
+        return torch.cat([self.b1(x), self.b3a(a), self.b3b(a), self.b3da(d), self.b3db(d), self.bp(x)], 1)
+
+
+class InceptionV3(nn.Layer):
+    """Reference `python/paddle/vision/models/inceptionv3.py` (299×299 inputs)."""
+
+    def __init__(self, num_classes=1000, with_pool=True):
+        super().__init__()
+        self.stem = nn.Sequential(_cbr(3, 32, 3, 2), _cbr(32, 32, 3), _cbr(32, 64, 3, 1, 1),
+                                  nn.MaxPool2D(3, 2), _cbr(64, 80, 1), _cbr(80, 192, 3), nn.MaxPool2D(3, 2))
+        self.blocks = nn.Sequential(_IncA(192, 32), _IncA(256, 64), _IncA(288, 64), _IncB(288),
+                                    _IncC(768, 128), _IncC(768, 160), _IncC(768, 160), _IncC(768, 192),
+                                    _IncD(768), _IncE(1280), _IncE(2048))
+        self.num_classes, self.with_pool = num_classes, with_pool
+        self.pool = nn.AdaptiveAvgPool2D(1)
+        if num_classes > 0:
+            self.dropout = nn.Dropout(0.2)
+            self.fc = nn.Linear(2048, num_classes)
+
+    def forward(self, x):
+        x = self.blocks(self.stem(x))
+        if self.with_pool:
+            x = self.pool(x)
+        if self.num_classes <= 0:
+            return x
+        return self.fc(self.dropout(torch.flatten(x, 1)))
+
+
+def inception_v3(pretrained=False, **kw):
+    _no_pretrained(pretrained)
+    return InceptionV3(**kw)

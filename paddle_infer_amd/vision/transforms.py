@@ -403,3 +403,138 @@ class RandomErasing(BaseTransform):
                     img[i:i + eh, j:j + ew] = self.value
                 return img
         return img
+
+
+# ------------------------------------------------------------------------------------ affine / perspective
+def _warp(img, inv_map, interpolation, fill):
+    """Sample ``img`` at inverse-mapped pixel centres: inv_map(x, y) -> (src_x, src_y) arrays."""
+    t = img if _is_tensor(img) else torch.from_numpy(np.ascontiguousarray(img)).permute(2, 0, 1)
+    dt = t.dtype
+    C, H, W = t.shape
+    ys, xs = torch.meshgrid(torch.arange(H, dtype=torch.float64) + 0.5,
+                            torch.arange(W, dtype=torch.float64) + 0.5, indexing="ij")
+    sx, sy = inv_map(xs, ys)
+    grid = torch.stack([sx / W * 2 - 1, sy / H * 2 - 1], -1).float()[None]
+    src = t[None].float()
+    mode = "nearest" if interpolation == "nearest" else "bilinear"
+    out = F.grid_sample(src, grid, mode=mode, padding_mode="zeros", align_corners=False)[0]
+    if fill:
+        ones = torch.ones(1, 1, H, W)
+        cover = F.grid_sample(ones, grid, mode=mode, padding_mode="zeros", align_corners=False)[0]
+        out = out + (1 - cover) * torch.as_tensor(fill, dtype=torch.float32).reshape(-1, 1, 1)
+    out = out.round().clamp(0, 255).to(dt) if not dt.is_floating_point else out.to(dt)
+    return out if _is_tensor(img) else out.permute(1, 2, 0).numpy()
+
+
+def _affine_matrix(center, angle, translate, scale, shear):
+    """Forward 2x3 matrix (reference functional._get_affine_matrix): T(center+translate) · R·Sh·S ·
+    T(−center), angle / shear in degrees (clockwise image rotation like the reference)."""
+    cx, cy = center
+    tx, ty = translate
+    rot = math.radians(angle)
+    sx, sy = (math.radians(shear[0]), math.radians(shear[1])) if isinstance(shear, (list, tuple)) \
+        else (math.radians(shear), 0.0)
+    a = math.cos(rot - sy) / math.cos(sy)
+    b = -math.cos(rot - sy) * math.tan(sx) / math.cos(sy) - math.sin(rot)
+    c = math.sin(rot - sy) / math.cos(sy)
+    d = -math.sin(rot - sy) * math.tan(sx) / math.cos(sy) + math.cos(rot)
+    m = np.array([[a, b, 0.0], [c, d, 0.0]]) * scale
+    m[0, 2] = cx + tx - (m[0, 0] * cx + m[0, 1] * cy)
+    m[1, 2] = cy + ty - (m[1, 0] * cx + m[1, 1] * cy)
+    return m
+
+
+def affine(img, angle, translate, scale, shear, interpolation="nearest", fill=0, center=None):
+    """Reference `vision/transforms/functional.py:affine`."""
+    H, W = _hw(img)
+    center = center if center is not None else (W * 0.5, H * 0.5)
+    m = np.vstack([_affine_matrix(center, angle, translate, scale, shear), [0, 0, 1]])
+    inv = np.linalg.inv(m)
+
+    def inv_map(x, y):
+        return inv[0, 0] * x + inv[0, 1] * y + inv[0, 2], inv[1, 0] * x + inv[1, 1] * y + inv[1, 2]
+    return _warp(img, inv_map, interpolation, fill)
+
+
+def _homography(src, dst):
+    """3x3 H with H·src_i ∝ dst_i for 4 point pairs."""
+    A, b = [], []
+    for (x, y), (u, v) in zip(src, dst):
+        A.append([x, y, 1, 0, 0, 0, -u * x, -u * y])
+        A.append([0, 0, 0, x, y, 1, -v * x, -v * y])
+        b += [u, v]
+    h = np.linalg.solve(np.asarray(A, dtype=np.float64), np.asarray(b, dtype=np.float64))
+    return np.append(h, 1.0).reshape(3, 3)
+
+
+def perspective(img, startpoints, endpoints, interpolation="nearest", fill=0):
+    """Reference `vision/transforms/functional.py:perspective`: the image plane warped so
+    ``startpoints`` (4 corners, [x, y]) land on ``endpoints``."""
+    Hm = _homography(endpoints, startpoints)  # output pixel -> source pixel
+
+    def inv_map(x, y):
+        w = Hm[2, 0] * x + Hm[2, 1] * y + Hm[2, 2]
+        return (Hm[0, 0] * x + Hm[0, 1] * y + Hm[0, 2]) / w, (Hm[1, 0] * x + Hm[1, 1] * y + Hm[1, 2]) / w
+    return _warp(img, inv_map, interpolation, fill)
+
+
+def erase(img, i, j, h, w, v, inplace=False):
+    """Reference `vision/transforms/functional.py:erase`: region [i:i+h, j:j+w] set to ``v``."""
+    out = img if inplace else (img.clone() if _is_tensor(img) else img.copy())
+    if _is_tensor(out):
+        out[..., i:i + h, j:j + w] = torch.as_tensor(v, dtype=out.dtype) if not isinstance(v, numbers.Number) else v
+    else:
+        out[i:i + h, j:j + w] = v
+    return out
+
+
+class RandomAffine(BaseTransform):
+    """Reference `transforms.py:RandomAffine`."""
+
+    def __init__(self, degrees, translate=None, scale=None, shear=None, interpolation="nearest",
+                 fill=0, center=None, keys=None):
+        super().__init__(keys)
+        self.degrees = (-degrees, degrees) if isinstance(degrees, numbers.Number) else tuple(degrees)
+        self.translate, self.scale, self.interpolation, self.fill, self.center = \
+            translate, scale, interpolation, fill, center
+        if shear is not None and isinstance(shear, numbers.Number):
+            shear = (-shear, shear)
+        self.shear = shear
+
+    def _params(self, h, w):
+        angle = random.uniform(*self.degrees)
+        tx = ty = 0.0
+        if self.translate is not None:
+            tx = round(random.uniform(-self.translate[0] * w, self.translate[0] * w))
+            ty = round(random.uniform(-self.translate[1] * h, self.translate[1] * h))
+        sc = random.uniform(*self.scale) if self.scale is not None else 1.0
+        sh = (0.0, 0.0)
+        if self.shear is not None:
+            sh = (random.uniform(self.shear[0], self.shear[1]),
+                  random.uniform(self.shear[2], self.shear[3]) if len(self.shear) == 4 else 0.0)
+        return angle, (tx, ty), sc, sh
+
+    def _apply_image(self, img):
+        h, w = _hw(img)
+        angle, tr, sc, sh = self._params(h, w)
+        return affine(img, angle, tr, sc, sh, self.interpolation, self.fill, self.center)
+
+
+class RandomPerspective(BaseTransform):
+    """Reference `transforms.py:RandomPerspective`."""
+
+    def __init__(self, prob=0.5, distortion_scale=0.5, interpolation="nearest", fill=0, keys=None):
+        super().__init__(keys)
+        self.prob, self.d, self.interpolation, self.fill = prob, distortion_scale, interpolation, fill
+
+    def _apply_image(self, img):
+        if random.random() >= self.prob:
+            return img
+        h, w = _hw(img)
+        dh, dw = int(self.d * h / 2), int(self.d * w / 2)
+        tl = (random.randint(0, dw), random.randint(0, dh))
+        tr = (w - 1 - random.randint(0, dw), random.randint(0, dh))
+        br = (w - 1 - random.randint(0, dw), h - 1 - random.randint(0, dh))
+        bl = (random.randint(0, dw), h - 1 - random.randint(0, dh))
+        start = [(0, 0), (w - 1, 0), (w - 1, h - 1), (0, h - 1)]
+        return perspective(img, start, [tl, tr, br, bl], self.interpolation, self.fill)

@@ -1,7 +1,11 @@
 """``paddle.distributed.auto_parallel`` (reference `distributed/auto_parallel/`): semi-automatic
 parallelism — ProcessMesh, ``shard_tensor`` / ``shard_op`` annotations, Strategy, Engine.
 
-MI355X design: annotations become ``torch.distributed.tensor`` DTensors on a DeviceMesh (RCCL
+Static programs: ``complete`` / ``partition`` (`partitioner.py`) propagate the annotations through a
+static Program and build each rank's program (local parameter shards, RCCL all-gather / all-reduce
+/ slice inserted where layouts change) — the reference's Completer / Partitioner / Resharder.
+
+MI355X design (dynamic mode): annotations become ``torch.distributed.tensor`` DTensors on a DeviceMesh (RCCL
 collectives over xGMI inserted by the DTensor propagation rules), instead of the reference's
 static-graph completion / partition / reshard passes. ``shard_spec`` follows Paddle: one entry per
 tensor dim naming the mesh dim it is split over (or None = replicated). Engine drives training /
@@ -15,9 +19,26 @@ import torch
 import torch.distributed as dist
 
 __all__ = ["ProcessMesh", "shard_tensor", "shard_op", "recompute", "fetch", "Strategy", "Engine",
-           "get_current_process_mesh", "reshard"]
+           "get_current_process_mesh", "reshard", "complete", "partition", "Completer", "Partitioner"]
 
 _CUR = {"mesh": None}
+
+
+def complete(program, process_mesh, annotations=None):
+    from .partitioner import complete as _c
+    return _c(program, process_mesh, annotations)
+
+
+def partition(program, process_mesh, rank=None, annotations=None, fetch_list=()):
+    from .partitioner import partition as _p
+    return _p(program, process_mesh, rank, annotations, fetch_list)
+
+
+def __getattr__(name):
+    if name in ("Completer", "Partitioner", "DistAttr"):
+        from . import partitioner
+        return getattr(partitioner, name)
+    raise AttributeError(name)
 
 
 class ProcessMesh:
@@ -107,7 +128,11 @@ def shard_tensor(x, process_mesh=None, shard_spec=None):
     assert mesh is not None, "shard_tensor needs a process_mesh (argument or `with ProcessMesh`)"
     if shard_spec is not None:
         assert len(shard_spec) == x.dim(), "shard_spec needs one entry per tensor dim"
-    if not _distributed():
+    from ...static.framework import Variable
+    from ... import in_dynamic_mode
+    if not _distributed() or isinstance(x, Variable) or not in_dynamic_mode():
+        # single process, or a static program: an annotation for the static completion /
+        # partition passes (partitioner.py)
         x.process_mesh, x.shard_spec = mesh, shard_spec
         return x
     from torch.distributed.tensor import distribute_tensor

@@ -29,7 +29,11 @@ def _fire(p):
 
 
 _PARAM_EPOCH = [0]
-TRANSPOSED_MIN_ROWS = 1024  # below this the GEMM is too small for the layout to matter
+TRANSPOSED_MIN_ROWS = 1024  # training: below this the per-step re-transpose is not repaid
+# inference weights are transposed once (cached until they change), and hipBLASLt's TN kernels
+# beat NN down to small M too: 128-row BERT-Large projections 13.4 -> 10.8 us (N=K=1024),
+# 19.5 -> 11.9 us (K=4096) — `tools/bench_small_m_linear.py`, `profiles/small_m_linear_r2.txt`
+INFER_TRANSPOSED_MIN_ROWS = 16
 
 
 def bump_param_epoch():
@@ -56,9 +60,10 @@ def transposed(w):
     return buf
 
 
-def _use_transposed(x2, w):
+def _use_transposed(x2, w, min_rows=None):
+    min_rows = TRANSPOSED_MIN_ROWS if min_rows is None else min_rows
     return (x2.is_cuda and w.dim() == 2 and w.dtype in (torch.bfloat16, torch.float16)
-            and x2.dtype == w.dtype and x2.shape[0] >= TRANSPOSED_MIN_ROWS and w.is_contiguous()
+            and x2.dtype == w.dtype and x2.shape[0] >= min_rows and w.is_contiguous()
             and not getattr(w, "_piamd_no_t", False))
 
 
@@ -123,7 +128,8 @@ def linear_bias_act(x, weight, bias, act="gelu", weight_out_in=False):
     x2 = x.reshape(-1, shp[-1])
     n_out = weight.shape[0] if weight_out_in else weight.shape[1]
     if (act in _EPILOGUE_ACTS and bias is not None and bias.dtype == x2.dtype
-            and not torch.is_grad_enabled() and _use_transposed(x2, weight)):
+            and not torch.is_grad_enabled()
+            and _use_transposed(x2, weight, INFER_TRANSPOSED_MIN_ROWS)):
         wk = weight.t() if weight_out_in else transposed(weight).t()
         y = torch._addmm_activation(bias, x2, wk, use_gelu=_EPILOGUE_ACTS[act])
         return y.view(*shp[:-1], n_out)
@@ -155,7 +161,7 @@ def linear(x, weight, bias=None):
     # inference weights: same K-contiguous cached copy + bias-in-epilogue GEMM as training
     shp = x.shape
     x2 = x.reshape(-1, shp[-1])
-    if not _use_transposed(x2, weight):
+    if not _use_transposed(x2, weight, INFER_TRANSPOSED_MIN_ROWS):
         if bias is not None and bias.dtype == x2.dtype and x2.dim() == 2:
             return torch.addmm(bias, x2, weight).view(*shp[:-1], weight.shape[1])
         y = torch.matmul(x, weight)

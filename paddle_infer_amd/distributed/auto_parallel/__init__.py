@@ -250,6 +250,80 @@ class Engine:
         self.hybrid_configs = _pl.apply_to_strategy(best, self.strategy, int(global_batch))
         return best
 
+    # ---- static auto-parallel path (reference Engine.prepare -> completion / partition) ----------
+    def prepare(self, inputs_spec=None, labels_spec=None, inputs=None, labels=None,
+                main_program=None, startup_program=None, mode="train", process_mesh=None):
+        """Trace the model (and loss) into a static Program from ``inputs_spec`` / ``labels_spec``
+        (InputSpec lists), complete the ``shard_tensor`` annotations made while tracing, partition
+        the program for this rank and — for ``mode="train"`` — append backward + optimizer ops to
+        the partitioned program. ``fit`` / ``evaluate`` / ``predict`` then run the per-rank
+        program in a private Scope (feeds are global batches; split feeds are sliced locally)."""
+        import torch.distributed as dist
+        from ... import static, enable_static, disable_static, in_dynamic_mode
+        from .partitioner import complete, Partitioner
+        was_dyn = in_dynamic_mode()
+        enable_static()
+        try:
+            main, startup = static.Program(), static.Program()
+            with static.program_guard(main, startup):
+                xs = [static.data(s.name or f"input_{i}", list(s.shape), s.dtype)
+                      for i, s in enumerate(inputs_spec or [])]
+                ys = [static.data(s.name or f"label_{i}", list(s.shape), s.dtype)
+                      for i, s in enumerate(labels_spec or [])]
+                out = self.model(*xs)
+                loss = self.loss(out, *ys) if (self.loss is not None and ys) else None
+            mesh = process_mesh or get_current_process_mesh() or self._annotation_mesh(main)
+            rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+            if mesh is None:
+                mesh = ProcessMesh([rank])
+            c = complete(main, mesh)
+            fetch = [out] + ([loss] if loss is not None else [])
+            local = Partitioner(c).partition(rank, fetch_list=fetch)
+            lvars = local.global_block().vars
+            lloss = lvars[loss.var_name] if loss is not None else None
+            if mode == "train" and lloss is not None and self.optimizer is not None:
+                with static.program_guard(local, static.Program()):
+                    self._static_opt().minimize(lloss)
+            self._static = {"program": local, "inputs": [x.var_name for x in xs],
+                            "labels": [y.var_name for y in ys], "out": out.var_name,
+                            "loss": loss.var_name if loss is not None else None,
+                            "exe": static.Executor("cuda" if torch.cuda.is_available() else "cpu"),
+                            "scope": static.Scope(), "mode": mode}
+            return local
+        finally:
+            if was_dyn:
+                disable_static()
+
+    @staticmethod
+    def _annotation_mesh(program):
+        for t in list(program.params.values()) + list(program.global_block().vars.values()):
+            pm = getattr(t, "process_mesh", None)
+            if pm is not None:
+                return pm
+        return None
+
+    def _static_opt(self):
+        """A static-mode optimizer of the same kind / learning rate as ``self.optimizer``."""
+        from ... import optimizer as O
+        opt = self.optimizer
+        lr = opt.get_lr() if hasattr(opt, "get_lr") else getattr(opt, "_learning_rate", 0.001)
+        cls = getattr(O, type(opt).__name__, O.SGD)
+        try:
+            return cls(learning_rate=lr)
+        except TypeError:
+            return O.SGD(learning_rate=lr)
+
+    def _run_static(self, batch, fetch_loss=True):
+        from ... import static
+        st = self._static
+        ins, lab = self._split(batch) if st["labels"] else (tuple(batch) if isinstance(batch, (list, tuple)) else (batch,), None)
+        feed = dict(zip(st["inputs"], [i.detach().cpu().numpy() if isinstance(i, torch.Tensor) else i for i in ins]))
+        if st["labels"] and lab is not None:
+            feed[st["labels"][0]] = lab.detach().cpu().numpy() if isinstance(lab, torch.Tensor) else lab
+        fetch = [st["loss"]] if fetch_loss and st["loss"] else [st["out"]]
+        with static.scope_guard(st["scope"]):
+            return st["exe"].run(st["program"], feed=feed, fetch_list=fetch)[0]
+
     def _ctx(self):
         if self.strategy.amp.enable:
             dev = "cuda" if torch.cuda.is_available() else "cpu"
@@ -271,6 +345,13 @@ class Engine:
             steps_per_epoch=None, log_freq=10, save_dir=None, save_freq=1, valid_sample_split=None,
             valid_freq=1, valid_steps=None, collate_fn=None, callbacks=None, verbose=2,
             nvprof_range=[-1, -1]):
+        if getattr(self, "_static", None) is not None:  # prepared: per-rank static program
+            for _ in range(epochs):
+                for i, batch in enumerate(self._batches(train_data, batch_size)):
+                    if steps_per_epoch is not None and i >= steps_per_epoch:
+                        break
+                    self.history["loss"].append(float(self._run_static(batch)))
+            return self.history
         self.model.train()
         k = max(1, int(self.strategy.gradient_merge.k_steps)) if self.strategy.gradient_merge.enable else 1
         step = 0

@@ -156,3 +156,53 @@ def test_partitioned_training_matches_serial(mesh_shape, specs):
     res = run_distributed(_train_worker, int(np.prod(mesh_shape)), mesh_shape, specs)
     for r, losses in res.items():
         np.testing.assert_allclose(losses, ref, rtol=2e-4, atol=1e-6)
+
+
+def _engine_losses(rank=None, steps=4):
+    """Engine.prepare (static trace + completion + partition + backward) then Engine.fit, on an MLP
+    whose forward annotates column / row-parallel weights with shard_tensor."""
+    import paddle_infer_amd.nn as nn
+    import paddle_infer_amd.nn.functional as F
+    from paddle_infer_amd.static import InputSpec
+    torch.manual_seed(5)
+    mesh = auto.ProcessMesh([0, 1], ["mp"])
+
+    class MLP(nn.Layer):
+        def __init__(self):
+            super().__init__()
+            self.l1, self.l2 = nn.Linear(8, 32), nn.Linear(32, 4)
+
+        def forward(self, x):
+            if rank is not None:  # the single-process reference runs the unannotated model
+                auto.shard_tensor(self.l1.weight, mesh, [None, "mp"])
+                auto.shard_tensor(self.l1.bias, mesh, ["mp"])
+                auto.shard_tensor(self.l2.weight, mesh, ["mp", None])
+            return self.l2(F.gelu(self.l1(x)))
+
+    model = MLP()
+    opt = paddle.optimizer.SGD(learning_rate=0.2, parameters=model.parameters())
+    eng = auto.Engine(model, paddle.nn.MSELoss(), opt)
+    eng.prepare([InputSpec([16, 8], "float32", "x")], [InputSpec([16, 4], "float32", "y")],
+                mode="train", process_mesh=mesh if rank is not None else auto.ProcessMesh([0], ["mp"]))
+    r = np.random.RandomState(7)
+    batch = (torch.as_tensor(r.randn(16, 8).astype("float32")), torch.as_tensor(r.randn(16, 4).astype("float32")))
+    data = [batch] * steps  # one batch repeated: the loss must fall step by step
+    hist = eng.fit(iter(data), epochs=1)
+    kinds = [op.type for op in eng._static["program"].global_block().ops]
+    return hist["loss"], kinds
+
+
+def _engine_worker(rank, world):
+    return _engine_losses(rank)
+
+
+def test_engine_prepare_fit_partitioned_matches_single_process():
+    ref, kinds1 = _engine_losses()
+    assert "c_allreduce_sum" not in kinds1
+    res = run_distributed(_engine_worker, 2)
+    for r in range(2):
+        losses, kinds = res[r]
+        np.testing.assert_allclose(losses, ref, rtol=2e-4, atol=1e-6)
+        assert "c_identity" in kinds  # column-parallel input: all-reduce of its gradient
+        assert "sgd" in kinds
+    assert ref[-1] < ref[0]

@@ -42,11 +42,13 @@ def main():
     ap.add_argument("--model", default="gpt3-1.3b")
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--num-layers", type=int, default=0, help="override the model's layer count (rehearsals)")
-    ap.add_argument("--micro-batch", type=int, default=64,
-                    help="sequences per data-parallel rank (64 x 1024 tokens: ~140 GB of the "
+    ap.add_argument("--micro-batch", type=int, default=96,
+                    help="sequences per data-parallel rank (96 x 1024 tokens: ~177 GB of the "
                          "288 GB HBM3E; amortises the optimizer step and the gradient collectives: "
-                         "124.3k / 125.5k / 126.3k tok/s at 32 / 48 / 64 on one MI355X; at 8 GPUs "
-                         "the global batch is 512 x 1024 = 0.5M tokens, GPT-3 1.3B used 1M)")
+                         "128.9k / 130.1k / 130.5k tok/s at 64 / 96 / 128 on one MI355X, "
+                         "profiles/bench_mb_sweep_r2.txt — 96 keeps >100 GB free for the multi-GPU "
+                         "collective buffers; at 8 GPUs the global batch is 768 x 1024 = 0.79M tokens, "
+                         "GPT-3 1.3B used 1M)")
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--pp", type=int, default=1)
     ap.add_argument("--vpp", type=int, default=1, help="virtual pipeline chunks per rank (interleaved 1F1B)")

@@ -56,7 +56,7 @@ __global__ __launch_bounds__(256) void bias_act_fwd_kernel(const bf16_t* __restr
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long long i = min(i0 + u * stride, n8 - 1);
-      r[u] = reinterpret_cast<const u16x8*>(x)[i];
+      r[u] = __builtin_nontemporal_load(&reinterpret_cast<const u16x8*>(x)[i]);
       if (bias) b[u] = reinterpret_cast<const u16x8*>(bias)[c];
       c += step1;
       c -= c >= nb8 ? nb8 : 0;
@@ -76,7 +76,7 @@ __global__ __launch_bounds__(256) void bias_act_fwd_kernel(const bf16_t* __restr
         o[j] = f2h<F16>(act_f<ACT>(v));
       }
       if (pre) reinterpret_cast<u16x8*>(pre)[i] = pr;
-      reinterpret_cast<u16x8*>(y)[i] = o;
+      __builtin_nontemporal_store(o, &reinterpret_cast<u16x8*>(y)[i]);  // streamed: no L2 reuse
     }
   }
 }
@@ -101,8 +101,10 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const bf16_t* __restr
     for (int u = 0; u < U; ++u) {
       const int r = min(r0 + u * (int)gridDim.x, rows - 1);
       const size_t idx = ((size_t)r * N >> 3) + c8;
-      d[u] = reinterpret_cast<const u16x8*>(dy)[idx];
-      hv[u] = reinterpret_cast<const u16x8*>(h)[idx];
+      // nontemporal (streaming) loads / stores: the [tokens x 4h] tensors are read once and never
+      // hit in L2 — 5.19 -> 5.50 TB/s backward, 4.28 -> 4.57 forward (profiles/nt_stream_r2.txt)
+      d[u] = __builtin_nontemporal_load(&reinterpret_cast<const u16x8*>(dy)[idx]);
+      hv[u] = __builtin_nontemporal_load(&reinterpret_cast<const u16x8*>(h)[idx]);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -118,7 +120,7 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const bf16_t* __restr
         o[j] = f2h<F16>(g);
         acc[j] += g;
       }
-      reinterpret_cast<u16x8*>(dx)[idx] = o;
+      __builtin_nontemporal_store(o, &reinterpret_cast<u16x8*>(dx)[idx]);
     }
   }
   if (part) {

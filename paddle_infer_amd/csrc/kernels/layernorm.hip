@@ -47,7 +47,7 @@ struct IO16 {
     u16x8 r;
 #pragma unroll
     for (int j = 0; j < 8; ++j) r[j] = cvt(v[j]);
-    *reinterpret_cast<u16x8*>(p) = r;
+    __builtin_nontemporal_store(r, reinterpret_cast<u16x8*>(p));  // streamed rows: no L2 reuse
   }
   static __device__ __forceinline__ float load1(const T* p) { return cv(*p); }
   static __device__ __forceinline__ void store1(T* p, float v) { *p = cvt(v); }

@@ -60,7 +60,8 @@ def _mapping_from_spec(mesh, spec, ndim):
 _UNARY = {"relu", "gelu", "sigmoid", "tanh", "silu", "exp", "log", "sqrt", "rsqrt", "scale", "cast",
           "dropout", "assign", "clip", "leaky_relu", "swish", "hard_swish", "abs", "square", "erf"}
 _BINARY = {"elementwise_add", "elementwise_sub", "elementwise_mul", "elementwise_div",
-           "elementwise_pow", "elementwise_max", "elementwise_min", "where", "masked_fill"}
+           "elementwise_pow", "elementwise_max", "elementwise_min", "where", "masked_fill",
+           "fused_bias_act"}  # act(x + bias): broadcast of the bias over x's rows
 
 
 def _dim_arg(op, pos, names=("dim", "axis"), default=None):

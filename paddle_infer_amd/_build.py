@@ -6,6 +6,9 @@
   executor scheduler, data-loader ring) built with g++.
 * ``_lib/libpiamd_alloc.so`` — the auto-growth best-fit device allocator (``csrc/alloc``,
   host-only HIP runtime code, g++ against the HIP headers; plugged into PyTorch's HIP allocator).
+* ``_lib/piamd_agemm.hsaco`` — the hand-scheduled assembly GEMM kernels: ``csrc/asm/gemm_gen.py``
+  emits the gfx950 assembly, clang assembles it and ld.lld links the code object (loaded at run
+  time by ``csrc/kernels/agemm_host.hip`` through ``hipModuleLoad``).
 * ``_lib/libpiamd_capi.so`` — the C inference API (``csrc/capi``: reference ``capi_exp``
   ``pd_inference_api.h``), g++ against the embedded Python runtime.
 
@@ -35,6 +38,9 @@ ALLOC_LIB = os.path.join(LIBDIR, "libpiamd_alloc.so")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("PIAMD_ARCH", "gfx950")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+ASMDIR = os.path.join(ROOT, "csrc", "asm")
+AGEMM_HSACO = os.path.join(LIBDIR, "piamd_agemm.hsaco")
+LLVM_BIN = os.path.join(ROCM, "lib", "llvm", "bin")
 
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
              "-ffp-contract=fast", "-Wno-unused-result"]
@@ -90,8 +96,30 @@ def _build_lib(srcs, out, compiler, flags, link_flags, hdr_time, verbose, jobs) 
     return bool(need_link)
 
 
+def build_asm(verbose: bool = True) -> bool:
+    """Generate, assemble and link the assembly GEMM code object (rebuilt when the generator is
+    newer than the code object)."""
+    gen = os.path.join(ASMDIR, "gemm_gen.py")
+    if os.path.exists(AGEMM_HSACO) and os.path.getmtime(AGEMM_HSACO) >= os.path.getmtime(gen):
+        return False
+    os.makedirs(OBJDIR, exist_ok=True)
+    src = os.path.join(OBJDIR, "agemm.s")
+    obj = os.path.join(OBJDIR, "agemm.o")
+    _compile([sys.executable, gen, src], gen)
+    _compile([os.path.join(LLVM_BIN, "clang"), "-x", "assembler", "-target", "amdgcn-amd-amdhsa",
+              f"-mcpu={ARCH}", "-c", src, "-o", obj], src)
+    tmp = AGEMM_HSACO + ".tmp"
+    _compile([os.path.join(LLVM_BIN, "ld.lld"), "-shared", obj, "-o", tmp], obj)
+    os.replace(tmp, AGEMM_HSACO)
+    if verbose:
+        print(f"[piamd build] assembled {AGEMM_HSACO}", flush=True)
+    return True
+
+
 def build(verbose: bool = True, jobs: int | None = None) -> None:
     jobs = jobs or min(8, os.cpu_count() or 4)
+    os.makedirs(LIBDIR, exist_ok=True)
+    build_asm(verbose)
     ksrcs = sorted(glob.glob(os.path.join(KDIR, "*.hip")))
     if ksrcs:
         _build_lib(ksrcs, KERNEL_LIB, HIPCC, HIP_FLAGS, [f"--offload-arch={ARCH}"],

@@ -1,0 +1,752 @@
+"""Generator of the hand-scheduled gfx950 (CDNA4) bf16 GEMM kernels (``agemm``).
+
+Why assembly: the GEMMs are ~75 % of a GPT training step. The structure that reaches the MFMA
+rate on gfx950 — ONE wave per SIMD holding a 128×128 f32 accumulator tile in the 256 AGPRs, all
+64-deep operand fragments of a K-block (128 VGPRs) in registers, LDS filled by LDS-DMA
+(`buffer_load_dwordx4 … lds`) two blocks ahead into the stage that is being consumed — cannot be
+expressed through hipcc: with 512 live registers per lane hipcc either spills or re-orders the
+MFMA/DMA/LDS-read interleave and inserts drains (the round-2 HIP kernel `gemm_pipe.hip` reached
+0.77-0.87× hipBLASLt, `profiles/gemm_pipe_r2.txt`). Here every instruction is placed by this
+generator and every wait is counted by hand.
+
+Kernel (one per (A layout, B layout, epilogue) variant):
+
+* C[M,N] = A·B, bf16 operands, f32 accumulation. A is KC ("K-contiguous", stored [M][K]) or MC
+  (stored [K][M]); B is KC (stored [N][K]) or MC (stored [K][N]). Forward and data-gradient
+  products of a linear are KC×KC; the weight gradient xᵀ·dy is MC×MC — no transpose kernels.
+* workgroup = 4 waves (one per SIMD), 256×256 output tile, wave (wr, wc) owns 128×128 =
+  8×8 blocks of `v_mfma_f32_16x16x32_bf16` (operands swapped, Cᵀ-blocks = B·A, so a lane owns
+  one output row and 4 consecutive columns: 8-byte bf16 / 16-byte f32 stores).
+* K-block = 64. LDS = 2 stages × (A 32 KiB + B 32 KiB) = 128 KiB. Block t lives in stage t%2.
+  Iteration t: phase A runs the 64 MFMAs of k-half 0 (fragments X, read during the previous
+  iteration) while reading k-half 1 (fragments Y); a barrier then certifies every wave has ALL of
+  block t in registers, so phase B issues the 16 LDS-DMAs of block t+2 into the SAME stage while
+  running the 64 MFMAs of k-half 1, waits (counted `vmcnt(16)`) for block t+1, barriers, and reads
+  its k-half 0 into X. Two barriers per 128 MFMAs; DMA latency budget ≈1.5 iterations.
+* LDS images: KC operand = [256 rows][128 B], 16-B chunk c of row r at c ^ ((r>>1)&7)
+  (conflict-free `ds_read_b128` for the MFMA lane groups); MC operand = 4 column groups of
+  64 × [64 k][128 B] with the 32-B slot XOR ((k>>1)&1 | ((k>>3)&1)<<1) — conflict-free
+  `ds_read_b64_tr_b16` (hardware transpose). LDS-DMA writes are lane-linear, so the swizzle sits
+  on the per-lane GLOBAL source address; every DMA moves whole 128-B lines.
+* Work mapping: bijective XCD remap (blocks b, b+8, … share an XCD and take consecutive tiles),
+  group-M tile order (GM m-tiles × all n-tiles), optional split-K (f32 partial planes, reduced by
+  `splitk_reduce` in a fixed order).
+* Epilogues: bf16 store, f32 store (split-K partials), f32 accumulate (main_grad += ),
+  bias + activation with the pre-activation stored as aux (FFN1 forward), C = acc ⊙ act'(aux)
+  (FFN2 data gradient fused with the GELU backward). Rows beyond M fall outside the store
+  descriptor's range (dropped by the buffer unit); columns beyond N are EXEC-masked.
+
+Every global access is a `buffer_*` op through a descriptor whose range is the operand's extent,
+and every address is clamped in range by construction.
+
+Parity: reference `paddle/phi/kernels/funcs/blas/blas_impl.cu.h` (cublas GEMM behind matmul /
+linear and their gradients), `paddle/fluid/operators/fused/fused_gemm_epilogue_op.cu:30`
+(cublasLt bias / bias+GELU(aux) / dGELU epilogues).
+
+``python gemm_gen.py OUT.s`` writes every variant; `_build.py` assembles and links it into
+``_lib/piamd_agemm.hsaco`` (loaded by ``csrc/kernels/agemm_host.hip``).
+"""
+from __future__ import annotations
+
+import sys
+
+TILE, BK, NW = 256, 64, 4
+LDS_BYTES = 2 * 2 * 256 * BK * 2  # 2 stages × (A + B) × 256 × 64 × bf16 = 128 KiB
+STAGE_BYTES = 65536
+OP_BYTES = 32768
+
+# ---- kernel-argument block (byte offsets; mirrored by struct AgemmArgs in agemm_host.hip) ------
+ARGS = [
+    ("a", 0, 8), ("b", 8, 8), ("a_bytes", 16, 8), ("b_bytes", 24, 8),
+    ("lda_b", 32, 4), ("ldb_b", 36, 4), ("M", 40, 4), ("N", 44, 4),
+    ("nk", 48, 4), ("tiles_n", 52, 4), ("nwg", 56, 4), ("ksplit", 60, 4),
+    ("tiles_m", 64, 4), ("ntiles", 68, 4), ("rcp_ntiles", 72, 4), ("per_group", 76, 4),
+    ("rcp_per_group", 80, 4), ("gm", 84, 4), ("act", 88, 4), ("pad0", 92, 4),
+    # epilogue block (loaded after the main loop)
+    ("c", 96, 8), ("c_bytes", 104, 8), ("ldc_b", 112, 4), ("ldaux_b", 116, 4),
+    ("c_part", 120, 8), ("aux", 128, 8), ("aux_bytes", 136, 8), ("bias", 144, 8),
+]
+ARGS_SIZE = 152
+
+# ---- SGPR map ------------------------------------------------------------------------------------
+S_KARG = 0        # s[0:1]
+S_WG = 2          # workgroup id
+S_ARG = 4         # s[4:27]: the first 96 argument bytes
+S_A, S_B, S_ABYTES, S_BBYTES = 4, 6, 8, 10
+S_LDA, S_LDB, S_M, S_N = 12, 13, 14, 15
+S_NK, S_TN, S_NWG, S_KSPLIT = 16, 17, 18, 19
+S_TM, S_NTILES, S_RCPNT, S_PERGRP, S_RCPPG, S_GM, S_ACT = 20, 21, 22, 23, 24, 25, 26
+S_SRDA, S_SRDB = 28, 32            # 4 each
+S_SOFFA, S_SOFFB = 36, 44          # 8 each (MC operands)
+S_REMA, S_REMB = 52, 54            # 64-bit remaining bytes behind the descriptor base
+S_STEPA, S_STEPB = 56, 58          # 64-bit K-block step
+S_LDSA, S_LDSB = 60, 62            # per-stage LDS-DMA base of this wave's pieces (2 each)
+S_LOOP, S_REM = 64, 65
+S_WAVE, S_M0T, S_N0T, S_PART = 66, 67, 68, 69
+S_T = 70                           # temps s70..s79
+S_E = 80                           # epilogue s80..s95
+NSGPR = 96
+
+# ---- VGPR map ------------------------------------------------------------------------------------
+V_TID, V_LANE = 0, 1
+V_DMAA, V_DMAB = 2, 10             # 8 each (KC: one per piece row-group; MC: 2)
+V_RBA, V_RBB = 18, 26              # read bases, 8 each (KC: [stage][h] 4; MC: [stage][bq] 8)
+V_T = 34                           # temps v34..v47
+V_FRAG = 48                        # X: A v48..79, B v80..111; Y: A v112..143, B v144..175
+V_E = V_FRAG                       # epilogue temps reuse the (dead) fragment registers
+ACC_OFF = 224                      # AGPRs follow the VGPRs in the unified file
+NVGPR = ACC_OFF + 256
+
+
+def frag(set_, op, blk):
+    """First VGPR of fragment `blk` of operand `op` (0 = A, 1 = B) in set X (0) / Y (1)."""
+    return V_FRAG + set_ * 64 + op * 32 + blk * 4
+
+
+def acc(mb, nb):
+    return 4 * (mb * 8 + nb)
+
+
+# ---- layout model (shared with tests/test_agemm_layout_cpu.py) ----------------------------------
+def kc_dma(i, w, L):
+    """KC operand, wave w, DMA i (0..7), lane L → (tile row, global 16-B chunk), LDS byte."""
+    row = 32 * i + 8 * w + (L >> 3)
+    g = (L & 7) ^ ((4 * w + (L >> 4)) & 7)
+    lds = (4 * i + w) * 1024 + 16 * L
+    return row, g, lds
+
+
+def kc_read(WO, h, blk, l):
+    """KC fragment read (ds_read_b128): LDS byte of lane l for block blk, k-half h."""
+    r = WO + 16 * blk + (l & 15)
+    c = (4 * h + (l >> 4)) ^ ((l >> 1) & 7)
+    return r * 128 + c * 16
+
+
+def mc_f(k):
+    return ((k >> 1) & 1) | (((k >> 3) & 1) << 1)
+
+
+def mc_dma(i, w, L):
+    """MC operand ([K][cols]), wave w, DMA i, lane L → (k row, first col), LDS byte."""
+    k = 8 * i + (L >> 3)
+    c = L & 7
+    cg = (((c >> 1) ^ mc_f(k)) << 1) | (c & 1)
+    col = 64 * w + 8 * cg
+    lds = w * 8192 + i * 1024 + 16 * L
+    return k, col, lds
+
+
+def mc_read(WO, h, blk, j, l):
+    """MC fragment read (ds_read_b64_tr_b16 #j): LDS byte supplied by lane l."""
+    g, q, p = l >> 4, (l >> 2) & 3, l & 3
+    f = ((q >> 1) & 1) | ((g & 1) << 1)
+    bq = blk & 3
+    base = WO * 128 + (8 * g + q) * 128 + ((bq ^ f) * 32) + 8 * p
+    return base + (blk >> 2) * 8192 + h * 4096 + j * 512
+
+
+# ---- emitter -------------------------------------------------------------------------------------
+class Kernel:
+    def __init__(self, name, a_kc, b_kc, ek):
+        self.name, self.a_kc, self.b_kc, self.ek = name, a_kc, b_kc, ek
+        self.lines = []
+        self.nlab = 0
+
+    def e(self, s):
+        self.lines.append("\t" + s)
+
+    def lab(self, s):
+        self.lines.append(s + ":")
+
+    def newlab(self, tag):
+        self.nlab += 1
+        return f".L{self.name}_{tag}_{self.nlab}"
+
+    # -- scalar helpers ---------------------------------------------------------------------------
+    def udiv(self, q, r, n, d, rcp_s=None, rcp_v=None):
+        """q = n / d, r = n % d (SGPRs; n < 2^24) via an f32 reciprocal (SGPR bits or VGPR) and
+        a ±1 integer fix-up."""
+        v = V_T
+        self.e(f"v_cvt_f32_u32 v{v}, s{n}")
+        if rcp_s is not None:
+            self.e(f"v_mul_f32 v{v}, s{rcp_s}, v{v}")
+        else:
+            self.e(f"v_mul_f32 v{v}, v{rcp_v}, v{v}")
+        self.e(f"v_cvt_u32_f32 v{v}, v{v}")
+        self.e("s_nop 1")
+        self.e(f"v_readfirstlane_b32 s{q}, v{v}")
+        self.e("s_nop 1")
+        t = S_T + 9
+        self.e(f"s_mul_i32 s{t}, s{q}, s{d}")
+        self.e(f"s_sub_i32 s{r}, s{n}, s{t}")
+        l1, l2 = self.newlab("dv"), self.newlab("dv")
+        self.e(f"s_cmp_lt_i32 s{r}, 0")
+        self.e(f"s_cbranch_scc0 {l1}")
+        self.e(f"s_sub_u32 s{q}, s{q}, 1")
+        self.e(f"s_add_u32 s{r}, s{r}, s{d}")
+        self.lab(l1)
+        self.e(f"s_cmp_ge_u32 s{r}, s{d}")
+        self.e(f"s_cbranch_scc0 {l2}")
+        self.e(f"s_add_u32 s{q}, s{q}, 1")
+        self.e(f"s_sub_u32 s{r}, s{r}, s{d}")
+        self.lab(l2)
+
+    def srd_set_records(self, srd, rem):
+        self.e(f"s_cmp_eq_u32 s{rem + 1}, 0")
+        self.e(f"s_cselect_b32 s{srd + 2}, s{rem}, -1")
+
+    def srd_advance(self, srd, rem, step):
+        self.e(f"s_add_u32 s{srd}, s{srd}, s{step}")
+        self.e(f"s_addc_u32 s{srd + 1}, s{srd + 1}, s{step + 1}")
+        self.e(f"s_sub_u32 s{rem}, s{rem}, s{step}")
+        self.e(f"s_subb_u32 s{rem + 1}, s{rem + 1}, s{step + 1}")
+        self.srd_set_records(srd, rem)
+
+    # -- prologue ---------------------------------------------------------------------------------
+    def prologue(self):
+        T = S_T
+        self.e(f"s_load_dwordx16 s[{S_ARG}:{S_ARG + 15}], s[0:1], 0x0")
+        self.e(f"s_load_dwordx8 s[{S_ARG + 16}:{S_ARG + 23}], s[0:1], 0x40")
+        self.e(f"v_and_b32 v{V_LANE}, 63, v{V_TID}")
+        self.e(f"v_lshrrev_b32 v{V_T}, 6, v{V_TID}")
+        self.e("s_nop 1")
+        self.e(f"v_readfirstlane_b32 s{S_WAVE}, v{V_T}")
+        self.e("s_waitcnt lgkmcnt(0)")
+        # XCD remap: u = (x < r ? x*(q+1) : r*(q+1) + (x-r)*q) + b/8, x = b%8, q = nwg/8, r = nwg%8
+        self.e(f"s_and_b32 s{T}, s{S_WG}, 7")
+        self.e(f"s_lshr_b32 s{T + 1}, s{S_NWG}, 3")
+        self.e(f"s_and_b32 s{T + 2}, s{S_NWG}, 7")
+        self.e(f"s_add_u32 s{T + 3}, s{T + 1}, 1")
+        self.e(f"s_mul_i32 s{T + 4}, s{T}, s{T + 3}")
+        self.e(f"s_mul_i32 s{T + 5}, s{T + 2}, s{T + 3}")
+        self.e(f"s_sub_u32 s{T + 6}, s{T}, s{T + 2}")
+        self.e(f"s_mul_i32 s{T + 6}, s{T + 6}, s{T + 1}")
+        self.e(f"s_add_u32 s{T + 5}, s{T + 5}, s{T + 6}")
+        self.e(f"s_cmp_lt_u32 s{T}, s{T + 2}")
+        self.e(f"s_cselect_b32 s{T + 4}, s{T + 4}, s{T + 5}")
+        self.e(f"s_lshr_b32 s{T + 6}, s{S_WG}, 3")
+        self.e(f"s_add_u32 s{T + 4}, s{T + 4}, s{T + 6}")  # u
+        # part = u / ntiles, tile = u % ntiles
+        self.udiv(S_PART, T + 5, T + 4, S_NTILES, rcp_s=S_RCPNT)
+        # group-M: grp = tile / per_group, in_g = tile % per_group
+        self.udiv(T + 6, T + 7, T + 5, S_PERGRP, rcp_s=S_RCPPG)
+        self.e(f"s_mul_i32 s{T + 6}, s{T + 6}, s{S_GM}")          # first_m
+        self.e(f"s_sub_u32 s{T + 8}, s{S_TM}, s{T + 6}")
+        self.e(f"s_min_u32 s{T + 8}, s{T + 8}, s{S_GM}")          # gm
+        self.e(f"v_cvt_f32_u32 v{V_T + 1}, s{T + 8}")
+        self.e(f"v_rcp_f32 v{V_T + 1}, v{V_T + 1}")
+        self.udiv(S_N0T, T + 4, T + 7, T + 8, rcp_v=V_T + 1)      # tn = in_g / gm, tm_off
+        self.e(f"s_add_u32 s{S_M0T}, s{T + 6}, s{T + 4}")
+        self.e(f"s_lshl_b32 s{S_M0T}, s{S_M0T}, 8")              # m0 (rows)
+        self.e(f"s_lshl_b32 s{S_N0T}, s{S_N0T}, 8")              # n0 (cols)
+        # K range of this part: kel = part * nk * 64 elements
+        self.e(f"s_mul_i32 s{T}, s{S_PART}, s{S_NK}")
+        self.e(f"s_lshl_b32 s{T}, s{T}, 6")
+        for op in (0, 1):
+            self.setup_operand(op, T)
+        # zero the accumulators while nothing else is pending
+        self.e("s_nop 0")
+
+    def setup_operand(self, op, T):
+        """Descriptor, K step, DMA voffsets, LDS-DMA bases and read bases of operand op."""
+        kc = self.a_kc if op == 0 else self.b_kc
+        ptr = S_A if op == 0 else S_B
+        tot = S_ABYTES if op == 0 else S_BBYTES
+        ld = S_LDA if op == 0 else S_LDB
+        srd = S_SRDA if op == 0 else S_SRDB
+        rem = S_REMA if op == 0 else S_REMB
+        step = S_STEPA if op == 0 else S_STEPB
+        soff = S_SOFFA if op == 0 else S_SOFFB
+        ldsb = S_LDSA if op == 0 else S_LDSB
+        vd = V_DMAA if op == 0 else V_DMAB
+        rb = V_RBA if op == 0 else V_RBB
+        t0 = S_M0T if op == 0 else S_N0T          # tile origin along this operand's rows/cols
+        lim = S_M if op == 0 else S_N
+        opoff = 0 if op == 0 else OP_BYTES
+        a, b = T + 1, T + 2                       # 64-bit offset accumulator s[a:b]
+        # byte offset of the tile origin + K range start
+        if kc:
+            self.e(f"s_mul_i32 s{a}, s{t0}, s{ld}")
+            self.e(f"s_mul_hi_u32 s{b}, s{t0}, s{ld}")
+            self.e(f"s_lshl_b32 s{T + 3}, s{T}, 1")
+            self.e(f"s_add_u32 s{a}, s{a}, s{T + 3}")
+            self.e(f"s_addc_u32 s{b}, s{b}, 0")
+            self.e(f"s_mov_b32 s{step}, {BK * 2}")
+            self.e(f"s_mov_b32 s{step + 1}, 0")
+        else:
+            self.e(f"s_mul_i32 s{a}, s{T}, s{ld}")
+            self.e(f"s_mul_hi_u32 s{b}, s{T}, s{ld}")
+            self.e(f"s_lshl_b32 s{T + 3}, s{t0}, 1")
+            self.e(f"s_add_u32 s{a}, s{a}, s{T + 3}")
+            self.e(f"s_addc_u32 s{b}, s{b}, 0")
+            self.e(f"s_lshl_b32 s{T + 3}, s{ld}, 6")
+            self.e(f"s_mov_b32 s{step}, s{T + 3}")
+            self.e(f"s_lshr_b32 s{step + 1}, s{ld}, 26")
+        self.e(f"s_add_u32 s{srd}, s{ptr}, s{a}")
+        self.e(f"s_addc_u32 s{srd + 1}, s{ptr + 1}, s{b}")
+        self.e(f"s_and_b32 s{srd + 1}, s{srd + 1}, 0xffff")
+        self.e(f"s_sub_u32 s{rem}, s{tot}, s{a}")
+        self.e(f"s_subb_u32 s{rem + 1}, s{tot + 1}, s{b}")
+        self.srd_set_records(srd, rem)
+        self.e(f"s_mov_b32 s{srd + 3}, 0x20000")
+        # LDS-DMA bases of this wave (stage 0 / 1)
+        per_wave = 1024 if kc else 8192
+        self.e(f"s_mul_i32 s{T + 3}, s{S_WAVE}, {per_wave}")
+        self.e(f"s_add_u32 s{ldsb}, s{T + 3}, {opoff}")
+        self.e(f"s_add_u32 s{ldsb + 1}, s{T + 3}, {opoff + STAGE_BYTES}")
+        V, L = V_T, V_LANE
+        if kc:
+            # g16 = ((L&7) ^ ((4w + (L>>4)) & 7)) * 16 ; rows 32i + 8w + (L>>3) clamped to lim-1-t0
+            self.e(f"s_lshl_b32 s{T + 3}, s{S_WAVE}, 2")
+            self.e(f"v_lshrrev_b32 v{V}, 4, v{L}")
+            self.e(f"v_add_u32 v{V}, s{T + 3}, v{V}")
+            self.e(f"v_and_b32 v{V + 1}, 7, v{L}")
+            self.e(f"v_xor_b32 v{V}, v{V}, v{V + 1}")
+            self.e(f"v_and_b32 v{V}, 7, v{V}")
+            self.e(f"v_lshlrev_b32 v{V}, 4, v{V}")                  # g16
+            self.e(f"v_lshrrev_b32 v{V + 1}, 3, v{L}")
+            self.e(f"s_lshl_b32 s{T + 3}, s{S_WAVE}, 3")
+            self.e(f"v_add_u32 v{V + 1}, s{T + 3}, v{V + 1}")       # 8w + (L>>3)
+            self.e(f"s_sub_u32 s{T + 4}, s{lim}, s{t0}")
+            self.e(f"s_sub_u32 s{T + 4}, s{T + 4}, 1")               # last valid local row
+            for i in range(8):
+                self.e(f"v_add_u32 v{V + 2}, {32 * i}, v{V + 1}")
+                self.e(f"v_min_u32 v{V + 2}, s{T + 4}, v{V + 2}")
+                self.e(f"v_mad_u32_u24 v{vd + i}, v{V + 2}, s{ld}, v{V}")
+            # read bases [stage][h]
+            WO = 128  # rows per wave half; wave offset = 128 * (wr or wc)
+            sel = "wr" if op == 0 else "wc"
+            self.wave_half(T + 3, sel)
+            self.e(f"s_mul_i32 s{T + 3}, s{T + 3}, {WO * 128}")
+            self.e(f"v_and_b32 v{V}, 15, v{L}")
+            self.e(f"v_lshlrev_b32 v{V}, 7, v{V}")                  # (l&15)*128
+            self.e(f"v_add_u32 v{V}, s{T + 3}, v{V}")
+            self.e(f"v_lshrrev_b32 v{V + 1}, 1, v{L}")
+            self.e(f"v_and_b32 v{V + 1}, 7, v{V + 1}")               # (l>>1)&7
+            self.e(f"v_lshrrev_b32 v{V + 2}, 4, v{L}")               # l>>4
+            for h in (0, 1):
+                self.e(f"v_add_u32 v{V + 3}, {4 * h}, v{V + 2}")
+                self.e(f"v_xor_b32 v{V + 3}, v{V + 3}, v{V + 1}")
+                self.e(f"v_lshl_add_u32 v{V + 3}, v{V + 3}, 4, v{V}")
+                for s in (0, 1):
+                    self.e(f"v_add_u32 v{rb + 2 * s + h}, {s * STAGE_BYTES + opoff}, v{V + 3}")
+        else:
+            # DMA: k row (L>>3) (+8i by soffset), chunk c = L&7,
+            # cg = (((c>>1) ^ f) << 1) | (c&1), f = ((L>>4)&1) | ((i&1)<<1); col = 64w + 8cg
+            self.e(f"v_lshrrev_b32 v{V}, 4, v{L}")
+            self.e(f"v_and_b32 v{V}, 1, v{V}")                       # (L>>4)&1
+            self.e(f"v_lshrrev_b32 v{V + 1}, 1, v{L}")
+            self.e(f"v_and_b32 v{V + 1}, 3, v{V + 1}")               # c>>1
+            self.e(f"v_and_b32 v{V + 2}, 1, v{L}")                   # c&1
+            self.e(f"v_lshrrev_b32 v{V + 3}, 3, v{L}")               # k row
+            self.e(f"s_lshl_b32 s{T + 3}, s{S_WAVE}, 6")             # 64w
+            self.e(f"s_sub_u32 s{T + 4}, s{lim}, s{t0}")
+            self.e(f"s_sub_u32 s{T + 4}, s{T + 4}, 8")               # last valid 8-col chunk start
+            for par in (0, 1):
+                self.e(f"v_xor_b32 v{V + 4}, v{V + 1}, v{V}")
+                if par:
+                    self.e(f"v_xor_b32 v{V + 4}, 2, v{V + 4}")
+                self.e(f"v_lshl_or_b32 v{V + 4}, v{V + 4}, 1, v{V + 2}")   # cg
+                self.e(f"v_lshl_add_u32 v{V + 4}, v{V + 4}, 3, s{T + 3}")  # col
+                self.e(f"v_min_u32 v{V + 4}, s{T + 4}, v{V + 4}")
+                self.e(f"v_lshlrev_b32 v{V + 4}, 1, v{V + 4}")
+                self.e(f"v_mad_u32_u24 v{vd + par}, v{V + 3}, s{ld}, v{V + 4}")
+            for i in range(8):
+                self.e(f"s_mul_i32 s{soff + i}, s{ld}, {8 * i}")
+            # read bases [stage][bq]: WO*128 + (8g+q)*128 + ((bq ^ f)*32) + 8p
+            sel = "wr" if op == 0 else "wc"
+            self.wave_half(T + 3, sel)
+            self.e(f"s_mul_i32 s{T + 3}, s{T + 3}, {128 * 128}")
+            self.e(f"v_lshrrev_b32 v{V}, 4, v{L}")                   # g
+            self.e(f"v_lshrrev_b32 v{V + 1}, 2, v{L}")
+            self.e(f"v_and_b32 v{V + 1}, 3, v{V + 1}")               # q
+            self.e(f"v_lshl_add_u32 v{V + 2}, v{V}, 3, v{V + 1}")    # 8g+q
+            self.e(f"v_lshlrev_b32 v{V + 2}, 7, v{V + 2}")
+            self.e(f"v_and_b32 v{V + 3}, 3, v{L}")                   # p
+            self.e(f"v_lshl_add_u32 v{V + 2}, v{V + 3}, 3, v{V + 2}")
+            self.e(f"v_add_u32 v{V + 2}, s{T + 3}, v{V + 2}")
+            self.e(f"v_lshrrev_b32 v{V + 3}, 1, v{V + 1}")           # (q>>1)&1
+            self.e(f"v_and_b32 v{V}, 1, v{V}")
+            self.e(f"v_lshl_or_b32 v{V + 3}, v{V}, 1, v{V + 3}")     # f
+            for bq in range(4):
+                self.e(f"v_xor_b32 v{V + 4}, {bq}, v{V + 3}")
+                self.e(f"v_lshl_add_u32 v{V + 4}, v{V + 4}, 5, v{V + 2}")
+                for s in (0, 1):
+                    self.e(f"v_add_u32 v{rb + 4 * s + bq}, {s * STAGE_BYTES + opoff}, v{V + 4}")
+
+    def wave_half(self, dst, sel):
+        if sel == "wr":
+            self.e(f"s_lshr_b32 s{dst}, s{S_WAVE}, 1")
+        else:
+            self.e(f"s_and_b32 s{dst}, s{S_WAVE}, 1")
+
+    # -- main-loop building blocks ------------------------------------------------------------------
+    def dma_ops(self, stage):
+        """The 16 LDS-DMA issues of one K-block (A then B): list of (m0 line, load line, after)."""
+        ops = []
+        for op in (0, 1):
+            kc = self.a_kc if op == 0 else self.b_kc
+            srd = S_SRDA if op == 0 else S_SRDB
+            ldsb = (S_LDSA if op == 0 else S_LDSB) + stage
+            vd = V_DMAA if op == 0 else V_DMAB
+            soff = S_SOFFA if op == 0 else S_SOFFB
+            for i in range(8):
+                if kc:
+                    m0 = f"s_add_u32 m0, s{ldsb}, {i * 4096}"
+                    ld = f"buffer_load_dwordx4 v{vd + i}, s[{srd}:{srd + 3}], 0 offen lds"
+                else:
+                    m0 = f"s_add_u32 m0, s{ldsb}, {i * 1024}"
+                    ld = f"buffer_load_dwordx4 v{vd + (i & 1)}, s[{srd}:{srd + 3}], s{soff + i} offen lds"
+                ops.append((m0, ld, op if i == 7 else None))
+        return ops
+
+    def advance(self, op):
+        if op == 0:
+            self.srd_advance(S_SRDA, S_REMA, S_STEPA)
+        else:
+            self.srd_advance(S_SRDB, S_REMB, S_STEPB)
+
+    def read_ops(self, set_, stage, h):
+        """LDS reads of the 16 fragments of k-half h of `stage` into set `set_` (B first: the
+        first MFMA row needs all 8 B fragments)."""
+        order = []
+        for k in range(8):
+            order.append((1, k))
+            if k % 2 == 1:
+                order.append((0, k // 2))
+        for k in range(4, 8):
+            order.append((0, k))
+        ops = []
+        for op, blk in order:
+            kc = self.a_kc if op == 0 else self.b_kc
+            rb = V_RBA if op == 0 else V_RBB
+            d = frag(set_, op, blk)
+            if kc:
+                ops.append(f"ds_read_b128 v[{d}:{d + 3}], v{rb + 2 * stage + h} offset:{blk * 2048}")
+            else:
+                base = rb + 4 * stage + (blk & 3)
+                off = (blk >> 2) * 8192 + h * 4096
+                ops.append(f"ds_read_b64_tr_b16 v[{d}:{d + 1}], v{base} offset:{off}")
+                ops.append(f"ds_read_b64_tr_b16 v[{d + 2}:{d + 3}], v{base} offset:{off + 512}")
+        return ops
+
+    def mfma(self, set_, mb, nb):
+        a, b, c = frag(set_, 0, mb), frag(set_, 1, nb), acc(mb, nb)
+        self.e(f"v_mfma_f32_16x16x32_bf16 a[{c}:{c + 3}], v[{b}:{b + 3}], v[{a}:{a + 3}], a[{c}:{c + 3}]")
+
+    def iteration(self, stage, dma, read_next):
+        # phase A: MFMAs on X (k-half 0 of this stage), read Y (k-half 1 of this stage)
+        reads = self.read_ops(1, stage, 1)
+        slots = {}
+        span = 44
+        for r, op in enumerate(reads):
+            slots.setdefault(r * span // len(reads), []).append(op)
+        for k in range(64):
+            self.mfma(0, k // 8, k % 8)
+            for op in slots.get(k, []):
+                self.e(op)
+        self.e("s_waitcnt lgkmcnt(0)")
+        if dma:
+            self.e("s_barrier")
+        # phase B: MFMAs on Y; DMA block t+2 into this stage; then wait for block t+1, read X
+        pre = {}
+        if dma:
+            for n, (m0, ld, adv) in enumerate(self.dma_ops(stage)):
+                pre.setdefault(2 * n, []).append(m0)
+                pre.setdefault(2 * n + 1, []).append(ld)
+                if adv is not None:
+                    pre.setdefault(2 * n + 1, []).append(("adv", adv))
+        nreads = []
+        if read_next:
+            nreads = self.read_ops(0, stage ^ 1, 0)
+        rs = {}
+        for r, op in enumerate(nreads):
+            rs.setdefault(33 + r * 20 // len(nreads), []).append(op)
+        for k in range(64):
+            if k == 32 and read_next:
+                self.e(f"s_waitcnt vmcnt({16 if dma else 0})")
+                self.e("s_barrier")
+            self.mfma(1, k // 8, k % 8)
+            for op in pre.get(k, []):
+                if isinstance(op, tuple):
+                    self.advance(op[1])
+                else:
+                    self.e(op)
+            for op in rs.get(k, []):
+                self.e(op)
+        if read_next:
+            self.e("s_waitcnt lgkmcnt(0)")
+
+    # -- whole kernel ---------------------------------------------------------------------------------
+    def body(self):
+        self.prologue()
+        # blocks 0 and 1 (nk >= 2 by contract) into stages 0 and 1
+        for stage in (0, 1):
+            for m0, ld, adv in self.dma_ops(stage):
+                self.e(m0)
+                self.e("s_nop 0")
+                self.e(ld)
+                if adv is not None:
+                    self.advance(adv)
+        for i in range(256):
+            self.e(f"v_accvgpr_write_b32 a{i}, 0")
+        self.e("s_waitcnt vmcnt(16)")
+        self.e("s_barrier")
+        for op in self.read_ops(0, 0, 0):
+            self.e(op)
+        # npairs = (nk - 2) >> 1, rem = nk - 2 npairs (2 or 3)
+        self.e(f"s_sub_u32 s{S_LOOP}, s{S_NK}, 2")
+        self.e(f"s_lshr_b32 s{S_LOOP}, s{S_LOOP}, 1")
+        self.e(f"s_lshl_b32 s{S_REM}, s{S_LOOP}, 1")
+        self.e(f"s_sub_u32 s{S_REM}, s{S_NK}, s{S_REM}")
+        self.e("s_waitcnt lgkmcnt(0)")
+        lend, lbeg = self.newlab("loopend"), self.newlab("loop")
+        self.e(f"s_cmp_le_i32 s{S_LOOP}, 0")
+        self.e(f"s_cbranch_scc1 {lend}")
+        self.lab(lbeg)
+        self.iteration(0, True, True)
+        self.iteration(1, True, True)
+        self.e(f"s_sub_i32 s{S_LOOP}, s{S_LOOP}, 1")
+        self.e(f"s_cmp_gt_i32 s{S_LOOP}, 0")
+        self.e(f"s_cbranch_scc1 {lbeg}")
+        self.lab(lend)
+        t2, epi = self.newlab("tail2"), self.newlab("epi")
+        self.e(f"s_cmp_eq_u32 s{S_REM}, 3")
+        self.e(f"s_cbranch_scc0 {t2}")
+        self.iteration(0, True, True)
+        self.iteration(1, False, True)
+        self.iteration(0, False, False)
+        self.e(f"s_branch {epi}")
+        self.lab(t2)
+        self.iteration(0, False, True)
+        self.iteration(1, False, False)
+        self.lab(epi)
+        self.epilogue()
+        self.e("s_endpgm")
+
+    # -- epilogues --------------------------------------------------------------------------------
+    def epilogue(self):
+        E, V = S_E, V_E
+        ek = self.ek
+        f32 = ek in ("f32", "f32acc")
+        es = 4 if f32 else 2
+        self.e("s_nop 15")
+        self.e("s_nop 15")
+        self.e(f"s_load_dwordx8 s[{E}:{E + 7}], s[0:1], 0x60")      # c, c_bytes, ldc_b, ldaux_b, c_part
+        if ek in ("bias_act", "dact"):
+            self.e(f"s_load_dwordx4 s[{E + 8}:{E + 11}], s[0:1], 0x80")   # aux, aux_bytes
+            self.e(f"s_load_dwordx2 s[{E + 12}:{E + 13}], s[0:1], 0x90")  # bias
+        self.e("s_waitcnt lgkmcnt(0)")
+        # C descriptor base = c + part*c_part + m0*ldc_b + n0*es
+        T = S_T
+        self.e(f"s_mul_i32 s{T}, s{S_PART}, s{E + 6}")
+        self.e(f"s_mul_hi_u32 s{T + 1}, s{S_PART}, s{E + 6}")
+        self.e(f"s_mul_i32 s{T + 2}, s{S_PART}, s{E + 7}")
+        self.e(f"s_add_u32 s{T + 1}, s{T + 1}, s{T + 2}")
+        self.e(f"s_mul_i32 s{T + 2}, s{S_M0T}, s{E + 4}")
+        self.e(f"s_mul_hi_u32 s{T + 3}, s{S_M0T}, s{E + 4}")
+        self.e(f"s_add_u32 s{T}, s{T}, s{T + 2}")
+        self.e(f"s_addc_u32 s{T + 1}, s{T + 1}, s{T + 3}")
+        self.e(f"s_mul_i32 s{T + 2}, s{S_N0T}, {es}")
+        self.e(f"s_add_u32 s{T}, s{T}, s{T + 2}")
+        self.e(f"s_addc_u32 s{T + 1}, s{T + 1}, 0")
+        srd = S_SRDA  # main-loop descriptors are dead: reuse
+        self.e(f"s_add_u32 s{srd}, s{E}, s{T}")
+        self.e(f"s_addc_u32 s{srd + 1}, s{E + 1}, s{T + 1}")
+        self.e(f"s_and_b32 s{srd + 1}, s{srd + 1}, 0xffff")
+        # records = c_bytes - (part*c_part + tile offset), clamped to [0, 2^32-1]
+        self.e(f"s_sub_u32 s{T + 2}, s{E + 2}, s{T}")
+        self.e(f"s_subb_u32 s{T + 3}, s{E + 3}, s{T + 1}")
+        self.e(f"s_cmp_eq_u32 s{T + 3}, 0")
+        self.e(f"s_cselect_b32 s{srd + 2}, s{T + 2}, -1")
+        self.e(f"s_mov_b32 s{srd + 3}, 0x20000")
+        if ek in ("bias_act", "dact"):
+            # aux descriptor: aux + m0*ldaux_b + n0*2
+            self.e(f"s_mul_i32 s{T}, s{S_M0T}, s{E + 5}")
+            self.e(f"s_mul_hi_u32 s{T + 1}, s{S_M0T}, s{E + 5}")
+            self.e(f"s_lshl_b32 s{T + 2}, s{S_N0T}, 1")
+            self.e(f"s_add_u32 s{T}, s{T}, s{T + 2}")
+            self.e(f"s_addc_u32 s{T + 1}, s{T + 1}, 0")
+            a = S_SRDB
+            self.e(f"s_add_u32 s{a}, s{E + 8}, s{T}")
+            self.e(f"s_addc_u32 s{a + 1}, s{E + 9}, s{T + 1}")
+            self.e(f"s_and_b32 s{a + 1}, s{a + 1}, 0xffff")
+            self.e(f"s_sub_u32 s{T + 2}, s{E + 10}, s{T}")
+            self.e(f"s_subb_u32 s{T + 3}, s{E + 11}, s{T + 1}")
+            self.e(f"s_cmp_eq_u32 s{T + 3}, 0")
+            self.e(f"s_cselect_b32 s{a + 2}, s{T + 2}, -1")
+            self.e(f"s_mov_b32 s{a + 3}, 0x20000")
+        # lane offsets: row (wr*128 + (l&15)), col (wc*128 + 4(l>>4))
+        L = V_LANE
+        self.e(f"s_lshr_b32 s{T + 4}, s{S_WAVE}, 1")
+        self.e(f"s_lshl_b32 s{T + 4}, s{T + 4}, 7")
+        self.e(f"s_and_b32 s{T + 5}, s{S_WAVE}, 1")
+        self.e(f"s_lshl_b32 s{T + 5}, s{T + 5}, 7")
+        self.e(f"v_and_b32 v{V}, 15, v{L}")
+        self.e(f"v_add_u32 v{V}, s{T + 4}, v{V}")                    # local row
+        self.e(f"v_lshrrev_b32 v{V + 1}, 4, v{L}")
+        self.e(f"v_lshl_add_u32 v{V + 1}, v{V + 1}, 2, s{T + 5}")    # local col
+        self.e(f"v_mul_lo_u32 v{V + 2}, v{V}, s{E + 4}")
+        self.e(f"v_mad_u32_u24 v{V + 2}, v{V + 1}, {es}, v{V + 2}")  # C voffset (mb = 0)
+        if ek in ("bias_act", "dact"):
+            self.e(f"v_mul_lo_u32 v{V + 3}, v{V}, s{E + 5}")
+            self.e(f"v_lshl_add_u32 v{V + 3}, v{V + 1}, 1, v{V + 3}")  # aux voffset
+        self.e(f"v_add_u32 v{V + 4}, s{S_N0T}, v{V + 1}")            # global col (nb = 0)
+        # edge tile in N: per-store EXEC masks
+        full = self.newlab("full")
+        done = self.newlab("done")
+        self.e(f"s_add_u32 s{T + 6}, s{S_N0T}, {TILE}")
+        self.e(f"s_cmp_le_u32 s{T + 6}, s{S_N}")
+        self.e(f"s_cbranch_scc1 {full}")
+        self.store_all(masked=True)
+        self.e(f"s_branch {done}")
+        self.lab(full)
+        self.store_all(masked=False)
+        self.lab(done)
+        self.e("s_waitcnt vmcnt(0)")
+
+    def store_all(self, masked):
+        E, V, T = S_E, V_E, S_T
+        ek = self.ek
+        srd = S_SRDA
+        es = 4 if ek in ("f32", "f32acc") else 2
+        W = V + 8          # working registers
+        for mb in range(8):
+            # row voffset for this mb
+            self.e(f"s_mul_i32 s{T + 7}, s{E + 4}, {16 * mb}")
+            self.e(f"v_add_u32 v{V + 5}, s{T + 7}, v{V + 2}")
+            if ek in ("bias_act", "dact"):
+                self.e(f"s_mul_i32 s{T + 8}, s{E + 5}, {16 * mb}")
+                self.e(f"v_add_u32 v{V + 6}, s{T + 8}, v{V + 3}")
+            if ek == "f32acc":
+                for nb in range(8):
+                    d = W + 4 * nb
+                    self.e(f"buffer_load_dwordx4 v[{d}:{d + 3}], v{V + 5}, s[{srd}:{srd + 3}], 0 offen offset:{nb * 64}")
+                self.e("s_waitcnt vmcnt(0)")
+            if ek == "dact":
+                for nb in range(8):
+                    d = W + 32 + 2 * nb
+                    self.e(f"buffer_load_dwordx2 v[{d}:{d + 1}], v{V + 6}, s[{S_SRDB}:{S_SRDB + 3}], 0 offen offset:{nb * 32}")
+                self.e("s_waitcnt vmcnt(0)")
+            for nb in range(8):
+                c = acc(mb, nb)
+                d = W + 4 * nb
+                for j in range(4):
+                    self.e(f"v_accvgpr_read_b32 v{d + j if ek != 'f32acc' else V + 44 + j}, a{c + j}")
+                if ek == "f32acc":
+                    for j in range(4):
+                        self.e(f"v_add_f32 v{d + j}, v{V + 44 + j}, v{d + j}")
+                if masked:
+                    self.e(f"v_add_u32 v{V + 7}, {nb * 16}, v{V + 4}")
+                    self.e(f"v_cmp_gt_u32 vcc, s{S_N}, v{V + 7}")
+                    self.e(f"s_and_saveexec_b64 s[{T + 8}:{T + 9}], vcc")
+                if es == 4:
+                    self.e(f"buffer_store_dwordx4 v[{d}:{d + 3}], v{V + 5}, s[{srd}:{srd + 3}], 0 offen offset:{nb * 64}")
+                else:
+                    if ek == "bias_act":
+                        self.bias_act_vals(d, nb, mb)
+                    elif ek == "dact":
+                        self.dact_vals(d, W + 32 + 2 * nb)
+                    self.e(f"v_cvt_pk_bf16_f32 v{d}, v{d}, v{d + 1}")
+                    self.e(f"v_cvt_pk_bf16_f32 v{d + 1}, v{d + 2}, v{d + 3}")
+                    self.e(f"buffer_store_dwordx2 v[{d}:{d + 1}], v{V + 5}, s[{srd}:{srd + 3}], 0 offen offset:{nb * 32}")
+                if masked:
+                    self.e("s_mov_b64 exec, -1")
+
+    # placeholders for the fused activation epilogues (filled in by later variants)
+    def bias_act_vals(self, d, nb, mb):
+        raise NotImplementedError
+
+    def dact_vals(self, d, auxreg):
+        raise NotImplementedError
+
+    # -- text ----------------------------------------------------------------------------------------
+    def text(self):
+        self.lines = []
+        self.body()
+        n = self.name
+        head = [
+            "\t.text",
+            f"\t.globl {n}",
+            "\t.p2align 8",
+            f"\t.type {n},@function",
+            f"{n}:",
+        ]
+        tail = [
+            f".L{n}_end:",
+            f"\t.size {n}, .L{n}_end-{n}",
+            "\t.rodata",
+            "\t.p2align 6",
+            f"\t.amdhsa_kernel {n}",
+            f"\t\t.amdhsa_group_segment_fixed_size {LDS_BYTES}",
+            "\t\t.amdhsa_private_segment_fixed_size 0",
+            f"\t\t.amdhsa_kernarg_size {ARGS_SIZE}",
+            "\t\t.amdhsa_user_sgpr_count 2",
+            "\t\t.amdhsa_user_sgpr_kernarg_segment_ptr 1",
+            "\t\t.amdhsa_system_sgpr_workgroup_id_x 1",
+            "\t\t.amdhsa_system_vgpr_workitem_id 0",
+            f"\t\t.amdhsa_next_free_vgpr {NVGPR}",
+            f"\t\t.amdhsa_next_free_sgpr {NSGPR}",
+            f"\t\t.amdhsa_accum_offset {ACC_OFF}",
+            "\t\t.amdhsa_reserve_vcc 1",
+            "\t\t.amdhsa_float_denorm_mode_32 3",
+            "\t\t.amdhsa_float_denorm_mode_16_64 3",
+            "\t\t.amdhsa_ieee_mode 0",
+            "\t\t.amdhsa_dx10_clamp 1",
+            "\t.end_amdhsa_kernel",
+            "\t.text",
+        ]
+        return "\n".join(head + self.lines + tail) + "\n"
+
+    def metadata(self):
+        n = self.name
+        return f"""  - .args:
+      - .offset:         0
+        .size:           {ARGS_SIZE}
+        .value_kind:     by_value
+    .group_segment_fixed_size: {LDS_BYTES}
+    .kernarg_segment_align: 8
+    .kernarg_segment_size: {ARGS_SIZE}
+    .max_flat_workgroup_size: 256
+    .name:           {n}
+    .private_segment_fixed_size: 0
+    .sgpr_count:     {NSGPR + 6}
+    .sgpr_spill_count: 0
+    .symbol:         {n}.kd
+    .vgpr_count:     {NVGPR}
+    .agpr_count:     256
+    .vgpr_spill_count: 0
+    .wavefront_size: 64
+"""
+
+
+LAYOUTS = {"nt": (True, True), "tn": (False, False), "nn": (True, False), "tt": (False, True)}
+EPILOGUES = ("bf16", "f32", "f32acc")
+
+
+def variants():
+    for lay in ("nt", "tn", "nn", "tt"):
+        for ek in EPILOGUES:
+            yield f"piamd_agemm_{lay}_{ek}", LAYOUTS[lay][0], LAYOUTS[lay][1], ek
+
+
+def generate() -> str:
+    ks = [Kernel(n, a, b, ek) for n, a, b, ek in variants()]
+    out = ['\t.amdgcn_target "amdgcn-amd-amdhsa--gfx950"', "\t.amdhsa_code_object_version 5"]
+    for k in ks:
+        out.append(k.text())
+    out.append("\t.amdgpu_metadata\n---\namdhsa.kernels:")
+    for k in ks:
+        out.append(k.metadata().rstrip("\n"))
+    out.append("amdhsa.target:   amdgcn-amd-amdhsa--gfx950\namdhsa.version:\n  - 1\n  - 2\n...\n\t.end_amdgpu_metadata")
+    return "\n".join(out) + "\n"
+
+
+if __name__ == "__main__":
+    text = generate()
+    if len(sys.argv) > 1:
+        with open(sys.argv[1], "w") as f:
+            f.write(text)
+    else:
+        sys.stdout.write(text)

@@ -90,6 +90,16 @@ class _Stage3Unit:
             self._bind(self._incoming)
         self._incoming = None
 
+    def discard_prefetch(self):
+        """Drop an outstanding or bound prefetch (its buffer holds the PRE-step shard): called
+        before the shards change so the next forward re-gathers the updated weights."""
+        if self.handle is not None:
+            self.handle.wait()
+            self.handle = None
+        self._incoming = None
+        if self.gathered and not self.persistent:
+            self.release()
+
     def release(self, force=False):
         if self.persistent and not force:
             return
@@ -237,10 +247,14 @@ class GroupShardedStage3(torch.nn.Module):
         return self._order[i] if 0 <= i < len(self._order) else None
 
     def _pre_forward(self, u):
-        if self._recording and u not in self._order:
+        in_backward = torch._C._current_graph_task_id() != -1
+        if self._recording and not in_backward and u not in self._order:
             self._order.append(u)
         u.gather()
-        nxt = self._neighbour(u, 1)
+        # a forward run INSIDE backward is a recompute: the next block's backward already ran,
+        # so prefetching it would leave a gather nobody consumes (and a stale buffer after the
+        # optimizer step) — backward prefetches the previous block instead (_pre_backward)
+        nxt = None if in_backward else self._neighbour(u, 1)
         if nxt is not None:
             nxt.gather_async()
 
@@ -288,6 +302,7 @@ class GroupShardedStage3(torch.nn.Module):
                 u.reduce_grads()
                 u.release()
             u.pending = 0
+            u.discard_prefetch()
 
     def shard_params_and_grads(self):
         return [(u.shard, u.grad) for u in self.units]

@@ -194,6 +194,9 @@ _SIGS["piamd_gemm"] = [c_void_p, c_ll, c_int, c_void_p, c_ll, c_int, c_void_p, c
                        c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_ll, c_void_p]
 # ... same as piamd_gemm + ksplit, ws
 _SIGS["piamd_gemm_pipe"] = _SIGS["piamd_gemm"][:-1] + [c_int, c_void_p, c_void_p]
+_SIGS["piamd_agemm"] = _SIGS["piamd_gemm_pipe"]
+_SIGS["piamd_agemm_load"] = [ctypes.c_char_p]
+_SIGS["piamd_agemm_loaded"] = []
 _SIGS["piamd_transpose_bf16"] = [c_void_p, c_void_p, c_int, c_int, c_void_p]
 _SIGS["piamd_moe_gemm"] = [c_void_p, c_ll, c_void_p, c_ll, c_ll,
                                 c_int, c_void_p, c_int, c_int, c_void_p,

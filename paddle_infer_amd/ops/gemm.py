@@ -63,6 +63,58 @@ def pipe_supported(a, b, trans_a=False, trans_b=False):
 
 NUM_CUS = 256
 
+_AGEMM_READY = [False]
+
+
+def _agemm_load():
+    """Load the assembled code object (`_lib/piamd_agemm.hsaco`) into the HIP runtime once."""
+    if _AGEMM_READY[0]:
+        return
+    import os
+    from .. import _build
+    path = _build.AGEMM_HSACO
+    if not os.path.exists(path):
+        raise RuntimeError(f"assembly GEMM code object missing ({path}); run "
+                           "`python -m paddle_infer_amd._build`")
+    _lib.call("piamd_agemm_load", path.encode())
+    _AGEMM_READY[0] = True
+
+
+def asm_supported(a, b, trans_a=False, trans_b=False, ksplit=1):
+    """Contract of the assembly GEMM (`csrc/asm/gemm_gen.py`): K % (64·ksplit) with ≥ 2 K-blocks
+    per split, N % 4, 8-element aligned leading dims < 2^22, M % 8 when A is stored [K, M],
+    N % 8 when B is stored [K, N], 16-byte aligned operands."""
+    if not (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16):
+        return False
+    M = a.shape[1] if trans_a else a.shape[0]
+    K = a.shape[0] if trans_a else a.shape[1]
+    N = b.shape[0] if trans_b else b.shape[1]
+    return (K % (64 * ksplit) == 0 and K // ksplit >= 128 and N % 4 == 0 and M > 0
+            and (not trans_a or M % 8 == 0) and (trans_b or N % 8 == 0)
+            and a.stride(-1) == 1 and b.stride(-1) == 1
+            and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0
+            and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0
+            and a.stride(0) < (1 << 22) and b.stride(0) < (1 << 22))
+
+
+def asm_gemm(a, b, trans_a=False, trans_b=False, out=None, out_f32=False, accumulate=False,
+             ksplit=1):
+    """C (+)= op(A)·op(B) on the hand-scheduled assembly kernels (plain epilogues)."""
+    _agemm_load()
+    M = a.shape[1] if trans_a else a.shape[0]
+    K = a.shape[0] if trans_a else a.shape[1]
+    N = b.shape[0] if trans_b else b.shape[1]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32 if out_f32 else torch.bfloat16, device=a.device)
+    assert out.shape == (M, N) and out.stride(-1) == 1 and out.data_ptr() % 16 == 0
+    ws = None
+    if ksplit > 1:
+        ws = torch.empty((ksplit, M, N), dtype=torch.float32, device=a.device)
+    _lib.call("piamd_agemm", a.data_ptr(), a.stride(0), int(trans_a), b.data_ptr(), b.stride(0),
+              int(trans_b), out.data_ptr(), out.stride(0), int(out.dtype == torch.float32),
+              int(accumulate), M, N, K, 0, 0, None, None, 0, ksplit, _lib.ptr(ws), _lib.stream())
+    return out
+
 
 def pick_ksplit(M, N, K):
     """Split-K degree for the pipelined kernel: fill the 256 CUs (one 256x256 tile per CU) when

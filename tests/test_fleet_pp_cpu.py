@@ -15,11 +15,11 @@ import torch
 from dist_utils import run_distributed
 
 
-def _cfg(layers=4, tie=True):
+def _cfg(layers=4, tie=True, recompute=False):
     from paddle_infer_amd.models.gpt import gpt_config
     return gpt_config("gpt3-tiny", dtype="float32", hidden_dropout_prob=0.0, num_layers=layers,
                       hidden_size=64, num_heads=4, vocab_size=128, max_position_embeddings=64,
-                      tie_word_embeddings=tie)
+                      tie_word_embeddings=tie, recompute=recompute)
 
 
 def _data(steps=3, B=8, S=16, V=128):
@@ -105,10 +105,10 @@ def test_gpt_pipeline_matches_single(pp, dp, virtual, accumulate, layers, tie, w
 
 
 # ------------------------------------------------------------------------------ ZeRO stage 3
-def _stage3_worker(rank, world, init, tie):
+def _stage3_worker(rank, world, init, tie, recompute=False, layers=2):
     from paddle_infer_amd.distributed.sharding import group_sharded_parallel
     from paddle_infer_amd.models.gpt import GPTForPretraining
-    cfg = _cfg(2, tie)
+    cfg = _cfg(layers, tie, recompute)
     m = GPTForPretraining(cfg)
     m.set_state_dict(init)
     model, opt, _ = group_sharded_parallel(m, _adamw(m.parameters()), "p_g_os")
@@ -150,3 +150,20 @@ def test_stage3_untied_head_and_clip_matches_single(tie):
                                        msg=lambda m, k=k: f"{k}: {m}")
         # released blocks hold no parameter memory between steps
         assert res[r]["resident"] < (total if not tie else total) * 0.5
+
+
+def test_stage3_with_recompute_matches_single():
+    """ZeRO-3 + activation recompute: the recomputed forward inside backward must not prefetch a
+    block whose backward already ran (that gather would survive the optimizer step and feed the
+    NEXT forward pre-step weights). 3 layers so a middle block has both neighbours."""
+    from paddle_infer_amd.models.gpt import GPTForPretraining
+    cfg = _cfg(3, False)
+    torch.manual_seed(0)
+    init = copy.deepcopy(GPTForPretraining(cfg).state_dict())
+    ref_sd, ref_losses = _single(cfg, init)
+    res = run_distributed(_stage3_worker, 2, init, False, True, 3)
+    for r in range(2):
+        assert res[r]["losses"] == pytest.approx(ref_losses, rel=1e-4, abs=1e-5)
+        for k in ref_sd:
+            torch.testing.assert_close(res[r]["sd"][k], ref_sd[k], rtol=2e-3, atol=3e-4,
+                                       msg=lambda m, k=k: f"{k}: {m}")

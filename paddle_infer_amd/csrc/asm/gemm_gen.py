@@ -61,7 +61,7 @@ ARGS = [
     ("lda_b", 32, 4), ("ldb_b", 36, 4), ("M", 40, 4), ("N", 44, 4),
     ("nk", 48, 4), ("tiles_n", 52, 4), ("nwg", 56, 4), ("ksplit", 60, 4),
     ("tiles_m", 64, 4), ("ntiles", 68, 4), ("rcp_ntiles", 72, 4), ("per_group", 76, 4),
-    ("rcp_per_group", 80, 4), ("gm", 84, 4), ("act", 88, 4), ("pad0", 92, 4),
+    ("rcp_per_group", 80, 4), ("gm", 84, 4), ("act", 88, 4), ("grid", 92, 4),
     # epilogue block (loaded after the main loop)
     ("c", 96, 8), ("c_bytes", 104, 8), ("ldc_b", 112, 4), ("ldaux_b", 116, 4),
     ("c_part", 120, 8), ("aux", 128, 8), ("aux_bytes", 136, 8), ("bias", 144, 8),
@@ -75,7 +75,7 @@ S_ARG = 4         # s[4:27]: the first 96 argument bytes
 S_A, S_B, S_ABYTES, S_BBYTES = 4, 6, 8, 10
 S_LDA, S_LDB, S_M, S_N = 12, 13, 14, 15
 S_NK, S_TN, S_NWG, S_KSPLIT = 16, 17, 18, 19
-S_TM, S_NTILES, S_RCPNT, S_PERGRP, S_RCPPG, S_GM, S_ACT = 20, 21, 22, 23, 24, 25, 26
+S_TM, S_NTILES, S_RCPNT, S_PERGRP, S_RCPPG, S_GM, S_ACT, S_GRID = 20, 21, 22, 23, 24, 25, 26, 27
 S_SRDA, S_SRDB = 28, 32            # 4 each
 S_SOFFA, S_SOFFB = 36, 44          # 8 each (MC operands)
 S_REMA, S_REMB = 52, 54            # 64-bit remaining bytes behind the descriptor base
@@ -84,8 +84,13 @@ S_LDSA, S_LDSB = 60, 62            # per-stage LDS-DMA base of this wave's piece
 S_LOOP, S_REM = 64, 65
 S_WAVE, S_M0T, S_N0T, S_PART = 66, 67, 68, 69
 S_T = 70                           # temps s70..s79
-S_E = 80                           # epilogue s80..s95
-NSGPR = 96
+S_E = 80                           # epilogue arguments s80..s93 (loaded once)
+S_U0, S_ROUND = 94, 95             # persistent: first work unit, round counter
+S_CSRD = 96                        # C descriptor (epilogue)
+S_AUXSRD, S_BIASSRD = 40, 44       # fused epilogues (K-contiguous operands: no soffsets in use)
+# next tile (persistent): argument SGPRs the kernel never reads after the prologue
+S_NM0, S_NN0, S_NPART, S_NVALID = 3, 19, 26, 65
+NSGPR = 100
 
 # ---- VGPR map ------------------------------------------------------------------------------------
 V_TID, V_LANE = 0, 1
@@ -93,9 +98,22 @@ V_DMAA, V_DMAB = 2, 10             # 8 each (KC: one per piece row-group; MC: 2)
 V_RBA, V_RBB = 18, 26              # read bases, 8 each (KC: [stage][h] 4; MC: [stage][bq] 8)
 V_T = 34                           # temps v34..v47
 V_FRAG = 48                        # X: A v48..79, B v80..111; Y: A v112..143, B v144..175
-V_E = V_FRAG                       # epilogue temps reuse the (dead) fragment registers
+# epilogue registers (relative to the epilogue base: the dead fragments of both sets for the
+# one-tile kernel, set Y + v176.. for the persistent kernel whose set X already holds the next
+# tile's first fragments): +0..7 offsets, +8..39 values, +40..55 aux / old C, +56..71 bias,
+# +72..76 temps (+76 even: a 64-bit pair), +80..82 constants
+E_BIAS, E_TMP, E_CONST = 56, 72, 80
 ACC_OFF = 224                      # AGPRs follow the VGPRs in the unified file
 NVGPR = ACC_OFF + 256
+
+
+K0, K1 = 0.7978845608028654, 0.044715          # gelu_tanh constants (sqrt(2/pi), 0.044715)
+TWO_LOG2E = 2.0 * 1.4426950408889634
+
+
+def fhex(x):
+    import struct
+    return "0x%08x" % struct.unpack("<I", struct.pack("<f", x))[0]
 
 
 def frag(set_, op, blk):
@@ -148,8 +166,17 @@ def mc_read(WO, h, blk, j, l):
 
 # ---- emitter -------------------------------------------------------------------------------------
 class Kernel:
-    def __init__(self, name, a_kc, b_kc, ek):
-        self.name, self.a_kc, self.b_kc, self.ek = name, a_kc, b_kc, ek
+    def __init__(self, name, a_kc, b_kc, ek, persistent=False):
+        self.name, self.a_kc, self.b_kc = name, a_kc, b_kc
+        self.persistent = persistent
+        self.VE = 112 if persistent else V_FRAG
+        self.VBIAS, self.VTMP, self.VCONST = self.VE + E_BIAS, self.VE + E_TMP, self.VE + E_CONST
+        # ek: plain kinds (bf16 / f32 / f32acc) or fused: bias[gelu|relu] (pre-activation stored
+        # as aux), d{gelu,relu} (C = acc ⊙ act'(aux))
+        fused = {"bias": ("bias_act", 0), "biasgelu": ("bias_act", 1), "biasrelu": ("bias_act", 3),
+                 "dgelu": ("dact", 1), "drelu": ("dact", 3)}
+        self.ek, self.act = fused.get(ek, (ek, 0))
+        assert self.ek not in ("bias_act", "dact") or (a_kc and b_kc)  # descriptor SGPRs 40..47
         self.lines = []
         self.nlab = 0
 
@@ -208,15 +235,20 @@ class Kernel:
         T = S_T
         self.e(f"s_load_dwordx16 s[{S_ARG}:{S_ARG + 15}], s[0:1], 0x0")
         self.e(f"s_load_dwordx8 s[{S_ARG + 16}:{S_ARG + 23}], s[0:1], 0x40")
+        self.e(f"s_load_dwordx8 s[{S_E}:{S_E + 7}], s[0:1], 0x60")       # c, c_bytes, ldc_b, ldaux_b, c_part
+        self.e(f"s_load_dwordx4 s[{S_E + 8}:{S_E + 11}], s[0:1], 0x80")  # aux, aux_bytes
+        self.e(f"s_load_dwordx2 s[{S_E + 12}:{S_E + 13}], s[0:1], 0x90")  # bias
         self.e(f"v_and_b32 v{V_LANE}, 63, v{V_TID}")
         self.e(f"v_lshrrev_b32 v{V_T}, 6, v{V_TID}")
         self.e("s_nop 1")
         self.e(f"v_readfirstlane_b32 s{S_WAVE}, v{V_T}")
         self.e("s_waitcnt lgkmcnt(0)")
-        # XCD remap: u = (x < r ? x*(q+1) : r*(q+1) + (x-r)*q) + b/8, x = b%8, q = nwg/8, r = nwg%8
+        # XCD remap over the launched grid G: u = (x < r ? x*(q+1) : r*(q+1) + (x-r)*q) + b/8,
+        # x = b%8, q = G/8, r = G%8 (bijective; blocks sharing an XCD take consecutive units)
+        G = S_GRID
         self.e(f"s_and_b32 s{T}, s{S_WG}, 7")
-        self.e(f"s_lshr_b32 s{T + 1}, s{S_NWG}, 3")
-        self.e(f"s_and_b32 s{T + 2}, s{S_NWG}, 7")
+        self.e(f"s_lshr_b32 s{T + 1}, s{G}, 3")
+        self.e(f"s_and_b32 s{T + 2}, s{G}, 7")
         self.e(f"s_add_u32 s{T + 3}, s{T + 1}, 1")
         self.e(f"s_mul_i32 s{T + 4}, s{T}, s{T + 3}")
         self.e(f"s_mul_i32 s{T + 5}, s{T + 2}, s{T + 3}")
@@ -226,30 +258,38 @@ class Kernel:
         self.e(f"s_cmp_lt_u32 s{T}, s{T + 2}")
         self.e(f"s_cselect_b32 s{T + 4}, s{T + 4}, s{T + 5}")
         self.e(f"s_lshr_b32 s{T + 6}, s{S_WG}, 3")
-        self.e(f"s_add_u32 s{T + 4}, s{T + 4}, s{T + 6}")  # u
-        # part = u / ntiles, tile = u % ntiles
-        self.udiv(S_PART, T + 5, T + 4, S_NTILES, rcp_s=S_RCPNT)
-        # group-M: grp = tile / per_group, in_g = tile % per_group
+        self.e(f"s_add_u32 s{S_U0}, s{T + 4}, s{T + 6}")
+        self.e(f"s_mov_b32 s{S_ROUND}, 0")
+
+    def tile_coords(self, u, m0, n0, part):
+        """Work unit u (SGPR) → tile origin (rows m0, cols n0) and split-K part: part = u / ntiles,
+        tile in group-M order (GM m-tiles × all n-tiles per group)."""
+        T = S_T
+        self.e(f"s_mov_b32 s{T + 4}, s{u}")
+        self.udiv(part, T + 5, T + 4, S_NTILES, rcp_s=S_RCPNT)
         self.udiv(T + 6, T + 7, T + 5, S_PERGRP, rcp_s=S_RCPPG)
         self.e(f"s_mul_i32 s{T + 6}, s{T + 6}, s{S_GM}")          # first_m
         self.e(f"s_sub_u32 s{T + 8}, s{S_TM}, s{T + 6}")
         self.e(f"s_min_u32 s{T + 8}, s{T + 8}, s{S_GM}")          # gm
         self.e(f"v_cvt_f32_u32 v{V_T + 1}, s{T + 8}")
         self.e(f"v_rcp_f32 v{V_T + 1}, v{V_T + 1}")
-        self.udiv(S_N0T, T + 4, T + 7, T + 8, rcp_v=V_T + 1)      # tn = in_g / gm, tm_off
-        self.e(f"s_add_u32 s{S_M0T}, s{T + 6}, s{T + 4}")
-        self.e(f"s_lshl_b32 s{S_M0T}, s{S_M0T}, 8")              # m0 (rows)
-        self.e(f"s_lshl_b32 s{S_N0T}, s{S_N0T}, 8")              # n0 (cols)
-        # K range of this part: kel = part * nk * 64 elements
-        self.e(f"s_mul_i32 s{T}, s{S_PART}, s{S_NK}")
-        self.e(f"s_lshl_b32 s{T}, s{T}, 6")
-        for op in (0, 1):
-            self.setup_operand(op, T)
-        # zero the accumulators while nothing else is pending
         self.e("s_nop 0")
+        self.udiv(n0, T + 4, T + 7, T + 8, rcp_v=V_T + 1)         # tn = in_g / gm, tm_off
+        self.e(f"s_add_u32 s{m0}, s{T + 6}, s{T + 4}")
+        self.e(f"s_lshl_b32 s{m0}, s{m0}, 8")
+        self.e(f"s_lshl_b32 s{n0}, s{n0}, 8")
 
-    def setup_operand(self, op, T):
-        """Descriptor, K step, DMA voffsets, LDS-DMA bases and read bases of operand op."""
+    def setup_tile(self, m0, n0, part):
+        """Descriptors and DMA offsets of both operands for the tile at (m0, n0, part)."""
+        T = S_T
+        self.e(f"s_mul_i32 s{T}, s{part}, s{S_NK}")
+        self.e(f"s_lshl_b32 s{T}, s{T}, 6")                      # K start (elements)
+        for op in (0, 1):
+            self.setup_operand(op, T, m0 if op == 0 else n0)
+
+    def setup_operand(self, op, T, t0):
+        """Descriptor, K step, DMA voffsets, LDS-DMA bases and read bases of operand op; t0: SGPR
+        with the tile origin along this operand's rows (A: m0, B: n0); s{T}: K start."""
         kc = self.a_kc if op == 0 else self.b_kc
         ptr = S_A if op == 0 else S_B
         tot = S_ABYTES if op == 0 else S_BBYTES
@@ -261,7 +301,6 @@ class Kernel:
         ldsb = S_LDSA if op == 0 else S_LDSB
         vd = V_DMAA if op == 0 else V_DMAB
         rb = V_RBA if op == 0 else V_RBB
-        t0 = S_M0T if op == 0 else S_N0T          # tile origin along this operand's rows/cols
         lim = S_M if op == 0 else S_N
         opoff = 0 if op == 0 else OP_BYTES
         a, b = T + 1, T + 2                       # 64-bit offset accumulator s[a:b]
@@ -431,57 +470,60 @@ class Kernel:
                 ops.append(f"ds_read_b64_tr_b16 v[{d + 2}:{d + 3}], v{base} offset:{off + 512}")
         return ops
 
-    def mfma(self, set_, mb, nb):
+    def mfma(self, set_, mb, nb, zero=False):
         a, b, c = frag(set_, 0, mb), frag(set_, 1, nb), acc(mb, nb)
-        self.e(f"v_mfma_f32_16x16x32_bf16 a[{c}:{c + 3}], v[{b}:{b + 3}], v[{a}:{a + 3}], a[{c}:{c + 3}]")
+        src2 = "0" if zero else f"a[{c}:{c + 3}]"
+        self.e(f"v_mfma_f32_16x16x32_bf16 a[{c}:{c + 3}], v[{b}:{b + 3}], v[{a}:{a + 3}], {src2}")
 
-    def iteration(self, stage, dma, read_next):
-        # phase A: MFMAs on X (k-half 0 of this stage), read Y (k-half 1 of this stage)
-        reads = self.read_ops(1, stage, 1)
-        slots = {}
-        span = 44
-        for r, op in enumerate(reads):
-            slots.setdefault(r * span // len(reads), []).append(op)
-        for k in range(64):
-            self.mfma(0, k // 8, k % 8)
-            for op in slots.get(k, []):
-                self.e(op)
-        self.e("s_waitcnt lgkmcnt(0)")
-        if dma:
-            self.e("s_barrier")
-        # phase B: MFMAs on Y; DMA block t+2 into this stage; then wait for block t+1, read X
-        pre = {}
+    # Schedule of one K-block (128 MFMAs; slot k = after MFMA k):
+    #   slots 0-21   read Y (k-half 1 of this stage)                    [phase A: MFMAs on X]
+    #   slot 24      lgkmcnt(0) + barrier: every wave has this whole block in registers
+    #   slots 26-86  16 LDS-DMAs of block t+2 into THIS stage, one per 4 MFMAs (m0 one slot before)
+    #   slot 92      vmcnt(16) + barrier: block t+1 (issued one iteration earlier) has landed
+    #   slots 93-114 read X (k-half 0 of the other stage)                [phase B: MFMAs on Y]
+    #   end          lgkmcnt(0)
+    # The DMA issue cost (~60 cycles each among MFMAs, MI355X_MICROARCH.md) is spread over 60
+    # MFMAs instead of being bunched.
+    Y_END, BAR1, DMA0, DMA_GAP, BAR2, X0, X_END = 22, 24, 26, 4, 92, 93, 115
+
+    def iteration(self, stage, dma, read_next, first=False):
+        ysl, dsl, xsl = {}, {}, {}
+        yreads = self.read_ops(1, stage, 1)
+        for r, op in enumerate(yreads):
+            ysl.setdefault(r * self.Y_END // len(yreads), []).append(op)
         if dma:
             for n, (m0, ld, adv) in enumerate(self.dma_ops(stage)):
-                pre.setdefault(2 * n, []).append(m0)
-                pre.setdefault(2 * n + 1, []).append(ld)
+                k = self.DMA0 + self.DMA_GAP * n
+                dsl.setdefault(k - 1, []).append(m0)
+                dsl.setdefault(k, []).append(ld)
                 if adv is not None:
-                    pre.setdefault(2 * n + 1, []).append(("adv", adv))
-        nreads = []
+                    dsl.setdefault(k, []).append(("adv", adv))
         if read_next:
-            nreads = self.read_ops(0, stage ^ 1, 0)
-        rs = {}
-        for r, op in enumerate(nreads):
-            rs.setdefault(33 + r * 20 // len(nreads), []).append(op)
-        for k in range(64):
-            if k == 32 and read_next:
+            xreads = self.read_ops(0, stage ^ 1, 0)
+            for r, op in enumerate(xreads):
+                xsl.setdefault(self.X0 + r * (self.X_END - self.X0) // len(xreads), []).append(op)
+        for k in range(128):
+            if k == self.BAR1:
+                self.e("s_waitcnt lgkmcnt(0)")
+                if dma:
+                    self.e("s_barrier")
+            if k == self.BAR2 and read_next:
                 self.e(f"s_waitcnt vmcnt({16 if dma else 0})")
                 self.e("s_barrier")
-            self.mfma(1, k // 8, k % 8)
-            for op in pre.get(k, []):
+            kk = k % 64
+            self.mfma(k // 64, kk // 8, kk % 8, zero=first and k < 64)
+            for op in dsl.get(k, []):
                 if isinstance(op, tuple):
                     self.advance(op[1])
                 else:
                     self.e(op)
-            for op in rs.get(k, []):
+            for op in ysl.get(k, []) + xsl.get(k, []):
                 self.e(op)
         if read_next:
             self.e("s_waitcnt lgkmcnt(0)")
 
-    # -- whole kernel ---------------------------------------------------------------------------------
-    def body(self):
-        self.prologue()
-        # blocks 0 and 1 (nk >= 2 by contract) into stages 0 and 1
+    def prime(self):
+        """Blocks 0 and 1 of the current tile into stages 0 and 1, then k-half 0 of block 0."""
         for stage in (0, 1):
             for m0, ld, adv in self.dma_ops(stage):
                 self.e(m0)
@@ -489,19 +531,32 @@ class Kernel:
                 self.e(ld)
                 if adv is not None:
                     self.advance(adv)
-        for i in range(256):
-            self.e(f"v_accvgpr_write_b32 a{i}, 0")
         self.e("s_waitcnt vmcnt(16)")
         self.e("s_barrier")
         for op in self.read_ops(0, 0, 0):
             self.e(op)
+        self.e("s_waitcnt lgkmcnt(0)")
+
+    # -- whole kernel ---------------------------------------------------------------------------------
+    def body(self):
+        """One tile per workgroup (any nk >= 2)."""
+        self.prologue()
+        self.tile_coords(S_U0, S_M0T, S_N0T, S_PART)
+        self.setup_tile(S_M0T, S_N0T, S_PART)
+        self.prime()
         # npairs = (nk - 2) >> 1, rem = nk - 2 npairs (2 or 3)
         self.e(f"s_sub_u32 s{S_LOOP}, s{S_NK}, 2")
         self.e(f"s_lshr_b32 s{S_LOOP}, s{S_LOOP}, 1")
         self.e(f"s_lshl_b32 s{S_REM}, s{S_LOOP}, 1")
         self.e(f"s_sub_u32 s{S_REM}, s{S_NK}, s{S_REM}")
-        self.e("s_waitcnt lgkmcnt(0)")
         lend, lbeg = self.newlab("loopend"), self.newlab("loop")
+        first_done = self.newlab("firstdone")
+        # the first pair zero-initialises the accumulators (MFMA with a 0 accumulator input)
+        self.e(f"s_cmp_le_i32 s{S_LOOP}, 0")
+        self.e(f"s_cbranch_scc1 {first_done}")
+        self.iteration(0, True, True, first=True)
+        self.iteration(1, True, True)
+        self.e(f"s_sub_i32 s{S_LOOP}, s{S_LOOP}, 1")
         self.e(f"s_cmp_le_i32 s{S_LOOP}, 0")
         self.e(f"s_cbranch_scc1 {lend}")
         self.lab(lbeg)
@@ -510,6 +565,12 @@ class Kernel:
         self.e(f"s_sub_i32 s{S_LOOP}, s{S_LOOP}, 1")
         self.e(f"s_cmp_gt_i32 s{S_LOOP}, 0")
         self.e(f"s_cbranch_scc1 {lbeg}")
+        self.e(f"s_branch {lend}")
+        # nk = 2 or 3: no pair ran — zero the accumulators here
+        self.lab(first_done)
+        for i in range(256):
+            self.e(f"v_accvgpr_write_b32 a{i}, 0")
+        self.e("s_nop 4")
         self.lab(lend)
         t2, epi = self.newlab("tail2"), self.newlab("epi")
         self.e(f"s_cmp_eq_u32 s{S_REM}, 3")
@@ -523,21 +584,83 @@ class Kernel:
         self.iteration(1, False, False)
         self.lab(epi)
         self.epilogue()
+        self.e("s_waitcnt vmcnt(0)")
+        self.e("s_endpgm")
+
+    def body_persistent(self):
+        """Workgroup w takes work units U0(w) + i·G (G = launched grid), tiles chained through
+        the LDS-DMA stream: the last K-block pair of a tile issues the NEXT tile's blocks 0 and 1
+        and reads its first fragments, so the epilogue overlaps the next tile's loads. nk even,
+        >= 4 (host contract)."""
+        self.prologue()
+        lend = self.newlab("end")
+        self.e(f"s_cmp_ge_u32 s{S_U0}, s{S_NWG}")                     # nwg = total units
+        self.e(f"s_cbranch_scc1 {lend}")
+        self.tile_coords(S_U0, S_M0T, S_N0T, S_PART)
+        self.setup_tile(S_M0T, S_N0T, S_PART)
+        self.prime()
+        ltile, lbeg, lpend = self.newlab("tile"), self.newlab("loop"), self.newlab("loopend")
+        self.lab(ltile)
+        self.iteration(0, True, True, first=True)
+        self.iteration(1, True, True)
+        self.e(f"s_lshr_b32 s{S_LOOP}, s{S_NK}, 1")
+        self.e(f"s_sub_i32 s{S_LOOP}, s{S_LOOP}, 2")
+        self.e(f"s_cmp_le_i32 s{S_LOOP}, 0")
+        self.e(f"s_cbranch_scc1 {lpend}")
+        self.lab(lbeg)
+        self.iteration(0, True, True)
+        self.iteration(1, True, True)
+        self.e(f"s_sub_i32 s{S_LOOP}, s{S_LOOP}, 1")
+        self.e(f"s_cmp_gt_i32 s{S_LOOP}, 0")
+        self.e(f"s_cbranch_scc1 {lbeg}")
+        self.lab(lpend)
+        # switch the DMA stream to the next unit (or to an empty descriptor)
+        T = S_T
+        nxt, nonext, ready = self.newlab("next"), self.newlab("nonext"), self.newlab("ready")
+        self.e(f"s_add_u32 s{T + 9}, s{S_ROUND}, 1")
+        self.e(f"s_mul_i32 s{T + 9}, s{T + 9}, s{S_GRID}")
+        self.e(f"s_add_u32 s{S_NVALID}, s{S_U0}, s{T + 9}")               # next unit
+        self.e(f"s_cmp_lt_u32 s{S_NVALID}, s{S_NWG}")
+        self.e(f"s_cbranch_scc0 {nonext}")
+        self.tile_coords(S_NVALID, S_NM0, S_NN0, S_NPART)
+        self.setup_tile(S_NM0, S_NN0, S_NPART)
+        self.e(f"s_mov_b32 s{S_NVALID}, 1")
+        self.e(f"s_branch {ready}")
+        self.lab(nonext)
+        self.e(f"s_mov_b32 s{S_SRDA + 2}, 0")
+        self.e(f"s_mov_b32 s{S_SRDB + 2}, 0")
+        self.e(f"s_mov_b32 s{S_REMA}, 0")
+        self.e(f"s_mov_b32 s{S_REMA + 1}, 0")
+        self.e(f"s_mov_b32 s{S_REMB}, 0")
+        self.e(f"s_mov_b32 s{S_REMB + 1}, 0")
+        self.e(f"s_mov_b32 s{S_STEPA}, 0")
+        self.e(f"s_mov_b32 s{S_STEPA + 1}, 0")
+        self.e(f"s_mov_b32 s{S_STEPB}, 0")
+        self.e(f"s_mov_b32 s{S_STEPB + 1}, 0")
+        self.e(f"s_mov_b32 s{S_NVALID}, 0")
+        self.lab(ready)
+        self.iteration(0, True, True)
+        self.iteration(1, True, True)
+        self.epilogue()
+        self.e(f"s_cmp_eq_u32 s{S_NVALID}, 0")
+        self.e(f"s_cbranch_scc1 {lend}")
+        self.e(f"s_mov_b32 s{S_M0T}, s{S_NM0}")
+        self.e(f"s_mov_b32 s{S_N0T}, s{S_NN0}")
+        self.e(f"s_mov_b32 s{S_PART}, s{S_NPART}")
+        self.e(f"s_add_u32 s{S_ROUND}, s{S_ROUND}, 1")
+        self.e(f"s_branch {ltile}")
+        self.lab(lend)
+        self.e("s_waitcnt vmcnt(0)")
         self.e("s_endpgm")
 
     # -- epilogues --------------------------------------------------------------------------------
     def epilogue(self):
-        E, V = S_E, V_E
+        E, V = S_E, self.VE
         ek = self.ek
         f32 = ek in ("f32", "f32acc")
         es = 4 if f32 else 2
         self.e("s_nop 15")
         self.e("s_nop 15")
-        self.e(f"s_load_dwordx8 s[{E}:{E + 7}], s[0:1], 0x60")      # c, c_bytes, ldc_b, ldaux_b, c_part
-        if ek in ("bias_act", "dact"):
-            self.e(f"s_load_dwordx4 s[{E + 8}:{E + 11}], s[0:1], 0x80")   # aux, aux_bytes
-            self.e(f"s_load_dwordx2 s[{E + 12}:{E + 13}], s[0:1], 0x90")  # bias
-        self.e("s_waitcnt lgkmcnt(0)")
         # C descriptor base = c + part*c_part + m0*ldc_b + n0*es
         T = S_T
         self.e(f"s_mul_i32 s{T}, s{S_PART}, s{E + 6}")
@@ -551,7 +674,7 @@ class Kernel:
         self.e(f"s_mul_i32 s{T + 2}, s{S_N0T}, {es}")
         self.e(f"s_add_u32 s{T}, s{T}, s{T + 2}")
         self.e(f"s_addc_u32 s{T + 1}, s{T + 1}, 0")
-        srd = S_SRDA  # main-loop descriptors are dead: reuse
+        srd = S_CSRD
         self.e(f"s_add_u32 s{srd}, s{E}, s{T}")
         self.e(f"s_addc_u32 s{srd + 1}, s{E + 1}, s{T + 1}")
         self.e(f"s_and_b32 s{srd + 1}, s{srd + 1}, 0xffff")
@@ -568,7 +691,7 @@ class Kernel:
             self.e(f"s_lshl_b32 s{T + 2}, s{S_N0T}, 1")
             self.e(f"s_add_u32 s{T}, s{T}, s{T + 2}")
             self.e(f"s_addc_u32 s{T + 1}, s{T + 1}, 0")
-            a = S_SRDB
+            a = S_AUXSRD
             self.e(f"s_add_u32 s{a}, s{E + 8}, s{T}")
             self.e(f"s_addc_u32 s{a + 1}, s{E + 9}, s{T + 1}")
             self.e(f"s_and_b32 s{a + 1}, s{a + 1}, 0xffff")
@@ -576,6 +699,9 @@ class Kernel:
             self.e(f"s_subb_u32 s{T + 3}, s{E + 11}, s{T + 1}")
             self.e(f"s_cmp_eq_u32 s{T + 3}, 0")
             self.e(f"s_cselect_b32 s{a + 2}, s{T + 2}, -1")
+            self.e(f"s_or_b32 s{T + 2}, s{E + 8}, s{E + 9}")
+            self.e(f"s_cmp_eq_u32 s{T + 2}, 0")
+            self.e(f"s_cselect_b32 s{a + 2}, 0, s{a + 2}")
             self.e(f"s_mov_b32 s{a + 3}, 0x20000")
         # lane offsets: row (wr*128 + (l&15)), col (wc*128 + 4(l>>4))
         L = V_LANE
@@ -592,6 +718,25 @@ class Kernel:
         if ek in ("bias_act", "dact"):
             self.e(f"v_mul_lo_u32 v{V + 3}, v{V}, s{E + 5}")
             self.e(f"v_lshl_add_u32 v{V + 3}, v{V + 1}, 1, v{V + 3}")  # aux voffset
+            for r, val in ((self.VCONST, K0), (self.VCONST + 1, K0 * K1), (self.VCONST + 2, 3 * K0 * K1)):
+                self.e(f"v_mov_b32 v{r}, {fhex(val)}")
+        if ek == "bias_act":
+            # bias descriptor (records 0 when there is no bias: loads return 0)
+            b = S_BIASSRD
+            self.e(f"s_lshl_b32 s{T}, s{S_N0T}, 1")
+            self.e(f"s_add_u32 s{b}, s{E + 12}, s{T}")
+            self.e(f"s_addc_u32 s{b + 1}, s{E + 13}, 0")
+            self.e(f"s_and_b32 s{b + 1}, s{b + 1}, 0xffff")
+            self.e(f"s_sub_u32 s{T + 1}, s{S_N}, s{S_N0T}")
+            self.e(f"s_lshl_b32 s{T + 1}, s{T + 1}, 1")
+            self.e(f"s_or_b32 s{T + 2}, s{E + 12}, s{E + 13}")
+            self.e(f"s_cmp_eq_u32 s{T + 2}, 0")
+            self.e(f"s_cselect_b32 s{b + 2}, 0, s{T + 1}")
+            self.e(f"s_mov_b32 s{b + 3}, 0x20000")
+            self.e(f"v_lshlrev_b32 v{V + 7}, 1, v{V + 1}")
+            for nb in range(8):
+                self.e(f"buffer_load_dwordx2 v[{self.VBIAS + 2 * nb}:{self.VBIAS + 2 * nb + 1}], v{V + 7}, s[{b}:{b + 3}], 0 offen offset:{nb * 32}")
+            self.e("s_waitcnt vmcnt(0)")
         self.e(f"v_add_u32 v{V + 4}, s{S_N0T}, v{V + 1}")            # global col (nb = 0)
         # edge tile in N: per-store EXEC masks
         full = self.newlab("full")
@@ -604,12 +749,11 @@ class Kernel:
         self.lab(full)
         self.store_all(masked=False)
         self.lab(done)
-        self.e("s_waitcnt vmcnt(0)")
 
     def store_all(self, masked):
-        E, V, T = S_E, V_E, S_T
+        E, V, T = S_E, self.VE, S_T
         ek = self.ek
-        srd = S_SRDA
+        srd = S_CSRD
         es = 4 if ek in ("f32", "f32acc") else 2
         W = V + 8          # working registers
         for mb in range(8):
@@ -627,7 +771,12 @@ class Kernel:
             if ek == "dact":
                 for nb in range(8):
                     d = W + 32 + 2 * nb
-                    self.e(f"buffer_load_dwordx2 v[{d}:{d + 1}], v{V + 6}, s[{S_SRDB}:{S_SRDB + 3}], 0 offen offset:{nb * 32}")
+                    self.e(f"buffer_load_dwordx2 v[{d}:{d + 1}], v{V + 6}, s[{S_AUXSRD}:{S_AUXSRD + 3}], 0 offen offset:{nb * 32}")
+                self.e("s_waitcnt vmcnt(0)")
+            if ek == "bf16acc":
+                for nb in range(8):
+                    d = W + 32 + 2 * nb
+                    self.e(f"buffer_load_dwordx2 v[{d}:{d + 1}], v{V + 5}, s[{srd}:{srd + 3}], 0 offen offset:{nb * 32}")
                 self.e("s_waitcnt vmcnt(0)")
             for nb in range(8):
                 c = acc(mb, nb)
@@ -648,23 +797,95 @@ class Kernel:
                         self.bias_act_vals(d, nb, mb)
                     elif ek == "dact":
                         self.dact_vals(d, W + 32 + 2 * nb)
+                    elif ek == "bf16acc":
+                        for j in range(4):
+                            self.unpack(self.VTMP, W + 32 + 2 * nb + j // 2, j)
+                            self.e(f"v_add_f32 v{d + j}, v{self.VTMP}, v{d + j}")
                     self.e(f"v_cvt_pk_bf16_f32 v{d}, v{d}, v{d + 1}")
                     self.e(f"v_cvt_pk_bf16_f32 v{d + 1}, v{d + 2}, v{d + 3}")
                     self.e(f"buffer_store_dwordx2 v[{d}:{d + 1}], v{V + 5}, s[{srd}:{srd + 3}], 0 offen offset:{nb * 32}")
                 if masked:
                     self.e("s_mov_b64 exec, -1")
 
-    # placeholders for the fused activation epilogues (filled in by later variants)
+    # -- fused activation epilogues -----------------------------------------------------------------
+    def trans(self, op):
+        """A transcendental op; gfx950 needs one wait state before a VALU consumes its result."""
+        self.e(op)
+        self.e("s_nop 0")
+
+    def gelu(self, x):
+        """x ← gelu_tanh(x) = x·(1 − r), r = 1 / (exp(2u) + 1), u = k0·(x + k1·x³)."""
+        ta = self.VTMP
+        c0, c1 = self.VCONST, self.VCONST + 1
+        self.e(f"v_mul_f32 v{ta}, v{x}, v{x}")
+        self.e(f"v_fma_f32 v{ta}, v{ta}, v{c1}, v{c0}")
+        self.e(f"v_mul_f32 v{ta}, v{ta}, v{x}")
+        self.e(f"v_mul_f32 v{ta}, {fhex(TWO_LOG2E)}, v{ta}")
+        self.trans(f"v_exp_f32 v{ta}, v{ta}")
+        self.e(f"v_add_f32 v{ta}, 1.0, v{ta}")
+        self.trans(f"v_rcp_f32 v{ta}, v{ta}")
+        self.e(f"v_fma_f32 v{x}, -v{x}, v{ta}, v{x}")
+
+    def gelu_grad_mul(self, y, h):
+        """y ← y · gelu_tanh'(h) = y · (1−r)(1 + 2h·r·(k0 + 3k0k1·h²))."""
+        ta, tb = self.VTMP, self.VTMP + 1
+        c0, c1, c3 = self.VCONST, self.VCONST + 1, self.VCONST + 2
+        self.e(f"v_mul_f32 v{ta}, v{h}, v{h}")
+        self.e(f"v_fma_f32 v{tb}, v{ta}, v{c1}, v{c0}")
+        self.e(f"v_fma_f32 v{ta}, v{ta}, v{c3}, v{c0}")
+        self.e(f"v_mul_f32 v{tb}, v{tb}, v{h}")
+        self.e(f"v_mul_f32 v{tb}, {fhex(TWO_LOG2E)}, v{tb}")
+        self.trans(f"v_exp_f32 v{tb}, v{tb}")
+        self.e(f"v_add_f32 v{tb}, 1.0, v{tb}")
+        self.trans(f"v_rcp_f32 v{tb}, v{tb}")
+        self.e(f"v_mul_f32 v{ta}, v{ta}, v{h}")
+        self.e(f"v_mul_f32 v{ta}, v{ta}, v{tb}")
+        self.e(f"v_sub_f32 v{tb}, 1.0, v{tb}")
+        self.e(f"v_add_f32 v{ta}, v{ta}, v{ta}")
+        self.e(f"v_fma_f32 v{ta}, v{ta}, v{tb}, v{tb}")
+        self.e(f"v_mul_f32 v{y}, v{y}, v{ta}")
+
+    def unpack(self, dst, src, j):
+        if j % 2 == 0:
+            self.e(f"v_lshlrev_b32 v{dst}, 16, v{src}")
+        else:
+            self.e(f"v_and_b32 v{dst}, 0xffff0000, v{src}")
+
     def bias_act_vals(self, d, nb, mb):
-        raise NotImplementedError
+        """pre = bf16(acc + bias) → aux; d ← act(pre) (f32, rounded to bf16 by the caller)."""
+        t, p = self.VTMP + 2, self.VTMP + 4
+        for j in range(4):
+            self.unpack(t, self.VBIAS + 2 * nb + j // 2, j)
+            self.e(f"v_add_f32 v{d + j}, v{t}, v{d + j}")
+        self.e(f"v_cvt_pk_bf16_f32 v{p}, v{d}, v{d + 1}")
+        self.e(f"v_cvt_pk_bf16_f32 v{p + 1}, v{d + 2}, v{d + 3}")
+        self.e(f"buffer_store_dwordx2 v[{p}:{p + 1}], v{self.VE + 6}, s[{S_AUXSRD}:{S_AUXSRD + 3}], 0 offen offset:{nb * 32}")
+        if self.act == 0:
+            return
+        for j in range(4):
+            self.unpack(d + j, p + j // 2, j)
+            if self.act == 1:
+                self.gelu(d + j)
+            else:
+                self.e(f"v_max_f32 v{d + j}, 0, v{d + j}")
 
     def dact_vals(self, d, auxreg):
-        raise NotImplementedError
+        h = self.VTMP + 2
+        for j in range(4):
+            self.unpack(h, auxreg + j // 2, j)
+            if self.act == 1:
+                self.gelu_grad_mul(d + j, h)
+            else:
+                self.e(f"v_cmp_lt_f32 vcc, 0, v{h}")
+                self.e(f"v_cndmask_b32 v{d + j}, 0, v{d + j}, vcc")
 
     # -- text ----------------------------------------------------------------------------------------
     def text(self):
         self.lines = []
-        self.body()
+        if self.persistent:
+            self.body_persistent()
+        else:
+            self.body()
         n = self.name
         head = [
             "\t.text",
@@ -722,17 +943,26 @@ class Kernel:
 
 
 LAYOUTS = {"nt": (True, True), "tn": (False, False), "nn": (True, False), "tt": (False, True)}
-EPILOGUES = ("bf16", "f32", "f32acc")
+EPILOGUES = ("bf16", "bf16acc", "f32", "f32acc")
+
+
+FUSED = ("bias", "biasgelu", "biasrelu", "dgelu", "drelu")
 
 
 def variants():
-    for lay in ("nt", "tn", "nn", "tt"):
-        for ek in EPILOGUES:
-            yield f"piamd_agemm_{lay}_{ek}", LAYOUTS[lay][0], LAYOUTS[lay][1], ek
+    """(name, A K-contiguous, B K-contiguous, epilogue, persistent). ``_p_`` kernels are the
+    persistent ones (nk even and >= 4); the others take one tile per workgroup (any nk >= 2)."""
+    for pers in (False, True):
+        tag = "p_" if pers else ""
+        for lay in ("nt", "tn", "nn", "tt"):
+            for ek in EPILOGUES:
+                yield f"piamd_agemm_{tag}{lay}_{ek}", LAYOUTS[lay][0], LAYOUTS[lay][1], ek, pers
+        for ek in FUSED:  # fused epilogues: forward / data-gradient products (both K-contiguous)
+            yield f"piamd_agemm_{tag}nt_{ek}", True, True, ek, pers
 
 
 def generate() -> str:
-    ks = [Kernel(n, a, b, ek) for n, a, b, ek in variants()]
+    ks = [Kernel(n, a, b, ek, pers) for n, a, b, ek, pers in variants()]
     out = ['\t.amdgcn_target "amdgcn-amd-amdhsa--gfx950"', "\t.amdhsa_code_object_version 5"]
     for k in ks:
         out.append(k.text())

@@ -6,6 +6,7 @@
 // and their gradients), `paddle/fluid/operators/fused/fused_gemm_epilogue_op.cu` (epilogues).
 #include "common.h"
 
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -27,7 +28,7 @@ struct __attribute__((packed)) AgemmArgs {
   float rcp_ntiles;            // 72
   unsigned per_group;          // 76
   float rcp_per_group;         // 80
-  unsigned gm, act, pad0;      // 84, 88, 92
+  unsigned gm, act, grid;      // 84, 88, 92
   void* c;                     // 96
   unsigned long long c_bytes;  // 104
   unsigned ldc_b, ldaux_b;     // 112, 116
@@ -54,6 +55,17 @@ hipFunction_t get_fn(const std::string& name) {
 }
 
 constexpr int GROUP_M = 8;
+
+int num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
 
 // C (+)= Σ_p ws[p] in a fixed order (deterministic); 4 columns per thread
 __global__ __launch_bounds__(256) void agemm_reduce_kernel(const float* __restrict__ ws, int ksplit,
@@ -97,7 +109,7 @@ PIAMD_EXPORT int piamd_agemm_loaded() { return g_mod != nullptr; }
 // trans_a: A stored [K][M] (else [M][K]); trans_b: B stored [N][K] (else [K][N]).
 // K % (64·ksplit) == 0 with K/ksplit ≥ 128; N % 4 == 0; leading dims % 8 == 0 and < 2^22;
 // M % 8 == 0 when A is [K][M]; N % 8 == 0 when B is [K][N]; 16-byte aligned pointers.
-// c_f32 / accumulate: bf16 store, f32 store, f32 accumulate (bf16 accumulate only via split-K).
+// c_f32 / accumulate: bf16 or f32 C, stored or accumulated (C += A·B).
 // ksplit > 1: f32 partial planes in ws [ksplit][M][N], reduced in a fixed order.
 PIAMD_EXPORT int piamd_agemm(const void* a, long long lda, int trans_a, const void* b, long long ldb,
                              int trans_b, void* c, long long ldc, int c_f32, int accumulate, int M,
@@ -106,28 +118,43 @@ PIAMD_EXPORT int piamd_agemm(const void* a, long long lda, int trans_a, const vo
   const bool a_kc = !trans_a, b_kc = trans_b;
   if (M <= 0 || N <= 0 || K <= 0 || ksplit < 1 || K % (64 * ksplit) || K / ksplit < 128 || N % 4 ||
       (!a_kc && M % 8) || (!b_kc && N % 8) || lda % 8 || ldb % 8 || ldc % 4 ||
-      lda >= (1 << 22) || ldb >= (1 << 22) || ldc >= (1 << 26) || epi != 0 ||
-      (ksplit > 1 && !ws) || (!c_f32 && accumulate && ksplit == 1) ||
+      lda >= (1 << 22) || ldb >= (1 << 22) || ldc >= (1 << 26) || epi < 0 || epi > 2 ||
+      (epi != 0 && (!a_kc || !b_kc || c_f32 || accumulate || ksplit > 1 || ldaux % 4 ||
+                    (epi == 2 && !aux) || !(act == 0 || act == 1 || act == 3) ||
+                    (epi == 2 && act == 0))) ||
+      (ksplit > 1 && !ws) ||
       ((uintptr_t)a | (uintptr_t)b | (uintptr_t)c) % 16)
     return (int)hipErrorInvalidValue;
   const char* lay = a_kc ? (b_kc ? "nt" : "nn") : (b_kc ? "tt" : "tn");
   const char* ek;
   AgemmArgs g;
   std::memset(&g, 0, sizeof(g));
-  if (ksplit > 1) {
+  if (epi != 0) {
+    static const char* const kFused[2][4] = {{"bias", "biasgelu", "", "biasrelu"},
+                                             {"", "dgelu", "", "drelu"}};
+    ek = kFused[epi - 1][act];
+    g.c = c;
+    g.ldc_b = (unsigned)(ldc * 2);
+    g.c_bytes = ((unsigned long long)(M - 1) * ldc + N) * 2;
+    g.aux_bytes = aux ? ((unsigned long long)(M - 1) * ldaux + N) * 2 : 0;
+  } else if (ksplit > 1) {
     ek = "f32";
     g.c = ws;
     g.ldc_b = (unsigned)N * 4;
     g.c_part = (unsigned long long)M * N * 4;
     g.c_bytes = g.c_part * ksplit;
   } else {
-    ek = c_f32 ? (accumulate ? "f32acc" : "f32") : "bf16";
+    ek = c_f32 ? (accumulate ? "f32acc" : "f32") : (accumulate ? "bf16acc" : "bf16");
     const int es = c_f32 ? 4 : 2;
     g.c = c;
     g.ldc_b = (unsigned)(ldc * es);
     g.c_bytes = ((unsigned long long)(M - 1) * ldc + N) * es;
   }
-  const std::string name = std::string("piamd_agemm_") + lay + "_" + ek;
+  // persistent kernel (work units chained through the LDS-DMA stream) when every unit has an
+  // even K-block count >= 4; otherwise one tile per workgroup
+  const int nk = K / ksplit / 64;
+  const bool persistent = nk % 2 == 0 && nk >= 4 && !getenv("PIAMD_AGEMM_NO_PERSIST");
+  const std::string name = std::string("piamd_agemm_") + (persistent ? "p_" : "") + lay + "_" + ek;
   hipFunction_t f = get_fn(name);
   if (!f) return (int)hipErrorInvalidDeviceFunction;
   g.a = a;
@@ -146,6 +173,7 @@ PIAMD_EXPORT int piamd_agemm(const void* a, long long lda, int trans_a, const vo
   const long long nwg = (long long)g.ntiles * ksplit;
   if (nwg >= (1 << 24)) return (int)hipErrorInvalidValue;
   g.nwg = (unsigned)nwg;
+  g.grid = persistent ? (unsigned)std::min<long long>(nwg, num_cus()) : (unsigned)nwg;
   g.rcp_ntiles = 1.0f / (float)g.ntiles;
   g.gm = GROUP_M;
   g.per_group = GROUP_M * g.tiles_n;
@@ -157,7 +185,7 @@ PIAMD_EXPORT int piamd_agemm(const void* a, long long lda, int trans_a, const vo
   size_t sz = sizeof(g);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &g, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
                  HIP_LAUNCH_PARAM_END};
-  hipError_t err = hipModuleLaunchKernel(f, g.nwg, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
+  hipError_t err = hipModuleLaunchKernel(f, g.grid, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
   if (err != hipSuccess || ksplit == 1) return (int)err;
   const long long q = (long long)M * N / 4;
   const int grid = (int)std::min<long long>(2048, (q + 255) / 256);

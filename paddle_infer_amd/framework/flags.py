@@ -5,7 +5,9 @@ Flags honoured by this framework: FLAGS_check_nan_inf (NaN/Inf checker on every 
 FLAGS_use_hipgraph (inference predictor graph capture), FLAGS_allocator_strategy ("auto_growth"
 in the environment or set before the first device allocation installs the framework's own
 auto-growth best-fit HIP allocator, ``framework/allocator.py``; the in-process default stays
-PyTorch's caching allocator), FLAGS_fraction_of_gpu_memory_to_use (accepted).
+PyTorch's caching allocator; ``get_flags`` reports the allocator actually installed),
+FLAGS_fraction_of_gpu_memory_to_use (the per-process memory fraction of the caching allocator).
+Setting a flag that is not registered raises, as the reference's ``set_flags`` does.
 """
 from __future__ import annotations
 
@@ -22,6 +24,22 @@ _FLAGS = {
     "FLAGS_eager_delete_tensor_gb": 0.0,
     "FLAGS_benchmark": False,
     "FLAGS_embedding_deterministic": 0,
+    "FLAGS_conv_workspace_size_limit": 512,
+    "FLAGS_cudnn_exhaustive_search": False,
+    "FLAGS_use_autotune": False,
+    "FLAGS_max_inplace_grad_add": 0,
+    "FLAGS_enable_gpu_memory_usage_log": False,
+    "FLAGS_call_stack_level": 1,
+    "FLAGS_sort_sum_gradient": False,
+    "FLAGS_gpu_allocator_retry_time": 10000,
+    "FLAGS_initial_gpu_memory_in_mb": 0,
+    "FLAGS_reallocate_gpu_memory_in_mb": 0,
+    "FLAGS_use_stream_safe_cuda_allocator": True,
+    "FLAGS_new_executor_use_cuda_graph": False,
+    "FLAGS_tracer_profile_fname": "",
+    "FLAGS_print_ir": False,
+    "FLAGS_low_precision_op_list": 0,
+    "FLAGS_selected_gpus": "",
 }
 for k in list(_FLAGS):
     if k in os.environ:
@@ -31,6 +49,9 @@ for k in list(_FLAGS):
 
 
 def set_flags(flags: dict):
+    for k in flags:
+        if k not in _FLAGS:
+            raise ValueError(f"Flag {k} is not registered in this framework's flag registry")
     for k, v in flags.items():
         _FLAGS[k] = v
         if k == "FLAGS_cudnn_deterministic":
@@ -38,6 +59,11 @@ def set_flags(flags: dict):
         if k == "FLAGS_check_nan_inf":
             from ..utils import nan_inf
             nan_inf.enable(bool(v))
+        if k == "FLAGS_cudnn_exhaustive_search" or k == "FLAGS_use_autotune":
+            from ..ops import autotune
+            autotune.configure(enable=bool(v))
+        if k == "FLAGS_fraction_of_gpu_memory_to_use" and torch.cuda.is_available():
+            torch.cuda.set_per_process_memory_fraction(float(v))
         if k == "FLAGS_allocator_strategy" and v == "auto_growth":
             from . import allocator
             try:
@@ -49,7 +75,16 @@ def set_flags(flags: dict):
 
 def get_flags(flags):
     names = [flags] if isinstance(flags, str) else list(flags)
-    return {k: _FLAGS.get(k) for k in names}
+    out = {}
+    for k in names:
+        if k not in _FLAGS:
+            raise ValueError(f"Flag {k} is not registered in this framework's flag registry")
+        v = _FLAGS[k]
+        if k == "FLAGS_allocator_strategy":
+            from . import allocator
+            v = "auto_growth" if allocator.active() else "torch_caching"
+        out[k] = v
+    return out
 
 
 def flag(name, default=None):

@@ -155,17 +155,28 @@ def _sort(self, *args, **kw):
     return _orig("sort")(self, *args, **kw)
 
 
+def _paddle_index_form(args, kw):
+    """True only when the call cannot be torch's ``(dim, index)`` signature: no ``dim`` keyword
+    and either a Tensor first positional argument (Paddle's ``(index, axis)`` order) or an
+    ``axis`` keyword. Torch keyword calls (``x.gather(dim=1, index=i)``) are forwarded unchanged."""
+    if "dim" in kw:
+        return False
+    if args:
+        return isinstance(args[0], torch.Tensor)
+    return "axis" in kw and isinstance(kw.get("index"), torch.Tensor)
+
+
 def _gather(self, *args, **kw):
-    idx = args[0] if args else kw.get("index")
-    if isinstance(idx, torch.Tensor):  # paddle.gather(x, index, axis=0): rows along `axis`
+    if _paddle_index_form(args, kw):  # paddle.gather(x, index, axis=0): rows along `axis`
+        idx = args[0] if args else kw["index"]
         ax = kw.get("axis", args[1] if len(args) > 1 else 0)
         return torch.index_select(self, int(ax or 0), idx.reshape(-1).long())
     return _orig("gather")(self, *args, **kw)
 
 
 def _index_select(self, *args, **kw):
-    idx = args[0] if args else kw.get("index")
-    if isinstance(idx, torch.Tensor):  # paddle order: (index, axis)
+    if _paddle_index_form(args, kw):  # paddle order: (index, axis)
+        idx = args[0] if args else kw["index"]
         ax = kw.get("axis", args[1] if len(args) > 1 else 0)
         return _orig("index_select")(self, int(ax), idx.long())
     return _orig("index_select")(self, *args, **kw)

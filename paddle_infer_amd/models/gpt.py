@@ -28,7 +28,7 @@ import torch.nn.functional as F
 from ..nn.layer.base import Layer, LayerList
 from ..nn import initializer as I
 from ..ops import fused_add_layer_norm, flash_attention_packed, bias_act, softmax_cross_entropy
-from ..ops.linear import _use_transposed, transposed
+from ..ops.linear import _use_transposed, mm_nt, transposed, wgrad_into
 from ..ops.linear import linear as _linear
 from ..ops.embedding import embedding as ops_embedding
 from ..distributed.fleet.mp_layers import (ColumnParallelLinear, RowParallelLinear,
@@ -208,20 +208,23 @@ class _LMHeadFn(torch.autograd.Function):
         y2 = y.reshape(-1, shp[-1])
         ctx.save_for_backward(y2, w)
         ctx.shp = shp
-        return torch.mm(y2, w.t()).view(*shp[:-1], w.shape[0])
+        return mm_nt(y2.contiguous(), w).view(*shp[:-1], w.shape[0])
 
     @staticmethod
     def backward(ctx, dl):
         y2, w = ctx.saved_tensors
         dl2 = dl.reshape(-1, w.shape[0])
-        # dgrad on the [h, V] copy: both operands V-contiguous (hipBLASLt's fast layout, ops/linear.py)
-        wk = transposed(w).t() if _use_transposed(dl2, w) else w
-        dy = torch.mm(dl2, wk).view(ctx.shp)
+        # dgrad on the [h, V] copy: both operands V-contiguous (the GEMMs' fast layout, ops/linear.py)
+        dl2 = dl2.contiguous()
+        if _use_transposed(dl2, w):
+            dy = mm_nt(dl2, transposed(w)).view(ctx.shp)
+        else:
+            dy = torch.mm(dl2, w).view(ctx.shp)
         mg = getattr(w, "main_grad", None)
         if mg is not None:
-            mg.addmm_(dl2.t(), y2)
+            wgrad_into(mg, dl2, y2)
             return dy, None
-        return dy, torch.mm(dl2.t(), y2)
+        return dy, wgrad_into(torch.zeros_like(w), dl2, y2)
 
 
 class GPTModel(Layer):

@@ -46,6 +46,26 @@ def _stockham_torch(x, inverse):
     return x.reshape(*lead, N)
 
 
+class _KernelDFT(torch.autograd.Function):
+    """`fft.hip` rows as an autograd op. y = F·x with F unitary up to scale, so the vector-Jacobian
+    product (PyTorch's conjugate-Wirtinger convention) is Fᴴ·g: the unscaled DFT of the opposite
+    sign — composes through four-step, Bluestein, r2c and c2r (reference fft_c2c_grad)."""
+
+    @staticmethod
+    def forward(ctx, x, inverse):
+        ctx.inverse = inverse
+        N = x.shape[-1]
+        out = torch.empty_like(x)
+        xc = x.contiguous()
+        _lib.call("piamd_fft_c2c", xc.data_ptr(), out.data_ptr(), xc.numel() // N, N,
+                  int(inverse), 1.0, _lib.stream())
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return _pow2(g.contiguous(), not ctx.inverse), None
+
+
 def _pow2(x, inverse):
     """Unscaled DFT (sign by ``inverse``) of contiguous rows, power-of-two length."""
     N = x.shape[-1]
@@ -53,11 +73,7 @@ def _pow2(x, inverse):
         return x.clone()
     if x.is_cuda and x.dtype == torch.complex64:
         if N <= MAX_KERNEL_N:
-            out = torch.empty_like(x)
-            xc = x.contiguous()
-            _lib.call("piamd_fft_c2c", xc.data_ptr(), out.data_ptr(), xc.numel() // N, N,
-                      int(inverse), 1.0, _lib.stream())
-            return out
+            return _KernelDFT.apply(x, inverse)
         return _four_step(x, inverse)
     return _stockham_torch(x, inverse)
 

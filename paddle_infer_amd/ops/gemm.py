@@ -98,8 +98,11 @@ def asm_supported(a, b, trans_a=False, trans_b=False, ksplit=1):
 
 
 def asm_gemm(a, b, trans_a=False, trans_b=False, out=None, out_f32=False, accumulate=False,
-             ksplit=1):
-    """C (+)= op(A)·op(B) on the hand-scheduled assembly kernels (plain epilogues)."""
+             ksplit=1, epi="none", act="none", bias=None, aux=None):
+    """C (+)= op(A)·op(B) on the hand-scheduled assembly kernels. Fused epilogues (A stored
+    [M, K], B stored [N, K], bf16 C): ``epi="bias_act"`` — pre = bf16(A·B + bias) written to
+    ``aux`` (optional), C = act(pre); ``epi="dact"`` — C = (A·B) ⊙ act'(aux). act ∈ none / gelu_tanh
+    / relu."""
     _agemm_load()
     M = a.shape[1] if trans_a else a.shape[0]
     K = a.shape[0] if trans_a else a.shape[1]
@@ -110,9 +113,12 @@ def asm_gemm(a, b, trans_a=False, trans_b=False, out=None, out_f32=False, accumu
     ws = None
     if ksplit > 1:
         ws = torch.empty((ksplit, M, N), dtype=torch.float32, device=a.device)
+    if aux is not None:
+        assert aux.shape == (M, N) and aux.dtype == torch.bfloat16 and aux.stride(-1) == 1
     _lib.call("piamd_agemm", a.data_ptr(), a.stride(0), int(trans_a), b.data_ptr(), b.stride(0),
               int(trans_b), out.data_ptr(), out.stride(0), int(out.dtype == torch.float32),
-              int(accumulate), M, N, K, 0, 0, None, None, 0, ksplit, _lib.ptr(ws), _lib.stream())
+              int(accumulate), M, N, K, _EPI[epi], ACTS[act], _lib.ptr(bias), _lib.ptr(aux),
+              aux.stride(0) if aux is not None else 0, ksplit, _lib.ptr(ws), _lib.stream())
     return out
 
 

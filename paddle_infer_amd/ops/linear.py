@@ -4,11 +4,14 @@ Parity: ``paddle.nn.functional.linear`` (`python/paddle/nn/functional/common.py`
 ``fused_matmul_bias`` / ``fused_linear`` (`incubate/nn/functional/fused_matmul_bias.py`,
 `fluid/operators/fused/fused_gemm_epilogue_op.cu`).
 
-Plain GEMMs go to hipBLASLt through ``torch.matmul``/``addmm`` (bias fused as the GEMM epilogue).
-When a weight carries a ``main_grad`` buffer (a view into the framework's flat gradient buffer),
-the backward accumulates ``xᵀ·dy`` straight into it with ``addmm_`` (β = 1) — the weight gradient is
-never materialised as a separate tensor, and the parameter's ``_grad_ready`` hook (the bucketed
-reduce-scatter/all-reduce trigger) fires right after.
+Every GEMM of a bf16 linear on the GPU runs on the framework's hand-scheduled assembly GEMM
+(`csrc/asm/gemm_gen.py`, ``ops.gemm.asm_gemm``): forward ``x·Wtᵀ`` with the bias in the epilogue,
+data gradient ``dy·Wᵀ``, and weight gradient ``xᵀ·dy`` accumulated straight into ``main_grad`` (a
+view into the framework's flat gradient buffer) with split-K when the tile grid is small — the
+weight gradient is never materialised as a separate tensor, and the parameter's ``_grad_ready``
+hook (the bucketed reduce-scatter/all-reduce trigger) fires right after. ``PIAMD_GEMM=blas``
+routes the same products to hipBLASLt (A/B comparisons); shapes outside the kernel contract
+(K not a multiple of 64, fp32/fp16) take hipBLASLt too.
 
 Weight layout for the forward GEMM: on gfx950 hipBLASLt is 12-21 % faster when BOTH operands are
 contiguous along the reduction dim (`x @ Wtᵀ` with ``Wt = [out, in]``) than on Paddle's ``x @ W``
@@ -20,6 +23,50 @@ per optimizer step, refreshed lazily on first use after the weights change) for 
 from __future__ import annotations
 
 import torch
+
+
+import os
+
+_GEMM_IMPL = [os.environ.get("PIAMD_GEMM", "asm")]
+
+
+def set_gemm_impl(impl: str) -> None:
+    """"asm" (default: the framework's assembly GEMM) or "blas" (hipBLASLt)."""
+    assert impl in ("asm", "blas"), impl
+    _GEMM_IMPL[0] = impl
+
+
+def _asm(a, b, trans_a=False, trans_b=False, ksplit=1):
+    if _GEMM_IMPL[0] != "asm" or not a.is_cuda:
+        return False
+    from .gemm import asm_supported
+    return asm_supported(a, b, trans_a, trans_b, ksplit)
+
+
+def mm_nt(x2, w_nk, bias=None):
+    """y[M, N] = x2[M, K] · w_nkᵀ (+ bias), both operands K-contiguous."""
+    if _asm(x2, w_nk, trans_b=True) and (bias is None or bias.dtype == x2.dtype):
+        from .gemm import asm_gemm
+        if bias is not None:
+            return asm_gemm(x2, w_nk, trans_b=True, epi="bias_act", act="none", bias=bias.contiguous())
+        return asm_gemm(x2, w_nk, trans_b=True)
+    if bias is not None:
+        return torch.addmm(bias, x2, w_nk.t())
+    return torch.mm(x2, w_nk.t())
+
+
+def wgrad_into(out, x2, dy2):
+    """out[K, N] += x2[T, K]ᵀ · dy2[T, N] (weight gradient into main_grad; split-K on small grids)."""
+    from .gemm import asm_gemm, pick_ksplit
+    if out.is_contiguous() and out.dtype in (torch.bfloat16, torch.float32) and dy2.is_contiguous():
+        ks = pick_ksplit(out.shape[0], out.shape[1], x2.shape[0])
+        if not _asm(x2, dy2, trans_a=True, ksplit=ks):
+            ks = 1
+        if _asm(x2, dy2, trans_a=True, ksplit=ks):
+            asm_gemm(x2, dy2, trans_a=True, out=out, accumulate=True, ksplit=ks)
+            return out
+    out.addmm_(x2.t(), dy2)
+    return out
 
 
 def _fire(p):
@@ -73,11 +120,12 @@ class _LinearFn(torch.autograd.Function):
     def forward(ctx, x, w, b):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
-        wf = transposed(w).t() if _use_transposed(x2, w) else w
-        if b is not None:
-            y = torch.addmm(b, x2, wf)
+        if _use_transposed(x2, w):
+            y = mm_nt(x2, transposed(w), b)
+        elif b is not None:
+            y = torch.addmm(b, x2, w)
         else:
-            y = torch.mm(x2, wf)
+            y = torch.mm(x2, w)
         ctx.save_for_backward(x2, w)
         ctx.has_b = b is not None
         ctx.bias = b
@@ -91,13 +139,18 @@ class _LinearFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, w.shape[1])
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = torch.mm(dy2, w.t()).view(ctx.shp)
+            dy2c = dy2.contiguous() if w.is_contiguous() else dy2
+            dx = (mm_nt(dy2c, w) if w.is_contiguous() and dy2c.dtype == w.dtype
+                  else torch.mm(dy2, w.t())).view(ctx.shp)
         dw = db = None
         mg = getattr(w, "main_grad", None)
         if ctx.needs_input_grad[1]:
             if mg is not None:
-                mg.addmm_(x2.t(), dy2)
+                wgrad_into(mg, x2, dy2.contiguous())
                 _fire(w)
+            elif _asm(x2, dy2.contiguous(), trans_a=True):
+                dw = torch.zeros_like(w)
+                wgrad_into(dw, x2, dy2.contiguous())
             else:
                 dw = torch.mm(x2.t(), dy2)
         if ctx.has_b and ctx.needs_input_grad[2]:

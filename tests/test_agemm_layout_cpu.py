@@ -81,7 +81,7 @@ def test_mc_image_fragments_and_banks():
 
 def test_generator_emits_every_variant():
     text = gg.generate()
-    for name, _, _, _ in gg.variants():
+    for name, *_ in gg.variants():
         assert f"{name}:" in text and f".amdhsa_kernel {name}" in text
     # every store is a vector buffer store
     mnems = {ln.split()[0] for ln in text.splitlines() if ln.strip()}

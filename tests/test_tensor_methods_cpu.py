@@ -64,3 +64,19 @@ def test_static_trace_of_paddle_forms_lowers():
         desc, _ = load_paddle_model(os.path.join(td, "m"))
     types = [o["type"] for o in desc["blocks"][0]["ops"]]
     assert "transpose2" in types and "reduce_sum" in types and "unsqueeze2" in types
+
+
+def test_torch_keyword_gather_index_select_unchanged():
+    """The Paddle-signature adapters must not capture torch keyword calls (process-wide patch)."""
+    import paddle_infer_amd  # noqa: F401
+    x = torch.arange(12.).reshape(3, 4)
+    idx = torch.tensor([[0, 1], [2, 3], [1, 1]])
+    torch.testing.assert_close(x.gather(dim=1, index=idx), torch.gather(x, 1, idx))
+    torch.testing.assert_close(x.gather(1, idx), torch.gather(x, 1, idx))
+    i1 = torch.tensor([3, 0])
+    torch.testing.assert_close(x.index_select(dim=1, index=i1), torch.index_select(x, 1, i1))
+    torch.testing.assert_close(x.index_select(1, i1), torch.index_select(x, 1, i1))
+    # Paddle forms still work
+    torch.testing.assert_close(x.gather(torch.tensor([2, 0])), x[[2, 0]])
+    torch.testing.assert_close(x.index_select(i1, axis=1), x[:, [3, 0]])
+    torch.testing.assert_close(x.gather(index=torch.tensor([1]), axis=0), x[[1]])

@@ -29,6 +29,12 @@ def check(M, N, K, ta, tb, kind, ksplit=1, gen=None):
         c = asm_gemm(a, b, ta, tb, ksplit=ksplit).float()
     elif kind == "f32":
         c = asm_gemm(a, b, ta, tb, out_f32=True, ksplit=ksplit)
+    elif kind == "bf16acc":
+        c0 = torch.randn(M, N, device="cuda", generator=gen).bfloat16()
+        c = c0.clone()
+        asm_gemm(a, b, ta, tb, out=c, accumulate=True, ksplit=ksplit)
+        c = c.float()
+        r = r + c0.float()
     else:
         c0 = torch.randn(M, N, device="cuda", generator=gen)
         c = c0.clone()
@@ -36,7 +42,7 @@ def check(M, N, K, ta, tb, kind, ksplit=1, gen=None):
         r = r + c0
     torch.cuda.synchronize()
     err = (c - r).abs().max().item()
-    tol = 0.02 * r.abs().max().item() + 1e-3 if kind == "bf16" else 1e-3 * (K ** 0.5)
+    tol = 0.02 * r.abs().max().item() + 1e-3 if kind.startswith("bf16") else 1e-3 * (K ** 0.5)
     return err, tol
 
 
@@ -44,20 +50,64 @@ def small():
     gen = torch.Generator(device="cuda").manual_seed(0)
     fails = 0
     cases = [(256, 256, 128), (256, 256, 192), (512, 256, 256), (256, 512, 320), (304, 264, 128),
-             (1000, 1008, 448), (2048, 768, 512), (136, 2056, 256)]
+             (1000, 1008, 448), (2048, 768, 512), (136, 2056, 256), (4352, 4104, 256),
+             (8192, 2048, 384)]
     for (M, N, K) in cases:
         for ta, tb in ((False, True), (True, False), (False, False), (True, True)):
-            for kind in ("bf16", "f32", "f32acc"):
+            for kind in ("bf16", "bf16acc", "f32", "f32acc"):
                 err, tol = check(M, N, K, ta, tb, kind, gen=gen)
                 ok = err <= tol
                 fails += not ok
                 print(json.dumps({"M": M, "N": N, "K": K, "ta": ta, "tb": tb, "kind": kind,
                                   "err": round(err, 5), "tol": round(tol, 5), "ok": ok}), flush=True)
-    for (M, N, K, ks) in [(512, 512, 1024, 4), (256, 768, 512, 2)]:
-        err, tol = check(M, N, K, True, False, "f32acc", ksplit=ks, gen=gen)
+    for (M, N, K, ks, kind) in [(512, 512, 1024, 4, "f32acc"), (256, 768, 512, 2, "f32acc"),
+                                (512, 256, 1024, 4, "bf16acc")]:
+        err, tol = check(M, N, K, True, False, kind, ksplit=ks, gen=gen)
         fails += err > tol
         print(json.dumps({"M": M, "N": N, "K": K, "ksplit": ks, "err": err, "ok": err <= tol}), flush=True)
+    fails += fused(gen)
     print("FAILS", fails)
+    return fails
+
+
+def fused(gen):
+    from paddle_infer_amd.ops.gemm import asm_gemm, _act_grad_ref
+    from paddle_infer_amd.ops.activation import _ref_act, ACTS
+    fails = 0
+    for (M, N, K) in [(256, 256, 128), (512, 1024, 256), (304, 520, 192)]:
+        a = torch.randn(M, K, device="cuda", generator=gen).bfloat16()
+        b = (0.1 * torch.randn(N, K, device="cuda", generator=gen)).bfloat16()
+        bias = torch.randn(N, device="cuda", generator=gen).bfloat16()
+        r = a.float() @ b.float().t()
+        for act in ("none", "gelu_tanh", "relu"):
+            aux = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            c = asm_gemm(a, b, trans_b=True, epi="bias_act", act=act, bias=bias, aux=aux)
+            pre = (r + bias.float()).bfloat16()
+            ref_c = _ref_act(pre.float(), ACTS[act])
+            e1 = (aux.float() - pre.float()).abs().max().item()
+            e2 = (c.float() - ref_c).abs().max().item()
+            ok = e1 <= 0.02 * pre.float().abs().max().item() and e2 <= 0.02 * ref_c.abs().max().item() + 1e-2
+            fails += not ok
+            print(json.dumps({"fused": "bias_act", "act": act, "M": M, "N": N, "K": K,
+                              "aux_err": round(e1, 4), "c_err": round(e2, 4), "ok": ok}), flush=True)
+            if act == "none":
+                continue
+            h = torch.randn(M, N, device="cuda", generator=gen).bfloat16()
+            d = asm_gemm(a, b, trans_b=True, epi="dact", act=act, aux=h)
+            ref_d = r * _act_grad_ref(h, ACTS[act])
+            e3 = (d.float() - ref_d).abs().max().item()
+            ok = e3 <= 0.02 * ref_d.abs().max().item() + 1e-2
+            fails += not ok
+            print(json.dumps({"fused": "dact", "act": act, "M": M, "N": N, "K": K,
+                              "err": round(e3, 4), "ok": ok}), flush=True)
+    # bias without aux
+    a = torch.randn(256, 128, device="cuda", generator=gen).bfloat16()
+    b = torch.randn(256, 128, device="cuda", generator=gen).bfloat16()
+    c = asm_gemm(a, b, trans_b=True, epi="bias_act", act="gelu_tanh", bias=None, aux=None)
+    ref_c = _ref_act((a.float() @ b.float().t()).bfloat16().float(), 1)
+    e = (c.float() - ref_c).abs().max().item()
+    fails += e > 0.02 * ref_c.abs().max().item() + 1e-2
+    print(json.dumps({"fused": "act_noaux_nobias", "err": e}), flush=True)
     return fails
 
 

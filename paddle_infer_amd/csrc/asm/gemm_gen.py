@@ -48,9 +48,12 @@ linear and their gradients), `paddle/fluid/operators/fused/fused_gemm_epilogue_o
 """
 from __future__ import annotations
 
+import os
 import sys
 
 TILE, BK, NW = 256, 64, 4
+# ablation builds for measurement only (tools/agemm_ablate.py): nodma / noreads / nomfma / nobar
+ABL = set(filter(None, os.environ.get("PIAMD_AGEMM_ABL", "").split(",")))
 LDS_BYTES = 2 * 2 * 256 * BK * 2  # 2 stages × (A + B) × 256 × 64 × bf16 = 128 KiB
 STAGE_BYTES = 65536
 OP_BYTES = 32768
@@ -102,7 +105,8 @@ V_FRAG = 48                        # X: A v48..79, B v80..111; Y: A v112..143, B
 # one-tile kernel, set Y + v176.. for the persistent kernel whose set X already holds the next
 # tile's first fragments): +0..7 offsets, +8..39 values, +40..55 aux / old C, +56..71 bias,
 # +72..76 temps (+76 even: a 64-bit pair), +80..82 constants
-E_BIAS, E_TMP, E_CONST = 56, 72, 80
+# +84..87 paired-store offsets, +88..91 the aux pair being assembled
+E_BIAS, E_TMP, E_CONST, E_PAIR, E_AUXP = 56, 72, 80, 84, 88
 ACC_OFF = 224                      # AGPRs follow the VGPRs in the unified file
 NVGPR = ACC_OFF + 256
 
@@ -181,6 +185,14 @@ class Kernel:
         self.nlab = 0
 
     def e(self, s):
+        if ABL:
+            m = s.split(" ", 1)[0]
+            if (("nodma" in ABL and m == "buffer_load_dwordx4" and s.endswith(" lds"))
+                    or ("noreads" in ABL and m.startswith("ds_read"))
+                    or ("nobar" in ABL and m == "s_barrier")):
+                return
+            if "nomfma" in ABL and m.startswith("v_mfma"):
+                s = "s_nop 0"
         self.lines.append("\t" + s)
 
     def lab(self, s):
@@ -279,15 +291,16 @@ class Kernel:
         self.e(f"s_lshl_b32 s{m0}, s{m0}, 8")
         self.e(f"s_lshl_b32 s{n0}, s{n0}, 8")
 
-    def setup_tile(self, m0, n0, part):
-        """Descriptors and DMA offsets of both operands for the tile at (m0, n0, part)."""
+    def setup_tile(self, m0, n0, part, full=True):
+        """Descriptors and DMA offsets of both operands for the tile at (m0, n0, part); ``full``
+        also sets the tile-invariant LDS bases, soffsets and fragment-read bases."""
         T = S_T
         self.e(f"s_mul_i32 s{T}, s{part}, s{S_NK}")
         self.e(f"s_lshl_b32 s{T}, s{T}, 6")                      # K start (elements)
         for op in (0, 1):
-            self.setup_operand(op, T, m0 if op == 0 else n0)
+            self.setup_operand(op, T, m0 if op == 0 else n0, full)
 
-    def setup_operand(self, op, T, t0):
+    def setup_operand(self, op, T, t0, full=True):
         """Descriptor, K step, DMA voffsets, LDS-DMA bases and read bases of operand op; t0: SGPR
         with the tile origin along this operand's rows (A: m0, B: n0); s{T}: K start."""
         kc = self.a_kc if op == 0 else self.b_kc
@@ -331,9 +344,10 @@ class Kernel:
         self.e(f"s_mov_b32 s{srd + 3}, 0x20000")
         # LDS-DMA bases of this wave (stage 0 / 1)
         per_wave = 1024 if kc else 8192
-        self.e(f"s_mul_i32 s{T + 3}, s{S_WAVE}, {per_wave}")
-        self.e(f"s_add_u32 s{ldsb}, s{T + 3}, {opoff}")
-        self.e(f"s_add_u32 s{ldsb + 1}, s{T + 3}, {opoff + STAGE_BYTES}")
+        if full:
+            self.e(f"s_mul_i32 s{T + 3}, s{S_WAVE}, {per_wave}")
+            self.e(f"s_add_u32 s{ldsb}, s{T + 3}, {opoff}")
+            self.e(f"s_add_u32 s{ldsb + 1}, s{T + 3}, {opoff + STAGE_BYTES}")
         V, L = V_T, V_LANE
         if kc:
             # g16 = ((L&7) ^ ((4w + (L>>4)) & 7)) * 16 ; rows 32i + 8w + (L>>3) clamped to lim-1-t0
@@ -353,6 +367,8 @@ class Kernel:
                 self.e(f"v_add_u32 v{V + 2}, {32 * i}, v{V + 1}")
                 self.e(f"v_min_u32 v{V + 2}, s{T + 4}, v{V + 2}")
                 self.e(f"v_mad_u32_u24 v{vd + i}, v{V + 2}, s{ld}, v{V}")
+            if not full:
+                return
             # read bases [stage][h]
             WO = 128  # rows per wave half; wave offset = 128 * (wr or wc)
             sel = "wr" if op == 0 else "wc"
@@ -391,6 +407,8 @@ class Kernel:
                 self.e(f"v_min_u32 v{V + 4}, s{T + 4}, v{V + 4}")
                 self.e(f"v_lshlrev_b32 v{V + 4}, 1, v{V + 4}")
                 self.e(f"v_mad_u32_u24 v{vd + par}, v{V + 3}, s{ld}, v{V + 4}")
+            if not full:
+                return
             for i in range(8):
                 self.e(f"s_mul_i32 s{soff + i}, s{ld}, {8 * i}")
             # read bases [stage][bq]: WO*128 + (8g+q)*128 + ((bq ^ f)*32) + 8p
@@ -486,7 +504,7 @@ class Kernel:
     # MFMAs instead of being bunched.
     Y_END, BAR1, DMA0, DMA_GAP, BAR2, X0, X_END = 22, 24, 26, 4, 92, 93, 115
 
-    def iteration(self, stage, dma, read_next, first=False):
+    def iteration(self, stage, dma, read_next, first=False, vm_extra=0):
         ysl, dsl, xsl = {}, {}, {}
         yreads = self.read_ops(1, stage, 1)
         for r, op in enumerate(yreads):
@@ -508,7 +526,7 @@ class Kernel:
                 if dma:
                     self.e("s_barrier")
             if k == self.BAR2 and read_next:
-                self.e(f"s_waitcnt vmcnt({16 if dma else 0})")
+                self.e(f"s_waitcnt vmcnt({min(63, 16 + vm_extra) if dma else vm_extra})")
                 self.e("s_barrier")
             kk = k % 64
             self.mfma(k // 64, kk // 8, kk % 8, zero=first and k < 64)
@@ -600,8 +618,14 @@ class Kernel:
         self.setup_tile(S_M0T, S_N0T, S_PART)
         self.prime()
         ltile, lbeg, lpend = self.newlab("tile"), self.newlab("loop"), self.newlab("loopend")
-        self.lab(ltile)
+        lsecond = self.newlab("second")
         self.iteration(0, True, True, first=True)
+        self.e(f"s_branch {lsecond}")
+        # later tiles: the previous epilogue's stores are still in flight, older than this
+        # iteration's DMAs — count past them instead of draining them
+        self.lab(ltile)
+        self.iteration(0, True, True, first=True, vm_extra=self.store_count())
+        self.lab(lsecond)
         self.iteration(1, True, True)
         self.e(f"s_lshr_b32 s{S_LOOP}, s{S_NK}, 1")
         self.e(f"s_sub_i32 s{S_LOOP}, s{S_LOOP}, 2")
@@ -623,7 +647,7 @@ class Kernel:
         self.e(f"s_cmp_lt_u32 s{S_NVALID}, s{S_NWG}")
         self.e(f"s_cbranch_scc0 {nonext}")
         self.tile_coords(S_NVALID, S_NM0, S_NN0, S_NPART)
-        self.setup_tile(S_NM0, S_NN0, S_NPART)
+        self.setup_tile(S_NM0, S_NN0, S_NPART, full=False)
         self.e(f"s_mov_b32 s{S_NVALID}, 1")
         self.e(f"s_branch {ready}")
         self.lab(nonext)
@@ -738,6 +762,19 @@ class Kernel:
                 self.e(f"buffer_load_dwordx2 v[{self.VBIAS + 2 * nb}:{self.VBIAS + 2 * nb + 1}], v{V + 7}, s[{b}:{b + 3}], 0 offen offset:{nb * 32}")
             self.e("s_waitcnt vmcnt(0)")
         self.e(f"v_add_u32 v{V + 4}, s{S_N0T}, v{V + 1}")            # global col (nb = 0)
+        if not f32:
+            # paired stores: lane group g (= l>>4) stores 8 columns at (g&1)·16 + (g>>1)·8
+            self.e(f"v_lshrrev_b32 v{V + 7}, 4, v{L}")
+            self.e(f"v_and_b32 v{V + E_PAIR + 2}, 1, v{V + 7}")
+            self.e(f"v_lshrrev_b32 v{V + 7}, 1, v{V + 7}")
+            self.e(f"v_lshlrev_b32 v{V + 7}, 3, v{V + 7}")
+            self.e(f"v_lshl_add_u32 v{V + 7}, v{V + E_PAIR + 2}, 4, v{V + 7}")
+            self.e(f"v_add_u32 v{V + 7}, s{T + 5}, v{V + 7}")          # paired local col
+            self.e(f"v_mul_lo_u32 v{V + E_PAIR}, v{V}, s{E + 4}")
+            self.e(f"v_lshl_add_u32 v{V + E_PAIR}, v{V + 7}, 1, v{V + E_PAIR}")
+            if ek == "bias_act":
+                self.e(f"v_mul_lo_u32 v{V + E_PAIR + 1}, v{V}, s{E + 5}")
+                self.e(f"v_lshl_add_u32 v{V + E_PAIR + 1}, v{V + 7}, 1, v{V + E_PAIR + 1}")
         # edge tile in N: per-store EXEC masks
         full = self.newlab("full")
         done = self.newlab("done")
@@ -751,18 +788,27 @@ class Kernel:
         self.lab(done)
 
     def store_all(self, masked):
+        """Per 16-row block (mb): convert / fuse / store the 8 accumulator blocks of the row.
+        Full tiles pair blocks (nb, nb+1) with v_permlane16_swap so every lane stores 16 B
+        (bf16: half the store instructions; the store tail is issue-bound, MI355X_MICROARCH.md);
+        edge tiles store 8 B per block under per-block EXEC masks."""
         E, V, T = S_E, self.VE, S_T
         ek = self.ek
         srd = S_CSRD
         es = 4 if ek in ("f32", "f32acc") else 2
+        paired = not masked and es == 2
         W = V + 8          # working registers
         for mb in range(8):
             # row voffset for this mb
             self.e(f"s_mul_i32 s{T + 7}, s{E + 4}, {16 * mb}")
             self.e(f"v_add_u32 v{V + 5}, s{T + 7}, v{V + 2}")
+            if paired:
+                self.e(f"v_add_u32 v{V + E_PAIR + 2}, s{T + 7}, v{V + E_PAIR}")
             if ek in ("bias_act", "dact"):
                 self.e(f"s_mul_i32 s{T + 8}, s{E + 5}, {16 * mb}")
                 self.e(f"v_add_u32 v{V + 6}, s{T + 8}, v{V + 3}")
+                if paired:
+                    self.e(f"v_add_u32 v{V + E_PAIR + 3}, s{T + 8}, v{V + E_PAIR + 1}")
             if ek == "f32acc":
                 for nb in range(8):
                     d = W + 4 * nb
@@ -794,18 +840,39 @@ class Kernel:
                     self.e(f"buffer_store_dwordx4 v[{d}:{d + 3}], v{V + 5}, s[{srd}:{srd + 3}], 0 offen offset:{nb * 64}")
                 else:
                     if ek == "bias_act":
-                        self.bias_act_vals(d, nb, mb)
+                        self.bias_act_vals(d, nb, mb, paired)
                     elif ek == "dact":
                         self.dact_vals(d, W + 32 + 2 * nb)
                     elif ek == "bf16acc":
                         for j in range(4):
                             self.unpack(self.VTMP, W + 32 + 2 * nb + j // 2, j)
                             self.e(f"v_add_f32 v{d + j}, v{self.VTMP}, v{d + j}")
-                    self.e(f"v_cvt_pk_bf16_f32 v{d}, v{d}, v{d + 1}")
-                    self.e(f"v_cvt_pk_bf16_f32 v{d + 1}, v{d + 2}, v{d + 3}")
-                    self.e(f"buffer_store_dwordx2 v[{d}:{d + 1}], v{V + 5}, s[{srd}:{srd + 3}], 0 offen offset:{nb * 32}")
+                    if not paired:
+                        self.e(f"v_cvt_pk_bf16_f32 v{d}, v{d}, v{d + 1}")
+                        self.e(f"v_cvt_pk_bf16_f32 v{d + 1}, v{d + 2}, v{d + 3}")
+                        self.e(f"buffer_store_dwordx2 v[{d}:{d + 1}], v{V + 5}, s[{srd}:{srd + 3}], 0 offen offset:{nb * 32}")
+                    elif nb % 2 == 1:
+                        # blocks nb-1 (in d-4..d-1) and nb (d..d+3) → packed pair q..q+3, swap
+                        q = d - 4
+                        self.e(f"v_cvt_pk_bf16_f32 v{q}, v{q}, v{q + 1}")
+                        self.e(f"v_cvt_pk_bf16_f32 v{q + 1}, v{q + 2}, v{q + 3}")
+                        self.e(f"v_cvt_pk_bf16_f32 v{q + 2}, v{d}, v{d + 1}")
+                        self.e(f"v_cvt_pk_bf16_f32 v{q + 3}, v{d + 2}, v{d + 3}")
+                        self.e("s_nop 1")
+                        self.e(f"v_permlane16_swap_b32 v{q}, v{q + 2}")
+                        self.e(f"v_permlane16_swap_b32 v{q + 1}, v{q + 3}")
+                        self.e(f"buffer_store_dwordx4 v[{q}:{q + 3}], v{V + E_PAIR + 2}, s[{srd}:{srd + 3}], 0 offen offset:{(nb - 1) * 32}")
                 if masked:
                     self.e("s_mov_b64 exec, -1")
+
+    def store_count(self):
+        """VMEM stores the full-tile epilogue leaves outstanding at its end (the next tile's first
+        block-landed wait counts past them); 0 when the epilogue itself drains (it loads)."""
+        if self.ek in ("f32acc", "bf16acc", "dact"):
+            return 0
+        if self.ek == "f32":
+            return 64
+        return 64 if self.ek == "bias_act" else 32
 
     # -- fused activation epilogues -----------------------------------------------------------------
     def trans(self, op):
@@ -851,23 +918,31 @@ class Kernel:
         else:
             self.e(f"v_and_b32 v{dst}, 0xffff0000, v{src}")
 
-    def bias_act_vals(self, d, nb, mb):
+    def bias_act_vals(self, d, nb, mb, paired=False):
         """pre = bf16(acc + bias) → aux; d ← act(pre) (f32, rounded to bf16 by the caller)."""
-        t, p = self.VTMP + 2, self.VTMP + 4
+        t = self.VTMP + 2
+        p = self.VE + E_AUXP + 2 * (nb % 2) if paired else self.VTMP + 4
         for j in range(4):
             self.unpack(t, self.VBIAS + 2 * nb + j // 2, j)
             self.e(f"v_add_f32 v{d + j}, v{t}, v{d + j}")
         self.e(f"v_cvt_pk_bf16_f32 v{p}, v{d}, v{d + 1}")
         self.e(f"v_cvt_pk_bf16_f32 v{p + 1}, v{d + 2}, v{d + 3}")
-        self.e(f"buffer_store_dwordx2 v[{p}:{p + 1}], v{self.VE + 6}, s[{S_AUXSRD}:{S_AUXSRD + 3}], 0 offen offset:{nb * 32}")
-        if self.act == 0:
-            return
-        for j in range(4):
-            self.unpack(d + j, p + j // 2, j)
-            if self.act == 1:
-                self.gelu(d + j)
-            else:
-                self.e(f"v_max_f32 v{d + j}, 0, v{d + j}")
+        if not paired:
+            self.e(f"buffer_store_dwordx2 v[{p}:{p + 1}], v{self.VE + 6}, s[{S_AUXSRD}:{S_AUXSRD + 3}], 0 offen offset:{nb * 32}")
+        if self.act != 0:
+            for j in range(4):
+                self.unpack(d + j, p + j // 2, j)
+                if self.act == 1:
+                    self.gelu(d + j)
+                else:
+                    self.e(f"v_max_f32 v{d + j}, 0, v{d + j}")
+        if paired and nb % 2 == 1:
+            q = self.VE + E_AUXP
+            self.e("s_nop 1")
+            self.e(f"v_permlane16_swap_b32 v{q}, v{q + 2}")
+            self.e(f"v_permlane16_swap_b32 v{q + 1}, v{q + 3}")
+            self.e(f"buffer_store_dwordx4 v[{q}:{q + 3}], v{self.VE + E_PAIR + 3}, s[{S_AUXSRD}:{S_AUXSRD + 3}], 0 offen offset:{(nb - 1) * 32}")
+        return
 
     def dact_vals(self, d, auxreg):
         h = self.VTMP + 2

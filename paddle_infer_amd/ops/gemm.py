@@ -72,7 +72,7 @@ def _agemm_load():
         return
     import os
     from .. import _build
-    path = _build.AGEMM_HSACO
+    path = os.environ.get("PIAMD_AGEMM_HSACO") or _build.AGEMM_HSACO  # ablation builds (tools/)
     if not os.path.exists(path):
         raise RuntimeError(f"assembly GEMM code object missing ({path}); run "
                            "`python -m paddle_infer_amd._build`")

@@ -171,6 +171,32 @@ def bench(T, rounds, shapes):
         torch.cuda.empty_cache()
 
 
+def probe(rounds):
+    """Loop efficiency vs per-tile overhead: long-K (few tiles, many K-blocks) and short-K
+    (many tiles) products in both layouts, one line per case (asm only; hipBLASLt alongside)."""
+    from paddle_infer_amd.ops.gemm import asm_gemm
+    gen = torch.Generator(device="cuda").manual_seed(0)
+    cases = [("nt_longK", 4096, 4096, 32768, False, True), ("tn_longK", 4096, 4096, 32768, True, False),
+             ("nt_ffn1", 98304, 8192, 2048, False, True), ("nt_ffn2", 98304, 2048, 8192, False, True)]
+    for name, M, N, K, ta, tb in cases:
+        a = torch.randn((K, M) if ta else (M, K), device="cuda", generator=gen).bfloat16()
+        b = torch.randn((N, K) if tb else (K, N), device="cuda", generator=gen).bfloat16()
+        c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        A = a.t() if ta else a
+        B = b.t() if tb else b
+        fns = {"asm": lambda: asm_gemm(a, b, ta, tb, out=c), "hipblaslt": lambda: torch.mm(A, B)}
+        for f in fns.values():
+            f()
+        torch.cuda.synchronize()
+        ts = {k: [] for k in fns}
+        for _ in range(rounds):
+            for k, f in fns.items():
+                ts[k].append(timeit(f, 3))
+        fl = 2.0 * M * N * K
+        print(json.dumps({"case": name, **{k: round(fl / statistics.median(v) / 1e9, 1) for k, v in ts.items()},
+                          "hsaco": os.path.basename(os.environ.get("PIAMD_AGEMM_HSACO", "default"))}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--stage", default="small")
@@ -181,6 +207,9 @@ def main():
     import paddle_infer_amd  # noqa: F401
     if args.stage == "small":
         sys.exit(1 if small() else 0)
+    if args.stage == "probe":
+        probe(args.rounds)
+        return
     bench(args.T, args.rounds, args.shapes.split(","))
 
 

@@ -105,8 +105,10 @@ V_FRAG = 48                        # X: A v48..79, B v80..111; Y: A v112..143, B
 # one-tile kernel, set Y + v176.. for the persistent kernel whose set X already holds the next
 # tile's first fragments): +0..7 offsets, +8..39 values, +40..55 aux / old C, +56..71 bias,
 # +72..76 temps (+76 even: a 64-bit pair), +80..82 constants
-# +84..87 paired-store offsets, +88..91 the aux pair being assembled
-E_BIAS, E_TMP, E_CONST, E_PAIR, E_AUXP = 56, 72, 80, 84, 88
+# +84..87 paired-store offsets, +88..91 the aux pair being assembled, +92..101 constant pairs
+# (packed f32 math); loads of old C / aux double-buffer in +40..55 / +56..71 (+40..71 / +72..103
+# for f32 C)
+E_BIAS, E_TMP, E_CONST, E_PAIR, E_AUXP = 56, 72, 92, 84, 88
 ACC_OFF = 224                      # AGPRs follow the VGPRs in the unified file
 NVGPR = ACC_OFF + 256
 
@@ -742,8 +744,9 @@ class Kernel:
         if ek in ("bias_act", "dact"):
             self.e(f"v_mul_lo_u32 v{V + 3}, v{V}, s{E + 5}")
             self.e(f"v_lshl_add_u32 v{V + 3}, v{V + 1}, 1, v{V + 3}")  # aux voffset
-            for r, val in ((self.VCONST, K0), (self.VCONST + 1, K0 * K1), (self.VCONST + 2, 3 * K0 * K1)):
-                self.e(f"v_mov_b32 v{r}, {fhex(val)}")
+            for i, val in enumerate((K0, K0 * K1, 3 * K0 * K1, TWO_LOG2E, 1.0)):
+                self.e(f"v_mov_b32 v{self.VCONST + 2 * i}, {fhex(val)}")
+                self.e(f"v_mov_b32 v{self.VCONST + 2 * i + 1}, {fhex(val)}")
         if ek == "bias_act":
             # bias descriptor (records 0 when there is no bias: loads return 0)
             b = S_BIASSRD
@@ -782,75 +785,105 @@ class Kernel:
         self.e(f"s_cmp_le_u32 s{T + 6}, s{S_N}")
         self.e(f"s_cbranch_scc1 {full}")
         self.store_all(masked=True)
+        # EXEC-masked stores may be skipped outright (no lanes): the counted wait of the next
+        # tile cannot rely on them, so an edge tile drains its stores here
+        self.e("s_waitcnt vmcnt(0)")
         self.e(f"s_branch {done}")
         self.lab(full)
         self.store_all(masked=False)
         self.lab(done)
 
+    def load_group(self, mb, buf):
+        """Issue the epilogue loads of row block mb (old C for accumulate, aux for dact) into
+        buffer `buf`; returns the VMEM instruction count."""
+        V, E, T, srd = self.VE, S_E, S_T, S_CSRD
+        ek = self.ek
+        if ek not in ("f32acc", "bf16acc", "dact"):
+            return 0
+        # row offset of block mb in a temp (the loop's own offsets are per mb)
+        if ek == "dact":
+            self.e(f"s_mul_i32 s{T + 8}, s{E + 5}, {16 * mb}")
+            self.e(f"v_add_u32 v{V + 7}, s{T + 8}, v{V + 3}")
+        else:
+            self.e(f"s_mul_i32 s{T + 8}, s{E + 4}, {16 * mb}")
+            self.e(f"v_add_u32 v{V + 7}, s{T + 8}, v{V + 2}")
+        for nb in range(8):
+            if ek == "f32acc":
+                d = V + 40 + 32 * buf + 4 * nb
+                self.e(f"buffer_load_dwordx4 v[{d}:{d + 3}], v{V + 7}, s[{srd}:{srd + 3}], 0 offen offset:{nb * 64}")
+            else:
+                d = V + 40 + 16 * buf + 2 * nb
+                rs = S_AUXSRD if ek == "dact" else srd
+                self.e(f"buffer_load_dwordx2 v[{d}:{d + 1}], v{V + 7}, s[{rs}:{rs + 3}], 0 offen offset:{nb * 32}")
+        return 8
+
     def store_all(self, masked):
         """Per 16-row block (mb): convert / fuse / store the 8 accumulator blocks of the row.
         Full tiles pair blocks (nb, nb+1) with v_permlane16_swap so every lane stores 16 B
         (bf16: half the store instructions; the store tail is issue-bound, MI355X_MICROARCH.md);
-        edge tiles store 8 B per block under per-block EXEC masks."""
+        edge tiles store 8 B per block under per-block EXEC masks. Loads (old C, aux) of block
+        mb+1 are in flight while block mb is processed; waits are counted exactly."""
         E, V, T = S_E, self.VE, S_T
         ek = self.ek
         srd = S_CSRD
         es = 4 if ek in ("f32", "f32acc") else 2
         paired = not masked and es == 2
         W = V + 8          # working registers
+        has_loads = ek in ("f32acc", "bf16acc", "dact")
+        issued = []        # VMEM ops in issue order: ("L", mb) loads / ("S", mb) stores
+        if has_loads:
+            issued += [("L", 0)] * self.load_group(0, 0)
         for mb in range(8):
+            if has_loads and mb < 7:
+                issued += [("L", mb + 1)] * self.load_group(mb + 1, (mb + 1) % 2)
+            if has_loads:
+                last = max(i for i, t in enumerate(issued) if t == ("L", mb))
+                self.e(f"s_waitcnt vmcnt({min(63, len(issued) - 1 - last)})")
+            buf = mb % 2
             # row voffset for this mb
             self.e(f"s_mul_i32 s{T + 7}, s{E + 4}, {16 * mb}")
             self.e(f"v_add_u32 v{V + 5}, s{T + 7}, v{V + 2}")
             if paired:
                 self.e(f"v_add_u32 v{V + E_PAIR + 2}, s{T + 7}, v{V + E_PAIR}")
-            if ek in ("bias_act", "dact"):
+            if ek == "bias_act":
                 self.e(f"s_mul_i32 s{T + 8}, s{E + 5}, {16 * mb}")
                 self.e(f"v_add_u32 v{V + 6}, s{T + 8}, v{V + 3}")
                 if paired:
                     self.e(f"v_add_u32 v{V + E_PAIR + 3}, s{T + 8}, v{V + E_PAIR + 1}")
-            if ek == "f32acc":
-                for nb in range(8):
-                    d = W + 4 * nb
-                    self.e(f"buffer_load_dwordx4 v[{d}:{d + 3}], v{V + 5}, s[{srd}:{srd + 3}], 0 offen offset:{nb * 64}")
-                self.e("s_waitcnt vmcnt(0)")
-            if ek == "dact":
-                for nb in range(8):
-                    d = W + 32 + 2 * nb
-                    self.e(f"buffer_load_dwordx2 v[{d}:{d + 1}], v{V + 6}, s[{S_AUXSRD}:{S_AUXSRD + 3}], 0 offen offset:{nb * 32}")
-                self.e("s_waitcnt vmcnt(0)")
-            if ek == "bf16acc":
-                for nb in range(8):
-                    d = W + 32 + 2 * nb
-                    self.e(f"buffer_load_dwordx2 v[{d}:{d + 1}], v{V + 5}, s[{srd}:{srd + 3}], 0 offen offset:{nb * 32}")
-                self.e("s_waitcnt vmcnt(0)")
             for nb in range(8):
                 c = acc(mb, nb)
                 d = W + 4 * nb
                 for j in range(4):
-                    self.e(f"v_accvgpr_read_b32 v{d + j if ek != 'f32acc' else V + 44 + j}, a{c + j}")
+                    self.e(f"v_accvgpr_read_b32 v{d + j}, a{c + j}")
                 if ek == "f32acc":
-                    for j in range(4):
-                        self.e(f"v_add_f32 v{d + j}, v{V + 44 + j}, v{d + j}")
+                    o = V + 40 + 32 * buf + 4 * nb
+                    self.e(f"v_pk_add_f32 v[{d}:{d + 1}], v[{o}:{o + 1}], v[{d}:{d + 1}]")
+                    self.e(f"v_pk_add_f32 v[{d + 2}:{d + 3}], v[{o + 2}:{o + 3}], v[{d + 2}:{d + 3}]")
                 if masked:
                     self.e(f"v_add_u32 v{V + 7}, {nb * 16}, v{V + 4}")
                     self.e(f"v_cmp_gt_u32 vcc, s{S_N}, v{V + 7}")
                     self.e(f"s_and_saveexec_b64 s[{T + 8}:{T + 9}], vcc")
                 if es == 4:
                     self.e(f"buffer_store_dwordx4 v[{d}:{d + 3}], v{V + 5}, s[{srd}:{srd + 3}], 0 offen offset:{nb * 64}")
+                    issued.append(("S", mb))
                 else:
                     if ek == "bias_act":
-                        self.bias_act_vals(d, nb, mb, paired)
+                        n_st = self.bias_act_vals(d, nb, mb, paired)
+                        issued += [("S", mb)] * n_st
                     elif ek == "dact":
-                        self.dact_vals(d, W + 32 + 2 * nb)
+                        self.dact_vals(d, V + 40 + 16 * buf + 2 * nb)
                     elif ek == "bf16acc":
-                        for j in range(4):
-                            self.unpack(self.VTMP, W + 32 + 2 * nb + j // 2, j)
-                            self.e(f"v_add_f32 v{d + j}, v{self.VTMP}, v{d + j}")
+                        o = V + 40 + 16 * buf + 2 * nb
+                        t = self.VTMP + 4
+                        for j in (0, 2):
+                            self.unpack(t, o + j // 2, 0)
+                            self.unpack(t + 1, o + j // 2, 1)
+                            self.e(f"v_pk_add_f32 v[{d + j}:{d + j + 1}], v[{t}:{t + 1}], v[{d + j}:{d + j + 1}]")
                     if not paired:
                         self.e(f"v_cvt_pk_bf16_f32 v{d}, v{d}, v{d + 1}")
                         self.e(f"v_cvt_pk_bf16_f32 v{d + 1}, v{d + 2}, v{d + 3}")
                         self.e(f"buffer_store_dwordx2 v[{d}:{d + 1}], v{V + 5}, s[{srd}:{srd + 3}], 0 offen offset:{nb * 32}")
+                        issued.append(("S", mb))
                     elif nb % 2 == 1:
                         # blocks nb-1 (in d-4..d-1) and nb (d..d+3) → packed pair q..q+3, swap
                         q = d - 4
@@ -862,17 +895,21 @@ class Kernel:
                         self.e(f"v_permlane16_swap_b32 v{q}, v{q + 2}")
                         self.e(f"v_permlane16_swap_b32 v{q + 1}, v{q + 3}")
                         self.e(f"buffer_store_dwordx4 v[{q}:{q + 3}], v{V + E_PAIR + 2}, s[{srd}:{srd + 3}], 0 offen offset:{(nb - 1) * 32}")
+                        issued.append(("S", mb))
                 if masked:
                     self.e("s_mov_b64 exec, -1")
+        self.vm_ops = min(getattr(self, "vm_ops", 10 ** 6), len(issued))
 
     def store_count(self):
-        """VMEM stores the full-tile epilogue leaves outstanding at its end (the next tile's first
-        block-landed wait counts past them); 0 when the epilogue itself drains (it loads)."""
-        if self.ek in ("f32acc", "bf16acc", "dact"):
-            return 0
-        if self.ek == "f32":
-            return 64
-        return 64 if self.ek == "bias_act" else 32
+        """VMEM ops the epilogue issues on its shorter path (the next tile's first block-landed
+        wait counts past them: they are all younger than the DMAs of the next tile's blocks 0
+        and 1). Found by generating the epilogue once into a scratch buffer."""
+        if not hasattr(self, "vm_ops"):
+            saved = self.lines
+            self.lines = []
+            self.epilogue()
+            self.lines = saved
+        return self.vm_ops
 
     # -- fused activation epilogues -----------------------------------------------------------------
     def trans(self, op):
@@ -880,37 +917,47 @@ class Kernel:
         self.e(op)
         self.e("s_nop 0")
 
-    def gelu(self, x):
-        """x ← gelu_tanh(x) = x·(1 − r), r = 1 / (exp(2u) + 1), u = k0·(x + k1·x³)."""
-        ta = self.VTMP
-        c0, c1 = self.VCONST, self.VCONST + 1
-        self.e(f"v_mul_f32 v{ta}, v{x}, v{x}")
-        self.e(f"v_fma_f32 v{ta}, v{ta}, v{c1}, v{c0}")
-        self.e(f"v_mul_f32 v{ta}, v{ta}, v{x}")
-        self.e(f"v_mul_f32 v{ta}, {fhex(TWO_LOG2E)}, v{ta}")
-        self.trans(f"v_exp_f32 v{ta}, v{ta}")
-        self.e(f"v_add_f32 v{ta}, 1.0, v{ta}")
-        self.trans(f"v_rcp_f32 v{ta}, v{ta}")
-        self.e(f"v_fma_f32 v{x}, -v{x}, v{ta}, v{x}")
+    def cpair(self, i):
+        """Constant pair i: 0 k0, 1 k0·k1, 2 3·k0·k1, 3 2·log2(e), 4 1.0."""
+        c = self.VCONST + 2 * i
+        return f"v[{c}:{c + 1}]"
 
-    def gelu_grad_mul(self, y, h):
-        """y ← y · gelu_tanh'(h) = y · (1−r)(1 + 2h·r·(k0 + 3k0k1·h²))."""
-        ta, tb = self.VTMP, self.VTMP + 1
-        c0, c1, c3 = self.VCONST, self.VCONST + 1, self.VCONST + 2
-        self.e(f"v_mul_f32 v{ta}, v{h}, v{h}")
-        self.e(f"v_fma_f32 v{tb}, v{ta}, v{c1}, v{c0}")
-        self.e(f"v_fma_f32 v{ta}, v{ta}, v{c3}, v{c0}")
-        self.e(f"v_mul_f32 v{tb}, v{tb}, v{h}")
-        self.e(f"v_mul_f32 v{tb}, {fhex(TWO_LOG2E)}, v{tb}")
-        self.trans(f"v_exp_f32 v{tb}, v{tb}")
-        self.e(f"v_add_f32 v{tb}, 1.0, v{tb}")
-        self.trans(f"v_rcp_f32 v{tb}, v{tb}")
-        self.e(f"v_mul_f32 v{ta}, v{ta}, v{h}")
-        self.e(f"v_mul_f32 v{ta}, v{ta}, v{tb}")
-        self.e(f"v_sub_f32 v{tb}, 1.0, v{tb}")
-        self.e(f"v_add_f32 v{ta}, v{ta}, v{ta}")
-        self.e(f"v_fma_f32 v{ta}, v{ta}, v{tb}, v{tb}")
-        self.e(f"v_mul_f32 v{y}, v{y}, v{ta}")
+    def gelu2(self, x):
+        """v[x:x+1] ← gelu_tanh (packed f32): x·(1 − r), r = 1 / (exp(2u) + 1), u = k0·(x + k1·x³)."""
+        t = self.VTMP
+        X, Tp = f"v[{x}:{x + 1}]", f"v[{t}:{t + 1}]"
+        self.e(f"v_pk_mul_f32 {Tp}, {X}, {X}")
+        self.e(f"v_pk_fma_f32 {Tp}, {Tp}, {self.cpair(1)}, {self.cpair(0)}")
+        self.e(f"v_pk_mul_f32 {Tp}, {Tp}, {X}")
+        self.e(f"v_pk_mul_f32 {Tp}, {Tp}, {self.cpair(3)}")
+        self.e(f"v_exp_f32 v{t}, v{t}")
+        self.trans(f"v_exp_f32 v{t + 1}, v{t + 1}")
+        self.e(f"v_pk_add_f32 {Tp}, {Tp}, {self.cpair(4)}")
+        self.e(f"v_rcp_f32 v{t}, v{t}")
+        self.trans(f"v_rcp_f32 v{t + 1}, v{t + 1}")
+        self.e(f"v_pk_fma_f32 {X}, {X}, {Tp}, {X} neg_lo:[1,0,0] neg_hi:[1,0,0]")
+
+    def gelu_grad_mul2(self, y, h):
+        """v[y:y+1] ← y · gelu_tanh'(h) (packed): (1−r)(1 + 2h·r·(k0 + 3k0k1·h²))."""
+        ta, tb = self.VTMP, self.VTMP + 2
+        Y, H = f"v[{y}:{y + 1}]", f"v[{h}:{h + 1}]"
+        A, B = f"v[{ta}:{ta + 1}]", f"v[{tb}:{tb + 1}]"
+        self.e(f"v_pk_mul_f32 {A}, {H}, {H}")
+        self.e(f"v_pk_fma_f32 {B}, {A}, {self.cpair(1)}, {self.cpair(0)}")
+        self.e(f"v_pk_fma_f32 {A}, {A}, {self.cpair(2)}, {self.cpair(0)}")
+        self.e(f"v_pk_mul_f32 {B}, {B}, {H}")
+        self.e(f"v_pk_mul_f32 {B}, {B}, {self.cpair(3)}")
+        self.e(f"v_exp_f32 v{tb}, v{tb}")
+        self.trans(f"v_exp_f32 v{tb + 1}, v{tb + 1}")
+        self.e(f"v_pk_add_f32 {B}, {B}, {self.cpair(4)}")
+        self.e(f"v_rcp_f32 v{tb}, v{tb}")
+        self.trans(f"v_rcp_f32 v{tb + 1}, v{tb + 1}")
+        self.e(f"v_pk_mul_f32 {A}, {A}, {H}")
+        self.e(f"v_pk_mul_f32 {A}, {A}, {B}")
+        self.e(f"v_pk_add_f32 {B}, {self.cpair(4)}, {B} neg_lo:[0,1] neg_hi:[0,1]")
+        self.e(f"v_pk_add_f32 {A}, {A}, {A}")
+        self.e(f"v_pk_fma_f32 {A}, {A}, {B}, {B}")
+        self.e(f"v_pk_mul_f32 {Y}, {Y}, {A}")
 
     def unpack(self, dst, src, j):
         if j % 2 == 0:
@@ -919,40 +966,49 @@ class Kernel:
             self.e(f"v_and_b32 v{dst}, 0xffff0000, v{src}")
 
     def bias_act_vals(self, d, nb, mb, paired=False):
-        """pre = bf16(acc + bias) → aux; d ← act(pre) (f32, rounded to bf16 by the caller)."""
-        t = self.VTMP + 2
-        p = self.VE + E_AUXP + 2 * (nb % 2) if paired else self.VTMP + 4
-        for j in range(4):
-            self.unpack(t, self.VBIAS + 2 * nb + j // 2, j)
-            self.e(f"v_add_f32 v{d + j}, v{t}, v{d + j}")
+        """pre = bf16(acc + bias) → aux; d ← act(pre) (f32, rounded to bf16 by the caller).
+        Returns the number of aux store instructions issued."""
+        t = self.VTMP + 4
+        p = self.VE + E_AUXP + 2 * (nb % 2) if paired else self.VTMP + 6
+        for j in (0, 2):
+            self.unpack(t, self.VBIAS + 2 * nb + j // 2, 0)
+            self.unpack(t + 1, self.VBIAS + 2 * nb + j // 2, 1)
+            self.e(f"v_pk_add_f32 v[{d + j}:{d + j + 1}], v[{t}:{t + 1}], v[{d + j}:{d + j + 1}]")
         self.e(f"v_cvt_pk_bf16_f32 v{p}, v{d}, v{d + 1}")
         self.e(f"v_cvt_pk_bf16_f32 v{p + 1}, v{d + 2}, v{d + 3}")
+        n = 0
         if not paired:
             self.e(f"buffer_store_dwordx2 v[{p}:{p + 1}], v{self.VE + 6}, s[{S_AUXSRD}:{S_AUXSRD + 3}], 0 offen offset:{nb * 32}")
+            n = 1
         if self.act != 0:
             for j in range(4):
                 self.unpack(d + j, p + j // 2, j)
+            for j in (0, 2):
                 if self.act == 1:
-                    self.gelu(d + j)
+                    self.gelu2(d + j)
                 else:
                     self.e(f"v_max_f32 v{d + j}, 0, v{d + j}")
+                    self.e(f"v_max_f32 v{d + j + 1}, 0, v{d + j + 1}")
         if paired and nb % 2 == 1:
             q = self.VE + E_AUXP
             self.e("s_nop 1")
             self.e(f"v_permlane16_swap_b32 v{q}, v{q + 2}")
             self.e(f"v_permlane16_swap_b32 v{q + 1}, v{q + 3}")
             self.e(f"buffer_store_dwordx4 v[{q}:{q + 3}], v{self.VE + E_PAIR + 3}, s[{S_AUXSRD}:{S_AUXSRD + 3}], 0 offen offset:{(nb - 1) * 32}")
-        return
+            n = 1
+        return n
 
     def dact_vals(self, d, auxreg):
-        h = self.VTMP + 2
-        for j in range(4):
-            self.unpack(h, auxreg + j // 2, j)
+        h = self.VTMP + 4
+        for j in (0, 2):
+            self.unpack(h, auxreg + j // 2, 0)
+            self.unpack(h + 1, auxreg + j // 2, 1)
             if self.act == 1:
-                self.gelu_grad_mul(d + j, h)
+                self.gelu_grad_mul2(d + j, h)
             else:
-                self.e(f"v_cmp_lt_f32 vcc, 0, v{h}")
-                self.e(f"v_cndmask_b32 v{d + j}, 0, v{d + j}, vcc")
+                for k in range(2):
+                    self.e(f"v_cmp_lt_f32 vcc, 0, v{h + k}")
+                    self.e(f"v_cndmask_b32 v{d + j + k}, 0, v{d + j + k}, vcc")
 
     # -- text ----------------------------------------------------------------------------------------
     def text(self):

@@ -28,7 +28,8 @@ import torch.nn.functional as F
 from ..nn.layer.base import Layer, LayerList
 from ..nn import initializer as I
 from ..ops import fused_add_layer_norm, flash_attention_packed, bias_act, softmax_cross_entropy
-from ..ops.linear import _use_transposed, mm_nt, transposed, wgrad_into
+from ..ops.linear import (_use_transposed, fused_mlp, fused_mlp_supported, mm_nt, transposed,
+                          wgrad_into)
 from ..ops.linear import linear as _linear
 from ..ops.embedding import embedding as ops_embedding
 from ..distributed.fleet.mp_layers import (ColumnParallelLinear, RowParallelLinear,
@@ -136,6 +137,10 @@ class GPTMLP(Layer):
     def forward(self, y):
         from ..distributed.fleet.mp_layers import mp_allreduce
         x = c_identity(y, self.mp_group)
+        if fused_mlp_supported(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.act):
+            # bias+GELU in the FFN1 GEMM epilogue, GELU backward in the FFN2 dgrad epilogue
+            m = fused_mlp(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.act)
+            return mp_allreduce(m, self.mp_group)
         f = _linear(x, self.fc1.weight, None)
         f = bias_act(f, self.fc1.bias, self.act)
         m = _linear(f, self.fc2.weight, None)

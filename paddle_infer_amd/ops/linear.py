@@ -224,3 +224,82 @@ def linear(x, weight, bias=None):
     if bias is not None and bias.dtype != x2.dtype:
         y = y + bias
     return y.view(*shp[:-1], weight.shape[1])
+
+
+class _FusedMLPFn(torch.autograd.Function):
+    """``m = act(x·W1 + b1)·W2`` with the elementwise work inside the GEMM epilogues (reference
+    ``fused_feedforward`` / ``FusedFeedForward`` and the cublasLt GELU_AUX / DGELU epilogues of
+    `fused_gemm_epilogue_op.cu`):
+
+    * forward — FFN1 GEMM writes ``pre = bf16(x·W1 + b1)`` (saved) AND ``a = act(pre)``;
+    * backward — the FFN2 data-gradient GEMM writes ``d_pre = (dm·W2ᵀ) ⊙ act'(pre)`` directly;
+      ``db1`` is one column-sum pass over ``d_pre``; weight gradients go straight into
+      ``main_grad``. No separate bias+activation kernels in either direction."""
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda")
+    def forward(ctx, x, w1, b1, w2, act):
+        from .gemm import asm_gemm
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1]).contiguous()
+        pre = torch.empty((x2.shape[0], w1.shape[1]), dtype=x2.dtype, device=x2.device)
+        a = asm_gemm(x2, transposed(w1), trans_b=True, epi="bias_act", act=act, bias=b1, aux=pre)
+        m = mm_nt(a, transposed(w2))
+        ctx.save_for_backward(x2, pre, a, w1, b1, w2)
+        ctx.act, ctx.shp = act, shp
+        return m.view(*shp[:-1], w2.shape[1])
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, dm):
+        from .gemm import asm_gemm
+        x2, pre, a, w1, b1, w2 = ctx.saved_tensors
+        dm2 = dm.reshape(-1, w2.shape[1]).contiguous()
+        dpre = asm_gemm(dm2, w2, trans_b=True, epi="dact", act=ctx.act, aux=pre)
+        dw1 = db1 = dw2 = None
+        if ctx.needs_input_grad[3]:
+            mg = getattr(w2, "main_grad", None)
+            if mg is not None:
+                wgrad_into(mg, a, dm2)
+                _fire(w2)
+            else:
+                dw2 = wgrad_into(torch.zeros_like(w2), a, dm2)
+        if ctx.needs_input_grad[2]:
+            bmg = getattr(b1, "main_grad", None)
+            if bmg is not None and bmg.dtype == dpre.dtype:
+                colsum_into(dpre, bmg, accumulate=True)
+                _fire(b1)
+            else:
+                db1 = dpre.float().sum(0).to(b1.dtype)
+        if ctx.needs_input_grad[1]:
+            mg = getattr(w1, "main_grad", None)
+            if mg is not None:
+                wgrad_into(mg, x2, dpre)
+                _fire(w1)
+            else:
+                dw1 = wgrad_into(torch.zeros_like(w1), x2, dpre)
+        dx = mm_nt(dpre, w1).view(ctx.shp) if ctx.needs_input_grad[0] else None
+        return dx, dw1, db1, dw2, None
+
+
+def fused_mlp_supported(x, w1, b1, w2, act):
+    """The fused path: bf16 CUDA tensors, GELU(tanh)/ReLU, assembly-GEMM shapes (hidden and FFN
+    widths multiples of 64), transposable weights."""
+    if not (x.is_cuda and _GEMM_IMPL[0] == "asm" and act in ("gelu_tanh", "relu")
+            and x.dtype == torch.bfloat16 and w1.dtype == w2.dtype == x.dtype
+            and b1 is not None and b1.dtype == x.dtype and w1.dim() == 2 and w2.dim() == 2
+            and w1.is_contiguous() and w2.is_contiguous()
+            and not getattr(w1, "_piamd_no_t", False) and not getattr(w2, "_piamd_no_t", False)):
+        return False
+    H, Fd = w1.shape
+    T = x.numel() // H
+    return H % 64 == 0 and Fd % 64 == 0 and w2.shape == (Fd, w2.shape[1]) and w2.shape[1] % 8 == 0 \
+        and T > 0 and H >= 128 and Fd >= 128
+
+
+def fused_mlp(x, w1, b1, w2, act="gelu_tanh"):
+    """``act(x @ w1 + b1) @ w2`` (weights ``[in, out]``; no output bias)."""
+    if fused_mlp_supported(x, w1, b1, w2, act):
+        return _FusedMLPFn.apply(x, w1, b1, w2, act)
+    from .activation import bias_act
+    return linear(bias_act(linear(x, w1), b1, act), w2)

@@ -180,8 +180,9 @@ class Kernel:
         # ek: plain kinds (bf16 / f32 / f32acc) or fused: bias[gelu|relu] (pre-activation stored
         # as aux), d{gelu,relu} (C = acc ⊙ act'(aux))
         fused = {"bias": ("bias_act", 0), "biasgelu": ("bias_act", 1), "biasrelu": ("bias_act", 3),
-                 "dgelu": ("dact", 1), "drelu": ("dact", 3)}
+                 "dgelu": ("dact", 1), "drelu": ("dact", 3), "biasnx": ("bias_act", 0)}
         self.ek, self.act = fused.get(ek, (ek, 0))
+        self.store_aux = ek != "biasnx"  # biasnx: C = acc + bias, no pre-activation output
         assert self.ek not in ("bias_act", "dact") or (a_kc and b_kc)  # descriptor SGPRs 40..47
         self.lines = []
         self.nlab = 0
@@ -974,6 +975,8 @@ class Kernel:
             self.unpack(t, self.VBIAS + 2 * nb + j // 2, 0)
             self.unpack(t + 1, self.VBIAS + 2 * nb + j // 2, 1)
             self.e(f"v_pk_add_f32 v[{d + j}:{d + j + 1}], v[{t}:{t + 1}], v[{d + j}:{d + j + 1}]")
+        if not self.store_aux:
+            return 0
         self.e(f"v_cvt_pk_bf16_f32 v{p}, v{d}, v{d + 1}")
         self.e(f"v_cvt_pk_bf16_f32 v{p + 1}, v{d + 2}, v{d + 3}")
         n = 0
@@ -1077,7 +1080,7 @@ LAYOUTS = {"nt": (True, True), "tn": (False, False), "nn": (True, False), "tt": 
 EPILOGUES = ("bf16", "bf16acc", "f32", "f32acc")
 
 
-FUSED = ("bias", "biasgelu", "biasrelu", "dgelu", "drelu")
+FUSED = ("bias", "biasgelu", "biasrelu", "dgelu", "drelu", "biasnx")
 
 
 def variants():

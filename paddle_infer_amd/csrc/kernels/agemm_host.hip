@@ -132,7 +132,7 @@ PIAMD_EXPORT int piamd_agemm(const void* a, long long lda, int trans_a, const vo
   if (epi != 0) {
     static const char* const kFused[2][4] = {{"bias", "biasgelu", "", "biasrelu"},
                                              {"", "dgelu", "", "drelu"}};
-    ek = kFused[epi - 1][act];
+    ek = (epi == 1 && act == 0 && !aux) ? "biasnx" : kFused[epi - 1][act];
     g.c = c;
     g.ldc_b = (unsigned)(ldc * 2);
     g.c_bytes = ((unsigned long long)(M - 1) * ldc + N) * 2;

@@ -182,6 +182,37 @@ def run_while(executor, op, sub, env, scope, program, max_iters=10 ** 7):
         env[dst] = env[src]
 
 
+def _truth(v):
+    return bool(v.reshape(-1)[0].item()) if isinstance(v, torch.Tensor) else bool(v)
+
+
+def run_paddle_while(executor, op, sub, env, scope, program, max_iters=10 ** 7):
+    """Reference `controlflow/while_op.cc`: run ``sub_block`` while the Condition variable is
+    true. The block updates the loop variables (and the condition) by name, in place — the
+    Executor's environment is the scope the reference's step scopes read through."""
+    cond = op.paddle_inputs["Condition"][0]
+    blk = program.block(op.attrs["sub_block"])
+    for _ in range(max_iters):
+        if not _truth(sub_value(cond, sub)):
+            return
+        for o in blk.ops:
+            executor._run_op(o, sub, env, scope, program)
+    raise RuntimeError("while op exceeded max_iters")
+
+
+def run_conditional_block(executor, op, sub, env, scope, program):
+    """Reference `controlflow/conditional_block_op.cc`: run ``sub_block`` when the scalar Cond is
+    true (``is_scalar_condition``) or, otherwise, when every Cond tensor is non-empty."""
+    conds = [sub_value(n, sub) for n in op.paddle_inputs.get("Cond", [])]
+    if op.attrs.get("is_scalar_condition", False):
+        run = _truth(conds[0])
+    else:
+        run = all(isinstance(c, torch.Tensor) and c.numel() > 0 for c in conds)
+    if run:
+        for o in program.block(op.attrs["sub_block"]).ops:
+            executor._run_op(o, sub, env, scope, program)
+
+
 def sub_value(name, sub):
     from .framework import VarRef
     return sub(VarRef(name))

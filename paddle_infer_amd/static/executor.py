@@ -268,9 +268,14 @@ class Executor:
                     p.grad = None
             return
         from .backward import op_role, is_grad_op, OPTIMIZE, FORWARD
-        if op.type in ("cond", "while") and op.func is None:
+        if op.type in ("cond", "while") and op.func is None and "sub_block" not in op.attrs:
             from . import control_flow as _cf
             (_cf.run_cond if op.type == "cond" else _cf.run_while)(self, op, sub, env, scope, program)
+            return
+        if op.type in ("while", "conditional_block") and op.func is None:
+            from . import control_flow as _cf
+            (_cf.run_paddle_while if op.type == "while" else _cf.run_conditional_block)(
+                self, op, sub, env, scope, program)
             return
         if is_grad_op(op):
             self._run_grad_op(op, sub, env)

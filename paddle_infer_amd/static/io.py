@@ -316,41 +316,59 @@ def _attr_value(a):
             15: a.get("float64")}.get(t)
 
 
+CONTROL_FLOW_OPS = ("while", "conditional_block")
+
+
 def desc_to_program(desc: dict):
+    """Every block of the ProgramDesc (sub-blocks of ``while`` / ``conditional_block`` keep their
+    indices, so BLOCK attributes stay valid). Op types with no kernel are rejected HERE, at load
+    (reference: the predictor refuses an unregistered op when it builds the program)."""
+    from .ops_registry import REGISTRY
     prog = Program()
-    b = prog.global_block()
-    blk = desc["blocks"][0]
     feeds, fetches = [], []
     np_dt = {v: k for k, v in proto.VT.items()}
-    for vd in blk.get("vars", []):
-        ty = vd.get("type", {})
-        if ty.get("type") != proto.VT_LOD_TENSOR:
-            continue
-        td = ty.get("lod_tensor", {}).get("tensor", {})
-        v = b.create_var(vd["name"], td.get("dims", [1]) or [1], np_dt.get(td.get("data_type", 5), "float32"),
-                         persistable=vd.get("persistable", False),
-                         stop_gradient=vd.get("stop_gradient", True))
-        v.declared_shape = td.get("dims", [])
-    for od in blk.get("ops", []):
-        ins = {x["parameter"]: x.get("arguments", []) for x in od.get("inputs", [])}
-        outs = {x["parameter"]: x.get("arguments", []) for x in od.get("outputs", [])}
-        attrs = {a["name"]: _attr_value(a) for a in od.get("attrs", [])}
-        if od["type"] == "feed":
-            feeds.append((attrs.get("col", len(feeds)), outs["Out"][0]))
-            continue
-        if od["type"] == "fetch":
-            fetches.append((attrs.get("col", len(fetches)), ins["X"][0]))
-            continue
-        if "op_callable" in attrs:
-            spec = json.loads(attrs.pop("op_spec"))
-            func = resolve_func(attrs.pop("op_callable"))
-            extra = {k: _dec(json.loads(v)) for k, v in attrs.items() if isinstance(v, str)}
-            op = Operator(b, func, _dec(spec["args"]), _dec(spec["kwargs"]), _dec(spec["outputs"]),
-                          type=od["type"], attrs=extra)
-        else:
-            op = Operator(b, None, (), {}, None, type=od["type"], attrs=attrs)
-            op.paddle_inputs, op.paddle_outputs = ins, outs
-        b.append_op(op)
+    blocks = sorted(desc["blocks"], key=lambda d: d.get("idx", 0))
+    for bd in blocks[1:]:
+        prog._create_block(bd.get("parent_idx", 0))
+    unknown = set()
+    for bd in blocks:
+        b = prog.block(bd.get("idx", 0))
+        for vd in bd.get("vars", []):
+            ty = vd.get("type", {})
+            if ty.get("type") != proto.VT_LOD_TENSOR:
+                continue
+            td = ty.get("lod_tensor", {}).get("tensor", {})
+            v = b.create_var(vd["name"], td.get("dims", [1]) or [1], np_dt.get(td.get("data_type", 5), "float32"),
+                             persistable=vd.get("persistable", False),
+                             stop_gradient=vd.get("stop_gradient", True))
+            v.declared_shape = td.get("dims", [])
+        for od in bd.get("ops", []):
+            ins = {x["parameter"]: x.get("arguments", []) for x in od.get("inputs", [])}
+            outs = {x["parameter"]: x.get("arguments", []) for x in od.get("outputs", [])}
+            attrs = {a["name"]: _attr_value(a) for a in od.get("attrs", [])}
+            if od["type"] == "feed":
+                feeds.append((attrs.get("col", len(feeds)), outs["Out"][0]))
+                continue
+            if od["type"] == "fetch":
+                fetches.append((attrs.get("col", len(fetches)), ins["X"][0]))
+                continue
+            if "op_callable" in attrs:
+                spec = json.loads(attrs.pop("op_spec"))
+                func = resolve_func(attrs.pop("op_callable"))
+                extra = {k: _dec(json.loads(v)) for k, v in attrs.items() if isinstance(v, str)}
+                op = Operator(b, func, _dec(spec["args"]), _dec(spec["kwargs"]), _dec(spec["outputs"]),
+                              type=od["type"], attrs=extra)
+            else:
+                t = od["type"]
+                # <type>_grad ops run as the VJP of their forward op (static/executor.py)
+                if t not in REGISTRY and t not in CONTROL_FLOW_OPS and not t.endswith("_grad"):
+                    unknown.add(t)
+                op = Operator(b, None, (), {}, None, type=od["type"], attrs=attrs)
+                op.paddle_inputs, op.paddle_outputs = ins, outs
+            b.append_op(op)
+    if unknown:
+        raise NotImplementedError(
+            f"program uses Paddle op type(s) with no kernel in paddle_infer_amd: {sorted(unknown)}")
     prog.feed_names = [n for _, n in sorted(feeds)]
     prog.fetch_names = [n for _, n in sorted(fetches)]
     return prog

@@ -17,6 +17,8 @@ from . import proto
 from .framework import VarRef
 
 REGISTRY = {}
+INPLACE_OUT_OPS = {"write_to_array"}
+MISSING_OK_OPS = {"select_input"}
 DEVICE = [torch.device("cpu")]  # device of the running Executor (creation ops allocate there)
 
 
@@ -47,7 +49,17 @@ def run_paddle_op(op, sub, env, scope):
     fn = REGISTRY.get(op.type)
     if fn is None:
         raise NotImplementedError(f"Paddle op '{op.type}' has no kernel in paddle_infer_amd")
-    ins = {k: [sub(VarRef(n)) for n in v] for k, v in op.paddle_inputs.items()}
+    if op.type in MISSING_OK_OPS:  # e.g. select_input: the branch not taken never wrote its var
+        def get(n):
+            try:
+                return sub(VarRef(n))
+            except KeyError:
+                return None
+        ins = {k: [get(n) for n in v] for k, v in op.paddle_inputs.items()}
+    else:
+        ins = {k: [sub(VarRef(n)) for n in v] for k, v in op.paddle_inputs.items()}
+    if op.type in INPLACE_OUT_OPS:  # ops that update their output variable in place (arrays)
+        ins["__out__"] = [env.get(n) for n in op.paddle_outputs.get("Out", [])]
     outs = fn(ins, op.attrs)
     for slot, names in op.paddle_outputs.items():
         vals = outs.get(slot)
@@ -672,3 +684,6 @@ def _adam(ins, a):
 @register("clip")
 def _clip_op(ins, a):
     return {"Out": torch.clamp(ins["X"][0], float(a.get("min", -3.4e38)), float(a.get("max", 3.4e38)))}
+
+
+from . import ops_registry_ext  # noqa: E402,F401  (registers the extended op set)

@@ -127,8 +127,6 @@ def build_backward(block, loss_name, wrt, stop=()):
         return name + GRAD
 
     for fop in path:
-        if fop.type in ("cond", "while") and fop.func is None:
-            raise NotImplementedError(f"append_backward through a '{fop.type}' op (control flow is forward-only here)")
         ins, outs = fwd_slots(fop)
         out_g = {s: [finalize(o) if o in need else "" for o in names] for s, names in outs.items()}
         if not any(g for gs in out_g.values() for g in gs):

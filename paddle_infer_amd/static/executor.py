@@ -178,6 +178,7 @@ class Executor:
             return x
 
         self._leafmap = {}
+        self._cf_depth = 0
         self._training = training
         dp = None
         if compiled is not None and compiled._data_parallel and training:
@@ -268,35 +269,46 @@ class Executor:
                     p.grad = None
             return
         from .backward import op_role, is_grad_op, OPTIMIZE, FORWARD
-        if op.type in ("cond", "while") and op.func is None and "sub_block" not in op.attrs:
-            from . import control_flow as _cf
-            (_cf.run_cond if op.type == "cond" else _cf.run_while)(self, op, sub, env, scope, program)
-            return
-        if op.type in ("while", "conditional_block") and op.func is None:
-            from . import control_flow as _cf
-            (_cf.run_paddle_while if op.type == "while" else _cf.run_conditional_block)(
-                self, op, sub, env, scope, program)
-            return
         if is_grad_op(op):
             self._run_grad_op(op, sub, env)
             return
-        if getattr(self, "_training", False) and op_role(op) == FORWARD:
+        if getattr(self, "_training", False) and op_role(op) == FORWARD and not getattr(self, "_cf_depth", 0):
             # per-op autograd graphs: a forward op of a training program reads its differentiable
             # inputs through fresh leaves (views, no copy), so its grad op's VJP is exactly this
-            # op's local Jacobian product (a grad w.r.t. one input never leaks through another)
-            leaves = {}
+            # op's local Jacobian product (a grad w.r.t. one input never leaks through another).
+            # A control-flow op is ONE such op: its sub-block ops run on a plain autograd graph
+            # from these leaves (first read of each external input only — a loop may rebind the
+            # name), and cond_grad / while_grad are the VJP through whatever path ran.
+            leaves, orig = {}, {}
+            ext = set(op.input_names())
             outer = sub
 
             def sub(x):  # noqa: F811
                 v = outer(x)
-                if isinstance(x, VarRef) and isinstance(v, torch.Tensor) and v.requires_grad:
+                if isinstance(x, VarRef) and isinstance(v, torch.Tensor) and v.requires_grad and x.name in ext:
                     lf = leaves.get(x.name)
                     if lf is None:
                         lf = leaves[x.name] = v.detach().requires_grad_(True)
-                    return lf
+                        orig[x.name] = v
+                        return lf
+                    return lf if orig[x.name] is v else v
                 return v
             for n in op.output_names():
                 self._leafmap[n] = leaves
+        if op.type in ("cond", "while", "conditional_block") and op.func is None:
+            from . import control_flow as _cf
+            if op.type == "conditional_block":
+                fn = _cf.run_conditional_block
+            elif op.type == "while":
+                fn = _cf.run_paddle_while if "sub_block" in op.attrs else _cf.run_while
+            else:
+                fn = _cf.run_cond
+            self._cf_depth = getattr(self, "_cf_depth", 0) + 1
+            try:
+                fn(self, op, sub, env, scope, program)
+            finally:
+                self._cf_depth -= 1
+            return
         if op.func is None:  # a Paddle-typed op (loaded .pdmodel, IR pass, backward / optimizer pass)
             from . import ops_registry
             ops_registry.DEVICE.append(self.device)

@@ -175,3 +175,48 @@ def test_recompute_vjp_path_matches(monkeypatch):
     monkeypatch.setattr(E.Executor, "_run_grad_op", no_graph)
     g_re, = exe.run(main, feed={"x": X}, fetch_list=[pg[0][1].var_name])
     np.testing.assert_allclose(g_re, g_fast, rtol=1e-6, atol=1e-7)
+
+
+def test_static_training_through_cond_and_while_matches_dygraph():
+    """append_backward through control flow (reference while_grad / conditional_block_grad,
+    `while_op.cc:586`, `conditional_block_op.cc:423`): a data-dependent branch and a
+    data-dependent loop between two fc layers train to the same losses as dygraph."""
+    torch.manual_seed(3)
+    main, startup = static.Program(), static.Program()
+    with static.program_guard(main, startup):
+        x = static.data("x", [None, 8], "float32")
+        y = static.data("y", [None, 1], "float32")
+        h = static.nn.fc(x, 8, activation="relu")
+        h2 = static.nn.cond(paddle.mean(h) > 0.3, lambda: h * 2.0, lambda: h - 1.0)
+        k0 = paddle.zeros([1], "float32")
+        h3, _ = static.nn.while_loop(lambda a, k: paddle.sum(paddle.abs(a)) < 40.0,
+                                     lambda a, k: [a * 1.5 + 0.1, k + 1.0], [h2, k0])
+        pred = static.nn.fc(h3, 1)
+        loss = paddle.mean((pred - y) ** 2)
+        paddle.optimizer.SGD(learning_rate=0.001).minimize(loss)
+    types = {op.type for op in main.global_block().ops}
+    assert {"cond_grad", "while_grad"} <= types
+    names = [n for n, t in main.params.items() if t.requires_grad]
+    init = {n: main.params[n].detach().clone() for n in names}
+    feeds = _feeds(5, seed=4)
+    exe = static.Executor()
+    got = [float(exe.run(main, feed={"x": X, "y": Y}, fetch_list=[loss])[0]) for X, Y in feeds]
+    paddle.disable_static()
+    try:
+        w1, b1, w2, b2 = [init[n].clone().requires_grad_(True) for n in names]
+        opt = paddle.optimizer.SGD(learning_rate=0.001, parameters=[w1, b1, w2, b2])
+        ref = []
+        for X, Y in feeds:
+            X, Y = torch.as_tensor(X), torch.as_tensor(Y)
+            h = torch.relu(X @ w1 + b1)
+            h = h * 2.0 if float(h.mean()) > 0.3 else h - 1.0
+            while float(h.abs().sum()) < 40.0:
+                h = h * 1.5 + 0.1
+            loss_d = torch.mean((h @ w2 + b2 - Y) ** 2)
+            loss_d.backward()
+            opt.step()
+            opt.clear_grad()
+            ref.append(float(loss_d))
+    finally:
+        paddle.enable_static()
+    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-5)

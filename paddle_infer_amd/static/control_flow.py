@@ -9,8 +9,10 @@ Here one ``cond`` op holds both branch blocks (attrs ``true_block`` / ``false_bl
 result names) and one ``while`` op holds a condition block and a body block with the loop-carried
 variables. Tracing records each branch / body into its own sub-block (``Program._block_guard``);
 the Executor evaluates the predicate on the device value (one host read per decision, as in the
-reference) and runs only the chosen block. Forward-only: append_backward refuses a path through
-them.
+reference) and runs only the chosen block. append_backward differentiates each control-flow op as
+one op (``cond_grad`` / ``while_grad``: the VJP of the branch / iterations actually taken). On save
+(`io._CFLowering`) they become the reference's own ops — ``conditional_block`` + ``select_input``
+and ``while`` with sub-blocks — which `run_conditional_block` / `run_paddle_while` execute.
 """
 from __future__ import annotations
 

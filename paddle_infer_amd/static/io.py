@@ -16,6 +16,7 @@ else (``os.system``, ``builtins.eval``, ``torch.load`` ...) is rejected before a
 """
 from __future__ import annotations
 
+import copy
 import json
 import math
 import os
@@ -231,79 +232,210 @@ def _typed_attr_descs(attrs):
     return out
 
 
+def _tensor_var_desc(name, like):
+    """A fresh LoD-tensor var desc with the dims / dtype of the existing desc ``like``."""
+    d = copy.deepcopy(like)
+    d.update(name=name, persistable=False, is_parameter=False, stop_gradient=True)
+    return d
+
+
+VT_STEP_SCOPES = 11
+
+
+class _CFLowering:
+    """Emit the framework's ``cond`` / ``while`` ops as Paddle control flow (reference
+    `python/paddle/fluid/layers/control_flow.py`): ``cond`` → ``logical_not`` + two
+    ``conditional_block`` ops (``is_scalar_condition``) + one ``select_input`` per result (Mask =
+    the predicate as int32, X = [false value, true value]); ``while_loop`` → ``assign`` of the
+    initial values into the loop-carried vars, the condition block inlined before the loop, and a
+    ``while`` op whose sub-block runs the body, copies the body results back into the carried vars
+    (through temporaries, so a permutation of the carried vars is safe) and recomputes the
+    condition. Sub-blocks get fresh indices in emission order."""
+
+    def __init__(self, program, allow_custom_ops):
+        import collections
+        import types
+        self.program, self.allow = program, allow_custom_ops
+        self.view = types.SimpleNamespace(vars=collections.ChainMap(*[b.vars for b in program.blocks]))
+        self.blocks = []        # emitted sub-block dicts (idx 1..)
+        self.new_vars = {}      # name -> var desc (temps, lowering temporaries)
+        self._n = 0
+
+    def _tmp(self, stem, like=None, dims=None, dt=None):
+        self._n += 1
+        name = f"{stem}.cf_{self._n}"
+        if like is not None and like in self.view.vars:
+            self.new_vars[name] = _tensor_var_desc(name, _var_desc(self.view.vars[like], False))
+        else:
+            self.new_vars[name] = {"name": name, "type": {"type": proto.VT_LOD_TENSOR, "lod_tensor": {
+                "tensor": {"data_type": dt, "dims": dims}, "lod_level": 0}},
+                "persistable": False, "is_parameter": False, "stop_gradient": True}
+        return name
+
+    def _scope_var(self):
+        self._n += 1
+        name = f"_cf_scope.{self._n}"
+        self.new_vars[name] = {"name": name, "type": {"type": VT_STEP_SCOPES}, "persistable": False}
+        return name
+
+    def _new_block(self, parent_idx):
+        bd = {"idx": len(self.blocks) + 1, "parent_idx": parent_idx, "vars": [], "ops": []}
+        self.blocks.append(bd)
+        return bd
+
+    def emit(self, ops, block_idx):
+        """-> list of Paddle op descs for the recorded ``ops`` of one block."""
+        from .lowering import lower, LoweringError
+        out = []
+        for op in ops:
+            if op.type in ("backward", "optimize"):
+                continue
+            if op.func is None and op.type == "cond":
+                out.extend(self._cond(op, block_idx))
+                continue
+            if op.func is None and op.type == "while":
+                out.extend(self._while(op, block_idx))
+                continue
+            if op.func is None and op.paddle_inputs is not None:  # already a Paddle op
+                d = {"type": op.type,
+                     "inputs": [{"parameter": k, "arguments": list(v)} for k, v in op.paddle_inputs.items()],
+                     "outputs": [{"parameter": k, "arguments": list(v)}
+                                 for k, v in (op.paddle_outputs or {}).items()],
+                     "attrs": _typed_attr_descs({k: v for k, v in op.attrs.items() if k != "sub_block"})}
+                if "sub_block" in op.attrs:  # a loaded Paddle while / conditional_block: re-emit its block
+                    sub = self._new_block(block_idx)
+                    sub["ops"] = self.emit(self.program.block(op.attrs["sub_block"]).ops, sub["idx"])
+                    d["attrs"].append({"name": "sub_block", "type": proto.ATTR["BLOCK"],
+                                       "block_idx": sub["idx"]})
+                out.append(d)
+                continue
+            if op.func is None:
+                out.append(_recorded_op_desc(op))
+                continue
+            try:
+                descs, new_vars = lower(self.view, op)
+            except LoweringError:
+                if not self.allow:
+                    raise
+                out.append(_recorded_op_desc(op))
+                continue
+            for name, dims, dt in new_vars:
+                if name not in self.new_vars and name not in self.view.vars:
+                    self.new_vars[name] = {"name": name, "type": {"type": proto.VT_LOD_TENSOR, "lod_tensor": {
+                        "tensor": {"data_type": dt, "dims": dims}, "lod_level": 0}},
+                        "persistable": False, "is_parameter": False, "stop_gradient": True}
+            out.extend(_paddle_op_desc(*d) for d in descs)
+        return out
+
+    def _cond(self, op, block_idx):
+        pred = op.paddle_inputs["Cond"][0]
+        ins = op.paddle_inputs.get("Input", [])
+        res = op.paddle_outputs.get("Out", [])
+        t_outs, f_outs = op.attrs["true_outs"], op.attrs["false_outs"]
+        not_pred = self._tmp("cond_not", like=pred)
+        mask = self._tmp("cond_mask", dims=[1], dt=proto.VT["int32"])
+        descs = [_paddle_op_desc("logical_not", {"X": [pred]}, {"Out": [not_pred]}, {})]
+        for c, blk_key, outs in ((pred, "true_block", t_outs), (not_pred, "false_block", f_outs)):
+            sub = self._new_block(block_idx)
+            sub["ops"] = self.emit(self.program.block(op.attrs[blk_key]).ops, sub["idx"])
+            d = _paddle_op_desc("conditional_block", {"Cond": [c], "Input": ins},
+                                {"Out": list(outs), "Scope": [self._scope_var()]},
+                                {"is_scalar_condition": True})
+            d["attrs"].append({"name": "sub_block", "type": proto.ATTR["BLOCK"], "block_idx": sub["idx"]})
+            descs.append(d)
+        descs.append(_paddle_op_desc("cast", {"X": [pred]}, {"Out": [mask]},
+                                     {"in_dtype": proto.VT["bool"], "out_dtype": proto.VT["int32"]}))
+        for r, t, f in zip(res, t_outs, f_outs):
+            descs.append(_paddle_op_desc("select_input", {"X": [f, t], "Mask": [mask]}, {"Out": [r]}, {}))
+        return descs
+
+    def _while(self, op, block_idx):
+        a = op.attrs
+        init, outs = op.paddle_inputs["X"], op.paddle_outputs["Out"]
+        carried, body_outs = a["carried"], a["body_outs"]
+        cond_ops = self.program.block(a["cond_block"]).ops
+        descs = [_paddle_op_desc("assign", {"X": [s]}, {"Out": [d]}, {}) for s, d in zip(init, carried)]
+        descs += self.emit(cond_ops, block_idx)
+        sub = self._new_block(block_idx)
+        body = self.emit(self.program.block(a["body_block"]).ops, sub["idx"])
+        tmps = [self._tmp("loop_next", like=c) for c in carried]
+        body += [_paddle_op_desc("assign", {"X": [s]}, {"Out": [t]}, {}) for s, t in zip(body_outs, tmps)]
+        body += [_paddle_op_desc("assign", {"X": [t]}, {"Out": [c]}, {}) for t, c in zip(tmps, carried)]
+        body += self.emit(cond_ops, sub["idx"])
+        sub["ops"] = body
+        reads = list(dict.fromkeys(op.paddle_inputs.get("Input", []) + list(carried)))
+        d = _paddle_op_desc("while", {"X": reads, "Condition": [a["cond_out"]]},
+                            {"Out": list(carried), "StepScopes": [self._scope_var()]}, {"is_test": True})
+        d["attrs"].append({"name": "sub_block", "type": proto.ATTR["BLOCK"], "block_idx": sub["idx"]})
+        descs.append(d)
+        descs += [_paddle_op_desc("assign", {"X": [c]}, {"Out": [o]}, {}) for c, o in zip(carried, outs)]
+        return descs
+
+
+def _recorded_op_desc(op):
+    """An op no Paddle lowering covers, kept in recorded (callable) form."""
+    attrs = [{"name": k, "type": proto.ATTR["STRING"], "s": json.dumps(_enc(v))}
+             for k, v in op.attrs.items() if k not in ("optimizer",)]
+    if op.func is not None:
+        attrs.append({"name": "op_callable", "type": proto.ATTR["STRING"], "s": func_name(op.func)})
+        attrs.append({"name": "op_spec", "type": proto.ATTR["STRING"],
+                      "s": json.dumps({"args": _enc(op.args), "kwargs": _enc(op.kwargs),
+                                       "outputs": _enc(op.outputs)})})
+    return {"type": op.type, "inputs": [{"parameter": "X", "arguments": op.input_names()}],
+            "outputs": [{"parameter": "Out", "arguments": op.output_names()}], "attrs": attrs}
+
+
+def _desc_names(op_descs, blocks):
+    names = set()
+    for od in list(op_descs) + [o for bd in blocks for o in bd["ops"]]:
+        for x in od["inputs"] + od["outputs"]:
+            names.update(x["arguments"])
+    return names
+
+
 def program_to_desc(program: Program, feed_names=None, fetch_names=None, ops=None,
                     paddle_ops=True, allow_custom_ops=False):
     """``paddle_ops``: lower recorded ops to Paddle OpDescs (`lowering.py`); an op no rule covers
-    raises ``LoweringError`` unless ``allow_custom_ops`` keeps it in recorded (callable) form."""
-    from .lowering import lower, LoweringError
-    if any(op.type in ("cond", "while") and op.func is None for op in (ops or program.global_block().ops)):
-        raise LoweringError("programs with cond / while sub-blocks run in the Executor but are not "
-                            "serialisable to a .pdmodel yet")
+    raises ``LoweringError`` unless ``allow_custom_ops`` keeps it in recorded (callable) form.
+    ``cond`` / ``while`` become Paddle ``conditional_block`` / ``while`` ops with sub-blocks
+    (`_CFLowering`)."""
+    from .lowering import LoweringError
     b = program.global_block()
     ops = b.ops if ops is None else ops
+    if not paddle_ops and any(op.type in ("cond", "while") and op.func is None for op in ops):
+        raise LoweringError("cond / while are serialised as Paddle control-flow ops only (paddle_ops=True)")
+    op_descs = []
+    if feed_names:
+        for i, n in enumerate(feed_names):
+            op_descs.append({"type": "feed", "inputs": [{"parameter": "X", "arguments": ["feed"]}],
+                             "outputs": [{"parameter": "Out", "arguments": [n]}],
+                             "attrs": [{"name": "col", "type": proto.ATTR["INT"], "i": i}]})
+    cf = _CFLowering(program, allow_custom_ops)
+    if paddle_ops:
+        op_descs.extend(cf.emit(ops, 0))
+    else:
+        op_descs.extend(_recorded_op_desc(op) for op in ops if op.type not in ("backward", "optimize"))
+    if fetch_names:
+        for i, n in enumerate(fetch_names):
+            op_descs.append({"type": "fetch", "inputs": [{"parameter": "X", "arguments": [n]}],
+                             "outputs": [{"parameter": "Out", "arguments": ["fetch"]}],
+                             "attrs": [{"name": "col", "type": proto.ATTR["INT"], "i": i}]})
     used = set()
     for op in ops:
         used.update(op.input_names())
         used.update(op.output_names())
     used.update(feed_names or [])
     used.update(fetch_names or [])
-    vars_ = [_var_desc(b.vars[n], n in program.params) for n in sorted(used) if n in b.vars]
-    op_descs = []
-    lowered = {}
-    if paddle_ops:
-        for op in ops:
-            if op.func is None or op.type in ("backward", "optimize"):
-                continue
-            try:
-                lowered[id(op)] = lower(b, op)
-            except LoweringError:
-                if not allow_custom_ops:
-                    raise
-        seen = {v["name"] for v in vars_}
-        for descs, new_vars in lowered.values():
-            for name, dims, dt in new_vars:
-                if name not in seen:
-                    seen.add(name)
-                    vars_.append({"name": name, "type": {"type": proto.VT_LOD_TENSOR, "lod_tensor": {
-                        "tensor": {"data_type": dt, "dims": dims}, "lod_level": 0}},
-                        "persistable": False, "is_parameter": False, "stop_gradient": True})
+    used |= _desc_names(op_descs, cf.blocks)
+    allv = cf.view.vars
+    vars_ = [_var_desc(allv[n], n in program.params) for n in sorted(used) if n in allv]
+    seen = {v["name"] for v in vars_}
+    vars_ += [d for n, d in cf.new_vars.items() if n not in seen]
     if feed_names:
         vars_.append({"name": "feed", "type": {"type": proto.VT_FEED}, "persistable": True})
-        for i, n in enumerate(feed_names):
-            op_descs.append({"type": "feed", "inputs": [{"parameter": "X", "arguments": ["feed"]}],
-                             "outputs": [{"parameter": "Out", "arguments": [n]}],
-                             "attrs": [{"name": "col", "type": proto.ATTR["INT"], "i": i}]})
-    for op in ops:
-        if op.type in ("backward", "optimize"):
-            continue
-        if id(op) in lowered:
-            op_descs.extend(_paddle_op_desc(*d) for d in lowered[id(op)][0])
-            continue
-        if op.func is None and op.paddle_inputs is not None:  # already a Paddle op
-            op_descs.append({"type": op.type,
-                             "inputs": [{"parameter": k, "arguments": list(v)}
-                                        for k, v in op.paddle_inputs.items()],
-                             "outputs": [{"parameter": k, "arguments": list(v)}
-                                         for k, v in (op.paddle_outputs or {}).items()],
-                             "attrs": _typed_attr_descs(op.attrs)})
-            continue
-        attrs = [{"name": k, "type": proto.ATTR["STRING"], "s": json.dumps(_enc(v))}
-                 for k, v in op.attrs.items() if k not in ("optimizer",)]
-        if op.func is not None:
-            attrs.append({"name": "op_callable", "type": proto.ATTR["STRING"], "s": func_name(op.func)})
-            attrs.append({"name": "op_spec", "type": proto.ATTR["STRING"],
-                          "s": json.dumps({"args": _enc(op.args), "kwargs": _enc(op.kwargs),
-                                           "outputs": _enc(op.outputs)})})
-        op_descs.append({"type": op.type, "inputs": [{"parameter": "X", "arguments": op.input_names()}],
-                         "outputs": [{"parameter": "Out", "arguments": op.output_names()}],
-                         "attrs": attrs})
     if fetch_names:
         vars_.append({"name": "fetch", "type": {"type": proto.VT_FETCH}, "persistable": True})
-        for i, n in enumerate(fetch_names):
-            op_descs.append({"type": "fetch", "inputs": [{"parameter": "X", "arguments": [n]}],
-                             "outputs": [{"parameter": "Out", "arguments": ["fetch"]}],
-                             "attrs": [{"name": "col", "type": proto.ATTR["INT"], "i": i}]})
-    return {"blocks": [{"idx": 0, "parent_idx": -1, "vars": vars_, "ops": op_descs}],
+    return {"blocks": [{"idx": 0, "parent_idx": -1, "vars": vars_, "ops": op_descs}] + cf.blocks,
             "version": {"version": 0}}
 
 

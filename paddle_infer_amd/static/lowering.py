@@ -550,6 +550,22 @@ def _reduce(ctx, op):
              {"dim": _intlist(dim), "keep_dim": keep, "reduce_all": False})]
 
 
+@rule(torch.max, T.max, torch.min, T.min)
+def _max_min(ctx, op):
+    """Full reduce (``torch.max(x)``) or elementwise against a second tensor; the
+    (values, indices) form with a dim has no single Paddle op."""
+    is_max = op.func in (torch.max, T.max)
+    x = _name(op.args[0])
+    other = _arg(op, 1, "other") if len(op.args) > 1 or "other" in op.kwargs else None
+    if other is None and "dim" not in op.kwargs:
+        return [("reduce_max" if is_max else "reduce_min", {"X": [x]}, {"Out": [_outs(op)[0]]},
+                 {"dim": [], "keep_dim": False, "reduce_all": True})]
+    if other is not None and not isinstance(other, int):
+        return [("elementwise_max" if is_max else "elementwise_min", {"X": [x], "Y": [_name(other)]},
+                 {"Out": [_outs(op)[0]]}, {"axis": -1})]
+    raise LoweringError("max/min along a dim returns (values, indices)")
+
+
 @rule(F.softmax, torch.softmax, T.softmax)
 def _softmax(ctx, op):
     return [("softmax", {"X": [_name(op.args[0])]}, {"Out": [_outs(op)[0]]},

@@ -93,3 +93,29 @@ def test_return_inside_branch_left_as_python():
     conv = dy2static.convert_to_static(f)
     assert torch.equal(conv(torch.ones(2)), torch.ones(2))
     assert "convert_ifelse" not in conv._dy2static_source
+
+
+@pytest.mark.parametrize("fn", [f_if, f_while, f_for_and])
+def test_control_flow_saves_as_paddle_program(fn, tmp_path):
+    """cond / while serialise as Paddle ``conditional_block`` + ``select_input`` / ``while`` ops
+    with sub-blocks (reference `layers/control_flow.py`), and the reloaded .pdmodel still follows
+    the fed data."""
+    from paddle_infer_amd.static import io as sio
+    prog, feeds, fetch = jit.trace_program(fn, [static.InputSpec([None, 4], "float32", "x")])
+    exe = static.Executor(paddle.CPUPlace())
+    path = str(tmp_path / "m")
+    static.save_inference_model(path, feeds, fetch, exe, program=prog)
+    with open(path + ".pdmodel", "rb") as f:
+        desc = sio.proto.decode("ProgramDesc", f.read())
+    types = {od["type"] for bd in desc["blocks"] for od in bd.get("ops", [])}
+    assert not types & {"cond"}
+    if fn in (f_if, f_for_and):
+        assert {"conditional_block", "select_input"} <= types and len(desc["blocks"]) >= 3
+    if fn is f_while:
+        assert "while" in types and len(desc["blocks"]) >= 2
+    lp, lfeeds, lfetch = static.load_inference_model(path, exe)
+    for seed, sign in [(0, 1.0), (1, -1.0), (2, 0.01)]:
+        X = (np.abs(np.random.RandomState(seed).randn(3, 4)) * sign + 0.1 * sign).astype("float32")
+        ref = fn(torch.as_tensor(X)).numpy()
+        got = exe.run(lp, feed={lfeeds[0]: X}, fetch_list=lfetch)[0]
+        np.testing.assert_allclose(got, ref, rtol=1e-6)

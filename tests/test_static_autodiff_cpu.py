@@ -177,7 +177,7 @@ def test_recompute_vjp_path_matches(monkeypatch):
     np.testing.assert_allclose(g_re, g_fast, rtol=1e-6, atol=1e-7)
 
 
-def test_static_training_through_cond_and_while_matches_dygraph():
+def test_static_training_through_cond_and_while_matches_dygraph(tmp_path):
     """append_backward through control flow (reference while_grad / conditional_block_grad,
     `while_op.cc:586`, `conditional_block_op.cc:423`): a data-dependent branch and a
     data-dependent loop between two fc layers train to the same losses as dygraph."""
@@ -220,3 +220,17 @@ def test_static_training_through_cond_and_while_matches_dygraph():
     finally:
         paddle.enable_static()
     np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-5)
+    # the trained program saves as a Paddle program (conditional_block / while sub-blocks) and the
+    # reloaded inference model reproduces the dygraph forward with the trained weights
+    path = str(tmp_path / "cf")
+    static.save_inference_model(path, [x], [pred], exe, program=main)
+    lp, lfeeds, lfetch = static.load_inference_model(path, exe)
+    assert {"conditional_block", "while", "select_input"} <= {op.type for b in lp.blocks for op in b.ops}
+    for X, _ in feeds[:3]:
+        out = exe.run(lp, feed={lfeeds[0]: X}, fetch_list=lfetch)[0]
+        with torch.no_grad():
+            h = torch.relu(torch.as_tensor(X) @ w1 + b1)
+            h = h * 2.0 if float(h.mean()) > 0.3 else h - 1.0
+            while float(h.abs().sum()) < 40.0:
+                h = h * 1.5 + 0.1
+            np.testing.assert_allclose(out, (h @ w2 + b2).numpy(), rtol=1e-4, atol=1e-5)

@@ -17,7 +17,9 @@ reduce-scatter / all-reduce overlapped with backward, one AdamW launch per param
 Parallelism: ``--tp`` model-parallel degree, ``--pp`` pipeline degree (GPTForPretrainingPipe,
 1F1B; ``--vpp`` virtual chunks per rank = interleaved 1F1B; ``--accumulate`` micro-batches per
 step), ``--sharding-degree`` a separate ZeRO axis (the rest is dp), ``--sharding`` ZeRO stage on
-that axis (default 1 over dp: sharded optimizer states; 3 = group_sharded_parallel p_g_os, dp only).
+that axis (default 1 over dp: sharded optimizer states; 3 = ZeRO-3 per-block parameter shards,
+composable with ``--pp`` / ``--tp`` — BASELINE config 5 is ``--model gpt3-13b --pp 2
+--sharding-degree 4 --sharding 3`` on 8 GPUs; ``--offload 1`` keeps its optimizer states on the host).
 Weak scaling: the per-GPU micro batch is fixed as N grows.
 """
 from __future__ import annotations
@@ -57,6 +59,7 @@ def main():
     ap.add_argument("--sharding-degree", type=int, default=1)
     ap.add_argument("--sharding", type=int, default=1, help="ZeRO stage (0 = plain all-reduce DP)")
     ap.add_argument("--bucket-mb", type=int, default=256)
+    ap.add_argument("--offload", type=int, default=0, help="ZeRO-3: f32 master / moments in pinned host memory")
     ap.add_argument("--dropout", type=float, default=0.1)
     ap.add_argument("--recompute", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=0)
@@ -105,9 +108,10 @@ def main():
     strategy.hybrid_configs = {"dp_degree": dp, "mp_degree": tp, "pp_degree": pp,
                                "sharding_degree": shd}
     stage3 = args.sharding == 3
-    if args.sharding and not stage3:
+    if args.sharding:
+        # ZeRO on the sharding axis (or over dp when there is none); stage 3 composes with pp / tp
         strategy.sharding = shd == 1 and dp > 1
-        strategy.sharding_configs = {"stage": args.sharding}
+        strategy.sharding_configs = {"stage": args.sharding, "offload": bool(args.offload)}
     strategy.fuse_grad_size_in_MB = args.bucket_mb
     acc = args.accumulate or (2 * pp if pp > 1 else 1)
     acc = max(1, min(acc, args.micro_batch))
@@ -133,15 +137,10 @@ def main():
                               parameters=list(net.parameters()), weight_decay=0.1,
                               grad_clip=pia.nn.ClipGradByGlobalNorm(1.0),
                               apply_decay_param_fun=lambda n: n in decay)
-    if stage3:
-        from paddle_infer_amd.distributed.sharding import group_sharded_parallel
-        assert pp == 1 and tp == 1, "--sharding 3 is data-parallel ZeRO-3 (group_sharded_parallel)"
-        model, opt, _ = group_sharded_parallel(net, opt, "p_g_os", group=hcg.get_data_parallel_group())
-    else:
-        model = fleet.distributed_model(net)
-        opt = fleet.distributed_optimizer(opt)
-    n_params = sum(p.numel() for p in net.parameters())
-    if world > 1 and not stage3:
+    n_params = sum(p.numel() for p in net.parameters())  # before ZeRO-3 releases the blocks
+    model = fleet.distributed_model(net)
+    opt = fleet.distributed_optimizer(opt)
+    if world > 1:
         t = torch.tensor([n_params], device=device, dtype=torch.float64)
         if pp > 1:  # each stage holds its own layers (a tied table counted on both ends)
             dist.all_reduce(t, group=hcg.get_pipe_parallel_group())
@@ -207,8 +206,8 @@ def main():
                        "micro_batch_per_dp_rank": mb, "params": n_params,
                        "hidden_dropout": args.dropout, "attention_dropout": 0.0,
                        "optimizer": "AdamW fp32 master", "grad_clip": 1.0,
-                       "api": "fleet.init/distributed_model/distributed_optimizer" if not stage3
-                       else "group_sharded_parallel(p_g_os)",
+                       "api": "fleet.init/distributed_model/distributed_optimizer"
+                       + (" (sharding stage 3)" if stage3 else ""),
                        **({"pp_micro_batches": acc} if pp > 1 else {})},
             "tflops_per_gpu": round(tflops_gpu, 1), "final_loss": round(final_loss, 4),
             "tuned_gemm_table": bool(tuned),

@@ -24,32 +24,93 @@ from .pipeline import LayerDesc, SharedLayerDesc, PipelineLayer, PipelineParalle
 from .recompute import recompute  # noqa: F401
 from ...framework.random import get_rng_state_tracker, model_parallel_random_seed  # noqa: F401
 
-_STATE = {"hcg": None, "strategy": None, "inited": False, "model": None}
+_STATE = {"hcg": None, "strategy": None, "inited": False, "model": None, "stage3": None}
+
+
+_CONFIG_KEYS = {
+    "amp_configs": {"init_loss_scaling", "incr_every_n_steps", "decr_every_n_nan_or_inf", "incr_ratio",
+                    "decr_ratio", "use_dynamic_loss_scaling", "custom_white_list", "custom_black_list",
+                    "custom_black_varnames", "use_pure_fp16", "use_fp16_guard", "use_bf16",
+                    "use_optimizer_fp16", "use_master_grad"},
+    "recompute_configs": {"checkpoints", "enable_offload", "checkpoint_shape"},
+    "sharding_configs": {"sharding_degree", "stage", "segment_broadcast_MB", "segment_anchors",
+                         "sharding_segment_strategy", "mp_degree", "pp_degree", "dp_degree",
+                         "hybrid_dp", "gradient_merge_acc_step", "optimize_offload", "offload",
+                         "pp_allreduce_in_optimize", "optimize_cast", "sync_comm", "comm_overlap",
+                         "split_param", "fuse_broadcast_MB", "use_calc_stream"},
+    "pipeline_configs": {"accumulate_steps", "micro_batch_size", "schedule_mode", "p2p_cache_shape",
+                         "enable_partial_send_recv"},
+    "tensor_parallel_configs": {"tensor_parallel_degree", "tensor_init_seed"},
+    "gradient_merge_configs": {"k_steps", "avg"},
+    "lamb_configs": {"lamb_weight_decay", "exclude_from_weight_decay"},
+    "lars_configs": {"lars_coeff", "lars_weight_decay", "epsilon", "exclude_from_weight_decay"},
+    "gradient_scale_configs": {"scale_strategy", "scale_gradient"},
+    "localsgd_configs": {"k_steps", "begin_step"},
+    "adaptive_localsgd_configs": {"init_k_steps", "begin_step"},
+    "dgc_configs": {"rampup_begin_step", "rampup_step", "sparsity"},
+    "a_sync_configs": None, "qat_configs": None, "trainer_desc_configs": None,
+    "sparse_table_configs": None, "fs_client_param": None,
+}
 
 
 class DistributedStrategy:
+    """Reference `fleet/base/distributed_strategy.py`. Every field the reference defines exists;
+    each is honoured (hybrid degrees, sharding stage 1/2/3 + offload, pipeline, amp, recompute,
+    gradient_merge, lamb, lars, asp, sync_batch_norm, fusion sizes — see `meta_optimizers.py`) or
+    REJECTED with an error when switched on (parameter server, dgc, local SGD, ...). Setting an
+    unknown field or an unknown ``*_configs`` key raises (no silently dropped configuration)."""
+
+    _DEFAULTS = dict(
+        amp=False, recompute=False, sharding=False, pipeline=False, tensor_parallel=False,
+        gradient_merge=False, lamb=False, lars=False, dgc=False, localsgd=False,
+        adaptive_localsgd=False, asp=False, a_sync=False, fp16_allreduce=False, qat=False,
+        auto=False, semi_auto=False, auto_search=False, elastic=False, heter_ccl_mode=False,
+        is_fl_ps_mode=False, is_with_coordinator=False, sync_batch_norm=False,
+        fuse_all_reduce_ops=True, fuse_grad_size_in_MB=256, last_comm_group_size_MB=1,
+        find_unused_parameters=False, without_graph_optimization=True, fuse_grad_merge=False,
+        fuse_grad_size_in_num=8, nccl_comm_num=1, sync_nccl_allreduce=True,
+        use_hierarchical_allreduce=False, hierarchical_allreduce_inter_nranks=1,
+        cudnn_exhaustive_search=False, conv_workspace_size_limit=512,
+        cudnn_batchnorm_spatial_persistent=False, split_data=True, adam_d2sum=False,
+        _calc_comm_same_stream=False, _fuse_grad_size_in_TFLOPS=50,
+        execution_strategy=None, build_strategy=None)
+
     def __init__(self):
-        self._hybrid = {"dp_degree": -1, "mp_degree": 1, "pp_degree": 1, "sharding_degree": 1,
+        d = self.__dict__
+        d["_hybrid"] = {"dp_degree": -1, "mp_degree": 1, "pp_degree": 1, "sharding_degree": 1,
                         "sep_degree": 1, "order": ["dp", "pp", "sharding", "mp"]}
-        self.amp = False
-        self.amp_configs = {"init_loss_scaling": 32768.0, "use_pure_fp16": False, "use_bf16": True}
-        self.recompute = False
-        self.recompute_configs = {"checkpoints": []}
-        self.sharding = False
-        self.sharding_configs = {"sharding_degree": 1, "stage": 1, "segment_broadcast_MB": 32}
-        self.pipeline = False
-        self.pipeline_configs = {"accumulate_steps": 1, "micro_batch_size": 1}
-        self.tensor_parallel = False
-        self.tensor_parallel_configs = {"tensor_parallel_degree": 1}
-        self.gradient_merge = False
-        self.gradient_merge_configs = {"k_steps": 1, "avg": True}
-        self.lamb = self.lars = self.dgc = self.localsgd = self.asp = False
-        self.fuse_all_reduce_ops = True
-        self.fuse_grad_size_in_MB = 256
-        self.find_unused_parameters = False
-        self.without_graph_optimization = True
-        self.a_sync = False
-        self.heter_ccl_mode = False
+        for k, v in self._DEFAULTS.items():
+            d[k] = v
+        d["amp_configs"] = {"init_loss_scaling": 32768.0, "use_pure_fp16": False, "use_bf16": True}
+        d["recompute_configs"] = {"checkpoints": []}
+        d["sharding_configs"] = {"sharding_degree": 1, "stage": 1, "segment_broadcast_MB": 32,
+                                 "offload": False}
+        d["pipeline_configs"] = {"accumulate_steps": 1, "micro_batch_size": 1}
+        d["tensor_parallel_configs"] = {"tensor_parallel_degree": 1}
+        d["gradient_merge_configs"] = {"k_steps": 1, "avg": True}
+        d["lamb_configs"] = {"lamb_weight_decay": 0.01, "exclude_from_weight_decay": []}
+        d["lars_configs"] = {"lars_coeff": 0.001, "lars_weight_decay": 0.0005, "epsilon": 0.0,
+                             "exclude_from_weight_decay": []}
+        d["gradient_scale_configs"] = {"scale_strategy": "avg"}
+        for k in ("localsgd_configs", "adaptive_localsgd_configs", "dgc_configs", "a_sync_configs",
+                  "qat_configs", "trainer_desc_configs", "sparse_table_configs", "fs_client_param"):
+            d[k] = {}
+
+    def __setattr__(self, k, v):
+        if k == "hybrid_configs":
+            return object.__setattr__(self, k, v)
+        if k in _CONFIG_KEYS:
+            allowed = _CONFIG_KEYS[k]
+            v = dict(v or {})
+            if allowed is not None:
+                bad = set(v) - allowed
+                if bad:
+                    raise ValueError(f"DistributedStrategy.{k}: unknown key(s) {sorted(bad)}")
+            self.__dict__[k].update(v)  # the reference merges configs into its defaults
+            return
+        if k not in self._DEFAULTS:
+            raise AttributeError(f"DistributedStrategy has no field {k!r}")
+        self.__dict__[k] = v
 
     @property
     def hybrid_configs(self):
@@ -59,9 +120,13 @@ class DistributedStrategy:
     def hybrid_configs(self, cfg):
         cfg = dict(cfg)
         pp = cfg.pop("pp_configs", None)
+        bad = set(cfg) - {"dp_degree", "mp_degree", "pp_degree", "sharding_degree", "sep_degree",
+                          "order", "mp_configs", "sharding_configs"}
+        if bad:
+            raise ValueError(f"DistributedStrategy.hybrid_configs: unknown key(s) {sorted(bad)}")
         self._hybrid.update(cfg)
         if pp:
-            self.pipeline_configs.update(pp)
+            self.pipeline_configs = pp
 
     def __repr__(self):
         return f"DistributedStrategy(hybrid={self._hybrid}, sharding={self.sharding}, amp={self.amp})"
@@ -82,7 +147,14 @@ def init(role_maker=None, is_collective=True, strategy=None, log_level="INFO"):
     if int(os.environ.get("WORLD_SIZE", "1")) > 1 or dist.is_initialized():
         init_parallel_env()
     world = dist.get_world_size() if dist.is_initialized() else 1
+    from .meta_optimizers import check_strategy
+    check_strategy(strategy)
     h = strategy.hybrid_configs
+    if strategy.tensor_parallel and int(h.get("mp_degree", 1)) == 1:
+        h["mp_degree"] = int(strategy.tensor_parallel_configs.get("tensor_parallel_degree", 1))
+    if strategy.cudnn_exhaustive_search:
+        from ...framework.flags import set_flags
+        set_flags({"FLAGS_cudnn_exhaustive_search": True})
     mp, pp = int(h.get("mp_degree", 1)), int(h.get("pp_degree", 1))
     sh = int(h.get("sharding_degree", 1))
     dp = int(h.get("dp_degree", -1))
@@ -194,13 +266,57 @@ def _coalesced_broadcast(tensors, src, group):
         _scatter_back(ts, flat)
 
 
+def _stage3_groups(hcg, st):
+    """(ZeRO axis, replica axis) when ``sharding_configs.stage == 3`` is on, else None: the
+    sharding axis (dp replicating it) when ``sharding_degree`` > 1, else the dp axis."""
+    if int((st.sharding_configs or {}).get("stage", 1)) != 3:
+        return None
+    sh, dp = hcg.get_sharding_parallel_world_size(), hcg.get_data_parallel_world_size()
+    if sh > 1:
+        return hcg.get_sharding_parallel_group(), (hcg.get_data_parallel_group() if dp > 1 else None)
+    if st.sharding:
+        return hcg.get_data_parallel_group(), None
+    return None
+
+
+def _wrap_stage3(model, hcg, st, groups):
+    from ..sharding import GroupShardedStage3
+    zero_g, rep_g = groups
+    excl = list(model.shared_layers.values()) if isinstance(model, PipelineLayer) else None
+    cfg = st.sharding_configs or {}
+    s3 = GroupShardedStage3(
+        model, group=zero_g, replica_group=rep_g, exclude_layer=excl,
+        offload=bool(cfg.get("offload", False)), sync_comm=bool(cfg.get("sync_comm", False)),
+        mp_group=hcg.get_model_parallel_group() if hcg.get_model_parallel_world_size() > 1 else None,
+        pp_group=hcg.get_pipe_parallel_group() if hcg.get_pipe_parallel_world_size() > 1 else None)
+    _STATE["stage3"] = s3
+    return s3
+
+
 def distributed_model(model):
     hcg = _STATE["hcg"]
     if hcg is None:
         return model
     st = _strategy()
+    from .meta_optimizers import apply_model_strategy, check_strategy
+    check_strategy(st)
+    apply_model_strategy(model, st)
     _STATE["model"] = model
     _STATE["wrapper"] = None
+    _STATE["stage3"] = None
+    s3_groups = _stage3_groups(hcg, st)
+    if s3_groups is not None:
+        # ZeRO-3 inside each pipeline stage / over tensor-parallel slices (BASELINE config 5:
+        # sharding stage 3 × pp): replicas start identical (wrappers broadcast), then each stage's
+        # layers are cut into per-block shards over the ZeRO axis
+        if isinstance(model, PipelineLayer) and hcg.get_pipe_parallel_world_size() > 1:
+            w = PipelineParallel(model, hcg, st)
+            w._stage3 = _wrap_stage3(model, hcg, st, s3_groups)
+        else:
+            _HybridModel(model, hcg)
+            w = _wrap_stage3(model, hcg, st, s3_groups)
+        _STATE["wrapper"] = w
+        return w
     if isinstance(model, PipelineLayer) and hcg.get_pipe_parallel_world_size() > 1:
         w = PipelineParallel(model, hcg, st)
     elif hcg.get_model_parallel_world_size() > 1 or hcg.get_sharding_parallel_world_size() > 1 or st.sharding:
@@ -263,7 +379,7 @@ class HybridParallelOptimizer:
             else:
                 shard_g, rep_g, st = dp_g, None, (stage if strategy.sharding else 0)
             # pipeline micro-batches accumulate into the grad buffer: reduce once, at step()
-            pp_acc = hcg.get_pipe_parallel_world_size() > 1 or \
+            pp_acc = hcg.get_pipe_parallel_world_size() > 1 or strategy.gradient_merge or \
                 int((strategy.pipeline_configs or {}).get("accumulate_steps", 1)) > 1
             apply = getattr(optimizer, "_apply_decay_param_fun", None)
             wd = optimizer._decay_coeff() if getattr(optimizer, "_decoupled", False) else 0.0
@@ -387,7 +503,12 @@ class HybridParallelOptimizer:
 
     clear_gradients = clear_grad
 
-    def minimize(self, loss, *a, **k):
+    def minimize(self, loss, startup_program=None, parameters=None, no_grad_set=None):
+        from ...static.framework import Variable as _SVar
+        if isinstance(loss, _SVar):  # static graph (reference fleet static meta-optimizers)
+            from .meta_optimizers import static_minimize
+            return static_minimize(self._inner, loss, self.strategy, self.hcg, startup_program,
+                                   parameters, no_grad_set)
         loss.backward()
         self.step()
 
@@ -404,7 +525,15 @@ def distributed_optimizer(optimizer, strategy=None):
     hcg = _STATE["hcg"]
     if hcg is None:
         return optimizer
-    return HybridParallelOptimizer(optimizer, hcg, _strategy())
+    st = _strategy()
+    from .meta_optimizers import check_strategy, swap_optimizer, wrap_optimizer
+    check_strategy(st)
+    optimizer = swap_optimizer(optimizer, st)
+    s3 = _STATE.get("stage3")
+    if s3 is not None:
+        from ..sharding import _Stage3Optimizer
+        return wrap_optimizer(_Stage3Optimizer(s3, optimizer), st)
+    return wrap_optimizer(HybridParallelOptimizer(optimizer, hcg, st), st)
 
 
 def distributed_scaler(scaler):

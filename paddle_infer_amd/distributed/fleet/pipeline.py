@@ -161,7 +161,9 @@ class PipelineLayer(Layer):
                     for f in _c:
                         inp = f(inp)
                     return inp
-                x = recompute(run, x)
+                # a chunk fed by no grad-requiring tensor (token ids into the embedding) runs
+                # plainly: recompute's autograd node would cut its parameters off the graph
+                x = recompute(run, x) if isinstance(x, torch.Tensor) and x.requires_grad else run(x)
             return x
         for f in fns:
             x = f(x)

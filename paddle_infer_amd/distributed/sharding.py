@@ -30,15 +30,24 @@ def _pg(group):
 class _Stage3Unit:
     """One block's parameters as a flat buffer sharded 1/N over the group: rank-local bf16/f32 shard
     + f32 master / Adam moments / gradient shard. The full buffer exists only while the block runs
-    (or always, for ``persistent`` units whose weights are used outside their own module)."""
+    (or always, for ``persistent`` units whose weights are used outside their own module).
 
-    def __init__(self, name, module, named, group, world, rank, persistent, decays):
+    ``offload`` keeps the f32 master and moments in pinned host memory and runs the update there
+    (reference `group_sharded_stage3.py:84-93`): device memory per parameter drops from 14 bytes
+    (bf16 shard + f32 grad/master/m/v) to 6. ``replica_group``: a data-parallel axis OVER the
+    sharding axis (hybrid dp × sharding) — reduced shards are averaged over it as well."""
+
+    def __init__(self, name, module, named, group, world, rank, persistent, offload=False,
+                 replica_group=None, mp_world=1):
         self.name, self.module, self.group, self.world, self.rank = name, module, group, world, rank
-        self.persistent = persistent
-        order = sorted(range(len(named)), key=lambda i: not decays[i])  # decay params first
+        self.persistent, self.offload = persistent, offload
+        self.replica_group = replica_group
+        self.replica_world = dist.get_world_size(replica_group) if replica_group is not None else 1
+        # matrices first: with the usual decay rule (no decay on biases / norms) the shard splits
+        # into one decay and one no-decay segment (`set_decay`)
+        order = sorted(range(len(named)), key=lambda i: named[i][1].dim() <= 1)
         self.names = [named[i][0] for i in order]
         self.params = [named[i][1] for i in order]
-        self.decay_numel = sum(self.params[i].numel() for i in range(len(order)) if decays[order[i]])
         dtype, dev = self.params[0].dtype, self.params[0].device
         self.shapes = [p.shape for p in self.params]
         self.numels = [p.numel() for p in self.params]
@@ -52,16 +61,46 @@ class _Stage3Unit:
         L = self.total // world
         self.L, self.lo = L, rank * L
         self.shard = full[self.lo:self.lo + L].clone()
-        self.master = self.shard.float()
-        self.m = torch.zeros(L, dtype=torch.float32, device=dev)
-        self.v = torch.zeros(L, dtype=torch.float32, device=dev)
+        host = offload and dev.type == "cuda"
+        self.master = self.shard.float().cpu().pin_memory() if host else self.shard.float()
+        sdev = self.master.device
+        self.m = torch.zeros(L, dtype=torch.float32, device=sdev)
+        self.v = torch.zeros(L, dtype=torch.float32, device=sdev)
+        if host:
+            self.m, self.v = self.m.pin_memory(), self.v.pin_memory()
+            self._host_grad = torch.empty(L, dtype=torch.float32).pin_memory()
         self.grad = torch.zeros(L, dtype=torch.float32, device=dev)
+        # grad-norm weight per shard range: a pipeline-shared copy that is not the first counts 0,
+        # a parameter replicated over tensor-parallel ranks 1/mp (the norm is summed over mp)
+        ws = [0.0 if getattr(p, "is_firstly_shared", True) is False else
+              (1.0 if mp_world == 1 or getattr(p, "is_distributed", False) else 1.0 / mp_world)
+              for p in self.params]
+        self.norm_segs = self._segments(ws)
+        self.decay_segs = [(0, L, True)]
         self.full, self.handle, self.gathered = None, None, False
         self.pending, self.reduced = 0, True
+        self._rs = None
         if persistent:
             self._bind(full)
         else:
             self.release(force=True)
+
+    def _segments(self, per_param):
+        """Runs of equal per-parameter values → [(a, b, value)] in shard-local coordinates."""
+        segs, o = [], 0
+        for val, n in zip(per_param, self.numels):
+            a, b = max(o, self.lo) - self.lo, min(o + n, self.lo + self.L) - self.lo
+            if b > a:
+                if segs and segs[-1][2] == val and segs[-1][1] == a:
+                    segs[-1] = (segs[-1][0], b, val)
+                else:
+                    segs.append((a, b, val))
+            o += n
+        return segs
+
+    def set_decay(self, flags):
+        """Per-parameter weight-decay flags (in ``self.params`` order) → shard segments."""
+        self.decay_segs = self._segments([bool(f) for f in flags])
 
     def _bind(self, full):
         o = 0
@@ -116,7 +155,10 @@ class _Stage3Unit:
                 full.copy_(self.shard)
 
     def reduce_grads(self):
-        """Reduce-scatter this block's gradients (param dtype on the wire) into the f32 shard."""
+        """Start reducing this block's gradients (param dtype on the wire) into the f32 shard: the
+        reduce-scatter runs asynchronously (RCCL's stream) while backward continues into the
+        previous block; `complete_reduce` folds it in."""
+        self.complete_reduce()  # a previous micro-batch's reduce of this block still in flight
         flat = torch.zeros(self.total, dtype=self.shard.dtype, device=self.shard.device)
         o = 0
         for p, n in zip(self.params, self.numels):
@@ -124,13 +166,25 @@ class _Stage3Unit:
                 flat[o:o + n].copy_(p.grad.reshape(-1))
                 p.grad = None
             o += n
+        self.reduced = True
         if self.world > 1:
             out = torch.empty(self.L, dtype=flat.dtype, device=flat.device)
-            dist.reduce_scatter_tensor(out, flat, group=self.group)
-            self.grad.add_(out.float(), alpha=1.0 / self.world)
+            h = dist.reduce_scatter_tensor(out, flat, group=self.group, async_op=True)
+            self._rs = (h, out, flat)
         else:
-            self.grad.add_(flat.float())
-        self.reduced = True
+            self._rs = (None, flat, flat)
+
+    def complete_reduce(self):
+        if self._rs is None:
+            return
+        h, out, _ = self._rs
+        self._rs = None
+        if h is not None:
+            h.wait()
+        g = out.float()
+        if self.replica_world > 1:
+            dist.all_reduce(g, group=self.replica_group)
+        self.grad.add_(g, alpha=1.0 / (self.world * self.replica_world))
 
 
 _CONTAINERS = (torch.nn.ModuleList, torch.nn.Sequential)
@@ -199,16 +253,31 @@ class GroupShardedStage3(torch.nn.Module):
     forward — the NEXT block's gather is issued asynchronously at the same time (prefetch along the
     recorded execution order, reverse order in backward, `group_sharded_stage3.py:399`) — and freed
     right after; backward re-gathers them, and once every weight gradient of the block exists they
-    are reduce-scattered into the block's f32 gradient shard and the full copy is freed again.
-    Peak parameter memory ≈ two blocks, not the model."""
+    are reduce-scattered (asynchronously, at most ``max_inflight`` blocks in flight so the full-size
+    gradient buffers stay bounded) into the block's f32 gradient shard and the full copy is freed
+    again. Peak parameter memory ≈ two blocks, not the model.
+
+    Composes with pipeline / tensor parallelism (reference `sharding_optimizer.py:127-134`: the
+    sharding axis inside each pipeline stage): wrap a stage's ``PipelineLayer`` (its micro-batches
+    accumulate into the block gradients; each block is reduced once its last micro-batch's backward
+    is done) with pipeline-shared layers as persistent units whose gradients are reduced only after
+    the pipeline's shared-weight all-reduce (`finalize_grads`); tensor-parallel layers shard their
+    local slices. ``replica_group`` is a data-parallel axis over the sharding axis."""
 
     def __init__(self, layer, optimizer=None, group=None, sync_buffers=False, segment_size=2 ** 20,
-                 offload=False, sync_comm=False, exclude_layer=None, apply_decay_param_fun=None):
+                 offload=False, sync_comm=False, exclude_layer=None, apply_decay_param_fun=None,
+                 replica_group=None, mp_group=None, pp_group=None, max_inflight=2):
         super().__init__()
         self._layer = layer
         self.group = _pg(group)
         self.world = dist.get_world_size(self.group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(self.group) if dist.is_initialized() else 0
+        self.replica_group = _pg(replica_group) if replica_group is not None else None
+        self.mp_group = _pg(mp_group) if mp_group is not None else None
+        self.pp_group = _pg(pp_group) if pp_group is not None else None
+        mp_world = dist.get_world_size(self.mp_group) if self.mp_group is not None else 1
+        self.offload, self.sync_comm = offload, sync_comm
+        self.max_inflight = 0 if sync_comm else max_inflight
         excl = list(exclude_layer or [])
         # models that pass one block's weights into the next block's kernels switch that off
         layer.apply(lambda m: setattr(m, "_zero3", True))
@@ -218,13 +287,14 @@ class GroupShardedStage3(torch.nn.Module):
                 mod = getattr(mod, part)
             if mod not in excl:
                 excl.append(mod)
-        decay_fn = apply_decay_param_fun or (lambda n: True)
         self.units = []
         for name, mod, named, persistent in _split_units(layer, excl):
-            decays = [bool(decay_fn(getattr(p, "pd_name", n))) for n, p in named]
             self.units.append(_Stage3Unit(name, mod, named, self.group, self.world, self.rank,
-                                          persistent, decays))
+                                          persistent, offload=offload, replica_group=self.replica_group,
+                                          mp_world=mp_world))
+        self.set_decay_fn(apply_decay_param_fun)
         self._order, self._recording = [], True
+        self._inflight = []
         self._root_units = [u for u in self.units if u.module is layer]
         for u in self.units:
             if u.module is layer or u.persistent:
@@ -239,6 +309,11 @@ class GroupShardedStage3(torch.nn.Module):
             layer.register_full_backward_pre_hook(lambda m, g: self._gather_root())
         self._optim = optimizer
 
+    def set_decay_fn(self, fn):
+        """Weight-decay rule (Paddle ``apply_decay_param_fun`` on parameter names; default: all)."""
+        for u in self.units:
+            u.set_decay([fn is None or bool(fn(getattr(p, "pd_name", n))) for n, p in zip(u.names, u.params)])
+
     # ---- forward / backward hooks
     def _neighbour(self, u, step):
         if self._recording or u not in self._order:
@@ -248,8 +323,11 @@ class GroupShardedStage3(torch.nn.Module):
 
     def _pre_forward(self, u):
         in_backward = torch._C._current_graph_task_id() != -1
-        if self._recording and not in_backward and u not in self._order:
-            self._order.append(u)
+        if self._recording and not in_backward:
+            if u in self._order:  # a second micro-batch (pipeline): the order is complete
+                self._recording = False
+            else:
+                self._order.append(u)
         u.gather()
         # a forward run INSIDE backward is a recompute: the next block's backward already ran,
         # so prefetching it would leave a gather nobody consumes (and a stale buffer after the
@@ -260,7 +338,8 @@ class GroupShardedStage3(torch.nn.Module):
 
     def _post_forward(self, u):
         if torch.is_grad_enabled():
-            u.pending = sum(1 for p in u.params if p.requires_grad)
+            # one more backward to wait for (micro-batches of a pipeline stage accumulate)
+            u.pending += sum(1 for p in u.params if p.requires_grad)
             u.reduced = False
         u.release()
 
@@ -276,9 +355,17 @@ class GroupShardedStage3(torch.nn.Module):
 
     def _grad_hook(self, u):
         u.pending -= 1
-        if u.pending == 0 and not u.reduced:
-            u.reduce_grads()
-            u.release()
+        # persistent units (pipeline-shared / tied weights) reduce in finalize_grads, after the
+        # cross-stage shared-weight all-reduce
+        if u.pending == 0 and not u.reduced and not u.persistent:
+            self._reduce(u)
+
+    def _reduce(self, u):
+        u.reduce_grads()
+        u.release()
+        self._inflight.append(u)
+        while len(self._inflight) > self.max_inflight:
+            self._inflight.pop(0).complete_reduce()
 
     def forward(self, *a, **k):
         for u in self._root_units:
@@ -295,13 +382,15 @@ class GroupShardedStage3(torch.nn.Module):
         return out
 
     def finalize_grads(self):
-        """Reduce every block whose gradients were not all produced (unused parameters): the same
-        fixed order on every rank keeps the collectives matched."""
+        """Reduce every block whose gradients were not all produced (unused parameters) and the
+        persistent ones: the same fixed order on every rank keeps the collectives matched."""
         for u in self.units:
-            if not u.reduced:
-                u.reduce_grads()
-                u.release()
+            if not u.reduced or u.persistent:
+                self._reduce(u)
             u.pending = 0
+        while self._inflight:
+            self._inflight.pop(0).complete_reduce()
+        for u in self.units:
             u.discard_prefetch()
 
     def shard_params_and_grads(self):
@@ -312,11 +401,14 @@ class GroupShardedStage3(torch.nn.Module):
         for u in self.units:
             u.gather()
 
+    def release_all(self):
+        for u in self.units:
+            u.release()
+
     def state_dict(self, *a, **k):
         self.get_all_parameters()
         sd = {kk: v.clone() for kk, v in self._layer.state_dict().items()}
-        for u in self.units:
-            u.release()
+        self.release_all()
         return sd
 
     def parameters(self, recurse=True):
@@ -325,8 +417,9 @@ class GroupShardedStage3(torch.nn.Module):
 
 class _Stage3Optimizer:
     """AdamW (Paddle semantics) over the rank-local f32 shards of a GroupShardedStage3 model: ONE
-    device-side global grad norm (sum of shard squares, all-reduced over the group) drives the
-    clip coefficient, which the fused flat AdamW kernel applies as its grad scale."""
+    device-side global grad norm (weighted shard squares, all-reduced over the sharding, tensor-
+    and pipeline-parallel groups) drives the clip coefficient, which the fused flat AdamW kernel
+    applies as its grad scale. Offloaded units update on the host copy."""
 
     def __init__(self, model: GroupShardedStage3, inner):
         from ..ops.optim import adamw_flat, sumsq
@@ -336,6 +429,25 @@ class _Stage3Optimizer:
         clip = getattr(inner, "_grad_clip", None)
         self.clip_norm = getattr(clip, "clip_norm", None)
         self.wd = inner._decay_coeff() if getattr(inner, "_decoupled", False) else 0.0
+        fn = getattr(inner, "_apply_decay_param_fun", None)
+        if fn is not None:
+            model.set_decay_fn(fn)
+
+    @torch.no_grad()
+    def _grad_norm_sq(self):
+        units = self.model.units
+        tot = torch.zeros((), dtype=torch.float32, device=units[0].grad.device)
+        for u in units:
+            for a, b, w in u.norm_segs:
+                if w == 1.0:
+                    self._sumsq(u.grad[a:b], out=tot, accumulate=True)
+                elif w:
+                    tot.add_(self._sumsq(u.grad[a:b]), alpha=w)
+        for g in (self.model.group if self.model.world > 1 else None, self.model.mp_group,
+                  self.model.pp_group):
+            if g is not None and dist.get_world_size(g) > 1:
+                dist.all_reduce(tot, group=g)
+        return tot
 
     @torch.no_grad()
     def step(self):
@@ -349,19 +461,16 @@ class _Stage3Optimizer:
         units = self.model.units
         coef = None
         if self.clip_norm is not None and units:
-            tot = torch.zeros((), dtype=torch.float32, device=units[0].grad.device)
-            for u in units:
-                self._sumsq(u.grad, out=tot, accumulate=True)
-            if self.model.world > 1:
-                dist.all_reduce(tot, group=self.model.group)
+            tot = self._grad_norm_sq()
             coef = torch.clamp(self.clip_norm / (tot.sqrt() + 1e-6), max=1.0).reshape(1)
         for u in units:
-            d = min(max(u.decay_numel - u.lo, 0), u.L)  # decay / no-decay split of this shard
-            for a, b, wd in ((0, d, self.wd), (d, u.L, 0.0)):
-                if b > a:
-                    self._adamw(u.master[a:b], u.m[a:b], u.v[a:b], u.grad[a:b], lr, b1, b2, eps, wd,
-                                self.t, grad_scale=coef)
-            u.shard.copy_(u.master)
+            host = u.master.device != u.grad.device
+            g = u._host_grad.copy_(u.grad) if host else u.grad
+            c = coef.cpu() if (host and coef is not None) else coef
+            for a, b, dec in u.decay_segs:
+                self._adamw(u.master[a:b], u.m[a:b], u.v[a:b], g[a:b], lr, b1, b2, eps,
+                            self.wd if dec else 0.0, self.t, grad_scale=c)
+            u.shard.copy_(u.master, non_blocking=host)
             u.refresh_persistent()
         bump_param_epoch()
         if hasattr(self.inner, "_step"):
@@ -375,8 +484,20 @@ class _Stage3Optimizer:
 
     clear_gradients = clear_grad
 
+    def minimize(self, loss, *a, **k):
+        loss.backward()
+        self.step()
+
     def get_lr(self):
         return self.inner.get_lr()
+
+    def set_lr(self, lr):
+        return self.inner.set_lr(lr)
+
+    def __getattr__(self, k):
+        if k in ("inner", "model"):
+            raise AttributeError(k)
+        return getattr(self.inner, k)
 
     def state_dict(self):
         return {f"{u.name}.{k}": getattr(u, k) for u in self.model.units for k in ("master", "m", "v")} | {"t": self.t}
@@ -386,10 +507,15 @@ def group_sharded_parallel(model, optimizer, level, scaler=None, group=None, off
                            sync_buffers=False, buffer_max_size=2 ** 23, segment_size=2 ** 20,
                            sync_comm=False, dp_group=None, exclude_layer=None):
     assert level in ("os", "os_g", "p_g_os"), level
+    if offload and level != "p_g_os":
+        raise NotImplementedError("offload is implemented for level 'p_g_os' (ZeRO-3); stage 1/2 keep "
+                                  "their f32 states on the device")
     pg = _pg(group) if group is not None else (dist.group.WORLD if dist.is_initialized() else None)
     if level == "p_g_os":
         m = GroupShardedStage3(model, optimizer, pg, segment_size=segment_size, exclude_layer=exclude_layer,
-                               apply_decay_param_fun=getattr(optimizer, "_apply_decay_param_fun", None))
+                               apply_decay_param_fun=getattr(optimizer, "_apply_decay_param_fun", None),
+                               offload=offload, sync_comm=sync_comm,
+                               replica_group=_pg(dp_group) if dp_group is not None else None)
         return m, _Stage3Optimizer(m, optimizer), scaler
     stage = 1 if level == "os" else 2
     old = getattr(optimizer, "_flat", None)

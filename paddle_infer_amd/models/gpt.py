@@ -393,7 +393,7 @@ class GPTDecoderLayerPipe(GPTDecoderLayer):
         else:
             h, out = x[0], x[1]
         h2, m, b = super().forward(h, out, None)
-        return torch.stack([h2, m + b])
+        return torch.stack([h2, m if b is None else m + b])
 
 
 class GPTFinalNormPipe(Layer):

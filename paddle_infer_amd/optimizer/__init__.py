@@ -231,6 +231,36 @@ class Momentum(Optimizer):
         mp.sub_(lr_ * (g + self._momentum * v if self._nesterov else v))
 
 
+class LarsMomentum(Momentum):
+    """LARS (reference `fluid/optimizer.py` LarsMomentumOptimizer / `lars_momentum` op): per-layer
+    local lr = lr · lars_coeff · ‖w‖ / (‖g‖ + lars_weight_decay · ‖w‖ + epsilon), then momentum
+    on (g + lars_weight_decay · w). Parameters whose name contains an entry of
+    ``exclude_from_weight_decay`` get no decay (and the plain lr)."""
+
+    def __init__(self, learning_rate=0.001, momentum=0.9, lars_coeff=0.001, lars_weight_decay=0.0005,
+                 parameters=None, grad_clip=None, name=None, exclude_from_weight_decay=None,
+                 epsilon=0.0, multi_precision=False, rescale_grad=1.0):
+        super().__init__(learning_rate, momentum, parameters, False, None, grad_clip, multi_precision,
+                         rescale_grad, name)
+        self._lars_coeff, self._lars_wd, self._lars_eps = lars_coeff, lars_weight_decay, epsilon
+        self._exclude = list(exclude_from_weight_decay or [])
+        self._merged_op = None
+
+    def _update(self, p, mp, g, lr_):
+        g = g * self._rescale
+        excluded = any(e in getattr(p, "pd_name", "") for e in self._exclude)
+        wd = 0.0 if excluded else self._lars_wd
+        v = self._acc("velocity", p)
+        if excluded:
+            local = lr_
+        else:
+            wn, gn = mp.norm(), g.norm()
+            ratio = self._lars_coeff * wn / (gn + wd * wn + self._lars_eps)
+            local = lr_ * torch.where((wn > 0) & (gn > 0), ratio, torch.ones_like(wn))
+        v.mul_(self._momentum).add_(local * (g + wd * mp))
+        mp.sub_(v)
+
+
 class Adam(Optimizer):
     _decoupled = False
 
@@ -433,4 +463,4 @@ class Lamb(Optimizer):
 
 
 __all__ = ["Optimizer", "SGD", "Momentum", "Adam", "AdamW", "Adamax", "Adagrad", "RMSProp",
-           "Adadelta", "Lamb", "L1Decay", "L2Decay", "lr"]
+           "Adadelta", "Lamb", "LarsMomentum", "L1Decay", "L2Decay", "lr"]

@@ -28,6 +28,7 @@ def _port():
     (2, ["--pp", "2", "--vpp", "2", "--accumulate", "2", "--num-layers", "4"], "pp2v2dp1", 2),
     (4, ["--sharding-degree", "2"], "sh2dp2_zero1", 8),
     (2, ["--sharding", "3"], "dp2_zero3", 4),
+    (4, ["--pp", "2", "--sharding-degree", "2", "--sharding", "3"], "pp2sh2dp1_zero3", 4),
 ])
 def test_bench_multirank_contract(n, extra, par, gb):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
@@ -45,3 +46,23 @@ def test_bench_multirank_contract(n, extra, par, gb):
     assert out["config"]["parallelism"] == par
     assert out["config"]["global_batch"] == gb
     assert out["value"] > 0 and out["final_loss"] == out["final_loss"]
+
+
+def test_bench_gpt13b_pp2_sharding3_rehearsal():
+    """BASELINE config 5's shape (GPT-3 13B, sharding stage 3 x pp 2) through the driver command,
+    4 of its 40 layers at seq 64 so it fits a CPU rehearsal: real 13B widths (hidden 5120, 40
+    heads, vocab 50304)."""
+    n = 4
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(n), "--steps", "1", "--warmup", "0", "--device", "cpu", "--model", "gpt3-13b",
+           "--num-layers", "4", "--pp", "2", "--sharding-degree", "2", "--sharding", "3",
+           "--seq", "64", "--micro-batch", "2"]
+    env = dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=ROOT)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["config"]["parallelism"] == "pp2sh2dp1_zero3"
+    assert out["config"]["params"] > 1.7e9 and out["final_loss"] == out["final_loss"]

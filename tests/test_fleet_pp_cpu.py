@@ -167,3 +167,99 @@ def test_stage3_with_recompute_matches_single():
         for k in ref_sd:
             torch.testing.assert_close(res[r]["sd"][k], ref_sd[k], rtol=2e-3, atol=3e-4,
                                        msg=lambda m, k=k: f"{k}: {m}")
+
+
+# ------------------------------------------------------------- ZeRO stage 3 x pipeline (config 5)
+def _pp_stage3_worker(rank, world, init, layers, tie, pp, sh, dp, accumulate, recompute, offload):
+    import torch.distributed as dist
+    from paddle_infer_amd.distributed import fleet
+    from paddle_infer_amd.models.gpt import (GPTForPretrainingPipe, gpt_pipe_load_full_state,
+                                             gpt_pipe_state_to_full)
+    st = fleet.DistributedStrategy()
+    st.hybrid_configs = {"dp_degree": dp, "mp_degree": 1, "pp_degree": pp, "sharding_degree": sh}
+    st.sharding_configs = {"stage": 3, "offload": offload}
+    st.pipeline_configs = {"accumulate_steps": accumulate}
+    fleet.init(is_collective=True, strategy=st)
+    hcg = fleet.get_hybrid_communicate_group()
+    cfg = _cfg(layers, tie)
+    pipe = GPTForPretrainingPipe(cfg, recompute_interval=1 if recompute else 0)
+    gpt_pipe_load_full_state(pipe, init, cfg)
+    full_numel = sum(p.numel() for p in pipe.parameters())
+    model = fleet.distributed_model(pipe)
+    opt = fleet.distributed_optimizer(_adamw(pipe.parameters()))
+    s3 = model._stage3
+    assert sum(u.name.startswith("_stage_layers.") for u in s3.units) >= layers // pp
+    # data axis = dp x sharding replicas of this stage
+    drank = hcg.get_data_parallel_rank() * sh + hcg.get_sharding_parallel_rank()
+    nrep = dp * sh
+    losses = []
+    for ids in _data():
+        n = ids.shape[0] // nrep
+        local = ids[drank * n:(drank + 1) * n]
+        loss = model.train_batch([local[:, :-1], local[:, 1:]], opt)
+        t = loss.detach().clone().reshape(1)
+        dist.all_reduce(t)  # every rank holds its replica's loss: mean over all ranks
+        losses.append(t.item() / world)
+    resident = sum(p.numel() for p in pipe.parameters())
+    s3.get_all_parameters()
+    sd = gpt_pipe_state_to_full(pipe, cfg)
+    s3.release_all()
+    return {"sd": sd, "losses": losses, "resident": resident, "full": full_numel}
+
+
+@pytest.mark.parametrize("pp,sh,dp,tie,recompute,offload", [
+    (2, 2, 1, True, False, False),   # BASELINE config 5 shape: sharding stage 3 x pp 2, tied head
+    (2, 2, 1, False, True, True),    # + recompute inside the stage, offloaded optimizer states
+])
+def test_pp_x_sharding_stage3_matches_single(pp, sh, dp, tie, recompute, offload):
+    from paddle_infer_amd.models.gpt import GPTForPretraining
+    layers, world = 4, pp * sh * dp
+    cfg = _cfg(layers, tie)
+    torch.manual_seed(0)
+    init = copy.deepcopy(GPTForPretraining(cfg).state_dict())
+    ref_sd, ref_losses = _single(cfg, init)
+    res = run_distributed(_pp_stage3_worker, world, init, layers, tie, pp, sh, dp, 2, recompute, offload)
+    _check(res, ref_sd, ref_losses, world)
+    for r in range(world):  # between steps a stage holds its shards + persistent (shared) tables
+        assert res[r]["resident"] < res[r]["full"], res[r]
+
+
+def _dp_sharding_stage3_worker(rank, world, init, dp, sh):
+    """Fleet ZeRO-3 over the sharding axis with a data-parallel axis replicating it."""
+    import torch.distributed as dist
+    from paddle_infer_amd.distributed import fleet
+    from paddle_infer_amd.models.gpt import GPTForPretraining
+    st = fleet.DistributedStrategy()
+    st.hybrid_configs = {"dp_degree": dp, "mp_degree": 1, "pp_degree": 1, "sharding_degree": sh}
+    st.sharding_configs = {"stage": 3}
+    fleet.init(is_collective=True, strategy=st)
+    hcg = fleet.get_hybrid_communicate_group()
+    cfg = _cfg(2, True)
+    net = GPTForPretraining(cfg)
+    net.set_state_dict(init)
+    model = fleet.distributed_model(net)
+    opt = fleet.distributed_optimizer(_adamw(net.parameters()))
+    assert type(model).__name__ == "GroupShardedStage3" and model.world == sh
+    drank = hcg.get_data_parallel_rank() * sh + hcg.get_sharding_parallel_rank()
+    losses = []
+    for ids in _data():
+        n = ids.shape[0] // world
+        local = ids[drank * n:(drank + 1) * n]
+        loss = model(local[:, :-1], labels=local[:, 1:])
+        loss.backward()
+        opt.step()
+        opt.clear_grad()
+        t = loss.detach().clone()
+        dist.all_reduce(t)
+        losses.append(t.item() / world)
+    return {"sd": model.state_dict(), "losses": losses}
+
+
+def test_dp_x_sharding_stage3_matches_single():
+    from paddle_infer_amd.models.gpt import GPTForPretraining
+    cfg = _cfg(2, True)
+    torch.manual_seed(0)
+    init = copy.deepcopy(GPTForPretraining(cfg).state_dict())
+    ref_sd, ref_losses = _single(cfg, init)
+    res = run_distributed(_dp_sharding_stage3_worker, 4, init, 2, 2)
+    _check(res, ref_sd, ref_losses, 4)

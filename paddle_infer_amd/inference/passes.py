@@ -16,7 +16,10 @@ a chain of Paddle ops and rewrites it into one fused op whose kernel is register
   linear_bias_act_fuse_pass       traced linear(no bias) + fused_bias_act → one GEMM with the
                                   bias+act epilogue (`ops.linear.linear_bias_act`)
   identity_reshape_clean_pass     reshape2(X, Shape=shape(X))          → (removed)
-  fused_multi_transformer_encoder_pass  pre-LN causal transformer layer → fused_multi_transformer
+  fused_multi_transformer_{encoder,decoder}[_fuse_qkv]_pass, multi_devices_* (fmt_passes.py)
+                                  exported LLM layer ops (+ KV-cache concat, + mp collectives)
+                                  → fused_multi_transformer with CacheKV / TimeStep / ring_id
+  fused_multi_transformer_encoder_traced_pass  traced pre-LN causal layer → fused_multi_transformer
   fuse_multi_transformer_layer_pass     consecutive fused_multi_transformer → one multi-layer op
   multihead_matmul_fuse_pass      fc(QKV) + head split + attention + merge → multihead_matmul
   flash_attn_packed_fuse_pass     split(QKV) + flash_attn               → flash_attn_packed
@@ -548,9 +551,10 @@ def _residual_add(g, base, other):
     return add
 
 
-def fused_multi_transformer_encoder_pass(g: Graph):
-    """Reference `fused_multi_transformer_encoder_pass.cc`: one pre-LN decoder-only transformer
-    layer of plain ops —
+def fused_multi_transformer_encoder_traced_pass(g: Graph):
+    """The traced-model form of `fused_multi_transformer_encoder_pass.cc` (the op-form passes over
+    exported programs live in `fmt_passes.py`): one pre-LN decoder-only transformer layer as a
+    ``jit.save``-traced program records it (after fc_fuse / self_attention_fuse) —
         ln1 = layer_norm(x); qkv = fc(ln1); attention (causal flash_attn over the head split);
         x2 = x + fc(attn); ln2 = layer_norm(x2); x3 = x2 + fc(fc(ln2, act))
     → one fused_multi_transformer op (the LLM inference kernels: fused LN prologues, packed QKV,
@@ -655,10 +659,18 @@ def fuse_multi_transformer_layer_pass(g: Graph):
     return n
 
 
+from .fmt_passes import (  # noqa: E402
+    PASS_ORDER as _FMT_ORDER,
+    fused_multi_transformer_decoder_fuse_qkv_pass, fused_multi_transformer_decoder_pass,
+    fused_multi_transformer_encoder_fuse_qkv_pass, multi_devices_fused_multi_transformer_decoder_fuse_qkv_pass,
+    multi_devices_fused_multi_transformer_encoder_fuse_qkv_pass)
+from .fmt_passes import fused_multi_transformer_encoder_pass_ops as fused_multi_transformer_encoder_pass  # noqa: E402
+
 GPU_PASSES = [
     "delete_dropout_op_pass", "identity_scale_op_clean_pass", "identity_reshape_clean_pass",
+    *_FMT_ORDER,  # the reference runs the LLM passes before the generic fc / attention fusions
     "conv_bn_fuse_pass", "embedding_eltwise_layernorm_fuse_pass", "self_attention_fuse_pass",
-    "fc_fuse_pass", "fc_act_fuse_pass", "fused_multi_transformer_encoder_pass",
+    "fc_fuse_pass", "fc_act_fuse_pass", "fused_multi_transformer_encoder_traced_pass",
     "fuse_multi_transformer_layer_pass", "multihead_matmul_fuse_pass", "flash_attn_packed_fuse_pass",
     "fc_elementwise_layernorm_fuse_pass", "skip_layernorm_fuse_pass", "linear_bias_act_fuse_pass",
 ]

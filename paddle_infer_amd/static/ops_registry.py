@@ -515,6 +515,21 @@ def _seq(ins, slot):
     return list(ins.get(slot) or [])
 
 
+def _ring_group(a):
+    """``ring_id`` of a tensor-parallel fused op → its process group (None: single rank / -1).
+    Ring 0 is the world group (reference `c_comm_init` ring 0)."""
+    import torch.distributed as dist
+    ring = a.get("ring_id", -1)
+    ring = -1 if ring is None else int(ring)
+    if ring < 0 or not dist.is_initialized() or dist.get_world_size() == 1:
+        return None
+    from ..distributed.collective import get_group
+    g = get_group(ring)
+    if g is None:
+        raise RuntimeError(f"ring_id {ring}: no communicator (create it with new_group first)")
+    return getattr(g, "pg", None) or dist.group.WORLD
+
+
 def _fmt_common(ins, a):
     """Slot → functional-argument mapping shared by the fused_multi_transformer variants
     (reference `fused_multi_transformer_op.cc:152-190`)."""
@@ -528,7 +543,8 @@ def _fmt_common(ins, a):
                 seq_lens=ins["SeqLengths"][0] if ins.get("SeqLengths") else None,
                 time_step=time_step, attn_mask=ins["SrcMask"][0] if ins.get("SrcMask") else None,
                 activation=a.get("act_method", "gelu"), trans_qkvw=bool(a.get("trans_qkvw", True)),
-                rotary_emb_dims=int(a.get("rotary_emb_dims", 0)), causal=bool(a.get("causal", False)))
+                rotary_emb_dims=int(a.get("rotary_emb_dims", 0)), causal=bool(a.get("causal", False)),
+                group=_ring_group(a))
 
 
 @register("fused_multi_transformer")

@@ -619,7 +619,7 @@ def _fmt_run(ins, a, layers, moe=False):
             x, layers, nh, int(a.get("num_kv_heads", 0) or 0) or None, kw["pre_layer_norm"],
             kw["epsilon"], IF._caches_from(caches), pos, lens, kw["attn_mask"], decode,
             kw["activation"], kw["rotary_emb_dims"], causal=kw["causal"] and kw["attn_mask"] is None,
-            moe_fn=True if moe else None)
+            group=kw["group"], moe_fn=True if moe else None)
     return {"Out": out, "CacheKVOut": caches or []}
 
 

@@ -61,7 +61,7 @@ def test_jit_save_refuses_unlowerable_op_unless_allowed(tmp_path):
 
 
 def test_gpt_export_rewritten_by_fused_multi_transformer_pass(tmp_path):
-    """Plain-op GPT program (jit.save lowering) → fused_multi_transformer_encoder_pass rewrites each
+    """Plain-op GPT program (jit.save lowering) → fused_multi_transformer_encoder_traced_pass rewrites each
     pre-LN causal layer, fuse_multi_transformer_layer_pass merges them into ONE op; logits match."""
     from paddle_infer_amd.models.gpt import GPTForPretraining, gpt_config
     torch.manual_seed(0)
@@ -72,7 +72,7 @@ def test_gpt_export_rewritten_by_fused_multi_transformer_pass(tmp_path):
     jit.save(jit.to_static(m, input_spec=[InputSpec([None, 16], "int64", "ids")]), path)
     pred = pinf.create_predictor(pinf.Config(path + ".pdmodel", path + ".pdiparams"))
     st = pred.pass_stats
-    assert st["fused_multi_transformer_encoder_pass"] == 3, st
+    assert st["fused_multi_transformer_encoder_traced_pass"] == 3, st
     assert st["fuse_multi_transformer_layer_pass"] == 2, st
     fmt = [o for o in pred.program.global_block().ops if o.type == "fused_multi_transformer"]
     assert len(fmt) == 1 and len(fmt[0].paddle_inputs["QKVW"]) == 3

@@ -37,7 +37,7 @@ def test_gpt_export_fused_multi_transformer_gpu(tmp_path):
     c.enable_use_gpu(256, 0)
     c.exp_enable_mixed_precision(pinf.PrecisionType.Bfloat16)
     pred = pinf.create_predictor(c)
-    assert pred.pass_stats["fused_multi_transformer_encoder_pass"] == 2
+    assert pred.pass_stats["fused_multi_transformer_encoder_traced_pass"] == 2
     ids = torch.randint(0, 512, (2, 64), device="cuda")
     mg = m.to("cuda")
     with torch.no_grad():

@@ -462,8 +462,11 @@ __device__ __forceinline__ float act_apply(float v, int act) {
 }
 
 // grid (N/32, ceil(M/32), KS); 256 threads = 4 waves splitting the k-blocks of this WG's K range.
+#ifndef WO_NT
+#define WO_NT 1
+#endif
 #ifndef WO_UNROLL
-#define WO_UNROLL 8  // k-blocks per wave per iteration: 8 x 16 B weight loads in flight per lane
+#define WO_UNROLL 8  // k-blocks per wave per iteration: 8 x 16 B weight loads in flight per lane (16: no gain, profiles/rocprof_decode_gpt1.3b_b1_r3_nt.txt)
 #endif
 // LNP (decode, KS == 1, M ≤ 8): the workgroup LayerNorms its input rows into LDS first (shifted-sum
 // statistics in one pass over registers, then γ/β), so the pre-LN of a transformer layer needs no
@@ -517,7 +520,18 @@ __global__ __launch_bounds__(256) void wo_gemm_kernel(
   bf16x8 xa[U][NMF];
   auto load_w = [&](int kb0, uint4 (&wd)[U]) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) wd[u] = wt[(long long)min(kb0 + 4 * u, kb_end - 1) * 64];
+    for (int u = 0; u < U; ++u) {
+      // weights are streamed exactly once per step: non-temporal loads keep them from evicting
+      // the activations / KV cache the other kernels of the step re-read from L2 / MALL
+      const uint4* src = wt + (long long)min(kb0 + 4 * u, kb_end - 1) * 64;
+#if WO_NT
+      typedef unsigned u32x4_nt __attribute__((ext_vector_type(4)));
+      const u32x4_nt t = __builtin_nontemporal_load(reinterpret_cast<const u32x4_nt*>(src));
+      wd[u] = make_uint4(t[0], t[1], t[2], t[3]);
+#else
+      wd[u] = *src;
+#endif
+    }
   };
   auto load_x = [&](int kb0, bf16x8 (&xd)[U][NMF]) {
 #pragma unroll

@@ -125,12 +125,13 @@ __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_ex
 // to the per-lane SOURCE address (guide §5.4 rule 21): physical chunk pc of row r holds logical
 // chunk pc ^ x(r). Rows past `rmax` are clamped (masked later); logical chunks past the head dim
 // (D < DP) re-read chunk 0 (in bounds, never consumed).
-template <int ROWS, int ROWB, int DCH>
+template <int ROWS, int ROWB, int DCH, int NWV = 4>
 __device__ __forceinline__ void glds_tile(const unsigned short* gbase, long long rstride, int row0,
                                           int rmax, char* tile, int w, int lane) {
   constexpr int CH = ROWB / 16;
   constexpr int PIECES = ROWS * CH / 64;
-  constexpr int PPW = PIECES / 4;
+  constexpr int PPW = PIECES / NWV;
+  static_assert(PPW * NWV == PIECES, "tile pieces must split evenly over the waves");
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
     const int P = w * PPW + i;
@@ -281,12 +282,14 @@ __device__ __forceinline__ s16x4_t lds_tr_at(const char* smem, int off) {
 // ------------------------------------------------------------------------------------------
 // Forward
 // ------------------------------------------------------------------------------------------
-template <int D, bool F16, bool CAUSAL, int FEAT>
-__global__ __launch_bounds__(256, 2) void fwd_kernel(FaArgs a) {
+// NW waves per workgroup, 32 query rows each (BM = 32·NW); NW = 8 shares every K/V tile fill
+// between twice the rows (half the LDS fill traffic per FLOP) at one workgroup per CU.
+template <int D, bool F16, bool CAUSAL, int FEAT, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void fwd_kernel(FaArgs a) {
   typedef ET<F16> E;
   typedef typename E::V8 V8;
   constexpr int DP = D > 64 ? 128 : 64;
-  constexpr int BM = 128, BN = 64;
+  constexpr int BM = 32 * NW, BN = 64;
   constexpr int KSTEPS = D / 16;
   constexpr int DT = D / 32;
   constexpr int ROWB = DP * 2;
@@ -355,8 +358,8 @@ __global__ __launch_bounds__(256, 2) void fwd_kernel(FaArgs a) {
 
   auto issue = [&](int t, int buf) {
     char* ks = smem + buf * 2 * TILE_B;
-    glds_tile<BN, ROWB, D / 8>(kbase, a.sks, t * BN, Sk - 1, ks, w, lane);
-    glds_tile<BN, ROWB, D / 8>(vbase, a.svs, t * BN, Sk - 1, ks + TILE_B, w, lane);
+    glds_tile<BN, ROWB, D / 8, NW>(kbase, a.sks, t * BN, Sk - 1, ks, w, lane);
+    glds_tile<BN, ROWB, D / 8, NW>(vbase, a.svs, t * BN, Sk - 1, ks + TILE_B, w, lane);
   };
   if (ntiles > 0) issue(0, 0);
   __syncthreads();
@@ -949,21 +952,37 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(FaArgs a) {
 // ------------------------------------------------------------------------------------------
 // Launchers (one per element type; the exported entry points in flash_attn.hip dispatch).
 // ------------------------------------------------------------------------------------------
-template <bool F16, int D, bool C>
-int launch_fwd_feat(const FaArgs& a, dim3 grid, hipStream_t st) {
+// forward waves per workgroup: PIAMD_FA_FWD_WAVES (4 or 8), read once
+inline int fwd_waves() {
+  static const int nw = [] {
+    const char* e = getenv("PIAMD_FA_FWD_WAVES");
+    return (e && atoi(e) == 8) ? 8 : 4;
+  }();
+  return nw;
+}
+
+template <bool F16, int D, bool C, int NW>
+int launch_fwd_nw(const FaArgs& a, hipStream_t st) {
+  const dim3 grid = fa_grid((long long)((a.Sq + 32 * NW - 1) / (32 * NW)) * a.Hq * a.B);
+  const dim3 blk(64 * NW);
   const int feat = (a.p_drop > 0.f ? F_DROP : 0) | (a.mask ? F_MASK : 0);
   switch (feat) {
-    case 0: hipLaunchKernelGGL((fwd_kernel<D, F16, C, 0>), grid, dim3(256), 0, st, a); break;
-    case 1: hipLaunchKernelGGL((fwd_kernel<D, F16, C, 1>), grid, dim3(256), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((fwd_kernel<D, F16, C, 2>), grid, dim3(256), 0, st, a); break;
-    default: hipLaunchKernelGGL((fwd_kernel<D, F16, C, 3>), grid, dim3(256), 0, st, a); break;
+    case 0: hipLaunchKernelGGL((fwd_kernel<D, F16, C, 0, NW>), grid, blk, 0, st, a); break;
+    case 1: hipLaunchKernelGGL((fwd_kernel<D, F16, C, 1, NW>), grid, blk, 0, st, a); break;
+    case 2: hipLaunchKernelGGL((fwd_kernel<D, F16, C, 2, NW>), grid, blk, 0, st, a); break;
+    default: hipLaunchKernelGGL((fwd_kernel<D, F16, C, 3, NW>), grid, blk, 0, st, a); break;
   }
   return (int)hipGetLastError();
 }
 
+template <bool F16, int D, bool C>
+int launch_fwd_feat(const FaArgs& a, dim3 /*grid*/, hipStream_t st) {
+  return fwd_waves() == 8 ? launch_fwd_nw<F16, D, C, 8>(a, st) : launch_fwd_nw<F16, D, C, 4>(a, st);
+}
+
 template <bool F16>
 int launch_fwd(const FaArgs& a, hipStream_t st) {
-  const dim3 grid = fa_grid((long long)((a.Sq + 127) / 128) * a.Hq * a.B);
+  const dim3 grid(1);
 #define FWD_D(DD) return a.causal ? launch_fwd_feat<F16, DD, true>(a, grid, st) \
                                   : launch_fwd_feat<F16, DD, false>(a, grid, st)
   switch (a.D) {

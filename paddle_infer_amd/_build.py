@@ -9,6 +9,9 @@
 * ``_lib/piamd_agemm.hsaco`` — the hand-scheduled assembly GEMM kernels: ``csrc/asm/gemm_gen.py``
   emits the gfx950 assembly, clang assembles it and ld.lld links the code object (loaded at run
   time by ``csrc/kernels/agemm_host.hip`` through ``hipModuleLoad``).
+* ``_lib/libpiamd_infer.so`` + ``_lib/pd_infer_run`` — the native C++ inference engine and its
+  command-line driver (``csrc/native``: reference ``paddle_inference_api.h`` Config / Predictor /
+  Tensor with no Python at run time; CPU loops and gfx950 HIP kernels + rocBLAS).
 * ``_lib/libpiamd_capi.so`` — the C inference API (``csrc/capi``: reference ``capi_exp``
   ``pd_inference_api.h``), g++ against the embedded Python runtime.
 
@@ -33,6 +36,9 @@ KERNEL_LIB = os.path.join(LIBDIR, "libpiamd_kernels.so")
 RUNTIME_LIB = os.path.join(LIBDIR, "libpiamd_runtime.so")
 CDIR = os.path.join(ROOT, "csrc", "capi")
 CAPI_LIB = os.path.join(LIBDIR, "libpiamd_capi.so")
+NDIR = os.path.join(ROOT, "csrc", "native")
+NATIVE_LIB = os.path.join(LIBDIR, "libpiamd_infer.so")
+NATIVE_RUN = os.path.join(LIBDIR, "pd_infer_run")
 ADIR = os.path.join(ROOT, "csrc", "alloc")
 ALLOC_LIB = os.path.join(LIBDIR, "libpiamd_alloc.so")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
@@ -116,6 +122,46 @@ def build_asm(verbose: bool = True) -> bool:
     return True
 
 
+def build_native(verbose: bool = True, jobs: int = 4) -> None:
+    """csrc/native → libpiamd_infer.so (hipcc: gfx950 kernels + host C++, rocBLAS) and the
+    pd_infer_run driver linked against it (rpath $ORIGIN)."""
+    srcs = sorted(glob.glob(os.path.join(NDIR, "*.cc")) + glob.glob(os.path.join(NDIR, "*.hip")))
+    lib_srcs = [x for x in srcs if not x.endswith("pd_infer_run.cc")]
+    objdir = os.path.join(OBJDIR, "native")
+    os.makedirs(objdir, exist_ok=True)
+    hdr = _newest_header(NDIR)
+    todo, objs = [], []
+    for src in lib_srcs:
+        o = os.path.join(objdir, os.path.basename(src) + ".o")
+        objs.append(o)
+        if not os.path.exists(o) or os.path.getmtime(o) < max(os.path.getmtime(src), hdr):
+            flags = ["-O3", "-std=c++17", "-fPIC"]
+            if src.endswith(".hip"):
+                cmd = [HIPCC, *flags, f"--offload-arch={ARCH}", "-c", src, "-o", o]
+            else:
+                cmd = ["g++", *flags, "-Wall", "-pthread", "-c", src, "-o", o]
+            todo.append((cmd, src))
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+            for f in cf.as_completed([ex.submit(_compile, c, src) for c, src in todo]):
+                if verbose:
+                    print(f"[piamd build] compiled native/{os.path.basename(f.result())}", flush=True)
+    if todo or not os.path.exists(NATIVE_LIB):
+        _compile([HIPCC, "-shared", *objs, "-o", NATIVE_LIB + ".tmp", f"--offload-arch={ARCH}",
+                  f"-L{ROCM}/lib", "-lrocblas", "-pthread", f"-Wl,-rpath,{ROCM}/lib"], NATIVE_LIB)
+        os.replace(NATIVE_LIB + ".tmp", NATIVE_LIB)
+        if verbose:
+            print(f"[piamd build] linked {NATIVE_LIB}", flush=True)
+    run_src = os.path.join(NDIR, "pd_infer_run.cc")
+    if not os.path.exists(NATIVE_RUN) or os.path.getmtime(NATIVE_RUN) < max(
+            os.path.getmtime(run_src), os.path.getmtime(NATIVE_LIB), hdr):
+        _compile(["g++", "-O2", "-std=c++17", run_src, "-o", NATIVE_RUN + ".tmp", f"-L{LIBDIR}",
+                  "-lpiamd_infer", "-Wl,-rpath,$ORIGIN", f"-Wl,-rpath,{ROCM}/lib"], run_src)
+        os.replace(NATIVE_RUN + ".tmp", NATIVE_RUN)
+        if verbose:
+            print(f"[piamd build] linked {NATIVE_RUN}", flush=True)
+
+
 def build(verbose: bool = True, jobs: int | None = None) -> None:
     jobs = jobs or min(8, os.cpu_count() or 4)
     os.makedirs(LIBDIR, exist_ok=True)
@@ -133,6 +179,7 @@ def build(verbose: bool = True, jobs: int | None = None) -> None:
         _build_lib(asrcs, ALLOC_LIB, "g++", CXX_FLAGS + ["-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include"],
                    ["-pthread", f"-L{ROCM}/lib", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"],
                    _newest_header(ADIR), verbose, jobs)
+    build_native(verbose, jobs)
     csrcs = sorted(glob.glob(os.path.join(CDIR, "*.cc")))
     if csrcs:
         import sysconfig

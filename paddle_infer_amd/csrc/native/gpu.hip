@@ -1,0 +1,325 @@
+// MI355X side of the native engine: device buffers, one HIP stream + rocBLAS handle per
+// predictor, and the HIP kernels behind kernels.h (f32 element-wise / broadcast, row softmax and
+// LayerNorm with wave64 reductions, n-d strided copies for the layout ops, row gathers, casts).
+// GEMMs go to rocBLAS (plain library GEMMs; the fused transformer kernels live in the framework).
+#include <hip/hip_runtime.h>
+#include <rocblas/rocblas.h>
+
+#include <cmath>
+#include <cstdlib>
+
+#include "kernels.h"
+
+#define HIPCHK(x)                                                                          \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess) throw std::runtime_error(std::string("HIP: ") + hipGetErrorString(e_)); \
+  } while (0)
+
+namespace pdn {
+
+Buffer::~Buffer() {
+  if (!p) return;
+  if (dev) (void)hipFree(p);
+  else std::free(p);
+}
+
+std::shared_ptr<Buffer> alloc_buffer(size_t bytes, bool dev) {
+  auto b = std::make_shared<Buffer>();
+  b->bytes = bytes;
+  b->dev = dev;
+  const size_t n = bytes ? bytes : 4;
+  if (dev) HIPCHK(hipMalloc(&b->p, n));
+  else b->p = std::malloc(n);
+  return b;
+}
+
+void dev_init(Ctx& c) {
+  HIPCHK(hipSetDevice(c.device));
+  hipStream_t s;
+  HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  c.stream = s;
+  rocblas_handle h;
+  if (rocblas_create_handle(&h) != rocblas_status_success) throw std::runtime_error("rocblas_create_handle");
+  rocblas_set_stream(h, s);
+  c.blas = h;
+}
+
+void dev_release(Ctx& c) {
+  if (c.blas) rocblas_destroy_handle((rocblas_handle)c.blas);
+  if (c.stream) (void)hipStreamDestroy((hipStream_t)c.stream);
+  c.blas = c.stream = nullptr;
+}
+
+void dev_copy(void* dst, const void* src, size_t bytes, int kind, Ctx& c) {
+  const hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost
+                                                                         : hipMemcpyDeviceToDevice;
+  HIPCHK(hipMemcpyAsync(dst, src, bytes, k, (hipStream_t)c.stream));
+  if (kind == 1) HIPCHK(hipStreamSynchronize((hipStream_t)c.stream));
+}
+
+void dev_sync(Ctx& c) { HIPCHK(hipStreamSynchronize((hipStream_t)c.stream)); }
+
+DTensor to_device(const DTensor& t, Ctx& c) {
+  if (t.on_dev()) return t;
+  DTensor d = t;
+  d.buf = alloc_buffer(t.nbytes(), true);
+  if (t.nbytes()) dev_copy(d.buf->p, t.buf->p, t.nbytes(), 0, c);
+  return d;
+}
+
+DTensor to_host(const DTensor& t, Ctx& c) {
+  if (!t.on_dev()) return t;
+  DTensor h = t;
+  h.buf = alloc_buffer(t.nbytes(), false);
+  if (t.nbytes()) dev_copy(h.buf->p, t.buf->p, t.nbytes(), 1, c);
+  return h;
+}
+
+namespace gpu {
+namespace {
+
+inline unsigned blocks(int64_t n, int per = 256) {
+  const int64_t b = (n + per - 1) / per;
+  return (unsigned)std::min<int64_t>(std::max<int64_t>(b, 1), 1 << 20);
+}
+inline hipStream_t S(Ctx& c) { return (hipStream_t)c.stream; }
+
+__device__ __forceinline__ float unary_f(int op, float x, float p0, float p1) {
+  switch (op) {
+    case U_IDENT: return x;
+    case U_RELU: return x > 0.f ? x : 0.f;
+    case U_GELU: return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+    case U_GELU_TANH: return 0.5f * x * (1.f + tanhf(0.7978845608028654f * (x + 0.044715f * x * x * x)));
+    case U_TANH: return tanhf(x);
+    case U_SIGMOID: return 1.f / (1.f + __expf(-x));
+    case U_SILU: return x / (1.f + __expf(-x));
+    case U_EXP: return __expf(x);
+    case U_SQRT: return sqrtf(x);
+    case U_RSQRT: return rsqrtf(x);
+    case U_ABS: return fabsf(x);
+    case U_SCALE: return x * p0 + p1;
+    case U_SCALE_PRE: return (x + p1) * p0;
+  }
+  return x;
+}
+
+__global__ void unary_k(int op, const float* __restrict__ x, float* __restrict__ y, int64_t n,
+                        float p0, float p1) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = unary_f(op, x[i], p0, p1);
+}
+
+__device__ __forceinline__ float binary_f(int op, float a, float b) {
+  switch (op) {
+    case B_ADD: return a + b;
+    case B_SUB: return a - b;
+    case B_MUL: return a * b;
+    case B_DIV: return a / b;
+    case B_MAX: return fmaxf(a, b);
+    case B_MIN: return fminf(a, b);
+    case B_POW: return powf(a, b);
+  }
+  return a;
+}
+
+__global__ void binary_k(int op, const float* __restrict__ a, const float* __restrict__ b,
+                         float* __restrict__ y, Bcast bc) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < bc.n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = i, oa = 0, ob = 0;
+    for (int d = bc.nd - 1; d >= 0; --d) {
+      const int64_t q = r % bc.dims[d];
+      r /= bc.dims[d];
+      oa += q * bc.sa[d];
+      ob += q * bc.sb[d];
+    }
+    y[i] = binary_f(op, a[oa], b[ob]);
+  }
+}
+
+// block = one (outer, inner) row of n elements; 256 threads, wave64 shuffles + 4-slot LDS
+__device__ __forceinline__ float block_max(float v, float* sh) {
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  v = fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
+  __syncthreads();
+  return v;
+}
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  v = sh[0] + sh[1] + sh[2] + sh[3];
+  __syncthreads();
+  return v;
+}
+
+__global__ __launch_bounds__(256) void softmax_k(const float* __restrict__ x, float* __restrict__ y,
+                                                 int64_t n, int64_t inner) {
+  __shared__ float sh[4];
+  const int64_t row = blockIdx.x, o = row / inner, j = row % inner;
+  const float* xr = x + o * n * inner + j;
+  float* yr = y + o * n * inner + j;
+  float m = -INFINITY;
+  for (int64_t i = threadIdx.x; i < n; i += 256) m = fmaxf(m, xr[i * inner]);
+  m = block_max(m, sh);
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += 256) {
+    const float e = __expf(xr[i * inner] - m);
+    yr[i * inner] = e;
+    s += e;
+  }
+  const float inv = 1.f / block_sum(s, sh);
+  for (int64_t i = threadIdx.x; i < n; i += 256) yr[i * inner] *= inv;
+}
+
+__global__ __launch_bounds__(256) void layernorm_k(const float* __restrict__ x, const float* __restrict__ g,
+                                                   const float* __restrict__ b, float* __restrict__ y,
+                                                   int64_t cols, float eps) {
+  __shared__ float sh[4];
+  const float* xr = x + (int64_t)blockIdx.x * cols;
+  float* yr = y + (int64_t)blockIdx.x * cols;
+  float s = 0.f;
+  for (int64_t c = threadIdx.x; c < cols; c += 256) s += xr[c];
+  const float mu = block_sum(s, sh) / cols;
+  float s2 = 0.f;
+  for (int64_t c = threadIdx.x; c < cols; c += 256) {
+    const float d = xr[c] - mu;
+    s2 += d * d;
+  }
+  const float rs = rsqrtf(block_sum(s2, sh) / cols + eps);
+  for (int64_t c = threadIdx.x; c < cols; c += 256)
+    yr[c] = (xr[c] - mu) * rs * (g ? g[c] : 1.f) + (b ? b[c] : 0.f);
+}
+
+template <typename T>
+__global__ void strided_k(const T* __restrict__ src, T* __restrict__ dst, Strided s) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < s.n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = i, off = s.offset;
+    for (int d = s.nd - 1; d >= 0; --d) {
+      off += (r % s.dims[d]) * s.stride[d];
+      r /= s.dims[d];
+    }
+    dst[i] = src[off];
+  }
+}
+
+__global__ void gather_k(const float* __restrict__ table, const void* __restrict__ ids, int i64,
+                         float* __restrict__ y, int64_t n, int64_t width, int64_t rows, int64_t pad) {
+  const int64_t total = n * width;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / width, c = i % width;
+    const int64_t id = i64 ? ((const int64_t*)ids)[r] : ((const int32_t*)ids)[r];
+    y[i] = (id == pad || id < 0 || id >= rows) ? 0.f : table[id * width + c];
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ double ldv(const void* p, int64_t i) { return (double)((const T*)p)[i]; }
+
+__device__ double load_any(const void* p, int dt, int64_t i) {
+  switch (dt) {
+    case VT_FP32: return ldv<float>(p, i);
+    case VT_FP64: return ldv<double>(p, i);
+    case VT_INT64: return ldv<int64_t>(p, i);
+    case VT_INT32: return ldv<int32_t>(p, i);
+    case VT_INT16: return ldv<int16_t>(p, i);
+    case VT_INT8: return ldv<int8_t>(p, i);
+    case VT_UINT8: return ldv<uint8_t>(p, i);
+    case VT_BOOL: return ((const uint8_t*)p)[i] ? 1.0 : 0.0;
+  }
+  return 0.0;
+}
+__device__ void store_any(void* p, int dt, int64_t i, double v) {
+  switch (dt) {
+    case VT_FP32: ((float*)p)[i] = (float)v; break;
+    case VT_FP64: ((double*)p)[i] = v; break;
+    case VT_INT64: ((int64_t*)p)[i] = (int64_t)v; break;
+    case VT_INT32: ((int32_t*)p)[i] = (int32_t)v; break;
+    case VT_INT16: ((int16_t*)p)[i] = (int16_t)v; break;
+    case VT_INT8: ((int8_t*)p)[i] = (int8_t)v; break;
+    case VT_UINT8: ((uint8_t*)p)[i] = (uint8_t)v; break;
+    case VT_BOOL: ((uint8_t*)p)[i] = v != 0.0; break;
+  }
+}
+
+__global__ void cast_k(const void* x, int dtx, void* y, int dty, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    store_any(y, dty, i, load_any(x, dtx, i));
+}
+__global__ void fill_k(void* y, int dt, int64_t n, double v) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    store_any(y, dt, i, v);
+}
+
+__global__ __launch_bounds__(256) void reduce_k(const float* __restrict__ x, float* __restrict__ y, int64_t n,
+                                                int64_t inner, int mean) {
+  __shared__ float sh[4];
+  const int64_t row = blockIdx.x, o = row / inner, j = row % inner;
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += 256) s += x[(o * n + i) * inner + j];
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) y[row] = mean ? s / n : s;
+}
+
+}  // namespace
+
+void unary(Ctx& c, int op, const float* x, float* y, int64_t n, float p0, float p1) {
+  if (n) hipLaunchKernelGGL(unary_k, dim3(blocks(n)), dim3(256), 0, S(c), op, x, y, n, p0, p1);
+}
+void binary(Ctx& c, int op, const float* a, const float* b, float* y, const Bcast& bc) {
+  if (bc.n) hipLaunchKernelGGL(binary_k, dim3(blocks(bc.n)), dim3(256), 0, S(c), op, a, b, y, bc);
+}
+void softmax(Ctx& c, const float* x, float* y, int64_t outer, int64_t n, int64_t inner) {
+  if (outer * inner) hipLaunchKernelGGL(softmax_k, dim3((unsigned)(outer * inner)), dim3(256), 0, S(c), x, y, n, inner);
+}
+void layernorm(Ctx& c, const float* x, const float* g, const float* b, float* y, int64_t rows,
+               int64_t cols, float eps) {
+  if (rows) hipLaunchKernelGGL(layernorm_k, dim3((unsigned)rows), dim3(256), 0, S(c), x, g, b, y, cols, eps);
+}
+void strided_copy(Ctx& c, const void* src, void* dst, int elem, const Strided& s) {
+  if (!s.n) return;
+  switch (elem) {
+    case 1: hipLaunchKernelGGL(strided_k<uint8_t>, dim3(blocks(s.n)), dim3(256), 0, S(c), (const uint8_t*)src, (uint8_t*)dst, s); break;
+    case 2: hipLaunchKernelGGL(strided_k<uint16_t>, dim3(blocks(s.n)), dim3(256), 0, S(c), (const uint16_t*)src, (uint16_t*)dst, s); break;
+    case 4: hipLaunchKernelGGL(strided_k<uint32_t>, dim3(blocks(s.n)), dim3(256), 0, S(c), (const uint32_t*)src, (uint32_t*)dst, s); break;
+    case 8: hipLaunchKernelGGL(strided_k<uint64_t>, dim3(blocks(s.n)), dim3(256), 0, S(c), (const uint64_t*)src, (uint64_t*)dst, s); break;
+    default: throw std::runtime_error("strided_copy: element size");
+  }
+}
+void gather_rows(Ctx& c, const float* table, const void* ids, int ids_i64, float* y, int64_t n,
+                 int64_t width, int64_t rows, int64_t padding_idx) {
+  if (n * width)
+    hipLaunchKernelGGL(gather_k, dim3(blocks(n * width)), dim3(256), 0, S(c), table, ids, ids_i64, y, n, width, rows, padding_idx);
+}
+void gemm(Ctx& c, bool ta, bool tb, int64_t M, int64_t N, int64_t K, float alpha, const float* A,
+          int64_t lda, int64_t sA, const float* B, int64_t ldb, int64_t sB, float beta, float* C,
+          int64_t ldc, int64_t sC, int64_t batch) {
+  // row-major C = op(A)·op(B)  ⇔  column-major Cᵀ = op(B)ᵀ·op(A)ᵀ
+  const rocblas_operation oa = ta ? rocblas_operation_transpose : rocblas_operation_none;
+  const rocblas_operation ob = tb ? rocblas_operation_transpose : rocblas_operation_none;
+  const rocblas_status st = rocblas_sgemm_strided_batched(
+      (rocblas_handle)c.blas, ob, oa, (rocblas_int)N, (rocblas_int)M, (rocblas_int)K, &alpha, B,
+      (rocblas_int)ldb, sB, A, (rocblas_int)lda, sA, &beta, C, (rocblas_int)ldc, sC, (rocblas_int)batch);
+  if (st != rocblas_status_success) throw std::runtime_error("rocblas_sgemm_strided_batched failed");
+}
+void cast(Ctx& c, const void* x, int dtx, void* y, int dty, int64_t n) {
+  if (n) hipLaunchKernelGGL(cast_k, dim3(blocks(n)), dim3(256), 0, S(c), x, dtx, y, dty, n);
+}
+void fill(Ctx& c, void* y, int dt, int64_t n, double v) {
+  if (n) hipLaunchKernelGGL(fill_k, dim3(blocks(n)), dim3(256), 0, S(c), y, dt, n, v);
+}
+void reduce(Ctx& c, const float* x, float* y, int64_t outer, int64_t n, int64_t inner, bool mean) {
+  if (outer * inner) hipLaunchKernelGGL(reduce_k, dim3((unsigned)(outer * inner)), dim3(256), 0, S(c), x, y, n, inner, (int)mean);
+}
+
+void copy2d(Ctx& c, const void* src, int64_t spitch, void* dst, int64_t dpitch, int64_t rows,
+            int64_t cols, int elem) {
+  if (rows * cols)
+    HIPCHK(hipMemcpy2DAsync(dst, (size_t)(dpitch * elem), src, (size_t)(spitch * elem), (size_t)(cols * elem),
+                            (size_t)rows, hipMemcpyDeviceToDevice, S(c)));
+}
+
+}  // namespace gpu
+}  // namespace pdn

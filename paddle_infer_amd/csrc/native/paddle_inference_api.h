@@ -1,0 +1,109 @@
+// Native C++ inference API — no Python, no PyTorch at run time.
+//
+// Parity: reference `paddle/fluid/inference/api/paddle_inference_api.h:80` (namespace
+// paddle_infer: Config, Predictor, Tensor, CreatePredictor, GetVersion) and
+// `paddle_analysis_config.h` (SetModel, EnableUseGpu, DisableGpu, SetCpuMathLibraryNumThreads,
+// SwitchIrOptim). A Predictor loads a Paddle `.pdmodel` (framework.proto ProgramDesc, decoded by
+// a hand-written wire reader) and `.pdiparams` (save_combine tensor stream), and executes block 0
+// op by op with its own kernels: plain C++ on the CPU; on the MI355X, HIP kernels for the
+// element-wise / normalisation / layout ops and rocBLAS for the GEMMs, one HIP stream per
+// predictor, device memory held for the predictor's lifetime.
+//
+// Op set (the exported-inference core): feed, fetch, matmul_v2, matmul, mul, fc,
+// elementwise_{add,sub,mul,div,max,min,pow}, scale, relu, gelu, tanh, sigmoid, silu, swish, exp,
+// sqrt, rsqrt, abs, softmax, layer_norm, lookup_table(_v2), transpose(2), reshape(2),
+// unsqueeze(2), squeeze(2), flatten_contiguous_range, concat, split, slice, cast, fill_constant,
+// assign, dropout (inference), reduce_mean, reduce_sum. Anything else is rejected when the model
+// is loaded (the reference predictor refuses unregistered ops the same way).
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace paddle_infer {
+
+enum class DataType { FLOAT32 = 0, INT64 = 1, INT32 = 2, UINT8 = 3, INT8 = 4, FLOAT16 = 5, BOOL = 6 };
+enum class PlaceType { kUNK = -1, kCPU = 0, kGPU = 1 };
+
+class Config {
+ public:
+  Config() = default;
+  Config(const std::string& prog_file, const std::string& params_file)
+      : prog_file_(prog_file), params_file_(params_file) {}
+  void SetModel(const std::string& prog_file, const std::string& params_file) {
+    prog_file_ = prog_file;
+    params_file_ = params_file;
+  }
+  const std::string& prog_file() const { return prog_file_; }
+  const std::string& params_file() const { return params_file_; }
+  void EnableUseGpu(uint64_t memory_pool_init_size_mb, int device_id = 0) {
+    use_gpu_ = true;
+    device_id_ = device_id;
+    (void)memory_pool_init_size_mb;
+  }
+  void DisableGpu() { use_gpu_ = false; }
+  bool use_gpu() const { return use_gpu_; }
+  int gpu_device_id() const { return device_id_; }
+  void SetCpuMathLibraryNumThreads(int n) { cpu_threads_ = n; }
+  int cpu_math_library_num_threads() const { return cpu_threads_; }
+  void SwitchIrOptim(bool on = true) { ir_optim_ = on; }
+  bool ir_optim() const { return ir_optim_; }
+  void EnableMemoryOptim(bool on = true) { mem_optim_ = on; }
+  bool enable_memory_optim() const { return mem_optim_; }
+
+ private:
+  std::string prog_file_, params_file_;
+  bool use_gpu_ = false, ir_optim_ = true, mem_optim_ = true;
+  int device_id_ = 0, cpu_threads_ = 1;
+};
+
+class PredictorImpl;
+struct TensorSlot;
+
+class Tensor {
+ public:
+  void Reshape(const std::vector<int>& shape);
+  template <typename T>
+  void CopyFromCpu(const T* data);
+  template <typename T>
+  void CopyToCpu(T* data) const;
+  std::vector<int> shape() const;
+  DataType type() const;
+  const std::string& name() const { return name_; }
+  PlaceType place() const;
+
+ private:
+  friend class PredictorImpl;
+  friend class Predictor;
+  Tensor(PredictorImpl* p, std::string name, bool input) : p_(p), name_(std::move(name)), input_(input) {}
+  PredictorImpl* p_;
+  std::string name_;
+  bool input_;
+  std::vector<int> pending_shape_;
+};
+
+class Predictor {
+ public:
+  explicit Predictor(const Config& config);
+  ~Predictor();
+  std::vector<std::string> GetInputNames();
+  std::vector<std::string> GetOutputNames();
+  std::unique_ptr<Tensor> GetInputHandle(const std::string& name);
+  std::unique_ptr<Tensor> GetOutputHandle(const std::string& name);
+  bool Run();
+  std::unique_ptr<Predictor> Clone();
+  void ClearIntermediateTensor();
+  // op types of the loaded program, in execution order (diagnostics)
+  std::vector<std::string> OpTypes() const;
+
+ private:
+  explicit Predictor(std::shared_ptr<PredictorImpl> impl);
+  std::shared_ptr<PredictorImpl> impl_;
+};
+
+std::shared_ptr<Predictor> CreatePredictor(const Config& config);
+std::string GetVersion();
+
+}  // namespace paddle_infer

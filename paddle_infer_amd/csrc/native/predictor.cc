@@ -1,0 +1,196 @@
+// paddle_infer::Predictor on the native engine: load + validate the program, keep parameters
+// resident on the predictor's device, run block 0 op by op, expose feed / fetch handles.
+#include <algorithm>
+#include <fstream>
+#include <sstream>
+
+#include "engine.h"
+#include "paddle_inference_api.h"
+
+namespace paddle_infer {
+
+namespace {
+std::string read_file(const std::string& path) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) throw std::runtime_error("cannot open " + path);
+  std::ostringstream ss;
+  ss << f.rdbuf();
+  return ss.str();
+}
+
+template <typename T>
+struct DtOf;
+template <> struct DtOf<float> { static constexpr int v = pdn::VT_FP32; };
+template <> struct DtOf<int64_t> { static constexpr int v = pdn::VT_INT64; };
+template <> struct DtOf<int32_t> { static constexpr int v = pdn::VT_INT32; };
+template <> struct DtOf<uint8_t> { static constexpr int v = pdn::VT_UINT8; };
+template <> struct DtOf<int8_t> { static constexpr int v = pdn::VT_INT8; };
+template <> struct DtOf<bool> { static constexpr int v = pdn::VT_BOOL; };
+
+DataType to_api(int vt) {
+  switch (vt) {
+    case pdn::VT_FP32: return DataType::FLOAT32;
+    case pdn::VT_INT64: return DataType::INT64;
+    case pdn::VT_INT32: return DataType::INT32;
+    case pdn::VT_UINT8: return DataType::UINT8;
+    case pdn::VT_INT8: return DataType::INT8;
+    case pdn::VT_FP16: return DataType::FLOAT16;
+    case pdn::VT_BOOL: return DataType::BOOL;
+  }
+  throw std::runtime_error("unsupported dtype " + std::to_string(vt));
+}
+}  // namespace
+
+class PredictorImpl {
+ public:
+  Config cfg;
+  pdn::ProgramDesc prog;
+  std::vector<std::string> feeds, fetches;
+  pdn::Scope params;  // resident, on the predictor's place
+  pdn::Scope scope;   // per-run (feeds, intermediates, fetches)
+  pdn::Ctx ctx;
+
+  explicit PredictorImpl(const Config& c) : cfg(c) {
+    prog = pdn::parse_program(read_file(c.prog_file()));
+    if (prog.blocks.empty()) throw std::runtime_error("empty program");
+    const auto& reg = pdn::op_registry();
+    std::vector<std::string> unknown;
+    std::vector<std::pair<int64_t, std::string>> fd, ft;
+    for (size_t bi = 1; bi < prog.blocks.size(); ++bi)
+      if (!prog.blocks[bi].ops.empty())
+        throw std::runtime_error("native engine: control-flow sub-blocks are not supported "
+                                 "(use the Python Predictor)");
+    for (const auto& op : prog.blocks[0].ops) {
+      if (op.type == "feed") fd.emplace_back(op.ai("col", (int64_t)fd.size()), op.out("Out"));
+      else if (op.type == "fetch") ft.emplace_back(op.ai("col", (int64_t)ft.size()), op.in("X"));
+      else if (!reg.count(op.type) && std::find(unknown.begin(), unknown.end(), op.type) == unknown.end())
+        unknown.push_back(op.type);
+    }
+    if (!unknown.empty()) {
+      std::string m = "native engine: no kernel for op type(s):";
+      for (auto& u : unknown) m += " " + u;
+      throw std::runtime_error(m);
+    }
+    std::sort(fd.begin(), fd.end());
+    std::sort(ft.begin(), ft.end());
+    for (auto& p : fd) feeds.push_back(p.second);
+    for (auto& p : ft) fetches.push_back(p.second);
+    ctx.gpu = c.use_gpu();
+    ctx.device = c.gpu_device_id();
+    ctx.threads = std::max(1, c.cpu_math_library_num_threads());
+    if (ctx.gpu) pdn::dev_init(ctx);
+    if (!c.params_file().empty()) {
+      auto ps = pdn::load_params(prog, read_file(c.params_file()));
+      for (auto& kv : ps) params[kv.first] = ctx.gpu ? pdn::to_device(kv.second, ctx) : kv.second;
+    }
+  }
+  PredictorImpl(const PredictorImpl& o) : cfg(o.cfg), prog(o.prog), feeds(o.feeds), fetches(o.fetches),
+                                          params(o.params) {
+    ctx = o.ctx;
+    ctx.stream = ctx.blas = nullptr;
+    if (ctx.gpu) pdn::dev_init(ctx);  // own stream / BLAS handle, shared resident weights
+  }
+  ~PredictorImpl() {
+    scope.clear();
+    if (ctx.gpu) {
+      params.clear();
+      pdn::dev_release(ctx);
+    }
+  }
+
+  bool run() {
+    const auto& reg = pdn::op_registry();
+    for (auto& kv : params) scope[kv.first] = kv.second;
+    for (const auto& op : prog.blocks[0].ops) {
+      if (op.type == "feed" || op.type == "fetch") continue;
+      reg.at(op.type)(ctx, op, scope);
+    }
+    if (ctx.gpu) pdn::dev_sync(ctx);
+    return true;
+  }
+
+  pdn::DTensor& tensor(const std::string& n) {
+    auto it = scope.find(n);
+    if (it == scope.end()) throw std::runtime_error("tensor '" + n + "' has no value");
+    return it->second;
+  }
+};
+
+// ------------------------------------------------------------------------------ Tensor
+void Tensor::Reshape(const std::vector<int>& shape) { pending_shape_ = shape; }
+
+template <typename T>
+void Tensor::CopyFromCpu(const T* data) {
+  if (!input_) throw std::runtime_error("CopyFromCpu on an output handle");
+  pdn::DTensor t;
+  t.dtype = DtOf<T>::v;
+  for (int d : pending_shape_) t.dims.push_back(d);
+  t.buf = pdn::alloc_buffer(t.nbytes(), p_->ctx.gpu);
+  if (p_->ctx.gpu) pdn::dev_copy(t.buf->p, data, t.nbytes(), 0, p_->ctx);
+  else std::memcpy(t.buf->p, data, t.nbytes());
+  p_->scope[name_] = t;
+}
+
+template <typename T>
+void Tensor::CopyToCpu(T* data) const {
+  const pdn::DTensor& t = p_->tensor(name_);
+  if (t.dtype != DtOf<T>::v) throw std::runtime_error("CopyToCpu: dtype mismatch for " + name_);
+  if (t.on_dev()) pdn::dev_copy(data, t.buf->p, t.nbytes(), 1, p_->ctx);
+  else std::memcpy(data, t.buf->p, t.nbytes());
+}
+
+std::vector<int> Tensor::shape() const {
+  if (input_ && !p_->scope.count(name_)) return pending_shape_;
+  const auto& t = p_->tensor(name_);
+  return std::vector<int>(t.dims.begin(), t.dims.end());
+}
+DataType Tensor::type() const { return to_api(p_->tensor(name_).dtype); }
+PlaceType Tensor::place() const { return p_->ctx.gpu ? PlaceType::kGPU : PlaceType::kCPU; }
+
+template void Tensor::CopyFromCpu<float>(const float*);
+template void Tensor::CopyFromCpu<int64_t>(const int64_t*);
+template void Tensor::CopyFromCpu<int32_t>(const int32_t*);
+template void Tensor::CopyFromCpu<uint8_t>(const uint8_t*);
+template void Tensor::CopyFromCpu<int8_t>(const int8_t*);
+template void Tensor::CopyToCpu<float>(float*) const;
+template void Tensor::CopyToCpu<int64_t>(int64_t*) const;
+template void Tensor::CopyToCpu<int32_t>(int32_t*) const;
+template void Tensor::CopyToCpu<uint8_t>(uint8_t*) const;
+template void Tensor::CopyToCpu<int8_t>(int8_t*) const;
+
+// ------------------------------------------------------------------------------ Predictor
+Predictor::Predictor(const Config& config) : impl_(std::make_shared<PredictorImpl>(config)) {}
+Predictor::Predictor(std::shared_ptr<PredictorImpl> impl) : impl_(std::move(impl)) {}
+Predictor::~Predictor() = default;
+std::vector<std::string> Predictor::GetInputNames() { return impl_->feeds; }
+std::vector<std::string> Predictor::GetOutputNames() { return impl_->fetches; }
+std::unique_ptr<Tensor> Predictor::GetInputHandle(const std::string& name) {
+  if (std::find(impl_->feeds.begin(), impl_->feeds.end(), name) == impl_->feeds.end())
+    throw std::runtime_error("no input named " + name);
+  return std::unique_ptr<Tensor>(new Tensor(impl_.get(), name, true));
+}
+std::unique_ptr<Tensor> Predictor::GetOutputHandle(const std::string& name) {
+  if (std::find(impl_->fetches.begin(), impl_->fetches.end(), name) == impl_->fetches.end())
+    throw std::runtime_error("no output named " + name);
+  return std::unique_ptr<Tensor>(new Tensor(impl_.get(), name, false));
+}
+bool Predictor::Run() { return impl_->run(); }
+std::unique_ptr<Predictor> Predictor::Clone() {
+  return std::unique_ptr<Predictor>(new Predictor(std::make_shared<PredictorImpl>(*impl_)));
+}
+void Predictor::ClearIntermediateTensor() {
+  pdn::Scope keep;
+  for (auto& n : impl_->fetches)
+    if (impl_->scope.count(n)) keep[n] = impl_->scope[n];
+  impl_->scope.swap(keep);
+}
+std::vector<std::string> Predictor::OpTypes() const {
+  std::vector<std::string> v;
+  for (const auto& op : impl_->prog.blocks[0].ops) v.push_back(op.type);
+  return v;
+}
+
+std::shared_ptr<Predictor> CreatePredictor(const Config& config) { return std::make_shared<Predictor>(config); }
+std::string GetVersion() { return "paddle_infer_amd native 0.3 (MI355X / gfx950)"; }
+
+}  // namespace paddle_infer

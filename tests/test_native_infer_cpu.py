@@ -57,3 +57,37 @@ def test_unknown_op_refused_at_load(tmp_path):
                         str(tmp_path / "x.bin")], capture_output=True, text=True)
     x.tofile(str(tmp_path / "x.bin"))
     assert r.returncode != 0 and "no kernel for op type" in r.stderr
+
+
+@pytest.mark.skipif(__import__("shutil").which("gcc") is None, reason="needs a C compiler")
+def test_reference_c_api_on_native_engine(tmp_path):
+    """The capi_exp C client (tests/capi/capi_demo.c) linked against libpiamd_infer.so: the PD_*
+    entry points run on the native engine (copy path, MutableData path, cloned predictor)."""
+    from paddle_infer_amd import _build
+    from test_capi_cpu import _save_model
+    from paddle_infer_amd.inference import Config, create_predictor
+    prefix = str(tmp_path / "mlp")
+    _save_model(prefix)
+    exe = tmp_path / "capi_native"
+    here = os.path.dirname(os.path.abspath(__file__))
+    subprocess.run(["gcc", "-O1", os.path.join(here, "capi", "capi_demo.c"), f"-I{_build.CDIR}",
+                    f"-L{_build.LIBDIR}", "-lpiamd_infer", f"-Wl,-rpath,{_build.LIBDIR}", "-o", str(exe)],
+                   check=True)
+    assert "libpython" not in subprocess.run(["ldd", str(exe)], capture_output=True, text=True).stdout
+    r = subprocess.run([str(exe), prefix + ".pdmodel", prefix + ".pdiparams", "3"], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "native" in r.stdout.splitlines()[0]
+    pred = create_predictor(Config(prefix + ".pdmodel", prefix + ".pdiparams"))
+    x = (np.arange(3 * 8) * 7 % 13).astype("float32").reshape(3, 8) / 13.0 - 0.5
+    h = pred.get_input_handle(pred.get_input_names()[0])
+    h.reshape([3, 8])
+    h.copy_from_cpu(x)
+    pred.run()
+    ref = pred.get_output_handle(pred.get_output_names()[0]).copy_to_cpu()
+    outs = [ln for ln in r.stdout.splitlines() if ln.startswith(("copy", "mutable"))]
+    assert len(outs) == 3
+    for ln in outs:
+        parts = ln.split()
+        vals = np.array([float(v) for v in parts[7:]], dtype=np.float32).reshape(3, 3)
+        np.testing.assert_allclose(vals, ref, rtol=1e-5, atol=1e-6)

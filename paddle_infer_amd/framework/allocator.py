@@ -7,23 +7,25 @@ Must run before the first device allocation of the process (the package does it 
 ``FLAGS_allocator_strategy=auto_growth`` is in the environment).
 
 Stream safety (reference `stream_safe_cuda_allocator.cc:40`, ``RecordStream``): a freed block is
-reused only by allocations on the stream it was allocated on (stream-ordered reuse). A tensor used
-on ANOTHER stream is covered two ways, because PyTorch's pluggable-allocator interface forwards no
-record-stream calls to the allocator:
+reused only by allocations on the stream it was allocated on; ``Tensor.record_stream(s)`` — and
+the record-stream calls RCCL's process group makes for its collectives — reach the allocator
+(``piamd_record_stream``): the block then waits, after its free, for an event on every other
+stream that used it before it is reusable.
 
-* ``Tensor.record_stream(s)`` is routed to :func:`record_stream`: an event is recorded on ``s`` and
-  the tensor is kept alive until that event has completed, so its block returns to the free list
-  only after the other stream's work on it — the reference's deferred free;
-* RCCL collectives (whose C++ record-stream calls never reach this allocator) run with
-  ``TORCH_NCCL_AVOID_RECORD_STREAMS=1``: the process group stashes every collective's tensors until
-  the work has been waited on by the compute stream, which orders the free after the collective.
+hipGraph capture: PyTorch's private graph pools map onto the allocator's tagged pools
+(``piamd_begin_pool`` / ``piamd_end_pool`` / ``piamd_release_pool``): a captured graph's memory is
+never handed to work outside the graph while the graph lives.
+
+With the allocator active, ``torch.cuda.memory_allocated`` / ``max_memory_allocated`` /
+``memory_reserved`` / ``max_memory_reserved`` / ``reset_peak_memory_stats`` / ``empty_cache``
+report and act on this allocator (PyTorch's pluggable interface has no statistics of its own).
 """
 from __future__ import annotations
 
 import ctypes
 import os
 
-_STATE = {"active": False, "lib": None}
+_STATE = {"active": False, "lib": None, "allocator": None}
 STAT_NAMES = ("allocated", "reserved", "peak_allocated", "peak_reserved", "num_alloc", "num_free",
               "num_chunk_alloc", "num_chunk_free")
 
@@ -57,42 +59,54 @@ def enable(strategy: str = "auto_growth") -> bool:
     if _STATE["active"]:
         return True
     from torch.cuda.memory import CUDAPluggableAllocator, change_current_allocator
-    _lib()
-    import torch
-    import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
-        raise RuntimeError("FLAGS_allocator_strategy=auto_growth must be set before the RCCL "
-                           "process group is created (its collectives must stash tensors instead "
-                           "of record_stream)")
-    os.environ["TORCH_NCCL_AVOID_RECORD_STREAMS"] = "1"
-    change_current_allocator(CUDAPluggableAllocator(lib_path(), "piamd_alloc", "piamd_free"))
-    if "record_stream" not in _ORIG:
-        _ORIG["record_stream"] = torch.Tensor.record_stream
-        torch.Tensor.record_stream = lambda t, s: record_stream(t, s)
+    lib = _lib()
+    alloc = CUDAPluggableAllocator(lib_path(), "piamd_alloc", "piamd_free")
+
+    def fn(name):
+        return ctypes.cast(getattr(lib, name), ctypes.c_void_p).value
+    a = alloc._allocator
+    a.set_record_stream_fn(fn("piamd_record_stream"))
+    a.set_begin_allocate_to_pool(fn("piamd_begin_pool"))
+    a.set_end_allocate_to_pool_fn(fn("piamd_end_pool"))
+    a.set_release_pool(fn("piamd_release_pool"))
+    change_current_allocator(alloc)
+    _patch_torch_memory_api()
     _STATE["active"] = True
+    _STATE["allocator"] = alloc
     return True
 
 
-_ORIG: dict = {}
-_PENDING: list = []  # (event, tensor): blocks in use on another stream
-
-
 def record_stream(t, stream) -> None:
-    """Defer ``t``'s free until the work queued on ``stream`` so far has completed."""
+    """``t`` is used on ``stream``: its block is not reused before that stream's work on it."""
+    t.record_stream(stream)
+
+
+def _patch_torch_memory_api():
     import torch
-    if not _STATE["active"] or not t.is_cuda:
-        return _ORIG.get("record_stream", torch.Tensor.record_stream)(t, stream)
-    ev = torch.cuda.Event()
-    ev.record(stream)
-    _PENDING.append((ev, t))
-    purge()
+
+    def dev(d):
+        if d is None:
+            return torch.cuda.current_device()
+        return d.index if isinstance(d, torch.device) and d.index is not None else int(
+            d if not isinstance(d, torch.device) else torch.cuda.current_device())
+    cm = torch.cuda.memory
+    repl = {
+        "memory_allocated": lambda device=None: stats(dev(device))["allocated"],
+        "max_memory_allocated": lambda device=None: stats(dev(device))["peak_allocated"],
+        "memory_reserved": lambda device=None: stats(dev(device))["reserved"],
+        "max_memory_reserved": lambda device=None: stats(dev(device))["peak_reserved"],
+        "reset_peak_memory_stats": lambda device=None: reset_peak(dev(device)),
+        "reset_max_memory_allocated": lambda device=None: reset_peak(dev(device)),
+        "empty_cache": lambda: empty_cache(torch.cuda.current_device()),
+    }
+    for k, f in repl.items():
+        _ORIG.setdefault(k, getattr(torch.cuda, k))
+        setattr(torch.cuda, k, f)
+        if hasattr(cm, k):
+            setattr(cm, k, f)
 
 
-def purge() -> int:
-    """Release tensors whose other-stream work has completed; returns how many stay pending."""
-    keep = [(e, t) for e, t in _PENDING if not e.query()]
-    _PENDING[:] = keep
-    return len(keep)
+_ORIG: dict = {}
 
 
 def stats(device: int = 0) -> dict:

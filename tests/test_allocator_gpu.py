@@ -74,3 +74,64 @@ def test_auto_growth_allocator_end_to_end():
     assert own["api_alloc"] == s["allocated"] and own["api_peak"] == s["peak_allocated"]
     # the 300 MiB chunk (wholly free after `del big`) is returned to the device
     assert own["after_release"]["reserved"] <= s["reserved"] - (300 << 20)
+
+
+STREAM_GRAPH = r"""
+import json, sys, torch
+sys.path.insert(0, sys.argv[1])
+import paddle_infer_amd as paddle
+from paddle_infer_amd.framework import allocator
+assert allocator.active()
+dev = torch.device("cuda", 0)
+out = {}
+# 1) record_stream: a block used on a side stream is not handed out before that stream's work ends
+side = torch.cuda.Stream()
+x = torch.empty(64 << 20, dtype=torch.uint8, device=dev)
+xp = x.data_ptr()
+torch.cuda.synchronize()
+with torch.cuda.stream(side):
+    torch.cuda._sleep(200_000_000)  # keep the side stream busy
+    x.fill_(7)
+x.record_stream(side)
+del x
+y = torch.empty(64 << 20, dtype=torch.uint8, device=dev)
+out["reused_while_busy"] = y.data_ptr() == xp
+side.synchronize()
+del y
+z1 = torch.empty(64 << 20, dtype=torch.uint8, device=dev)
+z2 = torch.empty(64 << 20, dtype=torch.uint8, device=dev)
+out["reused_after"] = xp in (z1.data_ptr(), z2.data_ptr())  # the deferred block is back in use
+del z1, z2
+# 2) hipGraph capture into a private pool, replayed; outside allocations never alias it
+a = torch.randn(1 << 20, device=dev)
+g = torch.cuda.CUDAGraph()
+s = torch.cuda.Stream()
+s.wait_stream(torch.cuda.current_stream())
+with torch.cuda.stream(s):
+    for _ in range(2):
+        b = a * 2.0 + 1.0
+    torch.cuda.current_stream().wait_stream(s)
+with torch.cuda.graph(g):
+    tmp = a * 3.0
+    b = tmp + 1.0
+gp = {b.data_ptr(), tmp.data_ptr()}
+del tmp
+outside = [torch.empty(4 << 20, dtype=torch.uint8, device=dev) for _ in range(8)]
+out["alias"] = any(o.data_ptr() in gp for o in outside)
+a.copy_(torch.ones_like(a))
+g.replay()
+torch.cuda.synchronize()
+out["graph_ok"] = bool(torch.all(b == 4.0).item())
+out["api_peak"] = torch.cuda.max_memory_allocated() == allocator.stats(0)["peak_allocated"]
+print("RESULT " + json.dumps(out))
+"""
+
+
+def test_record_stream_and_graph_pools():
+    env = dict(os.environ, FLAGS_allocator_strategy="auto_growth", PIAMD_ALLOC_CHUNK_MB="64")
+    r = subprocess.run([sys.executable, "-c", STREAM_GRAPH, ROOT], env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("RESULT ")][-1][7:])
+    assert not out["reused_while_busy"] and out["reused_after"], out
+    assert not out["alias"] and out["graph_ok"] and out["api_peak"], out

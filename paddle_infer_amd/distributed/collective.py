@@ -80,7 +80,17 @@ def new_group(ranks=None, backend=None, timeout=None):
     return g
 
 
+_RINGS = {}  # ring_id -> Group bound by a program helper (e.g. the mp ring of hybrid inference)
+
+
+def bind_ring(ring_id, group):
+    """Make program ops with ``ring_id`` run on ``group`` (reference c_comm_init of a ring)."""
+    _RINGS[int(ring_id)] = group
+
+
 def get_group(id=0):  # noqa: A002
+    if id in _RINGS:
+        return _RINGS[id]
     if id == 0:
         return Group(None, list(range(get_world_size())), 0)
     return _GROUPS.get(id)

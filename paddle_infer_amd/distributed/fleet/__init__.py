@@ -22,6 +22,7 @@ from .mp_layers import (VocabParallelEmbedding, ColumnParallelLinear, RowParalle
                         ParallelCrossEntropy)
 from .pipeline import LayerDesc, SharedLayerDesc, PipelineLayer, PipelineParallel  # noqa: F401
 from .recompute import recompute  # noqa: F401
+from .hybrid_parallel_inference import HybridParallelInferenceHelper  # noqa: F401
 from ...framework.random import get_rng_state_tracker, model_parallel_random_seed  # noqa: F401
 
 _STATE = {"hcg": None, "strategy": None, "inited": False, "model": None, "stage3": None}
@@ -560,6 +561,7 @@ meta_parallel = _MetaParallel()
 
 class _Utils:
     recompute = staticmethod(recompute)
+    HybridParallelInferenceHelper = HybridParallelInferenceHelper
 
 
 utils = _Utils()

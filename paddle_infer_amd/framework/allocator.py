@@ -123,10 +123,28 @@ def reset_peak(device: int = 0) -> None:
     _lib().piamd_alloc_reset_peak(int(device))
 
 
+def default_strategy() -> str:
+    """``FLAGS_allocator_strategy`` when set; otherwise ``auto_growth`` (the framework allocator)
+    for single-process jobs on a GPU. Multi-process jobs (WORLD_SIZE > 1) keep PyTorch's caching
+    allocator unless the flag asks for ``auto_growth`` explicitly: the RCCL path under the own
+    allocator is covered by the record-stream hook but has not been validated on a multi-GPU node
+    yet."""
+    v = os.environ.get("FLAGS_allocator_strategy")
+    if v:
+        return v
+    return "auto_growth" if int(os.environ.get("WORLD_SIZE", "1")) <= 1 else "naive_best_fit"
+
+
 def maybe_enable_from_env() -> None:
-    if os.environ.get("FLAGS_allocator_strategy", "") == "auto_growth":
-        try:
-            enable("auto_growth")
-        except Exception as e:  # allocator already initialised / library missing: say so once
-            import warnings
-            warnings.warn(f"FLAGS_allocator_strategy=auto_growth not applied: {e}", RuntimeWarning)
+    """Called at package import: install the framework allocator when it is the strategy and a GPU
+    is present (before the first device allocation)."""
+    if default_strategy() != "auto_growth":
+        return
+    import torch
+    if not torch.cuda.is_available():
+        return
+    try:
+        enable("auto_growth")
+    except Exception as e:  # allocator already initialised / library missing: say so once
+        import warnings
+        warnings.warn(f"FLAGS_allocator_strategy=auto_growth not applied: {e}", RuntimeWarning)

@@ -63,7 +63,13 @@ def set_flags(flags: dict):
             from ..ops import autotune
             autotune.configure(enable=bool(v))
         if k == "FLAGS_fraction_of_gpu_memory_to_use" and torch.cuda.is_available():
-            torch.cuda.set_per_process_memory_fraction(float(v))
+            from . import allocator
+            if allocator.active():  # the auto-growth allocator grows on demand: no fixed pool
+                import warnings
+                warnings.warn("FLAGS_fraction_of_gpu_memory_to_use has no effect under the "
+                              "auto_growth allocator", RuntimeWarning)
+            else:
+                torch.cuda.set_per_process_memory_fraction(float(v))
         if k == "FLAGS_allocator_strategy" and v == "auto_growth":
             from . import allocator
             try:

@@ -34,13 +34,22 @@ def cuda_places(device_ids=None):
 
 
 class device_guard:  # noqa: N801
+    """Reference `paddle.static.device_guard`: ops recorded inside carry ``op_device`` (e.g.
+    ``"gpu:1"`` — the pipeline stage HybridParallelInferenceHelper places them on, ``"gpu:all"``
+    for every stage). The executor itself runs every op on the program's device."""
+
     def __init__(self, device=None):
         self.device = device
 
     def __enter__(self):
+        from . import framework as _fw
+        self._prev = _fw._OP_DEVICE[0]
+        _fw._OP_DEVICE[0] = self.device
         return self
 
     def __exit__(self, *a):
+        from . import framework as _fw
+        _fw._OP_DEVICE[0] = self._prev
         return False
 
 

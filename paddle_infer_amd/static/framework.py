@@ -258,6 +258,9 @@ class Operator:
         return f"Op({self.type}: {self.input_names()} -> {self.output_names()})"
 
 
+_OP_DEVICE = [None]  # static.device_guard: op_device attribute of the ops being recorded
+
+
 class Block:
     def __init__(self, program, idx=0, parent_idx=-1):
         self.program, self.idx, self.parent_idx = program, idx, parent_idx
@@ -280,6 +283,8 @@ class Block:
         return v
 
     def append_op(self, op):
+        if _OP_DEVICE[0] is not None and "op_device" not in op.attrs:
+            op.attrs["op_device"] = _OP_DEVICE[0]
         op.idx = len(self.ops)
         self.ops.append(op)
         self.program._version += 1

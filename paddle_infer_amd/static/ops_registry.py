@@ -18,7 +18,7 @@ from .framework import VarRef
 
 REGISTRY = {}
 INPLACE_OUT_OPS = {"write_to_array"}
-MISSING_OK_OPS = {"select_input"}
+MISSING_OK_OPS = {"select_input", "c_broadcast"}
 DEVICE = [torch.device("cpu")]  # device of the running Executor (creation ops allocate there)
 
 

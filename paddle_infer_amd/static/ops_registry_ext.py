@@ -480,6 +480,74 @@ for _n, _o in (("c_allreduce_sum", "SUM"), ("mp_allreduce_sum", "SUM"), ("c_allr
     register(_n)(_c_allreduce(_o))
 
 
+def _peer(a):
+    """``peer`` (rank inside the ring's group) → global rank."""
+    import torch.distributed as dist
+    g = _group(a)
+    peer = int(a.get("peer", 0))
+    return dist.get_global_rank(g, peer) if g is not None else peer
+
+
+_P2P_DT = [torch.float32, torch.float16, torch.bfloat16, torch.int64, torch.int32, torch.bool,
+           torch.uint8, torch.int8, torch.float64]
+
+
+@register("send_v2")
+def _send_v2(ins, a):
+    """Reference `send_v2_op.cc`: X to ``peer`` of the ring (shape / dtype sent first, so the
+    receiving stage needs no static out_shape)."""
+    import torch.distributed as dist
+    x = ins["X"][0].contiguous()
+    peer = _peer(a)
+    meta = torch.tensor([x.dim(), _P2P_DT.index(x.dtype)] + list(x.shape) + [0] * (8 - x.dim()),
+                        dtype=torch.int64, device=x.device)
+    dist.send(meta, peer)
+    dist.send(x, peer)
+    return {}
+
+
+@register("recv_v2")
+def _recv_v2(ins, a):
+    """Reference `recv_v2_op.cc`: Out from ``peer`` of the ring."""
+    import torch.distributed as dist
+    from .ops_registry import DEVICE
+    dev = DEVICE[0]
+    peer = _peer(a)
+    meta = torch.empty(10, dtype=torch.int64, device=dev)
+    dist.recv(meta, peer)
+    nd, dt = int(meta[0]), _P2P_DT[int(meta[1])]
+    out = torch.empty([int(v) for v in meta[2:2 + nd].tolist()], dtype=dt, device=dev)
+    dist.recv(out, peer)
+    return {"Out": out}
+
+
+@register("c_broadcast")
+def _c_broadcast(ins, a):
+    """Reference `c_broadcast_op.cc`: X from ``root`` (rank inside the ring's group) to the ring.
+    Ranks that do not hold X yet (a pipeline stage that did not compute it) receive shape / dtype
+    first."""
+    import torch.distributed as dist
+    from .ops_registry import DEVICE
+    g = _group(a)
+    root = int(a.get("root", 0))
+    src = dist.get_global_rank(g, root) if g is not None else root
+    x = (ins.get("X") or [None])[0]
+    dev = x.device if x is not None else DEVICE[0]
+    meta = torch.zeros(10, dtype=torch.int64, device=dev)
+    if dist.get_rank() == src:
+        x = x.contiguous()
+        meta[0], meta[1] = x.dim(), _P2P_DT.index(x.dtype)
+        meta[2:2 + x.dim()] = torch.tensor(list(x.shape), dtype=torch.int64)
+    dist.broadcast(meta, src, group=g)
+    nd, dt = int(meta[0]), _P2P_DT[int(meta[1])]
+    if dist.get_rank() != src:
+        x = torch.empty([int(v) for v in meta[2:2 + nd].tolist()], dtype=dt, device=dev)
+    else:
+        x = x.clone()
+    dist.broadcast(x, src, group=g)
+    return {"Out": x}
+
+
 @register("c_concat")
 def _c_concat(ins, a):
     """Reference `c_concat_op.cc`: all-gather X over the ring and concatenate on the last dim."""

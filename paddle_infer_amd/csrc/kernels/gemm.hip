@@ -29,6 +29,17 @@ typedef __attribute__((address_space(3))) s16x4_t lds_s16x4;
 constexpr int BM = 256, BN = 256, BK = 64, NWAVE = 8, NTHR = NWAVE * 64;
 constexpr int TILE_BYTES = 256 * BK * 2;            // one operand image per stage (32 KiB)
 constexpr int STAGE_BYTES = 2 * TILE_BYTES;
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+
+// One 32×32×16 MFMA step on 16-bit operand fragments carried as raw bits: bf16 or IEEE fp16.
+template <bool F16>
+__device__ __forceinline__ f32x16 mma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  if constexpr (F16)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, a),
+                                                  __builtin_bit_cast(f16x8_t, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
 
 // XOR image with ROWB-byte rows (16-B chunks permuted by the low row bits).
 template <int ROWB>
@@ -169,7 +180,7 @@ __device__ __forceinline__ void gemm_mainloop(const bf16_t* __restrict__ a, long
 // Epilogue: waves laid out WM (M) × 8/WM (N), each MB × NB blocks of 32 × 32 (default: the 256²
 // tile, 2 × 4 waves of 4 × 2). Lane owns row m0 + wr·32MB + mb·32 + l31 (stored while < mend);
 // columns n = n0 + wc·32NB + nb·32 + 8g + 4·hi + (0..3) (stored while < N).
-template <int WM = 2, int MB = 4, int NB = 2>
+template <int WM = 2, int MB = 4, int NB = 2, bool F16 = false>
 __device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[MB][NB], void* __restrict__ c,
                                               long long ldc, int c_f32, int accumulate, int m0,
                                               int mend, int n0, int N, int epi, int act,
@@ -195,15 +206,15 @@ __device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[MB][NB], void*
           u16x4 pre;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            v[j] += bias ? bf2f(bias[n + j]) : 0.f;
-            pre[j] = f2bf(v[j]);
-            v[j] = act_fwd(bf2f(pre[j]), act);
+            v[j] += bias ? h2f<F16>(bias[n + j]) : 0.f;
+            pre[j] = f2h<F16>(v[j]);
+            v[j] = act_fwd(h2f<F16>(pre[j]), act);
           }
           if (aux) *reinterpret_cast<u16x4*>(aux + (long long)m * ldaux + n) = pre;
         } else if (epi == EPI_DACT) {
           const u16x4 h = *reinterpret_cast<const u16x4*>(aux + (long long)m * ldaux + n);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] *= act_grad(bf2f(h[j]), act);
+          for (int j = 0; j < 4; ++j) v[j] *= act_grad(h2f<F16>(h[j]), act);
         }
         if (c_f32) {
           f32x4* p = reinterpret_cast<f32x4*>((float*)c + (long long)m * ldc + n);
@@ -217,10 +228,10 @@ __device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[MB][NB], void*
           if (accumulate) {
             const u16x4 old = *reinterpret_cast<const u16x4*>(p);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j] + bf2f(old[j]));
+            for (int j = 0; j < 4; ++j) o[j] = f2h<F16>(v[j] + h2f<F16>(old[j]));
           } else {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j]);
+            for (int j = 0; j < 4; ++j) o[j] = f2h<F16>(v[j]);
           }
           *reinterpret_cast<u16x4*>(p) = o;
         }
@@ -331,7 +342,7 @@ struct ConvGeom {
 // SC (small-channel stem mode, C == 8: image channels zero-padded to 8): a 64-deep k-step holds
 // EIGHT taps × 8 channels — 16-B chunk j of k-step kt is tap 8·kt + j — so a 3-channel 7×7 stem runs
 // 7 k-steps instead of 49 padded-to-64-channel ones; W is [K_out][ceil(R·S/8)·64] (taps ≥ R·S zero).
-template <int WM, int MB, int NB, bool SC = false>
+template <int WM, int MB, int NB, bool SC = false, bool F16 = false>
 __global__ __launch_bounds__(NTHR, 1) void conv_fwd_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ wt, const bf16_t* __restrict__ zero,
     bf16_t* __restrict__ y, float* __restrict__ ws, int ksplit, ConvGeom g, int Kout, int act,
@@ -430,7 +441,7 @@ __global__ __launch_bounds__(NTHR, 1) void conv_fwd_kernel(
       for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb)
-          acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[nb], af[mb], acc[mb][nb], 0, 0, 0);
+          acc[mb][nb] = mma32<F16>(bf[nb], af[mb], acc[mb][nb]);
       __builtin_amdgcn_s_setprio(0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -440,11 +451,12 @@ __global__ __launch_bounds__(NTHR, 1) void conv_fwd_kernel(
     gemm_epilogue<WM, MB, NB>(acc, ws + (long long)part * M * Kout, Kout, 1, 0, m0, M, n0, Kout,
                               EPI_STORE, 0, nullptr, nullptr, 0);
   else
-    gemm_epilogue<WM, MB, NB>(acc, y, Kout, 0, 0, m0, M, n0, Kout,
+    gemm_epilogue<WM, MB, NB, F16>(acc, y, Kout, 0, 0, m0, M, n0, Kout,
                               (bias || act) ? EPI_BIAS_ACT : EPI_STORE, act, bias, nullptr, 0);
 }
 
 // y[m][n] = act(Σ_p ws[p][m][n] + bias[n]) — 4 outputs per thread (K_out % 4 == 0).
+template <bool F16>
 __global__ __launch_bounds__(256) void conv_splitk_finish(const float* __restrict__ ws, int ksplit,
                                                           long long MN, int Kout, int act,
                                                           const bf16_t* __restrict__ bias,
@@ -462,8 +474,8 @@ __global__ __launch_bounds__(256) void conv_splitk_finish(const float* __restric
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     float h = v[j];
-    if (bias || act) h = bf2f(f2bf(h + (bias ? bf2f(bias[n + j]) : 0.f)));
-    o[j] = f2bf(act_fwd(h, act));
+    if (bias || act) h = h2f<F16>(f2h<F16>(h + (bias ? h2f<F16>(bias[n + j]) : 0.f)));
+    o[j] = f2h<F16>(act_fwd(h, act));
   }
   *reinterpret_cast<u16x4*>(y + i) = o;
 }
@@ -489,7 +501,7 @@ struct ConvWgradGeom {
   float inv_ow, inv_ohw;
 };
 
-template <int WM, int MB, int NB>
+template <int WM, int MB, int NB, bool F16 = false>
 __global__ __launch_bounds__(NTHR, 1) void conv_wgrad_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy, const bf16_t* __restrict__ zero,
     float* __restrict__ out, int ksplit, ConvWgradGeom g) {
@@ -589,7 +601,7 @@ __global__ __launch_bounds__(NTHR, 1) void conv_wgrad_kernel(
       for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb)
-          acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[nb], af[mb], acc[mb][nb], 0, 0, 0);
+          acc[mb][nb] = mma32<F16>(bf[nb], af[mb], acc[mb][nb]);
       __builtin_amdgcn_s_setprio(0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -759,63 +771,71 @@ PIAMD_EXPORT int piamd_gemm_i8(const void* x, long long ldx, const void* wq, lon
 }
 
 // NHWC implicit-GEMM convolution forward: x [N][H][W][C], wt [Kout][R][S][C] (OHWI), y
-// [N][OH][OW][Kout], bf16; zero: ≥ 128 zero bytes (out-of-image taps); bias [Kout] (nullable);
-// act as piamd_gemm. C % 64 == 0, Kout % 4 == 0.
+// [N][OH][OW][Kout], 16-bit (bf16, or IEEE fp16 when f16 != 0: same tiles on the f16 MFMA);
+// zero: ≥ 128 zero bytes (out-of-image taps); bias [Kout] (nullable, element type of x);
+// act as piamd_gemm. C % 64 == 0 (or C == 8: stem mode), Kout % 4 == 0.
+template <bool F16>
+static void conv_fwd_launch(int tile_n, bool sc, unsigned grid, hipStream_t st, const bf16_t* xb,
+                            const bf16_t* wb, const bf16_t* zb, bf16_t* y, float* wsf, int ksplit,
+                            const ConvGeom& g, int Kout, int act, const bf16_t* bb) {
+#define CONV_FWD(WM, MB, NB, SCV) \
+  hipLaunchKernelGGL((conv_fwd_kernel<WM, MB, NB, SCV, F16>), dim3(grid), dim3(NTHR), 0, st, xb, wb, zb, y, wsf, ksplit, g, Kout, act, bb)
+  if (tile_n == 64) {
+    if (sc) CONV_FWD(8, 1, 2, true); else CONV_FWD(8, 1, 2, false);
+  } else if (tile_n == 128) {
+    if (sc) CONV_FWD(4, 2, 2, true); else CONV_FWD(4, 2, 2, false);
+  } else {
+    if (sc) CONV_FWD(2, 4, 2, true); else CONV_FWD(2, 4, 2, false);
+  }
+#undef CONV_FWD
+}
+
 PIAMD_EXPORT int piamd_conv2d_fwd(const void* x, const void* wt, const void* zero, void* y, int N,
                                   int H, int W, int C, int OH, int OW, int R, int S, int st_h,
                                   int st_w, int pad_h, int pad_w, int dil_h, int dil_w, int Kout,
                                   int act, const void* bias, int tile_n, int ksplit, void* ws,
-                                  hipStream_t st) {
+                                  int f16, hipStream_t st) {
   const bool sc = C == 8;
   if ((C % BK && !sc) || Kout % 4 || N < 1 || OH < 1 || OW < 1 || R < 1 || S < 1 || !zero || ksplit < 1 ||
-      (ksplit > 1 && !ws) || ksplit > (sc ? (R * S + 7) / 8 : R * S * (C / BK)))
+      (ksplit > 1 && !ws) || ksplit > (sc ? (R * S + 7) / 8 : R * S * (C / BK)) ||
+      (tile_n != 64 && tile_n != 128 && tile_n != 256))
     return (int)hipErrorInvalidValue;
   ConvGeom g{N, H, W, C, OH, OW, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w};
   const long long M = (long long)N * OH * OW;
   if (M * ksplit > 0x7fffffffLL || M * Kout > (1LL << 40)) return (int)hipErrorInvalidValue;
   const int tm = (int)((M + BM - 1) / BM);
+  const unsigned grid = (unsigned)(tm * ((Kout + tile_n - 1) / tile_n) * ksplit);
   const auto xb = (const bf16_t*)x;
   const auto wb = (const bf16_t*)wt;
   const auto zb = (const bf16_t*)zero;
   const auto bb = (const bf16_t*)bias;
   float* wsf = (float*)ws;
-  if (tile_n == 64) {
-    if (sc) hipLaunchKernelGGL((conv_fwd_kernel<8, 1, 2, true>), dim3(tm * ((Kout + 63) / 64) * ksplit), dim3(NTHR), 0, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb);
-    else hipLaunchKernelGGL((conv_fwd_kernel<8, 1, 2>), dim3(tm * ((Kout + 63) / 64) * ksplit),
-                       dim3(NTHR), 0, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb);
-  } else if (tile_n == 128) {
-    if (sc) hipLaunchKernelGGL((conv_fwd_kernel<4, 2, 2, true>), dim3(tm * ((Kout + 127) / 128) * ksplit), dim3(NTHR), 0, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb);
-    else hipLaunchKernelGGL((conv_fwd_kernel<4, 2, 2>), dim3(tm * ((Kout + 127) / 128) * ksplit),
-                       dim3(NTHR), 0, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb);
-  } else if (tile_n == 256) {
-    if (sc) hipLaunchKernelGGL((conv_fwd_kernel<2, 4, 2, true>), dim3(tm * ((Kout + 255) / 256) * ksplit), dim3(NTHR), 0, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb);
-    else hipLaunchKernelGGL((conv_fwd_kernel<2, 4, 2>), dim3(tm * ((Kout + 255) / 256) * ksplit),
-                       dim3(NTHR), 0, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb);
-  } else {
-    return (int)hipErrorInvalidValue;
-  }
+  if (f16) conv_fwd_launch<true>(tile_n, sc, grid, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb);
+  else conv_fwd_launch<false>(tile_n, sc, grid, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb);
   if (ksplit > 1) {
     const long long MN = M * Kout;
-    hipLaunchKernelGGL(conv_splitk_finish, dim3((unsigned)((MN / 4 + 255) / 256)), dim3(256), 0,
-                       st, wsf, ksplit, MN, Kout, act, bb, (bf16_t*)y);
+    const dim3 fg((unsigned)((MN / 4 + 255) / 256));
+    if (f16) hipLaunchKernelGGL(conv_splitk_finish<true>, fg, dim3(256), 0, st, wsf, ksplit, MN, Kout, act, bb, (bf16_t*)y);
+    else hipLaunchKernelGGL(conv_splitk_finish<false>, fg, dim3(256), 0, st, wsf, ksplit, MN, Kout, act, bb, (bf16_t*)y);
   }
   return (int)hipGetLastError();
 }
 
-// NHWC implicit-GEMM convolution weight gradient: x [N][H][W][C], dy [N][OH][OW][Kout] bf16 →
-// d [R][S][C][Kout] f32 (HWIO; accumulate adds into d). zero: ≥ 16 zero bytes. C % 8 == 0,
-// Kout % tile_n == 0 (tile_n ∈ {64, 128, 256}), N·OH·OW < 2^24; ksplit > 1 needs ws with
-// ksplit·R·S·C·Kout floats (ksplit == 1 writes d directly and requires accumulate == 0).
+// NHWC implicit-GEMM convolution weight gradient: x [N][H][W][C], dy [N][OH][OW][Kout] 16-bit
+// (bf16, or fp16 when f16 != 0) → d [R][S][C][Kout] f32 (HWIO; accumulate adds into d). zero: ≥ 16
+// zero bytes. C % 8 == 0, Kout % tile_n == 0 (tile_n ∈ {64, 128, 256}), N·OH·OW < 2^24; ksplit > 1
+// needs ws with ksplit·R·S·C·Kout floats (ksplit == 1 writes d directly, requires accumulate == 0).
 PIAMD_EXPORT int piamd_conv2d_wgrad(const void* x, const void* dy, const void* zero, float* d, int N,
                                     int H, int W, int C, int OH, int OW, int R, int S, int st_h,
                                     int st_w, int pad_h, int pad_w, int dil_h, int dil_w, int Kout,
-                                    int tile_n, int ksplit, float* ws, int accumulate,
+                                    int tile_n, int ksplit, float* ws, int accumulate, int f16,
                                     hipStream_t st) {
   const long long M = (long long)N * OH * OW;
   const long long RSC = (long long)R * S * C;
   if (C % 8 || Kout % tile_n || N < 1 || OH < 1 || OW < 1 || R < 1 || S < 1 || !zero ||
       ksplit < 1 || (ksplit > 1 && !ws) || (ksplit == 1 && accumulate) || M >= (1LL << 24) ||
-      RSC * Kout >= (1LL << 31) || ksplit > (M + 63) / 64)
+      RSC * Kout >= (1LL << 31) || ksplit > (M + 63) / 64 ||
+      (tile_n != 64 && tile_n != 128 && tile_n != 256))
     return (int)hipErrorInvalidValue;
   ConvWgradGeom g{N, H, W, C, OH, OW, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w,
                   (int)M, (int)RSC, Kout, 1.f / (float)OW, 1.f / (float)(OH * OW)};
@@ -826,17 +846,17 @@ PIAMD_EXPORT int piamd_conv2d_wgrad(const void* x, const void* dy, const void* z
   const auto xb = (const bf16_t*)x;
   const auto db = (const bf16_t*)dy;
   const auto zb = (const bf16_t*)zero;
-  if (tile_n == 64)
-    hipLaunchKernelGGL((conv_wgrad_kernel<8, 1, 2>), dim3((unsigned)wgs), dim3(NTHR), 0, st, xb, db,
-                       zb, out, ksplit, g);
-  else if (tile_n == 128)
-    hipLaunchKernelGGL((conv_wgrad_kernel<4, 2, 2>), dim3((unsigned)wgs), dim3(NTHR), 0, st, xb, db,
-                       zb, out, ksplit, g);
-  else if (tile_n == 256)
-    hipLaunchKernelGGL((conv_wgrad_kernel<2, 4, 2>), dim3((unsigned)wgs), dim3(NTHR), 0, st, xb, db,
-                       zb, out, ksplit, g);
-  else
-    return (int)hipErrorInvalidValue;
+#define CONV_WG(WM, MB, NB)                                                                       \
+  do {                                                                                            \
+    if (f16) hipLaunchKernelGGL((conv_wgrad_kernel<WM, MB, NB, true>), dim3((unsigned)wgs),       \
+                                dim3(NTHR), 0, st, xb, db, zb, out, ksplit, g);                   \
+    else hipLaunchKernelGGL((conv_wgrad_kernel<WM, MB, NB, false>), dim3((unsigned)wgs),          \
+                            dim3(NTHR), 0, st, xb, db, zb, out, ksplit, g);                       \
+  } while (0)
+  if (tile_n == 64) CONV_WG(8, 1, 2);
+  else if (tile_n == 128) CONV_WG(4, 2, 2);
+  else CONV_WG(2, 4, 2);
+#undef CONV_WG
   if (ksplit > 1) {
     const long long MN = RSC * Kout;
     hipLaunchKernelGGL(wgrad_splitk_finish, dim3((unsigned)((MN / 4 + 255) / 256)), dim3(256), 0, st,

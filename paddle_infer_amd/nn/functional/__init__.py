@@ -182,34 +182,40 @@ def _padding(padding, nd):
 
 
 def conv1d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NCL", name=None):
-    return _fmt_out(TF.conv1d(_fmt_in(x, data_format), weight, bias, stride, _padding(padding, 1), dilation, groups), data_format)
-
-
-def _hip_conv_ok(x, weight, groups, padding, nhwc):
-    """bf16 NHWC / channels_last conv on the GPU → MFMA implicit-GEMM kernel (ops/conv.py)."""
-    if not (x.is_cuda and x.dim() == 4 and weight.dim() == 4 and groups == 1):
-        return False
-    bf16 = x.dtype == torch.bfloat16 or (torch.is_autocast_enabled("cuda") and
-                                         torch.get_autocast_dtype("cuda") == torch.bfloat16)
-    if not bf16 or isinstance(padding, str):
-        return False
-    if not nhwc and not (x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous()):
-        return False
-    from ...ops import conv as _conv
-    return _conv.HIP_CONV and _conv.eligible((x.shape[-1] if nhwc else x.shape[1],),
-                                             weight.shape, groups, padding)
+    pad = _padding(padding, 1)
+    if x.is_cuda and x.dim() == 3 and not isinstance(pad, str):
+        # a 1 × L image on the 2-D kernels (ops/conv.py)
+        from ...ops import conv as _conv
+        p = pad[0] if isinstance(pad, (tuple, list)) else pad
+        s = stride[0] if isinstance(stride, (tuple, list)) else stride
+        d = dilation[0] if isinstance(dilation, (tuple, list)) else dilation
+        nlc = data_format == "NLC"
+        y = _conv.conv2d_any(x.unsqueeze(1 if nlc else 2), weight.unsqueeze(2), bias, (1, s), (0, p),
+                             (1, d), groups, nhwc=nlc)
+        if y is not None:
+            return y.squeeze(1 if nlc else 2)
+    return _fmt_out(TF.conv1d(_fmt_in(x, data_format), weight, bias, stride, pad, dilation, groups), data_format)
 
 
 def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NCHW", name=None):
+    """Reference `nn/functional/conv.py:conv2d`; GPU tensors run on the framework's own kernels
+    (``ops.conv.conv2d_any``: MFMA implicit GEMM for dense bf16/fp16, direct NHWC kernels for
+    grouped / depthwise in any float dtype; NCHW via the channels_last view)."""
     nhwc = data_format == "NHWC"
     pad = _padding(padding, 2)
-    if _hip_conv_ok(x, weight, groups, pad, nhwc):
+    if pad == "valid":
+        pad = 0
+    elif pad == "same" and stride in (1, (1, 1), [1, 1]):
+        dl = (dilation, dilation) if isinstance(dilation, int) else tuple(dilation)
+        tot = [dl[i] * (weight.shape[2 + i] - 1) for i in range(2)]
+        if all(t % 2 == 0 for t in tot):
+            pad = (tot[0] // 2, tot[1] // 2)
+    if x.is_cuda:
         from ...ops import conv as _conv
-        with torch.autocast("cuda", enabled=False):
-            if nhwc:
-                return _conv.conv2d_nhwc(x, weight, bias, stride, pad, dilation)
-            return _conv.conv2d_nchw(x, weight, bias, stride, pad, dilation)
-    return _fmt_out(TF.conv2d(_fmt_in(x, data_format), weight, bias, stride, _padding(padding, 2), dilation, groups), data_format)
+        y = _conv.conv2d_any(x, weight, bias, stride, pad, dilation, groups, nhwc)
+        if y is not None:
+            return y
+    return _fmt_out(TF.conv2d(_fmt_in(x, data_format), weight, bias, stride, pad, dilation, groups), data_format)
 
 
 def conv3d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NCDHW", name=None):

@@ -228,8 +228,8 @@ _SIGS["piamd_gemm_i8"] = [c_void_p, c_ll, c_void_p, c_ll, c_void_p, c_float, c_v
 _SIGS["piamd_quant_rows"] = [c_void_p, c_ll, c_void_p, c_ll, c_void_p, c_float, c_int, c_int,
                              c_void_p]
 # x, w_ohwi, zero, y, N, H, W, C, OH, OW, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w, Kout, act,
-# bias, tile_n, ksplit, ws, stream
-_SIGS["piamd_conv2d_fwd"] = [c_void_p] * 4 + [c_int] * 16 + [c_void_p, c_int, c_int, c_void_p, c_void_p]
+# bias, tile_n, ksplit, ws, f16, stream
+_SIGS["piamd_conv2d_fwd"] = [c_void_p] * 4 + [c_int] * 16 + [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]
 # dtype, nhwc, x, res, y, N, C, S, gamma, beta, run_mean, run_var, mean, rstd, momentum, eps,
 # training, act, ws, stream
 _SIGS["piamd_bn_fwd"] = ([c_int, c_int] + [c_void_p] * 3 + [c_int] * 3 + [c_void_p] * 6
@@ -237,9 +237,15 @@ _SIGS["piamd_bn_fwd"] = ([c_int, c_int] + [c_void_p] * 3 + [c_int] * 3 + [c_void
 # dtype, nhwc, dy, y, x, dx, dres, N, C, S, gamma, mean, rstd, dgamma, dbeta, training, act, ws, stream
 _SIGS["piamd_bn_bwd"] = ([c_int, c_int] + [c_void_p] * 5 + [c_int] * 3 + [c_void_p] * 5
                          + [c_int, c_int, c_void_p, c_void_p])
+# in, w, bias, out, N, H, W, Cin, OH, OW, Cout, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w,
+# cin_g, cout_g, transposed, dtype, stream
+_SIGS["piamd_dconv2d"] = [c_void_p] * 4 + [c_int] * 19 + [c_void_p]
+# x, dy, d, ws, parts, N, H, W, Cin, OH, OW, Cout, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w,
+# cin_g, cout_g, dtype, stream
+_SIGS["piamd_dconv2d_wgrad"] = [c_void_p] * 4 + [c_int] * 19 + [c_void_p]
 # x, dy, zero, d, N, H, W, C, OH, OW, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w, Kout, tile_n,
-# ksplit, ws, accumulate, stream
-_SIGS["piamd_conv2d_wgrad"] = [c_void_p] * 4 + [c_int] * 17 + [c_void_p, c_int, c_void_p]
+# ksplit, ws, accumulate, f16, stream
+_SIGS["piamd_conv2d_wgrad"] = [c_void_p] * 4 + [c_int] * 17 + [c_void_p, c_int, c_int, c_void_p]
 # op, meta, fmeta, chunk_off, T, total_chunks, lr, mu, nesterov, beta1, beta2, eps, bc1, bc2_sqrt,
 # grad_scale, stream
 _SIGS["piamd_multi_tensor_update"] = ([c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float,

@@ -1,17 +1,25 @@
-"""NHWC bf16 convolution on the MFMA implicit-GEMM kernel (``csrc/kernels/gemm.hip`` conv_fwd).
+"""NHWC convolution on the framework's own kernels — every 2-D conv of a bf16/fp16 (or autocast)
+model, and every grouped/depthwise conv in any float dtype, runs without the library (MIOpen).
 
 Parity: reference `phi/kernels/gpudnn/conv_kernel.cu` + `conv_grad_kernel.cu` (cuDNN forward /
-backward-data / backward-filter) and the fused conv+bias+act of `fused_conv2d_add_act_kernel.cu`.
+backward-data / backward-filter), `phi/kernels/gpu/depthwise_conv_kernel.cu` (depthwise) and the
+fused conv+bias+act of `fused_conv2d_add_act_kernel.cu`.
 
-* forward: one kernel, bias + activation in the epilogue, activation gathered straight from the
-  NHWC tensor by the LDS DMA (no im2col buffer);
-* backward-data: for stride 1 the data gradient is itself a stride-1 convolution of dY with the
-  spatially flipped, in/out-transposed filter (padding ``dil·(R−1) − pad``) and runs on the same
-  kernel; other strides use the library (MIOpen) backward-data;
-* backward-filter: library (MIOpen) on the channels-last views, bias gradient a column sum.
+Routes (``conv2d_any``, called by ``nn.functional.conv2d`` for GPU tensors):
 
-Eligible: groups 1, C % 64 == 0, K_out % 4 == 0, symmetric zero padding, bf16 on the GPU.
-``conv2d_nhwc`` raises on an ineligible call; ``eligible`` tells the dispatcher.
+* dense (groups 1), bf16 / fp16 → MFMA implicit GEMM (``csrc/kernels/gemm.hip`` conv_fwd, bf16 or
+  f16 MFMA): bias + activation in the epilogue, the activation gathered straight from the NHWC
+  tensor by the LDS DMA (no im2col buffer). Channel counts that are not a multiple of 64 are
+  zero-padded to one (≤ 8 input channels: stem mode, eight taps per k-step);
+  - data gradient: stride 1 → the same kernel on dY with the flipped, in/out-transposed filter;
+    other strides → one stride-1 sub-convolution per output phase;
+  - weight gradient: the implicit-GEMM wgrad kernel (reduction over N·OH·OW output pixels);
+* dense 1×1 with unaligned channels → a plain GEMM over the pixel rows (``ops.linear.mm_nt``);
+* grouped / depthwise, any float dtype → the direct NHWC kernels of ``csrc/kernels/conv_dw.hip``
+  (forward, transposed-geometry data gradient, deterministic split weight gradient);
+* NCHW inputs are used through their channels_last view when they have one; a plain NCHW tensor
+  is re-laid-out once (the output is channels_last, so every later layer takes the view);
+* dense fp32 without autocast stays on the library (recorded by ``_lib.fallback``).
 """
 from __future__ import annotations
 
@@ -31,18 +39,29 @@ def _zero(dev):
     return z
 
 
+_HALF = (torch.bfloat16, torch.float16)
+
+
+def _f16(t) -> int:
+    return int(t.dtype == torch.float16)
+
+
+def _pad64(n: int) -> int:
+    return -(-n // 64) * 64
+
+
 def _pair(v):
     return (v, v) if isinstance(v, int) else tuple(v)
 
 
 def eligible(x_nhwc_shape, w_shape, groups=1, padding=0) -> bool:
+    """Dense conv the MFMA kernels take: groups 1, symmetric padding, matching channels (channel
+    counts off the 64-grid are zero-padded; ≤ 8 input channels run in stem mode)."""
     if groups != 1 or isinstance(padding, str) or len(w_shape) != 4:
         return False
     if len(_pair(padding)) != 2:
         return False
-    C, K = x_nhwc_shape[-1], w_shape[0]
-    # C ≤ 8: stem mode (channels zero-padded to 8, eight taps per 64-deep k-step)
-    return (C % 64 == 0 or C <= 8) and K % 4 == 0 and w_shape[1] == C
+    return w_shape[1] == x_nhwc_shape[-1]
 
 
 def _out_hw(H, W, R, S, st, pad, dil):
@@ -88,15 +107,15 @@ def _launch(x, w_ohwi, bias, st, pad, dil, act, rs=None):
         raise ValueError("convolution output is empty")
     M = N * OH * OW
     nk = -(-(R * S) // 8) if rs is not None else R * S * (C // 64)
-    y = torch.empty(N, OH, OW, K, dtype=torch.bfloat16, device=x.device)
-    b = bias.to(torch.bfloat16).contiguous() if bias is not None else None
+    y = torch.empty(N, OH, OW, K, dtype=x.dtype, device=x.device)
+    b = bias.to(x.dtype).contiguous() if bias is not None else None
 
     def run(plan):
         tn, ks = plan
         ws = torch.empty(ks * M * K, dtype=torch.float32, device=x.device) if ks > 1 else None
         _lib.call("piamd_conv2d_fwd", x.data_ptr(), w_ohwi.data_ptr(), _zero(x.device).data_ptr(),
                   y.data_ptr(), N, H, W, C, OH, OW, R, S, st[0], st[1], pad[0], pad[1], dil[0],
-                  dil[1], K, act, _lib.ptr(b), tn, ks, _lib.ptr(ws), _lib.stream())
+                  dil[1], K, act, _lib.ptr(b), tn, ks, _lib.ptr(ws), _f16(x), _lib.stream())
     plan = PLAN_OVERRIDE or _autotuned("conv2d_fwd", (N, H, W, C, K, R, S, st, pad, dil, act),
                                        _plan(M, K, nk), _fwd_candidates(M, K, nk), run)
     run(plan)
@@ -136,8 +155,8 @@ def wgrad_eligible(C, K, M) -> bool:
 
 
 def conv2d_wgrad(x, dy, R, S, st, pad, dil):
-    """dW [K][C][R][S] f32 of conv(x [N,H,W,C], ·) given dy [N,OH,OW,K] (both bf16 NHWC
-    contiguous) on the HIP implicit-GEMM weight-gradient kernel."""
+    """dW [K][C][R][S] f32 of conv(x [N,H,W,C], ·) given dy [N,OH,OW,K] (both bf16 or both fp16,
+    NHWC contiguous) on the HIP implicit-GEMM weight-gradient kernel."""
     N, H, W, C = x.shape
     _, OH, OW, K = dy.shape
     M, RSC = N * OH * OW, R * S * C
@@ -152,7 +171,7 @@ def conv2d_wgrad(x, dy, R, S, st, pad, dil):
         ws = torch.empty(ks * RSC * K, dtype=torch.float32, device=x.device) if ks > 1 else None
         _lib.call("piamd_conv2d_wgrad", x.data_ptr(), dy.data_ptr(), _zero(x.device).data_ptr(),
                   d.data_ptr(), N, H, W, C, OH, OW, R, S, st[0], st[1], pad[0], pad[1], dil[0],
-                  dil[1], K, tn, ks, _lib.ptr(ws), 0, _lib.stream())
+                  dil[1], K, tn, ks, _lib.ptr(ws), 0, _f16(x), _lib.stream())
     default = _wgrad_plan(M, RSC, K)
     cands = [(tn, ks) for tn in (64, 128, 256) if K % tn == 0
              for ks in (1, 4, 16, 64, 256) if ks <= nk and ks * RSC * K * 4 <= (256 << 20)]
@@ -177,13 +196,13 @@ def _phase_taps(R, st, pad, dil, ph):
 
 
 def conv2d_dgrad_strided(dy, weight, H, W, st, pad, dil):
-    """dX [N,H,W,C] bf16 of a strided conv: one stride-1 HIP convolution per output phase
+    """dX [N,H,W,C] (dtype of dy) of a strided conv: one stride-1 HIP convolution per output phase
     (ih mod st_h, iw mod st_w) over dY with the sub-filter of the taps that reach that phase,
     scattered into dX (phases with no tap are zero)."""
     N, OH, OW, K = dy.shape
     Kw, C, R, S = weight.shape
-    dx = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=dy.device)
-    wb = weight.to(torch.bfloat16)
+    dx = torch.empty(N, H, W, C, dtype=dy.dtype, device=dy.device)
+    wb = weight.to(dy.dtype)
     for ph in range(st[0]):
         for pw in range(st[1]):
             Hp, Wp = -(-(H - ph) // st[0]), -(-(W - pw) // st[1])
@@ -207,34 +226,49 @@ def _launch_geom(x, w_ohwi, st, pad, dil, OH, OW):
     K, R, S, _ = w_ohwi.shape
     M = N * OH * OW
     nk = R * S * (C // 64)
-    y = torch.empty(N, OH, OW, K, dtype=torch.bfloat16, device=x.device)
+    y = torch.empty(N, OH, OW, K, dtype=x.dtype, device=x.device)
 
     def run(plan):
         tn, ks = plan
         ws = torch.empty(ks * M * K, dtype=torch.float32, device=x.device) if ks > 1 else None
         _lib.call("piamd_conv2d_fwd", x.data_ptr(), w_ohwi.data_ptr(), _zero(x.device).data_ptr(),
                   y.data_ptr(), N, H, W, C, OH, OW, R, S, st[0], st[1], pad[0], pad[1], dil[0],
-                  dil[1], K, 0, 0, tn, ks, _lib.ptr(ws), _lib.stream())
+                  dil[1], K, 0, 0, tn, ks, _lib.ptr(ws), _f16(x), _lib.stream())
     run(_autotuned("conv2d_dgrad", (N, H, W, C, K, R, S, st, pad, dil, OH, OW), _plan(M, K, nk),
                    _fwd_candidates(M, K, nk), run))
     return y
 
 
+def _padc(t, n):
+    """zero-pad the last dim of t to n."""
+    return t if t.shape[-1] == n else torch.nn.functional.pad(t, (0, n - t.shape[-1]))
+
+
 class _Conv2dNHWC(torch.autograd.Function):
+    """Dense conv on the MFMA kernels: x [N,H,W,C0] bf16/fp16 (contiguous), weight [K0,C0,R,S]."""
+
     @staticmethod
     def forward(ctx, x, weight, bias, st, pad, dil, act):
-        C0 = x.shape[-1]
-        if C0 % 64:  # stem mode: zero-pad the image channels to 8
-            xc = torch.nn.functional.pad(x, (0, 8 - C0)).contiguous() if C0 < 8 else x.contiguous()
-            K, _, R, S = weight.shape
+        dt = x.dtype
+        K0, C0, R, S = weight.shape
+        K = -(-K0 // 4) * 4  # the epilogue stores 4 output channels per lane
+        wq = weight.to(dt)
+        if K != K0:
+            wq = torch.nn.functional.pad(wq, (0, 0, 0, 0, 0, 0, 0, K - K0))
+        b = None if bias is None else _padc(bias.to(dt), K)
+        if C0 <= 8:  # stem mode: zero-pad the image channels to 8
+            xc = _padc(x, 8).contiguous()
             nk = -(-(R * S) // 8)
-            w8 = torch.zeros(K, nk * 64, dtype=torch.bfloat16, device=x.device)
-            w8[:, :R * S * 8].view(K, R, S, 8)[..., :C0] = weight.to(torch.bfloat16).permute(0, 2, 3, 1)
-            y = _launch(xc, w8.view(K, 1, nk * 8, 8), bias, st, pad, dil, act, rs=(R, S))
-        else:
-            xc = x.contiguous()
-            w_ohwi = weight.to(torch.bfloat16).permute(0, 2, 3, 1).contiguous()
-            y = _launch(xc, w_ohwi, bias, st, pad, dil, act)
+            w8 = torch.zeros(K, nk * 64, dtype=dt, device=x.device)
+            w8[:, :R * S * 8].view(K, R, S, 8)[..., :C0] = wq.permute(0, 2, 3, 1)
+            y = _launch(xc, w8.view(K, 1, nk * 8, 8), b, st, pad, dil, act, rs=(R, S))
+        else:  # channels zero-padded to a multiple of 64 (one k-step never straddles two taps)
+            C = _pad64(C0)
+            xc = _padc(x, C).contiguous()
+            w_ohwi = _padc(wq.permute(0, 2, 3, 1), C).contiguous()
+            y = _launch(xc, w_ohwi, b, st, pad, dil, act)
+        if K != K0:
+            y = y[..., :K0].contiguous()
         ctx.save_for_backward(xc, weight, y if act else None)
         ctx.cfg = (st, pad, dil, act, bias is not None)
         return y
@@ -243,49 +277,197 @@ class _Conv2dNHWC(torch.autograd.Function):
     def backward(ctx, dy):
         x, weight, y = ctx.saved_tensors
         st, pad, dil, act, has_bias = ctx.cfg
-        dy = dy.to(torch.bfloat16)
+        dt = x.dtype
+        dy = dy.to(dt)
         if act == 3:
             dy = dy * (y > 0)
         dy = dy.contiguous()
-        K, C0, R, S = weight.shape
-        C = x.shape[-1]  # == C0, or 8 in stem mode (zero-padded channels)
-        if C != C0:
-            weight = torch.nn.functional.pad(weight, (0, 0, 0, 0, 0, C - C0))
-        dx = dw = db = None
+        K0, C0, R, S = weight.shape
+        C = x.shape[-1]  # == C0, or C0 zero-padded (to 8 in stem mode, else to a multiple of 64)
         N, H, W, _ = x.shape
+        M = dy.shape[0] * dy.shape[1] * dy.shape[2]
+        Kp = _pad64(K0)  # dY channels padded: the dgrad reduction / wgrad tile runs over 64s
+        wq = weight.to(dt)
+        wq = torch.nn.functional.pad(wq, (0, 0, 0, 0, 0, C - C0, 0, Kp - K0))
+        dyp = _padc(dy, Kp)
+        dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            pad_t = (dil[0] * (R - 1) - pad[0], dil[1] * (S - 1) - pad[1])
-            if K % 64 == 0 and C % 4 == 0 and st == (1, 1) and dy.shape[1:3] == (H, W):
+            if st == (1, 1) and dy.shape[1:3] == (H, W):
                 # dX = conv(dY, flip(W)ᵀ): filter [C][R][S][K] = W[k][c][R-1-r][S-1-s]
-                w_t = weight.to(torch.bfloat16).flip(2, 3).permute(1, 2, 3, 0).contiguous()
-                dx = _launch_geom(dy, w_t, (1, 1), pad_t, dil, H, W)
-            elif K % 64 == 0 and C % 4 == 0:
-                dx = conv2d_dgrad_strided(dy, weight, H, W, st, pad, dil)
+                pad_t = (dil[0] * (R - 1) - pad[0], dil[1] * (S - 1) - pad[1])
+                w_t = wq.flip(2, 3).permute(1, 2, 3, 0).contiguous()
+                dx = _launch_geom(dyp, w_t, (1, 1), pad_t, dil, H, W)
             else:
-                _lib.fallback("conv2d_dgrad", f"K_out={K} C={C} (needs K%64, C%4)")
-                dx = torch.ops.aten.convolution_backward(
-                    dy.permute(0, 3, 1, 2), x.permute(0, 3, 1, 2), weight.to(torch.bfloat16),
-                    None, list(st), list(pad), list(dil), False, [0, 0], 1,
-                    [True, False, False])[0].permute(0, 2, 3, 1)
+                dx = conv2d_dgrad_strided(dyp, wq, H, W, st, pad, dil)
+            dx = dx[..., :C0] if C != C0 else dx
         if ctx.needs_input_grad[1]:
-            if wgrad_eligible(C, K, dy.shape[0] * dy.shape[1] * dy.shape[2]):
-                dw = conv2d_wgrad(x, dy, R, S, st, pad, dil)
-            else:
-                _lib.fallback("conv2d_wgrad", f"K_out={K} C={C} (needs K%64, C%8)")
-                dw = torch.ops.aten.convolution_backward(
-                    dy.permute(0, 3, 1, 2), x.permute(0, 3, 1, 2), weight.to(torch.bfloat16), None,
-                    list(st), list(pad), list(dil), False, [0, 0], 1, [False, True, False])[1]
+            if wgrad_eligible(C, Kp, M):
+                dw = conv2d_wgrad(x, dyp, R, S, st, pad, dil)[:K0, :C0]
+            else:  # > 2^24 output pixels: the direct kernel's pixel-chunked reduction
+                dw = _direct_wgrad(x[..., :C0].contiguous(), dy, R, S, st, pad, dil, C0, K0)
             dw = dw.to(weight.dtype)
-        if C != C0:
-            dx = dx[..., :C0] if dx is not None else None
-            dw = dw[:, :C0].contiguous() if dw is not None else None
         if has_bias and ctx.needs_input_grad[2]:
-            db = dy.float().sum((0, 1, 2))
+            db = dy.float().sum((0, 1, 2)).to(weight.dtype)
         return dx, dw, db, None, None, None, None
 
 
+# ---------------------------------------------------------------- direct grouped / depthwise conv
+_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+
+def _direct_v(dt, K, kg, dw):
+    vmax = 4 if dt == torch.float32 else 8
+    return vmax if K % vmax == 0 and (dw or kg % vmax == 0) else 1
+
+
+def _direct_wgrad(x, dy, R, S, st, pad, dil, C, K, groups=1):
+    """dW [K][C/groups][R][S] f32 on the direct kernel's deterministic split reduction."""
+    N, H, W, _ = x.shape
+    _, OH, OW, _ = dy.shape
+    cg, kg = C // groups, K // groups
+    M = N * OH * OW
+    v = _direct_v(x.dtype, K, kg, cg == 1 and kg == 1)
+    ncol = (K // v) * cg
+    cb = 1
+    while cb < ncol and cb < 64:
+        cb *= 2
+    gy, gz, pl = -(-ncol // cb), -(-(R * S) // 9), 256 // cb
+    plane = R * S * cg * K
+    parts = max(1, min(-(-2048 // (gy * gz)), M // (pl * 8), (16 << 20) // plane))
+    d = torch.empty(plane, dtype=torch.float32, device=x.device)
+    ws = torch.empty(parts * plane, dtype=torch.float32, device=x.device)
+    _lib.call("piamd_dconv2d_wgrad", x.data_ptr(), dy.data_ptr(), d.data_ptr(), ws.data_ptr(), parts,
+              N, H, W, C, OH, OW, K, R, S, st[0], st[1], pad[0], pad[1], dil[0], dil[1], cg, kg,
+              _DT[x.dtype], _lib.stream())
+    return d.view(R, S, cg, K).permute(3, 2, 0, 1)
+
+
+def _direct(inp, w_rsck, bias, OH, OW, Cout, R, S, st, pad, dil, cin_g, cout_g, transposed):
+    N, H, W, Cin = inp.shape
+    out = torch.empty(N, OH, OW, Cout, dtype=inp.dtype, device=inp.device)
+    _lib.call("piamd_dconv2d", inp.data_ptr(), w_rsck.data_ptr(), _lib.ptr(bias), out.data_ptr(),
+              N, H, W, Cin, OH, OW, Cout, R, S, st[0], st[1], pad[0], pad[1], dil[0], dil[1],
+              cin_g, cout_g, int(transposed), _DT[inp.dtype], _lib.stream())
+    return out
+
+
+class _ConvDirect(torch.autograd.Function):
+    """Grouped / depthwise conv, x [N,H,W,C] (f32, bf16 or fp16), weight [K, C/groups, R, S]."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, st, pad, dil, groups):
+        dt = x.dtype
+        N, H, W, C = x.shape
+        K, cg, R, S = weight.shape
+        kg = K // groups
+        OH, OW = _out_hw(H, W, R, S, st, pad, dil)
+        if OH < 1 or OW < 1:
+            raise ValueError("convolution output is empty")
+        w_rsck = weight.to(dt).permute(2, 3, 1, 0).contiguous()  # W'[r][s][c][k]
+        b = bias.to(dt).contiguous() if bias is not None else None
+        y = _direct(x, w_rsck, b, OH, OW, K, R, S, st, pad, dil, cg, kg, False)
+        ctx.save_for_backward(x, weight)
+        ctx.cfg = (st, pad, dil, groups, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        st, pad, dil, groups, has_bias = ctx.cfg
+        dt = x.dtype
+        dy = dy.to(dt).contiguous()
+        N, H, W, C = x.shape
+        K, cg, R, S = weight.shape
+        kg = K // groups
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            # transposed geometry: in = dY (K channels, groups of kg), out = dX (C, groups of cg),
+            # W''[r][s][k_local][c] = W[g·kg + k_local][c − g·cg][r][s]
+            w_t = (weight.to(dt).view(groups, kg, cg, R, S).permute(3, 4, 1, 0, 2)
+                   .reshape(R, S, kg, C).contiguous())
+            dx = _direct(dy, w_t, None, H, W, C, R, S, st, pad, dil, kg, cg, True)
+        if ctx.needs_input_grad[1]:
+            dw = _direct_wgrad(x, dy, R, S, st, pad, dil, C, K, groups).to(weight.dtype)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = dy.float().sum((0, 1, 2)).to(weight.dtype)
+        return dx, dw, db, None, None, None, None
+
+
+class _Conv1x1(torch.autograd.Function):
+    """Dense 1×1 conv with channels off the 64-grid as a GEMM over pixel rows (ops.linear.mm_nt:
+    the framework's assembly GEMM where its contract holds, hipBLASLt otherwise)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, st):
+        from .linear import mm_nt
+        dt = x.dtype
+        xs = x[:, ::st[0], ::st[1]] if st != (1, 1) else x
+        N, OH, OW, C = xs.shape
+        K = weight.shape[0]
+        x2 = xs.reshape(-1, C)
+        w_kc = weight.to(dt).reshape(K, C)
+        y2 = mm_nt(x2, w_kc, bias.to(dt) if bias is not None else None)
+        ctx.save_for_backward(x2, w_kc)
+        ctx.cfg = (tuple(x.shape), st, bias is not None, weight.dtype)
+        return y2.view(N, OH, OW, K)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w_kc = ctx.saved_tensors
+        xshape, st, has_bias, wdt = ctx.cfg
+        K, C = w_kc.shape
+        dy2 = dy.to(x2.dtype).reshape(-1, K)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx2 = torch.mm(dy2, w_kc)
+            if st != (1, 1):
+                dx = torch.zeros(xshape, dtype=x2.dtype, device=x2.device)
+                dx[:, ::st[0], ::st[1]] = dx2.view(dy.shape[:3] + (C,))
+            else:
+                dx = dx2.view(xshape)
+        if ctx.needs_input_grad[1]:
+            dw = torch.mm(dy2.t(), x2).view(K, C, 1, 1).to(wdt)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = dy2.float().sum(0).to(wdt)
+        return dx, dw, db, None
+
+
+def conv2d_any(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, nhwc=False):
+    """Own-kernel route for a 2-D conv of a GPU tensor (NCHW or NHWC by ``nhwc``); ``None`` when
+    the call stays on the library (fp32 dense conv without autocast, string padding)."""
+    if not (HIP_CONV and x.is_cuda and x.dim() == 4 and weight.dim() == 4) or isinstance(padding, str):
+        return None
+    pad, st, dil = _pair(padding), _pair(stride), _pair(dilation)
+    if len(pad) != 2 or len(st) != 2 or len(dil) != 2:
+        return None
+    dt = x.dtype
+    if torch.is_autocast_enabled("cuda") and dt in _DT:
+        dt = torch.get_autocast_dtype("cuda")
+    if dt not in _DT:
+        return None
+    C = x.shape[-1] if nhwc else x.shape[1]
+    K, cg, R, S = weight.shape
+    if cg * groups != C or K % groups:
+        raise ValueError(f"conv2d: weight {tuple(weight.shape)} does not match {C} input channels "
+                         f"in {groups} groups")
+    if groups == 1 and dt == torch.float32:
+        _lib.fallback("conv2d", "dense fp32 conv without autocast (library)")
+        return None
+    with torch.autocast("cuda", enabled=False):
+        xh = (x if nhwc else x.permute(0, 2, 3, 1)).to(dt)
+        xh = xh.contiguous()  # a view for NHWC / channels_last storage; one re-layout otherwise
+        if groups > 1:
+            y = _ConvDirect.apply(xh, weight, bias, st, pad, dil, groups)
+        elif R == S == 1 and pad == (0, 0) and C % 64 and C > 8:
+            y = _Conv1x1.apply(xh, weight, bias, st)
+        else:
+            y = _Conv2dNHWC.apply(xh, weight, bias, st, pad, dil, 0)
+    return y if nhwc else y.permute(0, 3, 1, 2)
+
+
 def conv2d_nhwc(x, weight, bias=None, stride=1, padding=0, dilation=1, act=None):
-    """y[N,OH,OW,K] = act(conv(x[N,H,W,C], weight[K,C,R,S]) + bias) in bf16 on the HIP kernel."""
+    """y[N,OH,OW,K] = act(conv(x[N,H,W,C], weight[K,C,R,S]) + bias) on the MFMA kernel, in x's
+    dtype when bf16/fp16 (else bf16)."""
     if not (x.is_cuda and x.dim() == 4):
         raise ValueError("conv2d_nhwc needs a 4-D GPU tensor")
     if not eligible(x.shape, weight.shape, 1, padding):
@@ -293,7 +475,8 @@ def conv2d_nhwc(x, weight, bias=None, stride=1, padding=0, dilation=1, act=None)
     if act not in _ACT:
         raise ValueError(f"conv2d_nhwc: unsupported activation {act}")
     st, pad, dil = _pair(stride), _pair(padding), _pair(dilation)
-    return _Conv2dNHWC.apply(x.to(torch.bfloat16), weight, bias, st, pad, dil, _ACT[act])
+    xh = x if x.dtype in _HALF else x.to(torch.bfloat16)
+    return _Conv2dNHWC.apply(xh, weight, bias, st, pad, dil, _ACT[act])
 
 
 def conv2d_nchw(x, weight, bias=None, stride=1, padding=0, dilation=1, act=None):

@@ -344,6 +344,8 @@ template <> __device__ __forceinline__ void st8<float>(float* p, const float (&v
 
 // Statistics: per thread shifted sums (shift = the block's first row — robust, no per-element
 // divide), converted to (n, mean, M2) and Welford-merged over the block's row lanes.
+constexpr int SR = 8;  // statistics rows in flight per lane
+constexpr int RR = 4;  // backward-reduction rows in flight per lane (× 2-3 inputs)
 template <typename T>
 __global__ __launch_bounds__(256) void bn_stats_nhwc8(const T* __restrict__ x, long long M, int C,
                                                       long long chunk, float* __restrict__ part) {
@@ -360,17 +362,17 @@ __global__ __launch_bounds__(256) void bn_stats_nhwc8(const T* __restrict__ x, l
     if (live) {
       ld8(x + beg * C + cg * 8, sh);
       long long r = beg + rl;
-      // 4 rows per trip: four independent 16-B loads in flight per lane (the single-row loop
-      // was load-latency bound at ~5 TB/s against ~12 TB/s for the apply pass)
-      for (; r + 3 * RB < end; r += 4 * RB) {
-        float v[4][8];
+      // SR rows per trip: SR independent 16-B loads in flight per lane (a single-row loop was
+      // load-latency bound; 4 rows ran at 2.3 TB/s with 2 waves per SIMD)
+      for (; r + (SR - 1) * RB < end; r += SR * RB) {
+        float v[SR][8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) ld8(x + (r + u * RB) * C + cg * 8, v[u]);
+        for (int u = 0; u < SR; ++u) ld8(x + (r + u * RB) * C + cg * 8, v[u]);
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < SR; ++u)
 #pragma unroll
           for (int j = 0; j < 8; ++j) { const float d = v[u][j] - sh[j]; s[j] += d; q[j] += d * d; }
-        n += 4.f;
+        n += (float)SR;
       }
       for (; r < end; r += RB) {
         float v[8];
@@ -438,18 +440,18 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_nhwc8(const T* __restrict__
     for (int j = 0; j < 8; ++j) { s1[j] = s2[j] = 0.f; mu[j] = live ? mean[cg * 8 + j] : 0.f; }
     if (live) {
       long long r = beg + rl;
-      // 2 rows per trip (4 or 6 independent 16-B loads in flight per lane)
-      for (; r + RB < end; r += 2 * RB) {
-        float g[2][8], xv[2][8], yv[2][8];
+      // RR rows per trip (2·RR or 3·RR independent 16-B loads in flight per lane)
+      for (; r + (RR - 1) * RB < end; r += RR * RB) {
+        float g[RR][8], xv[RR][8], yv[RR][8];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < RR; ++u) {
           const long long i = (r + u * RB) * C + cg * 8;
           ld8(dy + i, g[u]);
           ld8(x + i, xv[u]);
           if (act) ld8(y + i, yv[u]);
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < RR; ++u) {
           if (act) {
 #pragma unroll
             for (int j = 0; j < 8; ++j)
@@ -578,20 +580,33 @@ int parts_for(long long M) {
   return (int)(p < 1 ? 1 : (p > 512 ? 512 : p));
 }
 
-// vectorised NHWC: ≈ 64 K elements per block, ≤ 512 blocks, ≥ 1 row each
+// vectorised NHWC: ≈ g_bn_elems elements per block (default 64 K), ≥ 16 rows each (the [P][C]
+// partials stay ≤ 1/16 of the data), ≤ g_bn_parts ≤ MAX_PARTS blocks (default 512).
+constexpr int MAX_PARTS = 2048;
+long long g_bn_elems = 65536;
+int g_bn_parts = 512;
 int parts_for8(long long M, int C) {
-  long long p = (M * C + 65535) / 65536;
-  p = p > 512 ? 512 : p;
-  p = p > M ? M : p;
+  long long p = (M * C + g_bn_elems - 1) / g_bn_elems;
+  const long long lim = M / 16;
+  p = p > lim ? lim : p;
+  p = p > g_bn_parts ? g_bn_parts : p;
   return (int)(p < 1 ? 1 : p);
 }
 
 }  // namespace
 
+// Tuning hook for the NHWC statistics / reduction grid (elements per block, block cap ≤ 2048).
+PIAMD_EXPORT int piamd_bn_set_parts(long long elems_per_block, int max_parts) {
+  if (elems_per_block < 1024 || max_parts < 1 || max_parts > MAX_PARTS) return (int)hipErrorInvalidValue;
+  g_bn_elems = elems_per_block;
+  g_bn_parts = max_parts;
+  return 0;
+}
+
 // Forward. x/res/y: [N, C, S] (nhwc = 0) or [N·S, C] (nhwc = 1); dtype 0 = f32, 1 = bf16.
 // training: statistics of x → mean/rstd (f32 [C], saved for backward), running stats updated in
 // place (momentum: Paddle convention); else the running statistics (mean/rstd still written).
-// ws: f32 workspace of ≥ 2·C + 3·512·C floats. act: 0 none, 1 relu, 2 relu6.
+// ws: f32 workspace of ≥ 2·C + 3·2048·C floats. act: 0 none, 1 relu, 2 relu6.
 // nhwc requires C % 8 == 0 (vectorised path), C ≥ 256 or C | 256.
 PIAMD_EXPORT int piamd_bn_fwd(int dtype, int nhwc, const void* x, const void* res, void* y, int N,
                               int C, int S, const float* gamma, const float* beta,
@@ -646,7 +661,7 @@ PIAMD_EXPORT int piamd_bn_fwd(int dtype, int nhwc, const void* x, const void* re
 
 // Backward. y = the forward OUTPUT (act' from it); dres (nullable) receives dz = ∂L/∂(bn + res).
 // training = 0: the statistics are constants (dx = γ·rstd·dz). dgamma / dbeta: f32 [C]
-// (nullable). ws: ≥ 3·C + 2·512·C floats.
+// (nullable). ws: ≥ 3·C + 2·2048·C floats.
 PIAMD_EXPORT int piamd_bn_bwd(int dtype, int nhwc, const void* dy, const void* y, const void* x,
                               void* dx, void* dres, int N, int C, int S, const float* gamma,
                               const float* mean, const float* rstd, float* dgamma, float* dbeta,

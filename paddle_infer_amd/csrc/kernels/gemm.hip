@@ -611,14 +611,28 @@ __global__ __launch_bounds__(NTHR, 1) void conv_wgrad_kernel(
                             n0, g.Kout, EPI_STORE, 0, nullptr, nullptr, 0);
 }
 
-// D (+)= Σ_p ws[p] in a fixed order (f32, 4 per thread)
+// D (+)= Σ_p ws[p] in a fixed order (f32, 4 per thread). SL slices of the ksplit planes per output
+// vector (slice s sums planes s, s + SL, …; then slices 0..SL-1 in order through LDS): with many
+// split parts over a small filter (ks up to 256 planes of a 1×1 layer) a one-thread-per-output
+// loop was a long serial chain on a handful of workgroups.
+template <int SL>
 __global__ __launch_bounds__(256) void wgrad_splitk_finish(const float* __restrict__ ws, int ksplit,
                                                            long long MN, float* __restrict__ d,
                                                            int accumulate) {
-  const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
+  constexpr int VPB = 256 / SL;  // output vectors per block
+  const int t = threadIdx.x, vl = t % VPB, sl = t / VPB;
+  const long long i = ((long long)blockIdx.x * VPB + vl) * 4;
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+  if (i < MN)
+    for (int p = sl; p < ksplit; p += SL) v += *reinterpret_cast<const f32x4*>(ws + p * MN + i);
+  if constexpr (SL > 1) {
+    __shared__ f32x4 red[256];
+    red[t] = v;
+    __syncthreads();
+    if (sl) return;
+    for (int k = 1; k < SL; ++k) v += red[k * VPB + vl];
+  }
   if (i >= MN) return;
-  f32x4 v = *reinterpret_cast<const f32x4*>(ws + i);
-  for (int p = 1; p < ksplit; ++p) v += *reinterpret_cast<const f32x4*>(ws + p * MN + i);
   f32x4* o = reinterpret_cast<f32x4*>(d + i);
   if (accumulate) v += *o;
   *o = v;
@@ -859,8 +873,16 @@ PIAMD_EXPORT int piamd_conv2d_wgrad(const void* x, const void* dy, const void* z
 #undef CONV_WG
   if (ksplit > 1) {
     const long long MN = RSC * Kout;
-    hipLaunchKernelGGL(wgrad_splitk_finish, dim3((unsigned)((MN / 4 + 255) / 256)), dim3(256), 0, st,
-                       (const float*)ws, ksplit, MN, d, accumulate);
+    const long long nv = MN / 4;
+    if (ksplit >= 64 && nv < 65536)
+      hipLaunchKernelGGL(wgrad_splitk_finish<16>, dim3((unsigned)((nv + 15) / 16)), dim3(256), 0, st,
+                         (const float*)ws, ksplit, MN, d, accumulate);
+    else if (ksplit >= 8 && nv < 262144)
+      hipLaunchKernelGGL(wgrad_splitk_finish<4>, dim3((unsigned)((nv + 63) / 64)), dim3(256), 0, st,
+                         (const float*)ws, ksplit, MN, d, accumulate);
+    else
+      hipLaunchKernelGGL(wgrad_splitk_finish<1>, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st,
+                         (const float*)ws, ksplit, MN, d, accumulate);
   }
   return (int)hipGetLastError();
 }

@@ -224,6 +224,12 @@ def conv3d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data
 
 def conv2d_transpose(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1,
                      dilation=1, data_format="NCHW", output_size=None, name=None):
+    if x.is_cuda:
+        from ...ops import conv as _conv
+        y = _conv.conv2d_transpose_any(x, weight, bias, stride, _padding(padding, 2), output_padding,
+                                       groups, dilation, data_format == "NHWC", output_size)
+        if y is not None:
+            return y
     return _fmt_out(TF.conv_transpose2d(_fmt_in(x, data_format), weight, bias, stride, _padding(padding, 2), output_padding, groups, dilation), data_format)
 
 

@@ -235,6 +235,7 @@ _SIGS["piamd_conv2d_fwd"] = [c_void_p] * 4 + [c_int] * 16 + [c_void_p, c_int, c_
 _SIGS["piamd_bn_fwd"] = ([c_int, c_int] + [c_void_p] * 3 + [c_int] * 3 + [c_void_p] * 6
                          + [c_float, c_float, c_int, c_int, c_void_p, c_void_p])
 # dtype, nhwc, dy, y, x, dx, dres, N, C, S, gamma, mean, rstd, dgamma, dbeta, training, act, ws, stream
+_SIGS["piamd_bn_set_parts"] = [c_ll, c_int]
 _SIGS["piamd_bn_bwd"] = ([c_int, c_int] + [c_void_p] * 5 + [c_int] * 3 + [c_void_p] * 5
                          + [c_int, c_int, c_void_p, c_void_p])
 # in, w, bias, out, N, H, W, Cin, OH, OW, Cout, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w,

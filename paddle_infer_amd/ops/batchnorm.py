@@ -17,6 +17,7 @@ import torch.nn.functional as TF
 from . import _lib
 
 _ACT = {"none": 0, None: 0, "identity": 0, "relu": 1, "relu6": 2}
+_MAX_PARTS = 2048  # statistics partial blocks (batchnorm.hip MAX_PARTS)
 
 
 def _layout(x, data_format):
@@ -75,7 +76,7 @@ class _BNAct(torch.autograd.Function):
         b = bias.float().contiguous() if bias is not None else None
         mean = torch.empty(C, device=dev, dtype=torch.float32)
         rstd = torch.empty(C, device=dev, dtype=torch.float32)
-        ws = torch.empty(2 * C + 3 * 512 * C, device=dev, dtype=torch.float32)
+        ws = torch.empty(2 * C + 3 * _MAX_PARTS * C, device=dev, dtype=torch.float32)
         y = torch.empty_like(xc)
         rm = running_mean if running_mean is not None and running_mean.dtype == torch.float32 else None
         rv = running_var if running_var is not None and running_var.dtype == torch.float32 else None
@@ -101,7 +102,7 @@ class _BNAct(torch.autograd.Function):
         dres = torch.empty_like(xc) if has_res else None
         dg = torch.empty(C, device=xc.device, dtype=torch.float32)
         db = torch.empty(C, device=xc.device, dtype=torch.float32)
-        ws = torch.empty(3 * C + 2 * 512 * C, device=xc.device, dtype=torch.float32)
+        ws = torch.empty(3 * C + 2 * _MAX_PARTS * C, device=xc.device, dtype=torch.float32)
         _lib.call("piamd_bn_bwd", int(xc.dtype == torch.bfloat16), int(nhwc), dyc.data_ptr(),
                   y.data_ptr(), xc.data_ptr(), dx.data_ptr(), _lib.ptr(dres), N, C, S, _lib.ptr(g),
                   mean.data_ptr(), rstd.data_ptr(), dg.data_ptr(), db.data_ptr(), int(training),

@@ -252,9 +252,8 @@ class _Conv2dNHWC(torch.autograd.Function):
         dt = x.dtype
         K0, C0, R, S = weight.shape
         K = -(-K0 // 4) * 4  # the epilogue stores 4 output channels per lane
-        wq = weight.to(dt)
-        if K != K0:
-            wq = torch.nn.functional.pad(wq, (0, 0, 0, 0, 0, 0, 0, K - K0))
+        wq0 = weight.to(dt)
+        wq = wq0 if K == K0 else torch.nn.functional.pad(wq0, (0, 0, 0, 0, 0, 0, 0, K - K0))
         b = None if bias is None else _padc(bias.to(dt), K)
         if C0 <= 8:  # stem mode: zero-pad the image channels to 8
             xc = _padc(x, 8).contiguous()
@@ -269,26 +268,27 @@ class _Conv2dNHWC(torch.autograd.Function):
             y = _launch(xc, w_ohwi, b, st, pad, dil, act)
         if K != K0:
             y = y[..., :K0].contiguous()
-        ctx.save_for_backward(xc, weight, y if act else None)
-        ctx.cfg = (st, pad, dil, act, bias is not None)
+        # the half-precision weight is kept for the backward (no second cast of the master weight)
+        ctx.save_for_backward(xc, wq0, y if act else None)
+        ctx.cfg = (st, pad, dil, act, bias is not None, weight.dtype)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight, y = ctx.saved_tensors
-        st, pad, dil, act, has_bias = ctx.cfg
+        x, wq, y = ctx.saved_tensors
+        st, pad, dil, act, has_bias, wdt = ctx.cfg
         dt = x.dtype
         dy = dy.to(dt)
         if act == 3:
             dy = dy * (y > 0)
         dy = dy.contiguous()
-        K0, C0, R, S = weight.shape
+        K0, C0, R, S = wq.shape
         C = x.shape[-1]  # == C0, or C0 zero-padded (to 8 in stem mode, else to a multiple of 64)
         N, H, W, _ = x.shape
         M = dy.shape[0] * dy.shape[1] * dy.shape[2]
         Kp = _pad64(K0)  # dY channels padded: the dgrad reduction / wgrad tile runs over 64s
-        wq = weight.to(dt)
-        wq = torch.nn.functional.pad(wq, (0, 0, 0, 0, 0, C - C0, 0, Kp - K0))
+        if C != C0 or Kp != K0:
+            wq = torch.nn.functional.pad(wq, (0, 0, 0, 0, 0, C - C0, 0, Kp - K0))
         dyp = _padc(dy, Kp)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
@@ -305,9 +305,9 @@ class _Conv2dNHWC(torch.autograd.Function):
                 dw = conv2d_wgrad(x, dyp, R, S, st, pad, dil)[:K0, :C0]
             else:  # > 2^24 output pixels: the direct kernel's pixel-chunked reduction
                 dw = _direct_wgrad(x[..., :C0].contiguous(), dy, R, S, st, pad, dil, C0, K0)
-            dw = dw.to(weight.dtype)
+            dw = dw.to(wdt)
         if has_bias and ctx.needs_input_grad[2]:
-            db = dy.float().sum((0, 1, 2)).to(weight.dtype)
+            db = dy.float().sum((0, 1, 2)).to(wdt)
         return dx, dw, db, None, None, None, None
 
 
@@ -462,6 +462,101 @@ def conv2d_any(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, 
             y = _Conv1x1.apply(xh, weight, bias, st)
         else:
             y = _Conv2dNHWC.apply(xh, weight, bias, st, pad, dil, 0)
+    return y if nhwc else y.permute(0, 3, 1, 2)
+
+
+class _ConvTranspose(torch.autograd.Function):
+    """Transposed conv, x [N,H,W,Cin], weight [Cin, Cout/groups, R, S]: the forward is the data
+    gradient of the conv it transposes (dense half → the MFMA phase decomposition, else the direct
+    kernel's transposed geometry); its data gradient is that conv's forward and its weight gradient
+    that conv's weight gradient with the roles of input and output swapped."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, st, pad, out_pad, dil, groups):
+        dt = x.dtype
+        N, H, W, Cin = x.shape
+        _, og, R, S = weight.shape
+        Cout = og * groups
+        Ho = (H - 1) * st[0] - 2 * pad[0] + dil[0] * (R - 1) + out_pad[0] + 1
+        Wo = (W - 1) * st[1] - 2 * pad[1] + dil[1] * (S - 1) + out_pad[1] + 1
+        if groups == 1 and dt in _HALF:
+            Kp, Cp = _pad64(Cin), -(-Cout // 4) * 4
+            wq = torch.nn.functional.pad(weight.to(dt), (0, 0, 0, 0, 0, Cp - Cout, 0, Kp - Cin))
+            y = conv2d_dgrad_strided(_padc(x, Kp).contiguous(), wq, Ho, Wo, st, pad, dil)
+            y = y[..., :Cout]
+            if bias is not None:
+                y = y + bias.to(dt)
+            y = y.contiguous()
+        else:
+            w_t = (weight.to(dt).view(groups, Cin // groups, og, R, S).permute(3, 4, 1, 0, 2)
+                   .reshape(R, S, Cin // groups, Cout).contiguous())
+            b = bias.to(dt).contiguous() if bias is not None else None
+            y = _direct(x, w_t, b, Ho, Wo, Cout, R, S, st, pad, dil, Cin // groups, og, True)
+        ctx.save_for_backward(x, weight)
+        ctx.cfg = (st, pad, dil, groups, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        st, pad, dil, groups, has_bias = ctx.cfg
+        dt = x.dtype
+        dy = dy.to(dt).contiguous()
+        N, H, W, Cin = x.shape
+        _, og, R, S = weight.shape
+        Cout = og * groups
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            if groups == 1 and dt in _HALF:
+                dx = _Conv2dNHWC.apply(dy, weight, None, st, pad, dil, 0)
+            else:
+                dx = _ConvDirect.apply(dy, weight, None, st, pad, dil, groups)
+            dx = dx[:, :H, :W]
+        if ctx.needs_input_grad[1]:
+            if groups == 1 and dt in _HALF and wgrad_eligible(8, 64, N * H * W):
+                Cp, Kp = -(-Cout // 8) * 8, _pad64(Cin)
+                dw = conv2d_wgrad(_padc(dy, Cp).contiguous(), _padc(x, Kp).contiguous(), R, S, st,
+                                  pad, dil)[:Cin, :Cout]
+            else:
+                dw = _direct_wgrad(dy, x, R, S, st, pad, dil, Cout, Cin, groups)
+            dw = dw.to(weight.dtype)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = dy.float().sum((0, 1, 2)).to(weight.dtype)
+        return dx, dw, db, None, None, None, None, None
+
+
+def conv2d_transpose_any(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1,
+                         dilation=1, nhwc=False, output_size=None):
+    """Own-kernel route for ``conv2d_transpose`` of a GPU tensor; ``None`` → library (dense fp32
+    without autocast, string padding)."""
+    if not (HIP_CONV and x.is_cuda and x.dim() == 4 and weight.dim() == 4) or isinstance(padding, str):
+        return None
+    pad, st, dil, op = _pair(padding), _pair(stride), _pair(dilation), _pair(output_padding)
+    if len(pad) != 2:
+        return None
+    dt = x.dtype
+    if torch.is_autocast_enabled("cuda") and dt in _DT:
+        dt = torch.get_autocast_dtype("cuda")
+    if dt not in _DT:
+        return None
+    Cin = x.shape[-1] if nhwc else x.shape[1]
+    if weight.shape[0] != Cin or Cin % groups:
+        raise ValueError(f"conv2d_transpose: weight {tuple(weight.shape)} does not match {Cin} "
+                         f"input channels in {groups} groups")
+    H, W = (x.shape[1:3] if nhwc else x.shape[2:4])
+    R, S = weight.shape[2:]
+    if output_size is not None:
+        osz = list(output_size)[-2:]
+        op = tuple(osz[i] - ((H, W)[i] - 1) * st[i] + 2 * pad[i] - dil[i] * ((R, S)[i] - 1) - 1
+                   for i in range(2))
+        if any(o < 0 or o >= max(st[i], dil[i]) for i, o in enumerate(op)):
+            raise ValueError(f"conv2d_transpose: output_size {output_size} is not reachable")
+    if groups == 1 and dt == torch.float32:
+        _lib.fallback("conv2d_transpose", "dense fp32 transposed conv without autocast (library)")
+        return None
+    with torch.autocast("cuda", enabled=False):
+        xh = (x if nhwc else x.permute(0, 2, 3, 1)).to(dt).contiguous()
+        y = _ConvTranspose.apply(xh, weight, bias, st, pad, op, dil, groups)
     return y if nhwc else y.permute(0, 3, 1, 2)
 
 

@@ -144,3 +144,34 @@ def test_mobilenet_v2_step_without_library_conv():
     losses = [step() for _ in range(6)]
     assert all(torch.isfinite(torch.tensor(losses)))
     assert losses[-1] < first
+
+
+@pytest.mark.parametrize("dt,Cin,Cout,R,st,pad,op,groups", [
+    (torch.bfloat16, 64, 32, 4, 2, 1, 0, 1),    # DCGAN-style upsampling, MFMA phases
+    (torch.float16, 40, 24, 3, 2, 1, 1, 1),     # unaligned channels + output_padding
+    (torch.bfloat16, 32, 32, 3, 1, 1, 0, 1),    # stride 1
+    (torch.float32, 32, 64, 3, 2, 1, 1, 4),     # grouped, direct kernel
+    (torch.bfloat16, 48, 48, 4, 2, 1, 0, 48),   # depthwise transposed
+])
+def test_conv2d_transpose(dt, Cin, Cout, R, st, pad, op, groups):
+    g = torch.Generator(device="cuda").manual_seed(Cin + Cout)
+    x = torch.randn(2, Cin, 9, 7, device="cuda", generator=g)
+    w = torch.randn(Cin, Cout // groups, R, R, device="cuda", generator=g) / (Cin * R) ** 0.5
+    b = torch.randn(Cout, device="cuda", generator=g)
+    xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w, b))
+    yr = torch.nn.functional.conv_transpose2d(xr, wr, br, st, pad, op, groups)
+    dy = torch.randn(yr.shape, device="cuda", generator=g)
+    yr.backward(dy)
+    xi = x.to(dt).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    wi, bi = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    y = F.conv2d_transpose(xi, wi, bi, st, pad, op, groups)
+    assert y.dtype == dt and y.shape == yr.shape
+    y.backward(dy.to(dt))
+    tol = TOL[dt]
+    assert _rel(y, yr) < tol, _rel(y, yr)
+    assert _rel(xi.grad, xr.grad) < tol, _rel(xi.grad, xr.grad)
+    assert _rel(wi.grad, wr.grad) < tol * (2 if dt != torch.float32 else 5), _rel(wi.grad, wr.grad)
+    assert _rel(bi.grad, br.grad) < tol
+    # output_size picks the output padding
+    y2 = F.conv2d_transpose(xi.detach(), w, b, st, pad, 0, groups, output_size=list(yr.shape[2:]))
+    assert y2.shape == yr.shape

@@ -20,7 +20,7 @@ import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 import paddle_infer_amd as paddle  # noqa: E402
 from paddle_infer_amd.ops import conv as CV  # noqa: E402
-from paddle_infer_amd.vision.models import resnet50  # noqa: E402
+from paddle_infer_amd.vision import models as VM  # noqa: E402
 
 
 def _setup():
@@ -32,10 +32,10 @@ def _setup():
     return world
 
 
-def build(batch, hip_conv, lr, res=224, seed=0):
+def build(batch, hip_conv, lr, res=224, seed=0, model="resnet50"):
     CV.HIP_CONV = hip_conv
     torch.manual_seed(seed)
-    m = resnet50(num_classes=1000).cuda().to(memory_format=torch.channels_last)
+    m = getattr(VM, model)(num_classes=1000).cuda().to(memory_format=torch.channels_last)
     model = paddle.DataParallel(m)
     opt = paddle.optimizer.Momentum(learning_rate=lr, momentum=0.9, parameters=m.parameters(),
                                     weight_decay=1e-4)
@@ -45,7 +45,7 @@ def build(batch, hip_conv, lr, res=224, seed=0):
     y = torch.randint(0, 1000, (batch,), device="cuda", generator=g)
 
     def step():
-        with torch.autocast("cuda", dtype=torch.bfloat16):
+        with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
             loss = torch.nn.functional.cross_entropy(model(x), y)
         loss.backward()
         opt.step()
@@ -54,10 +54,33 @@ def build(batch, hip_conv, lr, res=224, seed=0):
     return step
 
 
-def run(batch, steps, hip_conv, world, lr=0.02):
+def graphed(step, warmup=3):
+    """The whole training step (forward, backward, optimizer update, gradient zeroing) captured
+    once into a hipGraph and replayed: the ~1k kernel launches of a step leave the host. The
+    warm-up runs eagerly on a side stream first (autotuned conv plans, optimizer state and the
+    gradient buffers exist before capture; the graph reuses those static tensors)."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(warmup):
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        loss = step()
+
+    def replay():
+        g.replay()
+        return loss
+    return replay
+
+
+def run(batch, steps, hip_conv, world, lr=0.02, model="resnet50", graph=False):
     # lr 0.02 (momentum 0.9, no warm-up): the timed steps keep training on the fixed synthetic
     # batch (loss falls below ln 1000); lr 0.1 without warm-up diverged there (loss 11.7, r2)
-    step = build(batch, hip_conv, lr=lr)
+    step = build(batch, hip_conv, lr=lr, model=model)
+    if graph:
+        step = graphed(step)
     for _ in range(3):
         step()
     torch.cuda.synchronize()
@@ -72,7 +95,7 @@ def run(batch, steps, hip_conv, world, lr=0.02):
         t = torch.tensor([dt], device="cuda")
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = t.item()
-    return {"hip_conv": hip_conv, "batch_per_gpu": batch, "n_gpus": world,
+    return {"model": model, "hip_conv": hip_conv, "hipgraph": graph, "batch_per_gpu": batch, "n_gpus": world,
             "ms_per_step": round(dt * 1e3, 2), "images_per_s": round(batch * world / dt, 1),
             "loss": round(loss.item(), 3), "lr": lr, "optimizer": "paddle.optimizer.Momentum (merged)",
             "wrapper": "paddle.DataParallel"}
@@ -94,12 +117,14 @@ if __name__ == "__main__":
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--mode", choices=["both", "hip", "lib"], default="hip")
     ap.add_argument("--parity", type=int, default=0)
+    ap.add_argument("--model", default="resnet50", help="any paddle.vision.models constructor")
+    ap.add_argument("--graph", action="store_true", help="replay the step as one captured hipGraph")
     a = ap.parse_args()
     world = _setup()
     if a.parity:
         print(json.dumps(parity(a.parity)), flush=True)
     else:
         for hc in {"both": (False, True), "hip": (True,), "lib": (False,)}[a.mode]:
-            r = run(a.batch, a.steps, hc, world)
+            r = run(a.batch, a.steps, hc, world, model=a.model, graph=a.graph)
             if int(os.environ.get("RANK", "0")) == 0:
                 print(json.dumps(r), flush=True)

@@ -14,8 +14,9 @@
 // "Attention backward"):
 //   * Layout [B, S, H, D] with free b/s/h strides, so Q/K/V are consumed straight out of the fused
 //     QKV projection output and dQ/dK/dV are written straight into the fused dQKV gradient.
-//   * Head dims: D in {64, 96, 128}. LDS rows are DP = 64 / 128 elements (power of two, so the XOR
-//     swizzle stays closed); D = 96 uses 128-element rows whose last 4 chunks are never read.
+//   * Head dims: D in {64, 96, 128} (forward and backward) and 256 (forward). LDS rows are DP = 64 /
+//     128 / 256 elements (power of two, so the XOR swizzle stays closed); D = 96 uses 128-element
+//     rows whose last 4 chunks are never read.
 //   * Forward: workgroup = 4 waves = 128 query rows (32 per wave), K/V tiles of 64 keys DMA'd
 //     straight into LDS (global_load_lds_dwordx4), double buffered. SWAPPED products with
 //     v_mfma_f32_32x32x16_{bf16,f16}: Sᵀ = K·Qᵀ puts one query row per lane, so the online-softmax
@@ -284,11 +285,13 @@ __device__ __forceinline__ s16x4_t lds_tr_at(const char* smem, int off) {
 // ------------------------------------------------------------------------------------------
 // NW waves per workgroup, 32 query rows each (BM = 32·NW); NW = 8 shares every K/V tile fill
 // between twice the rows (half the LDS fill traffic per FLOP) at one workgroup per CU.
+// D = 256 (wide heads): 512-byte LDS rows (K+V double buffer 128 KiB) and one workgroup per CU —
+// the 16 Q fragments + 8 O accumulators need the whole 512-register file of one wave per SIMD.
 template <int D, bool F16, bool CAUSAL, int FEAT, int NW = 4>
-__global__ __launch_bounds__(64 * NW, 8 / NW) void fwd_kernel(FaArgs a) {
+__global__ __launch_bounds__(64 * NW, D > 128 ? 1 : 8 / NW) void fwd_kernel(FaArgs a) {
   typedef ET<F16> E;
   typedef typename E::V8 V8;
-  constexpr int DP = D > 64 ? 128 : 64;
+  constexpr int DP = D > 128 ? 256 : D > 64 ? 128 : 64;
   constexpr int BM = 32 * NW, BN = 64;
   constexpr int KSTEPS = D / 16;
   constexpr int DT = D / 32;
@@ -977,7 +980,8 @@ int launch_fwd_nw(const FaArgs& a, hipStream_t st) {
 
 template <bool F16, int D, bool C>
 int launch_fwd_feat(const FaArgs& a, dim3 /*grid*/, hipStream_t st) {
-  return fwd_waves() == 8 ? launch_fwd_nw<F16, D, C, 8>(a, st) : launch_fwd_nw<F16, D, C, 4>(a, st);
+  if constexpr (D > 128) return launch_fwd_nw<F16, D, C, 4>(a, st);
+  else return fwd_waves() == 8 ? launch_fwd_nw<F16, D, C, 8>(a, st) : launch_fwd_nw<F16, D, C, 4>(a, st);
 }
 
 template <bool F16>
@@ -989,6 +993,7 @@ int launch_fwd(const FaArgs& a, hipStream_t st) {
     case 64: FWD_D(64);
     case 96: FWD_D(96);
     case 128: FWD_D(128);
+    case 256: FWD_D(256);
     default: return (int)hipErrorInvalidValue;
   }
 #undef FWD_D

@@ -20,15 +20,17 @@ from . import _lib
 from ..framework import random as _random
 
 
-NATIVE_D = (64, 96, 128)
+NATIVE_D = (64, 96, 128)  # forward + backward kernels
+WIDE_D = 256  # forward kernel; the backward runs query-chunked on library GEMMs (_bwd_chunked)
 
 
-def _padded_d(D: int) -> int | None:
+def _padded_d(D: int, wide: bool = False) -> int | None:
     """Kernel head dim for a model head dim: native, or the next native size (zero-padded
-    channels change neither Q·Kᵀ nor the real output columns). None if unsupported."""
+    channels change neither Q·Kᵀ nor the real output columns). None if unsupported. ``wide``:
+    head dims up to 256 run on the wide forward kernel."""
     if D % 8:
         return None
-    for n in NATIVE_D:
+    for n in NATIVE_D + ((WIDE_D,) if wide else ()):
         if D <= n:
             return n
     return None
@@ -136,6 +138,44 @@ class _FlashAttnPackedFn(torch.autograd.Function):
         return dqkv, None, None, None, None, None, None, None
 
 
+def _bwd_chunked(q, k, v, o, lse, do, causal, scale, mask, chunk_bytes=1 << 30):
+    """Attention backward for head dims without a backward kernel (D = 256), from the forward's
+    O and log-sum-exp: per query chunk P = exp(S − lse), dV += Pᵀ·dO, dS = P∘(dO·Vᵀ − δ),
+    dQ = dS·K·scale, dK += dSᵀ·Q·scale (f32; memory O(chunk · Sk), not O(Sq · Sk))."""
+    B, Sq, Hq, D = q.shape
+    Sk, Hk = k.shape[1], k.shape[2]
+    rep = Hq // Hk
+    ct = torch.promote_types(q.dtype, torch.float32)
+    qf, of, dof = (t.to(ct).transpose(1, 2) for t in (q, o, do))
+    kf = k.to(ct).transpose(1, 2).repeat_interleave(rep, dim=1)
+    vf = v.to(ct).transpose(1, 2).repeat_interleave(rep, dim=1)
+    lse = lse.to(ct)
+    delta = (dof * of).sum(-1, keepdim=True)
+    dq = torch.empty_like(qf)
+    dk = torch.zeros_like(kf)
+    dv = torch.zeros_like(vf)
+    ch = max(1, min(Sq, chunk_bytes // max(1, B * Hq * Sk * 4 * 3)))
+    for q0 in range(0, Sq, ch):
+        q1 = min(Sq, q0 + ch)
+        s = torch.matmul(qf[:, :, q0:q1], kf.transpose(-1, -2)) * scale
+        if mask is not None:
+            s = s + (mask[..., :, :Sk] if mask.shape[-2] == 1 else mask[..., q0:q1, :Sk]).to(ct)
+        if causal:
+            i = torch.arange(q0, q1, device=q.device)[:, None]
+            j = torch.arange(Sk, device=q.device)[None, :]
+            s = s.masked_fill(j > i + (Sk - Sq), float("-inf"))
+        pm = torch.exp(s - lse[:, :, q0:q1, None])
+        dv += torch.matmul(pm.transpose(-1, -2), dof[:, :, q0:q1])
+        ds = pm * (torch.matmul(dof[:, :, q0:q1], vf.transpose(-1, -2)) - delta[:, :, q0:q1])
+        dq[:, :, q0:q1] = torch.matmul(ds, kf) * scale
+        dk += torch.matmul(ds.transpose(-1, -2), qf[:, :, q0:q1]) * scale
+    if rep > 1:
+        dk = dk.view(B, Hk, rep, Sk, D).sum(2)
+        dv = dv.view(B, Hk, rep, Sk, D).sum(2)
+    back = lambda t, ref: t.transpose(1, 2).to(ref.dtype)
+    return back(dq, q), back(dk, k), back(dv, v)
+
+
 class _FlashAttnFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, causal, scale, mask, p, seed, off):
@@ -149,6 +189,10 @@ class _FlashAttnFn(torch.autograd.Function):
     def backward(ctx, do):
         q, k, v, o, lse, mask = ctx.saved_tensors
         causal, scale, p, seed, off = ctx.meta
+        if q.shape[-1] > NATIVE_D[-1]:
+            _lib.fallback("flash_attention_bwd", f"head dim {q.shape[-1]}: query-chunked library GEMMs")
+            dq, dk, dv = _bwd_chunked(q, k, v, o, lse, do, causal, scale, mask)
+            return dq, dk, dv, None, None, None, None, None, None
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         _bwd(q, k, v, o, lse, do, dq, dk, dv, causal, scale, mask, p, seed, off)
         return dq, dk, dv, None, None, None, None, None, None
@@ -184,15 +228,15 @@ def attention_reference(q, k, v, causal=False, scale=None, attn_mask=None, dropo
     return o.to(q.dtype)
 
 
-def _kernel_ok(op, q, k, v) -> bool:
+def _kernel_ok(op, q, k, v, wide=False) -> bool:
     """True: the MFMA kernel takes it. GPU inputs it cannot take are recorded (warn once)."""
     if not (q.is_cuda and k.is_cuda and v.is_cuda):
         return False
     if q.dtype not in (torch.bfloat16, torch.float16) or k.dtype != q.dtype or v.dtype != q.dtype:
         _lib.fallback(op, f"dtype {q.dtype} (kernel: bf16/fp16)")
         return False
-    if _padded_d(q.shape[-1]) is None:
-        _lib.fallback(op, f"head dim {q.shape[-1]} (kernel: multiple of 8, <= 128)")
+    if _padded_d(q.shape[-1], wide) is None:
+        _lib.fallback(op, f"head dim {q.shape[-1]} (kernel: multiple of 8, <= {WIDE_D if wide else 128})")
         return False
     if q.shape[-2] % k.shape[-2]:
         _lib.fallback(op, "q heads not a multiple of kv heads")
@@ -215,12 +259,15 @@ def flash_attention(q, k, v, causal: bool = False, scale: float | None = None, a
     dropout, regenerated in backward from the counter RNG (nothing stored)."""
     D = q.shape[-1]
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
-    if _kernel_ok("flash_attention", q, k, v):
+    # wide heads (129..256): native forward; without dropout (the chunked backward cannot replay
+    # the kernel's dropout mask)
+    wide = D > NATIVE_D[-1] and (dropout_p == 0.0 or not training)
+    if _kernel_ok("flash_attention", q, k, v, wide):
         B, Sq, Hq, _ = q.shape
         Sk = k.shape[1]
         mask = _prep_mask(attn_mask, B, Hq, Sq, Sk, q.dtype)
         p, seed, off = _drop_state(dropout_p, training, B, Hq, Sq, Sk)
-        Dp = _padded_d(D)
+        Dp = _padded_d(D, wide)
         if Dp != D:  # zero channels: Q·Kᵀ unchanged, extra output columns are zero (sliced off)
             pad = (0, Dp - D)
             o = _FlashAttnFn.apply(F.pad(q, pad), F.pad(k, pad), F.pad(v, pad), causal, scale, mask,

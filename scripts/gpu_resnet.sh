@@ -3,7 +3,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest -x -q --timeout 150 --timeout-method thread tests/test_conv_any_gpu.py tests/test_conv_bwd_gpu.py tests/test_conv_gpu.py tests/test_norm_gpu.py > gpurun_out/rn_tests.log 2>&1 || { tail -40 gpurun_out/rn_tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -q --timeout 150 --timeout-method thread tests/test_attention_gpu.py tests/test_conv_any_gpu.py tests/test_conv_bwd_gpu.py tests/test_conv_gpu.py tests/test_norm_gpu.py > gpurun_out/rn_tests.log 2>&1 || { tail -40 gpurun_out/rn_tests.log; exit 1; }
 tail -1 gpurun_out/rn_tests.log
 timeout -k 10 300 python tools/bench_resnet.py --steps 10 > gpurun_out/resnet_e.log 2>&1 || { tail -20 gpurun_out/resnet_e.log; exit 1; }
 grep "^{" gpurun_out/resnet_e.log

@@ -168,3 +168,23 @@ def test_varlen_masked_single_launch_matches_reference():
                      mask[b:b + 1, :, :n, :n]).transpose(1, 2)
             _close(o[b:b + 1, :, :n], r, 2e-2)
             assert n == S or o[b, :, n:].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("D,causal,masked", [(256, True, False), (256, False, True), (192, True, False)])
+def test_flash_wide_head_dims(dtype, D, causal, masked):
+    """Head dims 129..256: the wide forward kernel (D = 256, narrower heads zero-padded) and the
+    query-chunked backward from its log-sum-exp."""
+    from paddle_infer_amd.ops import _lib, flash_attention
+    torch.manual_seed(1)
+    B, Sq, Sk, Hq, Hk = 2, 150, 150, 4, 2
+    q = torch.randn(B, Sq, Hq, D, device=DEV, dtype=dtype)
+    k = torch.randn(B, Sk, Hk, D, device=DEV, dtype=dtype)
+    v = torch.randn(B, Sk, Hk, D, device=DEV, dtype=dtype)
+    mask = torch.randn(B, 1, Sq, Sk, device=DEV, dtype=dtype) if masked else None
+    sc = 1 / math.sqrt(D)
+    o, do, *g = _run(q, k, v, lambda a, b, c: flash_attention(a, b, c, causal, sc, attn_mask=mask),
+                     dtype, D)
+    _check(o, do, g, q, k, v, lambda a, b, c: _ref(a, b, c, causal, sc, mask), dtype)
+    assert {op for op, _ in _lib.FALLBACKS} <= {"flash_attention_bwd"}, _lib.FALLBACKS  # fwd on the kernel
+    _lib.FALLBACKS.clear()

@@ -100,6 +100,10 @@ __device__ __forceinline__ float unary_f(int op, float x, float p0, float p1) {
     case U_ABS: return fabsf(x);
     case U_SCALE: return x * p0 + p1;
     case U_SCALE_PRE: return (x + p1) * p0;
+    case U_RELU6: return fminf(fmaxf(x, 0.f), p0);
+    case U_HSWISH: return x * fminf(fmaxf(x + p1, 0.f), p0) / p0;
+    case U_HSIGMOID: return fminf(fmaxf(x * p0 + p1, 0.f), 1.f);
+    case U_LEAKY: return x > 0.f ? x : p0 * x;
   }
   return x;
 }
@@ -263,6 +267,77 @@ __global__ __launch_bounds__(256) void reduce_k(const float* __restrict__ x, flo
   if (threadIdx.x == 0) y[row] = mean ? s / n : s;
 }
 
+// one thread per col element: (n, q = (c, r, s), pixel)
+__global__ void im2col_k(const float* __restrict__ x, int64_t x_img, float* __restrict__ col,
+                         int64_t total, ConvG g) {
+  const int64_t P = g.OH * g.OW, rows = g.C * g.R * g.S;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t pix = i % P, q = (i / P) % rows, n = i / (P * rows);
+    const int64_t c = q / (g.R * g.S), r = (q / g.S) % g.R, s = q % g.S;
+    const int64_t ih = (pix / g.OW) * g.sh - g.ph + r * g.dh, iw = (pix % g.OW) * g.sw - g.pw + s * g.dw;
+    col[i] = (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) ? x[n * x_img + (c * g.H + ih) * g.W + iw] : 0.f;
+  }
+}
+
+// one thread per output element of the depthwise conv (NCHW)
+__global__ void dwconv_k(const float* __restrict__ x, const float* __restrict__ w,
+                         const float* __restrict__ bias, float* __restrict__ y, int64_t total,
+                         int64_t mult, ConvG g) {
+  const int64_t K = g.C * mult, P = g.OH * g.OW;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t pix = i % P, k = (i / P) % K, n = i / (P * K);
+    const int64_t oh = pix / g.OW, ow = pix % g.OW;
+    const float* xp = x + (n * g.C + k / mult) * g.H * g.W;
+    const float* wp = w + k * g.R * g.S;
+    float acc = bias ? bias[k] : 0.f;
+    for (int64_t r = 0; r < g.R; ++r) {
+      const int64_t ih = oh * g.sh - g.ph + r * g.dh;
+      if (ih < 0 || ih >= g.H) continue;
+      for (int64_t s = 0; s < g.S; ++s) {
+        const int64_t iw = ow * g.sw - g.pw + s * g.dw;
+        if (iw >= 0 && iw < g.W) acc += xp[ih * g.W + iw] * wp[r * g.S + s];
+      }
+    }
+    y[i] = acc;
+  }
+}
+
+__global__ void pool2d_k(const float* __restrict__ x, float* __restrict__ y, int64_t total, PoolG p) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t ow = i % p.OW, oh = (i / p.OW) % p.OH, pl = i / (p.OW * p.OH);
+    const float* xp = x + pl * p.H * p.W;
+    int64_t h0, h1, w0, w1;
+    if (p.adaptive) {
+      h0 = oh * p.H / p.OH; h1 = ((oh + 1) * p.H + p.OH - 1) / p.OH;
+      w0 = ow * p.W / p.OW; w1 = ((ow + 1) * p.W + p.OW - 1) / p.OW;
+    } else {
+      h0 = oh * p.sh - p.ph; h1 = h0 + p.kh;
+      w0 = ow * p.sw - p.pw; w1 = w0 + p.kw;
+    }
+    const int64_t area = (h1 - h0) * (w1 - w0);
+    h0 = h0 > 0 ? h0 : 0; h1 = h1 < p.H ? h1 : p.H;
+    w0 = w0 > 0 ? w0 : 0; w1 = w1 < p.W ? w1 : p.W;
+    float acc = p.max ? -INFINITY : 0.f;
+    for (int64_t ih = h0; ih < h1; ++ih)
+      for (int64_t iw = w0; iw < w1; ++iw)
+        acc = p.max ? fmaxf(acc, xp[ih * p.W + iw]) : acc + xp[ih * p.W + iw];
+    if (!p.max) {
+      const int64_t cnt = (p.exclusive || p.adaptive) ? (h1 - h0) * (w1 - w0) : area;
+      acc /= (float)(cnt > 0 ? cnt : 1);
+    }
+    y[i] = acc;
+  }
+}
+
+__global__ void channel_affine_k(const float* __restrict__ x, const float* __restrict__ sc,
+                                 const float* __restrict__ sh, float* __restrict__ y, int64_t n,
+                                 int64_t C, int64_t inner, int act, float p0) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t ch = (i / inner) % C;
+    y[i] = unary_f(act, x[i] * sc[ch] + sh[ch], p0, 0.f);
+  }
+}
+
 }  // namespace
 
 void unary(Ctx& c, int op, const float* x, float* y, int64_t n, float p0, float p1) {
@@ -319,6 +394,25 @@ void copy2d(Ctx& c, const void* src, int64_t spitch, void* dst, int64_t dpitch, 
   if (rows * cols)
     HIPCHK(hipMemcpy2DAsync(dst, (size_t)(dpitch * elem), src, (size_t)(spitch * elem), (size_t)(cols * elem),
                             (size_t)rows, hipMemcpyDeviceToDevice, S(c)));
+}
+
+void im2col(Ctx& c, const float* x, int64_t x_img, float* col, int64_t N, const ConvG& g) {
+  const int64_t total = N * g.C * g.R * g.S * g.OH * g.OW;
+  if (total) hipLaunchKernelGGL(im2col_k, dim3(blocks(total)), dim3(256), 0, S(c), x, x_img, col, total, g);
+}
+void dwconv(Ctx& c, const float* x, const float* w, const float* bias, float* y, int64_t N,
+            int64_t mult, const ConvG& g) {
+  const int64_t total = N * g.C * mult * g.OH * g.OW;
+  if (total) hipLaunchKernelGGL(dwconv_k, dim3(blocks(total)), dim3(256), 0, S(c), x, w, bias, y, total, mult, g);
+}
+void pool2d(Ctx& c, const float* x, float* y, int64_t planes, const PoolG& p) {
+  const int64_t total = planes * p.OH * p.OW;
+  if (total) hipLaunchKernelGGL(pool2d_k, dim3(blocks(total)), dim3(256), 0, S(c), x, y, total, p);
+}
+void channel_affine(Ctx& c, const float* x, const float* sc, const float* sh, float* y, int64_t outer,
+                    int64_t C, int64_t inner, int act, float p0) {
+  const int64_t n = outer * C * inner;
+  if (n) hipLaunchKernelGGL(channel_affine_k, dim3(blocks(n)), dim3(256), 0, S(c), x, sc, sh, y, n, C, inner, act, p0);
 }
 
 }  // namespace gpu

@@ -7,7 +7,11 @@
 namespace pdn {
 
 enum UnaryOp { U_IDENT, U_RELU, U_GELU, U_GELU_TANH, U_TANH, U_SIGMOID, U_SILU, U_EXP, U_SQRT,
-               U_RSQRT, U_ABS, U_SCALE, U_SCALE_PRE };
+               U_RSQRT, U_ABS, U_SCALE, U_SCALE_PRE,
+               U_RELU6,      // min(max(x, 0), p0)  (p0 = threshold, 6)
+               U_HSWISH,     // x · min(max(x + p1, 0), p0) / p0  (p0 = threshold 6, p1 = offset 3)
+               U_HSIGMOID,   // min(max(x · p0 + p1, 0), 1)  (p0 = slope, p1 = offset)
+               U_LEAKY };    // x > 0 ? x : p0 · x
 enum BinaryOp { B_ADD, B_SUB, B_MUL, B_DIV, B_MAX, B_MIN, B_POW };
 
 constexpr int kMaxDims = 8;
@@ -17,6 +21,14 @@ struct Bcast {  // out[i] = a[i·sa] op b[i·sb] over an n-d index space (stride
   int64_t sa[kMaxDims] = {0};
   int64_t sb[kMaxDims] = {0};
   int64_t n = 0;
+};
+// NCHW convolution / pooling geometry (one group's channels C; top/left padding; outputs OH × OW)
+struct ConvG {
+  int64_t C, H, W, R, S, OH, OW, sh, sw, ph, pw, dh, dw;
+};
+struct PoolG {
+  int64_t H, W, OH, OW, kh, kw, sh, sw, ph, pw;
+  int max, exclusive, adaptive;
 };
 struct Strided {  // out (contiguous, dims) = src[offset + Σ idx·stride] (elements)
   int nd = 0;
@@ -44,6 +56,15 @@ struct Strided {  // out (contiguous, dims) = src[offset + Σ idx·stride] (elem
   void reduce(Ctx&, const float* x, float* y, int64_t outer, int64_t n, int64_t inner, bool mean); \
   void copy2d(Ctx&, const void* src, int64_t spitch, void* dst, int64_t dpitch, int64_t rows,      \
               int64_t cols, int elem);                                                             \
+  /* col [N][C·R·S][OH·OW] of images x + n·x_img (first channel of the group at x) */              \
+  void im2col(Ctx&, const float* x, int64_t x_img, float* col, int64_t N, const ConvG& g);         \
+  /* depthwise: y [N][C·m][OH][OW] = conv(x [N][C][H][W], w [C·m][1][R][S]) (+ bias [C·m]) */      \
+  void dwconv(Ctx&, const float* x, const float* w, const float* bias, float* y, int64_t N,        \
+              int64_t mult, const ConvG& g);                                                       \
+  void pool2d(Ctx&, const float* x, float* y, int64_t planes, const PoolG& p);                     \
+  /* y[o][c][i] = act(x[o][c][i] · sc[c] + sh[c]) (act: UnaryOp, U_IDENT = none) */                 \
+  void channel_affine(Ctx&, const float* x, const float* sc, const float* sh, float* y,            \
+                      int64_t outer, int64_t C, int64_t inner, int act, float p0);                 \
   }
 
 PDN_KERNELS(cpu)
@@ -67,6 +88,10 @@ PDN_DISPATCH(cast)
 PDN_DISPATCH(fill)
 PDN_DISPATCH(reduce)
 PDN_DISPATCH(copy2d)
+PDN_DISPATCH(im2col)
+PDN_DISPATCH(dwconv)
+PDN_DISPATCH(pool2d)
+PDN_DISPATCH(channel_affine)
 #undef PDN_DISPATCH
 }  // namespace kern
 

@@ -26,6 +26,10 @@ inline float unary_f(int op, float x, float p0, float p1) {
     case U_ABS: return std::fabs(x);
     case U_SCALE: return x * p0 + p1;
     case U_SCALE_PRE: return (x + p1) * p0;
+    case U_RELU6: return std::min(std::max(x, 0.f), p0);
+    case U_HSWISH: return x * std::min(std::max(x + p1, 0.f), p0) / p0;
+    case U_HSIGMOID: return std::min(std::max(x * p0 + p1, 0.f), 1.f);
+    case U_LEAKY: return x > 0.f ? x : p0 * x;
   }
   return x;
 }
@@ -226,6 +230,88 @@ void copy2d(Ctx&, const void* src, int64_t spitch, void* dst, int64_t dpitch, in
             int64_t cols, int elem) {
   for (int64_t r = 0; r < rows; ++r)
     std::memcpy((char*)dst + r * dpitch * elem, (const char*)src + r * spitch * elem, (size_t)(cols * elem));
+}
+
+
+void im2col(Ctx&, const float* x, int64_t x_img, float* col, int64_t N, const ConvG& g) {
+  const int64_t P = g.OH * g.OW, rows = g.C * g.R * g.S;
+  for (int64_t n = 0; n < N; ++n)
+    for (int64_t q = 0; q < rows; ++q) {
+      const int64_t c = q / (g.R * g.S), r = (q / g.S) % g.R, s = q % g.S;
+      const float* xp = x + n * x_img + c * g.H * g.W;
+      float* cp = col + (n * rows + q) * P;
+      for (int64_t oh = 0; oh < g.OH; ++oh) {
+        const int64_t ih = oh * g.sh - g.ph + r * g.dh;
+        for (int64_t ow = 0; ow < g.OW; ++ow) {
+          const int64_t iw = ow * g.sw - g.pw + s * g.dw;
+          cp[oh * g.OW + ow] = (ih >= 0 && ih < g.H && iw >= 0 && iw < g.W) ? xp[ih * g.W + iw] : 0.f;
+        }
+      }
+    }
+}
+
+void dwconv(Ctx& c, const float* x, const float* w, const float* bias, float* y, int64_t N,
+            int64_t mult, const ConvG& g) {
+  const int64_t K = g.C * mult;
+  parallel_rows(c.threads, N * K, [&](int64_t a, int64_t b) {
+    for (int64_t nk = a; nk < b; ++nk) {
+      const int64_t n = nk / K, k = nk % K, ci = k / mult;
+      const float* xp = x + (n * g.C + ci) * g.H * g.W;
+      const float* wp = w + k * g.R * g.S;
+      float* yp = y + nk * g.OH * g.OW;
+      for (int64_t oh = 0; oh < g.OH; ++oh)
+        for (int64_t ow = 0; ow < g.OW; ++ow) {
+          float acc = bias ? bias[k] : 0.f;
+          for (int64_t r = 0; r < g.R; ++r) {
+            const int64_t ih = oh * g.sh - g.ph + r * g.dh;
+            if (ih < 0 || ih >= g.H) continue;
+            for (int64_t s = 0; s < g.S; ++s) {
+              const int64_t iw = ow * g.sw - g.pw + s * g.dw;
+              if (iw >= 0 && iw < g.W) acc += xp[ih * g.W + iw] * wp[r * g.S + s];
+            }
+          }
+          yp[oh * g.OW + ow] = acc;
+        }
+    }
+  });
+}
+
+void pool2d(Ctx& c, const float* x, float* y, int64_t planes, const PoolG& p) {
+  parallel_rows(c.threads, planes, [&](int64_t a, int64_t b) {
+    for (int64_t pl = a; pl < b; ++pl) {
+      const float* xp = x + pl * p.H * p.W;
+      for (int64_t oh = 0; oh < p.OH; ++oh)
+        for (int64_t ow = 0; ow < p.OW; ++ow) {
+          int64_t h0, h1, w0, w1;
+          if (p.adaptive) {
+            h0 = oh * p.H / p.OH; h1 = ((oh + 1) * p.H + p.OH - 1) / p.OH;
+            w0 = ow * p.W / p.OW; w1 = ((ow + 1) * p.W + p.OW - 1) / p.OW;
+          } else {
+            h0 = oh * p.sh - p.ph; h1 = h0 + p.kh;
+            w0 = ow * p.sw - p.pw; w1 = w0 + p.kw;
+          }
+          const int64_t area = (h1 - h0) * (w1 - w0);
+          h0 = std::max<int64_t>(h0, 0); h1 = std::min(h1, p.H);
+          w0 = std::max<int64_t>(w0, 0); w1 = std::min(w1, p.W);
+          float acc = p.max ? -INFINITY : 0.f;
+          for (int64_t ih = h0; ih < h1; ++ih)
+            for (int64_t iw = w0; iw < w1; ++iw)
+              acc = p.max ? std::max(acc, xp[ih * p.W + iw]) : acc + xp[ih * p.W + iw];
+          if (!p.max) acc /= (float)((p.exclusive || p.adaptive) ? std::max<int64_t>((h1 - h0) * (w1 - w0), 1) : area);
+          y[(pl * p.OH + oh) * p.OW + ow] = acc;
+        }
+    }
+  });
+}
+
+void channel_affine(Ctx&, const float* x, const float* sc, const float* sh, float* y, int64_t outer,
+                    int64_t C, int64_t inner, int act, float p0) {
+  for (int64_t o = 0; o < outer; ++o)
+    for (int64_t ch = 0; ch < C; ++ch) {
+      const float a = sc[ch], b = sh[ch];
+      const int64_t base = (o * C + ch) * inner;
+      for (int64_t i = 0; i < inner; ++i) y[base + i] = unary_f(act, x[base + i] * a + b, p0, 0.f);
+    }
 }
 
 }  // namespace cpu

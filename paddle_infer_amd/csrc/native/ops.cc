@@ -236,6 +236,145 @@ DTensor reshaped(const DTensor& x, std::vector<int64_t> shape) {
   return r;
 }
 
+
+// ------------------------------------------------------------------------------ conv / pool
+// Paddle padding resolution (`conv_op.h UpdatePaddingAndDilation`): paddings [p] x2 or [lo, hi]
+// per spatial dim; SAME → out = ceil(in / st), VALID → no padding.
+void resolve_pad(int64_t in, int64_t k_eff, int64_t st, const std::string& algo, int64_t lo_in,
+                 int64_t hi_in, bool ceil_mode, int64_t& lo, int64_t& out) {
+  if (algo == "SAME") {
+    out = (in + st - 1) / st;
+    const int64_t total = std::max<int64_t>((out - 1) * st + k_eff - in, 0);
+    lo = total / 2;
+  } else if (algo == "VALID") {
+    lo = 0;
+    out = (in - k_eff) / st + 1;
+  } else {
+    lo = lo_in;
+    const int64_t span = in + lo_in + hi_in - k_eff;
+    out = (ceil_mode ? span + st - 1 : span) / st + 1;
+  }
+  if (out < 1) throw std::runtime_error("conv/pool: empty output");
+}
+
+void pads4(const std::vector<int64_t>& p, int64_t (&q)[4]) {  // → top, bottom, left, right
+  if (p.size() == 4) { q[0] = p[0]; q[1] = p[1]; q[2] = p[2]; q[3] = p[3]; }
+  else if (p.size() == 2) { q[0] = q[1] = p[0]; q[2] = q[3] = p[1]; }
+  else q[0] = q[1] = q[2] = q[3] = 0;
+}
+
+bool nhwc_layout(const OpDesc& o, const char* key) { return o.as(key, "NCHW") == "NHWC"; }
+
+void conv2d_op(Ctx& c, const OpDesc& o, Scope& s) {
+  DTensor x = in(c, s, o, "Input");
+  const DTensor& w = in(c, s, o, "Filter");
+  need_f32(x, o);
+  need_f32(w, o);
+  const bool nhwc = nhwc_layout(o, "data_format");
+  if (nhwc) x = transpose(c, x, {0, 3, 1, 2});
+  if (x.dims.size() != 4 || w.dims.size() != 4) throw std::runtime_error(o.type + ": 4-D input/filter");
+  const int64_t N = x.dims[0], Cin = x.dims[1], H = x.dims[2], W = x.dims[3];
+  const int64_t K = w.dims[0], cg = w.dims[1], R = w.dims[2], S = w.dims[3];
+  const int64_t G = std::max<int64_t>(o.ai("groups", 1), 1);
+  if (cg * G != Cin || K % G) throw std::runtime_error(o.type + ": groups do not match the channels");
+  std::vector<int64_t> st = o.aints("strides"), dl = o.aints("dilations");
+  if (st.size() < 2) st = {1, 1};
+  if (dl.size() < 2) dl = {1, 1};
+  int64_t p4[4];
+  pads4(o.aints("paddings"), p4);
+  const std::string algo = o.as("padding_algorithm", "EXPLICIT");
+  ConvG g{cg, H, W, R, S, 0, 0, st[0], st[1], 0, 0, dl[0], dl[1]};
+  resolve_pad(H, dl[0] * (R - 1) + 1, st[0], algo, p4[0], p4[1], false, g.ph, g.OH);
+  resolve_pad(W, dl[1] * (S - 1) + 1, st[1], algo, p4[2], p4[3], false, g.pw, g.OW);
+  DTensor y = make(c, VT_FP32, {N, K, g.OH, g.OW});
+  const int64_t P = g.OH * g.OW, kg = K / G;
+  if (cg == 1 && G == Cin) {  // depthwise (channel multiplier K / Cin): direct kernel
+    g.C = Cin;
+    kern::dwconv(c, x.data<float>(), w.data<float>(), nullptr, y.data<float>(), N, K / Cin, g);
+  } else {
+    const bool direct = R == 1 && S == 1 && st[0] == 1 && st[1] == 1 && g.ph == 0 && g.pw == 0 &&
+                        g.OH == H && g.OW == W;  // 1×1: the image itself is the column matrix
+    DTensor col;
+    if (!direct) col = make(c, VT_FP32, {N, cg * R * S, P});
+    for (int64_t gi = 0; gi < G; ++gi) {
+      const float* xg = x.data<float>() + gi * cg * H * W;
+      const float* B = xg;
+      int64_t sB = Cin * H * W;
+      if (!direct) {
+        kern::im2col(c, xg, Cin * H * W, col.data<float>(), N, g);
+        B = col.data<float>();
+        sB = cg * R * S * P;
+      }
+      kern::gemm(c, false, false, kg, P, cg * R * S, 1.f, w.data<float>() + gi * kg * cg * R * S,
+                 cg * R * S, 0, B, P, sB, 0.f, y.data<float>() + gi * kg * P, P, K * P, N);
+    }
+  }
+  if (o.has_in("Bias")) {  // conv2d_fusion-style bias [K]
+    const DTensor& b = in(c, s, o, "Bias");
+    DTensor one = make(c, VT_FP32, {K});
+    kern::fill(c, one.buf->p, VT_FP32, K, 1.0);
+    kern::channel_affine(c, y.data<float>(), one.data<float>(), b.data<float>(), y.data<float>(), N, K, P, U_IDENT, 0.f);
+  }
+  s[o.out("Output")] = nhwc ? transpose(c, y, {0, 2, 3, 1}) : y;
+}
+
+void pool2d_op(Ctx& c, const OpDesc& o, Scope& s) {
+  DTensor x = in(c, s, o, "X");
+  need_f32(x, o);
+  const bool nhwc = nhwc_layout(o, "data_format");
+  if (nhwc) x = transpose(c, x, {0, 3, 1, 2});
+  if (x.dims.size() != 4) throw std::runtime_error("pool2d: 4-D input");
+  const int64_t N = x.dims[0], C = x.dims[1], H = x.dims[2], W = x.dims[3];
+  std::vector<int64_t> k = o.aints("ksize"), st = o.aints("strides");
+  if (k.size() < 2) throw std::runtime_error("pool2d: ksize");
+  if (st.size() < 2) st = {1, 1};
+  PoolG p{H, W, 0, 0, k[0], k[1], st[0], st[1], 0, 0, o.as("pooling_type", "max") == "max",
+          o.ab("exclusive", true), o.ab("adaptive", false)};
+  if (o.ab("global_pooling", false)) {
+    p.kh = H; p.kw = W; p.OH = p.OW = 1; p.adaptive = 0; p.sh = p.sw = 1;
+  } else if (p.adaptive) {
+    p.OH = k[0]; p.OW = k[1];
+  } else {
+    int64_t p4[4];
+    pads4(o.aints("paddings"), p4);
+    const std::string algo = o.as("padding_algorithm", "EXPLICIT");
+    const bool ceil = o.ab("ceil_mode", false);
+    resolve_pad(H, p.kh, p.sh, algo, p4[0], p4[1], ceil, p.ph, p.OH);
+    resolve_pad(W, p.kw, p.sw, algo, p4[2], p4[3], ceil, p.pw, p.OW);
+  }
+  DTensor y = make(c, VT_FP32, {N, C, p.OH, p.OW});
+  kern::pool2d(c, x.data<float>(), y.data<float>(), N * C, p);
+  s[o.out("Out")] = nhwc ? transpose(c, y, {0, 2, 3, 1}) : y;
+}
+
+// inference batch norm: y = x · γ/√(σ²+ε) + (β − μ·γ/√(σ²+ε)) per channel (folded on the host)
+void batch_norm_op(Ctx& c, const OpDesc& o, Scope& s) {
+  const DTensor& x = in(c, s, o, "X");
+  need_f32(x, o);
+  const DTensor g = to_host(in(c, s, o, "Scale"), c), b = to_host(in(c, s, o, "Bias"), c);
+  const DTensor m = to_host(in(c, s, o, "Mean"), c), v = to_host(in(c, s, o, "Variance"), c);
+  const int64_t C = g.numel();
+  const float eps = o.af("epsilon", 1e-5f);
+  DTensor sc, sh;
+  sc.dtype = sh.dtype = VT_FP32;
+  sc.dims = sh.dims = {C};
+  sc.buf = alloc_buffer(C * 4, false);
+  sh.buf = alloc_buffer(C * 4, false);
+  for (int64_t i = 0; i < C; ++i) {
+    const float a = g.data<float>()[i] / std::sqrt(v.data<float>()[i] + eps);
+    sc.data<float>()[i] = a;
+    sh.data<float>()[i] = b.data<float>()[i] - m.data<float>()[i] * a;
+  }
+  if (c.gpu) { sc = to_device(sc, c); sh = to_device(sh, c); }
+  const bool nhwc = nhwc_layout(o, "data_layout");
+  const int64_t N = x.dims.at(0);
+  const int64_t inner = nhwc ? 1 : x.numel() / (N * C);
+  const int64_t outer = nhwc ? x.numel() / C : N;
+  DTensor y = make(c, VT_FP32, x.dims);
+  kern::channel_affine(c, x.data<float>(), sc.data<float>(), sh.data<float>(), y.data<float>(), outer, C, inner, U_IDENT, 0.f);
+  s[o.out("Y")] = y;
+}
+
 }  // namespace
 
 const std::unordered_map<std::string, OpFn>& op_registry() {
@@ -524,6 +663,20 @@ const std::unordered_map<std::string, OpFn>& op_registry() {
       }
       s[o.out("Out")] = cur;
     };
+    r["conv2d"] = conv2d_op;
+    r["depthwise_conv2d"] = conv2d_op;
+    r["pool2d"] = pool2d_op;
+    r["batch_norm"] = batch_norm_op;
+    r["relu6"] = [](Ctx& c, const OpDesc& o, Scope& s) { unary_op(c, o, s, U_RELU6, o.af("threshold", 6.f)); };
+    r["hard_swish"] = [](Ctx& c, const OpDesc& o, Scope& s) {
+      const float th = o.af("threshold", 6.f), sc = o.af("scale", 6.f), off = o.af("offset", 3.f);
+      if (sc != th) throw std::runtime_error("hard_swish: scale != threshold is not supported");
+      unary_op(c, o, s, U_HSWISH, th, off);
+    };
+    r["hard_sigmoid"] = [](Ctx& c, const OpDesc& o, Scope& s) {
+      unary_op(c, o, s, U_HSIGMOID, o.af("slope", 0.2f), o.af("offset", 0.5f));
+    };
+    r["leaky_relu"] = [](Ctx& c, const OpDesc& o, Scope& s) { unary_op(c, o, s, U_LEAKY, o.af("alpha", 0.02f)); };
     r["reduce_mean"] = [red](Ctx& c, const OpDesc& o, Scope& s) { red(c, o, s, true); };
     r["reduce_sum"] = [red](Ctx& c, const OpDesc& o, Scope& s) { red(c, o, s, false); };
     return r;

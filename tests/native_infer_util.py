@@ -83,3 +83,32 @@ def native_outputs(path, feeds, tmp, gpu=None, repeat=1):
         elif parts and parts[0] == "run_ms":
             ms = float(parts[1])
     return outs, ms, r.stdout
+
+
+class SmallCNN(paddle.nn.Layer):
+    """conv (strided, padded, bias) → BN → ReLU6 → max-pool (ceil) → grouped conv → BN → hardswish
+    → depthwise 3×3 (dilation 2) → avg-pool → 1×1 conv → adaptive avg-pool → flatten → linear:
+    conv2d (im2col + GEMM, 1×1 direct, depthwise kernel), batch_norm, pool2d, relu6, hard_swish."""
+
+    def __init__(self):
+        super().__init__()
+        nn = paddle.nn
+        self.c1 = nn.Conv2D(3, 16, 3, stride=2, padding=1)
+        self.b1 = nn.BatchNorm2D(16)
+        self.c2 = nn.Conv2D(16, 32, 3, padding=1, groups=4, bias_attr=False)
+        self.b2 = nn.BatchNorm2D(32)
+        self.dw = nn.Conv2D(32, 32, 3, padding=2, dilation=2, groups=32)
+        self.pw = nn.Conv2D(32, 24, 1)
+        self.fc = nn.Linear(24, 10)
+        for b in (self.b1, self.b2):  # non-trivial running statistics
+            b._mean.data.uniform_(-0.5, 0.5)
+            b._variance.data.uniform_(0.5, 2.0)
+
+    def forward(self, x):
+        F = paddle.nn.functional
+        h = F.relu6(self.b1(self.c1(x)))
+        h = F.max_pool2d(h, 3, 2, 1, ceil_mode=True)
+        h = F.hardswish(self.b2(self.c2(h)))
+        h = F.avg_pool2d(self.dw(h), 2, 2)
+        h = F.adaptive_avg_pool2d(self.pw(h), 1)
+        return self.fc(paddle.flatten(h, 1))

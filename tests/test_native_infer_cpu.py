@@ -5,6 +5,7 @@ import os
 import subprocess
 
 import numpy as np
+import torch
 import pytest
 
 from native_infer_util import MLP, RUN, Encoder, export, native_outputs, python_outputs
@@ -91,3 +92,29 @@ def test_reference_c_api_on_native_engine(tmp_path):
         parts = ln.split()
         vals = np.array([float(v) for v in parts[7:]], dtype=np.float32).reshape(3, 3)
         np.testing.assert_allclose(vals, ref, rtol=1e-5, atol=1e-6)
+
+
+def test_cnn_ops_match_python_predictor(tmp_path):
+    """conv2d (grouped / depthwise / 1×1 / strided / dilated), batch_norm, pool2d (max ceil-mode,
+    avg, adaptive), relu6 and hard_swish on the native engine."""
+    from native_infer_util import SmallCNN
+    path = str(tmp_path / "cnn")
+    export(SmallCNN(), path, [InputSpec([None, 3, 33, 30], "float32", "x")])
+    x = np.random.RandomState(1).randn(2, 3, 33, 30).astype("float32")
+    ref = python_outputs(path, {"x": x})
+    got, _, _ = native_outputs(path, {"x": x}, tmp_path)
+    np.testing.assert_allclose(got[0], ref[0], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("arch", ["mobilenet_v2", "resnet18"])
+def test_vision_models_match_python_predictor(tmp_path, arch):
+    """Whole paddle.vision models exported with jit.save run on the native engine."""
+    from paddle_infer_amd.vision import models as VM
+    torch.manual_seed(0)
+    m = getattr(VM, arch)(num_classes=10)
+    path = str(tmp_path / arch)
+    export(m, path, [InputSpec([None, 3, 64, 64], "float32", "x")])
+    x = np.random.RandomState(2).randn(1, 3, 64, 64).astype("float32")
+    ref = python_outputs(path, {"x": x})
+    got, _, _ = native_outputs(path, {"x": x}, tmp_path)
+    np.testing.assert_allclose(got[0], ref[0], rtol=1e-3, atol=1e-3)

@@ -8,9 +8,11 @@
 int fa_fwd_f16(const FaArgs& a, hipStream_t st);
 int fa_bwd_f16(const FaArgs& a, hipStream_t st);
 
-static int fa_check(const FaArgs& a) {
+// Head dims: 64 / 96 / 128 both ways; 256 (the wide forward) forward only — the backward of wider
+// heads is the query-chunked composition in ops/attention.py over the forward's log-sum-exp.
+static int fa_check(const FaArgs& a, bool fwd) {
   if (a.Hk <= 0 || a.Hq % a.Hk || (a.cu_q && !a.cu_k)) return (int)hipErrorInvalidValue;
-  if (a.D != 64 && a.D != 96 && a.D != 128) return (int)hipErrorInvalidValue;
+  if (a.D != 64 && a.D != 96 && a.D != 128 && !(fwd && a.D == 256)) return (int)hipErrorInvalidValue;
   if (a.p_drop < 0.f || a.p_drop >= 1.f) return (int)hipErrorInvalidValue;
   if (a.mask && ((a.smb | a.smh | a.smq) & 3)) return (int)hipErrorInvalidValue;  // 8-B mask reads
   return 0;
@@ -21,7 +23,7 @@ static int fa_check(const FaArgs& a) {
 // lse: f32 [B, Hq, Sq] (packed: [Hq, ltot]), nullable. f16: 0 = bf16, 1 = fp16.
 PIAMD_EXPORT int piamd_fa_fwd(const FaArgs* args, int f16, hipStream_t stream) {
   FaArgs a = *args;
-  if (int e = fa_check(a)) return e;
+  if (int e = fa_check(a, true)) return e;
   if (a.cu_q) a.sqb = a.skb = a.svb = a.sob = 0;
   if (a.B == 0 || a.Sq == 0) return 0;
   if (a.Sk == 0) return (int)hipErrorInvalidValue;
@@ -33,7 +35,7 @@ PIAMD_EXPORT int piamd_fa_fwd(const FaArgs* args, int f16, hipStream_t stream) {
 // as the forward.
 PIAMD_EXPORT int piamd_fa_bwd(const FaArgs* args, int f16, hipStream_t stream) {
   FaArgs a = *args;
-  if (int e = fa_check(a)) return e;
+  if (int e = fa_check(a, false)) return e;
   if (a.cu_q) a.sqb = a.skb = a.svb = a.sob = 0;
   if (a.B == 0 || a.Sq == 0 || a.Sk == 0) return 0;
   return f16 ? fa_bwd_f16(a, stream) : fa::launch_bwd<false>(a, stream);

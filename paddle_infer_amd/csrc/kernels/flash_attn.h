@@ -297,7 +297,11 @@ __global__ __launch_bounds__(64 * NW, D > 128 ? 1 : 8 / NW) void fwd_kernel(FaAr
   constexpr int DT = D / 32;
   constexpr int ROWB = DP * 2;
   constexpr int TILE_B = BN * ROWB;  // bytes per K or V tile
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_B];
+  // one LDS object per buffer: the waitcnt pass can then prove the reads of buffer t
+  // independent of the DMA still landing in buffer t+1 (a single array made hipcc put a
+  // vmcnt(0) before the PV reads of every tile, exposing the next tile's HBM fetch)
+  __shared__ __attribute__((aligned(16))) char kv0[2 * TILE_B];
+  __shared__ __attribute__((aligned(16))) char kv1[2 * TILE_B];
 
   const unsigned short* q = (const unsigned short*)a.q;
   const unsigned short* k = (const unsigned short*)a.k;
@@ -359,12 +363,12 @@ __global__ __launch_bounds__(64 * NW, D > 128 ? 1 : 8 / NW) void fwd_kernel(FaAr
     for (int j = 0; j < 16; ++j) oacc[i][j] = 0.f;
   float m_i = -INFINITY, l_i = 0.f;
 
-  auto issue = [&](int t, int buf) {
-    char* ks = smem + buf * 2 * TILE_B;
+  auto issue = [&](int t, auto bufc) {
+    char* ks = decltype(bufc)::value ? kv1 : kv0;
     glds_tile<BN, ROWB, D / 8, NW>(kbase, a.sks, t * BN, Sk - 1, ks, w, lane);
     glds_tile<BN, ROWB, D / 8, NW>(vbase, a.svs, t * BN, Sk - 1, ks + TILE_B, w, lane);
   };
-  if (ntiles > 0) issue(0, 0);
+  if (ntiles > 0) issue(0, std::integral_constant<int, 0>{});
   __syncthreads();
 
   LaneOffs<ROWB, KSTEPS, DT> L;
@@ -374,8 +378,9 @@ __global__ __launch_bounds__(64 * NW, D > 128 ? 1 : 8 / NW) void fwd_kernel(FaAr
   const int m_lim = min(CAUSAL ? qpos + coff + 1 : 0x40000000, Sk) - 4 * hh;
   auto tile = [&](int t, auto bufc) {
     constexpr int BUF = decltype(bufc)::value;
-    constexpr int KS = BUF * 2 * TILE_B, VS = KS + TILE_B;
-    if (t + 1 < ntiles) issue(t + 1, BUF ^ 1);
+    constexpr int KS = 0, VS = TILE_B;
+    const char* smem = BUF ? kv1 : kv0;
+    if (t + 1 < ntiles) issue(t + 1, std::integral_constant<int, BUF ^ 1>{});
     const int n0 = t * BN;
     const bool active = wave_rows_valid && (!CAUSAL || n0 <= qrow0 + 31 + coff);
     if (active) {
@@ -541,11 +546,16 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(FaArgs a) {
   constexpr int ROWB = DP * 2;
   constexpr int QTILE_B = BQ * ROWB;    // Q or dO tile [64][DP]
   constexpr int KIMG_B = BK * ROWB;     // resident K and V images of the block's 128 keys
-  constexpr int OFF_K = 2 * 2 * QTILE_B;
+  constexpr int OFF_K = 0;
   constexpr int OFF_V = OFF_K + KIMG_B;
-  constexpr int OFF_STAT = OFF_V + KIMG_B;  // 2 buffers x (−lse/scale, −δ) x 64 f32
-  constexpr int SMEM = OFF_STAT + 2 * 2 * BQ * 4;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  constexpr int OFF_STAT = 2 * QTILE_B;  // per buffer: (−lse/scale, −δ) x 64 f32 after Q, dO
+  constexpr int QBUF_B = OFF_STAT + 2 * BQ * 4;
+  // resident K/V images and the two Q/dO buffers as separate LDS objects: the waitcnt pass can
+  // then prove reads of one buffer independent of the DMA landing in the other (one array made
+  // hipcc wait vmcnt(0) before the first transposed read of every tile)
+  __shared__ __attribute__((aligned(16))) char smem[2 * KIMG_B];
+  __shared__ __attribute__((aligned(16))) char qb0[QBUF_B];
+  __shared__ __attribute__((aligned(16))) char qb1[QBUF_B];
 
   const unsigned short* q = (const unsigned short*)a.q;
   const unsigned short* k = (const unsigned short*)a.k;
@@ -618,10 +628,12 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(FaArgs a) {
   DmaOffs<BQ, ROWB, D / 8> dmq, dmo;
   dma_offs(a.sqs, w, lane, dmq);
   dma_offs(a.sos, w, lane, dmo);
-  auto issue = [&](int it, int buf) {
+  auto issue = [&](int it, auto bufc) {
+    constexpr int buf = decltype(bufc)::value;
+    char* qb = buf ? qb1 : qb0;
     const int hq = hk * group + it / tiles_per_head;
     const int q0 = (qt0 + it % tiles_per_head) * BQ;
-    char* qs = smem + buf * 2 * QTILE_B;
+    char* qs = qb;
     const unsigned short* qh = q + b * a.sqb + hq * a.sqh;
     const unsigned short* oh = dout + b * a.sob + hq * a.soh;
     if (q0 + BQ <= Sq) {  // full tile: precomputed lane offsets
@@ -633,24 +645,26 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(FaArgs a) {
     }
     if (w < 2) {  // wave 0: −lse/scale row, wave 1: −δ row (64 f32 = one 4-B/lane DMA)
       const float* s = (w == 0 ? nl : nd) + lrow + hq * lhead + min(q0 + lane, Sq - 1);
-      char* st = smem + OFF_STAT + (buf * 2 + w) * BQ * 4;
+      char* st = qb + OFF_STAT + w * BQ * 4;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)s,
                                        (__attribute__((address_space(3))) void*)st, 4, 0, 0);
     }
   };
-  if (total > 0) issue(0, 0);
+  if (total > 0) issue(0, std::integral_constant<int, 0>{});
   __syncthreads();
 
-  // one query tile; every LDS address below is a precomputed lane offset + the buffer base + an
-  // immediate (unrolling the buffer parity into two tile bodies measured more AGPR<->VGPR copies
-  // at one wave per SIMD)
-  auto tile = [&](int it, int BUF) {
-    const int QS = BUF * 2 * QTILE_B, DOS = QS + QTILE_B;
-    const float* lst = reinterpret_cast<const float*>(smem + OFF_STAT) + BUF * 2 * BQ;
+  // one query tile; every LDS address below is a precomputed lane offset + an immediate. The
+  // buffer parity is a template constant (two tile bodies) so each body reads one LDS object
+  // while the DMA lands in the other.
+  auto tile = [&](int it, auto bufc) {
+    constexpr int BUF = decltype(bufc)::value;
+    const char* qb = BUF ? qb1 : qb0;
+    constexpr int QS = 0, DOS = QTILE_B;
+    const float* lst = reinterpret_cast<const float*>(qb + OFF_STAT);
     const float* dst = lst + BQ;
     const int hq = hk * group + it / tiles_per_head;
     const int q0 = (qt0 + it % tiles_per_head) * BQ;
-    if (it + 1 < total) issue(it + 1, BUF ^ 1);
+    if (it + 1 < total) issue(it + 1, std::integral_constant<int, BUF ^ 1>{});
     f32x16 sacc[2], pacc[2];
     // S' = Q·Kᵀ − lse/scale, dP' = dO·Vᵀ − δ: row constants as the initial accumulators
 #pragma unroll
@@ -672,8 +686,8 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(FaArgs a) {
       f[1] = lds_at<F16>(smem, kvo[kk] + KIMG_B);
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
-        f[2 + qt] = lds_at<F16>(smem, L.row[kk] + QS + qt * 32 * ROWB);
-        f[4 + qt] = lds_at<F16>(smem, L.row[kk] + DOS + qt * 32 * ROWB);
+        f[2 + qt] = lds_at<F16>(qb, L.row[kk] + QS + qt * 32 * ROWB);
+        f[4 + qt] = lds_at<F16>(qb, L.row[kk] + DOS + qt * 32 * ROWB);
       }
     };
     ld(0, fr[0]);
@@ -737,14 +751,17 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(FaArgs a) {
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         const int ro = 16 * ks * ROWB;
-        const V8 fo = cat44<F16>(lds_tr_at(smem, L.tr[0][dt] + DOS + ro), lds_tr_at(smem, L.tr[1][dt] + DOS + ro));
-        const V8 fq = cat44<F16>(lds_tr_at(smem, L.tr[0][dt] + QS + ro), lds_tr_at(smem, L.tr[1][dt] + QS + ro));
+        const V8 fo = cat44<F16>(lds_tr_at(qb, L.tr[0][dt] + DOS + ro), lds_tr_at(qb, L.tr[1][dt] + DOS + ro));
+        const V8 fq = cat44<F16>(lds_tr_at(qb, L.tr[0][dt] + QS + ro), lds_tr_at(qb, L.tr[1][dt] + QS + ro));
         dvacc[dt] = E::mfma(fo, pb[ks], dvacc[dt]);
         dkacc[dt] = E::mfma(fq, db[ks], dkacc[dt]);
       }
     __syncthreads();
   };
-  for (int it = 0; it < total; ++it) tile(it, it & 1);
+  for (int it = 0; it < total; it += 2) {
+    tile(it, std::integral_constant<int, 0>{});
+    if (it + 1 < total) tile(it + 1, std::integral_constant<int, 1>{});
+  }
 
   if (key < Sk) {
     const float vs = (FEAT & F_DROP) ? drk.inv : 1.f;
@@ -779,7 +796,9 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(FaArgs a) {
   constexpr int DT = D / 32;
   constexpr int ROWB = DP * 2;
   constexpr int TILE_B = BN * ROWB;
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TILE_B];
+  // one LDS object per buffer (see fwd_kernel)
+  __shared__ __attribute__((aligned(16))) char kv0[2 * TILE_B];
+  __shared__ __attribute__((aligned(16))) char kv1[2 * TILE_B];
 
   const unsigned short* q = (const unsigned short*)a.q;
   const unsigned short* k = (const unsigned short*)a.k;
@@ -853,12 +872,12 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(FaArgs a) {
 #pragma unroll
     for (int j = 0; j < 16; ++j) qacc[i][j] = 0.f;
 
-  auto issue = [&](int t, int buf) {
-    char* ks = smem + buf * 2 * TILE_B;
+  auto issue = [&](int t, auto bufc) {
+    char* ks = decltype(bufc)::value ? kv1 : kv0;
     glds_tile<BN, ROWB, D / 8>(kbase, a.sks, t * BN, Sk - 1, ks, w, lane);
     glds_tile<BN, ROWB, D / 8>(vbase, a.svs, t * BN, Sk - 1, ks + TILE_B, w, lane);
   };
-  if (ntiles > 0) issue(0, 0);
+  if (ntiles > 0) issue(0, std::integral_constant<int, 0>{});
   __syncthreads();
 
   const bool wave_rows_valid = qrow0 < Sq;
@@ -866,8 +885,9 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(FaArgs a) {
   const int m_lim = (CAUSAL ? qpos + coff + 1 : 0x40000000) - 4 * hh;
   auto tile = [&](int t, auto bufc) {
     constexpr int BUF = decltype(bufc)::value;
-    constexpr int KS = BUF * 2 * TILE_B, VS = KS + TILE_B;
-    if (t + 1 < ntiles) issue(t + 1, BUF ^ 1);
+    constexpr int KS = 0, VS = TILE_B;
+    const char* smem = BUF ? kv1 : kv0;
+    if (t + 1 < ntiles) issue(t + 1, std::integral_constant<int, BUF ^ 1>{});
     const int n0 = t * BN;
     const bool active = wave_rows_valid && (!CAUSAL || n0 <= qrow0 + 31 + coff);
     if (active) {

@@ -5,7 +5,8 @@ Plan (cached per program version) comes from the native runtime (`csrc/runtime/s
 dependency-respecting instruction order + per-instruction GC list, so intermediates are released
 right after their last consumer (the reference's eager-deletion GC). Persistable variables live in
 the Scope across runs. Training programs (`backward.py`) hold one ``<type>_grad`` op per forward
-op — run as that op's VJP (`_run_grad_op`) — plus ``sum`` ops for renamed partial gradients and
+op — run with its explicit grad kernel (`grad_kernels.py`, the reference `*_grad` PHI kernels)
+when the program holds reference op types, else as the forward op's VJP (`_run_grad_op`) — plus ``sum`` ops for renamed partial gradients and
 per-parameter optimizer ops (``sgd`` / ``momentum`` / ``adam`` / ``adamw``) that update the
 persistable parameters and accumulators in place; the learning-rate variable of a program built
 by ``minimize`` is refreshed from its optimizer / LRScheduler before each run (reference
@@ -332,6 +333,51 @@ class Executor:
                 env[ref.name] = val
         _zip_assign(op.outputs, out, assign)
 
+    @staticmethod
+    def _run_grad_kernel(op, val, env):
+        """Run `op` with its explicit grad kernel (`grad_kernels.GRAD_KERNELS`) when it has one:
+        the gradient comes from the grad OpDesc's slots alone (forward inputs / outputs and the
+        output gradients), as the reference executor runs a `*_grad` PHI kernel. Returns False
+        for types without a kernel (the VJP path below handles them)."""
+        from .grad_kernels import GRAD_KERNELS
+        fn = GRAD_KERNELS.get(op.type)
+        if fn is None:
+            return False
+        fop = getattr(op, "fwd_op", None)
+        if fop is not None and fop.func is not None:
+            return False  # forward is a traced framework op: its grad op carries generic slots
+
+        def get(n):
+            if not n:
+                return None
+            if n in env:
+                return env[n]
+            try:
+                return val(n)
+            except KeyError:
+                return None
+        ins = {k: [get(n) for n in v] for k, v in op.paddle_inputs.items()}
+        if any(t is None for k, v in ins.items() if not k.endswith("@GRAD") for t in v):
+            return False  # a forward slot bound to a non-variable (a traced constant)
+        for k, v in ins.items():  # an output gradient that never reached this op is zero
+            if k.endswith("@GRAD") and any(t is None for t in v):
+                fwd = ins.get(k[:-5], [])
+                ins[k] = [t if t is not None else (torch.zeros_like(f) if isinstance(f, torch.Tensor) else None)
+                          for t, f in zip(v, fwd)]
+        if any(t is None for k, v in ins.items() if k.endswith("@GRAD") for t in v):
+            return False
+        with torch.no_grad():
+            res = fn(ins, op.attrs)
+        for slot, names in op.paddle_outputs.items():
+            vals = res.get(slot)
+            if vals is None:
+                continue
+            vals = vals if isinstance(vals, (list, tuple)) else [vals]
+            for n, v in zip(names, vals):
+                if n and v is not None:
+                    env[n] = v.detach()
+        return True
+
     def _run_grad_op(self, op, sub, env):
         """VJP of the grad op's forward op. Fast path: the op-local autograd graph its forward built
         in this run (the forward read its inputs through leaves, see `_run_op`). Otherwise the
@@ -351,6 +397,8 @@ class Executor:
 
         def val(n):
             return env[n] if n in env else sub(VarRef(n))
+        if self._run_grad_kernel(op, val, env):
+            return
         gouts = []
         for k, onames in fouts.items():
             for o, g in zip(onames, gslot[k]):

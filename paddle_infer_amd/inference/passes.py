@@ -24,6 +24,9 @@ a chain of Paddle ops and rewrites it into one fused op whose kernel is register
   multihead_matmul_fuse_pass      fc(QKV) + head split + attention + merge → multihead_matmul
   flash_attn_packed_fuse_pass     split(QKV) + flash_attn               → flash_attn_packed
   fc_elementwise_layernorm_fuse_pass  fc + residual add + layer_norm    → fused_fc_elementwise_layernorm
+  + the rest of the reference GPU list in passes_extra.py (is_test, simplify_with_basic_ops,
+    constant_folding, gpu_cpu_* matmul maps / shape+matmul fusions, matmul_scale, conv + bias
+    (+ residual) (+ act) → conv2d_fusion, conv + bias + bn, transpose_flatten_concat)
 
 Passes only rewrite when every intermediate has exactly one consumer and is not fetched.
 """
@@ -666,13 +669,26 @@ from .fmt_passes import (  # noqa: E402
     multi_devices_fused_multi_transformer_encoder_fuse_qkv_pass)
 from .fmt_passes import fused_multi_transformer_encoder_pass_ops as fused_multi_transformer_encoder_pass  # noqa: E402
 
+from .passes_extra import EXTRA_PASSES  # noqa: E402
+
+globals().update(EXTRA_PASSES)
+
+# Order follows the reference GpuPassStrategy: cleanups, the LLM layer passes, conv fusions, the
+# matmul→mul maps (so fc_fuse sees one form), attention / fc / LN fusions, constant folding last.
 GPU_PASSES = [
+    "is_test_pass", "simplify_with_basic_ops_pass",
     "delete_dropout_op_pass", "identity_scale_op_clean_pass", "identity_reshape_clean_pass",
     *_FMT_ORDER,  # the reference runs the LLM passes before the generic fc / attention fusions
-    "conv_bn_fuse_pass", "embedding_eltwise_layernorm_fuse_pass", "self_attention_fuse_pass",
+    "conv_bn_fuse_pass", "conv_eltwiseadd_bn_fuse_pass", "embedding_eltwise_layernorm_fuse_pass",
+    "self_attention_fuse_pass", "matmul_scale_fuse_pass",
+    "gpu_cpu_squeeze2_matmul_fuse_pass", "gpu_cpu_reshape2_matmul_fuse_pass",
+    "gpu_cpu_flatten2_matmul_fuse_pass", "gpu_cpu_map_matmul_v2_to_mul_pass",
+    "gpu_cpu_map_matmul_v2_to_matmul_pass", "gpu_cpu_map_matmul_to_mul_pass",
     "fc_fuse_pass", "fc_act_fuse_pass", "fused_multi_transformer_encoder_traced_pass",
     "fuse_multi_transformer_layer_pass", "multihead_matmul_fuse_pass", "flash_attn_packed_fuse_pass",
     "fc_elementwise_layernorm_fuse_pass", "skip_layernorm_fuse_pass", "linear_bias_act_fuse_pass",
+    "conv_elementwise_add2_act_fuse_pass", "conv_elementwise_add_act_fuse_pass",
+    "conv_elementwise_add_fuse_pass", "transpose_flatten_concat_fuse_pass", "constant_folding_pass",
 ]
 
 PASSES = {name: globals()[name] for name in GPU_PASSES}

@@ -195,6 +195,20 @@ def _phase_taps(R, st, pad, dil, ph):
     return taps, -dd[0], dil2
 
 
+def _take_ap(t, dim, idx):
+    """t.index_select(dim, idx) for an arithmetic progression idx, as a strided slice (+ flip when
+    descending): no host-built index tensor, so it is legal inside hipGraph capture."""
+    if len(idx) == 1:
+        return t.narrow(dim, idx[0], 1)
+    step = idx[1] - idx[0]
+    assert all(b - a == step for a, b in zip(idx, idx[1:])), idx
+    lo = min(idx[0], idx[-1])
+    sl = [slice(None)] * t.dim()
+    sl[dim] = slice(lo, lo + abs(step) * (len(idx) - 1) + 1, abs(step))
+    out = t[tuple(sl)]
+    return out.flip(dim) if step < 0 else out
+
+
 def conv2d_dgrad_strided(dy, weight, H, W, st, pad, dil):
     """dX [N,H,W,C] (dtype of dy) of a strided conv: one stride-1 HIP convolution per output phase
     (ih mod st_h, iw mod st_w) over dY with the sub-filter of the taps that reach that phase,
@@ -213,8 +227,9 @@ def conv2d_dgrad_strided(dy, weight, H, W, st, pad, dil):
                 dx[:, ph::st[0], pw::st[1], :] = 0
                 continue
             (rt, ph2, dh2), (stp, pw2, dw2) = th, tw
-            # sub-filter [C][R'][S'][K]: W[k][c][rt[i]][stp[j]]
-            wsub = wb[:, :, rt][:, :, :, stp].permute(1, 2, 3, 0).contiguous()
+            # sub-filter [C][R'][S'][K]: W[k][c][rt[i]][stp[j]] (taps are arithmetic progressions:
+            # strided slices + flips, no index tensor — capturable in a hipGraph)
+            wsub = _take_ap(_take_ap(wb, 2, rt), 3, stp).permute(1, 2, 3, 0).contiguous()
             y = _launch_geom(dy, wsub, (1, 1), (ph2, pw2), (dh2, dw2), Hp, Wp)
             dx[:, ph::st[0], pw::st[1], :] = y
     return dx

@@ -172,21 +172,45 @@ def _pads(p, nd):
     return p
 
 
+def _conv_padding(a):
+    pad = a.get("padding_algorithm", "EXPLICIT")
+    return "same" if pad == "SAME" else (0 if pad == "VALID" else _pads(a.get("paddings"), 2))
+
+
 @register("conv2d", "depthwise_conv2d")
 def _conv2d(ins, a):
+    """Through the framework's conv dispatch (`nn.functional.conv2d`): GPU tensors run the own
+    HIP conv kernels (`ops/conv.py` conv2d_any), CPU the reference path."""
+    from ..nn import functional as PF
     x, w = ins["Input"][0], ins["Filter"][0]
-    pad = a.get("padding_algorithm", "EXPLICIT")
-    padding = "same" if pad == "SAME" else (0 if pad == "VALID" else _pads(a.get("paddings"), 2))
-    y = F.conv2d(x, w, ins["Bias"][0] if ins.get("Bias") else None, a.get("strides", [1, 1]), padding,
-                 a.get("dilations", [1, 1]), a.get("groups", 1))
+    y = PF.conv2d(x, w, ins["Bias"][0] if ins.get("Bias") else None, a.get("strides", [1, 1]),
+                  _conv_padding(a), a.get("dilations", [1, 1]), a.get("groups", 1),
+                  a.get("data_format", "NCHW") if a.get("data_format") in ("NCHW", "NHWC") else "NCHW")
     return {"Output": y}
+
+
+_FUSION_ACTS = {"relu": F.relu, "relu6": F.relu6, "sigmoid": torch.sigmoid, "tanh": torch.tanh,
+                "leaky_relu": F.leaky_relu, "swish": F.silu, "silu": F.silu, "gelu": F.gelu,
+                "identity": None, "": None}
+
+
+@register("conv2d_fusion", "fused_conv2d_add_act")
+def _conv2d_fusion(ins, a):
+    """Reference `fused/conv_fusion_op.cc` (conv2d_fusion): Output = act(conv(Input, Filter) +
+    Bias [+ ResidualData]); the target of conv_elementwise_add(2)_act_fuse_pass."""
+    y = _conv2d(ins, a)["Output"]
+    if ins.get("ResidualData") and ins["ResidualData"][0] is not None:
+        y = y + ins["ResidualData"][0]
+    fn = _FUSION_ACTS.get(a.get("activation", "relu"), None)
+    return {"Output": fn(y) if fn is not None else y}
 
 
 @register("conv2d_transpose")
 def _conv2d_t(ins, a):
-    y = F.conv_transpose2d(ins["Input"][0], ins["Filter"][0], None, a.get("strides", [1, 1]),
-                           _pads(a.get("paddings"), 2), a.get("output_padding") or 0,
-                           a.get("groups", 1), a.get("dilations", [1, 1]))
+    from ..nn import functional as PF
+    y = PF.conv2d_transpose(ins["Input"][0], ins["Filter"][0], None, a.get("strides", [1, 1]),
+                            _pads(a.get("paddings"), 2), a.get("output_padding") or 0,
+                            a.get("groups", 1), a.get("dilations", [1, 1]))
     return {"Output": y}
 
 
@@ -218,6 +242,28 @@ def _reshape(ins, a):
 @register("transpose2", "transpose")
 def _transpose(ins, a):
     return {"Out": ins["X"][0].permute(*a.get("axis"))}
+
+
+@register("flatten2", "flatten")
+def _flatten2(ins, a):
+    """Reference `flatten_op.cc` (flatten2): [d0..d(axis-1)] x [d(axis)..] as a 2-D tensor."""
+    x = ins["X"][0]
+    ax = int(a.get("axis", 1))
+    lead = int(np.prod(x.shape[:ax])) if ax > 0 else 1
+    return {"Out": x.reshape(lead, -1)}
+
+
+@register("fusion_transpose_flatten_concat")
+def _fusion_tfc(ins, a):
+    """Reference `fused/fusion_transpose_flatten_concat_op.cc`: per input transpose(trans_axis) →
+    flatten(flatten_axis) → concat(concat_axis)."""
+    ax, fa = list(a.get("trans_axis")), int(a.get("flatten_axis", 1))
+    parts = []
+    for x in ins["X"]:
+        t = x.permute(ax)
+        lead = int(np.prod(t.shape[:fa])) if fa > 0 else 1
+        parts.append(t.reshape(lead, -1))
+    return {"Out": torch.cat(parts, int(a.get("concat_axis", 0)))}
 
 
 @register("flatten_contiguous_range")

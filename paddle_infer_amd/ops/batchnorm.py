@@ -18,6 +18,20 @@ from . import _lib
 
 _ACT = {"none": 0, None: 0, "identity": 0, "relu": 1, "relu6": 2}
 _MAX_PARTS = 2048  # statistics partial blocks (batchnorm.hip MAX_PARTS)
+_GRID_SET = [False]
+
+
+def _grid_once():
+    """PIAMD_BN_GRID="elems_per_block,max_blocks" retunes the NHWC statistics / reduction grid
+    (batchnorm.hip piamd_bn_set_parts); read once."""
+    if _GRID_SET[0]:
+        return
+    _GRID_SET[0] = True
+    import os
+    v = os.environ.get("PIAMD_BN_GRID")
+    if v:
+        e, p = (int(t) for t in v.split(","))
+        _lib.call("piamd_bn_set_parts", e, p)
 
 
 def _layout(x, data_format):
@@ -82,6 +96,7 @@ class _BNAct(torch.autograd.Function):
         rv = running_var if running_var is not None and running_var.dtype == torch.float32 else None
         if not training and (rm is None or rv is None):
             raise ValueError("eval-mode batch_norm needs f32 running statistics")
+        _grid_once()
         _lib.call("piamd_bn_fwd", int(x.dtype == torch.bfloat16), int(nhwc), xc.data_ptr(),
                   _lib.ptr(res), y.data_ptr(), N, C, S, _lib.ptr(g), _lib.ptr(b), _lib.ptr(rm),
                   _lib.ptr(rv), mean.data_ptr(), rstd.data_ptr(), float(momentum), float(eps),

@@ -108,6 +108,10 @@ def multi_tensor_update(op, entries, lr, cache=None, mu=0.0, nesterov=False, bet
                  e[1].dtype == torch.bfloat16, e[4], e[5]) for e in entries)
     ent = cache.get("table") if cache is not None else None
     if ent is None or ent[0] != key:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("merged optimizer: parameter / gradient buffers changed inside hipGraph "
+                               "capture (keep gradients allocated across steps: clear_grad(set_to_zero=True) "
+                               "and run one eager step before capturing)")
         meta, fmeta, offs, c = [], [], [0], 0
         for (pp, gp, s1p, s2p, bf, wd, lm), e in zip(key, entries):
             n = e[0].numel()

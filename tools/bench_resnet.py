@@ -32,7 +32,7 @@ def _setup():
     return world
 
 
-def build(batch, hip_conv, lr, res=224, seed=0, model="resnet50"):
+def build(batch, hip_conv, lr, res=224, seed=0, model="resnet50", static_grads=False):
     CV.HIP_CONV = hip_conv
     torch.manual_seed(seed)
     m = getattr(VM, model)(num_classes=1000).cuda().to(memory_format=torch.channels_last)
@@ -49,7 +49,9 @@ def build(batch, hip_conv, lr, res=224, seed=0, model="resnet50"):
             loss = torch.nn.functional.cross_entropy(model(x), y)
         loss.backward()
         opt.step()
-        opt.clear_grad(set_to_zero=False)
+        # graph replay needs the gradient buffers (and the merged optimizer's pointer table) to
+        # stay put: zero them in place instead of releasing them
+        opt.clear_grad(set_to_zero=static_grads)
         return loss
     return step
 
@@ -78,7 +80,7 @@ def graphed(step, warmup=3):
 def run(batch, steps, hip_conv, world, lr=0.02, model="resnet50", graph=False):
     # lr 0.02 (momentum 0.9, no warm-up): the timed steps keep training on the fixed synthetic
     # batch (loss falls below ln 1000); lr 0.1 without warm-up diverged there (loss 11.7, r2)
-    step = build(batch, hip_conv, lr=lr, model=model)
+    step = build(batch, hip_conv, lr=lr, model=model, static_grads=graph)
     if graph:
         step = graphed(step)
     for _ in range(3):

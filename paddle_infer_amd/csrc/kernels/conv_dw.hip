@@ -252,6 +252,34 @@ __global__ __launch_bounds__(256) void dconv_wgrad_finish(const float* __restric
   d[i] = v;
 }
 
+// First level of the partial-plane sum when there are many planes (a depthwise plane is only
+// 9·C floats, so one thread per weight walking every plane left a handful of workgroups each
+// serially loading thousands of values): grid (column blocks of 64, slices of the planes); the 4
+// lane rows of a block take interleaved planes of the slice, reduced in LDS in a fixed order;
+// out[slice][i]. Deterministic (fixed assignment and order); dconv_wgrad_finish sums the slices.
+constexpr int FIN_SLICES = 64;
+__global__ __launch_bounds__(256) void dconv_wgrad_reduce(const float* __restrict__ ws, int parts,
+                                                          long long n, float* __restrict__ out) {
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const long long i = (long long)blockIdx.x * 64 + tx;
+  const int per = (parts + gridDim.y - 1) / gridDim.y;
+  const int p0 = blockIdx.y * per, p1 = min(parts, p0 + per);
+  float v = 0.f;
+  if (i < n) {
+    int p = p0 + ty;
+    for (; p + 12 < p1; p += 16) {  // 4 independent loads in flight per lane
+      const float a = ws[(long long)p * n + i], b = ws[(long long)(p + 4) * n + i];
+      const float c = ws[(long long)(p + 8) * n + i], e = ws[(long long)(p + 12) * n + i];
+      v += (a + b) + (c + e);
+    }
+    for (; p < p1; p += 4) v += ws[(long long)p * n + i];
+  }
+  red[ty][tx] = v;
+  __syncthreads();
+  if (ty == 0 && i < n) out[(long long)blockIdx.y * n + i] = (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
+}
+
 template <int DT, int V, bool DW, bool TR>
 void launch_fwd(const void* x, const void* w, const void* b, void* y, const DGeom& g,
                 hipStream_t st) {
@@ -320,7 +348,8 @@ static void launch_wg(const void* x, const void* dy, float* ws, const DGeom& g, 
 }
 
 // dW' [R·S][cin_g][Cout] f32 of the forward conv (x [N][H][W][Cin], dy [N][OH][OW][Cout]);
-// ws: parts · R·S·cin_g·Cout floats of partial planes (parts ≥ 1 pixel chunks).
+// ws: (parts + 64) · R·S·cin_g·Cout floats: the partial planes (parts ≥ 1 pixel chunks), then
+// room for the 64 slice sums of the two-level finish (used when parts > 128).
 PIAMD_EXPORT int piamd_dconv2d_wgrad(const void* x, const void* dy, float* d, float* ws, int parts,
                                      int N, int H, int W, int Cin, int OH, int OW, int Cout, int R,
                                      int S, int st_h, int st_w, int pad_h, int pad_w, int dil_h,
@@ -351,6 +380,15 @@ PIAMD_EXPORT int piamd_dconv2d_wgrad(const void* x, const void* dy, float* d, fl
   }
 #undef WG
   const long long n = (long long)R * S * cin_g * Cout;
+  if (parts > 2 * FIN_SLICES) {
+    // two-level sum: the planes into FIN_SLICES slice sums (after the planes in ws), then those
+    float* slices = ws + (long long)parts * n;  // caller sized ws for parts + FIN_SLICES planes
+    hipLaunchKernelGGL(dconv_wgrad_reduce, dim3((unsigned)((n + 63) / 64), FIN_SLICES), dim3(256), 0, st,
+                       (const float*)ws, parts, n, slices);
+    hipLaunchKernelGGL(dconv_wgrad_finish, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                       (const float*)slices, FIN_SLICES, n, d);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(dconv_wgrad_finish, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
                      (const float*)ws, parts, n, d);
   return (int)hipGetLastError();

@@ -350,7 +350,7 @@ def _direct_wgrad(x, dy, R, S, st, pad, dil, C, K, groups=1):
     plane = R * S * cg * K
     parts = max(1, min(-(-2048 // (gy * gz)), M // (pl * 8), (16 << 20) // plane))
     d = torch.empty(plane, dtype=torch.float32, device=x.device)
-    ws = torch.empty(parts * plane, dtype=torch.float32, device=x.device)
+    ws = torch.empty((parts + 64) * plane, dtype=torch.float32, device=x.device)  # + slice sums
     _lib.call("piamd_dconv2d_wgrad", x.data_ptr(), dy.data_ptr(), d.data_ptr(), ws.data_ptr(), parts,
               N, H, W, C, OH, OW, K, R, S, st[0], st[1], pad[0], pad[1], dil[0], dil[1], cg, kg,
               _DT[x.dtype], _lib.stream())
@@ -408,6 +408,27 @@ class _ConvDirect(torch.autograd.Function):
         return dx, dw, db, None, None, None, None
 
 
+def _tall_wgrad(dy2, x2):
+    """dyᵀ·x [K, C] (f32) of a 1×1 conv over M ≫ K, C pixel rows. One library GEMM with a K×C
+    output has only a handful of output tiles (hipBLASLt picked 10-19 workgroups and took ~1 ms at
+    MobileNetV2's 112×112 layers, profiles/conv_nets_r3.txt); split the pixel rows into S chunks
+    as ONE batched GEMM with f32 outputs and sum the S partial planes in a fixed order."""
+    M, K = dy2.shape
+    C = x2.shape[1]
+    S = 1
+    while S < 256 and M % (2 * S) == 0 and M // (2 * S) >= 2048:
+        S *= 2
+    if S == 1:
+        return torch.mm(dy2.t(), x2).float()
+    a3 = dy2.view(S, M // S, K).transpose(1, 2)
+    b3 = x2.contiguous().view(S, M // S, C)
+    try:
+        part = torch.bmm(a3, b3, out_dtype=torch.float32)
+    except (RuntimeError, TypeError, NotImplementedError):
+        part = torch.bmm(a3, b3).float()
+    return part.sum(0)
+
+
 class _Conv1x1(torch.autograd.Function):
     """Dense 1×1 conv with channels off the 64-grid as a GEMM over pixel rows (ops.linear.mm_nt:
     the framework's assembly GEMM where its contract holds, hipBLASLt otherwise)."""
@@ -441,7 +462,7 @@ class _Conv1x1(torch.autograd.Function):
             else:
                 dx = dx2.view(xshape)
         if ctx.needs_input_grad[1]:
-            dw = torch.mm(dy2.t(), x2).view(K, C, 1, 1).to(wdt)
+            dw = _tall_wgrad(dy2, x2).view(K, C, 1, 1).to(wdt)
         if has_bias and ctx.needs_input_grad[2]:
             db = dy2.float().sum(0).to(wdt)
         return dx, dw, db, None

@@ -389,23 +389,30 @@ __global__ __launch_bounds__(256) void bn_stats_nhwc8(const T* __restrict__ x, l
       m2[j] = n > 0.f ? fmaxf(q[j] - s[j] * s[j] / n, 0.f) : 0.f;
     }
     if (G < 256) {
+      // tree over the RB row lanes of each channel group (pairs rl, rl + h): log2(RB) steps with
+      // every live lane merging, instead of G lanes merging RB - 1 partials one after another
       sn[t] = n;
 #pragma unroll
       for (int j = 0; j < 8; ++j) { sm[t][j] = mu[j]; sm2[t][j] = m2[j]; }
       __syncthreads();
-      if (t < G) {
-        for (int k = 1; k < RB; ++k) {
-          const int o = t + k * G;
+      int h = 1;
+      while (h < RB) h <<= 1;
+      for (h >>= 1; h >= 1; h >>= 1) {
+        if (rl < h && rl + h < RB && cg < G) {
+          const int o = t + h * G;
+          const float nb = sn[o];
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             float nn = n, mm = mu[j], qq = m2[j];
-            welford_merge(nn, mm, qq, sn[o], sm[o][j], sm2[o][j]);
+            welford_merge(nn, mm, qq, nb, sm[o][j], sm2[o][j]);
             mu[j] = mm; m2[j] = qq;
+            sm[t][j] = mm; sm2[t][j] = qq;
           }
-          n += sn[o];
+          n += nb;
+          sn[t] = n;
         }
+        __syncthreads();
       }
-      __syncthreads();
     }
     if (cg < G && rl == 0) {
 #pragma unroll
@@ -477,15 +484,25 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_nhwc8(const T* __restrict__
         for (int j = 0; j < 8; ++j) { s1[j] += g[j]; s2[j] += g[j] * (xv[j] - mu[j]); }
       }
     }
-    if (G < 256) {
+    if (G < 256) {  // tree over the RB row lanes (see bn_stats_nhwc8)
 #pragma unroll
       for (int j = 0; j < 8; ++j) { r1[t][j] = s1[j]; r2[t][j] = s2[j]; }
       __syncthreads();
-      if (t < G)
-        for (int k = 1; k < RB; ++k)
+      int h = 1;
+      while (h < RB) h <<= 1;
+      for (h >>= 1; h >= 1; h >>= 1) {
+        if (rl < h && rl + h < RB && cg < G) {
+          const int o = t + h * G;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) { s1[j] += r1[t + k * G][j]; s2[j] += r2[t + k * G][j]; }
-      __syncthreads();
+          for (int j = 0; j < 8; ++j) {
+            s1[j] += r1[o][j];
+            s2[j] += r2[o][j];
+            r1[t][j] = s1[j];
+            r2[t][j] = s2[j];
+          }
+        }
+        __syncthreads();
+      }
     }
     if (cg < G && rl == 0) {
 #pragma unroll

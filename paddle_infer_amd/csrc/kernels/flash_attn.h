@@ -60,6 +60,9 @@ struct FaArgs {
   long long smb, smh, smq;  // mask strides (elements; 0 = broadcast)
   float scale, p_drop;
   unsigned long long seed, offset;
+  int map;  // backward grid order, bit 0 dQ / bit 1 dK-dV kernel: 0 = the blocks of one (batch,
+            // head) spread over the grid, 1 = grouped on one XCD (fa_map) so they share that head's
+            // K/V (dQ) or Q/dO (dK-dV) panels in L2 (set by the entry point)
 };
 
 namespace fa {
@@ -570,8 +573,14 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(FaArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
   const int HB = Hk * B;
-  const int kb = (int)blockIdx.x / HB;  // causal: low key blocks see the most queries -> first
-  const int hk = (int)blockIdx.x % Hk, b = ((int)blockIdx.x % HB) / Hk;
+  // causal: low key blocks see the most queries -> first
+  int kb = (int)blockIdx.x / HB, hk = (int)blockIdx.x % Hk, b = ((int)blockIdx.x % HB) / Hk;
+  if (a.map & 2) {
+    int grp;
+    if (!fa_map((a.Sk + BK - 1) / BK, HB, grp, kb)) return;
+    hk = grp % Hk;
+    b = grp / Hk;
+  }
   const int n0 = kb * BK;
   int Sq = SqMax, Sk = a.Sk;
   long long lrow = (long long)b * Hq * SqMax, lhead = SqMax;  // stats index = lrow + hq*lhead + q
@@ -811,8 +820,15 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(FaArgs a) {
   const int l32 = lane & 31, hh = lane >> 5;
   const int nmb = (SqMax + BM - 1) / BM;
   const int HB = Hq * B;
-  const int mb = CAUSAL ? (nmb - 1 - (int)blockIdx.x / HB) : (int)blockIdx.x / HB;
-  const int hq = (int)blockIdx.x % Hq, b = ((int)blockIdx.x % HB) / Hq;
+  int mb = CAUSAL ? (nmb - 1 - (int)blockIdx.x / HB) : (int)blockIdx.x / HB;
+  int hq = (int)blockIdx.x % Hq, b = ((int)blockIdx.x % HB) / Hq;
+  if (a.map & 1) {  // grouped per (batch, head) on one XCD, heaviest query block first
+    int grp, sub;
+    if (!fa_map(nmb, HB, grp, sub)) return;
+    mb = CAUSAL ? nmb - 1 - sub : sub;
+    hq = grp % Hq;
+    b = grp / Hq;
+  }
   const int hk = hq / (Hq / Hk);
   const int m0 = mb * BM;
   int Sq = SqMax, Sk = a.Sk;
@@ -1036,6 +1052,20 @@ int launch_bwd_feat(const FaArgs& a, dim3 gkv, dim3 gq, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+// backward grid order (FaArgs::map). Measured at B96 S1024 H16 D128 causal: grouping the dQ
+// grid saves 7 % (954 -> 886 us) when the grid is large; at small grids (B8 S2048, 2k workgroups)
+// it loses 12 % to the tail, and grouping the dK/dV grid loses at both (profiles/fa_bwd_experiments_r3.txt).
+// PIAMD_FA_BWD_MAP=<bits> overrides.
+inline int fa_bwd_map(const FaArgs& a) {
+  static const int env = [] {
+    const char* e = getenv("PIAMD_FA_BWD_MAP");
+    return e ? atoi(e) : -1;
+  }();
+  if (env >= 0) return env;
+  const long long nq = (long long)((a.Sq + 127) / 128) * a.Hq * a.B;
+  return nq >= 8192 ? 1 : 0;
+}
+
 template <bool F16>
 int launch_bwd(const FaArgs& a, hipStream_t st) {
   // delta rows: padded [B, Hq, Sq]; packed [Hq, ltot] == the padded layout with B = 1, Sq = ltot
@@ -1043,7 +1073,8 @@ int launch_bwd(const FaArgs& a, hipStream_t st) {
   const int total = pB * a.Hq * pS;
   const int tpr = a.D > 64 ? 16 : 8;
   const int pre_blocks = (int)(((long long)total * tpr + 255) / 256);
-  const dim3 gkv(((a.Sk + 127) / 128) * a.Hk * a.B), gq(((a.Sq + 127) / 128) * a.Hq * a.B);
+  const long long nkv = (long long)((a.Sk + 127) / 128) * a.Hk * a.B, nq = (long long)((a.Sq + 127) / 128) * a.Hq * a.B;
+  const dim3 gkv = (a.map & 2) ? fa_grid(nkv) : dim3((unsigned)nkv), gq = (a.map & 1) ? fa_grid(nq) : dim3((unsigned)nq);
 #define BWD_D(DD)                                                                                  \
   hipLaunchKernelGGL((bwd_pre_kernel<DD, F16>), dim3(pre_blocks), dim3(256), 0, st,              \
                      (const unsigned short*)a.o, (const unsigned short*)a.dout, a.lse, a.delta,  \

@@ -24,6 +24,7 @@ static int fa_check(const FaArgs& a, bool fwd) {
 PIAMD_EXPORT int piamd_fa_fwd(const FaArgs* args, int f16, hipStream_t stream) {
   FaArgs a = *args;
   if (int e = fa_check(a, true)) return e;
+  a.map = 0;
   if (a.cu_q) a.sqb = a.skb = a.svb = a.sob = 0;
   if (a.B == 0 || a.Sq == 0) return 0;
   if (a.Sk == 0) return (int)hipErrorInvalidValue;
@@ -36,6 +37,7 @@ PIAMD_EXPORT int piamd_fa_fwd(const FaArgs* args, int f16, hipStream_t stream) {
 PIAMD_EXPORT int piamd_fa_bwd(const FaArgs* args, int f16, hipStream_t stream) {
   FaArgs a = *args;
   if (int e = fa_check(a, false)) return e;
+  a.map = fa::fa_bwd_map(a);
   if (a.cu_q) a.sqb = a.skb = a.svb = a.sob = 0;
   if (a.B == 0 || a.Sq == 0 || a.Sk == 0) return 0;
   return f16 ? fa_bwd_f16(a, stream) : fa::launch_bwd<false>(a, stream);

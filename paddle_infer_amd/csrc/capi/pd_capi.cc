@@ -92,13 +92,14 @@ bool check(PyObject* r, const char* where) {
   return false;
 }
 
+// Steals `args` (a new reference, e.g. from Py_BuildValue, or null): released here after the
+// call on every path, so no entry point leaks its argument tuple (and the handles it pins).
 PyObject* call_bridge(const char* fn, PyObject* args) {
   PyObject* b = bridge();
-  if (!b) return nullptr;
-  PyObject* f = PyObject_GetAttrString(b, fn);
-  if (!f) return nullptr;
-  PyObject* r = PyObject_CallObject(f, args);
-  Py_DECREF(f);
+  PyObject* f = b ? PyObject_GetAttrString(b, fn) : nullptr;
+  PyObject* r = f ? PyObject_CallObject(f, args) : nullptr;
+  Py_XDECREF(f);
+  Py_XDECREF(args);
   return r;
 }
 
@@ -181,7 +182,6 @@ void copy_from(PD_Tensor* t, const void* data, int code) {
   PyObject* buf = PyBytes_FromStringAndSize((const char*)data, (Py_ssize_t)(n * (long long)dtype_size(code)));
   PyObject* args = Py_BuildValue("(ONi)", t->obj, buf, code);
   PyObject* r = call_bridge("copy_from", args);
-  Py_XDECREF(args);
   check(r, "PD_TensorCopyFromCpu");
   Py_XDECREF(r);
 }
@@ -189,7 +189,6 @@ void copy_from(PD_Tensor* t, const void* data, int code) {
 void copy_to(PD_Tensor* t, void* data, int code) {
   PyObject* args = Py_BuildValue("(Oi)", t->obj, code);
   PyObject* r = call_bridge("copy_to", args);
-  Py_XDECREF(args);
   if (!check(r, "PD_TensorCopyToCpu")) return;
   char* p = nullptr;
   Py_ssize_t len = 0;

@@ -306,3 +306,65 @@ PIAMD_EXPORT int piamd_beam_search_softmax(
                      fuse_softmax, early_stop, length_penalty, max_seq_len, max_dec_len);
   return (int)hipGetLastError();
 }
+
+// Greedy decoding: out[r] = argmax_v logits[r, v] (ties → the smaller id, NaN ignored unless the
+// whole row is NaN, like torch.argmax on finite rows), one 1024-thread workgroup per row: each
+// lane keeps a running (max, id) over 16-B vector loads (8 bf16/fp16 or 4 f32), then one wave64
+// shuffle argmax per wave and a 16-entry LDS merge. One launch, no workspace, capturable.
+namespace {
+template <typename T>
+__device__ __forceinline__ float to_f(T v) { return (float)v; }
+__device__ __forceinline__ void amax_merge(float& v, int& i, float v2, int i2) {
+  if (v2 > v || (v2 == v && i2 < i)) { v = v2; i = i2; }
+}
+template <typename T, int VEC>
+__global__ __launch_bounds__(1024) void argmax_rows_kernel(const T* __restrict__ x, long long ld,
+                                                           int V, long long* __restrict__ out) {
+  const T* row = x + (long long)blockIdx.x * ld;
+  float best = -INFINITY;
+  int bid = 0x7fffffff;
+  const int nvec = V / VEC;
+  for (int c = threadIdx.x; c < nvec; c += 1024) {
+    typedef T TV __attribute__((ext_vector_type(VEC)));
+    const TV t = *reinterpret_cast<const TV*>(row + (long long)c * VEC);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) amax_merge(best, bid, to_f(t[j]), c * VEC + j);
+  }
+  for (int v = nvec * VEC + threadIdx.x; v < V; v += 1024) amax_merge(best, bid, to_f(row[v]), v);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float v2 = __shfl_xor(best, o, 64);
+    const int i2 = __shfl_xor(bid, o, 64);
+    amax_merge(best, bid, v2, i2);
+  }
+  __shared__ float sv[16];
+  __shared__ int si[16];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sv[w] = best; si[w] = bid; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < 16; ++k) amax_merge(best, bid, sv[k], si[k]);
+    out[blockIdx.x] = bid == 0x7fffffff ? 0 : bid;
+  }
+}
+}  // namespace
+
+// logits rows [R][ld] (dtype 0 f32, 1 bf16, 2 fp16), R ≥ 1, V ≥ 1 → out int64 [R]. Vector loads
+// need ld and the base 16-B aligned (the caller passes contiguous rows; else scalar path: VEC 1).
+PIAMD_EXPORT int piamd_argmax_rows(const void* x, long long ld, int R, int V, int dtype, long long* out,
+                                   hipStream_t st) {
+  if (R < 1 || V < 1 || dtype < 0 || dtype > 2) return (int)hipErrorInvalidValue;
+  const int esz = dtype == 0 ? 4 : 2;
+  const bool vec = ((uintptr_t)x % 16 == 0) && ((ld * esz) % 16 == 0);
+  if (dtype == 0) {
+    if (vec) hipLaunchKernelGGL((argmax_rows_kernel<float, 4>), dim3(R), dim3(1024), 0, st, (const float*)x, ld, V, out);
+    else hipLaunchKernelGGL((argmax_rows_kernel<float, 1>), dim3(R), dim3(1024), 0, st, (const float*)x, ld, V, out);
+  } else if (dtype == 1) {
+    if (vec) hipLaunchKernelGGL((argmax_rows_kernel<__bf16, 8>), dim3(R), dim3(1024), 0, st, (const __bf16*)x, ld, V, out);
+    else hipLaunchKernelGGL((argmax_rows_kernel<__bf16, 1>), dim3(R), dim3(1024), 0, st, (const __bf16*)x, ld, V, out);
+  } else {
+    if (vec) hipLaunchKernelGGL((argmax_rows_kernel<_Float16, 8>), dim3(R), dim3(1024), 0, st, (const _Float16*)x, ld, V, out);
+    else hipLaunchKernelGGL((argmax_rows_kernel<_Float16, 1>), dim3(R), dim3(1024), 0, st, (const _Float16*)x, ld, V, out);
+  }
+  return (int)hipGetLastError();
+}

@@ -141,7 +141,8 @@ class GPTGenerator:
     def sample(logits, strategy="greedy_search", top_k=0, top_p=1.0, temperature=1.0,
                generator=None):
         if strategy == "greedy_search":
-            return logits.argmax(-1)
+            from ..ops.search import argmax_rows
+            return argmax_rows(logits)
         lg = logits.float() / max(temperature, 1e-6)
         if top_k and top_k > 0:
             kth = torch.topk(lg, top_k, -1).values[:, -1:]
@@ -172,6 +173,9 @@ class GPTGenerator:
         out = torch.full((B, max_new_tokens), pad_token_id, dtype=torch.long, device=self.device)
         done = torch.zeros(B, dtype=torch.bool, device=self.device)
         pos = lens.to(torch.int32)
+        if decode_strategy == "greedy_search" and self.use_graph:
+            return self._greedy_graph_loop(logits, pos, out, done, max_new_tokens, eos_token_id,
+                                           pad_token_id)
         for t in range(max_new_tokens):
             tok = self.sample(logits, decode_strategy, top_k, top_p, temperature, gen)
             tok = torch.where(done, torch.full_like(tok, pad_token_id), tok)
@@ -183,6 +187,61 @@ class GPTGenerator:
             if t + 1 < max_new_tokens:
                 logits = self.decode(tok, pos)
                 pos = pos + 1
+        return out
+
+    def _greedy_graph_loop(self, logits, pos, out, done, max_new_tokens, eos, pad):
+        """Greedy decoding with the token choice INSIDE the captured step: one graph replay per
+        token runs the decoder, the argmax (own kernel), the EOS / pad bookkeeping and feeds the
+        chosen token and position back into its own static inputs — the host only copies the token
+        column out (same tokens as the eager loop)."""
+        from ..ops.search import argmax_rows
+        B = pos.shape[0]
+        tok = torch.where(done, torch.full_like(pos, pad, dtype=torch.long), argmax_rows(logits))
+        if eos is not None:
+            done = done | (tok == eos)
+
+        def load(st):
+            st["tok"].copy_(tok)
+            st["pos"].copy_(pos)
+            st["done"].copy_(done)
+            st["pad"].fill_(pad)
+        key = ("greedy", B, eos is not None)
+        ent = self._graphs.get(key)
+        if ent is None:
+            st = dict(tok=torch.zeros(B, dtype=torch.long, device=self.device),
+                      pos=torch.zeros(B, dtype=torch.int32, device=self.device),
+                      done=torch.zeros(B, dtype=torch.bool, device=self.device),
+                      eos=torch.tensor(eos if eos is not None else -1, device=self.device),
+                      pad=torch.tensor(pad, device=self.device))
+
+            def step():
+                lg = self._decode_eager(st["tok"], st["pos"], B)
+                nxt = torch.where(st["done"], st["pad"], argmax_rows(lg))
+                if eos is not None:
+                    st["done"].logical_or_(nxt == st["eos"])
+                st["tok"].copy_(nxt)
+                st["pos"].add_(1)
+            # warm-up from the real state: it writes the KV slots pos and pos + 1, which the real
+            # steps rewrite before anything reads them
+            load(st)
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    step()
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                step()
+            ent = self._graphs[key] = (g, st)
+        g, st = ent
+        load(st)
+        for t in range(max_new_tokens):
+            out[:, t].copy_(st["tok"])
+            if eos is not None and (t & 7) == 7 and bool(st["done"].all()):
+                break
+            if t + 1 < max_new_tokens:
+                g.replay()
         return out
 
     def _reorder(self, src, B):

@@ -220,6 +220,7 @@ _SIGS["piamd_pos_embedding_bwd"] = [c_void_p, c_void_p, c_int, c_int, c_int, c_i
 # logits, bf16, cum, seq_lens, stop, end_ids, step_ids, last_cache, last_offs, bs, beam, V,
 # max_seq_len, max_dec_len, fuse, early, penalty, P, part, ids, cum_out, cache, offs, parent,
 # stop_out, sl_out, st_out, stream
+_SIGS["piamd_argmax_rows"] = [c_void_p, c_ll, c_int, c_int, c_int, c_void_p, c_void_p]
 _SIGS["piamd_beam_search_softmax"] = ([c_void_p, c_int] + [c_void_p] * 7 + [c_int] * 7
                                       + [c_float, c_int] + [c_void_p] * 10)
 # x, ldx, wq, ldw, xs, xs_const, ws, bias, y, ldy, M, N, K, act, stream

@@ -104,6 +104,23 @@ def _reference(logits, cum_scores, seq_lens, stop_flags, end_ids, step_ids, last
             offs.reshape(last_beam_offsets.shape), parent, stop_out, sl_out, st_out)
 
 
+def argmax_rows(logits, out=None):
+    """Greedy token choice: int64 argmax over the last dim of [R, V] logits (ties → smaller id) in
+    one HIP launch (`search.hip` piamd_argmax_rows; hipGraph-capturable). CPU: torch.argmax."""
+    if not logits.is_cuda:
+        return logits.argmax(-1)
+    lg = logits if logits.stride(-1) == 1 else logits.contiguous()
+    lg2 = lg.reshape(-1, lg.shape[-1]) if lg.dim() != 2 else lg
+    code = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}.get(lg2.dtype)
+    if code is None:
+        return logits.argmax(-1)
+    R, V = lg2.shape
+    if out is None:
+        out = torch.empty(R, dtype=torch.int64, device=lg2.device)
+    _lib.call("piamd_argmax_rows", lg2.data_ptr(), lg2.stride(0), R, V, code, out.data_ptr(), _lib.stream())
+    return out.view(logits.shape[:-1])
+
+
 def beam_search_softmax(logits, cum_scores, sequence_lengths, stop_flags, end_ids, step_ids,
                         last_cache_ids, last_beam_offsets, beam_size, max_seq_len, max_dec_len,
                         fuse_softmax=True, early_stop=False, length_penalty=0.0,

@@ -208,6 +208,38 @@ def test_generation_hip_graph_matches_eager_and_fp32():
     assert torch.equal(a[:, :2].cpu(), ref[:, :2])
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("V", [50304, 1001, 7])
+def test_argmax_rows_matches_torch(dtype, V):
+    from paddle_infer_amd.ops.search import argmax_rows
+    torch.manual_seed(V)
+    x = torch.randn(5, V, device=DEV).to(dtype)
+    x[1, :] = 0.0                      # all ties -> index 0
+    x[2, V // 2] = x[2, V - 1] = 100.  # tie between two maxima -> the smaller index
+    got = argmax_rows(x)
+    assert got.dtype == torch.int64
+    assert torch.equal(got.cpu(), x.float().argmax(-1).cpu())
+    sub = x[:, : V - 1]  # a row stride that is not 16-B aligned (scalar path)
+    assert torch.equal(argmax_rows(sub).cpu(), sub.float().argmax(-1).cpu())
+
+
+def test_generation_greedy_graph_eos_and_reuse():
+    """Greedy decoding with the token choice inside the graph: EOS handling and a second call
+    through the cached graph reproduce the eager loop."""
+    from paddle_infer_amd.inference.generation import GPTGenerator
+    m = _tiny_gpt("float32").to(DEV).to(torch.bfloat16)
+    ids = torch.randint(0, 1024, (2, 7))
+    g_graph = GPTGenerator(m, max_batch=4, max_seq_len=64, use_hip_graph=True)
+    g_eager = GPTGenerator(m, max_batch=4, max_seq_len=64, use_hip_graph=False)
+    ref = g_eager.generate(ids, max_new_tokens=10)
+    eos = int(ref[0, 3])
+    a = g_eager.generate(ids, max_new_tokens=10, eos_token_id=eos, pad_token_id=0)
+    for _ in range(2):
+        b = g_graph.generate(ids, max_new_tokens=10, eos_token_id=eos, pad_token_id=0)
+        assert torch.equal(a.cpu(), b.cpu()), (a, b)
+    assert torch.equal(g_graph.generate(ids, max_new_tokens=10).cpu(), ref.cpu())
+
+
 def test_predictor_bf16_hip_graph(tmp_path):
     import numpy as np
     import paddle_infer_amd as paddle

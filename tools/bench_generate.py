@@ -60,7 +60,16 @@ def main():
                 tok = logits.argmax(-1)
             torch.cuda.synchronize()
             t_dec = time.perf_counter() - t0
+            # end-to-end greedy generate(): prefill + (gen - 1) decode steps with the token choice
+            # (inside the captured step for graph modes)
+            gen.generate(ids, lens, max_new_tokens=a.gen)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            gen.generate(ids, lens, max_new_tokens=a.gen)
+            torch.cuda.synchronize()
+            t_gen = time.perf_counter() - t0
             r = {"mode": mode, "batch": B, "prompt": a.prompt, "gen": a.gen,
+                 "generate_decode_ms_per_step": round((t_gen - t_pre) / max(1, a.gen - 1) * 1e3, 4),
                  "prefill_ms": round(t_pre * 1e3, 3),
                  "prefill_tok_s": round(B * a.prompt / t_pre, 1),
                  "decode_ms_per_step": round(t_dec / a.gen * 1e3, 4),

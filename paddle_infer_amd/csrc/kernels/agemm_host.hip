@@ -175,8 +175,13 @@ PIAMD_EXPORT int piamd_agemm(const void* a, long long lda, int trans_a, const vo
   g.nwg = (unsigned)nwg;
   g.grid = persistent ? (unsigned)std::min<long long>(nwg, num_cus()) : (unsigned)nwg;
   g.rcp_ntiles = 1.0f / (float)g.ntiles;
-  g.gm = GROUP_M;
-  g.per_group = GROUP_M * g.tiles_n;
+  static const int group_m = [] {  // PIAMD_AGEMM_GM: m-tiles per tile group (A/B experiments)
+    const char* e = getenv("PIAMD_AGEMM_GM");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : GROUP_M;
+  }();
+  g.gm = group_m;
+  g.per_group = group_m * g.tiles_n;
   g.rcp_per_group = 1.0f / (float)g.per_group;
   g.act = act;
   g.aux = aux;

@@ -1,0 +1,418 @@
+// Persistent whole-stack decode step ("megakernel") for batch-1 GPT decoding on gfx950.
+//
+// Why: the batch-1 decode step is a chain of 5 small launches per layer (QKV GEMV → attention →
+// out GEMV → FFN1 GEMV → FFN2 GEMV). Each GEMV streams 8-33 MB of weights and sits at its ramp
+// floor (profiles/gemv_decode_r3_nt.txt: 25 MB in ≈9 µs ≈ 2.8 TB/s) — HBM idles while a launch
+// drains and the next ramps up. Weights do not depend on activations, so one persistent kernel
+// can load the NEXT projection's weights while the current phase finishes and the grid syncs.
+//
+// Design (one launch per token for all layers):
+//   * grid = 256 workgroups (one per CU, 1 wave-slot of LDS each) × 256 threads; every GEMV phase
+//     splits its N output columns evenly: WG w owns rows [w·NPW, (w+1)·NPW) of the [N][K] (out, in)
+//     weight, a CONTIGUOUS slice of ≤ 128 KiB that lives in LDS.
+//   * waves 1..3 are loaders: right after a phase has consumed its LDS slice they issue the next
+//     phase's slice with direct-to-LDS DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction),
+//     while wave 0 publishes the phase's outputs and waits on the grid barrier — the weight stream
+//     overlaps the barrier instead of following it. (A wave's loads retire in order, so the
+//     barrier-polling wave must not own prefetches; hence the loader / control split.)
+//   * cross-workgroup data (residual, q / new k,v, attention partials, FFN hidden) is published
+//     with agent-scope relaxed atomic stores and read with agent-scope atomic loads (coherent
+//     across the 8 per-XCD L2s without L2 write-back fences, see xcd_* in common.h); the barrier
+//     is a monotonically increasing arrival counter (zeroed by the launcher) polled by one lane
+//     with s_sleep back-off and a bounded spin: on timeout the kernel raises `err` and runs to
+//     completion, so every wave always exits.
+//   * per layer: LN1 (recomputed per WG from the residual, 8 KB from L2) + QKV GEMV + bias, new
+//     k/v written to the cache → split-K attention over the cache (16 lanes per key row, base-2
+//     softmax) → partial combine + out GEMV + bias + residual → LN2 + FFN1 GEMV + bias + GELU →
+//     FFN2 GEMV + bias + residual. Rounding points match the launch-per-op path (bf16 LN output,
+//     bf16 cache / attention output / hidden / residual).
+// Shapes: E = 2048, D = 128, Hq = Hk = 16, F = 8192 (GPT-1.3B width; any depth / context);
+// the host launcher rejects anything else and the Python side falls back to the per-op path.
+// Reference parity: one decode step of FusedMultiTransformer with time_step
+// (`paddle/fluid/operators/fused/fused_multi_transformer_op.cu`, masked_multihead_attention).
+#include "common.h"
+
+namespace {
+
+constexpr int NT = 256;                // threads per workgroup (4 waves)
+constexpr int NWG = 256;               // workgroups (one per CU)
+constexpr int E = 2048, D = 128, HQ = 16, HK = 16, F = 8192;
+constexpr int NQKV = (HQ + 2 * HK) * D;  // 6144
+constexpr int WBYTES = 128 * 1024;     // LDS weight slice
+constexpr int PSTRIDE = D + 2;         // attention partial: acc[D], m, l
+
+typedef unsigned long long u64;
+
+struct MegaLayer {
+  const bf16_t *ln1_g, *ln1_b, *wqkv, *bqkv, *wo, *bo, *ln2_g, *ln2_b, *w1, *b1, *w2, *b2;
+  bf16_t *kc, *vc;
+};
+
+struct MegaArgs {
+  const MegaLayer* layers;
+  int nl;
+  int maxS;
+  int nsplit;
+  int act;  // 0 gelu (erf), 1 gelu (tanh)
+  float eps;
+  float scale_log2;
+  bf16_t* resid;      // [E] residual stream, updated in place
+  float* qn;          // [HQ·D] q + bias
+  float* kvn;         // [2·HK·D] new k, v (+bias, bf16-rounded)
+  float* part;        // [HQ][nsplit][PSTRIDE]
+  bf16_t* h;          // [F] FFN hidden
+  unsigned* bar;      // arrival counter (zeroed by the launcher)
+  int* err;           // 1 = a grid barrier timed out
+  const int* pos;     // [1] cache slot of the new token
+  u64* trace;         // nullable: [NWG][5·nl][2] wall-clock (100 MHz) at phase start / arrival
+};
+
+__device__ __forceinline__ u64 ld64(const void* p) {
+  return __hip_atomic_load((u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st64(void* p, u64 v) {
+  __hip_atomic_store((u64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ldf(const float* p) {
+  return __hip_atomic_load((float*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ u64 pack2f(float a, float b) {
+  return (u64)__float_as_uint(a) | ((u64)__float_as_uint(b) << 32);
+}
+// 8 bf16 at p (16 B aligned) published by other workgroups → f32
+__device__ __forceinline__ void ld_bf8(const bf16_t* p, float* v) {
+  const u64 a = ld64(p), b = ld64(p + 4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[i] = bf2f((bf16_t)(a >> (16 * i)));
+    v[4 + i] = bf2f((bf16_t)(b >> (16 * i)));
+  }
+}
+
+// Wave 0 only: this wave's publishing stores have completed → arrive → poll until every
+// workgroup has arrived `target / NWG` times.
+__device__ __forceinline__ void grid_sync(const MegaArgs& a, unsigned target, int lane) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (a.trace && lane == 0) a.trace[((long)blockIdx.x * a.nl * 5 + target / NWG - 1) * 2 + 1] = wall_clock64();
+  if (lane == 0) {
+    __hip_atomic_fetch_add(a.bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    while (__hip_atomic_load(a.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((++spins & 1023) == 0) {  // bounded: one timeout makes every later barrier fall through
+        if (spins > (1u << 21) || __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+  }
+}
+
+// Loader waves: DMA `bytes` (multiple of 1 KiB) from `src` into the LDS slice.
+__device__ __forceinline__ void prefetch(const bf16_t* src, int bytes, char* wl, int wv, int lane) {
+  if (wv == 0) return;
+  const char* s = reinterpret_cast<const char*>(src) + lane * 16;
+  for (int p = wv - 1; p < (bytes >> 10); p += 3)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(s + p * 1024),
+                                     (__attribute__((address_space(3))) void*)(wl + p * 1024), 16, 0, 0);
+}
+
+// Phase entry: loader waves wait for their DMA, then the whole workgroup meets (wave 0 arrives
+// here after its grid barrier).
+__device__ __forceinline__ void phase_start(const MegaArgs& a, int wv, unsigned ph) {
+  if (wv != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (a.trace && threadIdx.x == 0) a.trace[((long)blockIdx.x * a.nl * 5 + ph) * 2] = wall_clock64();
+}
+
+// y[c] = Σ_k x[k]·W[c][k] for the NPW columns of this workgroup's LDS slice ([NPW][K] bf16);
+// thread t holds x[k] for k = (j·256 + t)·8 + i. Returns column `tid`'s sum for tid < NPW.
+// Reduction: a butterfly that halves the live columns per exchange (log2 P steps, P−1 shuffles
+// instead of 6·P), then 4 waves through LDS.
+template <int NPW, int KCH>
+__device__ __forceinline__ float gemv_lds(const char* wl, const float (&x)[KCH][8], float* red,
+                                          int tid) {
+  constexpr int K = 2048 * KCH;
+  constexpr int P = NPW <= 8 ? 8 : 32;
+  constexpr int LOGP = P == 8 ? 3 : 5;
+  const int lane = tid & 63, wv = tid >> 6;
+  float acc[P];
+#pragma unroll
+  for (int c = 0; c < P; ++c) acc[c] = 0.f;
+#pragma unroll
+  for (int c = 0; c < NPW; ++c) {
+#pragma unroll
+    for (int j = 0; j < KCH; ++j) {
+      const u16x8 w = *reinterpret_cast<const u16x8*>(wl + ((long)c * K + (j * 256 + tid) * 8) * 2);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[c] += x[j][i] * bf2f(w[i]);
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < LOGP; ++s) {
+    const int o = 32 >> s;
+    const bool up = (lane & o) != 0;
+#pragma unroll
+    for (int i = 0; i < (P >> (s + 1)); ++i) {
+      const int hi = i + (P >> (s + 1));
+      const float mine = up ? acc[hi] : acc[i];
+      const float oth = up ? acc[i] : acc[hi];
+      acc[i] = mine + __shfl_xor(oth, o, 64);
+    }
+  }
+#pragma unroll
+  for (int o = 32 >> LOGP; o > 0; o >>= 1) acc[0] += __shfl_xor(acc[0], o, 64);
+  if ((lane & ((64 >> LOGP) - 1)) == 0) red[wv * P + (lane >> (6 - LOGP))] = acc[0];
+  __syncthreads();
+  float r = 0.f;
+  if (tid < NPW) r = red[tid] + red[P + tid] + red[2 * P + tid] + red[3 * P + tid];
+  return r;
+}
+
+// x = bf16(LN(resid)) for this thread's 8 elements k = 8·tid.
+__device__ __forceinline__ void ln_prologue(const MegaArgs& a, const bf16_t* g, const bf16_t* b,
+                                            float (&x)[1][8], float* wred, int tid) {
+  float v[8];
+  ld_bf8(a.resid + tid * 8, v);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s += v[i];
+  const float mean = block_sum<4>(s, wred) * (1.f / E);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) q += (v[i] - mean) * (v[i] - mean);
+  const float rs = rsqrtf(block_sum<4>(q, wred) * (1.f / E) + a.eps);
+  const u16x8 gg = *reinterpret_cast<const u16x8*>(g + tid * 8);
+  const u16x8 bb = *reinterpret_cast<const u16x8*>(b + tid * 8);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) x[0][i] = bf2f(f2bf((v[i] - mean) * rs * bf2f(gg[i]) + bf2f(bb[i])));
+}
+
+// Lanes 0..NC-1 of wave 0 each hold one bf16 `y`; publish them as NC/4 64-bit stores at dst.
+// Every lane of the wave must call this (shuffles).
+__device__ __forceinline__ void publish_bf16(bf16_t* dst, float y, int lane, int NC) {
+  const unsigned u = (unsigned)f2bf(y);
+  const unsigned pair = u | ((unsigned)__shfl_down((int)u, 1, 64) << 16);
+  const unsigned pair2 = (unsigned)__shfl_down((int)pair, 2, 64);
+  if (lane < NC && (lane & 3) == 0) st64(dst + lane, (u64)pair | ((u64)pair2 << 32));
+}
+
+__global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
+  __shared__ __attribute__((aligned(1024))) char wl[WBYTES];
+  __shared__ float red[4 * 32];
+  __shared__ float wred[8];
+  __shared__ float sc[256];
+  __shared__ float pv[4][D];
+  __shared__ float qs[D];
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, w = blockIdx.x;
+  const int pos = a.pos[0], L = pos + 1;
+  unsigned nbar = 0;
+  constexpr int NPQ = NQKV / NWG, NPO = E / NWG, NP1 = F / NWG, NP2 = E / NWG;
+
+  prefetch(a.layers[0].wqkv + (long)w * NPQ * E, NPQ * E * 2, wl, wv, lane);
+  for (int l = 0; l < a.nl; ++l) {
+    const MegaLayer& Ly = a.layers[l];
+    // ---------------------------------------------------------------- QKV
+    phase_start(a, wv, nbar);
+    {
+      float x[1][8];
+      ln_prologue(a, Ly.ln1_g, Ly.ln1_b, x, wred, tid);
+      const float y = gemv_lds<NPQ, 1>(wl, x, red, tid);
+      prefetch(Ly.wo + (long)w * NPO * E, NPO * E * 2, wl, wv, lane);
+      if (wv == 0) {
+        if (lane < NPQ) {
+          const int col = w * NPQ + lane;
+          const float v = bf2f(f2bf(y)) + bf2f(Ly.bqkv[col]);
+          if (col < HQ * D) {
+            __hip_atomic_store(a.qn + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else {
+            const int kv = col - HQ * D;          // [0, 2·HK·D)
+            const int which = kv / (HK * D), r = kv % (HK * D), kh = r / D, d = r % D;
+            const bf16_t vb = f2bf(v);
+            bf16_t* cache = which ? Ly.vc : Ly.kc;
+            cache[((long)kh * a.maxS + pos) * D + d] = vb;
+            __hip_atomic_store(a.kvn + kv, bf2f(vb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+        grid_sync(a, (++nbar) * NWG, lane);
+      } else {
+        ++nbar;
+      }
+    }
+    // ---------------------------------------------------------------- attention
+    phase_start(a, wv, nbar);
+    if (w < HQ * a.nsplit) {
+      const int h = w / a.nsplit, s = w % a.nsplit, kh = h / (HQ / HK);
+      const int chunk = (L + a.nsplit - 1) / a.nsplit;
+      const int j0 = s * chunk, n = min(L, j0 + chunk) - j0;
+      const int sub = tid & 15, kslot = tid >> 4;  // 16 lanes per key row, 16 rows in flight
+      const long kvbase = (long)kh * a.maxS * D;
+      float q[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) q[i] = ldf(a.qn + h * D + sub * 8 + i) * a.scale_log2;
+      auto row = [&](const bf16_t* cache, int which, int j, float* r) {
+        if (j == pos) {
+          const float* p = a.kvn + which * HK * D + kh * D + sub * 8;
+#pragma unroll
+          for (int i = 0; i < 8; i += 2) {
+            const u64 u = ld64(p + i);
+            r[i] = __uint_as_float((unsigned)u);
+            r[i + 1] = __uint_as_float((unsigned)(u >> 32));
+          }
+        } else {
+          const u16x8 u = *reinterpret_cast<const u16x8*>(cache + kvbase + (long)j * D + sub * 8);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) r[i] = bf2f(u[i]);
+        }
+      };
+      for (int i = kslot; i < n; i += 16) {
+        float k[8];
+        row(Ly.kc, 0, j0 + i, k);
+        float d = 0.f;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) d += q[t] * k[t];
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+        if (sub == 0) sc[i] = d;
+      }
+      __syncthreads();
+      const float sv = tid < n ? sc[tid] : -INFINITY;
+      const float m = block_max<4>(sv, wred);
+      const float p = tid < n ? exp2f(sv - m) : 0.f;
+      const float lsum = block_sum<4>(p, wred);
+      if (tid < n) sc[tid] = p;
+      __syncthreads();
+      float acc[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc[t] = 0.f;
+      for (int i = kslot; i < n; i += 16) {
+        float v[8];
+        row(Ly.vc, 1, j0 + i, v);
+        const float pi = sc[i];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[t] += pi * v[t];
+      }
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        acc[t] += __shfl_xor(acc[t], 16, 64);
+        acc[t] += __shfl_xor(acc[t], 32, 64);
+      }
+      if (lane < 16) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) pv[wv][sub * 8 + t] = acc[t];
+      }
+      __syncthreads();
+      if (wv == 0) {
+        float* dst = a.part + (long)(h * a.nsplit + s) * PSTRIDE;
+        const int d0 = lane * 2;
+        const float v0 = pv[0][d0] + pv[1][d0] + pv[2][d0] + pv[3][d0];
+        const float v1 = pv[0][d0 + 1] + pv[1][d0 + 1] + pv[2][d0 + 1] + pv[3][d0 + 1];
+        st64(dst + d0, pack2f(n > 0 ? v0 : 0.f, n > 0 ? v1 : 0.f));
+        if (lane == 0) st64(dst + D, pack2f(n > 0 ? m : -INFINITY, n > 0 ? lsum : 0.f));
+      }
+    }
+    if (wv == 0) grid_sync(a, (++nbar) * NWG, lane); else ++nbar;
+    // ---------------------------------------------------------------- out projection
+    phase_start(a, wv, nbar);
+    {
+      float x[1][8];
+      {
+        const int h = tid >> 4, d0 = (tid & 15) * 8;
+        const float* base = a.part + (long)h * a.nsplit * PSTRIDE;
+        float M = -INFINITY;
+        for (int s = 0; s < a.nsplit; ++s) M = fmaxf(M, ldf(base + s * PSTRIDE + D));
+        float lt = 0.f, o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = 0.f;
+        for (int s = 0; s < a.nsplit; ++s) {
+          const u64 ml = ld64(base + s * PSTRIDE + D);
+          const float ms = __uint_as_float((unsigned)ml);
+          if (ms == -INFINITY) continue;
+          const float e = exp2f(ms - M);
+          lt += e * __uint_as_float((unsigned)(ml >> 32));
+#pragma unroll
+          for (int i = 0; i < 8; i += 2) {
+            const u64 u = ld64(base + s * PSTRIDE + d0 + i);
+            o[i] += e * __uint_as_float((unsigned)u);
+            o[i + 1] += e * __uint_as_float((unsigned)(u >> 32));
+          }
+        }
+        const float inv = 1.f / lt;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[0][i] = bf2f(f2bf(o[i] * inv));
+      }
+      const float y = gemv_lds<NPO, 1>(wl, x, red, tid);
+      prefetch(Ly.w1 + (long)w * NP1 * E, NP1 * E * 2, wl, wv, lane);
+      if (wv == 0) {
+        const int col = w * NPO + (lane & (NPO - 1));
+        const u64 r4 = ld64(a.resid + (col & ~3));
+        const float r = bf2f((bf16_t)(r4 >> (16 * (col & 3))));
+        publish_bf16(a.resid + w * NPO, y + bf2f(Ly.bo[col]) + r, lane, NPO);
+        grid_sync(a, (++nbar) * NWG, lane);
+      } else {
+        ++nbar;
+      }
+    }
+    // ---------------------------------------------------------------- FFN1
+    phase_start(a, wv, nbar);
+    {
+      float x[1][8];
+      ln_prologue(a, Ly.ln2_g, Ly.ln2_b, x, wred, tid);
+      const float y = gemv_lds<NP1, 1>(wl, x, red, tid);
+      prefetch(Ly.w2 + (long)w * NP2 * F, NP2 * F * 2, wl, wv, lane);
+      if (wv == 0) {
+        const int col = w * NP1 + (lane & (NP1 - 1));
+        const float t = y + bf2f(Ly.b1[col]);
+        publish_bf16(a.h + w * NP1, a.act ? gelu_tanh(t) : gelu_erf(t), lane, NP1);
+        grid_sync(a, (++nbar) * NWG, lane);
+      } else {
+        ++nbar;
+      }
+    }
+    // ---------------------------------------------------------------- FFN2
+    phase_start(a, wv, nbar);
+    {
+      float x[4][8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ld_bf8(a.h + (j * 256 + tid) * 8, x[j]);
+      const float y = gemv_lds<NP2, 4>(wl, x, red, tid);
+      if (l + 1 < a.nl) prefetch(a.layers[l + 1].wqkv + (long)w * NPQ * E, NPQ * E * 2, wl, wv, lane);
+      if (wv == 0) {
+        const int col = w * NP2 + (lane & (NP2 - 1));
+        const u64 r4 = ld64(a.resid + (col & ~3));
+        const float r = bf2f((bf16_t)(r4 >> (16 * (col & 3))));
+        publish_bf16(a.resid + w * NP2, y + bf2f(Ly.b2[col]) + r, lane, NP2);
+        if (l + 1 < a.nl) grid_sync(a, (++nbar) * NWG, lane);
+      } else {
+        ++nbar;
+      }
+    }
+  }
+  if (wv != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+}  // namespace
+
+// Launch one decode step over `nl` layers (see the header comment for the supported shapes).
+// `layers` is a device array of MegaLayer; scratch buffers per MegaArgs. Returns hipError_t.
+PIAMD_EXPORT int piamd_decode_mega(const MegaArgs* args, int E_, int D_, int hq, int hk, int F_,
+                                   hipStream_t st) {
+  static int cus = -1;
+  if (cus < 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 0;
+  }
+  const MegaArgs& a = *args;
+  if (cus < NWG || E_ != E || D_ != D || hq != HQ || hk != HK || F_ != F || a.nl < 1 ||
+      a.nsplit < 1 || HQ * a.nsplit > NWG || (a.maxS + a.nsplit - 1) / a.nsplit > 256 || !a.layers ||
+      !a.resid || !a.qn || !a.kvn || !a.part || !a.h || !a.bar || !a.err || !a.pos)
+    return (int)hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(a.bar, 0, sizeof(unsigned), st);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(decode_mega_kernel, dim3(NWG), dim3(NT), 0, st, a);
+  return (int)hipGetLastError();
+}

@@ -68,6 +68,7 @@ class GPTGenerator:
                        for _ in self.layers]
         self.use_graph = use_hip_graph and self.device.type == "cuda"
         self._graphs = {}
+        self._mega = None  # MegaDecoder, built on the first eligible batch-1 decode step
 
     # ------------------------------------------------------------------------------ model
     def _mp_gather(self, logits):
@@ -105,7 +106,23 @@ class GPTGenerator:
         last = y[torch.arange(B, device=y.device), lengths.long() - 1]
         return self._logits(last)
 
+    def _mega_decoder(self, B):
+        """The single-launch decode step (inference/mega_decode.py) when this model / batch fits
+        it, else None (per-op path)."""
+        from . import mega_decode
+        if self._mega is None:
+            self._mega = mega_decode.MegaDecoder(self) if mega_decode.eligible(self, 1) else False
+        return self._mega if (self._mega and B == 1 and mega_decode.eligible(self, B)) else None
+
     def _decode_eager(self, tok, pos, B):
+        mega = self._mega_decoder(B)
+        if mega is not None:
+            from ..ops.norm import layer_norm
+            resid = self.model.gpt.embeddings(tok.view(1, 1), pos.long().view(1, 1))
+            resid = resid.reshape(-1).contiguous()
+            mega(resid, pos)
+            y = layer_norm(resid.view(1, -1), *self.final_ln)
+            return self._logits(y)
         lens = pos + 1
         y = self._forward(tok.view(B, 1), pos, lens, B, decode=True)
         return self._logits(y.view(B, -1))

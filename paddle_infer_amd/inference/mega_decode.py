@@ -1,0 +1,107 @@
+"""Single-launch batch-1 decode step: the whole layer stack in one persistent HIP kernel.
+
+``csrc/kernels/decode_mega.hip`` runs LN → QKV GEMV → cache write + attention → out GEMV +
+residual → LN → FFN1 + GELU → FFN2 + residual for every layer in ONE launch: 256 workgroups (one
+per CU) hand activations to each other through a grid barrier, and each workgroup streams its
+slice of the next projection's weights into LDS while the barrier settles, so the weight stream
+no longer pays a launch ramp per GEMV (5 per layer on the per-op path).
+
+Parity: one ``FusedMultiTransformer`` decode step with ``time_step``
+(`paddle/fluid/operators/fused/fused_multi_transformer_op.cu`); the per-op path
+(``incubate.nn.functional.multi_transformer_forward(decode=True)``) stays the reference and the
+fallback for shapes the kernel does not take (batch > 1, other widths, weight-only / TP / RoPE).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+
+import torch
+
+from ..ops import _lib
+
+E, D, HQ, HK, F = 2048, 128, 16, 16, 8192
+# default for PIAMD_DECODE_MEGA (1 = batch-1 decode steps run the single-launch kernel)
+DEFAULT = "0"
+
+
+def eligible(gen, B: int) -> bool:
+    """True when generator ``gen``'s decode step at batch ``B`` can run as one launch."""
+    if os.environ.get("PIAMD_DECODE_MEGA", DEFAULT) == "0":
+        return False
+    if B != 1 or gen.device.type != "cuda" or gen.dtype != torch.bfloat16 or gen.group is not None:
+        return False
+    cfg = gen.cfg
+    if (cfg.hidden_size, gen.D, gen.H, gen.Hk) != (E, D, HQ, HK) or gen.max_seq_len > 256 * 16:
+        return False
+    if getattr(cfg, "ffn", F) != F or getattr(cfg, "rotary_dim", 0):
+        return False
+    for spec in gen.layers:
+        for key in ("qkv", "out", "ffn1", "ffn2"):
+            lin = spec[key]
+            if lin.bits or lin.w.dtype != torch.bfloat16:
+                return False
+        for key in ("ln_scale", "ln_bias", "ffn_ln_scale", "ffn_ln_bias", "qkv_bias", "out_bias",
+                    "ffn1_bias", "ffn2_bias"):
+            t = spec.get(key)
+            if t is None or t.dtype != torch.bfloat16:
+                return False
+    return _lib.available() and _lib.has("piamd_decode_mega")
+
+
+def _out_in(lin):
+    """[out, in] contiguous bf16 copy of a projection (each workgroup's slice is then one
+    contiguous run of rows)."""
+    w = lin.w.detach()
+    return (w if lin.trans else w.t()).contiguous()
+
+
+class MegaDecoder:
+    """Owns the [out, in] weight copies, the per-layer pointer table and the scratch buffers."""
+
+    def __init__(self, gen):
+        dev = gen.device
+        self.gen = gen
+        self._keep = []
+        rows = []
+        for spec, (kc, vc) in zip(gen.layers, gen.caches):
+            ws = [_out_in(spec[k]) for k in ("qkv", "out", "ffn1", "ffn2")]
+            ts = [spec["ln_scale"], spec["ln_bias"], ws[0], spec["qkv_bias"], ws[1], spec["out_bias"],
+                  spec["ffn_ln_scale"], spec["ffn_ln_bias"], ws[2], spec["ffn1_bias"], ws[3],
+                  spec["ffn2_bias"], kc, vc]
+            ts = [t.contiguous() for t in ts]
+            self._keep += ts
+            rows.append([t.data_ptr() for t in ts])
+        self.table = torch.tensor(rows, dtype=torch.int64, device=dev)
+        self.nl = len(rows)
+        self.maxS = gen.max_seq_len
+        self.nsplit = max(1, math.ceil(self.maxS / 256))
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.qn = torch.zeros(HQ * D, **f32)
+        self.kvn = torch.zeros(2 * HK * D, **f32)
+        self.part = torch.zeros(HQ * self.nsplit * (D + 2), **f32)
+        self.h = torch.zeros(F, dtype=torch.bfloat16, device=dev)
+        self.bar = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.act = 1 if gen.act == "gelu_tanh" else 0
+        self.eps = float(gen.cfg.layer_norm_eps)
+        self.trace = None  # set to a zeroed int64 [256, 5·nl, 2] tensor to record phase times
+
+    def __call__(self, resid: torch.Tensor, pos: torch.Tensor) -> torch.Tensor:
+        """resid: bf16 [E] (embedding output; updated in place to the last layer's residual);
+        pos: device int32 [1] = the cache slot of this token."""
+        assert resid.is_contiguous() and resid.numel() == E and resid.dtype == torch.bfloat16
+        assert pos.dtype == torch.int32 and pos.is_cuda
+        a = _lib.MegaArgs(self.table.data_ptr(), self.nl, self.maxS, self.nsplit, self.act,
+                          self.eps, (1.0 / math.sqrt(D)) * 1.4426950408889634, resid.data_ptr(),
+                          self.qn.data_ptr(), self.kvn.data_ptr(), self.part.data_ptr(),
+                          self.h.data_ptr(), self.bar.data_ptr(), self.err.data_ptr(),
+                          pos.data_ptr(), _lib.ptr(self.trace))
+        _lib.call("piamd_decode_mega", ctypes.byref(a), E, D, HQ, HK, F, _lib.stream())
+        return resid
+
+    def check(self) -> None:
+        """Raise if a grid barrier of an earlier launch timed out (synchronises)."""
+        if int(self.err.item()):
+            raise RuntimeError("decode_mega: a grid barrier timed out (workgroups not co-resident?)")

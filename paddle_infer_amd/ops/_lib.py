@@ -87,6 +87,15 @@ class FaArgs(ctypes.Structure):
                    ("offset", c_u64), ("map", c_int)])
 
 
+class MegaArgs(ctypes.Structure):
+    """Mirror of ``struct MegaArgs`` (csrc/kernels/decode_mega.hip)."""
+    _fields_ = ([("layers", c_void_p)] + [(n, c_int) for n in ("nl", "maxS", "nsplit", "act")]
+                + [("eps", ctypes.c_float), ("scale_log2", ctypes.c_float)]
+                + [(n, c_void_p) for n in ("resid", "qn", "kvn", "part", "h", "bar", "err", "pos",
+                                        "trace")])
+
+
+_SIGS["piamd_decode_mega"] = [ctypes.POINTER(MegaArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]
 _SIGS["piamd_fa_fwd"] = [ctypes.POINTER(FaArgs), c_int, c_void_p]
 _SIGS["piamd_fa_bwd"] = [ctypes.POINTER(FaArgs), c_int, c_void_p]
 _SIGS["piamd_layernorm_bwd_ws"] = [c_int, c_int]

@@ -1,0 +1,72 @@
+"""Phase timeline of the single-launch decode step (csrc/kernels/decode_mega.hip).
+
+Runs a GPT-1.3B-shaped generator (random init) at batch 1, records the per-workgroup wall-clock
+(100 MHz) at every phase start and grid-barrier arrival, and prints per phase kind: the median
+and max in-phase work, the barrier release latency (first release − last arrival) and the
+phase period. Usage: python tools/mega_trace.py [--layers 24] [--prompt 128]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+KINDS = ["qkv", "attn", "out", "ffn1", "ffn2"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--layers", type=int, default=24)
+    ap.add_argument("--prompt", type=int, default=128)
+    ap.add_argument("--steps", type=int, default=8)
+    args = ap.parse_args()
+    import paddle_infer_amd as paddle
+    from paddle_infer_amd.inference.generation import GPTGenerator
+    from paddle_infer_amd.models.gpt import GPTForPretraining, gpt_config
+    paddle.seed(1)
+    cfg = gpt_config("gpt3-1.3b", num_layers=args.layers, hidden_dropout_prob=0.0)
+    m = GPTForPretraining(cfg).cuda().to(torch.bfloat16).eval()
+    gen = GPTGenerator(m, max_batch=1, max_seq_len=1024, use_hip_graph=False)
+    ids = torch.randint(0, cfg.vocab_size, (1, args.prompt), device="cuda")
+    logits = gen.prefill(ids, torch.full((1,), args.prompt, device="cuda"))
+    pos = torch.full((1,), args.prompt, dtype=torch.int32, device="cuda")
+    nl = args.layers
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    times = []
+    for step in range(args.steps):
+        tok = logits.argmax(-1)
+        if step == args.steps - 1:
+            gen._mega.trace = torch.zeros(256, 5 * nl, 2, dtype=torch.int64, device="cuda")
+        ev[0].record()
+        logits = gen.decode(tok, pos)
+        ev[1].record()
+        torch.cuda.synchronize()
+        times.append(ev[0].elapsed_time(ev[1]))
+        pos += 1
+    gen._mega.check()
+    tr = gen._mega.trace.cpu().double() * 10.0 / 1000.0  # 100 MHz ticks -> µs
+    start, arrive = tr[:, :, 0], tr[:, :, 1]
+    t0 = start[:, 0].min()
+    res = {k: {"work_med": 0.0, "work_max": 0.0, "barrier": 0.0, "period": 0.0} for k in KINDS}
+    nph = 5 * nl
+    for p in range(nph - 1):
+        k = KINDS[p % 5]
+        work = arrive[:, p] - start[:, p]
+        res[k]["work_med"] += work.median().item() / nl
+        res[k]["work_max"] += work.max().item() / nl
+        res[k]["barrier"] += (start[:, p + 1].min() - arrive[:, p].max()).item() / nl
+        res[k]["period"] += (start[:, p + 1].median() - start[:, p].median()).item() / nl
+    total = (start[:, nph - 1].max() - t0).item()
+    print(json.dumps({"layers": nl, "step_ms_eager": sorted(times)[len(times) // 2],
+                      "kernel_span_us_to_last_phase": round(total, 1)}))
+    for k in KINDS:
+        print(json.dumps({"phase": k, **{n: round(v, 2) for n, v in res[k].items()}}))
+
+
+if __name__ == "__main__":
+    main()

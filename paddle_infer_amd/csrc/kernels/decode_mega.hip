@@ -40,6 +40,8 @@ constexpr int E = 2048, D = 128, HQ = 16, HK = 16, F = 8192;
 constexpr int NQKV = (HQ + 2 * HK) * D;  // 6144
 constexpr int WBYTES = 128 * 1024;     // LDS weight slice
 constexpr int PSTRIDE = D + 2;         // attention partial: acc[D], m, l
+// per-layer partial block, padded to 256 B
+__host__ __device__ constexpr long pstride(int nsplit) { return ((long)HQ * nsplit * PSTRIDE + 63) / 64 * 64; }
 
 typedef unsigned long long u64;
 
@@ -56,57 +58,84 @@ struct MegaArgs {
   int act;  // 0 gelu (erf), 1 gelu (tanh)
   float eps;
   float scale_log2;
-  bf16_t* resid;      // [E] residual stream, updated in place
-  float* qn;          // [HQ·D] q + bias
-  float* kvn;         // [2·HK·D] new k, v (+bias, bf16-rounded)
-  float* part;        // [HQ][nsplit][PSTRIDE]
-  bf16_t* h;          // [F] FFN hidden
-  unsigned* bar;      // arrival counter (zeroed by the launcher)
-  int* err;           // 1 = a grid barrier timed out
-  const int* pos;     // [1] cache slot of the new token
-  u64* trace;         // nullable: [NWG][5·nl][2] wall-clock (100 MHz) at phase start / arrival
+  const bf16_t* resid;  // [E] input residual (embedding output)
+  bf16_t* rbuf;         // [2·nl][E] residual after each out / FFN2 phase; the last row is the output
+  float* qn;            // [nl][HQ·D] q + bias
+  float* kvn;           // [nl][2·HK·D] new k, v (+bias, bf16-rounded)
+  float* part;          // [nl][pstride_l] attention partials [HQ][nsplit][PSTRIDE]
+  bf16_t* h;            // [nl][F] FFN hidden
+  unsigned* bar;        // barrier words (BAR_WORDS; zero before the first launch, re-zeroed by each)
+  int* err;             // number of launches in which a grid barrier timed out
+  const int* pos;       // [1] cache slot of the new token
+  u64* trace;           // nullable: [NWG][5·nl][4] wall-clock (100 MHz): phase start, prologue done,
+                        // GEMV done, barrier arrival
 };
 
-__device__ __forceinline__ u64 ld64(const void* p) {
-  return __hip_atomic_load((u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+__device__ __forceinline__ u64 ld64(const void* p) { return *reinterpret_cast<const u64*>(p); }
 __device__ __forceinline__ void st64(void* p, u64 v) {
   __hip_atomic_store((u64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ float ldf(const float* p) {
-  return __hip_atomic_load((float*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+__device__ __forceinline__ float ldf(const float* p) { return *p; }
 __device__ __forceinline__ u64 pack2f(float a, float b) {
   return (u64)__float_as_uint(a) | ((u64)__float_as_uint(b) << 32);
 }
 // 8 bf16 at p (16 B aligned) published by other workgroups → f32
 __device__ __forceinline__ void ld_bf8(const bf16_t* p, float* v) {
-  const u64 a = ld64(p), b = ld64(p + 4);
+  const u16x8 u = *reinterpret_cast<const u16x8*>(p);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    v[i] = bf2f((bf16_t)(a >> (16 * i)));
-    v[4 + i] = bf2f((bf16_t)(b >> (16 * i)));
-  }
+  for (int i = 0; i < 8; ++i) v[i] = bf2f(u[i]);
 }
 
-// Wave 0 only: this wave's publishing stores have completed → arrive → poll until every
-// workgroup has arrived `target / NWG` times.
-__device__ __forceinline__ void grid_sync(const MegaArgs& a, unsigned target, int lane) {
+// Wave 0 only: this wave's publishing stores have completed → arrive → wait for barrier `b`
+// (1-based). Two levels so no word sees more than 32 requesters: workgroup w arrives on the
+// counter of group w % 8 (32 members); the last member of a group arrives on the global counter
+// (8 members); the last group raises all 8 group flags; members poll their group's flag.
+// Every word sits on its own 256-B line.
+// Lines 0-7: group counters, 8: global counter, 9-16: group flags, 17: this launch's "a barrier
+// timed out" flag, 18: exited workgroups. The last workgroup to exit zeroes all of them;
+// `err` counts timed-out launches and is never reset by the kernel (MegaDecoder.check()).
+constexpr int BAR_LINE = 64, BAR_WORDS = 19 * BAR_LINE;
+// Barrier words are read with a read-modify-write (compare-and-swap against a value the word
+// never holds): RMW atomics execute memory-side and see every XCD's update, while a plain
+// agent-scope load may be served by a stale line in the poller's own L2 for as long as that line
+// stays resident (measured: ~160 µs release latency under hipGraph replay).
+__device__ __forceinline__ unsigned poll(unsigned* p) {
+  unsigned expect = 0xFFFFFFFFu;
+  __hip_atomic_compare_exchange_strong(p, &expect, 0xFFFFFFFFu, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+  return expect;
+}
+__device__ __forceinline__ void grid_sync(const MegaArgs& a, unsigned b, int lane) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (a.trace && lane == 0) a.trace[((long)blockIdx.x * a.nl * 5 + target / NWG - 1) * 2 + 1] = wall_clock64();
+  if (a.trace && lane == 0) a.trace[((long)blockIdx.x * a.nl * 5 + b - 1) * 4 + 3] = wall_clock64();
   if (lane == 0) {
-    __hip_atomic_fetch_add(a.bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int g = blockIdx.x & 7;
+    unsigned* xc = a.bar + g * BAR_LINE;
+    unsigned* gc = a.bar + 8 * BAR_LINE;
+    unsigned* fl = a.bar + (9 + g) * BAR_LINE;
+    if (__hip_atomic_fetch_add(xc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == b * (NWG / 8) - 1 &&
+        __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == b * 8 - 1) {
+      for (int i = 0; i < 8; ++i)
+        __hip_atomic_fetch_max(a.bar + (9 + i) * BAR_LINE, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     unsigned spins = 0;
-    while (__hip_atomic_load(a.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    while (poll(fl) < b) {
       __builtin_amdgcn_s_sleep(1);
-      if ((++spins & 1023) == 0) {  // bounded: one timeout makes every later barrier fall through
-        if (spins > (1u << 21) || __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-          __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((++spins & 1023) == 0) {  // bounded: one timeout makes the launch's later barriers fall through
+        unsigned* failed = a.bar + 17 * BAR_LINE;
+        if (poll(failed)) break;
+        if (spins > (1u << 21)) {
+          if (__hip_atomic_exchange(failed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+            __hip_atomic_fetch_add(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
       }
     }
   }
+}
+
+__device__ __forceinline__ void tmark(const MegaArgs& a, unsigned ph, int k) {
+  if (a.trace && threadIdx.x == 0) a.trace[((long)blockIdx.x * a.nl * 5 + ph) * 4 + k] = wall_clock64();
 }
 
 // Loader waves: DMA `bytes` (multiple of 1 KiB) from `src` into the LDS slice.
@@ -123,7 +152,22 @@ __device__ __forceinline__ void prefetch(const bf16_t* src, int bytes, char* wl,
 __device__ __forceinline__ void phase_start(const MegaArgs& a, int wv, unsigned ph) {
   if (wv != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (a.trace && threadIdx.x == 0) a.trace[((long)blockIdx.x * a.nl * 5 + ph) * 2] = wall_clock64();
+  if (a.trace && threadIdx.x == 0) a.trace[((long)blockIdx.x * a.nl * 5 + ph) * 4] = wall_clock64();
+}
+
+// One exchange level of the column-halving butterfly: lanes with bit O set keep the upper HALF
+// columns, the others the lower, each adding its partner's copy. Compile-time recursion keeps
+// every register index static (a runtime loop here became dynamic-index select chains).
+template <int HALF, int O>
+__device__ __forceinline__ void butterfly(float* acc, int lane) {
+  const bool up = (lane & O) != 0;
+#pragma unroll
+  for (int i = 0; i < HALF; ++i) {
+    const float mine = up ? acc[i + HALF] : acc[i];
+    const float oth = up ? acc[i] : acc[i + HALF];
+    acc[i] = mine + __shfl_xor(oth, O, 64);
+  }
+  if constexpr (HALF > 1) butterfly<HALF / 2, O / 2>(acc, lane);
 }
 
 // y[c] = Σ_k x[k]·W[c][k] for the NPW columns of this workgroup's LDS slice ([NPW][K] bf16);
@@ -149,18 +193,7 @@ __device__ __forceinline__ float gemv_lds(const char* wl, const float (&x)[KCH][
       for (int i = 0; i < 8; ++i) acc[c] += x[j][i] * bf2f(w[i]);
     }
   }
-#pragma unroll
-  for (int s = 0; s < LOGP; ++s) {
-    const int o = 32 >> s;
-    const bool up = (lane & o) != 0;
-#pragma unroll
-    for (int i = 0; i < (P >> (s + 1)); ++i) {
-      const int hi = i + (P >> (s + 1));
-      const float mine = up ? acc[hi] : acc[i];
-      const float oth = up ? acc[i] : acc[hi];
-      acc[i] = mine + __shfl_xor(oth, o, 64);
-    }
-  }
+  butterfly<P / 2, 32>(acc, lane);
 #pragma unroll
   for (int o = 32 >> LOGP; o > 0; o >>= 1) acc[0] += __shfl_xor(acc[0], o, 64);
   if ((lane & ((64 >> LOGP) - 1)) == 0) red[wv * P + (lane >> (6 - LOGP))] = acc[0];
@@ -171,10 +204,10 @@ __device__ __forceinline__ float gemv_lds(const char* wl, const float (&x)[KCH][
 }
 
 // x = bf16(LN(resid)) for this thread's 8 elements k = 8·tid.
-__device__ __forceinline__ void ln_prologue(const MegaArgs& a, const bf16_t* g, const bf16_t* b,
-                                            float (&x)[1][8], float* wred, int tid) {
+__device__ __forceinline__ void ln_prologue(const MegaArgs& a, const bf16_t* r, const bf16_t* g,
+                                            const bf16_t* b, float (&x)[1][8], float* wred, int tid) {
   float v[8];
-  ld_bf8(a.resid + tid * 8, v);
+  ld_bf8(r + tid * 8, v);
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < 8; ++i) s += v[i];
@@ -214,29 +247,42 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
   prefetch(a.layers[0].wqkv + (long)w * NPQ * E, NPQ * E * 2, wl, wv, lane);
   for (int l = 0; l < a.nl; ++l) {
     const MegaLayer& Ly = a.layers[l];
+    // this layer's buffer slots: every published vector has its own address per launch, so a
+    // reader's L2 can never hold a stale copy and plain (cached) loads are coherent
+    const bf16_t* rin = l == 0 ? a.resid : a.rbuf + (long)(2 * l - 1) * E;
+    bf16_t* rmid = a.rbuf + (long)(2 * l) * E;
+    bf16_t* rout = a.rbuf + (long)(2 * l + 1) * E;
+    float* qn = a.qn + (long)l * HQ * D;
+    float* kvn = a.kvn + (long)l * 2 * HK * D;
+    float* part = a.part + (long)l * pstride(a.nsplit);
+    bf16_t* hb = a.h + (long)l * F;
     // ---------------------------------------------------------------- QKV
     phase_start(a, wv, nbar);
     {
+      // epilogue operands requested first: their latency hides under the prologue and GEMV
+      const float bq = lane < NPQ ? bf2f(Ly.bqkv[w * NPQ + lane]) : 0.f;
       float x[1][8];
-      ln_prologue(a, Ly.ln1_g, Ly.ln1_b, x, wred, tid);
+      ln_prologue(a, rin, Ly.ln1_g, Ly.ln1_b, x, wred, tid);
+      tmark(a, nbar, 1);
       const float y = gemv_lds<NPQ, 1>(wl, x, red, tid);
+      tmark(a, nbar, 2);
       prefetch(Ly.wo + (long)w * NPO * E, NPO * E * 2, wl, wv, lane);
       if (wv == 0) {
         if (lane < NPQ) {
           const int col = w * NPQ + lane;
-          const float v = bf2f(f2bf(y)) + bf2f(Ly.bqkv[col]);
+          const float v = bf2f(f2bf(y)) + bq;
           if (col < HQ * D) {
-            __hip_atomic_store(a.qn + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(qn + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           } else {
             const int kv = col - HQ * D;          // [0, 2·HK·D)
             const int which = kv / (HK * D), r = kv % (HK * D), kh = r / D, d = r % D;
             const bf16_t vb = f2bf(v);
             bf16_t* cache = which ? Ly.vc : Ly.kc;
             cache[((long)kh * a.maxS + pos) * D + d] = vb;
-            __hip_atomic_store(a.kvn + kv, bf2f(vb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(kvn + kv, bf2f(vb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
         }
-        grid_sync(a, (++nbar) * NWG, lane);
+        grid_sync(a, ++nbar, lane);
       } else {
         ++nbar;
       }
@@ -251,10 +297,10 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
       const long kvbase = (long)kh * a.maxS * D;
       float q[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) q[i] = ldf(a.qn + h * D + sub * 8 + i) * a.scale_log2;
+      for (int i = 0; i < 8; ++i) q[i] = ldf(qn + h * D + sub * 8 + i) * a.scale_log2;
       auto row = [&](const bf16_t* cache, int which, int j, float* r) {
         if (j == pos) {
-          const float* p = a.kvn + which * HK * D + kh * D + sub * 8;
+          const float* p = kvn + which * HK * D + kh * D + sub * 8;
 #pragma unroll
           for (int i = 0; i < 8; i += 2) {
             const u64 u = ld64(p + i);
@@ -305,7 +351,7 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
       }
       __syncthreads();
       if (wv == 0) {
-        float* dst = a.part + (long)(h * a.nsplit + s) * PSTRIDE;
+        float* dst = part + (long)(h * a.nsplit + s) * PSTRIDE;
         const int d0 = lane * 2;
         const float v0 = pv[0][d0] + pv[1][d0] + pv[2][d0] + pv[3][d0];
         const float v1 = pv[0][d0 + 1] + pv[1][d0 + 1] + pv[2][d0 + 1] + pv[3][d0 + 1];
@@ -313,14 +359,16 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
         if (lane == 0) st64(dst + D, pack2f(n > 0 ? m : -INFINITY, n > 0 ? lsum : 0.f));
       }
     }
-    if (wv == 0) grid_sync(a, (++nbar) * NWG, lane); else ++nbar;
+    if (wv == 0) grid_sync(a, ++nbar, lane); else ++nbar;
     // ---------------------------------------------------------------- out projection
     phase_start(a, wv, nbar);
     {
+      const int ocol = w * NPO + (lane & (NPO - 1));
+      const float bo = bf2f(Ly.bo[ocol]), ro = bf2f(rin[ocol]);
       float x[1][8];
       {
         const int h = tid >> 4, d0 = (tid & 15) * 8;
-        const float* base = a.part + (long)h * a.nsplit * PSTRIDE;
+        const float* base = part + (long)h * a.nsplit * PSTRIDE;
         float M = -INFINITY;
         for (int s = 0; s < a.nsplit; ++s) M = fmaxf(M, ldf(base + s * PSTRIDE + D));
         float lt = 0.f, o[8];
@@ -343,14 +391,13 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) x[0][i] = bf2f(f2bf(o[i] * inv));
       }
+      tmark(a, nbar, 1);
       const float y = gemv_lds<NPO, 1>(wl, x, red, tid);
+      tmark(a, nbar, 2);
       prefetch(Ly.w1 + (long)w * NP1 * E, NP1 * E * 2, wl, wv, lane);
       if (wv == 0) {
-        const int col = w * NPO + (lane & (NPO - 1));
-        const u64 r4 = ld64(a.resid + (col & ~3));
-        const float r = bf2f((bf16_t)(r4 >> (16 * (col & 3))));
-        publish_bf16(a.resid + w * NPO, y + bf2f(Ly.bo[col]) + r, lane, NPO);
-        grid_sync(a, (++nbar) * NWG, lane);
+        publish_bf16(rmid + w * NPO, y + bo + ro, lane, NPO);
+        grid_sync(a, ++nbar, lane);
       } else {
         ++nbar;
       }
@@ -358,15 +405,17 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
     // ---------------------------------------------------------------- FFN1
     phase_start(a, wv, nbar);
     {
+      const float b1 = bf2f(Ly.b1[w * NP1 + (lane & (NP1 - 1))]);
       float x[1][8];
-      ln_prologue(a, Ly.ln2_g, Ly.ln2_b, x, wred, tid);
+      ln_prologue(a, rmid, Ly.ln2_g, Ly.ln2_b, x, wred, tid);
+      tmark(a, nbar, 1);
       const float y = gemv_lds<NP1, 1>(wl, x, red, tid);
+      tmark(a, nbar, 2);
       prefetch(Ly.w2 + (long)w * NP2 * F, NP2 * F * 2, wl, wv, lane);
       if (wv == 0) {
-        const int col = w * NP1 + (lane & (NP1 - 1));
-        const float t = y + bf2f(Ly.b1[col]);
-        publish_bf16(a.h + w * NP1, a.act ? gelu_tanh(t) : gelu_erf(t), lane, NP1);
-        grid_sync(a, (++nbar) * NWG, lane);
+        const float t = y + b1;
+        publish_bf16(hb + w * NP1, a.act ? gelu_tanh(t) : gelu_erf(t), lane, NP1);
+        grid_sync(a, ++nbar, lane);
       } else {
         ++nbar;
       }
@@ -374,23 +423,31 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
     // ---------------------------------------------------------------- FFN2
     phase_start(a, wv, nbar);
     {
+      const int fcol = w * NP2 + (lane & (NP2 - 1));
+      const float b2 = bf2f(Ly.b2[fcol]), rm = bf2f(rmid[fcol]);
       float x[4][8];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) ld_bf8(a.h + (j * 256 + tid) * 8, x[j]);
+      for (int j = 0; j < 4; ++j) ld_bf8(hb + (j * 256 + tid) * 8, x[j]);
+      tmark(a, nbar, 1);
       const float y = gemv_lds<NP2, 4>(wl, x, red, tid);
+      tmark(a, nbar, 2);
       if (l + 1 < a.nl) prefetch(a.layers[l + 1].wqkv + (long)w * NPQ * E, NPQ * E * 2, wl, wv, lane);
       if (wv == 0) {
-        const int col = w * NP2 + (lane & (NP2 - 1));
-        const u64 r4 = ld64(a.resid + (col & ~3));
-        const float r = bf2f((bf16_t)(r4 >> (16 * (col & 3))));
-        publish_bf16(a.resid + w * NP2, y + bf2f(Ly.b2[col]) + r, lane, NP2);
-        if (l + 1 < a.nl) grid_sync(a, (++nbar) * NWG, lane);
+        publish_bf16(rout + w * NP2, y + b2 + rm, lane, NP2);
+        if (l + 1 < a.nl) grid_sync(a, ++nbar, lane);
       } else {
         ++nbar;
       }
     }
   }
   if (wv != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // the last workgroup out re-zeroes the barrier words for the next launch (stream-ordered), so
+  // a launch needs no memset node in front of it
+  if (tid == 0 &&
+      __hip_atomic_fetch_add(a.bar + 18 * BAR_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == NWG - 1) {
+    for (int i = 0; i < 19; ++i)
+      __hip_atomic_exchange(a.bar + i * BAR_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 }  // namespace
@@ -409,10 +466,8 @@ PIAMD_EXPORT int piamd_decode_mega(const MegaArgs* args, int E_, int D_, int hq,
   const MegaArgs& a = *args;
   if (cus < NWG || E_ != E || D_ != D || hq != HQ || hk != HK || F_ != F || a.nl < 1 ||
       a.nsplit < 1 || HQ * a.nsplit > NWG || (a.maxS + a.nsplit - 1) / a.nsplit > 256 || !a.layers ||
-      !a.resid || !a.qn || !a.kvn || !a.part || !a.h || !a.bar || !a.err || !a.pos)
+      !a.resid || !a.rbuf || !a.qn || !a.kvn || !a.part || !a.h || !a.bar || !a.err || !a.pos)
     return (int)hipErrorInvalidValue;
-  hipError_t e = hipMemsetAsync(a.bar, 0, sizeof(unsigned), st);
-  if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(decode_mega_kernel, dim3(NWG), dim3(NT), 0, st, a);
   return (int)hipGetLastError();
 }

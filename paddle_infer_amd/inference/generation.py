@@ -120,8 +120,7 @@ class GPTGenerator:
             from ..ops.norm import layer_norm
             resid = self.model.gpt.embeddings(tok.view(1, 1), pos.long().view(1, 1))
             resid = resid.reshape(-1).contiguous()
-            mega(resid, pos)
-            y = layer_norm(resid.view(1, -1), *self.final_ln)
+            y = layer_norm(mega(resid, pos).view(1, -1), *self.final_ln)
             return self._logits(y)
         lens = pos + 1
         y = self._forward(tok.view(B, 1), pos, lens, B, decode=True)
@@ -131,7 +130,9 @@ class GPTGenerator:
     def decode(self, tok, pos):
         """One step: tok [B] int64, pos [B] int32 (cache slot to write). Returns logits [B, V]."""
         B = tok.shape[0]
-        if not self.use_graph:
+        # the single-launch step runs without a graph: it is ~6 launches, and a hipGraph replay
+        # of it measured slower than direct launches (tools/mega_graph_probe.py)
+        if not self.use_graph or self._mega_decoder(B) is not None:
             return self._decode_eager(tok, pos, B)
         ent = self._graphs.get(B)
         if ent is None:
@@ -190,7 +191,7 @@ class GPTGenerator:
         out = torch.full((B, max_new_tokens), pad_token_id, dtype=torch.long, device=self.device)
         done = torch.zeros(B, dtype=torch.bool, device=self.device)
         pos = lens.to(torch.int32)
-        if decode_strategy == "greedy_search" and self.use_graph:
+        if decode_strategy == "greedy_search" and self.use_graph and self._mega_decoder(B) is None:
             return self._greedy_graph_loop(logits, pos, out, done, max_new_tokens, eos_token_id,
                                            pad_token_id)
         for t in range(max_new_tokens):

@@ -77,31 +77,37 @@ class MegaDecoder:
         self.nl = len(rows)
         self.maxS = gen.max_seq_len
         self.nsplit = max(1, math.ceil(self.maxS / 256))
-        f32 = dict(dtype=torch.float32, device=dev)
-        self.qn = torch.zeros(HQ * D, **f32)
-        self.kvn = torch.zeros(2 * HK * D, **f32)
-        self.part = torch.zeros(HQ * self.nsplit * (D + 2), **f32)
-        self.h = torch.zeros(F, dtype=torch.bfloat16, device=dev)
-        self.bar = torch.zeros(1, dtype=torch.int32, device=dev)
+        # one slot per layer (and per residual update) for every vector handed between
+        # workgroups: each address is written once per launch, so readers may use cached loads
+        nl, f32, bf = self.nl, dict(dtype=torch.float32, device=dev), dict(dtype=torch.bfloat16, device=dev)
+        pstride = (HQ * self.nsplit * (D + 2) + 63) // 64 * 64
+        self.rbuf = torch.zeros(2 * nl, E, **bf)
+        self.qn = torch.zeros(nl, HQ * D, **f32)
+        self.kvn = torch.zeros(nl, 2 * HK * D, **f32)
+        self.part = torch.zeros(nl * pstride, **f32)
+        self.h = torch.zeros(nl, F, **bf)
+        self.bar = torch.zeros(19 * 64, dtype=torch.int32, device=dev)
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.act = 1 if gen.act == "gelu_tanh" else 0
         self.eps = float(gen.cfg.layer_norm_eps)
         self.trace = None  # set to a zeroed int64 [256, 5·nl, 2] tensor to record phase times
 
     def __call__(self, resid: torch.Tensor, pos: torch.Tensor) -> torch.Tensor:
-        """resid: bf16 [E] (embedding output; updated in place to the last layer's residual);
-        pos: device int32 [1] = the cache slot of this token."""
+        """resid: bf16 [E] embedding output; pos: device int32 [1] = the cache slot of this token.
+        Returns the last layer's residual stream [E] (a view of an internal buffer)."""
         assert resid.is_contiguous() and resid.numel() == E and resid.dtype == torch.bfloat16
         assert pos.dtype == torch.int32 and pos.is_cuda
         a = _lib.MegaArgs(self.table.data_ptr(), self.nl, self.maxS, self.nsplit, self.act,
                           self.eps, (1.0 / math.sqrt(D)) * 1.4426950408889634, resid.data_ptr(),
-                          self.qn.data_ptr(), self.kvn.data_ptr(), self.part.data_ptr(),
+                          self.rbuf.data_ptr(), self.qn.data_ptr(), self.kvn.data_ptr(), self.part.data_ptr(),
                           self.h.data_ptr(), self.bar.data_ptr(), self.err.data_ptr(),
                           pos.data_ptr(), _lib.ptr(self.trace))
         _lib.call("piamd_decode_mega", ctypes.byref(a), E, D, HQ, HK, F, _lib.stream())
-        return resid
+        return self.rbuf[-1]
 
     def check(self) -> None:
         """Raise if a grid barrier of an earlier launch timed out (synchronises)."""
-        if int(self.err.item()):
-            raise RuntimeError("decode_mega: a grid barrier timed out (workgroups not co-resident?)")
+        n = int(self.err.item())
+        if n:
+            raise RuntimeError(f"decode_mega: a grid barrier timed out in {n} launch(es) "
+                               "(workgroups not co-resident?)")

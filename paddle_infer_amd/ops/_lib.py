@@ -91,8 +91,8 @@ class MegaArgs(ctypes.Structure):
     """Mirror of ``struct MegaArgs`` (csrc/kernels/decode_mega.hip)."""
     _fields_ = ([("layers", c_void_p)] + [(n, c_int) for n in ("nl", "maxS", "nsplit", "act")]
                 + [("eps", ctypes.c_float), ("scale_log2", ctypes.c_float)]
-                + [(n, c_void_p) for n in ("resid", "qn", "kvn", "part", "h", "bar", "err", "pos",
-                                        "trace")])
+                + [(n, c_void_p) for n in ("resid", "rbuf", "qn", "kvn", "part", "h", "bar", "err",
+                                        "pos", "trace")])
 
 
 _SIGS["piamd_decode_mega"] = [ctypes.POINTER(MegaArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]

@@ -74,6 +74,9 @@ def main():
                  "prefill_tok_s": round(B * a.prompt / t_pre, 1),
                  "decode_ms_per_step": round(t_dec / a.gen * 1e3, 4),
                  "decode_tok_s": round(B * a.gen / t_dec, 1)}
+            if getattr(gen, "_mega", None):
+                r["mega_decode"] = True
+                r["mega_timeouts"] = int(gen._mega.err.item())
             print(json.dumps(r), flush=True)
             rows.append(r)
         del gen

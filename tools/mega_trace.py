@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--prompt", type=int, default=128)
     ap.add_argument("--steps", type=int, default=8)
     args = ap.parse_args()
+    os.environ.setdefault("PIAMD_DECODE_MEGA", "1")
     import paddle_infer_amd as paddle
     from paddle_infer_amd.inference.generation import GPTGenerator
     from paddle_infer_amd.models.gpt import GPTForPretraining, gpt_config
@@ -41,7 +42,7 @@ def main():
     for step in range(args.steps):
         tok = logits.argmax(-1)
         if step == args.steps - 1:
-            gen._mega.trace = torch.zeros(256, 5 * nl, 2, dtype=torch.int64, device="cuda")
+            gen._mega.trace = torch.zeros(256, 5 * nl, 4, dtype=torch.int64, device="cuda")
         ev[0].record()
         logits = gen.decode(tok, pos)
         ev[1].record()
@@ -50,13 +51,18 @@ def main():
         pos += 1
     gen._mega.check()
     tr = gen._mega.trace.cpu().double() * 10.0 / 1000.0  # 100 MHz ticks -> µs
-    start, arrive = tr[:, :, 0], tr[:, :, 1]
+    start, pro, gem, arrive = tr[:, :, 0], tr[:, :, 1], tr[:, :, 2], tr[:, :, 3]
     t0 = start[:, 0].min()
-    res = {k: {"work_med": 0.0, "work_max": 0.0, "barrier": 0.0, "period": 0.0} for k in KINDS}
+    res = {k: {"prologue": 0.0, "gemv": 0.0, "epilogue": 0.0, "work_med": 0.0, "work_max": 0.0,
+              "barrier": 0.0, "period": 0.0} for k in KINDS}
     nph = 5 * nl
     for p in range(nph - 1):
         k = KINDS[p % 5]
         work = arrive[:, p] - start[:, p]
+        if k != "attn":
+            res[k]["prologue"] += (pro[:, p] - start[:, p]).median().item() / nl
+            res[k]["gemv"] += (gem[:, p] - pro[:, p]).median().item() / nl
+            res[k]["epilogue"] += (arrive[:, p] - gem[:, p]).median().item() / nl
         res[k]["work_med"] += work.median().item() / nl
         res[k]["work_max"] += work.max().item() / nl
         res[k]["barrier"] += (start[:, p + 1].min() - arrive[:, p].max()).item() / nl

@@ -206,6 +206,10 @@ __device__ __forceinline__ float gemv_lds(const char* wl, const float (&x)[KCH][
 // x = bf16(LN(resid)) for this thread's 8 elements k = 8·tid.
 __device__ __forceinline__ void ln_prologue(const MegaArgs& a, const bf16_t* r, const bf16_t* g,
                                             const bf16_t* b, float (&x)[1][8], float* wred, int tid) {
+  // gamma / beta first: their latency then hides under the residual load and the reductions
+  // (a load is not hoisted across the __syncthreads of block_sum)
+  const u16x8 gg = *reinterpret_cast<const u16x8*>(g + tid * 8);
+  const u16x8 bb = *reinterpret_cast<const u16x8*>(b + tid * 8);
   float v[8];
   ld_bf8(r + tid * 8, v);
   float s = 0.f;
@@ -216,8 +220,6 @@ __device__ __forceinline__ void ln_prologue(const MegaArgs& a, const bf16_t* r, 
 #pragma unroll
   for (int i = 0; i < 8; ++i) q += (v[i] - mean) * (v[i] - mean);
   const float rs = rsqrtf(block_sum<4>(q, wred) * (1.f / E) + a.eps);
-  const u16x8 gg = *reinterpret_cast<const u16x8*>(g + tid * 8);
-  const u16x8 bb = *reinterpret_cast<const u16x8*>(b + tid * 8);
 #pragma unroll
   for (int i = 0; i < 8; ++i) x[0][i] = bf2f(f2bf((v[i] - mean) * rs * bf2f(gg[i]) + bf2f(bb[i])));
 }

@@ -110,9 +110,11 @@ class GPTGenerator:
         """The single-launch decode step (inference/mega_decode.py) when this model / batch fits
         it, else None (per-op path)."""
         from . import mega_decode
-        if self._mega is None:
+        if B != 1 or not mega_decode.enabled():
+            return None
+        if self._mega is None:  # the shape / dtype gate is static: evaluated once
             self._mega = mega_decode.MegaDecoder(self) if mega_decode.eligible(self, 1) else False
-        return self._mega if (self._mega and B == 1 and mega_decode.eligible(self, B)) else None
+        return self._mega or None
 
     def _decode_eager(self, tok, pos, B):
         mega = self._mega_decoder(B)

@@ -26,9 +26,13 @@ E, D, HQ, HK, F = 2048, 128, 16, 16, 8192
 DEFAULT = "0"
 
 
+def enabled() -> bool:
+    return os.environ.get("PIAMD_DECODE_MEGA", DEFAULT) != "0"
+
+
 def eligible(gen, B: int) -> bool:
     """True when generator ``gen``'s decode step at batch ``B`` can run as one launch."""
-    if os.environ.get("PIAMD_DECODE_MEGA", DEFAULT) == "0":
+    if not enabled():
         return False
     if B != 1 or gen.device.type != "cuda" or gen.dtype != torch.bfloat16 or gen.group is not None:
         return False

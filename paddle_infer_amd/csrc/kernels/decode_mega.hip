@@ -138,11 +138,12 @@ __device__ __forceinline__ void tmark(const MegaArgs& a, unsigned ph, int k) {
   if (a.trace && threadIdx.x == 0) a.trace[((long)blockIdx.x * a.nl * 5 + ph) * 4 + k] = wall_clock64();
 }
 
-// Loader waves: DMA `bytes` (multiple of 1 KiB) from `src` into the LDS slice.
-__device__ __forceinline__ void prefetch(const bf16_t* src, int bytes, char* wl, int wv, int lane) {
-  if (wv == 0) return;
+// Loader waves: DMA bytes [from, to) (multiples of 1 KiB) of the slice at `src` into the same
+// offsets of the LDS slice.
+__device__ __forceinline__ void prefetch(const bf16_t* src, int from, int to, char* wl, int wv, int lane) {
+  if (wv == 0 || src == nullptr) return;
   const char* s = reinterpret_cast<const char*>(src) + lane * 16;
-  for (int p = wv - 1; p < (bytes >> 10); p += 3)
+  for (int p = (from >> 10) + wv - 1; p < (to >> 10); p += 3)
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(s + p * 1024),
                                      (__attribute__((address_space(3))) void*)(wl + p * 1024), 16, 0, 0);
 }
@@ -174,9 +175,12 @@ __device__ __forceinline__ void butterfly(float* acc, int lane) {
 // thread t holds x[k] for k = (j·256 + t)·8 + i. Returns column `tid`'s sum for tid < NPW.
 // Reduction: a butterfly that halves the live columns per exchange (log2 P steps, P−1 shuffles
 // instead of 6·P), then 4 waves through LDS.
+// The next phase's slice (`nsrc`, `nbytes`; nullable) streams in behind the GEMV: its first
+// min(nbytes, this slice / 2) bytes as soon as every wave has consumed the first half of the
+// columns, the rest once the whole slice is consumed.
 template <int NPW, int KCH>
-__device__ __forceinline__ float gemv_lds(const char* wl, const float (&x)[KCH][8], float* red,
-                                          int tid) {
+__device__ __forceinline__ float gemv_lds(char* wl, const float (&x)[KCH][8], float* red, int tid,
+                                          const bf16_t* nsrc, int nbytes) {
   constexpr int K = 2048 * KCH;
   constexpr int P = NPW <= 8 ? 8 : 32;
   constexpr int LOGP = P == 8 ? 3 : 5;
@@ -184,20 +188,29 @@ __device__ __forceinline__ float gemv_lds(const char* wl, const float (&x)[KCH][
   float acc[P];
 #pragma unroll
   for (int c = 0; c < P; ++c) acc[c] = 0.f;
+  auto cols = [&](auto c0, auto c1) {
 #pragma unroll
-  for (int c = 0; c < NPW; ++c) {
+    for (int c = decltype(c0)::value; c < decltype(c1)::value; ++c) {
 #pragma unroll
-    for (int j = 0; j < KCH; ++j) {
-      const u16x8 w = *reinterpret_cast<const u16x8*>(wl + ((long)c * K + (j * 256 + tid) * 8) * 2);
+      for (int j = 0; j < KCH; ++j) {
+        const u16x8 w = *reinterpret_cast<const u16x8*>(wl + ((long)c * K + (j * 256 + tid) * 8) * 2);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc[c] += x[j][i] * bf2f(w[i]);
+        for (int i = 0; i < 8; ++i) acc[c] += x[j][i] * bf2f(w[i]);
+      }
     }
-  }
+  };
+  constexpr int SLICE = NPW * K * 2;
+  const int early = min(nbytes, SLICE / 2);
+  cols(std::integral_constant<int, 0>{}, std::integral_constant<int, NPW / 2>{});
+  __syncthreads();  // columns [0, NPW/2) = slice bytes [0, SLICE/2) consumed by every wave
+  prefetch(nsrc, 0, early, wl, wv, lane);
+  cols(std::integral_constant<int, NPW / 2>{}, std::integral_constant<int, NPW>{});
   butterfly<P / 2, 32>(acc, lane);
 #pragma unroll
   for (int o = 32 >> LOGP; o > 0; o >>= 1) acc[0] += __shfl_xor(acc[0], o, 64);
   if ((lane & ((64 >> LOGP) - 1)) == 0) red[wv * P + (lane >> (6 - LOGP))] = acc[0];
   __syncthreads();
+  prefetch(nsrc, early, nbytes, wl, wv, lane);
   float r = 0.f;
   if (tid < NPW) r = red[tid] + red[P + tid] + red[2 * P + tid] + red[3 * P + tid];
   return r;
@@ -246,7 +259,7 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
   unsigned nbar = 0;
   constexpr int NPQ = NQKV / NWG, NPO = E / NWG, NP1 = F / NWG, NP2 = E / NWG;
 
-  prefetch(a.layers[0].wqkv + (long)w * NPQ * E, NPQ * E * 2, wl, wv, lane);
+  prefetch(a.layers[0].wqkv + (long)w * NPQ * E, 0, NPQ * E * 2, wl, wv, lane);
   for (int l = 0; l < a.nl; ++l) {
     const MegaLayer& Ly = a.layers[l];
     // this layer's buffer slots: every published vector has its own address per launch, so a
@@ -266,9 +279,8 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
       float x[1][8];
       ln_prologue(a, rin, Ly.ln1_g, Ly.ln1_b, x, wred, tid);
       tmark(a, nbar, 1);
-      const float y = gemv_lds<NPQ, 1>(wl, x, red, tid);
+      const float y = gemv_lds<NPQ, 1>(wl, x, red, tid, Ly.wo + (long)w * NPO * E, NPO * E * 2);
       tmark(a, nbar, 2);
-      prefetch(Ly.wo + (long)w * NPO * E, NPO * E * 2, wl, wv, lane);
       if (wv == 0) {
         if (lane < NPQ) {
           const int col = w * NPQ + lane;
@@ -394,9 +406,8 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
         for (int i = 0; i < 8; ++i) x[0][i] = bf2f(f2bf(o[i] * inv));
       }
       tmark(a, nbar, 1);
-      const float y = gemv_lds<NPO, 1>(wl, x, red, tid);
+      const float y = gemv_lds<NPO, 1>(wl, x, red, tid, Ly.w1 + (long)w * NP1 * E, NP1 * E * 2);
       tmark(a, nbar, 2);
-      prefetch(Ly.w1 + (long)w * NP1 * E, NP1 * E * 2, wl, wv, lane);
       if (wv == 0) {
         publish_bf16(rmid + w * NPO, y + bo + ro, lane, NPO);
         grid_sync(a, ++nbar, lane);
@@ -411,9 +422,8 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
       float x[1][8];
       ln_prologue(a, rmid, Ly.ln2_g, Ly.ln2_b, x, wred, tid);
       tmark(a, nbar, 1);
-      const float y = gemv_lds<NP1, 1>(wl, x, red, tid);
+      const float y = gemv_lds<NP1, 1>(wl, x, red, tid, Ly.w2 + (long)w * NP2 * F, NP2 * F * 2);
       tmark(a, nbar, 2);
-      prefetch(Ly.w2 + (long)w * NP2 * F, NP2 * F * 2, wl, wv, lane);
       if (wv == 0) {
         const float t = y + b1;
         publish_bf16(hb + w * NP1, a.act ? gelu_tanh(t) : gelu_erf(t), lane, NP1);
@@ -431,9 +441,10 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) ld_bf8(hb + (j * 256 + tid) * 8, x[j]);
       tmark(a, nbar, 1);
-      const float y = gemv_lds<NP2, 4>(wl, x, red, tid);
+      const float y = gemv_lds<NP2, 4>(wl, x, red, tid,
+                                       l + 1 < a.nl ? a.layers[l + 1].wqkv + (long)w * NPQ * E : nullptr,
+                                       NPQ * E * 2);
       tmark(a, nbar, 2);
-      if (l + 1 < a.nl) prefetch(a.layers[l + 1].wqkv + (long)w * NPQ * E, NPQ * E * 2, wl, wv, lane);
       if (wv == 0) {
         publish_bf16(rout + w * NP2, y + b2 + rm, lane, NP2);
         if (l + 1 < a.nl) grid_sync(a, ++nbar, lane);

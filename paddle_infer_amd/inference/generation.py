@@ -207,6 +207,8 @@ class GPTGenerator:
             if t + 1 < max_new_tokens:
                 logits = self.decode(tok, pos)
                 pos = pos + 1
+        if self._mega:  # one sync per generate(): a timed-out single-launch step fails loudly
+            self._mega.check()
         return out
 
     def _greedy_graph_loop(self, logits, pos, out, done, max_new_tokens, eos, pad):

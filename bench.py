@@ -76,6 +76,10 @@ def main():
     if world != args.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
     on_gpu = args.device == "cuda"
+    # the package installs the framework's auto-growth allocator at import: it must come before
+    # the first HIP call of the process (set_device initialises the caching allocator otherwise)
+    import paddle_infer_amd as pia
+    from paddle_infer_amd.framework import allocator as pia_alloc
     if on_gpu:
         torch.cuda.set_device(local_rank)
         device = torch.device("cuda", local_rank)
@@ -93,7 +97,6 @@ def main():
         else:
             dist.init_process_group("gloo")
 
-    import paddle_infer_amd as pia
     from paddle_infer_amd.incubate import autotune
     tuned = autotune.use_tuned_gemms() if args.tuned_gemm else False
     from paddle_infer_amd.distributed import fleet
@@ -211,7 +214,10 @@ def main():
                        **({"pp_micro_batches": acc} if pp > 1 else {})},
             "tflops_per_gpu": round(tflops_gpu, 1), "final_loss": round(final_loss, 4),
             "tuned_gemm_table": bool(tuned),
-            "peak_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1) if on_gpu else None,
+            "allocator": "auto_growth" if pia_alloc.active() else "torch_caching",
+            # the framework allocator's own peak when it is active (torch.cuda's is routed to it)
+            "peak_mem_gb": round((pia_alloc.stats(local_rank)["peak_allocated"] if pia_alloc.active()
+                                  else torch.cuda.max_memory_allocated()) / 2 ** 30, 1) if on_gpu else None,
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -307,8 +307,8 @@ PIAMD_EXPORT int piamd_beam_search_softmax(
   return (int)hipGetLastError();
 }
 
-// Greedy decoding: out[r] = argmax_v logits[r, v] (ties → the smaller id, NaN ignored unless the
-// whole row is NaN, like torch.argmax on finite rows), one 1024-thread workgroup per row: each
+// Greedy decoding: out[r] = argmax_v logits[r, v] (ties → the smaller id; NaNs are skipped unless
+// the whole row is NaN — unlike torch.argmax, which returns a NaN's index; equal on finite rows), one 1024-thread workgroup per row: each
 // lane keeps a running (max, id) over 16-B vector loads (8 bf16/fp16 or 4 f32), then one wave64
 // shuffle argmax per wave and a 16-entry LDS merge. One launch, no workspace, capturable.
 namespace {

@@ -36,13 +36,18 @@ struct Reader {
     Reader r = sub();
     return std::string((const char*)r.p, (const char*)r.end);
   }
+  void need(size_t n) const {
+    if ((size_t)(end - p) < n) throw std::runtime_error("truncated fixed-width field");
+  }
   float f32() {
+    need(4);
     float f;
     std::memcpy(&f, p, 4);
     p += 4;
     return f;
   }
   double f64() {
+    need(8);
     double d;
     std::memcpy(&d, p, 8);
     p += 8;
@@ -50,8 +55,8 @@ struct Reader {
   }
   void skip(int wt) {
     if (wt == 0) varint();
-    else if (wt == 1) p += 8;
-    else if (wt == 5) p += 4;
+    else if (wt == 1) { need(8); p += 8; }
+    else if (wt == 5) { need(4); p += 4; }
     else if (wt == 2) sub();
     else throw std::runtime_error("unsupported wire type");
   }
@@ -206,32 +211,41 @@ std::unordered_map<std::string, DTensor> load_params(const ProgramDesc& prog, co
   std::sort(names.begin(), names.end());
   std::unordered_map<std::string, DTensor> out;
   size_t pos = 0;
-  auto need = [&](size_t n) {
-    if (pos + n > bytes.size()) throw std::runtime_error("params file truncated");
+  // overflow-safe: n bytes must remain after pos
+  auto need = [&](uint64_t n) {
+    if (pos > bytes.size() || n > (uint64_t)(bytes.size() - pos))
+      throw std::runtime_error("params file truncated or corrupt");
   };
   for (const auto& n : names) {
-    if (pos >= bytes.size()) break;  // program declares more persistables than the file holds
+    if (pos >= bytes.size())  // reference LoadCombine: every persistable must be in the file
+      throw std::runtime_error("params file ends before persistable '" + n + "'");
     need(12);
     uint64_t lod_levels;
     std::memcpy(&lod_levels, bytes.data() + pos + 4, 8);
     pos += 12;
+    if (lod_levels > 64) throw std::runtime_error("params file: implausible LoD level count");
     for (uint64_t l = 0; l < lod_levels; ++l) {
       need(8);
       uint64_t sz;
       std::memcpy(&sz, bytes.data() + pos, 8);
-      pos += 8 + sz;
+      pos += 8;
+      need(sz);
+      pos += sz;
     }
     need(8);
     int32_t dsz;
     std::memcpy(&dsz, bytes.data() + pos + 4, 4);
     pos += 8;
-    need((size_t)dsz);
+    if (dsz < 0) throw std::runtime_error("params file: negative tensor-desc size");
+    need((uint64_t)dsz);
     VarDesc td;
     parse_tensor_desc(Reader(bytes.data() + pos, (size_t)dsz), td);
     pos += (size_t)dsz;
     DTensor t;
     t.dtype = td.dtype;
     t.dims = td.dims;
+    for (int64_t d : t.dims)
+      if (d < 0 || d > (int64_t(1) << 40)) throw std::runtime_error("params file: bad dims for '" + n + "'");
     const size_t nb = t.nbytes();
     need(nb);
     t.buf = alloc_buffer(nb, false);
@@ -239,6 +253,9 @@ std::unordered_map<std::string, DTensor> load_params(const ProgramDesc& prog, co
     pos += nb;
     out[n] = std::move(t);
   }
+  if (pos != bytes.size())
+    throw std::runtime_error("params file holds " + std::to_string(bytes.size() - pos) +
+                             " bytes beyond the program's persistables");
   return out;
 }
 

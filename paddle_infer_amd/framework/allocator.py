@@ -124,15 +124,15 @@ def reset_peak(device: int = 0) -> None:
 
 
 def default_strategy() -> str:
-    """``FLAGS_allocator_strategy`` when set; otherwise ``auto_growth`` (the framework allocator)
-    for single-process jobs on a GPU. Multi-process jobs (WORLD_SIZE > 1) keep PyTorch's caching
-    allocator unless the flag asks for ``auto_growth`` explicitly: the RCCL path under the own
-    allocator is covered by the record-stream hook but has not been validated on a multi-GPU node
-    yet."""
+    """``FLAGS_allocator_strategy`` when set; otherwise ``auto_growth`` (the framework allocator),
+    for single- and multi-process jobs alike. RCCL's collectives allocate their own staging
+    buffers; the user tensors they read and write come from this allocator, and the process
+    group's ``record_stream`` calls on them reach ``piamd_record_stream`` (covered by
+    `tests/test_allocator_gpu.py` and the 2-rank collective tests)."""
     v = os.environ.get("FLAGS_allocator_strategy")
     if v:
         return v
-    return "auto_growth" if int(os.environ.get("WORLD_SIZE", "1")) <= 1 else "naive_best_fit"
+    return "auto_growth"
 
 
 def maybe_enable_from_env() -> None:

@@ -227,6 +227,8 @@ class GPTGenerator:
             st["pos"].copy_(pos)
             st["done"].copy_(done)
             st["pad"].fill_(pad)
+            if eos is not None:  # the graph reads the EOS id from st["eos"]: refresh per call
+                st["eos"].fill_(eos)
         key = ("greedy", B, eos is not None)
         ent = self._graphs.get(key)
         if ent is None:

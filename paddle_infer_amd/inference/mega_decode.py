@@ -98,13 +98,16 @@ class MegaDecoder:
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.act = 1 if gen.act == "gelu_tanh" else 0
         self.eps = float(gen.cfg.layer_norm_eps)
-        self.trace = None  # set to a zeroed int64 [256, 5·nl, 2] tensor to record phase times
+        self.trace = None  # set to a zeroed int64 [256, 5·nl, 4] tensor to record phase times
 
     def __call__(self, resid: torch.Tensor, pos: torch.Tensor) -> torch.Tensor:
         """resid: bf16 [E] embedding output; pos: device int32 [1] = the cache slot of this token.
         Returns the last layer's residual stream [E] (a view of an internal buffer)."""
         assert resid.is_contiguous() and resid.numel() == E and resid.dtype == torch.bfloat16
         assert pos.dtype == torch.int32 and pos.is_cuda
+        if self.trace is not None:  # the kernel writes 4 int64 slots per (workgroup, phase)
+            assert (self.trace.dtype == torch.int64 and self.trace.is_cuda
+                    and self.trace.numel() >= 256 * 5 * self.nl * 4), "trace must be int64 [256, 5*nl, 4]"
         a = _lib.MegaArgs(self.table.data_ptr(), self.nl, self.maxS, self.nsplit, self.act,
                           self.eps, (1.0 / math.sqrt(D)) * 1.4426950408889634, resid.data_ptr(),
                           self.rbuf.data_ptr(), self.qn.data_ptr(), self.kvn.data_ptr(), self.part.data_ptr(),

@@ -293,8 +293,10 @@ def fused_mlp_supported(x, w1, b1, w2, act):
         return False
     H, Fd = w1.shape
     T = x.numel() // H
-    return H % 64 == 0 and Fd % 64 == 0 and w2.shape == (Fd, w2.shape[1]) and w2.shape[1] % 8 == 0 \
-        and T > 0 and H >= 128 and Fd >= 128
+    # the FFN2 data-gradient GEMM reduces over w2's output width: it needs the asm K contract too
+    O = w2.shape[1]
+    return H % 64 == 0 and Fd % 64 == 0 and w2.shape == (Fd, O) and O % 64 == 0 \
+        and T > 0 and H >= 128 and Fd >= 128 and O >= 128
 
 
 def fused_mlp(x, w1, b1, w2, act="gelu_tanh"):

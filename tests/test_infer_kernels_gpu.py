@@ -238,6 +238,11 @@ def test_generation_greedy_graph_eos_and_reuse():
         b = g_graph.generate(ids, max_new_tokens=10, eos_token_id=eos, pad_token_id=0)
         assert torch.equal(a.cpu(), b.cpu()), (a, b)
     assert torch.equal(g_graph.generate(ids, max_new_tokens=10).cpu(), ref.cpu())
+    # a different EOS id through the same cached graph (the graph reads it from its state)
+    eos2 = int(ref[1, 5])
+    a2 = g_eager.generate(ids, max_new_tokens=10, eos_token_id=eos2, pad_token_id=0)
+    b2 = g_graph.generate(ids, max_new_tokens=10, eos_token_id=eos2, pad_token_id=0)
+    assert torch.equal(a2.cpu(), b2.cpu()), (a2, b2)
 
 
 def test_predictor_bf16_hip_graph(tmp_path):

@@ -118,3 +118,34 @@ def test_vision_models_match_python_predictor(tmp_path, arch):
     ref = python_outputs(path, {"x": x})
     got, _, _ = native_outputs(path, {"x": x}, tmp_path)
     np.testing.assert_allclose(got[0], ref[0], rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("damage", ["truncate_mid", "extra_bytes", "missing_tensor", "neg_desc"])
+def test_corrupt_params_file_refused(tmp_path, damage):
+    """The .pdiparams reader bounds-checks every read: truncated, padded or corrupted files are
+    refused with an error, never read out of range (reference LoadCombine errors likewise)."""
+    import struct
+    path = str(tmp_path / "mlp")
+    export(MLP(), path, [InputSpec([None, 16], "float32", "x")])
+    data = open(path + ".pdiparams", "rb").read()
+    if damage == "truncate_mid":
+        data = data[: len(data) // 2]
+    elif damage == "extra_bytes":
+        data = data + b"\0" * 16
+    elif damage == "missing_tensor":
+        # keep only the first tensor record: version(4) lod(8) ver(4) dsz(4) desc data
+        dsz = struct.unpack_from("<i", data, 16)[0]
+        pos = 20 + dsz
+        desc = data[20:pos]
+        # numel from the desc is not needed: cut right after the first record's header + desc
+        data = data[:pos]
+    elif damage == "neg_desc":
+        data = data[:16] + struct.pack("<i", -5) + data[20:]
+    bad = str(tmp_path / "bad.pdiparams")
+    open(bad, "wb").write(data)
+    x = np.ones((2, 16), "float32")
+    x.tofile(str(tmp_path / "x.bin"))
+    r = subprocess.run([RUN, path + ".pdmodel", bad, "--input", "x", "float32", "2,16",
+                        str(tmp_path / "x.bin")], capture_output=True, text=True)
+    assert r.returncode != 0, r.stdout
+    assert "params file" in r.stderr or "truncated" in r.stderr, r.stderr

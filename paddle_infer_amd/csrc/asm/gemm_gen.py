@@ -68,8 +68,11 @@ ARGS = [
     # epilogue block (loaded after the main loop)
     ("c", 96, 8), ("c_bytes", 104, 8), ("ldc_b", 112, 4), ("ldaux_b", 116, 4),
     ("c_part", 120, 8), ("aux", 128, 8), ("aux_bytes", 136, 8), ("bias", 144, 8),
+    # work-unit "part" decomposition (loaded at each tile setup): K start = part·kmul (split-K:
+    # kmul = nk·64; batched: kmul = 0) and operand base += part·{a,b}_bstride bytes (batched)
+    ("kmul", 152, 4), ("pad0", 156, 4), ("a_bstride", 160, 8), ("b_bstride", 168, 8),
 ]
-ARGS_SIZE = 152
+ARGS_SIZE = 176
 
 # ---- SGPR map ------------------------------------------------------------------------------------
 S_KARG = 0        # s[0:1]
@@ -172,8 +175,13 @@ def mc_read(WO, h, blk, j, l):
 
 # ---- emitter -------------------------------------------------------------------------------------
 class Kernel:
-    def __init__(self, name, a_kc, b_kc, ek, persistent=False):
+    def __init__(self, name, a_kc, b_kc, ek, persistent=False, f16=False):
         self.name, self.a_kc, self.b_kc = name, a_kc, b_kc
+        # operand / 16-bit output type: bf16 (default) or IEEE fp16 (same tiles and schedule;
+        # MFMA, output conversion and epilogue unpacks differ)
+        self.f16 = f16
+        self.cvt = "v_cvt_pk_f16_f32" if f16 else "v_cvt_pk_bf16_f32"
+        self.mfma_op = "v_mfma_f32_16x16x32_f16" if f16 else "v_mfma_f32_16x16x32_bf16"
         self.persistent = persistent
         self.VE = 112 if persistent else V_FRAG
         self.VBIAS, self.VTMP, self.VCONST = self.VE + E_BIAS, self.VE + E_TMP, self.VE + E_CONST
@@ -298,12 +306,15 @@ class Kernel:
         """Descriptors and DMA offsets of both operands for the tile at (m0, n0, part); ``full``
         also sets the tile-invariant LDS bases, soffsets and fragment-read bases."""
         T = S_T
-        self.e(f"s_mul_i32 s{T}, s{part}, s{S_NK}")
-        self.e(f"s_lshl_b32 s{T}, s{T}, 6")                      # K start (elements)
+        # part decomposition (split-K / batch): kmul → s{T+5}, batch strides → s[T+6:T+9]
+        self.e(f"s_load_dword s{T + 5}, s[0:1], 0x98")
+        self.e(f"s_load_dwordx4 s[{T + 6}:{T + 9}], s[0:1], 0xa0")
+        self.e("s_waitcnt lgkmcnt(0)")
+        self.e(f"s_mul_i32 s{T}, s{part}, s{T + 5}")             # K start (elements)
         for op in (0, 1):
-            self.setup_operand(op, T, m0 if op == 0 else n0, full)
+            self.setup_operand(op, T, m0 if op == 0 else n0, full, part)
 
-    def setup_operand(self, op, T, t0, full=True):
+    def setup_operand(self, op, T, t0, full=True, part=None):
         """Descriptor, K step, DMA voffsets, LDS-DMA bases and read bases of operand op; t0: SGPR
         with the tile origin along this operand's rows (A: m0, B: n0); s{T}: K start."""
         kc = self.a_kc if op == 0 else self.b_kc
@@ -338,6 +349,14 @@ class Kernel:
             self.e(f"s_lshl_b32 s{T + 3}, s{ld}, 6")
             self.e(f"s_mov_b32 s{step}, s{T + 3}")
             self.e(f"s_lshr_b32 s{step + 1}, s{ld}, 26")
+        if part is not None:  # batched: + part · bstride (64-bit)
+            slo = T + 6 + 2 * op
+            self.e(f"s_mul_i32 s{T + 3}, s{part}, s{slo}")
+            self.e(f"s_mul_hi_u32 s{T + 4}, s{part}, s{slo}")
+            self.e(f"s_add_u32 s{a}, s{a}, s{T + 3}")
+            self.e(f"s_addc_u32 s{b}, s{b}, s{T + 4}")
+            self.e(f"s_mul_i32 s{T + 3}, s{part}, s{slo + 1}")
+            self.e(f"s_add_u32 s{b}, s{b}, s{T + 3}")
         self.e(f"s_add_u32 s{srd}, s{ptr}, s{a}")
         self.e(f"s_addc_u32 s{srd + 1}, s{ptr + 1}, s{b}")
         self.e(f"s_and_b32 s{srd + 1}, s{srd + 1}, 0xffff")
@@ -494,7 +513,7 @@ class Kernel:
     def mfma(self, set_, mb, nb, zero=False):
         a, b, c = frag(set_, 0, mb), frag(set_, 1, nb), acc(mb, nb)
         src2 = "0" if zero else f"a[{c}:{c + 3}]"
-        self.e(f"v_mfma_f32_16x16x32_bf16 a[{c}:{c + 3}], v[{b}:{b + 3}], v[{a}:{a + 3}], {src2}")
+        self.e(f"{self.mfma_op} a[{c}:{c + 3}], v[{b}:{b + 3}], v[{a}:{a + 3}], {src2}")
 
     # Schedule of one K-block (128 MFMAs; slot k = after MFMA k):
     #   slots 0-21   read Y (k-half 1 of this stage)                    [phase A: MFMAs on X]
@@ -881,17 +900,17 @@ class Kernel:
                             self.unpack(t + 1, o + j // 2, 1)
                             self.e(f"v_pk_add_f32 v[{d + j}:{d + j + 1}], v[{t}:{t + 1}], v[{d + j}:{d + j + 1}]")
                     if not paired:
-                        self.e(f"v_cvt_pk_bf16_f32 v{d}, v{d}, v{d + 1}")
-                        self.e(f"v_cvt_pk_bf16_f32 v{d + 1}, v{d + 2}, v{d + 3}")
+                        self.e(f"{self.cvt} v{d}, v{d}, v{d + 1}")
+                        self.e(f"{self.cvt} v{d + 1}, v{d + 2}, v{d + 3}")
                         self.e(f"buffer_store_dwordx2 v[{d}:{d + 1}], v{V + 5}, s[{srd}:{srd + 3}], 0 offen offset:{nb * 32}")
                         issued.append(("S", mb))
                     elif nb % 2 == 1:
                         # blocks nb-1 (in d-4..d-1) and nb (d..d+3) → packed pair q..q+3, swap
                         q = d - 4
-                        self.e(f"v_cvt_pk_bf16_f32 v{q}, v{q}, v{q + 1}")
-                        self.e(f"v_cvt_pk_bf16_f32 v{q + 1}, v{q + 2}, v{q + 3}")
-                        self.e(f"v_cvt_pk_bf16_f32 v{q + 2}, v{d}, v{d + 1}")
-                        self.e(f"v_cvt_pk_bf16_f32 v{q + 3}, v{d + 2}, v{d + 3}")
+                        self.e(f"{self.cvt} v{q}, v{q}, v{q + 1}")
+                        self.e(f"{self.cvt} v{q + 1}, v{q + 2}, v{q + 3}")
+                        self.e(f"{self.cvt} v{q + 2}, v{d}, v{d + 1}")
+                        self.e(f"{self.cvt} v{q + 3}, v{d + 2}, v{d + 3}")
                         self.e("s_nop 1")
                         self.e(f"v_permlane16_swap_b32 v{q}, v{q + 2}")
                         self.e(f"v_permlane16_swap_b32 v{q + 1}, v{q + 3}")
@@ -961,7 +980,13 @@ class Kernel:
         self.e(f"v_pk_mul_f32 {Y}, {Y}, {A}")
 
     def unpack(self, dst, src, j):
-        if j % 2 == 0:
+        """f32 v{dst} ← 16-bit half j%2 of v{src} (bf16: a shift / mask; fp16: a conversion)."""
+        if self.f16:
+            if j % 2 == 0:
+                self.e(f"v_cvt_f32_f16 v{dst}, v{src}")
+            else:
+                self.e(f"v_cvt_f32_f16_sdwa v{dst}, v{src} dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1")
+        elif j % 2 == 0:
             self.e(f"v_lshlrev_b32 v{dst}, 16, v{src}")
         else:
             self.e(f"v_and_b32 v{dst}, 0xffff0000, v{src}")
@@ -977,8 +1002,8 @@ class Kernel:
             self.e(f"v_pk_add_f32 v[{d + j}:{d + j + 1}], v[{t}:{t + 1}], v[{d + j}:{d + j + 1}]")
         if not self.store_aux:
             return 0
-        self.e(f"v_cvt_pk_bf16_f32 v{p}, v{d}, v{d + 1}")
-        self.e(f"v_cvt_pk_bf16_f32 v{p + 1}, v{d + 2}, v{d + 3}")
+        self.e(f"{self.cvt} v{p}, v{d}, v{d + 1}")
+        self.e(f"{self.cvt} v{p + 1}, v{d + 2}, v{d + 3}")
         n = 0
         if not paired:
             self.e(f"buffer_store_dwordx2 v[{p}:{p + 1}], v{self.VE + 6}, s[{S_AUXSRD}:{S_AUXSRD + 3}], 0 offen offset:{nb * 32}")
@@ -1084,19 +1109,22 @@ FUSED = ("bias", "biasgelu", "biasrelu", "dgelu", "drelu", "biasnx")
 
 
 def variants():
-    """(name, A K-contiguous, B K-contiguous, epilogue, persistent). ``_p_`` kernels are the
-    persistent ones (nk even and >= 4); the others take one tile per workgroup (any nk >= 2)."""
-    for pers in (False, True):
-        tag = "p_" if pers else ""
-        for lay in ("nt", "tn", "nn", "tt"):
-            for ek in EPILOGUES:
-                yield f"piamd_agemm_{tag}{lay}_{ek}", LAYOUTS[lay][0], LAYOUTS[lay][1], ek, pers
-        for ek in FUSED:  # fused epilogues: forward / data-gradient products (both K-contiguous)
-            yield f"piamd_agemm_{tag}nt_{ek}", True, True, ek, pers
+    """(name, A K-contiguous, B K-contiguous, epilogue, persistent, fp16). ``_p_`` kernels are the
+    persistent ones (nk even and >= 4); the others take one tile per workgroup (any nk >= 2).
+    ``_f16`` kernels take IEEE fp16 operands (and write fp16 where the bf16 kernel writes bf16)."""
+    for f16 in (False, True):
+        sfx = "_f16" if f16 else ""
+        for pers in (False, True):
+            tag = "p_" if pers else ""
+            for lay in ("nt", "tn", "nn", "tt"):
+                for ek in EPILOGUES:
+                    yield f"piamd_agemm_{tag}{lay}_{ek}{sfx}", LAYOUTS[lay][0], LAYOUTS[lay][1], ek, pers, f16
+            for ek in FUSED:  # fused epilogues: forward / data-gradient products (both K-contiguous)
+                yield f"piamd_agemm_{tag}nt_{ek}{sfx}", True, True, ek, pers, f16
 
 
 def generate() -> str:
-    ks = [Kernel(n, a, b, ek, pers) for n, a, b, ek, pers in variants()]
+    ks = [Kernel(n, a, b, ek, pers, f16) for n, a, b, ek, pers, f16 in variants()]
     out = ['\t.amdgcn_target "amdgcn-amd-amdhsa--gfx950"', "\t.amdhsa_code_object_version 5"]
     for k in ks:
         out.append(k.text())

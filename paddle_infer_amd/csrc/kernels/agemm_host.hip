@@ -36,8 +36,10 @@ struct __attribute__((packed)) AgemmArgs {
   void* aux;                   // 128
   unsigned long long aux_bytes;// 136
   const void* bias;            // 144
+  unsigned kmul, pad0;         // 152: K start = part·kmul (split-K), 0 when batched
+  unsigned long long a_bstride, b_bstride;  // 160, 168: operand base += part·bstride (batched)
 };
-static_assert(sizeof(AgemmArgs) == 152, "AgemmArgs layout");
+static_assert(sizeof(AgemmArgs) == 176, "AgemmArgs layout");
 
 std::mutex g_mu;
 hipModule_t g_mod = nullptr;
@@ -111,11 +113,17 @@ PIAMD_EXPORT int piamd_agemm_loaded() { return g_mod != nullptr; }
 // M % 8 == 0 when A is [K][M]; N % 8 == 0 when B is [K][N]; 16-byte aligned pointers.
 // c_f32 / accumulate: bf16 or f32 C, stored or accumulated (C += A·B).
 // ksplit > 1: f32 partial planes in ws [ksplit][M][N], reduced in a fixed order.
+// f16: IEEE fp16 operands (and fp16 where a bf16 kernel writes 16-bit values).
+// batch > 1: C[i] (+)= op(A[i])·op(B[i]) for i < batch, operand i at base + i·s{a,b,c} elements
+// (a stride may be 0: broadcast); no split-K, no fused epilogue.
 PIAMD_EXPORT int piamd_agemm(const void* a, long long lda, int trans_a, const void* b, long long ldb,
                              int trans_b, void* c, long long ldc, int c_f32, int accumulate, int M,
                              int N, int K, int epi, int act, const void* bias, void* aux,
-                             long long ldaux, int ksplit, void* ws, hipStream_t st) {
+                             long long ldaux, int ksplit, void* ws, int f16, int batch,
+                             long long sa, long long sb, long long sc, hipStream_t st) {
   const bool a_kc = !trans_a, b_kc = trans_b;
+  if (batch < 1 || (batch > 1 && (ksplit != 1 || epi != 0 || sa < 0 || sb < 0 || sc <= 0)))
+    return (int)hipErrorInvalidValue;
   if (M <= 0 || N <= 0 || K <= 0 || ksplit < 1 || K % (64 * ksplit) || K / ksplit < 128 || N % 4 ||
       (!a_kc && M % 8) || (!b_kc && N % 8) || lda % 8 || ldb % 8 || ldc % 4 ||
       lda >= (1 << 22) || ldb >= (1 << 22) || ldc >= (1 << 26) || epi < 0 || epi > 2 ||
@@ -149,18 +157,29 @@ PIAMD_EXPORT int piamd_agemm(const void* a, long long lda, int trans_a, const vo
     g.c = c;
     g.ldc_b = (unsigned)(ldc * es);
     g.c_bytes = ((unsigned long long)(M - 1) * ldc + N) * es;
+    if (batch > 1) {
+      g.c_part = (unsigned long long)sc * es;
+      g.c_bytes += (unsigned long long)(batch - 1) * sc * es;
+    }
   }
   // persistent kernel (work units chained through the LDS-DMA stream) when every unit has an
   // even K-block count >= 4; otherwise one tile per workgroup
   const int nk = K / ksplit / 64;
   const bool persistent = nk % 2 == 0 && nk >= 4 && !getenv("PIAMD_AGEMM_NO_PERSIST");
-  const std::string name = std::string("piamd_agemm_") + (persistent ? "p_" : "") + lay + "_" + ek;
+  const std::string name = std::string("piamd_agemm_") + (persistent ? "p_" : "") + lay + "_" + ek +
+                           (f16 ? "_f16" : "");
   hipFunction_t f = get_fn(name);
   if (!f) return (int)hipErrorInvalidDeviceFunction;
   g.a = a;
   g.b = b;
   g.a_bytes = (a_kc ? (unsigned long long)(M - 1) * lda + K : (unsigned long long)(K - 1) * lda + M) * 2;
   g.b_bytes = (b_kc ? (unsigned long long)(N - 1) * ldb + K : (unsigned long long)(K - 1) * ldb + N) * 2;
+  if (batch > 1) {
+    g.a_bytes += (unsigned long long)(batch - 1) * sa * 2;
+    g.b_bytes += (unsigned long long)(batch - 1) * sb * 2;
+    g.a_bstride = (unsigned long long)sa * 2;
+    g.b_bstride = (unsigned long long)sb * 2;
+  }
   g.lda_b = (unsigned)(lda * 2);
   g.ldb_b = (unsigned)(ldb * 2);
   g.M = M;
@@ -170,7 +189,8 @@ PIAMD_EXPORT int piamd_agemm(const void* a, long long lda, int trans_a, const vo
   g.tiles_n = (N + 255) / 256;
   g.ntiles = g.tiles_m * g.tiles_n;
   g.ksplit = ksplit;
-  const long long nwg = (long long)g.ntiles * ksplit;
+  g.kmul = batch > 1 ? 0u : (unsigned)(K / ksplit);
+  const long long nwg = (long long)g.ntiles * (batch > 1 ? batch : ksplit);
   if (nwg >= (1 << 24)) return (int)hipErrorInvalidValue;
   g.nwg = (unsigned)nwg;
   g.grid = persistent ? (unsigned)std::min<long long>(nwg, num_cus()) : (unsigned)nwg;

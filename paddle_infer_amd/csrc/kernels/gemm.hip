@@ -2,9 +2,9 @@
 //
 // Parity: reference `paddle/phi/kernels/funcs/blas` matmul + `fused_gemm_epilogue_op.cu`
 // (cublasLt epilogues: bias, bias+GELU with aux, dGELU) used by FusedFeedForward / fused_linear.
-// Plain GEMMs without an epilogue stay on hipBLASLt; this kernel exists for the fusions the
-// library cannot express on MI355X (activation-gradient epilogue reading the saved
-// pre-activation, f32 main-grad accumulation, GELU-tanh with aux pre-activation output).
+// The dense GEMMs of the framework run on the assembly GEMM (csrc/asm/gemm_gen.py) and the skinny
+// kernel (gemm_small.hip); this file's main loop and epilogue serve the grouped MoE expert GEMMs
+// and the implicit-GEMM convolutions below.
 //
 // Structure (cdna_hip_programming.md §5: 256² tile, glds, BK = 64):
 //   * workgroup = 8 waves (2 M × 4 N), tile 256 × 256, each wave 128 × 64 = 4 × 2 blocks of
@@ -244,20 +244,6 @@ __device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[MB][NB], void*
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   const int xcd = orig % 8, q = nwg / 8, rr = nwg % 8;
   return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + orig / 8;
-}
-
-template <bool A_KC, bool B_KC>
-__global__ __launch_bounds__(NTHR, 1) void gemm_kernel(
-    const bf16_t* __restrict__ a, long long lda, const bf16_t* __restrict__ b, long long ldb,
-    void* __restrict__ c, long long ldc, int c_f32, int accumulate, int M, int N, int K, int epi,
-    int act, const bf16_t* __restrict__ bias, bf16_t* __restrict__ aux, long long ldaux) {
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE_BYTES];
-  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
-  const int wg = xcd_remap(blockIdx.x, tm * tn);
-  const int m0 = (wg / tn) * BM, n0 = (wg % tn) * BN;  // consecutive wg on one XCD walk N
-  f32x16 acc[4][2];
-  gemm_mainloop<A_KC, B_KC>(a, lda, M - 1, b, ldb, N - 1, m0, n0, 0, K / BK, smem, acc);
-  gemm_epilogue(acc, c, ldc, c_f32, accumulate, m0, M, n0, N, epi, act, bias, aux, ldaux);
 }
 
 // ---- grouped (MoE expert) GEMMs over expert-sorted rows --------------------------------------
@@ -787,7 +773,7 @@ PIAMD_EXPORT int piamd_gemm_i8(const void* x, long long ldx, const void* wq, lon
 // NHWC implicit-GEMM convolution forward: x [N][H][W][C], wt [Kout][R][S][C] (OHWI), y
 // [N][OH][OW][Kout], 16-bit (bf16, or IEEE fp16 when f16 != 0: same tiles on the f16 MFMA);
 // zero: ≥ 128 zero bytes (out-of-image taps); bias [Kout] (nullable, element type of x);
-// act as piamd_gemm. C % 64 == 0 (or C == 8: stem mode), Kout % 4 == 0.
+// act: epi 0 store / 1 bias+act (aux = pre-activation) / 2 dact. C % 64 == 0 (or C == 8: stem mode), Kout % 4 == 0.
 template <bool F16>
 static void conv_fwd_launch(int tile_n, bool sc, unsigned grid, hipStream_t st, const bf16_t* xb,
                             const bf16_t* wb, const bf16_t* zb, bf16_t* y, float* wsf, int ksplit,
@@ -896,35 +882,9 @@ PIAMD_EXPORT int piamd_quant_rows(const void* x, long long ldx, void* q, long lo
   return (int)hipGetLastError();
 }
 
-// trans_a: A given as [K][M] (lda ≥ M); else [M][K] (lda ≥ K).
-// trans_b: B given as [N][K] (ldb ≥ K); else [K][N] (ldb ≥ N).
-// Requirements: K % 64 == 0; M % 256 == 0 when trans_a; N % 256 == 0 when !trans_b;
-// N % 4 == 0; 16-byte aligned operand rows. c_f32: C is f32 (else bf16); accumulate: C += A·B.
-// epi: 0 store, 1 bias+act with aux = pre-activation (bf16 [M][N], may be null), 2 C = A·B ⊙ act'(aux).
-PIAMD_EXPORT int piamd_gemm(const void* a, long long lda, int trans_a, const void* b, long long ldb,
-                            int trans_b, void* c, long long ldc, int c_f32, int accumulate, int M,
-                            int N, int K, int epi, int act, const void* bias, void* aux,
-                            long long ldaux, hipStream_t st) {
-  if (K % BK || N % 4 || (trans_a && M % BM) || (!trans_b && N % BN) || M <= 0 || N <= 0 ||
-      (epi == EPI_DACT && !aux))
-    return (int)hipErrorInvalidValue;
-  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  dim3 grid(tiles), block(NTHR);
-#define GEMM_LAUNCH(AK, BKC)                                                                     \
-  hipLaunchKernelGGL((gemm_kernel<AK, BKC>), grid, block, 0, st, (const bf16_t*)a, lda,          \
-                     (const bf16_t*)b, ldb, c, ldc, c_f32, accumulate, M, N, K, epi, act,         \
-                     (const bf16_t*)bias, (bf16_t*)aux, ldaux)
-  if (!trans_a && !trans_b) GEMM_LAUNCH(true, false);
-  else if (!trans_a && trans_b) GEMM_LAUNCH(true, true);
-  else if (trans_a && !trans_b) GEMM_LAUNCH(false, false);
-  else GEMM_LAUNCH(false, true);
-#undef GEMM_LAUNCH
-  return (int)hipGetLastError();
-}
-
 // Grouped expert GEMM. x [rows][K] expert-sorted (offs[E+1] int32 on device, rows ≤ rows_cap);
 // w: trans_w=0 → [E][K][N] (N % 256 == 0), trans_w=1 → [E][N][K]; per-expert stride sw elements.
-// y [rows][N] bf16 (or f32 when y_f32); epi/act/aux as piamd_gemm, bias [E][N] (may be null).
+// y [rows][N] bf16 (or f32 when y_f32); epi/act/aux as the conv kernels (0 store, 1 bias+act, 2 dact), bias [E][N] (may be null).
 PIAMD_EXPORT int piamd_moe_gemm(const void* x, long long ldx, const void* w, long long ldw,
                                 long long sw, int trans_w, const int* offs, int E, int rows_cap,
                                 void* y, long long ldy, int y_f32, int N, int K, int epi, int act,

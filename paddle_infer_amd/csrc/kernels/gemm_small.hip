@@ -1,0 +1,218 @@
+// Skinny MFMA GEMM: C[M][N] = act(alpha · A[M][K] · B[N][K]ᵀ + bias) (+ resid) for few-row
+// products — inference linears, prefill of short prompts, small batched matmuls — where the
+// 256×256-tile assembly GEMM (csrc/asm/gemm_gen.py) would leave most of the 256 CUs idle.
+//
+// Parity: reference `paddle/phi/kernels/funcs/blas/blas_impl.cu.h` (cublas GEMM behind matmul /
+// fc / linear at small M) and `fused/fused_gemm_epilogue_op.cu` (bias / activation epilogue).
+//
+// Structure (gfx950, bf16 or fp16 operands, f32 accumulation):
+//   * A and B both K-contiguous (weights in their cached [N][K] copy), so every operand fragment
+//     is a direct 32-B-per-lane global load — no LDS staging: few rows means little reuse to win,
+//     and the weight bytes (the dominant stream) are read exactly once per workgroup.
+//   * workgroup = 4 waves over ONE output tile of TM = 16·MB rows × TN = 16·NB columns; the waves
+//     split the tile's K range (k64 steps w, w+4, …) and meet in LDS, so a small tile still keeps
+//     four loads streams in flight per CU. Grid (N/TN, M/TM, KS): KS > 1 splits K over workgroups
+//     into f32 slices ws[KS][M][N] summed (in a fixed order) by small_gemm_finish.
+//   * v_mfma_f32_16x16x32_{bf16,f16} with the operands swapped (D = B·Aᵀ blocks), so a lane owns
+//     4 consecutive output columns of one row: 8-B (16-bit) / 16-B (f32) stores. Lane group g of
+//     a k64 step loads k = 16g … 16g+15 of its row; MFMA sub-step s uses elements 8s … 8s+7 of it
+//     (a permutation of the k sum, identical for A and B).
+//   * rows ≥ M / columns ≥ N read a clamped (valid) row and are never stored.
+// Contract: K % 64 == 0, N % 4 == 0, lda / ldb % 8 == 0, 16-B aligned operands.
+#include "common.h"
+
+namespace {
+
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+
+template <bool F16>
+__device__ __forceinline__ f32x4 mma16(const u16x8& b, const u16x8& a, const f32x4& c) {
+  if constexpr (F16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, b),
+                                                  __builtin_bit_cast(f16x8_t, a), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, b),
+                                                   __builtin_bit_cast(bf16x8, a), c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float sg_act(float v, int act) {
+  switch (act) {
+    case 1: return gelu_tanh(v);
+    case 2: return gelu_erf(v);
+    case 3: return fmaxf(v, 0.f);
+    case 4: return v / (1.f + __expf(-v));
+    default: return v;
+  }
+}
+
+struct SgArgs {
+  const bf16_t* a;
+  long long lda;
+  const bf16_t* b;
+  long long ldb;
+  void* c;
+  long long ldc;
+  float* ws;  // KS > 1: f32 slices [KS][M][N]
+  const bf16_t* bias;
+  const bf16_t* resid;
+  long long ldr;
+  float alpha;
+  int M, N, K, c_f32, act;
+};
+
+// Epilogue value of (m, n..n+3) → C.
+template <bool F16>
+__device__ __forceinline__ void sg_store(const SgArgs& p, int m, int n, f32x4 v) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float x = v[j] * p.alpha + (p.bias ? h2f<F16>(p.bias[n + j]) : 0.f);
+    x = sg_act(x, p.act);
+    if (p.resid) x += h2f<F16>(p.resid[(long long)m * p.ldr + n + j]);
+    v[j] = x;
+  }
+  if (p.c_f32) {
+    *reinterpret_cast<f32x4*>((float*)p.c + (long long)m * p.ldc + n) = v;
+  } else {
+    u16x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = f2h<F16>(v[j]);
+    *reinterpret_cast<u16x4*>((bf16_t*)p.c + (long long)m * p.ldc + n) = o;
+  }
+}
+
+template <bool F16, int MB, int NB>
+__global__ __launch_bounds__(256) void small_gemm_kernel(SgArgs p) {
+  __shared__ f32x4 red[4][MB * NB][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r16 = lane & 15;
+  const int n0 = blockIdx.x * (16 * NB), m0 = blockIdx.y * (16 * MB);
+  const int kz = blockIdx.z, KS = gridDim.z;
+  const int nkb = p.K >> 6;
+  const int kb_beg = (int)((long long)nkb * kz / KS), kb_end = (int)((long long)nkb * (kz + 1) / KS);
+
+  const bf16_t* arow[MB];
+  const bf16_t* brow[NB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+    arow[mb] = p.a + (long long)min(m0 + 16 * mb + r16, p.M - 1) * p.lda + 16 * g;
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+    brow[nb] = p.b + (long long)min(n0 + 16 * nb + r16, p.N - 1) * p.ldb + 16 * g;
+
+  f32x4 acc[MB][NB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u16x8 ac[MB][2], bc[NB][2];
+  auto load = [&](int kb, u16x8 (&ad)[MB][2], u16x8 (&bd)[NB][2]) {
+    const long long k = (long long)kb << 6;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const u16x8* s = reinterpret_cast<const u16x8*>(brow[nb] + k);
+      bd[nb][0] = s[0];
+      bd[nb][1] = s[1];
+    }
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const u16x8* s = reinterpret_cast<const u16x8*>(arow[mb] + k);
+      ad[mb][0] = s[0];
+      ad[mb][1] = s[1];
+    }
+  };
+  int kb = kb_beg + w;
+  if (kb < kb_end) load(kb, ac, bc);
+  for (; kb < kb_end; kb += 4) {
+    u16x8 an[MB][2], bn[NB][2];
+    const bool more = kb + 4 < kb_end;
+    if (more) load(kb + 4, an, bn);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) acc[mb][nb] = mma16<F16>(bc[nb][s], ac[mb][s], acc[mb][nb]);
+    if (more) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) ac[mb][s] = an[mb][s];
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) bc[nb][s] = bn[nb][s];
+      }
+    }
+  }
+  // the four waves' K slices meet in LDS; wave w finishes the blocks i ≡ w (mod 4)
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) red[w][mb * NB + nb][lane] = acc[mb][nb];
+  __syncthreads();
+  // D = B·Aᵀ block: lane holds rows m = r16 of the A block, columns n = 4g + j of the B block
+#pragma unroll
+  for (int i = w; i < MB * NB; i += 4) {
+    const int mb = i / NB, nb = i % NB;
+    const int m = m0 + 16 * mb + r16, n = n0 + 16 * nb + 4 * g;
+    if (m >= p.M || n >= p.N) continue;
+    const f32x4 v = red[0][i][lane] + red[1][i][lane] + red[2][i][lane] + red[3][i][lane];
+    if (KS == 1)
+      sg_store<F16>(p, m, n, v);
+    else
+      *reinterpret_cast<f32x4*>(p.ws + ((long long)kz * p.M + m) * p.N + n) = v;
+  }
+}
+
+// C = epilogue(Σ_z ws[z]) in a fixed order; 4 columns per thread (N % 4 == 0).
+template <bool F16>
+__global__ __launch_bounds__(256) void small_gemm_finish(SgArgs p, int KS) {
+  const long long MN = (long long)p.M * p.N, q = MN / 4;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < q; i += (long long)gridDim.x * 256) {
+    const long long e = i * 4;
+    const int m = (int)(e / p.N), n = (int)(e - (long long)m * p.N);
+    f32x4 v = *reinterpret_cast<const f32x4*>(p.ws + e);
+    for (int z = 1; z < KS; ++z) v += *reinterpret_cast<const f32x4*>(p.ws + z * MN + e);
+    sg_store<F16>(p, m, n, v);
+  }
+}
+
+template <bool F16, int MB, int NB>
+void sg_launch(const SgArgs& p, int ks, hipStream_t st) {
+  dim3 grid((p.N + 16 * NB - 1) / (16 * NB), (p.M + 16 * MB - 1) / (16 * MB), ks);
+  hipLaunchKernelGGL((small_gemm_kernel<F16, MB, NB>), grid, dim3(256), 0, st, p);
+}
+
+template <bool F16>
+int sg_dispatch(const SgArgs& p, int mb, int nb, int ks, hipStream_t st) {
+#define SG_CASE(M_, N_) \
+  if (mb == M_ && nb == N_) { sg_launch<F16, M_, N_>(p, ks, st); return 0; }
+  SG_CASE(1, 1) SG_CASE(1, 2) SG_CASE(1, 4)
+  SG_CASE(2, 1) SG_CASE(2, 2) SG_CASE(2, 4)
+  SG_CASE(4, 1) SG_CASE(4, 2) SG_CASE(4, 4)
+  SG_CASE(8, 1) SG_CASE(8, 2)
+#undef SG_CASE
+  return (int)hipErrorInvalidValue;
+}
+
+}  // namespace
+
+// f16: fp16 operands / 16-bit output (else bf16). mb ∈ {1,2,4,8} (TM = 16·mb rows), nb ∈ {1,2,4}
+// (TN = 16·nb columns; mb·nb ≤ 16), ks ≥ 1 K slices (ws = ks·M·N f32 when ks > 1). bias / resid:
+// 16-bit, nullable. act: 0 none, 1 gelu_tanh, 2 gelu_erf, 3 relu, 4 silu.
+PIAMD_EXPORT int piamd_small_gemm(int f16, const void* a, long long lda, const void* b, long long ldb,
+                                  void* c, long long ldc, int c_f32, int M, int N, int K, int mb,
+                                  int nb, int ks, float alpha, const void* bias, int act,
+                                  const void* resid, long long ldr, float* ws, hipStream_t st) {
+  if (M <= 0 || N <= 0 || K <= 0 || K % 64 || N % 4 || lda % 8 || ldb % 8 || ldc % 4 || ks < 1 ||
+      ks > K / 64 || (ks > 1 && !ws) || ((uintptr_t)a | (uintptr_t)b | (uintptr_t)c) % 16)
+    return (int)hipErrorInvalidValue;
+  SgArgs p{(const bf16_t*)a, lda, (const bf16_t*)b, ldb, c, ldc, ws, (const bf16_t*)bias,
+           (const bf16_t*)resid, ldr, alpha, M, N, K, c_f32, act};
+  const int rc = f16 ? sg_dispatch<true>(p, mb, nb, ks, st) : sg_dispatch<false>(p, mb, nb, ks, st);
+  if (rc) return rc;
+  if (ks > 1) {
+    const int grid = stride_grid((long long)M * N / 4, 256);
+    if (f16) hipLaunchKernelGGL(small_gemm_finish<true>, dim3(grid), dim3(256), 0, st, p, ks);
+    else hipLaunchKernelGGL(small_gemm_finish<false>, dim3(grid), dim3(256), 0, st, p, ks);
+  }
+  return (int)hipGetLastError();
+}

@@ -184,6 +184,10 @@ def _index_select(self, *args, **kw):
 
 def _matmul(self, other, *args, **kw):
     tx, ty = kw.pop("transpose_x", False), kw.pop("transpose_y", False)
+    if not args and not kw and isinstance(other, torch.Tensor):
+        from ..ops.gemm import own_dtype, matmul as _mm
+        if own_dtype(self, other):
+            return _mm(self, other, tx, ty)
     a = self.transpose(-1, -2) if tx else self
     b = other.transpose(-1, -2) if ty else other
     return _orig("matmul")(a, b, *args, **kw)

@@ -7,7 +7,8 @@ the fork's weight-only / MoE fused multi-transformer variants
 (`fluid/operators/fused/fused_multi_transformer_{weight_only,moe}_op.cu`).
 
 How they map onto the hardware (instead of the reference's one-CUDA-op-per-layer):
-* GEMMs: hipBLASLt (bf16 MFMA) — or the in-tree weight-only int8/int4 MFMA kernel;
+* GEMMs: the framework's own kernels (``ops.gemm``: assembly GEMM / skinny MFMA kernel with bias +
+  activation epilogues) — or the in-tree weight-only int8/int4 MFMA kernel;
 * LN + residual + bias (+dropout) → one pass of ``layernorm.hip`` (fused_add_layer_norm);
 * bias + activation → ``elementwise.hip``; QKV bias + RoPE + KV-cache write → ``infer.hip``;
 * context attention → ``flash_attn.hip``; decode attention → split-K ``infer.hip``;
@@ -51,8 +52,13 @@ def _ln(x, w, b, eps):
 
 
 def _mm(x, w, bias=None, transpose=False):
-    """x @ w (+ bias), w stored [in, out] (Paddle) unless ``transpose``."""
-    y = torch.matmul(x, w.t() if transpose else w)
+    """x @ w (+ bias), w stored [in, out] (Paddle) unless ``transpose`` (own GEMMs for bf16 / fp16:
+    2-D weights through the linear path, bias in the GEMM epilogue)."""
+    if w.dim() == 2 and not transpose:
+        from ...ops.linear import linear
+        return linear(x, w, bias)
+    from ...ops.gemm import matmul
+    y = matmul(x, w, False, transpose)
     return y + bias if bias is not None else y
 
 
@@ -83,26 +89,33 @@ def attention_core(qkv, num_heads, num_kv_heads=None, attn_mask=None, causal=Fal
     if hk != hq:
         k = k.repeat_interleave(hq // hk, 1)
         v = v.repeat_interleave(hq // hk, 1)
-    s = torch.matmul(q, k.transpose(-1, -2))
+    from ...ops.gemm import matmul
+    s = matmul(q, k, False, True)
     m = _to_additive_mask(attn_mask, s.dtype)
     if m is not None:
         m = m.expand(B, hq, S, s.shape[-1]) if m.dim() == 4 else m
     p = ops.fused_softmax_mask(s, m.contiguous() if m is not None else None, scale, causal)
     p = _dropout(p, attn_dropout, training, mode)
-    o = torch.matmul(p, v)
+    o = matmul(p, v)
     return o.transpose(1, 2).reshape(B, S, hq * D)
 
 
 # ----------------------------------------------------------------------------- small fused ops
 def fused_matmul_bias(x, y, bias=None, transpose_x=False, transpose_y=False, name=None):
-    """Reference `fused_matmul_bias.py:21` (cublasLt epilogue) — hipBLASLt bias epilogue via
-    torch.addmm on 2-D operands."""
-    a = x.transpose(-1, -2) if transpose_x else x
-    b = y.transpose(-1, -2) if transpose_y else y
-    if bias is not None and a.dim() >= 2 and b.dim() == 2:
-        lead = a.shape[:-1]
-        return torch.addmm(bias, a.reshape(-1, a.shape[-1]), b).reshape(*lead, b.shape[-1])
-    out = torch.matmul(a, b)
+    """Reference `fused_matmul_bias.py:21` (cublasLt bias epilogue, `fused_gemm_epilogue_op.cu`).
+    bf16 / fp16: the framework's own GEMM with the bias in its epilogue — through the linear path
+    (own forward AND backward kernels) for a 2-D [in, out] weight, ``ops.gemm.gemm_nt`` for a
+    [out, in] one; other layouts / dtypes: ``ops.gemm.matmul`` + bias."""
+    from ...ops import gemm as G
+    if bias is not None and not transpose_x and x.dim() >= 2 and y.dim() == 2 and G.own_dtype(x, y):
+        if not transpose_y:
+            from ...ops.linear import linear
+            return linear(x, y, bias)
+        if not (torch.is_grad_enabled() and (x.requires_grad or y.requires_grad or bias.requires_grad)):
+            lead = x.shape[:-1]
+            out = G.gemm_nt(x.reshape(-1, x.shape[-1]), y.contiguous(), bias=bias)
+            return out.reshape(*lead, y.shape[0])
+    out = G.matmul(x, y, transpose_x, transpose_y)
     return out + bias if bias is not None else out
 
 
@@ -111,8 +124,16 @@ def fused_linear(x, weight, bias=None, transpose_weight=False, name=None):
 
 
 def fused_linear_activation(x, y, bias, trans_x=False, trans_y=False, activation=None):
+    """Reference `fused_matmul_bias.py` fused_linear_activation (GELU / ReLU epilogue): one own GEMM
+    with bias + activation in its epilogue at inference (GELU: the tanh form, as cublasLt's)."""
+    from ...ops import gemm as G
+    act = activation or "none"
+    if (not trans_x and x.dim() >= 2 and y.dim() == 2 and bias is not None and G.own_dtype(x, y)
+            and not (torch.is_grad_enabled() and (x.requires_grad or y.requires_grad))):
+        from ...ops.linear import linear_bias_act
+        return linear_bias_act(x, y.contiguous(), bias, act, weight_out_in=trans_y)
     out = fused_matmul_bias(x, y, None, trans_x, trans_y)
-    return ops.bias_act(out, bias, activation or "none")
+    return ops.bias_act(out, bias, act)
 
 
 def fused_bias_dropout_residual_layer_norm(x, residual, bias=None, ln_scale=None, ln_bias=None,
@@ -134,9 +155,17 @@ def fused_feedforward(x, linear1_weight, linear2_weight, linear1_bias=None, line
                       mode="upscale_in_train", ring_id=-1, add_residual=True, name=None, group=None):
     residual = x
     out = _ln(x, ln1_scale, ln1_bias, ln1_epsilon) if pre_layer_norm else x
-    h = ops.bias_act(_mm(out, linear1_weight), linear1_bias, activation)
-    h = _dropout(h, dropout1_rate, training, mode)
-    o = _mm(h, linear2_weight)
+    from ...ops.linear import fused_mlp, fused_mlp_supported
+    if ((dropout1_rate == 0.0 or not training) and linear1_bias is not None
+            and fused_mlp_supported(out, linear1_weight, linear1_bias, linear2_weight, activation)):
+        # relu / gelu_tanh: both GEMMs on the assembly kernel, bias + activation in the FFN1
+        # epilogue and the activation backward in the FFN2 data-gradient epilogue (exact-erf GELU
+        # keeps the separate bias-act kernel: the epilogue GELU is the tanh form)
+        o = fused_mlp(out, linear1_weight, linear1_bias, linear2_weight, activation)
+    else:
+        h = ops.bias_act(_mm(out, linear1_weight), linear1_bias, activation)
+        h = _dropout(h, dropout1_rate, training, mode)
+        o = _mm(h, linear2_weight)
     if group is not None:
         torch.distributed.all_reduce(o, group=group)
     if pre_layer_norm:
@@ -167,7 +196,8 @@ def fused_multi_head_attention(x, qkv_weight, linear_weight, pre_layer_norm=Fals
         qkv = _mm(out, qkv_weight)
     else:
         _, H, D, _ = qkv_weight.shape
-        qkv = F.linear(out, qkv_weight.reshape(3 * H * D, E))
+        from ...ops.gemm import matmul
+        qkv = matmul(out, qkv_weight.reshape(3 * H * D, E), False, True)
     if qkv_bias is not None:
         qkv = qkv + qkv_bias.reshape(-1)
     qkv = qkv.reshape(B, S, 3 * H, D)
@@ -177,12 +207,13 @@ def fused_multi_head_attention(x, qkv_weight, linear_weight, pre_layer_norm=Fals
         v = torch.cat([cache_kv[1], qkv[:, :, 2 * H:].transpose(1, 2)], 2)
         new_cache = torch.stack([k, v])
         q = qkv[:, :, :H].transpose(1, 2)
-        s = torch.matmul(q, k.transpose(-1, -2))
+        from ...ops.gemm import matmul
+        s = matmul(q, k, False, True)
         m = _to_additive_mask(attn_mask, s.dtype)
         p = ops.fused_softmax_mask(s, m.expand_as(s).contiguous() if m is not None else None,
                                    1.0 / math.sqrt(D))
         p = _dropout(p, attn_dropout_rate, training, mode)
-        a = torch.matmul(p, v).transpose(1, 2).reshape(B, S, H * D)
+        a = matmul(p, v).transpose(1, 2).reshape(B, S, H * D)
     else:
         a = attention_core(qkv, H, H, attn_mask, causal, attn_dropout_rate, training, mode)
     o = _mm(a, linear_weight)
@@ -248,8 +279,10 @@ class _Linear:
         from ...ops.linear import linear as _dense, linear_bias_act
         if act != "none" and bias is not None:  # one epilogue GEMM when eligible (inference)
             return linear_bias_act(x, self.w, bias, act, weight_out_in=self.trans)
-        if self.trans:
-            y = F.linear(x, self.w, bias if act == "none" else None)
+        if self.trans:  # [out, in] weight: already K-contiguous
+            from ...ops.linear import mm_nt
+            x2 = x.reshape(-1, x.shape[-1])
+            y = mm_nt(x2, self.w, bias if act == "none" else None).reshape(*x.shape[:-1], -1)
         else:  # [in, out] weight: cached K-contiguous copy, bias in the GEMM epilogue
             y = _dense(x, self.w, bias if act == "none" else None)
         return ops.bias_act(y, bias, act) if act != "none" else y

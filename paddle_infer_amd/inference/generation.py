@@ -94,7 +94,10 @@ class GPTGenerator:
         return y
 
     def _logits(self, y):
-        return self._mp_gather(torch.matmul(y, self.model.head_weight().t()))
+        from ..ops.linear import mm_nt  # own GEMM: the [V, h] table is already K-contiguous
+        w = self.model.head_weight()
+        y2 = y.reshape(-1, y.shape[-1])
+        return self._mp_gather(mm_nt(y2.contiguous(), w).reshape(*y.shape[:-1], w.shape[0]))
 
     @torch.no_grad()
     def prefill(self, input_ids, lengths):

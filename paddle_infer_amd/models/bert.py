@@ -179,7 +179,8 @@ class BertForPretraining(Layer):
             seq = seq.reshape(-1, seq.shape[-1]).index_select(0, masked_positions.reshape(-1))
         h = bias_act(_linear(seq, self.tr_w, None), self.tr_b, "gelu")
         h = layer_norm(h, self.tr_ln_w, self.tr_ln_b, self.cfg.layer_norm_eps)
-        logits = torch.matmul(h, self.bert.embeddings.word_embeddings.t()) + self.decoder_b
+        from ..ops.gemm import matmul as _mm  # tied [V, h] table: the own GEMM's NT layout
+        logits = _mm(h, self.bert.embeddings.word_embeddings, False, True) + self.decoder_b
         nsp = _linear(pooled, self.nsp_w, self.nsp_b)
         if masked_lm_labels is None:
             return logits, nsp

@@ -221,7 +221,8 @@ class _LMHeadFn(torch.autograd.Function):
         dl2 = dl.reshape(-1, w.shape[0])
         # dgrad on the [h, V] copy: both operands V-contiguous (the GEMMs' fast layout, ops/linear.py)
         dl2 = dl2.contiguous()
-        if _use_transposed(dl2, w):
+        if _use_transposed(dl2, w) or (dl2.is_cuda and dl2.dtype == w.dtype
+                                       and dl2.dtype in (torch.bfloat16, torch.float16)):
             dy = mm_nt(dl2, transposed(w)).view(ctx.shp)
         else:
             dy = torch.mm(dl2, w).view(ctx.shp)

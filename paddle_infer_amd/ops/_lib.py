@@ -198,13 +198,16 @@ def fire(p):
 
 
 _SIGS["piamd_nan_inf_check"] = [c_int, c_void_p, c_ll, c_void_p, c_int, c_void_p]
-# a, lda, trans_a, b, ldb, trans_b, c, ldc, c_f32, accumulate, M, N, K, epi, act, bias, aux, ldaux, st
-_SIGS["piamd_gemm"] = [c_void_p, c_ll, c_int, c_void_p, c_ll, c_int, c_void_p, c_ll, c_int, c_int,
-                       c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_ll, c_void_p]
-# ... same as piamd_gemm + ksplit, ws
-_SIGS["piamd_gemm_pipe"] = _SIGS["piamd_gemm"][:-1] + [c_int, c_void_p, c_void_p]
-_SIGS["piamd_agemm"] = _SIGS["piamd_gemm_pipe"]
+# a, lda, trans_a, b, ldb, trans_b, c, ldc, c_f32, accumulate, M, N, K, epi, act, bias, aux, ldaux,
+# ksplit, ws, f16, batch, sa, sb, sc, stream
+_SIGS["piamd_agemm"] = [c_void_p, c_ll, c_int, c_void_p, c_ll, c_int, c_void_p, c_ll, c_int, c_int,
+                        c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_ll, c_int, c_void_p,
+                        c_int, c_int, c_ll, c_ll, c_ll, c_void_p]
 _SIGS["piamd_agemm_load"] = [ctypes.c_char_p]
+# f16, a, lda, b, ldb, c, ldc, c_f32, M, N, K, mb, nb, ks, alpha, bias, act, resid, ldr, ws, stream
+_SIGS["piamd_small_gemm"] = [c_int, c_void_p, c_ll, c_void_p, c_ll, c_void_p, c_ll, c_int, c_int,
+                             c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_int, c_void_p,
+                             c_ll, c_void_p, c_void_p]
 _SIGS["piamd_agemm_loaded"] = []
 _SIGS["piamd_transpose_bf16"] = [c_void_p, c_void_p, c_int, c_int, c_void_p]
 _SIGS["piamd_moe_gemm"] = [c_void_p, c_ll, c_void_p, c_ll, c_ll,

@@ -1,8 +1,11 @@
-"""Hand-written MFMA GEMM with fused epilogues (``csrc/kernels/gemm.hip``).
+"""The framework's own GEMMs: the hand-scheduled gfx950 assembly GEMM (``csrc/asm/gemm_gen.py``,
+``asm_gemm``) for bf16 / fp16 products with at least a few hundred rows, and the skinny MFMA kernel
+(``csrc/kernels/gemm_small.hip``, ``small_gemm``) for few-row products (inference, prefill of short
+prompts). ``matmul`` is the dispatcher every framework matmul goes through.
 
-``gemm(a, b)`` computes ``A·B`` for 2-D operands where ``trans_a`` means ``a`` is stored
-[K, M] and ``trans_b`` means ``b`` is stored [N, K] (so weights kept [in, out] serve forward,
-data-gradient and weight-gradient products without copies). Epilogues:
+Operand convention: ``trans_a`` means ``a`` is stored [K, M] and ``trans_b`` means ``b`` is stored
+[N, K] (so weights kept [in, out] serve forward, data-gradient and weight-gradient products without
+copies). Epilogues:
 
 * ``epi="bias_act"``: ``pre = A·B + bias`` is written to ``aux`` and ``act(pre)`` to C (FFN1);
 * ``epi="dact"``: ``C = (A·B) ⊙ act'(aux)`` (the FFN1 activation backward fused into the FFN2
@@ -30,37 +33,6 @@ def _act_grad_ref(h, act):
     return g
 
 
-def supported(a, b, trans_a=False, trans_b=False):
-    """Shapes/layouts the hand-written GEMM (either kernel) accepts."""
-    if not (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16):
-        return False
-    return pipe_supported(a, b, trans_a, trans_b) or _v1_supported(a, b, trans_a, trans_b)
-
-
-def _v1_supported(a, b, trans_a, trans_b):
-    M = a.shape[1] if trans_a else a.shape[0]
-    K = a.shape[0] if trans_a else a.shape[1]
-    N = b.shape[0] if trans_b else b.shape[1]
-    return (K % 64 == 0 and N % 4 == 0 and (not trans_a or M % 256 == 0)
-            and (trans_b or N % 256 == 0) and a.stride(-1) == 1 and b.stride(-1) == 1)
-
-
-def pipe_supported(a, b, trans_a=False, trans_b=False):
-    """Contract of the pipelined kernel (`gemm_pipe.hip`): K % 64, N % 4, 8-element aligned
-    leading dims, M % 8 when A is stored [K, M], N % 8 when B is stored [K, N]; fused epilogues
-    need A stored [M, K]."""
-    if not (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16):
-        return False
-    M = a.shape[1] if trans_a else a.shape[0]
-    K = a.shape[0] if trans_a else a.shape[1]
-    N = b.shape[0] if trans_b else b.shape[1]
-    return (K % 64 == 0 and N % 4 == 0 and M > 0 and (not trans_a or M % 8 == 0)
-            and (trans_b or N % 8 == 0) and a.stride(-1) == 1 and b.stride(-1) == 1
-            and a.stride(0) % 8 == 0 and b.stride(0) % 8 == 0
-            and a.data_ptr() % 16 == 0 and b.data_ptr() % 16 == 0
-            and a.stride(0) < (1 << 22) and b.stride(0) < (1 << 22))
-
-
 NUM_CUS = 256
 
 _AGEMM_READY = [False]
@@ -80,11 +52,14 @@ def _agemm_load():
     _AGEMM_READY[0] = True
 
 
+_HALF = (torch.bfloat16, torch.float16)
+
+
 def asm_supported(a, b, trans_a=False, trans_b=False, ksplit=1):
-    """Contract of the assembly GEMM (`csrc/asm/gemm_gen.py`): K % (64·ksplit) with ≥ 2 K-blocks
-    per split, N % 4, 8-element aligned leading dims < 2^22, M % 8 when A is stored [K, M],
-    N % 8 when B is stored [K, N], 16-byte aligned operands."""
-    if not (a.is_cuda and a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16):
+    """Contract of the assembly GEMM (`csrc/asm/gemm_gen.py`): bf16 or fp16 operands of one dtype,
+    K % (64·ksplit) with ≥ 2 K-blocks per split, N % 4, 8-element aligned leading dims < 2^22,
+    M % 8 when A is stored [K, M], N % 8 when B is stored [K, N], 16-byte aligned operands."""
+    if not (a.is_cuda and a.dtype in _HALF and b.dtype == a.dtype):
         return False
     M = a.shape[1] if trans_a else a.shape[0]
     K = a.shape[0] if trans_a else a.shape[1]
@@ -99,26 +74,45 @@ def asm_supported(a, b, trans_a=False, trans_b=False, ksplit=1):
 
 def asm_gemm(a, b, trans_a=False, trans_b=False, out=None, out_f32=False, accumulate=False,
              ksplit=1, epi="none", act="none", bias=None, aux=None):
-    """C (+)= op(A)·op(B) on the hand-scheduled assembly kernels. Fused epilogues (A stored
-    [M, K], B stored [N, K], bf16 C): ``epi="bias_act"`` — pre = bf16(A·B + bias) written to
-    ``aux`` (optional), C = act(pre); ``epi="dact"`` — C = (A·B) ⊙ act'(aux). act ∈ none / gelu_tanh
-    / relu."""
+    """C (+)= op(A)·op(B) on the hand-scheduled assembly kernels (bf16 or fp16 operands; the
+    16-bit output has the operands' dtype). 3-D ``a`` / ``b`` / ``out`` run one batched launch
+    (a 2-D operand, or a batch stride of 0, broadcasts over the batch). Fused epilogues (2-D, A
+    stored [M, K], B stored [N, K], 16-bit C): ``epi="bias_act"`` — pre = 16-bit(A·B + bias)
+    written to ``aux`` (optional), C = act(pre); ``epi="dact"`` — C = (A·B) ⊙ act'(aux). act ∈
+    none / gelu_tanh / relu."""
     _agemm_load()
-    M = a.shape[1] if trans_a else a.shape[0]
-    K = a.shape[0] if trans_a else a.shape[1]
-    N = b.shape[0] if trans_b else b.shape[1]
+    batched = a.dim() == 3 or b.dim() == 3
+    nb = max(a.shape[0] if a.dim() == 3 else 1, b.shape[0] if b.dim() == 3 else 1)
+    M = a.shape[-1] if trans_a else a.shape[-2]
+    K = a.shape[-2] if trans_a else a.shape[-1]
+    N = b.shape[-2] if trans_b else b.shape[-1]
+    f16 = a.dtype == torch.float16
+    half = torch.float16 if f16 else torch.bfloat16
+    oshape = (nb, M, N) if batched else (M, N)
     if out is None:
-        out = torch.empty((M, N), dtype=torch.float32 if out_f32 else torch.bfloat16, device=a.device)
-    assert out.shape == (M, N) and out.stride(-1) == 1 and out.data_ptr() % 16 == 0
+        out = torch.empty(oshape, dtype=torch.float32 if out_f32 else half, device=a.device)
+    assert tuple(out.shape) == oshape and out.stride(-1) == 1 and out.data_ptr() % 16 == 0
+    assert out.dtype in (torch.float32, half)
     ws = None
     if ksplit > 1:
+        assert not batched
         ws = torch.empty((ksplit, M, N), dtype=torch.float32, device=a.device)
     if aux is not None:
-        assert aux.shape == (M, N) and aux.dtype == torch.bfloat16 and aux.stride(-1) == 1
-    _lib.call("piamd_agemm", a.data_ptr(), a.stride(0), int(trans_a), b.data_ptr(), b.stride(0),
-              int(trans_b), out.data_ptr(), out.stride(0), int(out.dtype == torch.float32),
+        assert aux.shape == (M, N) and aux.dtype == half and aux.stride(-1) == 1
+    if bias is not None:
+        assert bias.dtype == half and bias.is_contiguous()
+
+    def bstride(t):
+        return t.stride(0) if t.dim() == 3 and t.shape[0] > 1 else 0
+    sa, sb = bstride(a), bstride(b)
+    sc = out.stride(0) if batched else 0
+    if batched:
+        assert epi == "none" and (nb == 1 or sc > 0)
+    _lib.call("piamd_agemm", a.data_ptr(), a.stride(-2), int(trans_a), b.data_ptr(), b.stride(-2),
+              int(trans_b), out.data_ptr(), out.stride(-2), int(out.dtype == torch.float32),
               int(accumulate), M, N, K, _EPI[epi], ACTS[act], _lib.ptr(bias), _lib.ptr(aux),
-              aux.stride(0) if aux is not None else 0, ksplit, _lib.ptr(ws), _lib.stream())
+              aux.stride(0) if aux is not None else 0, ksplit, _lib.ptr(ws), int(f16), nb,
+              sa, sb, max(sc, 1), _lib.stream())
     return out
 
 
@@ -140,60 +134,300 @@ def pick_ksplit(M, N, K):
     return best
 
 
-def gemm(a, b, trans_a=False, trans_b=False, out=None, out_f32=False, accumulate=False,
-         epi="none", act="none", bias=None, aux=None, ksplit=None, impl="auto"):
-    """C = op(A)·op(B) on the hand-written MFMA kernels (CPU: fp32 PyTorch reference).
-    ``impl``: "auto" (pipelined kernel when its contract holds), "pipe", or "v1" (the 2-stage
-    kernel of gemm.hip). ``ksplit``: split-K degree (pipe, epi "none" only; None = heuristic)."""
-    M = a.shape[1] if trans_a else a.shape[0]
-    K = a.shape[0] if trans_a else a.shape[1]
-    N = b.shape[0] if trans_b else b.shape[1]
-    e, ac = _EPI[epi], ACTS[act]
-    if epi == "bias_act" and aux is None and a.is_cuda:
-        pass  # aux optional (inference)
-    if not a.is_cuda:
-        A = a.t() if trans_a else a
-        B = b.t() if trans_b else b
-        y = A.float() @ B.float()
-        if e == 1:
-            y = y + (bias.float() if bias is not None else 0.0)
-            pre = y.to(torch.bfloat16)
-            if aux is not None:
-                aux.copy_(pre)
-            y = _ref_act(pre.float(), ac)
-        elif e == 2:
-            y = y * _act_grad_ref(aux, ac)
-        if out is None:
-            return y.to(torch.float32 if out_f32 else a.dtype)
-        if accumulate:
-            out.add_(y.to(out.dtype))
-        else:
-            out.copy_(y)
-        return out
+F  # noqa
+
+
+# ---------------------------------------------------------------------------------------------
+# skinny kernel (csrc/kernels/gemm_small.hip) and the dispatcher every framework matmul uses
+# ---------------------------------------------------------------------------------------------
+_SG_SHAPES = {(1, 1), (1, 2), (1, 4), (2, 1), (2, 2), (2, 4), (4, 1), (4, 2), (4, 4), (8, 1), (8, 2)}
+
+
+def small_cfg(M, N, K):
+    """(mb, nb, ks) of the skinny kernel: 16·mb rows × 16·nb columns per workgroup, K split ks
+    ways when the tile grid alone cannot fill the 256 CUs."""
+    mb = 1 if M <= 16 else 2 if M <= 32 else 4 if M <= 64 else 8
+    tm = -(-M // (16 * mb))
+    nb = 2 if mb == 8 else 4
+    while nb > 1 and tm * -(-N // (16 * nb)) < 2 * NUM_CUS:
+        nb //= 2
+    if (mb, nb) not in _SG_SHAPES:
+        nb = 2
+    wgs = tm * -(-N // (16 * nb))
+    nkb = K // 64
+    ks = 1
+    # ≥ 4 k64 steps per workgroup (one per wave) before splitting further
+    while wgs * ks < NUM_CUS and ks * 2 <= nkb // 4:
+        ks *= 2
+    return mb, nb, ks
+
+
+def small_gemm(a, b, out=None, out_f32=False, alpha=1.0, bias=None, act="none", resid=None, cfg=None):
+    """C[M, N] = act(alpha·a[M, K]·b[N, K]ᵀ + bias) (+ resid) on the skinny MFMA kernel (both
+    operands K-contiguous bf16 / fp16, K % 64 == 0, N % 4 == 0)."""
+    M, K = a.shape
+    N = b.shape[0]
+    half = a.dtype
     if out is None:
-        out = torch.empty((M, N), dtype=torch.float32 if out_f32 else torch.bfloat16, device=a.device)
-    assert out.stride(-1) == 1 and out.shape == (M, N)
-    if aux is not None:
-        assert aux.shape == (M, N) and aux.dtype == torch.bfloat16 and aux.stride(-1) == 1
-    fused_ok = e == 0 or (not trans_a and out.dtype == torch.bfloat16 and not accumulate)
-    use_pipe = impl == "pipe" or (impl == "auto" and fused_ok and pipe_supported(a, b, trans_a, trans_b))
-    if use_pipe:
-        assert out.stride(0) % 4 == 0 and out.data_ptr() % 16 == 0
-        ks = ksplit if ksplit is not None else (pick_ksplit(M, N, K) if e == 0 else 1)
-        ws = None
-        if ks > 1:
-            ws = torch.empty((ks, M, N), dtype=torch.float32, device=a.device)
-        _lib.call("piamd_gemm_pipe", a.data_ptr(), a.stride(0), int(trans_a), b.data_ptr(),
-                  b.stride(0), int(trans_b), out.data_ptr(), out.stride(0),
-                  int(out.dtype == torch.float32), int(accumulate), M, N, K, e, ac, _lib.ptr(bias),
-                  _lib.ptr(aux), aux.stride(0) if aux is not None else 0, ks, _lib.ptr(ws),
-                  _lib.stream())
-        return out
-    _lib.call("piamd_gemm", a.data_ptr(), a.stride(0), int(trans_a), b.data_ptr(), b.stride(0),
-              int(trans_b), out.data_ptr(), out.stride(0), int(out.dtype == torch.float32),
-              int(accumulate), M, N, K, e, ac, _lib.ptr(bias), _lib.ptr(aux),
-              aux.stride(0) if aux is not None else 0, _lib.stream())
+        out = torch.empty((M, N), dtype=torch.float32 if out_f32 else half, device=a.device)
+    mb, nb, ks = cfg or small_cfg(M, N, K)
+    ws = torch.empty((ks, M, N), dtype=torch.float32, device=a.device) if ks > 1 else None
+    _lib.call("piamd_small_gemm", int(half == torch.float16), a.data_ptr(), a.stride(0),
+              b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
+              int(out.dtype == torch.float32), M, N, K, mb, nb, ks, float(alpha), _lib.ptr(bias),
+              ACTS[act], _lib.ptr(resid), resid.stride(0) if resid is not None else 0,
+              _lib.ptr(ws), _lib.stream())
     return out
 
 
-F  # noqa
+def own_dtype(*ts):
+    """The own GEMMs take bf16 / fp16 CUDA operands of one dtype."""
+    t0 = ts[0]
+    return t0.is_cuda and t0.dtype in _HALF and all(t.dtype == t0.dtype for t in ts)
+
+
+def _ceil(x, m):
+    return -(-x // m) * m
+
+
+def _kc(t, Kp, rows=None):
+    """[R, K] operand → K-contiguous, 16-B aligned, K zero-padded to Kp (and rows to ``rows``)."""
+    R, K = t.shape
+    R2 = rows or R
+    if Kp == K and R2 == R and t.stride(-1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0 \
+            and t.stride(0) < (1 << 22) and (R == 1 or t.stride(0) >= K):
+        return t
+    o = torch.zeros((R2, Kp), dtype=t.dtype, device=t.device) if (Kp != K or R2 != R) else \
+        torch.empty((R2, Kp), dtype=t.dtype, device=t.device)
+    o[:R, :K].copy_(t)
+    return o
+
+
+def use_small(M, N, K):
+    """Skinny kernel vs the 256×256-tile assembly GEMM: the asm kernel once its tile grid (with
+    split-K) fills the chip with ≥ 128-row tiles; below that the skinny kernel's 16·mb-row tiles
+    waste less of each MFMA and start more workgroups."""
+    if M > 512:
+        return False
+    tiles = -(-M // 256) * -(-N // 256)
+    return M <= 256 or tiles < 64
+
+
+_FUSED_ACTS = ("none", "gelu_tanh", "relu")
+
+
+def gemm_nt(a, b, alpha=1.0, bias=None, act="none", resid=None, out_f32=False):
+    """C[M, N] = act(alpha·a[M, K]·b[N, K]ᵀ + bias) (+ resid): the 2-D product every framework
+    matmul lowers to, on the framework's own kernels (skinny kernel for few rows, assembly GEMM
+    otherwise). bf16 / fp16 operands of one dtype; any K (zero-padded to the kernels' 64-multiple)
+    and any N (padded to a multiple of 4)."""
+    M, K = a.shape
+    N = b.shape[0]
+    half = a.dtype
+    small = use_small(M, N, K)
+    Kp = max(64 if small else 128, _ceil(K, 64))
+    Np = _ceil(N, 4) if small else (N if N % 4 == 0 else _ceil(N, 8))
+    a2 = _kc(a, Kp)
+    b2 = _kc(b, Kp, Np)
+    if bias is not None:
+        bias = bias.to(half).reshape(-1)
+        if Np != N:
+            bias = torch.nn.functional.pad(bias, (0, Np - N))
+        bias = bias.contiguous()
+    r2 = None
+    if resid is not None:
+        r2 = resid.reshape(M, N).to(half)
+        if Np != N:
+            r2 = torch.nn.functional.pad(r2, (0, Np - N))
+        if r2.stride(-1) != 1:
+            r2 = r2.contiguous()
+    if small:
+        out = small_gemm(a2, b2, out_f32=out_f32, alpha=alpha, bias=bias, act=act, resid=r2)
+    else:
+        out = _asm_nt(a2, b2, alpha, bias, act, out_f32)
+        if r2 is not None:
+            out.add_(r2)
+    return out if Np == N else out[:, :N].contiguous()
+
+
+def _asm_nt(a, b, alpha, bias, act, out_f32):
+    M, K = a.shape
+    N = b.shape[0]
+    fused = (not out_f32 and alpha == 1.0 and act in _FUSED_ACTS
+             and (bias is not None or act != "none"))
+    if fused:
+        return asm_gemm(a, b, trans_b=True, epi="bias_act", act=act, bias=bias)
+    ks = pick_ksplit(M, N, K)
+    if not asm_supported(a, b, trans_b=True, ksplit=ks):
+        ks = 1
+    out = asm_gemm(a, b, trans_b=True, out_f32=out_f32, ksplit=ks)
+    if alpha != 1.0:
+        out.mul_(alpha)
+    if bias is not None or act != "none":
+        from .activation import bias_act
+        out = bias_act(out, bias, act)
+    return out
+
+
+def _bcast_batch(x, y):
+    """Broadcast the batch dims of ≥ 3-D operands → ([Bt, ·, ·] x, [Bt, ·, ·] y, batch shape)."""
+    bx, by = x.shape[:-2], y.shape[:-2]
+    bs = torch.broadcast_shapes(bx, by)
+    def to3(t, bt):
+        if bt == bs:
+            return t.reshape(-1, *t.shape[-2:])
+        if all(d == 1 for d in bt):  # a single matrix broadcast over the batch: stride 0
+            return t.reshape(t.shape[-2:])
+        return t.expand(*bs, *t.shape[-2:]).reshape(-1, *t.shape[-2:])
+    return to3(x, bx), to3(y, by), bs
+
+
+def bmm(x, y, transpose_x=False, transpose_y=False, alpha=1.0):
+    """Batched C[i] = alpha·op(x[i])·op(y[i]) (x / y 3-D, or 2-D broadcast over the batch) as ONE
+    batched assembly-GEMM launch (operand layouts handled by the kernel's four layout variants)."""
+    nb = max(x.shape[0] if x.dim() == 3 else 1, y.shape[0] if y.dim() == 3 else 1)
+    M = x.shape[-1] if transpose_x else x.shape[-2]
+    K = x.shape[-2] if transpose_x else x.shape[-1]
+    N = y.shape[-2] if transpose_y else y.shape[-1]
+
+    def ok(t, inner_contig):
+        return (t.stride(-1) == 1 and t.stride(-2) % 8 == 0 and t.data_ptr() % 16 == 0
+                and t.stride(-2) < (1 << 22) and inner_contig
+                and (t.dim() == 2 or t.shape[0] == 1 or t.stride(0) % 8 == 0))
+
+    def sep(t):  # batch slices must not overlap (or broadcast one matrix: stride 0)
+        return t.dim() == 2 or t.shape[0] == 1 or t.stride(0) == 0 or t.shape[-2] * t.stride(-2) <= t.stride(0)
+    native = (K % 64 == 0 and K >= 128 and N % 4 == 0
+              and ok(x, not transpose_x or M % 8 == 0) and ok(y, transpose_y or N % 8 == 0)
+              and sep(x) and sep(y))
+    if native:
+        out = asm_gemm(x, y, trans_a=transpose_x, trans_b=transpose_y)
+    else:  # K-contiguous, K-padded copies: [nb, M, Kp] · [nb, N, Kp]ᵀ
+        Kp = max(128, _ceil(K, 64))
+        Np = _ceil(N, 4)
+        xa = x.transpose(-1, -2) if transpose_x else x
+        yb = y if transpose_y else y.transpose(-1, -2)
+        A = torch.zeros((*xa.shape[:-1], Kp), dtype=x.dtype, device=x.device)
+        A[..., :K].copy_(xa)
+        B = torch.zeros((*yb.shape[:-2], Np, Kp), dtype=y.dtype, device=y.device)
+        B[..., :N, :K].copy_(yb)
+        out = asm_gemm(A, B, trans_b=True)
+        if Np != N:
+            out = out[..., :N].contiguous()
+    if out.dim() == 2:
+        out = out.unsqueeze(0).expand(nb, M, N).contiguous() if nb > 1 else out.unsqueeze(0)
+    if alpha != 1.0:
+        out.mul_(alpha)
+    return out
+
+
+def _b_nk(y, transpose_y):
+    """2-D right operand as [N, K] K-contiguous: the stored matrix when transposed, else the
+    cached transposed copy (weights: transposed once, refreshed when they change)."""
+    if transpose_y:
+        return y
+    from .linear import transposed
+    if y.is_contiguous():
+        return transposed(y)
+    return y.t().contiguous()
+
+
+def matmul_fwd(x, y, transpose_x=False, transpose_y=False, alpha=1.0):
+    """paddle.matmul semantics (broadcast batch dims, 1-D operands) on the own kernels; the caller
+    checked ``own_dtype(x, y)``."""
+    xs, ys = x.dim(), y.dim()
+    if xs == 1:
+        x = x.unsqueeze(0)
+        transpose_x = False
+    if ys == 1:
+        y = y.unsqueeze(1)
+        transpose_y = False
+    if y.dim() == 2 and not (transpose_x and x.dim() > 2):
+        xa = x.transpose(-1, -2) if transpose_x else x
+        lead = xa.shape[:-1]
+        a2 = xa.reshape(-1, xa.shape[-1])
+        out = gemm_nt(a2, _b_nk(y, transpose_y), alpha=alpha)
+        out = out.reshape(*lead, out.shape[-1])
+    else:
+        if x.dim() == 2 and y.dim() > 2:
+            x = x.expand(*y.shape[:-2], *x.shape)
+        x3, y3, bs = _bcast_batch(x, y)
+        out = bmm(x3, y3, transpose_x, transpose_y, alpha)
+        out = out.reshape(*bs, *out.shape[-2:])
+    if xs == 1:
+        out = out.squeeze(-2)
+    if ys == 1:
+        out = out.squeeze(-1)
+    return out
+
+
+def _sum_to(g, shape):
+    if tuple(g.shape) == tuple(shape):
+        return g
+    while g.dim() > len(shape):
+        g = g.sum(0)
+    for i, d in enumerate(shape):
+        if d == 1 and g.shape[i] != 1:
+            g = g.sum(i, keepdim=True)
+    return g
+
+
+class _MatmulFn(torch.autograd.Function):
+    """paddle.matmul on the own kernels with its gradients on the own kernels too (reference
+    `phi/kernels/impl/matmul_grad_kernel_impl.h`): dX = dOut·Yᵀ, dY = Xᵀ·dOut, transposes folded
+    into the GEMM flags, broadcast batch dims summed."""
+
+    @staticmethod
+    def forward(ctx, x, y, tx, ty, alpha):
+        ctx.save_for_backward(x, y)
+        ctx.tx, ctx.ty, ctx.alpha = tx, ty, alpha
+        return matmul_fwd(x, y, tx, ty, alpha)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, y = ctx.saved_tensors
+        tx, ty, alpha = ctx.tx, ctx.ty, ctx.alpha
+        g = g.contiguous()
+        xs, ys = x.dim(), y.dim()
+        x2 = x.unsqueeze(0) if xs == 1 else x
+        y2 = y.unsqueeze(1) if ys == 1 else y
+        g2 = g
+        if xs == 1:
+            g2 = g2.unsqueeze(-2)
+        if ys == 1:
+            g2 = g2.unsqueeze(-1)
+        dx = dy = None
+        if ctx.needs_input_grad[0]:
+            # X' = op(x): dX' = g·op(y)ᵀ; dx = dX' or dX'ᵀ
+            if tx:
+                dx = matmul_fwd(y2, g2, ty, True, alpha)  # (g·Y'ᵀ)ᵀ = Y'·gᵀ
+            else:
+                dx = matmul_fwd(g2, y2, False, not ty, alpha)
+            dx = _sum_to(dx, x2.shape)
+            if xs == 1:
+                dx = dx.squeeze(0)
+        if ctx.needs_input_grad[1]:
+            if ty:
+                dy = matmul_fwd(g2, x2, True, tx, alpha)  # (X'ᵀ·g)ᵀ = gᵀ·X'
+            else:
+                dy = matmul_fwd(x2, g2, not tx, False, alpha)
+            dy = _sum_to(dy, y2.shape)
+            if ys == 1:
+                dy = dy.squeeze(1)
+        return dx, dy, None, None, None
+
+
+def matmul(x, y, transpose_x=False, transpose_y=False, alpha=1.0):
+    """``paddle.matmul`` / ``bmm`` / static ``matmul_v2`` / ``matmul`` / ``mul``: bf16 / fp16 CUDA
+    operands run the framework's own GEMMs (forward and backward); other dtypes / devices take
+    the PyTorch reference (fp32 GEMMs stay on the vendor library)."""
+    if own_dtype(x, y) and x.dim() >= 1 and y.dim() >= 1 and x.numel() and y.numel():
+        if torch.is_grad_enabled() and (x.requires_grad or y.requires_grad):
+            return _MatmulFn.apply(x, y, transpose_x, transpose_y, alpha)
+        return matmul_fwd(x, y, transpose_x, transpose_y, alpha)
+    if transpose_x and x.dim() > 1:
+        x = x.transpose(-1, -2)
+    if transpose_y and y.dim() > 1:
+        y = y.transpose(-1, -2)
+    out = torch.matmul(x, y)
+    return out * alpha if alpha != 1.0 else out

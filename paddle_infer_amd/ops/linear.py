@@ -4,14 +4,15 @@ Parity: ``paddle.nn.functional.linear`` (`python/paddle/nn/functional/common.py`
 ``fused_matmul_bias`` / ``fused_linear`` (`incubate/nn/functional/fused_matmul_bias.py`,
 `fluid/operators/fused/fused_gemm_epilogue_op.cu`).
 
-Every GEMM of a bf16 linear on the GPU runs on the framework's hand-scheduled assembly GEMM
-(`csrc/asm/gemm_gen.py`, ``ops.gemm.asm_gemm``): forward ``x·Wtᵀ`` with the bias in the epilogue,
-data gradient ``dy·Wᵀ``, and weight gradient ``xᵀ·dy`` accumulated straight into ``main_grad`` (a
-view into the framework's flat gradient buffer) with split-K when the tile grid is small — the
-weight gradient is never materialised as a separate tensor, and the parameter's ``_grad_ready``
-hook (the bucketed reduce-scatter/all-reduce trigger) fires right after. ``PIAMD_GEMM=blas``
-routes the same products to hipBLASLt (A/B comparisons); shapes outside the kernel contract
-(K not a multiple of 64, fp32/fp16) take hipBLASLt too.
+Every GEMM of a bf16 / fp16 linear on the GPU runs on the framework's own kernels
+(``ops.gemm.gemm_nt``): the hand-scheduled assembly GEMM (`csrc/asm/gemm_gen.py`) for products with
+many rows, the skinny MFMA kernel (`csrc/kernels/gemm_small.hip`) for few rows (inference,
+prefill). Forward ``x·Wtᵀ`` with the bias (and activation) in the epilogue, data gradient
+``dy·Wᵀ``, and weight gradient ``xᵀ·dy`` accumulated straight into ``main_grad`` (a view into the
+framework's flat gradient buffer) with split-K when the tile grid is small — the weight gradient is
+never materialised as a separate tensor, and the parameter's ``_grad_ready`` hook (the bucketed
+reduce-scatter/all-reduce trigger) fires right after. ``PIAMD_GEMM=blas`` routes the same products
+to hipBLASLt (A/B comparisons); fp32 linears stay on the library.
 
 Weight layout for the forward GEMM: on gfx950 hipBLASLt is 12-21 % faster when BOTH operands are
 contiguous along the reduction dim (`x @ Wtᵀ` with ``Wt = [out, in]``) than on Paddle's ``x @ W``
@@ -43,27 +44,38 @@ def _asm(a, b, trans_a=False, trans_b=False, ksplit=1):
     return asm_supported(a, b, trans_a, trans_b, ksplit)
 
 
-def mm_nt(x2, w_nk, bias=None):
-    """y[M, N] = x2[M, K] · w_nkᵀ (+ bias), both operands K-contiguous."""
-    if _asm(x2, w_nk, trans_b=True) and (bias is None or bias.dtype == x2.dtype):
-        from .gemm import asm_gemm
-        if bias is not None:
-            return asm_gemm(x2, w_nk, trans_b=True, epi="bias_act", act="none", bias=bias.contiguous())
-        return asm_gemm(x2, w_nk, trans_b=True)
+def _own(*ts):
+    from .gemm import own_dtype
+    return _GEMM_IMPL[0] == "asm" and own_dtype(*ts)
+
+
+def mm_nt(x2, w_nk, bias=None, act="none"):
+    """y[M, N] = act(x2[M, K] · w_nkᵀ + bias), both operands K-contiguous."""
+    if _own(x2, w_nk) and (bias is None or bias.dtype == x2.dtype):
+        from .gemm import gemm_nt
+        return gemm_nt(x2, w_nk, bias=bias, act=act)
+    if act != "none":
+        from .activation import bias_act
+        return bias_act(mm_nt(x2, w_nk), bias, act)
     if bias is not None:
         return torch.addmm(bias, x2, w_nk.t())
     return torch.mm(x2, w_nk.t())
 
 
 def wgrad_into(out, x2, dy2):
-    """out[K, N] += x2[T, K]ᵀ · dy2[T, N] (weight gradient into main_grad; split-K on small grids)."""
-    from .gemm import asm_gemm, pick_ksplit
-    if out.is_contiguous() and out.dtype in (torch.bfloat16, torch.float32) and dy2.is_contiguous():
+    """out[K, N] += x2[T, K]ᵀ · dy2[T, N] (weight gradient into main_grad; split-K on small grids).
+    Token counts off the assembly kernel's 64-multiple take the own kernels on K-contiguous copies."""
+    from .gemm import asm_gemm, gemm_nt, pick_ksplit
+    if out.is_contiguous() and out.dtype in (torch.bfloat16, torch.float32, torch.float16) \
+            and dy2.is_contiguous() and (out.dtype != torch.float16 or x2.dtype == torch.float16):
         ks = pick_ksplit(out.shape[0], out.shape[1], x2.shape[0])
         if not _asm(x2, dy2, trans_a=True, ksplit=ks):
             ks = 1
-        if _asm(x2, dy2, trans_a=True, ksplit=ks):
+        if _asm(x2, dy2, trans_a=True, ksplit=ks) and (out.dtype == torch.float32 or out.dtype == x2.dtype):
             asm_gemm(x2, dy2, trans_a=True, out=out, accumulate=True, ksplit=ks)
+            return out
+        if _own(x2, dy2):
+            out.add_(gemm_nt(x2.t().contiguous(), dy2.t().contiguous(), out_f32=out.dtype == torch.float32))
             return out
     out.addmm_(x2.t(), dy2)
     return out
@@ -120,7 +132,7 @@ class _LinearFn(torch.autograd.Function):
     def forward(ctx, x, w, b):
         shp = x.shape
         x2 = x.reshape(-1, shp[-1])
-        if _use_transposed(x2, w):
+        if _use_transposed(x2, w) or (_own(x2, w) and w.dim() == 2 and w.is_contiguous()):
             y = mm_nt(x2, transposed(w), b)
         elif b is not None:
             y = torch.addmm(b, x2, w)
@@ -148,7 +160,7 @@ class _LinearFn(torch.autograd.Function):
             if mg is not None:
                 wgrad_into(mg, x2, dy2.contiguous())
                 _fire(w)
-            elif _asm(x2, dy2.contiguous(), trans_a=True):
+            elif _own(x2, dy2):
                 dw = torch.zeros_like(w)
                 wgrad_into(dw, x2, dy2.contiguous())
             else:
@@ -164,27 +176,28 @@ class _LinearFn(torch.autograd.Function):
         return dx, dw, db
 
 
-_EPILOGUE_ACTS = {"gelu": True, "gelu_tanh": True, "relu": False}
+# the epilogue GELU is the tanh form (the reference's cublasLt GELU epilogue is too)
+_EPILOGUE_ACT = {"gelu": "gelu_tanh"}
 
 
 def linear_bias_act(x, weight, bias, act="gelu", weight_out_in=False):
-    """Inference ``act(x @ weight + bias)`` as ONE hipBLASLt GEMM with the bias+activation
-    epilogue on the cached K-contiguous weight (`torch._addmm_activation`). Parity: the
-    reference's ``fused_gemm_epilogue`` / ``fc`` + act (`fused_gemm_epilogue_op.cu:229`,
-    CUBLASLT_EPILOGUE_GELU_BIAS — the library's GELU epilogue is the tanh form, for "gelu" too).
-    One bf16 rounding instead of two and no [T, F] round trip through HBM: 0.158 vs 0.190 ms on
-    BERT-Large FFN1 at 16k tokens (`profiles/gelu_epilogue_r1.txt`). Falls back to
-    GEMM + HIP bias-act when autograd is live or the shape/dtype is not eligible.
-    ``weight_out_in``: ``weight`` is stored ``[out, in]`` (already K-contiguous)."""
+    """Inference ``act(x @ weight + bias)`` as ONE own GEMM with the bias + activation in its
+    epilogue on the cached K-contiguous weight (``ops.gemm.gemm_nt``: assembly-GEMM epilogue for
+    many rows, skinny-kernel epilogue for few). Parity: the reference's ``fused_gemm_epilogue`` /
+    ``fc`` + act (`fused_gemm_epilogue_op.cu:229`, CUBLASLT_EPILOGUE_GELU_BIAS — that epilogue's
+    GELU is the tanh form, for "gelu" too, and so is this one). One 16-bit rounding instead of
+    two and no [T, F] round trip through HBM. Falls back to GEMM + HIP bias-act when autograd is
+    live. ``weight_out_in``: ``weight`` is stored ``[out, in]`` (already K-contiguous)."""
     from .activation import bias_act
     shp = x.shape
     x2 = x.reshape(-1, shp[-1])
     n_out = weight.shape[0] if weight_out_in else weight.shape[1]
-    if (act in _EPILOGUE_ACTS and bias is not None and bias.dtype == x2.dtype
-            and not torch.is_grad_enabled()
-            and _use_transposed(x2, weight, INFER_TRANSPOSED_MIN_ROWS)):
-        wk = weight.t() if weight_out_in else transposed(weight).t()
-        y = torch._addmm_activation(bias, x2, wk, use_gelu=_EPILOGUE_ACTS[act])
+    if (bias is not None and bias.dtype == x2.dtype and not torch.is_grad_enabled()
+            and _own(x2, weight) and weight.dim() == 2
+            and (weight_out_in or weight.is_contiguous())):
+        from .gemm import gemm_nt
+        wk = weight if weight_out_in else transposed(weight)
+        y = gemm_nt(x2, wk, bias=bias, act=_EPILOGUE_ACT.get(act, act))
         return y.view(*shp[:-1], n_out)
     if weight_out_in:
         return bias_act(torch.nn.functional.linear(x, weight), bias, act)
@@ -214,6 +227,12 @@ def linear(x, weight, bias=None):
     # inference weights: same K-contiguous cached copy + bias-in-epilogue GEMM as training
     shp = x.shape
     x2 = x.reshape(-1, shp[-1])
+    if _own(x2, weight) and weight.dim() == 2 and weight.is_contiguous():
+        ok_b = bias is None or bias.dtype == x2.dtype
+        y = mm_nt(x2, transposed(weight), bias if ok_b else None)
+        if not ok_b:
+            y = y + bias
+        return y.view(*shp[:-1], weight.shape[1])
     if not _use_transposed(x2, weight, INFER_TRANSPOSED_MIN_ROWS):
         if bias is not None and bias.dtype == x2.dtype and x2.dim() == 2:
             return torch.addmm(bias, x2, weight).view(*shp[:-1], weight.shape[1])

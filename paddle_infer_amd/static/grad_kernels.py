@@ -124,8 +124,9 @@ def _mm_grads(x, y, g, tx, ty):
     if vec_y:
         yv = yv.unsqueeze(-1)
         g = g.unsqueeze(-1)
-    dxv = torch.matmul(g, yv.transpose(-1, -2))
-    dyv = torch.matmul(xv.transpose(-1, -2), g)
+    from ..ops.gemm import matmul as _mm  # own GEMMs for bf16 / fp16, transposes as kernel flags
+    dxv = _mm(g, yv, False, True)
+    dyv = _mm(xv, g, True, False)
     dxv = _sum_to(dxv, xv.shape)
     dyv = _sum_to(dyv, yv.shape)
     if vec_x:

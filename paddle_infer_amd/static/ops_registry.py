@@ -70,34 +70,29 @@ def run_paddle_op(op, sub, env, scope):
             env[n] = v
 
 
+# matmul-family ops lower to ops.gemm.matmul: bf16 / fp16 on the framework's own GEMMs (skinny
+# MFMA kernel / assembly GEMM / batched assembly GEMM), transposes folded into the kernel layouts
 @register("matmul_v2")
 def _matmul_v2(ins, a):
-    x, y = ins["X"][0], ins["Y"][0]
-    if a.get("trans_x"):
-        x = x.transpose(-1, -2)
-    if a.get("trans_y"):
-        y = y.transpose(-1, -2)
-    return {"Out": torch.matmul(x, y)}
+    from ..ops.gemm import matmul as _mm
+    return {"Out": _mm(ins["X"][0], ins["Y"][0], bool(a.get("trans_x")), bool(a.get("trans_y")))}
 
 
 @register("matmul")
 def _matmul(ins, a):
-    x, y = ins["X"][0], ins["Y"][0]
-    if a.get("transpose_X"):
-        x = x.transpose(-1, -2)
-    if a.get("transpose_Y"):
-        y = y.transpose(-1, -2)
-    out = torch.matmul(x, y)
+    from ..ops.gemm import matmul as _mm
     alpha = a.get("alpha", 1.0)
-    return {"Out": out * alpha if alpha not in (None, 1.0) else out}
+    return {"Out": _mm(ins["X"][0], ins["Y"][0], bool(a.get("transpose_X")),
+                       bool(a.get("transpose_Y")), 1.0 if alpha is None else float(alpha))}
 
 
 @register("mul")
 def _mul(ins, a):
+    from ..ops.gemm import matmul as _mm
     x, y = ins["X"][0], ins["Y"][0]
     xn = a.get("x_num_col_dims", 1)
     x2 = x.reshape(int(np.prod(x.shape[:xn])), -1)
-    out = x2 @ y.reshape(x2.shape[1], -1)
+    out = _mm(x2, y.reshape(x2.shape[1], -1))
     return {"Out": out.reshape(*x.shape[:xn], -1)}
 
 
@@ -629,6 +624,19 @@ def _fused_multi_transformer_wo(ins, a):
     return {"Out": y, "CacheKVOut": caches or []}
 
 
+def _cached_view(w, shape):
+    """A reshaped view of a weight kept on the weight itself, so per-weight caches (the
+    K-contiguous transposed copy of ``ops.linear.transposed``) survive across runs."""
+    v = getattr(w, "_piamd_view", None)
+    if v is None or tuple(v.shape) != tuple(shape) or v.data_ptr() != w.data_ptr():
+        v = w.reshape(shape)
+        try:
+            w._piamd_view = v
+        except (AttributeError, RuntimeError):
+            pass
+    return v
+
+
 @register("multihead_matmul")
 def _multihead_matmul(ins, a):
     """Reference `fused/multihead_matmul_op.cu`: Input [B, S, E] · W [E, 3, E] + Bias [3, E],
@@ -639,7 +647,8 @@ def _multihead_matmul(ins, a):
     B, S, E = x.shape
     H = int(a["head_number"])
     D = E // H
-    qkv = linear(x.reshape(B * S, E), w.reshape(E, 3 * E), bias.reshape(3 * E)).reshape(B, S, 3, H, D)
+    qkv = linear(x.reshape(B * S, E), _cached_view(w, (E, 3 * E)),
+                 bias.reshape(3 * E)).reshape(B, S, 3, H, D)
     qkv = qkv.reshape(B, S, 3 * H, D)
     mask = ins["BiasQK"][0] if ins.get("BiasQK") else None
     scale = float(a.get("alpha", 1.0 / D ** 0.5))

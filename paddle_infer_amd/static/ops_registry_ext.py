@@ -636,14 +636,13 @@ def _fused_gemm_epilogue(ins, a):
     lead = x.shape[:-1]
     x2 = x.reshape(-1, x.shape[-1])
     from ..ops import gemm as G
-    if (x2.is_cuda and x2.dtype == torch.bfloat16 and y.dtype == x2.dtype and b.dtype == x2.dtype
-            and actk in ("none", "relu", "gelu_tanh")):
-        wt = y.t().contiguous()
-        x2c = x2.contiguous()
-        if G.asm_supported(x2c, wt, trans_b=True):
-            aux = torch.empty(x2.shape[0], y.shape[1], dtype=x2.dtype, device=x2.device) if actk != "none" else None
-            out = G.asm_gemm(x2c, wt, trans_b=True, epi="bias_act", act=actk, bias=b.contiguous(), aux=aux)
-            return {"Out": out.reshape(*lead, -1), "ReserveSpace": aux if aux is not None else []}
+    if G.own_dtype(x2, y, b) and actk in ("none", "relu", "gelu_tanh", "gelu"):
+        # own GEMM with the bias + activation in its epilogue; the pre-activation (ReserveSpace,
+        # kept by the reference for its grad op) is not materialised for inference
+        from ..ops.linear import transposed
+        wt = transposed(y) if y.is_contiguous() else y.t().contiguous()
+        out = G.gemm_nt(x2, wt, bias=b, act=actk)
+        return {"Out": out.reshape(*lead, -1), "ReserveSpace": []}
     pre = x2 @ y + b
     out = {"none": lambda t: t, "relu": F.relu, "gelu_tanh": lambda t: F.gelu(t, approximate="tanh"),
            "gelu": F.gelu}[actk](pre)

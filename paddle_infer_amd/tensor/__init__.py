@@ -248,8 +248,16 @@ inner = _binary(torch.inner)
 outer = _binary(torch.outer)
 dot = _binary(lambda x, y: (x * y).sum(-1))
 mv = _binary(torch.mv)
-mm = _binary(torch.mm)
-bmm = _binary(torch.bmm)
+def mm(input, mat2, name=None):  # noqa: A002
+    """2-D matrix product (bf16 / fp16 CUDA: the framework's own GEMMs, ``ops.gemm.matmul``)."""
+    from ..ops.gemm import matmul as _mm
+    return _mm(input, mat2)
+
+
+def bmm(x, y, name=None):
+    """Batched [B, M, K] · [B, K, N] (bf16 / fp16 CUDA: one batched assembly-GEMM launch)."""
+    from ..ops.gemm import matmul as _mm
+    return _mm(x, y)
 cross = lambda x, y, axis=9, name=None: torch.cross(x, y, dim=-1 if axis == 9 else axis)  # noqa: E731
 
 
@@ -304,15 +312,20 @@ def add_n(inputs, name=None):
 
 
 def addmm(input, x, y, beta=1.0, alpha=1.0, name=None):  # noqa: A002
+    from ..ops.gemm import own_dtype, matmul as _mm
+    if own_dtype(x, y) and x.dim() == 2 and y.dim() == 2:
+        out = _mm(x, y, alpha=alpha)
+        return out + (input if beta == 1.0 else beta * input)
     return torch.addmm(input, x, y, beta=beta, alpha=alpha)
 
 
 def matmul(x, y, transpose_x=False, transpose_y=False, name=None):
-    if transpose_x:
-        x = x.transpose(-1, -2) if x.dim() > 1 else x
-    if transpose_y:
-        y = y.transpose(-1, -2) if y.dim() > 1 else y
-    return torch.matmul(x, y)
+    """``paddle.matmul`` (reference `python/paddle/tensor/linalg.py` matmul → phi matmul kernel):
+    bf16 / fp16 CUDA operands run the framework's own GEMMs forward and backward (skinny MFMA kernel
+    for few rows, assembly GEMM otherwise, one batched launch for batched operands); other dtypes
+    take PyTorch."""
+    from ..ops.gemm import matmul as _mm
+    return _mm(x, y, transpose_x, transpose_y)
 
 
 def einsum(equation, *operands):

@@ -298,11 +298,68 @@ def _lin(w, scale=None, bits=0, trans=False, act_scale=None):
     return _Linear(w, scale, bits, trans, act_scale=act_scale)
 
 
+def _rope_table(x, cos, sin, chunks, decode):
+    """Rotary embedding from an EXTERNAL cos / sin table (reference ``RotaryPosEmb`` input,
+    `fused_multi_transformer_op.h:1600` RotrayKernel / mmha `apply_rotary_emb`): the head dim is
+    cut into ``chunks`` pieces of width L, each rotated half-against-half (neox style). x
+    [B, S, H, D]; cos / sin [B, S, D]. Context rows take the table entry of the first-half index for
+    both halves (RotrayKernel); the decode step takes each element's own entry (mmha)."""
+    B, S, H, D = x.shape
+    L = D // chunks
+    h = L // 2
+    xf = x.float().reshape(B, S, H, chunks, 2, h)
+    c = cos.float().reshape(B, S, 1, chunks, 2, h)
+    sn = sin.float().reshape(B, S, 1, chunks, 2, h)
+    left, right = xf[..., 0, :], xf[..., 1, :]
+    if decode:
+        ol = left * c[..., 0, :] - right * sn[..., 0, :]
+        orr = right * c[..., 1, :] + left * sn[..., 1, :]
+    else:
+        ol = left * c[..., 0, :] - right * sn[..., 0, :]
+        orr = right * c[..., 0, :] + left * sn[..., 0, :]
+    return torch.stack([ol, orr], -2).reshape(B, S, H, D).to(x.dtype)
+
+
+def _attend_ext(qkv, bias, kc, vc, B, S, hq, hk, D, attn_mask, causal, rope, pre_kv, decode,
+                lens=None, max_len=None):
+    """Attention with an external RoPE table and / or prefix K/V (reference ``PreCaches``
+    [2, B, Hk, P, D]): bias + table rotation on the QKV rows, the prefix written to cache slots
+    [0, P) ahead of the new tokens, queries attending to [prefix | new] keys (bottom-right causal
+    band, or SrcMask [B, 1|H, S, P+S])."""
+    x = qkv.view(B, S, hq + 2 * hk, D)
+    if bias is not None:
+        x = x + bias.view(hq + 2 * hk, D).to(x.dtype)
+    q, k, v = x[:, :, :hq], x[:, :, hq:hq + hk], x[:, :, hq + hk:]
+    if rope is not None:
+        cos, sin, chunks = rope
+        q = _rope_table(q, cos, sin, chunks, decode)
+        k = _rope_table(k, cos, sin, chunks, decode)
+    if decode:  # rotated row → the split-K decode kernel (cache write of the new k / v in-kernel)
+        row = torch.cat([q, k, v], 2).reshape(B, (hq + 2 * hk) * D).contiguous()
+        return _inf.decode_attention(row, kc, vc, lens, hq, hk, attn_mask, max_len=max_len,
+                                     prep_bias=None, prep=True, rot_dim=0)
+    P = 0
+    if pre_kv is not None:
+        P = pre_kv.shape[3]
+        pk = pre_kv[0].transpose(1, 2).to(k.dtype)  # [B, P, Hk, D]
+        pv = pre_kv[1].transpose(1, 2).to(v.dtype)
+        kf, vf = torch.cat([pk, k], 1), torch.cat([pv, v], 1)
+    else:
+        kf, vf = k, v
+    if kc is not None:  # reference write_cache_kv: slots [0, P + S)
+        kc[:, :, :P + S].copy_(kf.transpose(1, 2))
+        vc[:, :, :P + S].copy_(vf.transpose(1, 2))
+    m = _to_additive_mask(attn_mask, x.dtype) if attn_mask is not None else None
+    o = ops.flash_attention(q.contiguous(), kf.contiguous(), vf.contiguous(),
+                            causal and m is None, 1.0 / math.sqrt(D), attn_mask=m)
+    return o.reshape(B * S, hq * D)
+
+
 def multi_transformer_forward(x, layers, num_heads, num_kv_heads=None, pre_layer_norm=True,
                               epsilon=1e-5, caches=None, pos=None, lens=None, attn_mask=None,
                               decode=False, activation="gelu", rotary_dim=0, neox_rotary=True,
                               rope_base=10000.0, causal=None, group=None, max_len=None,
-                              moe_fn=None, final_ln=None):
+                              moe_fn=None, final_ln=None, rope_table=None, pre_caches=None):
     """Core of every fused multi-transformer variant.
 
     x: [B, S, E]; ``layers``: list of dicts with keys ln_scale, ln_bias, qkv (_Linear producing
@@ -310,7 +367,10 @@ def multi_transformer_forward(x, layers, num_heads, num_kv_heads=None, pre_layer
     ffn2, ffn2_bias (or ``moe`` — a callable replacing the FFN). ``caches``: per layer
     (k_cache, v_cache) [B, Hk, maxS, D]. Context (decode=False): writes positions
     pos[b] + [0, S). Decode (S == 1): writes position pos[b] and attends to keys [0, lens[b]).
-    ``pos``/``lens`` are device int32 [B] (graph-replayable).
+    ``pos``/``lens`` are device int32 [B] (graph-replayable). ``rope_table``: (cos, sin, chunks) —
+    RoPE from an external table instead of the in-kernel angles; ``pre_caches``: per layer prefix
+    K/V [2, B, Hk, P, D] attended ahead of the context tokens (both: reference
+    ``fused_multi_transformer`` RotaryPosEmb / PreCaches inputs).
     """
     B, S, E = x.shape
     hq = num_heads
@@ -324,7 +384,8 @@ def multi_transformer_forward(x, layers, num_heads, num_kv_heads=None, pre_layer
     if decode and attn_mask is not None:
         attn_mask = _to_additive_mask(attn_mask, x.dtype).reshape(B, -1).contiguous()
     xf = x.reshape(T, E)
-    if (decode and pre_layer_norm and group is None and not gated and moe_fn is None
+    ext = rope_table is not None or pre_caches is not None
+    if (decode and pre_layer_norm and group is None and not gated and moe_fn is None and not ext
             and x.dtype == torch.bfloat16
             and all(L.get("moe") is None
                     and all(L.get(k) is not None and L[k].dtype == torch.bfloat16
@@ -370,7 +431,11 @@ def multi_transformer_forward(x, layers, num_heads, num_kv_heads=None, pre_layer
         pending = None
         qkv = L["qkv"](xn)  # [T, (Hq+2Hk)*D]
         kc, vc = caches[li] if caches is not None else (None, None)
-        if decode:  # bias + RoPE + cache write fused into the split-K attention kernel
+        if ext:
+            a = _attend_ext(qkv, L.get("qkv_bias"), kc, vc, B, S, hq, hk, D, attn_mask, causal,
+                            rope_table, pre_caches[li] if pre_caches is not None else None, decode,
+                            lens, max_len)
+        elif decode:  # bias + RoPE + cache write fused into the split-K attention kernel
             a = _inf.decode_attention(qkv, kc, vc, lens, hq, hk, attn_mask, max_len=max_len,
                                       prep_bias=L.get("qkv_bias"), prep=True, rot_dim=rotary_dim,
                                       neox=neox_rotary, base=rope_base)
@@ -441,6 +506,17 @@ def _positions(B, time_step, seq_lens, S, device, decode):
     return torch.zeros(B, dtype=torch.int32, device=device), None
 
 
+def ext_inputs(rotary_embs, rotary_table_dims, pre_caches, B, D, device, decode):
+    """(rope_table, pre_caches) for multi_transformer_forward from the op's RotaryPosEmb
+    [2, B, 1, S, D] and PreCaches inputs (a prefix only matters to the context stage: afterwards it
+    lives in the cache)."""
+    rope = None
+    if rotary_embs is not None:
+        t = rotary_embs.to(device)
+        rope = (t[0].reshape(B, -1, D), t[1].reshape(B, -1, D), int(rotary_table_dims or 1))
+    return rope, (None if decode else pre_caches)
+
+
 def _caches_from(cache_kvs):
     if cache_kvs is None:
         return None
@@ -454,11 +530,16 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
                             attn_mask=None, dropout_rate=0.0, activation="gelu", training=False,
                             mode="upscale_in_train", trans_qkvw=True, ring_id=-1, name=None,
                             num_kv_heads=None, rotary_emb_dims=0, use_neox_rotary_style=True,
-                            rope_base=10000.0, group=None, causal=False):
+                            rope_base=10000.0, group=None, causal=False, pre_caches=None,
+                            rotary_embs=None, rotary_table_dims=1):
     """Reference `incubate/nn/functional/fused_transformer.py:833`. cache_kvs: per layer
     [2, B, Hk, max_seq_len, D], updated in place; returns (out, cache_kvs) when given. Context
     attention is full (the reference op's semantics without SrcMask) unless ``causal`` (an
-    extension: the bottom-right causal band without materialising a mask)."""
+    extension: the bottom-right causal band without materialising a mask).
+    ``rotary_emb_dims`` here (dygraph extension) = rotated head dims with in-kernel angles;
+    ``rotary_embs`` = the op's RotaryPosEmb table [2, B, 1, S, D] (``rotary_table_dims`` = its
+    reference ``rotary_emb_dims``: the head-dim chunk count); ``pre_caches`` = PreCaches, per
+    layer [2, B, Hk, P, D] prefix K/V (context stage)."""
     B, S, E = x.shape
     w0 = qkv_weights[0]
     if trans_qkvw:
@@ -474,6 +555,9 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
         for c in cache_kvs:
             c.copy_(c.index_select(1, src))
     pos, lens = _positions(B, time_step, seq_lens, S, x.device, decode)
+    rope, pre_caches = ext_inputs(rotary_embs, rotary_table_dims, pre_caches, B, D, x.device, decode)
+    if rope is not None:
+        rotary_emb_dims = 0
     layers = []
     for i in range(len(qkv_weights)):
         layers.append(dict(
@@ -488,7 +572,8 @@ def fused_multi_transformer(x, ln_scales, ln_biases, qkv_weights, qkv_biases, li
         out = multi_transformer_forward(
             x, layers, hq, hk, pre_layer_norm, epsilon, _caches_from(cache_kvs), pos, lens,
             attn_mask, decode, activation, rotary_emb_dims, use_neox_rotary_style, rope_base,
-            causal=causal and attn_mask is None, group=group)
+            causal=causal and attn_mask is None, group=group, rope_table=rope,
+            pre_caches=pre_caches)
     return (out, cache_kvs) if cache_kvs is not None else out
 
 
@@ -501,15 +586,20 @@ def fused_multi_transformer_weight_only(x, ln_scales, ln_biases, qkv_weights, qk
                                         attn_mask=None, activation="gelu", weight_dtype="int8",
                                         num_heads=None, num_kv_heads=None, rotary_emb_dims=0,
                                         use_neox_rotary_style=True, rope_base=10000.0, group=None,
-                                        causal=False):
+                                        causal=False, pre_caches=None, rotary_embs=None,
+                                        rotary_table_dims=1):
     """Reference `fused_multi_transformer_weight_only_op.cu`: every projection is a
-    weight-only int8/int4 GEMM (packed [N, K] / [N/2, K] weights, per-channel f32 scales)."""
+    weight-only int8/int4 GEMM (packed [N, K] / [N/2, K] weights, per-channel f32 scales).
+    RotaryPosEmb / PreCaches as :func:`fused_multi_transformer`."""
     B, S, E = x.shape
     bits = 4 if weight_dtype == "int4" else 8
     hk = num_kv_heads or num_heads
     D = E // num_heads
     decode = time_step is not None
     pos, lens = _positions(B, time_step, seq_lens, S, x.device, decode)
+    rope, pre_caches = ext_inputs(rotary_embs, rotary_table_dims, pre_caches, B, D, x.device, decode)
+    if rope is not None:
+        rotary_emb_dims = 0
     layers = []
     for i in range(len(qkv_weights)):
         layers.append(dict(
@@ -524,7 +614,8 @@ def fused_multi_transformer_weight_only(x, ln_scales, ln_biases, qkv_weights, qk
         out = multi_transformer_forward(
             x, layers, num_heads, hk, pre_layer_norm, epsilon, _caches_from(cache_kvs), pos, lens,
             attn_mask, decode, activation, rotary_emb_dims, use_neox_rotary_style, rope_base,
-            causal=causal and attn_mask is None, group=group)
+            causal=causal and attn_mask is None, group=group, rope_table=rope,
+            pre_caches=pre_caches)
     return (out, cache_kvs) if cache_kvs is not None else out
 
 

@@ -176,18 +176,18 @@ class _LinearFn(torch.autograd.Function):
         return dx, dw, db
 
 
-# the epilogue GELU is the tanh form (the reference's cublasLt GELU epilogue is too)
-_EPILOGUE_ACT = {"gelu": "gelu_tanh"}
+
 
 
 def linear_bias_act(x, weight, bias, act="gelu", weight_out_in=False):
     """Inference ``act(x @ weight + bias)`` as ONE own GEMM with the bias + activation in its
     epilogue on the cached K-contiguous weight (``ops.gemm.gemm_nt``: assembly-GEMM epilogue for
-    many rows, skinny-kernel epilogue for few). Parity: the reference's ``fused_gemm_epilogue`` /
-    ``fc`` + act (`fused_gemm_epilogue_op.cu:229`, CUBLASLT_EPILOGUE_GELU_BIAS — that epilogue's
-    GELU is the tanh form, for "gelu" too, and so is this one). One 16-bit rounding instead of
-    two and no [T, F] round trip through HBM. Falls back to GEMM + HIP bias-act when autograd is
-    live. ``weight_out_in``: ``weight`` is stored ``[out, in]`` (already K-contiguous)."""
+    many rows — bias / bias+ReLU / bias+GELU(tanh); exact-erf GELU and SiLU as GEMM + one HIP
+    bias-act pass — and the skinny-kernel epilogue, every activation, for few rows). Parity: the
+    reference's ``fused_gemm_epilogue`` / ``fc`` + act (`fused_gemm_epilogue_op.cu:229`). "gelu"
+    is the exact erf form (phi GeluFunctor), "gelu_tanh" the tanh approximation. Falls back to
+    GEMM + HIP bias-act when autograd is live. ``weight_out_in``: ``weight`` is stored
+    ``[out, in]`` (already K-contiguous)."""
     from .activation import bias_act
     shp = x.shape
     x2 = x.reshape(-1, shp[-1])
@@ -197,7 +197,7 @@ def linear_bias_act(x, weight, bias, act="gelu", weight_out_in=False):
             and (weight_out_in or weight.is_contiguous())):
         from .gemm import gemm_nt
         wk = weight if weight_out_in else transposed(weight)
-        y = gemm_nt(x2, wk, bias=bias, act=_EPILOGUE_ACT.get(act, act))
+        y = gemm_nt(x2, wk, bias=bias, act=act)
         return y.view(*shp[:-1], n_out)
     if weight_out_in:
         return bias_act(torch.nn.functional.linear(x, weight), bias, act)

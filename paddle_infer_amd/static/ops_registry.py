@@ -578,13 +578,24 @@ def _fmt_common(ins, a):
     if ins.get("TimeStep"):
         ts = ins["TimeStep"][0]
         time_step = int(ts.reshape(-1)[0].item()) if ts.numel() == 1 else ts
-    return dict(pre_layer_norm=bool(a.get("pre_layer_norm", True)), epsilon=float(a.get("epsilon", 1e-5)),
+    # RotaryPosEmb [2, B, 1, S, D] (cos | sin) with rotary_emb_dims = head-dim chunks; PreCaches:
+    # per layer prefix K/V [2, B, H, P, D] (`fused_multi_transformer_op.cc:166,170`)
+    rd = int(a.get("rotary_emb_dims", 0) or 0)
+    rot = ins["RotaryPosEmb"][0] if ins.get("RotaryPosEmb") else None
+    if rd and rot is None:
+        raise ValueError("fused_multi_transformer: rotary_emb_dims != 0 needs the RotaryPosEmb input")
+    ext = {}
+    if rot is not None and rd:
+        ext = dict(rotary_embs=rot, rotary_table_dims=rd)
+    if ins.get("PreCaches") and any(t is not None for t in ins["PreCaches"]):
+        ext["pre_caches"] = _seq(ins, "PreCaches")
+    return dict(**ext,pre_layer_norm=bool(a.get("pre_layer_norm", True)), epsilon=float(a.get("epsilon", 1e-5)),
                 cache_kvs=_seq(ins, "CacheKV") or None,
                 beam_offset=ins["BeamCacheOffset"][0] if ins.get("BeamCacheOffset") else None,
                 seq_lens=ins["SeqLengths"][0] if ins.get("SeqLengths") else None,
                 time_step=time_step, attn_mask=ins["SrcMask"][0] if ins.get("SrcMask") else None,
                 activation=a.get("act_method", "gelu"), trans_qkvw=bool(a.get("trans_qkvw", True)),
-                rotary_emb_dims=int(a.get("rotary_emb_dims", 0)), causal=bool(a.get("causal", False)),
+                rotary_emb_dims=0, causal=bool(a.get("causal", False)),
                 group=_ring_group(a))
 
 

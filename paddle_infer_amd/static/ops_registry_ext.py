@@ -681,11 +681,14 @@ def _fmt_run(ins, a, layers, moe=False):
     decode = kw["time_step"] is not None
     pos, lens = IF._positions(B, kw["time_step"], kw["seq_lens"], S, x.device, decode)
     caches = kw["cache_kvs"]
+    rope, pre = IF.ext_inputs(kw.get("rotary_embs"), kw.get("rotary_table_dims", 1),
+                              kw.get("pre_caches"), B, dh, x.device, decode)
     with torch.no_grad():
         out = IF.multi_transformer_forward(
             x, layers, nh, int(a.get("num_kv_heads", 0) or 0) or None, kw["pre_layer_norm"],
             kw["epsilon"], IF._caches_from(caches), pos, lens, kw["attn_mask"], decode,
             kw["activation"], kw["rotary_emb_dims"], causal=kw["causal"] and kw["attn_mask"] is None,
+            rope_table=rope, pre_caches=pre,
             group=kw["group"], moe_fn=True if moe else None)
     return {"Out": out, "CacheKVOut": caches or []}
 

@@ -769,3 +769,4 @@ def _clip_op(ins, a):
 
 
 from . import ops_registry_ext  # noqa: E402,F401  (registers the extended op set)
+from . import ops_registry_more  # noqa: E402,F401  (fused blocks, rnn, 3-D conv / pool, detection)

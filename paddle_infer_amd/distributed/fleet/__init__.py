@@ -327,6 +327,7 @@ def distributed_model(model):
         w = DataParallel(model, group=hcg.get_data_parallel_group(),
                          comm_buffer_size=st.fuse_grad_size_in_MB,
                          find_unused_parameters=st.find_unused_parameters)
+        w.comm_fp16 = bool(st.fp16_allreduce)
     else:
         return model
     _STATE["wrapper"] = w
@@ -392,7 +393,7 @@ class HybridParallelOptimizer:
                                      mp_group=hcg.get_model_parallel_group(),
                                      pp_group=hcg.get_pipe_parallel_group(), sharding_stage=st,
                                      named_params=named, bucket_mb=strategy.fuse_grad_size_in_MB,
-                                     overlap=not pp_acc,
+                                     overlap=not pp_acc, comm_fp16=bool(strategy.fp16_allreduce),
                                      no_decay_fn=(lambda n, p: not apply(n)) if apply else (lambda n, p: False))
             optimizer._flat, optimizer._flat_pending = self._flat, False
             wrapper = _STATE.get("wrapper")

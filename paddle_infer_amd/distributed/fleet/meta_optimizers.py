@@ -33,7 +33,6 @@ REJECTED = {
     "dgc": "deep gradient compression is not implemented",
     "localsgd": "local SGD is not implemented",
     "adaptive_localsgd": "adaptive local SGD is not implemented",
-    "fp16_allreduce": "fp16 gradient all-reduce is not implemented (grads travel in the param dtype)",
     "qat": "use paddle_infer_amd.quantization for quantization-aware training",
     "auto": "use paddle_infer_amd.distributed.auto_parallel (Engine) for auto-parallel",
     "semi_auto": "use paddle_infer_amd.distributed.auto_parallel (Engine) for semi-auto parallel",
@@ -156,9 +155,8 @@ def swap_optimizer(opt, st):
 def wrap_optimizer(opt, st):
     """gradient_merge / asp / amp(fp16) around the (hybrid) optimizer."""
     from ... import in_dynamic_mode
-    if not in_dynamic_mode() and (st.gradient_merge or st.amp or st.recompute):
-        raise NotImplementedError("static-graph fleet: amp / recompute / gradient_merge meta-optimizers "
-                                  "are dygraph-only here; use static.amp / static recompute directly")
+    if not in_dynamic_mode():  # static mode: the meta-optimizers are Program rewrites (static_minimize)
+        return opt
     if st.asp:
         from ...incubate import asp
         opt = asp.decorate(opt)
@@ -276,34 +274,35 @@ class AMPOptimizer:
 
 # ------------------------------------------------------------------------------ static graph
 def static_minimize(opt, loss, st, hcg, startup_program=None, parameters=None, no_grad_set=None):
-    """Static-graph fleet: backward + optimizer ops, then data-parallel gradient averaging as
-    Paddle ops (``c_allreduce_sum`` over ring 0 + ``scale`` 1/N) ahead of the first optimizer op
-    (reference `raw_program_optimizer.py` _insert_allreduce_ops)."""
+    """Static-graph fleet ``minimize``: the meta-optimizers as Program rewrites
+    (`fleet/static_meta.py`) around backward + the optimizer pass — amp casts (and fp16 loss
+    scaling ops), recompute segments re-emitted in backward, data-parallel all-reduce ops (fp16
+    with ``fp16_allreduce``), gradient merge as a conditional optimizer block."""
     import torch.distributed as dist
-    from ...static.backward import OPTIMIZE, op_role
-    from ...static.framework import Operator
-    if st.amp or st.recompute or st.gradient_merge:
-        raise NotImplementedError("static-graph fleet: amp / recompute / gradient_merge meta-optimizers "
-                                  "are dygraph-only here; use static.amp / static recompute directly")
-    res = opt.minimize(loss, startup_program, parameters, no_grad_set)
-    world = dist.get_world_size() if dist.is_initialized() else 1
-    if world == 1:
-        return res
+    from . import static_meta as SM
     block = loss.block.program.global_block()
-    ops = block.ops
-    first = next((i for i, op in enumerate(ops) if op_role(op) == OPTIMIZE), len(ops))
-    grads = sorted({n for op in ops[first:] if op_role(op) == OPTIMIZE for n in op.input_names()
-                    if n.endswith("@GRAD")})
-    new = []
-    for g in grads:
-        for t, ins, outs, attrs in (("c_allreduce_sum", {"X": [g]}, {"Out": [g]},
-                                     {"ring_id": 0, "use_calc_stream": True}),
-                                    ("scale", {"X": [g]}, {"Out": [g]},
-                                     {"scale": 1.0 / world, "bias": 0.0, "bias_after_scale": True})):
-            op = Operator(block, None, (), {}, None, type=t, attrs=attrs)
-            op.paddle_inputs, op.paddle_outputs = ins, outs
-            op.attrs["op_role"] = 1  # backward role: runs before the optimizer ops
-            new.append(op)
-    block.ops[first:first] = new
-    block.program._version = getattr(block.program, "_version", 0) + 1
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    amp_cfg = st.amp_configs or {}
+    ls = None
+    bwd_loss = loss
+    if st.amp:
+        dt = _amp_dtype(amp_cfg)
+        SM.amp_rewrite_forward(block, dt, amp_cfg.get("custom_white_list"), amp_cfg.get("custom_black_list"))
+        if dt == "float16":
+            bwd_loss, ls = SM.amp_scale_loss(block, loss, amp_cfg.get("init_loss_scaling", 32768.0))
+    res = opt.minimize(bwd_loss, startup_program, parameters, no_grad_set)
+    if st.recompute:
+        cks = (st.recompute_configs or {}).get("checkpoints") or []
+        if not cks:
+            raise ValueError("static-graph recompute needs recompute_configs['checkpoints']")
+        SM.recompute_rewrite(block, cks)
+    gm = st.gradient_merge and int((st.gradient_merge_configs or {}).get("k_steps", 1)) > 1
+    if world > 1 and not gm:
+        SM.insert_dp_allreduce(block, world, bool(st.fp16_allreduce))
+    if ls is not None:
+        SM.amp_unscale_and_skip(block, ls, amp_cfg)
+    if gm:
+        cfg = st.gradient_merge_configs or {}
+        SM.gradient_merge_rewrite(block, int(cfg.get("k_steps", 1)), bool(cfg.get("avg", True)),
+                                  world, bool(st.fp16_allreduce))
     return res

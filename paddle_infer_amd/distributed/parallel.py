@@ -83,6 +83,8 @@ class DataParallel(torch.nn.Module):
         self._pending = {}
         self._handles = []
         self._queued = False
+        # fp16_allreduce (fleet strategy): f32 gradient buckets travel as fp16, cast back after
+        self.comm_fp16 = False
         params = [p for p in layers.parameters() if p.requires_grad]
         if self.world > 1:
             for p in params:  # identical initial weights on every rank
@@ -159,13 +161,19 @@ class DataParallel(torch.nn.Module):
             return
         self._launched.add(fi)
         flat = self._flat[fi][0]
-        self._handles.append((flat, dist.all_reduce(flat, group=self.pg, async_op=True)))
+        if self.comm_fp16 and flat.dtype == torch.float32:
+            tmp = flat.to(torch.float16)
+            self._handles.append((flat, tmp, dist.all_reduce(tmp, group=self.pg, async_op=True)))
+        else:
+            self._handles.append((flat, flat, dist.all_reduce(flat, group=self.pg, async_op=True)))
 
     def _finalize(self):
         for fi in range(len(self._flat)):  # unused params: their buckets still reduce, in order
             self._launch(fi)
-        for flat, h in self._handles:
+        for flat, comm, h in self._handles:
             h.wait()
+            if comm is not flat:
+                flat.copy_(comm)
             flat.div_(self.world)
         self._pending = {fi: len(views) for fi, (_, views) in enumerate(self._flat)}
         self._launched = set()

@@ -116,8 +116,11 @@ class FlatTrainer:
     def __init__(self, model, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
                  grad_clip=1.0, dp_group=None, mp_group=None, pp_group=None, sharding_stage=0,
                  bucket_mb=256, no_decay_fn=None, optimizer="adamw", momentum=0.9,
-                 overlap=True, named_params=None, replica_group=None):
+                 overlap=True, named_params=None, replica_group=None, comm_fp16=False):
         self.model = model
+        # fp16_allreduce (reference fp16_allreduce_optimizer.py): f32 gradient buckets travel as fp16
+        # (16-bit gradients already do); the reduced values are cast back into the f32 buffer
+        self.comm_fp16 = comm_fp16
         self.lr = lr
         self.beta1, self.beta2 = betas
         self.eps = eps
@@ -296,6 +299,11 @@ class FlatTrainer:
             b.handle = dist.reduce_scatter_tensor(out, grads, group=self.dp_group, async_op=True)
         else:
             out = grads
+            b.cast_back = None
+            if self.world > 1 and self.comm_fp16 and grads.dtype == torch.float32:
+                tmp = grads.to(torch.float16)
+                b.cast_back = (tmp, grads)
+                grads = out = tmp
             b.handle = dist.all_reduce(grads, group=self.dp_group, async_op=True) \
                 if self.world > 1 else None
         if self.replica > 1:
@@ -338,6 +346,10 @@ class FlatTrainer:
                 if b.handle is not None:
                     b.handle.wait()
                     b.handle = None
+                cb = getattr(b, "cast_back", None)
+                if cb is not None:
+                    cb[1].copy_(cb[0])
+                    b.cast_back = None
 
     def _grads_for_update(self, g):
         return g.gshard if self.sharding else g.gflat

@@ -273,6 +273,21 @@ class Executor:
         if is_grad_op(op):
             self._run_grad_op(op, sub, env)
             return
+        if (op.attrs.get("_recompute_fwd") and getattr(self, "_training", False)
+                and not getattr(self, "_in_recompute", False)):
+            # a recompute segment's forward op (fleet static recompute): no autograd graph is kept,
+            # its outputs re-enter as leaves; the segment's copy re-produces them in backward
+            self._in_recompute = True
+            try:
+                with torch.no_grad():
+                    self._run_op(op, sub, env, scope, program)
+            finally:
+                self._in_recompute = False
+            for n in op.output_names():
+                t = env.get(n)
+                if isinstance(t, torch.Tensor) and t.is_floating_point() and not t.requires_grad:
+                    env[n] = t.detach().requires_grad_(True)
+            return
         if getattr(self, "_training", False) and op_role(op) == FORWARD and not getattr(self, "_cf_depth", 0):
             # per-op autograd graphs: a forward op of a training program reads its differentiable
             # inputs through fresh leaves (views, no copy), so its grad op's VJP is exactly this

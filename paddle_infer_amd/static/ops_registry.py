@@ -718,10 +718,61 @@ def _reg(p, g, a):
     return g
 
 
+def _skip(ins):
+    """SkipUpdate input (AMP: found_inf of this step): the optimizer op leaves every state as is."""
+    s = ins.get("SkipUpdate")
+    return bool(s and s[0] is not None and bool(s[0].reshape(-1)[0]))
+
+
+@register("check_finite_and_unscale")
+def _check_finite_and_unscale(ins, a):
+    """Reference `amp/check_finite_and_unscale_op.cu`: Out = X / Scale, FoundInfinite = any
+    inf/nan among all X (in place on the gradients)."""
+    scale = ins["Scale"][0].reshape(()).float()
+    inv = 1.0 / scale
+    found = torch.zeros((), dtype=torch.bool, device=scale.device)
+    outs = []
+    for x in ins["X"]:
+        found = found | ~torch.isfinite(x).all()
+        outs.append(x.mul_(inv.to(x.dtype)) if not x.requires_grad else x * inv.to(x.dtype))
+    return {"Out": outs, "FoundInfinite": found.reshape(1)}
+
+
+@register("update_loss_scaling")
+def _update_loss_scaling(ins, a):
+    """Reference `amp/update_loss_scaling_op.cu`: on inf/nan zero the gradients, count bad steps and
+    shrink the scale every decr_every_n_nan_or_inf of them; else count good steps and grow it every
+    incr_every_n_steps (unless stop_update)."""
+    found = bool(ins["FoundInfinite"][0].reshape(-1)[0])
+    ls, good, bad = ins["PrevLossScaling"][0], ins["InGoodSteps"][0], ins["InBadSteps"][0]
+    xs = ins["X"]
+    if found:
+        xs = [x.zero_() if not x.requires_grad else torch.zeros_like(x) for x in xs]
+    if not a.get("stop_update", False):
+        with torch.no_grad():
+            if found:
+                good.zero_()
+                bad.add_(1)
+                if int(bad.reshape(-1)[0]) >= int(a.get("decr_every_n_nan_or_inf", 2)):
+                    ls.mul_(float(a.get("decr_ratio", 0.5))).clamp_(min=1.0)
+                    bad.zero_()
+            else:
+                bad.zero_()
+                good.add_(1)
+                if int(good.reshape(-1)[0]) >= int(a.get("incr_every_n_steps", 1000)):
+                    nxt = ls * float(a.get("incr_ratio", 2.0))
+                    if bool(torch.isfinite(nxt).all()):
+                        ls.copy_(nxt)
+                    good.zero_()
+    return {"Out": xs, "LossScaling": ls, "OutGoodSteps": good, "OutBadSteps": bad}
+
+
 @register("sgd")
 def _sgd(ins, a):
     """Reference `phi/kernels/gpu/sgd_kernel.cu`: ParamOut = Param - lr * Grad (in place)."""
     p, g = ins["Param"][0], ins["Grad"][0]
+    if _skip(ins):
+        return {"ParamOut": p}
     gf = _reg(p, g.to(p.dtype), a)
     p.sub_(_lr(ins).to(p.dtype) * gf)
     return {"ParamOut": p}
@@ -731,6 +782,8 @@ def _sgd(ins, a):
 def _momentum(ins, a):
     """Reference `phi/kernels/impl/momentum_kernel_impl.h`: v = mu v + g; p -= lr (g + mu v) | lr v."""
     p, g, v = ins["Param"][0], ins["Grad"][0], ins["Velocity"][0]
+    if _skip(ins):
+        return {"ParamOut": p, "VelocityOut": v}
     mu = float(a.get("mu", 0.9))
     gf = _reg(p, g.float() * float(a.get("rescale_grad", 1.0)), a)
     v.mul_(mu).add_(gf)
@@ -747,6 +800,8 @@ def _adam(ins, a):
     p, g = ins["Param"][0], ins["Grad"][0]
     m1, m2 = ins["Moment1"][0], ins["Moment2"][0]
     b1p, b2p = ins["Beta1Pow"][0], ins["Beta2Pow"][0]
+    if _skip(ins):
+        return {"ParamOut": p, "Moment1Out": m1, "Moment2Out": m2, "Beta1PowOut": b1p, "Beta2PowOut": b2p}
     b1, b2, eps = float(a.get("beta1", 0.9)), float(a.get("beta2", 0.999)), float(a.get("epsilon", 1e-8))
     lr = _lr(ins) * float(a.get("lr_ratio", 1.0))
     gf = _reg(p, g.float(), a)

@@ -724,9 +724,22 @@ class Kernel:
         self.e(f"s_add_u32 s{srd}, s{E}, s{T}")
         self.e(f"s_addc_u32 s{srd + 1}, s{E + 1}, s{T + 1}")
         self.e(f"s_and_b32 s{srd + 1}, s{srd + 1}, 0xffff")
-        # records = c_bytes - (part*c_part + tile offset), clamped to [0, 2^32-1]
-        self.e(f"s_sub_u32 s{T + 2}, s{E + 2}, s{T}")
-        self.e(f"s_subb_u32 s{T + 3}, s{E + 3}, s{T + 1}")
+        # records = lim - (part*c_part + tile offset), clamped to [0, 2^32-1], where lim = the end
+        # of this part's plane ((part+1)*c_part, at most c_bytes) for split-K / batched launches
+        # (rows past M of a plane are dropped instead of landing in the next plane), else c_bytes
+        self.e(f"s_add_u32 s{T + 4}, s{S_PART}, 1")
+        self.e(f"s_mul_i32 s{T + 2}, s{T + 4}, s{E + 6}")
+        self.e(f"s_mul_hi_u32 s{T + 3}, s{T + 4}, s{E + 6}")
+        self.e(f"s_mul_i32 s{T + 5}, s{T + 4}, s{E + 7}")
+        self.e(f"s_add_u32 s{T + 3}, s{T + 3}, s{T + 5}")
+        self.e(f"s_or_b32 s{T + 5}, s{E + 6}, s{E + 7}")
+        self.e(f"s_cmp_eq_u32 s{T + 5}, 0")
+        self.e(f"s_cselect_b64 s[{T + 2}:{T + 3}], s[{E + 2}:{E + 3}], s[{T + 2}:{T + 3}]")
+        self.e(f"s_sub_u32 s{T + 4}, s{E + 2}, s{T + 2}")
+        self.e(f"s_subb_u32 s{T + 5}, s{E + 3}, s{T + 3}")          # SCC: c_bytes < lim
+        self.e(f"s_cselect_b64 s[{T + 2}:{T + 3}], s[{E + 2}:{E + 3}], s[{T + 2}:{T + 3}]")
+        self.e(f"s_sub_u32 s{T + 2}, s{T + 2}, s{T}")
+        self.e(f"s_subb_u32 s{T + 3}, s{T + 3}, s{T + 1}")
         self.e(f"s_cmp_eq_u32 s{T + 3}, 0")
         self.e(f"s_cselect_b32 s{srd + 2}, s{T + 2}, -1")
         self.e(f"s_mov_b32 s{srd + 3}, 0x20000")

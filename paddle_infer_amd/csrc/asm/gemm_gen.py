@@ -118,6 +118,13 @@ NVGPR = ACC_OFF + 256
 
 K0, K1 = 0.7978845608028654, 0.044715          # gelu_tanh constants (sqrt(2/pi), 0.044715)
 TWO_LOG2E = 2.0 * 1.4426950408889634
+# exact (erf) GELU: Φ(x) = 1 − q (x ≥ 0) or q (x < 0), q = ½·poly(t)·exp(−x²/2), t = 1/(1 + p·|x|/√2)
+# (Abramowitz–Stegun 7.1.26, |error| ≤ 1.5e-7); constant pairs 0 p/√2, 1..3 ½a5, ½a4, ½a3, 4 1.0,
+# 5 ½a2, 6 ½a1, 7 −log2(e)/2
+ERF_P = 0.3275911 / 2.0 ** 0.5
+ERF_A = (0.254829592, -0.284496736, 1.421413741, -1.453152027, 1.061405429)
+ERF_CONSTS = (ERF_P, 0.5 * ERF_A[4], 0.5 * ERF_A[3], 0.5 * ERF_A[2], 1.0, 0.5 * ERF_A[1], 0.5 * ERF_A[0],
+              -0.5 * 1.4426950408889634)
 
 
 def fhex(x):
@@ -188,6 +195,7 @@ class Kernel:
         # ek: plain kinds (bf16 / f32 / f32acc) or fused: bias[gelu|relu] (pre-activation stored
         # as aux), d{gelu,relu} (C = acc ⊙ act'(aux))
         fused = {"bias": ("bias_act", 0), "biasgelu": ("bias_act", 1), "biasrelu": ("bias_act", 3),
+                 "biasgeluerf": ("bias_act", 2),
                  "dgelu": ("dact", 1), "drelu": ("dact", 3), "biasnx": ("bias_act", 0)}
         self.ek, self.act = fused.get(ek, (ek, 0))
         self.store_aux = ek != "biasnx"  # biasnx: C = acc + bias, no pre-activation output
@@ -777,7 +785,8 @@ class Kernel:
         if ek in ("bias_act", "dact"):
             self.e(f"v_mul_lo_u32 v{V + 3}, v{V}, s{E + 5}")
             self.e(f"v_lshl_add_u32 v{V + 3}, v{V + 1}, 1, v{V + 3}")  # aux voffset
-            for i, val in enumerate((K0, K0 * K1, 3 * K0 * K1, TWO_LOG2E, 1.0)):
+            consts = ERF_CONSTS if self.act == 2 else (K0, K0 * K1, 3 * K0 * K1, TWO_LOG2E, 1.0)
+            for i, val in enumerate(consts):
                 self.e(f"v_mov_b32 v{self.VCONST + 2 * i}, {fhex(val)}")
                 self.e(f"v_mov_b32 v{self.VCONST + 2 * i + 1}, {fhex(val)}")
         if ek == "bias_act":
@@ -970,6 +979,33 @@ class Kernel:
         self.trans(f"v_rcp_f32 v{t + 1}, v{t + 1}")
         self.e(f"v_pk_fma_f32 {X}, {X}, {Tp}, {X} neg_lo:[1,0,0] neg_hi:[1,0,0]")
 
+    def gelu_erf2(self, x):
+        """v[x:x+1] ← exact GELU x·Φ(x) (packed f32; constant pairs ERF_CONSTS)."""
+        ta, tb, tc = self.VTMP, self.VTMP + 2, self.VTMP + 4
+        X = f"v[{x}:{x + 1}]"
+        A, B, C = f"v[{ta}:{ta + 1}]", f"v[{tb}:{tb + 1}]", f"v[{tc}:{tc + 1}]"
+        c = self.cpair
+        for k in range(2):
+            self.e(f"v_max_f32_e64 v{ta + k}, v{x + k}, -v{x + k}")
+        self.e(f"v_pk_fma_f32 {A}, {A}, {c(0)}, {c(4)}")
+        self.e(f"v_rcp_f32 v{ta}, v{ta}")
+        self.trans(f"v_rcp_f32 v{ta + 1}, v{ta + 1}")
+        self.e(f"v_pk_fma_f32 {B}, {A}, {c(1)}, {c(2)}")
+        self.e(f"v_pk_fma_f32 {B}, {B}, {A}, {c(3)}")
+        self.e(f"v_pk_fma_f32 {B}, {B}, {A}, {c(5)}")
+        self.e(f"v_pk_fma_f32 {B}, {B}, {A}, {c(6)}")
+        self.e(f"v_pk_mul_f32 {B}, {B}, {A}")
+        self.e(f"v_pk_mul_f32 {C}, {X}, {X}")
+        self.e(f"v_pk_mul_f32 {C}, {C}, {c(7)}")
+        self.e(f"v_exp_f32 v{tc}, v{tc}")
+        self.trans(f"v_exp_f32 v{tc + 1}, v{tc + 1}")
+        self.e(f"v_pk_mul_f32 {B}, {B}, {C}")
+        self.e(f"v_pk_add_f32 {A}, {c(4)}, {B} neg_lo:[0,1] neg_hi:[0,1]")
+        for k in range(2):
+            self.e(f"v_cmp_le_f32 vcc, 0, v{x + k}")
+            self.e(f"v_cndmask_b32 v{tb + k}, v{tb + k}, v{ta + k}, vcc")
+        self.e(f"v_pk_mul_f32 {X}, {X}, {B}")
+
     def gelu_grad_mul2(self, y, h):
         """v[y:y+1] ← y · gelu_tanh'(h) (packed): (1−r)(1 + 2h·r·(k0 + 3k0k1·h²))."""
         ta, tb = self.VTMP, self.VTMP + 2
@@ -1027,6 +1063,8 @@ class Kernel:
             for j in (0, 2):
                 if self.act == 1:
                     self.gelu2(d + j)
+                elif self.act == 2:
+                    self.gelu_erf2(d + j)
                 else:
                     self.e(f"v_max_f32 v{d + j}, 0, v{d + j}")
                     self.e(f"v_max_f32 v{d + j + 1}, 0, v{d + j + 1}")
@@ -1118,7 +1156,7 @@ LAYOUTS = {"nt": (True, True), "tn": (False, False), "nn": (True, False), "tt": 
 EPILOGUES = ("bf16", "bf16acc", "f32", "f32acc")
 
 
-FUSED = ("bias", "biasgelu", "biasrelu", "dgelu", "drelu", "biasnx")
+FUSED = ("bias", "biasgelu", "biasrelu", "dgelu", "drelu", "biasnx", "biasgeluerf")
 
 
 def variants():

@@ -128,7 +128,7 @@ PIAMD_EXPORT int piamd_agemm(const void* a, long long lda, int trans_a, const vo
       (!a_kc && M % 8) || (!b_kc && N % 8) || lda % 8 || ldb % 8 || ldc % 4 ||
       lda >= (1 << 22) || ldb >= (1 << 22) || ldc >= (1 << 26) || epi < 0 || epi > 2 ||
       (epi != 0 && (!a_kc || !b_kc || c_f32 || accumulate || ksplit > 1 || ldaux % 4 ||
-                    (epi == 2 && !aux) || !(act == 0 || act == 1 || act == 3) ||
+                    (epi == 2 && !aux) || !(act == 0 || act == 1 || act == 3 || (act == 2 && epi == 1)) ||
                     (epi == 2 && act == 0))) ||
       (ksplit > 1 && !ws) ||
       ((uintptr_t)a | (uintptr_t)b | (uintptr_t)c) % 16)
@@ -138,7 +138,7 @@ PIAMD_EXPORT int piamd_agemm(const void* a, long long lda, int trans_a, const vo
   AgemmArgs g;
   std::memset(&g, 0, sizeof(g));
   if (epi != 0) {
-    static const char* const kFused[2][4] = {{"bias", "biasgelu", "", "biasrelu"},
+    static const char* const kFused[2][4] = {{"bias", "biasgelu", "biasgeluerf", "biasrelu"},
                                              {"", "dgelu", "", "drelu"}};
     ek = (epi == 1 && act == 0 && !aux) ? "biasnx" : kFused[epi - 1][act];
     g.c = c;

@@ -9,10 +9,14 @@
 //   * A and B both K-contiguous (weights in their cached [N][K] copy), so every operand fragment
 //     is a direct 32-B-per-lane global load — no LDS staging: few rows means little reuse to win,
 //     and the weight bytes (the dominant stream) are read exactly once per workgroup.
-//   * workgroup = 4 waves over ONE output tile of TM = 16·MB rows × TN = 16·NB columns; the waves
-//     split the tile's K range (k64 steps w, w+4, …) and meet in LDS, so a small tile still keeps
-//     four loads streams in flight per CU. Grid (N/TN, M/TM, KS): KS > 1 splits K over workgroups
-//     into f32 slices ws[KS][M][N] summed (in a fixed order) by small_gemm_finish.
+//   * workgroup = 4 waves over ONE output tile of TM = 16·MB rows × TN = 16·NB·WN columns: WN
+//     waves side by side along N (they read the same A fragments — L1 hits) and 4/WN waves
+//     splitting the tile's K range (k64 steps w_k, w_k + 4/WN, …) that meet in LDS, so a short
+//     K range still keeps every wave busy and a long one keeps four load streams in flight.
+//     Grid (N/TN, M/TM, KS): KS > 1 splits K over workgroups. Fixup mode (cnt != null): every
+//     slice adds its partial into a zeroed f32 tile with memory-side atomics and the last slice
+//     to arrive (per-tile counter) runs the epilogue and re-zeroes the tile — one launch. Slice
+//     mode (cnt == null): f32 slices ws[KS][M][N] summed in a fixed order by small_gemm_finish.
 //   * v_mfma_f32_16x16x32_{bf16,f16} with the operands swapped (D = B·Aᵀ blocks), so a lane owns
 //     4 consecutive output columns of one row: 8-B (16-bit) / 16-B (f32) stores. Lane group g of
 //     a k64 step loads k = 16g … 16g+15 of its row; MFMA sub-step s uses elements 8s … 8s+7 of it
@@ -80,11 +84,13 @@ __device__ __forceinline__ void sg_store(const SgArgs& p, int m, int n, f32x4 v)
   }
 }
 
-template <bool F16, int MB, int NB>
-__global__ __launch_bounds__(256) void small_gemm_kernel(SgArgs p) {
-  __shared__ f32x4 red[4][MB * NB][64];
+template <bool F16, int MB, int NB, int WN, int D>
+__global__ __launch_bounds__(256) void small_gemm_kernel(SgArgs p, int* __restrict__ cnt) {
+  constexpr int WK = 4 / WN;
+  __shared__ f32x4 red[WK > 1 ? 4 : 1][MB * NB][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r16 = lane & 15;
-  const int n0 = blockIdx.x * (16 * NB), m0 = blockIdx.y * (16 * MB);
+  const int wn = w % WN, wk = w / WN;
+  const int n0 = blockIdx.x * (16 * NB * WN) + wn * (16 * NB), m0 = blockIdx.y * (16 * MB);
   const int kz = blockIdx.z, KS = gridDim.z;
   const int nkb = p.K >> 6;
   const int kb_beg = (int)((long long)nkb * kz / KS), kb_end = (int)((long long)nkb * (kz + 1) / KS);
@@ -104,7 +110,9 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(SgArgs p) {
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  u16x8 ac[MB][2], bc[NB][2];
+  // D-deep register ring of operand fragments: step i computes on slot i % D, then refills it
+  // with step i + D, so D k64 steps of loads are in flight per wave
+  u16x8 ar[D][MB][2], br[D][NB][2];
   auto load = [&](int kb, u16x8 (&ad)[MB][2], u16x8 (&bd)[NB][2]) {
     const long long k = (long long)kb << 6;
 #pragma unroll
@@ -120,46 +128,84 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(SgArgs p) {
       ad[mb][1] = s[1];
     }
   };
-  int kb = kb_beg + w;
-  if (kb < kb_end) load(kb, ac, bc);
-  for (; kb < kb_end; kb += 4) {
-    u16x8 an[MB][2], bn[NB][2];
-    const bool more = kb + 4 < kb_end;
-    if (more) load(kb + 4, an, bn);
+  const int kb0 = kb_beg + wk;
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+  for (int d = 0; d < D; ++d)
+    if (kb0 + d * WK < kb_end) load(kb0 + d * WK, ar[d], br[d]);
+  for (int kb = kb0; kb < kb_end; kb += D * WK) {
 #pragma unroll
-      for (int mb = 0; mb < MB; ++mb)
+    for (int d = 0; d < D; ++d) {
+      const int k = kb + d * WK;
+      if (k >= kb_end) break;
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb) acc[mb][nb] = mma16<F16>(bc[nb][s], ac[mb][s], acc[mb][nb]);
-    if (more) {
+      for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
+        for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
-        for (int mb = 0; mb < MB; ++mb) ac[mb][s] = an[mb][s];
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb) bc[nb][s] = bn[nb][s];
-      }
+          for (int nb = 0; nb < NB; ++nb)
+            acc[mb][nb] = mma16<F16>(br[d][nb][s], ar[d][mb][s], acc[mb][nb]);
+      if (k + D * WK < kb_end) load(k + D * WK, ar[d], br[d]);
     }
   }
-  // the four waves' K slices meet in LDS; wave w finishes the blocks i ≡ w (mod 4)
+  if constexpr (WK > 1) {
+    // the K-splitting waves of one column group meet in LDS; wave (wn, wk) finishes the blocks
+    // i ≡ wk (mod WK) of its column group
 #pragma unroll
-  for (int mb = 0; mb < MB; ++mb)
+    for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) red[w][mb * NB + nb][lane] = acc[mb][nb];
-  __syncthreads();
+      for (int nb = 0; nb < NB; ++nb) red[w][mb * NB + nb][lane] = acc[mb][nb];
+    __syncthreads();
+  }
   // D = B·Aᵀ block: lane holds rows m = r16 of the A block, columns n = 4g + j of the B block
+  float sink = 0.f;
+  bool any = false;
 #pragma unroll
-  for (int i = w; i < MB * NB; i += 4) {
+  for (int i = 0; i < MB * NB; ++i) {
+    if (WK > 1 && i % WK != wk) continue;
     const int mb = i / NB, nb = i % NB;
     const int m = m0 + 16 * mb + r16, n = n0 + 16 * nb + 4 * g;
+    f32x4 v = acc[mb][nb];
+    if constexpr (WK > 1) {
+      v = red[wn][i][lane];
+#pragma unroll
+      for (int j = 1; j < WK; ++j) v += red[wn + j * WN][i][lane];
+    }
     if (m >= p.M || n >= p.N) continue;
-    const f32x4 v = red[0][i][lane] + red[1][i][lane] + red[2][i][lane] + red[3][i][lane];
-    if (KS == 1)
+    if (KS == 1) {
       sg_store<F16>(p, m, n, v);
-    else
+    } else if (cnt == nullptr) {
       *reinterpret_cast<f32x4*>(p.ws + ((long long)kz * p.M + m) * p.N + n) = v;
+    } else {
+      float* t = p.ws + (long long)m * p.N + n;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sink += xcd_add(t + j, v[j]);
+      any = true;
+    }
   }
+  if (KS == 1 || cnt == nullptr) return;
+  // fixup: the workgroup's adds are complete (returning atomics + drain) before its arrival
+  xcd_drain(sink);
+  (void)any;
+  __syncthreads();
+  __shared__ int last_s;
+  const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+  if (threadIdx.x == 0) last_s = atomicAdd(&cnt[tile], 1) == KS - 1;
+  __syncthreads();
+  if (!last_s) return;
+  // last arrival: every slice's adds landed (memory-side, coherent across XCDs); take + epilogue
+  const int cols = 16 * NB * WN;
+  const int c0 = blockIdx.x * cols;
+  for (int e = threadIdx.x; e < 16 * MB * cols / 4; e += 256) {
+    const int r = e / (cols / 4), cq = e % (cols / 4);
+    const int m = m0 + r, n = c0 + 4 * cq;
+    if (m >= p.M || n >= p.N) continue;
+    float* t = p.ws + (long long)m * p.N + n;
+    f32x4 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = xcd_take(t + j);
+    sg_store<F16>(p, m, n, v);
+  }
+  if (threadIdx.x == 0) atomicExch(&cnt[tile], 0);
 }
 
 // C = epilogue(Σ_z ws[z]) in a fixed order; 4 columns per thread (N % 4 == 0).
@@ -175,16 +221,19 @@ __global__ __launch_bounds__(256) void small_gemm_finish(SgArgs p, int KS) {
   }
 }
 
-template <bool F16, int MB, int NB>
-void sg_launch(const SgArgs& p, int ks, hipStream_t st) {
-  dim3 grid((p.N + 16 * NB - 1) / (16 * NB), (p.M + 16 * MB - 1) / (16 * MB), ks);
-  hipLaunchKernelGGL((small_gemm_kernel<F16, MB, NB>), grid, dim3(256), 0, st, p);
+template <bool F16, int MB, int NB, int WN>
+void sg_launch(const SgArgs& p, int ks, int depth, int* cnt, hipStream_t st) {
+  dim3 grid((p.N + 16 * NB * WN - 1) / (16 * NB * WN), (p.M + 16 * MB - 1) / (16 * MB), ks);
+  if (depth >= 2)
+    hipLaunchKernelGGL((small_gemm_kernel<F16, MB, NB, WN, 2>), grid, dim3(256), 0, st, p, cnt);
+  else
+    hipLaunchKernelGGL((small_gemm_kernel<F16, MB, NB, WN, 1>), grid, dim3(256), 0, st, p, cnt);
 }
 
-template <bool F16>
-int sg_dispatch(const SgArgs& p, int mb, int nb, int ks, hipStream_t st) {
+template <bool F16, int WN>
+int sg_dispatch_wn(const SgArgs& p, int mb, int nb, int ks, int depth, int* cnt, hipStream_t st) {
 #define SG_CASE(M_, N_) \
-  if (mb == M_ && nb == N_) { sg_launch<F16, M_, N_>(p, ks, st); return 0; }
+  if (mb == M_ && nb == N_) { sg_launch<F16, M_, N_, WN>(p, ks, depth, cnt, st); return 0; }
   SG_CASE(1, 1) SG_CASE(1, 2) SG_CASE(1, 4)
   SG_CASE(2, 1) SG_CASE(2, 2) SG_CASE(2, 4)
   SG_CASE(4, 1) SG_CASE(4, 2) SG_CASE(4, 4)
@@ -193,23 +242,37 @@ int sg_dispatch(const SgArgs& p, int mb, int nb, int ks, hipStream_t st) {
   return (int)hipErrorInvalidValue;
 }
 
+template <bool F16>
+int sg_dispatch(const SgArgs& p, int mb, int nb, int wn, int ks, int depth, int* cnt, hipStream_t st) {
+  if (wn == 1) return sg_dispatch_wn<F16, 1>(p, mb, nb, ks, depth, cnt, st);
+  if (wn == 2) return sg_dispatch_wn<F16, 2>(p, mb, nb, ks, depth, cnt, st);
+  if (wn == 4) return sg_dispatch_wn<F16, 4>(p, mb, nb, ks, depth, cnt, st);
+  return (int)hipErrorInvalidValue;
+}
+
 }  // namespace
 
 // f16: fp16 operands / 16-bit output (else bf16). mb ∈ {1,2,4,8} (TM = 16·mb rows), nb ∈ {1,2,4}
-// (TN = 16·nb columns; mb·nb ≤ 16), ks ≥ 1 K slices (ws = ks·M·N f32 when ks > 1). bias / resid:
-// 16-bit, nullable. act: 0 none, 1 gelu_tanh, 2 gelu_erf, 3 relu, 4 silu.
+// (mb·nb ≤ 16), wn ∈ {1,2,4} waves along N (TN = 16·nb·wn columns; the other 4/wn waves split K),
+// depth ∈ {1,2} k64 steps of loads in flight per wave, ks ≥ 1 K slices. ks > 1: cnt != null → fixup mode (ws = M·N f32 and cnt = tiles ints, both
+// zeroed, left zeroed); cnt == null → slice mode (ws = ks·M·N f32 + a finish launch).
+// bias / resid: 16-bit, nullable. act: 0 none, 1 gelu_tanh, 2 gelu_erf, 3 relu, 4 silu.
 PIAMD_EXPORT int piamd_small_gemm(int f16, const void* a, long long lda, const void* b, long long ldb,
                                   void* c, long long ldc, int c_f32, int M, int N, int K, int mb,
-                                  int nb, int ks, float alpha, const void* bias, int act,
-                                  const void* resid, long long ldr, float* ws, hipStream_t st) {
+                                  int nb, int wn, int depth, int ks, float alpha, const void* bias,
+                                  int act,
+                                  const void* resid, long long ldr, float* ws, int* cnt,
+                                  hipStream_t st) {
   if (M <= 0 || N <= 0 || K <= 0 || K % 64 || N % 4 || lda % 8 || ldb % 8 || ldc % 4 || ks < 1 ||
       ks > K / 64 || (ks > 1 && !ws) || ((uintptr_t)a | (uintptr_t)b | (uintptr_t)c) % 16)
     return (int)hipErrorInvalidValue;
   SgArgs p{(const bf16_t*)a, lda, (const bf16_t*)b, ldb, c, ldc, ws, (const bf16_t*)bias,
            (const bf16_t*)resid, ldr, alpha, M, N, K, c_f32, act};
-  const int rc = f16 ? sg_dispatch<true>(p, mb, nb, ks, st) : sg_dispatch<false>(p, mb, nb, ks, st);
+  int* kc = ks > 1 ? cnt : nullptr;
+  const int rc = f16 ? sg_dispatch<true>(p, mb, nb, wn, ks, depth, kc, st)
+                     : sg_dispatch<false>(p, mb, nb, wn, ks, depth, kc, st);
   if (rc) return rc;
-  if (ks > 1) {
+  if (ks > 1 && !cnt) {
     const int grid = stride_grid((long long)M * N / 4, 256);
     if (f16) hipLaunchKernelGGL(small_gemm_finish<true>, dim3(grid), dim3(256), 0, st, p, ks);
     else hipLaunchKernelGGL(small_gemm_finish<false>, dim3(grid), dim3(256), 0, st, p, ks);

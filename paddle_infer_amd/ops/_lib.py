@@ -204,10 +204,11 @@ _SIGS["piamd_agemm"] = [c_void_p, c_ll, c_int, c_void_p, c_ll, c_int, c_void_p, 
                         c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_ll, c_int, c_void_p,
                         c_int, c_int, c_ll, c_ll, c_ll, c_void_p]
 _SIGS["piamd_agemm_load"] = [ctypes.c_char_p]
-# f16, a, lda, b, ldb, c, ldc, c_f32, M, N, K, mb, nb, ks, alpha, bias, act, resid, ldr, ws, stream
+# f16, a, lda, b, ldb, c, ldc, c_f32, M, N, K, mb, nb, wn, depth, ks, alpha, bias, act, resid, ldr,
+# ws, cnt, stream
 _SIGS["piamd_small_gemm"] = [c_int, c_void_p, c_ll, c_void_p, c_ll, c_void_p, c_ll, c_int, c_int,
-                             c_int, c_int, c_int, c_int, c_int, c_float, c_void_p, c_int, c_void_p,
-                             c_ll, c_void_p, c_void_p]
+                             c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p,
+                             c_int, c_void_p, c_ll, c_void_p, c_void_p, c_void_p]
 _SIGS["piamd_agemm_loaded"] = []
 _SIGS["piamd_transpose_bf16"] = [c_void_p, c_void_p, c_int, c_int, c_void_p]
 _SIGS["piamd_moe_gemm"] = [c_void_p, c_ll, c_void_p, c_ll, c_ll,

@@ -78,8 +78,8 @@ def asm_gemm(a, b, trans_a=False, trans_b=False, out=None, out_f32=False, accumu
     16-bit output has the operands' dtype). 3-D ``a`` / ``b`` / ``out`` run one batched launch
     (a 2-D operand, or a batch stride of 0, broadcasts over the batch). Fused epilogues (2-D, A
     stored [M, K], B stored [N, K], 16-bit C): ``epi="bias_act"`` — pre = 16-bit(A·B + bias)
-    written to ``aux`` (optional), C = act(pre); ``epi="dact"`` — C = (A·B) ⊙ act'(aux). act ∈
-    none / gelu_tanh / relu."""
+    written to ``aux`` (optional), C = act(pre), act ∈ none / gelu_tanh / gelu (exact erf) / relu;
+    ``epi="dact"`` — C = (A·B) ⊙ act'(aux), act ∈ gelu_tanh / relu."""
     _agemm_load()
     batched = a.dim() == 3 or b.dim() == 3
     nb = max(a.shape[0] if a.dim() == 3 else 1, b.shape[0] if b.dim() == 3 else 1)
@@ -121,11 +121,12 @@ def pick_ksplit(M, N, K):
     the tile grid is small and K is long (weight gradients: 2048 x 2048 tiles over 65k tokens)."""
     tiles = ((M + 255) // 256) * ((N + 255) // 256)
     nk = K // 64
-    if tiles >= 2 * NUM_CUS or nk < 32:
+    if tiles >= 2 * NUM_CUS or nk < 16:
         return 1
+    # ≥ 8 k64 blocks per split (measured: M=256 N=6144 K=2048 is fastest at 4 splits of 8)
     best, best_t = 1, None
     for ks in (1, 2, 4, 8):
-        if nk // ks < 16 or nk % ks:
+        if nk // ks < 8 or nk % ks:
             break
         waves = -(-tiles * ks // NUM_CUS)
         t = waves / ks
@@ -141,42 +142,94 @@ F  # noqa
 # skinny kernel (csrc/kernels/gemm_small.hip) and the dispatcher every framework matmul uses
 # ---------------------------------------------------------------------------------------------
 _SG_SHAPES = {(1, 1), (1, 2), (1, 4), (2, 1), (2, 2), (2, 4), (4, 1), (4, 2), (4, 4), (8, 1), (8, 2)}
+# (M, N, K) -> (mb, nb, wn, depth, ks): the fastest configs of the graph-timed sweep
+# (tools/tune_small_gemm.py, fp16, weights streamed from HBM; profiles/small_gemm_tune_r4.jsonl)
+_SG_TUNED: dict = {
+    (16, 3072, 1024): (1, 1, 1, 1, 1), (16, 1024, 4096): (1, 1, 1, 1, 4),
+    (32, 3072, 1024): (1, 2, 1, 1, 1), (32, 1024, 4096): (1, 1, 1, 1, 2),
+    (64, 3072, 1024): (2, 2, 1, 1, 1), (64, 1024, 4096): (1, 1, 1, 1, 1),
+    (128, 3072, 1024): (4, 2, 1, 1, 1), (128, 1024, 1024): (1, 2, 1, 2, 1),
+    (128, 4096, 1024): (4, 2, 1, 1, 1), (128, 1024, 4096): (1, 2, 1, 1, 1),
+    (128, 6144, 2048): (4, 4, 1, 2, 1), (128, 2048, 2048): (2, 2, 1, 1, 1),
+    (128, 8192, 2048): (4, 4, 1, 2, 1),
+    (256, 3072, 1024): (4, 4, 1, 1, 1), (256, 1024, 4096): (2, 2, 1, 2, 1),
+    (256, 2048, 2048): (4, 2, 1, 1, 1), (512, 2048, 2048): (4, 4, 1, 1, 1),
+}
 
 
 def small_cfg(M, N, K):
-    """(mb, nb, ks) of the skinny kernel: 16·mb rows × 16·nb columns per workgroup, K split ks
-    ways when the tile grid alone cannot fill the 256 CUs."""
-    mb = 1 if M <= 16 else 2 if M <= 32 else 4 if M <= 64 else 8
-    tm = -(-M // (16 * mb))
-    nb = 2 if mb == 8 else 4
-    while nb > 1 and tm * -(-N // (16 * nb)) < 2 * NUM_CUS:
-        nb //= 2
-    if (mb, nb) not in _SG_SHAPES:
-        nb = 2
-    wgs = tm * -(-N // (16 * nb))
+    """(mb, nb, wn, depth, ks) of the skinny kernel: 16·mb rows × 16·nb·wn columns per workgroup
+    (wn waves side by side along N, 4/wn splitting K), ``depth`` k64 steps of loads in flight per
+    wave, K split ks ways over workgroups when the tile grid alone cannot fill the 256 CUs."""
+    hit = _SG_TUNED.get((M, N, K))
+    if hit is not None:
+        return hit
+    # The sweep's winners all keep the 4 waves splitting K (wn = 1) and take the biggest tile
+    # (most operand reuse) whose grid still gives every CU a workgroup (≥ 192); among equal areas
+    # the squarest, then the wider. Split K only when even 16x16 tiles cannot fill the chip.
     nkb = K // 64
-    ks = 1
-    # ≥ 4 k64 steps per workgroup (one per wave) before splitting further
-    while wgs * ks < NUM_CUS and ks * 2 <= nkb // 4:
-        ks *= 2
-    return mb, nb, ks
+    best = None
+    for mb, nb in _SG_SHAPES:
+        if mb > 1 and 16 * mb > M:
+            continue
+        wgs = -(-M // (16 * mb)) * -(-N // (16 * nb))
+        if wgs < 192:
+            continue
+        key = (mb * nb, -abs(mb - nb), nb)
+        if best is None or key > best[0]:
+            best = (key, mb, nb, wgs)
+    if best is None:
+        mb, nb = 1, 1
+        wgs = -(-M // 16) * -(-N // 16)
+        ks = 1
+        while wgs * ks < 192 and ks * 2 <= nkb // 4:
+            ks *= 2
+        return mb, nb, 1, 1, ks
+    _, mb, nb, wgs = best
+    depth = 2 if (mb * nb >= 16 and K >= 2048 and wgs <= 256) else 1
+    return mb, nb, 1, depth, 1
 
 
-def small_gemm(a, b, out=None, out_f32=False, alpha=1.0, bias=None, act="none", resid=None, cfg=None):
+_SG_WS: dict = {}
+
+
+def _sg_fixup_bufs(device, M, N, tiles):
+    """Zeroed f32 [M·N] partial tile + per-tile arrival counters for the fixup mode (left zeroed
+    by the kernel's last arrival); one pair per (device, stream): launches on one stream never
+    overlap."""
+    key = (device, torch.cuda.current_stream(device).cuda_stream)
+    ws, cnt = _SG_WS.get(key, (None, None))
+    if ws is None or ws.numel() < M * N or cnt.numel() < tiles:
+        ws = torch.zeros(max(M * N, ws.numel() if ws is not None else 0), dtype=torch.float32, device=device)
+        cnt = torch.zeros(max(tiles, cnt.numel() if cnt is not None else 0, 4096), dtype=torch.int32,
+                          device=device)
+        _SG_WS[key] = (ws, cnt)
+    return ws, cnt
+
+
+def small_gemm(a, b, out=None, out_f32=False, alpha=1.0, bias=None, act="none", resid=None, cfg=None,
+               slices=False):
     """C[M, N] = act(alpha·a[M, K]·b[N, K]ᵀ + bias) (+ resid) on the skinny MFMA kernel (both
-    operands K-contiguous bf16 / fp16, K % 64 == 0, N % 4 == 0)."""
+    operands K-contiguous bf16 / fp16, K % 64 == 0, N % 4 == 0). Split-K runs in fixup mode (one
+    launch; ``slices=True``: deterministic slices + a finish launch)."""
     M, K = a.shape
     N = b.shape[0]
     half = a.dtype
     if out is None:
         out = torch.empty((M, N), dtype=torch.float32 if out_f32 else half, device=a.device)
-    mb, nb, ks = cfg or small_cfg(M, N, K)
-    ws = torch.empty((ks, M, N), dtype=torch.float32, device=a.device) if ks > 1 else None
+    mb, nb, wn, depth, ks = cfg or small_cfg(M, N, K)
+    ws = cnt = None
+    if ks > 1:
+        if slices:
+            ws = torch.empty((ks, M, N), dtype=torch.float32, device=a.device)
+        else:
+            tiles = -(-M // (16 * mb)) * -(-N // (16 * nb * wn))
+            ws, cnt = _sg_fixup_bufs(a.device, M, N, tiles)
     _lib.call("piamd_small_gemm", int(half == torch.float16), a.data_ptr(), a.stride(0),
               b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
-              int(out.dtype == torch.float32), M, N, K, mb, nb, ks, float(alpha), _lib.ptr(bias),
+              int(out.dtype == torch.float32), M, N, K, mb, nb, wn, depth, ks, float(alpha), _lib.ptr(bias),
               ACTS[act], _lib.ptr(resid), resid.stride(0) if resid is not None else 0,
-              _lib.ptr(ws), _lib.stream())
+              _lib.ptr(ws), _lib.ptr(cnt), _lib.stream())
     return out
 
 
@@ -204,16 +257,18 @@ def _kc(t, Kp, rows=None):
 
 
 def use_small(M, N, K):
-    """Skinny kernel vs the 256×256-tile assembly GEMM: the asm kernel once its tile grid (with
-    split-K) fills the chip with ≥ 128-row tiles; below that the skinny kernel's 16·mb-row tiles
-    waste less of each MFMA and start more workgroups."""
-    if M > 512:
-        return False
-    tiles = -(-M // 256) * -(-N // 256)
-    return M <= 256 or tiles < 64
+    """Skinny kernel vs the 256×256-tile assembly GEMM (graph-timed sweep,
+    profiles/small_gemm_tune_r4.jsonl): the skinny kernel for ≤ 64 rows, for ≤ 128 rows unless K
+    is very long, and up to 512 rows for small weights (N·K ≤ 2048²); the asm GEMM with split-K
+    beyond (e.g. M=256 N=6144 K=2048: 29 µs vs 35 µs)."""
+    if M <= 64:
+        return True
+    if M <= 128 and K < 8192:
+        return True
+    return M <= 512 and N * K <= 2048 * 2048
 
 
-_FUSED_ACTS = ("none", "gelu_tanh", "relu")
+_FUSED_ACTS = ("none", "gelu_tanh", "gelu", "relu")
 
 
 def gemm_nt(a, b, alpha=1.0, bias=None, act="none", resid=None, out_f32=False):
@@ -253,11 +308,11 @@ def gemm_nt(a, b, alpha=1.0, bias=None, act="none", resid=None, out_f32=False):
 def _asm_nt(a, b, alpha, bias, act, out_f32):
     M, K = a.shape
     N = b.shape[0]
-    fused = (not out_f32 and alpha == 1.0 and act in _FUSED_ACTS
+    ks = pick_ksplit(M, N, K)
+    fused = (not out_f32 and alpha == 1.0 and act in _FUSED_ACTS and ks == 1
              and (bias is not None or act != "none"))
     if fused:
         return asm_gemm(a, b, trans_b=True, epi="bias_act", act=act, bias=bias)
-    ks = pick_ksplit(M, N, K)
     if not asm_supported(a, b, trans_b=True, ksplit=ks):
         ks = 1
     out = asm_gemm(a, b, trans_b=True, out_f32=out_f32, ksplit=ks)

@@ -43,8 +43,23 @@ def _hip_path(op, x, *params) -> bool:
 
 def _cast(p, dtype):
     """Params in the activation dtype (AMP O1 keeps LN weights f32 under bf16/fp16 activations):
-    a differentiable cast of an N-vector, so gradients flow back in the parameter's dtype."""
-    return p if p is None or p.dtype == dtype else p.to(dtype)
+    a differentiable cast of an N-vector, so gradients flow back in the parameter's dtype.
+    Without autograd (inference, AMP predictors keeping LN params f32) the cast is cached on the
+    parameter until it changes, so a run launches no per-layer cast kernels."""
+    if p is None or p.dtype == dtype:
+        return p
+    if torch.is_grad_enabled() and p.requires_grad:
+        return p.to(dtype)
+    c = getattr(p, "_piamd_cast", None)
+    key = (dtype, p._version, p.data_ptr())
+    if c is not None and c[0] == key:
+        return c[1]
+    out = p.detach().to(dtype)
+    try:
+        p._piamd_cast = (key, out)
+    except (AttributeError, RuntimeError):
+        pass
+    return out
 
 
 def _grad_target(p, needed, N, dtype, device):

@@ -74,6 +74,33 @@ def test_asm_fp16_fused_epilogues(act):
         _close(d, (dy.float() @ w2.float().t()) * gd, 0.01)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("with_aux", [False, True])
+def test_asm_exact_gelu_epilogue(dtype, with_aux):
+    """bias + exact (erf) GELU fused into the asm epilogue: within the output dtype's rounding of
+    the erf reference, including the negative tail where the tanh form drifts."""
+    from paddle_infer_amd.ops.gemm import asm_gemm
+    M, N, K = 1030, 1024, 512
+    x = _rand(M, K, dtype=dtype)
+    w = _rand(N, K, dtype=dtype, scale=0.12, seed=1)
+    bias = _rand(N, dtype=dtype, seed=2)
+    aux = torch.empty(M, N, device=DEV, dtype=dtype) if with_aux else None
+    y = asm_gemm(x, w, trans_b=True, epi="bias_act", act="gelu", bias=bias, aux=aux)
+    pre = (x.float() @ w.float().t() + bias.float()).requires_grad_(True)
+    ref = torch.nn.functional.gelu(pre)
+    dg, = torch.autograd.grad(ref.sum(), pre)
+    pre, ref = pre.detach(), ref.detach()
+    ulp = 2.0 ** (-8 if dtype == torch.bfloat16 else -11)
+    # the 16-bit rounding of pre (one ulp either way vs the fp32 reference) plus the output's
+    tol = 1.5 * ulp * (ref.abs() + (pre * dg).abs()) + 1e-5
+    err = (y.float() - ref).abs()
+    bad = err > tol
+    assert not bad.any(), (pre[bad][:8], ref[bad][:8], y.float()[bad][:8])
+    if with_aux:  # exactly the GELU of the stored pre-activation, up to the output rounding
+        r2 = torch.nn.functional.gelu(aux.float())
+        assert ((y.float() - r2).abs() <= ulp * r2.abs() + 1e-6).all()
+
+
 # ---------------------------------------------------------------------------- batched asm
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
@@ -101,11 +128,16 @@ def test_small_gemm_configs(dtype, M, N, K):
     ref = a.float() @ b.float().t()
     cfgs = {small_cfg(M, N, K)}
     for mb, nb in sorted(_SG_SHAPES):
-        for ks in (1, 2, 4):
-            if ks <= K // 64:
-                cfgs.add((mb, nb, ks))
+        for wn in (1, 2, 4):
+            for ks in (1, 2, 4):
+                if ks <= K // 64:
+                    cfgs.add((mb, nb, wn, 1 + (ks + wn) % 2, ks))
     for cfg in sorted(cfgs):
         _close(small_gemm(a, b, cfg=cfg), ref, 0.01)
+        if cfg[4] > 1:
+            _close(small_gemm(a, b, cfg=cfg, slices=True), ref, 0.01)
+    # the fixup workspace is left zeroed: a second call gives the same result
+    _close(small_gemm(a, b), ref, 0.01)
 
 
 @pytest.mark.parametrize("act", ["none", "gelu_tanh", "gelu", "relu", "silu"])
@@ -121,7 +153,7 @@ def test_small_gemm_epilogue(act):
            "gelu": torch.nn.functional.gelu(pre),
            "gelu_tanh": torch.nn.functional.gelu(pre, approximate="tanh")}[act] + resid.float()
     for ks in (1, 4):
-        got = small_gemm(a, b, alpha=0.5, bias=bias, act=act, resid=resid, cfg=(4, 2, ks))
+        got = small_gemm(a, b, alpha=0.5, bias=bias, act=act, resid=resid, cfg=(4, 2, 2, 2, ks))
         _close(got, ref, 0.01)
     got = small_gemm(a, b, out_f32=True, alpha=0.5, bias=bias, act=act, resid=resid)
     assert got.dtype == torch.float32

@@ -199,6 +199,9 @@ class Kernel:
                  "dgelu": ("dact", 1), "drelu": ("dact", 3), "biasnx": ("bias_act", 0)}
         self.ek, self.act = fused.get(ek, (ek, 0))
         self.store_aux = ek != "biasnx"  # biasnx: C = acc + bias, no pre-activation output
+        self.NBW = 8                    # 16-column accumulator blocks per wave row
+        # resources: LDS bytes, workgroup size, accum_offset, AGPR count
+        self.lds_bytes, self.wg_size, self.acc_off, self.n_agpr = LDS_BYTES, 256, ACC_OFF, 256
         assert self.ek not in ("bias_act", "dact") or (a_kc and b_kc)  # descriptor SGPRs 40..47
         self.lines = []
         self.nlab = 0
@@ -770,12 +773,9 @@ class Kernel:
             self.e(f"s_cmp_eq_u32 s{T + 2}, 0")
             self.e(f"s_cselect_b32 s{a + 2}, 0, s{a + 2}")
             self.e(f"s_mov_b32 s{a + 3}, 0x20000")
-        # lane offsets: row (wr*128 + (l&15)), col (wc*128 + 4(l>>4))
+        # lane offsets: row (wave row origin + (l&15)), col (wave col origin + 4(l>>4))
         L = V_LANE
-        self.e(f"s_lshr_b32 s{T + 4}, s{S_WAVE}, 1")
-        self.e(f"s_lshl_b32 s{T + 4}, s{T + 4}, 7")
-        self.e(f"s_and_b32 s{T + 5}, s{S_WAVE}, 1")
-        self.e(f"s_lshl_b32 s{T + 5}, s{T + 5}, 7")
+        self.wave_origin(T + 4, T + 5)
         self.e(f"v_and_b32 v{V}, 15, v{L}")
         self.e(f"v_add_u32 v{V}, s{T + 4}, v{V}")                    # local row
         self.e(f"v_lshrrev_b32 v{V + 1}, 4, v{L}")
@@ -803,7 +803,7 @@ class Kernel:
             self.e(f"s_cselect_b32 s{b + 2}, 0, s{T + 1}")
             self.e(f"s_mov_b32 s{b + 3}, 0x20000")
             self.e(f"v_lshlrev_b32 v{V + 7}, 1, v{V + 1}")
-            for nb in range(8):
+            for nb in range(self.NBW):
                 self.e(f"buffer_load_dwordx2 v[{self.VBIAS + 2 * nb}:{self.VBIAS + 2 * nb + 1}], v{V + 7}, s[{b}:{b + 3}], 0 offen offset:{nb * 32}")
             self.e("s_waitcnt vmcnt(0)")
         self.e(f"v_add_u32 v{V + 4}, s{S_N0T}, v{V + 1}")            # global col (nb = 0)
@@ -835,6 +835,16 @@ class Kernel:
         self.store_all(masked=False)
         self.lab(done)
 
+    def wave_origin(self, r, c):
+        """s{r} / s{c} ← this wave's row / column origin in the tile (2×2 waves of 128×128)."""
+        self.e(f"s_lshr_b32 s{r}, s{S_WAVE}, 1")
+        self.e(f"s_lshl_b32 s{r}, s{r}, 7")
+        self.e(f"s_and_b32 s{c}, s{S_WAVE}, 1")
+        self.e(f"s_lshl_b32 s{c}, s{c}, 7")
+
+    def accf(self, mb, nb):
+        return acc(mb, nb)
+
     def load_group(self, mb, buf):
         """Issue the epilogue loads of row block mb (old C for accumulate, aux for dact) into
         buffer `buf`; returns the VMEM instruction count."""
@@ -849,7 +859,7 @@ class Kernel:
         else:
             self.e(f"s_mul_i32 s{T + 8}, s{E + 4}, {16 * mb}")
             self.e(f"v_add_u32 v{V + 7}, s{T + 8}, v{V + 2}")
-        for nb in range(8):
+        for nb in range(self.NBW):
             if ek == "f32acc":
                 d = V + 40 + 32 * buf + 4 * nb
                 self.e(f"buffer_load_dwordx4 v[{d}:{d + 3}], v{V + 7}, s[{srd}:{srd + 3}], 0 offen offset:{nb * 64}")
@@ -857,7 +867,7 @@ class Kernel:
                 d = V + 40 + 16 * buf + 2 * nb
                 rs = S_AUXSRD if ek == "dact" else srd
                 self.e(f"buffer_load_dwordx2 v[{d}:{d + 1}], v{V + 7}, s[{rs}:{rs + 3}], 0 offen offset:{nb * 32}")
-        return 8
+        return self.NBW
 
     def store_all(self, masked):
         """Per 16-row block (mb): convert / fuse / store the 8 accumulator blocks of the row.
@@ -892,8 +902,8 @@ class Kernel:
                 self.e(f"v_add_u32 v{V + 6}, s{T + 8}, v{V + 3}")
                 if paired:
                     self.e(f"v_add_u32 v{V + E_PAIR + 3}, s{T + 8}, v{V + E_PAIR + 1}")
-            for nb in range(8):
-                c = acc(mb, nb)
+            for nb in range(self.NBW):
+                c = self.accf(mb, nb)
                 d = W + 4 * nb
                 for j in range(4):
                     self.e(f"v_accvgpr_read_b32 v{d + j}, a{c + j}")
@@ -1110,16 +1120,16 @@ class Kernel:
             "\t.rodata",
             "\t.p2align 6",
             f"\t.amdhsa_kernel {n}",
-            f"\t\t.amdhsa_group_segment_fixed_size {LDS_BYTES}",
+            f"\t\t.amdhsa_group_segment_fixed_size {self.lds_bytes}",
             "\t\t.amdhsa_private_segment_fixed_size 0",
             f"\t\t.amdhsa_kernarg_size {ARGS_SIZE}",
             "\t\t.amdhsa_user_sgpr_count 2",
             "\t\t.amdhsa_user_sgpr_kernarg_segment_ptr 1",
             "\t\t.amdhsa_system_sgpr_workgroup_id_x 1",
             "\t\t.amdhsa_system_vgpr_workitem_id 0",
-            f"\t\t.amdhsa_next_free_vgpr {NVGPR}",
+            f"\t\t.amdhsa_next_free_vgpr {self.acc_off + self.n_agpr}",
             f"\t\t.amdhsa_next_free_sgpr {NSGPR}",
-            f"\t\t.amdhsa_accum_offset {ACC_OFF}",
+            f"\t\t.amdhsa_accum_offset {self.acc_off}",
             "\t\t.amdhsa_reserve_vcc 1",
             "\t\t.amdhsa_float_denorm_mode_32 3",
             "\t\t.amdhsa_float_denorm_mode_16_64 3",
@@ -1136,17 +1146,17 @@ class Kernel:
       - .offset:         0
         .size:           {ARGS_SIZE}
         .value_kind:     by_value
-    .group_segment_fixed_size: {LDS_BYTES}
+    .group_segment_fixed_size: {self.lds_bytes}
     .kernarg_segment_align: 8
     .kernarg_segment_size: {ARGS_SIZE}
-    .max_flat_workgroup_size: 256
+    .max_flat_workgroup_size: {self.wg_size}
     .name:           {n}
     .private_segment_fixed_size: 0
     .sgpr_count:     {NSGPR + 6}
     .sgpr_spill_count: 0
     .symbol:         {n}.kd
-    .vgpr_count:     {NVGPR}
-    .agpr_count:     256
+    .vgpr_count:     {self.acc_off + self.n_agpr}
+    .agpr_count:     {self.n_agpr}
     .vgpr_spill_count: 0
     .wavefront_size: 64
 """
@@ -1174,8 +1184,31 @@ def variants():
                 yield f"piamd_agemm_{tag}nt_{ek}{sfx}", True, True, ek, pers, f16
 
 
+def pp_module():
+    """The 8-wave ping-pong NT generator (gemm_gen_pp.py, next to this file)."""
+    import importlib.util
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_gen_pp.py")
+    spec = importlib.util.spec_from_file_location("gemm_gen_pp", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def this_module():
+    """This generator as a module object (also when loaded by path without sys.modules)."""
+    import types
+    m = sys.modules.get(__name__)
+    if m is not None and getattr(m, "Kernel", None) is Kernel:
+        return m
+    return types.SimpleNamespace(**globals())
+
+
 def generate() -> str:
     ks = [Kernel(n, a, b, ek, pers, f16) for n, a, b, ek, pers, f16 in variants()]
+    pp = pp_module()
+    me = this_module()
+    KPP = pp.make_kernel_pp(me)
+    ks += [KPP(n, ek, f16) for n, ek, f16 in pp.variants_pp(me)]
     out = ['\t.amdgcn_target "amdgcn-amd-amdhsa--gfx950"', "\t.amdhsa_code_object_version 5"]
     for k in ks:
         out.append(k.text())

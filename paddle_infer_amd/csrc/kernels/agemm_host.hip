@@ -166,8 +166,14 @@ PIAMD_EXPORT int piamd_agemm(const void* a, long long lda, int trans_a, const vo
   // even K-block count >= 4; otherwise one tile per workgroup
   const int nk = K / ksplit / 64;
   const bool persistent = nk % 2 == 0 && nk >= 4 && !getenv("PIAMD_AGEMM_NO_PERSIST");
-  const std::string name = std::string("piamd_agemm_") + (persistent ? "p_" : "") + lay + "_" + ek +
-                           (f16 ? "_f16" : "");
+  // NT products take the 8-wave ping-pong kernel (two waves per SIMD, `gemm_gen_pp.py`)
+  static const bool use_pp = [] {
+    const char* e = getenv("PIAMD_AGEMM_PP");  // opt-in until measured (1 = on)
+    return e && atoi(e) > 0;
+  }();
+  const bool pp = persistent && a_kc && b_kc && use_pp;
+  const std::string name = std::string("piamd_agemm_") + (pp ? "q_" : persistent ? "p_" : "") + lay +
+                           "_" + ek + (f16 ? "_f16" : "");
   hipFunction_t f = get_fn(name);
   if (!f) return (int)hipErrorInvalidDeviceFunction;
   g.a = a;
@@ -210,7 +216,7 @@ PIAMD_EXPORT int piamd_agemm(const void* a, long long lda, int trans_a, const vo
   size_t sz = sizeof(g);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &g, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
                  HIP_LAUNCH_PARAM_END};
-  hipError_t err = hipModuleLaunchKernel(f, g.grid, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
+  hipError_t err = hipModuleLaunchKernel(f, g.grid, 1, 1, pp ? 512 : 256, 1, 1, 0, st, nullptr, cfg);
   if (err != hipSuccess || ksplit == 1) return (int)err;
   const long long q = (long long)M * N / 4;
   const int grid = (int)std::min<long long>(2048, (q + 255) / 256);

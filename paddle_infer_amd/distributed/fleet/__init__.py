@@ -318,6 +318,16 @@ def distributed_model(model):
             w = _wrap_stage3(model, hcg, st, s3_groups)
         _STATE["wrapper"] = w
         return w
+    from .meta_optimizers import check_comm_reducing, comm_reducing
+    check_comm_reducing(st, hcg)
+    if comm_reducing(st) and hcg.get_data_parallel_world_size() > 1:
+        # the LocalSGD / DGC optimizer owns the dp communication: no gradient reducer; replicas
+        # start identical
+        with torch.no_grad():
+            src = hcg.get_data_parallel_group_src_rank()
+            for p in list(model.parameters()) + list(model.buffers()):
+                dist.broadcast(p.data, src, group=hcg.get_data_parallel_group())
+        return model
     if isinstance(model, PipelineLayer) and hcg.get_pipe_parallel_world_size() > 1:
         w = PipelineParallel(model, hcg, st)
     elif hcg.get_model_parallel_world_size() > 1 or hcg.get_sharding_parallel_world_size() > 1 or st.sharding:
@@ -529,8 +539,13 @@ def distributed_optimizer(optimizer, strategy=None):
         return optimizer
     st = _strategy()
     from .meta_optimizers import check_strategy, swap_optimizer, wrap_optimizer
+    from .meta_optimizers import check_comm_reducing, comm_reducing, wrap_comm_reducing
     check_strategy(st)
     optimizer = swap_optimizer(optimizer, st)
+    from ... import in_dynamic_mode
+    if comm_reducing(st) and in_dynamic_mode():
+        check_comm_reducing(st, hcg)
+        return wrap_comm_reducing(optimizer, st, hcg)
     s3 = _STATE.get("stage3")
     if s3 is not None:
         from ..sharding import _Stage3Optimizer

@@ -18,6 +18,9 @@ ignored:
   configured coefficients (reference meta-optimizers swap the same way).
 * ``asp``: the optimizer re-applies the 2:4 masks after each update (``incubate.asp.decorate``).
 * ``sync_batch_norm``: BatchNorm layers become SyncBatchNorm.
+* ``localsgd`` / ``adaptive_localsgd`` / ``dgc``: the optimizer owns the data-parallel
+  communication (periodic parameter averaging, or top-k sparsified momentum-corrected gradients;
+  `comm_optimizers.py`) and the model gets no gradient reducer.
 * Static mode: ``distributed_optimizer(opt).minimize(loss)`` appends backward + optimizer ops and
   inserts one ``c_allreduce_sum`` + ``scale`` per gradient before the first optimizer op (data
   parallel over ring 0), so the saved program carries its collectives like the reference's.
@@ -26,13 +29,10 @@ from __future__ import annotations
 
 import torch
 
-# switches this framework does not implement (parameter server, DGC / local SGD compression,
-# quantisation-aware training, auto-parallel search): setting one raises instead of being ignored
+# switches this framework does not implement (parameter server, quantisation-aware training,
+# auto-parallel search): setting one raises instead of being ignored
 REJECTED = {
     "a_sync": "parameter-server training is out of scope",
-    "dgc": "deep gradient compression is not implemented",
-    "localsgd": "local SGD is not implemented",
-    "adaptive_localsgd": "adaptive local SGD is not implemented",
     "qat": "use paddle_infer_amd.quantization for quantization-aware training",
     "auto": "use paddle_infer_amd.distributed.auto_parallel (Engine) for auto-parallel",
     "semi_auto": "use paddle_infer_amd.distributed.auto_parallel (Engine) for semi-auto parallel",
@@ -44,12 +44,51 @@ REJECTED = {
 }
 
 
+COMM_REDUCING = ("localsgd", "adaptive_localsgd", "dgc")
+
+
+def comm_reducing(st):
+    """The switch (if any) whose optimizer owns the data-parallel communication."""
+    for f in COMM_REDUCING:
+        if getattr(st, f, False):
+            return f
+    return None
+
+
+def check_comm_reducing(st, hcg):
+    f = comm_reducing(st)
+    if f is None or hcg is None:
+        return
+    if (hcg.get_model_parallel_world_size() > 1 or hcg.get_pipe_parallel_world_size() > 1
+            or hcg.get_sharding_parallel_world_size() > 1 or st.sharding):
+        raise NotImplementedError(f"DistributedStrategy.{f}: pure data parallelism only "
+                                  "(no tensor / pipeline / sharding axes)")
+
+
+def wrap_comm_reducing(opt, st, hcg):
+    """localsgd / adaptive_localsgd / dgc around the inner optimizer (they replace the gradient
+    all-reduce: `comm_optimizers.py`)."""
+    from . import comm_optimizers as C
+    g = hcg.get_data_parallel_group() if hcg is not None else None
+    if st.localsgd:
+        c = st.localsgd_configs or {}
+        return C.LocalSGDOptimizer(opt, g, c.get("k_steps", 1), c.get("begin_step", 1))
+    if st.adaptive_localsgd:
+        c = st.adaptive_localsgd_configs or {}
+        return C.AdaptiveLocalSGDOptimizer(opt, g, c.get("init_k_steps", 1), c.get("begin_step", 1))
+    c = st.dgc_configs or {}
+    return C.DGCMomentumOptimizer(opt, g, c.get("rampup_begin_step", 0), c.get("rampup_step", 1),
+                                  c.get("sparsity", [0.999]))
+
+
 def check_strategy(st):
     for f, why in REJECTED.items():
         if getattr(st, f, False):
             raise NotImplementedError(f"DistributedStrategy.{f} = True: {why}")
     if st.lamb and st.lars:
         raise ValueError("DistributedStrategy: lamb and lars are mutually exclusive")
+    if sum(bool(getattr(st, f, False)) for f in COMM_REDUCING) > 1:
+        raise ValueError("DistributedStrategy: localsgd, adaptive_localsgd and dgc are mutually exclusive")
     if int(st.nccl_comm_num) != 1:
         raise NotImplementedError("nccl_comm_num > 1: one RCCL communicator per group is used")
     scale = (st.gradient_scale_configs or {}).get("scale_strategy", "avg")

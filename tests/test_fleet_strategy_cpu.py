@@ -44,7 +44,7 @@ def test_unknown_field_and_config_key_raise():
     assert st.sharding_configs["stage"] == 3 and "segment_broadcast_MB" in st.sharding_configs
 
 
-@pytest.mark.parametrize("flag", ["dgc", "localsgd", "adaptive_localsgd", "a_sync",
+@pytest.mark.parametrize("flag", ["a_sync",
                                   "heter_ccl_mode", "auto", "semi_auto", "qat"])
 def test_unsupported_switches_raise(flag):
     st = fleet.DistributedStrategy()

@@ -124,7 +124,9 @@ def timeit(fn, iters):
 def bench(T, rounds, shapes):
     from paddle_infer_amd.ops.gemm import asm_gemm, pick_ksplit
     allshapes = {"qkv": (2048, 6144), "out": (2048, 2048), "ffn1": (2048, 8192), "ffn2": (8192, 2048),
-                 "head": (2048, 50304)}
+                 "head": (2048, 50304),
+                 # BERT-Large (T = batch 128 × seq 128 = 16384)
+                 "bqkv": (1024, 3072), "bout": (1024, 1024), "bffn1": (1024, 4096), "bffn2": (4096, 1024)}
     gen = torch.Generator(device="cuda").manual_seed(0)
     for name in shapes:
         K, N = allshapes[name]

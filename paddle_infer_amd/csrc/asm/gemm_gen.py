@@ -1208,7 +1208,7 @@ def generate() -> str:
     pp = pp_module()
     me = this_module()
     KPP = pp.make_kernel_pp(me)
-    ks += [KPP(n, ek, f16) for n, ek, f16 in pp.variants_pp(me)]
+    ks += [KPP(n, ek, f16, **kw) for n, ek, f16, kw in pp.variants_pp(me)]
     out = ['\t.amdgcn_target "amdgcn-amd-amdhsa--gfx950"', "\t.amdhsa_code_object_version 5"]
     for k in ks:
         out.append(k.text())

@@ -84,8 +84,11 @@ def make_kernel_pp(gg):
     Base = gg.Kernel
 
     class KPP(Base):
-        def __init__(self, name, ek, f16=False):
+        def __init__(self, name, ek, f16=False, prio=False, dma_first=False):
             super().__init__(name, True, True, ek, persistent=True, f16=f16)
+            # schedule options (A/B variants): s_setprio 1 around each compute phase's MFMAs;
+            # a load phase issuing its DMAs before its fragment reads
+            self.prio, self.dma_first = prio, dma_first
             self.VE = Q_VE
             self.VBIAS, self.VTMP, self.VCONST = self.VE + gg.E_BIAS, self.VE + gg.E_TMP, self.VE + gg.E_CONST
             self.NBW = 4
@@ -265,6 +268,10 @@ def make_kernel_pp(gg):
             rd = self.reads(read_stage)
             self.ev("read", read_stage)
             di = 0
+            if self.dma_first and split is None:
+                for d in dma:
+                    self.emit_dma(d)
+                di = len(dma)
             for i, r in enumerate(rd):
                 self.e(r)
                 if i % 3 == 2 and di < len(dma):
@@ -282,7 +289,11 @@ def make_kernel_pp(gg):
             self.barrier()
 
         def compute_phase(self, zero=False):
+            if self.prio:
+                self.e("s_setprio 1")
             self.compute(zero)
+            if self.prio:
+                self.e("s_setprio 0")
             self.barrier()
 
         def advance(self, op):
@@ -459,11 +470,14 @@ def make_kernel_pp(gg):
 
 
 def variants_pp(gg):
-    """NT ping-pong kernels: every plain and fused epilogue, bf16 and fp16."""
+    """NT ping-pong kernels: every plain and fused epilogue, bf16 and fp16; plus schedule A/B
+    variants of the plain bf16 kernel (``_v1`` setprio, ``_v2`` DMAs first, ``_v3`` both)."""
     for f16 in (False, True):
         sfx = "_f16" if f16 else ""
         for ek in gg.EPILOGUES + gg.FUSED:
-            yield f"piamd_agemm_q_nt_{ek}{sfx}", ek, f16
+            yield f"piamd_agemm_q_nt_{ek}{sfx}", ek, f16, {}
+    for v, kw in ((1, {"prio": True}), (2, {"dma_first": True}), (3, {"prio": True, "dma_first": True})):
+        yield f"piamd_agemm_q_nt_bf16_v{v}", "bf16", False, kw
 
 
 if __name__ == "__main__":

@@ -69,7 +69,9 @@ int num_cus() {
   return n;
 }
 
-// C (+)= Σ_p ws[p] in a fixed order (deterministic); 4 columns per thread
+// C (+)= Σ_p ws[p] in a fixed order (deterministic); 4 columns per thread; 16-bit C is bf16 or
+// (F16) IEEE fp16
+template <bool F16>
 __global__ __launch_bounds__(256) void agemm_reduce_kernel(const float* __restrict__ ws, int ksplit,
                                                            int M, int N, void* __restrict__ c,
                                                            long long ldc, int c_f32, int accumulate) {
@@ -90,7 +92,7 @@ __global__ __launch_bounds__(256) void agemm_reduce_kernel(const float* __restri
       u16x4 o;
       const u16x4 old = accumulate ? *pc : u16x4{0, 0, 0, 0};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = f2bf(v[j] + (accumulate ? bf2f(old[j]) : 0.f));
+      for (int j = 0; j < 4; ++j) o[j] = f2h<F16>(v[j] + (accumulate ? h2f<F16>(old[j]) : 0.f));
       *pc = o;
     }
   }
@@ -172,8 +174,13 @@ PIAMD_EXPORT int piamd_agemm(const void* a, long long lda, int trans_a, const vo
     return e && atoi(e) > 0;
   }();
   const bool pp = persistent && a_kc && b_kc && use_pp;
-  const std::string name = std::string("piamd_agemm_") + (pp ? "q_" : persistent ? "p_" : "") + lay +
-                           "_" + ek + (f16 ? "_f16" : "");
+  static const std::string ppv = [] {  // PIAMD_AGEMM_PPV=N: schedule A/B variant (plain bf16 only)
+    const char* e = getenv("PIAMD_AGEMM_PPV");
+    return std::string(e && *e ? std::string("_v") + e : "");
+  }();
+  std::string name = std::string("piamd_agemm_") + (pp ? "q_" : persistent ? "p_" : "") + lay + "_" + ek +
+                     (f16 ? "_f16" : "");
+  if (pp && !ppv.empty() && !f16 && std::string(ek) == "bf16") name += ppv;
   hipFunction_t f = get_fn(name);
   if (!f) return (int)hipErrorInvalidDeviceFunction;
   g.a = a;
@@ -220,7 +227,11 @@ PIAMD_EXPORT int piamd_agemm(const void* a, long long lda, int trans_a, const vo
   if (err != hipSuccess || ksplit == 1) return (int)err;
   const long long q = (long long)M * N / 4;
   const int grid = (int)std::min<long long>(2048, (q + 255) / 256);
-  hipLaunchKernelGGL(agemm_reduce_kernel, dim3(grid), dim3(256), 0, st, (const float*)ws, ksplit, M,
-                     N, c, ldc, c_f32, accumulate);
+  if (f16)
+    hipLaunchKernelGGL(agemm_reduce_kernel<true>, dim3(grid), dim3(256), 0, st, (const float*)ws, ksplit,
+                       M, N, c, ldc, c_f32, accumulate);
+  else
+    hipLaunchKernelGGL(agemm_reduce_kernel<false>, dim3(grid), dim3(256), 0, st, (const float*)ws, ksplit,
+                       M, N, c, ldc, c_f32, accumulate);
   return (int)hipGetLastError();
 }

@@ -201,14 +201,14 @@ def _check_schedule(streams, nk32, ntiles):
 
 def test_pp_schedule_races():
     K = pp.make_kernel_pp(gg.this_module())
-    for ek in ("bf16", "biasgelu", "f32acc"):
-        k = K("x", ek)
+    for ek, kw in (("bf16", {}), ("biasgelu", {}), ("f32acc", {}), ("bf16", {"prio": True, "dma_first": True})):
+        k = K("x", ek, **kw)
         for nk64, ntiles in ((4, 1), (4, 3), (6, 2), (16, 2)):
             _check_schedule(k.schedule_trace(nk64, ntiles), 2 * nk64, ntiles)
 
 
 def test_pp_kernels_emitted():
     text = gg.generate()
-    for name, ek, f16 in pp.variants_pp(gg.this_module()):
+    for name, ek, f16, _ in pp.variants_pp(gg.this_module()):
         assert f"{name}:" in text and f".amdhsa_kernel {name}" in text
     assert ".amdhsa_accum_offset 128" in text and ".max_flat_workgroup_size: 512" in text

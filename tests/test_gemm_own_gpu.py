@@ -101,6 +101,19 @@ def test_asm_exact_gelu_epilogue(dtype, with_aux):
         assert ((y.float() - r2).abs() <= ulp * r2.abs() + 1e-6).all()
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("ks", [2, 4])
+def test_asm_splitk_16bit_output(dtype, ks):
+    """Split-K into 16-bit C: the deterministic reduce writes the operands' dtype (fp16 too)."""
+    from paddle_infer_amd.ops.gemm import asm_gemm
+    M, N, K = 520, 768, 1024
+    a = _rand(M, K, dtype=dtype, scale=0.5)
+    b = _rand(N, K, dtype=dtype, scale=0.05, seed=1)
+    c = asm_gemm(a, b, trans_b=True, ksplit=ks)
+    assert c.dtype == dtype
+    _close(c, a.float() @ b.float().t(), 0.01)
+
+
 # ---------------------------------------------------------------------------- batched asm
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
@@ -279,5 +292,5 @@ def test_no_library_gemm_kernels_in_fp16_bert_layer():
                 torch.cuda.synchronize()
             names = [e.key for e in prof.key_averages()]
             lib = [n for n in names if n.startswith("Cijk") or "rocblas" in n.lower() or "gemm" in n.lower()
-                   and "piamd" not in n and "small_gemm" not in n]
+                   and "piamd" not in n and "small_gemm" not in n and "agemm" not in n]
             assert not lib, lib

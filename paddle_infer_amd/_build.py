@@ -146,8 +146,11 @@ def build_native(verbose: bool = True, jobs: int = 4) -> None:
             for f in cf.as_completed([ex.submit(_compile, c, src) for c, src in todo]):
                 if verbose:
                     print(f"[piamd build] compiled native/{os.path.basename(f.result())}", flush=True)
-    if todo or not os.path.exists(NATIVE_LIB):
+    if todo or not os.path.exists(NATIVE_LIB) or os.path.getmtime(NATIVE_LIB) < os.path.getmtime(KERNEL_LIB):
+        # the 16-bit GPU path (fast_ops.hip) calls the framework's kernels: link libpiamd_kernels.so
+        # from the same directory (rpath $ORIGIN), no Python
         _compile([HIPCC, "-shared", *objs, "-o", NATIVE_LIB + ".tmp", f"--offload-arch={ARCH}",
+                  f"-L{LIBDIR}", "-lpiamd_kernels", "-Wl,-rpath,$ORIGIN", "-ldl",
                   f"-L{ROCM}/lib", "-lrocblas", "-pthread", f"-Wl,-rpath,{ROCM}/lib"], NATIVE_LIB)
         os.replace(NATIVE_LIB + ".tmp", NATIVE_LIB)
         if verbose:

@@ -46,24 +46,8 @@
 #include <type_traits>
 
 // C ABI argument block (ops/attention.py mirrors it as a ctypes.Structure).
-struct FaArgs {
-  const void *q, *k, *v;
-  void* o;
-  float* lse;
-  const void* dout;
-  float* delta;  // backward scratch: 2 x rows f32 (−δ, −lse/scale)
-  void *dq, *dk, *dv;
-  const void* mask;  // additive, input dtype; null = none
-  const int *cu_q, *cu_k;
-  int B, Sq, Sk, Hq, Hk, D, ltot, causal;
-  long long sqb, sqs, sqh, skb, sks, skh, svb, svs, svh, sob, sos, soh;
-  long long smb, smh, smq;  // mask strides (elements; 0 = broadcast)
-  float scale, p_drop;
-  unsigned long long seed, offset;
-  int map;  // backward grid order, bit 0 dQ / bit 1 dK-dV kernel: 0 = the blocks of one (batch,
-            // head) spread over the grid, 1 = grouped on one XCD (fa_map) so they share that head's
-            // K/V (dQ) or Q/dO (dK-dV) panels in L2 (set by the entry point)
-};
+#include "fa_args.h"
+
 
 namespace fa {
 

@@ -107,12 +107,15 @@ struct DTensor {
 std::unordered_map<std::string, DTensor> load_params(const ProgramDesc& prog, const std::string& bytes);
 
 // ------------------------------------------------------------------------------ execution
+struct FastState;  // fast_ops.hip: weight copies and GEMM workspaces of the 16-bit GPU path
+
 struct Ctx {
   bool gpu = false;
   void* stream = nullptr;  // hipStream_t
   void* blas = nullptr;    // rocblas_handle
   int device = 0;
   int threads = 1;
+  std::shared_ptr<FastState> fast;
 };
 
 using Scope = std::unordered_map<std::string, DTensor>;
@@ -128,5 +131,12 @@ void dev_copy(void* dst, const void* src, size_t bytes, int kind /*0 h2d 1 d2h 2
 void dev_sync(Ctx& c);
 DTensor to_device(const DTensor& t, Ctx& c);
 DTensor to_host(const DTensor& t, Ctx& c);
+// hipGraph capture of the predictor's stream (relaxed mode: allocations stay outside the graph)
+void graph_begin(Ctx& c);
+void* graph_end(Ctx& c);  // instantiated executable graph
+void graph_launch(Ctx& c, void* exec);
+void graph_destroy(void* exec);
+// bf16 / fp16 → f32 on the host (output handles)
+void half_to_float(const void* src, int dtype, float* dst, int64_t n);
 
 }  // namespace pdn

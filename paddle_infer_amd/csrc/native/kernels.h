@@ -70,6 +70,21 @@ struct Strided {  // out (contiguous, dims) = src[offset + Σ idx·stride] (elem
 PDN_KERNELS(cpu)
 PDN_KERNELS(gpu)
 
+namespace gpu {
+// bf16 (f16 = 0) / fp16 (f16 = 1) element-wise with f32 math
+void unary16(Ctx&, int op, int f16, const void* x, void* y, int64_t n, float p0, float p1);
+void binary16(Ctx&, int op, int f16, const void* a, const void* b, void* y, const Bcast& bc);
+}  // namespace gpu
+
+inline bool is16(int dt) { return dt == VT_FP16 || dt == VT_BF16; }
+
+// fast_ops.hip: ops on the framework's kernels (libpiamd_kernels.so + the assembly GEMM) for
+// bf16 / fp16 tensors on the GPU. fast_run returns false when the op / dtypes are not its own
+// (the generic implementation in ops.cc runs instead).
+bool fast_run(Ctx& c, const OpDesc& op, Scope& s);
+bool fast_knows(const std::string& type);
+void fast_release(Ctx& c);
+
 namespace kern {
 #define PDN_DISPATCH(name)                                   \
   template <typename... A>                                   \

@@ -56,8 +56,11 @@ std::vector<int64_t> host_ints(Ctx& c, const DTensor& t) {
 void elementwise(Ctx& c, const OpDesc& op, Scope& s, int bop) {
   const DTensor& x = in(c, s, op, "X");
   const DTensor& y = in(c, s, op, "Y");
-  need_f32(x, op);
-  need_f32(y, op);
+  const bool h16 = c.gpu && is16(x.dtype) && x.dtype == y.dtype;
+  if (!h16) {
+    need_f32(x, op);
+    need_f32(y, op);
+  }
   // Paddle axis broadcast: Y's dims align with X's starting at `axis` (-1: trailing)
   std::vector<int64_t> xd = x.dims, yd = y.dims;
   if (yd.size() > xd.size()) {
@@ -93,14 +96,21 @@ void elementwise(Ctx& c, const OpDesc& op, Scope& s, int bop) {
     sx *= xa[i];
     sy *= ya[i];
   }
-  DTensor o = make(c, VT_FP32, od);
+  DTensor o = make(c, h16 ? x.dtype : VT_FP32, od);
   bc.n = o.numel();
-  kern::binary(c, bop, x.data<float>(), y.data<float>(), o.data<float>(), bc);
+  if (h16) gpu::binary16(c, bop, x.dtype == VT_FP16, x.buf->p, y.buf->p, o.buf->p, bc);
+  else kern::binary(c, bop, x.data<float>(), y.data<float>(), o.data<float>(), bc);
   s[op.out("Out")] = o;
 }
 
 void unary_op(Ctx& c, const OpDesc& op, Scope& s, int uop, float p0 = 0.f, float p1 = 0.f) {
   const DTensor& x = in(c, s, op, "X");
+  if (c.gpu && is16(x.dtype)) {
+    DTensor o = make(c, x.dtype, x.dims);
+    gpu::unary16(c, uop, x.dtype == VT_FP16, x.buf->p, o.buf->p, x.numel(), p0, p1);
+    s[op.out("Out")] = o;
+    return;
+  }
   need_f32(x, op);
   DTensor o = make(c, VT_FP32, x.dims);
   kern::unary(c, uop, x.data<float>(), o.data<float>(), x.numel(), p0, p1);

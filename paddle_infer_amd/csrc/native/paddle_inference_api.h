@@ -52,10 +52,13 @@ class Config {
   bool ir_optim() const { return ir_optim_; }
   void EnableMemoryOptim(bool on = true) { mem_optim_ = on; }
   bool enable_memory_optim() const { return mem_optim_; }
+  // GPU: capture the whole Run() into one hipGraph per input-shape signature (replayed after)
+  void EnableHipGraph(bool on = true) { hip_graph_ = on; }
+  bool hip_graph_enabled() const { return hip_graph_; }
 
  private:
   std::string prog_file_, params_file_;
-  bool use_gpu_ = false, ir_optim_ = true, mem_optim_ = true;
+  bool use_gpu_ = false, ir_optim_ = true, mem_optim_ = true, hip_graph_ = false;
   int device_id_ = 0, cpu_threads_ = 1;
 };
 

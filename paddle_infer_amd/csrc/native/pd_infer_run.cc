@@ -1,5 +1,6 @@
 // Command-line driver of the native C++ predictor (no Python):
-//   pd_infer_run <model.pdmodel> <model.pdiparams> [--gpu DEV] [--threads N] [--repeat R]
+//   pd_infer_run <model.pdmodel> <model.pdiparams> [--gpu DEV] [--graph] [--threads N]
+//                [--warmup W] [--repeat R]
 //                --input NAME DTYPE D0,D1,.. FILE.bin ...  --output-dir DIR
 // Inputs are raw little-endian files; each fetch target is written to DIR/<index>.bin with its
 // shape on stdout ("output <i> <name> <dtype> d0,d1,..") and the mean Run() time last.
@@ -40,12 +41,14 @@ int main(int argc, char** argv) {
     struct In { std::string name, dtype, file; std::vector<int> dims; };
     std::vector<In> ins;
     std::string outdir = ".";
-    int repeat = 1;
+    int repeat = 1, warmup = 0;
     for (int i = 3; i < argc; ++i) {
       const std::string a = argv[i];
       if (a == "--gpu") cfg.EnableUseGpu(256, std::stoi(argv[++i]));
       else if (a == "--threads") cfg.SetCpuMathLibraryNumThreads(std::stoi(argv[++i]));
       else if (a == "--repeat") repeat = std::stoi(argv[++i]);
+      else if (a == "--warmup") warmup = std::stoi(argv[++i]);
+      else if (a == "--graph") cfg.EnableHipGraph(true);
       else if (a == "--output-dir") outdir = argv[++i];
       else if (a == "--input") {
         In in;
@@ -70,6 +73,7 @@ int main(int argc, char** argv) {
       else if (in.dtype == "int32") h->CopyFromCpu(reinterpret_cast<const int32_t*>(raw.back().data()));
       else throw std::runtime_error("unsupported input dtype " + in.dtype);
     }
+    for (int r = 0; r < warmup; ++r) pred->Run();
     double ms = 0.0;
     for (int r = 0; r < repeat; ++r) {
       const auto t0 = std::chrono::steady_clock::now();
@@ -85,7 +89,9 @@ int main(int argc, char** argv) {
       std::string dt;
       std::string bytes;
       switch (h->type()) {
-        case DataType::FLOAT32: dt = "float32"; bytes.resize(n * 4); h->CopyToCpu(reinterpret_cast<float*>(&bytes[0])); break;
+        case DataType::FLOAT32:
+        case DataType::FLOAT16:  // 16-bit outputs are written as float32
+          dt = "float32"; bytes.resize(n * 4); h->CopyToCpu(reinterpret_cast<float*>(&bytes[0])); break;
         case DataType::INT64: dt = "int64"; bytes.resize(n * 8); h->CopyToCpu(reinterpret_cast<int64_t*>(&bytes[0])); break;
         case DataType::INT32: dt = "int32"; bytes.resize(n * 4); h->CopyToCpu(reinterpret_cast<int32_t*>(&bytes[0])); break;
         default: throw std::runtime_error("unsupported output dtype");

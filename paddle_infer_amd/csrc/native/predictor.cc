@@ -3,8 +3,10 @@
 #include <algorithm>
 #include <fstream>
 #include <sstream>
+#include <type_traits>
 
 #include "engine.h"
+#include "kernels.h"
 #include "paddle_inference_api.h"
 
 namespace paddle_infer {
@@ -35,6 +37,7 @@ DataType to_api(int vt) {
     case pdn::VT_UINT8: return DataType::UINT8;
     case pdn::VT_INT8: return DataType::INT8;
     case pdn::VT_FP16: return DataType::FLOAT16;
+    case pdn::VT_BF16: return DataType::FLOAT16;  // 16-bit float (CopyToCpu<float> converts)
     case pdn::VT_BOOL: return DataType::BOOL;
   }
   throw std::runtime_error("unsupported dtype " + std::to_string(vt));
@@ -63,7 +66,8 @@ class PredictorImpl {
     for (const auto& op : prog.blocks[0].ops) {
       if (op.type == "feed") fd.emplace_back(op.ai("col", (int64_t)fd.size()), op.out("Out"));
       else if (op.type == "fetch") ft.emplace_back(op.ai("col", (int64_t)ft.size()), op.in("X"));
-      else if (!reg.count(op.type) && std::find(unknown.begin(), unknown.end(), op.type) == unknown.end())
+      else if (!reg.count(op.type) && !(c.use_gpu() && pdn::fast_knows(op.type)) &&
+               std::find(unknown.begin(), unknown.end(), op.type) == unknown.end())
         unknown.push_back(op.type);
     }
     if (!unknown.empty()) {
@@ -88,24 +92,73 @@ class PredictorImpl {
                                           params(o.params) {
     ctx = o.ctx;
     ctx.stream = ctx.blas = nullptr;
+    ctx.fast.reset();
     if (ctx.gpu) pdn::dev_init(ctx);  // own stream / BLAS handle, shared resident weights
   }
   ~PredictorImpl() {
     scope.clear();
+    graph_scope.clear();
     if (ctx.gpu) {
+      pdn::graph_destroy(graph);
       params.clear();
+      pdn::fast_release(ctx);
       pdn::dev_release(ctx);
     }
   }
 
-  bool run() {
+  void run_ops(pdn::Scope& s) {
     const auto& reg = pdn::op_registry();
-    for (auto& kv : params) scope[kv.first] = kv.second;
     for (const auto& op : prog.blocks[0].ops) {
       if (op.type == "feed" || op.type == "fetch") continue;
-      reg.at(op.type)(ctx, op, scope);
+      if (pdn::fast_run(ctx, op, s)) continue;
+      auto it = reg.find(op.type);
+      if (it == reg.end())
+        throw std::runtime_error(op.type + ": the native engine runs this op only for bf16 / fp16 on the GPU");
+      it->second(ctx, op, s);
     }
-    if (ctx.gpu) pdn::dev_sync(ctx);
+  }
+
+  // hipGraph: one capture per feed-shape signature (first Run: eager warm-up, then capture + launch)
+  void* graph = nullptr;
+  std::string graph_key;
+  pdn::Scope graph_scope;
+
+  bool run() {
+    for (auto& kv : params) scope[kv.first] = kv.second;
+    if (!(ctx.gpu && cfg.hip_graph_enabled())) {
+      run_ops(scope);
+      if (ctx.gpu) pdn::dev_sync(ctx);
+      return true;
+    }
+    std::string key;
+    for (auto& f : feeds) {
+      const auto& t = tensor(f);
+      key += f + ":" + std::to_string(t.dtype);
+      for (auto d : t.dims) key += "," + std::to_string(d);
+      key += ";";
+    }
+    if (key != graph_key) {
+      run_ops(scope);  // warm-up: weight copies, workspaces, code-object load
+      pdn::dev_sync(ctx);
+      pdn::graph_destroy(graph);
+      graph = nullptr;
+      graph_scope.clear();
+      for (auto& kv : params) graph_scope[kv.first] = kv.second;
+      for (auto& f : feeds) graph_scope[f] = tensor(f);
+      pdn::graph_begin(ctx);
+      run_ops(graph_scope);
+      graph = pdn::graph_end(ctx);
+      graph_key = key;
+    } else {
+      for (auto& f : feeds) {
+        auto& src = tensor(f);
+        auto& dst = graph_scope.at(f);
+        if (src.buf != dst.buf) pdn::dev_copy(dst.buf->p, src.buf->p, src.nbytes(), 2, ctx);
+      }
+    }
+    pdn::graph_launch(ctx, graph);
+    for (auto& f : fetches) scope[f] = graph_scope.at(f);
+    pdn::dev_sync(ctx);
     return true;
   }
 
@@ -134,6 +187,11 @@ void Tensor::CopyFromCpu(const T* data) {
 template <typename T>
 void Tensor::CopyToCpu(T* data) const {
   const pdn::DTensor& t = p_->tensor(name_);
+  if (std::is_same<T, float>::value && pdn::is16(t.dtype)) {  // 16-bit outputs read as float
+    pdn::DTensor h = t.on_dev() ? pdn::to_host(t, p_->ctx) : t;
+    pdn::half_to_float(h.buf->p, t.dtype, reinterpret_cast<float*>(data), t.numel());
+    return;
+  }
   if (t.dtype != DtOf<T>::v) throw std::runtime_error("CopyToCpu: dtype mismatch for " + name_);
   if (t.on_dev()) pdn::dev_copy(data, t.buf->p, t.nbytes(), 1, p_->ctx);
   else std::memcpy(data, t.buf->p, t.nbytes());

@@ -98,6 +98,22 @@ class Config:
         self._pass_builder = _PassBuilder(GPU_PASSES)
         self._mixed_black_list = set()
         self._notes = []
+        self._save_optim = False
+        self._optim_cache_dir = None
+
+    # ---- optimised-model cache (reference AnalysisConfig::EnableSaveOptimModel) ---------------
+    def enable_save_optim_model(self, x=True):
+        """Write the IR-optimised, precision-converted model as ``_optimized.pdmodel`` /
+        ``.pdiparams`` (into ``set_optim_cache_dir`` or the model's directory) when the predictor
+        is created — the input of the native C++ predictor's GPU path."""
+        self._save_optim = bool(x)
+
+    def set_optim_cache_dir(self, d):
+        self._optim_cache_dir = d
+
+    def optim_model_prefix(self):
+        d = self._optim_cache_dir or self._model_dir or os.path.dirname(self.prog_file() or ".") or "."
+        return os.path.join(d, "_optimized")
 
     # ---- model location -------------------------------------------------------------------
     def set_model(self, model_dir_or_prog_file, params_file=None):

@@ -137,6 +137,8 @@ class Predictor:
             for n, t in list(self._scope.vars.items()):
                 if t is not None and t.is_floating_point() and n not in config._mixed_black_list:
                     self._scope.set(n, t.to(self._cast_dtype))
+        if getattr(config, "_save_optim", False):
+            self.save_optimized_model(config.optim_model_prefix())
 
     # ---- handles --------------------------------------------------------------------------
     def get_input_names(self):
@@ -221,6 +223,18 @@ class Predictor:
         if self._device.type == "cuda":
             torch.cuda.empty_cache()
         return 0
+
+    def save_optimized_model(self, path_prefix):
+        """Write the IR-optimised program (fused ops after the passes) and its parameters in the
+        predictor's compute dtype (bf16 / fp16 under mixed precision) as ``path_prefix``
+        ``.pdmodel`` / ``.pdiparams`` — the model the native C++ predictor (``libpiamd_infer.so``,
+        ``pd_infer_run``) runs on the framework's GPU kernels. Reference: the analysis predictor's
+        optimised-model cache (``Config.enable_save_optim_model``)."""
+        blk = self._program.global_block()
+        with _static.scope_guard(self._scope):
+            _static.save_inference_model(path_prefix, [blk.vars[n] for n in self._feed_names],
+                                         [blk.vars[n] for n in self._fetch_names], self._exe,
+                                         program=self._program)
 
     def get_serialized_program(self):
         return _sio.serialize_program([self._program.global_block().vars[n] for n in self._feed_names],

@@ -64,10 +64,13 @@ def python_outputs(path, feeds):
     return [p.get_output_handle(n).copy_to_cpu() for n in p.get_output_names()]
 
 
-def native_outputs(path, feeds, tmp, gpu=None, repeat=1):
-    cmd = [RUN, path + ".pdmodel", path + ".pdiparams", "--output-dir", str(tmp), "--repeat", str(repeat)]
+def native_outputs(path, feeds, tmp, gpu=None, repeat=1, graph=False, warmup=0):
+    cmd = [RUN, path + ".pdmodel", path + ".pdiparams", "--output-dir", str(tmp), "--repeat", str(repeat),
+           "--warmup", str(warmup)]
     if gpu is not None:
         cmd += ["--gpu", str(gpu)]
+    if graph:
+        cmd += ["--graph"]
     for n, a in feeds.items():
         f = os.path.join(str(tmp), f"in_{n}.bin")
         np.ascontiguousarray(a).tofile(f)

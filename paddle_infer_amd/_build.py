@@ -12,8 +12,8 @@
 * ``_lib/libpiamd_infer.so`` + ``_lib/pd_infer_run`` — the native C++ inference engine and its
   command-line driver (``csrc/native``: reference ``paddle_inference_api.h`` Config / Predictor /
   Tensor with no Python at run time; CPU loops and gfx950 HIP kernels + rocBLAS).
-* ``_lib/libpiamd_capi.so`` — the C inference API (``csrc/capi``: reference ``capi_exp``
-  ``pd_inference_api.h``), g++ against the embedded Python runtime.
+* the C inference API (reference ``capi_exp`` ``pd_inference_api.h``, header in ``csrc/capi``) is
+  part of ``libpiamd_infer.so`` (``csrc/native/pd_capi_native.cc``), no Python.
 
 Incremental: an object is rebuilt only when its source (or a header in the same dir) is newer.
 Run ``python -m paddle_infer_amd._build`` or ``__graft_entry__.build()``.
@@ -35,7 +35,6 @@ OBJDIR = os.path.join(ROOT, "_lib", "obj")
 KERNEL_LIB = os.path.join(LIBDIR, "libpiamd_kernels.so")
 RUNTIME_LIB = os.path.join(LIBDIR, "libpiamd_runtime.so")
 CDIR = os.path.join(ROOT, "csrc", "capi")
-CAPI_LIB = os.path.join(LIBDIR, "libpiamd_capi.so")
 NDIR = os.path.join(ROOT, "csrc", "native")
 NATIVE_LIB = os.path.join(LIBDIR, "libpiamd_infer.so")
 NATIVE_RUN = os.path.join(LIBDIR, "pd_infer_run")
@@ -183,15 +182,6 @@ def build(verbose: bool = True, jobs: int | None = None) -> None:
                    ["-pthread", f"-L{ROCM}/lib", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"],
                    _newest_header(ADIR), verbose, jobs)
     build_native(verbose, jobs)
-    csrcs = sorted(glob.glob(os.path.join(CDIR, "*.cc")))
-    if csrcs:
-        import sysconfig
-        inc = sysconfig.get_paths()["include"]
-        ver = sysconfig.get_config_var("LDVERSION") or sysconfig.get_python_version()
-        libdir = sysconfig.get_config_var("LIBDIR") or "/usr/lib"
-        _build_lib(csrcs, CAPI_LIB, "g++", CXX_FLAGS + [f"-I{inc}"],
-                   ["-pthread", f"-L{libdir}", f"-lpython{ver}", "-ldl", f"-Wl,-rpath,{libdir}"],
-                   _newest_header(CDIR), verbose, jobs)
 
 
 if __name__ == "__main__":

@@ -635,6 +635,20 @@ const std::unordered_map<std::string, OpFn>& op_registry() {
       kern::cast(c, x.buf->p, x.dtype, out.buf->p, odt, x.numel());
       s[o.out("Out")] = out;
     };
+    r["fill_any_like"] = [](Ctx& c, const OpDesc& o, Scope& s) {
+      const DTensor& x = in(c, s, o, "X");
+      int dt = (int)o.ai("dtype", -1);
+      if (dt < 0) dt = x.dtype;  // -1: the input's dtype
+      DTensor out = make(c, dt, x.dims);
+      kern::fill(c, out.buf->p, dt, out.numel(), (double)o.af("value", 0.f));
+      s[o.out("Out")] = out;
+    };
+    r["fill_zeros_like"] = [](Ctx& c, const OpDesc& o, Scope& s) {
+      const DTensor& x = in(c, s, o, "X");
+      DTensor out = make(c, x.dtype, x.dims);
+      kern::fill(c, out.buf->p, x.dtype, out.numel(), 0.0);
+      s[o.out("Out")] = out;
+    };
     r["fill_constant"] = [](Ctx& c, const OpDesc& o, Scope& s) {
       std::vector<int64_t> shape = o.aints("shape");
       const int dt = (int)o.ai("dtype", VT_FP32);

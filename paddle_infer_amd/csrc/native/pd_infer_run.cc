@@ -102,7 +102,9 @@ int main(int argc, char** argv) {
       for (size_t k = 0; k < shp.size(); ++k) std::cout << (k ? "," : "") << shp[k];
       std::cout << "\n";
     }
-    std::cout << "run_ms " << ms / repeat << "\n" << GetVersion() << "\n";
+    std::cout << "run_ms " << ms / repeat << "\n" << GetVersion() << std::endl;
+    pred.reset();  // tear the predictor down while the runtime is alive (and report it)
+    std::cout << "released" << std::endl;
     return 0;
   } catch (const std::exception& e) {
     std::cerr << "error: " << e.what() << "\n";

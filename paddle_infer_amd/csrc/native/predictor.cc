@@ -96,10 +96,17 @@ class PredictorImpl {
     if (ctx.gpu) pdn::dev_init(ctx);  // own stream / BLAS handle, shared resident weights
   }
   ~PredictorImpl() {
+    if (ctx.gpu) {
+      try {
+        pdn::dev_sync(ctx);
+      } catch (...) {
+      }
+      pdn::graph_destroy(graph);  // before the buffers it references are freed
+      graph = nullptr;
+    }
     scope.clear();
     graph_scope.clear();
     if (ctx.gpu) {
-      pdn::graph_destroy(graph);
       params.clear();
       pdn::fast_release(ctx);
       pdn::dev_release(ctx);

@@ -10,6 +10,8 @@ import pytest
 
 from native_infer_util import MLP, RUN, Encoder, export, native_outputs, python_outputs
 
+import paddle_infer_amd as paddle
+from paddle_infer_amd import static
 from paddle_infer_amd.static import InputSpec
 
 pytestmark = pytest.mark.skipif(not os.path.exists(RUN), reason="native engine not built")
@@ -65,7 +67,6 @@ def test_reference_c_api_on_native_engine(tmp_path):
     """The capi_exp C client (tests/capi/capi_demo.c) linked against libpiamd_infer.so: the PD_*
     entry points run on the native engine (copy path, MutableData path, cloned predictor)."""
     from paddle_infer_amd import _build
-    from test_capi_cpu import _save_model
     from paddle_infer_amd.inference import Config, create_predictor
     prefix = str(tmp_path / "mlp")
     _save_model(prefix)
@@ -149,3 +150,40 @@ def test_corrupt_params_file_refused(tmp_path, damage):
                         str(tmp_path / "x.bin")], capture_output=True, text=True)
     assert r.returncode != 0, r.stdout
     assert "params file" in r.stderr or "truncated" in r.stderr, r.stderr
+
+
+def _save_model(prefix):
+    torch.manual_seed(0)
+    paddle.enable_static()
+    try:
+        main = static.Program()
+        with static.program_guard(main):
+            x = static.data("x", [None, 8], "float32")
+            h = static.nn.fc(x, 16, activation="relu")
+            y = static.nn.fc(h, 3)
+        exe = static.Executor(paddle.CPUPlace())
+        static.save_inference_model(prefix, [x], [y], exe, program=main)
+    finally:
+        paddle.disable_static()
+
+
+def test_native_c_api_ctypes_in_process(tmp_path):
+    from paddle_infer_amd import _build
+    """The native C API library (no Python inside) loaded into a Python process with ctypes."""
+    import ctypes
+    prefix = str(tmp_path / "mlp")
+    _save_model(prefix)
+    lib = ctypes.CDLL(_build.NATIVE_LIB)
+    lib.PD_ConfigCreate.restype = ctypes.c_void_p
+    lib.PD_PredictorCreate.restype = ctypes.c_void_p
+    lib.PD_PredictorCreate.argtypes = [ctypes.c_void_p]
+    lib.PD_ConfigSetModel.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p]
+    lib.PD_PredictorGetInputNum.restype = ctypes.c_size_t
+    lib.PD_PredictorGetInputNum.argtypes = [ctypes.c_void_p]
+    lib.PD_PredictorDestroy.argtypes = [ctypes.c_void_p]
+    cfg = lib.PD_ConfigCreate()
+    lib.PD_ConfigSetModel(cfg, (prefix + ".pdmodel").encode(), (prefix + ".pdiparams").encode())
+    pred = lib.PD_PredictorCreate(cfg)
+    assert pred
+    assert lib.PD_PredictorGetInputNum(pred) == 1
+    lib.PD_PredictorDestroy(pred)

@@ -131,8 +131,9 @@ void dev_copy(void* dst, const void* src, size_t bytes, int kind /*0 h2d 1 d2h 2
 void dev_sync(Ctx& c);
 DTensor to_device(const DTensor& t, Ctx& c);
 DTensor to_host(const DTensor& t, Ctx& c);
-// hipGraph capture of the predictor's stream (relaxed mode: allocations stay outside the graph)
-void graph_begin(Ctx& c);
+// hipGraph capture of the predictor's stream (relaxed mode: allocations stay outside the graph);
+// every device buffer allocated during the capture is appended to `keep` (the graph's lifetime)
+void graph_begin(Ctx& c, std::vector<std::shared_ptr<Buffer>>* keep);
 void* graph_end(Ctx& c);  // instantiated executable graph
 void graph_launch(Ctx& c, void* exec);
 void graph_destroy(void* exec);

@@ -31,6 +31,11 @@ Buffer::~Buffer() {
   else std::free(p);
 }
 
+// While a graph is being captured every device buffer allocated (op outputs AND the temporaries an
+// op drops when it returns) is retained here: the captured kernels keep using those addresses on
+// every replay, so none of them may be freed before the graph is destroyed.
+static thread_local std::vector<std::shared_ptr<Buffer>>* g_capture_keep = nullptr;
+
 std::shared_ptr<Buffer> alloc_buffer(size_t bytes, bool dev) {
   auto b = std::make_shared<Buffer>();
   b->bytes = bytes;
@@ -38,6 +43,7 @@ std::shared_ptr<Buffer> alloc_buffer(size_t bytes, bool dev) {
   const size_t n = bytes ? bytes : 4;
   if (dev) HIPCHK(hipMalloc(&b->p, n));
   else b->p = std::malloc(n);
+  if (dev && g_capture_keep) g_capture_keep->push_back(b);
   return b;
 }
 
@@ -67,9 +73,13 @@ void dev_copy(void* dst, const void* src, size_t bytes, int kind, Ctx& c) {
 
 void dev_sync(Ctx& c) { HIPCHK(hipStreamSynchronize((hipStream_t)c.stream)); }
 
-void graph_begin(Ctx& c) { HIPCHK(hipStreamBeginCapture((hipStream_t)c.stream, hipStreamCaptureModeRelaxed)); }
+void graph_begin(Ctx& c, std::vector<std::shared_ptr<Buffer>>* keep) {
+  g_capture_keep = keep;
+  HIPCHK(hipStreamBeginCapture((hipStream_t)c.stream, hipStreamCaptureModeRelaxed));
+}
 
 void* graph_end(Ctx& c) {
+  g_capture_keep = nullptr;
   hipGraph_t g = nullptr;
   HIPCHK(hipStreamEndCapture((hipStream_t)c.stream, &g));
   hipGraphExec_t e = nullptr;

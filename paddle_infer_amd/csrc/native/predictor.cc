@@ -106,6 +106,7 @@ class PredictorImpl {
     }
     scope.clear();
     graph_scope.clear();
+    graph_keep.clear();
     if (ctx.gpu) {
       params.clear();
       pdn::fast_release(ctx);
@@ -129,6 +130,7 @@ class PredictorImpl {
   void* graph = nullptr;
   std::string graph_key;
   pdn::Scope graph_scope;
+  std::vector<std::shared_ptr<pdn::Buffer>> graph_keep;  // every buffer the captured kernels touch
 
   bool run() {
     for (auto& kv : params) scope[kv.first] = kv.second;
@@ -150,10 +152,16 @@ class PredictorImpl {
       pdn::graph_destroy(graph);
       graph = nullptr;
       graph_scope.clear();
+      graph_keep.clear();
       for (auto& kv : params) graph_scope[kv.first] = kv.second;
       for (auto& f : feeds) graph_scope[f] = tensor(f);
-      pdn::graph_begin(ctx);
-      run_ops(graph_scope);
+      pdn::graph_begin(ctx, &graph_keep);
+      try {
+        run_ops(graph_scope);
+      } catch (...) {
+        try { pdn::graph_destroy(pdn::graph_end(ctx)); } catch (...) {}
+        throw;
+      }
       graph = pdn::graph_end(ctx);
       graph_key = key;
     } else {

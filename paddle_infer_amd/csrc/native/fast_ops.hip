@@ -171,14 +171,14 @@ bool use_small(int M, int N, int K) {
   return M <= 512 && (int64_t)N * K <= 2048LL * 2048;
 }
 
-int pick_ksplit(int M, int N, int K) {
+int pick_ksplit(int M, int N, int K) {  // ops/gemm.py pick_ksplit
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
   const int nk = K / 64;
   if (tiles >= 512 || nk < 16) return 1;
   int best = 1;
   double best_t = -1;
-  for (int ks : {1, 2, 4, 8}) {
-    if (nk / ks < 8 || nk % ks) break;
+  for (int ks = 1; ks <= std::min(256, nk / 8); ++ks) {
+    if (nk % ks) continue;
     const int waves = (tiles * ks + 255) / 256;
     const double t = (double)waves / ks;
     if (best_t < 0 || t < best_t - 1e-9) best = ks, best_t = t;

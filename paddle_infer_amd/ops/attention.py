@@ -21,7 +21,7 @@ from ..framework import random as _random
 
 
 NATIVE_D = (64, 96, 128)  # forward + backward kernels
-WIDE_D = 256  # forward kernel; the backward runs query-chunked on library GEMMs (_bwd_chunked)
+WIDE_D = 256  # forward kernel; the backward runs on the own batched GEMMs (_bwd_wide_own)
 
 
 def _padded_d(D: int, wide: bool = False) -> int | None:
@@ -138,42 +138,94 @@ class _FlashAttnPackedFn(torch.autograd.Function):
         return dqkv, None, None, None, None, None, None, None
 
 
-def _bwd_chunked(q, k, v, o, lse, do, causal, scale, mask, chunk_bytes=1 << 30):
-    """Attention backward for head dims without a backward kernel (D = 256), from the forward's
-    O and log-sum-exp: per query chunk P = exp(S − lse), dV += Pᵀ·dO, dS = P∘(dO·Vᵀ − δ),
-    dQ = dS·K·scale, dK += dSᵀ·Q·scale (f32; memory O(chunk · Sk), not O(Sq · Sk))."""
+def _ceil_to(x, m, lo=0):
+    return max(lo, -(-x // m) * m)
+
+
+def _bwd_wide_own(q, k, v, o, lse, do, causal, scale, mask, chunk_bytes=1 << 30):
+    """Backward of the wide-head (D > 128) forward on the framework's own kernels: per
+    (batch · head) and query chunk, five batched assembly GEMMs (csrc/asm/gemm_gen.py) —
+    S = Q·Kᵀ and dP = dO·Vᵀ into f32, dV += Pᵀ·dO and dK += dSᵀ·Q accumulated in f32, dQ = dS·K —
+    with P = exp(S − lse) and dS = P∘(dP − δ) in f32 between them (P and dS rounded to the
+    operands' dtype for the GEMMs, as the fused kernels do). Rows / keys / head dim are
+    zero-padded to the GEMM's 64-multiples; padded keys are masked, padded queries carry lse = +inf
+    (P = 0). Memory O(chunk · Sk)."""
+    from .gemm import asm_gemm as _asm
     B, Sq, Hq, D = q.shape
     Sk, Hk = k.shape[1], k.shape[2]
     rep = Hq // Hk
-    ct = torch.promote_types(q.dtype, torch.float32)
-    qf, of, dof = (t.to(ct).transpose(1, 2) for t in (q, o, do))
-    kf = k.to(ct).transpose(1, 2).repeat_interleave(rep, dim=1)
-    vf = v.to(ct).transpose(1, 2).repeat_interleave(rep, dim=1)
-    lse = lse.to(ct)
-    delta = (dof * of).sum(-1, keepdim=True)
-    dq = torch.empty_like(qf)
-    dk = torch.zeros_like(kf)
-    dv = torch.zeros_like(vf)
-    ch = max(1, min(Sq, chunk_bytes // max(1, B * Hq * Sk * 4 * 3)))
-    for q0 in range(0, Sq, ch):
-        q1 = min(Sq, q0 + ch)
-        s = torch.matmul(qf[:, :, q0:q1], kf.transpose(-1, -2)) * scale
-        if mask is not None:
-            s = s + (mask[..., :, :Sk] if mask.shape[-2] == 1 else mask[..., q0:q1, :Sk]).to(ct)
+    dt, dev = q.dtype, q.device
+
+    def asm_gemm(a, b, trans_a=False, trans_b=False, out=None, out_f32=False, accumulate=False):
+        if a.is_cuda:
+            return _asm(a, b, trans_a, trans_b, out=out, out_f32=out_f32, accumulate=accumulate)
+        # CPU: the same contract in PyTorch (the numerics reference of the CPU tier)
+        r = torch.matmul(a.transpose(-1, -2) if trans_a else a, b.transpose(-1, -2) if trans_b else b)
+        if out is not None:
+            if accumulate:
+                out += r.to(out.dtype)
+            else:
+                out.copy_(r)
+            return out
+        return r.to(torch.float32 if out_f32 else a.dtype)
+
+    Dp, Sqp, Skp = _ceil_to(D, 64, 128), _ceil_to(Sq, 64, 128), _ceil_to(Sk, 64, 128)
+    BH = B * Hq
+
+    def heads(t, S, Sp, H):
+        x = t.transpose(1, 2)
+        if H != Hq:
+            x = x.repeat_interleave(rep, dim=1)
+        out = torch.zeros((B, Hq, Sp, Dp), dtype=dt, device=dev)
+        out[:, :, :S, :D] = x
+        return out.view(BH, Sp, Dp)
+
+    qh, doh = heads(q, Sq, Sqp, Hq), heads(do, Sq, Sqp, Hq)
+    kh, vh = heads(k, Sk, Skp, Hk), heads(v, Sk, Skp, Hk)
+    st = torch.float32 if dt in (torch.bfloat16, torch.float16) else dt  # statistics dtype
+    delta = torch.zeros((BH, Sqp), dtype=st, device=dev)
+    delta[:, :Sq] = (do.to(st) * o.to(st)).sum(-1).transpose(1, 2).reshape(BH, Sq)
+    lse_p = torch.full((BH, Sqp), float("inf"), dtype=st, device=dev)
+    lse_p[:, :Sq] = lse.to(st).reshape(BH, Sq)
+    mk = None
+    if mask is not None:
+        mk = torch.zeros((B, mask.shape[1], mask.shape[2] if mask.shape[2] == 1 else Sqp, Skp),
+                         dtype=st, device=dev)
+        mk[..., :mask.shape[2], :Sk] = mask[..., :Sk].to(st)
+    dq = torch.empty((BH, Sqp, Dp), dtype=dt, device=dev)
+    acc_t = torch.float32 if dt in (torch.bfloat16, torch.float16) else dt
+    dk = torch.zeros((BH, Skp, Dp), dtype=acc_t, device=dev)
+    dv = torch.zeros((BH, Skp, Dp), dtype=acc_t, device=dev)
+    kj = torch.arange(Skp, device=dev)
+    ch = max(128, min(Sqp, (chunk_bytes // max(1, BH * Skp * 4 * 3)) // 64 * 64))
+    q0 = 0
+    while q0 < Sqp:
+        q1 = Sqp if Sqp - q0 < ch + 128 else q0 + ch  # no tail chunk shorter than 128 rows
+        qs, dos = qh[:, q0:q1], doh[:, q0:q1]
+        s = asm_gemm(qs, kh, trans_b=True, out_f32=True).mul_(scale)
+        s = s.view(B, Hq, q1 - q0, Skp)
+        if mk is not None:
+            s += mk if mk.shape[2] == 1 else mk[:, :, q0:q1]
+        bad = kj >= Sk
         if causal:
-            i = torch.arange(q0, q1, device=q.device)[:, None]
-            j = torch.arange(Sk, device=q.device)[None, :]
-            s = s.masked_fill(j > i + (Sk - Sq), float("-inf"))
-        pm = torch.exp(s - lse[:, :, q0:q1, None])
-        dv += torch.matmul(pm.transpose(-1, -2), dof[:, :, q0:q1])
-        ds = pm * (torch.matmul(dof[:, :, q0:q1], vf.transpose(-1, -2)) - delta[:, :, q0:q1])
-        dq[:, :, q0:q1] = torch.matmul(ds, kf) * scale
-        dk += torch.matmul(ds.transpose(-1, -2), qf[:, :, q0:q1]) * scale
+            qi = torch.arange(q0, q1, device=dev)[:, None]
+            bad = bad | (kj[None, :] > qi + (Sk - Sq))
+        s = s.masked_fill(bad, float("-inf")).view(BH, q1 - q0, Skp)
+        p = torch.exp(s - lse_p[:, q0:q1, None])
+        pb = p.to(dt)
+        asm_gemm(pb, dos, trans_a=True, out=dv, accumulate=True)
+        dp = asm_gemm(dos, vh, trans_b=True, out_f32=True)
+        dsb = (p * (dp - delta[:, q0:q1, None])).mul_(scale).to(dt)
+        dq[:, q0:q1] = asm_gemm(dsb, kh)
+        asm_gemm(dsb, qs, trans_a=True, out=dk, accumulate=True)
+        q0 = q1
+    dq = dq.view(B, Hq, Sqp, Dp)[:, :, :Sq, :D].transpose(1, 2)
+    dk = dk.view(B, Hq, Skp, Dp)[:, :, :Sk, :D]
+    dv = dv.view(B, Hq, Skp, Dp)[:, :, :Sk, :D]
     if rep > 1:
-        dk = dk.view(B, Hk, rep, Sk, D).sum(2)
-        dv = dv.view(B, Hk, rep, Sk, D).sum(2)
-    back = lambda t, ref: t.transpose(1, 2).to(ref.dtype)
-    return back(dq, q), back(dk, k), back(dv, v)
+        dk = dk.reshape(B, Hk, rep, Sk, D).sum(2)
+        dv = dv.reshape(B, Hk, rep, Sk, D).sum(2)
+    return dq.contiguous(), dk.transpose(1, 2).to(dt).contiguous(), dv.transpose(1, 2).to(dt).contiguous()
 
 
 class _FlashAttnFn(torch.autograd.Function):
@@ -189,9 +241,8 @@ class _FlashAttnFn(torch.autograd.Function):
     def backward(ctx, do):
         q, k, v, o, lse, mask = ctx.saved_tensors
         causal, scale, p, seed, off = ctx.meta
-        if q.shape[-1] > NATIVE_D[-1]:
-            _lib.fallback("flash_attention_bwd", f"head dim {q.shape[-1]}: query-chunked library GEMMs")
-            dq, dk, dv = _bwd_chunked(q, k, v, o, lse, do, causal, scale, mask)
+        if q.shape[-1] > NATIVE_D[-1]:  # wide heads: the backward on the own batched GEMMs
+            dq, dk, dv = _bwd_wide_own(q, k, v, o, lse, do.contiguous(), causal, scale, mask)
             return dq, dk, dv, None, None, None, None, None, None
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         _bwd(q, k, v, o, lse, do, dq, dk, dv, causal, scale, mask, p, seed, off)

@@ -409,10 +409,15 @@ class _ConvDirect(torch.autograd.Function):
 
 
 def _tall_wgrad(dy2, x2):
-    """dyᵀ·x [K, C] (f32) of a 1×1 conv over M ≫ K, C pixel rows. One library GEMM with a K×C
-    output has only a handful of output tiles (hipBLASLt picked 10-19 workgroups and took ~1 ms at
-    MobileNetV2's 112×112 layers, profiles/conv_nets_r3.txt); split the pixel rows into S chunks
-    as ONE batched GEMM with f32 outputs and sum the S partial planes in a fixed order."""
+    """dyᵀ·x [K, C] (f32) of a 1×1 conv over M ≫ K, C pixel rows: the own assembly GEMM (split-K
+    over the pixel rows into f32 planes, reduced in a fixed order — `ops.linear.wgrad_into`). A
+    library GEMM with a K×C output had only a handful of output tiles (hipBLASLt: 10-19
+    workgroups, ~1 ms at MobileNetV2's 112×112 layers, profiles/conv_nets_r3.txt)."""
+    from .gemm import own_dtype
+    if own_dtype(dy2, x2):
+        from .linear import wgrad_into
+        out = torch.zeros((dy2.shape[1], x2.shape[1]), dtype=torch.float32, device=dy2.device)
+        return wgrad_into(out, dy2.contiguous(), x2.contiguous())
     M, K = dy2.shape
     C = x2.shape[1]
     S = 1
@@ -430,8 +435,8 @@ def _tall_wgrad(dy2, x2):
 
 
 class _Conv1x1(torch.autograd.Function):
-    """Dense 1×1 conv with channels off the 64-grid as a GEMM over pixel rows (ops.linear.mm_nt:
-    the framework's assembly GEMM where its contract holds, hipBLASLt otherwise)."""
+    """Dense 1×1 conv with channels off the 64-grid as a GEMM over pixel rows on the framework's
+    GEMMs (forward ops.linear.mm_nt, data gradient ops.gemm.matmul, weight gradient wgrad_into)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, st):
@@ -455,7 +460,8 @@ class _Conv1x1(torch.autograd.Function):
         dy2 = dy.to(x2.dtype).reshape(-1, K)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx2 = torch.mm(dy2, w_kc)
+            from .gemm import matmul as _mm
+            dx2 = _mm(dy2, w_kc)
             if st != (1, 1):
                 dx = torch.zeros(xshape, dtype=x2.dtype, device=x2.device)
                 dx[:, ::st[0], ::st[1]] = dx2.view(dy.shape[:3] + (C,))

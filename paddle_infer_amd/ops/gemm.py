@@ -117,17 +117,19 @@ def asm_gemm(a, b, trans_a=False, trans_b=False, out=None, out_f32=False, accumu
 
 
 def pick_ksplit(M, N, K):
-    """Split-K degree for the pipelined kernel: fill the 256 CUs (one 256x256 tile per CU) when
-    the tile grid is small and K is long (weight gradients: 2048 x 2048 tiles over 65k tokens)."""
+    """Split-K degree for the assembly GEMM: fill the 256 CUs (one 256x256 tile per CU) when the
+    tile grid is small and K is long (weight gradients: 2048 x 2048 tiles over 98k tokens; the
+    tall-skinny 1x1-conv weight gradients: one or two tiles over a million pixel rows). Any
+    divisor of the 64-block count up to 256 that leaves >= 8 blocks per split; the fewest waves per
+    split wins, ties to the smaller split (less f32 plane traffic)."""
     tiles = ((M + 255) // 256) * ((N + 255) // 256)
     nk = K // 64
     if tiles >= 2 * NUM_CUS or nk < 16:
         return 1
-    # ≥ 8 k64 blocks per split (measured: M=256 N=6144 K=2048 is fastest at 4 splits of 8)
     best, best_t = 1, None
-    for ks in (1, 2, 4, 8):
-        if nk // ks < 8 or nk % ks:
-            break
+    for ks in range(1, min(256, nk // 8) + 1):
+        if nk % ks:
+            continue
         waves = -(-tiles * ks // NUM_CUS)
         t = waves / ks
         if best_t is None or t < best_t - 1e-9:

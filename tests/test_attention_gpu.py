@@ -174,7 +174,8 @@ def test_varlen_masked_single_launch_matches_reference():
 @pytest.mark.parametrize("D,causal,masked", [(256, True, False), (256, False, True), (192, True, False)])
 def test_flash_wide_head_dims(dtype, D, causal, masked):
     """Head dims 129..256: the wide forward kernel (D = 256, narrower heads zero-padded) and the
-    query-chunked backward from its log-sum-exp."""
+    backward from its log-sum-exp on the own batched assembly GEMMs — no op leaves the HIP path
+    (the autouse fixture)."""
     from paddle_infer_amd.ops import _lib, flash_attention
     torch.manual_seed(1)
     B, Sq, Sk, Hq, Hk = 2, 150, 150, 4, 2
@@ -186,5 +187,3 @@ def test_flash_wide_head_dims(dtype, D, causal, masked):
     o, do, *g = _run(q, k, v, lambda a, b, c: flash_attention(a, b, c, causal, sc, attn_mask=mask),
                      dtype, D)
     _check(o, do, g, q, k, v, lambda a, b, c: _ref(a, b, c, causal, sc, mask), dtype)
-    assert {op for op, _ in _lib.FALLBACKS} <= {"flash_attention_bwd"}, _lib.FALLBACKS  # fwd on the kernel
-    _lib.FALLBACKS.clear()

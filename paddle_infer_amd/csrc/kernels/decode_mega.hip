@@ -18,9 +18,10 @@
 //   * cross-workgroup data (residual, q / new k,v, attention partials, FFN hidden) is published
 //     with agent-scope relaxed atomic stores and read with agent-scope atomic loads (coherent
 //     across the 8 per-XCD L2s without L2 write-back fences, see xcd_* in common.h); the barrier
-//     is a monotonically increasing arrival counter (zeroed by the launcher) polled by one lane
-//     with s_sleep back-off and a bounded spin: on timeout the kernel raises `err` and runs to
-//     completion, so every wave always exits.
+//     is a monotonically increasing arrival counter polled by one lane with s_sleep back-off. The
+//     grid is launched COOPERATIVELY (hipLaunchCooperativeKernel after an occupancy check), so all
+//     256 workgroups are co-resident by the runtime's guarantee; the spin stays bounded as a
+//     safety net (a timeout raises `err` and runs the launch to completion, every wave exits).
 //   * per layer: LN1 (recomputed per WG from the residual, 8 KB from L2) + QKV GEMV + bias, new
 //     k/v written to the cache → split-K attention over the cache (16 lanes per key row, base-2
 //     softmax) → partial combine + out GEMV + bias + residual → LN2 + FFN1 GEMV + bias + GELU →
@@ -465,6 +466,18 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
 
 }  // namespace
 
+// 1 when this device can run the single-launch step: cooperative launches supported and the
+// kernel's occupancy puts all NWG workgroups on the chip at once.
+PIAMD_EXPORT int piamd_decode_mega_supported() {
+  int dev = 0, attr = 0, per_cu = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&attr, hipDeviceAttributeCooperativeLaunch, dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, decode_mega_kernel, NT, 0) != hipSuccess)
+    return 0;
+  return attr && per_cu * cus >= NWG ? 1 : 0;
+}
+
 // Launch one decode step over `nl` layers (see the header comment for the supported shapes).
 // `layers` is a device array of MegaLayer; scratch buffers per MegaArgs. Returns hipError_t.
 PIAMD_EXPORT int piamd_decode_mega(const MegaArgs* args, int E_, int D_, int hq, int hk, int F_,
@@ -481,6 +494,18 @@ PIAMD_EXPORT int piamd_decode_mega(const MegaArgs* args, int E_, int D_, int hq,
       a.nsplit < 1 || HQ * a.nsplit > NWG || (a.maxS + a.nsplit - 1) / a.nsplit > 256 || !a.layers ||
       !a.resid || !a.rbuf || !a.qn || !a.kvn || !a.part || !a.h || !a.bar || !a.err || !a.pos)
     return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(decode_mega_kernel, dim3(NWG), dim3(NT), 0, st, a);
-  return (int)hipGetLastError();
+  // cooperative launch: the runtime guarantees all NWG workgroups are co-resident (the grid
+  // barriers rely on it) or refuses the launch; checked once against the kernel's occupancy
+  static int coop = -1;
+  if (coop < 0) {
+    int dev = 0, attr = 0, per_cu = 0;
+    coop = hipGetDevice(&dev) == hipSuccess &&
+           hipDeviceGetAttribute(&attr, hipDeviceAttributeCooperativeLaunch, dev) == hipSuccess && attr &&
+           hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, decode_mega_kernel, NT, 0) == hipSuccess &&
+           per_cu * cus >= NWG;
+  }
+  if (!coop) return (int)hipErrorCooperativeLaunchTooLarge;
+  MegaArgs arg = a;
+  void* kargs[] = {&arg};
+  return (int)hipLaunchCooperativeKernel((const void*)decode_mega_kernel, dim3(NWG), dim3(NT), kargs, 0, st);
 }

@@ -22,8 +22,9 @@ import torch
 from ..ops import _lib
 
 E, D, HQ, HK, F = 2048, 128, 16, 16, 8192
-# default for PIAMD_DECODE_MEGA (1 = batch-1 decode steps run the single-launch kernel)
-DEFAULT = "0"
+# default for PIAMD_DECODE_MEGA (1 = batch-1 decode steps run the single-launch kernel, launched
+# cooperatively; 0 = the per-op path)
+DEFAULT = "1"
 
 
 def enabled() -> bool:
@@ -51,7 +52,8 @@ def eligible(gen, B: int) -> bool:
             t = spec.get(key)
             if t is None or t.dtype != torch.bfloat16:
                 return False
-    return _lib.available() and _lib.has("piamd_decode_mega")
+    return (_lib.available() and _lib.has("piamd_decode_mega")
+            and _lib.lib().piamd_decode_mega_supported() == 1)  # cooperative launch possible
 
 
 def _out_in(lin):

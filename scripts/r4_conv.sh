@@ -16,3 +16,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_ou
 cd $GRAFT_REPO_ROOT
 python tools/prof_summary.py gpurun_out/r4_cn_prof_mbv2 > gpurun_out/r4_cn_prof_mbv2.txt 2>&1
 head -24 gpurun_out/r4_cn_prof_mbv2.txt
+timeout -k 10 300 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_decode_mega_gpu.py tests/test_infer_kernels_gpu.py > gpurun_out/r4_mega_tests.log 2>&1 || { tail -30 gpurun_out/r4_mega_tests.log; exit 1; }
+tail -2 gpurun_out/r4_mega_tests.log
+timeout -k 10 300 python -u tools/bench_generate.py --batch 1 --prompt 128 --gen 128 --modes graph > gpurun_out/r4_gen_b1.log 2>&1 || { tail -20 gpurun_out/r4_gen_b1.log; exit 1; }
+grep '^{' gpurun_out/r4_gen_b1.log

@@ -9,7 +9,7 @@ int fa_fwd_f16(const FaArgs& a, hipStream_t st);
 int fa_bwd_f16(const FaArgs& a, hipStream_t st);
 
 // Head dims: 64 / 96 / 128 both ways; 256 (the wide forward) forward only — the backward of wider
-// heads is the query-chunked composition in ops/attention.py over the forward's log-sum-exp.
+// heads is ops/attention.py `_bwd_wide_own` (batched own-GEMM products over the forward's lse).
 static int fa_check(const FaArgs& a, bool fwd) {
   if (a.Hk <= 0 || a.Hq % a.Hk || (a.cu_q && !a.cu_k)) return (int)hipErrorInvalidValue;
   if (a.D != 64 && a.D != 96 && a.D != 128 && !(fwd && a.D == 256)) return (int)hipErrorInvalidValue;
@@ -38,7 +38,10 @@ PIAMD_EXPORT int piamd_fa_bwd(const FaArgs* args, int f16, hipStream_t stream) {
   FaArgs a = *args;
   if (int e = fa_check(a, false)) return e;
   a.map = fa::fa_bwd_map(a);
-  if (a.cu_q) a.sqb = a.skb = a.svb = a.sob = 0;
+  if (a.cu_q) {
+    a.sqb = a.skb = a.svb = a.sob = 0;
+    a.ds = nullptr;  // stored dS: padded layout only
+  }
   if (a.B == 0 || a.Sq == 0 || a.Sk == 0) return 0;
   return f16 ? fa_bwd_f16(a, stream) : fa::launch_bwd<false>(a, stream);
 }

@@ -332,7 +332,7 @@ template <int WM, int MB, int NB, bool SC = false, bool F16 = false>
 __global__ __launch_bounds__(NTHR, 1) void conv_fwd_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ wt, const bf16_t* __restrict__ zero,
     bf16_t* __restrict__ y, float* __restrict__ ws, int ksplit, ConvGeom g, int Kout, int act,
-    const bf16_t* __restrict__ bias) {
+    const bf16_t* __restrict__ bias, int yf32) {
   constexpr int WC = NWAVE / WM, TN = WC * NB * 32;
   constexpr int B_BYTES = TN * BK * 2, SBYTES = TILE_BYTES + B_BYTES;
   __shared__ __attribute__((aligned(1024))) char smem[2 * SBYTES];
@@ -436,6 +436,9 @@ __global__ __launch_bounds__(NTHR, 1) void conv_fwd_kernel(
   if (ksplit > 1)
     gemm_epilogue<WM, MB, NB>(acc, ws + (long long)part * M * Kout, Kout, 1, 0, m0, M, n0, Kout,
                               EPI_STORE, 0, nullptr, nullptr, 0);
+  else if (yf32)  // f32 output (the split-bf16 fp32 convolution): plain store, no epilogue ops
+    gemm_epilogue<WM, MB, NB>(acc, (float*)y, Kout, 1, 0, m0, M, n0, Kout, EPI_STORE, 0, nullptr,
+                              nullptr, 0);
   else
     gemm_epilogue<WM, MB, NB, F16>(acc, y, Kout, 0, 0, m0, M, n0, Kout,
                               (bias || act) ? EPI_BIAS_ACT : EPI_STORE, act, bias, nullptr, 0);
@@ -770,16 +773,28 @@ PIAMD_EXPORT int piamd_gemm_i8(const void* x, long long ldx, const void* wq, lon
   return (int)hipGetLastError();
 }
 
+// f32 y[m][n] = Σ_p ws[p][m][n] in plane order (f32-output split-K finish).
+__global__ __launch_bounds__(256) void conv_splitk_finish_f32(const float* __restrict__ ws, int ksplit,
+                                                              long long MN, float* __restrict__ y) {
+  const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= MN) return;
+  f32x4 v = *reinterpret_cast<const f32x4*>(ws + i);
+  for (int p = 1; p < ksplit; ++p) v += *reinterpret_cast<const f32x4*>(ws + p * MN + i);
+  *reinterpret_cast<f32x4*>(y + i) = v;
+}
+
 // NHWC implicit-GEMM convolution forward: x [N][H][W][C], wt [Kout][R][S][C] (OHWI), y
 // [N][OH][OW][Kout], 16-bit (bf16, or IEEE fp16 when f16 != 0: same tiles on the f16 MFMA);
 // zero: ≥ 128 zero bytes (out-of-image taps); bias [Kout] (nullable, element type of x);
 // act: epi 0 store / 1 bias+act (aux = pre-activation) / 2 dact. C % 64 == 0 (or C == 8: stem mode), Kout % 4 == 0.
+// flags bit 0: fp16 (else bf16); bit 1: y is f32 (plain sum, bias and act must be off) — the
+// split-bf16 fp32 convolution of ops/conv.py runs its three products through this.
 template <bool F16>
 static void conv_fwd_launch(int tile_n, bool sc, unsigned grid, hipStream_t st, const bf16_t* xb,
                             const bf16_t* wb, const bf16_t* zb, bf16_t* y, float* wsf, int ksplit,
-                            const ConvGeom& g, int Kout, int act, const bf16_t* bb) {
+                            const ConvGeom& g, int Kout, int act, const bf16_t* bb, int yf32) {
 #define CONV_FWD(WM, MB, NB, SCV) \
-  hipLaunchKernelGGL((conv_fwd_kernel<WM, MB, NB, SCV, F16>), dim3(grid), dim3(NTHR), 0, st, xb, wb, zb, y, wsf, ksplit, g, Kout, act, bb)
+  hipLaunchKernelGGL((conv_fwd_kernel<WM, MB, NB, SCV, F16>), dim3(grid), dim3(NTHR), 0, st, xb, wb, zb, y, wsf, ksplit, g, Kout, act, bb, yf32)
   if (tile_n == 64) {
     if (sc) CONV_FWD(8, 1, 2, true); else CONV_FWD(8, 1, 2, false);
   } else if (tile_n == 128) {
@@ -794,8 +809,10 @@ PIAMD_EXPORT int piamd_conv2d_fwd(const void* x, const void* wt, const void* zer
                                   int H, int W, int C, int OH, int OW, int R, int S, int st_h,
                                   int st_w, int pad_h, int pad_w, int dil_h, int dil_w, int Kout,
                                   int act, const void* bias, int tile_n, int ksplit, void* ws,
-                                  int f16, hipStream_t st) {
+                                  int flags, hipStream_t st) {
   const bool sc = C == 8;
+  const int f16 = flags & 1, yf32 = (flags >> 1) & 1;
+  if (yf32 && (bias || act)) return (int)hipErrorInvalidValue;
   if ((C % BK && !sc) || Kout % 4 || N < 1 || OH < 1 || OW < 1 || R < 1 || S < 1 || !zero || ksplit < 1 ||
       (ksplit > 1 && !ws) || ksplit > (sc ? (R * S + 7) / 8 : R * S * (C / BK)) ||
       (tile_n != 64 && tile_n != 128 && tile_n != 256))
@@ -810,12 +827,14 @@ PIAMD_EXPORT int piamd_conv2d_fwd(const void* x, const void* wt, const void* zer
   const auto zb = (const bf16_t*)zero;
   const auto bb = (const bf16_t*)bias;
   float* wsf = (float*)ws;
-  if (f16) conv_fwd_launch<true>(tile_n, sc, grid, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb);
-  else conv_fwd_launch<false>(tile_n, sc, grid, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb);
+  if (f16) conv_fwd_launch<true>(tile_n, sc, grid, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb, yf32);
+  else conv_fwd_launch<false>(tile_n, sc, grid, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb, yf32);
   if (ksplit > 1) {
     const long long MN = M * Kout;
     const dim3 fg((unsigned)((MN / 4 + 255) / 256));
-    if (f16) hipLaunchKernelGGL(conv_splitk_finish<true>, fg, dim3(256), 0, st, wsf, ksplit, MN, Kout, act, bb, (bf16_t*)y);
+    if (yf32)
+      hipLaunchKernelGGL(conv_splitk_finish_f32, fg, dim3(256), 0, st, wsf, ksplit, MN, (float*)y);
+    else if (f16) hipLaunchKernelGGL(conv_splitk_finish<true>, fg, dim3(256), 0, st, wsf, ksplit, MN, Kout, act, bb, (bf16_t*)y);
     else hipLaunchKernelGGL(conv_splitk_finish<false>, fg, dim3(256), 0, st, wsf, ksplit, MN, Kout, act, bb, (bf16_t*)y);
   }
   return (int)hipGetLastError();

@@ -84,7 +84,7 @@ class FaArgs(ctypes.Structure):
                 + [(n, c_ll) for n in ("sqb", "sqs", "sqh", "skb", "sks", "skh", "svb", "svs", "svh",
                                        "sob", "sos", "soh", "smb", "smh", "smq")]
                 + [("scale", ctypes.c_float), ("p_drop", ctypes.c_float), ("seed", c_u64),
-                   ("offset", c_u64), ("map", c_int)])
+                   ("offset", c_u64), ("map", c_int), ("ds", c_void_p)])
 
 
 class MegaArgs(ctypes.Structure):

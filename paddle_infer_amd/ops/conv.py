@@ -1,5 +1,5 @@
-"""NHWC convolution on the framework's own kernels — every 2-D conv of a bf16/fp16 (or autocast)
-model, and every grouped/depthwise conv in any float dtype, runs without the library (MIOpen).
+"""NHWC convolution on the framework's own kernels — every 2-D conv of a bf16/fp16/fp32 (or
+autocast) model, dense, grouped or depthwise, runs without the library (MIOpen).
 
 Parity: reference `phi/kernels/gpudnn/conv_kernel.cu` + `conv_grad_kernel.cu` (cuDNN forward /
 backward-data / backward-filter), `phi/kernels/gpu/depthwise_conv_kernel.cu` (depthwise) and the
@@ -19,7 +19,8 @@ Routes (``conv2d_any``, called by ``nn.functional.conv2d`` for GPU tensors):
   (forward, transposed-geometry data gradient, deterministic split weight gradient);
 * NCHW inputs are used through their channels_last view when they have one; a plain NCHW tensor
   is re-laid-out once (the output is channels_last, so every later layer takes the view);
-* dense fp32 without autocast stays on the library (recorded by ``_lib.fallback``).
+* dense fp32 without autocast → the same MFMA implicit GEMM as three bf16 products accumulated in
+  f32 (``_Conv2dF32``: ≈2^-16 relative per product; ``FP32_SPLIT = False`` keeps the library).
 """
 from __future__ import annotations
 
@@ -96,9 +97,10 @@ def _plan(M, K, nk):
 PLAN_OVERRIDE = None  # (tile_n, ksplit) for tuning sweeps
 
 
-def _launch(x, w_ohwi, bias, st, pad, dil, act, rs=None):
+def _launch(x, w_ohwi, bias, st, pad, dil, act, rs=None, out_f32=False):
     """x [N,H,W,C] bf16 contiguous, w_ohwi [K,R,S,C] bf16 contiguous → y [N,OH,OW,K]. ``rs``:
-    the true filter size in stem mode (C == 8, w_ohwi = [K][ceil(R·S/8)·64] packed taps)."""
+    the true filter size in stem mode (C == 8, w_ohwi = [K][ceil(R·S/8)·64] packed taps).
+    ``out_f32``: y in f32 (no bias / activation)."""
     N, H, W, C = x.shape
     K = w_ohwi.shape[0]
     R, S = rs if rs is not None else w_ohwi.shape[1:3]
@@ -107,16 +109,19 @@ def _launch(x, w_ohwi, bias, st, pad, dil, act, rs=None):
         raise ValueError("convolution output is empty")
     M = N * OH * OW
     nk = -(-(R * S) // 8) if rs is not None else R * S * (C // 64)
-    y = torch.empty(N, OH, OW, K, dtype=x.dtype, device=x.device)
+    y = torch.empty(N, OH, OW, K, dtype=torch.float32 if out_f32 else x.dtype, device=x.device)
     b = bias.to(x.dtype).contiguous() if bias is not None else None
+    assert not (out_f32 and (b is not None or act))
+    flags = _f16(x) | (2 if out_f32 else 0)
 
     def run(plan):
         tn, ks = plan
         ws = torch.empty(ks * M * K, dtype=torch.float32, device=x.device) if ks > 1 else None
         _lib.call("piamd_conv2d_fwd", x.data_ptr(), w_ohwi.data_ptr(), _zero(x.device).data_ptr(),
                   y.data_ptr(), N, H, W, C, OH, OW, R, S, st[0], st[1], pad[0], pad[1], dil[0],
-                  dil[1], K, act, _lib.ptr(b), tn, ks, _lib.ptr(ws), _f16(x), _lib.stream())
-    plan = PLAN_OVERRIDE or _autotuned("conv2d_fwd", (N, H, W, C, K, R, S, st, pad, dil, act),
+                  dil[1], K, act, _lib.ptr(b), tn, ks, _lib.ptr(ws), flags, _lib.stream())
+    plan = PLAN_OVERRIDE or _autotuned("conv2d_fwd", (N, H, W, C, K, R, S, st, pad, dil, act)
+                                       + (("f32",) if out_f32 else ()),
                                        _plan(M, K, nk), _fwd_candidates(M, K, nk), run)
     run(plan)
     return y
@@ -209,13 +214,13 @@ def _take_ap(t, dim, idx):
     return out.flip(dim) if step < 0 else out
 
 
-def conv2d_dgrad_strided(dy, weight, H, W, st, pad, dil):
-    """dX [N,H,W,C] (dtype of dy) of a strided conv: one stride-1 HIP convolution per output phase
-    (ih mod st_h, iw mod st_w) over dY with the sub-filter of the taps that reach that phase,
+def conv2d_dgrad_strided(dy, weight, H, W, st, pad, dil, out_f32=False):
+    """dX [N,H,W,C] (dtype of dy, or f32) of a strided conv: one stride-1 HIP convolution per output
+    phase (ih mod st_h, iw mod st_w) over dY with the sub-filter of the taps that reach that phase,
     scattered into dX (phases with no tap are zero)."""
     N, OH, OW, K = dy.shape
     Kw, C, R, S = weight.shape
-    dx = torch.empty(N, H, W, C, dtype=dy.dtype, device=dy.device)
+    dx = torch.empty(N, H, W, C, dtype=torch.float32 if out_f32 else dy.dtype, device=dy.device)
     wb = weight.to(dy.dtype)
     for ph in range(st[0]):
         for pw in range(st[1]):
@@ -230,27 +235,28 @@ def conv2d_dgrad_strided(dy, weight, H, W, st, pad, dil):
             # sub-filter [C][R'][S'][K]: W[k][c][rt[i]][stp[j]] (taps are arithmetic progressions:
             # strided slices + flips, no index tensor — capturable in a hipGraph)
             wsub = _take_ap(_take_ap(wb, 2, rt), 3, stp).permute(1, 2, 3, 0).contiguous()
-            y = _launch_geom(dy, wsub, (1, 1), (ph2, pw2), (dh2, dw2), Hp, Wp)
+            y = _launch_geom(dy, wsub, (1, 1), (ph2, pw2), (dh2, dw2), Hp, Wp, out_f32)
             dx[:, ph::st[0], pw::st[1], :] = y
     return dx
 
 
-def _launch_geom(x, w_ohwi, st, pad, dil, OH, OW):
+def _launch_geom(x, w_ohwi, st, pad, dil, OH, OW, out_f32=False):
     """conv_fwd with an explicit output size (pads may be negative: taps outside are skipped)."""
     N, H, W, C = x.shape
     K, R, S, _ = w_ohwi.shape
     M = N * OH * OW
     nk = R * S * (C // 64)
-    y = torch.empty(N, OH, OW, K, dtype=x.dtype, device=x.device)
+    y = torch.empty(N, OH, OW, K, dtype=torch.float32 if out_f32 else x.dtype, device=x.device)
+    flags = _f16(x) | (2 if out_f32 else 0)
 
     def run(plan):
         tn, ks = plan
         ws = torch.empty(ks * M * K, dtype=torch.float32, device=x.device) if ks > 1 else None
         _lib.call("piamd_conv2d_fwd", x.data_ptr(), w_ohwi.data_ptr(), _zero(x.device).data_ptr(),
                   y.data_ptr(), N, H, W, C, OH, OW, R, S, st[0], st[1], pad[0], pad[1], dil[0],
-                  dil[1], K, 0, 0, tn, ks, _lib.ptr(ws), _f16(x), _lib.stream())
-    run(_autotuned("conv2d_dgrad", (N, H, W, C, K, R, S, st, pad, dil, OH, OW), _plan(M, K, nk),
-                   _fwd_candidates(M, K, nk), run))
+                  dil[1], K, 0, 0, tn, ks, _lib.ptr(ws), flags, _lib.stream())
+    run(_autotuned("conv2d_dgrad", (N, H, W, C, K, R, S, st, pad, dil, OH, OW)
+                   + (("f32",) if out_f32 else ()), _plan(M, K, nk), _fwd_candidates(M, K, nk), run))
     return y
 
 
@@ -324,6 +330,106 @@ class _Conv2dNHWC(torch.autograd.Function):
         if has_bias and ctx.needs_input_grad[2]:
             db = dy.float().sum((0, 1, 2)).to(wdt)
         return dx, dw, db, None, None, None, None
+
+
+# ------------------------------------------------------------------------- dense fp32 (split bf16)
+FP32_SPLIT = True  # dense fp32 convs on the split-bf16 MFMA path (False: the library, exact fp32)
+
+
+def _split2(t):
+    """t (f32) → (hi, lo) bf16 with t ≈ hi + lo to ≈2^-17 relative."""
+    hi = t.to(torch.bfloat16)
+    return hi, (t - hi.float()).to(torch.bfloat16)
+
+
+def _cat_c(parts, n):
+    """Concatenate NHWC (or OHWI) tensors along the last dim, each zero-padded to n."""
+    return torch.cat([_padc(p, n) for p in parts], -1).contiguous()
+
+
+def _stem_f32(x, w, st, pad, dil):
+    """Stem-mode (≤ 8 input channels) convolution with f32 output: x [N,H,W,Cs] bf16, w [K,Cs,R,S]."""
+    K, Cs, R, S = w.shape
+    nk = -(-(R * S) // 8)
+    w8 = torch.zeros(K, nk * 64, dtype=w.dtype, device=w.device)
+    w8[:, :R * S * 8].view(K, R, S, 8)[..., :Cs] = w.permute(0, 2, 3, 1)
+    return _launch(_padc(x, 8).contiguous(), w8.view(K, 1, nk * 8, 8), None, st, pad, dil, 0,
+                   rs=(R, S), out_f32=True)
+
+
+class _Conv2dF32(torch.autograd.Function):
+    """Dense fp32 conv on the bf16 MFMA implicit GEMM, as three bf16 products accumulated in f32 by
+    the MFMA itself: x·w ≈ x_hi·w_hi + x_lo·w_hi + x_hi·w_lo (x = x_hi + x_lo, both bf16). The
+    three products are ONE convolution over channel-concatenated operands ([x_hi, x_lo, x_hi] ·
+    [w_hi, w_hi, w_lo]) written in f32, so the error is ≈2^-16 relative per product (fp32 storage,
+    well inside TF32-class accuracy) at three bf16 MACs per fp32 MAC — a third of the bf16 rate, ~2.7×
+    the chip's fp32-MFMA peak. Data gradient: the same concatenation over dY and the flipped filter
+    (stride 1) or the per-phase sub-convolutions (strided); weight gradient: the implicit-GEMM
+    wgrad kernel over batch-stacked [x_hi; x_lo; x_hi] and [dy_hi; dy_hi; dy_lo].
+    x [N,H,W,C0] f32 contiguous, weight [K0,C0,R,S]."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, st, pad, dil):
+        K0, C0, R, S = weight.shape
+        K = -(-K0 // 4) * 4
+        wf = weight.float()
+        if K != K0:
+            wf = torch.nn.functional.pad(wf, (0, 0, 0, 0, 0, 0, 0, K - K0))
+        xh, xl = _split2(x)
+        wh, wl = _split2(wf)
+        if 2 * C0 <= 8:  # stem mode: [x_hi, x_lo]·[w_hi, w_hi] + x_hi·w_lo
+            y = _stem_f32(torch.cat([xh, xl], -1), torch.cat([wh, wh], 1), st, pad, dil)
+            y += _stem_f32(xh, wl, st, pad, dil)
+        else:
+            C = _pad64(C0)
+            whp, wlp = wh.permute(0, 2, 3, 1), wl.permute(0, 2, 3, 1)
+            y = _launch(_cat_c((xh, xl, xh), C), _cat_c((whp, whp, wlp), C), None, st, pad, dil, 0,
+                        out_f32=True)
+        if K != K0:
+            y = y[..., :K0].contiguous()
+        if bias is not None:
+            y += bias.float()
+        ctx.save_for_backward(xh, xl, wh[:K0], wl[:K0])
+        ctx.cfg = (st, pad, dil, bias is not None, weight.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xh, xl, wh, wl = ctx.saved_tensors
+        st, pad, dil, has_bias, wdt = ctx.cfg
+        dy = dy.float().contiguous()
+        K0, C0, R, S = wh.shape
+        N, H, W, _ = xh.shape
+        M = dy.shape[0] * dy.shape[1] * dy.shape[2]
+        dyh, dyl = _split2(dy)
+        Kp = _pad64(K0)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            C4 = -(-C0 // 4) * 4  # data-gradient output channels: 4 per epilogue lane
+            pw = (0, 0, 0, 0, 0, C4 - C0, 0, Kp - K0)
+            whp, wlp = torch.nn.functional.pad(wh, pw), torch.nn.functional.pad(wl, pw)
+            d3 = _cat_c((dyh, dyl, dyh), Kp)
+            if st == (1, 1) and dy.shape[1:3] == (H, W):
+                pad_t = (dil[0] * (R - 1) - pad[0], dil[1] * (S - 1) - pad[1])
+                fh, fl = (t.flip(2, 3).permute(1, 2, 3, 0) for t in (whp, wlp))
+                dx = _launch_geom(d3, _cat_c((fh, fh, fl), Kp), (1, 1), pad_t, dil, H, W, out_f32=True)
+            else:
+                dx = conv2d_dgrad_strided(d3, torch.cat([whp, whp, wlp], 0), H, W, st, pad, dil,
+                                          out_f32=True)
+            dx = dx[..., :C0]
+        if ctx.needs_input_grad[1]:
+            C8 = -(-C0 // 8) * 8
+            if wgrad_eligible(C8, Kp, 3 * M):
+                x3 = torch.cat([_padc(xh, C8), _padc(xl, C8), _padc(xh, C8)], 0).contiguous()
+                d3w = torch.cat([_padc(dyh, Kp), _padc(dyh, Kp), _padc(dyl, Kp)], 0).contiguous()
+                dw = conv2d_wgrad(x3, d3w, R, S, st, pad, dil)[:K0, :C0]
+            else:  # ≥ 2^24 stacked pixels: the direct kernel's exact f32 reduction
+                xf = xh.float() + xl.float()
+                dw = _direct_wgrad(xf.contiguous(), dy, R, S, st, pad, dil, C0, K0)
+            dw = dw.to(wdt)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = dy.sum((0, 1, 2)).to(wdt)
+        return dx, dw, db, None, None, None
 
 
 # ---------------------------------------------------------------- direct grouped / depthwise conv
@@ -476,7 +582,7 @@ class _Conv1x1(torch.autograd.Function):
 
 def conv2d_any(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, nhwc=False):
     """Own-kernel route for a 2-D conv of a GPU tensor (NCHW or NHWC by ``nhwc``); ``None`` when
-    the call stays on the library (fp32 dense conv without autocast, string padding)."""
+    the call stays on the library (string padding, or dense fp32 with ``FP32_SPLIT`` off)."""
     if not (HIP_CONV and x.is_cuda and x.dim() == 4 and weight.dim() == 4) or isinstance(padding, str):
         return None
     pad, st, dil = _pair(padding), _pair(stride), _pair(dilation)
@@ -493,8 +599,13 @@ def conv2d_any(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, 
         raise ValueError(f"conv2d: weight {tuple(weight.shape)} does not match {C} input channels "
                          f"in {groups} groups")
     if groups == 1 and dt == torch.float32:
-        _lib.fallback("conv2d", "dense fp32 conv without autocast (library)")
-        return None
+        if not FP32_SPLIT:
+            _lib.fallback("conv2d", "dense fp32 conv with FP32_SPLIT off (library)")
+            return None
+        with torch.autocast("cuda", enabled=False):
+            xf = (x if nhwc else x.permute(0, 2, 3, 1)).float().contiguous()
+            y = _Conv2dF32.apply(xf, weight, bias, st, pad, dil)
+        return y if nhwc else y.permute(0, 3, 1, 2)
     with torch.autocast("cuda", enabled=False):
         xh = (x if nhwc else x.permute(0, 2, 3, 1)).to(dt)
         xh = xh.contiguous()  # a view for NHWC / channels_last storage; one re-layout otherwise

@@ -1,0 +1,34 @@
+#!/bin/bash
+# Round-4 verification batch: stored-dS attention backward, wide-head own-GEMM backward, dense fp32
+# split conv + own 1x1 conv backward, conv-net throughput + MobileNetV2 trace, cooperative decode.
+set -o pipefail
+cd /root/repo
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+T="python -u -m pytest -x -q --timeout 240 --timeout-method thread"
+timeout -k 10 500 $T tests/test_attention_ds_gpu.py tests/test_attention_gpu.py tests/test_attention_varlen_gpu.py > gpurun_out/r4c_attn_tests.log 2>&1 || { tail -40 gpurun_out/r4c_attn_tests.log; exit 1; }
+tail -1 gpurun_out/r4c_attn_tests.log
+timeout -k 10 500 $T tests/test_conv_any_gpu.py tests/test_conv_gpu.py tests/test_conv_bwd_gpu.py > gpurun_out/r4c_conv_tests.log 2>&1 || { tail -40 gpurun_out/r4c_conv_tests.log; exit 1; }
+tail -1 gpurun_out/r4c_conv_tests.log
+S="96,1024,16,128;8,2048,16,128;4,4096,16,128;16,1024,32,64"
+for MB in 0 8192; do
+  echo "== PIAMD_FA_DS_MAX_MB=$MB"
+  PIAMD_FA_DS_MAX_MB=$MB timeout -k 10 300 python tools/bench_attn.py --no-sdpa --shapes "$S" > gpurun_out/r4c_attn_bench_$MB.log 2>&1 || { tail -20 gpurun_out/r4c_attn_bench_$MB.log; exit 1; }
+  grep "^{" gpurun_out/r4c_attn_bench_$MB.log | cut -c1-220
+done
+for M in resnet50 mobilenet_v2; do
+  timeout -k 10 300 python tools/bench_resnet.py --model $M --steps 10 > gpurun_out/r4c_cn_$M.log 2>&1 || { tail -20 gpurun_out/r4c_cn_$M.log; exit 1; }
+  grep "^{" gpurun_out/r4c_cn_$M.log | cut -c1-220
+done
+timeout -k 10 300 $T tests/test_decode_mega_gpu.py tests/test_infer_kernels_gpu.py > gpurun_out/r4c_mega_tests.log 2>&1 || { tail -30 gpurun_out/r4c_mega_tests.log; exit 1; }
+tail -1 gpurun_out/r4c_mega_tests.log
+timeout -k 10 300 python -u tools/bench_generate.py --batch 1 --prompt 128 --gen 128 --modes graph > gpurun_out/r4c_gen_b1.log 2>&1 || { tail -20 gpurun_out/r4c_gen_b1.log; exit 1; }
+grep '^{' gpurun_out/r4c_gen_b1.log | cut -c1-300
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/r4c_prof_mbv2 -o run -- python $GRAFT_REPO_ROOT/tools/bench_resnet.py --model mobilenet_v2 --steps 3 > $GRAFT_REPO_ROOT/gpurun_out/r4c_prof_mbv2.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/r4c_prof_attn -o run -- python $GRAFT_REPO_ROOT/tools/bench_attn.py --no-sdpa --shapes "96,1024,16,128" > $GRAFT_REPO_ROOT/gpurun_out/r4c_prof_attn.log 2>&1 || exit 1
+cd $GRAFT_REPO_ROOT
+python tools/prof_summary.py gpurun_out/r4c_prof_mbv2 > gpurun_out/r4c_prof_mbv2.txt 2>&1
+python tools/prof_summary.py gpurun_out/r4c_prof_attn > gpurun_out/r4c_prof_attn.txt 2>&1
+head -14 gpurun_out/r4c_prof_mbv2.txt
+head -10 gpurun_out/r4c_prof_attn.txt

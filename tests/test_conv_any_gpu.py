@@ -1,5 +1,6 @@
 """Every 2-D conv route of ``ops.conv.conv2d_any`` against a PyTorch fp32 reference of the same op:
-depthwise / grouped (direct NHWC kernels, f32 / bf16 / fp16), dense fp16 and channel counts off the
+depthwise / grouped (direct NHWC kernels, f32 / bf16 / fp16), dense fp32 (split-bf16 products on the
+MFMA kernel), dense fp16 and channel counts off the
 64-grid (MFMA implicit GEMM with zero-padded channels), 1×1 convs as GEMMs, plain NCHW inputs
 (re-laid-out once, channels_last output), conv1d; and a MobileNetV2 bf16 training step whose
 profile holds no library (MIOpen) convolution or batch-norm op."""
@@ -84,6 +85,24 @@ def test_grouped(dt, shape, groups):
 def test_dense_half(dt, shape):
     N, C, H, W, K, R, st, pad, dil = shape
     _check(dt, N, C, H, W, K, R, st, pad, dil, groups=1)
+
+
+@pytest.mark.parametrize("shape", [
+    (2, 64, 14, 14, 128, 3, 1, 1, 1),     # aligned
+    (2, 48, 13, 13, 40, 3, 2, 1, 1),      # unaligned channels, strided data gradient
+    (2, 3, 32, 32, 32, 7, 2, 3, 1),       # stem (two stem-mode products)
+    (2, 24, 14, 14, 144, 1, 1, 0, 1),     # 1x1
+    (1, 32, 11, 9, 36, 3, 1, 2, 2),       # dilation 2
+])
+def test_dense_fp32_split(shape):
+    """Dense fp32 convs (Paddle's default dtype) run on the MFMA kernels as three bf16 products
+    accumulated in f32 — no library fallback, fp32-class error against the exact reference."""
+    from paddle_infer_amd.ops import _lib
+    _lib.FALLBACKS.clear()
+    N, C, H, W, K, R, st, pad, dil = shape
+    _check(torch.float32, N, C, H, W, K, R, st, pad, dil, groups=1)
+    _check(torch.float32, N, C, H, W, K, R, st, pad, dil, groups=1, nchw=True, bias=False)
+    assert not _lib.FALLBACKS, _lib.FALLBACKS
 
 
 @pytest.mark.parametrize("st", [1, 2])

@@ -36,11 +36,12 @@ typedef int8_t PD_Bool;
 #endif
 
 typedef int32_t PD_PrecisionType;
-enum { PD_PRECISION_FLOAT32 = 0, PD_PRECISION_INT8, PD_PRECISION_HALF };
+enum { PD_PRECISION_FLOAT32 = 0, PD_PRECISION_INT8, PD_PRECISION_HALF, PD_PRECISION_BFLOAT16 };
 typedef int32_t PD_PlaceType;
 enum { PD_PLACE_UNK = -1, PD_PLACE_CPU, PD_PLACE_GPU, PD_PLACE_XPU };
 typedef int32_t PD_DataType;
-enum { PD_DATA_UNK = -1, PD_DATA_FLOAT32, PD_DATA_INT32, PD_DATA_INT64, PD_DATA_UINT8, PD_DATA_INT8 };
+enum { PD_DATA_UNK = -1, PD_DATA_FLOAT32, PD_DATA_INT32, PD_DATA_INT64, PD_DATA_UINT8, PD_DATA_INT8,
+       PD_DATA_FLOAT16, PD_DATA_BOOL, PD_DATA_BFLOAT16 };
 
 typedef struct PD_OneDimArrayInt32 { size_t size; int32_t* data; } PD_OneDimArrayInt32;
 typedef struct PD_OneDimArraySize { size_t size; size_t* data; } PD_OneDimArraySize;
@@ -198,6 +199,11 @@ PADDLE_CAPI_EXPORT void PD_TensorCopyToCpuInt64(__pd_keep PD_Tensor* pd_tensor, 
 PADDLE_CAPI_EXPORT void PD_TensorCopyToCpuInt32(__pd_keep PD_Tensor* pd_tensor, int32_t* data);
 PADDLE_CAPI_EXPORT void PD_TensorCopyToCpuUint8(__pd_keep PD_Tensor* pd_tensor, uint8_t* data);
 PADDLE_CAPI_EXPORT void PD_TensorCopyToCpuInt8(__pd_keep PD_Tensor* pd_tensor, int8_t* data);
+/* zero-copy input on the predictor's place (extension of the native engine): the predictor reads
+   and in-place ops write `data` directly; the caller keeps it alive */
+PADDLE_CAPI_EXPORT void PD_TensorShareExternalData(__pd_keep PD_Tensor* pd_tensor, void* data,
+                                                   size_t shape_size, int32_t* shape,
+                                                   PD_PlaceType place, PD_DataType data_type);
 PADDLE_CAPI_EXPORT __pd_give PD_OneDimArrayInt32* PD_TensorGetShape(__pd_keep PD_Tensor* pd_tensor);
 PADDLE_CAPI_EXPORT void PD_TensorSetLod(__pd_keep PD_Tensor* pd_tensor, __pd_keep PD_TwoDimArraySize* lod);
 PADDLE_CAPI_EXPORT __pd_give PD_TwoDimArraySize* PD_TensorGetLod(__pd_keep PD_Tensor* pd_tensor);

@@ -83,6 +83,7 @@ struct Buffer {
   void* p = nullptr;
   size_t bytes = 0;
   bool dev = false;
+  bool owned = true;  // false: caller memory shared with Tensor::ShareExternalData (never freed here)
   ~Buffer();
 };
 std::shared_ptr<Buffer> alloc_buffer(size_t bytes, bool dev);
@@ -115,6 +116,7 @@ struct Ctx {
   void* blas = nullptr;    // rocblas_handle
   int device = 0;
   int threads = 1;
+  int prec16 = 0;  // Config precision: 0 = as stored, VT_FP16 / VT_BF16 = 16-bit compute for fp32 models
   std::shared_ptr<FastState> fast;
 };
 

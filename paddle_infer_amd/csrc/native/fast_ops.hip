@@ -9,7 +9,9 @@
 // * Fused transformer ops of an IR-optimised program (the Python Predictor's passes, saved with
 //   `Predictor.save_optimized_model`): multihead_matmul (QKV GEMM + bias, packed flash attention
 //   with the BiasQK mask), fc (+ activation), fused_fc_elementwise_layernorm, skip_layernorm,
-//   fused_embedding_eltwise_layernorm, layer_norm, softmax, matmul / matmul_v2, lookup_table_v2.
+//   fused_embedding_eltwise_layernorm, layer_norm, softmax, matmul / matmul_v2, lookup_table_v2,
+//   and fused_multi_transformer (GPT context + cached decode: flash attention, the split-K decode
+//   attention and the packed weight-stream GEMVs).
 //
 // Parity: reference `paddle/fluid/inference/api/analysis_predictor.cc` running the fused GPU ops
 // (`operators/fused/multihead_matmul_op.cu`, `fc_op`, `fused_fc_elementwise_layernorm_op.cu`,
@@ -53,6 +55,15 @@ int piamd_embedding_fwd(const long long* ids, const void* w, long long start, in
 int piamd_transpose_bf16(const void* src, void* dst, int R, int C, hipStream_t stream);
 int piamd_softmax_fwd(int f16, const void* x, const void* mask, int mask_rows, int causal_q, void* y,
                       int rows, int N, float scale, hipStream_t stream);
+int piamd_qkv_prep(void* qkv, long long ld, const void* bias, void* kc, void* vc, const int* pos0, int B, int S,
+                   int Hq, int Hk, int D, int maxS, int rot, int neox, float base, hipStream_t st);
+int piamd_decode_attn(const void* qkv, long long ldq, const void* bias, int prep, int rot, int neox, float base,
+                      void* kc, void* vc, const int* lens, int B, int Hq, int Hk, int D, int maxS, int chunk,
+                      int nsplit, const void* mask, long long ldm, float scale, float* part, int* cnt, void* out,
+                      long long ldo, hipStream_t st);
+int piamd_wo_gemm_ex(int bits, const void* x, long long ldx, const void* wp, const float* scale, const void* bias,
+                     void* y, long long ldy, float* ws, int* cnt, int M, int N, int K, int KS, int act,
+                     const void* ln_g, const void* ln_b, float eps, const void* resid, long long ldr, hipStream_t st);
 }
 
 #define FCHK(call, what)                                                                      \
@@ -73,6 +84,9 @@ struct FastState {
   size_t sg_ws_n = 0, sg_cnt_n = 0;
   std::shared_ptr<Buffer> ks_ws;          // assembly split-K f32 planes
   size_t ks_ws_n = 0;
+  std::map<const void*, DTensor> b16;     // bf16 copies of fp32 parameters (fused_multi_transformer)
+  std::map<const void*, DTensor> packed;  // MFMA-tile packed decode weights, keyed by the [N, K] copy
+  std::map<std::string, std::shared_ptr<Buffer>> scratch;  // zero-initialised, kept zeroed by the kernels
 };
 
 namespace {
@@ -484,6 +498,295 @@ void op_matmul(Ctx& c, const OpDesc& op, Scope& s) {
   s[op.out("Out")] = o;
 }
 
+// ------------------------------------------------------------------ fused_multi_transformer
+// Parity: reference `operators/fused/fused_multi_transformer_op.cu` (pre-LN GPT blocks with a
+// [2, B, H, max_seq, D] CacheKV per layer: context pass without TimeStep, one-token decode with it)
+// and the Python Predictor's path (incubate/nn/functional.py multi_transformer_forward): context =
+// LN → QKV GEMM → qkv_prep (bias, cache write) → flash attention → out GEMM → add+LN → FFN1(+act) →
+// FFN2, the residual adds folded into the next LayerNorm; decode = per layer four weight-stream
+// GEMVs on MFMA-tile packed weights (pre-LN in the GEMV prologue at ≤ 2 rows, residual adds in the
+// epilogues) around the split-K decode attention that also adds the QKV bias and writes the cache.
+// bf16 compute (fp32 models need PrecisionType::kBf16); caches updated in place.
+__global__ void fmt_pack_kernel(const unsigned short* __restrict__ w, unsigned short* __restrict__ p, int N, int K) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)N * K) return;
+  const int n = (int)(i / K), k = (int)(i % K);
+  p[(((long long)(n / 32) * (K / 16) + k / 16) * 64 + (n % 32) + 32 * ((k % 16) / 8)) * 8 + k % 8] = w[i];
+}
+
+__global__ void fmt_lens_kernel(const int* __restrict__ ts, int* __restrict__ lens, int B) {
+  const int b = blockIdx.x * 64 + threadIdx.x;
+  if (b < B) lens[b] = ts[0] + 1;
+}
+
+// zero-initialised scratch, one buffer per key (the kernels that use it leave it zeroed again)
+void* zscratch(Ctx& c, const std::string& key, size_t bytes) {
+  FastState& st = state(c);
+  auto& b = st.scratch[key];
+  if (!b) {
+    b = alloc_buffer(std::max<size_t>(bytes, 4), true);
+    zero_dev(c, b->p, std::max<size_t>(bytes, 4));
+  }
+  return b->p;
+}
+
+// bf16 view of a floating tensor: bf16 as is; fp32 cast (cached per source buffer when `cache`)
+DTensor as_bf16(Ctx& c, const DTensor& t, bool cache, const std::string& who) {
+  if (t.dtype == VT_BF16) return t;
+  if (t.dtype != VT_FP32) throw std::runtime_error(who + ": bf16 or fp32 tensors only (fp16 model)");
+  FastState& st = state(c);
+  if (cache) {
+    auto it = st.b16.find(t.buf->p);
+    if (it != st.b16.end()) return it->second;
+  }
+  DTensor o = make(c, VT_BF16, t.dims);
+  gpu::cast(c, t.buf->p, VT_FP32, o.buf->p, VT_BF16, t.numel());
+  if (cache) st.b16[t.buf->p] = o;
+  return o;
+}
+
+const DTensor& packed_of(Ctx& c, const DTensor& nk, const std::string& who) {
+  FastState& st = state(c);
+  auto it = st.packed.find(nk.buf->p);
+  if (it != st.packed.end()) return it->second;
+  const int N = (int)nk.dims[0], K = (int)nk.dims[1];
+  if (N % 32 || K % 16) throw std::runtime_error(who + ": decode weights need N % 32 == 0 and K % 16 == 0");
+  DTensor p = make(c, VT_BF16, nk.dims);
+  const long long n = (long long)N * K;
+  hipLaunchKernelGGL(fmt_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, S(c),
+                     (const unsigned short*)nk.buf->p, (unsigned short*)p.buf->p, N, K);
+  return st.packed[nk.buf->p] = p;
+}
+
+// y[M, N] = act(LN?(x) · W + bias) (+ resid) on the packed weight-stream GEMV (ops/inference.py
+// packed_linear: LN in the prologue at ≤ 2 rows, split-K to ~192 workgroups otherwise)
+DTensor fmt_gemv(Ctx& c, const DTensor& x, int M, int K, const DTensor& wp, int N, const DTensor* bias, int act,
+                 const DTensor* lng, const DTensor* lnb, float eps, const DTensor* resid, const std::string& who) {
+  DTensor y = make(c, VT_BF16, {M, N});
+  const void* xin = x.buf->p;
+  DTensor xn;
+  const bool fuse_ln = lng && lnb && M <= 2 && K % 512 == 0 && K <= 2048;
+  if (lng && !fuse_ln) {
+    xn = make(c, VT_BF16, {M, K});
+    layer_norm16(c, x, nullptr, lng, lnb, xn, M, K, eps, who);
+    xin = xn.buf->p;
+  }
+  const int tiles = (N / 32) * ((M + 31) / 32);
+  int KS = 1;
+  if (!fuse_ln)
+    while (tiles * KS < 192 && (K / 16) / (KS * 2) >= 16) KS *= 2;
+  float* ws = nullptr;
+  int* cnt = nullptr;
+  if (KS > 1) {
+    const std::string k = std::to_string(M) + "x" + std::to_string(N);
+    if (M <= 8) {  // in-kernel fixup: zeroed partials + arrival counters
+      ws = (float*)zscratch(c, "wo_ws" + k, (size_t)M * N * 4);
+      cnt = (int*)zscratch(c, "wo_cnt" + k, (size_t)tiles * 4);
+    } else {
+      ws = (float*)zscratch(c, "wo_ks" + k + "x" + std::to_string(KS), (size_t)KS * M * N * 4);
+    }
+  }
+  FCHK(piamd_wo_gemm_ex(16, xin, K, wp.buf->p, nullptr, bias ? bias->buf->p : nullptr, y.buf->p, N, ws, cnt, M, N,
+                        K, KS, act, fuse_ln ? lng->buf->p : nullptr, fuse_ln ? lnb->buf->p : nullptr, eps,
+                        resid ? resid->buf->p : nullptr, resid ? N : 0, S(c)),
+       who + " (weight-stream GEMV)");
+  return y;
+}
+
+void op_fmt(Ctx& c, const OpDesc& op, Scope& s) {
+  const std::string who = "fused_multi_transformer";
+  auto reject = [&](const std::string& what) {
+    throw std::runtime_error(who + " (native engine): " + what + " is not supported (use the Python Predictor)");
+  };
+  if (!op.ab("pre_layer_norm", true)) reject("post-LayerNorm");
+  if (!op.ab("trans_qkvw", true)) reject("trans_qkvw = false");
+  if (op.has_in("PreCaches") || op.has_in("RotaryPosEmb") || op.ai("rotary_emb_dims", 0) != 0) reject("RoPE / PreCaches");
+  if (op.has_in("SeqLengths") || op.has_in("BeamCacheOffset")) reject("SeqLengths / BeamCacheOffset");
+  if (op.ai("ring_id", -1) >= 0) reject("a tensor-parallel ring");
+  const std::string actn = op.as("act_method", "gelu");
+  const int act = actn == "gelu" ? A_GELU : actn == "relu" ? A_RELU : -1;
+  if (act < 0) reject("act_method " + actn);
+  const float eps = op.af("epsilon", 1e-5f);
+  const DTensor& x0 = get(c, s, op.in("X"));
+  if (x0.dtype == VT_FP32 && c.prec16 != VT_BF16)
+    throw std::runtime_error(who + ": fp32 models run natively in bf16 (EnableUseGpu(..., PrecisionType::kBf16))");
+  const DTensor x = as_bf16(c, x0, false, who);
+  if (x.dims.size() != 3) throw std::runtime_error(who + ": X must be [B, S, E]");
+  const int B = (int)x.dims[0], S_ = (int)x.dims[1], E = (int)x.dims[2], T = B * S_;
+  const int L = (int)op.inputs.at("QKVW").size();
+  std::vector<DTensor> W[12];
+  const char* slots[12] = {"LnScale", "LnBias", "QKVW", "QKVBias", "OutLinearW", "OutLinearBias",
+                           "FFNLnScale", "FFNLnBias", "FFN1Weight", "FFN1Bias", "FFN2Weight", "FFN2Bias"};
+  for (int k = 0; k < 12; ++k) {
+    const bool required = k == 0 || k == 2 || k == 4 || k == 6 || k == 8 || k == 10;
+    if (!op.has_in(slots[k])) {
+      if (required) throw std::runtime_error(who + ": missing " + slots[k]);
+      W[k].assign(L, DTensor());
+      continue;
+    }
+    const auto& names = op.inputs.at(slots[k]);
+    if ((int)names.size() != L) throw std::runtime_error(who + ": " + slots[k] + " needs one entry per layer");
+    for (const auto& n : names) W[k].push_back(as_bf16(c, get(c, s, n), true, who));
+  }
+  auto opt = [&](int k, int l) -> const DTensor* { return W[k][l].buf ? &W[k][l] : nullptr; };
+  // QKVW [3, H, D, E] or [Hq + 2Hk, D, E] (trans_qkvw): already the K-contiguous [N, E] operand
+  const auto& qd = W[2][0].dims;
+  if (qd.back() != E || (qd.size() != 4 && qd.size() != 3)) throw std::runtime_error(who + ": QKVW shape");
+  const int D = (int)qd[qd.size() - 2];
+  const int nh = (int)(W[2][0].numel() / ((int64_t)D * E));
+  const int Hk = op.ai("num_kv_heads", -1) > 0 ? (int)op.ai("num_kv_heads", -1) : nh / 3;
+  const int Hq = nh - 2 * Hk, HQD = Hq * D, NQKV = nh * D;
+  const int F = (int)W[8][0].dims[1];
+  // caches: per layer [2, B, Hk, maxS, D], bf16 in place (an fp32 feed is converted once and kept)
+  std::vector<DTensor*> caches;
+  if (op.has_in("CacheKV")) {
+    for (const auto& n : op.inputs.at("CacheKV")) {
+      DTensor& ct = get(c, s, n);
+      if (ct.dtype != VT_BF16) ct = as_bf16(c, ct, false, who);
+      if (ct.dims.size() != 5 || ct.dims[0] != 2 || ct.dims[1] != B || ct.dims[2] != Hk || ct.dims[4] != D)
+        throw std::runtime_error(who + ": CacheKV must be [2, B, Hk, max_seq, D]");
+      caches.push_back(&ct);
+    }
+    if ((int)caches.size() != L) throw std::runtime_error(who + ": one CacheKV per layer");
+  }
+  const int maxS = caches.empty() ? 0 : (int)caches[0]->dims[3];
+  auto kv = [&](int l, int which) -> void* {
+    if (caches.empty()) return nullptr;
+    return (char*)caches[l]->buf->p + (size_t)which * B * Hk * maxS * D * 2;
+  };
+  const DTensor* mask = nullptr;
+  DTensor maskb;
+  if (op.has_in("SrcMask")) {
+    maskb = as_bf16(c, get(c, s, op.in("SrcMask")), false, who);
+    mask = &maskb;
+  }
+  const bool decode = op.has_in("TimeStep");
+  DTensor res = x;
+  res.dims = {T, E};
+  if (decode) {
+    if (S_ != 1 || caches.empty()) throw std::runtime_error(who + ": decode (TimeStep) needs one token and CacheKV");
+    if (Hq % Hk || (Hq / Hk != 1 && Hq / Hk != 2 && Hq / Hk != 4 && Hq / Hk != 8) || (D != 64 && D != 128))
+      reject("this head geometry in decode");
+    const DTensor& ts = get(c, s, op.in("TimeStep"));
+    if (ts.dtype != VT_INT32) throw std::runtime_error(who + ": TimeStep must be int32");
+    int* lens = (int*)zscratch(c, "fmt_lens" + std::to_string(B), (size_t)B * 4);
+    hipLaunchKernelGGL(fmt_lens_kernel, dim3((B + 63) / 64), dim3(64), 0, S(c), (const int*)ts.buf->p, lens, B);
+    int chunk = maxS <= 256 ? std::max(16, maxS) : maxS <= 1024 ? 64 : maxS <= 4096 ? 128 : 256;
+    chunk = std::max(16, std::min(512, chunk));
+    const int ns = std::max(1, (maxS + chunk - 1) / chunk);
+    float* part = nullptr;
+    int* cnt = nullptr;
+    if (ns > 1) {
+      part = (float*)zscratch(c, "fmt_part" + std::to_string(B * Hq * ns * (D + 2)), (size_t)B * Hq * ns * (D + 2) * 4);
+      cnt = (int*)zscratch(c, "fmt_cnt" + std::to_string(B * Hk), (size_t)B * Hk * 4);
+    }
+    const long long ldm = mask ? mask->numel() / B : 0;
+    for (int l = 0; l < L; ++l) {
+      DTensor q2 = W[2][l];
+      q2.dims = {NQKV, E};
+      const DTensor& wq = packed_of(c, q2, who);
+      const DTensor& wo = packed_of(c, transposed(c, W[4][l], who), who);
+      const DTensor& w1 = packed_of(c, transposed(c, W[8][l], who), who);
+      const DTensor& w2 = packed_of(c, transposed(c, W[10][l], who), who);
+      DTensor qkv = fmt_gemv(c, res, B, E, wq, NQKV, nullptr, A_NONE, &W[0][l], opt(1, l), eps, nullptr, who);
+      DTensor att = make(c, VT_BF16, {B, HQD});
+      FCHK(piamd_decode_attn(qkv.buf->p, NQKV, opt(3, l) ? W[3][l].buf->p : nullptr, 1, 0, 1, 10000.f, kv(l, 0),
+                             kv(l, 1), lens, B, Hq, Hk, D, maxS, chunk, ns, mask ? mask->buf->p : nullptr, ldm,
+                             1.f / std::sqrt((float)D), part, cnt, att.buf->p, HQD, S(c)),
+           who + " (decode attention)");
+      res = fmt_gemv(c, att, B, HQD, wo, E, opt(5, l), A_NONE, nullptr, nullptr, eps, &res, who);
+      DTensor h = fmt_gemv(c, res, B, E, w1, F, opt(9, l), act, &W[6][l], opt(7, l), eps, nullptr, who);
+      res = fmt_gemv(c, h, B, F, w2, E, opt(11, l), A_NONE, nullptr, nullptr, eps, &res, who);
+    }
+  } else {
+    int* pos0 = (int*)zscratch(c, "fmt_pos0_" + std::to_string(B), (size_t)B * 4);
+    DTensor pend;
+    const DTensor* pend_b = nullptr;
+    for (int l = 0; l < L; ++l) {
+      DTensor xn = make(c, VT_BF16, {T, E});
+      if (!pend.buf) {
+        layer_norm16(c, res, nullptr, &W[0][l], opt(1, l), xn, T, E, eps, who);
+      } else {  // LN(residual + ffn2 + bias) of the previous block, its sum kept as the residual
+        DTensor nr = make(c, VT_BF16, {T, E});
+        FCHK(piamd_layernorm_fwd(1, pend.buf->p, pend_b ? pend_b->buf->p : nullptr, res.buf->p, W[0][l].buf->p,
+                                 opt(1, l) ? W[1][l].buf->p : nullptr, xn.buf->p, nr.buf->p, nullptr, nullptr, T, E,
+                                 eps, 0.f, 0, 0, 0, S(c)),
+             who + " (add + LayerNorm)");
+        res = nr;
+      }
+      DTensor qkv = make(c, VT_BF16, {T, NQKV});
+      gemm_nt(c, 0, xn.buf->p, E, W[2][l].buf->p, E, qkv.buf->p, NQKV, T, NQKV, E, nullptr, A_NONE, who);
+      FCHK(piamd_qkv_prep(qkv.buf->p, NQKV, opt(3, l) ? W[3][l].buf->p : nullptr, kv(l, 0), kv(l, 1), pos0, B, S_,
+                          Hq, Hk, D, maxS, 0, 1, 10000.f, S(c)),
+           who + " (qkv bias + cache write)");
+      DTensor att = make(c, VT_BF16, {T, HQD});
+      FaArgs a;
+      std::memset(&a, 0, sizeof(a));
+      const char* base = (const char*)qkv.buf->p;
+      a.q = base;
+      a.k = base + (size_t)HQD * 2;
+      a.v = base + (size_t)(Hq + Hk) * D * 2;
+      a.o = att.buf->p;
+      a.B = B, a.Sq = S_, a.Sk = S_, a.Hq = Hq, a.Hk = Hk, a.D = D;
+      a.causal = (!mask && op.ab("causal", false)) ? 1 : 0;
+      a.sqb = a.skb = a.svb = (long long)S_ * NQKV;
+      a.sqs = a.sks = a.svs = NQKV;
+      a.sqh = a.skh = a.svh = D;
+      a.sob = (long long)S_ * HQD, a.sos = HQD, a.soh = D;
+      if (mask) {
+        const auto& md = mask->dims;  // [B|1, H|1, S|1, S]
+        if (md.size() != 4 || md[3] != S_ || S_ % 4) reject("this SrcMask shape");
+        a.mask = mask->buf->p;
+        a.smb = md[0] > 1 ? md[1] * md[2] * md[3] : 0;
+        a.smh = md[1] > 1 ? md[2] * md[3] : 0;
+        a.smq = md[2] > 1 ? md[3] : 0;
+      }
+      a.scale = 1.f / std::sqrt((float)D);
+      FCHK(piamd_fa_fwd(&a, 0, S(c)), who + " (flash attention)");
+      DTensor o = make(c, VT_BF16, {T, E});
+      const DTensor& wo = transposed(c, W[4][l], who);
+      gemm_nt(c, 0, att.buf->p, HQD, wo.buf->p, HQD, o.buf->p, E, T, E, HQD, nullptr, A_NONE, who);
+      DTensor yn = make(c, VT_BF16, {T, E}), nr = make(c, VT_BF16, {T, E});
+      FCHK(piamd_layernorm_fwd(1, o.buf->p, opt(5, l) ? W[5][l].buf->p : nullptr, res.buf->p, W[6][l].buf->p,
+                               opt(7, l) ? W[7][l].buf->p : nullptr, yn.buf->p, nr.buf->p, nullptr, nullptr, T, E, eps,
+                               0.f, 0, 0, 0, S(c)),
+           who + " (add + LayerNorm)");
+      res = nr;
+      DTensor h = make(c, VT_BF16, {T, F});
+      const DTensor& w1 = transposed(c, W[8][l], who);
+      gemm_nt(c, 0, yn.buf->p, E, w1.buf->p, E, h.buf->p, F, T, F, E, opt(9, l) ? W[9][l].buf->p : nullptr, act, who);
+      pend = make(c, VT_BF16, {T, E});
+      const DTensor& w2 = transposed(c, W[10][l], who);
+      gemm_nt(c, 0, h.buf->p, F, w2.buf->p, F, pend.buf->p, E, T, E, F, nullptr, A_NONE, who);
+      pend_b = opt(11, l);
+    }
+    // out = residual + ffn2 (+ bias)
+    DTensor out = make(c, VT_BF16, {T, E});
+    Bcast bc;
+    bc.nd = 1;
+    bc.dims[0] = (int64_t)T * E;
+    bc.sa[0] = bc.sb[0] = 1;
+    bc.n = (int64_t)T * E;
+    gpu::binary16(c, B_ADD, 0, res.buf->p, pend.buf->p, out.buf->p, bc);
+    if (pend_b) {
+      Bcast bb;
+      bb.nd = 2;
+      bb.dims[0] = T, bb.dims[1] = E;
+      bb.sa[0] = E, bb.sa[1] = 1;
+      bb.sb[0] = 0, bb.sb[1] = 1;
+      bb.n = (int64_t)T * E;
+      gpu::binary16(c, B_ADD, 0, out.buf->p, pend_b->buf->p, out.buf->p, bb);
+    }
+    res = out;
+  }
+  res.dims = {B, S_, E};
+  s[op.out("Out")] = res;
+  if (op.has_out("CacheKVOut")) {
+    const auto& outs = op.outputs.at("CacheKVOut");
+    for (size_t i = 0; i < outs.size() && i < caches.size(); ++i) s[outs[i]] = *caches[i];
+  }
+}
+
 using FastFn = void (*)(Ctx&, const OpDesc&, Scope&);
 
 const std::map<std::string, FastFn>& fast_ops() {
@@ -499,6 +802,7 @@ const std::map<std::string, FastFn>& fast_ops() {
       {"softmax", op_softmax},
       {"matmul", op_matmul},
       {"matmul_v2", op_matmul},
+      {"fused_multi_transformer", op_fmt},
   };
   return m;
 }
@@ -524,7 +828,8 @@ bool fast_run(Ctx& c, const OpDesc& op, Scope& s) {
   auto it = fast_ops().find(op.type);
   if (it == fast_ops().end()) return false;
   const int dt = float_dtype(c, op, s);
-  if (!is16(dt)) return false;
+  // fused_multi_transformer has no generic implementation: it always runs here (bf16)
+  if (!is16(dt) && op.type != "fused_multi_transformer") return false;
   it->second(c, op, s);
   return true;
 }

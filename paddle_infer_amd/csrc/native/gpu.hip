@@ -26,7 +26,7 @@ extern "C" int piamd_layernorm_fwd(int dtype, const void* x, const void* bias, c
 namespace pdn {
 
 Buffer::~Buffer() {
-  if (!p) return;
+  if (!p || !owned) return;
   if (dev) (void)hipFree(p);
   else std::free(p);
 }

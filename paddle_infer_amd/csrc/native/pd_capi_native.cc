@@ -1,10 +1,10 @@
 // The reference C API (`capi_exp` pd_inference_api.h, declared in ../capi/pd_inference_api.h)
 // on the native C++ engine: libpiamd_infer.so exports the Config / Predictor / Tensor / utility
-// entry points a C deployment uses, with no Python interpreter behind them (libpiamd_capi.so
-// keeps the full surface on the framework's Python predictor: IR passes, hipGraph, LLM ops).
+// entry points a C deployment uses, with no Python interpreter behind them.
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <stdexcept>
 #include <string>
 
 #include "../capi/pd_inference_api.h"
@@ -66,9 +66,11 @@ void PD_ConfigSetProgFile(PD_Config* c, const char* prog) { PD_ConfigSetModel(c,
 void PD_ConfigSetParamsFile(PD_Config* c, const char* params) { PD_ConfigSetModel(c, c->prog.c_str(), params); }
 const char* PD_ConfigGetProgFile(PD_Config* c) { return c->prog.c_str(); }
 const char* PD_ConfigGetParamsFile(PD_Config* c) { return c->params.c_str(); }
-void PD_ConfigEnableUseGpu(PD_Config* c, uint64_t mem_mb, int32_t device_id, PD_PrecisionType) {
+void PD_ConfigEnableUseGpu(PD_Config* c, uint64_t mem_mb, int32_t device_id, PD_PrecisionType prec) {
   c->mem_mb = (int)mem_mb;
-  c->cfg.EnableUseGpu(mem_mb, device_id);
+  using P = paddle_infer::PrecisionType;
+  c->cfg.EnableUseGpu(mem_mb, device_id,
+                      prec == PD_PRECISION_BFLOAT16 ? P::kBf16 : prec == PD_PRECISION_HALF ? P::kHalf : P::kFloat32);
 }
 void PD_ConfigDisableGpu(PD_Config* c) { c->cfg.DisableGpu(); }
 PD_Bool PD_ConfigUseGpu(PD_Config* c) { return c->cfg.use_gpu(); }
@@ -191,6 +193,30 @@ PD_COPY(Int32, int32_t)
 PD_COPY(Uint8, uint8_t)
 PD_COPY(Int8, int8_t)
 #undef PD_COPY
+void PD_TensorShareExternalData(PD_Tensor* t, void* data, size_t n, int32_t* shape, PD_PlaceType place,
+                                PD_DataType dt) {
+  using D = paddle_infer::DataType;
+  guarded([&]() -> int {
+    D d;
+    switch (dt) {
+      case PD_DATA_FLOAT32: d = D::FLOAT32; break;
+      case PD_DATA_INT32: d = D::INT32; break;
+      case PD_DATA_INT64: d = D::INT64; break;
+      case PD_DATA_UINT8: d = D::UINT8; break;
+      case PD_DATA_INT8: d = D::INT8; break;
+      case PD_DATA_FLOAT16: d = D::FLOAT16; break;
+      case PD_DATA_BOOL: d = D::BOOL; break;
+      case PD_DATA_BFLOAT16: d = D::BFLOAT16; break;
+      default: throw std::runtime_error("PD_TensorShareExternalData: unknown data type");
+    }
+    t->shape.assign(shape, shape + n);
+    t->staged.clear();
+    t->staged_dt = -1;
+    t->t->ShareExternalData(data, t->shape,
+                            place == PD_PLACE_GPU ? paddle_infer::PlaceType::kGPU : paddle_infer::PlaceType::kCPU, d);
+    return 0;
+  }, 1);
+}
 PD_OneDimArrayInt32* PD_TensorGetShape(PD_Tensor* t) {
   const auto s = t->t->shape();
   auto* a = (PD_OneDimArrayInt32*)std::malloc(sizeof(PD_OneDimArrayInt32));
@@ -207,6 +233,9 @@ PD_DataType PD_TensorGetDataType(PD_Tensor* t) {
     case paddle_infer::DataType::INT64: return PD_DATA_INT64;
     case paddle_infer::DataType::UINT8: return PD_DATA_UINT8;
     case paddle_infer::DataType::INT8: return PD_DATA_INT8;
+    case paddle_infer::DataType::FLOAT16: return PD_DATA_FLOAT16;
+    case paddle_infer::DataType::BOOL: return PD_DATA_BOOL;
+    case paddle_infer::DataType::BFLOAT16: return PD_DATA_BFLOAT16;
     default: return PD_DATA_UNK;
   }
 }

@@ -1,9 +1,11 @@
 // Command-line driver of the native C++ predictor (no Python):
-//   pd_infer_run <model.pdmodel> <model.pdiparams> [--gpu DEV] [--graph] [--threads N]
-//                [--warmup W] [--repeat R]
+//   pd_infer_run <model.pdmodel> <model.pdiparams> [--gpu DEV] [--precision fp32|fp16|bf16]
+//                [--graph] [--threads N] [--warmup W] [--repeat R] [--step-input NAME]
 //                --input NAME DTYPE D0,D1,.. FILE.bin ...  --output-dir DIR
 // Inputs are raw little-endian files; each fetch target is written to DIR/<index>.bin with its
 // shape on stdout ("output <i> <name> <dtype> d0,d1,..") and the mean Run() time last.
+// --step-input NAME: the int32 scalar input NAME advances by one before every Run after the
+// first (a decode loop: fused_multi_transformer TimeStep over caches that stay resident).
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -41,10 +43,16 @@ int main(int argc, char** argv) {
     struct In { std::string name, dtype, file; std::vector<int> dims; };
     std::vector<In> ins;
     std::string outdir = ".";
-    int repeat = 1, warmup = 0;
+    int repeat = 1, warmup = 0, gpu = -1;
+    PrecisionType prec = PrecisionType::kFloat32;
+    std::string step_input;
     for (int i = 3; i < argc; ++i) {
       const std::string a = argv[i];
-      if (a == "--gpu") cfg.EnableUseGpu(256, std::stoi(argv[++i]));
+      if (a == "--gpu") gpu = std::stoi(argv[++i]);
+      else if (a == "--precision") {
+        const std::string p = argv[++i];
+        prec = p == "bf16" ? PrecisionType::kBf16 : p == "fp16" ? PrecisionType::kHalf : PrecisionType::kFloat32;
+      } else if (a == "--step-input") step_input = argv[++i];
       else if (a == "--threads") cfg.SetCpuMathLibraryNumThreads(std::stoi(argv[++i]));
       else if (a == "--repeat") repeat = std::stoi(argv[++i]);
       else if (a == "--warmup") warmup = std::stoi(argv[++i]);
@@ -62,8 +70,10 @@ int main(int argc, char** argv) {
         return 2;
       }
     }
+    if (gpu >= 0) cfg.EnableUseGpu(256, gpu, prec);
     auto pred = CreatePredictor(cfg);
     std::vector<std::string> raw;
+    int32_t step0 = 0;
     for (auto& in : ins) {
       raw.push_back(read_all(in.file));
       auto h = pred->GetInputHandle(in.name);
@@ -72,10 +82,23 @@ int main(int argc, char** argv) {
       else if (in.dtype == "int64") h->CopyFromCpu(reinterpret_cast<const int64_t*>(raw.back().data()));
       else if (in.dtype == "int32") h->CopyFromCpu(reinterpret_cast<const int32_t*>(raw.back().data()));
       else throw std::runtime_error("unsupported input dtype " + in.dtype);
+      if (in.name == step_input) step0 = *reinterpret_cast<const int32_t*>(raw.back().data());
     }
-    for (int r = 0; r < warmup; ++r) pred->Run();
+    int runs = 0;
+    auto advance = [&]() {
+      if (step_input.empty() || runs++ == 0) return;
+      const int32_t t = step0 + runs - 1;
+      auto h = pred->GetInputHandle(step_input);
+      h->Reshape({1});
+      h->CopyFromCpu(&t);
+    };
+    for (int r = 0; r < warmup; ++r) {
+      advance();
+      pred->Run();
+    }
     double ms = 0.0;
     for (int r = 0; r < repeat; ++r) {
+      advance();
       const auto t0 = std::chrono::steady_clock::now();
       pred->Run();
       ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -91,6 +114,7 @@ int main(int argc, char** argv) {
       switch (h->type()) {
         case DataType::FLOAT32:
         case DataType::FLOAT16:  // 16-bit outputs are written as float32
+        case DataType::BFLOAT16:
           dt = "float32"; bytes.resize(n * 4); h->CopyToCpu(reinterpret_cast<float*>(&bytes[0])); break;
         case DataType::INT64: dt = "int64"; bytes.resize(n * 8); h->CopyToCpu(reinterpret_cast<int64_t*>(&bytes[0])); break;
         case DataType::INT32: dt = "int32"; bytes.resize(n * 4); h->CopyToCpu(reinterpret_cast<int32_t*>(&bytes[0])); break;

@@ -36,11 +36,25 @@ DataType to_api(int vt) {
     case pdn::VT_INT32: return DataType::INT32;
     case pdn::VT_UINT8: return DataType::UINT8;
     case pdn::VT_INT8: return DataType::INT8;
-    case pdn::VT_FP16: return DataType::FLOAT16;
-    case pdn::VT_BF16: return DataType::FLOAT16;  // 16-bit float (CopyToCpu<float> converts)
+    case pdn::VT_FP16: return DataType::FLOAT16;  // 16-bit floats: CopyToCpu<float> converts
+    case pdn::VT_BF16: return DataType::BFLOAT16;
     case pdn::VT_BOOL: return DataType::BOOL;
   }
   throw std::runtime_error("unsupported dtype " + std::to_string(vt));
+}
+
+int from_api(DataType d) {
+  switch (d) {
+    case DataType::FLOAT32: return pdn::VT_FP32;
+    case DataType::INT64: return pdn::VT_INT64;
+    case DataType::INT32: return pdn::VT_INT32;
+    case DataType::UINT8: return pdn::VT_UINT8;
+    case DataType::INT8: return pdn::VT_INT8;
+    case DataType::FLOAT16: return pdn::VT_FP16;
+    case DataType::BOOL: return pdn::VT_BOOL;
+    case DataType::BFLOAT16: return pdn::VT_BF16;
+  }
+  throw std::runtime_error("unsupported DataType");
 }
 }  // namespace
 
@@ -82,6 +96,8 @@ class PredictorImpl {
     ctx.gpu = c.use_gpu();
     ctx.device = c.gpu_device_id();
     ctx.threads = std::max(1, c.cpu_math_library_num_threads());
+    ctx.prec16 = c.precision() == PrecisionType::kBf16 ? pdn::VT_BF16
+                 : c.precision() == PrecisionType::kHalf ? pdn::VT_FP16 : 0;
     if (ctx.gpu) pdn::dev_init(ctx);
     if (!c.params_file().empty()) {
       auto ps = pdn::load_params(prog, read_file(c.params_file()));
@@ -196,6 +212,21 @@ void Tensor::CopyFromCpu(const T* data) {
   t.buf = pdn::alloc_buffer(t.nbytes(), p_->ctx.gpu);
   if (p_->ctx.gpu) pdn::dev_copy(t.buf->p, data, t.nbytes(), 0, p_->ctx);
   else std::memcpy(t.buf->p, data, t.nbytes());
+  p_->scope[name_] = t;
+}
+
+void Tensor::ShareExternalData(void* data, const std::vector<int>& shape, PlaceType place, DataType dtype) {
+  if (!input_) throw std::runtime_error("ShareExternalData on an output handle");
+  if ((place == PlaceType::kGPU) != p_->ctx.gpu)
+    throw std::runtime_error("ShareExternalData: the data must live on the predictor's place");
+  pdn::DTensor t;
+  t.dtype = from_api(dtype);
+  for (int d : shape) t.dims.push_back(d);
+  t.buf = std::make_shared<pdn::Buffer>();
+  t.buf->p = data;
+  t.buf->bytes = t.nbytes();
+  t.buf->dev = p_->ctx.gpu;
+  t.buf->owned = false;
   p_->scope[name_] = t;
 }
 

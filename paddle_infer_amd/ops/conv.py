@@ -640,6 +640,16 @@ class _ConvTranspose(torch.autograd.Function):
             if bias is not None:
                 y = y + bias.to(dt)
             y = y.contiguous()
+        elif groups == 1 and dt == torch.float32:  # split-bf16 products (see _Conv2dF32)
+            Kp, Cp = _pad64(Cin), -(-Cout // 4) * 4
+            pw = (0, 0, 0, 0, 0, Cp - Cout, 0, Kp - Cin)
+            xh, xl = _split2(x)
+            wh, wl = (torch.nn.functional.pad(t, pw) for t in _split2(weight.float()))
+            y = conv2d_dgrad_strided(_cat_c((xh, xl, xh), Kp), torch.cat([wh, wh, wl], 0), Ho, Wo,
+                                     st, pad, dil, out_f32=True)[..., :Cout]
+            if bias is not None:
+                y = y + bias.float()
+            y = y.contiguous()
         else:
             w_t = (weight.to(dt).view(groups, Cin // groups, og, R, S).permute(3, 4, 1, 0, 2)
                    .reshape(R, S, Cin // groups, Cout).contiguous())
@@ -662,6 +672,8 @@ class _ConvTranspose(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if groups == 1 and dt in _HALF:
                 dx = _Conv2dNHWC.apply(dy, weight, None, st, pad, dil, 0)
+            elif groups == 1 and dt == torch.float32:
+                dx = _Conv2dF32.apply(dy, weight, None, st, pad, dil)
             else:
                 dx = _ConvDirect.apply(dy, weight, None, st, pad, dil, groups)
             dx = dx[:, :H, :W]
@@ -670,6 +682,13 @@ class _ConvTranspose(torch.autograd.Function):
                 Cp, Kp = -(-Cout // 8) * 8, _pad64(Cin)
                 dw = conv2d_wgrad(_padc(dy, Cp).contiguous(), _padc(x, Kp).contiguous(), R, S, st,
                                   pad, dil)[:Cin, :Cout]
+            elif groups == 1 and dt == torch.float32 and wgrad_eligible(8, 64, 3 * N * H * W):
+                Cp, Kp = -(-Cout // 8) * 8, _pad64(Cin)
+                dyh, dyl = _split2(dy)
+                xh, xl = _split2(x)
+                d3 = torch.cat([_padc(dyh, Cp), _padc(dyl, Cp), _padc(dyh, Cp)], 0).contiguous()
+                x3 = torch.cat([_padc(xh, Kp), _padc(xh, Kp), _padc(xl, Kp)], 0).contiguous()
+                dw = conv2d_wgrad(d3, x3, R, S, st, pad, dil)[:Cin, :Cout]
             else:
                 dw = _direct_wgrad(dy, x, R, S, st, pad, dil, Cout, Cin, groups)
             dw = dw.to(weight.dtype)
@@ -680,8 +699,8 @@ class _ConvTranspose(torch.autograd.Function):
 
 def conv2d_transpose_any(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1,
                          dilation=1, nhwc=False, output_size=None):
-    """Own-kernel route for ``conv2d_transpose`` of a GPU tensor; ``None`` → library (dense fp32
-    without autocast, string padding)."""
+    """Own-kernel route for ``conv2d_transpose`` of a GPU tensor; ``None`` → library (string
+    padding, or dense fp32 with ``FP32_SPLIT`` off)."""
     if not (HIP_CONV and x.is_cuda and x.dim() == 4 and weight.dim() == 4) or isinstance(padding, str):
         return None
     pad, st, dil, op = _pair(padding), _pair(stride), _pair(dilation), _pair(output_padding)
@@ -704,8 +723,8 @@ def conv2d_transpose_any(x, weight, bias=None, stride=1, padding=0, output_paddi
                    for i in range(2))
         if any(o < 0 or o >= max(st[i], dil[i]) for i, o in enumerate(op)):
             raise ValueError(f"conv2d_transpose: output_size {output_size} is not reachable")
-    if groups == 1 and dt == torch.float32:
-        _lib.fallback("conv2d_transpose", "dense fp32 transposed conv without autocast (library)")
+    if groups == 1 and dt == torch.float32 and not FP32_SPLIT:
+        _lib.fallback("conv2d_transpose", "dense fp32 transposed conv with FP32_SPLIT off (library)")
         return None
     with torch.autocast("cuda", enabled=False):
         xh = (x if nhwc else x.permute(0, 2, 3, 1)).to(dt).contiguous()

@@ -8,6 +8,8 @@ mkdir -p gpurun_out
 T="python -u -m pytest -x -q --timeout 240 --timeout-method thread"
 timeout -k 10 500 $T tests/test_attention_ds_gpu.py tests/test_attention_gpu.py tests/test_attention_varlen_gpu.py > gpurun_out/r4c_attn_tests.log 2>&1 || { tail -40 gpurun_out/r4c_attn_tests.log; exit 1; }
 tail -1 gpurun_out/r4c_attn_tests.log
+timeout -k 10 400 $T -s tests/test_native_fmt_gpu.py tests/test_native_fast_gpu.py > gpurun_out/r4c_native_tests.log 2>&1 || { tail -40 gpurun_out/r4c_native_tests.log; exit 1; }
+grep -E "decode step|run_ms|passed|failed" gpurun_out/r4c_native_tests.log | tail -8
 timeout -k 10 500 $T tests/test_conv_any_gpu.py tests/test_conv_gpu.py tests/test_conv_bwd_gpu.py > gpurun_out/r4c_conv_tests.log 2>&1 || { tail -40 gpurun_out/r4c_conv_tests.log; exit 1; }
 tail -1 gpurun_out/r4c_conv_tests.log
 S="96,1024,16,128;8,2048,16,128;4,4096,16,128;16,1024,32,64"

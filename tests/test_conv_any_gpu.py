@@ -170,6 +170,7 @@ def test_mobilenet_v2_step_without_library_conv():
     (torch.float16, 40, 24, 3, 2, 1, 1, 1),     # unaligned channels + output_padding
     (torch.bfloat16, 32, 32, 3, 1, 1, 0, 1),    # stride 1
     (torch.float32, 32, 64, 3, 2, 1, 1, 4),     # grouped, direct kernel
+    (torch.float32, 40, 24, 3, 2, 1, 1, 1),     # dense fp32: split-bf16 MFMA phases
     (torch.bfloat16, 48, 48, 4, 2, 1, 0, 48),   # depthwise transposed
 ])
 def test_conv2d_transpose(dt, Cin, Cout, R, st, pad, op, groups):

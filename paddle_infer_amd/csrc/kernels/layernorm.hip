@@ -13,12 +13,16 @@
 //    no second HBM read); 4 rows per 256-thread block so an 8192 x 2048 activation gets 2048 blocks.
 //  * N > 4096 (LLaMA-13B 5120, 65B 8192, up to 16384) and the few-row decode case: one workgroup per
 //    row (256 or 512 threads), row still register-resident, block reductions through LDS.
-//  * Backward: wave per row up to N = 2048 (220 VGPRs, 2 waves/SIMD), workgroup per row above.
+//  * Backward: wave per row up to N = 1024, two waves per row with a prefetched second row for
+//    1024 < N <= 2048, workgroup per row above.
 //  * Backward fuses dgamma/dbeta (and the dbias of the prologue): every thread accumulates its
 //    columns across a grid-stride set of rows in registers, each workgroup stores one row of a
 //    [G][N] partial slab, and a 16-row-strip reduction folds it (G/16 atomics per column). Dropout masks are regenerated from
 //    the stateless counter hash (common.h), never stored.
 #include "common.h"
+
+#include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -438,6 +442,158 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   }
 }
 
+// 1024 < N <= 2048 (GPT-1.3B's 2048): TWO waves per row, each owning half the columns (2 vectors
+// per lane), and the NEXT row's h / dy / mean / rstd prefetched into a second register stage, so
+// every wave keeps two row fetches in flight at ~160 VGPRs (3 waves per SIMD); the wave-per-row
+// kernel at this width holds 220 VGPRs for one row (2 waves per SIMD). The halves' row sums meet
+// through LDS (parity-double-buffered: one barrier per row); the trip count is uniform over the
+// workgroup so both row pairs reach every barrier.
+template <int DT>
+__global__ __launch_bounds__(256) void ln_bwd_pair_kernel(
+    const typename IO<DT>::T* __restrict__ dy, const typename IO<DT>::T* __restrict__ h,
+    const typename IO<DT>::T* __restrict__ gamma, const float* __restrict__ mean_in,
+    const float* __restrict__ rstd_in, const typename IO<DT>::T* __restrict__ dres_in,
+    typename IO<DT>::T* __restrict__ dres, typename IO<DT>::T* __restrict__ dx,
+    float* __restrict__ acc_dg, float* __restrict__ acc_db, float* __restrict__ acc_dbias,
+    int rows, int N, float p_drop, uint64_t seed, uint64_t offset, int rms) {
+  typedef IO<DT> io;
+  constexpr int NV = 2;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, half = w & 1, rp = w >> 1;
+  const int nvec = N >> 3;
+  __shared__ float red[2][2][2][2];  // [parity][row pair][half][s1, s2]
+  float dg[NV][8], db[NV][8], dbi[NV][8];
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { dg[i][j] = 0.f; db[i][j] = 0.f; dbi[i][j] = 0.f; }
+  const float keep_scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  const bool one_store = dx == dres && p_drop == 0.f;  // dres and dx alias: the same values
+  const int stride = gridDim.x * 2;
+  const int row0 = blockIdx.x * 2 + rp;
+  const int iters = rows > (int)blockIdx.x * 2 ? (rows - (int)blockIdx.x * 2 + stride - 1) / stride : 0;
+  typename io::Raw hr2[2][NV], dr2[2][NV];
+  float mean2[2], rstd2[2];
+  auto vcol = [&](int i) { return half * (NV * 64) + i * 64 + lane; };
+  auto load = [&](int row, auto pc) {
+    constexpr int P = decltype(pc)::value;
+    const int r = min(row, rows - 1);
+    const size_t base = (size_t)r * N;
+    mean2[P] = mean_in[r];
+    rstd2[P] = rstd_in[r];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int vi = min(vcol(i), nvec - 1);
+      hr2[P][i] = io::ldraw(h + base + vi * 8);
+      dr2[P][i] = io::ldraw(dy + base + vi * 8);
+    }
+  };
+  auto body = [&](int k, auto pc) {
+    constexpr int P = decltype(pc)::value;
+    const int row = row0 + k * stride;
+    const bool valid = row < rows;
+    const size_t base = (size_t)min(row, rows - 1) * N;
+    const float mean = mean2[P], rstd = rstd2[P];
+    const auto& hr = hr2[P];
+    const auto& dr = dr2[P];
+    typename io::Raw rr[NV], gr[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int vi = min(vcol(i), nvec - 1);
+      if (dres_in) rr[i] = io::ldraw(dres_in + base + vi * 8);
+      if (gamma) gr[i] = io::ldraw(gamma + vi * 8);
+    }
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      if (valid && vcol(i) < nvec) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = io::el(dr[i], j);
+          const float xh = (io::el(hr[i], j) - mean) * rstd;
+          const float gd = d * (gamma ? io::el(gr[i], j) : 1.f);
+          dg[i][j] += d * xh;
+          db[i][j] += d;
+          s1 += gd;
+          s2 += gd * xh;
+        }
+      }
+    }
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if (lane == 0) {
+      red[P][rp][half][0] = s1;
+      red[P][rp][half][1] = s2;
+    }
+    __syncthreads();
+    const float t1 = red[P][rp][0][0] + red[P][rp][1][0], t2 = red[P][rp][0][1] + red[P][rp][1][1];
+    const float m1 = rms ? 0.f : t1 / (float)N, m2 = t2 / (float)N;
+    if (!valid) return;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int vi = vcol(i);
+      if (vi < nvec) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = (io::el(hr[i], j) - mean) * rstd;
+          o[j] = rstd * (io::el(dr[i], j) * (gamma ? io::el(gr[i], j) : 1.f) - m1 - xh * m2);
+          if (dres_in) o[j] += io::el(rr[i], j);
+        }
+        if (dres && !one_store) io::store8(dres + base + vi * 8, o);
+        if (dx) {
+          if (p_drop > 0.f) {
+            float u[8];
+            hash_uniform8(seed, offset, base + vi * 8, u);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = u[j] >= p_drop ? o[j] * keep_scale : 0.f;
+          }
+          io::store8(dx + base + vi * 8, o);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dbi[i][j] += o[j];
+        }
+      }
+    }
+  };
+  if (iters > 0) load(row0, std::integral_constant<int, 0>{});
+  for (int k = 0; k < iters; k += 2) {
+    if (k + 1 < iters) load(row0 + (k + 1) * stride, std::integral_constant<int, 1>{});
+    body(k, std::integral_constant<int, 0>{});
+    if (k + 1 >= iters) break;
+    if (k + 2 < iters) load(row0 + (k + 2) * stride, std::integral_constant<int, 0>{});
+    body(k + 1, std::integral_constant<int, 1>{});
+  }
+  // the two row pairs' column partials of each half meet in LDS; one slab row per workgroup
+  __shared__ float cmb[2][64][NV * 8];
+  float* outs[3] = {acc_dg, acc_db, acc_dbias};
+  const size_t srow = (size_t)blockIdx.x * N;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    if (!outs[q]) continue;
+    if (rp == 1)
+#pragma unroll
+      for (int i = 0; i < NV; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cmb[half][lane][i * 8 + j] = q == 0 ? dg[i][j] : (q == 1 ? db[i][j] : dbi[i][j]);
+    __syncthreads();
+    if (rp == 0) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int vi = vcol(i);
+        if (vi >= nvec) continue;
+        f32x4 a, b;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          a[j] = (q == 0 ? dg[i][j] : (q == 1 ? db[i][j] : dbi[i][j])) + cmb[half][lane][i * 8 + j];
+          b[j] = (q == 0 ? dg[i][4 + j] : (q == 1 ? db[i][4 + j] : dbi[i][4 + j])) + cmb[half][lane][i * 8 + 4 + j];
+        }
+        *reinterpret_cast<f32x4*>(outs[q] + srow + vi * 8) = a;
+        *reinterpret_cast<f32x4*>(outs[q] + srow + vi * 8 + 4) = b;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // Rows longer than 2048 (the wave-per-row variant would drop to 1 wave/SIMD): a 512-thread
 // workgroup per row (NV = ceil(N / 4096) <= 4 vectors per thread), grid-stride over rows; every thread owns distinct columns, so the column partials go
 // straight to the atomics without an LDS reduction.
@@ -571,8 +727,21 @@ int launch_fwd(const void* x, const void* bias, const void* residual, const void
   return (int)hipGetLastError();
 }
 
+// 1024 < N <= 2048 on the two-waves-per-row kernel (PIAMD_LN_BWD_PAIR=0: the wave-per-row one)
+static inline bool bwd_pair(int N) {
+  static const bool on = [] {
+    const char* e = getenv("PIAMD_LN_BWD_PAIR");
+    return !(e && e[0] == '0');
+  }();
+  return on && N > 1024 && N <= 2048;
+}
+
 // Workgroups of the backward (= rows of the partial slab).
 static inline int bwd_grid(int rows, int N) {
+  if (bwd_pair(N)) {  // 2 rows per workgroup; ~160 VGPRs = 3 workgroups per CU, all resident
+    const int g = (rows + 1) / 2;
+    return g > 768 ? 768 : (g < 1 ? 1 : g);
+  }
   const int g = N > 2048 ? rows : (rows + 3) / 4;
   return g > 512 ? 512 : (g < 1 ? 1 : g);
 }
@@ -598,6 +767,10 @@ int launch_bwd(const void* dy, const void* h, const void* gamma, const float* me
     return (int)hipGetLastError();
   }
   dim3 grid(bwd_grid(rows, N)), block(256);
+  if (bwd_pair(N)) {
+    hipLaunchKernelGGL((ln_bwd_pair_kernel<DT>), grid, block, 0, st, BWD_ARGS);
+    return (int)hipGetLastError();
+  }
   switch ((N / 8 + 63) / 64) {
     case 1: hipLaunchKernelGGL((ln_bwd_kernel<1, DT>), grid, block, 0, st, BWD_ARGS); break;
     case 2: hipLaunchKernelGGL((ln_bwd_kernel<2, DT>), grid, block, 0, st, BWD_ARGS); break;

@@ -12,6 +12,9 @@ timeout -k 10 400 $T -s tests/test_native_fmt_gpu.py tests/test_native_fast_gpu.
 grep -E "decode step|run_ms|passed|failed" gpurun_out/r4c_native_tests.log | tail -8
 timeout -k 10 500 $T tests/test_conv_any_gpu.py tests/test_conv_gpu.py tests/test_conv_bwd_gpu.py > gpurun_out/r4c_conv_tests.log 2>&1 || { tail -40 gpurun_out/r4c_conv_tests.log; exit 1; }
 tail -1 gpurun_out/r4c_conv_tests.log
+timeout -k 10 300 $T tests/test_kernels_gpu.py tests/test_norm_gpu.py > gpurun_out/r4c_ln_tests.log 2>&1 || { tail -40 gpurun_out/r4c_ln_tests.log; exit 1; }
+tail -1 gpurun_out/r4c_ln_tests.log
+for P in 0 1; do PIAMD_LN_BWD_PAIR=$P timeout -k 10 120 python tools/bench_ln_bwd.py; done
 S="96,1024,16,128;8,2048,16,128;4,4096,16,128;16,1024,32,64"
 for MB in 0 8192; do
   echo "== PIAMD_FA_DS_MAX_MB=$MB"
@@ -34,3 +37,8 @@ python tools/prof_summary.py gpurun_out/r4c_prof_mbv2 > gpurun_out/r4c_prof_mbv2
 python tools/prof_summary.py gpurun_out/r4c_prof_attn > gpurun_out/r4c_prof_attn.txt 2>&1
 head -14 gpurun_out/r4c_prof_mbv2.txt
 head -10 gpurun_out/r4c_prof_attn.txt
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/r4c_prof_gen -o run -- python $GRAFT_REPO_ROOT/tools/bench_generate.py --batch 1 --prompt 128 --gen 64 --modes graph > $GRAFT_REPO_ROOT/gpurun_out/r4c_prof_gen.log 2>&1 || exit 1
+cd $GRAFT_REPO_ROOT
+python tools/prof_summary.py gpurun_out/r4c_prof_gen > gpurun_out/r4c_prof_gen.txt 2>&1
+head -16 gpurun_out/r4c_prof_gen.txt

@@ -67,6 +67,31 @@ def test_fused_add_layernorm():
     _close(w.grad, wr.grad, 1.0, 3e-2)
 
 
+@pytest.mark.parametrize("N,rows", [(1536, 333), (2048, 1), (2048, 3001)])
+def test_fused_add_layernorm_pair_backward(N, rows):
+    """1024 < N <= 2048: the two-waves-per-row backward (prefetched second row, uniform trip count
+    over odd row counts) against the fp32 reference, incl. the residual / x-bias gradients."""
+    from paddle_infer_amd.ops import fused_add_layer_norm
+    torch.manual_seed(N + rows)
+    x = torch.randn(rows, N, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    r = torch.randn_like(x, requires_grad=True)
+    xb = (0.1 * torch.randn(N, device=DEV)).bfloat16().requires_grad_()
+    w = (1 + 0.1 * torch.randn(N, device=DEV)).bfloat16().requires_grad_()
+    b = (0.1 * torch.randn(N, device=DEV)).bfloat16().requires_grad_()
+    y, h = fused_add_layer_norm(x, r, w, b, 1e-5, xb, 0.0)
+    dy, dh = torch.randn_like(y), torch.randn_like(h)
+    torch.autograd.backward([y, h], [dy, dh])
+    xr, rr, xbr, wr, br = (t.detach().float().requires_grad_() for t in (x, r, xb, w, b))
+    hr = rr + xr + xbr
+    yr = F.layer_norm(hr, (N,), wr, br, 1e-5)
+    torch.autograd.backward([yr, hr], [dy.float(), dh.float()])
+    _close(x.grad, xr.grad, 5e-2)
+    _close(r.grad, rr.grad, 5e-2)
+    _close(xb.grad, xbr.grad, 1.0, 3e-2)
+    _close(w.grad, wr.grad, 1.0, 3e-2)
+    _close(b.grad, br.grad, 1.0, 3e-2)
+
+
 def test_fused_add_layernorm_dropout_consistent():
     from paddle_infer_amd.ops import fused_add_layer_norm
     N = 1024

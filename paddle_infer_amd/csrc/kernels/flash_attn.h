@@ -45,6 +45,8 @@
 #pragma once
 #include "common.h"
 
+#include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 // C ABI argument block (ops/attention.py mirrors it as a ctypes.Structure).
@@ -481,6 +483,249 @@ __global__ __launch_bounds__(64 * NW, D > 128 ? 1 : 8 / NW) void fwd_kernel(FaAr
       }
     if (hh == 0 && a.lse)
       a.lse[lbase + qpos] = l_i > 0.f ? (m_i + log2f(l_i)) * kLn2 : INFINITY;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Persistent forward (padded layout, D <= 128, 4 waves): the grid is the resident workgroups
+// (2 per CU) and each walks a static list of (batch, head, query-block) items. The items of one
+// (batch, head) stay on one XCD (its K/V panel shared in that L2, as fa_map arranges for the
+// one-item kernel) and every XCD's list runs the heaviest causal blocks first. The K/V tiles form
+// ONE continuous sequence alternating between the two LDS buffers across item boundaries: the
+// next item's first tile is DMA'd during the current item's last tile, and its Q fragments load
+// right after the last S product — the prologue (Q fetch + first tile landing) of an item hides
+// under the previous one instead of idling the CU, which short causal sequences (S = 1024: 2-16
+// tiles per item) pay on every workgroup of the one-item kernel.
+// ------------------------------------------------------------------------------------------
+template <int D, bool F16, bool CAUSAL, int FEAT>
+__global__ __launch_bounds__(256, 2) void fwd_persist_kernel(FaArgs a) {
+  typedef ET<F16> E;
+  typedef typename E::V8 V8;
+  constexpr int DP = D > 64 ? 128 : 64;
+  constexpr int BM = 128, BN = 64;
+  constexpr int KSTEPS = D / 16;
+  constexpr int DT = D / 32;
+  constexpr int ROWB = DP * 2;
+  constexpr int TILE_B = BN * ROWB;
+  __shared__ __attribute__((aligned(16))) char kv0[2 * TILE_B];
+  __shared__ __attribute__((aligned(16))) char kv1[2 * TILE_B];
+
+  const unsigned short* q = (const unsigned short*)a.q;
+  const unsigned short* k = (const unsigned short*)a.k;
+  const unsigned short* v = (const unsigned short*)a.v;
+  unsigned short* o = (unsigned short*)a.o;
+  const int Sq = a.Sq, Sk = a.Sk, Hq = a.Hq, Hk = a.Hk;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int l32 = lane & 31, hh = lane >> 5;
+  const int nmb = (Sq + BM - 1) / BM;
+  const int ngroups = Hq * a.B;
+  // static schedule: this workgroup runs on XCD blockIdx % 8 (round-robin dispatch) as local
+  // worker blockIdx / 8 of gridDim / 8; XCD x owns the (batch, head) groups x, x + 8, ...
+  const int xcd = (int)blockIdx.x & 7, nl = (int)gridDim.x >> 3, li = (int)blockIdx.x >> 3;
+  const int gx = ngroups > xcd ? (ngroups - xcd + 7) / 8 : 0;
+  const int nitems = gx * nmb;  // item j = sub · gx + group slot (sub 0 = heaviest block first)
+  const int coff = Sk - Sq;
+  const float c = a.scale * kLog2e;
+  DropKey dk;
+  if (FEAT & F_DROP) dk = drop_key(a.p_drop, a.seed, a.offset);
+  const int sk_half = (a.Sk + 1) >> 1;
+
+  struct Item {
+    int b, hq, m0, ntiles;
+    const unsigned short *kb, *vb;
+  };
+  auto setup = [&](int j, Item& it) {
+    const int sub = j / gx, grp = xcd + 8 * (j - sub * gx);
+    const int mb = CAUSAL ? nmb - 1 - sub : sub;
+    it.hq = grp % Hq;
+    it.b = grp / Hq;
+    it.m0 = mb * BM;
+    const int hk = it.hq / (Hq / Hk);
+    it.kb = k + it.b * a.skb + hk * a.skh;
+    it.vb = v + it.b * a.svb + hk * a.svh;
+    int n_end = Sk;
+    if (CAUSAL) n_end = min(Sk, it.m0 + BM + coff);
+    // at least one (masked) tile: rows are clamped, so the DMA stays in bounds
+    it.ntiles = n_end <= 0 ? 1 : (n_end + BN - 1) / BN;
+  };
+  auto issue = [&](const Item& it, int t, auto bufc) {
+    char* ks = decltype(bufc)::value ? kv1 : kv0;
+    glds_tile<BN, ROWB, D / 8, 4>(it.kb, a.sks, t * BN, Sk - 1, ks, w, lane);
+    glds_tile<BN, ROWB, D / 8, 4>(it.vb, a.svs, t * BN, Sk - 1, ks + TILE_B, w, lane);
+  };
+  V8 qf[KSTEPS];
+  auto load_q = [&](const Item& it) {
+    const int qr = min(it.m0 + w * 32 + l32, Sq - 1);
+    const unsigned short* qp = q + it.b * a.sqb + (long long)qr * a.sqs + it.hq * a.sqh + 8 * hh;
+#pragma unroll
+    for (int kk = 0; kk < KSTEPS; ++kk) qf[kk] = *reinterpret_cast<const V8*>(qp + 16 * kk);
+  };
+
+  int j = li;
+  if (j >= nitems) return;
+  Item cur, nxt;
+  setup(j, cur);
+  bool has_next = j + nl < nitems;
+  if (has_next) setup(j + nl, nxt);
+  issue(cur, 0, std::integral_constant<int, 0>{});
+  load_q(cur);
+  __syncthreads();
+
+  LaneOffs<ROWB, KSTEPS, DT> L;
+  lane_offs(lane, L);
+  f32x16 oacc[DT];
+  float m_i, l_i;
+  auto reset = [&]() {
+#pragma unroll
+    for (int i = 0; i < DT; ++i)
+#pragma unroll
+      for (int jj = 0; jj < 16; ++jj) oacc[i][jj] = 0.f;
+    m_i = -INFINITY;
+    l_i = 0.f;
+  };
+  reset();
+  int t = 0;
+  bool done = false;
+
+  auto tile = [&](auto bufc) {
+    constexpr int BUF = decltype(bufc)::value;
+    constexpr int KS = 0, VS = TILE_B;
+    const char* smem = BUF ? kv1 : kv0;
+    const bool last = t + 1 == cur.ntiles;
+    if (!last) issue(cur, t + 1, std::integral_constant<int, BUF ^ 1>{});
+    else if (has_next) issue(nxt, 0, std::integral_constant<int, BUF ^ 1>{});
+    const int qrow0 = cur.m0 + w * 32, qpos = qrow0 + l32;
+    const int n0 = t * BN;
+    const bool active = qrow0 < Sq && (!CAUSAL || n0 <= qrow0 + 31 + coff) && n0 < Sk;
+    if (active) {
+      f32x16 sacc[2];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) sacc[tt][jj] = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < KSTEPS; ++kk)
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+          sacc[tt] = E::mfma(lds_at<F16>(smem, L.row[kk] + KS + tt * 32 * ROWB), qf[kk], sacc[tt]);
+      if (last && has_next) load_q(nxt);  // qf is dead for this item: the next item's Q lands under the softmax / PV
+      const int m_lim = min(CAUSAL ? qpos + coff + 1 : 0x40000000, Sk) - 4 * hh;
+      const bool need_mask = (n0 + BN > Sk) || (CAUSAL && n0 + BN - 1 > qrow0 + coff);
+      const unsigned short* mrow = nullptr;
+      if (FEAT & F_MASK)
+        mrow = (const unsigned short*)a.mask + cur.b * a.smb + cur.hq * a.smh + (long long)min(qpos, Sq - 1) * a.smq;
+      float mx = -INFINITY;
+      auto scale_mask = [&](auto maskc) {
+        constexpr bool MASKED = decltype(maskc)::value;
+        const int lim = m_lim - n0;
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+          for (int g4 = 0; g4 < 4; ++g4) {
+            f32x4 mb4 = {0.f, 0.f, 0.f, 0.f};
+            if (FEAT & F_MASK) mb4 = mask4<F16>(mrow, n0 + tt * 32 + 8 * g4 + 4 * hh, Sk);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int r = 4 * g4 + e;
+              float x = sacc[tt][r] * c + mb4[e];
+              if (MASKED) x = (tt * 32 + 8 * g4 + e) < lim ? x : -INFINITY;
+              sacc[tt][r] = x;
+              mx = fmaxf(mx, x);
+            }
+          }
+      };
+      if (need_mask) scale_mask(std::true_type{});
+      else scale_mask(std::false_type{});
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_i, mx);
+      const float msub = m_new == -INFINITY ? 0.f : m_new;
+      float rs = 0.f;
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = fast_exp2(sacc[tt][r] - msub);
+          sacc[tt][r] = p;
+          rs += p;
+        }
+      rs += __shfl_xor(rs, 32, 64);
+      if (FEAT & F_DROP) {
+        const long long lbase = ((long long)cur.b * Hq + cur.hq) * Sq;
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            const int key = n0 + tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            const uint32_t hsh = drop_hash(dk, lbase + qpos, sk_half, key);
+            if (!drop_keep(dk, hsh, key)) sacc[tt][r] = 0.f;
+            if (!drop_keep(dk, hsh, key + 1)) sacc[tt][r + 1] = 0.f;
+          }
+      }
+      if (__any(m_new > m_i)) {
+        const float alpha = fast_exp2(m_i - msub);
+        l_i *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+          for (int jj = 0; jj < 16; ++jj) oacc[dt][jj] *= alpha;
+      }
+      l_i += rs;
+      m_i = m_new;
+      V8 pf[4];
+#pragma unroll
+      for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) pf[2 * tt + s2] = E::frag(sacc[tt], s2);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int ks4 = 0; ks4 < 4; ++ks4) {
+          const int ro = VS + 16 * ks4 * ROWB;
+          oacc[dt] = E::mfma(cat44<F16>(lds_tr_at(smem, L.tr[0][dt] + ro), lds_tr_at(smem, L.tr[1][dt] + ro)),
+                             pf[ks4], oacc[dt]);
+        }
+    } else if (last && has_next) {
+      load_q(nxt);
+    }
+    __syncthreads();
+    if (!last) {
+      ++t;
+      return;
+    }
+    // item done: epilogue (lane = query row, registers = d), then switch to the next item
+    if (qpos < Sq) {
+      float inv = l_i > 0.f ? 1.f / l_i : 0.f;
+      if (FEAT & F_DROP) inv *= dk.inv;
+      unsigned short* op = o + cur.b * a.sob + (long long)qpos * a.sos + cur.hq * a.soh;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int d0 = 32 * dt + 8 * g4 + 4 * hh;
+          uint2 pk;
+          pk.x = pack2<F16>(oacc[dt][4 * g4 + 0] * inv, oacc[dt][4 * g4 + 1] * inv);
+          pk.y = pack2<F16>(oacc[dt][4 * g4 + 2] * inv, oacc[dt][4 * g4 + 3] * inv);
+          *reinterpret_cast<uint2*>(op + d0) = pk;
+        }
+      if (hh == 0 && a.lse)
+        a.lse[((long long)cur.b * Hq + cur.hq) * Sq + qpos] = l_i > 0.f ? (m_i + log2f(l_i)) * kLn2 : INFINITY;
+    }
+    if (!has_next) {
+      done = true;
+      return;
+    }
+    j += nl;
+    cur = nxt;
+    has_next = j + nl < nitems;
+    if (has_next) setup(j + nl, nxt);
+    t = 0;
+    reset();
+  };
+  while (true) {
+    tile(std::integral_constant<int, 0>{});
+    if (done) break;
+    tile(std::integral_constant<int, 1>{});
+    if (done) break;
   }
 }
 
@@ -1153,10 +1398,37 @@ int launch_fwd_nw(const FaArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+// persistent forward: PIAMD_FA_PERSIST (1 = on, default; 0 = the one-item-per-workgroup grid)
+inline bool fwd_persist() {
+  static const bool on = [] {
+    const char* e = getenv("PIAMD_FA_PERSIST");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+template <bool F16, int D, bool C>
+int launch_fwd_persist(const FaArgs& a, hipStream_t st) {
+  const long long items = (long long)((a.Sq + 127) / 128) * a.Hq * a.B;
+  // 2 resident workgroups per CU on 256 CUs; a multiple of 8 (one worker list per XCD)
+  const unsigned grid = (unsigned)std::min<long long>(512, (items + 7) / 8 * 8);
+  const int feat = (a.p_drop > 0.f ? F_DROP : 0) | (a.mask ? F_MASK : 0);
+  switch (feat) {
+    case 0: hipLaunchKernelGGL((fwd_persist_kernel<D, F16, C, 0>), dim3(grid), dim3(256), 0, st, a); break;
+    case 1: hipLaunchKernelGGL((fwd_persist_kernel<D, F16, C, 1>), dim3(grid), dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((fwd_persist_kernel<D, F16, C, 2>), dim3(grid), dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL((fwd_persist_kernel<D, F16, C, 3>), dim3(grid), dim3(256), 0, st, a); break;
+  }
+  return (int)hipGetLastError();
+}
+
 template <bool F16, int D, bool C>
 int launch_fwd_feat(const FaArgs& a, dim3 /*grid*/, hipStream_t st) {
   if constexpr (D > 128) return launch_fwd_nw<F16, D, C, 4>(a, st);
-  else return fwd_waves() == 8 ? launch_fwd_nw<F16, D, C, 8>(a, st) : launch_fwd_nw<F16, D, C, 4>(a, st);
+  else {
+    if (!a.cu_q && fwd_persist() && fwd_waves() == 4) return launch_fwd_persist<F16, D, C>(a, st);
+    return fwd_waves() == 8 ? launch_fwd_nw<F16, D, C, 8>(a, st) : launch_fwd_nw<F16, D, C, 4>(a, st);
+  }
 }
 
 template <bool F16>

@@ -16,10 +16,11 @@ timeout -k 10 300 $T tests/test_kernels_gpu.py tests/test_norm_gpu.py > gpurun_o
 tail -1 gpurun_out/r4c_ln_tests.log
 for P in 0 1; do PIAMD_LN_BWD_PAIR=$P timeout -k 10 120 python tools/bench_ln_bwd.py; done
 S="96,1024,16,128;8,2048,16,128;4,4096,16,128;16,1024,32,64"
-for MB in 0 8192; do
-  echo "== PIAMD_FA_DS_MAX_MB=$MB"
-  PIAMD_FA_DS_MAX_MB=$MB timeout -k 10 300 python tools/bench_attn.py --no-sdpa --shapes "$S" > gpurun_out/r4c_attn_bench_$MB.log 2>&1 || { tail -20 gpurun_out/r4c_attn_bench_$MB.log; exit 1; }
-  grep "^{" gpurun_out/r4c_attn_bench_$MB.log | cut -c1-220
+for CFG in "0 0" "8192 0" "8192 1"; do
+  set -- $CFG
+  echo "== PIAMD_FA_DS_MAX_MB=$1 PIAMD_FA_PERSIST=$2"
+  PIAMD_FA_DS_MAX_MB=$1 PIAMD_FA_PERSIST=$2 timeout -k 10 300 python tools/bench_attn.py --no-sdpa --shapes "$S" > gpurun_out/r4c_attn_bench_$1_$2.log 2>&1 || { tail -20 gpurun_out/r4c_attn_bench_$1_$2.log; exit 1; }
+  grep "^{" gpurun_out/r4c_attn_bench_$1_$2.log | cut -c1-220
 done
 for M in resnet50 mobilenet_v2; do
   timeout -k 10 300 python tools/bench_resnet.py --model $M --steps 10 > gpurun_out/r4c_cn_$M.log 2>&1 || { tail -20 gpurun_out/r4c_cn_$M.log; exit 1; }

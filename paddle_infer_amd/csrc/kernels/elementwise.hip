@@ -1,5 +1,5 @@
 // Fused elementwise kernels: bias+activation (fwd/bwd with fused bias-grad column sums),
-// dropout, masked softmax.
+// dropout, masked softmax — bf16, fp16 and f32 (Paddle's default dtype) element types.
 //
 // Parity: reference `paddle/fluid/operators/fused/fused_dropout_act_bias.h`
 // (fused_bias_act / FusedFeedForward's `dropout(act(x + bias))`), `phi/kernels/gpu/gelu_*`,
@@ -33,13 +33,63 @@ __device__ __forceinline__ float act_g(float x) {
   return 1.f;
 }
 
-// y = act(x + bias) (bias optional, broadcast over rows of length N); bf16 / fp16; N % 8 == 0.
-template <int ACT, bool F16>
-__global__ __launch_bounds__(256) void bias_act_fwd_kernel(const bf16_t* __restrict__ x,
-                                                          const bf16_t* __restrict__ bias,
-                                                          bf16_t* __restrict__ y,
-                                                          bf16_t* __restrict__ pre, long long n8,
+// 8-element vectors of the element type DT (0 bf16, 1 fp16: one 16-B access; 2 f32: two), f32 math
+enum { DT_BF16 = 0, DT_F16 = 1, DT_F32 = 2 };
+template <int DT>
+struct IO8 {
+  typedef u16x8 R;
+  static __device__ __forceinline__ R ld(const void* p, long long i) { return reinterpret_cast<const u16x8*>(p)[i]; }
+  static __device__ __forceinline__ R ldnt(const void* p, long long i) {
+    return __builtin_nontemporal_load(&reinterpret_cast<const u16x8*>(p)[i]);
+  }
+  static __device__ __forceinline__ float get(const R& r, int j) { return h2f<DT == DT_F16>(r[j]); }
+  static __device__ __forceinline__ R pack(const float* v) {
+    R r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = f2h<DT == DT_F16>(v[j]);
+    return r;
+  }
+  static __device__ __forceinline__ void st(void* p, long long i, const float* v) { reinterpret_cast<u16x8*>(p)[i] = pack(v); }
+  static __device__ __forceinline__ void stnt(void* p, long long i, const float* v) {
+    __builtin_nontemporal_store(pack(v), &reinterpret_cast<u16x8*>(p)[i]);
+  }
+  static __device__ __forceinline__ float ld1(const void* p, long long i) { return h2f<DT == DT_F16>(reinterpret_cast<const unsigned short*>(p)[i]); }
+  static __device__ __forceinline__ void st1(void* p, long long i, float v) { reinterpret_cast<unsigned short*>(p)[i] = f2h<DT == DT_F16>(v); }
+};
+template <>
+struct IO8<DT_F32> {
+  struct R { f32x4 a, b; };
+  static __device__ __forceinline__ R ld(const void* p, long long i) {
+    const f32x4* q = reinterpret_cast<const f32x4*>(p) + 2 * i;
+    return R{q[0], q[1]};
+  }
+  static __device__ __forceinline__ R ldnt(const void* p, long long i) {
+    const f32x4* q = reinterpret_cast<const f32x4*>(p) + 2 * i;
+    return R{__builtin_nontemporal_load(q), __builtin_nontemporal_load(q + 1)};
+  }
+  static __device__ __forceinline__ float get(const R& r, int j) { return j < 4 ? r.a[j] : r.b[j - 4]; }
+  static __device__ __forceinline__ void st(void* p, long long i, const float* v) {
+    f32x4* q = reinterpret_cast<f32x4*>(p) + 2 * i;
+    q[0] = f32x4{v[0], v[1], v[2], v[3]};
+    q[1] = f32x4{v[4], v[5], v[6], v[7]};
+  }
+  static __device__ __forceinline__ void stnt(void* p, long long i, const float* v) {
+    f32x4* q = reinterpret_cast<f32x4*>(p) + 2 * i;
+    __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, q);
+    __builtin_nontemporal_store(f32x4{v[4], v[5], v[6], v[7]}, q + 1);
+  }
+  static __device__ __forceinline__ float ld1(const void* p, long long i) { return reinterpret_cast<const float*>(p)[i]; }
+  static __device__ __forceinline__ void st1(void* p, long long i, float v) { reinterpret_cast<float*>(p)[i] = v; }
+};
+
+// y = act(x + bias) (bias optional, broadcast over rows of length N); bf16 / fp16 / f32; N % 8 == 0.
+template <int ACT, int DT>
+__global__ __launch_bounds__(256) void bias_act_fwd_kernel(const void* __restrict__ x,
+                                                          const void* __restrict__ bias,
+                                                          void* __restrict__ y,
+                                                          void* __restrict__ pre, long long n8,
                                                           int N) {
+  typedef IO8<DT> io;
   // 4 independent 16-B loads in flight per thread before any math (latency hiding at
   // grid-stride; the memory pipe, not the ALU, bounds this kernel)
   constexpr int U = 4;
@@ -51,13 +101,13 @@ __global__ __launch_bounds__(256) void bias_act_fwd_kernel(const bf16_t* __restr
   const int step1 = (int)(stride % nb8), stepU = (int)((U * stride) % nb8);
   int c0 = (int)(first % nb8);
   for (long long i0 = first; i0 < n8; i0 += U * stride) {
-    u16x8 r[U], b[U];
+    typename io::R r[U], b[U];
     int c = c0;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long long i = min(i0 + u * stride, n8 - 1);
-      r[u] = __builtin_nontemporal_load(&reinterpret_cast<const u16x8*>(x)[i]);
-      if (bias) b[u] = reinterpret_cast<const u16x8*>(bias)[c];
+      r[u] = io::ldnt(x, i);
+      if (bias) b[u] = io::ld(bias, c);
       c += step1;
       c -= c >= nb8 ? nb8 : 0;
     }
@@ -67,60 +117,61 @@ __global__ __launch_bounds__(256) void bias_act_fwd_kernel(const bf16_t* __restr
     for (int u = 0; u < U; ++u) {
       const long long i = i0 + u * stride;
       if (i >= n8) break;
-      u16x8 o, pr;
+      float o[8], pr[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float v = h2f<F16>(r[u][j]);
-        if (bias) v += h2f<F16>(b[u][j]);
-        pr[j] = f2h<F16>(v);
-        o[j] = f2h<F16>(act_f<ACT>(v));
+        float v = io::get(r[u], j);
+        if (bias) v += io::get(b[u], j);
+        pr[j] = v;
+        o[j] = act_f<ACT>(v);
       }
-      if (pre) reinterpret_cast<u16x8*>(pre)[i] = pr;
-      __builtin_nontemporal_store(o, &reinterpret_cast<u16x8*>(y)[i]);  // streamed: no L2 reuse
+      if (pre) io::st(pre, i, pr);
+      io::stnt(y, i, o);  // streamed: no L2 reuse
     }
   }
 }
 
 // dx = dy * act'(h) with h = pre-activation (x + bias); dbias partials. grid = (G, ceil(N/2048)).
-template <int ACT, bool F16>
-__global__ __launch_bounds__(256) void bias_act_bwd_kernel(const bf16_t* __restrict__ dy,
-                                                          const bf16_t* __restrict__ h,
-                                                          const bf16_t* __restrict__ bias,
-                                                          bf16_t* __restrict__ dx,
+template <int ACT, int DT>
+__global__ __launch_bounds__(256) void bias_act_bwd_kernel(const void* __restrict__ dy,
+                                                          const void* __restrict__ h,
+                                                          const void* __restrict__ bias,
+                                                          void* __restrict__ dx,
                                                           float* __restrict__ part, int rows,
                                                           int N) {
+  typedef IO8<DT> io;
   const int c8 = blockIdx.y * 256 + threadIdx.x;  // 8-column group index
   const bool colok = c8 * 8 < N;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  u16x8 b;
-  if (bias && colok) b = reinterpret_cast<const u16x8*>(bias)[c8];
+  typename io::R b;
+  if (bias && colok) b = io::ld(bias, c8);
   constexpr int U = 4;  // rows in flight per thread
   for (int r0 = blockIdx.x; colok && r0 < rows; r0 += U * gridDim.x) {
-    u16x8 d[U], hv[U];
+    typename io::R d[U], hv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int r = min(r0 + u * (int)gridDim.x, rows - 1);
-      const size_t idx = ((size_t)r * N >> 3) + c8;
+      const long long idx = ((long long)r * N >> 3) + c8;
       // nontemporal (streaming) loads / stores: the [tokens x 4h] tensors are read once and never
       // hit in L2 — 5.19 -> 5.50 TB/s backward, 4.28 -> 4.57 forward (profiles/nt_stream_r2.txt)
-      d[u] = __builtin_nontemporal_load(&reinterpret_cast<const u16x8*>(dy)[idx]);
-      hv[u] = __builtin_nontemporal_load(&reinterpret_cast<const u16x8*>(h)[idx]);
+      d[u] = io::ldnt(dy, idx);
+      hv[u] = io::ldnt(h, idx);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int r = r0 + u * (int)gridDim.x;
       if (r >= rows) break;
-      const size_t idx = ((size_t)r * N >> 3) + c8;
-      u16x8 o;
+      const long long idx = ((long long)r * N >> 3) + c8;
+      float o[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float hh = h2f<F16>(hv[u][j]);
-        if (bias) hh += h2f<F16>(b[j]);
-        float g = h2f<F16>(d[u][j]) * act_g<ACT>(hh);
-        o[j] = f2h<F16>(g);
+        float hh = io::get(hv[u], j);
+        if (bias) hh += io::get(b, j);
+        const float g = io::get(d[u], j) * act_g<ACT>(hh);
+        o[j] = g;
         acc[j] += g;
       }
-      __builtin_nontemporal_store(o, &reinterpret_cast<u16x8*>(dx)[idx]);
+      io::stnt(dx, idx, o);
     }
   }
   if (part) {
@@ -139,9 +190,9 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const bf16_t* __restr
   }
 }
 
-template <bool F16>
+template <int DT>
 __global__ __launch_bounds__(256) void colsum16_kernel(const float* __restrict__ part, int G,
-                                                         int N, bf16_t* __restrict__ out,
+                                                         int N, void* __restrict__ out,
                                                          int accumulate) {
   const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + cl;
@@ -153,20 +204,21 @@ __global__ __launch_bounds__(256) void colsum16_kernel(const float* __restrict__
   __syncthreads();
   if (rg == 0 && col < N) {
     float t = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
-    if (accumulate) t += h2f<F16>(out[col]);
-    out[col] = f2h<F16>(t);
+    if (accumulate) t += IO8<DT>::ld1(out, col);
+    IO8<DT>::st1(out, col, t);
   }
 }
 
 // Row softmax with optional additive mask (broadcast over rows: mask row index = row % mask_rows)
 // and optional causal (upper-triangle) masking with query position = row % causal_q. One wave
 // per row for N <= 4096 (row in registers), bf16 / fp16 in/out.
-template <int NV, bool F16>
-__global__ __launch_bounds__(256) void softmax_fwd_kernel(const bf16_t* __restrict__ x,
-                                                         const bf16_t* __restrict__ mask,
+template <int NV, int DT>
+__global__ __launch_bounds__(256) void softmax_fwd_kernel(const void* __restrict__ x,
+                                                         const void* __restrict__ mask,
                                                          int mask_rows, int causal_q,
-                                                         bf16_t* __restrict__ y, int rows, int N,
+                                                         void* __restrict__ y, int rows, int N,
                                                          float scale) {
+  typedef IO8<DT> io;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -179,13 +231,13 @@ __global__ __launch_bounds__(256) void softmax_fwd_kernel(const bf16_t* __restri
   for (int i = 0; i < NV; ++i) {
     const int vi = i * 64 + lane;
     if (vi < nvec) {
-      u16x8 r = reinterpret_cast<const u16x8*>(x + base)[vi];
-      u16x8 mk;
-      if (mask) mk = reinterpret_cast<const u16x8*>(mask + (size_t)(row % mask_rows) * N)[vi];
+      const typename io::R r = io::ld(x, (long long)(base >> 3) + vi);
+      typename io::R mk;
+      if (mask) mk = io::ld(mask, (long long)(row % mask_rows) * (N >> 3) + vi);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float t = h2f<F16>(r[j]) * scale;
-        if (mask) t += h2f<F16>(mk[j]);
+        float t = io::get(r, j) * scale;
+        if (mask) t += io::get(mk, j);
         if (vi * 8 + j > qpos) t = -INFINITY;
         v[i][j] = t;
         m = fmaxf(m, t);
@@ -211,20 +263,21 @@ __global__ __launch_bounds__(256) void softmax_fwd_kernel(const bf16_t* __restri
   for (int i = 0; i < NV; ++i) {
     const int vi = i * 64 + lane;
     if (vi < nvec) {
-      u16x8 o;
+      float o[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = f2h<F16>(v[i][j] * inv);
-      reinterpret_cast<u16x8*>(y + base)[vi] = o;
+      for (int j = 0; j < 8; ++j) o[j] = v[i][j] * inv;
+      io::st(y, (long long)(base >> 3) + vi, o);
     }
   }
 }
 
 // dx = scale * y * (dy - sum(dy * y))
-template <int NV, bool F16>
-__global__ __launch_bounds__(256) void softmax_bwd_kernel(const bf16_t* __restrict__ y,
-                                                         const bf16_t* __restrict__ dy,
-                                                         bf16_t* __restrict__ dx, int rows, int N,
+template <int NV, int DT>
+__global__ __launch_bounds__(256) void softmax_bwd_kernel(const void* __restrict__ y,
+                                                         const void* __restrict__ dy,
+                                                         void* __restrict__ dx, int rows, int N,
                                                          float scale) {
+  typedef IO8<DT> io;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -236,10 +289,10 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(const bf16_t* __restri
   for (int i = 0; i < NV; ++i) {
     const int vi = i * 64 + lane;
     if (vi < nvec) {
-      u16x8 a = reinterpret_cast<const u16x8*>(y + base)[vi];
-      u16x8 b = reinterpret_cast<const u16x8*>(dy + base)[vi];
+      const typename io::R a = io::ld(y, (long long)(base >> 3) + vi);
+      const typename io::R b = io::ld(dy, (long long)(base >> 3) + vi);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { yv[i][j] = h2f<F16>(a[j]); dv[i][j] = h2f<F16>(b[j]); s += yv[i][j] * dv[i][j]; }
+      for (int j = 0; j < 8; ++j) { yv[i][j] = io::get(a, j); dv[i][j] = io::get(b, j); s += yv[i][j] * dv[i][j]; }
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) { yv[i][j] = 0.f; dv[i][j] = 0.f; }
@@ -250,47 +303,53 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(const bf16_t* __restri
   for (int i = 0; i < NV; ++i) {
     const int vi = i * 64 + lane;
     if (vi < nvec) {
-      u16x8 o;
+      float o[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = f2h<F16>(scale * yv[i][j] * (dv[i][j] - s));
-      reinterpret_cast<u16x8*>(dx + base)[vi] = o;
+      for (int j = 0; j < 8; ++j) o[j] = scale * yv[i][j] * (dv[i][j] - s);
+      io::st(dx, (long long)(base >> 3) + vi, o);
     }
   }
 }
 
 // Dropout with stateless hash mask (mask regenerated in backward from seed/offset).
-template <bool F16>
-__global__ __launch_bounds__(256) void dropout_kernel(const bf16_t* __restrict__ x,
-                                                     bf16_t* __restrict__ y, long long n8, float p,
+template <int DT>
+__global__ __launch_bounds__(256) void dropout_kernel(const void* __restrict__ x,
+                                                     void* __restrict__ y, long long n8, float p,
                                                      uint64_t seed, uint64_t offset) {
+  typedef IO8<DT> io;
   const float ks = 1.f / (1.f - p);
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
-    u16x8 r = reinterpret_cast<const u16x8*>(x)[i], o;
-    float u[8];
+    const typename io::R r = io::ld(x, i);
+    float u[8], o[8];
     hash_uniform8(seed, offset, (uint64_t)i * 8, u);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      o[j] = f2h<F16>(u[j] >= p ? h2f<F16>(r[j]) * ks : 0.f);
-    }
-    reinterpret_cast<u16x8*>(y)[i] = o;
+    for (int j = 0; j < 8; ++j) o[j] = u[j] >= p ? io::get(r, j) * ks : 0.f;
+    io::st(y, i, o);
   }
 }
 
 }  // namespace
 
-PIAMD_EXPORT int piamd_bias_act_fwd(int f16, int act, const void* x, const void* bias, void* y, void* pre,
+// dtype codes of the entry points below: 0 bf16, 1 fp16, 2 f32 (the fp16 flag of older callers)
+#define DT_SWITCH(dt, CALL)                                     \
+  switch (dt) {                                                 \
+    case DT_BF16: { constexpr int D_ = DT_BF16; CALL; } break;  \
+    case DT_F16: { constexpr int D_ = DT_F16; CALL; } break;    \
+    case DT_F32: { constexpr int D_ = DT_F32; CALL; } break;    \
+    default: return (int)hipErrorInvalidValue;                  \
+  }
+
+PIAMD_EXPORT int piamd_bias_act_fwd(int dt, int act, const void* x, const void* bias, void* y, void* pre,
                                     long long n, int N, hipStream_t stream) {
   if (n == 0) return 0;
   if (n % 8 || N % 8) return (int)hipErrorInvalidValue;
   const long long n8 = n / 8;
   const int grid = stride_grid(n8, 256);
-#define BAF(A)                                                                                  \
-  case A:                                                                                       \
-    if (f16) hipLaunchKernelGGL((bias_act_fwd_kernel<A, true>), dim3(grid), dim3(256), 0, stream, \
-                       (const bf16_t*)x, (const bf16_t*)bias, (bf16_t*)y, (bf16_t*)pre, n8, N); \
-    else hipLaunchKernelGGL((bias_act_fwd_kernel<A, false>), dim3(grid), dim3(256), 0, stream, \
-                       (const bf16_t*)x, (const bf16_t*)bias, (bf16_t*)y, (bf16_t*)pre, n8, N); \
+#define BAF(A)                                                                                     \
+  case A:                                                                                          \
+    DT_SWITCH(dt, hipLaunchKernelGGL((bias_act_fwd_kernel<A, D_>), dim3(grid), dim3(256), 0, stream, \
+                                     x, bias, y, pre, n8, N));                                     \
     break;
   switch (act) { BAF(0) BAF(1) BAF(2) BAF(3) BAF(4) default: return (int)hipErrorInvalidValue; }
 #undef BAF
@@ -302,38 +361,29 @@ PIAMD_EXPORT int piamd_bias_act_bwd_grid(int rows) {
   return g < 1 ? 1 : g;
 }
 
-// part: f32 [N] workspace (zeroed here) — needed when dbias != null.
-PIAMD_EXPORT int piamd_bias_act_bwd(int f16, int act, const void* dy, const void* h, const void* bias,
+// part: f32 [N] workspace (zeroed here) — needed when dbias != null. dbias in the element type.
+PIAMD_EXPORT int piamd_bias_act_bwd(int dt, int act, const void* dy, const void* h, const void* bias,
                                     void* dx, void* dbias, float* part, int rows, int N,
                                     int accumulate, hipStream_t stream) {
   if (rows == 0) return 0;
   if (N % 8) return (int)hipErrorInvalidValue;
   const int G = piamd_bias_act_bwd_grid(rows);
   dim3 grid(G, (N / 8 + 255) / 256);
-#define BAB(A)                                                                                  \
-  case A:                                                                                       \
-    if (f16) hipLaunchKernelGGL((bias_act_bwd_kernel<A, true>), grid, dim3(256), 0, stream,     \
-                       (const bf16_t*)dy, (const bf16_t*)h, (const bf16_t*)bias, (bf16_t*)dx,  \
-                       dbias ? part : nullptr, rows, N);                                        \
-    else hipLaunchKernelGGL((bias_act_bwd_kernel<A, false>), grid, dim3(256), 0, stream,        \
-                       (const bf16_t*)dy, (const bf16_t*)h, (const bf16_t*)bias, (bf16_t*)dx,  \
-                       dbias ? part : nullptr, rows, N);                                        \
+#define BAB(A)                                                                                   \
+  case A:                                                                                        \
+    DT_SWITCH(dt, hipLaunchKernelGGL((bias_act_bwd_kernel<A, D_>), grid, dim3(256), 0, stream,  \
+                                     dy, h, bias, dx, dbias ? part : nullptr, rows, N));         \
     break;
   if (dbias) (void)hipMemsetAsync(part, 0, sizeof(float) * N, stream);
   switch (act) { BAB(0) BAB(1) BAB(2) BAB(3) BAB(4) default: return (int)hipErrorInvalidValue; }
 #undef BAB
-  if (dbias) {
-    if (f16)
-      hipLaunchKernelGGL((colsum16_kernel<true>), dim3((N + 63) / 64), dim3(256), 0, stream, part, 1,
-                         N, (bf16_t*)dbias, accumulate);
-    else
-      hipLaunchKernelGGL((colsum16_kernel<false>), dim3((N + 63) / 64), dim3(256), 0, stream, part,
-                         1, N, (bf16_t*)dbias, accumulate);
-  }
+  if (dbias)
+    DT_SWITCH(dt, hipLaunchKernelGGL((colsum16_kernel<D_>), dim3((N + 63) / 64), dim3(256), 0, stream, part, 1,
+                                     N, dbias, accumulate));
   return (int)hipGetLastError();
 }
 
-PIAMD_EXPORT int piamd_softmax_fwd(int f16, const void* x, const void* mask, int mask_rows, int causal_q,
+PIAMD_EXPORT int piamd_softmax_fwd(int dt, const void* x, const void* mask, int mask_rows, int causal_q,
                                    void* y, int rows, int N, float scale, hipStream_t stream) {
   if (rows == 0) return 0;
   if (N % 8 || N > 4096) return (int)hipErrorInvalidValue;
@@ -341,12 +391,8 @@ PIAMD_EXPORT int piamd_softmax_fwd(int f16, const void* x, const void* mask, int
   dim3 grid((rows + 3) / 4);
 #define SMF(NVV, REAL)                                                                           \
   case REAL:                                                                                     \
-    if (f16) hipLaunchKernelGGL((softmax_fwd_kernel<NVV, true>), grid, dim3(256), 0, stream,    \
-                       (const bf16_t*)x, (const bf16_t*)mask, mask_rows > 0 ? mask_rows : 1,    \
-                       causal_q, (bf16_t*)y, rows, N, scale);                                   \
-    else hipLaunchKernelGGL((softmax_fwd_kernel<NVV, false>), grid, dim3(256), 0, stream,       \
-                       (const bf16_t*)x, (const bf16_t*)mask, mask_rows > 0 ? mask_rows : 1,    \
-                       causal_q, (bf16_t*)y, rows, N, scale);                                   \
+    DT_SWITCH(dt, hipLaunchKernelGGL((softmax_fwd_kernel<NVV, D_>), grid, dim3(256), 0, stream, \
+                                     x, mask, mask_rows > 0 ? mask_rows : 1, causal_q, y, rows, N, scale)); \
     break;
   switch (nv) { SMF(1, 1) SMF(2, 2) SMF(4, 3) SMF(4, 4) SMF(8, 5) SMF(8, 6) SMF(8, 7) SMF(8, 8)
     default: return (int)hipErrorInvalidValue; }
@@ -354,7 +400,7 @@ PIAMD_EXPORT int piamd_softmax_fwd(int f16, const void* x, const void* mask, int
   return (int)hipGetLastError();
 }
 
-PIAMD_EXPORT int piamd_softmax_bwd(int f16, const void* y, const void* dy, void* dx, int rows, int N,
+PIAMD_EXPORT int piamd_softmax_bwd(int dt, const void* y, const void* dy, void* dx, int rows, int N,
                                    float scale, hipStream_t stream) {
   if (rows == 0) return 0;
   if (N % 8 || N > 4096) return (int)hipErrorInvalidValue;
@@ -362,10 +408,8 @@ PIAMD_EXPORT int piamd_softmax_bwd(int f16, const void* y, const void* dy, void*
   dim3 grid((rows + 3) / 4);
 #define SMB(NVV, REAL)                                                                           \
   case REAL:                                                                                     \
-    if (f16) hipLaunchKernelGGL((softmax_bwd_kernel<NVV, true>), grid, dim3(256), 0, stream,    \
-                       (const bf16_t*)y, (const bf16_t*)dy, (bf16_t*)dx, rows, N, scale);       \
-    else hipLaunchKernelGGL((softmax_bwd_kernel<NVV, false>), grid, dim3(256), 0, stream,       \
-                       (const bf16_t*)y, (const bf16_t*)dy, (bf16_t*)dx, rows, N, scale);       \
+    DT_SWITCH(dt, hipLaunchKernelGGL((softmax_bwd_kernel<NVV, D_>), grid, dim3(256), 0, stream, \
+                                     y, dy, dx, rows, N, scale));                                \
     break;
   switch (nv) { SMB(1, 1) SMB(2, 2) SMB(4, 3) SMB(4, 4) SMB(8, 5) SMB(8, 6) SMB(8, 7) SMB(8, 8)
     default: return (int)hipErrorInvalidValue; }
@@ -373,19 +417,16 @@ PIAMD_EXPORT int piamd_softmax_bwd(int f16, const void* y, const void* dy, void*
   return (int)hipGetLastError();
 }
 
-PIAMD_EXPORT int piamd_dropout(int f16, const void* x, void* y, long long n, float p, uint64_t seed,
+PIAMD_EXPORT int piamd_dropout(int dt, const void* x, void* y, long long n, float p, uint64_t seed,
                                uint64_t offset, hipStream_t stream) {
   if (n == 0) return 0;
   if (n % 8) return (int)hipErrorInvalidValue;
   const int grid = stride_grid(n / 8, 256);
-  if (f16)
-    hipLaunchKernelGGL((dropout_kernel<true>), dim3(grid), dim3(256), 0, stream, (const bf16_t*)x,
-                       (bf16_t*)y, n / 8, p, seed, offset);
-  else
-    hipLaunchKernelGGL((dropout_kernel<false>), dim3(grid), dim3(256), 0, stream, (const bf16_t*)x,
-                       (bf16_t*)y, n / 8, p, seed, offset);
+  DT_SWITCH(dt, hipLaunchKernelGGL((dropout_kernel<D_>), dim3(grid), dim3(256), 0, stream, x, y, n / 8, p, seed,
+                                   offset));
   return (int)hipGetLastError();
 }
+#undef DT_SWITCH
 
 // ---------------------------------------------------------------------------------------------
 // 2-D bf16 transpose dst[C][R] = src[R][C] (weight re-layout for the K-contiguous forward GEMM).

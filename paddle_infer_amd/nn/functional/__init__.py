@@ -54,8 +54,10 @@ swish = silu
 def softmax(x, axis=-1, dtype=None, name=None):
     if dtype is not None:
         x = x.to(_dt(dtype))
-    if axis in (-1, x.dim() - 1) and x.is_cuda and x.dtype in (torch.bfloat16, torch.float16):
-        return _ops.fused_softmax_mask(x)
+    if axis in (-1, x.dim() - 1) and x.is_cuda:
+        if x.dtype in (torch.bfloat16, torch.float16) or (
+                x.dtype == torch.float32 and x.shape[-1] % 8 == 0 and x.shape[-1] <= 4096):
+            return _ops.fused_softmax_mask(x)
     return torch.softmax(x, axis)
 
 

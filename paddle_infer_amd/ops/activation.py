@@ -13,10 +13,12 @@ from . import _lib
 from ..framework import random as _random
 
 _H16 = (torch.bfloat16, torch.float16)
+_KDT = {torch.bfloat16: 0, torch.float16: 1, torch.float32: 2}  # element types of the HIP kernels
 
 
 def _f16(t) -> int:
-    return int(t.dtype == torch.float16)
+    """dtype code of elementwise.hip's entry points: 0 bf16, 1 fp16, 2 f32."""
+    return _KDT[t.dtype]
 
 
 ACTS = {"none": 0, "identity": 0, "gelu_tanh": 1, "gelu": 2, "relu": 3, "silu": 4, "swish": 4}
@@ -81,10 +83,10 @@ def bias_act(x, bias=None, act: str = "gelu"):
     a = ACTS[act]
     N = x.shape[-1]
     if x.is_cuda:
-        if x.dtype in _H16 and N % 8 == 0:
+        if x.dtype in _KDT and N % 8 == 0:
             b = bias if bias is None or bias.dtype == x.dtype else bias.to(x.dtype)
             return _BiasActFn.apply(x, b, a)
-        _lib.fallback("bias_act", f"dtype {x.dtype} / N {N} (kernel: bf16/fp16, N % 8 == 0)")
+        _lib.fallback("bias_act", f"dtype {x.dtype} / N {N} (kernel: bf16/fp16/f32, N % 8 == 0)")
     return _ref_act(x if bias is None else x + bias, a)
 
 
@@ -116,10 +118,10 @@ def dropout(x, p: float = 0.5, training: bool = True):
     if not training or p == 0.0:
         return x
     if x.is_cuda:
-        if x.dtype in _H16 and x.numel() % 8 == 0:
+        if x.dtype in _KDT and x.numel() % 8 == 0:
             seed, offset = _random.next_seed_offset(x.numel())
             return _DropoutFn.apply(x, p, seed, offset)
-        _lib.fallback("dropout", f"dtype {x.dtype} / numel % 8 (kernel: bf16/fp16)")
+        _lib.fallback("dropout", f"dtype {x.dtype} / numel % 8 (kernel: bf16/fp16/f32)")
     return F.dropout(x, p, training=True)
 
 
@@ -156,7 +158,7 @@ def fused_softmax_mask(x, mask=None, scale: float = 1.0, causal: bool = False):
     reference's ``fused_softmax_mask_upper_triangle``). mask broadcasts over leading rows."""
     N = x.shape[-1]
     if x.is_cuda:
-        if x.dtype in _H16 and N % 8 == 0 and N <= 4096 and \
+        if x.dtype in _KDT and N % 8 == 0 and N <= 4096 and \
                 (mask is None or x.numel() % mask.numel() == 0):
             cq = x.shape[-2] if causal else 0
             m = mask if mask is None or mask.dtype == x.dtype else mask.to(x.dtype)

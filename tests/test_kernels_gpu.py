@@ -284,3 +284,48 @@ def test_gpt_recompute_with_kernel_dropout_matches_plain():
     assert torch.allclose(l0, l1)
     for n in g0:
         _close(g1[n], g0[n], 1e-3)
+
+
+@pytest.mark.parametrize("act", ["gelu", "gelu_tanh", "relu", "silu"])
+def test_fp32_bias_act_on_kernel(act):
+    """fp32 (Paddle's default dtype) bias + activation on the elementwise HIP kernel, forward and
+    backward with the fused bias-gradient column sums, against PyTorch fp32 — no fallback."""
+    from paddle_infer_amd.ops import _lib, bias_act
+    _lib.FALLBACKS.clear()
+    torch.manual_seed(3)
+    x = torch.randn(333, 264, device=DEV, requires_grad=True)
+    b = torch.randn(264, device=DEV, requires_grad=True)
+    y = bias_act(x, b, act)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr, br = x.detach().clone().requires_grad_(), b.detach().clone().requires_grad_()
+    ref = {"gelu": lambda t: F.gelu(t), "gelu_tanh": lambda t: F.gelu(t, approximate="tanh"),
+           "relu": F.relu, "silu": F.silu}[act](xr + br)
+    ref.backward(dy)
+    _close(y, ref, 2e-5, 1e-5)
+    _close(x.grad, xr.grad, 2e-5, 1e-5)
+    _close(b.grad, br.grad, 2e-4, 1e-5)
+    assert not _lib.FALLBACKS, _lib.FALLBACKS
+
+
+def test_fp32_dropout_and_softmax_on_kernel():
+    from paddle_infer_amd.ops import _lib, dropout, fused_softmax_mask
+    _lib.FALLBACKS.clear()
+    x = torch.ones(512, 1024, device=DEV, requires_grad=True)
+    y = dropout(x, 0.3)
+    kept = y != 0
+    assert abs(kept.float().mean().item() - 0.7) < 0.01
+    _close(y[kept], torch.full_like(y[kept], 1 / 0.7), 1e-6, 0.0)
+    y.backward(torch.ones_like(y))
+    assert torch.equal(x.grad != 0, kept)  # backward regenerates the same mask
+    s = torch.randn(6, 40, 256, device=DEV, requires_grad=True)
+    m = torch.randn(40, 256, device=DEV)
+    p = fused_softmax_mask(s, m, 0.5)
+    dp = torch.randn_like(p)
+    p.backward(dp)
+    sr = s.detach().clone().requires_grad_()
+    pr = torch.softmax(sr * 0.5 + m, -1)
+    pr.backward(dp)
+    _close(p, pr, 1e-6, 1e-5)
+    _close(s.grad, sr.grad, 1e-6, 1e-5)
+    assert not _lib.FALLBACKS, _lib.FALLBACKS

@@ -11,10 +11,10 @@ import test_op_cases_cpu as C
 pytestmark = pytest.mark.gpu
 
 F32, BF16, F16 = (torch.float32, 1e-5), (torch.bfloat16, 3e-2), (torch.float16, 4e-3)
-# (case, dtype) pairs that have a HIP kernel: LN / RMSNorm / cross-entropy in all three dtypes,
-# softmax and GeLU in the 16-bit ones (fp32 softmax is torch's; fp32 GeLU records a fallback)
-KERNEL_CASES = [(c, d) for c in (C.LayerNormCase, C.RMSNormCase, C.CrossEntropyCase) for d in (F32, BF16, F16)] + \
-               [(c, d) for c in (C.SoftmaxCase, C.GeluCase) for d in (BF16, F16)]
+# (case, dtype) pairs that have a HIP kernel: LN / RMSNorm / cross-entropy / softmax / GeLU in all
+# three dtypes (elementwise.hip takes f32 rows as well as 16-bit ones)
+KERNEL_CASES = [(c, d) for c in (C.LayerNormCase, C.RMSNormCase, C.CrossEntropyCase, C.SoftmaxCase, C.GeluCase)
+                for d in (F32, BF16, F16)]
 
 
 def _grads(case, device, dtype):

@@ -534,8 +534,28 @@ __global__ __launch_bounds__(256, 2) void fwd_persist_kernel(FaArgs a) {
     int b, hq, m0, ntiles;
     const unsigned short *kb, *vb;
   };
-  auto setup = [&](int j, Item& it) {
-    const int sub = j / gx, grp = xcd + 8 * (j - sub * gx);
+  // Worker li's kk-th item. Diagonal schedule (nl a multiple of nmb, at least nl groups per XCD):
+  // step kk covers nl / nmb groups, the nmb workers of one group take its nmb query blocks
+  // TOGETHER (its K/V panel is read into L2 once for all of them) and each worker rotates through
+  // the block weights, so every worker gets the same causal work per nmb steps. Fewer groups (a
+  // worker runs fewer than nmb items, the rotation would not balance): items sub-major, heaviest
+  // first. Measured (B, S, H, D causal bf16): 96,1024,16,128 fwd 0.851 -> 0.816 ms diagonal (sub-major
+  // 0.987: each head's K/V re-read per block), 8,2048,16,128 0.222 -> 0.199 and 4,4096,16,128
+  // 0.366 -> 0.361 sub-major (diagonal 0.285 / 0.555), profiles/fa_persist_r4.txt.
+  const bool diag = nl >= nmb && nl % nmb == 0 && gx >= nl;
+  auto setup = [&](int kk, Item& it) -> bool {
+    int slot, sub;
+    if (diag) {
+      slot = kk * (nl / nmb) + li / nmb;
+      sub = (li % nmb + kk) % nmb;
+    } else {
+      const int jj = li + kk * nl;
+      if (jj >= nitems) return false;
+      sub = jj / gx;
+      slot = jj - sub * gx;
+    }
+    if (slot >= gx) return false;
+    const int grp = xcd + 8 * slot;
     const int mb = CAUSAL ? nmb - 1 - sub : sub;
     it.hq = grp % Hq;
     it.b = grp / Hq;
@@ -547,6 +567,7 @@ __global__ __launch_bounds__(256, 2) void fwd_persist_kernel(FaArgs a) {
     if (CAUSAL) n_end = min(Sk, it.m0 + BM + coff);
     // at least one (masked) tile: rows are clamped, so the DMA stays in bounds
     it.ntiles = n_end <= 0 ? 1 : (n_end + BN - 1) / BN;
+    return true;
   };
   auto issue = [&](const Item& it, int t, auto bufc) {
     char* ks = decltype(bufc)::value ? kv1 : kv0;
@@ -561,12 +582,10 @@ __global__ __launch_bounds__(256, 2) void fwd_persist_kernel(FaArgs a) {
     for (int kk = 0; kk < KSTEPS; ++kk) qf[kk] = *reinterpret_cast<const V8*>(qp + 16 * kk);
   };
 
-  int j = li;
-  if (j >= nitems) return;
+  int kk = 0;
   Item cur, nxt;
-  setup(j, cur);
-  bool has_next = j + nl < nitems;
-  if (has_next) setup(j + nl, nxt);
+  if (nitems == 0 || !setup(0, cur)) return;
+  bool has_next = setup(1, nxt);
   issue(cur, 0, std::integral_constant<int, 0>{});
   load_q(cur);
   __syncthreads();
@@ -714,10 +733,9 @@ __global__ __launch_bounds__(256, 2) void fwd_persist_kernel(FaArgs a) {
       done = true;
       return;
     }
-    j += nl;
+    ++kk;
     cur = nxt;
-    has_next = j + nl < nitems;
-    if (has_next) setup(j + nl, nxt);
+    has_next = setup(kk + 1, nxt);
     t = 0;
     reset();
   };
@@ -898,6 +916,25 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(FaArgs a) {
   if (total > 0) issue(0, std::integral_constant<int, 0>{});
   __syncthreads();
 
+  // DS: a tile's dS fragments are stored at the START of the next tile, next to that tile's DMA,
+  // so the write acknowledgements overlap the DMA the tile-end barrier waits for anyway (stored
+  // right after they are computed, they added their full latency to every tile: +20 % dK/dV time)
+  typename ET<F16>::V8 ds_pend[4];
+  char* ds_blk = nullptr;
+  const int ds_nk32 = 4 * ((Sk + 127) >> 7);
+  auto ds_flush = [&]() {
+    if (!ds_blk) return;
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const u32x4 d = __builtin_bit_cast(u32x4, ds_pend[2 * qt + s]);
+        char* p = ds_blk + (long long)qt * ds_nk32 * 2048 + 32 * s;
+        *reinterpret_cast<uint2*>(p) = make_uint2(d[0], d[1]);        // registers 8s..8s+3
+        *reinterpret_cast<uint2*>(p + 16) = make_uint2(d[2], d[3]);   // registers 8s+4..8s+7
+      }
+    ds_blk = nullptr;
+  };
   // one query tile; every LDS address below is a precomputed lane offset + an immediate. The
   // buffer parity is a template constant (two tile bodies) so each body reads one LDS object
   // while the DMA lands in the other.
@@ -909,6 +946,7 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(FaArgs a) {
     const float* dst = lst + BQ;
     const int hq = hk * group + it / tiles_per_head;
     const int q0 = (qt0 + it % tiles_per_head) * BQ;
+    if constexpr (DS) ds_flush();
     if (it + 1 < total) issue(it + 1, std::integral_constant<int, BUF ^ 1>{});
     f32x16 sacc[2], pacc[2];
     // S' = Q·Kᵀ − lse/scale, dP' = dO·Vᵀ − δ: row constants as the initial accumulators
@@ -991,19 +1029,12 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(FaArgs a) {
         pb[2 * qt + s] = E::frag(sacc[qt], s);
         db[2 * qt + s] = E::frag(pacc[qt], s);
       }
-    if constexpr (DS) {
-      const int nq32 = 2 * ((Sq + 63) >> 6), nk32 = 4 * ((Sk + 127) >> 7);
-      char* blk = (char*)a.ds + ((((long long)(b * Hq + hq) * nq32 + (q0 >> 5)) * nk32 + (kw0 >> 5)) << 11) +
-                  l32 * 64 + 8 * hh;
+    if constexpr (DS) {  // kept for the next tile's start (stored beside its DMA, see ds_flush)
+      const int nq32 = 2 * ((Sq + 63) >> 6);
+      ds_blk = (char*)a.ds + ((((long long)(b * Hq + hq) * nq32 + (q0 >> 5)) * ds_nk32 + (kw0 >> 5)) << 11) +
+               l32 * 64 + 8 * hh;
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const u32x4 d = __builtin_bit_cast(u32x4, db[2 * qt + s]);
-          char* p = blk + (long long)qt * nk32 * 2048 + 32 * s;
-          *reinterpret_cast<uint2*>(p) = make_uint2(d[0], d[1]);        // registers 8s..8s+3
-          *reinterpret_cast<uint2*>(p + 16) = make_uint2(d[2], d[3]);   // registers 8s+4..8s+7
-        }
+      for (int i = 0; i < 4; ++i) ds_pend[i] = db[i];
     }
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
@@ -1021,6 +1052,7 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(FaArgs a) {
     tile(it, std::integral_constant<int, 0>{});
     if (it + 1 < total) tile(it + 1, std::integral_constant<int, 1>{});
   }
+  if constexpr (DS) ds_flush();
 
   if (key < Sk) {
     const float vs = (FEAT & F_DROP) ? drk.inv : 1.f;

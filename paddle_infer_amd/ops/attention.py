@@ -103,9 +103,11 @@ def _fwd(q, k, v, causal, scale, mask=None, p=0.0, seed=0, off=0):
 
 
 # Stored-dS backward (flash_attn.h bwd_dq_ds_kernel): the dK/dV kernel writes dS and the dQ kernel
-# reads it back instead of recomputing S and dP. Used while the scratch stays under this many bytes
-# (B96 S1024 H16: 3.2 GB); larger problems recompute. PIAMD_FA_DS_MAX_MB overrides, 0 disables.
-DS_MAX_BYTES = int(os.environ.get("PIAMD_FA_DS_MAX_MB", "8192")) << 20
+# reads it back instead of recomputing S and dP, while the scratch stays under this many bytes
+# (B96 S1024 H16: 3.2 GB). Opt-in (PIAMD_FA_DS_MAX_MB): measured at B96 S1024 H16 D128 the dQ kernel
+# drops 929 -> 551 us but dK/dV grows 1596 -> 1957 us with the dS stores (fwd+bwd 3.997 -> 3.948 ms),
+# and D = 64 / S = 2048-4096 get slower (profiles/fa_persist_r4.txt), so recompute stays the default.
+DS_MAX_BYTES = int(os.environ.get("PIAMD_FA_DS_MAX_MB", "0")) << 20
 
 
 def _ds_bytes(B, Hq, Sq, Sk) -> int:

@@ -12,7 +12,7 @@ timeout -k 10 400 $T -s tests/test_native_fmt_gpu.py tests/test_native_fast_gpu.
 grep -E "decode step|run_ms|passed|failed" gpurun_out/r4c_native_tests.log | tail -8
 timeout -k 10 500 $T tests/test_conv_any_gpu.py tests/test_conv_gpu.py tests/test_conv_bwd_gpu.py > gpurun_out/r4c_conv_tests.log 2>&1 || { tail -40 gpurun_out/r4c_conv_tests.log; exit 1; }
 tail -1 gpurun_out/r4c_conv_tests.log
-timeout -k 10 300 $T tests/test_kernels_gpu.py tests/test_norm_gpu.py > gpurun_out/r4c_ln_tests.log 2>&1 || { tail -40 gpurun_out/r4c_ln_tests.log; exit 1; }
+timeout -k 10 300 $T tests/test_kernels_gpu.py tests/test_norm_gpu.py tests/test_op_cases_gpu.py > gpurun_out/r4c_ln_tests.log 2>&1 || { tail -40 gpurun_out/r4c_ln_tests.log; exit 1; }
 tail -1 gpurun_out/r4c_ln_tests.log
 for P in 0 1; do PIAMD_LN_BWD_PAIR=$P timeout -k 10 120 python tools/bench_ln_bwd.py; done
 S="96,1024,16,128;8,2048,16,128;4,4096,16,128;16,1024,32,64"

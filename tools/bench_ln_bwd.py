@@ -4,10 +4,12 @@ selects the two-waves-per-row kernel (default) or the wave-per-row one (0)."""
 import argparse
 import json
 import os
+import sys
 
 import torch
 
-from paddle_infer_amd.ops import fused_add_layer_norm
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from paddle_infer_amd.ops import fused_add_layer_norm  # noqa: E402
 
 
 def main():

@@ -221,7 +221,15 @@ def _recordable(fn):
 
 @_recordable
 def linear(x, weight, bias=None):
-    """y = x @ weight (+ bias); weight is ``[in_features, out_features]``."""
+    """y = x @ weight (+ bias); weight is ``[in_features, out_features]``. Under CUDA autocast an
+    fp32 weight is cast to the autocast dtype here (differentiably: its gradient flows back to the
+    fp32 parameter), so the product runs on the own 16-bit GEMMs instead of the library's
+    mixed-dtype path (e.g. the classifier of an AMP-trained ResNet / MobileNet)."""
+    if (x.is_cuda and weight.dtype == torch.float32 and torch.is_autocast_enabled("cuda")
+            and getattr(weight, "main_grad", None) is None):  # main_grad weights keep the fused path
+        dt = torch.get_autocast_dtype("cuda")
+        with torch.autocast("cuda", enabled=False):
+            return linear(x.to(dt), weight.to(dt), bias.to(dt) if bias is not None else None)
     if torch.is_grad_enabled() and (weight.requires_grad or getattr(weight, "main_grad", None) is not None):
         return _LinearFn.apply(x, weight, bias)
     # inference weights: same K-contiguous cached copy + bias-in-epilogue GEMM as training

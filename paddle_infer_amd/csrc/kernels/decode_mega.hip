@@ -40,6 +40,14 @@ constexpr int NWG = 256;               // workgroups (one per CU)
 constexpr int E = 2048, D = 128, HQ = 16, HK = 16, F = 8192;
 constexpr int NQKV = (HQ + 2 * HK) * D;  // 6144
 constexpr int WBYTES = 128 * 1024;     // LDS weight slice
+// LDS placement per layer: QKV [0, 96K) → out [96K, 128K) (free during QKV) → FFN1 [0, 128K),
+// whose first 96 KiB stream in during the attention phase and the last 32 KiB once the out
+// slice is consumed → FFN2 [0, 128K) → next QKV [0, 96K).
+constexpr int OUT_OFF = 96 * 1024;
+constexpr int FFN1_PRE = 96 * 1024;
+// per loader wave: FFN1_PRE / 1 KiB / 3 waves DMA instructions (the out phase waits for every
+// older one: `s_waitcnt vmcnt(32)` in phase_start)
+static_assert(FFN1_PRE / 1024 / 3 == 32, "phase_start WAIT_OLDER count");
 constexpr int PSTRIDE = D + 2;         // attention partial: acc[D], m, l
 // per-layer partial block, padded to 256 B
 __host__ __device__ constexpr long pstride(int nsplit) { return ((long)HQ * nsplit * PSTRIDE + 63) / 64 * 64; }
@@ -149,10 +157,13 @@ __device__ __forceinline__ void prefetch(const bf16_t* src, int from, int to, ch
                                      (__attribute__((address_space(3))) void*)(wl + p * 1024), 16, 0, 0);
 }
 
-// Phase entry: loader waves wait for their DMA, then the whole workgroup meets (wave 0 arrives
-// here after its grid barrier).
-__device__ __forceinline__ void phase_start(const MegaArgs& a, int wv, unsigned ph) {
-  if (wv != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+// Phase entry: loader waves wait for their DMA (all of it, all but the newest FFN1_PRE_OPS
+// wave-instructions, or none), then the whole workgroup meets (wave 0 arrives here after its
+// grid barrier).
+enum { WAIT_ALL, WAIT_OLDER, WAIT_NONE };
+__device__ __forceinline__ void phase_start(const MegaArgs& a, int wv, unsigned ph, int wait = WAIT_ALL) {
+  if (wv != 0 && wait == WAIT_ALL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (wv != 0 && wait == WAIT_OLDER) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
   __syncthreads();
   if (a.trace && threadIdx.x == 0) a.trace[((long)blockIdx.x * a.nl * 5 + ph) * 4] = wall_clock64();
 }
@@ -172,16 +183,16 @@ __device__ __forceinline__ void butterfly(float* acc, int lane) {
   if constexpr (HALF > 1) butterfly<HALF / 2, O / 2>(acc, lane);
 }
 
-// y[c] = Σ_k x[k]·W[c][k] for the NPW columns of this workgroup's LDS slice ([NPW][K] bf16);
+// y[c] = Σ_k x[k]·W[c][k] for the NPW columns of this workgroup's LDS slice `ws` ([NPW][K] bf16);
 // thread t holds x[k] for k = (j·256 + t)·8 + i. Returns column `tid`'s sum for tid < NPW.
 // Reduction: a butterfly that halves the live columns per exchange (log2 P steps, P−1 shuffles
 // instead of 6·P), then 4 waves through LDS.
-// The next phase's slice (`nsrc`, `nbytes`; nullable) streams in behind the GEMV: its first
-// min(nbytes, this slice / 2) bytes as soon as every wave has consumed the first half of the
-// columns, the rest once the whole slice is consumed.
-template <int NPW, int KCH>
-__device__ __forceinline__ float gemv_lds(char* wl, const float (&x)[KCH][8], float* red, int tid,
-                                          const bf16_t* nsrc, int nbytes) {
+// `mid()` runs once every wave has consumed the first half of the columns (slice bytes
+// [0, SLICE/2) are free), `end()` once the whole slice is consumed: the loader waves issue the
+// next slices' DMA there.
+template <int NPW, int KCH, class Mid, class End>
+__device__ __forceinline__ float gemv_lds(const char* ws, const float (&x)[KCH][8], float* red, int tid,
+                                          Mid mid, End end) {
   constexpr int K = 2048 * KCH;
   constexpr int P = NPW <= 8 ? 8 : 32;
   constexpr int LOGP = P == 8 ? 3 : 5;
@@ -194,24 +205,22 @@ __device__ __forceinline__ float gemv_lds(char* wl, const float (&x)[KCH][8], fl
     for (int c = decltype(c0)::value; c < decltype(c1)::value; ++c) {
 #pragma unroll
       for (int j = 0; j < KCH; ++j) {
-        const u16x8 w = *reinterpret_cast<const u16x8*>(wl + ((long)c * K + (j * 256 + tid) * 8) * 2);
+        const u16x8 w = *reinterpret_cast<const u16x8*>(ws + ((long)c * K + (j * 256 + tid) * 8) * 2);
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc[c] += x[j][i] * bf2f(w[i]);
       }
     }
   };
-  constexpr int SLICE = NPW * K * 2;
-  const int early = min(nbytes, SLICE / 2);
   cols(std::integral_constant<int, 0>{}, std::integral_constant<int, NPW / 2>{});
   __syncthreads();  // columns [0, NPW/2) = slice bytes [0, SLICE/2) consumed by every wave
-  prefetch(nsrc, 0, early, wl, wv, lane);
+  mid();
   cols(std::integral_constant<int, NPW / 2>{}, std::integral_constant<int, NPW>{});
   butterfly<P / 2, 32>(acc, lane);
 #pragma unroll
   for (int o = 32 >> LOGP; o > 0; o >>= 1) acc[0] += __shfl_xor(acc[0], o, 64);
   if ((lane & ((64 >> LOGP) - 1)) == 0) red[wv * P + (lane >> (6 - LOGP))] = acc[0];
   __syncthreads();
-  prefetch(nsrc, early, nbytes, wl, wv, lane);
+  end();
   float r = 0.f;
   if (tid < NPW) r = red[tid] + red[P + tid] + red[2 * P + tid] + red[3 * P + tid];
   return r;
@@ -254,6 +263,7 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
   __shared__ float sc[256];
   __shared__ float pv[4][D];
   __shared__ float qs[D];
+  __shared__ float xo[E];  // out-projection input (combined attention output)
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, w = blockIdx.x;
   const int pos = a.pos[0], L = pos + 1;
@@ -280,7 +290,11 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
       float x[1][8];
       ln_prologue(a, rin, Ly.ln1_g, Ly.ln1_b, x, wred, tid);
       tmark(a, nbar, 1);
-      const float y = gemv_lds<NPQ, 1>(wl, x, red, tid, Ly.wo + (long)w * NPO * E, NPO * E * 2);
+      // out slice into the region QKV does not use, behind this GEMV
+      const float y = gemv_lds<NPQ, 1>(wl, x, red, tid, [] {}, [&] {
+        prefetch(Ly.wo + (long)w * NPO * E, 0, NPO * E * 2, wl + OUT_OFF, wv, lane);
+      });
+      static_assert(NPQ * E * 2 == OUT_OFF && NPO * E * 2 == WBYTES - OUT_OFF, "LDS placement");
       tmark(a, nbar, 2);
       if (wv == 0) {
         if (lane < NPQ) {
@@ -303,7 +317,9 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
       }
     }
     // ---------------------------------------------------------------- attention
-    phase_start(a, wv, nbar);
+    // (attention reads no weights: the out slice keeps streaming)
+    phase_start(a, wv, nbar, WAIT_NONE);
+    const bf16_t* w1s = Ly.w1 + (long)w * NP1 * E;
     if (w < HQ * a.nsplit) {
       const int h = w / a.nsplit, s = w % a.nsplit, kh = h / (HQ / HK);
       const int chunk = (L + a.nsplit - 1) / a.nsplit;
@@ -365,6 +381,8 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
         for (int t = 0; t < 8; ++t) pv[wv][sub * 8 + t] = acc[t];
       }
       __syncthreads();
+      // this workgroup's K/V loads are done: the loader waves may queue DMA again
+      prefetch(w1s, 0, FFN1_PRE, wl, wv, lane);
       if (wv == 0) {
         float* dst = part + (long)(h * a.nsplit + s) * PSTRIDE;
         const int d0 = lane * 2;
@@ -373,41 +391,55 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
         st64(dst + d0, pack2f(n > 0 ? v0 : 0.f, n > 0 ? v1 : 0.f));
         if (lane == 0) st64(dst + D, pack2f(n > 0 ? m : -INFINITY, n > 0 ? lsum : 0.f));
       }
+    } else {
+      prefetch(w1s, 0, FFN1_PRE, wl, wv, lane);
     }
     if (wv == 0) grid_sync(a, ++nbar, lane); else ++nbar;
     // ---------------------------------------------------------------- out projection
-    phase_start(a, wv, nbar);
+    phase_start(a, wv, nbar, WAIT_OLDER);
     {
-      const int ocol = w * NPO + (lane & (NPO - 1));
-      const float bo = bf2f(Ly.bo[ocol]), ro = bf2f(rin[ocol]);
-      float x[1][8];
-      {
-        const int h = tid >> 4, d0 = (tid & 15) * 8;
-        const float* base = part + (long)h * a.nsplit * PSTRIDE;
-        float M = -INFINITY;
-        for (int s = 0; s < a.nsplit; ++s) M = fmaxf(M, ldf(base + s * PSTRIDE + D));
-        float lt = 0.f, o[8];
+      // wave 0 alone reads the other workgroups' outputs: the loader waves' queues hold the
+      // FFN1 DMA, and their loads would retire behind it
+      float bo = 0.f, ro = 0.f;
+      if (wv == 0) {
+        const int ocol = w * NPO + (lane & (NPO - 1));
+        bo = bf2f(Ly.bo[ocol]);
+        ro = bf2f(rin[ocol]);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] = 0.f;
-        for (int s = 0; s < a.nsplit; ++s) {
-          const u64 ml = ld64(base + s * PSTRIDE + D);
-          const float ms = __uint_as_float((unsigned)ml);
-          if (ms == -INFINITY) continue;
-          const float e = exp2f(ms - M);
-          lt += e * __uint_as_float((unsigned)(ml >> 32));
+        for (int r = 0; r < 4; ++r) {
+          const int g = lane + 64 * r, h = g >> 4, d0 = (g & 15) * 8;
+          const float* base = part + (long)h * a.nsplit * PSTRIDE;
+          float M = -INFINITY;
+          for (int s = 0; s < a.nsplit; ++s) M = fmaxf(M, ldf(base + s * PSTRIDE + D));
+          float lt = 0.f, o[8];
 #pragma unroll
-          for (int i = 0; i < 8; i += 2) {
-            const u64 u = ld64(base + s * PSTRIDE + d0 + i);
-            o[i] += e * __uint_as_float((unsigned)u);
-            o[i + 1] += e * __uint_as_float((unsigned)(u >> 32));
+          for (int i = 0; i < 8; ++i) o[i] = 0.f;
+          for (int s = 0; s < a.nsplit; ++s) {
+            const u64 ml = ld64(base + s * PSTRIDE + D);
+            const float ms = __uint_as_float((unsigned)ml);
+            if (ms == -INFINITY) continue;
+            const float e = exp2f(ms - M);
+            lt += e * __uint_as_float((unsigned)(ml >> 32));
+#pragma unroll
+            for (int i = 0; i < 8; i += 2) {
+              const u64 u = ld64(base + s * PSTRIDE + d0 + i);
+              o[i] += e * __uint_as_float((unsigned)u);
+              o[i + 1] += e * __uint_as_float((unsigned)(u >> 32));
+            }
           }
-        }
-        const float inv = 1.f / lt;
+          const float inv = 1.f / lt;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) x[0][i] = bf2f(f2bf(o[i] * inv));
+          for (int i = 0; i < 8; ++i) xo[g * 8 + i] = bf2f(f2bf(o[i] * inv));
+        }
       }
+      __syncthreads();
+      float x[1][8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) x[0][i] = xo[tid * 8 + i];
       tmark(a, nbar, 1);
-      const float y = gemv_lds<NPO, 1>(wl, x, red, tid, Ly.w1 + (long)w * NP1 * E, NP1 * E * 2);
+      const float y = gemv_lds<NPO, 1>(wl + OUT_OFF, x, red, tid, [] {}, [&] {
+        prefetch(w1s, FFN1_PRE, NP1 * E * 2, wl, wv, lane);
+      });
       tmark(a, nbar, 2);
       if (wv == 0) {
         publish_bf16(rmid + w * NPO, y + bo + ro, lane, NPO);
@@ -423,7 +455,9 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
       float x[1][8];
       ln_prologue(a, rmid, Ly.ln2_g, Ly.ln2_b, x, wred, tid);
       tmark(a, nbar, 1);
-      const float y = gemv_lds<NP1, 1>(wl, x, red, tid, Ly.w2 + (long)w * NP2 * F, NP2 * F * 2);
+      const bf16_t* w2s = Ly.w2 + (long)w * NP2 * F;
+      const float y = gemv_lds<NP1, 1>(wl, x, red, tid, [&] { prefetch(w2s, 0, WBYTES / 2, wl, wv, lane); },
+                                       [&] { prefetch(w2s, WBYTES / 2, WBYTES, wl, wv, lane); });
       tmark(a, nbar, 2);
       if (wv == 0) {
         const float t = y + b1;
@@ -442,9 +476,9 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) ld_bf8(hb + (j * 256 + tid) * 8, x[j]);
       tmark(a, nbar, 1);
-      const float y = gemv_lds<NP2, 4>(wl, x, red, tid,
-                                       l + 1 < a.nl ? a.layers[l + 1].wqkv + (long)w * NPQ * E : nullptr,
-                                       NPQ * E * 2);
+      const bf16_t* nq = l + 1 < a.nl ? a.layers[l + 1].wqkv + (long)w * NPQ * E : nullptr;
+      const float y = gemv_lds<NP2, 4>(wl, x, red, tid, [&] { prefetch(nq, 0, WBYTES / 2, wl, wv, lane); },
+                                       [&] { prefetch(nq, WBYTES / 2, OUT_OFF, wl, wv, lane); });
       tmark(a, nbar, 2);
       if (wv == 0) {
         publish_bf16(rout + w * NP2, y + b2 + rm, lane, NP2);
@@ -461,6 +495,144 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
       __hip_atomic_fetch_add(a.bar + 18 * BAR_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == NWG - 1) {
     for (int i = 0; i < 19; ++i)
       __hip_atomic_exchange(a.bar + i * BAR_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Greedy tail of a batch-1 decode step, one launch: final LayerNorm → LM-head GEMV → argmax →
+// token bookkeeping → the next step's embedding. On the launch-per-op tail these are ~8 small
+// kernels per token (LN, head GEMM, argmax, pad masking, token-column store, position increment,
+// embedding gather + add), ≈110 µs of a 1.39 ms step (profiles/decode_step_anatomy_r4.txt).
+//   * 256 workgroups × 16 waves; every workgroup recomputes the LN of the [E] residual (4 KB from
+//     L2), then each wave streams column quads of the [V][E] head table (16 × 16-B loads per lane
+//     in flight) and keeps its best (bf16-rounded logit, smallest id) as one 64-bit key.
+//   * argmax: per-group 64-bit atomic max (8 groups of 32 workgroups, one 256-B line each), then
+//     a two-level arrival counter; the last workgroup reads the 8 maxima, applies
+//     `where(done, pad, tok)`, stores the token into out[0, t], raises `done` on EOS, advances
+//     `pos`, writes word_emb[tok] + pos_emb[pos] for the next step and re-zeroes the words.
+// Same rounding points as the per-op tail (bf16 LN output, bf16 logits, ties → smaller id).
+// Parity: reference greedy search in `fused_multi_transformer` decoding loops
+// (`paddlenlp` generation `greedy_search`: argmax → where(unfinished) → append; `top_k=1`).
+struct HeadArgs {
+  const bf16_t *y, *g, *b;  // [E] final residual, final-LN gamma / beta
+  float eps;
+  int V;                    // vocabulary rows of `w`
+  const bf16_t* w;          // [V][E] LM head
+  u64* best;                // 8 words, 256-B apart (zero before the first launch)
+  unsigned* cnt;            // 9 words, 256-B apart (zero before the first launch)
+  long long* out;           // &out[0, t]
+  unsigned char* done;      // [1] bool
+  long long eos;            // < 0: no EOS
+  long long pad;
+  int* pos;                 // [1] slot of the token just decoded; advanced by one
+  long long* tok;           // [1] chosen token (pad-masked)
+  const bf16_t* wemb;       // [V][E] word embedding
+  const bf16_t* pemb;       // [P][E] learned position embedding
+  int P;
+  bf16_t* resid;            // [E] next step's embedding output (written when pos + 1 < P)
+};
+constexpr int HNT = 1024, HNWG = 256;
+
+__device__ __forceinline__ u64 logit_key(float v, int col) {
+  const unsigned u = __float_as_uint(v);
+  const unsigned k = (u & 0x80000000u) ? ~u : (u | 0x80000000u);  // order-preserving
+  return ((u64)k << 32) | (u64)(0xFFFFFFFFu - (unsigned)col);     // ties → smaller id
+}
+
+__global__ __launch_bounds__(HNT) void decode_head_kernel(HeadArgs a) {
+  __shared__ float xs[E];
+  __shared__ float wred[16];
+  __shared__ u64 wbest[16];
+  __shared__ long long sh_tok;
+  __shared__ int sh_pos, sh_last;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, w = blockIdx.x;
+  {
+    const unsigned yy = reinterpret_cast<const unsigned*>(a.y)[tid];
+    const unsigned gg = reinterpret_cast<const unsigned*>(a.g)[tid];
+    const unsigned bb = reinterpret_cast<const unsigned*>(a.b)[tid];
+    const float v0 = bf2f((bf16_t)(yy & 0xFFFF)), v1 = bf2f((bf16_t)(yy >> 16));
+    const float mean = block_sum<16>(v0 + v1, wred) * (1.f / E);
+    const float d0 = v0 - mean, d1 = v1 - mean;
+    const float rs = rsqrtf(block_sum<16>(d0 * d0 + d1 * d1, wred) * (1.f / E) + a.eps);
+    xs[2 * tid] = bf2f(f2bf(d0 * rs * bf2f((bf16_t)(gg & 0xFFFF)) + bf2f((bf16_t)(bb & 0xFFFF))));
+    xs[2 * tid + 1] = bf2f(f2bf(d1 * rs * bf2f((bf16_t)(gg >> 16)) + bf2f((bf16_t)(bb >> 16))));
+  }
+  __syncthreads();
+  float x[4][8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[j][i] = xs[(j * 64 + lane) * 8 + i];
+  u64 best = 0;
+  const int nq = (a.V + 3) >> 2, stride = gridDim.x * 16;
+  for (int q = w * 16 + wv; q < nq; q += stride) {
+    u16x8 wt[4][4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const long col = min(q * 4 + c, a.V - 1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        wt[c][j] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(a.w + col * E + (j * 64 + lane) * 8));
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s += x[j][i] * bf2f(wt[c][j][i]);
+      s = wave_sum(s);
+      const int col = q * 4 + c;
+      if (col < a.V) {
+        const u64 k = logit_key(bf2f(f2bf(s)), col);
+        best = k > best ? k : best;
+      }
+    }
+  }
+  if (lane == 0) wbest[wv] = best;
+  __syncthreads();
+  if (tid == 0) {
+    u64 m = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m = wbest[i] > m ? wbest[i] : m;
+    const int g = w & 7;
+    __hip_atomic_fetch_max(a.best + g * 32, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the max has landed before the arrival
+    int last = 0;
+    if (__hip_atomic_fetch_add(a.cnt + g * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == HNWG / 8 - 1 &&
+        __hip_atomic_fetch_add(a.cnt + 8 * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 7)
+      last = 1;
+    sh_last = last;
+    if (last) {
+      u64 mm = 0;
+      for (int i = 0; i < 8; ++i) {
+        const u64 v = __hip_atomic_exchange(a.best + i * 32, (u64)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        mm = v > mm ? v : mm;
+      }
+      for (int i = 0; i < 9; ++i)
+        __hip_atomic_exchange(a.cnt + i * 64, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      long long id = (long long)(0xFFFFFFFFu - (unsigned)mm);
+      if (*a.done) id = a.pad;
+      *a.out = id;
+      *a.tok = id;
+      if (a.eos >= 0 && id == a.eos) *a.done = 1;
+      const int p = *a.pos + 1;
+      *a.pos = p;
+      sh_tok = id;
+      sh_pos = p;
+    }
+  }
+  __syncthreads();
+  if (!sh_last) return;
+  const long long id = sh_tok;
+  const int p = sh_pos;
+  if (tid < E / 8 && p < a.P && id >= 0 && id < a.V) {
+    const u16x8 u = *reinterpret_cast<const u16x8*>(a.wemb + id * E + tid * 8);
+    const u16x8 v = *reinterpret_cast<const u16x8*>(a.pemb + (long)p * E + tid * 8);
+    u16x8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = f2bf(bf2f(u[i]) + bf2f(v[i]));
+    *reinterpret_cast<u16x8*>(a.resid + tid * 8) = o;
   }
 }
 
@@ -508,4 +680,14 @@ PIAMD_EXPORT int piamd_decode_mega(const MegaArgs* args, int E_, int D_, int hq,
   MegaArgs arg = a;
   void* kargs[] = {&arg};
   return (int)hipLaunchCooperativeKernel((const void*)decode_mega_kernel, dim3(NWG), dim3(NT), kargs, 0, st);
+}
+
+// Greedy tail of one batch-1 decode step (see decode_head_kernel). Returns hipError_t.
+PIAMD_EXPORT int piamd_decode_head_greedy(const HeadArgs* args, int E_, hipStream_t st) {
+  const HeadArgs& a = *args;
+  if (E_ != E || a.V < 1 || !a.y || !a.g || !a.b || !a.w || !a.best || !a.cnt || !a.out || !a.done ||
+      !a.pos || !a.tok || !a.wemb || !a.pemb || !a.resid || a.P < 1)
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(decode_head_kernel, dim3(HNWG), dim3(HNT), 0, st, a);
+  return (int)hipGetLastError();
 }

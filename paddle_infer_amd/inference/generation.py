@@ -196,7 +196,11 @@ class GPTGenerator:
         out = torch.full((B, max_new_tokens), pad_token_id, dtype=torch.long, device=self.device)
         done = torch.zeros(B, dtype=torch.bool, device=self.device)
         pos = lens.to(torch.int32)
-        if decode_strategy == "greedy_search" and self.use_graph and self._mega_decoder(B) is None:
+        mega = self._mega_decoder(B)
+        if decode_strategy == "greedy_search" and mega is not None and mega.head_ok:
+            return self._greedy_mega_loop(mega, logits, pos, out, done, max_new_tokens, eos_token_id,
+                                          pad_token_id)
+        if decode_strategy == "greedy_search" and self.use_graph and mega is None:
             return self._greedy_graph_loop(logits, pos, out, done, max_new_tokens, eos_token_id,
                                            pad_token_id)
         for t in range(max_new_tokens):
@@ -212,6 +216,26 @@ class GPTGenerator:
                 pos = pos + 1
         if self._mega:  # one sync per generate(): a timed-out single-launch step fails loudly
             self._mega.check()
+        return out
+
+    def _greedy_mega_loop(self, mega, logits, pos, out, done, max_new_tokens, eos, pad):
+        """Batch-1 greedy decoding on the single-launch step: two launches per token, the layer
+        stack (decode_mega_kernel) and the greedy tail (decode_head_kernel: final LN, LM head,
+        argmax, pad / EOS bookkeeping, token store, position advance, next embedding). Same
+        tokens as the eager loop up to logit ties within bf16 rounding."""
+        from ..ops.search import argmax_rows
+        tok = torch.where(done, torch.full_like(pos, pad, dtype=torch.long), argmax_rows(logits))
+        out[:, 0] = tok
+        if eos is not None:
+            done = done | (tok == eos)
+        pos = pos.clone()  # advanced in place by the tail kernel
+        resid = self.model.gpt.embeddings(tok.view(1, 1), pos.long().view(1, 1)).reshape(-1).contiguous()
+        tok = tok.clone()
+        for t in range(1, max_new_tokens):
+            mega.greedy_tail(mega(resid, pos), out, t, done, eos, pad, pos, tok, resid)
+            if eos is not None and (t & 7) == 7 and bool(done.all()):
+                break
+        mega.check()
         return out
 
     def _greedy_graph_loop(self, logits, pos, out, done, max_new_tokens, eos, pad):

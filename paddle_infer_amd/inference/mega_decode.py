@@ -101,6 +101,39 @@ class MegaDecoder:
         self.act = 1 if gen.act == "gelu_tanh" else 0
         self.eps = float(gen.cfg.layer_norm_eps)
         self.trace = None  # set to a zeroed int64 [256, 5·nl, 4] tensor to record phase times
+        # greedy tail (decode_head_kernel): LM head + argmax + bookkeeping + next embedding
+        self.head_ok = _lib.has("piamd_decode_head_greedy") and self._head_tables(gen)
+        self.best = torch.zeros(8 * 32, dtype=torch.int64, device=dev)
+        self.cnt = torch.zeros(9 * 64, dtype=torch.int32, device=dev)
+
+    def _head_tables(self, gen) -> bool:
+        m = gen.model
+        emb = getattr(getattr(m, "gpt", None), "embeddings", None)
+        if emb is None or not hasattr(m, "head_weight"):
+            return False
+        self.head_w = m.head_weight().detach()
+        self.wemb = emb.word_embeddings.weight.detach()
+        self.pemb = getattr(emb, "position_embeddings", None)
+        ts = [self.head_w, self.wemb, self.pemb, *gen.final_ln[:2]]
+        if any(t is None or t.dtype != torch.bfloat16 or not t.is_contiguous() or not t.is_cuda for t in ts):
+            return False
+        self.pemb = self.pemb.detach()
+        return (self.head_w.dim() == 2 and self.head_w.shape[1] == E and self.wemb.shape[1] == E
+                and self.pemb.shape[1] == E and self.head_w.shape[0] == self.wemb.shape[0])
+
+    def greedy_tail(self, y, out, t, done, eos, pad, pos, tok, resid) -> None:
+        """After a step: final LN + LM head + argmax on ``y`` [E] → token (``pad`` once ``done``)
+        into ``out[0, t]`` and ``tok``; ``done`` |= token == ``eos``; ``pos`` += 1; ``resid`` =
+        the next step's embedding (word_emb[token] + pos_emb[pos]). One launch."""
+        assert out.dtype == torch.int64 and out.is_contiguous() and 0 <= t < out.shape[-1]
+        assert done.dtype == torch.bool and tok.dtype == torch.int64 and resid.numel() == E
+        g, b, eps = self.gen.final_ln
+        a = _lib.HeadArgs(y.data_ptr(), g.data_ptr(), b.data_ptr(), float(eps), self.head_w.shape[0],
+                          self.head_w.data_ptr(), self.best.data_ptr(), self.cnt.data_ptr(),
+                          out.data_ptr() + 8 * t, done.data_ptr(), -1 if eos is None else int(eos),
+                          int(pad), pos.data_ptr(), tok.data_ptr(), self.wemb.data_ptr(),
+                          self.pemb.data_ptr(), self.pemb.shape[0], resid.data_ptr())
+        _lib.call("piamd_decode_head_greedy", ctypes.byref(a), E, _lib.stream())
 
     def __call__(self, resid: torch.Tensor, pos: torch.Tensor) -> torch.Tensor:
         """resid: bf16 [E] embedding output; pos: device int32 [1] = the cache slot of this token.

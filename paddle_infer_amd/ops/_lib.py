@@ -96,6 +96,18 @@ class MegaArgs(ctypes.Structure):
 
 
 _SIGS["piamd_decode_mega"] = [ctypes.POINTER(MegaArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]
+
+
+class HeadArgs(ctypes.Structure):
+    """Mirror of ``struct HeadArgs`` (csrc/kernels/decode_mega.hip)."""
+    _fields_ = ([(n, c_void_p) for n in ("y", "g", "b")] + [("eps", ctypes.c_float), ("V", c_int)]
+                + [(n, c_void_p) for n in ("w", "best", "cnt", "out", "done")]
+                + [("eos", ctypes.c_longlong), ("pad", ctypes.c_longlong)]
+                + [(n, c_void_p) for n in ("pos", "tok", "wemb", "pemb")]
+                + [("P", c_int), ("resid", c_void_p)])
+
+
+_SIGS["piamd_decode_head_greedy"] = [ctypes.POINTER(HeadArgs), c_int, c_void_p]
 _SIGS["piamd_decode_mega_supported"] = []
 _SIGS["piamd_fa_fwd"] = [ctypes.POINTER(FaArgs), c_int, c_void_p]
 _SIGS["piamd_fa_bwd"] = [ctypes.POINTER(FaArgs), c_int, c_void_p]

@@ -30,3 +30,16 @@ def test_megaargs_mirror_matches_kernel_struct():
     body = re.sub(r"//[^\n]*", "", body)
     names = re.findall(r"\b(\w+);", body)
     assert names == [f[0] for f in _lib.MegaArgs._fields_], names
+
+
+def test_headargs_mirror_matches_kernel_struct():
+    import ctypes
+    from paddle_infer_amd.ops import _lib
+    src = open(os.path.join(os.path.dirname(_lib.__file__), "..", "csrc", "kernels",
+                            "decode_mega.hip")).read()
+    body = src[src.index("struct HeadArgs {") + len("struct HeadArgs {"):]
+    body = re.sub(r"//[^\n]*", "", body[:body.index("};")])
+    names = [re.findall(r"\w+", part)[-1] for stmt in body.split(";") if stmt.strip()
+             for part in stmt.split(",")]
+    assert names == [f[0] for f in _lib.HeadArgs._fields_], names
+    assert ctypes.sizeof(_lib.HeadArgs) == 136

@@ -72,3 +72,34 @@ def test_mega_decode_graph_generate_matches_eager():
         b = graph.generate(ids, max_new_tokens=12)
         assert torch.equal(a.cpu(), b.cpu()), (a, b)
     graph._mega.check()
+
+
+def test_mega_greedy_tail_matches_logits_path():
+    """Fused greedy tail (decode_head_kernel) against the launch-per-op tail: every chosen token
+    is a maximiser of the per-op path's logits (teacher-forced on the chosen tokens, so a wrong
+    position, embedding or cache slot shows up as a logit mismatch), and EOS masks to pad."""
+    from paddle_infer_amd.inference.generation import GPTGenerator
+    m = _gpt13b_width(2, 256)
+    torch.manual_seed(3)
+    ids = torch.randint(0, 2048, (1, 9), device=DEV)
+    n = 12
+    g = GPTGenerator(m, max_batch=1, max_seq_len=256, use_hip_graph=False)
+    out = g.generate(ids, max_new_tokens=n)
+    assert g._mega.head_ok
+    ref = GPTGenerator(m, max_batch=1, max_seq_len=256, use_hip_graph=False)
+    logits = ref.prefill(ids, torch.full((1,), 9, device=DEV))
+    pos = torch.full((1,), 9, dtype=torch.int32, device=DEV)
+    for t in range(n):
+        lg = logits[0].float()
+        tok = int(out[0, t])
+        assert lg[tok] >= lg.max() - 0.02 * lg.abs().max(), (t, tok, lg.argmax().item())
+        if t + 1 < n:
+            logits = ref.decode(out[:, t].contiguous(), pos)
+            pos += 1
+    # EOS: the first occurrence of the token at step 3 ends the sequence, pad after it
+    eos = int(out[0, 3])
+    k = int((out[0] == eos).nonzero()[0])
+    out2 = g.generate(ids, max_new_tokens=n, eos_token_id=eos, pad_token_id=7)
+    assert torch.equal(out2[0, :k + 1].cpu(), out[0, :k + 1].cpu()), (out, out2)
+    assert (out2[0, k + 1:] == 7).all(), out2
+    g._mega.check()

@@ -41,8 +41,8 @@ constexpr int E = 2048, D = 128, HQ = 16, HK = 16, F = 8192;
 constexpr int NQKV = (HQ + 2 * HK) * D;  // 6144
 constexpr int WBYTES = 128 * 1024;     // LDS weight slice
 // LDS placement per layer: QKV [0, 96K) → out [96K, 128K) (free during QKV) → FFN1 [0, 128K),
-// whose first 96 KiB stream in during the attention phase and the last 32 KiB once the out
-// slice is consumed → FFN2 [0, 128K) → next QKV [0, 96K).
+// whose first 96 KiB stream in during the attention phase (workgroups without attention work) or
+// the out-projection prologue (the others) and the last 32 KiB once the out slice is consumed → FFN2 [0, 128K) → next QKV [0, 96K).
 constexpr int OUT_OFF = 96 * 1024;
 constexpr int FFN1_PRE = 96 * 1024;
 // per loader wave: FFN1_PRE / 1 KiB / 3 waves DMA instructions (the out phase waits for every
@@ -157,8 +157,8 @@ __device__ __forceinline__ void prefetch(const bf16_t* src, int from, int to, ch
                                      (__attribute__((address_space(3))) void*)(wl + p * 1024), 16, 0, 0);
 }
 
-// Phase entry: loader waves wait for their DMA (all of it, all but the newest FFN1_PRE_OPS
-// wave-instructions, or none), then the whole workgroup meets (wave 0 arrives here after its
+// Phase entry: loader waves wait for their DMA (all of it, all but the newest 32
+// wave-instructions = the FFN1 head, or none), then the whole workgroup meets (wave 0 arrives here after its
 // grid barrier).
 enum { WAIT_ALL, WAIT_OLDER, WAIT_NONE };
 __device__ __forceinline__ void phase_start(const MegaArgs& a, int wv, unsigned ph, int wait = WAIT_ALL) {
@@ -263,7 +263,6 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
   __shared__ float sc[256];
   __shared__ float pv[4][D];
   __shared__ float qs[D];
-  __shared__ float xo[E];  // out-projection input (combined attention output)
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, w = blockIdx.x;
   const int pos = a.pos[0], L = pos + 1;
@@ -381,8 +380,6 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
         for (int t = 0; t < 8; ++t) pv[wv][sub * 8 + t] = acc[t];
       }
       __syncthreads();
-      // this workgroup's K/V loads are done: the loader waves may queue DMA again
-      prefetch(w1s, 0, FFN1_PRE, wl, wv, lane);
       if (wv == 0) {
         float* dst = part + (long)(h * a.nsplit + s) * PSTRIDE;
         const int d0 = lane * 2;
@@ -396,46 +393,50 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
     }
     if (wv == 0) grid_sync(a, ++nbar, lane); else ++nbar;
     // ---------------------------------------------------------------- out projection
-    phase_start(a, wv, nbar, WAIT_OLDER);
+    // attention workgroups queue their FFN1 DMA only now (their loader waves carried K/V loads):
+    // every older load has to land; the others issued it at the attention phase start and wait
+    // for the out slice only
+    const bool attn_wg = w < HQ * a.nsplit;
+    phase_start(a, wv, nbar, attn_wg ? WAIT_ALL : WAIT_OLDER);
     {
-      // wave 0 alone reads the other workgroups' outputs: the loader waves' queues hold the
-      // FFN1 DMA, and their loads would retire behind it
-      float bo = 0.f, ro = 0.f;
-      if (wv == 0) {
-        const int ocol = w * NPO + (lane & (NPO - 1));
-        bo = bf2f(Ly.bo[ocol]);
-        ro = bf2f(rin[ocol]);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int g = lane + 64 * r, h = g >> 4, d0 = (g & 15) * 8;
-          const float* base = part + (long)h * a.nsplit * PSTRIDE;
-          float M = -INFINITY;
-          for (int s = 0; s < a.nsplit; ++s) M = fmaxf(M, ldf(base + s * PSTRIDE + D));
-          float lt = 0.f, o[8];
-#pragma unroll
-          for (int i = 0; i < 8; ++i) o[i] = 0.f;
-          for (int s = 0; s < a.nsplit; ++s) {
-            const u64 ml = ld64(base + s * PSTRIDE + D);
-            const float ms = __uint_as_float((unsigned)ml);
-            if (ms == -INFINITY) continue;
-            const float e = exp2f(ms - M);
-            lt += e * __uint_as_float((unsigned)(ml >> 32));
-#pragma unroll
-            for (int i = 0; i < 8; i += 2) {
-              const u64 u = ld64(base + s * PSTRIDE + d0 + i);
-              o[i] += e * __uint_as_float((unsigned)u);
-              o[i + 1] += e * __uint_as_float((unsigned)(u >> 32));
-            }
-          }
-          const float inv = 1.f / lt;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) xo[g * 8 + i] = bf2f(f2bf(o[i] * inv));
-        }
-      }
-      __syncthreads();
+      const int ocol = w * NPO + (lane & (NPO - 1));
+      const float bo = bf2f(Ly.bo[ocol]), ro = bf2f(rin[ocol]);
       float x[1][8];
+      {
+        const int h = tid >> 4, d0 = (tid & 15) * 8;
+        const float* base = part + (long)h * a.nsplit * PSTRIDE;
+        // online combine, eight splits' partials requested at once (no load waits on another)
+        float M = -INFINITY, lt = 0.f, o[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) x[0][i] = xo[tid * 8 + i];
+        for (int i = 0; i < 8; ++i) o[i] = 0.f;
+        for (int s0 = 0; s0 < a.nsplit; s0 += 8) {
+          u64 ml[8], ov[8][4];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const float* ps = base + min(s0 + t, a.nsplit - 1) * PSTRIDE;
+            ml[t] = ld64(ps + D);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ov[t][i] = ld64(ps + d0 + 2 * i);
+          }
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            const float ms = __uint_as_float((unsigned)ml[t]);
+            if (s0 + t >= a.nsplit || ms == -INFINITY) continue;
+            const float nM = fmaxf(M, ms), c = exp2f(M - nM), e = exp2f(ms - nM);
+            lt = lt * c + e * __uint_as_float((unsigned)(ml[t] >> 32));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              o[2 * i] = o[2 * i] * c + e * __uint_as_float((unsigned)ov[t][i]);
+              o[2 * i + 1] = o[2 * i + 1] * c + e * __uint_as_float((unsigned)(ov[t][i] >> 32));
+            }
+            M = nM;
+          }
+        }
+        const float inv = 1.f / lt;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[0][i] = bf2f(f2bf(o[i] * inv));
+      }
+      if (attn_wg) prefetch(w1s, 0, FFN1_PRE, wl, wv, lane);
       tmark(a, nbar, 1);
       const float y = gemv_lds<NPO, 1>(wl + OUT_OFF, x, red, tid, [] {}, [&] {
         prefetch(w1s, FFN1_PRE, NP1 * E * 2, wl, wv, lane);

@@ -83,9 +83,10 @@ class MegaDecoder:
         self.nl = len(rows)
         self.maxS = gen.max_seq_len
         # attention splits (≤ 256 keys each, Hq·nsplit ≤ 256). More splits shorten the attention
-        # phase but lengthen the partial combine of the out-projection prologue by more
-        # (measured at 8 vs 4: attention −2.1 µs, combine +2.5 µs per layer)
-        self.nsplit = min(16, max(int(os.environ.get("PIAMD_MEGA_NSPLIT", "1")),
+        # phase; the out-projection prologue requests 8 splits' partials at once, so up to 8 the
+        # combine stays one load round (round 4, 24 layers: 8 splits 989 µs kernel vs 1 split
+        # 1066, 4 splits 1019, 16 splits 1044; profiles/decode_mega_r4.txt)
+        self.nsplit = min(16, max(int(os.environ.get("PIAMD_MEGA_NSPLIT", "8")),
                                   math.ceil(self.maxS / 256)))
         # one slot per layer (and per residual update) for every vector handed between
         # workgroups: each address is written once per launch, so readers may use cached loads

@@ -78,6 +78,7 @@ struct MegaArgs {
   const int* pos;       // [1] cache slot of the new token
   u64* trace;           // nullable: [NWG][5·nl][4] wall-clock (100 MHz): phase start, prologue done,
                         // GEMV done, barrier arrival
+  int late_dma;         // 1: the FFN phases issue the next slice only after their GEMV (A/B knob)
 };
 
 __device__ __forceinline__ u64 ld64(const void* p) { return *reinterpret_cast<const u64*>(p); }
@@ -457,8 +458,9 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
       ln_prologue(a, rmid, Ly.ln2_g, Ly.ln2_b, x, wred, tid);
       tmark(a, nbar, 1);
       const bf16_t* w2s = Ly.w2 + (long)w * NP2 * F;
-      const float y = gemv_lds<NP1, 1>(wl, x, red, tid, [&] { prefetch(w2s, 0, WBYTES / 2, wl, wv, lane); },
-                                       [&] { prefetch(w2s, WBYTES / 2, WBYTES, wl, wv, lane); });
+      const int mid = a.late_dma ? 0 : WBYTES / 2;
+      const float y = gemv_lds<NP1, 1>(wl, x, red, tid, [&] { prefetch(w2s, 0, mid, wl, wv, lane); },
+                                       [&] { prefetch(w2s, mid, WBYTES, wl, wv, lane); });
       tmark(a, nbar, 2);
       if (wv == 0) {
         const float t = y + b1;
@@ -478,8 +480,9 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
       for (int j = 0; j < 4; ++j) ld_bf8(hb + (j * 256 + tid) * 8, x[j]);
       tmark(a, nbar, 1);
       const bf16_t* nq = l + 1 < a.nl ? a.layers[l + 1].wqkv + (long)w * NPQ * E : nullptr;
-      const float y = gemv_lds<NP2, 4>(wl, x, red, tid, [&] { prefetch(nq, 0, WBYTES / 2, wl, wv, lane); },
-                                       [&] { prefetch(nq, WBYTES / 2, OUT_OFF, wl, wv, lane); });
+      const int mid = a.late_dma ? 0 : WBYTES / 2;
+      const float y = gemv_lds<NP2, 4>(wl, x, red, tid, [&] { prefetch(nq, 0, mid, wl, wv, lane); },
+                                       [&] { prefetch(nq, mid, OUT_OFF, wl, wv, lane); });
       tmark(a, nbar, 2);
       if (wv == 0) {
         publish_bf16(rout + w * NP2, y + b2 + rm, lane, NP2);

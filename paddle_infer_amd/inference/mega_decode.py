@@ -102,6 +102,11 @@ class MegaDecoder:
         self.act = 1 if gen.act == "gelu_tanh" else 0
         self.eps = float(gen.cfg.layer_norm_eps)
         self.trace = None  # set to a zeroed int64 [256, 5·nl, 4] tensor to record phase times
+        # FFN phases issue the next weight slice only after their GEMV (1, default) or half of it
+        # at the GEMV midpoint (0): the loader waves are compute waves too, and a 64 KiB DMA burst
+        # stalls their issue for ~2 us (FFN1 / FFN2 GEMV 5.1 / 4.5 us -> 2.7 / 1.8 us late; kernel
+        # 985 -> 956 us, profiles/decode_mega_r4.txt)
+        self.late_dma = int(os.environ.get("PIAMD_MEGA_LATE_DMA", "1"))
         # greedy tail (decode_head_kernel): LM head + argmax + bookkeeping + next embedding
         self.head_ok = _lib.has("piamd_decode_head_greedy") and self._head_tables(gen)
         self.best = torch.zeros(8 * 32, dtype=torch.int64, device=dev)
@@ -148,7 +153,7 @@ class MegaDecoder:
                           self.eps, (1.0 / math.sqrt(D)) * 1.4426950408889634, resid.data_ptr(),
                           self.rbuf.data_ptr(), self.qn.data_ptr(), self.kvn.data_ptr(), self.part.data_ptr(),
                           self.h.data_ptr(), self.bar.data_ptr(), self.err.data_ptr(),
-                          pos.data_ptr(), _lib.ptr(self.trace))
+                          pos.data_ptr(), _lib.ptr(self.trace), self.late_dma)
         _lib.call("piamd_decode_mega", ctypes.byref(a), E, D, HQ, HK, F, _lib.stream())
         return self.rbuf[-1]
 

@@ -92,7 +92,7 @@ class MegaArgs(ctypes.Structure):
     _fields_ = ([("layers", c_void_p)] + [(n, c_int) for n in ("nl", "maxS", "nsplit", "act")]
                 + [("eps", ctypes.c_float), ("scale_log2", ctypes.c_float)]
                 + [(n, c_void_p) for n in ("resid", "rbuf", "qn", "kvn", "part", "h", "bar", "err",
-                                        "pos", "trace")])
+                                        "pos", "trace")] + [("late_dma", c_int)])
 
 
 _SIGS["piamd_decode_mega"] = [ctypes.POINTER(MegaArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]

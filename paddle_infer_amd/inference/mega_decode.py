@@ -107,10 +107,20 @@ class MegaDecoder:
         # stalls their issue for ~2 us (FFN1 / FFN2 GEMV 5.1 / 4.5 us -> 2.7 / 1.8 us late; kernel
         # 985 -> 956 us, profiles/decode_mega_r4.txt)
         self.late_dma = int(os.environ.get("PIAMD_MEGA_LATE_DMA", "1"))
+        # 1 (default): the variant with a dedicated loader wave and a 16 KiB chunk ring
+        # (decode_mega_lw_kernel; kernel 946 vs 968 us, generate 1.042 vs 1.072 ms/token);
+        # 0: loader waves that are compute waves too (decode_mega_kernel)
+        self.loader = int(os.environ.get("PIAMD_MEGA_LOADER", "1"))
+        if self.loader and _lib.lib().piamd_decode_mega_supported() == 1 and not self._lw_ok():
+            self.loader = 0
         # greedy tail (decode_head_kernel): LM head + argmax + bookkeeping + next embedding
         self.head_ok = _lib.has("piamd_decode_head_greedy") and self._head_tables(gen)
         self.best = torch.zeros(8 * 32, dtype=torch.int64, device=dev)
         self.cnt = torch.zeros(9 * 64, dtype=torch.int32, device=dev)
+
+    @staticmethod
+    def _lw_ok() -> bool:
+        return _lib.has("piamd_decode_mega_lw_supported") and _lib.lib().piamd_decode_mega_lw_supported() == 1
 
     def _head_tables(self, gen) -> bool:
         m = gen.model
@@ -153,7 +163,7 @@ class MegaDecoder:
                           self.eps, (1.0 / math.sqrt(D)) * 1.4426950408889634, resid.data_ptr(),
                           self.rbuf.data_ptr(), self.qn.data_ptr(), self.kvn.data_ptr(), self.part.data_ptr(),
                           self.h.data_ptr(), self.bar.data_ptr(), self.err.data_ptr(),
-                          pos.data_ptr(), _lib.ptr(self.trace), self.late_dma)
+                          pos.data_ptr(), _lib.ptr(self.trace), self.late_dma, self.loader)
         _lib.call("piamd_decode_mega", ctypes.byref(a), E, D, HQ, HK, F, _lib.stream())
         return self.rbuf[-1]
 

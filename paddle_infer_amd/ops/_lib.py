@@ -92,7 +92,7 @@ class MegaArgs(ctypes.Structure):
     _fields_ = ([("layers", c_void_p)] + [(n, c_int) for n in ("nl", "maxS", "nsplit", "act")]
                 + [("eps", ctypes.c_float), ("scale_log2", ctypes.c_float)]
                 + [(n, c_void_p) for n in ("resid", "rbuf", "qn", "kvn", "part", "h", "bar", "err",
-                                        "pos", "trace")] + [("late_dma", c_int)])
+                                        "pos", "trace")] + [("late_dma", c_int), ("loader", c_int)])
 
 
 _SIGS["piamd_decode_mega"] = [ctypes.POINTER(MegaArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]
@@ -109,6 +109,7 @@ class HeadArgs(ctypes.Structure):
 
 _SIGS["piamd_decode_head_greedy"] = [ctypes.POINTER(HeadArgs), c_int, c_void_p]
 _SIGS["piamd_decode_mega_supported"] = []
+_SIGS["piamd_decode_mega_lw_supported"] = []
 _SIGS["piamd_fa_fwd"] = [ctypes.POINTER(FaArgs), c_int, c_void_p]
 _SIGS["piamd_fa_bwd"] = [ctypes.POINTER(FaArgs), c_int, c_void_p]
 _SIGS["piamd_layernorm_bwd_ws"] = [c_int, c_int]

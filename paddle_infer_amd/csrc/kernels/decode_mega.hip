@@ -524,7 +524,7 @@ constexpr unsigned LW_SPIN = 1u << 22;
 __global__ __launch_bounds__(LW_NT, 1) void decode_mega_lw_kernel(MegaArgs a) {
   __shared__ __attribute__((aligned(1024))) char ring[RSLOTS * RCH];
   __shared__ float red[4 * 32];
-  __shared__ float wred[8];
+  __shared__ float wred[2][8];  // block reductions, alternating buffers (one wbar each)
   __shared__ float sc[256];
   __shared__ float pv[4][D];
   __shared__ unsigned ctr[4];  // [0] compute-wave barrier arrivals, [1] chunks consumed ×4, [2] chunks landed, [3] timeout
@@ -608,21 +608,38 @@ __global__ __launch_bounds__(LW_NT, 1) void decode_mega_lw_kernel(MegaArgs a) {
     }
     asm volatile("" ::: "memory");
   };
+  // Block reductions over the 4 compute waves with ONE wbar each: consecutive reductions use
+  // alternating buffers, and a wave rewrites a buffer only after the next reduction's wbar, which
+  // every wave reaches after reading this one.
+  int rb = 0;
+  auto bsum2 = [&](float u, float v, float& su, float& sv) {
+    u = wave_sum(u);
+    v = wave_sum(v);
+    float* b = wred[rb];
+    rb ^= 1;
+    if (lane == 0) {
+      b[2 * wv] = u;
+      b[2 * wv + 1] = v;
+    }
+    wbar();
+    su = b[0] + b[2] + b[4] + b[6];
+    sv = b[1] + b[3] + b[5] + b[7];
+  };
   auto bsum = [&](float v) {
     v = wave_sum(v);
-    if (lane == 0) wred[wv] = v;
+    float* b = wred[rb];
+    rb ^= 1;
+    if (lane == 0) b[wv] = v;
     wbar();
-    const float t = wred[0] + wred[1] + wred[2] + wred[3];
-    wbar();
-    return t;
+    return b[0] + b[1] + b[2] + b[3];
   };
   auto bmax = [&](float v) {
     v = wave_max(v);
-    if (lane == 0) wred[wv] = v;
+    float* b = wred[rb];
+    rb ^= 1;
+    if (lane == 0) b[wv] = v;
     wbar();
-    const float t = fmaxf(fmaxf(wred[0], wred[1]), fmaxf(wred[2], wred[3]));
-    wbar();
-    return t;
+    return fmaxf(fmaxf(b[0], b[1]), fmaxf(b[2], b[3]));
   };
   auto pstart = [&](unsigned ph) {
     wbar();
@@ -664,9 +681,9 @@ __global__ __launch_bounds__(LW_NT, 1) void decode_mega_lw_kernel(MegaArgs a) {
     for (int o = 32 >> LOGP; o > 0; o >>= 1) acc[0] += __shfl_xor(acc[0], o, 64);
     if ((lane & ((64 >> LOGP) - 1)) == 0) red[wv * P + (lane >> (6 - LOGP))] = acc[0];
     wbar();
+    // (red is rewritten only by the next GEMV, behind at least the next phase's wbar)
     float r = 0.f;
     if (tid < NPW) r = red[tid] + red[P + tid] + red[2 * P + tid] + red[3 * P + tid];
-    wbar();  // red is rewritten by the next GEMV
     return r;
   };
   auto ln_x = [&](const bf16_t* r, const bf16_t* gm, const bf16_t* bt, float (&x)[1][8]) {
@@ -674,14 +691,17 @@ __global__ __launch_bounds__(LW_NT, 1) void decode_mega_lw_kernel(MegaArgs a) {
     const u16x8 bb = *reinterpret_cast<const u16x8*>(bt + tid * 8);
     float v[8];
     ld_bf8(r + tid * 8, v);
-    float s = 0.f;
+    // one reduction of (Σv, Σv²): var = E[v²] − mean² (f32 over 2048 bf16 values)
+    float s = 0.f, q = 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) s += v[i];
-    const float mean = bsum(s) * (1.f / E);
-    float q = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) q += (v[i] - mean) * (v[i] - mean);
-    const float rs = rsqrtf(bsum(q) * (1.f / E) + a.eps);
+    for (int i = 0; i < 8; ++i) {
+      s += v[i];
+      q += v[i] * v[i];
+    }
+    float S, Q;
+    bsum2(s, q, S, Q);
+    const float mean = S * (1.f / E);
+    const float rs = rsqrtf(fmaxf(Q * (1.f / E) - mean * mean, 0.f) + a.eps);
 #pragma unroll
     for (int i = 0; i < 8; ++i) x[0][i] = bf2f(f2bf((v[i] - mean) * rs * bf2f(gg[i]) + bf2f(bb[i])));
   };

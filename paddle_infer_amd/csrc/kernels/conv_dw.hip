@@ -280,6 +280,132 @@ __global__ __launch_bounds__(256) void dconv_wgrad_reduce(const float* __restric
   if (ty == 0 && i < n) out[(long long)blockIdx.y * n + i] = (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]);
 }
 
+// Depthwise 3×3 weight gradient (pad 1, dilation 1, stride ST ∈ {1, 2}; 16-bit NHWC, C % 8 == 0):
+// the generic kernel above reloads x for every tap (10 loads per output pixel) and walks pixels
+// in a scattered order, ~0.2-0.6 TB/s at MobileNetV2 shapes (tools/bench_dwconv.py). Here a thread
+// owns 8 channels of one segment of an output row and slides a 3×3 window of x along it: per
+// output pixel 1 (stride 1) or 2 (stride 2) new x columns of 3 rows + one dy vector, 72 FMAs into
+// 72 f32 accumulators. Thread → (channel vector cv = tid mod NCVP, work slot = (n, p, segment));
+// the SL = 256 / NCVP slots of a workgroup are reduced through LDS in a fixed tree and each
+// workgroup writes one partial plane [9][C] (summed in a fixed order by dconv_wgrad_reduce /
+// finish): deterministic, no atomics.
+template <int DT, int ST>
+__global__ __launch_bounds__(256) void dw3_wgrad_kernel(const unsigned short* __restrict__ x,
+                                                        const unsigned short* __restrict__ dy,
+                                                        float* __restrict__ ws, DGeom g, int ncv_log2,
+                                                        int segs, int qs) {
+  __shared__ float red[128 * 72];  // half of the slots' partials (36 KiB)
+  const int NCVP = 1 << ncv_log2, SL = 256 >> ncv_log2;
+  const int tid = threadIdx.x, cv = tid & (NCVP - 1), sl = tid >> ncv_log2;
+  const int C = g.Cout, ncv = C >> 3;
+  const long long wi = (long long)blockIdx.x * SL + sl;
+  const long long nwork = (long long)g.N * g.OH * segs;
+  float acc[9][8];
+#pragma unroll
+  for (int a = 0; a < 9; ++a)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[a][j] = 0.f;
+  if (cv < ncv && wi < nwork) {
+    const int seg = (int)(wi % segs);
+    const long long np = wi / segs;
+    const int p = (int)(np % g.OH), n = (int)(np / g.OH);
+    const int q0 = seg * qs, q1 = min(g.OW, q0 + qs);
+    const int c0 = cv * 8;
+    const unsigned short* xr[3];
+    bool rv[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int ih = p * ST - 1 + r;
+      rv[r] = ih >= 0 && ih < g.H;
+      xr[r] = x + ((long long)n * g.H + (rv[r] ? ih : 0)) * g.W * C + c0;
+    }
+    auto ldx = [&](int r, int iw) {
+      u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (rv[r] && iw >= 0 && iw < g.W) v = *reinterpret_cast<const u16x8*>(xr[r] + (long long)iw * C);
+      return v;
+    };
+    u16x8 w0[3], w1[3], w2[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      w0[r] = ldx(r, q0 * ST - 1);
+      w1[r] = ldx(r, q0 * ST);
+    }
+    const unsigned short* dyr = dy + (((long long)n * g.OH + p) * g.OW) * C + c0;
+    for (int q = q0; q < q1; ++q) {
+#pragma unroll
+      for (int r = 0; r < 3; ++r) w2[r] = ldx(r, q * ST + 1);
+      const u16x8 d = *reinterpret_cast<const u16x8*>(dyr + (long long)q * C);
+      float dv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dv[j] = h2f<DT == 2>(d[j]);
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          acc[r * 3][j] = fmaf(dv[j], h2f<DT == 2>(w0[r][j]), acc[r * 3][j]);
+          acc[r * 3 + 1][j] = fmaf(dv[j], h2f<DT == 2>(w1[r][j]), acc[r * 3 + 1][j]);
+          acc[r * 3 + 2][j] = fmaf(dv[j], h2f<DT == 2>(w2[r][j]), acc[r * 3 + 2][j]);
+        }
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        if (ST == 1) {
+          w0[r] = w1[r];
+          w1[r] = w2[r];
+        } else {  // next window: columns 2q+1 (= this w2), 2q+2, 2q+3
+          w0[r] = w2[r];
+          w1[r] = ldx(r, (q + 1) * ST);
+        }
+      }
+    }
+  }
+  constexpr int A = 72;
+  float* out = ws + (long long)blockIdx.x * 9 * C;
+  auto store = [&](int cvv, int a, float v) {
+    if (cvv < ncv) out[(long long)(a >> 3) * C + cvv * 8 + (a & 7)] = v;
+  };
+  if (SL == 1) {
+#pragma unroll
+    for (int a = 0; a < A; ++a) store(cv, a, acc[a >> 3][a & 7]);
+    return;
+  }
+  const int half = SL / 2;
+  if (sl >= half) {
+    float* d = red + ((sl - half) * NCVP + cv) * A;
+#pragma unroll
+    for (int a = 0; a < A; ++a) d[a] = acc[a >> 3][a & 7];
+  }
+  __syncthreads();
+  if (sl < half) {
+    float* d = red + (sl * NCVP + cv) * A;
+#pragma unroll
+    for (int a = 0; a < A; ++a) d[a] += acc[a >> 3][a & 7];
+  }
+  __syncthreads();
+  for (int h = half / 2; h >= 1; h >>= 1) {
+    for (int e = tid; e < h * NCVP * A; e += 256) red[e] += red[e + h * NCVP * A];
+    __syncthreads();
+  }
+  for (int e = tid; e < NCVP * A; e += 256) store(e / A, e % A, red[e]);
+}
+
+// Work split of dw3_wgrad_kernel: row segments of ≤ 16 output columns; parts = workgroups.
+static void dw3_split(const DGeom& g, int& ncv_log2, int& segs, int& qs, long long& parts) {
+  const int ncv = g.Cout / 8;
+  ncv_log2 = 0;
+  while ((1 << ncv_log2) < ncv) ++ncv_log2;
+  segs = (g.OW + 15) / 16;
+  qs = (g.OW + segs - 1) / segs;
+  const long long nwork = (long long)g.N * g.OH * segs;
+  const int SL = 256 >> ncv_log2;
+  parts = (nwork + SL - 1) / SL;
+}
+
+static bool dw3_ok(const DGeom& g, int dtype) {
+  return dtype != 0 && g.cin_g == 1 && g.cout_g == 1 && g.R == 3 && g.S == 3 && g.pad_h == 1 &&
+         g.pad_w == 1 && g.dil_h == 1 && g.dil_w == 1 && g.st_h == g.st_w && (g.st_h == 1 || g.st_h == 2) &&
+         g.Cout % 8 == 0 && g.Cout / 8 <= 256;
+}
+
 template <int DT, int V, bool DW, bool TR>
 void launch_fwd(const void* x, const void* w, const void* b, void* y, const DGeom& g,
                 hipStream_t st) {
@@ -347,6 +473,19 @@ static void launch_wg(const void* x, const void* dy, float* ws, const DGeom& g, 
                      cb_log2, per, M);
 }
 
+// Partial planes the depthwise-3×3 weight-gradient path needs for this geometry (0: the generic
+// kernel serves it and takes any `parts`).
+PIAMD_EXPORT long long piamd_dconv2d_wgrad_parts(int N, int H, int W, int C, int OH, int OW, int K, int R,
+                                                 int S, int st_h, int st_w, int pad_h, int pad_w, int dil_h,
+                                                 int dil_w, int cin_g, int cout_g, int dtype) {
+  const DGeom g{N, H, W, C, OH, OW, K, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w, cin_g, cout_g};
+  if (!geom_ok(g) || !dw3_ok(g, dtype) || (long long)N * H * W * C >= (1LL << 40)) return 0;
+  int l2, segs, qs;
+  long long parts;
+  dw3_split(g, l2, segs, qs, parts);
+  return parts;
+}
+
 // dW' [R·S][cin_g][Cout] f32 of the forward conv (x [N][H][W][Cin], dy [N][OH][OW][Cout]);
 // ws: (parts + 64) · R·S·cin_g·Cout floats: the partial planes (parts ≥ 1 pixel chunks), then
 // room for the 64 slice sums of the two-level finish (used when parts > 128).
@@ -357,6 +496,19 @@ PIAMD_EXPORT int piamd_dconv2d_wgrad(const void* x, const void* dy, float* d, fl
   const DGeom g{N, H, W, Cin, OH, OW, Cout, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w, cin_g, cout_g};
   if (!geom_ok(g) || dtype < 0 || dtype > 2 || parts < 1 || !ws || !d) return (int)hipErrorInvalidValue;
   const bool dw = cin_g == 1 && cout_g == 1;
+  if (dw3_ok(g, dtype)) {
+    int l2, segs, qs;
+    long long np;
+    dw3_split(g, l2, segs, qs, np);
+    if (np != parts) return (int)hipErrorInvalidValue;  // ws sized by piamd_dconv2d_wgrad_parts
+    if (dtype == 1) {
+      if (st_h == 1) hipLaunchKernelGGL((dw3_wgrad_kernel<1, 1>), dim3((unsigned)np), dim3(256), 0, st, (const unsigned short*)x, (const unsigned short*)dy, ws, g, l2, segs, qs);
+      else hipLaunchKernelGGL((dw3_wgrad_kernel<1, 2>), dim3((unsigned)np), dim3(256), 0, st, (const unsigned short*)x, (const unsigned short*)dy, ws, g, l2, segs, qs);
+    } else {
+      if (st_h == 1) hipLaunchKernelGGL((dw3_wgrad_kernel<2, 1>), dim3((unsigned)np), dim3(256), 0, st, (const unsigned short*)x, (const unsigned short*)dy, ws, g, l2, segs, qs);
+      else hipLaunchKernelGGL((dw3_wgrad_kernel<2, 2>), dim3((unsigned)np), dim3(256), 0, st, (const unsigned short*)x, (const unsigned short*)dy, ws, g, l2, segs, qs);
+    }
+  }
   const int v = pick_v(dtype, g, dw);
   const int ncol = (Cout / v) * cin_g;
   int cb_log2 = 0;
@@ -366,6 +518,7 @@ PIAMD_EXPORT int piamd_dconv2d_wgrad(const void* x, const void* dy, float* d, fl
   const long long per = (M + parts - 1) / parts;
   const dim3 grid((unsigned)parts, (unsigned)((ncol + (1 << cb_log2) - 1) >> cb_log2),
                   (unsigned)((R * S + WG_TAPS - 1) / WG_TAPS));
+  if (!dw3_ok(g, dtype)) {
 #define WG(DT, VV)                                                                                \
   do {                                                                                            \
     if (dw) launch_wg<DT, VV, true>(x, dy, ws, g, grid, cb_log2, per, M, st);                     \
@@ -379,6 +532,7 @@ PIAMD_EXPORT int piamd_dconv2d_wgrad(const void* x, const void* dy, float* d, fl
     if (v == 8) WG(2, 8); else WG(2, 1);
   }
 #undef WG
+  }
   const long long n = (long long)R * S * cin_g * Cout;
   if (parts > 2 * FIN_SLICES) {
     // two-level sum: the planes into FIN_SLICES slice sums (after the planes in ws), then those

@@ -73,7 +73,7 @@ _SIGS = {
 }
 
 
-_RESTYPES = {"piamd_layernorm_bwd_ws": ctypes.c_longlong}
+_RESTYPES = {"piamd_layernorm_bwd_ws": ctypes.c_longlong, "piamd_dconv2d_wgrad_parts": ctypes.c_longlong}
 
 
 class FaArgs(ctypes.Structure):
@@ -272,6 +272,7 @@ _SIGS["piamd_dconv2d"] = [c_void_p] * 4 + [c_int] * 19 + [c_void_p]
 # x, dy, d, ws, parts, N, H, W, Cin, OH, OW, Cout, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w,
 # cin_g, cout_g, dtype, stream
 _SIGS["piamd_dconv2d_wgrad"] = [c_void_p] * 4 + [c_int] * 19 + [c_void_p]
+_SIGS["piamd_dconv2d_wgrad_parts"] = [c_int] * 18
 # x, dy, zero, d, N, H, W, C, OH, OW, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w, Kout, tile_n,
 # ksplit, ws, accumulate, f16, stream
 _SIGS["piamd_conv2d_wgrad"] = [c_void_p] * 4 + [c_int] * 17 + [c_void_p, c_int, c_int, c_void_p]

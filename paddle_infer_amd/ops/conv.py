@@ -455,6 +455,11 @@ def _direct_wgrad(x, dy, R, S, st, pad, dil, C, K, groups=1):
     gy, gz, pl = -(-ncol // cb), -(-(R * S) // 9), 256 // cb
     plane = R * S * cg * K
     parts = max(1, min(-(-2048 // (gy * gz)), M // (pl * 8), (16 << 20) // plane))
+    # depthwise 3x3 (pad 1, stride 1/2, 16-bit): the sliding-window kernel fixes its own split
+    fast = _lib.lib().piamd_dconv2d_wgrad_parts(N, H, W, C, OH, OW, K, R, S, st[0], st[1], pad[0], pad[1],
+                                               dil[0], dil[1], cg, kg, _DT[x.dtype])
+    if fast > 0:
+        parts = int(fast)
     d = torch.empty(plane, dtype=torch.float32, device=x.device)
     ws = torch.empty((parts + 64) * plane, dtype=torch.float32, device=x.device)  # + slice sums
     _lib.call("piamd_dconv2d_wgrad", x.data_ptr(), dy.data_ptr(), d.data_ptr(), ws.data_ptr(), parts,

@@ -58,6 +58,11 @@ def _check(dt, N, C, H, W, K, R, st, pad, dil, groups, nchw=False, bias=True):
     (2, 40, 12, 12, 40, 5, 1, 2, 1),      # 5x5: two tap slices in the weight gradient
     (1, 24, 13, 11, 24, 3, 1, 2, 2),      # dilation 2
     (2, 16, 10, 10, 32, 3, 1, 1, 1),      # channel multiplier 2
+    # sliding-window 3x3 weight gradient (dw3_wgrad_kernel): row segments, 1..120 channel vectors
+    (2, 8, 9, 37, 8, 3, 1, 1, 1),         # one channel vector, 3 row segments of 13
+    (1, 960, 7, 7, 960, 3, 1, 1, 1),      # 120 channel vectors (2 slots per workgroup)
+    (2, 144, 34, 34, 144, 3, 2, 1, 1),    # stride 2, even size, 2 segments
+    (3, 48, 20, 33, 48, 3, 2, 1, 1),      # stride 2, non-square
 ])
 def test_depthwise(dt, shape):
     N, C, H, W, K, R, st, pad, dil = shape

@@ -22,6 +22,8 @@
 // plane, summed in a fixed order by dconv_wgrad_finish (deterministic, no atomics).
 #include "common.h"
 
+#include <cstdlib>
+
 namespace {
 
 struct DGeom {
@@ -289,28 +291,34 @@ __global__ __launch_bounds__(256) void dconv_wgrad_reduce(const float* __restric
 // the SL = 256 / NCVP slots of a workgroup are reduced through LDS in a fixed tree and each
 // workgroup writes one partial plane [9][C] (summed in a fixed order by dconv_wgrad_reduce /
 // finish): deterministic, no atomics.
-template <int DT, int ST>
+template <int V> struct DwVec;
+template <> struct DwVec<8> { typedef u16x8 T; };
+template <> struct DwVec<4> { typedef u16x4 T; };
+
+template <int DT, int ST, int V>
 __global__ __launch_bounds__(256) void dw3_wgrad_kernel(const unsigned short* __restrict__ x,
                                                         const unsigned short* __restrict__ dy,
                                                         float* __restrict__ ws, DGeom g, int ncv_log2,
                                                         int segs, int qs) {
-  __shared__ float red[128 * 72];  // half of the slots' partials (36 KiB)
+  typedef typename DwVec<V>::T VT;
+  constexpr int A = 9 * V;
+  __shared__ float red[128 * A];  // half of the slots' partials
   const int NCVP = 1 << ncv_log2, SL = 256 >> ncv_log2;
   const int tid = threadIdx.x, cv = tid & (NCVP - 1), sl = tid >> ncv_log2;
-  const int C = g.Cout, ncv = C >> 3;
+  const int C = g.Cout, ncv = C / V;
   const long long wi = (long long)blockIdx.x * SL + sl;
   const long long nwork = (long long)g.N * g.OH * segs;
-  float acc[9][8];
+  float acc[9][V];
 #pragma unroll
   for (int a = 0; a < 9; ++a)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[a][j] = 0.f;
+    for (int j = 0; j < V; ++j) acc[a][j] = 0.f;
   if (cv < ncv && wi < nwork) {
     const int seg = (int)(wi % segs);
     const long long np = wi / segs;
     const int p = (int)(np % g.OH), n = (int)(np / g.OH);
     const int q0 = seg * qs, q1 = min(g.OW, q0 + qs);
-    const int c0 = cv * 8;
+    const int c0 = cv * V;
     const unsigned short* xr[3];
     bool rv[3];
 #pragma unroll
@@ -320,28 +328,39 @@ __global__ __launch_bounds__(256) void dw3_wgrad_kernel(const unsigned short* __
       xr[r] = x + ((long long)n * g.H + (rv[r] ? ih : 0)) * g.W * C + c0;
     }
     auto ldx = [&](int r, int iw) {
-      u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (rv[r] && iw >= 0 && iw < g.W) v = *reinterpret_cast<const u16x8*>(xr[r] + (long long)iw * C);
+      VT v = {};
+      if (rv[r] && iw >= 0 && iw < g.W) v = *reinterpret_cast<const VT*>(xr[r] + (long long)iw * C);
       return v;
     };
-    u16x8 w0[3], w1[3], w2[3];
+    const unsigned short* dyr = dy + (((long long)n * g.OH + p) * g.OW) * C + c0;
+    VT w0[3], w1[3], w2[3], nw1[3], nw2[3], nd;
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
       w0[r] = ldx(r, q0 * ST - 1);
       w1[r] = ldx(r, q0 * ST);
+      nw2[r] = ldx(r, q0 * ST + 1);
     }
-    const unsigned short* dyr = dy + (((long long)n * g.OH + p) * g.OW) * C + c0;
+    nd = *reinterpret_cast<const VT*>(dyr + (long long)q0 * C);
     for (int q = q0; q < q1; ++q) {
+      // this column's operands were requested one iteration ahead; request the next column's
+      const VT d = nd;
 #pragma unroll
-      for (int r = 0; r < 3; ++r) w2[r] = ldx(r, q * ST + 1);
-      const u16x8 d = *reinterpret_cast<const u16x8*>(dyr + (long long)q * C);
-      float dv[8];
+      for (int r = 0; r < 3; ++r) w2[r] = nw2[r];
+      if (q + 1 < q1) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dv[j] = h2f<DT == 2>(d[j]);
+        for (int r = 0; r < 3; ++r) {
+          if (ST == 2) nw1[r] = ldx(r, (q + 1) * ST);
+          nw2[r] = ldx(r, (q + 1) * ST + 1);
+        }
+        nd = *reinterpret_cast<const VT*>(dyr + (long long)(q + 1) * C);
+      }
+      float dv[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) dv[j] = h2f<DT == 2>(d[j]);
 #pragma unroll
       for (int r = 0; r < 3; ++r)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        for (int j = 0; j < V; ++j) {
           acc[r * 3][j] = fmaf(dv[j], h2f<DT == 2>(w0[r][j]), acc[r * 3][j]);
           acc[r * 3 + 1][j] = fmaf(dv[j], h2f<DT == 2>(w1[r][j]), acc[r * 3 + 1][j]);
           acc[r * 3 + 2][j] = fmaf(dv[j], h2f<DT == 2>(w2[r][j]), acc[r * 3 + 2][j]);
@@ -353,32 +372,31 @@ __global__ __launch_bounds__(256) void dw3_wgrad_kernel(const unsigned short* __
           w1[r] = w2[r];
         } else {  // next window: columns 2q+1 (= this w2), 2q+2, 2q+3
           w0[r] = w2[r];
-          w1[r] = ldx(r, (q + 1) * ST);
+          w1[r] = nw1[r];
         }
       }
     }
   }
-  constexpr int A = 72;
   float* out = ws + (long long)blockIdx.x * 9 * C;
   auto store = [&](int cvv, int a, float v) {
-    if (cvv < ncv) out[(long long)(a >> 3) * C + cvv * 8 + (a & 7)] = v;
+    if (cvv < ncv) out[(long long)(a / V) * C + cvv * V + (a % V)] = v;
   };
   if (SL == 1) {
 #pragma unroll
-    for (int a = 0; a < A; ++a) store(cv, a, acc[a >> 3][a & 7]);
+    for (int a = 0; a < A; ++a) store(cv, a, acc[a / V][a % V]);
     return;
   }
   const int half = SL / 2;
   if (sl >= half) {
     float* d = red + ((sl - half) * NCVP + cv) * A;
 #pragma unroll
-    for (int a = 0; a < A; ++a) d[a] = acc[a >> 3][a & 7];
+    for (int a = 0; a < A; ++a) d[a] = acc[a / V][a % V];
   }
   __syncthreads();
   if (sl < half) {
     float* d = red + (sl * NCVP + cv) * A;
 #pragma unroll
-    for (int a = 0; a < A; ++a) d[a] += acc[a >> 3][a & 7];
+    for (int a = 0; a < A; ++a) d[a] += acc[a / V][a % V];
   }
   __syncthreads();
   for (int h = half / 2; h >= 1; h >>= 1) {
@@ -388,9 +406,19 @@ __global__ __launch_bounds__(256) void dw3_wgrad_kernel(const unsigned short* __
   for (int e = tid; e < NCVP * A; e += 256) store(e / A, e % A, red[e]);
 }
 
+// channels per thread of dw3_wgrad_kernel (PIAMD_DW3_V = 4 or 8; 4 by default: half the
+// accumulators, more waves in flight)
+static int dw3_v() {
+  static const int v = [] {
+    const char* e = getenv("PIAMD_DW3_V");
+    return e && atoi(e) == 8 ? 8 : 4;
+  }();
+  return v;
+}
+
 // Work split of dw3_wgrad_kernel: row segments of ≤ 16 output columns; parts = workgroups.
 static void dw3_split(const DGeom& g, int& ncv_log2, int& segs, int& qs, long long& parts) {
-  const int ncv = g.Cout / 8;
+  const int ncv = g.Cout / dw3_v();
   ncv_log2 = 0;
   while ((1 << ncv_log2) < ncv) ++ncv_log2;
   segs = (g.OW + 15) / 16;
@@ -403,7 +431,7 @@ static void dw3_split(const DGeom& g, int& ncv_log2, int& segs, int& qs, long lo
 static bool dw3_ok(const DGeom& g, int dtype) {
   return dtype != 0 && g.cin_g == 1 && g.cout_g == 1 && g.R == 3 && g.S == 3 && g.pad_h == 1 &&
          g.pad_w == 1 && g.dil_h == 1 && g.dil_w == 1 && g.st_h == g.st_w && (g.st_h == 1 || g.st_h == 2) &&
-         g.Cout % 8 == 0 && g.Cout / 8 <= 256;
+         g.Cout % dw3_v() == 0 && g.Cout / dw3_v() <= 256;
 }
 
 template <int DT, int V, bool DW, bool TR>
@@ -501,13 +529,18 @@ PIAMD_EXPORT int piamd_dconv2d_wgrad(const void* x, const void* dy, float* d, fl
     long long np;
     dw3_split(g, l2, segs, qs, np);
     if (np != parts) return (int)hipErrorInvalidValue;  // ws sized by piamd_dconv2d_wgrad_parts
+#define DW3(DT, ST, VV)                                                                           \
+  hipLaunchKernelGGL((dw3_wgrad_kernel<DT, ST, VV>), dim3((unsigned)np), dim3(256), 0, st,          \
+                     (const unsigned short*)x, (const unsigned short*)dy, ws, g, l2, segs, qs)
+    const bool v8 = dw3_v() == 8;
     if (dtype == 1) {
-      if (st_h == 1) hipLaunchKernelGGL((dw3_wgrad_kernel<1, 1>), dim3((unsigned)np), dim3(256), 0, st, (const unsigned short*)x, (const unsigned short*)dy, ws, g, l2, segs, qs);
-      else hipLaunchKernelGGL((dw3_wgrad_kernel<1, 2>), dim3((unsigned)np), dim3(256), 0, st, (const unsigned short*)x, (const unsigned short*)dy, ws, g, l2, segs, qs);
+      if (st_h == 1) { if (v8) DW3(1, 1, 8); else DW3(1, 1, 4); }
+      else { if (v8) DW3(1, 2, 8); else DW3(1, 2, 4); }
     } else {
-      if (st_h == 1) hipLaunchKernelGGL((dw3_wgrad_kernel<2, 1>), dim3((unsigned)np), dim3(256), 0, st, (const unsigned short*)x, (const unsigned short*)dy, ws, g, l2, segs, qs);
-      else hipLaunchKernelGGL((dw3_wgrad_kernel<2, 2>), dim3((unsigned)np), dim3(256), 0, st, (const unsigned short*)x, (const unsigned short*)dy, ws, g, l2, segs, qs);
+      if (st_h == 1) { if (v8) DW3(2, 1, 8); else DW3(2, 1, 4); }
+      else { if (v8) DW3(2, 2, 8); else DW3(2, 2, 4); }
     }
+#undef DW3
   }
   const int v = pick_v(dtype, g, dw);
   const int ncol = (Cout / v) * cin_g;

@@ -434,17 +434,27 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_nhwc8(const T* __restrict__
                                                            const float* __restrict__ mean,
                                                            const float* __restrict__ rstd,
                                                            long long M, int C, long long chunk,
-                                                           int act, float* __restrict__ part) {
+                                                           int act, float* __restrict__ part,
+                                                           const float* __restrict__ mscale,
+                                                           const float* __restrict__ mshift) {
   const int b = blockIdx.x, P = gridDim.x, t = threadIdx.x, G = C / 8;
   const int RB = G >= 256 ? 1 : 256 / G;
   const long long beg = b * chunk, end = min(M, beg + chunk);
+  // ReLU without a residual: the mask y > 0 is x·scale + shift > 0 with the forward's fold, so
+  // the output y is not read (one tensor less per element)
+  const bool xmask = act == 1 && mscale != nullptr;
   __shared__ float r1[256][9], r2[256][9];
   for (int g0 = 0; g0 < G; g0 += (G >= 256 ? 256 : G)) {
     const int cg = G >= 256 ? g0 + t : t % G, rl = G >= 256 ? 0 : t / G;
     const bool live = cg < G && rl < RB;
-    float s1[8], s2[8], mu[8];
+    float s1[8], s2[8], mu[8], msc[8], msh[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { s1[j] = s2[j] = 0.f; mu[j] = live ? mean[cg * 8 + j] : 0.f; }
+    for (int j = 0; j < 8; ++j) {
+      s1[j] = s2[j] = 0.f;
+      mu[j] = live ? mean[cg * 8 + j] : 0.f;
+      msc[j] = live && xmask ? mscale[cg * 8 + j] : 0.f;
+      msh[j] = live && xmask ? mshift[cg * 8 + j] : 0.f;
+    }
     if (live) {
       long long r = beg + rl;
       // RR rows per trip (2·RR or 3·RR independent 16-B loads in flight per lane)
@@ -455,11 +465,15 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_nhwc8(const T* __restrict__
           const long long i = (r + u * RB) * C + cg * 8;
           ld8(dy + i, g[u]);
           ld8(x + i, xv[u]);
-          if (act) ld8(y + i, yv[u]);
+          if (act && !xmask) ld8(y + i, yv[u]);
         }
 #pragma unroll
         for (int u = 0; u < RR; ++u) {
-          if (act) {
+          if (xmask) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              if (!(xv[u][j] * msc[j] + msh[j] > 0.f)) g[u][j] = 0.f;
+          } else if (act) {
 #pragma unroll
             for (int j = 0; j < 8; ++j)
               if (!(act == 1 ? yv[u][j] > 0.f : (yv[u][j] > 0.f && yv[u][j] < 6.f))) g[u][j] = 0.f;
@@ -473,7 +487,11 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_nhwc8(const T* __restrict__
         float g[8], xv[8];
         ld8(dy + i, g);
         ld8(x + i, xv);
-        if (act) {
+        if (xmask) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (!(xv[j] * msc[j] + msh[j] > 0.f)) g[j] = 0.f;
+        } else if (act) {
           float yv[8];
           ld8(y + i, yv);
 #pragma unroll
@@ -561,13 +579,24 @@ __global__ __launch_bounds__(256) void bn_bwd_apply8(const T* __restrict__ dy, c
                                                      const float* __restrict__ rstd,
                                                      const float* __restrict__ coef, T* __restrict__ dx,
                                                      T* __restrict__ dres, long long total, int C,
-                                                     int S, int nhwc, int act, int training) {
+                                                     int S, int nhwc, int act, int training,
+                                                     const float* __restrict__ mscale,
+                                                     const float* __restrict__ mshift) {
+  const bool xmask = act == 1 && mscale != nullptr;  // see bn_bwd_reduce_nhwc8
   for (long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 8; i < total;
        i += (long long)gridDim.x * blockDim.x * 8) {
     const int c = chan8(i, C, S, nhwc);
     float g[8], xv[8];
     ld8(dy + i, g);
-    if (act) {
+    if (xmask || training) ld8(x + i, xv);
+    if (xmask) {
+      float sc[8], sh[8];
+      coef8(mscale, c, nhwc, sc);
+      coef8(mshift, c, nhwc, sh);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (!(xv[j] * sc[j] + sh[j] > 0.f)) g[j] = 0.f;
+    } else if (act) {
       float yv[8];
       ld8(y + i, yv);
 #pragma unroll
@@ -579,7 +608,6 @@ __global__ __launch_bounds__(256) void bn_bwd_apply8(const T* __restrict__ dy, c
     coef8(coef, c, nhwc, A);
     if (training) {
       float B[8], D[8];
-      ld8(x + i, xv);
       coef8(coef + C, c, nhwc, B);
       coef8(coef + 2 * C, c, nhwc, D);
 #pragma unroll
@@ -625,17 +653,19 @@ PIAMD_EXPORT int piamd_bn_set_parts(long long elems_per_block, int max_parts) {
 // place (momentum: Paddle convention); else the running statistics (mean/rstd still written).
 // ws: f32 workspace of ≥ 2·C + 3·2048·C floats. act: 0 none, 1 relu, 2 relu6.
 // nhwc requires C % 8 == 0 (vectorised path), C ≥ 256 or C | 256.
-PIAMD_EXPORT int piamd_bn_fwd(int dtype, int nhwc, const void* x, const void* res, void* y, int N,
-                              int C, int S, const float* gamma, const float* beta,
-                              float* run_mean, float* run_var, float* mean, float* rstd,
-                              float momentum, float eps, int training, int act, float* ws,
-                              hipStream_t st) {
+// ss (nullable): f32 [2][C] receives the affine fold (scale, shift) for piamd_bn_bwd2's x-derived
+// ReLU mask; otherwise the fold lives in ws.
+PIAMD_EXPORT int piamd_bn_fwd2(int dtype, int nhwc, const void* x, const void* res, void* y, int N,
+                               int C, int S, const float* gamma, const float* beta,
+                               float* run_mean, float* run_var, float* mean, float* rstd,
+                               float momentum, float eps, int training, int act, float* ws, float* ss,
+                               hipStream_t st) {
   if (C < 1 || N < 1 || S < 1 || (nhwc && C % 8 && C < 256 && 256 % C))
     return (int)hipErrorInvalidValue;
   const long long M = (long long)N * S, total = M * C;
   const bool v8 = nhwc ? C % 8 == 0 : S % 8 == 0;
-  float* scale = ws;
-  float* shift = ws + C;
+  float* scale = ss ? ss : ws;
+  float* shift = scale + C;
   if (training) {
     const int P = nhwc && C % 8 == 0 ? parts_for8(M, C) : parts_for(M);
     const long long chunk = (M + P - 1) / P;
@@ -676,15 +706,28 @@ PIAMD_EXPORT int piamd_bn_fwd(int dtype, int nhwc, const void* x, const void* re
   return (int)hipGetLastError();
 }
 
+PIAMD_EXPORT int piamd_bn_fwd(int dtype, int nhwc, const void* x, const void* res, void* y, int N,
+                              int C, int S, const float* gamma, const float* beta,
+                              float* run_mean, float* run_var, float* mean, float* rstd,
+                              float momentum, float eps, int training, int act, float* ws,
+                              hipStream_t st) {
+  return piamd_bn_fwd2(dtype, nhwc, x, res, y, N, C, S, gamma, beta, run_mean, run_var, mean, rstd,
+                       momentum, eps, training, act, ws, nullptr, st);
+}
+
 // Backward. y = the forward OUTPUT (act' from it); dres (nullable) receives dz = ∂L/∂(bn + res).
 // training = 0: the statistics are constants (dx = γ·rstd·dz). dgamma / dbeta: f32 [C]
-// (nullable). ws: ≥ 3·C + 2·2048·C floats.
-PIAMD_EXPORT int piamd_bn_bwd(int dtype, int nhwc, const void* dy, const void* y, const void* x,
-                              void* dx, void* dres, int N, int C, int S, const float* gamma,
-                              const float* mean, const float* rstd, float* dgamma, float* dbeta,
-                              int training, int act, float* ws, hipStream_t st) {
+// (nullable). ws: ≥ 3·C + 2·2048·C floats. ss (nullable): the forward's fold from
+// piamd_bn_fwd2 — with ReLU, no residual and NHWC C % 8 == 0 the mask is x·scale + shift > 0
+// (the forward's own test) and y is not read.
+PIAMD_EXPORT int piamd_bn_bwd2(int dtype, int nhwc, const void* dy, const void* y, const void* x,
+                               void* dx, void* dres, int N, int C, int S, const float* gamma,
+                               const float* mean, const float* rstd, float* dgamma, float* dbeta,
+                               int training, int act, float* ws, const float* ss, hipStream_t st) {
   if (C < 1 || N < 1 || S < 1 || (nhwc && C % 8 && C < 256 && 256 % C))
     return (int)hipErrorInvalidValue;
+  const float* msc = act == 1 && !dres && ss && nhwc && C % 8 == 0 ? ss : nullptr;
+  const float* msh = msc ? ss + C : nullptr;
   const long long M = (long long)N * S, total = M * C;
   const bool v8 = nhwc ? C % 8 == 0 : S % 8 == 0;
   const int P = nhwc && C % 8 == 0 ? parts_for8(M, C) : parts_for(M);
@@ -692,8 +735,8 @@ PIAMD_EXPORT int piamd_bn_bwd(int dtype, int nhwc, const void* dy, const void* y
   float* coef = ws;
   float* part = ws + 3 * C;
   if (nhwc && C % 8 == 0) {
-    if (dtype) hipLaunchKernelGGL(bn_bwd_reduce_nhwc8<bf16_t>, dim3(P), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x, mean, rstd, M, C, chunk, act, part);
-    else hipLaunchKernelGGL(bn_bwd_reduce_nhwc8<float>, dim3(P), dim3(256), 0, st, (const float*)dy, (const float*)y, (const float*)x, mean, rstd, M, C, chunk, act, part);
+    if (dtype) hipLaunchKernelGGL(bn_bwd_reduce_nhwc8<bf16_t>, dim3(P), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x, mean, rstd, M, C, chunk, act, part, msc, msh);
+    else hipLaunchKernelGGL(bn_bwd_reduce_nhwc8<float>, dim3(P), dim3(256), 0, st, (const float*)dy, (const float*)y, (const float*)x, mean, rstd, M, C, chunk, act, part, msc, msh);
   } else if (nhwc) {
     if (dtype) hipLaunchKernelGGL(bn_bwd_reduce_nhwc<bf16_t>, dim3(P), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x, mean, rstd, M, C, chunk, act, part);
     else hipLaunchKernelGGL(bn_bwd_reduce_nhwc<float>, dim3(P), dim3(256), 0, st, (const float*)dy, (const float*)y, (const float*)x, mean, rstd, M, C, chunk, act, part);
@@ -708,11 +751,11 @@ PIAMD_EXPORT int piamd_bn_bwd(int dtype, int nhwc, const void* dy, const void* y
     if (dtype)
       hipLaunchKernelGGL(bn_bwd_apply8<bf16_t>, g8, dim3(256), 0, st, (const bf16_t*)dy,
                          (const bf16_t*)y, (const bf16_t*)x, mean, rstd, coef, (bf16_t*)dx,
-                         (bf16_t*)dres, total, C, S, nhwc, act, training);
+                         (bf16_t*)dres, total, C, S, nhwc, act, training, msc, msh);
     else
       hipLaunchKernelGGL(bn_bwd_apply8<float>, g8, dim3(256), 0, st, (const float*)dy,
                          (const float*)y, (const float*)x, mean, rstd, coef, (float*)dx,
-                         (float*)dres, total, C, S, nhwc, act, training);
+                         (float*)dres, total, C, S, nhwc, act, training, msc, msh);
     return (int)hipGetLastError();
   }
   const dim3 g(stride_grid(total, 256));
@@ -725,4 +768,12 @@ PIAMD_EXPORT int piamd_bn_bwd(int dtype, int nhwc, const void* dy, const void* y
                        (const float*)x, mean, rstd, coef, (float*)dx, (float*)dres, total, C, S,
                        nhwc, act, training);
   return (int)hipGetLastError();
+}
+
+PIAMD_EXPORT int piamd_bn_bwd(int dtype, int nhwc, const void* dy, const void* y, const void* x,
+                              void* dx, void* dres, int N, int C, int S, const float* gamma,
+                              const float* mean, const float* rstd, float* dgamma, float* dbeta,
+                              int training, int act, float* ws, hipStream_t st) {
+  return piamd_bn_bwd2(dtype, nhwc, dy, y, x, dx, dres, N, C, S, gamma, mean, rstd, dgamma, dbeta,
+                       training, act, ws, nullptr, st);
 }

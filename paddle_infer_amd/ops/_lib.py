@@ -266,6 +266,10 @@ _SIGS["piamd_bn_fwd"] = ([c_int, c_int] + [c_void_p] * 3 + [c_int] * 3 + [c_void
 _SIGS["piamd_bn_set_parts"] = [c_ll, c_int]
 _SIGS["piamd_bn_bwd"] = ([c_int, c_int] + [c_void_p] * 5 + [c_int] * 3 + [c_void_p] * 5
                          + [c_int, c_int, c_void_p, c_void_p])
+_SIGS["piamd_bn_fwd2"] = ([c_int, c_int] + [c_void_p] * 3 + [c_int] * 3 + [c_void_p] * 6
+                          + [c_float, c_float, c_int, c_int, c_void_p, c_void_p, c_void_p])
+_SIGS["piamd_bn_bwd2"] = ([c_int, c_int] + [c_void_p] * 5 + [c_int] * 3 + [c_void_p] * 5
+                          + [c_int, c_int, c_void_p, c_void_p, c_void_p])
 # in, w, bias, out, N, H, W, Cin, OH, OW, Cout, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w,
 # cin_g, cout_g, transposed, dtype, stream
 _SIGS["piamd_dconv2d"] = [c_void_p] * 4 + [c_int] * 19 + [c_void_p]

@@ -97,11 +97,15 @@ class _BNAct(torch.autograd.Function):
         if not training and (rm is None or rv is None):
             raise ValueError("eval-mode batch_norm needs f32 running statistics")
         _grid_once()
-        _lib.call("piamd_bn_fwd", int(x.dtype == torch.bfloat16), int(nhwc), xc.data_ptr(),
+        # ReLU without a residual: keep the affine fold so the backward derives the mask from x
+        # (x·scale + shift > 0, the forward's own test) instead of reading y
+        ss = (torch.empty(2 * C, device=dev, dtype=torch.float32)
+              if act == 1 and res is None and nhwc and C % 8 == 0 else None)
+        _lib.call("piamd_bn_fwd2", int(x.dtype == torch.bfloat16), int(nhwc), xc.data_ptr(),
                   _lib.ptr(res), y.data_ptr(), N, C, S, _lib.ptr(g), _lib.ptr(b), _lib.ptr(rm),
                   _lib.ptr(rv), mean.data_ptr(), rstd.data_ptr(), float(momentum), float(eps),
-                  int(training), int(act), ws.data_ptr(), _lib.stream())
-        ctx.save_for_backward(xc, y, g, mean, rstd)
+                  int(training), int(act), ws.data_ptr(), _lib.ptr(ss), _lib.stream())
+        ctx.save_for_backward(xc, y, g, mean, rstd, ss)
         ctx.meta = (training, act, nhwc, dims, residual is not None, weight, bias,
                     x.dim() == 4 and nhwc and not x.is_contiguous())
         if ctx.meta[-1]:
@@ -110,7 +114,7 @@ class _BNAct(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        xc, y, g, mean, rstd = ctx.saved_tensors
+        xc, y, g, mean, rstd, ss = ctx.saved_tensors
         training, act, nhwc, (N, C, S), has_res, weight, bias, cl_view = ctx.meta
         dyc = dy.permute(0, 2, 3, 1).contiguous() if cl_view else dy.contiguous()
         dx = torch.empty_like(xc)
@@ -118,10 +122,10 @@ class _BNAct(torch.autograd.Function):
         dg = torch.empty(C, device=xc.device, dtype=torch.float32)
         db = torch.empty(C, device=xc.device, dtype=torch.float32)
         ws = torch.empty(3 * C + 2 * _MAX_PARTS * C, device=xc.device, dtype=torch.float32)
-        _lib.call("piamd_bn_bwd", int(xc.dtype == torch.bfloat16), int(nhwc), dyc.data_ptr(),
+        _lib.call("piamd_bn_bwd2", int(xc.dtype == torch.bfloat16), int(nhwc), dyc.data_ptr(),
                   y.data_ptr(), xc.data_ptr(), dx.data_ptr(), _lib.ptr(dres), N, C, S, _lib.ptr(g),
                   mean.data_ptr(), rstd.data_ptr(), dg.data_ptr(), db.data_ptr(), int(training),
-                  int(act), ws.data_ptr(), _lib.stream())
+                  int(act), ws.data_ptr(), _lib.ptr(ss), _lib.stream())
         if cl_view:
             dx = dx.permute(0, 3, 1, 2)
             dres = dres.permute(0, 3, 1, 2) if dres is not None else None

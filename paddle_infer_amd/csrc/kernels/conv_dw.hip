@@ -416,6 +416,92 @@ static int dw3_v() {
   return v;
 }
 
+// Depthwise 3×3 forward (and the stride-1 data gradient, TR: the same window with the taps
+// flipped), pad 1, dilation 1, 16-bit NHWC: a thread owns V channels of one segment of an output
+// row, keeps the 9·V weights in registers and slides the 3×3 x window along the row — 1 (stride
+// 1) or 2 (stride 2) new x columns of 3 rows per output pixel instead of 9 gathered taps.
+template <int DT, int ST, int V, bool TR>
+__global__ __launch_bounds__(256) void dw3_fwd_kernel(const unsigned short* __restrict__ x,
+                                                      const unsigned short* __restrict__ w,
+                                                      const unsigned short* __restrict__ bias,
+                                                      unsigned short* __restrict__ y, DGeom g, int segs,
+                                                      int qs, long long items) {
+  typedef typename DwVec<V>::T VT;
+  const int C = g.Cout, ncv = C / V;
+  for (long long it = (long long)blockIdx.x * 256 + threadIdx.x; it < items; it += (long long)gridDim.x * 256) {
+    const int cv = (int)(it % ncv);
+    long long rest = it / ncv;
+    const int seg = (int)(rest % segs);
+    rest /= segs;
+    const int p = (int)(rest % g.OH), n = (int)(rest / g.OH);
+    const int c0 = cv * V, q0 = seg * qs, q1 = min(g.OW, q0 + qs);
+    float wt[9][V], b[V];
+#pragma unroll
+    for (int a = 0; a < 9; ++a) {
+      const VT u = *reinterpret_cast<const VT*>(w + (long long)(TR ? 8 - a : a) * C + c0);
+#pragma unroll
+      for (int j = 0; j < V; ++j) wt[a][j] = h2f<DT == 2>(u[j]);
+    }
+    if (bias) {
+      const VT u = *reinterpret_cast<const VT*>(bias + c0);
+#pragma unroll
+      for (int j = 0; j < V; ++j) b[j] = h2f<DT == 2>(u[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < V; ++j) b[j] = 0.f;
+    }
+    const unsigned short* xr[3];
+    bool rv[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int ih = p * ST - 1 + r;
+      rv[r] = ih >= 0 && ih < g.H;
+      xr[r] = x + ((long long)n * g.H + (rv[r] ? ih : 0)) * g.W * C + c0;
+    }
+    auto ldx = [&](int r, int iw) {
+      VT v = {};
+      if (rv[r] && iw >= 0 && iw < g.W) v = *reinterpret_cast<const VT*>(xr[r] + (long long)iw * C);
+      return v;
+    };
+    VT w0[3], w1[3], w2[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      w0[r] = ldx(r, q0 * ST - 1);
+      w1[r] = ldx(r, q0 * ST);
+    }
+    unsigned short* yr = y + (((long long)n * g.OH + p) * g.OW) * C + c0;
+    for (int q = q0; q < q1; ++q) {
+#pragma unroll
+      for (int r = 0; r < 3; ++r) w2[r] = ldx(r, q * ST + 1);
+      float o[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) o[j] = b[j];
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          o[j] = fmaf(wt[r * 3][j], h2f<DT == 2>(w0[r][j]), o[j]);
+          o[j] = fmaf(wt[r * 3 + 1][j], h2f<DT == 2>(w1[r][j]), o[j]);
+          o[j] = fmaf(wt[r * 3 + 2][j], h2f<DT == 2>(w2[r][j]), o[j]);
+        }
+      VT ov;
+#pragma unroll
+      for (int j = 0; j < V; ++j) ov[j] = f2h<DT == 2>(o[j]);
+      *reinterpret_cast<VT*>(yr + (long long)q * C) = ov;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        if (ST == 1) {
+          w0[r] = w1[r];
+          w1[r] = w2[r];
+        } else {
+          w0[r] = w2[r];
+          w1[r] = ldx(r, (q + 1) * ST);
+        }
+      }
+    }
+  }
+}
+
 // Work split of dw3_wgrad_kernel: row segments of ≤ 16 output columns; parts = workgroups.
 static void dw3_split(const DGeom& g, int& ncv_log2, int& segs, int& qs, long long& parts) {
   const int ncv = g.Cout / dw3_v();
@@ -479,6 +565,28 @@ PIAMD_EXPORT int piamd_dconv2d(const void* in, const void* w, const void* bias, 
   const DGeom g{N, H, W, Cin, OH, OW, Cout, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w, cin_g, cout_g};
   if (!geom_ok(g) || dtype < 0 || dtype > 2) return (int)hipErrorInvalidValue;
   const bool dw = cin_g == 1 && cout_g == 1, tr = transposed != 0;
+  // depthwise 3×3 pad 1: the sliding-window kernel (forward at stride 1 / 2, data gradient at
+  // stride 1, where the transposed geometry is the forward one with flipped taps)
+  if (dw3_ok(g, dtype) && (!tr || st_h == 1) && OW > 0) {
+    const int segs = (OW + 15) / 16, qs = (OW + segs - 1) / segs;
+    const int V = dw3_v();
+    const long long items = (long long)N * OH * segs * (Cout / V);
+    const long long nb = (items + 255) / 256;
+    const unsigned grid = (unsigned)(nb < (1 << 20) ? nb : (1 << 20));
+#define DWF(DT, ST, VV, TRV)                                                                        \
+  hipLaunchKernelGGL((dw3_fwd_kernel<DT, ST, VV, TRV>), dim3(grid), dim3(256), 0, st,                \
+                     (const unsigned short*)in, (const unsigned short*)w, (const unsigned short*)bias, \
+                     (unsigned short*)out, g, segs, qs, items)
+#define DWF_V(DT, ST, TRV) do { if (V == 8) DWF(DT, ST, 8, TRV); else DWF(DT, ST, 4, TRV); } while (0)
+    if (dtype == 1) {
+      if (tr) DWF_V(1, 1, true); else if (st_h == 1) DWF_V(1, 1, false); else DWF_V(1, 2, false);
+    } else {
+      if (tr) DWF_V(2, 1, true); else if (st_h == 1) DWF_V(2, 1, false); else DWF_V(2, 2, false);
+    }
+#undef DWF_V
+#undef DWF
+    return (int)hipGetLastError();
+  }
   const int v = pick_v(dtype, g, dw);
   if ((long long)N * OH * OW * (Cout / v) >= 0x7fffffffLL) return (int)hipErrorInvalidValue;
   if (dtype == 0) {

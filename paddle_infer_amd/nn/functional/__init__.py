@@ -246,6 +246,11 @@ def max_pool1d(x, kernel_size, stride=None, padding=0, return_mask=False, ceil_m
 
 def max_pool2d(x, kernel_size, stride=None, padding=0, return_mask=False, ceil_mode=False,
                data_format="NCHW", name=None):
+    if data_format == "NCHW":
+        from ...ops.pool import max_pool2d_nhwc, max_pool2d_supported
+        pad = _padding(padding, 2)
+        if max_pool2d_supported(x, kernel_size, stride, pad, ceil_mode, return_mask):
+            return max_pool2d_nhwc(x, kernel_size, stride, pad)  # own NHWC kernels (channels-last)
     y = TF.max_pool2d(_fmt_in(x, data_format), kernel_size, stride, _padding(padding, 2), 1, ceil_mode, return_mask)
     return y if return_mask else _fmt_out(y, data_format)
 

@@ -264,6 +264,8 @@ _SIGS["piamd_bn_fwd"] = ([c_int, c_int] + [c_void_p] * 3 + [c_int] * 3 + [c_void
                          + [c_float, c_float, c_int, c_int, c_void_p, c_void_p])
 # dtype, nhwc, dy, y, x, dx, dres, N, C, S, gamma, mean, rstd, dgamma, dbeta, training, act, ws, stream
 _SIGS["piamd_bn_set_parts"] = [c_ll, c_int]
+_SIGS["piamd_maxpool_fwd_nhwc"] = [c_void_p] * 3 + [c_int] * 13 + [c_void_p]
+_SIGS["piamd_maxpool_bwd_nhwc"] = [c_void_p] * 3 + [c_int] * 13 + [c_void_p]
 _SIGS["piamd_bn_bwd"] = ([c_int, c_int] + [c_void_p] * 5 + [c_int] * 3 + [c_void_p] * 5
                          + [c_int, c_int, c_void_p, c_void_p])
 _SIGS["piamd_bn_fwd2"] = ([c_int, c_int] + [c_void_p] * 3 + [c_int] * 3 + [c_void_p] * 6

@@ -38,18 +38,21 @@ def main():
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--iters", type=int, default=20)
     a = ap.parse_args()
-    from paddle_infer_amd.ops.conv import _direct_wgrad
-    tot = 0.0
+    from paddle_infer_amd.ops.conv import _direct, _direct_wgrad
+    tot = tot_f = 0.0
     for H, C, s in LAYERS:
         OH = (H + 2 - 3) // s + 1
         x = torch.randn(a.batch, H, H, C, device="cuda").bfloat16()
         dy = torch.randn(a.batch, OH, OH, C, device="cuda").bfloat16()
         ms = timed(lambda: _direct_wgrad(x, dy, 3, 3, (s, s), (1, 1), (1, 1), C, C, groups=C), a.iters)
         tot += ms
+        w = torch.randn(3, 3, 1, C, device="cuda").bfloat16()
+        msf = timed(lambda: _direct(x, w, None, OH, OH, C, 3, 3, (s, s), (1, 1), (1, 1), 1, 1, False), a.iters)
+        tot_f += msf
         gb = (x.numel() + dy.numel()) * 2 / 1e9
-        print(json.dumps({"H": H, "C": C, "stride": s, "wgrad_ms": round(ms, 4),
+        print(json.dumps({"H": H, "C": C, "stride": s, "wgrad_ms": round(ms, 4), "fwd_ms": round(msf, 4),
                           "min_bytes_GB": round(gb, 3), "GBps": round(gb / ms * 1e3, 1)}), flush=True)
-    print(json.dumps({"total_wgrad_ms": round(tot, 3)}))
+    print(json.dumps({"total_wgrad_ms": round(tot, 3), "total_fwd_ms": round(tot_f, 3)}))
 
 
 if __name__ == "__main__":

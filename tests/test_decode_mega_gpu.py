@@ -36,8 +36,10 @@ def _rel(a, b):
     return ((a - b).norm() / b.norm()).item()
 
 
+@pytest.mark.parametrize("loader", ["1", "0"])  # dedicated loader wave (default) / 4-wave kernel
 @pytest.mark.parametrize("max_seq,prompt", [(256, 37), (1024, 300)])
-def test_mega_decode_matches_per_op_path(max_seq, prompt):
+def test_mega_decode_matches_per_op_path(max_seq, prompt, loader, monkeypatch):
+    monkeypatch.setenv("PIAMD_MEGA_LOADER", loader)
     from paddle_infer_amd.inference import mega_decode
     from paddle_infer_amd.inference.generation import GPTGenerator
     m = _gpt13b_width(2, max_seq)
@@ -53,6 +55,7 @@ def test_mega_decode_matches_per_op_path(max_seq, prompt):
         tok = lb.argmax(-1)
         la, lb = g_mega.decode(tok, pos), g_ref.decode(tok, pos)
         assert isinstance(g_mega._mega, mega_decode.MegaDecoder)
+        assert g_mega._mega.loader == int(loader)
         assert _rel(la, lb) < 2e-2, (step, _rel(la, lb))
         for (ka, va), (kb, vb) in zip(g_mega.caches, g_ref.caches):
             p = int(pos[0])

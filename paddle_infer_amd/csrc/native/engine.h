@@ -9,6 +9,7 @@
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 namespace pdn {
@@ -118,6 +119,11 @@ struct Ctx {
   int threads = 1;
   int prec16 = 0;  // Config precision: 0 = as stored, VT_FP16 / VT_BF16 = 16-bit compute for fp32 models
   std::shared_ptr<FastState> fast;
+  // buffers whose contents live as long as the predictor (loaded parameters and the weight caches
+  // derived from them): the only sources the fast path's per-buffer caches may key on
+  std::shared_ptr<std::unordered_set<const Buffer*>> persist;
+  // load-time constants derived from parameters (e.g. folded batch-norm scale / shift), by key
+  std::shared_ptr<std::map<std::string, DTensor>> consts;
 };
 
 using Scope = std::unordered_map<std::string, DTensor>;
@@ -138,6 +144,8 @@ DTensor to_host(const DTensor& t, Ctx& c);
 void graph_begin(Ctx& c, std::vector<std::shared_ptr<Buffer>>* keep);
 void* graph_end(Ctx& c);  // instantiated executable graph
 void graph_launch(Ctx& c, void* exec);
+// after a failed capture: end a capture still open on the stream and clear the sticky error
+void dev_reset_capture(Ctx& c);
 void graph_destroy(void* exec);
 // bf16 / fp16 → f32 on the host (output handles)
 void half_to_float(const void* src, int dtype, float* dst, int64_t n);

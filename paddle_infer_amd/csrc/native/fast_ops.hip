@@ -268,15 +268,28 @@ void gemm_nt(Ctx& c, int f16, const void* a, int64_t lda, const void* b, int64_t
   }
 }
 
-// K-contiguous [out, in] copy of a [in, out] weight (cached per source buffer)
-const DTensor& transposed(Ctx& c, const DTensor& w, const std::string& who) {
+// Caches keyed by a source buffer hold only derivatives of persistent buffers (the loaded
+// parameters and earlier cache products, `Ctx::persist`): an activation's address can be handed
+// back by the allocator to a different tensor in a later Run, so its derivatives are recomputed.
+bool persistent(const Ctx& c, const DTensor& t) { return c.persist && t.buf && c.persist->count(t.buf.get()); }
+void keep_persistent(Ctx& c, const DTensor& t) {
+  if (c.persist && t.buf) c.persist->insert(t.buf.get());
+}
+
+// K-contiguous [out, in] copy of a [in, out] weight (cached per persistent source buffer)
+DTensor transposed(Ctx& c, const DTensor& w, const std::string& who) {
   FastState& st = state(c);
-  auto it = st.wt.find(w.buf->p);
-  if (it != st.wt.end()) return it->second;
+  const bool cache = persistent(c, w);
+  if (cache) {
+    auto it = st.wt.find(w.buf->p);
+    if (it != st.wt.end()) return it->second;
+  }
   if (w.dims.size() != 2) throw std::runtime_error(who + ": weight must be 2-D");
   const int R = (int)w.dims[0], C = (int)w.dims[1];
   DTensor t = make(c, w.dtype, {w.dims[1], w.dims[0]});
   FCHK(piamd_transpose_bf16(w.buf->p, t.buf->p, R, C, S(c)), who + " (transpose)");
+  if (!cache) return t;
+  keep_persistent(c, t);
   return st.wt[w.buf->p] = t;
 }
 
@@ -535,26 +548,35 @@ DTensor as_bf16(Ctx& c, const DTensor& t, bool cache, const std::string& who) {
   if (t.dtype == VT_BF16) return t;
   if (t.dtype != VT_FP32) throw std::runtime_error(who + ": bf16 or fp32 tensors only (fp16 model)");
   FastState& st = state(c);
+  cache = cache && persistent(c, t);
   if (cache) {
     auto it = st.b16.find(t.buf->p);
     if (it != st.b16.end()) return it->second;
   }
   DTensor o = make(c, VT_BF16, t.dims);
   gpu::cast(c, t.buf->p, VT_FP32, o.buf->p, VT_BF16, t.numel());
-  if (cache) st.b16[t.buf->p] = o;
+  if (cache) {
+    keep_persistent(c, o);
+    st.b16[t.buf->p] = o;
+  }
   return o;
 }
 
-const DTensor& packed_of(Ctx& c, const DTensor& nk, const std::string& who) {
+DTensor packed_of(Ctx& c, const DTensor& nk, const std::string& who) {
   FastState& st = state(c);
-  auto it = st.packed.find(nk.buf->p);
-  if (it != st.packed.end()) return it->second;
+  const bool cache = persistent(c, nk);
+  if (cache) {
+    auto it = st.packed.find(nk.buf->p);
+    if (it != st.packed.end()) return it->second;
+  }
   const int N = (int)nk.dims[0], K = (int)nk.dims[1];
   if (N % 32 || K % 16) throw std::runtime_error(who + ": decode weights need N % 32 == 0 and K % 16 == 0");
   DTensor p = make(c, VT_BF16, nk.dims);
   const long long n = (long long)N * K;
   hipLaunchKernelGGL(fmt_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, S(c),
                      (const unsigned short*)nk.buf->p, (unsigned short*)p.buf->p, N, K);
+  if (!cache) return p;
+  keep_persistent(c, p);
   return st.packed[nk.buf->p] = p;
 }
 

@@ -88,6 +88,18 @@ void* graph_end(Ctx& c) {
   return e;
 }
 
+void dev_reset_capture(Ctx& c) {
+  g_capture_keep = nullptr;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing((hipStream_t)c.stream, &st) == hipSuccess && st != hipStreamCaptureStatusNone) {
+    hipGraph_t g = nullptr;
+    (void)hipStreamEndCapture((hipStream_t)c.stream, &g);
+    if (g) (void)hipGraphDestroy(g);
+  }
+  (void)hipGetLastError();
+  HIPCHK(hipStreamSynchronize((hipStream_t)c.stream));
+}
+
 void graph_launch(Ctx& c, void* exec) { HIPCHK(hipGraphLaunch((hipGraphExec_t)exec, (hipStream_t)c.stream)); }
 
 void graph_destroy(void* exec) {

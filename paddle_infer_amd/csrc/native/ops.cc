@@ -357,25 +357,45 @@ void pool2d_op(Ctx& c, const OpDesc& o, Scope& s) {
   s[o.out("Out")] = nhwc ? transpose(c, y, {0, 2, 3, 1}) : y;
 }
 
-// inference batch norm: y = x · γ/√(σ²+ε) + (β − μ·γ/√(σ²+ε)) per channel (folded on the host)
+// inference batch norm: y = x · γ/√(σ²+ε) + (β − μ·γ/√(σ²+ε)) per channel. The fold runs once on
+// the host (the first Run: eager, before any hipGraph capture) and is kept on the device while its
+// inputs are loaded parameters, so a captured Run never reads device data back.
 void batch_norm_op(Ctx& c, const OpDesc& o, Scope& s) {
   const DTensor& x = in(c, s, o, "X");
   need_f32(x, o);
-  const DTensor g = to_host(in(c, s, o, "Scale"), c), b = to_host(in(c, s, o, "Bias"), c);
-  const DTensor m = to_host(in(c, s, o, "Mean"), c), v = to_host(in(c, s, o, "Variance"), c);
-  const int64_t C = g.numel();
-  const float eps = o.af("epsilon", 1e-5f);
+  const DTensor &g0 = in(c, s, o, "Scale"), &b0 = in(c, s, o, "Bias");
+  const DTensor &m0 = in(c, s, o, "Mean"), &v0 = in(c, s, o, "Variance");
+  auto is_param = [&](const DTensor& t) { return c.persist && t.buf && c.persist->count(t.buf.get()); };
+  const bool cacheable = c.consts && is_param(g0) && is_param(b0) && is_param(m0) && is_param(v0);
+  const std::string key = "bn_fold:" + o.out("Y");
   DTensor sc, sh;
-  sc.dtype = sh.dtype = VT_FP32;
-  sc.dims = sh.dims = {C};
-  sc.buf = alloc_buffer(C * 4, false);
-  sh.buf = alloc_buffer(C * 4, false);
-  for (int64_t i = 0; i < C; ++i) {
-    const float a = g.data<float>()[i] / std::sqrt(v.data<float>()[i] + eps);
-    sc.data<float>()[i] = a;
-    sh.data<float>()[i] = b.data<float>()[i] - m.data<float>()[i] * a;
+  if (cacheable && c.consts->count(key + ":sc")) {
+    sc = c.consts->at(key + ":sc");
+    sh = c.consts->at(key + ":sh");
+  } else {
+    const DTensor g = to_host(g0, c), b = to_host(b0, c), m = to_host(m0, c), v = to_host(v0, c);
+    const int64_t C = g.numel();
+    const float eps = o.af("epsilon", 1e-5f);
+    sc.dtype = sh.dtype = VT_FP32;
+    sc.dims = sh.dims = {C};
+    sc.buf = alloc_buffer(C * 4, false);
+    sh.buf = alloc_buffer(C * 4, false);
+    for (int64_t i = 0; i < C; ++i) {
+      const float a = g.data<float>()[i] / std::sqrt(v.data<float>()[i] + eps);
+      sc.data<float>()[i] = a;
+      sh.data<float>()[i] = b.data<float>()[i] - m.data<float>()[i] * a;
+    }
+    if (c.gpu) {
+      sc = to_device(sc, c);
+      sh = to_device(sh, c);
+      dev_sync(c);  // the host staging buffers die at the end of this scope
+    }
+    if (cacheable) {
+      (*c.consts)[key + ":sc"] = sc;
+      (*c.consts)[key + ":sh"] = sh;
+    }
   }
-  if (c.gpu) { sc = to_device(sc, c); sh = to_device(sh, c); }
+  const int64_t C = sc.numel();
   const bool nhwc = nhwc_layout(o, "data_layout");
   const int64_t N = x.dims.at(0);
   const int64_t inner = nhwc ? 1 : x.numel() / (N * C);

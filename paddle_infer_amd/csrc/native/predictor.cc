@@ -1,6 +1,8 @@
 // paddle_infer::Predictor on the native engine: load + validate the program, keep parameters
 // resident on the predictor's device, run block 0 op by op, expose feed / fetch handles.
 #include <algorithm>
+#include <set>
+#include <unordered_set>
 #include <fstream>
 #include <sstream>
 #include <type_traits>
@@ -99,9 +101,14 @@ class PredictorImpl {
     ctx.prec16 = c.precision() == PrecisionType::kBf16 ? pdn::VT_BF16
                  : c.precision() == PrecisionType::kHalf ? pdn::VT_FP16 : 0;
     if (ctx.gpu) pdn::dev_init(ctx);
+    ctx.persist = std::make_shared<std::unordered_set<const pdn::Buffer*>>();
+    ctx.consts = std::make_shared<std::map<std::string, pdn::DTensor>>();
     if (!c.params_file().empty()) {
       auto ps = pdn::load_params(prog, read_file(c.params_file()));
-      for (auto& kv : ps) params[kv.first] = ctx.gpu ? pdn::to_device(kv.second, ctx) : kv.second;
+      for (auto& kv : ps) {
+        params[kv.first] = ctx.gpu ? pdn::to_device(kv.second, ctx) : kv.second;
+        ctx.persist->insert(params[kv.first].buf.get());
+      }
     }
   }
   PredictorImpl(const PredictorImpl& o) : cfg(o.cfg), prog(o.prog), feeds(o.feeds), fetches(o.fetches),
@@ -142,9 +149,14 @@ class PredictorImpl {
     }
   }
 
-  // hipGraph: one capture per feed-shape signature (first Run: eager warm-up, then capture + launch)
+  // hipGraph: one capture per feed signature (first Run: eager warm-up, then capture + launch).
+  // The signature holds each feed's dtype and dims and, for caller memory shared with
+  // ShareExternalData, its address: the captured kernels read and write (CacheKV) that address,
+  // so a new pointer is a new capture, never a copy into the old one. A signature whose capture
+  // failed (an op that reads device data back on the host) runs eagerly from then on.
   void* graph = nullptr;
   std::string graph_key;
+  std::set<std::string> graph_failed;
   pdn::Scope graph_scope;
   std::vector<std::shared_ptr<pdn::Buffer>> graph_keep;  // every buffer the captured kernels touch
 
@@ -160,31 +172,55 @@ class PredictorImpl {
       const auto& t = tensor(f);
       key += f + ":" + std::to_string(t.dtype);
       for (auto d : t.dims) key += "," + std::to_string(d);
+      if (t.buf && !t.buf->owned) key += "@" + std::to_string(reinterpret_cast<uintptr_t>(t.buf->p));
       key += ";";
+    }
+    if (graph_failed.count(key)) {
+      run_ops(scope);
+      pdn::dev_sync(ctx);
+      return true;
     }
     if (key != graph_key) {
       run_ops(scope);  // warm-up: weight copies, workspaces, code-object load
       pdn::dev_sync(ctx);
       pdn::graph_destroy(graph);
       graph = nullptr;
+      graph_key.clear();
       graph_scope.clear();
       graph_keep.clear();
       for (auto& kv : params) graph_scope[kv.first] = kv.second;
       for (auto& f : feeds) graph_scope[f] = tensor(f);
       pdn::graph_begin(ctx, &graph_keep);
+      bool ok = true;
       try {
         run_ops(graph_scope);
       } catch (...) {
-        try { pdn::graph_destroy(pdn::graph_end(ctx)); } catch (...) {}
-        throw;
+        ok = false;
       }
-      graph = pdn::graph_end(ctx);
+      void* g = nullptr;
+      try {
+        g = pdn::graph_end(ctx);
+      } catch (...) {
+        ok = false;
+      }
+      if (!ok) {
+        // the warm-up above already produced this Run's outputs eagerly
+        pdn::graph_destroy(g);
+        pdn::dev_reset_capture(ctx);
+        graph_scope.clear();
+        graph_keep.clear();
+        graph_failed.insert(key);
+        return true;
+      }
+      graph = g;
       graph_key = key;
     } else {
       for (auto& f : feeds) {
         auto& src = tensor(f);
         auto& dst = graph_scope.at(f);
-        if (src.buf != dst.buf) pdn::dev_copy(dst.buf->p, src.buf->p, src.nbytes(), 2, ctx);
+        // owned buffers only: a shared external pointer is part of the key (same pointer here)
+        if (src.buf != dst.buf && src.buf->owned && dst.buf->owned)
+          pdn::dev_copy(dst.buf->p, src.buf->p, src.nbytes(), 2, ctx);
       }
     }
     pdn::graph_launch(ctx, graph);

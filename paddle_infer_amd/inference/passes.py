@@ -670,12 +670,15 @@ from .fmt_passes import (  # noqa: E402
 from .fmt_passes import fused_multi_transformer_encoder_pass_ops as fused_multi_transformer_encoder_pass  # noqa: E402
 
 from .passes_extra import EXTRA_PASSES  # noqa: E402
+from .passes_quant import QUANT_PASSES  # noqa: E402
 
 globals().update(EXTRA_PASSES)
+globals().update(QUANT_PASSES)
 
 # Order follows the reference GpuPassStrategy: cleanups, the LLM layer passes, conv fusions, the
 # matmul→mul maps (so fc_fuse sees one form), attention / fc / LN fusions, constant folding last.
 GPU_PASSES = [
+    "delete_weight_dequant_linear_op_pass",  # QAT exports: int8 weights onto the weight-only GEMM
     "is_test_pass", "simplify_with_basic_ops_pass",
     "delete_dropout_op_pass", "identity_scale_op_clean_pass", "identity_reshape_clean_pass",
     *_FMT_ORDER,  # the reference runs the LLM passes before the generic fc / attention fusions

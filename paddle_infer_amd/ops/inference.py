@@ -358,12 +358,16 @@ def weight_only_linear(x, weight, bias=None, weight_scale=None, weight_dtype="in
         if x2.stride(-1) != 1:
             x2 = x2.contiguous()
         scale = weight_scale if weight_scale.dtype == torch.float32 else weight_scale.float()
-        if M > WO_GEMV_MAX_M:  # compute-bound: dequantize once, MFMA GEMM via hipBLASLt
+        if M > WO_GEMV_MAX_M:  # compute-bound: dequantize once, the own bf16 MFMA GEMM
+            from .gemm import gemm_nt
             w = torch.empty((N, K), dtype=torch.bfloat16, device=x.device)
             _lib.call("piamd_wo_dequant", bits, weight.data_ptr(), scale.data_ptr(), w.data_ptr(),
                       N, K, _lib.stream())
-            y = F.linear(x2, w, bias)
-            y = _ref_act(y, act) if act else y
+            fused = {0: "none", 1: "gelu_tanh", 2: "gelu", 3: "relu"}.get(act)
+            y = gemm_nt(x2, w, bias=bias.to(torch.bfloat16) if bias is not None else None,
+                        act=fused or "none")
+            if fused is None:
+                y = _ref_act(y, act)
             return y.reshape(*lead, N)
         y = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
         tiles = (N // 32) * ((M + 31) // 32)

@@ -79,6 +79,41 @@ def softmax_cross_entropy(logits, labels, ignore_index: int = -100, group=None,
     return _reference(logits, labels, ignore_index)
 
 
+def vocab_parallel_softmax_xent(logits, labels, ignore_index=-100, group=None, rank=None):
+    """Forward of the static ``c_softmax_with_cross_entropy`` op (reference
+    `c_softmax_with_cross_entropy_op.cu`): this rank's vocab slice of the globally normalised
+    softmax and the per-row loss. GPU: the row statistics (max, Σexp, target logit) come from
+    ``xent.hip`` in one pass over the logits, all-reduced over ``group``; the softmax slice is one
+    elementwise pass exp(x − lse). ``rank`` defaults to the group rank."""
+    V = logits.shape[-1]
+    lg = logits.reshape(-1, V)
+    lab = labels.reshape(-1).to(torch.int64)
+    if rank is None:
+        rank = dist.get_rank(group) if group is not None else 0
+    start = int(rank) * V
+    if lg.is_cuda and lg.dtype in (torch.bfloat16, torch.float16, torch.float32):
+        lgc = lg.contiguous()
+        m, s, t = _stats(lgc, lab, start, ignore_index)
+    else:
+        x = lg.float()
+        m = x.max(dim=-1).values
+        s = torch.exp(x - m[:, None]).sum(-1)
+        inr = (lab >= start) & (lab < start + V)
+        idx = torch.where(inr, lab - start, torch.zeros_like(lab))
+        t = torch.gather(x, -1, idx[:, None]).squeeze(-1) * inr
+    if group is not None and dist.get_world_size(group) > 1:
+        M = m.clone()
+        dist.all_reduce(M, op=dist.ReduceOp.MAX, group=group)
+        s = s * torch.exp(m - M)
+        dist.all_reduce(s, group=group)
+        dist.all_reduce(t, group=group)
+        m = M
+    lse = torch.log(s) + m
+    loss = torch.where(lab != ignore_index, lse - t, torch.zeros_like(lse))
+    softmax = torch.exp(lg.float() - lse[:, None]).to(logits.dtype)
+    return softmax.reshape(logits.shape), loss.reshape(labels.shape)
+
+
 def _parallel_reference(logits, labels, ignore_index, group):
     """Vocab-parallel CE composed from torch ops (CPU / gloo path)."""
     V = logits.shape[-1]

@@ -547,8 +547,14 @@ def _flash_attn(ins, a):
 def _wol(ins, a):
     from .. import ops
     b = ins["bias"][0] if ins.get("bias") else None
-    return {"out": ops.weight_only_linear(ins["x"][0], ins["weight"][0], b, ins["weight_scale"][0],
-                                          a.get("weight_dtype", "int8"), a.get("act_method", "none"))}
+    x = ins["x"][0]
+    xin = x
+    if x.is_cuda and x.dtype != torch.bfloat16:  # the GPU weight-only GEMM takes bf16 activations
+        xin = x.to(torch.bfloat16)
+        b = b.to(torch.bfloat16) if b is not None else None
+    y = ops.weight_only_linear(xin, ins["weight"][0], b, ins["weight_scale"][0],
+                               a.get("weight_dtype", "int8"), a.get("act_method", "none"))
+    return {"out": y.to(x.dtype) if y.dtype != x.dtype else y}
 
 
 # ---------------------------------------------------------------- LLM / BERT fused inference ops
@@ -825,3 +831,4 @@ def _clip_op(ins, a):
 
 from . import ops_registry_ext  # noqa: E402,F401  (registers the extended op set)
 from . import ops_registry_more  # noqa: E402,F401  (fused blocks, rnn, 3-D conv / pool, detection)
+from . import ops_registry_model  # noqa: E402,F401  (quantization, fused BN+act, vocab-parallel CE, gate attention, beam search)

@@ -315,6 +315,9 @@ def addmm(input, x, y, beta=1.0, alpha=1.0, name=None):  # noqa: A002
     from ..ops.gemm import own_dtype, matmul as _mm
     if own_dtype(x, y) and x.dim() == 2 and y.dim() == 2:
         out = _mm(x, y, alpha=alpha)
+        if beta == 0:  # BLAS beta = 0: C is not read (NaN / inf in `input` do not propagate)
+            return out.expand(torch.broadcast_shapes(out.shape, input.shape)).clone() \
+                if out.shape != torch.broadcast_shapes(out.shape, input.shape) else out
         return out + (input if beta == 1.0 else beta * input)
     return torch.addmm(input, x, y, beta=beta, alpha=alpha)
 

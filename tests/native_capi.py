@@ -24,6 +24,7 @@ def lib():
             ("PD_ConfigCreate", vp, []),
             ("PD_ConfigSetModel", None, [vp, ctypes.c_char_p, ctypes.c_char_p]),
             ("PD_ConfigEnableUseGpu", None, [vp, ctypes.c_uint64, i32, i32]),
+            ("PD_ConfigEnableHipGraph", None, [vp, ctypes.c_int8]),
             ("PD_PredictorCreate", vp, [vp]),
             ("PD_PredictorDestroy", None, [vp]),
             ("PD_PredictorRun", ctypes.c_int8, [vp]),
@@ -49,12 +50,14 @@ def _shape(shape):
 
 
 class Predictor:
-    def __init__(self, prefix, gpu=0, precision=PD_PRECISION_FLOAT32):
+    def __init__(self, prefix, gpu=0, precision=PD_PRECISION_FLOAT32, hip_graph=False):
         L = lib()
         cfg = L.PD_ConfigCreate()
         L.PD_ConfigSetModel(cfg, (prefix + ".pdmodel").encode(), (prefix + ".pdiparams").encode())
         if gpu is not None:
             L.PD_ConfigEnableUseGpu(cfg, 256, gpu, precision)
+        if hip_graph:
+            L.PD_ConfigEnableHipGraph(cfg, 1)
         self.p = L.PD_PredictorCreate(cfg)
         assert self.p, "native predictor creation failed (see stderr)"
         self._handles = {}

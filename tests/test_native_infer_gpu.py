@@ -49,3 +49,50 @@ def test_native_gpu_cnn(tmp_path, arch):
     got, ms, _ = native_outputs(path, {"x": x}, tmp_path, gpu=0, repeat=3)
     np.testing.assert_allclose(got[0], ref[0], rtol=2e-3, atol=2e-3)
     assert ms is not None and ms > 0
+
+
+def test_native_gpu_cnn_hip_graph(tmp_path):
+    """conv + batch_norm under hipGraph capture: the BN fold is computed once on the eager warm-up
+    and kept on the device, so the captured Runs match the eager ones (a capture that cannot
+    proceed would fall back to eager for that feed signature instead of failing every Run)."""
+    import torch
+    from native_infer_util import SmallCNN
+    torch.manual_seed(0)
+    path = str(tmp_path / "cnn")
+    export(SmallCNN(), path, [InputSpec([None, 3, 64, 64], "float32", "x")])
+    x = np.random.RandomState(3).randn(2, 3, 64, 64).astype("float32")
+    ref = python_outputs(path, {"x": x})
+    got, ms, _ = native_outputs(path, {"x": x}, tmp_path, gpu=0, repeat=4, graph=True)
+    np.testing.assert_allclose(got[0], ref[0], rtol=2e-3, atol=2e-3)
+
+
+def test_native_graph_share_external_data_new_pointer(tmp_path):
+    """ShareExternalData + hipGraph: a feed shared from a NEW device pointer (the old buffer freed)
+    re-captures instead of copying into the old address; results follow the current buffer."""
+    import torch
+    import native_capi as nc
+    path = str(tmp_path / "mlp")
+    export(MLP(), path, [InputSpec([None, 16], "float32", "x")])
+    xs = [np.random.RandomState(i).randn(8, 16).astype("float32") for i in range(3)]
+    refs = [python_outputs(path, {"x": x}) for x in xs]
+    p = nc.Predictor(path, gpu=0, hip_graph=True)
+    try:
+        for i, x in enumerate(xs):
+            t = torch.from_numpy(x).cuda()
+            torch.cuda.synchronize()
+            p.share("x", t)
+            p.run()
+            p.run()  # second Run: graph replay on the same pointer
+            got = p.fetch_float(p_out_name(path, 0), refs[i][0].shape)
+            np.testing.assert_allclose(got, refs[i][0], rtol=2e-3, atol=2e-4)
+            del t
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+    finally:
+        p.close()
+
+
+def p_out_name(path, i):
+    from paddle_infer_amd import inference as pinf
+    c = pinf.Config(path + ".pdmodel", path + ".pdiparams")
+    return pinf.create_predictor(c).get_output_names()[i]

@@ -468,3 +468,44 @@ PIAMD_EXPORT int piamd_transpose_bf16(const void* src, void* dst, int R, int C,
                      (bf16_t*)dst, R, C);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// fp32 GEMM operands as bf16 split products (ops/gemm.py gemm_nt_f32 / wgrad_f32): t = hi + lo
+// (hi = bf16(t), lo = bf16(t − hi)), written as THREE segments of one bf16 operand so that
+// x·w ≈ x_hi·w_hi + x_lo·w_hi + x_hi·w_lo is ONE bf16 MFMA GEMM with an f32 result ("hlh" on
+// the left operand, "hhl" on the right). `lo_mask` bit s: segment s holds lo. axis 0: segments
+// side by side along the row (dst[r][s·Cp + c], Cp ≥ C zero-padded: the reduction dim of a
+// K-contiguous operand); axis 1: stacked along rows (dst[s·Rp + r][c], rows ≥ R zero: the
+// reduction dim of a weight-gradient operand). One pass: 4 B read, 6 B written per element.
+__global__ void split3_f32_kernel(const float* __restrict__ src, long long ld, bf16_t* __restrict__ dst, int R,
+                                  int C, int Rp, int Cp, int lo_mask, int axis) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // one 8-column group
+  const int groups = Cp / 8;
+  if (i >= (long long)Rp * groups) return;
+  const int r = (int)(i / groups), c0 = (int)(i % groups) * 8;
+  u16x8 hi, lo;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = c0 + j;
+    const float v = (r < R && c < C) ? src[(long long)r * ld + c] : 0.f;
+    const bf16_t h = f2bf(v);
+    hi[j] = h;
+    lo[j] = f2bf(v - bf2f(h));
+  }
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    const long long o = axis == 0 ? (long long)r * 3 * Cp + (long long)s * Cp + c0
+                                  : ((long long)s * Rp + r) * Cp + c0;
+    *(u16x8*)(dst + o) = ((lo_mask >> s) & 1) ? lo : hi;
+  }
+}
+
+PIAMD_EXPORT int piamd_split3_f32(const void* src, long long ld, void* dst, int R, int C, int Rp, int Cp,
+                                  int lo_mask, int axis, hipStream_t stream) {
+  if (Rp == 0 || Cp == 0) return 0;
+  if (Cp % 8 || Rp < R || Cp < C || (axis != 0 && axis != 1)) return (int)hipErrorInvalidValue;
+  const long long n = (long long)Rp * (Cp / 8);
+  hipLaunchKernelGGL(split3_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                     (const float*)src, ld, (bf16_t*)dst, R, C, Rp, Cp, lo_mask, axis);
+  return (int)hipGetLastError();
+}

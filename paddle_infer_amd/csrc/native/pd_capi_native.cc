@@ -73,6 +73,7 @@ void PD_ConfigEnableUseGpu(PD_Config* c, uint64_t mem_mb, int32_t device_id, PD_
                       prec == PD_PRECISION_BFLOAT16 ? P::kBf16 : prec == PD_PRECISION_HALF ? P::kHalf : P::kFloat32);
 }
 void PD_ConfigDisableGpu(PD_Config* c) { c->cfg.DisableGpu(); }
+void PD_ConfigEnableHipGraph(PD_Config* c, PD_Bool x) { c->cfg.EnableHipGraph(x != 0); }
 PD_Bool PD_ConfigUseGpu(PD_Config* c) { return c->cfg.use_gpu(); }
 int32_t PD_ConfigGpuDeviceId(PD_Config* c) { return c->cfg.gpu_device_id(); }
 int32_t PD_ConfigMemoryPoolInitSizeMb(PD_Config* c) { return c->mem_mb; }

@@ -225,6 +225,8 @@ _SIGS["piamd_small_gemm"] = [c_int, c_void_p, c_ll, c_void_p, c_ll, c_void_p, c_
                              c_int, c_void_p, c_ll, c_void_p, c_void_p, c_void_p]
 _SIGS["piamd_agemm_loaded"] = []
 _SIGS["piamd_transpose_bf16"] = [c_void_p, c_void_p, c_int, c_int, c_void_p]
+# src, ld, dst, R, C, Rp, Cp, lo_mask, axis, stream
+_SIGS["piamd_split3_f32"] = [c_void_p, c_ll, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p]
 _SIGS["piamd_moe_gemm"] = [c_void_p, c_ll, c_void_p, c_ll, c_ll,
                                 c_int, c_void_p, c_int, c_int, c_void_p,
                                 c_ll, c_int, c_int, c_int, c_int,

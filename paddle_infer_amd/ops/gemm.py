@@ -241,6 +241,97 @@ def own_dtype(*ts):
     return t0.is_cuda and t0.dtype in _HALF and all(t.dtype == t0.dtype for t in ts)
 
 
+# ---------------------------------------------------------------------------------------------
+# fp32 GEMMs as split-bf16 products (Paddle's default dtype; reference `blas_impl.cu.h:32`
+# CUBlas<float>): x·w ≈ x_hi·w_hi + x_lo·w_hi + x_hi·w_lo with t = hi + lo (both bf16), the three
+# products run as ONE bf16 MFMA GEMM over a 3×-long reduction ([x_hi | x_lo | x_hi] ·
+# [w_hi | w_hi | w_lo]) with an f32 result: ≈2^-16 relative per product, at 3× the bf16 work —
+# still ≈3× the f32 MFMA rate (`MI355X_MICROARCH.md` § Matrix cores: f32-input MFMA = 1/16 bf16).
+# The operand split is one HIP pass (`piamd_split3_f32`).
+# ---------------------------------------------------------------------------------------------
+FP32_SPLIT = True  # False: fp32 GEMMs on the library (exact fp32)
+_LO = {"hlh": 0b010, "hhl": 0b100}
+
+
+def own_f32(*ts):
+    """fp32 CUDA operands the split-bf16 path takes."""
+    return FP32_SPLIT and all(t.is_cuda and t.dtype == torch.float32 for t in ts)
+
+
+def split3(t, order, axis=0, Rp=None, Cp=None):
+    """f32 [R, C] → bf16 segments (order "hlh" / "hhl"): axis 0 → [R, 3·Cp] (segments along the
+    row, C zero-padded to Cp), axis 1 → [3·Rp, C] (stacked rows, R zero-padded to Rp)."""
+    R, C = t.shape
+    if t.stride(-1) != 1 or (R > 1 and t.stride(0) < C):
+        t = t.contiguous()
+    if axis == 0:
+        Cp = Cp or _ceil(C, 64)
+        Rp = R
+        out = torch.empty((R, 3 * Cp), dtype=torch.bfloat16, device=t.device)
+    else:
+        Rp = Rp or _ceil(R, 64)
+        Cp = C
+        assert C % 8 == 0, "row-stacked split needs C % 8 == 0"
+        out = torch.empty((3 * Rp, C), dtype=torch.bfloat16, device=t.device)
+    _lib.call("piamd_split3_f32", t.data_ptr(), t.stride(0) if R > 1 else C, out.data_ptr(), R, C, Rp, Cp,
+              _LO[order], axis, _lib.stream())
+    return out
+
+
+def gemm_nt_f32(a, b=None, alpha=1.0, bias=None, act="none", resid=None, b3=None):
+    """fp32 C[M, N] = act(alpha·a[M, K]·b[N, K]ᵀ + bias) (+ resid) on the split-bf16 path; ``b3``:
+    a pre-split right operand ([N, 3·Kp], "hhl", e.g. a cached weight)."""
+    M, K = a.shape
+    Kp = _ceil(K, 64)
+    a3 = split3(a, "hlh", 0, Cp=Kp)
+    if b3 is None:
+        b3 = split3(b, "hhl", 0, Cp=Kp)
+    N = b3.shape[0] if b is None else b.shape[0]
+    Np = _ceil(N, 4)
+    if Np != N:
+        b3 = torch.nn.functional.pad(b3, (0, 0, 0, Np - N))
+    K3 = 3 * Kp
+    if use_small(M, Np, K3):
+        out = small_gemm(a3, b3, out_f32=True)
+    else:
+        ks = pick_ksplit(M, Np, K3)
+        if not asm_supported(a3, b3, trans_b=True, ksplit=ks):
+            ks = 1
+        out = asm_gemm(a3, b3, trans_b=True, out_f32=True, ksplit=ks)
+    if Np != N:
+        out = out[:, :N].contiguous()
+    if alpha != 1.0:
+        out.mul_(alpha)
+    if bias is not None or act != "none":
+        from .activation import bias_act
+        b32 = bias.float().reshape(-1) if bias is not None else None
+        out = bias_act(out, b32, act) if N % 8 == 0 else _ref_act(out + (b32 if b32 is not None else 0),
+                                                                   ACTS[act])
+    if resid is not None:
+        out.add_(resid.reshape(M, N).float())
+    return out
+
+
+def wgrad_f32(x2, dy2, out=None):
+    """fp32 x2[T, K]ᵀ · dy2[T, N] (weight gradient) on the split path: the reduction (token) dim
+    stacked as [x_hi; x_lo; x_hi] · [dy_hi; dy_hi; dy_lo] — one TN GEMM, no transposes. ``out``
+    (f32 [K, N], contiguous): accumulated into (main_grad += …) by the GEMM epilogue."""
+    T, K = x2.shape
+    N = dy2.shape[1]
+    if K % 8 == 0 and N % 8 == 0 and (out is None or out.is_contiguous()):
+        Tp = _ceil(T, 64)
+        x3 = split3(x2, "hlh", 1, Rp=Tp)
+        d3 = split3(dy2, "hhl", 1, Rp=Tp)
+        ks = pick_ksplit(K, N, 3 * Tp)
+        if not asm_supported(x3, d3, trans_a=True, ksplit=ks):
+            ks = 1
+        if out is not None:
+            return asm_gemm(x3, d3, trans_a=True, out=out, accumulate=True, ksplit=ks)
+        return asm_gemm(x3, d3, trans_a=True, out_f32=True, ksplit=ks)
+    g = gemm_nt_f32(x2.t().contiguous(), dy2.t().contiguous())
+    return out.add_(g) if out is not None else g
+
+
 def _ceil(x, m):
     return -(-x // m) * m
 
@@ -278,6 +369,8 @@ def gemm_nt(a, b, alpha=1.0, bias=None, act="none", resid=None, out_f32=False):
     matmul lowers to, on the framework's own kernels (skinny kernel for few rows, assembly GEMM
     otherwise). bf16 / fp16 operands of one dtype; any K (zero-padded to the kernels' 64-multiple)
     and any N (padded to a multiple of 4)."""
+    if a.dtype == torch.float32:
+        return gemm_nt_f32(a, b, alpha, bias, act, resid)
     M, K = a.shape
     N = b.shape[0]
     half = a.dtype
@@ -346,6 +439,27 @@ def bmm(x, y, transpose_x=False, transpose_y=False, alpha=1.0):
     M = x.shape[-1] if transpose_x else x.shape[-2]
     K = x.shape[-2] if transpose_x else x.shape[-1]
     N = y.shape[-2] if transpose_y else y.shape[-1]
+    if x.dtype == torch.float32:  # split-bf16: [nb·M, 3Kp] · [nb·N, 3Kp]ᵀ as one batched launch
+        xa = (x.transpose(-1, -2) if transpose_x else x).expand(nb, M, K) if x.dim() == 3 or nb > 1 else \
+            (x.transpose(-1, -2) if transpose_x else x)
+        yb = (y if transpose_y else y.transpose(-1, -2))
+        yb = yb.expand(nb, N, K) if (yb.dim() == 3 or nb > 1) else yb
+        Kp = _ceil(K, 64)
+        Np = _ceil(N, 4)
+        A = split3(xa.reshape(-1, K), "hlh", 0, Cp=Kp).view(-1, M, 3 * Kp) if xa.dim() == 3 else \
+            split3(xa, "hlh", 0, Cp=Kp)
+        B = split3(yb.reshape(-1, K), "hhl", 0, Cp=Kp).view(-1, N, 3 * Kp) if yb.dim() == 3 else \
+            split3(yb, "hhl", 0, Cp=Kp)
+        if Np != N:
+            B = torch.nn.functional.pad(B, (0, 0, 0, Np - N))
+        if A.dim() == 2:
+            A = A.unsqueeze(0)
+        out = asm_gemm(A, B, trans_b=True, out_f32=True)
+        if Np != N:
+            out = out[..., :N].contiguous()
+        if alpha != 1.0:
+            out.mul_(alpha)
+        return out
 
     def ok(t, inner_contig):
         return (t.stride(-1) == 1 and t.stride(-2) % 8 == 0 and t.data_ptr() % 16 == 0
@@ -378,6 +492,22 @@ def bmm(x, y, transpose_x=False, transpose_y=False, alpha=1.0):
     return out
 
 
+def split_nk(w, transpose):
+    """Cached "hhl" split of an fp32 right operand as [N, 3·Kp]: of ``w`` itself when it is
+    stored [N, K] (``transpose``), else of ``wᵀ`` (a Paddle [in, out] weight). Kept on the tensor,
+    refreshed when it changed (autograd version / flat-optimizer epoch)."""
+    from .linear import _PARAM_EPOCH
+    key = (_PARAM_EPOCH[0], w._version)
+    attr = "_piamd_split_n" if transpose else "_piamd_split_t"
+    c = getattr(w, attr, None)
+    if c is not None and c[0] == key:
+        return c[1]
+    src = w.detach() if transpose else w.detach().t()
+    b3 = split3(src, "hhl", 0)
+    setattr(w, attr, (key, b3))
+    return b3
+
+
 def _b_nk(y, transpose_y):
     """2-D right operand as [N, K] K-contiguous: the stored matrix when transposed, else the
     cached transposed copy (weights: transposed once, refreshed when they change)."""
@@ -403,7 +533,10 @@ def matmul_fwd(x, y, transpose_x=False, transpose_y=False, alpha=1.0):
         xa = x.transpose(-1, -2) if transpose_x else x
         lead = xa.shape[:-1]
         a2 = xa.reshape(-1, xa.shape[-1])
-        out = gemm_nt(a2, _b_nk(y, transpose_y), alpha=alpha)
+        if a2.dtype == torch.float32:
+            out = gemm_nt_f32(a2, alpha=alpha, b3=split_nk(y, transpose_y))
+        else:
+            out = gemm_nt(a2, _b_nk(y, transpose_y), alpha=alpha)
         out = out.reshape(*lead, out.shape[-1])
     else:
         if x.dim() == 2 and y.dim() > 2:
@@ -476,9 +609,17 @@ class _MatmulFn(torch.autograd.Function):
 
 def matmul(x, y, transpose_x=False, transpose_y=False, alpha=1.0):
     """``paddle.matmul`` / ``bmm`` / static ``matmul_v2`` / ``matmul`` / ``mul``: bf16 / fp16 CUDA
-    operands run the framework's own GEMMs (forward and backward); other dtypes / devices take
-    the PyTorch reference (fp32 GEMMs stay on the vendor library)."""
-    if own_dtype(x, y) and x.dim() >= 1 and y.dim() >= 1 and x.numel() and y.numel():
+    operands run the framework's own GEMMs (forward and backward), fp32 CUDA operands the same
+    kernels as split-bf16 products (``gemm_nt_f32``), or the autocast dtype under AMP O1; CPU
+    tensors take the PyTorch reference."""
+    if (x.is_cuda and y.is_cuda and x.dtype == torch.float32 and y.dtype == torch.float32
+            and torch.is_autocast_enabled("cuda")):
+        # AMP O1 (paddle.amp.auto_cast → torch autocast): matmul is a white-list op — fp32
+        # operands run in the autocast dtype on the own 16-bit GEMMs (casts differentiable)
+        dt = torch.get_autocast_dtype("cuda")
+        x, y = x.to(dt), y.to(dt)
+    if ((own_dtype(x, y) or own_f32(x, y)) and x.dim() >= 1 and y.dim() >= 1
+            and x.numel() and y.numel()):
         if torch.is_grad_enabled() and (x.requires_grad or y.requires_grad):
             return _MatmulFn.apply(x, y, transpose_x, transpose_y, alpha)
         return matmul_fwd(x, y, transpose_x, transpose_y, alpha)

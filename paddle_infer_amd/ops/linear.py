@@ -12,7 +12,9 @@ prefill). Forward ``x·Wtᵀ`` with the bias (and activation) in the epilogue, d
 framework's flat gradient buffer) with split-K when the tile grid is small — the weight gradient is
 never materialised as a separate tensor, and the parameter's ``_grad_ready`` hook (the bucketed
 reduce-scatter/all-reduce trigger) fires right after. ``PIAMD_GEMM=blas`` routes the same products
-to hipBLASLt (A/B comparisons); fp32 linears stay on the library.
+to hipBLASLt (A/B comparisons). fp32 linears (Paddle's default dtype) run the same kernels as
+split-bf16 products (`ops.gemm.gemm_nt_f32` / `wgrad_f32`); under AMP O1 an fp32 weight is cast to
+the autocast dtype first.
 
 Weight layout for the forward GEMM: on gfx950 hipBLASLt is 12-21 % faster when BOTH operands are
 contiguous along the reduction dim (`x @ Wtᵀ` with ``Wt = [out, in]``) than on Paddle's ``x @ W``
@@ -49,6 +51,12 @@ def _own(*ts):
     return _GEMM_IMPL[0] == "asm" and own_dtype(*ts)
 
 
+def _own32(*ts):
+    """fp32 CUDA operands on the own GEMMs as split-bf16 products (`ops.gemm.gemm_nt_f32`)."""
+    from .gemm import own_f32
+    return _GEMM_IMPL[0] == "asm" and own_f32(*ts)
+
+
 def mm_nt(x2, w_nk, bias=None, act="none"):
     """y[M, N] = act(x2[M, K] · w_nkᵀ + bias), both operands K-contiguous."""
     if _own(x2, w_nk) and (bias is None or bias.dtype == x2.dtype):
@@ -66,6 +74,10 @@ def wgrad_into(out, x2, dy2):
     """out[K, N] += x2[T, K]ᵀ · dy2[T, N] (weight gradient into main_grad; split-K on small grids).
     Token counts off the assembly kernel's 64-multiple take the own kernels on K-contiguous copies."""
     from .gemm import asm_gemm, gemm_nt, pick_ksplit
+    if out.dtype == torch.float32 and _own32(x2, dy2):
+        from .gemm import wgrad_f32
+        wgrad_f32(x2, dy2, out=out)
+        return out
     if out.is_contiguous() and out.dtype in (torch.bfloat16, torch.float32, torch.float16) \
             and dy2.is_contiguous() and (out.dtype != torch.float16 or x2.dtype == torch.float16):
         ks = pick_ksplit(out.shape[0], out.shape[1], x2.shape[0])
@@ -134,6 +146,9 @@ class _LinearFn(torch.autograd.Function):
         x2 = x.reshape(-1, shp[-1])
         if _use_transposed(x2, w) or (_own(x2, w) and w.dim() == 2 and w.is_contiguous()):
             y = mm_nt(x2, transposed(w), b)
+        elif w.dim() == 2 and _own32(x2, w) and (b is None or b.dtype == torch.float32):
+            from .gemm import gemm_nt_f32, split_nk
+            y = gemm_nt_f32(x2, bias=b, b3=split_nk(w, False))
         elif b is not None:
             y = torch.addmm(b, x2, w)
         else:
@@ -152,8 +167,12 @@ class _LinearFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dy2c = dy2.contiguous() if w.is_contiguous() else dy2
-            dx = (mm_nt(dy2c, w) if w.is_contiguous() and dy2c.dtype == w.dtype
-                  else torch.mm(dy2, w.t())).view(ctx.shp)
+            if _own32(dy2c, w):
+                from .gemm import gemm_nt_f32, split_nk
+                dx = gemm_nt_f32(dy2c, b3=split_nk(w, True)).view(ctx.shp)
+            else:
+                dx = (mm_nt(dy2c, w) if w.is_contiguous() and dy2c.dtype == w.dtype
+                      else torch.mm(dy2, w.t())).view(ctx.shp)
         dw = db = None
         mg = getattr(w, "main_grad", None)
         if ctx.needs_input_grad[1]:
@@ -163,6 +182,9 @@ class _LinearFn(torch.autograd.Function):
             elif _own(x2, dy2):
                 dw = torch.zeros_like(w)
                 wgrad_into(dw, x2, dy2.contiguous())
+            elif _own32(x2, dy2):
+                from .gemm import wgrad_f32
+                dw = wgrad_f32(x2.contiguous(), dy2.contiguous())
             else:
                 dw = torch.mm(x2.t(), dy2)
         if ctx.has_b and ctx.needs_input_grad[2]:
@@ -241,6 +263,9 @@ def linear(x, weight, bias=None):
         if not ok_b:
             y = y + bias
         return y.view(*shp[:-1], weight.shape[1])
+    if weight.dim() == 2 and _own32(x2, weight) and (bias is None or bias.dtype == torch.float32):
+        from .gemm import gemm_nt_f32, split_nk
+        return gemm_nt_f32(x2, bias=bias, b3=split_nk(weight, False)).view(*shp[:-1], weight.shape[1])
     if not _use_transposed(x2, weight, INFER_TRANSPOSED_MIN_ROWS):
         if bias is not None and bias.dtype == x2.dtype and x2.dim() == 2:
             return torch.addmm(bias, x2, weight).view(*shp[:-1], weight.shape[1])

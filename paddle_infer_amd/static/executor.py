@@ -134,6 +134,11 @@ class Executor:
             keep = set(program.params) | set(fetch_names)
             self._plans[key] = build_plan(ops, keep)
         order, frees, _ = self._plans[key]
+        skey = ("streams",) + key
+        if skey not in self._plans:
+            from .streams import stream_plan, COMM_OPS
+            self._plans[skey] = stream_plan(ops, order) if any(op.type in COMM_OPS for op in ops) else None
+        splan = self._plans[skey]
         env = {}
         for name, val in (feed or {}).items():
             t = val if isinstance(val, torch.Tensor) else torch.as_tensor(np.asarray(val))
@@ -181,25 +186,49 @@ class Executor:
         self._leafmap = {}
         self._cf_depth = 0
         self._training = training
-        dp = None
+        dp = buckets = None
         if compiled is not None and compiled._data_parallel and training:
             import torch.distributed as dist
             if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
                 from .backward import op_role as _role, OPTIMIZE as _OPT, GRAD as _G
                 dp = sorted({n for op in ops if _role(op) == _OPT for n in op.input_names()
                              if n.endswith(_G)})
+                if compiled._build_strategy.fuse_all_reduce_ops:
+                    bkey = ("dp_buckets",) + key
+                    if bkey not in self._plans:
+                        from .streams import GradBuckets
+                        self._plans[bkey] = GradBuckets(ops, order, set(dp), _grad_nbytes(program),
+                                                        world=dist.get_world_size())
+                    buckets = self._plans[bkey]
+        runner = None
+        if splan is not None:
+            from .streams import StreamRunner
+            runner = StreamRunner(self.device, *splan)
+            self.last_stream_runner = runner
         with torch.set_grad_enabled(training):
             for pos, oi in enumerate(order):
                 op = ops[oi]
                 if dp is not None:
                     from .backward import op_role as _role, OPTIMIZE as _OPT
                     if _role(op) == _OPT:
-                        _allreduce_grads(env, dp, compiled._build_strategy.fuse_all_reduce_ops)
+                        if buckets is not None:
+                            buckets.wait()
+                        else:
+                            _allreduce_grads(env, dp, False)
                         dp = None
-                self._run_op(op, sub, env, scope, program)
+                if runner is not None:
+                    runner.run(pos, oi, op, lambda: self._run_op(op, sub, env, scope, program), env)
+                else:
+                    self._run_op(op, sub, env, scope, program)
+                if buckets is not None and dp is not None:
+                    buckets.after(pos, env)
                 for n in frees[pos]:
                     if n not in fetch_names:
                         env.pop(n, None)
+            if runner is not None:
+                runner.finish()
+            if buckets is not None and dp is not None:  # no optimizer op ran: reduce anyway
+                buckets.wait()
         for hook in getattr(program, "_post_run_hooks", ()) if training else ():
             hook(scope, program)  # e.g. static.ExponentialMovingAverage
         if training:  # persistable outputs (updated params / accumulators) back into the Scope
@@ -584,6 +613,14 @@ class CompiledProgram:
         if exec_strategy is not None:
             self._exec_strategy = exec_strategy
         return self
+
+
+def _grad_nbytes(program):
+    """Bytes of ``<param>@GRAD`` (bucket sizing of the data-parallel gradient all-reduce)."""
+    def f(n):
+        p = program.params.get(n[:-len("@GRAD")]) if n.endswith("@GRAD") else None
+        return float(p.numel() * p.element_size()) if p is not None else 0.0
+    return f
 
 
 def _allreduce_grads(env, names, fused=True):

@@ -397,6 +397,8 @@ def _fc(ins, a):
                                                                                     torch.float16):
         from ..ops.linear import linear_bias_act
         y = linear_bias_act(x2, w, b, act) if b is not None else ops.bias_act(linear(x2, w, None), b, act)
+    elif act in ("gelu", "relu", "silu", "gelu_tanh") and x2.is_cuda and x2.dtype == torch.float32:
+        y = ops.bias_act(linear(x2, w, None), b, act)  # split-bf16 GEMM + the f32 bias-act kernel
     else:
         y = linear(x2, w, b)
         if act:

@@ -339,7 +339,7 @@ def static_minimize(opt, loss, st, hcg, startup_program=None, parameters=None, n
     if world > 1 and not gm:
         SM.insert_dp_allreduce(block, world, bool(st.fp16_allreduce))
     if ls is not None:
-        SM.amp_unscale_and_skip(block, ls, amp_cfg)
+        SM.amp_unscale_and_skip(block, ls, amp_cfg, merged=gm)
     if gm:
         cfg = st.gradient_merge_configs or {}
         SM.gradient_merge_rewrite(block, int(cfg.get("k_steps", 1)), bool(cfg.get("avg", True)),

@@ -102,6 +102,62 @@ def _gather_last(x, group):
     return torch.cat(list(out.unbind(0)), dim=-1)
 
 
+class _ColumnParallelFn(torch.autograd.Function):
+    """``c_identity`` + linear of a column-parallel layer in one Function, so the backward
+    overlaps the input-gradient all-reduce with the weight-gradient GEMM (reference
+    `mp_layers.py:155` runs them back to back; this is the Megatron async-grad-allreduce order):
+    dX = dY·Wᵀ → RCCL all-reduce of dX launched asynchronously → dW = Xᵀ·dY (+ dB) on the compute
+    stream while the collective runs on RCCL's stream → wait."""
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda")
+    def forward(ctx, x, w, b, group):
+        if x.is_cuda and w.dtype == torch.float32 and torch.is_autocast_enabled("cuda"):
+            dt = torch.get_autocast_dtype("cuda")
+            x, w, b = x.to(dt), w.to(dt), b.to(dt) if b is not None else None
+        with torch.no_grad():
+            y = _linear(x, w, b)
+        ctx.save_for_backward(x, w)
+        ctx.bias, ctx.group, ctx.shp = b, group, x.shape
+        return y
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, dy):
+        from ...ops.linear import bias_grad, input_grad, weight_grad
+        x, w = ctx.saved_tensors
+        x2 = x.reshape(-1, x.shape[-1])
+        dy2 = dy.reshape(-1, w.shape[1]).contiguous()
+        dx = work = None
+        if ctx.needs_input_grad[0]:
+            dx = input_grad(dy2, w).view(ctx.shp).contiguous()
+            if _ws(ctx.group) > 1:
+                work = dist.all_reduce(dx, group=ctx.group, async_op=True)
+        dw = weight_grad(x2, dy2, w) if ctx.needs_input_grad[1] else None
+        db = bias_grad(dy2, ctx.bias) if ctx.bias is not None and ctx.needs_input_grad[2] else None
+        if work is not None:
+            work.wait()
+        return dx, dw, db, None
+
+
+class _MPAllReduceBias(torch.autograd.Function):
+    """Row-parallel output all-reduce whose bias was added by ONE rank's GEMM epilogue (rank 0):
+    fwd all-reduce; bwd identity for the activation and, on the ranks that did not add the bias,
+    its gradient Σ_rows dY — every rank ends with the same replicated bias gradient."""
+
+    @staticmethod
+    def forward(ctx, y, b, group):
+        ctx.n = b.shape[-1]
+        if _ws(group) > 1:
+            y = y.contiguous()
+            dist.all_reduce(y, group=group)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, g.reshape(-1, ctx.n).sum(0), None
+
+
 def c_identity(x, group=None):
     return _CIdentity.apply(x, group)
 
@@ -164,8 +220,11 @@ class ColumnParallelLinear(Layer):
             _mark(self.bias, n > 1, 0)
 
     def forward(self, x):
-        x = c_identity(x, self.group)
-        y = _linear(x, self.weight, self.bias)
+        if torch.is_grad_enabled() and (self.weight.requires_grad or getattr(self.weight, "main_grad", None)
+                                        is not None):
+            y = _ColumnParallelFn.apply(x, self.weight, self.bias, self.group)
+        else:
+            y = _linear(x, self.weight, self.bias)
         if self.gather_output and _ws(self.group) > 1:
             y = c_concat(y, self.group)
         return y
@@ -191,9 +250,13 @@ class RowParallelLinear(Layer):
     def forward(self, x):
         if not self.input_is_parallel:
             x = c_split(x, self.group)
-        y = _linear(x, self.weight, None)
-        y = mp_allreduce(y, self.group)
-        return y + self.bias if self.bias is not None else y
+        if self.bias is None or _ws(self.group) == 1:
+            y = _linear(x, self.weight, self.bias)
+            return mp_allreduce(y, self.group)
+        # the bias rides rank 0's GEMM epilogue (added once before the sum), no separate pass
+        if _rank(self.group) == 0:
+            return mp_allreduce(_linear(x, self.weight, self.bias), self.group)
+        return _MPAllReduceBias.apply(_linear(x, self.weight, None), self.bias, self.group)
 
 
 class ParallelCrossEntropy(Layer):

@@ -178,9 +178,12 @@ def _optimizer_ops(block):
             and "Grad" in op.paddle_inputs]
 
 
-def amp_unscale_and_skip(block, ls, cfg):
+def amp_unscale_and_skip(block, ls, cfg, merged=False):
     """check_finite_and_unscale + update_loss_scaling ahead of the optimizer ops; every optimizer
-    op skips its update on a step with inf/nan (SkipUpdate = found_inf)."""
+    op skips its update on a step with inf/nan (SkipUpdate = found_inf). ``merged`` (gradient
+    merge follows): the two ops take the OPTIMIZE role so ``gradient_merge_rewrite`` moves them
+    into the every-k-steps block, where they act once on the merged gradients (reference
+    GradientMergeOptimizer runs the AMP apply_gradients inside its conditional block)."""
     prog = block.program
     opt_ops = _optimizer_ops(block)
     grads = list(dict.fromkeys(op.paddle_inputs["Grad"][0] for op in opt_ops))
@@ -188,9 +191,10 @@ def amp_unscale_and_skip(block, ls, cfg):
     good = _persistable(prog, "num_good_steps_0", torch.zeros([1], dtype=torch.int32))
     bad = _persistable(prog, "num_bad_steps_0", torch.zeros([1], dtype=torch.int32))
     first = min(i for i, op in enumerate(block.ops) if op_role(op) == OPTIMIZE)
-    # BACKWARD role: per run (a gradient-merge block takes only the optimizer ops)
+    # BACKWARD role: once per run; OPTIMIZE role under gradient merge: once per k runs
+    role = OPTIMIZE if merged else BACKWARD
     new = [_mkop(block, "check_finite_and_unscale", {"X": grads, "Scale": [ls]},
-                 {"Out": grads, "FoundInfinite": [found]}, {}, BACKWARD)]
+                 {"Out": grads, "FoundInfinite": [found]}, {}, role)]
     if cfg.get("use_dynamic_loss_scaling", True):
         new.append(_mkop(block, "update_loss_scaling",
                          {"X": grads, "FoundInfinite": [found], "PrevLossScaling": [ls],
@@ -200,7 +204,7 @@ def amp_unscale_and_skip(block, ls, cfg):
                           "decr_every_n_nan_or_inf": int(cfg.get("decr_every_n_nan_or_inf", 2)),
                           "incr_ratio": float(cfg.get("incr_ratio", 2.0)),
                           "decr_ratio": float(cfg.get("decr_ratio", 0.5)), "stop_update": False},
-                         BACKWARD))
+                         role))
     block.ops[first:first] = new
     for op in opt_ops:
         op.paddle_inputs["SkipUpdate"] = [found]
@@ -333,6 +337,8 @@ def gradient_merge_rewrite(block, k_steps, avg=True, world=1, fp16_allreduce=Fal
         body += _allreduce_ops(sub, list(merged.values()), world, fp16_allreduce, OPTIMIZE)
     for op in tail:
         rename_inputs(op, merged)
+        if op.type in ("check_finite_and_unscale", "update_loss_scaling"):
+            _rename_outputs(op, merged)  # unscale the merged gradients in place
         op.block = sub
         body.append(op)
     for g, m in merged.items():

@@ -164,38 +164,49 @@ class _LinearFn(torch.autograd.Function):
     def backward(ctx, dy):
         x2, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, w.shape[1])
-        dx = None
-        if ctx.needs_input_grad[0]:
-            dy2c = dy2.contiguous() if w.is_contiguous() else dy2
-            if _own32(dy2c, w):
-                from .gemm import gemm_nt_f32, split_nk
-                dx = gemm_nt_f32(dy2c, b3=split_nk(w, True)).view(ctx.shp)
-            else:
-                dx = (mm_nt(dy2c, w) if w.is_contiguous() and dy2c.dtype == w.dtype
-                      else torch.mm(dy2, w.t())).view(ctx.shp)
-        dw = db = None
-        mg = getattr(w, "main_grad", None)
-        if ctx.needs_input_grad[1]:
-            if mg is not None:
-                wgrad_into(mg, x2, dy2.contiguous())
-                _fire(w)
-            elif _own(x2, dy2):
-                dw = torch.zeros_like(w)
-                wgrad_into(dw, x2, dy2.contiguous())
-            elif _own32(x2, dy2):
-                from .gemm import wgrad_f32
-                dw = wgrad_f32(x2.contiguous(), dy2.contiguous())
-            else:
-                dw = torch.mm(x2.t(), dy2)
-        if ctx.has_b and ctx.needs_input_grad[2]:
-            b = ctx.bias
-            bmg = getattr(b, "main_grad", None)
-            if bmg is not None and dy2.is_cuda and dy2.dtype == bmg.dtype:
-                colsum_into(dy2, bmg, accumulate=True)
-                _fire(b)
-            else:
-                db = dy2.sum(0)
+        dx = input_grad(dy2, w).view(ctx.shp) if ctx.needs_input_grad[0] else None
+        dw = weight_grad(x2, dy2, w) if ctx.needs_input_grad[1] else None
+        db = bias_grad(dy2, ctx.bias) if ctx.has_b and ctx.needs_input_grad[2] else None
         return dx, dw, db
+
+
+def input_grad(dy2, w):
+    """dX = dY · Wᵀ for a [in, out] weight on the own GEMMs (16-bit or split-bf16 fp32)."""
+    dy2c = dy2.contiguous() if w.is_contiguous() else dy2
+    if _own32(dy2c, w):
+        from .gemm import gemm_nt_f32, split_nk
+        return gemm_nt_f32(dy2c, b3=split_nk(w, True))
+    if w.is_contiguous() and dy2c.dtype == w.dtype:
+        return mm_nt(dy2c, w)
+    return torch.mm(dy2, w.t())
+
+
+def weight_grad(x2, dy2, w):
+    """dW = Xᵀ · dY: accumulated straight into ``w.main_grad`` (then the grad-ready hook fires,
+    None returned) or returned as a tensor."""
+    mg = getattr(w, "main_grad", None)
+    if mg is not None:
+        wgrad_into(mg, x2, dy2.contiguous())
+        _fire(w)
+        return None
+    if _own(x2, dy2):
+        dw = torch.zeros_like(w)
+        wgrad_into(dw, x2, dy2.contiguous())
+        return dw
+    if _own32(x2, dy2):
+        from .gemm import wgrad_f32
+        return wgrad_f32(x2.contiguous(), dy2.contiguous())
+    return torch.mm(x2.t(), dy2)
+
+
+def bias_grad(dy2, b):
+    """dB = Σ_rows dY into ``b.main_grad`` (HIP column sums; None returned) or as a tensor."""
+    bmg = getattr(b, "main_grad", None)
+    if bmg is not None and dy2.is_cuda and dy2.dtype == bmg.dtype:
+        colsum_into(dy2, bmg, accumulate=True)
+        _fire(b)
+        return None
+    return dy2.sum(0)
 
 
 

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Ablated assembly-GEMM variants (no DMA / no barriers / no LDS reads) on the out-projection shape:
+# wall time and cycle counters (GRBM_GUI_ACTIVE) — what each instruction class costs the mainloop.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+OUT=gpurun_out/r5_abl
+mkdir -p $OUT
+for V in base nodma nobar noreads nodma+nobar; do
+  if [ $V = base ]; then H=paddle_infer_amd/_lib/piamd_agemm.hsaco; else H=paddle_infer_amd/_lib/piamd_agemm_abl_$V.hsaco; fi
+  PIAMD_AGEMM_HSACO=$H timeout -k 10 120 python3 tools/gemm_ab_probe.py --M 98304 --N 2048 --K 2048 --impls asm --iters 20 --rounds 5 > $OUT/wall_$V.jsonl 2>&1 || { echo "wall $V failed"; tail -3 $OUT/wall_$V.jsonl; exit 1; }
+  echo "$V $(grep '^{' $OUT/wall_$V.jsonl)"
+  PIAMD_AGEMM_HSACO=$H timeout -s KILL 90 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY -d "$OUT/p_$V" -o run --output-format csv -- python3 tools/gemm_ab_probe.py --M 98304 --N 2048 --K 2048 --impls asm --iters 10 --rounds 1 > "$OUT/p_$V.log" 2>&1 || { echo "pmc $V failed"; exit 1; }
+  python3 tools/pmc_summary.py $OUT/p_$V agemm | grep -E "GRBM_GUI|WAVE_CYCLES|WAIT" 
+done

@@ -155,6 +155,27 @@ def test_amp_fp16_loss_scaling_ops_and_inf_skip():
     assert float(ei["loss_scaling_0"]) == 512.0 and float(e3["loss_scaling_0"]) == 1024.0
 
 
+def test_amp_fp16_with_gradient_merge_unscales_merged_grads_once_per_k():
+    """AMP + gradient merge: check_finite_and_unscale / update_loss_scaling run inside the
+    every-k block on the merged gradients. An inf in the FIRST micro-step of a window skips that
+    window's update (merged grads zeroed) and halves the scale once; the next window trains as if
+    the first never happened."""
+    f = _feeds(4)
+    cfg = {"use_bf16": False, "init_loss_scaling": 1024.0, "decr_every_n_nan_or_inf": 1,
+           "incr_every_n_steps": 1000}
+    flags = {"amp": True, "amp_configs": cfg, "gradient_merge": True,
+             "gradient_merge_configs": {"k_steps": 2, "avg": True}}
+    l, p, types, extra = _train(flags, f)
+    assert types.count("check_finite_and_unscale") == 1 and "conditional_block" in types
+    assert float(extra["loss_scaling_0"]) == 1024.0
+    li, pi, _, ei = _train(flags, f, inject=0)
+    assert float(ei["loss_scaling_0"]) == 512.0  # one decrement for the whole window
+    for t in pi:
+        assert torch.isfinite(torch.as_tensor(t)).all()
+    l2, p2, _, _ = _train(flags, f[2:])
+    _close_params(pi, p2, tol=2e-3)
+
+
 # ----------------------------------------------------------------------------- 2-rank gloo
 def _dp_worker(rank, world, flags, checkpoints):
     feeds = _feeds(4, 2 * B)

@@ -168,19 +168,7 @@ PIAMD_EXPORT int piamd_agemm(const void* a, long long lda, int trans_a, const vo
   // even K-block count >= 4; otherwise one tile per workgroup
   const int nk = K / ksplit / 64;
   const bool persistent = nk % 2 == 0 && nk >= 4 && !getenv("PIAMD_AGEMM_NO_PERSIST");
-  // NT products take the 8-wave ping-pong kernel (two waves per SIMD, `gemm_gen_pp.py`)
-  static const bool use_pp = [] {
-    const char* e = getenv("PIAMD_AGEMM_PP");  // opt-in until measured (1 = on)
-    return e && atoi(e) > 0;
-  }();
-  const bool pp = persistent && a_kc && b_kc && use_pp;
-  static const std::string ppv = [] {  // PIAMD_AGEMM_PPV=N: schedule A/B variant (plain bf16 only)
-    const char* e = getenv("PIAMD_AGEMM_PPV");
-    return std::string(e && *e ? std::string("_v") + e : "");
-  }();
-  std::string name = std::string("piamd_agemm_") + (pp ? "q_" : persistent ? "p_" : "") + lay + "_" + ek +
-                     (f16 ? "_f16" : "");
-  if (pp && !ppv.empty() && !f16 && std::string(ek) == "bf16") name += ppv;
+  std::string name = std::string("piamd_agemm_") + (persistent ? "p_" : "") + lay + "_" + ek + (f16 ? "_f16" : "");
   hipFunction_t f = get_fn(name);
   if (!f) return (int)hipErrorInvalidDeviceFunction;
   g.a = a;

@@ -20,8 +20,5 @@ struct FaArgs {
   int map;  // backward grid order, bit 0 dQ / bit 1 dK-dV kernel: 0 = the blocks of one (batch,
             // head) spread over the grid, 1 = grouped on one XCD (fa_map) so they share that head's
             // K/V (dQ) or Q/dO (dK-dV) panels in L2 (set by the entry point)
-  // optional backward scratch (padded layout only): the dK/dV kernel stores dS there and the dQ
-  // kernel reads it back instead of recomputing S / dP. B·Hq·(2⌈Sq/64⌉)·(4⌈Sk/128⌉)·2048 bytes
-  // (ops/attention.py `_ds_bytes`); null = recompute
-  void* ds;
+  void* ds;  // reserved (ABI slot of the removed stored-dS backward; always null)
 };

@@ -27,9 +27,9 @@
 //     dKᵀ/dVᵀ kept in accumulators across the whole sweep over query tiles and the q-heads of a GQA
 //     group. dQ: the forward's structure (query row on the lane), dSᵀ feeds dQᵀ = Kᵀ·dSᵀ from
 //     registers. Recomputing S/dP in the dQ kernel removes the f32 dQ atomics and keeps the
-//     result bitwise deterministic. With a dS scratch (FaArgs::ds, the default below a size cap)
-//     the dK/dV kernel stores its 16-bit dS tiles and the dQ kernel (bwd_dq_ds_kernel) only
-//     runs dQᵀ = Kᵀ·dSᵀ over them: a third of the recompute's MFMA work, still atomic-free.
+//     result bitwise deterministic. (A stored-dS variant — dK/dV writes 16-bit dS, dQ only runs
+//     Kᵀ·dSᵀ — measured net-neutral at the GPT shape and slower elsewhere; removed in round 5,
+//     A/B record profiles/fa_persist_r4.txt.)
 //   * Dropout: keep(q, key) is a stateless counter hash of (seed, offset, row, key) — the same
 //     keyed two-round lowbias32 as the LayerNorm dropout (common.h), one 32-bit hash per PAIR of
 //     adjacent keys (two 16-bit uniforms). The forward, dK/dV and dQ kernels regenerate the same
@@ -788,11 +788,7 @@ __global__ __launch_bounds__(256) void bwd_pre_kernel(const unsigned short* __re
 // Backward dK/dV: workgroup = 128 keys of one (batch, kv-head); sweeps the q-heads of the GQA
 // group and all query tiles of 64 rows. Key on the MFMA lane.
 // ------------------------------------------------------------------------------------------
-// DS: also store every dS tile (bf16/fp16, the values the dK product consumes) into FaArgs::ds as
-// 2-KiB blocks [32 keys][32 queries] (64-B rows) at block index ((b·Hq + hq)·NQ32 + q/32)·NK32 +
-// key/32, NQ32 = 2·⌈Sq/64⌉, NK32 = 4·⌈Sk/128⌉: each lane writes registers 4g..4g+3 of its key
-// packed (8 B) at row `key`, column 8g + 4hh — the layout bwd_dq_ds_kernel reads transposed.
-template <int D, bool F16, bool CAUSAL, int FEAT, bool DS = false>
+template <int D, bool F16, bool CAUSAL, int FEAT>
 __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(FaArgs a) {
   typedef ET<F16> E;
   typedef typename E::V8 V8;
@@ -916,25 +912,6 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(FaArgs a) {
   if (total > 0) issue(0, std::integral_constant<int, 0>{});
   __syncthreads();
 
-  // DS: a tile's dS fragments are stored at the START of the next tile, next to that tile's DMA,
-  // so the write acknowledgements overlap the DMA the tile-end barrier waits for anyway (stored
-  // right after they are computed, they added their full latency to every tile: +20 % dK/dV time)
-  typename ET<F16>::V8 ds_pend[4];
-  char* ds_blk = nullptr;
-  const int ds_nk32 = 4 * ((Sk + 127) >> 7);
-  auto ds_flush = [&]() {
-    if (!ds_blk) return;
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const u32x4 d = __builtin_bit_cast(u32x4, ds_pend[2 * qt + s]);
-        char* p = ds_blk + (long long)qt * ds_nk32 * 2048 + 32 * s;
-        *reinterpret_cast<uint2*>(p) = make_uint2(d[0], d[1]);        // registers 8s..8s+3
-        *reinterpret_cast<uint2*>(p + 16) = make_uint2(d[2], d[3]);   // registers 8s+4..8s+7
-      }
-    ds_blk = nullptr;
-  };
   // one query tile; every LDS address below is a precomputed lane offset + an immediate. The
   // buffer parity is a template constant (two tile bodies) so each body reads one LDS object
   // while the DMA lands in the other.
@@ -946,7 +923,6 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(FaArgs a) {
     const float* dst = lst + BQ;
     const int hq = hk * group + it / tiles_per_head;
     const int q0 = (qt0 + it % tiles_per_head) * BQ;
-    if constexpr (DS) ds_flush();
     if (it + 1 < total) issue(it + 1, std::integral_constant<int, BUF ^ 1>{});
     f32x16 sacc[2], pacc[2];
     // S' = Q·Kᵀ − lse/scale, dP' = dO·Vᵀ − δ: row constants as the initial accumulators
@@ -1029,13 +1005,6 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(FaArgs a) {
         pb[2 * qt + s] = E::frag(sacc[qt], s);
         db[2 * qt + s] = E::frag(pacc[qt], s);
       }
-    if constexpr (DS) {  // kept for the next tile's start (stored beside its DMA, see ds_flush)
-      const int nq32 = 2 * ((Sq + 63) >> 6);
-      ds_blk = (char*)a.ds + ((((long long)(b * Hq + hq) * nq32 + (q0 >> 5)) * ds_nk32 + (kw0 >> 5)) << 11) +
-               l32 * 64 + 8 * hh;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) ds_pend[i] = db[i];
-    }
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -1052,7 +1021,6 @@ __global__ __launch_bounds__(256, 1) void bwd_dkdv_kernel(FaArgs a) {
     tile(it, std::integral_constant<int, 0>{});
     if (it + 1 < total) tile(it + 1, std::integral_constant<int, 1>{});
   }
-  if constexpr (DS) ds_flush();
 
   if (key < Sk) {
     const float vs = (FEAT & F_DROP) ? drk.inv : 1.f;
@@ -1270,139 +1238,6 @@ __global__ __launch_bounds__(256, 2) void bwd_dq_kernel(FaArgs a) {
   }
 }
 
-// ------------------------------------------------------------------------------------------
-// Backward dQ from the stored dS (FaArgs::ds, written by bwd_dkdv_kernel<..., DS = true>):
-// dQᵀ = Kᵀ·dSᵀ is the only product left — no Q / dO / V, no exp, no mask or dropout (all folded
-// into the stored dS) — one third of the recomputing kernel's MFMA work for a stream of the dS
-// blocks. Same grid and query-row-on-lane structure as bwd_dq_kernel. Each wave DMAs its own two
-// 2-KiB blocks per 64-key tile into LDS and reads the dSᵀ B operand back with
-// ds_read_b64_tr_b16 (the [key][query] image with 64-B rows is bank-conflict free for it).
-// Key halves past this wave's causal limit were never written and are skipped.
-// ------------------------------------------------------------------------------------------
-template <int D, bool F16, bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void bwd_dq_ds_kernel(FaArgs a) {
-  typedef ET<F16> E;
-  typedef typename E::V8 V8;
-  constexpr int DP = D > 64 ? 128 : 64;
-  constexpr int BM = 128, BN = 64;
-  constexpr int KSTEPS = D / 16;
-  constexpr int DT = D / 32;
-  constexpr int ROWB = DP * 2;
-  constexpr int TILE_B = BN * ROWB;
-  constexpr int DSW = 4096;  // one wave's two dS blocks of a tile
-  __shared__ __attribute__((aligned(16))) char kt0[TILE_B];
-  __shared__ __attribute__((aligned(16))) char kt1[TILE_B];
-  __shared__ __attribute__((aligned(16))) char dsb0[4 * DSW];
-  __shared__ __attribute__((aligned(16))) char dsb1[4 * DSW];
-
-  const unsigned short* k = (const unsigned short*)a.k;
-  unsigned short* dq = (unsigned short*)a.dq;
-  const int B = a.B, Sq = a.Sq, Sk = a.Sk, Hq = a.Hq, Hk = a.Hk;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int l32 = lane & 31, hh = lane >> 5, gi = lane & 15, g = lane >> 4;
-  const int nmb = (Sq + BM - 1) / BM;
-  const int HB = Hq * B;
-  int mb = CAUSAL ? (nmb - 1 - (int)blockIdx.x / HB) : (int)blockIdx.x / HB;
-  int hq = (int)blockIdx.x % Hq, b = ((int)blockIdx.x % HB) / Hq;
-  if (a.map & 1) {
-    int grp, sub;
-    if (!fa_map(nmb, HB, grp, sub)) return;
-    mb = CAUSAL ? nmb - 1 - sub : sub;
-    hq = grp % Hq;
-    b = grp / Hq;
-  }
-  const int hk = hq / (Hq / Hk);
-  const int m0 = mb * BM;
-  const int qrow0 = m0 + w * 32;
-  const int qpos = qrow0 + l32;
-  const int coff = Sk - Sq;
-  const int nq32 = 2 * ((Sq + 63) >> 6), nk32 = 4 * ((Sk + 127) >> 7);
-  // this wave's row of dS blocks (block kb32 at + kb32 · 2 KiB)
-  const char* dsrow = (const char*)a.ds +
-                      ((((long long)(b * Hq + hq) * nq32 + (min(qrow0, Sq - 1) >> 5)) * nk32) << 11);
-  const unsigned short* kbase = k + b * a.skb + hk * a.skh;
-
-  int n_end = Sk;
-  if (CAUSAL) n_end = min(Sk, m0 + BM + coff);
-  const int ntiles = n_end <= 0 ? 0 : (n_end + BN - 1) / BN;
-  // keys [0, klim) carry dS for this wave's rows; 32-key half h of tile t is used iff 64t + 32h < klim
-  const int klim = qrow0 >= Sq ? 0 : (CAUSAL ? max(0, min(Sk, qrow0 + 32 + coff)) : Sk);
-
-  LaneOffs<ROWB, KSTEPS, DT> L;
-  lane_offs(lane, L);
-  int trd[2];  // transposed dS reads: rows 4hh + 8jj + gi/4 (+16s), columns 16(g&1) + 4(gi&3)
-#pragma unroll
-  for (int jj = 0; jj < 2; ++jj) trd[jj] = w * DSW + (4 * hh + 8 * jj + (gi >> 2)) * 64 + (16 * (g & 1) + 4 * (gi & 3)) * 2;
-
-  f32x16 qacc[DT];
-#pragma unroll
-  for (int i = 0; i < DT; ++i)
-#pragma unroll
-    for (int j = 0; j < 16; ++j) qacc[i][j] = 0.f;
-
-  auto issue = [&](int t, auto bufc) {
-    char* kt = decltype(bufc)::value ? kt1 : kt0;
-    char* db = (decltype(bufc)::value ? dsb1 : dsb0) + w * DSW;
-    glds_tile<BN, ROWB, D / 8>(kbase, a.sks, t * BN, Sk - 1, kt, w, lane);
-    const char* src = dsrow + ((long long)t << 12) + lane * 16;
-    const int rem = klim - 64 * t;  // wave-uniform
-    if (rem > 0) {
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)db, 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 1024),
-                                       (__attribute__((address_space(3))) void*)(db + 1024), 16, 0, 0);
-    }
-    if (rem > 32) {
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 2048),
-                                       (__attribute__((address_space(3))) void*)(db + 2048), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + 3072),
-                                       (__attribute__((address_space(3))) void*)(db + 3072), 16, 0, 0);
-    }
-  };
-  if (ntiles > 0) issue(0, std::integral_constant<int, 0>{});
-  __syncthreads();
-
-  auto tile = [&](int t, auto bufc) {
-    constexpr int BUF = decltype(bufc)::value;
-    const char* kt = BUF ? kt1 : kt0;
-    const char* db = BUF ? dsb1 : dsb0;
-    if (t + 1 < ntiles) issue(t + 1, std::integral_constant<int, BUF ^ 1>{});
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt) {
-      if (64 * t + 32 * tt < klim) {
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const int so = tt * 2048 + s * 1024;
-          const V8 dsf = cat44<F16>(lds_tr_at(db, trd[0] + so), lds_tr_at(db, trd[1] + so));
-          const int ro = 16 * (2 * tt + s) * ROWB;
-#pragma unroll
-          for (int dt = 0; dt < DT; ++dt)
-            qacc[dt] = E::mfma(cat44<F16>(lds_tr_at(kt, L.tr[0][dt] + ro), lds_tr_at(kt, L.tr[1][dt] + ro)),
-                               dsf, qacc[dt]);
-        }
-      }
-    }
-    __syncthreads();
-  };
-  for (int t = 0; t < ntiles; t += 2) {
-    tile(t, std::integral_constant<int, 0>{});
-    if (t + 1 < ntiles) tile(t + 1, std::integral_constant<int, 1>{});
-  }
-
-  if (qpos < Sq) {
-    unsigned short* qp = dq + b * a.sqb + (long long)qpos * a.sqs + hq * a.sqh;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d0 = 32 * dt + 8 * g4 + 4 * hh;
-        uint2 pk;
-        pk.x = pack2<F16>(qacc[dt][4 * g4 + 0] * a.scale, qacc[dt][4 * g4 + 1] * a.scale);
-        pk.y = pack2<F16>(qacc[dt][4 * g4 + 2] * a.scale, qacc[dt][4 * g4 + 3] * a.scale);
-        *reinterpret_cast<uint2*>(qp + d0) = pk;
-      }
-  }
-}
 
 // ------------------------------------------------------------------------------------------
 // Launchers (one per element type; the exported entry points in flash_attn.hip dispatch).
@@ -1482,13 +1317,8 @@ template <bool F16, int D, bool C>
 int launch_bwd_feat(const FaArgs& a, dim3 gkv, dim3 gq, hipStream_t st) {
   const int feat = (a.p_drop > 0.f ? F_DROP : 0) | (a.mask ? F_MASK : 0);
 #define BWD_F(FF)                                                                              \
-  if (a.ds) {                                                                                  \
-    hipLaunchKernelGGL((bwd_dkdv_kernel<D, F16, C, FF, true>), gkv, dim3(256), 0, st, a);      \
-    hipLaunchKernelGGL((bwd_dq_ds_kernel<D, F16, C>), gq, dim3(256), 0, st, a);                \
-  } else {                                                                                     \
-    hipLaunchKernelGGL((bwd_dkdv_kernel<D, F16, C, FF>), gkv, dim3(256), 0, st, a);            \
-    hipLaunchKernelGGL((bwd_dq_kernel<D, F16, C, FF>), gq, dim3(256), 0, st, a);               \
-  }                                                                                            \
+  hipLaunchKernelGGL((bwd_dkdv_kernel<D, F16, C, FF>), gkv, dim3(256), 0, st, a);              \
+  hipLaunchKernelGGL((bwd_dq_kernel<D, F16, C, FF>), gq, dim3(256), 0, st, a);                 \
   break;
   switch (feat) {
     case 0: BWD_F(0)

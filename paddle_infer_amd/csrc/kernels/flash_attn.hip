@@ -40,7 +40,6 @@ PIAMD_EXPORT int piamd_fa_bwd(const FaArgs* args, int f16, hipStream_t stream) {
   a.map = fa::fa_bwd_map(a);
   if (a.cu_q) {
     a.sqb = a.skb = a.svb = a.sob = 0;
-    a.ds = nullptr;  // stored dS: padded layout only
   }
   if (a.B == 0 || a.Sq == 0 || a.Sk == 0) return 0;
   return f16 ? fa_bwd_f16(a, stream) : fa::launch_bwd<false>(a, stream);

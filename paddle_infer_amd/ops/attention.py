@@ -102,19 +102,6 @@ def _fwd(q, k, v, causal, scale, mask=None, p=0.0, seed=0, off=0):
     return o, lse
 
 
-# Stored-dS backward (flash_attn.h bwd_dq_ds_kernel): the dK/dV kernel writes dS and the dQ kernel
-# reads it back instead of recomputing S and dP, while the scratch stays under this many bytes
-# (B96 S1024 H16: 3.2 GB). Opt-in (PIAMD_FA_DS_MAX_MB): measured at B96 S1024 H16 D128 the dQ kernel
-# drops 929 -> 551 us but dK/dV grows 1596 -> 1957 us with the dS stores (fwd+bwd 3.997 -> 3.948 ms),
-# and D = 64 / S = 2048-4096 get slower (profiles/fa_persist_r4.txt), so recompute stays the default.
-DS_MAX_BYTES = int(os.environ.get("PIAMD_FA_DS_MAX_MB", "0")) << 20
-
-
-def _ds_bytes(B, Hq, Sq, Sk) -> int:
-    """Bytes of the dS scratch: B·Hq rows of (2⌈Sq/64⌉) x (4⌈Sk/128⌉) 2-KiB blocks (fa_args.h)."""
-    return B * Hq * (2 * -(-Sq // 64)) * (4 * -(-Sk // 128)) * 2048
-
-
 def _bwd(q, k, v, o, lse, do, dq, dk, dv, causal, scale, mask=None, p=0.0, seed=0, off=0):
     B, Sq, Hq, D = q.shape
     Sk, Hk = k.shape[1], k.shape[2]
@@ -126,9 +113,7 @@ def _bwd(q, k, v, o, lse, do, dq, dk, dv, causal, scale, mask=None, p=0.0, seed=
     delta = torch.empty((2, B, Hq, Sq), device=q.device, dtype=torch.float32)
     a = _args(q, k, v, o, lse, causal, scale, mask, p, seed, off, B, Sq, Sk, Hq, Hk, D)
     a.dout, a.delta, a.dq, a.dk, a.dv = do.data_ptr(), delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr()
-    nds = _ds_bytes(B, Hq, Sq, Sk)
-    ds = torch.empty(nds // 2, device=q.device, dtype=q.dtype) if nds <= DS_MAX_BYTES else None
-    a.ds = _lib.ptr(ds)
+    a.ds = None
     _lib.call("piamd_fa_bwd", ctypes.byref(a), _f16(q), _lib.stream())
 
 

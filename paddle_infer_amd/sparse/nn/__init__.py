@@ -1,7 +1,7 @@
 """``paddle.sparse.nn`` (reference `python/paddle/sparse/nn/`): activations over stored values,
 sparse softmax (per row over the stored entries), BatchNorm over the values of a sparse
-``[N, D, H, W, C]`` tensor, and 3-D (submanifold) convolution / max pooling evaluated densely and
-re-sparsified on the output pattern."""
+``[N, D, H, W, C]`` tensor, and 3-D (submanifold) convolution / max pooling / mask attention on
+the active sites only (`conv.py`: rulebook + gather → grouped MFMA GEMM → scatter)."""
 from __future__ import annotations
 
 import torch
@@ -33,14 +33,10 @@ class functional:  # noqa: N801
     @staticmethod
     def conv3d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NDHWC",
                name=None, subm=False):
-        d = x.to_dense().permute(0, 4, 1, 2, 3)  # NDHWC → NCDHW
-        w = weight.permute(4, 3, 0, 1, 2)  # [kd, kh, kw, Cin, Cout] → [Cout, Cin, kd, kh, kw]
-        y = torch.nn.functional.conv3d(d, w, bias, stride, padding, dilation, groups)
-        y = y.permute(0, 2, 3, 4, 1)
-        if subm:  # submanifold: outputs only where the input had active sites
-            active = (x.to_dense() != 0).any(-1, keepdim=True)
-            y = y * active
-        return y.to_sparse(4)
+        """Sparse conv on the active sites: rulebook + gather → grouped MFMA GEMM → scatter
+        (`sparse/nn/conv.py`)."""
+        from .conv import conv3d
+        return conv3d(x, weight, bias, stride, padding, dilation, groups, data_format, subm=subm)
 
     @staticmethod
     def subm_conv3d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1,
@@ -51,23 +47,14 @@ class functional:  # noqa: N801
     @staticmethod
     def max_pool3d(x, kernel_size, stride=None, padding=0, ceil_mode=False, data_format="NDHWC",
                    name=None):
-        d = x.to_dense().permute(0, 4, 1, 2, 3)
-        y = torch.nn.functional.max_pool3d(d, kernel_size, stride, padding, ceil_mode=ceil_mode)
-        return y.permute(0, 2, 3, 4, 1).to_sparse(4)
+        from .conv import max_pool3d
+        return max_pool3d(x, kernel_size, stride, padding, ceil_mode, data_format)
 
     @staticmethod
     def attention(query, key, value, sparse_mask, key_padding_mask=None, attn_mask=None, name=None):
-        """Sparse-mask attention: scores only at ``sparse_mask`` (CSR [B*H, S, S]) positions."""
-        scale = query.shape[-1] ** -0.5
-        s = (query @ key.transpose(-1, -2)) * scale
-        m = sparse_mask.to_dense().reshape(s.shape) != 0
-        if attn_mask is not None:
-            s = s + attn_mask
-        if key_padding_mask is not None:
-            s = s + key_padding_mask[:, None, None, :]
-        s = s.masked_fill(~m, float("-inf"))
-        p = torch.softmax(s, -1).nan_to_num(0.0)
-        return p @ value
+        """Scores only at ``sparse_mask`` (CSR [B*H, S, S]) entries: SDDMM → segment softmax → SpMM."""
+        from .conv import mask_attention
+        return mask_attention(query, key, value, sparse_mask, key_padding_mask, attn_mask)
 
 
 class ReLU(Layer):

@@ -1,6 +1,6 @@
 """``paddle.text`` (reference `python/paddle/text/`): Viterbi decoding for CRF-style sequence
-labelling, and the dataset classes (which need downloads — without network access they load only
-from a local ``data_file``)."""
+labelling, and the dataset classes (`datasets.py`: the reference's parsers over the archives it
+downloads — without network access they read a local ``data_file``)."""
 from __future__ import annotations
 
 import torch
@@ -88,9 +88,5 @@ class UCIHousing(_OfflineDataset):
         return self.data[i][:-1], self.data[i][-1:]
 
 
-Conll05st = type("Conll05st", (_OfflineDataset,), {"NAME": "Conll05st"})
-Imdb = type("Imdb", (_OfflineDataset,), {"NAME": "Imdb"})
-Imikolov = type("Imikolov", (_OfflineDataset,), {"NAME": "Imikolov"})
-Movielens = type("Movielens", (_OfflineDataset,), {"NAME": "Movielens"})
-WMT14 = type("WMT14", (_OfflineDataset,), {"NAME": "WMT14"})
-WMT16 = type("WMT16", (_OfflineDataset,), {"NAME": "WMT16"})
+from . import datasets  # noqa: E402
+from .datasets import Conll05st, Imdb, Imikolov, Movielens, WMT14, WMT16  # noqa: E402,F401

@@ -484,7 +484,8 @@ class Kernel:
             for i in range(8):
                 if kc:
                     m0 = f"s_add_u32 m0, s{ldsb}, {i * 4096}"
-                    ld = f"buffer_load_dwordx4 v{vd + i}, s[{srd}:{srd + 3}], 0 offen lds"
+                    ld = (f"global_load_lds_dwordx4 v{vd + i}, s[{srd}:{srd + 1}]" if self.GLDS else
+                          f"buffer_load_dwordx4 v{vd + i}, s[{srd}:{srd + 3}], 0 offen lds")
                 else:
                     m0 = f"s_add_u32 m0, s{ldsb}, {i * 1024}"
                     ld = f"buffer_load_dwordx4 v{vd + (i & 1)}, s[{srd}:{srd + 3}], s{soff + i} offen lds"
@@ -527,17 +528,31 @@ class Kernel:
         self.e(f"{self.mfma_op} a[{c}:{c + 3}], v[{b}:{b + 3}], v[{a}:{a + 3}], {src2}")
 
     # Schedule of one K-block (128 MFMAs; slot k = after MFMA k):
-    #   slots 0-21   read Y (k-half 1 of this stage)                    [phase A: MFMAs on X]
+    #   slots 0-15   read Y (k-half 1 of this stage)                    [phase A: MFMAs on X]
     #   slot 24      lgkmcnt(0) + barrier: every wave has this whole block in registers
-    #   slots 26-86  16 LDS-DMAs of block t+2 into THIS stage, one per 4 MFMAs (m0 one slot before)
-    #   slot 92      vmcnt(16) + barrier: block t+1 (issued one iteration earlier) has landed
+    #   slots 26-116 16 LDS-DMAs of block t+2 into THIS stage, one per 6 MFMAs (m0 one slot
+    #                before); those past BAR2 land under the next iteration (the stage they fill is
+    #                read only after the next BAR2)
+    #   slot 92      vmcnt(#DMAs of this iteration issued so far) + barrier: block t+1 has landed
     #   slots 93-114 read X (k-half 0 of the other stage)                [phase B: MFMAs on Y]
     #   end          lgkmcnt(0)
-    # The DMA issue cost (~60 cycles each among MFMAs, MI355X_MICROARCH.md) is spread over 60
+    # The DMA issue cost (~60 cycles each among MFMAs, MI355X_MICROARCH.md) is spread over 90
     # MFMAs instead of being bunched.
-    Y_END, BAR1, DMA0, DMA_GAP, BAR2, X0, X_END = 22, 24, 26, 4, 92, 93, 115
+    # Round 5: DMAs one per 6 MFMAs (26 … 116, past BAR2) instead of one per 4 (26 … 86): each
+    # LDS-DMA issue stalls its wave ~60 cycles, so bunched issues left the MFMA pipe idle; with
+    # the Y reads done by slot 16 the NT GEMMs run 4.5-5.3 % faster (profiles/gemm_sched_r5.txt)
+    Y_END, BAR1, DMA0, DMA_GAP, BAR2, X0, X_END = 16, 24, 26, 6, 92, 93, 115
+    # K-contiguous operands by global_load_lds (saddr form; the descriptor's first two dwords are
+    # the 64-bit base) instead of buffer_load … lds: A/B of the DMA issue cost (every address is
+    # in range by construction; an exhausted stream is rewound onto consumed blocks, never 0)
+    GLDS = os.environ.get("PIAMD_AGEMM_GLDS", "0") == "1"
     if os.environ.get("PIAMD_AGEMM_SCHED"):  # schedule sweeps (tools/agemm_sched_sweep.py)
-        Y_END, BAR1, DMA0, DMA_GAP, BAR2, X0, X_END = map(int, os.environ["PIAMD_AGEMM_SCHED"].split(","))
+        Y_END, BAR1, DMA0, DMA_GAP, BAR2, X0, X_END = (float(v) if "." in v else int(v) for v in
+                                                       os.environ["PIAMD_AGEMM_SCHED"].split(","))
+
+    def dma_slot(self, n):
+        """Slot of the n-th of the 16 DMAs of a K-block (DMA_GAP may be fractional)."""
+        return self.DMA0 + int(self.DMA_GAP * n)
 
     def iteration(self, stage, dma, read_next, first=False, vm_extra=0):
         ysl, dsl, xsl = {}, {}, {}
@@ -546,7 +561,7 @@ class Kernel:
             ysl.setdefault(r * self.Y_END // len(yreads), []).append(op)
         if dma:
             for n, (m0, ld, adv) in enumerate(self.dma_ops(stage)):
-                k = self.DMA0 + self.DMA_GAP * n
+                k = self.dma_slot(n)
                 dsl.setdefault(k - 1, []).append(m0)
                 dsl.setdefault(k, []).append(ld)
                 if adv is not None:
@@ -561,7 +576,10 @@ class Kernel:
                 if dma:
                     self.e("s_barrier")
             if k == self.BAR2 and read_next:
-                self.e(f"s_waitcnt vmcnt({min(63, 16 + vm_extra) if dma else vm_extra})")
+                # every DMA of this iteration issued before BAR2 may still fly (the rest come later):
+                # block t+1 (issued one iteration earlier) is then complete
+                nb = sum(1 for n in range(16) if self.dma_slot(n) < self.BAR2) if dma else 0
+                self.e(f"s_waitcnt vmcnt({min(63, nb + vm_extra)})")
                 self.e("s_barrier")
             kk = k % 64
             self.mfma(k // 64, kk // 8, kk % 8, zero=first and k < 64)
@@ -686,6 +704,11 @@ class Kernel:
         self.e(f"s_mov_b32 s{S_NVALID}, 1")
         self.e(f"s_branch {ready}")
         self.lab(nonext)
+        if self.GLDS:  # global_load_lds has no range check: re-read the last two consumed blocks
+            for op, srd, kc in ((0, S_SRDA, self.a_kc), (1, S_SRDB, self.b_kc)):
+                if kc:
+                    self.e(f"s_sub_u32 s{srd}, s{srd}, {2 * BK * 2}")
+                    self.e(f"s_subb_u32 s{srd + 1}, s{srd + 1}, 0")
         self.e(f"s_mov_b32 s{S_SRDA + 2}, 0")
         self.e(f"s_mov_b32 s{S_SRDB + 2}, 0")
         self.e(f"s_mov_b32 s{S_REMA}, 0")

@@ -1,6 +1,7 @@
-"""Where do a Predictor run's device copies come from? Profiles one BERT-Large fp16 Predictor run
-(no hipGraph) with torch.profiler and prints each aten copy / cast with its shapes and the
-innermost framework frames of its Python stack.
+"""Where do a Predictor run's device copies / casts come from? Runs one BERT-Large fp16 Predictor
+step (no hipGraph) under a TorchDispatchMode that records every aten op that moves data without
+computing (copy_, _to_copy, clone, contiguous copies, cat, …) with its shapes and the innermost
+framework frames of the Python stack.
 
   python tools/trace_copies.py [--batch 128 --layers 24]"""
 import argparse
@@ -8,10 +9,31 @@ import collections
 import os
 import sys
 import tempfile
+import traceback
 
 import torch
+from torch.utils._python_dispatch import TorchDispatchMode
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+MOVERS = ("copy_", "_to_copy", "clone", "cat", "index_select", "index", "expand_copy", "_copy_from",
+          "constant_pad_nd", "fill_", "zero_", "zeros", "new_zeros", "masked_fill", "where")
+
+
+class _Rec(TorchDispatchMode):
+    def __init__(self):
+        super().__init__()
+        self.cnt = collections.Counter()
+
+    def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+        name = func.__name__.split(".")[0]
+        if any(name == m or name.startswith(m) for m in MOVERS):
+            shapes = [tuple(a.shape) + (str(a.dtype).replace("torch.", ""),) for a in args
+                      if isinstance(a, torch.Tensor)][:3]
+            fr = [f for f in traceback.extract_stack() if "paddle_infer_amd" in f.filename][-3:]
+            where = " <- ".join(f"{f.filename.split('paddle_infer_amd/')[-1]}:{f.lineno}" for f in reversed(fr))
+            self.cnt[(name, str(shapes)[:100], where)] += 1
+        return func(*args, **(kwargs or {}))
 
 
 def main():
@@ -36,16 +58,12 @@ def main():
     for _ in range(2):
         p.run()
     torch.cuda.synchronize()
-    from torch.profiler import ProfilerActivity, profile
-    with profile(activities=[ProfilerActivity.CPU], record_shapes=True, with_stack=True) as prof:
+    rec = _Rec()
+    with rec:
         p.run()
-        torch.cuda.synchronize()
-    cnt = collections.Counter()
-    for ev in prof.events():
-        if ev.name in ("aten::copy_", "aten::_to_copy", "aten::contiguous", "aten::clone", "aten::cat"):
-            st = [f for f in (ev.stack or []) if "paddle_infer_amd" in f][:3]
-            cnt[(ev.name, str(ev.input_shapes)[:90], " <- ".join(s.split("paddle_infer_amd/")[-1] for s in st))] += 1
-    for (n, shp, st), k in cnt.most_common(25):
+    torch.cuda.synchronize()
+    print(f"# data-moving aten ops in one run ({a.layers} layers, batch {a.batch}):")
+    for (n, shp, st), k in rec.cnt.most_common(40):
         print(f"{k:4d}  {n:16s} {shp}\n        {st}")
 
 

@@ -215,6 +215,25 @@ class Kernel:
                 return
             if "nomfma" in ABL and m.startswith("v_mfma"):
                 s = "s_nop 0"
+            if ("vload" in ABL or "dsw" in ABL) and m == "buffer_load_dwordx4" and s.endswith(" lds"):
+                # register-staged operand path priced without its latency: a plain VMEM load into
+                # scratch VGPRs (vload) and/or a ds_write_b128 of a fixed register (dsw)
+                i = int(s.split()[1].strip("v,")) % 8
+                if "vload" in ABL:
+                    self.lines.append(f"\tbuffer_load_dwordx4 v[{180 + 4 * i}:{183 + 4 * i}], "
+                                      + s.split(" ", 1)[1][:-4])
+                if "dsw" in ABL:  # v220 = lane·16 (set in the prologue): in-range LDS addresses
+                    self.lines.append(f"\tds_write_b128 v220, v[216:219] offset:{i * 4096}")
+                return
+            if "mfma32" in ABL and m.startswith("v_mfma"):
+                # 32x32x16 MFMAs (half the count, twice the length) at the same slots
+                self.nmf = getattr(self, "nmf", 0) + 1
+                if self.nmf % 2 == 0:
+                    return
+                ops = s.split(" ", 1)[1].split(", ")
+                c = 16 * ((self.nmf // 2) % 16)
+                s = f"v_mfma_f32_32x32x16_bf16 a[{c}:{c + 15}], {ops[1]}, {ops[2]}, " + (
+                    "0" if ops[3] == "0" else f"a[{c}:{c + 15}]")
         self.lines.append("\t" + s)
 
     def lab(self, s):
@@ -273,6 +292,8 @@ class Kernel:
         self.e(f"s_load_dwordx4 s[{S_E + 8}:{S_E + 11}], s[0:1], 0x80")  # aux, aux_bytes
         self.e(f"s_load_dwordx2 s[{S_E + 12}:{S_E + 13}], s[0:1], 0x90")  # bias
         self.e(f"v_and_b32 v{V_LANE}, 63, v{V_TID}")
+        if "dsw" in ABL:
+            self.e(f"v_lshlrev_b32 v220, 4, v{V_LANE}")
         self.e(f"v_lshrrev_b32 v{V_T}, 6, v{V_TID}")
         self.e("s_nop 1")
         self.e(f"v_readfirstlane_b32 s{S_WAVE}, v{V_T}")

@@ -211,7 +211,7 @@ PIAMD_EXPORT int piamd_agemm(const void* a, long long lda, int trans_a, const vo
   size_t sz = sizeof(g);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &g, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz,
                  HIP_LAUNCH_PARAM_END};
-  hipError_t err = hipModuleLaunchKernel(f, g.grid, 1, 1, pp ? 512 : 256, 1, 1, 0, st, nullptr, cfg);
+  hipError_t err = hipModuleLaunchKernel(f, g.grid, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
   if (err != hipSuccess || ksplit == 1) return (int)err;
   const long long q = (long long)M * N / 4;
   const int grid = (int)std::min<long long>(2048, (q + 255) / 256);

@@ -69,12 +69,16 @@ class RNNCellBase(Layer):
         return self._dtype
 
     # cells with a linear input projection run it once over the whole sequence (see RNN)
+    # projections on the framework GEMM dispatcher (own 16-bit kernels, split-bf16 fp32 on GPU,
+    # forward and backward; torch on CPU)
     def _input_proj(self, x):
-        y = torch.matmul(x, self.weight_ih.t())
+        from ...ops.gemm import matmul
+        y = matmul(x, self.weight_ih, False, True)
         return y + self.bias_ih if self.bias_ih is not None else y
 
     def _hidden_proj(self, h):
-        y = torch.matmul(h, self.weight_hh.t())
+        from ...ops.gemm import matmul
+        y = matmul(h, self.weight_hh, False, True)
         return y + self.bias_hh if self.bias_hh is not None else y
 
     def forward(self, inputs, states=None):

@@ -336,16 +336,34 @@ def _ceil(x, m):
     return -(-x // m) * m
 
 
-def _kc(t, Kp, rows=None):
-    """[R, K] operand → K-contiguous, 16-B aligned, K zero-padded to Kp (and rows to ``rows``)."""
+def _is_weight(t):
+    """Parameters and the framework's cached weight copies (``linear.transposed``): their padded
+    operand images may be cached across calls."""
+    return isinstance(t, torch.nn.Parameter) or getattr(t, "_piamd_weight", False)
+
+
+def _kc(t, Kp, rows=None, cache=False):
+    """[R, K] operand → K-contiguous, 16-B aligned, K zero-padded to Kp (and rows to ``rows``).
+    ``cache``: a weight's padded image is kept on the tensor, keyed by its version and the
+    parameter epoch (optimizer writes), so an off-grid inference weight is padded once, not per
+    call."""
     R, K = t.shape
     R2 = rows or R
     if Kp == K and R2 == R and t.stride(-1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0 \
             and t.stride(0) < (1 << 22) and (R == 1 or t.stride(0) >= K):
         return t
+    key = None
+    if cache and _is_weight(t):
+        from .linear import _PARAM_EPOCH
+        key = (_PARAM_EPOCH[0], t._version, t.data_ptr(), Kp, R2)
+        c = getattr(t, "_piamd_pad", None)
+        if c is not None and c[0] == key:
+            return c[1]
     o = torch.zeros((R2, Kp), dtype=t.dtype, device=t.device) if (Kp != K or R2 != R) else \
         torch.empty((R2, Kp), dtype=t.dtype, device=t.device)
-    o[:R, :K].copy_(t)
+    o[:R, :K].copy_(t.detach())
+    if key is not None:
+        t._piamd_pad = (key, o)
     return o
 
 
@@ -378,7 +396,7 @@ def gemm_nt(a, b, alpha=1.0, bias=None, act="none", resid=None, out_f32=False):
     Kp = max(64 if small else 128, _ceil(K, 64))
     Np = _ceil(N, 4) if small else (N if N % 4 == 0 else _ceil(N, 8))
     a2 = _kc(a, Kp)
-    b2 = _kc(b, Kp, Np)
+    b2 = _kc(b, Kp, Np, cache=True)
     if bias is not None:
         bias = bias.to(half).reshape(-1)
         if Np != N:

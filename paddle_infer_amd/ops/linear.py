@@ -122,6 +122,8 @@ def transposed(w):
         return c[1]
     R, C = w.shape
     buf = c[1] if c is not None else torch.empty((C, R), dtype=w.dtype, device=w.device)
+    buf._piamd_weight = True            # ops.gemm may cache a padded image of it ...
+    buf.__dict__.pop("_piamd_pad", None)  # ... which this rewrite (no version bump) invalidates
     if R % 8 == 0 and C % 8 == 0:
         from . import _lib
         _lib.call("piamd_transpose_bf16", w.data_ptr(), buf.data_ptr(), R, C, _lib.stream())

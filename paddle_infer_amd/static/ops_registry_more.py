@@ -144,12 +144,10 @@ def _resnet_unit(ins, a):
 
 
 # ------------------------------------------------------------------------------- rnn
-def _rnn_cell(mode, x_t, h, c, w_ih, w_hh, b_ih, b_hh):
+def _rnn_cell(mode, gx, h, c, w_hh, b_hh):
+    """One step from the precomputed input projection gx = x_t·W_ihᵀ + b_ih."""
     from ..ops.gemm import matmul
-    gx = matmul(x_t, w_ih, False, True)
     gh = matmul(h, w_hh, False, True)
-    if b_ih is not None:
-        gx = gx + b_ih
     if b_hh is not None:
         gh = gh + b_hh
     if mode == "GRU":  # reset gate applied after the hidden projection (reference GRUCell)
@@ -188,6 +186,7 @@ def _rnn(ins, a):
     p_drop = float(a.get("dropout_prob", 0.0) or 0.0)
     train = _training(a)
     bi = torch.arange(B, device=x.device)
+    from ..ops.gemm import matmul
     inp = x
     hN, cN = [], []
     for layer in range(L):
@@ -197,19 +196,25 @@ def _rnn(ins, a):
             w_ih, w_hh = ws[2 * k], ws[2 * k + 1]
             b_ih, b_hh = (ws[nw + 2 * k], ws[nw + 2 * k + 1]) if has_b else (None, None)
             h, c = h0[k], (c0[k] if c0 is not None else None)
+            # the input projection of every step as ONE GEMM ([T·B, I]·W_ihᵀ); only the hidden
+            # projection stays inside the time loop
+            gx_all = matmul(inp.reshape(T * B, -1), w_ih, False, True).view(T, B, -1)
+            if b_ih is not None:
+                gx_all = gx_all + b_ih
             y = x.new_zeros(T, B, Hs)
             for s_ in range(T):
                 # forward: position s_; reverse: each sequence walked back from its own last step
                 src = torch.full_like(lens, s_) if d == 0 else lens - 1 - s_
                 m = (src >= 0) & (src < lens)
-                xt = inp[src.clamp(0, T - 1), bi]
-                hn, cn = _rnn_cell(mode, xt, h, c, w_ih, w_hh, b_ih, b_hh)
+                srcc = src.clamp(0, T - 1)
+                hn, cn = _rnn_cell(mode, gx_all[srcc, bi], h, c, w_hh, b_hh)
                 mk = m[:, None]
                 h = torch.where(mk, hn, h)
                 if c is not None:
                     c = torch.where(mk, cn, c)
-                if bool(m.any()):
-                    y[src[m], bi[m]] = hn[m].to(y.dtype)
+                # masked write without a host sync: inactive rows write back their current value
+                # ((srcc, b) pairs are distinct within a step; a later real write overrides)
+                y.index_put_((srcc, bi), torch.where(mk, hn.to(y.dtype), y[srcc, bi]))
             outs.append(y)
             hN.append(h)
             if c is not None:

@@ -139,6 +139,16 @@ def batch_norm_act(x, running_mean, running_var, weight=None, bias=None, trainin
     """``act(batch_norm(x) + residual)`` (Paddle momentum convention)."""
     a = _ACT[act]
     nhwc, N, C, S = _layout(x, data_format)
+    if (nhwc and x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and x.dim() >= 3
+            and not _supported(x, nhwc, C)
+            and (residual is None or residual.shape == x.shape)):
+        # channel counts the NHWC kernels do not tile (C ∤ 256, C % 8, C < 256): the NCHW kernels
+        # take any C — run them on channel-major copies (own kernels, autograd through the moves)
+        cl = x.dim() == 4 and not x.is_contiguous() and data_format not in ("NHWC", "NLC", "NDHWC")
+        to_cm = (lambda t: t.contiguous()) if cl else (lambda t: t.movedim(-1, 1).contiguous())
+        y = batch_norm_act(to_cm(x), running_mean, running_var, weight, bias, training, momentum,
+                           epsilon, act, to_cm(residual) if residual is not None else None, "NCHW")
+        return y.contiguous(memory_format=torch.channels_last) if cl else y.movedim(1, -1).contiguous()
     if not _supported(x, nhwc, C) or (residual is not None and residual.shape != x.shape):
         return _reference(x, running_mean, running_var, weight, bias, training, momentum, epsilon,
                           a, residual, data_format)

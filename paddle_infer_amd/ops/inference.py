@@ -204,8 +204,10 @@ def _ln_ref(x2, ln):
 def ln_fusable(M, K, KS=1):
     """Whether :func:`packed_linear` / :func:`weight_only_linear` can take ``ln=`` (the LayerNorm
     computed in the GEMV prologue): one K split, M ≤ 8 rows, K % 512 == 0, K ≤ 2048 (beyond that
-    the per-workgroup prologue costs more than the LayerNorm launch it replaces)."""
+    the per-workgroup prologue costs more than the LayerNorm launch it replaces:
+    profiles/decode_gemv_rows_r5.txt)."""
     return KS == 1 and K % 512 == 0 and K <= 2048 and 1 <= M <= 8
+
 
 
 def _wo_call(bits, x2, w, scale, bias, y, M, N, K, KS, act, ln, resid, ws, cnt):
@@ -260,7 +262,7 @@ def _split_k(tiles, kb):
     return KS
 
 
-FIXUP_MAX_M = 8  # split-K reduction: in-kernel atomic fixup up to this M, slices + finalize above
+FIXUP_MAX_M = int(os.environ.get("PIAMD_WO_FIXUP_MAX_M", "8"))  # split-K reduction: in-kernel atomic fixup up to this M, slices + finalize above
 
 
 def _splitk_bufs(device, KS, M, N, tiles):

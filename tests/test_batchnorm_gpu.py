@@ -29,8 +29,8 @@ def _ref(x, rm, rv, w, b, training, act, res):
                                         (36, True)])
 def test_bn_act(layout, dtype, training, C, residual):
     from paddle_infer_amd.ops.batchnorm import batch_norm_act
-    if layout == "nhwc" and C % 8 and C < 256 and 256 % C:
-        pytest.skip("NHWC kernel needs C % 8 == 0, C | 256 or C >= 256")
+    # NHWC / channels_last with C ∤ 256, C % 8 != 0, C < 256 (C = 36) runs the NCHW kernels on
+    # channel-major copies: same parity bar
     torch.manual_seed(C)
     N, H, W = 4, 9, 7
     x = (torch.randn(N, C, H, W, device=DEV) * 2 + 0.5).to(dtype)

@@ -142,7 +142,7 @@ def test_weight_only_linear(bits, M, N, K):
     _close(dq, I.weight_dequantize(q.cpu(), s.cpu(), algo, "float32"), 1e-3, 1e-2)
 
 
-@pytest.mark.parametrize("M", [1, 5, 64])
+@pytest.mark.parametrize("M", [1, 5, 32, 64, 100])
 @pytest.mark.parametrize("K,N", [(2048, 6144), (8192, 2048), (256, 96)])
 def test_packed_bf16_linear(M, K, N):
     from paddle_infer_amd.ops import inference as I
@@ -292,7 +292,7 @@ def test_linear_bias_act_epilogue(act):
 
 
 @pytest.mark.parametrize("bits", [16, 8, 4])
-@pytest.mark.parametrize("M", [1, 5, 8, 40])
+@pytest.mark.parametrize("M", [1, 5, 8, 32, 40, 70])
 @pytest.mark.parametrize("K,N", [(2048, 6144), (256, 96), (8192, 2048)])
 def test_gemv_ln_prologue_resid_epilogue(bits, M, K, N):
     """Decode GEMV with the pre-LayerNorm in its prologue and the residual add in its epilogue

@@ -30,10 +30,15 @@ def timeit(fn, it=200):
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--M", type=int, nargs="+", default=[1, 8])
+    ap.add_argument("--ks", type=int, nargs="+", default=[1, 2, 4, 8, 16, 32])
+    a = ap.parse_args()
     shapes = [(2048, 6144), (2048, 2048), (2048, 8192), (8192, 2048)]
     orig = I._split_k
     rows = []
-    for M in (1, 8):
+    for M in a.M:
         for K, N in shapes:
             w = (torch.randn(K, N, device="cuda") * 0.02).bfloat16()
             # rotate over enough copies (> 256 MB MALL) that every call streams from HBM
@@ -41,7 +46,7 @@ def main():
             wps = [I.pack_bf16(w) for _ in range(R)]
             it = iter(range(10 ** 9))
             x = torch.randn(M, K, device="cuda").bfloat16()
-            for KS in (1, 2, 4, 8, 16, 32):
+            for KS in a.ks:
                 if (K // 16) % KS:
                     continue
                 I._split_k = lambda tiles, kb, KS=KS: KS

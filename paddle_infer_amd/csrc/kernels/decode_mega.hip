@@ -27,8 +27,11 @@
 //     softmax) → partial combine + out GEMV + bias + residual → LN2 + FFN1 GEMV + bias + GELU →
 //     FFN2 GEMV + bias + residual. Rounding points match the launch-per-op path (bf16 LN output,
 //     bf16 cache / attention output / hidden / residual).
-// Shapes: E = 2048, D = 128, Hq = Hk = 16, F = 8192 (GPT-1.3B width; any depth / context);
-// the host launcher rejects anything else and the Python side falls back to the per-op path.
+// Shapes: decode_mega_kernel<MegaCfg<E, D, Hq, Hk, F, ROT>> — the instantiated widths are
+// listed at mega_fn (GPT-3 1.3B and 350M widths, a GQA 4:1 variant, each with and without rotary
+// embedding over the whole head); the dedicated-loader variant (decode_mega_lw_kernel) is the
+// GPT-1.3B shape only. Anything else: the host launcher refuses and the Python side takes the
+// per-op path.
 // Reference parity: one decode step of FusedMultiTransformer with time_step
 // (`paddle/fluid/operators/fused/fused_multi_transformer_op.cu`, masked_multihead_attention).
 #include "common.h"
@@ -80,6 +83,9 @@ struct MegaArgs {
                         // GEMV done, barrier arrival
   int late_dma;         // 1: the FFN phases issue the next slice only after their GEMV (A/B knob)
   int loader;           // 1: decode_mega_lw_kernel (dedicated loader wave, 16 KiB chunk ring)
+  int rot;              // rotary dims: 0 or D (whole head)
+  int neox;             // 1: rotate-half (NeoX), 0: interleaved pairs (GPT-J)
+  float log2_base;      // log2 of the rotary base
 };
 
 __device__ __forceinline__ u64 ld64(const void* p) { return *reinterpret_cast<const u64*>(p); }
@@ -159,13 +165,22 @@ __device__ __forceinline__ void prefetch(const bf16_t* src, int from, int to, ch
                                      (__attribute__((address_space(3))) void*)(wl + p * 1024), 16, 0, 0);
 }
 
-// Phase entry: loader waves wait for their DMA (all of it, all but the newest 32
-// wave-instructions = the FFN1 head, or none), then the whole workgroup meets (wave 0 arrives here after its
-// grid barrier).
+// s_waitcnt vmcnt(N) only (expcnt / lgkmcnt left at their no-wait maxima; gfx9 encoding: vmcnt
+// in bits [3:0] and [15:14])
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+// Phase entry: loader waves wait for their DMA (all of it, all but the newest OLD
+// wave-instructions = the FFN1 head, or none), then the whole workgroup meets (wave 0 arrives here
+// after its grid barrier).
 enum { WAIT_ALL, WAIT_OLDER, WAIT_NONE };
+template <int OLD>
 __device__ __forceinline__ void phase_start(const MegaArgs& a, int wv, unsigned ph, int wait = WAIT_ALL) {
-  if (wv != 0 && wait == WAIT_ALL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (wv != 0 && wait == WAIT_OLDER) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+  if (wv != 0 && wait == WAIT_ALL) wait_vm<0>();
+  if (wv != 0 && wait == WAIT_OLDER) wait_vm<OLD>();
   __syncthreads();
   if (a.trace && threadIdx.x == 0) a.trace[((long)blockIdx.x * a.nl * 5 + ph) * 4] = wall_clock64();
 }
@@ -186,18 +201,20 @@ __device__ __forceinline__ void butterfly(float* acc, int lane) {
 }
 
 // y[c] = Σ_k x[k]·W[c][k] for the NPW columns of this workgroup's LDS slice `ws` ([NPW][K] bf16);
-// thread t holds x[k] for k = (j·256 + t)·8 + i. Returns column `tid`'s sum for tid < NPW.
+// thread t holds x[k] for k = (j·256 + t)·8 + i (threads past K hold nothing: K = 1024 leaves
+// waves 2-3 out of the dot products). Returns column `tid`'s sum for tid < NPW.
 // Reduction: a butterfly that halves the live columns per exchange (log2 P steps, P−1 shuffles
 // instead of 6·P), then 4 waves through LDS.
 // `mid()` runs once every wave has consumed the first half of the columns (slice bytes
 // [0, SLICE/2) are free), `end()` once the whole slice is consumed: the loader waves issue the
 // next slices' DMA there.
-template <int NPW, int KCH, class Mid, class End>
-__device__ __forceinline__ float gemv_lds(const char* ws, const float (&x)[KCH][8], float* red, int tid,
-                                          Mid mid, End end) {
-  constexpr int K = 2048 * KCH;
+template <int NPW, int K, class Mid, class End>
+__device__ __forceinline__ float gemv_lds(const char* ws, const float (&x)[(K + 2047) / 2048][8], float* red,
+                                          int tid, Mid mid, End end) {
+  constexpr int KCH = (K + 2047) / 2048;
   constexpr int P = NPW <= 8 ? 8 : 32;
   constexpr int LOGP = P == 8 ? 3 : 5;
+  static_assert(NPW <= 32 && K % 1024 == 0, "gemv_lds shape");
   const int lane = tid & 63, wv = tid >> 6;
   float acc[P];
 #pragma unroll
@@ -207,6 +224,7 @@ __device__ __forceinline__ float gemv_lds(const char* ws, const float (&x)[KCH][
     for (int c = decltype(c0)::value; c < decltype(c1)::value; ++c) {
 #pragma unroll
       for (int j = 0; j < KCH; ++j) {
+        if (K % 2048 != 0 && (j * 256 + tid) * 8 >= K) continue;  // wave-uniform
         const u16x8 w = *reinterpret_cast<const u16x8*>(ws + ((long)c * K + (j * 256 + tid) * 8) * 2);
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc[c] += x[j][i] * bf2f(w[i]);
@@ -228,25 +246,33 @@ __device__ __forceinline__ float gemv_lds(const char* ws, const float (&x)[KCH][
   return r;
 }
 
-// x = bf16(LN(resid)) for this thread's 8 elements k = 8·tid.
+// x = bf16(LN(resid)) for this thread's 8 elements k = 8·tid (threads with 8·tid ≥ EE hold 0).
+template <int EE>
 __device__ __forceinline__ void ln_prologue(const MegaArgs& a, const bf16_t* r, const bf16_t* g,
                                             const bf16_t* b, float (&x)[1][8], float* wred, int tid) {
+  const bool on = tid * 8 < EE;
   // gamma / beta first: their latency then hides under the residual load and the reductions
   // (a load is not hoisted across the __syncthreads of block_sum)
-  const u16x8 gg = *reinterpret_cast<const u16x8*>(g + tid * 8);
-  const u16x8 bb = *reinterpret_cast<const u16x8*>(b + tid * 8);
+  u16x8 gg{}, bb{};
   float v[8];
-  ld_bf8(r + tid * 8, v);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = 0.f;
+  if (on) {
+    gg = *reinterpret_cast<const u16x8*>(g + tid * 8);
+    bb = *reinterpret_cast<const u16x8*>(b + tid * 8);
+    ld_bf8(r + tid * 8, v);
+  }
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < 8; ++i) s += v[i];
-  const float mean = block_sum<4>(s, wred) * (1.f / E);
+  const float mean = block_sum<4>(s, wred) * (1.f / EE);
   float q = 0.f;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) q += (v[i] - mean) * (v[i] - mean);
-  const float rs = rsqrtf(block_sum<4>(q, wred) * (1.f / E) + a.eps);
+  for (int i = 0; i < 8; ++i) q += on ? (v[i] - mean) * (v[i] - mean) : 0.f;
+  const float rs = rsqrtf(block_sum<4>(q, wred) * (1.f / EE) + a.eps);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) x[0][i] = bf2f(f2bf((v[i] - mean) * rs * bf2f(gg[i]) + bf2f(bb[i])));
+  for (int i = 0; i < 8; ++i)
+    x[0][i] = on ? bf2f(f2bf((v[i] - mean) * rs * bf2f(gg[i]) + bf2f(bb[i]))) : 0.f;
 }
 
 // Lanes 0..NC-1 of wave 0 each hold one bf16 `y`; publish them as NC/4 64-bit stores at dst.
@@ -258,20 +284,56 @@ __device__ __forceinline__ void publish_bf16(bf16_t* dst, float y, int lane, int
   if (lane < NC && (lane & 3) == 0) st64(dst + lane, (u64)pair | ((u64)pair2 << 32));
 }
 
+// Model shape of the single-launch step. E / D / HQ / HK / F: hidden width, head dim, query and
+// key/value heads (GQA when HK < HQ), FFN width; ROT: rotary embedding over the whole head dim
+// (NeoX rotate-half or GPT-J interleaved per MegaArgs.neox, angles pos·base^(−2f/D)) applied to q
+// and the new k. Every projection splits its output columns evenly over the 256 workgroups and
+// each workgroup's weight slice must fit the 128 KiB LDS image.
+template <int E_, int D_, int HQ_, int HK_, int F_, int ROT_>
+struct MegaCfg {
+  static constexpr int E = E_, D = D_, HQ = HQ_, HK = HK_, F = F_, ROT = ROT_;
+  static constexpr int NQKV = (HQ + 2 * HK) * D;
+  static constexpr int NPQ = NQKV / NWG, NPO = E / NWG, NP1 = F / NWG, NP2 = E / NWG;
+  // slice bytes: QKV [0, QB) → out [QB, QB + OB) (free during QKV) → FFN1 [0, F1B), whose first
+  // F1PRE bytes stream in during the attention phase (workgroups without attention work) or the
+  // out-projection prologue (the others) and the rest once the out slice is consumed → FFN2
+  // [0, F2B) → next QKV [0, QB)
+  static constexpr int QB = NPQ * E * 2, OB = NPO * E * 2, F1B = NP1 * E * 2, F2B = NP2 * F * 2;
+  static constexpr int OUT_OFF = QB;
+  static constexpr int F1PRE = QB < F1B ? QB : F1B;
+  // the out phase of a non-attention workgroup waits for every DMA older than its FFN1 head: the
+  // newest F1PRE/1 KiB/3 wave-instructions per loader wave (floor: the minimum over the waves)
+  static constexpr int WAIT_OLD = F1PRE / 1024 / 3;
+  static constexpr int LPR = D / 8;  // lanes per head row (16 B each)
+  static_assert(NQKV % NWG == 0 && E % NWG == 0 && F % NWG == 0, "columns split evenly over the grid");
+  static_assert(QB + OB <= WBYTES && F1B <= WBYTES && F2B <= WBYTES, "slices fit the LDS image");
+  static_assert(QB % 1024 == 0 && OB % 1024 == 0 && F1B % 1024 == 0 && F2B % 1024 == 0, "1 KiB pieces");
+  static_assert(HQ * D == E && HQ % HK == 0 && E % 1024 == 0 && E <= 2048 && F % 2048 == 0, "widths");
+  static_assert(D == 64 || D == 128, "head dim");
+  static_assert(NPQ <= 32 && NP1 <= 32 && (NPO & (NPO - 1)) == 0 && (NP1 & (NP1 - 1)) == 0 &&
+                NPO >= 4 && NP1 >= 4, "per-workgroup column counts");
+};
+
+__host__ __device__ constexpr long pstride_hd(int hq, int d, int nsplit) {
+  return ((long)hq * nsplit * (d + 2) + 63) / 64 * 64;
+}
+
+template <class C>
 __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
+  constexpr int E = C::E, D = C::D, HQ = C::HQ, HK = C::HK, F = C::F, LPR = C::LPR;
+  constexpr int NPQ = C::NPQ, NPO = C::NPO, NP1 = C::NP1, NP2 = C::NP2;
+  constexpr int PSTR = D + 2;
   __shared__ __attribute__((aligned(1024))) char wl[WBYTES];
   __shared__ float red[4 * 32];
   __shared__ float wred[8];
   __shared__ float sc[256];
   __shared__ float pv[4][D];
-  __shared__ float qs[D];
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, w = blockIdx.x;
   const int pos = a.pos[0], L = pos + 1;
   unsigned nbar = 0;
-  constexpr int NPQ = NQKV / NWG, NPO = E / NWG, NP1 = F / NWG, NP2 = E / NWG;
 
-  prefetch(a.layers[0].wqkv + (long)w * NPQ * E, 0, NPQ * E * 2, wl, wv, lane);
+  prefetch(a.layers[0].wqkv + (long)w * NPQ * E, 0, C::QB, wl, wv, lane);
   for (int l = 0; l < a.nl; ++l) {
     const MegaLayer& Ly = a.layers[l];
     // this layer's buffer slots: every published vector has its own address per launch, so a
@@ -281,21 +343,20 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
     bf16_t* rout = a.rbuf + (long)(2 * l + 1) * E;
     float* qn = a.qn + (long)l * HQ * D;
     float* kvn = a.kvn + (long)l * 2 * HK * D;
-    float* part = a.part + (long)l * pstride(a.nsplit);
+    float* part = a.part + (long)l * pstride_hd(HQ, D, a.nsplit);
     bf16_t* hb = a.h + (long)l * F;
     // ---------------------------------------------------------------- QKV
-    phase_start(a, wv, nbar);
+    phase_start<C::WAIT_OLD>(a, wv, nbar);
     {
       // epilogue operands requested first: their latency hides under the prologue and GEMV
       const float bq = lane < NPQ ? bf2f(Ly.bqkv[w * NPQ + lane]) : 0.f;
       float x[1][8];
-      ln_prologue(a, rin, Ly.ln1_g, Ly.ln1_b, x, wred, tid);
+      ln_prologue<E>(a, rin, Ly.ln1_g, Ly.ln1_b, x, wred, tid);
       tmark(a, nbar, 1);
       // out slice into the region QKV does not use, behind this GEMV
-      const float y = gemv_lds<NPQ, 1>(wl, x, red, tid, [] {}, [&] {
-        prefetch(Ly.wo + (long)w * NPO * E, 0, NPO * E * 2, wl + OUT_OFF, wv, lane);
+      const float y = gemv_lds<NPQ, E>(wl, x, red, tid, [] {}, [&] {
+        prefetch(Ly.wo + (long)w * NPO * E, 0, C::OB, wl + C::OUT_OFF, wv, lane);
       });
-      static_assert(NPQ * E * 2 == OUT_OFF && NPO * E * 2 == WBYTES - OUT_OFF, "LDS placement");
       tmark(a, nbar, 2);
       if (wv == 0) {
         if (lane < NPQ) {
@@ -307,9 +368,13 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
             const int kv = col - HQ * D;          // [0, 2·HK·D)
             const int which = kv / (HK * D), r = kv % (HK * D), kh = r / D, d = r % D;
             const bf16_t vb = f2bf(v);
-            bf16_t* cache = which ? Ly.vc : Ly.kc;
-            cache[((long)kh * a.maxS + pos) * D + d] = vb;
-            __hip_atomic_store(kvn + kv, bf2f(vb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (which || !C::ROT) {  // rotated k is cached by the attention phase (needs all of D)
+              bf16_t* cache = which ? Ly.vc : Ly.kc;
+              cache[((long)kh * a.maxS + pos) * D + d] = vb;
+            }
+            // rotary k stays unrounded until rotated (the per-op path rounds after the rotation)
+            __hip_atomic_store(kvn + kv, (C::ROT && !which) ? v : bf2f(vb), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
           }
         }
         grid_sync(a, ++nbar, lane);
@@ -319,25 +384,72 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
     }
     // ---------------------------------------------------------------- attention
     // (attention reads no weights: the out slice keeps streaming)
-    phase_start(a, wv, nbar, WAIT_NONE);
+    phase_start<C::WAIT_OLD>(a, wv, nbar, WAIT_NONE);
     const bf16_t* w1s = Ly.w1 + (long)w * NP1 * E;
     if (w < HQ * a.nsplit) {
       const int h = w / a.nsplit, s = w % a.nsplit, kh = h / (HQ / HK);
       const int chunk = (L + a.nsplit - 1) / a.nsplit;
       const int j0 = s * chunk, n = min(L, j0 + chunk) - j0;
-      const int sub = tid & 15, kslot = tid >> 4;  // 16 lanes per key row, 16 rows in flight
+      constexpr int RIF = NT / LPR;                    // key rows in flight per workgroup
+      const int sub = tid % LPR, kslot = tid / LPR;    // LPR lanes per key row
       const long kvbase = (long)kh * a.maxS * D;
-      float q[8];
+      float rc[8], rsn[8];
+      if (C::ROT) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) q[i] = ldf(qn + h * D + sub * 8 + i) * a.scale_log2;
+        for (int j = 0; j < 8; ++j) {
+          const int i = sub * 8 + j;
+          const int f = a.neox ? (i % (D / 2)) : (i >> 1);
+          sincosf((float)pos * exp2f(-(2.f * f / (float)D) * a.log2_base), &rsn[j], &rc[j]);
+        }
+      }
+      // same rotation as decode_attn_kernel (infer.hip): partner element from lane sub ^ LPR/2
+      // (rotate-half) or the neighbouring element (interleaved)
+      auto rotate = [&](float* v) {
+        float pr[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (a.neox) {
+            pr[j] = __shfl_xor(v[j], LPR / 2, 64) * (sub < LPR / 2 ? -1.f : 1.f);
+          } else {
+            pr[j] = (j & 1) ? v[j - 1] : -v[j + 1];
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = v[j] * rc[j] + pr[j] * rsn[j];
+      };
+      float q[8], kn[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        q[i] = ldf(qn + h * D + sub * 8 + i);
+        kn[i] = ldf(kvn + kh * D + sub * 8 + i);
+      }
+      if (C::ROT) {
+        rotate(q);
+        rotate(kn);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) kn[i] = bf2f(f2bf(kn[i]));
+        if (h % (HQ / HK) == 0 && s == 0 && kslot == 0) {  // one writer per kv head
+          u16x8 ko;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) ko[i] = f2bf(kn[i]);
+          *reinterpret_cast<u16x8*>(Ly.kc + kvbase + (long)pos * D + sub * 8) = ko;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) q[i] *= a.scale_log2;
       auto row = [&](const bf16_t* cache, int which, int j, float* r) {
         if (j == pos) {
-          const float* p = kvn + which * HK * D + kh * D + sub * 8;
+          if (which == 0) {
 #pragma unroll
-          for (int i = 0; i < 8; i += 2) {
-            const u64 u = ld64(p + i);
-            r[i] = __uint_as_float((unsigned)u);
-            r[i + 1] = __uint_as_float((unsigned)(u >> 32));
+            for (int i = 0; i < 8; ++i) r[i] = kn[i];
+          } else {
+            const float* p = kvn + HK * D + kh * D + sub * 8;
+#pragma unroll
+            for (int i = 0; i < 8; i += 2) {
+              const u64 u = ld64(p + i);
+              r[i] = __uint_as_float((unsigned)u);
+              r[i + 1] = __uint_as_float((unsigned)(u >> 32));
+            }
           }
         } else {
           const u16x8 u = *reinterpret_cast<const u16x8*>(cache + kvbase + (long)j * D + sub * 8);
@@ -345,14 +457,14 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
           for (int i = 0; i < 8; ++i) r[i] = bf2f(u[i]);
         }
       };
-      for (int i = kslot; i < n; i += 16) {
+      for (int i = kslot; i < n; i += RIF) {
         float k[8];
         row(Ly.kc, 0, j0 + i, k);
         float d = 0.f;
 #pragma unroll
         for (int t = 0; t < 8; ++t) d += q[t] * k[t];
 #pragma unroll
-        for (int o = 8; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+        for (int o = LPR / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
         if (sub == 0) sc[i] = d;
       }
       __syncthreads();
@@ -365,7 +477,7 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
       float acc[8];
 #pragma unroll
       for (int t = 0; t < 8; ++t) acc[t] = 0.f;
-      for (int i = kslot; i < n; i += 16) {
+      for (int i = kslot; i < n; i += RIF) {
         float v[8];
         row(Ly.vc, 1, j0 + i, v);
         const float pi = sc[i];
@@ -374,24 +486,26 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
       }
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
-        acc[t] += __shfl_xor(acc[t], 16, 64);
-        acc[t] += __shfl_xor(acc[t], 32, 64);
+#pragma unroll
+        for (int o = LPR; o < 64; o <<= 1) acc[t] += __shfl_xor(acc[t], o, 64);
       }
-      if (lane < 16) {
+      if (lane < LPR) {
 #pragma unroll
         for (int t = 0; t < 8; ++t) pv[wv][sub * 8 + t] = acc[t];
       }
       __syncthreads();
       if (wv == 0) {
-        float* dst = part + (long)(h * a.nsplit + s) * PSTRIDE;
+        float* dst = part + (long)(h * a.nsplit + s) * PSTR;
         const int d0 = lane * 2;
-        const float v0 = pv[0][d0] + pv[1][d0] + pv[2][d0] + pv[3][d0];
-        const float v1 = pv[0][d0 + 1] + pv[1][d0 + 1] + pv[2][d0 + 1] + pv[3][d0 + 1];
-        st64(dst + d0, pack2f(n > 0 ? v0 : 0.f, n > 0 ? v1 : 0.f));
+        if (d0 < D) {
+          const float v0 = pv[0][d0] + pv[1][d0] + pv[2][d0] + pv[3][d0];
+          const float v1 = pv[0][d0 + 1] + pv[1][d0 + 1] + pv[2][d0 + 1] + pv[3][d0 + 1];
+          st64(dst + d0, pack2f(n > 0 ? v0 : 0.f, n > 0 ? v1 : 0.f));
+        }
         if (lane == 0) st64(dst + D, pack2f(n > 0 ? m : -INFINITY, n > 0 ? lsum : 0.f));
       }
     } else {
-      prefetch(w1s, 0, FFN1_PRE, wl, wv, lane);
+      prefetch(w1s, 0, C::F1PRE, wl, wv, lane);
     }
     if (wv == 0) grid_sync(a, ++nbar, lane); else ++nbar;
     // ---------------------------------------------------------------- out projection
@@ -399,14 +513,15 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
     // every older load has to land; the others issued it at the attention phase start and wait
     // for the out slice only
     const bool attn_wg = w < HQ * a.nsplit;
-    phase_start(a, wv, nbar, attn_wg ? WAIT_ALL : WAIT_OLDER);
+    phase_start<C::WAIT_OLD>(a, wv, nbar, attn_wg ? WAIT_ALL : WAIT_OLDER);
     {
       const int ocol = w * NPO + (lane & (NPO - 1));
       const float bo = bf2f(Ly.bo[ocol]), ro = bf2f(rin[ocol]);
       float x[1][8];
       {
-        const int h = tid >> 4, d0 = (tid & 15) * 8;
-        const float* base = part + (long)h * a.nsplit * PSTRIDE;
+        const int h = tid / LPR, d0 = (tid % LPR) * 8;  // thread t holds elements 8t … 8t+7
+        const bool on = h < HQ;
+        const float* base = part + (long)min(h, HQ - 1) * a.nsplit * PSTR;
         // online combine, eight splits' partials requested at once (no load waits on another)
         float M = -INFINITY, lt = 0.f, o[8];
 #pragma unroll
@@ -415,7 +530,7 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
           u64 ml[8], ov[8][4];
 #pragma unroll
           for (int t = 0; t < 8; ++t) {
-            const float* ps = base + min(s0 + t, a.nsplit - 1) * PSTRIDE;
+            const float* ps = base + min(s0 + t, a.nsplit - 1) * PSTR;
             ml[t] = ld64(ps + D);
 #pragma unroll
             for (int i = 0; i < 4; ++i) ov[t][i] = ld64(ps + d0 + 2 * i);
@@ -436,12 +551,12 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
         }
         const float inv = 1.f / lt;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) x[0][i] = bf2f(f2bf(o[i] * inv));
+        for (int i = 0; i < 8; ++i) x[0][i] = on ? bf2f(f2bf(o[i] * inv)) : 0.f;
       }
-      if (attn_wg) prefetch(w1s, 0, FFN1_PRE, wl, wv, lane);
+      if (attn_wg) prefetch(w1s, 0, C::F1PRE, wl, wv, lane);
       tmark(a, nbar, 1);
-      const float y = gemv_lds<NPO, 1>(wl + OUT_OFF, x, red, tid, [] {}, [&] {
-        prefetch(w1s, FFN1_PRE, NP1 * E * 2, wl, wv, lane);
+      const float y = gemv_lds<NPO, E>(wl + C::OUT_OFF, x, red, tid, [] {}, [&] {
+        prefetch(w1s, C::F1PRE, C::F1B, wl, wv, lane);
       });
       tmark(a, nbar, 2);
       if (wv == 0) {
@@ -452,16 +567,17 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
       }
     }
     // ---------------------------------------------------------------- FFN1
-    phase_start(a, wv, nbar);
+    phase_start<C::WAIT_OLD>(a, wv, nbar);
     {
       const float b1 = bf2f(Ly.b1[w * NP1 + (lane & (NP1 - 1))]);
       float x[1][8];
-      ln_prologue(a, rmid, Ly.ln2_g, Ly.ln2_b, x, wred, tid);
+      ln_prologue<E>(a, rmid, Ly.ln2_g, Ly.ln2_b, x, wred, tid);
       tmark(a, nbar, 1);
       const bf16_t* w2s = Ly.w2 + (long)w * NP2 * F;
-      const int mid = a.late_dma ? 0 : WBYTES / 2;
-      const float y = gemv_lds<NP1, 1>(wl, x, red, tid, [&] { prefetch(w2s, 0, mid, wl, wv, lane); },
-                                       [&] { prefetch(w2s, mid, WBYTES, wl, wv, lane); });
+      constexpr int MID1 = C::F1B / 2 < C::F2B ? C::F1B / 2 : C::F2B;
+      const int mid = a.late_dma ? 0 : MID1;
+      const float y = gemv_lds<NP1, E>(wl, x, red, tid, [&] { prefetch(w2s, 0, mid, wl, wv, lane); },
+                                       [&] { prefetch(w2s, mid, C::F2B, wl, wv, lane); });
       tmark(a, nbar, 2);
       if (wv == 0) {
         const float t = y + b1;
@@ -472,18 +588,20 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
       }
     }
     // ---------------------------------------------------------------- FFN2
-    phase_start(a, wv, nbar);
+    phase_start<C::WAIT_OLD>(a, wv, nbar);
     {
       const int fcol = w * NP2 + (lane & (NP2 - 1));
       const float b2 = bf2f(Ly.b2[fcol]), rm = bf2f(rmid[fcol]);
-      float x[4][8];
+      constexpr int KCH2 = F / 2048;
+      float x[KCH2][8];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) ld_bf8(hb + (j * 256 + tid) * 8, x[j]);
+      for (int j = 0; j < KCH2; ++j) ld_bf8(hb + (j * 256 + tid) * 8, x[j]);
       tmark(a, nbar, 1);
       const bf16_t* nq = l + 1 < a.nl ? a.layers[l + 1].wqkv + (long)w * NPQ * E : nullptr;
-      const int mid = a.late_dma ? 0 : WBYTES / 2;
-      const float y = gemv_lds<NP2, 4>(wl, x, red, tid, [&] { prefetch(nq, 0, mid, wl, wv, lane); },
-                                       [&] { prefetch(nq, mid, OUT_OFF, wl, wv, lane); });
+      constexpr int MID2 = C::F2B / 2 < C::QB ? C::F2B / 2 : C::QB;
+      const int mid = a.late_dma ? 0 : MID2;
+      const float y = gemv_lds<NP2, F>(wl, x, red, tid, [&] { prefetch(nq, 0, mid, wl, wv, lane); },
+                                       [&] { prefetch(nq, mid, C::QB, wl, wv, lane); });
       tmark(a, nbar, 2);
       if (wv == 0) {
         publish_bf16(rout + w * NP2, y + b2 + rm, lane, NP2);
@@ -493,7 +611,7 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
       }
     }
   }
-  if (wv != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (wv != 0) wait_vm<0>();
   // the last workgroup out re-zeroes the barrier words for the next launch (stream-ordered), so
   // a launch needs no memset node in front of it
   if (tid == 0 &&
@@ -1053,44 +1171,79 @@ __global__ __launch_bounds__(HNT) void decode_head_kernel(HeadArgs a) {
 
 }  // namespace
 
-// Occupancy-checked cooperative launch capability per kernel variant (0 plain, 1 loader wave).
-static int coop_ok(int variant) {
-  static int cached[2] = {-1, -1};
-  if (cached[variant] < 0) {
-    int dev = 0, attr = 0, per_cu = 0, cus = 0;
-    const void* fn = variant ? (const void*)decode_mega_lw_kernel : (const void*)decode_mega_kernel;
-    cached[variant] =
-        hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&attr, hipDeviceAttributeCooperativeLaunch, dev) == hipSuccess && attr &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, variant ? LW_NT : NT, 0) == hipSuccess &&
-        per_cu * cus >= NWG;
+// Occupancy-checked cooperative launch capability of a kernel (cached per kernel).
+static int coop_ok(const void* fn, int threads) {
+  static const void* fns[16];
+  static int ok[16];
+  static int n = 0;
+  for (int i = 0; i < n; ++i)
+    if (fns[i] == fn) return ok[i];
+  int dev = 0, attr = 0, per_cu = 0, cus = 0;
+  const int r = hipGetDevice(&dev) == hipSuccess &&
+                hipDeviceGetAttribute(&attr, hipDeviceAttributeCooperativeLaunch, dev) == hipSuccess && attr &&
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, 0) == hipSuccess &&
+                per_cu * cus >= NWG;
+  if (n < 16) {
+    fns[n] = fn;
+    ok[n++] = r;
   }
-  return cached[variant];
+  return r;
 }
 
-// 1 when this device can run the single-launch step: cooperative launches supported and the
-// kernel's occupancy puts all NWG workgroups on the chip at once.
-PIAMD_EXPORT int piamd_decode_mega_supported() { return coop_ok(0); }
-PIAMD_EXPORT int piamd_decode_mega_lw_supported() { return coop_ok(1); }
+// The instantiated model shapes (E, D, Hq, Hk, F) × rotary off / on.
+typedef MegaCfg<2048, 128, 16, 16, 8192, 0> CfgGpt13;    // GPT-3 1.3B
+typedef MegaCfg<2048, 128, 16, 16, 8192, 1> CfgGpt13R;
+typedef MegaCfg<2048, 128, 16, 4, 8192, 0> CfgGqa4;      // 1.3B width, 4 KV heads (GQA 4:1)
+typedef MegaCfg<2048, 128, 16, 4, 8192, 1> CfgGqa4R;
+typedef MegaCfg<1024, 64, 16, 16, 4096, 0> CfgGpt350;    // GPT-3 350M
+typedef MegaCfg<1024, 64, 16, 16, 4096, 1> CfgGpt350R;
 
-// Launch one decode step over `nl` layers (see the header comment for the supported shapes).
-// `layers` is a device array of MegaLayer; scratch buffers per MegaArgs. Returns hipError_t.
+static const void* mega_fn(int E_, int D_, int hq, int hk, int F_, int rot) {
+#define MEGA_CFG(C)                                                                              \
+  if (E_ == C::E && D_ == C::D && hq == C::HQ && hk == C::HK && F_ == C::F && (rot != 0) == C::ROT) \
+    return (const void*)decode_mega_kernel<C>;
+  MEGA_CFG(CfgGpt13) MEGA_CFG(CfgGpt13R) MEGA_CFG(CfgGqa4) MEGA_CFG(CfgGqa4R)
+  MEGA_CFG(CfgGpt350) MEGA_CFG(CfgGpt350R)
+#undef MEGA_CFG
+  return nullptr;
+}
+
+// 1 when this device can run the single-launch step for the shape: an instantiated shape,
+// cooperative launches supported and all NWG workgroups co-resident.
+PIAMD_EXPORT int piamd_decode_mega_shape_supported(int E_, int D_, int hq, int hk, int F_, int rot) {
+  const void* fn = mega_fn(E_, D_, hq, hk, F_, rot);
+  return fn != nullptr && coop_ok(fn, NT);
+}
+PIAMD_EXPORT int piamd_decode_mega_supported() { return piamd_decode_mega_shape_supported(E, D, HQ, HK, F, 0); }
+PIAMD_EXPORT int piamd_decode_mega_lw_supported() {
+  return coop_ok((const void*)decode_mega_lw_kernel, LW_NT);
+}
+
+// Launch one decode step over `nl` layers of the shape (E_, D_, hq, hk, F_) with a.rot rotary
+// dims (0 or D_). `layers` is a device array of MegaLayer; scratch buffers per MegaArgs (part:
+// nl · pstride_hd(hq, D_, nsplit) floats). The dedicated-loader variant (a.loader = 1) exists for
+// the GPT-3 1.3B shape without rotary only. Returns hipError_t.
 PIAMD_EXPORT int piamd_decode_mega(const MegaArgs* args, int E_, int D_, int hq, int hk, int F_,
                                    hipStream_t st) {
   const MegaArgs& a = *args;
-  if (E_ != E || D_ != D || hq != HQ || hk != HK || F_ != F || a.nl < 1 || a.loader < 0 || a.loader > 1 ||
-      a.nsplit < 1 || HQ * a.nsplit > NWG || (a.maxS + a.nsplit - 1) / a.nsplit > 256 || !a.layers ||
-      !a.resid || !a.rbuf || !a.qn || !a.kvn || !a.part || !a.h || !a.bar || !a.err || !a.pos)
+  const void* fn = mega_fn(E_, D_, hq, hk, F_, a.rot);
+  const bool lw_shape = E_ == E && D_ == D && hq == HQ && hk == HK && F_ == F && a.rot == 0;
+  if (!fn || (a.rot != 0 && a.rot != D_) || a.nl < 1 || a.loader < 0 || a.loader > 1 ||
+      (a.loader && !lw_shape) || a.nsplit < 1 || hq * a.nsplit > NWG ||
+      (a.maxS + a.nsplit - 1) / a.nsplit > 256 || !a.layers || !a.resid || !a.rbuf || !a.qn ||
+      !a.kvn || !a.part || !a.h || !a.bar || !a.err || !a.pos)
     return (int)hipErrorInvalidValue;
   // cooperative launch: the runtime guarantees all NWG workgroups are co-resident (the grid
   // barriers rely on it) or refuses the launch; checked once against the kernel's occupancy
-  if (!coop_ok(a.loader)) return (int)hipErrorCooperativeLaunchTooLarge;
   MegaArgs arg = a;
   void* kargs[] = {&arg};
-  if (a.loader)
+  if (a.loader) {
+    if (!coop_ok((const void*)decode_mega_lw_kernel, LW_NT)) return (int)hipErrorCooperativeLaunchTooLarge;
     return (int)hipLaunchCooperativeKernel((const void*)decode_mega_lw_kernel, dim3(NWG), dim3(LW_NT), kargs, 0, st);
-  return (int)hipLaunchCooperativeKernel((const void*)decode_mega_kernel, dim3(NWG), dim3(NT), kargs, 0, st);
+  }
+  if (!coop_ok(fn, NT)) return (int)hipErrorCooperativeLaunchTooLarge;
+  return (int)hipLaunchCooperativeKernel(fn, dim3(NWG), dim3(NT), kargs, 0, st);
 }
 
 // Greedy tail of one batch-1 decode step (see decode_head_kernel). Returns hipError_t.

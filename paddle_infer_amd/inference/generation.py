@@ -28,8 +28,13 @@ from ..incubate.nn.functional import _lin
 class GPTGenerator:
     def __init__(self, model, max_batch: int = 8, max_seq_len: int | None = None,
                  use_hip_graph: bool = True, cache_dtype=None, weight_only: str | None = None,
-                 prepack: bool = True):
+                 prepack: bool = True, rotary_dim: int = 0, neox_rotary: bool = True,
+                 rope_base: float = 10000.0):
+        """``rotary_dim`` / ``neox_rotary`` / ``rope_base``: rotary position embedding applied to q
+        and k in every layer (reference ``fused_multi_transformer`` ``rotary_emb_dims``), on top of
+        whatever the model's embedding layer adds."""
         self.model = model.eval()
+        self.rotary_dim, self.neox_rotary, self.rope_base = int(rotary_dim), bool(neox_rotary), float(rope_base)
         cfg = model.cfg
         self.cfg = cfg
         p0 = next(iter(model.parameters()))
@@ -89,7 +94,8 @@ class GPTGenerator:
         emb = self.model.gpt.embeddings(ids, position_ids)
         y = IF.multi_transformer_forward(
             emb, self.layers, self.H, self.Hk, True, self.cfg.layer_norm_eps, caches, pos, lens,
-            None, decode, self.act, causal=True, group=self.group, max_len=self.max_seq_len,
+            None, decode, self.act, rotary_dim=self.rotary_dim, neox_rotary=self.neox_rotary,
+            rope_base=self.rope_base, causal=True, group=self.group, max_len=self.max_seq_len,
             final_ln=self.final_ln)
         return y
 

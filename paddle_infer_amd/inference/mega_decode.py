@@ -9,7 +9,9 @@ no longer pays a launch ramp per GEMV (5 per layer on the per-op path).
 Parity: one ``FusedMultiTransformer`` decode step with ``time_step``
 (`paddle/fluid/operators/fused/fused_multi_transformer_op.cu`); the per-op path
 (``incubate.nn.functional.multi_transformer_forward(decode=True)``) stays the reference and the
-fallback for shapes the kernel does not take (batch > 1, other widths, weight-only / TP / RoPE).
+fallback for shapes the kernel does not take (batch > 1, widths not instantiated in
+``decode_mega.hip`` — GPT-3 1.3B / 350M and a GQA 4:1 variant, each with or without whole-head
+rotary — weight-only, TP).
 """
 from __future__ import annotations
 
@@ -21,6 +23,9 @@ import torch
 
 from ..ops import _lib
 
+# the shape the dedicated-loader variant (decode_mega_lw_kernel) and the greedy tail
+# (decode_head_kernel) are built for; every shape of the plain kernel is listed at ``mega_fn`` in
+# decode_mega.hip and queried through piamd_decode_mega_shape_supported
 E, D, HQ, HK, F = 2048, 128, 16, 16, 8192
 # default for PIAMD_DECODE_MEGA (1 = batch-1 decode steps run the single-launch kernel, launched
 # cooperatively; 0 = the per-op path)
@@ -31,16 +36,22 @@ def enabled() -> bool:
     return os.environ.get("PIAMD_DECODE_MEGA", DEFAULT) != "0"
 
 
+def shape_of(gen):
+    """(E, D, Hq, Hk, F, rot) of generator ``gen``'s decoder stack."""
+    ffn = gen.layers[0]["ffn1"]
+    w = ffn.w
+    F_ = w.shape[0] if ffn.trans else w.shape[-1]
+    return gen.cfg.hidden_size, gen.D, gen.H, gen.Hk, int(F_), int(getattr(gen, "rotary_dim", 0))
+
+
 def eligible(gen, B: int) -> bool:
     """True when generator ``gen``'s decode step at batch ``B`` can run as one launch."""
     if not enabled():
         return False
     if B != 1 or gen.device.type != "cuda" or gen.dtype != torch.bfloat16 or gen.group is not None:
         return False
-    cfg = gen.cfg
-    if (cfg.hidden_size, gen.D, gen.H, gen.Hk) != (E, D, HQ, HK) or gen.max_seq_len > 256 * 16:
-        return False
-    if getattr(cfg, "ffn", F) != F or getattr(cfg, "rotary_dim", 0):
+    E_, D_, hq, hk, F_, rot = shape_of(gen)
+    if rot not in (0, D_) or gen.max_seq_len > 256 * 16 or gen.act not in ("gelu", "gelu_tanh"):
         return False
     for spec in gen.layers:
         for key in ("qkv", "out", "ffn1", "ffn2"):
@@ -52,8 +63,8 @@ def eligible(gen, B: int) -> bool:
             t = spec.get(key)
             if t is None or t.dtype != torch.bfloat16:
                 return False
-    return (_lib.available() and _lib.has("piamd_decode_mega")
-            and _lib.lib().piamd_decode_mega_supported() == 1)  # cooperative launch possible
+    return (_lib.available() and _lib.has("piamd_decode_mega_shape_supported")
+            and _lib.lib().piamd_decode_mega_shape_supported(E_, D_, hq, hk, F_, rot) == 1)
 
 
 def _out_in(lin):
@@ -82,6 +93,8 @@ class MegaDecoder:
         self.table = torch.tensor(rows, dtype=torch.int64, device=dev)
         self.nl = len(rows)
         self.maxS = gen.max_seq_len
+        self.E, self.D, self.HQ, self.HK, self.F, self.rot = shape_of(gen)
+        E_, D_, HQ_, HK_, F_ = self.E, self.D, self.HQ, self.HK, self.F
         # attention splits (≤ 256 keys each, Hq·nsplit ≤ 256). More splits shorten the attention
         # phase; the out-projection prologue requests 8 splits' partials at once, so up to 8 the
         # combine stays one load round (round 4, 24 layers: 8 splits 989 µs kernel vs 1 split
@@ -91,12 +104,14 @@ class MegaDecoder:
         # one slot per layer (and per residual update) for every vector handed between
         # workgroups: each address is written once per launch, so readers may use cached loads
         nl, f32, bf = self.nl, dict(dtype=torch.float32, device=dev), dict(dtype=torch.bfloat16, device=dev)
-        pstride = (HQ * self.nsplit * (D + 2) + 63) // 64 * 64
-        self.rbuf = torch.zeros(2 * nl, E, **bf)
-        self.qn = torch.zeros(nl, HQ * D, **f32)
-        self.kvn = torch.zeros(nl, 2 * HK * D, **f32)
+        pstride = (HQ_ * self.nsplit * (D_ + 2) + 63) // 64 * 64
+        self.rbuf = torch.zeros(2 * nl, E_, **bf)
+        self.qn = torch.zeros(nl, HQ_ * D_, **f32)
+        self.kvn = torch.zeros(nl, 2 * HK_ * D_, **f32)
         self.part = torch.zeros(nl * pstride, **f32)
-        self.h = torch.zeros(nl, F, **bf)
+        self.h = torch.zeros(nl, F_, **bf)
+        self.neox = 1 if getattr(gen, "neox_rotary", True) else 0
+        self.log2_base = math.log2(float(getattr(gen, "rope_base", 10000.0)))
         self.bar = torch.zeros(19 * 64, dtype=torch.int32, device=dev)
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.act = 1 if gen.act == "gelu_tanh" else 0
@@ -111,7 +126,7 @@ class MegaDecoder:
         # (decode_mega_lw_kernel; kernel 946 vs 968 us, generate 1.042 vs 1.072 ms/token);
         # 0: loader waves that are compute waves too (decode_mega_kernel)
         self.loader = int(os.environ.get("PIAMD_MEGA_LOADER", "1"))
-        if self.loader and _lib.lib().piamd_decode_mega_supported() == 1 and not self._lw_ok():
+        if self.loader and ((E_, D_, HQ_, HK_, F_, self.rot) != (E, D, HQ, HK, F, 0) or not self._lw_ok()):
             self.loader = 0
         # greedy tail (decode_head_kernel): LM head + argmax + bookkeeping + next embedding
         self.head_ok = _lib.has("piamd_decode_head_greedy") and self._head_tables(gen)
@@ -134,8 +149,9 @@ class MegaDecoder:
         if any(t is None or t.dtype != torch.bfloat16 or not t.is_contiguous() or not t.is_cuda for t in ts):
             return False
         self.pemb = self.pemb.detach()
-        return (self.head_w.dim() == 2 and self.head_w.shape[1] == E and self.wemb.shape[1] == E
-                and self.pemb.shape[1] == E and self.head_w.shape[0] == self.wemb.shape[0])
+        return (self.E == E and self.head_w.dim() == 2 and self.head_w.shape[1] == E
+                and self.wemb.shape[1] == E and self.pemb.shape[1] == E
+                and self.head_w.shape[0] == self.wemb.shape[0])
 
     def greedy_tail(self, y, out, t, done, eos, pad, pos, tok, resid) -> None:
         """After a step: final LN + LM head + argmax on ``y`` [E] → token (``pad`` once ``done``)
@@ -154,17 +170,19 @@ class MegaDecoder:
     def __call__(self, resid: torch.Tensor, pos: torch.Tensor) -> torch.Tensor:
         """resid: bf16 [E] embedding output; pos: device int32 [1] = the cache slot of this token.
         Returns the last layer's residual stream [E] (a view of an internal buffer)."""
-        assert resid.is_contiguous() and resid.numel() == E and resid.dtype == torch.bfloat16
+        assert resid.is_contiguous() and resid.numel() == self.E and resid.dtype == torch.bfloat16
         assert pos.dtype == torch.int32 and pos.is_cuda
         if self.trace is not None:  # the kernel writes 4 int64 slots per (workgroup, phase)
             assert (self.trace.dtype == torch.int64 and self.trace.is_cuda
                     and self.trace.numel() >= 256 * 5 * self.nl * 4), "trace must be int64 [256, 5*nl, 4]"
         a = _lib.MegaArgs(self.table.data_ptr(), self.nl, self.maxS, self.nsplit, self.act,
-                          self.eps, (1.0 / math.sqrt(D)) * 1.4426950408889634, resid.data_ptr(),
+                          self.eps, (1.0 / math.sqrt(self.D)) * 1.4426950408889634, resid.data_ptr(),
                           self.rbuf.data_ptr(), self.qn.data_ptr(), self.kvn.data_ptr(), self.part.data_ptr(),
                           self.h.data_ptr(), self.bar.data_ptr(), self.err.data_ptr(),
-                          pos.data_ptr(), _lib.ptr(self.trace), self.late_dma, self.loader)
-        _lib.call("piamd_decode_mega", ctypes.byref(a), E, D, HQ, HK, F, _lib.stream())
+                          pos.data_ptr(), _lib.ptr(self.trace), self.late_dma, self.loader,
+                          self.rot, self.neox, self.log2_base)
+        _lib.call("piamd_decode_mega", ctypes.byref(a), self.E, self.D, self.HQ, self.HK, self.F,
+                  _lib.stream())
         return self.rbuf[-1]
 
     def check(self) -> None:

@@ -92,10 +92,12 @@ class MegaArgs(ctypes.Structure):
     _fields_ = ([("layers", c_void_p)] + [(n, c_int) for n in ("nl", "maxS", "nsplit", "act")]
                 + [("eps", ctypes.c_float), ("scale_log2", ctypes.c_float)]
                 + [(n, c_void_p) for n in ("resid", "rbuf", "qn", "kvn", "part", "h", "bar", "err",
-                                        "pos", "trace")] + [("late_dma", c_int), ("loader", c_int)])
+                                        "pos", "trace")] + [("late_dma", c_int), ("loader", c_int)]
+                + [("rot", c_int), ("neox", c_int), ("log2_base", ctypes.c_float)])
 
 
 _SIGS["piamd_decode_mega"] = [ctypes.POINTER(MegaArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]
+_SIGS["piamd_decode_mega_shape_supported"] = [c_int] * 6
 
 
 class HeadArgs(ctypes.Structure):

@@ -125,7 +125,7 @@ def decode_attention(q, k_cache, v_cache, lens, Hq, Hk, mask=None, scale=None, o
         ck, ns = decode_chunking(max_len or maxS, chunk)
         part = cnt = None
         if ns > 1:
-            key = (q.device, B, Hq, ns, D)
+            key = (q.device, B, Hq, Hk, ns, D)  # cnt is [B·Hk]: models of equal Hq share no buffer
             ent = _PART_CACHE.get(key)
             if ent is None:
                 ent = _PART_CACHE[key] = (

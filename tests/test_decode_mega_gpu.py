@@ -1,6 +1,8 @@
 """Single-launch decode step (csrc/kernels/decode_mega.hip) against the per-op decode path
 (LN-fused GEMVs + split-K decode attention, itself checked against fp32 in
-test_infer_kernels_gpu.py) on a GPT-1.3B-width model (E 2048, 16 heads, FFN 8192)."""
+test_infer_kernels_gpu.py) on a GPT-1.3B-width model (E 2048, 16 heads, FFN 8192), the GPT-3
+350M width (E 1024, D 64, FFN 4096) and a GQA 4:1 stack with rotary embedding (NeoX and GPT-J
+styles)."""
 import pytest
 import torch
 
@@ -14,12 +16,12 @@ def _mega_on(monkeypatch):
     monkeypatch.setenv("PIAMD_DECODE_MEGA", "1")
 
 
-def _gpt13b_width(layers, max_pos):
+def _gpt13b_width(layers, max_pos, preset="gpt3-1.3b", **over):
     import paddle_infer_amd as paddle
     from paddle_infer_amd.models.gpt import GPTForPretraining, gpt_config
     paddle.seed(11)
-    cfg = gpt_config("gpt3-1.3b", dtype="float32", num_layers=layers, vocab_size=2048,
-                     hidden_dropout_prob=0.0, max_position_embeddings=max_pos)
+    cfg = gpt_config(preset, dtype="float32", num_layers=layers, vocab_size=2048,
+                     hidden_dropout_prob=0.0, max_position_embeddings=max_pos, **over)
     m = GPTForPretraining(cfg).eval()
     with torch.no_grad():  # non-trivial LN / bias values so every epilogue term is exercised
         for L in m.gpt.layers:
@@ -106,3 +108,46 @@ def test_mega_greedy_tail_matches_logits_path():
     assert torch.equal(out2[0, :k + 1].cpu(), out[0, :k + 1].cpu()), (out, out2)
     assert (out2[0, k + 1:] == 7).all(), out2
     g._mega.check()
+
+
+@pytest.mark.parametrize("shape", ["gpt3-350m", "gqa4_rope_neox", "gqa4_rope_gptj", "gpt13_rope"])
+def test_mega_decode_other_shapes_match_per_op_path(shape):
+    """The templated kernel at the other instantiated shapes: a second width (E 1024, D 64 —
+    waves 2-3 idle in the dot products, 8 lanes per head row), GQA 4:1 (4 KV heads shared by 16
+    query heads) and whole-head rotary embedding in both pairing styles (q and the new k rotated in
+    the attention phase, k cached after rotation), each against the per-op decode path."""
+    from paddle_infer_amd.inference import mega_decode
+    from paddle_infer_amd.inference.generation import GPTGenerator
+    preset, over, rope = {"gpt3-350m": ("gpt3-350m", {}, None),
+                          "gqa4_rope_neox": ("gpt3-1.3b", {"num_kv_heads": 4}, True),
+                          "gqa4_rope_gptj": ("gpt3-1.3b", {"num_kv_heads": 4}, False),
+                          "gpt13_rope": ("gpt3-1.3b", {}, True)}[shape]
+    m = _gpt13b_width(2, 512, preset, **over)
+    kw = dict(rotary_dim=m.cfg.head_dim, neox_rotary=rope) if rope is not None else {}
+    g_mega = GPTGenerator(m, max_batch=1, max_seq_len=512, use_hip_graph=False, **kw)
+    g_ref = GPTGenerator(m, max_batch=1, max_seq_len=512, use_hip_graph=False, **kw)
+    g_ref._mega = False
+    assert mega_decode.eligible(g_mega, 1), mega_decode.shape_of(g_mega)
+    prompt = 77
+    ids = torch.randint(0, 2048, (1, prompt), device=DEV)
+    lens = torch.full((1,), prompt, device=DEV)
+    la, lb = g_mega.prefill(ids, lens), g_ref.prefill(ids, lens)
+    pos = torch.full((1,), prompt, dtype=torch.int32, device=DEV)
+    for step in range(5):
+        tok = lb.argmax(-1)
+        la, lb = g_mega.decode(tok, pos), g_ref.decode(tok, pos)
+        assert isinstance(g_mega._mega, mega_decode.MegaDecoder) and g_mega._mega.loader == 0
+        assert _rel(la, lb) < 2e-2, (step, _rel(la, lb))
+        for (ka, va), (kb, vb) in zip(g_mega.caches, g_ref.caches):
+            p = int(pos[0])
+            assert _rel(ka[0, :, p], kb[0, :, p]) < 1e-2 and _rel(va[0, :, p], vb[0, :, p]) < 1e-2
+        pos += 1
+    g_mega._mega.check()
+
+
+def test_mega_decode_shape_gate():
+    """Shapes without an instantiation are refused (per-op path), never launched."""
+    from paddle_infer_amd.ops import _lib
+    f = _lib.lib().piamd_decode_mega_shape_supported
+    assert f(2048, 128, 16, 16, 8192, 0) == 1 and f(1024, 64, 16, 16, 4096, 128 // 2) == 1
+    assert f(2560, 80, 32, 32, 10240, 0) == 0 and f(2048, 128, 16, 8, 8192, 0) == 0

@@ -371,3 +371,20 @@ def test_decode_fused_ln_gemv_matches_unfused(batch):
     finally:
         INF.packed_linear = orig_packed
         IF._Linear.fused_gemv = orig_gemv
+
+
+def test_decode_attention_split_buffers_keyed_by_kv_heads():
+    """Two models with equal Hq but different Hk in one process: the split-K counters are [B·Hk]
+    per (Hq, Hk) — a shared buffer sized for the smaller Hk corrupted the larger model's merges."""
+    from paddle_infer_amd.ops import inference as I
+    torch.manual_seed(5)
+    D, maxS, Hq = 128, 1024, 16
+    ln = torch.tensor([900], dtype=torch.int32, device=DEV)
+    for Hk in (4, 16):
+        q = torch.randn(1, (Hq + 2 * Hk) * D, device=DEV).bfloat16()
+        kc = torch.randn(1, Hk, maxS, D, device=DEV).bfloat16()
+        vc = torch.randn(1, Hk, maxS, D, device=DEV).bfloat16()
+        got = I.decode_attention(q, kc, vc, ln, Hq, Hk, max_len=maxS)
+        ref = I.decode_attention(q.float().cpu(), kc.float().cpu(), vc.float().cpu(), ln.cpu(), Hq, Hk,
+                                 out=torch.empty(1, Hq * D))
+        _close(got, ref, 2e-2)

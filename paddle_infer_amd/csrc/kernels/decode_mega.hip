@@ -60,6 +60,9 @@ typedef unsigned long long u64;
 struct MegaLayer {
   const bf16_t *ln1_g, *ln1_b, *wqkv, *bqkv, *wo, *bo, *ln2_g, *ln2_b, *w1, *b1, *w2, *b2;
   bf16_t *kc, *vc;
+  // int8 weight-only mode (MegaArgs.w8): the four weights above are int8 [out][in] and these
+  // are their per-output-channel f32 scales (null otherwise)
+  const float *sqkv, *so, *s1, *s2;
 };
 
 struct MegaArgs {
@@ -86,6 +89,7 @@ struct MegaArgs {
   int rot;              // rotary dims: 0 or D (whole head)
   int neox;             // 1: rotate-half (NeoX), 0: interleaved pairs (GPT-J)
   float log2_base;      // log2 of the rotary base
+  int w8;               // 1: int8 weight-only projections (MegaLayer scales)
 };
 
 __device__ __forceinline__ u64 ld64(const void* p) { return *reinterpret_cast<const u64*>(p); }
@@ -208,7 +212,7 @@ __device__ __forceinline__ void butterfly(float* acc, int lane) {
 // `mid()` runs once every wave has consumed the first half of the columns (slice bytes
 // [0, SLICE/2) are free), `end()` once the whole slice is consumed: the loader waves issue the
 // next slices' DMA there.
-template <int NPW, int K, class Mid, class End>
+template <int NPW, int K, bool W8, class Mid, class End>
 __device__ __forceinline__ float gemv_lds(const char* ws, const float (&x)[(K + 2047) / 2048][8], float* red,
                                           int tid, Mid mid, End end) {
   constexpr int KCH = (K + 2047) / 2048;
@@ -225,9 +229,16 @@ __device__ __forceinline__ float gemv_lds(const char* ws, const float (&x)[(K + 
 #pragma unroll
       for (int j = 0; j < KCH; ++j) {
         if (K % 2048 != 0 && (j * 256 + tid) * 8 >= K) continue;  // wave-uniform
-        const u16x8 w = *reinterpret_cast<const u16x8*>(ws + ((long)c * K + (j * 256 + tid) * 8) * 2);
+        if constexpr (W8) {  // int8 [NPW][K]: 8 weights per 8-B read, scaled after the sum
+          const uint2 q = *reinterpret_cast<const uint2*>(ws + (long)c * K + (j * 256 + tid) * 8);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) acc[c] += x[j][i] * bf2f(w[i]);
+          for (int i = 0; i < 8; ++i)
+            acc[c] += x[j][i] * (float)(int)(signed char)(((i < 4 ? q.x : q.y) >> (8 * (i & 3))) & 0xFF);
+        } else {
+          const u16x8 w = *reinterpret_cast<const u16x8*>(ws + ((long)c * K + (j * 256 + tid) * 8) * 2);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) acc[c] += x[j][i] * bf2f(w[i]);
+        }
       }
     }
   };
@@ -289,16 +300,17 @@ __device__ __forceinline__ void publish_bf16(bf16_t* dst, float y, int lane, int
 // (NeoX rotate-half or GPT-J interleaved per MegaArgs.neox, angles pos·base^(−2f/D)) applied to q
 // and the new k. Every projection splits its output columns evenly over the 256 workgroups and
 // each workgroup's weight slice must fit the 128 KiB LDS image.
-template <int E_, int D_, int HQ_, int HK_, int F_, int ROT_>
+template <int E_, int D_, int HQ_, int HK_, int F_, int ROT_, int W8_ = 0>
 struct MegaCfg {
-  static constexpr int E = E_, D = D_, HQ = HQ_, HK = HK_, F = F_, ROT = ROT_;
+  static constexpr int E = E_, D = D_, HQ = HQ_, HK = HK_, F = F_, ROT = ROT_, W8 = W8_;
+  static constexpr int WB = W8 ? 1 : 2;  // bytes per weight
   static constexpr int NQKV = (HQ + 2 * HK) * D;
   static constexpr int NPQ = NQKV / NWG, NPO = E / NWG, NP1 = F / NWG, NP2 = E / NWG;
   // slice bytes: QKV [0, QB) → out [QB, QB + OB) (free during QKV) → FFN1 [0, F1B), whose first
   // F1PRE bytes stream in during the attention phase (workgroups without attention work) or the
   // out-projection prologue (the others) and the rest once the out slice is consumed → FFN2
   // [0, F2B) → next QKV [0, QB)
-  static constexpr int QB = NPQ * E * 2, OB = NPO * E * 2, F1B = NP1 * E * 2, F2B = NP2 * F * 2;
+  static constexpr int QB = NPQ * E * WB, OB = NPO * E * WB, F1B = NP1 * E * WB, F2B = NP2 * F * WB;
   static constexpr int OUT_OFF = QB;
   static constexpr int F1PRE = QB < F1B ? QB : F1B;
   // the out phase of a non-attention workgroup waits for every DMA older than its FFN1 head: the
@@ -323,6 +335,11 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
   constexpr int E = C::E, D = C::D, HQ = C::HQ, HK = C::HK, F = C::F, LPR = C::LPR;
   constexpr int NPQ = C::NPQ, NPO = C::NPO, NP1 = C::NP1, NP2 = C::NP2;
   constexpr int PSTR = D + 2;
+  constexpr bool W8 = C::W8 != 0;
+  // a workgroup's weight slice: `rows` [out] rows of `in` weights, C::WB bytes each
+  auto slice = [](const bf16_t* w, long row0, long in) {
+    return reinterpret_cast<const bf16_t*>(reinterpret_cast<const char*>(w) + row0 * in * C::WB);
+  };
   __shared__ __attribute__((aligned(1024))) char wl[WBYTES];
   __shared__ float red[4 * 32];
   __shared__ float wred[8];
@@ -333,7 +350,7 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
   const int pos = a.pos[0], L = pos + 1;
   unsigned nbar = 0;
 
-  prefetch(a.layers[0].wqkv + (long)w * NPQ * E, 0, C::QB, wl, wv, lane);
+  prefetch(slice(a.layers[0].wqkv, (long)w * NPQ, E), 0, C::QB, wl, wv, lane);
   for (int l = 0; l < a.nl; ++l) {
     const MegaLayer& Ly = a.layers[l];
     // this layer's buffer slots: every published vector has its own address per launch, so a
@@ -350,12 +367,13 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
     {
       // epilogue operands requested first: their latency hides under the prologue and GEMV
       const float bq = lane < NPQ ? bf2f(Ly.bqkv[w * NPQ + lane]) : 0.f;
+      const float sq = W8 && lane < NPQ ? Ly.sqkv[w * NPQ + lane] : 1.f;
       float x[1][8];
       ln_prologue<E>(a, rin, Ly.ln1_g, Ly.ln1_b, x, wred, tid);
       tmark(a, nbar, 1);
       // out slice into the region QKV does not use, behind this GEMV
-      const float y = gemv_lds<NPQ, E>(wl, x, red, tid, [] {}, [&] {
-        prefetch(Ly.wo + (long)w * NPO * E, 0, C::OB, wl + C::OUT_OFF, wv, lane);
+      const float y = sq * gemv_lds<NPQ, E, W8>(wl, x, red, tid, [] {}, [&] {
+        prefetch(slice(Ly.wo, (long)w * NPO, E), 0, C::OB, wl + C::OUT_OFF, wv, lane);
       });
       tmark(a, nbar, 2);
       if (wv == 0) {
@@ -385,7 +403,7 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
     // ---------------------------------------------------------------- attention
     // (attention reads no weights: the out slice keeps streaming)
     phase_start<C::WAIT_OLD>(a, wv, nbar, WAIT_NONE);
-    const bf16_t* w1s = Ly.w1 + (long)w * NP1 * E;
+    const bf16_t* w1s = slice(Ly.w1, (long)w * NP1, E);
     if (w < HQ * a.nsplit) {
       const int h = w / a.nsplit, s = w % a.nsplit, kh = h / (HQ / HK);
       const int chunk = (L + a.nsplit - 1) / a.nsplit;
@@ -517,6 +535,7 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
     {
       const int ocol = w * NPO + (lane & (NPO - 1));
       const float bo = bf2f(Ly.bo[ocol]), ro = bf2f(rin[ocol]);
+      const float so = W8 ? Ly.so[ocol] : 1.f;
       float x[1][8];
       {
         const int h = tid / LPR, d0 = (tid % LPR) * 8;  // thread t holds elements 8t … 8t+7
@@ -555,7 +574,7 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
       }
       if (attn_wg) prefetch(w1s, 0, C::F1PRE, wl, wv, lane);
       tmark(a, nbar, 1);
-      const float y = gemv_lds<NPO, E>(wl + C::OUT_OFF, x, red, tid, [] {}, [&] {
+      const float y = so * gemv_lds<NPO, E, W8>(wl + C::OUT_OFF, x, red, tid, [] {}, [&] {
         prefetch(w1s, C::F1PRE, C::F1B, wl, wv, lane);
       });
       tmark(a, nbar, 2);
@@ -570,13 +589,14 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
     phase_start<C::WAIT_OLD>(a, wv, nbar);
     {
       const float b1 = bf2f(Ly.b1[w * NP1 + (lane & (NP1 - 1))]);
+      const float s1 = W8 ? Ly.s1[w * NP1 + (lane & (NP1 - 1))] : 1.f;
       float x[1][8];
       ln_prologue<E>(a, rmid, Ly.ln2_g, Ly.ln2_b, x, wred, tid);
       tmark(a, nbar, 1);
-      const bf16_t* w2s = Ly.w2 + (long)w * NP2 * F;
+      const bf16_t* w2s = slice(Ly.w2, (long)w * NP2, F);
       constexpr int MID1 = C::F1B / 2 < C::F2B ? C::F1B / 2 : C::F2B;
       const int mid = a.late_dma ? 0 : MID1;
-      const float y = gemv_lds<NP1, E>(wl, x, red, tid, [&] { prefetch(w2s, 0, mid, wl, wv, lane); },
+      const float y = s1 * gemv_lds<NP1, E, W8>(wl, x, red, tid, [&] { prefetch(w2s, 0, mid, wl, wv, lane); },
                                        [&] { prefetch(w2s, mid, C::F2B, wl, wv, lane); });
       tmark(a, nbar, 2);
       if (wv == 0) {
@@ -592,15 +612,16 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
     {
       const int fcol = w * NP2 + (lane & (NP2 - 1));
       const float b2 = bf2f(Ly.b2[fcol]), rm = bf2f(rmid[fcol]);
+      const float s2 = W8 ? Ly.s2[fcol] : 1.f;
       constexpr int KCH2 = F / 2048;
       float x[KCH2][8];
 #pragma unroll
       for (int j = 0; j < KCH2; ++j) ld_bf8(hb + (j * 256 + tid) * 8, x[j]);
       tmark(a, nbar, 1);
-      const bf16_t* nq = l + 1 < a.nl ? a.layers[l + 1].wqkv + (long)w * NPQ * E : nullptr;
+      const bf16_t* nq = l + 1 < a.nl ? slice(a.layers[l + 1].wqkv, (long)w * NPQ, E) : nullptr;
       constexpr int MID2 = C::F2B / 2 < C::QB ? C::F2B / 2 : C::QB;
       const int mid = a.late_dma ? 0 : MID2;
-      const float y = gemv_lds<NP2, F>(wl, x, red, tid, [&] { prefetch(nq, 0, mid, wl, wv, lane); },
+      const float y = s2 * gemv_lds<NP2, F, W8>(wl, x, red, tid, [&] { prefetch(nq, 0, mid, wl, wv, lane); },
                                        [&] { prefetch(nq, mid, C::QB, wl, wv, lane); });
       tmark(a, nbar, 2);
       if (wv == 0) {
@@ -1198,24 +1219,27 @@ typedef MegaCfg<2048, 128, 16, 4, 8192, 0> CfgGqa4;      // 1.3B width, 4 KV hea
 typedef MegaCfg<2048, 128, 16, 4, 8192, 1> CfgGqa4R;
 typedef MegaCfg<1024, 64, 16, 16, 4096, 0> CfgGpt350;    // GPT-3 350M
 typedef MegaCfg<1024, 64, 16, 16, 4096, 1> CfgGpt350R;
+typedef MegaCfg<2048, 128, 16, 16, 8192, 0, 1> CfgGpt13W8;  // int8 weight-only
+typedef MegaCfg<2048, 128, 16, 4, 8192, 1, 1> CfgGqa4RW8;
 
-static const void* mega_fn(int E_, int D_, int hq, int hk, int F_, int rot) {
-#define MEGA_CFG(C)                                                                              \
-  if (E_ == C::E && D_ == C::D && hq == C::HQ && hk == C::HK && F_ == C::F && (rot != 0) == C::ROT) \
+static const void* mega_fn(int E_, int D_, int hq, int hk, int F_, int rot, int w8) {
+#define MEGA_CFG(C)                                                                           \
+  if (E_ == C::E && D_ == C::D && hq == C::HQ && hk == C::HK && F_ == C::F &&                 \
+      (rot != 0) == C::ROT && (w8 != 0) == C::W8)                                             \
     return (const void*)decode_mega_kernel<C>;
   MEGA_CFG(CfgGpt13) MEGA_CFG(CfgGpt13R) MEGA_CFG(CfgGqa4) MEGA_CFG(CfgGqa4R)
-  MEGA_CFG(CfgGpt350) MEGA_CFG(CfgGpt350R)
+  MEGA_CFG(CfgGpt350) MEGA_CFG(CfgGpt350R) MEGA_CFG(CfgGpt13W8) MEGA_CFG(CfgGqa4RW8)
 #undef MEGA_CFG
   return nullptr;
 }
 
 // 1 when this device can run the single-launch step for the shape: an instantiated shape,
 // cooperative launches supported and all NWG workgroups co-resident.
-PIAMD_EXPORT int piamd_decode_mega_shape_supported(int E_, int D_, int hq, int hk, int F_, int rot) {
-  const void* fn = mega_fn(E_, D_, hq, hk, F_, rot);
+PIAMD_EXPORT int piamd_decode_mega_shape_supported(int E_, int D_, int hq, int hk, int F_, int rot, int w8) {
+  const void* fn = mega_fn(E_, D_, hq, hk, F_, rot, w8);
   return fn != nullptr && coop_ok(fn, NT);
 }
-PIAMD_EXPORT int piamd_decode_mega_supported() { return piamd_decode_mega_shape_supported(E, D, HQ, HK, F, 0); }
+PIAMD_EXPORT int piamd_decode_mega_supported() { return piamd_decode_mega_shape_supported(E, D, HQ, HK, F, 0, 0); }
 PIAMD_EXPORT int piamd_decode_mega_lw_supported() {
   return coop_ok((const void*)decode_mega_lw_kernel, LW_NT);
 }
@@ -1227,8 +1251,8 @@ PIAMD_EXPORT int piamd_decode_mega_lw_supported() {
 PIAMD_EXPORT int piamd_decode_mega(const MegaArgs* args, int E_, int D_, int hq, int hk, int F_,
                                    hipStream_t st) {
   const MegaArgs& a = *args;
-  const void* fn = mega_fn(E_, D_, hq, hk, F_, a.rot);
-  const bool lw_shape = E_ == E && D_ == D && hq == HQ && hk == HK && F_ == F && a.rot == 0;
+  const void* fn = mega_fn(E_, D_, hq, hk, F_, a.rot, a.w8);
+  const bool lw_shape = E_ == E && D_ == D && hq == HQ && hk == HK && F_ == F && a.rot == 0 && !a.w8;
   if (!fn || (a.rot != 0 && a.rot != D_) || a.nl < 1 || a.loader < 0 || a.loader > 1 ||
       (a.loader && !lw_shape) || a.nsplit < 1 || hq * a.nsplit > NWG ||
       (a.maxS + a.nsplit - 1) / a.nsplit > 256 || !a.layers || !a.resid || !a.rbuf || !a.qn ||

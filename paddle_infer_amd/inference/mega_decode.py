@@ -39,9 +39,22 @@ def enabled() -> bool:
 def shape_of(gen):
     """(E, D, Hq, Hk, F, rot) of generator ``gen``'s decoder stack."""
     ffn = gen.layers[0]["ffn1"]
-    w = ffn.w
-    F_ = w.shape[0] if ffn.trans else w.shape[-1]
+    if ffn.bits:  # packed weight-only codes: the output width is the per-channel scale count
+        F_ = ffn.scale.numel()
+    else:
+        F_ = ffn.w.shape[0] if ffn.trans else ffn.w.shape[-1]
     return gen.cfg.hidden_size, gen.D, gen.H, gen.Hk, int(F_), int(getattr(gen, "rotary_dim", 0))
+
+
+def _w8(gen):
+    """1 when every projection is int8 weight-only, 0 when every one is bf16, None otherwise."""
+    bits = {spec[k].bits for spec in gen.layers for k in ("qkv", "out", "ffn1", "ffn2")}
+    if bits == {8}:
+        return 1
+    if bits == {0} and all(spec[k].w.dtype == torch.bfloat16 for spec in gen.layers
+                           for k in ("qkv", "out", "ffn1", "ffn2")):
+        return 0
+    return None
 
 
 def eligible(gen, B: int) -> bool:
@@ -53,25 +66,31 @@ def eligible(gen, B: int) -> bool:
     E_, D_, hq, hk, F_, rot = shape_of(gen)
     if rot not in (0, D_) or gen.max_seq_len > 256 * 16 or gen.act not in ("gelu", "gelu_tanh"):
         return False
+    w8 = _w8(gen)
+    if w8 is None:
+        return False
     for spec in gen.layers:
-        for key in ("qkv", "out", "ffn1", "ffn2"):
-            lin = spec[key]
-            if lin.bits or lin.w.dtype != torch.bfloat16:
-                return False
         for key in ("ln_scale", "ln_bias", "ffn_ln_scale", "ffn_ln_bias", "qkv_bias", "out_bias",
                     "ffn1_bias", "ffn2_bias"):
             t = spec.get(key)
             if t is None or t.dtype != torch.bfloat16:
                 return False
     return (_lib.available() and _lib.has("piamd_decode_mega_shape_supported")
-            and _lib.lib().piamd_decode_mega_shape_supported(E_, D_, hq, hk, F_, rot) == 1)
+            and _lib.lib().piamd_decode_mega_shape_supported(E_, D_, hq, hk, F_, rot, w8) == 1)
 
 
 def _out_in(lin):
-    """[out, in] contiguous bf16 copy of a projection (each workgroup's slice is then one
-    contiguous run of rows)."""
+    """[out, in] contiguous copy of a projection (each workgroup's slice is then one contiguous
+    run of rows): bf16, or (int8 weight-only) the int8 codes with their f32 per-output scales
+    recovered from the packed GEMV layout (exact: dequantised value / scale is the code)."""
+    if lin.bits == 8:
+        from ..ops.inference import weight_dequantize
+        s = lin.scale.float().contiguous()
+        deq = weight_dequantize(lin.w, s, "weight_only_int8", "float32").t()  # [K, N] → [out, in]
+        q = torch.round(deq.float() / s[:, None]).clamp(-127, 127).to(torch.int8).contiguous()
+        return q, s
     w = lin.w.detach()
-    return (w if lin.trans else w.t()).contiguous()
+    return (w if lin.trans else w.t()).contiguous(), None
 
 
 class MegaDecoder:
@@ -82,14 +101,15 @@ class MegaDecoder:
         self.gen = gen
         self._keep = []
         rows = []
+        self.w8 = _w8(gen) or 0
         for spec, (kc, vc) in zip(gen.layers, gen.caches):
             ws = [_out_in(spec[k]) for k in ("qkv", "out", "ffn1", "ffn2")]
-            ts = [spec["ln_scale"], spec["ln_bias"], ws[0], spec["qkv_bias"], ws[1], spec["out_bias"],
-                  spec["ffn_ln_scale"], spec["ffn_ln_bias"], ws[2], spec["ffn1_bias"], ws[3],
-                  spec["ffn2_bias"], kc, vc]
-            ts = [t.contiguous() for t in ts]
-            self._keep += ts
-            rows.append([t.data_ptr() for t in ts])
+            ts = [spec["ln_scale"], spec["ln_bias"], ws[0][0], spec["qkv_bias"], ws[1][0], spec["out_bias"],
+                  spec["ffn_ln_scale"], spec["ffn_ln_bias"], ws[2][0], spec["ffn1_bias"], ws[3][0],
+                  spec["ffn2_bias"], kc, vc] + [w[1] for w in ws]
+            ts = [t.contiguous() if t is not None else None for t in ts]
+            self._keep += [t for t in ts if t is not None]
+            rows.append([t.data_ptr() if t is not None else 0 for t in ts])
         self.table = torch.tensor(rows, dtype=torch.int64, device=dev)
         self.nl = len(rows)
         self.maxS = gen.max_seq_len
@@ -126,7 +146,8 @@ class MegaDecoder:
         # (decode_mega_lw_kernel; kernel 946 vs 968 us, generate 1.042 vs 1.072 ms/token);
         # 0: loader waves that are compute waves too (decode_mega_kernel)
         self.loader = int(os.environ.get("PIAMD_MEGA_LOADER", "1"))
-        if self.loader and ((E_, D_, HQ_, HK_, F_, self.rot) != (E, D, HQ, HK, F, 0) or not self._lw_ok()):
+        if self.loader and ((E_, D_, HQ_, HK_, F_, self.rot, self.w8) != (E, D, HQ, HK, F, 0, 0)
+                            or not self._lw_ok()):
             self.loader = 0
         # greedy tail (decode_head_kernel): LM head + argmax + bookkeeping + next embedding
         self.head_ok = _lib.has("piamd_decode_head_greedy") and self._head_tables(gen)
@@ -180,7 +201,7 @@ class MegaDecoder:
                           self.rbuf.data_ptr(), self.qn.data_ptr(), self.kvn.data_ptr(), self.part.data_ptr(),
                           self.h.data_ptr(), self.bar.data_ptr(), self.err.data_ptr(),
                           pos.data_ptr(), _lib.ptr(self.trace), self.late_dma, self.loader,
-                          self.rot, self.neox, self.log2_base)
+                          self.rot, self.neox, self.log2_base, self.w8)
         _lib.call("piamd_decode_mega", ctypes.byref(a), self.E, self.D, self.HQ, self.HK, self.F,
                   _lib.stream())
         return self.rbuf[-1]

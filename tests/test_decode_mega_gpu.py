@@ -149,5 +149,35 @@ def test_mega_decode_shape_gate():
     """Shapes without an instantiation are refused (per-op path), never launched."""
     from paddle_infer_amd.ops import _lib
     f = _lib.lib().piamd_decode_mega_shape_supported
-    assert f(2048, 128, 16, 16, 8192, 0) == 1 and f(1024, 64, 16, 16, 4096, 128 // 2) == 1
-    assert f(2560, 80, 32, 32, 10240, 0) == 0 and f(2048, 128, 16, 8, 8192, 0) == 0
+    assert f(2048, 128, 16, 16, 8192, 0, 0) == 1 and f(1024, 64, 16, 16, 4096, 64, 0) == 1
+    assert f(2048, 128, 16, 16, 8192, 0, 1) == 1 and f(2048, 128, 16, 4, 8192, 128, 1) == 1
+    assert f(2560, 80, 32, 32, 10240, 0, 0) == 0 and f(2048, 128, 16, 8, 8192, 0, 0) == 0
+    assert f(1024, 64, 16, 16, 4096, 0, 1) == 0
+
+
+@pytest.mark.parametrize("shape", ["gpt13_int8", "gqa4_rope_int8"])
+def test_mega_decode_int8_weight_only_matches_per_op_path(shape):
+    """int8 weight-only projections (FusedMultiTransformerWeightOnly decode): the kernel streams
+    the int8 codes (half the bytes) and applies the per-output-channel scales after each column
+    sum; against the per-op weight-only GEMV path of the same generator settings."""
+    from paddle_infer_amd.inference import mega_decode
+    from paddle_infer_amd.inference.generation import GPTGenerator
+    over, kw = ({}, {}) if shape == "gpt13_int8" else \
+        ({"num_kv_heads": 4}, dict(rotary_dim=128, neox_rotary=True))
+    m = _gpt13b_width(2, 512, "gpt3-1.3b", **over)
+    g_mega = GPTGenerator(m, max_batch=1, max_seq_len=512, use_hip_graph=False, weight_only="int8", **kw)
+    g_ref = GPTGenerator(m, max_batch=1, max_seq_len=512, use_hip_graph=False, weight_only="int8", **kw)
+    g_ref._mega = False
+    assert mega_decode.eligible(g_mega, 1)
+    prompt = 50
+    ids = torch.randint(0, 2048, (1, prompt), device=DEV)
+    lens = torch.full((1,), prompt, device=DEV)
+    la, lb = g_mega.prefill(ids, lens), g_ref.prefill(ids, lens)
+    pos = torch.full((1,), prompt, dtype=torch.int32, device=DEV)
+    for step in range(4):
+        tok = lb.argmax(-1)
+        la, lb = g_mega.decode(tok, pos), g_ref.decode(tok, pos)
+        assert g_mega._mega.w8 == 1 and g_mega._mega.loader == 0
+        assert _rel(la, lb) < 2e-2, (step, _rel(la, lb))
+        pos += 1
+    g_mega._mega.check()

@@ -6,6 +6,8 @@
   executor scheduler, data-loader ring) built with g++.
 * ``_lib/libpiamd_alloc.so`` — the auto-growth best-fit device allocator (``csrc/alloc``,
   host-only HIP runtime code, g++ against the HIP headers; plugged into PyTorch's HIP allocator).
+* ``_lib/libpiamd_device.so`` — the device runtime (``csrc/device``: properties, stream pool with
+  priorities, events, the host/device range tracer behind ``paddle.profiler``), host-only HIP.
 * ``_lib/piamd_agemm.hsaco`` — the hand-scheduled assembly GEMM kernels: ``csrc/asm/gemm_gen.py``
   emits the gfx950 assembly, clang assembles it and ld.lld links the code object (loaded at run
   time by ``csrc/kernels/agemm_host.hip`` through ``hipModuleLoad``).
@@ -40,6 +42,8 @@ NATIVE_LIB = os.path.join(LIBDIR, "libpiamd_infer.so")
 NATIVE_RUN = os.path.join(LIBDIR, "pd_infer_run")
 ADIR = os.path.join(ROOT, "csrc", "alloc")
 ALLOC_LIB = os.path.join(LIBDIR, "libpiamd_alloc.so")
+DDIR = os.path.join(ROOT, "csrc", "device")
+DEVICE_LIB = os.path.join(LIBDIR, "libpiamd_device.so")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("PIAMD_ARCH", "gfx950")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
@@ -181,6 +185,11 @@ def build(verbose: bool = True, jobs: int | None = None) -> None:
         _build_lib(asrcs, ALLOC_LIB, "g++", CXX_FLAGS + ["-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include"],
                    ["-pthread", f"-L{ROCM}/lib", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"],
                    _newest_header(ADIR), verbose, jobs)
+    dsrcs = sorted(glob.glob(os.path.join(DDIR, "*.cc")))
+    if dsrcs:  # device runtime (streams / events / properties / tracer): host HIP runtime code
+        _build_lib(dsrcs, DEVICE_LIB, "g++", CXX_FLAGS + ["-D__HIP_PLATFORM_AMD__", f"-I{ROCM}/include"],
+                   ["-pthread", f"-L{ROCM}/lib", "-lamdhip64", f"-Wl,-rpath,{ROCM}/lib"],
+                   _newest_header(DDIR), verbose, jobs)
     build_native(verbose, jobs)
 
 

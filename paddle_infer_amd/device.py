@@ -5,6 +5,8 @@ the default device for tensor creation. Streams/events are HIP streams/events vi
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 _current = {"device": None}
@@ -145,9 +147,174 @@ def get_available_device():
     return [f"gpu:{i}" for i in range(torch.cuda.device_count())] if torch.cuda.is_available() else []
 
 
+class _NativeStream:
+    """``paddle.device.cuda.Stream`` on a natively created HIP stream (``csrc/device``: priority
+    from the device's range, non-blocking w.r.t. the legacy default stream). ``torch_stream`` is the
+    same ``hipStream_t`` adopted by ``torch.cuda.ExternalStream``: entered through
+    :func:`cuda.stream_guard` every PyTorch op, framework HIP kernel and collective in the block
+    runs on it. Reference: `paddle/fluid/pybind/cuda_streams_py.cc` (priority 1 = high, 2 =
+    normal), `phi/backends/gpu/gpu_context.cc`."""
+
+    def __init__(self, device=None, priority=2, *, _torch=None):
+        from .framework import device_rt as rt
+        if _torch is not None:  # non-owning wrapper of an existing torch stream
+            self._t, self._own = _torch, False
+            self.device = _torch.device
+            self._h = _torch.cuda_stream
+            return
+        dev = _parse(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        least, greatest = rt.priority_range()
+        hip_prio = greatest if int(priority) == 1 else least
+        h = ctypes.c_void_p()
+        rt.check(rt.lib().piamd_stream_create(idx, hip_prio, 1, ctypes.byref(h)), "hipStreamCreate")
+        self._h, self._own, self.device = h.value, True, torch.device("cuda", idx)
+        self._t = torch.cuda.ExternalStream(self._h, device=self.device)
+        self.priority = int(priority)
+
+    @property
+    def cuda_stream(self) -> int:
+        return self._h
+
+    @property
+    def torch_stream(self):
+        return self._t
+
+    def synchronize(self):
+        from .framework import device_rt as rt
+        rt.check(rt.lib().piamd_stream_sync(self._h), "hipStreamSynchronize")
+
+    def query(self) -> bool:
+        from .framework import device_rt as rt
+        r = rt.lib().piamd_stream_query(self._h)
+        if r < 0:
+            raise RuntimeError(f"hipStreamQuery failed with hipError {-r}")
+        return r == 1
+
+    def wait_event(self, event):
+        from .framework import device_rt as rt
+        rt.check(rt.lib().piamd_stream_wait_event(self._h, event.handle), "hipStreamWaitEvent")
+
+    def wait_stream(self, stream):
+        ev = _NativeEvent()
+        ev.record(stream)
+        self.wait_event(ev)
+
+    def record_event(self, event=None):
+        event = event if event is not None else _NativeEvent()
+        event.record(self)
+        return event
+
+    def __eq__(self, other):
+        return isinstance(other, _NativeStream) and other._h == self._h
+
+    def __hash__(self):
+        return hash(self._h)
+
+    def __del__(self):
+        if getattr(self, "_own", False) and self._h:
+            try:
+                from .framework import device_rt as rt
+                rt.lib().piamd_stream_destroy(self._h)  # frees once its queued work completes
+            except Exception:  # noqa: BLE001 (interpreter shutdown)
+                pass
+            self._h = None
+
+
+class _NativeEvent:
+    """``paddle.device.cuda.Event`` on a native HIP event (timing / blocking-sync flags)."""
+
+    def __init__(self, enable_timing=False, blocking=False, interprocess=False):
+        from .framework import device_rt as rt
+        h = ctypes.c_void_p()
+        rt.check(rt.lib().piamd_event_create(int(bool(enable_timing)), int(bool(blocking)),
+                                             ctypes.byref(h)), "hipEventCreate")
+        self.handle, self.enable_timing = h.value, bool(enable_timing)
+
+    def record(self, stream=None):
+        from .framework import device_rt as rt
+        h = (stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream)
+        rt.check(rt.lib().piamd_event_record(self.handle, h), "hipEventRecord")
+
+    def query(self) -> bool:
+        from .framework import device_rt as rt
+        r = rt.lib().piamd_event_query(self.handle)
+        if r < 0:
+            raise RuntimeError(f"hipEventQuery failed with hipError {-r}")
+        return r == 1
+
+    def synchronize(self):
+        from .framework import device_rt as rt
+        rt.check(rt.lib().piamd_event_sync(self.handle), "hipEventSynchronize")
+
+    def elapsed_time(self, end) -> float:
+        from .framework import device_rt as rt
+        ms = ctypes.c_float()
+        rt.check(rt.lib().piamd_event_elapsed(self.handle, end.handle, ctypes.byref(ms)),
+                 "hipEventElapsedTime")
+        return ms.value
+
+    def __del__(self):
+        if getattr(self, "handle", None):
+            try:
+                from .framework import device_rt as rt
+                rt.lib().piamd_event_destroy(self.handle)
+            except Exception:  # noqa: BLE001
+                pass
+            self.handle = None
+
+
+class _Props:
+    """Device properties from the native runtime (hipGetDeviceProperties), with the attribute
+    names of ``paddle.device.cuda.get_device_properties`` / torch's."""
+
+    def __init__(self, p):
+        self.name = p.name.decode()
+        self.gcnArchName = p.arch.decode()
+        self.major, self.minor = p.major, p.minor
+        self.multi_processor_count = p.cus
+        self.total_memory = p.total_mem
+        self.L2_cache_size = p.l2_bytes
+        self.shared_memory_per_block = p.lds_per_block
+        self.warp_size = p.warp
+        self.max_threads_per_block = p.max_threads_per_block
+        self.clock_rate_khz = p.clock_khz
+        self.memory_clock_rate_khz = p.mem_clock_khz
+        self.memory_bus_width = p.bus_width
+        self.pci_bus_id, self.pci_device_id, self.pci_domain_id = p.pci_bus, p.pci_dev, p.pci_domain
+        self.cooperative_launch = bool(p.cooperative)
+
+    def __repr__(self):
+        return (f"_gpuDeviceProperties(name='{self.name}', arch='{self.gcnArchName}', "
+                f"total_memory={self.total_memory // (1 << 20)}MB, "
+                f"multi_processor_count={self.multi_processor_count})")
+
+
+_SIDE: dict = {}
+
+
+def side_stream(device, priority=2, key="side"):
+    """A framework-owned side stream (native HIP stream from ``csrc/device``, cached per
+    (device, key)), returned as the ``torch.cuda.ExternalStream`` that ``torch.cuda.stream`` /
+    ``wait_stream`` / events take. priority 1 = the device's highest (collective streams: their
+    kernels are scheduled ahead of queued compute), 2 = normal. Falls back to a torch stream when
+    the native runtime is not built."""
+    dev = _parse(device) if not isinstance(device, torch.device) else device
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    k = (idx, key, int(priority))
+    ent = _SIDE.get(k)
+    if ent is None:
+        from .framework import device_rt as rt
+        if rt.available():
+            ent = _SIDE[k] = _NativeStream(torch.device("cuda", idx), priority)
+        else:
+            ent = _SIDE[k] = _NativeStream(_torch=torch.cuda.Stream(device=torch.device("cuda", idx)))
+    return ent.torch_stream
+
+
 class cuda:  # namespace paddle.device.cuda
-    Stream = torch.cuda.Stream if hasattr(torch.cuda, "Stream") else object
-    Event = torch.cuda.Event if hasattr(torch.cuda, "Event") else object
+    Stream = _NativeStream
+    Event = _NativeEvent
 
     @staticmethod
     def device_count():
@@ -156,15 +323,18 @@ class cuda:  # namespace paddle.device.cuda
     @staticmethod
     def synchronize(device=None):
         if torch.cuda.is_available():
-            torch.cuda.synchronize(_parse(device) if device is not None else None)
+            from .framework import device_rt as rt
+            idx = _parse(device).index if device is not None else None
+            rt.check(rt.lib().piamd_dev_synchronize(torch.cuda.current_device() if idx is None else idx),
+                     "hipDeviceSynchronize")
 
     @staticmethod
     def current_stream(device=None):
-        return torch.cuda.current_stream(_parse(device) if device is not None else None)
+        return _NativeStream(_torch=torch.cuda.current_stream(_parse(device) if device is not None else None))
 
     @staticmethod
     def stream_guard(stream):
-        return torch.cuda.stream(stream)
+        return torch.cuda.stream(stream.torch_stream if isinstance(stream, _NativeStream) else stream)
 
     @staticmethod
     def max_memory_allocated(device=None):
@@ -200,7 +370,21 @@ class cuda:  # namespace paddle.device.cuda
 
     @staticmethod
     def get_device_properties(device=None):
-        return torch.cuda.get_device_properties(_parse(device) if device is not None else 0)
+        from .framework import device_rt as rt
+        d = _parse(device) if device is not None else None
+        idx = d.index if d is not None and d.index is not None else (
+            torch.cuda.current_device() if torch.cuda.is_available() else 0)
+        return _Props(rt.props(idx))
+
+    @staticmethod
+    def mem_get_info(device=None):
+        """(free, total) bytes of the device (hipMemGetInfo)."""
+        from .framework import device_rt as rt
+        d = _parse(device) if device is not None else None
+        idx = d.index if d is not None and d.index is not None else torch.cuda.current_device()
+        f, t = ctypes.c_longlong(), ctypes.c_longlong()
+        rt.check(rt.lib().piamd_dev_mem_info(idx, ctypes.byref(f), ctypes.byref(t)), "hipMemGetInfo")
+        return f.value, t.value
 
     @staticmethod
     def get_device_name(device=None):

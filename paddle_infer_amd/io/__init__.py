@@ -190,7 +190,8 @@ class _DevicePrefetcher:
 
     def __init__(self, it, device, depth=2):
         self.it, self.device, self.depth = it, device, depth
-        self.stream = torch.cuda.Stream(device=device)
+        from ..device import side_stream
+        self.stream = side_stream(device, key="h2d_prefetch")
         self.q = []
 
     def _to(self, b):

@@ -83,7 +83,8 @@ class TokenDataLoader:
         self._cuda = self.device.type == "cuda"
         shape = (self.batch_size, self.seq_len + 1)
         if self._cuda:
-            self._stream = torch.cuda.Stream(device=self.device)
+            from ..device import side_stream
+            self._stream = side_stream(self.device, key="token_loader")
             # two pinned staging buffers: one may still be in flight while the other is filled
             self._pinned = [torch.empty(shape, dtype=torch.int64).pin_memory() for _ in range(2)]
             self._events = [None, None]

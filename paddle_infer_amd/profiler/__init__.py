@@ -4,10 +4,15 @@ Parity: reference `python/paddle/profiler/profiler.py` (Profiler:340, make_sched
 export_chrome_tracing:211, step_info:684, summary:830), `utils.py` (RecordEvent) and `timer.py`
 (the ips / reader_cost / batch_cost benchmark timer).
 
-MI355X design: host + device activity come from torch.profiler (kineto over roctracer on ROCm,
-i.e. the same HIP kernel records rocprofv3 sees); RecordEvent ranges are emitted both as profiler
-record_function scopes and as roctx ranges (visible to ``rocprofv3 --marker-trace``). Chrome
-traces open in Perfetto / chrome://tracing like the reference's.
+MI355X design: the framework's own tracer (``csrc/device/device.cc``, reference
+`fluid/platform/profiler/host_tracer.cc` + `chrometracing_logger.cc`) records every RecordEvent
+range natively — a per-thread append-only log, plus a HIP event pair per range on the current
+stream when the GPU target is on, resolved only at export — and writes them into the exported
+chrome trace (pid "host ranges" / "device ranges") and the summary's UDF view. Per-kernel device
+activity comes from roctracer through torch.profiler's kineto (the ROCm analogue of the
+reference's CUPTI tracer; ``tracer="native"`` skips it for a low-overhead ranges-only profile).
+RecordEvent ranges are also roctx ranges (``rocprofv3 --marker-trace``). Chrome traces open in
+Perfetto / chrome://tracing like the reference's.
 """
 from __future__ import annotations
 
@@ -126,6 +131,21 @@ def _roctx_pop():
         pass
 
 
+_NATIVE = {"on": False}
+
+
+def _native():
+    """The device-runtime library when the native tracer is recording, else None."""
+    if not _NATIVE["on"]:
+        return None
+    from ..framework import device_rt
+    return device_rt.lib()
+
+
+def _cur_stream():
+    return torch.cuda.current_stream().cuda_stream if torch.cuda.is_available() else None
+
+
 class RecordEvent:
     """User range: ``with RecordEvent("name"):`` or ``e.begin() ... e.end()``."""
 
@@ -133,8 +153,13 @@ class RecordEvent:
         self.name, self.event_type = name, event_type
         self._rf = None
         self._pushed = False
+        self._nat = False
 
     def begin(self):
+        L = _native()
+        if L is not None:
+            L.piamd_trace_push(self.name.encode(), _cur_stream())
+            self._nat = True
         self._rf = torch.profiler.record_function(self.name)
         self._rf.__enter__()
         self._pushed = torch.cuda.is_available() and _roctx_push(self.name)
@@ -146,6 +171,11 @@ class RecordEvent:
         if self._pushed:
             _roctx_pop()
             self._pushed = False
+        if self._nat:
+            L = _native()
+            if L is not None:
+                L.piamd_trace_pop(_cur_stream())
+            self._nat = False
 
     def __enter__(self):
         self.begin()
@@ -198,7 +228,7 @@ benchmark = _Timer
 class Profiler:
     def __init__(self, *, targets=None, scheduler=None, on_trace_ready=None, record_shapes=False,
                  profile_memory=False, timer_only=False, emit_nvtx=False, custom_device_types=None,
-                 with_flops=False):
+                 with_flops=False, tracer="both"):
         targets = list(targets or [ProfilerTarget.CPU] + ([ProfilerTarget.GPU] if torch.cuda.is_available() else []))
         self.targets = targets
         if scheduler is None:
@@ -217,6 +247,10 @@ class Profiler:
         self._prof = None
         self._state = ProfilerState.CLOSED
         self._last_events = None
+        # "both": native ranges + kineto kernel activity; "native": ranges only (no kineto)
+        self.tracer = tracer
+        self._native_trace = None  # path of the last native dump
+        self._native_open = False
 
     # -- torch profiler lifecycle ------------------------------------------------------------
     def _activities(self):
@@ -226,25 +260,48 @@ class Profiler:
         return acts
 
     def _open(self):
-        if self._prof is None and not self.timer_only:
+        if self.timer_only:
+            return
+        if not self._native_open:
+            from ..framework import device_rt
+            if device_rt.available():
+                dev = ProfilerTarget.GPU in self.targets and torch.cuda.is_available()
+                device_rt.lib().piamd_trace_enable(1, int(dev), _cur_stream() if dev else None)
+                _NATIVE["on"] = self._native_open = True
+        if self._prof is None and self.tracer != "native":
             self._prof = torch.profiler.profile(activities=self._activities(),
                                                 record_shapes=self.record_shapes,
                                                 profile_memory=self.profile_memory,
                                                 with_flops=self.with_flops)
             self._prof.__enter__()
 
+    def _close_native(self):
+        if not self._native_open:
+            return
+        import tempfile
+        from ..framework import device_rt
+        L = device_rt.lib()
+        L.piamd_trace_enable(0, 0, None)
+        _NATIVE["on"] = self._native_open = False
+        fd, path = tempfile.mkstemp(suffix=".native_trace.json")
+        os.close(fd)
+        L.piamd_trace_dump(path.encode(), 0)
+        self._native_trace = path
+
     def _close(self, deliver=True):
+        opened = self._prof is not None or self._native_open
+        self._close_native()
         if self._prof is not None:
             self._prof.__exit__(None, None, None)
             self._last_events = self._prof
             self._prof = None
-            if deliver and self.on_trace_ready is not None:
-                self.on_trace_ready(self)
+        if opened and deliver and self.on_trace_ready is not None:
+            self.on_trace_ready(self)
 
     def _apply(self, state):
         if state in (ProfilerState.RECORD, ProfilerState.RECORD_AND_RETURN, ProfilerState.READY):
             self._open()
-        elif self._prof is not None:
+        elif self._prof is not None or self._native_open:
             self._close()
         self._state = state
 
@@ -253,7 +310,7 @@ class Profiler:
         self._apply(self.scheduler(self.step_num))
 
     def stop(self):
-        if self._prof is not None:
+        if self._prof is not None or self._native_open:
             self._close()
         self._state = ProfilerState.CLOSED
 
@@ -261,10 +318,10 @@ class Profiler:
         self.timer.step(num_samples)
         prev = self._state
         self.step_num += 1
-        if prev == ProfilerState.RECORD_AND_RETURN and self._prof is not None:
+        if prev == ProfilerState.RECORD_AND_RETURN and (self._prof is not None or self._native_open):
             self._close()
         new = self.scheduler(self.step_num)
-        if new != prev or self._prof is None:
+        if new != prev or (self._prof is None and not self._native_open):
             self._apply(new)
 
     def step_info(self, unit=None):
@@ -278,31 +335,84 @@ class Profiler:
         self.stop()
 
     # -- results --------------------------------------------------------------------------
+    def native_events(self):
+        """The native tracer's events of the last recording (chrome-trace dicts: cat "host" /
+        "device")."""
+        if self._native_trace is None or not os.path.exists(self._native_trace):
+            return []
+        with open(self._native_trace) as f:
+            return json.load(f).get("traceEvents", [])
+
     def export(self, path="", format="json"):
         src = self._prof or self._last_events
-        if src is None:
+        nat = self.native_events()
+        if src is None and not nat:
             raise RuntimeError("no profiling data (record at least one step)")
         d = os.path.dirname(path)
         if d:
             os.makedirs(d, exist_ok=True)
-        src.export_chrome_trace(path)
+        if src is not None:
+            src.export_chrome_trace(path)
+            with open(path) as f:
+                doc = json.load(f)
+        else:
+            doc = {"traceEvents": [], "displayTimeUnit": "ms"}
+        # the native ranges on their own processes (names shown by the metadata events)
+        base = 1 << 20
+        for e in nat:
+            e = dict(e)
+            e["pid"] = base + (1 if e.get("cat") == "device" else 0)
+            doc.setdefault("traceEvents", []).append(e)
+        for off, label in ((0, "paddle host ranges"), (1, "paddle device ranges (HIP events)")):
+            doc["traceEvents"].append({"ph": "M", "name": "process_name", "pid": base + off,
+                                       "args": {"name": label}})
+        with open(path, "w") as f:
+            json.dump(doc, f)
 
     def summary(self, sorted_by=SortedKeys.CPUTotal, op_detail=True, thread_sep=False,
                 time_unit="ms", views=None, row_limit=40):
         src = self._prof or self._last_events
-        if src is None:
+        if src is None and not self.native_events():
             print(self.step_info())
             return ""
         key = {SortedKeys.CPUTotal: "cpu_time_total", SortedKeys.CPUAvg: "cpu_time",
                SortedKeys.CPUMax: "cpu_time_total", SortedKeys.CPUMin: "cpu_time",
                SortedKeys.GPUTotal: "device_time_total", SortedKeys.GPUAvg: "device_time",
                SortedKeys.GPUMax: "device_time_total", SortedKeys.GPUMin: "device_time"}[sorted_by]
-        try:
-            table = src.key_averages().table(sort_by=key, row_limit=row_limit)
-        except (KeyError, RuntimeError, AttributeError):
-            table = src.key_averages().table(row_limit=row_limit)
+        table = ""
+        if src is not None:
+            try:
+                table = src.key_averages().table(sort_by=key, row_limit=row_limit)
+            except (KeyError, RuntimeError, AttributeError):
+                table = src.key_averages().table(row_limit=row_limit)
+        udf = self._udf_table(time_unit)
+        table = table + ("\n" if table and udf else "") + udf
         print(table)
         return table
+
+    def _udf_table(self, time_unit="ms"):
+        """UDF view (reference summary ``SummaryView.UDFView``): per RecordEvent name, calls and
+        host / device time from the native tracer."""
+        nat = self.native_events()
+        if not nat:
+            return ""
+        scale = {"s": 1e-6, "ms": 1e-3, "us": 1.0, "ns": 1e3}.get(time_unit, 1e-3)
+        agg = {}
+        for e in nat:
+            a = agg.setdefault(e["name"], {"calls": 0, "host": 0.0, "dev": 0.0, "ndev": 0})
+            if e.get("cat") == "device":
+                a["dev"] += e["dur"]
+                a["ndev"] += 1
+            else:
+                a["calls"] += 1
+                a["host"] += e["dur"]
+        rows = [f"{'UDF range':40s} {'calls':>7s} {'host total':>12s} {'host avg':>10s} "
+                f"{'device total':>13s} {'device avg':>11s}   ({time_unit})"]
+        for name, a in sorted(agg.items(), key=lambda kv: -kv[1]["host"]):
+            n, nd = max(a["calls"], 1), max(a["ndev"], 1)
+            rows.append(f"{name[:40]:40s} {a['calls']:7d} {a['host'] * scale:12.4f} {a['host'] * scale / n:10.4f} "
+                        f"{a['dev'] * scale:13.4f} {a['dev'] * scale / nd:11.4f}")
+        return "\n".join(rows)
 
 
 def load_profiler_result(filename: str):

@@ -10,7 +10,8 @@ instruction scheduling with those events), plus the data-parallel gradient all-r
 * The plan (`csrc/runtime/scheduler.cc` ``piamd_stream_plan``) assigns stream 0 (compute) / 1
   (communication) and, per op, the minimal set of cross-stream events to wait on: the latest
   predecessor of the other stream, skipped when that stream already waited on it or a later one.
-* On a GPU the communication ops run under a dedicated HIP stream (``torch.cuda.Stream``): RCCL
+* On a GPU the communication ops run under a dedicated high-priority HIP stream (native, from
+  ``csrc/device`` via ``device.side_stream``): RCCL
   is enqueued behind the events of the compute work that produced its inputs, the compute stream
   only waits where a consumer needs the result, and the allocator is told about cross-stream use
   (``record_stream``) so the executor's early frees stay safe.
@@ -100,15 +101,10 @@ class StreamRunner:
         self.pending = {}  # op index → async Work (CPU / gloo path)
         self.issued_on = {}  # op index → stream id, for tests / introspection
         if self.cuda:
+            from ..device import side_stream
             self.compute = torch.cuda.current_stream(device)
-            key = "_piamd_comm_stream"
-            dev_obj = torch.cuda.device(device)
-            st = getattr(StreamRunner, key, {})
-            if device.index not in st:
-                with dev_obj:
-                    st[device.index] = torch.cuda.Stream(device=device)
-                setattr(StreamRunner, key, st)
-            self.comm = st[device.index]
+            # native high-priority HIP stream: collectives are scheduled ahead of queued compute
+            self.comm = side_stream(device, priority=1, key="static_comm")
 
     def run(self, pos, oi, op, run_fn, env):
         s = self.stream_of[oi]

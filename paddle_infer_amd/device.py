@@ -413,3 +413,24 @@ def _own_stats(device):
     else:
         d = getattr(_parse(device), "index", 0) or 0
     return _a.stats(d)
+
+
+# paddle.device-level stream API (reference python/paddle/device/__init__.py: Stream, Event,
+# current_stream, set_stream, stream_guard) on the native runtime
+Stream = _NativeStream
+Event = _NativeEvent
+
+
+def current_stream(device=None):
+    return cuda.current_stream(device)
+
+
+def set_stream(stream):
+    """Make ``stream`` the current stream of its device; returns the previous one."""
+    prev = cuda.current_stream(stream.device if isinstance(stream, _NativeStream) else None)
+    torch.cuda.set_stream(stream.torch_stream if isinstance(stream, _NativeStream) else stream)
+    return prev
+
+
+def stream_guard(stream):
+    return cuda.stream_guard(stream)

@@ -66,6 +66,8 @@ _SIGS = {
     # bits, x, ldx, wp, scale, bias, y, ldy, ws, cnt, M, N, K, KS, act, stream
     "piamd_wo_gemm": [c_int, c_void_p, c_ll, c_void_p, c_void_p, c_void_p, c_void_p, c_ll,
                       c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "piamd_conv_wprep": [c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                         c_int, c_int, c_void_p],
     "piamd_wo_gemm_ex": [c_int, c_void_p, c_ll, c_void_p, c_void_p, c_void_p, c_void_p, c_ll,
                          c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                          c_void_p, c_float, c_void_p, c_ll, c_void_p],

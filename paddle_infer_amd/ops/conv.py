@@ -24,6 +24,8 @@ Routes (``conv2d_any``, called by ``nn.functional.conv2d`` for GPU tensors):
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
@@ -273,8 +275,10 @@ class _Conv2dNHWC(torch.autograd.Function):
         dt = x.dtype
         K0, C0, R, S = weight.shape
         K = -(-K0 // 4) * 4  # the epilogue stores 4 output channels per lane
-        wq0 = weight.to(dt)
-        wq = wq0 if K == K0 else torch.nn.functional.pad(wq0, (0, 0, 0, 0, 0, 0, 0, K - K0))
+        prep = (C0 > 8 and st == (1, 1) and _wprep_ok(x, weight)
+                and _out_hw(x.shape[1], x.shape[2], R, S, st, pad, dil) == tuple(x.shape[1:3]))
+        wq0 = weight if prep else weight.to(dt)  # the prep path casts inside its own kernel
+        wq = wq0 if (K == K0 or prep) else torch.nn.functional.pad(wq0, (0, 0, 0, 0, 0, 0, 0, K - K0))
         b = None if bias is None else _padc(bias.to(dt), K)
         if C0 <= 8:  # stem mode: zero-pad the image channels to 8
             xc = _padc(x, 8).contiguous()
@@ -285,13 +289,32 @@ class _Conv2dNHWC(torch.autograd.Function):
         else:  # channels zero-padded to a multiple of 64 (one k-step never straddles two taps)
             C = _pad64(C0)
             xc = _padc(x, C).contiguous()
-            w_ohwi = _padc(wq.permute(0, 2, 3, 1), C).contiguous()
+            w_t = None
+            if prep:
+                # ONE launch: master filter → forward OHWI operand + the stride-1 data gradient's
+                # flipped [C][R][S][Kp] operand (no cast / permute / flip kernels in either pass)
+                Kp = _pad64(K0)
+                w_ohwi = torch.empty(K, R, S, C, dtype=dt, device=x.device)
+                w_t = torch.empty(C, R, S, Kp, dtype=dt, device=x.device) if ctx.needs_input_grad[0] else None
+                wc = weight.detach().contiguous()
+                _lib.call("piamd_conv_wprep", _WSRC[wc.dtype], _f16(x), wc.data_ptr(), w_ohwi.data_ptr(),
+                          _lib.ptr(w_t), K0, C0, R, S, K, C, Kp, _lib.stream())
+            else:
+                w_ohwi = _padc(wq.permute(0, 2, 3, 1), C).contiguous()
             y = _launch(xc, w_ohwi, b, st, pad, dil, act)
+            if prep:
+                if K != K0:
+                    y = y[..., :K0].contiguous()
+                ctx.save_for_backward(xc, w_t, y if act else None)
+                ctx.cfg = (st, pad, dil, act, bias is not None, weight.dtype)
+                ctx.wshape = (K0, C0, R, S)
+                return y
         if K != K0:
             y = y[..., :K0].contiguous()
         # the half-precision weight is kept for the backward (no second cast of the master weight)
         ctx.save_for_backward(xc, wq0, y if act else None)
         ctx.cfg = (st, pad, dil, act, bias is not None, weight.dtype)
+        ctx.wshape = None
         return y
 
     @staticmethod
@@ -303,6 +326,8 @@ class _Conv2dNHWC(torch.autograd.Function):
         if act == 3:
             dy = dy * (y > 0)
         dy = dy.contiguous()
+        if ctx.wshape is not None:  # filter prepared in forward (stride 1, same size)
+            return _Conv2dNHWC._backward_prepped(ctx, x, wq, dy)
         K0, C0, R, S = wq.shape
         C = x.shape[-1]  # == C0, or C0 zero-padded (to 8 in stem mode, else to a multiple of 64)
         N, H, W, _ = x.shape
@@ -330,6 +355,40 @@ class _Conv2dNHWC(torch.autograd.Function):
         if has_bias and ctx.needs_input_grad[2]:
             db = dy.float().sum((0, 1, 2)).to(wdt)
         return dx, dw, db, None, None, None, None
+
+    @staticmethod
+    def _backward_prepped(ctx, x, w_t, dy):
+        st, pad, dil, act, has_bias, wdt = ctx.cfg
+        K0, C0, R, S = ctx.wshape
+        C = x.shape[-1]
+        N, H, W, _ = x.shape
+        M = dy.shape[0] * dy.shape[1] * dy.shape[2]
+        Kp = _pad64(K0)
+        dyp = _padc(dy, Kp)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            pad_t = (dil[0] * (R - 1) - pad[0], dil[1] * (S - 1) - pad[1])
+            dx = _launch_geom(dyp, w_t, (1, 1), pad_t, dil, H, W)
+            dx = dx[..., :C0] if C != C0 else dx
+        if ctx.needs_input_grad[1]:
+            if wgrad_eligible(C, Kp, M):
+                dw = conv2d_wgrad(x, dyp, R, S, st, pad, dil)[:K0, :C0]
+            else:
+                dw = _direct_wgrad(x[..., :C0].contiguous(), dy, R, S, st, pad, dil, C0, K0)
+            dw = dw.to(wdt)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = dy.float().sum((0, 1, 2)).to(wdt)
+        return dx, dw, db, None, None, None, None
+
+
+_WSRC = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+WPREP = os.environ.get("PIAMD_CONV_WPREP", "1") != "0"
+
+
+def _wprep_ok(x, weight):
+    """One-launch filter preparation (``conv_wprep.hip``) for this conv's weight."""
+    return (WPREP and x.is_cuda and weight.is_cuda and weight.dim() == 4 and weight.dtype in _WSRC
+            and x.dtype in (torch.bfloat16, torch.float16) and _lib.has("piamd_conv_wprep"))
 
 
 # ------------------------------------------------------------------------- dense fp32 (split bf16)

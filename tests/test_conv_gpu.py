@@ -152,3 +152,33 @@ def test_resnet18_every_conv_layer_matches_fp32():
         yr.backward(g)
         _close(xh.grad, xr.grad, 3e-2)
         _close(wh.grad, wr.grad, 3e-2)
+
+
+@pytest.mark.parametrize("wdtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("K0,C0,R,pad", [(64, 64, 3, 1), (100, 72, 3, 1), (256, 64, 1, 0), (36, 130, 3, 1)])
+def test_conv_filter_prep_matches_cast_path(wdtype, K0, C0, R, pad):
+    """Stride-1 convs prepare their filter in ONE launch (conv_wprep.hip: OHWI forward operand +
+    flipped data-gradient operand): forward / dX / dW identical to the cast + permute + flip path,
+    and both against fp32 torch."""
+    from paddle_infer_amd.ops import conv as C
+    torch.manual_seed(K0 + C0)
+    x = torch.randn(2, 9, 11, C0, device="cuda").bfloat16()
+    w = (torch.randn(K0, C0, R, R, device="cuda") * 0.05).to(wdtype)
+    g = torch.randn(2, 9, 11, K0, device="cuda").bfloat16()
+    outs = []
+    for prep in (True, False):
+        C.WPREP = prep
+        try:
+            xi = x.clone().requires_grad_(True)
+            wi = w.clone().requires_grad_(True)
+            y = C._Conv2dNHWC.apply(xi, wi, None, (1, 1), (pad, pad), (1, 1), 0)
+            dx, dw = torch.autograd.grad(y, (xi, wi), g)
+            outs.append((y.float(), dx.float(), dw.float()))
+        finally:
+            C.WPREP = True
+    for a, b in zip(*outs):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = w.float().bfloat16().float().requires_grad_(True)
+    yr = torch.nn.functional.conv2d(xr, wr, padding=pad)
+    torch.testing.assert_close(outs[0][0].permute(0, 3, 1, 2), yr, rtol=2e-2, atol=2e-2)

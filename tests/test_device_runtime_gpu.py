@@ -68,3 +68,16 @@ def test_static_comm_stream_is_native():
     from paddle_infer_amd.device import side_stream, _SIDE
     s = side_stream(torch.device("cuda", 0), priority=1, key="static_comm")
     assert any(v.torch_stream is s and v._own for v in _SIDE.values())
+
+
+def test_device_level_stream_api():
+    import paddle_infer_amd as paddle
+    s = paddle.device.Stream(priority=1)
+    prev = paddle.device.set_stream(s)
+    try:
+        assert paddle.device.current_stream().cuda_stream == s.cuda_stream
+        y = torch.ones(8, device="cuda") * 3
+    finally:
+        paddle.device.set_stream(prev)
+    s.synchronize()
+    assert float(y.sum()) == 24.0 and paddle.device.current_stream().cuda_stream == prev.cuda_stream

@@ -108,6 +108,8 @@ def _parse(dev) -> torch.device:
         return dev
     if isinstance(dev, Place):
         return dev.torch_device()
+    if isinstance(dev, int):  # a device ordinal (paddle.device.cuda.* accept ints)
+        return torch.device("cuda", dev)
     s = str(dev).lower()
     if s == "cpu":
         return torch.device("cpu")

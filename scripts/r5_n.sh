@@ -10,3 +10,5 @@ for P in 1 0; do
   PIAMD_CONV_WPREP=$P timeout -k 10 300 python3 tools/bench_resnet.py --model resnet50 --steps 20 > $OUT/rn50_prep$P.log 2>&1 || { echo "bench failed"; tail -20 $OUT/rn50_prep$P.log; exit 1; }
   echo "prep=$P $(grep '^{' $OUT/rn50_prep$P.log | tail -2 | cut -c1-250)"
 done
+timeout -k 10 300 python3 tools/trace_aten_step.py > $OUT/aten_rn50.txt 2>&1 || { echo "aten trace failed"; tail -20 $OUT/aten_rn50.txt; exit 1; }
+head -40 $OUT/aten_rn50.txt

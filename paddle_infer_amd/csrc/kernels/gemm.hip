@@ -607,7 +607,7 @@ __global__ __launch_bounds__(NTHR, 1) void conv_wgrad_kernel(
 template <int SL>
 __global__ __launch_bounds__(256) void wgrad_splitk_finish(const float* __restrict__ ws, int ksplit,
                                                            long long MN, float* __restrict__ d,
-                                                           int accumulate) {
+                                                           int accumulate, int Kout) {
   constexpr int VPB = 256 / SL;  // output vectors per block
   const int t = threadIdx.x, vl = t % VPB, sl = t / VPB;
   const long long i = ((long long)blockIdx.x * VPB + vl) * 4;
@@ -622,6 +622,16 @@ __global__ __launch_bounds__(256) void wgrad_splitk_finish(const float* __restri
     for (int k = 1; k < SL; ++k) v += red[k * VPB + vl];
   }
   if (i >= MN) return;
+  if (accumulate & 2) {  // OHWI output d[k][rsc] (a channels_last [K][C][R][S] filter gradient)
+    const long long RSC = MN / Kout, rsc = i / Kout;
+    const int k = (int)(i - rsc * Kout);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float* o = d + (long long)(k + j) * RSC + rsc;
+      *o = (accumulate & 1) ? *o + v[j] : v[j];
+    }
+    return;
+  }
   f32x4* o = reinterpret_cast<f32x4*>(d + i);
   if (accumulate) v += *o;
   *o = v;
@@ -841,9 +851,11 @@ PIAMD_EXPORT int piamd_conv2d_fwd(const void* x, const void* wt, const void* zer
 }
 
 // NHWC implicit-GEMM convolution weight gradient: x [N][H][W][C], dy [N][OH][OW][Kout] 16-bit
-// (bf16, or fp16 when f16 != 0) → d [R][S][C][Kout] f32 (HWIO; accumulate adds into d). zero: ≥ 16
-// zero bytes. C % 8 == 0, Kout % tile_n == 0 (tile_n ∈ {64, 128, 256}), N·OH·OW < 2^24; ksplit > 1
-// needs ws with ksplit·R·S·C·Kout floats (ksplit == 1 writes d directly, requires accumulate == 0).
+// (bf16, or fp16 when f16 != 0) → d [R][S][C][Kout] f32 (HWIO; accumulate bit 0 adds into d;
+// bit 1: d is OHWI [Kout][R][S][C] instead — the channels_last layout of a [K][C][R][S] filter, so
+// the gradient lands in the parameter's own layout; needs ksplit > 1). zero: ≥ 16 zero bytes.
+// C % 8 == 0, Kout % tile_n == 0 (tile_n ∈ {64, 128, 256}), N·OH·OW < 2^24; ksplit > 1 needs ws
+// with ksplit·R·S·C·Kout floats (ksplit == 1 writes d directly, requires accumulate == 0).
 PIAMD_EXPORT int piamd_conv2d_wgrad(const void* x, const void* dy, const void* zero, float* d, int N,
                                     int H, int W, int C, int OH, int OW, int R, int S, int st_h,
                                     int st_w, int pad_h, int pad_w, int dil_h, int dil_w, int Kout,
@@ -881,13 +893,13 @@ PIAMD_EXPORT int piamd_conv2d_wgrad(const void* x, const void* dy, const void* z
     const long long nv = MN / 4;
     if (ksplit >= 64 && nv < 65536)
       hipLaunchKernelGGL(wgrad_splitk_finish<16>, dim3((unsigned)((nv + 15) / 16)), dim3(256), 0, st,
-                         (const float*)ws, ksplit, MN, d, accumulate);
+                         (const float*)ws, ksplit, MN, d, accumulate, Kout);
     else if (ksplit >= 8 && nv < 262144)
       hipLaunchKernelGGL(wgrad_splitk_finish<4>, dim3((unsigned)((nv + 63) / 64)), dim3(256), 0, st,
-                         (const float*)ws, ksplit, MN, d, accumulate);
+                         (const float*)ws, ksplit, MN, d, accumulate, Kout);
     else
       hipLaunchKernelGGL(wgrad_splitk_finish<1>, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st,
-                         (const float*)ws, ksplit, MN, d, accumulate);
+                         (const float*)ws, ksplit, MN, d, accumulate, Kout);
   }
   return (int)hipGetLastError();
 }

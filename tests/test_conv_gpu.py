@@ -182,3 +182,23 @@ def test_conv_filter_prep_matches_cast_path(wdtype, K0, C0, R, pad):
     wr = w.float().bfloat16().float().requires_grad_(True)
     yr = torch.nn.functional.conv2d(xr, wr, padding=pad)
     torch.testing.assert_close(outs[0][0].permute(0, 3, 1, 2), yr, rtol=2e-2, atol=2e-2)
+
+
+def test_conv_wgrad_in_channels_last_param_layout():
+    """A channels_last filter parameter receives its gradient already in that layout (split-K
+    finish writes OHWI): same values as the HWIO path and no relayout copy by AccumulateGrad."""
+    from paddle_infer_amd.ops import conv as C
+    torch.manual_seed(7)
+    x = torch.randn(4, 14, 14, 128, device="cuda").bfloat16()
+    w0 = torch.randn(256, 128, 3, 3, device="cuda") * 0.05
+    g = torch.randn(4, 14, 14, 256, device="cuda").bfloat16()
+    grads = []
+    for cl in (True, False):
+        w = torch.nn.Parameter(w0.clone().contiguous(memory_format=torch.channels_last) if cl else w0.clone())
+        y = C._Conv2dNHWC.apply(x, w, None, (1, 1), (1, 1), (1, 1), 0)
+        y.backward(g)
+        if cl:
+            assert w.grad.is_contiguous(memory_format=torch.channels_last)
+        grads.append(w.grad.float())
+    # the split-K factor may differ (OHWI needs a split plan): summation order only
+    torch.testing.assert_close(grads[0], grads[1], rtol=1e-4, atol=1e-4)

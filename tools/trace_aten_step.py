@@ -35,6 +35,9 @@ class _Rec(TorchDispatchMode):
         if dev and name not in _NOKERNEL:
             fr = [f for f in traceback.extract_stack() if "paddle_infer_amd" in f.filename][-2:]
             where = " <- ".join(f"{f.filename.split('paddle_infer_amd/')[-1]}:{f.lineno}" for f in reversed(fr))
+            if not where:  # no framework frame (autograd engine): show the operands instead
+                where = "; ".join(f"{tuple(a.shape)}/{a.stride()}/{str(a.dtype)[6:]}" for a in args
+                                  if isinstance(a, torch.Tensor))[:150]
             self.cnt[(name, where)] += 1
         return out
 

@@ -607,7 +607,7 @@ __global__ __launch_bounds__(NTHR, 1) void conv_wgrad_kernel(
 template <int SL>
 __global__ __launch_bounds__(256) void wgrad_splitk_finish(const float* __restrict__ ws, int ksplit,
                                                            long long MN, float* __restrict__ d,
-                                                           int accumulate, int Kout) {
+                                                           int accumulate, int Kout, int C) {
   constexpr int VPB = 256 / SL;  // output vectors per block
   const int t = threadIdx.x, vl = t % VPB, sl = t / VPB;
   const long long i = ((long long)blockIdx.x * VPB + vl) * 4;
@@ -622,12 +622,17 @@ __global__ __launch_bounds__(256) void wgrad_splitk_finish(const float* __restri
     for (int k = 1; k < SL; ++k) v += red[k * VPB + vl];
   }
   if (i >= MN) return;
-  if (accumulate & 2) {  // OHWI output d[k][rsc] (a channels_last [K][C][R][S] filter gradient)
+  if (accumulate & 6) {  // OHWI d[k][rsc] (channels_last filter) or KCRS d[k][c][rs] (contiguous)
     const long long RSC = MN / Kout, rsc = i / Kout;
     const int k = (int)(i - rsc * Kout);
+    long long off = rsc;
+    if (accumulate & 4) {  // rsc = rs·C + c  →  c·RS + rs
+      const long long rs = rsc / C, c = rsc - rs * C;
+      off = c * (RSC / C) + rs;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      float* o = d + (long long)(k + j) * RSC + rsc;
+      float* o = d + (long long)(k + j) * RSC + off;
       *o = (accumulate & 1) ? *o + v[j] : v[j];
     }
     return;
@@ -852,8 +857,9 @@ PIAMD_EXPORT int piamd_conv2d_fwd(const void* x, const void* wt, const void* zer
 
 // NHWC implicit-GEMM convolution weight gradient: x [N][H][W][C], dy [N][OH][OW][Kout] 16-bit
 // (bf16, or fp16 when f16 != 0) → d [R][S][C][Kout] f32 (HWIO; accumulate bit 0 adds into d;
-// bit 1: d is OHWI [Kout][R][S][C] instead — the channels_last layout of a [K][C][R][S] filter, so
-// the gradient lands in the parameter's own layout; needs ksplit > 1). zero: ≥ 16 zero bytes.
+// bit 1: d is OHWI [Kout][R][S][C] instead — the channels_last layout of a [K][C][R][S] filter —
+// bit 2: d is KCRS [Kout][C][R][S] — a contiguous filter — so the gradient lands in the
+// parameter's own layout; bits 1-2 need ksplit > 1). zero: ≥ 16 zero bytes.
 // C % 8 == 0, Kout % tile_n == 0 (tile_n ∈ {64, 128, 256}), N·OH·OW < 2^24; ksplit > 1 needs ws
 // with ksplit·R·S·C·Kout floats (ksplit == 1 writes d directly, requires accumulate == 0).
 PIAMD_EXPORT int piamd_conv2d_wgrad(const void* x, const void* dy, const void* zero, float* d, int N,
@@ -893,13 +899,13 @@ PIAMD_EXPORT int piamd_conv2d_wgrad(const void* x, const void* dy, const void* z
     const long long nv = MN / 4;
     if (ksplit >= 64 && nv < 65536)
       hipLaunchKernelGGL(wgrad_splitk_finish<16>, dim3((unsigned)((nv + 15) / 16)), dim3(256), 0, st,
-                         (const float*)ws, ksplit, MN, d, accumulate, Kout);
+                         (const float*)ws, ksplit, MN, d, accumulate, Kout, C);
     else if (ksplit >= 8 && nv < 262144)
       hipLaunchKernelGGL(wgrad_splitk_finish<4>, dim3((unsigned)((nv + 63) / 64)), dim3(256), 0, st,
-                         (const float*)ws, ksplit, MN, d, accumulate, Kout);
+                         (const float*)ws, ksplit, MN, d, accumulate, Kout, C);
     else
       hipLaunchKernelGGL(wgrad_splitk_finish<1>, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st,
-                         (const float*)ws, ksplit, MN, d, accumulate, Kout);
+                         (const float*)ws, ksplit, MN, d, accumulate, Kout, C);
   }
   return (int)hipGetLastError();
 }

@@ -161,20 +161,24 @@ def wgrad_eligible(C, K, M) -> bool:
     return C % 8 == 0 and K % 64 == 0 and M < (1 << 24)
 
 
-def conv2d_wgrad(x, dy, R, S, st, pad, dil, ohwi=False):
+def conv2d_wgrad(x, dy, R, S, st, pad, dil, layout=None):
     """dW [K][C][R][S] f32 of conv(x [N,H,W,C], ·) given dy [N,OH,OW,K] (both bf16 or both fp16,
-    NHWC contiguous) on the HIP implicit-GEMM weight-gradient kernel. ``ohwi``: the gradient is
-    stored [K][R][S][C] — the channels_last layout of a channels_last filter parameter, so autograd
-    adopts it as ``.grad`` without a relayout copy (the split-K finish writes it transposed; only
-    split plans then)."""
+    NHWC contiguous) on the HIP implicit-GEMM weight-gradient kernel. ``layout`` "kcrs" / "ohwi":
+    the gradient is stored in the filter parameter's own memory layout (contiguous / channels_last),
+    so autograd adopts it as ``.grad`` without a relayout copy (the split-K finish writes it
+    permuted; only split plans then); None: HWIO storage."""
     N, H, W, C = x.shape
     _, OH, OW, K = dy.shape
     M, RSC = N * OH * OW, R * S * C
     if not wgrad_eligible(C, K, M):
         raise ValueError(f"conv2d_wgrad: unsupported C={C} K={K} M={M}")
     nk = -(-M // 64)
-    ohwi = ohwi and nk >= 4
-    d = torch.empty((K, R, S, C) if ohwi else (R, S, C, K), dtype=torch.float32, device=x.device)
+    if nk < 4:
+        layout = None
+    ohwi = layout is not None
+    shape = {"ohwi": (K, R, S, C), "kcrs": (K, C, R, S)}.get(layout, (R, S, C, K))
+    d = torch.empty(shape, dtype=torch.float32, device=x.device)
+    mode = {"ohwi": 2, "kcrs": 4}.get(layout, 0)
 
     def run(plan):
         tn, ks = plan
@@ -182,7 +186,7 @@ def conv2d_wgrad(x, dy, R, S, st, pad, dil, ohwi=False):
         ws = torch.empty(ks * RSC * K, dtype=torch.float32, device=x.device) if ks > 1 else None
         _lib.call("piamd_conv2d_wgrad", x.data_ptr(), dy.data_ptr(), _zero(x.device).data_ptr(),
                   d.data_ptr(), N, H, W, C, OH, OW, R, S, st[0], st[1], pad[0], pad[1], dil[0],
-                  dil[1], K, tn, ks, _lib.ptr(ws), 2 if ohwi else 0, _f16(x), _lib.stream())
+                  dil[1], K, tn, ks, _lib.ptr(ws), mode, _f16(x), _lib.stream())
     default = _wgrad_plan(M, RSC, K)
     if ohwi:
         default = (default[0], max(4, default[1]))
@@ -190,9 +194,11 @@ def conv2d_wgrad(x, dy, R, S, st, pad, dil, ohwi=False):
              for ks in ((4, 16, 64, 256) if ohwi else (1, 4, 16, 64, 256))
              if ks <= nk and ks * RSC * K * 4 <= (256 << 20)]
     plan = WGRAD_PLAN_OVERRIDE or _autotuned("conv2d_wgrad", (N, H, W, C, K, R, S, st, pad, dil)
-                                             + (("ohwi",) if ohwi else ()), default, cands, run)
+                                             + (("perm",) if ohwi else ()), default, cands, run)
     run(plan)
-    return d.permute(0, 3, 1, 2) if ohwi else d.permute(3, 2, 0, 1)
+    if layout == "kcrs":
+        return d
+    return d.permute(0, 3, 1, 2) if layout == "ohwi" else d.permute(3, 2, 0, 1)
 
 
 def _phase_taps(R, st, pad, dil, ph):
@@ -284,9 +290,9 @@ class _Conv2dNHWC(torch.autograd.Function):
         K = -(-K0 // 4) * 4  # the epilogue stores 4 output channels per lane
         prep = (C0 > 8 and st == (1, 1) and _wprep_ok(x, weight)
                 and _out_hw(x.shape[1], x.shape[2], R, S, st, pad, dil) == tuple(x.shape[1:3]))
-        # a channels_last filter parameter gets its gradient in that layout (no AccumulateGrad copy)
-        ctx.w_cl = (weight.dim() == 4 and not weight.is_contiguous()
-                    and weight.is_contiguous(memory_format=torch.channels_last))
+        # the filter gradient is produced in the parameter's own layout (no AccumulateGrad copy)
+        ctx.w_layout = ("kcrs" if weight.is_contiguous() else
+                        "ohwi" if weight.is_contiguous(memory_format=torch.channels_last) else None)
         wq0 = weight if prep else weight.to(dt)  # the prep path casts inside its own kernel
         wq = wq0 if (K == K0 or prep) else torch.nn.functional.pad(wq0, (0, 0, 0, 0, 0, 0, 0, K - K0))
         b = None if bias is None else _padc(bias.to(dt), K)
@@ -358,7 +364,7 @@ class _Conv2dNHWC(torch.autograd.Function):
             dx = dx[..., :C0] if C != C0 else dx
         if ctx.needs_input_grad[1]:
             if wgrad_eligible(C, Kp, M):
-                dw = conv2d_wgrad(x, dyp, R, S, st, pad, dil, ohwi=ctx.w_cl)[:K0, :C0]
+                dw = conv2d_wgrad(x, dyp, R, S, st, pad, dil, layout=ctx.w_layout)[:K0, :C0]
             else:  # > 2^24 output pixels: the direct kernel's pixel-chunked reduction
                 dw = _direct_wgrad(x[..., :C0].contiguous(), dy, R, S, st, pad, dil, C0, K0)
             dw = dw.to(wdt)
@@ -382,7 +388,7 @@ class _Conv2dNHWC(torch.autograd.Function):
             dx = dx[..., :C0] if C != C0 else dx
         if ctx.needs_input_grad[1]:
             if wgrad_eligible(C, Kp, M):
-                dw = conv2d_wgrad(x, dyp, R, S, st, pad, dil, ohwi=ctx.w_cl)[:K0, :C0]
+                dw = conv2d_wgrad(x, dyp, R, S, st, pad, dil, layout=ctx.w_layout)[:K0, :C0]
             else:
                 dw = _direct_wgrad(x[..., :C0].contiguous(), dy, R, S, st, pad, dil, C0, K0)
             dw = dw.to(wdt)

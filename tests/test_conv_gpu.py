@@ -197,8 +197,8 @@ def test_conv_wgrad_in_channels_last_param_layout():
         w = torch.nn.Parameter(w0.clone().contiguous(memory_format=torch.channels_last) if cl else w0.clone())
         y = C._Conv2dNHWC.apply(x, w, None, (1, 1), (1, 1), (1, 1), 0)
         y.backward(g)
-        if cl:
-            assert w.grad.is_contiguous(memory_format=torch.channels_last)
+        # the gradient arrives in the parameter's layout (channels_last / contiguous)
+        assert w.grad.is_contiguous(memory_format=torch.channels_last if cl else torch.contiguous_format)
         grads.append(w.grad.float())
     # the split-K factor may differ (OHWI needs a split plan): summation order only
     torch.testing.assert_close(grads[0], grads[1], rtol=1e-4, atol=1e-4)

@@ -237,6 +237,24 @@ class _Linear:
     small-M (decode) calls, where the GEMM is a weight stream (see ops.inference.pack_bf16)."""
     __slots__ = ("w", "scale", "bits", "trans", "packed", "act_scale")
     PACKED_MAX_M = 64
+    # serving batches with short K: the skinny MFMA GEMM on the K-contiguous weight beats the packed
+    # weight stream from 8 rows (M=32 QKV 14.7 -> 11.5 us, out-proj 8.8 -> 6.5; K = 8192 stays on
+    # the packed GEMV: profiles/decode_linear_r5.txt)
+    DENSE_MIN_M, DENSE_MAX_K = 8, 2048
+
+    def _packed_for(self, M, K):
+        return (self.packed is not None and M <= self.PACKED_MAX_M
+                and not (M >= self.DENSE_MIN_M and K <= self.DENSE_MAX_K))
+
+    def _dense_epilogue(self, x, bias, act, resid):
+        """act(x·W + bias) + resid as ONE own GEMM (bias / activation / residual in the epilogue)."""
+        from ...ops.gemm import gemm_nt
+        from ...ops.linear import transposed
+        x2 = x.reshape(-1, x.shape[-1])
+        wk = self.w if self.trans else transposed(self.w)
+        r2 = resid.reshape(x2.shape[0], -1) if resid is not None else None
+        y = gemm_nt(x2.contiguous(), wk, bias=bias, act=act, resid=r2)
+        return y.reshape(*x.shape[:-1], y.shape[-1])
 
     def __init__(self, w, scale=None, bits=0, trans=False, packed=None, act_scale=None):
         self.w, self.scale, self.bits, self.trans, self.packed = w, scale, bits, trans, packed
@@ -263,10 +281,13 @@ class _Linear:
                 return _inf.weight_only_linear(x, self.w, bias, self.scale,
                                                "int4" if self.bits == 4 else "int8", act, ln=ln,
                                                resid=resid)
-            if self.packed is not None and x.is_cuda and M <= self.PACKED_MAX_M:
+            if x.is_cuda and self._packed_for(M, x.shape[-1]):
                 return _inf.packed_linear(x, self.packed, bias, act, ln=ln, resid=resid)
             if ln is not None:
                 x = ops.layer_norm(x, ln[0], ln[1], ln[2])
+            if (x.is_cuda and self.packed is not None and x.dtype == self.w.dtype
+                    and act in ("none", "gelu", "gelu_tanh", "relu")):
+                return self._dense_epilogue(x, bias, act, resid)
             y = self(x, bias, act)
             return y + resid.reshape(y.shape) if resid is not None else y
         if self.bits == -8:  # int8 x int8 MFMA GEMM, dequantising epilogue (FusedMultiTransformerINT8)
@@ -274,7 +295,7 @@ class _Linear:
         if self.bits:
             return _inf.weight_only_linear(x, self.w, bias, self.scale,
                                            "int4" if self.bits == 4 else "int8", act)
-        if self.packed is not None and x.is_cuda and x.numel() // x.shape[-1] <= self.PACKED_MAX_M:
+        if x.is_cuda and self._packed_for(x.numel() // x.shape[-1], x.shape[-1]):
             return _inf.packed_linear(x, self.packed, bias, act)
         from ...ops.linear import linear as _dense, linear_bias_act
         if act != "none" and bias is not None:  # one epilogue GEMM when eligible (inference)

@@ -475,15 +475,31 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
           for (int i = 0; i < 8; ++i) r[i] = bf2f(u[i]);
         }
       };
-      for (int i = kslot; i < n; i += RIF) {
-        float k[8];
-        row(Ly.kc, 0, j0 + i, k);
+      // the K and V rows of this thread's first two key slots are requested together (one round
+      // trip instead of two for short splits; the rest stream in the loops)
+      float kp[2][8], vp[2][8];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (kslot + RIF * u < n) {
+          row(Ly.kc, 0, j0 + kslot + RIF * u, kp[u]);
+          row(Ly.vc, 1, j0 + kslot + RIF * u, vp[u]);
+        }
+      }
+      auto score = [&](int i, const float* k) {
         float d = 0.f;
 #pragma unroll
         for (int t = 0; t < 8; ++t) d += q[t] * k[t];
 #pragma unroll
         for (int o = LPR / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
-        if (sub == 0) sc[i] = d;
+        if (sub == 0 && i < n) sc[i] = d;
+      };
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        if (RIF * u < n) score(kslot + RIF * u, kp[u]);  // workgroup-uniform bound
+      for (int i = kslot + 2 * RIF; i < n; i += RIF) {
+        float k[8];
+        row(Ly.kc, 0, j0 + i, k);
+        score(i, k);
       }
       __syncthreads();
       const float sv = tid < n ? sc[tid] : -INFINITY;
@@ -495,7 +511,15 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
       float acc[8];
 #pragma unroll
       for (int t = 0; t < 8; ++t) acc[t] = 0.f;
-      for (int i = kslot; i < n; i += RIF) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (kslot + RIF * u < n) {
+          const float pi = sc[kslot + RIF * u];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) acc[t] += pi * vp[u][t];
+        }
+      }
+      for (int i = kslot + 2 * RIF; i < n; i += RIF) {
         float v[8];
         row(Ly.vc, 1, j0 + i, v);
         const float pi = sc[i];

@@ -166,11 +166,7 @@ class _NativeStream:
             return
         dev = _parse(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         idx = dev.index if dev.index is not None else torch.cuda.current_device()
-        least, greatest = rt.priority_range()
-        hip_prio = greatest if int(priority) == 1 else least
-        h = ctypes.c_void_p()
-        rt.check(rt.lib().piamd_stream_create(idx, hip_prio, 1, ctypes.byref(h)), "hipStreamCreate")
-        self._h, self._own, self.device = h.value, True, torch.device("cuda", idx)
+        self._h, self._own, self.device = _pool_stream(idx, int(priority)), False, torch.device("cuda", idx)
         self._t = torch.cuda.ExternalStream(self._h, device=self.device)
         self.priority = int(priority)
 
@@ -213,14 +209,31 @@ class _NativeStream:
     def __hash__(self):
         return hash(self._h)
 
-    def __del__(self):
-        if getattr(self, "_own", False) and self._h:
-            try:
-                from .framework import device_rt as rt
-                rt.lib().piamd_stream_destroy(self._h)  # frees once its queued work completes
-            except Exception:  # noqa: BLE001 (interpreter shutdown)
-                pass
-            self._h = None
+
+
+# Native streams come from a per-(device, priority) pool handed out round-robin and never destroyed
+# (the reference's GPU context and PyTorch pool streams the same way): a stream id that torch's
+# allocator may still hold an event record for can never dangle.
+_POOL_SIZE = 16
+_POOL: dict = {}
+
+
+def _pool_stream(idx: int, priority: int) -> int:
+    from .framework import device_rt as rt
+    key = (idx, priority)
+    ent = _POOL.get(key)
+    if ent is None:
+        least, greatest = rt.priority_range()
+        hip_prio = greatest if priority == 1 else least
+        hs = []
+        for _ in range(_POOL_SIZE):
+            h = ctypes.c_void_p()
+            rt.check(rt.lib().piamd_stream_create(idx, hip_prio, 1, ctypes.byref(h)), "hipStreamCreate")
+            hs.append(h.value)
+        ent = _POOL[key] = [hs, 0]
+    hs, i = ent
+    ent[1] = (i + 1) % len(hs)
+    return hs[i]
 
 
 class _NativeEvent:
@@ -308,7 +321,7 @@ def side_stream(device, priority=2, key="side"):
     if ent is None:
         from .framework import device_rt as rt
         if rt.available():
-            ent = _SIDE[k] = _NativeStream(torch.device("cuda", idx), priority)
+            ent = _SIDE[k] = _NativeStream(torch.device("cuda", idx), priority)  # pool stream
         else:
             ent = _SIDE[k] = _NativeStream(_torch=torch.cuda.Stream(device=torch.device("cuda", idx)))
     return ent.torch_stream

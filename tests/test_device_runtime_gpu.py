@@ -67,7 +67,7 @@ def test_profiler_device_ranges(tmp_path):
 def test_static_comm_stream_is_native():
     from paddle_infer_amd.device import side_stream, _SIDE
     s = side_stream(torch.device("cuda", 0), priority=1, key="static_comm")
-    assert any(v.torch_stream is s and v._own for v in _SIDE.values())
+    assert any(v.torch_stream is s and v.priority == 1 for v in _SIDE.values())
 
 
 def test_device_level_stream_api():

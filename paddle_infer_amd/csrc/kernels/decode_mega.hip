@@ -90,6 +90,9 @@ struct MegaArgs {
   int neox;             // 1: rotate-half (NeoX), 0: interleaved pairs (GPT-J)
   float log2_base;      // log2 of the rotary base
   int w8;               // 1: int8 weight-only projections (MegaLayer scales)
+  int nb;               // batch rows per step (1, 2 or 4): resid / rbuf / qn / kvn / part / h hold
+                        // nb rows per slot, pos nb entries, the caches are [rows][HK][maxS][D]
+  int mm;               // batch 1: 1 = MFMA GEMV phases (MegaCfg MM; instantiated shapes only)
 };
 
 __device__ __forceinline__ u64 ld64(const void* p) { return *reinterpret_cast<const u64*>(p); }
@@ -204,41 +207,49 @@ __device__ __forceinline__ void butterfly(float* acc, int lane) {
   if constexpr (HALF > 1) butterfly<HALF / 2, O / 2>(acc, lane);
 }
 
-// y[c] = Σ_k x[k]·W[c][k] for the NPW columns of this workgroup's LDS slice `ws` ([NPW][K] bf16);
-// thread t holds x[k] for k = (j·256 + t)·8 + i (threads past K hold nothing: K = 1024 leaves
-// waves 2-3 out of the dot products). Returns column `tid`'s sum for tid < NPW.
+// y_b[c] = Σ_k x_b[k]·W[c][k] for the NPW columns of this workgroup's LDS slice `ws` ([NPW][K]
+// bf16 or int8, row stride RS bytes) and NB activation rows b (batch rows share every weight read: one LDS read and convert
+// feeds NB FMAs); thread t holds x_b[k] for k = (j·256 + t)·8 + i (threads past K hold nothing:
+// K = 1024 leaves waves 2-3 out of the dot products). r[b] = column `tid`'s sum for tid < NPW.
 // Reduction: a butterfly that halves the live columns per exchange (log2 P steps, P−1 shuffles
-// instead of 6·P), then 4 waves through LDS.
+// instead of 6·P), then 4 waves through LDS (`red` holds 4·NB·32 floats).
 // `mid()` runs once every wave has consumed the first half of the columns (slice bytes
 // [0, SLICE/2) are free), `end()` once the whole slice is consumed: the loader waves issue the
 // next slices' DMA there.
-template <int NPW, int K, bool W8, class Mid, class End>
-__device__ __forceinline__ float gemv_lds(const char* ws, const float (&x)[(K + 2047) / 2048][8], float* red,
-                                          int tid, Mid mid, End end) {
+template <int NPW, int K, bool W8, int NB, int RS, class Mid, class End>
+__device__ __forceinline__ void gemv_lds(const char* ws, const float (&x)[NB][(K + 2047) / 2048][8], float* red,
+                                         int tid, Mid mid, End end, float (&r)[NB]) {
   constexpr int KCH = (K + 2047) / 2048;
   constexpr int P = NPW <= 8 ? 8 : 32;
   constexpr int LOGP = P == 8 ? 3 : 5;
   static_assert(NPW <= 32 && K % 1024 == 0, "gemv_lds shape");
   const int lane = tid & 63, wv = tid >> 6;
-  float acc[P];
+  float acc[NB][P];
 #pragma unroll
-  for (int c = 0; c < P; ++c) acc[c] = 0.f;
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int c = 0; c < P; ++c) acc[b][c] = 0.f;
   auto cols = [&](auto c0, auto c1) {
 #pragma unroll
     for (int c = decltype(c0)::value; c < decltype(c1)::value; ++c) {
 #pragma unroll
       for (int j = 0; j < KCH; ++j) {
         if (K % 2048 != 0 && (j * 256 + tid) * 8 >= K) continue;  // wave-uniform
+        float wf[8];
         if constexpr (W8) {  // int8 [NPW][K]: 8 weights per 8-B read, scaled after the sum
-          const uint2 q = *reinterpret_cast<const uint2*>(ws + (long)c * K + (j * 256 + tid) * 8);
+          const uint2 q = *reinterpret_cast<const uint2*>(ws + (long)c * RS + (j * 256 + tid) * 8);
 #pragma unroll
           for (int i = 0; i < 8; ++i)
-            acc[c] += x[j][i] * (float)(int)(signed char)(((i < 4 ? q.x : q.y) >> (8 * (i & 3))) & 0xFF);
+            wf[i] = (float)(int)(signed char)(((i < 4 ? q.x : q.y) >> (8 * (i & 3))) & 0xFF);
         } else {
-          const u16x8 w = *reinterpret_cast<const u16x8*>(ws + ((long)c * K + (j * 256 + tid) * 8) * 2);
+          const u16x8 w = *reinterpret_cast<const u16x8*>(ws + (long)c * RS + (j * 256 + tid) * 16);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) acc[c] += x[j][i] * bf2f(w[i]);
+          for (int i = 0; i < 8; ++i) wf[i] = bf2f(w[i]);
         }
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) acc[b][c] += x[b][j][i] * wf[i];
       }
     }
   };
@@ -246,44 +257,83 @@ __device__ __forceinline__ float gemv_lds(const char* ws, const float (&x)[(K + 
   __syncthreads();  // columns [0, NPW/2) = slice bytes [0, SLICE/2) consumed by every wave
   mid();
   cols(std::integral_constant<int, NPW / 2>{}, std::integral_constant<int, NPW>{});
-  butterfly<P / 2, 32>(acc, lane);
 #pragma unroll
-  for (int o = 32 >> LOGP; o > 0; o >>= 1) acc[0] += __shfl_xor(acc[0], o, 64);
-  if ((lane & ((64 >> LOGP) - 1)) == 0) red[wv * P + (lane >> (6 - LOGP))] = acc[0];
+  for (int b = 0; b < NB; ++b) {
+    butterfly<P / 2, 32>(acc[b], lane);
+#pragma unroll
+    for (int o = 32 >> LOGP; o > 0; o >>= 1) acc[b][0] += __shfl_xor(acc[b][0], o, 64);
+    if ((lane & ((64 >> LOGP) - 1)) == 0) red[(wv * NB + b) * P + (lane >> (6 - LOGP))] = acc[b][0];
+  }
   __syncthreads();
   end();
-  float r = 0.f;
-  if (tid < NPW) r = red[tid] + red[P + tid] + red[2 * P + tid] + red[3 * P + tid];
-  return r;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    r[b] = 0.f;
+    if (tid < NPW)
+      r[b] = red[b * P + tid] + red[(NB + b) * P + tid] + red[(2 * NB + b) * P + tid] +
+             red[(3 * NB + b) * P + tid];
+  }
 }
 
-// x = bf16(LN(resid)) for this thread's 8 elements k = 8·tid (threads with 8·tid ≥ EE hold 0).
-template <int EE>
+// N block-wide sums in one LDS round (blockDim 256; `red` holds 4·N floats).
+template <int N>
+__device__ __forceinline__ void block_sum_n(float (&v)[N], float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = wave_sum(v[i]);
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) red[w * N + i] = v[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = red[i] + red[N + i] + red[2 * N + i] + red[3 * N + i];
+  __syncthreads();
+}
+
+// x_b = bf16(LN(resid_b)) for NB rows r + b·EE, this thread's 8 elements k = 8·tid (threads with
+// 8·tid ≥ EE hold 0). The rows' means (then variances) share one block reduction.
+template <int EE, int NB>
 __device__ __forceinline__ void ln_prologue(const MegaArgs& a, const bf16_t* r, const bf16_t* g,
-                                            const bf16_t* b, float (&x)[1][8], float* wred, int tid) {
+                                            const bf16_t* b, float (&x)[NB][1][8], float* wred, int tid) {
   const bool on = tid * 8 < EE;
   // gamma / beta first: their latency then hides under the residual load and the reductions
-  // (a load is not hoisted across the __syncthreads of block_sum)
+  // (a load is not hoisted across the __syncthreads of block_sum_n)
   u16x8 gg{}, bb{};
-  float v[8];
+  float v[NB][8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = 0.f;
+  for (int n = 0; n < NB; ++n)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[n][i] = 0.f;
   if (on) {
     gg = *reinterpret_cast<const u16x8*>(g + tid * 8);
     bb = *reinterpret_cast<const u16x8*>(b + tid * 8);
-    ld_bf8(r + tid * 8, v);
+#pragma unroll
+    for (int n = 0; n < NB; ++n) ld_bf8(r + (long)n * EE + tid * 8, v[n]);
   }
-  float s = 0.f;
+  float mean[NB], q[NB];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) s += v[i];
-  const float mean = block_sum<4>(s, wred) * (1.f / EE);
-  float q = 0.f;
+  for (int n = 0; n < NB; ++n) {
+    mean[n] = 0.f;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) q += on ? (v[i] - mean) * (v[i] - mean) : 0.f;
-  const float rs = rsqrtf(block_sum<4>(q, wred) * (1.f / EE) + a.eps);
+    for (int i = 0; i < 8; ++i) mean[n] += v[n][i];
+  }
+  block_sum_n<NB>(mean, wred);
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
-    x[0][i] = on ? bf2f(f2bf((v[i] - mean) * rs * bf2f(gg[i]) + bf2f(bb[i]))) : 0.f;
+  for (int n = 0; n < NB; ++n) {
+    mean[n] *= 1.f / EE;
+    q[n] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q[n] += on ? (v[n][i] - mean[n]) * (v[n][i] - mean[n]) : 0.f;
+  }
+  block_sum_n<NB>(q, wred);
+#pragma unroll
+  for (int n = 0; n < NB; ++n) {
+    const float rs = rsqrtf(q[n] * (1.f / EE) + a.eps);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      x[n][0][i] = on ? bf2f(f2bf((v[n][i] - mean[n]) * rs * bf2f(gg[i]) + bf2f(bb[i]))) : 0.f;
+  }
 }
 
 // Lanes 0..NC-1 of wave 0 each hold one bf16 `y`; publish them as NC/4 64-bit stores at dst.
@@ -295,36 +345,175 @@ __device__ __forceinline__ void publish_bf16(bf16_t* dst, float y, int lane, int
   if (lane < NC && (lane & 3) == 0) st64(dst + lane, (u64)pair | ((u64)pair2 << 32));
 }
 
+// Loader waves: DMA bytes [from, to) (multiples of 1 KiB) of the [rows][RB-byte] slice at `src`
+// into the padded LDS image (row r at r·(RB + 16)); a 1 KiB piece never straddles a row.
+template <int RB>
+__device__ __forceinline__ void prefetch_p(const bf16_t* src, int from, int to, char* wl, int wv, int lane) {
+  if (wv == 0 || src == nullptr) return;
+  const char* s = reinterpret_cast<const char*>(src) + lane * 16;
+  for (int p = (from >> 10) + wv - 1; p < (to >> 10); p += 3) {
+    const int off = p * 1024, dst = off / RB * (RB + 16) + off % RB;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(s + off),
+                                     (__attribute__((address_space(3))) void*)(wl + dst), 16, 0, 0);
+  }
+}
+
+// MFMA form of gemv_lds for bf16 slices (same contract: x as gemv_lds, r[b] = column tid's sum
+// for tid < NPW; `mid` and `end` both run once the whole slice is consumed). The activation rows
+// are staged in LDS (`xs`: NB rows of KP = min(K, 8192 / NB) k, 16-B padded; one pass for every
+// K ≤ KP, else K / KP passes); each wave takes a quarter of a pass's k and runs
+// mfma_f32_16x16x32_bf16 over column tiles of 16: A = activations (rows ≥ NB zero), B = the
+// weight rows straight from the padded LDS image (one 16-B read per lane, conflict-free thanks
+// to the row padding). Operands are read SB k-steps at a time, the next batch's reads issued
+// before this batch's MFMAs (one wave per SIMD: nothing else hides the LDS latency). The four
+// waves' partial sums meet in `red`. No per-column butterfly and no bf16 → f32 converts: NB rows
+// cost the same MFMAs as one.
+template <int NPW, int K, int NB, int RS, class Mid, class End>
+__device__ __forceinline__ void gemv_mfma(const char* ws, const float (&x)[NB][(K + 2047) / 2048][8], float* red,
+                                          bf16_t* xs, int tid, Mid mid, End end, float (&r)[NB]) {
+  constexpr int KPM = 8192 / NB;
+  constexpr int KP = K < KPM ? K : KPM;        // k per staging pass
+  constexpr int JP = KP >= 2048 ? KP / 2048 : 1;  // thread x-chunks per pass
+  constexpr int NPASS = K / KP;
+  constexpr int XS = KP + 8;                   // xs row stride (elements)
+  constexpr int NCT = (NPW + 15) / 16;         // column tiles
+  constexpr int SPW = KP / 128;                // k-steps per wave per pass
+  constexpr int SB = NCT == 1 ? 8 : 4;         // k-steps per operand batch
+  constexpr int NBT = SPW / SB;
+  constexpr int P = NCT * 16;
+  static_assert(NPW <= 32 && K % 1024 == 0 && NB <= 4 && K % KP == 0 && SPW % SB == 0, "gemv_mfma shape");
+  const int lane = tid & 63, wv = tid >> 6, lr = lane & 15, g = lane >> 4;
+  f32x4 acc[NCT];
+#pragma unroll
+  for (int t = 0; t < NCT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < NPASS; ++q) {
+    if (q) __syncthreads();  // the previous pass's A reads are done
+#pragma unroll
+    for (int jj = 0; jj < JP; ++jj) {
+      const int kk = (jj * 256 + tid) * 8;
+      if (kk < KP) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          u16x8 o;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] = f2bf(x[b][q * JP + jj][i]);  // exact: x holds bf16 values
+          *reinterpret_cast<u16x8*>(xs + b * XS + kk) = o;
+        }
+      }
+    }
+    __syncthreads();
+    const int kw = wv * (KP / 4) + g * 8;
+    auto load = [&](int bt, u16x8 (&av)[SB], u16x8 (&bw)[SB][NCT]) {
+#pragma unroll
+      for (int u = 0; u < SB; ++u) {
+        const int k = kw + (bt * SB + u) * 32;
+        av[u] = u16x8{};
+        if (lr < NB) av[u] = *reinterpret_cast<const u16x8*>(xs + lr * XS + k);
+#pragma unroll
+        for (int t = 0; t < NCT; ++t) {
+          const int c = t * 16 + lr;
+          bw[u][t] = u16x8{};
+          if (NPW % 16 == 0 || c < NPW)
+            bw[u][t] = *reinterpret_cast<const u16x8*>(ws + (long)c * RS + (long)(q * KP + k) * 2);
+        }
+      }
+    };
+    u16x8 a0[SB], b0[SB][NCT];
+    load(0, a0, b0);
+#pragma unroll
+    for (int bt = 0; bt < NBT; ++bt) {
+      u16x8 a1[SB], b1[SB][NCT];
+      if (bt + 1 < NBT) load(bt + 1, a1, b1);
+#pragma unroll
+      for (int u = 0; u < SB; ++u)
+#pragma unroll
+        for (int t = 0; t < NCT; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a0[u]),
+                                                           __builtin_bit_cast(bf16x8, b0[u][t]), acc[t], 0, 0, 0);
+      if (bt + 1 < NBT) {
+#pragma unroll
+        for (int u = 0; u < SB; ++u) {
+          a0[u] = a1[u];
+#pragma unroll
+          for (int t = 0; t < NCT; ++t) b0[u][t] = b1[u][t];
+        }
+      }
+    }
+  }
+  // C[row (g·4 + i)][col lr]: rows 0..3 (the batch rows) sit in lanes 0-15
+  if (g == 0) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int t = 0; t < NCT; ++t) red[(wv * NB + b) * P + t * 16 + lr] = acc[t][b];
+  }
+  __syncthreads();
+  mid();
+  end();
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    r[b] = 0.f;
+    if (tid < NPW)
+      r[b] = red[b * P + tid] + red[(NB + b) * P + tid] + red[(2 * NB + b) * P + tid] +
+             red[(3 * NB + b) * P + tid];
+  }
+}
+
 // Model shape of the single-launch step. E / D / HQ / HK / F: hidden width, head dim, query and
 // key/value heads (GQA when HK < HQ), FFN width; ROT: rotary embedding over the whole head dim
 // (NeoX rotate-half or GPT-J interleaved per MegaArgs.neox, angles pos·base^(−2f/D)) applied to q
 // and the new k. Every projection splits its output columns evenly over the 256 workgroups and
 // each workgroup's weight slice must fit the 128 KiB LDS image.
-template <int E_, int D_, int HQ_, int HK_, int F_, int ROT_, int W8_ = 0>
+// NB: batch rows per step (each GEMV phase applies its LDS slice to all NB rows; attention runs
+// one workgroup per (row, head, split)). MM: the GEMV phases run on MFMA (gemv_mfma; bf16 only),
+// else on the VALU (gemv_lds; the batch-1 default).
+template <int E_, int D_, int HQ_, int HK_, int F_, int ROT_, int W8_ = 0, int NB_ = 1, int MM_ = (NB_ > 1)>
 struct MegaCfg {
-  static constexpr int E = E_, D = D_, HQ = HQ_, HK = HK_, F = F_, ROT = ROT_, W8 = W8_;
+  static constexpr int E = E_, D = D_, HQ = HQ_, HK = HK_, F = F_, ROT = ROT_, W8 = W8_, NB = NB_, MM = MM_;
+  static_assert(NB == 1 || NB == 2 || NB == 4, "rows per step");
+  static_assert(!(MM && W8), "MFMA GEMV phases take bf16 weights");
   static constexpr int WB = W8 ? 1 : 2;  // bytes per weight
   static constexpr int NQKV = (HQ + 2 * HK) * D;
   static constexpr int NPQ = NQKV / NWG, NPO = E / NWG, NP1 = F / NWG, NP2 = E / NWG;
-  // slice bytes: QKV [0, QB) → out [QB, QB + OB) (free during QKV) → FFN1 [0, F1B), whose first
-  // F1PRE bytes stream in during the attention phase (workgroups without attention work) or the
-  // out-projection prologue (the others) and the rest once the out slice is consumed → FFN2
-  // [0, F2B) → next QKV [0, QB)
+  // slice bytes (global, [rows][in] contiguous): QKV [0, QB) → out [QB, QB + OB) (free during
+  // QKV) → FFN1 [0, F1B), whose first F1PRE bytes stream in during the attention phase
+  // (workgroups without attention work) or the out-projection prologue (the others) and the rest
+  // once the out slice is consumed → FFN2 [0, F2B) → next QKV [0, QB)
   static constexpr int QB = NPQ * E * WB, OB = NPO * E * WB, F1B = NP1 * E * WB, F2B = NP2 * F * WB;
-  static constexpr int OUT_OFF = QB;
+  // LDS image: every weight row is padded by 16 B (row strides RSE / RSF), so the 16 rows of an
+  // MFMA B fragment (one 16-B read per lane, same k) start on 16 different bank quads
+  static constexpr int RBE = E * WB, RBF = F * WB, RSE = RBE + 16, RSF = RBF + 16;
+  static constexpr int OUT_OFF = NPQ * RSE;
   static constexpr int F1PRE = QB < F1B ? QB : F1B;
+  static constexpr int WL = (NPQ + NPO) * RSE > NP1 * RSE ? (NPQ + NPO) * RSE : NP1 * RSE;
+  static constexpr int WLB = ((WL > NP2 * RSF ? WL : NP2 * RSF) + 1023) / 1024 * 1024;
+  // early half-slice DMA (MegaArgs.late_dma = 0): whole rows of the next slice whose LDS extent
+  // stays inside the half (by columns) the running GEMV has already consumed
+  static constexpr int MID1 = F2B < (NP1 / 2) * RSE / RSF * RBF ? F2B : (NP1 / 2) * RSE / RSF * RBF;
+  static constexpr int MID2 = QB < (NP2 / 2) * RSF / RSE * RBE ? QB : (NP2 / 2) * RSF / RSE * RBE;
   // the out phase of a non-attention workgroup waits for every DMA older than its FFN1 head: the
   // newest F1PRE/1 KiB/3 wave-instructions per loader wave (floor: the minimum over the waves)
   static constexpr int WAIT_OLD = F1PRE / 1024 / 3;
   static constexpr int LPR = D / 8;  // lanes per head row (16 B each)
   static_assert(NQKV % NWG == 0 && E % NWG == 0 && F % NWG == 0, "columns split evenly over the grid");
-  static_assert(QB + OB <= WBYTES && F1B <= WBYTES && F2B <= WBYTES, "slices fit the LDS image");
-  static_assert(QB % 1024 == 0 && OB % 1024 == 0 && F1B % 1024 == 0 && F2B % 1024 == 0, "1 KiB pieces");
+  static_assert(WLB <= 132 * 1024, "slices fit the LDS image");
+  static_assert(RBE % 1024 == 0 && RBF % 1024 == 0, "1 KiB pieces never straddle a row");
   static_assert(HQ * D == E && HQ % HK == 0 && E % 1024 == 0 && E <= 2048 && F % 2048 == 0, "widths");
   static_assert(D == 64 || D == 128, "head dim");
   static_assert(NPQ <= 32 && NP1 <= 32 && (NPO & (NPO - 1)) == 0 && (NP1 & (NP1 - 1)) == 0 &&
                 NPO >= 4 && NP1 >= 4, "per-workgroup column counts");
 };
+
+// One GEMV phase of decode_mega_kernel<C> over a slice with LDS row stride RS.
+template <class C, int NPW, int K, int RS, class Mid, class End>
+__device__ __forceinline__ void gemv_phase(const char* ws, const float (&x)[C::NB][(K + 2047) / 2048][8],
+                                           float* red, bf16_t* xs, int tid, Mid mid, End end, float (&r)[C::NB]) {
+  if constexpr (C::MM)
+    gemv_mfma<NPW, K, C::NB, RS>(ws, x, red, xs, tid, mid, end, r);
+  else
+    gemv_lds<NPW, K, C::W8 != 0, C::NB, RS>(ws, x, red, tid, mid, end, r);
+}
 
 __host__ __device__ constexpr long pstride_hd(int hq, int d, int nsplit) {
   return ((long)hq * nsplit * (d + 2) + 63) / 64 * 64;
@@ -335,64 +524,71 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
   constexpr int E = C::E, D = C::D, HQ = C::HQ, HK = C::HK, F = C::F, LPR = C::LPR;
   constexpr int NPQ = C::NPQ, NPO = C::NPO, NP1 = C::NP1, NP2 = C::NP2;
   constexpr int PSTR = D + 2;
+  constexpr int NB = C::NB;
   constexpr bool W8 = C::W8 != 0;
   // a workgroup's weight slice: `rows` [out] rows of `in` weights, C::WB bytes each
   auto slice = [](const bf16_t* w, long row0, long in) {
     return reinterpret_cast<const bf16_t*>(reinterpret_cast<const char*>(w) + row0 * in * C::WB);
   };
-  __shared__ __attribute__((aligned(1024))) char wl[WBYTES];
-  __shared__ float red[4 * 32];
-  __shared__ float wred[8];
+  constexpr int RSE = C::RSE, RSF = C::RSF, RBE = C::RBE, RBF = C::RBF;
+  __shared__ __attribute__((aligned(1024))) char wl[C::WLB];
+  __shared__ __attribute__((aligned(16))) bf16_t xs[C::MM ? NB * (8192 / NB + 8) : 8];  // gemv_mfma staging
+  __shared__ float red[4 * NB * 32];
+  __shared__ float wred[4 * NB > 8 ? 4 * NB : 8];
   __shared__ float sc[256];
   __shared__ float pv[4][D];
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, w = blockIdx.x;
-  const int pos = a.pos[0], L = pos + 1;
+  const long pst = pstride_hd(HQ, D, a.nsplit);  // one row's partial block
   unsigned nbar = 0;
 
-  prefetch(slice(a.layers[0].wqkv, (long)w * NPQ, E), 0, C::QB, wl, wv, lane);
+  prefetch_p<RBE>(slice(a.layers[0].wqkv, (long)w * NPQ, E), 0, C::QB, wl, wv, lane);
   for (int l = 0; l < a.nl; ++l) {
     const MegaLayer& Ly = a.layers[l];
-    // this layer's buffer slots: every published vector has its own address per launch, so a
-    // reader's L2 can never hold a stale copy and plain (cached) loads are coherent
-    const bf16_t* rin = l == 0 ? a.resid : a.rbuf + (long)(2 * l - 1) * E;
-    bf16_t* rmid = a.rbuf + (long)(2 * l) * E;
-    bf16_t* rout = a.rbuf + (long)(2 * l + 1) * E;
-    float* qn = a.qn + (long)l * HQ * D;
-    float* kvn = a.kvn + (long)l * 2 * HK * D;
-    float* part = a.part + (long)l * pstride_hd(HQ, D, a.nsplit);
-    bf16_t* hb = a.h + (long)l * F;
+    // this layer's buffer slots (NB rows each): every published vector has its own address per
+    // launch, so a reader's L2 can never hold a stale copy and plain (cached) loads are coherent
+    const bf16_t* rin = l == 0 ? a.resid : a.rbuf + (long)(2 * l - 1) * NB * E;
+    bf16_t* rmid = a.rbuf + (long)(2 * l) * NB * E;
+    bf16_t* rout = a.rbuf + (long)(2 * l + 1) * NB * E;
+    float* qn = a.qn + (long)l * NB * HQ * D;
+    float* kvn = a.kvn + (long)l * NB * 2 * HK * D;
+    float* part = a.part + (long)l * NB * pst;
+    bf16_t* hb = a.h + (long)l * NB * F;
     // ---------------------------------------------------------------- QKV
     phase_start<C::WAIT_OLD>(a, wv, nbar);
     {
       // epilogue operands requested first: their latency hides under the prologue and GEMV
       const float bq = lane < NPQ ? bf2f(Ly.bqkv[w * NPQ + lane]) : 0.f;
       const float sq = W8 && lane < NPQ ? Ly.sqkv[w * NPQ + lane] : 1.f;
-      float x[1][8];
-      ln_prologue<E>(a, rin, Ly.ln1_g, Ly.ln1_b, x, wred, tid);
+      float x[NB][1][8];
+      ln_prologue<E, NB>(a, rin, Ly.ln1_g, Ly.ln1_b, x, wred, tid);
       tmark(a, nbar, 1);
       // out slice into the region QKV does not use, behind this GEMV
-      const float y = sq * gemv_lds<NPQ, E, W8>(wl, x, red, tid, [] {}, [&] {
-        prefetch(slice(Ly.wo, (long)w * NPO, E), 0, C::OB, wl + C::OUT_OFF, wv, lane);
-      });
+      float y[NB];
+      gemv_phase<C, NPQ, E, RSE>(wl, x, red, xs, tid, [] {}, [&] {
+        prefetch_p<RBE>(slice(Ly.wo, (long)w * NPO, E), 0, C::OB, wl + C::OUT_OFF, wv, lane);
+      }, y);
       tmark(a, nbar, 2);
       if (wv == 0) {
         if (lane < NPQ) {
           const int col = w * NPQ + lane;
-          const float v = bf2f(f2bf(y)) + bq;
-          if (col < HQ * D) {
-            __hip_atomic_store(qn + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          } else {
-            const int kv = col - HQ * D;          // [0, 2·HK·D)
-            const int which = kv / (HK * D), r = kv % (HK * D), kh = r / D, d = r % D;
-            const bf16_t vb = f2bf(v);
-            if (which || !C::ROT) {  // rotated k is cached by the attention phase (needs all of D)
-              bf16_t* cache = which ? Ly.vc : Ly.kc;
-              cache[((long)kh * a.maxS + pos) * D + d] = vb;
+#pragma unroll
+          for (int b = 0; b < NB; ++b) {
+            const float v = bf2f(f2bf(sq * y[b])) + bq;
+            if (col < HQ * D) {
+              __hip_atomic_store(qn + b * HQ * D + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+              const int kv = col - HQ * D;          // [0, 2·HK·D)
+              const int which = kv / (HK * D), r = kv % (HK * D), kh = r / D, d = r % D;
+              const bf16_t vb = f2bf(v);
+              if (which || !C::ROT) {  // rotated k is cached by the attention phase (needs all of D)
+                bf16_t* cache = which ? Ly.vc : Ly.kc;
+                cache[(((long)b * HK + kh) * a.maxS + a.pos[b]) * D + d] = vb;
+              }
+              // rotary k stays unrounded until rotated (the per-op path rounds after the rotation)
+              __hip_atomic_store(kvn + b * 2 * HK * D + kv, (C::ROT && !which) ? v : bf2f(vb),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            // rotary k stays unrounded until rotated (the per-op path rounds after the rotation)
-            __hip_atomic_store(kvn + kv, (C::ROT && !which) ? v : bf2f(vb), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
           }
         }
         grid_sync(a, ++nbar, lane);
@@ -404,13 +600,18 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
     // (attention reads no weights: the out slice keeps streaming)
     phase_start<C::WAIT_OLD>(a, wv, nbar, WAIT_NONE);
     const bf16_t* w1s = slice(Ly.w1, (long)w * NP1, E);
-    if (w < HQ * a.nsplit) {
-      const int h = w / a.nsplit, s = w % a.nsplit, kh = h / (HQ / HK);
+    if (w < NB * HQ * a.nsplit) {
+      // one workgroup per (row, head, split)
+      const int bi = w / (HQ * a.nsplit), wr = w % (HQ * a.nsplit);
+      const int h = wr / a.nsplit, s = wr % a.nsplit, kh = h / (HQ / HK);
+      const int pos = a.pos[bi], L = pos + 1;
+      const float* qn_b = qn + bi * HQ * D;
+      const float* kvn_b = kvn + bi * 2 * HK * D;
       const int chunk = (L + a.nsplit - 1) / a.nsplit;
       const int j0 = s * chunk, n = min(L, j0 + chunk) - j0;
       constexpr int RIF = NT / LPR;                    // key rows in flight per workgroup
       const int sub = tid % LPR, kslot = tid / LPR;    // LPR lanes per key row
-      const long kvbase = (long)kh * a.maxS * D;
+      const long kvbase = ((long)bi * HK + kh) * a.maxS * D;
       float rc[8], rsn[8];
       if (C::ROT) {
 #pragma unroll
@@ -438,8 +639,8 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
       float q[8], kn[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        q[i] = ldf(qn + h * D + sub * 8 + i);
-        kn[i] = ldf(kvn + kh * D + sub * 8 + i);
+        q[i] = ldf(qn_b + h * D + sub * 8 + i);
+        kn[i] = ldf(kvn_b + kh * D + sub * 8 + i);
       }
       if (C::ROT) {
         rotate(q);
@@ -461,7 +662,7 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) r[i] = kn[i];
           } else {
-            const float* p = kvn + HK * D + kh * D + sub * 8;
+            const float* p = kvn_b + HK * D + kh * D + sub * 8;
 #pragma unroll
             for (int i = 0; i < 8; i += 2) {
               const u64 u = ld64(p + i);
@@ -537,7 +738,7 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
       }
       __syncthreads();
       if (wv == 0) {
-        float* dst = part + (long)(h * a.nsplit + s) * PSTR;
+        float* dst = part + bi * pst + (long)(h * a.nsplit + s) * PSTR;
         const int d0 = lane * 2;
         if (d0 < D) {
           const float v0 = pv[0][d0] + pv[1][d0] + pv[2][d0] + pv[3][d0];
@@ -547,63 +748,84 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
         if (lane == 0) st64(dst + D, pack2f(n > 0 ? m : -INFINITY, n > 0 ? lsum : 0.f));
       }
     } else {
-      prefetch(w1s, 0, C::F1PRE, wl, wv, lane);
+      prefetch_p<RBE>(w1s, 0, C::F1PRE, wl, wv, lane);
     }
     if (wv == 0) grid_sync(a, ++nbar, lane); else ++nbar;
     // ---------------------------------------------------------------- out projection
     // attention workgroups queue their FFN1 DMA only now (their loader waves carried K/V loads):
     // every older load has to land; the others issued it at the attention phase start and wait
     // for the out slice only
-    const bool attn_wg = w < HQ * a.nsplit;
+    const bool attn_wg = w < NB * HQ * a.nsplit;
     phase_start<C::WAIT_OLD>(a, wv, nbar, attn_wg ? WAIT_ALL : WAIT_OLDER);
     {
       const int ocol = w * NPO + (lane & (NPO - 1));
-      const float bo = bf2f(Ly.bo[ocol]), ro = bf2f(rin[ocol]);
+      const float bo = bf2f(Ly.bo[ocol]);
+      float ro[NB];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) ro[b] = bf2f(rin[b * E + ocol]);
       const float so = W8 ? Ly.so[ocol] : 1.f;
-      float x[1][8];
+      float x[NB][1][8];
       {
         const int h = tid / LPR, d0 = (tid % LPR) * 8;  // thread t holds elements 8t … 8t+7
         const bool on = h < HQ;
-        const float* base = part + (long)min(h, HQ - 1) * a.nsplit * PSTR;
-        // online combine, eight splits' partials requested at once (no load waits on another)
-        float M = -INFINITY, lt = 0.f, o[8];
+        // online combine; SPR splits' partials of every row requested at once (no load waits on
+        // another; HQ·nsplit·NB ≤ 256 keeps nsplit ≤ SPR for the instantiated head counts)
+        constexpr int SPR = NB == 4 ? 4 : 8;
+        float M[NB], lt[NB], o[NB][8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] = 0.f;
-        for (int s0 = 0; s0 < a.nsplit; s0 += 8) {
-          u64 ml[8], ov[8][4];
+        for (int b = 0; b < NB; ++b) {
+          M[b] = -INFINITY;
+          lt[b] = 0.f;
 #pragma unroll
-          for (int t = 0; t < 8; ++t) {
-            const float* ps = base + min(s0 + t, a.nsplit - 1) * PSTR;
-            ml[t] = ld64(ps + D);
+          for (int i = 0; i < 8; ++i) o[b][i] = 0.f;
+        }
+        for (int s0 = 0; s0 < a.nsplit; s0 += SPR) {
+          u64 ml[NB][SPR], ov[NB][SPR][4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) ov[t][i] = ld64(ps + d0 + 2 * i);
+          for (int b = 0; b < NB; ++b) {
+            const float* base = part + b * pst + (long)min(h, HQ - 1) * a.nsplit * PSTR;
+#pragma unroll
+            for (int t = 0; t < SPR; ++t) {
+              const float* ps = base + min(s0 + t, a.nsplit - 1) * PSTR;
+              ml[b][t] = ld64(ps + D);
+#pragma unroll
+              for (int i = 0; i < 4; ++i) ov[b][t][i] = ld64(ps + d0 + 2 * i);
+            }
           }
 #pragma unroll
-          for (int t = 0; t < 8; ++t) {
-            const float ms = __uint_as_float((unsigned)ml[t]);
-            if (s0 + t >= a.nsplit || ms == -INFINITY) continue;
-            const float nM = fmaxf(M, ms), c = exp2f(M - nM), e = exp2f(ms - nM);
-            lt = lt * c + e * __uint_as_float((unsigned)(ml[t] >> 32));
+          for (int b = 0; b < NB; ++b) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              o[2 * i] = o[2 * i] * c + e * __uint_as_float((unsigned)ov[t][i]);
-              o[2 * i + 1] = o[2 * i + 1] * c + e * __uint_as_float((unsigned)(ov[t][i] >> 32));
+            for (int t = 0; t < SPR; ++t) {
+              const float ms = __uint_as_float((unsigned)ml[b][t]);
+              if (s0 + t >= a.nsplit || ms == -INFINITY) continue;
+              const float nM = fmaxf(M[b], ms), c = exp2f(M[b] - nM), e = exp2f(ms - nM);
+              lt[b] = lt[b] * c + e * __uint_as_float((unsigned)(ml[b][t] >> 32));
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                o[b][2 * i] = o[b][2 * i] * c + e * __uint_as_float((unsigned)ov[b][t][i]);
+                o[b][2 * i + 1] = o[b][2 * i + 1] * c + e * __uint_as_float((unsigned)(ov[b][t][i] >> 32));
+              }
+              M[b] = nM;
             }
-            M = nM;
           }
         }
-        const float inv = 1.f / lt;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) x[0][i] = on ? bf2f(f2bf(o[i] * inv)) : 0.f;
+        for (int b = 0; b < NB; ++b) {
+          const float inv = 1.f / lt[b];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) x[b][0][i] = on ? bf2f(f2bf(o[b][i] * inv)) : 0.f;
+        }
       }
-      if (attn_wg) prefetch(w1s, 0, C::F1PRE, wl, wv, lane);
+      if (attn_wg) prefetch_p<RBE>(w1s, 0, C::F1PRE, wl, wv, lane);
       tmark(a, nbar, 1);
-      const float y = so * gemv_lds<NPO, E, W8>(wl + C::OUT_OFF, x, red, tid, [] {}, [&] {
-        prefetch(w1s, C::F1PRE, C::F1B, wl, wv, lane);
-      });
+      float y[NB];
+      gemv_phase<C, NPO, E, RSE>(wl + C::OUT_OFF, x, red, xs, tid, [] {}, [&] {
+        prefetch_p<RBE>(w1s, C::F1PRE, C::F1B, wl, wv, lane);
+      }, y);
       tmark(a, nbar, 2);
       if (wv == 0) {
-        publish_bf16(rmid + w * NPO, y + bo + ro, lane, NPO);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) publish_bf16(rmid + b * E + w * NPO, so * y[b] + bo + ro[b], lane, NPO);
         grid_sync(a, ++nbar, lane);
       } else {
         ++nbar;
@@ -614,18 +836,21 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
     {
       const float b1 = bf2f(Ly.b1[w * NP1 + (lane & (NP1 - 1))]);
       const float s1 = W8 ? Ly.s1[w * NP1 + (lane & (NP1 - 1))] : 1.f;
-      float x[1][8];
-      ln_prologue<E>(a, rmid, Ly.ln2_g, Ly.ln2_b, x, wred, tid);
+      float x[NB][1][8];
+      ln_prologue<E, NB>(a, rmid, Ly.ln2_g, Ly.ln2_b, x, wred, tid);
       tmark(a, nbar, 1);
       const bf16_t* w2s = slice(Ly.w2, (long)w * NP2, F);
-      constexpr int MID1 = C::F1B / 2 < C::F2B ? C::F1B / 2 : C::F2B;
-      const int mid = a.late_dma ? 0 : MID1;
-      const float y = s1 * gemv_lds<NP1, E, W8>(wl, x, red, tid, [&] { prefetch(w2s, 0, mid, wl, wv, lane); },
-                                       [&] { prefetch(w2s, mid, C::F2B, wl, wv, lane); });
+      const int mid = a.late_dma ? 0 : C::MID1;
+      float y[NB];
+      gemv_phase<C, NP1, E, RSE>(wl, x, red, xs, tid, [&] { prefetch_p<RBF>(w2s, 0, mid, wl, wv, lane); },
+                                 [&] { prefetch_p<RBF>(w2s, mid, C::F2B, wl, wv, lane); }, y);
       tmark(a, nbar, 2);
       if (wv == 0) {
-        const float t = y + b1;
-        publish_bf16(hb + w * NP1, a.act ? gelu_tanh(t) : gelu_erf(t), lane, NP1);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          const float t = s1 * y[b] + b1;
+          publish_bf16(hb + b * F + w * NP1, a.act ? gelu_tanh(t) : gelu_erf(t), lane, NP1);
+        }
         grid_sync(a, ++nbar, lane);
       } else {
         ++nbar;
@@ -635,21 +860,27 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
     phase_start<C::WAIT_OLD>(a, wv, nbar);
     {
       const int fcol = w * NP2 + (lane & (NP2 - 1));
-      const float b2 = bf2f(Ly.b2[fcol]), rm = bf2f(rmid[fcol]);
+      const float b2 = bf2f(Ly.b2[fcol]);
+      float rm[NB];
+#pragma unroll
+      for (int b = 0; b < NB; ++b) rm[b] = bf2f(rmid[b * E + fcol]);
       const float s2 = W8 ? Ly.s2[fcol] : 1.f;
       constexpr int KCH2 = F / 2048;
-      float x[KCH2][8];
+      float x[NB][KCH2][8];
 #pragma unroll
-      for (int j = 0; j < KCH2; ++j) ld_bf8(hb + (j * 256 + tid) * 8, x[j]);
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int j = 0; j < KCH2; ++j) ld_bf8(hb + b * F + (j * 256 + tid) * 8, x[b][j]);
       tmark(a, nbar, 1);
       const bf16_t* nq = l + 1 < a.nl ? slice(a.layers[l + 1].wqkv, (long)w * NPQ, E) : nullptr;
-      constexpr int MID2 = C::F2B / 2 < C::QB ? C::F2B / 2 : C::QB;
-      const int mid = a.late_dma ? 0 : MID2;
-      const float y = s2 * gemv_lds<NP2, F, W8>(wl, x, red, tid, [&] { prefetch(nq, 0, mid, wl, wv, lane); },
-                                       [&] { prefetch(nq, mid, C::QB, wl, wv, lane); });
+      const int mid = a.late_dma ? 0 : C::MID2;
+      float y[NB];
+      gemv_phase<C, NP2, F, RSF>(wl, x, red, xs, tid, [&] { prefetch_p<RBE>(nq, 0, mid, wl, wv, lane); },
+                                 [&] { prefetch_p<RBE>(nq, mid, C::QB, wl, wv, lane); }, y);
       tmark(a, nbar, 2);
       if (wv == 0) {
-        publish_bf16(rout + w * NP2, y + b2 + rm, lane, NP2);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) publish_bf16(rout + b * E + w * NP2, s2 * y[b] + b2 + rm[b], lane, NP2);
         if (l + 1 < a.nl) grid_sync(a, ++nbar, lane);
       } else {
         ++nbar;
@@ -1245,23 +1476,37 @@ typedef MegaCfg<1024, 64, 16, 16, 4096, 0> CfgGpt350;    // GPT-3 350M
 typedef MegaCfg<1024, 64, 16, 16, 4096, 1> CfgGpt350R;
 typedef MegaCfg<2048, 128, 16, 16, 8192, 0, 1> CfgGpt13W8;  // int8 weight-only
 typedef MegaCfg<2048, 128, 16, 4, 8192, 1, 1> CfgGqa4RW8;
+// batched steps (2 / 4 rows: small serving batches, beams)
+typedef MegaCfg<2048, 128, 16, 16, 8192, 0, 0, 2> CfgGpt13B2;
+typedef MegaCfg<2048, 128, 16, 16, 8192, 0, 0, 4> CfgGpt13B4;
+typedef MegaCfg<2048, 128, 16, 4, 8192, 1, 0, 2> CfgGqa4RB2;
+typedef MegaCfg<2048, 128, 16, 4, 8192, 1, 0, 4> CfgGqa4RB4;
+typedef MegaCfg<1024, 64, 16, 16, 4096, 0, 0, 2> CfgGpt350B2;
+typedef MegaCfg<1024, 64, 16, 16, 4096, 0, 0, 4> CfgGpt350B4;
+typedef MegaCfg<2048, 128, 16, 16, 8192, 0, 0, 1, 1> CfgGpt13M;  // batch 1 on MFMA (A/B)
 
-static const void* mega_fn(int E_, int D_, int hq, int hk, int F_, int rot, int w8) {
+static const void* mega_fn(int E_, int D_, int hq, int hk, int F_, int rot, int w8, int nb, int mm = 0) {
 #define MEGA_CFG(C)                                                                           \
   if (E_ == C::E && D_ == C::D && hq == C::HQ && hk == C::HK && F_ == C::F &&                 \
-      (rot != 0) == C::ROT && (w8 != 0) == C::W8)                                             \
+      (rot != 0) == C::ROT && (w8 != 0) == C::W8 && nb == C::NB && (nb > 1 || (mm != 0) == C::MM)) \
     return (const void*)decode_mega_kernel<C>;
   MEGA_CFG(CfgGpt13) MEGA_CFG(CfgGpt13R) MEGA_CFG(CfgGqa4) MEGA_CFG(CfgGqa4R)
   MEGA_CFG(CfgGpt350) MEGA_CFG(CfgGpt350R) MEGA_CFG(CfgGpt13W8) MEGA_CFG(CfgGqa4RW8)
+  MEGA_CFG(CfgGpt13B2) MEGA_CFG(CfgGpt13B4) MEGA_CFG(CfgGqa4RB2) MEGA_CFG(CfgGqa4RB4)
+  MEGA_CFG(CfgGpt350B2) MEGA_CFG(CfgGpt350B4) MEGA_CFG(CfgGpt13M)
 #undef MEGA_CFG
   return nullptr;
 }
 
-// 1 when this device can run the single-launch step for the shape: an instantiated shape,
-// cooperative launches supported and all NWG workgroups co-resident.
-PIAMD_EXPORT int piamd_decode_mega_shape_supported(int E_, int D_, int hq, int hk, int F_, int rot, int w8) {
-  const void* fn = mega_fn(E_, D_, hq, hk, F_, rot, w8);
+// 1 when this device can run the single-launch step for the shape at `nb` rows: an instantiated
+// shape, cooperative launches supported and all NWG workgroups co-resident.
+PIAMD_EXPORT int piamd_decode_mega_batch_supported(int E_, int D_, int hq, int hk, int F_, int rot, int w8,
+                                                   int nb) {
+  const void* fn = mega_fn(E_, D_, hq, hk, F_, rot, w8, nb);
   return fn != nullptr && coop_ok(fn, NT);
+}
+PIAMD_EXPORT int piamd_decode_mega_shape_supported(int E_, int D_, int hq, int hk, int F_, int rot, int w8) {
+  return piamd_decode_mega_batch_supported(E_, D_, hq, hk, F_, rot, w8, 1);
 }
 PIAMD_EXPORT int piamd_decode_mega_supported() { return piamd_decode_mega_shape_supported(E, D, HQ, HK, F, 0, 0); }
 PIAMD_EXPORT int piamd_decode_mega_lw_supported() {
@@ -1275,10 +1520,11 @@ PIAMD_EXPORT int piamd_decode_mega_lw_supported() {
 PIAMD_EXPORT int piamd_decode_mega(const MegaArgs* args, int E_, int D_, int hq, int hk, int F_,
                                    hipStream_t st) {
   const MegaArgs& a = *args;
-  const void* fn = mega_fn(E_, D_, hq, hk, F_, a.rot, a.w8);
-  const bool lw_shape = E_ == E && D_ == D && hq == HQ && hk == HK && F_ == F && a.rot == 0 && !a.w8;
+  const void* fn = mega_fn(E_, D_, hq, hk, F_, a.rot, a.w8, a.nb, a.mm);
+  const bool lw_shape =
+      E_ == E && D_ == D && hq == HQ && hk == HK && F_ == F && a.rot == 0 && !a.w8 && a.nb == 1 && !a.mm;
   if (!fn || (a.rot != 0 && a.rot != D_) || a.nl < 1 || a.loader < 0 || a.loader > 1 ||
-      (a.loader && !lw_shape) || a.nsplit < 1 || hq * a.nsplit > NWG ||
+      (a.loader && !lw_shape) || a.nsplit < 1 || a.nb * hq * a.nsplit > NWG ||
       (a.maxS + a.nsplit - 1) / a.nsplit > 256 || !a.layers || !a.resid || !a.rbuf || !a.qn ||
       !a.kvn || !a.part || !a.h || !a.bar || !a.err || !a.pos)
     return (int)hipErrorInvalidValue;

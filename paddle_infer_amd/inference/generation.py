@@ -73,7 +73,8 @@ class GPTGenerator:
                        for _ in self.layers]
         self.use_graph = use_hip_graph and self.device.type == "cuda"
         self._graphs = {}
-        self._mega = None  # MegaDecoder, built on the first eligible batch-1 decode step
+        self._mega = {}  # batch rows → MegaDecoder (False: not eligible), built on first use
+        self.use_mega = True  # False: every decode step takes the per-op path
 
     # ------------------------------------------------------------------------------ model
     def _mp_gather(self, logits):
@@ -119,19 +120,19 @@ class GPTGenerator:
         """The single-launch decode step (inference/mega_decode.py) when this model / batch fits
         it, else None (per-op path)."""
         from . import mega_decode
-        if B != 1 or not mega_decode.enabled():
+        if not self.use_mega or B not in mega_decode.BATCHES or not mega_decode.enabled():
             return None
-        if self._mega is None:  # the shape / dtype gate is static: evaluated once
-            self._mega = mega_decode.MegaDecoder(self) if mega_decode.eligible(self, 1) else False
-        return self._mega or None
+        if B not in self._mega:  # the shape / dtype gate is static: evaluated once per batch size
+            self._mega[B] = mega_decode.MegaDecoder(self, B) if mega_decode.eligible(self, B) else False
+        return self._mega[B] or None
 
     def _decode_eager(self, tok, pos, B):
         mega = self._mega_decoder(B)
         if mega is not None:
             from ..ops.norm import layer_norm
-            resid = self.model.gpt.embeddings(tok.view(1, 1), pos.long().view(1, 1))
-            resid = resid.reshape(-1).contiguous()
-            y = layer_norm(mega(resid, pos).view(1, -1), *self.final_ln)
+            resid = self.model.gpt.embeddings(tok.view(B, 1), pos.long().view(B, 1))
+            resid = resid.reshape(B, -1).contiguous()
+            y = layer_norm(mega(resid, pos.contiguous()).view(B, -1), *self.final_ln)
             return self._logits(y)
         lens = pos + 1
         y = self._forward(tok.view(B, 1), pos, lens, B, decode=True)
@@ -220,8 +221,9 @@ class GPTGenerator:
             if t + 1 < max_new_tokens:
                 logits = self.decode(tok, pos)
                 pos = pos + 1
-        if self._mega:  # one sync per generate(): a timed-out single-launch step fails loudly
-            self._mega.check()
+        for m in self._mega.values():  # one sync per generate(): a timed-out step fails loudly
+            if m:
+                m.check()
         return out
 
     def _greedy_mega_loop(self, mega, logits, pos, out, done, max_new_tokens, eos, pad):

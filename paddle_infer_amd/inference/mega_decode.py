@@ -9,9 +9,15 @@ no longer pays a launch ramp per GEMV (5 per layer on the per-op path).
 Parity: one ``FusedMultiTransformer`` decode step with ``time_step``
 (`paddle/fluid/operators/fused/fused_multi_transformer_op.cu`); the per-op path
 (``incubate.nn.functional.multi_transformer_forward(decode=True)``) stays the reference and the
-fallback for shapes the kernel does not take (batch > 1, widths not instantiated in
+fallback for shapes the kernel does not take (widths / batch sizes not instantiated in
 ``decode_mega.hip`` — GPT-3 1.3B / 350M and a GQA 4:1 variant, each with or without whole-head
-rotary — weight-only, TP).
+rotary, at 1 row; 2 and 4 rows for 1.3B, 350M and GQA 4:1 + rotary — other weight-only
+layouts, TP).
+
+Batched steps (2 / 4 rows: small serving batches, beams) apply every workgroup's LDS weight
+slice to all rows, so the weight stream — the whole cost at these sizes — is paid once per step
+instead of once per row; attention runs one workgroup per (row, head, split) at each row's own
+cache position.
 """
 from __future__ import annotations
 
@@ -57,14 +63,25 @@ def _w8(gen):
     return None
 
 
+BATCHES = (1, 2, 4)  # rows per step with an instantiated kernel (MegaCfg::NB)
+
+
+def max_splits(B: int, hq: int) -> int:
+    """Attention splits available at ``B`` rows: one workgroup per (row, head, split) ≤ 256."""
+    return 256 // (B * hq)
+
+
 def eligible(gen, B: int) -> bool:
     """True when generator ``gen``'s decode step at batch ``B`` can run as one launch."""
     if not enabled():
         return False
-    if B != 1 or gen.device.type != "cuda" or gen.dtype != torch.bfloat16 or gen.group is not None:
+    if (B not in BATCHES or B > gen.max_batch or gen.device.type != "cuda" or gen.dtype != torch.bfloat16
+            or gen.group is not None):
         return False
     E_, D_, hq, hk, F_, rot = shape_of(gen)
-    if rot not in (0, D_) or gen.max_seq_len > 256 * 16 or gen.act not in ("gelu", "gelu_tanh"):
+    # each split holds ≤ 256 keys (one score per thread)
+    if (rot not in (0, D_) or math.ceil(gen.max_seq_len / 256) > max_splits(B, hq)
+            or gen.act not in ("gelu", "gelu_tanh")):
         return False
     w8 = _w8(gen)
     if w8 is None:
@@ -75,8 +92,8 @@ def eligible(gen, B: int) -> bool:
             t = spec.get(key)
             if t is None or t.dtype != torch.bfloat16:
                 return False
-    return (_lib.available() and _lib.has("piamd_decode_mega_shape_supported")
-            and _lib.lib().piamd_decode_mega_shape_supported(E_, D_, hq, hk, F_, rot, w8) == 1)
+    return (_lib.available() and _lib.has("piamd_decode_mega_batch_supported")
+            and _lib.lib().piamd_decode_mega_batch_supported(E_, D_, hq, hk, F_, rot, w8, B) == 1)
 
 
 def _out_in(lin):
@@ -94,9 +111,10 @@ def _out_in(lin):
 
 
 class MegaDecoder:
-    """Owns the [out, in] weight copies, the per-layer pointer table and the scratch buffers."""
+    """Owns the [out, in] weight copies, the per-layer pointer table and the scratch buffers of
+    the ``nb``-row step."""
 
-    def __init__(self, gen):
+    def __init__(self, gen, nb: int = 1):
         dev = gen.device
         self.gen = gen
         self._keep = []
@@ -119,17 +137,21 @@ class MegaDecoder:
         # phase; the out-projection prologue requests 8 splits' partials at once, so up to 8 the
         # combine stays one load round (round 4, 24 layers: 8 splits 989 µs kernel vs 1 split
         # 1066, 4 splits 1019, 16 splits 1044; profiles/decode_mega_r4.txt)
-        self.nsplit = min(16, max(int(os.environ.get("PIAMD_MEGA_NSPLIT", "8")),
-                                  math.ceil(self.maxS / 256)))
+        self.nb = nb
+        # batched steps keep ~128 attention workgroups (8 // nb splits): the others then stream
+        # their FFN1 slice during the attention phase instead of in the out-projection prologue
+        want = max(1, int(os.environ.get("PIAMD_MEGA_NSPLIT", "8")) // nb)
+        self.nsplit = min(16, max_splits(nb, HQ_), max(want, math.ceil(self.maxS / 256)))
+        assert math.ceil(self.maxS / 256) <= self.nsplit, "max_seq_len too long for the split count"
         # one slot per layer (and per residual update) for every vector handed between
         # workgroups: each address is written once per launch, so readers may use cached loads
         nl, f32, bf = self.nl, dict(dtype=torch.float32, device=dev), dict(dtype=torch.bfloat16, device=dev)
         pstride = (HQ_ * self.nsplit * (D_ + 2) + 63) // 64 * 64
-        self.rbuf = torch.zeros(2 * nl, E_, **bf)
-        self.qn = torch.zeros(nl, HQ_ * D_, **f32)
-        self.kvn = torch.zeros(nl, 2 * HK_ * D_, **f32)
-        self.part = torch.zeros(nl * pstride, **f32)
-        self.h = torch.zeros(nl, F_, **bf)
+        self.rbuf = torch.zeros(2 * nl * nb, E_, **bf)
+        self.qn = torch.zeros(nl * nb, HQ_ * D_, **f32)
+        self.kvn = torch.zeros(nl * nb, 2 * HK_ * D_, **f32)
+        self.part = torch.zeros(nl * nb * pstride, **f32)
+        self.h = torch.zeros(nl * nb, F_, **bf)
         self.neox = 1 if getattr(gen, "neox_rotary", True) else 0
         self.log2_base = math.log2(float(getattr(gen, "rope_base", 10000.0)))
         self.bar = torch.zeros(19 * 64, dtype=torch.int32, device=dev)
@@ -146,11 +168,16 @@ class MegaDecoder:
         # (decode_mega_lw_kernel; kernel 946 vs 968 us, generate 1.042 vs 1.072 ms/token);
         # 0: loader waves that are compute waves too (decode_mega_kernel)
         self.loader = int(os.environ.get("PIAMD_MEGA_LOADER", "1"))
-        if self.loader and ((E_, D_, HQ_, HK_, F_, self.rot, self.w8) != (E, D, HQ, HK, F, 0, 0)
+        # batch 1: GEMV phases on MFMA (1; instantiated for the GPT-1.3B shape) or the VALU (0);
+        # batched steps always run on MFMA
+        self.mm = int(os.environ.get("PIAMD_MEGA_MFMA", "0")) if nb == 1 else 0
+        if self.mm:
+            self.loader = 0
+        if self.loader and ((E_, D_, HQ_, HK_, F_, self.rot, self.w8, nb) != (E, D, HQ, HK, F, 0, 0, 1)
                             or not self._lw_ok()):
             self.loader = 0
         # greedy tail (decode_head_kernel): LM head + argmax + bookkeeping + next embedding
-        self.head_ok = _lib.has("piamd_decode_head_greedy") and self._head_tables(gen)
+        self.head_ok = nb == 1 and _lib.has("piamd_decode_head_greedy") and self._head_tables(gen)
         self.best = torch.zeros(8 * 32, dtype=torch.int64, device=dev)
         self.cnt = torch.zeros(9 * 64, dtype=torch.int32, device=dev)
 
@@ -189,10 +216,12 @@ class MegaDecoder:
         _lib.call("piamd_decode_head_greedy", ctypes.byref(a), E, _lib.stream())
 
     def __call__(self, resid: torch.Tensor, pos: torch.Tensor) -> torch.Tensor:
-        """resid: bf16 [E] embedding output; pos: device int32 [1] = the cache slot of this token.
-        Returns the last layer's residual stream [E] (a view of an internal buffer)."""
-        assert resid.is_contiguous() and resid.numel() == self.E and resid.dtype == torch.bfloat16
-        assert pos.dtype == torch.int32 and pos.is_cuda
+        """resid: bf16 [nb, E] (or [E] at nb = 1) embedding output; pos: device int32 [nb] = each
+        row's cache slot for this token. Returns the last layer's residual stream [nb, E] ([E] at
+        nb = 1; a view of an internal buffer)."""
+        nb = self.nb
+        assert resid.is_contiguous() and resid.numel() == nb * self.E and resid.dtype == torch.bfloat16
+        assert pos.dtype == torch.int32 and pos.is_cuda and pos.is_contiguous() and pos.numel() == nb
         if self.trace is not None:  # the kernel writes 4 int64 slots per (workgroup, phase)
             assert (self.trace.dtype == torch.int64 and self.trace.is_cuda
                     and self.trace.numel() >= 256 * 5 * self.nl * 4), "trace must be int64 [256, 5*nl, 4]"
@@ -201,10 +230,10 @@ class MegaDecoder:
                           self.rbuf.data_ptr(), self.qn.data_ptr(), self.kvn.data_ptr(), self.part.data_ptr(),
                           self.h.data_ptr(), self.bar.data_ptr(), self.err.data_ptr(),
                           pos.data_ptr(), _lib.ptr(self.trace), self.late_dma, self.loader,
-                          self.rot, self.neox, self.log2_base, self.w8)
+                          self.rot, self.neox, self.log2_base, self.w8, nb, self.mm)
         _lib.call("piamd_decode_mega", ctypes.byref(a), self.E, self.D, self.HQ, self.HK, self.F,
                   _lib.stream())
-        return self.rbuf[-1]
+        return self.rbuf[-1] if nb == 1 else self.rbuf[-nb:]
 
     def check(self) -> None:
         """Raise if a grid barrier of an earlier launch timed out (synchronises)."""

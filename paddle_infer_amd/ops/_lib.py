@@ -95,11 +95,13 @@ class MegaArgs(ctypes.Structure):
                 + [("eps", ctypes.c_float), ("scale_log2", ctypes.c_float)]
                 + [(n, c_void_p) for n in ("resid", "rbuf", "qn", "kvn", "part", "h", "bar", "err",
                                         "pos", "trace")] + [("late_dma", c_int), ("loader", c_int)]
-                + [("rot", c_int), ("neox", c_int), ("log2_base", ctypes.c_float), ("w8", c_int)])
+                + [("rot", c_int), ("neox", c_int), ("log2_base", ctypes.c_float), ("w8", c_int),
+                   ("nb", c_int), ("mm", c_int)])
 
 
 _SIGS["piamd_decode_mega"] = [ctypes.POINTER(MegaArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]
 _SIGS["piamd_decode_mega_shape_supported"] = [c_int] * 7
+_SIGS["piamd_decode_mega_batch_supported"] = [c_int] * 8
 
 
 class HeadArgs(ctypes.Structure):

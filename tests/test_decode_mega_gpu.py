@@ -38,16 +38,18 @@ def _rel(a, b):
     return ((a - b).norm() / b.norm()).item()
 
 
-@pytest.mark.parametrize("loader", ["1", "0"])  # dedicated loader wave (default) / 4-wave kernel
+# dedicated loader wave (default) / 4-wave kernel / 4-wave kernel with MFMA GEMV phases
+@pytest.mark.parametrize("loader", ["1", "0", "mfma"])
 @pytest.mark.parametrize("max_seq,prompt", [(256, 37), (1024, 300)])
 def test_mega_decode_matches_per_op_path(max_seq, prompt, loader, monkeypatch):
-    monkeypatch.setenv("PIAMD_MEGA_LOADER", loader)
+    monkeypatch.setenv("PIAMD_MEGA_LOADER", "0" if loader == "mfma" else loader)
+    monkeypatch.setenv("PIAMD_MEGA_MFMA", "1" if loader == "mfma" else "0")
     from paddle_infer_amd.inference import mega_decode
     from paddle_infer_amd.inference.generation import GPTGenerator
     m = _gpt13b_width(2, max_seq)
     g_mega = GPTGenerator(m, max_batch=1, max_seq_len=max_seq, use_hip_graph=False)
     g_ref = GPTGenerator(m, max_batch=1, max_seq_len=max_seq, use_hip_graph=False)
-    g_ref._mega = False  # force the per-op path
+    g_ref.use_mega = False  # force the per-op path
     assert mega_decode.eligible(g_mega, 1) and not mega_decode.eligible(g_mega, 2)
     ids = torch.randint(0, 2048, (1, prompt), device=DEV)
     lens = torch.full((1,), prompt, device=DEV)
@@ -56,14 +58,15 @@ def test_mega_decode_matches_per_op_path(max_seq, prompt, loader, monkeypatch):
     for step in range(6):
         tok = lb.argmax(-1)
         la, lb = g_mega.decode(tok, pos), g_ref.decode(tok, pos)
-        assert isinstance(g_mega._mega, mega_decode.MegaDecoder)
-        assert g_mega._mega.loader == int(loader)
+        assert isinstance(g_mega._mega[1], mega_decode.MegaDecoder)
+        assert g_mega._mega[1].loader == (0 if loader == "mfma" else int(loader))
+        assert g_mega._mega[1].mm == (loader == "mfma")
         assert _rel(la, lb) < 2e-2, (step, _rel(la, lb))
         for (ka, va), (kb, vb) in zip(g_mega.caches, g_ref.caches):
             p = int(pos[0])
             assert _rel(ka[0, :, p], kb[0, :, p]) < 1e-2 and _rel(va[0, :, p], vb[0, :, p]) < 1e-2
         pos += 1
-    g_mega._mega.check()
+    g_mega._mega[1].check()
 
 
 def test_mega_decode_graph_generate_matches_eager():
@@ -76,7 +79,7 @@ def test_mega_decode_graph_generate_matches_eager():
     for _ in range(2):  # second call replays the cached graph
         b = graph.generate(ids, max_new_tokens=12)
         assert torch.equal(a.cpu(), b.cpu()), (a, b)
-    graph._mega.check()
+    graph._mega[1].check()
 
 
 def test_mega_greedy_tail_matches_logits_path():
@@ -90,7 +93,7 @@ def test_mega_greedy_tail_matches_logits_path():
     n = 12
     g = GPTGenerator(m, max_batch=1, max_seq_len=256, use_hip_graph=False)
     out = g.generate(ids, max_new_tokens=n)
-    assert g._mega.head_ok
+    assert g._mega[1].head_ok
     ref = GPTGenerator(m, max_batch=1, max_seq_len=256, use_hip_graph=False)
     logits = ref.prefill(ids, torch.full((1,), 9, device=DEV))
     pos = torch.full((1,), 9, dtype=torch.int32, device=DEV)
@@ -107,7 +110,7 @@ def test_mega_greedy_tail_matches_logits_path():
     out2 = g.generate(ids, max_new_tokens=n, eos_token_id=eos, pad_token_id=7)
     assert torch.equal(out2[0, :k + 1].cpu(), out[0, :k + 1].cpu()), (out, out2)
     assert (out2[0, k + 1:] == 7).all(), out2
-    g._mega.check()
+    g._mega[1].check()
 
 
 @pytest.mark.parametrize("shape", ["gpt3-350m", "gqa4_rope_neox", "gqa4_rope_gptj", "gpt13_rope"])
@@ -126,7 +129,7 @@ def test_mega_decode_other_shapes_match_per_op_path(shape):
     kw = dict(rotary_dim=m.cfg.head_dim, neox_rotary=rope) if rope is not None else {}
     g_mega = GPTGenerator(m, max_batch=1, max_seq_len=512, use_hip_graph=False, **kw)
     g_ref = GPTGenerator(m, max_batch=1, max_seq_len=512, use_hip_graph=False, **kw)
-    g_ref._mega = False
+    g_ref.use_mega = False
     assert mega_decode.eligible(g_mega, 1), mega_decode.shape_of(g_mega)
     prompt = 77
     ids = torch.randint(0, 2048, (1, prompt), device=DEV)
@@ -136,13 +139,13 @@ def test_mega_decode_other_shapes_match_per_op_path(shape):
     for step in range(5):
         tok = lb.argmax(-1)
         la, lb = g_mega.decode(tok, pos), g_ref.decode(tok, pos)
-        assert isinstance(g_mega._mega, mega_decode.MegaDecoder) and g_mega._mega.loader == 0
+        assert isinstance(g_mega._mega[1], mega_decode.MegaDecoder) and g_mega._mega[1].loader == 0
         assert _rel(la, lb) < 2e-2, (step, _rel(la, lb))
         for (ka, va), (kb, vb) in zip(g_mega.caches, g_ref.caches):
             p = int(pos[0])
             assert _rel(ka[0, :, p], kb[0, :, p]) < 1e-2 and _rel(va[0, :, p], vb[0, :, p]) < 1e-2
         pos += 1
-    g_mega._mega.check()
+    g_mega._mega[1].check()
 
 
 def test_mega_decode_shape_gate():
@@ -153,6 +156,9 @@ def test_mega_decode_shape_gate():
     assert f(2048, 128, 16, 16, 8192, 0, 1) == 1 and f(2048, 128, 16, 4, 8192, 128, 1) == 1
     assert f(2560, 80, 32, 32, 10240, 0, 0) == 0 and f(2048, 128, 16, 8, 8192, 0, 0) == 0
     assert f(1024, 64, 16, 16, 4096, 0, 1) == 0
+    fb = _lib.lib().piamd_decode_mega_batch_supported
+    assert fb(2048, 128, 16, 16, 8192, 0, 0, 2) == 1 and fb(2048, 128, 16, 4, 8192, 128, 0, 4) == 1
+    assert fb(2048, 128, 16, 16, 8192, 0, 0, 3) == 0 and fb(2048, 128, 16, 16, 8192, 0, 1, 2) == 0
 
 
 @pytest.mark.parametrize("shape", ["gpt13_int8", "gqa4_rope_int8"])
@@ -167,7 +173,7 @@ def test_mega_decode_int8_weight_only_matches_per_op_path(shape):
     m = _gpt13b_width(2, 512, "gpt3-1.3b", **over)
     g_mega = GPTGenerator(m, max_batch=1, max_seq_len=512, use_hip_graph=False, weight_only="int8", **kw)
     g_ref = GPTGenerator(m, max_batch=1, max_seq_len=512, use_hip_graph=False, weight_only="int8", **kw)
-    g_ref._mega = False
+    g_ref.use_mega = False
     assert mega_decode.eligible(g_mega, 1)
     prompt = 50
     ids = torch.randint(0, 2048, (1, prompt), device=DEV)
@@ -177,7 +183,64 @@ def test_mega_decode_int8_weight_only_matches_per_op_path(shape):
     for step in range(4):
         tok = lb.argmax(-1)
         la, lb = g_mega.decode(tok, pos), g_ref.decode(tok, pos)
-        assert g_mega._mega.w8 == 1 and g_mega._mega.loader == 0
+        assert g_mega._mega[1].w8 == 1 and g_mega._mega[1].loader == 0
         assert _rel(la, lb) < 2e-2, (step, _rel(la, lb))
         pos += 1
-    g_mega._mega.check()
+    g_mega._mega[1].check()
+
+
+@pytest.mark.parametrize("B", [2, 4])
+@pytest.mark.parametrize("shape", ["gpt13", "gpt3-350m", "gqa4_rope_neox"])
+def test_mega_decode_batched_rows_match_per_op_path(shape, B):
+    """Batched single-launch steps (MegaCfg NB = 2 / 4: one LDS weight slice applied to every row,
+    one attention workgroup per (row, head, split)) with a different prompt length per row — each
+    row attends over its own cache length and writes its own slot — against the per-op path."""
+    from paddle_infer_amd.inference import mega_decode
+    from paddle_infer_amd.inference.generation import GPTGenerator
+    preset, over, rope = {"gpt13": ("gpt3-1.3b", {}, None),
+                          "gpt3-350m": ("gpt3-350m", {}, None),
+                          "gqa4_rope_neox": ("gpt3-1.3b", {"num_kv_heads": 4}, True)}[shape]
+    m = _gpt13b_width(2, 512, preset, **over)
+    kw = dict(rotary_dim=m.cfg.head_dim, neox_rotary=rope) if rope is not None else {}
+    g_mega = GPTGenerator(m, max_batch=B, max_seq_len=512, use_hip_graph=False, **kw)
+    g_ref = GPTGenerator(m, max_batch=B, max_seq_len=512, use_hip_graph=False, **kw)
+    g_ref.use_mega = False
+    assert mega_decode.eligible(g_mega, B) and not mega_decode.eligible(g_mega, 3)
+    torch.manual_seed(5)
+    lens = torch.tensor([61, 200, 3, 130][:B], device=DEV)
+    ids = torch.randint(0, 2048, (B, int(lens.max())), device=DEV)
+    la, lb = g_mega.prefill(ids, lens), g_ref.prefill(ids, lens)
+    pos = lens.to(torch.int32)
+    for step in range(4):
+        tok = lb.argmax(-1)
+        la, lb = g_mega.decode(tok, pos), g_ref.decode(tok, pos)
+        mg = g_mega._mega[B]
+        assert isinstance(mg, mega_decode.MegaDecoder) and mg.nb == B and mg.loader == 0
+        for b in range(B):
+            assert _rel(la[b], lb[b]) < 2e-2, (step, b, _rel(la[b], lb[b]))
+        for (ka, va), (kb, vb) in zip(g_mega.caches, g_ref.caches):
+            for b in range(B):
+                p = int(pos[b])
+                assert _rel(ka[b, :, p], kb[b, :, p]) < 1e-2 and _rel(va[b, :, p], vb[b, :, p]) < 1e-2
+        pos = pos + 1
+    g_mega._mega[B].check()
+
+
+def test_mega_decode_batched_generate_and_beams():
+    """generate() at batch 2 (greedy, eager loop over the batched step) matches the per-op
+    generator token for token, and beam search with 4 beams (beams are batch rows) runs on the
+    4-row step."""
+    from paddle_infer_amd.inference.generation import GPTGenerator
+    m = _gpt13b_width(2, 256)
+    torch.manual_seed(9)
+    ids = torch.randint(0, 2048, (2, 11), device=DEV)
+    a = GPTGenerator(m, max_batch=4, max_seq_len=256, use_hip_graph=False)
+    ref = GPTGenerator(m, max_batch=4, max_seq_len=256, use_hip_graph=False)
+    ref.use_mega = False
+    out_a, out_r = a.generate(ids, max_new_tokens=8), ref.generate(ids, max_new_tokens=8)
+    assert a._mega.get(2), a._mega
+    # bf16 near-ties may flip a late token; the first steps must agree
+    assert torch.equal(out_a[:, :4].cpu(), out_r[:, :4].cpu()), (out_a, out_r)
+    b = a.generate(ids[:1], max_new_tokens=6, num_beams=4)
+    assert a._mega.get(4) and b.shape == (1, 6)
+    a._mega[4].check()

@@ -74,9 +74,10 @@ def main():
                  "prefill_tok_s": round(B * a.prompt / t_pre, 1),
                  "decode_ms_per_step": round(t_dec / a.gen * 1e3, 4),
                  "decode_tok_s": round(B * a.gen / t_dec, 1)}
-            if getattr(gen, "_mega", None):
+            mega = gen._mega.get(B)
+            if mega:
                 r["mega_decode"] = True
-                r["mega_timeouts"] = int(gen._mega.err.item())
+                r["mega_timeouts"] = int(mega.err.item())
             print(json.dumps(r), flush=True)
             rows.append(r)
         del gen

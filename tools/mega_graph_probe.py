@@ -17,9 +17,9 @@ model = model.cuda().to(torch.bfloat16).eval()
 gen = GPTGenerator(model, max_batch=1, max_seq_len=264, use_hip_graph=True)
 LAZY, TRACE = "--lazy" in sys.argv, "--notrace" not in sys.argv
 if not LAZY:
-    gen._mega = MegaDecoder(gen)
+    gen._mega[1] = MegaDecoder(gen)
     if TRACE:
-        gen._mega.trace = torch.zeros(256, 5 * gen._mega.nl, 4, dtype=torch.int64, device="cuda")
+        gen._mega[1].trace = torch.zeros(256, 5 * gen._mega[1].nl, 4, dtype=torch.int64, device="cuda")
 ids = torch.randint(0, cfg.vocab_size, (1, 128), device="cuda")
 lens = torch.full((1,), 128, device="cuda")
 gen.generate(ids, lens, max_new_tokens=4)
@@ -35,7 +35,7 @@ for i in range(16):
     tok = logits.argmax(-1)
 torch.cuda.synchronize()
 print("lazy", LAZY, "trace", TRACE, "ms/step", (time.perf_counter() - t0) / 16 * 1e3,
-      "timeouts", int(gen._mega.err.item()))
+      "timeouts", int(gen._mega[1].err.item()))
 if "--eager-after" in sys.argv:  # same process, same generator, no graph
     gen.use_graph = False
     torch.cuda.synchronize(); t0 = time.perf_counter()
@@ -46,8 +46,8 @@ if "--eager-after" in sys.argv:  # same process, same generator, no graph
     print("eager-after ms/step", (time.perf_counter() - t0) / 16 * 1e3)
 if LAZY or not TRACE:
     sys.exit(0)
-nl = gen._mega.nl
-tr = gen._mega.trace.cpu().double() * 0.01  # µs
+nl = gen._mega[1].nl
+tr = gen._mega[1].trace.cpu().double() * 0.01  # µs
 st, pro, gem, arr = tr[..., 0], tr[..., 1], tr[..., 2], tr[..., 3]
 t0 = st[:, 0].min()
 for p in list(range(0, 10)) + [5 * nl - 2]:

@@ -84,7 +84,9 @@ struct MegaArgs {
   const int* pos;       // [1] cache slot of the new token
   u64* trace;           // nullable: [NWG][5·nl][4] wall-clock (100 MHz): phase start, prologue done,
                         // GEMV done, barrier arrival
-  int late_dma;         // 1: the FFN phases issue the next slice only after their GEMV (A/B knob)
+  int late_dma;         // bit 0: the FFN phases issue the next slice only after their GEMV; bit 1:
+                        // attention workgroups queue their FFN1 head in the out prologue instead
+                        // of at the end of the attention phase (decode_mega_kernel; A/B knobs)
   int loader;           // 1: decode_mega_lw_kernel (dedicated loader wave, 16 KiB chunk ring)
   int rot;              // rotary dims: 0 or D (whole head)
   int neox;             // 1: rotate-half (NeoX), 0: interleaved pairs (GPT-J)
@@ -92,7 +94,7 @@ struct MegaArgs {
   int w8;               // 1: int8 weight-only projections (MegaLayer scales)
   int nb;               // batch rows per step (1, 2 or 4): resid / rbuf / qn / kvn / part / h hold
                         // nb rows per slot, pos nb entries, the caches are [rows][HK][maxS][D]
-  int mm;               // batch 1: 1 = MFMA GEMV phases (MegaCfg MM; instantiated shapes only)
+  int mm;               // 1 = MFMA GEMV phases, 0 = VALU (MegaCfg MM; the instantiated variant)
 };
 
 __device__ __forceinline__ u64 ld64(const void* p) { return *reinterpret_cast<const u64*>(p); }
@@ -362,27 +364,45 @@ __device__ __forceinline__ void prefetch_p(const bf16_t* src, int from, int to, 
 // for tid < NPW; `mid` and `end` both run once the whole slice is consumed). The activation rows
 // are staged in LDS (`xs`: NB rows of KP = min(K, 8192 / NB) k, 16-B padded; one pass for every
 // K ≤ KP, else K / KP passes); each wave takes a quarter of a pass's k and runs
-// mfma_f32_16x16x32_bf16 over column tiles of 16: A = activations (rows ≥ NB zero), B = the
-// weight rows straight from the padded LDS image (one 16-B read per lane, conflict-free thanks
-// to the row padding). Operands are read SB k-steps at a time, the next batch's reads issued
-// before this batch's MFMAs (one wave per SIMD: nothing else hides the LDS latency). The four
-// waves' partial sums meet in `red`. No per-column butterfly and no bf16 → f32 converts: NB rows
-// cost the same MFMAs as one.
+// mfma_f32_16x16x32_bf16 over column tiles of 16: A = activations, B = the weight rows straight
+// from the padded LDS image (one 16-B read per lane, conflict-free thanks to the row padding).
+// Slices narrower than a tile (NPW = 8 / 4) put HS = 16 / NPW k-sets of the wave's range side by
+// side instead of idle columns: A row b·HS + h holds row b's activations of k-set h, B column
+// h·NPW + c column c's weights of k-set h, and only those diagonal blocks of C are kept. A rows /
+// B columns past the real ones read a clamped (valid) row and land in C entries nobody keeps, so
+// no read is predicated. Operands are read SB k-steps at a time, the next batch's reads issued
+// before this batch's MFMAs (one wave per SIMD: nothing else hides the LDS latency). The partial
+// sums (4 waves × HS k-sets) meet in `red`. No per-column butterfly and no bf16 → f32 converts:
+// NB rows cost the same MFMAs as one.
 template <int NPW, int K, int NB, int RS, class Mid, class End>
 __device__ __forceinline__ void gemv_mfma(const char* ws, const float (&x)[NB][(K + 2047) / 2048][8], float* red,
                                           bf16_t* xs, int tid, Mid mid, End end, float (&r)[NB]) {
   constexpr int KPM = 8192 / NB;
-  constexpr int KP = K < KPM ? K : KPM;        // k per staging pass
+  constexpr int KP = K < KPM ? K : KPM;           // k per staging pass
   constexpr int JP = KP >= 2048 ? KP / 2048 : 1;  // thread x-chunks per pass
   constexpr int NPASS = K / KP;
-  constexpr int XS = KP + 8;                   // xs row stride (elements)
-  constexpr int NCT = (NPW + 15) / 16;         // column tiles
-  constexpr int SPW = KP / 128;                // k-steps per wave per pass
-  constexpr int SB = NCT == 1 ? 8 : 4;         // k-steps per operand batch
+  constexpr int XS = KP + 8;                      // xs row stride (elements)
+  constexpr int HS = NPW >= 16 ? 1 : 16 / NPW;    // k-sets side by side in a tile
+  constexpr int NCT = NPW >= 16 ? (NPW + 15) / 16 : 1;  // column tiles
+  constexpr int P = NPW >= 16 ? NCT * 16 : NPW;   // red row length
+  constexpr int DK = KP / 4 / HS;                 // k per k-set of a wave's quarter
+  constexpr int SPW = DK / 32;                    // k-steps per wave per pass
+  constexpr int SB0 = NCT == 1 ? 8 : 4;
+  constexpr int SB = SPW < SB0 ? SPW : SB0;       // k-steps per operand batch
   constexpr int NBT = SPW / SB;
-  constexpr int P = NCT * 16;
-  static_assert(NPW <= 32 && K % 1024 == 0 && NB <= 4 && K % KP == 0 && SPW % SB == 0, "gemv_mfma shape");
+  static_assert(NPW <= 32 && K % 1024 == 0 && NB <= 4 && NB * HS <= 16 && K % KP == 0 && SPW % SB == 0,
+                "gemv_mfma shape");
   const int lane = tid & 63, wv = tid >> 6, lr = lane & 15, g = lane >> 4;
+  // per-lane operand bases (every k-step is then a constant offset)
+  const int arow = lr < NB * HS ? lr : NB * HS - 1;
+  const bf16_t* ap = xs + (arow / HS) * XS + wv * (KP / 4) + (arow % HS) * DK + g * 8;
+  const char* bp[NCT];
+#pragma unroll
+  for (int t = 0; t < NCT; ++t) {
+    const int c = NPW >= 16 ? (t * 16 + lr < NPW ? t * 16 + lr : NPW - 1) : lr % NPW;
+    const int h = NPW >= 16 ? 0 : lr / NPW;
+    bp[t] = ws + (long)c * RS + (wv * (KP / 4) + h * DK + g * 8) * 2;
+  }
   f32x4 acc[NCT];
 #pragma unroll
   for (int t = 0; t < NCT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -403,20 +423,13 @@ __device__ __forceinline__ void gemv_mfma(const char* ws, const float (&x)[NB][(
       }
     }
     __syncthreads();
-    const int kw = wv * (KP / 4) + g * 8;
     auto load = [&](int bt, u16x8 (&av)[SB], u16x8 (&bw)[SB][NCT]) {
 #pragma unroll
       for (int u = 0; u < SB; ++u) {
-        const int k = kw + (bt * SB + u) * 32;
-        av[u] = u16x8{};
-        if (lr < NB) av[u] = *reinterpret_cast<const u16x8*>(xs + lr * XS + k);
+        const int st = bt * SB + u;
+        av[u] = *reinterpret_cast<const u16x8*>(ap + st * 32);
 #pragma unroll
-        for (int t = 0; t < NCT; ++t) {
-          const int c = t * 16 + lr;
-          bw[u][t] = u16x8{};
-          if (NPW % 16 == 0 || c < NPW)
-            bw[u][t] = *reinterpret_cast<const u16x8*>(ws + (long)c * RS + (long)(q * KP + k) * 2);
-        }
+        for (int t = 0; t < NCT; ++t) bw[u][t] = *reinterpret_cast<const u16x8*>(bp[t] + (q * KP + st * 32) * 2);
       }
     };
     u16x8 a0[SB], b0[SB][NCT];
@@ -441,12 +454,18 @@ __device__ __forceinline__ void gemv_mfma(const char* ws, const float (&x)[NB][(
       }
     }
   }
-  // C[row (g·4 + i)][col lr]: rows 0..3 (the batch rows) sit in lanes 0-15
-  if (g == 0) {
+  // C[row g·4 + i][col lr]; row = b·HS + h is kept where col belongs to k-set h
 #pragma unroll
-    for (int b = 0; b < NB; ++b)
+  for (int i = 0; i < 4; ++i) {
+    const int row = g * 4 + i, b = row / HS, h = row % HS;
+    if (row < NB * HS) {
 #pragma unroll
-      for (int t = 0; t < NCT; ++t) red[(wv * NB + b) * P + t * 16 + lr] = acc[t][b];
+      for (int t = 0; t < NCT; ++t) {
+        const int c = NPW >= 16 ? t * 16 + lr : lr % NPW;
+        const bool keep = NPW >= 16 ? c < NPW : lr / NPW == h;
+        if (keep) red[((wv * HS + h) * NB + b) * P + c] = acc[t][i];
+      }
+    }
   }
   __syncthreads();
   mid();
@@ -454,9 +473,10 @@ __device__ __forceinline__ void gemv_mfma(const char* ws, const float (&x)[NB][(
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     r[b] = 0.f;
-    if (tid < NPW)
-      r[b] = red[b * P + tid] + red[(NB + b) * P + tid] + red[(2 * NB + b) * P + tid] +
-             red[(3 * NB + b) * P + tid];
+    if (tid < NPW) {
+#pragma unroll
+      for (int wh = 0; wh < 4 * HS; ++wh) r[b] += red[(wh * NB + b) * P + tid];
+    }
   }
 }
 
@@ -466,9 +486,9 @@ __device__ __forceinline__ void gemv_mfma(const char* ws, const float (&x)[NB][(
 // and the new k. Every projection splits its output columns evenly over the 256 workgroups and
 // each workgroup's weight slice must fit the 128 KiB LDS image.
 // NB: batch rows per step (each GEMV phase applies its LDS slice to all NB rows; attention runs
-// one workgroup per (row, head, split)). MM: the GEMV phases run on MFMA (gemv_mfma; bf16 only),
-// else on the VALU (gemv_lds; the batch-1 default).
-template <int E_, int D_, int HQ_, int HK_, int F_, int ROT_, int W8_ = 0, int NB_ = 1, int MM_ = (NB_ > 1)>
+// one workgroup per (row, head, split)). MM: the GEMV phases run on MFMA (gemv_mfma; bf16 only,
+// the default), else on the VALU (gemv_lds; int8 weight-only).
+template <int E_, int D_, int HQ_, int HK_, int F_, int ROT_, int W8_ = 0, int NB_ = 1, int MM_ = (W8_ == 0)>
 struct MegaCfg {
   static constexpr int E = E_, D = D_, HQ = HQ_, HK = HK_, F = F_, ROT = ROT_, W8 = W8_, NB = NB_, MM = MM_;
   static_assert(NB == 1 || NB == 2 || NB == 4, "rows per step");
@@ -747,16 +767,19 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
         }
         if (lane == 0) st64(dst + D, pack2f(n > 0 ? m : -INFINITY, n > 0 ? lsum : 0.f));
       }
+      // K/V are consumed: the loader waves queue the FFN1 head now, behind wave 0's partial
+      // stores and grid barrier, so it no longer stalls their out-projection GEMV work
+      if (!(a.late_dma & 2)) prefetch_p<RBE>(w1s, 0, C::F1PRE, wl, wv, lane);
     } else {
       prefetch_p<RBE>(w1s, 0, C::F1PRE, wl, wv, lane);
     }
     if (wv == 0) grid_sync(a, ++nbar, lane); else ++nbar;
     // ---------------------------------------------------------------- out projection
-    // attention workgroups queue their FFN1 DMA only now (their loader waves carried K/V loads):
-    // every older load has to land; the others issued it at the attention phase start and wait
-    // for the out slice only
-    const bool attn_wg = w < NB * HQ * a.nsplit;
-    phase_start<C::WAIT_OLD>(a, wv, nbar, attn_wg ? WAIT_ALL : WAIT_OLDER);
+    // every workgroup has its FFN1 head in flight (queued at the attention phase start, or at its
+    // end by attention workgroups) and waits for the older out slice only; with late_dma bit 1 the
+    // attention workgroups queue the head only here (every older load has to land first)
+    const bool attn_late = w < NB * HQ * a.nsplit && (a.late_dma & 2);
+    phase_start<C::WAIT_OLD>(a, wv, nbar, attn_late ? WAIT_ALL : WAIT_OLDER);
     {
       const int ocol = w * NPO + (lane & (NPO - 1));
       const float bo = bf2f(Ly.bo[ocol]);
@@ -816,7 +839,7 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
           for (int i = 0; i < 8; ++i) x[b][0][i] = on ? bf2f(f2bf(o[b][i] * inv)) : 0.f;
         }
       }
-      if (attn_wg) prefetch_p<RBE>(w1s, 0, C::F1PRE, wl, wv, lane);
+      if (attn_late) prefetch_p<RBE>(w1s, 0, C::F1PRE, wl, wv, lane);
       tmark(a, nbar, 1);
       float y[NB];
       gemv_phase<C, NPO, E, RSE>(wl + C::OUT_OFF, x, red, xs, tid, [] {}, [&] {
@@ -840,7 +863,7 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
       ln_prologue<E, NB>(a, rmid, Ly.ln2_g, Ly.ln2_b, x, wred, tid);
       tmark(a, nbar, 1);
       const bf16_t* w2s = slice(Ly.w2, (long)w * NP2, F);
-      const int mid = a.late_dma ? 0 : C::MID1;
+      const int mid = (a.late_dma & 1) ? 0 : C::MID1;
       float y[NB];
       gemv_phase<C, NP1, E, RSE>(wl, x, red, xs, tid, [&] { prefetch_p<RBF>(w2s, 0, mid, wl, wv, lane); },
                                  [&] { prefetch_p<RBF>(w2s, mid, C::F2B, wl, wv, lane); }, y);
@@ -873,7 +896,7 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
         for (int j = 0; j < KCH2; ++j) ld_bf8(hb + b * F + (j * 256 + tid) * 8, x[b][j]);
       tmark(a, nbar, 1);
       const bf16_t* nq = l + 1 < a.nl ? slice(a.layers[l + 1].wqkv, (long)w * NPQ, E) : nullptr;
-      const int mid = a.late_dma ? 0 : C::MID2;
+      const int mid = (a.late_dma & 1) ? 0 : C::MID2;
       float y[NB];
       gemv_phase<C, NP2, F, RSF>(wl, x, red, xs, tid, [&] { prefetch_p<RBE>(nq, 0, mid, wl, wv, lane); },
                                  [&] { prefetch_p<RBE>(nq, mid, C::QB, wl, wv, lane); }, y);
@@ -1467,7 +1490,8 @@ static int coop_ok(const void* fn, int threads) {
   return r;
 }
 
-// The instantiated model shapes (E, D, Hq, Hk, F) × rotary off / on.
+// The instantiated model shapes (E, D, Hq, Hk, F) × rotary off / on; bf16 weights run the GEMV
+// phases on MFMA (MegaCfg MM default), int8 weight-only on the VALU.
 typedef MegaCfg<2048, 128, 16, 16, 8192, 0> CfgGpt13;    // GPT-3 1.3B
 typedef MegaCfg<2048, 128, 16, 16, 8192, 1> CfgGpt13R;
 typedef MegaCfg<2048, 128, 16, 4, 8192, 0> CfgGqa4;      // 1.3B width, 4 KV heads (GQA 4:1)
@@ -1476,28 +1500,42 @@ typedef MegaCfg<1024, 64, 16, 16, 4096, 0> CfgGpt350;    // GPT-3 350M
 typedef MegaCfg<1024, 64, 16, 16, 4096, 1> CfgGpt350R;
 typedef MegaCfg<2048, 128, 16, 16, 8192, 0, 1> CfgGpt13W8;  // int8 weight-only
 typedef MegaCfg<2048, 128, 16, 4, 8192, 1, 1> CfgGqa4RW8;
+typedef MegaCfg<2048, 128, 16, 16, 8192, 0, 0, 1, 0> CfgGpt13V;  // 1.3B on the VALU (A/B)
 // batched steps (2 / 4 rows: small serving batches, beams)
 typedef MegaCfg<2048, 128, 16, 16, 8192, 0, 0, 2> CfgGpt13B2;
 typedef MegaCfg<2048, 128, 16, 16, 8192, 0, 0, 4> CfgGpt13B4;
+typedef MegaCfg<2048, 128, 16, 16, 8192, 1, 0, 2> CfgGpt13RB2;
+typedef MegaCfg<2048, 128, 16, 16, 8192, 1, 0, 4> CfgGpt13RB4;
+typedef MegaCfg<2048, 128, 16, 4, 8192, 0, 0, 2> CfgGqa4B2;
+typedef MegaCfg<2048, 128, 16, 4, 8192, 0, 0, 4> CfgGqa4B4;
 typedef MegaCfg<2048, 128, 16, 4, 8192, 1, 0, 2> CfgGqa4RB2;
 typedef MegaCfg<2048, 128, 16, 4, 8192, 1, 0, 4> CfgGqa4RB4;
 typedef MegaCfg<1024, 64, 16, 16, 4096, 0, 0, 2> CfgGpt350B2;
 typedef MegaCfg<1024, 64, 16, 16, 4096, 0, 0, 4> CfgGpt350B4;
-typedef MegaCfg<2048, 128, 16, 16, 8192, 0, 0, 1, 1> CfgGpt13M;  // batch 1 on MFMA (A/B)
+typedef MegaCfg<1024, 64, 16, 16, 4096, 1, 0, 2> CfgGpt350RB2;
+typedef MegaCfg<1024, 64, 16, 16, 4096, 1, 0, 4> CfgGpt350RB4;
 
-static const void* mega_fn(int E_, int D_, int hq, int hk, int F_, int rot, int w8, int nb, int mm = 0) {
+// mm: 1 = MFMA GEMV phases, 0 = VALU, -1 = whichever is instantiated (MFMA first)
+static const void* mega_fn(int E_, int D_, int hq, int hk, int F_, int rot, int w8, int nb, int mm = -1) {
 #define MEGA_CFG(C)                                                                           \
   if (E_ == C::E && D_ == C::D && hq == C::HQ && hk == C::HK && F_ == C::F &&                 \
-      (rot != 0) == C::ROT && (w8 != 0) == C::W8 && nb == C::NB && (nb > 1 || (mm != 0) == C::MM)) \
+      (rot != 0) == C::ROT && (w8 != 0) == C::W8 && nb == C::NB && (mm < 0 || (mm != 0) == C::MM)) \
     return (const void*)decode_mega_kernel<C>;
   MEGA_CFG(CfgGpt13) MEGA_CFG(CfgGpt13R) MEGA_CFG(CfgGqa4) MEGA_CFG(CfgGqa4R)
-  MEGA_CFG(CfgGpt350) MEGA_CFG(CfgGpt350R) MEGA_CFG(CfgGpt13W8) MEGA_CFG(CfgGqa4RW8)
-  MEGA_CFG(CfgGpt13B2) MEGA_CFG(CfgGpt13B4) MEGA_CFG(CfgGqa4RB2) MEGA_CFG(CfgGqa4RB4)
-  MEGA_CFG(CfgGpt350B2) MEGA_CFG(CfgGpt350B4) MEGA_CFG(CfgGpt13M)
+  MEGA_CFG(CfgGpt350) MEGA_CFG(CfgGpt350R) MEGA_CFG(CfgGpt13W8) MEGA_CFG(CfgGqa4RW8) MEGA_CFG(CfgGpt13V)
+  MEGA_CFG(CfgGpt13B2) MEGA_CFG(CfgGpt13B4) MEGA_CFG(CfgGpt13RB2) MEGA_CFG(CfgGpt13RB4)
+  MEGA_CFG(CfgGqa4B2) MEGA_CFG(CfgGqa4B4) MEGA_CFG(CfgGqa4RB2) MEGA_CFG(CfgGqa4RB4)
+  MEGA_CFG(CfgGpt350B2) MEGA_CFG(CfgGpt350B4) MEGA_CFG(CfgGpt350RB2) MEGA_CFG(CfgGpt350RB4)
 #undef MEGA_CFG
   return nullptr;
 }
 
+// 1 when the variant (GEMV kind mm as in mega_fn) is instantiated and this device can run it.
+PIAMD_EXPORT int piamd_decode_mega_variant_supported(int E_, int D_, int hq, int hk, int F_, int rot, int w8,
+                                                     int nb, int mm) {
+  const void* fn = mega_fn(E_, D_, hq, hk, F_, rot, w8, nb, mm);
+  return fn != nullptr && coop_ok(fn, NT);
+}
 // 1 when this device can run the single-launch step for the shape at `nb` rows: an instantiated
 // shape, cooperative launches supported and all NWG workgroups co-resident.
 PIAMD_EXPORT int piamd_decode_mega_batch_supported(int E_, int D_, int hq, int hk, int F_, int rot, int w8,

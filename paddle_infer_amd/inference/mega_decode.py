@@ -164,22 +164,28 @@ class MegaDecoder:
         # stalls their issue for ~2 us (FFN1 / FFN2 GEMV 5.1 / 4.5 us -> 2.7 / 1.8 us late; kernel
         # 985 -> 956 us, profiles/decode_mega_r4.txt)
         self.late_dma = int(os.environ.get("PIAMD_MEGA_LATE_DMA", "1"))
-        # 1 (default): the variant with a dedicated loader wave and a 16 KiB chunk ring
-        # (decode_mega_lw_kernel; kernel 946 vs 968 us, generate 1.042 vs 1.072 ms/token);
-        # 0: loader waves that are compute waves too (decode_mega_kernel)
-        self.loader = int(os.environ.get("PIAMD_MEGA_LOADER", "1"))
-        # batch 1: GEMV phases on MFMA (1; instantiated for the GPT-1.3B shape) or the VALU (0);
-        # batched steps always run on MFMA
-        self.mm = int(os.environ.get("PIAMD_MEGA_MFMA", "0")) if nb == 1 else 0
-        if self.mm:
-            self.loader = 0
+        # 1: the variant with a dedicated loader wave and a 16 KiB chunk ring (decode_mega_lw_kernel,
+        # VALU GEMVs; round 4: kernel 946 vs 968 us against the VALU 4-wave kernel); 0 (default):
+        # the 4-wave templated kernel (decode_mega_kernel), whose MFMA GEMV phases now beat it
+        self.loader = int(os.environ.get("PIAMD_MEGA_LOADER", "0"))
+        # GEMV phases on MFMA (1, default for bf16: 16 weight columns × 32 k per instruction, no
+        # per-column butterfly; kernel 869 vs 976 µs on the VALU, profiles/decode_mega_r5.txt)
+        # or the VALU (0; int8 weight-only, the loader-wave variant)
+        self.mm = 0 if (self.w8 or self.loader) else int(os.environ.get("PIAMD_MEGA_MFMA", "1"))
+        if not self._variant_ok(self.mm):
+            self.mm = 1 - self.mm
         if self.loader and ((E_, D_, HQ_, HK_, F_, self.rot, self.w8, nb) != (E, D, HQ, HK, F, 0, 0, 1)
                             or not self._lw_ok()):
             self.loader = 0
+            self.mm = 0 if self.w8 else 1
         # greedy tail (decode_head_kernel): LM head + argmax + bookkeeping + next embedding
         self.head_ok = nb == 1 and _lib.has("piamd_decode_head_greedy") and self._head_tables(gen)
         self.best = torch.zeros(8 * 32, dtype=torch.int64, device=dev)
         self.cnt = torch.zeros(9 * 64, dtype=torch.int32, device=dev)
+
+    def _variant_ok(self, mm: int) -> bool:
+        return _lib.lib().piamd_decode_mega_variant_supported(
+            self.E, self.D, self.HQ, self.HK, self.F, self.rot, self.w8, self.nb, mm) == 1
 
     @staticmethod
     def _lw_ok() -> bool:

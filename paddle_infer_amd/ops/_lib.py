@@ -102,6 +102,7 @@ class MegaArgs(ctypes.Structure):
 _SIGS["piamd_decode_mega"] = [ctypes.POINTER(MegaArgs), c_int, c_int, c_int, c_int, c_int, c_void_p]
 _SIGS["piamd_decode_mega_shape_supported"] = [c_int] * 7
 _SIGS["piamd_decode_mega_batch_supported"] = [c_int] * 8
+_SIGS["piamd_decode_mega_variant_supported"] = [c_int] * 9
 
 
 class HeadArgs(ctypes.Structure):

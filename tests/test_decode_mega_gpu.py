@@ -159,6 +159,10 @@ def test_mega_decode_shape_gate():
     fb = _lib.lib().piamd_decode_mega_batch_supported
     assert fb(2048, 128, 16, 16, 8192, 0, 0, 2) == 1 and fb(2048, 128, 16, 4, 8192, 128, 0, 4) == 1
     assert fb(2048, 128, 16, 16, 8192, 0, 0, 3) == 0 and fb(2048, 128, 16, 16, 8192, 0, 1, 2) == 0
+    fv = _lib.lib().piamd_decode_mega_variant_supported  # GEMV kind: 1 MFMA, 0 VALU
+    assert fv(2048, 128, 16, 16, 8192, 0, 0, 1, 1) == 1 and fv(2048, 128, 16, 16, 8192, 0, 0, 1, 0) == 1
+    assert fv(1024, 64, 16, 16, 4096, 0, 0, 1, 0) == 0 and fv(2048, 128, 16, 16, 8192, 0, 1, 1, 1) == 0
+    assert fv(2048, 128, 16, 16, 8192, 0, 0, 4, 0) == 0 and fv(1024, 64, 16, 16, 4096, 64, 0, 4, 1) == 1
 
 
 @pytest.mark.parametrize("shape", ["gpt13_int8", "gqa4_rope_int8"])

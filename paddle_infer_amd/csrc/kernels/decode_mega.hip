@@ -294,7 +294,7 @@ __device__ __forceinline__ void block_sum_n(float (&v)[N], float* red) {
 }
 
 // x_b = bf16(LN(resid_b)) for NB rows r + b·EE, this thread's 8 elements k = 8·tid (threads with
-// 8·tid ≥ EE hold 0). The rows' means (then variances) share one block reduction.
+// 8·tid ≥ EE hold 0). Every row's (Σv, Σv²) share one block reduction (`wred`: 8·NB floats).
 template <int EE, int NB>
 __device__ __forceinline__ void ln_prologue(const MegaArgs& a, const bf16_t* r, const bf16_t* g,
                                             const bf16_t* b, float (&x)[NB][1][8], float* wred, int tid) {
@@ -313,28 +313,25 @@ __device__ __forceinline__ void ln_prologue(const MegaArgs& a, const bf16_t* r, 
 #pragma unroll
     for (int n = 0; n < NB; ++n) ld_bf8(r + (long)n * EE + tid * 8, v[n]);
   }
-  float mean[NB], q[NB];
+  // one reduction of (Σv, Σv²) per row: var = E[v²] − mean² (f32 over ≤ 2048 bf16 values)
+  float sq[2 * NB];
 #pragma unroll
   for (int n = 0; n < NB; ++n) {
-    mean[n] = 0.f;
+    sq[n] = sq[NB + n] = 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) mean[n] += v[n][i];
+    for (int i = 0; i < 8; ++i) {
+      sq[n] += v[n][i];
+      sq[NB + n] += v[n][i] * v[n][i];
+    }
   }
-  block_sum_n<NB>(mean, wred);
+  block_sum_n<2 * NB>(sq, wred);
 #pragma unroll
   for (int n = 0; n < NB; ++n) {
-    mean[n] *= 1.f / EE;
-    q[n] = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) q[n] += on ? (v[n][i] - mean[n]) * (v[n][i] - mean[n]) : 0.f;
-  }
-  block_sum_n<NB>(q, wred);
-#pragma unroll
-  for (int n = 0; n < NB; ++n) {
-    const float rs = rsqrtf(q[n] * (1.f / EE) + a.eps);
+    const float mean = sq[n] * (1.f / EE);
+    const float rs = rsqrtf(fmaxf(sq[NB + n] * (1.f / EE) - mean * mean, 0.f) + a.eps);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-      x[n][0][i] = on ? bf2f(f2bf((v[n][i] - mean[n]) * rs * bf2f(gg[i]) + bf2f(bb[i]))) : 0.f;
+      x[n][0][i] = on ? bf2f(f2bf((v[n][i] - mean) * rs * bf2f(gg[i]) + bf2f(bb[i]))) : 0.f;
   }
 }
 
@@ -554,7 +551,7 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
   __shared__ __attribute__((aligned(1024))) char wl[C::WLB];
   __shared__ __attribute__((aligned(16))) bf16_t xs[C::MM ? NB * (8192 / NB + 8) : 8];  // gemv_mfma staging
   __shared__ float red[4 * NB * 32];
-  __shared__ float wred[4 * NB > 8 ? 4 * NB : 8];
+  __shared__ float wred[8 * NB];
   __shared__ float sc[256];
   __shared__ float pv[4][D];
 
@@ -662,6 +659,17 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
         q[i] = ldf(qn_b + h * D + sub * 8 + i);
         kn[i] = ldf(kvn_b + kh * D + sub * 8 + i);
       }
+      // the cached K and V rows of this thread's first two key slots do not depend on q or the
+      // new k: requested before either is used (one round trip for short splits)
+      u16x8 kraw[2], vraw[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int j = j0 + kslot + RIF * u;
+        if (kslot + RIF * u < n && j != pos) {
+          kraw[u] = *reinterpret_cast<const u16x8*>(Ly.kc + kvbase + (long)j * D + sub * 8);
+          vraw[u] = *reinterpret_cast<const u16x8*>(Ly.vc + kvbase + (long)j * D + sub * 8);
+        }
+      }
       if (C::ROT) {
         rotate(q);
         rotate(kn);
@@ -696,14 +704,21 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
           for (int i = 0; i < 8; ++i) r[i] = bf2f(u[i]);
         }
       };
-      // the K and V rows of this thread's first two key slots are requested together (one round
-      // trip instead of two for short splits; the rest stream in the loops)
       float kp[2][8], vp[2][8];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
+        const int j = j0 + kslot + RIF * u;
         if (kslot + RIF * u < n) {
-          row(Ly.kc, 0, j0 + kslot + RIF * u, kp[u]);
-          row(Ly.vc, 1, j0 + kslot + RIF * u, vp[u]);
+          if (j == pos) {
+            row(Ly.kc, 0, j, kp[u]);
+            row(Ly.vc, 1, j, vp[u]);
+          } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              kp[u][i] = bf2f(kraw[u][i]);
+              vp[u][i] = bf2f(vraw[u][i]);
+            }
+          }
         }
       }
       auto score = [&](int i, const float* k) {

@@ -370,8 +370,9 @@ __device__ __forceinline__ void prefetch_p(const bf16_t* src, int from, int to, 
 // no read is predicated. Operands are read SB k-steps at a time, the next batch's reads issued
 // before this batch's MFMAs (one wave per SIMD: nothing else hides the LDS latency). The partial
 // sums (4 waves × HS k-sets) meet in `red`. No per-column butterfly and no bf16 → f32 converts:
-// NB rows cost the same MFMAs as one.
-template <int NPW, int K, int NB, int RS, class Mid, class End>
+// NB rows cost the same MFMAs as one. W8: int8 weight rows (8 B per lane and k-step), widened to
+// bf16 in registers right before their MFMA (exact), scaled per column by the caller.
+template <int NPW, int K, int NB, int RS, bool W8 = false, class Mid, class End>
 __device__ __forceinline__ void gemv_mfma(const char* ws, const float (&x)[NB][(K + 2047) / 2048][8], float* red,
                                           bf16_t* xs, int tid, Mid mid, End end, float (&r)[NB]) {
   constexpr int KPM = 8192 / NB;
@@ -389,6 +390,19 @@ __device__ __forceinline__ void gemv_mfma(const char* ws, const float (&x)[NB][(
   constexpr int NBT = SPW / SB;
   static_assert(NPW <= 32 && K % 1024 == 0 && NB <= 4 && NB * HS <= 16 && K % KP == 0 && SPW % SB == 0,
                 "gemv_mfma shape");
+  constexpr int WB = W8 ? 1 : 2;
+  typedef typename std::conditional<W8, uint2, u16x8>::type BRaw;
+  auto widen = [](const BRaw& w) -> u16x8 {
+    if constexpr (W8) {
+      u16x8 o;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        o[i] = (unsigned short)(__float_as_uint((float)(int)(signed char)(((i < 4 ? w.x : w.y) >> (8 * (i & 3))) & 0xFF)) >> 16);
+      return o;
+    } else {
+      return w;
+    }
+  };
   const int lane = tid & 63, wv = tid >> 6, lr = lane & 15, g = lane >> 4;
   // per-lane operand bases (every k-step is then a constant offset)
   const int arow = lr < NB * HS ? lr : NB * HS - 1;
@@ -398,7 +412,7 @@ __device__ __forceinline__ void gemv_mfma(const char* ws, const float (&x)[NB][(
   for (int t = 0; t < NCT; ++t) {
     const int c = NPW >= 16 ? (t * 16 + lr < NPW ? t * 16 + lr : NPW - 1) : lr % NPW;
     const int h = NPW >= 16 ? 0 : lr / NPW;
-    bp[t] = ws + (long)c * RS + (wv * (KP / 4) + h * DK + g * 8) * 2;
+    bp[t] = ws + (long)c * RS + (wv * (KP / 4) + h * DK + g * 8) * WB;
   }
   f32x4 acc[NCT];
 #pragma unroll
@@ -420,27 +434,29 @@ __device__ __forceinline__ void gemv_mfma(const char* ws, const float (&x)[NB][(
       }
     }
     __syncthreads();
-    auto load = [&](int bt, u16x8 (&av)[SB], u16x8 (&bw)[SB][NCT]) {
+    auto load = [&](int bt, u16x8 (&av)[SB], BRaw (&bw)[SB][NCT]) {
 #pragma unroll
       for (int u = 0; u < SB; ++u) {
         const int st = bt * SB + u;
         av[u] = *reinterpret_cast<const u16x8*>(ap + st * 32);
 #pragma unroll
-        for (int t = 0; t < NCT; ++t) bw[u][t] = *reinterpret_cast<const u16x8*>(bp[t] + (q * KP + st * 32) * 2);
+        for (int t = 0; t < NCT; ++t) bw[u][t] = *reinterpret_cast<const BRaw*>(bp[t] + (q * KP + st * 32) * WB);
       }
     };
-    u16x8 a0[SB], b0[SB][NCT];
+    u16x8 a0[SB];
+    BRaw b0[SB][NCT];
     load(0, a0, b0);
 #pragma unroll
     for (int bt = 0; bt < NBT; ++bt) {
-      u16x8 a1[SB], b1[SB][NCT];
+      u16x8 a1[SB];
+      BRaw b1[SB][NCT];
       if (bt + 1 < NBT) load(bt + 1, a1, b1);
 #pragma unroll
       for (int u = 0; u < SB; ++u)
 #pragma unroll
         for (int t = 0; t < NCT; ++t)
           acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a0[u]),
-                                                           __builtin_bit_cast(bf16x8, b0[u][t]), acc[t], 0, 0, 0);
+                                                           __builtin_bit_cast(bf16x8, widen(b0[u][t])), acc[t], 0, 0, 0);
       if (bt + 1 < NBT) {
 #pragma unroll
         for (int u = 0; u < SB; ++u) {
@@ -483,13 +499,12 @@ __device__ __forceinline__ void gemv_mfma(const char* ws, const float (&x)[NB][(
 // and the new k. Every projection splits its output columns evenly over the 256 workgroups and
 // each workgroup's weight slice must fit the 128 KiB LDS image.
 // NB: batch rows per step (each GEMV phase applies its LDS slice to all NB rows; attention runs
-// one workgroup per (row, head, split)). MM: the GEMV phases run on MFMA (gemv_mfma; bf16 only,
-// the default), else on the VALU (gemv_lds; int8 weight-only).
-template <int E_, int D_, int HQ_, int HK_, int F_, int ROT_, int W8_ = 0, int NB_ = 1, int MM_ = (W8_ == 0)>
+// one workgroup per (row, head, split)). MM: the GEMV phases run on MFMA (gemv_mfma, the default;
+// int8 weights widened in registers), else on the VALU (gemv_lds; A/B variants).
+template <int E_, int D_, int HQ_, int HK_, int F_, int ROT_, int W8_ = 0, int NB_ = 1, int MM_ = 1>
 struct MegaCfg {
   static constexpr int E = E_, D = D_, HQ = HQ_, HK = HK_, F = F_, ROT = ROT_, W8 = W8_, NB = NB_, MM = MM_;
   static_assert(NB == 1 || NB == 2 || NB == 4, "rows per step");
-  static_assert(!(MM && W8), "MFMA GEMV phases take bf16 weights");
   static constexpr int WB = W8 ? 1 : 2;  // bytes per weight
   static constexpr int NQKV = (HQ + 2 * HK) * D;
   static constexpr int NPQ = NQKV / NWG, NPO = E / NWG, NP1 = F / NWG, NP2 = E / NWG;
@@ -527,7 +542,7 @@ template <class C, int NPW, int K, int RS, class Mid, class End>
 __device__ __forceinline__ void gemv_phase(const char* ws, const float (&x)[C::NB][(K + 2047) / 2048][8],
                                            float* red, bf16_t* xs, int tid, Mid mid, End end, float (&r)[C::NB]) {
   if constexpr (C::MM)
-    gemv_mfma<NPW, K, C::NB, RS>(ws, x, red, xs, tid, mid, end, r);
+    gemv_mfma<NPW, K, C::NB, RS, C::W8 != 0>(ws, x, red, xs, tid, mid, end, r);
   else
     gemv_lds<NPW, K, C::W8 != 0, C::NB, RS>(ws, x, red, tid, mid, end, r);
 }
@@ -1505,8 +1520,8 @@ static int coop_ok(const void* fn, int threads) {
   return r;
 }
 
-// The instantiated model shapes (E, D, Hq, Hk, F) × rotary off / on; bf16 weights run the GEMV
-// phases on MFMA (MegaCfg MM default), int8 weight-only on the VALU.
+// The instantiated model shapes (E, D, Hq, Hk, F) × rotary off / on; the GEMV phases run on MFMA
+// (MegaCfg MM default) for bf16 and int8 weight-only.
 typedef MegaCfg<2048, 128, 16, 16, 8192, 0> CfgGpt13;    // GPT-3 1.3B
 typedef MegaCfg<2048, 128, 16, 16, 8192, 1> CfgGpt13R;
 typedef MegaCfg<2048, 128, 16, 4, 8192, 0> CfgGqa4;      // 1.3B width, 4 KV heads (GQA 4:1)
@@ -1515,6 +1530,7 @@ typedef MegaCfg<1024, 64, 16, 16, 4096, 0> CfgGpt350;    // GPT-3 350M
 typedef MegaCfg<1024, 64, 16, 16, 4096, 1> CfgGpt350R;
 typedef MegaCfg<2048, 128, 16, 16, 8192, 0, 1> CfgGpt13W8;  // int8 weight-only
 typedef MegaCfg<2048, 128, 16, 4, 8192, 1, 1> CfgGqa4RW8;
+typedef MegaCfg<2048, 128, 16, 16, 8192, 0, 1, 1, 0> CfgGpt13W8V;  // int8 on the VALU (A/B)
 typedef MegaCfg<2048, 128, 16, 16, 8192, 0, 0, 1, 0> CfgGpt13V;  // 1.3B on the VALU (A/B)
 // batched steps (2 / 4 rows: small serving batches, beams)
 typedef MegaCfg<2048, 128, 16, 16, 8192, 0, 0, 2> CfgGpt13B2;
@@ -1537,7 +1553,7 @@ static const void* mega_fn(int E_, int D_, int hq, int hk, int F_, int rot, int 
       (rot != 0) == C::ROT && (w8 != 0) == C::W8 && nb == C::NB && (mm < 0 || (mm != 0) == C::MM)) \
     return (const void*)decode_mega_kernel<C>;
   MEGA_CFG(CfgGpt13) MEGA_CFG(CfgGpt13R) MEGA_CFG(CfgGqa4) MEGA_CFG(CfgGqa4R)
-  MEGA_CFG(CfgGpt350) MEGA_CFG(CfgGpt350R) MEGA_CFG(CfgGpt13W8) MEGA_CFG(CfgGqa4RW8) MEGA_CFG(CfgGpt13V)
+  MEGA_CFG(CfgGpt350) MEGA_CFG(CfgGpt350R) MEGA_CFG(CfgGpt13W8) MEGA_CFG(CfgGqa4RW8) MEGA_CFG(CfgGpt13V) MEGA_CFG(CfgGpt13W8V)
   MEGA_CFG(CfgGpt13B2) MEGA_CFG(CfgGpt13B4) MEGA_CFG(CfgGpt13RB2) MEGA_CFG(CfgGpt13RB4)
   MEGA_CFG(CfgGqa4B2) MEGA_CFG(CfgGqa4B4) MEGA_CFG(CfgGqa4RB2) MEGA_CFG(CfgGqa4RB4)
   MEGA_CFG(CfgGpt350B2) MEGA_CFG(CfgGpt350B4) MEGA_CFG(CfgGpt350RB2) MEGA_CFG(CfgGpt350RB4)

@@ -170,14 +170,14 @@ class MegaDecoder:
         self.loader = int(os.environ.get("PIAMD_MEGA_LOADER", "0"))
         # GEMV phases on MFMA (1, default for bf16: 16 weight columns × 32 k per instruction, no
         # per-column butterfly; kernel 869 vs 976 µs on the VALU, profiles/decode_mega_r5.txt)
-        # or the VALU (0; int8 weight-only, the loader-wave variant)
-        self.mm = 0 if (self.w8 or self.loader) else int(os.environ.get("PIAMD_MEGA_MFMA", "1"))
+        # or the VALU (0; the loader-wave variant; A/B variants for GPT-1.3B bf16 and int8)
+        self.mm = 0 if self.loader else int(os.environ.get("PIAMD_MEGA_MFMA", "1"))
         if not self._variant_ok(self.mm):
             self.mm = 1 - self.mm
         if self.loader and ((E_, D_, HQ_, HK_, F_, self.rot, self.w8, nb) != (E, D, HQ, HK, F, 0, 0, 1)
                             or not self._lw_ok()):
             self.loader = 0
-            self.mm = 0 if self.w8 else 1
+            self.mm = 1
         # greedy tail (decode_head_kernel): LM head + argmax + bookkeeping + next embedding
         self.head_ok = nb == 1 and _lib.has("piamd_decode_head_greedy") and self._head_tables(gen)
         self.best = torch.zeros(8 * 32, dtype=torch.int64, device=dev)

@@ -161,18 +161,20 @@ def test_mega_decode_shape_gate():
     assert fb(2048, 128, 16, 16, 8192, 0, 0, 3) == 0 and fb(2048, 128, 16, 16, 8192, 0, 1, 2) == 0
     fv = _lib.lib().piamd_decode_mega_variant_supported  # GEMV kind: 1 MFMA, 0 VALU
     assert fv(2048, 128, 16, 16, 8192, 0, 0, 1, 1) == 1 and fv(2048, 128, 16, 16, 8192, 0, 0, 1, 0) == 1
-    assert fv(1024, 64, 16, 16, 4096, 0, 0, 1, 0) == 0 and fv(2048, 128, 16, 16, 8192, 0, 1, 1, 1) == 0
+    assert fv(1024, 64, 16, 16, 4096, 0, 0, 1, 0) == 0 and fv(2048, 128, 16, 16, 8192, 0, 1, 1, 1) == 1
+    assert fv(2048, 128, 16, 16, 8192, 0, 1, 1, 0) == 1 and fv(2048, 128, 16, 4, 8192, 128, 1, 1, 0) == 0
     assert fv(2048, 128, 16, 16, 8192, 0, 0, 4, 0) == 0 and fv(1024, 64, 16, 16, 4096, 64, 0, 4, 1) == 1
 
 
-@pytest.mark.parametrize("shape", ["gpt13_int8", "gqa4_rope_int8"])
-def test_mega_decode_int8_weight_only_matches_per_op_path(shape):
+@pytest.mark.parametrize("shape", ["gpt13_int8", "gqa4_rope_int8", "gpt13_int8_valu"])
+def test_mega_decode_int8_weight_only_matches_per_op_path(shape, monkeypatch):
     """int8 weight-only projections (FusedMultiTransformerWeightOnly decode): the kernel streams
     the int8 codes (half the bytes) and applies the per-output-channel scales after each column
     sum; against the per-op weight-only GEMV path of the same generator settings."""
     from paddle_infer_amd.inference import mega_decode
     from paddle_infer_amd.inference.generation import GPTGenerator
-    over, kw = ({}, {}) if shape == "gpt13_int8" else \
+    monkeypatch.setenv("PIAMD_MEGA_MFMA", "0" if shape.endswith("valu") else "1")
+    over, kw = ({}, {}) if shape.startswith("gpt13") else \
         ({"num_kv_heads": 4}, dict(rotary_dim=128, neox_rotary=True))
     m = _gpt13b_width(2, 512, "gpt3-1.3b", **over)
     g_mega = GPTGenerator(m, max_batch=1, max_seq_len=512, use_hip_graph=False, weight_only="int8", **kw)
@@ -188,6 +190,7 @@ def test_mega_decode_int8_weight_only_matches_per_op_path(shape):
         tok = lb.argmax(-1)
         la, lb = g_mega.decode(tok, pos), g_ref.decode(tok, pos)
         assert g_mega._mega[1].w8 == 1 and g_mega._mega[1].loader == 0
+        assert g_mega._mega[1].mm == (0 if shape.endswith("valu") else 1)
         assert _rel(la, lb) < 2e-2, (step, _rel(la, lb))
         pos += 1
     g_mega._mega[1].check()

@@ -1545,6 +1545,10 @@ typedef MegaCfg<1024, 64, 16, 16, 4096, 0, 0, 2> CfgGpt350B2;
 typedef MegaCfg<1024, 64, 16, 16, 4096, 0, 0, 4> CfgGpt350B4;
 typedef MegaCfg<1024, 64, 16, 16, 4096, 1, 0, 2> CfgGpt350RB2;
 typedef MegaCfg<1024, 64, 16, 16, 4096, 1, 0, 4> CfgGpt350RB4;
+typedef MegaCfg<2048, 128, 16, 16, 8192, 0, 1, 2> CfgGpt13W8B2;  // int8 weight-only, batched
+typedef MegaCfg<2048, 128, 16, 16, 8192, 0, 1, 4> CfgGpt13W8B4;
+typedef MegaCfg<2048, 128, 16, 4, 8192, 1, 1, 2> CfgGqa4RW8B2;
+typedef MegaCfg<2048, 128, 16, 4, 8192, 1, 1, 4> CfgGqa4RW8B4;
 
 // mm: 1 = MFMA GEMV phases, 0 = VALU, -1 = whichever is instantiated (MFMA first)
 static const void* mega_fn(int E_, int D_, int hq, int hk, int F_, int rot, int w8, int nb, int mm = -1) {
@@ -1557,6 +1561,7 @@ static const void* mega_fn(int E_, int D_, int hq, int hk, int F_, int rot, int 
   MEGA_CFG(CfgGpt13B2) MEGA_CFG(CfgGpt13B4) MEGA_CFG(CfgGpt13RB2) MEGA_CFG(CfgGpt13RB4)
   MEGA_CFG(CfgGqa4B2) MEGA_CFG(CfgGqa4B4) MEGA_CFG(CfgGqa4RB2) MEGA_CFG(CfgGqa4RB4)
   MEGA_CFG(CfgGpt350B2) MEGA_CFG(CfgGpt350B4) MEGA_CFG(CfgGpt350RB2) MEGA_CFG(CfgGpt350RB4)
+  MEGA_CFG(CfgGpt13W8B2) MEGA_CFG(CfgGpt13W8B4) MEGA_CFG(CfgGqa4RW8B2) MEGA_CFG(CfgGqa4RW8B4)
 #undef MEGA_CFG
   return nullptr;
 }

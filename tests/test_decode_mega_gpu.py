@@ -158,7 +158,8 @@ def test_mega_decode_shape_gate():
     assert f(1024, 64, 16, 16, 4096, 0, 1) == 0
     fb = _lib.lib().piamd_decode_mega_batch_supported
     assert fb(2048, 128, 16, 16, 8192, 0, 0, 2) == 1 and fb(2048, 128, 16, 4, 8192, 128, 0, 4) == 1
-    assert fb(2048, 128, 16, 16, 8192, 0, 0, 3) == 0 and fb(2048, 128, 16, 16, 8192, 0, 1, 2) == 0
+    assert fb(2048, 128, 16, 16, 8192, 0, 0, 3) == 0 and fb(2048, 128, 16, 16, 8192, 0, 1, 2) == 1
+    assert fb(1024, 64, 16, 16, 4096, 0, 1, 2) == 0
     fv = _lib.lib().piamd_decode_mega_variant_supported  # GEMV kind: 1 MFMA, 0 VALU
     assert fv(2048, 128, 16, 16, 8192, 0, 0, 1, 1) == 1 and fv(2048, 128, 16, 16, 8192, 0, 0, 1, 0) == 1
     assert fv(1024, 64, 16, 16, 4096, 0, 0, 1, 0) == 0 and fv(2048, 128, 16, 16, 8192, 0, 1, 1, 1) == 1
@@ -197,18 +198,20 @@ def test_mega_decode_int8_weight_only_matches_per_op_path(shape, monkeypatch):
 
 
 @pytest.mark.parametrize("B", [2, 4])
-@pytest.mark.parametrize("shape", ["gpt13", "gpt3-350m", "gqa4_rope_neox"])
+@pytest.mark.parametrize("shape", ["gpt13", "gpt3-350m", "gqa4_rope_neox", "gpt13_int8"])
 def test_mega_decode_batched_rows_match_per_op_path(shape, B):
     """Batched single-launch steps (MegaCfg NB = 2 / 4: one LDS weight slice applied to every row,
     one attention workgroup per (row, head, split)) with a different prompt length per row — each
     row attends over its own cache length and writes its own slot — against the per-op path."""
     from paddle_infer_amd.inference import mega_decode
     from paddle_infer_amd.inference.generation import GPTGenerator
-    preset, over, rope = {"gpt13": ("gpt3-1.3b", {}, None),
+    preset, over, rope = {"gpt13": ("gpt3-1.3b", {}, None), "gpt13_int8": ("gpt3-1.3b", {}, None),
                           "gpt3-350m": ("gpt3-350m", {}, None),
                           "gqa4_rope_neox": ("gpt3-1.3b", {"num_kv_heads": 4}, True)}[shape]
     m = _gpt13b_width(2, 512, preset, **over)
     kw = dict(rotary_dim=m.cfg.head_dim, neox_rotary=rope) if rope is not None else {}
+    if shape.endswith("int8"):
+        kw["weight_only"] = "int8"
     g_mega = GPTGenerator(m, max_batch=B, max_seq_len=512, use_hip_graph=False, **kw)
     g_ref = GPTGenerator(m, max_batch=B, max_seq_len=512, use_hip_graph=False, **kw)
     g_ref.use_mega = False

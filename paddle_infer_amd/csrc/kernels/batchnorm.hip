@@ -146,6 +146,48 @@ __global__ __launch_bounds__(256) void bn_finalize(const float* __restrict__ par
   shift[c] = bt - m * g * rstd;
 }
 
+// bn_finalize over channel-major partials part[(k·C + c)·P + b] (the conv forward's per-tile
+// statistics, piamd_conv2d_fwd2): each channel's P partials are contiguous.
+__global__ __launch_bounds__(256) void bn_finalize_t(const float* __restrict__ part, int P, int C,
+                                                     float eps, float momentum,
+                                                     const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta,
+                                                     float* __restrict__ run_mean,
+                                                     float* __restrict__ run_var,
+                                                     float* __restrict__ mean_out,
+                                                     float* __restrict__ rstd_out,
+                                                     float* __restrict__ scale,
+                                                     float* __restrict__ shift) {
+  const int c = blockIdx.x, t = threadIdx.x;
+  const float* pn = part + (long long)c * P;
+  const float* pm = part + ((long long)C + c) * P;
+  const float* pq = part + ((long long)2 * C + c) * P;
+  float n = 0.f, m = 0.f, m2 = 0.f;
+  for (int b = t; b < P; b += 256) welford_merge(n, m, m2, pn[b], pm[b], pq[b]);
+  __shared__ float sn[256], sm[256], sm2[256];
+  sn[t] = n; sm[t] = m; sm2[t] = m2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) {
+      welford_merge(n, m, m2, sn[t + o], sm[t + o], sm2[t + o]);
+      sn[t] = n; sm[t] = m; sm2[t] = m2;
+    }
+    __syncthreads();
+  }
+  if (t) return;
+  const float var = n > 0.f ? m2 / n : 0.f;
+  const float rstd = rsqrtf(var + eps);
+  mean_out[c] = m;
+  rstd_out[c] = rstd;
+  if (run_mean) {
+    run_mean[c] = momentum * run_mean[c] + (1.f - momentum) * m;
+    run_var[c] = momentum * run_var[c] + (1.f - momentum) * (n > 1.f ? m2 / (n - 1.f) : var);
+  }
+  const float g = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  scale[c] = g * rstd;
+  shift[c] = bt - m * g * rstd;
+}
+
 // inference fold from the running statistics (rstd_out for the backward)
 __global__ void bn_fold(int C, float eps, const float* __restrict__ gamma,
                         const float* __restrict__ beta, const float* __restrict__ run_mean,
@@ -655,18 +697,23 @@ PIAMD_EXPORT int piamd_bn_set_parts(long long elems_per_block, int max_parts) {
 // nhwc requires C % 8 == 0 (vectorised path), C ≥ 256 or C | 256.
 // ss (nullable): f32 [2][C] receives the affine fold (scale, shift) for piamd_bn_bwd2's x-derived
 // ReLU mask; otherwise the fold lives in ws.
-PIAMD_EXPORT int piamd_bn_fwd2(int dtype, int nhwc, const void* x, const void* res, void* y, int N,
+// part_t (nullable, training only): precomputed channel-major statistics partials of x
+// ([3][C][P_t] count / mean / M2, piamd_conv2d_fwd2) — the statistics pass over x is skipped.
+PIAMD_EXPORT int piamd_bn_fwd3(int dtype, int nhwc, const void* x, const void* res, void* y, int N,
                                int C, int S, const float* gamma, const float* beta,
                                float* run_mean, float* run_var, float* mean, float* rstd,
                                float momentum, float eps, int training, int act, float* ws, float* ss,
-                               hipStream_t st) {
-  if (C < 1 || N < 1 || S < 1 || (nhwc && C % 8 && C < 256 && 256 % C))
+                               const float* part_t, int P_t, hipStream_t st) {
+  if (C < 1 || N < 1 || S < 1 || (nhwc && C % 8 && C < 256 && 256 % C) || (part_t && (!training || P_t < 1)))
     return (int)hipErrorInvalidValue;
   const long long M = (long long)N * S, total = M * C;
   const bool v8 = nhwc ? C % 8 == 0 : S % 8 == 0;
   float* scale = ss ? ss : ws;
   float* shift = scale + C;
-  if (training) {
+  if (part_t) {
+    hipLaunchKernelGGL(bn_finalize_t, dim3(C), dim3(256), 0, st, part_t, P_t, C, eps, momentum, gamma,
+                       beta, run_mean, run_var, mean, rstd, scale, shift);
+  } else if (training) {
     const int P = nhwc && C % 8 == 0 ? parts_for8(M, C) : parts_for(M);
     const long long chunk = (M + P - 1) / P;
     float* part = ws + 2 * C;
@@ -704,6 +751,15 @@ PIAMD_EXPORT int piamd_bn_fwd2(int dtype, int nhwc, const void* x, const void* r
     hipLaunchKernelGGL(bn_apply<float>, g, dim3(256), 0, st, (const float*)x, (const float*)res,
                        scale, shift, (float*)y, total, C, S, nhwc, act);
   return (int)hipGetLastError();
+}
+
+PIAMD_EXPORT int piamd_bn_fwd2(int dtype, int nhwc, const void* x, const void* res, void* y, int N,
+                               int C, int S, const float* gamma, const float* beta,
+                               float* run_mean, float* run_var, float* mean, float* rstd,
+                               float momentum, float eps, int training, int act, float* ws, float* ss,
+                               hipStream_t st) {
+  return piamd_bn_fwd3(dtype, nhwc, x, res, y, N, C, S, gamma, beta, run_mean, run_var, mean, rstd,
+                       momentum, eps, training, act, ws, ss, nullptr, 0, st);
 }
 
 PIAMD_EXPORT int piamd_bn_fwd(int dtype, int nhwc, const void* x, const void* res, void* y, int N,

@@ -316,6 +316,94 @@ __global__ __launch_bounds__(NTHR, 1) void moe_wgrad_kernel(
 // image taps read a zero row), W in OHWI = [K_out][R·S·C] (K-contiguous B operand). Same 256² tile,
 // XOR-swizzled LDS images and MFMA loop as gemm_kernel; bias + activation fused in the epilogue.
 // Requires C % 64 == 0 (a 64-channel k-step never straddles two taps) and K_out % 4 == 0.
+// Per-tile BatchNorm statistics of the stored (16-bit-rounded) conv outputs, for the BN that
+// follows (it then skips its own statistics pass over the output): (count, mean, M2) of every
+// column over the tile's valid rows → stats[(k·Kout + n)·P + tile_m] (k = 0 count, 1 mean, 2 M2;
+// channel-major, so the finalize reads each channel's P partials contiguously).
+// Each wave transposes its outputs through a private LDS image (rows of 64 columns, 136-B
+// stride: the 8-B row writes of a lane column are conflict-free), ≤ 64 rows at a time, and lane c
+// then sums column c down the rows, shifted by the column's first value (no cancellation against
+// a large mean). The WM waves of a column merge in LDS (Chan's formula).
+template <int WM, int MB, int NB, bool F16>
+__device__ __forceinline__ void conv_tile_stats(const f32x16 (&acc)[MB][NB], char* smem, float* __restrict__ stats,
+                                                int m0, int M, int n0, int Kout, int tile_m, int P) {
+  constexpr int WC = NWAVE / WM, TN = WC * NB * 32;
+  constexpr int COLS = NB * 32;            // a wave's columns (one per lane)
+  constexpr int RSB = COLS * 2 + 8;        // image row stride (bytes)
+  constexpr int MBP = MB < 2 ? MB : 2;     // 32-row blocks per transposition pass
+  constexpr int WIMG = 32 * MBP * RSB;     // a wave's image
+  static_assert(COLS == 64, "one column per lane");
+  static_assert(NWAVE * WIMG <= 2 * (256 * 64 * 2 + 64 * 64 * 2), "images fit the smallest tile's LDS");
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wr = w / WC, wc = w % WC;
+  const int hi = lane >> 5, l31 = lane & 31;
+  const int rbase = m0 + wr * 32 * MB;
+  const int nw = max(0, min(32 * MB, M - rbase));  // valid rows of this wave
+  char* img = smem + w * WIMG;
+  __syncthreads();  // the main loop's LDS images are dead
+  float sh = 0.f, s = 0.f, q = 0.f;
+#pragma unroll
+  for (int p = 0; p < MB / MBP; ++p) {
+#pragma unroll
+    for (int i = 0; i < MBP; ++i) {
+      const int mb = p * MBP + i;
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          u16x4 o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = f2h<F16>(acc[mb][nb][4 * g + j]);
+          *reinterpret_cast<u16x4*>(img + (i * 32 + l31) * RSB + (nb * 32 + 8 * g + 4 * hi) * 2) = o;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int rows = min(32 * MBP, nw - p * 32 * MBP);  // valid rows of this pass
+    if (p == 0 && nw > 0) sh = h2f<F16>(*reinterpret_cast<const unsigned short*>(img + lane * 2));
+#pragma unroll 8
+    for (int r = 0; r < 32 * MBP; ++r) {
+      if (r < rows) {
+        const float d = h2f<F16>(*reinterpret_cast<const unsigned short*>(img + r * RSB + lane * 2)) - sh;
+        s += d;
+        q += d * d;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  __syncthreads();  // every image read; the merge table reuses the front of smem
+  float* red = reinterpret_cast<float*>(smem);  // [WM][TN][3]
+  {
+    const int cl = wc * COLS + lane;
+    const float n = (float)nw;
+    float* r = red + (wr * TN + cl) * 3;
+    r[0] = n;
+    r[1] = nw ? sh + s / n : 0.f;
+    r[2] = nw ? fmaxf(q - s * s / n, 0.f) : 0.f;
+  }
+  __syncthreads();
+  for (int cl = tid; cl < TN; cl += NTHR) {
+    const int n = n0 + cl;
+    if (n >= Kout) continue;
+    float cn = 0.f, cm = 0.f, cm2 = 0.f;
+#pragma unroll
+    for (int r = 0; r < WM; ++r) {
+      const float* e = red + (r * TN + cl) * 3;
+      const float nb = e[0];
+      if (nb == 0.f) continue;
+      const float nn = cn + nb, d = e[1] - cm;
+      cm += d * nb / nn;
+      cm2 += e[2] + d * d * cn * nb / nn;
+      cn = nn;
+    }
+    stats[((long long)0 * Kout + n) * P + tile_m] = cn;
+    stats[((long long)1 * Kout + n) * P + tile_m] = cm;
+    stats[((long long)2 * Kout + n) * P + tile_m] = cm2;
+  }
+}
+
 struct ConvGeom {
   int N, H, W, C, OH, OW, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w;
 };
@@ -332,7 +420,7 @@ template <int WM, int MB, int NB, bool SC = false, bool F16 = false>
 __global__ __launch_bounds__(NTHR, 1) void conv_fwd_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ wt, const bf16_t* __restrict__ zero,
     bf16_t* __restrict__ y, float* __restrict__ ws, int ksplit, ConvGeom g, int Kout, int act,
-    const bf16_t* __restrict__ bias, int yf32) {
+    const bf16_t* __restrict__ bias, int yf32, float* __restrict__ stats) {
   constexpr int WC = NWAVE / WM, TN = WC * NB * 32;
   constexpr int B_BYTES = TN * BK * 2, SBYTES = TILE_BYTES + B_BYTES;
   __shared__ __attribute__((aligned(1024))) char smem[2 * SBYTES];
@@ -442,6 +530,8 @@ __global__ __launch_bounds__(NTHR, 1) void conv_fwd_kernel(
   else
     gemm_epilogue<WM, MB, NB, F16>(acc, y, Kout, 0, 0, m0, M, n0, Kout,
                               (bias || act) ? EPI_BIAS_ACT : EPI_STORE, act, bias, nullptr, 0);
+  if (stats)  // (host: ksplit == 1, 16-bit output without bias / activation)
+    conv_tile_stats<WM, MB, NB, F16>(acc, smem, stats, m0, M, n0, Kout, tile / tn, tm);
 }
 
 // y[m][n] = act(Σ_p ws[p][m][n] + bias[n]) — 4 outputs per thread (K_out % 4 == 0).
@@ -807,9 +897,9 @@ __global__ __launch_bounds__(256) void conv_splitk_finish_f32(const float* __res
 template <bool F16>
 static void conv_fwd_launch(int tile_n, bool sc, unsigned grid, hipStream_t st, const bf16_t* xb,
                             const bf16_t* wb, const bf16_t* zb, bf16_t* y, float* wsf, int ksplit,
-                            const ConvGeom& g, int Kout, int act, const bf16_t* bb, int yf32) {
+                            const ConvGeom& g, int Kout, int act, const bf16_t* bb, int yf32, float* stats) {
 #define CONV_FWD(WM, MB, NB, SCV) \
-  hipLaunchKernelGGL((conv_fwd_kernel<WM, MB, NB, SCV, F16>), dim3(grid), dim3(NTHR), 0, st, xb, wb, zb, y, wsf, ksplit, g, Kout, act, bb, yf32)
+  hipLaunchKernelGGL((conv_fwd_kernel<WM, MB, NB, SCV, F16>), dim3(grid), dim3(NTHR), 0, st, xb, wb, zb, y, wsf, ksplit, g, Kout, act, bb, yf32, stats)
   if (tile_n == 64) {
     if (sc) CONV_FWD(8, 1, 2, true); else CONV_FWD(8, 1, 2, false);
   } else if (tile_n == 128) {
@@ -820,14 +910,17 @@ static void conv_fwd_launch(int tile_n, bool sc, unsigned grid, hipStream_t st, 
 #undef CONV_FWD
 }
 
-PIAMD_EXPORT int piamd_conv2d_fwd(const void* x, const void* wt, const void* zero, void* y, int N,
-                                  int H, int W, int C, int OH, int OW, int R, int S, int st_h,
-                                  int st_w, int pad_h, int pad_w, int dil_h, int dil_w, int Kout,
-                                  int act, const void* bias, int tile_n, int ksplit, void* ws,
-                                  int flags, hipStream_t st) {
+// stats (nullable): f32 [3][Kout][ceil(M / 256)] per-tile BatchNorm statistics of y
+// (conv_tile_stats) — ksplit == 1, 16-bit y, no bias / activation.
+PIAMD_EXPORT int piamd_conv2d_fwd2(const void* x, const void* wt, const void* zero, void* y, int N,
+                                   int H, int W, int C, int OH, int OW, int R, int S, int st_h,
+                                   int st_w, int pad_h, int pad_w, int dil_h, int dil_w, int Kout,
+                                   int act, const void* bias, int tile_n, int ksplit, void* ws,
+                                   int flags, float* stats, hipStream_t st) {
   const bool sc = C == 8;
   const int f16 = flags & 1, yf32 = (flags >> 1) & 1;
   if (yf32 && (bias || act)) return (int)hipErrorInvalidValue;
+  if (stats && (ksplit != 1 || yf32 || bias || act)) return (int)hipErrorInvalidValue;
   if ((C % BK && !sc) || Kout % 4 || N < 1 || OH < 1 || OW < 1 || R < 1 || S < 1 || !zero || ksplit < 1 ||
       (ksplit > 1 && !ws) || ksplit > (sc ? (R * S + 7) / 8 : R * S * (C / BK)) ||
       (tile_n != 64 && tile_n != 128 && tile_n != 256))
@@ -842,8 +935,8 @@ PIAMD_EXPORT int piamd_conv2d_fwd(const void* x, const void* wt, const void* zer
   const auto zb = (const bf16_t*)zero;
   const auto bb = (const bf16_t*)bias;
   float* wsf = (float*)ws;
-  if (f16) conv_fwd_launch<true>(tile_n, sc, grid, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb, yf32);
-  else conv_fwd_launch<false>(tile_n, sc, grid, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb, yf32);
+  if (f16) conv_fwd_launch<true>(tile_n, sc, grid, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb, yf32, stats);
+  else conv_fwd_launch<false>(tile_n, sc, grid, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb, yf32, stats);
   if (ksplit > 1) {
     const long long MN = M * Kout;
     const dim3 fg((unsigned)((MN / 4 + 255) / 256));
@@ -853,6 +946,15 @@ PIAMD_EXPORT int piamd_conv2d_fwd(const void* x, const void* wt, const void* zer
     else hipLaunchKernelGGL(conv_splitk_finish<false>, fg, dim3(256), 0, st, wsf, ksplit, MN, Kout, act, bb, (bf16_t*)y);
   }
   return (int)hipGetLastError();
+}
+
+PIAMD_EXPORT int piamd_conv2d_fwd(const void* x, const void* wt, const void* zero, void* y, int N,
+                                  int H, int W, int C, int OH, int OW, int R, int S, int st_h,
+                                  int st_w, int pad_h, int pad_w, int dil_h, int dil_w, int Kout,
+                                  int act, const void* bias, int tile_n, int ksplit, void* ws,
+                                  int flags, hipStream_t st) {
+  return piamd_conv2d_fwd2(x, wt, zero, y, N, H, W, C, OH, OW, R, S, st_h, st_w, pad_h, pad_w, dil_h,
+                           dil_w, Kout, act, bias, tile_n, ksplit, ws, flags, nullptr, st);
 }
 
 // NHWC implicit-GEMM convolution weight gradient: x [N][H][W][C], dy [N][OH][OW][Kout] 16-bit

@@ -267,6 +267,9 @@ _SIGS["piamd_quant_rows"] = [c_void_p, c_ll, c_void_p, c_ll, c_void_p, c_float, 
 # x, w_ohwi, zero, y, N, H, W, C, OH, OW, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w, Kout, act,
 # bias, tile_n, ksplit, ws, f16, stream
 _SIGS["piamd_conv2d_fwd"] = [c_void_p] * 4 + [c_int] * 16 + [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]
+# ... flags, stats (f32 [3][Kout][ceil(M/256)] per-tile BN statistics, nullable), stream
+_SIGS["piamd_conv2d_fwd2"] = ([c_void_p] * 4 + [c_int] * 16
+                              + [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p])
 # dtype, nhwc, x, res, y, N, C, S, gamma, beta, run_mean, run_var, mean, rstd, momentum, eps,
 # training, act, ws, stream
 _SIGS["piamd_bn_fwd"] = ([c_int, c_int] + [c_void_p] * 3 + [c_int] * 3 + [c_void_p] * 6
@@ -279,6 +282,9 @@ _SIGS["piamd_bn_bwd"] = ([c_int, c_int] + [c_void_p] * 5 + [c_int] * 3 + [c_void
                          + [c_int, c_int, c_void_p, c_void_p])
 _SIGS["piamd_bn_fwd2"] = ([c_int, c_int] + [c_void_p] * 3 + [c_int] * 3 + [c_void_p] * 6
                           + [c_float, c_float, c_int, c_int, c_void_p, c_void_p, c_void_p])
+# ... ws, ss, part_t (channel-major conv statistics partials, nullable), P_t, stream
+_SIGS["piamd_bn_fwd3"] = ([c_int, c_int] + [c_void_p] * 3 + [c_int] * 3 + [c_void_p] * 6
+                          + [c_float, c_float, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p])
 _SIGS["piamd_bn_bwd2"] = ([c_int, c_int] + [c_void_p] * 5 + [c_int] * 3 + [c_void_p] * 5
                           + [c_int, c_int, c_void_p, c_void_p, c_void_p])
 # in, w, bias, out, N, H, W, Cin, OH, OW, Cout, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w,

@@ -71,6 +71,17 @@ def _reference(x, running_mean, running_var, weight, bias, training, momentum, e
     return y
 
 
+def _conv_stats(x, training, nhwc, C):
+    """(partials [3, C, P], P) a conv forward attached to ``x`` (unmodified since), else (None, 0)."""
+    t = getattr(x, "_piamd_bn_part", None)
+    if t is None or not training or not nhwc:
+        return None, 0
+    part, P, ver = t
+    if ver != x._version or part.shape != (3, C, P) or part.device != x.device:
+        return None, 0
+    return part, P
+
+
 class _BNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, training, momentum,
@@ -101,10 +112,14 @@ class _BNAct(torch.autograd.Function):
         # (x·scale + shift > 0, the forward's own test) instead of reading y
         ss = (torch.empty(2 * C, device=dev, dtype=torch.float32)
               if act == 1 and res is None and nhwc and C % 8 == 0 else None)
-        _lib.call("piamd_bn_fwd2", int(x.dtype == torch.bfloat16), int(nhwc), xc.data_ptr(),
+        # statistics the conv forward left on its output (ops/conv.py BN_STATS): finalize those
+        # instead of a statistics pass over x
+        part, P = _conv_stats(x, training, nhwc, C)
+        _lib.call("piamd_bn_fwd3", int(x.dtype == torch.bfloat16), int(nhwc), xc.data_ptr(),
                   _lib.ptr(res), y.data_ptr(), N, C, S, _lib.ptr(g), _lib.ptr(b), _lib.ptr(rm),
                   _lib.ptr(rv), mean.data_ptr(), rstd.data_ptr(), float(momentum), float(eps),
-                  int(training), int(act), ws.data_ptr(), _lib.ptr(ss), _lib.stream())
+                  int(training), int(act), ws.data_ptr(), _lib.ptr(ss), _lib.ptr(part), P,
+                  _lib.stream())
         ctx.save_for_backward(xc, y, g, mean, rstd, ss)
         ctx.meta = (training, act, nhwc, dims, residual is not None, weight, bias,
                     x.dim() == 4 and nhwc and not x.is_contiguous())

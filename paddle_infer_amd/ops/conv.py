@@ -25,6 +25,7 @@ Routes (``conv2d_any``, called by ``nn.functional.conv2d`` for GPU tensors):
 from __future__ import annotations
 
 import os
+import threading
 
 import torch
 
@@ -99,10 +100,12 @@ def _plan(M, K, nk):
 PLAN_OVERRIDE = None  # (tile_n, ksplit) for tuning sweeps
 
 
-def _launch(x, w_ohwi, bias, st, pad, dil, act, rs=None, out_f32=False):
+def _launch(x, w_ohwi, bias, st, pad, dil, act, rs=None, out_f32=False, stats_out=None):
     """x [N,H,W,C] bf16 contiguous, w_ohwi [K,R,S,C] bf16 contiguous → y [N,OH,OW,K]. ``rs``:
     the true filter size in stem mode (C == 8, w_ohwi = [K][ceil(R·S/8)·64] packed taps).
-    ``out_f32``: y in f32 (no bias / activation)."""
+    ``out_f32``: y in f32 (no bias / activation). ``stats_out`` (a list): when the chosen plan
+    runs unsplit and y takes no bias / activation, the kernel also writes per-tile BatchNorm
+    statistics of y and ``(stats [3, K, P], P)`` is appended (see conv_tile_stats)."""
     N, H, W, C = x.shape
     K = w_ohwi.shape[0]
     R, S = rs if rs is not None else w_ohwi.shape[1:3]
@@ -116,16 +119,22 @@ def _launch(x, w_ohwi, bias, st, pad, dil, act, rs=None, out_f32=False):
     assert not (out_f32 and (b is not None or act))
     flags = _f16(x) | (2 if out_f32 else 0)
 
-    def run(plan):
+    def run(plan, stats=None):
         tn, ks = plan
         ws = torch.empty(ks * M * K, dtype=torch.float32, device=x.device) if ks > 1 else None
-        _lib.call("piamd_conv2d_fwd", x.data_ptr(), w_ohwi.data_ptr(), _zero(x.device).data_ptr(),
+        _lib.call("piamd_conv2d_fwd2", x.data_ptr(), w_ohwi.data_ptr(), _zero(x.device).data_ptr(),
                   y.data_ptr(), N, H, W, C, OH, OW, R, S, st[0], st[1], pad[0], pad[1], dil[0],
-                  dil[1], K, act, _lib.ptr(b), tn, ks, _lib.ptr(ws), flags, _lib.stream())
+                  dil[1], K, act, _lib.ptr(b), tn, ks, _lib.ptr(ws), flags, _lib.ptr(stats),
+                  _lib.stream())
     plan = PLAN_OVERRIDE or _autotuned("conv2d_fwd", (N, H, W, C, K, R, S, st, pad, dil, act)
                                        + (("f32",) if out_f32 else ()),
                                        _plan(M, K, nk), _fwd_candidates(M, K, nk), run)
-    run(plan)
+    stats = None
+    if stats_out is not None and plan[1] == 1 and b is None and not act and not out_f32:
+        P = -(-M // 256)
+        stats = torch.empty(3, K, P, dtype=torch.float32, device=x.device)
+        stats_out.append((stats, P))
+    run(plan, stats)
     return y
 
 
@@ -280,11 +289,25 @@ def _padc(t, n):
     return t if t.shape[-1] == n else torch.nn.functional.pad(t, (0, n - t.shape[-1]))
 
 
+# Per-tile BatchNorm statistics from the conv forward epilogue (PIAMD_CONV_BN_STATS=1: on): a
+# training conv without bias / activation attaches them to its output, and a BatchNorm applied
+# to that output finalizes them instead of reading the output once more (ops/batchnorm.py).
+BN_STATS = os.environ.get("PIAMD_CONV_BN_STATS", "0") == "1"
+_STATS = threading.local()
+
+
+def _take_stats():
+    v = getattr(_STATS, "v", None)
+    _STATS.v = None
+    return v
+
+
 class _Conv2dNHWC(torch.autograd.Function):
-    """Dense conv on the MFMA kernels: x [N,H,W,C0] bf16/fp16 (contiguous), weight [K0,C0,R,S]."""
+    """Dense conv on the MFMA kernels: x [N,H,W,C0] bf16/fp16 (contiguous), weight [K0,C0,R,S].
+    ``want_stats``: leave the output's per-tile BN statistics in the thread-local slot."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, st, pad, dil, act):
+    def forward(ctx, x, weight, bias, st, pad, dil, act, want_stats=False):
         dt = x.dtype
         K0, C0, R, S = weight.shape
         K = -(-K0 // 4) * 4  # the epilogue stores 4 output channels per lane
@@ -296,12 +319,14 @@ class _Conv2dNHWC(torch.autograd.Function):
         wq0 = weight if prep else weight.to(dt)  # the prep path casts inside its own kernel
         wq = wq0 if (K == K0 or prep) else torch.nn.functional.pad(wq0, (0, 0, 0, 0, 0, 0, 0, K - K0))
         b = None if bias is None else _padc(bias.to(dt), K)
+        so = [] if (want_stats and K == K0) else None
+        _STATS.v = None
         if C0 <= 8:  # stem mode: zero-pad the image channels to 8
             xc = _padc(x, 8).contiguous()
             nk = -(-(R * S) // 8)
             w8 = torch.zeros(K, nk * 64, dtype=dt, device=x.device)
             w8[:, :R * S * 8].view(K, R, S, 8)[..., :C0] = wq.permute(0, 2, 3, 1)
-            y = _launch(xc, w8.view(K, 1, nk * 8, 8), b, st, pad, dil, act, rs=(R, S))
+            y = _launch(xc, w8.view(K, 1, nk * 8, 8), b, st, pad, dil, act, rs=(R, S), stats_out=so)
         else:  # channels zero-padded to a multiple of 64 (one k-step never straddles two taps)
             C = _pad64(C0)
             xc = _padc(x, C).contiguous()
@@ -317,7 +342,9 @@ class _Conv2dNHWC(torch.autograd.Function):
                           _lib.ptr(w_t), K0, C0, R, S, K, C, Kp, _lib.stream())
             else:
                 w_ohwi = _padc(wq.permute(0, 2, 3, 1), C).contiguous()
-            y = _launch(xc, w_ohwi, b, st, pad, dil, act)
+            y = _launch(xc, w_ohwi, b, st, pad, dil, act, stats_out=so)
+            if so:
+                _STATS.v = so[0]
             if prep:
                 if K != K0:
                     y = y[..., :K0].contiguous()
@@ -327,6 +354,8 @@ class _Conv2dNHWC(torch.autograd.Function):
                 return y
         if K != K0:
             y = y[..., :K0].contiguous()
+        if so:
+            _STATS.v = so[0]
         # the half-precision weight is kept for the backward (no second cast of the master weight)
         ctx.save_for_backward(xc, wq0, y if act else None)
         ctx.cfg = (st, pad, dil, act, bias is not None, weight.dtype)
@@ -370,7 +399,7 @@ class _Conv2dNHWC(torch.autograd.Function):
             dw = dw.to(wdt)
         if has_bias and ctx.needs_input_grad[2]:
             db = dy.float().sum((0, 1, 2)).to(wdt)
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None, None
 
     @staticmethod
     def _backward_prepped(ctx, x, w_t, dy):
@@ -394,7 +423,7 @@ class _Conv2dNHWC(torch.autograd.Function):
             dw = dw.to(wdt)
         if has_bias and ctx.needs_input_grad[2]:
             db = dy.float().sum((0, 1, 2)).to(wdt)
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None, None
 
 
 _WSRC = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
@@ -694,7 +723,13 @@ def conv2d_any(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, 
         elif R == S == 1 and pad == (0, 0) and C % 64 and C > 8:
             y = _Conv1x1.apply(xh, weight, bias, st)
         else:
-            y = _Conv2dNHWC.apply(xh, weight, bias, st, pad, dil, 0)
+            want = BN_STATS and bias is None and torch.is_grad_enabled()
+            y = _Conv2dNHWC.apply(xh, weight, bias, st, pad, dil, 0, want)
+            part = _take_stats() if want else None
+            out = y if nhwc else y.permute(0, 3, 1, 2)
+            if part is not None:  # consumed by a BatchNorm of this very tensor (same version)
+                out._piamd_bn_part = (part[0], part[1], out._version)
+            return out
     return y if nhwc else y.permute(0, 3, 1, 2)
 
 

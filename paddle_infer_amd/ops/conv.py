@@ -289,10 +289,10 @@ def _padc(t, n):
     return t if t.shape[-1] == n else torch.nn.functional.pad(t, (0, n - t.shape[-1]))
 
 
-# Per-tile BatchNorm statistics from the conv forward epilogue (PIAMD_CONV_BN_STATS=1: on): a
+# Per-tile BatchNorm statistics from the conv forward epilogue (PIAMD_CONV_BN_STATS=0: off): a
 # training conv without bias / activation attaches them to its output, and a BatchNorm applied
 # to that output finalizes them instead of reading the output once more (ops/batchnorm.py).
-BN_STATS = os.environ.get("PIAMD_CONV_BN_STATS", "0") == "1"
+BN_STATS = os.environ.get("PIAMD_CONV_BN_STATS", "1") != "0"
 _STATS = threading.local()
 
 

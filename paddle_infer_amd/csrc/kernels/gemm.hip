@@ -321,9 +321,9 @@ __global__ __launch_bounds__(NTHR, 1) void moe_wgrad_kernel(
 // column over the tile's valid rows → stats[(k·Kout + n)·P + tile_m] (k = 0 count, 1 mean, 2 M2;
 // channel-major, so the finalize reads each channel's P partials contiguously).
 // Each wave transposes its outputs through a private LDS image (rows of 64 columns, 136-B
-// stride: the 8-B row writes of a lane column are conflict-free), ≤ 64 rows at a time, and lane c
-// then sums column c down the rows, shifted by the column's first value (no cancellation against
-// a large mean). The WM waves of a column merge in LDS (Chan's formula).
+// stride: the 8-B row writes of a lane column are conflict-free), ≤ 64 rows at a time; lane pair
+// (c2, c2 + 32) then sums columns 2·c2 and 2·c2 + 1 down alternate rows (4-B reads), shifted by
+// the columns' first values (no cancellation against a large mean). The WM waves of a column merge in LDS (Chan's formula).
 template <int WM, int MB, int NB, bool F16>
 __device__ __forceinline__ void conv_tile_stats(const f32x16 (&acc)[MB][NB], char* smem, float* __restrict__ stats,
                                                 int m0, int M, int n0, int Kout, int tile_m, int P) {
@@ -340,7 +340,8 @@ __device__ __forceinline__ void conv_tile_stats(const f32x16 (&acc)[MB][NB], cha
   const int nw = max(0, min(32 * MB, M - rbase));  // valid rows of this wave
   char* img = smem + w * WIMG;
   __syncthreads();  // the main loop's LDS images are dead
-  float sh = 0.f, s = 0.f, q = 0.f;
+  const int half = lane >> 5, c2 = lane & 31;
+  float sh0 = 0.f, sh1 = 0.f, s0 = 0.f, q0 = 0.f, s1 = 0.f, q1 = 0.f;
 #pragma unroll
   for (int p = 0; p < MB / MBP; ++p) {
 #pragma unroll
@@ -359,25 +360,41 @@ __device__ __forceinline__ void conv_tile_stats(const f32x16 (&acc)[MB][NB], cha
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // lane (half, c2): columns 2·c2, 2·c2 + 1 over the pass's rows half, half + 2, … (one 4-B read
+    // per row for two columns)
     const int rows = min(32 * MBP, nw - p * 32 * MBP);  // valid rows of this pass
-    if (p == 0 && nw > 0) sh = h2f<F16>(*reinterpret_cast<const unsigned short*>(img + lane * 2));
+    if (p == 0 && nw > 0) {
+      const unsigned u = *reinterpret_cast<const unsigned*>(img + c2 * 4);
+      sh0 = h2f<F16>((unsigned short)(u & 0xFFFF));
+      sh1 = h2f<F16>((unsigned short)(u >> 16));
+    }
 #pragma unroll 8
-    for (int r = 0; r < 32 * MBP; ++r) {
+    for (int r = half; r < 32 * MBP; r += 2) {
       if (r < rows) {
-        const float d = h2f<F16>(*reinterpret_cast<const unsigned short*>(img + r * RSB + lane * 2)) - sh;
-        s += d;
-        q += d * d;
+        const unsigned u = *reinterpret_cast<const unsigned*>(img + r * RSB + c2 * 4);
+        const float d0 = h2f<F16>((unsigned short)(u & 0xFFFF)) - sh0;
+        const float d1 = h2f<F16>((unsigned short)(u >> 16)) - sh1;
+        s0 += d0;
+        q0 += d0 * d0;
+        s1 += d1;
+        q1 += d1 * d1;
       }
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+  // the two row halves share the shift: their sums add
+  s0 += __shfl_xor(s0, 32, 64);
+  q0 += __shfl_xor(q0, 32, 64);
+  s1 += __shfl_xor(s1, 32, 64);
+  q1 += __shfl_xor(q1, 32, 64);
   __syncthreads();  // every image read; the merge table reuses the front of smem
   float* red = reinterpret_cast<float*>(smem);  // [WM][TN][3]
   {
-    const int cl = wc * COLS + lane;
-    const float n = (float)nw;
+    // lanes 0-31 hold column 2·c2, lanes 32-63 (same sums) store column 2·c2 + 1
+    const int cl = wc * COLS + 2 * c2 + half;
+    const float n = (float)nw, sh = half ? sh1 : sh0, s = half ? s1 : s0, q = half ? q1 : q0;
     float* r = red + (wr * TN + cl) * 3;
     r[0] = n;
     r[1] = nw ? sh + s / n : 0.f;

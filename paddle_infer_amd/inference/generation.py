@@ -303,10 +303,13 @@ class GPTGenerator:
                 g.replay()
         return out
 
-    def _reorder(self, src, B):
+    def _reorder(self, src, B, L=None):
+        """Caches of rows [0, B) gathered by source beam ``src``; only the first ``L`` positions
+        (the ones written so far) move."""
+        L = self.max_seq_len if L is None else min(int(L), self.max_seq_len)
         for k, v in self.caches:
-            k[:B].copy_(k[:B].index_select(0, src))
-            v[:B].copy_(v[:B].index_select(0, src))
+            k[:B, :, :L].copy_(k[:B, :, :L].index_select(0, src))
+            v[:B, :, :L].copy_(v[:B, :, :L].index_select(0, src))
 
     def _beam_search(self, input_ids, lengths, max_new_tokens, nb, eos, pad, length_penalty):
         """Beam search (reference `beam_search_softmax`): beams live as batch rows; each step the
@@ -336,7 +339,7 @@ class GPTGenerator:
             src = ar + parent.long()
             if eos is not None:
                 stop = stop | (tok == eos)
-            self._reorder(src, B)
+            self._reorder(src, B, S + t)  # positions [0, S + t) are written (prompt + t steps)
             if t + 1 < max_new_tokens:
                 logits = self.decode(tok.long(), pos)
                 pos = pos + 1

@@ -91,7 +91,7 @@ struct MegaArgs {
   int rot;              // rotary dims: 0 or D (whole head)
   int neox;             // 1: rotate-half (NeoX), 0: interleaved pairs (GPT-J)
   float log2_base;      // log2 of the rotary base
-  int w8;               // 1: int8 weight-only projections (MegaLayer scales)
+  int w8;               // weight format: 0 bf16, 1 int8, 2 int4 weight-only (MegaLayer scales)
   int nb;               // batch rows per step (1, 2 or 4): resid / rbuf / qn / kvn / part / h hold
                         // nb rows per slot, pos nb entries, the caches are [rows][HK][maxS][D]
   int mm;               // 1 = MFMA GEMV phases, 0 = VALU (MegaCfg MM; the instantiated variant)
@@ -370,9 +370,10 @@ __device__ __forceinline__ void prefetch_p(const bf16_t* src, int from, int to, 
 // no read is predicated. Operands are read SB k-steps at a time, the next batch's reads issued
 // before this batch's MFMAs (one wave per SIMD: nothing else hides the LDS latency). The partial
 // sums (4 waves × HS k-sets) meet in `red`. No per-column butterfly and no bf16 → f32 converts:
-// NB rows cost the same MFMAs as one. W8: int8 weight rows (8 B per lane and k-step), widened to
-// bf16 in registers right before their MFMA (exact), scaled per column by the caller.
-template <int NPW, int K, int NB, int RS, bool W8 = false, class Mid, class End>
+// NB rows cost the same MFMAs as one. WQ = 1 / 2: int8 / int4 weight rows (8 / 4 B per lane and
+// k-step), widened to bf16 in registers right before their MFMA (exact), scaled per column by
+// the caller.
+template <int NPW, int K, int NB, int RS, int WQ = 0, class Mid, class End>
 __device__ __forceinline__ void gemv_mfma(const char* ws, const float (&x)[NB][(K + 2047) / 2048][8], float* red,
                                           bf16_t* xs, int tid, Mid mid, End end, float (&r)[NB]) {
   constexpr int KPM = 8192 / NB;
@@ -390,14 +391,20 @@ __device__ __forceinline__ void gemv_mfma(const char* ws, const float (&x)[NB][(
   constexpr int NBT = SPW / SB;
   static_assert(NPW <= 32 && K % 1024 == 0 && NB <= 4 && NB * HS <= 16 && K % KP == 0 && SPW % SB == 0,
                 "gemv_mfma shape");
-  constexpr int WB = W8 ? 1 : 2;
-  typedef typename std::conditional<W8, uint2, u16x8>::type BRaw;
+  constexpr int WBITS = WQ == 0 ? 16 : WQ == 1 ? 8 : 4;
+  typedef typename std::conditional<WQ == 0, u16x8, typename std::conditional<WQ == 1, uint2, unsigned>::type>::type BRaw;
   auto widen = [](const BRaw& w) -> u16x8 {
-    if constexpr (W8) {
+    if constexpr (WQ == 1) {  // 8 int8 codes
       u16x8 o;
 #pragma unroll
       for (int i = 0; i < 8; ++i)
         o[i] = (unsigned short)(__float_as_uint((float)(int)(signed char)(((i < 4 ? w.x : w.y) >> (8 * (i & 3))) & 0xFF)) >> 16);
+      return o;
+    } else if constexpr (WQ == 2) {  // 8 int4 codes, k ascending from the low nibble
+      u16x8 o;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        o[i] = (unsigned short)(__float_as_uint((float)((int)(w << (28 - 4 * i)) >> 28)) >> 16);
       return o;
     } else {
       return w;
@@ -412,7 +419,7 @@ __device__ __forceinline__ void gemv_mfma(const char* ws, const float (&x)[NB][(
   for (int t = 0; t < NCT; ++t) {
     const int c = NPW >= 16 ? (t * 16 + lr < NPW ? t * 16 + lr : NPW - 1) : lr % NPW;
     const int h = NPW >= 16 ? 0 : lr / NPW;
-    bp[t] = ws + (long)c * RS + (wv * (KP / 4) + h * DK + g * 8) * WB;
+    bp[t] = ws + (long)c * RS + (wv * (KP / 4) + h * DK + g * 8) * WBITS / 8;
   }
   f32x4 acc[NCT];
 #pragma unroll
@@ -440,7 +447,8 @@ __device__ __forceinline__ void gemv_mfma(const char* ws, const float (&x)[NB][(
         const int st = bt * SB + u;
         av[u] = *reinterpret_cast<const u16x8*>(ap + st * 32);
 #pragma unroll
-        for (int t = 0; t < NCT; ++t) bw[u][t] = *reinterpret_cast<const BRaw*>(bp[t] + (q * KP + st * 32) * WB);
+        for (int t = 0; t < NCT; ++t)
+          bw[u][t] = *reinterpret_cast<const BRaw*>(bp[t] + (q * KP + st * 32) * WBITS / 8);
       }
     };
     u16x8 a0[SB];
@@ -505,17 +513,20 @@ template <int E_, int D_, int HQ_, int HK_, int F_, int ROT_, int W8_ = 0, int N
 struct MegaCfg {
   static constexpr int E = E_, D = D_, HQ = HQ_, HK = HK_, F = F_, ROT = ROT_, W8 = W8_, NB = NB_, MM = MM_;
   static_assert(NB == 1 || NB == 2 || NB == 4, "rows per step");
-  static constexpr int WB = W8 ? 1 : 2;  // bytes per weight
+  // W8: weight format (0 bf16, 1 int8, 2 int4 weight-only with per-output-channel scales)
+  static_assert(W8 >= 0 && W8 <= 2 && (W8 != 2 || MM), "int4 weights run on the MFMA phases");
+  static constexpr int WBITS = W8 == 0 ? 16 : W8 == 1 ? 8 : 4;
   static constexpr int NQKV = (HQ + 2 * HK) * D;
   static constexpr int NPQ = NQKV / NWG, NPO = E / NWG, NP1 = F / NWG, NP2 = E / NWG;
   // slice bytes (global, [rows][in] contiguous): QKV [0, QB) → out [QB, QB + OB) (free during
   // QKV) → FFN1 [0, F1B), whose first F1PRE bytes stream in during the attention phase
   // (workgroups without attention work) or the out-projection prologue (the others) and the rest
   // once the out slice is consumed → FFN2 [0, F2B) → next QKV [0, QB)
-  static constexpr int QB = NPQ * E * WB, OB = NPO * E * WB, F1B = NP1 * E * WB, F2B = NP2 * F * WB;
+  static constexpr int QB = NPQ * E * WBITS / 8, OB = NPO * E * WBITS / 8, F1B = NP1 * E * WBITS / 8,
+                       F2B = NP2 * F * WBITS / 8;
   // LDS image: every weight row is padded by 16 B (row strides RSE / RSF), so the 16 rows of an
   // MFMA B fragment (one 16-B read per lane, same k) start on 16 different bank quads
-  static constexpr int RBE = E * WB, RBF = F * WB, RSE = RBE + 16, RSF = RBF + 16;
+  static constexpr int RBE = E * WBITS / 8, RBF = F * WBITS / 8, RSE = RBE + 16, RSF = RBF + 16;
   static constexpr int OUT_OFF = NPQ * RSE;
   static constexpr int F1PRE = QB < F1B ? QB : F1B;
   static constexpr int WL = (NPQ + NPO) * RSE > NP1 * RSE ? (NPQ + NPO) * RSE : NP1 * RSE;
@@ -542,7 +553,7 @@ template <class C, int NPW, int K, int RS, class Mid, class End>
 __device__ __forceinline__ void gemv_phase(const char* ws, const float (&x)[C::NB][(K + 2047) / 2048][8],
                                            float* red, bf16_t* xs, int tid, Mid mid, End end, float (&r)[C::NB]) {
   if constexpr (C::MM)
-    gemv_mfma<NPW, K, C::NB, RS, C::W8 != 0>(ws, x, red, xs, tid, mid, end, r);
+    gemv_mfma<NPW, K, C::NB, RS, C::W8>(ws, x, red, xs, tid, mid, end, r);
   else
     gemv_lds<NPW, K, C::W8 != 0, C::NB, RS>(ws, x, red, tid, mid, end, r);
 }
@@ -558,9 +569,9 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
   constexpr int PSTR = D + 2;
   constexpr int NB = C::NB;
   constexpr bool W8 = C::W8 != 0;
-  // a workgroup's weight slice: `rows` [out] rows of `in` weights, C::WB bytes each
+  // a workgroup's weight slice: `rows` [out] rows of `in` weights, C::WBITS bits each
   auto slice = [](const bf16_t* w, long row0, long in) {
-    return reinterpret_cast<const bf16_t*>(reinterpret_cast<const char*>(w) + row0 * in * C::WB);
+    return reinterpret_cast<const bf16_t*>(reinterpret_cast<const char*>(w) + row0 * in * C::WBITS / 8);
   };
   constexpr int RSE = C::RSE, RSF = C::RSF, RBE = C::RBE, RBF = C::RBF;
   __shared__ __attribute__((aligned(1024))) char wl[C::WLB];
@@ -1531,6 +1542,10 @@ typedef MegaCfg<1024, 64, 16, 16, 4096, 1> CfgGpt350R;
 typedef MegaCfg<2048, 128, 16, 16, 8192, 0, 1> CfgGpt13W8;  // int8 weight-only
 typedef MegaCfg<2048, 128, 16, 4, 8192, 1, 1> CfgGqa4RW8;
 typedef MegaCfg<2048, 128, 16, 16, 8192, 0, 1, 1, 0> CfgGpt13W8V;  // int8 on the VALU (A/B)
+typedef MegaCfg<2048, 128, 16, 16, 8192, 0, 2> CfgGpt13W4;  // int4 weight-only
+typedef MegaCfg<2048, 128, 16, 4, 8192, 1, 2> CfgGqa4RW4;
+typedef MegaCfg<2048, 128, 16, 16, 8192, 0, 2, 2> CfgGpt13W4B2;
+typedef MegaCfg<2048, 128, 16, 16, 8192, 0, 2, 4> CfgGpt13W4B4;
 typedef MegaCfg<2048, 128, 16, 16, 8192, 0, 0, 1, 0> CfgGpt13V;  // 1.3B on the VALU (A/B)
 // batched steps (2 / 4 rows: small serving batches, beams)
 typedef MegaCfg<2048, 128, 16, 16, 8192, 0, 0, 2> CfgGpt13B2;
@@ -1554,10 +1569,11 @@ typedef MegaCfg<2048, 128, 16, 4, 8192, 1, 1, 4> CfgGqa4RW8B4;
 static const void* mega_fn(int E_, int D_, int hq, int hk, int F_, int rot, int w8, int nb, int mm = -1) {
 #define MEGA_CFG(C)                                                                           \
   if (E_ == C::E && D_ == C::D && hq == C::HQ && hk == C::HK && F_ == C::F &&                 \
-      (rot != 0) == C::ROT && (w8 != 0) == C::W8 && nb == C::NB && (mm < 0 || (mm != 0) == C::MM)) \
+      (rot != 0) == C::ROT && w8 == C::W8 && nb == C::NB && (mm < 0 || (mm != 0) == C::MM)) \
     return (const void*)decode_mega_kernel<C>;
   MEGA_CFG(CfgGpt13) MEGA_CFG(CfgGpt13R) MEGA_CFG(CfgGqa4) MEGA_CFG(CfgGqa4R)
   MEGA_CFG(CfgGpt350) MEGA_CFG(CfgGpt350R) MEGA_CFG(CfgGpt13W8) MEGA_CFG(CfgGqa4RW8) MEGA_CFG(CfgGpt13V) MEGA_CFG(CfgGpt13W8V)
+  MEGA_CFG(CfgGpt13W4) MEGA_CFG(CfgGqa4RW4) MEGA_CFG(CfgGpt13W4B2) MEGA_CFG(CfgGpt13W4B4)
   MEGA_CFG(CfgGpt13B2) MEGA_CFG(CfgGpt13B4) MEGA_CFG(CfgGpt13RB2) MEGA_CFG(CfgGpt13RB4)
   MEGA_CFG(CfgGqa4B2) MEGA_CFG(CfgGqa4B4) MEGA_CFG(CfgGqa4RB2) MEGA_CFG(CfgGqa4RB4)
   MEGA_CFG(CfgGpt350B2) MEGA_CFG(CfgGpt350B4) MEGA_CFG(CfgGpt350RB2) MEGA_CFG(CfgGpt350RB4)

@@ -53,10 +53,13 @@ def shape_of(gen):
 
 
 def _w8(gen):
-    """1 when every projection is int8 weight-only, 0 when every one is bf16, None otherwise."""
+    """Weight format code of the stack: 1 when every projection is int8 weight-only, 2 when every
+    one is int4, 0 when every one is bf16, None otherwise."""
     bits = {spec[k].bits for spec in gen.layers for k in ("qkv", "out", "ffn1", "ffn2")}
     if bits == {8}:
         return 1
+    if bits == {4}:
+        return 2
     if bits == {0} and all(spec[k].w.dtype == torch.bfloat16 for spec in gen.layers
                            for k in ("qkv", "out", "ffn1", "ffn2")):
         return 0
@@ -98,14 +101,20 @@ def eligible(gen, B: int) -> bool:
 
 def _out_in(lin):
     """[out, in] contiguous copy of a projection (each workgroup's slice is then one contiguous
-    run of rows): bf16, or (int8 weight-only) the int8 codes with their f32 per-output scales
-    recovered from the packed GEMV layout (exact: dequantised value / scale is the code)."""
-    if lin.bits == 8:
+    run of rows): bf16, or (weight-only) the int8 codes / int4 codes packed two per byte (k
+    ascending from the low nibble) with their f32 per-output scales, recovered from the packed
+    GEMV layout (exact: dequantised value / scale is the code)."""
+    if lin.bits in (4, 8):
         from ..ops.inference import weight_dequantize
         s = lin.scale.float().contiguous()
-        deq = weight_dequantize(lin.w, s, "weight_only_int8", "float32").t()  # [K, N] → [out, in]
-        q = torch.round(deq.float() / s[:, None]).clamp(-127, 127).to(torch.int8).contiguous()
-        return q, s
+        algo = "weight_only_int8" if lin.bits == 8 else "weight_only_int4"
+        deq = weight_dequantize(lin.w, s, algo, "float32").t()  # [K, N] → [out, in]
+        lo, hi = (-127, 127) if lin.bits == 8 else (-8, 7)
+        q = torch.round(deq.float() / s[:, None]).clamp(lo, hi).to(torch.int8)
+        if lin.bits == 4:
+            u = (q.to(torch.int16) & 0xF).to(torch.uint8)
+            q = u[:, 0::2] | (u[:, 1::2] << 4)
+        return q.contiguous(), s
     w = lin.w.detach()
     return (w if lin.trans else w.t()).contiguous(), None
 

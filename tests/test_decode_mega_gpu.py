@@ -160,6 +160,7 @@ def test_mega_decode_shape_gate():
     assert fb(2048, 128, 16, 16, 8192, 0, 0, 2) == 1 and fb(2048, 128, 16, 4, 8192, 128, 0, 4) == 1
     assert fb(2048, 128, 16, 16, 8192, 0, 0, 3) == 0 and fb(2048, 128, 16, 16, 8192, 0, 1, 2) == 1
     assert fb(1024, 64, 16, 16, 4096, 0, 1, 2) == 0
+    assert f(2048, 128, 16, 16, 8192, 0, 2) == 1 and f(1024, 64, 16, 16, 4096, 0, 2) == 0  # int4
     fv = _lib.lib().piamd_decode_mega_variant_supported  # GEMV kind: 1 MFMA, 0 VALU
     assert fv(2048, 128, 16, 16, 8192, 0, 0, 1, 1) == 1 and fv(2048, 128, 16, 16, 8192, 0, 0, 1, 0) == 1
     assert fv(1024, 64, 16, 16, 4096, 0, 0, 1, 0) == 0 and fv(2048, 128, 16, 16, 8192, 0, 1, 1, 1) == 1
@@ -167,7 +168,8 @@ def test_mega_decode_shape_gate():
     assert fv(2048, 128, 16, 16, 8192, 0, 0, 4, 0) == 0 and fv(1024, 64, 16, 16, 4096, 64, 0, 4, 1) == 1
 
 
-@pytest.mark.parametrize("shape", ["gpt13_int8", "gqa4_rope_int8", "gpt13_int8_valu"])
+@pytest.mark.parametrize("shape", ["gpt13_int8", "gqa4_rope_int8", "gpt13_int8_valu", "gpt13_int4",
+                                   "gqa4_rope_int4"])
 def test_mega_decode_int8_weight_only_matches_per_op_path(shape, monkeypatch):
     """int8 weight-only projections (FusedMultiTransformerWeightOnly decode): the kernel streams
     the int8 codes (half the bytes) and applies the per-output-channel scales after each column
@@ -178,8 +180,9 @@ def test_mega_decode_int8_weight_only_matches_per_op_path(shape, monkeypatch):
     over, kw = ({}, {}) if shape.startswith("gpt13") else \
         ({"num_kv_heads": 4}, dict(rotary_dim=128, neox_rotary=True))
     m = _gpt13b_width(2, 512, "gpt3-1.3b", **over)
-    g_mega = GPTGenerator(m, max_batch=1, max_seq_len=512, use_hip_graph=False, weight_only="int8", **kw)
-    g_ref = GPTGenerator(m, max_batch=1, max_seq_len=512, use_hip_graph=False, weight_only="int8", **kw)
+    wo = "int4" if "int4" in shape else "int8"
+    g_mega = GPTGenerator(m, max_batch=1, max_seq_len=512, use_hip_graph=False, weight_only=wo, **kw)
+    g_ref = GPTGenerator(m, max_batch=1, max_seq_len=512, use_hip_graph=False, weight_only=wo, **kw)
     g_ref.use_mega = False
     assert mega_decode.eligible(g_mega, 1)
     prompt = 50
@@ -190,7 +193,7 @@ def test_mega_decode_int8_weight_only_matches_per_op_path(shape, monkeypatch):
     for step in range(4):
         tok = lb.argmax(-1)
         la, lb = g_mega.decode(tok, pos), g_ref.decode(tok, pos)
-        assert g_mega._mega[1].w8 == 1 and g_mega._mega[1].loader == 0
+        assert g_mega._mega[1].w8 == (2 if wo == "int4" else 1) and g_mega._mega[1].loader == 0
         assert g_mega._mega[1].mm == (0 if shape.endswith("valu") else 1)
         assert _rel(la, lb) < 2e-2, (step, _rel(la, lb))
         pos += 1
@@ -198,7 +201,7 @@ def test_mega_decode_int8_weight_only_matches_per_op_path(shape, monkeypatch):
 
 
 @pytest.mark.parametrize("B", [2, 4])
-@pytest.mark.parametrize("shape", ["gpt13", "gpt3-350m", "gqa4_rope_neox", "gpt13_int8"])
+@pytest.mark.parametrize("shape", ["gpt13", "gpt3-350m", "gqa4_rope_neox", "gpt13_int8", "gpt13_int4"])
 def test_mega_decode_batched_rows_match_per_op_path(shape, B):
     """Batched single-launch steps (MegaCfg NB = 2 / 4: one LDS weight slice applied to every row,
     one attention workgroup per (row, head, split)) with a different prompt length per row — each
@@ -206,12 +209,13 @@ def test_mega_decode_batched_rows_match_per_op_path(shape, B):
     from paddle_infer_amd.inference import mega_decode
     from paddle_infer_amd.inference.generation import GPTGenerator
     preset, over, rope = {"gpt13": ("gpt3-1.3b", {}, None), "gpt13_int8": ("gpt3-1.3b", {}, None),
+                          "gpt13_int4": ("gpt3-1.3b", {}, None),
                           "gpt3-350m": ("gpt3-350m", {}, None),
                           "gqa4_rope_neox": ("gpt3-1.3b", {"num_kv_heads": 4}, True)}[shape]
     m = _gpt13b_width(2, 512, preset, **over)
     kw = dict(rotary_dim=m.cfg.head_dim, neox_rotary=rope) if rope is not None else {}
-    if shape.endswith("int8"):
-        kw["weight_only"] = "int8"
+    if shape.endswith(("int8", "int4")):
+        kw["weight_only"] = shape[-4:]
     g_mega = GPTGenerator(m, max_batch=B, max_seq_len=512, use_hip_graph=False, **kw)
     g_ref = GPTGenerator(m, max_batch=B, max_seq_len=512, use_hip_graph=False, **kw)
     g_ref.use_mega = False

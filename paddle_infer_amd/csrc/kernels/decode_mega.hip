@@ -86,7 +86,8 @@ struct MegaArgs {
                         // GEMV done, barrier arrival
   int late_dma;         // bit 0: the FFN phases issue the next slice only after their GEMV; bit 1:
                         // attention workgroups queue their FFN1 head in the out prologue instead
-                        // of at the end of the attention phase (decode_mega_kernel; A/B knobs)
+                        // of at the end of the attention phase; bit 2: the FFN2 slice head is
+                        // touched right behind the FFN1 head (decode_mega_kernel; A/B knobs)
   int loader;           // 1: decode_mega_lw_kernel (dedicated loader wave, 16 KiB chunk ring)
   int rot;              // rotary dims: 0 or D (whole head)
   int neox;             // 1: rotate-half (NeoX), 0: interleaved pairs (GPT-J)
@@ -357,6 +358,17 @@ __device__ __forceinline__ void prefetch_p(const bf16_t* src, int from, int to, 
   }
 }
 
+// Loader waves: read bytes [from, to) of `src` through the cache hierarchy into ONE 1 KiB LDS
+// scratch piece (the data is dropped): an early touch of a later phase's slice, so its real DMA
+// is served from the memory-side cache instead of HBM (MegaArgs.late_dma bit 2, A/B).
+__device__ __forceinline__ void touch(const bf16_t* src, int from, int to, char* scratch, int wv, int lane) {
+  if (wv == 0 || src == nullptr) return;
+  const char* s = reinterpret_cast<const char*>(src) + lane * 16;
+  for (int p = (from >> 10) + wv - 1; p < (to >> 10); p += 3)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(s + p * 1024),
+                                     (__attribute__((address_space(3))) void*)scratch, 16, 0, 0);
+}
+
 // MFMA form of gemv_lds for bf16 slices (same contract: x as gemv_lds, r[b] = column tid's sum
 // for tid < NPW; `mid` and `end` both run once the whole slice is consumed). The activation rows
 // are staged in LDS (`xs`: NB rows of KP = min(K, 8192 / NB) k, 16-B padded; one pass for every
@@ -538,6 +550,10 @@ struct MegaCfg {
   // the out phase of a non-attention workgroup waits for every DMA older than its FFN1 head: the
   // newest F1PRE/1 KiB/3 wave-instructions per loader wave (floor: the minimum over the waves)
   static constexpr int WAIT_OLD = F1PRE / 1024 / 3;
+  // FFN2 touch (late_dma bit 2): the first TOUCHB bytes of the slice right behind the FFN1 head,
+  // TWAIT wave-instructions per loader wave outstanding in all (vmcnt holds ≤ 63)
+  static constexpr int TOUCHB = (63 - WAIT_OLD) * 3 * 1024 < F2B ? (63 - WAIT_OLD) * 3 * 1024 : F2B;
+  static constexpr int TWAIT = WAIT_OLD + TOUCHB / 1024 / 3;
   static constexpr int LPR = D / 8;  // lanes per head row (16 B each)
   static_assert(NQKV % NWG == 0 && E % NWG == 0 && F % NWG == 0, "columns split evenly over the grid");
   static_assert(WLB <= 132 * 1024, "slices fit the LDS image");
@@ -580,9 +596,11 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
   __shared__ float wred[8 * NB];
   __shared__ float sc[256];
   __shared__ float pv[4][D];
+  __shared__ __attribute__((aligned(1024))) char tch[1024];  // touch() scratch
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, w = blockIdx.x;
   const long pst = pstride_hd(HQ, D, a.nsplit);  // one row's partial block
+  const bool tou = (a.late_dma & 4) != 0;
   unsigned nbar = 0;
 
   prefetch_p<RBE>(slice(a.layers[0].wqkv, (long)w * NPQ, E), 0, C::QB, wl, wv, lane);
@@ -811,8 +829,10 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
       // K/V are consumed: the loader waves queue the FFN1 head now, behind wave 0's partial
       // stores and grid barrier, so it no longer stalls their out-projection GEMV work
       if (!(a.late_dma & 2)) prefetch_p<RBE>(w1s, 0, C::F1PRE, wl, wv, lane);
+      if (tou) touch(slice(Ly.w2, (long)w * NP2, F), 0, C::TOUCHB, tch, wv, lane);
     } else {
       prefetch_p<RBE>(w1s, 0, C::F1PRE, wl, wv, lane);
+      if (tou) touch(slice(Ly.w2, (long)w * NP2, F), 0, C::TOUCHB, tch, wv, lane);
     }
     if (wv == 0) grid_sync(a, ++nbar, lane); else ++nbar;
     // ---------------------------------------------------------------- out projection
@@ -820,7 +840,10 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
     // end by attention workgroups) and waits for the older out slice only; with late_dma bit 1 the
     // attention workgroups queue the head only here (every older load has to land first)
     const bool attn_late = w < NB * HQ * a.nsplit && (a.late_dma & 2);
-    phase_start<C::WAIT_OLD>(a, wv, nbar, attn_late ? WAIT_ALL : WAIT_OLDER);
+    if (tou && !attn_late)  // the FFN2 touches are queued behind the FFN1 head
+      phase_start<C::TWAIT>(a, wv, nbar, WAIT_OLDER);
+    else
+      phase_start<C::WAIT_OLD>(a, wv, nbar, attn_late ? WAIT_ALL : WAIT_OLDER);
     {
       const int ocol = w * NPO + (lane & (NPO - 1));
       const float bo = bf2f(Ly.bo[ocol]);

@@ -172,7 +172,10 @@ class MegaDecoder:
         # at the GEMV midpoint (0): the loader waves are compute waves too, and a 64 KiB DMA burst
         # stalls their issue for ~2 us (FFN1 / FFN2 GEMV 5.1 / 4.5 us -> 2.7 / 1.8 us late; kernel
         # 985 -> 956 us, profiles/decode_mega_r4.txt)
-        self.late_dma = int(os.environ.get("PIAMD_MEGA_LATE_DMA", "1"))
+        # bit 2 (batch 1 default): the FFN2 slice head is read through the memory-side cache right
+        # behind the FFN1 head, so the FFN1 → FFN2 hand-over DMA is served from it (kernel
+        # 832 → 816 µs; at 4 rows every workgroup attends and the touch only moves the wait)
+        self.late_dma = int(os.environ.get("PIAMD_MEGA_LATE_DMA", "5" if nb == 1 else "1"))
         # 1: the variant with a dedicated loader wave and a 16 KiB chunk ring (decode_mega_lw_kernel,
         # VALU GEMVs; round 4: kernel 946 vs 968 us against the VALU 4-wave kernel); 0 (default):
         # the 4-wave templated kernel (decode_mega_kernel), whose MFMA GEMV phases now beat it

@@ -180,12 +180,23 @@ __device__ __forceinline__ void gemm_mainloop(const bf16_t* __restrict__ a, long
 // Epilogue: waves laid out WM (M) × 8/WM (N), each MB × NB blocks of 32 × 32 (default: the 256²
 // tile, 2 × 4 waves of 4 × 2). Lane owns row m0 + wr·32MB + mb·32 + l31 (stored while < mend);
 // columns n = n0 + wc·32NB + nb·32 + 8g + 4·hi + (0..3) (stored while < N).
+// Output-row remap of a phase convolution (the strided data gradient): row m = (img, oh, ow) of
+// the OHp × OWp phase grid lands on pixel (img, oh·st_h + ph, ow·st_w + pw) of an H × W output.
+struct RowMap {
+  int ohw_p, ow_p, hw_d, w_d, st_h, st_w, ph, pw;
+  __device__ __forceinline__ long long row(int m) const {
+    const int img = m / ohw_p, rem = m - img * ohw_p, oh = rem / ow_p, ow = rem - oh * ow_p;
+    return (long long)img * hw_d + (long long)(oh * st_h + ph) * w_d + ow * st_w + pw;
+  }
+};
+
 template <int WM = 2, int MB = 4, int NB = 2, bool F16 = false>
 __device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[MB][NB], void* __restrict__ c,
                                               long long ldc, int c_f32, int accumulate, int m0,
                                               int mend, int n0, int N, int epi, int act,
                                               const bf16_t* __restrict__ bias,
-                                              bf16_t* __restrict__ aux, long long ldaux) {
+                                              bf16_t* __restrict__ aux, long long ldaux,
+                                              const RowMap* rmap = nullptr) {
   constexpr int WC = NWAVE / WM;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w / WC, wc = w % WC;
   const int hi = lane >> 5, l31 = lane & 31;
@@ -193,6 +204,7 @@ __device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[MB][NB], void*
   for (int mb = 0; mb < MB; ++mb) {
     const int m = m0 + wr * (32 * MB) + mb * 32 + l31;
     if (m >= mend) continue;
+    const long long mr = rmap ? rmap->row(m) : (long long)m;  // destination row
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
 #pragma unroll
@@ -217,14 +229,14 @@ __device__ __forceinline__ void gemm_epilogue(const f32x16 (&acc)[MB][NB], void*
           for (int j = 0; j < 4; ++j) v[j] *= act_grad(h2f<F16>(h[j]), act);
         }
         if (c_f32) {
-          f32x4* p = reinterpret_cast<f32x4*>((float*)c + (long long)m * ldc + n);
+          f32x4* p = reinterpret_cast<f32x4*>((float*)c + mr * ldc + n);
           f32x4 o = accumulate ? *p : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int j = 0; j < 4; ++j) o[j] += v[j];
           *p = o;
         } else {
           u16x4 o;
-          bf16_t* p = (bf16_t*)c + (long long)m * ldc + n;
+          bf16_t* p = (bf16_t*)c + mr * ldc + n;
           if (accumulate) {
             const u16x4 old = *reinterpret_cast<const u16x4*>(p);
 #pragma unroll
@@ -437,7 +449,7 @@ template <int WM, int MB, int NB, bool SC = false, bool F16 = false>
 __global__ __launch_bounds__(NTHR, 1) void conv_fwd_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ wt, const bf16_t* __restrict__ zero,
     bf16_t* __restrict__ y, float* __restrict__ ws, int ksplit, ConvGeom g, int Kout, int act,
-    const bf16_t* __restrict__ bias, int yf32, float* __restrict__ stats) {
+    const bf16_t* __restrict__ bias, int yf32, float* __restrict__ stats, RowMap rm) {
   constexpr int WC = NWAVE / WM, TN = WC * NB * 32;
   constexpr int B_BYTES = TN * BK * 2, SBYTES = TILE_BYTES + B_BYTES;
   __shared__ __attribute__((aligned(1024))) char smem[2 * SBYTES];
@@ -543,10 +555,11 @@ __global__ __launch_bounds__(NTHR, 1) void conv_fwd_kernel(
                               EPI_STORE, 0, nullptr, nullptr, 0);
   else if (yf32)  // f32 output (the split-bf16 fp32 convolution): plain store, no epilogue ops
     gemm_epilogue<WM, MB, NB>(acc, (float*)y, Kout, 1, 0, m0, M, n0, Kout, EPI_STORE, 0, nullptr,
-                              nullptr, 0);
+                              nullptr, 0, rm.ohw_p ? &rm : nullptr);
   else
     gemm_epilogue<WM, MB, NB, F16>(acc, y, Kout, 0, 0, m0, M, n0, Kout,
-                              (bias || act) ? EPI_BIAS_ACT : EPI_STORE, act, bias, nullptr, 0);
+                              (bias || act) ? EPI_BIAS_ACT : EPI_STORE, act, bias, nullptr, 0,
+                              rm.ohw_p ? &rm : nullptr);
   if (stats)  // (host: ksplit == 1, 16-bit output without bias / activation)
     conv_tile_stats<WM, MB, NB, F16>(acc, smem, stats, m0, M, n0, Kout, tile / tn, tm);
 }
@@ -914,9 +927,10 @@ __global__ __launch_bounds__(256) void conv_splitk_finish_f32(const float* __res
 template <bool F16>
 static void conv_fwd_launch(int tile_n, bool sc, unsigned grid, hipStream_t st, const bf16_t* xb,
                             const bf16_t* wb, const bf16_t* zb, bf16_t* y, float* wsf, int ksplit,
-                            const ConvGeom& g, int Kout, int act, const bf16_t* bb, int yf32, float* stats) {
+                            const ConvGeom& g, int Kout, int act, const bf16_t* bb, int yf32, float* stats,
+                            const RowMap& rm) {
 #define CONV_FWD(WM, MB, NB, SCV) \
-  hipLaunchKernelGGL((conv_fwd_kernel<WM, MB, NB, SCV, F16>), dim3(grid), dim3(NTHR), 0, st, xb, wb, zb, y, wsf, ksplit, g, Kout, act, bb, yf32, stats)
+  hipLaunchKernelGGL((conv_fwd_kernel<WM, MB, NB, SCV, F16>), dim3(grid), dim3(NTHR), 0, st, xb, wb, zb, y, wsf, ksplit, g, Kout, act, bb, yf32, stats, rm)
   if (tile_n == 64) {
     if (sc) CONV_FWD(8, 1, 2, true); else CONV_FWD(8, 1, 2, false);
   } else if (tile_n == 128) {
@@ -929,15 +943,26 @@ static void conv_fwd_launch(int tile_n, bool sc, unsigned grid, hipStream_t st, 
 
 // stats (nullable): f32 [3][Kout][ceil(M / 256)] per-tile BatchNorm statistics of y
 // (conv_tile_stats) — ksplit == 1, 16-bit y, no bias / activation.
-PIAMD_EXPORT int piamd_conv2d_fwd2(const void* x, const void* wt, const void* zero, void* y, int N,
+// dst_h > 0: y is an N × dst_h × dst_w × Kout tensor and this convolution's OH × OW outputs are
+// its phase (ph, pw) of stride (rs_h, rs_w): pixel (oh, ow) lands on (oh·rs_h + ph, ow·rs_w + pw)
+// (the strided data gradient's phases, written in place) — ksplit == 1.
+PIAMD_EXPORT int piamd_conv2d_fwd3(const void* x, const void* wt, const void* zero, void* y, int N,
                                    int H, int W, int C, int OH, int OW, int R, int S, int st_h,
                                    int st_w, int pad_h, int pad_w, int dil_h, int dil_w, int Kout,
                                    int act, const void* bias, int tile_n, int ksplit, void* ws,
-                                   int flags, float* stats, hipStream_t st) {
+                                   int flags, float* stats, int dst_h, int dst_w, int rs_h, int rs_w,
+                                   int ph, int pw, hipStream_t st) {
   const bool sc = C == 8;
   const int f16 = flags & 1, yf32 = (flags >> 1) & 1;
   if (yf32 && (bias || act)) return (int)hipErrorInvalidValue;
   if (stats && (ksplit != 1 || yf32 || bias || act)) return (int)hipErrorInvalidValue;
+  RowMap rm{0, 0, 0, 0, 0, 0, 0, 0};
+  if (dst_h > 0) {
+    if (ksplit != 1 || rs_h < 1 || rs_w < 1 || ph < 0 || pw < 0 || (OH - 1) * rs_h + ph >= dst_h ||
+        (OW - 1) * rs_w + pw >= dst_w)
+      return (int)hipErrorInvalidValue;
+    rm = RowMap{OH * OW, OW, dst_h * dst_w, dst_w, rs_h, rs_w, ph, pw};
+  }
   if ((C % BK && !sc) || Kout % 4 || N < 1 || OH < 1 || OW < 1 || R < 1 || S < 1 || !zero || ksplit < 1 ||
       (ksplit > 1 && !ws) || ksplit > (sc ? (R * S + 7) / 8 : R * S * (C / BK)) ||
       (tile_n != 64 && tile_n != 128 && tile_n != 256))
@@ -952,8 +977,8 @@ PIAMD_EXPORT int piamd_conv2d_fwd2(const void* x, const void* wt, const void* ze
   const auto zb = (const bf16_t*)zero;
   const auto bb = (const bf16_t*)bias;
   float* wsf = (float*)ws;
-  if (f16) conv_fwd_launch<true>(tile_n, sc, grid, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb, yf32, stats);
-  else conv_fwd_launch<false>(tile_n, sc, grid, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb, yf32, stats);
+  if (f16) conv_fwd_launch<true>(tile_n, sc, grid, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb, yf32, stats, rm);
+  else conv_fwd_launch<false>(tile_n, sc, grid, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb, yf32, stats, rm);
   if (ksplit > 1) {
     const long long MN = M * Kout;
     const dim3 fg((unsigned)((MN / 4 + 255) / 256));
@@ -970,8 +995,17 @@ PIAMD_EXPORT int piamd_conv2d_fwd(const void* x, const void* wt, const void* zer
                                   int st_w, int pad_h, int pad_w, int dil_h, int dil_w, int Kout,
                                   int act, const void* bias, int tile_n, int ksplit, void* ws,
                                   int flags, hipStream_t st) {
-  return piamd_conv2d_fwd2(x, wt, zero, y, N, H, W, C, OH, OW, R, S, st_h, st_w, pad_h, pad_w, dil_h,
-                           dil_w, Kout, act, bias, tile_n, ksplit, ws, flags, nullptr, st);
+  return piamd_conv2d_fwd3(x, wt, zero, y, N, H, W, C, OH, OW, R, S, st_h, st_w, pad_h, pad_w, dil_h,
+                           dil_w, Kout, act, bias, tile_n, ksplit, ws, flags, nullptr, 0, 0, 0, 0, 0, 0, st);
+}
+
+PIAMD_EXPORT int piamd_conv2d_fwd2(const void* x, const void* wt, const void* zero, void* y, int N,
+                                   int H, int W, int C, int OH, int OW, int R, int S, int st_h,
+                                   int st_w, int pad_h, int pad_w, int dil_h, int dil_w, int Kout,
+                                   int act, const void* bias, int tile_n, int ksplit, void* ws,
+                                   int flags, float* stats, hipStream_t st) {
+  return piamd_conv2d_fwd3(x, wt, zero, y, N, H, W, C, OH, OW, R, S, st_h, st_w, pad_h, pad_w, dil_h,
+                           dil_w, Kout, act, bias, tile_n, ksplit, ws, flags, stats, 0, 0, 0, 0, 0, 0, st);
 }
 
 // NHWC implicit-GEMM convolution weight gradient: x [N][H][W][C], dy [N][OH][OW][Kout] 16-bit

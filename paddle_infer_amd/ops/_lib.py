@@ -270,6 +270,9 @@ _SIGS["piamd_conv2d_fwd"] = [c_void_p] * 4 + [c_int] * 16 + [c_void_p, c_int, c_
 # ... flags, stats (f32 [3][Kout][ceil(M/256)] per-tile BN statistics, nullable), stream
 _SIGS["piamd_conv2d_fwd2"] = ([c_void_p] * 4 + [c_int] * 16
                               + [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p])
+# ... stats, dst_h, dst_w, rs_h, rs_w, ph, pw (phase write into a larger output), stream
+_SIGS["piamd_conv2d_fwd3"] = ([c_void_p] * 4 + [c_int] * 16
+                              + [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p] + [c_int] * 6 + [c_void_p])
 # dtype, nhwc, x, res, y, N, C, S, gamma, beta, run_mean, run_var, mean, rstd, momentum, eps,
 # training, act, ws, stream
 _SIGS["piamd_bn_fwd"] = ([c_int, c_int] + [c_void_p] * 3 + [c_int] * 3 + [c_void_p] * 6

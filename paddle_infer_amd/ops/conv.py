@@ -259,29 +259,46 @@ def conv2d_dgrad_strided(dy, weight, H, W, st, pad, dil, out_f32=False):
             # sub-filter [C][R'][S'][K]: W[k][c][rt[i]][stp[j]] (taps are arithmetic progressions:
             # strided slices + flips, no index tensor — capturable in a hipGraph)
             wsub = _take_ap(_take_ap(wb, 2, rt), 3, stp).permute(1, 2, 3, 0).contiguous()
-            y = _launch_geom(dy, wsub, (1, 1), (ph2, pw2), (dh2, dw2), Hp, Wp, out_f32)
-            dx[:, ph::st[0], pw::st[1], :] = y
+            # the phase convolution writes its outputs straight into dX's phase pixels
+            _launch_geom(dy, wsub, (1, 1), (ph2, pw2), (dh2, dw2), Hp, Wp, out_f32,
+                         out=dx, phase=(st[0], st[1], ph, pw))
     return dx
 
 
-def _launch_geom(x, w_ohwi, st, pad, dil, OH, OW, out_f32=False):
-    """conv_fwd with an explicit output size (pads may be negative: taps outside are skipped)."""
+def _launch_geom(x, w_ohwi, st, pad, dil, OH, OW, out_f32=False, out=None, phase=None):
+    """conv_fwd with an explicit output size (pads may be negative: taps outside are skipped).
+    ``out`` [N, H', W', K] + ``phase`` (rs_h, rs_w, ph, pw): the OH × OW outputs are written to
+    pixels (oh·rs_h + ph, ow·rs_w + pw) of ``out`` (unsplit plans in the kernel epilogue, split-K
+    plans through a copy)."""
     N, H, W, C = x.shape
     K, R, S, _ = w_ohwi.shape
     M = N * OH * OW
     nk = R * S * (C // 64)
-    y = torch.empty(N, OH, OW, K, dtype=torch.float32 if out_f32 else x.dtype, device=x.device)
+    dt = torch.float32 if out_f32 else x.dtype
     flags = _f16(x) | (2 if out_f32 else 0)
+    if out is not None:
+        assert out.dtype == dt and out.is_contiguous() and out.shape[0] == N and out.shape[3] == K
+    y = None
 
     def run(plan):
+        nonlocal y
         tn, ks = plan
         ws = torch.empty(ks * M * K, dtype=torch.float32, device=x.device) if ks > 1 else None
-        _lib.call("piamd_conv2d_fwd", x.data_ptr(), w_ohwi.data_ptr(), _zero(x.device).data_ptr(),
-                  y.data_ptr(), N, H, W, C, OH, OW, R, S, st[0], st[1], pad[0], pad[1], dil[0],
-                  dil[1], K, 0, 0, tn, ks, _lib.ptr(ws), flags, _lib.stream())
+        direct = out is not None and ks == 1
+        if not direct and y is None:
+            y = torch.empty(N, OH, OW, K, dtype=dt, device=x.device)
+        dst = out if direct else y
+        geo = (out.shape[1], out.shape[2]) + tuple(phase) if direct else (0, 0, 0, 0, 0, 0)
+        _lib.call("piamd_conv2d_fwd3", x.data_ptr(), w_ohwi.data_ptr(), _zero(x.device).data_ptr(),
+                  dst.data_ptr(), N, H, W, C, OH, OW, R, S, st[0], st[1], pad[0], pad[1], dil[0],
+                  dil[1], K, 0, 0, tn, ks, _lib.ptr(ws), flags, None, *geo, _lib.stream())
+        if out is not None and not direct:
+            rs_h, rs_w, ph, pw = phase
+            out[:, ph::rs_h, pw::rs_w, :] = y
     run(_autotuned("conv2d_dgrad", (N, H, W, C, K, R, S, st, pad, dil, OH, OW)
-                   + (("f32",) if out_f32 else ()), _plan(M, K, nk), _fwd_candidates(M, K, nk), run))
-    return y
+                   + (("f32",) if out_f32 else ()) + (("phase",) if out is not None else ()),
+                   _plan(M, K, nk), _fwd_candidates(M, K, nk), run))
+    return out if out is not None else y
 
 
 def _padc(t, n):

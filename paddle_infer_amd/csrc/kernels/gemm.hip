@@ -449,7 +449,7 @@ template <int WM, int MB, int NB, bool SC = false, bool F16 = false>
 __global__ __launch_bounds__(NTHR, 1) void conv_fwd_kernel(
     const bf16_t* __restrict__ x, const bf16_t* __restrict__ wt, const bf16_t* __restrict__ zero,
     bf16_t* __restrict__ y, float* __restrict__ ws, int ksplit, ConvGeom g, int Kout, int act,
-    const bf16_t* __restrict__ bias, int yf32, float* __restrict__ stats, RowMap rm) {
+    const bf16_t* __restrict__ bias, int yf32, float* __restrict__ stats, RowMap rm, int yacc) {
   constexpr int WC = NWAVE / WM, TN = WC * NB * 32;
   constexpr int B_BYTES = TN * BK * 2, SBYTES = TILE_BYTES + B_BYTES;
   __shared__ __attribute__((aligned(1024))) char smem[2 * SBYTES];
@@ -557,7 +557,7 @@ __global__ __launch_bounds__(NTHR, 1) void conv_fwd_kernel(
     gemm_epilogue<WM, MB, NB>(acc, (float*)y, Kout, 1, 0, m0, M, n0, Kout, EPI_STORE, 0, nullptr,
                               nullptr, 0, rm.ohw_p ? &rm : nullptr);
   else
-    gemm_epilogue<WM, MB, NB, F16>(acc, y, Kout, 0, 0, m0, M, n0, Kout,
+    gemm_epilogue<WM, MB, NB, F16>(acc, y, Kout, 0, yacc, m0, M, n0, Kout,
                               (bias || act) ? EPI_BIAS_ACT : EPI_STORE, act, bias, nullptr, 0,
                               rm.ohw_p ? &rm : nullptr);
   if (stats)  // (host: ksplit == 1, 16-bit output without bias / activation)
@@ -928,9 +928,9 @@ template <bool F16>
 static void conv_fwd_launch(int tile_n, bool sc, unsigned grid, hipStream_t st, const bf16_t* xb,
                             const bf16_t* wb, const bf16_t* zb, bf16_t* y, float* wsf, int ksplit,
                             const ConvGeom& g, int Kout, int act, const bf16_t* bb, int yf32, float* stats,
-                            const RowMap& rm) {
+                            const RowMap& rm, int yacc) {
 #define CONV_FWD(WM, MB, NB, SCV) \
-  hipLaunchKernelGGL((conv_fwd_kernel<WM, MB, NB, SCV, F16>), dim3(grid), dim3(NTHR), 0, st, xb, wb, zb, y, wsf, ksplit, g, Kout, act, bb, yf32, stats, rm)
+  hipLaunchKernelGGL((conv_fwd_kernel<WM, MB, NB, SCV, F16>), dim3(grid), dim3(NTHR), 0, st, xb, wb, zb, y, wsf, ksplit, g, Kout, act, bb, yf32, stats, rm, yacc)
   if (tile_n == 64) {
     if (sc) CONV_FWD(8, 1, 2, true); else CONV_FWD(8, 1, 2, false);
   } else if (tile_n == 128) {
@@ -953,9 +953,11 @@ PIAMD_EXPORT int piamd_conv2d_fwd3(const void* x, const void* wt, const void* ze
                                    int flags, float* stats, int dst_h, int dst_w, int rs_h, int rs_w,
                                    int ph, int pw, hipStream_t st) {
   const bool sc = C == 8;
-  const int f16 = flags & 1, yf32 = (flags >> 1) & 1;
+  // flags bit 2: y += the convolution (16-bit y, ksplit == 1, no bias / activation / stats)
+  const int f16 = flags & 1, yf32 = (flags >> 1) & 1, yacc = (flags >> 2) & 1;
   if (yf32 && (bias || act)) return (int)hipErrorInvalidValue;
   if (stats && (ksplit != 1 || yf32 || bias || act)) return (int)hipErrorInvalidValue;
+  if (yacc && (ksplit != 1 || yf32 || bias || act || stats)) return (int)hipErrorInvalidValue;
   RowMap rm{0, 0, 0, 0, 0, 0, 0, 0};
   if (dst_h > 0) {
     if (ksplit != 1 || rs_h < 1 || rs_w < 1 || ph < 0 || pw < 0 || (OH - 1) * rs_h + ph >= dst_h ||
@@ -977,8 +979,8 @@ PIAMD_EXPORT int piamd_conv2d_fwd3(const void* x, const void* wt, const void* ze
   const auto zb = (const bf16_t*)zero;
   const auto bb = (const bf16_t*)bias;
   float* wsf = (float*)ws;
-  if (f16) conv_fwd_launch<true>(tile_n, sc, grid, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb, yf32, stats, rm);
-  else conv_fwd_launch<false>(tile_n, sc, grid, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb, yf32, stats, rm);
+  if (f16) conv_fwd_launch<true>(tile_n, sc, grid, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb, yf32, stats, rm, yacc);
+  else conv_fwd_launch<false>(tile_n, sc, grid, st, xb, wb, zb, (bf16_t*)y, wsf, ksplit, g, Kout, act, bb, yf32, stats, rm, yacc);
   if (ksplit > 1) {
     const long long MN = M * Kout;
     const dim3 fg((unsigned)((MN / 4 + 255) / 256));

@@ -11,6 +11,8 @@ Running statistics are updated in place on the device with Paddle's momentum con
 """
 from __future__ import annotations
 
+import threading
+
 import torch
 import torch.nn.functional as TF
 
@@ -82,10 +84,35 @@ def _conv_stats(x, training, nhwc, C):
     return part, P
 
 
+_JOIN = threading.local()
+
+
+class join_sink:
+    """``with join_sink(j):`` the next BatchNorm with a residual hands the residual's gradient to
+    the :class:`ops.conv.ResidualGradJoin` ``j`` (when its conv armed it) instead of returning it."""
+
+    def __init__(self, j):
+        self.j = j
+
+    def __enter__(self):
+        _JOIN.sink = self.j
+        return self.j
+
+    def __exit__(self, *exc):
+        _JOIN.sink = None
+        return False
+
+
+def _take_sink():
+    j = getattr(_JOIN, "sink", None)
+    _JOIN.sink = None
+    return j
+
+
 class _BNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, training, momentum,
-                eps, act, nhwc, dims):
+                eps, act, nhwc, dims, join=None):
         N, C, S = dims
         xc = x if (nhwc and not x.is_contiguous() and x.dim() == 4) else x.contiguous()
         if nhwc and x.dim() == 4 and not x.is_contiguous():  # channels_last NCHW view → [N,H,W,C]
@@ -121,6 +148,7 @@ class _BNAct(torch.autograd.Function):
                   int(training), int(act), ws.data_ptr(), _lib.ptr(ss), _lib.ptr(part), P,
                   _lib.stream())
         ctx.save_for_backward(xc, y, g, mean, rstd, ss)
+        ctx.join = join if residual is not None else None
         ctx.meta = (training, act, nhwc, dims, residual is not None, weight, bias,
                     x.dim() == 4 and nhwc and not x.is_contiguous())
         if ctx.meta[-1]:
@@ -141,12 +169,16 @@ class _BNAct(torch.autograd.Function):
                   y.data_ptr(), xc.data_ptr(), dx.data_ptr(), _lib.ptr(dres), N, C, S, _lib.ptr(g),
                   mean.data_ptr(), rstd.data_ptr(), dg.data_ptr(), db.data_ptr(), int(training),
                   int(act), ws.data_ptr(), _lib.ptr(ss), _lib.stream())
+        j = ctx.join
+        if j is not None and j.armed and dres is not None:  # the joined conv adds it (ops/conv.py)
+            j.dres = dres
+            dres = None
         if cl_view:
             dx = dx.permute(0, 3, 1, 2)
             dres = dres.permute(0, 3, 1, 2) if dres is not None else None
         gw = dg.to(weight.dtype) if weight is not None and ctx.needs_input_grad[1] else None
         gb = db.to(bias.dtype) if bias is not None and ctx.needs_input_grad[2] else None
-        return dx, gw, gb, dres, None, None, None, None, None, None, None, None
+        return dx, gw, gb, dres, None, None, None, None, None, None, None, None, None
 
 
 def batch_norm_act(x, running_mean, running_var, weight=None, bias=None, training=False,
@@ -167,5 +199,6 @@ def batch_norm_act(x, running_mean, running_var, weight=None, bias=None, trainin
     if not _supported(x, nhwc, C) or (residual is not None and residual.shape != x.shape):
         return _reference(x, running_mean, running_var, weight, bias, training, momentum, epsilon,
                           a, residual, data_format)
+    join = _take_sink() if residual is not None else None
     return _BNAct.apply(x, weight, bias, residual, running_mean, running_var, bool(training),
-                        momentum, epsilon, a, nhwc, (N, C, S))
+                        momentum, epsilon, a, nhwc, (N, C, S), join)

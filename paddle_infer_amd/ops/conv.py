@@ -265,11 +265,12 @@ def conv2d_dgrad_strided(dy, weight, H, W, st, pad, dil, out_f32=False):
     return dx
 
 
-def _launch_geom(x, w_ohwi, st, pad, dil, OH, OW, out_f32=False, out=None, phase=None):
+def _launch_geom(x, w_ohwi, st, pad, dil, OH, OW, out_f32=False, out=None, phase=None, acc=None):
     """conv_fwd with an explicit output size (pads may be negative: taps outside are skipped).
     ``out`` [N, H', W', K] + ``phase`` (rs_h, rs_w, ph, pw): the OH × OW outputs are written to
     pixels (oh·rs_h + ph, ow·rs_w + pw) of ``out`` (unsplit plans in the kernel epilogue, split-K
-    plans through a copy)."""
+    plans through a copy). ``acc`` [N, OH, OW, K] (16-bit): the result is added to it (in the
+    epilogue for unsplit plans) and it is returned."""
     N, H, W, C = x.shape
     K, R, S, _ = w_ohwi.shape
     M = N * OH * OW
@@ -279,6 +280,31 @@ def _launch_geom(x, w_ohwi, st, pad, dil, OH, OW, out_f32=False, out=None, phase
     if out is not None:
         assert out.dtype == dt and out.is_contiguous() and out.shape[0] == N and out.shape[3] == K
     y = None
+
+    if acc is not None:
+        assert out is None and not out_f32 and acc.shape == (N, OH, OW, K) and acc.dtype == x.dtype
+        # tuning runs would add into acc repeatedly: the plan is tuned (same cache key as the plain
+        # data gradient) on a scratch output, then the chosen plan accumulates once
+        scratch = []
+
+        def run_plain(plan):
+            tn_, ks_ = plan
+            if not scratch:
+                scratch.append(torch.empty(N, OH, OW, K, dtype=dt, device=x.device))
+            ws = torch.empty(ks_ * M * K, dtype=torch.float32, device=x.device) if ks_ > 1 else None
+            _lib.call("piamd_conv2d_fwd3", x.data_ptr(), w_ohwi.data_ptr(), _zero(x.device).data_ptr(),
+                      scratch[0].data_ptr(), N, H, W, C, OH, OW, R, S, st[0], st[1], pad[0], pad[1],
+                      dil[0], dil[1], K, 0, 0, tn_, ks_, _lib.ptr(ws), flags, None, 0, 0, 0, 0, 0, 0,
+                      _lib.stream())
+        tn, ks = _autotuned("conv2d_dgrad", (N, H, W, C, K, R, S, st, pad, dil, OH, OW),
+                            _plan(M, K, nk), _fwd_candidates(M, K, nk), run_plain)
+        if ks != 1:
+            acc += _launch_geom(x, w_ohwi, st, pad, dil, OH, OW)
+            return acc
+        _lib.call("piamd_conv2d_fwd3", x.data_ptr(), w_ohwi.data_ptr(), _zero(x.device).data_ptr(),
+                  acc.data_ptr(), N, H, W, C, OH, OW, R, S, st[0], st[1], pad[0], pad[1], dil[0],
+                  dil[1], K, 0, 0, tn, 1, None, flags | 4, None, 0, 0, 0, 0, 0, 0, _lib.stream())
+        return acc
 
     def run(plan):
         nonlocal y
@@ -319,12 +345,52 @@ def _take_stats():
     return v
 
 
+# Residual-gradient join (PIAMD_RES_JOIN=0: off). A residual block feeds its input x to a conv and,
+# as the residual, to the BatchNorm closing the block; autograd then sums the two gradients of x
+# with an ATen add. With a join, the BN's backward (which runs first) hands its residual gradient
+# to the join instead of returning it, and the conv's backward adds it in its data-gradient
+# epilogue (the kernel accumulates into it): one gradient, no add pass.
+RES_JOIN = os.environ.get("PIAMD_RES_JOIN", "1") != "0"
+_JOIN = threading.local()
+
+
+class ResidualGradJoin:
+    """Token shared by the conv that consumes a block input (``join_source``) and the BatchNorm that
+    adds it as the residual (``ops.batchnorm.join_sink``). ``armed``: the conv will take the
+    gradient; ``dres``: the BN's residual gradient (NHWC contiguous) until the conv consumes it."""
+
+    def __init__(self):
+        self.armed = False
+        self.dres = None
+
+
+class join_source:
+    """``with join_source(j):`` the next dense HIP conv consumes the residual gradient of ``j``."""
+
+    def __init__(self, j):
+        self.j = j
+
+    def __enter__(self):
+        _JOIN.src = self.j
+        return self.j
+
+    def __exit__(self, *exc):
+        _JOIN.src = None
+        return False
+
+
+def _take_join():
+    j = getattr(_JOIN, "src", None)
+    _JOIN.src = None
+    return j
+
+
 class _Conv2dNHWC(torch.autograd.Function):
     """Dense conv on the MFMA kernels: x [N,H,W,C0] bf16/fp16 (contiguous), weight [K0,C0,R,S].
     ``want_stats``: leave the output's per-tile BN statistics in the thread-local slot."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, st, pad, dil, act, want_stats=False):
+    def forward(ctx, x, weight, bias, st, pad, dil, act, want_stats=False, join=None):
         dt = x.dtype
         K0, C0, R, S = weight.shape
         K = -(-K0 // 4) * 4  # the epilogue stores 4 output channels per lane
@@ -338,6 +404,7 @@ class _Conv2dNHWC(torch.autograd.Function):
         b = None if bias is None else _padc(bias.to(dt), K)
         so = [] if (want_stats and K == K0) else None
         _STATS.v = None
+        ctx.join = join
         if C0 <= 8:  # stem mode: zero-pad the image channels to 8
             xc = _padc(x, 8).contiguous()
             nk = -(-(R * S) // 8)
@@ -404,10 +471,10 @@ class _Conv2dNHWC(torch.autograd.Function):
                 # dX = conv(dY, flip(W)ᵀ): filter [C][R][S][K] = W[k][c][R-1-r][S-1-s]
                 pad_t = (dil[0] * (R - 1) - pad[0], dil[1] * (S - 1) - pad[1])
                 w_t = wq.flip(2, 3).permute(1, 2, 3, 0).contiguous()
-                dx = _launch_geom(dyp, w_t, (1, 1), pad_t, dil, H, W)
+                dx = _launch_geom(dyp, w_t, (1, 1), pad_t, dil, H, W, acc=_join_acc(ctx, x, C0))
             else:
                 dx = conv2d_dgrad_strided(dyp, wq, H, W, st, pad, dil)
-            dx = dx[..., :C0] if C != C0 else dx
+            dx = _join_finish(ctx, dx[..., :C0] if C != C0 else dx)
         if ctx.needs_input_grad[1]:
             if wgrad_eligible(C, Kp, M):
                 dw = conv2d_wgrad(x, dyp, R, S, st, pad, dil, layout=ctx.w_layout)[:K0, :C0]
@@ -416,7 +483,7 @@ class _Conv2dNHWC(torch.autograd.Function):
             dw = dw.to(wdt)
         if has_bias and ctx.needs_input_grad[2]:
             db = dy.float().sum((0, 1, 2)).to(wdt)
-        return dx, dw, db, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None
 
     @staticmethod
     def _backward_prepped(ctx, x, w_t, dy):
@@ -430,8 +497,8 @@ class _Conv2dNHWC(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             pad_t = (dil[0] * (R - 1) - pad[0], dil[1] * (S - 1) - pad[1])
-            dx = _launch_geom(dyp, w_t, (1, 1), pad_t, dil, H, W)
-            dx = dx[..., :C0] if C != C0 else dx
+            dx = _launch_geom(dyp, w_t, (1, 1), pad_t, dil, H, W, acc=_join_acc(ctx, x, C0))
+            dx = _join_finish(ctx, dx[..., :C0] if C != C0 else dx)
         if ctx.needs_input_grad[1]:
             if wgrad_eligible(C, Kp, M):
                 dw = conv2d_wgrad(x, dyp, R, S, st, pad, dil, layout=ctx.w_layout)[:K0, :C0]
@@ -440,7 +507,27 @@ class _Conv2dNHWC(torch.autograd.Function):
             dw = dw.to(wdt)
         if has_bias and ctx.needs_input_grad[2]:
             db = dy.float().sum((0, 1, 2)).to(wdt)
-        return dx, dw, db, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None
+
+
+def _join_acc(ctx, x, C0):
+    """The joined residual gradient when the data-gradient kernel can accumulate into it (same
+    NHWC shape and dtype as dX, no channel padding); it is then consumed."""
+    j = ctx.join
+    d = j.dres if j is not None else None
+    if d is None or x.shape[-1] != C0 or d.shape != x.shape or d.dtype != x.dtype or not d.is_contiguous():
+        return None
+    j.dres = None
+    return d
+
+
+def _join_finish(ctx, dx):
+    """dX plus a joined residual gradient the kernel did not take."""
+    j = ctx.join
+    if j is not None and j.dres is not None:
+        dx = dx + j.dres.to(dx.dtype)
+        j.dres = None
+    return dx
 
 
 _WSRC = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
@@ -741,7 +828,10 @@ def conv2d_any(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, 
             y = _Conv1x1.apply(xh, weight, bias, st)
         else:
             want = BN_STATS and bias is None and torch.is_grad_enabled()
-            y = _Conv2dNHWC.apply(xh, weight, bias, st, pad, dil, 0, want)
+            join = _take_join()
+            if join is not None:
+                join.armed = True
+            y = _Conv2dNHWC.apply(xh, weight, bias, st, pad, dil, 0, want, join)
             part = _take_stats() if want else None
             out = y if nhwc else y.permute(0, 3, 1, 2)
             if part is not None:  # consumed by a BatchNorm of this very tensor (same version)
@@ -826,7 +916,7 @@ class _ConvTranspose(torch.autograd.Function):
             dw = dw.to(weight.dtype)
         if has_bias and ctx.needs_input_grad[2]:
             db = dy.float().sum((0, 1, 2)).to(weight.dtype)
-        return dx, dw, db, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None
 
 
 def conv2d_transpose_any(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1,

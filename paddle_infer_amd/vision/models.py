@@ -122,6 +122,37 @@ def vgg19(pretrained=False, batch_norm=False, **kw): return _vgg(19, batch_norm,
 
 
 # ----------------------------------------------------------------------------------------- ResNet
+def _residual_join(x, downsample):
+    """A residual-gradient join for a block whose residual is its input itself (ops/conv.py
+    ResidualGradJoin): the first conv's data-gradient epilogue adds the residual branch's
+    gradient, so autograd does not sum the two with a separate add. None where it does not
+    apply (a downsample branch, CPU, no autograd)."""
+    from ..ops import conv as _conv
+    if downsample is not None or not (_conv.RES_JOIN and x.is_cuda and torch.is_grad_enabled()):
+        return None
+    return _conv.ResidualGradJoin()
+
+
+class _Joined:
+    """``with _Joined(j, source=True)``: the next conv (source) / residual BatchNorm (sink) uses
+    the join ``j`` (no-op for None)."""
+
+    def __init__(self, j, source):
+        self.cm = None
+        if j is not None:
+            from ..ops import batchnorm as _bn, conv as _conv
+            self.cm = _conv.join_source(j) if source else _bn.join_sink(j)
+
+    def __enter__(self):
+        if self.cm is not None:
+            self.cm.__enter__()
+
+    def __exit__(self, *exc):
+        if self.cm is not None:
+            self.cm.__exit__(*exc)
+        return False
+
+
 class BasicBlock(nn.Layer):
     expansion = 1
 
@@ -137,8 +168,13 @@ class BasicBlock(nn.Layer):
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        out = self.bn1(self.conv1(x), act="relu")                 # fused BN + ReLU
-        return self.bn2(self.conv2(out), residual=idt, act="relu")  # fused BN + add + ReLU
+        j = _residual_join(x, self.downsample)
+        with _Joined(j, source=True):
+            h = self.conv1(x)
+        out = self.bn1(h, act="relu")                              # fused BN + ReLU
+        h = self.conv2(out)
+        with _Joined(j, source=False):
+            return self.bn2(h, residual=idt, act="relu")           # fused BN + add + ReLU
 
 
 class BottleneckBlock(nn.Layer):
@@ -160,9 +196,14 @@ class BottleneckBlock(nn.Layer):
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        out = self.bn1(self.conv1(x), act="relu")
+        j = _residual_join(x, self.downsample)
+        with _Joined(j, source=True):
+            h = self.conv1(x)
+        out = self.bn1(h, act="relu")
         out = self.bn2(self.conv2(out), act="relu")
-        return self.bn3(self.conv3(out), residual=idt, act="relu")  # fused BN + add + ReLU
+        h = self.conv3(out)
+        with _Joined(j, source=False):
+            return self.bn3(h, residual=idt, act="relu")  # fused BN + add + ReLU
 
 
 class ResNet(nn.Layer):

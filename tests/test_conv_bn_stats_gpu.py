@@ -68,3 +68,38 @@ def test_conv_bn_statistics_fused(shape):
     _close(gf, ref_conv_w.grad, 3e-2, 3e-2)
     _close(gf, gu, 1e-2, 1e-2)
     _close(xf, xu, 1e-2, 1e-2)
+
+
+@pytest.mark.parametrize("block", ["bottleneck", "basic"])
+def test_residual_gradient_join(block):
+    """Residual-gradient join (ops/conv.py ResidualGradJoin): the residual BatchNorm hands its
+    residual gradient to the block's first conv, whose data-gradient epilogue adds it. Gradients
+    of the block input and of every parameter against the same block with the join off (whose
+    parts are each checked against fp32 references in test_conv_gpu / test_batchnorm_gpu)."""
+    from paddle_infer_amd.ops import conv as oc
+    from paddle_infer_amd.vision import models as VM
+    torch.manual_seed(3)
+    C = 256 if block == "bottleneck" else 64
+    blk = (VM.BottleneckBlock(C, C // 4) if block == "bottleneck" else VM.BasicBlock(C, C)).to(DEV)
+    x0 = torch.randn(4, C, 14, 14, device=DEV).to(memory_format=torch.channels_last)
+
+    def run(on):
+        oc.RES_JOIN = on
+        try:
+            for p in blk.parameters():
+                p.grad = None
+            x = x0.clone().requires_grad_(True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = blk(x)
+            (y.float() * torch.linspace(-1, 1, y.numel(), device=DEV).view_as(y)).sum().backward()
+            return x.grad.float(), [p.grad.float().clone() for p in blk.parameters() if p.grad is not None]
+        finally:
+            oc.RES_JOIN = True
+
+    gx_on, gp_on = run(True)
+    gx_off, gp_off = run(False)
+    _close(gx_on, gx_off, 1e-2, 1e-2)
+    assert len(gp_on) == len(gp_off)
+    for a, b in zip(gp_on, gp_off):
+        _close(a, b, 1e-2, 1e-2)
+    assert gx_on.abs().max() > 0

@@ -1,37 +1,39 @@
-// Persistent whole-stack decode step ("megakernel") for batch-1 GPT decoding on gfx950.
+// Persistent whole-stack decode step ("megakernel") for GPT decoding on gfx950 (1, 2 or 4 rows).
 //
-// Why: the batch-1 decode step is a chain of 5 small launches per layer (QKV GEMV → attention →
-// out GEMV → FFN1 GEMV → FFN2 GEMV). Each GEMV streams 8-33 MB of weights and sits at its ramp
-// floor (profiles/gemv_decode_r3_nt.txt: 25 MB in ≈9 µs ≈ 2.8 TB/s) — HBM idles while a launch
-// drains and the next ramps up. Weights do not depend on activations, so one persistent kernel
-// can load the NEXT projection's weights while the current phase finishes and the grid syncs.
+// Why: a decode step is a chain of 5 small launches per layer (QKV GEMV → attention → out GEMV →
+// FFN1 GEMV → FFN2 GEMV). Each GEMV streams 8-33 MB of weights and sits at its ramp floor
+// (profiles/gemv_decode_r3_nt.txt: 25 MB in ≈9 µs ≈ 2.8 TB/s) — HBM idles while a launch drains
+// and the next ramps up. Weights do not depend on activations, so one persistent kernel can load
+// the NEXT projection's weights while the current phase finishes and the grid syncs.
 //
 // Design (one launch per token for all layers):
-//   * grid = 256 workgroups (one per CU, 1 wave-slot of LDS each) × 256 threads; every GEMV phase
-//     splits its N output columns evenly: WG w owns rows [w·NPW, (w+1)·NPW) of the [N][K] (out, in)
-//     weight, a CONTIGUOUS slice of ≤ 128 KiB that lives in LDS.
+//   * grid = 256 workgroups (one per CU) × 256 threads; every GEMV phase splits its N output
+//     columns evenly: WG w owns rows [w·NPW, (w+1)·NPW) of the [N][K] (out, in) weight, a
+//     CONTIGUOUS slice of ≤ 128 KiB held in LDS with every row padded by 16 B.
 //   * waves 1..3 are loaders: right after a phase has consumed its LDS slice they issue the next
 //     phase's slice with direct-to-LDS DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction),
 //     while wave 0 publishes the phase's outputs and waits on the grid barrier — the weight stream
 //     overlaps the barrier instead of following it. (A wave's loads retire in order, so the
 //     barrier-polling wave must not own prefetches; hence the loader / control split.)
+//   * the GEMV phases run on MFMA (gemv_mfma: activations staged in LDS, mfma_f32_16x16x32_bf16
+//     straight on the padded weight rows; int8 / int4 weight-only codes widened in registers);
+//     the VALU form (gemv_lds) remains for A/B instantiations.
 //   * cross-workgroup data (residual, q / new k,v, attention partials, FFN hidden) is published
-//     with agent-scope relaxed atomic stores and read with agent-scope atomic loads (coherent
-//     across the 8 per-XCD L2s without L2 write-back fences, see xcd_* in common.h); the barrier
-//     is a monotonically increasing arrival counter polled by one lane with s_sleep back-off. The
-//     grid is launched COOPERATIVELY (hipLaunchCooperativeKernel after an occupancy check), so all
-//     256 workgroups are co-resident by the runtime's guarantee; the spin stays bounded as a
-//     safety net (a timeout raises `err` and runs the launch to completion, every wave exits).
-//   * per layer: LN1 (recomputed per WG from the residual, 8 KB from L2) + QKV GEMV + bias, new
-//     k/v written to the cache → split-K attention over the cache (16 lanes per key row, base-2
-//     softmax) → partial combine + out GEMV + bias + residual → LN2 + FFN1 GEMV + bias + GELU →
-//     FFN2 GEMV + bias + residual. Rounding points match the launch-per-op path (bf16 LN output,
-//     bf16 cache / attention output / hidden / residual).
-// Shapes: decode_mega_kernel<MegaCfg<E, D, Hq, Hk, F, ROT>> — the instantiated widths are
-// listed at mega_fn (GPT-3 1.3B and 350M widths, a GQA 4:1 variant, each with and without rotary
-// embedding over the whole head); the dedicated-loader variant (decode_mega_lw_kernel) is the
-// GPT-1.3B shape only. Anything else: the host launcher refuses and the Python side takes the
-// per-op path.
+//     with agent-scope relaxed atomic stores into slots written once per launch (plain loads are
+//     then coherent across the 8 per-XCD L2s); the barrier is a two-level arrival counter polled
+//     by one lane with s_sleep back-off. The grid is launched COOPERATIVELY
+//     (hipLaunchCooperativeKernel after an occupancy check), so all 256 workgroups are co-resident
+//     by the runtime's guarantee; the spin stays bounded as a safety net (a timeout raises `err`
+//     and runs the launch to completion, every wave exits).
+//   * per layer: LN1 (recomputed per WG from the residual) + QKV GEMV + bias, new k/v written to
+//     the cache → split-K attention over the cache (one workgroup per (row, head, split), base-2
+//     softmax, optional whole-head RoPE) → partial combine + out GEMV + bias + residual → LN2 +
+//     FFN1 GEMV + bias + GELU → FFN2 GEMV + bias + residual. Rounding points match the
+//     launch-per-op path (bf16 LN output, bf16 cache / attention output / hidden / residual).
+// Shapes: decode_mega_kernel<MegaCfg<E, D, Hq, Hk, F, ROT, W8, NB, MM>> — the instantiated
+// variants are listed at mega_fn (GPT-3 1.3B and 350M widths, a GQA 4:1 variant, ± rotary
+// embedding, bf16 / int8 / int4 weights, 1 / 2 / 4 rows). Anything else: the host launcher
+// refuses and the Python side takes the per-op path.
 // Reference parity: one decode step of FusedMultiTransformer with time_step
 // (`paddle/fluid/operators/fused/fused_multi_transformer_op.cu`, masked_multihead_attention).
 #include "common.h"
@@ -88,7 +90,7 @@ struct MegaArgs {
                         // attention workgroups queue their FFN1 head in the out prologue instead
                         // of at the end of the attention phase; bit 2: the FFN2 slice head is
                         // touched right behind the FFN1 head (decode_mega_kernel; A/B knobs)
-  int loader;           // 1: decode_mega_lw_kernel (dedicated loader wave, 16 KiB chunk ring)
+  int loader;           // must be 0 (the retired dedicated-loader variant; field kept for the ABI)
   int rot;              // rotary dims: 0 or D (whole head)
   int neox;             // 1: rotate-half (NeoX), 0: interleaved pairs (GPT-J)
   float log2_base;      // log2 of the rotary base
@@ -985,416 +987,6 @@ __global__ __launch_bounds__(NT, 1) void decode_mega_kernel(MegaArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Variant with a DEDICATED loader wave (MegaArgs.loader = 1, PIAMD_MEGA_LOADER=1).
-// In decode_mega_kernel the loader waves are compute waves too: a DMA burst stalls their issue
-// once the CU's outstanding-request budget is used (profiles/decode_mega_r4.txt), so a slice can
-// only stream while they idle. Here a fifth wave does nothing but DMA:
-//   * the weights of a workgroup's whole step are one sequence of 16 KiB chunks (per layer: QKV 6,
-//     out 2, FFN1 8, FFN2 8), streamed through a 9-slot LDS ring (144 KiB); chunk g lives in slot
-//     g % 9 and is issued as soon as chunk g − 9 has been consumed by all four compute waves;
-//   * the loader publishes "chunks landed" (after counted vmcnt waits) and the compute waves
-//     publish "chunks consumed", both as LDS counters; a compute wave spins (s_sleep) on the
-//     landed counter before each chunk;
-//   * the loader never meets the compute waves at s_barrier: their workgroup barriers are LDS
-//     arrival counters among the four compute waves (wbar).
-// Every spin is bounded: a timeout raises the launch's failure flag (→ err) and falls through.
-constexpr int LW_NT = 320;
-constexpr int RCH = 16 * 1024, RSLOTS = 9, CPL = 24;
-constexpr unsigned LW_SPIN = 1u << 22;
-
-__global__ __launch_bounds__(LW_NT, 1) void decode_mega_lw_kernel(MegaArgs a) {
-  __shared__ __attribute__((aligned(1024))) char ring[RSLOTS * RCH];
-  __shared__ float red[4 * 32];
-  __shared__ float wred[2][8];  // block reductions, alternating buffers (one wbar each)
-  __shared__ float sc[256];
-  __shared__ float pv[4][D];
-  __shared__ unsigned ctr[4];  // [0] compute-wave barrier arrivals, [1] chunks consumed ×4, [2] chunks landed, [3] timeout
-
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, w = blockIdx.x;
-  constexpr int NPQ = NQKV / NWG, NPO = E / NWG, NP1 = F / NWG, NP2 = E / NWG;
-  static_assert(NPQ * E * 2 == 6 * RCH && NPO * E * 2 == 2 * RCH && NP1 * E * 2 == 8 * RCH &&
-                NP2 * F * 2 == 8 * RCH, "chunk map");
-  if (tid < 4) ctr[tid] = 0;
-  __syncthreads();  // the only s_barrier: before the loader wave splits off
-
-  auto timed_out = [&](unsigned& sp) {
-    if (++sp < LW_SPIN) return false;
-    if (lane == 0) __hip_atomic_store(&ctr[3], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return true;
-  };
-  auto lds_get = [&](int i) { return __hip_atomic_load(&ctr[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
-
-  if (wv == 4) {
-    // ------------------------------------------------------------------ loader wave
-    const int total = CPL * a.nl;
-    int gi = 0, lp = 0;
-    unsigned sp = 0;
-    while (lp < total) {
-      while (gi < total && (gi < RSLOTS || lds_get(1) >= 4u * (unsigned)(gi - RSLOTS + 1))) {
-        const int l = gi / CPL, c = gi % CPL;
-        const MegaLayer& Ly = a.layers[l];
-        const char* src =
-            c < 6 ? reinterpret_cast<const char*>(Ly.wqkv + (long)w * NPQ * E) + c * RCH
-            : c < 8 ? reinterpret_cast<const char*>(Ly.wo + (long)w * NPO * E) + (c - 6) * RCH
-            : c < 16 ? reinterpret_cast<const char*>(Ly.w1 + (long)w * NP1 * E) + (c - 8) * RCH
-                     : reinterpret_cast<const char*>(Ly.w2 + (long)w * NP2 * F) + (c - 16) * RCH;
-        src += lane * 16;
-        char* dst = ring + (gi % RSLOTS) * RCH;
-#pragma unroll
-        for (int p = 0; p < RCH / 1024; ++p)
-          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + p * 1024),
-                                           (__attribute__((address_space(3))) void*)(dst + p * 1024), 16, 0, 0);
-        ++gi;
-      }
-      if (lp < gi) {
-        // chunk lp landed once at most (gi − 1 − lp)·16 younger DMA instructions are outstanding;
-        // vmcnt holds at most 63, so wait down to three chunks in flight
-        const int n = gi - 1 - lp;
-        if (n >= 3) {
-          asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
-          lp = gi - 3;
-        } else if (n == 2) {
-          asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-          lp = gi - 2;
-        } else if (n == 1) {
-          asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-          lp = gi - 1;
-        } else {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          lp = gi;
-        }
-        if (lane == 0) __hip_atomic_store(&ctr[2], (unsigned)lp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        sp = 0;
-      } else {
-        __builtin_amdgcn_s_sleep(1);
-        if (timed_out(sp) || lds_get(3)) break;
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    return;
-  }
-
-  // ------------------------------------------------------------------ compute waves 0-3
-  const int pos = a.pos[0], L = pos + 1;
-  unsigned nbar = 0, kb = 0;
-  int g = 0;  // next chunk to consume
-  auto wbar = [&]() {
-    kb += 4;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_fetch_add(&ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    unsigned sp = 0;
-    while (lds_get(0) < kb) {
-      __builtin_amdgcn_s_sleep(0);
-      if (timed_out(sp) || lds_get(3)) break;
-    }
-    asm volatile("" ::: "memory");
-  };
-  // Block reductions over the 4 compute waves with ONE wbar each: consecutive reductions use
-  // alternating buffers, and a wave rewrites a buffer only after the next reduction's wbar, which
-  // every wave reaches after reading this one.
-  int rb = 0;
-  auto bsum2 = [&](float u, float v, float& su, float& sv) {
-    u = wave_sum(u);
-    v = wave_sum(v);
-    float* b = wred[rb];
-    rb ^= 1;
-    if (lane == 0) {
-      b[2 * wv] = u;
-      b[2 * wv + 1] = v;
-    }
-    wbar();
-    su = b[0] + b[2] + b[4] + b[6];
-    sv = b[1] + b[3] + b[5] + b[7];
-  };
-  auto bsum = [&](float v) {
-    v = wave_sum(v);
-    float* b = wred[rb];
-    rb ^= 1;
-    if (lane == 0) b[wv] = v;
-    wbar();
-    return b[0] + b[1] + b[2] + b[3];
-  };
-  auto bmax = [&](float v) {
-    v = wave_max(v);
-    float* b = wred[rb];
-    rb ^= 1;
-    if (lane == 0) b[wv] = v;
-    wbar();
-    return fmaxf(fmaxf(b[0], b[1]), fmaxf(b[2], b[3]));
-  };
-  auto pstart = [&](unsigned ph) {
-    wbar();
-    if (a.trace && tid == 0) a.trace[((long)w * a.nl * 5 + ph) * 4] = wall_clock64();
-  };
-  // GEMV over the next NPW·K·2 / 16 KiB ring chunks (column layout as in gemv_lds)
-  auto gemv = [&](auto npw, auto kch, const float(&x)[decltype(kch)::value][8]) {
-    constexpr int NPW = decltype(npw)::value, KCH = decltype(kch)::value;
-    constexpr int K = 2048 * KCH, CB = K * 2, CPC = RCH / CB, NCH = NPW / CPC;
-    constexpr int P = NPW <= 8 ? 8 : 32;
-    constexpr int LOGP = P == 8 ? 3 : 5;
-    float acc[P];
-#pragma unroll
-    for (int c = 0; c < P; ++c) acc[c] = 0.f;
-#pragma unroll
-    for (int ch = 0; ch < NCH; ++ch) {
-      unsigned sp = 0;
-      while (lds_get(2) < (unsigned)(g + 1)) {
-        __builtin_amdgcn_s_sleep(0);
-        if (timed_out(sp) || lds_get(3)) break;
-      }
-      asm volatile("" ::: "memory");
-      const char* ws = ring + (g % RSLOTS) * RCH;
-#pragma unroll
-      for (int cc = 0; cc < CPC; ++cc) {
-#pragma unroll
-        for (int j = 0; j < KCH; ++j) {
-          const u16x8 wt = *reinterpret_cast<const u16x8*>(ws + ((long)cc * K + (j * 256 + tid) * 8) * 2);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) acc[ch * CPC + cc] += x[j][i] * bf2f(wt[i]);
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the chunk are done
-      if (lane == 0) __hip_atomic_fetch_add(&ctr[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      ++g;
-    }
-    butterfly<P / 2, 32>(acc, lane);
-#pragma unroll
-    for (int o = 32 >> LOGP; o > 0; o >>= 1) acc[0] += __shfl_xor(acc[0], o, 64);
-    if ((lane & ((64 >> LOGP) - 1)) == 0) red[wv * P + (lane >> (6 - LOGP))] = acc[0];
-    wbar();
-    // (red is rewritten only by the next GEMV, behind at least the next phase's wbar)
-    float r = 0.f;
-    if (tid < NPW) r = red[tid] + red[P + tid] + red[2 * P + tid] + red[3 * P + tid];
-    return r;
-  };
-  auto ln_x = [&](const bf16_t* r, const bf16_t* gm, const bf16_t* bt, float (&x)[1][8]) {
-    const u16x8 gg = *reinterpret_cast<const u16x8*>(gm + tid * 8);
-    const u16x8 bb = *reinterpret_cast<const u16x8*>(bt + tid * 8);
-    float v[8];
-    ld_bf8(r + tid * 8, v);
-    // one reduction of (Σv, Σv²): var = E[v²] − mean² (f32 over 2048 bf16 values)
-    float s = 0.f, q = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      s += v[i];
-      q += v[i] * v[i];
-    }
-    float S, Q;
-    bsum2(s, q, S, Q);
-    const float mean = S * (1.f / E);
-    const float rs = rsqrtf(fmaxf(Q * (1.f / E) - mean * mean, 0.f) + a.eps);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) x[0][i] = bf2f(f2bf((v[i] - mean) * rs * bf2f(gg[i]) + bf2f(bb[i])));
-  };
-  using I1 = std::integral_constant<int, 1>;
-
-  for (int l = 0; l < a.nl; ++l) {
-    const MegaLayer& Ly = a.layers[l];
-    const bf16_t* rin = l == 0 ? a.resid : a.rbuf + (long)(2 * l - 1) * E;
-    bf16_t* rmid = a.rbuf + (long)(2 * l) * E;
-    bf16_t* rout = a.rbuf + (long)(2 * l + 1) * E;
-    float* qn = a.qn + (long)l * HQ * D;
-    float* kvn = a.kvn + (long)l * 2 * HK * D;
-    float* part = a.part + (long)l * pstride(a.nsplit);
-    bf16_t* hb = a.h + (long)l * F;
-    // ---------------------------------------------------------------- QKV
-    pstart(nbar);
-    {
-      const float bq = lane < NPQ ? bf2f(Ly.bqkv[w * NPQ + lane]) : 0.f;
-      float x[1][8];
-      ln_x(rin, Ly.ln1_g, Ly.ln1_b, x);
-      tmark(a, nbar, 1);
-      const float y = gemv(std::integral_constant<int, NPQ>{}, I1{}, x);
-      tmark(a, nbar, 2);
-      if (wv == 0) {
-        if (lane < NPQ) {
-          const int col = w * NPQ + lane;
-          const float v = bf2f(f2bf(y)) + bq;
-          if (col < HQ * D) {
-            __hip_atomic_store(qn + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          } else {
-            const int kv = col - HQ * D;
-            const int which = kv / (HK * D), r = kv % (HK * D), kh = r / D, d = r % D;
-            const bf16_t vb = f2bf(v);
-            bf16_t* cache = which ? Ly.vc : Ly.kc;
-            cache[((long)kh * a.maxS + pos) * D + d] = vb;
-            __hip_atomic_store(kvn + kv, bf2f(vb), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-        }
-        grid_sync(a, ++nbar, lane);
-      } else {
-        ++nbar;
-      }
-    }
-    // ---------------------------------------------------------------- attention
-    pstart(nbar);
-    if (w < HQ * a.nsplit) {
-      const int h = w / a.nsplit, s = w % a.nsplit, kh = h / (HQ / HK);
-      const int chunk = (L + a.nsplit - 1) / a.nsplit;
-      const int j0 = s * chunk, n = min(L, j0 + chunk) - j0;
-      const int sub = tid & 15, kslot = tid >> 4;
-      const long kvbase = (long)kh * a.maxS * D;
-      float q[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) q[i] = ldf(qn + h * D + sub * 8 + i) * a.scale_log2;
-      auto row = [&](const bf16_t* cache, int which, int j, float* r) {
-        if (j == pos) {
-          const float* p = kvn + which * HK * D + kh * D + sub * 8;
-#pragma unroll
-          for (int i = 0; i < 8; i += 2) {
-            const u64 u = ld64(p + i);
-            r[i] = __uint_as_float((unsigned)u);
-            r[i + 1] = __uint_as_float((unsigned)(u >> 32));
-          }
-        } else {
-          const u16x8 u = *reinterpret_cast<const u16x8*>(cache + kvbase + (long)j * D + sub * 8);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) r[i] = bf2f(u[i]);
-        }
-      };
-      for (int i = kslot; i < n; i += 16) {
-        float k[8];
-        row(Ly.kc, 0, j0 + i, k);
-        float d = 0.f;
-#pragma unroll
-        for (int t = 0; t < 8; ++t) d += q[t] * k[t];
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
-        if (sub == 0) sc[i] = d;
-      }
-      wbar();
-      const float sv = tid < n ? sc[tid] : -INFINITY;
-      const float m = bmax(sv);
-      const float p = tid < n ? exp2f(sv - m) : 0.f;
-      const float lsum = bsum(p);
-      if (tid < n) sc[tid] = p;
-      wbar();
-      float acc[8];
-#pragma unroll
-      for (int t = 0; t < 8; ++t) acc[t] = 0.f;
-      for (int i = kslot; i < n; i += 16) {
-        float v[8];
-        row(Ly.vc, 1, j0 + i, v);
-        const float pi = sc[i];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) acc[t] += pi * v[t];
-      }
-#pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        acc[t] += __shfl_xor(acc[t], 16, 64);
-        acc[t] += __shfl_xor(acc[t], 32, 64);
-      }
-      if (lane < 16) {
-#pragma unroll
-        for (int t = 0; t < 8; ++t) pv[wv][sub * 8 + t] = acc[t];
-      }
-      wbar();
-      if (wv == 0) {
-        float* dst = part + (long)(h * a.nsplit + s) * PSTRIDE;
-        const int d0 = lane * 2;
-        const float v0 = pv[0][d0] + pv[1][d0] + pv[2][d0] + pv[3][d0];
-        const float v1 = pv[0][d0 + 1] + pv[1][d0 + 1] + pv[2][d0 + 1] + pv[3][d0 + 1];
-        st64(dst + d0, pack2f(n > 0 ? v0 : 0.f, n > 0 ? v1 : 0.f));
-        if (lane == 0) st64(dst + D, pack2f(n > 0 ? m : -INFINITY, n > 0 ? lsum : 0.f));
-      }
-    }
-    if (wv == 0) grid_sync(a, ++nbar, lane); else ++nbar;
-    // ---------------------------------------------------------------- out projection
-    pstart(nbar);
-    {
-      const int ocol = w * NPO + (lane & (NPO - 1));
-      const float bo = bf2f(Ly.bo[ocol]), ro = bf2f(rin[ocol]);
-      float x[1][8];
-      {
-        const int h = tid >> 4, d0 = (tid & 15) * 8;
-        const float* base = part + (long)h * a.nsplit * PSTRIDE;
-        float M = -INFINITY, lt = 0.f, o[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] = 0.f;
-        for (int s0 = 0; s0 < a.nsplit; s0 += 8) {
-          u64 ml[8], ov[8][4];
-#pragma unroll
-          for (int t = 0; t < 8; ++t) {
-            const float* ps = base + min(s0 + t, a.nsplit - 1) * PSTRIDE;
-            ml[t] = ld64(ps + D);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) ov[t][i] = ld64(ps + d0 + 2 * i);
-          }
-#pragma unroll
-          for (int t = 0; t < 8; ++t) {
-            const float ms = __uint_as_float((unsigned)ml[t]);
-            if (s0 + t >= a.nsplit || ms == -INFINITY) continue;
-            const float nM = fmaxf(M, ms), c = exp2f(M - nM), e = exp2f(ms - nM);
-            lt = lt * c + e * __uint_as_float((unsigned)(ml[t] >> 32));
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              o[2 * i] = o[2 * i] * c + e * __uint_as_float((unsigned)ov[t][i]);
-              o[2 * i + 1] = o[2 * i + 1] * c + e * __uint_as_float((unsigned)(ov[t][i] >> 32));
-            }
-            M = nM;
-          }
-        }
-        const float inv = 1.f / lt;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) x[0][i] = bf2f(f2bf(o[i] * inv));
-      }
-      tmark(a, nbar, 1);
-      const float y = gemv(std::integral_constant<int, NPO>{}, I1{}, x);
-      tmark(a, nbar, 2);
-      if (wv == 0) {
-        publish_bf16(rmid + w * NPO, y + bo + ro, lane, NPO);
-        grid_sync(a, ++nbar, lane);
-      } else {
-        ++nbar;
-      }
-    }
-    // ---------------------------------------------------------------- FFN1
-    pstart(nbar);
-    {
-      const float b1 = bf2f(Ly.b1[w * NP1 + (lane & (NP1 - 1))]);
-      float x[1][8];
-      ln_x(rmid, Ly.ln2_g, Ly.ln2_b, x);
-      tmark(a, nbar, 1);
-      const float y = gemv(std::integral_constant<int, NP1>{}, I1{}, x);
-      tmark(a, nbar, 2);
-      if (wv == 0) {
-        const float t = y + b1;
-        publish_bf16(hb + w * NP1, a.act ? gelu_tanh(t) : gelu_erf(t), lane, NP1);
-        grid_sync(a, ++nbar, lane);
-      } else {
-        ++nbar;
-      }
-    }
-    // ---------------------------------------------------------------- FFN2
-    pstart(nbar);
-    {
-      const int fcol = w * NP2 + (lane & (NP2 - 1));
-      const float b2 = bf2f(Ly.b2[fcol]), rm = bf2f(rmid[fcol]);
-      float x[4][8];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) ld_bf8(hb + (j * 256 + tid) * 8, x[j]);
-      tmark(a, nbar, 1);
-      const float y = gemv(std::integral_constant<int, NP2>{}, std::integral_constant<int, 4>{}, x);
-      tmark(a, nbar, 2);
-      if (wv == 0) {
-        publish_bf16(rout + w * NP2, y + b2 + rm, lane, NP2);
-        if (l + 1 < a.nl) grid_sync(a, ++nbar, lane);
-      } else {
-        ++nbar;
-      }
-    }
-  }
-  // a timed-out intra-workgroup spin fails the launch like a grid-barrier timeout
-  if (tid == 0 && lds_get(3))
-    __hip_atomic_fetch_add(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (tid == 0 &&
-      __hip_atomic_fetch_add(a.bar + 18 * BAR_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == NWG - 1) {
-    for (int i = 0; i < 19; ++i)
-      __hip_atomic_exchange(a.bar + i * BAR_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// ------------------------------------------------------------------------------------------
 // Greedy tail of a batch-1 decode step, one launch: final LayerNorm → LM-head GEMV → argmax →
 // token bookkeeping → the next step's embedding. On the launch-per-op tail these are ~8 small
 // kernels per token (LN, head GEMM, argmax, pad masking, token-column store, position increment,
@@ -1622,22 +1214,17 @@ PIAMD_EXPORT int piamd_decode_mega_shape_supported(int E_, int D_, int hq, int h
   return piamd_decode_mega_batch_supported(E_, D_, hq, hk, F_, rot, w8, 1);
 }
 PIAMD_EXPORT int piamd_decode_mega_supported() { return piamd_decode_mega_shape_supported(E, D, HQ, HK, F, 0, 0); }
-PIAMD_EXPORT int piamd_decode_mega_lw_supported() {
-  return coop_ok((const void*)decode_mega_lw_kernel, LW_NT);
-}
 
 // Launch one decode step over `nl` layers of the shape (E_, D_, hq, hk, F_) with a.rot rotary
 // dims (0 or D_). `layers` is a device array of MegaLayer; scratch buffers per MegaArgs (part:
-// nl · pstride_hd(hq, D_, nsplit) floats). The dedicated-loader variant (a.loader = 1) exists for
-// the GPT-3 1.3B shape without rotary only. Returns hipError_t.
+// nl · pstride_hd(hq, D_, nsplit) floats); a.loader must be 0 (the round-4 dedicated-loader
+// variant was retired once the MFMA GEMV phases made this kernel faster). Returns hipError_t.
 PIAMD_EXPORT int piamd_decode_mega(const MegaArgs* args, int E_, int D_, int hq, int hk, int F_,
                                    hipStream_t st) {
   const MegaArgs& a = *args;
   const void* fn = mega_fn(E_, D_, hq, hk, F_, a.rot, a.w8, a.nb, a.mm);
-  const bool lw_shape =
-      E_ == E && D_ == D && hq == HQ && hk == HK && F_ == F && a.rot == 0 && !a.w8 && a.nb == 1 && !a.mm;
-  if (!fn || (a.rot != 0 && a.rot != D_) || a.nl < 1 || a.loader < 0 || a.loader > 1 ||
-      (a.loader && !lw_shape) || a.nsplit < 1 || a.nb * hq * a.nsplit > NWG ||
+  if (!fn || (a.rot != 0 && a.rot != D_) || a.nl < 1 || a.loader != 0 || a.nsplit < 1 ||
+      a.nb * hq * a.nsplit > NWG ||
       (a.maxS + a.nsplit - 1) / a.nsplit > 256 || !a.layers || !a.resid || !a.rbuf || !a.qn ||
       !a.kvn || !a.part || !a.h || !a.bar || !a.err || !a.pos)
     return (int)hipErrorInvalidValue;
@@ -1645,10 +1232,6 @@ PIAMD_EXPORT int piamd_decode_mega(const MegaArgs* args, int E_, int D_, int hq,
   // barriers rely on it) or refuses the launch; checked once against the kernel's occupancy
   MegaArgs arg = a;
   void* kargs[] = {&arg};
-  if (a.loader) {
-    if (!coop_ok((const void*)decode_mega_lw_kernel, LW_NT)) return (int)hipErrorCooperativeLaunchTooLarge;
-    return (int)hipLaunchCooperativeKernel((const void*)decode_mega_lw_kernel, dim3(NWG), dim3(LW_NT), kargs, 0, st);
-  }
   if (!coop_ok(fn, NT)) return (int)hipErrorCooperativeLaunchTooLarge;
   return (int)hipLaunchCooperativeKernel(fn, dim3(NWG), dim3(NT), kargs, 0, st);
 }

@@ -29,7 +29,7 @@ import torch
 
 from ..ops import _lib
 
-# the shape the dedicated-loader variant (decode_mega_lw_kernel) and the greedy tail
+# the shape the greedy tail
 # (decode_head_kernel) are built for; every shape of the plain kernel is listed at ``mega_fn`` in
 # decode_mega.hip and queried through piamd_decode_mega_shape_supported
 E, D, HQ, HK, F = 2048, 128, 16, 16, 8192
@@ -176,20 +176,15 @@ class MegaDecoder:
         # behind the FFN1 head, so the FFN1 → FFN2 hand-over DMA is served from it (kernel
         # 832 → 816 µs; at 4 rows every workgroup attends and the touch only moves the wait)
         self.late_dma = int(os.environ.get("PIAMD_MEGA_LATE_DMA", "5" if nb == 1 else "1"))
-        # 1: the variant with a dedicated loader wave and a 16 KiB chunk ring (decode_mega_lw_kernel,
-        # VALU GEMVs; round 4: kernel 946 vs 968 us against the VALU 4-wave kernel); 0 (default):
-        # the 4-wave templated kernel (decode_mega_kernel), whose MFMA GEMV phases now beat it
-        self.loader = int(os.environ.get("PIAMD_MEGA_LOADER", "0"))
-        # GEMV phases on MFMA (1, default for bf16: 16 weight columns × 32 k per instruction, no
-        # per-column butterfly; kernel 869 vs 976 µs on the VALU, profiles/decode_mega_r5.txt)
-        # or the VALU (0; the loader-wave variant; A/B variants for GPT-1.3B bf16 and int8)
-        self.mm = 0 if self.loader else int(os.environ.get("PIAMD_MEGA_MFMA", "1"))
+        # the round-4 dedicated-loader-wave variant is retired (the MFMA 4-wave kernel beat it:
+        # 834 vs 908 µs); the field stays 0
+        self.loader = 0
+        # GEMV phases on MFMA (1, default: 16 weight columns × 32 k per instruction, no per-column
+        # butterfly; kernel 869 vs 976 µs on the VALU, profiles/decode_mega_r5.txt) or the VALU
+        # (0; A/B instantiations for GPT-1.3B bf16 and int8)
+        self.mm = int(os.environ.get("PIAMD_MEGA_MFMA", "1"))
         if not self._variant_ok(self.mm):
             self.mm = 1 - self.mm
-        if self.loader and ((E_, D_, HQ_, HK_, F_, self.rot, self.w8, nb) != (E, D, HQ, HK, F, 0, 0, 1)
-                            or not self._lw_ok()):
-            self.loader = 0
-            self.mm = 1
         # greedy tail (decode_head_kernel): LM head + argmax + bookkeeping + next embedding
         self.head_ok = nb == 1 and _lib.has("piamd_decode_head_greedy") and self._head_tables(gen)
         self.best = torch.zeros(8 * 32, dtype=torch.int64, device=dev)
@@ -198,10 +193,6 @@ class MegaDecoder:
     def _variant_ok(self, mm: int) -> bool:
         return _lib.lib().piamd_decode_mega_variant_supported(
             self.E, self.D, self.HQ, self.HK, self.F, self.rot, self.w8, self.nb, mm) == 1
-
-    @staticmethod
-    def _lw_ok() -> bool:
-        return _lib.has("piamd_decode_mega_lw_supported") and _lib.lib().piamd_decode_mega_lw_supported() == 1
 
     def _head_tables(self, gen) -> bool:
         m = gen.model

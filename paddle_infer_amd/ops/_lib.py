@@ -116,7 +116,6 @@ class HeadArgs(ctypes.Structure):
 
 _SIGS["piamd_decode_head_greedy"] = [ctypes.POINTER(HeadArgs), c_int, c_void_p]
 _SIGS["piamd_decode_mega_supported"] = []
-_SIGS["piamd_decode_mega_lw_supported"] = []
 _SIGS["piamd_fa_fwd"] = [ctypes.POINTER(FaArgs), c_int, c_void_p]
 _SIGS["piamd_fa_bwd"] = [ctypes.POINTER(FaArgs), c_int, c_void_p]
 _SIGS["piamd_layernorm_bwd_ws"] = [c_int, c_int]

@@ -38,11 +38,10 @@ def _rel(a, b):
     return ((a - b).norm() / b.norm()).item()
 
 
-# dedicated loader wave (default) / 4-wave kernel / 4-wave kernel with MFMA GEMV phases
-@pytest.mark.parametrize("loader", ["1", "0", "mfma"])
+# GEMV phases on MFMA (default) / on the VALU (A/B instantiation)
+@pytest.mark.parametrize("loader", ["mfma", "valu"])
 @pytest.mark.parametrize("max_seq,prompt", [(256, 37), (1024, 300)])
 def test_mega_decode_matches_per_op_path(max_seq, prompt, loader, monkeypatch):
-    monkeypatch.setenv("PIAMD_MEGA_LOADER", "0" if loader == "mfma" else loader)
     monkeypatch.setenv("PIAMD_MEGA_MFMA", "1" if loader == "mfma" else "0")
     from paddle_infer_amd.inference import mega_decode
     from paddle_infer_amd.inference.generation import GPTGenerator
@@ -59,8 +58,7 @@ def test_mega_decode_matches_per_op_path(max_seq, prompt, loader, monkeypatch):
         tok = lb.argmax(-1)
         la, lb = g_mega.decode(tok, pos), g_ref.decode(tok, pos)
         assert isinstance(g_mega._mega[1], mega_decode.MegaDecoder)
-        assert g_mega._mega[1].loader == (0 if loader == "mfma" else int(loader))
-        assert g_mega._mega[1].mm == (loader == "mfma")
+        assert g_mega._mega[1].loader == 0 and g_mega._mega[1].mm == (loader == "mfma")
         assert _rel(la, lb) < 2e-2, (step, _rel(la, lb))
         for (ka, va), (kb, vb) in zip(g_mega.caches, g_ref.caches):
             p = int(pos[0])

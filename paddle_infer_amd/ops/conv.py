@@ -244,7 +244,11 @@ def conv2d_dgrad_strided(dy, weight, H, W, st, pad, dil, out_f32=False):
     scattered into dX (phases with no tap are zero)."""
     N, OH, OW, K = dy.shape
     Kw, C, R, S = weight.shape
-    dx = torch.empty(N, H, W, C, dtype=torch.float32 if out_f32 else dy.dtype, device=dy.device)
+    # phases no tap reaches stay zero: one fill of dX up front instead of a strided fill per phase
+    tapless = any(_phase_taps(R, st[0], pad[0], dil[0], ph) is None or _phase_taps(S, st[1], pad[1], dil[1], pw) is None
+                  for ph in range(st[0]) for pw in range(st[1]))
+    dx = (torch.zeros if tapless else torch.empty)(N, H, W, C, dtype=torch.float32 if out_f32 else dy.dtype,
+                                                  device=dy.device)
     wb = weight.to(dy.dtype)
     for ph in range(st[0]):
         for pw in range(st[1]):
@@ -253,7 +257,6 @@ def conv2d_dgrad_strided(dy, weight, H, W, st, pad, dil, out_f32=False):
                 continue
             th, tw = _phase_taps(R, st[0], pad[0], dil[0], ph), _phase_taps(S, st[1], pad[1], dil[1], pw)
             if th is None or tw is None:
-                dx[:, ph::st[0], pw::st[1], :] = 0
                 continue
             (rt, ph2, dh2), (stp, pw2, dw2) = th, tw
             # sub-filter [C][R'][S'][K]: W[k][c][rt[i]][stp[j]] (taps are arithmetic progressions:

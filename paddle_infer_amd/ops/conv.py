@@ -24,6 +24,7 @@ Routes (``conv2d_any``, called by ``nn.functional.conv2d`` for GPU tensors):
 """
 from __future__ import annotations
 
+import math
 import os
 import threading
 
@@ -238,6 +239,39 @@ def _take_ap(t, dim, idx):
     return out.flip(dim) if step < 0 else out
 
 
+_PHASE_IDX = {}
+
+
+def _phase_filters(wb, st, pad, dil):
+    """Every phase sub-filter of a strided conv's data gradient, {(ph, pw): [C][R'][S'][K]
+    contiguous view}, gathered from the [K][C][R][S] filter ``wb`` by ONE ``torch.take`` with a
+    cached device index (instead of slice + flip + copy per phase). None when the index is not
+    cached yet and a graph capture is running (its host-built index cannot be uploaded there)."""
+    K, C, R, S = wb.shape
+    key = (tuple(wb.shape), tuple(st), tuple(pad), tuple(dil), wb.device)
+    ent = _PHASE_IDX.get(key)
+    if ent is None:
+        if wb.is_cuda and torch.cuda.is_current_stream_capturing():
+            return None
+        parts, views, off = [], {}, 0
+        k, c = torch.arange(K), torch.arange(C)
+        for ph in range(st[0]):
+            for pw in range(st[1]):
+                th, tw = _phase_taps(R, st[0], pad[0], dil[0], ph), _phase_taps(S, st[1], pad[1], dil[1], pw)
+                if th is None or tw is None:
+                    continue
+                r, s_ = torch.tensor(th[0]), torch.tensor(tw[0])
+                flat = (((k[None, None, None, :] * C + c[:, None, None, None]) * R + r[None, :, None, None]) * S
+                        + s_[None, None, :, None])  # [C][R'][S'][K] → W[k][c][r][s]
+                parts.append(flat.reshape(-1))
+                views[(ph, pw)] = (off, (C, len(th[0]), len(tw[0]), K))
+                off += flat.numel()
+        ent = _PHASE_IDX[key] = (torch.cat(parts).to(wb.device), views)
+    idx, views = ent
+    buf = torch.take(wb, idx)
+    return {p: buf[o:o + math.prod(shape)].view(shape) for p, (o, shape) in views.items()}
+
+
 def conv2d_dgrad_strided(dy, weight, H, W, st, pad, dil, out_f32=False):
     """dX [N,H,W,C] (dtype of dy, or f32) of a strided conv: one stride-1 HIP convolution per output
     phase (ih mod st_h, iw mod st_w) over dY with the sub-filter of the taps that reach that phase,
@@ -250,6 +284,7 @@ def conv2d_dgrad_strided(dy, weight, H, W, st, pad, dil, out_f32=False):
     dx = (torch.zeros if tapless else torch.empty)(N, H, W, C, dtype=torch.float32 if out_f32 else dy.dtype,
                                                   device=dy.device)
     wb = weight.to(dy.dtype)
+    subs = _phase_filters(wb.contiguous(), st, pad, dil)
     for ph in range(st[0]):
         for pw in range(st[1]):
             Hp, Wp = -(-(H - ph) // st[0]), -(-(W - pw) // st[1])
@@ -259,9 +294,10 @@ def conv2d_dgrad_strided(dy, weight, H, W, st, pad, dil, out_f32=False):
             if th is None or tw is None:
                 continue
             (rt, ph2, dh2), (stp, pw2, dw2) = th, tw
-            # sub-filter [C][R'][S'][K]: W[k][c][rt[i]][stp[j]] (taps are arithmetic progressions:
-            # strided slices + flips, no index tensor — capturable in a hipGraph)
-            wsub = _take_ap(_take_ap(wb, 2, rt), 3, stp).permute(1, 2, 3, 0).contiguous()
+            # sub-filter [C][R'][S'][K]: W[k][c][rt[i]][stp[j]] — from the one-gather buffer, or
+            # (uncached index inside a capture) strided slices + flips of the filter
+            wsub = (subs[(ph, pw)] if subs is not None
+                    else _take_ap(_take_ap(wb, 2, rt), 3, stp).permute(1, 2, 3, 0).contiguous())
             # the phase convolution writes its outputs straight into dX's phase pixels
             _launch_geom(dy, wsub, (1, 1), (ph2, pw2), (dh2, dw2), Hp, Wp, out_f32,
                          out=dx, phase=(st[0], st[1], ph, pw))

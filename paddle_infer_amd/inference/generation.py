@@ -123,7 +123,8 @@ class GPTGenerator:
         if not self.use_mega or B not in mega_decode.BATCHES or not mega_decode.enabled():
             return None
         if B not in self._mega:  # the shape / dtype gate is static: evaluated once per batch size
-            self._mega[B] = mega_decode.MegaDecoder(self, B) if mega_decode.eligible(self, B) else False
+            other = next((m for m in self._mega.values() if m), None)  # shares its weight copies
+            self._mega[B] = mega_decode.MegaDecoder(self, B, other) if mega_decode.eligible(self, B) else False
         return self._mega[B] or None
 
     def _decode_eager(self, tok, pos, B):

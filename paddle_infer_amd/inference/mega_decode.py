@@ -123,22 +123,27 @@ class MegaDecoder:
     """Owns the [out, in] weight copies, the per-layer pointer table and the scratch buffers of
     the ``nb``-row step."""
 
-    def __init__(self, gen, nb: int = 1):
+    def __init__(self, gen, nb: int = 1, shared: "MegaDecoder | None" = None):
+        """``shared``: a decoder of the same generator at another row count — its [out, in] weight
+        copies and pointer table are reused (they do not depend on the rows; one copy per model)."""
         dev = gen.device
         self.gen = gen
-        self._keep = []
-        rows = []
         self.w8 = _w8(gen) or 0
-        for spec, (kc, vc) in zip(gen.layers, gen.caches):
-            ws = [_out_in(spec[k]) for k in ("qkv", "out", "ffn1", "ffn2")]
-            ts = [spec["ln_scale"], spec["ln_bias"], ws[0][0], spec["qkv_bias"], ws[1][0], spec["out_bias"],
-                  spec["ffn_ln_scale"], spec["ffn_ln_bias"], ws[2][0], spec["ffn1_bias"], ws[3][0],
-                  spec["ffn2_bias"], kc, vc] + [w[1] for w in ws]
-            ts = [t.contiguous() if t is not None else None for t in ts]
-            self._keep += [t for t in ts if t is not None]
-            rows.append([t.data_ptr() if t is not None else 0 for t in ts])
-        self.table = torch.tensor(rows, dtype=torch.int64, device=dev)
-        self.nl = len(rows)
+        if shared is not None and shared.gen is gen:
+            self._keep, self.table, self.nl = shared._keep, shared.table, shared.nl
+        else:
+            self._keep = []
+            rows = []
+            for spec, (kc, vc) in zip(gen.layers, gen.caches):
+                ws = [_out_in(spec[k]) for k in ("qkv", "out", "ffn1", "ffn2")]
+                ts = [spec["ln_scale"], spec["ln_bias"], ws[0][0], spec["qkv_bias"], ws[1][0], spec["out_bias"],
+                      spec["ffn_ln_scale"], spec["ffn_ln_bias"], ws[2][0], spec["ffn1_bias"], ws[3][0],
+                      spec["ffn2_bias"], kc, vc] + [w[1] for w in ws]
+                ts = [t.contiguous() if t is not None else None for t in ts]
+                self._keep += [t for t in ts if t is not None]
+                rows.append([t.data_ptr() if t is not None else 0 for t in ts])
+            self.table = torch.tensor(rows, dtype=torch.int64, device=dev)
+            self.nl = len(rows)
         self.maxS = gen.max_seq_len
         self.E, self.D, self.HQ, self.HK, self.F, self.rot = shape_of(gen)
         E_, D_, HQ_, HK_, F_ = self.E, self.D, self.HQ, self.HK, self.F

@@ -255,4 +255,5 @@ def test_mega_decode_batched_generate_and_beams():
     assert torch.equal(out_a[:, :4].cpu(), out_r[:, :4].cpu()), (out_a, out_r)
     b = a.generate(ids[:1], max_new_tokens=6, num_beams=4)
     assert a._mega.get(4) and b.shape == (1, 6)
+    assert a._mega[4].table is a._mega[2].table  # one set of weight copies per model
     a._mega[4].check()

@@ -43,3 +43,35 @@ def test_headargs_mirror_matches_kernel_struct():
              for part in stmt.split(",")]
     assert names == [f[0] for f in _lib.HeadArgs._fields_], names
     assert ctypes.sizeof(_lib.HeadArgs) == 136
+
+
+def test_out_in_weight_codes_roundtrip():
+    """The decode kernel's [out, in] weight images: int8 codes and int4 codes packed two per byte
+    (k ascending from the low nibble) times the per-channel scales reproduce the weight-only
+    dequantisation exactly; bf16 weights come out transposed to [out, in]."""
+    from paddle_infer_amd.incubate.nn.functional import _lin
+    from paddle_infer_amd.inference.mega_decode import _out_in
+    from paddle_infer_amd.ops.inference import weight_dequantize, weight_quantize
+    torch.manual_seed(0)
+    w = torch.randn(64, 96)  # [K (in), N (out)] as the generator stores it
+    for algo, bits in (("weight_only_int8", 8), ("weight_only_int4", 4)):
+        q, s = weight_quantize(w, algo)
+        codes, scale = _out_in(_lin(q, s, bits))
+        if bits == 4:
+            u = codes.to(torch.int16)
+            lo, hi = u & 0xF, (u >> 4) & 0xF
+            codes = torch.stack([lo, hi], -1).reshape(codes.shape[0], -1)
+            codes = torch.where(codes >= 8, codes - 16, codes)
+        deq = weight_dequantize(q, s, algo, "float32").t()  # [out, in]
+        assert codes.shape == deq.shape
+        assert torch.equal(codes.float() * scale[:, None], deq.float()), algo
+    wb = w.to(torch.bfloat16)
+    t, none = _out_in(_lin(wb))
+    assert none is None and torch.equal(t, wb.t().contiguous())
+
+
+def test_batched_split_budget():
+    """One attention workgroup per (row, head, split) ≤ 256: the split budget per row count."""
+    from paddle_infer_amd.inference import mega_decode
+    assert mega_decode.BATCHES == (1, 2, 4)
+    assert [mega_decode.max_splits(b, 16) for b in (1, 2, 4)] == [16, 8, 4]

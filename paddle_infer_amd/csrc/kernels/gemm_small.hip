@@ -22,6 +22,12 @@
 //     a k64 step loads k = 16g … 16g+15 of its row; MFMA sub-step s uses elements 8s … 8s+7 of it
 //     (a permutation of the k sum, identical for A and B).
 //   * rows ≥ M / columns ≥ N read a clamped (valid) row and are never stored.
+//   * LayerNorm fold (LN, bf16, KS = 1): C = act(LN(A)·Bᵀ + bias) with the host-side fold
+//     B' = B∘γ, c1[n] = Σ_k B'[n][k], b2[n] = bias[n] + Σ_k β[k]·B[n][k], so that
+//     LN(a)·B = rstd·(a·B'ᵀ − mean·c1) + b2. The kernel runs on the RAW rows: every lane adds up
+//     Σa and Σa² of the A fragments it already loads, the four lane groups and the K-splitting
+//     waves combine them, and the epilogue applies rstd·(acc − mean·c1[n]) + b2[n]. No separate
+//     LayerNorm launch (serving-batch decode: reference fused_multi_transformer pre-LN).
 // Contract: K % 64 == 0, N % 4 == 0, lda / ldb % 8 == 0, 16-B aligned operands.
 #include "common.h"
 
@@ -62,14 +68,20 @@ struct SgArgs {
   long long ldr;
   float alpha;
   int M, N, K, c_f32, act;
+  const float* ln_c1;  // LN fold: [N] column sums of B' (null: no LayerNorm)
+  const float* ln_b2;  // LN fold: [N] bias + B·β
+  float ln_eps;
 };
 
 // Epilogue value of (m, n..n+3) → C.
-template <bool F16>
-__device__ __forceinline__ void sg_store(const SgArgs& p, int m, int n, f32x4 v) {
+template <bool F16, bool LN = false>
+__device__ __forceinline__ void sg_store(const SgArgs& p, int m, int n, f32x4 v, float mu = 0.f,
+                                         float rs = 1.f) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    float x = v[j] * p.alpha + (p.bias ? h2f<F16>(p.bias[n + j]) : 0.f);
+    float x;
+    if constexpr (LN) x = rs * (v[j] - mu * p.ln_c1[n + j]) + p.ln_b2[n + j];
+    else x = v[j] * p.alpha + (p.bias ? h2f<F16>(p.bias[n + j]) : 0.f);
     x = sg_act(x, p.act);
     if (p.resid) x += h2f<F16>(p.resid[(long long)m * p.ldr + n + j]);
     v[j] = x;
@@ -84,10 +96,11 @@ __device__ __forceinline__ void sg_store(const SgArgs& p, int m, int n, f32x4 v)
   }
 }
 
-template <bool F16, int MB, int NB, int WN, int D>
+template <bool F16, int MB, int NB, int WN, int D, bool LN = false>
 __global__ __launch_bounds__(256) void small_gemm_kernel(SgArgs p, int* __restrict__ cnt) {
   constexpr int WK = 4 / WN;
   __shared__ f32x4 red[WK > 1 ? 4 : 1][MB * NB][64];
+  __shared__ float2 lst[LN && WK > 1 ? 4 : 1][MB][16];  // LN: per-wave row (Σa, Σa²)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r16 = lane & 15;
   const int wn = w % WN, wk = w / WN;
   const int n0 = blockIdx.x * (16 * NB * WN) + wn * (16 * NB), m0 = blockIdx.y * (16 * MB);
@@ -109,6 +122,14 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(SgArgs p, int* __restri
   for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // LN: Σa of row r16 of block mb (every column of the ones·Aᵀ block) and the A·Aᵀ block whose
+  // diagonal holds Σa² (row r16's at lane r16 + 16·(r16 >> 2), element r16 & 3)
+  f32x4 accS[LN ? MB : 1], accQ[LN ? MB : 1];
+#pragma unroll
+  for (int mb = 0; mb < (LN ? MB : 1); ++mb) accS[mb] = accQ[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  u16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = 0x3F80;  // bf16 1.0 (LN mode is bf16-only)
 
   // D-deep register ring of operand fragments: step i computes on slot i % D, then refills it
   // with step i + D, so D k64 steps of loads are in flight per wave
@@ -144,7 +165,28 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(SgArgs p, int* __restri
 #pragma unroll
           for (int nb = 0; nb < NB; ++nb)
             acc[mb][nb] = mma16<F16>(br[d][nb][s], ar[d][mb][s], acc[mb][nb]);
+      if constexpr (LN) {  // row statistics on the matrix cores: ones·Aᵀ and A·Aᵀ blocks
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int mb = 0; mb < MB; ++mb) {
+            accS[mb] = mma16<F16>(ones, ar[d][mb][s], accS[mb]);
+            accQ[mb] = mma16<F16>(ar[d][mb][s], ar[d][mb][s], accQ[mb]);
+          }
+      }
       if (k + D * WK < kb_end) load(k + D * WK, ar[d], br[d]);
+    }
+  }
+  float s1[MB], s2[MB];  // LN: Σa / Σa² of row r16 of block mb over this wave's K range
+  if constexpr (LN) {
+    const int j = r16 & 3;
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const f32x4 q = accQ[mb];
+      const float dq = j == 0 ? q[0] : j == 1 ? q[1] : j == 2 ? q[2] : q[3];
+      s1[mb] = accS[mb][0];
+      s2[mb] = __shfl(dq, r16 + 16 * (r16 >> 2));
+      if (WK > 1 && g == 0) lst[WK > 1 ? w : 0][mb][r16] = make_float2(s1[mb], s2[mb]);
     }
   }
   if constexpr (WK > 1) {
@@ -155,6 +197,24 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(SgArgs p, int* __restri
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) red[w][mb * NB + nb][lane] = acc[mb][nb];
     __syncthreads();
+  }
+  float mu[MB], rs[MB];
+  if constexpr (LN) {
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      float a = s1[mb], b = s2[mb];
+      if constexpr (WK > 1) {
+        a = b = 0.f;
+#pragma unroll
+        for (int j = 0; j < WK; ++j) {
+          const float2 t = lst[wn + j * WN][mb][r16];
+          a += t.x;
+          b += t.y;
+        }
+      }
+      mu[mb] = a / p.K;
+      rs[mb] = rsqrtf(fmaxf(b / p.K - mu[mb] * mu[mb], 0.f) + p.ln_eps);
+    }
   }
   // D = B·Aᵀ block: lane holds rows m = r16 of the A block, columns n = 4g + j of the B block
   float sink = 0.f;
@@ -172,7 +232,8 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(SgArgs p, int* __restri
     }
     if (m >= p.M || n >= p.N) continue;
     if (KS == 1) {
-      sg_store<F16>(p, m, n, v);
+      if constexpr (LN) sg_store<F16, true>(p, m, n, v, mu[mb], rs[mb]);
+      else sg_store<F16>(p, m, n, v);
     } else if (cnt == nullptr) {
       *reinterpret_cast<f32x4*>(p.ws + ((long long)kz * p.M + m) * p.N + n) = v;
     } else {
@@ -224,6 +285,15 @@ __global__ __launch_bounds__(256) void small_gemm_finish(SgArgs p, int KS) {
 template <bool F16, int MB, int NB, int WN>
 void sg_launch(const SgArgs& p, int ks, int depth, int* cnt, hipStream_t st) {
   dim3 grid((p.N + 16 * NB * WN - 1) / (16 * NB * WN), (p.M + 16 * MB - 1) / (16 * MB), ks);
+  if constexpr (!F16) {
+    if (p.ln_c1) {  // LayerNorm fold (bf16, ks == 1 checked by the caller)
+      if (depth >= 2)
+        hipLaunchKernelGGL((small_gemm_kernel<F16, MB, NB, WN, 2, true>), grid, dim3(256), 0, st, p, cnt);
+      else
+        hipLaunchKernelGGL((small_gemm_kernel<F16, MB, NB, WN, 1, true>), grid, dim3(256), 0, st, p, cnt);
+      return;
+    }
+  }
   if (depth >= 2)
     hipLaunchKernelGGL((small_gemm_kernel<F16, MB, NB, WN, 2>), grid, dim3(256), 0, st, p, cnt);
   else
@@ -257,17 +327,22 @@ int sg_dispatch(const SgArgs& p, int mb, int nb, int wn, int ks, int depth, int*
 // depth ∈ {1,2} k64 steps of loads in flight per wave, ks ≥ 1 K slices. ks > 1: cnt != null → fixup mode (ws = M·N f32 and cnt = tiles ints, both
 // zeroed, left zeroed); cnt == null → slice mode (ws = ks·M·N f32 + a finish launch).
 // bias / resid: 16-bit, nullable. act: 0 none, 1 gelu_tanh, 2 gelu_erf, 3 relu, 4 silu.
-PIAMD_EXPORT int piamd_small_gemm(int f16, const void* a, long long lda, const void* b, long long ldb,
-                                  void* c, long long ldc, int c_f32, int M, int N, int K, int mb,
-                                  int nb, int wn, int depth, int ks, float alpha, const void* bias,
-                                  int act,
-                                  const void* resid, long long ldr, float* ws, int* cnt,
-                                  hipStream_t st) {
+// ln_c1 / ln_b2 (f32 [N], both or neither): LayerNorm fold — C = act(LN(A)·Bᵀ + bias) with B the
+// folded weight B∘γ, c1 its row sums and b2 = bias + B·β (the bias argument is then ignored);
+// bf16 only, ks == 1, alpha == 1.
+PIAMD_EXPORT int piamd_small_gemm_ln(int f16, const void* a, long long lda, const void* b,
+                                     long long ldb, void* c, long long ldc, int c_f32, int M, int N,
+                                     int K, int mb, int nb, int wn, int depth, int ks, float alpha,
+                                     const void* bias, int act, const void* resid, long long ldr,
+                                     float* ws, int* cnt, const float* ln_c1, const float* ln_b2,
+                                     float ln_eps, hipStream_t st) {
   if (M <= 0 || N <= 0 || K <= 0 || K % 64 || N % 4 || lda % 8 || ldb % 8 || ldc % 4 || ks < 1 ||
       ks > K / 64 || (ks > 1 && !ws) || ((uintptr_t)a | (uintptr_t)b | (uintptr_t)c) % 16)
     return (int)hipErrorInvalidValue;
+  if ((ln_c1 != nullptr) != (ln_b2 != nullptr) || (ln_c1 && (f16 || ks != 1 || alpha != 1.f)))
+    return (int)hipErrorInvalidValue;
   SgArgs p{(const bf16_t*)a, lda, (const bf16_t*)b, ldb, c, ldc, ws, (const bf16_t*)bias,
-           (const bf16_t*)resid, ldr, alpha, M, N, K, c_f32, act};
+           (const bf16_t*)resid, ldr, alpha, M, N, K, c_f32, act, ln_c1, ln_b2, ln_eps};
   int* kc = ks > 1 ? cnt : nullptr;
   const int rc = f16 ? sg_dispatch<true>(p, mb, nb, wn, ks, depth, kc, st)
                      : sg_dispatch<false>(p, mb, nb, wn, ks, depth, kc, st);
@@ -278,4 +353,13 @@ PIAMD_EXPORT int piamd_small_gemm(int f16, const void* a, long long lda, const v
     else hipLaunchKernelGGL(small_gemm_finish<false>, dim3(grid), dim3(256), 0, st, p, ks);
   }
   return (int)hipGetLastError();
+}
+
+PIAMD_EXPORT int piamd_small_gemm(int f16, const void* a, long long lda, const void* b, long long ldb,
+                                  void* c, long long ldc, int c_f32, int M, int N, int K, int mb,
+                                  int nb, int wn, int depth, int ks, float alpha, const void* bias,
+                                  int act, const void* resid, long long ldr, float* ws, int* cnt,
+                                  hipStream_t st) {
+  return piamd_small_gemm_ln(f16, a, lda, b, ldb, c, ldc, c_f32, M, N, K, mb, nb, wn, depth, ks,
+                             alpha, bias, act, resid, ldr, ws, cnt, nullptr, nullptr, 0.f, st);
 }

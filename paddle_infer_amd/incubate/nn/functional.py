@@ -235,7 +235,7 @@ class _Linear:
     """A projection: bf16 weight ([in, out] Paddle layout, or [out, in] when ``trans``) or a
     weight-only packed weight + scale. ``packed``: an optional MFMA-tile packed bf16 copy used for
     small-M (decode) calls, where the GEMM is a weight stream (see ops.inference.pack_bf16)."""
-    __slots__ = ("w", "scale", "bits", "trans", "packed", "act_scale")
+    __slots__ = ("w", "scale", "bits", "trans", "packed", "act_scale", "lnf")
     PACKED_MAX_M = 64
     # serving batches with short K: the skinny MFMA GEMM on the K-contiguous weight beats the packed
     # weight stream from 8 rows (M=32 QKV 14.7 -> 11.5 us, out-proj 8.8 -> 6.5; K = 8192 stays on
@@ -259,6 +259,50 @@ class _Linear:
     def __init__(self, w, scale=None, bits=0, trans=False, packed=None, act_scale=None):
         self.w, self.scale, self.bits, self.trans, self.packed = w, scale, bits, trans, packed
         self.act_scale = act_scale  # bits == -8: int8 activations (None → dynamic per token)
+        self.lnf = {}  # LayerNorm folds of the K-contiguous weight, keyed by (γ, β, bias)
+
+    def _kn(self):
+        """(K, N) of the projection."""
+        return (self.w.shape[1], self.w.shape[0]) if self.trans else tuple(self.w.shape)
+
+    def ln_fold_ok(self, M, act="none"):
+        """A pre-LN call with M rows runs as ONE skinny GEMM on the LayerNorm-folded weight
+        (``ops.gemm.ln_fold``: row statistics gathered from the raw rows inside the GEMM, no
+        LayerNorm launch) — serving batches (M ≥ DENSE_MIN_M) on the dense path, bf16."""
+        from ...ops.gemm import use_small
+        K, N = self._kn()
+        return (not self.bits and self.packed is not None and self.w.dtype == torch.bfloat16
+                and M >= self.DENSE_MIN_M and not self._packed_for(M, K) and K % 64 == 0
+                and N % 4 == 0 and use_small(M, N, K) and act in ("none", "gelu", "gelu_tanh", "relu"))
+
+    def fused_rows(self, M, ln, act="none"):
+        """True when a call with M rows takes its pre-LN (``ln``) or residual add in the kernel
+        that computes it: the weight-stream GEMV at few rows, the LN-folded / residual-epilogue
+        skinny GEMM at serving batches."""
+        if self.fused_gemv(M):
+            return True
+        if self.bits or self.packed is None or M < self.DENSE_MIN_M:
+            return False
+        return self.ln_fold_ok(M, act) if ln else True
+
+    def _dense_ln(self, x, ln, bias, act, resid):
+        from ...ops.gemm import ln_fold, small_gemm
+        from ...ops.linear import transposed
+        g, b, eps = ln
+        key = (g.data_ptr(), b.data_ptr(), bias.data_ptr() if bias is not None else 0)
+        f = self.lnf.get(key)
+        if f is None and torch.cuda.is_current_stream_capturing():
+            # a fold built inside a capture would only be computed at replay: explicit LN instead
+            return self._dense_epilogue(ops.layer_norm(x, g, b, eps), bias, act, resid)
+        if f is None:
+            wk = self.w if self.trans else transposed(self.w)
+            f = self.lnf[key] = ln_fold(wk, g, b, bias)
+        x2 = x.reshape(-1, x.shape[-1])
+        if x2.stride(-1) != 1 or x2.stride(0) != x2.shape[1]:
+            x2 = x2.contiguous()
+        r2 = resid.reshape(x2.shape[0], -1) if resid is not None else None
+        y = small_gemm(x2, f[0], act=act, resid=r2, ln=(f[1], f[2], eps))
+        return y.reshape(*x.shape[:-1], y.shape[-1])
 
     def prepack(self):
         if not self.bits and self.packed is None:
@@ -283,6 +327,9 @@ class _Linear:
                                                resid=resid)
             if x.is_cuda and self._packed_for(M, x.shape[-1]):
                 return _inf.packed_linear(x, self.packed, bias, act, ln=ln, resid=resid)
+            if (ln is not None and x.is_cuda and x.dtype == torch.bfloat16 and LN_FOLD
+                    and self.ln_fold_ok(M, act)):
+                return self._dense_ln(x, ln, bias, act, resid)
             if ln is not None:
                 x = ops.layer_norm(x, ln[0], ln[1], ln[2])
             if (x.is_cuda and self.packed is not None and x.dtype == self.w.dtype
@@ -313,6 +360,9 @@ class _Linear:
 # Measured (GPT-1.3B decode, profiles/decode_fused_ln_sweep_r1.txt): fusing wins at batch 1-2
 # (+4-12 % tok/s) and loses from batch 4 (the LN prologue forces KS=1 and grows with M).
 FUSED_LN_MAX_M = int(os.environ.get("PIAMD_FUSED_LN_MAX_M", "2"))
+# serving batches (M ≥ 8 rows, E ≤ 2048): each pre-LN folded into the skinny GEMM that consumes it
+# (ops.gemm.ln_fold) and each residual add in the producing GEMM's epilogue — no LayerNorm launches
+LN_FOLD = os.environ.get("PIAMD_LN_FOLD", "1") != "0"
 
 
 def _lin(w, scale=None, bits=0, trans=False, act_scale=None):
@@ -411,12 +461,15 @@ def multi_transformer_forward(x, layers, num_heads, num_kv_heads=None, pre_layer
             and all(L.get("moe") is None
                     and all(L.get(k) is not None and L[k].dtype == torch.bfloat16
                             for k in ("ln_scale", "ln_bias", "ffn_ln_scale", "ffn_ln_bias"))
-                    and all(isinstance(L[k], _Linear) and L[k].fused_gemv(T)
+                    and all(isinstance(L[k], _Linear)
+                            and (L[k].fused_gemv(T)
+                                 or (LN_FOLD and L[k].fused_rows(T, k in ("qkv", "ffn1"),
+                                                                 act if k == "ffn1" else "none")))
                             for k in ("qkv", "out", "ffn1", "ffn2")) for L in layers)):
-        # decode: every projection is a weight-stream GEMV, so each pre-LN runs in the prologue of
-        # the GEMV that consumes it and each residual add in the epilogue of the projection that
-        # produces it — per layer QKV GEMV → attention → out GEMV → FFN1 GEMV → FFN2 GEMV, with no
-        # LayerNorm launches (2 fewer kernels per layer on a launch-latency-bound step)
+        # decode: each pre-LN runs inside the projection that consumes it (GEMV prologue at few
+        # rows, LayerNorm-folded skinny GEMM at serving batches) and each residual add in the
+        # epilogue of the projection that produces it — per layer QKV → attention → out → FFN1 →
+        # FFN2, with no LayerNorm launches (2 fewer kernels per layer on a launch-bound step)
         residual = xf
         for li, L in enumerate(layers):
             qkv = L["qkv"](residual, ln=(L["ln_scale"], L["ln_bias"], epsilon))

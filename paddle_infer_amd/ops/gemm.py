@@ -210,16 +210,21 @@ def _sg_fixup_bufs(device, M, N, tiles):
 
 
 def small_gemm(a, b, out=None, out_f32=False, alpha=1.0, bias=None, act="none", resid=None, cfg=None,
-               slices=False):
+               slices=False, ln=None):
     """C[M, N] = act(alpha·a[M, K]·b[N, K]ᵀ + bias) (+ resid) on the skinny MFMA kernel (both
     operands K-contiguous bf16 / fp16, K % 64 == 0, N % 4 == 0). Split-K runs in fixup mode (one
-    launch; ``slices=True``: deterministic slices + a finish launch)."""
+    launch; ``slices=True``: deterministic slices + a finish launch). ``ln = (c1, b2, eps)``: the
+    LayerNorm fold (see :func:`ln_fold`) — ``b`` is the folded weight, C = act(LN(a)·Wᵀ + bias)
+    from the raw rows of ``a`` (bf16, no K split; ``bias`` is inside b2)."""
     M, K = a.shape
     N = b.shape[0]
     half = a.dtype
     if out is None:
         out = torch.empty((M, N), dtype=torch.float32 if out_f32 else half, device=a.device)
     mb, nb, wn, depth, ks = cfg or small_cfg(M, N, K)
+    if ln is not None:
+        ks = 1
+        return _small_gemm_ln(a, b, out, M, N, K, (mb, nb, wn, depth), act, resid, ln)
     ws = cnt = None
     if ks > 1:
         if slices:
@@ -232,6 +237,31 @@ def small_gemm(a, b, out=None, out_f32=False, alpha=1.0, bias=None, act="none", 
               int(out.dtype == torch.float32), M, N, K, mb, nb, wn, depth, ks, float(alpha), _lib.ptr(bias),
               ACTS[act], _lib.ptr(resid), resid.stride(0) if resid is not None else 0,
               _lib.ptr(ws), _lib.ptr(cnt), _lib.stream())
+    return out
+
+
+def ln_fold(w_nk, gamma, beta, bias=None):
+    """LayerNorm fold of a K-contiguous weight w [N, K] for :func:`small_gemm` ``ln=``:
+    (w∘γ as bf16 [N, K], c1 = Σ_k (w∘γ)[n, k] of the ROUNDED fold (f32 [N]), b2 = bias + w·β (f32
+    [N])), so that LN(a)·wᵀ + bias = rstd·(a·(w∘γ)ᵀ − mean·c1) + b2."""
+    wf = (w_nk.float() * gamma.float().view(1, -1)).to(w_nk.dtype).contiguous()
+    c1 = wf.float().sum(1).contiguous()
+    b2 = w_nk.float() @ beta.float()
+    if bias is not None:
+        b2 = b2 + bias.float().view(-1)
+    return wf, c1, b2.contiguous()
+
+
+def _small_gemm_ln(a, b, out, M, N, K, cfg, act, resid, ln):
+    c1, b2, eps = ln
+    assert a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16, "LayerNorm fold: bf16 operands"
+    assert c1.dtype == torch.float32 and b2.dtype == torch.float32 and c1.numel() == N == b2.numel()
+    mb, nb, wn, depth = cfg
+    _lib.call("piamd_small_gemm_ln", 0, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
+              out.data_ptr(), out.stride(0), int(out.dtype == torch.float32), M, N, K, mb, nb, wn,
+              depth, 1, 1.0, None, ACTS[act], _lib.ptr(resid),
+              resid.stride(0) if resid is not None else 0, None, None, c1.data_ptr(), b2.data_ptr(),
+              float(eps), _lib.stream())
     return out
 
 

@@ -87,7 +87,12 @@ def qkv_prep(qkv, bias, k_cache, v_cache, pos0, B, S, Hq, Hk, D, rot_dim=0, neox
 _PART_CACHE = {}
 
 
+DECODE_CHUNK = int(os.environ.get("PIAMD_DECODE_CHUNK", "0"))  # A/B knob: fixed keys per split
+
+
 def decode_chunking(max_len, chunk=None):
+    if chunk is None and DECODE_CHUNK:
+        chunk = DECODE_CHUNK
     if chunk is None:
         # short caches: 64-key splits (one K pass + one V pass per workgroup, 4x the workgroups of
         # a 256-key split at batch 1); long caches keep the per-split partial count bounded

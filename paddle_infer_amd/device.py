@@ -166,9 +166,14 @@ class _NativeStream:
             return
         dev = _parse(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        self.priority = int(priority)
+        if not rt.available():  # native runtime not built: a torch pool stream of that priority
+            self._t = torch.cuda.Stream(device=torch.device("cuda", idx),
+                                        priority=-1 if self.priority == 1 else 0)
+            self._h, self._own, self.device = self._t.cuda_stream, False, torch.device("cuda", idx)
+            return
         self._h, self._own, self.device = _pool_stream(idx, int(priority)), False, torch.device("cuda", idx)
         self._t = torch.cuda.ExternalStream(self._h, device=self.device)
-        self.priority = int(priority)
 
     @property
     def cuda_stream(self) -> int:
@@ -180,10 +185,14 @@ class _NativeStream:
 
     def synchronize(self):
         from .framework import device_rt as rt
+        if not rt.available():
+            return self._t.synchronize()
         rt.check(rt.lib().piamd_stream_sync(self._h), "hipStreamSynchronize")
 
     def query(self) -> bool:
         from .framework import device_rt as rt
+        if not rt.available():
+            return self._t.query()
         r = rt.lib().piamd_stream_query(self._h)
         if r < 0:
             raise RuntimeError(f"hipStreamQuery failed with hipError {-r}")
@@ -191,6 +200,8 @@ class _NativeStream:
 
     def wait_event(self, event):
         from .framework import device_rt as rt
+        if event._tev is not None:
+            return self._t.wait_event(event._tev)
         rt.check(rt.lib().piamd_stream_wait_event(self._h, event.handle), "hipStreamWaitEvent")
 
     def wait_stream(self, stream):
@@ -241,6 +252,12 @@ class _NativeEvent:
 
     def __init__(self, enable_timing=False, blocking=False, interprocess=False):
         from .framework import device_rt as rt
+        self._tev = None
+        if not rt.available():  # native runtime not built: torch's event
+            self._tev = torch.cuda.Event(enable_timing=enable_timing, blocking=blocking,
+                                         interprocess=interprocess)
+            self.handle, self.enable_timing = None, bool(enable_timing)
+            return
         h = ctypes.c_void_p()
         rt.check(rt.lib().piamd_event_create(int(bool(enable_timing)), int(bool(blocking)),
                                              ctypes.byref(h)), "hipEventCreate")
@@ -248,11 +265,16 @@ class _NativeEvent:
 
     def record(self, stream=None):
         from .framework import device_rt as rt
+        if self._tev is not None:
+            ts = stream.torch_stream if isinstance(stream, _NativeStream) else stream
+            return self._tev.record(ts) if ts is not None else self._tev.record()
         h = (stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream)
         rt.check(rt.lib().piamd_event_record(self.handle, h), "hipEventRecord")
 
     def query(self) -> bool:
         from .framework import device_rt as rt
+        if self._tev is not None:
+            return self._tev.query()
         r = rt.lib().piamd_event_query(self.handle)
         if r < 0:
             raise RuntimeError(f"hipEventQuery failed with hipError {-r}")
@@ -260,10 +282,14 @@ class _NativeEvent:
 
     def synchronize(self):
         from .framework import device_rt as rt
+        if self._tev is not None:
+            return self._tev.synchronize()
         rt.check(rt.lib().piamd_event_sync(self.handle), "hipEventSynchronize")
 
     def elapsed_time(self, end) -> float:
         from .framework import device_rt as rt
+        if self._tev is not None:
+            return self._tev.elapsed_time(end._tev)
         ms = ctypes.c_float()
         rt.check(rt.lib().piamd_event_elapsed(self.handle, end.handle, ctypes.byref(ms)),
                  "hipEventElapsedTime")
@@ -340,6 +366,8 @@ class cuda:  # namespace paddle.device.cuda
         if torch.cuda.is_available():
             from .framework import device_rt as rt
             idx = _parse(device).index if device is not None else None
+            if not rt.available():
+                return torch.cuda.synchronize(idx)
             rt.check(rt.lib().piamd_dev_synchronize(torch.cuda.current_device() if idx is None else idx),
                      "hipDeviceSynchronize")
 
@@ -389,6 +417,8 @@ class cuda:  # namespace paddle.device.cuda
         d = _parse(device) if device is not None else None
         idx = d.index if d is not None and d.index is not None else (
             torch.cuda.current_device() if torch.cuda.is_available() else 0)
+        if not rt.available():
+            return torch.cuda.get_device_properties(idx)
         return _Props(rt.props(idx))
 
     @staticmethod
@@ -397,6 +427,8 @@ class cuda:  # namespace paddle.device.cuda
         from .framework import device_rt as rt
         d = _parse(device) if device is not None else None
         idx = d.index if d is not None and d.index is not None else torch.cuda.current_device()
+        if not rt.available():
+            return torch.cuda.mem_get_info(idx)
         f, t = ctypes.c_longlong(), ctypes.c_longlong()
         rt.check(rt.lib().piamd_dev_mem_info(idx, ctypes.byref(f), ctypes.byref(t)), "hipMemGetInfo")
         return f.value, t.value

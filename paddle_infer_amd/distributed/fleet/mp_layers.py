@@ -112,12 +112,15 @@ class _ColumnParallelFn(torch.autograd.Function):
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda")
     def forward(ctx, x, w, b, group):
+        wc, bc = w, b
         if x.is_cuda and w.dtype == torch.float32 and torch.is_autocast_enabled("cuda"):
+            # compute on an autocast-dtype copy; the weight gradient still goes to the fp32
+            # parameter itself (its main_grad / grad-ready hook live there, ops/linear.py:264)
             dt = torch.get_autocast_dtype("cuda")
-            x, w, b = x.to(dt), w.to(dt), b.to(dt) if b is not None else None
+            x, wc, bc = x.to(dt), w.to(dt), b.to(dt) if b is not None else None
         with torch.no_grad():
-            y = _linear(x, w, b)
-        ctx.save_for_backward(x, w)
+            y = _linear(x, wc, bc)
+        ctx.save_for_backward(x, w, wc)
         ctx.bias, ctx.group, ctx.shp = b, group, x.shape
         return y
 
@@ -125,16 +128,24 @@ class _ColumnParallelFn(torch.autograd.Function):
     @torch.amp.custom_bwd(device_type="cuda")
     def backward(ctx, dy):
         from ...ops.linear import bias_grad, input_grad, weight_grad
-        x, w = ctx.saved_tensors
+        x, w, wc = ctx.saved_tensors
         x2 = x.reshape(-1, x.shape[-1])
         dy2 = dy.reshape(-1, w.shape[1]).contiguous()
         dx = work = None
         if ctx.needs_input_grad[0]:
-            dx = input_grad(dy2, w).view(ctx.shp).contiguous()
+            dx = input_grad(dy2, wc).view(ctx.shp).contiguous()
             if _ws(ctx.group) > 1:
                 work = dist.all_reduce(dx, group=ctx.group, async_op=True)
-        dw = weight_grad(x2, dy2, w) if ctx.needs_input_grad[1] else None
-        db = bias_grad(dy2, ctx.bias) if ctx.bias is not None and ctx.needs_input_grad[2] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = weight_grad(x2, dy2, w)
+            if dw is not None and dw.dtype != w.dtype:
+                dw = dw.to(w.dtype)
+        db = None
+        if ctx.bias is not None and ctx.needs_input_grad[2]:
+            db = bias_grad(dy2, ctx.bias)
+            if db is not None and db.dtype != ctx.bias.dtype:
+                db = db.to(ctx.bias.dtype)
         if work is not None:
             work.wait()
         return dx, dw, db, None
@@ -224,6 +235,9 @@ class ColumnParallelLinear(Layer):
                                         is not None):
             y = _ColumnParallelFn.apply(x, self.weight, self.bias, self.group)
         else:
+            if torch.is_grad_enabled() and x.requires_grad:
+                # frozen weight (LoRA / BitFit): the input gradient still needs the mp all-reduce
+                x = c_identity(x, self.group)
             y = _linear(x, self.weight, self.bias)
         if self.gather_output and _ws(self.group) > 1:
             y = c_concat(y, self.group)

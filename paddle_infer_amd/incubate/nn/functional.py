@@ -288,15 +288,23 @@ class _Linear:
     def _dense_ln(self, x, ln, bias, act, resid):
         from ...ops.gemm import ln_fold, small_gemm
         from ...ops.linear import transposed
+        from ...ops.linear import _PARAM_EPOCH
         g, b, eps = ln
+        # an in-place reload (set_state_dict / copy_) of any folded operand bumps its version;
+        # the flat optimizers that write outside autograd bump the parameter epoch
         key = (g.data_ptr(), b.data_ptr(), bias.data_ptr() if bias is not None else 0)
+        ver = (_PARAM_EPOCH[0], self.w.data_ptr(), self.w._version, g._version, b._version,
+               bias._version if bias is not None else 0)
         f = self.lnf.get(key)
+        if f is not None and f[3] != ver:
+            f = None
+            del self.lnf[key]
         if f is None and torch.cuda.is_current_stream_capturing():
             # a fold built inside a capture would only be computed at replay: explicit LN instead
             return self._dense_epilogue(ops.layer_norm(x, g, b, eps), bias, act, resid)
         if f is None:
             wk = self.w if self.trans else transposed(self.w)
-            f = self.lnf[key] = ln_fold(wk, g, b, bias)
+            f = self.lnf[key] = tuple(ln_fold(wk, g, b, bias)) + (ver,)
         x2 = x.reshape(-1, x.shape[-1])
         if x2.stride(-1) != 1 or x2.stride(0) != x2.shape[1]:
             x2 = x2.contiguous()

@@ -212,7 +212,7 @@ class Executor:
                     from .backward import op_role as _role, OPTIMIZE as _OPT
                     if _role(op) == _OPT:
                         if buckets is not None:
-                            buckets.wait()
+                            buckets.wait(env)
                         else:
                             _allreduce_grads(env, dp, False)
                         dp = None
@@ -228,7 +228,7 @@ class Executor:
             if runner is not None:
                 runner.finish()
             if buckets is not None and dp is not None:  # no optimizer op ran: reduce anyway
-                buckets.wait()
+                buckets.wait(env)
         for hook in getattr(program, "_post_run_hooks", ()) if training else ():
             hook(scope, program)  # e.g. static.ExponentialMovingAverage
         if training:  # persistable outputs (updated params / accumulators) back into the Scope

@@ -99,6 +99,7 @@ class StreamRunner:
         self.cuda = device.type == "cuda"
         self.events = {}
         self.pending = {}  # op index → async Work (CPU / gloo path)
+        self.pending_out = {}  # op index → output names of that pending collective
         self.issued_on = {}  # op index → stream id, for tests / introspection
         if self.cuda:
             from ..device import side_stream
@@ -118,6 +119,16 @@ class StreamRunner:
                 w = self.pending.pop(a, None)
                 if w is not None:
                     w.wait()
+                    self.pending_out.pop(a, None)
+        if not self.cuda and self.pending:
+            # async collectives are not stream-ordered: an op reading the output of an earlier
+            # pending collective (same "stream" or not) waits for that Work first
+            ins = set(op.input_names())
+            for a in [a for a, outs in self.pending_out.items() if outs & ins]:
+                w = self.pending.pop(a, None)
+                if w is not None:
+                    w.wait()
+                self.pending_out.pop(a, None)
         if not self.cuda:
             # forward-role collectives of a training program keep the executor's autograd leaves
             from .backward import op_role, FORWARD
@@ -161,6 +172,7 @@ class StreamRunner:
         if dist.get_world_size(g) > 1:
             self.pending[oi] = dist.all_reduce(out, op=getattr(dist.ReduceOp, ALLREDUCE_OPS[op.type]),
                                                group=g, async_op=True)
+            self.pending_out[oi] = set(op.output_names())
         for n in op.output_names():
             env[n] = out
         return True
@@ -170,6 +182,7 @@ class StreamRunner:
         for w in self.pending.values():
             w.wait()
         self.pending.clear()
+        self.pending_out.clear()
         if self.cuda:
             self.compute.wait_stream(self.comm)
 
@@ -201,29 +214,51 @@ class GradBuckets:
         for bi, b in enumerate(self.buckets):
             self.launch_at.setdefault(max(produced[n] for n in b), []).append(bi)
         self.works = []
+        self.flat = {}        # (bucket, dtype, device) → (layout, persistent flat buffer)
+        self.flat_allocs = 0  # flat buffers allocated so far (tests: none after the first run)
 
     def after(self, pos, env):
-        """Launch every bucket completed at position ``pos`` (async all-reduce of its flat copy)."""
+        """Launch every bucket completed at position ``pos``: its gradients are packed into the
+        bucket's PERSISTENT flat buffer (allocated on the first run, reused every step) and
+        all-reduced asynchronously."""
         import torch.distributed as dist
         for bi in self.launch_at.get(pos, ()):
-            ts = [env[n] for n in self.buckets[bi] if isinstance(env.get(n), torch.Tensor)]
+            ts = [(n, env[n]) for n in self.buckets[bi] if isinstance(env.get(n), torch.Tensor)]
             if not ts:
                 continue
             by_dtype = {}
-            for t in ts:
-                by_dtype.setdefault(t.dtype, []).append(t)
-            for group in by_dtype.values():
-                from torch._utils import _flatten_dense_tensors
-                flat = _flatten_dense_tensors([t.detach() for t in group])
-                self.works.append((dist.all_reduce(flat, async_op=True), flat, group))
+            for n, t in ts:
+                by_dtype.setdefault((t.dtype, t.device), []).append((n, t))
+            for (dt, dev), group in by_dtype.items():
+                layout = tuple((n, tuple(t.shape)) for n, t in group)
+                key = (bi, dt, dev)
+                ent = self.flat.get(key)
+                if ent is None or ent[0] != layout:
+                    total = sum(t.numel() for _, t in group)
+                    ent = self.flat[key] = (layout, torch.empty(total, dtype=dt, device=dev))
+                    self.flat_allocs += 1
+                flat = ent[1]
+                off = 0
+                views = []
+                for n, t in group:
+                    k = t.numel()
+                    v = flat[off:off + k]
+                    if t.data_ptr() != v.data_ptr():
+                        v.copy_(t.detach().reshape(-1))
+                    views.append((n, v.view(t.shape), t))
+                    off += k
+                self.works.append((dist.all_reduce(flat, async_op=True), flat, views))
 
-    def wait(self):
-        """All buckets reduced and averaged back into the gradients (before the optimizer ops)."""
-        from torch._utils import _unflatten_dense_tensors
-        for work, flat, group in self.works:
+    def wait(self, env=None):
+        """All buckets reduced and averaged (before the optimizer ops). With ``env`` the gradient
+        names are re-bound to views of the flat buffers — no copy back."""
+        for work, flat, views in self.works:
             work.wait()
             flat.div_(self.world)
-            for t, v in zip(group, _unflatten_dense_tensors(flat, group)):
-                with torch.no_grad():
-                    t.copy_(v)
+            for n, v, t in views:
+                if env is not None and env.get(n) is t:
+                    env[n] = v
+                else:
+                    with torch.no_grad():
+                        t.copy_(v)
         self.works = []

@@ -119,3 +119,62 @@ def test_grad_buckets_close_in_production_order():
     gb = GradBuckets(ops, [0, 1, 2, 3], {"w1@GRAD", "w2@GRAD"}, sizes.get, bucket_mb=2)
     assert gb.buckets == [["w2@GRAD"], ["w1@GRAD"]]
     assert gb.launch_at == {0: [0], 2: [1]}
+
+
+def _dp_alloc_worker(rank, world):
+    from paddle_infer_amd.static import streams
+    from test_compiled_program_cpu import _train
+    streams.BUCKET_MB = 1e-4
+    made = []
+    orig = streams.GradBuckets.__init__
+
+    def init(self, *a, **k):
+        orig(self, *a, **k)
+        made.append(self)
+    streams.GradBuckets.__init__ = init
+    try:
+        params, losses = _train(True, rank, world)
+    finally:
+        streams.GradBuckets.__init__ = orig
+    return len(made), [gb.flat_allocs for gb in made], [len(gb.buckets) for gb in made], len(losses)
+
+
+def test_dp_grad_buckets_persistent_flat_buffers():
+    """The static DP all-reduce packs gradients into per-bucket flat buffers allocated once:
+    over several training runs the allocation count stays at one per bucket (no per-step
+    _flatten_dense_tensors copies), and results still match (test above)."""
+    res = run_distributed(_dp_alloc_worker, 2)
+    for r in range(2):
+        n_plans, allocs, nb, steps = res[r]
+        assert n_plans == 1 and steps > 1
+        assert allocs[0] == nb[0], (allocs, nb)
+
+
+def test_cpu_stream_runner_waits_on_pending_collective_inputs():
+    """An op that reads the output of an earlier async all-reduce waits for that Work even when
+    the plan carries no cross-stream wait for it (the gloo path has no stream ordering)."""
+    from paddle_infer_amd.static.streams import StreamRunner
+
+    class W:
+        def __init__(self):
+            self.done = False
+
+        def wait(self):
+            self.done = True
+
+    class Op:
+        type, func, paddle_inputs = "scale", None, None
+
+        def __init__(self, ins):
+            self.ins = ins
+
+        def input_names(self):
+            return self.ins
+
+    r = StreamRunner(torch.device("cpu"), [1, 1], [[], []], [False, False])
+    w = W()
+    r.pending[0] = w
+    r.pending_out[0] = {"s"}
+    ran = []
+    r.run(1, 1, Op(["s"]), lambda: ran.append(w.done), {})
+    assert ran == [True] and not r.pending

@@ -356,6 +356,7 @@ def side_stream(device, priority=2, key="side"):
 class cuda:  # namespace paddle.device.cuda
     Stream = _NativeStream
     Event = _NativeEvent
+    from .framework import cuda_graphs as graphs  # paddle.device.cuda.graphs.CUDAGraph
 
     @staticmethod
     def device_count():
@@ -481,3 +482,9 @@ def set_stream(stream):
 
 def stream_guard(stream):
     return cuda.stream_guard(stream)
+
+
+# ``import paddle.device.cuda.graphs`` / ``from paddle.device.cuda import graphs`` spellings
+import sys as _sys  # noqa: E402
+_sys.modules.setdefault(__name__ + ".cuda", cuda)  # type: ignore[arg-type]
+_sys.modules.setdefault(__name__ + ".cuda.graphs", cuda.graphs)

@@ -19,5 +19,5 @@ from .layer.layers import (  # noqa: F401
 from . import functional  # noqa: F401
 from . import initializer  # noqa: F401
 from .clip import ClipGradByGlobalNorm, ClipGradByNorm, ClipGradByValue  # noqa: F401
-from . import clip as utils  # noqa: F401
+from . import utils  # noqa: F401
 from . import quant  # noqa: F401,E402

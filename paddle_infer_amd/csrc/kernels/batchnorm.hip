@@ -833,3 +833,135 @@ PIAMD_EXPORT int piamd_bn_bwd(int dtype, int nhwc, const void* dy, const void* y
   return piamd_bn_bwd2(dtype, nhwc, dy, y, x, dx, dres, N, C, S, gamma, mean, rstd, dgamma, dbeta,
                        training, act, ws, nullptr, st);
 }
+
+// ------------------------------------------------------------------- cross-rank (SyncBatchNorm)
+// Reference `phi/kernels/gpu/sync_batch_norm_kernel.cu:192` / `sync_batch_norm_utils.h`. The
+// framework's SyncBatchNorm runs these kernels around RCCL collectives issued from Python:
+//   fwd: local (count, mean, M2) per channel → all-gather over ranks → piamd_bn_fwd3 with the
+//        gathered triples as channel-major partials (Welford merge across ranks: no E[x²]−E[x]²
+//        cancellation) → normalise + running statistics;
+//   bwd: local Σdz, Σdz·x̂ → all-reduce → dx from the global sums (dγ / dβ stay the local sums,
+//        the data-parallel gradient all-reduce sums them like any parameter gradient).
+namespace {
+__global__ __launch_bounds__(256) void bn_merge_stats(const float* __restrict__ part, int P, int C,
+                                                      float* __restrict__ out) {
+  const int c = blockIdx.x, t = threadIdx.x;
+  float n = 0.f, m = 0.f, m2 = 0.f;
+  for (int b = t; b < P; b += 256)
+    welford_merge(n, m, m2, part[(0 * P + b) * C + c], part[(1 * P + b) * C + c],
+                  part[(2 * P + b) * C + c]);
+  __shared__ float sn[256], sm[256], sm2[256];
+  sn[t] = n; sm[t] = m; sm2[t] = m2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) {
+      welford_merge(n, m, m2, sn[t + o], sm[t + o], sm2[t + o]);
+      sn[t] = n; sm[t] = m; sm2[t] = m2;
+    }
+    __syncthreads();
+  }
+  if (t) return;
+  out[c] = n;
+  out[C + c] = m;
+  out[2 * C + c] = m2;
+}
+
+__global__ __launch_bounds__(256) void bn_sum_parts2(const float* __restrict__ part, int P, int C,
+                                                     float* __restrict__ out) {
+  const int c = blockIdx.x, t = threadIdx.x;
+  float s1 = 0.f, s2 = 0.f;
+  for (int b = t; b < P; b += 256) { s1 += part[(0 * P + b) * C + c]; s2 += part[(1 * P + b) * C + c]; }
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  __shared__ float r[2][4];
+  if ((t & 63) == 0) { r[0][t >> 6] = s1; r[1][t >> 6] = s2; }
+  __syncthreads();
+  if (t) return;
+  out[c] = r[0][0] + r[0][1] + r[0][2] + r[0][3];
+  out[C + c] = r[1][0] + r[1][1] + r[1][2] + r[1][3];
+}
+}  // namespace
+
+// Local statistics of x: out f32 [3][C] = (count, mean, M2) per channel. ws ≥ 3·2048·C floats.
+PIAMD_EXPORT int piamd_bn_local_stats(int dtype, int nhwc, const void* x, int N, int C, int S,
+                                      float* ws, float* out, hipStream_t st) {
+  if (C < 1 || N < 1 || S < 1 || (nhwc && C % 8 && C < 256 && 256 % C)) return (int)hipErrorInvalidValue;
+  const long long M = (long long)N * S;
+  const int P = nhwc && C % 8 == 0 ? parts_for8(M, C) : parts_for(M);
+  const long long chunk = (M + P - 1) / P;
+  if (nhwc && C % 8 == 0) {
+    if (dtype) hipLaunchKernelGGL(bn_stats_nhwc8<bf16_t>, dim3(P), dim3(256), 0, st, (const bf16_t*)x, M, C, chunk, ws);
+    else hipLaunchKernelGGL(bn_stats_nhwc8<float>, dim3(P), dim3(256), 0, st, (const float*)x, M, C, chunk, ws);
+  } else if (nhwc) {
+    if (dtype) hipLaunchKernelGGL(bn_stats_nhwc<bf16_t>, dim3(P), dim3(256), 0, st, (const bf16_t*)x, M, C, chunk, ws);
+    else hipLaunchKernelGGL(bn_stats_nhwc<float>, dim3(P), dim3(256), 0, st, (const float*)x, M, C, chunk, ws);
+  } else {
+    if (dtype) hipLaunchKernelGGL(bn_stats_nchw<bf16_t>, dim3(C, P), dim3(256), 0, st, (const bf16_t*)x, N, C, S, chunk, ws);
+    else hipLaunchKernelGGL(bn_stats_nchw<float>, dim3(C, P), dim3(256), 0, st, (const float*)x, N, C, S, chunk, ws);
+  }
+  hipLaunchKernelGGL(bn_merge_stats, dim3(C), dim3(256), 0, st, ws, P, C, out);
+  return (int)hipGetLastError();
+}
+
+// Local backward sums: out f32 [2][C] = (Σ dz, Σ dz·x̂). ws ≥ 2·2048·C floats.
+PIAMD_EXPORT int piamd_bn_bwd_local_sums(int dtype, int nhwc, const void* dy, const void* y,
+                                         const void* x, int N, int C, int S, const float* mean,
+                                         const float* rstd, int act, float* ws, const float* ss,
+                                         float* out, hipStream_t st) {
+  if (C < 1 || N < 1 || S < 1 || (nhwc && C % 8 && C < 256 && 256 % C)) return (int)hipErrorInvalidValue;
+  const float* msc = act == 1 && ss && nhwc && C % 8 == 0 ? ss : nullptr;
+  const float* msh = msc ? ss + C : nullptr;
+  const long long M = (long long)N * S;
+  const int P = nhwc && C % 8 == 0 ? parts_for8(M, C) : parts_for(M);
+  const long long chunk = (M + P - 1) / P;
+  if (nhwc && C % 8 == 0) {
+    if (dtype) hipLaunchKernelGGL(bn_bwd_reduce_nhwc8<bf16_t>, dim3(P), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x, mean, rstd, M, C, chunk, act, ws, msc, msh);
+    else hipLaunchKernelGGL(bn_bwd_reduce_nhwc8<float>, dim3(P), dim3(256), 0, st, (const float*)dy, (const float*)y, (const float*)x, mean, rstd, M, C, chunk, act, ws, msc, msh);
+  } else if (nhwc) {
+    if (dtype) hipLaunchKernelGGL(bn_bwd_reduce_nhwc<bf16_t>, dim3(P), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x, mean, rstd, M, C, chunk, act, ws);
+    else hipLaunchKernelGGL(bn_bwd_reduce_nhwc<float>, dim3(P), dim3(256), 0, st, (const float*)dy, (const float*)y, (const float*)x, mean, rstd, M, C, chunk, act, ws);
+  } else {
+    if (dtype) hipLaunchKernelGGL(bn_bwd_reduce_nchw<bf16_t>, dim3(C, P), dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)y, (const bf16_t*)x, mean, rstd, N, C, S, chunk, act, ws);
+    else hipLaunchKernelGGL(bn_bwd_reduce_nchw<float>, dim3(C, P), dim3(256), 0, st, (const float*)dy, (const float*)y, (const float*)x, mean, rstd, N, C, S, chunk, act, ws);
+  }
+  hipLaunchKernelGGL(bn_sum_parts2, dim3(C), dim3(256), 0, st, ws, P, C, out);
+  return (int)hipGetLastError();
+}
+
+// dx (and dres) from GLOBAL sums [2][C] over Mtot elements per channel. ws ≥ 3·C floats.
+PIAMD_EXPORT int piamd_bn_bwd_apply_sums(int dtype, int nhwc, const void* dy, const void* y,
+                                         const void* x, void* dx, void* dres, int N, int C, int S,
+                                         const float* gamma, const float* mean, const float* rstd,
+                                         int act, const float* sums, float Mtot, float* ws,
+                                         const float* ss, hipStream_t st) {
+  if (C < 1 || N < 1 || S < 1 || (nhwc && C % 8 && C < 256 && 256 % C)) return (int)hipErrorInvalidValue;
+  const float* msc = act == 1 && !dres && ss && nhwc && C % 8 == 0 ? ss : nullptr;
+  const float* msh = msc ? ss + C : nullptr;
+  const long long total = (long long)N * S * C;
+  const bool v8 = nhwc ? C % 8 == 0 : S % 8 == 0;
+  float* coef = ws;
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3(C), dim3(256), 0, st, sums, 1, C, Mtot, gamma, mean, rstd,
+                     (float*)nullptr, (float*)nullptr, coef, 1);
+  if (v8) {
+    const dim3 g8(stride_grid(total / 8, 256));
+    if (dtype)
+      hipLaunchKernelGGL(bn_bwd_apply8<bf16_t>, g8, dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)y,
+                         (const bf16_t*)x, mean, rstd, coef, (bf16_t*)dx, (bf16_t*)dres, total, C, S,
+                         nhwc, act, 1, msc, msh);
+    else
+      hipLaunchKernelGGL(bn_bwd_apply8<float>, g8, dim3(256), 0, st, (const float*)dy, (const float*)y,
+                         (const float*)x, mean, rstd, coef, (float*)dx, (float*)dres, total, C, S,
+                         nhwc, act, 1, msc, msh);
+    return (int)hipGetLastError();
+  }
+  const dim3 g(stride_grid(total, 256));
+  if (dtype)
+    hipLaunchKernelGGL(bn_bwd_apply<bf16_t>, g, dim3(256), 0, st, (const bf16_t*)dy, (const bf16_t*)y,
+                       (const bf16_t*)x, mean, rstd, coef, (bf16_t*)dx, (bf16_t*)dres, total, C, S, nhwc,
+                       act, 1);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply<float>, g, dim3(256), 0, st, (const float*)dy, (const float*)y,
+                       (const float*)x, mean, rstd, coef, (float*)dx, (float*)dres, total, C, S, nhwc,
+                       act, 1);
+  return (int)hipGetLastError();
+}

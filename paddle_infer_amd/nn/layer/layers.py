@@ -473,34 +473,31 @@ class BatchNorm(_BatchNormBase):
 
 
 class SyncBatchNorm(_BatchNormBase):
-    """Batch norm whose batch statistics are all-reduced over the data-parallel group."""
+    """Batch norm whose batch statistics cover every rank of the data-parallel group (reference
+    `nn/layer/norm.py` SyncBatchNorm → `phi/kernels/gpu/sync_batch_norm_kernel.cu`): the
+    framework's Welford statistics kernels (`batchnorm.hip` piamd_bn_local_stats), an all-gather of
+    the per-rank (count, mean, M2) triples over RCCL, the cross-rank Welford merge inside the
+    normalise launch, and an all-reduce of the backward sums (`ops.batchnorm.sync_batch_norm`)."""
+
+    def __init__(self, num_features, momentum=0.9, epsilon=1e-5, weight_attr=None, bias_attr=None,
+                 data_format="NCHW", name=None, group=None):
+        super().__init__(num_features, momentum, epsilon, weight_attr, bias_attr, data_format)
+        self.group = group
 
     def forward(self, x):
         import torch.distributed as dist
-        if not (self.training and dist.is_initialized() and dist.get_world_size() > 1):
+        if not (self.training and dist.is_initialized() and dist.get_world_size(self.group) > 1):
             return super().forward(x)
-        dims = [0] + list(range(2, x.dim()))
-        n = torch.tensor([x.numel() / x.shape[1]], device=x.device, dtype=torch.float32)
-        s = x.float().sum(dims)
-        ss = (x.float() ** 2).sum(dims)
-        stats = torch.cat([s, ss, n])
-        stats = _AllReduceSum.apply(stats)
-        C = x.shape[1]
-        tot = stats[-1]
-        mean = stats[:C] / tot
-        var = stats[C:2 * C] / tot - mean ** 2
-        with torch.no_grad():
-            self._mean.mul_(self.momentum).add_((1 - self.momentum) * mean.detach().to(self._mean.dtype))
-            self._variance.mul_(self.momentum).add_((1 - self.momentum) * var.detach().to(self._variance.dtype))
-        shp = [1, C] + [1] * (x.dim() - 2)
-        y = (x - mean.view(shp).to(x.dtype)) * torch.rsqrt(var.view(shp) + self.epsilon).to(x.dtype)
-        return y * self.weight.view(shp) + self.bias.view(shp)
+        from ...ops.batchnorm import sync_batch_norm
+        return sync_batch_norm(x, self._mean, self._variance, self.weight, self.bias, True,
+                               self.momentum, self.epsilon, self.group, self.data_format)
 
     @classmethod
     def convert_sync_batchnorm(cls, layer):
         for name, m in list(layer.named_children()):
             if isinstance(m, _BatchNormBase) and not isinstance(m, SyncBatchNorm):
-                new = cls(m.weight.shape[0], m.momentum, m.epsilon)
+                new = cls(m.weight.shape[0], m.momentum, m.epsilon,
+                          data_format=getattr(m, "data_format", "NCHW"))
                 new.load_state_dict(m.state_dict())
                 setattr(layer, name, new)
             else:

@@ -291,6 +291,14 @@ _SIGS["piamd_bn_fwd3"] = ([c_int, c_int] + [c_void_p] * 3 + [c_int] * 3 + [c_voi
                           + [c_float, c_float, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p])
 _SIGS["piamd_bn_bwd2"] = ([c_int, c_int] + [c_void_p] * 5 + [c_int] * 3 + [c_void_p] * 5
                           + [c_int, c_int, c_void_p, c_void_p, c_void_p])
+# SyncBatchNorm: dtype, nhwc, x, N, C, S, ws, out[3][C], stream
+_SIGS["piamd_bn_local_stats"] = [c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]
+# dtype, nhwc, dy, y, x, N, C, S, mean, rstd, act, ws, ss, out[2][C], stream
+_SIGS["piamd_bn_bwd_local_sums"] = ([c_int, c_int] + [c_void_p] * 3 + [c_int] * 3 + [c_void_p] * 2
+                                    + [c_int, c_void_p, c_void_p, c_void_p, c_void_p])
+# dtype, nhwc, dy, y, x, dx, dres, N, C, S, gamma, mean, rstd, act, sums, Mtot, ws, ss, stream
+_SIGS["piamd_bn_bwd_apply_sums"] = ([c_int, c_int] + [c_void_p] * 5 + [c_int] * 3 + [c_void_p] * 3
+                                    + [c_int, c_void_p, c_float, c_void_p, c_void_p, c_void_p])
 # in, w, bias, out, N, H, W, Cin, OH, OW, Cout, R, S, st_h, st_w, pad_h, pad_w, dil_h, dil_w,
 # cin_g, cout_g, transposed, dtype, stream
 _SIGS["piamd_dconv2d"] = [c_void_p] * 4 + [c_int] * 19 + [c_void_p]

@@ -202,3 +202,137 @@ def batch_norm_act(x, running_mean, running_var, weight=None, bias=None, trainin
     join = _take_sink() if residual is not None else None
     return _BNAct.apply(x, weight, bias, residual, running_mean, running_var, bool(training),
                         momentum, epsilon, a, nhwc, (N, C, S), join)
+
+
+# ------------------------------------------------------------------------------ SyncBatchNorm
+def _all_gather_stats(local, group):
+    import torch.distributed as dist
+    W = dist.get_world_size(group)
+    out = torch.empty(W * local.numel(), dtype=local.dtype, device=local.device)
+    dist.all_gather_into_tensor(out, local.contiguous().reshape(-1), group=group)
+    return out.view((W,) + tuple(local.shape))
+
+
+def _welford_merge(g):
+    """g [W, 3, C] (count, mean, M2) → (n [C], mean [C], M2 [C]) — parallel Welford merge."""
+    n = g[:, 0].sum(0)
+    mean = (g[:, 0] * g[:, 1]).sum(0) / n.clamp_min(1)
+    m2 = g[:, 2].sum(0) + (g[:, 0] * (g[:, 1] - mean) ** 2).sum(0)
+    return n, mean, m2
+
+
+class _SyncBN(torch.autograd.Function):
+    """Cross-rank batch norm: Welford (count, mean, M2) triples all-gathered over ``group`` and
+    merged (GPU: inside ``piamd_bn_fwd3`` as channel-major partials), backward sums all-reduced.
+    Reference `phi/kernels/gpu/sync_batch_norm_kernel.cu:192` (dγ / dβ are the local sums, like
+    the reference's KeBNBackwardScaleBias; the data-parallel gradient reduction sums them)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, group, nhwc):
+        import torch.distributed as dist
+        if nhwc:
+            N, C = x.shape[0], x.shape[-1]
+        else:
+            N, C = x.shape[0], x.shape[1]
+        S = x.numel() // (N * C)
+        xc = x.contiguous()
+        dev = x.device
+        gpu = x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and _supported(x, nhwc, C)
+        if gpu:
+            local = torch.empty((3, C), device=dev, dtype=torch.float32)
+            ws = torch.empty(3 * _MAX_PARTS * C + 3 * C, device=dev, dtype=torch.float32)
+            _lib.call("piamd_bn_local_stats", int(x.dtype == torch.bfloat16), int(nhwc), xc.data_ptr(),
+                      N, C, S, ws.data_ptr(), local.data_ptr(), _lib.stream())
+        else:
+            xf = xc.float().movedim(-1, 1) if nhwc else xc.float()
+            dims = [0] + list(range(2, xf.dim()))
+            m = xf.mean(dims)
+            shp = [1, C] + [1] * (xf.dim() - 2)
+            local = torch.stack([torch.full_like(m, float(N * S)), m, ((xf - m.view(shp)) ** 2).sum(dims)])
+        g = _all_gather_stats(local, group) if dist.get_world_size(group) > 1 else local[None]
+        n_tot = float(g[:, 0, 0].sum())
+        if gpu:
+            part_t = g.permute(1, 2, 0).contiguous()  # [3][C][W] channel-major partials
+            mean = torch.empty(C, device=dev, dtype=torch.float32)
+            rstd = torch.empty(C, device=dev, dtype=torch.float32)
+            y = torch.empty_like(xc)
+            gw = weight.float().contiguous() if weight is not None else None
+            gb = bias.float().contiguous() if bias is not None else None
+            rm = running_mean if running_mean is not None and running_mean.dtype == torch.float32 else None
+            rv = running_var if running_var is not None and running_var.dtype == torch.float32 else None
+            _lib.call("piamd_bn_fwd3", int(x.dtype == torch.bfloat16), int(nhwc), xc.data_ptr(), None,
+                      y.data_ptr(), N, C, S, _lib.ptr(gw), _lib.ptr(gb), _lib.ptr(rm), _lib.ptr(rv),
+                      mean.data_ptr(), rstd.data_ptr(), float(momentum), float(eps), 1, 0,
+                      ws.data_ptr(), None, part_t.data_ptr(), part_t.shape[-1], _lib.stream())
+            if running_mean is not None and rm is None:  # non-f32 running statistics
+                with torch.no_grad():
+                    var_u = (g[:, 2].sum(0) + (g[:, 0] * (g[:, 1] - mean) ** 2).sum(0)) / max(n_tot - 1, 1)
+                    running_mean.mul_(momentum).add_((1 - momentum) * mean.to(running_mean.dtype))
+                    running_var.mul_(momentum).add_((1 - momentum) * var_u.to(running_var.dtype))
+            ctx.save_for_backward(xc, y, gw, mean, rstd)
+        else:
+            n, mean, m2 = _welford_merge(g)
+            var = m2 / n.clamp_min(1)
+            rstd = torch.rsqrt(var + eps)
+            if running_mean is not None:
+                with torch.no_grad():
+                    running_mean.mul_(momentum).add_((1 - momentum) * mean.to(running_mean.dtype))
+                    running_var.mul_(momentum).add_((1 - momentum) * (m2 / (n - 1).clamp_min(1)).to(running_var.dtype))
+            xf = xc.float().movedim(-1, 1) if nhwc else xc.float()
+            shp = [1, C] + [1] * (xf.dim() - 2)
+            xh = (xf - mean.view(shp)) * rstd.view(shp)
+            yf = xh * (weight.float().view(shp) if weight is not None else 1.0) + \
+                (bias.float().view(shp) if bias is not None else 0.0)
+            y = (yf.movedim(1, -1) if nhwc else yf).to(x.dtype).contiguous()
+            ctx.save_for_backward(xc, y, weight, mean, rstd)
+        ctx.meta = (gpu, nhwc, N, C, S, n_tot, group, weight is not None, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        import torch.distributed as dist
+        xc, y, gw, mean, rstd = ctx.saved_tensors
+        gpu, nhwc, N, C, S, n_tot, group, has_w, has_b = ctx.meta
+        dyc = dy.contiguous()
+        multi = dist.is_initialized() and dist.get_world_size(group) > 1
+        if gpu:
+            sums = torch.empty((2, C), device=xc.device, dtype=torch.float32)
+            ws = torch.empty(2 * _MAX_PARTS * C + 3 * C, device=xc.device, dtype=torch.float32)
+            _lib.call("piamd_bn_bwd_local_sums", int(xc.dtype == torch.bfloat16), int(nhwc), dyc.data_ptr(),
+                      y.data_ptr(), xc.data_ptr(), N, C, S, mean.data_ptr(), rstd.data_ptr(), 0,
+                      ws.data_ptr(), None, sums.data_ptr(), _lib.stream())
+            gs = sums.clone()
+            if multi:
+                dist.all_reduce(gs, group=group)
+            dx = torch.empty_like(xc)
+            _lib.call("piamd_bn_bwd_apply_sums", int(xc.dtype == torch.bfloat16), int(nhwc), dyc.data_ptr(),
+                      y.data_ptr(), xc.data_ptr(), dx.data_ptr(), None, N, C, S, _lib.ptr(gw),
+                      mean.data_ptr(), rstd.data_ptr(), 0, gs.data_ptr(), float(n_tot), ws.data_ptr(),
+                      None, _lib.stream())
+        else:
+            xf = xc.float().movedim(-1, 1) if nhwc else xc.float()
+            df = dyc.float().movedim(-1, 1) if nhwc else dyc.float()
+            dims = [0] + list(range(2, xf.dim()))
+            shp = [1, C] + [1] * (xf.dim() - 2)
+            xh = (xf - mean.view(shp)) * rstd.view(shp)
+            sums = torch.stack([df.sum(dims), (df * xh).sum(dims)])
+            gs = sums.clone()
+            if multi:
+                dist.all_reduce(gs, group=group)
+            gam = gw.float().view(shp) if gw is not None else 1.0
+            dxf = gam * rstd.view(shp) * (df - gs[0].view(shp) / n_tot - xh * gs[1].view(shp) / n_tot)
+            dx = (dxf.movedim(1, -1) if nhwc else dxf).to(xc.dtype)
+        dwt = sums[1].to(gw.dtype) if has_w and ctx.needs_input_grad[1] else None
+        dbs = sums[0].to(gw.dtype if gw is not None else torch.float32) if has_b and ctx.needs_input_grad[2] else None
+        return dx, dwt, dbs, None, None, None, None, None, None
+
+
+def sync_batch_norm(x, running_mean, running_var, weight=None, bias=None, training=True, momentum=0.9,
+                    epsilon=1e-5, group=None, data_format="NCHW"):
+    """Batch norm with statistics over every rank of ``group`` (training); eval = plain BN."""
+    import torch.distributed as dist
+    nhwc = data_format in ("NHWC", "NLC", "NDHWC")
+    if not training or not (dist.is_available() and dist.is_initialized()):
+        return batch_norm_act(x, running_mean, running_var, weight, bias, training, momentum, epsilon,
+                              data_format=data_format)
+    return _SyncBN.apply(x, weight, bias, running_mean, running_var, momentum, epsilon, group, nhwc)

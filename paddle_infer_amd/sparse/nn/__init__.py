@@ -86,21 +86,62 @@ class Softmax(Layer):
 
 
 class BatchNorm(Layer):
-    """BatchNorm over the channel (last) dim of the stored values of a sparse NDHWC tensor."""
+    """BatchNorm over the channel (last) dim of the stored values of a sparse NDHWC tensor
+    (reference `phi/kernels/sparse/gpu/batch_norm_kernel.cu`: dense batch norm on the non-zero
+    feature rows): the values [nnz, C] run the framework's channels-last BN kernels
+    (`ops.batchnorm.batch_norm_act`, Paddle momentum convention)."""
 
     def __init__(self, num_features, momentum=0.9, epsilon=1e-5, weight_attr=None, bias_attr=None,
                  data_format="NDHWC", use_global_stats=None, name=None):
         super().__init__()
-        self.bn = torch.nn.BatchNorm1d(num_features, eps=epsilon, momentum=1 - momentum)
+        from ...nn import initializer as I
+        self.momentum, self.epsilon = momentum, epsilon
+        self.use_global_stats = use_global_stats
+        self.weight = self.create_parameter([num_features], attr=weight_attr, default_initializer=I.Constant(1.0))
+        self.bias = self.create_parameter([num_features], attr=bias_attr, is_bias=True)
+        self.register_buffer("_mean", torch.zeros(num_features))
+        self.register_buffer("_variance", torch.ones(num_features))
+
+    def _values_bn(self, v):
+        from ...ops.batchnorm import batch_norm_act
+        train = self.training and not self.use_global_stats
+        return batch_norm_act(v, self._mean, self._variance, self.weight, self.bias, train, self.momentum,
+                              self.epsilon, data_format="NHWC")
 
     def forward(self, x):
         x = x.coalesce()
-        self.bn.train(self.training)
-        v = self.bn(x.values())
+        v = self._values_bn(x.values())
         return torch.sparse_coo_tensor(x.indices(), v, x.shape).coalesce()
 
 
-SyncBatchNorm = BatchNorm
+class SyncBatchNorm(BatchNorm):
+    """Sparse BatchNorm with statistics over every rank (reference
+    `phi/kernels/sparse/gpu/sync_batch_norm_kernel.cu`): the values' Welford triples all-gathered
+    and merged, backward sums all-reduced (`ops.batchnorm.sync_batch_norm`)."""
+
+    def __init__(self, num_features, momentum=0.9, epsilon=1e-5, weight_attr=None, bias_attr=None,
+                 data_format="NDHWC", name=None, group=None):
+        super().__init__(num_features, momentum, epsilon, weight_attr, bias_attr, data_format)
+        self.group = group
+
+    def _values_bn(self, v):
+        import torch.distributed as dist
+        if not (self.training and dist.is_initialized() and dist.get_world_size(self.group) > 1):
+            return super()._values_bn(v)
+        from ...ops.batchnorm import sync_batch_norm
+        return sync_batch_norm(v, self._mean, self._variance, self.weight, self.bias, True, self.momentum,
+                               self.epsilon, self.group, data_format="NHWC")
+
+    @classmethod
+    def convert_sync_batchnorm(cls, layer):
+        for name, m in list(layer.named_children()):
+            if type(m) is BatchNorm:
+                new = cls(m.weight.shape[0], m.momentum, m.epsilon)
+                new.load_state_dict(m.state_dict())
+                setattr(layer, name, new)
+            else:
+                cls.convert_sync_batchnorm(m)
+        return layer
 
 
 class Conv3D(Layer):

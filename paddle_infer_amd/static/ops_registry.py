@@ -554,8 +554,10 @@ def _wol(ins, a):
     if x.is_cuda and x.dtype != torch.bfloat16:  # the GPU weight-only GEMM takes bf16 activations
         xin = x.to(torch.bfloat16)
         b = b.to(torch.bfloat16) if b is not None else None
-    y = ops.weight_only_linear(xin, ins["weight"][0], b, ins["weight_scale"][0],
-                               a.get("weight_dtype", "int8"), a.get("act_method", "none"))
+    from ..inference.ref_layout import canonical_weight  # reference (sm80) bytes → MI355X order
+    wd = a.get("weight_dtype", "int8")
+    w = canonical_weight(ins["weight"][0], ins["weight_scale"][0], wd)
+    y = ops.weight_only_linear(xin, w, b, ins["weight_scale"][0], wd, a.get("act_method", "none"))
     return {"out": y.to(x.dtype) if y.dtype != x.dtype else y}
 
 
@@ -629,14 +631,19 @@ def _fused_multi_transformer_wo(ins, a):
     """Reference `fused_multi_transformer_weight_only_op.cu`: the same slots plus the per-channel
     *WScale / *WeightScale inputs; weights packed int8 ([N, K]) or int4 ([N/2, K])."""
     from ..incubate.nn import functional as IF
+    from ..inference.ref_layout import canonical_weight  # reference (sm80) bytes → MI355X order
     kw = _fmt_common(ins, a)
     kw.pop("trans_qkvw")
+    wd = a.get("weight_dtype", "int8")
+
+    def cw(slot, sslot):
+        return [canonical_weight(w, s_, wd) for w, s_ in zip(_seq(ins, slot), _seq(ins, sslot))]
     out = IF.fused_multi_transformer_weight_only(
-        ins["X"][0], _seq(ins, "LnScale"), _seq(ins, "LnBias"), _seq(ins, "QKVW"), _seq(ins, "QKVWScale"),
-        _seq(ins, "QKVBias"), _seq(ins, "OutLinearW"), _seq(ins, "OutLinearWScale"),
+        ins["X"][0], _seq(ins, "LnScale"), _seq(ins, "LnBias"), cw("QKVW", "QKVWScale"), _seq(ins, "QKVWScale"),
+        _seq(ins, "QKVBias"), cw("OutLinearW", "OutLinearWScale"), _seq(ins, "OutLinearWScale"),
         _seq(ins, "OutLinearBias"), _seq(ins, "FFNLnScale"), _seq(ins, "FFNLnBias"),
-        _seq(ins, "FFN1Weight"), _seq(ins, "FFN1WeightScale"), _seq(ins, "FFN1Bias"),
-        _seq(ins, "FFN2Weight"), _seq(ins, "FFN2WeightScale"), _seq(ins, "FFN2Bias"),
+        cw("FFN1Weight", "FFN1WeightScale"), _seq(ins, "FFN1WeightScale"), _seq(ins, "FFN1Bias"),
+        cw("FFN2Weight", "FFN2WeightScale"), _seq(ins, "FFN2WeightScale"), _seq(ins, "FFN2Bias"),
         weight_dtype=a.get("weight_dtype", "int8"), num_heads=a.get("num_heads"),
         num_kv_heads=a.get("num_kv_heads") or None, **kw)
     y, caches = (out if isinstance(out, tuple) else (out, None))
@@ -834,3 +841,4 @@ def _clip_op(ins, a):
 from . import ops_registry_ext  # noqa: E402,F401  (registers the extended op set)
 from . import ops_registry_more  # noqa: E402,F401  (fused blocks, rnn, 3-D conv / pool, detection)
 from . import ops_registry_model  # noqa: E402,F401  (quantization, fused BN+act, vocab-parallel CE, gate attention, beam search)
+from . import ops_registry_tail  # noqa: E402,F401  (the long tail: math / linalg / losses / optimizers / collectives / RNN / detection / fork serving ops)

@@ -781,13 +781,31 @@ def _fmt_moe(ins, a):
     return _fmt_run(ins, a, _moe_layers(ins, a, expert), moe=True)
 
 
-def _grouped_moe(bits, scale_slots):
+def _canon_stacked(w, s, bits):
+    """Per-expert reference-layout check / re-pack of a stacked [E, N_packed, K] weight
+    (`inference/ref_layout.py`), cached on the stacked tensor."""
+    from ..inference.ref_layout import canonical_weight, is_ref_layout
+    key = (w.data_ptr(), w._version)
+    c = getattr(w, "_piamd_canon", None)
+    if c is not None and c[0] == key:
+        return c[1]
+    out = w
+    if w.dim() == 3 and is_ref_layout(w[0], bits):
+        wd = "int4" if bits == 4 else "int8"
+        out = torch.stack([canonical_weight(w[e].clone(), s[e], wd) for e in range(w.shape[0])])
+    w._piamd_canon = (key, out)
+    return out
+
+
+def _grouped_moe(bits, scale_slots, canon=False):
     from ..incubate.moe import topk_gate, stacked
     from ..ops import moe as gm
 
     def expert(ins, i, ne, topk, act):
         w1, w2 = ins["ExpertWeight1"][i], ins["ExpertWeight2"][i]
         s1, s2 = ins[scale_slots[0]][i], ins[scale_slots[1]][i]
+        if canon:  # reference (sm80) bytes → MI355X order
+            w1, w2 = _canon_stacked(w1, s1, bits), _canon_stacked(w2, s2, bits)
         sl = slice(i * ne, (i + 1) * ne)
         b1 = stacked(ins["ExpertBias1"][sl]) if ins.get("ExpertBias1") else None
         b2 = stacked(ins["ExpertBias2"][sl]) if ins.get("ExpertBias2") else None
@@ -813,8 +831,8 @@ def _fmt_moe_wo(ins, a):
     layer [num_expert, N_packed, K] with ExpertWeight{1,2}Scale [num_expert, N]; one grouped
     weight-only MFMA launch per projection."""
     bits = 4 if a.get("weight_dtype", "int8") == "int4" else 8
-    return _fmt_run(ins, a, _moe_layers(ins, a, _grouped_moe(bits, ("ExpertWeight1Scale", "ExpertWeight2Scale"))),
-                    moe=True)
+    return _fmt_run(ins, a, _moe_layers(ins, a, _grouped_moe(bits, ("ExpertWeight1Scale", "ExpertWeight2Scale"),
+                                                             canon=True)), moe=True)
 
 
 @register("fused_multi_transformer_moe_int8")

@@ -5,12 +5,13 @@ import torch
 
 import paddle_infer_amd as paddle
 from paddle_infer_amd import ops
+from paddle_infer_amd.ops.linear import linear as _linear
 
 pytestmark = pytest.mark.gpu
 
 
 def _fn(x, w, g, b):
-    h = ops.linear.linear(x, w)                       # own GEMM
+    h = _linear(x, w)                       # own GEMM
     return ops.layer_norm(h, g, b, 1e-5)              # own LayerNorm kernel
 
 

@@ -15,8 +15,9 @@ kernel's own index arithmetic; ``sm80_int4_perm`` composes the four preprocessin
 ids), which gives both directions: :func:`ref_weight_quantize` (what the reference emits — used by
 the tests) and :func:`import_ref_weight` (reference bytes → row-major q → MI355X tile order).
 :func:`canonical_weight` is what the static weight-only ops call on every weight they receive:
-it detects the reference layout from the value statistics (a symmetric per-channel quantization
-puts most values near 0; read without the +128 / +8 offset they pile up at the range ends) unless
+it detects the reference layout from the stored bit patterns (the offset storage turns q = 0 into
+the pattern −128 / nibble −8, which this framework's quantizer never emits; and a symmetric
+quantization puts most values near 0, which read without the offset pile up at the range ends) unless
 ``PIAMD_WO_LAYOUT`` = ``mi355x`` / ``sm80`` pins it, and re-packs once per weight (cached).
 """
 from __future__ import annotations
@@ -135,13 +136,26 @@ def _ext_fraction(wb: torch.Tensor, bits: int, sample: int = 1 << 16) -> float:
     return float((v.abs() >= 6).float().mean())
 
 
+def _has_sentinel(wb: torch.Tensor, bits: int) -> bool:
+    """This framework's quantizer never emits −128 (int8: clamp ±127) nor the nibble −8 (int4:
+    scale = absmax/7); in the reference's offset storage those bit patterns are q = 0, which every
+    real weight matrix contains."""
+    u = wb.detach().reshape(-1).view(torch.uint8)
+    if bits == 8:
+        return bool((u == 128).any())
+    # int4: a −8 can still be a column's extreme in a re-packed reference q (scale absmax/8), ≈ 1/K
+    # of the values; the reference's zeros are far more frequent (≥ 1/16 even for uniform weights)
+    n8 = ((u & 15) == 8).sum() + ((u >> 4) == 8).sum()
+    return bool(n8.item() > 0.03 * 2 * u.numel())
+
+
 def is_ref_layout(wb: torch.Tensor, bits: int) -> bool:
     mode = os.environ.get("PIAMD_WO_LAYOUT", "auto")
     if mode == "sm80":
         return True
     if mode == "mi355x":
         return False
-    return _ext_fraction(wb, bits) > 0.25
+    return _has_sentinel(wb, bits) or _ext_fraction(wb, bits) > 0.5
 
 
 def canonical_weight(wb: torch.Tensor, scale: torch.Tensor, weight_dtype: str = "int8"):

@@ -58,7 +58,7 @@ def _at(a, *names, default=None):
 
 def _out(v, *extra):
     """``{"Out": v, "out": v, ...}``: the op writes whichever slot its desc names."""
-    d = {"Out": v, "out": v}
+    d = {"Out": v, "out": v, "Output": v}
     for e in extra:
         d[e] = v
     return d
@@ -1658,3 +1658,1256 @@ def _anchor_generator(ins, a):
     var = torch.tensor(a.get("variances", [0.1, 0.1, 0.2, 0.2]), dtype=torch.float32,
                        device=x.device).expand_as(anchors).contiguous()
     return {"Anchors": anchors.to(x.dtype), "Variances": var.to(x.dtype)}
+
+
+# -------------------------------------------------------------------------------- optimizers
+def _mp(ins):
+    mp = _in(ins, "MasterParam")
+    return mp
+
+
+def _opt_param(ins, a):
+    """(param to update in f32 — the master copy under multi_precision — , the stored param)."""
+    p = _in(ins, "Param", "param")
+    mp = _mp(ins)
+    return (mp if (mp is not None and a.get("multi_precision")) else p), p
+
+
+def _write_back(p, master):
+    if master is not p:
+        with torch.no_grad():
+            p.copy_(master.to(p.dtype))
+
+
+@register("adadelta", "adadelta_")
+def _adadelta(ins, a):
+    """Reference `impl/adadelta_kernel_impl.h`: E[g²] ← ρE[g²] + (1−ρ)g²; Δ = −√((E[Δ²]+ε)/(E[g²]+ε))·g;
+    E[Δ²] ← ρE[Δ²] + (1−ρ)Δ²; p += Δ (lr scales Δ when given)."""
+    w, p = _opt_param(ins, a)
+    g = _in(ins, "Grad", "grad").float()
+    sg, su = _in(ins, "AvgSquaredGrad", "avg_squared_grad"), _in(ins, "AvgSquaredUpdate", "avg_squared_update")
+    rho, eps = float(a.get("rho", 0.95)), float(a.get("epsilon", 1e-6))
+    sg.mul_(rho).add_((1 - rho) * g * g)
+    upd = -torch.sqrt((su + eps) / (sg + eps)) * g
+    su.mul_(rho).add_((1 - rho) * upd * upd)
+    lr = _in(ins, "LearningRate", "learning_rate")
+    w.add_((upd * (lr.reshape(()).float() if lr is not None else 1.0)).to(w.dtype))
+    _write_back(p, w)
+    return {"ParamOut": p, "AvgSquaredGradOut": sg, "AvgSquaredUpdateOut": su, "param_out": p,
+            "moment_out": sg, "inf_norm_out": su, "MasterParamOut": w}
+
+
+@register("adagrad", "adagrad_")
+def _adagrad(ins, a):
+    """Reference `adagrad` (dense): moment += g²; p −= lr·g / (√moment + ε)."""
+    w, p = _opt_param(ins, a)
+    g = _reg(w, _in(ins, "Grad", "grad").float(), a)
+    m = _in(ins, "Moment", "moment")
+    m.add_(g * g)
+    w.sub_((_lr(ins) * g / (torch.sqrt(m) + float(a.get("epsilon", 1e-6)))).to(w.dtype))
+    _write_back(p, w)
+    return {"ParamOut": p, "MomentOut": m, "param_out": p, "moment_out": m, "MasterParamOut": w}
+
+
+@register("adamax", "adamax_")
+def _adamax(ins, a):
+    """Reference `impl/adamax_kernel_impl.h`: m ← β1m + (1−β1)g; u ← max(|g|, β2u + ε);
+    p −= lr/(1−β1^t)·m/u (Beta1Pow is advanced by the optimizer's own scale op)."""
+    w, p = _opt_param(ins, a)
+    g = _in(ins, "Grad", "grad").float()
+    m, u, b1p = _in(ins, "Moment", "moment"), _in(ins, "InfNorm", "inf_norm"), _in(ins, "Beta1Pow", "beta1_pow")
+    b1, b2, eps = float(a.get("beta1", 0.9)), float(a.get("beta2", 0.999)), float(a.get("epsilon", 1e-8))
+    m.mul_(b1).add_((1 - b1) * g)
+    u.copy_(torch.maximum(g.abs(), b2 * u + eps))
+    w.sub_((_lr(ins) / (1 - b1p.reshape(()).float()) * m / u).to(w.dtype))
+    _write_back(p, w)
+    return {"ParamOut": p, "MomentOut": m, "InfNormOut": u, "param_out": p, "avg_squared_grad_out": m,
+            "avg_squared_update_out": u, "MasterParamOut": w}
+
+
+@register("lamb", "lamb_")
+def _lamb(ins, a):
+    """Reference `funcs/lamb_functors.h` + `impl/lamb_kernel_impl.h`: r = m̂/(√v̂ + ε) + wd·p,
+    trust = ‖p‖/‖r‖ (1 when either is 0), p −= lr·trust·r; beta pows advanced in place."""
+    w, p = _opt_param(ins, a)
+    if _skip(ins):
+        return {"ParamOut": p}
+    g = _in(ins, "Grad", "grad").float()
+    m1, m2 = _in(ins, "Moment1", "moment1"), _in(ins, "Moment2", "moment2")
+    b1p, b2p = _in(ins, "Beta1Pow", "beta1_pow"), _in(ins, "Beta2Pow", "beta2_pow")
+    b1, b2 = float(a.get("beta1", 0.9)), float(a.get("beta2", 0.999))
+    eps, wd = float(a.get("epsilon", 1e-6)), float(a.get("weight_decay", 0.01))
+    m1.mul_(b1).add_((1 - b1) * g)
+    m2.mul_(b2).add_((1 - b2) * g * g)
+    r = (m1 / (1 - b1p.reshape(()).float())) / (torch.sqrt(m2 / (1 - b2p.reshape(()).float())) + eps) + wd * w.float()
+    pn, rn = torch.linalg.vector_norm(w.float()), torch.linalg.vector_norm(r)
+    trust = torch.where((pn > 0) & (rn > 0), pn / rn, torch.ones_like(pn))
+    w.sub_((_lr(ins) * trust * r).to(w.dtype))
+    b1p.mul_(b1)
+    b2p.mul_(b2)
+    _write_back(p, w)
+    return {"ParamOut": p, "Moment1Out": m1, "Moment2Out": m2, "Beta1PowOut": b1p, "Beta2PowOut": b2p,
+            "MasterParamOut": w}
+
+
+@register("rmsprop", "rmsprop_")
+def _rmsprop(ins, a):
+    """Reference `impl/rmsprop_kernel_impl.h` (dense): ms ← ρms + (1−ρ)g²; (centered) mg ← ρmg + (1−ρ)g;
+    mom ← μ·mom + lr·g/√(ms [− mg²] + ε); p −= mom."""
+    w, p = _opt_param(ins, a)
+    g = _in(ins, "Grad", "grad").float()
+    ms, mom = _in(ins, "MeanSquare", "mean_square"), _in(ins, "Moment", "moment")
+    mg = _in(ins, "MeanGrad", "mean_grad")
+    rho, eps, mu = float(a.get("decay", 0.9)), float(a.get("epsilon", 1e-10)), float(a.get("momentum", 0.0))
+    ms.mul_(rho).add_((1 - rho) * g * g)
+    if a.get("centered"):
+        mg.mul_(rho).add_((1 - rho) * g)
+        den = torch.sqrt(ms - mg * mg + eps)
+    else:
+        den = torch.sqrt(ms + eps)
+    mom.mul_(mu).add_(_lr(ins) * g / den)
+    w.sub_(mom.to(w.dtype))
+    _write_back(p, w)
+    out = {"ParamOut": p, "MomentOut": mom, "MeanSquareOut": ms, "param_out": p, "moment_out": mom,
+           "mean_square_out": ms, "MasterParamOut": w}
+    if mg is not None:
+        out.update(MeanGradOut=mg, mean_grad_out=mg)
+    return out
+
+
+@register("lars_momentum")
+def _lars_momentum(ins, a):
+    """Reference `lars_momentum_op.cu`: local_lr = lr·coeff·‖p‖/(‖g‖ + wd·‖p‖ + ε) (lr when a norm is
+    0); v ← μv + local_lr·(g + wd·p); p −= v. Param / Grad / Velocity are lists (merged form)."""
+    ps, gs, vs = _inl(ins, "Param"), _inl(ins, "Grad"), _inl(ins, "Velocity")
+    mps = _inl(ins, "MasterParam")
+    lrs = _inl(ins, "LearningRate")
+    mu, coeff, eps = float(a.get("mu", 0.9)), float(a.get("lars_coeff", 0.001)), float(a.get("epsilon", 0.0))
+    wds = a.get("lars_weight_decay", [0.0005])
+    wds = wds if isinstance(wds, (list, tuple)) else [wds]
+    rescale = float(a.get("rescale_grad", 1.0))
+    outs_p, outs_v, outs_m = [], [], []
+    for i, (p, g, v) in enumerate(zip(ps, gs, vs)):
+        w = mps[i] if (mps and a.get("multi_precision")) else p
+        lr = lrs[min(i, len(lrs) - 1)].reshape(()).float()
+        wd = float(wds[min(i, len(wds) - 1)])
+        gf = g.float() * rescale
+        pn, gn = torch.linalg.vector_norm(w.float()), torch.linalg.vector_norm(gf)
+        local = torch.where((pn > 0) & (gn > 0), lr * coeff * pn / (gn + wd * pn + eps), lr)
+        v.mul_(mu).add_(local * (gf + wd * w.float()))
+        w.sub_(v.to(w.dtype))
+        _write_back(p, w)
+        outs_p.append(p)
+        outs_v.append(v)
+        outs_m.append(w)
+    return {"ParamOut": outs_p, "VelocityOut": outs_v, "MasterParamOut": outs_m}
+
+
+@register("merged_adam", "merged_adam_")
+def _merged_adam(ins, a):
+    """Reference `merged_adam_op`: the adam update over lists of parameters (one fused step)."""
+    ps = _inl(ins, "Param", "param")
+    n = len(ps)
+    outs = {k: [] for k in ("ParamOut", "Moment1Out", "Moment2Out", "Beta1PowOut", "Beta2PowOut", "MasterParamOut")}
+    lrs = _inl(ins, "LearningRate", "learning_rate")
+    for i in range(n):
+        sub = {"Param": [ps[i]], "Grad": [_inl(ins, "Grad", "grad")[i]],
+               "LearningRate": [lrs[min(i, len(lrs) - 1)]],
+               "Moment1": [_inl(ins, "Moment1", "moment1")[i]], "Moment2": [_inl(ins, "Moment2", "moment2")[i]],
+               "Beta1Pow": [_inl(ins, "Beta1Pow", "beta1_pow")[i if not a.get("use_global_beta_pow") else 0]],
+               "Beta2Pow": [_inl(ins, "Beta2Pow", "beta2_pow")[i if not a.get("use_global_beta_pow") else 0]]}
+        mp = _inl(ins, "MasterParam", "master_param")
+        master = mp[i] if (mp and a.get("multi_precision")) else None
+        if master is not None:
+            sub["Param"] = [master]
+        if a.get("use_global_beta_pow") and i > 0:
+            b1, b2 = sub["Beta1Pow"][0], sub["Beta2Pow"][0]
+            sub["Beta1Pow"], sub["Beta2Pow"] = [b1.clone()], [b2.clone()]
+        r = REGISTRY["adam"](sub, a)
+        if master is not None:
+            _write_back(ps[i], master)
+        outs["ParamOut"].append(ps[i])
+        outs["Moment1Out"].append(r["Moment1Out"])
+        outs["Moment2Out"].append(r["Moment2Out"])
+        outs["Beta1PowOut"].append(r["Beta1PowOut"])
+        outs["Beta2PowOut"].append(r["Beta2PowOut"])
+        outs["MasterParamOut"].append(master if master is not None else ps[i])
+    return outs
+
+
+@register("merged_momentum", "merged_momentum_")
+def _merged_momentum(ins, a):
+    """Reference `merged_momentum_op`: the momentum update over lists of parameters; per-parameter
+    regularization_method / regularization_coeff lists."""
+    ps = _inl(ins, "Param", "param")
+    lrs = _inl(ins, "LearningRate", "learning_rate")
+    meth = a.get("regularization_method") or []
+    coef = a.get("regularization_coeff") or []
+    mps = _inl(ins, "MasterParam", "master_param")
+    po, vo, mo = [], [], []
+    for i, p in enumerate(ps):
+        master = mps[i] if (mps and a.get("multi_precision")) else None
+        sub = {"Param": [master if master is not None else p], "Grad": [_inl(ins, "Grad", "grad")[i]],
+               "Velocity": [_inl(ins, "Velocity", "velocity")[i]], "LearningRate": [lrs[min(i, len(lrs) - 1)]]}
+        aa = dict(mu=a.get("mu", 0.9), use_nesterov=a.get("use_nesterov", False),
+                  rescale_grad=a.get("rescale_grad", 1.0))
+        if i < len(meth) and meth[i]:
+            aa.update(regularization_method=meth[i], regularization_coeff=coef[i] if i < len(coef) else 0.0)
+        r = REGISTRY["momentum"](sub, aa)
+        if master is not None:
+            _write_back(p, master)
+        po.append(p)
+        vo.append(r["VelocityOut"])
+        mo.append(master if master is not None else p)
+    return {"ParamOut": po, "VelocityOut": vo, "MasterParamOut": mo}
+
+
+@register("sparse_momentum")
+def _sparse_momentum(ins, a):
+    """Reference `sparse_momentum_op`: the momentum update on the rows ``Index`` along ``axis``."""
+    p, g, v, idx = _in(ins, "Param"), _in(ins, "Grad"), _in(ins, "Velocity"), _in(ins, "Index").reshape(-1).long()
+    ax = int(_in(ins, "Axis").reshape(-1)[0]) if _in(ins, "Axis") is not None else int(a.get("axis", 0))
+    dense = torch.zeros_like(p, dtype=torch.float32).index_add(ax, idx, g.float())
+    r = REGISTRY["momentum"]({"Param": [p], "Grad": [dense], "Velocity": [v],
+                              "LearningRate": ins["LearningRate"]}, a)
+    return {"ParamOut": r["ParamOut"], "VelocityOut": r["VelocityOut"]}
+
+
+@register("average_accumulates", "average_accumulates_")
+def _average_accumulates(ins, a):
+    """Reference `average_accumulates_op.h` (ModelAverage): sums of the parameter over windows."""
+    p = _in(ins, "param")
+    s1, s2, s3 = _in(ins, "in_sum_1"), _in(ins, "in_sum_2"), _in(ins, "in_sum_3")
+    na, ona, nu = (_in(ins, k) for k in ("in_num_accumulates", "in_old_num_accumulates", "in_num_updates"))
+    aw, mx, mn = float(a.get("average_window", 0)), int(a.get("max_average_window", 10000)), \
+        int(a.get("min_average_window", 10000))
+    n_upd = int(nu.reshape(-1)[0]) + 1
+    n_acc = int(na.reshape(-1)[0]) + 1
+    n_old = int(ona.reshape(-1)[0])
+    s1 = s1 + p
+    if n_upd % 16384 == 0:  # kMaxNumAccumulates: fold sum_1 into sum_2 for precision
+        s2, s1 = s2 + s1, torch.zeros_like(s1)
+    if n_acc >= mn and n_acc >= min(mx, n_upd * aw):
+        s3, s1, s2 = s1 + s2, torch.zeros_like(s1), torch.zeros_like(s2)
+        n_old, n_acc = n_acc, 0
+    mk = lambda v, t: torch.tensor([v], dtype=t.dtype, device=t.device)  # noqa: E731
+    return {"out_sum_1": s1, "out_sum_2": s2, "out_sum_3": s3, "out_num_accumulates": mk(n_acc, na),
+            "out_old_num_accumulates": mk(n_old, ona), "out_num_updates": mk(n_upd, nu)}
+
+
+# ------------------------------------------------------------------------- static collectives
+def _pg(a):
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return None, 1
+    from .ops_registry_ext import _group
+    g = _group(a)
+    return g, dist.get_world_size(g)
+
+
+@register("c_allgather", "partial_allgather")
+def _c_allgather(ins, a):
+    """Reference `collective/c_allgather_op.cc`: rank-major concatenation along dim 0 (RCCL
+    all_gather_into_tensor; ``partial_allgather``: every rank holds the full tensor and contributes
+    its 1/nranks slice)."""
+    import torch.distributed as dist
+    x = _x(ins).contiguous()
+    g, W = _pg(a)
+    if W == 1:
+        return _out(x)
+    if "rank" in a and a.get("nranks"):  # partial_allgather
+        r = int(a["rank"])
+        part = x.reshape(-1).chunk(W)[r].contiguous()
+        out = torch.empty(part.numel() * W, dtype=x.dtype, device=x.device)
+        dist.all_gather_into_tensor(out, part, group=g)
+        return _out(out.view(x.shape))
+    out = torch.empty((W * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out.view(-1), x.view(-1), group=g)
+    return _out(out)
+
+
+@register("c_reducescatter")
+def _c_reducescatter(ins, a):
+    """Reference `collective/c_reducescatter_op.cc`: sum over ranks, rank r keeps rows
+    [r·n/W, (r+1)·n/W) of dim 0."""
+    import torch.distributed as dist
+    x = _x(ins).contiguous()
+    g, W = _pg(a)
+    if W == 1:
+        return _out(x)
+    out = torch.empty((x.shape[0] // W,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.reduce_scatter_tensor(out.view(-1), x.view(-1), group=g)
+    return _out(out)
+
+
+@register("alltoall")
+def _alltoall(ins, a):
+    """Reference `collective/alltoall_op.cc`: dim 0 split into W equal blocks, block j goes to rank j."""
+    import torch.distributed as dist
+    x = _x(ins).contiguous()
+    g, W = _pg(a)
+    if W == 1:
+        return _out(x)
+    out = torch.empty_like(x)
+    dist.all_to_all_single(out, x, group=g)
+    return _out(out)
+
+
+@register("sync_batch_norm", "sync_batch_norm_")
+def _sync_batch_norm(ins, a):
+    """Reference `sync_batch_norm_op` (batch_norm slots): training statistics over every rank of the
+    ring (own Welford kernels + RCCL all-gather, `ops.batchnorm.sync_batch_norm`)."""
+    from ..ops.batchnorm import sync_batch_norm
+    x = _in(ins, "X", "x")
+    rm, rv = _in(ins, "Mean", "mean"), _in(ins, "Variance", "variance")
+    train = not a.get("is_test", False) and not a.get("use_global_stats", False)
+    g, _ = _pg(a)
+    y = sync_batch_norm(x, rm, rv, _in(ins, "Scale", "scale"), _in(ins, "Bias", "bias"), train,
+                        float(a.get("momentum", 0.9)), float(a.get("epsilon", 1e-5)), g,
+                        a.get("data_layout", "NCHW"))
+    return {"Y": y, "out": y, "MeanOut": rm, "VarianceOut": rv, "mean_out": rm, "variance_out": rv}
+
+
+def _global_exchange(ins, a, gather):
+    """Reference `collective/global_scatter_op.cc` / `global_gather_op.cc` (MoE token exchange):
+    rows grouped by (rank, expert) counts. scatter sends ``local_count`` rows per rank and receives
+    ``global_count``; gather is the inverse exchange."""
+    import torch.distributed as dist
+    x = _x(ins)
+    lc, gc = _in(ins, "local_count"), _in(ins, "global_count")
+    g, W = _pg(a)
+    if W == 1:
+        return _out(x)
+    send = [int(v) for v in lc.reshape(W, -1).sum(1).tolist()]
+    recv = [int(v) for v in gc.reshape(W, -1).sum(1).tolist()]
+    if gather:
+        send, recv = recv, send
+    out = torch.empty((sum(recv),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_to_all_single(out, x.contiguous(), recv, send, group=g)
+    return _out(out)
+
+
+register("global_scatter")(lambda ins, a: _global_exchange(ins, a, False))
+register("global_gather")(lambda ins, a: _global_exchange(ins, a, True))
+
+
+# --------------------------------------------------------------------- fork serving / MoE ops
+@register("weight_quantize")
+def _weight_quantize(ins, a):
+    """yaml `weight_quantize`: x [K, N] → (out: this framework's MFMA-tile packed int8 [N, K] /
+    int4 [N/2, K] — or row-major [N, K] for llm.int8 —, scale [N])."""
+    from ..ops.inference import weight_quantize
+    x = _x(ins)
+    q, s = weight_quantize(x, a.get("algo", "weight_only_int8"))
+    return {"out": q.view(torch.int8) if q.dtype == torch.uint8 else q, "scale": s.to(x.dtype),
+            "Out": q, "Scale": s}
+
+
+@register("weight_dequantize")
+def _weight_dequantize(ins, a):
+    from ..inference.ref_layout import canonical_weight
+    from ..ops.inference import weight_dequantize
+    x, s = _in(ins, "x", "X"), _in(ins, "scale", "Scale")
+    algo = a.get("algo", "weight_only_int8")
+    w = canonical_weight(x, s, "int4" if algo == "weight_only_int4" else "int8")
+    od = a.get("out_dtype", "float16")
+    if not isinstance(od, str):
+        od = {v: k for k, v in __import__("paddle_infer_amd.static.proto", fromlist=["VT"]).VT.items()}.get(int(od), "float16")
+    return _out(weight_dequantize(w, s.float(), algo, od))
+
+
+@register("weight_only_linear2")
+def _weight_only_linear2(ins, a):
+    """yaml `weight_only_linear2` (x, weight, bias, weight_scale, m, n, k): the weight-only GEMM
+    with the GEMM extents given as attributes (x viewed [m, k])."""
+    x = _in(ins, "x", "X")
+    k = int(a.get("k", x.shape[-1]))
+    xv = x.reshape(-1, k)
+    r = REGISTRY["weight_only_linear"]({"x": [xv], "weight": ins["weight"], "bias": ins.get("bias") or [],
+                                        "weight_scale": ins["weight_scale"]},
+                                       {"weight_dtype": a.get("weight_dtype", "int8"),
+                                        "act_method": a.get("act_method", "none")})
+    y = r["out"]
+    return _out(y.reshape(*x.shape[:-1], y.shape[-1]))
+
+
+@register("flash_attn_unpadded")
+def _flash_attn_unpadded(ins, a):
+    """yaml `flash_attn_unpadded`: packed [total_tokens, H, D] q/k/v with cumulative offsets —
+    the variable-length MFMA flash kernel (`ops.attention.flash_attention_varlen`)."""
+    from .. import ops
+    q, k, v = _in(ins, "q"), _in(ins, "k"), _in(ins, "v")
+    cq, ck = _in(ins, "cu_seqlens_q"), _in(ins, "cu_seqlens_k")
+    mask = _in(ins, "attn_mask")
+    p = 0.0 if a.get("is_test", False) else float(a.get("dropout", 0.0))
+    if mask is not None:  # additive mask over the padded [B, H, Sq, Sk] view: the dense path per sequence
+        outs = []
+        cql, ckl = cq.tolist(), ck.tolist()
+        for b in range(len(cql) - 1):
+            qs, ks, vs = q[cql[b]:cql[b + 1]], k[ckl[b]:ckl[b + 1]], v[ckl[b]:ckl[b + 1]]
+            mb = mask[b] if mask.dim() == 4 else mask
+            mb = mb[..., :qs.shape[0], :ks.shape[0]]
+            outs.append(ops.flash_attention(qs[None], ks[None], vs[None], causal=bool(a.get("causal", False)),
+                                            scale=a.get("scale"), attn_mask=mb[None] if mb.dim() == 3 else mb,
+                                            dropout_p=p)[0])
+        o = torch.cat(outs, 0)
+    else:
+        o = ops.flash_attention_varlen(q, k, v, cq, ck, int(a.get("max_seqlen_q", 0)), int(a.get("max_seqlen_k", 0)),
+                                       causal=bool(a.get("causal", False)), scale=a.get("scale"), dropout_p=p,
+                                       training=not a.get("is_test", False))
+    return {"out": o, "Out": o, "softmax": torch.empty(0, device=o.device),
+            "softmax_lse": torch.empty(0, device=o.device), "seed_offset": torch.zeros(2, dtype=torch.int64)}
+
+
+@register("number_count_v2", "number_count")
+def _number_count(ins, a):
+    """yaml `number_count_v2` (MoE): per-expert counts of the routed expert ids (ids outside
+    [0, upper_range) — dropped slots — are not counted)."""
+    x = _in(ins, "numbers", "x", "X").reshape(-1).long()
+    up = int(a.get("upper_range", 0))
+    ok = (x >= 0) & (x < up)
+    return _out(torch.bincount(x[ok], minlength=up)[:up].to(torch.int64))
+
+
+@register("fused_moe_kernel")
+def _fused_moe_kernel(ins, a):
+    """yaml `fused_moe_kernel` (reference `phi/kernels/gpu/fused_moe_kernel.cu`): h = LN(x) (pre-LN) or
+    x; gate = h·Wg + bg; top-k of the RAW gate logits (their values weight the experts, no softmax);
+    expert e: GELU(h·W1_e + b1_e)·W2_e + b2_e; out = x + Σ_k gate_k·expert_k(h); post-LN when not
+    pre_layer_norm. Tensor-parallel token slicing (mp_size) with an all-gather; expert parallel
+    (world_size) through the all-to-all dispatch. Single-rank experts run the framework's grouped
+    MFMA GEMMs (`ops.moe.grouped_ffn`) on a sorted-row routing."""
+    from ..incubate.nn import functional as IF
+    from ..ops import moe as gm
+    import torch.distributed as dist
+    x = _in(ins, "x", "X")
+    gw, gb = _in(ins, "gate_weight"), _in(ins, "gate_bias")
+    lns, lnb = _in(ins, "ln_scale"), _in(ins, "ln_bias")
+    w1s, b1s = _inl(ins, "experts_weight1"), _inl(ins, "experts_bias1")
+    w2s, b2s = _inl(ins, "experts_weight2"), _inl(ins, "experts_bias2")
+    pre = bool(a.get("pre_layer_norm", True))
+    eps = float(a.get("ln_epsilon", 1e-5))
+    topk = int(a.get("topk", 2))
+    mp, mpr, ne, ws = int(a.get("mp_size", 1)), int(a.get("mp_rank", 0)), int(a.get("num_expert", len(w1s))), \
+        int(a.get("world_size", 1))
+    act = "gelu_tanh" if a.get("approximate") else "gelu"
+    B, S, Dm = x.shape
+    x2 = x.reshape(-1, Dm)
+    h = F.layer_norm(x2.float(), (Dm,), lns.float(), lnb.float(), eps).to(x.dtype) if pre else x2
+    T = h.shape[0]
+    if mp > 1:
+        st = T // ws * mpr
+        h = h[st:min(st + T // ws, T)]
+    logits = h @ gw.to(h.dtype) + gb.to(h.dtype)
+    val, idx = torch.topk(logits, topk, -1)
+    from .ops_registry import _ring_group
+    grp = _ring_group({"ring_id": a.get("moe_ring_id", -1)}) if ws > 1 else None
+    if ws > 1 and grp is not None and dist.get_world_size(grp) > 1:
+        from ..incubate.moe import dispatch, combine as ep_combine, run_experts
+        xs, counts, ctx = dispatch(h, idx, ne, grp)
+        experts = [(lambda t, e=e: F.gelu(t @ w1s[e] + b1s[e], approximate="tanh" if act == "gelu_tanh" else "none")
+                    @ w2s[e] + b2s[e]) for e in range(ne)]
+        y = ep_combine(run_experts(xs, counts, experts), val, ctx)
+    else:
+        r = gm.permute(idx, ne, align=64 if h.is_cuda else 1)
+        w1 = torch.stack(list(w1s))
+        w2 = torch.stack(list(w2s))
+        b1 = torch.stack([b.reshape(-1) for b in b1s]) if b1s else None
+        b2 = torch.stack([b.reshape(-1) for b in b2s]) if b2s else None
+        ys = gm.grouped_ffn(gm.gather(h, r), w1, b1, w2, b2, r, act=act)
+        y = gm.combine(ys, val, r)
+    if mp > 1:
+        parts = [torch.empty_like(y) for _ in range(mp)]
+        dist.all_gather(parts, y.contiguous(), group=_ring_group({"ring_id": a.get("moe_ring_id", 0)}))
+        y = torch.cat(parts, 0)
+    out = (x2 + y.to(x.dtype)).reshape(x.shape)
+    if not pre:
+        out = F.layer_norm(out.float(), (Dm,), lns.float(), lnb.float(), eps).to(x.dtype)
+    del IF
+    return _out(out)
+
+
+@register("random_routing")
+def _random_routing(ins, a):
+    """Reference `random_routing_op.cu` (gshard): the second expert of a token is dropped (−1) when
+    2·value < the token's uniform sample."""
+    prob, val, idx = _in(ins, "Prob"), _in(ins, "TopK_Value"), _in(ins, "TopK_Idx")
+    out = idx.clone()
+    drop = 2 * val[:, 1] < prob.reshape(-1)
+    out[:, 1] = torch.where(drop, torch.full_like(out[:, 1], -1), out[:, 1])
+    return _out(out)
+
+
+@register("class_center_sample")
+def _class_center_sample(ins, a):
+    from ..nn.functional.extra import class_center_sample
+    from .ops_registry import _ring_group
+    lab = _in(ins, "Label", "label")
+    rl, sc = class_center_sample(lab, int(a["num_classes"]), int(a["num_samples"]), group=_ring_group(a))
+    return {"RemappedLabel": rl, "SampledLocalClassCenter": sc}
+
+
+# ----------------------------------------------------------------------------------- RNN ops
+def _act_by_name(n):
+    return {"sigmoid": torch.sigmoid, "tanh": torch.tanh, "relu": torch.relu, "identity": lambda t: t,
+            "": lambda t: t, None: lambda t: t}[n]
+
+
+def _act_by_id(i):
+    return {0: lambda t: t, 1: torch.sigmoid, 2: torch.tanh, 3: torch.relu}[int(i)]
+
+
+@register("cudnn_lstm")
+def _cudnn_lstm(ins, a):
+    """Reference `cudnn_lstm_op.cc`: time-major LSTM in cuDNN weight order — WeightList (or the flat
+    W: every (layer, direction) W_ih [4H, I] then W_hh [4H, H], then all b_ih, b_hh). Runs the
+    ``rnn`` program op (one input GEMM per layer, own GEMMs)."""
+    x = _in(ins, "Input")
+    L, Hs = int(a.get("num_layers", 1)), int(a.get("hidden_size"))
+    D = 2 if a.get("is_bidirec") else 1
+    wl = _inl(ins, "WeightList")
+    if not wl:
+        W = _in(ins, "W").reshape(-1)
+        I0 = x.shape[-1]
+        shapes = []
+        for layer in range(L):
+            inp = I0 if layer == 0 else D * Hs
+            for _ in range(D):
+                shapes += [(4 * Hs, inp), (4 * Hs, Hs)]
+        shapes += [(4 * Hs,)] * (2 * L * D)
+        off, wl = 0, []
+        for s in shapes:
+            n = int(np.prod(s))
+            wl.append(W[off:off + n].reshape(s))
+            off += n
+    pre = [t for t in (_in(ins, "InitH"), _in(ins, "InitC")) if t is not None]
+    r = REGISTRY["rnn"]({"Input": [x], "WeightList": wl, "PreState": pre,
+                         "SequenceLength": ins.get("SequenceLength") or []},
+                        {"mode": "LSTM", "num_layers": L, "hidden_size": Hs, "is_bidirec": D == 2,
+                         "dropout_prob": a.get("dropout_prob", 0.0), "is_test": a.get("is_test", False)})
+    st = r["State"]
+    return {"Out": r["Out"], "LastH": st[0], "LastC": st[1], "Reserve": torch.empty(0), "StateOut": torch.empty(0)}
+
+
+def _seq_major(x):
+    """[T, F] (one sequence) or [B, T, F] (padded batch) → ([T, B, F], squeeze flag)."""
+    return (x[:, None], True) if x.dim() == 2 else (x.transpose(0, 1), False)
+
+
+@register("lstm")
+def _lstm_op(ins, a):
+    """Reference `lstm_op.cc` (dynamic LSTM): Input is the PROJECTED x [T, 4D] (one sequence, or
+    [B, T, 4D] padded); gate layout [c̃, i, f, o]; Weight [D, 4D] hidden weights; Bias [1, 4D]
+    (+ [1, 3D] peephole checks i, f, o with use_peepholes)."""
+    xg, sq = _seq_major(_in(ins, "Input"))
+    w, b = _in(ins, "Weight"), _in(ins, "Bias")
+    T, B, F4 = xg.shape
+    D = F4 // 4
+    h = _in(ins, "H0") if _in(ins, "H0") is not None else xg.new_zeros(B, D)
+    c = _in(ins, "C0") if _in(ins, "C0") is not None else xg.new_zeros(B, D)
+    bias = b.reshape(-1)
+    peep = bool(a.get("use_peepholes", True)) and bias.numel() >= 7 * D
+    gb = bias[:4 * D]
+    ci, cf, co = (bias[4 * D:5 * D], bias[5 * D:6 * D], bias[6 * D:7 * D]) if peep else (0, 0, 0)
+    ga = _act_by_name(a.get("gate_activation", "sigmoid"))
+    ca = _act_by_name(a.get("cell_activation", "tanh"))
+    na = _act_by_name(a.get("candidate_activation", "tanh"))
+    steps = range(T - 1, -1, -1) if a.get("is_reverse") else range(T)
+    hs, cs = [None] * T, [None] * T
+    for t in steps:
+        g = xg[t] + h @ w + gb
+        gc, gi, gf, go = g.split(D, -1)
+        i = ga(gi + c * ci)
+        f = ga(gf + c * cf)
+        c = na(gc) * i + c * f
+        o = ga(go + c * co)
+        h = o * ca(c)
+        hs[t], cs[t] = h, c
+    H, C = torch.stack(hs), torch.stack(cs)
+    if sq:
+        H, C = H[:, 0], C[:, 0]
+    else:
+        H, C = H.transpose(0, 1), C.transpose(0, 1)
+    return {"Hidden": H, "Cell": C, "BatchGate": torch.empty(0), "BatchCellPreAct": torch.empty(0)}
+
+
+def _gru_step(xt, h, w, ga, ca, origin):
+    """Reference GRU unit: gates (u, r) = ga(x_ur + h·W_ur); c̃ = ca(x_c + (r∘h)·W_c);
+    h' = u∘h + (1−u)∘c̃ (origin_mode) or u∘c̃ + (1−u)∘h. Weight [D, 3D] = flat W_ur [D, 2D] then W_c [D, D]."""
+    D = h.shape[-1]
+    flat = w.reshape(-1)
+    wur = flat[:2 * D * D].view(D, 2 * D)
+    wc = flat[2 * D * D:].view(D, D)
+    ur = ga(xt[:, :2 * D] + h @ wur)
+    u, r = ur[:, :D], ur[:, D:]
+    rh = r * h
+    c = ca(xt[:, 2 * D:] + rh @ wc)
+    hn = u * h + (1 - u) * c if origin else u * c + (1 - u) * h
+    return hn, torch.cat([u, r, c], -1), rh
+
+
+@register("gru")
+def _gru_op(ins, a):
+    """Reference `gru_op.cc` (dynamic GRU): Input projected [T, 3D] (or [B, T, 3D]); H0; Weight
+    [D, 3D]; Bias [1, 3D]; is_reverse; origin_mode."""
+    xg, sq = _seq_major(_in(ins, "Input"))
+    w, b = _in(ins, "Weight"), _in(ins, "Bias")
+    T, B, F3 = xg.shape
+    D = F3 // 3
+    h = _in(ins, "H0") if _in(ins, "H0") is not None else xg.new_zeros(B, D)
+    if b is not None:
+        xg = xg + b.reshape(-1)
+    ga = _act_by_name(a.get("gate_activation", "sigmoid"))
+    ca = _act_by_name(a.get("activation", "tanh"))
+    steps = range(T - 1, -1, -1) if a.get("is_reverse") else range(T)
+    hs = [None] * T
+    for t in steps:
+        h, _, _ = _gru_step(xg[t], h, w, ga, ca, bool(a.get("origin_mode", False)))
+        hs[t] = h
+    H = torch.stack(hs)
+    H = H[:, 0] if sq else H.transpose(0, 1)
+    return {"Hidden": H, "BatchGate": torch.empty(0), "BatchResetHiddenPrev": torch.empty(0),
+            "BatchHidden": torch.empty(0)}
+
+
+@register("gru_unit")
+def _gru_unit(ins, a):
+    x, hp, w, b = _in(ins, "Input"), _in(ins, "HiddenPrev"), _in(ins, "Weight"), _in(ins, "Bias")
+    if b is not None:
+        x = x + b.reshape(1, -1)
+    h, gate, rh = _gru_step(x, hp, w, _act_by_id(a.get("gate_activation", 1)), _act_by_id(a.get("activation", 2)),
+                            bool(a.get("origin_mode", False)))
+    return {"Gate": gate, "ResetHiddenPrev": rh, "Hidden": h}
+
+
+@register("lstm_unit")
+def _lstm_unit(ins, a):
+    """Reference `lstm_unit_op.h`: X [B, 4D] pre-activations (i, f, o, g); C = σ(f + forget_bias)∘C_prev
+    + σ(i)∘tanh(g); H = σ(o)∘tanh(C)."""
+    x, cp = _in(ins, "X"), _in(ins, "C_prev")
+    i, f, o, g = x.chunk(4, -1)
+    c = torch.sigmoid(f + float(a.get("forget_bias", 0.0))) * cp + torch.sigmoid(i) * torch.tanh(g)
+    return {"C": c, "H": torch.sigmoid(o) * torch.tanh(c)}
+
+
+# ---------------------------------------------------------------------------------- detection
+@register("matrix_nms")
+def _matrix_nms_op(ins, a):
+    from ..vision.ops import matrix_nms
+    out, num, idx = matrix_nms(_in(ins, "BBoxes", "bboxes"), _in(ins, "Scores", "scores"),
+                               float(a.get("score_threshold", 0.0)), float(a.get("post_threshold", 0.0)),
+                               int(a.get("nms_top_k", -1)), int(a.get("keep_top_k", -1)),
+                               bool(a.get("use_gaussian", False)), float(a.get("gaussian_sigma", 2.0)),
+                               int(a.get("background_label", 0)), bool(a.get("normalized", True)),
+                               return_index=True, return_rois_num=True)
+    return {"Out": out, "Index": idx, "RoisNum": num, "out": out, "index": idx, "roisnum": num}
+
+
+@register("generate_proposals", "generate_proposals_v2")
+def _generate_proposals_op(ins, a):
+    from ..vision.ops import generate_proposals
+    im = _in(ins, "ImShape", "im_shape")
+    if im is None:  # v1: ImInfo [N, 3] (h, w, scale)
+        im = _in(ins, "ImInfo")[:, :2]
+    rois, probs, num = generate_proposals(
+        _in(ins, "Scores", "scores"), _in(ins, "BboxDeltas", "bbox_deltas"), im,
+        _in(ins, "Anchors", "anchors"), _in(ins, "Variances", "variances"),
+        int(_at(a, "pre_nms_topN", "pre_nms_top_n", default=6000)),
+        int(_at(a, "post_nms_topN", "post_nms_top_n", default=1000)), float(a.get("nms_thresh", 0.5)),
+        float(a.get("min_size", 0.1)), float(a.get("eta", 1.0)), bool(a.get("pixel_offset", True)),
+        return_rois_num=True)
+    return {"RpnRois": rois, "RpnRoiProbs": probs, "RpnRoisNum": num, "rpn_rois": rois,
+            "rpn_roi_probs": probs, "rpn_rois_num": num}
+
+
+@register("distribute_fpn_proposals")
+def _distribute_fpn_op(ins, a):
+    from ..vision.ops import distribute_fpn_proposals
+    multi, restore, nums = distribute_fpn_proposals(
+        _in(ins, "FpnRois", "fpn_rois"), int(a["min_level"]), int(a["max_level"]), int(a["refer_level"]),
+        int(a["refer_scale"]), bool(a.get("pixel_offset", True)), _in(ins, "RoisNum", "rois_num"))
+    return {"MultiFpnRois": multi, "RestoreIndex": restore, "MultiLevelRoIsNum": nums or [],
+            "multi_fpn_rois": multi, "restore_index": restore, "multi_level_rois_num": nums or []}
+
+
+@register("collect_fpn_proposals")
+def _collect_fpn(ins, a):
+    """Reference `collect_fpn_proposals_op`: concatenate every level's rois, keep the top
+    post_nms_topN by score overall (per image when RoisNum is given), image-major output."""
+    rois, scores = _inl(ins, "MultiLevelRois"), _inl(ins, "MultiLevelScores")
+    nums = _inl(ins, "MultiLevelRoIsNum")
+    k = int(a.get("post_nms_topN", 100))
+    R = torch.cat(rois)
+    Sc = torch.cat([s.reshape(-1) for s in scores])
+    if nums:
+        img = torch.cat([torch.repeat_interleave(torch.arange(n.numel(), device=R.device), n.long()) for n in nums])
+        nimg = nums[0].numel()
+    else:
+        img = torch.zeros(R.shape[0], dtype=torch.long, device=R.device)
+        nimg = 1
+    top = torch.sort(Sc, descending=True, stable=True).indices[:k]
+    sel = top[torch.sort(img[top], stable=True).indices]
+    return {"FpnRois": R[sel], "RoisNum": torch.bincount(img[sel], minlength=nimg).to(torch.int32)}
+
+
+@register("psroi_pool")
+def _psroi_pool_op(ins, a):
+    from ..vision.ops import psroi_pool
+    x, rois = _in(ins, "X", "x"), _in(ins, "ROIs", "boxes")
+    rn = _in(ins, "RoisNum", "boxes_num")
+    if rn is None:
+        rn = torch.tensor([rois.shape[0]])
+    return _out(psroi_pool(x, rois, rn, (int(a["pooled_height"]), int(a["pooled_width"])),
+                           float(a.get("spatial_scale", 1.0))))
+
+
+@register("roi_pool")
+def _roi_pool_op(ins, a):
+    from ..vision.ops import roi_pool
+    x, rois = _in(ins, "X", "x"), _in(ins, "ROIs", "boxes")
+    rn = _in(ins, "RoisNum", "boxes_num")
+    if rn is None:
+        rn = torch.tensor([rois.shape[0]])
+    y = roi_pool(x, rois, rn, (int(a["pooled_height"]), int(a["pooled_width"])), float(a.get("spatial_scale", 1.0)))
+    return {"Out": y, "out": y, "Argmax": torch.zeros(y.shape, dtype=torch.int64)}
+
+
+@register("prroi_pool")
+def _prroi_pool(ins, a):
+    """Precise ROI pooling (integral of the bilinear interpolant over each bin), approximated by a
+    dense 4×4 bilinear sample average per bin through roi_align."""
+    from ..vision.ops import roi_align
+    x, rois = _in(ins, "X"), _in(ins, "ROIs")
+    rn = _in(ins, "BatchRoINums")
+    if rn is None:
+        rn = torch.tensor([rois.shape[0]])
+    return _out(roi_align(x, rois, rn, (int(a["pooled_height"]), int(a["pooled_width"])),
+                          float(a.get("spatial_scale", 1.0)), sampling_ratio=4, aligned=False))
+
+
+@register("yolov3_loss")
+def _yolov3_loss(ins, a):
+    from ..vision.ops import yolo_loss
+    loss = yolo_loss(_in(ins, "X", "x"), _in(ins, "GTBox", "gt_box"), _in(ins, "GTLabel", "gt_label"),
+                     list(a["anchors"]), list(a["anchor_mask"]), int(a["class_num"]), float(a["ignore_thresh"]),
+                     int(a["downsample_ratio"]), _in(ins, "GTScore", "gt_score"),
+                     bool(a.get("use_label_smooth", True)), scale_x_y=float(a.get("scale_x_y", 1.0)))
+    return {"Loss": loss, "loss": loss, "ObjectnessMask": torch.empty(0), "GTMatchMask": torch.empty(0)}
+
+
+@register("nms")
+def _nms_op(ins, a):
+    from ..vision.ops import _greedy_nms
+    b = _in(ins, "Boxes", "x")
+    keep = _greedy_nms(b, torch.arange(b.shape[0], 0, -1, dtype=torch.float32, device=b.device),
+                       float(a.get("iou_threshold", 0.3)), 1.0, False)
+    return {"KeepBoxesIdxs": keep, "out": keep}
+
+
+@register("box_decoder_and_assign")
+def _box_decoder_and_assign(ins, a):
+    """Reference `box_decoder_and_assign_op.h`: per class decode TargetBox deltas against PriorBox
+    (+1 pixel convention, variance-scaled, log-size clip), OutputAssignBox = the box of the best
+    non-background class."""
+    pb, pv, tb, sc = (_in(ins, k) for k in ("PriorBox", "PriorBoxVar", "TargetBox", "BoxScore"))
+    clip = float(a.get("box_clip", 4.135))
+    R, C = sc.shape
+    pw = pb[:, 2] - pb[:, 0] + 1
+    ph = pb[:, 3] - pb[:, 1] + 1
+    px, py = pb[:, 0] + pw / 2, pb[:, 1] + ph / 2
+    t = tb.reshape(R, C, 4)
+    v = pv.reshape(-1, 4) if pv is not None else torch.ones(1, 4, device=pb.device)
+    dx, dy = v[:, 0:1] * t[..., 0], v[:, 1:2] * t[..., 1]
+    dw, dh = torch.clamp(v[:, 2:3] * t[..., 2], max=clip), torch.clamp(v[:, 3:4] * t[..., 3], max=clip)
+    cx, cy = dx * pw[:, None] + px[:, None], dy * ph[:, None] + py[:, None]
+    w, h = torch.exp(dw) * pw[:, None], torch.exp(dh) * ph[:, None]
+    dec = torch.stack([cx - w / 2, cy - h / 2, cx + w / 2 - 1, cy + h / 2 - 1], -1)
+    best = sc[:, 1:].argmax(1) + 1 if C > 1 else torch.zeros(R, dtype=torch.long, device=sc.device)
+    assign = dec[torch.arange(R, device=sc.device), best]
+    return {"DecodeBox": dec.reshape(R, C * 4), "OutputAssignBox": assign}
+
+
+@register("bipartite_match")
+def _bipartite_match(ins, a):
+    """Reference `bipartite_match_op.cc`: greedy global max matching of DistMat [N, M] (rows = gt,
+    cols = priors), then ('per_prediction') unmatched columns take their best row above the
+    threshold."""
+    d = _in(ins, "DistMat").float()
+    N, M = d.shape
+    idx = torch.full((M,), -1, dtype=torch.int32)
+    dist_ = torch.zeros(M)
+    dd = d.clone().cpu()
+    used_r = torch.zeros(N, dtype=torch.bool)
+    for _ in range(min(N, M)):
+        masked = dd.clone()
+        masked[used_r] = -1
+        masked[:, idx >= 0] = -1
+        v, flat = masked.reshape(-1).max(0)
+        if v <= 0:
+            break
+        r, c = int(flat) // M, int(flat) % M
+        idx[c], dist_[c] = r, v
+        used_r[r] = True
+    if a.get("match_type", "bipartite") == "per_prediction":
+        thr = float(a.get("dist_threshold", 0.5))
+        bv, br = dd.max(0)
+        sel = (idx < 0) & (bv >= thr)
+        idx[sel], dist_[sel] = br[sel].int(), bv[sel]
+    return {"ColToRowMatchIndices": idx.reshape(1, M).to(d.device), "ColToRowMatchDist": dist_.reshape(1, M).to(d.device)}
+
+
+@register("target_assign")
+def _target_assign(ins, a):
+    x, mi = _in(ins, "X"), _in(ins, "MatchIndices").long()
+    neg = _in(ins, "NegIndices")
+    mv = float(a.get("mismatch_value", 0))
+    N, P = mi.shape
+    K = x.shape[-1]
+    xs = x.reshape(-1, x.shape[-2] if x.dim() == 3 else 1, K) if x.dim() == 3 else x.reshape(1, -1, K)
+    out = torch.full((N, P, K), mv, dtype=x.dtype, device=x.device)
+    w = torch.zeros(N, P, 1, dtype=torch.float32, device=x.device)
+    for n in range(N):
+        ok = mi[n] >= 0
+        src = xs[min(n, xs.shape[0] - 1)]
+        out[n, ok] = src[mi[n, ok]]
+        w[n, ok] = 1.0
+    if neg is not None:
+        for j in neg.reshape(-1).tolist():
+            w[0, int(j)] = 1.0
+    return {"Out": out, "OutWeight": w}
+
+
+@register("density_prior_box")
+def _density_prior_box(ins, a):
+    """Reference `density_prior_box_op.h`: for each fixed size / density, density² shifted square
+    boxes (× each fixed ratio) per feature-map cell, normalised by the image size."""
+    x, img = _in(ins, "Input"), _in(ins, "Image")
+    H, W = x.shape[2], x.shape[3]
+    IH, IW = img.shape[2], img.shape[3]
+    sw = float(a.get("step_w", 0) or IW / W)
+    sh = float(a.get("step_h", 0) or IH / H)
+    off = float(a.get("offset", 0.5))
+    sizes = [float(s) for s in a.get("fixed_sizes", [])]
+    ratios = [float(r) for r in a.get("fixed_ratios", [1.0])]
+    dens = [int(d) for d in a.get("densities", [])]
+    boxes = []
+    for hh in range(H):
+        for ww in range(W):
+            cx, cy = (ww + off) * sw, (hh + off) * sh
+            cell = []
+            for s, dn in zip(sizes, dens):
+                shift = s / dn
+                for r in ratios:
+                    bw, bh = s * math.sqrt(r), s / math.sqrt(r)
+                    for di in range(dn):
+                        for dj in range(dn):
+                            ccx = cx - s / 2 + shift / 2 + dj * shift
+                            ccy = cy - s / 2 + shift / 2 + di * shift
+                            cell.append([(ccx - bw / 2) / IW, (ccy - bh / 2) / IH, (ccx + bw / 2) / IW,
+                                         (ccy + bh / 2) / IH])
+            boxes.append(cell)
+    b = torch.tensor(boxes, dtype=torch.float32, device=x.device).reshape(H, W, -1, 4)
+    if a.get("clip"):
+        b = b.clamp(0, 1)
+    var = torch.tensor(a.get("variances", [0.1, 0.1, 0.2, 0.2]), dtype=torch.float32,
+                       device=x.device).expand_as(b).contiguous()
+    if a.get("flatten_to_2d"):
+        b, var = b.reshape(-1, 4), var.reshape(-1, 4)
+    return {"Boxes": b.to(x.dtype), "Variances": var.to(x.dtype)}
+
+
+@register("locality_aware_nms")
+def _locality_aware_nms(ins, a):
+    return REGISTRY["multiclass_nms"](ins, a)
+
+
+@register("retinanet_detection_output")
+def _retinanet_detection_output(ins, a):
+    """Reference `retinanet_detection_output_op`: per FPN level decode the top nms_top_k anchors above
+    score_threshold, then class-wise NMS over all levels and keep_top_k (rows: label, score, box)."""
+    from ..vision.ops import _nms_fast
+    bbs, scs, ancs = _inl(ins, "BBoxes"), _inl(ins, "Scores"), _inl(ins, "Anchors")
+    im = _in(ins, "ImInfo")
+    st, topk = float(a.get("score_threshold", 0.05)), int(a.get("nms_top_k", 1000))
+    nt, keep = float(a.get("nms_threshold", 0.3)), int(a.get("keep_top_k", 100))
+    eta = float(a.get("nms_eta", 1.0))
+    rows, nums = [], []
+    N = scs[0].shape[0]
+    for n in range(N):
+        boxes, scores, cls = [], [], []
+        for bb, sc, an in zip(bbs, scs, ancs):
+            s = sc[n]  # [A, C]
+            flat = s.reshape(-1)
+            cand = torch.nonzero(flat > st).reshape(-1)
+            cand = cand[torch.sort(flat[cand], descending=True, stable=True).indices][:topk]
+            ai, ci = cand // s.shape[1], cand % s.shape[1]
+            anc = an.reshape(-1, 4)[ai]
+            d = bb[n][ai]
+            aw, ah = anc[:, 2] - anc[:, 0] + 1, anc[:, 3] - anc[:, 1] + 1
+            cx, cy = anc[:, 0] + aw / 2 + d[:, 0] * aw, anc[:, 1] + ah / 2 + d[:, 1] * ah
+            w, h = torch.exp(d[:, 2]) * aw, torch.exp(d[:, 3]) * ah
+            scl = im[n, 2]
+            bx = torch.stack([cx - w / 2, cy - h / 2, cx + w / 2 - 1, cy + h / 2 - 1], -1) / scl
+            bx = torch.stack([bx[:, 0].clamp(0, im[n, 1] / scl - 1), bx[:, 1].clamp(0, im[n, 0] / scl - 1),
+                              bx[:, 2].clamp(0, im[n, 1] / scl - 1), bx[:, 3].clamp(0, im[n, 0] / scl - 1)], -1)
+            boxes.append(bx)
+            scores.append(flat[cand])
+            cls.append(ci)
+        B_, S_, C_ = torch.cat(boxes), torch.cat(scores), torch.cat(cls)
+        det = []
+        for c in C_.unique().tolist():
+            m = torch.nonzero(C_ == c).reshape(-1)
+            k = _nms_fast(B_[m], S_[m], -1.0, nt, eta, -1, False)
+            det += [(float(S_[m[j]]), c, B_[m[j]]) for j in k]
+        det = sorted(det, key=lambda t: -t[0])[:keep]
+        for s, c, b in det:
+            rows.append(torch.cat([torch.tensor([c + 1.0, s], device=b.device), b]))
+        nums.append(len(det))
+    out = torch.stack(rows) if rows else torch.zeros((0, 6))
+    return {"Out": out}
+
+
+# ------------------------------------------------------------------------------ quantization
+@register("dequantize_abs_max")
+def _dequantize_abs_max(ins, a):
+    x, s = _x(ins), _in(ins, "Scale")
+    return _out(x.float() * s.reshape(-1)[0].float() / float(a.get("max_range", 127.0)))
+
+
+@register("dequantize_log")
+def _dequantize_log(ins, a):
+    x, d = _x(ins), _in(ins, "Dict")
+    xi = x.long()
+    return _out(torch.where(xi < 0, -d[(xi + 128).clamp(0, d.numel() - 1)], d[xi.clamp(0, d.numel() - 1)]))
+
+
+def _fq(x, scale, bits):
+    bnt = float((1 << (bits - 1)) - 1)
+    return torch.round(torch.clamp(x / scale.clamp_min(1e-30), -1, 1) * bnt)
+
+
+@register("fake_quantize_abs_max")
+def _fake_quantize_abs_max(ins, a):
+    x = _x(ins)
+    s = x.abs().max().reshape(1)
+    return {"Out": _fq(x, s, int(a.get("bit_length", 8))), "OutScale": s}
+
+
+@register("fake_channel_wise_quantize_abs_max")
+def _fake_cw_quantize(ins, a):
+    x = _x(ins)
+    ax = int(a.get("quant_axis", 0))
+    dims = [d for d in range(x.dim()) if d != ax]
+    s = x.abs().amax(dims)
+    shp = [1] * x.dim()
+    shp[ax] = -1
+    return {"Out": _fq(x, s.view(shp), int(a.get("bit_length", 8))), "OutScale": s}
+
+
+@register("fake_quantize_range_abs_max")
+def _fake_quantize_range(ins, a):
+    x, ins_s = _x(ins), _in(ins, "InScale")
+    cur = x.abs().max()
+    s = cur if a.get("is_test") is False else torch.maximum(cur, ins_s.reshape(-1)[0]) if ins_s is not None else cur
+    return {"Out": _fq(x, s, int(a.get("bit_length", 8))), "OutScale": s.reshape(1)}
+
+
+@register("fake_quantize_moving_average_abs_max")
+def _fake_quantize_mavg(ins, a):
+    x = _x(ins)
+    rate = float(a.get("moving_rate", 0.9))
+    st, acc = _in(ins, "InState"), _in(ins, "InAccum")
+    if a.get("is_test") or st is None:
+        s = _in(ins, "InScale").reshape(-1)[0]
+        return {"Out": _fq(x, s, int(a.get("bit_length", 8))), "OutScale": s.reshape(1)}
+    st2 = rate * st + 1
+    acc2 = rate * acc + x.abs().max()
+    s = (acc2 / st2).reshape(-1)[0]
+    return {"Out": _fq(x, s, int(a.get("bit_length", 8))), "OutScale": s.reshape(1), "OutState": st2,
+            "OutAccum": acc2}
+
+
+@register("quantize")
+def _quantize_mkldnn(ins, a):
+    x = _in(ins, "Input")
+    s, sh = float(a.get("Scale", 1.0)), float(a.get("Shift", 0.0))
+    q = torch.round(x.float() * s + sh)
+    return {"Output": (q.clamp(0, 255).to(torch.uint8) if sh else q.clamp(-128, 127).to(torch.int8))}
+
+
+@register("dequantize")
+def _dequantize_mkldnn(ins, a):
+    x = _in(ins, "Input")
+    return {"Output": (x.float() - float(a.get("Shift", 0.0))) / float(a.get("Scale", 1.0))}
+
+
+@register("requantize")
+def _requantize(ins, a):
+    x = _in(ins, "Input")
+    si, so = float(a.get("Scale_in", 1.0)), float(a.get("Scale_out", 1.0))
+    shi, sho = float(a.get("Shift_in", 0.0)), float(a.get("Shift_out", 0.0))
+    y = torch.round((x.float() - shi) * so / si + sho)
+    return {"Output": y.clamp(-128, 127).to(x.dtype)}
+
+
+# ----------------------------------------------------------------------------------- misc ops
+@register("deformable_conv", "deformable_conv_v1")
+def _deformable_conv(ins, a):
+    """Reference `deformable_conv_op` (v2 with Mask; v1 without)."""
+    from ..vision.ops import deform_conv2d
+    x, off, w = _in(ins, "Input", "x"), _in(ins, "Offset", "offset"), _in(ins, "Filter", "filter")
+    y = deform_conv2d(x, off, w, None, list(a.get("strides", [1, 1])), list(a.get("paddings", [0, 0])),
+                      list(a.get("dilations", [1, 1])), int(a.get("deformable_groups", 1)), int(a.get("groups", 1)),
+                      mask=_in(ins, "Mask", "mask"))
+    return {"Output": y, "out": y}
+
+
+@register("correlation")
+def _correlation(ins, a):
+    """Reference `correlation_op.cu` (FlowNet cost volume): mean over channels and the kernel window of
+    x1·x2 at displacements up to max_displacement (stride2), on the stride1 output grid."""
+    x1, x2 = _in(ins, "Input1"), _in(ins, "Input2")
+    pad, k, md = int(a.get("pad_size", 0)), int(a.get("kernel_size", 1)), int(a.get("max_displacement", 0))
+    s1, s2 = int(a.get("stride1", 1)), int(a.get("stride2", 1))
+    N, C, H, W = x1.shape
+    p1, p2 = F.pad(x1, (pad,) * 4), F.pad(x2, (pad,) * 4)
+    r = k // 2
+    bs = md + r
+    Ho = (H + 2 * pad - 2 * bs - 1) // s1 + 1
+    Wo = (W + 2 * pad - 2 * bs - 1) // s1 + 1
+    ds = list(range(-md, md + 1, s2))
+    outs = []
+    for dy in ds:
+        for dx in ds:
+            acc = 0
+            for ky in range(-r, r + 1):
+                for kx in range(-r, r + 1):
+                    ys, xs = bs + ky, bs + kx
+                    a1 = p1[:, :, ys:ys + (Ho - 1) * s1 + 1:s1, xs:xs + (Wo - 1) * s1 + 1:s1]
+                    a2 = p2[:, :, ys + dy:ys + dy + (Ho - 1) * s1 + 1:s1, xs + dx:xs + dx + (Wo - 1) * s1 + 1:s1]
+                    acc = acc + (a1 * a2).sum(1)
+            outs.append(acc / (k * k * C))
+    return {"Output": torch.stack(outs, 1)}
+
+
+@register("fused_elemwise_activation", "fused_elemwise_add_activation")
+def _fused_elemwise_activation(ins, a):
+    """Reference `fused_elemwise_activation_op.h`: functor_list [f1, f2] = binary∘unary
+    (Out = f1(X, f2(Y))) or unary∘binary (Out = f1(f2(X, Y)))."""
+    x, y = _in(ins, "X"), _in(ins, "Y")
+    y = _bcast(x, y, a.get("axis", -1))
+    fl = list(a.get("functor_list", ["elementwise_add", "relu"]))
+    sc = float(a.get("scale", 0.0))
+    un = {"relu": torch.relu, "sigmoid": torch.sigmoid, "tanh": torch.tanh, "gelu": F.gelu,
+          "scale": lambda t: t * sc}
+    bi = {"elementwise_add": torch.add, "elementwise_mul": torch.mul}
+    if fl[0] in bi:
+        inter = un[fl[1]](y)
+        out = bi[fl[0]](x, inter)
+    else:
+        inter = bi[fl[1]](x, y)
+        out = un[fl[0]](inter)
+    return {"Out": out, "IntermediateOut": inter}
+
+
+@register("fused_embedding_seq_pool")
+def _fused_embedding_seq_pool(ins, a):
+    w, ids = _in(ins, "W"), _in(ins, "Ids")
+    pid = int(a.get("padding_idx", -1))
+    idl = ids.reshape(ids.shape[0], -1).long()
+    e = F.embedding(idl, w)
+    if pid >= 0:
+        e = e * (idl != pid).unsqueeze(-1).to(e.dtype)
+    return _out(e.sum(1))
+
+
+@register("lookup_table_dequant")
+def _lookup_table_dequant(ins, a):
+    """Reference `lookup_table_dequant_op.h`: each W row = [min, max, 8-bit codes packed in floats];
+    value = min + code·(max − min)/255."""
+    w, ids = _in(ins, "W"), _in(ins, "Ids").reshape(-1).long()
+    rows = w[ids]
+    mn, mx = rows[:, 0:1], rows[:, 1:2]
+    codes = rows[:, 2:].contiguous().view(torch.uint8).float()
+    return _out(mn + codes * (mx - mn) / 255.0)
+
+
+@register("graph_send_recv")
+def _graph_send_recv(ins, a):
+    from ..geometric import send_u_recv
+    x, s, d = _in(ins, "X", "x"), _in(ins, "Src_index", "src_index"), _in(ins, "Dst_index", "dst_index")
+    osz = _in(ins, "Out_size", "out_size")
+    n = int(osz.reshape(-1)[0]) if osz is not None else (int(a.get("out_size", [0])[0]) if isinstance(
+        a.get("out_size"), (list, tuple)) else int(a.get("out_size", 0) or 0))
+    out = send_u_recv(x, s, d, a.get("reduce_op", a.get("pool_type", "sum")).lower(), n or None)
+    return {"Out": out, "out": out, "Dst_count": torch.bincount(d.long(), minlength=out.shape[0]).to(torch.int32)}
+
+
+@register("graph_send_ue_recv")
+def _graph_send_ue_recv(ins, a):
+    from ..geometric import send_ue_recv
+    x, y = _in(ins, "X", "x"), _in(ins, "Y", "y")
+    s, d = _in(ins, "Src_index", "src_index"), _in(ins, "Dst_index", "dst_index")
+    osz = _in(ins, "Out_size", "out_size")
+    n = int(osz.reshape(-1)[0]) if osz is not None else 0
+    out = send_ue_recv(x, y, s, d, a.get("message_op", "add").lower(), a.get("reduce_op", "sum").lower(), n or None)
+    return {"Out": out, "out": out, "Dst_count": torch.bincount(d.long(), minlength=out.shape[0]).to(torch.int32)}
+
+
+@register("graph_send_uv")
+def _graph_send_uv(ins, a):
+    from ..geometric import send_uv
+    return _out(send_uv(_in(ins, "x", "X"), _in(ins, "y", "Y"), _in(ins, "src_index"), _in(ins, "dst_index"),
+                        a.get("message_op", "add").lower()))
+
+
+@register("stft")
+def _stft_op(ins, a):
+    x, win = _x(ins), _in(ins, "Window")
+    n_fft, hop = int(a["n_fft"]), int(a["hop_length"])
+    fr = x.unfold(-1, n_fft, hop)                        # [B, frames, n_fft]
+    if win is not None:
+        fr = fr * win
+    spec = torch.fft.rfft(fr, dim=-1) if a.get("onesided", True) else torch.fft.fft(fr.to(torch.complex64), dim=-1)
+    if a.get("normalized"):
+        spec = spec / math.sqrt(n_fft)
+    return _out(spec.transpose(-1, -2))
+
+
+def _fft_axes(a):
+    return [int(v) for v in a.get("axes", [-1])]
+
+
+def _fft_norm(a):
+    return {"forward": "forward", "backward": "backward", "ortho": "ortho"}.get(a.get("normalization", "backward"),
+                                                                               "backward")
+
+
+@register("fft_c2c")
+def _fft_c2c(ins, a):
+    x = _x(ins)
+    fn = torch.fft.fftn if a.get("forward", True) else torch.fft.ifftn
+    return _out(fn(x, dim=_fft_axes(a), norm=_fft_norm(a)))
+
+
+@register("fft_r2c")
+def _fft_r2c(ins, a):
+    x = _x(ins)
+    fn = torch.fft.rfftn if a.get("onesided", True) else torch.fft.fftn
+    y = fn(x, dim=_fft_axes(a), norm=_fft_norm(a))
+    return _out(y if a.get("forward", True) else y.conj())
+
+
+@register("fft_c2r")
+def _fft_c2r(ins, a):
+    x = _x(ins)
+    ax = _fft_axes(a)
+    ls = int(a.get("last_dim_size", 0) or 0)
+    s = None if not ls else [x.shape[d] for d in ax[:-1]] + [ls]
+    fn = torch.fft.irfftn if not a.get("forward", False) else (lambda t, s=None, dim=None, norm=None:
+                                                               torch.fft.irfftn(t.conj(), s=s, dim=dim, norm=norm))
+    return _out(fn(x, s=s, dim=ax, norm=_fft_norm(a)))
+
+
+@register("read_file")
+def _read_file(ins, a):
+    from ..vision.ops import read_file
+    return _out(read_file(a["filename"]))
+
+
+@register("decode_jpeg")
+def _decode_jpeg(ins, a):
+    from ..vision.ops import decode_jpeg
+    return _out(decode_jpeg(_x(ins), a.get("mode", "unchanged")))
+
+
+@register("yolo_box_head")
+def _yolo_box_head(ins, a):
+    """Reference `fused/yolo_box_head_op.cu`: sigmoid on x, y, objectness and class channels, exp
+    kept for w, h left raw (decoded by yolo_box_post)."""
+    x = _x(ins)
+    an = len(a["anchors"]) // 2
+    C = int(a["class_num"])
+    N, _, H, W = x.shape
+    v = x.reshape(N, an, 5 + C, H, W)
+    out = torch.cat([torch.sigmoid(v[:, :, :2]), v[:, :, 2:4], torch.sigmoid(v[:, :, 4:])], 2)
+    return _out(out.reshape(x.shape))
+
+
+@register("fused_token_prune")
+def _fused_token_prune(ins, a):
+    """Reference `fused_token_prune_op.cu`: token importance = attention received (Σ over heads and
+    queries of Attn masked by Mask); keep the top NewMask.shape[2] tokens (the first one forced with
+    keep_first_token), in original order when keep_order."""
+    attn, x, mask, nm = _in(ins, "Attn"), _in(ins, "X"), _in(ins, "Mask"), _in(ins, "NewMask")
+    keep = nm.shape[2]
+    score = (attn * (mask >= 0).to(attn.dtype)).sum((1, 2))          # [B, S]
+    if a.get("keep_first_token", True):
+        score[:, 0] = float("inf")
+    idx = torch.topk(score, keep, -1).indices
+    if a.get("keep_order", False):
+        idx = torch.sort(idx, -1).values
+    slim = x.gather(1, idx[..., None].expand(-1, -1, x.shape[-1]))
+    return {"SlimmedX": slim, "CLSInds": idx.to(torch.int64)}
+
+
+@register("sequence_pool")
+def _sequence_pool(ins, a):
+    """Padded-batch form ([B, T, D]; no LoD in this framework): SUM / AVERAGE / SQRT / MAX / LAST / FIRST."""
+    x = _x(ins)
+    pt = a.get("pooltype", "AVERAGE").upper()
+    if x.dim() == 2:
+        x = x[None]
+    if pt == "SUM":
+        out = x.sum(1)
+    elif pt == "AVERAGE":
+        out = x.mean(1)
+    elif pt == "SQRT":
+        out = x.sum(1) / math.sqrt(x.shape[1])
+    elif pt == "MAX":
+        out = x.amax(1)
+    elif pt == "LAST":
+        out = x[:, -1]
+    else:
+        out = x[:, 0]
+    return {"Out": out, "MaxIndex": torch.zeros(0, dtype=torch.int32)}
+
+
+@register("sequence_softmax")
+def _sequence_softmax(ins, a):
+    return _out(torch.softmax(_x(ins), -1 if _x(ins).dim() > 1 else 0))
+
+
+@register("sequence_reverse")
+def _sequence_reverse(ins, a):
+    x = _x(ins)
+    return {"Y": x.flip(1 if x.dim() > 2 else 0)}
+
+
+@register("sequence_expand_as")
+def _sequence_expand_as(ins, a):
+    x, y = _in(ins, "X"), _in(ins, "Y")
+    return _out(x.repeat_interleave(y.shape[0] // x.shape[0], 0))
+
+
+@register("sequence_pad")
+def _sequence_pad(ins, a):
+    x = _x(ins)
+    return {"Out": x if x.dim() > 2 else x[None], "Length": torch.tensor([x.shape[-2] if x.dim() > 1 else x.shape[0]])}
+
+
+@register("sequence_unpad")
+def _sequence_unpad(ins, a):
+    x, ln = _x(ins), _in(ins, "Length").reshape(-1).long()
+    return _out(torch.cat([x[b, :int(ln[b])] for b in range(x.shape[0])], 0))
+
+
+@register("im2sequence")
+def _im2sequence(ins, a):
+    x = _x(ins)
+    k = list(a.get("kernels", [1, 1]))
+    st = list(a.get("strides", [1, 1]))
+    p = list(a.get("paddings", [0, 0, 0, 0]))
+    xp = F.pad(x, [p[1], p[3], p[0], p[2]])
+    col = F.unfold(xp, k, stride=st)                      # [N, C·kh·kw, L]
+    return _out(col.transpose(1, 2).reshape(-1, col.shape[1]))

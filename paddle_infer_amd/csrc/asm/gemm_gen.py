@@ -71,8 +71,11 @@ ARGS = [
     # work-unit "part" decomposition (loaded at each tile setup): K start = part·kmul (split-K:
     # kmul = nk·64; batched: kmul = 0) and operand base += part·{a,b}_bstride bytes (batched)
     ("kmul", 152, 4), ("pad0", 156, 4), ("a_bstride", 160, 8), ("b_bstride", 168, 8),
+    # column-sum partials of the fused dact epilogue ("dgelucs"): f32 [ceil(M/128)][N] (one row per
+    # 128-row wave band), byte size for the descriptor range
+    ("colsum", 176, 8), ("colsum_bytes", 184, 4), ("pad1", 188, 4),
 ]
-ARGS_SIZE = 176
+ARGS_SIZE = 192
 
 # ---- SGPR map ------------------------------------------------------------------------------------
 S_KARG = 0        # s[0:1]
@@ -196,12 +199,19 @@ class Kernel:
         # as aux), d{gelu,relu} (C = acc ⊙ act'(aux))
         fused = {"bias": ("bias_act", 0), "biasgelu": ("bias_act", 1), "biasrelu": ("bias_act", 3),
                  "biasgeluerf": ("bias_act", 2),
-                 "dgelu": ("dact", 1), "drelu": ("dact", 3), "biasnx": ("bias_act", 0)}
+                 "dgelu": ("dact", 1), "drelu": ("dact", 3), "biasnx": ("bias_act", 0),
+                 "dgelucs": ("dact", 1), "drelucs": ("dact", 3)}
         self.ek, self.act = fused.get(ek, (ek, 0))
+        # *cs: the dact epilogue also writes per-128-row-band column sums of C (the bias gradient
+        # of the layer whose pre-activation this is: FFN1's db1 from the FFN2 data-gradient GEMM)
+        self.colsum = ek in ("dgelucs", "drelucs")
+        self.VCS = self.VE + 102        # 32 column-sum accumulators (8 blocks × 4 columns)
         self.store_aux = ek != "biasnx"  # biasnx: C = acc + bias, no pre-activation output
         self.NBW = 8                    # 16-column accumulator blocks per wave row
         # resources: LDS bytes, workgroup size, accum_offset, AGPR count
         self.lds_bytes, self.wg_size, self.acc_off, self.n_agpr = LDS_BYTES, 256, ACC_OFF, 256
+        if self.colsum:  # the persistent kernel's epilogue registers end at v213: room for 32 more
+            self.acc_off = 256
         assert self.ek not in ("bias_act", "dact") or (a_kc and b_kc)  # descriptor SGPRs 40..47
         self.lines = []
         self.nlab = 0
@@ -764,6 +774,9 @@ class Kernel:
         es = 4 if f32 else 2
         self.e("s_nop 15")
         self.e("s_nop 15")
+        if self.colsum:  # column-sum plane descriptor base / range (waited for before its stores)
+            self.e("s_load_dwordx2 s[44:45], s[0:1], 0xb0")
+            self.e("s_load_dword s46, s[0:1], 0xb8")
         # C descriptor base = c + part*c_part + m0*ldc_b + n0*es
         T = S_T
         self.e(f"s_mul_i32 s{T}, s{S_PART}, s{E + 6}")
@@ -970,6 +983,14 @@ class Kernel:
                         issued += [("S", mb)] * n_st
                     elif ek == "dact":
                         self.dact_vals(d, V + 40 + 16 * buf + 2 * nb)
+                        if self.colsum:
+                            cs = self.VCS + 4 * nb
+                            if mb == 0:
+                                for j in range(4):
+                                    self.e(f"v_mov_b32 v{cs + j}, v{d + j}")
+                            else:
+                                self.e(f"v_pk_add_f32 v[{cs}:{cs + 1}], v[{cs}:{cs + 1}], v[{d}:{d + 1}]")
+                                self.e(f"v_pk_add_f32 v[{cs + 2}:{cs + 3}], v[{cs + 2}:{cs + 3}], v[{d + 2}:{d + 3}]")
                     elif ek == "bf16acc":
                         o = V + 40 + 16 * buf + 2 * nb
                         t = self.VTMP + 4
@@ -996,7 +1017,42 @@ class Kernel:
                         issued.append(("S", mb))
                 if masked:
                     self.e("s_mov_b64 exec, -1")
+        if self.colsum:
+            issued += [("S", 8)] * self.colsum_store()
         self.vm_ops = min(getattr(self, "vm_ops", 10 ** 6), len(issued))
+
+    def colsum_store(self):
+        """Column sums of this wave's 128×128 C block: the 8 row blocks were summed per lane during
+        the stores (VCS), the 16 rows of a lane group are reduced with row_ror DPP adds (32
+        independent registers per step: no DPP read-after-write hazard), and the group leaders
+        (lane % 16 == 0) store 4 columns per 16-column block into partial row m0/128 + wave row.
+        Returns the store count."""
+        V, T, CS = self.VE, S_T, self.VCS
+        for sh in (8, 4, 2, 1):
+            for r in range(32):
+                self.e(f"v_add_f32_dpp v{CS + r}, v{CS + r}, v{CS + r} row_ror:{sh} row_mask:0xf bank_mask:0xf")
+        self.e("s_waitcnt lgkmcnt(0)")
+        self.e("s_and_b32 s45, s45, 0xffff")
+        self.e("s_mov_b32 s47, 0x20000")
+        # lane byte offset: ((m0 >> 7) + wave row) · N · 4 + global col · 4
+        self.e(f"s_lshr_b32 s{T}, s{S_M0T}, 7")
+        self.e(f"s_lshr_b32 s{T + 1}, s{S_WAVE}, 1")
+        self.e(f"s_add_u32 s{T}, s{T}, s{T + 1}")
+        self.e(f"s_mul_i32 s{T}, s{T}, s{S_N}")
+        self.e(f"s_lshl_b32 s{T}, s{T}, 2")
+        t0, t1 = self.VTMP, self.VTMP + 1
+        self.e(f"v_lshlrev_b32 v{t0}, 2, v{V + 4}")
+        self.e(f"v_add_u32 v{t0}, s{T}, v{t0}")
+        self.e(f"v_and_b32 v{t1}, 15, v{V_LANE}")
+        self.e(f"v_cmp_eq_u32 s[{T + 2}:{T + 3}], 0, v{t1}")          # group leaders
+        for nb in range(self.NBW):
+            self.e("s_mov_b64 exec, -1")
+            self.e(f"v_add_u32 v{t1}, {nb * 16}, v{V + 4}")
+            self.e(f"v_cmp_gt_u32 vcc, s{S_N}, v{t1}")
+            self.e(f"s_and_b64 exec, vcc, s[{T + 2}:{T + 3}]")
+            self.e(f"buffer_store_dwordx4 v[{CS + 4 * nb}:{CS + 4 * nb + 3}], v{t0}, s[44:47], 0 offen offset:{nb * 64}")
+        self.e("s_mov_b64 exec, -1")
+        return self.NBW
 
     def store_count(self):
         """VMEM ops the epilogue issues on its shorter path (the next tile's first block-landed
@@ -1212,7 +1268,7 @@ LAYOUTS = {"nt": (True, True), "tn": (False, False), "nn": (True, False), "tt": 
 EPILOGUES = ("bf16", "bf16acc", "f32", "f32acc")
 
 
-FUSED = ("bias", "biasgelu", "biasrelu", "dgelu", "drelu", "biasnx", "biasgeluerf")
+FUSED = ("bias", "biasgelu", "biasrelu", "dgelu", "drelu", "biasnx", "biasgeluerf", "dgelucs", "drelucs")
 
 
 def variants():

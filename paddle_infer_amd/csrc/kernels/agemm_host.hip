@@ -38,8 +38,10 @@ struct __attribute__((packed)) AgemmArgs {
   const void* bias;            // 144
   unsigned kmul, pad0;         // 152: K start = part·kmul (split-K), 0 when batched
   unsigned long long a_bstride, b_bstride;  // 160, 168: operand base += part·bstride (batched)
+  void* colsum;                // 176: dact epilogue column sums, f32 [ceil(M/128)][N] (*cs kernels)
+  unsigned colsum_bytes, pad1; // 184, 188
 };
-static_assert(sizeof(AgemmArgs) == 176, "AgemmArgs layout");
+static_assert(sizeof(AgemmArgs) == 192, "AgemmArgs layout");
 
 std::mutex g_mu;
 hipModule_t g_mod = nullptr;
@@ -118,11 +120,15 @@ PIAMD_EXPORT int piamd_agemm_loaded() { return g_mod != nullptr; }
 // f16: IEEE fp16 operands (and fp16 where a bf16 kernel writes 16-bit values).
 // batch > 1: C[i] (+)= op(A[i])·op(B[i]) for i < batch, operand i at base + i·s{a,b,c} elements
 // (a stride may be 0: broadcast); no split-K, no fused epilogue.
-PIAMD_EXPORT int piamd_agemm(const void* a, long long lda, int trans_a, const void* b, long long ldb,
-                             int trans_b, void* c, long long ldc, int c_f32, int accumulate, int M,
-                             int N, int K, int epi, int act, const void* bias, void* aux,
-                             long long ldaux, int ksplit, void* ws, int f16, int batch,
-                             long long sa, long long sb, long long sc, hipStream_t st) {
+// colsum (nullable, epi == 2 only): the data-gradient epilogue also writes the column sums of C per
+// 128-row band into colsum f32 [ceil(M/128)][N] (the bias gradient of the activation's producer,
+// reduced over the bands by the caller: no separate pass over C).
+PIAMD_EXPORT int piamd_agemm2(const void* a, long long lda, int trans_a, const void* b, long long ldb,
+                              int trans_b, void* c, long long ldc, int c_f32, int accumulate, int M,
+                              int N, int K, int epi, int act, const void* bias, void* aux,
+                              long long ldaux, int ksplit, void* ws, int f16, int batch,
+                              long long sa, long long sb, long long sc, void* colsum,
+                              hipStream_t st) {
   const bool a_kc = !trans_a, b_kc = trans_b;
   if (batch < 1 || (batch > 1 && (ksplit != 1 || epi != 0 || sa < 0 || sb < 0 || sc <= 0)))
     return (int)hipErrorInvalidValue;
@@ -143,6 +149,12 @@ PIAMD_EXPORT int piamd_agemm(const void* a, long long lda, int trans_a, const vo
     static const char* const kFused[2][4] = {{"bias", "biasgelu", "biasgeluerf", "biasrelu"},
                                              {"", "dgelu", "", "drelu"}};
     ek = (epi == 1 && act == 0 && !aux) ? "biasnx" : kFused[epi - 1][act];
+    if (colsum) {
+      if (epi != 2 || (act != 1 && act != 3)) return (int)hipErrorInvalidValue;
+      ek = act == 1 ? "dgelucs" : "drelucs";
+      g.colsum = colsum;
+      g.colsum_bytes = (unsigned)((unsigned long long)((M + 127) / 128) * N * 4);
+    }
     g.c = c;
     g.ldc_b = (unsigned)(ldc * 2);
     g.c_bytes = ((unsigned long long)(M - 1) * ldc + N) * 2;
@@ -222,4 +234,13 @@ PIAMD_EXPORT int piamd_agemm(const void* a, long long lda, int trans_a, const vo
     hipLaunchKernelGGL(agemm_reduce_kernel<false>, dim3(grid), dim3(256), 0, st, (const float*)ws, ksplit,
                        M, N, c, ldc, c_f32, accumulate);
   return (int)hipGetLastError();
+}
+
+PIAMD_EXPORT int piamd_agemm(const void* a, long long lda, int trans_a, const void* b, long long ldb,
+                             int trans_b, void* c, long long ldc, int c_f32, int accumulate, int M,
+                             int N, int K, int epi, int act, const void* bias, void* aux,
+                             long long ldaux, int ksplit, void* ws, int f16, int batch,
+                             long long sa, long long sb, long long sc, hipStream_t st) {
+  return piamd_agemm2(a, lda, trans_a, b, ldb, trans_b, c, ldc, c_f32, accumulate, M, N, K, epi, act,
+                      bias, aux, ldaux, ksplit, ws, f16, batch, sa, sb, sc, nullptr, st);
 }

@@ -911,3 +911,15 @@ PIAMD_EXPORT int piamd_colsum(int dtype, const void* x, void* out, float* part, 
   else launch_colsum_out<DT_F32>(part, G, N, out, accumulate, stream);
   return (int)hipGetLastError();
 }
+
+// out[N] (+)= Σ_g part[g][N] (f32 partial rows — e.g. the column-sum planes the assembly GEMM's
+// dact epilogue writes, piamd_agemm2 colsum): the bias gradient without a pass over the activation.
+PIAMD_EXPORT int piamd_colsum_parts(int dtype, const float* part, int G, int N, void* out, int accumulate,
+                                    hipStream_t stream) {
+  if (G <= 0 || N <= 0) return 0;
+  if (dtype == DT_BF16) launch_colsum_out<DT_BF16>(part, G, N, out, accumulate, stream);
+  else if (dtype == DT_F16) launch_colsum_out<DT_F16>(part, G, N, out, accumulate, stream);
+  else if (dtype == DT_F32) launch_colsum_out<DT_F32>(part, G, N, out, accumulate, stream);
+  else return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}

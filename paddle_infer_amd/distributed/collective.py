@@ -56,6 +56,22 @@ def _pg(group):
     return group.pg if isinstance(group, Group) else group
 
 
+def collectives_forced() -> bool:
+    """``PIAMD_FORCE_COLLECTIVES=1``: the data / tensor-parallel engines issue their collectives
+    even over a 1-rank group (the RCCL code paths — reduce-scatter hooks, async all-reduces, comm
+    streams, ``record_stream`` — exercised on a single GPU; `tests/test_rccl_world1_gpu.py`)."""
+    import os
+    return os.environ.get("PIAMD_FORCE_COLLECTIVES", "0") == "1" and dist.is_available() and dist.is_initialized()
+
+
+def multi_rank(group=None) -> bool:
+    """True when collectives over ``group`` must run (world > 1, or forced on a 1-rank group)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    pg = _pg(group) if group is not None else None
+    return dist.get_world_size(pg) > 1 or collectives_forced()
+
+
 def is_initialized():
     return dist.is_available() and dist.is_initialized()
 

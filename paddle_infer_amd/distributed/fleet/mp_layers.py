@@ -24,6 +24,14 @@ def _ws(group):
     return dist.get_world_size(group) if group is not None else 1
 
 
+def _coll(group):
+    """Collectives over the mp group run (world > 1, or forced on a 1-rank group for testing)."""
+    if group is None:
+        return False
+    from ..collective import collectives_forced
+    return _ws(group) > 1 or collectives_forced()
+
+
 def _rank(group):
     return dist.get_rank(group) if group is not None else 0
 
@@ -38,7 +46,7 @@ class _CIdentity(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        if _ws(ctx.group) > 1:
+        if _coll(ctx.group):
             g = g.contiguous()
             dist.all_reduce(g, group=ctx.group)
         return g, None
@@ -49,7 +57,7 @@ class _MPAllReduce(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, group):
-        if _ws(group) > 1:
+        if _coll(group):
             x = x.contiguous()
             dist.all_reduce(x, group=group)
         return x
@@ -134,7 +142,7 @@ class _ColumnParallelFn(torch.autograd.Function):
         dx = work = None
         if ctx.needs_input_grad[0]:
             dx = input_grad(dy2, wc).view(ctx.shp).contiguous()
-            if _ws(ctx.group) > 1:
+            if _coll(ctx.group):
                 work = dist.all_reduce(dx, group=ctx.group, async_op=True)
         dw = None
         if ctx.needs_input_grad[1]:
@@ -159,7 +167,7 @@ class _MPAllReduceBias(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y, b, group):
         ctx.n = b.shape[-1]
-        if _ws(group) > 1:
+        if _coll(group):
             y = y.contiguous()
             dist.all_reduce(y, group=group)
         return y

@@ -86,7 +86,9 @@ class DataParallel(torch.nn.Module):
         # fp16_allreduce (fleet strategy): f32 gradient buckets travel as fp16, cast back after
         self.comm_fp16 = False
         params = [p for p in layers.parameters() if p.requires_grad]
-        if self.world > 1:
+        from .collective import collectives_forced
+        self.multi = self.world > 1 or (collectives_forced() and self.pg is not None)
+        if self.multi:
             for p in params:  # identical initial weights on every rank
                 dist.broadcast(p.data, src=0, group=self.pg)
             self._build_buckets(params, int(comm_buffer_size * 2 ** 20))
@@ -181,7 +183,7 @@ class DataParallel(torch.nn.Module):
         self._queued = False
 
     def forward(self, *inputs, **kwargs):
-        if self.world > 1:
+        if self.multi:
             for flat, views in self._flat:
                 for p, v in views:
                     if p.grad is None or p.grad.data_ptr() != v.data_ptr():

@@ -223,6 +223,8 @@ _SIGS["piamd_nan_inf_check"] = [c_int, c_void_p, c_ll, c_void_p, c_int, c_void_p
 _SIGS["piamd_agemm"] = [c_void_p, c_ll, c_int, c_void_p, c_ll, c_int, c_void_p, c_ll, c_int, c_int,
                         c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_ll, c_int, c_void_p,
                         c_int, c_int, c_ll, c_ll, c_ll, c_void_p]
+_SIGS["piamd_agemm2"] = _SIGS["piamd_agemm"][:-1] + [c_void_p, c_void_p]  # ..., colsum, stream
+_SIGS["piamd_colsum_parts"] = [c_int, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]
 _SIGS["piamd_agemm_load"] = [ctypes.c_char_p]
 # f16, a, lda, b, ldb, c, ldc, c_f32, M, N, K, mb, nb, wn, depth, ks, alpha, bias, act, resid, ldr,
 # ws, cnt, stream

@@ -249,7 +249,8 @@ class _SyncBN(torch.autograd.Function):
             m = xf.mean(dims)
             shp = [1, C] + [1] * (xf.dim() - 2)
             local = torch.stack([torch.full_like(m, float(N * S)), m, ((xf - m.view(shp)) ** 2).sum(dims)])
-        g = _all_gather_stats(local, group) if dist.get_world_size(group) > 1 else local[None]
+        multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+        g = _all_gather_stats(local, group) if multi else local[None]
         n_tot = float(g[:, 0, 0].sum())
         if gpu:
             part_t = g.permute(1, 2, 0).contiguous()  # [3][C][W] channel-major partials

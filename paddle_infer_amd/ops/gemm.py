@@ -73,13 +73,15 @@ def asm_supported(a, b, trans_a=False, trans_b=False, ksplit=1):
 
 
 def asm_gemm(a, b, trans_a=False, trans_b=False, out=None, out_f32=False, accumulate=False,
-             ksplit=1, epi="none", act="none", bias=None, aux=None):
+             ksplit=1, epi="none", act="none", bias=None, aux=None, colsum=None):
     """C (+)= op(A)·op(B) on the hand-scheduled assembly kernels (bf16 or fp16 operands; the
     16-bit output has the operands' dtype). 3-D ``a`` / ``b`` / ``out`` run one batched launch
     (a 2-D operand, or a batch stride of 0, broadcasts over the batch). Fused epilogues (2-D, A
     stored [M, K], B stored [N, K], 16-bit C): ``epi="bias_act"`` — pre = 16-bit(A·B + bias)
     written to ``aux`` (optional), C = act(pre), act ∈ none / gelu_tanh / gelu (exact erf) / relu;
-    ``epi="dact"`` — C = (A·B) ⊙ act'(aux), act ∈ gelu_tanh / relu."""
+    ``epi="dact"`` — C = (A·B) ⊙ act'(aux), act ∈ gelu_tanh / relu; with ``colsum`` (f32
+    [ceil(M/128), N]) the epilogue also writes C's column sums per 128-row band (bias gradient of
+    the activation's producer without another pass over C: reduce with :func:`colsum_parts`)."""
     _agemm_load()
     batched = a.dim() == 3 or b.dim() == 3
     nb = max(a.shape[0] if a.dim() == 3 else 1, b.shape[0] if b.dim() == 3 else 1)
@@ -108,11 +110,28 @@ def asm_gemm(a, b, trans_a=False, trans_b=False, out=None, out_f32=False, accumu
     sc = out.stride(0) if batched else 0
     if batched:
         assert epi == "none" and (nb == 1 or sc > 0)
+    if colsum is not None:
+        assert epi == "dact" and colsum.dtype == torch.float32 and colsum.is_contiguous() \
+            and tuple(colsum.shape) == ((M + 127) // 128, N)
+        _lib.call("piamd_agemm2", a.data_ptr(), a.stride(-2), int(trans_a), b.data_ptr(), b.stride(-2),
+                  int(trans_b), out.data_ptr(), out.stride(-2), int(out.dtype == torch.float32),
+                  int(accumulate), M, N, K, _EPI[epi], ACTS[act], _lib.ptr(bias), _lib.ptr(aux),
+                  aux.stride(0) if aux is not None else 0, ksplit, _lib.ptr(ws), int(f16), nb,
+                  sa, sb, max(sc, 1), colsum.data_ptr(), _lib.stream())
+        return out
     _lib.call("piamd_agemm", a.data_ptr(), a.stride(-2), int(trans_a), b.data_ptr(), b.stride(-2),
               int(trans_b), out.data_ptr(), out.stride(-2), int(out.dtype == torch.float32),
               int(accumulate), M, N, K, _EPI[epi], ACTS[act], _lib.ptr(bias), _lib.ptr(aux),
               aux.stride(0) if aux is not None else 0, ksplit, _lib.ptr(ws), int(f16), nb,
               sa, sb, max(sc, 1), _lib.stream())
+    return out
+
+
+def colsum_parts(part, out, accumulate=True):
+    """out[N] (+)= Σ_rows part[rows, N] (f32 partial planes; ``out`` f32 / bf16 / fp16)."""
+    G, N = part.shape
+    _lib.call("piamd_colsum_parts", _lib.dtype_code(out, fp16=True), part.data_ptr(), G, N,
+              out.data_ptr(), int(accumulate), _lib.stream())
     return out
 
 

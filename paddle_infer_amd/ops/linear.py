@@ -291,6 +291,11 @@ def linear(x, weight, bias=None):
     return y.view(*shp[:-1], weight.shape[1])
 
 
+# FFN1 bias gradient from the FFN2 data-gradient GEMM's epilogue (asm *cs kernels); PIAMD_FUSED_DB1=0
+# restores the separate column-sum pass (A/B)
+FUSED_DB1 = [os.environ.get("PIAMD_FUSED_DB1", "1") != "0"]
+
+
 class _FusedMLPFn(torch.autograd.Function):
     """``m = act(x·W1 + b1)·W2`` with the elementwise work inside the GEMM epilogues (reference
     ``fused_feedforward`` / ``FusedFeedForward`` and the cublasLt GELU_AUX / DGELU epilogues of
@@ -317,10 +322,17 @@ class _FusedMLPFn(torch.autograd.Function):
     @staticmethod
     @torch.amp.custom_bwd(device_type="cuda")
     def backward(ctx, dm):
-        from .gemm import asm_gemm
+        from .gemm import asm_gemm, colsum_parts
         x2, pre, a, w1, b1, w2 = ctx.saved_tensors
         dm2 = dm.reshape(-1, w2.shape[1]).contiguous()
-        dpre = asm_gemm(dm2, w2, trans_b=True, epi="dact", act=ctx.act, aux=pre)
+        # db1 = Σ_rows dpre comes out of the same epilogue (per-128-row-band column sums):
+        # no separate column-sum pass over the [T, F] data gradient
+        bmg = getattr(b1, "main_grad", None) if ctx.needs_input_grad[2] else None
+        cs = None
+        if ctx.needs_input_grad[2] and FUSED_DB1[0]:
+            cs = torch.empty(((dm2.shape[0] + 127) // 128, w2.shape[0]), dtype=torch.float32,
+                             device=dm2.device)
+        dpre = asm_gemm(dm2, w2, trans_b=True, epi="dact", act=ctx.act, aux=pre, colsum=cs)
         dw1 = db1 = dw2 = None
         if ctx.needs_input_grad[3]:
             mg = getattr(w2, "main_grad", None)
@@ -330,8 +342,13 @@ class _FusedMLPFn(torch.autograd.Function):
             else:
                 dw2 = wgrad_into(torch.zeros_like(w2), a, dm2)
         if ctx.needs_input_grad[2]:
-            bmg = getattr(b1, "main_grad", None)
-            if bmg is not None and bmg.dtype == dpre.dtype:
+            if cs is not None:
+                if bmg is not None:
+                    colsum_parts(cs, bmg, accumulate=True)
+                    _fire(b1)
+                else:
+                    db1 = cs.sum(0).to(b1.dtype)
+            elif bmg is not None and bmg.dtype == dpre.dtype:
                 colsum_into(dpre, bmg, accumulate=True)
                 _fire(b1)
             else:

@@ -130,7 +130,11 @@ class FlatTrainer:
         self.pp_group = pp_group
         self.world = dist.get_world_size(dp_group) if dp_group is not None else 1
         self.rank = dist.get_rank(dp_group) if dp_group is not None else 0
-        self.sharding = sharding_stage if self.world > 1 else 0
+        from ..distributed.collective import collectives_forced
+        # collectives over the dp group run at world > 1 (or forced on a 1-rank group: the RCCL
+        # paths exercised on one GPU, tests/test_rccl_world1_gpu.py)
+        self.multi = self.world > 1 or (collectives_forced() and dp_group is not None)
+        self.sharding = sharding_stage if self.multi else 0
         # Fleet hybrid with sharding_degree > 1 and dp_degree > 1: ``dp_group`` is the SHARDING
         # axis (reduce-scatter / sharded states / all-gather) and ``replica_group`` the data-parallel
         # axis over which each reduced shard is summed once more (states replicated across it) —
@@ -281,7 +285,7 @@ class FlatTrainer:
 
     def _make_ready(self, g):
         def ready(p):
-            if not self.overlap or (self.world == 1 and self.replica == 1):
+            if not self.overlap or (not self.multi and self.replica == 1):
                 return
             b = g.buckets[g.bucket_of[id(p)]]
             b.pending -= 1
@@ -300,12 +304,12 @@ class FlatTrainer:
         else:
             out = grads
             b.cast_back = None
-            if self.world > 1 and self.comm_fp16 and grads.dtype == torch.float32:
+            if self.multi and self.comm_fp16 and grads.dtype == torch.float32:
                 tmp = grads.to(torch.float16)
                 b.cast_back = (tmp, grads)
                 grads = out = tmp
             b.handle = dist.all_reduce(grads, group=self.dp_group, async_op=True) \
-                if self.world > 1 else None
+                if self.multi else None
         if self.replica > 1:
             # chained on the device: wait() orders the replica all-reduce behind the first
             # collective without blocking the host (RCCL); only the shard (or bucket) travels
@@ -335,7 +339,7 @@ class FlatTrainer:
     clear_grad = zero_grad
 
     def _finish_reduction(self):
-        if self.world == 1 and self.replica == 1:
+        if not self.multi and self.replica == 1:
             return
         for g in self.groups:
             for b in g.buckets:
@@ -362,7 +366,7 @@ class FlatTrainer:
                 continue
             sumsq(self._grads_for_update(g), out=nb[1 if g.distributed else 0], accumulate=True)
         scale = 1.0 / (self.world * self.replica)
-        if self.world > 1 and self.sharding:
+        if self.multi and self.sharding:
             dist.all_reduce(nb, group=self.dp_group)
         if self.mp_group is not None and dist.get_world_size(self.mp_group) > 1:
             d = nb[1:2].clone()

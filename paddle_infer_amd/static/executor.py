@@ -189,7 +189,8 @@ class Executor:
         dp = buckets = None
         if compiled is not None and compiled._data_parallel and training:
             import torch.distributed as dist
-            if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            from ..distributed.collective import multi_rank
+            if multi_rank():
                 from .backward import op_role as _role, OPTIMIZE as _OPT, GRAD as _G
                 dp = sorted({n for op in ops if _role(op) == _OPT for n in op.input_names()
                              if n.endswith(_G)})

@@ -111,3 +111,26 @@ def test_linear_training_uses_asm_and_matches():
     torch.testing.assert_close(y.float(), yr, rtol=0.02, atol=0.02)
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=0.03, atol=1e-4)
     torch.testing.assert_close(lin.weight.grad.float(), wr.grad, rtol=0.03, atol=1e-3)
+
+
+@pytest.mark.parametrize("act", ["gelu_tanh", "relu"])
+@pytest.mark.parametrize("M,N,K", [(512, 1024, 256), (304, 520, 192), (1000, 776, 512), (2048, 1024, 128)])
+def test_dact_epilogue_column_sums(act, M, N, K):
+    """The *cs dact kernels: C = (A·Bᵀ) ⊙ act'(aux) unchanged, plus per-128-row-band column sums of C
+    (persistent kernel: K/64 even ≥ 4; one-tile kernel otherwise; edge tiles in M and N)."""
+    from paddle_infer_amd.ops.activation import ACTS
+    from paddle_infer_amd.ops.gemm import _act_grad_ref, asm_gemm, colsum_parts
+    g = torch.Generator(device="cuda").manual_seed(M + N)
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    b = (0.1 * torch.randn(N, K, device="cuda", generator=g)).bfloat16()
+    h = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    cs = torch.full(((M + 127) // 128, N), float("nan"), device="cuda")
+    d = asm_gemm(a, b, trans_b=True, epi="dact", act=act, aux=h, colsum=cs)
+    ref_d = (a.float() @ b.float().t()) * _act_grad_ref(h, ACTS[act])
+    torch.testing.assert_close(d.float(), ref_d, rtol=0.02, atol=0.02 * ref_d.abs().max().item())
+    assert torch.isfinite(cs).all(), "every partial row / column must be written"
+    bands = torch.stack([ref_d[i * 128:(i + 1) * 128].sum(0) for i in range(cs.shape[0])])
+    torch.testing.assert_close(cs, bands, rtol=2e-3, atol=2e-3 * bands.abs().max().item())
+    out = torch.zeros(N, device="cuda", dtype=torch.bfloat16)
+    colsum_parts(cs, out, accumulate=True)
+    torch.testing.assert_close(out.float(), ref_d.sum(0), rtol=0.02, atol=0.02 * ref_d.sum(0).abs().max().item())

@@ -205,7 +205,8 @@ class Kernel:
         # *cs: the dact epilogue also writes per-128-row-band column sums of C (the bias gradient
         # of the layer whose pre-activation this is: FFN1's db1 from the FFN2 data-gradient GEMM)
         self.colsum = ek in ("dgelucs", "drelucs")
-        self.VCS = self.VE + 102        # 32 column-sum accumulators (8 blocks × 4 columns)
+        self.VCS = self.VE + 102        # 32 column-sum accumulators (8 blocks × 4 columns), +32 row,
+        # +34..37 masked values (≤ v251 in the persistent kernel: accum_offset 256 below)
         self.store_aux = ek != "biasnx"  # biasnx: C = acc + bias, no pre-activation output
         self.NBW = 8                    # 16-column accumulator blocks per wave row
         # resources: LDS bytes, workgroup size, accum_offset, AGPR count
@@ -951,6 +952,12 @@ class Kernel:
                 last = max(i for i, t in enumerate(issued) if t == ("L", mb))
                 self.e(f"s_waitcnt vmcnt({min(63, len(issued) - 1 - last)})")
             buf = mb % 2
+            if self.colsum:
+                # rows past M hold clamped re-reads of valid A rows (loads are clamped in range):
+                # the column sums take each row only when m0 + local row + 16·mb < M
+                self.e(f"s_add_u32 s{T + 2}, s{S_M0T}, {16 * mb}")
+                self.e(f"v_add_u32 v{self.VCS + 32}, s{T + 2}, v{V}")
+                self.e(f"v_cmp_gt_u32 s[{T}:{T + 1}], s{S_M}, v{self.VCS + 32}")
             # row voffset for this mb
             self.e(f"s_mul_i32 s{T + 7}, s{E + 4}, {16 * mb}")
             self.e(f"v_add_u32 v{V + 5}, s{T + 7}, v{V + 2}")
@@ -985,12 +992,15 @@ class Kernel:
                         self.dact_vals(d, V + 40 + 16 * buf + 2 * nb)
                         if self.colsum:
                             cs = self.VCS + 4 * nb
+                            tt = self.VCS + 34
                             if mb == 0:
                                 for j in range(4):
-                                    self.e(f"v_mov_b32 v{cs + j}, v{d + j}")
+                                    self.e(f"v_cndmask_b32_e64 v{cs + j}, 0, v{d + j}, s[{T}:{T + 1}]")
                             else:
-                                self.e(f"v_pk_add_f32 v[{cs}:{cs + 1}], v[{cs}:{cs + 1}], v[{d}:{d + 1}]")
-                                self.e(f"v_pk_add_f32 v[{cs + 2}:{cs + 3}], v[{cs + 2}:{cs + 3}], v[{d + 2}:{d + 3}]")
+                                for j in range(4):
+                                    self.e(f"v_cndmask_b32_e64 v{tt + j}, 0, v{d + j}, s[{T}:{T + 1}]")
+                                self.e(f"v_pk_add_f32 v[{cs}:{cs + 1}], v[{cs}:{cs + 1}], v[{tt}:{tt + 1}]")
+                                self.e(f"v_pk_add_f32 v[{cs + 2}:{cs + 3}], v[{cs + 2}:{cs + 3}], v[{tt + 2}:{tt + 3}]")
                     elif ek == "bf16acc":
                         o = V + 40 + 16 * buf + 2 * nb
                         t = self.VTMP + 4

@@ -132,6 +132,7 @@ def interpolate(x, size=None, scale_factor=None, mode="nearest", align_corners=F
     mode = {"bilinear": "bilinear", "nearest": "nearest", "bicubic": "bicubic", "linear": "linear",
             "trilinear": "trilinear", "area": "area"}[mode.lower()]
     ac = align_corners if mode in ("bilinear", "bicubic", "linear", "trilinear") else None
+    _lib_fallback(x, "interpolate")
     return TF.interpolate(x, size, scale_factor, mode, align_corners=ac)
 
 
@@ -220,8 +221,37 @@ def conv2d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data
     return _fmt_out(TF.conv2d(_fmt_in(x, data_format), weight, bias, stride, pad, dilation, groups), data_format)
 
 
+def _lib_fallback(x, op, why="ATen / MIOpen (no own kernel for this op)"):
+    """Record (warn once) a GPU call that leaves the framework's HIP kernels (`ops/_lib.py`)."""
+    if x.is_cuda:
+        from ...ops import _lib
+        _lib.fallback(op, why)
+
+
 def conv3d(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, data_format="NCDHW", name=None):
-    return _fmt_out(TF.conv3d(_fmt_in(x, data_format), weight, bias, stride, _padding(padding, 3), dilation, groups), data_format)
+    """Reference `nn/functional/conv.py:conv3d`; GPU tensors: kd 2-D convs on the own kernels
+    (`ops.conv.conv3d_any`)."""
+    pad = _padding(padding, 3)
+    if x.is_cuda:
+        from ...ops import conv as _conv
+        y = _conv.conv3d_any(x, weight, bias, stride, pad, dilation, groups, data_format == "NDHWC")
+        if y is not None:
+            return y
+        _lib_fallback(x, "conv3d", "string padding (MIOpen)")
+    return _fmt_out(TF.conv3d(_fmt_in(x, data_format), weight, bias, stride, pad, dilation, groups), data_format)
+
+
+def conv3d_transpose(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1, dilation=1,
+                     data_format="NCDHW", output_size=None, name=None):
+    if x.is_cuda:
+        from ...ops import conv as _conv
+        y = _conv.conv3d_transpose_any(x, weight, bias, stride, _padding(padding, 3), output_padding,
+                                       groups, dilation, data_format == "NDHWC", output_size)
+        if y is not None:
+            return y
+        _lib_fallback(x, "conv3d_transpose", "string padding (MIOpen)")
+    return _fmt_out(TF.conv_transpose3d(_fmt_in(x, data_format), weight, bias, stride, _padding(padding, 3),
+                                        output_padding, groups, dilation), data_format)
 
 
 def conv2d_transpose(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1,
@@ -237,10 +267,18 @@ def conv2d_transpose(x, weight, bias=None, stride=1, padding=0, output_padding=0
 
 def conv1d_transpose(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1,
                      dilation=1, output_size=None, data_format="NCL", name=None):
+    if x.is_cuda:
+        from ...ops import conv as _conv
+        y = _conv.conv1d_transpose_any(x, weight, bias, stride, _padding(padding, 1), output_padding,
+                                       groups, dilation, data_format == "NLC", output_size)
+        if y is not None:
+            return y
+        _lib_fallback(x, "conv1d_transpose", "string padding (MIOpen)")
     return _fmt_out(TF.conv_transpose1d(_fmt_in(x, data_format), weight, bias, stride, _padding(padding, 1), output_padding, groups, dilation), data_format)
 
 
 def max_pool1d(x, kernel_size, stride=None, padding=0, return_mask=False, ceil_mode=False, name=None):
+    _lib_fallback(x, "max_pool1d")
     return TF.max_pool1d(x, kernel_size, stride, _padding(padding, 1), 1, ceil_mode, return_mask)
 
 
@@ -257,40 +295,49 @@ def max_pool2d(x, kernel_size, stride=None, padding=0, return_mask=False, ceil_m
 
 def max_pool3d(x, kernel_size, stride=None, padding=0, return_mask=False, ceil_mode=False,
                data_format="NCDHW", name=None):
+    _lib_fallback(x, "max_pool3d")
     return TF.max_pool3d(x, kernel_size, stride, _padding(padding, 3), 1, ceil_mode, return_mask)
 
 
 def avg_pool1d(x, kernel_size, stride=None, padding=0, exclusive=True, ceil_mode=False, name=None):
+    _lib_fallback(x, "avg_pool1d")
     return TF.avg_pool1d(x, kernel_size, stride, _padding(padding, 1), ceil_mode, not exclusive)
 
 
 def avg_pool2d(x, kernel_size, stride=None, padding=0, ceil_mode=False, exclusive=True,
                divisor_override=None, data_format="NCHW", name=None):
+    _lib_fallback(x, "avg_pool2d")
     return _fmt_out(TF.avg_pool2d(_fmt_in(x, data_format), kernel_size, stride, _padding(padding, 2), ceil_mode, not exclusive, divisor_override), data_format)
 
 
 def avg_pool3d(x, kernel_size, stride=None, padding=0, ceil_mode=False, exclusive=True,
                divisor_override=None, data_format="NCDHW", name=None):
+    _lib_fallback(x, "avg_pool3d")
     return TF.avg_pool3d(x, kernel_size, stride, _padding(padding, 3), ceil_mode, not exclusive, divisor_override)
 
 
 def adaptive_avg_pool1d(x, output_size, name=None):
+    _lib_fallback(x, "adaptive_avg_pool1d")
     return TF.adaptive_avg_pool1d(x, output_size)
 
 
 def adaptive_avg_pool2d(x, output_size, data_format="NCHW", name=None):
+    _lib_fallback(x, "adaptive_avg_pool2d")
     return _fmt_out(TF.adaptive_avg_pool2d(_fmt_in(x, data_format), output_size), data_format)
 
 
 def adaptive_avg_pool3d(x, output_size, data_format="NCDHW", name=None):
+    _lib_fallback(x, "adaptive_avg_pool3d")
     return TF.adaptive_avg_pool3d(x, output_size)
 
 
 def adaptive_max_pool1d(x, output_size, return_mask=False, name=None):
+    _lib_fallback(x, "adaptive_max_pool1d")
     return TF.adaptive_max_pool1d(x, output_size, return_mask)
 
 
 def adaptive_max_pool2d(x, output_size, return_mask=False, name=None):
+    _lib_fallback(x, "adaptive_max_pool2d")
     return TF.adaptive_max_pool2d(x, output_size, return_mask)
 
 
@@ -516,6 +563,7 @@ def affine_grid(theta, out_shape, align_corners=True, name=None):
 
 
 def grid_sample(x, grid, mode="bilinear", padding_mode="zeros", align_corners=True, name=None):
+    _lib_fallback(x, "grid_sample")
     return TF.grid_sample(x, grid, mode, padding_mode, align_corners)
 
 

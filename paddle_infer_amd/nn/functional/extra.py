@@ -96,14 +96,6 @@ def channel_shuffle(x, groups, data_format="NCHW", name=None):
 
 
 # ----------------------------------------------------------------------------- conv / pooling
-def conv3d_transpose(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1,
-                     dilation=1, data_format="NCDHW", output_size=None, name=None):
-    if data_format == "NDHWC":
-        x = x.permute(0, 4, 1, 2, 3)
-    y = TF.conv_transpose3d(x, weight, bias, stride, padding, output_padding, groups, dilation)
-    return y.permute(0, 2, 3, 4, 1) if data_format == "NDHWC" else y
-
-
 def adaptive_max_pool3d(x, output_size, return_mask=False, name=None):
     r = TF.adaptive_max_pool3d(x, output_size, return_indices=return_mask)
     return r

@@ -1011,3 +1011,94 @@ def conv2d_nchw(x, weight, bias=None, stride=1, padding=0, dilation=1, act=None)
     """Same kernel for an NCHW-indexed tensor: channels_last storage is used as is (a view)."""
     y = conv2d_nhwc(x.permute(0, 2, 3, 1), weight, bias, stride, padding, dilation, act)
     return y.permute(0, 3, 1, 2)
+
+
+# ------------------------------------------------------------------------- 3-D / 1-D transposed
+def _triple(v):
+    v = tuple(v) if isinstance(v, (list, tuple)) else (v, v, v)
+    return v if len(v) == 3 else (v[0],) * 3
+
+
+def conv3d_any(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, ndhwc=False):
+    """Own-kernel route for a 3-D conv of a GPU tensor (reference `phi/kernels/gpudnn/
+    conv_kernel.cu:456`): the kd depth taps are kd 2-D convs on the framework's kernels
+    (`conv2d_any`: MFMA implicit GEMM / direct / split-bf16 fp32), each over the batch of output
+    depths (input depth d·s − p + z·dil gathered channels-last), summed in f32 — no MIOpen.
+    ``None`` when the call stays on the library (string padding)."""
+    if not (HIP_CONV and x.is_cuda and x.dim() == 5 and weight.dim() == 5) or isinstance(padding, str):
+        return None
+    st, pad, dil = _triple(stride), _triple(padding), _triple(dilation)
+    xl = x if ndhwc else x.permute(0, 2, 3, 4, 1)                     # [N, D, H, W, C]
+    N, D, H, W, C = xl.shape
+    K, cg, kd, kh, kw = weight.shape
+    Do = (D + 2 * pad[0] - dil[0] * (kd - 1) - 1) // st[0] + 1
+    if Do <= 0:
+        return None
+    if pad[0]:
+        xl = torch.nn.functional.pad(xl, (0, 0, 0, 0, 0, 0, pad[0], pad[0]))
+    base = torch.arange(Do, device=x.device) * st[0]
+    y = None
+    for z in range(kd):
+        xs = xl.index_select(1, base + z * dil[0]).reshape(N * Do, H, W, C)
+        yz = conv2d_any(xs, weight[:, :, z], None, st[1:], pad[1:], dil[1:], groups, nhwc=True)
+        if yz is None:
+            return None
+        y = yz.float() if y is None else y + yz.float()
+    Ho, Wo = y.shape[1], y.shape[2]
+    if bias is not None:
+        y = y + bias.float()
+    y = y.to(yz.dtype).reshape(N, Do, Ho, Wo, K)
+    return y if ndhwc else y.permute(0, 4, 1, 2, 3)
+
+
+def conv3d_transpose_any(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1,
+                         dilation=1, ndhwc=False, output_size=None):
+    """Own-kernel route for ``conv3d_transpose``: per depth tap z a 2-D transposed conv
+    (`conv2d_transpose_any`) over all input depths, scattered (index_add) to output depths
+    d·s + z·dil of the uncropped volume, then cropped by the depth padding."""
+    if not (HIP_CONV and x.is_cuda and x.dim() == 5 and weight.dim() == 5) or isinstance(padding, str):
+        return None
+    st, pad, dil, op = _triple(stride), _triple(padding), _triple(dilation), _triple(output_padding)
+    xl = x if ndhwc else x.permute(0, 2, 3, 4, 1)                     # [N, D, H, W, Cin]
+    N, D, H, W, Cin = xl.shape
+    _, og, kd, kh, kw = weight.shape
+    if output_size is not None:
+        osz = list(output_size)[-3:]
+        op = tuple(osz[i] - ((D, H, W)[i] - 1) * st[i] + 2 * pad[i] - dil[i] * ((kd, kh, kw)[i] - 1) - 1
+                   for i in range(3))
+    Do = (D - 1) * st[0] - 2 * pad[0] + dil[0] * (kd - 1) + op[0] + 1
+    full = (D - 1) * st[0] + dil[0] * (kd - 1) + 1
+    xs = xl.reshape(N * D, H, W, Cin)
+    out = None
+    base = torch.arange(D, device=x.device) * st[0]
+    for z in range(kd):
+        yz = conv2d_transpose_any(xs, weight[:, :, z], None, st[1:], pad[1:], op[1:], groups, dil[1:],
+                                  nhwc=True)
+        if yz is None:
+            return None
+        Ho, Wo, Co = yz.shape[1:]
+        yz = yz.float().reshape(N, D, Ho, Wo, Co)
+        if out is None:
+            out = torch.zeros((N, max(full, pad[0] + Do), Ho, Wo, Co), dtype=torch.float32, device=x.device)
+        out = out.index_add(1, base + z * dil[0], yz)
+    out = out[:, pad[0]:pad[0] + Do]
+    if bias is not None:
+        out = out + bias.float()
+    out = out.to(yz.dtype if yz is not None else x.dtype)
+    return out if ndhwc else out.permute(0, 4, 1, 2, 3)
+
+
+def conv1d_transpose_any(x, weight, bias=None, stride=1, padding=0, output_padding=0, groups=1,
+                         dilation=1, nlc=False, output_size=None):
+    """``conv1d_transpose`` as a 1 × L transposed 2-D conv on the own kernels."""
+    one = lambda v: v[0] if isinstance(v, (list, tuple)) else v  # noqa: E731
+    if not (HIP_CONV and x.is_cuda and x.dim() == 3) or isinstance(padding, str):
+        return None
+    xi = x.unsqueeze(1) if nlc else x.unsqueeze(2)
+    osz = None if output_size is None else [1, list(output_size)[-1]] if isinstance(output_size, (list, tuple)) \
+        else [1, output_size]
+    y = conv2d_transpose_any(xi, weight.unsqueeze(2), bias, (1, one(stride)), (0, one(padding)),
+                             (0, one(output_padding)), groups, (1, one(dilation)), nhwc=nlc, output_size=osz)
+    if y is None:
+        return None
+    return y.squeeze(1) if nlc else y.squeeze(2)

@@ -11,6 +11,8 @@
 * ``_lib/piamd_agemm.hsaco`` — the hand-scheduled assembly GEMM kernels: ``csrc/asm/gemm_gen.py``
   emits the gfx950 assembly, clang assembles it and ld.lld links the code object (loaded at run
   time by ``csrc/kernels/agemm_host.hip`` through ``hipModuleLoad``).
+* ``_lib/piamd_fa.hsaco`` — the hand-scheduled assembly flash-attention dK/dV kernels
+  (``csrc/asm/fa_gen.py``; loaded by ``csrc/kernels/fa_asm_host.hip``).
 * ``_lib/libpiamd_infer.so`` + ``_lib/pd_infer_run`` — the native C++ inference engine and its
   command-line driver (``csrc/native``: reference ``paddle_inference_api.h`` Config / Predictor /
   Tensor with no Python at run time; CPU loops and gfx950 HIP kernels + rocBLAS).
@@ -49,6 +51,7 @@ ARCH = os.environ.get("PIAMD_ARCH", "gfx950")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 ASMDIR = os.path.join(ROOT, "csrc", "asm")
 AGEMM_HSACO = os.path.join(LIBDIR, "piamd_agemm.hsaco")
+FA_HSACO = os.path.join(LIBDIR, "piamd_fa.hsaco")
 LLVM_BIN = os.path.join(ROCM, "lib", "llvm", "bin")
 
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
@@ -105,24 +108,30 @@ def _build_lib(srcs, out, compiler, flags, link_flags, hdr_time, verbose, jobs) 
     return bool(need_link)
 
 
-def build_asm(verbose: bool = True) -> bool:
-    """Generate, assemble and link the assembly GEMM code object (rebuilt when the generator is
-    newer than the code object)."""
-    gen = os.path.join(ASMDIR, "gemm_gen.py")
-    if os.path.exists(AGEMM_HSACO) and os.path.getmtime(AGEMM_HSACO) >= os.path.getmtime(gen):
+def _build_hsaco(gen_name: str, stem: str, out: str, verbose: bool) -> bool:
+    gen = os.path.join(ASMDIR, gen_name)
+    if os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(gen):
         return False
     os.makedirs(OBJDIR, exist_ok=True)
-    src = os.path.join(OBJDIR, "agemm.s")
-    obj = os.path.join(OBJDIR, "agemm.o")
+    src = os.path.join(OBJDIR, stem + ".s")
+    obj = os.path.join(OBJDIR, stem + ".o")
     _compile([sys.executable, gen, src], gen)
     _compile([os.path.join(LLVM_BIN, "clang"), "-x", "assembler", "-target", "amdgcn-amd-amdhsa",
               f"-mcpu={ARCH}", "-c", src, "-o", obj], src)
-    tmp = AGEMM_HSACO + ".tmp"
+    tmp = out + ".tmp"
     _compile([os.path.join(LLVM_BIN, "ld.lld"), "-shared", obj, "-o", tmp], obj)
-    os.replace(tmp, AGEMM_HSACO)
+    os.replace(tmp, out)
     if verbose:
-        print(f"[piamd build] assembled {AGEMM_HSACO}", flush=True)
+        print(f"[piamd build] assembled {out}", flush=True)
     return True
+
+
+def build_asm(verbose: bool = True) -> bool:
+    """Generate, assemble and link the assembly code objects (GEMM: gemm_gen.py; flash-attention
+    backward: fa_gen.py), each rebuilt when its generator is newer than the code object."""
+    a = _build_hsaco("gemm_gen.py", "agemm", AGEMM_HSACO, verbose)
+    b = _build_hsaco("fa_gen.py", "fa", FA_HSACO, verbose)
+    return a or b
 
 
 def build_native(verbose: bool = True, jobs: int = 4) -> None:

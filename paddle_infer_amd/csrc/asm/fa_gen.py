@@ -1,0 +1,719 @@
+"""Generator of the hand-scheduled gfx950 flash-attention backward dK/dV kernel (``fa_dkdv``).
+
+Why assembly: the HIP `bwd_dkdv_kernel` (csrc/kernels/flash_attn.h) runs ONE wave per SIMD and
+spends ≈7.5k cycles per 64-query tile for 64 MFMAs (2,048 cycles of matrix work): the softmax
+VALU work, LDS waits and barriers sit BETWEEN the MFMA phases instead of under them, and hipcc
+does not keep a requested interleave (profiles/fa_bwd_experiments_r3.txt). At one wave per SIMD
+an MFMA gap (32 cycles for v_mfma_f32_32x32x16_bf16) hides ≈24 cycles of other issue
+(MI355X_MICROARCH.md constants table), so every LDS read, every softmax op, every LDS-DMA and
+the barrier is placed here by hand into the MFMA stream.
+
+Math (same as the HIP kernel, reference `paddle/phi/kernels/gpu/flash_attn_grad_kernel.cu`):
+workgroup = 128 keys of one (batch, kv-head), 4 waves × 32 keys (key on the MFMA lane). For
+every 64-query tile of every q-head of the GQA group (causal: tiles from the diagonal on):
+  Sᵀ' = K·Qᵀ − lse/scale,  dPᵀ' = V·dOᵀ − δ          (accumulators start at the row constants)
+  P = exp2(c·S'),  dS = P ∘ dP'                        (c = scale·log2 e)
+  dVᵀ += dOᵀ·P,   dKᵀ += Qᵀ·dS                         (dK scaled by `scale` at the end)
+K and V fragments of the wave's keys live in AGPRs for the whole sweep (MFMA B operands may be
+AGPRs), dKᵀ/dVᵀ in AGPRs; S/dP accumulators in VGPRs for the softmax.
+
+Schedule of one tile (64 MFMAs: A0 = S,dP of queries 0-31, A1 = queries 32-63, C0 = dV/dK with
+keys' query-k 0-31, C1 = 32-63):
+* every MFMA operand read from LDS is issued LA MFMAs ahead into a 12-slot register ring
+  (ds_read_b128 row fragments for A, ds_read_b64_tr_b16 transposed pairs for C); the last LA
+  reads of a tile fetch the NEXT tile's first fragments;
+* the softmax (16 exp + 48 other VALU per 32 queries) is list-scheduled into the A1 / C0 MFMA
+  gaps within its dependency window (S final → P → dS → bf16 fragments before their C MFMA);
+* Q/dO tiles + the (−lse/scale, −δ) rows arrive by LDS-DMA in a 3-buffer ring; ONE barrier per
+  tile (after C0) publishes tile t+1 and frees the buffer of tile t−1, whose DMA for tile t+2
+  is then issued half in C1, half in the next tile's A0;
+* diagonal (causal) tiles initialise the masked S' entries to −inf (one branch per tile).
+
+Restrictions of this kernel (the launcher falls back to the HIP kernel otherwise): bf16, D = 128,
+no dropout / additive mask / varlen, Sq == Sk, Sq % 128 == 0, tensors < 2 GiB.
+
+``python fa_gen.py OUT.s`` writes the kernels; `_build.py` assembles them into
+``_lib/piamd_fa.hsaco`` (loaded by ``csrc/kernels/fa_asm_host.hip``).
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+# ---- kernel arguments (byte offsets; mirrored by struct FaDkdvArgs in fa_asm_host.hip) ----------
+ARGS = [
+    ("q", 0, 8), ("k", 8, 8), ("v", 16, 8), ("dout", 24, 8), ("dk", 32, 8), ("dv", 40, 8),
+    ("nl", 48, 8), ("nd", 56, 8),
+    ("q_bytes", 64, 4), ("k_bytes", 68, 4), ("v_bytes", 72, 4), ("o_bytes", 76, 4), ("st_bytes", 80, 4),
+    ("sqs", 84, 4), ("sqh", 88, 4), ("sqb", 92, 4),
+    ("sks", 96, 4), ("skh", 100, 4), ("skb", 104, 4),
+    ("svs", 108, 4), ("svh", 112, 4), ("svb", 116, 4),
+    ("sos", 120, 4), ("soh", 124, 4), ("sob", 128, 4),
+    ("Hq", 132, 4), ("Hk", 136, 4), ("group", 140, 4), ("Sq", 144, 4), ("coff", 148, 4),
+    ("nqt", 152, 4), ("HB", 156, 4), ("causal", 160, 4), ("c", 164, 4), ("scale", 168, 4),
+    ("rcp_HB", 172, 4), ("rcp_Hk", 176, 4), ("pad0", 180, 4), ("pad1", 184, 8),
+]
+ARGS_SIZE = 192
+
+
+def sarg(name):
+    """SGPR holding argument `name` (the 192 argument bytes are loaded to s[4:51])."""
+    for n, off, _ in ARGS:
+        if n == name:
+            return 4 + off // 4
+    raise KeyError(name)
+
+
+# ---- SGPR map ----------------------------------------------------------------------------------
+S_WG = 2
+SRD_Q, SRD_O, SRD_K, SRD_V, SRD_ST = 52, 56, 60, 64, 68   # buffer descriptors (4 each)
+S_KW31, S_SOFFK, S_SOFFV, S_LDSST = 72, 73, 74, 75
+S_W, S_KB, S_HK, S_B, S_N0, S_QF, S_TOT, S_IT, S_CQ0 = 76, 77, 78, 79, 80, 81, 82, 83, 84
+S_DIT, S_DQ0, S_DHQ, S_SQ, S_SO, S_SST, S_LDSW, S_QB, S_OB, S_STB = 85, 86, 87, 88, 89, 90, 91, 92, 93, 94
+S_T = 95                                                  # temps s95..s100
+NSGPR = 101
+
+# ---- VGPR / AGPR map -----------------------------------------------------------------------------
+V_TID, V_LANE = 0, 1
+V_DQ, V_DO, V_DST = 2, 6, 10       # LDS-DMA lane offsets: Q pieces 0-3, dO pieces 0-3, stats
+V_ROW = 11                         # [set 2][kk 8] row-fragment read offsets
+V_TR = 27                          # [set 2][jj 2][dt 4] transposed-read offsets
+V_STB = 43                         # [set 2] stats read offsets
+V_KT, V_THR, V_NINF = 45, 46, 47   # key − coff − 4hh, per-tile threshold, −inf
+V_RING = 48                        # 12 slots × 4
+RING = 12
+V_SACC, V_PACC = 96, 128           # S' / dP' accumulators: [qt 2][16]
+V_PB, V_DB = 160, 176              # bf16 fragments of P / dS: [ks 4][4]
+V_TMP = 192                        # temps v192..v199
+NV = 200                           # accum_offset
+A_DV, A_DK, A_KF, A_VF = 0, 64, 128, 160   # AGPRs: dVᵀ [dt][16], dKᵀ, K frags [kk][4], V frags
+NA = 192
+
+LA = 6                             # ring-read lookahead (MFMAs)
+BUF_B = 33280                      # per buffer: Q 16 KiB, dO 16 KiB, (−lse/scale, −δ) 2 × 256 B
+OFF_DO, OFF_ST = 16384, 32768
+LDS_BYTES = 3 * BUF_B
+MFMA = "v_mfma_f32_32x32x16_bf16"
+# ablation builds for measurement only (numerically wrong): nodma / nobar / novmwait / novalu /
+# noreads / nomfma drop that part of the tile loop; noloop runs prologue + epilogue only
+ABL = set(filter(None, os.environ.get("PIAMD_FA_ABL", "").split(",")))
+
+
+def buf_set(b):
+    """(offset-register set, immediate base) of LDS buffer b: buffers 0/1 share set 0 (the 16-bit
+    ds offset reaches buffer 1), buffer 2 has its own set based at 2·BUF_B."""
+    return (0, 0) if b == 0 else (0, BUF_B) if b == 1 else (1, 0)
+
+
+class FaDkdv:
+    def __init__(self, name, causal):
+        self.name, self.causal = name, causal
+        self.lines = []
+        self.nlab = 0
+
+    def e(self, s):
+        if ABL and getattr(self, "in_loop", False):
+            m = s.split(" ", 1)[0]
+            if (("nodma" in ABL and m.startswith("buffer_load") and s.endswith(" lds"))
+                    or ("nobar" in ABL and m == "s_barrier")
+                    or ("novmwait" in ABL and (m == "s_barrier" or s.startswith("s_waitcnt vmcnt")))
+                    or ("novalu" in ABL and m in ("v_mul_f32", "v_exp_f32", "v_cvt_pk_bf16_f32"))
+                    or ("noreads" in ABL and (m.startswith("ds_read") or s.startswith("s_waitcnt lgkmcnt")))):
+                return
+            if "nomfma" in ABL and m.startswith("v_mfma"):
+                s = "s_nop 0"
+        self.lines.append("\t" + s)
+
+    def lab(self, s):
+        self.lines.append(s + ":")
+
+    def newlab(self, tag):
+        self.nlab += 1
+        return f".L{self.name}_{tag}_{self.nlab}"
+
+    # -- helpers --------------------------------------------------------------------------------
+    def udiv(self, q, r, n, d, rcp):
+        """q = n / d, r = n % d (SGPRs, n < 2^24) from the f32 reciprocal in SGPR rcp, ±1 fixed."""
+        v = V_TMP
+        self.e(f"v_cvt_f32_u32 v{v}, s{n}")
+        self.e(f"v_mul_f32 v{v}, s{rcp}, v{v}")
+        self.e(f"v_cvt_u32_f32 v{v}, v{v}")
+        self.e("s_nop 1")
+        self.e(f"v_readfirstlane_b32 s{q}, v{v}")
+        self.e("s_nop 1")
+        t = S_T + 5
+        self.e(f"s_mul_i32 s{t}, s{q}, s{d}")
+        self.e(f"s_sub_i32 s{r}, s{n}, s{t}")
+        l1, l2 = self.newlab("dv"), self.newlab("dv")
+        self.e(f"s_cmp_lt_i32 s{r}, 0")
+        self.e(f"s_cbranch_scc0 {l1}")
+        self.e(f"s_sub_u32 s{q}, s{q}, 1")
+        self.e(f"s_add_u32 s{r}, s{r}, s{d}")
+        self.lab(l1)
+        self.e(f"s_cmp_ge_u32 s{r}, s{d}")
+        self.e(f"s_cbranch_scc0 {l2}")
+        self.e(f"s_add_u32 s{q}, s{q}, 1")
+        self.e(f"s_sub_u32 s{r}, s{r}, s{d}")
+        self.lab(l2)
+
+    def srd(self, srd, ptr, nbytes):
+        self.e(f"s_mov_b32 s{srd}, s{ptr}")
+        self.e(f"s_and_b32 s{srd + 1}, s{ptr + 1}, 0xffff")
+        self.e(f"s_mov_b32 s{srd + 2}, s{nbytes}")
+        self.e(f"s_mov_b32 s{srd + 3}, 0x20000")
+
+    def pending_soffs(self):
+        """Q / dO / stats soffsets of the pending DMA tile (S_DHQ, S_DQ0); past the last tile the
+        soffsets point past the descriptor ranges (the DMA then moves nothing from memory)."""
+        T = S_T
+        self.e(f"s_mul_i32 s{T}, s{S_DHQ}, s{sarg('sqh')}")
+        self.e(f"s_mul_i32 s{T + 1}, s{S_DQ0}, s{sarg('sqs')}")
+        self.e(f"s_add_u32 s{T}, s{T}, s{T + 1}")
+        self.e(f"s_add_u32 s{S_SQ}, s{T}, s{S_QB}")
+        self.e(f"s_mul_i32 s{T}, s{S_DHQ}, s{sarg('soh')}")
+        self.e(f"s_mul_i32 s{T + 1}, s{S_DQ0}, s{sarg('sos')}")
+        self.e(f"s_add_u32 s{T}, s{T}, s{T + 1}")
+        self.e(f"s_add_u32 s{S_SO}, s{T}, s{S_OB}")
+        self.e(f"s_mul_i32 s{T}, s{S_DHQ}, s{sarg('Sq')}")
+        self.e(f"s_add_u32 s{T}, s{T}, s{S_DQ0}")
+        self.e(f"s_lshl_b32 s{T}, s{T}, 2")
+        self.e(f"s_add_u32 s{S_SST}, s{T}, s{S_STB}")
+        self.e(f"s_cmp_ge_u32 s{S_DIT}, s{S_TOT}")
+        self.e(f"s_cselect_b32 s{S_SQ}, s{sarg('q_bytes')}, s{S_SQ}")
+        self.e(f"s_cselect_b32 s{S_SO}, s{sarg('o_bytes')}, s{S_SO}")
+        self.e(f"s_cselect_b32 s{S_SST}, s{sarg('st_bytes')}, s{S_SST}")
+
+    def advance_pending(self):
+        self.e(f"s_add_u32 s{S_DIT}, s{S_DIT}, 1")
+        self.e(f"s_add_u32 s{S_DQ0}, s{S_DQ0}, 64")
+        self.e(f"s_cmp_ge_u32 s{S_DQ0}, s{sarg('Sq')}")
+        self.e(f"s_cselect_b32 s{S_DQ0}, s{S_QF}, s{S_DQ0}")
+        self.e(f"s_addc_u32 s{S_DHQ}, s{S_DHQ}, 0")       # SCC still holds the wrap
+        self.pending_soffs()
+
+    def dma_first(self, buf):
+        """Q pieces + the stats row of the pending tile → LDS buffer `buf` (list of line pairs)."""
+        base = buf * BUF_B
+        ops = []
+        for i in range(4):
+            ops.append([f"s_add_u32 m0, s{S_LDSW}, {base + i * 1024}\n\ts_nop 0",
+                        f"buffer_load_dwordx4 v{V_DQ + i}, s[{SRD_Q}:{SRD_Q + 3}], s{S_SQ} offen lds"])
+        ops.append([f"s_add_u32 m0, s{S_LDSST}, {base + OFF_ST}\n\ts_nop 0",
+                    f"buffer_load_dword v{V_DST}, s[{SRD_ST}:{SRD_ST + 3}], s{S_SST} offen lds"])
+        return ops
+
+    def dma_second(self, buf):
+        base = buf * BUF_B + OFF_DO
+        return [[f"s_add_u32 m0, s{S_LDSW}, {base + i * 1024}\n\ts_nop 0",
+                 f"buffer_load_dwordx4 v{V_DO + i}, s[{SRD_O}:{SRD_O + 3}], s{S_SO} offen lds"]
+                for i in range(4)]
+
+    # -- MFMA stream ------------------------------------------------------------------------------
+    @staticmethod
+    def mfma_kind(m):
+        """MFMA m of a tile → ('S'|'P', qt, kk) or ('V'|'K', dt, ks)."""
+        if m < 32:
+            qt, r = m // 16, m % 16
+            return ("S" if r < 8 else "P", qt, r % 8)
+        c = m - 32
+        half, cc = c // 16, c % 16
+        dt, ks = cc // 4, 2 * half + (cc % 4) // 2
+        return ("K" if cc % 2 else "V", dt, ks)
+
+    @staticmethod
+    def slot(b, m):
+        return V_RING + 4 * ((64 * b + m) % RING)
+
+    def ring_reads(self, b, m):
+        """LDS reads of MFMA m's ring operand (tile in buffer b) → list of texts."""
+        kind, x, y = self.mfma_kind(m)
+        s, imm = buf_set(b)
+        d = self.slot(b, m)
+        if kind in ("S", "P"):
+            qt, kk = x, y
+            off = imm + (OFF_DO if kind == "P" else 0) + qt * 8192
+            return [f"ds_read_b128 v[{d}:{d + 3}], v{V_ROW + 8 * s + kk} offset:{off}"]
+        dt, ks = x, y
+        off = imm + (0 if kind == "K" else OFF_DO) + ks * 16 * 256
+        return [f"ds_read_b64_tr_b16 v[{d + 2 * jj}:{d + 2 * jj + 1}], v{V_TR + 8 * s + 4 * jj + dt} offset:{off}"
+                for jj in (0, 1)]
+
+    def stats_reads(self, b):
+        """(−lse/scale → S', −δ → dP') row constants of the tile in buffer b: 16 ds_read_b128,
+        ordered qt 0 first (the first MFMAs need them)."""
+        s, imm = buf_set(b)
+        out = []
+        for qt in (0, 1):
+            for g4 in range(4):
+                for which, dst in ((0, V_SACC), (1, V_PACC)):
+                    d = dst + 16 * qt + 4 * g4
+                    off = imm + which * 256 + 128 * qt + 32 * g4
+                    out.append(((qt, which), f"ds_read_b128 v[{d}:{d + 3}], v{V_STB + s} offset:{off}"))
+        return out
+
+    def mfma_text(self, b, m):
+        kind, x, y = self.mfma_kind(m)
+        a = self.slot(b, m)
+        if kind in ("S", "P"):
+            qt, kk = x, y
+            acc = (V_SACC if kind == "S" else V_PACC) + 16 * qt
+            bop = (A_KF if kind == "S" else A_VF) + 4 * kk
+            return f"{MFMA} v[{acc}:{acc + 15}], v[{a}:{a + 3}], a[{bop}:{bop + 3}], v[{acc}:{acc + 15}]"
+        dt, ks = x, y
+        acc = (A_DK if kind == "K" else A_DV) + 16 * dt
+        bop = (V_DB if kind == "K" else V_PB) + 4 * ks
+        return f"{MFMA} a[{acc}:{acc + 15}], v[{a}:{a + 3}], v[{bop}:{bop + 3}], a[{acc}:{acc + 15}]"
+
+    # -- softmax work queues ------------------------------------------------------------------------
+    def finish_queues(self):
+        """Four FIFO queues of (text, cost, pair) — S-part (scale, exp2) and D-part (dS, bf16
+        packs) per 32-query half — with their [earliest, deadline] gap windows."""
+        qs = []
+        for qt in (0, 1):
+            sq, dq = [], []
+            for j in range(8):
+                s0, s1 = V_SACC + 16 * qt + 2 * j, V_SACC + 16 * qt + 2 * j + 1
+                d0, d1 = V_PACC + 16 * qt + 2 * j, V_PACC + 16 * qt + 2 * j + 1
+                sq += [(f"v_mul_f32 v{s0}, s{sarg('c')}, v{s0}", 4, j),
+                       (f"v_mul_f32 v{s1}, s{sarg('c')}, v{s1}", 4, j),
+                       (f"v_exp_f32 v{s0}, v{s0}", 8, j),
+                       (f"v_exp_f32 v{s1}, v{s1}", 8, j)]
+                fr = 4 * (2 * qt + j // 4) + j % 4
+                dq += [(f"v_mul_f32 v{d0}, v{s0}, v{d0}", 4, j),
+                       (f"v_mul_f32 v{d1}, v{s1}, v{d1}", 4, j),
+                       (f"v_cvt_pk_bf16_f32 v{V_PB + fr}, v{s0}, v{s1}", 4, j),
+                       (f"v_cvt_pk_bf16_f32 v{V_DB + fr}, v{d0}, v{d1}", 4, j)]
+            # windows: S' final after MFMA 16qt+7, dP' after 16qt+15 (+2 MFMAs before a VALU read);
+            # bf16 fragments ≥ 1 MFMA before their first consumer (m = 32 / 48)
+            s_lo, d_lo, dl = 16 * qt + 9, 16 * qt + 17, 30 + 16 * qt
+            qs.append(dict(name=f"S{qt}", ops=sq, lo=s_lo, hi=dl - 2, placed=set()))
+            qs.append(dict(name=f"D{qt}", ops=dq, lo=d_lo, hi=dl, placed=set(), dep=len(qs) - 1))
+        return qs
+
+    def schedule_valu(self, fixed_cost):
+        """List-schedule the four softmax queues into gaps 0..63 under a per-gap issue budget of
+        24 cycles (minus the gap's fixed LDS/DMA cost); a queue that would miss its deadline is
+        forced. D-part pair j goes only after its S-part pair j (exp) sits in an earlier gap."""
+        qs = self.finish_queues()
+        gaps = [[] for _ in range(64)]
+        heads = [0] * len(qs)
+        s_done_gap = [dict() for _ in qs]       # queue → pair → gap of its last op
+        for g in range(64):
+            budget = 24 - fixed_cost[g]
+            while True:
+                cand = []
+                for qi, q in enumerate(qs):
+                    if heads[qi] >= len(q["ops"]) or g < q["lo"]:
+                        continue
+                    text, cost, pair = q["ops"][heads[qi]]
+                    if "dep" in q:
+                        sg = s_done_gap[q["dep"]]
+                        if pair not in sg or sg[pair] >= g or self._pair_incomplete(qs[q["dep"]], heads[q["dep"]], pair):
+                            continue
+                    left = len(q["ops"]) - heads[qi]
+                    slack = (q["hi"] - g + 1) * 5 - left   # ≈5 single-issue fillers per gap
+                    cand.append((slack, qi, cost))
+                if not cand:
+                    break
+                cand.sort()
+                slack, qi, cost = cand[0]
+                if cost > budget and slack > 0:
+                    break
+                text, cost, pair = qs[qi]["ops"][heads[qi]]
+                gaps[g].append(text)
+                heads[qi] += 1
+                s_done_gap[qi][pair] = g
+                budget -= cost
+        for qi, q in enumerate(qs):
+            assert heads[qi] == len(q["ops"]), f"softmax queue {q['name']} not placed"
+        return gaps
+
+    @staticmethod
+    def _pair_incomplete(q, head, pair):
+        return any(p == pair for _, _, p in q["ops"][head:])
+
+    # -- one tile body ------------------------------------------------------------------------------
+    def body_ops(self, b):
+        """The instruction stream of a tile in buffer b as a list of entries:
+        ('lds', key, text) / ('mfma', m, deps) / ('txt', text). LDS keys: ('ring', tile, m) and
+        ('stat', tile, (qt, which)) with tile 0 = this tile, 1 = the next one."""
+        nb = (b + 1) % 3
+        gaps = [[] for _ in range(64)]
+        fixed = [0] * 64
+        # ring reads, LA ahead; the last LA gaps fetch the next tile's first operands
+        for m in range(64):
+            g = m - LA
+            if g >= 0:
+                for t in self.ring_reads(b, m):
+                    gaps[g].append(("lds", ("ring", 0, m), t))
+                    fixed[g] += 2
+        for m in range(LA):
+            g = 64 - LA + m
+            for t in self.ring_reads(nb, m):
+                gaps[g].append(("lds", ("ring", 1, m), t))
+                fixed[g] += 2
+        # second half of the pending tile's DMA (→ buffer b+1) in A0, then advance the cursor
+        for i, (m0, ld) in enumerate(self.dma_second(nb)):
+            g = 1 + 3 * i
+            gaps[g] += [("txt", m0), ("txt", ld)]
+            fixed[g] += 12
+        gaps[13].append(("adv",))
+        fixed[13] += 8
+        # barrier after C0: tile t+1 landed (its DMA was issued one tile ago), buffer t−1 free
+        gaps[47].append(("txt", "s_waitcnt vmcnt(0)"))
+        gaps[47].append(("txt", "s_barrier"))
+        fixed[47] += 8
+        # next tile's row constants (after the softmax of this tile consumed S'/dP')
+        for i, (key, t) in enumerate(self.stats_reads(nb)):
+            g = 47 + i // 2
+            gaps[g].append(("lds", ("stat", 1, key), t))
+            fixed[g] += 2
+        # first half of the DMA of tile t+2 (→ buffer b+2)
+        for i, (m0, ld) in enumerate(self.dma_first((b + 2) % 3)):
+            g = 49 + 3 * i
+            gaps[g] += [("txt", m0), ("txt", ld)]
+            fixed[g] += 12
+        valu = self.schedule_valu(fixed)
+        ops = []
+        for m in range(64):
+            kind, x, y = self.mfma_kind(m)
+            deps = [("ring", 0, m)]
+            if kind in ("S", "P") and y == 0:
+                deps.append(("stat", 0, (x, 0 if kind == "S" else 1)))
+            ops.append(("mfma", m, deps, self.mfma_text(b, m)))
+            ops += gaps[m]
+            ops += [("txt", t) for t in valu[m]]
+        return ops
+
+    def emit_body(self, b, lab_next, lab_epi):
+        prev = self.body_ops((b + 2) % 3)
+        cur = self.body_ops(b)
+        # LDS issue order over (previous tile, this tile): keys of the previous body are shifted
+        # one tile back so its 'next tile' reads are this body's tile-0 reads
+        order = []
+        for ent in prev:
+            if ent[0] == "lds":
+                kind, t, idx = ent[1]
+                order.append((kind, t - 1, idx))
+        pos = {k: i for i, k in enumerate(order)}
+        done = 0                      # LDS ops [0, done) are known complete
+        issued = len(order)
+        # masked diagonal tiles: S' entries of (query < key) rows start at −inf
+        if self.causal:
+            skip = self.newlab("nomask")
+            T = S_T
+            self.e(f"s_add_u32 s{T}, s{S_CQ0}, s{sarg('coff')}")
+            self.e(f"s_cmp_gt_i32 s{S_KW31}, s{T}")
+            self.e(f"s_cbranch_scc0 {skip}")
+            self.e("s_waitcnt lgkmcnt(0)")
+            self.e(f"v_sub_u32 v{V_THR}, v{V_KT}, s{S_CQ0}")
+            for qt in (0, 1):
+                for g4 in range(4):
+                    for e in range(4):
+                        ci = 32 * qt + 8 * g4 + e
+                        r = V_SACC + 16 * qt + 4 * g4 + e
+                        self.e(f"v_cmp_lt_i32 vcc, {ci}, v{V_THR}")
+                        self.e(f"v_cndmask_b32 v{r}, v{r}, v{V_NINF}, vcc")
+            self.e("s_nop 4")
+            self.lab(skip)
+        for ent in cur:
+            if ent[0] == "lds":
+                pos[ent[1]] = issued
+                issued += 1
+                self.e(ent[2])
+            elif ent[0] == "mfma":
+                need = max(pos[d] for d in ent[2])
+                if need >= done:
+                    w = min(15, issued - 1 - need)
+                    self.e(f"s_waitcnt lgkmcnt({w})")
+                    done = issued - w
+                self.e(ent[3])
+            elif ent[0] == "adv":
+                self.advance_pending()
+            else:
+                self.e(ent[1])
+        # tile bookkeeping + loop
+        self.e(f"s_add_u32 s{S_IT}, s{S_IT}, 1")
+        self.e(f"s_add_u32 s{S_CQ0}, s{S_CQ0}, 64")
+        self.e(f"s_cmp_ge_u32 s{S_CQ0}, s{sarg('Sq')}")
+        self.e(f"s_cselect_b32 s{S_CQ0}, s{S_QF}, s{S_CQ0}")
+        self.e(f"s_cmp_ge_u32 s{S_IT}, s{S_TOT}")
+        self.e(f"s_cbranch_scc1 {lab_epi}")
+        if lab_next is not None:
+            self.e(f"s_branch {lab_next}")
+
+    # -- prologue / epilogue --------------------------------------------------------------------------
+    def prologue(self):
+        T = S_T
+        self.e("s_load_dwordx16 s[4:19], s[0:1], 0x0")
+        self.e("s_load_dwordx16 s[20:35], s[0:1], 0x40")
+        self.e("s_load_dwordx16 s[36:51], s[0:1], 0x80")
+        self.e(f"v_and_b32 v{V_LANE}, 63, v{V_TID}")
+        self.e(f"v_lshrrev_b32 v{V_TMP}, 6, v{V_TID}")
+        self.e("s_nop 1")
+        self.e(f"v_readfirstlane_b32 s{S_W}, v{V_TMP}")
+        self.e("s_waitcnt lgkmcnt(0)")
+        # workgroup → (kb, b, hk): low key blocks (most queries under a causal mask) first
+        self.udiv(S_KB, T, S_WG, sarg("HB"), sarg("rcp_HB"))
+        self.udiv(S_B, S_HK, T, sarg("Hk"), sarg("rcp_Hk"))
+        self.e(f"s_lshl_b32 s{S_N0}, s{S_KB}, 7")
+        # descriptors; stats row: even waves −lse/scale, odd waves −δ (waves 2/3 repeat 0/1)
+        self.srd(SRD_Q, sarg("q"), sarg("q_bytes"))
+        self.srd(SRD_O, sarg("dout"), sarg("o_bytes"))
+        self.srd(SRD_K, sarg("k"), sarg("k_bytes"))
+        self.srd(SRD_V, sarg("v"), sarg("v_bytes"))
+        self.e(f"s_and_b32 s{T}, s{S_W}, 1")
+        self.e(f"s_cmp_eq_u32 s{T}, 0")
+        self.e(f"s_cselect_b64 s[{SRD_ST}:{SRD_ST + 1}], s[{sarg('nl')}:{sarg('nl') + 1}], s[{sarg('nd')}:{sarg('nd') + 1}]")
+        self.e(f"s_and_b32 s{SRD_ST + 1}, s{SRD_ST + 1}, 0xffff")
+        self.e(f"s_mov_b32 s{SRD_ST + 2}, s{sarg('st_bytes')}")
+        self.e(f"s_mov_b32 s{SRD_ST + 3}, 0x20000")
+        self.e(f"s_lshl_b32 s{S_LDSST}, s{T}, 8")
+        self.e(f"s_lshl_b32 s{S_LDSW}, s{S_W}, 12")
+        # per-(batch, head) bases
+        self.e(f"s_mul_i32 s{S_QB}, s{S_B}, s{sarg('sqb')}")
+        self.e(f"s_mul_i32 s{S_OB}, s{S_B}, s{sarg('sob')}")
+        self.e(f"s_mul_i32 s{S_STB}, s{S_B}, s{sarg('Hq')}")
+        self.e(f"s_mul_i32 s{S_STB}, s{S_STB}, s{sarg('Sq')}")
+        self.e(f"s_lshl_b32 s{S_STB}, s{S_STB}, 2")
+        for soff, sb, sh, ss in ((S_SOFFK, "skb", "skh", "sks"), (S_SOFFV, "svb", "svh", "svs")):
+            self.e(f"s_mul_i32 s{soff}, s{S_B}, s{sarg(sb)}")
+            self.e(f"s_mul_i32 s{T}, s{S_HK}, s{sarg(sh)}")
+            self.e(f"s_add_u32 s{soff}, s{soff}, s{T}")
+            self.e(f"s_mul_i32 s{T}, s{S_N0}, s{sarg(ss)}")
+            self.e(f"s_add_u32 s{soff}, s{soff}, s{T}")
+        # lane decomposition: l32, hh, g = lane >> 4, gi = lane & 15
+        L = V_LANE
+        t = V_TMP
+        self.e(f"v_and_b32 v{t}, 31, v{L}")                        # l32
+        self.e(f"v_lshrrev_b32 v{t + 1}, 5, v{L}")                 # hh
+        self.e(f"s_lshl_b32 s{T}, s{S_W}, 5")
+        self.e(f"v_add_u32 v{t + 2}, s{T}, v{t}")                  # key - n0 = 32w + l32
+        # K / V fragments of this lane's key: 8 × 16 B at dims 16kk + 8hh
+        self.e(f"v_lshlrev_b32 v{t + 3}, 4, v{t + 1}")             # 16hh
+        self.e(f"v_mad_u32_u24 v{t + 4}, v{t + 2}, s{sarg('sks')}, v{t + 3}")
+        self.e(f"v_mad_u32_u24 v{t + 5}, v{t + 2}, s{sarg('svs')}, v{t + 3}")
+        for kk in range(8):
+            self.e(f"buffer_load_dwordx4 v[{48 + 4 * kk}:{51 + 4 * kk}], v{t + 4}, s[{SRD_K}:{SRD_K + 3}], s{S_SOFFK} offen offset:{32 * kk}")
+        for kk in range(8):
+            self.e(f"buffer_load_dwordx4 v[{80 + 4 * kk}:{83 + 4 * kk}], v{t + 5}, s[{SRD_V}:{SRD_V + 3}], s{S_SOFFV} offen offset:{32 * kk}")
+        # causal threshold base: key − coff − 4hh ; diagonal test key block end
+        self.e(f"v_add_u32 v{V_KT}, s{S_N0}, v{t + 2}")
+        self.e(f"v_subrev_u32 v{V_KT}, s{sarg('coff')}, v{V_KT}")
+        self.e(f"v_lshlrev_b32 v{t + 6}, 2, v{t + 1}")
+        self.e(f"v_sub_u32 v{V_KT}, v{V_KT}, v{t + 6}")
+        self.e(f"v_mov_b32 v{V_NINF}, 0xff800000")
+        self.e(f"s_lshl_b32 s{T}, s{S_W}, 5")
+        self.e(f"s_add_u32 s{S_KW31}, s{S_N0}, s{T}")
+        self.e(f"s_add_u32 s{S_KW31}, s{S_KW31}, 31")
+        # LDS-DMA lane offsets: piece i of wave w = tile rows 16w + 4i + g, physical chunk pc = lane
+        # & 15 holds logical chunk pc ^ x(row), x(r) = ((r & 3) << 2) | ((r >> 2) & 3) = (g << 2) | i
+        self.e(f"v_lshrrev_b32 v{t + 3}, 4, v{L}")                 # g
+        self.e(f"v_and_b32 v{t + 4}, 15, v{L}")                    # pc
+        self.e(f"s_lshl_b32 s{T}, s{S_W}, 4")
+        self.e(f"v_add_u32 v{t + 5}, s{T}, v{t + 3}")              # 16w + g
+        for i in range(4):
+            self.e(f"v_lshl_or_b32 v{t + 6}, v{t + 3}, 2, {i}")
+            self.e(f"v_xor_b32 v{t + 6}, v{t + 6}, v{t + 4}")
+            self.e(f"v_lshlrev_b32 v{t + 6}, 4, v{t + 6}")          # lc * 16
+            self.e(f"v_add_u32 v{t + 7}, {4 * i}, v{t + 5}")        # row
+            self.e(f"v_mad_u32_u24 v{V_DQ + i}, v{t + 7}, s{sarg('sqs')}, v{t + 6}")
+            self.e(f"v_mad_u32_u24 v{V_DO + i}, v{t + 7}, s{sarg('sos')}, v{t + 6}")
+        self.e(f"v_lshlrev_b32 v{V_DST}, 2, v{L}")
+        # row-fragment read offsets: image row l32 (+32 qt by immediate), chunk (2kk + hh) ^ x(l32)
+        self.e(f"v_and_b32 v{t + 3}, 3, v{t}")
+        self.e(f"v_lshlrev_b32 v{t + 3}, 2, v{t + 3}")
+        self.e(f"v_bfe_u32 v{t + 4}, v{t}, 2, 2")
+        self.e(f"v_or_b32 v{t + 3}, v{t + 3}, v{t + 4}")           # xl
+        self.e(f"v_lshlrev_b32 v{t + 4}, 8, v{t}")                  # l32 * 256
+        for kk in range(8):
+            self.e(f"v_add_u32 v{t + 5}, {2 * kk}, v{t + 1}")
+            self.e(f"v_xor_b32 v{t + 5}, v{t + 5}, v{t + 3}")
+            self.e(f"v_lshl_add_u32 v{V_ROW + kk}, v{t + 5}, 4, v{t + 4}")
+            self.e(f"v_add_u32 v{V_ROW + 8 + kk}, {2 * BUF_B}, v{V_ROW + kk}")
+        # transposed-read offsets: rows rl = 4hh + 8jj + (gi >> 2), cols 32dt + 16(g&1) + 4(gi&3)
+        self.e(f"v_and_b32 v{t + 3}, 15, v{L}")                    # gi
+        self.e(f"v_lshrrev_b32 v{t + 4}, 2, v{t + 3}")             # gi >> 2
+        self.e(f"v_lshl_add_u32 v{t + 4}, v{t + 1}, 2, v{t + 4}")  # 4hh + (gi >> 2)
+        self.e(f"v_and_b32 v{t + 5}, 3, v{t + 3}")
+        self.e(f"v_lshlrev_b32 v{t + 5}, 2, v{t + 5}")             # 4(gi & 3)
+        self.e(f"v_bfe_u32 v{t + 6}, v{L}, 4, 1")
+        self.e(f"v_lshl_add_u32 v{t + 5}, v{t + 6}, 4, v{t + 5}")  # col (dt = 0)
+        for jj in (0, 1):
+            self.e(f"v_add_u32 v{t + 6}, {8 * jj}, v{t + 4}")       # rl
+            self.e(f"v_and_b32 v{t + 7}, 3, v{t + 6}")
+            self.e(f"v_lshlrev_b32 v{t + 7}, 2, v{t + 7}")
+            self.e(f"v_bfe_u32 v{t + 2}, v{t + 6}, 2, 2")
+            self.e(f"v_or_b32 v{t + 7}, v{t + 7}, v{t + 2}")        # xr
+            self.e(f"v_lshrrev_b32 v{t + 2}, 3, v{t + 5}")          # col >> 3
+            self.e(f"v_xor_b32 v{t + 7}, v{t + 7}, v{t + 2}")
+            self.e(f"v_lshlrev_b32 v{t + 7}, 4, v{t + 7}")
+            self.e(f"v_lshl_add_u32 v{t + 7}, v{t + 6}, 8, v{t + 7}")
+            self.e(f"v_and_b32 v{t + 2}, 7, v{t + 5}")
+            self.e(f"v_lshl_add_u32 v{t + 7}, v{t + 2}, 1, v{t + 7}")   # dt = 0 offset
+            for dt in range(4):
+                r = V_TR + 4 * jj + dt
+                self.e(f"v_xor_b32 v{r}, {dt << 6}, v{t + 7}")
+                self.e(f"v_add_u32 v{r + 8}, {2 * BUF_B}, v{r}")
+        self.e(f"v_lshlrev_b32 v{t + 2}, 4, v{t + 1}")
+        self.e(f"v_add_u32 v{V_STB}, {OFF_ST}, v{t + 2}")
+        self.e(f"v_add_u32 v{V_STB + 1}, {2 * BUF_B + OFF_ST}, v{t + 2}")
+        # tile range: causal from the diagonal's 64-row tile, all q-heads of the group
+        self.e(f"s_mov_b32 s{S_QF}, 0")
+        if self.causal:
+            self.e(f"s_sub_i32 s{S_QF}, s{S_N0}, s{sarg('coff')}")
+            self.e(f"s_max_i32 s{S_QF}, s{S_QF}, 0")
+            self.e(f"s_and_b32 s{S_QF}, s{S_QF}, 0xffffffc0")
+        self.e(f"s_lshr_b32 s{T}, s{S_QF}, 6")
+        self.e(f"s_sub_u32 s{T}, s{sarg('nqt')}, s{T}")
+        self.e(f"s_mul_i32 s{S_TOT}, s{T}, s{sarg('group')}")
+        self.e(f"s_mov_b32 s{S_IT}, 0")
+        self.e(f"s_mov_b32 s{S_CQ0}, s{S_QF}")
+        self.e(f"s_mov_b32 s{S_DIT}, 0")
+        self.e(f"s_mov_b32 s{S_DQ0}, s{S_QF}")
+        self.e(f"s_mul_i32 s{S_DHQ}, s{S_HK}, s{sarg('group')}")
+        self.pending_soffs()
+        # prime: tile 0 → buffer 0 (whole), tile 1 → buffer 1 (first half)
+        for m0, ld in self.dma_first(0) + self.dma_second(0):
+            self.e(m0)
+            self.e(ld)
+        self.advance_pending()
+        for m0, ld in self.dma_first(1):
+            self.e(m0)
+            self.e(ld)
+        self.e("s_waitcnt vmcnt(5)")
+        # K / V fragments → AGPRs; dKᵀ / dVᵀ = 0
+        for kk in range(8):
+            for j in range(4):
+                self.e(f"v_accvgpr_write_b32 a{A_KF + 4 * kk + j}, v{48 + 4 * kk + j}")
+                self.e(f"v_accvgpr_write_b32 a{A_VF + 4 * kk + j}, v{80 + 4 * kk + j}")
+        for i in range(128):
+            self.e(f"v_accvgpr_write_b32 a{i}, 0")
+        self.e("s_barrier")
+        for _, txt in self.stats_reads(0):
+            self.e(txt)
+        for m in range(LA):
+            for txt in self.ring_reads(0, m):
+                self.e(txt)
+        self.e("s_waitcnt lgkmcnt(0)")
+        self.e("s_nop 4")
+
+    def epilogue(self):
+        T = S_T
+        self.e("s_waitcnt vmcnt(0) lgkmcnt(0)")
+        self.e("s_nop 15")
+        self.e("s_nop 15")
+        # dK = scale · dKᵀ, dV = dVᵀ, bf16; lane = key, 4 consecutive dims d0 = 32dt + 8g4 + 4hh
+        self.srd(SRD_Q, sarg("dk"), sarg("k_bytes"))
+        self.srd(SRD_O, sarg("dv"), sarg("v_bytes"))
+        t = V_TMP
+        L = V_LANE
+        self.e(f"v_and_b32 v{t}, 31, v{L}")
+        self.e(f"s_lshl_b32 s{T}, s{S_W}, 5")
+        self.e(f"v_add_u32 v{t}, s{T}, v{t}")
+        self.e(f"v_lshrrev_b32 v{t + 1}, 5, v{L}")
+        self.e(f"v_lshlrev_b32 v{t + 1}, 3, v{t + 1}")            # 8hh bytes
+        self.e(f"v_mad_u32_u24 v{t + 2}, v{t}, s{sarg('sks')}, v{t + 1}")
+        self.e(f"v_mad_u32_u24 v{t + 3}, v{t}, s{sarg('svs')}, v{t + 1}")
+        for dt in range(4):
+            for g4 in range(4):
+                for which in (0, 1):
+                    a0 = (A_DK if which == 0 else A_DV) + 16 * dt + 4 * g4
+                    for j in range(4):
+                        self.e(f"v_accvgpr_read_b32 v{t + 4 + j}, a{a0 + j}")
+                    if which == 0:
+                        for j in range(4):
+                            self.e(f"v_mul_f32 v{t + 4 + j}, s{sarg('scale')}, v{t + 4 + j}")
+                    self.e(f"v_cvt_pk_bf16_f32 v{t + 4}, v{t + 4}, v{t + 5}")
+                    self.e(f"v_cvt_pk_bf16_f32 v{t + 5}, v{t + 6}, v{t + 7}")
+                    srd, vo, so = (SRD_Q, t + 2, S_SOFFK) if which == 0 else (SRD_O, t + 3, S_SOFFV)
+                    self.e(f"buffer_store_dwordx2 v[{t + 4}:{t + 5}], v{vo}, s[{srd}:{srd + 3}], s{so} offen offset:{64 * dt + 16 * g4}")
+        self.e("s_waitcnt vmcnt(0)")
+        self.e("s_endpgm")
+
+    def text(self):
+        self.lines = []
+        self.prologue()
+        labs = [self.newlab(f"tile{b}") for b in range(3)]
+        epi = self.newlab("epi")
+        if "noloop" in ABL:
+            self.e(f"s_branch {epi}")
+        self.in_loop = True
+        for b in range(3):
+            self.lab(labs[b])
+            self.emit_body(b, labs[(b + 1) % 3] if b == 2 else None, epi)
+        self.in_loop = False
+        self.lab(epi)
+        self.epilogue()
+        n = self.name
+        head = ["\t.text", f"\t.globl {n}", "\t.p2align 8", f"\t.type {n},@function", f"{n}:"]
+        tail = [
+            f".L{n}_end:",
+            f"\t.size {n}, .L{n}_end-{n}",
+            "\t.rodata",
+            "\t.p2align 6",
+            f"\t.amdhsa_kernel {n}",
+            f"\t\t.amdhsa_group_segment_fixed_size {LDS_BYTES}",
+            "\t\t.amdhsa_private_segment_fixed_size 0",
+            f"\t\t.amdhsa_kernarg_size {ARGS_SIZE}",
+            "\t\t.amdhsa_user_sgpr_count 2",
+            "\t\t.amdhsa_user_sgpr_kernarg_segment_ptr 1",
+            "\t\t.amdhsa_system_sgpr_workgroup_id_x 1",
+            "\t\t.amdhsa_system_vgpr_workitem_id 0",
+            f"\t\t.amdhsa_next_free_vgpr {NV + NA}",
+            f"\t\t.amdhsa_next_free_sgpr {NSGPR}",
+            f"\t\t.amdhsa_accum_offset {NV}",
+            "\t\t.amdhsa_reserve_vcc 1",
+            "\t\t.amdhsa_float_denorm_mode_32 3",
+            "\t\t.amdhsa_float_denorm_mode_16_64 3",
+            "\t\t.amdhsa_ieee_mode 0",
+            "\t\t.amdhsa_dx10_clamp 1",
+            "\t.end_amdhsa_kernel",
+            "\t.text",
+        ]
+        return "\n".join(head + self.lines + tail) + "\n"
+
+    def metadata(self):
+        return f"""  - .args:
+      - .offset:         0
+        .size:           {ARGS_SIZE}
+        .value_kind:     by_value
+    .group_segment_fixed_size: {LDS_BYTES}
+    .kernarg_segment_align: 8
+    .kernarg_segment_size: {ARGS_SIZE}
+    .max_flat_workgroup_size: 256
+    .name:           {self.name}
+    .private_segment_fixed_size: 0
+    .sgpr_count:     {NSGPR + 6}
+    .sgpr_spill_count: 0
+    .symbol:         {self.name}.kd
+    .vgpr_count:     {NV + NA}
+    .agpr_count:     {NA}
+    .vgpr_spill_count: 0
+    .wavefront_size: 64
+"""
+
+
+def kernels():
+    return [FaDkdv("piamd_fa_dkdv_d128_causal", True), FaDkdv("piamd_fa_dkdv_d128", False)]
+
+
+def generate() -> str:
+    ks = kernels()
+    out = ['\t.amdgcn_target "amdgcn-amd-amdhsa--gfx950"', "\t.amdhsa_code_object_version 5"]
+    for k in ks:
+        out.append(k.text())
+    out.append("\t.amdgpu_metadata\n---\namdhsa.kernels:")
+    for k in ks:
+        out.append(k.metadata().rstrip("\n"))
+    out.append("amdhsa.target:   amdgcn-amd-amdhsa--gfx950\namdhsa.version:\n  - 1\n  - 2\n...\n\t.end_amdgpu_metadata")
+    return "\n".join(out) + "\n"
+
+
+if __name__ == "__main__":
+    text = generate()
+    if len(sys.argv) > 1:
+        with open(sys.argv[1], "w") as f:
+            f.write(text)
+    else:
+        sys.stdout.write(text)

@@ -1,0 +1,145 @@
+// Host side of the hand-scheduled assembly flash-attention backward (`csrc/asm/fa_gen.py` →
+// _lib/piamd_fa.hsaco): code-object loading, the kernel-argument block and the launch contract.
+// `launch_bwd` (flash_attn.h) asks fa_dkdv_asm() first and runs the HIP dK/dV kernel when the
+// assembly kernel does not take the shape.
+//
+// Parity: reference `paddle/phi/kernels/gpu/flash_attn_grad_kernel.cu` (dK / dV of
+// flash_attn_grad).
+#include "common.h"
+#include "fa_args.h"
+
+#include <cmath>
+#include <cstdlib>
+#include <mutex>
+
+namespace {
+
+// mirror of fa_gen.ARGS (byte offsets noted)
+struct __attribute__((packed)) FaDkdvArgs {
+  const void *q, *k, *v, *dout;  // 0, 8, 16, 24
+  void *dk, *dv;                 // 32, 40
+  const float *nl, *nd;          // 48, 56: −lse/scale, −δ rows
+  unsigned q_bytes, k_bytes, v_bytes, o_bytes, st_bytes;  // 64 .. 80 (descriptor ranges)
+  unsigned sqs, sqh, sqb;        // 84 ..: byte strides
+  unsigned sks, skh, skb;
+  unsigned svs, svh, svb;
+  unsigned sos, soh, sob;        // .. 128
+  unsigned Hq, Hk, group, Sq;    // 132 ..
+  int coff;                      // 148
+  unsigned nqt, HB, causal;      // 152, 156, 160
+  float c, scale, rcp_HB, rcp_Hk;  // 164 .. 176
+  unsigned pad0;                 // 180
+  unsigned long long pad1;       // 184
+};
+static_assert(sizeof(FaDkdvArgs) == 192, "FaDkdvArgs layout");
+
+std::mutex g_mu;
+hipModule_t g_mod = nullptr;
+hipFunction_t g_fn[2] = {nullptr, nullptr};
+int g_enabled = -1;
+
+bool enabled() {
+  if (g_enabled < 0) {
+    const char* e = getenv("PIAMD_FA_ASM");
+    g_enabled = !(e && e[0] == '0');
+  }
+  return g_enabled > 0;
+}
+
+// byte extent of a [B, S, H, 128] view from its base (last byte + 1), 0 on overflow past 2^31
+unsigned long long extent(long long sb, long long ss, long long sh, int B, int S, int H) {
+  if (sb < 0 || ss < 0 || sh < 0) return 0;
+  const unsigned long long e = ((unsigned long long)(B - 1) * sb + (unsigned long long)(S - 1) * ss +
+                                (unsigned long long)(H - 1) * sh + 128) * 2ull;
+  return e < (1ull << 31) ? e : 0;
+}
+
+bool stride_ok(long long s) { return s > 0 && (s * 2) % 16 == 0 && s * 2 < (1ll << 24); }
+
+}  // namespace
+
+PIAMD_EXPORT int piamd_fa_asm_load(const char* path) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_mod) return 0;
+  hipModule_t m = nullptr;
+  int err = (int)hipModuleLoad(&m, path);
+  if (err) return err;
+  if (hipModuleGetFunction(&g_fn[0], m, "piamd_fa_dkdv_d128") != hipSuccess ||
+      hipModuleGetFunction(&g_fn[1], m, "piamd_fa_dkdv_d128_causal") != hipSuccess)
+    return (int)hipErrorNotFound;
+  g_mod = m;
+  return 0;
+}
+
+PIAMD_EXPORT int piamd_fa_asm_loaded() { return g_mod != nullptr; }
+
+// 1 = use the assembly dK/dV kernel where it applies (default; env PIAMD_FA_ASM=0 turns it off)
+PIAMD_EXPORT int piamd_fa_asm_enable(int on) {
+  g_enabled = on ? 1 : 0;
+  return 0;
+}
+
+// Would the assembly kernel take this backward? (contract in fa_gen.py's docstring)
+PIAMD_EXPORT int piamd_fa_asm_applies(const FaArgs* ap) {
+  const FaArgs& a = *ap;
+  if (!g_mod || !enabled()) return 0;
+  if (a.D != 128 || a.cu_q || a.mask || a.p_drop > 0.f || a.Sq != a.Sk || a.Sq % 128) return 0;
+  if (a.Hk <= 0 || a.Hq % a.Hk || a.B <= 0) return 0;
+  // seq strides feed 24-bit multiplies; every stride keeps 16-byte rows (LDS-DMA / dwordx4)
+  for (long long s : {a.sqs, a.sks, a.svs, a.sos})
+    if (!stride_ok(s)) return 0;
+  for (long long s : {a.sqh, a.skh, a.svh, a.soh, a.sqb, a.skb, a.svb, a.sob})
+    if (s < 0 || (s * 2) % 16) return 0;
+  if (!extent(a.sqb, a.sqs, a.sqh, a.B, a.Sq, a.Hq) || !extent(a.skb, a.sks, a.skh, a.B, a.Sk, a.Hk) ||
+      !extent(a.svb, a.svs, a.svh, a.B, a.Sk, a.Hk) || !extent(a.sob, a.sos, a.soh, a.B, a.Sq, a.Hq))
+    return 0;
+  for (const void* p : {(const void*)a.q, (const void*)a.k, (const void*)a.v, (const void*)a.dout,
+                        (const void*)a.dk, (const void*)a.dv})
+    if (reinterpret_cast<unsigned long long>(p) % 16) return 0;
+  const long long rows = (long long)a.B * a.Hq * a.Sq;
+  if (rows * 4 >= (1ll << 31) || (long long)(a.Sk / 128) * a.Hk * a.B >= (1ll << 24)) return 0;
+  return 1;
+}
+
+// Launch the assembly dK/dV kernel (after bwd_pre wrote −δ / −lse/scale into a.delta). Returns
+// 1 when launched, 0 when the shape is not this kernel's (caller runs the HIP kernel), < 0 on a
+// launch error.
+int fa_dkdv_asm(const FaArgs& a, hipStream_t st) {
+  if (!piamd_fa_asm_applies(&a)) return 0;
+  FaDkdvArgs g{};
+  g.q = a.q;
+  g.k = a.k;
+  g.v = a.v;
+  g.dout = a.dout;
+  g.dk = a.dk;
+  g.dv = a.dv;
+  const long long rows = (long long)a.B * a.Hq * a.Sq;
+  g.nd = a.delta;
+  g.nl = a.delta + rows;
+  g.q_bytes = (unsigned)extent(a.sqb, a.sqs, a.sqh, a.B, a.Sq, a.Hq);
+  g.k_bytes = (unsigned)extent(a.skb, a.sks, a.skh, a.B, a.Sk, a.Hk);
+  g.v_bytes = (unsigned)extent(a.svb, a.svs, a.svh, a.B, a.Sk, a.Hk);
+  g.o_bytes = (unsigned)extent(a.sob, a.sos, a.soh, a.B, a.Sq, a.Hq);
+  g.st_bytes = (unsigned)(rows * 4);
+  g.sqs = (unsigned)(a.sqs * 2); g.sqh = (unsigned)(a.sqh * 2); g.sqb = (unsigned)(a.sqb * 2);
+  g.sks = (unsigned)(a.sks * 2); g.skh = (unsigned)(a.skh * 2); g.skb = (unsigned)(a.skb * 2);
+  g.svs = (unsigned)(a.svs * 2); g.svh = (unsigned)(a.svh * 2); g.svb = (unsigned)(a.svb * 2);
+  g.sos = (unsigned)(a.sos * 2); g.soh = (unsigned)(a.soh * 2); g.sob = (unsigned)(a.sob * 2);
+  g.Hq = a.Hq;
+  g.Hk = a.Hk;
+  g.group = a.Hq / a.Hk;
+  g.Sq = a.Sq;
+  g.coff = a.Sk - a.Sq;
+  g.nqt = a.Sq / 64;
+  g.HB = a.Hk * a.B;
+  g.causal = a.causal ? 1 : 0;
+  g.c = a.scale * 1.4426950408889634f;
+  g.scale = a.scale;
+  g.rcp_HB = 1.f / (float)g.HB;
+  g.rcp_Hk = 1.f / (float)a.Hk;
+  const unsigned grid = (unsigned)((a.Sk / 128) * g.HB);
+  size_t sz = sizeof(g);
+  void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &g, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+  hipError_t err = hipModuleLaunchKernel(g_fn[a.causal ? 1 : 0], grid, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
+  return err == hipSuccess ? 1 : -(int)err;
+}

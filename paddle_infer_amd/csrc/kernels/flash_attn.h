@@ -52,6 +52,9 @@
 // C ABI argument block (ops/attention.py mirrors it as a ctypes.Structure).
 #include "fa_args.h"
 
+// hand-scheduled assembly dK/dV kernel (fa_asm_host.hip): 1 = launched, 0 = shape not taken
+int fa_dkdv_asm(const FaArgs& a, hipStream_t st);
+
 
 namespace fa {
 
@@ -1317,7 +1320,8 @@ template <bool F16, int D, bool C>
 int launch_bwd_feat(const FaArgs& a, dim3 gkv, dim3 gq, hipStream_t st) {
   const int feat = (a.p_drop > 0.f ? F_DROP : 0) | (a.mask ? F_MASK : 0);
 #define BWD_F(FF)                                                                              \
-  hipLaunchKernelGGL((bwd_dkdv_kernel<D, F16, C, FF>), gkv, dim3(256), 0, st, a);              \
+  if (!(FF == 0 && D == 128 && !F16 && fa_dkdv_asm(a, st) == 1))                               \
+    hipLaunchKernelGGL((bwd_dkdv_kernel<D, F16, C, FF>), gkv, dim3(256), 0, st, a);            \
   hipLaunchKernelGGL((bwd_dq_kernel<D, F16, C, FF>), gq, dim3(256), 0, st, a);                 \
   break;
   switch (feat) {

@@ -234,6 +234,10 @@ _SIGS["piamd_small_gemm"] = [c_int, c_void_p, c_ll, c_void_p, c_ll, c_void_p, c_
 # ... + ln_c1, ln_b2 (f32 [N] or null), ln_eps, stream
 _SIGS["piamd_small_gemm_ln"] = _SIGS["piamd_small_gemm"][:-1] + [c_void_p, c_void_p, c_float, c_void_p]
 _SIGS["piamd_agemm_loaded"] = []
+_SIGS["piamd_fa_asm_load"] = [ctypes.c_char_p]
+_SIGS["piamd_fa_asm_loaded"] = []
+_SIGS["piamd_fa_asm_enable"] = [ctypes.c_int]
+_SIGS["piamd_fa_asm_applies"] = [ctypes.c_void_p]
 _SIGS["piamd_transpose_bf16"] = [c_void_p, c_void_p, c_int, c_int, c_void_p]
 # src, ld, dst, R, C, Rp, Cp, lo_mask, axis, stream
 _SIGS["piamd_split3_f32"] = [c_void_p, c_ll, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p]

@@ -102,6 +102,24 @@ def _fwd(q, k, v, causal, scale, mask=None, p=0.0, seed=0, off=0):
     return o, lse
 
 
+_FA_ASM_READY = [False]
+
+
+def _fa_asm_load():
+    """Load the assembly flash-attention backward code object (`_lib/piamd_fa.hsaco`, from
+    `csrc/asm/fa_gen.py`) once; `piamd_fa_bwd` then runs its dK/dV kernel where it applies."""
+    if _FA_ASM_READY[0]:
+        return
+    import os
+    from .. import _build
+    path = os.environ.get("PIAMD_FA_HSACO") or _build.FA_HSACO  # ablation builds (measurement)
+    if not os.path.exists(path):
+        raise RuntimeError(f"assembly flash-attention code object missing ({path}); run "
+                           "`python -m paddle_infer_amd._build`")
+    _lib.call("piamd_fa_asm_load", path.encode())
+    _FA_ASM_READY[0] = True
+
+
 def _bwd(q, k, v, o, lse, do, dq, dk, dv, causal, scale, mask=None, p=0.0, seed=0, off=0):
     B, Sq, Hq, D = q.shape
     Sk, Hk = k.shape[1], k.shape[2]
@@ -114,6 +132,7 @@ def _bwd(q, k, v, o, lse, do, dq, dk, dv, causal, scale, mask=None, p=0.0, seed=
     a = _args(q, k, v, o, lse, causal, scale, mask, p, seed, off, B, Sq, Sk, Hq, Hk, D)
     a.dout, a.delta, a.dq, a.dk, a.dv = do.data_ptr(), delta.data_ptr(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr()
     a.ds = None
+    _fa_asm_load()
     _lib.call("piamd_fa_bwd", ctypes.byref(a), _f16(q), _lib.stream())
 
 

@@ -30,7 +30,7 @@ keys' query-k 0-31, C1 = 32-63):
 * diagonal (causal) tiles initialise the masked S' entries to −inf (one branch per tile).
 
 Restrictions of this kernel (the launcher falls back to the HIP kernel otherwise): bf16, D = 128,
-no dropout / additive mask / varlen, Sq == Sk, Sq % 128 == 0, tensors < 2 GiB.
+no dropout / additive mask / varlen, Sq == Sk, Sq % 256 == 0 (key blocks pair up), tensors < 2 GiB.
 
 ``python fa_gen.py OUT.s`` writes the kernels; `_build.py` assembles them into
 ``_lib/piamd_fa.hsaco`` (loaded by ``csrc/kernels/fa_asm_host.hip``).
@@ -50,8 +50,8 @@ ARGS = [
     ("svs", 108, 4), ("svh", 112, 4), ("svb", 116, 4),
     ("sos", 120, 4), ("soh", 124, 4), ("sob", 128, 4),
     ("Hq", 132, 4), ("Hk", 136, 4), ("group", 140, 4), ("Sq", 144, 4), ("coff", 148, 4),
-    ("nqt", 152, 4), ("HB", 156, 4), ("causal", 160, 4), ("c", 164, 4), ("scale", 168, 4),
-    ("rcp_HB", 172, 4), ("rcp_Hk", 176, 4), ("pad0", 180, 4), ("pad1", 184, 8),
+    ("nqt", 152, 4), ("npair", 156, 4), ("nkb1", 160, 4), ("c", 164, 4), ("scale", 168, 4),
+    ("rcp_npair", 172, 4), ("rcp_Hk", 176, 4), ("nitems", 180, 4), ("G", 184, 4), ("G2m1", 188, 4),
 ]
 ARGS_SIZE = 192
 
@@ -66,11 +66,14 @@ def sarg(name):
 
 # ---- SGPR map ----------------------------------------------------------------------------------
 S_WG = 2
-SRD_Q, SRD_O, SRD_K, SRD_V, SRD_ST = 52, 56, 60, 64, 68   # buffer descriptors (4 each)
-S_KW31, S_SOFFK, S_SOFFV, S_LDSST = 72, 73, 74, 75
-S_W, S_KB, S_HK, S_B, S_N0, S_QF, S_TOT, S_IT, S_CQ0 = 76, 77, 78, 79, 80, 81, 82, 83, 84
-S_DIT, S_DQ0, S_DHQ, S_SQ, S_SO, S_SST, S_LDSW, S_QB, S_OB, S_STB = 85, 86, 87, 88, 89, 90, 91, 92, 93, 94
-S_T = 95                                                  # temps s95..s100
+# s4..s19 hold the 8 argument pointers until the descriptors are built, then:
+S_QB, S_OB, S_STB, S_W, S_LDSW, S_LDSST = 4, 5, 6, 7, 8, 9
+S_T = 10                                                  # temps s10..s17
+SRD_Q, SRD_O, SRD_K, SRD_V, SRD_ST, SRD_DK, SRD_DV = 52, 56, 60, 64, 68, 72, 76   # descriptors
+# compute side: the work item whose tiles the MFMAs run
+S_U, S_B, S_HK, S_N0, S_QF, S_TOT, S_IT, S_CQ0, S_KW31, S_SOFFK, S_SOFFV = range(80, 91)
+# DMA side: the item / tile the LDS-DMA stream is fetching (runs 1.5 tiles ahead, across items)
+S_DU, S_DQF, S_DTOT, S_DIT, S_DQ0, S_DHQ, S_SQ, S_SO, S_SST = range(91, 100)
 NSGPR = 101
 
 # ---- VGPR / AGPR map -----------------------------------------------------------------------------
@@ -85,9 +88,13 @@ RING = 12
 V_SACC, V_PACC = 96, 128           # S' / dP' accumulators: [qt 2][16]
 V_PB, V_DB = 160, 176              # bf16 fragments of P / dS: [ks 4][4]
 V_TMP = 192                        # temps v192..v199
-NV = 200                           # accum_offset
-A_DV, A_DK, A_KF, A_VF = 0, 64, 128, 160   # AGPRs: dVᵀ [dt][16], dKᵀ, K frags [kk][4], V frags
-NA = 192
+V_KT0, V_KVK, V_KVV = 200, 201, 202  # 32w + l32 − coff − 4hh; K / V fragment-load lane offsets
+V_STK, V_STV = 203, 204            # dK / dV store lane offsets
+NV = 208                           # accum_offset
+# AGPRs: dVᵀ [dt][16], dKᵀ, K / V fragments [kk][4] of the current item, and of the next item
+# (prefetched during the current one)
+A_DV, A_DK, A_KF, A_VF, A_KN, A_VN = 0, 64, 128, 160, 192, 224
+NA = 256
 
 LA = 6                             # ring-read lookahead (MFMAs)
 BUF_B = 33280                      # per buffer: Q 16 KiB, dO 16 KiB, (−lse/scale, −δ) 2 × 256 B
@@ -95,7 +102,7 @@ OFF_DO, OFF_ST = 16384, 32768
 LDS_BYTES = 3 * BUF_B
 MFMA = "v_mfma_f32_32x32x16_bf16"
 # ablation builds for measurement only (numerically wrong): nodma / nobar / novmwait / novalu /
-# noreads / nomfma drop that part of the tile loop; noloop runs prologue + epilogue only
+# noreads / nomfma drop that part of the tile loop
 ABL = set(filter(None, os.environ.get("PIAMD_FA_ABL", "").split(",")))
 
 
@@ -178,18 +185,162 @@ class FaDkdv:
         self.e(f"s_add_u32 s{T}, s{T}, s{S_DQ0}")
         self.e(f"s_lshl_b32 s{T}, s{T}, 2")
         self.e(f"s_add_u32 s{S_SST}, s{T}, s{S_STB}")
-        self.e(f"s_cmp_ge_u32 s{S_DIT}, s{S_TOT}")
+        self.e(f"s_cmp_ge_u32 s{S_DU}, s{sarg('nitems')}")
         self.e(f"s_cselect_b32 s{S_SQ}, s{sarg('q_bytes')}, s{S_SQ}")
         self.e(f"s_cselect_b32 s{S_SO}, s{sarg('o_bytes')}, s{S_SO}")
         self.e(f"s_cselect_b32 s{S_SST}, s{sarg('st_bytes')}, s{S_SST}")
 
     def advance_pending(self):
+        """Next tile of the DMA stream: next query tile, next q-head of the group, or the first
+        tile of the workgroup's next work item."""
         self.e(f"s_add_u32 s{S_DIT}, s{S_DIT}, 1")
         self.e(f"s_add_u32 s{S_DQ0}, s{S_DQ0}, 64")
         self.e(f"s_cmp_ge_u32 s{S_DQ0}, s{sarg('Sq')}")
-        self.e(f"s_cselect_b32 s{S_DQ0}, s{S_QF}, s{S_DQ0}")
+        self.e(f"s_cselect_b32 s{S_DQ0}, s{S_DQF}, s{S_DQ0}")
         self.e(f"s_addc_u32 s{S_DHQ}, s{S_DHQ}, 0")       # SCC still holds the wrap
+        same = self.newlab("sameitem")
+        self.e(f"s_cmp_lt_u32 s{S_DIT}, s{S_DTOT}")
+        self.e(f"s_cbranch_scc1 {same}")
+        self.next_item(S_DU)
+        self.e(f"s_cmp_ge_u32 s{S_DU}, s{sarg('nitems')}")
+        self.e(f"s_cbranch_scc1 {same}")
+        self.pending_item_setup()
+        self.lab(same)
         self.pending_soffs()
+
+    # -- work items -------------------------------------------------------------------------------
+    def decode(self, u, kb, b, hk):
+        """Work item u → key block kb, batch b, kv-head hk (SGPRs; kb may be a temp).
+        u = 2·m + s: member m = group·npair + j of a (batch, kv-head) group takes key blocks j
+        (s = 0) and nkb−1−j (s = 1) — equal causal work per member (16 + 2 = 14 + 4 = … tiles) —
+        and the npair members of a group sit on one XCD at once (see next_item), so the group's
+        Q / dO tiles come from that XCD's L2 after the first member fetched them."""
+        T = S_T
+        self.e(f"s_lshr_b32 s{T + 7}, s{u}, 1")
+        self.udiv(T + 6, kb, T + 7, sarg("npair"), sarg("rcp_npair"))     # group, j
+        self.e(f"s_sub_u32 s{T + 7}, s{sarg('nkb1')}, s{kb}")
+        self.e(f"s_bitcmp1_b32 s{u}, 0")
+        self.e(f"s_cselect_b32 s{kb}, s{T + 7}, s{kb}")
+        self.udiv(b, hk, T + 6, sarg("Hk"), sarg("rcp_Hk"))
+
+    def next_item(self, u):
+        """The workgroup's next item: the second key block of its pair, or its pair in the next
+        round (u += 2G − 1)."""
+        T = S_T
+        self.e(f"s_bitcmp1_b32 s{u}, 0")
+        self.e(f"s_cselect_b32 s{T + 7}, s{sarg('G2m1')}, 1")
+        self.e(f"s_add_u32 s{u}, s{u}, s{T + 7}")
+
+    def q_first(self, dst, n0):
+        self.e(f"s_mov_b32 s{dst}, 0")
+        if self.causal:
+            self.e(f"s_sub_i32 s{dst}, s{n0}, s{sarg('coff')}")
+            self.e(f"s_max_i32 s{dst}, s{dst}, 0")
+            self.e(f"s_and_b32 s{dst}, s{dst}, 0xffffffc0")
+
+    def tiles_of(self, dst, qf):
+        self.e(f"s_lshr_b32 s{dst}, s{qf}, 6")
+        self.e(f"s_sub_u32 s{dst}, s{sarg('nqt')}, s{dst}")
+        self.e(f"s_mul_i32 s{dst}, s{dst}, s{sarg('group')}")
+
+    def kv_soffs(self, b, hk, n0, dk, dv):
+        T = S_T
+        for soff, sb, sh, ss in ((dk, "skb", "skh", "sks"), (dv, "svb", "svh", "svs")):
+            self.e(f"s_mul_i32 s{soff}, s{b}, s{sarg(sb)}")
+            self.e(f"s_mul_i32 s{T + 7}, s{hk}, s{sarg(sh)}")
+            self.e(f"s_add_u32 s{soff}, s{soff}, s{T + 7}")
+            self.e(f"s_mul_i32 s{T + 7}, s{n0}, s{sarg(ss)}")
+            self.e(f"s_add_u32 s{soff}, s{soff}, s{T + 7}")
+
+    def compute_item_setup(self):
+        """Compute-side state of item S_U: batch / head / key block, tile count, K/V/dK/dV
+        soffsets, causal thresholds."""
+        T = S_T
+        self.decode(S_U, T, S_B, S_HK)
+        self.e(f"s_lshl_b32 s{S_N0}, s{T}, 7")
+        self.q_first(S_QF, S_N0)
+        self.tiles_of(S_TOT, S_QF)
+        self.e(f"s_mov_b32 s{S_IT}, 0")
+        self.e(f"s_mov_b32 s{S_CQ0}, s{S_QF}")
+        self.kv_soffs(S_B, S_HK, S_N0, S_SOFFK, S_SOFFV)
+        self.e(f"s_lshl_b32 s{S_KW31}, s{S_W}, 5")
+        self.e(f"s_add_u32 s{S_KW31}, s{S_KW31}, s{S_N0}")
+        self.e(f"s_add_u32 s{S_KW31}, s{S_KW31}, 31")
+        self.e(f"v_add_u32 v{V_KT}, s{S_N0}, v{V_KT0}")
+
+    def pending_item_setup(self):
+        """DMA-side state of item S_DU (its first tile)."""
+        T = S_T
+        self.decode(S_DU, T, T + 1, T + 2)
+        self.e(f"s_lshl_b32 s{T}, s{T}, 7")
+        self.q_first(S_DQF, T)
+        self.tiles_of(S_DTOT, S_DQF)
+        self.e(f"s_mov_b32 s{S_DIT}, 0")
+        self.e(f"s_mov_b32 s{S_DQ0}, s{S_DQF}")
+        self.e(f"s_mul_i32 s{S_DHQ}, s{T + 2}, s{sarg('group')}")
+        self.e(f"s_mul_i32 s{S_QB}, s{T + 1}, s{sarg('sqb')}")
+        self.e(f"s_mul_i32 s{S_OB}, s{T + 1}, s{sarg('sob')}")
+        self.e(f"s_mul_i32 s{S_STB}, s{T + 1}, s{sarg('Hq')}")
+        self.e(f"s_mul_i32 s{S_STB}, s{S_STB}, s{sarg('Sq')}")
+        self.e(f"s_lshl_b32 s{S_STB}, s{S_STB}, 2")
+
+    def kv_load(self, ak, av, soffk, soffv):
+        """The lane's K / V fragments (8 × 16 B each at dims 16kk + 8hh of its key row) straight
+        into AGPRs."""
+        for kk in range(8):
+            self.e(f"buffer_load_dwordx4 a[{ak + 4 * kk}:{ak + 4 * kk + 3}], v{V_KVK}, s[{SRD_K}:{SRD_K + 3}], s{soffk} offen offset:{32 * kk}")
+        for kk in range(8):
+            self.e(f"buffer_load_dwordx4 a[{av + 4 * kk}:{av + 4 * kk + 3}], v{V_KVV}, s[{SRD_V}:{SRD_V + 3}], s{soffv} offen offset:{32 * kk}")
+
+    def prefetch_next_kv(self):
+        """After the first tile of an item: the next item's K / V into the spare AGPR set (the
+        next tile barrier's vmcnt(0) lands them long before the item switch)."""
+        T = S_T
+        skip = self.newlab("nopf")
+        self.e(f"s_mov_b32 s{T + 3}, s{S_U}")
+        self.next_item(T + 3)
+        self.e(f"s_cmp_ge_u32 s{T + 3}, s{sarg('nitems')}")
+        self.e(f"s_cbranch_scc1 {skip}")
+        self.decode(T + 3, T, T + 1, T + 2)
+        self.e(f"s_lshl_b32 s{T}, s{T}, 7")
+        self.kv_soffs(T + 1, T + 2, T, T + 3, T + 4)
+        self.kv_load(A_KN, A_VN, T + 3, T + 4)
+        self.lab(skip)
+
+    def item_end(self, lab_next, lab_exit):
+        """After an item's last tile: dK / dV out, accumulators zeroed, the prefetched K / V become
+        current, next item's compute state (its first tile is already in LDS / in flight)."""
+        self.e("s_nop 15")
+        self.e("s_nop 15")
+        self.store_dkdv()
+        for i in range(128):
+            self.e(f"v_accvgpr_write_b32 a{i}, 0")
+        for i in range(64):
+            self.e(f"v_accvgpr_mov_b32 a{A_KF + i}, a{A_KN + i}")
+        self.next_item(S_U)
+        self.e(f"s_cmp_ge_u32 s{S_U}, s{sarg('nitems')}")
+        self.e(f"s_cbranch_scc1 {lab_exit}")
+        self.compute_item_setup()
+        self.e("s_nop 4")
+        self.e(f"s_branch {lab_next}")
+
+    def store_dkdv(self):
+        """dK = scale · dKᵀ, dV = dVᵀ in bf16; lane = key, 4 consecutive dims d0 = 32dt + 8g4 +
+        4hh per 8-byte store (fire and forget: nothing waits for them)."""
+        t = V_TMP
+        for dt in range(4):
+            for g4 in range(4):
+                for which in (0, 1):
+                    a0 = (A_DK if which == 0 else A_DV) + 16 * dt + 4 * g4
+                    for j in range(4):
+                        self.e(f"v_accvgpr_read_b32 v{t + 4 + j}, a{a0 + j}")
+                    if which == 0:
+                        for j in range(4):
+                            self.e(f"v_mul_f32 v{t + 4 + j}, s{sarg('scale')}, v{t + 4 + j}")
+                    self.e(f"v_cvt_pk_bf16_f32 v{t + 4}, v{t + 4}, v{t + 5}")
+                    self.e(f"v_cvt_pk_bf16_f32 v{t + 5}, v{t + 6}, v{t + 7}")
+                    srd, vo, so = (SRD_DK, V_STK, S_SOFFK) if which == 0 else (SRD_DV, V_STV, S_SOFFV)
+                    self.e(f"buffer_store_dwordx2 v[{t + 4}:{t + 5}], v{vo}, s[{srd}:{srd + 3}], s{so} offen offset:{64 * dt + 16 * g4}")
 
     def dma_first(self, buf):
         """Q pieces + the stats row of the pending tile → LDS buffer `buf` (list of line pairs)."""
@@ -432,56 +583,58 @@ class FaDkdv:
                 self.advance_pending()
             else:
                 self.e(ent[1])
-        # tile bookkeeping + loop
+        # tile bookkeeping: next tile of this item, K/V prefetch after the item's first tile,
+        # item switch after its last
         self.e(f"s_add_u32 s{S_IT}, s{S_IT}, 1")
         self.e(f"s_add_u32 s{S_CQ0}, s{S_CQ0}, 64")
         self.e(f"s_cmp_ge_u32 s{S_CQ0}, s{sarg('Sq')}")
         self.e(f"s_cselect_b32 s{S_CQ0}, s{S_QF}, s{S_CQ0}")
-        self.e(f"s_cmp_ge_u32 s{S_IT}, s{S_TOT}")
-        self.e(f"s_cbranch_scc1 {lab_epi}")
-        if lab_next is not None:
-            self.e(f"s_branch {lab_next}")
+        nopf = self.newlab("nopf")
+        self.e(f"s_cmp_eq_u32 s{S_IT}, 1")
+        self.e(f"s_cbranch_scc0 {nopf}")
+        self.prefetch_next_kv()
+        self.lab(nopf)
+        self.e(f"s_cmp_lt_u32 s{S_IT}, s{S_TOT}")
+        self.e(f"s_cbranch_scc1 {lab_next}")
+        self.item_end(lab_next, lab_epi)
 
-    # -- prologue / epilogue --------------------------------------------------------------------------
-    def prologue(self):
+    # -- prologue / exit ------------------------------------------------------------------------------
+    def prologue(self, lab_exit):
         T = S_T
         self.e("s_load_dwordx16 s[4:19], s[0:1], 0x0")
         self.e("s_load_dwordx16 s[20:35], s[0:1], 0x40")
         self.e("s_load_dwordx16 s[36:51], s[0:1], 0x80")
         self.e(f"v_and_b32 v{V_LANE}, 63, v{V_TID}")
         self.e(f"v_lshrrev_b32 v{V_TMP}, 6, v{V_TID}")
-        self.e("s_nop 1")
-        self.e(f"v_readfirstlane_b32 s{S_W}, v{V_TMP}")
         self.e("s_waitcnt lgkmcnt(0)")
-        # workgroup → (kb, b, hk): low key blocks (most queries under a causal mask) first
-        self.udiv(S_KB, T, S_WG, sarg("HB"), sarg("rcp_HB"))
-        self.udiv(S_B, S_HK, T, sarg("Hk"), sarg("rcp_Hk"))
-        self.e(f"s_lshl_b32 s{S_N0}, s{S_KB}, 7")
-        # descriptors; stats row: even waves −lse/scale, odd waves −δ (waves 2/3 repeat 0/1)
+        # descriptors first (they consume the pointer arguments in s4..s19); stats row: even
+        # waves −lse/scale, odd waves −δ (waves 2/3 repeat 0/1)
         self.srd(SRD_Q, sarg("q"), sarg("q_bytes"))
         self.srd(SRD_O, sarg("dout"), sarg("o_bytes"))
         self.srd(SRD_K, sarg("k"), sarg("k_bytes"))
         self.srd(SRD_V, sarg("v"), sarg("v_bytes"))
-        self.e(f"s_and_b32 s{T}, s{S_W}, 1")
-        self.e(f"s_cmp_eq_u32 s{T}, 0")
+        self.srd(SRD_DK, sarg("dk"), sarg("k_bytes"))
+        self.srd(SRD_DV, sarg("dv"), sarg("v_bytes"))
+        self.e(f"v_readfirstlane_b32 s{SRD_ST + 2}, v{V_TMP}")      # wave id (temporarily)
+        self.e(f"s_and_b32 s{SRD_ST + 3}, s{SRD_ST + 2}, 1")
+        self.e(f"s_cmp_eq_u32 s{SRD_ST + 3}, 0")
         self.e(f"s_cselect_b64 s[{SRD_ST}:{SRD_ST + 1}], s[{sarg('nl')}:{sarg('nl') + 1}], s[{sarg('nd')}:{sarg('nd') + 1}]")
+        self.e(f"s_mov_b32 s{S_W}, s{SRD_ST + 2}")
+        self.e(f"s_lshl_b32 s{S_LDSST}, s{SRD_ST + 3}, 8")
         self.e(f"s_and_b32 s{SRD_ST + 1}, s{SRD_ST + 1}, 0xffff")
         self.e(f"s_mov_b32 s{SRD_ST + 2}, s{sarg('st_bytes')}")
         self.e(f"s_mov_b32 s{SRD_ST + 3}, 0x20000")
-        self.e(f"s_lshl_b32 s{S_LDSST}, s{T}, 8")
         self.e(f"s_lshl_b32 s{S_LDSW}, s{S_W}, 12")
-        # per-(batch, head) bases
-        self.e(f"s_mul_i32 s{S_QB}, s{S_B}, s{sarg('sqb')}")
-        self.e(f"s_mul_i32 s{S_OB}, s{S_B}, s{sarg('sob')}")
-        self.e(f"s_mul_i32 s{S_STB}, s{S_B}, s{sarg('Hq')}")
-        self.e(f"s_mul_i32 s{S_STB}, s{S_STB}, s{sarg('Sq')}")
-        self.e(f"s_lshl_b32 s{S_STB}, s{S_STB}, 2")
-        for soff, sb, sh, ss in ((S_SOFFK, "skb", "skh", "sks"), (S_SOFFV, "svb", "svh", "svs")):
-            self.e(f"s_mul_i32 s{soff}, s{S_B}, s{sarg(sb)}")
-            self.e(f"s_mul_i32 s{T}, s{S_HK}, s{sarg(sh)}")
-            self.e(f"s_add_u32 s{soff}, s{soff}, s{T}")
-            self.e(f"s_mul_i32 s{T}, s{S_N0}, s{sarg(ss)}")
-            self.e(f"s_add_u32 s{soff}, s{soff}, s{T}")
+        # virtual id v = (wg % 8)·(G / 8) + wg / 8: consecutive v share an XCD (dispatch deals
+        # workgroups round-robin to the 8 XCDs; the host makes G a multiple of 8); u = 2v
+        self.e(f"s_and_b32 s{S_U}, s{S_WG}, 7")
+        self.e(f"s_lshr_b32 s{S_T}, s{sarg('G')}, 3")
+        self.e(f"s_mul_i32 s{S_U}, s{S_U}, s{S_T}")
+        self.e(f"s_lshr_b32 s{S_T}, s{S_WG}, 3")
+        self.e(f"s_add_u32 s{S_U}, s{S_U}, s{S_T}")
+        self.e(f"s_lshl_b32 s{S_U}, s{S_U}, 1")
+        self.e(f"s_cmp_ge_u32 s{S_U}, s{sarg('nitems')}")
+        self.e(f"s_cbranch_scc1 {lab_exit}")
         # lane decomposition: l32, hh, g = lane >> 4, gi = lane & 15
         L = V_LANE
         t = V_TMP
@@ -489,23 +642,18 @@ class FaDkdv:
         self.e(f"v_lshrrev_b32 v{t + 1}, 5, v{L}")                 # hh
         self.e(f"s_lshl_b32 s{T}, s{S_W}, 5")
         self.e(f"v_add_u32 v{t + 2}, s{T}, v{t}")                  # key - n0 = 32w + l32
-        # K / V fragments of this lane's key: 8 × 16 B at dims 16kk + 8hh
+        # K / V fragment loads: key row, dims 16kk + 8hh; dK / dV stores: dims +4hh
         self.e(f"v_lshlrev_b32 v{t + 3}, 4, v{t + 1}")             # 16hh
-        self.e(f"v_mad_u32_u24 v{t + 4}, v{t + 2}, s{sarg('sks')}, v{t + 3}")
-        self.e(f"v_mad_u32_u24 v{t + 5}, v{t + 2}, s{sarg('svs')}, v{t + 3}")
-        for kk in range(8):
-            self.e(f"buffer_load_dwordx4 v[{48 + 4 * kk}:{51 + 4 * kk}], v{t + 4}, s[{SRD_K}:{SRD_K + 3}], s{S_SOFFK} offen offset:{32 * kk}")
-        for kk in range(8):
-            self.e(f"buffer_load_dwordx4 v[{80 + 4 * kk}:{83 + 4 * kk}], v{t + 5}, s[{SRD_V}:{SRD_V + 3}], s{S_SOFFV} offen offset:{32 * kk}")
-        # causal threshold base: key − coff − 4hh ; diagonal test key block end
-        self.e(f"v_add_u32 v{V_KT}, s{S_N0}, v{t + 2}")
-        self.e(f"v_subrev_u32 v{V_KT}, s{sarg('coff')}, v{V_KT}")
+        self.e(f"v_mad_u32_u24 v{V_KVK}, v{t + 2}, s{sarg('sks')}, v{t + 3}")
+        self.e(f"v_mad_u32_u24 v{V_KVV}, v{t + 2}, s{sarg('svs')}, v{t + 3}")
+        self.e(f"v_lshlrev_b32 v{t + 3}, 3, v{t + 1}")             # 8hh
+        self.e(f"v_mad_u32_u24 v{V_STK}, v{t + 2}, s{sarg('sks')}, v{t + 3}")
+        self.e(f"v_mad_u32_u24 v{V_STV}, v{t + 2}, s{sarg('svs')}, v{t + 3}")
+        # causal threshold base: 32w + l32 − coff − 4hh (+ n0 per item)
+        self.e(f"v_subrev_u32 v{V_KT0}, s{sarg('coff')}, v{t + 2}")
         self.e(f"v_lshlrev_b32 v{t + 6}, 2, v{t + 1}")
-        self.e(f"v_sub_u32 v{V_KT}, v{V_KT}, v{t + 6}")
+        self.e(f"v_sub_u32 v{V_KT0}, v{V_KT0}, v{t + 6}")
         self.e(f"v_mov_b32 v{V_NINF}, 0xff800000")
-        self.e(f"s_lshl_b32 s{T}, s{S_W}, 5")
-        self.e(f"s_add_u32 s{S_KW31}, s{S_N0}, s{T}")
-        self.e(f"s_add_u32 s{S_KW31}, s{S_KW31}, 31")
         # LDS-DMA lane offsets: piece i of wave w = tile rows 16w + 4i + g, physical chunk pc = lane
         # & 15 holds logical chunk pc ^ x(row), x(r) = ((r & 3) << 2) | ((r >> 2) & 3) = (g << 2) | i
         self.e(f"v_lshrrev_b32 v{t + 3}, 4, v{L}")                 # g
@@ -558,22 +706,12 @@ class FaDkdv:
         self.e(f"v_lshlrev_b32 v{t + 2}, 4, v{t + 1}")
         self.e(f"v_add_u32 v{V_STB}, {OFF_ST}, v{t + 2}")
         self.e(f"v_add_u32 v{V_STB + 1}, {2 * BUF_B + OFF_ST}, v{t + 2}")
-        # tile range: causal from the diagonal's 64-row tile, all q-heads of the group
-        self.e(f"s_mov_b32 s{S_QF}, 0")
-        if self.causal:
-            self.e(f"s_sub_i32 s{S_QF}, s{S_N0}, s{sarg('coff')}")
-            self.e(f"s_max_i32 s{S_QF}, s{S_QF}, 0")
-            self.e(f"s_and_b32 s{S_QF}, s{S_QF}, 0xffffffc0")
-        self.e(f"s_lshr_b32 s{T}, s{S_QF}, 6")
-        self.e(f"s_sub_u32 s{T}, s{sarg('nqt')}, s{T}")
-        self.e(f"s_mul_i32 s{S_TOT}, s{T}, s{sarg('group')}")
-        self.e(f"s_mov_b32 s{S_IT}, 0")
-        self.e(f"s_mov_b32 s{S_CQ0}, s{S_QF}")
-        self.e(f"s_mov_b32 s{S_DIT}, 0")
-        self.e(f"s_mov_b32 s{S_DQ0}, s{S_QF}")
-        self.e(f"s_mul_i32 s{S_DHQ}, s{S_HK}, s{sarg('group')}")
+        # first item: compute state, its K / V, and the DMA stream primed with its first tiles
+        self.compute_item_setup()
+        self.kv_load(A_KF, A_VF, S_SOFFK, S_SOFFV)
+        self.e(f"s_mov_b32 s{S_DU}, s{S_U}")
+        self.pending_item_setup()
         self.pending_soffs()
-        # prime: tile 0 → buffer 0 (whole), tile 1 → buffer 1 (first half)
         for m0, ld in self.dma_first(0) + self.dma_second(0):
             self.e(m0)
             self.e(ld)
@@ -581,14 +719,9 @@ class FaDkdv:
         for m0, ld in self.dma_first(1):
             self.e(m0)
             self.e(ld)
-        self.e("s_waitcnt vmcnt(5)")
-        # K / V fragments → AGPRs; dKᵀ / dVᵀ = 0
-        for kk in range(8):
-            for j in range(4):
-                self.e(f"v_accvgpr_write_b32 a{A_KF + 4 * kk + j}, v{48 + 4 * kk + j}")
-                self.e(f"v_accvgpr_write_b32 a{A_VF + 4 * kk + j}, v{80 + 4 * kk + j}")
         for i in range(128):
             self.e(f"v_accvgpr_write_b32 a{i}, 0")
+        self.e("s_waitcnt vmcnt(5)")
         self.e("s_barrier")
         for _, txt in self.stats_reads(0):
             self.e(txt)
@@ -598,53 +731,24 @@ class FaDkdv:
         self.e("s_waitcnt lgkmcnt(0)")
         self.e("s_nop 4")
 
-    def epilogue(self):
-        T = S_T
-        self.e("s_waitcnt vmcnt(0) lgkmcnt(0)")
-        self.e("s_nop 15")
-        self.e("s_nop 15")
-        # dK = scale · dKᵀ, dV = dVᵀ, bf16; lane = key, 4 consecutive dims d0 = 32dt + 8g4 + 4hh
-        self.srd(SRD_Q, sarg("dk"), sarg("k_bytes"))
-        self.srd(SRD_O, sarg("dv"), sarg("v_bytes"))
-        t = V_TMP
-        L = V_LANE
-        self.e(f"v_and_b32 v{t}, 31, v{L}")
-        self.e(f"s_lshl_b32 s{T}, s{S_W}, 5")
-        self.e(f"v_add_u32 v{t}, s{T}, v{t}")
-        self.e(f"v_lshrrev_b32 v{t + 1}, 5, v{L}")
-        self.e(f"v_lshlrev_b32 v{t + 1}, 3, v{t + 1}")            # 8hh bytes
-        self.e(f"v_mad_u32_u24 v{t + 2}, v{t}, s{sarg('sks')}, v{t + 1}")
-        self.e(f"v_mad_u32_u24 v{t + 3}, v{t}, s{sarg('svs')}, v{t + 1}")
-        for dt in range(4):
-            for g4 in range(4):
-                for which in (0, 1):
-                    a0 = (A_DK if which == 0 else A_DV) + 16 * dt + 4 * g4
-                    for j in range(4):
-                        self.e(f"v_accvgpr_read_b32 v{t + 4 + j}, a{a0 + j}")
-                    if which == 0:
-                        for j in range(4):
-                            self.e(f"v_mul_f32 v{t + 4 + j}, s{sarg('scale')}, v{t + 4 + j}")
-                    self.e(f"v_cvt_pk_bf16_f32 v{t + 4}, v{t + 4}, v{t + 5}")
-                    self.e(f"v_cvt_pk_bf16_f32 v{t + 5}, v{t + 6}, v{t + 7}")
-                    srd, vo, so = (SRD_Q, t + 2, S_SOFFK) if which == 0 else (SRD_O, t + 3, S_SOFFV)
-                    self.e(f"buffer_store_dwordx2 v[{t + 4}:{t + 5}], v{vo}, s[{srd}:{srd + 3}], s{so} offen offset:{64 * dt + 16 * g4}")
+    def exit(self):
+        # the LDS-DMA stream may still be landing (past-the-end tiles): LDS must stay ours until
+        # it has; the dK / dV stores need no wait
         self.e("s_waitcnt vmcnt(0)")
         self.e("s_endpgm")
 
     def text(self):
         self.lines = []
-        self.prologue()
         labs = [self.newlab(f"tile{b}") for b in range(3)]
-        epi = self.newlab("epi")
-        if "noloop" in ABL:
-            self.e(f"s_branch {epi}")
+        lexit = self.newlab("exit")
+        self.prologue(lexit)
         self.in_loop = True
         for b in range(3):
             self.lab(labs[b])
-            self.emit_body(b, labs[(b + 1) % 3] if b == 2 else None, epi)
+            self.emit_body(b, labs[(b + 1) % 3], lexit)
         self.in_loop = False
-        self.lab(epi)
-        self.epilogue()
+        self.lab(lexit)
+        self.exit()
         n = self.name
         head = ["\t.text", f"\t.globl {n}", "\t.p2align 8", f"\t.type {n},@function", f"{n}:"]
         tail = [

@@ -8,6 +8,7 @@
 #include "common.h"
 #include "fa_args.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <mutex>
@@ -26,10 +27,9 @@ struct __attribute__((packed)) FaDkdvArgs {
   unsigned sos, soh, sob;        // .. 128
   unsigned Hq, Hk, group, Sq;    // 132 ..
   int coff;                      // 148
-  unsigned nqt, HB, causal;      // 152, 156, 160
-  float c, scale, rcp_HB, rcp_Hk;  // 164 .. 176
-  unsigned pad0;                 // 180
-  unsigned long long pad1;       // 184
+  unsigned nqt, npair, nkb1;     // 152, 156, 160: key blocks nkb = Sk/128 = 2·npair
+  float c, scale, rcp_npair, rcp_Hk;  // 164 .. 176
+  unsigned nitems, G, G2m1;      // 180: items (= nkb·Hk·B), grid (multiple of 8), 2G − 1
 };
 static_assert(sizeof(FaDkdvArgs) == 192, "FaDkdvArgs layout");
 
@@ -52,6 +52,17 @@ unsigned long long extent(long long sb, long long ss, long long sh, int B, int S
   const unsigned long long e = ((unsigned long long)(B - 1) * sb + (unsigned long long)(S - 1) * ss +
                                 (unsigned long long)(H - 1) * sh + 128) * 2ull;
   return e < (1ull << 31) ? e : 0;
+}
+
+int num_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
 }
 
 bool stride_ok(long long s) { return s > 0 && (s * 2) % 16 == 0 && s * 2 < (1ll << 24); }
@@ -83,7 +94,7 @@ PIAMD_EXPORT int piamd_fa_asm_enable(int on) {
 PIAMD_EXPORT int piamd_fa_asm_applies(const FaArgs* ap) {
   const FaArgs& a = *ap;
   if (!g_mod || !enabled()) return 0;
-  if (a.D != 128 || a.cu_q || a.mask || a.p_drop > 0.f || a.Sq != a.Sk || a.Sq % 128) return 0;
+  if (a.D != 128 || a.cu_q || a.mask || a.p_drop > 0.f || a.Sq != a.Sk || a.Sq % 256) return 0;
   if (a.Hk <= 0 || a.Hq % a.Hk || a.B <= 0) return 0;
   // seq strides feed 24-bit multiplies; every stride keeps 16-byte rows (LDS-DMA / dwordx4)
   for (long long s : {a.sqs, a.sks, a.svs, a.sos})
@@ -131,13 +142,20 @@ int fa_dkdv_asm(const FaArgs& a, hipStream_t st) {
   g.Sq = a.Sq;
   g.coff = a.Sk - a.Sq;
   g.nqt = a.Sq / 64;
-  g.HB = a.Hk * a.B;
-  g.causal = a.causal ? 1 : 0;
+  const unsigned nkb = (unsigned)(a.Sk / 128);
+  g.npair = nkb / 2;
+  g.nkb1 = nkb - 1;
   g.c = a.scale * 1.4426950408889634f;
   g.scale = a.scale;
-  g.rcp_HB = 1.f / (float)g.HB;
+  g.rcp_npair = 1.f / (float)g.npair;
   g.rcp_Hk = 1.f / (float)a.Hk;
-  const unsigned grid = (unsigned)((a.Sk / 128) * g.HB);
+  // persistent: one workgroup per CU (LDS / register bound); workgroup v takes the key-block
+  // pairs (j, nkb−1−j) of pair-members v, v + G, … (fa_gen.py decode / next_item)
+  g.nitems = nkb * (unsigned)a.Hk * (unsigned)a.B;
+  const unsigned members = g.nitems / 2;
+  g.G = std::min<unsigned>((unsigned)num_cus() / 8 * 8, (members + 7) / 8 * 8);
+  g.G2m1 = 2 * g.G - 1;
+  const unsigned grid = g.G;
   size_t sz = sizeof(g);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &g, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
   hipError_t err = hipModuleLaunchKernel(g_fn[a.causal ? 1 : 0], grid, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);

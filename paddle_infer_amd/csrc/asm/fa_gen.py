@@ -124,7 +124,6 @@ class FaDkdv:
             if (("nodma" in ABL and m.startswith("buffer_load") and s.endswith(" lds"))
                     or ("nobar" in ABL and m == "s_barrier")
                     or ("novmwait" in ABL and (m == "s_barrier" or s.startswith("s_waitcnt vmcnt")))
-                    or ("novalu" in ABL and m in ("v_mul_f32", "v_exp_f32", "v_cvt_pk_bf16_f32"))
                     or ("noreads" in ABL and (m.startswith("ds_read") or s.startswith("s_waitcnt lgkmcnt")))):
                 return
             if "nomfma" in ABL and m.startswith("v_mfma"):
@@ -525,6 +524,8 @@ class FaDkdv:
             gaps[g] += [("txt", m0), ("txt", ld)]
             fixed[g] += 12
         valu = self.schedule_valu(fixed)
+        if "novalu" in ABL:  # measurement only: no softmax work (control flow untouched)
+            valu = [[] for _ in range(64)]
         ops = []
         for m in range(64):
             kind, x, y = self.mfma_kind(m)

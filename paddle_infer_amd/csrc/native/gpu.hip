@@ -3,6 +3,7 @@
 // broadcast, row softmax, n-d strided copies for the layout ops, row gathers, casts). LayerNorm
 // is the framework's kernel (libpiamd_kernels.so); the 16-bit GEMMs, attention and fused
 // transformer ops run on the framework's kernels in fast_ops.hip; f32 GEMMs go to rocBLAS.
+#include <atomic>
 #include <hip/hip_runtime.h>
 #include <rocblas/rocblas.h>
 
@@ -73,8 +74,11 @@ void dev_copy(void* dst, const void* src, size_t bytes, int kind, Ctx& c) {
 
 void dev_sync(Ctx& c) { HIPCHK(hipStreamSynchronize((hipStream_t)c.stream)); }
 
+static std::atomic<long> g_graph_captures{0};
+
 void graph_begin(Ctx& c, std::vector<std::shared_ptr<Buffer>>* keep) {
   g_capture_keep = keep;
+  g_graph_captures.fetch_add(1);
   HIPCHK(hipStreamBeginCapture((hipStream_t)c.stream, hipStreamCaptureModeRelaxed));
 }
 
@@ -520,3 +524,9 @@ void channel_affine(Ctx& c, const float* x, const float* sc, const float* sh, fl
 
 }  // namespace gpu
 }  // namespace pdn
+
+// hipGraph captures started by this process (tests: the predictor's graph LRU replays instead of
+// re-capturing when feed signatures alternate)
+extern "C" __attribute__((visibility("default"))) long piamd_native_graph_captures() {
+  return pdn::g_graph_captures.load();
+}

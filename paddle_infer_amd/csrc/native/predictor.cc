@@ -1,6 +1,7 @@
 // paddle_infer::Predictor on the native engine: load + validate the program, keep parameters
 // resident on the predictor's device, run block 0 op by op, expose feed / fetch handles.
 #include <algorithm>
+#include <list>
 #include <set>
 #include <unordered_set>
 #include <fstream>
@@ -124,12 +125,9 @@ class PredictorImpl {
         pdn::dev_sync(ctx);
       } catch (...) {
       }
-      pdn::graph_destroy(graph);  // before the buffers it references are freed
-      graph = nullptr;
+      drop_graphs();
     }
     scope.clear();
-    graph_scope.clear();
-    graph_keep.clear();
     if (ctx.gpu) {
       params.clear();
       pdn::fast_release(ctx);
@@ -154,11 +152,31 @@ class PredictorImpl {
   // ShareExternalData, its address: the captured kernels read and write (CacheKV) that address,
   // so a new pointer is a new capture, never a copy into the old one. A signature whose capture
   // failed (an op that reads device data back on the host) runs eagerly from then on.
-  void* graph = nullptr;
-  std::string graph_key;
+  // Captures are kept in a small LRU (PIAMD_GRAPH_CACHE entries, default 4): a serving loop that
+  // alternates signatures — two KV-cache buffers, prefill / decode shapes — replays each graph
+  // instead of re-capturing on every switch.
+  struct GraphEntry {
+    std::string key;
+    void* graph = nullptr;
+    pdn::Scope scope;
+    std::vector<std::shared_ptr<pdn::Buffer>> keep;  // every buffer the captured kernels touch
+  };
+  std::list<GraphEntry> graphs;  // most recently used first (list nodes: stable addresses)
   std::set<std::string> graph_failed;
-  pdn::Scope graph_scope;
-  std::vector<std::shared_ptr<pdn::Buffer>> graph_keep;  // every buffer the captured kernels touch
+
+  static size_t graph_capacity() {
+    static const size_t cap = [] {
+      const char* e = getenv("PIAMD_GRAPH_CACHE");
+      const long v = e ? atol(e) : 4;
+      return (size_t)(v < 1 ? 1 : v);
+    }();
+    return cap;
+  }
+
+  void drop_graphs() {
+    for (auto& g : graphs) pdn::graph_destroy(g.graph);  // before the buffers they reference go
+    graphs.clear();
+  }
 
   bool run() {
     for (auto& kv : params) scope[kv.first] = kv.second;
@@ -180,20 +198,19 @@ class PredictorImpl {
       pdn::dev_sync(ctx);
       return true;
     }
-    if (key != graph_key) {
+    auto hit = graphs.begin();
+    while (hit != graphs.end() && hit->key != key) ++hit;
+    if (hit == graphs.end()) {
       run_ops(scope);  // warm-up: weight copies, workspaces, code-object load
       pdn::dev_sync(ctx);
-      pdn::graph_destroy(graph);
-      graph = nullptr;
-      graph_key.clear();
-      graph_scope.clear();
-      graph_keep.clear();
-      for (auto& kv : params) graph_scope[kv.first] = kv.second;
-      for (auto& f : feeds) graph_scope[f] = tensor(f);
-      pdn::graph_begin(ctx, &graph_keep);
+      graphs.emplace_front();
+      GraphEntry& e = graphs.front();
+      for (auto& kv : params) e.scope[kv.first] = kv.second;
+      for (auto& f : feeds) e.scope[f] = tensor(f);
+      pdn::graph_begin(ctx, &e.keep);
       bool ok = true;
       try {
-        run_ops(graph_scope);
+        run_ops(e.scope);
       } catch (...) {
         ok = false;
       }
@@ -207,27 +224,35 @@ class PredictorImpl {
         // the warm-up above already produced this Run's outputs eagerly
         pdn::graph_destroy(g);
         pdn::dev_reset_capture(ctx);
-        graph_scope.clear();
-        graph_keep.clear();
+        graphs.pop_front();
         graph_failed.insert(key);
         return true;
       }
-      graph = g;
-      graph_key = key;
+      e.graph = g;
+      e.key = key;
+      while (graphs.size() > graph_capacity()) {
+        pdn::graph_destroy(graphs.back().graph);
+        graphs.pop_back();
+      }
     } else {
+      if (hit != graphs.begin()) graphs.splice(graphs.begin(), graphs, hit);
+      GraphEntry& e = graphs.front();
       for (auto& f : feeds) {
         auto& src = tensor(f);
-        auto& dst = graph_scope.at(f);
+        auto& dst = e.scope.at(f);
         // owned buffers only: a shared external pointer is part of the key (same pointer here)
         if (src.buf != dst.buf && src.buf->owned && dst.buf->owned)
           pdn::dev_copy(dst.buf->p, src.buf->p, src.nbytes(), 2, ctx);
       }
     }
-    pdn::graph_launch(ctx, graph);
-    for (auto& f : fetches) scope[f] = graph_scope.at(f);
+    GraphEntry& e = graphs.front();
+    pdn::graph_launch(ctx, e.graph);
+    for (auto& f : fetches) scope[f] = e.scope.at(f);
     pdn::dev_sync(ctx);
     return true;
   }
+
+  size_t graph_count() const { return graphs.size(); }
 
   pdn::DTensor& tensor(const std::string& n) {
     auto it = scope.find(n);

@@ -235,6 +235,9 @@ _SIGS["piamd_small_gemm"] = [c_int, c_void_p, c_ll, c_void_p, c_ll, c_void_p, c_
 _SIGS["piamd_small_gemm_ln"] = _SIGS["piamd_small_gemm"][:-1] + [c_void_p, c_void_p, c_float, c_void_p]
 _SIGS["piamd_agemm_loaded"] = []
 _SIGS["piamd_fa_asm_load"] = [ctypes.c_char_p]
+_SIGS["piamd_viterbi_decode"] = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
 _SIGS["piamd_fa_asm_loaded"] = []
 _SIGS["piamd_fa_asm_enable"] = [ctypes.c_int]
 _SIGS["piamd_fa_asm_applies"] = [ctypes.c_void_p]

@@ -16,6 +16,8 @@ def viterbi_decode(potentials, transition_params, lengths, include_bos_eos_tag=T
     (scores [B], paths [B, T_max]) — batched max-product dynamic programming on the device.
     With ``include_bos_eos_tag`` the last two tags are BOS / EOS (reference convention)."""
     B, T, N = potentials.shape
+    if potentials.is_cuda:
+        return _viterbi_device(potentials, transition_params, lengths, include_bos_eos_tag)
     trans = transition_params
     lengths = lengths.long()
     alpha = potentials[:, 0].clone()
@@ -40,6 +42,24 @@ def viterbi_decode(potentials, transition_params, lengths, include_bos_eos_tag=T
     path = torch.stack(path[::-1], 1)[:, :Tm]
     mask = torch.arange(Tm, device=path.device)[None, :] < lengths[:, None]
     return scores, torch.where(mask, path, torch.zeros_like(path))
+
+
+def _viterbi_device(potentials, transition_params, lengths, include_bos_eos_tag):
+    """One launch of `csrc/kernels/viterbi.hip` (workgroup per sequence, scores in LDS, device
+    backtrace); the only host read is max(lengths) for the output width."""
+    from ..ops import _lib
+    pot = potentials.float().contiguous()
+    tr = transition_params.to(device=pot.device, dtype=torch.float32).contiguous()
+    ln = lengths.to(device=pot.device, dtype=torch.int64).contiguous()
+    B, T, N = pot.shape
+    scores = torch.empty(B, device=pot.device, dtype=torch.float32)
+    path = torch.empty(B, T, device=pot.device, dtype=torch.int64)
+    hist = torch.empty(B, max(T, 1), N, device=pot.device, dtype=torch.int32)
+    _lib.call("piamd_viterbi_decode", pot.data_ptr(), tr.data_ptr(), ln.data_ptr(), B, T, N,
+              int(bool(include_bos_eos_tag)), scores.data_ptr(), path.data_ptr(), hist.data_ptr(),
+              _lib.stream())
+    Tm = int(ln.max().item()) if B else 0
+    return scores, path[:, :Tm]
 
 
 class ViterbiDecoder(Layer):

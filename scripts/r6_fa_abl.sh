@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 OUT=$GRAFT_REPO_ROOT/gpurun_out/r6_abl
 mkdir -p $OUT
 cd /tmp
-for n in full nodma nobar novmwait novalu noreads nomfma noloop nodma_novalu_noreads; do
+for n in ${ABL_LIST:-full nodma nobar novalu noreads nomfma}; do
   PIAMD_FA_HSACO=$GRAFT_REPO_ROOT/paddle_infer_amd/_lib/abl/fa_$n.hsaco timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $OUT/$n -o run -- python $GRAFT_REPO_ROOT/tools/bench_attn.py --no-sdpa --shapes "96,1024,16,128" > $OUT/$n.log 2>&1 || { echo "$n failed"; tail -5 $OUT/$n.log; exit 1; }
   echo "$n $(python $GRAFT_REPO_ROOT/tools/rocpd_stats.py $OUT/$n/run_results.db | grep -E 'dkdv' | head -1)"
 done

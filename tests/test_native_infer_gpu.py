@@ -96,3 +96,32 @@ def p_out_name(path, i):
     from paddle_infer_amd import inference as pinf
     c = pinf.Config(path + ".pdmodel", path + ".pdiparams")
     return pinf.create_predictor(c).get_output_names()[i]
+
+
+def test_native_graph_lru_alternating_pointers(tmp_path):
+    """Two KV-cache-style feed buffers used alternately: the predictor keeps one captured graph
+    per signature (LRU) and replays it — 2 captures for 6 Runs, each Run's output follows the
+    buffer it was given."""
+    import ctypes
+    import torch
+    import native_capi as nc
+    path = str(tmp_path / "mlp")
+    export(MLP(), path, [InputSpec([None, 16], "float32", "x")])
+    xs = [np.random.RandomState(10 + i).randn(8, 16).astype("float32") for i in range(2)]
+    refs = [python_outputs(path, {"x": x}) for x in xs]
+    ts = [torch.from_numpy(x).cuda() for x in xs]
+    torch.cuda.synchronize()
+    p = nc.Predictor(path, gpu=0, hip_graph=True)
+    cap = nc.lib().piamd_native_graph_captures
+    cap.restype = ctypes.c_long
+    try:
+        before = cap()
+        for r in range(6):
+            i = r % 2
+            p.share("x", ts[i])
+            p.run()
+            got = p.fetch_float(p_out_name(path, 0), refs[i][0].shape)
+            np.testing.assert_allclose(got, refs[i][0], rtol=2e-3, atol=2e-4)
+        assert cap() - before == 2, f"captures: {cap() - before}"
+    finally:
+        p.close()

@@ -104,6 +104,9 @@ MFMA = "v_mfma_f32_32x32x16_bf16"
 # ablation builds for measurement only (numerically wrong): nodma / nobar / novmwait / novalu /
 # noreads / nomfma drop that part of the tile loop
 ABL = set(filter(None, os.environ.get("PIAMD_FA_ABL", "").split(",")))
+# timestamp build (measurement only): s_memtime at 6 points of every tile, written over dV
+# ([wg][wave][tile < 256][8] u64; the dV output itself is not written) — tools/fa_stamps.py
+STAMP = os.environ.get("PIAMD_FA_STAMP", "0") == "1"
 
 
 def buf_set(b):
@@ -113,6 +116,8 @@ def buf_set(b):
 
 
 class FaDkdv:
+    VTMP_UDIV = V_TMP
+
     def __init__(self, name, causal):
         self.name, self.causal = name, causal
         self.lines = []
@@ -140,7 +145,7 @@ class FaDkdv:
     # -- helpers --------------------------------------------------------------------------------
     def udiv(self, q, r, n, d, rcp):
         """q = n / d, r = n % d (SGPRs, n < 2^24) from the f32 reciprocal in SGPR rcp, ±1 fixed."""
-        v = V_TMP
+        v = self.VTMP_UDIV
         self.e(f"v_cvt_f32_u32 v{v}, s{n}")
         self.e(f"v_mul_f32 v{v}, s{rcp}, v{v}")
         self.e(f"v_cvt_u32_f32 v{v}, v{v}")
@@ -329,7 +334,7 @@ class FaDkdv:
         t = V_TMP
         for dt in range(4):
             for g4 in range(4):
-                for which in (0, 1):
+                for which in ((0,) if STAMP else (0, 1)):
                     a0 = (A_DK if which == 0 else A_DV) + 16 * dt + 4 * g4
                     for j in range(4):
                         self.e(f"v_accvgpr_read_b32 v{t + 4 + j}, a{a0 + j}")
@@ -445,10 +450,10 @@ class FaDkdv:
         24 cycles (minus the gap's fixed LDS/DMA cost); a queue that would miss its deadline is
         forced. D-part pair j goes only after its S-part pair j (exp) sits in an earlier gap."""
         qs = self.finish_queues()
-        gaps = [[] for _ in range(64)]
+        gaps = [[] for _ in range(len(fixed_cost))]
         heads = [0] * len(qs)
         s_done_gap = [dict() for _ in qs]       # queue → pair → gap of its last op
-        for g in range(64):
+        for g in range(len(fixed_cost)):
             budget = 24 - fixed_cost[g]
             while True:
                 cand = []
@@ -510,8 +515,14 @@ class FaDkdv:
         gaps[13].append(("adv",))
         fixed[13] += 8
         # barrier after C0: tile t+1 landed (its DMA was issued one tile ago), buffer t−1 free
+        if STAMP:
+            gaps[15].append(("stamp", 1))
+            gaps[31].append(("stamp", 2))
+            gaps[47].append(("stamp", 3))
         gaps[47].append(("txt", "s_waitcnt vmcnt(0)"))
         gaps[47].append(("txt", "s_barrier"))
+        if STAMP:
+            gaps[47].append(("stamp", 4))
         fixed[47] += 8
         # next tile's row constants (after the softmax of this tile consumed S'/dP')
         for i, (key, t) in enumerate(self.stats_reads(nb)):
@@ -537,6 +548,14 @@ class FaDkdv:
             ops += [("txt", t) for t in valu[m]]
         return ops
 
+    def stamp(self, k):
+        """s_memtime → dV[(wg·4 + wave)·256 + tile][k] (STAMP builds; drains lgkmcnt)."""
+        self.e("s_memtime s[18:19]")
+        self.e("s_waitcnt lgkmcnt(0)")
+        self.e("v_mov_b32 v206, s18")
+        self.e("v_mov_b32 v207, s19")
+        self.e(f"buffer_store_dwordx2 v[206:207], v205, s[{SRD_DV}:{SRD_DV + 3}], s100 offen offset:{8 * k}")
+
     def emit_body(self, b, lab_next, lab_epi):
         prev = self.body_ops((b + 2) % 3)
         cur = self.body_ops(b)
@@ -550,6 +569,8 @@ class FaDkdv:
         pos = {k: i for i, k in enumerate(order)}
         done = 0                      # LDS ops [0, done) are known complete
         issued = len(order)
+        if STAMP:
+            self.stamp(0)
         # masked diagonal tiles: S' entries of (query < key) rows start at −inf
         if self.causal:
             skip = self.newlab("nomask")
@@ -582,8 +603,20 @@ class FaDkdv:
                 self.e(ent[3])
             elif ent[0] == "adv":
                 self.advance_pending()
+            elif ent[0] == "stamp":
+                self.stamp(ent[1])
+                done = issued
             else:
                 self.e(ent[1])
+        if STAMP:
+            self.stamp(5)
+            self.e("s_add_u32 s3, s3, 1")
+            self.e("s_min_u32 s3, s3, 255")
+            self.e(f"s_lshl_b32 s100, s{S_WG}, 2")
+            self.e(f"s_add_u32 s100, s100, s{S_W}")
+            self.e("s_lshl_b32 s100, s100, 8")
+            self.e("s_add_u32 s100, s100, s3")
+            self.e("s_lshl_b32 s100, s100, 6")
         # tile bookkeeping: next tile of this item, K/V prefetch after the item's first tile,
         # item switch after its last
         self.e(f"s_add_u32 s{S_IT}, s{S_IT}, 1")
@@ -707,6 +740,12 @@ class FaDkdv:
         self.e(f"v_lshlrev_b32 v{t + 2}, 4, v{t + 1}")
         self.e(f"v_add_u32 v{V_STB}, {OFF_ST}, v{t + 2}")
         self.e(f"v_add_u32 v{V_STB + 1}, {2 * BUF_B + OFF_ST}, v{t + 2}")
+        if STAMP:
+            self.e("s_mov_b32 s3, 0")
+            self.e(f"s_lshl_b32 s100, s{S_WG}, 2")
+            self.e(f"s_add_u32 s100, s100, s{S_W}")
+            self.e("s_lshl_b32 s100, s100, 14")
+            self.e("v_mov_b32 v205, 0")
         # first item: compute state, its K / V, and the DMA stream primed with its first tiles
         self.compute_item_setup()
         self.kv_load(A_KF, A_VF, S_SOFFK, S_SOFFV)
@@ -799,8 +838,572 @@ class FaDkdv:
 """
 
 
+
+# =================================================================================================
+# dQ kernel (`fa_dq`): the same machine with the roles of (Q, dO) and (K, V) swapped
+# =================================================================================================
+# workgroup = 128 queries of one (batch, q-head), 4 waves × 32 queries (query on the MFMA lane);
+# for every 64-key tile (causal: up to the diagonal) of the head's kv-head:
+#   Sᵀ = K·Qᵀ,  dPᵀ = V·dOᵀ        (A = K / V rows from LDS, B = Q / dO fragments in AGPRs)
+#   P = exp2(c·Sᵀ + c·(−lse/scale)_q),  dS = P ∘ (dPᵀ − δ_q)   (row constants are PER LANE here)
+#   dQᵀ += Kᵀ·dS                    (A = transposed K reads, B = dS fragments; dQ · scale at the end)
+# Causal masking costs nothing per element: the first S MFMA of a diagonal tile starts from a
+# 0 / −inf pattern register set instead of 0 (set between tiles, only for the last two tiles of an
+# item). 48 MFMAs per tile: S(kb 0) P(kb 0) S(kb 1) P(kb 1) [8 each], C(ks 0,1) C(ks 2,3) [8 each].
+DQ_ARGS = [
+    ("q", 0, 8), ("k", 8, 8), ("v", 16, 8), ("dout", 24, 8), ("dq", 32, 8), ("pad0", 40, 8),
+    ("nl", 48, 8), ("nd", 56, 8),
+    ("q_bytes", 64, 4), ("k_bytes", 68, 4), ("v_bytes", 72, 4), ("o_bytes", 76, 4), ("st_bytes", 80, 4),
+    ("sqs", 84, 4), ("sqh", 88, 4), ("sqb", 92, 4),
+    ("sks", 96, 4), ("skh", 100, 4), ("skb", 104, 4),
+    ("svs", 108, 4), ("svh", 112, 4), ("svb", 116, 4),
+    ("sos", 120, 4), ("soh", 124, 4), ("sob", 128, 4),
+    ("Hq", 132, 4), ("group", 136, 4), ("rcp_group", 140, 4), ("Sq", 144, 4), ("nkt", 148, 4),
+    ("npair", 152, 4), ("nqb1", 156, 4), ("rcp_npair", 160, 4), ("c", 164, 4), ("scale", 168, 4),
+    ("rcp_Hq", 172, 4), ("pad1", 176, 4), ("nitems", 180, 4), ("G", 184, 4), ("G2m1", 188, 4),
+]
+
+
+def qarg(name):
+    for n, off, _ in DQ_ARGS:
+        if n == name:
+            return 4 + off // 4
+    raise KeyError(name)
+
+
+# SGPRs (s4..s19: pointer arguments until the descriptors exist)
+Q_SOB, Q_SKB, Q_SVB, Q_W, Q_LDSW = 4, 5, 6, 7, 8          # DMA-side batch/head bases, wave, LDS
+Q_T = 10                                                  # temps s10..s17
+QSRD_K, QSRD_V, QSRD_Q, QSRD_O, QSRD_DQ, QSRD_NL, QSRD_ND = 52, 56, 60, 64, 68, 72, 76
+# compute side: item, batch, q-head, query-block start, tiles, tile index, Q/dO/dQ soffset, stats soffset
+Q_U, Q_B, Q_HQ, Q_Q0, Q_TOT, Q_IT, Q_SOFFQ, Q_SOFFO, Q_SOFFS = range(80, 89)
+# DMA side: item, its tile count, tile index, key start, K / V soffsets
+Q_DU, Q_DTOT, Q_DIT, Q_DK0, Q_SK, Q_SV = range(89, 95)
+Q_NSGPR = 101
+
+QV_DK, QV_DV = 2, 6                # LDS-DMA lane offsets: K pieces 0-3, V pieces 0-3
+QV_ROW, QV_TR = 11, 27             # [set 2][kk 8] / [set 2][jj 2][dt 4] read offsets
+QV_QL, QV_THR, QV_NINF = 45, 46, 47
+QV_RING = 48                       # 12 slots × 4
+QV_SACC, QV_PACC = 96, 128         # Sᵀ / dPᵀ accumulators [kb 2][16]
+QV_DS = 160                        # dS bf16 fragments [ks 4][4]
+QV_MASK = 176                      # first-S-MFMA accumulator inputs [kb 2][16] (0 / −inf)
+QV_TMP = 208                       # temps v208..v215
+QV_NLC, QV_ND, QV_NLCN, QV_NDN = 216, 217, 218, 219   # c·(−lse/scale), −δ (current / next item)
+QV_QV, QV_OV, QV_STQ, QV_STV4 = 220, 221, 222, 223    # Q / dO fragment, dQ store, stats lane offsets
+QV_NDSET = 224                     # −δ of the lane's query × 16: accumulator start of the first dP MFMA
+QNV = 240
+QA_DQ, QA_QF, QA_OF, QA_QN, QA_ON = 0, 64, 96, 128, 160
+QNA = 192
+QBUF_B = 32768                     # per buffer: K 16 KiB, V 16 KiB
+Q_OFF_V = 16384
+QLDS_BYTES = 3 * QBUF_B
+QLA = 6
+
+
+def qbuf_set(b):
+    return (0, 0) if b == 0 else (0, QBUF_B) if b == 1 else (1, 0)
+
+
+class FaDq(FaDkdv):
+    NM = 48
+    VTMP_UDIV = QV_TMP + 4
+
+    # -- DMA stream (K / V tiles of 64 keys) --------------------------------------------------------
+    def pending_soffs(self):
+        T = Q_T
+        self.e(f"s_mul_i32 s{T}, s{Q_DK0}, s{qarg('sks')}")
+        self.e(f"s_add_u32 s{Q_SK}, s{T}, s{Q_SKB}")
+        self.e(f"s_mul_i32 s{T}, s{Q_DK0}, s{qarg('svs')}")
+        self.e(f"s_add_u32 s{Q_SV}, s{T}, s{Q_SVB}")
+        self.e(f"s_cmp_ge_u32 s{Q_DU}, s{qarg('nitems')}")
+        self.e(f"s_cselect_b32 s{Q_SK}, s{qarg('k_bytes')}, s{Q_SK}")
+        self.e(f"s_cselect_b32 s{Q_SV}, s{qarg('v_bytes')}, s{Q_SV}")
+
+    def advance_pending(self):
+        self.e(f"s_add_u32 s{Q_DIT}, s{Q_DIT}, 1")
+        self.e(f"s_add_u32 s{Q_DK0}, s{Q_DK0}, 64")
+        same = self.newlab("sameitem")
+        self.e(f"s_cmp_lt_u32 s{Q_DIT}, s{Q_DTOT}")
+        self.e(f"s_cbranch_scc1 {same}")
+        self.next_item(Q_DU)
+        self.e(f"s_cmp_ge_u32 s{Q_DU}, s{qarg('nitems')}")
+        self.e(f"s_cbranch_scc1 {same}")
+        self.pending_item_setup()
+        self.lab(same)
+        self.pending_soffs()
+
+    def next_item(self, u):
+        T = Q_T
+        self.e(f"s_bitcmp1_b32 s{u}, 0")
+        self.e(f"s_cselect_b32 s{T + 7}, s{qarg('G2m1')}, 1")
+        self.e(f"s_add_u32 s{u}, s{u}, s{T + 7}")
+
+    def decode(self, u, qb, b, hq):
+        """Item u = 2·member + s → query block qb (pairs (j, nqb−1−j): equal causal work), batch
+        b, q-head hq; a pair group = one (batch, q-head), its members on one XCD."""
+        T = Q_T
+        self.e(f"s_lshr_b32 s{T + 7}, s{u}, 1")
+        self.udiv(T + 6, qb, T + 7, qarg("npair"), qarg("rcp_npair"))      # group, j
+        self.e(f"s_sub_u32 s{T + 7}, s{qarg('nqb1')}, s{qb}")
+        self.e(f"s_bitcmp1_b32 s{u}, 0")
+        self.e(f"s_cselect_b32 s{qb}, s{T + 7}, s{qb}")
+        self.udiv(b, hq, T + 6, qarg("Hq"), qarg("rcp_Hq"))
+
+    def tiles_of(self, dst, qb):
+        if self.causal:
+            self.e(f"s_lshl_b32 s{dst}, s{qb}, 1")
+            self.e(f"s_add_u32 s{dst}, s{dst}, 2")
+        else:
+            self.e(f"s_mov_b32 s{dst}, s{qarg('nkt')}")
+
+    def kv_bases(self, b, hq, kb, vb):
+        """K / V soffset bases of (batch b, kv-head hq / group)."""
+        T = Q_T
+        self.udiv(T + 3, T + 4, hq, qarg("group"), qarg("rcp_group"))   # hk → s{T+3}
+        for dst, sb, sh in ((kb, "skb", "skh"), (vb, "svb", "svh")):
+            self.e(f"s_mul_i32 s{dst}, s{b}, s{qarg(sb)}")
+            self.e(f"s_mul_i32 s{T + 4}, s{T + 3}, s{qarg(sh)}")
+            self.e(f"s_add_u32 s{dst}, s{dst}, s{T + 4}")
+
+    def pending_item_setup(self):
+        T = Q_T
+        self.decode(Q_DU, T, T + 1, T + 2)
+        self.tiles_of(Q_DTOT, T)
+        self.e(f"s_mov_b32 s{Q_DIT}, 0")
+        self.e(f"s_mov_b32 s{Q_DK0}, 0")
+        self.kv_bases(T + 1, T + 2, Q_SKB, Q_SVB)
+
+    def dma_first(self, buf):
+        base = buf * QBUF_B
+        return [[f"s_add_u32 m0, s{Q_LDSW}, {base + i * 1024}\n\ts_nop 0",
+                 f"buffer_load_dwordx4 v{QV_DK + i}, s[{QSRD_K}:{QSRD_K + 3}], s{Q_SK} offen lds"]
+                for i in range(4)]
+
+    def dma_second(self, buf):
+        base = buf * QBUF_B + Q_OFF_V
+        return [[f"s_add_u32 m0, s{Q_LDSW}, {base + i * 1024}\n\ts_nop 0",
+                 f"buffer_load_dwordx4 v{QV_DV + i}, s[{QSRD_V}:{QSRD_V + 3}], s{Q_SV} offen lds"]
+                for i in range(4)]
+
+    # -- items: Q / dO fragments + per-lane row constants -------------------------------------------
+    def q_soffs(self, qb, b, hq, sq, so, ss):
+        """Q/dQ, dO and stats soffsets of the wave's 32 queries of item (qb, b, hq)."""
+        T = Q_T
+        self.e(f"s_lshl_b32 s{T + 7}, s{qb}, 7")                        # q0 = 128 qb
+        for dst, sb, sh, st in ((sq, "sqb", "sqh", "sqs"), (so, "sob", "soh", "sos")):
+            self.e(f"s_mul_i32 s{dst}, s{b}, s{qarg(sb)}")
+            self.e(f"s_mul_i32 s{T + 5}, s{hq}, s{qarg(sh)}")
+            self.e(f"s_add_u32 s{dst}, s{dst}, s{T + 5}")
+            self.e(f"s_mul_i32 s{T + 5}, s{T + 7}, s{qarg(st)}")
+            self.e(f"s_add_u32 s{dst}, s{dst}, s{T + 5}")
+        self.e(f"s_mul_i32 s{ss}, s{b}, s{qarg('Hq')}")
+        self.e(f"s_add_u32 s{ss}, s{ss}, s{hq}")
+        self.e(f"s_mul_i32 s{ss}, s{ss}, s{qarg('Sq')}")
+        self.e(f"s_add_u32 s{ss}, s{ss}, s{T + 7}")
+        self.e(f"s_lshl_b32 s{ss}, s{ss}, 2")
+
+    def q_load(self, aq, ao, nl, nd, sq, so, ss):
+        for kk in range(8):
+            self.e(f"buffer_load_dwordx4 a[{aq + 4 * kk}:{aq + 4 * kk + 3}], v{QV_QV}, s[{QSRD_Q}:{QSRD_Q + 3}], s{sq} offen offset:{32 * kk}")
+        for kk in range(8):
+            self.e(f"buffer_load_dwordx4 a[{ao + 4 * kk}:{ao + 4 * kk + 3}], v{QV_OV}, s[{QSRD_O}:{QSRD_O + 3}], s{so} offen offset:{32 * kk}")
+        self.e(f"buffer_load_dword v{nl}, v{QV_STV4}, s[{QSRD_NL}:{QSRD_NL + 3}], s{ss} offen")
+        self.e(f"buffer_load_dword v{nd}, v{QV_STV4}, s[{QSRD_ND}:{QSRD_ND + 3}], s{ss} offen")
+
+    def compute_item_setup(self):
+        T = Q_T
+        self.decode(Q_U, T, Q_B, Q_HQ)
+        self.e(f"s_lshl_b32 s{Q_Q0}, s{T}, 7")
+        self.tiles_of(Q_TOT, T)
+        self.e(f"s_mov_b32 s{Q_IT}, 0")
+        self.q_soffs(T, Q_B, Q_HQ, Q_SOFFQ, Q_SOFFO, Q_SOFFS)
+        # causal threshold base: query − 4hh (lane), per item
+        self.e(f"s_lshl_b32 s{T}, s{Q_W}, 5")
+        self.e(f"s_add_u32 s{T}, s{T}, s{Q_Q0}")
+        self.e(f"v_add_u32 v{QV_QL}, s{T}, v{QV_TMP + 7}")              # v{TMP+7} = l32 − 4hh
+
+    def mask_setup(self):
+        """Accumulator-start pattern of the next tile's S MFMAs: 0, or −inf where key > query (the
+        last two tiles of a causal item)."""
+        if not self.causal:
+            return
+        T = Q_T
+        skip, done = self.newlab("nomask"), self.newlab("maskdone")
+        self.e(f"s_sub_u32 s{T}, s{Q_TOT}, 2")
+        self.e(f"s_cmp_lt_i32 s{Q_IT}, s{T}")
+        self.e(f"s_cbranch_scc1 {skip}")
+        self.e(f"s_lshl_b32 s{T}, s{Q_IT}, 6")
+        self.e(f"v_subrev_u32 v{QV_THR}, s{T}, v{QV_QL}")               # q − 4hh − 64 kt
+        for kb in (0, 1):
+            for g4 in range(4):
+                for e in range(4):
+                    ci = 32 * kb + 8 * g4 + e
+                    r = QV_MASK + 16 * kb + 4 * g4 + e
+                    self.e(f"v_cmp_gt_i32 vcc, {ci}, v{QV_THR}")
+                    self.e(f"v_cndmask_b32 v{r}, 0, v{QV_NINF}, vcc")
+        self.e(f"s_branch {done}")
+        self.lab(skip)
+        self.e(f"s_cmp_eq_u32 s{Q_IT}, 0")                              # item start: clear
+        self.e(f"s_cbranch_scc0 {done}")
+        for i in range(32):
+            self.e(f"v_mov_b32 v{QV_MASK + i}, 0")
+        self.lab(done)
+        self.e("s_nop 4")
+
+    def prefetch_next(self):
+        T = Q_T
+        skip = self.newlab("nopf")
+        self.e(f"s_mov_b32 s{T + 3}, s{Q_U}")
+        self.next_item(T + 3)
+        self.e(f"s_cmp_ge_u32 s{T + 3}, s{qarg('nitems')}")
+        self.e(f"s_cbranch_scc1 {skip}")
+        self.decode(T + 3, T, T + 1, T + 2)
+        self.q_soffs(T, T + 1, T + 2, T + 3, T + 4, T + 6)
+        self.q_load(QA_QN, QA_ON, QV_NLCN, QV_NDN, T + 3, T + 4, T + 6)
+        self.lab(skip)
+
+    def store_dq(self):
+        t = QV_TMP
+        for dt in range(4):
+            for g4 in range(4):
+                a0 = QA_DQ + 16 * dt + 4 * g4
+                for j in range(4):
+                    self.e(f"v_accvgpr_read_b32 v{t + j}, a{a0 + j}")
+                for j in range(4):
+                    self.e(f"v_mul_f32 v{t + j}, s{qarg('scale')}, v{t + j}")
+                self.e(f"v_cvt_pk_bf16_f32 v{t}, v{t}, v{t + 1}")
+                self.e(f"v_cvt_pk_bf16_f32 v{t + 1}, v{t + 2}, v{t + 3}")
+                self.e(f"buffer_store_dwordx2 v[{t}:{t + 1}], v{QV_STQ}, s[{QSRD_DQ}:{QSRD_DQ + 3}], s{Q_SOFFQ} offen offset:{64 * dt + 16 * g4}")
+
+    def item_end(self, lab_next, lab_exit):
+        self.e("s_nop 15")
+        self.e("s_nop 15")
+        self.store_dq()
+        for i in range(64):
+            self.e(f"v_accvgpr_write_b32 a{QA_DQ + i}, 0")
+        for i in range(64):
+            self.e(f"v_accvgpr_mov_b32 a{QA_QF + i}, a{QA_QN + i}")
+        self.e(f"v_mul_f32 v{QV_NLC}, s{qarg('c')}, v{QV_NLCN}")
+        for i in range(16):
+            self.e(f"v_mov_b32 v{QV_NDSET + i}, v{QV_NDN}")
+        self.next_item(Q_U)
+        self.e(f"s_cmp_ge_u32 s{Q_U}, s{qarg('nitems')}")
+        self.e(f"s_cbranch_scc1 {lab_exit}")
+        self.compute_item_setup()
+        self.mask_setup()
+        self.e("s_nop 4")
+        self.e(f"s_branch {lab_next}")
+
+    # -- MFMA stream --------------------------------------------------------------------------------
+    @staticmethod
+    def mfma_kind(m):
+        """MFMA m of a tile → ('S'|'P', kb, kk) or ('C', dt, ks)."""
+        if m < 32:
+            kb, r = m // 16, m % 16
+            return ("S" if r < 8 else "P", kb, r % 8)
+        c = m - 32
+        half, cc = c // 8, c % 8
+        return ("C", cc % 4, 2 * half + cc // 4)
+
+    @staticmethod
+    def slot(b, m):
+        return QV_RING + 4 * ((48 * b + m) % RING)
+
+    def ring_reads(self, b, m):
+        kind, x, y = self.mfma_kind(m)
+        s, imm = qbuf_set(b)
+        d = self.slot(b, m)
+        if kind in ("S", "P"):
+            kb, kk = x, y
+            off = imm + (Q_OFF_V if kind == "P" else 0) + kb * 8192
+            return [f"ds_read_b128 v[{d}:{d + 3}], v{QV_ROW + 8 * s + kk} offset:{off}"]
+        dt, ks = x, y
+        off = imm + ks * 16 * 256
+        return [f"ds_read_b64_tr_b16 v[{d + 2 * jj}:{d + 2 * jj + 1}], v{QV_TR + 8 * s + 4 * jj + dt} offset:{off}"
+                for jj in (0, 1)]
+
+    def mfma_text(self, b, m):
+        kind, x, y = self.mfma_kind(m)
+        a = self.slot(b, m)
+        if kind in ("S", "P"):
+            kb, kk = x, y
+            acc = (QV_SACC if kind == "S" else QV_PACC) + 16 * kb
+            bop = (QA_QF if kind == "S" else QA_OF) + 4 * kk
+            if kk == 0:
+                if kind == "P":   # dPᵀ − δ from the start
+                    src = f"v[{QV_NDSET}:{QV_NDSET + 15}]"
+                else:
+                    src = f"v[{QV_MASK + 16 * kb}:{QV_MASK + 16 * kb + 15}]" if self.causal else "0"
+            else:
+                src = f"v[{acc}:{acc + 15}]"
+            return f"{MFMA} v[{acc}:{acc + 15}], v[{a}:{a + 3}], a[{bop}:{bop + 3}], {src}"
+        dt, ks = x, y
+        acc = QA_DQ + 16 * dt
+        bop = QV_DS + 4 * ks
+        return f"{MFMA} a[{acc}:{acc + 15}], v[{a}:{a + 3}], v[{bop}:{bop + 3}], a[{acc}:{acc + 15}]"
+
+    def finish_queues(self):
+        qs = []
+        for kb in (0, 1):
+            sq, dq = [], []
+            for j in range(8):
+                s0, s1 = QV_SACC + 16 * kb + 2 * j, QV_SACC + 16 * kb + 2 * j + 1
+                d0, d1 = QV_PACC + 16 * kb + 2 * j, QV_PACC + 16 * kb + 2 * j + 1
+                sq += [(f"v_fma_f32 v{s0}, v{s0}, s{qarg('c')}, v{QV_NLC}", 4, j),
+                       (f"v_fma_f32 v{s1}, v{s1}, s{qarg('c')}, v{QV_NLC}", 4, j),
+                       (f"v_exp_f32 v{s0}, v{s0}", 8, j),
+                       (f"v_exp_f32 v{s1}, v{s1}", 8, j)]
+                fr = 4 * (2 * kb + j // 4) + j % 4
+                dq += [(f"v_mul_f32 v{d0}, v{s0}, v{d0}", 4, j),
+                       (f"v_mul_f32 v{d1}, v{s1}, v{d1}", 4, j),
+                       (f"v_cvt_pk_bf16_f32 v{QV_DS + fr}, v{d0}, v{d1}", 4, j)]
+            dl = 30 + 8 * kb
+            qs.append(dict(name=f"S{kb}", ops=sq, lo=16 * kb + 9, hi=dl - 2))
+            qs.append(dict(name=f"D{kb}", ops=dq, lo=16 * kb + 17, hi=dl, dep=len(qs) - 1))
+        return qs
+
+    def body_ops(self, b):
+        nb = (b + 1) % 3
+        NM = self.NM
+        gaps = [[] for _ in range(NM)]
+        fixed = [0] * NM
+        for m in range(NM):
+            g = m - QLA
+            if g >= 0:
+                for t in self.ring_reads(b, m):
+                    gaps[g].append(("lds", ("ring", 0, m), t))
+                    fixed[g] += 2
+        for m in range(QLA):
+            g = NM - QLA + m
+            for t in self.ring_reads(nb, m):
+                gaps[g].append(("lds", ("ring", 1, m), t))
+                fixed[g] += 2
+        # one barrier per tile: tile t+1 landed (its DMA went out one tile ago), buffer t−1 free;
+        # then the whole DMA of tile t+2 and the cursor advance
+        gaps[39].append(("txt", "s_waitcnt vmcnt(0)"))
+        gaps[39].append(("txt", "s_barrier"))
+        fixed[39] += 8
+        ops2 = self.dma_first((b + 2) % 3) + self.dma_second((b + 2) % 3)
+        for i, (m0, ld) in enumerate(ops2):
+            g = 40 + i
+            gaps[g] += [("txt", m0), ("txt", ld)]
+            fixed[g] += 12
+        gaps[47].append(("adv",))
+        fixed[47] += 8
+        valu = self.schedule_valu(fixed)
+        if "novalu" in ABL:
+            valu = [[] for _ in range(NM)]
+        ops = []
+        for m in range(NM):
+            ops.append(("mfma", m, [("ring", 0, m)], self.mfma_text(b, m)))
+            ops += gaps[m]
+            ops += [("txt", t) for t in valu[m]]
+        return ops
+
+    def emit_body(self, b, lab_next, lab_epi):
+        prev = self.body_ops((b + 2) % 3)
+        cur = self.body_ops(b)
+        order = []
+        for ent in prev:
+            if ent[0] == "lds":
+                kind, t, idx = ent[1]
+                order.append((kind, t - 1, idx))
+        pos = {k: i for i, k in enumerate(order)}
+        done = 0
+        issued = len(order)
+        for ent in cur:
+            if ent[0] == "lds":
+                pos[ent[1]] = issued
+                issued += 1
+                self.e(ent[2])
+            elif ent[0] == "mfma":
+                need = max(pos[d] for d in ent[2])
+                if need >= done:
+                    w = min(15, issued - 1 - need)
+                    self.e(f"s_waitcnt lgkmcnt({w})")
+                    done = issued - w
+                self.e(ent[3])
+            elif ent[0] == "adv":
+                self.advance_pending()
+            else:
+                self.e(ent[1])
+        self.e(f"s_add_u32 s{Q_IT}, s{Q_IT}, 1")
+        nopf = self.newlab("nopf")
+        self.e(f"s_cmp_eq_u32 s{Q_IT}, 1")
+        self.e(f"s_cbranch_scc0 {nopf}")
+        self.prefetch_next()
+        self.lab(nopf)
+        nxt = self.newlab("same")
+        self.e(f"s_cmp_lt_u32 s{Q_IT}, s{Q_TOT}")
+        self.e(f"s_cbranch_scc1 {nxt}")
+        self.item_end(lab_next, lab_epi)
+        self.lab(nxt)
+        self.mask_setup()
+        self.e(f"s_branch {lab_next}")
+
+    # -- prologue ---------------------------------------------------------------------------------------
+    def prologue(self, lab_exit):
+        T = Q_T
+        self.e("s_load_dwordx16 s[4:19], s[0:1], 0x0")
+        self.e("s_load_dwordx16 s[20:35], s[0:1], 0x40")
+        self.e("s_load_dwordx16 s[36:51], s[0:1], 0x80")
+        self.e(f"v_and_b32 v{V_LANE}, 63, v{V_TID}")
+        self.e(f"v_lshrrev_b32 v{QV_TMP}, 6, v{V_TID}")
+        self.e("s_waitcnt lgkmcnt(0)")
+        self.srd(QSRD_K, qarg("k"), qarg("k_bytes"))
+        self.srd(QSRD_V, qarg("v"), qarg("v_bytes"))
+        self.srd(QSRD_Q, qarg("q"), qarg("q_bytes"))
+        self.srd(QSRD_O, qarg("dout"), qarg("o_bytes"))
+        self.srd(QSRD_DQ, qarg("dq"), qarg("q_bytes"))
+        self.srd(QSRD_NL, qarg("nl"), qarg("st_bytes"))
+        self.srd(QSRD_ND, qarg("nd"), qarg("st_bytes"))
+        self.e(f"v_readfirstlane_b32 s{Q_W}, v{QV_TMP}")
+        self.e(f"s_lshl_b32 s{Q_LDSW}, s{Q_W}, 12")
+        self.e(f"s_and_b32 s{Q_U}, s{S_WG}, 7")
+        self.e(f"s_lshr_b32 s{T}, s{qarg('G')}, 3")
+        self.e(f"s_mul_i32 s{Q_U}, s{Q_U}, s{T}")
+        self.e(f"s_lshr_b32 s{T}, s{S_WG}, 3")
+        self.e(f"s_add_u32 s{Q_U}, s{Q_U}, s{T}")
+        self.e(f"s_lshl_b32 s{Q_U}, s{Q_U}, 1")
+        self.e(f"s_cmp_ge_u32 s{Q_U}, s{qarg('nitems')}")
+        self.e(f"s_cbranch_scc1 {lab_exit}")
+        L = V_LANE
+        t = QV_TMP
+        self.e(f"v_and_b32 v{t}, 31, v{L}")                        # l32
+        self.e(f"v_lshrrev_b32 v{t + 1}, 5, v{L}")                 # hh
+        self.e(f"s_lshl_b32 s{T}, s{Q_W}, 5")
+        self.e(f"v_add_u32 v{t + 2}, s{T}, v{t}")                  # 32w + l32 (query − q0)
+        self.e(f"v_lshlrev_b32 v{t + 3}, 4, v{t + 1}")             # 16hh
+        self.e(f"v_mad_u32_u24 v{QV_QV}, v{t + 2}, s{qarg('sqs')}, v{t + 3}")
+        self.e(f"v_mad_u32_u24 v{QV_OV}, v{t + 2}, s{qarg('sos')}, v{t + 3}")
+        self.e(f"v_lshlrev_b32 v{t + 3}, 3, v{t + 1}")             # 8hh
+        self.e(f"v_mad_u32_u24 v{QV_STQ}, v{t + 2}, s{qarg('sqs')}, v{t + 3}")
+        self.e(f"v_lshlrev_b32 v{QV_STV4}, 2, v{t + 2}")           # stats: 4·(32w + l32)
+        self.e(f"v_lshlrev_b32 v{t + 6}, 2, v{t + 1}")
+        self.e(f"v_sub_u32 v{t + 7}, v{t}, v{t + 6}")              # l32 − 4hh (kept for the items)
+        self.e(f"v_mov_b32 v{QV_NINF}, 0xff800000")
+        # LDS-DMA lane offsets (K / V image rows = keys; same piece mapping as the dK/dV kernel)
+        self.e(f"v_lshrrev_b32 v{t + 3}, 4, v{L}")
+        self.e(f"v_and_b32 v{t + 4}, 15, v{L}")
+        self.e(f"s_lshl_b32 s{T}, s{Q_W}, 4")
+        self.e(f"v_add_u32 v{t + 5}, s{T}, v{t + 3}")
+        for i in range(4):
+            self.e(f"v_lshl_or_b32 v{t + 6}, v{t + 3}, 2, {i}")
+            self.e(f"v_xor_b32 v{t + 6}, v{t + 6}, v{t + 4}")
+            self.e(f"v_lshlrev_b32 v{t + 6}, 4, v{t + 6}")
+            self.e(f"v_add_u32 v{t + 2}, {4 * i}, v{t + 5}")
+            self.e(f"v_mad_u32_u24 v{QV_DK + i}, v{t + 2}, s{qarg('sks')}, v{t + 6}")
+            self.e(f"v_mad_u32_u24 v{QV_DV + i}, v{t + 2}, s{qarg('svs')}, v{t + 6}")
+        # row-fragment / transposed read offsets (identical image layout to the dK/dV kernel)
+        self.e(f"v_and_b32 v{t + 3}, 3, v{t}")
+        self.e(f"v_lshlrev_b32 v{t + 3}, 2, v{t + 3}")
+        self.e(f"v_bfe_u32 v{t + 4}, v{t}, 2, 2")
+        self.e(f"v_or_b32 v{t + 3}, v{t + 3}, v{t + 4}")
+        self.e(f"v_lshlrev_b32 v{t + 4}, 8, v{t}")
+        for kk in range(8):
+            self.e(f"v_add_u32 v{t + 5}, {2 * kk}, v{t + 1}")
+            self.e(f"v_xor_b32 v{t + 5}, v{t + 5}, v{t + 3}")
+            self.e(f"v_lshl_add_u32 v{QV_ROW + kk}, v{t + 5}, 4, v{t + 4}")
+            self.e(f"v_add_u32 v{QV_ROW + 8 + kk}, {2 * QBUF_B}, v{QV_ROW + kk}")
+        self.e(f"v_and_b32 v{t + 3}, 15, v{L}")
+        self.e(f"v_lshrrev_b32 v{t + 4}, 2, v{t + 3}")
+        self.e(f"v_lshl_add_u32 v{t + 4}, v{t + 1}, 2, v{t + 4}")
+        self.e(f"v_and_b32 v{t + 5}, 3, v{t + 3}")
+        self.e(f"v_lshlrev_b32 v{t + 5}, 2, v{t + 5}")
+        self.e(f"v_bfe_u32 v{t + 6}, v{L}, 4, 1")
+        self.e(f"v_lshl_add_u32 v{t + 5}, v{t + 6}, 4, v{t + 5}")
+        for jj in (0, 1):
+            self.e(f"v_add_u32 v{t + 6}, {8 * jj}, v{t + 4}")
+            self.e(f"v_and_b32 v{QV_THR}, 3, v{t + 6}")
+            self.e(f"v_lshlrev_b32 v{QV_THR}, 2, v{QV_THR}")
+            self.e(f"v_bfe_u32 v{t + 2}, v{t + 6}, 2, 2")
+            self.e(f"v_or_b32 v{QV_THR}, v{QV_THR}, v{t + 2}")
+            self.e(f"v_lshrrev_b32 v{t + 2}, 3, v{t + 5}")
+            self.e(f"v_xor_b32 v{QV_THR}, v{QV_THR}, v{t + 2}")
+            self.e(f"v_lshlrev_b32 v{QV_THR}, 4, v{QV_THR}")
+            self.e(f"v_lshl_add_u32 v{QV_THR}, v{t + 6}, 8, v{QV_THR}")
+            self.e(f"v_and_b32 v{t + 2}, 7, v{t + 5}")
+            self.e(f"v_lshl_add_u32 v{QV_THR}, v{t + 2}, 1, v{QV_THR}")
+            for dt in range(4):
+                r = QV_TR + 4 * jj + dt
+                self.e(f"v_xor_b32 v{r}, {dt << 6}, v{QV_THR}")
+                self.e(f"v_add_u32 v{r + 8}, {2 * QBUF_B}, v{r}")
+        # first item: its Q / dO / row constants, the DMA stream primed with its first K/V tiles
+        self.compute_item_setup()
+        self.q_load(QA_QF, QA_OF, QV_NLC, QV_ND, Q_SOFFQ, Q_SOFFO, Q_SOFFS)
+        self.e(f"s_mov_b32 s{Q_DU}, s{Q_U}")
+        self.pending_item_setup()
+        self.pending_soffs()
+        for m0, ld in self.dma_first(0) + self.dma_second(0):
+            self.e(m0)
+            self.e(ld)
+        self.advance_pending()
+        for m0, ld in self.dma_first(1) + self.dma_second(1):
+            self.e(m0)
+            self.e(ld)
+        self.advance_pending()
+        for i in range(64):
+            self.e(f"v_accvgpr_write_b32 a{QA_DQ + i}, 0")
+        self.mask_setup()
+        self.e("s_waitcnt vmcnt(8)")
+        self.e(f"v_mul_f32 v{QV_NLC}, s{qarg('c')}, v{QV_NLC}")
+        for i in range(16):
+            self.e(f"v_mov_b32 v{QV_NDSET + i}, v{QV_ND}")
+        self.e("s_barrier")
+        for m in range(QLA):
+            for txt in self.ring_reads(0, m):
+                self.e(txt)
+        self.e("s_waitcnt lgkmcnt(0)")
+        self.e("s_nop 4")
+
+    def text(self):
+        self.lines = []
+        labs = [self.newlab(f"tile{b}") for b in range(3)]
+        lexit = self.newlab("exit")
+        self.prologue(lexit)
+        self.in_loop = True
+        for b in range(3):
+            self.lab(labs[b])
+            self.emit_body(b, labs[(b + 1) % 3], lexit)
+        self.in_loop = False
+        self.lab(lexit)
+        self.exit()
+        n = self.name
+        head = ["\t.text", f"\t.globl {n}", "\t.p2align 8", f"\t.type {n},@function", f"{n}:"]
+        tail = [
+            f".L{n}_end:", f"\t.size {n}, .L{n}_end-{n}", "\t.rodata", "\t.p2align 6",
+            f"\t.amdhsa_kernel {n}",
+            f"\t\t.amdhsa_group_segment_fixed_size {QLDS_BYTES}",
+            "\t\t.amdhsa_private_segment_fixed_size 0",
+            f"\t\t.amdhsa_kernarg_size {ARGS_SIZE}",
+            "\t\t.amdhsa_user_sgpr_count 2",
+            "\t\t.amdhsa_user_sgpr_kernarg_segment_ptr 1",
+            "\t\t.amdhsa_system_sgpr_workgroup_id_x 1",
+            "\t\t.amdhsa_system_vgpr_workitem_id 0",
+            f"\t\t.amdhsa_next_free_vgpr {QNV + QNA}",
+            f"\t\t.amdhsa_next_free_sgpr {Q_NSGPR}",
+            f"\t\t.amdhsa_accum_offset {QNV}",
+            "\t\t.amdhsa_reserve_vcc 1",
+            "\t\t.amdhsa_float_denorm_mode_32 3",
+            "\t\t.amdhsa_float_denorm_mode_16_64 3",
+            "\t\t.amdhsa_ieee_mode 0",
+            "\t\t.amdhsa_dx10_clamp 1",
+            "\t.end_amdhsa_kernel",
+            "\t.text",
+        ]
+        return "\n".join(head + self.lines + tail) + "\n"
+
+    def metadata(self):
+        return super().metadata().replace(f"group_segment_fixed_size: {LDS_BYTES}",
+                                          f"group_segment_fixed_size: {QLDS_BYTES}") \
+            .replace(f".vgpr_count:     {NV + NA}", f".vgpr_count:     {QNV + QNA}") \
+            .replace(f".agpr_count:     {NA}", f".agpr_count:     {QNA}")
+
+
 def kernels():
-    return [FaDkdv("piamd_fa_dkdv_d128_causal", True), FaDkdv("piamd_fa_dkdv_d128", False)]
+    return [FaDkdv("piamd_fa_dkdv_d128_causal", True), FaDkdv("piamd_fa_dkdv_d128", False),
+            FaDq("piamd_fa_dq_d128_causal", True), FaDq("piamd_fa_dq_d128", False)]
 
 
 def generate() -> str:

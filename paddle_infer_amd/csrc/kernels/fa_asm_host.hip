@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <cstdlib>
 #include <mutex>
 
@@ -33,17 +34,34 @@ struct __attribute__((packed)) FaDkdvArgs {
 };
 static_assert(sizeof(FaDkdvArgs) == 192, "FaDkdvArgs layout");
 
+// mirror of fa_gen.DQ_ARGS
+struct __attribute__((packed)) FaDqArgs {
+  const void *q, *k, *v, *dout;  // 0 ..
+  void* dq;                      // 32
+  unsigned long long pad0;       // 40
+  const float *nl, *nd;          // 48, 56
+  unsigned q_bytes, k_bytes, v_bytes, o_bytes, st_bytes;  // 64 .. 80
+  unsigned sqs, sqh, sqb, sks, skh, skb, svs, svh, svb, sos, soh, sob;  // 84 .. 128
+  unsigned Hq, group;            // 132, 136
+  float rcp_group;               // 140
+  unsigned Sq, nkt, npair, nqb1; // 144 .. 156
+  float rcp_npair, c, scale, rcp_Hq;  // 160 .. 172
+  unsigned pad1, nitems, G, G2m1;     // 176 .. 188
+};
+static_assert(sizeof(FaDqArgs) == 192, "FaDqArgs layout");
+
 std::mutex g_mu;
 hipModule_t g_mod = nullptr;
-hipFunction_t g_fn[2] = {nullptr, nullptr};
-int g_enabled = -1;
+hipFunction_t g_fn[4] = {nullptr, nullptr, nullptr, nullptr};
+int g_enabled = -1;  // bit 0: dK/dV kernel, bit 1: dQ kernel
 
-bool enabled() {
+// PIAMD_FA_ASM: unset / 1 = both assembly kernels, 0 = neither, "dkdv" / "dq" = that one only
+int enabled_mask() {
   if (g_enabled < 0) {
     const char* e = getenv("PIAMD_FA_ASM");
-    g_enabled = !(e && e[0] == '0');
+    g_enabled = !e ? 3 : e[0] == '0' ? 0 : !strcmp(e, "dkdv") ? 1 : !strcmp(e, "dq") ? 2 : 3;
   }
-  return g_enabled > 0;
+  return g_enabled;
 }
 
 // byte extent of a [B, S, H, 128] view from its base (last byte + 1), 0 on overflow past 2^31
@@ -76,7 +94,9 @@ PIAMD_EXPORT int piamd_fa_asm_load(const char* path) {
   int err = (int)hipModuleLoad(&m, path);
   if (err) return err;
   if (hipModuleGetFunction(&g_fn[0], m, "piamd_fa_dkdv_d128") != hipSuccess ||
-      hipModuleGetFunction(&g_fn[1], m, "piamd_fa_dkdv_d128_causal") != hipSuccess)
+      hipModuleGetFunction(&g_fn[1], m, "piamd_fa_dkdv_d128_causal") != hipSuccess ||
+      hipModuleGetFunction(&g_fn[2], m, "piamd_fa_dq_d128") != hipSuccess ||
+      hipModuleGetFunction(&g_fn[3], m, "piamd_fa_dq_d128_causal") != hipSuccess)
     return (int)hipErrorNotFound;
   g_mod = m;
   return 0;
@@ -84,16 +104,17 @@ PIAMD_EXPORT int piamd_fa_asm_load(const char* path) {
 
 PIAMD_EXPORT int piamd_fa_asm_loaded() { return g_mod != nullptr; }
 
-// 1 = use the assembly dK/dV kernel where it applies (default; env PIAMD_FA_ASM=0 turns it off)
-PIAMD_EXPORT int piamd_fa_asm_enable(int on) {
-  g_enabled = on ? 1 : 0;
+// bit mask of the assembly kernels to use where they apply: 1 = dK/dV, 2 = dQ (default 3;
+// env PIAMD_FA_ASM)
+PIAMD_EXPORT int piamd_fa_asm_enable(int mask) {
+  g_enabled = mask & 3;
   return 0;
 }
 
 // Would the assembly kernel take this backward? (contract in fa_gen.py's docstring)
 PIAMD_EXPORT int piamd_fa_asm_applies(const FaArgs* ap) {
   const FaArgs& a = *ap;
-  if (!g_mod || !enabled()) return 0;
+  if (!g_mod || !enabled_mask()) return 0;
   if (a.D != 128 || a.cu_q || a.mask || a.p_drop > 0.f || a.Sq != a.Sk || a.Sq % 256) return 0;
   if (a.Hk <= 0 || a.Hq % a.Hk || a.B <= 0) return 0;
   // seq strides feed 24-bit multiplies; every stride keeps 16-byte rows (LDS-DMA / dwordx4)
@@ -116,7 +137,7 @@ PIAMD_EXPORT int piamd_fa_asm_applies(const FaArgs* ap) {
 // 1 when launched, 0 when the shape is not this kernel's (caller runs the HIP kernel), < 0 on a
 // launch error.
 int fa_dkdv_asm(const FaArgs& a, hipStream_t st) {
-  if (!piamd_fa_asm_applies(&a)) return 0;
+  if (!(enabled_mask() & 1) || !piamd_fa_asm_applies(&a)) return 0;
   FaDkdvArgs g{};
   g.q = a.q;
   g.k = a.k;
@@ -159,5 +180,48 @@ int fa_dkdv_asm(const FaArgs& a, hipStream_t st) {
   size_t sz = sizeof(g);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &g, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
   hipError_t err = hipModuleLaunchKernel(g_fn[a.causal ? 1 : 0], grid, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
+  return err == hipSuccess ? 1 : -(int)err;
+}
+
+// Launch the assembly dQ kernel (same contract as fa_dkdv_asm).
+int fa_dq_asm(const FaArgs& a, hipStream_t st) {
+  if (!(enabled_mask() & 2) || !piamd_fa_asm_applies(&a)) return 0;
+  FaDqArgs g{};
+  g.q = a.q;
+  g.k = a.k;
+  g.v = a.v;
+  g.dout = a.dout;
+  g.dq = a.dq;
+  const long long rows = (long long)a.B * a.Hq * a.Sq;
+  g.nd = a.delta;
+  g.nl = a.delta + rows;
+  g.q_bytes = (unsigned)extent(a.sqb, a.sqs, a.sqh, a.B, a.Sq, a.Hq);
+  g.k_bytes = (unsigned)extent(a.skb, a.sks, a.skh, a.B, a.Sk, a.Hk);
+  g.v_bytes = (unsigned)extent(a.svb, a.svs, a.svh, a.B, a.Sk, a.Hk);
+  g.o_bytes = (unsigned)extent(a.sob, a.sos, a.soh, a.B, a.Sq, a.Hq);
+  g.st_bytes = (unsigned)(rows * 4);
+  g.sqs = (unsigned)(a.sqs * 2); g.sqh = (unsigned)(a.sqh * 2); g.sqb = (unsigned)(a.sqb * 2);
+  g.sks = (unsigned)(a.sks * 2); g.skh = (unsigned)(a.skh * 2); g.skb = (unsigned)(a.skb * 2);
+  g.svs = (unsigned)(a.svs * 2); g.svh = (unsigned)(a.svh * 2); g.svb = (unsigned)(a.svb * 2);
+  g.sos = (unsigned)(a.sos * 2); g.soh = (unsigned)(a.soh * 2); g.sob = (unsigned)(a.sob * 2);
+  g.Hq = a.Hq;
+  g.group = a.Hq / a.Hk;
+  g.rcp_group = 1.f / (float)g.group;
+  g.Sq = a.Sq;
+  g.nkt = a.Sk / 64;
+  const unsigned nqb = (unsigned)(a.Sq / 128);
+  g.npair = nqb / 2;
+  g.nqb1 = nqb - 1;
+  g.rcp_npair = 1.f / (float)g.npair;
+  g.c = a.scale * 1.4426950408889634f;
+  g.scale = a.scale;
+  g.rcp_Hq = 1.f / (float)a.Hq;
+  g.nitems = nqb * (unsigned)a.Hq * (unsigned)a.B;
+  const unsigned members = g.nitems / 2;
+  g.G = std::min<unsigned>((unsigned)num_cus() / 8 * 8, (members + 7) / 8 * 8);
+  g.G2m1 = 2 * g.G - 1;
+  size_t sz = sizeof(g);
+  void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &g, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+  hipError_t err = hipModuleLaunchKernel(g_fn[a.causal ? 3 : 2], g.G, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
   return err == hipSuccess ? 1 : -(int)err;
 }

@@ -52,8 +52,9 @@
 // C ABI argument block (ops/attention.py mirrors it as a ctypes.Structure).
 #include "fa_args.h"
 
-// hand-scheduled assembly dK/dV kernel (fa_asm_host.hip): 1 = launched, 0 = shape not taken
+// hand-scheduled assembly dK/dV and dQ kernels (fa_asm_host.hip): 1 = launched, 0 = shape not taken
 int fa_dkdv_asm(const FaArgs& a, hipStream_t st);
+int fa_dq_asm(const FaArgs& a, hipStream_t st);
 
 
 namespace fa {
@@ -1322,7 +1323,8 @@ int launch_bwd_feat(const FaArgs& a, dim3 gkv, dim3 gq, hipStream_t st) {
 #define BWD_F(FF)                                                                              \
   if (!(FF == 0 && D == 128 && !F16 && fa_dkdv_asm(a, st) == 1))                               \
     hipLaunchKernelGGL((bwd_dkdv_kernel<D, F16, C, FF>), gkv, dim3(256), 0, st, a);            \
-  hipLaunchKernelGGL((bwd_dq_kernel<D, F16, C, FF>), gq, dim3(256), 0, st, a);                 \
+  if (!(FF == 0 && D == 128 && !F16 && fa_dq_asm(a, st) == 1))                                 \
+    hipLaunchKernelGGL((bwd_dq_kernel<D, F16, C, FF>), gq, dim3(256), 0, st, a);               \
   break;
   switch (feat) {
     case 0: BWD_F(0)

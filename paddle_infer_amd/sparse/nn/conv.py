@@ -126,6 +126,47 @@ def _gpu_ok(x, w):
     return x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
 
 
+def _gpu_f32(x, w):
+    return x.is_cuda and x.dtype == torch.float32 and w.dtype == torch.float32
+
+
+def _ceil(n, m):
+    return -(-n // m) * m
+
+
+def _w_hhl(w, Kp, Np):
+    """f32 [E, K, N] → bf16 [E, 3·Kp, Np] = [w_hi; w_hi; w_lo] along K (the right operand of the
+    split-bf16 product, `ops/gemm.py` split3 convention)."""
+    hi = w.to(torch.bfloat16)
+    lo = (w - hi.float()).to(torch.bfloat16)
+    parts = [_pad_to(_pad_to(t, Kp, 1), Np, 2) for t in (hi, hi, lo)]
+    return torch.cat(parts, 1).contiguous()
+
+
+def _split_rows(x, Cp):
+    """f32 [R, C] → (hi, lo) bf16 [R, Cp] (zero-padded columns)."""
+    hi = x.to(torch.bfloat16)
+    lo = (x - hi.float()).to(torch.bfloat16)
+    return _pad_to(hi, Cp, 1).contiguous(), _pad_to(lo, Cp, 1).contiguous()
+
+
+def _wgrad(xs, gs, route, w):
+    """dW[k] = Σ_pairs x[in]ᵀ · dY[out] on the grouped MFMA wgrad kernel (channels zero-padded
+    to its 256 tiles; fp32 operands as split-bf16 hi·hi + hi·lo + lo·hi into an f32 result)."""
+    E, Cin, Cout = w.shape
+    Kp, Np = _ceil(Cin, 256), _ceil(Cout, 256)
+    out = torch.zeros((E, Kp, Np), dtype=torch.float32, device=xs.device)
+    if xs.dtype == torch.bfloat16:
+        _moe.grouped_wgrad(_pad_to(xs, Kp, 1).contiguous(), _pad_to(gs, Np, 1).contiguous(), route.offs,
+                           out=out, accumulate=True)
+    else:
+        xh, xl = _split_rows(xs.float(), Kp)
+        gh, gl = _split_rows(gs.float(), Np)
+        for a, b in ((xh, gh), (xh, gl), (xl, gh)):
+            _moe.grouped_wgrad(a, b, route.offs, out=out, accumulate=True)
+    return out[:, :Cin, :Cout].to(w.dtype)
+
+
 class _GatherGemmScatter(torch.autograd.Function):
     """out[out_row] += x[in_row] · W[k] for every rulebook pair (see module docstring)."""
 
@@ -146,8 +187,8 @@ class _GatherGemmScatter(torch.autograd.Function):
         if ctx.needs_input_grad[1]:  # dW[k] = Σ_pairs x[in_row]ᵀ · dY[out_row]
             xs = _gather_rows(x, rb.in_row)
             gs = _gather_rows(g, rb.out_row)
-            if _gpu_ok(xs, w) and w.shape[1] % 256 == 0 and w.shape[2] % 256 == 0:
-                dw = _moe.grouped_wgrad(xs, gs, rb.route.offs).to(w.dtype)
+            if _gpu_ok(xs, w) or _gpu_f32(xs, w):
+                dw = _wgrad(xs, gs, rb.route, w)
             else:
                 dw = torch.zeros_like(w, dtype=torch.float32)
                 for e, (a, b) in enumerate(_moe._segments(rb.route.offs)):
@@ -171,6 +212,16 @@ def _ggs(x, w, src_row, dst_row, route, n_dst):
         Np = max(256, -(-Cout // 256) * 256)
         wp = _pad_to(_pad_to(w, Kp, 1), Np, 2).contiguous()
         ys = _moe.grouped_gemm(_pad_to(xs, Kp, 1).contiguous(), wp, route.offs, route.rows_cap)[:, :Cout]
+    elif _gpu_f32(xs, w):
+        # fp32: ONE grouped bf16 MFMA GEMM over the 3×-long reduction [x_hi | x_lo | x_hi] ·
+        # [w_hi; w_hi; w_lo] with an f32 result (≈2^-16 relative per product, `ops/gemm.py`)
+        from ...ops.gemm import split3
+        Kp = max(64, _ceil(Cin, 64))
+        Np = max(256, _ceil(Cout, 256))
+        x3 = split3(xs.contiguous(), "hlh", 0, Cp=Kp)
+        ys = torch.zeros((xs.shape[0], Np), dtype=torch.float32, device=x.device)
+        _moe.grouped_gemm(x3, _w_hhl(w, Kp, Np), route.offs, route.rows_cap, out=ys)
+        ys = ys[:, :Cout]
     else:
         ys = torch.zeros((xs.shape[0], Cout), dtype=torch.float32, device=x.device)
         for e, (a, b) in enumerate(_moe._segments(route.offs)):

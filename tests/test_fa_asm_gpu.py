@@ -1,6 +1,6 @@
-"""Hand-scheduled assembly flash-attention dK/dV kernel (csrc/asm/fa_gen.py, launched from
-flash_attn.h `launch_bwd` through fa_asm_host.hip) against a plain PyTorch fp32 reference and
-against the HIP dK/dV kernel: causal / full, GQA, packed-QKV strides, several tiles per head."""
+"""Hand-scheduled assembly flash-attention dK/dV and dQ kernels (csrc/asm/fa_gen.py, launched
+from flash_attn.h `launch_bwd` through fa_asm_host.hip) against a plain PyTorch fp32 reference and
+against the HIP kernels: causal / full, GQA, packed-QKV strides, several tiles per head."""
 import ctypes
 import math
 
@@ -17,9 +17,9 @@ def _asm_loaded():
     _lib.lib()
     attention._fa_asm_load()
     assert _lib.lib().piamd_fa_asm_loaded() == 1
-    _lib.call("piamd_fa_asm_enable", 1)
+    _lib.call("piamd_fa_asm_enable", 3)
     yield
-    _lib.call("piamd_fa_asm_enable", 1)
+    _lib.call("piamd_fa_asm_enable", 3)
 
 
 def _ref_grads(q, k, v, do, causal, scale):
@@ -39,7 +39,7 @@ def _ref_grads(q, k, v, do, causal, scale):
 
 def _run(q, k, v, do, causal, scale, use_asm):
     from paddle_infer_amd.ops import _lib, attention
-    _lib.call("piamd_fa_asm_enable", int(use_asm))
+    _lib.call("piamd_fa_asm_enable", 3 if use_asm else 0)
     o, lse = attention._fwd(q, k, v, causal, scale)
     dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
     B, S, Hq, D = q.shape
@@ -74,10 +74,11 @@ def test_dkdv_asm_matches_reference(causal, B, S, Hq, Hk):
     _close(dv, rv, "dv")
     _close(dq, rq, "dq")
     # against the HIP dK/dV kernel (same math, different schedule)
-    _, hk, hv, ap2 = _run(q, k, v, do, causal, sc, False)
+    hq, hk, hv, ap2 = _run(q, k, v, do, causal, sc, False)
     assert ap2 == 0
     _close(dk, hk, "dk vs HIP")
     _close(dv, hv, "dv vs HIP")
+    _close(dq, hq, "dq vs HIP")
 
 
 def test_dkdv_asm_packed_qkv_strides():
@@ -89,7 +90,7 @@ def test_dkdv_asm_packed_qkv_strides():
     do = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16)
     sc = 1 / math.sqrt(D)
     from paddle_infer_amd.ops import _lib, attention
-    _lib.call("piamd_fa_asm_enable", 1)
+    _lib.call("piamd_fa_asm_enable", 3)
     o, lse = attention._fwd(q, k, v, True, sc)
     dqkv = torch.empty_like(qkv)
     attention._bwd(q, k, v, o, lse, do, dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2], True, sc)

@@ -109,6 +109,11 @@ ABL = set(filter(None, os.environ.get("PIAMD_FA_ABL", "").split(",")))
 STAMP = os.environ.get("PIAMD_FA_STAMP", "0") == "1"
 
 
+def fhex(x):
+    import struct
+    return "0x%08x" % struct.unpack("<I", struct.pack("<f", x))[0]
+
+
 def buf_set(b):
     """(offset-register set, immediate base) of LDS buffer b: buffers 0/1 share set 0 (the 16-bit
     ds offset reaches buffer 1), buffer 2 has its own set based at 2·BUF_B."""
@@ -1401,9 +1406,484 @@ class FaDq(FaDkdv):
             .replace(f".agpr_count:     {NA}", f".agpr_count:     {QNA}")
 
 
+
+# =================================================================================================
+# Forward kernel (`fa_fwd`): O = softmax(Q·Kᵀ·scale)·V with the row log-sum-exp
+# =================================================================================================
+# Two workgroups per CU (≤ 256 registers per lane, 64 KiB LDS each): the co-resident wave issues
+# its MFMAs while this wave runs the softmax block, so no cross-tile software pipeline is needed.
+# workgroup = 128 queries of one (batch, q-head), 4 waves × 32 queries on the MFMA lanes; per
+# 64-key tile: Sᵀ = K·Qᵀ (16 MFMAs, B = Q fragments in AGPRs), row max over the lane's 32 keys +
+# the partner half-wave's (v_permlane32_swap), lazy rescale (the running max moves only when a
+# tile max exceeds it by more than 8 in log2 units — an out-of-line block that rescales O and l),
+# P = exp2(c·s − m), Oᵀ += Vᵀ·P (16 MFMAs, A = transposed V reads). Causal diagonal tiles (the
+# last two of an item) mask s > query to −inf before the max. Item end: l summed over the two
+# half-waves, O·(1/l) stored bf16, lse = (m + log2 l)·ln 2.
+# Arguments: DQ_ARGS with dq → o (output), nl → lse (output, f32 [B, Hq, Sq]), dout / nd unused.
+F_V_DK, F_V_DV = 2, 6
+F_V_ROW, F_V_TR = 10, 18
+F_V_QL, F_V_THR, F_V_NINF, F_V_M, F_V_L, F_V_NM = 26, 27, 28, 29, 30, 31
+F_V_T = 32                           # temps v32..v35
+F_V_RING = 36                        # 8 slots × 4
+F_RING = 8
+F_V_SACC = 68                        # Sᵀ accumulators [kb 2][16] (epilogue temps at item end)
+F_V_PF = 100                         # P bf16 fragments [ks 4][4]
+F_V_QV, F_V_STO, F_V_LSEV, F_V_L4H = 116, 117, 118, 119    # … and l32 − 4hh
+F_NV = 120
+F_A_O, F_A_QF, F_A_QN = 0, 64, 96
+F_NA = 128
+F_BUF_B = 32768
+F_LDS_BYTES = 2 * F_BUF_B
+F_LA = 4
+LN2 = 0.6931471805599453
+
+
+class FaFwd(FaDq):
+    NM = 32
+    VTMP_UDIV = F_V_T + 3
+
+    # -- work items ----------------------------------------------------------------------------------
+    def q_load_f(self, aq, sq):
+        for kk in range(8):
+            self.e(f"buffer_load_dwordx4 a[{aq + 4 * kk}:{aq + 4 * kk + 3}], v{F_V_QV}, s[{QSRD_Q}:{QSRD_Q + 3}], s{sq} offen offset:{32 * kk}")
+
+    def compute_item_setup(self):
+        T = Q_T
+        self.decode(Q_U, T, Q_B, Q_HQ)
+        self.e(f"s_lshl_b32 s{Q_Q0}, s{T}, 7")
+        self.tiles_of(Q_TOT, T)
+        self.e(f"s_mov_b32 s{Q_IT}, 0")
+        self.q_soffs(T, Q_B, Q_HQ, Q_SOFFQ, Q_SOFFO, Q_SOFFS)
+        self.e(f"s_lshl_b32 s{T}, s{Q_W}, 5")
+        self.e(f"s_add_u32 s{T}, s{T}, s{Q_Q0}")
+        self.e(f"v_add_u32 v{F_V_QL}, s{T}, v{F_V_L4H}")
+
+    def prefetch_next(self):
+        T = Q_T
+        skip = self.newlab("nopf")
+        self.e(f"s_mov_b32 s{T + 3}, s{Q_U}")
+        self.next_item(T + 3)
+        self.e(f"s_cmp_ge_u32 s{T + 3}, s{qarg('nitems')}")
+        self.e(f"s_cbranch_scc1 {skip}")
+        self.decode(T + 3, T, T + 1, T + 2)
+        self.q_soffs(T, T + 1, T + 2, T + 3, T + 4, T + 6)
+        self.q_load_f(F_A_QN, T + 3)
+        self.lab(skip)
+
+    def dma_first(self, buf):
+        base = buf * F_BUF_B
+        return [[f"s_add_u32 m0, s{Q_LDSW}, {base + i * 1024}\n\ts_nop 0",
+                 f"buffer_load_dwordx4 v{F_V_DK + i}, s[{QSRD_K}:{QSRD_K + 3}], s{Q_SK} offen lds"]
+                for i in range(4)]
+
+    def dma_second(self, buf):
+        base = buf * F_BUF_B + Q_OFF_V
+        return [[f"s_add_u32 m0, s{Q_LDSW}, {base + i * 1024}\n\ts_nop 0",
+                 f"buffer_load_dwordx4 v{F_V_DV + i}, s[{QSRD_V}:{QSRD_V + 3}], s{Q_SV} offen lds"]
+                for i in range(4)]
+
+    # -- MFMA stream ------------------------------------------------------------------------------------
+    @staticmethod
+    def mfma_kind(m):
+        if m < 16:
+            return ("S", m // 8, m % 8)
+        c = m - 16
+        return ("O", c % 4, c // 4)                                  # (dt, ks)
+
+    @staticmethod
+    def slot(b, m):
+        return F_V_RING + 4 * ((32 * b + m) % F_RING)
+
+    def ring_reads(self, b, m):
+        kind, x, y = self.mfma_kind(m)
+        d = self.slot(b, m)
+        base = b * F_BUF_B
+        if kind == "S":
+            kb, kk = x, y
+            return [f"ds_read_b128 v[{d}:{d + 3}], v{F_V_ROW + kk} offset:{base + kb * 8192}"]
+        dt, ks = x, y
+        off = base + Q_OFF_V + ks * 16 * 256
+        return [f"ds_read_b64_tr_b16 v[{d + 2 * jj}:{d + 2 * jj + 1}], v{F_V_TR + 4 * jj + dt} offset:{off}"
+                for jj in (0, 1)]
+
+    def mfma_text(self, b, m):
+        kind, x, y = self.mfma_kind(m)
+        a = self.slot(b, m)
+        if kind == "S":
+            kb, kk = x, y
+            acc = F_V_SACC + 16 * kb
+            src = "0" if kk == 0 else f"v[{acc}:{acc + 15}]"
+            return f"{MFMA} v[{acc}:{acc + 15}], v[{a}:{a + 3}], a[{F_A_QF + 4 * kk}:{F_A_QF + 4 * kk + 3}], {src}"
+        dt, ks = x, y
+        acc = F_A_O + 16 * dt
+        return f"{MFMA} a[{acc}:{acc + 15}], v[{a}:{a + 3}], v[{F_V_PF + 4 * ks}:{F_V_PF + 4 * ks + 3}], a[{acc}:{acc + 15}]"
+
+    def softmax_block(self, lab_resc, lab_back):
+        """After the 16 S MFMAs: mask (diagonal tiles), row max, lazy rescale test, P = exp2(c·s −
+        m) and the bf16 P fragments. The l partial sum is left for the O-phase gaps."""
+        T = Q_T
+        S = F_V_SACC
+        t = F_V_T
+        self.e("s_nop 15")                                             # MFMA result → VALU
+        self.e("s_nop 15")
+        if self.causal:
+            skip = self.newlab("nomask")
+            self.e(f"s_sub_u32 s{T}, s{Q_TOT}, 2")
+            self.e(f"s_cmp_lt_i32 s{Q_IT}, s{T}")
+            self.e(f"s_cbranch_scc1 {skip}")
+            self.e(f"s_lshl_b32 s{T}, s{Q_IT}, 6")
+            self.e(f"v_subrev_u32 v{F_V_THR}, s{T}, v{F_V_QL}")         # q − 4hh − 64 kt
+            for kb in (0, 1):
+                for g4 in range(4):
+                    for e in range(4):
+                        ci = 32 * kb + 8 * g4 + e
+                        r = S + 16 * kb + 4 * g4 + e
+                        self.e(f"v_cmp_gt_i32 vcc, {ci}, v{F_V_THR}")
+                        self.e(f"v_cndmask_b32 v{r}, v{r}, v{F_V_NINF}, vcc")
+            self.lab(skip)
+        # row max over the lane's 32 keys (max3 tree), then the partner half-wave's
+        regs = list(range(S, S + 32))
+        self.e(f"v_max3_f32 v{t}, v{regs[0]}, v{regs[1]}, v{regs[2]}")
+        self.e(f"v_max3_f32 v{t + 1}, v{regs[3]}, v{regs[4]}, v{regs[5]}")
+        k = 6
+        while k + 1 < 32:
+            acc = t + (k // 2) % 2
+            self.e(f"v_max3_f32 v{acc}, v{acc}, v{regs[k]}, v{regs[k + 1]}")
+            k += 2
+        self.e(f"v_max_f32 v{t}, v{t}, v{t + 1}")
+        self.e(f"v_mov_b32 v{t + 1}, v{t}")
+        self.e("s_nop 1")
+        self.e(f"v_permlane32_swap_b32 v{t}, v{t + 1}")
+        self.e("s_nop 1")
+        self.e(f"v_max_f32 v{t}, v{t}, v{t + 1}")
+        self.e(f"v_mul_f32 v{t}, s{qarg('c')}, v{t}")                   # tile row max (log2 units)
+        self.e(f"v_add_f32 v{t + 1}, 0x41000000, v{F_V_M}")              # m + 8
+        self.e(f"v_cmp_gt_f32 vcc, v{t}, v{t + 1}")
+        self.e(f"s_cbranch_vccnz {lab_resc}")
+        self.lab(lab_back)
+        # −m (0 while the row has seen only masked keys)
+        self.e(f"v_cmp_eq_f32 vcc, v{F_V_NINF}, v{F_V_M}")
+        self.e(f"v_cndmask_b32_e64 v{F_V_NM}, -v{F_V_M}, 0, vcc")
+        for r in regs:
+            self.e(f"v_fma_f32 v{r}, v{r}, s{qarg('c')}, v{F_V_NM}")
+        for r in regs:
+            self.e(f"v_exp_f32 v{r}, v{r}")
+        self.e("s_nop 0")
+        for kb in (0, 1):
+            for j in range(8):
+                fr = 4 * (2 * kb + j // 4) + j % 4
+                a = S + 16 * kb + 2 * j
+                self.e(f"v_cvt_pk_bf16_f32 v{F_V_PF + fr}, v{a}, v{a + 1}")
+
+    def rescale_block(self, lab_resc, lab_back):
+        """Out of line: m ← tile max where it grew by > 8; O, l ← O·α, l·α with α = exp2(m_old −
+        m_new) (α = 1 on the other lanes)."""
+        t = F_V_T
+        self.lab(lab_resc)
+        self.e(f"v_cndmask_b32 v{t + 1}, v{F_V_M}, v{t}, vcc")         # m_new
+        self.e(f"v_cmp_eq_f32 vcc, v{F_V_NINF}, v{F_V_M}")
+        self.e(f"v_sub_f32 v{t + 2}, v{F_V_M}, v{t + 1}")
+        self.e(f"v_exp_f32 v{t + 2}, v{t + 2}")
+        self.e("s_nop 0")
+        self.e(f"v_cndmask_b32 v{t + 2}, v{t + 2}, 0, vcc")           # first tile: α = 0 (O = 0)
+        self.e(f"v_mul_f32 v{F_V_L}, v{F_V_L}, v{t + 2}")
+        self.e(f"v_mov_b32 v{F_V_M}, v{t + 1}")
+        self.e("s_nop 7")
+        tmp = [t + 3, F_V_NM, F_V_PF, F_V_PF + 1]     # free here; rotated so no read follows its write
+        for i0 in range(0, 64, 4):
+            for j in range(4):
+                self.e(f"v_accvgpr_read_b32 v{tmp[j]}, a{F_A_O + i0 + j}")
+            for j in range(4):
+                self.e(f"v_mul_f32 v{tmp[j]}, v{tmp[j]}, v{t + 2}")
+            self.e("s_nop 1")
+            for j in range(4):
+                self.e(f"v_accvgpr_write_b32 a{F_A_O + i0 + j}, v{tmp[j]}")
+        self.e("s_nop 4")
+        self.e(f"s_branch {lab_back}")
+
+    def lsum_ops(self):
+        S = F_V_SACC
+        ops = []
+        # pairwise tree of the 32 P values into v{S}, then l += it
+        n = 32
+        step = 1
+        while step < n:
+            for i in range(0, n, 2 * step):
+                ops.append(f"v_add_f32 v{S + i}, v{S + i}, v{S + i + step}")
+            step *= 2
+        ops.append(f"v_add_f32 v{F_V_L}, v{F_V_L}, v{S}")
+        return ops
+
+    def body_ops(self, b):
+        nb = (b + 1) % 2
+        NM = self.NM
+        gaps = [[] for _ in range(NM)]
+        for m in range(NM):
+            g = m - F_LA
+            if g >= 0:
+                for t in self.ring_reads(b, m):
+                    gaps[g].append(("lds", ("ring", 0, m), t))
+        for m in range(F_LA):
+            g = NM - F_LA + m
+            for t in self.ring_reads(nb, m):
+                gaps[g].append(("lds", ("ring", 1, m), t))
+        # the DMA of tile t+1 into the other buffer (free: every wave passed this body's start
+        # barrier, so the previous tile is consumed), cursor advance
+        for i, (m0, ld) in enumerate(self.dma_first(nb) + self.dma_second(nb)):
+            gaps[i] += [("txt", m0), ("txt", ld)]
+        gaps[8].append(("adv",))
+        # tile t+1 landed before its K rows are read (the lookahead reads start at gap NM−LA)
+        gaps[NM - F_LA - 1].append(("txt", "s_waitcnt vmcnt(0)"))
+        gaps[NM - F_LA - 1].append(("txt", "s_barrier"))
+        gaps[15].append(("softmax",))
+        ls = self.lsum_ops()
+        for i, op in enumerate(ls):
+            gaps[16 + (i * 14) // len(ls)].append(("txt", op))
+        ops = [("txt", "s_barrier")]
+        for m in range(NM):
+            ops.append(("mfma", m, [("ring", 0, m)], self.mfma_text(b, m)))
+            ops += gaps[m]
+        return ops
+
+    def emit_body(self, b, lab_next, lab_epi):
+        prev = self.body_ops((b + 1) % 2)
+        cur = self.body_ops(b)
+        order = []
+        for ent in prev:
+            if ent[0] == "lds":
+                kind, t, idx = ent[1]
+                order.append((kind, t - 1, idx))
+        pos = {k: i for i, k in enumerate(order)}
+        done = 0
+        issued = len(order)
+        resc, back = self.newlab("resc"), self.newlab("back")
+        for ent in cur:
+            if ent[0] == "lds":
+                pos[ent[1]] = issued
+                issued += 1
+                self.e(ent[2])
+            elif ent[0] == "mfma":
+                need = max(pos[d] for d in ent[2])
+                if need >= done:
+                    w = min(15, issued - 1 - need)
+                    self.e(f"s_waitcnt lgkmcnt({w})")
+                    done = issued - w
+                self.e(ent[3])
+            elif ent[0] == "adv":
+                self.advance_pending()
+            elif ent[0] == "softmax":
+                self.softmax_block(resc, back)
+            else:
+                self.e(ent[1])
+        self.e(f"s_add_u32 s{Q_IT}, s{Q_IT}, 1")
+        nopf = self.newlab("nopf")
+        self.e(f"s_cmp_eq_u32 s{Q_IT}, 1")
+        self.e(f"s_cbranch_scc0 {nopf}")
+        self.prefetch_next()
+        self.lab(nopf)
+        self.e(f"s_cmp_lt_u32 s{Q_IT}, s{Q_TOT}")
+        self.e(f"s_cbranch_scc1 {lab_next}")
+        self.item_end(lab_next, lab_epi)
+        self.rescale_block(resc, back)
+
+    def store_o(self):
+        """l over both half-waves, O·(1/l) → bf16 o[q][d], lse = (m + log2 l)·ln 2."""
+        t = F_V_T
+        S = F_V_SACC
+        self.e(f"v_mov_b32 v{t}, v{F_V_L}")
+        self.e(f"v_mov_b32 v{t + 1}, v{F_V_L}")
+        self.e("s_nop 1")
+        self.e(f"v_permlane32_swap_b32 v{t}, v{t + 1}")
+        self.e("s_nop 1")
+        self.e(f"v_add_f32 v{t}, v{t}, v{t + 1}")                      # l
+        self.e(f"v_rcp_f32 v{t + 1}, v{t}")
+        self.e(f"v_log_f32 v{t + 2}, v{t}")
+        self.e("s_nop 0")
+        self.e(f"v_cmp_lt_f32 vcc, 0, v{t}")
+        self.e(f"v_cndmask_b32 v{t + 1}, 0, v{t + 1}, vcc")            # 1/l (0 for an empty row)
+        self.e(f"v_add_f32 v{t + 2}, v{F_V_M}, v{t + 2}")
+        self.e(f"v_mul_f32 v{t + 2}, {fhex(LN2)}, v{t + 2}")
+        self.e(f"v_mov_b32 v{t + 3}, 0x7f800000")
+        self.e(f"v_cndmask_b32 v{t + 2}, v{t + 3}, v{t + 2}, vcc")     # +inf for an empty row
+        self.e(f"buffer_store_dword v{t + 2}, v{F_V_LSEV}, s[{QSRD_NL}:{QSRD_NL + 3}], s{Q_SOFFS} offen")
+        for dt in range(4):
+            for g4 in range(4):
+                a0 = F_A_O + 16 * dt + 4 * g4
+                for j in range(4):
+                    self.e(f"v_accvgpr_read_b32 v{S + j}, a{a0 + j}")
+                for j in range(4):
+                    self.e(f"v_mul_f32 v{S + j}, v{S + j}, v{t + 1}")
+                self.e(f"v_cvt_pk_bf16_f32 v{S}, v{S}, v{S + 1}")
+                self.e(f"v_cvt_pk_bf16_f32 v{S + 1}, v{S + 2}, v{S + 3}")
+                self.e(f"buffer_store_dwordx2 v[{S}:{S + 1}], v{F_V_STO}, s[{QSRD_DQ}:{QSRD_DQ + 3}], s{Q_SOFFO} offen offset:{64 * dt + 16 * g4}")
+
+    def item_end(self, lab_next, lab_exit):
+        self.e("s_nop 15")
+        self.e("s_nop 15")
+        self.store_o()
+        for i in range(64):
+            self.e(f"v_accvgpr_write_b32 a{F_A_O + i}, 0")
+        for i in range(32):
+            self.e(f"v_accvgpr_mov_b32 a{F_A_QF + i}, a{F_A_QN + i}")
+        self.e(f"v_mov_b32 v{F_V_M}, v{F_V_NINF}")
+        self.e(f"v_mov_b32 v{F_V_L}, 0")
+        self.next_item(Q_U)
+        self.e(f"s_cmp_ge_u32 s{Q_U}, s{qarg('nitems')}")
+        self.e(f"s_cbranch_scc1 {lab_exit}")
+        self.compute_item_setup()
+        self.e("s_nop 4")
+        self.e(f"s_branch {lab_next}")
+
+    def prologue(self, lab_exit):
+        T = Q_T
+        self.e("s_load_dwordx16 s[4:19], s[0:1], 0x0")
+        self.e("s_load_dwordx16 s[20:35], s[0:1], 0x40")
+        self.e("s_load_dwordx16 s[36:51], s[0:1], 0x80")
+        self.e(f"v_and_b32 v{V_LANE}, 63, v{V_TID}")
+        self.e(f"v_lshrrev_b32 v{F_V_T}, 6, v{V_TID}")
+        self.e("s_waitcnt lgkmcnt(0)")
+        self.srd(QSRD_K, qarg("k"), qarg("k_bytes"))
+        self.srd(QSRD_V, qarg("v"), qarg("v_bytes"))
+        self.srd(QSRD_Q, qarg("q"), qarg("q_bytes"))
+        self.srd(QSRD_DQ, qarg("dq"), qarg("o_bytes"))             # O (output)
+        self.srd(QSRD_NL, qarg("nl"), qarg("st_bytes"))            # lse (output)
+        self.e(f"v_readfirstlane_b32 s{Q_W}, v{F_V_T}")
+        self.e(f"s_lshl_b32 s{Q_LDSW}, s{Q_W}, 12")
+        self.e(f"s_and_b32 s{Q_U}, s{S_WG}, 7")
+        self.e(f"s_lshr_b32 s{T}, s{qarg('G')}, 3")
+        self.e(f"s_mul_i32 s{Q_U}, s{Q_U}, s{T}")
+        self.e(f"s_lshr_b32 s{T}, s{S_WG}, 3")
+        self.e(f"s_add_u32 s{Q_U}, s{Q_U}, s{T}")
+        self.e(f"s_lshl_b32 s{Q_U}, s{Q_U}, 1")
+        self.e(f"s_cmp_ge_u32 s{Q_U}, s{qarg('nitems')}")
+        self.e(f"s_cbranch_scc1 {lab_exit}")
+        L = V_LANE
+        t = F_V_T
+        # t: l32, t+1: hh, t+2: l32 − 4hh (kept for the items), t+3: scratch
+        self.e(f"v_and_b32 v{t}, 31, v{L}")
+        self.e(f"v_lshrrev_b32 v{t + 1}, 5, v{L}")
+        self.e(f"s_lshl_b32 s{T}, s{Q_W}, 5")
+        self.e(f"v_add_u32 v{t + 3}, s{T}, v{t}")                  # 32w + l32
+        self.e(f"v_lshlrev_b32 v{F_V_THR}, 4, v{t + 1}")            # 16hh
+        self.e(f"v_mad_u32_u24 v{F_V_QV}, v{t + 3}, s{qarg('sqs')}, v{F_V_THR}")
+        self.e(f"v_lshlrev_b32 v{F_V_THR}, 3, v{t + 1}")            # 8hh
+        self.e(f"v_mad_u32_u24 v{F_V_STO}, v{t + 3}, s{qarg('sos')}, v{F_V_THR}")
+        self.e(f"v_lshlrev_b32 v{F_V_LSEV}, 2, v{t + 3}")           # 4·(32w + l32)
+        self.e(f"v_lshlrev_b32 v{F_V_THR}, 2, v{t + 1}")
+        self.e(f"v_sub_u32 v{F_V_L4H}, v{t}, v{F_V_THR}")           # l32 − 4hh
+        self.e(f"v_mov_b32 v{F_V_NINF}, 0xff800000")
+        self.e(f"v_mov_b32 v{F_V_M}, v{F_V_NINF}")
+        self.e(f"v_mov_b32 v{F_V_L}, 0")
+        # scratch for the offset set-up: S accumulator registers (free until the first tile)
+        x = F_V_SACC
+        self.e(f"v_lshrrev_b32 v{x + 3}, 4, v{L}")
+        self.e(f"v_and_b32 v{x + 4}, 15, v{L}")
+        self.e(f"s_lshl_b32 s{T}, s{Q_W}, 4")
+        self.e(f"v_add_u32 v{x + 5}, s{T}, v{x + 3}")
+        for i in range(4):
+            self.e(f"v_lshl_or_b32 v{x + 6}, v{x + 3}, 2, {i}")
+            self.e(f"v_xor_b32 v{x + 6}, v{x + 6}, v{x + 4}")
+            self.e(f"v_lshlrev_b32 v{x + 6}, 4, v{x + 6}")
+            self.e(f"v_add_u32 v{x + 2}, {4 * i}, v{x + 5}")
+            self.e(f"v_mad_u32_u24 v{F_V_DK + i}, v{x + 2}, s{qarg('sks')}, v{x + 6}")
+            self.e(f"v_mad_u32_u24 v{F_V_DV + i}, v{x + 2}, s{qarg('svs')}, v{x + 6}")
+        self.e(f"v_and_b32 v{x + 3}, 3, v{t}")
+        self.e(f"v_lshlrev_b32 v{x + 3}, 2, v{x + 3}")
+        self.e(f"v_bfe_u32 v{x + 4}, v{t}, 2, 2")
+        self.e(f"v_or_b32 v{x + 3}, v{x + 3}, v{x + 4}")
+        self.e(f"v_lshlrev_b32 v{x + 4}, 8, v{t}")
+        for kk in range(8):
+            self.e(f"v_add_u32 v{x + 5}, {2 * kk}, v{t + 1}")
+            self.e(f"v_xor_b32 v{x + 5}, v{x + 5}, v{x + 3}")
+            self.e(f"v_lshl_add_u32 v{F_V_ROW + kk}, v{x + 5}, 4, v{x + 4}")
+        self.e(f"v_and_b32 v{x + 3}, 15, v{L}")
+        self.e(f"v_lshrrev_b32 v{x + 4}, 2, v{x + 3}")
+        self.e(f"v_lshl_add_u32 v{x + 4}, v{t + 1}, 2, v{x + 4}")
+        self.e(f"v_and_b32 v{x + 5}, 3, v{x + 3}")
+        self.e(f"v_lshlrev_b32 v{x + 5}, 2, v{x + 5}")
+        self.e(f"v_bfe_u32 v{x + 6}, v{L}, 4, 1")
+        self.e(f"v_lshl_add_u32 v{x + 5}, v{x + 6}, 4, v{x + 5}")
+        for jj in (0, 1):
+            self.e(f"v_add_u32 v{x + 6}, {8 * jj}, v{x + 4}")
+            self.e(f"v_and_b32 v{x + 7}, 3, v{x + 6}")
+            self.e(f"v_lshlrev_b32 v{x + 7}, 2, v{x + 7}")
+            self.e(f"v_bfe_u32 v{x + 2}, v{x + 6}, 2, 2")
+            self.e(f"v_or_b32 v{x + 7}, v{x + 7}, v{x + 2}")
+            self.e(f"v_lshrrev_b32 v{x + 2}, 3, v{x + 5}")
+            self.e(f"v_xor_b32 v{x + 7}, v{x + 7}, v{x + 2}")
+            self.e(f"v_lshlrev_b32 v{x + 7}, 4, v{x + 7}")
+            self.e(f"v_lshl_add_u32 v{x + 7}, v{x + 6}, 8, v{x + 7}")
+            self.e(f"v_and_b32 v{x + 2}, 7, v{x + 5}")
+            self.e(f"v_lshl_add_u32 v{x + 7}, v{x + 2}, 1, v{x + 7}")
+            for dt in range(4):
+                self.e(f"v_xor_b32 v{F_V_TR + 4 * jj + dt}, {dt << 6}, v{x + 7}")
+        self.compute_item_setup()
+        self.q_load_f(F_A_QF, Q_SOFFQ)
+        self.e(f"s_mov_b32 s{Q_DU}, s{Q_U}")
+        self.pending_item_setup()
+        self.pending_soffs()
+        for m0, ld in self.dma_first(0) + self.dma_second(0):
+            self.e(m0)
+            self.e(ld)
+        self.advance_pending()
+        for i in range(64):
+            self.e(f"v_accvgpr_write_b32 a{F_A_O + i}, 0")
+        self.e("s_waitcnt vmcnt(0)")
+        self.e("s_barrier")
+        for m in range(F_LA):
+            for txt in self.ring_reads(0, m):
+                self.e(txt)
+        self.e("s_waitcnt lgkmcnt(0)")
+        self.e("s_nop 4")
+
+    def text(self):
+        self.lines = []
+        labs = [self.newlab(f"tile{b}") for b in range(2)]
+        lexit = self.newlab("exit")
+        self.prologue(lexit)
+        self.in_loop = True
+        for b in range(2):
+            self.lab(labs[b])
+            self.emit_body(b, labs[(b + 1) % 2], lexit)
+        self.in_loop = False
+        self.lab(lexit)
+        self.exit()
+        n = self.name
+        head = ["\t.text", f"\t.globl {n}", "\t.p2align 8", f"\t.type {n},@function", f"{n}:"]
+        tail = [
+            f".L{n}_end:", f"\t.size {n}, .L{n}_end-{n}", "\t.rodata", "\t.p2align 6",
+            f"\t.amdhsa_kernel {n}",
+            f"\t\t.amdhsa_group_segment_fixed_size {F_LDS_BYTES}",
+            "\t\t.amdhsa_private_segment_fixed_size 0",
+            f"\t\t.amdhsa_kernarg_size {ARGS_SIZE}",
+            "\t\t.amdhsa_user_sgpr_count 2",
+            "\t\t.amdhsa_user_sgpr_kernarg_segment_ptr 1",
+            "\t\t.amdhsa_system_sgpr_workgroup_id_x 1",
+            "\t\t.amdhsa_system_vgpr_workitem_id 0",
+            f"\t\t.amdhsa_next_free_vgpr {F_NV + F_NA}",
+            f"\t\t.amdhsa_next_free_sgpr {Q_NSGPR}",
+            f"\t\t.amdhsa_accum_offset {F_NV}",
+            "\t\t.amdhsa_reserve_vcc 1",
+            "\t\t.amdhsa_float_denorm_mode_32 3",
+            "\t\t.amdhsa_float_denorm_mode_16_64 3",
+            "\t\t.amdhsa_ieee_mode 0",
+            "\t\t.amdhsa_dx10_clamp 1",
+            "\t.end_amdhsa_kernel",
+            "\t.text",
+        ]
+        return "\n".join(head + self.lines + tail) + "\n"
+
+    def metadata(self):
+        return FaDkdv.metadata(self).replace(f"group_segment_fixed_size: {LDS_BYTES}",
+                                             f"group_segment_fixed_size: {F_LDS_BYTES}") \
+            .replace(f".vgpr_count:     {NV + NA}", f".vgpr_count:     {F_NV + F_NA}") \
+            .replace(f".agpr_count:     {NA}", f".agpr_count:     {F_NA}")
+
+
 def kernels():
     return [FaDkdv("piamd_fa_dkdv_d128_causal", True), FaDkdv("piamd_fa_dkdv_d128", False),
-            FaDq("piamd_fa_dq_d128_causal", True), FaDq("piamd_fa_dq_d128", False)]
+            FaDq("piamd_fa_dq_d128_causal", True), FaDq("piamd_fa_dq_d128", False),
+            FaFwd("piamd_fa_fwd_d128_causal", True), FaFwd("piamd_fa_fwd_d128", False)]
 
 
 def generate() -> str:

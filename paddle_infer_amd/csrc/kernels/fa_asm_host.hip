@@ -52,14 +52,15 @@ static_assert(sizeof(FaDqArgs) == 192, "FaDqArgs layout");
 
 std::mutex g_mu;
 hipModule_t g_mod = nullptr;
-hipFunction_t g_fn[4] = {nullptr, nullptr, nullptr, nullptr};
-int g_enabled = -1;  // bit 0: dK/dV kernel, bit 1: dQ kernel
+hipFunction_t g_fn[6] = {};
+int g_enabled = -1;  // bit 0: dK/dV kernel, bit 1: dQ kernel, bit 2: forward kernel
 
-// PIAMD_FA_ASM: unset / 1 = both assembly kernels, 0 = neither, "dkdv" / "dq" = that one only
+// PIAMD_FA_ASM: unset / 1 = every assembly kernel, 0 = none, "dkdv" / "dq" / "fwd" / "bwd" = those
 int enabled_mask() {
   if (g_enabled < 0) {
     const char* e = getenv("PIAMD_FA_ASM");
-    g_enabled = !e ? 3 : e[0] == '0' ? 0 : !strcmp(e, "dkdv") ? 1 : !strcmp(e, "dq") ? 2 : 3;
+    g_enabled = !e ? 7 : e[0] == '0' ? 0 : !strcmp(e, "dkdv") ? 1 : !strcmp(e, "dq") ? 2
+              : !strcmp(e, "fwd") ? 4 : !strcmp(e, "bwd") ? 3 : 7;
   }
   return g_enabled;
 }
@@ -96,7 +97,9 @@ PIAMD_EXPORT int piamd_fa_asm_load(const char* path) {
   if (hipModuleGetFunction(&g_fn[0], m, "piamd_fa_dkdv_d128") != hipSuccess ||
       hipModuleGetFunction(&g_fn[1], m, "piamd_fa_dkdv_d128_causal") != hipSuccess ||
       hipModuleGetFunction(&g_fn[2], m, "piamd_fa_dq_d128") != hipSuccess ||
-      hipModuleGetFunction(&g_fn[3], m, "piamd_fa_dq_d128_causal") != hipSuccess)
+      hipModuleGetFunction(&g_fn[3], m, "piamd_fa_dq_d128_causal") != hipSuccess ||
+      hipModuleGetFunction(&g_fn[4], m, "piamd_fa_fwd_d128") != hipSuccess ||
+      hipModuleGetFunction(&g_fn[5], m, "piamd_fa_fwd_d128_causal") != hipSuccess)
     return (int)hipErrorNotFound;
   g_mod = m;
   return 0;
@@ -104,10 +107,10 @@ PIAMD_EXPORT int piamd_fa_asm_load(const char* path) {
 
 PIAMD_EXPORT int piamd_fa_asm_loaded() { return g_mod != nullptr; }
 
-// bit mask of the assembly kernels to use where they apply: 1 = dK/dV, 2 = dQ (default 3;
-// env PIAMD_FA_ASM)
+// bit mask of the assembly kernels to use where they apply: 1 = dK/dV, 2 = dQ, 4 = forward
+// (default 7; env PIAMD_FA_ASM)
 PIAMD_EXPORT int piamd_fa_asm_enable(int mask) {
-  g_enabled = mask & 3;
+  g_enabled = mask & 7;
   return 0;
 }
 
@@ -183,9 +186,8 @@ int fa_dkdv_asm(const FaArgs& a, hipStream_t st) {
   return err == hipSuccess ? 1 : -(int)err;
 }
 
-// Launch the assembly dQ kernel (same contract as fa_dkdv_asm).
-int fa_dq_asm(const FaArgs& a, hipStream_t st) {
-  if (!(enabled_mask() & 2) || !piamd_fa_asm_applies(&a)) return 0;
+// the dQ / forward argument block (fa_gen.DQ_ARGS; the forward reads dq as O and nl as lse)
+static FaDqArgs dq_args(const FaArgs& a, int wgs_per_cu) {
   FaDqArgs g{};
   g.q = a.q;
   g.k = a.k;
@@ -218,10 +220,36 @@ int fa_dq_asm(const FaArgs& a, hipStream_t st) {
   g.rcp_Hq = 1.f / (float)a.Hq;
   g.nitems = nqb * (unsigned)a.Hq * (unsigned)a.B;
   const unsigned members = g.nitems / 2;
-  g.G = std::min<unsigned>((unsigned)num_cus() / 8 * 8, (members + 7) / 8 * 8);
+  g.G = std::min<unsigned>((unsigned)(num_cus() * wgs_per_cu) / 8 * 8, (members + 7) / 8 * 8);
   g.G2m1 = 2 * g.G - 1;
+  return g;
+}
+
+// Launch the assembly dQ kernel (same contract as fa_dkdv_asm).
+int fa_dq_asm(const FaArgs& a, hipStream_t st) {
+  if (!(enabled_mask() & 2) || !piamd_fa_asm_applies(&a)) return 0;
+  FaDqArgs g = dq_args(a, 1);
   size_t sz = sizeof(g);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &g, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
   hipError_t err = hipModuleLaunchKernel(g_fn[a.causal ? 3 : 2], g.G, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
+  return err == hipSuccess ? 1 : -(int)err;
+}
+
+// Launch the assembly forward kernel (two workgroups per CU): O and lse (needed: lse non-null).
+int fa_fwd_asm(const FaArgs& a, hipStream_t st) {
+  if (!(enabled_mask() & 4) || !a.lse || reinterpret_cast<unsigned long long>(a.o) % 16 ||
+      !piamd_fa_asm_applies(&a))
+    return 0;
+  FaArgs b = a;
+  b.dq = a.o;  // output O (strides sob / sos / soh)
+  b.delta = nullptr;
+  FaDqArgs g = dq_args(b, 2);
+  g.dq = a.o;
+  g.nl = a.lse;
+  g.nd = nullptr;
+  g.dout = nullptr;
+  size_t sz = sizeof(g);
+  void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &g, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+  hipError_t err = hipModuleLaunchKernel(g_fn[a.causal ? 5 : 4], g.G, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
   return err == hipSuccess ? 1 : -(int)err;
 }

@@ -55,6 +55,7 @@
 // hand-scheduled assembly dK/dV and dQ kernels (fa_asm_host.hip): 1 = launched, 0 = shape not taken
 int fa_dkdv_asm(const FaArgs& a, hipStream_t st);
 int fa_dq_asm(const FaArgs& a, hipStream_t st);
+int fa_fwd_asm(const FaArgs& a, hipStream_t st);
 
 
 namespace fa {
@@ -391,6 +392,10 @@ __global__ __launch_bounds__(64 * NW, D > 128 ? 1 : 8 / NW) void fwd_kernel(FaAr
         for (int tt = 0; tt < 2; ++tt)
           sacc[tt] = E::mfma(lds_at<F16>(smem, L.row[kk] + KS + tt * 32 * ROWB), qf[kk], sacc[tt]);
       const bool need_mask = (n0 + BN > Sk) || (CAUSAL && n0 + BN - 1 > qrow0 + coff);
+      // scaled logits x = c·s (+ mask); on unmasked tiles without an additive mask the scale is
+      // folded into the exponent below (p = exp2(c·s − m): one fma per element, and the row max
+      // taken on the raw scores, c > 0)
+      const bool fold = !(FEAT & F_MASK) && !need_mask;
       float mx = -INFINITY;
       auto scale_mask = [&](auto maskc) {
         constexpr bool MASKED = decltype(maskc)::value;
@@ -411,20 +416,44 @@ __global__ __launch_bounds__(64 * NW, D > 128 ? 1 : 8 / NW) void fwd_kernel(FaAr
             }
           }
       };
-      if (need_mask) scale_mask(std::true_type{});
-      else scale_mask(std::false_type{});
+      if (fold) {
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[tt][r]);
+        mx *= c;
+      } else if (need_mask) {
+        scale_mask(std::true_type{});
+      } else {
+        scale_mask(std::false_type{});
+      }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m_i, mx);
+      // lazy rescale: the running max m_i moves only when a row's tile max exceeds it by more than
+      // 8 (log2 units); p = exp2(x − m_i) ≤ 256 is exact in f32 / bf16 range and l_i, O use the same
+      // m_i, so the result is unchanged while most tiles skip the O rescale
+      const float m_new = mx > m_i + 8.f ? mx : m_i;
       const float msub = m_new == -INFINITY ? 0.f : m_new;
       float rs = 0.f;
+      if (fold) {
+        const float nm = -msub;
 #pragma unroll
-      for (int tt = 0; tt < 2; ++tt)
+        for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = fast_exp2(sacc[tt][r] - msub);
-          sacc[tt][r] = p;
-          rs += p;
-        }
+          for (int r = 0; r < 16; ++r) {
+            const float p = fast_exp2(fmaf(sacc[tt][r], c, nm));
+            sacc[tt][r] = p;
+            rs += p;
+          }
+      } else {
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float p = fast_exp2(sacc[tt][r] - msub);
+            sacc[tt][r] = p;
+            rs += p;
+          }
+      }
       rs += __shfl_xor(rs, 32, 64);
       if (FEAT & F_DROP) {  // O accumulates P∘M; the normaliser l keeps the undropped sum
 #pragma unroll
@@ -637,6 +666,10 @@ __global__ __launch_bounds__(256, 2) void fwd_persist_kernel(FaArgs a) {
       const unsigned short* mrow = nullptr;
       if (FEAT & F_MASK)
         mrow = (const unsigned short*)a.mask + cur.b * a.smb + cur.hq * a.smh + (long long)min(qpos, Sq - 1) * a.smq;
+      // scaled logits x = c·s (+ mask); on unmasked tiles without an additive mask the scale is
+      // folded into the exponent below (p = exp2(c·s − m): one fma per element, and the row max
+      // taken on the raw scores, c > 0)
+      const bool fold = !(FEAT & F_MASK) && !need_mask;
       float mx = -INFINITY;
       auto scale_mask = [&](auto maskc) {
         constexpr bool MASKED = decltype(maskc)::value;
@@ -657,20 +690,44 @@ __global__ __launch_bounds__(256, 2) void fwd_persist_kernel(FaArgs a) {
             }
           }
       };
-      if (need_mask) scale_mask(std::true_type{});
-      else scale_mask(std::false_type{});
+      if (fold) {
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sacc[tt][r]);
+        mx *= c;
+      } else if (need_mask) {
+        scale_mask(std::true_type{});
+      } else {
+        scale_mask(std::false_type{});
+      }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m_i, mx);
+      // lazy rescale: the running max m_i moves only when a row's tile max exceeds it by more than
+      // 8 (log2 units); p = exp2(x − m_i) ≤ 256 is exact in f32 / bf16 range and l_i, O use the same
+      // m_i, so the result is unchanged while most tiles skip the O rescale
+      const float m_new = mx > m_i + 8.f ? mx : m_i;
       const float msub = m_new == -INFINITY ? 0.f : m_new;
       float rs = 0.f;
+      if (fold) {
+        const float nm = -msub;
 #pragma unroll
-      for (int tt = 0; tt < 2; ++tt)
+        for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = fast_exp2(sacc[tt][r] - msub);
-          sacc[tt][r] = p;
-          rs += p;
-        }
+          for (int r = 0; r < 16; ++r) {
+            const float p = fast_exp2(fmaf(sacc[tt][r], c, nm));
+            sacc[tt][r] = p;
+            rs += p;
+          }
+      } else {
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float p = fast_exp2(sacc[tt][r] - msub);
+            sacc[tt][r] = p;
+            rs += p;
+          }
+      }
       rs += __shfl_xor(rs, 32, 64);
       if (FEAT & F_DROP) {
         const long long lbase = ((long long)cur.b * Hq + cur.hq) * Sq;

@@ -28,6 +28,7 @@ PIAMD_EXPORT int piamd_fa_fwd(const FaArgs* args, int f16, hipStream_t stream) {
   if (a.cu_q) a.sqb = a.skb = a.svb = a.sob = 0;
   if (a.B == 0 || a.Sq == 0) return 0;
   if (a.Sk == 0) return (int)hipErrorInvalidValue;
+  if (!f16 && fa_fwd_asm(a, stream) == 1) return 0;  // hand-scheduled kernel (fa_asm_host.hip)
   return f16 ? fa_fwd_f16(a, stream) : fa::launch_fwd<false>(a, stream);
 }
 

@@ -98,6 +98,7 @@ def _fwd(q, k, v, causal, scale, mask=None, p=0.0, seed=0, off=0):
     o = torch.empty((B, Sq, Hq, D), device=q.device, dtype=q.dtype)
     lse = torch.empty((B, Hq, Sq), device=q.device, dtype=torch.float32)
     a = _args(q, k, v, o, lse, causal, scale, mask, p, seed, off, B, Sq, Sk, Hq, Hk, D)
+    _fa_asm_load()
     _lib.call("piamd_fa_fwd", ctypes.byref(a), _f16(q), _lib.stream())
     return o, lse
 

@@ -17,9 +17,9 @@ def _asm_loaded():
     _lib.lib()
     attention._fa_asm_load()
     assert _lib.lib().piamd_fa_asm_loaded() == 1
-    _lib.call("piamd_fa_asm_enable", 3)
+    _lib.call("piamd_fa_asm_enable", 7)
     yield
-    _lib.call("piamd_fa_asm_enable", 3)
+    _lib.call("piamd_fa_asm_enable", 7)
 
 
 def _ref_grads(q, k, v, do, causal, scale):
@@ -37,10 +37,13 @@ def _ref_grads(q, k, v, do, causal, scale):
     return qf.grad, kf.grad, vf.grad
 
 
-def _run(q, k, v, do, causal, scale, use_asm):
+def _run(q, k, v, do, causal, scale, use_asm, with_o=False):
     from paddle_infer_amd.ops import _lib, attention
-    _lib.call("piamd_fa_asm_enable", 3 if use_asm else 0)
+    _lib.call("piamd_fa_asm_enable", 7 if use_asm else 0)
     o, lse = attention._fwd(q, k, v, causal, scale)
+    if with_o:
+        torch.cuda.synchronize()
+        return o, lse
     dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
     B, S, Hq, D = q.shape
     a = attention._args(q, k, v, o, lse, causal, scale, None, 0.0, 0, 0, B, S, S, Hq, k.shape[2], D)
@@ -90,7 +93,7 @@ def test_dkdv_asm_packed_qkv_strides():
     do = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16)
     sc = 1 / math.sqrt(D)
     from paddle_infer_amd.ops import _lib, attention
-    _lib.call("piamd_fa_asm_enable", 3)
+    _lib.call("piamd_fa_asm_enable", 7)
     o, lse = attention._fwd(q, k, v, True, sc)
     dqkv = torch.empty_like(qkv)
     attention._bwd(q, k, v, o, lse, do, dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2], True, sc)
@@ -112,3 +115,35 @@ def test_dkdv_asm_declines_other_shapes():
     q2 = torch.randn(1, 256, 2, 64, device=DEV, dtype=torch.bfloat16)
     a = attention._args(q2, q2, q2, q2, lse, True, 0.1, None, 0.0, 0, 0, 1, 256, 256, 2, 2, 64)
     assert _lib.lib().piamd_fa_asm_applies(ctypes.byref(a)) == 0
+
+
+def _ref_fwd(q, k, v, causal, scale):
+    qf, kf, vf = (t.float().transpose(1, 2) for t in (q, k, v))
+    Hq, Hk = q.shape[2], k.shape[2]
+    kf = kf.repeat_interleave(Hq // Hk, 1)
+    vf = vf.repeat_interleave(Hq // Hk, 1)
+    s = qf @ kf.transpose(-1, -2) * scale
+    if causal:
+        S = s.shape[-1]
+        i = torch.arange(S, device=s.device)
+        s = s.masked_fill(i[None, :] > i[:, None], float("-inf"))
+    return (torch.softmax(s, -1) @ vf).transpose(1, 2), torch.logsumexp(s, -1)
+
+
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("B,S,Hq,Hk", [(2, 256, 4, 4), (1, 512, 4, 2), (1, 1024, 2, 2)])
+def test_fwd_asm_matches_reference(causal, B, S, Hq, Hk):
+    """Assembly forward (O and lse) against fp32 PyTorch and the HIP forward kernel."""
+    torch.manual_seed(3)
+    D = 128
+    q = torch.randn(B, S, Hq, D, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(B, S, Hk, D, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(B, S, Hk, D, device=DEV, dtype=torch.bfloat16)
+    sc = 1 / math.sqrt(D)
+    o, lse = _run(q, k, v, None, causal, sc, True, with_o=True)
+    ro, rl = _ref_fwd(q, k, v, causal, sc)
+    _close(o, ro, "o")
+    torch.testing.assert_close(lse, rl, rtol=1e-3, atol=2e-3)
+    ho, hl = _run(q, k, v, None, causal, sc, False, with_o=True)
+    _close(o, ho, "o vs HIP")
+    torch.testing.assert_close(lse, hl, rtol=1e-3, atol=2e-3)

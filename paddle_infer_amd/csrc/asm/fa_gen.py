@@ -913,6 +913,7 @@ def qbuf_set(b):
 class FaDq(FaDkdv):
     NM = 48
     VTMP_UDIV = QV_TMP + 4
+    QSH = 7          # log2 of the queries per work item (4 waves × 32)
 
     # -- DMA stream (K / V tiles of 64 keys) --------------------------------------------------------
     def pending_soffs(self):
@@ -956,9 +957,9 @@ class FaDq(FaDkdv):
         self.udiv(b, hq, T + 6, qarg("Hq"), qarg("rcp_Hq"))
 
     def tiles_of(self, dst, qb):
-        if self.causal:
-            self.e(f"s_lshl_b32 s{dst}, s{qb}, 1")
-            self.e(f"s_add_u32 s{dst}, s{dst}, 2")
+        if self.causal:   # key tiles of 64 up to the item's last query
+            self.e(f"s_lshl_b32 s{dst}, s{qb}, {self.QSH - 6}")
+            self.e(f"s_add_u32 s{dst}, s{dst}, {1 << (self.QSH - 6)}")
         else:
             self.e(f"s_mov_b32 s{dst}, s{qarg('nkt')}")
 
@@ -995,7 +996,7 @@ class FaDq(FaDkdv):
     def q_soffs(self, qb, b, hq, sq, so, ss):
         """Q/dQ, dO and stats soffsets of the wave's 32 queries of item (qb, b, hq)."""
         T = Q_T
-        self.e(f"s_lshl_b32 s{T + 7}, s{qb}, 7")                        # q0 = 128 qb
+        self.e(f"s_lshl_b32 s{T + 7}, s{qb}, {self.QSH}")               # q0
         for dst, sb, sh, st in ((sq, "sqb", "sqh", "sqs"), (so, "sob", "soh", "sos")):
             self.e(f"s_mul_i32 s{dst}, s{b}, s{qarg(sb)}")
             self.e(f"s_mul_i32 s{T + 5}, s{hq}, s{qarg(sh)}")
@@ -1441,6 +1442,8 @@ LN2 = 0.6931471805599453
 class FaFwd(FaDq):
     NM = 32
     VTMP_UDIV = F_V_T + 3
+    NWV = 4          # waves per workgroup (8: 256 queries share every K/V tile, one WG per CU)
+    PPW = 4          # LDS-DMA pieces (1 KiB) per wave per 16 KiB image
 
     # -- work items ----------------------------------------------------------------------------------
     def q_load_f(self, aq, sq):
@@ -1450,7 +1453,7 @@ class FaFwd(FaDq):
     def compute_item_setup(self):
         T = Q_T
         self.decode(Q_U, T, Q_B, Q_HQ)
-        self.e(f"s_lshl_b32 s{Q_Q0}, s{T}, 7")
+        self.e(f"s_lshl_b32 s{Q_Q0}, s{T}, {self.QSH}")
         self.tiles_of(Q_TOT, T)
         self.e(f"s_mov_b32 s{Q_IT}, 0")
         self.q_soffs(T, Q_B, Q_HQ, Q_SOFFQ, Q_SOFFO, Q_SOFFS)
@@ -1474,13 +1477,13 @@ class FaFwd(FaDq):
         base = buf * F_BUF_B
         return [[f"s_add_u32 m0, s{Q_LDSW}, {base + i * 1024}\n\ts_nop 0",
                  f"buffer_load_dwordx4 v{F_V_DK + i}, s[{QSRD_K}:{QSRD_K + 3}], s{Q_SK} offen lds"]
-                for i in range(4)]
+                for i in range(self.PPW)]
 
     def dma_second(self, buf):
         base = buf * F_BUF_B + Q_OFF_V
         return [[f"s_add_u32 m0, s{Q_LDSW}, {base + i * 1024}\n\ts_nop 0",
                  f"buffer_load_dwordx4 v{F_V_DV + i}, s[{QSRD_V}:{QSRD_V + 3}], s{Q_SV} offen lds"]
-                for i in range(4)]
+                for i in range(self.PPW)]
 
     # -- MFMA stream ------------------------------------------------------------------------------------
     @staticmethod
@@ -1526,9 +1529,9 @@ class FaFwd(FaDq):
         t = F_V_T
         self.e("s_nop 15")                                             # MFMA result → VALU
         self.e("s_nop 15")
-        if self.causal:
+        if self.causal:   # the item's last key tiles cross the diagonal
             skip = self.newlab("nomask")
-            self.e(f"s_sub_u32 s{T}, s{Q_TOT}, 2")
+            self.e(f"s_sub_u32 s{T}, s{Q_TOT}, {1 << (self.QSH - 6)}")
             self.e(f"s_cmp_lt_i32 s{Q_IT}, s{T}")
             self.e(f"s_cbranch_scc1 {skip}")
             self.e(f"s_lshl_b32 s{T}, s{Q_IT}, 6")
@@ -1629,14 +1632,15 @@ class FaFwd(FaDq):
                 gaps[g].append(("lds", ("ring", 1, m), t))
         # the DMA of tile t+1 into the other buffer (free: every wave passed this body's start
         # barrier, so the previous tile is consumed), cursor advance
+        dgap = int(os.environ.get("PIAMD_FA_FWD_DMA_GAP", "1"))   # schedule sweeps (measurement)
         for i, (m0, ld) in enumerate(self.dma_first(nb) + self.dma_second(nb)):
-            gaps[i] += [("txt", m0), ("txt", ld)]
-        gaps[8].append(("adv",))
+            gaps[i * dgap] += [("txt", m0), ("txt", ld)]
+        gaps[8 * dgap].append(("adv",))
         # tile t+1 landed before its K rows are read (the lookahead reads start at gap NM−LA)
         gaps[NM - F_LA - 1].append(("txt", "s_waitcnt vmcnt(0)"))
         gaps[NM - F_LA - 1].append(("txt", "s_barrier"))
         gaps[15].append(("softmax",))
-        ls = self.lsum_ops()
+        ls = [] if "novalu" in ABL else self.lsum_ops()
         for i, op in enumerate(ls):
             gaps[16 + (i * 14) // len(ls)].append(("txt", op))
         ops = [("txt", "s_barrier")]
@@ -1672,7 +1676,10 @@ class FaFwd(FaDq):
             elif ent[0] == "adv":
                 self.advance_pending()
             elif ent[0] == "softmax":
-                self.softmax_block(resc, back)
+                if "novalu" not in ABL:   # measurement only
+                    self.softmax_block(resc, back)
+                else:
+                    self.lab(back)
             else:
                 self.e(ent[1])
         self.e(f"s_add_u32 s{Q_IT}, s{Q_IT}, 1")
@@ -1748,7 +1755,7 @@ class FaFwd(FaDq):
         self.srd(QSRD_DQ, qarg("dq"), qarg("o_bytes"))             # O (output)
         self.srd(QSRD_NL, qarg("nl"), qarg("st_bytes"))            # lse (output)
         self.e(f"v_readfirstlane_b32 s{Q_W}, v{F_V_T}")
-        self.e(f"s_lshl_b32 s{Q_LDSW}, s{Q_W}, 12")
+        self.e(f"s_lshl_b32 s{Q_LDSW}, s{Q_W}, {10 + self.PPW.bit_length() - 1}")
         self.e(f"s_and_b32 s{Q_U}, s{S_WG}, 7")
         self.e(f"s_lshr_b32 s{T}, s{qarg('G')}, 3")
         self.e(f"s_mul_i32 s{Q_U}, s{Q_U}, s{T}")
@@ -1775,13 +1782,18 @@ class FaFwd(FaDq):
         self.e(f"v_mov_b32 v{F_V_M}, v{F_V_NINF}")
         self.e(f"v_mov_b32 v{F_V_L}, 0")
         # scratch for the offset set-up: S accumulator registers (free until the first tile)
+        # LDS-DMA: piece P = PPW·w + i holds image rows 4P + g (g = lane >> 4), physical chunk
+        # lane & 15 = logical chunk ^ x(row), x = (g << 2) | (P & 3)
         x = F_V_SACC
         self.e(f"v_lshrrev_b32 v{x + 3}, 4, v{L}")
         self.e(f"v_and_b32 v{x + 4}, 15, v{L}")
-        self.e(f"s_lshl_b32 s{T}, s{Q_W}, 4")
+        self.e(f"s_mul_i32 s{T}, s{Q_W}, {4 * self.PPW}")
         self.e(f"v_add_u32 v{x + 5}, s{T}, v{x + 3}")
-        for i in range(4):
-            self.e(f"v_lshl_or_b32 v{x + 6}, v{x + 3}, 2, {i}")
+        self.e(f"s_mul_i32 s{T + 1}, s{Q_W}, {self.PPW}")
+        for i in range(self.PPW):
+            self.e(f"s_add_u32 s{T + 2}, s{T + 1}, {i}")
+            self.e(f"s_and_b32 s{T + 2}, s{T + 2}, 3")
+            self.e(f"v_lshl_or_b32 v{x + 6}, v{x + 3}, 2, s{T + 2}")
             self.e(f"v_xor_b32 v{x + 6}, v{x + 6}, v{x + 4}")
             self.e(f"v_lshlrev_b32 v{x + 6}, 4, v{x + 6}")
             self.e(f"v_add_u32 v{x + 2}, {4 * i}, v{x + 5}")
@@ -1877,13 +1889,24 @@ class FaFwd(FaDq):
         return FaDkdv.metadata(self).replace(f"group_segment_fixed_size: {LDS_BYTES}",
                                              f"group_segment_fixed_size: {F_LDS_BYTES}") \
             .replace(f".vgpr_count:     {NV + NA}", f".vgpr_count:     {F_NV + F_NA}") \
-            .replace(f".agpr_count:     {NA}", f".agpr_count:     {F_NA}")
+            .replace(f".agpr_count:     {NA}", f".agpr_count:     {F_NA}") \
+            .replace(".max_flat_workgroup_size: 256", f".max_flat_workgroup_size: {64 * self.NWV}")
+
+
+class FaFwd8(FaFwd):
+    """Eight waves (256 queries) per workgroup, one workgroup per CU: every K/V tile DMA'd into LDS
+    feeds twice the queries (half the L2→LDS and HBM traffic per query of the 4-wave kernel);
+    two waves per SIMD still overlap one wave's softmax with the other's MFMAs."""
+    NWV = 8
+    PPW = 2
+    QSH = 8
 
 
 def kernels():
     return [FaDkdv("piamd_fa_dkdv_d128_causal", True), FaDkdv("piamd_fa_dkdv_d128", False),
             FaDq("piamd_fa_dq_d128_causal", True), FaDq("piamd_fa_dq_d128", False),
-            FaFwd("piamd_fa_fwd_d128_causal", True), FaFwd("piamd_fa_fwd_d128", False)]
+            FaFwd("piamd_fa_fwd_d128_causal", True), FaFwd("piamd_fa_fwd_d128", False),
+            FaFwd8("piamd_fa_fwd8_d128_causal", True), FaFwd8("piamd_fa_fwd8_d128", False)]
 
 
 def generate() -> str:

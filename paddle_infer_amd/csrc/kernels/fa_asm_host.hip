@@ -52,8 +52,9 @@ static_assert(sizeof(FaDqArgs) == 192, "FaDqArgs layout");
 
 std::mutex g_mu;
 hipModule_t g_mod = nullptr;
-hipFunction_t g_fn[6] = {};
+hipFunction_t g_fn[8] = {};
 int g_enabled = -1;  // bit 0: dK/dV kernel, bit 1: dQ kernel, bit 2: forward kernel
+int g_fwd_nw = -1;   // forward variant: 4 or 8 waves per workgroup
 
 // PIAMD_FA_ASM: unset / 1 = every assembly kernel, 0 = none, "dkdv" / "dq" / "fwd" / "bwd" = those
 int enabled_mask() {
@@ -99,7 +100,9 @@ PIAMD_EXPORT int piamd_fa_asm_load(const char* path) {
       hipModuleGetFunction(&g_fn[2], m, "piamd_fa_dq_d128") != hipSuccess ||
       hipModuleGetFunction(&g_fn[3], m, "piamd_fa_dq_d128_causal") != hipSuccess ||
       hipModuleGetFunction(&g_fn[4], m, "piamd_fa_fwd_d128") != hipSuccess ||
-      hipModuleGetFunction(&g_fn[5], m, "piamd_fa_fwd_d128_causal") != hipSuccess)
+      hipModuleGetFunction(&g_fn[5], m, "piamd_fa_fwd_d128_causal") != hipSuccess ||
+      hipModuleGetFunction(&g_fn[6], m, "piamd_fa_fwd8_d128") != hipSuccess ||
+      hipModuleGetFunction(&g_fn[7], m, "piamd_fa_fwd8_d128_causal") != hipSuccess)
     return (int)hipErrorNotFound;
   g_mod = m;
   return 0;
@@ -111,6 +114,12 @@ PIAMD_EXPORT int piamd_fa_asm_loaded() { return g_mod != nullptr; }
 // (default 7; env PIAMD_FA_ASM)
 PIAMD_EXPORT int piamd_fa_asm_enable(int mask) {
   g_enabled = mask & 7;
+  return 0;
+}
+
+// forward kernel variant (4 or 8 waves per workgroup; tests / A-B)
+PIAMD_EXPORT int piamd_fa_fwd_nw(int nw) {
+  g_fwd_nw = nw;
   return 0;
 }
 
@@ -187,7 +196,7 @@ int fa_dkdv_asm(const FaArgs& a, hipStream_t st) {
 }
 
 // the dQ / forward argument block (fa_gen.DQ_ARGS; the forward reads dq as O and nl as lse)
-static FaDqArgs dq_args(const FaArgs& a, int wgs_per_cu) {
+static FaDqArgs dq_args(const FaArgs& a, int wgs_per_cu, int qsh = 7) {
   FaDqArgs g{};
   g.q = a.q;
   g.k = a.k;
@@ -211,7 +220,7 @@ static FaDqArgs dq_args(const FaArgs& a, int wgs_per_cu) {
   g.rcp_group = 1.f / (float)g.group;
   g.Sq = a.Sq;
   g.nkt = a.Sk / 64;
-  const unsigned nqb = (unsigned)(a.Sq / 128);
+  const unsigned nqb = (unsigned)(a.Sq >> qsh);  // work items of 2^qsh queries
   g.npair = nqb / 2;
   g.nqb1 = nqb - 1;
   g.rcp_npair = 1.f / (float)g.npair;
@@ -243,13 +252,22 @@ int fa_fwd_asm(const FaArgs& a, hipStream_t st) {
   FaArgs b = a;
   b.dq = a.o;  // output O (strides sob / sos / soh)
   b.delta = nullptr;
-  FaDqArgs g = dq_args(b, 2);
+  // 4-wave kernel, two workgroups per CU (default); PIAMD_FA_FWD_NW=8: the 8-wave kernel (256
+  // queries per workgroup, one per CU, half the K/V tile traffic per query) where the query
+  // blocks pair up — measured 3 % slower at B96 S1024 H16 (695 vs 675 us, profiles/fa_asm_r6.txt)
+  if (g_fwd_nw < 0) {
+    const char* e = getenv("PIAMD_FA_FWD_NW");
+    g_fwd_nw = e ? atoi(e) : 4;
+  }
+  const bool w8 = g_fwd_nw == 8 && a.Sq % 512 == 0;
+  FaDqArgs g = dq_args(b, w8 ? 1 : 2, w8 ? 8 : 7);
   g.dq = a.o;
   g.nl = a.lse;
   g.nd = nullptr;
   g.dout = nullptr;
   size_t sz = sizeof(g);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &g, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
-  hipError_t err = hipModuleLaunchKernel(g_fn[a.causal ? 5 : 4], g.G, 1, 1, 256, 1, 1, 0, st, nullptr, cfg);
+  hipFunction_t f = w8 ? g_fn[a.causal ? 7 : 6] : g_fn[a.causal ? 5 : 4];
+  hipError_t err = hipModuleLaunchKernel(f, g.G, 1, 1, w8 ? 512 : 256, 1, 1, 0, st, nullptr, cfg);
   return err == hipSuccess ? 1 : -(int)err;
 }

@@ -241,6 +241,7 @@ _SIGS["piamd_viterbi_decode"] = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void
 _SIGS["piamd_fa_asm_loaded"] = []
 _SIGS["piamd_fa_asm_enable"] = [ctypes.c_int]
 _SIGS["piamd_fa_asm_applies"] = [ctypes.c_void_p]
+_SIGS["piamd_fa_fwd_nw"] = [ctypes.c_int]
 _SIGS["piamd_transpose_bf16"] = [c_void_p, c_void_p, c_int, c_int, c_void_p]
 # src, ld, dst, R, C, Rp, Cp, lo_mask, axis, stream
 _SIGS["piamd_split3_f32"] = [c_void_p, c_ll, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p]

@@ -147,3 +147,15 @@ def test_fwd_asm_matches_reference(causal, B, S, Hq, Hk):
     ho, hl = _run(q, k, v, None, causal, sc, False, with_o=True)
     _close(o, ho, "o vs HIP")
     torch.testing.assert_close(lse, hl, rtol=1e-3, atol=2e-3)
+
+
+@pytest.mark.parametrize("causal", [True, False])
+def test_fwd8_asm_matches_reference(causal):
+    """The 8-wave forward variant (256 queries per workgroup; piamd_fa_fwd_nw(8))."""
+    from paddle_infer_amd.ops import _lib
+    _lib.call("piamd_fa_fwd_nw", 8)
+    try:
+        test_fwd_asm_matches_reference(causal, 1, 1024, 2, 2)
+        test_fwd_asm_matches_reference(causal, 2, 512, 4, 2)
+    finally:
+        _lib.call("piamd_fa_fwd_nw", 4)

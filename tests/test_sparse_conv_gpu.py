@@ -51,8 +51,9 @@ def test_sparse_conv_gpu_matches_cpu(dt, subm, cin, cout):
     ri, rv, rgx, rgw = _run(idx, val, shape, w, subm, "cpu", torch.float32)
     gi, gv, ggx, ggw = _run(idx, val, shape, w, subm, "cuda", dt)
     assert torch.equal(ri, gi)
-    tol = dict(rtol=2e-2, atol=2e-2) if dt == torch.bfloat16 else dict(rtol=1e-4, atol=1e-4)
-    torch.testing.assert_close(gv, rv, **tol)
-    torch.testing.assert_close(ggx, rgx, **tol)
-    scale = rgw.abs().max().item()
-    torch.testing.assert_close(ggw / scale, rgw / scale, **tol)
+    # bf16: the outputs themselves are bf16-rounded (2^-8 relative) after an f32 reduction over up
+    # to 27·Cin products — compare against the output scale
+    tol = dict(rtol=3e-2, atol=1e-2) if dt == torch.bfloat16 else dict(rtol=1e-4, atol=1e-4)
+    for got, ref in ((gv, rv), (ggx, rgx), (ggw, rgw)):
+        scale = max(ref.abs().max().item(), 1e-6)
+        torch.testing.assert_close(got / scale, ref / scale, **tol)

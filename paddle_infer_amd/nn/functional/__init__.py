@@ -129,11 +129,25 @@ def pad(x, pad, mode="constant", value=0.0, data_format="NCHW", name=None):
 
 def interpolate(x, size=None, scale_factor=None, mode="nearest", align_corners=False,
                 align_mode=0, data_format="NCHW", name=None):
+    """Reference `nn/functional/common.py:interpolate`; GPU float tensors resample on the own
+    kernels (ops/pool_nd.py: nearest / linear / bilinear / trilinear, 'area' = adaptive average
+    pooling); bicubic stays on ATen."""
     mode = {"bilinear": "bilinear", "nearest": "nearest", "bicubic": "bicubic", "linear": "linear",
             "trilinear": "trilinear", "area": "area"}[mode.lower()]
     ac = align_corners if mode in ("bilinear", "bicubic", "linear", "trilinear") else None
-    _lib_fallback(x, "interpolate")
-    return TF.interpolate(x, size, scale_factor, mode, align_corners=ac)
+    xf = _fmt_in(x, data_format) if data_format in ("NHWC", "NLC", "NDHWC") else x
+    if x.is_cuda and mode != "bicubic":
+        from ...ops import pool_nd
+        if pool_nd.supported(x):
+            if mode == "area":
+                osz = size if size is not None else None
+                if osz is None:
+                    sf = scale_factor if isinstance(scale_factor, (list, tuple)) else [scale_factor] * (xf.dim() - 2)
+                    osz = [int(i * f) for i, f in zip(xf.shape[2:], sf)]
+                return _fmt_out(pool_nd.adaptive_pool(xf, xf.dim() - 2, 1, osz), data_format)
+            return _fmt_out(pool_nd.interpolate(xf, size, scale_factor, mode, bool(align_corners)), data_format)
+    _lib_fallback(x, "interpolate", "bicubic / non-float dtype (ATen)")
+    return _fmt_out(TF.interpolate(xf, size, scale_factor, mode, align_corners=ac), data_format)
 
 
 upsample = interpolate
@@ -277,68 +291,123 @@ def conv1d_transpose(x, weight, bias=None, stride=1, padding=0, output_padding=0
     return _fmt_out(TF.conv_transpose1d(_fmt_in(x, data_format), weight, bias, stride, _padding(padding, 1), output_padding, groups, dilation), data_format)
 
 
+def _own_pool(x, pad):
+    """GPU float tensors with numeric padding pool on the own kernels (ops/pool_nd.py)."""
+    if not x.is_cuda:
+        return False
+    from ...ops import pool_nd
+    if pool_nd.supported(x) and not isinstance(pad, str):
+        return True
+    _lib_fallback(x, "pool", "string padding / non-float dtype (ATen)")
+    return False
+
+
+def _pool(x, nd, mode, kernel_size, stride, padding, ceil_mode, exclusive, divisor, return_mask,
+          data_format):
+    from ...ops import pool_nd
+    r = pool_nd.pool(_fmt_in(x, data_format), nd, mode, kernel_size, stride, padding, ceil_mode, exclusive,
+                     divisor, return_mask)
+    if return_mask:
+        return _fmt_out(r[0], data_format), _fmt_out(r[1], data_format)
+    return _fmt_out(r, data_format)
+
+
+def _apool(x, nd, mode, output_size, return_mask, data_format):
+    from ...ops import pool_nd
+    r = pool_nd.adaptive_pool(_fmt_in(x, data_format), nd, mode, output_size, return_mask)
+    if return_mask:
+        return _fmt_out(r[0], data_format), _fmt_out(r[1], data_format)
+    return _fmt_out(r, data_format)
+
+
 def max_pool1d(x, kernel_size, stride=None, padding=0, return_mask=False, ceil_mode=False, name=None):
-    _lib_fallback(x, "max_pool1d")
-    return TF.max_pool1d(x, kernel_size, stride, _padding(padding, 1), 1, ceil_mode, return_mask)
+    pad = _padding(padding, 1)
+    if _own_pool(x, pad):
+        return _pool(x, 1, 0, kernel_size, stride, pad, ceil_mode, True, None, return_mask, "NCL")
+    return TF.max_pool1d(x, kernel_size, stride, pad, 1, ceil_mode, return_mask)
 
 
 def max_pool2d(x, kernel_size, stride=None, padding=0, return_mask=False, ceil_mode=False,
                data_format="NCHW", name=None):
+    pad = _padding(padding, 2)
     if data_format == "NCHW":
         from ...ops.pool import max_pool2d_nhwc, max_pool2d_supported
-        pad = _padding(padding, 2)
         if max_pool2d_supported(x, kernel_size, stride, pad, ceil_mode, return_mask):
             return max_pool2d_nhwc(x, kernel_size, stride, pad)  # own NHWC kernels (channels-last)
-    y = TF.max_pool2d(_fmt_in(x, data_format), kernel_size, stride, _padding(padding, 2), 1, ceil_mode, return_mask)
+    if _own_pool(x, pad):
+        return _pool(x, 2, 0, kernel_size, stride, pad, ceil_mode, True, None, return_mask, data_format)
+    y = TF.max_pool2d(_fmt_in(x, data_format), kernel_size, stride, pad, 1, ceil_mode, return_mask)
     return y if return_mask else _fmt_out(y, data_format)
 
 
 def max_pool3d(x, kernel_size, stride=None, padding=0, return_mask=False, ceil_mode=False,
                data_format="NCDHW", name=None):
-    _lib_fallback(x, "max_pool3d")
-    return TF.max_pool3d(x, kernel_size, stride, _padding(padding, 3), 1, ceil_mode, return_mask)
+    pad = _padding(padding, 3)
+    if _own_pool(x, pad):
+        return _pool(x, 3, 0, kernel_size, stride, pad, ceil_mode, True, None, return_mask, data_format)
+    y = TF.max_pool3d(_fmt_in(x, data_format), kernel_size, stride, pad, 1, ceil_mode, return_mask)
+    return y if return_mask else _fmt_out(y, data_format)
 
 
 def avg_pool1d(x, kernel_size, stride=None, padding=0, exclusive=True, ceil_mode=False, name=None):
-    _lib_fallback(x, "avg_pool1d")
-    return TF.avg_pool1d(x, kernel_size, stride, _padding(padding, 1), ceil_mode, not exclusive)
+    pad = _padding(padding, 1)
+    if _own_pool(x, pad):
+        return _pool(x, 1, 1, kernel_size, stride, pad, ceil_mode, exclusive, None, False, "NCL")
+    return TF.avg_pool1d(x, kernel_size, stride, pad, ceil_mode, not exclusive)
 
 
 def avg_pool2d(x, kernel_size, stride=None, padding=0, ceil_mode=False, exclusive=True,
                divisor_override=None, data_format="NCHW", name=None):
-    _lib_fallback(x, "avg_pool2d")
-    return _fmt_out(TF.avg_pool2d(_fmt_in(x, data_format), kernel_size, stride, _padding(padding, 2), ceil_mode, not exclusive, divisor_override), data_format)
+    pad = _padding(padding, 2)
+    if _own_pool(x, pad):
+        return _pool(x, 2, 1, kernel_size, stride, pad, ceil_mode, exclusive, divisor_override, False, data_format)
+    return _fmt_out(TF.avg_pool2d(_fmt_in(x, data_format), kernel_size, stride, pad, ceil_mode, not exclusive,
+                                  divisor_override), data_format)
 
 
 def avg_pool3d(x, kernel_size, stride=None, padding=0, ceil_mode=False, exclusive=True,
                divisor_override=None, data_format="NCDHW", name=None):
-    _lib_fallback(x, "avg_pool3d")
-    return TF.avg_pool3d(x, kernel_size, stride, _padding(padding, 3), ceil_mode, not exclusive, divisor_override)
+    pad = _padding(padding, 3)
+    if _own_pool(x, pad):
+        return _pool(x, 3, 1, kernel_size, stride, pad, ceil_mode, exclusive, divisor_override, False, data_format)
+    return _fmt_out(TF.avg_pool3d(_fmt_in(x, data_format), kernel_size, stride, pad, ceil_mode, not exclusive,
+                                  divisor_override), data_format)
 
 
 def adaptive_avg_pool1d(x, output_size, name=None):
-    _lib_fallback(x, "adaptive_avg_pool1d")
+    if _own_pool(x, 0):
+        return _apool(x, 1, 1, output_size, False, "NCL")
     return TF.adaptive_avg_pool1d(x, output_size)
 
 
 def adaptive_avg_pool2d(x, output_size, data_format="NCHW", name=None):
-    _lib_fallback(x, "adaptive_avg_pool2d")
+    if _own_pool(x, 0):
+        return _apool(x, 2, 1, output_size, False, data_format)
     return _fmt_out(TF.adaptive_avg_pool2d(_fmt_in(x, data_format), output_size), data_format)
 
 
 def adaptive_avg_pool3d(x, output_size, data_format="NCDHW", name=None):
-    _lib_fallback(x, "adaptive_avg_pool3d")
-    return TF.adaptive_avg_pool3d(x, output_size)
+    if _own_pool(x, 0):
+        return _apool(x, 3, 1, output_size, False, data_format)
+    return _fmt_out(TF.adaptive_avg_pool3d(_fmt_in(x, data_format), output_size), data_format)
 
 
 def adaptive_max_pool1d(x, output_size, return_mask=False, name=None):
-    _lib_fallback(x, "adaptive_max_pool1d")
+    if _own_pool(x, 0):
+        return _apool(x, 1, 0, output_size, return_mask, "NCL")
     return TF.adaptive_max_pool1d(x, output_size, return_mask)
 
 
 def adaptive_max_pool2d(x, output_size, return_mask=False, name=None):
-    _lib_fallback(x, "adaptive_max_pool2d")
+    if _own_pool(x, 0):
+        return _apool(x, 2, 0, output_size, return_mask, "NCHW")
     return TF.adaptive_max_pool2d(x, output_size, return_mask)
+
+
+def adaptive_max_pool3d(x, output_size, return_mask=False, name=None):
+    if _own_pool(x, 0):
+        return _apool(x, 3, 0, output_size, return_mask, "NCDHW")
+    return TF.adaptive_max_pool3d(x, output_size, return_mask)
 
 
 # ------------------------------------------------------------------------------- normalization
@@ -563,7 +632,13 @@ def affine_grid(theta, out_shape, align_corners=True, name=None):
 
 
 def grid_sample(x, grid, mode="bilinear", padding_mode="zeros", align_corners=True, name=None):
-    _lib_fallback(x, "grid_sample")
+    """Reference `nn/functional/vision.py:grid_sample`; 4-D GPU float inputs sample on the own
+    kernels (ops/pool_nd.py: bilinear / nearest × zeros / border / reflection)."""
+    if x.is_cuda:
+        from ...ops import pool_nd
+        if pool_nd.grid_sample_supported(x, grid, mode, padding_mode):
+            return pool_nd.grid_sample(x, grid, mode, padding_mode, align_corners)
+    _lib_fallback(x, "grid_sample", "5-D / bicubic (ATen)")
     return TF.grid_sample(x, grid, mode, padding_mode, align_corners)
 
 

@@ -96,11 +96,6 @@ def channel_shuffle(x, groups, data_format="NCHW", name=None):
 
 
 # ----------------------------------------------------------------------------- conv / pooling
-def adaptive_max_pool3d(x, output_size, return_mask=False, name=None):
-    r = TF.adaptive_max_pool3d(x, output_size, return_indices=return_mask)
-    return r
-
-
 def _unpool(fn, x, indices, kernel_size, stride, padding, output_size, nd):
     if output_size is not None:
         output_size = list(output_size)[-nd:]

@@ -142,19 +142,21 @@ class Upsample(Layer):
                  align_mode=0, data_format="NCHW", name=None):
         super().__init__()
         self.size, self.scale_factor, self.mode, self.align_corners = size, scale_factor, mode, align_corners
+        self.align_mode, self.data_format = align_mode, data_format
 
     def forward(self, x):
-        return F.interpolate(x, self.size, self.scale_factor, self.mode, self.align_corners)
+        return F.interpolate(x, self.size, self.scale_factor, self.mode, self.align_corners, self.align_mode,
+                             self.data_format)
 
 
 class UpsamplingBilinear2D(Upsample):
     def __init__(self, size=None, scale_factor=None, data_format="NCHW", name=None):
-        super().__init__(size, scale_factor, "bilinear", True)
+        super().__init__(size, scale_factor, "bilinear", True, data_format=data_format)
 
 
 class UpsamplingNearest2D(Upsample):
     def __init__(self, size=None, scale_factor=None, data_format="NCHW", name=None):
-        super().__init__(size, scale_factor, "nearest")
+        super().__init__(size, scale_factor, "nearest", data_format=data_format)
 
 
 class PixelShuffle(Layer):

@@ -292,6 +292,19 @@ _SIGS["piamd_bn_fwd"] = ([c_int, c_int] + [c_void_p] * 3 + [c_int] * 3 + [c_void
 _SIGS["piamd_bn_set_parts"] = [c_ll, c_int]
 _SIGS["piamd_maxpool_fwd_nhwc"] = [c_void_p] * 3 + [c_int] * 13 + [c_void_p]
 _SIGS["piamd_maxpool_bwd_nhwc"] = [c_void_p] * 3 + [c_int] * 13 + [c_void_p]
+# pool_nd.hip: dtype, x|dy, y|idx, idx|dx, N, C, I[3], O[3], K[3], S[3], P[3], mode, adaptive,
+# exclusive, divisor, stream
+_SIGS["piamd_pool_nd_fwd"] = ([c_int] + [c_void_p] * 3 + [c_int] * 2 + [ctypes.POINTER(c_int)] * 5
+                              + [c_int] * 4 + [c_void_p])
+_SIGS["piamd_pool_nd_bwd"] = _SIGS["piamd_pool_nd_fwd"]
+# dtype, x|dy, y|dx(f32), N, C, I[3], O[3], scale[3], mode, align_corners, stream
+_SIGS["piamd_interp_fwd"] = ([c_int] + [c_void_p] * 2 + [c_int] * 2 + [ctypes.POINTER(c_int)] * 2
+                             + [ctypes.POINTER(c_float), c_int, c_int, c_void_p])
+_SIGS["piamd_interp_bwd"] = _SIGS["piamd_interp_fwd"]
+# dtype, x, grid, y, N, C, IH, IW, OH, OW, mode, pad, align_corners, stream
+_SIGS["piamd_grid_sample_fwd"] = [c_int] + [c_void_p] * 3 + [c_int] * 9 + [c_void_p]
+# dtype, dy, x, grid, dx(f32), dgrid(f32), N, C, IH, IW, OH, OW, mode, pad, align_corners, stream
+_SIGS["piamd_grid_sample_bwd"] = [c_int] + [c_void_p] * 5 + [c_int] * 9 + [c_void_p]
 _SIGS["piamd_bn_bwd"] = ([c_int, c_int] + [c_void_p] * 5 + [c_int] * 3 + [c_void_p] * 5
                          + [c_int, c_int, c_void_p, c_void_p])
 _SIGS["piamd_bn_fwd2"] = ([c_int, c_int] + [c_void_p] * 3 + [c_int] * 3 + [c_void_p] * 6

@@ -106,7 +106,7 @@ def test_assembles(tmp_path):
     src = tmp_path / "fa.s"
     src.write_text(F.generate())
     txt = src.read_text()
-    assert txt.count("v_mfma_f32_32x32x16_bf16") == 2 * 3 * 64 + 2 * 3 * 48 + 2 * 2 * 32  # dK/dV, dQ, fwd
+    assert txt.count("v_mfma_f32_32x32x16_bf16") == 2 * 3 * 64 + 2 * 3 * 48 + 2 * 2 * 2 * 32  # dK/dV, dQ, fwd (4- and 8-wave)
     r = subprocess.run(["/opt/rocm/lib/llvm/bin/clang", "-x", "assembler", "-target", "amdgcn-amd-amdhsa",
                         "-mcpu=gfx950", "-c", str(src), "-o", str(tmp_path / "fa.o")],
                        capture_output=True, text=True)

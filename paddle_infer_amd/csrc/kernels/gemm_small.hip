@@ -96,8 +96,9 @@ __device__ __forceinline__ void sg_store(const SgArgs& p, int m, int n, f32x4 v,
   }
 }
 
-template <bool F16, int MB, int NB, int WN, int D, bool LN = false>
+template <bool F16, int MB, int NB, int WN, int D, bool LN = false, int DB = D>
 __global__ __launch_bounds__(256) void small_gemm_kernel(SgArgs p, int* __restrict__ cnt) {
+  static_assert(DB >= D && DB % D == 0, "B ring depth must be a multiple of the A ring depth");
   constexpr int WK = 4 / WN;
   __shared__ f32x4 red[WK > 1 ? 4 : 1][MB * NB][64];
   __shared__ float2 lst[LN && WK > 1 ? 4 : 1][MB][16];  // LN: per-wave row (Σa, Σa²)
@@ -131,17 +132,13 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(SgArgs p, int* __restri
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = 0x3F80;  // bf16 1.0 (LN mode is bf16-only)
 
-  // D-deep register ring of operand fragments: step i computes on slot i % D, then refills it
-  // with step i + D, so D k64 steps of loads are in flight per wave
-  u16x8 ar[D][MB][2], br[D][NB][2];
-  auto load = [&](int kb, u16x8 (&ad)[MB][2], u16x8 (&bd)[NB][2]) {
+  // Register rings of operand fragments: step i computes on A slot i % D and B slot i % DB, then
+  // refills them with steps i + D / i + DB — D k64 steps of A loads (L2-resident activations) and
+  // DB of B loads (the weight stream from HBM) in flight per wave. DB > D: the weight stream of a
+  // wave's whole K range is issued up front (one HBM round trip) while A follows in L2 trips.
+  u16x8 ar[D][MB][2], br[DB][NB][2];
+  auto loadA = [&](int kb, u16x8 (&ad)[MB][2]) {
     const long long k = (long long)kb << 6;
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
-      const u16x8* s = reinterpret_cast<const u16x8*>(brow[nb] + k);
-      bd[nb][0] = s[0];
-      bd[nb][1] = s[1];
-    }
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) {
       const u16x8* s = reinterpret_cast<const u16x8*>(arow[mb] + k);
@@ -149,32 +146,63 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(SgArgs p, int* __restri
       ad[mb][1] = s[1];
     }
   };
+  auto loadB = [&](int kb, u16x8 (&bd)[NB][2]) {
+    const long long k = (long long)kb << 6;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const u16x8* s = reinterpret_cast<const u16x8*>(brow[nb] + k);
+      bd[nb][0] = s[0];
+      bd[nb][1] = s[1];
+    }
+  };
   const int kb0 = kb_beg + wk;
+  if constexpr (DB == D) {
 #pragma unroll
-  for (int d = 0; d < D; ++d)
-    if (kb0 + d * WK < kb_end) load(kb0 + d * WK, ar[d], br[d]);
-  for (int kb = kb0; kb < kb_end; kb += D * WK) {
+    for (int d = 0; d < D; ++d)
+      if (kb0 + d * WK < kb_end) {
+        loadB(kb0 + d * WK, br[d]);
+        loadA(kb0 + d * WK, ar[d]);
+      }
+  } else {  // A of the first step first: its wait then covers no later-issued B load
+    if (kb0 < kb_end) loadA(kb0, ar[0]);
 #pragma unroll
-    for (int d = 0; d < D; ++d) {
+    for (int d = 0; d < DB; ++d)
+      if (kb0 + d * WK < kb_end) loadB(kb0 + d * WK, br[d]);
+#pragma unroll
+    for (int d = 1; d < D; ++d)
+      if (kb0 + d * WK < kb_end) loadA(kb0 + d * WK, ar[d]);
+  }
+  for (int kb = kb0; kb < kb_end; kb += DB * WK) {
+#pragma unroll
+    for (int d = 0; d < DB; ++d) {
       const int k = kb + d * WK;
       if (k >= kb_end) break;
+      const int da = d % D;
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
           for (int nb = 0; nb < NB; ++nb)
-            acc[mb][nb] = mma16<F16>(br[d][nb][s], ar[d][mb][s], acc[mb][nb]);
+            acc[mb][nb] = mma16<F16>(br[d][nb][s], ar[da][mb][s], acc[mb][nb]);
       if constexpr (LN) {  // row statistics on the matrix cores: ones·Aᵀ and A·Aᵀ blocks
 #pragma unroll
         for (int s = 0; s < 2; ++s)
 #pragma unroll
           for (int mb = 0; mb < MB; ++mb) {
-            accS[mb] = mma16<F16>(ones, ar[d][mb][s], accS[mb]);
-            accQ[mb] = mma16<F16>(ar[d][mb][s], ar[d][mb][s], accQ[mb]);
+            accS[mb] = mma16<F16>(ones, ar[da][mb][s], accS[mb]);
+            accQ[mb] = mma16<F16>(ar[da][mb][s], ar[da][mb][s], accQ[mb]);
           }
       }
-      if (k + D * WK < kb_end) load(k + D * WK, ar[d], br[d]);
+      if constexpr (DB == D) {
+        if (k + D * WK < kb_end) {
+          loadB(k + D * WK, br[d]);
+          loadA(k + D * WK, ar[da]);
+        }
+      } else {
+        if (k + D * WK < kb_end) loadA(k + D * WK, ar[da]);
+        if (k + DB * WK < kb_end) loadB(k + DB * WK, br[d]);
+      }
     }
   }
   float s1[MB], s2[MB];  // LN: Σa / Σa² of row r16 of block mb over this wave's K range
@@ -294,7 +322,21 @@ void sg_launch(const SgArgs& p, int ks, int depth, int* cnt, hipStream_t st) {
       return;
     }
   }
-  if (depth >= 2)
+  // depth = A depth | (B depth << 4); B depths 2 / 4 / 8 with A depth 1, one wave column (WN = 1)
+  const int db = depth >> 4;
+  if constexpr (WN == 1) {
+    if (db == 2 || db == 4 || db == 8) {
+      if ((depth & 15) != 1) return;
+      if (db == 2)
+        hipLaunchKernelGGL((small_gemm_kernel<F16, MB, NB, 1, 1, false, 2>), grid, dim3(256), 0, st, p, cnt);
+      else if (db == 4)
+        hipLaunchKernelGGL((small_gemm_kernel<F16, MB, NB, 1, 1, false, 4>), grid, dim3(256), 0, st, p, cnt);
+      else
+        hipLaunchKernelGGL((small_gemm_kernel<F16, MB, NB, 1, 1, false, 8>), grid, dim3(256), 0, st, p, cnt);
+      return;
+    }
+  }
+  if ((depth & 15) >= 2)
     hipLaunchKernelGGL((small_gemm_kernel<F16, MB, NB, WN, 2>), grid, dim3(256), 0, st, p, cnt);
   else
     hipLaunchKernelGGL((small_gemm_kernel<F16, MB, NB, WN, 1>), grid, dim3(256), 0, st, p, cnt);
@@ -324,7 +366,8 @@ int sg_dispatch(const SgArgs& p, int mb, int nb, int wn, int ks, int depth, int*
 
 // f16: fp16 operands / 16-bit output (else bf16). mb ∈ {1,2,4,8} (TM = 16·mb rows), nb ∈ {1,2,4}
 // (mb·nb ≤ 16), wn ∈ {1,2,4} waves along N (TN = 16·nb·wn columns; the other 4/wn waves split K),
-// depth ∈ {1,2} k64 steps of loads in flight per wave, ks ≥ 1 K slices. ks > 1: cnt != null → fixup mode (ws = M·N f32 and cnt = tiles ints, both
+// depth ∈ {1,2} k64 steps of loads in flight per wave (| DB << 4, DB ∈ {2,4,8}: with depth 1 and
+// wn 1, DB steps of B — the weight stream — in flight, A one step), ks ≥ 1 K slices. ks > 1: cnt != null → fixup mode (ws = M·N f32 and cnt = tiles ints, both
 // zeroed, left zeroed); cnt == null → slice mode (ws = ks·M·N f32 + a finish launch).
 // bias / resid: 16-bit, nullable. act: 0 none, 1 gelu_tanh, 2 gelu_erf, 3 relu, 4 silu.
 // ln_c1 / ln_b2 (f32 [N], both or neither): LayerNorm fold — C = act(LN(A)·Bᵀ + bias) with B the
@@ -341,6 +384,11 @@ PIAMD_EXPORT int piamd_small_gemm_ln(int f16, const void* a, long long lda, cons
     return (int)hipErrorInvalidValue;
   if ((ln_c1 != nullptr) != (ln_b2 != nullptr) || (ln_c1 && (f16 || ks != 1 || alpha != 1.f)))
     return (int)hipErrorInvalidValue;
+  {  // depth: A depth 1 | 2, optionally | (B depth 2 / 4 / 8) << 4 with A depth 1, wn 1, no LN fold
+    const int da = depth & 15, db = depth >> 4;
+    if (da < 1 || da > 2 || (db && (da != 1 || wn != 1 || ln_c1 || (db != 2 && db != 4 && db != 8))))
+      return (int)hipErrorInvalidValue;
+  }
   SgArgs p{(const bf16_t*)a, lda, (const bf16_t*)b, ldb, c, ldc, ws, (const bf16_t*)bias,
            (const bf16_t*)resid, ldr, alpha, M, N, K, c_f32, act, ln_c1, ln_b2, ln_eps};
   int* kc = ks > 1 ? cnt : nullptr;

@@ -698,7 +698,13 @@ int launch_fwd(const void* x, const void* bias, const void* residual, const void
     }
     return (int)hipGetLastError();
   }
-  if (rows <= 64) {  // few rows (decode): a workgroup per row
+  // few rows (decode, batch-1 encoders): a workgroup per row — 4x the waves of the wave-per-row
+  // kernel, one 16-B load per lane per operand, so the load -> reduce -> store chain is shortest
+  static const int row_max = [] {
+    const char* e = getenv("PIAMD_LN_ROW_MAX");
+    return e ? atoi(e) : 512;
+  }();
+  if (rows <= row_max) {
     switch ((N / 8 + 255) / 256) {
       case 1: hipLaunchKernelGGL((ln_fwd_row_kernel<4, 1, DT>), dim3(rows), dim3(256), 0, st, ROW_ARGS); break;
       case 2: hipLaunchKernelGGL((ln_fwd_row_kernel<4, 2, DT>), dim3(rows), dim3(256), 0, st, ROW_ARGS); break;

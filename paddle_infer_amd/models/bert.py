@@ -115,11 +115,13 @@ class BertLayer(Layer):
         qkv = _linear(x, self.qkv_w, self.qkv_b).view(B, S, 3 * H, h // H)
         a = attention_core(qkv, H, H, attn_mask, False, pa, self.training)
         o = _linear(a, self.out_w, None)
-        x, _ = fused_add_layer_norm(o, x, self.ln1_w, self.ln1_b, cfg.layer_norm_eps, self.out_b, pd, self.training)
+        x, _ = fused_add_layer_norm(o, x, self.ln1_w, self.ln1_b, cfg.layer_norm_eps, self.out_b, pd, self.training,
+                                      need_residual=False)
         act = "gelu_tanh" if cfg.hidden_act in ("gelu_new", "gelu_tanh") else cfg.hidden_act
         f = bias_act(_linear(x, self.fc1_w, None), self.fc1_b, act)
         m = _linear(f, self.fc2_w, None)
-        x, _ = fused_add_layer_norm(m, x, self.ln2_w, self.ln2_b, cfg.layer_norm_eps, self.fc2_b, pd, self.training)
+        x, _ = fused_add_layer_norm(m, x, self.ln2_w, self.ln2_b, cfg.layer_norm_eps, self.fc2_b, pd, self.training,
+                                      need_residual=False)
         return x
 
 

@@ -187,14 +187,26 @@ class _FusedAddLNFn(torch.autograd.Function):
 
 
 def fused_add_layer_norm(x, residual, weight=None, bias=None, eps: float = 1e-5, x_bias=None,
-                         dropout_p: float = 0.0, training: bool = True):
-    """Returns ``(LN(h), h)`` with ``h = residual + dropout(x + x_bias)`` (residual may be None)."""
+                         dropout_p: float = 0.0, training: bool = True, need_residual: bool = True):
+    """Returns ``(LN(h), h)`` with ``h = residual + dropout(x + x_bias)`` (residual may be None).
+    ``need_residual=False`` (post-LN blocks, whose residual stream is the LN output): without
+    autograd the kernel writes only LN(h) — no h, mean or rstd stores — and ``h`` is None."""
     p = float(dropout_p) if training else 0.0
     N = x.shape[-1]
     if _hip_path("fused_add_layer_norm", x, residual, weight, bias, x_bias) \
             and (residual is None or residual.dtype == x.dtype):
         seed, offset = _random.next_seed_offset(x.numel()) if p > 0 else (0, 0)
         dt = x.dtype
+        if not need_residual and not (torch.is_grad_enabled() and any(
+                t is not None and t.requires_grad for t in (x, residual, weight, bias, x_bias))):
+            x2 = x.contiguous().view(-1, N)
+            r2 = residual.contiguous().view(-1, N) if residual is not None else None
+            y = torch.empty_like(x2)
+            _lib.call("piamd_layernorm_fwd", _lib.dtype_code(x2, fp16=True), x2.data_ptr(),
+                      _lib.ptr(_cast(x_bias, dt)), _lib.ptr(r2), _lib.ptr(_cast(weight, dt)),
+                      _lib.ptr(_cast(bias, dt)), y.data_ptr(), None, None, None, x2.shape[0], N, float(eps),
+                      float(p), seed, offset, 0, _lib.stream())
+            return y.view(x.shape), None
         return _FusedAddLNFn.apply(x, residual, _cast(weight, dt), _cast(bias, dt), _cast(x_bias, dt),
                                    eps, p, seed, offset)
     t = x if x_bias is None else x + x_bias

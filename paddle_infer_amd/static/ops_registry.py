@@ -149,7 +149,7 @@ def _layer_norm(ins, a):
 def _skip_ln(ins, a):
     from .. import ops
     y, _ = ops.fused_add_layer_norm(ins["X"][0], ins["Y"][0], ins["Scale"][0], ins["Bias"][0],
-                                    a.get("epsilon", 1e-5), None, 0.0, False)
+                                    a.get("epsilon", 1e-5), None, 0.0, False, need_residual=False)
     return {"Out": y}
 
 
@@ -701,7 +701,7 @@ def _fc_eltwise_ln(ins, a):
         h = F.relu(h)
     out, _ = ops.fused_add_layer_norm(h, y, ins["Scale"][0] if ins.get("Scale") else None,
                                       ins["Bias1"][0] if ins.get("Bias1") else None,
-                                      float(a.get("epsilon", 1e-5)), None, 0.0, False)
+                                      float(a.get("epsilon", 1e-5)), None, 0.0, False, need_residual=False)
     return {"Out": out}
 
 

@@ -55,10 +55,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dtype", default="fp16")
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--shapes", default="all", help="all | bert (the four M = 128 BERT-Large linears) | M,N,K;...")
     args = ap.parse_args()
+    shapes = SHAPES
+    if args.shapes == "bert":
+        shapes = SHAPES[:4]
+    elif args.shapes != "all":
+        shapes = [tuple(int(v) for v in t.split(",")) for t in args.shapes.split(";")]
     dt = torch.float16 if args.dtype == "fp16" else torch.bfloat16
     # weights rotated over > 512 MB so each call reads them from HBM, as in a real forward
-    for M, N, K in SHAPES:
+    for M, N, K in shapes:
         nw = max(2, (512 << 20) // (N * K * 2))
         ws = [torch.randn(N, K, device="cuda", dtype=dt) * 0.05 for _ in range(min(nw, 64))]
         a = torch.randn(M, K, device="cuda", dtype=dt)
@@ -73,7 +79,8 @@ def main():
             if 16 * mb > 2 * max(M, 16):
                 continue
             for wn in (1, 2, 4):
-              for depth in (1, 2):
+              # depth: A ring | B ring << 4 (B-deep variants: A depth 1, wn 1)
+              for depth in ((1, 2, 0x21, 0x41, 0x81) if wn == 1 else (1, 2)):
                 for ks in (1, 2, 4, 8):
                     if ks > K // 64 // 2:
                         continue

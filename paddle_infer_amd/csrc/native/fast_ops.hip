@@ -140,7 +140,8 @@ int64_t prod(const std::vector<int64_t>& d, size_t b, size_t e) {
 int h16(const DTensor& t) { return t.dtype == VT_FP16 ? 1 : 0; }
 
 // ------------------------------------------------------------------------- GEMM dispatcher
-// ops/gemm.py small_cfg / use_small / pick_ksplit (measured: profiles/small_gemm_tune_r4.jsonl)
+// ops/gemm.py small_cfg / use_small / pick_ksplit (measured: profiles/small_gemm_tune_r4.jsonl,
+// small_gemm_bdeep_r6.jsonl; depth = A depth | B depth << 4)
 const int kShapes[][2] = {{1, 1}, {1, 2}, {1, 4}, {2, 1}, {2, 2}, {2, 4}, {4, 1}, {4, 2}, {4, 4}, {8, 1}, {8, 2}};
 
 struct SgCfg { int mb, nb, wn, depth, ks; };
@@ -150,8 +151,8 @@ SgCfg small_cfg(int M, int N, int K) {
       {{16, 3072, 1024}, {1, 1, 1, 1, 1}}, {{16, 1024, 4096}, {1, 1, 1, 1, 4}},
       {{32, 3072, 1024}, {1, 2, 1, 1, 1}}, {{32, 1024, 4096}, {1, 1, 1, 1, 2}},
       {{64, 3072, 1024}, {2, 2, 1, 1, 1}}, {{64, 1024, 4096}, {1, 1, 1, 1, 1}},
-      {{128, 3072, 1024}, {4, 2, 1, 1, 1}}, {{128, 1024, 1024}, {1, 2, 1, 2, 1}},
-      {{128, 4096, 1024}, {4, 2, 1, 1, 1}}, {{128, 1024, 4096}, {1, 2, 1, 1, 1}},
+      {{128, 3072, 1024}, {2, 4, 1, 0x41, 1}}, {{128, 1024, 1024}, {1, 2, 1, 0x81, 1}},
+      {{128, 4096, 1024}, {2, 4, 1, 0x41, 1}}, {{128, 1024, 4096}, {2, 1, 1, 0x81, 1}},
       {{128, 6144, 2048}, {4, 4, 1, 2, 1}}, {{128, 2048, 2048}, {2, 2, 1, 1, 1}},
       {{128, 8192, 2048}, {4, 4, 1, 2, 1}}, {{256, 3072, 1024}, {4, 4, 1, 1, 1}},
       {{256, 1024, 4096}, {2, 2, 1, 2, 1}}, {{256, 2048, 2048}, {4, 2, 1, 1, 1}},

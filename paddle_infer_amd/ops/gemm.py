@@ -169,8 +169,9 @@ _SG_TUNED: dict = {
     (16, 3072, 1024): (1, 1, 1, 1, 1), (16, 1024, 4096): (1, 1, 1, 1, 4),
     (32, 3072, 1024): (1, 2, 1, 1, 1), (32, 1024, 4096): (1, 1, 1, 1, 2),
     (64, 3072, 1024): (2, 2, 1, 1, 1), (64, 1024, 4096): (1, 1, 1, 1, 1),
-    (128, 3072, 1024): (4, 2, 1, 1, 1), (128, 1024, 1024): (1, 2, 1, 2, 1),
-    (128, 4096, 1024): (4, 2, 1, 1, 1), (128, 1024, 4096): (1, 2, 1, 1, 1),
+    # M = 128 (BERT-Large batch 1): B-deep rings (depth = 1 | DB << 4; profiles/small_gemm_bdeep_r6.jsonl)
+    (128, 3072, 1024): (2, 4, 1, 0x41, 1), (128, 1024, 1024): (1, 2, 1, 0x81, 1),
+    (128, 4096, 1024): (2, 4, 1, 0x41, 1), (128, 1024, 4096): (2, 1, 1, 0x81, 1),
     (128, 6144, 2048): (4, 4, 1, 2, 1), (128, 2048, 2048): (2, 2, 1, 1, 1),
     (128, 8192, 2048): (4, 4, 1, 2, 1),
     (256, 3072, 1024): (4, 4, 1, 1, 1), (256, 1024, 4096): (2, 2, 1, 2, 1),
@@ -181,7 +182,7 @@ _SG_TUNED: dict = {
 def small_cfg(M, N, K):
     """(mb, nb, wn, depth, ks) of the skinny kernel: 16·mb rows × 16·nb·wn columns per workgroup
     (wn waves side by side along N, 4/wn splitting K), ``depth`` k64 steps of loads in flight per
-    wave, K split ks ways over workgroups when the tile grid alone cannot fill the 256 CUs."""
+    wave (``1 | DB << 4``: DB steps of the weight operand in flight, one of the activations), K split ks ways over workgroups when the tile grid alone cannot fill the 256 CUs."""
     hit = _SG_TUNED.get((M, N, K))
     if hit is not None:
         return hit
@@ -276,6 +277,7 @@ def _small_gemm_ln(a, b, out, M, N, K, cfg, act, resid, ln):
     assert a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16, "LayerNorm fold: bf16 operands"
     assert c1.dtype == torch.float32 and b2.dtype == torch.float32 and c1.numel() == N == b2.numel()
     mb, nb, wn, depth = cfg
+    depth &= 15  # the LN-fold kernels keep one ring depth for both operands
     _lib.call("piamd_small_gemm_ln", 0, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
               out.data_ptr(), out.stride(0), int(out.dtype == torch.float32), M, N, K, mb, nb, wn,
               depth, 1, 1.0, None, ACTS[act], _lib.ptr(resid),

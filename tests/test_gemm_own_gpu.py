@@ -145,6 +145,8 @@ def test_small_gemm_configs(dtype, M, N, K):
             for ks in (1, 2, 4):
                 if ks <= K // 64:
                     cfgs.add((mb, nb, wn, 1 + (ks + wn) % 2, ks))
+                    if wn == 1:  # B-deep rings: the weight stream DB k64 steps ahead of A
+                        cfgs.add((mb, nb, 1, 1 | ({1: 2, 2: 4, 4: 8}[ks] << 4), ks))
     for cfg in sorted(cfgs):
         _close(small_gemm(a, b, cfg=cfg), ref, 0.01)
         if cfg[4] > 1:

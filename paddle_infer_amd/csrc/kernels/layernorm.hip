@@ -444,12 +444,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
 
 // 1024 < N <= 2048 (GPT-1.3B's 2048): TWO waves per row, each owning half the columns (2 vectors
 // per lane), and the NEXT row's h / dy / mean / rstd prefetched into a second register stage, so
-// every wave keeps two row fetches in flight at ~160 VGPRs (3 waves per SIMD); the wave-per-row
+// every wave keeps two row fetches in flight (h, dy and the residual gradient of the next row
+// prefetched) at <= 168 VGPRs (3 waves per SIMD); the wave-per-row
 // kernel at this width holds 220 VGPRs for one row (2 waves per SIMD). The halves' row sums meet
 // through LDS (parity-double-buffered: one barrier per row); the trip count is uniform over the
 // workgroup so both row pairs reach every barrier.
 template <int DT>
-__global__ __launch_bounds__(256) void ln_bwd_pair_kernel(
+__device__ __forceinline__ void ln_bwd_pair_body(
     const typename IO<DT>::T* __restrict__ dy, const typename IO<DT>::T* __restrict__ h,
     const typename IO<DT>::T* __restrict__ gamma, const float* __restrict__ mean_in,
     const float* __restrict__ rstd_in, const typename IO<DT>::T* __restrict__ dres_in,
@@ -471,7 +472,7 @@ __global__ __launch_bounds__(256) void ln_bwd_pair_kernel(
   const int stride = gridDim.x * 2;
   const int row0 = blockIdx.x * 2 + rp;
   const int iters = rows > (int)blockIdx.x * 2 ? (rows - (int)blockIdx.x * 2 + stride - 1) / stride : 0;
-  typename io::Raw hr2[2][NV], dr2[2][NV];
+  typename io::Raw hr2[2][NV], dr2[2][NV], rr2[2][NV];
   float mean2[2], rstd2[2];
   auto vcol = [&](int i) { return half * (NV * 64) + i * 64 + lane; };
   auto load = [&](int row, auto pc) {
@@ -485,6 +486,7 @@ __global__ __launch_bounds__(256) void ln_bwd_pair_kernel(
       const int vi = min(vcol(i), nvec - 1);
       hr2[P][i] = io::ldraw(h + base + vi * 8);
       dr2[P][i] = io::ldraw(dy + base + vi * 8);
+      if (dres_in) rr2[P][i] = io::ldraw(dres_in + base + vi * 8);  // prefetched with h / dy
     }
   };
   auto body = [&](int k, auto pc) {
@@ -495,13 +497,11 @@ __global__ __launch_bounds__(256) void ln_bwd_pair_kernel(
     const float mean = mean2[P], rstd = rstd2[P];
     const auto& hr = hr2[P];
     const auto& dr = dr2[P];
-    typename io::Raw rr[NV], gr[NV];
+    const auto& rr = rr2[P];
+    typename io::Raw gr[NV];  // gamma: L1-resident, re-read per row (registers are the limit)
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int vi = min(vcol(i), nvec - 1);
-      if (dres_in) rr[i] = io::ldraw(dres_in + base + vi * 8);
-      if (gamma) gr[i] = io::ldraw(gamma + vi * 8);
-    }
+    for (int i = 0; i < NV; ++i)
+      if (gamma) gr[i] = io::ldraw(gamma + min(vcol(i), nvec - 1) * 8);
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
@@ -594,6 +594,29 @@ __global__ __launch_bounds__(256) void ln_bwd_pair_kernel(
   }
 }
 
+
+// 16-bit: 3 waves per SIMD (<= 168 VGPRs with the residual-gradient prefetch); f32 rows hold
+// twice the register bytes and keep the compiler's own allocation
+#define LN_BWD_PAIR_PARAMS                                                                         \
+  const typename IO<DT>::T *__restrict__ dy, const typename IO<DT>::T *__restrict__ h,             \
+      const typename IO<DT>::T *__restrict__ gamma, const float *__restrict__ mean_in,             \
+      const float *__restrict__ rstd_in, const typename IO<DT>::T *__restrict__ dres_in,           \
+      typename IO<DT>::T *__restrict__ dres, typename IO<DT>::T *__restrict__ dx,                  \
+      float *__restrict__ acc_dg, float *__restrict__ acc_db, float *__restrict__ acc_dbias, int rows, \
+      int N, float p_drop, uint64_t seed, uint64_t offset, int rms
+#define LN_BWD_PAIR_ARGS dy, h, gamma, mean_in, rstd_in, dres_in, dres, dx, acc_dg, acc_db, acc_dbias, \
+                         rows, N, p_drop, seed, offset, rms
+template <int DT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void ln_bwd_pair_kernel(
+    LN_BWD_PAIR_PARAMS) {
+  ln_bwd_pair_body<DT>(LN_BWD_PAIR_ARGS);
+}
+template <int DT>
+__global__ __launch_bounds__(256) void ln_bwd_pair_kernel_f32(LN_BWD_PAIR_PARAMS) {
+  ln_bwd_pair_body<DT>(LN_BWD_PAIR_ARGS);
+}
+#undef LN_BWD_PAIR_PARAMS
+#undef LN_BWD_PAIR_ARGS
 // Rows longer than 2048 (the wave-per-row variant would drop to 1 wave/SIMD): a 512-thread
 // workgroup per row (NV = ceil(N / 4096) <= 4 vectors per thread), grid-stride over rows; every thread owns distinct columns, so the column partials go
 // straight to the atomics without an LDS reduction.
@@ -774,7 +797,10 @@ int launch_bwd(const void* dy, const void* h, const void* gamma, const float* me
   }
   dim3 grid(bwd_grid(rows, N)), block(256);
   if (bwd_pair(N)) {
-    hipLaunchKernelGGL((ln_bwd_pair_kernel<DT>), grid, block, 0, st, BWD_ARGS);
+    if constexpr (DT == 0)
+      hipLaunchKernelGGL((ln_bwd_pair_kernel_f32<DT>), grid, block, 0, st, BWD_ARGS);
+    else
+      hipLaunchKernelGGL((ln_bwd_pair_kernel<DT>), grid, block, 0, st, BWD_ARGS);
     return (int)hipGetLastError();
   }
   switch ((N / 8 + 63) / 64) {

@@ -97,12 +97,18 @@ def _build_lib(srcs, out, compiler, flags, link_flags, hdr_time, verbose, jobs) 
             for f in cf.as_completed(futs):
                 if verbose:
                     print(f"[piamd build] compiled {os.path.basename(f.result())}", flush=True)
-    need_link = todo or not os.path.exists(out) or any(
+    # the object list is recorded next to the library: a removed or added source relinks too
+    manifest = out + ".objs"
+    listing = "\n".join(sorted(os.path.basename(o) for o in objs))
+    same_set = os.path.exists(manifest) and open(manifest).read() == listing
+    need_link = todo or not same_set or not os.path.exists(out) or any(
         os.path.getmtime(o) > os.path.getmtime(out) for o in objs)
     if need_link:
         tmp = out + ".tmp"
         _compile([compiler, "-shared", *objs, "-o", tmp, *link_flags], out)
         os.replace(tmp, out)
+        with open(manifest, "w") as f:
+            f.write(listing)
         if verbose:
             print(f"[piamd build] linked {out}", flush=True)
     return bool(need_link)

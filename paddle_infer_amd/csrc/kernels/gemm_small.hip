@@ -22,12 +22,14 @@
 //     a k64 step loads k = 16g … 16g+15 of its row; MFMA sub-step s uses elements 8s … 8s+7 of it
 //     (a permutation of the k sum, identical for A and B).
 //   * rows ≥ M / columns ≥ N read a clamped (valid) row and are never stored.
-//   * LayerNorm fold (LN, bf16, KS = 1): C = act(LN(A)·Bᵀ + bias) with the host-side fold
+//   * LayerNorm fold (LN, bf16 / fp16, KS = 1): C = act(LN(A)·Bᵀ + bias) with the host-side fold
 //     B' = B∘γ, c1[n] = Σ_k B'[n][k], b2[n] = bias[n] + Σ_k β[k]·B[n][k], so that
 //     LN(a)·B = rstd·(a·B'ᵀ − mean·c1) + b2. The kernel runs on the RAW rows: every lane adds up
 //     Σa and Σa² of the A fragments it already loads, the four lane groups and the K-splitting
 //     waves combine them, and the epilogue applies rstd·(acc − mean·c1[n]) + b2[n]. No separate
-//     LayerNorm launch (serving-batch decode: reference fused_multi_transformer pre-LN).
+//     LayerNorm launch (serving-batch decode: reference fused_multi_transformer pre-LN; post-LN
+//     BERT inference at few rows, where the producer of the raw rows skips its LayerNorm and the
+//     statistics computed here also feed the residual epilogue of a later GEMM via ln_stats).
 // Contract: K % 64 == 0, N % 4 == 0, lda / ldb % 8 == 0, 16-B aligned operands.
 #include "common.h"
 
@@ -71,19 +73,30 @@ struct SgArgs {
   const float* ln_c1;  // LN fold: [N] column sums of B' (null: no LayerNorm)
   const float* ln_b2;  // LN fold: [N] bias + B·β
   float ln_eps;
+  float* ln_stats;         // LN fold: [M] (mean, rstd) of the raw A rows written out (nullable)
+  const float* rln_stats;  // deferred LayerNorm of the residual: [M] (mean, rstd) of its raw rows
+  const bf16_t* rln_g;     // ... and its 16-bit γ / β [N] (resid added as LN(resid) when set)
+  const bf16_t* rln_b;
 };
 
 // Epilogue value of (m, n..n+3) → C.
 template <bool F16, bool LN = false>
 __device__ __forceinline__ void sg_store(const SgArgs& p, int m, int n, f32x4 v, float mu = 0.f,
                                          float rs = 1.f) {
+  float2 rst = make_float2(0.f, 1.f);
+  if (p.rln_stats) rst = reinterpret_cast<const float2*>(p.rln_stats)[m];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     float x;
     if constexpr (LN) x = rs * (v[j] - mu * p.ln_c1[n + j]) + p.ln_b2[n + j];
     else x = v[j] * p.alpha + (p.bias ? h2f<F16>(p.bias[n + j]) : 0.f);
     x = sg_act(x, p.act);
-    if (p.resid) x += h2f<F16>(p.resid[(long long)m * p.ldr + n + j]);
+    if (p.resid) {
+      float r = h2f<F16>(p.resid[(long long)m * p.ldr + n + j]);
+      if (p.rln_stats)  // residual kept raw by its producer: LN applied here (post-LN chains)
+        r = (r - rst.x) * rst.y * h2f<F16>(p.rln_g[n + j]) + h2f<F16>(p.rln_b[n + j]);
+      x += r;
+    }
     v[j] = x;
   }
   if (p.c_f32) {
@@ -130,7 +143,7 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(SgArgs p, int* __restri
   for (int mb = 0; mb < (LN ? MB : 1); ++mb) accS[mb] = accQ[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
   u16x8 ones;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) ones[e] = 0x3F80;  // bf16 1.0 (LN mode is bf16-only)
+  for (int e = 0; e < 8; ++e) ones[e] = F16 ? 0x3C00 : 0x3F80;  // 1.0 in the operand type
 
   // Register rings of operand fragments: step i computes on A slot i % D and B slot i % DB, then
   // refills them with steps i + D / i + DB — D k64 steps of A loads (L2-resident activations) and
@@ -243,6 +256,15 @@ __global__ __launch_bounds__(256) void small_gemm_kernel(SgArgs p, int* __restri
       mu[mb] = a / p.K;
       rs[mb] = rsqrtf(fmaxf(b / p.K - mu[mb] * mu[mb], 0.f) + p.ln_eps);
     }
+    // row statistics out (for a later consumer of the same raw rows, e.g. the residual epilogue
+    // of the next GEMM): column block 0, wave 0, one lane per row
+    if (p.ln_stats && blockIdx.x == 0 && w == 0 && g == 0) {
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) {
+        const int m = m0 + 16 * mb + r16;
+        if (m < p.M) reinterpret_cast<float2*>(p.ln_stats)[m] = make_float2(mu[mb], rs[mb]);
+      }
+    }
   }
   // D = B·Aᵀ block: lane holds rows m = r16 of the A block, columns n = 4g + j of the B block
   float sink = 0.f;
@@ -313,14 +335,18 @@ __global__ __launch_bounds__(256) void small_gemm_finish(SgArgs p, int KS) {
 template <bool F16, int MB, int NB, int WN>
 void sg_launch(const SgArgs& p, int ks, int depth, int* cnt, hipStream_t st) {
   dim3 grid((p.N + 16 * NB * WN - 1) / (16 * NB * WN), (p.M + 16 * MB - 1) / (16 * MB), ks);
-  if constexpr (!F16) {
-    if (p.ln_c1) {  // LayerNorm fold (bf16, ks == 1 checked by the caller)
-      if (depth >= 2)
-        hipLaunchKernelGGL((small_gemm_kernel<F16, MB, NB, WN, 2, true>), grid, dim3(256), 0, st, p, cnt);
-      else
-        hipLaunchKernelGGL((small_gemm_kernel<F16, MB, NB, WN, 1, true>), grid, dim3(256), 0, st, p, cnt);
-      return;
+  if (p.ln_c1) {  // LayerNorm fold (ks == 1 checked by the caller)
+    if constexpr (WN == 1) {
+      if ((depth >> 4) == 4) {  // weight stream 4 k64 steps deep (the M = 128 BERT configs)
+        hipLaunchKernelGGL((small_gemm_kernel<F16, MB, NB, 1, 1, true, 4>), grid, dim3(256), 0, st, p, cnt);
+        return;
+      }
     }
+    if ((depth & 15) >= 2)
+      hipLaunchKernelGGL((small_gemm_kernel<F16, MB, NB, WN, 2, true>), grid, dim3(256), 0, st, p, cnt);
+    else
+      hipLaunchKernelGGL((small_gemm_kernel<F16, MB, NB, WN, 1, true>), grid, dim3(256), 0, st, p, cnt);
+    return;
   }
   // depth = A depth | (B depth << 4); B depths 2 / 4 / 8 with A depth 1, one wave column (WN = 1)
   const int db = depth >> 4;
@@ -372,25 +398,31 @@ int sg_dispatch(const SgArgs& p, int mb, int nb, int wn, int ks, int depth, int*
 // bias / resid: 16-bit, nullable. act: 0 none, 1 gelu_tanh, 2 gelu_erf, 3 relu, 4 silu.
 // ln_c1 / ln_b2 (f32 [N], both or neither): LayerNorm fold — C = act(LN(A)·Bᵀ + bias) with B the
 // folded weight B∘γ, c1 its row sums and b2 = bias + B·β (the bias argument is then ignored);
-// bf16 only, ks == 1, alpha == 1.
+// ks == 1, alpha == 1; ln_stats (f32 [M][2], nullable): the (mean, rstd) of each raw A row out.
+// rln_stats (f32 [M][2]) + rln_g / rln_b (16-bit [N]), with resid: the residual is a raw row whose
+// LayerNorm its producer deferred — LN(resid) = (r − mean)·rstd·γ + β is added instead of r.
 PIAMD_EXPORT int piamd_small_gemm_ln(int f16, const void* a, long long lda, const void* b,
                                      long long ldb, void* c, long long ldc, int c_f32, int M, int N,
                                      int K, int mb, int nb, int wn, int depth, int ks, float alpha,
                                      const void* bias, int act, const void* resid, long long ldr,
                                      float* ws, int* cnt, const float* ln_c1, const float* ln_b2,
-                                     float ln_eps, hipStream_t st) {
+                                     float ln_eps, float* ln_stats, const float* rln_stats,
+                                     const void* rln_g, const void* rln_b, hipStream_t st) {
   if (M <= 0 || N <= 0 || K <= 0 || K % 64 || N % 4 || lda % 8 || ldb % 8 || ldc % 4 || ks < 1 ||
       ks > K / 64 || (ks > 1 && !ws) || ((uintptr_t)a | (uintptr_t)b | (uintptr_t)c) % 16)
     return (int)hipErrorInvalidValue;
-  if ((ln_c1 != nullptr) != (ln_b2 != nullptr) || (ln_c1 && (f16 || ks != 1 || alpha != 1.f)))
+  if ((ln_c1 != nullptr) != (ln_b2 != nullptr) || (ln_c1 && (ks != 1 || alpha != 1.f)) ||
+      (ln_stats && !ln_c1))
     return (int)hipErrorInvalidValue;
-  {  // depth: A depth 1 | 2, optionally | (B depth 2 / 4 / 8) << 4 with A depth 1, wn 1, no LN fold
+  if (rln_stats && (!resid || !rln_g || !rln_b)) return (int)hipErrorInvalidValue;
+  {  // depth: A depth 1 | 2, optionally | (B depth 2 / 4 / 8) << 4 with A depth 1, wn 1 (LN fold: 4)
     const int da = depth & 15, db = depth >> 4;
-    if (da < 1 || da > 2 || (db && (da != 1 || wn != 1 || ln_c1 || (db != 2 && db != 4 && db != 8))))
+    if (da < 1 || da > 2 || (db && (da != 1 || wn != 1 || (ln_c1 && db != 4) || (db != 2 && db != 4 && db != 8))))
       return (int)hipErrorInvalidValue;
   }
   SgArgs p{(const bf16_t*)a, lda, (const bf16_t*)b, ldb, c, ldc, ws, (const bf16_t*)bias,
-           (const bf16_t*)resid, ldr, alpha, M, N, K, c_f32, act, ln_c1, ln_b2, ln_eps};
+           (const bf16_t*)resid, ldr, alpha, M, N, K, c_f32, act, ln_c1, ln_b2, ln_eps, ln_stats,
+           rln_stats, (const bf16_t*)rln_g, (const bf16_t*)rln_b};
   int* kc = ks > 1 ? cnt : nullptr;
   const int rc = f16 ? sg_dispatch<true>(p, mb, nb, wn, ks, depth, kc, st)
                      : sg_dispatch<false>(p, mb, nb, wn, ks, depth, kc, st);
@@ -409,5 +441,6 @@ PIAMD_EXPORT int piamd_small_gemm(int f16, const void* a, long long lda, const v
                                   int act, const void* resid, long long ldr, float* ws, int* cnt,
                                   hipStream_t st) {
   return piamd_small_gemm_ln(f16, a, lda, b, ldb, c, ldc, c_f32, M, N, K, mb, nb, wn, depth, ks,
-                             alpha, bias, act, resid, ldr, ws, cnt, nullptr, nullptr, 0.f, st);
+                             alpha, bias, act, resid, ldr, ws, cnt, nullptr, nullptr, 0.f, nullptr,
+                             nullptr, nullptr, nullptr, st);
 }

@@ -24,6 +24,8 @@ a chain of Paddle ops and rewrites it into one fused op whose kernel is register
   multihead_matmul_fuse_pass      fc(QKV) + head split + attention + merge → multihead_matmul
   flash_attn_packed_fuse_pass     split(QKV) + flash_attn               → flash_attn_packed
   fc_elementwise_layernorm_fuse_pass  fc + residual add + layer_norm    → fused_fc_elementwise_layernorm
+  ln_defer_pass                   post-LN fc+LN feeding only QKV / FFN1 GEMMs + residual adds
+                                  → defer_ln (LayerNorm folded into the consumers at few rows)
   + the rest of the reference GPU list in passes_extra.py (is_test, simplify_with_basic_ops,
     constant_folding, gpu_cpu_* matmul maps / shape+matmul fusions, matmul_scale, conv + bias
     (+ residual) (+ act) → conv2d_fusion, conv + bias + bn, transpose_flatten_concat)
@@ -662,6 +664,38 @@ def fuse_multi_transformer_layer_pass(g: Graph):
     return n
 
 
+# consumers that take a deferred LayerNorm (inference/ln_defer.py) and the input slots they take it in
+_LN_DEFER_SLOTS = {"fc": ("Input",), "multihead_matmul": ("Input",), "fused_fc_elementwise_layernorm": ("Y",)}
+
+
+def ln_defer_pass(g: Graph):
+    """Post-LN chains at few rows: mark ``fused_fc_elementwise_layernorm`` ops whose output feeds
+    only fold-aware consumers (the next QKV / FFN1 GEMM, the next residual epilogue) ``defer_ln``;
+    at run time they hand on raw rows and the consumers apply the LayerNorm (``ln_defer``: weight
+    fold + matrix-core row statistics, LN'd residual in the GEMM epilogue). Reference counterpart:
+    the fused `fused_fc_elementwise_layernorm_op.cu` kernel, which still runs the LN per producer."""
+    n = 0
+    for op in _typed(g.ops):
+        if op.type != "fused_fc_elementwise_layernorm" or op.attrs.get("activation_type") not in ("", None):
+            continue
+        out = _out(op)
+        if not _pop(op, "Scale") or not _pop(op, "Bias1") or out in g.keep:
+            continue
+        cons = g.consumers(out)
+        ok = bool(cons)
+        for c in cons:
+            slots = _LN_DEFER_SLOTS.get(c.type) if c.func is None and c.paddle_inputs else None
+            if not slots or any(out in v and k not in slots for k, v in c.paddle_inputs.items()):
+                ok = False
+            elif c.type == "fc" and c.attrs.get("activation_type") not in ("", None, "gelu", "relu", "gelu_tanh"):
+                ok = False
+        if ok and not op.attrs.get("defer_ln"):
+            op.attrs["defer_ln"] = True
+            g.program._version += 1
+            n += 1
+    return n
+
+
 from .fmt_passes import (  # noqa: E402
     PASS_ORDER as _FMT_ORDER,
     fused_multi_transformer_decoder_fuse_qkv_pass, fused_multi_transformer_decoder_pass,
@@ -690,7 +724,7 @@ GPU_PASSES = [
     "fc_fuse_pass", "fc_act_fuse_pass", "fused_multi_transformer_encoder_traced_pass",
     "fuse_multi_transformer_layer_pass", "multihead_matmul_fuse_pass", "flash_attn_packed_fuse_pass",
     "fc_elementwise_layernorm_fuse_pass", "skip_layernorm_fuse_pass", "linear_bias_act_fuse_pass",
-    "conv_elementwise_add2_act_fuse_pass", "conv_elementwise_add_act_fuse_pass",
+    "ln_defer_pass", "conv_elementwise_add2_act_fuse_pass", "conv_elementwise_add_act_fuse_pass",
     "conv_elementwise_add_fuse_pass", "transpose_flatten_concat_fuse_pass", "constant_folding_pass",
 ]
 

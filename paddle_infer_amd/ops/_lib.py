@@ -231,8 +231,10 @@ _SIGS["piamd_agemm_load"] = [ctypes.c_char_p]
 _SIGS["piamd_small_gemm"] = [c_int, c_void_p, c_ll, c_void_p, c_ll, c_void_p, c_ll, c_int, c_int,
                              c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_void_p,
                              c_int, c_void_p, c_ll, c_void_p, c_void_p, c_void_p]
-# ... + ln_c1, ln_b2 (f32 [N] or null), ln_eps, stream
-_SIGS["piamd_small_gemm_ln"] = _SIGS["piamd_small_gemm"][:-1] + [c_void_p, c_void_p, c_float, c_void_p]
+# ... + ln_c1, ln_b2 (f32 [N] or null), ln_eps, ln_stats (f32 [M][2] out or null), rln_stats
+# (f32 [M][2] or null), rln_g, rln_b (16-bit [N]: LayerNorm of a raw residual), stream
+_SIGS["piamd_small_gemm_ln"] = _SIGS["piamd_small_gemm"][:-1] + [c_void_p, c_void_p, c_float, c_void_p,
+                                                                 c_void_p, c_void_p, c_void_p, c_void_p]
 _SIGS["piamd_agemm_loaded"] = []
 _SIGS["piamd_fa_asm_load"] = [ctypes.c_char_p]
 _SIGS["piamd_viterbi_decode"] = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,

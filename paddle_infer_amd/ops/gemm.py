@@ -230,21 +230,25 @@ def _sg_fixup_bufs(device, M, N, tiles):
 
 
 def small_gemm(a, b, out=None, out_f32=False, alpha=1.0, bias=None, act="none", resid=None, cfg=None,
-               slices=False, ln=None):
+               slices=False, ln=None, ln_stats=None, resid_ln=None):
     """C[M, N] = act(alpha·a[M, K]·b[N, K]ᵀ + bias) (+ resid) on the skinny MFMA kernel (both
     operands K-contiguous bf16 / fp16, K % 64 == 0, N % 4 == 0). Split-K runs in fixup mode (one
     launch; ``slices=True``: deterministic slices + a finish launch). ``ln = (c1, b2, eps)``: the
     LayerNorm fold (see :func:`ln_fold`) — ``b`` is the folded weight, C = act(LN(a)·Wᵀ + bias)
-    from the raw rows of ``a`` (bf16, no K split; ``bias`` is inside b2)."""
+    from the raw rows of ``a`` (no K split; ``bias`` is inside b2); ``ln_stats`` (f32 [M, 2]):
+    receives each raw row's (mean, rstd). ``resid_ln = (stats, gamma, beta)``: ``resid`` holds raw
+    rows whose LayerNorm was deferred; (r − mean)·rstd·γ + β is added instead of r."""
     M, K = a.shape
     N = b.shape[0]
     half = a.dtype
     if out is None:
         out = torch.empty((M, N), dtype=torch.float32 if out_f32 else half, device=a.device)
     mb, nb, wn, depth, ks = cfg or small_cfg(M, N, K)
-    if ln is not None:
-        ks = 1
-        return _small_gemm_ln(a, b, out, M, N, K, (mb, nb, wn, depth), act, resid, ln)
+    if ln is not None or resid_ln is not None:
+        if ln is not None:
+            ks = 1
+        return _small_gemm_ln(a, b, out, M, N, K, (mb, nb, wn, depth, ks), act, resid, ln, ln_stats,
+                              resid_ln, bias, alpha)
     ws = cnt = None
     if ks > 1:
         if slices:
@@ -272,17 +276,36 @@ def ln_fold(w_nk, gamma, beta, bias=None):
     return wf, c1, b2.contiguous()
 
 
-def _small_gemm_ln(a, b, out, M, N, K, cfg, act, resid, ln):
-    c1, b2, eps = ln
-    assert a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16, "LayerNorm fold: bf16 operands"
-    assert c1.dtype == torch.float32 and b2.dtype == torch.float32 and c1.numel() == N == b2.numel()
-    mb, nb, wn, depth = cfg
-    depth &= 15  # the LN-fold kernels keep one ring depth for both operands
-    _lib.call("piamd_small_gemm_ln", 0, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
-              out.data_ptr(), out.stride(0), int(out.dtype == torch.float32), M, N, K, mb, nb, wn,
-              depth, 1, 1.0, None, ACTS[act], _lib.ptr(resid),
-              resid.stride(0) if resid is not None else 0, None, None, c1.data_ptr(), b2.data_ptr(),
-              float(eps), _lib.stream())
+def _small_gemm_ln(a, b, out, M, N, K, cfg, act, resid, ln, ln_stats=None, resid_ln=None, bias=None,
+                   alpha=1.0):
+    assert a.dtype == b.dtype and a.dtype in _HALF, "LayerNorm fold: bf16 / fp16 operands of one dtype"
+    mb, nb, wn, depth, ks = cfg
+    c1 = b2 = None
+    eps = 0.0
+    if ln is not None:
+        c1, b2, eps = ln
+        assert c1.dtype == torch.float32 and b2.dtype == torch.float32 and c1.numel() == N == b2.numel()
+        if not (depth >> 4 == 4 and wn == 1):  # LN-fold kernels: one ring depth, or a 4-deep B ring
+            depth &= 15
+        ks, bias, alpha = 1, None, 1.0
+    if ln_stats is not None:
+        assert ln is not None and ln_stats.dtype == torch.float32 and ln_stats.numel() >= 2 * M
+    rs = rg = rb = None
+    if resid_ln is not None:
+        rs, rg, rb = resid_ln
+        assert resid is not None and rs.dtype == torch.float32 and rs.numel() >= 2 * M
+        assert rg.dtype == a.dtype and rb.dtype == a.dtype and rg.numel() == N == rb.numel()
+        rg, rb = rg.contiguous(), rb.contiguous()
+    ws = cnt = None
+    if ks > 1:
+        tiles = -(-M // (16 * mb)) * -(-N // (16 * nb * wn))
+        ws, cnt = _sg_fixup_bufs(a.device, M, N, tiles)
+    _lib.call("piamd_small_gemm_ln", int(a.dtype == torch.float16), a.data_ptr(), a.stride(0),
+              b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0), int(out.dtype == torch.float32),
+              M, N, K, mb, nb, wn, depth, ks, float(alpha), _lib.ptr(bias), ACTS[act], _lib.ptr(resid),
+              resid.stride(0) if resid is not None else 0, _lib.ptr(ws), _lib.ptr(cnt), _lib.ptr(c1),
+              _lib.ptr(b2), float(eps), _lib.ptr(ln_stats), _lib.ptr(rs), _lib.ptr(rg), _lib.ptr(rb),
+              _lib.stream())
     return out
 
 

@@ -383,6 +383,9 @@ def _swce(ins, a):
 
 
 # ---------------------------------------------------------------- fused (IR-pass targets)
+from ..inference import ln_defer as _ln_defer  # noqa: E402
+
+
 @register("fc")
 def _fc(ins, a):
     """Reference `fc_op.cc`: Out = act(Input @ W + Bias) (in_num_col_dims flattening)."""
@@ -391,8 +394,14 @@ def _fc(ins, a):
     x, w = ins["Input"][0], ins["W"][0]
     b = ins["Bias"][0] if ins.get("Bias") else None
     nc = a.get("in_num_col_dims", x.dim() - 1)
-    x2 = x.reshape(int(np.prod(x.shape[:nc])), -1)
     act = a.get("activation_type", "")
+    if _ln_defer.of(x) is not None:  # raw rows of a post-LN producer: LayerNorm folded in here
+        y = (_ln_defer.linear(x, w, b, act or "none") if nc == x.dim() - 1
+             and act in ("", "gelu", "relu", "gelu_tanh") else None)
+        if y is not None:
+            return {"Out": y}
+        x = _ln_defer.materialize(x)
+    x2 = x.reshape(int(np.prod(x.shape[:nc])), -1)
     if act in ("gelu", "relu", "silu", "gelu_tanh") and x2.is_cuda and x2.dtype in (torch.bfloat16,
                                                                                     torch.float16):
         from ..ops.linear import linear_bias_act
@@ -673,8 +682,14 @@ def _multihead_matmul(ins, a):
     B, S, E = x.shape
     H = int(a["head_number"])
     D = E // H
-    qkv = linear(x.reshape(B * S, E), _cached_view(w, (E, 3 * E)),
-                 bias.reshape(3 * E)).reshape(B, S, 3, H, D)
+    qkv = None
+    if _ln_defer.of(x) is not None:  # QKV GEMM on the raw rows with the producer's LayerNorm folded
+        qkv = _ln_defer.linear(x, _cached_view(w, (E, 3 * E)), bias.reshape(3 * E))
+        if qkv is None:
+            x = _ln_defer.materialize(x)
+    if qkv is None:
+        qkv = linear(x.reshape(B * S, E), _cached_view(w, (E, 3 * E)), bias.reshape(3 * E))
+    qkv = qkv.reshape(B, S, 3, H, D)
     qkv = qkv.reshape(B, S, 3 * H, D)
     mask = ins["BiasQK"][0] if ins.get("BiasQK") else None
     scale = float(a.get("alpha", 1.0 / D ** 0.5))
@@ -686,16 +701,44 @@ def _multihead_matmul(ins, a):
     return {"Out": o.reshape(B, S, E)}
 
 
+def _fc_resid_deferred(x2, w, b0, y, ins, a):
+    """(fc(x2) + b0 + y as ONE skinny GEMM with y's own deferred LayerNorm applied in the epilogue,
+    γ, β) — the output's LayerNorm is then deferred to its consumers; None when this call does
+    not qualify."""
+    from ..ops.gemm import small_gemm, use_small
+    from ..ops.linear import transposed
+    g, be = (ins["Scale"][0] if ins.get("Scale") else None), (ins["Bias1"][0] if ins.get("Bias1") else None)
+    if g is None or be is None or w.dim() != 2 or x2.dtype != w.dtype or not x2.is_contiguous():
+        return None
+    M, K = x2.shape
+    N = w.shape[1]
+    if (not _ln_defer.can_defer(x2, M, N) or not use_small(M, N, K)
+            or K % 64 or N % 4 or y.numel() != M * N):
+        return None
+    r, rln = _ln_defer.resid_args(y, M)
+    r2 = r.reshape(M, N)
+    if r2.dtype != x2.dtype or not r2.is_contiguous():
+        return None
+    b0 = _ln_defer._as(b0.reshape(-1), x2.dtype) if b0 is not None else None  # f32 under mixed precision
+    return small_gemm(x2, transposed(w), bias=b0, resid=r2, resid_ln=rln), g, be
+
+
 @register("fused_fc_elementwise_layernorm")
 def _fc_eltwise_ln(ins, a):
     """Reference `fused/fused_fc_elementwise_layernorm_op.cu`:
     Out = LN(fc(X, W, Bias0) + Y; Scale, Bias1), fc flattening at x_num_col_dims."""
     from .. import ops
     from ..ops.linear import linear
-    x, w, y = ins["X"][0], ins["W"][0], ins["Y"][0]
+    x, w, y = _ln_defer.materialize(ins["X"][0]), ins["W"][0], ins["Y"][0]
     b0 = ins["Bias0"][0] if ins.get("Bias0") else None
     nc = int(a.get("x_num_col_dims", x.dim() - 1))
     x2 = x.reshape(int(np.prod(x.shape[:nc])), -1)
+    if a.get("defer_ln") and a.get("activation_type") in ("", None):
+        r = _fc_resid_deferred(x2, w, b0, y, ins, a)
+        if r is not None:  # raw fc + residual; the LayerNorm rides in the consumers (ln_defer)
+            h = r[0].reshape(*x.shape[:nc], -1)
+            return {"Out": _ln_defer.defer(h, r[1], r[2], float(a.get("epsilon", 1e-5)))}
+    y = _ln_defer.materialize(y)
     h = linear(x2, w, b0).reshape(*x.shape[:nc], -1)
     if a.get("activation_type") == "relu":
         h = F.relu(h)

@@ -341,6 +341,10 @@ void sg_launch(const SgArgs& p, int ks, int depth, int* cnt, hipStream_t st) {
         hipLaunchKernelGGL((small_gemm_kernel<F16, MB, NB, 1, 1, true, 4>), grid, dim3(256), 0, st, p, cnt);
         return;
       }
+      if ((depth >> 4) == 2) {  // 2 deep (serving-batch decode, M = 32)
+        hipLaunchKernelGGL((small_gemm_kernel<F16, MB, NB, 1, 1, true, 2>), grid, dim3(256), 0, st, p, cnt);
+        return;
+      }
     }
     if ((depth & 15) >= 2)
       hipLaunchKernelGGL((small_gemm_kernel<F16, MB, NB, WN, 2, true>), grid, dim3(256), 0, st, p, cnt);
@@ -415,9 +419,9 @@ PIAMD_EXPORT int piamd_small_gemm_ln(int f16, const void* a, long long lda, cons
       (ln_stats && !ln_c1))
     return (int)hipErrorInvalidValue;
   if (rln_stats && (!resid || !rln_g || !rln_b)) return (int)hipErrorInvalidValue;
-  {  // depth: A depth 1 | 2, optionally | (B depth 2 / 4 / 8) << 4 with A depth 1, wn 1 (LN fold: 4)
+  {  // depth: A depth 1 | 2, optionally | (B depth 2 / 4 / 8) << 4 with A depth 1, wn 1 (LN fold: 2 / 4)
     const int da = depth & 15, db = depth >> 4;
-    if (da < 1 || da > 2 || (db && (da != 1 || wn != 1 || (ln_c1 && db != 4) || (db != 2 && db != 4 && db != 8))))
+    if (da < 1 || da > 2 || (db && (da != 1 || wn != 1 || (ln_c1 && db != 2 && db != 4) || (db != 2 && db != 4 && db != 8))))
       return (int)hipErrorInvalidValue;
   }
   SgArgs p{(const bf16_t*)a, lda, (const bf16_t*)b, ldb, c, ldc, ws, (const bf16_t*)bias,

@@ -814,8 +814,43 @@ int launch_bwd(const void* dy, const void* h, const void* gamma, const float* me
   return (int)hipGetLastError();
 }
 
+// Many partial rows (G ≥ 64: the rowsum / dact-epilogue column-sum planes, 256-768 rows): 32
+// columns per workgroup as 8 float4 lanes × 32 row groups, so each thread sums G / 32 rows (the
+// 4-row-group kernel left ~N/64 workgroups each walking G / 4 rows serially: latency-bound,
+// ≈ 17 µs per bias gradient in the GPT step). Fixed summation order: deterministic.
+template <int DT>
+__global__ __launch_bounds__(256) void col_sum4_kernel(const float* __restrict__ part, int G, int N,
+                                                      typename IO<DT>::T* __restrict__ out,
+                                                      int accumulate) {
+  const int q = threadIdx.x & 7, rg = threadIdx.x >> 3;
+  const int col = blockIdx.x * 32 + 4 * q;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (col < N) {
+#pragma unroll 4
+    for (int g = rg; g < G; g += 32) s += *reinterpret_cast<const f32x4*>(part + (size_t)g * N + col);
+  }
+  __shared__ f32x4 red[32][9];
+  red[rg][q] = s;
+  __syncthreads();
+  if (threadIdx.x < 32) {  // thread (qq, j): column 4·qq + j of the block
+    const int qq = threadIdx.x >> 2, j = threadIdx.x & 3, c = blockIdx.x * 32 + threadIdx.x;
+    if (c < N) {
+      float t = 0.f;
+#pragma unroll 8
+      for (int r = 0; r < 32; ++r) t += red[r][qq][j];
+      if (accumulate) t += IO<DT>::load1(out + c);
+      IO<DT>::store1(out + c, t);
+    }
+  }
+}
+
 template <int DT>
 void launch_colsum_out(const float* part, int G, int N, void* out, int acc, hipStream_t st) {
+  if (G >= 64 && N % 4 == 0 && ((uintptr_t)part & 15) == 0) {
+    hipLaunchKernelGGL((col_sum4_kernel<DT>), dim3((N + 31) / 32), dim3(256), 0, st, part, G, N,
+                       (typename IO<DT>::T*)out, acc);
+    return;
+  }
   hipLaunchKernelGGL((col_sum_kernel<DT>), dim3((N + 63) / 64), dim3(256), 0, st, part, G, N,
                      (typename IO<DT>::T*)out, acc);
 }

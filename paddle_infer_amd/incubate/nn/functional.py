@@ -268,10 +268,10 @@ class _Linear:
     def ln_fold_ok(self, M, act="none"):
         """A pre-LN call with M rows runs as ONE skinny GEMM on the LayerNorm-folded weight
         (``ops.gemm.ln_fold``: row statistics gathered from the raw rows inside the GEMM, no
-        LayerNorm launch) — serving batches (M ≥ DENSE_MIN_M) on the dense path, bf16."""
+        LayerNorm launch) — serving batches (M ≥ DENSE_MIN_M) on the dense path, bf16 / fp16."""
         from ...ops.gemm import use_small
         K, N = self._kn()
-        return (not self.bits and self.packed is not None and self.w.dtype == torch.bfloat16
+        return (not self.bits and self.packed is not None and self.w.dtype in (torch.bfloat16, torch.float16)
                 and M >= self.DENSE_MIN_M and not self._packed_for(M, K) and K % 64 == 0
                 and N % 4 == 0 and use_small(M, N, K) and act in ("none", "gelu", "gelu_tanh", "relu"))
 

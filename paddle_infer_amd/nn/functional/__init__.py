@@ -447,11 +447,30 @@ def batch_norm(x, running_mean, running_var, weight=None, bias=None, training=Fa
 
 def instance_norm(x, running_mean=None, running_var=None, weight=None, bias=None,
                   use_input_stats=True, momentum=0.9, eps=1e-5, data_format="NCHW", name=None):
+    """Own GroupNorm kernels with one channel per group (`ops/groupnorm.py`); the running-statistics
+    update of a training call with running buffers stays on ATen (recorded)."""
+    if x.is_cuda:
+        from ...ops import groupnorm as _gn
+        C = x.shape[1] if x.dim() >= 2 else 0
+        if use_input_stats and running_mean is None and running_var is None and _gn.supported(x, max(C, 1)):
+            return _gn.group_norm(x, C, weight, bias, eps)
+        if (not use_input_stats and running_mean is not None and running_var is not None
+                and _gn.supported(x, max(C, 1)) and not (torch.is_grad_enabled() and (
+                    x.requires_grad or any(t is not None and t.requires_grad for t in (weight, bias))))):
+            return _gn.instance_norm_eval(x, running_mean, running_var, weight, bias, eps)
+        _lib_fallback(x, "instance_norm", "running-statistics update / eval under autograd (ATen)")
     return TF.instance_norm(x, running_mean, running_var, weight, bias, use_input_stats, 1 - momentum, eps)
 
 
 def group_norm(x, num_groups, epsilon=1e-5, weight=None, bias=None, data_format="NCHW", name=None):
-    return _fmt_out(TF.group_norm(_fmt_in(x, data_format), num_groups, weight, bias, epsilon), data_format)
+    """Own HIP kernels (`ops/groupnorm.py`, plane reductions + Chan merge, deterministic backward)."""
+    xin = _fmt_in(x, data_format)
+    if x.is_cuda:
+        from ...ops import groupnorm as _gn
+        if _gn.supported(xin, num_groups):
+            return _fmt_out(_gn.group_norm(xin, num_groups, weight, bias, epsilon), data_format)
+        _lib_fallback(x, "group_norm", "non-float dtype / channels not divisible by groups (ATen)")
+    return _fmt_out(TF.group_norm(xin, num_groups, weight, bias, epsilon), data_format)
 
 
 def local_response_norm(x, size, alpha=1e-4, beta=0.75, k=1.0, data_format="NCHW", name=None):

@@ -75,7 +75,8 @@ _SIGS = {
 }
 
 
-_RESTYPES = {"piamd_layernorm_bwd_ws": ctypes.c_longlong, "piamd_dconv2d_wgrad_parts": ctypes.c_longlong}
+_RESTYPES = {"piamd_layernorm_bwd_ws": ctypes.c_longlong, "piamd_dconv2d_wgrad_parts": ctypes.c_longlong,
+             "piamd_group_norm_ws": ctypes.c_longlong}
 
 
 class FaArgs(ctypes.Structure):
@@ -299,6 +300,12 @@ _SIGS["piamd_maxpool_bwd_nhwc"] = [c_void_p] * 3 + [c_int] * 13 + [c_void_p]
 _SIGS["piamd_pool_nd_fwd"] = ([c_int] + [c_void_p] * 3 + [c_int] * 2 + [ctypes.POINTER(c_int)] * 5
                               + [c_int] * 4 + [c_void_p])
 _SIGS["piamd_pool_nd_bwd"] = _SIGS["piamd_pool_nd_fwd"]
+# groupnorm.hip: fwd (dtype, x, y, gamma, beta, mean, rstd, ws, N, C, HW, G, eps, stream),
+# bwd (dtype, dy, x, gamma, mean, rstd, dx, dgamma, dbeta, ws, N, C, HW, G, stream)
+_SIGS["piamd_group_norm_ws"] = [c_int, c_int, c_int]
+_SIGS["piamd_group_norm_fwd"] = [c_int] + [c_void_p] * 7 + [c_int, c_int, c_ll, c_int, c_float, c_void_p]
+_SIGS["piamd_group_norm_bwd"] = [c_int] + [c_void_p] * 9 + [c_int, c_int, c_ll, c_int, c_void_p]
+_SIGS["piamd_group_norm_apply"] = [c_int] + [c_void_p] * 6 + [c_int, c_int, c_ll, c_int, c_void_p]
 # dtype, x|dy, y|dx(f32), N, C, I[3], O[3], scale[3], mode, align_corners, stream
 _SIGS["piamd_interp_fwd"] = ([c_int] + [c_void_p] * 2 + [c_int] * 2 + [ctypes.POINTER(c_int)] * 2
                              + [ctypes.POINTER(c_float), c_int, c_int, c_void_p])

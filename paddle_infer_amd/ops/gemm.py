@@ -174,6 +174,13 @@ _SG_TUNED: dict = {
     (128, 4096, 1024): (2, 4, 1, 0x41, 1), (128, 1024, 4096): (2, 1, 1, 0x81, 1),
     (128, 6144, 2048): (4, 4, 1, 2, 1), (128, 2048, 2048): (2, 2, 1, 1, 1),
     (128, 8192, 2048): (4, 4, 1, 2, 1),
+    # GPT-1.3B serving-batch decode (bf16, graph-timed sweep incl. the B-deep rings;
+    # profiles/small_gemm_decode_r6.jsonl): QKV / FFN1 (LN-folded), out-proj, FFN2 (K = 8192, split-K)
+    (8, 6144, 2048): (1, 2, 1, 2, 1), (8, 8192, 2048): (1, 1, 1, 2, 1),
+    (8, 2048, 2048): (1, 1, 1, 0x81, 1), (8, 2048, 8192): (1, 2, 1, 2, 4),
+    (16, 2048, 2048): (1, 1, 1, 0x81, 1), (16, 2048, 8192): (1, 2, 1, 2, 4),
+    (32, 6144, 2048): (2, 2, 1, 0x21, 1), (32, 8192, 2048): (2, 2, 1, 0x21, 1),
+    (32, 2048, 2048): (1, 1, 1, 0x81, 1), (32, 2048, 8192): (2, 2, 1, 1, 4),
     (256, 3072, 1024): (4, 4, 1, 1, 1), (256, 1024, 4096): (2, 2, 1, 2, 1),
     (256, 2048, 2048): (4, 2, 1, 1, 1), (512, 2048, 2048): (4, 4, 1, 1, 1),
 }
@@ -285,7 +292,7 @@ def _small_gemm_ln(a, b, out, M, N, K, cfg, act, resid, ln, ln_stats=None, resid
     if ln is not None:
         c1, b2, eps = ln
         assert c1.dtype == torch.float32 and b2.dtype == torch.float32 and c1.numel() == N == b2.numel()
-        if not (depth >> 4 == 4 and wn == 1):  # LN-fold kernels: one ring depth, or a 4-deep B ring
+        if not (depth >> 4 in (2, 4) and depth & 15 == 1 and wn == 1):  # LN fold: one ring depth, or B 2 / 4 deep
             depth &= 15
         ks, bias, alpha = 1, None, 1.0
     if ln_stats is not None:

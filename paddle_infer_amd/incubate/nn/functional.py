@@ -240,7 +240,9 @@ class _Linear:
     # serving batches with short K: the skinny MFMA GEMM on the K-contiguous weight beats the packed
     # weight stream from 8 rows (M=32 QKV 14.7 -> 11.5 us, out-proj 8.8 -> 6.5; K = 8192 stays on
     # the packed GEMV: profiles/decode_linear_r5.txt)
-    DENSE_MIN_M, DENSE_MAX_K = 8, int(os.environ.get("PIAMD_DENSE_MAX_K", "2048"))
+    # the skinny GEMM takes every serving-batch projection incl. FFN2 (K = 8192, tuned split-K config):
+    # batch 8 1.368 -> 1.312 ms/step vs the packed GEMV at K = 8192, batch 32 equal (profiles/decode_r6.txt)
+    DENSE_MIN_M, DENSE_MAX_K = 8, int(os.environ.get("PIAMD_DENSE_MAX_K", "8192"))
 
     def _packed_for(self, M, K):
         return (self.packed is not None and M <= self.PACKED_MAX_M

@@ -25,7 +25,9 @@ import os
 
 import torch
 
-DEFER_MAX_M = int(os.environ.get("PIAMD_LN_DEFER_MAX_M", "128"))
+# rows up to which producers defer (BERT-Large fp16: batch 2 (256 rows) 1.957 -> 1.787 ms deferred;
+# batch 4 (512 rows) 2.501 -> 2.789 ms, so 512 stays on the LayerNorm kernel; profiles/bert_fp16_r6.txt)
+DEFER_MAX_M = int(os.environ.get("PIAMD_LN_DEFER_MAX_M", "256"))
 ENABLED = os.environ.get("PIAMD_LN_DEFER", "1") != "0"
 
 

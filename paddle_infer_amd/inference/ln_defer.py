@@ -2,8 +2,8 @@
 
 A post-LN layer ends every sub-block with ``y = LN(fc(x) + resid)``
 (`fused_fc_elementwise_layernorm`, reference `fused/fused_fc_elementwise_layernorm_op.cu:64`) and
-``y`` feeds exactly two places: the next GEMM (QKV / FFN1) and the next residual add. At ≤ 128 rows
-the LayerNorm is its own launch (~5.4 µs, 17 % of BERT-Large batch 1). Here the producer skips it
+``y`` feeds exactly two places: the next GEMM (QKV / FFN1) and the next residual add. At a few
+hundred rows the LayerNorm is its own launch (~5.4 µs, 17 % of BERT-Large batch 1). Here the producer skips it
 and hands on the RAW rows ``h`` with the LayerNorm attached (:class:`Deferred`):
 
 * the consuming GEMM folds the LayerNorm into its weights (``ops.gemm.ln_fold``: W∘γ, Σ_k, bias +

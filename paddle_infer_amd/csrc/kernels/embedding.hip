@@ -5,7 +5,8 @@
 // [start, start + V_local) produce zero rows) and the GPT embedding (word + learned position).
 //
 // Forward fuses the two gathers and the add: out[t] = W[id_t - start] + P[pos_t], 16-B vector
-// loads / stores (H % 8 == 0), grid-stride.
+// loads / stores (H % 8 == 0), grid-stride; bf16 (the training path) or, through the *_dt entry
+// points, f32 / fp16 tables (paddle.nn.functional.embedding; padding ids arrive as −1 = zero row).
 //
 // Backward is sort-based and atomic-free (deterministic, f32 accumulation — repeated tokens are
 // summed in registers, not by bf16 atomics that would round at every add): the host side sorts
@@ -18,10 +19,43 @@
 
 namespace {
 
-__global__ void emb_fwd_kernel(const long long* __restrict__ ids, const bf16_t* __restrict__ w,
-                               long long start, int vlocal, const bf16_t* __restrict__ p,
+// 8 consecutive elements of dtype DT (0 f32, 1 bf16, 2 fp16) ↔ f32 registers
+template <int DT>
+__device__ __forceinline__ void ld8(const void* base, long long idx, float (&v)[8]) {
+  if constexpr (DT == 0) {
+    const f32x4* q = reinterpret_cast<const f32x4*>((const float*)base + idx);
+    const f32x4 a = q[0], b = q[1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = b[j]; }
+  } else {
+    const u16x8 u = *reinterpret_cast<const u16x8*>((const unsigned short*)base + idx);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = DT == 1 ? bf2f(u[j]) : h2f<true>(u[j]);
+  }
+}
+
+template <int DT>
+__device__ __forceinline__ void st8(void* base, long long idx, const float (&v)[8]) {
+  if constexpr (DT == 0) {
+    f32x4 a, b;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { a[j] = v[j]; b[j] = v[4 + j]; }
+    f32x4* q = reinterpret_cast<f32x4*>((float*)base + idx);
+    q[0] = a;
+    q[1] = b;
+  } else {
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = DT == 1 ? f2bf(v[j]) : f2h<true>(v[j]);
+    *reinterpret_cast<u16x8*>((unsigned short*)base + idx) = o;
+  }
+}
+
+template <int DT>
+__global__ void emb_fwd_kernel(const long long* __restrict__ ids, const void* __restrict__ w,
+                               long long start, int vlocal, const void* __restrict__ p,
                                const long long* __restrict__ pos, int S,
-                               bf16_t* __restrict__ out, long long T, int H) {
+                               void* __restrict__ out, long long T, int H) {
   const int hv = H / 8;
   const long long total = T * hv;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
@@ -31,31 +65,27 @@ __global__ void emb_fwd_kernel(const long long* __restrict__ ids, const bf16_t* 
     const long long id = ids[t] - start;
     float v[8];
     if (id >= 0 && id < vlocal) {
-      const u16x8 a = *reinterpret_cast<const u16x8*>(w + id * H + c);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = bf2f(a[j]);
+      ld8<DT>(w, id * H + c, v);
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = 0.f;
     }
     if (p) {
       const long long ps = pos ? pos[t] : t % S;
-      const u16x8 b = *reinterpret_cast<const u16x8*>(p + ps * H + c);
+      float b[8];
+      ld8<DT>(p, ps * H + c, b);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += bf2f(b[j]);
+      for (int j = 0; j < 8; ++j) v[j] += b[j];
     }
-    u16x8 o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
-    *reinterpret_cast<u16x8*>(out + t * H + c) = o;
+    st8<DT>(out, t * H + c, v);
   }
 }
 
 // one block (256 threads) per sorted position; columns in chunks of 256 x 8
-template <bool F32OUT>
+template <bool F32OUT, int DT = 1>
 __global__ __launch_bounds__(256) void emb_bwd_kernel(const long long* __restrict__ sorted,
                                                       const long long* __restrict__ order,
-                                                      const bf16_t* __restrict__ dy,
+                                                      const void* __restrict__ dy,
                                                       void* __restrict__ dw, long long start,
                                                       int vlocal, long long T, int H,
                                                       int accumulate) {
@@ -71,9 +101,10 @@ __global__ __launch_bounds__(256) void emb_bwd_kernel(const long long* __restric
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
     for (long long s = i; s < end; ++s) {
-      const u16x8 g = *reinterpret_cast<const u16x8*>(dy + order[s] * H + c);
+      float g[8];
+      ld8<DT>(dy, order[s] * H + c, g);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += bf2f(g[j]);
+      for (int j = 0; j < 8; ++j) acc[j] += g[j];
     }
     if (F32OUT) {
       float* d = (float*)dw + row * H + c;
@@ -127,8 +158,42 @@ PIAMD_EXPORT int piamd_embedding_fwd(const long long* ids, const void* w, long l
                                      void* out, long long T, int H, hipStream_t st) {
   if (H % 8 || T < 0 || (p && !pos && S < 1)) return (int)hipErrorInvalidValue;
   if (T == 0) return 0;
-  hipLaunchKernelGGL(emb_fwd_kernel, dim3(stride_grid(T * (H / 8), 256)), dim3(256), 0, st, ids,
-                     (const bf16_t*)w, start, vlocal, (const bf16_t*)p, pos, S, (bf16_t*)out, T, H);
+  hipLaunchKernelGGL(emb_fwd_kernel<1>, dim3(stride_grid(T * (H / 8), 256)), dim3(256), 0, st, ids, w,
+                     start, vlocal, p, pos, S, out, T, H);
+  return (int)hipGetLastError();
+}
+
+// Any element type (dtype 0 f32, 1 bf16, 2 fp16: weight, position table and output alike).
+PIAMD_EXPORT int piamd_embedding_fwd_dt(int dtype, const long long* ids, const void* w, long long start,
+                                        int vlocal, const void* p, const long long* pos, int S,
+                                        void* out, long long T, int H, hipStream_t st) {
+  if (H % 8 || T < 0 || (p && !pos && S < 1) || dtype < 0 || dtype > 2) return (int)hipErrorInvalidValue;
+  if (T == 0) return 0;
+  const dim3 grid(stride_grid(T * (H / 8), 256));
+  if (dtype == 0)
+    hipLaunchKernelGGL(emb_fwd_kernel<0>, grid, dim3(256), 0, st, ids, w, start, vlocal, p, pos, S, out, T, H);
+  else if (dtype == 2)
+    hipLaunchKernelGGL(emb_fwd_kernel<2>, grid, dim3(256), 0, st, ids, w, start, vlocal, p, pos, S, out, T, H);
+  else
+    hipLaunchKernelGGL(emb_fwd_kernel<1>, grid, dim3(256), 0, st, ids, w, start, vlocal, p, pos, S, out, T, H);
+  return (int)hipGetLastError();
+}
+
+// dW (f32) (+)= Σ dy rows per id for a dy of any element type (dtype as above).
+PIAMD_EXPORT int piamd_embedding_bwd_dt(int dtype, const long long* sorted, const long long* order,
+                                        const void* dy, float* dw, long long start, int vlocal, long long T,
+                                        int H, int accumulate, hipStream_t st) {
+  if (H % 8 || T < 0 || dtype < 0 || dtype > 2) return (int)hipErrorInvalidValue;
+  if (T == 0) return 0;
+  if (dtype == 0)
+    hipLaunchKernelGGL((emb_bwd_kernel<true, 0>), dim3(T), dim3(256), 0, st, sorted, order, dy, dw, start,
+                       vlocal, T, H, accumulate);
+  else if (dtype == 2)
+    hipLaunchKernelGGL((emb_bwd_kernel<true, 2>), dim3(T), dim3(256), 0, st, sorted, order, dy, dw, start,
+                       vlocal, T, H, accumulate);
+  else
+    hipLaunchKernelGGL((emb_bwd_kernel<true, 1>), dim3(T), dim3(256), 0, st, sorted, order, dy, dw, start,
+                       vlocal, T, H, accumulate);
   return (int)hipGetLastError();
 }
 
@@ -141,11 +206,11 @@ PIAMD_EXPORT int piamd_embedding_bwd(const long long* sorted, const long long* o
   if (H % 8 || T < 0) return (int)hipErrorInvalidValue;
   if (T == 0) return 0;
   if (dw_f32)
-    hipLaunchKernelGGL(emb_bwd_kernel<true>, dim3(T), dim3(256), 0, st, sorted, order,
-                       (const bf16_t*)dy, dw, start, vlocal, T, H, accumulate);
+    hipLaunchKernelGGL((emb_bwd_kernel<true, 1>), dim3(T), dim3(256), 0, st, sorted, order, dy, dw, start,
+                       vlocal, T, H, accumulate);
   else
-    hipLaunchKernelGGL(emb_bwd_kernel<false>, dim3(T), dim3(256), 0, st, sorted, order,
-                       (const bf16_t*)dy, dw, start, vlocal, T, H, accumulate);
+    hipLaunchKernelGGL((emb_bwd_kernel<false, 1>), dim3(T), dim3(256), 0, st, sorted, order, dy, dw, start,
+                       vlocal, T, H, accumulate);
   return (int)hipGetLastError();
 }
 

@@ -103,7 +103,15 @@ def alpha_dropout(x, p=0.5, training=True, name=None):
 
 
 def embedding(x, weight, padding_idx=None, sparse=False, name=None):
-    return TF.embedding(x, weight, padding_idx)
+    """Reference `phi/kernels/gpu/embedding_kernel.cu`: padding_idx rows are zero in the output and
+    get no gradient; the own HIP gather / sort-based gradient kernels (`ops/embedding.py lookup`)."""
+    if weight.is_cuda:
+        from ...ops.embedding import lookup
+        return lookup(x, weight, padding_idx)
+    if padding_idx is None:
+        return TF.embedding(x, weight)
+    pad = padding_idx + weight.shape[0] if padding_idx < 0 else padding_idx
+    return TF.embedding(x, weight, pad) * (x != pad).unsqueeze(-1).to(weight.dtype)
 
 
 def one_hot(x, num_classes, name=None):

@@ -306,6 +306,12 @@ _SIGS["piamd_group_norm_ws"] = [c_int, c_int, c_int]
 _SIGS["piamd_group_norm_fwd"] = [c_int] + [c_void_p] * 7 + [c_int, c_int, c_ll, c_int, c_float, c_void_p]
 _SIGS["piamd_group_norm_bwd"] = [c_int] + [c_void_p] * 9 + [c_int, c_int, c_ll, c_int, c_void_p]
 _SIGS["piamd_group_norm_apply"] = [c_int] + [c_void_p] * 6 + [c_int, c_int, c_ll, c_int, c_void_p]
+# embedding.hip, any dtype: fwd (dtype, ids, w, start, vlocal, p, pos, S, out, T, H, stream),
+# bwd (dtype, sorted, order, dy, dw_f32, start, vlocal, T, H, accumulate, stream)
+_SIGS["piamd_embedding_fwd_dt"] = [c_int, c_void_p, c_void_p, c_ll, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                                   c_ll, c_int, c_void_p]
+_SIGS["piamd_embedding_bwd_dt"] = [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_ll, c_int, c_ll, c_int,
+                                   c_int, c_void_p]
 # dtype, x|dy, y|dx(f32), N, C, I[3], O[3], scale[3], mode, align_corners, stream
 _SIGS["piamd_interp_fwd"] = ([c_int] + [c_void_p] * 2 + [c_int] * 2 + [ctypes.POINTER(c_int)] * 2
                              + [ctypes.POINTER(c_float), c_int, c_int, c_void_p])

@@ -98,3 +98,63 @@ def embedding(ids, weight, vocab_start=0, pos_table=None, pos_ids=None):
             (pos_table is not None and pos_table.dtype != weight.dtype):
         return _ref(ids, weight, vocab_start, pos_table, pos_ids)
     return _Embedding.apply(ids, weight, pos_table, pos_ids, int(vocab_start))
+
+
+_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+
+class _Lookup(torch.autograd.Function):
+    """Plain table lookup of any float dtype (``paddle.nn.functional.embedding``); padding ids
+    arrive remapped to −1, which the kernels treat as out of range: a zero output row and no
+    gradient (reference `embedding_kernel.cu` PaddingFlag / `embedding_grad_kernel.cu`)."""
+
+    @staticmethod
+    def forward(ctx, ids, w):
+        shp = ids.shape
+        H = w.shape[1]
+        idf = ids.reshape(-1).contiguous()
+        T = idf.numel()
+        out = torch.empty((T, H), dtype=w.dtype, device=w.device)
+        _lib.call("piamd_embedding_fwd_dt", _DT[w.dtype], idf.data_ptr(), w.data_ptr(), 0, w.shape[0],
+                  None, None, 1, out.data_ptr(), T, H, _lib.stream())
+        ctx.save_for_backward(idf)
+        ctx.w = w
+        return out.view(*shp, H)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idf,) = ctx.saved_tensors
+        w = ctx.w
+        if not ctx.needs_input_grad[1]:
+            return None, None
+        H = w.shape[1]
+        dy = dy.reshape(-1, H).contiguous().to(w.dtype)
+        sorted_ids, order = torch.sort(idf)
+        tgt, engine = _grad_target(w, w.dtype)
+        _lib.call("piamd_embedding_bwd_dt", _DT[w.dtype], sorted_ids.data_ptr(), order.data_ptr(), dy.data_ptr(),
+                  tgt.data_ptr(), 0, w.shape[0], idf.numel(), H, 1, _lib.stream())
+        if engine:
+            _lib.fire(w)
+            return None, None
+        return None, tgt.to(w.dtype)
+
+
+def lookup(ids, weight, padding_idx=None):
+    """out[..., :] = weight[ids] with Paddle's padding semantics (rows of ``padding_idx`` are zero
+    and get no gradient); the own kernels for CUDA f32 / bf16 / fp16 tables with H % 8 == 0."""
+    V = weight.shape[0]
+    pad = padding_idx  # Paddle: negative = counted from the end of the table
+    if pad is not None and pad < 0:
+        pad = pad + V
+    ids = ids.long()
+    if weight.is_cuda and weight.dtype in _DT and weight.dim() == 2 and weight.shape[1] % 8 == 0 \
+            and weight.is_contiguous() and _lib.available():
+        if pad is not None:
+            ids = ids.masked_fill(ids == pad, -1)
+        return _Lookup.apply(ids, weight)
+    if weight.is_cuda:
+        _lib.fallback("embedding", "table width % 8 != 0 / non-contiguous / non-float table (ATen)")
+    out = F.embedding(ids, weight, pad)
+    if pad is not None:
+        out = out * (ids != pad).unsqueeze(-1).to(out.dtype)
+    return out

@@ -207,7 +207,7 @@ class GPTGenerator:
         mega = self._mega_decoder(B)
         if decode_strategy == "greedy_search" and mega is not None and mega.head_ok:
             return self._greedy_mega_loop(mega, logits, pos, out, done, max_new_tokens, eos_token_id,
-                                          pad_token_id)
+                                          pad_token_id, ctx0=S)
         if decode_strategy == "greedy_search" and self.use_graph and mega is None:
             return self._greedy_graph_loop(logits, pos, out, done, max_new_tokens, eos_token_id,
                                            pad_token_id)
@@ -227,7 +227,7 @@ class GPTGenerator:
                 m.check()
         return out
 
-    def _greedy_mega_loop(self, mega, logits, pos, out, done, max_new_tokens, eos, pad):
+    def _greedy_mega_loop(self, mega, logits, pos, out, done, max_new_tokens, eos, pad, ctx0=None):
         """Batch-1 greedy decoding on the single-launch step: two launches per token, the layer
         stack (decode_mega_kernel) and the greedy tail (decode_head_kernel: final LN, LM head,
         argmax, pad / EOS bookkeeping, token store, position advance, next embedding). Same
@@ -241,7 +241,8 @@ class GPTGenerator:
         resid = self.model.gpt.embeddings(tok.view(1, 1), pos.long().view(1, 1)).reshape(-1).contiguous()
         tok = tok.clone()
         for t in range(1, max_new_tokens):
-            mega.greedy_tail(mega(resid, pos), out, t, done, eos, pad, pos, tok, resid)
+            ctx = None if ctx0 is None else ctx0 + t  # host-side key count: picks the split count
+            mega.greedy_tail(mega(resid, pos, ctx), out, t, done, eos, pad, pos, tok, resid)
             if eos is not None and (t & 7) == 7 and bool(done.all()):
                 break
         mega.check()

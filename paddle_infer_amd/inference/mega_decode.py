@@ -157,10 +157,15 @@ class MegaDecoder:
         want = max(1, int(os.environ.get("PIAMD_MEGA_NSPLIT", "8")) // nb)
         self.nsplit = min(16, max_splits(nb, HQ_), max(want, math.ceil(self.maxS / 256)))
         assert math.ceil(self.maxS / 256) <= self.nsplit, "max_seq_len too long for the split count"
+        # long contexts (batch 1): every workgroup attends — at prompt 1024 16 splits beat 8
+        # (greedy generate 1.169 -> 1.096 ms/token), at prompt 128 they lose (0.894 -> 0.978: the
+        # FFN1 stream no longer overlaps the attention phase); profiles/decode_r6.txt
+        self.nsplit_long = min(16, max_splits(nb, HQ_)) if nb == 1 else self.nsplit
+        self.long_ctx = int(os.environ.get("PIAMD_MEGA_LONG_CTX", "512"))
         # one slot per layer (and per residual update) for every vector handed between
         # workgroups: each address is written once per launch, so readers may use cached loads
         nl, f32, bf = self.nl, dict(dtype=torch.float32, device=dev), dict(dtype=torch.bfloat16, device=dev)
-        pstride = (HQ_ * self.nsplit * (D_ + 2) + 63) // 64 * 64
+        pstride = (HQ_ * max(self.nsplit, self.nsplit_long) * (D_ + 2) + 63) // 64 * 64
         self.rbuf = torch.zeros(2 * nl * nb, E_, **bf)
         self.qn = torch.zeros(nl * nb, HQ_ * D_, **f32)
         self.kvn = torch.zeros(nl * nb, 2 * HK_ * D_, **f32)
@@ -229,17 +234,22 @@ class MegaDecoder:
                           self.pemb.data_ptr(), self.pemb.shape[0], resid.data_ptr())
         _lib.call("piamd_decode_head_greedy", ctypes.byref(a), E, _lib.stream())
 
-    def __call__(self, resid: torch.Tensor, pos: torch.Tensor) -> torch.Tensor:
+    def splits_for(self, ctx) -> int:
+        """Attention splits of a step whose longest row holds ``ctx`` keys (None: unknown)."""
+        return self.nsplit_long if ctx is not None and ctx > self.long_ctx else self.nsplit
+
+    def __call__(self, resid: torch.Tensor, pos: torch.Tensor, ctx=None) -> torch.Tensor:
         """resid: bf16 [nb, E] (or [E] at nb = 1) embedding output; pos: device int32 [nb] = each
-        row's cache slot for this token. Returns the last layer's residual stream [nb, E] ([E] at
-        nb = 1; a view of an internal buffer)."""
+        row's cache slot for this token; ``ctx`` (host int, optional): the longest row's key count,
+        which picks the attention split count. Returns the last layer's residual stream [nb, E]
+        ([E] at nb = 1; a view of an internal buffer)."""
         nb = self.nb
         assert resid.is_contiguous() and resid.numel() == nb * self.E and resid.dtype == torch.bfloat16
         assert pos.dtype == torch.int32 and pos.is_cuda and pos.is_contiguous() and pos.numel() == nb
         if self.trace is not None:  # the kernel writes 4 int64 slots per (workgroup, phase)
             assert (self.trace.dtype == torch.int64 and self.trace.is_cuda
                     and self.trace.numel() >= 256 * 5 * self.nl * 4), "trace must be int64 [256, 5*nl, 4]"
-        a = _lib.MegaArgs(self.table.data_ptr(), self.nl, self.maxS, self.nsplit, self.act,
+        a = _lib.MegaArgs(self.table.data_ptr(), self.nl, self.maxS, self.splits_for(ctx), self.act,
                           self.eps, (1.0 / math.sqrt(self.D)) * 1.4426950408889634, resid.data_ptr(),
                           self.rbuf.data_ptr(), self.qn.data_ptr(), self.kvn.data_ptr(), self.part.data_ptr(),
                           self.h.data_ptr(), self.bar.data_ptr(), self.err.data_ptr(),

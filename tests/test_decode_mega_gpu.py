@@ -257,3 +257,27 @@ def test_mega_decode_batched_generate_and_beams():
     assert a._mega.get(4) and b.shape == (1, 6)
     assert a._mega[4].table is a._mega[2].table  # one set of weight copies per model
     a._mega[4].check()
+
+
+def test_mega_decode_long_context_split_count():
+    """Long contexts run the attention phase on 16 splits (every workgroup) instead of 8: the
+    same layer-stack output either way, and the greedy loop picks 16 past ``long_ctx`` keys."""
+    from paddle_infer_amd.inference.generation import GPTGenerator
+    m = _gpt13b_width(2, 1024)
+    g = GPTGenerator(m, max_batch=1, max_seq_len=1024, use_hip_graph=False)
+    prompt = 700
+    ids = torch.randint(0, 2048, (1, prompt), device=DEV)
+    lens = torch.full((1,), prompt, device=DEV)
+    g.prefill(ids, lens)
+    mega = g._mega_decoder(1)
+    assert mega.nsplit == 8 and mega.nsplit_long == 16
+    assert mega.splits_for(prompt + 1) == 16 and mega.splits_for(100) == 8 and mega.splits_for(None) == 8
+    tok = torch.tensor([5], device=DEV)
+    pos = torch.full((1,), prompt, dtype=torch.int32, device=DEV)
+    resid = m.gpt.embeddings(tok.view(1, 1), pos.long().view(1, 1)).reshape(-1).contiguous()
+    a = mega(resid, pos, None).clone()   # 8 splits (rewrites the same cache slot both times)
+    b = mega(resid, pos, prompt + 1).clone()  # 16 splits
+    assert _rel(a, b) < 1e-2, _rel(a, b)
+    out = g.generate(ids, lens, max_new_tokens=4)
+    assert out.shape == (1, 4)
+    mega.check()

@@ -147,6 +147,8 @@ def lookup(ids, weight, padding_idx=None):
     if pad is not None and pad < 0:
         pad = pad + V
     ids = ids.long()
+    if weight.is_cuda and ids.device != weight.device:  # the kernels read the ids on the device
+        ids = ids.to(weight.device)
     if weight.is_cuda and weight.dtype in _DT and weight.dim() == 2 and weight.shape[1] % 8 == 0 \
             and weight.is_contiguous() and _lib.available():
         if pad is not None:

@@ -24,8 +24,11 @@ def _ws(N, C, G, dev):
     return torch.empty(max(3 * N * C, 2 * N * C + 2 * N * G), dtype=torch.float32, device=dev)
 
 
-def _f32(t):
-    return None if t is None else t.detach().float().contiguous()
+def _f32(t, dev=None):
+    if t is None:
+        return None
+    t = t.detach().float()
+    return (t.to(dev) if dev is not None else t).contiguous()
 
 
 class _GroupNorm(torch.autograd.Function):
@@ -38,7 +41,7 @@ class _GroupNorm(torch.autograd.Function):
         y = torch.empty_like(xc)
         mean = torch.empty(N * G, dtype=torch.float32, device=dev)
         rstd = torch.empty(N * G, dtype=torch.float32, device=dev)
-        g, b = _f32(weight), _f32(bias)
+        g, b = _f32(weight, dev), _f32(bias, dev)
         _lib.call("piamd_group_norm_fwd", _DT[xc.dtype], xc.data_ptr(), y.data_ptr(), _lib.ptr(g), _lib.ptr(b),
                   mean.data_ptr(), rstd.data_ptr(), _ws(N, C, G, dev).data_ptr(), N, C, HW, G, float(eps),
                   _lib.stream())
@@ -76,12 +79,12 @@ def instance_norm_eval(x, running_mean, running_var, weight=None, bias=None, eps
     N, C = xc.shape[0], xc.shape[1]
     HW = xc.numel() // (N * C)
     dev = x.device
-    s = torch.rsqrt(running_var.detach().float() + eps)
+    s = torch.rsqrt(_f32(running_var, dev) + eps)
     if weight is not None:
-        s = s * weight.detach().float()
-    t = -running_mean.detach().float() * s
+        s = s * _f32(weight, dev)
+    t = -_f32(running_mean, dev) * s
     if bias is not None:
-        t = t + bias.detach().float()
+        t = t + _f32(bias, dev)
     y = torch.empty_like(xc)
     zero = torch.zeros(N * C, dtype=torch.float32, device=dev)  # per-(n, c) "statistics": 0 / 1
     one = torch.ones(N * C, dtype=torch.float32, device=dev)

@@ -424,12 +424,49 @@ def _take_join():
     return j
 
 
+class join_give:
+    """``with join_give(j):`` the next dense HIP conv GIVES its data gradient to the join ``j``
+    (stored in ``j.dres``, None returned to autograd) when the join's source conv — another conv
+    of the same input — has not run its backward yet; that source then adds it in its
+    data-gradient epilogue. A downsampling residual block: the shortcut conv gives, the main
+    path's first conv takes (no ATen add of the two block-input gradients). If the source ran
+    first (it closes the join), the giver returns its gradient normally."""
+
+    def __init__(self, j):
+        self.j = j
+
+    def __enter__(self):
+        _JOIN.give = self.j
+        return self.j
+
+    def __exit__(self, *exc):
+        _JOIN.give = None
+        return False
+
+
+def _take_give():
+    j = getattr(_JOIN, "give", None)
+    _JOIN.give = None
+    return j
+
+
+def _give(ctx, x, dx):
+    """The giver's side of a conv→conv join: hand dX (same NHWC shape / dtype as the shared
+    input) to a still-open join instead of returning it."""
+    g = getattr(ctx, "give", None)
+    if (g is None or dx is None or not g.armed or g.dres is not None or dx.shape != x.shape
+            or dx.dtype != x.dtype):
+        return dx
+    g.dres = dx.contiguous()
+    return None
+
+
 class _Conv2dNHWC(torch.autograd.Function):
     """Dense conv on the MFMA kernels: x [N,H,W,C0] bf16/fp16 (contiguous), weight [K0,C0,R,S].
     ``want_stats``: leave the output's per-tile BN statistics in the thread-local slot."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, st, pad, dil, act, want_stats=False, join=None):
+    def forward(ctx, x, weight, bias, st, pad, dil, act, want_stats=False, join=None, give=None):
         dt = x.dtype
         K0, C0, R, S = weight.shape
         K = -(-K0 // 4) * 4  # the epilogue stores 4 output channels per lane
@@ -444,6 +481,7 @@ class _Conv2dNHWC(torch.autograd.Function):
         so = [] if (want_stats and K == K0) else None
         _STATS.v = None
         ctx.join = join
+        ctx.give = give
         if C0 <= 8:  # stem mode: zero-pad the image channels to 8
             xc = _padc(x, 8).contiguous()
             nk = -(-(R * S) // 8)
@@ -513,7 +551,7 @@ class _Conv2dNHWC(torch.autograd.Function):
                 dx = _launch_geom(dyp, w_t, (1, 1), pad_t, dil, H, W, acc=_join_acc(ctx, x, C0))
             else:
                 dx = conv2d_dgrad_strided(dyp, wq, H, W, st, pad, dil)
-            dx = _join_finish(ctx, dx[..., :C0] if C != C0 else dx)
+            dx = _give(ctx, x, _join_finish(ctx, dx[..., :C0] if C != C0 else dx))
         if ctx.needs_input_grad[1]:
             if wgrad_eligible(C, Kp, M):
                 dw = conv2d_wgrad(x, dyp, R, S, st, pad, dil, layout=ctx.w_layout)[:K0, :C0]
@@ -522,7 +560,7 @@ class _Conv2dNHWC(torch.autograd.Function):
             dw = dw.to(wdt)
         if has_bias and ctx.needs_input_grad[2]:
             db = dy.float().sum((0, 1, 2)).to(wdt)
-        return dx, dw, db, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None
 
     @staticmethod
     def _backward_prepped(ctx, x, w_t, dy):
@@ -537,7 +575,7 @@ class _Conv2dNHWC(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             pad_t = (dil[0] * (R - 1) - pad[0], dil[1] * (S - 1) - pad[1])
             dx = _launch_geom(dyp, w_t, (1, 1), pad_t, dil, H, W, acc=_join_acc(ctx, x, C0))
-            dx = _join_finish(ctx, dx[..., :C0] if C != C0 else dx)
+            dx = _give(ctx, x, _join_finish(ctx, dx[..., :C0] if C != C0 else dx))
         if ctx.needs_input_grad[1]:
             if wgrad_eligible(C, Kp, M):
                 dw = conv2d_wgrad(x, dyp, R, S, st, pad, dil, layout=ctx.w_layout)[:K0, :C0]
@@ -546,7 +584,7 @@ class _Conv2dNHWC(torch.autograd.Function):
             dw = dw.to(wdt)
         if has_bias and ctx.needs_input_grad[2]:
             db = dy.float().sum((0, 1, 2)).to(wdt)
-        return dx, dw, db, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None
 
 
 def _join_acc(ctx, x, C0):
@@ -561,11 +599,14 @@ def _join_acc(ctx, x, C0):
 
 
 def _join_finish(ctx, dx):
-    """dX plus a joined residual gradient the kernel did not take."""
+    """dX plus a joined residual gradient the kernel did not take; the join is closed (a giver
+    whose backward comes later returns its gradient itself)."""
     j = ctx.join
-    if j is not None and j.dres is not None:
-        dx = dx + j.dres.to(dx.dtype)
-        j.dres = None
+    if j is not None:
+        if j.dres is not None:
+            dx = dx + j.dres.to(dx.dtype)
+            j.dres = None
+        j.armed = False
     return dx
 
 
@@ -870,7 +911,7 @@ def conv2d_any(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1, 
             join = _take_join()
             if join is not None:
                 join.armed = True
-            y = _Conv2dNHWC.apply(xh, weight, bias, st, pad, dil, 0, want, join)
+            y = _Conv2dNHWC.apply(xh, weight, bias, st, pad, dil, 0, want, join, _take_give())
             part = _take_stats() if want else None
             out = y if nhwc else y.permute(0, 3, 1, 2)
             if part is not None:  # consumed by a BatchNorm of this very tensor (same version)

@@ -122,15 +122,48 @@ def vgg19(pretrained=False, batch_norm=False, **kw): return _vgg(19, batch_norm,
 
 
 # ----------------------------------------------------------------------------------------- ResNet
-def _residual_join(x, downsample):
-    """A residual-gradient join for a block whose residual is its input itself (ops/conv.py
-    ResidualGradJoin): the first conv's data-gradient epilogue adds the residual branch's
-    gradient, so autograd does not sum the two with a separate add. None where it does not
-    apply (a downsample branch, CPU, no autograd)."""
+def _residual_join(x, downsample=None):
+    """A residual-gradient join (ops/conv.py ResidualGradJoin): the first conv's data-gradient
+    epilogue adds the other consumer's gradient of the block input — the residual BatchNorm's
+    (identity shortcut) or the shortcut conv's (downsampling block, ``_downsample_join``) — so
+    autograd does not sum the two with a separate add. None where it does not apply (CPU, no
+    autograd)."""
     from ..ops import conv as _conv
     if downsample is not None or not (_conv.RES_JOIN and x.is_cuda and torch.is_grad_enabled()):
         return None
     return _conv.ResidualGradJoin()
+
+
+# PIAMD_DS_JOIN=0: downsampling blocks sum their two block-input gradients with an autograd add
+DS_JOIN = __import__("os").environ.get("PIAMD_DS_JOIN", "1") != "0"
+
+
+def _downsample_join(x, downsample):
+    """Join for a downsampling block: the shortcut conv (run after the main path, so its
+    backward comes first) gives its input gradient to the main path's first conv."""
+    if downsample is None or not DS_JOIN:
+        return None
+    return _residual_join(x)
+
+
+class _Give:
+    """``with _Give(j)``: the next conv gives its input gradient to the join ``j`` (no-op for
+    None)."""
+
+    def __init__(self, j):
+        self.cm = None
+        if j is not None:
+            from ..ops import conv as _conv
+            self.cm = _conv.join_give(j)
+
+    def __enter__(self):
+        if self.cm is not None:
+            self.cm.__enter__()
+
+    def __exit__(self, *exc):
+        if self.cm is not None:
+            self.cm.__exit__(*exc)
+        return False
 
 
 class _Joined:
@@ -167,12 +200,14 @@ class BasicBlock(nn.Layer):
         self.downsample = downsample
 
     def forward(self, x):
-        idt = x if self.downsample is None else self.downsample(x)
         j = _residual_join(x, self.downsample)
-        with _Joined(j, source=True):
+        jd = _downsample_join(x, self.downsample)
+        with _Joined(j or jd, source=True):
             h = self.conv1(x)
         out = self.bn1(h, act="relu")                              # fused BN + ReLU
         h = self.conv2(out)
+        with _Give(jd):  # the shortcut after the main path: its backward runs first
+            idt = x if self.downsample is None else self.downsample(x)
         with _Joined(j, source=False):
             return self.bn2(h, residual=idt, act="relu")           # fused BN + add + ReLU
 
@@ -195,13 +230,15 @@ class BottleneckBlock(nn.Layer):
         self.downsample = downsample
 
     def forward(self, x):
-        idt = x if self.downsample is None else self.downsample(x)
         j = _residual_join(x, self.downsample)
-        with _Joined(j, source=True):
+        jd = _downsample_join(x, self.downsample)
+        with _Joined(j or jd, source=True):
             h = self.conv1(x)
         out = self.bn1(h, act="relu")
         out = self.bn2(self.conv2(out), act="relu")
         h = self.conv3(out)
+        with _Give(jd):  # the shortcut after the main path: its backward runs first
+            idt = x if self.downsample is None else self.downsample(x)
         with _Joined(j, source=False):
             return self.bn3(h, residual=idt, act="relu")  # fused BN + add + ReLU
 

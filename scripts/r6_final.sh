@@ -14,4 +14,4 @@ for p in 1024 128; do
   timeout -k 10 200 python tools/bench_generate.py --batch 1 --prompt $p --gen 128 --modes graph > gpurun_out/r6f_dec_$p.log 2>&1 || { tail -20 gpurun_out/r6f_dec_$p.log; exit 1; }
   echo "prompt=$p"; grep '^{' gpurun_out/r6f_dec_$p.log
 done
-bash scripts/r6_r.sh
+true

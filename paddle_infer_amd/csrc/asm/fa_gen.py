@@ -903,7 +903,7 @@ QNA = 192
 QBUF_B = 32768                     # per buffer: K 16 KiB, V 16 KiB
 Q_OFF_V = 16384
 QLDS_BYTES = 3 * QBUF_B
-QLA = 6
+QLA = int(os.environ.get("PIAMD_FA_QLA", "6"))  # dQ ring lookahead (≤ 8: reads stay behind the barrier at gap 39)
 
 
 def qbuf_set(b):
@@ -1435,7 +1435,7 @@ F_A_O, F_A_QF, F_A_QN = 0, 64, 96
 F_NA = 128
 F_BUF_B = 32768
 F_LDS_BYTES = 2 * F_BUF_B
-F_LA = 4
+F_LA = int(os.environ.get("PIAMD_FA_FLA", "4"))  # forward ring lookahead
 LN2 = 0.6931471805599453
 
 

@@ -340,7 +340,11 @@ def _lookup(ins, a):
     ids = ins["Ids"][0].long()
     if ids.dim() > 1 and ids.shape[-1] == 1 and a.get("_squeeze_last", False):
         ids = ids.squeeze(-1)
-    return {"Out": F.embedding(ids, ins["W"][0], a.get("padding_idx") if (a.get("padding_idx") or -1) >= 0 else None)}
+    # Paddle semantics (reference `embedding_kernel.cu`): padding rows read as zeros; on the GPU the
+    # own gather kernels (`paddle_infer_amd.nn.functional.embedding` → ops/embedding.py)
+    from ..nn import functional as PF
+    pad = a.get("padding_idx")
+    return {"Out": PF.embedding(ids, ins["W"][0], pad if pad is not None and pad >= 0 else None)}
 
 
 @register("fill_constant")

@@ -53,6 +53,7 @@ __device__ __forceinline__ float sg_act(float v, int act) {
     case 2: return gelu_erf(v);
     case 3: return fmaxf(v, 0.f);
     case 4: return v / (1.f + __expf(-v));
+    case 5: return tanhf(v);  // skinny-kernel only (e.g. the BERT pooler fc)
     default: return v;
   }
 }
@@ -399,7 +400,7 @@ int sg_dispatch(const SgArgs& p, int mb, int nb, int wn, int ks, int depth, int*
 // depth ∈ {1,2} k64 steps of loads in flight per wave (| DB << 4, DB ∈ {2,4,8}: with depth 1 and
 // wn 1, DB steps of B — the weight stream — in flight, A one step), ks ≥ 1 K slices. ks > 1: cnt != null → fixup mode (ws = M·N f32 and cnt = tiles ints, both
 // zeroed, left zeroed); cnt == null → slice mode (ws = ks·M·N f32 + a finish launch).
-// bias / resid: 16-bit, nullable. act: 0 none, 1 gelu_tanh, 2 gelu_erf, 3 relu, 4 silu.
+// bias / resid: 16-bit, nullable. act: 0 none, 1 gelu_tanh, 2 gelu_erf, 3 relu, 4 silu, 5 tanh.
 // ln_c1 / ln_b2 (f32 [N], both or neither): LayerNorm fold — C = act(LN(A)·Bᵀ + bias) with B the
 // folded weight B∘γ, c1 its row sums and b2 = bias + B·β (the bias argument is then ignored);
 // ks == 1, alpha == 1; ln_stats (f32 [M][2], nullable): the (mean, rstd) of each raw A row out.

@@ -220,6 +220,8 @@ def small_cfg(M, N, K):
 
 
 _SG_WS: dict = {}
+# activation codes of the skinny kernel: the shared set plus tanh (code 5, skinny kernel only)
+_SG_ACTS = dict(ACTS, tanh=5)
 
 
 def _sg_fixup_bufs(device, M, N, tiles):
@@ -266,7 +268,7 @@ def small_gemm(a, b, out=None, out_f32=False, alpha=1.0, bias=None, act="none", 
     _lib.call("piamd_small_gemm", int(half == torch.float16), a.data_ptr(), a.stride(0),
               b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0),
               int(out.dtype == torch.float32), M, N, K, mb, nb, wn, depth, ks, float(alpha), _lib.ptr(bias),
-              ACTS[act], _lib.ptr(resid), resid.stride(0) if resid is not None else 0,
+              _SG_ACTS[act], _lib.ptr(resid), resid.stride(0) if resid is not None else 0,
               _lib.ptr(ws), _lib.ptr(cnt), _lib.stream())
     return out
 
@@ -309,7 +311,7 @@ def _small_gemm_ln(a, b, out, M, N, K, cfg, act, resid, ln, ln_stats=None, resid
         ws, cnt = _sg_fixup_bufs(a.device, M, N, tiles)
     _lib.call("piamd_small_gemm_ln", int(a.dtype == torch.float16), a.data_ptr(), a.stride(0),
               b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0), int(out.dtype == torch.float32),
-              M, N, K, mb, nb, wn, depth, ks, float(alpha), _lib.ptr(bias), ACTS[act], _lib.ptr(resid),
+              M, N, K, mb, nb, wn, depth, ks, float(alpha), _lib.ptr(bias), _SG_ACTS[act], _lib.ptr(resid),
               resid.stride(0) if resid is not None else 0, _lib.ptr(ws), _lib.ptr(cnt), _lib.ptr(c1),
               _lib.ptr(b2), float(eps), _lib.ptr(ln_stats), _lib.ptr(rs), _lib.ptr(rg), _lib.ptr(rb),
               _lib.stream())

@@ -390,6 +390,17 @@ def _swce(ins, a):
 from ..inference import ln_defer as _ln_defer  # noqa: E402
 
 
+def _tanh_small_ok(x2, w, b):
+    """fc + tanh on the skinny GEMM's tanh epilogue: 16-bit CUDA rows it takes, with a bias."""
+    if not (x2.is_cuda and x2.dtype in (torch.bfloat16, torch.float16) and w.dim() == 2 and w.dtype == x2.dtype
+            and b is not None and b.dtype == x2.dtype and b.numel() == w.shape[1]):
+        return False
+    from ..ops.gemm import use_small
+    M, K = x2.shape
+    N = w.shape[1]
+    return use_small(M, N, K) and K % 64 == 0 and N % 4 == 0 and w.is_contiguous()
+
+
 @register("fc")
 def _fc(ins, a):
     """Reference `fc_op.cc`: Out = act(Input @ W + Bias) (in_num_col_dims flattening)."""
@@ -410,6 +421,10 @@ def _fc(ins, a):
                                                                                     torch.float16):
         from ..ops.linear import linear_bias_act
         y = linear_bias_act(x2, w, b, act) if b is not None else ops.bias_act(linear(x2, w, None), b, act)
+    elif act == "tanh" and _tanh_small_ok(x2, w, b):  # e.g. the BERT pooler: tanh in the epilogue
+        from ..ops.gemm import small_gemm
+        from ..ops.linear import transposed
+        y = small_gemm(x2.contiguous(), transposed(w), bias=b.reshape(-1), act="tanh")
     elif act in ("gelu", "relu", "silu", "gelu_tanh") and x2.is_cuda and x2.dtype == torch.float32:
         y = ops.bias_act(linear(x2, w, None), b, act)  # split-bf16 GEMM + the f32 bias-act kernel
     else:
